@@ -1,0 +1,205 @@
+/*
+ * tsdbhip.h -- C ABI of libtsdbhip, the MI355X (gfx950) engine for OpenTSDB's
+ * query-time aggregation path.
+ *
+ * Drop-in boundary.  In the reference the path starts where storage I/O ends:
+ *   TsdbQuery.GroupByAndAggregateCB.call(SortedMap<byte[],Span>) -> DataPoints[]
+ *   (reference src/core/TsdbQuery.java:916-1049)
+ * and is evaluated lazily by SpanGroup.iterator() -> AggregationIterator.create
+ *   (src/core/SpanGroup.java:527-532, src/core/AggregationIterator.java:351-380).
+ * The Java host keeps TsdbQuery/TSQuery, Aggregators.get, DownsamplingSpecification
+ * and RateOptions unchanged; a GpuGroupByAndAggregateCB flattens
+ * the scanned Spans into a tsdbhip_batch, calls tsdbhip_run and wraps the
+ * tsdbhip_result arrays as DataPoints.
+ *
+ * Everything crossing this boundary is plain C: pointers, sizes, enums.  No torch,
+ * no HIP types.  Functions return 0 on success or a negative TSDB_E_* code that maps
+ * 1:1 to the Java exception the reference would throw; tsdbhip_last_error() gives the
+ * message (thread-local).
+ */
+#ifndef TSDBHIP_H
+#define TSDBHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TSDBHIP_ABI_VERSION 1
+
+/* ---- error codes: one per Java exception on the path --------------------- */
+enum {
+  TSDB_OK = 0,
+  TSDB_E_ILLEGAL_DATA = -2,      /* IllegalDataException  (src/core/RowSeq.java:242-265, Internal.java:307-321) */
+  TSDB_E_ILLEGAL_ARGUMENT = -3,  /* IllegalArgumentException (DownsamplingSpecification.java:84-185, DateTime.java:186-226) */
+  TSDB_E_ILLEGAL_STATE = -4,     /* IllegalStateException (AggregationIterator.java:640-643, RateSpan.java:129-134) */
+  TSDB_E_UNSUPPORTED = -5,       /* UnsupportedOperationException (Downsampler.java:208-211) */
+  TSDB_E_RUNTIME = -6,           /* RuntimeException "unhandled fill policy" (FillingDownsampler.java:273-274) */
+  TSDB_E_NO_SUCH_ELEMENT = -7,   /* NoSuchElementException (Aggregators.get, iterators) */
+  TSDB_E_ASSERTION = -8,         /* AssertionError (AggregationIterator.java:701-703,769-771) */
+  TSDB_E_CLASS_CAST = -9,        /* ClassCastException */
+  TSDB_E_HIP = -20,              /* device/runtime failure (no reference counterpart) */
+  TSDB_E_NOMEM = -21,
+  TSDB_E_NOT_IMPLEMENTED = -22   /* valid reference query this engine does not run yet */
+};
+
+/* ---- Aggregators (src/core/Aggregators.java:47-203) ----------------------- */
+enum {
+  TSDB_AGG_SUM = 0, TSDB_AGG_PFSUM, TSDB_AGG_MIN, TSDB_AGG_MAX, TSDB_AGG_AVG,
+  TSDB_AGG_MEDIAN, TSDB_AGG_NONE, TSDB_AGG_MULT, TSDB_AGG_DEV, TSDB_AGG_DIFF,
+  TSDB_AGG_ZIMSUM, TSDB_AGG_MIMMIN, TSDB_AGG_MIMMAX, TSDB_AGG_SQUARESUM,
+  TSDB_AGG_COUNT, TSDB_AGG_FIRST, TSDB_AGG_LAST,
+  /* PercentileAgg (Aggregators.java:125-173), LEGACY estimation */
+  TSDB_AGG_P999, TSDB_AGG_P99, TSDB_AGG_P95, TSDB_AGG_P90, TSDB_AGG_P75, TSDB_AGG_P50,
+  /* R_3 estimation */
+  TSDB_AGG_EP999R3, TSDB_AGG_EP99R3, TSDB_AGG_EP95R3, TSDB_AGG_EP90R3, TSDB_AGG_EP75R3, TSDB_AGG_EP50R3,
+  /* R_7 estimation */
+  TSDB_AGG_EP999R7, TSDB_AGG_EP99R7, TSDB_AGG_EP95R7, TSDB_AGG_EP90R7, TSDB_AGG_EP75R7, TSDB_AGG_EP50R7,
+  TSDB_AGG_COUNT_ALL
+};
+
+/* Aggregators.Interpolation (src/core/Aggregators.java:38-44) */
+enum { TSDB_INTERP_LERP = 0, TSDB_INTERP_ZIM, TSDB_INTERP_MAX, TSDB_INTERP_MIN, TSDB_INTERP_PREV };
+
+/* FillPolicy (src/core/FillPolicy.java:22-28) */
+enum { TSDB_FILL_NONE = 0, TSDB_FILL_ZERO, TSDB_FILL_NAN, TSDB_FILL_NULL, TSDB_FILL_SCALAR };
+
+/* ---- Batch: the Spans found by TsdbQuery.findSpans, flattened to CSR ------
+ * Series s owns rows [series_row_ptr[s], series_row_ptr[s+1]) sorted by base time
+ * (Span.checkRowOrder, src/core/Span.java:387-392).  Row r is one compacted cell
+ * (RowSeq, src/core/RowSeq.java:39-77): its qualifier bytes are
+ * qual[row_qual_off[r] .. row_qual_off[r+1]) and its value bytes (including the
+ * trailing meta byte written by CompactionQueue, src/core/CompactionQueue.java:594-612)
+ * are val[row_val_off[r] .. row_val_off[r+1]).  Everything big-endian, byte-identical
+ * to the HBase cells.  group_id[s] is the dense index of the series' SpanGroup in
+ * ByteMap key order (TsdbQuery.java:987-1043); series are given in SpanCmp order.
+ */
+typedef struct {
+  int64_t n_series;
+  const int64_t* series_row_ptr;   /* [n_series + 1] */
+  int64_t n_rows;
+  const uint32_t* row_base_time;   /* [n_rows]   seconds (row key bytes, Internal.baseTime) */
+  const uint64_t* row_qual_off;    /* [n_rows + 1] */
+  const uint64_t* row_val_off;     /* [n_rows + 1] */
+  const uint8_t* qual;             /* [row_qual_off[n_rows]] */
+  const uint8_t* val;              /* [row_val_off[n_rows]] */
+  const int32_t* group_id;         /* [n_series]; -1 drops the series (no matching group-by tag) */
+} tsdbhip_batch;
+
+/* ---- Query: TsdbQuery state that reaches the aggregation path ------------- */
+typedef struct {
+  int64_t start_time;        /* TsdbQuery.setStartTime: unix seconds or ms (TsdbQuery.java:262-289) */
+  int64_t end_time;          /* TsdbQuery.setEndTime */
+  int32_t aggregator;        /* TSDB_AGG_*: group-by aggregator */
+  /* DownsamplingSpecification (src/core/DownsamplingSpecification.java:25-191) */
+  int32_t ds_function;       /* TSDB_AGG_* or -1 for NO_DOWNSAMPLER */
+  int32_t ds_fill;           /* TSDB_FILL_* */
+  int32_t ds_all;            /* "0all-..." : one bucket over [query start, query end) */
+  int32_t ds_calendar;       /* 'c' suffix; not implemented yet (TSDB_E_NOT_IMPLEMENTED) */
+  int64_t ds_interval_ms;
+  /* RateOptions (src/core/RateOptions.java:27-97) */
+  int32_t rate;
+  int32_t rate_counter;
+  int32_t rate_drop_resets;
+  int32_t flags;             /* TSDB_QF_* */
+  int64_t rate_counter_max;  /* default Long.MAX_VALUE */
+  int64_t rate_reset_value;  /* default 0 */
+} tsdbhip_query;
+
+/* Query flags. */
+#define TSDB_QF_ORDERED 0x1  /* cross-series float reductions in SpanGroup index order (bit-exact, slower) */
+
+/* ---- Result: DataPoints[] (one entry per SpanGroup, in emission order) ----- */
+typedef struct {
+  int64_t n_groups;
+  const int32_t* group_id;     /* [n_groups] batch group id of each emitted SpanGroup (-1..: raw span index for NONE) */
+  const int64_t* group_ptr;    /* [n_groups + 1] point range of each group */
+  const int64_t* ts_ms;        /* [n_points] DataPoint.timestamp() */
+  const uint64_t* value_bits;  /* [n_points] longValue() or Double.doubleToRawLongBits(doubleValue()) */
+  const uint8_t* is_int;       /* [n_points] DataPoint.isInteger() */
+} tsdbhip_result;
+
+/* Per-stage device timing of the last tsdbhip_run (hipEvents on the engine stream). */
+typedef struct {
+  double decode_downsample_ms;   /* fused decode + downsample + per-tile group partials */
+  double group_reduce_ms;        /* cross-tile group reduction + emission */
+  double total_ms;
+  int64_t datapoints;            /* raw datapoints decoded */
+  int64_t bytes;                 /* algorithmic HBM bytes read (qualifiers+values+row index) */
+} tsdbhip_timing;
+
+/* ---- library-level helpers (host logic of the reference, restated) ------- */
+int tsdbhip_abi_version(void);
+const char* tsdbhip_last_error(void);
+/* Aggregators.get(name) (src/core/Aggregators.java:222-228); returns id or TSDB_E_NO_SUCH_ELEMENT */
+int tsdbhip_aggregator_get(const char* name);
+/* Aggregator.interpolationMethod() */
+int tsdbhip_aggregator_interpolation(int aggregator);
+/* DateTime.parseDuration (src/utils/DateTime.java:186-226) */
+int tsdbhip_parse_duration(const char* duration, int64_t* out_ms);
+/* new DownsamplingSpecification(String) (src/core/DownsamplingSpecification.java:116-191);
+ * fills the ds_* fields of q */
+int tsdbhip_parse_downsample(const char* spec, tsdbhip_query* q);
+/* TsdbQuery.getScanStartTimeSeconds / getScanEndTimeSeconds (src/core/TsdbQuery.java:1506-1606) */
+int tsdbhip_scan_bounds(const tsdbhip_query* q, int64_t* scan_start_s, int64_t* scan_end_s);
+
+/* ---- engine ------------------------------------------------------------- */
+typedef struct tsdbhip_ctx tsdbhip_ctx;
+
+/* One context per GPU (hipSetDevice(device)); one process per GPU in multi-GPU runs. */
+int tsdbhip_init(int device, tsdbhip_ctx** out);
+void tsdbhip_destroy(tsdbhip_ctx* ctx);
+/* Copy a host batch into HBM (re-laid out: rows 16-B aligned).  Replaces any previous batch. */
+int tsdbhip_load(tsdbhip_ctx* ctx, const tsdbhip_batch* host_batch);
+/* Synthetic MockBase-equivalent store generated directly in HBM (see tsdbhip_synth_spec). */
+typedef struct {
+  int64_t n_series;
+  int64_t start_s;          /* first timestamp (seconds) */
+  int64_t n_points;         /* datapoints per series */
+  int64_t period_ms;        /* sampling period (>= 1000 and multiple of 1000 -> second qualifiers) */
+  int32_t value_kind;       /* 0 = float32 50+10(u-0.5); 1 = int hash % int_mod; 2 = even series int, odd float32 */
+  int32_t n_groups;         /* group_id = series % n_groups, series sorted by group */
+  int64_t int_mod;
+  uint64_t seed;
+} tsdbhip_synth_spec;
+int tsdbhip_synth(tsdbhip_ctx* ctx, const tsdbhip_synth_spec* spec);
+/* Copy the resident batch back to host (for parity checks); host arrays sized by tsdbhip_batch_sizes. */
+int tsdbhip_batch_sizes(tsdbhip_ctx* ctx, int64_t* n_series, int64_t* n_rows, uint64_t* qual_bytes, uint64_t* val_bytes);
+int tsdbhip_batch_download(tsdbhip_ctx* ctx, int64_t* series_row_ptr, uint32_t* row_base_time,
+                           uint64_t* row_qual_off, uint64_t* row_val_off, uint8_t* qual, uint8_t* val,
+                           int32_t* group_id);
+
+/* Run the query over the resident batch: TsdbQuery.run() from GroupByAndAggregateCB on. */
+int tsdbhip_run(tsdbhip_ctx* ctx, const tsdbhip_query* q, tsdbhip_result** out);
+void tsdbhip_result_free(tsdbhip_result* r);
+int tsdbhip_last_timing(tsdbhip_ctx* ctx, tsdbhip_timing* out);
+
+/* ---- multi-GPU (series sharded over ranks; decomposable partial exchange) ----
+ * tsdbhip_partials_layout: size in bytes of the per-(group, slot) partial-state buffer
+ * and its reduction structure: the buffer is n_sum doubles (reduce SUM), then
+ * n_min doubles (MIN), then n_max doubles (MAX); the caller all-reduces each segment
+ * (RCCL over xGMI) and hands the reduced buffer to tsdbhip_finalize. */
+typedef struct {
+  int64_t n_groups;
+  int64_t n_slots;
+  int64_t n_sum;
+  int64_t n_min;
+  int64_t n_max;
+  int64_t bytes;
+} tsdbhip_partials_layout;
+int tsdbhip_partials_layout_get(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_global,
+                                tsdbhip_partials_layout* out);
+/* Computes this shard's partial states into device memory d_partials (layout above). */
+int tsdbhip_run_partials(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_global, void* d_partials);
+/* Turns reduced partial states into the result (on the calling rank). */
+int tsdbhip_finalize(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_global,
+                     const void* d_partials, tsdbhip_result** out);
+/* Device synchronisation helper for host code that does not use HIP directly. */
+int tsdbhip_sync(tsdbhip_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TSDBHIP_H */

@@ -1,0 +1,234 @@
+"""ctypes mirror of include/tsdbhip.h (the C ABI of libtsdbhip).
+
+Pure declarations: enums, structs and the helpers that turn numpy arrays into a
+``tsdbhip_batch``.  Shared by the engine binding (:mod:`opentsdb_amd.engine`) and by the
+test-only oracle binding (oracle/oracle.py), which consumes the same boundary types.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+# ---- error codes (tsdbhip.h) -------------------------------------------------
+TSDB_OK = 0
+TSDB_E_ILLEGAL_DATA = -2
+TSDB_E_ILLEGAL_ARGUMENT = -3
+TSDB_E_ILLEGAL_STATE = -4
+TSDB_E_UNSUPPORTED = -5
+TSDB_E_RUNTIME = -6
+TSDB_E_NO_SUCH_ELEMENT = -7
+TSDB_E_ASSERTION = -8
+TSDB_E_CLASS_CAST = -9
+TSDB_E_HIP = -20
+TSDB_E_NOMEM = -21
+TSDB_E_NOT_IMPLEMENTED = -22
+
+ERROR_NAMES = {
+    TSDB_E_ILLEGAL_DATA: "IllegalDataException",
+    TSDB_E_ILLEGAL_ARGUMENT: "IllegalArgumentException",
+    TSDB_E_ILLEGAL_STATE: "IllegalStateException",
+    TSDB_E_UNSUPPORTED: "UnsupportedOperationException",
+    TSDB_E_RUNTIME: "RuntimeException",
+    TSDB_E_NO_SUCH_ELEMENT: "NoSuchElementException",
+    TSDB_E_ASSERTION: "AssertionError",
+    TSDB_E_CLASS_CAST: "ClassCastException",
+    TSDB_E_HIP: "HipError",
+    TSDB_E_NOMEM: "OutOfMemory",
+    TSDB_E_NOT_IMPLEMENTED: "NotImplemented",
+}
+
+# ---- aggregators (src/core/Aggregators.java:47-203) ---------------------------
+AGGREGATOR_NAMES = [
+    "sum", "pfsum", "min", "max", "avg", "median", "none", "mult", "dev", "diff",
+    "zimsum", "mimmin", "mimmax", "squareSum", "count", "first", "last",
+    "p999", "p99", "p95", "p90", "p75", "p50",
+    "ep999r3", "ep99r3", "ep95r3", "ep90r3", "ep75r3", "ep50r3",
+    "ep999r7", "ep99r7", "ep95r7", "ep90r7", "ep75r7", "ep50r7",
+]
+AGG = {n: i for i, n in enumerate(AGGREGATOR_NAMES)}
+
+INTERP_LERP, INTERP_ZIM, INTERP_MAX, INTERP_MIN, INTERP_PREV = range(5)
+FILL_NONE, FILL_ZERO, FILL_NAN, FILL_NULL, FILL_SCALAR = range(5)
+FILL_NAMES = ["none", "zero", "nan", "null", "scalar"]
+
+QF_ORDERED = 0x1
+
+LONG_MAX = (1 << 63) - 1
+
+
+def interpolation_of(agg: int) -> int:
+    """Aggregator.interpolationMethod() (src/core/Aggregators.java:47-173)."""
+    name = AGGREGATOR_NAMES[agg]
+    if name == "pfsum":
+        return INTERP_PREV
+    if name in ("none", "zimsum", "squareSum", "count", "first", "last"):
+        return INTERP_ZIM
+    if name == "mimmin":
+        return INTERP_MAX
+    if name == "mimmax":
+        return INTERP_MIN
+    return INTERP_LERP
+
+
+class Batch(C.Structure):
+    _fields_ = [
+        ("n_series", C.c_int64),
+        ("series_row_ptr", C.POINTER(C.c_int64)),
+        ("n_rows", C.c_int64),
+        ("row_base_time", C.POINTER(C.c_uint32)),
+        ("row_qual_off", C.POINTER(C.c_uint64)),
+        ("row_val_off", C.POINTER(C.c_uint64)),
+        ("qual", C.POINTER(C.c_uint8)),
+        ("val", C.POINTER(C.c_uint8)),
+        ("group_id", C.POINTER(C.c_int32)),
+    ]
+
+
+class Query(C.Structure):
+    _fields_ = [
+        ("start_time", C.c_int64),
+        ("end_time", C.c_int64),
+        ("aggregator", C.c_int32),
+        ("ds_function", C.c_int32),
+        ("ds_fill", C.c_int32),
+        ("ds_all", C.c_int32),
+        ("ds_calendar", C.c_int32),
+        ("ds_interval_ms", C.c_int64),
+        ("rate", C.c_int32),
+        ("rate_counter", C.c_int32),
+        ("rate_drop_resets", C.c_int32),
+        ("flags", C.c_int32),
+        ("rate_counter_max", C.c_int64),
+        ("rate_reset_value", C.c_int64),
+    ]
+
+
+class Result(C.Structure):
+    _fields_ = [
+        ("n_groups", C.c_int64),
+        ("group_id", C.POINTER(C.c_int32)),
+        ("group_ptr", C.POINTER(C.c_int64)),
+        ("ts_ms", C.POINTER(C.c_int64)),
+        ("value_bits", C.POINTER(C.c_uint64)),
+        ("is_int", C.POINTER(C.c_uint8)),
+    ]
+
+
+class Timing(C.Structure):
+    _fields_ = [
+        ("decode_downsample_ms", C.c_double),
+        ("group_reduce_ms", C.c_double),
+        ("total_ms", C.c_double),
+        ("datapoints", C.c_int64),
+        ("bytes", C.c_int64),
+    ]
+
+
+class SynthSpec(C.Structure):
+    _fields_ = [
+        ("n_series", C.c_int64),
+        ("start_s", C.c_int64),
+        ("n_points", C.c_int64),
+        ("period_ms", C.c_int64),
+        ("value_kind", C.c_int32),
+        ("n_groups", C.c_int32),
+        ("int_mod", C.c_int64),
+        ("seed", C.c_uint64),
+    ]
+
+
+class PartialsLayout(C.Structure):
+    _fields_ = [
+        ("n_groups", C.c_int64),
+        ("n_slots", C.c_int64),
+        ("n_sum", C.c_int64),
+        ("n_min", C.c_int64),
+        ("n_max", C.c_int64),
+        ("bytes", C.c_int64),
+    ]
+
+
+def new_query(start_time: int, end_time: int, aggregator: str | int = "sum", *,
+              ds_function: int = -1, ds_interval_ms: int = 0, ds_fill: int = FILL_NONE,
+              ds_all: bool = False, rate: bool = False, counter: bool = False,
+              counter_max: int = LONG_MAX, reset_value: int = 0, drop_resets: bool = False,
+              flags: int = 0) -> Query:
+    q = Query()
+    q.start_time = start_time
+    q.end_time = end_time
+    q.aggregator = AGG[aggregator] if isinstance(aggregator, str) else aggregator
+    q.ds_function = ds_function
+    q.ds_fill = ds_fill
+    q.ds_all = int(ds_all)
+    q.ds_calendar = 0
+    q.ds_interval_ms = ds_interval_ms
+    q.rate = int(rate)
+    q.rate_counter = int(counter)
+    q.rate_drop_resets = int(drop_resets)
+    q.rate_counter_max = counter_max
+    q.rate_reset_value = reset_value
+    q.flags = flags
+    return q
+
+
+def _ptr(a: np.ndarray, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+class HostBatch:
+    """Owns the numpy arrays behind a :class:`Batch` (keeps them alive)."""
+
+    def __init__(self, series_row_ptr, row_base_time, row_qual_off, row_val_off, qual, val, group_id):
+        self.series_row_ptr = np.ascontiguousarray(series_row_ptr, dtype=np.int64)
+        self.row_base_time = np.ascontiguousarray(row_base_time, dtype=np.uint32)
+        self.row_qual_off = np.ascontiguousarray(row_qual_off, dtype=np.uint64)
+        self.row_val_off = np.ascontiguousarray(row_val_off, dtype=np.uint64)
+        self.qual = np.ascontiguousarray(qual, dtype=np.uint8)
+        self.val = np.ascontiguousarray(val, dtype=np.uint8)
+        self.group_id = np.ascontiguousarray(group_id, dtype=np.int32)
+        if self.qual.size == 0:
+            self.qual = np.zeros(1, np.uint8)
+        if self.val.size == 0:
+            self.val = np.zeros(1, np.uint8)
+        n = len(self.series_row_ptr) - 1
+        assert n >= 0 and len(self.group_id) == n
+        assert len(self.row_qual_off) == len(self.row_base_time) + 1
+        assert len(self.row_val_off) == len(self.row_base_time) + 1
+        self.c = Batch(
+            n, _ptr(self.series_row_ptr, C.c_int64), len(self.row_base_time),
+            _ptr(self.row_base_time, C.c_uint32), _ptr(self.row_qual_off, C.c_uint64),
+            _ptr(self.row_val_off, C.c_uint64), _ptr(self.qual, C.c_uint8),
+            _ptr(self.val, C.c_uint8), _ptr(self.group_id, C.c_int32))
+
+    @property
+    def n_series(self) -> int:
+        return len(self.series_row_ptr) - 1
+
+    @property
+    def n_rows(self) -> int:
+        return len(self.row_base_time)
+
+
+def result_to_groups(res: Result):
+    """Copies a tsdbhip_result / ref_result into a list of
+    (group_id, ts[int64], bits[uint64], is_int[uint8]) numpy tuples."""
+    groups = []
+    n = res.n_groups
+    if n == 0:
+        return groups
+    gp = np.ctypeslib.as_array(res.group_ptr, shape=(n + 1,)).copy()
+    gid = np.ctypeslib.as_array(res.group_id, shape=(n,)).copy()
+    tot = int(gp[-1])
+    if tot:
+        ts = np.ctypeslib.as_array(res.ts_ms, shape=(tot,)).copy()
+        bits = np.ctypeslib.as_array(res.value_bits, shape=(tot,)).copy()
+        isi = np.ctypeslib.as_array(res.is_int, shape=(tot,)).copy()
+    else:
+        ts = np.zeros(0, np.int64)
+        bits = np.zeros(0, np.uint64)
+        isi = np.zeros(0, np.uint8)
+    for g in range(n):
+        a, b = int(gp[g]), int(gp[g + 1])
+        groups.append((int(gid[g]), ts[a:b], bits[a:b], isi[a:b]))
+    return groups

@@ -1,0 +1,259 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes binding of the CPU oracle (oracle/refcpu.c).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module.  The product (opentsdb_amd, libtsdbhip) never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import struct
+import subprocess
+
+import numpy as np
+
+from opentsdb_amd import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "librefcpu.so")
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-C", HERE], check=True, stdout=subprocess.DEVNULL)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(LIB_PATH)
+        vp = C.c_void_p
+        L.ref_last_error.restype = C.c_char_p
+        L.ref_view_array.restype = vp
+        L.ref_view_array.argtypes = [C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.c_int64, C.c_int]
+        L.ref_view_span.restype = vp
+        L.ref_view_span.argtypes = [C.c_int64, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                    C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)]
+        L.ref_view_downsampler.restype = vp
+        L.ref_view_downsampler.argtypes = [vp, C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_int64, C.c_int64,
+                                           C.c_int64, C.c_int64]
+        L.ref_view_rate.restype = vp
+        L.ref_view_rate.argtypes = [vp, C.c_int32, C.c_int64, C.c_int64, C.c_int32]
+        L.ref_view_aggregate.restype = vp
+        L.ref_view_aggregate.argtypes = [C.POINTER(vp), C.c_int64, C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32]
+        L.ref_view_free.argtypes = [vp]
+        L.ref_has_next.argtypes = [vp]
+        L.ref_seek.argtypes = [vp, C.c_int64]
+        L.ref_drain.restype = C.c_int64
+        L.ref_drain.argtypes = [vp, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]
+        L.ref_agg_run_long.argtypes = [C.c_int32, C.POINTER(C.c_int64), C.c_int64, C.POINTER(C.c_int64)]
+        L.ref_agg_run_double.argtypes = [C.c_int32, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double)]
+        L.ref_parse_duration.argtypes = [C.c_char_p, C.POINTER(C.c_int64)]
+        L.ref_parse_downsample.argtypes = [C.c_char_p, C.POINTER(abi.Query)]
+        L.ref_aggregator_get.argtypes = [C.c_char_p]
+        L.ref_scan_bounds.argtypes = [C.POINTER(abi.Query), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+        L.ref_run_query.argtypes = [C.POINTER(abi.Batch), C.POINTER(abi.Query), C.POINTER(C.POINTER(abi.Result))]
+        L.ref_run_query_mt.argtypes = [C.POINTER(abi.Batch), C.POINTER(abi.Query), C.c_int,
+                                       C.POINTER(C.POINTER(abi.Result))]
+        L.ref_result_free.argtypes = [C.POINTER(abi.Result)]
+        _lib = L
+    return _lib
+
+
+class OracleError(Exception):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{abi.ERROR_NAMES.get(code, code)}: {msg}")
+        self.code = code
+        self.java = abi.ERROR_NAMES.get(code, str(code))
+
+
+def _err(code):
+    raise OracleError(code, lib().ref_last_error().decode(errors="replace"))
+
+
+def d2bits(x: float) -> int:
+    return struct.unpack("<q", struct.pack("<d", x))[0]
+
+
+def bits2d(b: int) -> float:
+    return struct.unpack("<d", struct.pack("<Q", b & 0xFFFFFFFFFFFFFFFF))[0]
+
+
+class View:
+    """Owning handle of a ref_view; ownership moves into wrapping views."""
+
+    def __init__(self, ptr, keep=()):
+        if not ptr:
+            _err(-3)
+        self.ptr = ptr
+        self.keep = list(keep)
+        self.owned = True
+
+    def _take(self):
+        assert self.owned, "view already consumed"
+        self.owned = False
+        return self.ptr
+
+    def seek(self, ts: int):
+        rc = lib().ref_seek(self.ptr, ts)
+        if rc < 0:
+            _err(rc)
+
+    def has_next(self) -> bool:
+        rc = lib().ref_has_next(self.ptr)
+        if rc < 0:
+            _err(rc)
+        return bool(rc)
+
+    def drain(self, cap: int = 1 << 20):
+        ts = np.zeros(cap, np.int64)
+        isi = np.zeros(cap, np.int32)
+        bits = np.zeros(cap, np.uint64)
+        n = lib().ref_drain(self.ptr, cap, ts.ctypes.data_as(C.POINTER(C.c_int64)),
+                            isi.ctypes.data_as(C.POINTER(C.c_int32)), bits.ctypes.data_as(C.POINTER(C.c_uint64)))
+        if n < 0:
+            _err(n)
+        n = min(n, cap)
+        out = []
+        for i in range(n):
+            if isi[i]:
+                out.append((int(ts[i]), True, int(np.int64(bits[i].astype(np.int64)))))
+            else:
+                out.append((int(ts[i]), False, bits2d(int(bits[i]))))
+        return out
+
+    def __del__(self):
+        if getattr(self, "owned", False) and self.ptr:
+            try:
+                lib().ref_view_free(self.ptr)
+            except Exception:
+                pass
+
+
+def array_view(points, generator: bool = False) -> View:
+    """points: iterable of (ts_ms, is_int, value)."""
+    pts = list(points)
+    n = len(pts)
+    ts = np.array([p[0] for p in pts] or [0], np.int64)
+    isi = np.array([1 if p[1] else 0 for p in pts] or [0], np.int32)
+    bits = np.array([(int(p[2]) if p[1] else d2bits(float(p[2]))) for p in pts] or [0], np.int64)
+    ptr = lib().ref_view_array(ts.ctypes.data_as(C.POINTER(C.c_int64)), isi.ctypes.data_as(C.POINTER(C.c_int32)),
+                               bits.ctypes.data_as(C.POINTER(C.c_int64)), n, int(generator))
+    return View(ptr)
+
+
+def span_view(base_times, quals, vals) -> View:
+    """One Span from a list of compacted rows (base_time_s, qualifier bytes, value bytes)."""
+    qo = np.zeros(len(quals) + 1, np.uint64)
+    vo = np.zeros(len(vals) + 1, np.uint64)
+    qo[1:] = np.cumsum([len(q) for q in quals])
+    vo[1:] = np.cumsum([len(v) for v in vals])
+    qb = np.frombuffer(b"".join(quals) or b"\0", np.uint8).copy()
+    vb = np.frombuffer(b"".join(vals) or b"\0", np.uint8).copy()
+    bt = np.array(base_times, np.uint32)
+    ptr = lib().ref_view_span(len(quals), bt.ctypes.data_as(C.POINTER(C.c_uint32)),
+                              qo.ctypes.data_as(C.POINTER(C.c_uint64)), vo.ctypes.data_as(C.POINTER(C.c_uint64)),
+                              qb.ctypes.data_as(C.POINTER(C.c_uint8)), vb.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return View(ptr, keep=(qo, vo, qb, vb, bt))
+
+
+def parse_downsample(spec: str) -> abi.Query:
+    q = abi.new_query(0, 0)
+    rc = lib().ref_parse_downsample(spec.encode(), C.byref(q))
+    if rc < 0:
+        _err(rc)
+    return q
+
+
+def downsampler(src: View, spec: str, start_time: int = 0, end_time: int = 0,
+                query_start: int = 0, query_end: int = abi.LONG_MAX) -> View:
+    """Downsampler (fill none) or FillingDownsampler, as Span.downsampler builds them."""
+    q = parse_downsample(spec)
+    ptr = lib().ref_view_downsampler(src._take(), q.ds_function, q.ds_interval_ms, q.ds_fill, q.ds_all,
+                                     start_time, end_time, query_start, query_end)
+    if not ptr:
+        _err(-3)
+    return View(ptr, keep=src.keep)
+
+
+def downsampler_raw(src: View, function: str, interval_ms: int, fill: int = abi.FILL_NONE,
+                    start_time: int = 0, end_time: int = 0) -> View:
+    """The deprecated Downsampler(source, interval_ms, function) constructor."""
+    ptr = lib().ref_view_downsampler(src._take(), abi.AGG[function], interval_ms, fill, 0,
+                                     start_time, end_time, 0, 0)
+    if not ptr:
+        _err(-3)
+    return View(ptr, keep=src.keep)
+
+
+def rate(src: View, counter=False, counter_max=abi.LONG_MAX, reset_value=0, drop_resets=False) -> View:
+    ptr = lib().ref_view_rate(src._take(), int(counter), counter_max, reset_value, int(drop_resets))
+    return View(ptr, keep=src.keep)
+
+
+def aggregate(srcs, start_time: int, end_time: int, aggregator: str, interpolation: int | None = None,
+              rate: bool = False) -> View:
+    agg = abi.AGG[aggregator]
+    if interpolation is None:
+        interpolation = abi.interpolation_of(agg)
+    arr = (C.c_void_p * max(1, len(srcs)))()
+    keep = []
+    for i, s in enumerate(srcs):
+        arr[i] = s._take()
+        keep += s.keep
+    ptr = lib().ref_view_aggregate(arr, len(srcs), start_time, end_time, agg, interpolation, int(rate))
+    if not ptr:
+        _err(-3)
+    return View(ptr, keep=keep)
+
+
+def agg_run_long(name: str, values) -> int:
+    v = np.ascontiguousarray(values, np.int64)
+    out = C.c_int64()
+    rc = lib().ref_agg_run_long(abi.AGG[name], v.ctypes.data_as(C.POINTER(C.c_int64)), len(v), C.byref(out))
+    if rc < 0:
+        _err(rc)
+    return out.value
+
+
+def agg_run_double(name: str, values) -> float:
+    v = np.ascontiguousarray(values, np.float64)
+    out = C.c_double()
+    rc = lib().ref_agg_run_double(abi.AGG[name], v.ctypes.data_as(C.POINTER(C.c_double)), len(v), C.byref(out))
+    if rc < 0:
+        _err(rc)
+    return out.value
+
+
+def parse_duration(s: str) -> int:
+    out = C.c_int64()
+    rc = lib().ref_parse_duration(s.encode(), C.byref(out))
+    if rc < 0:
+        _err(rc)
+    return out.value
+
+
+def scan_bounds(q: abi.Query):
+    s, e = C.c_int64(), C.c_int64()
+    lib().ref_scan_bounds(C.byref(q), C.byref(s), C.byref(e))
+    return s.value, e.value
+
+
+def run_query(batch: abi.HostBatch, q: abi.Query, threads: int = 1):
+    """TsdbQuery.run() on the oracle: list of (group_id, ts, bits, is_int)."""
+    res = C.POINTER(abi.Result)()
+    if threads > 1:
+        rc = lib().ref_run_query_mt(C.byref(batch.c), C.byref(q), threads, C.byref(res))
+    else:
+        rc = lib().ref_run_query(C.byref(batch.c), C.byref(q), C.byref(res))
+    if rc < 0:
+        _err(rc)
+    try:
+        return abi.result_to_groups(res.contents)
+    finally:
+        lib().ref_result_free(res)

@@ -1,0 +1,86 @@
+/*
+ * refcpu.h -- TEST INFRASTRUCTURE ONLY.  CPU restatement of the reference
+ * OpenTSDB 2.4 query-aggregation path, used as the parity oracle and as the CPU
+ * baseline ("port").  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it.  The product (libtsdbhip) never links or calls it.
+ *
+ * The functions mirror the reference's iterator objects one for one so that the
+ * reference's own unit tests (SeekableViewsForTest-driven) can be replayed:
+ *   ref_view_array        <-> SeekableViewsForTest.MockSeekableView / DataPointGenerator
+ *   ref_view_span         <-> Span.Iterator over RowSeq compacted cells
+ *   ref_view_downsampler  <-> Downsampler / FillingDownsampler (Span.downsampler)
+ *   ref_view_rate         <-> RateSpan
+ *   ref_view_aggregate    <-> AggregationIterator
+ *   ref_run_query         <-> TsdbQuery.run() from GroupByAndAggregateCB through
+ *                             SpanGroup.iterator() for every group
+ */
+#ifndef REFCPU_H
+#define REFCPU_H
+#include <stdint.h>
+#include "../include/tsdbhip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ref_view ref_view;
+
+typedef struct {
+  int64_t ts;
+  int32_t is_int;
+  int32_t bad;        /* nonzero: reading the value throws this TSDB_E_* code (lazy Java semantics) */
+  int64_t lv;         /* longValue() when is_int */
+  double dv;          /* doubleValue() when !is_int */
+} ref_dp;
+
+const char* ref_last_error(void);
+
+/* Views.  Every constructor returns NULL on error (ref_last_error()). */
+ref_view* ref_view_array(const int64_t* ts, const int32_t* is_int, const int64_t* bits, int64_t n,
+                         int generator_seek);
+ref_view* ref_view_span(int64_t n_rows, const uint32_t* base_time, const uint64_t* qual_off,
+                        const uint64_t* val_off, const uint8_t* qual, const uint8_t* val);
+ref_view* ref_view_downsampler(ref_view* src, int32_t function, int64_t interval_ms, int32_t fill,
+                               int32_t run_all, int64_t start_time, int64_t end_time,
+                               int64_t query_start, int64_t query_end);
+ref_view* ref_view_rate(ref_view* src, int32_t counter, int64_t counter_max, int64_t reset_value,
+                        int32_t drop_resets);
+ref_view* ref_view_aggregate(ref_view** srcs, int64_t n, int64_t start_time, int64_t end_time,
+                             int32_t aggregator, int32_t interpolation, int32_t rate);
+void ref_view_free(ref_view* v);
+
+/* Iteration: 1/0 on success, <0 on exception. */
+int ref_has_next(ref_view* v);
+/* Drains v: writes up to cap points (ts, is_int, value bits).  Returns count or <0. */
+int64_t ref_drain(ref_view* v, int64_t cap, int64_t* ts, int32_t* is_int, uint64_t* bits);
+int ref_seek(ref_view* v, int64_t ts);
+
+/* Aggregator.runLong / runDouble over a plain array (TestAggregators' Numbers). */
+int ref_agg_run_long(int32_t aggregator, const int64_t* v, int64_t n, int64_t* out);
+int ref_agg_run_double(int32_t aggregator, const double* v, int64_t n, double* out);
+
+/* Host logic restatements (same contract as the tsdbhip_* helpers). */
+int ref_parse_duration(const char* s, int64_t* out_ms);
+int ref_parse_downsample(const char* spec, tsdbhip_query* q);
+int ref_aggregator_get(const char* name);
+int ref_scan_bounds(const tsdbhip_query* q, int64_t* s, int64_t* e);
+
+/* End-to-end query (TsdbQuery.run). Result arrays are malloc'd; free with ref_result_free. */
+typedef struct {
+  int64_t n_groups;
+  int32_t* group_id;
+  int64_t* group_ptr;
+  int64_t* ts_ms;
+  uint64_t* value_bits;
+  uint8_t* is_int;
+  int64_t n_points;
+} ref_result;
+int ref_run_query(const tsdbhip_batch* b, const tsdbhip_query* q, ref_result** out);
+/* Same, but groups processed by nthreads std threads (CPU baseline "parallel over groups"). */
+int ref_run_query_mt(const tsdbhip_batch* b, const tsdbhip_query* q, int nthreads, ref_result** out);
+void ref_result_free(ref_result* r);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

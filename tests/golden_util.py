@@ -1,0 +1,95 @@
+"""Helpers shared by the golden-vector tests: load fixtures, build oracle pipelines,
+replay stores, compare outputs."""
+from __future__ import annotations
+
+import json
+import math
+import os
+
+import numpy as np
+
+from opentsdb_amd import abi
+from opentsdb_amd.query import TsdbQuery, RateOptions
+from opentsdb_amd.store import MockStore
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def build_view(O, node):
+    op = node["op"]
+    if op == "array":
+        return O.array_view(node["points"], node["generator"])
+    if op == "downsample":
+        return O.downsampler(build_view(O, node["src"]), node["spec"], node["start"], node["end"], node["qs"], node["qe"])
+    if op == "downsample_raw":
+        return O.downsampler_raw(build_view(O, node["src"]), node["fn"], node["interval"],
+                                 abi.FILL_NAMES.index(node["fill"]), node["start"], node["end"])
+    if op == "rate":
+        return O.rate(build_view(O, node["src"]), node["counter"], node["counter_max"], node["reset"], node["drop"])
+    if op == "aggregate":
+        interp = node["interp"]
+        ip = None if interp is None else ["lerp", "zim", "max", "min", "prev"].index(interp)
+        return O.aggregate([build_view(O, s) for s in node["srcs"]], node["start"], node["end"], node["fn"], ip,
+                           node["rate"])
+    raise ValueError(op)
+
+
+def values_match(got, want, tol):
+    if isinstance(want, float) and math.isnan(want):
+        return isinstance(got, float) and math.isnan(got)
+    if isinstance(got, float) and math.isnan(got):
+        return False
+    return abs(got - want) <= tol
+
+
+def assert_points(got, expect, tol, check_int=True, ctx=""):
+    """got: [(ts, is_int, value)], expect: [[ts, is_int, value]]"""
+    assert len(got) == len(expect), f"{ctx}: {len(got)} points, expected {len(expect)}"
+    for i, (g, e) in enumerate(zip(got, expect)):
+        assert g[0] == e[0], f"{ctx}[{i}]: ts {g[0]} != {e[0]}"
+        if check_int:
+            assert bool(g[1]) == bool(e[1]), f"{ctx}[{i}] @ {g[0]}: is_int {g[1]} != {e[1]}"
+        if e[1] and g[1]:
+            assert int(g[2]) == int(e[2]), f"{ctx}[{i}] @ {g[0]}: {g[2]} != {e[2]}"
+        else:
+            assert values_match(float(g[2]), float(e[2]), tol), f"{ctx}[{i}] @ {g[0]}: {g[2]} != {e[2]} (tol {tol})"
+
+
+def store_from(points, fix_duplicates=False):
+    st = MockStore(fix_duplicates=fix_duplicates)
+    for metric, tags, ts, kind, value in points:
+        if kind == "long":
+            st.add_long(metric, ts, value, tags)
+        elif kind == "float":
+            st.add_float(metric, ts, value, tags)
+        else:
+            st.add_double(metric, ts, value, tags)
+    return st
+
+
+def query_from(case, store, runner):
+    q = TsdbQuery(store, runner=runner)
+    q.setStartTime(case["start"])
+    q.setEndTime(case["end"])
+    ro = case.get("rate_options")
+    q.setTimeSeries(case["metric"], case["tags"], case["aggregator"], case["rate"],
+                    RateOptions(*ro) if ro else None)
+    ds = case.get("downsample")
+    if ds:
+        q.downsample("-".join(ds))
+    return q
+
+
+def groups_as_points(dps_list):
+    out = []
+    for dps in dps_list:
+        pts = []
+        for dp in dps:
+            pts.append((dp.timestamp(), dp.isInteger(), dp.longValue() if dp.isInteger() else dp.doubleValue()))
+        out.append(pts)
+    return out
