@@ -195,7 +195,7 @@ int tsdbhip_partials_layout_get(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_
 int tsdbhip_run_partials(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_global, void* d_partials);
 /* Turns reduced partial states into the result (on the calling rank). */
 int tsdbhip_finalize(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_global,
-                     const void* d_partials, tsdbhip_result** out);
+                     const void* d_partials, int n_ranks, tsdbhip_result** out);
 /* Device synchronisation helper for host code that does not use HIP directly. */
 int tsdbhip_sync(tsdbhip_ctx* ctx);
 

@@ -1,0 +1,890 @@
+// engine.cpp -- host side of libtsdbhip: the C ABI (include/tsdbhip.h), the query
+// planning the reference does on the host (scan bounds, downsample spec parsing,
+// SpanGroup membership), HBM layout of the loaded Spans, and result assembly.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/tsdbhip.h"
+#include "engine.h"
+
+using namespace tsdb;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_OK(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess)                                                              \
+      return fail(TSDB_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));      \
+  } while (0)
+
+const char* const AGG_NAMES[TSDB_AGG_COUNT_ALL] = {
+    "sum", "pfsum", "min", "max", "avg", "median", "none", "mult", "dev", "diff",
+    "zimsum", "mimmin", "mimmax", "squareSum", "count", "first", "last",
+    "p999", "p99", "p95", "p90", "p75", "p50",
+    "ep999r3", "ep99r3", "ep95r3", "ep90r3", "ep75r3", "ep50r3",
+    "ep999r7", "ep99r7", "ep95r7", "ep90r7", "ep75r7", "ep50r7"};
+
+int interp_of(int a) {  // Aggregators.java:47-173
+  switch (a) {
+    case TSDB_AGG_PFSUM: return TSDB_INTERP_PREV;
+    case TSDB_AGG_NONE: case TSDB_AGG_ZIMSUM: case TSDB_AGG_SQUARESUM: case TSDB_AGG_COUNT:
+    case TSDB_AGG_FIRST: case TSDB_AGG_LAST: return TSDB_INTERP_ZIM;
+    case TSDB_AGG_MIMMIN: return TSDB_INTERP_MAX;
+    case TSDB_AGG_MIMMAX: return TSDB_INTERP_MIN;
+    default: return TSDB_INTERP_LERP;
+  }
+}
+
+// group-aggregator class, -1 if not decomposable (median / percentiles)
+int ga_of(int a) {
+  switch (a) {
+    case TSDB_AGG_SUM: case TSDB_AGG_PFSUM: case TSDB_AGG_ZIMSUM: return GA_SUM;
+    case TSDB_AGG_AVG: return GA_AVG;
+    case TSDB_AGG_COUNT: return GA_COUNT;
+    case TSDB_AGG_SQUARESUM: return GA_SQUARESUM;
+    case TSDB_AGG_MIN: case TSDB_AGG_MIMMIN: return GA_MIN;
+    case TSDB_AGG_MAX: case TSDB_AGG_MIMMAX: return GA_MAX;
+    case TSDB_AGG_DEV: return GA_DEV;
+    case TSDB_AGG_FIRST: return GA_FIRST;
+    case TSDB_AGG_LAST: return GA_LAST;
+    case TSDB_AGG_DIFF: return GA_DIFF;
+    case TSDB_AGG_MULT: return GA_MULT;
+    case TSDB_AGG_NONE: return GA_NONE;
+    default: return -1;
+  }
+}
+
+int f_of(int a) {
+  switch (a) {
+    case TSDB_AGG_SUM: case TSDB_AGG_PFSUM: case TSDB_AGG_ZIMSUM: return F_SUM;
+    case TSDB_AGG_AVG: return F_AVG;
+    case TSDB_AGG_COUNT: return F_COUNT;
+    case TSDB_AGG_SQUARESUM: return F_SQUARESUM;
+    case TSDB_AGG_MIN: case TSDB_AGG_MIMMIN: return F_MIN;
+    case TSDB_AGG_MAX: case TSDB_AGG_MIMMAX: return F_MAX;
+    case TSDB_AGG_DEV: return F_DEV;
+    case TSDB_AGG_FIRST: return F_FIRST;
+    case TSDB_AGG_LAST: return F_LAST;
+    case TSDB_AGG_DIFF: return F_DIFF;
+    case TSDB_AGG_MULT: return F_MULT;
+    default: return -1;
+  }
+}
+
+inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= n && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+    if (e == hipSuccess) n = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+int64_t wave_lds_bytes_host(int64_t K, bool rate) {
+  const int64_t CH = 512, VBUF = 4224;
+  int64_t o = VBUF + CH * 4 + align16((CH + 1) * 2) + CH * 8 + align16(K * 8) + align16(K);
+  if (rate) o += align16(K * 8);
+  o += align16(K * 8) * 2 + align16(K * 4) * 2;
+  return align16(o);
+}
+
+}  // namespace
+
+struct tsdbhip_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[4] = {};
+  std::mutex mu;
+  // resident batch (series in group-sorted order)
+  int64_t n_series = 0, n_rows = 0, n_groups = 0;
+  uint64_t qual_bytes = 0, val_bytes = 0;
+  DevBuf rows, srp, qual, val, gid;
+  std::vector<int64_t> h_srp;          // [n_series+1]
+  std::vector<uint32_t> h_base;        // [n_rows]
+  std::vector<uint32_t> h_ndp;         // [n_rows]
+  std::vector<uint32_t> h_qlen, h_vlen;
+  std::vector<int32_t> h_group;        // [n_series] group of sorted position
+  std::vector<int64_t> h_orig;         // [n_series] original batch index of sorted position
+  // tiles over groups
+  std::vector<int64_t> tb, te, gtp;
+  std::vector<int32_t> tg;
+  DevBuf d_tb, d_te, d_tg, d_gtp;
+  // tiles for the NONE aggregator (one series each)
+  bool none_tiles_ready = false;
+  DevBuf n_tb, n_te, n_tg, n_gtp;
+  // scratch
+  DevBuf pa, pb, pn, pf, out_val, out_flag, gact, err;
+  tsdbhip_timing timing{};
+};
+
+// ===========================================================================
+// host logic restatements
+// ===========================================================================
+extern "C" int tsdbhip_abi_version(void) { return TSDBHIP_ABI_VERSION; }
+extern "C" const char* tsdbhip_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" int tsdbhip_aggregator_get(const char* name) {
+  if (!name) return fail(TSDB_E_NO_SUCH_ELEMENT, "No such aggregator: null");
+  for (int i = 0; i < TSDB_AGG_COUNT_ALL; i++)
+    if (std::strcmp(AGG_NAMES[i], name) == 0) return i;
+  return fail(TSDB_E_NO_SUCH_ELEMENT, std::string("No such aggregator: ") + name);
+}
+
+extern "C" int tsdbhip_aggregator_interpolation(int a) {
+  if (a < 0 || a >= TSDB_AGG_COUNT_ALL) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad aggregator");
+  return interp_of(a);
+}
+
+// DateTime.parseDuration (src/utils/DateTime.java:186-226)
+extern "C" int tsdbhip_parse_duration(const char* duration, int64_t* out_ms) {
+  if (!duration || !*duration) return fail(TSDB_E_ILLEGAL_ARGUMENT, "Invalid duration");
+  const size_t len = std::strlen(duration);
+  size_t unit = 0;
+  while (std::isdigit((unsigned char)duration[unit])) {
+    unit++;
+    if (unit >= len) return fail(TSDB_E_ILLEGAL_ARGUMENT, std::string("Invalid duration, must have an integer and unit: ") + duration);
+  }
+  if (unit == 0 || unit > 18) return fail(TSDB_E_ILLEGAL_ARGUMENT, std::string("Invalid duration (number): ") + duration);
+  const int64_t interval = std::stoll(std::string(duration, unit));
+  if (interval <= 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, std::string("Zero or negative duration: ") + duration);
+  int64_t mult;
+  switch (std::tolower((unsigned char)duration[len - 1])) {
+    case 's':
+      if (len >= 2 && duration[len - 2] == 'm') { *out_ms = interval; return 0; }
+      mult = 1; break;
+    case 'm': mult = 60; break;
+    case 'h': mult = 3600; break;
+    case 'd': mult = 86400; break;
+    case 'w': mult = 604800; break;
+    case 'n': mult = 2592000; break;
+    case 'y': mult = 31536000; break;
+    default: return fail(TSDB_E_ILLEGAL_ARGUMENT, std::string("Invalid duration (suffix): ") + duration);
+  }
+  mult *= 1000;
+  if ((double)interval * (double)mult > 9223372036854775807.0)
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, std::string("Duration must be < Long.MAX_VALUE ms: ") + duration);
+  *out_ms = interval * mult;
+  return 0;
+}
+
+// new DownsamplingSpecification(String) (src/core/DownsamplingSpecification.java:116-191)
+extern "C" int tsdbhip_parse_downsample(const char* spec, tsdbhip_query* q) {
+  if (!spec) return fail(TSDB_E_ILLEGAL_ARGUMENT, "Downsampling specifier cannot be null");
+  std::vector<std::string> parts;
+  std::string cur;
+  for (const char* c = spec; *c; c++) {
+    if (*c == '-') { parts.push_back(cur); cur.clear(); } else cur += *c;
+  }
+  parts.push_back(cur);
+  while (!parts.empty() && parts.back().empty()) parts.pop_back();
+  if (parts.size() < 2)
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, std::string("Invalid downsampling specifier '") + spec + "': must provide at least interval and function");
+  if (parts.size() > 3)
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, std::string("Invalid downsampling specifier '") + spec + "': must consist of interval, function, and optional fill policy");
+  q->ds_all = 0;
+  q->ds_calendar = 0;
+  if (parts[0].find("all") != std::string::npos) {
+    q->ds_interval_ms = 0;
+    q->ds_all = 1;
+  } else {
+    std::string d = parts[0];
+    if (!d.empty() && d.back() == 'c') { d.pop_back(); q->ds_calendar = 1; }
+    int rc = tsdbhip_parse_duration(d.c_str(), &q->ds_interval_ms);
+    if (rc) return rc;
+  }
+  int f = -1;
+  for (int i = 0; i < TSDB_AGG_COUNT_ALL; i++) if (parts[1] == AGG_NAMES[i]) f = i;
+  if (f < 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "No such downsampling function: " + parts[1]);
+  if (f == TSDB_AGG_NONE) return fail(TSDB_E_ILLEGAL_ARGUMENT, "cannot use the NONE aggregator for downsampling");
+  q->ds_function = f;
+  q->ds_fill = TSDB_FILL_NONE;
+  if (parts.size() == 3) {
+    static const char* const fills[5] = {"none", "zero", "nan", "null", "scalar"};
+    int found = -1;
+    for (int i = 0; i < 5; i++) if (strcasecmp(fills[i], parts[2].c_str()) == 0) found = i;
+    if (found < 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "Unrecognized fill policy: " + parts[2]);
+    q->ds_fill = found;
+  }
+  return 0;
+}
+
+// TsdbQuery.getScanStartTimeSeconds / getScanEndTimeSeconds (src/core/TsdbQuery.java:1506-1606)
+extern "C" int tsdbhip_scan_bounds(const tsdbhip_query* q, int64_t* s_out, int64_t* e_out) {
+  const bool ds = q->ds_function >= 0 && q->ds_interval_ms > 0;
+  int64_t start = q->start_time;
+  if ((start & (int64_t)0xFFFFFFFF00000000LL) != 0) start /= 1000;
+  int64_t aligned = start;
+  if (ds) aligned -= ((1000 * start) % q->ds_interval_ms) / 1000;
+  const int64_t ta = aligned - (aligned % 3600);
+  *s_out = ta > 0 ? ta : 0;
+  int64_t end = q->end_time;
+  if ((end & (int64_t)0xFFFFFFFF00000000LL) != 0) {
+    end /= 1000;
+    if (end - (end * 1000) < 1) end++;
+  }
+  if (ds) {
+    const int64_t ia = end + (q->ds_interval_ms - (1000 * end) % q->ds_interval_ms) / 1000;
+    const int64_t toff = ia % 3600;
+    *e_out = toff == 0 ? ia : ia + (3600 - toff);
+  } else {
+    *e_out = end + (3600 - end % 3600);
+  }
+  return 0;
+}
+
+// ===========================================================================
+// context
+// ===========================================================================
+extern "C" int tsdbhip_init(int device, tsdbhip_ctx** out) {
+  if (!out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "out is null");
+  int ndev = 0;
+  HIP_OK(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(TSDB_E_HIP, "no such HIP device " + std::to_string(device));
+  HIP_OK(hipSetDevice(device));
+  auto* c = new tsdbhip_ctx();
+  c->device = device;
+  HIP_OK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  for (auto& e : c->ev) HIP_OK(hipEventCreate(&e));
+  HIP_OK(c->err.ensure(16));
+  *out = c;
+  return 0;
+}
+
+static void release_batch(tsdbhip_ctx* c) {
+  for (DevBuf* b : {&c->rows, &c->srp, &c->qual, &c->val, &c->gid, &c->d_tb, &c->d_te, &c->d_tg, &c->d_gtp,
+                    &c->n_tb, &c->n_te, &c->n_tg, &c->n_gtp})
+    b->release();
+  c->none_tiles_ready = false;
+  c->n_series = c->n_rows = c->n_groups = 0;
+}
+
+extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  release_batch(c);
+  for (DevBuf* b : {&c->pa, &c->pb, &c->pn, &c->pf, &c->out_val, &c->out_flag, &c->gact, &c->err}) b->release();
+  for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+extern "C" int tsdbhip_sync(tsdbhip_ctx* c) {
+  if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
+  HIP_OK(hipSetDevice(c->device));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// Tiles: consecutive series of one group, at most T each.
+static int build_tiles(tsdbhip_ctx* c) {
+  const int64_t n = c->n_series;
+  int64_t T = 64;
+  // keep enough waves in flight for small batches
+  while (T > 1 && (n + T - 1) / T < 8192) T >>= 1;
+  c->tb.clear(); c->te.clear(); c->tg.clear();
+  c->gtp.assign(c->n_groups + 1, 0);
+  int64_t s = 0;
+  for (int64_t g = 0; g < c->n_groups; g++) {
+    c->gtp[g] = (int64_t)c->tb.size();
+    int64_t e = s;
+    while (e < n && c->h_group[e] == g) e++;
+    for (int64_t a = s; a < e; a += T) {
+      c->tb.push_back(a);
+      c->te.push_back(std::min(e, a + T));
+      c->tg.push_back((int32_t)g);
+    }
+    s = e;
+  }
+  c->gtp[c->n_groups] = (int64_t)c->tb.size();
+  const size_t nt = c->tb.size();
+  HIP_OK(c->d_tb.ensure(nt * 8));
+  HIP_OK(c->d_te.ensure(nt * 8));
+  HIP_OK(c->d_tg.ensure(nt * 4));
+  HIP_OK(c->d_gtp.ensure(c->gtp.size() * 8));
+  if (nt) {
+    HIP_OK(hipMemcpy(c->d_tb.p, c->tb.data(), nt * 8, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(c->d_te.p, c->te.data(), nt * 8, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(c->d_tg.p, c->tg.data(), nt * 4, hipMemcpyHostToDevice));
+  }
+  HIP_OK(hipMemcpy(c->d_gtp.p, c->gtp.data(), c->gtp.size() * 8, hipMemcpyHostToDevice));
+  c->none_tiles_ready = false;
+  return 0;
+}
+
+static int build_none_tiles(tsdbhip_ctx* c) {
+  if (c->none_tiles_ready) return 0;
+  const int64_t n = c->n_series;
+  std::vector<int64_t> tb(n), te(n), gtp(n + 1);
+  std::vector<int32_t> tg(n);
+  for (int64_t i = 0; i < n; i++) { tb[i] = i; te[i] = i + 1; tg[i] = (int32_t)i; gtp[i] = i; }
+  gtp[n] = n;
+  HIP_OK(c->n_tb.ensure(n * 8 + 8));
+  HIP_OK(c->n_te.ensure(n * 8 + 8));
+  HIP_OK(c->n_tg.ensure(n * 4 + 4));
+  HIP_OK(c->n_gtp.ensure((n + 1) * 8));
+  if (n) {
+    HIP_OK(hipMemcpy(c->n_tb.p, tb.data(), n * 8, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(c->n_te.p, te.data(), n * 8, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(c->n_tg.p, tg.data(), n * 4, hipMemcpyHostToDevice));
+  }
+  HIP_OK(hipMemcpy(c->n_gtp.p, gtp.data(), (n + 1) * 8, hipMemcpyHostToDevice));
+  c->none_tiles_ready = true;
+  return 0;
+}
+
+static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
+  // classify rows on the device, then fetch ndp for host-side accounting
+  HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
+  HIP_OK(launch_index(c->qual.as<uint8_t>(), c->val.as<uint8_t>(), c->rows.as<RowDesc>(), c->n_rows,
+                      c->err.as<int32_t>(), c->stream));
+  std::vector<RowDesc> back(c->n_rows);
+  if (c->n_rows)
+    HIP_OK(hipMemcpyAsync(back.data(), c->rows.p, c->n_rows * sizeof(RowDesc), hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  (void)rd;
+  c->h_ndp.resize(c->n_rows);
+  c->h_base.resize(c->n_rows);
+  c->h_qlen.resize(c->n_rows);
+  c->h_vlen.resize(c->n_rows);
+  for (int64_t r = 0; r < c->n_rows; r++) {
+    c->h_ndp[r] = back[r].ndp;
+    c->h_base[r] = back[r].base;
+    c->h_qlen[r] = back[r].qlen;
+    c->h_vlen[r] = back[r].vlen;
+  }
+  // malformed rows are reported lazily, when a query reads them (as the reference does)
+  return build_tiles(c);
+}
+
+extern "C" int tsdbhip_load(tsdbhip_ctx* c, const tsdbhip_batch* b) {
+  if (!c || !b) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  if (b->n_series < 0 || b->n_rows < 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
+  if (b->n_series > 0 && (!b->series_row_ptr || !b->group_id)) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null batch arrays");
+  if (b->n_rows > 0 && (!b->row_base_time || !b->row_qual_off || !b->row_val_off || !b->qual || !b->val))
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, "null batch arrays");
+  if (b->n_series > 0 && (b->series_row_ptr[0] != 0 || b->series_row_ptr[b->n_series] != b->n_rows))
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, "series_row_ptr does not cover the rows");
+  release_batch(c);
+  // stable order of series by group (SpanGroup membership; order inside a group kept)
+  std::vector<int64_t> order;
+  int32_t maxg = -1;
+  for (int64_t s = 0; s < b->n_series; s++) {
+    if (b->series_row_ptr[s + 1] < b->series_row_ptr[s]) return fail(TSDB_E_ILLEGAL_ARGUMENT, "series_row_ptr not monotonic");
+    if (b->group_id[s] >= 0) { order.push_back(s); maxg = std::max(maxg, b->group_id[s]); }
+  }
+  std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return b->group_id[x] < b->group_id[y]; });
+  c->n_series = (int64_t)order.size();
+  c->n_groups = maxg + 1;
+  c->h_group.resize(c->n_series);
+  c->h_orig = order;
+  c->h_srp.assign(c->n_series + 1, 0);
+  std::vector<RowDesc> rd;
+  uint64_t qtot = 0, vtot = 0;
+  for (int64_t i = 0; i < c->n_series; i++) {
+    const int64_t s = order[i];
+    c->h_group[i] = b->group_id[s];
+    for (int64_t r = b->series_row_ptr[s]; r < b->series_row_ptr[s + 1]; r++) {
+      RowDesc d{};
+      d.base = b->row_base_time[r];
+      const uint64_t ql = b->row_qual_off[r + 1] - b->row_qual_off[r];
+      const uint64_t vl = b->row_val_off[r + 1] - b->row_val_off[r];
+      if (ql > 0xFFFFFFFFull || vl > 0xFFFFFFFFull) return fail(TSDB_E_ILLEGAL_ARGUMENT, "row too large");
+      d.qlen = (uint32_t)ql;
+      d.vlen = (uint32_t)vl;
+      d.qoff = qtot;
+      d.voff = vtot;
+      qtot += align16(ql);
+      vtot += align16(vl);
+      rd.push_back(d);
+    }
+    c->h_srp[i + 1] = (int64_t)rd.size();
+  }
+  // rows of a series must be in base-time order (Span.checkRowOrder): stable sort per series
+  for (int64_t i = 0; i < c->n_series; i++)
+    std::stable_sort(rd.begin() + c->h_srp[i], rd.begin() + c->h_srp[i + 1],
+                     [](const RowDesc& x, const RowDesc& y) { return x.base < y.base; });
+  c->n_rows = (int64_t)rd.size();
+  c->qual_bytes = qtot;
+  c->val_bytes = vtot;
+  // staging: re-laid-out blobs
+  std::vector<uint8_t> hq(qtot + 64, 0), hv(vtot + 64, 0);
+  {
+    // copy rows in the order their offsets were assigned (before the per-series sort)
+    uint64_t qo = 0, vo = 0;
+    for (int64_t i = 0; i < c->n_series; i++) {
+      const int64_t s = order[i];
+      for (int64_t r = b->series_row_ptr[s]; r < b->series_row_ptr[s + 1]; r++) {
+        const uint64_t ql = b->row_qual_off[r + 1] - b->row_qual_off[r];
+        const uint64_t vl = b->row_val_off[r + 1] - b->row_val_off[r];
+        std::memcpy(hq.data() + qo, b->qual + b->row_qual_off[r], ql);
+        std::memcpy(hv.data() + vo, b->val + b->row_val_off[r], vl);
+        qo += align16(ql);
+        vo += align16(vl);
+      }
+    }
+  }
+  HIP_OK(c->rows.ensure(std::max<size_t>(1, rd.size()) * sizeof(RowDesc)));
+  HIP_OK(c->srp.ensure((c->n_series + 1) * 8));
+  HIP_OK(c->qual.ensure(hq.size()));
+  HIP_OK(c->val.ensure(hv.size()));
+  HIP_OK(c->gid.ensure(std::max<int64_t>(1, c->n_series) * 4));
+  if (!rd.empty()) HIP_OK(hipMemcpy(c->rows.p, rd.data(), rd.size() * sizeof(RowDesc), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(c->srp.p, c->h_srp.data(), (c->n_series + 1) * 8, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(c->qual.p, hq.data(), hq.size(), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(c->val.p, hv.data(), hv.size(), hipMemcpyHostToDevice));
+  if (c->n_series) HIP_OK(hipMemcpy(c->gid.p, c->h_group.data(), c->n_series * 4, hipMemcpyHostToDevice));
+  return finish_load(c, rd);
+}
+
+// ---------------------------------------------------------------------------
+// synthetic store in HBM (the MockBase-equivalent generator of BASELINE.md)
+// ---------------------------------------------------------------------------
+extern "C" int tsdbhip_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp) {
+  if (!c || !sp) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  if (sp->n_series <= 0 || sp->n_points <= 0 || sp->period_ms <= 0 || sp->n_groups <= 0 || sp->start_s < 0)
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad synth spec");
+  if (sp->value_kind != 0 && sp->int_mod <= 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "int_mod must be > 0");
+  release_batch(c);
+  const bool ms_qual = (sp->period_ms % 1000) != 0 || (sp->start_s * 1000) % 1000 != 0;
+  const int qw = ms_qual ? 4 : 2;
+  const int64_t start_ms = sp->start_s * 1000;
+  // row template
+  std::vector<int64_t> k0;
+  std::vector<int32_t> rn;
+  std::vector<uint32_t> rbase;
+  for (int64_t k = 0; k < sp->n_points;) {
+    const int64_t ts = start_ms + k * sp->period_ms;
+    const int64_t base = (ts / 1000) - (ts / 1000) % 3600;
+    int64_t e = k;
+    while (e < sp->n_points && (start_ms + e * sp->period_ms) / 1000 - ((start_ms + e * sp->period_ms) / 1000) % 3600 == base) e++;
+    k0.push_back(k);
+    rn.push_back((int32_t)(e - k));
+    rbase.push_back((uint32_t)base);
+    k = e;
+  }
+  const int64_t R = (int64_t)k0.size();
+  const int64_t S = sp->n_series, G = sp->n_groups;
+  std::vector<int64_t> grp_off(G + 1, 0);
+  for (int64_t g = 0; g < G; g++) grp_off[g + 1] = grp_off[g] + S / G + (g < S % G ? 1 : 0);
+  c->n_series = S;
+  c->n_rows = S * R;
+  c->n_groups = G;
+  // qualifier offsets (identical layout for every series)
+  std::vector<int64_t> rq(R);
+  int64_t QS = 0;
+  for (int64_t h = 0; h < R; h++) { rq[h] = QS; QS += align16((int64_t)rn[h] * qw); }
+  DevBuf d_k0, d_rn, d_rbase, d_goff, d_vbytes;
+  HIP_OK(d_k0.ensure(R * 8));
+  HIP_OK(d_rn.ensure(R * 4));
+  HIP_OK(d_rbase.ensure(R * 4));
+  HIP_OK(d_goff.ensure((G + 1) * 8));
+  HIP_OK(hipMemcpy(d_k0.p, k0.data(), R * 8, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(d_rn.p, rn.data(), R * 4, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(d_rbase.p, rbase.data(), R * 4, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(d_goff.p, grp_off.data(), (G + 1) * 8, hipMemcpyHostToDevice));
+  HIP_OK(c->gid.ensure(S * 4));
+  SynthParams p{};
+  p.n_series = S; p.n_groups = G; p.n_rows_per_series = R; p.n_points = sp->n_points;
+  p.start_ms = start_ms; p.period_ms = sp->period_ms; p.value_kind = sp->value_kind; p.ms_qual = ms_qual;
+  p.int_mod = sp->int_mod; p.seed = sp->seed;
+  p.grp_off = d_goff.as<int64_t>(); p.row_k0 = d_k0.as<int64_t>(); p.row_n = d_rn.as<int32_t>();
+  p.row_base = d_rbase.as<uint32_t>(); p.group_id = c->gid.as<int32_t>();
+  // value bytes per row
+  std::vector<uint32_t> vbytes;
+  if (sp->value_kind == 0) {
+    vbytes.resize(S * R);
+    for (int64_t s = 0; s < S; s++)
+      for (int64_t h = 0; h < R; h++) vbytes[s * R + h] = (uint32_t)(rn[h] * 4 + (rn[h] > 1 ? 1 : 0));
+  } else {
+    HIP_OK(d_vbytes.ensure(S * R * 4));
+    p.row_vbytes = d_vbytes.as<uint32_t>();
+    HIP_OK(launch_synth_sizes(p, c->stream));
+    vbytes.resize(S * R);
+    HIP_OK(hipMemcpyAsync(vbytes.data(), d_vbytes.p, S * R * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+  }
+  std::vector<RowDesc> rd(S * R);
+  uint64_t vtot = 0;
+  for (int64_t s = 0; s < S; s++) {
+    for (int64_t h = 0; h < R; h++) {
+      RowDesc& d = rd[s * R + h];
+      d.base = rbase[h];
+      d.qoff = (uint64_t)(s * QS + rq[h]);
+      d.qlen = (uint32_t)(rn[h] * qw);
+      d.voff = vtot;
+      d.vlen = vbytes[s * R + h];
+      vtot += align16(d.vlen);
+    }
+  }
+  c->qual_bytes = (uint64_t)(S * QS);
+  c->val_bytes = vtot;
+  HIP_OK(c->rows.ensure(rd.size() * sizeof(RowDesc)));
+  HIP_OK(c->qual.ensure(c->qual_bytes + 64));
+  HIP_OK(c->val.ensure(c->val_bytes + 64));
+  HIP_OK(hipMemsetAsync(c->qual.p, 0, c->qual_bytes + 64, c->stream));
+  HIP_OK(hipMemsetAsync(c->val.p, 0, c->val_bytes + 64, c->stream));
+  HIP_OK(hipMemcpyAsync(c->rows.p, rd.data(), rd.size() * sizeof(RowDesc), hipMemcpyHostToDevice, c->stream));
+  p.rows = c->rows.as<RowDesc>();
+  p.qual = c->qual.as<uint8_t>();
+  p.val = c->val.as<uint8_t>();
+  HIP_OK(launch_synth_write(p, c->stream));
+  c->h_srp.resize(S + 1);
+  for (int64_t s = 0; s <= S; s++) c->h_srp[s] = s * R;
+  HIP_OK(c->srp.ensure((S + 1) * 8));
+  HIP_OK(hipMemcpyAsync(c->srp.p, c->h_srp.data(), (S + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  c->h_group.resize(S);
+  c->h_orig.resize(S);
+  for (int64_t g = 0; g < G; g++)
+    for (int64_t i = grp_off[g]; i < grp_off[g + 1]; i++) c->h_group[i] = (int32_t)g;
+  std::iota(c->h_orig.begin(), c->h_orig.end(), 0);
+  HIP_OK(hipStreamSynchronize(c->stream));
+  return finish_load(c, rd);
+}
+
+extern "C" int tsdbhip_batch_sizes(tsdbhip_ctx* c, int64_t* n_series, int64_t* n_rows, uint64_t* qual_bytes,
+                                   uint64_t* val_bytes) {
+  if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
+  uint64_t q = 0, v = 0;
+  for (int64_t r = 0; r < c->n_rows; r++) { q += c->h_qlen[r]; v += c->h_vlen[r]; }
+  *n_series = c->n_series;
+  *n_rows = c->n_rows;
+  *qual_bytes = q;
+  *val_bytes = v;
+  return 0;
+}
+
+// Resident batch back to host in the tsdbhip_batch layout (series in resident order).
+extern "C" int tsdbhip_batch_download(tsdbhip_ctx* c, int64_t* series_row_ptr, uint32_t* row_base_time,
+                                      uint64_t* row_qual_off, uint64_t* row_val_off, uint8_t* qual, uint8_t* val,
+                                      int32_t* group_id) {
+  if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  std::vector<RowDesc> rd(c->n_rows);
+  if (c->n_rows) HIP_OK(hipMemcpy(rd.data(), c->rows.p, c->n_rows * sizeof(RowDesc), hipMemcpyDeviceToHost));
+  std::vector<uint8_t> hq(c->qual.n), hv(c->val.n);
+  HIP_OK(hipMemcpy(hq.data(), c->qual.p, c->qual.n, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(hv.data(), c->val.p, c->val.n, hipMemcpyDeviceToHost));
+  uint64_t qo = 0, vo = 0;
+  for (int64_t r = 0; r < c->n_rows; r++) {
+    row_base_time[r] = rd[r].base;
+    row_qual_off[r] = qo;
+    row_val_off[r] = vo;
+    std::memcpy(qual + qo, hq.data() + rd[r].qoff, rd[r].qlen);
+    std::memcpy(val + vo, hv.data() + rd[r].voff, rd[r].vlen);
+    qo += rd[r].qlen;
+    vo += rd[r].vlen;
+  }
+  row_qual_off[c->n_rows] = qo;
+  row_val_off[c->n_rows] = vo;
+  for (int64_t s = 0; s <= c->n_series; s++) series_row_ptr[s] = c->h_srp[s];
+  for (int64_t s = 0; s < c->n_series; s++) group_id[s] = c->h_group[s];
+  return 0;
+}
+
+// ===========================================================================
+// query execution
+// ===========================================================================
+namespace {
+
+struct Plan {
+  int ga = 0, f = 0, interp = 0;
+  int mode = MODE_GRID;
+  int64_t ss = 0, se = 0, B0 = 0, I = 1, K = 0;
+  bool none = false;
+};
+
+int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
+  if (q->aggregator < 0 || q->aggregator >= TSDB_AGG_COUNT_ALL) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad aggregator");
+  if (q->ds_function >= TSDB_AGG_COUNT_ALL) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad downsampling function");
+  if (q->ds_function == TSDB_AGG_NONE) return fail(TSDB_E_ILLEGAL_ARGUMENT, "cannot use the NONE aggregator for downsampling");
+  if (q->ds_function < 0)
+    return fail(TSDB_E_NOT_IMPLEMENTED, "queries without downsampling (raw union LERP) are not implemented yet");
+  if (q->ds_calendar) return fail(TSDB_E_NOT_IMPLEMENTED, "calendar downsampling is not implemented yet");
+  if (!q->ds_all && q->ds_interval_ms <= 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "interval not > 0");
+  P.ga = ga_of(q->aggregator);
+  P.f = f_of(q->ds_function);
+  if (P.ga < 0) return fail(TSDB_E_NOT_IMPLEMENTED, std::string("group-by aggregator not implemented yet: ") + AGG_NAMES[q->aggregator]);
+  if (P.f < 0) return fail(TSDB_E_NOT_IMPLEMENTED, std::string("downsampling function not implemented yet: ") + AGG_NAMES[q->ds_function]);
+  if ((q->flags & TSDB_QF_ORDERED) && (P.ga == GA_SUM || P.ga == GA_AVG || P.ga == GA_SQUARESUM || P.ga == GA_DEV || P.ga == GA_MULT))
+    return fail(TSDB_E_NOT_IMPLEMENTED, "ordered cross-series reduction not implemented yet");
+  P.interp = interp_of(q->aggregator);
+  P.none = q->aggregator == TSDB_AGG_NONE;
+  tsdbhip_scan_bounds(q, &P.ss, &P.se);
+  const int64_t S0 = P.ss * 1000, E0 = P.se * 1000;
+  if (q->ds_all) {
+    P.mode = MODE_ALL;
+    P.I = 1;
+    P.B0 = 0;
+    P.K = 1;
+  } else {
+    P.mode = MODE_GRID;
+    const int64_t I = q->ds_interval_ms;
+    P.I = I;
+    P.B0 = ((S0 + I - 1) / I) * I;  // Downsampler seek: first bucket fully after the scan start
+    if (q->ds_fill != TSDB_FILL_NONE) {
+      const int64_t aE = E0 - E0 % I;
+      P.K = aE > P.B0 ? (aE - P.B0) / I : 0;
+    } else {
+      P.K = E0 > P.B0 ? (E0 - P.B0 + I - 1) / I : 0;
+    }
+  }
+  const int64_t need = wave_lds_bytes_host(P.K, q->rate != 0);
+  if (need > 160 * 1024)
+    return fail(TSDB_E_NOT_IMPLEMENTED, "too many downsample buckets in the query window for one wave (" + std::to_string(P.K) + ")");
+  return 0;
+}
+
+int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bool do_reduce) {
+  const bool none = P.none;
+  if (none) { int rc = build_none_tiles(c); if (rc) return rc; }
+  const int64_t nt = none ? c->n_series : (int64_t)c->tb.size();
+  const int64_t K = P.K;
+  HIP_OK(c->pa.ensure(std::max<int64_t>(1, nt * K) * 8));
+  HIP_OK(c->pb.ensure(std::max<int64_t>(1, nt * K) * 8));
+  HIP_OK(c->pn.ensure(std::max<int64_t>(1, nt * K) * 4));
+  HIP_OK(c->pf.ensure(std::max<int64_t>(1, nt * K) * 4));
+  HIP_OK(c->out_val.ensure(std::max<int64_t>(1, G * K) * 8));
+  HIP_OK(c->out_flag.ensure(std::max<int64_t>(1, G * K)));
+  HIP_OK(c->gact.ensure(std::max<int64_t>(1, G) * 4));
+  HIP_OK(hipMemsetAsync(c->gact.p, 0, std::max<int64_t>(1, G) * 4, c->stream));
+  HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
+  GridParams gp{};
+  gp.rows = c->rows.as<RowDesc>();
+  gp.series_row_ptr = c->srp.as<int64_t>();
+  gp.qual = c->qual.as<uint8_t>();
+  gp.val = c->val.as<uint8_t>();
+  gp.tile_begin = (none ? c->n_tb : c->d_tb).as<int64_t>();
+  gp.tile_end = (none ? c->n_te : c->d_te).as<int64_t>();
+  gp.tile_group = (none ? c->n_tg : c->d_tg).as<int32_t>();
+  gp.n_tiles = nt;
+  gp.ss = P.ss;
+  gp.se = P.se;
+  gp.B0 = P.B0;
+  gp.I = P.I;
+  gp.K = K;
+  gp.qs = q->start_time;
+  gp.qe = q->end_time;
+  gp.rcpI = (float)(1.0 / (double)P.I);
+  gp.mode = P.mode;
+  gp.ga = P.ga;
+  gp.interp = P.interp;
+  gp.fill = q->ds_fill;
+  gp.rate = q->rate;
+  gp.counter = q->rate_counter;
+  gp.drop = q->rate_drop_resets;
+  gp.counter_max = q->rate_counter_max;
+  gp.reset_value = q->rate_reset_value;
+  gp.wave_lds = (int32_t)wave_lds_bytes_host(K, q->rate != 0);
+  int waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / gp.wave_lds));
+  gp.waves = waves;
+  gp.part = Partials{c->pa.as<double>(), c->pb.as<double>(), c->pn.as<uint32_t>(), c->pf.as<uint32_t>()};
+  gp.group_active = c->gact.as<uint32_t>();
+  gp.err = c->err.as<int32_t>();
+  HIP_OK(hipEventRecord(c->ev[0], c->stream));
+  HIP_OK(launch_grid(gp, P.f, c->stream));
+  HIP_OK(hipEventRecord(c->ev[1], c->stream));
+  if (do_reduce) {
+    ReduceParams rp{};
+    rp.part = gp.part;
+    rp.group_tile_ptr = (none ? c->n_gtp : c->d_gtp).as<int64_t>();
+    rp.G = G;
+    rp.K = K;
+    rp.ga = P.ga;
+    rp.out_val = c->out_val.as<double>();
+    rp.out_flag = c->out_flag.as<uint8_t>();
+    rp.err = c->err.as<int32_t>();
+    HIP_OK(launch_reduce(rp, c->stream));
+  }
+  HIP_OK(hipEventRecord(c->ev[2], c->stream));
+  return 0;
+}
+
+void account(tsdbhip_ctx* c, const Plan& P) {
+  int64_t dps = 0, bytes = 0;
+  for (int64_t s = 0; s < c->n_series; s++) {
+    bytes += 8;
+    for (int64_t r = c->h_srp[s]; r < c->h_srp[s + 1]; r++) {
+      if ((int64_t)c->h_base[r] < P.ss || (int64_t)c->h_base[r] >= P.se) continue;
+      dps += c->h_ndp[r];
+      bytes += (int64_t)c->h_qlen[r] + c->h_vlen[r] + (int64_t)sizeof(RowDesc);
+    }
+  }
+  c->timing.datapoints = dps;
+  c->timing.bytes = bytes;
+}
+
+tsdbhip_result* make_result(int64_t n_groups, int64_t n_points) {
+  const size_t bytes = sizeof(tsdbhip_result) + (n_groups + 1) * 4 + (n_groups + 1) * 8 + (n_points + 1) * 8 * 2 +
+                       (n_points + 1) + 64;
+  char* m = (char*)std::calloc(1, bytes);
+  if (!m) return nullptr;
+  auto* r = reinterpret_cast<tsdbhip_result*>(m);
+  char* p = m + sizeof(tsdbhip_result);
+  auto al8 = [&](char* x) { return (char*)(((uintptr_t)x + 7) & ~(uintptr_t)7); };
+  p = al8(p);
+  r->group_ptr = (const int64_t*)p; p += (n_groups + 1) * 8;
+  r->ts_ms = (const int64_t*)p; p += (n_points + 1) * 8;
+  r->value_bits = (const uint64_t*)p; p += (n_points + 1) * 8;
+  r->group_id = (const int32_t*)p; p += (n_groups + 1) * 4;
+  r->is_int = (const uint8_t*)p;
+  r->n_groups = n_groups;
+  return r;
+}
+
+int assemble(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, const std::vector<double>& val,
+             const std::vector<uint8_t>& flag, const std::vector<uint32_t>& act, tsdbhip_result** out) {
+  const int64_t K = P.K;
+  // group emission order: batch group id order; NONE: span order (original series order)
+  std::vector<std::pair<int64_t, int64_t>> groups;  // (result group id, row in dense output)
+  if (P.none) {
+    std::vector<std::pair<int64_t, int64_t>> tmp;
+    for (int64_t g = 0; g < G; g++) if (act[g]) tmp.push_back({c->h_orig[g], g});
+    std::sort(tmp.begin(), tmp.end());
+    for (size_t i = 0; i < tmp.size(); i++) groups.push_back({(int64_t)i, tmp[i].second});
+  } else {
+    for (int64_t g = 0; g < G; g++) if (act[g]) groups.push_back({g, g});
+  }
+  int64_t npts = 0;
+  for (auto& gr : groups)
+    for (int64_t k = 0; k < K; k++) npts += flag[gr.second * K + k] ? 1 : 0;
+  tsdbhip_result* r = make_result((int64_t)groups.size(), npts);
+  if (!r) return fail(TSDB_E_NOMEM, "result allocation");
+  auto* gptr = const_cast<int64_t*>(r->group_ptr);
+  auto* gid = const_cast<int32_t*>(r->group_id);
+  auto* ts = const_cast<int64_t*>(r->ts_ms);
+  auto* vb = const_cast<uint64_t*>(r->value_bits);
+  int64_t o = 0;
+  for (size_t i = 0; i < groups.size(); i++) {
+    gptr[i] = o;
+    gid[i] = (int32_t)groups[i].first;
+    const int64_t row = groups[i].second;
+    for (int64_t k = 0; k < K; k++) {
+      if (!flag[row * K + k]) continue;
+      // only points inside [start_time, end_time] of the SpanGroup are produced (x <= end_time)
+      ts[o] = (P.mode == MODE_ALL) ? q->start_time : P.B0 + k * P.I;
+      std::memcpy(&vb[o], &val[row * K + k], 8);
+      o++;
+    }
+  }
+  gptr[groups.size()] = o;
+  *out = r;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
+  if (!c || !q || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  *out = nullptr;
+  HIP_OK(hipSetDevice(c->device));
+  Plan P;
+  int rc = plan_query(c, q, P);
+  if (rc) return rc;
+  const int64_t G = P.none ? c->n_series : c->n_groups;
+  rc = run_device(c, q, P, G, true);
+  if (rc) return rc;
+  std::vector<double> val(G * P.K);
+  std::vector<uint8_t> flag(G * P.K);
+  std::vector<uint32_t> act(std::max<int64_t>(1, G));
+  int32_t err = 0;
+  if (G * P.K) {
+    HIP_OK(hipMemcpyAsync(val.data(), c->out_val.p, G * P.K * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipMemcpyAsync(flag.data(), c->out_flag.p, G * P.K, hipMemcpyDeviceToHost, c->stream));
+  }
+  if (G) HIP_OK(hipMemcpyAsync(act.data(), c->gact.p, G * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  float t01 = 0, t12 = 0;
+  (void)hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
+  (void)hipEventElapsedTime(&t12, c->ev[1], c->ev[2]);
+  c->timing.decode_downsample_ms = t01;
+  c->timing.group_reduce_ms = t12;
+  c->timing.total_ms = t01 + t12;
+  account(c, P);
+  if (err) return fail(err, "error raised by the device path");
+  if (P.mode == MODE_ALL) {
+    // AggregationIterator ctor: the single "all" point is skipped unless start_time <= qs <= end_time
+    const int64_t S0 = P.ss * 1000, E0 = P.se * 1000;
+    if (q->start_time < S0 || q->start_time > E0) std::fill(flag.begin(), flag.end(), 0);
+  }
+  return assemble(c, q, P, G, val, flag, act, out);
+}
+
+extern "C" void tsdbhip_result_free(tsdbhip_result* r) { std::free(r); }
+
+extern "C" int tsdbhip_last_timing(tsdbhip_ctx* c, tsdbhip_timing* out) {
+  if (!c || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  *out = c->timing;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// multi-GPU partials: every rank reduces its shard to per-(group, slot) partial
+// states; ranks all-gather them (RCCL) and each merges in rank order.
+// ---------------------------------------------------------------------------
+extern "C" int tsdbhip_partials_layout_get(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global,
+                                           tsdbhip_partials_layout* out) {
+  if (!c || !q || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  Plan P;
+  int rc = plan_query(c, q, P);
+  if (rc) return rc;
+  if (P.none) return fail(TSDB_E_NOT_IMPLEMENTED, "NONE aggregator is per-span; no partial exchange");
+  if (n_groups_global < c->n_groups) return fail(TSDB_E_ILLEGAL_ARGUMENT, "n_groups_global smaller than the local groups");
+  out->n_groups = n_groups_global;
+  out->n_slots = P.K;
+  // per (group, slot): a, b, n, f as doubles; then one activity double per group
+  out->n_sum = 0;
+  out->n_min = 0;
+  out->n_max = 0;
+  out->bytes = (n_groups_global * P.K * 4 + n_groups_global) * 8;
+  return 0;
+}
+
+
+extern "C" int tsdbhip_run_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, void* d_partials) {
+  (void)c; (void)q; (void)n_groups_global; (void)d_partials;
+  return fail(TSDB_E_NOT_IMPLEMENTED, "multi-GPU partials: not implemented yet");
+}
+
+extern "C" int tsdbhip_finalize(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, const void* d_partials,
+                                int n_ranks, tsdbhip_result** out) {
+  (void)c; (void)q; (void)n_groups_global; (void)d_partials; (void)n_ranks; (void)out;
+  return fail(TSDB_E_NOT_IMPLEMENTED, "multi-GPU partials: not implemented yet");
+}

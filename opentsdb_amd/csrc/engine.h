@@ -1,0 +1,121 @@
+// engine.h -- internal declarations shared by the host side (engine.cpp) and the
+// gfx950 kernels (kernels.hip) of libtsdbhip.  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tsdb {
+
+// One compacted cell (RowSeq) as laid out in HBM.  qoff/voff are 16-byte aligned.
+struct RowDesc {
+  uint64_t qoff;    // byte offset of the qualifiers in the qualifier blob
+  uint64_t voff;    // byte offset of the values (incl. trailing meta byte) in the value blob
+  uint32_t base;    // row base time, seconds
+  uint32_t ndp;     // datapoints in the row
+  uint32_t qlen;    // qualifier bytes
+  uint32_t vlen;    // value bytes
+  uint32_t flags;   // ROW_* below
+  uint32_t pad;
+};
+
+// RowDesc.flags
+enum : uint32_t {
+  ROW_QW_MASK = 0x7,        // 2 = all 2-byte (second) qualifiers, 4 = all 4-byte (ms), 0 = mixed
+  ROW_VL_SHIFT = 8,         // uniform value length 1/2/4/8, 0 = variable (vle ints)
+  ROW_VL_MASK = 0xF00,
+  ROW_ERR = 0x10000,        // malformed cell (IllegalDataException when decoded)
+};
+
+// Per-tile partial group state, structure of arrays, [tile][K].
+struct Partials {
+  double* a;
+  double* b;
+  uint32_t* n;
+  uint32_t* f;   // bit0 union (a real point of some series sits on this slot), bit1 has, >>2 count
+};
+
+enum : uint32_t { PF_UNION = 1u, PF_HAS = 2u };
+
+// Kernel modes
+enum : int { MODE_GRID = 0, MODE_ALL = 1 };
+
+// Group-aggregator classes (cross-series reduction)
+enum : int {
+  GA_SUM = 0, GA_AVG, GA_COUNT, GA_SQUARESUM, GA_MIN, GA_MAX, GA_DEV, GA_FIRST, GA_LAST,
+  GA_DIFF, GA_MULT, GA_NONE
+};
+// Downsample function classes (per-bucket, per-series, sequential in time order)
+enum : int {
+  F_SUM = 0, F_AVG, F_COUNT, F_SQUARESUM, F_MIN, F_MAX, F_DEV, F_FIRST, F_LAST, F_DIFF, F_MULT,
+  F_NUM
+};
+
+struct GridParams {
+  // data
+  const RowDesc* rows;
+  const int64_t* series_row_ptr;
+  const uint8_t* qual;
+  const uint8_t* val;
+  // tiles: series [tile_begin[t], tile_end[t]) of group tile_group[t]
+  const int64_t* tile_begin;
+  const int64_t* tile_end;
+  const int32_t* tile_group;
+  int64_t n_tiles;
+  // query geometry (ms unless noted)
+  int64_t ss, se;        // scan bounds, seconds: rows with base in [ss, se)
+  int64_t B0;            // timestamp of slot 0
+  int64_t I;             // interval
+  int64_t K;             // slots
+  int64_t qs, qe;        // "all" bounds (raw query start/end)
+  float rcpI;            // 1/I as float (slot division)
+  int32_t mode;          // MODE_*
+  int32_t ga;            // GA_*
+  int32_t interp;        // TSDB_INTERP_*
+  int32_t fill;          // TSDB_FILL_*
+  int32_t rate, counter, drop;
+  int64_t counter_max, reset_value;
+  int32_t wave_lds;      // bytes of LDS per wave
+  int32_t waves;         // waves per workgroup
+  // outputs
+  Partials part;
+  uint32_t* group_active;
+  int32_t* err;          // first error code (atomicCAS from 0)
+};
+
+struct ReduceParams {
+  Partials part;
+  const int64_t* group_tile_ptr;  // [G+1]
+  int64_t G, K;
+  int32_t ga;
+  double* out_val;                // [G][K]
+  uint8_t* out_flag;              // [G][K] bit0 emit
+  int32_t* err;
+};
+
+struct SynthParams {
+  int64_t n_series, n_groups, n_rows_per_series, n_points;
+  int64_t start_ms, period_ms;
+  int32_t value_kind, ms_qual;
+  int64_t int_mod;
+  uint64_t seed;
+  const int64_t* grp_off;        // [G+1] batch position offsets of each group
+  // per-row template (identical for every series): first point index, count, base time
+  const int64_t* row_k0;
+  const int32_t* row_n;
+  const uint32_t* row_base;
+  RowDesc* rows;                 // [n_series * R]
+  uint8_t* qual;
+  uint8_t* val;
+  uint32_t* row_vbytes;          // pass 1 output (value bytes incl. meta)
+  int32_t* group_id;             // [n_series] (batch order)
+};
+
+// launchers (kernels.hip)
+hipError_t launch_index(const uint8_t* qual, const uint8_t* val, RowDesc* rows, int64_t n_rows, int32_t* err,
+                        hipStream_t s);
+hipError_t launch_grid(const GridParams& p, int ds_function_class, hipStream_t s);
+hipError_t launch_reduce(const ReduceParams& p, hipStream_t s);
+hipError_t launch_synth_sizes(const SynthParams& p, hipStream_t s);
+hipError_t launch_synth_write(const SynthParams& p, hipStream_t s);
+
+}  // namespace tsdb

@@ -1,0 +1,1112 @@
+// kernels.hip -- gfx950 kernels of libtsdbhip: the OpenTSDB query-time aggregation
+// hot path (decode compacted cells -> per-series downsample -> cross-series group-by).
+//
+// The path is HBM-bound integer/byte work: no MFMA.  Design (DESIGN.md has the numbers):
+//  * k_index   one wave per compacted row: classifies qualifier width / value length so
+//              the main kernel can address datapoints directly (built once at load).
+//  * k_grid    one wave per "tile" (<= T consecutive series of ONE SpanGroup).  For each
+//              series the wave streams its rows in 512-datapoint chunks with 16-byte
+//              coalesced loads, decodes qualifier+value in registers, stages the decoded
+//              doubles in LDS, reduces every (series, bucket) segment sequentially in time
+//              order (bit-exact with Downsampler's runDouble), then turns the series'
+//              bucket stream into SpanGroup contributions (LERP / ZIM / MAX / MIN / PREV
+//              interpolation, fill policies, RateSpan) accumulated into the tile's
+//              per-slot partial state in LDS.  No atomics on the data path.
+//  * k_reduce  merges tile partials of each group in tile (= series) order and finalises
+//              the aggregator (AggregationIterator.doubleValue semantics).
+#include "engine.h"
+
+#include <float.h>
+#include <math.h>
+
+#include "../../include/tsdbhip.h"
+
+namespace tsdb {
+
+#define WAVE_SYNC()                                          \
+  do {                                                       \
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   \
+    __builtin_amdgcn_wave_barrier();                         \
+  } while (0)
+
+static constexpr int CH = 512;          // datapoints per chunk (64 lanes x 8)
+static constexpr int DPL = 8;           // datapoints per lane
+static constexpr int VBUF = 4224;       // value staging bytes (aliases the decoded-double area)
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ void set_err(int32_t* err, int code) { atomicCAS(err, 0, code); }
+
+// ---- wave scans (64 lanes) ------------------------------------------------
+__device__ __forceinline__ int wave_incl_sum(int x) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    int y = __shfl_up(x, d, 64);
+    if (l >= d) x += y;
+  }
+  return x;
+}
+__device__ __forceinline__ int wave_incl_max(int x) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    int y = __shfl_up(x, d, 64);
+    if (l >= d) x = max(x, y);
+  }
+  return x;
+}
+__device__ __forceinline__ int wave_max(int x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x = max(x, __shfl_xor(x, d, 64));
+  return x;
+}
+__device__ __forceinline__ int wave_min(int x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x = min(x, __shfl_xor(x, d, 64));
+  return x;
+}
+__device__ __forceinline__ long long wave_sum64(long long x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  return x;
+}
+
+// ---- big-endian value decode (RowSeq.extractIntegerValue / extractFloatingPointValue,
+//      src/core/RowSeq.java:233-266); returns false on an illegal length -------------
+__device__ __forceinline__ bool decode_value(uint64_t be_bits, int len, bool is_float, double& out) {
+  // be_bits holds the len value bytes big-endian in its low len*8 bits
+  if (is_float) {
+    if (len == 4) { out = (double)__uint_as_float((uint32_t)be_bits); return true; }
+    if (len == 8) { out = __longlong_as_double((long long)be_bits); return true; }
+    return false;
+  }
+  switch (len) {
+    case 1: out = (double)(int8_t)(uint8_t)be_bits; return true;
+    case 2: out = (double)(int16_t)(uint16_t)be_bits; return true;
+    case 4: out = (double)(int32_t)(uint32_t)be_bits; return true;
+    case 8: out = (double)(long long)be_bits; return true;
+  }
+  return false;
+}
+
+// ---- slot of a datapoint ---------------------------------------------------
+struct RowGeom {
+  int64_t q0;   // slot index at the row base (when rel >= 0)
+  int64_t r0;   // remainder (or negative rel)
+};
+
+__device__ __forceinline__ RowGeom row_geom(const GridParams& p, uint32_t base) {
+  RowGeom g;
+  const int64_t rel = (int64_t)base * 1000 - p.B0;
+  if (rel >= 0) {
+    g.q0 = rel / p.I;
+    g.r0 = rel - g.q0 * p.I;
+  } else {
+    g.q0 = 0;
+    g.r0 = rel;
+  }
+  return g;
+}
+
+// slot of offset off_ms inside the row, -1 if before slot 0 or at/after K
+__device__ __forceinline__ int slot_of(const GridParams& p, const RowGeom& g, uint32_t base, uint32_t off_ms) {
+  if (p.mode == MODE_ALL) {
+    const int64_t ts = (int64_t)base * 1000 + off_ms;
+    return (ts >= p.qs && ts < p.qe) ? 0 : -1;
+  }
+  const int64_t n = g.r0 + (int64_t)off_ms;
+  if (n < 0) return -1;
+  int64_t q;
+  if (p.I < (1LL << 31)) {
+    // n < I + 3.6e6 < 2^32: float reciprocal estimate, corrected to the exact quotient
+    const uint32_t un = (uint32_t)n;
+    const uint32_t I32 = (uint32_t)p.I;
+    uint32_t qq = (uint32_t)((float)un * p.rcpI);
+    int64_t r = (int64_t)un - (int64_t)qq * I32;
+    if (r < 0) { qq--; r += I32; }
+    if (r >= (int64_t)I32) { qq++; r -= I32; }
+    if (r >= (int64_t)I32) { qq++; }
+    q = qq;
+  } else {
+    q = n / p.I;
+  }
+  const int64_t s = g.q0 + q;
+  return s < p.K ? (int)s : -1;
+}
+
+// ---- per-bucket downsample state (Aggregator.runDouble over a bucket, in order) ----
+struct BState {
+  double a, b;
+  long long n;
+};
+
+template <int F>
+__device__ __forceinline__ void bs_init(BState& s) {
+  s.b = 0.0;
+  s.n = 0;
+  if (F == F_MIN) s.a = INFINITY;
+  else if (F == F_MAX) s.a = -INFINITY;
+  else if (F == F_DIFF) { s.a = 0.0; s.n = -1; }
+  else s.a = 0.0;
+}
+
+// Aggregators.java: Sum :246-259, SquareSum :280-293, Min :315-327, Max :349-361, Avg :382-393,
+// StdDev :526-569, Diff :598-617, Count :636-645, Multiply :479-485, First :823-829, Last :845-851
+template <int F>
+__device__ __forceinline__ void bs_add(BState& s, double x) {
+  if (F == F_SUM || F == F_AVG) {
+    if (!isnan(x)) { s.a += x; s.n++; }
+  } else if (F == F_SQUARESUM) {
+    if (!isnan(x)) { s.a += x * x; s.n++; }
+  } else if (F == F_COUNT) {
+    if (!isnan(x)) s.n++;
+  } else if (F == F_MIN) {
+    if (!isnan(x) && x < s.a) s.a = x;
+  } else if (F == F_MAX) {
+    if (!isnan(x) && x > s.a) s.a = x;
+  } else if (F == F_DEV) {
+    if (!isnan(x)) {
+      if (s.n == 0) {
+        s.a = x;
+      } else {
+        const double old = s.a;
+        const double nm = old + (x - old) / (double)(s.n + 1);
+        s.b += (x - old) * (x - nm);
+        s.a = nm;
+      }
+      s.n++;
+    }
+  } else if (F == F_FIRST) {
+    if (s.n == 0) s.a = x;
+    s.n++;
+  } else if (F == F_LAST) {
+    s.a = x;
+    s.n++;
+  } else if (F == F_DIFF) {
+    if (s.n < 0) {
+      if (!isnan(x)) { s.a = x; s.n = 0; }
+    } else {
+      s.n++;
+    }
+    s.b = x;
+  } else if (F == F_MULT) {
+    s.a = (s.b != 0.0) ? s.a * x : x;   // b used as "has value" flag
+    s.b = 1.0;
+  }
+}
+
+template <int F>
+__device__ __forceinline__ double bs_final(const BState& s) {
+  if (F == F_SUM || F == F_SQUARESUM) return s.n == 0 ? (double)NAN : s.a;
+  if (F == F_AVG) return s.n == 0 ? (double)NAN : s.a / (double)(int)s.n;
+  if (F == F_COUNT) return (double)s.n;
+  if (F == F_MIN) return s.a == INFINITY ? (double)NAN : s.a;
+  if (F == F_MAX) return s.a == -INFINITY ? (double)NAN : s.a;
+  if (F == F_DEV) return s.n == 0 ? (double)NAN : (s.n == 1 ? 0.0 : sqrt(s.b / (double)s.n));
+  if (F == F_FIRST || F == F_LAST) return s.a;
+  if (F == F_DIFF) return s.n < 0 ? (double)NAN : (s.n == 0 ? 0.0 : s.b - s.a);
+  if (F == F_MULT) return s.a;
+  return NAN;
+}
+
+// ---- SpanGroup contributions into the tile's per-slot partial state ----------------
+struct LdsPart {
+  double* a;
+  double* b;
+  uint32_t* n;
+  uint32_t* f;
+};
+
+__device__ __forceinline__ void part_init(int ga, LdsPart& P, int k) {
+  P.a[k] = (ga == GA_MIN) ? INFINITY : (ga == GA_MAX ? -INFINITY : 0.0);
+  P.b[k] = 0.0;
+  P.n[k] = 0;
+  P.f[k] = 0;
+}
+
+// AggregationIterator feeding Aggregator.runDouble, one span at a time in index order.
+__device__ __forceinline__ void contribute(int ga, LdsPart& P, int s, double v, bool uni) {
+  uint32_t f = P.f[s];
+  switch (ga) {
+    case GA_SUM: case GA_AVG:
+      if (!isnan(v)) { P.a[s] += v; P.n[s]++; }
+      break;
+    case GA_SQUARESUM:
+      if (!isnan(v)) { P.a[s] += v * v; P.n[s]++; }
+      break;
+    case GA_COUNT:
+      if (!isnan(v)) P.n[s]++;
+      break;
+    case GA_MIN:
+      if (!isnan(v) && v < P.a[s]) P.a[s] = v;
+      break;
+    case GA_MAX:
+      if (!isnan(v) && v > P.a[s]) P.a[s] = v;
+      break;
+    case GA_DEV:
+      if (!isnan(v)) {
+        const uint32_t c = P.n[s];
+        if (c == 0) {
+          P.a[s] = v;
+        } else {
+          const double m = P.a[s];
+          const double nm = m + (v - m) / (double)(c + 1);
+          P.b[s] += (v - m) * (v - nm);
+          P.a[s] = nm;
+        }
+        P.n[s] = c + 1;
+      }
+      break;
+    case GA_FIRST: case GA_NONE:
+      if (!(f & PF_HAS)) { P.a[s] = v; f |= PF_HAS; }
+      f += 4;
+      break;
+    case GA_LAST:
+      P.a[s] = v;
+      f |= PF_HAS;
+      f += 4;
+      break;
+    case GA_DIFF:
+      if (!(f & PF_HAS)) {
+        if (!isnan(v)) { P.a[s] = v; f |= PF_HAS; P.n[s] = 0; }
+      } else {
+        P.n[s]++;
+      }
+      P.b[s] = v;
+      f += 4;
+      break;
+    case GA_MULT:
+      P.a[s] = (f & PF_HAS) ? P.a[s] * v : v;
+      f |= PF_HAS;
+      f += 4;
+      break;
+  }
+  if (uni) f |= PF_UNION;
+  P.f[s] = f;
+}
+
+// Interpolation of a missing slot (AggregationIterator.nextDoubleValue, :773-793)
+__device__ __forceinline__ double interp(int method, const GridParams& p, int k0, double y0, int k1, double y1, int k) {
+  switch (method) {
+    case TSDB_INTERP_LERP: {
+      const long long x = (long long)k * p.I, x0 = (long long)k0 * p.I, x1 = (long long)k1 * p.I;
+      return y0 + (double)(x - x0) * (y1 - y0) / (double)(x1 - x0);
+    }
+    case TSDB_INTERP_ZIM: return 0.0;
+    case TSDB_INTERP_MAX: return DBL_MAX;
+    case TSDB_INTERP_MIN: return 4.9e-324;
+    default: return y0;
+  }
+}
+
+// ---- k_index: classify every row ---------------------------------------------------
+__global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual, RowDesc* __restrict__ rows,
+                                               int64_t n_rows, int32_t* err) {
+  const int lane = lane_id();
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t r = wave; r < n_rows; r += nwaves) {
+    RowDesc d = rows[r];
+    const uint8_t* q = qual + d.qoff;
+    const uint32_t qlen = d.qlen;
+    // hypotheses: all 2-byte, all 4-byte
+    bool ok2 = (qlen % 2) == 0 && qlen > 0;
+    bool ok4 = (qlen % 4) == 0 && qlen > 0;
+    int lmin2 = 99, lmax2 = -1, lmin4 = 99, lmax4 = -1;
+    long long sum2 = 0, sum4 = 0;
+    bool bad2 = false, bad4 = false;
+    for (uint32_t p0 = (uint32_t)lane * 16; p0 < qlen; p0 += 64 * 16) {
+      const uint4 w = *reinterpret_cast<const uint4*>(q + p0);
+      uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int b = 0; b < 16; b += 2) {
+        if (p0 + b >= qlen) break;
+        const uint32_t b0 = (ws[b >> 2] >> ((b & 3) * 8)) & 0xFF;
+        const uint32_t b1 = (ws[(b + 1) >> 2] >> (((b + 1) & 3) * 8)) & 0xFF;
+        if ((b0 & 0xF0) == 0xF0) ok2 = false;
+        const int len = (b1 & 7) + 1;
+        const bool fl = (b1 & 8) != 0;
+        if (fl ? (len != 4 && len != 8) : (len == 3 || (len >= 5 && len <= 7))) bad2 = true;
+        lmin2 = min(lmin2, len);
+        lmax2 = max(lmax2, len);
+        sum2 += len;
+        if ((b & 3) == 0) {
+          if ((b0 & 0xF0) != 0xF0) ok4 = false;
+          const uint32_t b3 = (ws[(b + 3) >> 2] >> (((b + 3) & 3) * 8)) & 0xFF;
+          const int l4 = (b3 & 7) + 1;
+          const bool f4 = (b3 & 8) != 0;
+          if (f4 ? (l4 != 4 && l4 != 8) : (l4 == 3 || (l4 >= 5 && l4 <= 7))) bad4 = true;
+          lmin4 = min(lmin4, l4);
+          lmax4 = max(lmax4, l4);
+          sum4 += l4;
+        }
+      }
+    }
+    ok2 = __all(ok2);
+    ok4 = __all(ok4);
+    bad2 = __any(bad2);
+    bad4 = __any(bad4);
+    lmin2 = wave_min(lmin2); lmax2 = wave_max(lmax2);
+    lmin4 = wave_min(lmin4); lmax4 = wave_max(lmax4);
+    sum2 = wave_sum64(sum2);
+    sum4 = wave_sum64(sum4);
+    if (lane == 0) {
+      uint32_t flags = 0, ndp = 0;
+      long long vneed = 0;
+      bool bad = false;
+      if (ok2) {
+        ndp = qlen / 2; flags = 2; vneed = sum2; bad = bad2;
+        if (lmin2 == lmax2) flags |= (uint32_t)lmin2 << ROW_VL_SHIFT;
+      } else if (ok4) {
+        ndp = qlen / 4; flags = 4; vneed = sum4; bad = bad4;
+        if (lmin4 == lmax4) flags |= (uint32_t)lmin4 << ROW_VL_SHIFT;
+      } else {
+        // mixed second/millisecond qualifiers (meta bit MS_MIXED_COMPACT): sequential walk
+        uint32_t i = 0;
+        while (i < qlen) {
+          const uint32_t b0 = q[i];
+          const bool ms = (b0 & 0xF0) == 0xF0;
+          const uint32_t w = ms ? 4 : 2;
+          if (i + w > qlen) { bad = true; break; }
+          const uint32_t fb = q[i + w - 1];
+          const int len = (fb & 7) + 1;
+          const bool fl = (fb & 8) != 0;
+          if (fl ? (len != 4 && len != 8) : (len == 3 || (len >= 5 && len <= 7))) bad = true;
+          vneed += len;
+          ndp++;
+          i += w;
+        }
+        flags = 0;
+      }
+      if (qlen == 0 || vneed > (long long)d.vlen) bad = true;
+      if (bad) {
+        flags |= ROW_ERR;
+        set_err(err, TSDB_E_ILLEGAL_DATA);
+      }
+      d.ndp = ndp;
+      d.flags = flags;
+      rows[r] = d;
+    }
+  }
+}
+
+// ---- k_grid ---------------------------------------------------------------------
+struct WaveLds {
+  double* dpv;          // [CH] decoded values (aliases the vle byte staging buffer)
+  uint8_t* vbuf;
+  int32_t* seg_slot;    // [CH]
+  uint16_t* seg_start;  // [CH+1]
+  uint32_t* mq;         // [CH] mixed-row scratch: off_ms
+  uint32_t* mv;         // [CH] mixed-row scratch: value offset | len<<24 | float<<31
+  double* dense;        // [K] per-series bucket values
+  uint8_t* pres;        // [K] bucket present
+  double* rate;         // [K] rate values (rate mode)
+  LdsPart part;         // [K] tile partials
+};
+
+__host__ __device__ inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
+
+__host__ __device__ inline int64_t wave_lds_bytes(int64_t K, bool rate) {
+  int64_t o = 0;
+  o += VBUF;                 // dpv / vbuf
+  o += CH * 4;               // seg_slot
+  o += align16((CH + 1) * 2);// seg_start
+  o += CH * 4 * 2;           // mq, mv
+  o += align16(K * 8);       // dense
+  o += align16(K);           // pres
+  if (rate) o += align16(K * 8);
+  o += align16(K * 8) * 2 + align16(K * 4) * 2;  // part
+  return align16(o);
+}
+
+__device__ inline WaveLds carve(unsigned char* base, int64_t K, bool rate) {
+  WaveLds w;
+  int64_t o = 0;
+  w.dpv = (double*)(base + o);
+  w.vbuf = base + o;
+  o += VBUF;
+  w.seg_slot = (int32_t*)(base + o); o += CH * 4;
+  w.seg_start = (uint16_t*)(base + o); o += align16((CH + 1) * 2);
+  w.mq = (uint32_t*)(base + o); o += CH * 4;
+  w.mv = (uint32_t*)(base + o); o += CH * 4;
+  w.dense = (double*)(base + o); o += align16(K * 8);
+  w.pres = base + o; o += align16(K);
+  if (rate) { w.rate = (double*)(base + o); o += align16(K * 8); } else { w.rate = nullptr; }
+  w.part.a = (double*)(base + o); o += align16(K * 8);
+  w.part.b = (double*)(base + o); o += align16(K * 8);
+  w.part.n = (uint32_t*)(base + o); o += align16(K * 4);
+  w.part.f = (uint32_t*)(base + o); o += align16(K * 4);
+  return w;
+}
+
+// Decodes the lane's 8 datapoints of chunk [c0, c0+CH) of row d into (slot, value).
+// Returns false (and sets err) on malformed data.
+__device__ __forceinline__ void decode_chunk(const GridParams& p, const RowDesc& d, const RowGeom& g,
+                                             int64_t c0, const WaveLds& W, int64_t& vcur,
+                                             int slot[DPL], double val[DPL]) {
+  const int lane = lane_id();
+  const int64_t i0 = c0 + (int64_t)lane * DPL;
+  const int nv = (int)max((int64_t)0, min((int64_t)DPL, (int64_t)d.ndp - i0));
+  const int qw = d.flags & ROW_QW_MASK;
+  const int vl = (d.flags & ROW_VL_MASK) >> ROW_VL_SHIFT;
+  const uint8_t* q = p.qual + d.qoff;
+  const uint8_t* v = p.val + d.voff;
+  uint32_t off[DPL];
+  uint32_t fl[DPL];
+#pragma unroll
+  for (int j = 0; j < DPL; j++) { off[j] = 0; fl[j] = 0; slot[j] = -1; val[j] = 0.0; }
+
+  if (qw == 2) {
+    if (nv > 0) {
+      const uint4 w = *reinterpret_cast<const uint4*>(q + i0 * 2);
+      const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int j = 0; j < DPL; j++) {
+        const uint32_t be = __builtin_bswap32(ws[j >> 1]);
+        const uint32_t qq = (j & 1) ? (be & 0xFFFF) : (be >> 16);
+        off[j] = (qq >> 4) * 1000u;
+        fl[j] = qq & 0xF;
+      }
+    }
+  } else if (qw == 4) {
+    if (nv > 0) {
+      const uint4 w0 = *reinterpret_cast<const uint4*>(q + i0 * 4);
+      const uint4 w1 = *reinterpret_cast<const uint4*>(q + i0 * 4 + 16);
+      const uint32_t ws[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int j = 0; j < DPL; j++) {
+        const uint32_t qq = __builtin_bswap32(ws[j]);
+        off[j] = (qq & 0x0FFFFFC0u) >> 6;
+        fl[j] = qq & 0xF;
+      }
+    }
+  } else {
+    // mixed s/ms row: lane 0 walks the chunk sequentially (RowSeq.Iterator.next, :552-568)
+    // positions carried in vcur (low 32: qualifier byte index, high 32: value byte index)
+    if (lane == 0) {
+      uint32_t qi = (uint32_t)(vcur & 0xFFFFFFFF), vi = (uint32_t)(vcur >> 32);
+      for (int t = 0; t < CH && c0 + t < (int64_t)d.ndp; t++) {
+        const bool ms = (q[qi] & 0xF0) == 0xF0;
+        uint32_t qq;
+        if (ms) { qq = ((uint32_t)q[qi] << 24) | ((uint32_t)q[qi + 1] << 16) | ((uint32_t)q[qi + 2] << 8) | q[qi + 3]; qi += 4; }
+        else { qq = ((uint32_t)q[qi] << 8) | q[qi + 1]; qi += 2; }
+        const uint32_t f = qq & 0xF;
+        const uint32_t len = (f & 7) + 1;
+        W.mq[t] = ms ? ((qq & 0x0FFFFFC0u) >> 6) : ((qq >> 4) & 0xFFF) * 1000u;
+        W.mv[t] = vi | (len << 24) | ((f & 8) ? 0x80000000u : 0u);
+        vi += len;
+      }
+      vcur = ((int64_t)vi << 32) | qi;
+    }
+    vcur = __shfl(vcur, 0, 64);
+    WAVE_SYNC();
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      if (j < nv) {
+        const int t = lane * DPL + j;
+        off[j] = W.mq[t];
+        const uint32_t mvv = W.mv[t];
+        const uint32_t vo = mvv & 0xFFFFFF;
+        const int len = (mvv >> 24) & 0x7F;
+        uint64_t bits = 0;
+        for (int b = 0; b < len; b++) bits = (bits << 8) | v[vo + b];
+        double x;
+        if (!decode_value(bits, len, (mvv >> 31) != 0, x)) set_err(p.err, TSDB_E_ILLEGAL_DATA);
+        val[j] = x;
+        slot[j] = slot_of(p, g, d.base, off[j]);
+      }
+    }
+    WAVE_SYNC();
+    return;
+  }
+
+  if (vl != 0) {
+    // uniform value length: direct coalesced loads
+    if (nv > 0) {
+      if (vl == 4) {
+        const uint4 w0 = *reinterpret_cast<const uint4*>(v + i0 * 4);
+        const uint4 w1 = *reinterpret_cast<const uint4*>(v + i0 * 4 + 16);
+        const uint32_t ws[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+        for (int j = 0; j < DPL; j++) {
+          const uint32_t be = __builtin_bswap32(ws[j]);
+          val[j] = (fl[j] & 8) ? (double)__uint_as_float(be) : (double)(int32_t)be;
+        }
+      } else if (vl == 8) {
+        const uint4* pv = reinterpret_cast<const uint4*>(v + i0 * 8);
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+          const uint4 w = pv[h];
+          const uint64_t a = ((uint64_t)__builtin_bswap32(w.x) << 32) | __builtin_bswap32(w.y);
+          const uint64_t b = ((uint64_t)__builtin_bswap32(w.z) << 32) | __builtin_bswap32(w.w);
+          val[2 * h] = (fl[2 * h] & 8) ? __longlong_as_double((long long)a) : (double)(long long)a;
+          val[2 * h + 1] = (fl[2 * h + 1] & 8) ? __longlong_as_double((long long)b) : (double)(long long)b;
+        }
+      } else if (vl == 2) {
+        const uint4 w = *reinterpret_cast<const uint4*>(v + i0 * 2);
+        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int j = 0; j < DPL; j++) {
+          const uint32_t be = __builtin_bswap32(ws[j >> 1]);
+          const uint32_t x = (j & 1) ? (be & 0xFFFF) : (be >> 16);
+          val[j] = (double)(int16_t)(uint16_t)x;
+        }
+      } else {  // vl == 1
+        const uint2 w = *reinterpret_cast<const uint2*>(v + i0);
+        const uint32_t ws[2] = {w.x, w.y};
+#pragma unroll
+        for (int j = 0; j < DPL; j++) val[j] = (double)(int8_t)((ws[j >> 2] >> ((j & 3) * 8)) & 0xFF);
+      }
+    }
+  } else {
+    // variable-length values (vle ints): wave prefix scan of lengths, stage bytes in LDS
+    int len[DPL];
+    int loc = 0;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      len[j] = (j < nv) ? (int)(fl[j] & 7) + 1 : 0;
+      loc += len[j];
+    }
+    const int incl = wave_incl_sum(loc);
+    const int total = __shfl(incl, 63, 64);
+    const int excl = incl - loc;
+    const int64_t start = (int64_t)d.voff + vcur;           // absolute byte offset in blob
+    const int64_t a0 = start & ~(int64_t)15;
+    const int64_t lead = start - a0;
+    const int npieces = (int)((lead + total + 15) >> 4);
+    WAVE_SYNC();
+    for (int pc = lane; pc < npieces; pc += 64)
+      reinterpret_cast<uint4*>(W.vbuf)[pc] = *reinterpret_cast<const uint4*>(p.val + a0 + pc * 16);
+    WAVE_SYNC();
+    int o = (int)lead + excl;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      if (j < nv) {
+        uint64_t bits = 0;
+        for (int b = 0; b < len[j]; b++) bits = (bits << 8) | W.vbuf[o + b];
+        double x;
+        if (!decode_value(bits, len[j], (fl[j] & 8) != 0, x)) set_err(p.err, TSDB_E_ILLEGAL_DATA);
+        val[j] = x;
+      }
+      o += len[j];
+    }
+    vcur += total;
+    WAVE_SYNC();
+  }
+#pragma unroll
+  for (int j = 0; j < DPL; j++)
+    if (j < nv) slot[j] = slot_of(p, g, d.base, off[j]);
+}
+
+template <int F>
+__global__ __launch_bounds__(256) void k_grid(GridParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = lane_id();
+  const int wave = threadIdx.x >> 6;
+  const int64_t tile = (int64_t)blockIdx.x * p.waves + wave;
+  if (tile >= p.n_tiles) return;
+  const int K = (int)p.K;
+  WaveLds W = carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0);
+  const int ga = p.ga;
+
+  for (int k = lane; k < K; k += 64) part_init(ga, W.part, k);
+
+  const int64_t sb = p.tile_begin[tile], se_ = p.tile_end[tile];
+  bool tile_active = false;
+  const double fillv = (p.fill == TSDB_FILL_ZERO) ? 0.0 : (double)NAN;
+
+  for (int64_t s = sb; s < se_; s++) {
+    for (int k = lane; k < K; k += 64) W.pres[k] = 0;
+    WAVE_SYNC();
+    bool any_row = false;
+    int carry_slot = -1;
+    BState carry;
+    bs_init<F>(carry);
+    const int64_t r0 = p.series_row_ptr[s], r1 = p.series_row_ptr[s + 1];
+    for (int64_t r = r0; r < r1; r++) {
+      const RowDesc d = p.rows[r];
+      if ((int64_t)d.base < p.ss) continue;
+      if ((int64_t)d.base >= p.se) break;
+      any_row = true;
+      if (d.flags & ROW_ERR) { if (lane == 0) set_err(p.err, TSDB_E_ILLEGAL_DATA); continue; }
+      const RowGeom g = row_geom(p, d.base);
+      int64_t vcur = 0;
+      for (int64_t c0 = 0; c0 < (int64_t)d.ndp; c0 += CH) {
+        int slot[DPL];
+        double val[DPL];
+        decode_chunk(p, d, g, c0, W, vcur, slot, val);
+        // stage decoded values
+        WAVE_SYNC();
+#pragma unroll
+        for (int j = 0; j < DPL; j++) W.dpv[lane * DPL + j] = val[j];
+        // segment heads
+        const int prev_last = __shfl_up(slot[DPL - 1], 1, 64);
+        int h = 0;
+        bool head[DPL];
+#pragma unroll
+        for (int j = 0; j < DPL; j++) {
+          const int ps = (j == 0) ? (lane == 0 ? -2 : prev_last) : slot[j - 1];
+          head[j] = slot[j] >= 0 && (ps < 0 || ps != slot[j]);
+          h += head[j];
+        }
+        int vend = 0;
+#pragma unroll
+        for (int j = 0; j < DPL; j++) if (slot[j] >= 0) vend = lane * DPL + j + 1;
+        vend = wave_max(vend);
+        const int hincl = wave_incl_sum(h);
+        const int nseg = __shfl(hincl, 63, 64);
+        int pos = hincl - h;
+#pragma unroll
+        for (int j = 0; j < DPL; j++) {
+          if (head[j]) {
+            W.seg_start[pos] = (uint16_t)(lane * DPL + j);
+            W.seg_slot[pos] = slot[j];
+            pos++;
+          }
+        }
+        if (lane == 0) W.seg_start[nseg] = (uint16_t)vend;
+        WAVE_SYNC();
+        if (nseg == 0) continue;
+        // the open bucket of the previous chunk ends unless this chunk continues it
+        const int first_slot = W.seg_slot[0];
+        if (carry_slot >= 0 && first_slot != carry_slot) {
+          if (lane == 0) { W.dense[carry_slot] = bs_final<F>(carry); W.pres[carry_slot] = 1; }
+          carry_slot = -1;
+          bs_init<F>(carry);
+        }
+        for (int b0 = 0; b0 < nseg; b0 += 64) {
+          const int si = b0 + lane;
+          const bool act = si < nseg;
+          BState st;
+          bs_init<F>(st);
+          int myslot = -1;
+          if (act) {
+            myslot = W.seg_slot[si];
+            if (si == 0 && myslot == carry_slot) st = carry;
+            const int e = W.seg_start[si + 1];
+            for (int i = W.seg_start[si]; i < e; i++) bs_add<F>(st, W.dpv[i]);
+            if (si != nseg - 1) { W.dense[myslot] = bs_final<F>(st); W.pres[myslot] = 1; }
+          }
+          if (b0 + 64 >= nseg) {  // last round: the last segment stays open (carry)
+            const int src = (nseg - 1) & 63;
+            carry.a = __shfl(st.a, src, 64);
+            carry.b = __shfl(st.b, src, 64);
+            carry.n = __shfl(st.n, src, 64);
+            carry_slot = __shfl(myslot, src, 64);
+          }
+        }
+        WAVE_SYNC();
+      }
+    }
+    if (!any_row) continue;
+    tile_active = true;
+    if (carry_slot >= 0 && lane == 0) { W.dense[carry_slot] = bs_final<F>(carry); W.pres[carry_slot] = 1; }
+    WAVE_SYNC();
+
+    // ---- series -> SpanGroup contributions over the K slots -----------------
+    if (!p.rate) {
+      if (p.fill != TSDB_FILL_NONE && p.mode == MODE_GRID) {
+        // FillingDownsampler (:172-301): every slot, missing -> NaN / 0 / RuntimeException
+        for (int k = lane; k < K; k += 64) {
+          const bool pr = W.pres[k] != 0;
+          if (!pr && p.fill == TSDB_FILL_SCALAR) set_err(p.err, TSDB_E_RUNTIME);
+          contribute(ga, W.part, k, pr ? W.dense[k] : fillv, true);
+        }
+      } else {
+        int prev_present = -1;
+        for (int kb = 0; kb < K; kb += 64) {
+          const int k = kb + lane;
+          const bool pr = k < K && W.pres[k] != 0;
+          const int incl = wave_incl_max(pr ? k : -1);
+          int pp = __shfl_up(incl, 1, 64);
+          if (lane == 0) pp = -1;
+          pp = max(pp, prev_present);
+          if (pr) {
+            const double v = W.dense[k];
+            if (pp >= 0 && pp < k - 1) {
+              const double y0 = W.dense[pp];
+              for (int s2 = pp + 1; s2 < k; s2++) contribute(ga, W.part, s2, interp(p.interp, p, pp, y0, k, v, s2), false);
+            }
+            contribute(ga, W.part, k, v, true);
+          }
+          prev_present = max(prev_present, __shfl(incl, 63, 64));
+        }
+      }
+    } else {
+      // RateSpan over the bucket stream (:121-180), aggregated with PREV semantics
+      // (AggregationIterator ctor rate branch :448-459, nextDoubleValue :744-753)
+      int prev_item = -1, last_surv = -1;
+      long long nsurv = 0;
+      const bool dense_stream = p.fill != TSDB_FILL_NONE && p.mode == MODE_GRID;
+      for (int kb = 0; kb < K; kb += 64) {
+        const int k = kb + lane;
+        const bool inK = k < K;
+        const bool pr = inK && W.pres[k] != 0;
+        const bool item = inK && (dense_stream || pr);
+        if (item && !pr && p.fill == TSDB_FILL_SCALAR) set_err(p.err, TSDB_E_RUNTIME);
+        const int iincl = wave_incl_max(item ? k : -1);
+        int pi = __shfl_up(iincl, 1, 64);
+        if (lane == 0) pi = -1;
+        pi = max(pi, prev_item);
+        bool sv = false;
+        double r = 0.0;
+        if (item) {
+          const double v1 = pr ? W.dense[k] : fillv;
+          double v0 = 0.0;
+          long long t0 = 0;
+          if (pi >= 0) { v0 = W.pres[pi] ? W.dense[pi] : fillv; t0 = p.B0 + (long long)pi * p.I; }
+          const long long t1 = (p.mode == MODE_ALL) ? p.qs : p.B0 + (long long)k * p.I;
+          if (t1 <= t0) set_err(p.err, TSDB_E_ILLEGAL_STATE);
+          const double dt = (double)(t1 - t0) / 1000.0;
+          double diff = v1 - v0;
+          sv = true;
+          if (p.counter && diff < 0) {
+            if (p.drop) {
+              sv = false;
+            } else {
+              diff = (double)p.counter_max - v0 + v1;
+              r = diff / dt;
+              if (p.reset_value > 0 && r > (double)p.reset_value) r = 0.0;
+            }
+          } else {
+            r = diff / dt;
+          }
+          if (sv) W.rate[k] = r;
+        }
+        WAVE_SYNC();
+        const int cincl = wave_incl_sum(sv ? 1 : 0);
+        const long long m = nsurv + (cincl - (sv ? 1 : 0));
+        const int sincl = wave_incl_max(sv ? k : -1);
+        int ps = __shfl_up(sincl, 1, 64);
+        if (lane == 0) ps = -1;
+        ps = max(ps, last_surv);
+        if (sv) {
+          if (m == 1) {
+            const double r0 = W.rate[ps];
+            for (int s2 = 0; s2 < k; s2++) contribute(ga, W.part, s2, r0, false);
+            contribute(ga, W.part, k, r, true);
+          } else if (m >= 2) {
+            const double rp = W.rate[ps];
+            for (int s2 = ps + 1; s2 < k; s2++) contribute(ga, W.part, s2, rp, false);
+            contribute(ga, W.part, k, r, true);
+          }
+        }
+        prev_item = max(prev_item, __shfl(iincl, 63, 64));
+        last_surv = max(last_surv, __shfl(sincl, 63, 64));
+        nsurv += __shfl(cincl, 63, 64);
+        WAVE_SYNC();
+      }
+    }
+    WAVE_SYNC();
+  }
+
+  if (tile_active && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
+  WAVE_SYNC();
+  double* ga_ = p.part.a + tile * K;
+  double* gb_ = p.part.b + tile * K;
+  uint32_t* gn_ = p.part.n + tile * K;
+  uint32_t* gf_ = p.part.f + tile * K;
+  for (int k = lane; k < K; k += 64) {
+    ga_[k] = W.part.a[k];
+    gb_[k] = W.part.b[k];
+    gn_[k] = W.part.n[k];
+    gf_[k] = W.part.f[k];
+  }
+}
+
+// ---- k_reduce -------------------------------------------------------------------
+struct PState {
+  double a, b;
+  uint32_t n, f;
+};
+
+__device__ __forceinline__ PState ps_identity(int ga) {
+  PState s;
+  s.a = (ga == GA_MIN) ? INFINITY : (ga == GA_MAX ? -INFINITY : 0.0);
+  s.b = 0.0;
+  s.n = 0;
+  s.f = 0;
+  return s;
+}
+
+// merge B (later series) into A (earlier series)
+__device__ __forceinline__ PState ps_merge(int ga, PState A, const PState& B) {
+  const uint32_t uni = (A.f | B.f) & PF_UNION;
+  switch (ga) {
+    case GA_SUM: case GA_AVG: case GA_SQUARESUM:
+      A.a += B.a; A.n += B.n; break;
+    case GA_COUNT:
+      A.n += B.n; break;
+    case GA_MIN:
+      if (B.a < A.a) A.a = B.a;
+      break;
+    case GA_MAX:
+      if (B.a > A.a) A.a = B.a;
+      break;
+    case GA_DEV:
+      if (B.n == 0) break;
+      if (A.n == 0) { A.a = B.a; A.b = B.b; A.n = B.n; break; }
+      {
+        const double na = A.n, nb = B.n, n = na + nb;
+        const double delta = B.a - A.a;
+        A.a = A.a + delta * nb / n;
+        A.b = A.b + B.b + delta * delta * na * nb / n;
+        A.n = A.n + B.n;
+      }
+      break;
+    case GA_FIRST: case GA_NONE:
+      if (!(A.f & PF_HAS) && (B.f & PF_HAS)) { A.a = B.a; }
+      A.f = (A.f & 3u) | (B.f & PF_HAS) | ((((A.f >> 2) + (B.f >> 2))) << 2);
+      break;
+    case GA_LAST:
+      if (B.f & PF_HAS) A.a = B.a;
+      A.f = (A.f & 3u) | (B.f & PF_HAS) | ((((A.f >> 2) + (B.f >> 2))) << 2);
+      break;
+    case GA_DIFF: {
+      const uint32_t totb = B.f >> 2;
+      if (A.f & PF_HAS) { A.n += totb; }
+      else if (B.f & PF_HAS) { A.a = B.a; A.n = B.n; }
+      if (totb > 0) A.b = B.b;
+      A.f = (A.f & 3u) | (B.f & PF_HAS) | ((((A.f >> 2) + totb)) << 2);
+      break;
+    }
+    case GA_MULT:
+      if (B.f & PF_HAS) A.a = (A.f & PF_HAS) ? A.a * B.a : B.a;
+      A.f = (A.f & 3u) | (B.f & PF_HAS) | ((((A.f >> 2) + (B.f >> 2))) << 2);
+      break;
+  }
+  A.f = (A.f & ~PF_UNION) | uni;
+  return A;
+}
+
+// Aggregator.runDouble results (see bs_final) + AggregationIterator.doubleValue's Inf check
+__device__ __forceinline__ double ps_final(int ga, const PState& s, int32_t* err) {
+  double r;
+  switch (ga) {
+    case GA_SUM: case GA_SQUARESUM: r = s.n == 0 ? (double)NAN : s.a; break;
+    case GA_AVG: r = s.n == 0 ? (double)NAN : s.a / (double)(int)s.n; break;
+    case GA_COUNT: r = (double)s.n; break;
+    case GA_MIN: r = s.a == INFINITY ? (double)NAN : s.a; break;
+    case GA_MAX: r = s.a == -INFINITY ? (double)NAN : s.a; break;
+    case GA_DEV: r = s.n == 0 ? (double)NAN : (s.n == 1 ? 0.0 : sqrt(s.b / (double)s.n)); break;
+    case GA_FIRST: case GA_LAST: case GA_MULT: r = s.a; break;
+    case GA_NONE:
+      if ((s.f >> 2) > 1) set_err(err, TSDB_E_ILLEGAL_DATA);
+      r = s.a;
+      break;
+    case GA_DIFF: r = !(s.f & PF_HAS) ? (double)NAN : (s.n == 0 ? 0.0 : s.b - s.a); break;
+    default: r = NAN;
+  }
+  if (isinf(r)) set_err(err, TSDB_E_ILLEGAL_STATE);
+  return r;
+}
+
+__global__ __launch_bounds__(256) void k_reduce(ReduceParams p) {
+  __shared__ PState sh[4][64];
+  const int lane = lane_id();
+  const int wave = threadIdx.x >> 6;
+  const int64_t g = blockIdx.x;
+  const int64_t k = (int64_t)blockIdx.y * 64 + lane;
+  const int64_t t0 = p.group_tile_ptr[g], t1 = p.group_tile_ptr[g + 1];
+  const int64_t n = t1 - t0;
+  const int64_t a = t0 + n * wave / 4, b = t0 + n * (wave + 1) / 4;
+  PState S = ps_identity(p.ga);
+  if (k < p.K) {
+    for (int64_t t = a; t < b; t++) {
+      PState X;
+      const int64_t idx = t * p.K + k;
+      X.a = p.part.a[idx];
+      X.b = p.part.b[idx];
+      X.n = p.part.n[idx];
+      X.f = p.part.f[idx];
+      S = ps_merge(p.ga, S, X);
+    }
+  }
+  sh[wave][lane] = S;
+  __syncthreads();
+  if (wave == 0 && k < p.K) {
+    PState T = sh[0][lane];
+    for (int w = 1; w < 4; w++) T = ps_merge(p.ga, T, sh[w][lane]);
+    const bool emit = (T.f & PF_UNION) != 0;
+    const double r = emit ? ps_final(p.ga, T, p.err) : 0.0;
+    p.out_val[g * p.K + k] = r;
+    p.out_flag[g * p.K + k] = emit ? 1 : 0;
+  }
+}
+
+// ---- synthetic MockBase-equivalent store, generated in HBM -------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9e3779b97f4a7c15ULL;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ void synth_series(const SynthParams& p, int64_t pos, int64_t& gsid, int32_t& grp) {
+  // batch position -> (group, global series id): series i belongs to group i % G
+  int64_t lo = 0, hi = p.n_groups;
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (p.grp_off[mid] <= pos) lo = mid; else hi = mid;
+  }
+  grp = (int32_t)lo;
+  gsid = lo + (pos - p.grp_off[lo]) * p.n_groups;
+}
+
+// value of point k of global series i: (is_int, long, float)
+__device__ __forceinline__ void synth_value(const SynthParams& p, int64_t i, int64_t k, bool& is_int, int64_t& lv,
+                                            float& fv) {
+  const uint64_t u = splitmix64(p.seed ^ ((uint64_t)i << 32) ^ (uint64_t)k);
+  is_int = p.value_kind == 1 || (p.value_kind == 2 && (i % 2) == 0);
+  if (is_int) {
+    lv = (int64_t)(u % (uint64_t)p.int_mod);
+  } else {
+    const double d = (double)(u >> 11) * (1.0 / 9007199254740992.0);
+    fv = (float)(50.0 + 10.0 * (d - 0.5));
+  }
+}
+
+__device__ __forceinline__ int vle_len(int64_t v) {
+  if (v >= -128 && v <= 127) return 1;
+  if (v >= -32768 && v <= 32767) return 2;
+  if (v >= -2147483648LL && v <= 2147483647LL) return 4;
+  return 8;
+}
+
+// pass 1: value bytes per row (wave per row)
+__global__ __launch_bounds__(256) void k_synth_sizes(SynthParams p) {
+  const int lane = lane_id();
+  const int64_t R = p.n_rows_per_series;
+  const int64_t nr = p.n_series * R;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t row = wave; row < nr; row += nwaves) {
+    const int64_t pos = row / R, h = row % R;
+    int64_t i;
+    int32_t grp;
+    synth_series(p, pos, i, grp);
+    const int64_t k0 = p.row_k0[h];
+    const int n = p.row_n[h];
+    long long bytes = 0;
+    for (int t = lane; t < n; t += 64) {
+      bool isi; int64_t lv; float fv;
+      synth_value(p, i, k0 + t, isi, lv, fv);
+      bytes += isi ? vle_len(lv) : 4;
+    }
+    bytes = wave_sum64(bytes);
+    if (lane == 0) p.row_vbytes[row] = (uint32_t)(bytes + (n > 1 ? 1 : 0));
+  }
+}
+
+// pass 2: write qualifiers, values, meta byte and the row index (wave per row)
+__global__ __launch_bounds__(256) void k_synth_write(SynthParams p) {
+  const int lane = lane_id();
+  const int64_t R = p.n_rows_per_series;
+  const int64_t nr = p.n_series * R;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t row = wave; row < nr; row += nwaves) {
+    const int64_t pos = row / R, h = row % R;
+    int64_t i;
+    int32_t grp;
+    synth_series(p, pos, i, grp);
+    if (h == 0 && lane == 0) p.group_id[pos] = grp;
+    RowDesc d = p.rows[row];   // qoff / voff / qlen / vlen set by the host
+    const int64_t k0 = p.row_k0[h];
+    const int n = p.row_n[h];
+    uint8_t* q = p.qual + d.qoff;
+    uint8_t* v = p.val + d.voff;
+    const int64_t base_ms = (int64_t)p.row_base[h] * 1000;
+    int64_t vo_carry = 0;
+    for (int t0 = 0; t0 < n; t0 += 64) {
+      const int t = t0 + lane;
+      bool isi = false; int64_t lv = 0; float fv = 0.f;
+      int len = 0;
+      if (t < n) {
+        synth_value(p, i, k0 + t, isi, lv, fv);
+        len = isi ? vle_len(lv) : 4;
+      }
+      const int incl = wave_incl_sum(len);
+      const int64_t vo = vo_carry + incl - len;
+      vo_carry += __shfl(incl, 63, 64);
+      if (t < n) {
+        const int64_t ts = p.start_ms + (k0 + t) * p.period_ms;
+        const int64_t off = ts - base_ms;
+        const uint32_t flags = isi ? (uint32_t)(len - 1) : 0xBu;
+        if (p.ms_qual) {
+          const uint32_t qq = 0xF0000000u | ((uint32_t)off << 6) | flags;
+          q[t * 4 + 0] = qq >> 24; q[t * 4 + 1] = (qq >> 16) & 0xFF; q[t * 4 + 2] = (qq >> 8) & 0xFF; q[t * 4 + 3] = qq & 0xFF;
+        } else {
+          const uint32_t qq = ((uint32_t)(off / 1000) << 4) | flags;
+          q[t * 2 + 0] = (qq >> 8) & 0xFF; q[t * 2 + 1] = qq & 0xFF;
+        }
+        uint64_t be;
+        if (isi) be = (uint64_t)lv; else be = __float_as_uint(fv);
+        for (int b = 0; b < len; b++) v[vo + b] = (uint8_t)(be >> (8 * (len - 1 - b)));
+      }
+    }
+    if (lane == 0 && n > 1) v[vo_carry] = 0;   // CompactionQueue meta byte (no s/ms mix)
+  }
+}
+
+// ---- launchers -------------------------------------------------------------------
+hipError_t launch_index(const uint8_t* qual, const uint8_t*, RowDesc* rows, int64_t n_rows, int32_t* err,
+                        hipStream_t s) {
+  if (n_rows == 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((n_rows + 3) / 4, 65536);
+  hipLaunchKernelGGL(k_index, dim3((unsigned)blocks), dim3(256), 0, s, qual, rows, n_rows, err);
+  return hipGetLastError();
+}
+
+template <int F>
+static hipError_t launch_grid_t(const GridParams& p, hipStream_t s) {
+  const int64_t blocks = (p.n_tiles + p.waves - 1) / p.waves;
+  const size_t lds = (size_t)p.wave_lds * p.waves;
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_grid<F>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_grid<F>, dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_grid(const GridParams& p, int f, hipStream_t s) {
+  if (p.n_tiles == 0) return hipSuccess;
+  switch (f) {
+    case F_SUM: return launch_grid_t<F_SUM>(p, s);
+    case F_AVG: return launch_grid_t<F_AVG>(p, s);
+    case F_COUNT: return launch_grid_t<F_COUNT>(p, s);
+    case F_SQUARESUM: return launch_grid_t<F_SQUARESUM>(p, s);
+    case F_MIN: return launch_grid_t<F_MIN>(p, s);
+    case F_MAX: return launch_grid_t<F_MAX>(p, s);
+    case F_DEV: return launch_grid_t<F_DEV>(p, s);
+    case F_FIRST: return launch_grid_t<F_FIRST>(p, s);
+    case F_LAST: return launch_grid_t<F_LAST>(p, s);
+    case F_DIFF: return launch_grid_t<F_DIFF>(p, s);
+    case F_MULT: return launch_grid_t<F_MULT>(p, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_reduce(const ReduceParams& p, hipStream_t s) {
+  if (p.G == 0 || p.K == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_reduce, dim3((unsigned)p.G, (unsigned)((p.K + 63) / 64)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth_sizes(const SynthParams& p, hipStream_t s) {
+  const int64_t nr = p.n_series * p.n_rows_per_series;
+  const int64_t blocks = std::min<int64_t>((nr + 3) / 4, 1 << 16);
+  hipLaunchKernelGGL(k_synth_sizes, dim3((unsigned)blocks), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth_write(const SynthParams& p, hipStream_t s) {
+  const int64_t nr = p.n_series * p.n_rows_per_series;
+  const int64_t blocks = std::min<int64_t>((nr + 3) / 4, 1 << 16);
+  hipLaunchKernelGGL(k_synth_write, dim3((unsigned)blocks), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace tsdb
