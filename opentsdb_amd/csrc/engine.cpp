@@ -110,13 +110,6 @@ struct DevBuf {
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-int64_t wave_lds_bytes_host(int64_t K, bool rate) {
-  const int64_t CH = 512, VBUF = 4224;
-  int64_t o = VBUF + CH * 4 + align16((CH + 1) * 2) + CH * 8 + align16(K * 8) + align16(K);
-  if (rate) o += align16(K * 8);
-  o += align16(K * 8) * 2 + align16(K * 4) * 2;
-  return align16(o);
-}
 
 }  // namespace
 
@@ -143,7 +136,7 @@ struct tsdbhip_ctx {
   bool none_tiles_ready = false;
   DevBuf n_tb, n_te, n_tg, n_gtp;
   // scratch
-  DevBuf pa, pb, pn, pf, out_val, out_flag, gact, err;
+  DevBuf pa, pb, pn, pf, out_val, out_flag, gact, err, g_dense, g_pres, g_rate;
   tsdbhip_timing timing{};
 };
 
@@ -293,7 +286,7 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   release_batch(c);
-  for (DevBuf* b : {&c->pa, &c->pb, &c->pn, &c->pf, &c->out_val, &c->out_flag, &c->gact, &c->err}) b->release();
+  for (DevBuf* b : {&c->pa, &c->pb, &c->pn, &c->pf, &c->out_val, &c->out_flag, &c->gact, &c->err, &c->g_dense, &c->g_pres, &c->g_rate}) b->release();
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -627,6 +620,7 @@ struct Plan {
   int mode = MODE_GRID;
   int64_t ss = 0, se = 0, B0 = 0, I = 1, K = 0;
   bool none = false;
+  bool gslot = false;
 };
 
 int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
@@ -664,9 +658,8 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
       P.K = E0 > P.B0 ? (E0 - P.B0 + I - 1) / I : 0;
     }
   }
-  const int64_t need = wave_lds_bytes_host(P.K, q->rate != 0);
-  if (need > 160 * 1024)
-    return fail(TSDB_E_NOT_IMPLEMENTED, "too many downsample buckets in the query window for one wave (" + std::to_string(P.K) + ")");
+  // slot arrays live in LDS when they fit next to 4 waves' worth of staging, else in HBM
+  P.gslot = grid_wave_lds(P.K, q->rate != 0, false) > 40 * 1024;
   return 0;
 }
 
@@ -710,8 +703,16 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   gp.drop = q->rate_drop_resets;
   gp.counter_max = q->rate_counter_max;
   gp.reset_value = q->rate_reset_value;
-  gp.wave_lds = (int32_t)wave_lds_bytes_host(K, q->rate != 0);
+  gp.wave_lds = (int32_t)grid_wave_lds(K, q->rate != 0, P.gslot);
   int waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / gp.wave_lds));
+  if (P.gslot) {
+    HIP_OK(c->g_dense.ensure(std::max<int64_t>(1, nt * K) * 8));
+    HIP_OK(c->g_pres.ensure(std::max<int64_t>(1, nt * K)));
+    if (q->rate) HIP_OK(c->g_rate.ensure(std::max<int64_t>(1, nt * K) * 8));
+    gp.g_dense = c->g_dense.as<double>();
+    gp.g_pres = c->g_pres.as<uint8_t>();
+    gp.g_rate = q->rate ? c->g_rate.as<double>() : nullptr;
+  }
   gp.waves = waves;
   gp.part = Partials{c->pa.as<double>(), c->pb.as<double>(), c->pn.as<uint32_t>(), c->pf.as<uint32_t>()};
   gp.group_active = c->gact.as<uint32_t>();

@@ -15,8 +15,11 @@ struct RowDesc {
   uint32_t qlen;    // qualifier bytes
   uint32_t vlen;    // value bytes
   uint32_t flags;   // ROW_* below
-  uint32_t pad;
+  int32_t lsb;      // exactness certificate: min exponent of the least significant set bit
+                    // over the row's non-zero finite values (INT32_MAX if none)
+  double absmax;    // max |value| over the row (inf if any +-inf)
 };
+static_assert(sizeof(RowDesc) == 48, "RowDesc layout");
 
 // RowDesc.flags
 enum : uint32_t {
@@ -76,6 +79,10 @@ struct GridParams {
   int64_t counter_max, reset_value;
   int32_t wave_lds;      // bytes of LDS per wave
   int32_t waves;         // waves per workgroup
+  // slot arrays in global memory (large K): [tile][K]
+  double* g_dense;
+  uint8_t* g_pres;
+  double* g_rate;
   // outputs
   Partials part;
   uint32_t* group_active;
@@ -115,6 +122,7 @@ hipError_t launch_index(const uint8_t* qual, const uint8_t* val, RowDesc* rows, 
                         hipStream_t s);
 hipError_t launch_grid(const GridParams& p, int ds_function_class, hipStream_t s);
 hipError_t launch_reduce(const ReduceParams& p, hipStream_t s);
+int64_t grid_wave_lds(int64_t K, bool rate, bool gslot);
 hipError_t launch_synth_sizes(const SynthParams& p, hipStream_t s);
 hipError_t launch_synth_write(const SynthParams& p, hipStream_t s);
 

@@ -218,7 +218,7 @@ struct LdsPart {
   uint32_t* f;
 };
 
-__device__ __forceinline__ void part_init(int ga, LdsPart& P, int k) {
+__device__ __forceinline__ void part_init(int ga, const LdsPart& P, int k) {
   P.a[k] = (ga == GA_MIN) ? INFINITY : (ga == GA_MAX ? -INFINITY : 0.0);
   P.b[k] = 0.0;
   P.n[k] = 0;
@@ -226,7 +226,7 @@ __device__ __forceinline__ void part_init(int ga, LdsPart& P, int k) {
 }
 
 // AggregationIterator feeding Aggregator.runDouble, one span at a time in index order.
-__device__ __forceinline__ void contribute(int ga, LdsPart& P, int s, double v, bool uni) {
+__device__ __forceinline__ void contribute(int ga, const LdsPart& P, int s, double v, bool uni) {
   uint32_t f = P.f[s];
   switch (ga) {
     case GA_SUM: case GA_AVG:
@@ -300,25 +300,34 @@ __device__ __forceinline__ double interp(int method, const GridParams& p, int k0
   }
 }
 
-// ---- k_index: classify every row ---------------------------------------------------
-__global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual, RowDesc* __restrict__ rows,
-                                               int64_t n_rows, int32_t* err) {
+// ---- exactness certificate helpers ---------------------------------------------------
+// lsb(x): exponent of the least significant set bit of a finite non-zero double.
+__device__ __forceinline__ int lsb_exp(double x) {
+  const unsigned long long bits = (unsigned long long)__double_as_longlong(x);
+  const int E = (int)((bits >> 52) & 0x7FF);
+  const unsigned long long M = bits & 0xFFFFFFFFFFFFFULL;
+  if (E == 0) return -1074 + __ffsll((long long)M) - 1;
+  return E - 1075 + __ffsll((long long)(M | 0x10000000000000ULL)) - 1;
+}
+
+// ---- k_index: classify every row, validate it, certificate stats ---------------------
+__global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual, const uint8_t* __restrict__ val,
+                                               RowDesc* __restrict__ rows, int64_t n_rows, int32_t* err) {
   const int lane = lane_id();
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t r = wave; r < n_rows; r += nwaves) {
     RowDesc d = rows[r];
     const uint8_t* q = qual + d.qoff;
+    const uint8_t* v = val + d.voff;
     const uint32_t qlen = d.qlen;
     // hypotheses: all 2-byte, all 4-byte
     bool ok2 = (qlen % 2) == 0 && qlen > 0;
     bool ok4 = (qlen % 4) == 0 && qlen > 0;
     int lmin2 = 99, lmax2 = -1, lmin4 = 99, lmax4 = -1;
-    long long sum2 = 0, sum4 = 0;
-    bool bad2 = false, bad4 = false;
     for (uint32_t p0 = (uint32_t)lane * 16; p0 < qlen; p0 += 64 * 16) {
       const uint4 w = *reinterpret_cast<const uint4*>(q + p0);
-      uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+      const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
       for (int b = 0; b < 16; b += 2) {
         if (p0 + b >= qlen) break;
@@ -326,66 +335,105 @@ __global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual,
         const uint32_t b1 = (ws[(b + 1) >> 2] >> (((b + 1) & 3) * 8)) & 0xFF;
         if ((b0 & 0xF0) == 0xF0) ok2 = false;
         const int len = (b1 & 7) + 1;
-        const bool fl = (b1 & 8) != 0;
-        if (fl ? (len != 4 && len != 8) : (len == 3 || (len >= 5 && len <= 7))) bad2 = true;
         lmin2 = min(lmin2, len);
         lmax2 = max(lmax2, len);
-        sum2 += len;
         if ((b & 3) == 0) {
           if ((b0 & 0xF0) != 0xF0) ok4 = false;
           const uint32_t b3 = (ws[(b + 3) >> 2] >> (((b + 3) & 3) * 8)) & 0xFF;
           const int l4 = (b3 & 7) + 1;
-          const bool f4 = (b3 & 8) != 0;
-          if (f4 ? (l4 != 4 && l4 != 8) : (l4 == 3 || (l4 >= 5 && l4 <= 7))) bad4 = true;
           lmin4 = min(lmin4, l4);
           lmax4 = max(lmax4, l4);
-          sum4 += l4;
         }
       }
     }
     ok2 = __all(ok2);
     ok4 = __all(ok4);
-    bad2 = __any(bad2);
-    bad4 = __any(bad4);
     lmin2 = wave_min(lmin2); lmax2 = wave_max(lmax2);
     lmin4 = wave_min(lmin4); lmax4 = wave_max(lmax4);
-    sum2 = wave_sum64(sum2);
-    sum4 = wave_sum64(sum4);
-    if (lane == 0) {
-      uint32_t flags = 0, ndp = 0;
-      long long vneed = 0;
-      bool bad = false;
-      if (ok2) {
-        ndp = qlen / 2; flags = 2; vneed = sum2; bad = bad2;
-        if (lmin2 == lmax2) flags |= (uint32_t)lmin2 << ROW_VL_SHIFT;
-      } else if (ok4) {
-        ndp = qlen / 4; flags = 4; vneed = sum4; bad = bad4;
-        if (lmin4 == lmax4) flags |= (uint32_t)lmin4 << ROW_VL_SHIFT;
-      } else {
-        // mixed second/millisecond qualifiers (meta bit MS_MIXED_COMPACT): sequential walk
+    uint32_t flags = 0, ndp = 0;
+    if (ok2) {
+      ndp = qlen / 2; flags = 2;
+      if (lmin2 == lmax2) flags |= (uint32_t)lmin2 << ROW_VL_SHIFT;
+    } else if (ok4) {
+      ndp = qlen / 4; flags = 4;
+      if (lmin4 == lmax4) flags |= (uint32_t)lmin4 << ROW_VL_SHIFT;
+    } else {
+      // mixed second/millisecond qualifiers (meta bit MS_MIXED_COMPACT): count sequentially
+      if (lane == 0) {
         uint32_t i = 0;
         while (i < qlen) {
-          const uint32_t b0 = q[i];
-          const bool ms = (b0 & 0xF0) == 0xF0;
-          const uint32_t w = ms ? 4 : 2;
-          if (i + w > qlen) { bad = true; break; }
-          const uint32_t fb = q[i + w - 1];
-          const int len = (fb & 7) + 1;
-          const bool fl = (fb & 8) != 0;
-          if (fl ? (len != 4 && len != 8) : (len == 3 || (len >= 5 && len <= 7))) bad = true;
-          vneed += len;
+          const uint32_t w = ((q[i] & 0xF0) == 0xF0) ? 4 : 2;
+          if (i + w > qlen) break;
           ndp++;
           i += w;
         }
-        flags = 0;
       }
-      if (qlen == 0 || vneed > (long long)d.vlen) bad = true;
+      ndp = __shfl(ndp, 0, 64);
+    }
+    // walk every datapoint: validate qualifier/value lengths, certificate stats
+    bool bad = qlen == 0;
+    int lsbmin = INT32_MAX;
+    double amax = 0.0;
+    long long vcarry = 0;
+    uint32_t qcarry = 0;
+    for (uint32_t i0 = 0; i0 < ndp; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      const bool in = i < ndp;
+      uint32_t qpos = 0, w = 2;
+      if (flags & ROW_QW_MASK) {
+        w = flags & ROW_QW_MASK;
+        qpos = i * w;
+      } else {
+        // mixed: positions found by the sequential walk below
+      }
+      uint32_t fb = 0;
+      if (flags & ROW_QW_MASK) {
+        if (in) fb = q[qpos + w - 1];
+      } else {
+        // mixed rows are rare: lane 0 computes every width sequentially, then broadcasts through shuffles
+        uint32_t pos = qcarry, mypos = 0, myw = 2;
+        for (int t = 0; t < 64 && i0 + t < ndp; t++) {
+          const uint32_t ww = ((q[pos] & 0xF0) == 0xF0) ? 4 : 2;
+          if (t == lane) { mypos = pos; myw = ww; }
+          pos += ww;
+        }
+        qpos = mypos;
+        w = myw;
+        if (in) fb = q[qpos + w - 1];
+        qcarry = __shfl(pos, 0, 64);
+      }
+      const int len = in ? (int)(fb & 7) + 1 : 0;
+      const bool fl = (fb & 8) != 0;
+      if (in && (fl ? (len != 4 && len != 8) : (len == 3 || (len >= 5 && len <= 7)))) bad = true;
+      const int incl = wave_incl_sum(len);
+      const long long vo = vcarry + incl - len;
+      vcarry += __shfl(incl, 63, 64);
+      if (in && !bad && vo + len <= (long long)d.vlen) {
+        uint64_t bits = 0;
+        for (int b = 0; b < len; b++) bits = (bits << 8) | v[vo + b];
+        double x = 0.0;
+        decode_value(bits, len, fl, x);
+        if (!isnan(x)) {
+          const double ax = fabs(x);
+          if (ax > amax || isinf(ax)) amax = fmax(amax, ax);
+          if (x != 0.0 && !isinf(x)) lsbmin = min(lsbmin, lsb_exp(x));
+        }
+      }
+    }
+    if (vcarry > (long long)d.vlen) bad = true;
+    bad = __any(bad);
+    lsbmin = wave_min(lsbmin);
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) amax = fmax(amax, __shfl_xor(amax, dd, 64));
+    if (lane == 0) {
       if (bad) {
         flags |= ROW_ERR;
         set_err(err, TSDB_E_ILLEGAL_DATA);
       }
       d.ndp = ndp;
       d.flags = flags;
+      d.lsb = lsbmin;
+      d.absmax = amax;
       rows[r] = d;
     }
   }
@@ -393,12 +441,12 @@ __global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual,
 
 // ---- k_grid ---------------------------------------------------------------------
 struct WaveLds {
-  double* dpv;          // [CH] decoded values (aliases the vle byte staging buffer)
+  double* dpv;          // [CH] decoded values; aliases the vle byte staging and mixed-row scratch
   uint8_t* vbuf;
-  int32_t* seg_slot;    // [CH]
-  uint16_t* seg_start;  // [CH+1]
   uint32_t* mq;         // [CH] mixed-row scratch: off_ms
   uint32_t* mv;         // [CH] mixed-row scratch: value offset | len<<24 | float<<31
+  int32_t* seg_slot;    // [CH]
+  uint16_t* seg_start;  // [CH+1]
   double* dense;        // [K] per-series bucket values
   uint8_t* pres;        // [K] bucket present
   double* rate;         // [K] rate values (rate mode)
@@ -407,83 +455,210 @@ struct WaveLds {
 
 __host__ __device__ inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 
-__host__ __device__ inline int64_t wave_lds_bytes(int64_t K, bool rate) {
-  int64_t o = 0;
-  o += VBUF;                 // dpv / vbuf
-  o += CH * 4;               // seg_slot
-  o += align16((CH + 1) * 2);// seg_start
-  o += CH * 4 * 2;           // mq, mv
-  o += align16(K * 8);       // dense
-  o += align16(K);           // pres
+// fixed per-wave LDS (decode staging + segment lists)
+__host__ __device__ constexpr int64_t fixed_lds_bytes() { return VBUF + CH * 4 + ((CH + 1) * 2 + 15) / 16 * 16; }
+
+__host__ __device__ inline int64_t slot_lds_bytes(int64_t K, bool rate) {
+  int64_t o = align16(K * 8) + align16(K);
   if (rate) o += align16(K * 8);
-  o += align16(K * 8) * 2 + align16(K * 4) * 2;  // part
-  return align16(o);
+  o += align16(K * 8) * 2 + align16(K * 4) * 2;
+  return o;
 }
 
-__device__ inline WaveLds carve(unsigned char* base, int64_t K, bool rate) {
+template <bool GSLOT>
+__device__ inline WaveLds carve(const GridParams& p, unsigned char* base, int64_t tile, int64_t K, bool rate) {
   WaveLds w;
   int64_t o = 0;
   w.dpv = (double*)(base + o);
   w.vbuf = base + o;
+  w.mq = (uint32_t*)(base + o);
+  w.mv = (uint32_t*)(base + o + CH * 4);
   o += VBUF;
   w.seg_slot = (int32_t*)(base + o); o += CH * 4;
   w.seg_start = (uint16_t*)(base + o); o += align16((CH + 1) * 2);
-  w.mq = (uint32_t*)(base + o); o += CH * 4;
-  w.mv = (uint32_t*)(base + o); o += CH * 4;
-  w.dense = (double*)(base + o); o += align16(K * 8);
-  w.pres = base + o; o += align16(K);
-  if (rate) { w.rate = (double*)(base + o); o += align16(K * 8); } else { w.rate = nullptr; }
-  w.part.a = (double*)(base + o); o += align16(K * 8);
-  w.part.b = (double*)(base + o); o += align16(K * 8);
-  w.part.n = (uint32_t*)(base + o); o += align16(K * 4);
-  w.part.f = (uint32_t*)(base + o); o += align16(K * 4);
+  if (GSLOT) {
+    w.dense = p.g_dense + tile * K;
+    w.pres = p.g_pres + tile * K;
+    w.rate = rate ? p.g_rate + tile * K : nullptr;
+    w.part.a = p.part.a + tile * K;
+    w.part.b = p.part.b + tile * K;
+    w.part.n = p.part.n + tile * K;
+    w.part.f = p.part.f + tile * K;
+  } else {
+    w.dense = (double*)(base + o); o += align16(K * 8);
+    w.pres = base + o; o += align16(K);
+    if (rate) { w.rate = (double*)(base + o); o += align16(K * 8); } else { w.rate = nullptr; }
+    w.part.a = (double*)(base + o); o += align16(K * 8);
+    w.part.b = (double*)(base + o); o += align16(K * 8);
+    w.part.n = (uint32_t*)(base + o); o += align16(K * 4);
+    w.part.f = (uint32_t*)(base + o); o += align16(K * 4);
+  }
   return w;
 }
 
-// Decodes the lane's 8 datapoints of chunk [c0, c0+CH) of row d into (slot, value).
-// Returns false (and sets err) on malformed data.
-__device__ __forceinline__ void decode_chunk(const GridParams& p, const RowDesc& d, const RowGeom& g,
-                                             int64_t c0, const WaveLds& W, int64_t& vcur,
-                                             int slot[DPL], double val[DPL]) {
+// Raw bytes of one lane's 8 datapoints of a uniform row (qualifier width 2/4, value length 1/2/4/8)
+struct Raw {
+  uint4 q0, q1;
+  uint4 v0, v1, v2, v3;
+};
+
+__device__ __forceinline__ bool row_uniform(const RowDesc& d) {
+  return (d.flags & ROW_QW_MASK) != 0 && (d.flags & ROW_VL_MASK) != 0 && !(d.flags & ROW_ERR);
+}
+
+__device__ __forceinline__ void load_raw(const GridParams& p, const RowDesc& d, int64_t c0, Raw& rw) {
+  const int lane = lane_id();
+  const int64_t i0 = c0 + (int64_t)lane * DPL;
+  if (i0 >= (int64_t)d.ndp) return;
+  const int qw = d.flags & ROW_QW_MASK;
+  const int vl = (d.flags & ROW_VL_MASK) >> ROW_VL_SHIFT;
+  const uint8_t* q = p.qual + d.qoff + i0 * qw;
+  const uint8_t* v = p.val + d.voff + i0 * vl;
+  rw.q0 = *reinterpret_cast<const uint4*>(q);
+  if (qw == 4) rw.q1 = *reinterpret_cast<const uint4*>(q + 16);
+  if (vl == 1) {
+    const uint2 t = *reinterpret_cast<const uint2*>(v);
+    rw.v0 = make_uint4(t.x, t.y, 0, 0);
+  } else {
+    rw.v0 = *reinterpret_cast<const uint4*>(v);
+    if (vl >= 4) rw.v1 = *reinterpret_cast<const uint4*>(v + 16);
+    if (vl == 8) {
+      rw.v2 = *reinterpret_cast<const uint4*>(v + 32);
+      rw.v3 = *reinterpret_cast<const uint4*>(v + 48);
+    }
+  }
+}
+
+// Decodes the lane's 8 datapoints of a uniform row from raw registers into (slot, value).
+__device__ __forceinline__ void decode_raw(const GridParams& p, const RowDesc& d, const RowGeom& g, int64_t c0,
+                                           const Raw& rw, int slot[DPL], double val[DPL]) {
   const int lane = lane_id();
   const int64_t i0 = c0 + (int64_t)lane * DPL;
   const int nv = (int)max((int64_t)0, min((int64_t)DPL, (int64_t)d.ndp - i0));
   const int qw = d.flags & ROW_QW_MASK;
   const int vl = (d.flags & ROW_VL_MASK) >> ROW_VL_SHIFT;
-  const uint8_t* q = p.qual + d.qoff;
-  const uint8_t* v = p.val + d.voff;
-  uint32_t off[DPL];
-  uint32_t fl[DPL];
-#pragma unroll
-  for (int j = 0; j < DPL; j++) { off[j] = 0; fl[j] = 0; slot[j] = -1; val[j] = 0.0; }
-
+  uint32_t off[DPL], fl[DPL];
   if (qw == 2) {
-    if (nv > 0) {
-      const uint4 w = *reinterpret_cast<const uint4*>(q + i0 * 2);
-      const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+    const uint32_t ws[4] = {rw.q0.x, rw.q0.y, rw.q0.z, rw.q0.w};
 #pragma unroll
-      for (int j = 0; j < DPL; j++) {
-        const uint32_t be = __builtin_bswap32(ws[j >> 1]);
-        const uint32_t qq = (j & 1) ? (be & 0xFFFF) : (be >> 16);
-        off[j] = (qq >> 4) * 1000u;
-        fl[j] = qq & 0xF;
-      }
-    }
-  } else if (qw == 4) {
-    if (nv > 0) {
-      const uint4 w0 = *reinterpret_cast<const uint4*>(q + i0 * 4);
-      const uint4 w1 = *reinterpret_cast<const uint4*>(q + i0 * 4 + 16);
-      const uint32_t ws[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-#pragma unroll
-      for (int j = 0; j < DPL; j++) {
-        const uint32_t qq = __builtin_bswap32(ws[j]);
-        off[j] = (qq & 0x0FFFFFC0u) >> 6;
-        fl[j] = qq & 0xF;
-      }
+    for (int j = 0; j < DPL; j++) {
+      const uint32_t be = __builtin_bswap32(ws[j >> 1]);
+      const uint32_t qq = (j & 1) ? (be & 0xFFFF) : (be >> 16);
+      off[j] = (qq >> 4) * 1000u;
+      fl[j] = qq & 0xF;
     }
   } else {
-    // mixed s/ms row: lane 0 walks the chunk sequentially (RowSeq.Iterator.next, :552-568)
-    // positions carried in vcur (low 32: qualifier byte index, high 32: value byte index)
+    const uint32_t ws[8] = {rw.q0.x, rw.q0.y, rw.q0.z, rw.q0.w, rw.q1.x, rw.q1.y, rw.q1.z, rw.q1.w};
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      const uint32_t qq = __builtin_bswap32(ws[j]);
+      off[j] = (qq & 0x0FFFFFC0u) >> 6;
+      fl[j] = qq & 0xF;
+    }
+  }
+  if (vl == 4) {
+    const uint32_t ws[8] = {rw.v0.x, rw.v0.y, rw.v0.z, rw.v0.w, rw.v1.x, rw.v1.y, rw.v1.z, rw.v1.w};
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      const uint32_t be = __builtin_bswap32(ws[j]);
+      val[j] = (fl[j] & 8) ? (double)__uint_as_float(be) : (double)(int32_t)be;
+    }
+  } else if (vl == 8) {
+    const uint32_t ws[16] = {rw.v0.x, rw.v0.y, rw.v0.z, rw.v0.w, rw.v1.x, rw.v1.y, rw.v1.z, rw.v1.w,
+                             rw.v2.x, rw.v2.y, rw.v2.z, rw.v2.w, rw.v3.x, rw.v3.y, rw.v3.z, rw.v3.w};
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      const uint64_t a = ((uint64_t)__builtin_bswap32(ws[2 * j]) << 32) | __builtin_bswap32(ws[2 * j + 1]);
+      val[j] = (fl[j] & 8) ? __longlong_as_double((long long)a) : (double)(long long)a;
+    }
+  } else if (vl == 2) {
+    const uint32_t ws[4] = {rw.v0.x, rw.v0.y, rw.v0.z, rw.v0.w};
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      const uint32_t be = __builtin_bswap32(ws[j >> 1]);
+      const uint32_t x = (j & 1) ? (be & 0xFFFF) : (be >> 16);
+      val[j] = (double)(int16_t)(uint16_t)x;
+    }
+  } else {
+    const uint32_t ws[2] = {rw.v0.x, rw.v0.y};
+#pragma unroll
+    for (int j = 0; j < DPL; j++) val[j] = (double)(int8_t)((ws[j >> 2] >> ((j & 3) * 8)) & 0xFF);
+  }
+#pragma unroll
+  for (int j = 0; j < DPL; j++) slot[j] = (j < nv) ? slot_of(p, g, d.base, off[j]) : -1;
+}
+
+// Generic decode (variable-length values, mixed qualifier widths); loads inside.
+__device__ __forceinline__ void decode_generic(const GridParams& p, const RowDesc& d, const RowGeom& g, int64_t c0,
+                               const WaveLds& W, int64_t& vcur, int slot[DPL], double val[DPL]) {
+  const int lane = lane_id();
+  const int64_t i0 = c0 + (int64_t)lane * DPL;
+  const int nv = (int)max((int64_t)0, min((int64_t)DPL, (int64_t)d.ndp - i0));
+  const int qw = d.flags & ROW_QW_MASK;
+  const uint8_t* q = p.qual + d.qoff;
+  const uint8_t* v = p.val + d.voff;
+  uint32_t off[DPL], fl[DPL];
+#pragma unroll
+  for (int j = 0; j < DPL; j++) { off[j] = 0; fl[j] = 0; slot[j] = -1; val[j] = 0.0; }
+  WAVE_SYNC();
+  if (qw == 2 || qw == 4) {
+    if (nv > 0) {
+      if (qw == 2) {
+        const uint4 w = *reinterpret_cast<const uint4*>(q + i0 * 2);
+        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int j = 0; j < DPL; j++) {
+          const uint32_t be = __builtin_bswap32(ws[j >> 1]);
+          const uint32_t qq = (j & 1) ? (be & 0xFFFF) : (be >> 16);
+          off[j] = (qq >> 4) * 1000u;
+          fl[j] = qq & 0xF;
+        }
+      } else {
+        const uint4 w0 = *reinterpret_cast<const uint4*>(q + i0 * 4);
+        const uint4 w1 = *reinterpret_cast<const uint4*>(q + i0 * 4 + 16);
+        const uint32_t ws[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+        for (int j = 0; j < DPL; j++) {
+          const uint32_t qq = __builtin_bswap32(ws[j]);
+          off[j] = (qq & 0x0FFFFFC0u) >> 6;
+          fl[j] = qq & 0xF;
+        }
+      }
+    }
+    // variable-length values: wave prefix scan of lengths, stage the chunk's bytes in LDS
+    int len[DPL];
+    int loc = 0;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      len[j] = (j < nv) ? (int)(fl[j] & 7) + 1 : 0;
+      loc += len[j];
+    }
+    const int incl = wave_incl_sum(loc);
+    const int total = __shfl(incl, 63, 64);
+    const int excl = incl - loc;
+    const int64_t start = (int64_t)d.voff + vcur;
+    const int64_t a0 = start & ~(int64_t)15;
+    const int64_t lead = start - a0;
+    const int npieces = (int)((lead + total + 15) >> 4);
+    for (int pc = lane; pc < npieces; pc += 64)
+      reinterpret_cast<uint4*>(W.vbuf)[pc] = *reinterpret_cast<const uint4*>(p.val + a0 + pc * 16);
+    WAVE_SYNC();
+    int o = (int)lead + excl;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      if (j < nv) {
+        uint64_t bits = 0;
+        for (int b = 0; b < len[j]; b++) bits = (bits << 8) | W.vbuf[o + b];
+        double x = 0.0;
+        if (!decode_value(bits, len[j], (fl[j] & 8) != 0, x)) set_err(p.err, TSDB_E_ILLEGAL_DATA);
+        val[j] = x;
+        slot[j] = slot_of(p, g, d.base, off[j]);
+      }
+      o += len[j];
+    }
+    vcur += total;
+  } else {
+    // mixed s/ms row: lane 0 walks the chunk (RowSeq.Iterator.next, :552-568); positions in vcur
     if (lane == 0) {
       uint32_t qi = (uint32_t)(vcur & 0xFFFFFFFF), vi = (uint32_t)(vcur >> 32);
       for (int t = 0; t < CH && c0 + t < (int64_t)d.ndp; t++) {
@@ -505,101 +680,396 @@ __device__ __forceinline__ void decode_chunk(const GridParams& p, const RowDesc&
     for (int j = 0; j < DPL; j++) {
       if (j < nv) {
         const int t = lane * DPL + j;
-        off[j] = W.mq[t];
         const uint32_t mvv = W.mv[t];
         const uint32_t vo = mvv & 0xFFFFFF;
         const int len = (mvv >> 24) & 0x7F;
         uint64_t bits = 0;
         for (int b = 0; b < len; b++) bits = (bits << 8) | v[vo + b];
-        double x;
+        double x = 0.0;
         if (!decode_value(bits, len, (mvv >> 31) != 0, x)) set_err(p.err, TSDB_E_ILLEGAL_DATA);
         val[j] = x;
-        slot[j] = slot_of(p, g, d.base, off[j]);
+        slot[j] = slot_of(p, g, d.base, W.mq[t]);
       }
     }
-    WAVE_SYNC();
-    return;
   }
+  WAVE_SYNC();
+}
 
-  if (vl != 0) {
-    // uniform value length: direct coalesced loads
-    if (nv > 0) {
-      if (vl == 4) {
-        const uint4 w0 = *reinterpret_cast<const uint4*>(v + i0 * 4);
-        const uint4 w1 = *reinterpret_cast<const uint4*>(v + i0 * 4 + 16);
-        const uint32_t ws[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+// ---- fast per-bucket reduction: order-free state combined across lanes ----------------
+// Used for downsample functions whose result is exact in any association order: min, max,
+// count, first, last, and sum / avg / squareSum under the exactness certificate.
+template <int F>
+__device__ __forceinline__ constexpr bool fast_capable() {
+  return F == F_SUM || F == F_AVG || F == F_COUNT || F == F_SQUARESUM || F == F_MIN || F == F_MAX ||
+         F == F_FIRST || F == F_LAST;
+}
+template <int F>
+__device__ __forceinline__ constexpr bool needs_cert() {
+  return F == F_SUM || F == F_AVG || F == F_SQUARESUM;
+}
+
+struct FS {
+  double v;
+  int n;
+};
+
+template <int F>
+__device__ __forceinline__ FS fs_id() {
+  FS s;
+  s.v = (F == F_MIN) ? (double)INFINITY : (F == F_MAX ? -(double)INFINITY : 0.0);
+  s.n = 0;
+  return s;
+}
+template <int F>
+__device__ __forceinline__ FS fs_of(double x) {
+  FS s = fs_id<F>();
+  if (F == F_FIRST || F == F_LAST) { s.v = x; s.n = 1; return s; }
+  if (isnan(x)) return s;
+  if (F == F_SQUARESUM) s.v = x * x;
+  else if (F != F_COUNT) s.v = x;
+  s.n = 1;
+  return s;
+}
+template <int F>
+__device__ __forceinline__ FS fs_op(const FS& a, const FS& b) {
+  FS r;
+  if (F == F_MIN) { r = (b.v < a.v) ? b : a; return r; }
+  if (F == F_MAX) { r = (b.v > a.v) ? b : a; return r; }
+  if (F == F_FIRST) return a.n ? a : b;
+  if (F == F_LAST) return b.n ? b : a;
+  r.v = (F == F_COUNT) ? 0.0 : a.v + b.v;
+  r.n = a.n + b.n;
+  return r;
+}
+template <int F>
+__device__ __forceinline__ double fs_final(const FS& s) {
+  if (F == F_SUM || F == F_SQUARESUM) return s.n == 0 ? (double)NAN : s.v;
+  if (F == F_AVG) return s.n == 0 ? (double)NAN : s.v / (double)s.n;
+  if (F == F_COUNT) return (double)s.n;
+  if (F == F_MIN) return s.v == INFINITY ? (double)NAN : s.v;
+  if (F == F_MAX) return s.v == -INFINITY ? (double)NAN : s.v;
+  return s.v;
+}
+
+__device__ __forceinline__ FS shfl_up_fs(const FS& s, int d) {
+  FS r;
+  r.v = __shfl_up(s.v, d, 64);
+  r.n = __shfl_up(s.n, d, 64);
+  return r;
+}
+__device__ __forceinline__ FS shfl_fs(const FS& s, int src) {
+  FS r;
+  r.v = __shfl(s.v, src, 64);
+  r.n = __shfl(s.n, src, 64);
+  return r;
+}
+
+// Per-series state carried across chunks / rows.
+struct SeriesState {
+  int carry_slot;
+  FS fcarry;       // fast-path open bucket
+  BState scarry;   // slow-path open bucket
+  int nmax;        // largest bucket (datapoint count) emitted by the fast path
+};
+
+template <int F>
+__device__ __forceinline__ void emit_bucket(const WaveLds& W, int k, double v) {
+  W.dense[k] = v;
+  W.pres[k] = 1;
+}
+
+// Fast path: segmented reduction of one decoded chunk, keys = slots (non-decreasing).
+template <int F>
+__device__ __forceinline__ void fast_chunk(const WaveLds& W, SeriesState& st, const int slot[DPL], const double val[DPL]) {
+  const int lane = lane_id();
+  int kf = -1, kl = -1, cur_key = -1, nruns = 0;
+  FS Pf = fs_id<F>(), cur = fs_id<F>();
+  int mymax = 0;
 #pragma unroll
-        for (int j = 0; j < DPL; j++) {
-          const uint32_t be = __builtin_bswap32(ws[j]);
-          val[j] = (fl[j] & 8) ? (double)__uint_as_float(be) : (double)(int32_t)be;
+  for (int j = 0; j < DPL; j++) {
+    if (slot[j] < 0) continue;
+    const FS x = fs_of<F>(val[j]);
+    if (slot[j] != cur_key) {
+      if (cur_key >= 0) {
+        if (nruns == 1) { Pf = cur; kf = cur_key; }
+        else { emit_bucket<F>(W, cur_key, fs_final<F>(cur)); mymax = max(mymax, cur.n); }
+      }
+      cur_key = slot[j];
+      cur = x;
+      nruns++;
+    } else {
+      cur = fs_op<F>(cur, x);
+    }
+  }
+  FS Pl = cur;
+  kl = cur_key;
+  if (nruns == 1) { kf = kl; Pf = Pl; }
+  const bool has = nruns > 0;
+  const bool multi = nruns >= 2;
+  const unsigned long long hm = __ballot(has);
+  if (hm == 0) return;
+  const int fv = __ffsll((long long)hm) - 1;          // first lane with datapoints
+  const int lv = 63 - __clzll((long long)hm);        // last lane with datapoints
+  // open bucket from the previous chunk
+  const int kf_fv = __shfl(kf, fv, 64);
+  if (st.carry_slot >= 0) {
+    if (kf_fv == st.carry_slot) {
+      if (lane == fv) {
+        Pf = fs_op<F>(st.fcarry, Pf);
+        if (!multi) Pl = Pf;
+      }
+    } else if (lane == 0) {
+      emit_bucket<F>(W, st.carry_slot, fs_final<F>(st.fcarry));
+      mymax = max(mymax, st.fcarry.n);
+    }
+  }
+  // segmented inclusive scan of the last runs
+  const int kl_prev = __shfl_up(kl, 1, 64);
+  int h = (!has || multi || lane == 0 || kl_prev != kf) ? 1 : 0;
+  FS T = has ? Pl : fs_id<F>();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const FS To = shfl_up_fs(T, d);
+    const int ho = __shfl_up(h, d, 64);
+    if (lane >= d) {
+      if (!h) T = fs_op<F>(To, T);
+      h |= ho;
+    }
+  }
+  const FS Tprev = shfl_up_fs(T, 1);
+  const int kf_next = __shfl_down(kf, 1, 64);
+  if (has && multi) {
+    const FS tot = (lane > 0 && kl_prev == kf && lane > fv) ? fs_op<F>(Tprev, Pf) : Pf;
+    emit_bucket<F>(W, kf, fs_final<F>(tot));
+    mymax = max(mymax, tot.n);
+  }
+  if (has && lane != lv && kf_next != kl) {
+    emit_bucket<F>(W, kl, fs_final<F>(T));
+    mymax = max(mymax, T.n);
+  }
+  st.carry_slot = __shfl(kl, lv, 64);
+  st.fcarry = shfl_fs(T, lv);
+  st.nmax = max(st.nmax, wave_max(mymax));
+}
+
+// Slow path: every (series, bucket) reduced sequentially in time order (bit-exact always).
+template <int F>
+__device__ __forceinline__ void slow_chunk(const WaveLds& W, SeriesState& st, const int slot[DPL], const double val[DPL]) {
+  const int lane = lane_id();
+  WAVE_SYNC();
+#pragma unroll
+  for (int j = 0; j < DPL; j++) W.dpv[lane * DPL + j] = val[j];
+  const int prev_last = __shfl_up(slot[DPL - 1], 1, 64);
+  int h = 0;
+  bool head[DPL];
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    const int ps = (j == 0) ? (lane == 0 ? -2 : prev_last) : slot[j - 1];
+    head[j] = slot[j] >= 0 && (ps < 0 || ps != slot[j]);
+    h += head[j];
+  }
+  int vend = 0;
+#pragma unroll
+  for (int j = 0; j < DPL; j++) if (slot[j] >= 0) vend = lane * DPL + j + 1;
+  vend = wave_max(vend);
+  const int hincl = wave_incl_sum(h);
+  const int nseg = __shfl(hincl, 63, 64);
+  int pos = hincl - h;
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    if (head[j]) {
+      W.seg_start[pos] = (uint16_t)(lane * DPL + j);
+      W.seg_slot[pos] = slot[j];
+      pos++;
+    }
+  }
+  if (lane == 0) W.seg_start[nseg] = (uint16_t)vend;
+  WAVE_SYNC();
+  if (nseg == 0) return;
+  const int first_slot = W.seg_slot[0];
+  if (st.carry_slot >= 0 && first_slot != st.carry_slot) {
+    if (lane == 0) emit_bucket<F>(W, st.carry_slot, bs_final<F>(st.scarry));
+    st.carry_slot = -1;
+    bs_init<F>(st.scarry);
+  }
+  for (int b0 = 0; b0 < nseg; b0 += 64) {
+    const int si = b0 + lane;
+    const bool act = si < nseg;
+    BState s;
+    bs_init<F>(s);
+    int myslot = -1;
+    if (act) {
+      myslot = W.seg_slot[si];
+      if (si == 0 && myslot == st.carry_slot) s = st.scarry;
+      const int e = W.seg_start[si + 1];
+      int i = W.seg_start[si];
+      // 4 LDS reads in flight per step
+      for (; i + 4 <= e; i += 4) {
+        const double x0 = W.dpv[i], x1 = W.dpv[i + 1], x2 = W.dpv[i + 2], x3 = W.dpv[i + 3];
+        bs_add<F>(s, x0); bs_add<F>(s, x1); bs_add<F>(s, x2); bs_add<F>(s, x3);
+      }
+      for (; i < e; i++) bs_add<F>(s, W.dpv[i]);
+      if (si != nseg - 1) emit_bucket<F>(W, myslot, bs_final<F>(s));
+    }
+    if (b0 + 64 >= nseg) {
+      const int src = (nseg - 1) & 63;
+      st.scarry.a = __shfl(s.a, src, 64);
+      st.scarry.b = __shfl(s.b, src, 64);
+      st.scarry.n = __shfl(s.n, src, 64);
+      st.carry_slot = __shfl(myslot, src, 64);
+    }
+  }
+  WAVE_SYNC();
+}
+
+// ---- series -> SpanGroup contributions over the K slots -----------------------------
+__device__ __forceinline__ void emit_series(const GridParams& p, const WaveLds& W, int K) {
+  const int lane = lane_id();
+  const int ga = p.ga;
+  const double fillv = (p.fill == TSDB_FILL_ZERO) ? 0.0 : (double)NAN;
+  WAVE_SYNC();
+  if (!p.rate) {
+    if (p.fill != TSDB_FILL_NONE && p.mode == MODE_GRID) {
+      // FillingDownsampler (:172-301): every slot, missing -> NaN / 0 / RuntimeException
+      for (int k = lane; k < K; k += 64) {
+        const bool pr = W.pres[k] != 0;
+        if (!pr && p.fill == TSDB_FILL_SCALAR) set_err(p.err, TSDB_E_RUNTIME);
+        contribute(ga, W.part, k, pr ? W.dense[k] : fillv, true);
+      }
+    } else {
+      int prev_present = -1;
+      for (int kb = 0; kb < K; kb += 64) {
+        const int k = kb + lane;
+        const bool pr = k < K && W.pres[k] != 0;
+        const int incl = wave_incl_max(pr ? k : -1);
+        int pp = __shfl_up(incl, 1, 64);
+        if (lane == 0) pp = -1;
+        pp = max(pp, prev_present);
+        if (pr) {
+          const double v = W.dense[k];
+          if (pp >= 0 && pp < k - 1) {
+            const double y0 = W.dense[pp];
+            for (int s2 = pp + 1; s2 < k; s2++) contribute(ga, W.part, s2, interp(p.interp, p, pp, y0, k, v, s2), false);
+          }
+          contribute(ga, W.part, k, v, true);
         }
-      } else if (vl == 8) {
-        const uint4* pv = reinterpret_cast<const uint4*>(v + i0 * 8);
-#pragma unroll
-        for (int h = 0; h < 4; h++) {
-          const uint4 w = pv[h];
-          const uint64_t a = ((uint64_t)__builtin_bswap32(w.x) << 32) | __builtin_bswap32(w.y);
-          const uint64_t b = ((uint64_t)__builtin_bswap32(w.z) << 32) | __builtin_bswap32(w.w);
-          val[2 * h] = (fl[2 * h] & 8) ? __longlong_as_double((long long)a) : (double)(long long)a;
-          val[2 * h + 1] = (fl[2 * h + 1] & 8) ? __longlong_as_double((long long)b) : (double)(long long)b;
-        }
-      } else if (vl == 2) {
-        const uint4 w = *reinterpret_cast<const uint4*>(v + i0 * 2);
-        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-        for (int j = 0; j < DPL; j++) {
-          const uint32_t be = __builtin_bswap32(ws[j >> 1]);
-          const uint32_t x = (j & 1) ? (be & 0xFFFF) : (be >> 16);
-          val[j] = (double)(int16_t)(uint16_t)x;
-        }
-      } else {  // vl == 1
-        const uint2 w = *reinterpret_cast<const uint2*>(v + i0);
-        const uint32_t ws[2] = {w.x, w.y};
-#pragma unroll
-        for (int j = 0; j < DPL; j++) val[j] = (double)(int8_t)((ws[j >> 2] >> ((j & 3) * 8)) & 0xFF);
+        prev_present = max(prev_present, __shfl(incl, 63, 64));
       }
     }
   } else {
-    // variable-length values (vle ints): wave prefix scan of lengths, stage bytes in LDS
-    int len[DPL];
-    int loc = 0;
-#pragma unroll
-    for (int j = 0; j < DPL; j++) {
-      len[j] = (j < nv) ? (int)(fl[j] & 7) + 1 : 0;
-      loc += len[j];
-    }
-    const int incl = wave_incl_sum(loc);
-    const int total = __shfl(incl, 63, 64);
-    const int excl = incl - loc;
-    const int64_t start = (int64_t)d.voff + vcur;           // absolute byte offset in blob
-    const int64_t a0 = start & ~(int64_t)15;
-    const int64_t lead = start - a0;
-    const int npieces = (int)((lead + total + 15) >> 4);
-    WAVE_SYNC();
-    for (int pc = lane; pc < npieces; pc += 64)
-      reinterpret_cast<uint4*>(W.vbuf)[pc] = *reinterpret_cast<const uint4*>(p.val + a0 + pc * 16);
-    WAVE_SYNC();
-    int o = (int)lead + excl;
-#pragma unroll
-    for (int j = 0; j < DPL; j++) {
-      if (j < nv) {
-        uint64_t bits = 0;
-        for (int b = 0; b < len[j]; b++) bits = (bits << 8) | W.vbuf[o + b];
-        double x;
-        if (!decode_value(bits, len[j], (fl[j] & 8) != 0, x)) set_err(p.err, TSDB_E_ILLEGAL_DATA);
-        val[j] = x;
+    // RateSpan over the bucket stream (:121-180), aggregated with PREV semantics
+    // (AggregationIterator ctor rate branch :448-459, nextDoubleValue :744-753)
+    int prev_item = -1, last_surv = -1;
+    long long nsurv = 0;
+    const bool dense_stream = p.fill != TSDB_FILL_NONE && p.mode == MODE_GRID;
+    for (int kb = 0; kb < K; kb += 64) {
+      const int k = kb + lane;
+      const bool inK = k < K;
+      const bool pr = inK && W.pres[k] != 0;
+      const bool item = inK && (dense_stream || pr);
+      if (item && !pr && p.fill == TSDB_FILL_SCALAR) set_err(p.err, TSDB_E_RUNTIME);
+      const int iincl = wave_incl_max(item ? k : -1);
+      int pi = __shfl_up(iincl, 1, 64);
+      if (lane == 0) pi = -1;
+      pi = max(pi, prev_item);
+      bool sv = false;
+      double r = 0.0;
+      if (item) {
+        const double v1 = pr ? W.dense[k] : fillv;
+        double v0 = 0.0;
+        long long t0 = 0;
+        if (pi >= 0) { v0 = W.pres[pi] ? W.dense[pi] : fillv; t0 = p.B0 + (long long)pi * p.I; }
+        const long long t1 = (p.mode == MODE_ALL) ? p.qs : p.B0 + (long long)k * p.I;
+        if (t1 <= t0) set_err(p.err, TSDB_E_ILLEGAL_STATE);
+        const double dt = (double)(t1 - t0) / 1000.0;
+        double diff = v1 - v0;
+        sv = true;
+        if (p.counter && diff < 0) {
+          if (p.drop) {
+            sv = false;
+          } else {
+            diff = (double)p.counter_max - v0 + v1;
+            r = diff / dt;
+            if (p.reset_value > 0 && r > (double)p.reset_value) r = 0.0;
+          }
+        } else {
+          r = diff / dt;
+        }
+        if (sv) W.rate[k] = r;
       }
-      o += len[j];
+      WAVE_SYNC();
+      const int cincl = wave_incl_sum(sv ? 1 : 0);
+      const long long m = nsurv + (cincl - (sv ? 1 : 0));
+      const int sincl = wave_incl_max(sv ? k : -1);
+      int ps = __shfl_up(sincl, 1, 64);
+      if (lane == 0) ps = -1;
+      ps = max(ps, last_surv);
+      if (sv) {
+        if (m == 1) {
+          const double r0 = W.rate[ps];
+          for (int s2 = 0; s2 < k; s2++) contribute(ga, W.part, s2, r0, false);
+          contribute(ga, W.part, k, r, true);
+        } else if (m >= 2) {
+          const double rp = W.rate[ps];
+          for (int s2 = ps + 1; s2 < k; s2++) contribute(ga, W.part, s2, rp, false);
+          contribute(ga, W.part, k, r, true);
+        }
+      }
+      prev_item = max(prev_item, __shfl(iincl, 63, 64));
+      last_surv = max(last_surv, __shfl(sincl, 63, 64));
+      nsurv += __shfl(cincl, 63, 64);
+      WAVE_SYNC();
     }
-    vcur += total;
-    WAVE_SYNC();
   }
-#pragma unroll
-  for (int j = 0; j < DPL; j++)
-    if (j < nv) slot[j] = slot_of(p, g, d.base, off[j]);
+  WAVE_SYNC();
 }
 
+// Next row of the tile inside the scan range, starting at (s, r) inclusive.
+__device__ __forceinline__ bool seek_row(const GridParams& p, int64_t s_end, int64_t& s, int64_t& r, RowDesc& d) {
+  while (s < s_end) {
+    const int64_t r1 = p.series_row_ptr[s + 1];
+    for (; r < r1; r++) {
+      d = p.rows[r];
+      if ((int64_t)d.base < p.ss) continue;
+      if ((int64_t)d.base >= p.se) break;
+      return true;
+    }
+    s++;
+    if (s < s_end) r = p.series_row_ptr[s];
+  }
+  return false;
+}
+
+// The slow path over one whole series (after a failed certificate, or for
+// order-sensitive downsample functions).
 template <int F>
+__device__ __forceinline__ void series_slow(const GridParams& p, const WaveLds& W, int64_t s, int K) {
+  const int lane = lane_id();
+  for (int k = lane; k < K; k += 64) W.pres[k] = 0;
+  WAVE_SYNC();
+  SeriesState st;
+  st.carry_slot = -1;
+  bs_init<F>(st.scarry);
+  const int64_t r0 = p.series_row_ptr[s], r1 = p.series_row_ptr[s + 1];
+  for (int64_t r = r0; r < r1; r++) {
+    const RowDesc d = p.rows[r];
+    if ((int64_t)d.base < p.ss) continue;
+    if ((int64_t)d.base >= p.se) break;
+    if (d.flags & ROW_ERR) { if (lane == 0) set_err(p.err, TSDB_E_ILLEGAL_DATA); continue; }
+    const RowGeom g = row_geom(p, d.base);
+    int64_t vcur = 0;
+    for (int64_t c0 = 0; c0 < (int64_t)d.ndp; c0 += CH) {
+      int slot[DPL];
+      double val[DPL];
+      decode_generic(p, d, g, c0, W, vcur, slot, val);
+      slow_chunk<F>(W, st, slot, val);
+    }
+  }
+  if (st.carry_slot >= 0 && lane == 0) emit_bucket<F>(W, st.carry_slot, bs_final<F>(st.scarry));
+  WAVE_SYNC();
+}
+
+template <int F, bool GSLOT>
 __global__ __launch_bounds__(256) void k_grid(GridParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
@@ -607,211 +1077,121 @@ __global__ __launch_bounds__(256) void k_grid(GridParams p) {
   const int64_t tile = (int64_t)blockIdx.x * p.waves + wave;
   if (tile >= p.n_tiles) return;
   const int K = (int)p.K;
-  WaveLds W = carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0);
-  const int ga = p.ga;
+  const WaveLds W = carve<GSLOT>(p, smem + (int64_t)wave * p.wave_lds, tile, K, p.rate != 0);
+  for (int k = lane; k < K; k += 64) part_init(p.ga, W.part, k);
 
-  for (int k = lane; k < K; k += 64) part_init(ga, W.part, k);
+  const int64_t s_end = p.tile_end[tile];
+  int64_t cs = p.tile_begin[tile];
+  int64_t cr = (cs < s_end) ? p.series_row_ptr[cs] : 0;
+  RowDesc cd;
+  bool cok = seek_row(p, s_end, cs, cr, cd);
+  if (cok && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
+  // one row of look-ahead (descriptor prefetch)
+  int64_t ns = cs, nr = cr + 1;
+  RowDesc nd;
+  bool nok = cok ? seek_row(p, s_end, ns, nr, nd) : false;
 
-  const int64_t sb = p.tile_begin[tile], se_ = p.tile_end[tile];
-  bool tile_active = false;
-  const double fillv = (p.fill == TSDB_FILL_ZERO) ? 0.0 : (double)NAN;
+  SeriesState st;
+  st.carry_slot = -1;
+  st.fcarry = fs_id<F>();
+  bs_init<F>(st.scarry);
+  st.nmax = 0;
+  int lsb = INT32_MAX;
+  double amax = 0.0;
+  bool force_slow = !fast_capable<F>();
+  for (int k = lane; k < K; k += 64) W.pres[k] = 0;
+  WAVE_SYNC();
 
-  for (int64_t s = sb; s < se_; s++) {
-    for (int k = lane; k < K; k += 64) W.pres[k] = 0;
-    WAVE_SYNC();
-    bool any_row = false;
-    int carry_slot = -1;
-    BState carry;
-    bs_init<F>(carry);
-    const int64_t r0 = p.series_row_ptr[s], r1 = p.series_row_ptr[s + 1];
-    for (int64_t r = r0; r < r1; r++) {
-      const RowDesc d = p.rows[r];
-      if ((int64_t)d.base < p.ss) continue;
-      if ((int64_t)d.base >= p.se) break;
-      any_row = true;
-      if (d.flags & ROW_ERR) { if (lane == 0) set_err(p.err, TSDB_E_ILLEGAL_DATA); continue; }
-      const RowGeom g = row_geom(p, d.base);
-      int64_t vcur = 0;
-      for (int64_t c0 = 0; c0 < (int64_t)d.ndp; c0 += CH) {
-        int slot[DPL];
-        double val[DPL];
-        decode_chunk(p, d, g, c0, W, vcur, slot, val);
-        // stage decoded values
-        WAVE_SYNC();
-#pragma unroll
-        for (int j = 0; j < DPL; j++) W.dpv[lane * DPL + j] = val[j];
-        // segment heads
-        const int prev_last = __shfl_up(slot[DPL - 1], 1, 64);
-        int h = 0;
-        bool head[DPL];
-#pragma unroll
-        for (int j = 0; j < DPL; j++) {
-          const int ps = (j == 0) ? (lane == 0 ? -2 : prev_last) : slot[j - 1];
-          head[j] = slot[j] >= 0 && (ps < 0 || ps != slot[j]);
-          h += head[j];
-        }
-        int vend = 0;
-#pragma unroll
-        for (int j = 0; j < DPL; j++) if (slot[j] >= 0) vend = lane * DPL + j + 1;
-        vend = wave_max(vend);
-        const int hincl = wave_incl_sum(h);
-        const int nseg = __shfl(hincl, 63, 64);
-        int pos = hincl - h;
-#pragma unroll
-        for (int j = 0; j < DPL; j++) {
-          if (head[j]) {
-            W.seg_start[pos] = (uint16_t)(lane * DPL + j);
-            W.seg_slot[pos] = slot[j];
-            pos++;
-          }
-        }
-        if (lane == 0) W.seg_start[nseg] = (uint16_t)vend;
-        WAVE_SYNC();
-        if (nseg == 0) continue;
-        // the open bucket of the previous chunk ends unless this chunk continues it
-        const int first_slot = W.seg_slot[0];
-        if (carry_slot >= 0 && first_slot != carry_slot) {
-          if (lane == 0) { W.dense[carry_slot] = bs_final<F>(carry); W.pres[carry_slot] = 1; }
-          carry_slot = -1;
-          bs_init<F>(carry);
-        }
-        for (int b0 = 0; b0 < nseg; b0 += 64) {
-          const int si = b0 + lane;
-          const bool act = si < nseg;
-          BState st;
-          bs_init<F>(st);
-          int myslot = -1;
-          if (act) {
-            myslot = W.seg_slot[si];
-            if (si == 0 && myslot == carry_slot) st = carry;
-            const int e = W.seg_start[si + 1];
-            for (int i = W.seg_start[si]; i < e; i++) bs_add<F>(st, W.dpv[i]);
-            if (si != nseg - 1) { W.dense[myslot] = bs_final<F>(st); W.pres[myslot] = 1; }
-          }
-          if (b0 + 64 >= nseg) {  // last round: the last segment stays open (carry)
-            const int src = (nseg - 1) & 63;
-            carry.a = __shfl(st.a, src, 64);
-            carry.b = __shfl(st.b, src, 64);
-            carry.n = __shfl(st.n, src, 64);
-            carry_slot = __shfl(myslot, src, 64);
-          }
-        }
-        WAVE_SYNC();
+  int64_t c0 = 0;
+  int64_t vcur = 0;
+  Raw rc = {};
+  if (cok && !force_slow && row_uniform(cd)) load_raw(p, cd, 0, rc);
+  bool row_start = true;
+  while (cok) {
+    if (row_start) {
+      if (cd.flags & ROW_ERR) { if (lane == 0) set_err(p.err, TSDB_E_ILLEGAL_DATA); }
+      lsb = min(lsb, cd.lsb);
+      amax = fmax(amax, cd.absmax);
+      row_start = false;
+    }
+    const bool more_in_row = c0 + CH < (int64_t)cd.ndp;
+    // prefetch the next chunk (same row, or the first chunk of the next row)
+    Raw rn = {};
+    if (!force_slow) {
+      if (more_in_row) {
+        if (row_uniform(cd)) load_raw(p, cd, c0 + CH, rn);
+      } else if (nok && row_uniform(nd)) {
+        load_raw(p, nd, 0, rn);
       }
     }
-    if (!any_row) continue;
-    tile_active = true;
-    if (carry_slot >= 0 && lane == 0) { W.dense[carry_slot] = bs_final<F>(carry); W.pres[carry_slot] = 1; }
-    WAVE_SYNC();
-
-    // ---- series -> SpanGroup contributions over the K slots -----------------
-    if (!p.rate) {
-      if (p.fill != TSDB_FILL_NONE && p.mode == MODE_GRID) {
-        // FillingDownsampler (:172-301): every slot, missing -> NaN / 0 / RuntimeException
-        for (int k = lane; k < K; k += 64) {
-          const bool pr = W.pres[k] != 0;
-          if (!pr && p.fill == TSDB_FILL_SCALAR) set_err(p.err, TSDB_E_RUNTIME);
-          contribute(ga, W.part, k, pr ? W.dense[k] : fillv, true);
-        }
-      } else {
-        int prev_present = -1;
-        for (int kb = 0; kb < K; kb += 64) {
-          const int k = kb + lane;
-          const bool pr = k < K && W.pres[k] != 0;
-          const int incl = wave_incl_max(pr ? k : -1);
-          int pp = __shfl_up(incl, 1, 64);
-          if (lane == 0) pp = -1;
-          pp = max(pp, prev_present);
-          if (pr) {
-            const double v = W.dense[k];
-            if (pp >= 0 && pp < k - 1) {
-              const double y0 = W.dense[pp];
-              for (int s2 = pp + 1; s2 < k; s2++) contribute(ga, W.part, s2, interp(p.interp, p, pp, y0, k, v, s2), false);
-            }
-            contribute(ga, W.part, k, v, true);
-          }
-          prev_present = max(prev_present, __shfl(incl, 63, 64));
-        }
-      }
-    } else {
-      // RateSpan over the bucket stream (:121-180), aggregated with PREV semantics
-      // (AggregationIterator ctor rate branch :448-459, nextDoubleValue :744-753)
-      int prev_item = -1, last_surv = -1;
-      long long nsurv = 0;
-      const bool dense_stream = p.fill != TSDB_FILL_NONE && p.mode == MODE_GRID;
-      for (int kb = 0; kb < K; kb += 64) {
-        const int k = kb + lane;
-        const bool inK = k < K;
-        const bool pr = inK && W.pres[k] != 0;
-        const bool item = inK && (dense_stream || pr);
-        if (item && !pr && p.fill == TSDB_FILL_SCALAR) set_err(p.err, TSDB_E_RUNTIME);
-        const int iincl = wave_incl_max(item ? k : -1);
-        int pi = __shfl_up(iincl, 1, 64);
-        if (lane == 0) pi = -1;
-        pi = max(pi, prev_item);
-        bool sv = false;
-        double r = 0.0;
-        if (item) {
-          const double v1 = pr ? W.dense[k] : fillv;
-          double v0 = 0.0;
-          long long t0 = 0;
-          if (pi >= 0) { v0 = W.pres[pi] ? W.dense[pi] : fillv; t0 = p.B0 + (long long)pi * p.I; }
-          const long long t1 = (p.mode == MODE_ALL) ? p.qs : p.B0 + (long long)k * p.I;
-          if (t1 <= t0) set_err(p.err, TSDB_E_ILLEGAL_STATE);
-          const double dt = (double)(t1 - t0) / 1000.0;
-          double diff = v1 - v0;
-          sv = true;
-          if (p.counter && diff < 0) {
-            if (p.drop) {
-              sv = false;
-            } else {
-              diff = (double)p.counter_max - v0 + v1;
-              r = diff / dt;
-              if (p.reset_value > 0 && r > (double)p.reset_value) r = 0.0;
-            }
-          } else {
-            r = diff / dt;
-          }
-          if (sv) W.rate[k] = r;
-        }
-        WAVE_SYNC();
-        const int cincl = wave_incl_sum(sv ? 1 : 0);
-        const long long m = nsurv + (cincl - (sv ? 1 : 0));
-        const int sincl = wave_incl_max(sv ? k : -1);
-        int ps = __shfl_up(sincl, 1, 64);
-        if (lane == 0) ps = -1;
-        ps = max(ps, last_surv);
-        if (sv) {
-          if (m == 1) {
-            const double r0 = W.rate[ps];
-            for (int s2 = 0; s2 < k; s2++) contribute(ga, W.part, s2, r0, false);
-            contribute(ga, W.part, k, r, true);
-          } else if (m >= 2) {
-            const double rp = W.rate[ps];
-            for (int s2 = ps + 1; s2 < k; s2++) contribute(ga, W.part, s2, rp, false);
-            contribute(ga, W.part, k, r, true);
-          }
-        }
-        prev_item = max(prev_item, __shfl(iincl, 63, 64));
-        last_surv = max(last_surv, __shfl(sincl, 63, 64));
-        nsurv += __shfl(cincl, 63, 64);
-        WAVE_SYNC();
-      }
+    if (!force_slow && !(cd.flags & ROW_ERR)) {
+      const RowGeom g = row_geom(p, cd.base);
+      int slot[DPL];
+      double val[DPL];
+      if (row_uniform(cd)) decode_raw(p, cd, g, c0, rc, slot, val);
+      else decode_generic(p, cd, g, c0, W, vcur, slot, val);
+      fast_chunk<F>(W, st, slot, val);
     }
-    WAVE_SYNC();
+    if (more_in_row) {
+      c0 += CH;
+      rc = rn;
+      continue;
+    }
+    // row done
+    const bool series_end = !nok || ns != cs;
+    if (series_end) {
+      bool slow = force_slow;
+      if (!slow) {
+        if (st.carry_slot >= 0 && lane == 0) emit_bucket<F>(W, st.carry_slot, fs_final<F>(st.fcarry));
+        if (st.carry_slot >= 0) st.nmax = max(st.nmax, st.fcarry.n);
+        if (needs_cert<F>()) {
+          // all partial sums exactly representable => any association order == Java's order
+          const int L = (F == F_SQUARESUM) ? 2 * lsb : lsb;
+          const double A = (F == F_SQUARESUM) ? amax * amax : amax;
+          const bool ok = (A == 0.0) ||
+                          (lsb != INT32_MAX && !isinf(A) && (double)st.nmax * A * (1.0 + 1e-12) <= ldexp(1.0, 52 + L));
+          slow = !ok;
+        }
+      }
+      if (slow) series_slow<F>(p, W, cs, K);
+      emit_series(p, W, K);
+      // next series
+      for (int k = lane; k < K; k += 64) W.pres[k] = 0;
+      WAVE_SYNC();
+      st.carry_slot = -1;
+      st.fcarry = fs_id<F>();
+      bs_init<F>(st.scarry);
+      st.nmax = 0;
+      lsb = INT32_MAX;
+      amax = 0.0;
+    }
+    cs = ns;
+    cr = nr;
+    cd = nd;
+    cok = nok;
+    c0 = 0;
+    vcur = 0;
+    rc = rn;
+    row_start = true;
+    if (cok) {
+      ns = cs;
+      nr = cr + 1;
+      nok = seek_row(p, s_end, ns, nr, nd);
+    }
   }
 
-  if (tile_active && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
-  WAVE_SYNC();
-  double* ga_ = p.part.a + tile * K;
-  double* gb_ = p.part.b + tile * K;
-  uint32_t* gn_ = p.part.n + tile * K;
-  uint32_t* gf_ = p.part.f + tile * K;
-  for (int k = lane; k < K; k += 64) {
-    ga_[k] = W.part.a[k];
-    gb_[k] = W.part.b[k];
-    gn_[k] = W.part.n[k];
-    gf_[k] = W.part.f[k];
+  if (!GSLOT) {
+    WAVE_SYNC();
+    double* ga_ = p.part.a + tile * K;
+    double* gb_ = p.part.b + tile * K;
+    uint32_t* gn_ = p.part.n + tile * K;
+    uint32_t* gf_ = p.part.f + tile * K;
+    for (int k = lane; k < K; k += 64) {
+      ga_[k] = W.part.a[k];
+      gb_[k] = W.part.b[k];
+      gn_[k] = W.part.n[k];
+      gf_[k] = W.part.f[k];
+    }
   }
 }
 
@@ -1051,42 +1431,51 @@ __global__ __launch_bounds__(256) void k_synth_write(SynthParams p) {
 }
 
 // ---- launchers -------------------------------------------------------------------
-hipError_t launch_index(const uint8_t* qual, const uint8_t*, RowDesc* rows, int64_t n_rows, int32_t* err,
+hipError_t launch_index(const uint8_t* qual, const uint8_t* val, RowDesc* rows, int64_t n_rows, int32_t* err,
                         hipStream_t s) {
   if (n_rows == 0) return hipSuccess;
   const int64_t blocks = std::min<int64_t>((n_rows + 3) / 4, 65536);
-  hipLaunchKernelGGL(k_index, dim3((unsigned)blocks), dim3(256), 0, s, qual, rows, n_rows, err);
+  hipLaunchKernelGGL(k_index, dim3((unsigned)blocks), dim3(256), 0, s, qual, val, rows, n_rows, err);
   return hipGetLastError();
 }
 
-template <int F>
+template <int F, bool G>
 static hipError_t launch_grid_t(const GridParams& p, hipStream_t s) {
   const int64_t blocks = (p.n_tiles + p.waves - 1) / p.waves;
   const size_t lds = (size_t)p.wave_lds * p.waves;
   if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_grid<F>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute((const void*)k_grid<F, G>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_grid<F>, dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p);
+  hipLaunchKernelGGL((k_grid<F, G>), dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p);
   return hipGetLastError();
+}
+
+template <int F>
+static hipError_t launch_grid_f(const GridParams& p, hipStream_t s) {
+  return p.g_dense ? launch_grid_t<F, true>(p, s) : launch_grid_t<F, false>(p, s);
 }
 
 hipError_t launch_grid(const GridParams& p, int f, hipStream_t s) {
   if (p.n_tiles == 0) return hipSuccess;
   switch (f) {
-    case F_SUM: return launch_grid_t<F_SUM>(p, s);
-    case F_AVG: return launch_grid_t<F_AVG>(p, s);
-    case F_COUNT: return launch_grid_t<F_COUNT>(p, s);
-    case F_SQUARESUM: return launch_grid_t<F_SQUARESUM>(p, s);
-    case F_MIN: return launch_grid_t<F_MIN>(p, s);
-    case F_MAX: return launch_grid_t<F_MAX>(p, s);
-    case F_DEV: return launch_grid_t<F_DEV>(p, s);
-    case F_FIRST: return launch_grid_t<F_FIRST>(p, s);
-    case F_LAST: return launch_grid_t<F_LAST>(p, s);
-    case F_DIFF: return launch_grid_t<F_DIFF>(p, s);
-    case F_MULT: return launch_grid_t<F_MULT>(p, s);
+    case F_SUM: return launch_grid_f<F_SUM>(p, s);
+    case F_AVG: return launch_grid_f<F_AVG>(p, s);
+    case F_COUNT: return launch_grid_f<F_COUNT>(p, s);
+    case F_SQUARESUM: return launch_grid_f<F_SQUARESUM>(p, s);
+    case F_MIN: return launch_grid_f<F_MIN>(p, s);
+    case F_MAX: return launch_grid_f<F_MAX>(p, s);
+    case F_DEV: return launch_grid_f<F_DEV>(p, s);
+    case F_FIRST: return launch_grid_f<F_FIRST>(p, s);
+    case F_LAST: return launch_grid_f<F_LAST>(p, s);
+    case F_DIFF: return launch_grid_f<F_DIFF>(p, s);
+    case F_MULT: return launch_grid_f<F_MULT>(p, s);
   }
   return hipErrorInvalidValue;
+}
+
+int64_t grid_wave_lds(int64_t K, bool rate, bool gslot) {
+  return align16(fixed_lds_bytes() + (gslot ? 0 : slot_lds_bytes(K, rate)));
 }
 
 hipError_t launch_reduce(const ReduceParams& p, hipStream_t s) {
