@@ -128,6 +128,9 @@ typedef struct {
   double total_ms;
   int64_t datapoints;            /* raw datapoints decoded */
   int64_t bytes;                 /* algorithmic HBM bytes read (qualifiers+values+row index) */
+  int64_t tiles;                 /* series tiles of the query */
+  int64_t redo_tiles;            /* tiles the streaming kernel handed to the general kernel */
+  double fast_ms;                /* streaming kernel (k_fast) alone; 0 when not used */
 } tsdbhip_timing;
 
 /* ---- library-level helpers (host logic of the reference, restated) ------- */

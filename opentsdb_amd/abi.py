@@ -122,6 +122,9 @@ class Timing(C.Structure):
         ("total_ms", C.c_double),
         ("datapoints", C.c_int64),
         ("bytes", C.c_int64),
+        ("tiles", C.c_int64),
+        ("redo_tiles", C.c_int64),
+        ("fast_ms", C.c_double),
     ]
 
 

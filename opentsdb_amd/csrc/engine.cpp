@@ -7,6 +7,7 @@
 #include <cctype>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <numeric>
@@ -136,7 +137,10 @@ struct tsdbhip_ctx {
   bool none_tiles_ready = false;
   DevBuf n_tb, n_te, n_tg, n_gtp;
   // scratch
-  DevBuf pa, pb, pn, pf, out_val, out_flag, gact, err, g_dense, g_pres, g_rate;
+  DevBuf pa, pb, pn, pf, out_val, out_flag, gact, err, g_dense, g_pres, g_rate, redo, redo_n;
+  // dominant uniform row class of the batch (k_fast specialisation), 0 = none
+  int fast_qw = 0, fast_vl = 0;
+  bool fast_used = false;
   tsdbhip_timing timing{};
 };
 
@@ -286,7 +290,9 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   release_batch(c);
-  for (DevBuf* b : {&c->pa, &c->pb, &c->pn, &c->pf, &c->out_val, &c->out_flag, &c->gact, &c->err, &c->g_dense, &c->g_pres, &c->g_rate}) b->release();
+  for (DevBuf* b : {&c->pa, &c->pb, &c->pn, &c->pf, &c->out_val, &c->out_flag, &c->gact, &c->err, &c->g_dense,
+                    &c->g_pres, &c->g_rate, &c->redo, &c->redo_n})
+    b->release();
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -370,12 +376,22 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
   c->h_base.resize(c->n_rows);
   c->h_qlen.resize(c->n_rows);
   c->h_vlen.resize(c->n_rows);
+  int64_t cls[2][2] = {{0, 0}, {0, 0}};   // [qw 2/4][vl 4/8] uniform float rows
   for (int64_t r = 0; r < c->n_rows; r++) {
     c->h_ndp[r] = back[r].ndp;
     c->h_base[r] = back[r].base;
     c->h_qlen[r] = back[r].qlen;
     c->h_vlen[r] = back[r].vlen;
+    const uint32_t f = back[r].flags;
+    const uint32_t qw = f & ROW_QW_MASK, vl = (f & ROW_VL_MASK) >> ROW_VL_SHIFT;
+    if ((f & ROW_ALLF) && !(f & (ROW_ERR | ROW_NAN | ROW_UNSORTED)) && (qw == 2 || qw == 4) && (vl == 4 || vl == 8))
+      cls[qw == 4][vl == 8] += back[r].ndp;
   }
+  c->fast_qw = c->fast_vl = 0;
+  int64_t best = 0;
+  for (int a = 0; a < 2; a++)
+    for (int b2 = 0; b2 < 2; b2++)
+      if (cls[a][b2] > best) { best = cls[a][b2]; c->fast_qw = a ? 4 : 2; c->fast_vl = b2 ? 8 : 4; }
   // malformed rows are reported lazily, when a query reads them (as the reference does)
   return build_tiles(c);
 }
@@ -426,9 +442,11 @@ extern "C" int tsdbhip_load(tsdbhip_ctx* c, const tsdbhip_batch* b) {
     c->h_srp[i + 1] = (int64_t)rd.size();
   }
   // rows of a series must be in base-time order (Span.checkRowOrder): stable sort per series
-  for (int64_t i = 0; i < c->n_series; i++)
+  for (int64_t i = 0; i < c->n_series; i++) {
     std::stable_sort(rd.begin() + c->h_srp[i], rd.begin() + c->h_srp[i + 1],
                      [](const RowDesc& x, const RowDesc& y) { return x.base < y.base; });
+    if (c->h_srp[i + 1] > c->h_srp[i]) rd[c->h_srp[i]].flags |= ROW_SFIRST;
+  }
   c->n_rows = (int64_t)rd.size();
   c->qual_bytes = qtot;
   c->val_bytes = vtot;
@@ -541,6 +559,7 @@ extern "C" int tsdbhip_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp) {
       d.qlen = (uint32_t)(rn[h] * qw);
       d.voff = vtot;
       d.vlen = vbytes[s * R + h];
+      d.flags = h == 0 ? ROW_SFIRST : 0;
       vtot += align16(d.vlen);
     }
   }
@@ -717,7 +736,34 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   gp.part = Partials{c->pa.as<double>(), c->pb.as<double>(), c->pn.as<uint32_t>(), c->pf.as<uint32_t>()};
   gp.group_active = c->gact.as<uint32_t>();
   gp.err = c->err.as<int32_t>();
+  // streaming kernel first (when the batch's row class and the query allow it), then the
+  // general kernel over the tiles it handed back
+  bool fast = false;
+  if (P.mode == MODE_GRID && c->fast_qw && fast_supported(P.f, c->fast_qw, c->fast_vl) && P.I <= (1LL << 29) &&
+      fast_wave_lds(K, q->rate != 0) <= 32 * 1024 && K > 0) {
+    const char* env = std::getenv("TSDBHIP_FAST");
+    fast = !(env && env[0] == '0');
+  }
+  c->fast_used = fast;
   HIP_OK(hipEventRecord(c->ev[0], c->stream));
+  if (fast) {
+    GridParams fp = gp;
+    fp.unit_s = (c->fast_qw == 2 && P.I % 1000 == 0 && P.B0 % 1000 == 0) ? 1 : 0;
+    fp.In = (int32_t)(fp.unit_s ? P.I / 1000 : P.I);
+    fp.B0n = fp.unit_s ? P.B0 / 1000 : P.B0;
+    fp.rcpn = std::nextafter(1.0 / (double)fp.In, INFINITY);
+    fp.wave_lds = (int32_t)fast_wave_lds(K, q->rate != 0);
+    fp.waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / fp.wave_lds));
+    HIP_OK(c->redo.ensure(std::max<int64_t>(1, nt) * 4));
+    HIP_OK(c->redo_n.ensure(16));
+    HIP_OK(hipMemsetAsync(c->redo_n.p, 0, 4, c->stream));
+    fp.redo_list = c->redo.as<int32_t>();
+    fp.redo_n = c->redo_n.as<int32_t>();
+    HIP_OK(launch_fast(fp, P.f, c->fast_qw, c->fast_vl, c->stream));
+    HIP_OK(hipEventRecord(c->ev[3], c->stream));
+    gp.tile_list = c->redo.as<int32_t>();
+    gp.tile_list_n = c->redo_n.as<int32_t>();
+  }
   HIP_OK(launch_grid(gp, P.f, c->stream));
   HIP_OK(hipEventRecord(c->ev[1], c->stream));
   if (do_reduce) {
@@ -831,13 +877,19 @@ extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_resul
   }
   if (G) HIP_OK(hipMemcpyAsync(act.data(), c->gact.p, G * 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
+  int32_t redo_n = 0;
+  if (c->fast_used) HIP_OK(hipMemcpyAsync(&redo_n, c->redo_n.p, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
-  float t01 = 0, t12 = 0;
+  float t01 = 0, t12 = 0, t03 = 0;
   (void)hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
   (void)hipEventElapsedTime(&t12, c->ev[1], c->ev[2]);
+  if (c->fast_used) (void)hipEventElapsedTime(&t03, c->ev[0], c->ev[3]);
   c->timing.decode_downsample_ms = t01;
   c->timing.group_reduce_ms = t12;
   c->timing.total_ms = t01 + t12;
+  c->timing.fast_ms = t03;
+  c->timing.tiles = P.none ? c->n_series : (int64_t)c->tb.size();
+  c->timing.redo_tiles = c->fast_used ? redo_n : c->timing.tiles;
   account(c, P);
   if (err) return fail(err, "error raised by the device path");
   if (P.mode == MODE_ALL) {

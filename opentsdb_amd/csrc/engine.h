@@ -27,6 +27,11 @@ enum : uint32_t {
   ROW_VL_SHIFT = 8,         // uniform value length 1/2/4/8, 0 = variable (vle ints)
   ROW_VL_MASK = 0xF00,
   ROW_ERR = 0x10000,        // malformed cell (IllegalDataException when decoded)
+  ROW_ALLF = 0x20000,       // every value is floating point
+  ROW_NAN = 0x40000,        // some value is NaN
+  ROW_NEGZ = 0x80000,       // some value is -0.0
+  ROW_UNSORTED = 0x100000,  // datapoint offsets not strictly increasing
+  ROW_SFIRST = 0x200000,    // first row of its series (set by the host at load)
 };
 
 // Per-tile partial group state, structure of arrays, [tile][K].
@@ -87,6 +92,17 @@ struct GridParams {
   Partials part;
   uint32_t* group_active;
   int32_t* err;          // first error code (atomicCAS from 0)
+  // k_grid over a tile list (tiles k_fast handed back): tile = tile_list[i], i < *tile_list_n
+  const int32_t* tile_list;
+  const int32_t* tile_list_n;
+  // k_fast: geometry in "n-units" (seconds when every row has second qualifiers and the
+  // interval / slot origin are whole seconds, else milliseconds) and the redo list
+  int32_t unit_s;        // 1: n-units are seconds
+  int32_t In;            // interval in n-units
+  int64_t B0n;           // slot-0 timestamp in n-units
+  double rcpn;           // 1/In rounded up (floor(n * rcpn) == n / In for 0 <= n < 2^50)
+  int32_t* redo_list;
+  int32_t* redo_n;
 };
 
 struct ReduceParams {
@@ -121,6 +137,11 @@ struct SynthParams {
 hipError_t launch_index(const uint8_t* qual, const uint8_t* val, RowDesc* rows, int64_t n_rows, int32_t* err,
                         hipStream_t s);
 hipError_t launch_grid(const GridParams& p, int ds_function_class, hipStream_t s);
+// k_fast: uniform float rows of one (qualifier width, value length) class; returns
+// hipErrorNotSupported when no specialisation exists for (f, qw, vl)
+bool fast_supported(int ds_function_class, int qw, int vl);
+hipError_t launch_fast(const GridParams& p, int ds_function_class, int qw, int vl, hipStream_t s);
+int64_t fast_wave_lds(int64_t K, bool rate);
 hipError_t launch_reduce(const ReduceParams& p, hipStream_t s);
 int64_t grid_wave_lds(int64_t K, bool rate, bool gslot);
 hipError_t launch_synth_sizes(const SynthParams& p, hipStream_t s);

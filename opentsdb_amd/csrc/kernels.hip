@@ -56,21 +56,25 @@ __device__ __forceinline__ int wave_incl_max(int x) {
   }
   return x;
 }
+// Butterfly reductions: every lane holds the result; readfirstlane tells the compiler so
+// (keeps loop-carried state that depends on it in SGPRs / uniform control flow).
 __device__ __forceinline__ int wave_max(int x) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) x = max(x, __shfl_xor(x, d, 64));
-  return x;
+  return __builtin_amdgcn_readfirstlane(x);
 }
 __device__ __forceinline__ int wave_min(int x) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) x = min(x, __shfl_xor(x, d, 64));
-  return x;
+  return __builtin_amdgcn_readfirstlane(x);
 }
 __device__ __forceinline__ long long wave_sum64(long long x) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-  return x;
+  return __builtin_amdgcn_readfirstlane(x);
 }
+// value of lane l (uniform result)
+__device__ __forceinline__ int lane_bcast(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
 
 // ---- big-endian value decode (RowSeq.extractIntegerValue / extractFloatingPointValue,
 //      src/core/RowSeq.java:233-266); returns false on an illegal length -------------
@@ -372,10 +376,12 @@ __global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual,
     }
     // walk every datapoint: validate qualifier/value lengths, certificate stats
     bool bad = qlen == 0;
+    bool allf = true, hasnan = false, negz = false, unsorted = false;
     int lsbmin = INT32_MAX;
     double amax = 0.0;
     long long vcarry = 0;
     uint32_t qcarry = 0;
+    long long prev_off = -1;   // offset (ms) of the previous datapoint
     for (uint32_t i0 = 0; i0 < ndp; i0 += 64) {
       const uint32_t i = i0 + lane;
       const bool in = i < ndp;
@@ -404,6 +410,18 @@ __global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual,
       }
       const int len = in ? (int)(fb & 7) + 1 : 0;
       const bool fl = (fb & 8) != 0;
+      // offset order (strictly increasing in a well-formed compacted cell)
+      long long off = -1;
+      if (in) {
+        if (w == 4) off = (long long)((((uint32_t)q[qpos] << 24) | ((uint32_t)q[qpos + 1] << 16) |
+                                       ((uint32_t)q[qpos + 2] << 8) | q[qpos + 3]) & 0x0FFFFFC0u) >> 6;
+        else off = (long long)((((uint32_t)q[qpos] << 8) | q[qpos + 1]) >> 4) * 1000;
+      }
+      long long po = __shfl_up(off, 1, 64);
+      if (lane == 0) po = prev_off;
+      if (in && off <= po) unsorted = true;
+      prev_off = __shfl(off, (int)min((uint32_t)63, ndp - 1 - i0), 64);
+      if (in && !fl) allf = false;
       if (in && (fl ? (len != 4 && len != 8) : (len == 3 || (len >= 5 && len <= 7)))) bad = true;
       const int incl = wave_incl_sum(len);
       const long long vo = vcarry + incl - len;
@@ -413,6 +431,8 @@ __global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual,
         for (int b = 0; b < len; b++) bits = (bits << 8) | v[vo + b];
         double x = 0.0;
         decode_value(bits, len, fl, x);
+        if (isnan(x)) hasnan = true;
+        if (x == 0.0 && signbit(x)) negz = true;
         if (!isnan(x)) {
           const double ax = fabs(x);
           if (ax > amax || isinf(ax)) amax = fmax(amax, ax);
@@ -422,6 +442,10 @@ __global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual,
     }
     if (vcarry > (long long)d.vlen) bad = true;
     bad = __any(bad);
+    allf = __all(allf);
+    hasnan = __any(hasnan);
+    negz = __any(negz);
+    unsorted = __any(unsorted);
     lsbmin = wave_min(lsbmin);
 #pragma unroll
     for (int dd = 32; dd >= 1; dd >>= 1) amax = fmax(amax, __shfl_xor(amax, dd, 64));
@@ -430,6 +454,11 @@ __global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual,
         flags |= ROW_ERR;
         set_err(err, TSDB_E_ILLEGAL_DATA);
       }
+      if (allf) flags |= ROW_ALLF;
+      if (hasnan) flags |= ROW_NAN;
+      if (negz) flags |= ROW_NEGZ;
+      if (unsorted) flags |= ROW_UNSORTED;
+      flags |= d.flags & ROW_SFIRST;
       d.ndp = ndp;
       d.flags = flags;
       d.lsb = lsbmin;
@@ -953,7 +982,7 @@ __device__ __forceinline__ void emit_series(const GridParams& p, const WaveLds& 
           }
           contribute(ga, W.part, k, v, true);
         }
-        prev_present = max(prev_present, __shfl(incl, 63, 64));
+        prev_present = max(prev_present, lane_bcast(incl, 63));
       }
     }
   } else {
@@ -1015,9 +1044,9 @@ __device__ __forceinline__ void emit_series(const GridParams& p, const WaveLds& 
           contribute(ga, W.part, k, r, true);
         }
       }
-      prev_item = max(prev_item, __shfl(iincl, 63, 64));
-      last_surv = max(last_surv, __shfl(sincl, 63, 64));
-      nsurv += __shfl(cincl, 63, 64);
+      prev_item = max(prev_item, lane_bcast(iincl, 63));
+      last_surv = max(last_surv, lane_bcast(sincl, 63));
+      nsurv += lane_bcast(cincl, 63);
       WAVE_SYNC();
     }
   }
@@ -1073,8 +1102,12 @@ template <int F, bool GSLOT>
 __global__ __launch_bounds__(256) void k_grid(GridParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
-  const int wave = threadIdx.x >> 6;
-  const int64_t tile = (int64_t)blockIdx.x * p.waves + wave;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (scalar) tile index
+  int64_t tile = (int64_t)blockIdx.x * p.waves + wave;
+  if (p.tile_list) {
+    if (tile >= (int64_t)*p.tile_list_n) return;
+    tile = p.tile_list[tile];
+  }
   if (tile >= p.n_tiles) return;
   const int K = (int)p.K;
   const WaveLds W = carve<GSLOT>(p, smem + (int64_t)wave * p.wave_lds, tile, K, p.rate != 0);
@@ -1195,6 +1228,383 @@ __global__ __launch_bounds__(256) void k_grid(GridParams p) {
   }
 }
 
+// ---- k_fast: the streaming kernel ------------------------------------------------
+// For tiles whose rows are all "uniform float" cells of one (qualifier width QW, value
+// length VL) class, sorted, NaN-free, and whose buckets pass the exactness certificate,
+// the order in which a bucket's values are added cannot change the bit pattern of the
+// result.  k_fast therefore reduces each lane's 8 datapoints in registers (at most two
+// bucket runs per lane) and folds them into per-series slot accumulators in LDS with
+// LDS atomics -- no per-chunk wave scan, no carry -- while a D-deep ring of chunk loads
+// keeps ~D x 3 KB per wave in flight.  A tile that breaks any premise (other row class,
+// malformed / NaN row, failed certificate) is appended to the redo list and recomputed
+// by k_grid, the general (sequential-order) kernel.
+struct FMeta {
+  uint32_t bits;   // datapoints of the row from this chunk's start | FM_* flags
+  int32_t rrel;    // row index relative to the tile's first row
+};
+enum : uint32_t { FM_NV = 0x1FFFFFFFu, FM_OK = 1u << 29, FM_NEWSER = 1u << 30, FM_NEWROW = 1u << 31 };
+
+template <int QW, int VL>
+struct FRaw {
+  uint4 q[QW / 2];   // 8 qualifiers of QW bytes
+  uint4 v[VL / 2];   // 8 values of VL bytes
+};
+
+template <int F>
+__device__ __forceinline__ constexpr bool fast_f() {
+  return F == F_SUM || F == F_AVG || F == F_COUNT || F == F_SQUARESUM || F == F_MIN || F == F_MAX;
+}
+
+__host__ __device__ inline int64_t fast_slot_bytes(int64_t K, bool rate) {
+  // acc (f64, also the dense bucket values), cnt (u32), pres (u8), [rate f64], partials
+  return align16(K * 8) + align16(K * 4) + align16(K) + (rate ? align16(K * 8) : 0) + align16(K * 8) * 2 +
+         align16(K * 4) * 2;
+}
+
+struct FastLds {
+  double* acc;
+  uint32_t* cnt;
+  WaveLds w;   // dense == acc, pres, rate, part
+};
+
+__device__ __forceinline__ FastLds fast_carve(unsigned char* base, int64_t K, bool rate) {
+  FastLds f;
+  int64_t o = 0;
+  f.acc = (double*)(base + o); o += align16(K * 8);
+  f.cnt = (uint32_t*)(base + o); o += align16(K * 4);
+  f.w.dense = f.acc;
+  f.w.pres = base + o; o += align16(K);
+  if (rate) { f.w.rate = (double*)(base + o); o += align16(K * 8); } else { f.w.rate = nullptr; }
+  f.w.part.a = (double*)(base + o); o += align16(K * 8);
+  f.w.part.b = (double*)(base + o); o += align16(K * 8);
+  f.w.part.n = (uint32_t*)(base + o); o += align16(K * 4);
+  f.w.part.f = (uint32_t*)(base + o); o += align16(K * 4);
+  f.w.dpv = nullptr; f.w.vbuf = nullptr; f.w.mq = nullptr; f.w.mv = nullptr;
+  f.w.seg_slot = nullptr; f.w.seg_start = nullptr;
+  return f;
+}
+
+template <int F>
+__device__ __forceinline__ double fast_identity() {
+  return F == F_MIN ? (double)INFINITY : (F == F_MAX ? -(double)INFINITY : 0.0);
+}
+
+template <int F>
+__device__ __forceinline__ void fast_fold(const FastLds& L, int k, double v, uint32_t n) {
+  if (F == F_MIN) __hip_atomic_fetch_min(&L.acc[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  else if (F == F_MAX) __hip_atomic_fetch_max(&L.acc[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  else if (F != F_COUNT) __hip_atomic_fetch_add(&L.acc[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  __hip_atomic_fetch_add(&L.cnt[k], n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+template <int QW, int VL>
+__device__ __forceinline__ bool fast_row_ok(uint32_t flags, bool minmax) {
+  const uint32_t want = (uint32_t)QW | ((uint32_t)VL << ROW_VL_SHIFT) | ROW_ALLF;
+  const uint32_t mask = ROW_QW_MASK | ROW_VL_MASK | ROW_ALLF | ROW_ERR | ROW_NAN | ROW_UNSORTED |
+                        (minmax ? ROW_NEGZ : 0u);
+  return (flags & mask) == want;
+}
+
+// Row walker: the tile's rows in order, filtered to the scan range, cut in CH-datapoint
+// chunks.  Descriptors are read with scalar loads, one row ahead.
+struct FDesc {       // the descriptor fields the walker needs
+  uint64_t qoff, voff;
+  uint32_t base, ndp, flags;
+};
+
+__device__ __forceinline__ FDesc fdesc(const RowDesc* __restrict__ rows, int64_t r) {
+  const RowDesc& x = rows[r];
+  FDesc d;
+  d.qoff = x.qoff; d.voff = x.voff; d.base = x.base; d.ndp = x.ndp; d.flags = x.flags;
+  return d;
+}
+
+struct FWalk {
+  int64_t r0;        // first row of the tile
+  int32_t r, rend;   // current row, end of the tile's rows (relative to r0)
+  int32_t c0;        // next chunk offset inside row r
+  int32_t sf;        // a series start was passed since the last issued chunk
+  FDesc d, nd;       // rows r and r + 1
+};
+
+__device__ __forceinline__ void fwalk_next_row(const RowDesc* __restrict__ rows, FWalk& w) {
+  w.r++;
+  w.c0 = 0;
+  w.d = w.nd;
+  if (w.r + 1 < w.rend) w.nd = fdesc(rows, w.r0 + w.r + 1);
+}
+
+// 0 = chunk issued, 1 = end of tile, 2 = row the kernel cannot take (redo the tile)
+template <int F, int QW, int VL>
+__device__ __forceinline__ int fast_issue(const GridParams& p, const RowDesc* __restrict__ rows, FWalk& w,
+                                          FRaw<QW, VL>& b, FMeta& m) {
+  m.bits = 0;
+  for (;;) {
+    if (w.r >= w.rend) return 1;
+    if (w.c0 == 0) {
+      w.sf |= (w.d.flags & ROW_SFIRST) != 0;
+      if ((int64_t)w.d.base < p.ss || (int64_t)w.d.base >= p.se) { fwalk_next_row(rows, w); continue; }
+      if (!fast_row_ok<QW, VL>(w.d.flags, F == F_MIN || F == F_MAX)) return 2;
+    }
+    if (w.c0 < (int64_t)w.d.ndp) break;
+    fwalk_next_row(rows, w);
+  }
+  const int lane = lane_id();
+  const int nv0 = (int)w.d.ndp - w.c0;
+  m.bits = (uint32_t)nv0 | FM_OK | (w.sf ? FM_NEWSER : 0u) | (w.c0 == 0 ? FM_NEWROW : 0u);
+  m.rrel = w.r;
+  w.sf = 0;
+  // lanes past the end of the row re-read its first datapoints (in bounds, ignored)
+  const int64_t i0 = (lane * DPL < nv0) ? w.c0 + (int64_t)lane * DPL : 0;
+  const uint4* q = reinterpret_cast<const uint4*>(p.qual + w.d.qoff + i0 * QW);
+  const uint4* v = reinterpret_cast<const uint4*>(p.val + w.d.voff + i0 * VL);
+#pragma unroll
+  for (int k = 0; k < QW / 2; k++) b.q[k] = q[k];
+#pragma unroll
+  for (int k = 0; k < VL / 2; k++) b.v[k] = v[k];
+  w.c0 += CH;
+  return 0;
+}
+
+// offset field of datapoint j (seconds for QW == 2, milliseconds for QW == 4)
+template <int QW, int VL>
+__device__ __forceinline__ uint32_t f_field(const FRaw<QW, VL>& b, int j) {
+  if (QW == 2) {
+    const uint32_t wd = (j >> 1) == 0 ? b.q[0].x : (j >> 1) == 1 ? b.q[0].y : (j >> 1) == 2 ? b.q[0].z : b.q[0].w;
+    const uint32_t t = __builtin_bswap32(wd);
+    return (j & 1) ? ((t >> 4) & 0xFFF) : (t >> 20);
+  } else {
+    const uint4 u = b.q[j >> 2];
+    const uint32_t wd = (j & 3) == 0 ? u.x : (j & 3) == 1 ? u.y : (j & 3) == 2 ? u.z : u.w;
+    return (__builtin_bswap32(wd) >> 6) & 0x3FFFFF;
+  }
+}
+
+template <int QW, int VL>
+__device__ __forceinline__ double f_value(const FRaw<QW, VL>& b, int j) {
+  if (VL == 4) {
+    const uint4 u = b.v[j >> 2];
+    const uint32_t wd = (j & 3) == 0 ? u.x : (j & 3) == 1 ? u.y : (j & 3) == 2 ? u.z : u.w;
+    return (double)__uint_as_float(__builtin_bswap32(wd));
+  } else {
+    const uint4 u = b.v[j >> 1];
+    const uint32_t hi = (j & 1) ? u.z : u.x;
+    const uint32_t lo = (j & 1) ? u.w : u.y;
+    return __longlong_as_double((long long)(((uint64_t)__builtin_bswap32(hi) << 32) | __builtin_bswap32(lo)));
+  }
+}
+
+struct FGeom {
+  int q0, r0;   // slot at the row base, remainder in n-units (r0 < 0: row starts before slot 0)
+};
+
+__device__ __forceinline__ FGeom fgeom(const GridParams& p, uint32_t base) {
+  const int64_t rel = p.unit_s ? (int64_t)base - p.B0n : (int64_t)base * 1000 - p.B0n;
+  FGeom g;
+  if (rel >= 0) {
+    g.q0 = (int)((double)rel * p.rcpn);
+    g.r0 = (int)(rel - (int64_t)g.q0 * p.In);
+  } else {
+    g.q0 = 0;
+    g.r0 = (int)rel;
+  }
+  return g;
+}
+
+__device__ __forceinline__ int f_slot(const GridParams& p, const FGeom& m, int n) {
+  return m.q0 + (int)((double)n * p.rcpn);
+}
+
+// Folds one chunk into the series' slot accumulators.
+template <int F, int QW, int VL, bool FULL>
+__device__ __forceinline__ void fast_chunk(const GridParams& p, const FastLds& L, const FRaw<QW, VL>& b,
+                                           const FGeom& m, int nv0, int K) {
+  const int lane = lane_id();
+  const int nvl = FULL ? DPL : max(0, min(DPL, nv0 - lane * DPL));
+  const int uq = (QW == 2 && !p.unit_s) ? 1000 : 1;
+  uint32_t fld[DPL];
+#pragma unroll
+  for (int j = 0; j < DPL; j++) fld[j] = f_field<QW, VL>(b, j);
+  uint32_t flast = fld[DPL - 1];
+  if (!FULL) {
+#pragma unroll
+    for (int j = 0; j < DPL - 1; j++) if (j == nvl - 1) flast = fld[j];
+  }
+  const int n0 = m.r0 + (int)fld[0] * uq;
+  const int nl = m.r0 + (int)flast * uq;
+  const int sfirst = n0 >= 0 ? f_slot(p, m, n0) : -1;
+  const int slast = nl >= 0 ? f_slot(p, m, nl) : -1;
+  const bool simple = nvl == 0 || (n0 >= 0 && slast < K && slast <= sfirst + 1);
+  if (__builtin_expect(__all(simple), 1)) {
+    if (nvl == 0) return;
+    // first run: offsets below the next bucket boundary
+    const int Dn = (sfirst - m.q0 + 1) * p.In - m.r0;   // > 0
+    const uint32_t Tf = (uint32_t)((Dn + uq - 1) / uq);
+    double P = fast_identity<F>(), sF = 0.0, mL = fast_identity<F>();
+    int cF = 0;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      const bool valid = FULL || j < nvl;
+      const bool inF = valid && fld[j] < Tf;
+      double x = f_value<QW, VL>(b, j);
+      if (F == F_SQUARESUM) x = x * x;
+      if (F == F_MIN) {
+        P = fmin(P, valid ? x : (double)INFINITY);
+        if (!inF && valid) mL = fmin(mL, x);
+      } else if (F == F_MAX) {
+        P = fmax(P, valid ? x : -(double)INFINITY);
+        if (!inF && valid) mL = fmax(mL, x);
+      } else if (F != F_COUNT) {
+        P += valid ? x : 0.0;
+      }
+      if (inF) { sF = P; cF = j + 1; }
+    }
+    const int nL = nvl - cF;
+    double sL;
+    if (F == F_MIN || F == F_MAX) sL = mL;
+    else sL = P - sF;   // exact: every partial sum is representable (certificate)
+    fast_fold<F>(L, sfirst, sF, (uint32_t)cF);
+    if (nL > 0) fast_fold<F>(L, sfirst + 1, sL, (uint32_t)nL);
+  } else {
+    // some lane spans more than two buckets or the edge of the slot range: per datapoint
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      if (j < nvl) {
+        const int n = m.r0 + (int)fld[j] * uq;
+        if (n >= 0) {
+          const int s = f_slot(p, m, n);
+          if (s < K) {
+            double x = f_value<QW, VL>(b, j);
+            if (F == F_SQUARESUM) x = x * x;
+            fast_fold<F>(L, s, x, 1u);
+          }
+        }
+      }
+    }
+  }
+}
+
+// Series end: buckets -> dense values, certificate, SpanGroup contributions, reset.
+template <int F>
+__device__ __forceinline__ bool fast_series_end(const GridParams& p, const FastLds& L, int K, int lsb, double amax) {
+  const int lane = lane_id();
+  WAVE_SYNC();
+  uint32_t nmax = 0;
+  for (int k = lane; k < K; k += 64) {
+    const uint32_t c = L.cnt[k];
+    const double a = L.acc[k];
+    nmax = max(nmax, c);
+    L.w.pres[k] = c != 0;
+    double v;
+    if (F == F_SUM || F == F_SQUARESUM) v = c ? a : (double)NAN;
+    else if (F == F_AVG) v = c ? a / (double)(int)c : (double)NAN;
+    else if (F == F_COUNT) v = (double)c;
+    else if (F == F_MIN) v = a == INFINITY ? (double)NAN : a;
+    else v = a == -INFINITY ? (double)NAN : a;
+    L.acc[k] = v;
+  }
+  nmax = (uint32_t)wave_max((int)nmax);
+  if (needs_cert<F>()) {
+    const int Lb = (F == F_SQUARESUM) ? 2 * lsb : lsb;
+    const double A = (F == F_SQUARESUM) ? amax * amax : amax;
+    const bool ok = (A == 0.0) || (lsb != INT32_MAX && Lb >= -1022 && !isinf(A) &&
+                                   (double)nmax * A * (1.0 + 1e-12) <= ldexp(1.0, 52 + Lb));
+    if (!ok) return false;
+  }
+  emit_series(p, L.w, K);
+  for (int k = lane; k < K; k += 64) {
+    L.acc[k] = fast_identity<F>();
+    L.cnt[k] = 0;
+    L.w.pres[k] = 0;
+  }
+  WAVE_SYNC();
+  return true;
+}
+
+template <int F, int QW, int VL, int D>
+__global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __restrict__ rows,
+                                              const int64_t* __restrict__ srp, const int64_t* __restrict__ tbeg,
+                                              const int64_t* __restrict__ tend) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (scalar) tile index
+  const int64_t tile = (int64_t)blockIdx.x * p.waves + wave;
+  if (tile >= p.n_tiles) return;
+  const int K = (int)p.K;
+  const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0);
+  for (int k = lane; k < K; k += 64) {
+    part_init(p.ga, L.w.part, k);
+    L.acc[k] = fast_identity<F>();
+    L.cnt[k] = 0;
+    L.w.pres[k] = 0;
+  }
+  FWalk w;
+  w.r0 = srp[tbeg[tile]];
+  w.r = 0;
+  w.rend = (int32_t)(srp[tend[tile]] - w.r0);
+  w.c0 = 0;
+  w.sf = 0;
+  if (w.rend > 0) w.d = fdesc(rows, w.r0);
+  if (w.rend > 1) w.nd = fdesc(rows, w.r0 + 1);
+  WAVE_SYNC();
+
+  FRaw<QW, VL> buf[D];
+  FMeta meta[D];
+  bool redo = false;
+#pragma unroll
+  for (int i = 0; i < D; i++) {
+    if (fast_issue<F, QW, VL>(p, rows, w, buf[i], meta[i]) == 2) redo = true;
+  }
+  if ((meta[0].bits & FM_OK) && !redo && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
+  bool have = false;
+  int lsb = INT32_MAX;
+  double amax = 0.0;
+  FGeom g = {0, 0};
+  bool done = redo;
+  while (!done) {
+#pragma unroll
+    for (int i = 0; i < D; i++) {
+      if (!done) {
+        const uint32_t mb = meta[i].bits;
+        if (!(mb & FM_OK) || (mb & FM_NEWSER)) {
+          if (have && !fast_series_end<F>(p, L, K, lsb, amax)) { redo = true; done = true; }
+          lsb = INT32_MAX;
+          amax = 0.0;
+          have = true;
+          if (!(mb & FM_OK)) done = true;
+        }
+        if (!done) {
+          if (mb & FM_NEWROW) {
+            const RowDesc& x = rows[w.r0 + meta[i].rrel];
+            lsb = min(lsb, x.lsb);
+            amax = fmax(amax, x.absmax);
+            g = fgeom(p, x.base);
+          }
+          const int nv0 = (int)(mb & FM_NV);
+          if (nv0 >= CH) fast_chunk<F, QW, VL, true>(p, L, buf[i], g, nv0, K);
+          else fast_chunk<F, QW, VL, false>(p, L, buf[i], g, nv0, K);
+          if (fast_issue<F, QW, VL>(p, rows, w, buf[i], meta[i]) == 2) { redo = true; done = true; }
+        }
+      }
+    }
+  }
+  if (redo) {
+    if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
+    return;
+  }
+  WAVE_SYNC();
+  double* ga_ = p.part.a + tile * K;
+  double* gb_ = p.part.b + tile * K;
+  uint32_t* gn_ = p.part.n + tile * K;
+  uint32_t* gf_ = p.part.f + tile * K;
+  for (int k = lane; k < K; k += 64) {
+    ga_[k] = L.w.part.a[k];
+    gb_[k] = L.w.part.b[k];
+    gn_[k] = L.w.part.n[k];
+    gf_[k] = L.w.part.f[k];
+  }
+}
+
 // ---- k_reduce -------------------------------------------------------------------
 struct PState {
   double a, b;
@@ -1285,7 +1695,7 @@ __device__ __forceinline__ double ps_final(int ga, const PState& s, int32_t* err
 __global__ __launch_bounds__(256) void k_reduce(ReduceParams p) {
   __shared__ PState sh[4][64];
   const int lane = lane_id();
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (scalar) tile index
   const int64_t g = blockIdx.x;
   const int64_t k = (int64_t)blockIdx.y * 64 + lane;
   const int64_t t0 = p.group_tile_ptr[g], t1 = p.group_tile_ptr[g + 1];
@@ -1473,6 +1883,49 @@ hipError_t launch_grid(const GridParams& p, int f, hipStream_t s) {
   }
   return hipErrorInvalidValue;
 }
+
+template <int F, int QW, int VL>
+static hipError_t launch_fast_t(const GridParams& p, hipStream_t s) {
+  constexpr int D = (QW * 2 + VL * 2 <= 16) ? 3 : 2;   // ring depth: chunk registers per lane
+  const int64_t blocks = (p.n_tiles + p.waves - 1) / p.waves;
+  const size_t lds = (size_t)p.wave_lds * p.waves;
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_fast<F, QW, VL, D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((k_fast<F, QW, VL, D>), dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p, p.rows,
+                     p.series_row_ptr, p.tile_begin, p.tile_end);
+  return hipGetLastError();
+}
+
+template <int F>
+static hipError_t launch_fast_f(const GridParams& p, int qw, int vl, hipStream_t s) {
+  if (qw == 2 && vl == 4) return launch_fast_t<F, 2, 4>(p, s);
+  if (qw == 2 && vl == 8) return launch_fast_t<F, 2, 8>(p, s);
+  if (qw == 4 && vl == 4) return launch_fast_t<F, 4, 4>(p, s);
+  if (qw == 4 && vl == 8) return launch_fast_t<F, 4, 8>(p, s);
+  return hipErrorNotSupported;
+}
+
+bool fast_supported(int f, int qw, int vl) {
+  return (f == F_SUM || f == F_AVG || f == F_COUNT || f == F_SQUARESUM || f == F_MIN || f == F_MAX) &&
+         (qw == 2 || qw == 4) && (vl == 4 || vl == 8);
+}
+
+hipError_t launch_fast(const GridParams& p, int f, int qw, int vl, hipStream_t s) {
+  if (p.n_tiles == 0) return hipSuccess;
+  switch (f) {
+    case F_SUM: return launch_fast_f<F_SUM>(p, qw, vl, s);
+    case F_AVG: return launch_fast_f<F_AVG>(p, qw, vl, s);
+    case F_COUNT: return launch_fast_f<F_COUNT>(p, qw, vl, s);
+    case F_SQUARESUM: return launch_fast_f<F_SQUARESUM>(p, qw, vl, s);
+    case F_MIN: return launch_fast_f<F_MIN>(p, qw, vl, s);
+    case F_MAX: return launch_fast_f<F_MAX>(p, qw, vl, s);
+  }
+  return hipErrorNotSupported;
+}
+
+int64_t fast_wave_lds(int64_t K, bool rate) { return align16(fast_slot_bytes(K, rate)); }
 
 int64_t grid_wave_lds(int64_t K, bool rate, bool gslot) {
   return align16(fixed_lds_bytes() + (gslot ? 0 : slot_lds_bytes(K, rate)));

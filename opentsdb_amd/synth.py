@@ -7,6 +7,8 @@ functions of (seed, global series id i, point index k) via splitmix64:
   value_kind 0: float32 50 + 10 (u - 0.5)            (addPoint(float), 4 bytes)
   value_kind 1: int  u mod int_mod                    (addPoint(long), 1/2/4/8 bytes)
   value_kind 2: even series int, odd series float32
+  value_kind 3: float64 holding the kind-0 float32 value (8-byte float cells; host only)
+  value_kind 4: float64 50 + 10 (u - 0.5) with a full 53-bit mantissa (host only)
 Series i belongs to group i % n_groups; the batch lists series grouped (group-major).
 """
 from __future__ import annotations
@@ -42,6 +44,10 @@ def values(seed: int, i: int, k: np.ndarray, value_kind: int, int_mod: int):
     if is_int:
         return True, (u % np.uint64(int_mod)).astype(np.int64)
     d = (u >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+    if value_kind == 4:
+        return False, 50.0 + 10.0 * (d - 0.5)
+    if value_kind == 3:
+        return False, (50.0 + 10.0 * (d - 0.5)).astype(np.float32).astype(np.float64)
     return False, (50.0 + 10.0 * (d - 0.5)).astype(np.float32)
 
 
@@ -77,6 +83,9 @@ def generate(n_series: int, start_s: int, n_points: int, period_ms: int, value_k
             if is_int:
                 L = vle_lengths(v[a:b])
                 flags = (L - 1).astype(np.uint32)
+            elif v.dtype == np.float64:
+                L = np.full(n, 8, np.int64)
+                flags = np.full(n, 0xF, np.uint32)
             else:
                 L = np.full(n, 4, np.int64)
                 flags = np.full(n, 0xB, np.uint32)
@@ -90,6 +99,8 @@ def generate(n_series: int, start_s: int, n_points: int, period_ms: int, value_k
                 for x, l in zip(vv.tolist(), L.tolist()):
                     parts.append(int(x).to_bytes(l, "big", signed=True))
                 vb = b"".join(parts)
+            elif v.dtype == np.float64:
+                vb = v[a:b].astype(">f8").tobytes()
             else:
                 vb = v[a:b].astype(">f4").tobytes()
             if n > 1:
