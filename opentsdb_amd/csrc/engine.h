@@ -143,6 +143,9 @@ bool fast_supported(int ds_function_class, int qw, int vl);
 hipError_t launch_fast(const GridParams& p, int ds_function_class, int qw, int vl, hipStream_t s);
 int64_t fast_wave_lds(int64_t K, bool rate);
 hipError_t launch_reduce(const ReduceParams& p, hipStream_t s);
+// per-downsample-function instantiations (k_grid.hip / k_fast.hip, one object per F)
+template <int F> hipError_t launch_grid_inst(const GridParams& p, hipStream_t s);
+template <int F> hipError_t launch_fast_inst(const GridParams& p, int qw, int vl, hipStream_t s);
 int64_t grid_wave_lds(int64_t K, bool rate, bool gslot);
 hipError_t launch_synth_sizes(const SynthParams& p, hipStream_t s);
 hipError_t launch_synth_write(const SynthParams& p, hipStream_t s);

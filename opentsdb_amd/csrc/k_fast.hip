@@ -1,0 +1,35 @@
+// k_fast.hip -- instantiates the streaming kernel k_fast for ONE downsample function
+// (F_ID, set by the Makefile) and the four uniform row classes (qualifier width 2/4 x
+// value length 4/8).
+#include "kcommon.h"
+
+#ifndef F_ID
+#error "compile with -DF_ID=<downsample function class>"
+#endif
+
+namespace tsdb {
+
+template <int F, int QW, int VL>
+static hipError_t launch_fast_t(const GridParams& p, hipStream_t s) {
+  constexpr int D = (QW * 2 + VL * 2 <= 16) ? 3 : 2;   // ring depth: chunk registers per lane
+  const int64_t blocks = (p.n_tiles + p.waves - 1) / p.waves;
+  const size_t lds = (size_t)p.wave_lds * p.waves;
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_fast<F, QW, VL, D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((k_fast<F, QW, VL, D>), dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p, p.rows,
+                     p.series_row_ptr, p.tile_begin, p.tile_end);
+  return hipGetLastError();
+}
+
+template <>
+hipError_t launch_fast_inst<F_ID>(const GridParams& p, int qw, int vl, hipStream_t s) {
+  if (qw == 2 && vl == 4) return launch_fast_t<F_ID, 2, 4>(p, s);
+  if (qw == 2 && vl == 8) return launch_fast_t<F_ID, 2, 8>(p, s);
+  if (qw == 4 && vl == 4) return launch_fast_t<F_ID, 4, 4>(p, s);
+  if (qw == 4 && vl == 8) return launch_fast_t<F_ID, 4, 8>(p, s);
+  return hipErrorNotSupported;
+}
+
+}  // namespace tsdb

@@ -37,7 +37,7 @@ class EngineError(Exception):
 
 def build(force: bool = False) -> str:
     if force or not os.path.exists(LIB_PATH):
-        subprocess.run(["make", "-C", CSRC], check=True)
+        subprocess.run(["make", "-j8", "-C", CSRC], check=True)
     return LIB_PATH
 
 
