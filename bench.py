@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--value-kind", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH/WRITE_SIZE child passes")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -66,6 +68,54 @@ def cpu_baseline(args, target_s: float):
     return {"value": dps / dt, "unit": "datapoints/s", "cores": 1, "kind": "port",
             "sample": f"{n} series x {args.points} dp ({args.ds} {args.interval}, {args.agg} over "
                       f"{min(args.groups, n)} groups), {reps} reps, {dt:.1f} s, oracle/refcpu.c single thread"}
+
+
+def pmc_traffic(args, kernel_prefix: str):
+    """HBM bytes per launch of the dominant kernel from rocprofv3 PMC counters.
+
+    Two separate child runs of this script (FETCH_SIZE and WRITE_SIZE cannot share a pass,
+    MI355X_MICROARCH.md "rocprofv3 PMC slots"), each profiling 3 launches of the same
+    workload.  FETCH_SIZE is in KiB and on gfx950 reports half the bytes of a 16-B/lane
+    streaming read, so it is doubled; WRITE_SIZE is exact (same guide, "HBM").  Returns
+    (bytes_per_launch, detail) or (None, reason)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, "rocprofv3 not found"
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "3", "--warmup", "0",
+             "--series", str(args.series), "--points", str(args.points), "--period-ms", str(args.period_ms),
+             "--groups", str(args.groups), "--interval", args.interval, "--ds", args.ds, "--agg", args.agg,
+             "--value-kind", str(args.value_kind)]
+    out = {}
+    tmp = tempfile.mkdtemp(prefix="tsdb_pmc_")
+    env = dict(os.environ, TMPDIR="/tmp")
+    try:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, ctr)
+            cmd = ["timeout", "-s", "KILL", "120", exe, "--pmc", ctr, "--kernel-trace", "--output-format", "csv",
+                   "-d", d, "-o", "run", "--"] + child
+            r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env, cwd=ROOT)
+            if r.returncode != 0:
+                return None, f"rocprofv3 --pmc {ctr} exited {r.returncode}"
+            vals = []
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                with open(f) as fh:
+                    for row in csv.DictReader(fh):
+                        if row["Counter_Name"] == ctr and row["Kernel_Name"].startswith(kernel_prefix):
+                            vals.append(float(row["Counter_Value"]))
+            if not vals:
+                return None, f"no {ctr} rows for {kernel_prefix}"
+            out[ctr] = sum(vals) / len(vals)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    fetch = out["FETCH_SIZE"] * 1024.0 * 2.0
+    write = out["WRITE_SIZE"] * 1024.0
+    return fetch + write, {"fetch_bytes": fetch, "write_bytes": write, "fetch_size_kib_raw": out["FETCH_SIZE"],
+                           "correction": "FETCH_SIZE x2 (gfx950 streaming-read undercount), KiB->B"}
 
 
 def query(args):
@@ -102,8 +152,15 @@ def main():
     def step():
         if dist is None:
             return eng.run(q)
-        return eng.run_distributed(q, dist, args.groups)
+        from opentsdb_amd.dist import run_distributed
+        return run_distributed(eng, q, dist, args.groups, device=f"cuda:{local_rank}")
 
+    if args.pmc_child:
+        for _ in range(args.steps):
+            step()
+        eng.sync()
+        eng.close()
+        return
     for _ in range(args.warmup):
         step()
     if dist is not None:
@@ -112,12 +169,14 @@ def main():
         torch.cuda.synchronize()
     eng.sync()
     kernel_ms = []
+    fast_ms = []
     reduce_ms = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         tm = eng.timing()
         kernel_ms.append(tm.decode_downsample_ms)
+        fast_ms.append(tm.fast_ms)
         reduce_ms.append(tm.group_reduce_ms)
     eng.sync()
     if dist is not None:
@@ -134,10 +193,17 @@ def main():
     ms_per_step = elapsed * 1000.0 / args.steps
     dps_step = tm.datapoints * world
     value = dps_step / (ms_per_step / 1000.0)
-    k_avg = sum(kernel_ms) / len(kernel_ms)
+    # dominant kernel: the streaming kernel k_fast when the batch's row class allows it
+    # (every tile handed back to k_grid otherwise); hipEvents on the engine stream
+    use_fast = min(fast_ms) > 0 and tm.redo_tiles == 0
+    k_avg = sum(fast_ms if use_fast else kernel_ms) / args.steps
+    kname = "k_fast" if use_fast else "k_grid"
     achieved = tm.bytes / (k_avg / 1000.0) / 1e9
     if rank == 0:
-        cpu = None if args.no_cpu_baseline else cpu_baseline(args, args.cpu_seconds)
+        cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(args, args.cpu_seconds)
+        traffic, traffic_note = (None, "not collected (--no-pmc or N>1)")
+        if not args.no_pmc and world == 1:
+            traffic, traffic_note = pmc_traffic(args, f"void tsdb::{kname}")
         line = {
             "metric": "raw datapoints/sec through downsample+group-by; % of HBM BW, 1-8 GPUs",
             "value": value,
@@ -166,10 +232,13 @@ def main():
                 "peak": BYTES_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / BYTES_PEAK_GBS,
-                "traffic": None,
-                "kernel": "k_grid (fused decode+downsample+tile group partials)",
+                "traffic": traffic,
+                "traffic_detail": traffic_note,
+                "kernel": kname + (" (streaming decode+downsample+tile group partials)" if use_fast
+                                   else " (fused decode+downsample+tile group partials)"),
                 "kernel_ms": k_avg,
                 "bytes_per_launch": tm.bytes,
+                "bytes_per_dp": tm.bytes / max(1, tm.datapoints),
                 "group_reduce_ms": sum(reduce_ms) / len(reduce_ms),
             },
             "cpu_baseline": cpu,

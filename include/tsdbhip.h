@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define TSDBHIP_ABI_VERSION 1
+#define TSDBHIP_ABI_VERSION 2
 
 /* ---- error codes: one per Java exception on the path --------------------- */
 enum {
@@ -127,7 +127,7 @@ typedef struct {
   double group_reduce_ms;        /* cross-tile group reduction + emission */
   double total_ms;
   int64_t datapoints;            /* raw datapoints decoded */
-  int64_t bytes;                 /* algorithmic HBM bytes read (qualifiers+values+row index) */
+  int64_t bytes;                 /* algorithmic HBM bytes: per row q+v+4+16, per series 4 */
   int64_t tiles;                 /* series tiles of the query */
   int64_t redo_tiles;            /* tiles the streaming kernel handed to the general kernel */
   double fast_ms;                /* streaming kernel (k_fast) alone; 0 when not used */
@@ -179,26 +179,37 @@ int tsdbhip_run(tsdbhip_ctx* ctx, const tsdbhip_query* q, tsdbhip_result** out);
 void tsdbhip_result_free(tsdbhip_result* r);
 int tsdbhip_last_timing(tsdbhip_ctx* ctx, tsdbhip_timing* out);
 
-/* ---- multi-GPU (series sharded over ranks; decomposable partial exchange) ----
- * tsdbhip_partials_layout: size in bytes of the per-(group, slot) partial-state buffer
- * and its reduction structure: the buffer is n_sum doubles (reduce SUM), then
- * n_min doubles (MIN), then n_max doubles (MAX); the caller all-reduces each segment
- * (RCCL over xGMI) and hands the reduced buffer to tsdbhip_finalize. */
+/* ---- multi-GPU (series sharded over ranks; one exchange step) --------------
+ * One process per GPU, each with its own context and its own contiguous shard of the
+ * group-sorted series.  A SpanGroup may straddle ranks.  Every rank reduces
+ * its shard to one partial state per (group, output slot); the caller all-gathers the
+ * per-rank buffers (RCCL ncclAllGather over xGMI) into n_ranks consecutive copies in rank
+ * order, and tsdbhip_finalize merges them in rank order -- which is SpanGroup series order,
+ * so first/last/diff/mult keep the reference's semantics -- and finalises the aggregator
+ * (AggregationIterator.doubleValue / Aggregator.runDouble).  An all-gather rather than an
+ * all-reduce because the merge is not an RCCL operator for dev (Chan merge of Welford
+ * states), first/last/diff/mult (ordered), and because the buffer is small:
+ * n_groups * n_slots * 24 B (config 2: 64 x 60 -> 92 KB per rank).
+ *
+ * Buffer layout of one rank (bytes = tsdbhip_partials_layout.bytes, 16-B aligned parts):
+ *   double   a[n_groups * n_slots]    sum / min / max / mean / first / last / product
+ *   double   b[n_groups * n_slots]    Welford M2 / last value (diff)
+ *   uint32_t n[n_groups * n_slots]    non-NaN contributions
+ *   uint32_t f[n_groups * n_slots]    bit0 union point, bit1 has-value, >>2 contributions
+ *   uint32_t active[n_groups]         the group has a span in [scan start, scan end]
+ * Index [g * n_slots + k]; slot k is timestamp B0 + k * interval (or the "all" bucket). */
 typedef struct {
   int64_t n_groups;
   int64_t n_slots;
-  int64_t n_sum;
-  int64_t n_min;
-  int64_t n_max;
-  int64_t bytes;
+  int64_t bytes;             /* per rank */
 } tsdbhip_partials_layout;
 int tsdbhip_partials_layout_get(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_global,
                                 tsdbhip_partials_layout* out);
-/* Computes this shard's partial states into device memory d_partials (layout above). */
-int tsdbhip_run_partials(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_global, void* d_partials);
-/* Turns reduced partial states into the result (on the calling rank). */
+/* Computes this shard's partial states into `partials` (device or host memory, layout above). */
+int tsdbhip_run_partials(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_global, void* partials);
+/* Merges n_ranks rank-ordered partial buffers (device or host memory) and builds the result. */
 int tsdbhip_finalize(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_global,
-                     const void* d_partials, int n_ranks, tsdbhip_result** out);
+                     const void* partials, int n_ranks, tsdbhip_result** out);
 /* Device synchronisation helper for host code that does not use HIP directly. */
 int tsdbhip_sync(tsdbhip_ctx* ctx);
 

@@ -145,9 +145,6 @@ class PartialsLayout(C.Structure):
     _fields_ = [
         ("n_groups", C.c_int64),
         ("n_slots", C.c_int64),
-        ("n_sum", C.c_int64),
-        ("n_min", C.c_int64),
-        ("n_max", C.c_int64),
         ("bytes", C.c_int64),
     ]
 

@@ -138,10 +138,14 @@ struct tsdbhip_ctx {
   DevBuf n_tb, n_te, n_tg, n_gtp;
   // scratch
   DevBuf pa, pb, pn, pf, out_val, out_flag, gact, err, g_dense, g_pres, g_rate, redo, redo_n;
+  DevBuf xbuf, gbuf;                   // multi-GPU: this rank's partial states, gathered states
   // dominant uniform row class of the batch (k_fast specialisation), 0 = none
   int fast_qw = 0, fast_vl = 0;
   bool fast_used = false;
   tsdbhip_timing timing{};
+  // account() cache (invalidated by every load)
+  bool acct_valid = false;
+  int64_t acct_ss = 0, acct_se = 0, acct_dps = 0, acct_bytes = 0;
 };
 
 // ===========================================================================
@@ -282,6 +286,7 @@ static void release_batch(tsdbhip_ctx* c) {
                     &c->n_tb, &c->n_te, &c->n_tg, &c->n_gtp})
     b->release();
   c->none_tiles_ready = false;
+  c->acct_valid = false;
   c->n_series = c->n_rows = c->n_groups = 0;
 }
 
@@ -291,7 +296,7 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   release_batch(c);
   for (DevBuf* b : {&c->pa, &c->pb, &c->pn, &c->pf, &c->out_val, &c->out_flag, &c->gact, &c->err, &c->g_dense,
-                    &c->g_pres, &c->g_rate, &c->redo, &c->redo_n})
+                    &c->g_pres, &c->g_rate, &c->redo, &c->redo_n, &c->xbuf, &c->gbuf})
     b->release();
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -782,16 +787,30 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   return 0;
 }
 
+// Raw datapoints and algorithmic HBM bytes of the query:
+//   per row in the scan range: qualifier bytes + value bytes (incl. the meta byte)
+//                              + 4 B base time + 2 x 8 B CSR offsets;  per series: 4 B group id.
+// Cached per scan range (the batch is resident; the loop is O(rows)).
 void account(tsdbhip_ctx* c, const Plan& P) {
+  if (c->acct_valid && c->acct_ss == P.ss && c->acct_se == P.se) {
+    c->timing.datapoints = c->acct_dps;
+    c->timing.bytes = c->acct_bytes;
+    return;
+  }
   int64_t dps = 0, bytes = 0;
   for (int64_t s = 0; s < c->n_series; s++) {
-    bytes += 8;
+    bytes += 4;
     for (int64_t r = c->h_srp[s]; r < c->h_srp[s + 1]; r++) {
       if ((int64_t)c->h_base[r] < P.ss || (int64_t)c->h_base[r] >= P.se) continue;
       dps += c->h_ndp[r];
-      bytes += (int64_t)c->h_qlen[r] + c->h_vlen[r] + (int64_t)sizeof(RowDesc);
+      bytes += (int64_t)c->h_qlen[r] + c->h_vlen[r] + 4 + 16;
     }
   }
+  c->acct_valid = true;
+  c->acct_ss = P.ss;
+  c->acct_se = P.se;
+  c->acct_dps = dps;
+  c->acct_bytes = bytes;
   c->timing.datapoints = dps;
   c->timing.bytes = bytes;
 }
@@ -856,30 +875,10 @@ int assemble(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, c
 
 }  // namespace
 
-extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
-  if (!c || !q || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
-  std::lock_guard<std::mutex> lk(c->mu);
-  *out = nullptr;
-  HIP_OK(hipSetDevice(c->device));
-  Plan P;
-  int rc = plan_query(c, q, P);
-  if (rc) return rc;
-  const int64_t G = P.none ? c->n_series : c->n_groups;
-  rc = run_device(c, q, P, G, true);
-  if (rc) return rc;
-  std::vector<double> val(G * P.K);
-  std::vector<uint8_t> flag(G * P.K);
-  std::vector<uint32_t> act(std::max<int64_t>(1, G));
-  int32_t err = 0;
-  if (G * P.K) {
-    HIP_OK(hipMemcpyAsync(val.data(), c->out_val.p, G * P.K * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipMemcpyAsync(flag.data(), c->out_flag.p, G * P.K, hipMemcpyDeviceToHost, c->stream));
-  }
-  if (G) HIP_OK(hipMemcpyAsync(act.data(), c->gact.p, G * 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
-  int32_t redo_n = 0;
-  if (c->fast_used) HIP_OK(hipMemcpyAsync(&redo_n, c->redo_n.p, 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipStreamSynchronize(c->stream));
+namespace {
+
+// Device timings of the last run (events recorded by run_device).
+void record_timing(tsdbhip_ctx* c, const Plan& P, int32_t redo_n) {
   float t01 = 0, t12 = 0, t03 = 0;
   (void)hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
   (void)hipEventElapsedTime(&t12, c->ev[1], c->ev[2]);
@@ -891,6 +890,24 @@ extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_resul
   c->timing.tiles = P.none ? c->n_series : (int64_t)c->tb.size();
   c->timing.redo_tiles = c->fast_used ? redo_n : c->timing.tiles;
   account(c, P);
+}
+
+// Dense [G][K] outputs on the device -> result (after the stream's work is queued).
+int collect(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bool timed, tsdbhip_result** out) {
+  std::vector<double> val(G * P.K);
+  std::vector<uint8_t> flag(G * P.K);
+  std::vector<uint32_t> act(std::max<int64_t>(1, G));
+  int32_t err = 0;
+  if (G * P.K) {
+    HIP_OK(hipMemcpyAsync(val.data(), c->out_val.p, G * P.K * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipMemcpyAsync(flag.data(), c->out_flag.p, G * P.K, hipMemcpyDeviceToHost, c->stream));
+  }
+  if (G) HIP_OK(hipMemcpyAsync(act.data(), c->gact.p, G * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
+  int32_t redo_n = 0;
+  if (timed && c->fast_used) HIP_OK(hipMemcpyAsync(&redo_n, c->redo_n.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  if (timed) record_timing(c, P, redo_n);
   if (err) return fail(err, "error raised by the device path");
   if (P.mode == MODE_ALL) {
     // AggregationIterator ctor: the single "all" point is skipped unless start_time <= qs <= end_time
@@ -898,6 +915,22 @@ extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_resul
     if (q->start_time < S0 || q->start_time > E0) std::fill(flag.begin(), flag.end(), 0);
   }
   return assemble(c, q, P, G, val, flag, act, out);
+}
+
+}  // namespace
+
+extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
+  if (!c || !q || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  *out = nullptr;
+  HIP_OK(hipSetDevice(c->device));
+  Plan P;
+  int rc = plan_query(c, q, P);
+  if (rc) return rc;
+  const int64_t G = P.none ? c->n_series : c->n_groups;
+  rc = run_device(c, q, P, G, true);
+  if (rc) return rc;
+  return collect(c, q, P, G, true, out);
 }
 
 extern "C" void tsdbhip_result_free(tsdbhip_result* r) { std::free(r); }
@@ -912,32 +945,122 @@ extern "C" int tsdbhip_last_timing(tsdbhip_ctx* c, tsdbhip_timing* out) {
 // multi-GPU partials: every rank reduces its shard to per-(group, slot) partial
 // states; ranks all-gather them (RCCL) and each merges in rank order.
 // ---------------------------------------------------------------------------
+namespace {
+
+struct PartLayout {
+  int64_t off_b, off_n, off_f, off_act, bytes;
+};
+
+PartLayout part_layout(int64_t G, int64_t K) {
+  PartLayout L;
+  const int64_t n = G * K;
+  L.off_b = align16(n * 8);
+  L.off_n = L.off_b + align16(n * 8);
+  L.off_f = L.off_n + align16(n * 4);
+  L.off_act = L.off_f + align16(n * 4);
+  L.bytes = L.off_act + align16(std::max<int64_t>(1, G) * 4);
+  return L;
+}
+
+int plan_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, Plan& P) {
+  int rc = plan_query(c, q, P);
+  if (rc) return rc;
+  if (P.none) return fail(TSDB_E_NOT_IMPLEMENTED, "NONE aggregator is per-span; it has no cross-rank exchange");
+  if (n_groups_global < c->n_groups) return fail(TSDB_E_ILLEGAL_ARGUMENT, "n_groups_global smaller than the local groups");
+  return 0;
+}
+
+}  // namespace
+
 extern "C" int tsdbhip_partials_layout_get(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global,
                                            tsdbhip_partials_layout* out) {
   if (!c || !q || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   Plan P;
-  int rc = plan_query(c, q, P);
+  int rc = plan_partials(c, q, n_groups_global, P);
   if (rc) return rc;
-  if (P.none) return fail(TSDB_E_NOT_IMPLEMENTED, "NONE aggregator is per-span; no partial exchange");
-  if (n_groups_global < c->n_groups) return fail(TSDB_E_ILLEGAL_ARGUMENT, "n_groups_global smaller than the local groups");
   out->n_groups = n_groups_global;
   out->n_slots = P.K;
-  // per (group, slot): a, b, n, f as doubles; then one activity double per group
-  out->n_sum = 0;
-  out->n_min = 0;
-  out->n_max = 0;
-  out->bytes = (n_groups_global * P.K * 4 + n_groups_global) * 8;
+  out->bytes = part_layout(n_groups_global, P.K).bytes;
   return 0;
 }
 
-
-extern "C" int tsdbhip_run_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, void* d_partials) {
-  (void)c; (void)q; (void)n_groups_global; (void)d_partials;
-  return fail(TSDB_E_NOT_IMPLEMENTED, "multi-GPU partials: not implemented yet");
+extern "C" int tsdbhip_run_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, void* partials) {
+  if (!c || !q || !partials) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  Plan P;
+  int rc = plan_partials(c, q, n_groups_global, P);
+  if (rc) return rc;
+  const int64_t G = n_groups_global, K = P.K;
+  const PartLayout L = part_layout(G, K);
+  rc = run_device(c, q, P, c->n_groups, false);
+  if (rc) return rc;
+  // merged per-(group, slot) states of this shard; groups this rank does not hold keep
+  // the identity state (zero bytes except the min / max identities written below)
+  HIP_OK(c->xbuf.ensure(L.bytes));
+  unsigned char* xb = c->xbuf.as<unsigned char>();
+  HIP_OK(hipMemsetAsync(xb, 0, L.bytes, c->stream));
+  if (c->n_groups * K) {
+    ReduceParams rp{};
+    rp.part = Partials{c->pa.as<double>(), c->pb.as<double>(), c->pn.as<uint32_t>(), c->pf.as<uint32_t>()};
+    rp.group_tile_ptr = c->d_gtp.as<int64_t>();
+    rp.G = c->n_groups;
+    rp.K = K;
+    rp.ga = P.ga;
+    rp.err = c->err.as<int32_t>();
+    rp.state = Partials{reinterpret_cast<double*>(xb), reinterpret_cast<double*>(xb + L.off_b),
+                        reinterpret_cast<uint32_t*>(xb + L.off_n), reinterpret_cast<uint32_t*>(xb + L.off_f)};
+    HIP_OK(launch_reduce(rp, c->stream));
+  }
+  if (G > c->n_groups && (P.ga == GA_MIN || P.ga == GA_MAX)) {
+    std::vector<double> ident((G - c->n_groups) * K, P.ga == GA_MIN ? INFINITY : -INFINITY);
+    HIP_OK(hipMemcpyAsync(xb + c->n_groups * K * 8, ident.data(), ident.size() * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+  }
+  if (c->n_groups) HIP_OK(hipMemcpyAsync(xb + L.off_act, c->gact.p, c->n_groups * 4, hipMemcpyDeviceToDevice, c->stream));
+  HIP_OK(hipEventRecord(c->ev[2], c->stream));
+  HIP_OK(hipMemcpyAsync(partials, xb, L.bytes, hipMemcpyDefault, c->stream));
+  int32_t err = 0, redo_n = 0;
+  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
+  if (c->fast_used) HIP_OK(hipMemcpyAsync(&redo_n, c->redo_n.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  record_timing(c, P, redo_n);
+  if (err) return fail(err, "error raised by the device path");
+  return 0;
 }
 
-extern "C" int tsdbhip_finalize(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, const void* d_partials,
+extern "C" int tsdbhip_finalize(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, const void* partials,
                                 int n_ranks, tsdbhip_result** out) {
-  (void)c; (void)q; (void)n_groups_global; (void)d_partials; (void)n_ranks; (void)out;
-  return fail(TSDB_E_NOT_IMPLEMENTED, "multi-GPU partials: not implemented yet");
+  if (!c || !q || !partials || !out || n_ranks < 1) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  *out = nullptr;
+  HIP_OK(hipSetDevice(c->device));
+  Plan P;
+  int rc = plan_partials(c, q, n_groups_global, P);
+  if (rc) return rc;
+  const int64_t G = n_groups_global, K = P.K;
+  const PartLayout L = part_layout(G, K);
+  HIP_OK(c->gbuf.ensure(L.bytes * n_ranks));
+  HIP_OK(hipMemcpyAsync(c->gbuf.p, partials, L.bytes * n_ranks, hipMemcpyDefault, c->stream));
+  HIP_OK(c->out_val.ensure(std::max<int64_t>(1, G * K) * 8));
+  HIP_OK(c->out_flag.ensure(std::max<int64_t>(1, G * K)));
+  HIP_OK(c->gact.ensure(std::max<int64_t>(1, G) * 4));
+  HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
+  RankMergeParams mp{};
+  mp.base = c->gbuf.as<unsigned char>();
+  mp.stride = L.bytes;
+  mp.off_b = L.off_b;
+  mp.off_n = L.off_n;
+  mp.off_f = L.off_f;
+  mp.off_act = L.off_act;
+  mp.n_ranks = n_ranks;
+  mp.G = G;
+  mp.K = K;
+  mp.ga = P.ga;
+  mp.out_val = c->out_val.as<double>();
+  mp.out_flag = c->out_flag.as<uint8_t>();
+  mp.out_act = c->gact.as<uint32_t>();
+  mp.err = c->err.as<int32_t>();
+  HIP_OK(launch_rank_merge(mp, c->stream));
+  return collect(c, q, P, G, false, out);
 }

@@ -113,6 +113,21 @@ struct ReduceParams {
   double* out_val;                // [G][K]
   uint8_t* out_flag;              // [G][K] bit0 emit
   int32_t* err;
+  Partials state;                 // non-null a: write the merged (unfinalised) state instead
+};
+
+// Rank-ordered merge of all-gathered per-rank partial buffers (tsdbhip_finalize).
+struct RankMergeParams {
+  const unsigned char* base;      // n_ranks consecutive buffers of `stride` bytes
+  int64_t stride;
+  int64_t off_b, off_n, off_f, off_act;   // byte offsets of the parts inside one buffer
+  int32_t n_ranks;
+  int64_t G, K;
+  int32_t ga;
+  double* out_val;
+  uint8_t* out_flag;
+  uint32_t* out_act;
+  int32_t* err;
 };
 
 struct SynthParams {
@@ -143,6 +158,7 @@ bool fast_supported(int ds_function_class, int qw, int vl);
 hipError_t launch_fast(const GridParams& p, int ds_function_class, int qw, int vl, hipStream_t s);
 int64_t fast_wave_lds(int64_t K, bool rate);
 hipError_t launch_reduce(const ReduceParams& p, hipStream_t s);
+hipError_t launch_rank_merge(const RankMergeParams& p, hipStream_t s);
 // per-downsample-function instantiations (k_grid.hip / k_fast.hip, one object per F)
 template <int F> hipError_t launch_grid_inst(const GridParams& p, hipStream_t s);
 template <int F> hipError_t launch_fast_inst(const GridParams& p, int qw, int vl, hipStream_t s);

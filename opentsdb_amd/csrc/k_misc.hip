@@ -185,10 +185,47 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceParams p) {
   if (wave == 0 && k < p.K) {
     PState T = sh[0][lane];
     for (int w = 1; w < 4; w++) T = ps_merge(p.ga, T, sh[w][lane]);
-    const bool emit = (T.f & PF_UNION) != 0;
-    const double r = emit ? ps_final(p.ga, T, p.err) : 0.0;
-    p.out_val[g * p.K + k] = r;
-    p.out_flag[g * p.K + k] = emit ? 1 : 0;
+    const int64_t o = g * p.K + k;
+    if (p.state.a) {
+      p.state.a[o] = T.a;
+      p.state.b[o] = T.b;
+      p.state.n[o] = T.n;
+      p.state.f[o] = T.f;
+    } else {
+      const bool emit = (T.f & PF_UNION) != 0;
+      const double r = emit ? ps_final(p.ga, T, p.err) : 0.0;
+      p.out_val[o] = r;
+      p.out_flag[o] = emit ? 1 : 0;
+    }
+  }
+}
+
+// ---- k_rank_merge: multi-GPU exchange step ------------------------------------------
+// Rank r holds series shard r of the group-sorted span order, so merging the gathered
+// per-rank states in rank order continues ps_merge's series order across GPUs.
+__global__ __launch_bounds__(256) void k_rank_merge(RankMergeParams p) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = p.G * p.K;
+  if (i < n) {
+    PState S = ps_identity(p.ga);
+    for (int r = 0; r < p.n_ranks; r++) {
+      const unsigned char* b = p.base + (int64_t)r * p.stride;
+      PState X;
+      X.a = reinterpret_cast<const double*>(b)[i];
+      X.b = reinterpret_cast<const double*>(b + p.off_b)[i];
+      X.n = reinterpret_cast<const uint32_t*>(b + p.off_n)[i];
+      X.f = reinterpret_cast<const uint32_t*>(b + p.off_f)[i];
+      S = ps_merge(p.ga, S, X);
+    }
+    const bool emit = (S.f & PF_UNION) != 0;
+    p.out_val[i] = emit ? ps_final(p.ga, S, p.err) : 0.0;
+    p.out_flag[i] = emit ? 1 : 0;
+  }
+  if (i < p.G) {
+    uint32_t act = 0;
+    for (int r = 0; r < p.n_ranks; r++)
+      act |= reinterpret_cast<const uint32_t*>(p.base + (int64_t)r * p.stride + p.off_act)[i];
+    p.out_act[i] = act;
   }
 }
 
@@ -361,6 +398,13 @@ int64_t grid_wave_lds(int64_t K, bool rate, bool gslot) {
 hipError_t launch_reduce(const ReduceParams& p, hipStream_t s) {
   if (p.G == 0 || p.K == 0) return hipSuccess;
   hipLaunchKernelGGL(k_reduce, dim3((unsigned)p.G, (unsigned)((p.K + 63) / 64)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_rank_merge(const RankMergeParams& p, hipStream_t s) {
+  const int64_t n = std::max(p.G * p.K, p.G);
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rank_merge, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 

@@ -158,6 +158,26 @@ class Engine:
     def sync(self):
         _check(lib().tsdbhip_sync(self.ctx))
 
+    # ---- multi-GPU exchange (see include/tsdbhip.h and opentsdb_amd/dist.py) ----
+    def partials_layout(self, q: abi.Query, n_groups_global: int) -> abi.PartialsLayout:
+        lay = abi.PartialsLayout()
+        _check(lib().tsdbhip_partials_layout_get(self.ctx, C.byref(q), n_groups_global, C.byref(lay)))
+        return lay
+
+    def run_partials(self, q: abi.Query, n_groups_global: int, ptr: int):
+        """This shard's per-(group, slot) partial states into `ptr` (device or host memory)."""
+        _check(lib().tsdbhip_run_partials(self.ctx, C.byref(q), n_groups_global, C.c_void_p(ptr)))
+
+    def finalize(self, q: abi.Query, n_groups_global: int, ptr: int, n_ranks: int):
+        """Rank-ordered merge of n_ranks gathered partial buffers at `ptr` -> groups."""
+        res = C.POINTER(abi.Result)()
+        _check(lib().tsdbhip_finalize(self.ctx, C.byref(q), n_groups_global, C.c_void_p(ptr), n_ranks,
+                                      C.byref(res)))
+        try:
+            return abi.result_to_groups(res.contents)
+        finally:
+            lib().tsdbhip_result_free(res)
+
 
 _default = None
 

@@ -1,0 +1,100 @@
+"""Multi-GPU driver (opentsdb_amd/dist.py) on CPU: sharding and the gloo exchange step.
+
+The per-rank partial states come from the GPU (tsdbhip_run_partials); here a stand-in
+engine writes rank-tagged bytes so the test checks what the driver owns: byte-balanced
+contiguous shards in SpanGroup order, and an all-gather that hands tsdbhip_finalize the
+rank buffers in rank order (the GPU tests check the merge itself)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from opentsdb_amd import abi, dist, synth
+
+T0 = 1356998400
+
+
+def test_shard_bounds_balanced():
+    w = np.arange(1, 101)
+    for world in (1, 2, 3, 4, 8):
+        b = dist.shard_bounds(w, world)
+        assert b[0] == 0 and b[-1] == 100 and all(x <= y for x, y in zip(b, b[1:]))
+        sums = [w[b[r]:b[r + 1]].sum() for r in range(world)]
+        assert max(sums) - min(sums) <= 2 * w.max()
+
+
+def test_shard_bounds_more_ranks_than_series():
+    b = dist.shard_bounds([5, 5], 4)
+    assert b[0] == 0 and b[-1] == 2 and len(b) == 5
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5])
+def test_shards_concatenate_to_group_order(world):
+    b = synth.generate(37, T0, 400, 10000, value_kind=2, n_groups=4, int_mod=30000, seed=11)
+    # scramble group ids so the group-sorted order differs from batch order
+    gid = b.group_id.copy()
+    gid[::3] = (gid[::3] + 1) % 4
+    gid[5] = -1
+    b = abi.HostBatch(b.series_row_ptr, b.row_base_time, b.row_qual_off, b.row_val_off, b.qual, b.val, gid)
+    order = dist.group_sorted_order(b)
+    shards = [dist.shard_batch(b, r, world) for r in range(world)]
+    assert sum(s.n_series for s in shards) == len(order)
+    np.testing.assert_array_equal(np.concatenate([s.group_id for s in shards]), gid[order])
+    qual = np.concatenate([s.qual[:int(s.row_qual_off[-1])] for s in shards])
+    want = np.concatenate([b.qual[int(b.row_qual_off[r]):int(b.row_qual_off[r + 1])]
+                           for s in order for r in range(b.series_row_ptr[s], b.series_row_ptr[s + 1])])
+    np.testing.assert_array_equal(qual, want)
+    gs = np.concatenate([s.group_id for s in shards])
+    assert np.all(np.diff(gs) >= 0)
+
+
+class TaggedEngine:
+    """Stand-in for Engine: partial buffers of rank-tagged bytes; finalize returns them."""
+
+    def __init__(self, rank, nbytes):
+        self.rank, self.nbytes = rank, nbytes
+
+    def partials_layout(self, q, G):
+        lay = abi.PartialsLayout()
+        lay.n_groups, lay.n_slots, lay.bytes = G, 1, self.nbytes
+        return lay
+
+    def run_partials(self, q, G, ptr):
+        data = (np.arange(self.nbytes) * 7 + self.rank * 31).astype(np.uint8)
+        C.memmove(ptr, data.ctypes.data, self.nbytes)
+
+    def finalize(self, q, G, ptr, n_ranks):
+        return np.ctypeslib.as_array((C.c_uint8 * (self.nbytes * n_ranks)).from_address(ptr)).copy()
+
+
+def _worker(rank, world, port, nbytes, out):
+    import torch.distributed as td
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    td.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q = abi.new_query(T0, T0 + 3599, "sum")
+        got = dist.run_distributed(TaggedEngine(rank, nbytes), q, td, 4)
+        np.save(os.path.join(out, f"r{rank}.npy"), got)
+    finally:
+        td.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_exchange_rank_order(tmp_path, world):
+    nbytes = 1000
+    mp.spawn(_worker, args=(world, _free_port(), nbytes, str(tmp_path)), nprocs=world, join=True)
+    want = np.concatenate([(np.arange(nbytes) * 7 + r * 31).astype(np.uint8) for r in range(world)])
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / f"r{r}.npy"), want)

@@ -1,0 +1,115 @@
+"""Multi-GPU exchange on the device: shards reduced by separate libtsdbhip contexts,
+partial states merged in rank order by tsdbhip_finalize, checked against the oracle over
+the whole (unsharded) batch.
+
+Ranks are emulated by several contexts on cuda:0 (the round-end 8-GPU run uses one
+process per GPU with RCCL; tests/test_dist_cpu.py covers the gloo exchange itself), plus
+one real 2-process gloo run through opentsdb_amd/dist.run_distributed."""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from opentsdb_amd import abi, dist, synth
+from oracle import oracle as O
+from tests.test_gpu_parity import assert_groups_match
+
+pytestmark = pytest.mark.gpu
+
+T0 = 1356998400
+
+
+@pytest.fixture(scope="module")
+def engines():
+    from opentsdb_amd.engine import Engine
+    es = [Engine(0) for _ in range(4)]
+    yield es
+    for e in es:
+        e.close()
+
+
+@pytest.fixture(scope="module")
+def batch():
+    return synth.generate(150, T0, 360, 10000, value_kind=2, n_groups=7, int_mod=30000, seed=0x5EED)
+
+
+def run_sharded(engines, b, q, world):
+    G = dist.n_groups_of(b)
+    bufs = []
+    for r in range(world):
+        e = engines[r]
+        e.load(dist.shard_batch(b, r, world))
+        lay = e.partials_layout(q, G)
+        buf = np.zeros(int(lay.bytes), np.uint8)
+        e.run_partials(q, G, buf.ctypes.data)
+        bufs.append(buf)
+    gathered = np.concatenate(bufs)
+    return engines[0].finalize(q, G, gathered.ctypes.data, world)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+@pytest.mark.parametrize("agg", ["sum", "avg", "min", "max", "count", "dev", "first", "last", "diff", "zimsum",
+                                 "mimmax", "pfsum"])
+def test_sharded_equals_oracle(engines, batch, world, agg):
+    q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+    assert_groups_match(run_sharded(engines, batch, q, world), O.run_query(batch, q), agg, ctx=f"{agg} x{world}")
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_fill_rate_all(engines, batch, world):
+    cases = [
+        ("sum", dict(ds_function=abi.AGG["sum"], ds_interval_ms=60000, ds_fill=abi.FILL_NAN)),
+        ("avg", dict(ds_function=abi.AGG["max"], ds_interval_ms=300000, ds_fill=abi.FILL_ZERO)),
+        ("sum", dict(ds_function=abi.AGG["avg"], ds_interval_ms=60000, rate=True)),
+        ("sum", dict(ds_function=abi.AGG["sum"], ds_all=True)),
+    ]
+    for agg, kw in cases:
+        q = abi.new_query(T0, T0 + 3599, agg, **kw)
+        assert_groups_match(run_sharded(engines, batch, q, world), O.run_query(batch, q), agg, ctx=f"{kw} x{world}")
+
+
+def test_group_on_one_rank_only(engines):
+    """More ranks than groups: most ranks hold no span of most groups."""
+    b = synth.generate(12, T0, 360, 10000, value_kind=0, n_groups=2, seed=3)
+    for agg in ["min", "max", "sum", "dev"]:
+        q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+        assert_groups_match(run_sharded(engines, b, q, 4), O.run_query(b, q), agg, ctx=agg)
+
+
+def _worker(rank, world, port, out):
+    import torch.distributed as td
+    from opentsdb_amd.engine import Engine
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    td.init_process_group("gloo", rank=rank, world_size=world)
+    eng = Engine(0)
+    try:
+        b = synth.generate(150, T0, 360, 10000, value_kind=2, n_groups=7, int_mod=30000, seed=0x5EED)
+        eng.load(dist.shard_batch(b, rank, world))
+        q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+        groups = dist.run_distributed(eng, q, td, dist.n_groups_of(b))
+        np.savez(os.path.join(out, f"r{rank}.npz"), gid=np.array([g[0] for g in groups]),
+                 n=np.array([len(g[1]) for g in groups]), ts=np.concatenate([g[1] for g in groups]),
+                 bits=np.concatenate([g[2] for g in groups]), isi=np.concatenate([g[3] for g in groups]))
+    finally:
+        eng.close()
+        td.destroy_process_group()
+
+
+def test_two_process_gloo(tmp_path, batch):
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+    want = O.run_query(batch, q)
+    for r in range(2):
+        z = np.load(tmp_path / f"r{r}.npz")
+        cut = np.concatenate([[0], np.cumsum(z["n"])])
+        got = [(int(z["gid"][i]), z["ts"][cut[i]:cut[i + 1]], z["bits"][cut[i]:cut[i + 1]], z["isi"][cut[i]:cut[i + 1]])
+               for i in range(len(z["gid"]))]
+        assert_groups_match(got, want, "sum", ctx=f"gloo rank {r}")
