@@ -127,6 +127,7 @@ struct tsdbhip_ctx {
   std::vector<uint32_t> h_base;        // [n_rows]
   std::vector<uint32_t> h_ndp;         // [n_rows]
   std::vector<uint32_t> h_qlen, h_vlen;
+  std::vector<uint32_t> h_flags;       // [n_rows] RowDesc.flags after k_index
   std::vector<int32_t> h_group;        // [n_series] group of sorted position
   std::vector<int64_t> h_orig;         // [n_series] original batch index of sorted position
   // tiles over groups
@@ -138,7 +139,10 @@ struct tsdbhip_ctx {
   DevBuf n_tb, n_te, n_tg, n_gtp;
   // scratch
   DevBuf pa, pb, pn, pf, out_val, out_flag, gact, err, g_dense, g_pres, g_rate, redo, redo_n;
-  DevBuf xbuf, gbuf;                   // multi-GPU: this rank's partial states, gathered states
+  DevBuf xbuf, gbuf;
+  // raw path scratch
+  DevBuf r_rowpt, r_spoff, r_spn, r_grp, r_pts, r_rank, r_bm, r_wb, r_U, r_ooff, r_sg, r_su, r_ots, r_obits, r_oint,
+      r_gcur, r_gmask;                   // multi-GPU: this rank's partial states, gathered states
   // dominant uniform row class of the batch (k_fast specialisation), 0 = none
   int fast_qw = 0, fast_vl = 0;
   bool fast_used = false;
@@ -296,7 +300,9 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   release_batch(c);
   for (DevBuf* b : {&c->pa, &c->pb, &c->pn, &c->pf, &c->out_val, &c->out_flag, &c->gact, &c->err, &c->g_dense,
-                    &c->g_pres, &c->g_rate, &c->redo, &c->redo_n, &c->xbuf, &c->gbuf})
+                    &c->g_pres, &c->g_rate, &c->redo, &c->redo_n, &c->xbuf, &c->gbuf, &c->r_rowpt,
+                    &c->r_spoff, &c->r_spn, &c->r_grp, &c->r_pts, &c->r_rank, &c->r_bm, &c->r_wb, &c->r_U, &c->r_ooff,
+                    &c->r_sg, &c->r_su, &c->r_ots, &c->r_obits, &c->r_oint, &c->r_gcur, &c->r_gmask})
     b->release();
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -381,12 +387,14 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
   c->h_base.resize(c->n_rows);
   c->h_qlen.resize(c->n_rows);
   c->h_vlen.resize(c->n_rows);
+  c->h_flags.resize(c->n_rows);
   int64_t cls[2][2] = {{0, 0}, {0, 0}};   // [qw 2/4][vl 4/8] uniform float rows
   for (int64_t r = 0; r < c->n_rows; r++) {
     c->h_ndp[r] = back[r].ndp;
     c->h_base[r] = back[r].base;
     c->h_qlen[r] = back[r].qlen;
     c->h_vlen[r] = back[r].vlen;
+    c->h_flags[r] = back[r].flags;
     const uint32_t f = back[r].flags;
     const uint32_t qw = f & ROW_QW_MASK, vl = (f & ROW_VL_MASK) >> ROW_VL_SHIFT;
     if ((f & ROW_ALLF) && !(f & (ROW_ERR | ROW_NAN | ROW_UNSORTED)) && (qw == 2 || qw == 4) && (vl == 4 || vl == 8))
@@ -645,14 +653,22 @@ struct Plan {
   int64_t ss = 0, se = 0, B0 = 0, I = 1, K = 0;
   bool none = false;
   bool gslot = false;
+  bool raw = false;   // no downsampling: AggregationIterator over the raw timestamp union
 };
 
 int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
   if (q->aggregator < 0 || q->aggregator >= TSDB_AGG_COUNT_ALL) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad aggregator");
   if (q->ds_function >= TSDB_AGG_COUNT_ALL) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad downsampling function");
   if (q->ds_function == TSDB_AGG_NONE) return fail(TSDB_E_ILLEGAL_ARGUMENT, "cannot use the NONE aggregator for downsampling");
-  if (q->ds_function < 0)
-    return fail(TSDB_E_NOT_IMPLEMENTED, "queries without downsampling (raw union LERP) are not implemented yet");
+  if (q->ds_function < 0) {
+    P.raw = true;
+    P.ga = ga_of(q->aggregator);
+    if (P.ga < 0) return fail(TSDB_E_NOT_IMPLEMENTED, std::string("group-by aggregator not implemented yet: ") + AGG_NAMES[q->aggregator]);
+    P.interp = interp_of(q->aggregator);
+    P.none = q->aggregator == TSDB_AGG_NONE;
+    tsdbhip_scan_bounds(q, &P.ss, &P.se);
+    return 0;
+  }
   if (q->ds_calendar) return fail(TSDB_E_NOT_IMPLEMENTED, "calendar downsampling is not implemented yet");
   if (!q->ds_all && q->ds_interval_ms <= 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "interval not > 0");
   P.ga = ga_of(q->aggregator);
@@ -919,6 +935,233 @@ int collect(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bo
 
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// raw path (k_raw.hip): no downsampling
+// ---------------------------------------------------------------------------
+namespace {
+
+int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_result** out) {
+  const int64_t S = c->n_series;
+  const int64_t start = P.ss * 1000, end = P.se * 1000;
+  // points of every series inside the scan range (rows with base in [ss, se), Span order)
+  std::vector<int64_t> row_pt(std::max<int64_t>(1, c->n_rows), -1), sp_off(S + 1, 0);
+  std::vector<int32_t> sp_n(std::max<int64_t>(1, S), 0);
+  bool all_s = true, any_int = false, any_float = false;
+  int64_t np = 0;
+  for (int64_t s = 0; s < S; s++) {
+    sp_off[s] = np;
+    for (int64_t r = c->h_srp[s]; r < c->h_srp[s + 1]; r++) {
+      if ((int64_t)c->h_base[r] < P.ss || (int64_t)c->h_base[r] >= P.se) continue;
+      const uint32_t f = c->h_flags[r];
+      if (f & ROW_UNSORTED) return fail(TSDB_E_NOT_IMPLEMENTED, "raw path over a cell with unsorted datapoints");
+      if ((f & ROW_QW_MASK) != 2) all_s = false;
+      if (f & ROW_ALLF) any_float = true;
+      else { any_int = true; if (!(f & ROW_ALLI)) any_float = true; }
+      row_pt[r] = np;
+      np += c->h_ndp[r];
+    }
+    sp_n[s] = (int32_t)(np - sp_off[s]);
+  }
+  sp_off[S] = np;
+  // groups: dense batch groups, or one per span for NONE (TsdbQuery.java:941-962)
+  std::vector<int64_t> grp_ser;
+  std::vector<int64_t> gid_of;   // result group id of each group row
+  if (P.none) {
+    std::vector<std::pair<int64_t, int64_t>> tmp;
+    for (int64_t s = 0; s < S; s++) if (sp_n[s] > 0) tmp.push_back({c->h_orig[s], s});
+    std::sort(tmp.begin(), tmp.end());
+    // NONE groups must be contiguous series ranges: one series each, in resident order
+    grp_ser.resize(S + 1);
+    for (int64_t s = 0; s <= S; s++) grp_ser[s] = s;
+    gid_of.assign(S, -1);
+    for (size_t i = 0; i < tmp.size(); i++) gid_of[tmp[i].second] = (int64_t)i;
+  } else {
+    grp_ser.assign(c->n_groups + 1, 0);
+    for (int64_t g = 0, s = 0; g < c->n_groups; g++) {
+      grp_ser[g] = s;
+      while (s < S && c->h_group[s] == g) s++;
+      grp_ser[g + 1] = s;
+    }
+  }
+  const int64_t G = (int64_t)grp_ser.size() - 1;
+  std::vector<uint8_t> act(std::max<int64_t>(1, G), 0);
+  for (int64_t g = 0; g < G; g++)
+    for (int64_t s = grp_ser[g]; s < grp_ser[g + 1]; s++) if (sp_n[s] > 0) { act[g] = 1; break; }
+  // device arrays
+  const int64_t R = std::max<int64_t>(1, c->n_rows);
+  HIP_OK(c->r_rowpt.ensure(R * 8));
+  HIP_OK(c->r_spoff.ensure((S + 1) * 8));
+  HIP_OK(c->r_spn.ensure(std::max<int64_t>(1, S) * 4));
+  HIP_OK(c->r_grp.ensure((G + 1) * 8));
+  HIP_OK(c->r_pts.ensure(std::max<int64_t>(1, np) * sizeof(RawPt)));
+  HIP_OK(c->r_rank.ensure(std::max<int64_t>(1, np) * 4));
+  HIP_OK(hipMemcpyAsync(c->r_rowpt.p, row_pt.data(), R * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipMemcpyAsync(c->r_spoff.p, sp_off.data(), (S + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipMemcpyAsync(c->r_spn.p, sp_n.data(), std::max<int64_t>(1, S) * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipMemcpyAsync(c->r_grp.p, grp_ser.data(), (G + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
+  RawParams rp{};
+  rp.rows = c->rows.as<RowDesc>();
+  rp.qual = c->qual.as<uint8_t>();
+  rp.val = c->val.as<uint8_t>();
+  rp.n_rows = c->n_rows;
+  rp.row_pt_off = c->r_rowpt.as<int64_t>();
+  rp.pts = c->r_pts.as<RawPt>();
+  rp.n_series = S;
+  rp.sp_off = c->r_spoff.as<int64_t>();
+  rp.sp_n = c->r_spn.as<int32_t>();
+  rp.rate = q->rate;
+  rp.counter = q->rate_counter;
+  rp.drop = q->rate_drop_resets;
+  rp.counter_max = q->rate_counter_max;
+  rp.reset_value = q->rate_reset_value;
+  rp.start_ms = start;
+  rp.gran = all_s ? 1000 : 1;
+  const int64_t nbits = std::max<int64_t>(1, (end - start + rp.gran - 1) / rp.gran);
+  rp.W = (nbits + 31) / 32;
+  rp.grp_ser = c->r_grp.as<int64_t>();
+  rp.rank = c->r_rank.as<int32_t>();
+  rp.ga = P.ga;
+  rp.interp = P.interp;
+  rp.do_long = !q->rate && any_int;
+  rp.do_double = q->rate || any_float;
+  if (!rp.do_long && !rp.do_double) rp.do_double = 1;
+  rp.err = c->err.as<int32_t>();
+  HIP_OK(hipEventRecord(c->ev[0], c->stream));
+  HIP_OK(launch_raw_decode(rp, c->stream));
+  if (q->rate) {
+    HIP_OK(launch_raw_rate(rp, c->stream));
+    HIP_OK(hipMemcpyAsync(sp_n.data(), c->r_spn.p, std::max<int64_t>(1, S) * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+  }
+  // group chunks whose timestamp bitmaps fit the budget
+  const int64_t budget = (int64_t)2 << 30;
+  const int64_t per_chunk = std::max<int64_t>(1, budget / (rp.W * 8));
+  std::vector<int64_t> res_ts;
+  std::vector<uint64_t> res_bits;
+  std::vector<uint8_t> res_int;
+  std::vector<int64_t> g_ptr(G + 1, 0);
+  double eval_ms = 0.0;
+  for (int64_t g0 = 0; g0 < G; g0 += per_chunk) {
+    const int64_t g1 = std::min(G, g0 + per_chunk);
+    const int64_t ng = g1 - g0;
+    rp.g0 = g0;
+    rp.g1 = g1;
+    HIP_OK(c->r_bm.ensure(ng * rp.W * 4));
+    HIP_OK(c->r_wb.ensure(ng * rp.W * 4));
+    HIP_OK(c->r_U.ensure(ng * 4));
+    rp.bitmap = c->r_bm.as<uint32_t>();
+    rp.wbase = c->r_wb.as<uint32_t>();
+    rp.U = c->r_U.as<int32_t>();
+    HIP_OK(hipMemsetAsync(rp.bitmap, 0, ng * rp.W * 4, c->stream));
+    HIP_OK(launch_raw_union(rp, grp_ser[g0], grp_ser[g1], c->stream));
+    std::vector<int32_t> U(ng);
+    HIP_OK(hipMemcpyAsync(U.data(), rp.U, ng * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    std::vector<int64_t> ooff(ng + 1, 0);
+    std::vector<int32_t> sg, su;
+    int64_t kmax = 1;
+    for (int64_t i = 0; i < ng; i++) {
+      ooff[i + 1] = ooff[i] + U[i];
+      for (int64_t u = 0; u < U[i]; u += RAW_STRIP) { sg.push_back((int32_t)i); su.push_back((int32_t)u); }
+      if (U[i] > 0) kmax = std::max(kmax, grp_ser[g0 + i + 1] - grp_ser[g0 + i]);
+    }
+    const int64_t nout = ooff[ng];
+    const int64_t ns = (int64_t)sg.size();
+    HIP_OK(c->r_ooff.ensure((ng + 1) * 8));
+    HIP_OK(c->r_sg.ensure(std::max<int64_t>(1, ns) * 4));
+    HIP_OK(c->r_su.ensure(std::max<int64_t>(1, ns) * 4));
+    HIP_OK(c->r_ots.ensure(std::max<int64_t>(1, nout) * 8));
+    HIP_OK(c->r_obits.ensure(std::max<int64_t>(1, nout) * 8));
+    HIP_OK(c->r_oint.ensure(std::max<int64_t>(1, nout)));
+    HIP_OK(hipMemcpyAsync(c->r_ooff.p, ooff.data(), (ng + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    if (ns) {
+      HIP_OK(hipMemcpyAsync(c->r_sg.p, sg.data(), ns * 4, hipMemcpyHostToDevice, c->stream));
+      HIP_OK(hipMemcpyAsync(c->r_su.p, su.data(), ns * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    rp.out_off = c->r_ooff.as<int64_t>();
+    rp.strip_g = c->r_sg.as<int32_t>();
+    rp.strip_u = c->r_su.as<int32_t>();
+    rp.n_strips = ns;
+    rp.out_ts = c->r_ots.as<int64_t>();
+    rp.out_bits = c->r_obits.as<uint64_t>();
+    rp.out_int = c->r_oint.as<uint8_t>();
+    rp.kmax = (int32_t)kmax;
+    if (kmax > RAW_LDS_SPANS) {
+      HIP_OK(c->r_gcur.ensure(std::max<int64_t>(1, ns * kmax) * 4));
+      HIP_OK(c->r_gmask.ensure(std::max<int64_t>(1, ns * kmax) * 8));
+      rp.g_cur = c->r_gcur.as<int32_t>();
+      rp.g_mask = c->r_gmask.as<uint64_t>();
+    }
+    HIP_OK(launch_raw_rank(rp, grp_ser[g0], grp_ser[g1], c->stream));
+    HIP_OK(hipEventRecord(c->ev[3], c->stream));
+    HIP_OK(launch_raw_eval(rp, c->stream));
+    HIP_OK(hipEventRecord(c->ev[1], c->stream));
+    const size_t base = res_ts.size();
+    res_ts.resize(base + nout);
+    res_bits.resize(base + nout);
+    res_int.resize(base + nout);
+    if (nout) {
+      HIP_OK(hipMemcpyAsync(res_ts.data() + base, rp.out_ts, nout * 8, hipMemcpyDeviceToHost, c->stream));
+      HIP_OK(hipMemcpyAsync(res_bits.data() + base, rp.out_bits, nout * 8, hipMemcpyDeviceToHost, c->stream));
+      HIP_OK(hipMemcpyAsync(res_int.data() + base, rp.out_int, nout, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_OK(hipStreamSynchronize(c->stream));
+    float te = 0;
+    (void)hipEventElapsedTime(&te, c->ev[3], c->ev[1]);
+    eval_ms += te;
+    for (int64_t i = 0; i < ng; i++) g_ptr[g0 + i + 1] = (int64_t)base + ooff[i + 1];
+  }
+  int32_t err = 0;
+  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  float t01 = 0;
+  (void)hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
+  c->fast_used = false;
+  c->timing.decode_downsample_ms = t01;
+  c->timing.group_reduce_ms = eval_ms;
+  c->timing.total_ms = t01;
+  c->timing.fast_ms = 0;
+  c->timing.tiles = G;
+  c->timing.redo_tiles = 0;
+  account(c, P);
+  if (err) return fail(err, "error raised by the device path");
+  // result: emitted groups in emission order
+  std::vector<std::pair<int64_t, int64_t>> order;   // (result group id, group row)
+  for (int64_t g = 0; g < G; g++) {
+    if (!act[g]) continue;
+    order.push_back({P.none ? gid_of[g] : g, g});
+  }
+  std::sort(order.begin(), order.end());
+  int64_t npts = 0;
+  for (auto& o : order) npts += g_ptr[o.second + 1] - g_ptr[o.second];
+  tsdbhip_result* r = make_result((int64_t)order.size(), npts);
+  if (!r) return fail(TSDB_E_NOMEM, "result allocation");
+  auto* gptr = const_cast<int64_t*>(r->group_ptr);
+  auto* gid = const_cast<int32_t*>(r->group_id);
+  auto* ts = const_cast<int64_t*>(r->ts_ms);
+  auto* vb = const_cast<uint64_t*>(r->value_bits);
+  auto* isi = const_cast<uint8_t*>(r->is_int);
+  int64_t o = 0;
+  for (size_t i = 0; i < order.size(); i++) {
+    const int64_t g = order[i].second;
+    gptr[i] = o;
+    gid[i] = (int32_t)order[i].first;
+    const int64_t a = g_ptr[g], n = g_ptr[g + 1] - a;
+    if (n) {
+      std::memcpy(ts + o, res_ts.data() + a, n * 8);
+      std::memcpy(vb + o, res_bits.data() + a, n * 8);
+      std::memcpy(isi + o, res_int.data() + a, n);
+    }
+    o += n;
+  }
+  gptr[order.size()] = o;
+  *out = r;
+  return 0;
+}
+
+}  // namespace
+
 extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
   if (!c || !q || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
@@ -928,6 +1171,7 @@ extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_resul
   int rc = plan_query(c, q, P);
   if (rc) return rc;
   const int64_t G = P.none ? c->n_series : c->n_groups;
+  if (P.raw) return run_raw(c, q, P, out);
   rc = run_device(c, q, P, G, true);
   if (rc) return rc;
   return collect(c, q, P, G, true, out);
@@ -966,6 +1210,7 @@ int plan_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_globa
   int rc = plan_query(c, q, P);
   if (rc) return rc;
   if (P.none) return fail(TSDB_E_NOT_IMPLEMENTED, "NONE aggregator is per-span; it has no cross-rank exchange");
+  if (P.raw) return fail(TSDB_E_NOT_IMPLEMENTED, "multi-GPU raw (union LERP) queries are not implemented yet");
   if (n_groups_global < c->n_groups) return fail(TSDB_E_ILLEGAL_ARGUMENT, "n_groups_global smaller than the local groups");
   return 0;
 }

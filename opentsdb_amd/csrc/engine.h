@@ -32,6 +32,7 @@ enum : uint32_t {
   ROW_NEGZ = 0x80000,       // some value is -0.0
   ROW_UNSORTED = 0x100000,  // datapoint offsets not strictly increasing
   ROW_SFIRST = 0x200000,    // first row of its series (set by the host at load)
+  ROW_ALLI = 0x400000,      // every value is an integer
 };
 
 // Per-tile partial group state, structure of arrays, [tile][K].
@@ -130,6 +131,56 @@ struct RankMergeParams {
   int32_t* err;
 };
 
+// ---- raw path (no downsampling): AggregationIterator over the timestamp union ----
+// A decoded datapoint: tsf = timestamp (ms) | RAW_FLOAT when the value bits are a double
+// (AggregationIterator keeps exactly this FLAG_FLOAT encoding, src/core/AggregationIterator.java:112-118).
+struct RawPt {
+  int64_t tsf;
+  uint64_t bits;
+};
+static constexpr int64_t RAW_FLOAT = (int64_t)0x8000000000000000ULL;
+static constexpr int64_t RAW_TIME_MASK = 0x7FFFFFFFFFFFFFFFLL;
+static constexpr int RAW_STRIP = 1024;     // union points per k_raw_eval wave
+static constexpr int RAW_LDS_SPANS = 4096; // spans whose cursors fit in LDS
+
+struct RawParams {
+  // decode
+  const RowDesc* rows;
+  const uint8_t* qual;
+  const uint8_t* val;
+  int64_t n_rows;
+  const int64_t* row_pt_off;   // [n_rows] first point of the row, -1 outside the scan range
+  RawPt* pts;                  // [n_pts]
+  // series (resident, group-sorted order)
+  int64_t n_series;
+  const int64_t* sp_off;       // [n_series + 1] point range of each series
+  int32_t* sp_n;               // [n_series] points (rate mode: kept rate points, compacted in place)
+  // rate (RateSpan, src/core/RateSpan.java:121-180)
+  int32_t rate, counter, drop;
+  int64_t counter_max, reset_value;
+  // union of timestamps, one chunk of groups [g0, g1) at a time
+  int64_t start_ms, gran, W;   // bitmap origin, granularity (ms), words per group
+  int64_t g0, g1;
+  const int64_t* grp_ser;      // [G + 1] series range of each group
+  uint32_t* bitmap;            // [(g1 - g0) * W]
+  uint32_t* wbase;             // [(g1 - g0) * W] exclusive popcount prefix
+  int32_t* U;                  // [g1 - g0] union size
+  int32_t* rank;               // [n_pts] union points strictly before the point
+  // evaluation
+  const int64_t* out_off;      // [g1 - g0] chunk-relative output offset of each group
+  const int32_t* strip_g;      // [n_strips] chunk-relative group
+  const int32_t* strip_u;      // [n_strips] first union point
+  int64_t n_strips;
+  int32_t ga, interp, do_long, do_double;
+  int64_t* out_ts;
+  uint64_t* out_bits;
+  uint8_t* out_int;
+  int32_t* g_cur;              // [n_strips][kmax] cursors when kmax > RAW_LDS_SPANS
+  uint64_t* g_mask;
+  int32_t kmax;
+  int32_t* err;
+};
+
 struct SynthParams {
   int64_t n_series, n_groups, n_rows_per_series, n_points;
   int64_t start_ms, period_ms;
@@ -164,6 +215,12 @@ template <int F> hipError_t launch_grid_inst(const GridParams& p, hipStream_t s)
 template <int F> hipError_t launch_fast_inst(const GridParams& p, int qw, int vl, hipStream_t s);
 int64_t grid_wave_lds(int64_t K, bool rate, bool gslot);
 hipError_t launch_synth_sizes(const SynthParams& p, hipStream_t s);
+// raw path (k_raw.hip)
+hipError_t launch_raw_decode(const RawParams& p, hipStream_t s);
+hipError_t launch_raw_rate(const RawParams& p, hipStream_t s);
+hipError_t launch_raw_union(const RawParams& p, int64_t s_begin, int64_t s_end, hipStream_t s);  // mark + scan
+hipError_t launch_raw_rank(const RawParams& p, int64_t s_begin, int64_t s_end, hipStream_t s);   // rank + union ts
+hipError_t launch_raw_eval(const RawParams& p, hipStream_t s);
 hipError_t launch_synth_write(const SynthParams& p, hipStream_t s);
 
 }  // namespace tsdb

@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual,
     }
     // walk every datapoint: validate qualifier/value lengths, certificate stats
     bool bad = qlen == 0;
-    bool allf = true, hasnan = false, negz = false, unsorted = false;
+    bool allf = true, alli = true, hasnan = false, negz = false, unsorted = false;
     int lsbmin = INT32_MAX;
     double amax = 0.0;
     long long vcarry = 0;
@@ -113,6 +113,7 @@ __global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual,
       if (in && off <= po) unsorted = true;
       prev_off = __shfl(off, (int)min((uint32_t)63, ndp - 1 - i0), 64);
       if (in && !fl) allf = false;
+      if (in && fl) alli = false;
       if (in && (fl ? (len != 4 && len != 8) : (len == 3 || (len >= 5 && len <= 7)))) bad = true;
       const int incl = wave_incl_sum(len);
       const long long vo = vcarry + incl - len;
@@ -134,6 +135,7 @@ __global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual,
     if (vcarry > (long long)d.vlen) bad = true;
     bad = __any(bad);
     allf = __all(allf);
+    alli = __all(alli);
     hasnan = __any(hasnan);
     negz = __any(negz);
     unsorted = __any(unsorted);
@@ -146,6 +148,7 @@ __global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual,
         set_err(err, TSDB_E_ILLEGAL_DATA);
       }
       if (allf) flags |= ROW_ALLF;
+      if (alli) flags |= ROW_ALLI;
       if (hasnan) flags |= ROW_NAN;
       if (negz) flags |= ROW_NEGZ;
       if (unsorted) flags |= ROW_UNSORTED;

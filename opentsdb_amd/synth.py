@@ -115,3 +115,97 @@ def generate(n_series: int, start_s: int, n_points: int, period_ms: int, value_k
     vo[1:] = np.cumsum([len(x) for x in vals])
     return abi.HostBatch(np.array(row_ptr, np.int64), np.array(row_base, np.uint32), qo, vo,
                          np.frombuffer(b"".join(quals), np.uint8), np.frombuffer(b"".join(vals), np.uint8), grp)
+
+
+def encode_rows(ts_ms, lvals, fvals, kind, ms):
+    """Compacted hour rows of one series, as TSDB.addPoint + CompactionQueue write them.
+
+    Per point: ts_ms (sorted, distinct), kind 0 = long (vle 1/2/4/8 B), 1 = float32 (4 B),
+    2 = float64 (8 B); ms = millisecond qualifier (4 B, src/core/Internal.java:848-856) or
+    second qualifier (2 B).  A row mixing both carries meta byte MS_MIXED_COMPACT (0x01,
+    src/core/Const.java:83; CompactionQueue.java:594-612).  Returns [(base_s, qual, val)]."""
+    ts_ms = np.asarray(ts_ms, np.int64)
+    bases = (ts_ms // 1000) - (ts_ms // 1000) % 3600
+    rows = []
+    a = 0
+    n = len(ts_ms)
+    while a < n:
+        b = a
+        while b < n and bases[b] == bases[a]:
+            b += 1
+        base = int(bases[a])
+        q, v = [], []
+        any_ms = any_s = False
+        for j in range(a, b):
+            off = int(ts_ms[j]) - base * 1000
+            if kind[j] == 0:
+                x = int(lvals[j])
+                L = 1 if -128 <= x <= 127 else 2 if -32768 <= x <= 32767 else 4 if -(1 << 31) <= x < (1 << 31) else 8
+                flags = L - 1
+                vb = x.to_bytes(L, "big", signed=True)
+            elif kind[j] == 1:
+                flags = 0xB
+                vb = np.array([fvals[j]], ">f4").tobytes()   # (numpy scalars are always native-endian)
+            else:
+                flags = 0xF
+                vb = np.array([fvals[j]], ">f8").tobytes()
+            if ms[j]:
+                any_ms = True
+                q.append((0xF0000000 | (off << 6) | flags).to_bytes(4, "big"))
+            else:
+                any_s = True
+                assert off % 1000 == 0
+                q.append((((off // 1000) << 4) | flags).to_bytes(2, "big"))
+            v.append(vb)
+        val = b"".join(v)
+        if b - a > 1:
+            val += b"\x01" if (any_ms and any_s) else b"\x00"
+        rows.append((base, b"".join(q), val))
+        a = b
+    return rows
+
+
+def from_series(series_rows, group_ids) -> abi.HostBatch:
+    """HostBatch from per-series row lists (encode_rows output) and group ids."""
+    quals, vals, row_base = [], [], []
+    row_ptr = [0]
+    for rows in series_rows:
+        for base, q, v in rows:
+            row_base.append(base)
+            quals.append(q)
+            vals.append(v)
+        row_ptr.append(len(row_base))
+    qo = np.zeros(len(quals) + 1, np.uint64)
+    vo = np.zeros(len(vals) + 1, np.uint64)
+    qo[1:] = np.cumsum([len(x) for x in quals])
+    vo[1:] = np.cumsum([len(x) for x in vals])
+    qb = np.frombuffer(b"".join(quals), np.uint8) if quals else np.zeros(0, np.uint8)
+    vb = np.frombuffer(b"".join(vals), np.uint8) if vals else np.zeros(0, np.uint8)
+    return abi.HostBatch(np.array(row_ptr, np.int64), np.array(row_base, np.uint32), qo, vo, qb, vb,
+                         np.asarray(group_ids, np.int32))
+
+
+def generate_counters(n_series: int, start_s: int, n_points: int, period_ms: int = 10000,
+                      jitter_ms: int = 4000, n_groups: int = 64, reset_p: float = 1.0 / 500,
+                      seed: int = 0x5EED) -> abi.HostBatch:
+    """BASELINE config 4 shape: jittered millisecond timestamps (nominal period, uniform
+    integer jitter in [-jitter, +jitter]), monotone counters (start [0, 1e9), increments
+    [0, 1000)) that reset to [0, 100) with probability reset_p per point.  Series i
+    belongs to group i % n_groups; batch in group-major order."""
+    order, grp = series_order(n_series, n_groups)
+    rows = []
+    for i in order:
+        rng = np.random.default_rng([seed, int(i)])
+        k = np.arange(n_points, dtype=np.int64)
+        ts = start_s * 1000 + k * period_ms + rng.integers(-jitter_ms, jitter_ms + 1, n_points)
+        assert period_ms > 2 * jitter_ms, "jitter must keep timestamps strictly increasing"
+        inc = rng.integers(0, 1000, n_points)
+        v = np.empty(n_points, np.int64)
+        cur = int(rng.integers(0, 1_000_000_000))
+        resets = rng.random(n_points) < reset_p
+        rv = rng.integers(0, 100, n_points)
+        for j in range(n_points):
+            cur = int(rv[j]) if resets[j] else cur + int(inc[j])
+            v[j] = cur
+        rows.append(encode_rows(ts, v, None, np.zeros(n_points, np.int64), np.ones(n_points, bool)))
+    return from_series(rows, grp)

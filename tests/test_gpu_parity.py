@@ -56,7 +56,7 @@ def assert_groups_match(got, want, agg, tol=None, ctx=""):
 
 # ---- reference known answers (downsampled queries) through the engine --------------
 QUERIES = G.load("queries.json")
-GRID_CASES = [c for c in QUERIES["cases"] if c.get("downsample")]
+GRID_CASES = QUERIES["cases"]
 
 
 @pytest.mark.parametrize("case", GRID_CASES, ids=[c["name"] for c in GRID_CASES])
