@@ -46,6 +46,25 @@ def group_sorted_order(batch: abi.HostBatch):
     return keep[np.argsort(g[keep], kind="stable")]
 
 
+def select_series(batch: abi.HostBatch, series) -> abi.HostBatch:
+    """A batch holding only `series` (indices, in the given order); group ids unchanged."""
+    srp = batch.series_row_ptr
+    qo, vo = batch.row_qual_off.astype(np.int64), batch.row_val_off.astype(np.int64)
+    series = np.asarray(series, np.int64)
+    rows = [np.arange(srp[s], srp[s + 1]) for s in series]
+    rows = np.concatenate(rows) if rows else np.zeros(0, np.int64)
+    new_srp = np.zeros(len(series) + 1, np.int64)
+    if len(series):
+        new_srp[1:] = np.cumsum(srp[series + 1] - srp[series])
+    ql = qo[rows + 1] - qo[rows]
+    vl = vo[rows + 1] - vo[rows]
+    nqo = np.concatenate([[0], np.cumsum(ql)]).astype(np.uint64)
+    nvo = np.concatenate([[0], np.cumsum(vl)]).astype(np.uint64)
+    q = np.concatenate([batch.qual[qo[r]:qo[r + 1]] for r in rows]) if len(rows) else np.zeros(0, np.uint8)
+    v = np.concatenate([batch.val[vo[r]:vo[r + 1]] for r in rows]) if len(rows) else np.zeros(0, np.uint8)
+    return abi.HostBatch(new_srp, batch.row_base_time[rows], nqo, nvo, q, v, batch.group_id[series])
+
+
 def shard_batch(batch: abi.HostBatch, rank: int, world: int) -> abi.HostBatch:
     """The rank's shard of a host batch (group ids stay global)."""
     order = group_sorted_order(batch)
@@ -53,18 +72,7 @@ def shard_batch(batch: abi.HostBatch, rank: int, world: int) -> abi.HostBatch:
     qo, vo = batch.row_qual_off.astype(np.int64), batch.row_val_off.astype(np.int64)
     sbytes = [(qo[srp[s + 1]] - qo[srp[s]]) + (vo[srp[s + 1]] - vo[srp[s]]) for s in order]
     b = shard_bounds(sbytes, world)
-    mine = order[b[rank]:b[rank + 1]]
-    rows = [np.arange(srp[s], srp[s + 1]) for s in mine]
-    rows = np.concatenate(rows) if rows else np.zeros(0, np.int64)
-    new_srp = np.zeros(len(mine) + 1, np.int64)
-    new_srp[1:] = np.cumsum([srp[s + 1] - srp[s] for s in mine]) if len(mine) else []
-    ql = (qo[rows + 1] - qo[rows]) if len(rows) else np.zeros(0, np.int64)
-    vl = (vo[rows + 1] - vo[rows]) if len(rows) else np.zeros(0, np.int64)
-    nqo = np.concatenate([[0], np.cumsum(ql)]).astype(np.uint64)
-    nvo = np.concatenate([[0], np.cumsum(vl)]).astype(np.uint64)
-    q = np.concatenate([batch.qual[qo[r]:qo[r + 1]] for r in rows]) if len(rows) else np.zeros(0, np.uint8)
-    v = np.concatenate([batch.val[vo[r]:vo[r + 1]] for r in rows]) if len(rows) else np.zeros(0, np.uint8)
-    return abi.HostBatch(new_srp, batch.row_base_time[rows], nqo, nvo, q, v, batch.group_id[mine])
+    return select_series(batch, order[b[rank]:b[rank + 1]])
 
 
 def n_groups_of(batch: abi.HostBatch) -> int:

@@ -185,27 +185,76 @@ def from_series(series_rows, group_ids) -> abi.HostBatch:
                          np.asarray(group_ids, np.int32))
 
 
+def _h(seed: int, i: np.ndarray, k: np.ndarray, salt: int) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        return splitmix64(np.uint64(seed ^ salt) ^ (i.astype(np.uint64) << np.uint64(32)) ^ k.astype(np.uint64))
+
+
 def generate_counters(n_series: int, start_s: int, n_points: int, period_ms: int = 10000,
                       jitter_ms: int = 4000, n_groups: int = 64, reset_p: float = 1.0 / 500,
                       seed: int = 0x5EED) -> abi.HostBatch:
-    """BASELINE config 4 shape: jittered millisecond timestamps (nominal period, uniform
-    integer jitter in [-jitter, +jitter]), monotone counters (start [0, 1e9), increments
-    [0, 1000)) that reset to [0, 100) with probability reset_p per point.  Series i
-    belongs to group i % n_groups; batch in group-major order."""
+    """BASELINE config 4 shape, vectorised: jittered millisecond timestamps (nominal period,
+    uniform integer jitter in [-jitter, +jitter]), monotone counters (start [0, 1e9),
+    increments [0, 1000)) that reset to [0, 100) with probability ~reset_p per point.  Every
+    draw is a splitmix64 hash of (seed, global series id i, point k).  Series i belongs to
+    group i % n_groups; the batch is group-major.  Cells are what TSDB.addPoint(long) with
+    millisecond timestamps + compaction write: 4-byte ms qualifiers, vle values, meta 0x00."""
+    assert period_ms > 2 * jitter_ms, "jitter must keep timestamps strictly increasing"
     order, grp = series_order(n_series, n_groups)
-    rows = []
-    for i in order:
-        rng = np.random.default_rng([seed, int(i)])
-        k = np.arange(n_points, dtype=np.int64)
-        ts = start_s * 1000 + k * period_ms + rng.integers(-jitter_ms, jitter_ms + 1, n_points)
-        assert period_ms > 2 * jitter_ms, "jitter must keep timestamps strictly increasing"
-        inc = rng.integers(0, 1000, n_points)
-        v = np.empty(n_points, np.int64)
-        cur = int(rng.integers(0, 1_000_000_000))
-        resets = rng.random(n_points) < reset_p
-        rv = rng.integers(0, 100, n_points)
-        for j in range(n_points):
-            cur = int(rv[j]) if resets[j] else cur + int(inc[j])
-            v[j] = cur
-        rows.append(encode_rows(ts, v, None, np.zeros(n_points, np.int64), np.ones(n_points, bool)))
-    return from_series(rows, grp)
+    S, P = len(order), n_points
+    I = np.repeat(order, P).reshape(S, P)
+    K = np.tile(np.arange(P, dtype=np.int64), S).reshape(S, P)
+    jit = (_h(seed, I, K, 0x11) % np.uint64(2 * jitter_ms + 1)).astype(np.int64) - jitter_ms
+    ts = start_s * 1000 + K * period_ms + jit
+    inc = (_h(seed, I, K, 0x22) % np.uint64(1000)).astype(np.int64)
+    reset = (_h(seed, I, K, 0x33).astype(np.float64) / 18446744073709551616.0) < reset_p
+    rval = (_h(seed, I, K, 0x44) % np.uint64(100)).astype(np.int64)
+    start = (_h(seed, I[:, :1], K[:, :1], 0x55) % np.uint64(1_000_000_000)).astype(np.int64)
+    # value[k] = value at the last reset (or the start) + increments since
+    step = np.where(reset, 0, inc)
+    step[:, 0] = np.where(reset[:, 0], 0, inc[:, 0])
+    anchor = np.where(reset, rval, 0)
+    anchor[:, 0] = np.where(reset[:, 0], rval[:, 0], start[:, 0] + inc[:, 0])
+    step[:, 0] = 0
+    cs = np.cumsum(step, axis=1)
+    seg = np.maximum.accumulate(np.where(reset | (K == 0), K, 0), axis=1)
+    base_v = np.take_along_axis(anchor, seg, axis=1)
+    v = base_v + cs - np.take_along_axis(cs, seg, axis=1)
+    # vle lengths and the flat byte layout (rows split at hour boundaries)
+    L = vle_lengths(v)
+    bases = (ts // 1000) - (ts // 1000) % 3600
+    newrow = np.ones((S, P), bool)
+    newrow[:, 1:] = bases[:, 1:] != bases[:, :-1]
+    flat_new = newrow.ravel()
+    row_id = np.cumsum(flat_new) - 1
+    n_rows = int(row_id[-1]) + 1
+    row_start = np.flatnonzero(flat_new)
+    row_n = np.diff(np.concatenate([row_start, [S * P]]))
+    row_base = bases.ravel()[row_start].astype(np.uint32)
+    series_of_row = row_start // P
+    row_ptr = np.searchsorted(series_of_row, np.arange(S + 1), side="left").astype(np.int64)
+    # qualifiers: 4 B each
+    off = ts.ravel() - bases.ravel() * 1000
+    q = (np.uint32(0xF0000000) | (off.astype(np.uint32) << np.uint32(6)) | (L.ravel() - 1).astype(np.uint32))
+    qual = q.astype(">u4").view(np.uint8)
+    qo = np.zeros(n_rows + 1, np.uint64)
+    qo[1:] = np.cumsum(row_n * 4)
+    # values: vle bytes + one meta byte per multi-point row
+    Lf = L.ravel()
+    row_vbytes = np.add.reduceat(Lf, row_start) + (row_n > 1)
+    vo = np.zeros(n_rows + 1, np.uint64)
+    vo[1:] = np.cumsum(row_vbytes)
+    # byte position of each point's value
+    excl = np.cumsum(Lf) - Lf
+    row_excl0 = excl[row_start]
+    pos = vo[row_id].astype(np.int64) + (excl - row_excl0[row_id])
+    val = np.zeros(int(vo[-1]), np.uint8)
+    vf = v.ravel()
+    for nb in (1, 2, 4, 8):
+        sel = np.flatnonzero(Lf == nb)
+        if not len(sel):
+            continue
+        be = vf[sel].astype(">i8").view(np.uint8).reshape(-1, 8)[:, 8 - nb:]
+        idx = pos[sel][:, None] + np.arange(nb)[None, :]
+        val[idx.ravel()] = be.ravel()
+    return abi.HostBatch(row_ptr, row_base, qo, vo, qual, val, grp)
