@@ -142,7 +142,7 @@ struct tsdbhip_ctx {
   DevBuf xbuf, gbuf;
   // raw path scratch
   DevBuf r_rowpt, r_spoff, r_spn, r_grp, r_pts, r_rank, r_bm, r_wb, r_U, r_ooff, r_sg, r_su, r_ots, r_obits, r_oint,
-      r_gcur, r_gmask;                   // multi-GPU: this rank's partial states, gathered states
+      r_coff, r_cur;                   // multi-GPU: this rank's partial states, gathered states
   // dominant uniform row class of the batch (k_fast specialisation), 0 = none
   int fast_qw = 0, fast_vl = 0;
   bool fast_used = false;
@@ -302,7 +302,7 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   for (DevBuf* b : {&c->pa, &c->pb, &c->pn, &c->pf, &c->out_val, &c->out_flag, &c->gact, &c->err, &c->g_dense,
                     &c->g_pres, &c->g_rate, &c->redo, &c->redo_n, &c->xbuf, &c->gbuf, &c->r_rowpt,
                     &c->r_spoff, &c->r_spn, &c->r_grp, &c->r_pts, &c->r_rank, &c->r_bm, &c->r_wb, &c->r_U, &c->r_ooff,
-                    &c->r_sg, &c->r_su, &c->r_ots, &c->r_obits, &c->r_oint, &c->r_gcur, &c->r_gmask})
+                    &c->r_sg, &c->r_su, &c->r_ots, &c->r_obits, &c->r_oint, &c->r_coff, &c->r_cur})
     b->release();
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1058,42 +1058,41 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
     std::vector<int32_t> U(ng);
     HIP_OK(hipMemcpyAsync(U.data(), rp.U, ng * 4, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
-    std::vector<int64_t> ooff(ng + 1, 0);
-    std::vector<int32_t> sg, su;
-    int64_t kmax = 1;
+    std::vector<int64_t> ooff(ng + 1, 0), coff(ng + 1, 0);
+    std::vector<int32_t> sg, st;
     for (int64_t i = 0; i < ng; i++) {
       ooff[i + 1] = ooff[i] + U[i];
-      for (int64_t u = 0; u < U[i]; u += RAW_STRIP) { sg.push_back((int32_t)i); su.push_back((int32_t)u); }
-      if (U[i] > 0) kmax = std::max(kmax, grp_ser[g0 + i + 1] - grp_ser[g0 + i]);
+      const int64_t nst = (U[i] + RAW_STRIP - 1) / RAW_STRIP;
+      for (int64_t t = 0; t < nst; t++) { sg.push_back((int32_t)i); st.push_back((int32_t)t); }
+      coff[i + 1] = coff[i] + nst * (grp_ser[g0 + i + 1] - grp_ser[g0 + i]);
     }
     const int64_t nout = ooff[ng];
     const int64_t ns = (int64_t)sg.size();
     HIP_OK(c->r_ooff.ensure((ng + 1) * 8));
+    HIP_OK(c->r_coff.ensure((ng + 1) * 8));
+    HIP_OK(c->r_cur.ensure(std::max<int64_t>(1, coff[ng]) * 4));
     HIP_OK(c->r_sg.ensure(std::max<int64_t>(1, ns) * 4));
     HIP_OK(c->r_su.ensure(std::max<int64_t>(1, ns) * 4));
     HIP_OK(c->r_ots.ensure(std::max<int64_t>(1, nout) * 8));
     HIP_OK(c->r_obits.ensure(std::max<int64_t>(1, nout) * 8));
     HIP_OK(c->r_oint.ensure(std::max<int64_t>(1, nout)));
     HIP_OK(hipMemcpyAsync(c->r_ooff.p, ooff.data(), (ng + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(c->r_coff.p, coff.data(), (ng + 1) * 8, hipMemcpyHostToDevice, c->stream));
     if (ns) {
       HIP_OK(hipMemcpyAsync(c->r_sg.p, sg.data(), ns * 4, hipMemcpyHostToDevice, c->stream));
-      HIP_OK(hipMemcpyAsync(c->r_su.p, su.data(), ns * 4, hipMemcpyHostToDevice, c->stream));
+      HIP_OK(hipMemcpyAsync(c->r_su.p, st.data(), ns * 4, hipMemcpyHostToDevice, c->stream));
     }
     rp.out_off = c->r_ooff.as<int64_t>();
+    rp.cur_off = c->r_coff.as<int64_t>();
+    rp.cur = c->r_cur.as<int32_t>();
     rp.strip_g = c->r_sg.as<int32_t>();
-    rp.strip_u = c->r_su.as<int32_t>();
+    rp.strip_t = c->r_su.as<int32_t>();
     rp.n_strips = ns;
     rp.out_ts = c->r_ots.as<int64_t>();
     rp.out_bits = c->r_obits.as<uint64_t>();
     rp.out_int = c->r_oint.as<uint8_t>();
-    rp.kmax = (int32_t)kmax;
-    if (kmax > RAW_LDS_SPANS) {
-      HIP_OK(c->r_gcur.ensure(std::max<int64_t>(1, ns * kmax) * 4));
-      HIP_OK(c->r_gmask.ensure(std::max<int64_t>(1, ns * kmax) * 8));
-      rp.g_cur = c->r_gcur.as<int32_t>();
-      rp.g_mask = c->r_gmask.as<uint64_t>();
-    }
     HIP_OK(launch_raw_rank(rp, grp_ser[g0], grp_ser[g1], c->stream));
+    HIP_OK(launch_raw_cursor(rp, grp_ser[g0], grp_ser[g1], c->stream));
     HIP_OK(hipEventRecord(c->ev[3], c->stream));
     HIP_OK(launch_raw_eval(rp, c->stream));
     HIP_OK(hipEventRecord(c->ev[1], c->stream));

@@ -140,8 +140,8 @@ struct RawPt {
 };
 static constexpr int64_t RAW_FLOAT = (int64_t)0x8000000000000000ULL;
 static constexpr int64_t RAW_TIME_MASK = 0x7FFFFFFFFFFFFFFFLL;
-static constexpr int RAW_STRIP = 1024;     // union points per k_raw_eval wave
-static constexpr int RAW_LDS_SPANS = 4096; // spans whose cursors fit in LDS
+static constexpr int RAW_W = 8;                // 64-point windows per k_raw_eval wave
+static constexpr int RAW_STRIP = 64 * RAW_W;   // union points per k_raw_eval wave
 
 struct RawParams {
   // decode
@@ -169,15 +169,14 @@ struct RawParams {
   // evaluation
   const int64_t* out_off;      // [g1 - g0] chunk-relative output offset of each group
   const int32_t* strip_g;      // [n_strips] chunk-relative group
-  const int32_t* strip_u;      // [n_strips] first union point
+  const int32_t* strip_t;      // [n_strips] strip index inside the group (first union point t * RAW_STRIP)
   int64_t n_strips;
+  const int64_t* cur_off;      // [g1 - g0] offset of the group's cursor table
+  int32_t* cur;                // per group [strip][span]: counted points with rank < strip start
   int32_t ga, interp, do_long, do_double;
   int64_t* out_ts;
   uint64_t* out_bits;
   uint8_t* out_int;
-  int32_t* g_cur;              // [n_strips][kmax] cursors when kmax > RAW_LDS_SPANS
-  uint64_t* g_mask;
-  int32_t kmax;
   int32_t* err;
 };
 
@@ -220,7 +219,9 @@ hipError_t launch_raw_decode(const RawParams& p, hipStream_t s);
 hipError_t launch_raw_rate(const RawParams& p, hipStream_t s);
 hipError_t launch_raw_union(const RawParams& p, int64_t s_begin, int64_t s_end, hipStream_t s);  // mark + scan
 hipError_t launch_raw_rank(const RawParams& p, int64_t s_begin, int64_t s_end, hipStream_t s);   // rank + union ts
+hipError_t launch_raw_cursor(const RawParams& p, int64_t s_begin, int64_t s_end, hipStream_t s);
 hipError_t launch_raw_eval(const RawParams& p, hipStream_t s);
+template <int GA> hipError_t launch_raw_eval_inst(const RawParams& p, hipStream_t s);   // k_raw_eval.hip
 hipError_t launch_synth_write(const SynthParams& p, hipStream_t s);
 
 }  // namespace tsdb

@@ -15,13 +15,8 @@
 //   k_raw_scan    one block per group: exclusive popcount prefix over the bitmap -> U
 //   k_raw_rank    one wave per series: rank[p] = union points strictly before p
 //   k_raw_ts      one thread per bitmap word: the union timestamps, in order
-//   k_raw_eval    one wave per strip of RAW_STRIP union points: lanes own union points;
-//                 spans are visited sequentially in SpanGroup order, so every aggregator
-//                 (float sums included) sees its values in the reference's order.  Per
-//                 64-point window a lane-parallel pre-pass advances every span's cursor
-//                 (points with rank < window start) and records which window positions
-//                 are the span's own points (a 64-bit mask); a lane then finds its
-//                 segment with one popcount.
+//   k_raw_cursor  one wave per series: the span's cursor at every strip start
+//   k_raw_eval    (k_raw_eval.hip) one wave per strip of RAW_STRIP union points.
 #include "kcommon.h"
 
 namespace tsdb {
@@ -105,10 +100,6 @@ __global__ __launch_bounds__(256) void k_raw_decode(RawParams p) {
 }
 
 // ---- RateSpan over raw points ----------------------------------------------------------
-__device__ __forceinline__ double pt_double(int64_t tsf, uint64_t bits) {
-  return (tsf & RAW_FLOAT) ? __longlong_as_double((long long)bits) : (double)(long long)bits;
-}
-
 // RateSpan.populateNextRate (src/core/RateSpan.java:121-180): the rate at every point
 // against its predecessor (the first against (t=0, long 0), :112); with drop_resets a
 // negative counter delta drops the point but it stays the predecessor of the next one.
@@ -256,292 +247,31 @@ __global__ __launch_bounds__(256) void k_raw_ts(RawParams p) {
   }
 }
 
-// ---- evaluation ---------------------------------------------------------------------
-// Java long arithmetic (wrapping) and the LERP of nextLongValue (:682-729):
-//   y0 + (x - x0) * (y1 - y0) / (x1 - x0)   with truncating division
-__device__ __forceinline__ int64_t jdiv_pos(int64_t num, int64_t den) {
-  // den > 0.  |num| < 2^53: double quotient, corrected to the exact truncated one.
-  const uint64_t an = num < 0 ? (uint64_t)0 - (uint64_t)num : (uint64_t)num;
-  if (an < (1ULL << 53) && den < (1LL << 53)) {
-    int64_t q = (int64_t)((double)num / (double)den);
-    int64_t r = num - q * den;
-    if (num >= 0) {
-      if (r < 0) { q--; r += den; }
-      if (r >= den) { q++; }
-    } else {
-      if (r > 0) { q++; r -= den; }
-      if (r <= -den) { q--; }
-    }
-    return q;
-  }
-  return num / den;
-}
-
-__device__ __forceinline__ int64_t jlerp(int interp, int64_t x, int64_t x0, int64_t y0, int64_t x1, int64_t y1) {
-  switch (interp) {
-    case TSDB_INTERP_LERP: {
-      const uint64_t prod = (uint64_t)(x - x0) * ((uint64_t)y1 - (uint64_t)y0);
-      return (int64_t)((uint64_t)y0 + (uint64_t)jdiv_pos((int64_t)prod, x1 - x0));
-    }
-    case TSDB_INTERP_ZIM: return 0;
-    case TSDB_INTERP_MAX: return 0x7FFFFFFFFFFFFFFFLL;
-    case TSDB_INTERP_MIN: return (int64_t)0x8000000000000000ULL;
-    default: return y0;
-  }
-}
-
-// nextDoubleValue (:735-797)
-__device__ __forceinline__ double dlerp(int interp, int64_t x, int64_t x0, double y0, int64_t x1, double y1) {
-  switch (interp) {
-    case TSDB_INTERP_LERP: return y0 + (double)(x - x0) * (y1 - y0) / (double)(x1 - x0);
-    case TSDB_INTERP_ZIM: return 0.0;
-    case TSDB_INTERP_MAX: return DBL_MAX;
-    case TSDB_INTERP_MIN: return 4.9e-324;   // Double.MIN_VALUE
-    default: return y0;
-  }
-}
-
-// Aggregator.runLong / runDouble as a stream over the spans' values in index order
-// (src/core/Aggregators.java; the oracle's agg_run_long / agg_run_double).
-struct RAcc {
-  double da, db;      // runDouble state
-  int64_t la;         // runLong state
-  double lm, lM2;     // runLong dev (Welford in double)
-  int32_t dn, ln;     // counts
-  int32_t dst, lst;   // stage flags
-  uint64_t lfirst;    // runLong diff: first value
-  bool bad;           // NONE with more than one value
-};
-
-__device__ __forceinline__ void racc_init(RAcc& a, int ga) {
-  a.da = (ga == GA_MIN) ? INFINITY : (ga == GA_MAX ? -INFINITY : 0.0);
-  a.db = 0.0;
-  a.la = 0;
-  a.lm = 0.0;
-  a.lM2 = 0.0;
-  a.dn = 0;
-  a.ln = 0;
-  a.dst = 0;
-  a.lst = 0;
-  a.lfirst = 0;
-  a.bad = false;
-}
-
-__device__ __forceinline__ void racc_double(RAcc& a, int ga, double x) {
-  switch (ga) {
-    case GA_SUM: case GA_AVG: if (!isnan(x)) { a.da += x; a.dn++; } break;
-    case GA_SQUARESUM: if (!isnan(x)) { a.da += x * x; a.dn++; } break;
-    case GA_COUNT: if (!isnan(x)) a.dn++; break;
-    case GA_MIN: if (!isnan(x) && x < a.da) a.da = x; break;
-    case GA_MAX: if (!isnan(x) && x > a.da) a.da = x; break;
-    case GA_DEV:
-      if (a.dst == 0) {
-        if (!isnan(x)) { a.da = x; a.dst = 1; a.dn = 2; }
-      } else if (!isnan(x)) {
-        const double nm = a.da + (x - a.da) / (double)a.dn;
-        a.db += (x - a.da) * (x - nm);
-        a.da = nm;
-        a.dn++;
-      }
-      break;
-    case GA_DIFF:
-      if (a.dst == 0) { if (!isnan(x)) { a.da = x; a.dst = 1; } }
-      else { a.db = x; a.dst = 2; }
-      break;
-    case GA_FIRST: if (a.dst == 0) { a.da = x; a.dst = 1; } break;
-    case GA_LAST: a.da = x; break;
-    case GA_MULT: a.da = a.dst ? a.da * x : x; a.dst = 1; break;
-    case GA_NONE: if (a.dst) a.bad = true; a.da = x; a.dst = 1; break;
-  }
-}
-
-__device__ __forceinline__ double racc_double_final(const RAcc& a, int ga) {
-  switch (ga) {
-    case GA_SUM: case GA_SQUARESUM: return a.dn == 0 ? (double)NAN : a.da;
-    case GA_AVG: return a.dn == 0 ? (double)NAN : a.da / (double)a.dn;
-    case GA_COUNT: return (double)a.dn;
-    case GA_MIN: return a.da == INFINITY ? (double)NAN : a.da;
-    case GA_MAX: return a.da == -INFINITY ? (double)NAN : a.da;
-    case GA_DEV: return a.dst == 0 ? (double)NAN : (a.dn == 2 ? 0.0 : sqrt(a.db / (double)(a.dn - 1)));
-    case GA_DIFF: return a.dst == 0 ? (double)NAN : (a.dst == 1 ? 0.0 : a.db - a.da);
-    default: return a.da;
-  }
-}
-
-__device__ __forceinline__ void racc_long(RAcc& a, int ga, int64_t x) {
-  const uint64_t ux = (uint64_t)x;
-  switch (ga) {
-    case GA_SUM: a.la = (int64_t)((uint64_t)a.la + ux); break;
-    case GA_AVG: a.la = (int64_t)((uint64_t)a.la + ux); a.ln++; break;
-    case GA_SQUARESUM: a.la = (int64_t)((uint64_t)a.la + ux * ux); break;
-    case GA_COUNT: a.ln++; break;
-    case GA_MIN: if (a.lst == 0 || x < a.la) a.la = x; a.lst = 1; break;
-    case GA_MAX: if (a.lst == 0 || x > a.la) a.la = x; a.lst = 1; break;
-    case GA_DEV:
-      if (a.lst == 0) { a.lm = (double)x; a.lst = 1; a.ln = 2; }
-      else {
-        const double xd = (double)x;
-        const double nm = a.lm + (xd - a.lm) / (double)a.ln;
-        a.lM2 += (xd - a.lm) * (xd - nm);
-        a.lm = nm;
-        a.ln++;
-        a.lst = 2;
-      }
-      break;
-    case GA_DIFF:
-      if (a.lst == 0) { a.lfirst = ux; a.lst = 1; }
-      else { a.la = x; a.lst = 2; }
-      break;
-    case GA_FIRST: if (a.lst == 0) { a.la = x; a.lst = 1; } break;
-    case GA_LAST: a.la = x; break;
-    case GA_MULT: a.la = a.lst ? (int64_t)((uint64_t)a.la * ux) : x; a.lst = 1; break;
-    case GA_NONE: if (a.lst) a.bad = true; a.la = x; a.lst = 1; break;
-  }
-}
-
-__device__ __forceinline__ int64_t jd2l(double d) {
-  if (isnan(d)) return 0;
-  if (d >= 9223372036854775807.0) return 0x7FFFFFFFFFFFFFFFLL;
-  if (d <= -9223372036854775808.0) return (int64_t)0x8000000000000000ULL;
-  return (int64_t)d;
-}
-
-__device__ __forceinline__ int64_t racc_long_final(const RAcc& a, int ga) {
-  switch (ga) {
-    case GA_AVG: return a.ln == 0 ? 0 : (a.la == (int64_t)0x8000000000000000ULL && a.ln == -1 ? a.la : a.la / a.ln);
-    case GA_COUNT: return a.ln;
-    case GA_DEV: return a.lst < 2 ? 0 : jd2l(sqrt(a.lM2 / (double)(a.ln - 1)));
-    case GA_DIFF: return a.lst < 2 ? 0 : (int64_t)((uint64_t)a.la - a.lfirst);
-    default: return a.la;
-  }
-}
-
-template <bool DL, bool DD>
-__device__ __forceinline__ void raw_eval_strip(const RawParams& p, int64_t strip, int32_t* cur, uint64_t* mask) {
+// ---- strip cursors -----------------------------------------------------------------
+// cur[t][i] = counted points of span i with rank < t * RAW_STRIP.  Counted point q (rank
+// r_q, strictly increasing) is the cursor of the strips t with r_{q-1} < t * S <= r_q.
+__global__ __launch_bounds__(256) void k_raw_cursor(RawParams p, int64_t s_begin, int64_t s_end) {
   const int lane = lane_id();
-  const int64_t gi = p.strip_g[strip];
-  const int64_t g = gi + p.g0;
-  const int64_t U = p.U[gi];
-  const int64_t ua = p.strip_u[strip];
-  const int64_t ub = min(U, ua + (int64_t)RAW_STRIP);
-  const int64_t sb = p.grp_ser[g];
-  const int k = (int)(p.grp_ser[g + 1] - sb);
-  const int first = p.rate ? 1 : 0;
-  const int ga = p.ga;
-  // cursors at the strip start: counted points with rank < ua (binary search)
-  for (int i = lane; i < k; i += 64) {
-    const int64_t s = sb + i;
-    const int n = p.sp_n[s];
-    const int32_t* rk = p.rank + p.sp_off[s];
-    int lo = first, hi = max(first, n);
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (rk[mid] < ua) lo = mid + 1; else hi = mid;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t s = s_begin + wave; s < s_end; s += nwaves) {
+    const int64_t g = group_of_series(p, s);
+    const int64_t gi = g - p.g0;
+    const int64_t U = p.U[gi];
+    const int64_t ns = (U + RAW_STRIP - 1) / RAW_STRIP;
+    const int64_t n = p.sp_n[s];
+    const int first = p.rate ? 1 : 0;
+    const int64_t nc = max((int64_t)0, n - first);
+    const int64_t k = p.grp_ser[g + 1] - p.grp_ser[g];
+    const int64_t i = s - p.grp_ser[g];
+    int32_t* cur = p.cur + p.cur_off[gi] + i;
+    const int32_t* rk = p.rank + p.sp_off[s] + first;
+    for (int64_t q = lane; q <= nc; q += 64) {
+      const int64_t t_lo = q == 0 ? 0 : (int64_t)rk[q - 1] / RAW_STRIP + 1;
+      const int64_t t_hi = q == nc ? ns - 1 : (int64_t)rk[q] / RAW_STRIP;
+      for (int64_t t = t_lo; t <= t_hi; t++) cur[t * k] = (int32_t)q;
     }
-    cur[i] = lo - first;
   }
-  WAVE_SYNC();
-  const int64_t obase = p.out_off[gi];
-  for (int64_t u0 = ua; u0 < ub; u0 += 64) {
-    // pre-pass: each span's own points in [u0, u0 + 64)
-    for (int i = lane; i < k; i += 64) {
-      const int64_t s = sb + i;
-      const int n = p.sp_n[s];
-      const int32_t* rk = p.rank + p.sp_off[s];
-      int c = cur[i] + first;
-      uint64_t M = 0;
-      while (c < n) {
-        const int32_t r = rk[c];
-        if (r >= u0 + 64) break;
-        M |= 1ULL << (r - u0);
-        c++;
-      }
-      mask[i] = M;
-    }
-    WAVE_SYNC();
-    const int64_t u = u0 + lane;
-    const int64_t x = (u < ub) ? (p.out_ts[obase + u] & RAW_TIME_MASK) : 0;
-    const uint64_t below = (lane == 63) ? ~0ULL : ((2ULL << lane) - 1ULL);
-    RAcc acc;
-    racc_init(acc, ga);
-    bool flt = false;
-    for (int i = 0; i < k; i++) {
-      const int64_t s = sb + i;
-      const int n = p.sp_n[s];
-      if (p.rate && n < 2) continue;
-      const RawPt* pts = p.pts + p.sp_off[s];
-      const uint64_t M = mask[i];
-      const int cnt = cur[i] + __popcll(M & below);
-      const bool own = (M >> lane) & 1ULL;
-      if (p.rate) {
-        // step semantics (:744-753): the latest rate at or before x, the first kept rate
-        // before the span's second one; ended after its last rate (the zeroing, :521-526)
-        if (cnt == n - 1 && !own) continue;
-        const RawPt r = pts[cnt];
-        racc_double(acc, ga, __longlong_as_double((long long)r.bits));
-        continue;
-      }
-      if (cnt == 0) {   // not started: its next slot still counts for isInteger (:612-625)
-        flt |= (pts[0].tsf & RAW_FLOAT) != 0;
-        continue;
-      }
-      const int j = cnt - 1;
-      const RawPt a = pts[j];
-      if (j == n - 1) {
-        if (!own) continue;   // ended
-        flt |= (a.tsf & RAW_FLOAT) != 0;
-        if (DL) racc_long(acc, ga, (int64_t)a.bits);
-        if (DD) racc_double(acc, ga, pt_double(a.tsf, a.bits));
-        continue;
-      }
-      const RawPt b = pts[j + 1];
-      flt |= ((a.tsf | b.tsf) & RAW_FLOAT) != 0;
-      if (own) {
-        if (DL) racc_long(acc, ga, (int64_t)a.bits);
-        if (DD) racc_double(acc, ga, pt_double(a.tsf, a.bits));
-      } else {
-        const int64_t x0 = a.tsf & RAW_TIME_MASK, x1 = b.tsf & RAW_TIME_MASK;
-        if (DL) racc_long(acc, ga, jlerp(p.interp, x, x0, (int64_t)a.bits, x1, (int64_t)b.bits));
-        if (DD) racc_double(acc, ga, dlerp(p.interp, x, x0, pt_double(a.tsf, a.bits), x1, pt_double(b.tsf, b.bits)));
-      }
-    }
-    if (u < ub) {
-      const bool is_int = !p.rate && !flt;
-      uint64_t bits;
-      if (is_int) {
-        bits = DL ? (uint64_t)racc_long_final(acc, ga) : 0;
-        if (!DL) set_err(p.err, TSDB_E_HIP);   // planning error: integer output without the long path
-      } else {
-        const double r = DD ? racc_double_final(acc, ga) : 0.0;
-        if (!DD) set_err(p.err, TSDB_E_HIP);
-        if (isinf(r)) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // doubleValue (:640-643)
-        bits = (uint64_t)__double_as_longlong(r);
-      }
-      if (acc.bad) set_err(p.err, TSDB_E_ILLEGAL_DATA);   // None: "More than one value" (:454-460)
-      p.out_bits[obase + u] = bits;
-      p.out_int[obase + u] = is_int ? 1 : 0;
-    }
-    WAVE_SYNC();
-    for (int i = lane; i < k; i += 64) cur[i] += __popcll(mask[i]);
-    WAVE_SYNC();
-  }
-}
-
-template <bool DL, bool DD>
-__global__ __launch_bounds__(64) void k_raw_eval(RawParams p) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int64_t strip = blockIdx.x;
-  if (strip >= p.n_strips) return;
-  int32_t* cur;
-  uint64_t* mask;
-  if (p.kmax <= RAW_LDS_SPANS) {
-    mask = reinterpret_cast<uint64_t*>(smem);
-    cur = reinterpret_cast<int32_t*>(smem + (size_t)p.kmax * 8);
-  } else {
-    mask = p.g_mask + strip * p.kmax;
-    cur = p.g_cur + strip * p.kmax;
-  }
-  raw_eval_strip<DL, DD>(p, strip, cur, mask);
 }
 
 // ---- launchers --------------------------------------------------------------------
@@ -582,14 +312,29 @@ hipError_t launch_raw_rank(const RawParams& p, int64_t s_begin, int64_t s_end, h
   return hipGetLastError();
 }
 
+hipError_t launch_raw_cursor(const RawParams& p, int64_t s_begin, int64_t s_end, hipStream_t s) {
+  if (s_end <= s_begin) return hipSuccess;
+  hipLaunchKernelGGL(k_raw_cursor, dim3(wave_blocks(s_end - s_begin)), dim3(256), 0, s, p, s_begin, s_end);
+  return hipGetLastError();
+}
+
 hipError_t launch_raw_eval(const RawParams& p, hipStream_t s) {
   if (p.n_strips == 0) return hipSuccess;
-  const size_t lds = p.kmax <= RAW_LDS_SPANS ? (size_t)p.kmax * 12 + 16 : 16;
-  const dim3 grid((unsigned)p.n_strips), block(64);
-  if (p.do_long && p.do_double) hipLaunchKernelGGL((k_raw_eval<true, true>), grid, block, lds, s, p);
-  else if (p.do_long) hipLaunchKernelGGL((k_raw_eval<true, false>), grid, block, lds, s, p);
-  else hipLaunchKernelGGL((k_raw_eval<false, true>), grid, block, lds, s, p);
-  return hipGetLastError();
+  switch (p.ga) {
+    case GA_SUM: return launch_raw_eval_inst<GA_SUM>(p, s);
+    case GA_AVG: return launch_raw_eval_inst<GA_AVG>(p, s);
+    case GA_COUNT: return launch_raw_eval_inst<GA_COUNT>(p, s);
+    case GA_SQUARESUM: return launch_raw_eval_inst<GA_SQUARESUM>(p, s);
+    case GA_MIN: return launch_raw_eval_inst<GA_MIN>(p, s);
+    case GA_MAX: return launch_raw_eval_inst<GA_MAX>(p, s);
+    case GA_DEV: return launch_raw_eval_inst<GA_DEV>(p, s);
+    case GA_FIRST: return launch_raw_eval_inst<GA_FIRST>(p, s);
+    case GA_LAST: return launch_raw_eval_inst<GA_LAST>(p, s);
+    case GA_DIFF: return launch_raw_eval_inst<GA_DIFF>(p, s);
+    case GA_MULT: return launch_raw_eval_inst<GA_MULT>(p, s);
+    case GA_NONE: return launch_raw_eval_inst<GA_NONE>(p, s);
+  }
+  return hipErrorInvalidValue;
 }
 
 }  // namespace tsdb

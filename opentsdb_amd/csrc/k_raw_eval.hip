@@ -1,0 +1,325 @@
+// k_raw_eval.hip -- evaluation kernel of the raw path, instantiated for ONE group
+// aggregator class (GA_ID, set by the Makefile) so each aggregator keeps only its own
+// state in registers.
+//
+// One wave per strip of RAW_STRIP = 64 x RAW_W union points of one group.  Lane l owns
+// the union points ua + 64 w + l (w < RAW_W) and keeps one aggregator state per point.
+// Spans are visited sequentially in SpanGroup index order (the order in which
+// AggregationIterator.nextDoubleValue / nextLongValue hand values to the aggregator,
+// src/core/AggregationIterator.java:667-797), so every aggregator -- float sums included --
+// sees the reference's operand order.  Per (strip, span):
+//   c = cursor[strip][span]  counted points of the span with rank < ua
+//   m = cursor[strip+1][span] - c  the span's points inside the strip
+// m == 0 (the common case for groups of many spans): one segment for the whole strip;
+// its two end points are wave-uniform loads and every window is a plain LERP.
+// m > 0: the span's in-strip ranks are OR-ed into RAW_W 64-bit window masks in LDS; a
+// lane's segment is cursor + popcount(mask bits at or below its position).
+#include "kcommon.h"
+
+#ifndef GA_ID
+#error "compile with -DGA_ID=<group aggregator class>"
+#endif
+
+namespace tsdb {
+
+// Java long arithmetic (wrapping) and the LERP of nextLongValue (:682-729):
+//   y0 + (x - x0) * (y1 - y0) / (x1 - x0)   with truncating division
+__device__ __forceinline__ int64_t jdiv_pos(int64_t num, int64_t den) {
+  // den > 0.  |num| < 2^53: double quotient, corrected to the exact truncated one.
+  const uint64_t an = num < 0 ? (uint64_t)0 - (uint64_t)num : (uint64_t)num;
+  if (an < (1ULL << 53) && den < (1LL << 53)) {
+    int64_t q = (int64_t)((double)num / (double)den);
+    const int64_t r = num - q * den;
+    if (num >= 0) {
+      if (r < 0) q--;
+      else if (r >= den) q++;
+    } else {
+      if (r > 0) q++;
+      else if (r <= -den) q--;
+    }
+    return q;
+  }
+  return num / den;
+}
+
+__device__ __forceinline__ int64_t jlerp(int interp, int64_t x, int64_t x0, int64_t y0, int64_t x1, int64_t y1) {
+  switch (interp) {
+    case TSDB_INTERP_LERP: {
+      const uint64_t prod = (uint64_t)(x - x0) * ((uint64_t)y1 - (uint64_t)y0);
+      return (int64_t)((uint64_t)y0 + (uint64_t)jdiv_pos((int64_t)prod, x1 - x0));
+    }
+    case TSDB_INTERP_ZIM: return 0;
+    case TSDB_INTERP_MAX: return 0x7FFFFFFFFFFFFFFFLL;
+    case TSDB_INTERP_MIN: return (int64_t)0x8000000000000000ULL;
+    default: return y0;
+  }
+}
+
+// nextDoubleValue (:735-797), evaluated with exactly Java's association and no FMA
+__device__ __forceinline__ double dlerp(int interp, int64_t x, int64_t x0, double y0, int64_t x1, double y1) {
+  switch (interp) {
+    case TSDB_INTERP_LERP: return y0 + (double)(x - x0) * (y1 - y0) / (double)(x1 - x0);
+    case TSDB_INTERP_ZIM: return 0.0;
+    case TSDB_INTERP_MAX: return DBL_MAX;
+    case TSDB_INTERP_MIN: return 4.9e-324;   // Double.MIN_VALUE
+    default: return y0;
+  }
+}
+
+__device__ __forceinline__ int64_t jd2l(double d) {   // Java (long) of a double
+  if (isnan(d)) return 0;
+  if (d >= 9223372036854775807.0) return 0x7FFFFFFFFFFFFFFFLL;
+  if (d <= -9223372036854775808.0) return (int64_t)0x8000000000000000ULL;
+  return (int64_t)d;
+}
+
+// Aggregator.runLong / runDouble as a stream over the spans' values in index order
+// (src/core/Aggregators.java: Sum :237-259, SquareSum :269-293, Min :303-327,
+// Max :337-361, Avg :371-393, None :445-460, Multiply :470-485, StdDev :504-569,
+// Diff :582-617, Count :626-645, First :815-829, Last :837-851).
+struct RAcc {
+  double da, db;      // runDouble
+  int64_t la;         // runLong
+  double lm, lM2;     // runLong dev (Welford in double)
+  uint64_t lfirst;    // runLong diff
+  int32_t dn, ln;
+  int32_t dst, lst;
+  bool bad;           // None: more than one value
+};
+
+template <int GA>
+__device__ __forceinline__ void racc_init(RAcc& a) {
+  a.da = (GA == GA_MIN) ? INFINITY : (GA == GA_MAX ? -INFINITY : 0.0);
+  a.db = 0.0;
+  a.la = 0;
+  a.lm = 0.0;
+  a.lM2 = 0.0;
+  a.lfirst = 0;
+  a.dn = 0;
+  a.ln = 0;
+  a.dst = 0;
+  a.lst = 0;
+  a.bad = false;
+}
+
+template <int GA>
+__device__ __forceinline__ void racc_double(RAcc& a, double x) {
+  if constexpr (GA == GA_SUM || GA == GA_AVG) { if (!isnan(x)) { a.da += x; a.dn++; } }
+  else if constexpr (GA == GA_SQUARESUM) { if (!isnan(x)) { a.da += x * x; a.dn++; } }
+  else if constexpr (GA == GA_COUNT) { if (!isnan(x)) a.dn++; }
+  else if constexpr (GA == GA_MIN) { if (!isnan(x) && x < a.da) a.da = x; }
+  else if constexpr (GA == GA_MAX) { if (!isnan(x) && x > a.da) a.da = x; }
+  else if constexpr (GA == GA_DEV) {
+    if (a.dst == 0) {
+      if (!isnan(x)) { a.da = x; a.dst = 1; a.dn = 2; }
+    } else if (!isnan(x)) {
+      const double nm = a.da + (x - a.da) / (double)a.dn;
+      a.db += (x - a.da) * (x - nm);
+      a.da = nm;
+      a.dn++;
+    }
+  } else if constexpr (GA == GA_DIFF) {
+    if (a.dst == 0) { if (!isnan(x)) { a.da = x; a.dst = 1; } }
+    else { a.db = x; a.dst = 2; }
+  } else if constexpr (GA == GA_FIRST) { if (a.dst == 0) { a.da = x; a.dst = 1; } }
+  else if constexpr (GA == GA_LAST) { a.da = x; }
+  else if constexpr (GA == GA_MULT) { a.da = a.dst ? a.da * x : x; a.dst = 1; }
+  else if constexpr (GA == GA_NONE) { if (a.dst) a.bad = true; a.da = x; a.dst = 1; }
+}
+
+template <int GA>
+__device__ __forceinline__ double racc_double_final(const RAcc& a) {
+  if constexpr (GA == GA_SUM || GA == GA_SQUARESUM) return a.dn == 0 ? (double)NAN : a.da;
+  else if constexpr (GA == GA_AVG) return a.dn == 0 ? (double)NAN : a.da / (double)a.dn;
+  else if constexpr (GA == GA_COUNT) return (double)a.dn;
+  else if constexpr (GA == GA_MIN) return a.da == INFINITY ? (double)NAN : a.da;
+  else if constexpr (GA == GA_MAX) return a.da == -INFINITY ? (double)NAN : a.da;
+  else if constexpr (GA == GA_DEV) return a.dst == 0 ? (double)NAN : (a.dn == 2 ? 0.0 : sqrt(a.db / (double)(a.dn - 1)));
+  else if constexpr (GA == GA_DIFF) return a.dst == 0 ? (double)NAN : (a.dst == 1 ? 0.0 : a.db - a.da);
+  else return a.da;
+}
+
+template <int GA>
+__device__ __forceinline__ void racc_long(RAcc& a, int64_t x) {
+  const uint64_t ux = (uint64_t)x;
+  if constexpr (GA == GA_SUM) a.la = (int64_t)((uint64_t)a.la + ux);
+  else if constexpr (GA == GA_AVG) { a.la = (int64_t)((uint64_t)a.la + ux); a.ln++; }
+  else if constexpr (GA == GA_SQUARESUM) a.la = (int64_t)((uint64_t)a.la + ux * ux);
+  else if constexpr (GA == GA_COUNT) a.ln++;
+  else if constexpr (GA == GA_MIN) { if (a.lst == 0 || x < a.la) a.la = x; a.lst = 1; }
+  else if constexpr (GA == GA_MAX) { if (a.lst == 0 || x > a.la) a.la = x; a.lst = 1; }
+  else if constexpr (GA == GA_DEV) {
+    if (a.lst == 0) { a.lm = (double)x; a.lst = 1; a.ln = 2; }
+    else {
+      const double xd = (double)x;
+      const double nm = a.lm + (xd - a.lm) / (double)a.ln;
+      a.lM2 += (xd - a.lm) * (xd - nm);
+      a.lm = nm;
+      a.ln++;
+      a.lst = 2;
+    }
+  } else if constexpr (GA == GA_DIFF) {
+    if (a.lst == 0) { a.lfirst = ux; a.lst = 1; }
+    else { a.la = x; a.lst = 2; }
+  } else if constexpr (GA == GA_FIRST) { if (a.lst == 0) { a.la = x; a.lst = 1; } }
+  else if constexpr (GA == GA_LAST) a.la = x;
+  else if constexpr (GA == GA_MULT) { a.la = a.lst ? (int64_t)((uint64_t)a.la * ux) : x; a.lst = 1; }
+  else if constexpr (GA == GA_NONE) { if (a.lst) a.bad = true; a.la = x; a.lst = 1; }
+}
+
+template <int GA>
+__device__ __forceinline__ int64_t racc_long_final(const RAcc& a) {
+  if constexpr (GA == GA_AVG) return a.ln == 0 ? 0 : a.la / (int64_t)a.ln;
+  else if constexpr (GA == GA_COUNT) return a.ln;
+  else if constexpr (GA == GA_DEV) return a.lst < 2 ? 0 : jd2l(sqrt(a.lM2 / (double)(a.ln - 1)));
+  else if constexpr (GA == GA_DIFF) return a.lst < 2 ? 0 : (int64_t)((uint64_t)a.la - a.lfirst);
+  else return a.la;
+}
+
+// One value (exact or interpolated) of a span at union time x.
+template <int GA, bool DL, bool DD>
+__device__ __forceinline__ void feed(RAcc& acc, int interp, bool own, int64_t x, const RawPt& a, const RawPt& b) {
+  if (own) {
+    if (DL) racc_long<GA>(acc, (int64_t)a.bits);
+    if (DD) racc_double<GA>(acc, pt_double(a.tsf, a.bits));
+  } else {
+    const int64_t x0 = a.tsf & RAW_TIME_MASK, x1 = b.tsf & RAW_TIME_MASK;
+    if (DL) racc_long<GA>(acc, jlerp(interp, x, x0, (int64_t)a.bits, x1, (int64_t)b.bits));
+    if (DD) racc_double<GA>(acc, dlerp(interp, x, x0, pt_double(a.tsf, a.bits), x1, pt_double(b.tsf, b.bits)));
+  }
+}
+
+template <int GA, bool DL, bool DD, bool RATE>
+__global__ __launch_bounds__(64) void k_raw_eval(RawParams p) {
+  __shared__ uint64_t wmask[RAW_W];
+  const int lane = lane_id();
+  const int64_t strip = blockIdx.x;
+  if (strip >= p.n_strips) return;
+  const int64_t gi = p.strip_g[strip];
+  const int64_t t = p.strip_t[strip];
+  const int64_t g = gi + p.g0;
+  const int64_t U = p.U[gi];
+  const int64_t ns = (U + RAW_STRIP - 1) / RAW_STRIP;
+  const int64_t ua = t * RAW_STRIP;
+  const int64_t ub = min(U, ua + (int64_t)RAW_STRIP);
+  const int64_t sb = p.grp_ser[g];
+  const int k = (int)(p.grp_ser[g + 1] - sb);
+  constexpr int first = RATE ? 1 : 0;
+  const int interp = p.interp;
+  const int32_t* crow = p.cur + p.cur_off[gi] + t * k;
+  const int32_t* cnext = (t + 1 < ns) ? crow + k : nullptr;
+  const int64_t obase = p.out_off[gi];
+  const uint64_t below = (lane == 63) ? ~0ULL : ((2ULL << lane) - 1ULL);
+
+  int64_t x[RAW_W];
+  RAcc acc[RAW_W];
+  uint32_t flt = 0;   // bit w: some slot at union point w holds a double (isInteger, :612-625)
+#pragma unroll
+  for (int w = 0; w < RAW_W; w++) {
+    const int64_t u = ua + 64 * w + lane;
+    x[w] = (u < ub) ? p.out_ts[obase + u] : 0;
+    racc_init<GA>(acc[w]);
+  }
+
+  for (int i = 0; i < k; i++) {
+    const int64_t s = sb + i;
+    const int n = p.sp_n[s];
+    if (n < (RATE ? 2 : 1)) continue;   // empty span; rate: endReached with nothing current (:448-459)
+    const int nc = n - first;
+    const RawPt* pts = p.pts + p.sp_off[s];
+    const int c = crow[i];
+    const int m = (cnext ? cnext[i] : nc) - c;
+    if (m == 0) {
+      // one segment for the whole strip (wave-uniform)
+      if (RATE) {
+        if (c == nc) continue;   // ended after its last rate (the zeroing, :521-526)
+        const double y = __longlong_as_double((long long)pts[c].bits);   // step / PREV (:744-753)
+#pragma unroll
+        for (int w = 0; w < RAW_W; w++) racc_double<GA>(acc[w], y);
+      } else {
+        if (c == 0) {            // not started: its next slot still counts for isInteger
+          if (pts[0].tsf & RAW_FLOAT) flt = (1u << RAW_W) - 1;
+          continue;
+        }
+        if (c == n) continue;    // ended
+        const RawPt a = pts[c - 1], b = pts[c];
+        if ((a.tsf | b.tsf) & RAW_FLOAT) flt = (1u << RAW_W) - 1;
+#pragma unroll
+        for (int w = 0; w < RAW_W; w++) feed<GA, DL, DD>(acc[w], interp, false, x[w], a, b);
+      }
+      continue;
+    }
+    // the span has points inside the strip: window masks of their ranks
+    if (lane < RAW_W) wmask[lane] = 0;
+    WAVE_SYNC();
+    const int32_t* rk = p.rank + p.sp_off[s] + first + c;
+    for (int l = lane; l < m; l += 64) {
+      const int64_t o = rk[l] - ua;
+      __hip_atomic_fetch_or(&wmask[o >> 6], 1ULL << (o & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    WAVE_SYNC();
+    int tb = 0;
+#pragma unroll
+    for (int w = 0; w < RAW_W; w++) {
+      const uint64_t M = wmask[w];
+      const int cnt = c + tb + __popcll(M & below);   // counted points with rank <= u
+      const bool own = (M >> lane) & 1ULL;
+      tb += __popcll(M);
+      if (RATE) {
+        if (cnt == nc && !own) continue;
+        racc_double<GA>(acc[w], __longlong_as_double((long long)pts[cnt].bits));
+      } else {
+        if (cnt == 0) {
+          if (pts[0].tsf & RAW_FLOAT) flt |= 1u << w;
+          continue;
+        }
+        const int j = cnt - 1;
+        const RawPt a = pts[j];
+        if (j == n - 1) {
+          if (!own) continue;
+          if (a.tsf & RAW_FLOAT) flt |= 1u << w;
+          if (DL) racc_long<GA>(acc[w], (int64_t)a.bits);
+          if (DD) racc_double<GA>(acc[w], pt_double(a.tsf, a.bits));
+          continue;
+        }
+        const RawPt b = pts[j + 1];
+        if ((a.tsf | b.tsf) & RAW_FLOAT) flt |= 1u << w;
+        feed<GA, DL, DD>(acc[w], interp, own, x[w], a, b);
+      }
+    }
+    WAVE_SYNC();
+  }
+
+#pragma unroll
+  for (int w = 0; w < RAW_W; w++) {
+    const int64_t u = ua + 64 * w + lane;
+    if (u >= ub) continue;
+    const bool is_int = !RATE && !((flt >> w) & 1);
+    uint64_t bits = 0;
+    if (is_int) {
+      if (DL) bits = (uint64_t)racc_long_final<GA>(acc[w]);
+      else set_err(p.err, TSDB_E_HIP);   // planning error: integer output without the long path
+    } else {
+      double r = 0.0;
+      if (DD) r = racc_double_final<GA>(acc[w]);
+      else set_err(p.err, TSDB_E_HIP);
+      if (isinf(r)) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // doubleValue (:640-643)
+      bits = (uint64_t)__double_as_longlong(r);
+    }
+    if (acc[w].bad) set_err(p.err, TSDB_E_ILLEGAL_DATA);   // None: "More than one value" (:454-460)
+    p.out_bits[obase + u] = bits;
+    p.out_int[obase + u] = is_int ? 1 : 0;
+  }
+}
+
+template <>
+hipError_t launch_raw_eval_inst<GA_ID>(const RawParams& p, hipStream_t s) {
+  const dim3 grid((unsigned)p.n_strips), block(64);
+  if (p.rate) hipLaunchKernelGGL((k_raw_eval<GA_ID, false, true, true>), grid, block, 0, s, p);
+  else if (p.do_long && p.do_double) hipLaunchKernelGGL((k_raw_eval<GA_ID, true, true, false>), grid, block, 0, s, p);
+  else if (p.do_long) hipLaunchKernelGGL((k_raw_eval<GA_ID, true, false, false>), grid, block, 0, s, p);
+  else hipLaunchKernelGGL((k_raw_eval<GA_ID, false, true, false>), grid, block, 0, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace tsdb

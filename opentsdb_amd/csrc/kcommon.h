@@ -308,6 +308,11 @@ __device__ __forceinline__ double interp(int method, const GridParams& p, int k0
   }
 }
 
+// value of a raw datapoint as a double (DataPoint.toDouble)
+__device__ __forceinline__ double pt_double(int64_t tsf, uint64_t bits) {
+  return (tsf & RAW_FLOAT) ? __longlong_as_double((long long)bits) : (double)(long long)bits;
+}
+
 // ---- exactness certificate helpers ---------------------------------------------------
 // lsb(x): exponent of the least significant set bit of a finite non-zero double.
 __device__ __forceinline__ int lsb_exp(double x) {

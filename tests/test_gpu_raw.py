@@ -136,3 +136,15 @@ def test_raw_long_overflow_wraps(eng):
     for agg in ["sum", "avg", "squareSum", "mult", "diff", "dev"]:
         q = abi.new_query(T0, T0 + 3599, agg)
         exact(eng.run_batch(b, q), O.run_query(b, q), agg, agg)
+
+
+def test_raw_spans_outside_scan_range(eng):
+    """Series whose rows all lie outside the scan range sit in the group with no points."""
+    rows = [synth.encode_rows([T0 * 1000 + 5000, T0 * 1000 + 65000], [3, 9], None, [0, 0], [False, False]),
+            synth.encode_rows([(T0 + 7200) * 1000 + 1000], [7], None, [0], [False]),
+            synth.encode_rows([T0 * 1000 + 20000, T0 * 1000 + 80000], [1.5, 2.5], [1.5, 2.5], [1, 1], [False, False])]
+    b = synth.from_series(rows, [0, 0, 0])
+    for agg in ["sum", "min", "count"]:
+        for rate in (False, True):
+            q = abi.new_query(T0, T0 + 3599, agg, rate=rate)
+            exact(eng.run_batch(b, q), O.run_query(b, q), agg, f"{agg} rate={rate}")
