@@ -210,9 +210,18 @@ class HostBatch:
         return len(self.row_base_time)
 
 
-def result_to_groups(res: Result):
-    """Copies a tsdbhip_result / ref_result into a list of
-    (group_id, ts[int64], bits[uint64], is_int[uint8]) numpy tuples."""
+def _view(ptr, n: int, dtype, owner):
+    """numpy view of n elements at a ctypes pointer; `owner` is kept alive by the view."""
+    nbytes = n * np.dtype(dtype).itemsize
+    buf = (C.c_uint8 * nbytes).from_address(C.cast(ptr, C.c_void_p).value)
+    buf._owner = owner
+    return np.frombuffer(buf, dtype)
+
+
+def result_to_groups(res: Result, owner=None):
+    """A tsdbhip_result / ref_result as a list of (group_id, ts[int64], bits[uint64],
+    is_int[uint8]) numpy tuples.  Without `owner` the arrays are copies; with it they are
+    views into the result memory, which `owner` frees when the last view is gone."""
     groups = []
     n = res.n_groups
     if n == 0:
@@ -220,7 +229,11 @@ def result_to_groups(res: Result):
     gp = np.ctypeslib.as_array(res.group_ptr, shape=(n + 1,)).copy()
     gid = np.ctypeslib.as_array(res.group_id, shape=(n,)).copy()
     tot = int(gp[-1])
-    if tot:
+    if tot and owner is not None:
+        ts = _view(res.ts_ms, tot, np.int64, owner)
+        bits = _view(res.value_bits, tot, np.uint64, owner)
+        isi = _view(res.is_int, tot, np.uint8, owner)
+    elif tot:
         ts = np.ctypeslib.as_array(res.ts_ms, shape=(tot,)).copy()
         bits = np.ctypeslib.as_array(res.value_bits, shape=(tot,)).copy()
         isi = np.ctypeslib.as_array(res.is_int, shape=(tot,)).copy()

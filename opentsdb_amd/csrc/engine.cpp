@@ -834,8 +834,10 @@ void account(tsdbhip_ctx* c, const Plan& P) {
 tsdbhip_result* make_result(int64_t n_groups, int64_t n_points) {
   const size_t bytes = sizeof(tsdbhip_result) + (n_groups + 1) * 4 + (n_groups + 1) * 8 + (n_points + 1) * 8 * 2 +
                        (n_points + 1) + 64;
-  char* m = (char*)std::calloc(1, bytes);
+  // every array is fully written by the callers: malloc, not calloc (results can be GBs)
+  char* m = (char*)std::malloc(bytes);
   if (!m) return nullptr;
+  std::memset(m, 0, sizeof(tsdbhip_result));
   auto* r = reinterpret_cast<tsdbhip_result*>(m);
   char* p = m + sizeof(tsdbhip_result);
   auto al8 = [&](char* x) { return (char*)(((uintptr_t)x + 7) & ~(uintptr_t)7); };
@@ -1042,6 +1044,12 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
   std::vector<uint8_t> res_int;
   std::vector<int64_t> g_ptr(G + 1, 0);
   double eval_ms = 0.0;
+  const bool direct = !P.none && per_chunk >= G;
+  tsdbhip_result* direct_r = nullptr;
+  struct Guard {
+    tsdbhip_result** r;
+    ~Guard() { if (*r) std::free(*r); }
+  } guard{&direct_r};
   for (int64_t g0 = 0; g0 < G; g0 += per_chunk) {
     const int64_t g1 = std::min(G, g0 + per_chunk);
     const int64_t ng = g1 - g0;
@@ -1097,13 +1105,26 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
     HIP_OK(launch_raw_eval(rp, c->stream));
     HIP_OK(hipEventRecord(c->ev[1], c->stream));
     const size_t base = res_ts.size();
-    res_ts.resize(base + nout);
-    res_bits.resize(base + nout);
-    res_int.resize(base + nout);
-    if (nout) {
-      HIP_OK(hipMemcpyAsync(res_ts.data() + base, rp.out_ts, nout * 8, hipMemcpyDeviceToHost, c->stream));
-      HIP_OK(hipMemcpyAsync(res_bits.data() + base, rp.out_bits, nout * 8, hipMemcpyDeviceToHost, c->stream));
-      HIP_OK(hipMemcpyAsync(res_int.data() + base, rp.out_int, nout, hipMemcpyDeviceToHost, c->stream));
+    if (direct) {
+      // one chunk, groups emitted in batch order: device layout == result layout
+      int64_t nact = 0;
+      for (int64_t g = 0; g < G; g++) nact += act[g];
+      direct_r = make_result(nact, nout);
+      if (!direct_r) return fail(TSDB_E_NOMEM, "result allocation");
+      if (nout) {
+        HIP_OK(hipMemcpyAsync(const_cast<int64_t*>(direct_r->ts_ms), rp.out_ts, nout * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipMemcpyAsync(const_cast<uint64_t*>(direct_r->value_bits), rp.out_bits, nout * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipMemcpyAsync(const_cast<uint8_t*>(direct_r->is_int), rp.out_int, nout, hipMemcpyDeviceToHost, c->stream));
+      }
+    } else {
+      res_ts.resize(base + nout);
+      res_bits.resize(base + nout);
+      res_int.resize(base + nout);
+      if (nout) {
+        HIP_OK(hipMemcpyAsync(res_ts.data() + base, rp.out_ts, nout * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipMemcpyAsync(res_bits.data() + base, rp.out_bits, nout * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipMemcpyAsync(res_int.data() + base, rp.out_int, nout, hipMemcpyDeviceToHost, c->stream));
+      }
     }
     HIP_OK(hipStreamSynchronize(c->stream));
     float te = 0;
@@ -1125,6 +1146,21 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
   c->timing.redo_tiles = 0;
   account(c, P);
   if (err) return fail(err, "error raised by the device path");
+  if (direct) {
+    auto* gptr = const_cast<int64_t*>(direct_r->group_ptr);
+    auto* gid = const_cast<int32_t*>(direct_r->group_id);
+    int64_t i = 0;
+    for (int64_t g = 0; g < G; g++) {
+      if (!act[g]) continue;
+      gid[i] = (int32_t)g;
+      gptr[i] = g_ptr[g];
+      i++;
+    }
+    gptr[i] = g_ptr[G];
+    *out = direct_r;
+    direct_r = nullptr;
+    return 0;
+  }
   // result: emitted groups in emission order
   std::vector<std::pair<int64_t, int64_t>> order;   // (result group id, group row)
   for (int64_t g = 0; g < G; g++) {

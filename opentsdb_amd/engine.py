@@ -94,6 +94,19 @@ def scan_bounds(q: abi.Query):
     return s.value, e.value
 
 
+class _ResultOwner:
+    """Frees a tsdbhip_result when the numpy views into it are gone."""
+
+    def __init__(self, res):
+        self.res = res
+        self.free = lib().tsdbhip_result_free
+
+    def __del__(self):
+        if self.res:
+            self.free(self.res)
+            self.res = None
+
+
 class Engine:
     """One tsdbhip context bound to one GPU."""
 
@@ -138,12 +151,11 @@ class Engine:
         return abi.HostBatch(srp, base[:nr.value], qo, vo, q[:qb.value], v[:vb.value], g[:ns.value])
 
     def run(self, q: abi.Query):
+        """tsdbhip_run -> [(group_id, ts, bits, is_int)]; the arrays are views into the
+        library's result, freed when the last of them is garbage-collected."""
         res = C.POINTER(abi.Result)()
         _check(lib().tsdbhip_run(self.ctx, C.byref(q), C.byref(res)))
-        try:
-            return abi.result_to_groups(res.contents)
-        finally:
-            lib().tsdbhip_result_free(res)
+        return abi.result_to_groups(res.contents, owner=_ResultOwner(res))
 
     def run_batch(self, batch: abi.HostBatch, q: abi.Query):
         """Runner for TsdbQuery: load the query's spans, then run."""
