@@ -873,6 +873,7 @@ int assemble(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, c
   auto* gid = const_cast<int32_t*>(r->group_id);
   auto* ts = const_cast<int64_t*>(r->ts_ms);
   auto* vb = const_cast<uint64_t*>(r->value_bits);
+  auto* isi = const_cast<uint8_t*>(r->is_int);
   int64_t o = 0;
   for (size_t i = 0; i < groups.size(); i++) {
     gptr[i] = o;
@@ -883,6 +884,7 @@ int assemble(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, c
       // only points inside [start_time, end_time] of the SpanGroup are produced (x <= end_time)
       ts[o] = (P.mode == MODE_ALL) ? q->start_time : P.B0 + k * P.I;
       std::memcpy(&vb[o], &val[row * K + k], 8);
+      isi[o] = 0;   // downsampled values are always doubles (Downsampler.isInteger, :259-262)
       o++;
     }
   }
