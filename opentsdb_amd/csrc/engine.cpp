@@ -140,6 +140,7 @@ struct tsdbhip_ctx {
   // scratch
   DevBuf pa, pb, pn, pf, out_val, out_flag, gact, err, g_dense, g_pres, g_rate, redo, redo_n;
   DevBuf xbuf, gbuf;
+  DevBuf pre_dense, pre_pres;          // percentile / median downsampling
   // raw path scratch
   DevBuf r_rowpt, r_spoff, r_spn, r_grp, r_pts, r_rank, r_bm, r_wb, r_U, r_ooff, r_sg, r_su, r_ots, r_obits, r_oint,
       r_coff, r_cur;                   // multi-GPU: this rank's partial states, gathered states
@@ -302,7 +303,7 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   for (DevBuf* b : {&c->pa, &c->pb, &c->pn, &c->pf, &c->out_val, &c->out_flag, &c->gact, &c->err, &c->g_dense,
                     &c->g_pres, &c->g_rate, &c->redo, &c->redo_n, &c->xbuf, &c->gbuf, &c->r_rowpt,
                     &c->r_spoff, &c->r_spn, &c->r_grp, &c->r_pts, &c->r_rank, &c->r_bm, &c->r_wb, &c->r_U, &c->r_ooff,
-                    &c->r_sg, &c->r_su, &c->r_ots, &c->r_obits, &c->r_oint, &c->r_coff, &c->r_cur})
+                    &c->r_sg, &c->r_su, &c->r_ots, &c->r_obits, &c->r_oint, &c->r_coff, &c->r_cur, &c->pre_dense, &c->pre_pres})
     b->release();
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -673,6 +674,7 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
   if (!q->ds_all && q->ds_interval_ms <= 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "interval not > 0");
   P.ga = ga_of(q->aggregator);
   P.f = f_of(q->ds_function);
+  if (P.f < 0 && (q->ds_function == TSDB_AGG_MEDIAN || q->ds_function >= TSDB_AGG_P999)) P.f = F_SEL;
   if (P.ga < 0) return fail(TSDB_E_NOT_IMPLEMENTED, std::string("group-by aggregator not implemented yet: ") + AGG_NAMES[q->aggregator]);
   if (P.f < 0) return fail(TSDB_E_NOT_IMPLEMENTED, std::string("downsampling function not implemented yet: ") + AGG_NAMES[q->ds_function]);
   if ((q->flags & TSDB_QF_ORDERED) && (P.ga == GA_SUM || P.ga == GA_AVG || P.ga == GA_SQUARESUM || P.ga == GA_DEV || P.ga == GA_MULT))
@@ -757,6 +759,32 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   gp.part = Partials{c->pa.as<double>(), c->pb.as<double>(), c->pn.as<uint32_t>(), c->pf.as<uint32_t>()};
   gp.group_active = c->gact.as<uint32_t>();
   gp.err = c->err.as<int32_t>();
+  if (P.f == F_SEL) {
+    // percentile / median: per-series bucket order statistics, then the group-by step
+    HIP_OK(c->pre_dense.ensure(std::max<int64_t>(1, c->n_series * K) * 8));
+    HIP_OK(c->pre_pres.ensure(std::max<int64_t>(1, c->n_series * K)));
+    gp.sel_fn = q->ds_function;
+    gp.n_series = c->n_series;
+    gp.pre_dense = c->pre_dense.as<double>();
+    gp.pre_pres = c->pre_pres.as<uint8_t>();
+    const int64_t elds = align16(K * 8) * 2 + align16(K * 4) * 2 + (q->rate ? align16(K * 8) : 0);
+    if (elds > 48 * 1024) {
+      HIP_OK(c->g_dense.ensure(std::max<int64_t>(1, nt * K) * 8));
+      if (q->rate) HIP_OK(c->g_rate.ensure(std::max<int64_t>(1, nt * K) * 8));
+      gp.g_dense = c->g_dense.as<double>();
+      gp.g_rate = q->rate ? c->g_rate.as<double>() : nullptr;
+      gp.wave_lds = 16;
+    } else {
+      gp.g_dense = nullptr;
+      gp.wave_lds = (int32_t)std::max<int64_t>(16, elds);
+    }
+    gp.waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / gp.wave_lds));
+    c->fast_used = false;
+    HIP_OK(hipEventRecord(c->ev[0], c->stream));
+    HIP_OK(launch_pct(gp, c->stream));
+    HIP_OK(launch_emit(gp, c->stream));
+    HIP_OK(hipEventRecord(c->ev[1], c->stream));
+  } else {
   // streaming kernel first (when the batch's row class and the query allow it), then the
   // general kernel over the tiles it handed back
   bool fast = false;
@@ -787,6 +815,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   }
   HIP_OK(launch_grid(gp, P.f, c->stream));
   HIP_OK(hipEventRecord(c->ev[1], c->stream));
+  }
   if (do_reduce) {
     ReduceParams rp{};
     rp.part = gp.part;

@@ -56,7 +56,8 @@ enum : int {
 // Downsample function classes (per-bucket, per-series, sequential in time order)
 enum : int {
   F_SUM = 0, F_AVG, F_COUNT, F_SQUARESUM, F_MIN, F_MAX, F_DEV, F_FIRST, F_LAST, F_DIFF, F_MULT,
-  F_NUM
+  F_NUM,
+  F_SEL = 100   // percentile / median: order statistics per bucket (k_pct.hip)
 };
 
 struct GridParams {
@@ -104,6 +105,11 @@ struct GridParams {
   double rcpn;           // 1/In rounded up (floor(n * rcpn) == n / In for 0 <= n < 2^50)
   int32_t* redo_list;
   int32_t* redo_n;
+  // k_pct / k_emit: per-series bucket values computed before the group-by step
+  int32_t sel_fn;        // TSDB_AGG_* of the percentile / median downsample function
+  int64_t n_series;
+  double* pre_dense;     // [n_series][K]
+  uint8_t* pre_pres;     // [n_series][K]
 };
 
 struct ReduceParams {
@@ -208,6 +214,10 @@ bool fast_supported(int ds_function_class, int qw, int vl);
 hipError_t launch_fast(const GridParams& p, int ds_function_class, int qw, int vl, hipStream_t s);
 int64_t fast_wave_lds(int64_t K, bool rate);
 hipError_t launch_reduce(const ReduceParams& p, hipStream_t s);
+// percentile / median downsampling (k_pct.hip): bucket order statistics, then group-by
+static constexpr int PCT_CAP = 4096;   // values per bucket sorted in LDS
+hipError_t launch_pct(const GridParams& p, hipStream_t s);
+hipError_t launch_emit(const GridParams& p, hipStream_t s);
 hipError_t launch_rank_merge(const RankMergeParams& p, hipStream_t s);
 // per-downsample-function instantiations (k_grid.hip / k_fast.hip, one object per F)
 template <int F> hipError_t launch_grid_inst(const GridParams& p, hipStream_t s);

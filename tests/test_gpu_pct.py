@@ -1,0 +1,115 @@
+"""GPU parity of percentile / median downsampling (BASELINE config 5's 1h-p99 /
+1h-ep99r7): per-bucket order statistics with commons-math3 LEGACY estimation (the
+reference's runDouble ignores ep*r3 / ep*r7, src/core/Aggregators.java:690), NaNs skipped,
+then the usual group-by.  Downsampled values are bit-exact (checked through the
+order-insensitive max / min / count group aggregators); float sums within REL_TOL."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from opentsdb_amd import abi, synth
+from oracle import oracle as O
+from tests.test_gpu_parity import assert_groups_match
+
+pytestmark = pytest.mark.gpu
+
+T0 = 1356998400
+SEL = ["p999", "p99", "p95", "p90", "p75", "p50", "ep99r3", "ep99r7", "ep50r3", "ep999r7", "median"]
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from opentsdb_amd.engine import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def day_batch():
+    # config 5 shape at small scale: 1 day @10 s, float32 (360 values per 1 h bucket)
+    return synth.generate(24, T0, 8640, 10000, value_kind=0, n_groups=3, seed=0x5EED)
+
+
+@pytest.fixture(scope="module")
+def mixed_batch():
+    return synth.generate(30, T0, 720, 5000, value_kind=2, n_groups=4, int_mod=30000, seed=7)
+
+
+@pytest.mark.parametrize("fn", SEL)
+def test_pct_1h_config5_shape(eng, day_batch, fn):
+    q = abi.new_query(T0, T0 + 86399, "max", ds_function=abi.AGG[fn], ds_interval_ms=3600000)
+    assert_groups_match(eng.run_batch(day_batch, q), O.run_query(day_batch, q), "max", ctx=fn)
+
+
+@pytest.mark.parametrize("fn", ["p99", "p50", "ep90r7", "median"])
+@pytest.mark.parametrize("interval", [15000, 60000, 600000, 3600000])
+def test_pct_bucket_sizes(eng, mixed_batch, fn, interval):
+    # 3 .. 720 values per bucket: register sort (<= 512) and LDS sort (> 512)
+    q = abi.new_query(T0, T0 + 3599, "min", ds_function=abi.AGG[fn], ds_interval_ms=interval)
+    assert_groups_match(eng.run_batch(mixed_batch, q), O.run_query(mixed_batch, q), "min", ctx=f"{fn} {interval}")
+
+
+@pytest.mark.parametrize("agg", ["sum", "avg", "count", "dev", "zimsum", "mimmax", "first", "last"])
+def test_pct_groupby_aggregators(eng, day_batch, agg):
+    q = abi.new_query(T0, T0 + 86399, agg, ds_function=abi.AGG["p99"], ds_interval_ms=3600000)
+    assert_groups_match(eng.run_batch(day_batch, q), O.run_query(day_batch, q), agg, ctx=agg)
+
+
+@pytest.mark.parametrize("fill", [abi.FILL_NAN, abi.FILL_ZERO])
+def test_pct_fill_and_rate(eng, fill):
+    b = synth.generate(20, T0 + 1800, 200, 10000, value_kind=1, n_groups=2, int_mod=1000, seed=3)
+    q = abi.new_query(T0, T0 + 7199, "sum", ds_function=abi.AGG["p90"], ds_interval_ms=300000, ds_fill=fill)
+    assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "sum", ctx=f"fill {fill}")
+    q = abi.new_query(T0, T0 + 7199, "sum", ds_function=abi.AGG["median"], ds_interval_ms=300000, rate=True)
+    assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "sum", ctx="rate")
+
+
+def test_pct_nan_values_and_all(eng):
+    rng = np.random.default_rng(5)
+    rows, gids = [], []
+    for s in range(10):
+        ts = T0 * 1000 + np.sort(rng.choice(np.arange(0, 3600), 300, replace=False)) * 1000
+        f = rng.normal(0, 10, 300)
+        f[rng.random(300) < 0.2] = np.nan
+        if s == 3:
+            f[:] = np.nan   # buckets of NaNs only -> NaN values (present buckets)
+        kind = np.full(300, 2)
+        rows.append(synth.encode_rows(ts, np.zeros(300, np.int64), f, kind, np.zeros(300, bool)))
+        gids.append(s % 2)
+    order = sorted(range(10), key=lambda i: gids[i])
+    b = synth.from_series([rows[i] for i in order], [gids[i] for i in order])
+    for fn in ["p99", "median", "p50"]:
+        for agg in ["max", "count"]:
+            q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG[fn], ds_interval_ms=600000)
+            assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), agg, ctx=f"{fn} {agg}")
+    q = abi.new_query(T0, T0 + 3600, "max", ds_function=abi.AGG["p95"], ds_all=True)
+    assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "max", ctx="all")
+
+
+def test_pct_large_bucket_lds_sort(eng):
+    # 1 h @ 1 s: 3600 values per bucket (LDS sort up to PCT_CAP = 4096)
+    b = synth.generate(6, T0, 3600, 1000, value_kind=4, n_groups=2, seed=9)
+    q = abi.new_query(T0, T0 + 3599, "max", ds_function=abi.AGG["p99"], ds_interval_ms=3600000)
+    assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "max", ctx="3600/bucket")
+
+
+def test_pct_bucket_over_capacity_is_reported(eng):
+    from opentsdb_amd.engine import EngineError
+    b = synth.generate(2, T0, 7200, 1000, value_kind=0, n_groups=1, seed=9)
+    q = abi.new_query(T0, T0 + 7199, "max", ds_function=abi.AGG["p99"], ds_interval_ms=7200000)
+    with pytest.raises(EngineError) as ei:
+        eng.run_batch(b, q)
+    assert ei.value.java == "NotImplemented"
+
+
+def test_pct_sharded(eng, day_batch):
+    from tests.test_gpu_dist import run_sharded
+    from opentsdb_amd.engine import Engine
+    es = [eng, Engine(0)]
+    try:
+        q = abi.new_query(T0, T0 + 86399, "sum", ds_function=abi.AGG["ep99r7"], ds_interval_ms=3600000)
+        assert_groups_match(run_sharded(es, day_batch, q, 2), O.run_query(day_batch, q), "sum", ctx="x2")
+    finally:
+        es[1].close()
