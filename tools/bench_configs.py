@@ -9,6 +9,13 @@
                O(U*k) AggregationIterator work).
   The CPU baseline is the oracle (oracle/refcpu.c, single thread) on ONE full group of the
   same workload, scaled by the number of groups (every group has the same shape).
+  --config 3   the 1-GPU point of config 3: 10M series x 1 h @10 s (even series int
+               [0, 30000), odd float32), {avg,min,max,count,dev}:1m-avg, 1000 groups -- one
+               pass per aggregator, as the reference runs one TsdbQuery per sub-query.
+  --config 5   one GPU's shard of config 5: 1.25M series x 1 day @10 s float32 (the 8-GPU
+               run holds 10M), sum:1h-p99 and sum:1h-ep99r7, 64 groups.
+  Configs 3 and 5 report HBM GB/s of the dominant kernel like bench.py (SURVEY 8d bytes);
+  their CPU baseline is the oracle on a 256-series sample of the same query.
 """
 from __future__ import annotations
 
@@ -24,6 +31,43 @@ sys.path.insert(0, ROOT)
 T0 = 1356998400
 
 
+def grid_config(args, eng, queries, n_series, n_points, value_kind, int_mod, groups):
+    from opentsdb_amd import abi
+    t = time.perf_counter()
+    eng.synth(n_series, T0, n_points, 10000, value_kind, groups, int_mod, 0x5EED)
+    eng.sync()
+    gen_s = time.perf_counter() - t
+    for name, q in queries.items():
+        eng.run(q)
+        ms, kms = [], []
+        for _ in range(args.steps):
+            t = time.perf_counter()
+            eng.run(q)
+            ms.append((time.perf_counter() - t) * 1000)
+            tm = eng.timing()
+            kms.append(tm.fast_ms if tm.fast_ms > 0 and tm.redo_tiles == 0 else tm.decode_downsample_ms)
+        step_ms = sum(ms) / len(ms)
+        k_ms = sum(kms) / len(kms)
+        line = {"config": args.config, "query": name, "series": n_series, "points": n_points, "groups": groups,
+                "datapoints": int(tm.datapoints), "ms_per_step": step_ms,
+                "datapoints_per_s": tm.datapoints / (step_ms / 1000), "kernel_ms": k_ms,
+                "kernel": "k_fast" if tm.fast_ms > 0 and tm.redo_tiles == 0 else "decode+downsample kernels",
+                "redo_tiles": int(tm.redo_tiles), "tiles": int(tm.tiles),
+                "bytes": int(tm.bytes), "hbm_gbs": tm.bytes / (k_ms / 1000) / 1e9,
+                "hbm_frac_of_8tbs": tm.bytes / (k_ms / 1000) / 8e12, "gen_s": gen_s}
+        if args.cpu:
+            from oracle import oracle as O
+            from opentsdb_amd import synth
+            b = synth.generate(256, T0, n_points, 10000, value_kind=value_kind, n_groups=min(groups, 256),
+                               int_mod=int_mod, seed=0x5EED)
+            t = time.perf_counter()
+            O.run_query(b, q)
+            cpu_s = time.perf_counter() - t
+            line["cpu_baseline"] = {"kind": "port", "cores": 1, "sample": f"256 series x {n_points} dp, same query",
+                                    "datapoints_per_s": 256 * n_points / cpu_s}
+        print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=4)
@@ -33,7 +77,28 @@ def main():
     ap.add_argument("--cpu", action="store_true", help="time the oracle on one group")
     args = ap.parse_args()
     from opentsdb_amd import abi, dist, synth
-    from opentsdb_amd.engine import Engine
+    from opentsdb_amd.engine import Engine, parse_downsample
+
+    def dsq(agg, spec, end):
+        d = parse_downsample(spec)
+        return abi.new_query(T0, end, agg, ds_function=d.ds_function, ds_interval_ms=d.ds_interval_ms,
+                             ds_fill=d.ds_fill)
+
+    if args.config == 3:
+        eng = Engine(0)
+        series = args.series if args.series != 100_000 else 10_000_000
+        groups = args.groups if args.groups != 64 else 1000
+        qs = {f"{a}:1m-avg": dsq(a, "1m-avg", T0 + 3599) for a in ["avg", "min", "max", "count", "dev"]}
+        grid_config(args, eng, qs, series, 360, 2, 30000, groups)
+        eng.close()
+        return
+    if args.config == 5:
+        eng = Engine(0)
+        series = args.series if args.series != 100_000 else 1_250_000
+        qs = {f"sum:1h-{f}": dsq("sum", f"1h-{f}", T0 + 86399) for f in ["p99", "ep99r7"]}
+        grid_config(args, eng, qs, series, 8640, 0, 1, args.groups)
+        eng.close()
+        return
 
     t = time.perf_counter()
     b = synth.generate_counters(args.series, T0, 360, n_groups=args.groups, seed=0x5EED)
