@@ -138,15 +138,17 @@ struct tsdbhip_ctx {
   bool none_tiles_ready = false;
   DevBuf n_tb, n_te, n_tg, n_gtp;
   // scratch
-  DevBuf pa, pb, pn, pf, out_val, out_flag, gact, err, g_dense, g_pres, g_rate, redo, redo_n;
+  DevBuf pa, pb, pn, pf, out_val, out_flag, gact, err, g_dense, g_pres, g_rate, redo, redo_n, redo2, redo2_n;
   DevBuf xbuf, gbuf;
   DevBuf pre_dense, pre_pres;          // percentile / median downsampling
   // raw path scratch
   DevBuf r_rowpt, r_spoff, r_spn, r_grp, r_pts, r_rank, r_bm, r_wb, r_U, r_ooff, r_sg, r_su, r_ots, r_obits, r_oint,
       r_coff, r_cur;                   // multi-GPU: this rank's partial states, gathered states
   // dominant uniform row class of the batch (k_fast specialisation), 0 = none
-  int fast_qw = 0, fast_vl = 0;
+  int fast_qw = 0, fast_vl = 0;        // dominant k_fast row class (0 = none)
+  int fast_qw2 = 0, fast_vl2 = 0;      // second class, chained over the first one's redo list
   bool fast_used = false;
+  const int32_t* redo_final = nullptr;   // device counter of the tiles left for k_grid
   tsdbhip_timing timing{};
   // account() cache (invalidated by every load)
   bool acct_valid = false;
@@ -301,7 +303,7 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   release_batch(c);
   for (DevBuf* b : {&c->pa, &c->pb, &c->pn, &c->pf, &c->out_val, &c->out_flag, &c->gact, &c->err, &c->g_dense,
-                    &c->g_pres, &c->g_rate, &c->redo, &c->redo_n, &c->xbuf, &c->gbuf, &c->r_rowpt,
+                    &c->g_pres, &c->g_rate, &c->redo, &c->redo_n, &c->redo2, &c->redo2_n, &c->xbuf, &c->gbuf, &c->r_rowpt,
                     &c->r_spoff, &c->r_spn, &c->r_grp, &c->r_pts, &c->r_rank, &c->r_bm, &c->r_wb, &c->r_U, &c->r_ooff,
                     &c->r_sg, &c->r_su, &c->r_ots, &c->r_obits, &c->r_oint, &c->r_coff, &c->r_cur, &c->pre_dense, &c->pre_pres})
     b->release();
@@ -390,6 +392,7 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
   c->h_vlen.resize(c->n_rows);
   c->h_flags.resize(c->n_rows);
   int64_t cls[2][2] = {{0, 0}, {0, 0}};   // [qw 2/4][vl 4/8] uniform float rows
+  int64_t cls_vle = 0;                    // 2-byte qualifiers, 1-2 byte integers, one chunk
   for (int64_t r = 0; r < c->n_rows; r++) {
     c->h_ndp[r] = back[r].ndp;
     c->h_base[r] = back[r].base;
@@ -400,12 +403,16 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
     const uint32_t qw = f & ROW_QW_MASK, vl = (f & ROW_VL_MASK) >> ROW_VL_SHIFT;
     if ((f & ROW_ALLF) && !(f & (ROW_ERR | ROW_NAN | ROW_UNSORTED)) && (qw == 2 || qw == 4) && (vl == 4 || vl == 8))
       cls[qw == 4][vl == 8] += back[r].ndp;
+    if ((f & ROW_ALLI) && (f & ROW_VLE2) && !(f & (ROW_ERR | ROW_UNSORTED)) && qw == 2 && back[r].ndp <= 512)
+      cls_vle += back[r].ndp;
   }
-  c->fast_qw = c->fast_vl = 0;
-  int64_t best = 0;
-  for (int a = 0; a < 2; a++)
-    for (int b2 = 0; b2 < 2; b2++)
-      if (cls[a][b2] > best) { best = cls[a][b2]; c->fast_qw = a ? 4 : 2; c->fast_vl = b2 ? 8 : 4; }
+  // the two largest k_fast row classes by datapoints
+  struct Cand { int64_t n; int qw, vl; };
+  std::vector<Cand> cand = {{cls[0][0], 2, 4}, {cls[0][1], 2, 8}, {cls[1][0], 4, 4}, {cls[1][1], 4, 8}, {cls_vle, 2, 0}};
+  std::stable_sort(cand.begin(), cand.end(), [](const Cand& x, const Cand& y) { return x.n > y.n; });
+  c->fast_qw = c->fast_vl = c->fast_qw2 = c->fast_vl2 = 0;
+  if (cand[0].n > 0) { c->fast_qw = cand[0].qw; c->fast_vl = cand[0].vl; }
+  if (cand[1].n > 0) { c->fast_qw2 = cand[1].qw; c->fast_vl2 = cand[1].vl; }
   // malformed rows are reported lazily, when a query reads them (as the reference does)
   return build_tiles(c);
 }
@@ -788,7 +795,9 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   // streaming kernel first (when the batch's row class and the query allow it), then the
   // general kernel over the tiles it handed back
   bool fast = false;
-  if (P.mode == MODE_GRID && c->fast_qw && fast_supported(P.f, c->fast_qw, c->fast_vl) && P.I <= (1LL << 29) &&
+  if (P.mode == MODE_GRID && c->fast_qw &&
+      (fast_supported(P.f, c->fast_qw, c->fast_vl) || (c->fast_qw2 && fast_supported(P.f, c->fast_qw2, c->fast_vl2))) &&
+      P.I <= (1LL << 29) &&
       fast_wave_lds(K, q->rate != 0) <= 32 * 1024 && K > 0) {
     const char* env = std::getenv("TSDBHIP_FAST");
     fast = !(env && env[0] == '0');
@@ -796,22 +805,36 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   c->fast_used = fast;
   HIP_OK(hipEventRecord(c->ev[0], c->stream));
   if (fast) {
-    GridParams fp = gp;
-    fp.unit_s = (c->fast_qw == 2 && P.I % 1000 == 0 && P.B0 % 1000 == 0) ? 1 : 0;
-    fp.In = (int32_t)(fp.unit_s ? P.I / 1000 : P.I);
-    fp.B0n = fp.unit_s ? P.B0 / 1000 : P.B0;
-    fp.rcpn = std::nextafter(1.0 / (double)fp.In, INFINITY);
-    fp.wave_lds = (int32_t)fast_wave_lds(K, q->rate != 0);
-    fp.waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / fp.wave_lds));
-    HIP_OK(c->redo.ensure(std::max<int64_t>(1, nt) * 4));
-    HIP_OK(c->redo_n.ensure(16));
-    HIP_OK(hipMemsetAsync(c->redo_n.p, 0, 4, c->stream));
-    fp.redo_list = c->redo.as<int32_t>();
-    fp.redo_n = c->redo_n.as<int32_t>();
-    HIP_OK(launch_fast(fp, P.f, c->fast_qw, c->fast_vl, c->stream));
+    // class 1 over every tile, class 2 over the tiles class 1 handed back; k_grid takes the rest
+    const int cq[2] = {c->fast_qw, c->fast_qw2}, cv[2] = {c->fast_vl, c->fast_vl2};
+    DevBuf* lists[2] = {&c->redo, &c->redo2};
+    DevBuf* counts[2] = {&c->redo_n, &c->redo2_n};
+    const int32_t* in_list = nullptr;
+    const int32_t* in_n = nullptr;
+    for (int k = 0; k < 2; k++) {
+      if (!cq[k] || !fast_supported(P.f, cq[k], cv[k])) continue;
+      GridParams fp = gp;
+      fp.unit_s = (cq[k] == 2 && P.I % 1000 == 0 && P.B0 % 1000 == 0) ? 1 : 0;
+      fp.In = (int32_t)(fp.unit_s ? P.I / 1000 : P.I);
+      fp.B0n = fp.unit_s ? P.B0 / 1000 : P.B0;
+      fp.rcpn = std::nextafter(1.0 / (double)fp.In, INFINITY);
+      fp.wave_lds = (int32_t)fast_wave_lds(K, q->rate != 0);
+      fp.waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / fp.wave_lds));
+      HIP_OK(lists[k]->ensure(std::max<int64_t>(1, nt) * 4));
+      HIP_OK(counts[k]->ensure(16));
+      HIP_OK(hipMemsetAsync(counts[k]->p, 0, 4, c->stream));
+      fp.tile_list = in_list;
+      fp.tile_list_n = in_n;
+      fp.redo_list = lists[k]->as<int32_t>();
+      fp.redo_n = counts[k]->as<int32_t>();
+      HIP_OK(launch_fast(fp, P.f, cq[k], cv[k], c->stream));
+      in_list = fp.redo_list;
+      in_n = fp.redo_n;
+    }
     HIP_OK(hipEventRecord(c->ev[3], c->stream));
-    gp.tile_list = c->redo.as<int32_t>();
-    gp.tile_list_n = c->redo_n.as<int32_t>();
+    gp.tile_list = in_list;
+    gp.tile_list_n = in_n;
+    c->redo_final = in_n;
   }
   HIP_OK(launch_grid(gp, P.f, c->stream));
   HIP_OK(hipEventRecord(c->ev[1], c->stream));
@@ -954,7 +977,7 @@ int collect(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bo
   if (G) HIP_OK(hipMemcpyAsync(act.data(), c->gact.p, G * 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
   int32_t redo_n = 0;
-  if (timed && c->fast_used) HIP_OK(hipMemcpyAsync(&redo_n, c->redo_n.p, 4, hipMemcpyDeviceToHost, c->stream));
+  if (timed && c->fast_used) HIP_OK(hipMemcpyAsync(&redo_n, c->redo_final, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
   if (timed) record_timing(c, P, redo_n);
   if (err) return fail(err, "error raised by the device path");
@@ -1333,7 +1356,7 @@ extern "C" int tsdbhip_run_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int6
   HIP_OK(hipMemcpyAsync(partials, xb, L.bytes, hipMemcpyDefault, c->stream));
   int32_t err = 0, redo_n = 0;
   HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
-  if (c->fast_used) HIP_OK(hipMemcpyAsync(&redo_n, c->redo_n.p, 4, hipMemcpyDeviceToHost, c->stream));
+  if (c->fast_used) HIP_OK(hipMemcpyAsync(&redo_n, c->redo_final, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
   record_timing(c, P, redo_n);
   if (err) return fail(err, "error raised by the device path");

@@ -33,6 +33,7 @@ enum : uint32_t {
   ROW_UNSORTED = 0x100000,  // datapoint offsets not strictly increasing
   ROW_SFIRST = 0x200000,    // first row of its series (set by the host at load)
   ROW_ALLI = 0x400000,      // every value is an integer
+  ROW_VLE2 = 0x800000,      // every value is 1 or 2 bytes long
 };
 
 // Per-tile partial group state, structure of arrays, [tile][K].

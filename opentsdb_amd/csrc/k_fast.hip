@@ -29,6 +29,7 @@ hipError_t launch_fast_inst<F_ID>(const GridParams& p, int qw, int vl, hipStream
   if (qw == 2 && vl == 8) return launch_fast_t<F_ID, 2, 8>(p, s);
   if (qw == 4 && vl == 4) return launch_fast_t<F_ID, 4, 4>(p, s);
   if (qw == 4 && vl == 8) return launch_fast_t<F_ID, 4, 8>(p, s);
+  if (qw == 2 && vl == 0) return launch_fast_t<F_ID, 2, 0>(p, s);
   return hipErrorNotSupported;
 }
 

@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual,
     }
     // walk every datapoint: validate qualifier/value lengths, certificate stats
     bool bad = qlen == 0;
-    bool allf = true, alli = true, hasnan = false, negz = false, unsorted = false;
+    bool allf = true, alli = true, vmax2 = true, hasnan = false, negz = false, unsorted = false;
     int lsbmin = INT32_MAX;
     double amax = 0.0;
     long long vcarry = 0;
@@ -114,6 +114,7 @@ __global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual,
       prev_off = __shfl(off, (int)min((uint32_t)63, ndp - 1 - i0), 64);
       if (in && !fl) allf = false;
       if (in && fl) alli = false;
+      if (in && len > 2) vmax2 = false;
       if (in && (fl ? (len != 4 && len != 8) : (len == 3 || (len >= 5 && len <= 7)))) bad = true;
       const int incl = wave_incl_sum(len);
       const long long vo = vcarry + incl - len;
@@ -136,6 +137,7 @@ __global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual,
     bad = __any(bad);
     allf = __all(allf);
     alli = __all(alli);
+    vmax2 = __all(vmax2);
     hasnan = __any(hasnan);
     negz = __any(negz);
     unsorted = __any(unsorted);
@@ -149,6 +151,7 @@ __global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual,
       }
       if (allf) flags |= ROW_ALLF;
       if (alli) flags |= ROW_ALLI;
+      if (vmax2) flags |= ROW_VLE2;
       if (hasnan) flags |= ROW_NAN;
       if (negz) flags |= ROW_NEGZ;
       if (unsorted) flags |= ROW_UNSORTED;
@@ -376,7 +379,7 @@ hipError_t launch_grid(const GridParams& p, int f, hipStream_t s) {
 
 bool fast_supported(int f, int qw, int vl) {
   return (f == F_SUM || f == F_AVG || f == F_COUNT || f == F_SQUARESUM || f == F_MIN || f == F_MAX) &&
-         (qw == 2 || qw == 4) && (vl == 4 || vl == 8);
+         (((qw == 2 || qw == 4) && (vl == 4 || vl == 8)) || (qw == 2 && vl == 0));
 }
 
 hipError_t launch_fast(const GridParams& p, int f, int qw, int vl, hipStream_t s) {
@@ -392,7 +395,7 @@ hipError_t launch_fast(const GridParams& p, int f, int qw, int vl, hipStream_t s
   return hipErrorNotSupported;
 }
 
-int64_t fast_wave_lds(int64_t K, bool rate) { return align16(fast_slot_bytes(K, rate)); }
+int64_t fast_wave_lds(int64_t K, bool rate) { return align16(1024 + fast_slot_bytes(K, rate)); }   // + VL==0 value stage
 
 int64_t grid_wave_lds(int64_t K, bool rate, bool gslot) {
   return align16(fixed_lds_bytes() + (gslot ? 0 : slot_lds_bytes(K, rate)));

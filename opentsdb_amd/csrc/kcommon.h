@@ -1100,10 +1100,13 @@ struct FMeta {
 };
 enum : uint32_t { FM_NV = 0x1FFFFFFFu, FM_OK = 1u << 29, FM_NEWSER = 1u << 30, FM_NEWROW = 1u << 31 };
 
+// VL == 0: the vle-integer class (values of 1 or 2 bytes, rows of <= CH datapoints): the
+// lane loads a fixed 16-byte slice of the row's value bytes; values are located after a
+// wave prefix sum of the qualifier lengths and read back from an LDS stage.
 template <int QW, int VL>
 struct FRaw {
-  uint4 q[QW / 2];   // 8 qualifiers of QW bytes
-  uint4 v[VL / 2];   // 8 values of VL bytes
+  uint4 q[QW / 2];               // 8 qualifiers of QW bytes
+  uint4 v[VL == 0 ? 1 : VL / 2]; // 8 values of VL bytes / a 16-B slice of the row's values
 };
 
 template <int F>
@@ -1120,12 +1123,15 @@ __host__ __device__ inline int64_t fast_slot_bytes(int64_t K, bool rate) {
 struct FastLds {
   double* acc;
   uint32_t* cnt;
-  WaveLds w;   // dense == acc, pres, rate, part
+  WaveLds w;          // dense == acc, pres, rate, part
+  uint8_t* vstage;    // VL == 0: the row's value bytes (64 lanes x 16 B)
 };
 
 __device__ __forceinline__ FastLds fast_carve(unsigned char* base, int64_t K, bool rate) {
   FastLds f;
   int64_t o = 0;
+  f.vstage = base;    // used only by the VL == 0 instantiations (fast_wave_lds reserves it)
+  o += 1024;
   f.acc = (double*)(base + o); o += align16(K * 8);
   f.cnt = (uint32_t*)(base + o); o += align16(K * 4);
   f.w.dense = f.acc;
@@ -1155,6 +1161,11 @@ __device__ __forceinline__ void fast_fold(const FastLds& L, int k, double v, uin
 
 template <int QW, int VL>
 __device__ __forceinline__ bool fast_row_ok(uint32_t flags, bool minmax) {
+  if (VL == 0) {
+    const uint32_t want = (uint32_t)QW | ROW_ALLI | ROW_VLE2;
+    const uint32_t mask = ROW_QW_MASK | ROW_ALLI | ROW_VLE2 | ROW_ERR | ROW_UNSORTED;
+    return (flags & mask) == want;
+  }
   const uint32_t want = (uint32_t)QW | ((uint32_t)VL << ROW_VL_SHIFT) | ROW_ALLF;
   const uint32_t mask = ROW_QW_MASK | ROW_VL_MASK | ROW_ALLF | ROW_ERR | ROW_NAN | ROW_UNSORTED |
                         (minmax ? ROW_NEGZ : 0u);
@@ -1201,6 +1212,7 @@ __device__ __forceinline__ int fast_issue(const GridParams& p, const RowDesc* __
       w.sf |= (w.d.flags & ROW_SFIRST) != 0;
       if ((int64_t)w.d.base < p.ss || (int64_t)w.d.base >= p.se) { fwalk_next_row(rows, w); continue; }
       if (!fast_row_ok<QW, VL>(w.d.flags, F == F_MIN || F == F_MAX)) return 2;
+      if (VL == 0 && w.d.ndp > CH) return 2;
     }
     if (w.c0 < (int64_t)w.d.ndp) break;
     fwalk_next_row(rows, w);
@@ -1213,11 +1225,15 @@ __device__ __forceinline__ int fast_issue(const GridParams& p, const RowDesc* __
   // lanes past the end of the row re-read its first datapoints (in bounds, ignored)
   const int64_t i0 = (lane * DPL < nv0) ? w.c0 + (int64_t)lane * DPL : 0;
   const uint4* q = reinterpret_cast<const uint4*>(p.qual + w.d.qoff + i0 * QW);
-  const uint4* v = reinterpret_cast<const uint4*>(p.val + w.d.voff + i0 * VL);
 #pragma unroll
   for (int k = 0; k < QW / 2; k++) b.q[k] = q[k];
+  if (VL == 0) {
+    b.v[0] = *reinterpret_cast<const uint4*>(p.val + w.d.voff + (int64_t)lane * 16);
+  } else {
+    const uint4* v = reinterpret_cast<const uint4*>(p.val + w.d.voff + i0 * VL);
 #pragma unroll
-  for (int k = 0; k < VL / 2; k++) b.v[k] = v[k];
+    for (int k = 0; k < VL / 2; k++) b.v[k] = v[k];
+  }
   w.c0 += CH;
   return 0;
 }
@@ -1247,6 +1263,48 @@ __device__ __forceinline__ double f_value(const FRaw<QW, VL>& b, int j) {
     const uint32_t hi = (j & 1) ? u.z : u.x;
     const uint32_t lo = (j & 1) ? u.w : u.y;
     return __longlong_as_double((long long)(((uint64_t)__builtin_bswap32(hi) << 32) | __builtin_bswap32(lo)));
+  }
+}
+
+// qualifier flags (low nibble) of datapoint j
+template <int QW, int VL>
+__device__ __forceinline__ uint32_t f_flags(const FRaw<QW, VL>& b, int j) {
+  if (QW == 2) {
+    const uint32_t wd = (j >> 1) == 0 ? b.q[0].x : (j >> 1) == 1 ? b.q[0].y : (j >> 1) == 2 ? b.q[0].z : b.q[0].w;
+    const uint32_t t = __builtin_bswap32(wd);
+    return (j & 1) ? (t & 0xF) : ((t >> 16) & 0xF);
+  } else {
+    const uint4 u = b.q[j >> 2];
+    const uint32_t wd = (j & 3) == 0 ? u.x : (j & 3) == 1 ? u.y : (j & 3) == 2 ? u.z : u.w;
+    return __builtin_bswap32(wd) & 0xF;
+  }
+}
+
+// VL == 0: the lane's 8 vle integers (1 or 2 bytes, RowSeq.extractIntegerValue
+// src/core/RowSeq.java:233-245) from the row's value bytes staged in LDS.  Called by the
+// whole wave.
+template <int QW, int VL>
+__device__ __forceinline__ void f_values_vle(const FastLds& L, const FRaw<QW, VL>& b, int nvl, double xs[DPL]) {
+  const int lane = lane_id();
+  int len[DPL];
+  int tot = 0;
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    len[j] = (j < nvl) ? (int)(f_flags<QW, VL>(b, j) & 7) + 1 : 0;
+    tot += len[j];
+  }
+  const int incl = wave_incl_sum(tot);
+  int o = incl - tot;
+  WAVE_SYNC();
+  reinterpret_cast<uint4*>(L.vstage)[lane] = b.v[0];
+  WAVE_SYNC();
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    int64_t v = 0;
+    if (len[j] == 1) v = (int8_t)L.vstage[o];
+    else if (len[j] == 2) v = (int16_t)(uint16_t)(((uint32_t)L.vstage[o] << 8) | L.vstage[o + 1]);
+    xs[j] = (double)v;
+    o += len[j];
   }
 }
 
@@ -1281,6 +1339,13 @@ __device__ __forceinline__ void fast_chunk(const GridParams& p, const FastLds& L
   uint32_t fld[DPL];
 #pragma unroll
   for (int j = 0; j < DPL; j++) fld[j] = f_field<QW, VL>(b, j);
+  double xs[DPL];
+  if (VL == 0) {
+    f_values_vle<QW, VL>(L, b, nvl, xs);
+  } else {
+#pragma unroll
+    for (int j = 0; j < DPL; j++) xs[j] = f_value<QW, VL>(b, j);
+  }
   uint32_t flast = fld[DPL - 1];
   if (!FULL) {
 #pragma unroll
@@ -1302,7 +1367,7 @@ __device__ __forceinline__ void fast_chunk(const GridParams& p, const FastLds& L
     for (int j = 0; j < DPL; j++) {
       const bool valid = FULL || j < nvl;
       const bool inF = valid && fld[j] < Tf;
-      double x = f_value<QW, VL>(b, j);
+      double x = xs[j];
       if (F == F_SQUARESUM) x = x * x;
       if (F == F_MIN) {
         P = fmin(P, valid ? x : (double)INFINITY);
@@ -1330,7 +1395,7 @@ __device__ __forceinline__ void fast_chunk(const GridParams& p, const FastLds& L
         if (n >= 0) {
           const int s = f_slot(p, m, n);
           if (s < K) {
-            double x = f_value<QW, VL>(b, j);
+            double x = xs[j];
             if (F == F_SQUARESUM) x = x * x;
             fast_fold<F>(L, s, x, 1u);
           }
@@ -1384,7 +1449,11 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (scalar) tile index
-  const int64_t tile = (int64_t)blockIdx.x * p.waves + wave;
+  int64_t tile = (int64_t)blockIdx.x * p.waves + wave;
+  if (p.tile_list) {   // chained launch over the tiles an earlier k_fast class handed back
+    if (tile >= (int64_t)*p.tile_list_n) return;
+    tile = p.tile_list[tile];
+  }
   if (tile >= p.n_tiles) return;
   const int K = (int)p.K;
   const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0);

@@ -170,3 +170,46 @@ def test_fast_device_bench_shape(eng):
     q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
     t = check(eng, None, q, "sum", "config2 4096 series", expect_redo=False)
     assert t.datapoints == 4096 * 3600
+
+
+# ---- vle-integer class (k_fast<F, 2, 0>): 1-2 byte integers in one-chunk rows ----------
+@pytest.mark.parametrize("ds", DS)
+@pytest.mark.parametrize("interval", [10000, 60000, 90000, 3600000])
+def test_fast_vle_ints_config1_shape(eng, ds, interval):
+    b = synth.generate(96, T0, 360, 10000, value_kind=1, n_groups=3, int_mod=2000, seed=13)
+    q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG[ds], ds_interval_ms=interval)
+    check(eng, b, q, "sum", f"vle {ds}-{interval}", expect_redo=False)
+
+
+@pytest.mark.parametrize("agg", ["sum", "avg", "min", "max", "count", "dev"])
+def test_fast_config3_shape_two_classes(eng, agg):
+    """Even series int [0, 30000), odd series float32 (config 3).  With an even number of
+    groups every tile is one class: the float class runs first, the vle class takes the
+    tiles it hands back, nothing is left for k_grid."""
+    b = synth.generate(256, T0, 360, 10000, value_kind=2, n_groups=4, int_mod=30000, seed=0x5EED)
+    q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+    check(eng, b, q, agg, f"config3 {agg}", expect_redo=False)
+
+
+def test_fast_mixed_tiles_fall_through_to_grid(eng):
+    b = synth.generate(120, T0, 360, 10000, value_kind=2, n_groups=3, int_mod=30000, seed=1)
+    q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+    check(eng, b, q, "sum", "mixed tiles", expect_redo=True)
+    # 4-byte integers are outside the vle class
+    b = synth.generate(96, T0, 360, 10000, value_kind=1, n_groups=2, int_mod=1 << 20, seed=2)
+    check(eng, b, q, "sum", "4-byte ints", expect_redo=True)
+
+
+def test_fast_vle_rate_and_fill(eng):
+    b = synth.generate(64, T0 + 900, 200, 10000, value_kind=1, n_groups=2, int_mod=30000, seed=8)
+    q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000, rate=True)
+    check(eng, b, q, "sum", "vle rate", expect_redo=False)
+    q = abi.new_query(T0, T0 + 7199, "avg", ds_function=abi.AGG["sum"], ds_interval_ms=60000, ds_fill=abi.FILL_ZERO)
+    check(eng, b, q, "avg", "vle fill", expect_redo=False)
+
+
+def test_fast_device_config3_shape(eng):
+    eng.synth(20000, T0, 360, 10000, 2, 1000, 30000, 0x5EED)
+    q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+    t = check(eng, None, q, "sum", "config3 20000 series", expect_redo=False)
+    assert t.datapoints == 20000 * 360
