@@ -91,6 +91,10 @@ int f_of(int a) {
 
 inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 
+// bytes past the end of the qualifier / value blobs that kernels may read (never use):
+// k_fast's vle class loads a 1 KB value window from each row start
+constexpr int64_t BLOB_SLACK = 1024 + 64;
+
 struct DevBuf {
   void* p = nullptr;
   size_t n = 0;
@@ -472,7 +476,8 @@ extern "C" int tsdbhip_load(tsdbhip_ctx* c, const tsdbhip_batch* b) {
   c->qual_bytes = qtot;
   c->val_bytes = vtot;
   // staging: re-laid-out blobs
-  std::vector<uint8_t> hq(qtot + 64, 0), hv(vtot + 64, 0);
+  // tail slack: k_fast's vle class reads a fixed 1 KB value window from every row start
+  std::vector<uint8_t> hq(qtot + BLOB_SLACK, 0), hv(vtot + BLOB_SLACK, 0);
   {
     // copy rows in the order their offsets were assigned (before the per-series sort)
     uint64_t qo = 0, vo = 0;
@@ -587,10 +592,10 @@ extern "C" int tsdbhip_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp) {
   c->qual_bytes = (uint64_t)(S * QS);
   c->val_bytes = vtot;
   HIP_OK(c->rows.ensure(rd.size() * sizeof(RowDesc)));
-  HIP_OK(c->qual.ensure(c->qual_bytes + 64));
-  HIP_OK(c->val.ensure(c->val_bytes + 64));
-  HIP_OK(hipMemsetAsync(c->qual.p, 0, c->qual_bytes + 64, c->stream));
-  HIP_OK(hipMemsetAsync(c->val.p, 0, c->val_bytes + 64, c->stream));
+  HIP_OK(c->qual.ensure(c->qual_bytes + BLOB_SLACK));
+  HIP_OK(c->val.ensure(c->val_bytes + BLOB_SLACK));
+  HIP_OK(hipMemsetAsync(c->qual.p, 0, c->qual_bytes + BLOB_SLACK, c->stream));
+  HIP_OK(hipMemsetAsync(c->val.p, 0, c->val_bytes + BLOB_SLACK, c->stream));
   HIP_OK(hipMemcpyAsync(c->rows.p, rd.data(), rd.size() * sizeof(RowDesc), hipMemcpyHostToDevice, c->stream));
   p.rows = c->rows.as<RowDesc>();
   p.qual = c->qual.as<uint8_t>();
@@ -766,6 +771,10 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   gp.part = Partials{c->pa.as<double>(), c->pb.as<double>(), c->pn.as<uint32_t>(), c->pf.as<uint32_t>()};
   gp.group_active = c->gact.as<uint32_t>();
   gp.err = c->err.as<int32_t>();
+  if (const char* dbg = std::getenv("TSDBHIP_DBG")) gp.dbg = std::atoi(dbg);
+  gp.n_rows_total = c->n_rows;
+  gp.qual_cap = c->qual.n;
+  gp.val_cap = c->val.n;
   if (P.f == F_SEL) {
     // percentile / median: per-series bucket order statistics, then the group-by step
     HIP_OK(c->pre_dense.ensure(std::max<int64_t>(1, c->n_series * K) * 8));
@@ -788,7 +797,16 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     gp.waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / gp.wave_lds));
     c->fast_used = false;
     HIP_OK(hipEventRecord(c->ev[0], c->stream));
-    HIP_OK(launch_pct(gp, c->stream));
+    HIP_OK(c->redo.ensure(std::max<int64_t>(1, c->n_series) * 4));
+    HIP_OK(c->redo_n.ensure(16));
+    HIP_OK(hipMemsetAsync(c->redo_n.p, 0, 4, c->stream));
+    gp.redo_list = c->redo.as<int32_t>();
+    gp.redo_n = c->redo_n.as<int32_t>();
+    HIP_OK(launch_pct(gp, false, c->n_series, c->stream));
+    int32_t nbig = 0;   // series with a bucket of more than 512 values: the LDS-sort pass
+    HIP_OK(hipMemcpyAsync(&nbig, c->redo_n.p, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    HIP_OK(launch_pct(gp, true, nbig, c->stream));
     HIP_OK(launch_emit(gp, c->stream));
     HIP_OK(hipEventRecord(c->ev[1], c->stream));
   } else {

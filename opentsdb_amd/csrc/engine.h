@@ -111,6 +111,11 @@ struct GridParams {
   int64_t n_series;
   double* pre_dense;     // [n_series][K]
   uint8_t* pre_pres;     // [n_series][K]
+  int32_t dbg;           // profiling switches (TSDBHIP_DBG): 1 skip emit, 2 skip fold, 4 skip chunk
+  // allocation bounds: k_fast checks every descriptor / chunk address against them and
+  // reports TSDB_E_BOUNDS instead of touching memory outside the blobs
+  int64_t n_rows_total;
+  uint64_t qual_cap, val_cap;
 };
 
 struct ReduceParams {
@@ -217,7 +222,7 @@ int64_t fast_wave_lds(int64_t K, bool rate);
 hipError_t launch_reduce(const ReduceParams& p, hipStream_t s);
 // percentile / median downsampling (k_pct.hip): bucket order statistics, then group-by
 static constexpr int PCT_CAP = 4096;   // values per bucket sorted in LDS
-hipError_t launch_pct(const GridParams& p, hipStream_t s);
+hipError_t launch_pct(const GridParams& p, bool big, int64_t n, hipStream_t s);
 hipError_t launch_emit(const GridParams& p, hipStream_t s);
 hipError_t launch_rank_merge(const RankMergeParams& p, hipStream_t s);
 // per-downsample-function instantiations (k_grid.hip / k_fast.hip, one object per F)

@@ -3,10 +3,11 @@
 // :397-431), then the group-by step over the resulting bucket values.
 //
 //  * k_pct   one wave per series.  Decodes the series' rows in 512-datapoint chunks
-//            (decode_generic: every row class), gathers each bucket's non-NaN values in
-//            an LDS buffer, and at the bucket's end sorts them -- in registers with a
-//            64-lane bitonic network when <= 512 values (8 per lane), in LDS otherwise
-//            (<= PCT_CAP) -- and selects.  Downsampler.runDouble is always called, and
+//            (prefetched register decode for uniform rows, decode_generic otherwise),
+//            gathers each bucket's non-NaN values in an LDS buffer, and at the bucket's
+//            end sorts them -- in registers with a 64-lane bitonic network (<= 512
+//            values, 8 per lane); series with larger buckets go to a second pass that
+//            sorts in LDS (<= PCT_CAP values) -- and selects.  Downsampler.runDouble is always called, and
 //            PercentileAgg.runDouble ignores the estimation type (:690), so every
 //            percentile uses commons-math3 3.4.1 LEGACY: pos = p (n + 1).
 //  * k_emit  one wave per tile: the bucket values -> SpanGroup contributions (LERP, fill,
@@ -107,7 +108,7 @@ __device__ __forceinline__ double reg_at(const double v[DPL], int i) {
 __device__ __forceinline__ double bucket_value(const GridParams& p, double* buf, int n) {
   const int lane = lane_id();
   if (n == 0) return (double)NAN;
-  if (n > PCT_CAP) {
+  if (n > PCT_CAP) {   // only the BIG pass gets here
     if (lane == 0) set_err(p.err, TSDB_E_NOT_IMPLEMENTED);
     return (double)NAN;
   }
@@ -129,11 +130,18 @@ __device__ __forceinline__ double bucket_value(const GridParams& p, double* buf,
   return select_sorted(p.sel_fn, n, [&](int i) { return buf[i]; });
 }
 
-__global__ __launch_bounds__(128) void k_pct(GridParams p) {
+// Order statistics per (series, bucket).  BIG = false: every series, buckets of at most
+// CH values (register sort), 4 waves per block; a series with a larger bucket is appended
+// to p.redo_list and left to the BIG pass (one wave per listed series, LDS buffer of
+// PCT_CAP values).  Uniform rows are decoded from registers with a one-chunk prefetch
+// (load_raw / decode_raw, as k_grid); other row classes through decode_generic.
+template <bool BIG>
+__global__ __launch_bounds__(256) void k_pct(GridParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int CAP = BIG ? PCT_CAP : CH;
   const int lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  unsigned char* base = smem + (int64_t)wave * (VBUF + PCT_CAP * 8);
+  unsigned char* base = smem + (int64_t)wave * (VBUF + CAP * 8);
   WaveLds W;
   W.dpv = (double*)base;
   W.vbuf = base;
@@ -141,25 +149,55 @@ __global__ __launch_bounds__(128) void k_pct(GridParams p) {
   W.mv = (uint32_t*)(base + CH * 4);
   double* buf = (double*)(base + VBUF);
   const int K = (int)p.K;
-  const int64_t s = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+  int64_t s = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+  if (BIG) {
+    if (s >= (int64_t)*p.redo_n) return;
+    s = p.redo_list[s];
+  }
   if (s >= p.n_series) return;
   double* dense = p.pre_dense + s * K;
   uint8_t* pres = p.pre_pres + s * K;
   for (int k = lane; k < K; k += 64) pres[k] = 0;
+  // rows of the series inside the scan range: [ra, rb) (rows are in base-time order)
+  const int64_t r0 = p.series_row_ptr[s], r1 = p.series_row_ptr[s + 1];
+  int64_t ra = r0;
+  while (ra < r1 && (int64_t)p.rows[ra].base < p.ss) ra++;
+  int64_t rb = ra;
+  while (rb < r1 && (int64_t)p.rows[rb].base < p.se) rb++;
   int cur = -1;      // open bucket
   int cnt = 0;       // its non-NaN values (in buf)
-  const int64_t r0 = p.series_row_ptr[s], r1 = p.series_row_ptr[s + 1];
-  for (int64_t r = r0; r < r1; r++) {
-    const RowDesc d = p.rows[r];
-    if ((int64_t)d.base < p.ss) continue;
-    if ((int64_t)d.base >= p.se) break;
-    if (d.flags & ROW_ERR) { if (lane == 0) set_err(p.err, TSDB_E_ILLEGAL_DATA); continue; }
+  bool big = false;
+  Raw rc = {}, rn = {};
+  RowDesc d = {};
+  if (ra < rb) {
+    d = p.rows[ra];
+    if (row_uniform(d)) load_raw(p, d, 0, rc);
+  }
+  for (int64_t r = ra; r < rb && !big; r++) {
+    const bool has_next = r + 1 < rb;
+    RowDesc nd = {};
+    if (has_next) nd = p.rows[r + 1];
+    if (d.flags & ROW_ERR) {
+      if (lane == 0) set_err(p.err, TSDB_E_ILLEGAL_DATA);
+      if (has_next && row_uniform(nd)) load_raw(p, nd, 0, rc);
+      d = nd;
+      continue;
+    }
     const RowGeom g = row_geom(p, d.base);
+    const bool uni = row_uniform(d);
     int64_t vcur = 0;
-    for (int64_t c0 = 0; c0 < (int64_t)d.ndp; c0 += CH) {
+    for (int64_t c0 = 0; c0 < (int64_t)d.ndp && !big; c0 += CH) {
+      // prefetch the next chunk (same row, or the first chunk of the next row)
+      if (c0 + CH < (int64_t)d.ndp) {
+        if (uni) load_raw(p, d, c0 + CH, rn);
+      } else if (has_next && row_uniform(nd)) {
+        load_raw(p, nd, 0, rn);
+      }
       int slot[DPL];
       double val[DPL];
-      decode_generic(p, d, g, c0, W, vcur, slot, val);
+      if (uni) decode_raw(p, d, g, c0, rc, slot, val);
+      else decode_generic(p, d, g, c0, W, vcur, slot, val);
+      rc = rn;
       bool left[DPL];
 #pragma unroll
       for (int j = 0; j < DPL; j++) left[j] = slot[j] >= 0;
@@ -182,21 +220,31 @@ __global__ __launch_bounds__(128) void k_pct(GridParams p) {
 #pragma unroll
         for (int j = 0; j < DPL; j++) if (left[j] && slot[j] == mn && !isnan(val[j])) mine++;
         const int incl = wave_incl_sum(mine);
+        const int total = __shfl(incl, 63, 64);
+        if (!BIG && cnt + total > CAP) {   // bucket too large for the register sort
+          big = true;
+          break;
+        }
         int o = cnt + incl - mine;
 #pragma unroll
         for (int j = 0; j < DPL; j++) {
           if (left[j] && slot[j] == mn) {
             if (!isnan(val[j])) {
-              if (o < PCT_CAP) buf[o] = val[j];
+              if (o < CAP) buf[o] = val[j];
               o++;
             }
             left[j] = false;
           }
         }
-        cnt += __shfl(incl, 63, 64);
+        cnt += total;
         WAVE_SYNC();
       }
     }
+    d = nd;
+  }
+  if (big) {
+    if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)s;
+    return;
   }
   if (cur >= 0) {
     const double x = bucket_value(p, buf, cnt);
@@ -254,12 +302,17 @@ __global__ __launch_bounds__(256) void k_emit(GridParams p) {
   }
 }
 
-hipError_t launch_pct(const GridParams& p, hipStream_t s) {
-  if (p.n_series == 0) return hipSuccess;
-  const size_t lds = 2 * (size_t)(VBUF + PCT_CAP * 8);
-  hipError_t e = hipFuncSetAttribute((const void*)k_pct, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_pct, dim3((unsigned)((p.n_series + 1) / 2)), dim3(128), lds, s, p);
+hipError_t launch_pct(const GridParams& p, bool big, int64_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (big) {
+    const size_t lds = 2 * (size_t)(VBUF + PCT_CAP * 8);
+    hipError_t e = hipFuncSetAttribute((const void*)k_pct<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pct<true>, dim3((unsigned)((n + 1) / 2)), dim3(128), lds, s, p);
+  } else {
+    const size_t lds = 4 * (size_t)(VBUF + CH * 8);
+    hipLaunchKernelGGL(k_pct<false>, dim3((unsigned)((n + 3) / 4)), dim3(256), lds, s, p);
+  }
   return hipGetLastError();
 }
 

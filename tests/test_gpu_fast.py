@@ -214,3 +214,24 @@ def test_fast_device_config3_shape(eng):
     q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
     t = check(eng, None, q, "sum", "config3 20000 series", expect_redo=False)
     assert t.datapoints == 20000 * 360
+
+
+def test_fast_full_tiles_config3_shape(eng):
+    """>= 524288 series: full 64-series tiles (64 rows in the walker's LDS window); both
+    k_fast classes against the general kernel, bit for bit."""
+    eng.synth(600000, T0, 360, 10000, 2, 1000, 30000, 0x5EED)
+    q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+    fast, tf = run_path(eng, None, q, True)
+    gen, tg = run_path(eng, None, q, False)
+    assert tf.redo_tiles == 0 and tf.fast_ms > 0
+    assert_bit_equal(fast, gen, "config3 600k")
+
+
+def test_fast_multi_row_series_window_refill(eng):
+    """Tiles of 64 series x 24 rows: the descriptor window refills every 64 rows."""
+    eng.synth(600000, T0, 24 * 36, 100000, 0, 64, 1, 7)
+    q = abi.new_query(T0, T0 + 86399, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=3600000)
+    fast, tf = run_path(eng, None, q, True)
+    gen, tg = run_path(eng, None, q, False)
+    assert tf.redo_tiles == 0 and tf.fast_ms > 0
+    assert_bit_equal(fast, gen, "24 rows per series")
