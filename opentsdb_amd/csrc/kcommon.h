@@ -1207,12 +1207,9 @@ __device__ __forceinline__ void fwin_fill(const GridParams& p, const RowDesc* __
       set_err(p.err, TSDB_E_BOUNDS);
       return;
     }
-    const uint4* src = reinterpret_cast<const uint4*>(rows + w.r0 + w0 + lane);
-    uint4* dst = reinterpret_cast<uint4*>(L.dwin + lane);
-    const uint4 a = src[0], b = src[1], c = src[2];
-    dst[0] = a;
-    dst[1] = b;
-    dst[2] = c;
+    // typed copy: the window is read back through RowDesc fields, so it must also be
+    // written as RowDesc (a uint4 store would not alias them under strict aliasing)
+    L.dwin[lane] = rows[w.r0 + w0 + lane];
   }
   WAVE_SYNC();
   w.w0 = w0;
