@@ -116,6 +116,7 @@ struct GridParams {
   // reports TSDB_E_BOUNDS instead of touching memory outside the blobs
   int64_t n_rows_total;
   uint64_t qual_cap, val_cap;
+  uint64_t* bounds_info;  // [8] details of the first failed check (host reports them)
 };
 
 struct ReduceParams {

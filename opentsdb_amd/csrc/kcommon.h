@@ -1226,10 +1226,11 @@ __device__ __forceinline__ const RowDesc& fwin_row(const GridParams& p, const Ro
 __device__ __forceinline__ void fwalk_load(const GridParams& p, const RowDesc* __restrict__ rows, const FastLds& L,
                                            FWalk& w) {
   const RowDesc& x = fwin_row(p, rows, L, w, w.r);
-  w.d.qoff = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x.qoff >> 32)) << 32) |
-             __builtin_amdgcn_readfirstlane((uint32_t)x.qoff);
-  w.d.voff = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x.voff >> 32)) << 32) |
-             __builtin_amdgcn_readfirstlane((uint32_t)x.voff);
+  // (readfirstlane returns int: go through uint32_t so the low half is not sign-extended)
+  w.d.qoff = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x.qoff >> 32)) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x.qoff);
+  w.d.voff = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x.voff >> 32)) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x.voff);
   w.d.base = __builtin_amdgcn_readfirstlane(x.base);
   w.d.ndp = __builtin_amdgcn_readfirstlane(x.ndp);
   w.d.flags = __builtin_amdgcn_readfirstlane(x.flags);
@@ -1274,7 +1275,11 @@ __device__ __forceinline__ int fast_issue(const GridParams& p, const RowDesc* __
     const uint64_t qend = w.d.qoff + last * QW;
     const uint64_t vend = w.d.voff + (VL == 0 ? 1024ull : last * VL);
     if (qend > p.qual_cap || vend > p.val_cap) {
-      set_err(p.err, TSDB_E_BOUNDS);
+      if (lane == 0 && atomicCAS(p.err, 0, TSDB_E_BOUNDS) == 0 && p.bounds_info) {
+        p.bounds_info[0] = (uint64_t)w.r0; p.bounds_info[1] = (uint64_t)w.r; p.bounds_info[2] = (uint64_t)w.w0;
+        p.bounds_info[3] = (uint64_t)w.c0; p.bounds_info[4] = w.d.qoff; p.bounds_info[5] = w.d.voff;
+        p.bounds_info[6] = w.d.ndp; p.bounds_info[7] = w.d.base;
+      }
       return 2;
     }
   }
