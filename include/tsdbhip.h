@@ -42,8 +42,7 @@ enum {
   TSDB_E_CLASS_CAST = -9,        /* ClassCastException */
   TSDB_E_HIP = -20,              /* device/runtime failure (no reference counterpart) */
   TSDB_E_NOMEM = -21,
-  TSDB_E_NOT_IMPLEMENTED = -22,  /* valid reference query this engine does not run yet */
-  TSDB_E_BOUNDS = -23            /* internal: a kernel address check failed (nothing was read) */
+  TSDB_E_NOT_IMPLEMENTED = -22   /* valid reference query this engine does not run yet */
 };
 
 /* ---- Aggregators (src/core/Aggregators.java:47-203) ----------------------- */

@@ -23,7 +23,6 @@ TSDB_E_CLASS_CAST = -9
 TSDB_E_HIP = -20
 TSDB_E_NOMEM = -21
 TSDB_E_NOT_IMPLEMENTED = -22
-TSDB_E_BOUNDS = -23
 
 ERROR_NAMES = {
     TSDB_E_ILLEGAL_DATA: "IllegalDataException",
@@ -37,7 +36,6 @@ ERROR_NAMES = {
     TSDB_E_HIP: "HipError",
     TSDB_E_NOMEM: "OutOfMemory",
     TSDB_E_NOT_IMPLEMENTED: "NotImplemented",
-    TSDB_E_BOUNDS: "BoundsCheck",
 }
 
 # ---- aggregators (src/core/Aggregators.java:47-203) ---------------------------

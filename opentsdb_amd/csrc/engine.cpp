@@ -145,7 +145,6 @@ struct tsdbhip_ctx {
   DevBuf pa, pb, pn, pf, out_val, out_flag, gact, err, g_dense, g_pres, g_rate, redo, redo_n, redo2, redo2_n;
   DevBuf xbuf, gbuf;
   DevBuf pre_dense, pre_pres;          // percentile / median downsampling
-  DevBuf binfo;                        // k_fast bounds-check report
   // raw path scratch
   DevBuf r_rowpt, r_spoff, r_spn, r_grp, r_pts, r_rank, r_bm, r_wb, r_U, r_ooff, r_sg, r_su, r_ots, r_obits, r_oint,
       r_coff, r_cur;                   // multi-GPU: this rank's partial states, gathered states
@@ -310,7 +309,7 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   for (DevBuf* b : {&c->pa, &c->pb, &c->pn, &c->pf, &c->out_val, &c->out_flag, &c->gact, &c->err, &c->g_dense,
                     &c->g_pres, &c->g_rate, &c->redo, &c->redo_n, &c->redo2, &c->redo2_n, &c->xbuf, &c->gbuf, &c->r_rowpt,
                     &c->r_spoff, &c->r_spn, &c->r_grp, &c->r_pts, &c->r_rank, &c->r_bm, &c->r_wb, &c->r_U, &c->r_ooff,
-                    &c->r_sg, &c->r_su, &c->r_ots, &c->r_obits, &c->r_oint, &c->r_coff, &c->r_cur, &c->pre_dense, &c->pre_pres, &c->binfo})
+                    &c->r_sg, &c->r_su, &c->r_ots, &c->r_obits, &c->r_oint, &c->r_coff, &c->r_cur, &c->pre_dense, &c->pre_pres})
     b->release();
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -773,12 +772,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   gp.group_active = c->gact.as<uint32_t>();
   gp.err = c->err.as<int32_t>();
   if (const char* dbg = std::getenv("TSDBHIP_DBG")) gp.dbg = std::atoi(dbg);
-  gp.n_rows_total = c->n_rows;
-  gp.qual_cap = c->qual.n;
-  gp.val_cap = c->val.n;
-  HIP_OK(c->binfo.ensure(64));
-  HIP_OK(hipMemsetAsync(c->binfo.p, 0, 64, c->stream));
-  gp.bounds_info = c->binfo.as<uint64_t>();
+
   if (P.f == F_SEL) {
     // percentile / median: per-series bucket order statistics, then the group-by step
     HIP_OK(c->pre_dense.ensure(std::max<int64_t>(1, c->n_series * K) * 8));
@@ -1002,17 +996,6 @@ int collect(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bo
   if (timed && c->fast_used) HIP_OK(hipMemcpyAsync(&redo_n, c->redo_final, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
   if (timed) record_timing(c, P, redo_n);
-  if (err == TSDB_E_BOUNDS) {
-    uint64_t bi[8] = {};
-    HIP_OK(hipMemcpy(bi, c->binfo.p, 64, hipMemcpyDeviceToHost));
-    char msg[512];
-    std::snprintf(msg, sizeof msg,
-                  "bounds check: r0=%llu r=%llu w0=%lld c0=%lld qoff=%llu voff=%llu ndp=%llu base=%llu qcap=%llu vcap=%llu",
-                  (unsigned long long)bi[0], (unsigned long long)bi[1], (long long)bi[2], (long long)bi[3],
-                  (unsigned long long)bi[4], (unsigned long long)bi[5], (unsigned long long)bi[6],
-                  (unsigned long long)bi[7], (unsigned long long)c->qual.n, (unsigned long long)c->val.n);
-    return fail(err, msg);
-  }
   if (err) return fail(err, "error raised by the device path");
   if (P.mode == MODE_ALL) {
     // AggregationIterator ctor: the single "all" point is skipped unless start_time <= qs <= end_time

@@ -112,11 +112,6 @@ struct GridParams {
   double* pre_dense;     // [n_series][K]
   uint8_t* pre_pres;     // [n_series][K]
   int32_t dbg;           // profiling switches (TSDBHIP_DBG): 1 skip emit, 2 skip fold, 4 skip chunk
-  // allocation bounds: k_fast checks every descriptor / chunk address against them and
-  // reports TSDB_E_BOUNDS instead of touching memory outside the blobs
-  int64_t n_rows_total;
-  uint64_t qual_cap, val_cap;
-  uint64_t* bounds_info;  // [8] details of the first failed check (host reports them)
 };
 
 struct ReduceParams {

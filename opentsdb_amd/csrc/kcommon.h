@@ -1096,9 +1096,7 @@ __global__ __launch_bounds__(256) void k_grid(GridParams p) {
 // by k_grid, the general (sequential-order) kernel.
 struct FMeta {
   uint32_t bits;   // datapoints of the row from this chunk's start | FM_* flags
-  uint32_t base;   // FM_NEWROW chunks: the row's base time and certificate inputs
-  int32_t lsb;
-  double amax;
+  int32_t rrel;    // row index relative to the tile's first row
 };
 enum : uint32_t { FM_NV = 0x1FFFFFFFu, FM_OK = 1u << 29, FM_NEWSER = 1u << 30, FM_NEWROW = 1u << 31 };
 
@@ -1116,10 +1114,6 @@ __device__ __forceinline__ constexpr bool fast_f() {
   return F == F_SUM || F == F_AVG || F == F_COUNT || F == F_SQUARESUM || F == F_MIN || F == F_MAX;
 }
 
-// row descriptors per k_fast descriptor window (LDS): the walker reads them from LDS
-// instead of chasing scalar loads row by row
-static constexpr int FWIN = 64;
-
 __host__ __device__ inline int64_t fast_slot_bytes(int64_t K, bool rate) {
   // acc (f64, also the dense bucket values), cnt (u32), pres (u8), [rate f64], partials
   return align16(K * 8) + align16(K * 4) + align16(K) + (rate ? align16(K * 8) : 0) + align16(K * 8) * 2 +
@@ -1131,7 +1125,6 @@ struct FastLds {
   uint32_t* cnt;
   WaveLds w;          // dense == acc, pres, rate, part
   uint8_t* vstage;    // VL == 0: the row's value bytes (64 lanes x 16 B)
-  RowDesc* dwin;      // FWIN row descriptors of the tile (the walker's window)
 };
 
 __device__ __forceinline__ FastLds fast_carve(unsigned char* base, int64_t K, bool rate) {
@@ -1139,8 +1132,6 @@ __device__ __forceinline__ FastLds fast_carve(unsigned char* base, int64_t K, bo
   int64_t o = 0;
   f.vstage = base;    // used only by the VL == 0 instantiations (fast_wave_lds reserves it)
   o += 1024;
-  f.dwin = (RowDesc*)(base + o);
-  o += FWIN * (int64_t)sizeof(RowDesc);
   f.acc = (double*)(base + o); o += align16(K * 8);
   f.cnt = (uint32_t*)(base + o); o += align16(K * 4);
   f.w.dense = f.acc;
@@ -1188,101 +1179,49 @@ struct FDesc {       // the descriptor fields the walker needs
   uint32_t base, ndp, flags;
 };
 
+__device__ __forceinline__ FDesc fdesc(const RowDesc* __restrict__ rows, int64_t r) {
+  const RowDesc& x = rows[r];
+  FDesc d;
+  d.qoff = x.qoff; d.voff = x.voff; d.base = x.base; d.ndp = x.ndp; d.flags = x.flags;
+  return d;
+}
+
 struct FWalk {
   int64_t r0;        // first row of the tile
   int32_t r, rend;   // current row, end of the tile's rows (relative to r0)
   int32_t c0;        // next chunk offset inside row r
   int32_t sf;        // a series start was passed since the last issued chunk
-  int32_t w0;        // first row (relative) held in the LDS descriptor window
-  FDesc d;           // row r
+  FDesc d, nd;       // rows r and r + 1
 };
 
-// Loads rows [w0, w0 + FWIN) of the tile into the LDS window (whole wave, coalesced).
-__device__ __forceinline__ void fwin_fill(const GridParams& p, const RowDesc* __restrict__ rows, const FastLds& L,
-                                          FWalk& w, int32_t w0) {
-  const int lane = lane_id();
-  WAVE_SYNC();
-  if (w0 + lane < w.rend) {
-    if (w.r0 + w0 + lane >= p.n_rows_total) {   // never expected: report, do not read
-      set_err(p.err, TSDB_E_BOUNDS);
-      return;
-    }
-    // typed copy: the window is read back through RowDesc fields, so it must also be
-    // written as RowDesc (a uint4 store would not alias them under strict aliasing)
-    L.dwin[lane] = rows[w.r0 + w0 + lane];
-  }
-  WAVE_SYNC();
-  w.w0 = w0;
-}
-
-// Descriptor of relative row r from the window (chunks in the ring carry what they need
-// of their row in FMeta, so the window only ever moves forward).
-__device__ __forceinline__ const RowDesc& fwin_row(const GridParams& p, const RowDesc* __restrict__ rows,
-                                                  const FastLds& L, FWalk& w, int32_t r) {
-  if (r >= w.w0 + FWIN) fwin_fill(p, rows, L, w, r);
-  return L.dwin[r - w.w0];
-}
-
-__device__ __forceinline__ void fwalk_load(const GridParams& p, const RowDesc* __restrict__ rows, const FastLds& L,
-                                           FWalk& w) {
-  const RowDesc& x = fwin_row(p, rows, L, w, w.r);
-  // (readfirstlane returns int: go through uint32_t so the low half is not sign-extended)
-  w.d.qoff = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x.qoff >> 32)) << 32) |
-             (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x.qoff);
-  w.d.voff = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x.voff >> 32)) << 32) |
-             (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x.voff);
-  w.d.base = __builtin_amdgcn_readfirstlane(x.base);
-  w.d.ndp = __builtin_amdgcn_readfirstlane(x.ndp);
-  w.d.flags = __builtin_amdgcn_readfirstlane(x.flags);
-}
-
-__device__ __forceinline__ void fwalk_next_row(const GridParams& p, const RowDesc* __restrict__ rows, const FastLds& L,
-                                               FWalk& w) {
+__device__ __forceinline__ void fwalk_next_row(const RowDesc* __restrict__ rows, FWalk& w) {
   w.r++;
   w.c0 = 0;
-  if (w.r < w.rend) fwalk_load(p, rows, L, w);
+  w.d = w.nd;
+  if (w.r + 1 < w.rend) w.nd = fdesc(rows, w.r0 + w.r + 1);
 }
 
 // 0 = chunk issued, 1 = end of tile, 2 = row the kernel cannot take (redo the tile)
 template <int F, int QW, int VL>
-__device__ __forceinline__ int fast_issue(const GridParams& p, const RowDesc* __restrict__ rows, const FastLds& L, FWalk& w,
+__device__ __forceinline__ int fast_issue(const GridParams& p, const RowDesc* __restrict__ rows, FWalk& w,
                                           FRaw<QW, VL>& b, FMeta& m) {
   m.bits = 0;
   for (;;) {
     if (w.r >= w.rend) return 1;
     if (w.c0 == 0) {
       w.sf |= (w.d.flags & ROW_SFIRST) != 0;
-      if ((int64_t)w.d.base < p.ss || (int64_t)w.d.base >= p.se) { fwalk_next_row(p, rows, L, w); continue; }
+      if ((int64_t)w.d.base < p.ss || (int64_t)w.d.base >= p.se) { fwalk_next_row(rows, w); continue; }
       if (!fast_row_ok<QW, VL>(w.d.flags, F == F_MIN || F == F_MAX)) return 2;
       if (VL == 0 && w.d.ndp > CH) return 2;
     }
     if (w.c0 < (int64_t)w.d.ndp) break;
-    fwalk_next_row(p, rows, L, w);
+    fwalk_next_row(rows, w);
   }
   const int lane = lane_id();
   const int nv0 = (int)w.d.ndp - w.c0;
   m.bits = (uint32_t)nv0 | FM_OK | (w.sf ? FM_NEWSER : 0u) | (w.c0 == 0 ? FM_NEWROW : 0u);
-  if (w.c0 == 0) {
-    const RowDesc& x = L.dwin[w.r - w.w0];
-    m.base = w.d.base;
-    m.lsb = __builtin_amdgcn_readfirstlane(x.lsb);
-    m.amax = x.absmax;
-  }
+  m.rrel = w.r;
   w.sf = 0;
-  // the whole chunk window must lie inside the blobs (checked per chunk, wave-uniform)
-  {
-    const uint64_t last = (uint64_t)w.c0 + (uint64_t)min(CH, (nv0 + DPL - 1) / DPL * DPL);
-    const uint64_t qend = w.d.qoff + last * QW;
-    const uint64_t vend = w.d.voff + (VL == 0 ? 1024ull : last * VL);
-    if (qend > p.qual_cap || vend > p.val_cap) {
-      if (lane == 0 && atomicCAS(p.err, 0, TSDB_E_BOUNDS) == 0 && p.bounds_info) {
-        p.bounds_info[0] = (uint64_t)w.r0; p.bounds_info[1] = (uint64_t)w.r; p.bounds_info[2] = (uint64_t)w.w0;
-        p.bounds_info[3] = (uint64_t)w.c0; p.bounds_info[4] = w.d.qoff; p.bounds_info[5] = w.d.voff;
-        p.bounds_info[6] = w.d.ndp; p.bounds_info[7] = w.d.base;
-      }
-      return 2;
-    }
-  }
   // lanes past the end of the row re-read its first datapoints (in bounds, ignored)
   const int64_t i0 = (lane * DPL < nv0) ? w.c0 + (int64_t)lane * DPL : 0;
   const uint4* q = reinterpret_cast<const uint4*>(p.qual + w.d.qoff + i0 * QW);
@@ -1445,12 +1384,8 @@ __device__ __forceinline__ void fast_chunk(const GridParams& p, const FastLds& L
     double sL;
     if (F == F_MIN || F == F_MAX) sL = mL;
     else sL = P - sF;   // exact: every partial sum is representable (certificate)
-    if (!(p.dbg & 2)) {
-      fast_fold<F>(L, sfirst, sF, (uint32_t)cF);
-      if (nL > 0) fast_fold<F>(L, sfirst + 1, sL, (uint32_t)nL);
-    } else if (sF == 1.2345 && nL == 7) {
-      L.cnt[0] = 1;
-    }
+    fast_fold<F>(L, sfirst, sF, (uint32_t)cF);
+    if (nL > 0) fast_fold<F>(L, sfirst + 1, sL, (uint32_t)nL);
   } else {
     // some lane spans more than two buckets or the edge of the slot range: per datapoint
 #pragma unroll
@@ -1497,7 +1432,7 @@ __device__ __forceinline__ bool fast_series_end(const GridParams& p, const FastL
                                    (double)nmax * A * (1.0 + 1e-12) <= ldexp(1.0, 52 + Lb));
     if (!ok) return false;
   }
-  if (!(p.dbg & 1)) emit_series(p, L.w, K);
+  emit_series(p, L.w, K);
   for (int k = lane; k < K; k += 64) {
     L.acc[k] = fast_identity<F>();
     L.cnt[k] = 0;
@@ -1534,8 +1469,8 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
   w.rend = (int32_t)(srp[tend[tile]] - w.r0);
   w.c0 = 0;
   w.sf = 0;
-  w.w0 = -FWIN;
-  if (w.rend > 0) fwalk_load(p, rows, L, w);
+  if (w.rend > 0) w.d = fdesc(rows, w.r0);
+  if (w.rend > 1) w.nd = fdesc(rows, w.r0 + 1);
   WAVE_SYNC();
 
   FRaw<QW, VL> buf[D];
@@ -1543,7 +1478,7 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
   bool redo = false;
 #pragma unroll
   for (int i = 0; i < D; i++) {
-    if (fast_issue<F, QW, VL>(p, rows, L, w, buf[i], meta[i]) == 2) redo = true;
+    if (fast_issue<F, QW, VL>(p, rows, w, buf[i], meta[i]) == 2) redo = true;
   }
   if ((meta[0].bits & FM_OK) && !redo && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
   bool have = false;
@@ -1565,20 +1500,15 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
         }
         if (!done) {
           if (mb & FM_NEWROW) {
-            lsb = min(lsb, meta[i].lsb);
-            amax = fmax(amax, meta[i].amax);
-            g = fgeom(p, meta[i].base);
+            const RowDesc& x = rows[w.r0 + meta[i].rrel];
+            lsb = min(lsb, x.lsb);
+            amax = fmax(amax, x.absmax);
+            g = fgeom(p, x.base);
           }
           const int nv0 = (int)(mb & FM_NV);
-          if (!(p.dbg & 4)) {
-            if (nv0 >= CH) fast_chunk<F, QW, VL, true>(p, L, buf[i], g, nv0, K);
-            else fast_chunk<F, QW, VL, false>(p, L, buf[i], g, nv0, K);
-          } else {
-            // keep the loads live
-            uint32_t x = buf[i].q[0].x ^ buf[i].v[0].y;
-            if (x == 0x12345678u && nv0 == 3) L.cnt[0] = x;
-          }
-          if (fast_issue<F, QW, VL>(p, rows, L, w, buf[i], meta[i]) == 2) { redo = true; done = true; }
+          if (nv0 >= CH) fast_chunk<F, QW, VL, true>(p, L, buf[i], g, nv0, K);
+          else fast_chunk<F, QW, VL, false>(p, L, buf[i], g, nv0, K);
+          if (fast_issue<F, QW, VL>(p, rows, w, buf[i], meta[i]) == 2) { redo = true; done = true; }
         }
       }
     }
