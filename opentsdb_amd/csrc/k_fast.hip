@@ -9,18 +9,25 @@
 
 namespace tsdb {
 
-template <int F, int QW, int VL>
-static hipError_t launch_fast_t(const GridParams& p, hipStream_t s) {
+template <int F, int QW, int VL, bool KR>
+static hipError_t launch_fast_k(const GridParams& p, hipStream_t s) {
   constexpr int D = (QW * 2 + VL * 2 <= 16) ? 3 : 2;   // ring depth: chunk registers per lane
   const int64_t blocks = (p.n_tiles + p.waves - 1) / p.waves;
   const size_t lds = (size_t)p.wave_lds * p.waves;
   if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_fast<F, QW, VL, D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute((const void*)k_fast<F, QW, VL, D, KR>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((k_fast<F, QW, VL, D>), dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p, p.rows,
+  hipLaunchKernelGGL((k_fast<F, QW, VL, D, KR>), dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p, p.rows,
                      p.series_row_ptr, p.tile_begin, p.tile_end);
   return hipGetLastError();
+}
+
+// register partials when every slot has its own lane and the series emit needs no rate pass
+template <int F, int QW, int VL>
+static hipError_t launch_fast_t(const GridParams& p, hipStream_t s) {
+  if (p.K <= 64 && !p.rate) return launch_fast_k<F, QW, VL, true>(p, s);
+  return launch_fast_k<F, QW, VL, false>(p, s);
 }
 
 template <>

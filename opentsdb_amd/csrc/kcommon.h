@@ -233,65 +233,97 @@ __device__ __forceinline__ void part_init(int ga, const LdsPart& P, int k) {
   P.f[k] = 0;
 }
 
+// Slot accessors: the same contribution code updates LDS partials (slot s of a tile
+// array) or register partials (the lane's own slot, K <= 64).
+struct LdsSlot {
+  const LdsPart& P;
+  int s;
+  __device__ double& a() const { return P.a[s]; }
+  __device__ double& b() const { return P.b[s]; }
+  __device__ uint32_t& n() const { return P.n[s]; }
+  __device__ uint32_t& f() const { return P.f[s]; }
+};
+
+struct RegPart {
+  double pa, pb;
+  uint32_t pn, pf;
+  __device__ double& a() { return pa; }
+  __device__ double& b() { return pb; }
+  __device__ uint32_t& n() { return pn; }
+  __device__ uint32_t& f() { return pf; }
+};
+
 // AggregationIterator feeding Aggregator.runDouble, one span at a time in index order.
-__device__ __forceinline__ void contribute(int ga, const LdsPart& P, int s, double v, bool uni) {
-  uint32_t f = P.f[s];
+template <class S>
+__device__ __forceinline__ void contribute_slot(int ga, S&& P, double v, bool uni) {
+  uint32_t f = P.f();
   switch (ga) {
     case GA_SUM: case GA_AVG:
-      if (!isnan(v)) { P.a[s] += v; P.n[s]++; }
+      if (!isnan(v)) { P.a() += v; P.n()++; }
       break;
     case GA_SQUARESUM:
-      if (!isnan(v)) { P.a[s] += v * v; P.n[s]++; }
+      if (!isnan(v)) { P.a() += v * v; P.n()++; }
       break;
     case GA_COUNT:
-      if (!isnan(v)) P.n[s]++;
+      if (!isnan(v)) P.n()++;
       break;
     case GA_MIN:
-      if (!isnan(v) && v < P.a[s]) P.a[s] = v;
+      if (!isnan(v) && v < P.a()) P.a() = v;
       break;
     case GA_MAX:
-      if (!isnan(v) && v > P.a[s]) P.a[s] = v;
+      if (!isnan(v) && v > P.a()) P.a() = v;
       break;
     case GA_DEV:
       if (!isnan(v)) {
-        const uint32_t c = P.n[s];
+        const uint32_t c = P.n();
         if (c == 0) {
-          P.a[s] = v;
+          P.a() = v;
         } else {
-          const double m = P.a[s];
+          const double m = P.a();
           const double nm = m + (v - m) / (double)(c + 1);
-          P.b[s] += (v - m) * (v - nm);
-          P.a[s] = nm;
+          P.b() += (v - m) * (v - nm);
+          P.a() = nm;
         }
-        P.n[s] = c + 1;
+        P.n() = c + 1;
       }
       break;
     case GA_FIRST: case GA_NONE:
-      if (!(f & PF_HAS)) { P.a[s] = v; f |= PF_HAS; }
+      if (!(f & PF_HAS)) { P.a() = v; f |= PF_HAS; }
       f += 4;
       break;
     case GA_LAST:
-      P.a[s] = v;
+      P.a() = v;
       f |= PF_HAS;
       f += 4;
       break;
     case GA_DIFF:
       if (!(f & PF_HAS)) {
-        if (!isnan(v)) { P.a[s] = v; f |= PF_HAS; P.n[s] = 0; }
+        if (!isnan(v)) { P.a() = v; f |= PF_HAS; P.n() = 0; }
       } else {
-        P.n[s]++;
+        P.n()++;
       }
-      P.b[s] = v;
+      P.b() = v;
       f += 4;
       break;
     case GA_MULT:
-      P.a[s] = (f & PF_HAS) ? P.a[s] * v : v;
+      P.a() = (f & PF_HAS) ? P.a() * v : v;
       f |= PF_HAS;
       f += 4;
       break;
   }
   if (uni) f |= PF_UNION;
-  P.f[s] = f;
+  P.f() = f;
+}
+
+__device__ __forceinline__ void contribute(int ga, const LdsPart& P, int s, double v, bool uni) {
+  contribute_slot(ga, LdsSlot{P, s}, v, uni);
+}
+
+__device__ __forceinline__ void regpart_init(int ga, RegPart& P) {
+  P.pa = (ga == GA_MIN) ? INFINITY : (ga == GA_MAX ? -INFINITY : 0.0);
+  P.pb = 0.0;
+  P.pn = 0;
+  P.pf = 0;
 }
 
 // Interpolation of a missing slot (AggregationIterator.nextDoubleValue, :773-793)
@@ -909,6 +941,41 @@ __device__ __forceinline__ void emit_series(const GridParams& p, const WaveLds& 
   WAVE_SYNC();
 }
 
+// emit_series for K <= 64 without rate: lane k owns slot k; the series' bucket k arrives
+// in registers (pr, v) and the tile partial of slot k lives in the lane's registers, so
+// neither the bucket values nor the partials round-trip through LDS.  Same contributions,
+// same per-slot order (one per series) as emit_series.
+__device__ __forceinline__ void emit_series_reg(const GridParams& p, int K, bool pr_in, double v, RegPart& P) {
+  const int lane = lane_id();
+  const bool inK = lane < K;
+  const bool pr = inK && pr_in;
+  if (p.fill != TSDB_FILL_NONE && p.mode == MODE_GRID) {
+    // FillingDownsampler (:172-301): every slot, missing -> NaN / 0 / RuntimeException
+    const double fillv = (p.fill == TSDB_FILL_ZERO) ? 0.0 : (double)NAN;
+    if (inK) {
+      if (!pr && p.fill == TSDB_FILL_SCALAR) set_err(p.err, TSDB_E_RUNTIME);
+      contribute_slot(p.ga, P, pr ? v : fillv, true);
+    }
+    return;
+  }
+  // previous and next present slot of every lane
+  int prv = wave_incl_max(pr ? lane : -1);
+  prv = __shfl_up(prv, 1, 64);
+  if (lane == 0) prv = -1;
+  int nxt = pr ? lane : 64;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_down(nxt, d, 64);
+    if (lane + d < 64) nxt = min(nxt, y);
+  }
+  nxt = __shfl_down(nxt, 1, 64);
+  if (lane == 63) nxt = 64;
+  const double y0 = __shfl(v, max(prv, 0), 64);
+  const double y1 = __shfl(v, min(nxt, 63), 64);
+  if (pr) contribute_slot(p.ga, P, v, true);
+  else if (inK && prv >= 0 && nxt < K) contribute_slot(p.ga, P, interp(p.interp, p, prv, y0, nxt, y1, lane), false);
+}
+
 // Next row of the tile inside the scan range, starting at (s, r) inclusive.
 __device__ __forceinline__ bool seek_row(const GridParams& p, int64_t s_end, int64_t& s, int64_t& r, RowDesc& d) {
   while (s < s_end) {
@@ -1407,6 +1474,47 @@ __device__ __forceinline__ void fast_chunk(const GridParams& p, const FastLds& L
 
 // Series end: buckets -> dense values, certificate, SpanGroup contributions, reset.
 template <int F>
+__device__ __forceinline__ bool fast_cert(uint32_t nmax, int lsb, double amax) {
+  if (!needs_cert<F>()) return true;
+  const int Lb = (F == F_SQUARESUM) ? 2 * lsb : lsb;
+  const double A = (F == F_SQUARESUM) ? amax * amax : amax;
+  return (A == 0.0) || (lsb != INT32_MAX && Lb >= -1022 && !isinf(A) &&
+                        (double)nmax * A * (1.0 + 1e-12) <= ldexp(1.0, 52 + Lb));
+}
+
+template <int F>
+__device__ __forceinline__ double fast_bucket_value(uint32_t c, double a) {
+  if (F == F_SUM || F == F_SQUARESUM) return c ? a : (double)NAN;
+  if (F == F_AVG) return c ? a / (double)(int)c : (double)NAN;
+  if (F == F_COUNT) return (double)c;
+  if (F == F_MIN) return a == INFINITY ? (double)NAN : a;
+  return a == -INFINITY ? (double)NAN : a;
+}
+
+// K <= 64, no rate: the register-partial variant (emit_series_reg).
+template <int F>
+__device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const FastLds& L, int K, int lsb, double amax,
+                                                    RegPart& P) {
+  const int lane = lane_id();
+  WAVE_SYNC();
+  uint32_t c = 0;
+  double a = 0.0;
+  if (lane < K) {
+    c = L.cnt[lane];
+    a = L.acc[lane];
+  }
+  const uint32_t nmax = (uint32_t)wave_max((int)c);
+  if (!fast_cert<F>(nmax, lsb, amax)) return false;
+  emit_series_reg(p, K, c != 0, fast_bucket_value<F>(c, a), P);
+  if (lane < K) {
+    L.acc[lane] = fast_identity<F>();
+    L.cnt[lane] = 0;
+  }
+  WAVE_SYNC();
+  return true;
+}
+
+template <int F>
 __device__ __forceinline__ bool fast_series_end(const GridParams& p, const FastLds& L, int K, int lsb, double amax) {
   const int lane = lane_id();
   WAVE_SYNC();
@@ -1442,7 +1550,7 @@ __device__ __forceinline__ bool fast_series_end(const GridParams& p, const FastL
   return true;
 }
 
-template <int F, int QW, int VL, int D>
+template <int F, int QW, int VL, int D, bool KR>
 __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __restrict__ rows,
                                               const int64_t* __restrict__ srp, const int64_t* __restrict__ tbeg,
                                               const int64_t* __restrict__ tend) {
@@ -1458,11 +1566,13 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
   const int K = (int)p.K;
   const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0);
   for (int k = lane; k < K; k += 64) {
-    part_init(p.ga, L.w.part, k);
+    if (!KR) part_init(p.ga, L.w.part, k);
     L.acc[k] = fast_identity<F>();
     L.cnt[k] = 0;
     L.w.pres[k] = 0;
   }
+  RegPart RP;
+  regpart_init(p.ga, RP);
   FWalk w;
   w.r0 = srp[tbeg[tile]];
   w.r = 0;
@@ -1492,7 +1602,10 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
       if (!done) {
         const uint32_t mb = meta[i].bits;
         if (!(mb & FM_OK) || (mb & FM_NEWSER)) {
-          if (have && !fast_series_end<F>(p, L, K, lsb, amax)) { redo = true; done = true; }
+          if (have) {
+            const bool ok = KR ? fast_series_end_reg<F>(p, L, K, lsb, amax, RP) : fast_series_end<F>(p, L, K, lsb, amax);
+            if (!ok) { redo = true; done = true; }
+          }
           lsb = INT32_MAX;
           amax = 0.0;
           have = true;
@@ -1522,6 +1635,15 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
   double* gb_ = p.part.b + tile * K;
   uint32_t* gn_ = p.part.n + tile * K;
   uint32_t* gf_ = p.part.f + tile * K;
+  if (KR) {
+    if (lane < K) {
+      ga_[lane] = RP.pa;
+      gb_[lane] = RP.pb;
+      gn_[lane] = RP.pn;
+      gf_[lane] = RP.pf;
+    }
+    return;
+  }
   for (int k = lane; k < K; k += 64) {
     ga_[k] = L.w.part.a[k];
     gb_[k] = L.w.part.b[k];

@@ -15,7 +15,7 @@ import numpy as np
 from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libtsdbhip.so")
+LIB_PATH = os.environ.get("TSDBHIP_LIB") or os.path.join(HERE, "lib", "libtsdbhip.so")
 CSRC = os.path.join(HERE, "csrc")
 
 # every symbol include/tsdbhip.h declares
