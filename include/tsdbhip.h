@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define TSDBHIP_ABI_VERSION 2
+#define TSDBHIP_ABI_VERSION 3
 
 /* ---- error codes: one per Java exception on the path --------------------- */
 enum {
@@ -210,6 +210,54 @@ int tsdbhip_run_partials(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_gro
 /* Merges n_ranks rank-ordered partial buffers (device or host memory) and builds the result. */
 int tsdbhip_finalize(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_global,
                      const void* partials, int n_ranks, tsdbhip_result** out);
+/* ---- rollup generation --------------------------------
+ * RollupInterval (src/rollup/RollupInterval.java:62-240): `interval` e.g. "1h", `row_span`
+ * e.g. "1d"; validateAndCompile's checks and arithmetic, IllegalArgumentException ->
+ * TSDB_E_ILLEGAL_ARGUMENT. */
+typedef struct {
+  int32_t interval_s;        /* getIntervalSeconds() */
+  int32_t intervals;         /* getIntervals(): span seconds / interval (12 .. 7774) */
+  char units;                /* getUnits(): row span unit 'h' 'd' 'n' 'y' */
+  char interval_units;       /* getIntervalUnits(): last character of the interval string */
+  int16_t unit_multiplier;   /* getUnitMultiplier(): row span count */
+} tsdbhip_rollup_interval;
+int tsdbhip_rollup_interval_parse(const char* interval, const char* row_span, tsdbhip_rollup_interval* out);
+/* RollupUtils.getRollupBasetime (src/rollup/RollupUtils.java:52-112); timestamp in s or ms. */
+int tsdbhip_rollup_basetime(int64_t timestamp, const tsdbhip_rollup_interval* iv, int32_t* out);
+/* RollupUtils.buildRollupQualifier (src/rollup/RollupUtils.java:143-171): 3 bytes
+ * [aggregator id][BE16((offset_in_intervals << 4) | flags)]. */
+int tsdbhip_rollup_qualifier(int64_t timestamp, int32_t basetime, int16_t flags, int32_t aggregator_id,
+                             const tsdbhip_rollup_interval* iv, uint8_t out[3]);
+
+/* Rollup generation over the resident batch.  The reference ingests rollups
+ * (/api/rollup, src/tsd/RollupDataPointRpc.java:157-165 -> TSDB.addAggregatePoint,
+ * src/core/TSDB.java:1322-1588) but never computes them; the engine computes them as the
+ * Downsampler (fixed interval = the rollup interval, fill none) of every series with each
+ * requested function, and writes each bucket as the cell addAggregatePoint would store:
+ *   qualifier  buildRollupQualifier(bucket start, base, flags, agg_id[i], interval)
+ *   row base   getRollupBasetime(bucket start, interval)
+ *   value      count, and sum/min/max of a series whose every datapoint is an integer:
+ *                vleEncodeLong((long) v)                        (flags = length - 1)
+ *              otherwise a float32 when (float) v == v          (flags 0xB, Tags.fitsInFloat)
+ *              else a float64                                   (flags 0xF)
+ *              NaN / +-Inf -> TSDB_E_ILLEGAL_ARGUMENT (addAggregatePoint rejects them).
+ * Buckets whose start lies in [start_s, end_s) are written.  Cells are ordered by
+ * (function index i, batch series index, time).  Output stays on the device until
+ * tsdbhip_rollup_download. */
+typedef struct {
+  tsdbhip_rollup_interval interval;
+  int64_t start_s, end_s;
+  int32_t n_funcs;           /* 1..4 */
+  int32_t func[4];           /* TSDB_AGG_SUM / COUNT / MAX / MIN (any order) */
+  int32_t agg_id[4];         /* RollupConfig id written in the qualifier (TestTsdbQueryRollup: sum 0, count 1, max 2, min 3) */
+} tsdbhip_rollup_spec;
+int tsdbhip_rollup_run(tsdbhip_ctx* ctx, const tsdbhip_rollup_spec* spec, int64_t* n_cells, uint64_t* value_bytes);
+/* Copies the last rollup_run's cells to caller-allocated host arrays:
+ * series[n_cells] (batch series index), base_time[n_cells], qualifier[3 * n_cells],
+ * val_off[n_cells + 1], value[value_bytes]. */
+int tsdbhip_rollup_download(tsdbhip_ctx* ctx, int32_t* series, uint32_t* base_time, uint8_t* qualifier,
+                            uint64_t* val_off, uint8_t* value);
+
 /* Device synchronisation helper for host code that does not use HIP directly. */
 int tsdbhip_sync(tsdbhip_ctx* ctx);
 

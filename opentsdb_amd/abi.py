@@ -149,6 +149,28 @@ class PartialsLayout(C.Structure):
     ]
 
 
+class RollupInterval(C.Structure):
+    """tsdbhip_rollup_interval (RollupInterval, src/rollup/RollupInterval.java)."""
+    _fields_ = [
+        ("interval_s", C.c_int32),
+        ("intervals", C.c_int32),
+        ("units", C.c_char),
+        ("interval_units", C.c_char),
+        ("unit_multiplier", C.c_int16),
+    ]
+
+
+class RollupSpec(C.Structure):
+    _fields_ = [
+        ("interval", RollupInterval),
+        ("start_s", C.c_int64),
+        ("end_s", C.c_int64),
+        ("n_funcs", C.c_int32),
+        ("func", C.c_int32 * 4),
+        ("agg_id", C.c_int32 * 4),
+    ]
+
+
 def new_query(start_time: int, end_time: int, aggregator: str | int = "sum", *,
               ds_function: int = -1, ds_interval_ms: int = 0, ds_fill: int = FILL_NONE,
               ds_all: bool = False, rate: bool = False, counter: bool = False,

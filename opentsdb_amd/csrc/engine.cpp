@@ -157,6 +157,16 @@ struct tsdbhip_ctx {
   // account() cache (invalidated by every load)
   bool acct_valid = false;
   int64_t acct_ss = 0, acct_se = 0, acct_dps = 0, acct_bytes = 0;
+  // rollup generation: scratch and the per-function cells of the last tsdbhip_rollup_run
+  DevBuf ro_allint, ro_ord, ro_orig, ro_cnt, ro_vsz, ro_coff, ro_voff;
+  void* ro_tmp = nullptr;
+  size_t ro_tmp_bytes = 0;
+  struct RollupOut {
+    DevBuf series, base, qual, voff, val;
+    int64_t cells = 0;
+    uint64_t bytes = 0;
+  } ro_out[4];
+  int ro_n = 0;
 };
 
 // ===========================================================================
@@ -309,8 +319,12 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   for (DevBuf* b : {&c->pa, &c->pb, &c->pn, &c->pf, &c->out_val, &c->out_flag, &c->gact, &c->err, &c->g_dense,
                     &c->g_pres, &c->g_rate, &c->redo, &c->redo_n, &c->redo2, &c->redo2_n, &c->xbuf, &c->gbuf, &c->r_rowpt,
                     &c->r_spoff, &c->r_spn, &c->r_grp, &c->r_pts, &c->r_rank, &c->r_bm, &c->r_wb, &c->r_U, &c->r_ooff,
-                    &c->r_sg, &c->r_su, &c->r_ots, &c->r_obits, &c->r_oint, &c->r_coff, &c->r_cur, &c->pre_dense, &c->pre_pres})
+                    &c->r_sg, &c->r_su, &c->r_ots, &c->r_obits, &c->r_oint, &c->r_coff, &c->r_cur, &c->pre_dense, &c->pre_pres,
+                    &c->ro_allint, &c->ro_ord, &c->ro_orig, &c->ro_cnt, &c->ro_vsz, &c->ro_coff, &c->ro_voff})
     b->release();
+  for (auto& o : c->ro_out)
+    for (DevBuf* b : {&o.series, &o.base, &o.qual, &o.voff, &o.val}) b->release();
+  if (c->ro_tmp) (void)hipFree(c->ro_tmp);
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1413,4 +1427,235 @@ extern "C" int tsdbhip_finalize(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t 
   mp.err = c->err.as<int32_t>();
   HIP_OK(launch_rank_merge(mp, c->stream));
   return collect(c, q, P, G, false, out);
+}
+
+// ===========================================================================
+// rollup codec and generation
+// ===========================================================================
+namespace {
+
+RollupIv to_iv(const tsdbhip_rollup_interval* iv) {
+  RollupIv r;
+  r.interval_s = iv->interval_s;
+  r.intervals = iv->intervals;
+  r.units = iv->units;
+  r.mult = iv->unit_multiplier;
+  return r;
+}
+
+bool iv_valid(const tsdbhip_rollup_interval* iv) {
+  return iv && iv->interval_s >= 1 && iv->intervals >= 1 &&
+         (iv->units == 'h' || iv->units == 'd' || iv->units == 'n' || iv->units == 'y');
+}
+
+}  // namespace
+
+// new RollupInterval(builder) + validateAndCompile (src/rollup/RollupInterval.java:62-103,169-235),
+// with DateTime.getDurationUnits / getDurationInterval (src/utils/DateTime.java:237-284).
+extern "C" int tsdbhip_rollup_interval_parse(const char* interval, const char* row_span, tsdbhip_rollup_interval* out) {
+  if (!out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "out is null");
+  if (!row_span || !*row_span) return fail(TSDB_E_ILLEGAL_ARGUMENT, "Duration cannot be null or empty");
+  size_t u = 0;
+  const size_t n = std::strlen(row_span);
+  while (u < n && std::isdigit((unsigned char)row_span[u])) u++;
+  std::string units(row_span + u);
+  for (auto& ch : units) ch = (char)std::tolower((unsigned char)ch);
+  static const char* const ok[] = {"ms", "s", "m", "h", "d", "w", "n", "y"};
+  bool valid = false;
+  for (const char* o : ok) valid |= units == o;
+  if (!valid) return fail(TSDB_E_ILLEGAL_ARGUMENT, "Invalid units in the duration: " + units);
+  if (units.size() > 1) return fail(TSDB_E_ILLEGAL_ARGUMENT, "Milliseconds are not supported");
+  if (std::strchr(row_span, '.')) return fail(TSDB_E_ILLEGAL_ARGUMENT, "Floating point intervals are not supported");
+  if (u == 0 || u > 10) return fail(TSDB_E_ILLEGAL_ARGUMENT, std::string("Invalid duration (number): ") + row_span);
+  const long long mult_ll = std::stoll(std::string(row_span, u));
+  if (mult_ll > 2147483647LL) return fail(TSDB_E_ILLEGAL_ARGUMENT, std::string("Invalid duration (number): ") + row_span);
+  const int32_t mult = (int32_t)mult_ll;
+  if (mult <= 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, std::string("Zero or negative duration: ") + row_span);
+  const char un = units[0];
+  if (un != 'h' && mult > 1) return fail(TSDB_E_ILLEGAL_ARGUMENT, "Multipliers are only usable with the 'h' unit");
+  if (un == 'h' && mult > 1 && mult % 2 != 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "The multiplier must be 1 or an even value");
+  if (!interval) return fail(TSDB_E_ILLEGAL_ARGUMENT, "interval is null");
+  int64_t ms = 0;
+  int rc = tsdbhip_parse_duration(interval, &ms);
+  if (rc) return rc;
+  const int32_t iv_s = (int32_t)(uint32_t)(uint64_t)(ms / 1000);   // Java (int) of a long
+  if (iv_s < 1) return fail(TSDB_E_ILLEGAL_ARGUMENT, "Millisecond intervals are not supported");
+  if (iv_s >= 2147483647) return fail(TSDB_E_ILLEGAL_ARGUMENT, "Interval is too big");
+  int32_t num_span;
+  switch (un) {
+    case 'h': num_span = 3600; break;
+    case 'd': num_span = 86400; break;
+    case 'n': num_span = 86400 * 32; break;
+    case 'y': num_span = 86400 * 366; break;
+    default: return fail(TSDB_E_ILLEGAL_ARGUMENT, std::string("Unrecogznied span '") + un + "'");
+  }
+  num_span = (int32_t)((uint32_t)num_span * (uint32_t)mult);
+  if (iv_s >= num_span) return fail(TSDB_E_ILLEGAL_ARGUMENT, "Interval is too large for the span");
+  const int32_t intervals = num_span / iv_s;
+  if (intervals > 7774) return fail(TSDB_E_ILLEGAL_ARGUMENT, "Too many intervals in the span");
+  if (intervals < 12) return fail(TSDB_E_ILLEGAL_ARGUMENT, "Not enough intervals for the span");
+  out->interval_s = iv_s;
+  out->intervals = intervals;
+  out->units = un;
+  out->interval_units = interval[std::strlen(interval) - 1];
+  out->unit_multiplier = (int16_t)std::min<int32_t>(mult, 32767);
+  return 0;
+}
+
+extern "C" int tsdbhip_rollup_basetime(int64_t timestamp, const tsdbhip_rollup_interval* iv, int32_t* out) {
+  if (!iv || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  if (!rc_basetime(timestamp, to_iv(iv), *out))
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, "Not supporting negative timestamps / unrecognised span");
+  return 0;
+}
+
+extern "C" int tsdbhip_rollup_qualifier(int64_t timestamp, int32_t basetime, int16_t flags, int32_t aggregator_id,
+                                        const tsdbhip_rollup_interval* iv, uint8_t out[3]) {
+  if (!iv || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  if (iv->interval_s < 1) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad interval");
+  if (!rc_qualifier(timestamp, basetime, flags, aggregator_id, to_iv(iv), out))
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, "Offset was greater than the configured intervals");
+  return 0;
+}
+
+extern "C" int tsdbhip_rollup_run(tsdbhip_ctx* c, const tsdbhip_rollup_spec* sp, int64_t* n_cells, uint64_t* value_bytes) {
+  if (!c || !sp) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  if (!iv_valid(&sp->interval)) return fail(TSDB_E_ILLEGAL_ARGUMENT, "invalid rollup interval");
+  if (sp->n_funcs < 1 || sp->n_funcs > 4) return fail(TSDB_E_ILLEGAL_ARGUMENT, "1..4 rollup functions");
+  if (sp->start_s < 0 || sp->end_s <= sp->start_s) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad rollup time range");
+  for (int i = 0; i < sp->n_funcs; i++) {
+    const int f = sp->func[i];
+    if (f != TSDB_AGG_SUM && f != TSDB_AGG_COUNT && f != TSDB_AGG_MAX && f != TSDB_AGG_MIN)
+      return fail(TSDB_E_ILLEGAL_ARGUMENT, "rollup functions are sum, count, max and min");
+  }
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  c->ro_n = 0;
+  const int64_t n = c->n_series;
+  // batch order -> sorted position, and the per-series integer flag
+  {
+    std::vector<int64_t> ord(n);
+    std::iota(ord.begin(), ord.end(), 0);
+    std::sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return c->h_orig[a] < c->h_orig[b]; });
+    HIP_OK(c->ro_ord.ensure(std::max<int64_t>(1, n) * 8));
+    HIP_OK(c->ro_orig.ensure(std::max<int64_t>(1, n) * 8));
+    HIP_OK(c->ro_allint.ensure(std::max<int64_t>(1, n)));
+    if (n) {
+      HIP_OK(hipMemcpyAsync(c->ro_ord.p, ord.data(), n * 8, hipMemcpyHostToDevice, c->stream));
+      HIP_OK(hipMemcpyAsync(c->ro_orig.p, c->h_orig.data(), n * 8, hipMemcpyHostToDevice, c->stream));
+    }
+    HIP_OK(launch_series_allint(c->rows.as<RowDesc>(), c->srp.as<int64_t>(), n, c->ro_allint.as<uint8_t>(), c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));   // `ord` leaves scope
+  }
+  for (int fi = 0; fi < sp->n_funcs; fi++) {
+    // Downsampler of every series (NONE aggregator: one SpanGroup per span), fill none
+    tsdbhip_query q{};
+    q.start_time = sp->start_s;
+    q.end_time = sp->end_s - 1;
+    q.aggregator = TSDB_AGG_NONE;
+    q.ds_function = sp->func[fi];
+    q.ds_fill = TSDB_FILL_NONE;
+    q.ds_interval_ms = (int64_t)sp->interval.interval_s * 1000;
+    q.rate_counter_max = INT64_MAX;
+    Plan P;
+    int rc = plan_query(c, &q, P);
+    if (rc) return rc;
+    rc = run_device(c, &q, P, n, true);
+    if (rc) return rc;
+    const int64_t NK = n * P.K;
+    HIP_OK(c->ro_cnt.ensure(std::max<int64_t>(1, NK) * 4));
+    HIP_OK(c->ro_vsz.ensure(std::max<int64_t>(1, NK) * 4));
+    HIP_OK(c->ro_coff.ensure(std::max<int64_t>(1, NK) * 8));
+    HIP_OK(c->ro_voff.ensure(std::max<int64_t>(1, NK) * 8));
+    RollupParams rp{};
+    rp.val = c->out_val.as<double>();
+    rp.flag = c->out_flag.as<uint8_t>();
+    rp.ord = c->ro_ord.as<int64_t>();
+    rp.orig = c->ro_orig.as<int64_t>();
+    rp.allint = c->ro_allint.as<uint8_t>();
+    rp.n = NK;
+    rp.K = P.K;
+    rp.B0 = P.B0;
+    rp.I = P.I;
+    rp.start_ms = sp->start_s * 1000;
+    rp.end_ms = sp->end_s * 1000;
+    rp.iv = to_iv(&sp->interval);
+    rp.agg_id = sp->agg_id[fi];
+    rp.as_long_all = sp->func[fi] == TSDB_AGG_COUNT;
+    rp.cnt = c->ro_cnt.as<uint32_t>();
+    rp.vsz = c->ro_vsz.as<uint32_t>();
+    rp.coff = c->ro_coff.as<int64_t>();
+    rp.voff = c->ro_voff.as<uint64_t>();
+    rp.err = c->err.as<int32_t>();
+    HIP_OK(launch_rollup_size(rp, c->stream));
+    if (NK > 0x7FFFFFFFLL) return fail(TSDB_E_NOT_IMPLEMENTED, "more than 2^31 rollup buckets in one pass");
+    if (NK) HIP_OK(rollup_scan(rp.cnt, c->ro_coff.as<int64_t>(), rp.vsz, c->ro_voff.as<uint64_t>(), NK, &c->ro_tmp,
+                               &c->ro_tmp_bytes, c->stream));
+    // totals = last offset + last element
+    int64_t last_off = 0;
+    uint64_t last_voff = 0;
+    uint32_t last_c = 0, last_v = 0;
+    int32_t err = 0;
+    if (NK) {
+      HIP_OK(hipMemcpyAsync(&last_off, c->ro_coff.as<int64_t>() + NK - 1, 8, hipMemcpyDeviceToHost, c->stream));
+      HIP_OK(hipMemcpyAsync(&last_voff, c->ro_voff.as<uint64_t>() + NK - 1, 8, hipMemcpyDeviceToHost, c->stream));
+      HIP_OK(hipMemcpyAsync(&last_c, rp.cnt + NK - 1, 4, hipMemcpyDeviceToHost, c->stream));
+      HIP_OK(hipMemcpyAsync(&last_v, rp.vsz + NK - 1, 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    // an infinite bucket value trips AggregationIterator's Inf check (IllegalStateException)
+    // in the NONE-aggregator pass; for a rollup it is addAggregatePoint's rejection
+    if (err == TSDB_E_ILLEGAL_STATE) err = TSDB_E_ILLEGAL_ARGUMENT;
+    if (err) return fail(err, "rollup generation: value or offset rejected (addAggregatePoint / buildRollupQualifier)");
+    auto& o = c->ro_out[fi];
+    o.cells = last_off + last_c;
+    o.bytes = last_voff + last_v;
+    HIP_OK(o.series.ensure(std::max<int64_t>(1, o.cells) * 4));
+    HIP_OK(o.base.ensure(std::max<int64_t>(1, o.cells) * 4));
+    HIP_OK(o.qual.ensure(std::max<int64_t>(1, o.cells) * 3));
+    HIP_OK(o.voff.ensure((o.cells + 1) * 8));
+    HIP_OK(o.val.ensure(std::max<uint64_t>(1, o.bytes)));
+    rp.o_series = o.series.as<int32_t>();
+    rp.o_base = o.base.as<uint32_t>();
+    rp.o_qual = o.qual.as<uint8_t>();
+    rp.o_voff = o.voff.as<uint64_t>();
+    rp.o_val = o.val.as<uint8_t>();
+    HIP_OK(launch_rollup_write(rp, c->stream));
+    HIP_OK(hipMemcpyAsync(o.voff.as<uint64_t>() + o.cells, &o.bytes, 8, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    c->ro_n = fi + 1;
+  }
+  int64_t cells = 0;
+  uint64_t bytes = 0;
+  for (int i = 0; i < c->ro_n; i++) { cells += c->ro_out[i].cells; bytes += c->ro_out[i].bytes; }
+  if (n_cells) *n_cells = cells;
+  if (value_bytes) *value_bytes = bytes;
+  return 0;
+}
+
+extern "C" int tsdbhip_rollup_download(tsdbhip_ctx* c, int32_t* series, uint32_t* base_time, uint8_t* qualifier,
+                                       uint64_t* val_off, uint8_t* value) {
+  if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  int64_t cell0 = 0;
+  uint64_t byte0 = 0;
+  for (int i = 0; i < c->ro_n; i++) {
+    const auto& o = c->ro_out[i];
+    if (o.cells) {
+      if (series) HIP_OK(hipMemcpy(series + cell0, o.series.p, o.cells * 4, hipMemcpyDeviceToHost));
+      if (base_time) HIP_OK(hipMemcpy(base_time + cell0, o.base.p, o.cells * 4, hipMemcpyDeviceToHost));
+      if (qualifier) HIP_OK(hipMemcpy(qualifier + 3 * cell0, o.qual.p, o.cells * 3, hipMemcpyDeviceToHost));
+      if (val_off) {
+        HIP_OK(hipMemcpy(val_off + cell0, o.voff.p, o.cells * 8, hipMemcpyDeviceToHost));
+        for (int64_t k = 0; k < o.cells; k++) val_off[cell0 + k] += byte0;
+      }
+      if (value && o.bytes) HIP_OK(hipMemcpy(value + byte0, o.val.p, o.bytes, hipMemcpyDeviceToHost));
+    }
+    cell0 += o.cells;
+    byte0 += o.bytes;
+  }
+  if (val_off) val_off[cell0] = byte0;
+  return 0;
 }

@@ -2,6 +2,8 @@
 // gfx950 kernels (kernels.hip) of libtsdbhip.  Not part of the public ABI.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include "rollup_codec.h"
 #include <stdint.h>
 
 namespace tsdb {
@@ -205,6 +207,34 @@ struct SynthParams {
   uint32_t* row_vbytes;          // pass 1 output (value bytes incl. meta)
   int32_t* group_id;             // [n_series] (batch order)
 };
+
+// rollup generation (k_rollup.hip); grid = n series (batch order) x K slots
+struct RollupParams {
+  const double* val;        // [G][K] downsampled bucket values (sorted series positions)
+  const uint8_t* flag;      // [G][K] bucket present
+  const int64_t* ord;       // [n series] sorted position of the i-th series in batch order
+  const int64_t* orig;      // [G] batch index of sorted position
+  const uint8_t* allint;    // [G] every datapoint of the series is an integer
+  int64_t n, K, B0, I, start_ms, end_ms;
+  RollupIv iv;
+  int32_t agg_id;
+  int32_t as_long_all;      // count: every value is a long
+  uint32_t* cnt;            // [n] cell flag      -> coff
+  uint32_t* vsz;            // [n] value length   -> voff
+  const int64_t* coff;
+  const uint64_t* voff;
+  int32_t* o_series;
+  uint32_t* o_base;
+  uint8_t* o_qual;
+  uint64_t* o_voff;
+  uint8_t* o_val;
+  int32_t* err;
+};
+hipError_t launch_series_allint(const RowDesc* rows, const int64_t* srp, int64_t n, uint8_t* allint, hipStream_t s);
+hipError_t launch_rollup_size(const RollupParams& p, hipStream_t s);
+hipError_t launch_rollup_write(const RollupParams& p, hipStream_t s);
+hipError_t rollup_scan(const uint32_t* cnt, int64_t* coff, const uint32_t* vsz, uint64_t* voff, int64_t n,
+                       void** tmp, size_t* tmp_bytes, hipStream_t s);
 
 // launchers (kernels.hip)
 hipError_t launch_index(const uint8_t* qual, const uint8_t* val, RowDesc* rows, int64_t n_rows, int32_t* err,

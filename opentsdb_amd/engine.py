@@ -24,7 +24,8 @@ EXPORTS = [
     "tsdbhip_parse_duration", "tsdbhip_parse_downsample", "tsdbhip_scan_bounds", "tsdbhip_init",
     "tsdbhip_destroy", "tsdbhip_load", "tsdbhip_synth", "tsdbhip_batch_sizes", "tsdbhip_batch_download",
     "tsdbhip_run", "tsdbhip_result_free", "tsdbhip_last_timing", "tsdbhip_partials_layout_get",
-    "tsdbhip_run_partials", "tsdbhip_finalize", "tsdbhip_sync",
+    "tsdbhip_run_partials", "tsdbhip_finalize", "tsdbhip_sync", "tsdbhip_rollup_interval_parse",
+    "tsdbhip_rollup_basetime", "tsdbhip_rollup_qualifier", "tsdbhip_rollup_run", "tsdbhip_rollup_download",
 ]
 
 
@@ -72,6 +73,12 @@ def lib():
         L.tsdbhip_finalize.argtypes = [vp, C.POINTER(abi.Query), C.c_int64, C.c_void_p, C.c_int,
                                        C.POINTER(C.POINTER(abi.Result))]
         L.tsdbhip_sync.argtypes = [vp]
+        L.tsdbhip_rollup_interval_parse.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(abi.RollupInterval)]
+        L.tsdbhip_rollup_basetime.argtypes = [C.c_int64, C.POINTER(abi.RollupInterval), C.POINTER(C.c_int32)]
+        L.tsdbhip_rollup_qualifier.argtypes = [C.c_int64, C.c_int32, C.c_int16, C.c_int32,
+                                               C.POINTER(abi.RollupInterval), C.c_void_p]
+        L.tsdbhip_rollup_run.argtypes = [vp, C.POINTER(abi.RollupSpec), C.POINTER(C.c_int64), C.POINTER(C.c_uint64)]
+        L.tsdbhip_rollup_download.argtypes = [vp] + [C.c_void_p] * 5
         _lib = L
     return _lib
 
@@ -92,6 +99,46 @@ def scan_bounds(q: abi.Query):
     s, e = C.c_int64(), C.c_int64()
     _check(lib().tsdbhip_scan_bounds(C.byref(q), C.byref(s), C.byref(e)))
     return s.value, e.value
+
+
+def rollup_interval(interval: str, row_span: str) -> abi.RollupInterval:
+    """RollupInterval.builder().setInterval(interval).setRowSpan(row_span).build()."""
+    iv = abi.RollupInterval()
+    _check(lib().tsdbhip_rollup_interval_parse(interval.encode(), row_span.encode(), C.byref(iv)))
+    return iv
+
+
+def rollup_basetime(timestamp: int, iv: abi.RollupInterval) -> int:
+    """RollupUtils.getRollupBasetime."""
+    out = C.c_int32()
+    _check(lib().tsdbhip_rollup_basetime(timestamp, C.byref(iv), C.byref(out)))
+    return out.value
+
+
+def rollup_qualifier(timestamp: int, basetime: int, flags: int, aggregator_id: int, iv: abi.RollupInterval) -> bytes:
+    """RollupUtils.buildRollupQualifier."""
+    out = (C.c_uint8 * 3)()
+    _check(lib().tsdbhip_rollup_qualifier(timestamp, basetime, flags, aggregator_id, C.byref(iv), out))
+    return bytes(out)
+
+
+class RollupCells:
+    """Cells of one rollup generation, in (function, series, time) order."""
+
+    def __init__(self, series, base_time, qualifier, val_off, value):
+        self.series = series          # int32 [n] batch series index
+        self.base_time = base_time    # uint32 [n] row base time (s)
+        self.qualifier = qualifier    # uint8 [n, 3]
+        self.val_off = val_off        # uint64 [n + 1]
+        self.value = value            # uint8 [val_off[-1]]
+
+    def __len__(self):
+        return len(self.series)
+
+    def cell(self, i):
+        """(series, base_time, qualifier bytes, value bytes) of cell i."""
+        return (int(self.series[i]), int(self.base_time[i]), bytes(self.qualifier[i]),
+                bytes(self.value[self.val_off[i]:self.val_off[i + 1]]))
 
 
 class _ResultOwner:
@@ -169,6 +216,37 @@ class Engine:
 
     def sync(self):
         _check(lib().tsdbhip_sync(self.ctx))
+
+    # ---- rollup generation (tsdbhip_rollup_run) ----
+    def rollup_run(self, interval: abi.RollupInterval, start_s: int, end_s: int,
+                   funcs=(("sum", 0), ("count", 1), ("max", 2), ("min", 3))):
+        """Generates the rollup cells of the resident batch on the device; returns
+        (n_cells, value_bytes).  funcs = [(downsample function, rollup aggregator id)]."""
+        sp = abi.RollupSpec()
+        sp.interval = interval
+        sp.start_s = start_s
+        sp.end_s = end_s
+        sp.n_funcs = len(funcs)
+        for i, (fn, aid) in enumerate(funcs):
+            sp.func[i] = abi.AGG[fn] if isinstance(fn, str) else fn
+            sp.agg_id[i] = aid
+        n, b = C.c_int64(), C.c_uint64()
+        _check(lib().tsdbhip_rollup_run(self.ctx, C.byref(sp), C.byref(n), C.byref(b)))
+        return n.value, b.value
+
+    def rollup_download(self, n_cells: int, value_bytes: int) -> RollupCells:
+        series = np.zeros(max(1, n_cells), np.int32)
+        base = np.zeros(max(1, n_cells), np.uint32)
+        qual = np.zeros((max(1, n_cells), 3), np.uint8)
+        voff = np.zeros(n_cells + 1, np.uint64)
+        val = np.zeros(max(1, value_bytes), np.uint8)
+        _check(lib().tsdbhip_rollup_download(self.ctx, series.ctypes.data, base.ctypes.data, qual.ctypes.data,
+                                             voff.ctypes.data, val.ctypes.data))
+        return RollupCells(series[:n_cells], base[:n_cells], qual[:n_cells], voff, val[:value_bytes])
+
+    def rollup(self, interval: abi.RollupInterval, start_s: int, end_s: int,
+               funcs=(("sum", 0), ("count", 1), ("max", 2), ("min", 3))) -> RollupCells:
+        return self.rollup_download(*self.rollup_run(interval, start_s, end_s, funcs))
 
     # ---- multi-GPU exchange (see include/tsdbhip.h and opentsdb_amd/dist.py) ----
     def partials_layout(self, q: abi.Query, n_groups_global: int) -> abi.PartialsLayout:
