@@ -151,6 +151,7 @@ struct tsdbhip_ctx {
   // dominant uniform row class of the batch (k_fast specialisation), 0 = none
   int fast_qw = 0, fast_vl = 0;        // dominant k_fast row class (0 = none)
   int fast_qw2 = 0, fast_vl2 = 0;      // second class, chained over the first one's redo list
+  int64_t short_tiles = 0;             // tiles whose series have exactly one row each (k_short)
   bool fast_used = false;
   const int32_t* redo_final = nullptr;   // device counter of the tiles left for k_grid
   tsdbhip_timing timing{};
@@ -359,6 +360,9 @@ static int build_tiles(tsdbhip_ctx* c) {
   }
   c->gtp[c->n_groups] = (int64_t)c->tb.size();
   const size_t nt = c->tb.size();
+  c->short_tiles = 0;
+  for (size_t t = 0; t < nt; t++)
+    if (c->h_srp[c->te[t]] - c->h_srp[c->tb[t]] == c->te[t] - c->tb[t]) c->short_tiles++;
   HIP_OK(c->d_tb.ensure(nt * 8));
   HIP_OK(c->d_te.ensure(nt * 8));
   HIP_OK(c->d_tg.ensure(nt * 4));
@@ -835,31 +839,42 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   c->fast_used = fast;
   HIP_OK(hipEventRecord(c->ev[0], c->stream));
   if (fast) {
-    // class 1 over every tile, class 2 over the tiles class 1 handed back; k_grid takes the rest
-    const int cq[2] = {c->fast_qw, c->fast_qw2}, cv[2] = {c->fast_vl, c->fast_vl2};
+    // class 1 over every tile, class 2 over the tiles class 1 handed back; k_grid takes the rest.
+    // Batches of one-row series (short windows) go through k_short first, per class.
+    struct Pass { int qw, vl, shortk; };
+    std::vector<Pass> passes;
+    const char* senv = std::getenv("TSDBHIP_SHORT");
+    const bool use_short = !(senv && senv[0] == '0') && !none && c->short_tiles * 2 >= nt;
+    for (int sh = use_short ? 1 : 0; sh >= 0; sh--) {
+      passes.push_back({c->fast_qw, c->fast_vl, sh});
+      passes.push_back({c->fast_qw2, c->fast_vl2, sh});
+    }
     DevBuf* lists[2] = {&c->redo, &c->redo2};
     DevBuf* counts[2] = {&c->redo_n, &c->redo2_n};
     const int32_t* in_list = nullptr;
     const int32_t* in_n = nullptr;
-    for (int k = 0; k < 2; k++) {
-      if (!cq[k] || !fast_supported(P.f, cq[k], cv[k])) continue;
+    int slot = 0;
+    for (const Pass& ps : passes) {
+      if (!ps.qw || !fast_supported(P.f, ps.qw, ps.vl)) continue;
       GridParams fp = gp;
-      fp.unit_s = (cq[k] == 2 && P.I % 1000 == 0 && P.B0 % 1000 == 0) ? 1 : 0;
+      fp.shortk = ps.shortk;
+      fp.unit_s = (ps.qw == 2 && P.I % 1000 == 0 && P.B0 % 1000 == 0) ? 1 : 0;
       fp.In = (int32_t)(fp.unit_s ? P.I / 1000 : P.I);
       fp.B0n = fp.unit_s ? P.B0 / 1000 : P.B0;
       fp.rcpn = std::nextafter(1.0 / (double)fp.In, INFINITY);
       fp.wave_lds = (int32_t)fast_wave_lds(K, q->rate != 0);
       fp.waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / fp.wave_lds));
-      HIP_OK(lists[k]->ensure(std::max<int64_t>(1, nt) * 4));
-      HIP_OK(counts[k]->ensure(16));
-      HIP_OK(hipMemsetAsync(counts[k]->p, 0, 4, c->stream));
+      HIP_OK(lists[slot]->ensure(std::max<int64_t>(1, nt) * 4));
+      HIP_OK(counts[slot]->ensure(16));
+      HIP_OK(hipMemsetAsync(counts[slot]->p, 0, 4, c->stream));
       fp.tile_list = in_list;
       fp.tile_list_n = in_n;
-      fp.redo_list = lists[k]->as<int32_t>();
-      fp.redo_n = counts[k]->as<int32_t>();
-      HIP_OK(launch_fast(fp, P.f, cq[k], cv[k], c->stream));
+      fp.redo_list = lists[slot]->as<int32_t>();
+      fp.redo_n = counts[slot]->as<int32_t>();
+      HIP_OK(launch_fast(fp, P.f, ps.qw, ps.vl, c->stream));
       in_list = fp.redo_list;
       in_n = fp.redo_n;
+      slot ^= 1;
     }
     HIP_OK(hipEventRecord(c->ev[3], c->stream));
     gp.tile_list = in_list;

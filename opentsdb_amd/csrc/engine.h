@@ -113,6 +113,7 @@ struct GridParams {
   int64_t n_series;
   double* pre_dense;     // [n_series][K]
   uint8_t* pre_pres;     // [n_series][K]
+  int32_t shortk;        // k_fast launch runs k_short (one row per series, descriptors up front)
   int32_t dbg;           // profiling switches (TSDBHIP_DBG): 1 skip emit, 2 skip fold, 4 skip chunk
 };
 

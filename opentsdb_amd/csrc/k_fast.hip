@@ -14,6 +14,16 @@ static hipError_t launch_fast_k(const GridParams& p, hipStream_t s) {
   constexpr int D = (QW * 2 + VL * 2 <= 16) ? 3 : 2;   // ring depth: chunk registers per lane
   const int64_t blocks = (p.n_tiles + p.waves - 1) / p.waves;
   const size_t lds = (size_t)p.wave_lds * p.waves;
+  if (p.shortk) {
+    constexpr int DS = (QW * 2 + VL * 2 <= 16) ? 4 : 2;
+    if (lds > 65536) {
+      hipError_t e = hipFuncSetAttribute((const void*)k_short<F, QW, VL, DS, KR>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((k_short<F, QW, VL, DS, KR>), dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p, p.rows,
+                       p.series_row_ptr, p.tile_begin, p.tile_end);
+    return hipGetLastError();
+  }
   if (lds > 65536) {
     hipError_t e = hipFuncSetAttribute((const void*)k_fast<F, QW, VL, D, KR>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;

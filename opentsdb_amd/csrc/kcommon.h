@@ -1652,6 +1652,132 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
   }
 }
 
+// ---- k_short: tiles whose series have exactly one row each (short windows) --------------
+// config 3 (10M series x 1 h @10 s) is one 360-point row per series: k_fast's per-row walker
+// (scalar descriptor chain, chunk metadata) costs as much as the decode there.  Here lane i
+// loads the descriptor of the tile's series i up front, so every chunk address is known and
+// the D-deep load ring runs across series with no walker.  Same chunk fold and series end
+// as k_fast (bit-identical partials); a tile that breaks a premise goes to the redo list.
+template <int QW, int VL>
+__device__ __forceinline__ void short_issue(const GridParams& p, uint64_t qoff, uint64_t voff, int ndp,
+                                            FRaw<QW, VL>& b) {
+  const int lane = lane_id();
+  const int64_t i0 = (lane * DPL < ndp) ? (int64_t)lane * DPL : 0;
+  const uint4* q = reinterpret_cast<const uint4*>(p.qual + qoff + i0 * QW);
+#pragma unroll
+  for (int k = 0; k < QW / 2; k++) b.q[k] = q[k];
+  if (VL == 0) {
+    b.v[0] = *reinterpret_cast<const uint4*>(p.val + voff + (int64_t)lane * 16);
+  } else {
+    const uint4* v = reinterpret_cast<const uint4*>(p.val + voff + i0 * VL);
+#pragma unroll
+    for (int k = 0; k < VL / 2; k++) b.v[k] = v[k];
+  }
+}
+
+__device__ __forceinline__ uint64_t rl64(uint64_t x, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+template <int F, int QW, int VL, int D, bool KR>
+__global__ __launch_bounds__(256) void k_short(GridParams p, const RowDesc* __restrict__ rows,
+                                               const int64_t* __restrict__ srp, const int64_t* __restrict__ tbeg,
+                                               const int64_t* __restrict__ tend) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int64_t tile = (int64_t)blockIdx.x * p.waves + wave;
+  if (p.tile_list) {
+    if (tile >= (int64_t)*p.tile_list_n) return;
+    tile = p.tile_list[tile];
+  }
+  if (tile >= p.n_tiles) return;
+  const int K = (int)p.K;
+  const int64_t s0 = tbeg[tile];
+  const int ns = (int)(tend[tile] - s0);
+  const int64_t r0 = srp[s0];
+  // premise: one row per series, in the scan range, of this kernel's class, one chunk long
+  bool ok = ns <= 64 && srp[s0 + ns] - r0 == ns;
+  uint64_t dq = 0, dv = 0, damax = 0;
+  int dbase = 0, dndp = 0, dlsb = INT32_MAX;
+  if (ok && lane < ns) {
+    const RowDesc& x = rows[r0 + lane];
+    dq = x.qoff;
+    dv = x.voff;
+    dbase = (int)x.base;
+    dndp = (int)x.ndp;
+    dlsb = x.lsb;
+    damax = (uint64_t)__double_as_longlong(x.absmax);
+    const uint32_t fl = x.flags;
+    ok = (int64_t)x.base >= p.ss && (int64_t)x.base < p.se && dndp >= 1 && dndp <= CH &&
+         fast_row_ok<QW, VL>(fl, F == F_MIN || F == F_MAX);
+  }
+  if (!__all(ok)) {
+    if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
+    return;
+  }
+  const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0);
+  for (int k = lane; k < K; k += 64) {
+    if (!KR) part_init(p.ga, L.w.part, k);
+    L.acc[k] = fast_identity<F>();
+    L.cnt[k] = 0;
+    L.w.pres[k] = 0;
+  }
+  RegPart RP;
+  regpart_init(p.ga, RP);
+  if (ns > 0 && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
+  WAVE_SYNC();
+  FRaw<QW, VL> buf[D];
+#pragma unroll
+  for (int i = 0; i < D; i++)
+    if (i < ns) short_issue<QW, VL>(p, rl64(dq, i), rl64(dv, i), __builtin_amdgcn_readlane(dndp, i), buf[i]);
+  bool redo = false;
+  for (int jb = 0; jb < ns && !redo; jb += D) {
+#pragma unroll
+    for (int i = 0; i < D; i++) {
+      const int j = jb + i;
+      if (j < ns && !redo) {
+        const int nv0 = __builtin_amdgcn_readlane(dndp, j);
+        const FGeom g = fgeom(p, (uint32_t)__builtin_amdgcn_readlane(dbase, j));
+        if (nv0 >= CH) fast_chunk<F, QW, VL, true>(p, L, buf[i], g, nv0, K);
+        else fast_chunk<F, QW, VL, false>(p, L, buf[i], g, nv0, K);
+        if (j + D < ns)
+          short_issue<QW, VL>(p, rl64(dq, j + D), rl64(dv, j + D), __builtin_amdgcn_readlane(dndp, j + D), buf[i]);
+        const int lsb = __builtin_amdgcn_readlane(dlsb, j);
+        const double amax = __longlong_as_double((long long)rl64(damax, j));
+        const bool fine = KR ? fast_series_end_reg<F>(p, L, K, lsb, amax, RP) : fast_series_end<F>(p, L, K, lsb, amax);
+        if (!fine) redo = true;
+      }
+    }
+  }
+  if (redo) {
+    if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
+    return;
+  }
+  WAVE_SYNC();
+  double* ga_ = p.part.a + tile * K;
+  double* gb_ = p.part.b + tile * K;
+  uint32_t* gn_ = p.part.n + tile * K;
+  uint32_t* gf_ = p.part.f + tile * K;
+  if (KR) {
+    if (lane < K) {
+      ga_[lane] = RP.pa;
+      gb_[lane] = RP.pb;
+      gn_[lane] = RP.pn;
+      gf_[lane] = RP.pf;
+    }
+    return;
+  }
+  for (int k = lane; k < K; k += 64) {
+    ga_[k] = L.w.part.a[k];
+    gb_[k] = L.w.part.b[k];
+    gn_[k] = L.w.part.n[k];
+    gf_[k] = L.w.part.f[k];
+  }
+}
+
 // ---- k_reduce -------------------------------------------------------------------
 struct PState {
   double a, b;

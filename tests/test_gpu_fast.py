@@ -235,3 +235,49 @@ def test_fast_multi_row_series_window_refill(eng):
     gen, tg = run_path(eng, None, q, False)
     assert tf.redo_tiles == 0 and tf.fast_ms > 0
     assert_bit_equal(fast, gen, "24 rows per series")
+
+
+def run_short(eng, batch, q, short: bool):
+    old = os.environ.get("TSDBHIP_SHORT")
+    os.environ["TSDBHIP_SHORT"] = "1" if short else "0"
+    try:
+        return run_path(eng, batch, q, True)
+    finally:
+        if old is None:
+            del os.environ["TSDBHIP_SHORT"]
+        else:
+            os.environ["TSDBHIP_SHORT"] = old
+
+
+@pytest.mark.parametrize("agg,ds", [("sum", "avg"), ("avg", "sum"), ("dev", "avg"), ("min", "max"), ("max", "min"),
+                                    ("count", "count"), ("sum", "squareSum")])
+def test_short_kernel_matches_walker(eng, agg, ds):
+    """k_short (one row per series, descriptors up front) against k_fast's row walker and
+    k_grid, bit for bit, on the config 3 shape."""
+    eng.synth(40000, T0, 360, 10000, 2, 1000, 30000, 0x5EED)
+    q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG[ds], ds_interval_ms=60000)
+    s, ts = run_short(eng, None, q, True)
+    w, tw = run_short(eng, None, q, False)
+    g, tg = run_path(eng, None, q, False)
+    assert ts.redo_tiles == 0 and ts.fast_ms > 0
+    assert_bit_equal(s, w, f"short vs walker {agg}:{ds}")
+    assert_bit_equal(s, g, f"short vs general {agg}:{ds}")
+
+
+def test_short_kernel_mixed_row_counts(eng):
+    """Tiles mixing one-row and two-row series, and rows outside the scan range: k_short
+    hands those tiles to k_fast; results identical to the general kernel and the oracle."""
+    rng = np.random.default_rng(3)
+    series, gids = [], []
+    for s in range(300):
+        start = T0 + (1800 if s % 7 == 0 else 0) + (7200 if s % 11 == 0 else 0)
+        ts = (start + np.arange(360) * 10) * 1000
+        fv = np.round(rng.normal(50, 5, 360), 3)
+        series.append(synth.encode_rows(ts, None, fv, np.ones(360, int), np.zeros(360, bool)))
+        gids.append(s % 3)
+    b = synth.from_series(series, gids)
+    q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+    s, ts = run_short(eng, b, q, True)
+    g, tg = run_path(eng, b, q, False)
+    assert_bit_equal(s, g, "mixed row counts")
+    assert_groups_match(s, O.run_query(b, q), "sum", ctx="mixed row counts vs oracle")
