@@ -151,9 +151,15 @@ struct tsdbhip_ctx {
   // dominant uniform row class of the batch (k_fast specialisation), 0 = none
   int fast_qw = 0, fast_vl = 0;        // dominant k_fast row class (0 = none)
   int fast_qw2 = 0, fast_vl2 = 0;      // second class, chained over the first one's redo list
-  int64_t short_tiles = 0;             // tiles whose series have exactly one row each (k_short)
+  // tile lists by k_fast row class (built at load): [class A / class B][walker / short],
+  // and the tiles of neither class (general kernel only).  Short = one row per series of at
+  // most CH datapoints (k_short).
+  std::vector<int32_t> tl[2][2], tl_other;
+  DevBuf d_tl, d_tl_n, r1a, r1b, r2, r_n;   // device copies; k_short / k_fast redo lists
+  int64_t tl_off[5] = {};
   bool fast_used = false;
-  const int32_t* redo_final = nullptr;   // device counter of the tiles left for k_grid
+  const int32_t* redo_final = nullptr;   // device counter of the tiles k_fast handed to k_grid
+  int64_t redo_other = 0;                // + tiles of neither row class (k_grid only)
   tsdbhip_timing timing{};
   // account() cache (invalidated by every load)
   bool acct_valid = false;
@@ -318,7 +324,7 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   release_batch(c);
   for (DevBuf* b : {&c->pa, &c->pb, &c->pn, &c->pf, &c->out_val, &c->out_flag, &c->gact, &c->err, &c->g_dense,
-                    &c->g_pres, &c->g_rate, &c->redo, &c->redo_n, &c->redo2, &c->redo2_n, &c->xbuf, &c->gbuf, &c->r_rowpt,
+                    &c->g_pres, &c->g_rate, &c->redo, &c->redo_n, &c->redo2, &c->redo2_n, &c->d_tl, &c->d_tl_n, &c->r1a, &c->r1b, &c->r2, &c->r_n, &c->xbuf, &c->gbuf, &c->r_rowpt,
                     &c->r_spoff, &c->r_spn, &c->r_grp, &c->r_pts, &c->r_rank, &c->r_bm, &c->r_wb, &c->r_U, &c->r_ooff,
                     &c->r_sg, &c->r_su, &c->r_ots, &c->r_obits, &c->r_oint, &c->r_coff, &c->r_cur, &c->pre_dense, &c->pre_pres,
                     &c->ro_allint, &c->ro_ord, &c->ro_orig, &c->ro_cnt, &c->ro_vsz, &c->ro_coff, &c->ro_voff})
@@ -360,9 +366,43 @@ static int build_tiles(tsdbhip_ctx* c) {
   }
   c->gtp[c->n_groups] = (int64_t)c->tb.size();
   const size_t nt = c->tb.size();
-  c->short_tiles = 0;
-  for (size_t t = 0; t < nt; t++)
-    if (c->h_srp[c->te[t]] - c->h_srp[c->tb[t]] == c->te[t] - c->tb[t]) c->short_tiles++;
+  // per-tile k_fast class: every row of the tile in class A (or B); the kernels re-check
+  for (auto& a : c->tl) for (auto& b : a) b.clear();
+  c->tl_other.clear();
+  auto row_class = [&](int64_t r, int qw, int vl) {
+    const uint32_t f = c->h_flags[r];
+    if (!qw) return false;
+    if ((f & ROW_QW_MASK) != (uint32_t)qw || (f & (ROW_ERR | ROW_UNSORTED))) return false;
+    if (vl == 0) return (f & ROW_ALLI) && (f & ROW_VLE2) && c->h_ndp[r] <= (uint32_t)CH_ROWS;
+    return ((f & ROW_VL_MASK) >> ROW_VL_SHIFT) == (uint32_t)vl && (f & ROW_ALLF) && !(f & ROW_NAN);
+  };
+  for (size_t t = 0; t < nt; t++) {
+    const int64_t r0 = c->h_srp[c->tb[t]], r1 = c->h_srp[c->te[t]];
+    int cls = -1;
+    for (int k = 0; k < 2 && cls < 0; k++) {
+      const int qw = k ? c->fast_qw2 : c->fast_qw, vl = k ? c->fast_vl2 : c->fast_vl;
+      bool all = r1 > r0;
+      for (int64_t r = r0; r < r1 && all; r++) all = row_class(r, qw, vl);
+      if (all) cls = k;
+    }
+    if (cls < 0) { c->tl_other.push_back((int32_t)t); continue; }
+    bool shrt = r1 - r0 == c->te[t] - c->tb[t];
+    for (int64_t r = r0; r < r1 && shrt; r++) shrt = c->h_ndp[r] <= (uint32_t)CH_ROWS;
+    c->tl[cls][shrt ? 1 : 0].push_back((int32_t)t);
+  }
+  {
+    std::vector<int32_t> all, cnt;
+    const std::vector<int32_t>* parts[5] = {&c->tl[0][0], &c->tl[0][1], &c->tl[1][0], &c->tl[1][1], &c->tl_other};
+    for (int i = 0; i < 5; i++) {
+      c->tl_off[i] = (int64_t)all.size();
+      all.insert(all.end(), parts[i]->begin(), parts[i]->end());
+      cnt.push_back((int32_t)parts[i]->size());
+    }
+    HIP_OK(c->d_tl.ensure(std::max<size_t>(1, all.size()) * 4));
+    HIP_OK(c->d_tl_n.ensure(5 * 4));
+    if (!all.empty()) HIP_OK(hipMemcpy(c->d_tl.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(c->d_tl_n.p, cnt.data(), 5 * 4, hipMemcpyHostToDevice));
+  }
   HIP_OK(c->d_tb.ensure(nt * 8));
   HIP_OK(c->d_te.ensure(nt * 8));
   HIP_OK(c->d_tg.ensure(nt * 4));
@@ -839,49 +879,100 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   c->fast_used = fast;
   HIP_OK(hipEventRecord(c->ev[0], c->stream));
   if (fast) {
-    // class 1 over every tile, class 2 over the tiles class 1 handed back; k_grid takes the rest.
-    // Batches of one-row series (short windows) go through k_short first, per class.
-    struct Pass { int qw, vl, shortk; };
-    std::vector<Pass> passes;
+    // Per row class (A, B): k_short over its one-row-series tiles, k_fast over its other
+    // tiles and over what k_short handed back; k_grid over what k_fast handed back and over
+    // the tiles of neither class.  Lists by class are built at load (no per-tile appends
+    // for class mismatches); only tiles that break a premise at run time are appended.
     const char* senv = std::getenv("TSDBHIP_SHORT");
-    const bool use_short = !(senv && senv[0] == '0') && !none && c->short_tiles * 2 >= nt;
-    for (int sh = use_short ? 1 : 0; sh >= 0; sh--) {
-      passes.push_back({c->fast_qw, c->fast_vl, sh});
-      passes.push_back({c->fast_qw2, c->fast_vl2, sh});
-    }
-    DevBuf* lists[2] = {&c->redo, &c->redo2};
-    DevBuf* counts[2] = {&c->redo_n, &c->redo2_n};
-    const int32_t* in_list = nullptr;
-    const int32_t* in_n = nullptr;
-    int slot = 0;
-    for (const Pass& ps : passes) {
-      if (!ps.qw || !fast_supported(P.f, ps.qw, ps.vl)) continue;
+    const bool use_short = !(senv && senv[0] == '0');
+    const int32_t* dl = c->d_tl.as<int32_t>();
+    const int32_t* dn = c->d_tl_n.as<int32_t>();
+    HIP_OK(c->r1a.ensure(std::max<int64_t>(1, nt) * 4));
+    HIP_OK(c->r1b.ensure(std::max<int64_t>(1, nt) * 4));
+    HIP_OK(c->r2.ensure(std::max<int64_t>(1, nt) * 4));
+    HIP_OK(c->r_n.ensure(16));
+    HIP_OK(hipMemsetAsync(c->r_n.p, 0, 16, c->stream));
+    int32_t* rn = c->r_n.as<int32_t>();   // [0] r1a, [1] r1b, [2] r2
+    auto fast_launch = [&](int cls, int shortk, const int32_t* list, const int32_t* list_n, int64_t cap,
+                           int32_t* out, int32_t* out_n) -> int {
+      const int qw = cls ? c->fast_qw2 : c->fast_qw, vl = cls ? c->fast_vl2 : c->fast_vl;
+      if (cap == 0 || !qw || !fast_supported(P.f, qw, vl)) return 1;   // not run: caller routes the list on
       GridParams fp = gp;
-      fp.shortk = ps.shortk;
-      fp.unit_s = (ps.qw == 2 && P.I % 1000 == 0 && P.B0 % 1000 == 0) ? 1 : 0;
+      fp.shortk = shortk;
+      fp.unit_s = (qw == 2 && P.I % 1000 == 0 && P.B0 % 1000 == 0) ? 1 : 0;
       fp.In = (int32_t)(fp.unit_s ? P.I / 1000 : P.I);
       fp.B0n = fp.unit_s ? P.B0 / 1000 : P.B0;
       fp.rcpn = std::nextafter(1.0 / (double)fp.In, INFINITY);
       fp.wave_lds = (int32_t)fast_wave_lds(K, q->rate != 0);
       fp.waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / fp.wave_lds));
-      HIP_OK(lists[slot]->ensure(std::max<int64_t>(1, nt) * 4));
-      HIP_OK(counts[slot]->ensure(16));
-      HIP_OK(hipMemsetAsync(counts[slot]->p, 0, 4, c->stream));
-      fp.tile_list = in_list;
-      fp.tile_list_n = in_n;
-      fp.redo_list = lists[slot]->as<int32_t>();
-      fp.redo_n = counts[slot]->as<int32_t>();
-      HIP_OK(launch_fast(fp, P.f, ps.qw, ps.vl, c->stream));
-      in_list = fp.redo_list;
-      in_n = fp.redo_n;
-      slot ^= 1;
+      fp.tile_list = list;
+      fp.tile_list_n = list_n;
+      fp.n_launch = cap;
+      fp.redo_list = out;
+      fp.redo_n = out_n;
+      hipError_t e = launch_fast(fp, P.f, qw, vl, c->stream);
+      if (e != hipSuccess) return fail(TSDB_E_HIP, std::string("launch_fast: ") + hipGetErrorString(e));
+      return 0;
+    };
+    // lists that no fast kernel takes go to k_grid: collect them
+    std::vector<std::pair<const int32_t*, std::pair<const int32_t*, int64_t>>> to_grid;
+    int32_t* r1[2] = {c->r1a.as<int32_t>(), c->r1b.as<int32_t>()};
+    int64_t routed = 0;   // tiles of host lists sent straight to k_grid
+    if (none) {
+      // NONE aggregator: one tile per series (not the group tiles the lists index) --
+      // class A over every tile, class B over what A handed back
+      int rc = fast_launch(0, 0, nullptr, nullptr, nt, r1[0], rn + 0);
+      if (rc < 0) return rc;
+      const bool a = rc == 0;
+      rc = fast_launch(1, 0, a ? r1[0] : nullptr, a ? rn + 0 : nullptr, nt, c->r2.as<int32_t>(), rn + 2);
+      if (rc < 0) return rc;
+      if (rc == 1) {
+        if (a) to_grid.push_back({r1[0], {rn + 0, nt}});
+        else return fail(TSDB_E_HIP, "no fast class ran");   // unreachable: `fast` needs one
+      }
     }
+    for (int cls = 0; cls < 2 && !none; cls++) {
+      const int64_t n0 = (int64_t)c->tl[cls][0].size(), n1 = (int64_t)c->tl[cls][1].size();
+      const int32_t* l0 = dl + c->tl_off[2 * cls];
+      const int32_t* l1 = dl + c->tl_off[2 * cls + 1];
+      int rc;
+      if (use_short && n1) {
+        rc = fast_launch(cls, 1, l1, dn + 2 * cls + 1, n1, r1[cls], rn + cls);
+        if (rc < 0) return rc;
+        if (rc == 0) {
+          rc = fast_launch(cls, 0, r1[cls], rn + cls, n1, c->r2.as<int32_t>(), rn + 2);
+          if (rc < 0) return rc;
+          if (rc == 1) to_grid.push_back({r1[cls], {rn + cls, n1}});
+        } else {
+          to_grid.push_back({l1, {dn + 2 * cls + 1, n1}});
+          routed += n1;
+        }
+      } else if (n1) {
+        rc = fast_launch(cls, 0, l1, dn + 2 * cls + 1, n1, c->r2.as<int32_t>(), rn + 2);
+        if (rc < 0) return rc;
+        if (rc == 1) { to_grid.push_back({l1, {dn + 2 * cls + 1, n1}}); routed += n1; }
+      }
+      if (n0) {
+        rc = fast_launch(cls, 0, l0, dn + 2 * cls, n0, c->r2.as<int32_t>(), rn + 2);
+        if (rc < 0) return rc;
+        if (rc == 1) { to_grid.push_back({l0, {dn + 2 * cls, n0}}); routed += n0; }
+      }
+    }
+    to_grid.push_back({c->r2.as<int32_t>(), {rn + 2, nt}});
+    if (!none && !c->tl_other.empty()) to_grid.push_back({dl + c->tl_off[4], {dn + 4, (int64_t)c->tl_other.size()}});
     HIP_OK(hipEventRecord(c->ev[3], c->stream));
-    gp.tile_list = in_list;
-    gp.tile_list_n = in_n;
-    c->redo_final = in_n;
+    for (auto& tg : to_grid) {
+      GridParams g2 = gp;
+      g2.tile_list = tg.first;
+      g2.tile_list_n = tg.second.first;
+      g2.n_launch = tg.second.second;
+      HIP_OK(launch_grid(g2, P.f, c->stream));
+    }
+    c->redo_final = rn + 2;
+    c->redo_other = none ? 0 : (int64_t)c->tl_other.size() + routed;
+  } else {
+    HIP_OK(launch_grid(gp, P.f, c->stream));
   }
-  HIP_OK(launch_grid(gp, P.f, c->stream));
   HIP_OK(hipEventRecord(c->ev[1], c->stream));
   }
   if (do_reduce) {
@@ -1005,7 +1096,7 @@ void record_timing(tsdbhip_ctx* c, const Plan& P, int32_t redo_n) {
   c->timing.total_ms = t01 + t12;
   c->timing.fast_ms = t03;
   c->timing.tiles = P.none ? c->n_series : (int64_t)c->tb.size();
-  c->timing.redo_tiles = c->fast_used ? redo_n : c->timing.tiles;
+  c->timing.redo_tiles = c->fast_used ? redo_n + c->redo_other : c->timing.tiles;
   account(c, P);
 }
 

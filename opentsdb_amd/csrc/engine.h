@@ -8,6 +8,8 @@
 
 namespace tsdb {
 
+static constexpr int CH_ROWS = 512;   // k_fast chunk: datapoints per chunk (64 lanes x 8), = CH in kcommon.h
+
 // One compacted cell (RowSeq) as laid out in HBM.  qoff/voff are 16-byte aligned.
 struct RowDesc {
   uint64_t qoff;    // byte offset of the qualifiers in the qualifier blob
@@ -74,6 +76,7 @@ struct GridParams {
   const int64_t* tile_end;
   const int32_t* tile_group;
   int64_t n_tiles;
+  int64_t n_launch;      // waves launched (list launches: the list's capacity); 0 = n_tiles
   // query geometry (ms unless noted)
   int64_t ss, se;        // scan bounds, seconds: rows with base in [ss, se)
   int64_t B0;            // timestamp of slot 0

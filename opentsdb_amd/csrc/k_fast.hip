@@ -7,15 +7,23 @@
 #error "compile with -DF_ID=<downsample function class>"
 #endif
 
+#ifndef SHORT_D0
+#define SHORT_D0 2     // k_short ring depth, vle class
+#endif
+#ifndef SHORT_D
+#define SHORT_D 2      // k_short ring depth, 4-byte float class
+#endif
+
 namespace tsdb {
 
 template <int F, int QW, int VL, bool KR>
 static hipError_t launch_fast_k(const GridParams& p, hipStream_t s) {
   constexpr int D = (QW * 2 + VL * 2 <= 16) ? 3 : 2;   // ring depth: chunk registers per lane
-  const int64_t blocks = (p.n_tiles + p.waves - 1) / p.waves;
+  const int64_t nl = p.n_launch > 0 ? p.n_launch : p.n_tiles;
+  const int64_t blocks = (nl + p.waves - 1) / p.waves;
   const size_t lds = (size_t)p.wave_lds * p.waves;
   if (p.shortk) {
-    constexpr int DS = (QW * 2 + VL * 2 <= 16) ? 4 : 2;
+    constexpr int DS = VL == 0 ? SHORT_D0 : (QW * 2 + VL * 2 <= 16) ? SHORT_D : 2;
     if (lds > 65536) {
       hipError_t e = hipFuncSetAttribute((const void*)k_short<F, QW, VL, DS, KR>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) return e;

@@ -10,7 +10,8 @@ namespace tsdb {
 
 template <int F, bool G>
 static hipError_t launch_grid_t(const GridParams& p, hipStream_t s) {
-  const int64_t blocks = (p.n_tiles + p.waves - 1) / p.waves;
+  const int64_t nl = p.n_launch > 0 ? p.n_launch : p.n_tiles;
+  const int64_t blocks = (nl + p.waves - 1) / p.waves;
   const size_t lds = (size_t)p.wave_lds * p.waves;
   if (lds > 65536) {
     hipError_t e = hipFuncSetAttribute((const void*)k_grid<F, G>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -33,7 +33,7 @@ namespace tsdb {
     __builtin_amdgcn_wave_barrier();                         \
   } while (0)
 
-static constexpr int CH = 512;          // datapoints per chunk (64 lanes x 8)
+static constexpr int CH = CH_ROWS;      // datapoints per chunk (64 lanes x 8)
 static constexpr int DPL = 8;           // datapoints per lane
 static constexpr int VBUF = 4224;       // value staging bytes (aliases the decoded-double area)
 
@@ -42,6 +42,19 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ void set_err(int32_t* err, int code) { atomicCAS(err, 0, code); }
 
 // ---- wave scans (64 lanes) ------------------------------------------------
+// ballot-based (no LDS round trip): lanes below this one in a 64-bit lane mask
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+// exclusive prefix sum of small non-negative values (< 2^B), bit-sliced over ballots
+template <int B>
+__device__ __forceinline__ int wave_excl_sum_small(int x) {
+  int r = 0;
+#pragma unroll
+  for (int b = 0; b < B; b++) r += lanes_below(__ballot((x >> b) & 1)) << b;
+  return r;
+}
+
 __device__ __forceinline__ int wave_incl_sum(int x) {
   const int l = lane_id();
 #pragma unroll
@@ -958,20 +971,22 @@ __device__ __forceinline__ void emit_series_reg(const GridParams& p, int K, bool
     }
     return;
   }
-  // previous and next present slot of every lane
-  int prv = wave_incl_max(pr ? lane : -1);
-  prv = __shfl_up(prv, 1, 64);
-  if (lane == 0) prv = -1;
-  int nxt = pr ? lane : 64;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_down(nxt, d, 64);
-    if (lane + d < 64) nxt = min(nxt, y);
+  // previous and next present slot of every lane, from the presence ballot
+  const uint64_t pm = __ballot(pr);
+  if (pm == (K >= 64 ? ~0ull : ((1ull << K) - 1))) {   // every slot present: no interpolation
+    if (inK) contribute_slot(p.ga, P, v, true);
+    return;
   }
-  nxt = __shfl_down(nxt, 1, 64);
-  if (lane == 63) nxt = 64;
-  const double y0 = __shfl(v, max(prv, 0), 64);
-  const double y1 = __shfl(v, min(nxt, 63), 64);
+  const uint64_t below = pm & ((1ull << lane) - 1);
+  const uint64_t above = lane == 63 ? 0ull : (pm & ~((2ull << lane) - 1));
+  const int prv = below ? 63 - __clzll((long long)below) : -1;
+  const int nxt = above ? __ffsll((long long)above) - 1 : 64;
+  const bool need = inK && !pr && prv >= 0 && nxt < K;
+  double y0 = 0.0, y1 = 0.0;
+  if (__ballot(need)) {
+    y0 = __shfl(v, max(prv, 0), 64);
+    y1 = __shfl(v, min(nxt, 63), 64);
+  }
   if (pr) contribute_slot(p.ga, P, v, true);
   else if (inK && prv >= 0 && nxt < K) contribute_slot(p.ga, P, interp(p.interp, p, prv, y0, nxt, y1, lane), false);
 }
@@ -1360,8 +1375,7 @@ __device__ __forceinline__ void f_values_vle(const FastLds& L, const FRaw<QW, VL
     len[j] = (j < nvl) ? (int)(f_flags<QW, VL>(b, j) & 7) + 1 : 0;
     tot += len[j];
   }
-  const int incl = wave_incl_sum(tot);
-  int o = incl - tot;
+  int o = wave_excl_sum_small<5>(tot);   // tot <= 16
   WAVE_SYNC();
   reinterpret_cast<uint4*>(L.vstage)[lane] = b.v[0];
   WAVE_SYNC();
@@ -1494,7 +1508,7 @@ __device__ __forceinline__ double fast_bucket_value(uint32_t c, double a) {
 // K <= 64, no rate: the register-partial variant (emit_series_reg).
 template <int F>
 __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const FastLds& L, int K, int lsb, double amax,
-                                                    RegPart& P) {
+                                                    RegPart& P, uint32_t nbound = 0) {
   const int lane = lane_id();
   WAVE_SYNC();
   uint32_t c = 0;
@@ -1503,8 +1517,12 @@ __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const F
     c = L.cnt[lane];
     a = L.acc[lane];
   }
-  const uint32_t nmax = (uint32_t)wave_max((int)c);
-  if (!fast_cert<F>(nmax, lsb, amax)) return false;
+  // certificate: the series' datapoint count bounds every bucket count (nbound), else the
+  // bucket maximum
+  if (!(nbound && fast_cert<F>(nbound, lsb, amax))) {
+    const uint32_t nmax = (uint32_t)wave_max((int)c);
+    if (!fast_cert<F>(nmax, lsb, amax)) return false;
+  }
   emit_series_reg(p, K, c != 0, fast_bucket_value<F>(c, a), P);
   if (lane < K) {
     L.acc[lane] = fast_identity<F>();
@@ -1729,26 +1747,53 @@ __global__ __launch_bounds__(256) void k_short(GridParams p, const RowDesc* __re
   regpart_init(p.ga, RP);
   if (ns > 0 && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
   WAVE_SYNC();
+  // The ring issues unconditionally (series index clamped to the last one) so that the
+  // compiler's vmcnt bookkeeping stays exact: a conditional issue makes it wait for every
+  // outstanding load (vmcnt(0)) and the ring degenerates to one series in flight.
   FRaw<QW, VL> buf[D];
+  const int nlast = ns - 1;
 #pragma unroll
-  for (int i = 0; i < D; i++)
-    if (i < ns) short_issue<QW, VL>(p, rl64(dq, i), rl64(dv, i), __builtin_amdgcn_readlane(dndp, i), buf[i]);
+  for (int i = 0; i < D; i++) {
+    const int jn = min(i, nlast);
+    short_issue<QW, VL>(p, rl64(dq, jn), rl64(dv, jn), __builtin_amdgcn_readlane(dndp, jn), buf[i]);
+  }
   bool redo = false;
-  for (int jb = 0; jb < ns && !redo; jb += D) {
+  auto series = [&](const FRaw<QW, VL>& b, int j) {
+    const int nv0 = __builtin_amdgcn_readlane(dndp, j);
+    const FGeom g = fgeom(p, (uint32_t)__builtin_amdgcn_readlane(dbase, j));
+    if (!(p.dbg & 2)) {   // TSDBHIP_DBG profiling switches (results invalid when set)
+      fast_chunk<F, QW, VL, false>(p, L, b, g, nv0, K);   // one variant: code size matters here
+    } else if (p.dbg & 8) {
+      uint32_t x = b.q[0].x ^ b.v[0].x;
+      if (x == 0x12345678u) L.cnt[0] = x;
+    }
+    return nv0;
+  };
+  auto series_end = [&](int j, int nv0) {
+    if (p.dbg & 1) return;
+    const int lsb = __builtin_amdgcn_readlane(dlsb, j);
+    const double amax = __longlong_as_double((long long)rl64(damax, j));
+    const bool fine =
+        KR ? fast_series_end_reg<F>(p, L, K, lsb, amax, RP, (uint32_t)nv0) : fast_series_end<F>(p, L, K, lsb, amax);
+    if (!fine) redo = true;
+  };
+  int j = 0;
+  for (; j + D <= ns; j += D) {
 #pragma unroll
     for (int i = 0; i < D; i++) {
-      const int j = jb + i;
-      if (j < ns && !redo) {
-        const int nv0 = __builtin_amdgcn_readlane(dndp, j);
-        const FGeom g = fgeom(p, (uint32_t)__builtin_amdgcn_readlane(dbase, j));
-        if (nv0 >= CH) fast_chunk<F, QW, VL, true>(p, L, buf[i], g, nv0, K);
-        else fast_chunk<F, QW, VL, false>(p, L, buf[i], g, nv0, K);
-        if (j + D < ns)
-          short_issue<QW, VL>(p, rl64(dq, j + D), rl64(dv, j + D), __builtin_amdgcn_readlane(dndp, j + D), buf[i]);
-        const int lsb = __builtin_amdgcn_readlane(dlsb, j);
-        const double amax = __longlong_as_double((long long)rl64(damax, j));
-        const bool fine = KR ? fast_series_end_reg<F>(p, L, K, lsb, amax, RP) : fast_series_end<F>(p, L, K, lsb, amax);
-        if (!fine) redo = true;
+      const int nv0 = series(buf[i], j + i);
+      const int jn = min(j + i + D, nlast);
+      short_issue<QW, VL>(p, rl64(dq, jn), rl64(dv, jn), __builtin_amdgcn_readlane(dndp, jn), buf[i]);
+      series_end(j + i, nv0);
+    }
+    if (redo) break;
+  }
+  if (!redo) {
+#pragma unroll
+    for (int i = 0; i < D; i++) {
+      if (j + i < ns) {
+        const int nv0 = series(buf[i], j + i);
+        series_end(j + i, nv0);
       }
     }
   }
