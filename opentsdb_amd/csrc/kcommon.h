@@ -1441,7 +1441,9 @@ __device__ __forceinline__ void fast_chunk(const GridParams& p, const FastLds& L
     if (nvl == 0) return;
     // first run: offsets below the next bucket boundary
     const int Dn = (sfirst - m.q0 + 1) * p.In - m.r0;   // > 0
-    const uint32_t Tf = (uint32_t)((Dn + uq - 1) / uq);
+    uint32_t Tf;
+    if (uq == 1) Tf = (uint32_t)Dn;                      // uniform branch: no runtime integer division
+    else Tf = (uint32_t)((Dn + 999) / 1000);
     double P = fast_identity<F>(), sF = 0.0, mL = fast_identity<F>();
     int cF = 0;
 #pragma unroll
@@ -1483,6 +1485,19 @@ __device__ __forceinline__ void fast_chunk(const GridParams& p, const FastLds& L
         }
       }
     }
+  }
+}
+
+// A chunk of a row shorter than CH: when every lane is either full or empty (a row of a
+// multiple of 8 datapoints, e.g. 360), the full-lane code runs on the non-empty lanes.
+template <int F, int QW, int VL>
+__device__ __forceinline__ void fast_chunk_any(const GridParams& p, const FastLds& L, const FRaw<QW, VL>& b,
+                                               const FGeom& m, int nv0, int K) {
+  const int nvl = max(0, min(DPL, nv0 - lane_id() * DPL));
+  if (__all(nvl == 0 || nvl == DPL)) {
+    if (nvl) fast_chunk<F, QW, VL, true>(p, L, b, m, nv0, K);
+  } else {
+    fast_chunk<F, QW, VL, false>(p, L, b, m, nv0, K);
   }
 }
 
@@ -1680,6 +1695,7 @@ template <int QW, int VL>
 __device__ __forceinline__ void short_issue(const GridParams& p, uint64_t qoff, uint64_t voff, int ndp,
                                             FRaw<QW, VL>& b) {
   const int lane = lane_id();
+  if (p.dbg & 32) { qoff = 0; voff = 0; }
   const int64_t i0 = (lane * DPL < ndp) ? (int64_t)lane * DPL : 0;
   const uint4* q = reinterpret_cast<const uint4*>(p.qual + qoff + i0 * QW);
 #pragma unroll
@@ -1699,8 +1715,11 @@ __device__ __forceinline__ uint64_t rl64(uint64_t x, int l) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+#ifndef SHORT_OCC
+#define SHORT_OCC 6   // waves per SIMD k_short is compiled for (VGPR budget)
+#endif
 template <int F, int QW, int VL, int D, bool KR>
-__global__ __launch_bounds__(256) void k_short(GridParams p, const RowDesc* __restrict__ rows,
+__global__ __launch_bounds__(256, SHORT_OCC) void k_short(GridParams p, const RowDesc* __restrict__ rows,
                                                const int64_t* __restrict__ srp, const int64_t* __restrict__ tbeg,
                                                const int64_t* __restrict__ tend) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1736,6 +1755,14 @@ __global__ __launch_bounds__(256) void k_short(GridParams p, const RowDesc* __re
     if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
     return;
   }
+  if (p.dbg & 16) return;
+  // bucket geometry of every series' row, computed once per tile (lane = series)
+  int gq0, gr0;
+  {
+    const FGeom g = fgeom(p, (uint32_t)dbase);
+    gq0 = g.q0;
+    gr0 = g.r0;
+  }
   const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0);
   for (int k = lane; k < K; k += 64) {
     if (!KR) part_init(p.ga, L.w.part, k);
@@ -1760,9 +1787,9 @@ __global__ __launch_bounds__(256) void k_short(GridParams p, const RowDesc* __re
   bool redo = false;
   auto series = [&](const FRaw<QW, VL>& b, int j) {
     const int nv0 = __builtin_amdgcn_readlane(dndp, j);
-    const FGeom g = fgeom(p, (uint32_t)__builtin_amdgcn_readlane(dbase, j));
+    const FGeom g = {__builtin_amdgcn_readlane(gq0, j), __builtin_amdgcn_readlane(gr0, j)};
     if (!(p.dbg & 2)) {   // TSDBHIP_DBG profiling switches (results invalid when set)
-      fast_chunk<F, QW, VL, false>(p, L, b, g, nv0, K);   // one variant: code size matters here
+      fast_chunk_any<F, QW, VL>(p, L, b, g, nv0, K);
     } else if (p.dbg & 8) {
       uint32_t x = b.q[0].x ^ b.v[0].x;
       if (x == 0x12345678u) L.cnt[0] = x;
