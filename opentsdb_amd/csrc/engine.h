@@ -117,7 +117,8 @@ struct GridParams {
   double* pre_dense;     // [n_series][K]
   uint8_t* pre_pres;     // [n_series][K]
   int32_t shortk;        // k_fast launch runs k_short (one row per series, descriptors up front)
-  int32_t dbg;           // profiling switches (TSDBHIP_DBG): 1 skip emit, 2 skip fold, 4 skip chunk
+  int32_t dbg;           // k_short profiling switches (TSDBHIP_DBG, results invalid): 1 skip series end,
+                         // 2 skip chunk fold, 8 consume loads, 16 stop after the descriptors, 32 load row 0 only
 };
 
 struct ReduceParams {

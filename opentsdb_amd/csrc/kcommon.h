@@ -46,6 +46,16 @@ __device__ __forceinline__ void set_err(int32_t* err, int code) { atomicCAS(err,
 __device__ __forceinline__ int lanes_below(uint64_t m) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
+// inclusive prefix sum with DPP (gfx9 row_shr / row_bcast): 6 VALU ops, no LDS round trip
+__device__ __forceinline__ int wave_incl_sum_dpp(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);   // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);   // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);   // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);   // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
+  return x;
+}
 // exclusive prefix sum of small non-negative values (< 2^B), bit-sliced over ballots
 template <int B>
 __device__ __forceinline__ int wave_excl_sum_small(int x) {
@@ -1389,6 +1399,33 @@ __device__ __forceinline__ void f_values_vle(const FastLds& L, const FRaw<QW, VL
   }
 }
 
+// VL == 0, integer form: the lane's 8 vle integers as int32 (1- or 2-byte values), one
+// unaligned 16-bit LDS read each (gfx950 LDS serves unaligned ds_read_u16).
+template <int QW, int VL>
+__device__ __forceinline__ void f_values_vle_i(const FastLds& L, const FRaw<QW, VL>& b, int nvl, int xi[DPL]) {
+  const int lane = lane_id();
+  int len[DPL];
+  int tot = 0;
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    len[j] = (j < nvl) ? (int)(f_flags<QW, VL>(b, j) & 7) + 1 : 0;
+    tot += len[j];
+  }
+  int o = wave_incl_sum_dpp(tot) - tot;
+  WAVE_SYNC();
+  reinterpret_cast<uint4*>(L.vstage)[lane] = b.v[0];
+  WAVE_SYNC();
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    uint16_t u;
+    __builtin_memcpy(&u, L.vstage + o, 2);   // bytes o (low half), o + 1
+    const int v1 = (int)(int8_t)(uint8_t)u;
+    const int v2 = (int)(int16_t)(uint16_t)((u << 8) | (u >> 8));
+    xi[j] = len[j] == 2 ? v2 : v1;
+    o += len[j];
+  }
+}
+
 struct FGeom {
   int q0, r0;   // slot at the row base, remainder in n-units (r0 < 0: row starts before slot 0)
 };
@@ -1420,9 +1457,17 @@ __device__ __forceinline__ void fast_chunk(const GridParams& p, const FastLds& L
   uint32_t fld[DPL];
 #pragma unroll
   for (int j = 0; j < DPL; j++) fld[j] = f_field<QW, VL>(b, j);
+  // vle integers (1-2 bytes): the in-lane runs are folded in int32 (8 values of |x| < 2^15
+  // sum exactly) and converted once per run; squareSum stays in double
+  constexpr bool IP = (VL == 0) && (F != F_SQUARESUM);
   double xs[DPL];
+  int xi[DPL];
   if (VL == 0) {
-    f_values_vle<QW, VL>(L, b, nvl, xs);
+    f_values_vle_i<QW, VL>(L, b, nvl, xi);
+    if (!IP) {
+#pragma unroll
+      for (int j = 0; j < DPL; j++) xs[j] = (double)xi[j];
+    }
   } else {
 #pragma unroll
     for (int j = 0; j < DPL; j++) xs[j] = f_value<QW, VL>(b, j);
@@ -1444,6 +1489,31 @@ __device__ __forceinline__ void fast_chunk(const GridParams& p, const FastLds& L
     uint32_t Tf;
     if (uq == 1) Tf = (uint32_t)Dn;                      // uniform branch: no runtime integer division
     else Tf = (uint32_t)((Dn + 999) / 1000);
+    if constexpr (IP) {
+      constexpr int ID = F == F_MIN ? INT32_MAX : (F == F_MAX ? INT32_MIN : 0);
+      int P = ID, sF = 0, mL = ID, cF = 0;
+#pragma unroll
+      for (int j = 0; j < DPL; j++) {
+        const bool valid = FULL || j < nvl;
+        const bool inF = valid && fld[j] < Tf;
+        const int x = xi[j];
+        if (F == F_MIN) {
+          P = min(P, valid ? x : INT32_MAX);
+          if (!inF && valid) mL = min(mL, x);
+        } else if (F == F_MAX) {
+          P = max(P, valid ? x : INT32_MIN);
+          if (!inF && valid) mL = max(mL, x);
+        } else if (F != F_COUNT) {
+          P += valid ? x : 0;
+        }
+        if (inF) { sF = P; cF = j + 1; }
+      }
+      const int nL = nvl - cF;
+      const int iL = (F == F_MIN || F == F_MAX) ? mL : P - sF;
+      fast_fold<F>(L, sfirst, (double)sF, (uint32_t)cF);
+      if (nL > 0) fast_fold<F>(L, sfirst + 1, (double)iL, (uint32_t)nL);
+      return;
+    }
     double P = fast_identity<F>(), sF = 0.0, mL = fast_identity<F>();
     int cF = 0;
 #pragma unroll
@@ -1478,7 +1548,7 @@ __device__ __forceinline__ void fast_chunk(const GridParams& p, const FastLds& L
         if (n >= 0) {
           const int s = f_slot(p, m, n);
           if (s < K) {
-            double x = xs[j];
+            double x = IP ? (double)xi[j] : xs[j];
             if (F == F_SQUARESUM) x = x * x;
             fast_fold<F>(L, s, x, 1u);
           }
