@@ -68,6 +68,31 @@ def grid_config(args, eng, queries, n_series, n_points, value_kind, int_mod, gro
         print(json.dumps(line), flush=True)
 
 
+def rollup_bench(args, eng, n_series):
+    """Config 5 rollup generation over the resident batch: 1 h rollups in 1 d rows and
+    1 d rollups in monthly rows, sum/count/max/min each."""
+    from opentsdb_amd import engine
+    tm = eng.timing()
+    in_bytes = int(tm.bytes)
+    for iv, span in [("1h", "1d"), ("1d", "1n")]:
+        riv = engine.rollup_interval(iv, span)
+        nc, nb = eng.rollup_run(riv, T0, T0 + 86400)
+        ms = []
+        for _ in range(args.steps):
+            t = time.perf_counter()
+            nc, nb = eng.rollup_run(riv, T0, T0 + 86400)
+            ms.append((time.perf_counter() - t) * 1000)
+        step_ms = sum(ms) / len(ms)
+        out_bytes = nc * (4 + 4 + 3 + 8) + nb
+        line = {"config": args.config, "query": f"rollup {iv} in {span} rows x sum,count,max,min",
+                "series": n_series, "datapoints": int(tm.datapoints), "cells": nc, "value_bytes": nb,
+                "ms_per_step": step_ms, "datapoints_per_s": tm.datapoints / (step_ms / 1000),
+                "algorithmic_bytes": in_bytes + out_bytes,
+                "hbm_frac_of_8tbs": (in_bytes + out_bytes) / (step_ms / 1000) / 8e12,
+                "note": "one downsample pass per function (4 input reads); algorithmic bytes count one"}
+        print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=4)
@@ -88,7 +113,7 @@ def main():
         eng = Engine(0)
         series = args.series if args.series != 100_000 else 10_000_000
         groups = args.groups if args.groups != 64 else 1000
-        qs = {f"{a}:1m-avg": dsq(a, "1m-avg", T0 + 3599) for a in ["avg", "min", "max", "count", "dev"]}
+        qs = {f"{a}:1m-avg": dsq(a, "1m-avg", T0 + 3599) for a in ["sum", "avg", "min", "max", "count", "dev"]}
         grid_config(args, eng, qs, series, 360, 2, 30000, groups)
         eng.close()
         return
@@ -97,6 +122,7 @@ def main():
         series = args.series if args.series != 100_000 else 1_250_000
         qs = {f"sum:1h-{f}": dsq("sum", f"1h-{f}", T0 + 86399) for f in ["p99", "ep99r7"]}
         grid_config(args, eng, qs, series, 8640, 0, 1, args.groups)
+        rollup_bench(args, eng, series)
         eng.close()
         return
 
