@@ -104,6 +104,103 @@ __device__ __forceinline__ double reg_at(const double v[DPL], int i) {
   return __shfl(t, i / DPL, 64);
 }
 
+// one DPP step of a 64-lane max / min of a double (identity where the source is invalid)
+template <bool MAX, int CTRL, int RMASK>
+__device__ __forceinline__ double dpp_ext_step(double x) {
+  const double id = MAX ? -(double)INFINITY : (double)INFINITY;
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(id), __double2loint(x), CTRL, RMASK, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(id), __double2hiint(x), CTRL, RMASK, 0xF, false);
+  const double y = __hiloint2double(hi, lo);
+  return MAX ? fmax(x, y) : fmin(x, y);
+}
+
+// 64-lane max / min of a double with DPP (row_shr + row_bcast), result in every lane
+template <bool MAX>
+__device__ __forceinline__ double wave_ext_f64(double x) {
+  x = dpp_ext_step<MAX, 0x111, 0xF>(x);   // row_shr:1
+  x = dpp_ext_step<MAX, 0x112, 0xF>(x);   // row_shr:2
+  x = dpp_ext_step<MAX, 0x114, 0xF>(x);   // row_shr:4
+  x = dpp_ext_step<MAX, 0x118, 0xF>(x);   // row_shr:8
+  x = dpp_ext_step<MAX, 0x142, 0xA>(x);   // row_bcast:15 -> rows 1, 3
+  x = dpp_ext_step<MAX, 0x143, 0xC>(x);   // row_bcast:31 -> rows 2, 3
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), 63);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), 63);
+  return __hiloint2double(hi, lo);
+}
+
+// Order statistics by extraction: the k largest (MAX) or smallest values of the multiset
+// held 8 per lane (pads = the opposite infinity), one per step, one occurrence removed per
+// step; returns the last two extracted (e_k, e_{k-1}).  Used when the requested order
+// statistics lie within 24 of either end (p95..p999 of 1 h @10 s buckets: 1..19 steps)
+// instead of a 512-element bitonic sort; the values are the same order statistics.
+template <bool MAX>
+__device__ __forceinline__ void extract_k(double v[DPL], int k, double& ek, double& ek1) {
+  const int lane = lane_id();
+  const double gone = MAX ? -(double)INFINITY : (double)INFINITY;
+  ek = ek1 = gone;
+  for (int t = 0; t < k; t++) {
+    double m = v[0];
+#pragma unroll
+    for (int j = 1; j < DPL; j++) m = MAX ? fmax(m, v[j]) : fmin(m, v[j]);
+    const double w = wave_ext_f64<MAX>(m);
+    const uint64_t holders = __ballot(m == w);
+    const int first = __ffsll((long long)holders) - 1;
+    if (lane == first) {
+      bool done = false;
+#pragma unroll
+      for (int j = 0; j < DPL; j++) {
+        if (!done && v[j] == w) { v[j] = gone; done = true; }
+      }
+    }
+    ek1 = ek;
+    ek = w;
+  }
+}
+
+// LEGACY estimate from the extremes when the needed order statistics are within 24 of an
+// end; false = use the sort
+__device__ __forceinline__ bool select_extreme(int fn, int n, const double* buf, double& out) {
+  if (fn == TSDB_AGG_MEDIAN || n < 2 || n > CH) return false;
+  const int lane = lane_id();
+  const double q = pct_quantile(fn) / 100.0;
+  const double pos = q * (double)(n + 1);
+  const int ip = (int)floor(pos);
+  // ascending indices lo_i, hi_i (select_sorted / Percentile.estimate)
+  int lo_i, hi_i;
+  if (pos < 1) { lo_i = hi_i = 0; }
+  else if (pos >= (double)n) { lo_i = hi_i = n - 1; }
+  else { lo_i = ip - 1; hi_i = ip; }
+  const int ktop = n - lo_i, kbot = hi_i + 1;
+  if (min(ktop, kbot) > 24) return false;
+  double v[DPL];
+  double a, b;   // extracted values at lo_i / hi_i
+  if (ktop <= kbot) {
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      const int e = lane * DPL + j;
+      v[j] = e < n ? buf[e] : -(double)INFINITY;
+    }
+    double ek, ek1;
+    extract_k<true>(v, ktop, ek, ek1);   // e_ktop is index lo_i, e_{ktop-1} index lo_i + 1
+    a = ek;
+    b = (hi_i == lo_i) ? ek : ek1;
+  } else {
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      const int e = lane * DPL + j;
+      v[j] = e < n ? buf[e] : (double)INFINITY;
+    }
+    double ek, ek1;
+    extract_k<false>(v, kbot, ek, ek1);  // m_kbot is index hi_i, m_{kbot-1} index hi_i - 1
+    b = ek;
+    a = (hi_i == lo_i) ? ek : ek1;
+  }
+  if (lo_i == hi_i) { out = a; return true; }
+  const double dif = pos - floor(pos);
+  out = a + dif * (b - a);
+  return true;
+}
+
 // value of a finished bucket holding n non-NaN values in buf (tot values incl. NaN)
 __device__ __forceinline__ double bucket_value(const GridParams& p, double* buf, int n) {
   const int lane = lane_id();
@@ -112,6 +209,8 @@ __device__ __forceinline__ double bucket_value(const GridParams& p, double* buf,
     if (lane == 0) set_err(p.err, TSDB_E_NOT_IMPLEMENTED);
     return (double)NAN;
   }
+  double sel;
+  if (select_extreme(p.sel_fn, n, buf, sel)) return sel;
   if (n <= CH) {
     double v[DPL];
 #pragma unroll

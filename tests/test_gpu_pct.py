@@ -113,3 +113,13 @@ def test_pct_sharded(eng, day_batch):
         assert_groups_match(run_sharded(es, day_batch, q, 2), O.run_query(day_batch, q), "sum", ctx="x2")
     finally:
         es[1].close()
+
+
+@pytest.mark.parametrize("fn", ["p999", "p99", "p95", "ep99r3", "ep99r7", "ep999r7"])
+@pytest.mark.parametrize("interval", [60000, 600000, 3600000])
+def test_pct_extreme_selection_with_ties(eng, fn, interval):
+    # order statistics near either end (selection by extraction): integer values with many
+    # ties (5 distinct values) and 6..360 values per bucket
+    b = synth.generate(16, T0, 360, 10000, value_kind=1, n_groups=2, int_mod=5, seed=11)
+    q = abi.new_query(T0, T0 + 3599, "max", ds_function=abi.AGG[fn], ds_interval_ms=interval)
+    assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "max", ctx=f"{fn} {interval}")
