@@ -151,6 +151,7 @@ struct tsdbhip_ctx {
   // dominant uniform row class of the batch (k_fast specialisation), 0 = none
   int fast_qw = 0, fast_vl = 0;        // dominant k_fast row class (0 = none)
   int fast_qw2 = 0, fast_vl2 = 0;      // second class, chained over the first one's redo list
+  int pct_qw = 0, pct_vl = 0;          // dominant uniform class of one-chunk rows (k_pct_rows)
   // tile lists by k_fast row class (built at load): [class A / class B][walker / short],
   // and the tiles of neither class (general kernel only).  Short = one row per series of at
   // most CH datapoints (k_short).
@@ -455,6 +456,7 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
   c->h_flags.resize(c->n_rows);
   int64_t cls[2][2] = {{0, 0}, {0, 0}};   // [qw 2/4][vl 4/8] uniform float rows
   int64_t cls_vle = 0;                    // 2-byte qualifiers, 1-2 byte integers, one chunk
+  int64_t cls_pct[2][9] = {};             // [qw 2/4][vl]: uniform sorted rows of <= 512 dp
   for (int64_t r = 0; r < c->n_rows; r++) {
     c->h_ndp[r] = back[r].ndp;
     c->h_base[r] = back[r].base;
@@ -467,6 +469,9 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
       cls[qw == 4][vl == 8] += back[r].ndp;
     if ((f & ROW_ALLI) && (f & ROW_VLE2) && !(f & (ROW_ERR | ROW_UNSORTED)) && qw == 2 && back[r].ndp <= 512)
       cls_vle += back[r].ndp;
+    if (!(f & (ROW_ERR | ROW_UNSORTED)) && (qw == 2 || qw == 4) && (vl == 1 || vl == 2 || vl == 4 || vl == 8) &&
+        back[r].ndp <= 512)
+      cls_pct[qw == 4][vl] += back[r].ndp;
   }
   // the two largest k_fast row classes by datapoints
   struct Cand { int64_t n; int qw, vl; };
@@ -475,6 +480,11 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
   c->fast_qw = c->fast_vl = c->fast_qw2 = c->fast_vl2 = 0;
   if (cand[0].n > 0) { c->fast_qw = cand[0].qw; c->fast_vl = cand[0].vl; }
   if (cand[1].n > 0) { c->fast_qw2 = cand[1].qw; c->fast_vl2 = cand[1].vl; }
+  c->pct_qw = c->pct_vl = 0;
+  int64_t best = 0;
+  for (int a = 0; a < 2; a++)
+    for (int v = 1; v <= 8; v++)
+      if (cls_pct[a][v] > best) { best = cls_pct[a][v]; c->pct_qw = a ? 4 : 2; c->pct_vl = v; }
   // malformed rows are reported lazily, when a query reads them (as the reference does)
   return build_tiles(c);
 }
@@ -858,11 +868,34 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     HIP_OK(hipMemsetAsync(c->redo_n.p, 0, 4, c->stream));
     gp.redo_list = c->redo.as<int32_t>();
     gp.redo_n = c->redo_n.as<int32_t>();
-    HIP_OK(launch_pct(gp, false, c->n_series, c->stream));
+    // Buckets inside rows (interval | 1 h) and a statistic near the ends (p90 and up):
+    // k_pct_rows, with k_pct over the series it hands back; else k_pct over every series.
+    const int sel_i = (q->ds_function - TSDB_AGG_P999) % 6;
+    const char* renv = std::getenv("TSDBHIP_PCTROWS");
+    const bool rows_path = P.mode == MODE_GRID && q->ds_function != TSDB_AGG_MEDIAN && sel_i <= 3 && P.I > 0 &&
+                           3600000 % P.I == 0 && P.B0 % P.I == 0 && pct_rows_supported(c->pct_qw, c->pct_vl) &&
+                           !(renv && renv[0] == '0');
+    if (rows_path) {
+      HIP_OK(c->redo2.ensure(std::max<int64_t>(1, c->n_series) * 4));
+      HIP_OK(c->redo2_n.ensure(16));
+      HIP_OK(hipMemsetAsync(c->redo2_n.p, 0, 4, c->stream));
+      GridParams rp = gp;
+      rp.redo_list = c->redo2.as<int32_t>();
+      rp.redo_n = c->redo2_n.as<int32_t>();
+      HIP_OK(launch_pct_rows(rp, c->pct_qw, c->pct_vl, c->stream));
+      int32_t nback = 0;
+      HIP_OK(hipMemcpyAsync(&nback, c->redo2_n.p, 4, hipMemcpyDeviceToHost, c->stream));
+      HIP_OK(hipStreamSynchronize(c->stream));
+      gp.tile_list = c->redo2.as<int32_t>();
+      gp.tile_list_n = c->redo2_n.as<int32_t>();
+      HIP_OK(launch_pct(gp, 1, nback, c->stream));
+    } else {
+      HIP_OK(launch_pct(gp, 0, c->n_series, c->stream));
+    }
     int32_t nbig = 0;   // series with a bucket of more than 512 values: the LDS-sort pass
     HIP_OK(hipMemcpyAsync(&nbig, c->redo_n.p, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
-    HIP_OK(launch_pct(gp, true, nbig, c->stream));
+    HIP_OK(launch_pct(gp, 2, nbig, c->stream));
     HIP_OK(launch_emit(gp, c->stream));
     HIP_OK(hipEventRecord(c->ev[1], c->stream));
   } else {

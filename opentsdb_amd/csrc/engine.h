@@ -253,7 +253,11 @@ int64_t fast_wave_lds(int64_t K, bool rate);
 hipError_t launch_reduce(const ReduceParams& p, hipStream_t s);
 // percentile / median downsampling (k_pct.hip): bucket order statistics, then group-by
 static constexpr int PCT_CAP = 4096;   // values per bucket sorted in LDS
-hipError_t launch_pct(const GridParams& p, bool big, int64_t n, hipStream_t s);
+// pass 0: every series; 1: the series k_pct_rows handed back (tile_list); 2: the LDS-sort
+// pass over redo_list
+hipError_t launch_pct(const GridParams& p, int pass, int64_t n, hipStream_t s);
+bool pct_rows_supported(int qw, int vl);
+hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s);
 hipError_t launch_emit(const GridParams& p, hipStream_t s);
 hipError_t launch_rank_merge(const RankMergeParams& p, hipStream_t s);
 // per-downsample-function instantiations (k_grid.hip / k_fast.hip, one object per F)

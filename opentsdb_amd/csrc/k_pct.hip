@@ -234,7 +234,7 @@ __device__ __forceinline__ double bucket_value(const GridParams& p, double* buf,
 // to p.redo_list and left to the BIG pass (one wave per listed series, LDS buffer of
 // PCT_CAP values).  Uniform rows are decoded from registers with a one-chunk prefetch
 // (load_raw / decode_raw, as k_grid); other row classes through decode_generic.
-template <bool BIG>
+template <bool BIG, bool LIST>
 __global__ __launch_bounds__(256) void k_pct(GridParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int CAP = BIG ? PCT_CAP : CH;
@@ -252,6 +252,9 @@ __global__ __launch_bounds__(256) void k_pct(GridParams p) {
   if (BIG) {
     if (s >= (int64_t)*p.redo_n) return;
     s = p.redo_list[s];
+  } else if (LIST) {   // series k_pct_rows handed back
+    if (s >= (int64_t)*p.tile_list_n) return;
+    s = p.tile_list[s];
   }
   if (s >= p.n_series) return;
   double* dense = p.pre_dense + s * K;
@@ -401,18 +404,281 @@ __global__ __launch_bounds__(256) void k_emit(GridParams p) {
   }
 }
 
-hipError_t launch_pct(const GridParams& p, bool big, int64_t n, hipStream_t s) {
+// ---- k_pct_rows: buckets inside rows, order statistics near the ends ------------------
+//
+// When the interval divides one hour (and slot 0 is interval-aligned, as the Downsampler's
+// seek makes it) no bucket spans two rows, so every row is independent work: a wave takes a
+// series, loads all its row descriptors at once (lane i: row i of a 64-row window) and runs
+// a two-deep load ring over the rows with no walker.  Each bucket's order statistics come
+// from extraction over the decoded registers (select_extreme's arithmetic, values removed
+// through a per-lane keep mask), so the per-wave state is ~60 VGPRs and the kernel keeps
+// far more waves in flight than k_pct.  A series that breaks a premise -- a row of another
+// class, > CH datapoints, unsorted or malformed, an offset >= 1 h, a repeated base time, or a
+// bucket whose statistic lies more than EXT_MAX from both ends -- is appended to
+// p.redo_list for k_pct (which recomputes it whole).
+
+static constexpr int EXT_MAX = 24;
+
+// DPP int min across the wave (uniform result)
+__device__ __forceinline__ int wave_min_dpp(int x) {
+  x = min(x, __builtin_amdgcn_update_dpp(INT32_MAX, x, 0x111, 0xF, 0xF, false));
+  x = min(x, __builtin_amdgcn_update_dpp(INT32_MAX, x, 0x112, 0xF, 0xF, false));
+  x = min(x, __builtin_amdgcn_update_dpp(INT32_MAX, x, 0x114, 0xF, 0xF, false));
+  x = min(x, __builtin_amdgcn_update_dpp(INT32_MAX, x, 0x118, 0xF, 0xF, false));
+  x = min(x, __builtin_amdgcn_update_dpp(INT32_MAX, x, 0x142, 0xA, 0xF, false));
+  x = min(x, __builtin_amdgcn_update_dpp(INT32_MAX, x, 0x143, 0xC, 0xF, false));
+  return __builtin_amdgcn_readlane(x, 63);
+}
+
+// k-th largest (MAX) / smallest value of the multiset {val[j] : keep bit j}, and the
+// (k-1)-th; one occurrence removed per step (ties kept as a multiset)
+template <bool MAX>
+__device__ __forceinline__ void extract_masked(const double val[DPL], uint32_t keep, int k, double& ek, double& ek1) {
+  const int lane = lane_id();
+  const double gone = MAX ? -(double)INFINITY : (double)INFINITY;
+  ek = ek1 = gone;
+  for (int t = 0; t < k; t++) {
+    double m = gone;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      const double c = MAX ? fmax(m, val[j]) : fmin(m, val[j]);
+      m = ((keep >> j) & 1) ? c : m;
+    }
+    const double w = wave_ext_f64<MAX>(m);
+    const uint64_t holders = __ballot(keep != 0 && m == w);
+    const int first = __ffsll((long long)holders) - 1;
+    if (lane == first) {
+      uint32_t hit = 0;
+#pragma unroll
+      for (int j = DPL - 1; j >= 0; j--) if (((keep >> j) & 1) && val[j] == w) hit = 1u << j;
+      keep &= ~hit;
+    }
+    ek1 = ek;
+    ek = w;
+  }
+}
+
+struct RowLite {
+  uint64_t qoff, voff;
+  uint32_t base, ndp;
+};
+
+__device__ __forceinline__ RowLite row_of_lane(const RowDesc& d, int l) {
+  RowLite r;
+  r.qoff = rl64(d.qoff, l);
+  r.voff = rl64(d.voff, l);
+  r.base = (uint32_t)__builtin_amdgcn_readlane((int)d.base, l);
+  r.ndp = (uint32_t)__builtin_amdgcn_readlane((int)d.ndp, l);
+  return r;
+}
+
+template <int QW, int VL>
+struct RawT {
+  uint4 q[QW / 2];
+  uint4 v[VL <= 2 ? 1 : VL / 2];
+};
+
+template <int QW, int VL>
+__device__ __forceinline__ void load_row(const GridParams& p, const RowLite& d, RawT<QW, VL>& rw) {
+  const int64_t i0 = (int64_t)lane_id() * DPL;
+  if (i0 >= (int64_t)d.ndp) return;
+  const uint8_t* q = p.qual + d.qoff + i0 * QW;
+  const uint8_t* v = p.val + d.voff + i0 * VL;
+#pragma unroll
+  for (int i = 0; i < QW / 2; i++) rw.q[i] = reinterpret_cast<const uint4*>(q)[i];
+  if (VL == 1) {
+    const uint2 t = *reinterpret_cast<const uint2*>(v);
+    rw.v[0] = make_uint4(t.x, t.y, 0, 0);
+  } else {
+#pragma unroll
+    for (int i = 0; i < (VL <= 2 ? 1 : VL / 2); i++) rw.v[i] = reinterpret_cast<const uint4*>(v)[i];
+  }
+}
+
+// the lane's 8 datapoints: slot (-1 = none), value, and whether every offset is < 1 h
+template <int QW, int VL>
+__device__ __forceinline__ bool decode_row(const GridParams& p, const RowLite& d, const RowGeom& g,
+                                           const RawT<QW, VL>& rw, int slot[DPL], double val[DPL]) {
+  const int64_t i0 = (int64_t)lane_id() * DPL;
+  const int nv = (int)max((int64_t)0, min((int64_t)DPL, (int64_t)d.ndp - i0));
+  uint32_t off[DPL], fl[DPL];
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    if (QW == 2) {
+      const uint32_t w = (&rw.q[0].x)[j >> 1];
+      const uint32_t be = __builtin_bswap32(w);
+      const uint32_t qq = (j & 1) ? (be & 0xFFFF) : (be >> 16);
+      off[j] = (qq >> 4) * 1000u;
+      fl[j] = qq & 0xF;
+    } else {
+      const uint32_t qq = __builtin_bswap32((&rw.q[0].x)[j]);
+      off[j] = (qq & 0x0FFFFFC0u) >> 6;
+      fl[j] = qq & 0xF;
+    }
+  }
+  const uint32_t* vw = &rw.v[0].x;
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    if (VL == 4) {
+      const uint32_t be = __builtin_bswap32(vw[j]);
+      val[j] = (fl[j] & 8) ? (double)__uint_as_float(be) : (double)(int32_t)be;
+    } else if (VL == 8) {
+      const uint64_t a = ((uint64_t)__builtin_bswap32(vw[2 * j]) << 32) | __builtin_bswap32(vw[2 * j + 1]);
+      val[j] = (fl[j] & 8) ? __longlong_as_double((long long)a) : (double)(long long)a;
+    } else if (VL == 2) {
+      const uint32_t be = __builtin_bswap32(vw[j >> 1]);
+      const uint32_t x = (j & 1) ? (be & 0xFFFF) : (be >> 16);
+      val[j] = (double)(int16_t)(uint16_t)x;
+    } else {
+      val[j] = (double)(int8_t)((vw[j >> 2] >> ((j & 3) * 8)) & 0xFF);
+    }
+  }
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    slot[j] = (j < nv) ? slot_of(p, g, d.base, off[j]) : -1;
+    ok = ok && (j >= nv || off[j] < 3600000u);
+  }
+  return ok;
+}
+
+template <int QW, int VL>
+__global__ __launch_bounds__(256) void k_pct_rows(GridParams p) {
+  const int lane = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t s = (int64_t)blockIdx.x * 4 + wave;
+  if (s >= p.n_series) return;
+  const int K = (int)p.K;
+  double* dense = p.pre_dense + s * K;
+  uint8_t* pres = p.pre_pres + s * K;
+  for (int k = lane; k < K; k += 64) pres[k] = 0;
+  const double q = pct_quantile(p.sel_fn) / 100.0;
+  const int64_t r0 = p.series_row_ptr[s], r1 = p.series_row_ptr[s + 1];
+  int64_t last_base = -1;   // base of the previous in-range row (repeated bases: redo)
+  for (int64_t w0 = r0; w0 < r1; w0 += 64) {
+    const int nr = (int)min((int64_t)64, r1 - w0);
+    RowDesc d = {};
+    bool in = false, bad = false;
+    if (lane < nr) {
+      d = p.rows[w0 + lane];
+      in = (int64_t)d.base >= p.ss && (int64_t)d.base < p.se;
+      const uint32_t f = d.flags;
+      bad = in && ((f & (ROW_ERR | ROW_UNSORTED)) || (int)(f & ROW_QW_MASK) != QW ||
+                   (int)((f & ROW_VL_MASK) >> ROW_VL_SHIFT) != VL || d.ndp > (uint32_t)CH);
+    }
+    // strictly increasing bases (rows of one series are in base order; equal = two cells)
+    const int prev = __shfl_up((int)d.base, 1, 64);
+    if (in && lane > 0 && (uint32_t)prev >= d.base) bad = true;
+    if (in && lane == 0 && last_base >= (int64_t)d.base) bad = true;
+    if (__ballot(bad)) {
+      if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)s;
+      return;
+    }
+    uint64_t m = __ballot(in);
+    if (!m) continue;
+    // rows of a series are in base order, so in-range rows are contiguous: the last one
+    // of this window is the highest set bit
+    last_base = (uint32_t)__builtin_amdgcn_readlane((int)d.base, 63 - __clzll((long long)m));
+    RowLite cd = row_of_lane(d, __ffsll((long long)m) - 1);
+    RawT<QW, VL> rc = {}, rn = {};
+    load_row<QW, VL>(p, cd, rc);
+    for (;;) {
+      m &= m - 1;
+      const bool has_next = m != 0;
+      RowLite nd = {};
+      if (has_next) {
+        nd = row_of_lane(d, __ffsll((long long)m) - 1);
+        load_row<QW, VL>(p, nd, rn);
+      }
+      const RowGeom g = row_geom(p, cd.base);
+      int slot[DPL];
+      double val[DPL];
+      const bool ok = decode_row<QW, VL>(p, cd, g, rc, slot, val);
+      if (__ballot(!ok)) {
+        if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)s;
+        return;
+      }
+      uint32_t left = 0;
+#pragma unroll
+      for (int j = 0; j < DPL; j++) left |= (slot[j] >= 0 ? 1u : 0u) << j;
+      for (;;) {
+        int mn = INT32_MAX;
+#pragma unroll
+        for (int j = 0; j < DPL; j++) if ((left >> j) & 1) mn = min(mn, slot[j]);
+        mn = wave_min_dpp(mn);
+        if (mn == INT32_MAX) break;
+        uint32_t keep = 0;
+#pragma unroll
+        for (int j = 0; j < DPL; j++) {
+          if (((left >> j) & 1) && slot[j] == mn) {
+            left &= ~(1u << j);
+            if (!isnan(val[j])) keep |= 1u << j;
+          }
+        }
+        const int n = __builtin_amdgcn_readlane(wave_incl_sum_dpp(__popc(keep)), 63);
+        double x = (double)NAN;
+        if (n > 0) {
+          // select_sorted / select_extreme: LEGACY pos = p (n + 1)
+          const double pos = q * (double)(n + 1);
+          const int ip = (int)floor(pos);
+          int lo_i, hi_i;
+          if (pos < 1) { lo_i = hi_i = 0; }
+          else if (pos >= (double)n) { lo_i = hi_i = n - 1; }
+          else { lo_i = ip - 1; hi_i = ip; }
+          const int ktop = n - lo_i, kbot = hi_i + 1;
+          if (min(ktop, kbot) > EXT_MAX) {
+            if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)s;
+            return;
+          }
+          double a, b, ek, ek1;
+          if (ktop <= kbot) {
+            extract_masked<true>(val, keep, ktop, ek, ek1);
+            a = ek;
+            b = (hi_i == lo_i) ? ek : ek1;
+          } else {
+            extract_masked<false>(val, keep, kbot, ek, ek1);
+            b = ek;
+            a = (hi_i == lo_i) ? ek : ek1;
+          }
+          x = (lo_i == hi_i) ? a : a + (pos - floor(pos)) * (b - a);
+        }
+        if (lane == 0) { dense[mn] = x; pres[mn] = 1; }
+      }
+      if (!has_next) break;
+      cd = nd;
+      rc = rn;
+    }
+  }
+}
+
+hipError_t launch_pct(const GridParams& p, int pass, int64_t n, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  if (big) {
+  if (pass == 2) {
     const size_t lds = 2 * (size_t)(VBUF + PCT_CAP * 8);
-    hipError_t e = hipFuncSetAttribute((const void*)k_pct<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute((const void*)k_pct<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_pct<true>, dim3((unsigned)((n + 1) / 2)), dim3(128), lds, s, p);
+    hipLaunchKernelGGL((k_pct<true, false>), dim3((unsigned)((n + 1) / 2)), dim3(128), lds, s, p);
   } else {
     const size_t lds = 4 * (size_t)(VBUF + CH * 8);
-    hipLaunchKernelGGL(k_pct<false>, dim3((unsigned)((n + 3) / 4)), dim3(256), lds, s, p);
+    if (pass == 1)
+      hipLaunchKernelGGL((k_pct<false, true>), dim3((unsigned)((n + 3) / 4)), dim3(256), lds, s, p);
+    else
+      hipLaunchKernelGGL((k_pct<false, false>), dim3((unsigned)((n + 3) / 4)), dim3(256), lds, s, p);
   }
   return hipGetLastError();
+}
+
+bool pct_rows_supported(int qw, int vl) { return (qw == 2 || qw == 4) && (vl == 1 || vl == 2 || vl == 4 || vl == 8); }
+
+hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s) {
+  if (p.n_series == 0) return hipSuccess;
+  const dim3 grid((unsigned)((p.n_series + 3) / 4)), block(256);
+#define PCT_ROWS_CASE(Q, V) \
+  if (qw == Q && vl == V) { hipLaunchKernelGGL((k_pct_rows<Q, V>), grid, block, 0, s, p); return hipGetLastError(); }
+  PCT_ROWS_CASE(2, 1) PCT_ROWS_CASE(2, 2) PCT_ROWS_CASE(2, 4) PCT_ROWS_CASE(2, 8)
+  PCT_ROWS_CASE(4, 1) PCT_ROWS_CASE(4, 2) PCT_ROWS_CASE(4, 4) PCT_ROWS_CASE(4, 8)
+#undef PCT_ROWS_CASE
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_emit(const GridParams& p, hipStream_t s) {
