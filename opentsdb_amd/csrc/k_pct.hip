@@ -14,6 +14,8 @@
 //            rate), exactly emit_series of k_grid, into tile partials for k_reduce.
 #include "kcommon.h"
 
+#include <cstdlib>
+
 namespace tsdb {
 
 // compare-exchange keeping (lo, hi); ties keep both values (multiset preserved)
@@ -495,12 +497,14 @@ __device__ __forceinline__ void load_row(const GridParams& p, const RowLite& d, 
   }
 }
 
-// the lane's 8 datapoints: slot (-1 = none), value, and whether every offset is < 1 h
+// the lane's 8 datapoints: slot (-1 = none), value, and whether every offset is < 1 h.
+// slot0 = the row base's slot (exact: base and slot 0 are multiples of I); a datapoint at
+// offset off lies in slot0 + off / I (one bucket per row when I = 1 h).
 template <int QW, int VL>
-__device__ __forceinline__ bool decode_row(const GridParams& p, const RowLite& d, const RowGeom& g,
+__device__ __forceinline__ bool decode_row(const GridParams& p, const RowLite& d, int slot0, bool one,
                                            const RawT<QW, VL>& rw, int slot[DPL], double val[DPL]) {
-  const int64_t i0 = (int64_t)lane_id() * DPL;
-  const int nv = (int)max((int64_t)0, min((int64_t)DPL, (int64_t)d.ndp - i0));
+  const int i0 = lane_id() * DPL;
+  const int nv = max(0, min(DPL, (int)d.ndp - i0));
   uint32_t off[DPL], fl[DPL];
 #pragma unroll
   for (int j = 0; j < DPL; j++) {
@@ -534,15 +538,110 @@ __device__ __forceinline__ bool decode_row(const GridParams& p, const RowLite& d
     }
   }
   bool ok = true;
+  const uint32_t I32 = (uint32_t)p.I;
 #pragma unroll
   for (int j = 0; j < DPL; j++) {
-    slot[j] = (j < nv) ? slot_of(p, g, d.base, off[j]) : -1;
+    int sl = slot0;
+    if (!one) {
+      // off < 3.6e6 (exact in float): reciprocal estimate, corrected to the exact quotient
+      uint32_t qq = (uint32_t)((float)off[j] * p.rcpI);
+      int64_t r = (int64_t)off[j] - (int64_t)qq * I32;
+      if (r < 0) { qq--; r += I32; }
+      if (r >= (int64_t)I32) { qq++; r -= I32; }
+      if (r >= (int64_t)I32) { qq++; }
+      sl += (int)qq;
+    }
+    slot[j] = (j < nv && sl >= 0 && sl < (int)p.K) ? sl : -1;
     ok = ok && (j >= nv || off[j] < 3600000u);
   }
   return ok;
 }
 
+// order statistic of the bucket {val[j] : keep bit j} holding n non-NaN values (n >= 1)
+// by extraction; false = more than EXT_MAX from both ends
+__device__ __forceinline__ bool select_keep(const double val[DPL], uint32_t keep, int n, double q, double& x) {
+  // select_sorted / select_extreme: LEGACY pos = p (n + 1)
+  const double pos = q * (double)(n + 1);
+  const int ip = (int)floor(pos);
+  int lo_i, hi_i;
+  if (pos < 1) { lo_i = hi_i = 0; }
+  else if (pos >= (double)n) { lo_i = hi_i = n - 1; }
+  else { lo_i = ip - 1; hi_i = ip; }
+  const int ktop = n - lo_i, kbot = hi_i + 1;
+  if (min(ktop, kbot) > EXT_MAX) return false;
+  double a, b, ek, ek1;
+  if (ktop <= kbot) {
+    extract_masked<true>(val, keep, ktop, ek, ek1);
+    a = ek;
+    b = (hi_i == lo_i) ? ek : ek1;
+  } else {
+    extract_masked<false>(val, keep, kbot, ek, ek1);
+    b = ek;
+    a = (hi_i == lo_i) ? ek : ek1;
+  }
+  x = (lo_i == hi_i) ? a : a + (pos - floor(pos)) * (b - a);
+  return true;
+}
+
+// one in-range row: its buckets' order statistics into dense / pres; false = hand the
+// series back (offset >= 1 h, or a statistic more than EXT_MAX from both ends)
 template <int QW, int VL>
+__device__ __forceinline__ bool pct_row(const GridParams& p, const RowLite& cd, const RawT<QW, VL>& rc, double q,
+                                        double* dense, uint8_t* pres) {
+  const int lane = lane_id();
+  RowLite d;
+  d.base = (uint32_t)__builtin_amdgcn_readfirstlane((int)cd.base);
+  d.ndp = (uint32_t)__builtin_amdgcn_readfirstlane((int)cd.ndp);
+  // slot of the row base: (base * 1000 - B0) / I, an exact multiple (double division exact)
+  const int64_t rel = (int64_t)d.base * 1000 - p.B0;
+  const int slot0 = (int)__builtin_amdgcn_readfirstlane((int)((double)rel / (double)p.I));
+  const bool one = p.I == 3600000;
+  if (one && (slot0 < 0 || slot0 >= (int)p.K)) return true;   // the row's bucket is out of range
+  int slot[DPL];
+  double val[DPL];
+  const bool ok = decode_row<QW, VL>(p, d, slot0, one, rc, slot, val);
+  if (__ballot(!ok)) return false;
+  if (one) {
+    uint32_t keep = 0;
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      any = any || slot[j] >= 0;
+      keep |= (slot[j] >= 0 && !isnan(val[j]) ? 1u : 0u) << j;
+    }
+    if (!__ballot(any)) return true;
+    const int n = __builtin_amdgcn_readlane(wave_incl_sum_dpp(__popc(keep)), 63);
+    double x = (double)NAN;
+    if (n > 0 && !select_keep(val, keep, n, q, x)) return false;
+    if (lane == 0) { dense[slot0] = x; pres[slot0] = 1; }
+    return true;
+  }
+  uint32_t left = 0;
+#pragma unroll
+  for (int j = 0; j < DPL; j++) left |= (slot[j] >= 0 ? 1u : 0u) << j;
+  for (;;) {
+    int mn = INT32_MAX;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) if ((left >> j) & 1) mn = min(mn, slot[j]);
+    mn = wave_min_dpp(mn);
+    if (mn == INT32_MAX) break;
+    uint32_t keep = 0;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      if (((left >> j) & 1) && slot[j] == mn) {
+        left &= ~(1u << j);
+        if (!isnan(val[j])) keep |= 1u << j;
+      }
+    }
+    const int n = __builtin_amdgcn_readlane(wave_incl_sum_dpp(__popc(keep)), 63);
+    double x = (double)NAN;
+    if (n > 0 && !select_keep(val, keep, n, q, x)) return false;
+    if (lane == 0) { dense[mn] = x; pres[mn] = 1; }
+  }
+  return true;
+}
+
+template <int QW, int VL, int D>
 __global__ __launch_bounds__(256) void k_pct_rows(GridParams p) {
   const int lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -557,13 +656,18 @@ __global__ __launch_bounds__(256) void k_pct_rows(GridParams p) {
   int64_t last_base = -1;   // base of the previous in-range row (repeated bases: redo)
   for (int64_t w0 = r0; w0 < r1; w0 += 64) {
     const int nr = (int)min((int64_t)64, r1 - w0);
-    RowDesc d = {};
+    RowDesc d = {};   // only qoff / voff / base / ndp / flags are read
     bool in = false, bad = false;
     if (lane < nr) {
-      d = p.rows[w0 + lane];
+      const RowDesc* src = p.rows + w0 + lane;
+      d.qoff = src->qoff;
+      d.voff = src->voff;
+      d.base = src->base;
+      d.ndp = src->ndp;
+      d.flags = src->flags;
       in = (int64_t)d.base >= p.ss && (int64_t)d.base < p.se;
       const uint32_t f = d.flags;
-      bad = in && ((f & (ROW_ERR | ROW_UNSORTED)) || (int)(f & ROW_QW_MASK) != QW ||
+      bad = in && ((f & (ROW_ERR | ROW_UNSORTED)) || (d.base % 3600u) != 0 || (int)(f & ROW_QW_MASK) != QW ||
                    (int)((f & ROW_VL_MASK) >> ROW_VL_SHIFT) != VL || d.ndp > (uint32_t)CH);
     }
     // strictly increasing bases (rows of one series are in base order; equal = two cells)
@@ -576,77 +680,37 @@ __global__ __launch_bounds__(256) void k_pct_rows(GridParams p) {
     }
     uint64_t m = __ballot(in);
     if (!m) continue;
-    // rows of a series are in base order, so in-range rows are contiguous: the last one
-    // of this window is the highest set bit
-    last_base = (uint32_t)__builtin_amdgcn_readlane((int)d.base, 63 - __clzll((long long)m));
-    RowLite cd = row_of_lane(d, __ffsll((long long)m) - 1);
-    RawT<QW, VL> rc = {}, rn = {};
-    load_row<QW, VL>(p, cd, rc);
-    for (;;) {
-      m &= m - 1;
-      const bool has_next = m != 0;
-      RowLite nd = {};
-      if (has_next) {
-        nd = row_of_lane(d, __ffsll((long long)m) - 1);
-        load_row<QW, VL>(p, nd, rn);
+    // rows of a series are in base order, so the in-range rows are the contiguous lanes
+    // [lo, hi] of this window
+    const int lo = __ffsll((long long)m) - 1, hi = 63 - __clzll((long long)m);
+    last_base = (uint32_t)__builtin_amdgcn_readlane((int)d.base, hi);
+    const int nin = hi - lo + 1;
+    // D-deep ring, shifted by one row per step: ring[0] is row t, ring[1 .. D-1] rows
+    // t+1 .. t+D-1 in flight
+    RawT<QW, VL> ring[D];
+    RowLite rl[D];
+#pragma unroll
+    for (int u = 0; u < D; u++) {
+      ring[u] = {};
+      if (u < D - 1 && u < nin) {
+        rl[u] = row_of_lane(d, lo + u);
+        load_row<QW, VL>(p, rl[u], ring[u]);
       }
-      const RowGeom g = row_geom(p, cd.base);
-      int slot[DPL];
-      double val[DPL];
-      const bool ok = decode_row<QW, VL>(p, cd, g, rc, slot, val);
-      if (__ballot(!ok)) {
+    }
+    for (int t = 0; t < nin; t++) {
+      if (t + D - 1 < nin) {
+        rl[D - 1] = row_of_lane(d, lo + t + D - 1);
+        load_row<QW, VL>(p, rl[D - 1], ring[D - 1]);
+      }
+      if (!pct_row<QW, VL>(p, rl[0], ring[0], q, dense, pres)) {
         if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)s;
         return;
       }
-      uint32_t left = 0;
 #pragma unroll
-      for (int j = 0; j < DPL; j++) left |= (slot[j] >= 0 ? 1u : 0u) << j;
-      for (;;) {
-        int mn = INT32_MAX;
-#pragma unroll
-        for (int j = 0; j < DPL; j++) if ((left >> j) & 1) mn = min(mn, slot[j]);
-        mn = wave_min_dpp(mn);
-        if (mn == INT32_MAX) break;
-        uint32_t keep = 0;
-#pragma unroll
-        for (int j = 0; j < DPL; j++) {
-          if (((left >> j) & 1) && slot[j] == mn) {
-            left &= ~(1u << j);
-            if (!isnan(val[j])) keep |= 1u << j;
-          }
-        }
-        const int n = __builtin_amdgcn_readlane(wave_incl_sum_dpp(__popc(keep)), 63);
-        double x = (double)NAN;
-        if (n > 0) {
-          // select_sorted / select_extreme: LEGACY pos = p (n + 1)
-          const double pos = q * (double)(n + 1);
-          const int ip = (int)floor(pos);
-          int lo_i, hi_i;
-          if (pos < 1) { lo_i = hi_i = 0; }
-          else if (pos >= (double)n) { lo_i = hi_i = n - 1; }
-          else { lo_i = ip - 1; hi_i = ip; }
-          const int ktop = n - lo_i, kbot = hi_i + 1;
-          if (min(ktop, kbot) > EXT_MAX) {
-            if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)s;
-            return;
-          }
-          double a, b, ek, ek1;
-          if (ktop <= kbot) {
-            extract_masked<true>(val, keep, ktop, ek, ek1);
-            a = ek;
-            b = (hi_i == lo_i) ? ek : ek1;
-          } else {
-            extract_masked<false>(val, keep, kbot, ek, ek1);
-            b = ek;
-            a = (hi_i == lo_i) ? ek : ek1;
-          }
-          x = (lo_i == hi_i) ? a : a + (pos - floor(pos)) * (b - a);
-        }
-        if (lane == 0) { dense[mn] = x; pres[mn] = 1; }
+      for (int u = 0; u < D - 1; u++) {
+        ring[u] = ring[u + 1];
+        rl[u] = rl[u + 1];
       }
-      if (!has_next) break;
-      cd = nd;
-      rc = rn;
     }
   }
 }
@@ -673,8 +737,15 @@ bool pct_rows_supported(int qw, int vl) { return (qw == 2 || qw == 4) && (vl == 
 hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s) {
   if (p.n_series == 0) return hipSuccess;
   const dim3 grid((unsigned)((p.n_series + 3) / 4)), block(256);
-#define PCT_ROWS_CASE(Q, V) \
-  if (qw == Q && vl == V) { hipLaunchKernelGGL((k_pct_rows<Q, V>), grid, block, 0, s, p); return hipGetLastError(); }
+  const char* denv = std::getenv("TSDBHIP_PCTD");
+  const int D = denv ? std::atoi(denv) : 3;
+#define PCT_ROWS_CASE(Q, V)                                                                                  \
+  if (qw == Q && vl == V) {                                                                                \
+    if (D == 2) hipLaunchKernelGGL((k_pct_rows<Q, V, 2>), grid, block, 0, s, p);                          \
+    else if (D == 4) hipLaunchKernelGGL((k_pct_rows<Q, V, 4>), grid, block, 0, s, p);                     \
+    else hipLaunchKernelGGL((k_pct_rows<Q, V, 3>), grid, block, 0, s, p);                                 \
+    return hipGetLastError();                                                                              \
+  }
   PCT_ROWS_CASE(2, 1) PCT_ROWS_CASE(2, 2) PCT_ROWS_CASE(2, 4) PCT_ROWS_CASE(2, 8)
   PCT_ROWS_CASE(4, 1) PCT_ROWS_CASE(4, 2) PCT_ROWS_CASE(4, 4) PCT_ROWS_CASE(4, 8)
 #undef PCT_ROWS_CASE
