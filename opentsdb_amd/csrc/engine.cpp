@@ -145,6 +145,9 @@ struct tsdbhip_ctx {
   DevBuf pa, pb, pn, pf, out_val, out_flag, gact, err, g_dense, g_pres, g_rate, redo, redo_n, redo2, redo2_n;
   DevBuf xbuf, gbuf;
   DevBuf pre_dense, pre_pres;          // percentile / median downsampling
+  DevBuf sel_vals, sel_sorted, sel_uni, sel_gsp, sel_beg, sel_end;   // percentile / median group-by
+  void* sel_tmp = nullptr;
+  size_t sel_tmp_bytes = 0;
   // raw path scratch
   DevBuf r_rowpt, r_spoff, r_spn, r_grp, r_pts, r_rank, r_bm, r_wb, r_U, r_ooff, r_sg, r_su, r_ots, r_obits, r_oint,
       r_coff, r_cur;                   // multi-GPU: this rank's partial states, gathered states
@@ -333,6 +336,8 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   for (auto& o : c->ro_out)
     for (DevBuf* b : {&o.series, &o.base, &o.qual, &o.voff, &o.val}) b->release();
   if (c->ro_tmp) (void)hipFree(c->ro_tmp);
+  for (DevBuf* b : {&c->sel_vals, &c->sel_sorted, &c->sel_uni, &c->sel_gsp, &c->sel_beg, &c->sel_end}) b->release();
+  if (c->sel_tmp) (void)hipFree(c->sel_tmp);
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -735,7 +740,11 @@ struct Plan {
   bool none = false;
   bool gslot = false;
   bool raw = false;   // no downsampling: AggregationIterator over the raw timestamp union
+  int gsel = 0;       // TSDB_AGG_* when the group-by aggregator is a percentile / median (0: none)
+  bool no_inf = false;   // per-span pass feeding the percentile group-by: no +-Inf check
 };
+
+bool is_sel_agg(int a) { return a == TSDB_AGG_MEDIAN || (a >= TSDB_AGG_P999 && a < TSDB_AGG_COUNT_ALL); }
 
 int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
   if (q->aggregator < 0 || q->aggregator >= TSDB_AGG_COUNT_ALL) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad aggregator");
@@ -743,6 +752,9 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
   if (q->ds_function == TSDB_AGG_NONE) return fail(TSDB_E_ILLEGAL_ARGUMENT, "cannot use the NONE aggregator for downsampling");
   if (q->ds_function < 0) {
     P.raw = true;
+    if (is_sel_agg(q->aggregator))
+      return fail(TSDB_E_NOT_IMPLEMENTED, std::string("percentile / median group-by without downsampling: ") +
+                                              AGG_NAMES[q->aggregator]);
     P.ga = ga_of(q->aggregator);
     if (P.ga < 0) return fail(TSDB_E_NOT_IMPLEMENTED, std::string("group-by aggregator not implemented yet: ") + AGG_NAMES[q->aggregator]);
     P.interp = interp_of(q->aggregator);
@@ -755,6 +767,10 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
   P.ga = ga_of(q->aggregator);
   P.f = f_of(q->ds_function);
   if (P.f < 0 && (q->ds_function == TSDB_AGG_MEDIAN || q->ds_function >= TSDB_AGG_P999)) P.f = F_SEL;
+  if (P.ga < 0 && is_sel_agg(q->aggregator)) {
+    P.gsel = q->aggregator;   // order statistics per (group, slot): run_sel_group
+    P.ga = GA_NONE;           // placeholder: no partial state is built for these
+  }
   if (P.ga < 0) return fail(TSDB_E_NOT_IMPLEMENTED, std::string("group-by aggregator not implemented yet: ") + AGG_NAMES[q->aggregator]);
   if (P.f < 0) return fail(TSDB_E_NOT_IMPLEMENTED, std::string("downsampling function not implemented yet: ") + AGG_NAMES[q->ds_function]);
   if ((q->flags & TSDB_QF_ORDERED) && (P.ga == GA_SUM || P.ga == GA_AVG || P.ga == GA_SQUARESUM || P.ga == GA_DEV || P.ga == GA_MULT))
@@ -896,7 +912,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     HIP_OK(hipMemcpyAsync(&nbig, c->redo_n.p, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
     HIP_OK(launch_pct(gp, 2, nbig, c->stream));
-    HIP_OK(launch_emit(gp, c->stream));
+    if (!P.gsel) HIP_OK(launch_emit(gp, c->stream));   // gsel: run_sel_group takes the bucket values
     HIP_OK(hipEventRecord(c->ev[1], c->stream));
   } else {
   // streaming kernel first (when the batch's row class and the query allow it), then the
@@ -1018,6 +1034,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     rp.out_val = c->out_val.as<double>();
     rp.out_flag = c->out_flag.as<uint8_t>();
     rp.err = c->err.as<int32_t>();
+    rp.no_inf = P.no_inf ? 1 : 0;
     HIP_OK(launch_reduce(rp, c->stream));
   }
   HIP_OK(hipEventRecord(c->ev[2], c->stream));
@@ -1119,6 +1136,125 @@ int assemble(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, c
 namespace {
 
 // Device timings of the last run (events recorded by run_device).
+// Percentile / median as the group-by aggregator (downsampled queries):
+//  1. every series' bucket values: k_pct for a percentile / median downsample function,
+//     else a NONE-aggregator pass without rate (= each span's Downsampler output);
+//  2. k_emit_vals: the SpanGroup contributions (rate, fill, LERP) into (group, slot) segments;
+//  3. segmented radix sort; 4. k_sel_group: runDouble's order statistic per (group, slot).
+int run_sel_group(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G) {
+  const int64_t S = c->n_series, K = P.K;
+  if (S * K > 0x7FFFFFFFLL) return fail(TSDB_E_NOT_IMPLEMENTED, "percentile group-by over more than 2^31 (series, slot) values");
+  HIP_OK(c->pre_dense.ensure(std::max<int64_t>(1, S * K) * 8));
+  HIP_OK(c->pre_pres.ensure(std::max<int64_t>(1, S * K)));
+  if (P.f == F_SEL) {
+    int rc = run_device(c, q, P, G, false);   // k_pct -> pre_dense / pre_pres (no k_emit)
+    if (rc) return rc;
+  } else {
+    tsdbhip_query q2 = *q;
+    q2.aggregator = TSDB_AGG_NONE;
+    q2.rate = 0;
+    q2.flags &= ~TSDB_QF_ORDERED;
+    Plan P2;
+    int rc = plan_query(c, &q2, P2);
+    if (rc) return rc;
+    P2.no_inf = true;
+    rc = run_device(c, &q2, P2, S, true);
+    if (rc) return rc;
+    if (S * K) {
+      HIP_OK(hipMemcpyAsync(c->pre_dense.p, c->out_val.p, S * K * 8, hipMemcpyDeviceToDevice, c->stream));
+      HIP_OK(hipMemcpyAsync(c->pre_pres.p, c->out_flag.p, S * K, hipMemcpyDeviceToDevice, c->stream));
+    }
+  }
+  // group -> first series (resident order is group-sorted)
+  std::vector<int64_t> gsp(G + 1, 0);
+  for (int64_t s = 0; s < S; s++) gsp[c->h_group[s] + 1]++;
+  for (int64_t g = 0; g < G; g++) gsp[g + 1] += gsp[g];
+  std::vector<int64_t> beg(std::max<int64_t>(1, G * K)), end(std::max<int64_t>(1, G * K));
+  for (int64_t g = 0; g < G; g++) {
+    const int64_t ng = gsp[g + 1] - gsp[g];
+    for (int64_t k = 0; k < K; k++) {
+      beg[g * K + k] = gsp[g] * K + k * ng;
+      end[g * K + k] = beg[g * K + k] + ng;
+    }
+  }
+  HIP_OK(c->sel_gsp.ensure((G + 1) * 8));
+  HIP_OK(c->sel_beg.ensure(std::max<int64_t>(1, G * K) * 8));
+  HIP_OK(c->sel_end.ensure(std::max<int64_t>(1, G * K) * 8));
+  HIP_OK(c->sel_vals.ensure(std::max<int64_t>(1, S * K) * 8));
+  HIP_OK(c->sel_sorted.ensure(std::max<int64_t>(1, S * K) * 8));
+  HIP_OK(c->sel_uni.ensure(std::max<int64_t>(1, G * K)));
+  HIP_OK(c->out_val.ensure(std::max<int64_t>(1, G * K) * 8));
+  HIP_OK(c->out_flag.ensure(std::max<int64_t>(1, G * K)));
+  HIP_OK(c->gact.ensure(std::max<int64_t>(1, G) * 4));
+  HIP_OK(hipMemcpyAsync(c->sel_gsp.p, gsp.data(), (G + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  if (G * K) {
+    HIP_OK(hipMemcpyAsync(c->sel_beg.p, beg.data(), G * K * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(c->sel_end.p, end.data(), G * K * 8, hipMemcpyHostToDevice, c->stream));
+  }
+  if (S * K) HIP_OK(hipMemsetD32Async((hipDeviceptr_t)c->sel_vals.p, 0x7FF87FF8, S * K * 2, c->stream));   // +NaN
+  HIP_OK(hipMemsetAsync(c->sel_uni.p, 0, std::max<int64_t>(1, G * K), c->stream));
+  HIP_OK(hipMemsetAsync(c->gact.p, 0, std::max<int64_t>(1, G) * 4, c->stream));
+  if (P.f != F_SEL) HIP_OK(hipEventRecord(c->ev[0], c->stream));
+  const int64_t nt = (int64_t)c->tb.size();
+  GridParams gp{};
+  gp.rows = c->rows.as<RowDesc>();
+  gp.series_row_ptr = c->srp.as<int64_t>();
+  gp.tile_begin = c->d_tb.as<int64_t>();
+  gp.tile_end = c->d_te.as<int64_t>();
+  gp.tile_group = c->d_tg.as<int32_t>();
+  gp.n_tiles = nt;
+  gp.ss = P.ss;
+  gp.se = P.se;
+  gp.B0 = P.B0;
+  gp.I = P.I;
+  gp.K = K;
+  gp.qs = q->start_time;
+  gp.qe = q->end_time;
+  gp.mode = P.mode;
+  gp.ga = P.ga;
+  gp.interp = P.interp;
+  gp.fill = q->ds_fill;
+  gp.rate = q->rate;
+  gp.counter = q->rate_counter;
+  gp.drop = q->rate_drop_resets;
+  gp.counter_max = q->rate_counter_max;
+  gp.reset_value = q->rate_reset_value;
+  gp.pre_dense = c->pre_dense.as<double>();
+  gp.pre_pres = c->pre_pres.as<uint8_t>();
+  gp.sel_vals = c->sel_vals.as<double>();
+  gp.sel_uni = c->sel_uni.as<uint8_t>();
+  gp.group_series_ptr = c->sel_gsp.as<int64_t>();
+  gp.group_active = c->gact.as<uint32_t>();
+  gp.err = c->err.as<int32_t>();
+  gp.wave_lds = q->rate ? (int32_t)align16(K * 8) : 16;
+  if (gp.wave_lds > 48 * 1024) {
+    HIP_OK(c->g_rate.ensure(std::max<int64_t>(1, nt * K) * 8));
+    gp.g_rate = c->g_rate.as<double>();
+    gp.wave_lds = 16;
+  }
+  gp.waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / gp.wave_lds));
+  HIP_OK(launch_emit_vals(gp, c->stream));
+  hipError_t e = sort_segments(c->sel_vals.as<double>(), c->sel_sorted.as<double>(), S * K, G * K,
+                               c->sel_beg.as<int64_t>(), c->sel_end.as<int64_t>(), &c->sel_tmp, &c->sel_tmp_bytes,
+                               c->stream);
+  if (e != hipSuccess) return fail(TSDB_E_HIP, std::string("segmented sort: ") + hipGetErrorString(e));
+  SelParams sp{};
+  sp.sorted = c->sel_sorted.as<double>();
+  sp.uni = c->sel_uni.as<uint8_t>();
+  sp.group_series_ptr = c->sel_gsp.as<int64_t>();
+  sp.G = G;
+  sp.K = K;
+  sp.fn = P.gsel;
+  sp.out_val = c->out_val.as<double>();
+  sp.out_flag = c->out_flag.as<uint8_t>();
+  sp.err = c->err.as<int32_t>();
+  HIP_OK(launch_sel_group(sp, c->stream));
+  HIP_OK(hipEventRecord(c->ev[1], c->stream));
+  HIP_OK(hipEventRecord(c->ev[2], c->stream));
+  c->fast_used = false;
+  return 0;
+}
+
 void record_timing(tsdbhip_ctx* c, const Plan& P, int32_t redo_n) {
   float t01 = 0, t12 = 0, t03 = 0;
   (void)hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
@@ -1430,6 +1566,11 @@ extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_resul
   if (rc) return rc;
   const int64_t G = P.none ? c->n_series : c->n_groups;
   if (P.raw) return run_raw(c, q, P, out);
+  if (P.gsel) {
+    rc = run_sel_group(c, q, P, G);
+    if (rc) return rc;
+    return collect(c, q, P, G, true, out);
+  }
   rc = run_device(c, q, P, G, true);
   if (rc) return rc;
   return collect(c, q, P, G, true, out);
@@ -1469,6 +1610,7 @@ int plan_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_globa
   if (rc) return rc;
   if (P.none) return fail(TSDB_E_NOT_IMPLEMENTED, "NONE aggregator is per-span; it has no cross-rank exchange");
   if (P.raw) return fail(TSDB_E_NOT_IMPLEMENTED, "multi-GPU raw (union LERP) queries are not implemented yet");
+  if (P.gsel) return fail(TSDB_E_NOT_IMPLEMENTED, "multi-GPU percentile / median group-by is not implemented yet");
   if (n_groups_global < c->n_groups) return fail(TSDB_E_ILLEGAL_ARGUMENT, "n_groups_global smaller than the local groups");
   return 0;
 }

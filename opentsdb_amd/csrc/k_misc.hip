@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceParams p) {
       p.state.f[o] = T.f;
     } else {
       const bool emit = (T.f & PF_UNION) != 0;
-      const double r = emit ? ps_final(p.ga, T, p.err) : 0.0;
+      const double r = emit ? ps_final(p.ga, T, p.err, !p.no_inf) : 0.0;
       p.out_val[o] = r;
       p.out_flag[o] = emit ? 1 : 0;
     }

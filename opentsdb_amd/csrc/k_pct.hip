@@ -12,6 +12,8 @@
 //            percentile uses commons-math3 3.4.1 LEGACY: pos = p (n + 1).
 //  * k_emit  one wave per tile: the bucket values -> SpanGroup contributions (LERP, fill,
 //            rate), exactly emit_series of k_grid, into tile partials for k_reduce.
+#include <hipcub/hipcub.hpp>
+
 #include "kcommon.h"
 
 #include <cstdlib>
@@ -733,6 +735,115 @@ hipError_t launch_pct(const GridParams& p, int pass, int64_t n, hipStream_t s) {
 }
 
 bool pct_rows_supported(int qw, int vl) { return (qw == 2 || qw == 4) && (vl == 1 || vl == 2 || vl == 4 || vl == 8); }
+
+// ---- percentile / median as the group-by aggregator ----------------------------------
+//
+// AggregationIterator feeds PercentileAgg.runDouble / Median.runDouble with one value per
+// span at every union timestamp (the span's bucket value, or its LERP between neighbouring
+// buckets; src/core/AggregationIterator.java:735-797), and runDouble drops NaNs
+// (src/core/Aggregators.java:689-706, :416-430).  k_emit_vals writes each series' value for
+// every slot into the (group, slot) segment (NaN = no value), a segmented sort orders the
+// segments, and k_sel_group takes the order statistic of the non-NaN prefix.
+
+__device__ __forceinline__ double canon_nan(double v) {
+  return isnan(v) ? __longlong_as_double(0x7FF8000000000000LL) : v;   // +NaN sorts after +Inf
+}
+
+// One wave per tile (<= 64 series of one group).
+__global__ __launch_bounds__(256) void k_emit_vals(GridParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t tile = (int64_t)blockIdx.x * p.waves + wave;
+  if (tile >= p.n_tiles) return;
+  const int K = (int)p.K;
+  const int32_t g = p.tile_group[tile];
+  const int64_t gs0 = p.group_series_ptr[g];
+  const int64_t ng = p.group_series_ptr[g + 1] - gs0;
+  double* seg = p.sel_vals + gs0 * K;
+  uint8_t* uni = p.sel_uni + (int64_t)g * K;
+  WaveLds W;
+  W.rate = !p.rate ? nullptr : (p.g_rate ? p.g_rate + tile * K : (double*)(smem + (int64_t)wave * p.wave_lds));
+  bool active = false;
+  for (int64_t s = p.tile_begin[tile]; s < p.tile_end[tile]; s++) {
+    bool any = false;
+    for (int64_t r = p.series_row_ptr[s]; r < p.series_row_ptr[s + 1]; r++) {
+      const uint32_t base = p.rows[r].base;
+      if ((int64_t)base >= p.ss && (int64_t)base < p.se) { any = true; break; }
+    }
+    if (!any) continue;
+    active = true;
+    W.dense = p.pre_dense + s * K;
+    W.pres = p.pre_pres + s * K;
+    const int64_t col = s - gs0;
+    emit_series_to(p, W, K, [&](int k, double v, bool u) {
+      seg[(int64_t)k * ng + col] = canon_nan(v);
+      if (u) uni[k] = 1;
+    });
+  }
+  if (active && lane_id() == 0) atomicOr(&p.group_active[g], 1u);
+}
+
+// One thread per (group, slot).
+__global__ __launch_bounds__(256) void k_sel_group(SelParams p) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.G * p.K) return;
+  if (!p.uni[i]) {
+    p.out_val[i] = 0.0;
+    p.out_flag[i] = 0;
+    return;
+  }
+  const int64_t g = i / p.K, k = i - g * p.K;
+  const int64_t gs0 = p.group_series_ptr[g], ng = p.group_series_ptr[g + 1] - gs0;
+  const double* v = p.sorted + gs0 * p.K + k * ng;
+  int64_t lo = 0, hi = ng;   // NaNs sort last: n = values before the first NaN
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (isnan(v[mid])) hi = mid; else lo = mid + 1;
+  }
+  const int n = (int)lo;
+  const double r = n == 0 ? (double)NAN : select_sorted(p.fn, n, [&](int j) { return v[j]; });
+  if (isinf(r)) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // AggregationIterator.doubleValue :640-643
+  p.out_val[i] = r;
+  p.out_flag[i] = 1;
+}
+
+hipError_t launch_emit_vals(const GridParams& p, hipStream_t s) {
+  if (p.n_tiles == 0) return hipSuccess;
+  const int64_t blocks = (p.n_tiles + p.waves - 1) / p.waves;
+  const size_t lds = (size_t)p.wave_lds * p.waves;
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_emit_vals, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_emit_vals, dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_sel_group(const SelParams& p, hipStream_t s) {
+  const int64_t n = p.G * p.K;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sel_group, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t sort_segments(const double* in, double* out, int64_t n_items, int64_t n_seg, const int64_t* d_begin,
+                         const int64_t* d_end, void** tmp, size_t* tmp_bytes, hipStream_t s) {
+  if (n_items == 0 || n_seg == 0) return hipSuccess;
+  size_t need = 0;
+  hipError_t e = hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, need, in, out, (int)n_items, (int)n_seg,
+                                                            d_begin, d_end, 0, 64, s);
+  if (e != hipSuccess) return e;
+  if (need > *tmp_bytes) {
+    if (*tmp) (void)hipFree(*tmp);
+    *tmp = nullptr;
+    *tmp_bytes = 0;
+    e = hipMalloc(tmp, need);
+    if (e != hipSuccess) return e;
+    *tmp_bytes = need;
+  }
+  return hipcub::DeviceSegmentedRadixSort::SortKeys(*tmp, need, in, out, (int)n_items, (int)n_seg, d_begin, d_end,
+                                                    0, 64, s);
+}
 
 hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s) {
   if (p.n_series == 0) return hipSuccess;

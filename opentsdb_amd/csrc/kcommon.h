@@ -863,9 +863,10 @@ __device__ __forceinline__ void slow_chunk(const WaveLds& W, SeriesState& st, co
 }
 
 // ---- series -> SpanGroup contributions over the K slots -----------------------------
-__device__ __forceinline__ void emit_series(const GridParams& p, const WaveLds& W, int K) {
+// put(slot, value, union) receives each contribution of the series, at most one per slot.
+template <class Put>
+__device__ __forceinline__ void emit_series_to(const GridParams& p, const WaveLds& W, int K, Put&& put) {
   const int lane = lane_id();
-  const int ga = p.ga;
   const double fillv = (p.fill == TSDB_FILL_ZERO) ? 0.0 : (double)NAN;
   WAVE_SYNC();
   if (!p.rate) {
@@ -874,7 +875,7 @@ __device__ __forceinline__ void emit_series(const GridParams& p, const WaveLds& 
       for (int k = lane; k < K; k += 64) {
         const bool pr = W.pres[k] != 0;
         if (!pr && p.fill == TSDB_FILL_SCALAR) set_err(p.err, TSDB_E_RUNTIME);
-        contribute(ga, W.part, k, pr ? W.dense[k] : fillv, true);
+        put(k, pr ? W.dense[k] : fillv, true);
       }
     } else {
       int prev_present = -1;
@@ -889,9 +890,9 @@ __device__ __forceinline__ void emit_series(const GridParams& p, const WaveLds& 
           const double v = W.dense[k];
           if (pp >= 0 && pp < k - 1) {
             const double y0 = W.dense[pp];
-            for (int s2 = pp + 1; s2 < k; s2++) contribute(ga, W.part, s2, interp(p.interp, p, pp, y0, k, v, s2), false);
+            for (int s2 = pp + 1; s2 < k; s2++) put(s2, interp(p.interp, p, pp, y0, k, v, s2), false);
           }
-          contribute(ga, W.part, k, v, true);
+          put(k, v, true);
         }
         prev_present = max(prev_present, lane_bcast(incl, 63));
       }
@@ -947,12 +948,12 @@ __device__ __forceinline__ void emit_series(const GridParams& p, const WaveLds& 
       if (sv) {
         if (m == 1) {
           const double r0 = W.rate[ps];
-          for (int s2 = 0; s2 < k; s2++) contribute(ga, W.part, s2, r0, false);
-          contribute(ga, W.part, k, r, true);
+          for (int s2 = 0; s2 < k; s2++) put(s2, r0, false);
+          put(k, r, true);
         } else if (m >= 2) {
           const double rp = W.rate[ps];
-          for (int s2 = ps + 1; s2 < k; s2++) contribute(ga, W.part, s2, rp, false);
-          contribute(ga, W.part, k, r, true);
+          for (int s2 = ps + 1; s2 < k; s2++) put(s2, rp, false);
+          put(k, r, true);
         }
       }
       prev_item = max(prev_item, lane_bcast(iincl, 63));
@@ -962,6 +963,11 @@ __device__ __forceinline__ void emit_series(const GridParams& p, const WaveLds& 
     }
   }
   WAVE_SYNC();
+}
+
+__device__ __forceinline__ void emit_series(const GridParams& p, const WaveLds& W, int K) {
+  const int ga = p.ga;
+  emit_series_to(p, W, K, [&](int s, double v, bool uni) { contribute(ga, W.part, s, v, uni); });
 }
 
 // emit_series for K <= 64 without rate: lane k owns slot k; the series' bucket k arrives
@@ -1986,7 +1992,7 @@ __device__ __forceinline__ PState ps_merge(int ga, PState A, const PState& B) {
 }
 
 // Aggregator.runDouble results (see bs_final) + AggregationIterator.doubleValue's Inf check
-__device__ __forceinline__ double ps_final(int ga, const PState& s, int32_t* err) {
+__device__ __forceinline__ double ps_final(int ga, const PState& s, int32_t* err, bool chk_inf = true) {
   double r;
   switch (ga) {
     case GA_SUM: case GA_SQUARESUM: r = s.n == 0 ? (double)NAN : s.a; break;
@@ -2003,7 +2009,7 @@ __device__ __forceinline__ double ps_final(int ga, const PState& s, int32_t* err
     case GA_DIFF: r = !(s.f & PF_HAS) ? (double)NAN : (s.n == 0 ? 0.0 : s.b - s.a); break;
     default: r = NAN;
   }
-  if (isinf(r)) set_err(err, TSDB_E_ILLEGAL_STATE);
+  if (chk_inf && isinf(r)) set_err(err, TSDB_E_ILLEGAL_STATE);
   return r;
 }
 

@@ -1,0 +1,125 @@
+"""GPU parity of percentiles / median as the GROUP-BY aggregator:
+AggregationIterator hands PercentileAgg.runDouble / Median.runDouble one value per span at
+each union timestamp -- the span's bucket value or its LERP between neighbouring buckets
+(src/core/AggregationIterator.java:735-797) -- and runDouble drops NaNs and always uses
+LEGACY estimation (src/core/Aggregators.java:689-706; Median :416-430).  Downsampled
+queries only: the engine refuses them without a downsampler (NOT_IMPLEMENTED).
+
+Results are order statistics of exactly computed per-series values (plus commons-math3's
+`lower + d * (upper - lower)`), so the bar is bit-exact against the oracle."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from opentsdb_amd import abi, synth
+from opentsdb_amd.query import TsdbQuery
+from oracle import oracle as O
+from tests.test_gpu_parity import assert_groups_match
+
+pytestmark = pytest.mark.gpu
+
+T0 = 1356998400
+GSEL = ["p999", "p99", "p95", "p90", "p75", "p50", "ep99r3", "ep99r7", "median"]
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from opentsdb_amd.engine import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def mixed_batch():
+    return synth.generate(70, T0, 720, 5000, value_kind=2, n_groups=3, int_mod=30000, seed=11)
+
+
+@pytest.mark.parametrize("agg", GSEL)
+def test_pct_group_aggregators(eng, mixed_batch, agg):
+    q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+    assert_groups_match(eng.run_batch(mixed_batch, q), O.run_query(mixed_batch, q), agg, tol=0.0, ctx=agg)
+
+
+@pytest.mark.parametrize("ds", ["sum", "max", "min", "count", "dev", "first", "p99", "median"])
+def test_pct_group_over_downsample_functions(eng, mixed_batch, ds):
+    q = abi.new_query(T0, T0 + 3599, "p95", ds_function=abi.AGG[ds], ds_interval_ms=300000)
+    assert_groups_match(eng.run_batch(mixed_batch, q), O.run_query(mixed_batch, q), "p95", tol=0.0, ctx=ds)
+
+
+def test_pct_group_single_group_many_series(eng):
+    # one group of 300 series: segments longer than a wave, ties between integer series
+    b = synth.generate(300, T0, 360, 10000, value_kind=1, n_groups=1, int_mod=50, seed=3)
+    for agg in ["p99", "p50", "median", "p999"]:
+        q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["max"], ds_interval_ms=60000)
+        assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), agg, tol=0.0, ctx=agg)
+
+
+@pytest.mark.parametrize("fill", [abi.FILL_NAN, abi.FILL_ZERO, abi.FILL_NULL])
+def test_pct_group_fill(eng, fill):
+    b = synth.generate(20, T0 + 1800, 200, 10000, value_kind=2, n_groups=2, int_mod=1000, seed=4)
+    q = abi.new_query(T0, T0 + 7199, "p90", ds_function=abi.AGG["avg"], ds_interval_ms=300000, ds_fill=fill)
+    assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "p90", tol=0.0, ctx=f"fill {fill}")
+
+
+@pytest.mark.parametrize("opts", [dict(), dict(counter=True), dict(counter=True, drop_resets=True)])
+def test_pct_group_rate(eng, opts):
+    b = synth.generate(24, T0, 360, 10000, value_kind=1, n_groups=3, int_mod=1000, seed=9)
+    for ds in ["avg", "p75"]:
+        q = abi.new_query(T0, T0 + 3599, "p50", ds_function=abi.AGG[ds], ds_interval_ms=60000, rate=True, **opts)
+        assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "p50", tol=0.0, ctx=f"{ds} {opts}")
+
+
+def test_pct_group_all(eng, mixed_batch):
+    q = abi.new_query(T0 * 1000, (T0 + 3600) * 1000, "p75", ds_function=abi.AGG["sum"], ds_all=True)
+    assert_groups_match(eng.run_batch(mixed_batch, q), O.run_query(mixed_batch, q), "p75", tol=0.0, ctx="all")
+
+
+def test_pct_group_sparse_lerp(eng):
+    """Series with missing buckets and different extents: LERP-interpolated members."""
+    rng = np.random.default_rng(17)
+    from opentsdb_amd.store import MockStore
+    st = MockStore()
+    for s in range(40):
+        ts = np.sort(rng.choice(np.arange(0, 7200, 7), size=rng.integers(3, 150), replace=False))
+        for t in ts:
+            if s % 3 == 0:
+                st.add_float("m", T0 + int(t), float(rng.normal(10, 5)), {"h": f"h{s}", "g": f"g{s % 3}"})
+            else:
+                st.add_long("m", T0 + int(t), int(rng.integers(-1000, 1000)), {"h": f"h{s}", "g": f"g{s % 3}"})
+    for agg in ["p99", "p50", "median", "ep90r7"]:
+        q = TsdbQuery(st, runner=eng.run_batch)
+        q.setStartTime(T0)
+        q.setEndTime(T0 + 7199)
+        q.setTimeSeries("m", {"g": "*"}, agg, False)
+        q.downsample("2m-avg")
+        batch, _ = q.build_batch()
+        assert_groups_match(eng.run_batch(batch, q.to_abi()), O.run_query(batch, q.to_abi()), agg, tol=0.0, ctx=agg)
+
+
+def test_pct_group_nan_members(eng):
+    """Buckets of NaNs (present, value NaN) are dropped by runDouble; a slot whose members
+    are all NaN yields NaN."""
+    rng = np.random.default_rng(5)
+    rows, gids = [], []
+    for s in range(12):
+        ts = T0 * 1000 + np.sort(rng.choice(np.arange(0, 3600), 300, replace=False)) * 1000
+        f = rng.normal(0, 10, 300)
+        f[rng.random(300) < 0.2] = np.nan
+        if s in (3, 4, 5):
+            f[:] = np.nan
+        kind = np.full(300, 2)
+        rows.append(synth.encode_rows(ts, np.zeros(300, np.int64), f, kind, np.zeros(300, bool)))
+        gids.append(0 if s < 6 else 1)
+    b = synth.from_series(rows, gids)
+    for agg in ["p90", "median"]:
+        q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["max"], ds_interval_ms=600000)
+        assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), agg, tol=0.0, ctx=agg)
+
+
+def test_pct_group_without_downsampling_not_implemented(eng, mixed_batch):
+    q = abi.new_query(T0, T0 + 3599, "p99")
+    with pytest.raises(Exception) as ei:
+        eng.run_batch(mixed_batch, q)
+    assert "notimplemented" in str(ei.value).lower().replace(" ", "")
