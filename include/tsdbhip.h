@@ -210,6 +210,35 @@ int tsdbhip_run_partials(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_gro
 /* Merges n_ranks rank-ordered partial buffers (device or host memory) and builds the result. */
 int tsdbhip_finalize(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_global,
                      const void* partials, int n_ranks, tsdbhip_result** out);
+/* ---- multi-GPU percentile / median group-by (non-decomposable) ---------------
+ * PercentileAgg / Median have no mergeable partial state (src/core/Aggregators.java:397-431,
+ * 657-708), so every span's value per (group, slot) travels to the group's owning rank
+ * (SURVEY.md 8e).  Per query, on every rank:
+ *   1. tsdbhip_sel_layout: counts[g] = local spans of group g (n_groups_global entries),
+ *      n_slots = K;
+ *   2. tsdbhip_sel_run_values: the local spans' contributions (Downsampler, RateSpan, fill,
+ *      LERP -- what AggregationIterator hands runDouble) into
+ *        double  vals[sum_g counts[g] * K]   group g at K * sum_{g'<g} counts[g'], then
+ *                                            [k][i] (slot-major, i = span index; +NaN = none)
+ *        uint8_t uni[n_groups * K]           a real point of some span (emit flag)
+ *        uint32_t act[n_groups]              the group has a span in the scan range;
+ *   3. the caller moves each group's blocks to its owner (all-to-all over RCCL) and
+ *      concatenates them per slot, OR-reduces uni / act;
+ *   4. tsdbhip_sel_select on the owner: same layout with the gathered counts, segments
+ *      sorted and runDouble's order statistic taken -> dense out_val [n_groups * K] f64 and
+ *      out_flag [n_groups * K] u8 (groups with count 0: NaN where uni is set);
+ *   5. after the owners' rows are combined, tsdbhip_assemble builds the usual result.
+ * All buffer pointers may be device or host memory. */
+int tsdbhip_sel_layout(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_global, int64_t* counts,
+                       int64_t* n_slots);
+int tsdbhip_sel_run_values(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_global, void* vals,
+                           void* uni, void* act);
+int tsdbhip_sel_select(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_global, const void* vals,
+                       const int64_t* counts, const void* uni, void* out_val, void* out_flag);
+/* Result of a downsampled group-by from dense per-(group, slot) values, emit flags and
+ * group-active flags (layouts as tsdbhip_sel_select / tsdbhip_sel_run_values). */
+int tsdbhip_assemble(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_global, const void* val,
+                     const void* flag, const void* act, tsdbhip_result** out);
 /* ---- rollup generation --------------------------------
  * RollupInterval (src/rollup/RollupInterval.java:62-240): `interval` e.g. "1h", `row_span`
  * e.g. "1d"; validateAndCompile's checks and arithmetic, IllegalArgumentException ->

@@ -1141,7 +1141,23 @@ namespace {
 //     else a NONE-aggregator pass without rate (= each span's Downsampler output);
 //  2. k_emit_vals: the SpanGroup contributions (rate, fill, LERP) into (group, slot) segments;
 //  3. segmented radix sort; 4. k_sel_group: runDouble's order statistic per (group, slot).
-int run_sel_group(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G) {
+// Group -> first value of its segments in the [g][k][i] layout: prefix of `counts`.
+std::vector<int64_t> seg_ptr(const std::vector<int64_t>& counts) {
+  std::vector<int64_t> gsp(counts.size() + 1, 0);
+  for (size_t g = 0; g < counts.size(); g++) gsp[g + 1] = gsp[g] + counts[g];
+  return gsp;
+}
+
+// local series per group id g < G (resident order is group-sorted)
+std::vector<int64_t> local_counts(tsdbhip_ctx* c, int64_t G) {
+  std::vector<int64_t> n(G, 0);
+  for (int64_t s = 0; s < c->n_series; s++) n[c->h_group[s]]++;
+  return n;
+}
+
+// Stages 1-2 of the percentile / median group-by: every local span's contribution to each
+// (group, slot) into c->sel_vals ([g][k][i], NaN = none), c->sel_uni [G][K], c->gact [G].
+int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G) {
   const int64_t S = c->n_series, K = P.K;
   if (S * K > 0x7FFFFFFFLL) return fail(TSDB_E_NOT_IMPLEMENTED, "percentile group-by over more than 2^31 (series, slot) values");
   HIP_OK(c->pre_dense.ensure(std::max<int64_t>(1, S * K) * 8));
@@ -1165,36 +1181,15 @@ int run_sel_group(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t
       HIP_OK(hipMemcpyAsync(c->pre_pres.p, c->out_flag.p, S * K, hipMemcpyDeviceToDevice, c->stream));
     }
   }
-  // group -> first series (resident order is group-sorted)
-  std::vector<int64_t> gsp(G + 1, 0);
-  for (int64_t s = 0; s < S; s++) gsp[c->h_group[s] + 1]++;
-  for (int64_t g = 0; g < G; g++) gsp[g + 1] += gsp[g];
-  std::vector<int64_t> beg(std::max<int64_t>(1, G * K)), end(std::max<int64_t>(1, G * K));
-  for (int64_t g = 0; g < G; g++) {
-    const int64_t ng = gsp[g + 1] - gsp[g];
-    for (int64_t k = 0; k < K; k++) {
-      beg[g * K + k] = gsp[g] * K + k * ng;
-      end[g * K + k] = beg[g * K + k] + ng;
-    }
-  }
+  const std::vector<int64_t> gsp = seg_ptr(local_counts(c, G));
   HIP_OK(c->sel_gsp.ensure((G + 1) * 8));
-  HIP_OK(c->sel_beg.ensure(std::max<int64_t>(1, G * K) * 8));
-  HIP_OK(c->sel_end.ensure(std::max<int64_t>(1, G * K) * 8));
   HIP_OK(c->sel_vals.ensure(std::max<int64_t>(1, S * K) * 8));
-  HIP_OK(c->sel_sorted.ensure(std::max<int64_t>(1, S * K) * 8));
   HIP_OK(c->sel_uni.ensure(std::max<int64_t>(1, G * K)));
-  HIP_OK(c->out_val.ensure(std::max<int64_t>(1, G * K) * 8));
-  HIP_OK(c->out_flag.ensure(std::max<int64_t>(1, G * K)));
   HIP_OK(c->gact.ensure(std::max<int64_t>(1, G) * 4));
   HIP_OK(hipMemcpyAsync(c->sel_gsp.p, gsp.data(), (G + 1) * 8, hipMemcpyHostToDevice, c->stream));
-  if (G * K) {
-    HIP_OK(hipMemcpyAsync(c->sel_beg.p, beg.data(), G * K * 8, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(c->sel_end.p, end.data(), G * K * 8, hipMemcpyHostToDevice, c->stream));
-  }
   if (S * K) HIP_OK(hipMemsetD32Async((hipDeviceptr_t)c->sel_vals.p, 0x7FF87FF8, S * K * 2, c->stream));   // +NaN
   HIP_OK(hipMemsetAsync(c->sel_uni.p, 0, std::max<int64_t>(1, G * K), c->stream));
   HIP_OK(hipMemsetAsync(c->gact.p, 0, std::max<int64_t>(1, G) * 4, c->stream));
-  if (P.f != F_SEL) HIP_OK(hipEventRecord(c->ev[0], c->stream));
   const int64_t nt = (int64_t)c->tb.size();
   GridParams gp{};
   gp.rows = c->rows.as<RowDesc>();
@@ -1234,13 +1229,41 @@ int run_sel_group(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t
   }
   gp.waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / gp.wave_lds));
   HIP_OK(launch_emit_vals(gp, c->stream));
-  hipError_t e = sort_segments(c->sel_vals.as<double>(), c->sel_sorted.as<double>(), S * K, G * K,
-                               c->sel_beg.as<int64_t>(), c->sel_end.as<int64_t>(), &c->sel_tmp, &c->sel_tmp_bytes,
-                               c->stream);
+  c->fast_used = false;
+  return 0;
+}
+
+// Stages 3-4: sort the (group, slot) segments of `vals` (device, [g][k][i], counts[g] values
+// per slot of group g) and take each order statistic -> c->out_val / c->out_flag [G][K].
+int sel_select(tsdbhip_ctx* c, const Plan& P, int64_t G, double* vals, const std::vector<int64_t>& counts,
+               const uint8_t* uni) {
+  const int64_t K = P.K;
+  const std::vector<int64_t> gsp = seg_ptr(counts);
+  const int64_t n_items = gsp[G] * K;
+  if (n_items > 0x7FFFFFFFLL) return fail(TSDB_E_NOT_IMPLEMENTED, "percentile group-by over more than 2^31 values");
+  std::vector<int64_t> beg(std::max<int64_t>(1, G * K)), end(std::max<int64_t>(1, G * K));
+  for (int64_t g = 0; g < G; g++)
+    for (int64_t k = 0; k < K; k++) {
+      beg[g * K + k] = gsp[g] * K + k * counts[g];
+      end[g * K + k] = beg[g * K + k] + counts[g];
+    }
+  HIP_OK(c->sel_gsp.ensure((G + 1) * 8));
+  HIP_OK(c->sel_beg.ensure(std::max<int64_t>(1, G * K) * 8));
+  HIP_OK(c->sel_end.ensure(std::max<int64_t>(1, G * K) * 8));
+  HIP_OK(c->sel_sorted.ensure(std::max<int64_t>(1, n_items) * 8));
+  HIP_OK(c->out_val.ensure(std::max<int64_t>(1, G * K) * 8));
+  HIP_OK(c->out_flag.ensure(std::max<int64_t>(1, G * K)));
+  HIP_OK(hipMemcpyAsync(c->sel_gsp.p, gsp.data(), (G + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  if (G * K) {
+    HIP_OK(hipMemcpyAsync(c->sel_beg.p, beg.data(), G * K * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(c->sel_end.p, end.data(), G * K * 8, hipMemcpyHostToDevice, c->stream));
+  }
+  hipError_t e = sort_segments(vals, c->sel_sorted.as<double>(), n_items, G * K, c->sel_beg.as<int64_t>(),
+                               c->sel_end.as<int64_t>(), &c->sel_tmp, &c->sel_tmp_bytes, c->stream);
   if (e != hipSuccess) return fail(TSDB_E_HIP, std::string("segmented sort: ") + hipGetErrorString(e));
   SelParams sp{};
   sp.sorted = c->sel_sorted.as<double>();
-  sp.uni = c->sel_uni.as<uint8_t>();
+  sp.uni = uni;
   sp.group_series_ptr = c->sel_gsp.as<int64_t>();
   sp.G = G;
   sp.K = K;
@@ -1249,9 +1272,21 @@ int run_sel_group(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t
   sp.out_flag = c->out_flag.as<uint8_t>();
   sp.err = c->err.as<int32_t>();
   HIP_OK(launch_sel_group(sp, c->stream));
+  return 0;
+}
+
+// Percentile / median as the group-by aggregator (downsampled queries):
+//  1. every series' bucket values: k_pct for a percentile / median downsample function,
+//     else a NONE-aggregator pass without rate (= each span's Downsampler output);
+//  2. k_emit_vals: the SpanGroup contributions (rate, fill, LERP) into (group, slot) segments;
+//  3. segmented radix sort; 4. k_sel_group: runDouble's order statistic per (group, slot).
+int run_sel_group(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G) {
+  int rc = sel_values(c, q, P, G);
+  if (rc) return rc;
+  rc = sel_select(c, P, G, c->sel_vals.as<double>(), local_counts(c, G), c->sel_uni.as<uint8_t>());
+  if (rc) return rc;
   HIP_OK(hipEventRecord(c->ev[1], c->stream));
   HIP_OK(hipEventRecord(c->ev[2], c->stream));
-  c->fast_used = false;
   return 0;
 }
 
@@ -1707,6 +1742,113 @@ extern "C" int tsdbhip_finalize(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t 
   mp.out_act = c->gact.as<uint32_t>();
   mp.err = c->err.as<int32_t>();
   HIP_OK(launch_rank_merge(mp, c->stream));
+  return collect(c, q, P, G, false, out);
+}
+
+// ---------------------------------------------------------------------------
+// multi-GPU percentile / median group-by: values go to the group's owning rank
+// ---------------------------------------------------------------------------
+namespace {
+
+int plan_sel(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, Plan& P) {
+  int rc = plan_query(c, q, P);
+  if (rc) return rc;
+  if (!P.gsel) return fail(TSDB_E_ILLEGAL_ARGUMENT, "not a percentile / median group-by query");
+  if (n_groups_global < c->n_groups) return fail(TSDB_E_ILLEGAL_ARGUMENT, "n_groups_global smaller than the local groups");
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int tsdbhip_sel_layout(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, int64_t* counts,
+                                  int64_t* n_slots) {
+  if (!c || !q || !counts || !n_slots) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  Plan P;
+  int rc = plan_sel(c, q, n_groups_global, P);
+  if (rc) return rc;
+  const std::vector<int64_t> n = local_counts(c, n_groups_global);
+  for (int64_t g = 0; g < n_groups_global; g++) counts[g] = n[g];
+  *n_slots = P.K;
+  return 0;
+}
+
+extern "C" int tsdbhip_sel_run_values(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, void* vals,
+                                      void* uni, void* act) {
+  if (!c || !q || !vals || !uni || !act) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  Plan P;
+  int rc = plan_sel(c, q, n_groups_global, P);
+  if (rc) return rc;
+  const int64_t G = n_groups_global, K = P.K;
+  HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
+  rc = sel_values(c, q, P, G);
+  if (rc) return rc;
+  const int64_t n = c->n_series * K;
+  if (n) HIP_OK(hipMemcpyAsync(vals, c->sel_vals.p, n * 8, hipMemcpyDefault, c->stream));
+  if (G * K) HIP_OK(hipMemcpyAsync(uni, c->sel_uni.p, G * K, hipMemcpyDefault, c->stream));
+  if (G) HIP_OK(hipMemcpyAsync(act, c->gact.p, G * 4, hipMemcpyDefault, c->stream));
+  int32_t err = 0;
+  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  if (err) return fail(err, "error raised by the device path");
+  return 0;
+}
+
+extern "C" int tsdbhip_sel_select(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, const void* vals,
+                                  const int64_t* counts, const void* uni, void* out_val, void* out_flag) {
+  if (!c || !q || !counts || !uni || !out_val || !out_flag) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  Plan P;
+  int rc = plan_sel(c, q, n_groups_global, P);
+  if (rc) return rc;
+  const int64_t G = n_groups_global, K = P.K;
+  std::vector<int64_t> cnt(counts, counts + G);
+  int64_t n = 0;
+  for (int64_t g = 0; g < G; g++) {
+    if (cnt[g] < 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "negative count");
+    n += cnt[g] * K;
+  }
+  if (n && !vals) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null vals");
+  HIP_OK(c->sel_vals.ensure(std::max<int64_t>(1, n) * 8));
+  HIP_OK(c->sel_uni.ensure(std::max<int64_t>(1, G * K)));
+  if (n) HIP_OK(hipMemcpyAsync(c->sel_vals.p, vals, n * 8, hipMemcpyDefault, c->stream));
+  if (G * K) HIP_OK(hipMemcpyAsync(c->sel_uni.p, uni, G * K, hipMemcpyDefault, c->stream));
+  HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
+  rc = sel_select(c, P, G, c->sel_vals.as<double>(), cnt, c->sel_uni.as<uint8_t>());
+  if (rc) return rc;
+  if (G * K) {
+    HIP_OK(hipMemcpyAsync(out_val, c->out_val.p, G * K * 8, hipMemcpyDefault, c->stream));
+    HIP_OK(hipMemcpyAsync(out_flag, c->out_flag.p, G * K, hipMemcpyDefault, c->stream));
+  }
+  int32_t err = 0;
+  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  if (err) return fail(err, "error raised by the device path");
+  return 0;
+}
+
+extern "C" int tsdbhip_assemble(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, const void* val,
+                                const void* flag, const void* act, tsdbhip_result** out) {
+  if (!c || !q || !val || !flag || !act || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  *out = nullptr;
+  HIP_OK(hipSetDevice(c->device));
+  Plan P;
+  int rc = plan_query(c, q, P);
+  if (rc) return rc;
+  if (P.raw || P.none) return fail(TSDB_E_ILLEGAL_ARGUMENT, "assemble takes downsampled group-by queries");
+  const int64_t G = n_groups_global, K = P.K;
+  HIP_OK(c->out_val.ensure(std::max<int64_t>(1, G * K) * 8));
+  HIP_OK(c->out_flag.ensure(std::max<int64_t>(1, G * K)));
+  HIP_OK(c->gact.ensure(std::max<int64_t>(1, G) * 4));
+  HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
+  if (G * K) {
+    HIP_OK(hipMemcpyAsync(c->out_val.p, val, G * K * 8, hipMemcpyDefault, c->stream));
+    HIP_OK(hipMemcpyAsync(c->out_flag.p, flag, G * K, hipMemcpyDefault, c->stream));
+  }
+  if (G) HIP_OK(hipMemcpyAsync(c->gact.p, act, G * 4, hipMemcpyDefault, c->stream));
   return collect(c, q, P, G, false, out);
 }
 

@@ -98,3 +98,116 @@ def run_distributed(eng, q: abi.Query, dist, n_groups_global: int, device=None):
     if on_gpu:
         torch.cuda.current_stream(dev).synchronize()
     return eng.finalize(q, n_groups_global, gathered.data_ptr(), world)
+
+
+# ---- percentile / median as the group-by aggregator: values to the owning rank --------
+#
+# PercentileAgg / Median.runDouble need every span's value of a (group, slot) at once
+# (src/core/Aggregators.java:397-431, 657-708): there is no partial state to all-gather.
+# Group g is owned by rank g % world; every rank sends its spans' contributions of g to
+# that rank (one all-to-all over RCCL), the owner sorts and selects, and the owners' dense
+# rows are all-gathered (G x K x 9 B) so every rank can build the full result.
+
+def sel_owner(n_groups: int, world: int):
+    return np.arange(n_groups) % world
+
+
+def sel_pack(vals, counts, K: int, world: int):
+    """This rank's [g][k][i] contribution buffer reordered by owning rank.
+
+    Returns (send, in_splits): `send` holds, for owner 0, 1, ..., the blocks of the groups
+    it owns in increasing group order; in_splits[o] is the element count for owner o."""
+    import torch
+    counts = np.asarray(counts, np.int64)
+    off = np.concatenate([[0], np.cumsum(counts * K)])
+    own = sel_owner(len(counts), world)
+    pieces, splits = [], []
+    for o in range(world):
+        gs = np.nonzero(own == o)[0]
+        splits.append(int(sum(counts[g] * K for g in gs)))
+        pieces += [vals[int(off[g]):int(off[g + 1])] for g in gs if counts[g]]
+    send = torch.cat(pieces) if pieces else vals[:0]
+    return send, splits
+
+
+def sel_unpack(recv, counts_all, K: int, me: int):
+    """The owner's side: `recv` holds, per source rank r (in rank order), r's blocks of the
+    groups `me` owns ([K][n_rg] each, increasing g).  Returns (vals, seg_counts): per owned
+    group the slots' values of every rank side by side ([g][k][j], j over all ranks' spans),
+    and the per-group span counts (0 for groups owned elsewhere)."""
+    import torch
+    counts_all = np.asarray(counts_all, np.int64)
+    world, G = counts_all.shape
+    own = sel_owner(G, world)
+    mine = np.nonzero(own == me)[0]
+    blocks = {}
+    pos = 0
+    for r in range(world):
+        for g in mine:
+            n = int(counts_all[r, g])
+            if n:
+                blocks.setdefault(int(g), []).append(recv[pos:pos + n * K].reshape(K, n))
+                pos += n * K
+    seg = np.zeros(G, np.int64)
+    out = []
+    for g in mine:
+        if int(g) in blocks:
+            b = torch.cat(blocks[int(g)], dim=1)
+            seg[g] = b.shape[1]
+            out.append(b.reshape(-1))
+    vals = torch.cat(out) if out else recv[:0]
+    return vals, seg
+
+
+def sel_combine(rows_all, G: int, K: int, world: int):
+    """Row g of the dense [G][K] outputs from its owner (rows_all: [world, G * K])."""
+    own = sel_owner(G, world)
+    r = rows_all.reshape(world, G, K)
+    import torch
+    idx = torch.as_tensor(own, device=r.device)
+    return r[idx, torch.arange(G, device=r.device)].reshape(-1)
+
+
+def run_distributed_sel(eng, q: abi.Query, dist, n_groups_global: int, device=None):
+    """A percentile / median group-by query over the sharded store:
+    local contributions -> all-to-all to the owning ranks -> sort + select on the owners ->
+    all-gather of the owners' rows -> result on every rank."""
+    import torch
+
+    world, me = dist.get_world_size(), dist.get_rank()
+    on_gpu = dist.get_backend() == "nccl"
+    dev = device if on_gpu else "cpu"
+    G = n_groups_global
+    counts, K = eng.sel_layout(q, G)
+    vals = torch.empty(max(1, int(counts.sum()) * K), dtype=torch.float64, device=dev)
+    uni = torch.empty(max(1, G * K), dtype=torch.uint8, device=dev)
+    act = torch.empty(max(1, G), dtype=torch.int32, device=dev)
+    eng.sel_run_values(q, G, vals.data_ptr(), uni.data_ptr(), act.data_ptr())
+    vals = vals[:int(counts.sum()) * K]
+    c_mine = torch.as_tensor(counts, dtype=torch.int64, device=dev)
+    c_all = torch.empty(world * G, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(c_all, c_mine)
+    counts_all = c_all.cpu().numpy().reshape(world, G)
+    send, in_splits = sel_pack(vals, counts, K, world)
+    own = sel_owner(G, world)
+    out_splits = [int(sum(counts_all[r, g] * K for g in np.nonzero(own == me)[0])) for r in range(world)]
+    recv = torch.empty(sum(out_splits), dtype=torch.float64, device=dev)
+    dist.all_to_all_single(recv, send.contiguous(), out_splits, in_splits)
+    dist.all_reduce(uni, op=dist.ReduceOp.MAX)
+    dist.all_reduce(act, op=dist.ReduceOp.MAX)
+    ovals, seg = sel_unpack(recv, counts_all, K, me)
+    ovals = ovals.contiguous()
+    ov = torch.empty(max(1, G * K), dtype=torch.float64, device=dev)
+    of = torch.empty(max(1, G * K), dtype=torch.uint8, device=dev)
+    if on_gpu:
+        torch.cuda.current_stream(dev).synchronize()
+    eng.sel_select(q, G, ovals.data_ptr(), seg, uni.data_ptr(), ov.data_ptr(), of.data_ptr())
+    ov_all = torch.empty(world * ov.numel(), dtype=torch.float64, device=dev)
+    of_all = torch.empty(world * of.numel(), dtype=torch.uint8, device=dev)
+    dist.all_gather_into_tensor(ov_all, ov)
+    dist.all_gather_into_tensor(of_all, of)
+    val = sel_combine(ov_all, G, K, world).contiguous() if G * K else ov
+    flag = sel_combine(of_all, G, K, world).contiguous() if G * K else of
+    if on_gpu:
+        torch.cuda.current_stream(dev).synchronize()
+    return eng.assemble(q, G, val.data_ptr(), flag.data_ptr(), act.data_ptr())

@@ -26,6 +26,7 @@ EXPORTS = [
     "tsdbhip_run", "tsdbhip_result_free", "tsdbhip_last_timing", "tsdbhip_partials_layout_get",
     "tsdbhip_run_partials", "tsdbhip_finalize", "tsdbhip_sync", "tsdbhip_rollup_interval_parse",
     "tsdbhip_rollup_basetime", "tsdbhip_rollup_qualifier", "tsdbhip_rollup_run", "tsdbhip_rollup_download",
+    "tsdbhip_sel_layout", "tsdbhip_sel_run_values", "tsdbhip_sel_select", "tsdbhip_assemble",
 ]
 
 
@@ -73,6 +74,12 @@ def lib():
         L.tsdbhip_finalize.argtypes = [vp, C.POINTER(abi.Query), C.c_int64, C.c_void_p, C.c_int,
                                        C.POINTER(C.POINTER(abi.Result))]
         L.tsdbhip_sync.argtypes = [vp]
+        L.tsdbhip_sel_layout.argtypes = [vp, C.POINTER(abi.Query), C.c_int64, C.c_void_p, C.POINTER(C.c_int64)]
+        L.tsdbhip_sel_run_values.argtypes = [vp, C.POINTER(abi.Query), C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.tsdbhip_sel_select.argtypes = [vp, C.POINTER(abi.Query), C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_void_p]
+        L.tsdbhip_assemble.argtypes = [vp, C.POINTER(abi.Query), C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.POINTER(C.POINTER(abi.Result))]
         L.tsdbhip_rollup_interval_parse.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(abi.RollupInterval)]
         L.tsdbhip_rollup_basetime.argtypes = [C.c_int64, C.POINTER(abi.RollupInterval), C.POINTER(C.c_int32)]
         L.tsdbhip_rollup_qualifier.argtypes = [C.c_int64, C.c_int32, C.c_int16, C.c_int32,
@@ -263,6 +270,36 @@ class Engine:
         res = C.POINTER(abi.Result)()
         _check(lib().tsdbhip_finalize(self.ctx, C.byref(q), n_groups_global, C.c_void_p(ptr), n_ranks,
                                       C.byref(res)))
+        try:
+            return abi.result_to_groups(res.contents)
+        finally:
+            lib().tsdbhip_result_free(res)
+
+
+    # ---- multi-GPU percentile / median group-by (values to the owning rank) ----
+    def sel_layout(self, q: abi.Query, n_groups_global: int):
+        """(local spans per group [n_groups_global] int64, slots K)."""
+        counts = np.zeros(max(1, n_groups_global), np.int64)
+        k = C.c_int64()
+        _check(lib().tsdbhip_sel_layout(self.ctx, C.byref(q), n_groups_global, counts.ctypes.data, C.byref(k)))
+        return counts[:n_groups_global], int(k.value)
+
+    def sel_run_values(self, q: abi.Query, n_groups_global: int, vals: int, uni: int, act: int):
+        """Local span contributions ([g][k][i] f64), emit flags [G][K] u8, group active [G] u32."""
+        _check(lib().tsdbhip_sel_run_values(self.ctx, C.byref(q), n_groups_global, C.c_void_p(vals),
+                                            C.c_void_p(uni), C.c_void_p(act)))
+
+    def sel_select(self, q: abi.Query, n_groups_global: int, vals: int, counts: np.ndarray, uni: int,
+                   out_val: int, out_flag: int):
+        counts = np.ascontiguousarray(counts, np.int64)
+        _check(lib().tsdbhip_sel_select(self.ctx, C.byref(q), n_groups_global, C.c_void_p(vals),
+                                        C.c_void_p(counts.ctypes.data), C.c_void_p(uni), C.c_void_p(out_val),
+                                        C.c_void_p(out_flag)))
+
+    def assemble(self, q: abi.Query, n_groups_global: int, val: int, flag: int, act: int):
+        res = C.POINTER(abi.Result)()
+        _check(lib().tsdbhip_assemble(self.ctx, C.byref(q), n_groups_global, C.c_void_p(val), C.c_void_p(flag),
+                                      C.c_void_p(act), C.byref(res)))
         try:
             return abi.result_to_groups(res.contents)
         finally:

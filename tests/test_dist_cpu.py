@@ -98,3 +98,111 @@ def test_gloo_exchange_rank_order(tmp_path, world):
     want = np.concatenate([(np.arange(nbytes) * 7 + r * 31).astype(np.uint8) for r in range(world)])
     for r in range(world):
         np.testing.assert_array_equal(np.load(tmp_path / f"r{r}.npy"), want)
+
+
+# ---- percentile / median group-by exchange (values to the owning rank) --------------
+def _emulate_sel_exchange(per_rank_vals, per_rank_counts, K):
+    """all-to-all of sel_pack outputs, in-process: recv[me] = concat over r of r's piece for me."""
+    import torch
+    world = len(per_rank_vals)
+    sends = [dist.sel_pack(per_rank_vals[r], per_rank_counts[r], K, world) for r in range(world)]
+    counts_all = np.stack(per_rank_counts)
+    outs = []
+    for me in range(world):
+        pieces = []
+        for r in range(world):
+            send, splits = sends[r]
+            off = int(sum(splits[:me]))
+            pieces.append(send[off:off + splits[me]])
+        recv = torch.cat(pieces)
+        outs.append(dist.sel_unpack(recv, counts_all, K, me))
+    return outs
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+def test_sel_pack_unpack_routes_every_value(world):
+    import torch
+    rng = np.random.default_rng(world)
+    G, K = 7, 5
+    counts = [rng.integers(0, 4, G) for _ in range(world)]
+    vals = []
+    for r in range(world):
+        v = []
+        for g in range(G):
+            for k in range(K):
+                for i in range(counts[r][g]):
+                    v.append(r * 1e6 + g * 1e4 + k * 1e2 + i)
+        vals.append(torch.tensor(v, dtype=torch.float64))
+    outs = _emulate_sel_exchange(vals, counts, K)
+    for me, (ov, seg) in enumerate(outs):
+        pos = 0
+        for g in range(G):
+            if g % world != me:
+                assert seg[g] == 0
+                continue
+            n = sum(int(counts[r][g]) for r in range(world))
+            assert seg[g] == n
+            for k in range(K):
+                want = [r * 1e6 + g * 1e4 + k * 1e2 + i for r in range(world) for i in range(counts[r][g])]
+                np.testing.assert_array_equal(ov[pos:pos + n].numpy(), want)
+                pos += n
+        assert pos == ov.numel()
+
+
+def test_sel_combine_takes_owner_rows():
+    import torch
+    world, G, K = 3, 5, 2
+    rows = torch.zeros(world, G * K, dtype=torch.float64)
+    for r in range(world):
+        rows[r] = r + 10 * torch.arange(G * K)
+    got = dist.sel_combine(rows.reshape(-1), G, K, world).reshape(G, K)
+    for g in range(G):
+        np.testing.assert_array_equal(got[g].numpy(), (g % world) + 10 * np.arange(g * K, g * K + K))
+
+
+def _sel_gloo_worker(rank, world, port, out):
+    """The collective sequence of run_distributed_sel over gloo, with the engine calls
+    replaced by host arithmetic (no GPU here): every rank contributes known values, and
+    the owner's gathered segments must hold every rank's values of its groups."""
+    import torch
+    import torch.distributed as td
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    td.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        G, K = 6, 3
+        counts = np.array([(rank + g) % 3 for g in range(G)], np.int64)
+        vals = torch.tensor([rank * 1e6 + g * 1e4 + k * 1e2 + i for g in range(G) for k in range(K)
+                             for i in range(counts[g])], dtype=torch.float64)
+        c_all = torch.empty(world * G, dtype=torch.int64)
+        td.all_gather_into_tensor(c_all, torch.as_tensor(counts))
+        counts_all = c_all.numpy().reshape(world, G)
+        send, in_splits = dist.sel_pack(vals, counts, K, world)
+        own = dist.sel_owner(G, world)
+        out_splits = [int(sum(counts_all[r, g] * K for g in np.nonzero(own == rank)[0])) for r in range(world)]
+        recv = torch.empty(sum(out_splits), dtype=torch.float64)
+        td.all_to_all_single(recv, send.contiguous(), out_splits, in_splits)
+        ov, seg = dist.sel_unpack(recv, counts_all, K, rank)
+        np.savez(os.path.join(out, f"s{rank}.npz"), ov=ov.numpy(), seg=seg, counts_all=counts_all)
+    finally:
+        td.destroy_process_group()
+
+
+def test_sel_exchange_gloo_two_ranks(tmp_path):
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_sel_gloo_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    G, K = 6, 3
+    for me in range(2):
+        z = np.load(tmp_path / f"s{me}.npz")
+        ca = z["counts_all"]
+        want = []
+        for g in range(G):
+            if g % 2 != me:
+                continue
+            for k in range(K):
+                want += [r * 1e6 + g * 1e4 + k * 1e2 + i for r in range(2) for i in range(ca[r, g])]
+        np.testing.assert_array_equal(z["ov"], want)

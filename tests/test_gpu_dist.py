@@ -113,3 +113,97 @@ def test_two_process_gloo(tmp_path, batch):
         got = [(int(z["gid"][i]), z["ts"][cut[i]:cut[i + 1]], z["bits"][cut[i]:cut[i + 1]], z["isi"][cut[i]:cut[i + 1]])
                for i in range(len(z["gid"]))]
         assert_groups_match(got, want, "sum", ctx=f"gloo rank {r}")
+
+
+# ---- percentile / median group-by: values to the owning rank ----------
+def run_sharded_sel(engines, b, q, world):
+    """run_distributed_sel with the collectives done in-process (one context per rank)."""
+    import torch
+    G = dist.n_groups_of(b)
+    vals, counts, unis, acts = [], [], [], []
+    K = 0
+    for r in range(world):
+        e = engines[r]
+        e.load(dist.shard_batch(b, r, world))
+        c, K = e.sel_layout(q, G)
+        v = np.zeros(max(1, int(c.sum()) * K))
+        u = np.zeros(max(1, G * K), np.uint8)
+        a = np.zeros(max(1, G), np.int32)
+        e.sel_run_values(q, G, v.ctypes.data, u.ctypes.data, a.ctypes.data)
+        vals.append(torch.from_numpy(v[:int(c.sum()) * K]))
+        counts.append(c)
+        unis.append(u)
+        acts.append(a)
+    uni = np.maximum.reduce(unis)
+    act = np.maximum.reduce(acts)
+    sends = [dist.sel_pack(vals[r], counts[r], K, world) for r in range(world)]
+    counts_all = np.stack(counts)
+    rows_v, rows_f = [], []
+    for me in range(world):
+        pieces = []
+        for r in range(world):
+            send, splits = sends[r]
+            off = int(sum(splits[:me]))
+            pieces.append(send[off:off + splits[me]])
+        ov, seg = dist.sel_unpack(torch.cat(pieces), counts_all, K, me)
+        ov = np.ascontiguousarray(ov.numpy())
+        out_v = np.zeros(max(1, G * K))
+        out_f = np.zeros(max(1, G * K), np.uint8)
+        engines[me].sel_select(q, G, ov.ctypes.data, seg, uni.ctypes.data, out_v.ctypes.data, out_f.ctypes.data)
+        rows_v.append(out_v)
+        rows_f.append(out_f)
+    val = np.ascontiguousarray(dist.sel_combine(torch.from_numpy(np.stack(rows_v)), G, K, world).numpy())
+    flag = np.ascontiguousarray(dist.sel_combine(torch.from_numpy(np.stack(rows_f)), G, K, world).numpy())
+    return engines[0].assemble(q, G, val.ctypes.data, flag.ctypes.data, act.ctypes.data)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+@pytest.mark.parametrize("agg,ds", [("p99", "avg"), ("p50", "max"), ("median", "sum"), ("p90", "p99"),
+                                    ("ep95r7", "avg")])
+def test_sharded_percentile_group_equals_oracle(engines, batch, world, agg, ds):
+    q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG[ds], ds_interval_ms=60000)
+    assert_groups_match(run_sharded_sel(engines, batch, q, world), O.run_query(batch, q), agg, tol=0.0,
+                        ctx=f"{agg}:{ds} x{world}")
+
+
+def test_sharded_percentile_group_rate_fill(engines, batch):
+    for kw in [dict(ds_function=abi.AGG["avg"], ds_interval_ms=60000, rate=True),
+               dict(ds_function=abi.AGG["sum"], ds_interval_ms=300000, ds_fill=abi.FILL_NAN)]:
+        q = abi.new_query(T0, T0 + 3599, "p75", **kw)
+        assert_groups_match(run_sharded_sel(engines, batch, q, 3), O.run_query(batch, q), "p75", tol=0.0, ctx=str(kw))
+
+
+def _sel_worker(rank, world, port, out):
+    import torch.distributed as td
+    from opentsdb_amd.engine import Engine
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    td.init_process_group("gloo", rank=rank, world_size=world)
+    eng = Engine(0)
+    try:
+        b = synth.generate(150, T0, 360, 10000, value_kind=2, n_groups=7, int_mod=30000, seed=0x5EED)
+        eng.load(dist.shard_batch(b, rank, world))
+        q = abi.new_query(T0, T0 + 3599, "p99", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+        groups = dist.run_distributed_sel(eng, q, td, dist.n_groups_of(b))
+        np.savez(os.path.join(out, f"p{rank}.npz"), gid=np.array([g[0] for g in groups]),
+                 n=np.array([len(g[1]) for g in groups]), ts=np.concatenate([g[1] for g in groups]),
+                 bits=np.concatenate([g[2] for g in groups]), isi=np.concatenate([g[3] for g in groups]))
+    finally:
+        eng.close()
+        td.destroy_process_group()
+
+
+def test_two_process_gloo_percentile(tmp_path, batch):
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_sel_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    q = abi.new_query(T0, T0 + 3599, "p99", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+    want = O.run_query(batch, q)
+    for r in range(2):
+        z = np.load(tmp_path / f"p{r}.npz")
+        cut = np.concatenate([[0], np.cumsum(z["n"])])
+        got = [(int(z["gid"][i]), z["ts"][cut[i]:cut[i + 1]], z["bits"][cut[i]:cut[i + 1]], z["isi"][cut[i]:cut[i + 1]])
+               for i in range(len(z["gid"]))]
+        assert_groups_match(got, want, "p99", tol=0.0, ctx=f"gloo rank {r}")
