@@ -211,3 +211,54 @@ def run_distributed_sel(eng, q: abi.Query, dist, n_groups_global: int, device=No
     if on_gpu:
         torch.cuda.current_stream(dev).synchronize()
     return eng.assemble(q, G, val.data_ptr(), flag.data_ptr(), act.data_ptr())
+
+
+# ---- raw (no-downsampling) queries: whole SpanGroups per rank -------------------------
+#
+# Without a downsampler the group-by runs over the union of the group's raw timestamps
+# (AggregationIterator, src/core/AggregationIterator.java:500-797): O(U k) interpolations per
+# group, compute-bound, with Java's span-order operand sequence for float sums.  Splitting a
+# group over ranks would need the union itself exchanged and a rank-order merge of every
+# aggregator state per union point; instead the raw path shards by GROUP -- each rank holds
+# whole SpanGroups (contiguous, byte-balanced ranges of group ids), evaluates them exactly as
+# one GPU does (bit-exact), and only the finished points are gathered.  No data-path
+# collective.
+
+def group_shard_bounds(batch: abi.HostBatch, world: int):
+    """world+1 group ids: rank r owns groups [b[r], b[r+1]), byte-balanced."""
+    G = n_groups_of(batch)
+    srp = batch.series_row_ptr
+    qo, vo = batch.row_qual_off.astype(np.int64), batch.row_val_off.astype(np.int64)
+    gbytes = np.zeros(G, np.float64)
+    for s in range(batch.n_series):
+        g = int(batch.group_id[s])
+        if g >= 0:
+            gbytes[g] += (qo[srp[s + 1]] - qo[srp[s]]) + (vo[srp[s + 1]] - vo[srp[s]])
+    return shard_bounds(gbytes, world)
+
+
+def shard_batch_by_group(batch: abi.HostBatch, rank: int, world: int) -> abi.HostBatch:
+    """The rank's whole groups (group ids stay global, SpanGroup order kept)."""
+    b = group_shard_bounds(batch, world)
+    order = group_sorted_order(batch)
+    g = batch.group_id[order]
+    keep = order[(g >= b[rank]) & (g < b[rank + 1])]
+    return select_series(batch, keep)
+
+
+def merge_group_results(parts):
+    """Concatenate per-rank result groups (disjoint group ids) in group id order."""
+    groups = [g for p in parts for g in p]
+    groups.sort(key=lambda x: x[0])
+    return groups
+
+
+def run_distributed_raw(eng, q: abi.Query, dist):
+    """A raw (no-downsampling) query over a group-sharded store (shard_batch_by_group):
+    local evaluation, then the points of every rank gathered to every rank."""
+    if q.aggregator == abi.AGG["none"]:
+        raise NotImplementedError("NONE aggregator: one group per span, ids are per rank")
+    local = [(int(g), np.asarray(ts), np.asarray(bits), np.asarray(isi)) for g, ts, bits, isi in eng.run(q)]
+    parts = [None] * dist.get_world_size()
+    dist.all_gather_object(parts, local)
+    return merge_group_results(parts)

@@ -206,3 +206,22 @@ def test_sel_exchange_gloo_two_ranks(tmp_path):
             for k in range(K):
                 want += [r * 1e6 + g * 1e4 + k * 1e2 + i for r in range(2) for i in range(ca[r, g])]
         np.testing.assert_array_equal(z["ov"], want)
+
+
+# ---- raw queries: group-sharded (whole SpanGroups per rank) ---------------------------
+@pytest.mark.parametrize("world", [1, 2, 3, 5])
+def test_shard_by_group_keeps_groups_whole(world):
+    b = synth.generate_counters(60, 1356998400, 40, n_groups=7, seed=5)
+    seen = []
+    owner = {}
+    for r in range(world):
+        s = dist.shard_batch_by_group(b, r, world)
+        for g in np.unique(s.group_id):
+            assert owner.setdefault(int(g), r) == r, "group split across ranks"
+        seen.append(s.n_series)
+        # series of a group keep their batch (SpanGroup) order
+        for g in np.unique(s.group_id):
+            idx = np.nonzero(s.group_id == g)[0]
+            assert np.all(np.diff(idx) == 1)
+    assert sum(seen) == b.n_series
+    assert sorted(owner) == list(range(7))

@@ -207,3 +207,65 @@ def test_two_process_gloo_percentile(tmp_path, batch):
         got = [(int(z["gid"][i]), z["ts"][cut[i]:cut[i + 1]], z["bits"][cut[i]:cut[i + 1]], z["isi"][cut[i]:cut[i + 1]])
                for i in range(len(z["gid"]))]
         assert_groups_match(got, want, "p99", tol=0.0, ctx=f"gloo rank {r}")
+
+
+# ---- raw (no-downsampling) queries: whole groups per rank ---------------------------
+@pytest.fixture(scope="module")
+def raw_batch():
+    from tests.test_gpu_raw import random_batch
+    return random_batch(21, n_series=60, n_groups=5)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+@pytest.mark.parametrize("agg", ["sum", "avg", "min", "max", "dev", "zimsum", "mimmax", "first", "diff", "pfsum"])
+def test_group_sharded_raw_equals_oracle(engines, raw_batch, world, agg):
+    q = abi.new_query(T0, T0 + 7199, agg)
+    parts = []
+    for r in range(world):
+        parts.append(engines[r].run_batch(dist.shard_batch_by_group(raw_batch, r, world), q))
+    assert_groups_match(dist.merge_group_results(parts), O.run_query(raw_batch, q), agg, tol=0.0,
+                        ctx=f"{agg} x{world}")
+
+
+def test_group_sharded_raw_counters_rate(engines):
+    b = synth.generate_counters(80, T0, 120, n_groups=6, seed=9)
+    for kw in [dict(rate=True, counter=True, counter_max=1 << 32, reset_value=1000000), dict()]:
+        q = abi.new_query(T0, T0 + 3599, "sum", **kw)
+        parts = [engines[r].run_batch(dist.shard_batch_by_group(b, r, 3), q) for r in range(3)]
+        assert_groups_match(dist.merge_group_results(parts), O.run_query(b, q), "sum", tol=0.0, ctx=str(kw))
+
+
+def _raw_worker(rank, world, port, out):
+    import torch.distributed as td
+    from opentsdb_amd.engine import Engine
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    td.init_process_group("gloo", rank=rank, world_size=world)
+    eng = Engine(0)
+    try:
+        b = synth.generate_counters(80, T0, 120, n_groups=6, seed=9)
+        eng.load(dist.shard_batch_by_group(b, rank, world))
+        q = abi.new_query(T0, T0 + 3599, "sum")
+        groups = dist.run_distributed_raw(eng, q, td)
+        np.savez(os.path.join(out, f"w{rank}.npz"), gid=np.array([g[0] for g in groups]),
+                 n=np.array([len(g[1]) for g in groups]), ts=np.concatenate([g[1] for g in groups]),
+                 bits=np.concatenate([g[2] for g in groups]), isi=np.concatenate([g[3] for g in groups]))
+    finally:
+        eng.close()
+        td.destroy_process_group()
+
+
+def test_two_process_gloo_raw(tmp_path):
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_raw_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    b = synth.generate_counters(80, T0, 120, n_groups=6, seed=9)
+    want = O.run_query(b, abi.new_query(T0, T0 + 3599, "sum"))
+    for r in range(2):
+        z = np.load(tmp_path / f"w{r}.npz")
+        cut = np.concatenate([[0], np.cumsum(z["n"])])
+        got = [(int(z["gid"][i]), z["ts"][cut[i]:cut[i + 1]], z["bits"][cut[i]:cut[i + 1]], z["isi"][cut[i]:cut[i + 1]])
+               for i in range(len(z["gid"]))]
+        assert_groups_match(got, want, "sum", tol=0.0, ctx=f"gloo raw rank {r}")
