@@ -97,7 +97,7 @@ typedef struct {
   int32_t ds_function;       /* TSDB_AGG_* or -1 for NO_DOWNSAMPLER */
   int32_t ds_fill;           /* TSDB_FILL_* */
   int32_t ds_all;            /* "0all-..." : one bucket over [query start, query end) */
-  int32_t ds_calendar;       /* 'c' suffix; not implemented yet (TSDB_E_NOT_IMPLEMENTED) */
+  int32_t ds_calendar;       /* 'c' suffix: TSDB_CAL_* unit of the interval (0 = epoch-aligned); UTC */
   int64_t ds_interval_ms;
   /* RateOptions (src/core/RateOptions.java:27-97) */
   int32_t rate;
@@ -107,6 +107,17 @@ typedef struct {
   int64_t rate_counter_max;  /* default Long.MAX_VALUE */
   int64_t rate_reset_value;  /* default 0 */
 } tsdbhip_query;
+
+/* Calendar units of a 'c' downsampling interval (DateTime.unitsToCalendarType,
+ * src/utils/DateTime.java:616-640); the interval count is ds_interval_ms / the unit's
+ * parseDuration length (ms 1, s 1e3, m 6e4, h 3.6e6, d 8.64e7, w 6.048e8, n 30 d, y 365 d).
+ * The engine aligns on the UTC calendar (the DownsamplingSpecification default timezone);
+ * it runs the units whose grid is one global sequence -- ms (1000 % n == 0), s / m
+ * (60 % n == 0), h (24 % n == 0), d (n == 1), w (n == 1, weeks from Sunday) -- and returns
+ * TSDB_E_NOT_IMPLEMENTED for months, years and intervals anchored per span. */
+enum {
+  TSDB_CAL_NONE = 0, TSDB_CAL_MS, TSDB_CAL_S, TSDB_CAL_M, TSDB_CAL_H, TSDB_CAL_D, TSDB_CAL_W, TSDB_CAL_N, TSDB_CAL_Y
+};
 
 /* Query flags. */
 #define TSDB_QF_ORDERED 0x1  /* cross-series float reductions in SpanGroup index order (bit-exact, slower) */

@@ -52,6 +52,9 @@ INTERP_LERP, INTERP_ZIM, INTERP_MAX, INTERP_MIN, INTERP_PREV = range(5)
 FILL_NONE, FILL_ZERO, FILL_NAN, FILL_NULL, FILL_SCALAR = range(5)
 FILL_NAMES = ["none", "zero", "nan", "null", "scalar"]
 
+# calendar units of a 'c' downsampling interval (tsdbhip.h TSDB_CAL_*)
+CAL_NONE, CAL_MS, CAL_S, CAL_M, CAL_H, CAL_D, CAL_W, CAL_N, CAL_Y = range(9)
+
 QF_ORDERED = 0x1
 
 LONG_MAX = (1 << 63) - 1

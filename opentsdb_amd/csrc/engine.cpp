@@ -91,6 +91,48 @@ int f_of(int a) {
 
 inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 
+// ---- calendar intervals (UTC) -----------------------------------------------------------
+constexpr int64_t CAL_UNIT_MS[9] = {0, 1, 1000, 60000, 3600000, 86400000, 604800000, 2592000000LL, 31536000000LL};
+
+int cal_unit_of(const std::string& d) {   // suffix of a parseDuration string (parse already checked it)
+  if (d.size() >= 2 && (d.compare(d.size() - 2, 2, "ms") == 0)) return TSDB_CAL_MS;
+  switch (d.empty() ? 0 : d.back()) {
+    case 's': return TSDB_CAL_S;
+    case 'm': return TSDB_CAL_M;
+    case 'h': return TSDB_CAL_H;
+    case 'd': return TSDB_CAL_D;
+    case 'w': return TSDB_CAL_W;
+    case 'n': return TSDB_CAL_N;
+    case 'y': return TSDB_CAL_Y;
+  }
+  return TSDB_CAL_NONE;
+}
+
+inline int64_t floor_div(int64_t a, int64_t b) { int64_t q = a / b; if ((a % b) && ((a < 0) != (b < 0))) q--; return q; }
+
+// A calendar interval whose DateTime.previousInterval grid (src/utils/DateTime.java:445-606)
+// is one global sequence in UTC: width W ms, boundaries at O + j W.  ms / s / m / h intervals
+// that divide the next unit start at the top of the second / minute / hour / day, which are
+// multiples of W since the epoch; "1dc" steps days from midnight; "1wc" steps 7 days from
+// Sunday (default US locale; 1970-01-04 was a Sunday, O = 3 days).  0 = not such an interval.
+bool cal_grid(int unit, int64_t interval_ms, int64_t* W, int64_t* O) {
+  if (unit < TSDB_CAL_MS || unit > TSDB_CAL_Y) return false;
+  const int64_t n = interval_ms / CAL_UNIT_MS[unit];
+  if (n < 1 || n * CAL_UNIT_MS[unit] != interval_ms) return false;
+  bool ok = false;
+  switch (unit) {
+    case TSDB_CAL_MS: ok = 1000 % n == 0; break;
+    case TSDB_CAL_S: case TSDB_CAL_M: ok = 60 % n == 0; break;
+    case TSDB_CAL_H: ok = 24 % n == 0; break;
+    case TSDB_CAL_D: case TSDB_CAL_W: ok = n == 1; break;
+    default: ok = false;   // months / years: variable widths
+  }
+  if (!ok) return false;
+  *W = interval_ms;
+  *O = unit == TSDB_CAL_W ? 3 * 86400000LL : 0;
+  return true;
+}
+
 // bytes past the end of the qualifier / value blobs that kernels may read (never use):
 // k_fast's vle class loads a 1 KB value window from each row start
 constexpr int64_t BLOB_SLACK = 1024 + 64;
@@ -251,9 +293,11 @@ extern "C" int tsdbhip_parse_downsample(const char* spec, tsdbhip_query* q) {
     q->ds_all = 1;
   } else {
     std::string d = parts[0];
-    if (!d.empty() && d.back() == 'c') { d.pop_back(); q->ds_calendar = 1; }
+    const bool cal = !d.empty() && d.back() == 'c';
+    if (cal) d.pop_back();
     int rc = tsdbhip_parse_duration(d.c_str(), &q->ds_interval_ms);
     if (rc) return rc;
+    if (cal) q->ds_calendar = cal_unit_of(d);   // DateTime.unitsToCalendarType (src/utils/DateTime.java:616-640)
   }
   int f = -1;
   for (int i = 0; i < TSDB_AGG_COUNT_ALL; i++) if (parts[1] == AGG_NAMES[i]) f = i;
@@ -762,8 +806,11 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
     tsdbhip_scan_bounds(q, &P.ss, &P.se);
     return 0;
   }
-  if (q->ds_calendar) return fail(TSDB_E_NOT_IMPLEMENTED, "calendar downsampling is not implemented yet");
   if (!q->ds_all && q->ds_interval_ms <= 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "interval not > 0");
+  int64_t calW = 0, calO = 0;
+  if (q->ds_calendar && !q->ds_all && !cal_grid(q->ds_calendar, q->ds_interval_ms, &calW, &calO))
+    return fail(TSDB_E_NOT_IMPLEMENTED, "calendar interval without a global UTC grid (months, years, or an "
+                                        "interval that does not divide its unit) is not implemented yet");
   P.ga = ga_of(q->aggregator);
   P.f = f_of(q->ds_function);
   if (P.f < 0 && (q->ds_function == TSDB_AGG_MEDIAN || q->ds_function >= TSDB_AGG_P999)) P.f = F_SEL;
@@ -788,12 +835,30 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
     P.mode = MODE_GRID;
     const int64_t I = q->ds_interval_ms;
     P.I = I;
-    P.B0 = ((S0 + I - 1) / I) * I;  // Downsampler seek: first bucket fully after the scan start
-    if (q->ds_fill != TSDB_FILL_NONE) {
-      const int64_t aE = E0 - E0 % I;
-      P.K = aE > P.B0 ? (aE - P.B0) / I : 0;
+    if (q->ds_calendar) {
+      // Downsampler.seekInterval :420-432 (previousInterval, next one if the seek time is
+      // past it); FillingDownsampler ctor :113-135: buckets from previousInterval(start) to
+      // previousInterval(end), one bucket when both are the same.
+      auto cfloor = [&](int64_t t) { return calO + floor_div(t - calO, I) * I; };
+      const int64_t f0 = cfloor(S0);
+      P.B0 = f0 == S0 ? S0 : f0 + I;
+      if (q->ds_fill != TSDB_FILL_NONE) {
+        if (f0 < P.B0)
+          return fail(TSDB_E_NOT_IMPLEMENTED, "filled calendar interval starting before the scan start (weeks)");
+        int64_t eC = cfloor(E0);
+        if (eC == f0) eC += I;
+        P.K = eC > P.B0 ? (eC - P.B0) / I : 0;
+      } else {
+        P.K = E0 > P.B0 ? (E0 - P.B0 + I - 1) / I : 0;
+      }
     } else {
-      P.K = E0 > P.B0 ? (E0 - P.B0 + I - 1) / I : 0;
+      P.B0 = ((S0 + I - 1) / I) * I;  // Downsampler seek: first bucket fully after the scan start
+      if (q->ds_fill != TSDB_FILL_NONE) {
+        const int64_t aE = E0 - E0 % I;
+        P.K = aE > P.B0 ? (aE - P.B0) / I : 0;
+      } else {
+        P.K = E0 > P.B0 ? (E0 - P.B0 + I - 1) / I : 0;
+      }
     }
   }
   // slot arrays live in LDS when they fit next to 4 waves' worth of staging, else in HBM

@@ -78,6 +78,7 @@ class DownsamplingSpecification:
     fill_policy: str = "none"
     run_all: bool = False
     use_calendar: bool = False
+    calendar_unit: int = 0     # abi.CAL_* of a 'c' interval (UTC; DateTime.unitsToCalendarType)
 
     @classmethod
     def parse(cls, spec: str) -> "DownsamplingSpecification":
@@ -94,6 +95,10 @@ class DownsamplingSpecification:
         elif parts[0].endswith("c"):
             ds.interval = parse_duration(parts[0][:-1])
             ds.use_calendar = True
+            d = parts[0][:-1]
+            ds.calendar_unit = abi.CAL_MS if d.lower().endswith("ms") else \
+                {"s": abi.CAL_S, "m": abi.CAL_M, "h": abi.CAL_H, "d": abi.CAL_D, "w": abi.CAL_W, "n": abi.CAL_N,
+                 "y": abi.CAL_Y}[d[-1]]
         else:
             ds.interval = parse_duration(parts[0])
         if parts[1] not in abi.AGG:
@@ -263,7 +268,7 @@ class TsdbQuery:
             counter_max=self.rate_options.counter_max, reset_value=self.rate_options.reset_value,
             drop_resets=self.rate_options.drop_resets, flags=self.flags)
         if ds and ds.use_calendar:
-            q.ds_calendar = 1
+            q.ds_calendar = ds.calendar_unit
         return q
 
     def scan_bounds(self):

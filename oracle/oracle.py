@@ -41,7 +41,7 @@ def lib():
                                     C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)]
         L.ref_view_downsampler.restype = vp
         L.ref_view_downsampler.argtypes = [vp, C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_int64, C.c_int64,
-                                           C.c_int64, C.c_int64]
+                                           C.c_int64, C.c_int64, C.c_int32]
         L.ref_view_rate.restype = vp
         L.ref_view_rate.argtypes = [vp, C.c_int32, C.c_int64, C.c_int64, C.c_int32]
         L.ref_view_aggregate.restype = vp
@@ -175,7 +175,7 @@ def downsampler(src: View, spec: str, start_time: int = 0, end_time: int = 0,
     """Downsampler (fill none) or FillingDownsampler, as Span.downsampler builds them."""
     q = parse_downsample(spec)
     ptr = lib().ref_view_downsampler(src._take(), q.ds_function, q.ds_interval_ms, q.ds_fill, q.ds_all,
-                                     start_time, end_time, query_start, query_end)
+                                     start_time, end_time, query_start, query_end, q.ds_calendar)
     if not ptr:
         _err(-3)
     return View(ptr, keep=src.keep)
@@ -185,7 +185,7 @@ def downsampler_raw(src: View, function: str, interval_ms: int, fill: int = abi.
                     start_time: int = 0, end_time: int = 0) -> View:
     """The deprecated Downsampler(source, interval_ms, function) constructor."""
     ptr = lib().ref_view_downsampler(src._take(), abi.AGG[function], interval_ms, fill, 0,
-                                     start_time, end_time, 0, 0)
+                                     start_time, end_time, 0, 0, 0)
     if not ptr:
         _err(-3)
     return View(ptr, keep=src.keep)

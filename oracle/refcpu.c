@@ -781,6 +781,131 @@ static void span_first_last(span_view* s, int64_t* first, int64_t* last, int64_t
 }
 
 /* ======================================================================== */
+/* UTC calendar (java.util.GregorianCalendar in the UTC zone, default US locale: weeks   */
+/* start on Sunday) -- the arithmetic DateTime.previousInterval and the calendar          */
+/* Downsampler / FillingDownsampler use (src/utils/DateTime.java:445-606,                 */
+/* src/core/Downsampler.java:131-147,336-350,390-400,420-432,446-447,                     */
+/* src/core/FillingDownsampler.java:113-135,280-286).                                     */
+/* ======================================================================== */
+static const int64_t CAL_UNIT_MS[9] = {0, 1, 1000, 60000, 3600000, 86400000, 604800000, 2592000000LL, 31536000000LL};
+
+static int cal_unit_of(const char* dur) {  /* suffix of a parseDuration string */
+  size_t l = strlen(dur);
+  if (l >= 2 && strcasecmp(dur + l - 2, "ms") == 0) return TSDB_CAL_MS;
+  if (l == 0) return 0;
+  switch (dur[l - 1]) {
+    case 's': return TSDB_CAL_S;
+    case 'm': return TSDB_CAL_M;
+    case 'h': return TSDB_CAL_H;
+    case 'd': return TSDB_CAL_D;
+    case 'w': return TSDB_CAL_W;
+    case 'n': return TSDB_CAL_N;
+    case 'y': return TSDB_CAL_Y;
+  }
+  return 0;
+}
+
+static int64_t cal_fdiv(int64_t a, int64_t b) { int64_t q = a / b; if ((a % b) && ((a < 0) != (b < 0))) q--; return q; }
+/* days since 1970-01-01 of a proleptic Gregorian civil date, and back */
+static int64_t days_from_civil(int64_t y, int m, int d) {
+  y -= m <= 2;
+  const int64_t era = cal_fdiv(y, 400);
+  const int64_t yoe = y - era * 400;
+  const int64_t doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+  const int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  return era * 146097 + doe - 719468;
+}
+static void civil_from_days(int64_t z, int64_t* y, int* m, int* d) {
+  z += 719468;
+  const int64_t era = cal_fdiv(z, 146097);
+  const int64_t doe = z - era * 146097;
+  const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+  const int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+  const int64_t mp = (5 * doy + 2) / 153;
+  *d = (int)(doy - (153 * mp + 2) / 5 + 1);
+  *m = (int)(mp < 10 ? mp + 3 : mp - 9);
+  *y = yoe + era * 400 + (*m <= 2);
+}
+static int month_days(int64_t y, int m) {
+  static const int md[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+  const int leap = (y % 4 == 0 && y % 100 != 0) || y % 400 == 0;
+  return m == 2 ? 28 + leap : md[m - 1];
+}
+/* Calendar.add(unit, n) in UTC (fixed-length units are exact millisecond sums) */
+static int64_t cal_add(int64_t ts, int unit, int64_t n) {
+  if (unit != TSDB_CAL_N && unit != TSDB_CAL_Y) return ts + n * CAL_UNIT_MS[unit];
+  const int64_t day = cal_fdiv(ts, 86400000), tod = ts - day * 86400000;
+  int64_t y; int m, d;
+  civil_from_days(day, &y, &m, &d);
+  if (unit == TSDB_CAL_N) {
+    const int64_t mm = y * 12 + (m - 1) + n;
+    y = cal_fdiv(mm, 12);
+    m = (int)(mm - y * 12) + 1;
+  } else {
+    y += n;
+  }
+  const int ml = month_days(y, m);
+  if (d > ml) d = ml;   /* add() pins the day of month */
+  return days_from_civil(y, m, d) * 86400000 + tod;
+}
+/* one Downsampler step: interval units, or interval * WEEK_LENGTH days for weeks */
+static int64_t cal_step(int64_t ts, int unit, int64_t n, int sign) {
+  if (unit == TSDB_CAL_W) return cal_add(ts, TSDB_CAL_D, sign * n * 7);
+  return cal_add(ts, unit, sign * n);
+}
+/* DateTime.previousInterval(ts, interval, unit, UTC) :445-606 */
+static int64_t cal_prev(int64_t ts, int64_t n, int unit) {
+  if (ts < 0) jthrow(TSDB_E_ILLEGAL_ARGUMENT, "Timestamp cannot be less than zero");
+  if (n < 1) jthrow(TSDB_E_ILLEGAL_ARGUMENT, "Interval must be greater than zero");
+  int uo = unit;
+  int64_t io = n;
+  const int64_t day = cal_fdiv(ts, 86400000);
+  int64_t y; int m, d;
+  civil_from_days(day, &y, &m, &d);
+  int64_t c;
+  switch (unit) {
+    case TSDB_CAL_MS:
+      if (1000 % n == 0) { c = ts - ts % 1000; if (n > 1000) c -= n; }
+      else c = ts - ts % 60000;
+      break;
+    case TSDB_CAL_S:
+      if (60 % n == 0) { c = ts - ts % 60000; if (n > 60) c -= n * 1000; }
+      else c = ts - ts % 3600000;
+      break;
+    case TSDB_CAL_M:
+      if (60 % n == 0) { c = ts - ts % 3600000; if (n > 60) c -= n * 60000; }
+      else c = day * 86400000;
+      break;
+    case TSDB_CAL_H:
+      if (24 % n == 0) { c = day * 86400000; if (n > 24) c -= n * 3600000; }
+      else c = days_from_civil(y, m, 1) * 86400000;
+      break;
+    case TSDB_CAL_D:
+      if (n == 1) c = days_from_civil(y, m, 1) * 86400000;
+      else c = days_from_civil(y, 1, 1) * 86400000;
+      break;
+    case TSDB_CAL_W:
+      if (2 % n == 0) {
+        /* set(DAY_OF_WEEK, SUNDAY): the Sunday of the Sunday-first week (1970-01-04 was one) */
+        const int64_t dow = ((day - 3) % 7 + 7) % 7;
+        c = (day - dow) * 86400000;
+      } else {
+        /* set(MONTH, 0) then set(DAY_OF_WEEK, ...): lenient resolution of a January week */
+        jthrow(TSDB_E_NOT_IMPLEMENTED, "calendar intervals of more than 2 weeks");
+      }
+      uo = TSDB_CAL_D;   /* the loop steps 7 days whatever the interval */
+      io = 7;
+      break;
+    default:   /* MONTH, YEAR: from the top of the year */
+      c = days_from_civil(y, 1, 1) * 86400000;
+      break;
+  }
+  if (c == ts) return c;
+  while (c <= ts) c = cal_add(c, uo, io);
+  return cal_add(c, uo, -io);
+}
+
+/* ======================================================================== */
 /* Downsampler / FillingDownsampler                                          */
 /* ======================================================================== */
 typedef struct {
@@ -801,6 +926,12 @@ typedef struct {
   ref_dp next_dp;
   int next_dp_null;
   int initialized;
+  /* useCalendar: unit, interval count, Downsampler.previous_calendar / next_calendar, and
+   * FillingDownsampler's own previous_calendar / next_calendar (FillingDownsampler.java:38-41) */
+  int cal;
+  int64_t cal_n;
+  int64_t prev_cal, next_cal;
+  int64_t fprev_cal, fnext_cal;
 } ds_view;
 
 static inline int64_t ds_align(ds_view* d, int64_t t) { return t - (t % d->interval); }
@@ -830,21 +961,47 @@ static void viv_init(ds_view* d) {  /* :327-354 */
     d->initialized = 1;
     if (v_has_next(d->src)) {
       viv_move_to_next_value(d);
-      if (!d->run_all) d->tei = ds_align(d, d->next_dp.ts) + d->interval;
+      if (!d->run_all) {
+        if (d->cal) {
+          d->prev_cal = cal_prev(d->next_dp.ts, d->cal_n, d->cal);
+          d->next_cal = cal_step(d->prev_cal, d->cal, d->cal_n, 1);
+          d->tei = d->next_cal;
+        } else {
+          d->tei = ds_align(d, d->next_dp.ts) + d->interval;
+        }
+      }
     }
   }
 }
 static void viv_reset_end(ds_view* d) {  /* :388-406 */
-  if (d->has_src && !d->run_all) d->tei = ds_align(d, d->next_dp.ts) + d->interval;
+  if (d->has_src && !d->run_all) {
+    if (d->cal) {
+      while (d->next_dp.ts >= d->tei) {
+        d->prev_cal = cal_step(d->prev_cal, d->cal, d->cal_n, 1);
+        d->next_cal = cal_step(d->next_cal, d->cal, d->cal_n, 1);
+        d->tei = d->next_cal;
+      }
+    } else {
+      d->tei = ds_align(d, d->next_dp.ts) + d->interval;
+    }
+  }
 }
 static void viv_move_to_next_interval(ds_view* d) { viv_init(d); viv_reset_end(d); }
 static void viv_seek(ds_view* d, int64_t ts) {  /* :415-437 */
-  if (d->run_all) v_seek(d->src, ts);
-  else v_seek(d->src, ds_align(d, ts + d->interval - 1));
+  if (d->run_all) {
+    v_seek(d->src, ts);
+  } else if (d->cal) {
+    int64_t sc = cal_prev(ts, d->cal_n, d->cal);
+    if (ts > sc) sc = cal_step(sc, d->cal, d->cal_n, 1);
+    v_seek(d->src, sc);
+  } else {
+    v_seek(d->src, ds_align(d, ts + d->interval - 1));
+  }
   d->initialized = 0;
 }
 static int64_t viv_interval_ts(ds_view* d) {  /* :440-452 */
   if (d->run_all) return d->tei;
+  if (d->cal) return d->prev_cal;
   return ds_align(d, d->tei - d->interval);
 }
 static int viv_has(void* c) {  /* :464-471 */
@@ -900,8 +1057,15 @@ static ref_dp ds_next(ref_view* v) {
       default: jthrow(TSDB_E_RUNTIME, "unhandled fill policy");
     }
   }
-  if (!d->run_all) d->timestamp += d->interval;
-  return dp_of_double(d->run_all ? d->qs : d->timestamp - d->interval, d->value);
+  if (d->run_all) return dp_of_double(d->qs, d->value);
+  if (d->cal) {   /* advance :280-286; timestamp() = previous_calendar :304-311 */
+    d->fprev_cal = cal_step(d->fprev_cal, d->cal, d->cal_n, 1);
+    d->fnext_cal = cal_step(d->fnext_cal, d->cal, d->cal_n, 1);
+    d->timestamp = d->fnext_cal;
+    return dp_of_double(d->fprev_cal, d->value);
+  }
+  d->timestamp += d->interval;
+  return dp_of_double(d->timestamp - d->interval, d->value);
 }
 static void ds_seek(ref_view* v, int64_t ts) { viv_seek((ds_view*)v, ts); }
 static void ds_destroy(ref_view* v) { ds_view* d = (ds_view*)v; ref_view_free(d->src); free(d); }
@@ -909,7 +1073,7 @@ static const view_vt DS_VT = {ds_has_next, ds_next, ds_seek, ds_destroy};
 
 static ref_view* make_downsampler(ref_view* src, int32_t function, int64_t interval_ms, int32_t fill,
                                   int32_t run_all, int64_t start_time, int64_t end_time,
-                                  int64_t query_start, int64_t query_end) {
+                                  int64_t query_start, int64_t query_end, int32_t calendar) {
   if (function == TSDB_AGG_NONE) jthrow(TSDB_E_ILLEGAL_ARGUMENT, "cannot use the NONE aggregator for downsampling");
   if (!run_all && interval_ms <= 0) jthrow(TSDB_E_ILLEGAL_ARGUMENT, "interval not > 0");
   ds_view* d = (ds_view*)xcalloc(1, sizeof(ds_view));
@@ -924,10 +1088,22 @@ static ref_view* make_downsampler(ref_view* src, int32_t function, int64_t inter
   d->filling = fill != TSDB_FILL_NONE;   /* Span.downsampler :545-560 */
   d->next_dp_null = 1;
   d->tei = run_all ? query_end : interval_ms;  /* ValuesInInterval() :318-324 */
+  if (calendar && !run_all) {   /* Downsampler ctor :131-142 */
+    if (calendar < TSDB_CAL_MS || calendar > TSDB_CAL_Y) jthrow(TSDB_E_ILLEGAL_ARGUMENT, "Unrecognized unit type");
+    d->cal = calendar;
+    d->cal_n = interval_ms / CAL_UNIT_MS[calendar];
+  }
   if (d->filling) {
     if (run_all) {
       d->timestamp = start_time;
       d->end_timestamp = end_time;
+    } else if (d->cal) {   /* FillingDownsampler ctor :113-135 */
+      d->fnext_cal = cal_prev(start_time, d->cal_n, d->cal);
+      d->fprev_cal = cal_step(d->fnext_cal, d->cal, d->cal_n, -1);
+      int64_t end_cal = cal_prev(end_time, d->cal_n, d->cal);
+      if (end_cal == d->fnext_cal) end_cal = cal_step(end_cal, d->cal, d->cal_n, 1);
+      d->timestamp = d->fnext_cal;
+      d->end_timestamp = end_cal;
     } else {
       d->timestamp = ds_align(d, start_time);
       d->end_timestamp = ds_align(d, end_time);
@@ -938,9 +1114,9 @@ static ref_view* make_downsampler(ref_view* src, int32_t function, int64_t inter
 
 ref_view* ref_view_downsampler(ref_view* src, int32_t function, int64_t interval_ms, int32_t fill,
                                int32_t run_all, int64_t start_time, int64_t end_time,
-                               int64_t query_start, int64_t query_end) {
+                               int64_t query_start, int64_t query_end, int32_t calendar) {
   ref_view* r = NULL;
-  TRY { r = make_downsampler(src, function, interval_ms, fill, run_all, start_time, end_time, query_start, query_end); }
+  TRY { r = make_downsampler(src, function, interval_ms, fill, run_all, start_time, end_time, query_start, query_end, calendar); }
   CATCH(e) { (void)e; r = NULL; } END_TRY
   return r;
 }
@@ -1329,12 +1505,17 @@ int ref_parse_downsample(const char* spec, tsdbhip_query* q) {
     q->ds_all = 1;
   } else {
     size_t l = strlen(parts[0]);
+    int cal = 0;
     if (l > 0 && parts[0][l - 1] == 'c') {
       parts[0][l - 1] = 0;
-      q->ds_calendar = 1;
+      cal = 1;
     }
     int rc = ref_parse_duration(parts[0], &q->ds_interval_ms);
     if (rc) return rc;
+    if (cal) {
+      q->ds_calendar = cal_unit_of(parts[0]);   /* DateTime.unitsToCalendarType :616-640 */
+      if (!q->ds_calendar) { snprintf(g_msg, sizeof g_msg, "Unrecognized unit type: %s", parts[0]); return TSDB_E_ILLEGAL_ARGUMENT; }
+    }
   }
   int f = ref_aggregator_get(parts[1]);
   if (f < 0) { snprintf(g_msg, sizeof g_msg, "No such downsampling function: %s", parts[1]); return TSDB_E_ILLEGAL_ARGUMENT; }
@@ -1442,7 +1623,7 @@ static void run_group(const query_env* env, group_job* g) {
       if (size == 0 || !(first <= env->scan_end_ms && last >= env->scan_start_ms)) { ref_view_free(it); continue; }
       if (has_downsampler(q)) {
         it = make_downsampler(it, q->ds_function, q->ds_interval_ms, q->ds_fill, q->ds_all,
-                              env->scan_start_ms, env->scan_end_ms, q->start_time, q->end_time);
+                              env->scan_start_ms, env->scan_end_ms, q->start_time, q->end_time, q->ds_calendar);
       }
       if (q->rate) it = ref_view_rate(it, q->rate_counter, q->rate_counter_max, q->rate_reset_value, q->rate_drop_resets);
       its[k++] = it;
@@ -1492,7 +1673,6 @@ static int run_query_impl(const tsdbhip_batch* b, const tsdbhip_query* q, int nt
   TRY {
     if (has_downsampler(q)) {
       if (q->ds_function == TSDB_AGG_NONE) jthrow(TSDB_E_ILLEGAL_ARGUMENT, "cannot use the NONE aggregator for downsampling");
-      if (q->ds_calendar) jthrow(TSDB_E_NOT_IMPLEMENTED, "calendar downsampling not implemented");
     }
     int64_t ss, se;
     ref_scan_bounds(q, &ss, &se);

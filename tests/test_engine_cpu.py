@@ -97,3 +97,15 @@ def test_host_synth_is_mockbase_encoding():
             assert base == b.row_base_time[row]
             assert q == bytes(b.qual[b.row_qual_off[row]:b.row_qual_off[row + 1]])
             assert v == bytes(b.val[b.row_val_off[row]:b.row_val_off[row + 1]])
+
+
+def test_calendar_spec_units_match_oracle():
+    """tsdbhip_parse_downsample records the calendar unit of a 'c' interval like the oracle
+    (DownsamplingSpecification :140-147 + DateTime.unitsToCalendarType :616-640)."""
+    from opentsdb_amd import engine
+    from oracle import oracle as O
+    for spec in ["1wc-sum", "1dc-avg-nan", "2nc-max", "1yc-sum", "500msc-sum", "30sc-avg", "15mc-min", "6hc-count",
+                 "1m-sum", "0all-sum"]:
+        a, b = engine.parse_downsample(spec), O.parse_downsample(spec)
+        assert (a.ds_calendar, a.ds_interval_ms, a.ds_fill, a.ds_all) == (b.ds_calendar, b.ds_interval_ms, b.ds_fill,
+                                                                          b.ds_all), spec
