@@ -786,6 +786,7 @@ struct Plan {
   bool raw = false;   // no downsampling: AggregationIterator over the raw timestamp union
   int gsel = 0;       // TSDB_AGG_* when the group-by aggregator is a percentile / median (0: none)
   bool no_inf = false;   // per-span pass feeding the percentile group-by: no +-Inf check
+  bool dense_out = false;   // grid kernels write per-series bucket values to pre_dense / pre_pres
 };
 
 bool is_sel_agg(int a) { return a == TSDB_AGG_MEDIAN || (a >= TSDB_AGG_P999 && a < TSDB_AGG_COUNT_ALL); }
@@ -921,6 +922,13 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   gp.group_active = c->gact.as<uint32_t>();
   gp.err = c->err.as<int32_t>();
   if (const char* dbg = std::getenv("TSDBHIP_DBG")) gp.dbg = std::atoi(dbg);
+  if (P.dense_out) {
+    HIP_OK(c->pre_dense.ensure(std::max<int64_t>(1, c->n_series * K) * 8));
+    HIP_OK(c->pre_pres.ensure(std::max<int64_t>(1, c->n_series * K)));
+    HIP_OK(hipMemsetAsync(c->pre_pres.p, 0, std::max<int64_t>(1, c->n_series * K), c->stream));
+    gp.dense_out = c->pre_dense.as<double>();
+    gp.pres_out = c->pre_pres.as<uint8_t>();
+  }
 
   if (P.f == F_SEL) {
     // percentile / median: per-series bucket order statistics, then the group-by step
@@ -1231,20 +1239,16 @@ int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G)
     int rc = run_device(c, q, P, G, false);   // k_pct -> pre_dense / pre_pres (no k_emit)
     if (rc) return rc;
   } else {
+    // the grid kernels over the group tiles, each series' Downsampler output (no rate: the
+    // SpanGroup step below applies it) written to pre_dense / pre_pres
     tsdbhip_query q2 = *q;
-    q2.aggregator = TSDB_AGG_NONE;
     q2.rate = 0;
-    q2.flags &= ~TSDB_QF_ORDERED;
     Plan P2;
     int rc = plan_query(c, &q2, P2);
     if (rc) return rc;
-    P2.no_inf = true;
-    rc = run_device(c, &q2, P2, S, true);
+    P2.dense_out = true;
+    rc = run_device(c, &q2, P2, G, false);
     if (rc) return rc;
-    if (S * K) {
-      HIP_OK(hipMemcpyAsync(c->pre_dense.p, c->out_val.p, S * K * 8, hipMemcpyDeviceToDevice, c->stream));
-      HIP_OK(hipMemcpyAsync(c->pre_pres.p, c->out_flag.p, S * K, hipMemcpyDeviceToDevice, c->stream));
-    }
   }
   const std::vector<int64_t> gsp = seg_ptr(local_counts(c, G));
   HIP_OK(c->sel_gsp.ensure((G + 1) * 8));

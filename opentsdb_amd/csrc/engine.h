@@ -123,6 +123,10 @@ struct GridParams {
   double* sel_vals;
   uint8_t* sel_uni;            // [G][K]: some series contributed with a real point (emit)
   const int64_t* group_series_ptr;   // [G + 1]
+  // non-null: the grid kernels write every series' bucket values / presence here
+  // ([series][K], before rate and fill) instead of its SpanGroup contributions
+  double* dense_out;
+  uint8_t* pres_out;
   int32_t dbg;           // k_short profiling switches (TSDBHIP_DBG, results invalid): 1 skip series end,
                          // 2 skip chunk fold, 8 consume loads, 16 stop after the descriptors, 32 load row 0 only
 };

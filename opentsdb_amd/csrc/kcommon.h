@@ -970,6 +970,21 @@ __device__ __forceinline__ void emit_series(const GridParams& p, const WaveLds& 
   emit_series_to(p, W, K, [&](int s, double v, bool uni) { contribute(ga, W.part, s, v, uni); });
 }
 
+// End of series s: its SpanGroup contributions, or (dense_out) its bucket values.
+__device__ __forceinline__ void series_out(const GridParams& p, const WaveLds& W, int K, int64_t s) {
+  if (p.dense_out) {
+    const int lane = lane_id();
+    WAVE_SYNC();
+    for (int k = lane; k < K; k += 64) {
+      p.dense_out[s * K + k] = W.dense[k];
+      p.pres_out[s * K + k] = W.pres[k];
+    }
+    WAVE_SYNC();
+    return;
+  }
+  emit_series(p, W, K);
+}
+
 // emit_series for K <= 64 without rate: lane k owns slot k; the series' bucket k arrives
 // in registers (pr, v) and the tile partial of slot k lives in the lane's registers, so
 // neither the bucket values nor the partials round-trip through LDS.  Same contributions,
@@ -1141,7 +1156,7 @@ __global__ __launch_bounds__(256) void k_grid(GridParams p) {
         }
       }
       if (slow) series_slow<F>(p, W, cs, K);
-      emit_series(p, W, K);
+      series_out(p, W, K, cs);
       // next series
       for (int k = lane; k < K; k += 64) W.pres[k] = 0;
       WAVE_SYNC();
@@ -1599,7 +1614,7 @@ __device__ __forceinline__ double fast_bucket_value(uint32_t c, double a) {
 // K <= 64, no rate: the register-partial variant (emit_series_reg).
 template <int F>
 __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const FastLds& L, int K, int lsb, double amax,
-                                                    RegPart& P, uint32_t nbound = 0) {
+                                                    RegPart& P, int64_t s, uint32_t nbound = 0) {
   const int lane = lane_id();
   WAVE_SYNC();
   uint32_t c = 0;
@@ -1614,7 +1629,14 @@ __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const F
     const uint32_t nmax = (uint32_t)wave_max((int)c);
     if (!fast_cert<F>(nmax, lsb, amax)) return false;
   }
-  emit_series_reg(p, K, c != 0, fast_bucket_value<F>(c, a), P);
+  if (p.dense_out) {
+    if (lane < K) {
+      p.dense_out[s * K + lane] = fast_bucket_value<F>(c, a);
+      p.pres_out[s * K + lane] = c != 0;
+    }
+  } else {
+    emit_series_reg(p, K, c != 0, fast_bucket_value<F>(c, a), P);
+  }
   if (lane < K) {
     L.acc[lane] = fast_identity<F>();
     L.cnt[lane] = 0;
@@ -1624,7 +1646,8 @@ __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const F
 }
 
 template <int F>
-__device__ __forceinline__ bool fast_series_end(const GridParams& p, const FastLds& L, int K, int lsb, double amax) {
+__device__ __forceinline__ bool fast_series_end(const GridParams& p, const FastLds& L, int K, int lsb, double amax,
+                                                int64_t s) {
   const int lane = lane_id();
   WAVE_SYNC();
   uint32_t nmax = 0;
@@ -1649,7 +1672,7 @@ __device__ __forceinline__ bool fast_series_end(const GridParams& p, const FastL
                                    (double)nmax * A * (1.0 + 1e-12) <= ldexp(1.0, 52 + Lb));
     if (!ok) return false;
   }
-  emit_series(p, L.w, K);
+  series_out(p, L.w, K, s);
   for (int k = lane; k < K; k += 64) {
     L.acc[k] = fast_identity<F>();
     L.cnt[k] = 0;
@@ -1704,6 +1727,7 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
   int lsb = INT32_MAX;
   double amax = 0.0;
   FGeom g = {0, 0};
+  int32_t last_rrel = 0;
   bool done = redo;
   while (!done) {
 #pragma unroll
@@ -1712,7 +1736,14 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
         const uint32_t mb = meta[i].bits;
         if (!(mb & FM_OK) || (mb & FM_NEWSER)) {
           if (have) {
-            const bool ok = KR ? fast_series_end_reg<F>(p, L, K, lsb, amax, RP) : fast_series_end<F>(p, L, K, lsb, amax);
+            int64_t s = -1;
+            if (p.dense_out) {   // the series of the last row folded (dense output only)
+              const int64_t row = w.r0 + last_rrel;
+              s = tbeg[tile];
+              while (s + 1 < tend[tile] && srp[s + 1] <= row) s++;
+            }
+            const bool ok =
+                KR ? fast_series_end_reg<F>(p, L, K, lsb, amax, RP, s) : fast_series_end<F>(p, L, K, lsb, amax, s);
             if (!ok) { redo = true; done = true; }
           }
           lsb = INT32_MAX;
@@ -1722,6 +1753,7 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
         }
         if (!done) {
           if (mb & FM_NEWROW) {
+            last_rrel = meta[i].rrel;
             const RowDesc& x = rows[w.r0 + meta[i].rrel];
             lsb = min(lsb, x.lsb);
             amax = fmax(amax, x.absmax);
@@ -1877,7 +1909,8 @@ __global__ __launch_bounds__(256, SHORT_OCC) void k_short(GridParams p, const Ro
     const int lsb = __builtin_amdgcn_readlane(dlsb, j);
     const double amax = __longlong_as_double((long long)rl64(damax, j));
     const bool fine =
-        KR ? fast_series_end_reg<F>(p, L, K, lsb, amax, RP, (uint32_t)nv0) : fast_series_end<F>(p, L, K, lsb, amax);
+        KR ? fast_series_end_reg<F>(p, L, K, lsb, amax, RP, s0 + j, (uint32_t)nv0)
+           : fast_series_end<F>(p, L, K, lsb, amax, s0 + j);
     if (!fine) redo = true;
   };
   int j = 0;

@@ -100,6 +100,7 @@ def main():
     ap.add_argument("--groups", type=int, default=64)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--cpu", action="store_true", help="time the oracle on one group")
+    ap.add_argument("--only", default="", help="comma-separated group-by aggregators to run (config 3)")
     args = ap.parse_args()
     from opentsdb_amd import abi, dist, synth
     from opentsdb_amd.engine import Engine, parse_downsample
@@ -113,7 +114,8 @@ def main():
         eng = Engine(0)
         series = args.series if args.series != 100_000 else 10_000_000
         groups = args.groups if args.groups != 64 else 1000
-        qs = {f"{a}:1m-avg": dsq(a, "1m-avg", T0 + 3599) for a in ["sum", "avg", "min", "max", "count", "dev"]}
+        aggs = args.only.split(",") if args.only else ["sum", "avg", "min", "max", "count", "dev", "p99", "median"]
+        qs = {f"{a}:1m-avg": dsq(a, "1m-avg", T0 + 3599) for a in aggs}
         grid_config(args, eng, qs, series, 360, 2, 30000, groups)
         eng.close()
         return
