@@ -229,12 +229,12 @@ int tsdbhip_finalize(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_
  *      n_slots = K;
  *   2. tsdbhip_sel_run_values: the local spans' contributions (Downsampler, RateSpan, fill,
  *      LERP -- what AggregationIterator hands runDouble) into
- *        double  vals[sum_g counts[g] * K]   group g at K * sum_{g'<g} counts[g'], then
- *                                            [k][i] (slot-major, i = span index; +NaN = none)
+ *        double  vals[sum_g counts[g] * K]   [span][slot], spans group by group in SpanGroup
+ *                                            order (a span's K values contiguous; +NaN = none)
  *        uint8_t uni[n_groups * K]           a real point of some span (emit flag)
  *        uint32_t act[n_groups]              the group has a span in the scan range;
- *   3. the caller moves each group's blocks to its owner (all-to-all over RCCL) and
- *      concatenates them per slot, OR-reduces uni / act;
+ *   3. the caller moves each group's block ([counts[g]][K]) to its owner (all-to-all over
+ *      RCCL), concatenates the ranks' blocks of a group span-wise, OR-reduces uni / act;
  *   4. tsdbhip_sel_select on the owner: same layout with the gathered counts, segments
  *      sorted and runDouble's order statistic taken -> dense out_val [n_groups * K] f64 and
  *      out_flag [n_groups * K] u8 (groups with count 0: NaN where uni is set);

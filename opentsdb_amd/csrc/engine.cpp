@@ -187,9 +187,7 @@ struct tsdbhip_ctx {
   DevBuf pa, pb, pn, pf, out_val, out_flag, gact, err, g_dense, g_pres, g_rate, redo, redo_n, redo2, redo2_n;
   DevBuf xbuf, gbuf;
   DevBuf pre_dense, pre_pres;          // percentile / median downsampling
-  DevBuf sel_vals, sel_sorted, sel_uni, sel_gsp, sel_beg, sel_end;   // percentile / median group-by
-  void* sel_tmp = nullptr;
-  size_t sel_tmp_bytes = 0;
+  DevBuf sel_vals, sel_sorted, sel_uni, sel_gsp;   // percentile / median group-by
   // raw path scratch
   DevBuf r_rowpt, r_spoff, r_spn, r_grp, r_pts, r_rank, r_bm, r_wb, r_U, r_ooff, r_sg, r_su, r_ots, r_obits, r_oint,
       r_coff, r_cur;                   // multi-GPU: this rank's partial states, gathered states
@@ -380,8 +378,7 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   for (auto& o : c->ro_out)
     for (DevBuf* b : {&o.series, &o.base, &o.qual, &o.voff, &o.val}) b->release();
   if (c->ro_tmp) (void)hipFree(c->ro_tmp);
-  for (DevBuf* b : {&c->sel_vals, &c->sel_sorted, &c->sel_uni, &c->sel_gsp, &c->sel_beg, &c->sel_end}) b->release();
-  if (c->sel_tmp) (void)hipFree(c->sel_tmp);
+  for (DevBuf* b : {&c->sel_vals, &c->sel_sorted, &c->sel_uni, &c->sel_gsp}) b->release();
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1212,8 +1209,8 @@ namespace {
 // Percentile / median as the group-by aggregator (downsampled queries):
 //  1. every series' bucket values: k_pct for a percentile / median downsample function,
 //     else a NONE-aggregator pass without rate (= each span's Downsampler output);
-//  2. k_emit_vals: the SpanGroup contributions (rate, fill, LERP) into (group, slot) segments;
-//  3. segmented radix sort; 4. k_sel_group: runDouble's order statistic per (group, slot).
+//  2. k_emit_vals: the SpanGroup contributions (rate, fill, LERP) per (series, slot);
+//  3. k_sel_seg: runDouble's order statistic per (group, slot) by radix select.
 // Group -> first value of its segments in the [g][k][i] layout: prefix of `counts`.
 std::vector<int64_t> seg_ptr(const std::vector<int64_t>& counts) {
   std::vector<int64_t> gsp(counts.size() + 1, 0);
@@ -1229,7 +1226,7 @@ std::vector<int64_t> local_counts(tsdbhip_ctx* c, int64_t G) {
 }
 
 // Stages 1-2 of the percentile / median group-by: every local span's contribution to each
-// (group, slot) into c->sel_vals ([g][k][i], NaN = none), c->sel_uni [G][K], c->gact [G].
+// (group, slot) into c->sel_vals ([series][K], NaN = none), c->sel_uni [G][K], c->gact [G].
 int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G) {
   const int64_t S = c->n_series, K = P.K;
   if (S * K > 0x7FFFFFFFLL) return fail(TSDB_E_NOT_IMPLEMENTED, "percentile group-by over more than 2^31 (series, slot) values");
@@ -1302,36 +1299,22 @@ int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G)
   return 0;
 }
 
-// Stages 3-4: sort the (group, slot) segments of `vals` (device, [g][k][i], counts[g] values
-// per slot of group g) and take each order statistic -> c->out_val / c->out_flag [G][K].
+// Stage 3: the order statistic of every (group, slot) column of `vals` (device,
+// [series][K] with counts[g] series in group g) -> c->out_val / c->out_flag [G][K].
 int sel_select(tsdbhip_ctx* c, const Plan& P, int64_t G, double* vals, const std::vector<int64_t>& counts,
                const uint8_t* uni) {
   const int64_t K = P.K;
   const std::vector<int64_t> gsp = seg_ptr(counts);
-  const int64_t n_items = gsp[G] * K;
-  if (n_items > 0x7FFFFFFFLL) return fail(TSDB_E_NOT_IMPLEMENTED, "percentile group-by over more than 2^31 values");
-  std::vector<int64_t> beg(std::max<int64_t>(1, G * K)), end(std::max<int64_t>(1, G * K));
-  for (int64_t g = 0; g < G; g++)
-    for (int64_t k = 0; k < K; k++) {
-      beg[g * K + k] = gsp[g] * K + k * counts[g];
-      end[g * K + k] = beg[g * K + k] + counts[g];
-    }
+  int64_t maxn = 0;
+  for (int64_t g = 0; g < G; g++) maxn = std::max(maxn, counts[g]);
   HIP_OK(c->sel_gsp.ensure((G + 1) * 8));
-  HIP_OK(c->sel_beg.ensure(std::max<int64_t>(1, G * K) * 8));
-  HIP_OK(c->sel_end.ensure(std::max<int64_t>(1, G * K) * 8));
-  HIP_OK(c->sel_sorted.ensure(std::max<int64_t>(1, n_items) * 8));
   HIP_OK(c->out_val.ensure(std::max<int64_t>(1, G * K) * 8));
   HIP_OK(c->out_flag.ensure(std::max<int64_t>(1, G * K)));
+  if (maxn > SEL_CAP) HIP_OK(c->sel_sorted.ensure(std::max<int64_t>(1, gsp[G] * K) * 8));   // key space
   HIP_OK(hipMemcpyAsync(c->sel_gsp.p, gsp.data(), (G + 1) * 8, hipMemcpyHostToDevice, c->stream));
-  if (G * K) {
-    HIP_OK(hipMemcpyAsync(c->sel_beg.p, beg.data(), G * K * 8, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(c->sel_end.p, end.data(), G * K * 8, hipMemcpyHostToDevice, c->stream));
-  }
-  hipError_t e = sort_segments(vals, c->sel_sorted.as<double>(), n_items, G * K, c->sel_beg.as<int64_t>(),
-                               c->sel_end.as<int64_t>(), &c->sel_tmp, &c->sel_tmp_bytes, c->stream);
-  if (e != hipSuccess) return fail(TSDB_E_HIP, std::string("segmented sort: ") + hipGetErrorString(e));
   SelParams sp{};
-  sp.sorted = c->sel_sorted.as<double>();
+  sp.vals = vals;
+  sp.scratch = maxn > SEL_CAP ? c->sel_sorted.as<double>() : nullptr;
   sp.uni = uni;
   sp.group_series_ptr = c->sel_gsp.as<int64_t>();
   sp.G = G;
@@ -1340,15 +1323,15 @@ int sel_select(tsdbhip_ctx* c, const Plan& P, int64_t G, double* vals, const std
   sp.out_val = c->out_val.as<double>();
   sp.out_flag = c->out_flag.as<uint8_t>();
   sp.err = c->err.as<int32_t>();
-  HIP_OK(launch_sel_group(sp, c->stream));
+  HIP_OK(launch_sel_seg(sp, c->stream));
   return 0;
 }
 
 // Percentile / median as the group-by aggregator (downsampled queries):
 //  1. every series' bucket values: k_pct for a percentile / median downsample function,
 //     else a NONE-aggregator pass without rate (= each span's Downsampler output);
-//  2. k_emit_vals: the SpanGroup contributions (rate, fill, LERP) into (group, slot) segments;
-//  3. segmented radix sort; 4. k_sel_group: runDouble's order statistic per (group, slot).
+//  2. k_emit_vals: the SpanGroup contributions (rate, fill, LERP) per (series, slot);
+//  3. k_sel_seg: runDouble's order statistic per (group, slot) by radix select.
 int run_sel_group(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G) {
   int rc = sel_values(c, q, P, G);
   if (rc) return rc;

@@ -117,9 +117,9 @@ struct GridParams {
   double* pre_dense;     // [n_series][K]
   uint8_t* pre_pres;     // [n_series][K]
   int32_t shortk;        // k_fast launch runs k_short (one row per series, descriptors up front)
-  // percentile / median as the group-by aggregator (k_emit_vals, k_sel_group): every
-  // series' contribution to slot k of group g goes to sel_vals[gsp[g] * K + k * n_g + i]
-  // (i = the series' index in the group, n_g = gsp[g + 1] - gsp[g]); NaN = no contribution
+  // percentile / median as the group-by aggregator (k_emit_vals, k_sel_seg): the value of
+  // span i of group g at slot k goes to sel_vals[(gsp[g] + i) * K + k] ([series][slot], the
+  // span's K values contiguous); NaN = no contribution
   double* sel_vals;
   uint8_t* sel_uni;            // [G][K]: some series contributed with a real point (emit)
   const int64_t* group_series_ptr;   // [G + 1]
@@ -143,10 +143,11 @@ struct ReduceParams {
   int32_t no_inf;                 // per-span pass feeding another aggregator: no +-Inf check
 };
 
-// Order statistic per (group, slot) over sorted value segments (percentile / median
-// group-by aggregator)
+// Order statistic per (group, slot) (percentile / median group-by aggregator): segment
+// (g, k) is vals[(gsp[g] + i) * K + k], i < gsp[g + 1] - gsp[g].
 struct SelParams {
-  const double* sorted;           // segments as GridParams.sel_vals, each sorted ascending
+  const double* vals;
+  double* scratch;                // [sum n_g * K] key space for segments longer than SEL_CAP
   const uint8_t* uni;             // [G][K]
   const int64_t* group_series_ptr;
   int64_t G, K;
@@ -155,6 +156,7 @@ struct SelParams {
   uint8_t* out_flag;
   int32_t* err;
 };
+static constexpr int SEL_CAP = 12288;   // values of one segment staged in LDS (96 KB)
 
 // Rank-ordered merge of all-gathered per-rank partial buffers (tsdbhip_finalize).
 struct RankMergeParams {
@@ -284,10 +286,7 @@ bool pct_rows_supported(int qw, int vl);
 hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s);
 hipError_t launch_emit(const GridParams& p, hipStream_t s);
 hipError_t launch_emit_vals(const GridParams& p, hipStream_t s);
-hipError_t launch_sel_group(const SelParams& p, hipStream_t s);
-// ascending sort of the (group, slot) value segments (hipCUB segmented radix sort)
-hipError_t sort_segments(const double* in, double* out, int64_t n_items, int64_t n_seg, const int64_t* d_begin,
-                         const int64_t* d_end, void** tmp, size_t* tmp_bytes, hipStream_t s);
+hipError_t launch_sel_seg(const SelParams& p, hipStream_t s);
 hipError_t launch_rank_merge(const RankMergeParams& p, hipStream_t s);
 // per-downsample-function instantiations (k_grid.hip / k_fast.hip, one object per F)
 template <int F> hipError_t launch_grid_inst(const GridParams& p, hipStream_t s);

@@ -12,8 +12,6 @@
 //            percentile uses commons-math3 3.4.1 LEGACY: pos = p (n + 1).
 //  * k_emit  one wave per tile: the bucket values -> SpanGroup contributions (LERP, fill,
 //            rate), exactly emit_series of k_grid, into tile partials for k_reduce.
-#include <hipcub/hipcub.hpp>
-
 #include "kcommon.h"
 
 #include <cstdlib>
@@ -742,11 +740,12 @@ bool pct_rows_supported(int qw, int vl) { return (qw == 2 || qw == 4) && (vl == 
 // span at every union timestamp (the span's bucket value, or its LERP between neighbouring
 // buckets; src/core/AggregationIterator.java:735-797), and runDouble drops NaNs
 // (src/core/Aggregators.java:689-706, :416-430).  k_emit_vals writes each series' value for
-// every slot into the (group, slot) segment (NaN = no value), a segmented sort orders the
-// segments, and k_sel_group takes the order statistic of the non-NaN prefix.
+// every slot ([series][slot], NaN = no value); k_sel_seg stages one (group, slot) column in
+// LDS as order-preserving integer keys and finds the one or two order statistics
+// select_sorted needs by an 8-pass radix select -- no sort.
 
 __device__ __forceinline__ double canon_nan(double v) {
-  return isnan(v) ? __longlong_as_double(0x7FF8000000000000LL) : v;   // +NaN sorts after +Inf
+  return isnan(v) ? __longlong_as_double(0x7FF8000000000000LL) : v;   // +NaN: the largest key
 }
 
 // One wave per tile (<= 64 series of one group).
@@ -757,9 +756,6 @@ __global__ __launch_bounds__(256) void k_emit_vals(GridParams p) {
   if (tile >= p.n_tiles) return;
   const int K = (int)p.K;
   const int32_t g = p.tile_group[tile];
-  const int64_t gs0 = p.group_series_ptr[g];
-  const int64_t ng = p.group_series_ptr[g + 1] - gs0;
-  double* seg = p.sel_vals + gs0 * K;
   uint8_t* uni = p.sel_uni + (int64_t)g * K;
   WaveLds W;
   W.rate = !p.rate ? nullptr : (p.g_rate ? p.g_rate + tile * K : (double*)(smem + (int64_t)wave * p.wave_lds));
@@ -774,37 +770,166 @@ __global__ __launch_bounds__(256) void k_emit_vals(GridParams p) {
     active = true;
     W.dense = p.pre_dense + s * K;
     W.pres = p.pre_pres + s * K;
-    const int64_t col = s - gs0;
+    double* row = p.sel_vals + s * K;
     emit_series_to(p, W, K, [&](int k, double v, bool u) {
-      seg[(int64_t)k * ng + col] = canon_nan(v);
+      row[k] = canon_nan(v);
       if (u) uni[k] = 1;
     });
   }
   if (active && lane_id() == 0) atomicOr(&p.group_active[g], 1u);
 }
 
-// One thread per (group, slot).
-__global__ __launch_bounds__(256) void k_sel_group(SelParams p) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= p.G * p.K) return;
+__device__ __forceinline__ uint64_t f2key(double x) {   // ascending double order == unsigned key order
+  const uint64_t b = (uint64_t)__double_as_longlong(x);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
+}
+__device__ __forceinline__ double key2f(uint64_t k) {
+  return __longlong_as_double((long long)((k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFULL) : ~k));
+}
+
+// The key of rank r (0-based, ascending) among keys[0..n): MSB-first radix select, 8 bits a
+// pass; the bin holding rank r is found by wave 0 with a prefix sum over its lanes' 4 bins,
+// and once at most SEL_FIN keys share the selected prefix they are gathered and ranked
+// directly (one thread per candidate).  Called by the whole block.
+constexpr int SEL_FIN = 256;
+struct SelShared {
+  uint32_t hist[256];
+  uint64_t cand[SEL_FIN];
+  uint64_t bin, rr, res;
+  uint32_t ncand;
+};
+__device__ uint64_t radix_select(const uint64_t* keys, int64_t n, int64_t r, SelShared& S) {
+  const int tid = threadIdx.x;
+  uint64_t prefix = 0, mask = 0;
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    for (int b = tid; b < 256; b += blockDim.x) S.hist[b] = 0;
+    __syncthreads();
+    for (int64_t j = tid; j < n; j += blockDim.x) {
+      const uint64_t k = keys[j];
+      if ((k & mask) == prefix) atomicAdd(&S.hist[(k >> shift) & 255], 1u);
+    }
+    __syncthreads();
+    if (tid < 64) {
+      uint32_t c[4], t = 0;
+#pragma unroll
+      for (int q = 0; q < 4; q++) { c[q] = S.hist[tid * 4 + q]; t += c[q]; }
+      const int64_t incl = wave_incl_sum((int)t);
+      int64_t ex = incl - t;
+      if (ex <= r && r < incl) {
+        int q = 0;
+        for (; q < 3; q++) {
+          if (r < ex + c[q]) break;
+          ex += c[q];
+        }
+        S.bin = (uint64_t)(tid * 4 + q);
+        S.rr = (uint64_t)(r - ex);
+        S.ncand = c[q];
+      }
+    }
+    __syncthreads();
+    prefix |= S.bin << shift;
+    mask |= 255ULL << shift;
+    r = (int64_t)S.rr;
+    const uint32_t nc = S.ncand;
+    __syncthreads();
+    if (shift == 0) break;
+    if (nc <= SEL_FIN) {
+      if (tid == 0) S.ncand = 0;
+      __syncthreads();
+      for (int64_t j = tid; j < n; j += blockDim.x) {
+        const uint64_t k = keys[j];
+        if ((k & mask) == prefix) S.cand[atomicAdd(&S.ncand, 1u)] = k;
+      }
+      __syncthreads();
+      if ((uint32_t)tid < nc) {
+        const uint64_t x = S.cand[tid];
+        uint32_t less = 0, eq = 0;
+        for (uint32_t q = 0; q < nc; q++) {
+          const uint64_t y = S.cand[q];
+          less += y < x;
+          eq += y == x;
+        }
+        if ((int64_t)less <= r && r < (int64_t)(less + eq)) S.res = x;
+      }
+      __syncthreads();
+      const uint64_t res = S.res;
+      __syncthreads();
+      return res;
+    }
+  }
+  return prefix;
+}
+
+// One block per (group, slot).  Blocks are dealt to the 8 XCDs in contiguous runs of
+// segments, so the K columns of one group (interleaved in memory) share an L2.
+__global__ __launch_bounds__(512) void k_sel_seg(SelParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ SelShared S;
+  __shared__ unsigned long long red[2];
+  const int64_t nseg = p.G * p.K;
+  const int64_t per = (nseg + 7) / 8;
+  const int64_t i = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (i >= nseg) return;
+  const int tid = threadIdx.x;
   if (!p.uni[i]) {
-    p.out_val[i] = 0.0;
-    p.out_flag[i] = 0;
+    if (tid == 0) { p.out_val[i] = 0.0; p.out_flag[i] = 0; }
     return;
   }
   const int64_t g = i / p.K, k = i - g * p.K;
-  const int64_t gs0 = p.group_series_ptr[g], ng = p.group_series_ptr[g + 1] - gs0;
-  const double* v = p.sorted + gs0 * p.K + k * ng;
-  int64_t lo = 0, hi = ng;   // NaNs sort last: n = values before the first NaN
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (isnan(v[mid])) hi = mid; else lo = mid + 1;
+  const int64_t gs0 = p.group_series_ptr[g], n = p.group_series_ptr[g + 1] - gs0;
+  uint64_t* keys = n <= SEL_CAP ? reinterpret_cast<uint64_t*>(smem) : reinterpret_cast<uint64_t*>(p.scratch) + gs0 * p.K + k * n;
+  if (tid == 0) red[0] = 0;
+  __syncthreads();
+  uint32_t nan_local = 0;
+  for (int64_t j = tid; j < n; j += blockDim.x) {
+    const double x = p.vals[(gs0 + j) * p.K + k];
+    nan_local += isnan(x) ? 1u : 0u;
+    keys[j] = f2key(canon_nan(x));
   }
-  const int n = (int)lo;
-  const double r = n == 0 ? (double)NAN : select_sorted(p.fn, n, [&](int j) { return v[j]; });
-  if (isinf(r)) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // AggregationIterator.doubleValue :640-643
-  p.out_val[i] = r;
-  p.out_flag[i] = 1;
+  if (nan_local) atomicAdd(&red[0], (unsigned long long)nan_local);
+  __syncthreads();
+  const int64_t m = n - (int64_t)red[0];   // non-NaN values (they hold ranks 0 .. m-1)
+  // the indices select_sorted reads (src/core/Aggregators.java runDouble; commons-math3 LEGACY)
+  int64_t r0 = 0, r1 = -1;
+  if (m > 0) {
+    if (p.fn == TSDB_AGG_MEDIAN) {
+      r0 = m / 2;
+    } else if (m > 1) {
+      const double q = pct_quantile(p.fn) / 100.0;
+      const double pos = (q == 0.0) ? 0.0 : (q == 1.0 ? (double)m : q * (double)(m + 1));
+      if (pos < 1) r0 = 0;
+      else if (pos >= (double)m) r0 = m - 1;
+      else { r0 = (int64_t)floor(pos) - 1; r1 = r0 + 1; }
+    }
+  }
+  double v0 = NAN, v1 = NAN;
+  if (m > 0) {
+    const uint64_t k0 = radix_select(keys, n, r0, S);
+    v0 = key2f(k0);
+    if (r1 >= 0) {
+      // rank r0 + 1: the same key when more than r0 + 1 keys are <= k0, else the next larger key
+      if (tid == 0) { red[0] = 0; red[1] = ~0ULL; }
+      __syncthreads();
+      uint32_t le = 0;
+      uint64_t gt = ~0ULL;
+      for (int64_t j = tid; j < n; j += blockDim.x) {
+        const uint64_t kk = keys[j];
+        if (kk <= k0) le++;
+        else gt = kk < gt ? kk : gt;
+      }
+      atomicAdd(&red[0], (unsigned long long)le);
+      atomicMin(&red[1], (unsigned long long)gt);
+      __syncthreads();
+      v1 = (int64_t)red[0] > r1 ? v0 : key2f(red[1]);
+    }
+  }
+  if (tid == 0) {
+    const double r = m == 0 ? (double)NAN
+                            : select_sorted(p.fn, (int)m, [&](int j) { return (int64_t)j == r0 ? v0 : v1; });
+    if (isinf(r)) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // AggregationIterator.doubleValue :640-643
+    p.out_val[i] = r;
+    p.out_flag[i] = 1;
+  }
 }
 
 hipError_t launch_emit_vals(const GridParams& p, hipStream_t s) {
@@ -819,30 +944,15 @@ hipError_t launch_emit_vals(const GridParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_sel_group(const SelParams& p, hipStream_t s) {
+hipError_t launch_sel_seg(const SelParams& p, hipStream_t s) {
   const int64_t n = p.G * p.K;
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_sel_group, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p);
-  return hipGetLastError();
-}
-
-hipError_t sort_segments(const double* in, double* out, int64_t n_items, int64_t n_seg, const int64_t* d_begin,
-                         const int64_t* d_end, void** tmp, size_t* tmp_bytes, hipStream_t s) {
-  if (n_items == 0 || n_seg == 0) return hipSuccess;
-  size_t need = 0;
-  hipError_t e = hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, need, in, out, (int)n_items, (int)n_seg,
-                                                            d_begin, d_end, 0, 64, s);
+  const int64_t per = (n + 7) / 8;
+  const size_t lds = (size_t)SEL_CAP * 8;
+  hipError_t e = hipFuncSetAttribute((const void*)k_sel_seg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  if (need > *tmp_bytes) {
-    if (*tmp) (void)hipFree(*tmp);
-    *tmp = nullptr;
-    *tmp_bytes = 0;
-    e = hipMalloc(tmp, need);
-    if (e != hipSuccess) return e;
-    *tmp_bytes = need;
-  }
-  return hipcub::DeviceSegmentedRadixSort::SortKeys(*tmp, need, in, out, (int)n_items, (int)n_seg, d_begin, d_end,
-                                                    0, 64, s);
+  hipLaunchKernelGGL(k_sel_seg, dim3((unsigned)(per * 8)), dim3(512), lds, s, p);
+  return hipGetLastError();
 }
 
 hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s) {

@@ -113,7 +113,8 @@ def sel_owner(n_groups: int, world: int):
 
 
 def sel_pack(vals, counts, K: int, world: int):
-    """This rank's [g][k][i] contribution buffer reordered by owning rank.
+    """This rank's [span][slot] contribution buffer (spans group by group) reordered by
+    owning rank.
 
     Returns (send, in_splits): `send` holds, for owner 0, 1, ..., the blocks of the groups
     it owns in increasing group order; in_splits[o] is the element count for owner o."""
@@ -132,9 +133,9 @@ def sel_pack(vals, counts, K: int, world: int):
 
 def sel_unpack(recv, counts_all, K: int, me: int):
     """The owner's side: `recv` holds, per source rank r (in rank order), r's blocks of the
-    groups `me` owns ([K][n_rg] each, increasing g).  Returns (vals, seg_counts): per owned
-    group the slots' values of every rank side by side ([g][k][j], j over all ranks' spans),
-    and the per-group span counts (0 for groups owned elsewhere)."""
+    groups `me` owns ([n_rg][K] each, increasing g).  Returns (vals, seg_counts): per owned
+    group every rank's spans one after the other ([g][j][k], j over all ranks' spans -- rank
+    order is SpanGroup order), and the per-group span counts (0 for groups owned elsewhere)."""
     import torch
     counts_all = np.asarray(counts_all, np.int64)
     world, G = counts_all.shape
@@ -146,15 +147,15 @@ def sel_unpack(recv, counts_all, K: int, me: int):
         for g in mine:
             n = int(counts_all[r, g])
             if n:
-                blocks.setdefault(int(g), []).append(recv[pos:pos + n * K].reshape(K, n))
+                blocks.setdefault(int(g), []).append(recv[pos:pos + n * K])
                 pos += n * K
     seg = np.zeros(G, np.int64)
     out = []
     for g in mine:
         if int(g) in blocks:
-            b = torch.cat(blocks[int(g)], dim=1)
-            seg[g] = b.shape[1]
-            out.append(b.reshape(-1))
+            b = torch.cat(blocks[int(g)])
+            seg[g] = b.numel() // K
+            out.append(b)
     vals = torch.cat(out) if out else recv[:0]
     return vals, seg
 

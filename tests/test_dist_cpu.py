@@ -129,8 +129,8 @@ def test_sel_pack_unpack_routes_every_value(world):
     for r in range(world):
         v = []
         for g in range(G):
-            for k in range(K):
-                for i in range(counts[r][g]):
+            for i in range(counts[r][g]):
+                for k in range(K):
                     v.append(r * 1e6 + g * 1e4 + k * 1e2 + i)
         vals.append(torch.tensor(v, dtype=torch.float64))
     outs = _emulate_sel_exchange(vals, counts, K)
@@ -142,10 +142,10 @@ def test_sel_pack_unpack_routes_every_value(world):
                 continue
             n = sum(int(counts[r][g]) for r in range(world))
             assert seg[g] == n
-            for k in range(K):
-                want = [r * 1e6 + g * 1e4 + k * 1e2 + i for r in range(world) for i in range(counts[r][g])]
-                np.testing.assert_array_equal(ov[pos:pos + n].numpy(), want)
-                pos += n
+            want = [r * 1e6 + g * 1e4 + k * 1e2 + i for r in range(world) for i in range(counts[r][g])
+                    for k in range(K)]
+            np.testing.assert_array_equal(ov[pos:pos + n * K].numpy(), want)
+            pos += n * K
         assert pos == ov.numel()
 
 
@@ -172,8 +172,8 @@ def _sel_gloo_worker(rank, world, port, out):
     try:
         G, K = 6, 3
         counts = np.array([(rank + g) % 3 for g in range(G)], np.int64)
-        vals = torch.tensor([rank * 1e6 + g * 1e4 + k * 1e2 + i for g in range(G) for k in range(K)
-                             for i in range(counts[g])], dtype=torch.float64)
+        vals = torch.tensor([rank * 1e6 + g * 1e4 + k * 1e2 + i for g in range(G) for i in range(counts[g])
+                             for k in range(K)], dtype=torch.float64)
         c_all = torch.empty(world * G, dtype=torch.int64)
         td.all_gather_into_tensor(c_all, torch.as_tensor(counts))
         counts_all = c_all.numpy().reshape(world, G)
@@ -203,8 +203,7 @@ def test_sel_exchange_gloo_two_ranks(tmp_path):
         for g in range(G):
             if g % 2 != me:
                 continue
-            for k in range(K):
-                want += [r * 1e6 + g * 1e4 + k * 1e2 + i for r in range(2) for i in range(ca[r, g])]
+            want += [r * 1e6 + g * 1e4 + k * 1e2 + i for r in range(2) for i in range(ca[r, g]) for k in range(K)]
         np.testing.assert_array_equal(z["ov"], want)
 
 

@@ -123,3 +123,13 @@ def test_pct_group_without_downsampling_not_implemented(eng, mixed_batch):
     with pytest.raises(Exception) as ei:
         eng.run_batch(mixed_batch, q)
     assert "notimplemented" in str(ei.value).lower().replace(" ", "")
+
+
+def test_pct_group_segment_beyond_lds(eng):
+    """One group of 13000 spans: each (group, slot) column exceeds the LDS stage (SEL_CAP =
+    12288 values) and is selected in the global-memory key space."""
+    eng.synth(13000, T0, 360, 10000, 2, 1, 30000, 0x5EED)
+    b = eng.download()
+    for agg in ["p99", "median", "p50"]:
+        q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["avg"], ds_interval_ms=300000)
+        assert_groups_match(eng.run(q), O.run_query(b, q), agg, tol=0.0, ctx=agg)
