@@ -133,6 +133,40 @@ bool cal_grid(int unit, int64_t interval_ms, int64_t* W, int64_t* O) {
   return true;
 }
 
+// Month-based calendar intervals (UTC): n months (12 % n == 0) or 1 year, anchored at the
+// top of the year (DateTime.previousInterval :580-588), so every span sees the same grid.
+// Month index m = 12 * year + (month - 1) <-> first instant of that month (ms).
+int64_t month_start_ms(int64_t m) {
+  int64_t y = floor_div(m, 12);
+  const int mo = (int)(m - y * 12) + 1;
+  y -= mo <= 2;   // days_from_civil
+  const int64_t era = floor_div(y, 400);
+  const int64_t yoe = y - era * 400;
+  const int64_t doy = (153 * (mo + (mo > 2 ? -3 : 9)) + 2) / 5;
+  const int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  return (era * 146097 + doe - 719468) * 86400000LL;
+}
+int64_t month_of_ms(int64_t t) {   // month index containing t
+  int64_t m = floor_div(floor_div(t, 86400000LL) * 4800, 146097) + 1970 * 12;   // estimate (days / 30.44)
+  while (month_start_ms(m) > t) m--;
+  while (month_start_ms(m + 1) <= t) m++;
+  return m;
+}
+bool cal_months(int unit, int64_t interval_ms, int64_t* step_months) {
+  if (unit == TSDB_CAL_N) {
+    const int64_t n = interval_ms / CAL_UNIT_MS[TSDB_CAL_N];
+    if (n < 1 || n * CAL_UNIT_MS[TSDB_CAL_N] != interval_ms || 12 % n) return false;
+    *step_months = n;
+    return true;
+  }
+  if (unit == TSDB_CAL_Y) {
+    if (interval_ms != CAL_UNIT_MS[TSDB_CAL_Y]) return false;
+    *step_months = 12;
+    return true;
+  }
+  return false;
+}
+
 // bytes past the end of the qualifier / value blobs that kernels may read (never use):
 // k_fast's vle class loads a 1 KB value window from each row start
 constexpr int64_t BLOB_SLACK = 1024 + 64;
@@ -188,6 +222,7 @@ struct tsdbhip_ctx {
   DevBuf xbuf, gbuf;
   DevBuf pre_dense, pre_pres;          // percentile / median downsampling
   DevBuf sel_vals, sel_sorted, sel_uni, sel_gsp;   // percentile / median group-by
+  DevBuf cal_bounds;                                // calendar month / year slot boundaries
   // raw path scratch
   DevBuf r_rowpt, r_spoff, r_spn, r_grp, r_pts, r_rank, r_bm, r_wb, r_U, r_ooff, r_sg, r_su, r_ots, r_obits, r_oint,
       r_coff, r_cur;                   // multi-GPU: this rank's partial states, gathered states
@@ -378,7 +413,7 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   for (auto& o : c->ro_out)
     for (DevBuf* b : {&o.series, &o.base, &o.qual, &o.voff, &o.val}) b->release();
   if (c->ro_tmp) (void)hipFree(c->ro_tmp);
-  for (DevBuf* b : {&c->sel_vals, &c->sel_sorted, &c->sel_uni, &c->sel_gsp}) b->release();
+  for (DevBuf* b : {&c->sel_vals, &c->sel_sorted, &c->sel_uni, &c->sel_gsp, &c->cal_bounds}) b->release();
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -784,6 +819,8 @@ struct Plan {
   int gsel = 0;       // TSDB_AGG_* when the group-by aggregator is a percentile / median (0: none)
   bool no_inf = false;   // per-span pass feeding the percentile group-by: no +-Inf check
   bool dense_out = false;   // grid kernels write per-series bucket values to pre_dense / pre_pres
+  std::vector<int64_t> bounds;   // MODE_TABLE: K + 1 calendar slot boundaries (ms)
+  int64_t seek = 0;              // MODE_TABLE: first timestamp the spans' Downsamplers read
 };
 
 bool is_sel_agg(int a) { return a == TSDB_AGG_MEDIAN || (a >= TSDB_AGG_P999 && a < TSDB_AGG_COUNT_ALL); }
@@ -805,10 +842,14 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
     return 0;
   }
   if (!q->ds_all && q->ds_interval_ms <= 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "interval not > 0");
-  int64_t calW = 0, calO = 0;
-  if (q->ds_calendar && !q->ds_all && !cal_grid(q->ds_calendar, q->ds_interval_ms, &calW, &calO))
-    return fail(TSDB_E_NOT_IMPLEMENTED, "calendar interval without a global UTC grid (months, years, or an "
-                                        "interval that does not divide its unit) is not implemented yet");
+  int64_t calW = 0, calO = 0, calM = 0;
+  bool table = false;
+  if (q->ds_calendar && !q->ds_all && !cal_grid(q->ds_calendar, q->ds_interval_ms, &calW, &calO)) {
+    if (!cal_months(q->ds_calendar, q->ds_interval_ms, &calM))
+      return fail(TSDB_E_NOT_IMPLEMENTED, "calendar interval anchored per span (one that does not divide its "
+                                          "unit) is not implemented yet");
+    table = true;
+  }
   P.ga = ga_of(q->aggregator);
   P.f = f_of(q->ds_function);
   if (P.f < 0 && (q->ds_function == TSDB_AGG_MEDIAN || q->ds_function >= TSDB_AGG_P999)) P.f = F_SEL;
@@ -833,7 +874,35 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
     P.mode = MODE_GRID;
     const int64_t I = q->ds_interval_ms;
     P.I = I;
-    if (q->ds_calendar) {
+    if (table) {
+      // slot boundaries of the month grid: first slot = seekInterval(scan start) :420-432
+      P.mode = MODE_TABLE;
+      auto mprev = [&](int64_t t) {   // previousInterval: the n-month block of t, from January
+        const int64_t m = month_of_ms(t);
+        const int64_t y = floor_div(m, 12);
+        return y * 12 + floor_div(m - y * 12, calM) * calM;
+      };
+      const int64_t f0 = mprev(S0);
+      const int64_t m0 = month_start_ms(f0) == S0 ? f0 : f0 + calM;
+      int64_t mbeg = m0, mend;   // first slot's month, first month index not covered
+      if (q->ds_fill != TSDB_FILL_NONE) {
+        // FillingDownsampler :113-135 emits from previousInterval(start); a leading block
+        // before the seek point gets no points (fill value only)
+        mbeg = f0;
+        int64_t eC = mprev(E0);
+        if (eC == f0) eC += calM;
+        mend = eC;
+      } else {
+        mend = m0;
+        while (month_start_ms(mend) < E0) mend += calM;
+      }
+      P.seek = month_start_ms(m0);
+      P.bounds.clear();
+      for (int64_t m = mbeg; m <= mend; m += calM) P.bounds.push_back(month_start_ms(m));
+      if (P.bounds.size() < 2) { P.bounds.assign(1, month_start_ms(m0)); P.K = 0; }
+      else P.K = (int64_t)P.bounds.size() - 1;
+      P.B0 = P.bounds[0];
+    } else if (q->ds_calendar) {
       // Downsampler.seekInterval :420-432 (previousInterval, next one if the seek time is
       // past it); FillingDownsampler ctor :113-135: buckets from previousInterval(start) to
       // previousInterval(end), one bucket when both are the same.
@@ -841,11 +910,20 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
       const int64_t f0 = cfloor(S0);
       P.B0 = f0 == S0 ? S0 : f0 + I;
       if (q->ds_fill != TSDB_FILL_NONE) {
-        if (f0 < P.B0)
-          return fail(TSDB_E_NOT_IMPLEMENTED, "filled calendar interval starting before the scan start (weeks)");
         int64_t eC = cfloor(E0);
         if (eC == f0) eC += I;
-        P.K = eC > P.B0 ? (eC - P.B0) / I : 0;
+        if (f0 < P.B0) {
+          // a leading slot before the seek point (weeks): a boundary table whose slot 0
+          // receives no points
+          P.mode = MODE_TABLE;
+          P.seek = P.B0;
+          P.bounds.clear();
+          for (int64_t t = f0; t <= eC; t += I) P.bounds.push_back(t);
+          P.K = (int64_t)P.bounds.size() - 1;
+          P.B0 = f0;
+        } else {
+          P.K = eC > P.B0 ? (eC - P.B0) / I : 0;
+        }
       } else {
         P.K = E0 > P.B0 ? (E0 - P.B0 + I - 1) / I : 0;
       }
@@ -859,6 +937,8 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
       }
     }
   }
+  if (P.mode == MODE_TABLE && P.f == F_SEL)
+    return fail(TSDB_E_NOT_IMPLEMENTED, "percentile downsampling over variable-width calendar slots");
   // slot arrays live in LDS when they fit next to 4 waves' worth of staging, else in HBM
   P.gslot = grid_wave_lds(P.K, q->rate != 0, false) > 40 * 1024;
   return 0;
@@ -899,6 +979,13 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   gp.ga = P.ga;
   gp.interp = P.interp;
   gp.fill = q->ds_fill;
+  if (P.mode == MODE_TABLE) {
+    HIP_OK(c->cal_bounds.ensure((int64_t)P.bounds.size() * 8));
+    HIP_OK(hipMemcpyAsync(c->cal_bounds.p, P.bounds.data(), P.bounds.size() * 8, hipMemcpyHostToDevice, c->stream));
+    gp.bounds = c->cal_bounds.as<int64_t>();
+    gp.seek_ms = P.seek;
+    gp.skip0 = P.bounds[0] < P.ss * 1000 ? 1 : 0;
+  }
   gp.rate = q->rate;
   gp.counter = q->rate_counter;
   gp.drop = q->rate_drop_resets;
@@ -1190,7 +1277,7 @@ int assemble(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, c
     for (int64_t k = 0; k < K; k++) {
       if (!flag[row * K + k]) continue;
       // only points inside [start_time, end_time] of the SpanGroup are produced (x <= end_time)
-      ts[o] = (P.mode == MODE_ALL) ? q->start_time : P.B0 + k * P.I;
+      ts[o] = (P.mode == MODE_ALL) ? q->start_time : (P.mode == MODE_TABLE ? P.bounds[k] : P.B0 + k * P.I);
       std::memcpy(&vb[o], &val[row * K + k], 8);
       isi[o] = 0;   // downsampled values are always doubles (Downsampler.isInteger, :259-262)
       o++;
@@ -1275,6 +1362,13 @@ int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G)
   gp.ga = P.ga;
   gp.interp = P.interp;
   gp.fill = q->ds_fill;
+  if (P.mode == MODE_TABLE) {
+    HIP_OK(c->cal_bounds.ensure((int64_t)P.bounds.size() * 8));
+    HIP_OK(hipMemcpyAsync(c->cal_bounds.p, P.bounds.data(), P.bounds.size() * 8, hipMemcpyHostToDevice, c->stream));
+    gp.bounds = c->cal_bounds.as<int64_t>();
+    gp.seek_ms = P.seek;
+    gp.skip0 = P.bounds[0] < P.ss * 1000 ? 1 : 0;
+  }
   gp.rate = q->rate;
   gp.counter = q->rate_counter;
   gp.drop = q->rate_drop_resets;

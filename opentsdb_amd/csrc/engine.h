@@ -51,7 +51,7 @@ struct Partials {
 enum : uint32_t { PF_UNION = 1u, PF_HAS = 2u };
 
 // Kernel modes
-enum : int { MODE_GRID = 0, MODE_ALL = 1 };
+enum : int { MODE_GRID = 0, MODE_ALL = 1, MODE_TABLE = 2 };   // TABLE: slot k = [bounds[k], bounds[k+1]) (calendar months / years)
 
 // Group-aggregator classes (cross-series reduction)
 enum : int {
@@ -83,6 +83,10 @@ struct GridParams {
   int64_t I;             // interval
   int64_t K;             // slots
   int64_t qs, qe;        // "all" bounds (raw query start/end)
+  const int64_t* bounds; // MODE_TABLE: K + 1 slot boundaries (ms)
+  int64_t seek_ms;       // MODE_TABLE: points before this are skipped (Downsampler.seekInterval)
+  int32_t skip0;         // MODE_TABLE: slot 0 lies before the SpanGroup start (a filled leading
+                         // bucket): it feeds RateSpan but AggregationIterator drops it
   float rcpI;            // 1/I as float (slot division)
   int32_t mode;          // MODE_*
   int32_t ga;            // GA_*

@@ -146,6 +146,16 @@ __device__ __forceinline__ int slot_of(const GridParams& p, const RowGeom& g, ui
     const int64_t ts = (int64_t)base * 1000 + off_ms;
     return (ts >= p.qs && ts < p.qe) ? 0 : -1;
   }
+  if (p.mode == MODE_TABLE) {   // variable-width calendar slots: bounds[lo] <= ts < bounds[lo + 1]
+    const int64_t ts = (int64_t)base * 1000 + off_ms;
+    if (ts < p.seek_ms || ts < p.bounds[0] || ts >= p.bounds[p.K]) return -1;
+    int lo = 0, hi = (int)p.K;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (p.bounds[mid] <= ts) lo = mid; else hi = mid;
+    }
+    return lo;
+  }
   const int64_t n = g.r0 + (int64_t)off_ms;
   if (n < 0) return -1;
   int64_t q;
@@ -350,10 +360,15 @@ __device__ __forceinline__ void regpart_init(int ga, RegPart& P) {
 }
 
 // Interpolation of a missing slot (AggregationIterator.nextDoubleValue, :773-793)
+// timestamp of slot k relative to slot 0 (ms)
+__device__ __forceinline__ long long slot_rel(const GridParams& p, int k) {
+  return p.mode == MODE_TABLE ? (long long)(p.bounds[k] - p.bounds[0]) : (long long)k * p.I;
+}
+
 __device__ __forceinline__ double interp(int method, const GridParams& p, int k0, double y0, int k1, double y1, int k) {
   switch (method) {
     case TSDB_INTERP_LERP: {
-      const long long x = (long long)k * p.I, x0 = (long long)k0 * p.I, x1 = (long long)k1 * p.I;
+      const long long x = slot_rel(p, k), x0 = slot_rel(p, k0), x1 = slot_rel(p, k1);
       return y0 + (double)(x - x0) * (y1 - y0) / (double)(x1 - x0);
     }
     case TSDB_INTERP_ZIM: return 0.0;
@@ -870,11 +885,12 @@ __device__ __forceinline__ void emit_series_to(const GridParams& p, const WaveLd
   const double fillv = (p.fill == TSDB_FILL_ZERO) ? 0.0 : (double)NAN;
   WAVE_SYNC();
   if (!p.rate) {
-    if (p.fill != TSDB_FILL_NONE && p.mode == MODE_GRID) {
+    if (p.fill != TSDB_FILL_NONE && p.mode != MODE_ALL) {
       // FillingDownsampler (:172-301): every slot, missing -> NaN / 0 / RuntimeException
       for (int k = lane; k < K; k += 64) {
         const bool pr = W.pres[k] != 0;
         if (!pr && p.fill == TSDB_FILL_SCALAR) set_err(p.err, TSDB_E_RUNTIME);
+        if (k == 0 && p.skip0) continue;   // before start_time: AggregationIterator ctor :424-441
         put(k, pr ? W.dense[k] : fillv, true);
       }
     } else {
@@ -902,7 +918,7 @@ __device__ __forceinline__ void emit_series_to(const GridParams& p, const WaveLd
     // (AggregationIterator ctor rate branch :448-459, nextDoubleValue :744-753)
     int prev_item = -1, last_surv = -1;
     long long nsurv = 0;
-    const bool dense_stream = p.fill != TSDB_FILL_NONE && p.mode == MODE_GRID;
+    const bool dense_stream = p.fill != TSDB_FILL_NONE && p.mode != MODE_ALL;
     for (int kb = 0; kb < K; kb += 64) {
       const int k = kb + lane;
       const bool inK = k < K;
@@ -919,8 +935,8 @@ __device__ __forceinline__ void emit_series_to(const GridParams& p, const WaveLd
         const double v1 = pr ? W.dense[k] : fillv;
         double v0 = 0.0;
         long long t0 = 0;
-        if (pi >= 0) { v0 = W.pres[pi] ? W.dense[pi] : fillv; t0 = p.B0 + (long long)pi * p.I; }
-        const long long t1 = (p.mode == MODE_ALL) ? p.qs : p.B0 + (long long)k * p.I;
+        if (pi >= 0) { v0 = W.pres[pi] ? W.dense[pi] : fillv; t0 = p.B0 + slot_rel(p, pi); }
+        const long long t1 = (p.mode == MODE_ALL) ? p.qs : p.B0 + slot_rel(p, k);
         if (t1 <= t0) set_err(p.err, TSDB_E_ILLEGAL_STATE);
         const double dt = (double)(t1 - t0) / 1000.0;
         double diff = v1 - v0;
@@ -936,6 +952,7 @@ __device__ __forceinline__ void emit_series_to(const GridParams& p, const WaveLd
         } else {
           r = diff / dt;
         }
+        if (k == 0 && p.skip0) sv = false;   // its rate is dropped with the point (ctor :424-441)
         if (sv) W.rate[k] = r;
       }
       WAVE_SYNC();
@@ -993,7 +1010,7 @@ __device__ __forceinline__ void emit_series_reg(const GridParams& p, int K, bool
   const int lane = lane_id();
   const bool inK = lane < K;
   const bool pr = inK && pr_in;
-  if (p.fill != TSDB_FILL_NONE && p.mode == MODE_GRID) {
+  if (p.fill != TSDB_FILL_NONE && p.mode != MODE_ALL) {
     // FillingDownsampler (:172-301): every slot, missing -> NaN / 0 / RuntimeException
     const double fillv = (p.fill == TSDB_FILL_ZERO) ? 0.0 : (double)NAN;
     if (inK) {

@@ -4,8 +4,9 @@ DateTime.previousInterval / the calendar Downsampler and FillingDownsampler
 src/core/FillingDownsampler.java:113-135,280-286).  The oracle's calendar arithmetic is
 pinned by tests/golden/calendar.json (TestDownsampler's UTC cases); here the engine is
 checked against the oracle on multi-series stores.  The engine takes the intervals whose
-UTC grid is one global sequence (ms / s / m / h dividing their unit, 1d, 1w) and refuses
-months, years and per-span anchored intervals with NOT_IMPLEMENTED."""
+UTC grid is one global sequence: ms / s / m / h dividing their unit, 1d, 1w (fixed width),
+and n months with 12 % n == 0 or 1 year (a slot-boundary table); per-span anchored intervals
+and percentile downsampling over months return NOT_IMPLEMENTED."""
 from __future__ import annotations
 
 import pytest
@@ -61,19 +62,45 @@ def test_calendar_days_weeks(eng, week_batch, spec):
     assert_groups_match(eng.run_batch(week_batch, q), O.run_query(week_batch, q), "sum", ctx=spec)
 
 
-@pytest.mark.parametrize("spec", ["1dc-sum-nan", "1hc-avg-zero", "15mc-max-null", "1dc-count-zero"])
+@pytest.mark.parametrize("spec", ["1dc-sum-nan", "1hc-avg-zero", "15mc-max-null", "1dc-count-zero", "1wc-sum-nan",
+                                  "1wc-avg-zero"])
 def test_calendar_fill(eng, week_batch, spec):
     q = q_of(spec, T0 + 3 * 86400, T0 + 10 * 86400 - 1, "sum")
     assert_groups_match(eng.run_batch(week_batch, q), O.run_query(week_batch, q), "sum", ctx=spec)
 
 
-def test_calendar_rate(eng, hour_batch):
+def test_calendar_rate(eng, hour_batch, week_batch):
     q = q_of("5mc-avg", T0, T0 + 3599, "sum")
     q.rate = 1
     assert_groups_match(eng.run_batch(hour_batch, q), O.run_query(hour_batch, q), "sum", ctx="rate")
+    for spec in ["1wc-avg-zero", "1wc-sum-nan", "1dc-max-zero"]:   # leading filled week feeds the first rate
+        q = q_of(spec, T0 + 3 * 86400, T0 + 20 * 86400 - 1, "sum")
+        q.rate = 1
+        assert_groups_match(eng.run_batch(week_batch, q), O.run_query(week_batch, q), "sum", ctx=f"rate {spec}")
 
 
-@pytest.mark.parametrize("spec", ["1nc-sum", "1yc-sum", "7sc-sum", "2wc-sum", "2dc-sum"])
+@pytest.fixture(scope="module")
+def year_batch():
+    # 14 months @6 h from 2012-12-01 (leap-year February 2012 is before; 2013 is not leap)
+    return synth.generate(12, T0 - 31 * 86400, 14 * 30 * 4, 6 * 3600000, value_kind=2, n_groups=2, int_mod=1000,
+                          seed=8)
+
+
+@pytest.mark.parametrize("spec", ["1nc-sum", "1nc-avg", "2nc-max", "3nc-count", "6nc-sum", "1yc-sum", "1nc-dev",
+                                  "1nc-sum-nan", "1nc-avg-zero"])
+@pytest.mark.parametrize("agg", ["sum", "p90", "min"])
+def test_calendar_months_years(eng, year_batch, spec, agg):
+    q = q_of(spec, T0 - 31 * 86400, T0 + 400 * 86400, agg)
+    assert_groups_match(eng.run_batch(year_batch, q), O.run_query(year_batch, q), agg, ctx=f"{spec} {agg}")
+
+
+def test_calendar_months_rate(eng, year_batch):
+    q = q_of("1nc-avg", T0 - 31 * 86400, T0 + 400 * 86400, "sum")
+    q.rate = 1
+    assert_groups_match(eng.run_batch(year_batch, q), O.run_query(year_batch, q), "sum", ctx="rate")
+
+
+@pytest.mark.parametrize("spec", ["7sc-sum", "2wc-sum", "2dc-sum", "5nc-sum", "2yc-sum", "1nc-p99", "1wc-p99-nan"])
 def test_calendar_without_global_grid_not_implemented(eng, hour_batch, spec):
     q = q_of(spec, T0, T0 + 3599, "sum")
     with pytest.raises(Exception) as ei:
