@@ -203,6 +203,7 @@ struct tsdbhip_ctx {
   int64_t n_series = 0, n_rows = 0, n_groups = 0;
   uint64_t qual_bytes = 0, val_bytes = 0;
   DevBuf rows, srp, qual, val, gid;
+  DevBuf val2;                         // int16 copy of vle-integer values (k_index), at qualifier offsets
   std::vector<int64_t> h_srp;          // [n_series+1]
   std::vector<uint32_t> h_base;        // [n_rows]
   std::vector<uint32_t> h_ndp;         // [n_rows]
@@ -391,7 +392,7 @@ extern "C" int tsdbhip_init(int device, tsdbhip_ctx** out) {
 }
 
 static void release_batch(tsdbhip_ctx* c) {
-  for (DevBuf* b : {&c->rows, &c->srp, &c->qual, &c->val, &c->gid, &c->d_tb, &c->d_te, &c->d_tg, &c->d_gtp,
+  for (DevBuf* b : {&c->rows, &c->srp, &c->qual, &c->val, &c->val2, &c->gid, &c->d_tb, &c->d_te, &c->d_tg, &c->d_gtp,
                     &c->n_tb, &c->n_te, &c->n_tg, &c->n_gtp})
     b->release();
   c->none_tiles_ready = false;
@@ -523,12 +524,25 @@ static int build_none_tiles(tsdbhip_ctx* c) {
 static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
   // classify rows on the device, then fetch ndp for host-side accounting
   HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
-  HIP_OK(launch_index(c->qual.as<uint8_t>(), c->val.as<uint8_t>(), c->rows.as<RowDesc>(), c->n_rows,
+  HIP_OK(launch_index(c->qual.as<uint8_t>(), c->val.as<uint8_t>(), nullptr, c->rows.as<RowDesc>(), c->n_rows,
                       c->err.as<int32_t>(), c->stream));
   std::vector<RowDesc> back(c->n_rows);
   if (c->n_rows)
     HIP_OK(hipMemcpyAsync(back.data(), c->rows.p, c->n_rows * sizeof(RowDesc), hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
+  // rows of the vle-integer class (2-byte qualifiers, 1-2-byte integers): a second pass
+  // writes their values as int16 at the qualifier offsets (val2), the layout k_short /
+  // k_fast read -- allocated only when such rows exist
+  bool need_val2 = false;
+  for (const RowDesc& d : back)
+    if ((d.flags & (ROW_QW_MASK | ROW_ALLI | ROW_VLE2 | ROW_ERR)) == (2u | ROW_ALLI | ROW_VLE2)) { need_val2 = true; break; }
+  c->val2.release();
+  if (need_val2) {
+    HIP_OK(c->val2.ensure(c->qual_bytes + BLOB_SLACK));
+    HIP_OK(launch_index(c->qual.as<uint8_t>(), c->val.as<uint8_t>(), c->val2.as<uint8_t>(), c->rows.as<RowDesc>(),
+                        c->n_rows, c->err.as<int32_t>(), c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+  }
   (void)rd;
   c->h_ndp.resize(c->n_rows);
   c->h_base.resize(c->n_rows);
@@ -963,6 +977,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   gp.series_row_ptr = c->srp.as<int64_t>();
   gp.qual = c->qual.as<uint8_t>();
   gp.val = c->val.as<uint8_t>();
+  gp.val2 = c->val2.as<uint8_t>();
   gp.tile_begin = (none ? c->n_tb : c->d_tb).as<int64_t>();
   gp.tile_end = (none ? c->n_te : c->d_te).as<int64_t>();
   gp.tile_group = (none ? c->n_tg : c->d_tg).as<int32_t>();

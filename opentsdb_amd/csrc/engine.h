@@ -71,6 +71,7 @@ struct GridParams {
   const int64_t* series_row_ptr;
   const uint8_t* qual;
   const uint8_t* val;
+  const uint8_t* val2;   // int16 copy of 1-2-byte integer values, at the row's qualifier offset
   // tiles: series [tile_begin[t], tile_end[t]) of group tile_group[t]
   const int64_t* tile_begin;
   const int64_t* tile_end;
@@ -272,7 +273,7 @@ hipError_t rollup_scan(const uint32_t* cnt, int64_t* coff, const uint32_t* vsz, 
                        void** tmp, size_t* tmp_bytes, hipStream_t s);
 
 // launchers (kernels.hip)
-hipError_t launch_index(const uint8_t* qual, const uint8_t* val, RowDesc* rows, int64_t n_rows, int32_t* err,
+hipError_t launch_index(const uint8_t* qual, const uint8_t* val, uint8_t* val2, RowDesc* rows, int64_t n_rows, int32_t* err,
                         hipStream_t s);
 hipError_t launch_grid(const GridParams& p, int ds_function_class, hipStream_t s);
 // k_fast: uniform float rows of one (qualifier width, value length) class; returns

@@ -6,8 +6,12 @@
 namespace tsdb {
 
 // ---- k_index: classify every row, validate it, certificate stats ---------------------
+// Also writes val2: for 2-byte-qualifier rows, every integer value of 1 or 2 bytes as a
+// little-endian int16 at val2 + qoff + 2 i (same offsets as the qualifiers), the layout the
+// vle-integer class of k_short / k_fast reads.
 __global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual, const uint8_t* __restrict__ val,
-                                               RowDesc* __restrict__ rows, int64_t n_rows, int32_t* err) {
+                                               uint8_t* __restrict__ val2, RowDesc* __restrict__ rows, int64_t n_rows,
+                                               int32_t* err) {
   const int lane = lane_id();
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -124,6 +128,8 @@ __global__ __launch_bounds__(256) void k_index(const uint8_t* __restrict__ qual,
         for (int b = 0; b < len; b++) bits = (bits << 8) | v[vo + b];
         double x = 0.0;
         decode_value(bits, len, fl, x);
+        if (val2 && w == 2 && (flags & ROW_QW_MASK) == 2 && !fl && len <= 2)
+          reinterpret_cast<int16_t*>(val2 + d.qoff)[i] = (int16_t)(long long)x;
         if (isnan(x)) hasnan = true;
         if (x == 0.0 && signbit(x)) negz = true;
         if (!isnan(x)) {
@@ -351,11 +357,11 @@ __global__ __launch_bounds__(256) void k_synth_write(SynthParams p) {
 }
 
 // ---- launchers -------------------------------------------------------------------
-hipError_t launch_index(const uint8_t* qual, const uint8_t* val, RowDesc* rows, int64_t n_rows, int32_t* err,
-                        hipStream_t s) {
+hipError_t launch_index(const uint8_t* qual, const uint8_t* val, uint8_t* val2, RowDesc* rows, int64_t n_rows,
+                        int32_t* err, hipStream_t s) {
   if (n_rows == 0) return hipSuccess;
   const int64_t blocks = std::min<int64_t>((n_rows + 3) / 4, 65536);
-  hipLaunchKernelGGL(k_index, dim3((unsigned)blocks), dim3(256), 0, s, qual, val, rows, n_rows, err);
+  hipLaunchKernelGGL(k_index, dim3((unsigned)blocks), dim3(256), 0, s, qual, val, val2, rows, n_rows, err);
   return hipGetLastError();
 }
 

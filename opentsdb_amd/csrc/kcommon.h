@@ -1358,7 +1358,7 @@ __device__ __forceinline__ int fast_issue(const GridParams& p, const RowDesc* __
 #pragma unroll
   for (int k = 0; k < QW / 2; k++) b.q[k] = q[k];
   if (VL == 0) {
-    b.v[0] = *reinterpret_cast<const uint4*>(p.val + w.d.voff + (int64_t)lane * 16);
+    b.v[0] = *reinterpret_cast<const uint4*>(p.val2 + w.d.qoff + i0 * 2);   // the lane's 8 int16 values
   } else {
     const uint4* v = reinterpret_cast<const uint4*>(p.val + w.d.voff + i0 * VL);
 #pragma unroll
@@ -1411,57 +1411,25 @@ __device__ __forceinline__ uint32_t f_flags(const FRaw<QW, VL>& b, int j) {
 }
 
 // VL == 0: the lane's 8 vle integers (1 or 2 bytes, RowSeq.extractIntegerValue
-// src/core/RowSeq.java:233-245) from the row's value bytes staged in LDS.  Called by the
-// whole wave.
+// src/core/RowSeq.java:233-245), read from the load-time int16 copy of the row's values
+// (k_index writes val2[qoff + 2 i] for every 1-2-byte integer of a 2-byte-qualifier row), so
+// the query needs no in-wave prefix sum of value lengths and no LDS staging.
 template <int QW, int VL>
-__device__ __forceinline__ void f_values_vle(const FastLds& L, const FRaw<QW, VL>& b, int nvl, double xs[DPL]) {
-  const int lane = lane_id();
-  int len[DPL];
-  int tot = 0;
-#pragma unroll
-  for (int j = 0; j < DPL; j++) {
-    len[j] = (j < nvl) ? (int)(f_flags<QW, VL>(b, j) & 7) + 1 : 0;
-    tot += len[j];
-  }
-  int o = wave_excl_sum_small<5>(tot);   // tot <= 16
-  WAVE_SYNC();
-  reinterpret_cast<uint4*>(L.vstage)[lane] = b.v[0];
-  WAVE_SYNC();
-#pragma unroll
-  for (int j = 0; j < DPL; j++) {
-    int64_t v = 0;
-    if (len[j] == 1) v = (int8_t)L.vstage[o];
-    else if (len[j] == 2) v = (int16_t)(uint16_t)(((uint32_t)L.vstage[o] << 8) | L.vstage[o + 1]);
-    xs[j] = (double)v;
-    o += len[j];
-  }
+__device__ __forceinline__ int f_int16(const FRaw<QW, VL>& b, int j) {
+  const uint32_t wd = (j >> 1) == 0 ? b.v[0].x : (j >> 1) == 1 ? b.v[0].y : (j >> 1) == 2 ? b.v[0].z : b.v[0].w;
+  return (j & 1) ? ((int)wd >> 16) : (int)(int16_t)(wd & 0xFFFF);
 }
 
-// VL == 0, integer form: the lane's 8 vle integers as int32 (1- or 2-byte values), one
-// unaligned 16-bit LDS read each (gfx950 LDS serves unaligned ds_read_u16).
+template <int QW, int VL>
+__device__ __forceinline__ void f_values_vle(const FastLds& L, const FRaw<QW, VL>& b, int nvl, double xs[DPL]) {
+#pragma unroll
+  for (int j = 0; j < DPL; j++) xs[j] = (double)f_int16<QW, VL>(b, j);
+}
+
 template <int QW, int VL>
 __device__ __forceinline__ void f_values_vle_i(const FastLds& L, const FRaw<QW, VL>& b, int nvl, int xi[DPL]) {
-  const int lane = lane_id();
-  int len[DPL];
-  int tot = 0;
 #pragma unroll
-  for (int j = 0; j < DPL; j++) {
-    len[j] = (j < nvl) ? (int)(f_flags<QW, VL>(b, j) & 7) + 1 : 0;
-    tot += len[j];
-  }
-  int o = wave_incl_sum_dpp(tot) - tot;
-  WAVE_SYNC();
-  reinterpret_cast<uint4*>(L.vstage)[lane] = b.v[0];
-  WAVE_SYNC();
-#pragma unroll
-  for (int j = 0; j < DPL; j++) {
-    uint16_t u;
-    __builtin_memcpy(&u, L.vstage + o, 2);   // bytes o (low half), o + 1
-    const int v1 = (int)(int8_t)(uint8_t)u;
-    const int v2 = (int)(int16_t)(uint16_t)((u << 8) | (u >> 8));
-    xi[j] = len[j] == 2 ? v2 : v1;
-    o += len[j];
-  }
+  for (int j = 0; j < DPL; j++) xi[j] = f_int16<QW, VL>(b, j);
 }
 
 struct FGeom {
@@ -1826,7 +1794,7 @@ __device__ __forceinline__ void short_issue(const GridParams& p, uint64_t qoff, 
 #pragma unroll
   for (int k = 0; k < QW / 2; k++) b.q[k] = q[k];
   if (VL == 0) {
-    b.v[0] = *reinterpret_cast<const uint4*>(p.val + voff + (int64_t)lane * 16);
+    b.v[0] = *reinterpret_cast<const uint4*>(p.val2 + qoff + i0 * 2);   // the lane's 8 int16 values
   } else {
     const uint4* v = reinterpret_cast<const uint4*>(p.val + voff + i0 * VL);
 #pragma unroll
