@@ -1809,7 +1809,7 @@ __device__ __forceinline__ uint64_t rl64(uint64_t x, int l) {
 }
 
 #ifndef SHORT_OCC
-#define SHORT_OCC 6   // waves per SIMD k_short is compiled for (VGPR budget)
+#define SHORT_OCC 5   // waves per SIMD k_short is compiled for (VGPR budget). Config 3: 3-5 -> 3.8 ms, 6 -> 4.5 ms, 8 -> 9.4 ms
 #endif
 template <int F, int QW, int VL, int D, bool KR>
 __global__ __launch_bounds__(256, SHORT_OCC) void k_short(GridParams p, const RowDesc* __restrict__ rows,
