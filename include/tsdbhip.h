@@ -120,7 +120,8 @@ enum {
 };
 
 /* Query flags. */
-#define TSDB_QF_ORDERED 0x1  /* cross-series float reductions in SpanGroup index order (bit-exact, slower) */
+#define TSDB_QF_ORDERED 0x1  /* cross-series float reductions in SpanGroup index order (bit-exact, slower;
+                                one GPU: tsdbhip_run_partials refuses it) */
 
 /* ---- Result: DataPoints[] (one entry per SpanGroup, in emission order) ----- */
 typedef struct {

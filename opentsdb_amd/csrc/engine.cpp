@@ -835,6 +835,7 @@ struct Plan {
   bool dense_out = false;   // grid kernels write per-series bucket values to pre_dense / pre_pres
   std::vector<int64_t> bounds;   // MODE_TABLE: K + 1 calendar slot boundaries (ms)
   int64_t seek = 0;              // MODE_TABLE: first timestamp the spans' Downsamplers read
+  bool ordered = false;          // TSDB_QF_ORDERED float reduction: run_ordered
 };
 
 bool is_sel_agg(int a) { return a == TSDB_AGG_MEDIAN || (a >= TSDB_AGG_P999 && a < TSDB_AGG_COUNT_ALL); }
@@ -873,8 +874,10 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
   }
   if (P.ga < 0) return fail(TSDB_E_NOT_IMPLEMENTED, std::string("group-by aggregator not implemented yet: ") + AGG_NAMES[q->aggregator]);
   if (P.f < 0) return fail(TSDB_E_NOT_IMPLEMENTED, std::string("downsampling function not implemented yet: ") + AGG_NAMES[q->ds_function]);
-  if ((q->flags & TSDB_QF_ORDERED) && (P.ga == GA_SUM || P.ga == GA_AVG || P.ga == GA_SQUARESUM || P.ga == GA_DEV || P.ga == GA_MULT))
-    return fail(TSDB_E_NOT_IMPLEMENTED, "ordered cross-series reduction not implemented yet");
+  // TSDB_QF_ORDERED: float reductions in SpanGroup index order (bit-exact); the other
+  // aggregators are already order-exact on the partials path
+  P.ordered = (q->flags & TSDB_QF_ORDERED) && !P.gsel &&
+              (P.ga == GA_SUM || P.ga == GA_AVG || P.ga == GA_SQUARESUM || P.ga == GA_DEV || P.ga == GA_MULT);
   P.interp = interp_of(q->aggregator);
   P.none = q->aggregator == TSDB_AGG_NONE;
   tsdbhip_scan_bounds(q, &P.ss, &P.se);
@@ -1451,6 +1454,30 @@ int run_sel_group(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t
   return 0;
 }
 
+// TSDB_QF_ORDERED: the span values per (group, slot) as for the percentile group-by
+// (stages 1-2), then k_ordered folds each (group, slot) over the group's spans in SpanGroup
+// index order -- Aggregator.runDouble's operand sequence, so float sums are bit-exact.
+int run_ordered(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G) {
+  int rc = sel_values(c, q, P, G);
+  if (rc) return rc;
+  HIP_OK(c->out_val.ensure(std::max<int64_t>(1, G * P.K) * 8));
+  HIP_OK(c->out_flag.ensure(std::max<int64_t>(1, G * P.K)));
+  OrdParams op{};
+  op.vals = c->sel_vals.as<double>();
+  op.uni = c->sel_uni.as<uint8_t>();
+  op.group_series_ptr = c->sel_gsp.as<int64_t>();
+  op.G = G;
+  op.K = P.K;
+  op.ga = P.ga;
+  op.out_val = c->out_val.as<double>();
+  op.out_flag = c->out_flag.as<uint8_t>();
+  op.err = c->err.as<int32_t>();
+  HIP_OK(launch_ordered(op, c->stream));
+  HIP_OK(hipEventRecord(c->ev[1], c->stream));
+  HIP_OK(hipEventRecord(c->ev[2], c->stream));
+  return 0;
+}
+
 void record_timing(tsdbhip_ctx* c, const Plan& P, int32_t redo_n) {
   float t01 = 0, t12 = 0, t03 = 0;
   (void)hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
@@ -1762,8 +1789,8 @@ extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_resul
   if (rc) return rc;
   const int64_t G = P.none ? c->n_series : c->n_groups;
   if (P.raw) return run_raw(c, q, P, out);
-  if (P.gsel) {
-    rc = run_sel_group(c, q, P, G);
+  if (P.gsel || P.ordered) {
+    rc = P.gsel ? run_sel_group(c, q, P, G) : run_ordered(c, q, P, G);
     if (rc) return rc;
     return collect(c, q, P, G, true, out);
   }
@@ -1806,7 +1833,8 @@ int plan_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_globa
   if (rc) return rc;
   if (P.none) return fail(TSDB_E_NOT_IMPLEMENTED, "NONE aggregator is per-span; it has no cross-rank exchange");
   if (P.raw) return fail(TSDB_E_NOT_IMPLEMENTED, "multi-GPU raw (union LERP) queries are not implemented yet");
-  if (P.gsel) return fail(TSDB_E_NOT_IMPLEMENTED, "multi-GPU percentile / median group-by is not implemented yet");
+  if (P.gsel) return fail(TSDB_E_NOT_IMPLEMENTED, "percentile / median group-by: use the tsdbhip_sel_* exchange");
+  if (P.ordered) return fail(TSDB_E_NOT_IMPLEMENTED, "ordered (TSDB_QF_ORDERED) reduction across ranks");
   if (n_groups_global < c->n_groups) return fail(TSDB_E_ILLEGAL_ARGUMENT, "n_groups_global smaller than the local groups");
   return 0;
 }

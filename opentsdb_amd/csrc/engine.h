@@ -163,6 +163,18 @@ struct SelParams {
 };
 static constexpr int SEL_CAP = 12288;   // values of one segment staged in LDS (96 KB)
 
+// Ordered (TSDB_QF_ORDERED) reduction of the span values per (group, slot).
+struct OrdParams {
+  const double* vals;             // [series][K] as GridParams.sel_vals (fill pattern = no value)
+  const uint8_t* uni;             // [G][K]
+  const int64_t* group_series_ptr;
+  int64_t G, K;
+  int32_t ga;
+  double* out_val;
+  uint8_t* out_flag;
+  int32_t* err;
+};
+
 // Rank-ordered merge of all-gathered per-rank partial buffers (tsdbhip_finalize).
 struct RankMergeParams {
   const unsigned char* base;      // n_ranks consecutive buffers of `stride` bytes
@@ -292,6 +304,7 @@ hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s);
 hipError_t launch_emit(const GridParams& p, hipStream_t s);
 hipError_t launch_emit_vals(const GridParams& p, hipStream_t s);
 hipError_t launch_sel_seg(const SelParams& p, hipStream_t s);
+hipError_t launch_ordered(const OrdParams& p, hipStream_t s);
 hipError_t launch_rank_merge(const RankMergeParams& p, hipStream_t s);
 // per-downsample-function instantiations (k_grid.hip / k_fast.hip, one object per F)
 template <int F> hipError_t launch_grid_inst(const GridParams& p, hipStream_t s);

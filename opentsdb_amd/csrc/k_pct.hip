@@ -932,6 +932,39 @@ __global__ __launch_bounds__(512) void k_sel_seg(SelParams p) {
   }
 }
 
+// One thread per (group, slot), consecutive slots in consecutive lanes (coalesced rows):
+// contribute_slot over the group's spans in index order, then ps_final.  A span without a
+// value at the slot holds sel_values' fill pattern (0x7FF87FF87FF87FF8), distinct from the
+// canonical NaN of a real NaN value (which MULT / FIRST / LAST see).
+__global__ __launch_bounds__(256) void k_ordered(OrdParams p) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.G * p.K) return;
+  const int64_t g = i / p.K, k = i - g * p.K;
+  RegPart R;
+  regpart_init(p.ga, R);
+  const int64_t s1 = p.group_series_ptr[g + 1];
+  for (int64_t s = p.group_series_ptr[g]; s < s1; s++) {
+    const double v = p.vals[s * p.K + k];
+    if ((uint64_t)__double_as_longlong(v) == 0x7FF87FF87FF87FF8ULL) continue;
+    contribute_slot(p.ga, R, v, false);
+  }
+  const bool emit = p.uni[i] != 0;
+  PState S;
+  S.a = R.pa;
+  S.b = R.pb;
+  S.n = R.pn;
+  S.f = R.pf | (emit ? PF_UNION : 0u);
+  p.out_val[i] = emit ? ps_final(p.ga, S, p.err) : 0.0;
+  p.out_flag[i] = emit ? 1 : 0;
+}
+
+hipError_t launch_ordered(const OrdParams& p, hipStream_t s) {
+  const int64_t n = p.G * p.K;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ordered, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
 hipError_t launch_emit_vals(const GridParams& p, hipStream_t s) {
   if (p.n_tiles == 0) return hipSuccess;
   const int64_t blocks = (p.n_tiles + p.waves - 1) / p.waves;

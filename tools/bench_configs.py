@@ -101,6 +101,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--cpu", action="store_true", help="time the oracle on one group")
     ap.add_argument("--only", default="", help="comma-separated group-by aggregators to run (config 3)")
+    ap.add_argument("--ordered", action="store_true", help="TSDB_QF_ORDERED (bit-exact span-order float reductions)")
     args = ap.parse_args()
     from opentsdb_amd import abi, dist, synth
     from opentsdb_amd.engine import Engine, parse_downsample
@@ -116,6 +117,10 @@ def main():
         groups = args.groups if args.groups != 64 else 1000
         aggs = args.only.split(",") if args.only else ["sum", "avg", "min", "max", "count", "dev", "p99", "median"]
         qs = {f"{a}:1m-avg": dsq(a, "1m-avg", T0 + 3599) for a in aggs}
+        if args.ordered:
+            for q in qs.values():
+                q.flags = abi.QF_ORDERED
+            qs = {k + " (ordered)": v for k, v in qs.items()}
         grid_config(args, eng, qs, series, 360, 2, 30000, groups)
         eng.close()
         return
