@@ -121,7 +121,7 @@ enum {
 
 /* Query flags. */
 #define TSDB_QF_ORDERED 0x1  /* cross-series float reductions in SpanGroup index order (bit-exact, slower;
-                                one GPU: tsdbhip_run_partials refuses it) */
+                                across ranks through the tsdbhip_sel_* exchange, not run_partials) */
 
 /* ---- Result: DataPoints[] (one entry per SpanGroup, in emission order) ----- */
 typedef struct {

@@ -1087,7 +1087,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     HIP_OK(hipMemcpyAsync(&nbig, c->redo_n.p, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
     HIP_OK(launch_pct(gp, 2, nbig, c->stream));
-    if (!P.gsel) HIP_OK(launch_emit(gp, c->stream));   // gsel: run_sel_group takes the bucket values
+    if (!P.gsel && !P.ordered) HIP_OK(launch_emit(gp, c->stream));   // else sel_values takes the bucket values
     HIP_OK(hipEventRecord(c->ev[1], c->stream));
   } else {
   // streaming kernel first (when the batch's row class and the query allow it), then the
@@ -1834,7 +1834,7 @@ int plan_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_globa
   if (P.none) return fail(TSDB_E_NOT_IMPLEMENTED, "NONE aggregator is per-span; it has no cross-rank exchange");
   if (P.raw) return fail(TSDB_E_NOT_IMPLEMENTED, "multi-GPU raw (union LERP) queries are not implemented yet");
   if (P.gsel) return fail(TSDB_E_NOT_IMPLEMENTED, "percentile / median group-by: use the tsdbhip_sel_* exchange");
-  if (P.ordered) return fail(TSDB_E_NOT_IMPLEMENTED, "ordered (TSDB_QF_ORDERED) reduction across ranks");
+  if (P.ordered) return fail(TSDB_E_NOT_IMPLEMENTED, "TSDB_QF_ORDERED across ranks: use the tsdbhip_sel_* exchange");
   if (n_groups_global < c->n_groups) return fail(TSDB_E_ILLEGAL_ARGUMENT, "n_groups_global smaller than the local groups");
   return 0;
 }
@@ -1942,7 +1942,8 @@ namespace {
 int plan_sel(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, Plan& P) {
   int rc = plan_query(c, q, P);
   if (rc) return rc;
-  if (!P.gsel) return fail(TSDB_E_ILLEGAL_ARGUMENT, "not a percentile / median group-by query");
+  if (!P.gsel && !P.ordered)
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, "not a percentile / median group-by or TSDB_QF_ORDERED query");
   if (n_groups_global < c->n_groups) return fail(TSDB_E_ILLEGAL_ARGUMENT, "n_groups_global smaller than the local groups");
   return 0;
 }
@@ -2005,7 +2006,26 @@ extern "C" int tsdbhip_sel_select(tsdbhip_ctx* c, const tsdbhip_query* q, int64_
   if (n) HIP_OK(hipMemcpyAsync(c->sel_vals.p, vals, n * 8, hipMemcpyDefault, c->stream));
   if (G * K) HIP_OK(hipMemcpyAsync(c->sel_uni.p, uni, G * K, hipMemcpyDefault, c->stream));
   HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
-  rc = sel_select(c, P, G, c->sel_vals.as<double>(), cnt, c->sel_uni.as<uint8_t>());
+  if (P.ordered) {   // the owner folds each (group, slot) over the ranks' spans in rank (= span) order
+    const std::vector<int64_t> gsp = seg_ptr(cnt);
+    HIP_OK(c->sel_gsp.ensure((G + 1) * 8));
+    HIP_OK(c->out_val.ensure(std::max<int64_t>(1, G * K) * 8));
+    HIP_OK(c->out_flag.ensure(std::max<int64_t>(1, G * K)));
+    HIP_OK(hipMemcpyAsync(c->sel_gsp.p, gsp.data(), (G + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    OrdParams op{};
+    op.vals = c->sel_vals.as<double>();
+    op.uni = c->sel_uni.as<uint8_t>();
+    op.group_series_ptr = c->sel_gsp.as<int64_t>();
+    op.G = G;
+    op.K = K;
+    op.ga = P.ga;
+    op.out_val = c->out_val.as<double>();
+    op.out_flag = c->out_flag.as<uint8_t>();
+    op.err = c->err.as<int32_t>();
+    HIP_OK(launch_ordered(op, c->stream));
+  } else {
+    rc = sel_select(c, P, G, c->sel_vals.as<double>(), cnt, c->sel_uni.as<uint8_t>());
+  }
   if (rc) return rc;
   if (G * K) {
     HIP_OK(hipMemcpyAsync(out_val, c->out_val.p, G * K * 8, hipMemcpyDefault, c->stream));

@@ -170,7 +170,8 @@ def sel_combine(rows_all, G: int, K: int, world: int):
 
 
 def run_distributed_sel(eng, q: abi.Query, dist, n_groups_global: int, device=None):
-    """A percentile / median group-by query over the sharded store:
+    """A percentile / median group-by query -- or a TSDB_QF_ORDERED one, whose owner folds
+    the spans in rank (= SpanGroup) order -- over the sharded store:
     local contributions -> all-to-all to the owning ranks -> sort + select on the owners ->
     all-gather of the owners' rows -> result on every rank."""
     import torch

@@ -269,3 +269,12 @@ def test_two_process_gloo_raw(tmp_path):
         got = [(int(z["gid"][i]), z["ts"][cut[i]:cut[i + 1]], z["bits"][cut[i]:cut[i + 1]], z["isi"][cut[i]:cut[i + 1]])
                for i in range(len(z["gid"]))]
         assert_groups_match(got, want, "sum", tol=0.0, ctx=f"gloo raw rank {r}")
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("agg", ["sum", "avg", "dev", "squareSum"])
+def test_sharded_ordered_bit_exact(engines, batch, world, agg):
+    """TSDB_QF_ORDERED over ranks: span values to the owner, folded in rank (= span) order."""
+    q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["avg"], ds_interval_ms=60000, flags=abi.QF_ORDERED)
+    assert_groups_match(run_sharded_sel(engines, batch, q, world), O.run_query(batch, q), agg, tol=0.0,
+                        ctx=f"ordered {agg} x{world}")
