@@ -584,7 +584,63 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
   return build_tiles(c);
 }
 
-extern "C" int tsdbhip_load(tsdbhip_ctx* c, const tsdbhip_batch* b) {
+// RowSeq.addRow (src/core/RowSeq.java:91-222): ordered merge of the remote cell into the
+// local one by qualifier offset (Internal.compareQualifiers :511-519), the remote datapoint
+// dropped on equal offsets, meta byte MS_MIXED_COMPACT if either side has it.  false: a
+// malformed cell (left unmerged; k_index reports it).
+static bool merge_cells(std::vector<uint8_t>& lq, std::vector<uint8_t>& lv, const uint8_t* rq, size_t rql,
+                        const uint8_t* rv, size_t rvl) {
+  auto qlen_at = [](const uint8_t* q, size_t i) -> size_t { return (q[i] & 0xF0) == 0xF0 ? 4 : 2; };
+  auto off_at = [](const uint8_t* q, size_t i) -> int64_t {
+    if ((q[i] & 0xF0) == 0xF0)
+      return (int64_t)(((((uint32_t)q[i] << 24) | ((uint32_t)q[i + 1] << 16) | ((uint32_t)q[i + 2] << 8) | q[i + 3]) &
+                        0x0FFFFFC0u) >> 6);
+    return (int64_t)((((uint32_t)q[i] << 8) | q[i + 1]) >> 4) * 1000;
+  };
+  if (lv.empty() || rvl == 0) return false;
+  const uint8_t* q0 = lq.data();
+  const uint8_t* v0 = lv.data();
+  // value bytes are located through the qualifiers; the last byte of each side is its meta
+  // byte (for a single-datapoint cell, the value's own last byte -- as the reference reads it)
+  const size_t ql = lq.size(), vl = lv.size(), rvl0 = rvl;
+  std::vector<uint8_t> mq, mv;
+  mq.reserve(ql + rql);
+  mv.reserve(vl + rvl0 + 1);
+  size_t li = 0, ri = 0, lvi = 0, rvi = 0;
+  while (ri < rql || li < ql) {
+    bool remote;
+    if (ri >= rql) remote = false;
+    else if (li >= ql) remote = true;
+    else {
+      if (ri + qlen_at(rq, ri) > rql || li + qlen_at(q0, li) > ql) return false;
+      const int64_t a = off_at(rq, ri), b2 = off_at(q0, li);
+      if (a == b2) {
+        rvi += (rq[ri + qlen_at(rq, ri) - 1] & 7) + 1;
+        ri += qlen_at(rq, ri);
+        continue;
+      }
+      remote = a < b2;
+    }
+    const uint8_t* q = remote ? rq : q0;
+    const uint8_t* v = remote ? rv : v0;
+    size_t& qi = remote ? ri : li;
+    size_t& vi = remote ? rvi : lvi;
+    const size_t qn = qlen_at(q, qi);
+    if (qi + qn > (remote ? rql : ql)) return false;
+    const size_t vn = (q[qi + qn - 1] & 7) + 1;
+    if (vi + vn > (remote ? rvl0 : vl)) return false;
+    mq.insert(mq.end(), q + qi, q + qi + qn);
+    mv.insert(mv.end(), v + vi, v + vi + vn);
+    qi += qn;
+    vi += vn;
+  }
+  mv.push_back(((v0[vl - 1] & 1) || (rv[rvl0 - 1] & 1)) ? 1 : 0);
+  lq.swap(mq);
+  lv.swap(mv);
+  return true;
+}
+
+static int load_impl(tsdbhip_ctx* c, const tsdbhip_batch* b) {
   if (!c || !b) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_OK(hipSetDevice(c->device));
@@ -672,6 +728,68 @@ extern "C" int tsdbhip_load(tsdbhip_ctx* c, const tsdbhip_batch* b) {
 // ---------------------------------------------------------------------------
 // synthetic store in HBM (the MockBase-equivalent generator of BASELINE.md)
 // ---------------------------------------------------------------------------
+
+// Span.addRow (src/core/Span.java:177-220): several cells of one series with the same base
+// time (salt-bucket duplicates) merge into one RowSeq (RowSeq.addRow).  Batches without such
+// rows are loaded as given; otherwise the merged batch is built first.
+extern "C" int tsdbhip_load(tsdbhip_ctx* c, const tsdbhip_batch* b) {
+  if (!c || !b) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  bool dup = false;
+  if (b->n_series > 0 && b->n_rows > 0 && b->series_row_ptr && b->row_base_time && b->row_qual_off &&
+      b->row_val_off && b->qual && b->val) {
+    std::vector<uint32_t> bases;
+    for (int64_t s = 0; s < b->n_series && !dup; s++) {
+      const int64_t r0 = b->series_row_ptr[s], r1 = b->series_row_ptr[s + 1];
+      if (r1 - r0 < 2 || r0 < 0 || r1 > b->n_rows) continue;
+      bases.assign(b->row_base_time + r0, b->row_base_time + r1);
+      std::sort(bases.begin(), bases.end());
+      dup = std::adjacent_find(bases.begin(), bases.end()) != bases.end();
+    }
+  }
+  if (!dup) return load_impl(c, b);
+  std::vector<int64_t> srp(b->n_series + 1, 0);
+  std::vector<uint32_t> base;
+  std::vector<uint64_t> qoff{0}, voff{0};
+  std::vector<uint8_t> qual, val;
+  for (int64_t s = 0; s < b->n_series; s++) {
+    std::vector<uint32_t> obase;
+    std::vector<std::vector<uint8_t>> oq, ov;
+    for (int64_t r = b->series_row_ptr[s]; r < b->series_row_ptr[s + 1]; r++) {
+      const uint8_t* q = b->qual + b->row_qual_off[r];
+      const uint8_t* v = b->val + b->row_val_off[r];
+      const size_t ql = b->row_qual_off[r + 1] - b->row_qual_off[r], vl = b->row_val_off[r + 1] - b->row_val_off[r];
+      size_t j = 0;
+      while (j < obase.size() && obase[j] != b->row_base_time[r]) j++;
+      if (j < obase.size()) {
+        std::vector<uint8_t> mq = oq[j], mv = ov[j];
+        if (merge_cells(mq, mv, q, ql, v, vl)) { oq[j].swap(mq); ov[j].swap(mv); continue; }
+      }
+      obase.push_back(b->row_base_time[r]);
+      oq.emplace_back(q, q + ql);
+      ov.emplace_back(v, v + vl);
+    }
+    for (size_t j = 0; j < obase.size(); j++) {
+      base.push_back(obase[j]);
+      qual.insert(qual.end(), oq[j].begin(), oq[j].end());
+      val.insert(val.end(), ov[j].begin(), ov[j].end());
+      qoff.push_back(qual.size());
+      voff.push_back(val.size());
+    }
+    srp[s + 1] = (int64_t)base.size();
+  }
+  if (qual.empty()) qual.push_back(0);
+  if (val.empty()) val.push_back(0);
+  tsdbhip_batch m = *b;
+  m.n_rows = (int64_t)base.size();
+  m.series_row_ptr = srp.data();
+  m.row_base_time = base.data();
+  m.row_qual_off = qoff.data();
+  m.row_val_off = voff.data();
+  m.qual = qual.data();
+  m.val = val.data();
+  return load_impl(c, &m);
+}
+
 extern "C" int tsdbhip_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp) {
   if (!c || !sp) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);

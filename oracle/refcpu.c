@@ -669,6 +669,8 @@ typedef struct {
   int64_t nrows;
   int64_t row_index;
   row_it cur;
+  uint8_t** owned;      /* merged cells (RowSeq.addRow) owned by the span */
+  int64_t n_owned;
 } span_view;
 
 static int sv_has_next(ref_view* v) {  /* Span.Iterator.hasNext :421-435 */
@@ -712,7 +714,13 @@ static void sv_seek(ref_view* v, int64_t ts) {  /* :464-471 with seekRow :360-38
   }
   row_it_seek(&s->cur, ts);
 }
-static void sv_destroy(ref_view* v) { span_view* s = (span_view*)v; free(s->rows); free(s); }
+static void sv_destroy(ref_view* v) {
+  span_view* s = (span_view*)v;
+  for (int64_t i = 0; i < s->n_owned; i++) free(s->owned[i]);
+  free(s->owned);
+  free(s->rows);
+  free(s);
+}
 static const view_vt SPAN_VT = {sv_has_next, sv_next, sv_seek, sv_destroy};
 
 static int cmp_rowseq(const void* a, const void* b) {
@@ -721,21 +729,88 @@ static int cmp_rowseq(const void* a, const void* b) {
   return x->base < y->base ? -1 : (x->base > y->base ? 1 : 0);
 }
 
+/* Internal.getQualifierLength :712-727 / getValueLengthFromQualifier :680-690 */
+static int64_t qual_len_at(const uint8_t* q, int64_t i) { return in_ms(q[i]) ? 4 : 2; }
+static int64_t val_len_at(const uint8_t* q, int64_t i) { return (q[i + qual_len_at(q, i) - 1] & 7) + 1; }
+static int64_t qual_offset_ms(const uint8_t* q, int64_t i) {   /* getOffsetFromQualifier :647-658 */
+  return in_ms(q[i]) ? (int64_t)((be32(q + i) & 0x0FFFFFC0u) >> 6) : (int64_t)(be16(q + i) >> 4) * 1000;
+}
+
+/* RowSeq.addRow :91-222: ordered merge of the remote cell into the local one by qualifier
+ * offset (Internal.compareQualifiers :511-519); on equal offsets the remote datapoint is
+ * dropped; the meta byte is MS_MIXED_COMPACT if either side has it. */
+static void rowseq_merge(span_view* s, rowseq* local, const rowseq* remote) {
+  const int64_t ql = local->qlen, rql = remote->qlen;
+  uint8_t* mq = (uint8_t*)xcalloc((size_t)(ql + rql + 1), 1);
+  uint8_t* mv = (uint8_t*)xcalloc((size_t)(local->vlen + remote->vlen + 1), 1);
+  int64_t li = 0, ri = 0, mi = 0, lv = 0, rv = 0, mvi = 0;
+  while (ri < rql || li < ql) {
+    int take_remote;
+    if (ri >= rql) take_remote = 0;
+    else if (li >= ql) take_remote = 1;
+    else {
+      const int64_t a = qual_offset_ms(remote->q, ri), b = qual_offset_ms(local->q, li);
+      if (a == b) {   /* duplicate: skip the remote one */
+        rv += val_len_at(remote->q, ri);
+        ri += qual_len_at(remote->q, ri);
+        continue;
+      }
+      take_remote = a < b;
+    }
+    const uint8_t* q = take_remote ? remote->q : local->q;
+    const uint8_t* v = take_remote ? remote->v : local->v;
+    int64_t* qi = take_remote ? &ri : &li;
+    int64_t* vi = take_remote ? &rv : &lv;
+    const int64_t vl = val_len_at(q, *qi), qlen = qual_len_at(q, *qi);
+    if (*vi + vl > (take_remote ? remote->vlen : local->vlen)) jthrow(TSDB_E_ILLEGAL_DATA, "value out of bounds in addRow");
+    memcpy(mv + mvi, v + *vi, (size_t)vl);
+    memcpy(mq + mi, q + *qi, (size_t)qlen);
+    *vi += vl;
+    mvi += vl;
+    *qi += qlen;
+    mi += qlen;
+  }
+  const uint8_t meta_l = local->vlen ? local->v[local->vlen - 1] : 0;
+  const uint8_t meta_r = remote->vlen ? remote->v[remote->vlen - 1] : 0;
+  mv[mvi] = ((meta_l & 1) || (meta_r & 1)) ? 1 : 0;   /* Const.MS_MIXED_COMPACT */
+  s->owned = (uint8_t**)realloc(s->owned, (size_t)(s->n_owned + 2) * sizeof(uint8_t*));
+  s->owned[s->n_owned++] = mq;
+  s->owned[s->n_owned++] = mv;
+  local->q = mq;
+  local->qlen = mi;
+  local->v = mv;
+  local->vlen = mvi + 1;
+}
+
 static ref_view* make_span(int64_t n_rows, const uint32_t* base_time, const uint64_t* qual_off,
                            const uint64_t* val_off, const uint8_t* qual, const uint8_t* val,
                            const int64_t* row_ids) {
   span_view* s = (span_view*)xcalloc(1, sizeof(span_view));
   s->base.vt = &SPAN_VT;
-  s->rows = (rowseq*)xcalloc((size_t)n_rows, sizeof(rowseq));
-  s->nrows = n_rows;
+  s->rows = (rowseq*)xcalloc((size_t)(n_rows ? n_rows : 1), sizeof(rowseq));
+  s->nrows = 0;
+  /* Span.addRow :177-220 in arrival order: a cell whose first timestamp is not after the
+   * last row's last one merges into the row with the same key (same series, same base) */
   for (int64_t i = 0; i < n_rows; i++) {
     const int64_t r = row_ids ? row_ids[i] : i;
-    s->rows[i].base = base_time[r];
-    s->rows[i].q = qual + qual_off[r];
-    s->rows[i].qlen = (int64_t)(qual_off[r + 1] - qual_off[r]);
-    s->rows[i].v = val + val_off[r];
-    s->rows[i].vlen = (int64_t)(val_off[r + 1] - val_off[r]);
+    rowseq nr;
+    nr.base = base_time[r];
+    nr.q = qual + qual_off[r];
+    nr.qlen = (int64_t)(qual_off[r + 1] - qual_off[r]);
+    nr.v = val + val_off[r];
+    nr.vlen = (int64_t)(val_off[r + 1] - val_off[r]);
+    if (s->nrows > 0) {
+      const rowseq* last = &s->rows[s->nrows - 1];
+      const int64_t last_ts = row_timestamp(last, row_size(last) - 1);
+      if (last_ts >= row_timestamp(&nr, 0)) {
+        int64_t j = 0;
+        for (; j < s->nrows; j++) if (s->rows[j].base == nr.base) break;
+        if (j < s->nrows) { rowseq_merge(s, &s->rows[j], &nr); continue; }
+      }
+    }
+    s->rows[s->nrows++] = nr;
   }
+  n_rows = s->nrows;
   /* Span.checkRowOrder: Collections.sort (stable) by base time */
   int sorted = 1;
   for (int64_t i = 1; i < n_rows; i++) if (s->rows[i].base < s->rows[i - 1].base) sorted = 0;
