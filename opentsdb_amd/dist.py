@@ -264,3 +264,37 @@ def run_distributed_raw(eng, q: abi.Query, dist):
     parts = [None] * dist.get_world_size()
     dist.all_gather_object(parts, local)
     return merge_group_results(parts)
+
+
+# ---- NONE aggregator: one SpanGroup per span ---------------------------------------------
+#
+# TsdbQuery with the NONE aggregator emits every span as its own group, in span order
+# (src/core/TsdbQuery.java:941-962).  Ranks take contiguous ranges of spans in batch order;
+# each rank's result lists its spans in order, so concatenating the ranks' results in rank
+# order and renumbering the groups reproduces the single-GPU result.  No data exchange.
+
+def shard_batch_spans(batch: abi.HostBatch, rank: int, world: int) -> abi.HostBatch:
+    """Contiguous, byte-balanced range of spans in batch order (NONE aggregator)."""
+    keep = np.nonzero(batch.group_id >= 0)[0]
+    srp = batch.series_row_ptr
+    qo, vo = batch.row_qual_off.astype(np.int64), batch.row_val_off.astype(np.int64)
+    sbytes = [(qo[srp[s + 1]] - qo[srp[s]]) + (vo[srp[s + 1]] - vo[srp[s]]) for s in keep]
+    b = shard_bounds(sbytes, world)
+    return select_series(batch, keep[b[rank]:b[rank + 1]])
+
+
+def merge_none_results(parts):
+    """Rank-ordered concatenation of per-rank NONE results, group ids renumbered."""
+    out = []
+    for p in parts:
+        for g in p:
+            out.append((len(out), g[1], g[2], g[3]))
+    return out
+
+
+def run_distributed_none(eng, q: abi.Query, dist):
+    """A NONE-aggregator query over a span-sharded store (shard_batch_spans)."""
+    local = [(int(g), np.asarray(ts), np.asarray(bits), np.asarray(isi)) for g, ts, bits, isi in eng.run(q)]
+    parts = [None] * dist.get_world_size()
+    dist.all_gather_object(parts, local)
+    return merge_none_results(parts)

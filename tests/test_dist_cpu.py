@@ -224,3 +224,15 @@ def test_shard_by_group_keeps_groups_whole(world):
             assert np.all(np.diff(idx) == 1)
     assert sum(seen) == b.n_series
     assert sorted(owner) == list(range(7))
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_shard_spans_covers_batch_in_order(world):
+    b = synth.generate(17, 1356998400, 30, 10000, value_kind=0, n_groups=4, seed=1)
+    got = []
+    for r in range(world):
+        s = dist.shard_batch_spans(b, r, world)
+        got.append(s.n_series)
+    assert sum(got) == b.n_series
+    parts = [[(0, np.zeros(1), np.zeros(1), np.zeros(1))] * n for n in got]
+    assert [g[0] for g in dist.merge_none_results(parts)] == list(range(b.n_series))

@@ -278,3 +278,12 @@ def test_sharded_ordered_bit_exact(engines, batch, world, agg):
     q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["avg"], ds_interval_ms=60000, flags=abi.QF_ORDERED)
     assert_groups_match(run_sharded_sel(engines, batch, q, world), O.run_query(batch, q), agg, tol=0.0,
                         ctx=f"ordered {agg} x{world}")
+
+
+# ---- NONE aggregator: span-sharded, results concatenated in rank order -----------------
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+def test_span_sharded_none_equals_oracle(engines, batch, raw_batch, world):
+    for b, q in [(batch, abi.new_query(T0, T0 + 3599, "none", ds_function=abi.AGG["avg"], ds_interval_ms=60000)),
+                 (raw_batch, abi.new_query(T0, T0 + 7199, "none"))]:
+        parts = [engines[r].run_batch(dist.shard_batch_spans(b, r, world), q) for r in range(world)]
+        assert_groups_match(dist.merge_none_results(parts), O.run_query(b, q), "none", tol=0.0, ctx=f"none x{world}")
