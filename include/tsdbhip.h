@@ -188,6 +188,11 @@ int tsdbhip_batch_download(tsdbhip_ctx* ctx, int64_t* series_row_ptr, uint32_t* 
 
 /* Run the query over the resident batch: TsdbQuery.run() from GroupByAndAggregateCB on. */
 int tsdbhip_run(tsdbhip_ctx* ctx, const tsdbhip_query* q, tsdbhip_result** out);
+/* n queries that share the time range and the downsampling specification (a TSQuery with
+ * several sub-queries over one metric).  A percentile / median downsampling is computed once
+ * and shared by the queries' group-by steps; the cheap functions run one fused pass per
+ * query.  outs[i] as tsdbhip_run's result; on error none is returned. */
+int tsdbhip_run_multi(tsdbhip_ctx* ctx, const tsdbhip_query* qs, int n, tsdbhip_result** outs);
 void tsdbhip_result_free(tsdbhip_result* r);
 int tsdbhip_last_timing(tsdbhip_ctx* ctx, tsdbhip_timing* out);
 

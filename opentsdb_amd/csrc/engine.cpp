@@ -954,6 +954,8 @@ struct Plan {
   std::vector<int64_t> bounds;   // MODE_TABLE: K + 1 calendar slot boundaries (ms)
   int64_t seek = 0;              // MODE_TABLE: first timestamp the spans' Downsamplers read
   bool ordered = false;          // TSDB_QF_ORDERED float reduction: run_ordered
+  bool values_only = false;      // percentile downsampling pass without the group-by step
+  bool emit_only = false;        // group-by step over bucket values already in pre_dense / pre_pres
 };
 
 bool is_sel_agg(int a) { return a == TSDB_AGG_MEDIAN || (a >= TSDB_AGG_P999 && a < TSDB_AGG_COUNT_ALL); }
@@ -1150,8 +1152,9 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     gp.pres_out = c->pre_pres.as<uint8_t>();
   }
 
-  if (P.f == F_SEL) {
+  if (P.f == F_SEL || P.emit_only) {
     // percentile / median: per-series bucket order statistics, then the group-by step
+    // (emit_only: the group-by step alone, over buckets a previous pass left in pre_dense)
     HIP_OK(c->pre_dense.ensure(std::max<int64_t>(1, c->n_series * K) * 8));
     HIP_OK(c->pre_pres.ensure(std::max<int64_t>(1, c->n_series * K)));
     gp.sel_fn = q->ds_function;
@@ -1172,6 +1175,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     gp.waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / gp.wave_lds));
     c->fast_used = false;
     HIP_OK(hipEventRecord(c->ev[0], c->stream));
+    if (!P.emit_only) {
     HIP_OK(c->redo.ensure(std::max<int64_t>(1, c->n_series) * 4));
     HIP_OK(c->redo_n.ensure(16));
     HIP_OK(hipMemsetAsync(c->redo_n.p, 0, 4, c->stream));
@@ -1205,7 +1209,9 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     HIP_OK(hipMemcpyAsync(&nbig, c->redo_n.p, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
     HIP_OK(launch_pct(gp, 2, nbig, c->stream));
-    if (!P.gsel && !P.ordered) HIP_OK(launch_emit(gp, c->stream));   // else sel_values takes the bucket values
+    }
+    if (!P.gsel && !P.ordered && !P.values_only)
+      HIP_OK(launch_emit(gp, c->stream));   // else the caller takes the bucket values
     HIP_OK(hipEventRecord(c->ev[1], c->stream));
   } else {
   // streaming kernel first (when the batch's row class and the query allow it), then the
@@ -1915,6 +1921,86 @@ extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_resul
   rc = run_device(c, q, P, G, true);
   if (rc) return rc;
   return collect(c, q, P, G, true, out);
+}
+
+// Several group-by aggregators over one downsampling (a TSQuery with several sub-queries over
+// one metric).  With a percentile / median downsampling function one bucket-selection pass
+// leaves every series' buckets in pre_dense / pre_pres and each query runs only its SpanGroup
+// step (k_emit + k_reduce) over them; with the cheap functions each query runs the fused
+// streaming pass.  The queries must share the time range and the downsampling specification;
+// rate, aggregator and flags may differ.
+extern "C" int tsdbhip_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_result** outs) {
+  if (!c || !qs || !outs || n < 1) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad argument");
+  for (int i = 0; i < n; i++) outs[i] = nullptr;
+  for (int i = 1; i < n; i++) {
+    const tsdbhip_query &a = qs[0], &b = qs[i];
+    if (a.start_time != b.start_time || a.end_time != b.end_time || a.ds_function != b.ds_function ||
+        a.ds_interval_ms != b.ds_interval_ms || a.ds_fill != b.ds_fill || a.ds_all != b.ds_all ||
+        a.ds_calendar != b.ds_calendar)
+      return fail(TSDB_E_ILLEGAL_ARGUMENT, "tsdbhip_run_multi: the queries must share the time range and downsampling");
+  }
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  const int64_t G = c->n_groups;
+  tsdbhip_query q0 = qs[0];
+  q0.rate = 0;
+  q0.aggregator = TSDB_AGG_SUM;
+  q0.flags = 0;
+  Plan P0;
+  int rc = plan_query(c, &q0, P0);
+  if (rc) return rc;
+  if (P0.raw) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_run_multi needs a downsampling specification");
+  if (P0.f != F_SEL) {
+    // Cheap downsampling functions: the streaming kernels fuse decode, downsample and the
+    // group-by step in one pass that beats the generic group-by step over stored buckets
+    // (config 3, 5 aggregators: 22 ms as separate passes vs 35 ms sharing one), so each
+    // query runs its own pass.
+    for (int i = 0; i < n; i++) {
+      Plan P;
+      rc = plan_query(c, &qs[i], P);
+      if (!rc) {
+        if (P.raw) rc = fail(TSDB_E_ILLEGAL_ARGUMENT, "bad query");
+        else if (P.gsel || P.ordered) rc = P.gsel ? run_sel_group(c, &qs[i], P, G) : run_ordered(c, &qs[i], P, G);
+        else rc = run_device(c, &qs[i], P, P.none ? c->n_series : G, true);
+        if (!rc) rc = collect(c, &qs[i], P, P.none ? c->n_series : G, true, &outs[i]);
+      }
+      if (rc) {
+        for (int j = 0; j < n; j++) { std::free(outs[j]); outs[j] = nullptr; }
+        return rc;
+      }
+    }
+    return 0;
+  }
+  // percentile / median downsampling: its bucket selection dominates -- share it
+  P0.values_only = true;
+  rc = run_device(c, &q0, P0, G, false);
+  if (rc) return rc;
+  int32_t err = 0;
+  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  if (err) return fail(err, "error raised by the device path");
+  for (int i = 0; i < n; i++) {
+    Plan P;
+    rc = plan_query(c, &qs[i], P);
+    if (!rc) {
+      if (P.gsel || P.ordered) {
+        rc = P.gsel ? run_sel_group(c, &qs[i], P, G) : run_ordered(c, &qs[i], P, G);
+        if (!rc) {   // those pipelines overwrote pre_dense: restore the shared buckets
+          rc = collect(c, &qs[i], P, G, true, &outs[i]);
+          if (!rc && i + 1 < n) rc = run_device(c, &q0, P0, G, false);
+        }
+      } else {
+        P.emit_only = true;
+        rc = run_device(c, &qs[i], P, G, true);
+        if (!rc) rc = collect(c, &qs[i], P, G, true, &outs[i]);
+      }
+    }
+    if (rc) {
+      for (int j = 0; j < n; j++) { std::free(outs[j]); outs[j] = nullptr; }
+      return rc;
+    }
+  }
+  return 0;
 }
 
 extern "C" void tsdbhip_result_free(tsdbhip_result* r) { std::free(r); }

@@ -26,7 +26,7 @@ EXPORTS = [
     "tsdbhip_run", "tsdbhip_result_free", "tsdbhip_last_timing", "tsdbhip_partials_layout_get",
     "tsdbhip_run_partials", "tsdbhip_finalize", "tsdbhip_sync", "tsdbhip_rollup_interval_parse",
     "tsdbhip_rollup_basetime", "tsdbhip_rollup_qualifier", "tsdbhip_rollup_run", "tsdbhip_rollup_download",
-    "tsdbhip_sel_layout", "tsdbhip_sel_run_values", "tsdbhip_sel_select", "tsdbhip_assemble",
+    "tsdbhip_sel_layout", "tsdbhip_sel_run_values", "tsdbhip_sel_select", "tsdbhip_assemble", "tsdbhip_run_multi",
 ]
 
 
@@ -74,6 +74,7 @@ def lib():
         L.tsdbhip_finalize.argtypes = [vp, C.POINTER(abi.Query), C.c_int64, C.c_void_p, C.c_int,
                                        C.POINTER(C.POINTER(abi.Result))]
         L.tsdbhip_sync.argtypes = [vp]
+        L.tsdbhip_run_multi.argtypes = [vp, C.POINTER(abi.Query), C.c_int, C.POINTER(C.POINTER(abi.Result))]
         L.tsdbhip_sel_layout.argtypes = [vp, C.POINTER(abi.Query), C.c_int64, C.c_void_p, C.POINTER(C.c_int64)]
         L.tsdbhip_sel_run_values.argtypes = [vp, C.POINTER(abi.Query), C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
         L.tsdbhip_sel_select.argtypes = [vp, C.POINTER(abi.Query), C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -210,6 +211,14 @@ class Engine:
         res = C.POINTER(abi.Result)()
         _check(lib().tsdbhip_run(self.ctx, C.byref(q), C.byref(res)))
         return abi.result_to_groups(res.contents, owner=_ResultOwner(res))
+
+    def run_multi(self, queries):
+        """tsdbhip_run_multi: one decode + downsample pass shared by several queries."""
+        n = len(queries)
+        arr = (abi.Query * n)(*queries)
+        outs = (C.POINTER(abi.Result) * n)()
+        _check(lib().tsdbhip_run_multi(self.ctx, arr, n, outs))
+        return [abi.result_to_groups(outs[i].contents, owner=_ResultOwner(outs[i])) for i in range(n)]
 
     def run_batch(self, batch: abi.HostBatch, q: abi.Query):
         """Runner for TsdbQuery: load the query's spans, then run."""

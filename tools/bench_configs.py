@@ -102,6 +102,7 @@ def main():
     ap.add_argument("--cpu", action="store_true", help="time the oracle on one group")
     ap.add_argument("--only", default="", help="comma-separated group-by aggregators to run (config 3)")
     ap.add_argument("--ordered", action="store_true", help="TSDB_QF_ORDERED (bit-exact span-order float reductions)")
+    ap.add_argument("--multi", action="store_true", help="config 3: the queries through one tsdbhip_run_multi call")
     args = ap.parse_args()
     from opentsdb_amd import abi, dist, synth
     from opentsdb_amd.engine import Engine, parse_downsample
@@ -121,7 +122,24 @@ def main():
             for q in qs.values():
                 q.flags = abi.QF_ORDERED
             qs = {k + " (ordered)": v for k, v in qs.items()}
-        grid_config(args, eng, qs, series, 360, 2, 30000, groups)
+        if args.multi:
+            eng.synth(series, T0, 360, 10000, 2, groups, 30000, 0x5EED)
+            eng.sync()
+            ql = list(qs.values())
+            eng.run_multi(ql)
+            ms = []
+            for _ in range(args.steps):
+                t = time.perf_counter()
+                eng.run_multi(ql)
+                ms.append((time.perf_counter() - t) * 1000)
+            tm = eng.timing()
+            step = sum(ms) / len(ms)
+            print(json.dumps({"config": 3, "query": "run_multi " + ",".join(qs), "series": series, "groups": groups,
+                              "datapoints": int(tm.datapoints), "ms_per_step": step,
+                              "separate_queries_note": "compare with the per-query ms_per_step lines",
+                              "datapoints_per_s_per_query": tm.datapoints * len(ql) / (step / 1000)}), flush=True)
+        else:
+            grid_config(args, eng, qs, series, 360, 2, 30000, groups)
         eng.close()
         return
     if args.config == 5:
@@ -129,6 +147,16 @@ def main():
         series = args.series if args.series != 100_000 else 1_250_000
         qs = {f"sum:1h-{f}": dsq("sum", f"1h-{f}", T0 + 86399) for f in ["p99", "ep99r7"]}
         grid_config(args, eng, qs, series, 8640, 0, 1, args.groups)
+        # four group-by aggregators over one 1h-p99 downsampling: shared selection pass
+        ql = [dsq(a, "1h-p99", T0 + 86399) for a in ["sum", "max", "min", "avg"]]
+        eng.run_multi(ql)
+        ms = []
+        for _ in range(args.steps):
+            t = time.perf_counter()
+            eng.run_multi(ql)
+            ms.append((time.perf_counter() - t) * 1000)
+        print(json.dumps({"config": 5, "query": "run_multi {sum,max,min,avg}:1h-p99", "series": series,
+                          "ms_per_step": sum(ms) / len(ms)}), flush=True)
         rollup_bench(args, eng, series)
         eng.close()
         return
