@@ -226,7 +226,7 @@ struct tsdbhip_ctx {
   DevBuf cal_bounds;                                // calendar month / year slot boundaries
   // raw path scratch
   DevBuf r_rowpt, r_spoff, r_spn, r_grp, r_pts, r_rank, r_bm, r_wb, r_U, r_ooff, r_sg, r_su, r_ots, r_obits, r_oint,
-      r_coff, r_cur;                   // multi-GPU: this rank's partial states, gathered states
+      r_coff, r_cur, r_voff, r_vl, r_vd, r_vp;                   // multi-GPU: this rank's partial states, gathered states
   // dominant uniform row class of the batch (k_fast specialisation), 0 = none
   int fast_qw = 0, fast_vl = 0;        // dominant k_fast row class (0 = none)
   int fast_qw2 = 0, fast_vl2 = 0;      // second class, chained over the first one's redo list
@@ -408,7 +408,7 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   for (DevBuf* b : {&c->pa, &c->pb, &c->pn, &c->pf, &c->out_val, &c->out_flag, &c->gact, &c->err, &c->g_dense,
                     &c->g_pres, &c->g_rate, &c->redo, &c->redo_n, &c->redo2, &c->redo2_n, &c->d_tl, &c->d_tl_n, &c->r1a, &c->r1b, &c->r2, &c->r_n, &c->xbuf, &c->gbuf, &c->r_rowpt,
                     &c->r_spoff, &c->r_spn, &c->r_grp, &c->r_pts, &c->r_rank, &c->r_bm, &c->r_wb, &c->r_U, &c->r_ooff,
-                    &c->r_sg, &c->r_su, &c->r_ots, &c->r_obits, &c->r_oint, &c->r_coff, &c->r_cur, &c->pre_dense, &c->pre_pres,
+                    &c->r_sg, &c->r_su, &c->r_ots, &c->r_obits, &c->r_oint, &c->r_coff, &c->r_cur, &c->r_voff, &c->r_vl, &c->r_vd, &c->r_vp, &c->pre_dense, &c->pre_pres,
                     &c->ro_allint, &c->ro_ord, &c->ro_orig, &c->ro_cnt, &c->ro_vsz, &c->ro_coff, &c->ro_voff})
     b->release();
   for (auto& o : c->ro_out)
@@ -966,10 +966,11 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
   if (q->ds_function == TSDB_AGG_NONE) return fail(TSDB_E_ILLEGAL_ARGUMENT, "cannot use the NONE aggregator for downsampling");
   if (q->ds_function < 0) {
     P.raw = true;
-    if (is_sel_agg(q->aggregator))
-      return fail(TSDB_E_NOT_IMPLEMENTED, std::string("percentile / median group-by without downsampling: ") +
-                                              AGG_NAMES[q->aggregator]);
     P.ga = ga_of(q->aggregator);
+    if (P.ga < 0 && is_sel_agg(q->aggregator)) {
+      P.gsel = q->aggregator;   // span operands per union point, then k_raw_sel
+      P.ga = GA_NONE;           // placeholder: k_raw_eval does not run
+    }
     if (P.ga < 0) return fail(TSDB_E_NOT_IMPLEMENTED, std::string("group-by aggregator not implemented yet: ") + AGG_NAMES[q->aggregator]);
     P.interp = interp_of(q->aggregator);
     P.none = q->aggregator == TSDB_AGG_NONE;
@@ -1807,8 +1808,38 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
     rp.out_int = c->r_oint.as<uint8_t>();
     HIP_OK(launch_raw_rank(rp, grp_ser[g0], grp_ser[g1], c->stream));
     HIP_OK(launch_raw_cursor(rp, grp_ser[g0], grp_ser[g1], c->stream));
-    HIP_OK(hipEventRecord(c->ev[3], c->stream));
-    HIP_OK(launch_raw_eval(rp, c->stream));
+    if (P.gsel) {
+      // percentile / median: every span operand of every union point (span-major per group)
+      std::vector<int64_t> voff(ng + 1, 0);
+      for (int64_t i = 0; i < ng; i++) {
+        const int64_t k = grp_ser[g0 + i + 1] - grp_ser[g0 + i];
+        if (k > SEL_CAP)
+          return fail(TSDB_E_NOT_IMPLEMENTED, "percentile / median group-by without downsampling over a group of more than " +
+                                                  std::to_string(SEL_CAP) + " spans");
+        voff[i + 1] = voff[i] + (int64_t)U[i] * k;
+      }
+      const int64_t nv = voff[ng];
+      if (nv > ((int64_t)1 << 28))
+        return fail(TSDB_E_NOT_IMPLEMENTED, "percentile / median group-by without downsampling: more than 2^28 span operands");
+      HIP_OK(c->r_voff.ensure((ng + 1) * 8));
+      HIP_OK(c->r_vl.ensure(std::max<int64_t>(1, nv) * 8));
+      HIP_OK(c->r_vd.ensure(std::max<int64_t>(1, nv) * 8));
+      HIP_OK(c->r_vp.ensure(std::max<int64_t>(1, nv)));
+      HIP_OK(hipMemcpyAsync(c->r_voff.p, voff.data(), (ng + 1) * 8, hipMemcpyHostToDevice, c->stream));
+      HIP_OK(hipMemsetAsync(c->r_vp.p, 0, std::max<int64_t>(1, nv), c->stream));
+      HIP_OK(hipMemsetAsync(c->r_vd.p, 0xFF, std::max<int64_t>(1, nv) * 8, c->stream));   // NaN: no operand
+      rp.sel_fn = P.gsel;
+      rp.vals_off = c->r_voff.as<int64_t>();
+      rp.vals_l = c->r_vl.as<int64_t>();
+      rp.vals_d = c->r_vd.as<double>();
+      rp.vals_p = c->r_vp.as<uint8_t>();
+      HIP_OK(hipEventRecord(c->ev[3], c->stream));
+      HIP_OK(launch_raw_vals(rp, c->stream));
+      HIP_OK(launch_raw_sel(rp, nout, c->stream));
+    } else {
+      HIP_OK(hipEventRecord(c->ev[3], c->stream));
+      HIP_OK(launch_raw_eval(rp, c->stream));
+    }
     HIP_OK(hipEventRecord(c->ev[1], c->stream));
     const size_t base = res_ts.size();
     if (direct) {

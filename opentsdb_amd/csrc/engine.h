@@ -236,6 +236,13 @@ struct RawParams {
   uint64_t* out_bits;
   uint8_t* out_int;
   int32_t* err;
+  // percentile / median group-by (k_raw_vals, k_raw_sel): span i's value at union point u of
+  // chunk group gi sits at vals_off[gi] + i * U + u (span-major: lanes over u coalesce)
+  int32_t sel_fn;              // TSDB_AGG_* (median / pXX / epXXrY); 0 = not a selection query
+  const int64_t* vals_off;     // [g1 - g0]
+  int64_t* vals_l;             // runLong operands
+  double* vals_d;              // runDouble operands (NaN = no value; runDouble skips NaNs)
+  uint8_t* vals_p;             // 1 = the span has a long operand at the point
 };
 
 struct SynthParams {
@@ -318,6 +325,8 @@ hipError_t launch_raw_union(const RawParams& p, int64_t s_begin, int64_t s_end, 
 hipError_t launch_raw_rank(const RawParams& p, int64_t s_begin, int64_t s_end, hipStream_t s);   // rank + union ts
 hipError_t launch_raw_cursor(const RawParams& p, int64_t s_begin, int64_t s_end, hipStream_t s);
 hipError_t launch_raw_eval(const RawParams& p, hipStream_t s);
+hipError_t launch_raw_vals(const RawParams& p, hipStream_t s);
+hipError_t launch_raw_sel(const RawParams& p, int64_t n_out, hipStream_t s);
 template <int GA> hipError_t launch_raw_eval_inst(const RawParams& p, hipStream_t s);   // k_raw_eval.hip
 hipError_t launch_synth_write(const SynthParams& p, hipStream_t s);
 

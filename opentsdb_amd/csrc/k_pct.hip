@@ -1018,4 +1018,146 @@ hipError_t launch_emit(const GridParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---- percentile / median group-by without downsampling (raw timestamp union) --------------
+// One block per union point.  The point's span operands (k_raw_vals) are staged in LDS as
+// order-preserving keys; the order statistics come from radix_select.  isInteger at the point
+// (AggregationIterator.isInteger :612-625) picks the reducer, as longValue / doubleValue do:
+//   runLong   (src/core/Aggregators.java:403-413 Median, :675-686 PercentileAgg): every span
+//             operand, the estimation type honoured (LEGACY / R_3 / R_7), (long) of the estimate;
+//   runDouble (:416-430, :689-706): NaNs skipped, LEGACY always.
+__device__ __forceinline__ int64_t sel_d2l(double d) {   // Java (long) of a double
+  if (isnan(d)) return 0;
+  if (d >= 9223372036854775807.0) return 0x7FFFFFFFFFFFFFFFLL;
+  if (d <= -9223372036854775808.0) return (int64_t)0x8000000000000000ULL;
+  return (int64_t)d;
+}
+
+__global__ __launch_bounds__(256) void k_raw_sel(RawParams p, int64_t n_out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ SelShared S;
+  __shared__ unsigned long long red[2];
+  const int64_t idx = blockIdx.x;
+  if (idx >= n_out) return;
+  const int tid = threadIdx.x;
+  // chunk group of the point: out_off is ascending over [0, g1 - g0]
+  int64_t lo = 0, hi = p.g1 - p.g0;   // out_off[lo] <= idx < out_off[hi]
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (p.out_off[mid] <= idx) lo = mid; else hi = mid;
+  }
+  const int64_t gi = lo;
+  const int64_t U = p.out_off[gi + 1] - p.out_off[gi];
+  const int64_t u = idx - p.out_off[gi];
+  const int64_t g = gi + p.g0;
+  const int64_t k = p.grp_ser[g + 1] - p.grp_ser[g];
+  const int64_t vb = p.vals_off[gi] + u;
+  const bool is_int = p.out_int[idx] != 0;
+  uint64_t* keys = reinterpret_cast<uint64_t*>(smem);
+  if (tid == 0) { red[0] = 0; red[1] = 0; }
+  __syncthreads();
+  int64_t m = 0;
+  if (is_int) {
+    // present long operands, compacted (their order does not matter to a selection)
+    for (int64_t i = tid; i < k; i += blockDim.x) {
+      if (p.vals_p[vb + i * U]) {
+        const uint64_t key = (uint64_t)p.vals_l[vb + i * U] ^ 0x8000000000000000ULL;
+        keys[atomicAdd(&red[0], 1ULL)] = key;
+      }
+    }
+    __syncthreads();
+    m = (int64_t)red[0];
+  } else {
+    uint32_t nan_local = 0;
+    for (int64_t i = tid; i < k; i += blockDim.x) {
+      const double x = p.vals_d[vb + i * U];
+      nan_local += isnan(x) ? 1u : 0u;
+      keys[i] = f2key(canon_nan(x));
+    }
+    if (nan_local) atomicAdd(&red[0], (unsigned long long)nan_local);
+    __syncthreads();
+    m = k - (int64_t)red[0];
+  }
+  const int64_t n = is_int ? m : k;   // keys staged
+  const int fn = p.sel_fn;
+  // ranks r0 (and r1 = r0 + 1 when interpolating) and the weight of the estimate
+  int64_t r0 = 0, r1 = -1;
+  double dif = 0.0;
+  const int est = fn == TSDB_AGG_MEDIAN ? 0 : (is_int ? (fn - TSDB_AGG_P999) / 6 : 0);   // runDouble: LEGACY
+  if (m > 1 && fn != TSDB_AGG_MEDIAN) {
+    const double q = pct_quantile(fn) / 100.0;
+    double pos;
+    if (est == 1) {            // R_3
+      pos = (q <= 0.5 / (double)m) ? 0.0 : rint((double)m * q);
+    } else if (est == 2) {     // R_7
+      pos = (q == 0.0) ? 0.0 : (q == 1.0 ? (double)m : 1.0 + (double)(m - 1) * q);
+    } else {                   // LEGACY
+      pos = (q == 0.0) ? 0.0 : (q == 1.0 ? (double)m : q * (double)(m + 1));
+    }
+    const double fpos = floor(pos);
+    if (pos < 1) r0 = 0;
+    else if (pos >= (double)m) r0 = m - 1;
+    else { r0 = (int64_t)fpos - 1; r1 = r0 + 1; dif = pos - fpos; }
+  } else if (m > 0 && fn == TSDB_AGG_MEDIAN) {
+    r0 = m / 2;
+  }
+  uint64_t k0 = 0, k1 = 0;
+  if (m > 0) {
+    k0 = radix_select(keys, n, r0, S);
+    k1 = k0;
+    if (r1 >= 0) {
+      if (tid == 0) { red[0] = 0; red[1] = ~0ULL; }
+      __syncthreads();
+      uint32_t le = 0;
+      uint64_t gt = ~0ULL;
+      for (int64_t j = tid; j < n; j += blockDim.x) {
+        const uint64_t kk = keys[j];
+        if (kk <= k0) le++;
+        else gt = kk < gt ? kk : gt;
+      }
+      atomicAdd(&red[0], (unsigned long long)le);
+      atomicMin(&red[1], (unsigned long long)gt);
+      __syncthreads();
+      k1 = (int64_t)red[0] > r1 ? k0 : red[1];
+    }
+  }
+  if (tid != 0) return;
+  uint64_t bits;
+  if (is_int) {
+    const int64_t l0 = (int64_t)(k0 ^ 0x8000000000000000ULL), l1 = (int64_t)(k1 ^ 0x8000000000000000ULL);
+    int64_t r;
+    if (fn == TSDB_AGG_MEDIAN) {
+      if (m == 0) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // "Shouldn't be here without any data"
+      r = l0;
+    } else if (m == 0) {
+      r = 0;                                               // (long) NaN
+    } else if (r1 < 0) {
+      r = sel_d2l((double)l0);
+    } else {
+      const double lower = (double)l0, upper = (double)l1;
+      r = sel_d2l(lower + dif * (upper - lower));
+    }
+    bits = (uint64_t)r;
+  } else {
+    double r;
+    if (m == 0) r = NAN;
+    else if (r1 < 0) r = key2f(k0);
+    else {
+      const double lower = key2f(k0), upper = key2f(k1);
+      r = lower + dif * (upper - lower);
+    }
+    if (isinf(r)) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // doubleValue (:640-643)
+    bits = (uint64_t)__double_as_longlong(r);
+  }
+  p.out_bits[idx] = bits;
+}
+
+hipError_t launch_raw_sel(const RawParams& p, int64_t n_out, hipStream_t s) {
+  if (n_out == 0) return hipSuccess;
+  const size_t lds = (size_t)SEL_CAP * 8;
+  hipError_t e = hipFuncSetAttribute((const void*)k_raw_sel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_raw_sel, dim3((unsigned)n_out), dim3(256), lds, s, p, n_out);
+  return hipGetLastError();
+}
+
 }  // namespace tsdb

@@ -322,4 +322,146 @@ hipError_t launch_raw_eval_inst<GA_ID>(const RawParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+#if GA_ID == 11
+// Percentile / median as the group-by aggregator without downsampling (PercentileAgg and
+// Median collect the span values of each union point, src/core/Aggregators.java:397-431,
+// :657-708): the traversal of k_raw_eval, but each span's operand (exact or interpolated,
+// long and/or double as nextLongValue / nextDoubleValue produce it) is stored at
+// vals_off[gi] + i * U + u instead of being folded; k_raw_sel (k_pct.hip) selects.
+template <bool DL, bool DD, bool RATE>
+__global__ __launch_bounds__(64) void k_raw_vals(RawParams p) {
+  __shared__ uint64_t wmask[RAW_W];
+  const int lane = lane_id();
+  const int64_t strip = blockIdx.x;
+  if (strip >= p.n_strips) return;
+  const int64_t gi = p.strip_g[strip];
+  const int64_t t = p.strip_t[strip];
+  const int64_t g = gi + p.g0;
+  const int64_t U = p.U[gi];
+  const int64_t ns = (U + RAW_STRIP - 1) / RAW_STRIP;
+  const int64_t ua = t * RAW_STRIP;
+  const int64_t ub = min(U, ua + (int64_t)RAW_STRIP);
+  const int64_t sb = p.grp_ser[g];
+  const int k = (int)(p.grp_ser[g + 1] - sb);
+  constexpr int first = RATE ? 1 : 0;
+  const int interp = p.interp;
+  const int32_t* crow = p.cur + p.cur_off[gi] + t * k;
+  const int32_t* cnext = (t + 1 < ns) ? crow + k : nullptr;
+  const int64_t obase = p.out_off[gi];
+  const int64_t vbase = p.vals_off[gi];
+  const uint64_t below = (lane == 63) ? ~0ULL : ((2ULL << lane) - 1ULL);
+
+  int64_t x[RAW_W];
+  bool in[RAW_W];
+  uint32_t flt = 0;
+#pragma unroll
+  for (int w = 0; w < RAW_W; w++) {
+    const int64_t u = ua + 64 * w + lane;
+    in[w] = u < ub;
+    x[w] = in[w] ? p.out_ts[obase + u] : 0;
+  }
+  auto put_l = [&](int i, int w, int64_t v) {
+    if (!in[w]) return;
+    const int64_t o = vbase + (int64_t)i * U + ua + 64 * w + lane;
+    p.vals_l[o] = v;
+    p.vals_p[o] = 1;
+  };
+  auto put_d = [&](int i, int w, double v) {
+    if (!in[w]) return;
+    p.vals_d[vbase + (int64_t)i * U + ua + 64 * w + lane] = v;
+  };
+
+  for (int i = 0; i < k; i++) {
+    const int64_t s = sb + i;
+    const int n = p.sp_n[s];
+    if (n < (RATE ? 2 : 1)) continue;
+    const int nc = n - first;
+    const RawPt* pts = p.pts + p.sp_off[s];
+    const int c = crow[i];
+    const int m = (cnext ? cnext[i] : nc) - c;
+    if (m == 0) {
+      if (RATE) {
+        if (c == nc) continue;
+        const double y = __longlong_as_double((long long)pts[c].bits);
+#pragma unroll
+        for (int w = 0; w < RAW_W; w++) put_d(i, w, y);
+      } else {
+        if (c == 0) {
+          if (pts[0].tsf & RAW_FLOAT) flt = (1u << RAW_W) - 1;
+          continue;
+        }
+        if (c == n) continue;
+        const RawPt a = pts[c - 1], b = pts[c];
+        if ((a.tsf | b.tsf) & RAW_FLOAT) flt = (1u << RAW_W) - 1;
+        const int64_t x0 = a.tsf & RAW_TIME_MASK, x1 = b.tsf & RAW_TIME_MASK;
+#pragma unroll
+        for (int w = 0; w < RAW_W; w++) {
+          if (DL) put_l(i, w, jlerp(interp, x[w], x0, (int64_t)a.bits, x1, (int64_t)b.bits));
+          if (DD) put_d(i, w, dlerp(interp, x[w], x0, pt_double(a.tsf, a.bits), x1, pt_double(b.tsf, b.bits)));
+        }
+      }
+      continue;
+    }
+    if (lane < RAW_W) wmask[lane] = 0;
+    WAVE_SYNC();
+    const int32_t* rk = p.rank + p.sp_off[s] + first + c;
+    for (int l = lane; l < m; l += 64) {
+      const int64_t o = rk[l] - ua;
+      __hip_atomic_fetch_or(&wmask[o >> 6], 1ULL << (o & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    WAVE_SYNC();
+    int tb = 0;
+#pragma unroll
+    for (int w = 0; w < RAW_W; w++) {
+      const uint64_t M = wmask[w];
+      const int cnt = c + tb + __popcll(M & below);
+      const bool own = (M >> lane) & 1ULL;
+      tb += __popcll(M);
+      if (RATE) {
+        if (cnt == nc && !own) continue;
+        put_d(i, w, __longlong_as_double((long long)pts[cnt].bits));
+      } else {
+        if (cnt == 0) {
+          if (pts[0].tsf & RAW_FLOAT) flt |= 1u << w;
+          continue;
+        }
+        const int j = cnt - 1;
+        const RawPt a = pts[j];
+        if (j == n - 1 && !own) continue;
+        if (j == n - 1 || own) {
+          if (a.tsf & RAW_FLOAT) flt |= 1u << w;
+          if (j < n - 1 && (pts[j + 1].tsf & RAW_FLOAT)) flt |= 1u << w;
+          if (DL) put_l(i, w, (int64_t)a.bits);
+          if (DD) put_d(i, w, pt_double(a.tsf, a.bits));
+          continue;
+        }
+        const RawPt b = pts[j + 1];
+        if ((a.tsf | b.tsf) & RAW_FLOAT) flt |= 1u << w;
+        const int64_t x0 = a.tsf & RAW_TIME_MASK, x1 = b.tsf & RAW_TIME_MASK;
+        if (DL) put_l(i, w, jlerp(interp, x[w], x0, (int64_t)a.bits, x1, (int64_t)b.bits));
+        if (DD) put_d(i, w, dlerp(interp, x[w], x0, pt_double(a.tsf, a.bits), x1, pt_double(b.tsf, b.bits)));
+      }
+    }
+    WAVE_SYNC();
+  }
+
+#pragma unroll
+  for (int w = 0; w < RAW_W; w++) {
+    const int64_t u = ua + 64 * w + lane;
+    if (u >= ub) continue;
+    p.out_int[obase + u] = (!RATE && !((flt >> w) & 1)) ? 1 : 0;
+  }
+}
+
+hipError_t launch_raw_vals(const RawParams& p, hipStream_t s) {
+  if (p.n_strips == 0) return hipSuccess;
+  const dim3 grid((unsigned)p.n_strips), block(64);
+  if (p.rate) hipLaunchKernelGGL((k_raw_vals<false, true, true>), grid, block, 0, s, p);
+  else if (p.do_long && p.do_double) hipLaunchKernelGGL((k_raw_vals<true, true, false>), grid, block, 0, s, p);
+  else if (p.do_long) hipLaunchKernelGGL((k_raw_vals<true, false, false>), grid, block, 0, s, p);
+  else hipLaunchKernelGGL((k_raw_vals<false, true, false>), grid, block, 0, s, p);
+  return hipGetLastError();
+}
+#endif
+
 }  // namespace tsdb

@@ -217,7 +217,8 @@ def raw_batch():
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 4])
-@pytest.mark.parametrize("agg", ["sum", "avg", "min", "max", "dev", "zimsum", "mimmax", "first", "diff", "pfsum"])
+@pytest.mark.parametrize("agg", ["sum", "avg", "min", "max", "dev", "zimsum", "mimmax", "first", "diff", "pfsum",
+                                 "p99", "ep90r3", "median"])
 def test_group_sharded_raw_equals_oracle(engines, raw_batch, world, agg):
     q = abi.new_query(T0, T0 + 7199, agg)
     parts = []

@@ -2,8 +2,8 @@
 AggregationIterator hands PercentileAgg.runDouble / Median.runDouble one value per span at
 each union timestamp -- the span's bucket value or its LERP between neighbouring buckets
 (src/core/AggregationIterator.java:735-797) -- and runDouble drops NaNs and always uses
-LEGACY estimation (src/core/Aggregators.java:689-706; Median :416-430).  Downsampled
-queries only: the engine refuses them without a downsampler (NOT_IMPLEMENTED).
+LEGACY estimation (src/core/Aggregators.java:689-706; Median :416-430).  Queries without a
+downsampler run on the raw path (tests/test_gpu_pct_raw.py).
 
 Results are order statistics of exactly computed per-series values (plus commons-math3's
 `lower + d * (upper - lower)`), so the bar is bit-exact against the oracle."""
@@ -116,13 +116,6 @@ def test_pct_group_nan_members(eng):
     for agg in ["p90", "median"]:
         q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["max"], ds_interval_ms=600000)
         assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), agg, tol=0.0, ctx=agg)
-
-
-def test_pct_group_without_downsampling_not_implemented(eng, mixed_batch):
-    q = abi.new_query(T0, T0 + 3599, "p99")
-    with pytest.raises(Exception) as ei:
-        eng.run_batch(mixed_batch, q)
-    assert "notimplemented" in str(ei.value).lower().replace(" ", "")
 
 
 def test_pct_group_segment_beyond_lds(eng):
