@@ -1809,33 +1809,57 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
     HIP_OK(launch_raw_rank(rp, grp_ser[g0], grp_ser[g1], c->stream));
     HIP_OK(launch_raw_cursor(rp, grp_ser[g0], grp_ser[g1], c->stream));
     if (P.gsel) {
-      // percentile / median: every span operand of every union point (span-major per group)
-      std::vector<int64_t> voff(ng + 1, 0);
-      for (int64_t i = 0; i < ng; i++) {
-        const int64_t k = grp_ser[g0 + i + 1] - grp_ser[g0 + i];
-        if (k > SEL_CAP)
+      // percentile / median: every span operand of every union point, strip by strip
+      // (RAW_STRIP points x the group's spans each), in batches of at most kSelOps operands
+      int64_t kSelOps = (int64_t)1 << 28;
+      if (const char* e = std::getenv("TSDBHIP_SELOPS")) kSelOps = std::max<int64_t>(1, std::atoll(e));   // tests: force batches
+      for (int64_t i = 0; i < ng; i++)
+        if (grp_ser[g0 + i + 1] - grp_ser[g0 + i] > SEL_CAP)
           return fail(TSDB_E_NOT_IMPLEMENTED, "percentile / median group-by without downsampling over a group of more than " +
                                                   std::to_string(SEL_CAP) + " spans");
-        voff[i + 1] = voff[i] + (int64_t)U[i] * k;
+      std::vector<int64_t> soff(ns + 1, 0);
+      for (int64_t t = 0; t < ns; t++) soff[t + 1] = soff[t] + (grp_ser[g0 + sg[t] + 1] - grp_ser[g0 + sg[t]]) * RAW_STRIP;
+      // batches [bat[i], bat[i + 1]) of strips: at least one strip each, else <= kSelOps operands
+      std::vector<int64_t> bat{0};
+      int64_t nv_max = 1;
+      for (int64_t s0 = 0; s0 < ns;) {
+        int64_t s1 = s0 + 1;
+        while (s1 < ns && soff[s1 + 1] - soff[s0] <= kSelOps) s1++;
+        nv_max = std::max<int64_t>(nv_max, soff[s1] - soff[s0]);
+        bat.push_back(s1);
+        s0 = s1;
       }
-      const int64_t nv = voff[ng];
-      if (nv > ((int64_t)1 << 28))
-        return fail(TSDB_E_NOT_IMPLEMENTED, "percentile / median group-by without downsampling: more than 2^28 span operands");
-      HIP_OK(c->r_voff.ensure((ng + 1) * 8));
-      HIP_OK(c->r_vl.ensure(std::max<int64_t>(1, nv) * 8));
-      HIP_OK(c->r_vd.ensure(std::max<int64_t>(1, nv) * 8));
-      HIP_OK(c->r_vp.ensure(std::max<int64_t>(1, nv)));
-      HIP_OK(hipMemcpyAsync(c->r_voff.p, voff.data(), (ng + 1) * 8, hipMemcpyHostToDevice, c->stream));
-      HIP_OK(hipMemsetAsync(c->r_vp.p, 0, std::max<int64_t>(1, nv), c->stream));
-      HIP_OK(hipMemsetAsync(c->r_vd.p, 0xFF, std::max<int64_t>(1, nv) * 8, c->stream));   // NaN: no operand
+      HIP_OK(c->r_voff.ensure(std::max<int64_t>(1, ns) * 8));
+      HIP_OK(c->r_vl.ensure(nv_max * 8));
+      HIP_OK(c->r_vd.ensure(nv_max * 8));
+      HIP_OK(c->r_vp.ensure(nv_max));
       rp.sel_fn = P.gsel;
-      rp.vals_off = c->r_voff.as<int64_t>();
       rp.vals_l = c->r_vl.as<int64_t>();
       rp.vals_d = c->r_vd.as<double>();
       rp.vals_p = c->r_vp.as<uint8_t>();
       HIP_OK(hipEventRecord(c->ev[3], c->stream));
-      HIP_OK(launch_raw_vals(rp, c->stream));
-      HIP_OK(launch_raw_sel(rp, nout, c->stream));
+      // every strip's operand offset relative to its batch, uploaded once
+      std::vector<int64_t> boff(std::max<int64_t>(1, ns), 0);
+      for (size_t bi = 0; bi + 1 < bat.size(); bi++)
+        for (int64_t t = bat[bi]; t < bat[bi + 1]; t++) boff[t] = soff[t] - soff[bat[bi]];
+      HIP_OK(hipMemcpyAsync(c->r_voff.p, boff.data(), std::max<int64_t>(1, ns) * 8, hipMemcpyHostToDevice, c->stream));
+      HIP_OK(hipStreamSynchronize(c->stream));   // `boff` leaves scope before the chunk's sync
+      HIP_OK(hipMemsetAsync(rp.out_int, 1, std::max<int64_t>(1, nout), c->stream));   // isInteger until a double is seen
+      for (size_t bi = 0; bi + 1 < bat.size(); bi++) {
+        const int64_t s0 = bat[bi], s1 = bat[bi + 1];
+        const int64_t nv = soff[s1] - soff[s0];
+        HIP_OK(hipMemsetAsync(c->r_vp.p, 0, nv, c->stream));
+        HIP_OK(hipMemsetAsync(c->r_vd.p, 0xFF, nv * 8, c->stream));   // NaN: no operand
+        RawParams bp = rp;
+        bp.strip_g = rp.strip_g + s0;
+        bp.strip_t = rp.strip_t + s0;
+        bp.n_strips = s1 - s0;
+        bp.vals_off = c->r_voff.as<int64_t>() + s0;
+        int64_t k_max = 1;
+        for (int64_t t = s0; t < s1; t++) k_max = std::max<int64_t>(k_max, grp_ser[g0 + sg[t] + 1] - grp_ser[g0 + sg[t]]);
+        HIP_OK(launch_raw_vals(bp, k_max, c->stream));
+        HIP_OK(launch_raw_sel(bp, k_max, c->stream));
+      }
     } else {
       HIP_OK(hipEventRecord(c->ev[3], c->stream));
       HIP_OK(launch_raw_eval(rp, c->stream));

@@ -200,6 +200,7 @@ static constexpr int64_t RAW_FLOAT = (int64_t)0x8000000000000000ULL;
 static constexpr int64_t RAW_TIME_MASK = 0x7FFFFFFFFFFFFFFFLL;
 static constexpr int RAW_W = 8;                // 64-point windows per k_raw_eval wave
 static constexpr int RAW_STRIP = 64 * RAW_W;   // union points per k_raw_eval wave
+static constexpr int RAW_SEL_SPANS = 32;       // spans per k_raw_vals wave
 
 struct RawParams {
   // decode
@@ -236,10 +237,11 @@ struct RawParams {
   uint64_t* out_bits;
   uint8_t* out_int;
   int32_t* err;
-  // percentile / median group-by (k_raw_vals, k_raw_sel): span i's value at union point u of
-  // chunk group gi sits at vals_off[gi] + i * U + u (span-major: lanes over u coalesce)
+  // percentile / median group-by (k_raw_vals, k_raw_sel) over a batch of strips (strip_g /
+  // strip_t point at the batch's first strip): span i's operand at point ua + j of batch
+  // strip b sits at vals_off[b] + i * RAW_STRIP + j (span-major: the lanes of a wave coalesce)
   int32_t sel_fn;              // TSDB_AGG_* (median / pXX / epXXrY); 0 = not a selection query
-  const int64_t* vals_off;     // [g1 - g0]
+  const int64_t* vals_off;     // [n_strips] of the batch
   int64_t* vals_l;             // runLong operands
   double* vals_d;              // runDouble operands (NaN = no value; runDouble skips NaNs)
   uint8_t* vals_p;             // 1 = the span has a long operand at the point
@@ -325,8 +327,8 @@ hipError_t launch_raw_union(const RawParams& p, int64_t s_begin, int64_t s_end, 
 hipError_t launch_raw_rank(const RawParams& p, int64_t s_begin, int64_t s_end, hipStream_t s);   // rank + union ts
 hipError_t launch_raw_cursor(const RawParams& p, int64_t s_begin, int64_t s_end, hipStream_t s);
 hipError_t launch_raw_eval(const RawParams& p, hipStream_t s);
-hipError_t launch_raw_vals(const RawParams& p, hipStream_t s);
-hipError_t launch_raw_sel(const RawParams& p, int64_t n_out, hipStream_t s);
+hipError_t launch_raw_vals(const RawParams& p, int64_t k_max, hipStream_t s);
+hipError_t launch_raw_sel(const RawParams& p, int64_t k_max, hipStream_t s);
 template <int GA> hipError_t launch_raw_eval_inst(const RawParams& p, hipStream_t s);   // k_raw_eval.hip
 hipError_t launch_synth_write(const SynthParams& p, hipStream_t s);
 

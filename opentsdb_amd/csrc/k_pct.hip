@@ -1032,25 +1032,23 @@ __device__ __forceinline__ int64_t sel_d2l(double d) {   // Java (long) of a dou
   return (int64_t)d;
 }
 
-__global__ __launch_bounds__(256) void k_raw_sel(RawParams p, int64_t n_out) {
+// One block per union point of the batch's strips: block b -> strip b / RAW_STRIP, point j.
+__global__ __launch_bounds__(256) void k_raw_sel(RawParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ SelShared S;
   __shared__ unsigned long long red[2];
-  const int64_t idx = blockIdx.x;
-  if (idx >= n_out) return;
+  const int64_t sl = blockIdx.x / RAW_STRIP;
+  const int64_t j = blockIdx.x - sl * RAW_STRIP;
+  if (sl >= p.n_strips) return;
   const int tid = threadIdx.x;
-  // chunk group of the point: out_off is ascending over [0, g1 - g0]
-  int64_t lo = 0, hi = p.g1 - p.g0;   // out_off[lo] <= idx < out_off[hi]
-  while (hi - lo > 1) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (p.out_off[mid] <= idx) lo = mid; else hi = mid;
-  }
-  const int64_t gi = lo;
-  const int64_t U = p.out_off[gi + 1] - p.out_off[gi];
-  const int64_t u = idx - p.out_off[gi];
+  const int64_t gi = p.strip_g[sl];
+  const int64_t u = (int64_t)p.strip_t[sl] * RAW_STRIP + j;
+  if (u >= p.U[gi]) return;
+  const int64_t idx = p.out_off[gi] + u;
   const int64_t g = gi + p.g0;
   const int64_t k = p.grp_ser[g + 1] - p.grp_ser[g];
-  const int64_t vb = p.vals_off[gi] + u;
+  const int64_t vb = p.vals_off[sl] + j;
+  constexpr int64_t U = RAW_STRIP;   // operand stride between spans
   const bool is_int = p.out_int[idx] != 0;
   uint64_t* keys = reinterpret_cast<uint64_t*>(smem);
   if (tid == 0) { red[0] = 0; red[1] = 0; }
@@ -1151,12 +1149,14 @@ __global__ __launch_bounds__(256) void k_raw_sel(RawParams p, int64_t n_out) {
   p.out_bits[idx] = bits;
 }
 
-hipError_t launch_raw_sel(const RawParams& p, int64_t n_out, hipStream_t s) {
-  if (n_out == 0) return hipSuccess;
-  const size_t lds = (size_t)SEL_CAP * 8;
-  hipError_t e = hipFuncSetAttribute((const void*)k_raw_sel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+// k_max: the largest group of the batch.  LDS is sized to it (not to SEL_CAP) so that groups
+// of a few thousand spans keep several blocks per CU.
+hipError_t launch_raw_sel(const RawParams& p, int64_t k_max, hipStream_t s) {
+  if (p.n_strips == 0) return hipSuccess;
+  const size_t lds = (size_t)std::max<int64_t>(1, std::min<int64_t>(k_max, SEL_CAP)) * 8;
+  hipError_t e = hipFuncSetAttribute((const void*)k_raw_sel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SEL_CAP * 8);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_raw_sel, dim3((unsigned)n_out), dim3(256), lds, s, p, n_out);
+  hipLaunchKernelGGL(k_raw_sel, dim3((unsigned)(p.n_strips * RAW_STRIP)), dim3(256), lds, s, p);
   return hipGetLastError();
 }
 

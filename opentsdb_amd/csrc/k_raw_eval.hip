@@ -327,13 +327,15 @@ hipError_t launch_raw_eval_inst<GA_ID>(const RawParams& p, hipStream_t s) {
 // Median collect the span values of each union point, src/core/Aggregators.java:397-431,
 // :657-708): the traversal of k_raw_eval, but each span's operand (exact or interpolated,
 // long and/or double as nextLongValue / nextDoubleValue produce it) is stored at
-// vals_off[gi] + i * U + u instead of being folded; k_raw_sel (k_pct.hip) selects.
+// vals_off[strip] + i * RAW_STRIP + (u - ua) instead of being folded; k_raw_sel (k_pct.hip)
+// selects.
 template <bool DL, bool DD, bool RATE>
 __global__ __launch_bounds__(64) void k_raw_vals(RawParams p) {
   __shared__ uint64_t wmask[RAW_W];
   const int lane = lane_id();
   const int64_t strip = blockIdx.x;
   if (strip >= p.n_strips) return;
+  // blockIdx.y: a run of RAW_SEL_SPANS spans of the strip (the spans are independent here)
   const int64_t gi = p.strip_g[strip];
   const int64_t t = p.strip_t[strip];
   const int64_t g = gi + p.g0;
@@ -343,12 +345,15 @@ __global__ __launch_bounds__(64) void k_raw_vals(RawParams p) {
   const int64_t ub = min(U, ua + (int64_t)RAW_STRIP);
   const int64_t sb = p.grp_ser[g];
   const int k = (int)(p.grp_ser[g + 1] - sb);
+  const int i0 = (int)blockIdx.y * RAW_SEL_SPANS;
+  if (i0 >= k) return;
+  const int i1 = min(k, i0 + RAW_SEL_SPANS);
   constexpr int first = RATE ? 1 : 0;
   const int interp = p.interp;
   const int32_t* crow = p.cur + p.cur_off[gi] + t * k;
   const int32_t* cnext = (t + 1 < ns) ? crow + k : nullptr;
   const int64_t obase = p.out_off[gi];
-  const int64_t vbase = p.vals_off[gi];
+  const int64_t vbase = p.vals_off[strip];
   const uint64_t below = (lane == 63) ? ~0ULL : ((2ULL << lane) - 1ULL);
 
   int64_t x[RAW_W];
@@ -362,16 +367,16 @@ __global__ __launch_bounds__(64) void k_raw_vals(RawParams p) {
   }
   auto put_l = [&](int i, int w, int64_t v) {
     if (!in[w]) return;
-    const int64_t o = vbase + (int64_t)i * U + ua + 64 * w + lane;
+    const int64_t o = vbase + (int64_t)i * RAW_STRIP + 64 * w + lane;
     p.vals_l[o] = v;
     p.vals_p[o] = 1;
   };
   auto put_d = [&](int i, int w, double v) {
     if (!in[w]) return;
-    p.vals_d[vbase + (int64_t)i * U + ua + 64 * w + lane] = v;
+    p.vals_d[vbase + (int64_t)i * RAW_STRIP + 64 * w + lane] = v;
   };
 
-  for (int i = 0; i < k; i++) {
+  for (int i = i0; i < i1; i++) {
     const int64_t s = sb + i;
     const int n = p.sp_n[s];
     if (n < (RATE ? 2 : 1)) continue;
@@ -449,13 +454,14 @@ __global__ __launch_bounds__(64) void k_raw_vals(RawParams p) {
   for (int w = 0; w < RAW_W; w++) {
     const int64_t u = ua + 64 * w + lane;
     if (u >= ub) continue;
-    p.out_int[obase + u] = (!RATE && !((flt >> w) & 1)) ? 1 : 0;
+    // out_int starts at 1; any run of spans that sees a double at the point clears it
+    if (RATE || ((flt >> w) & 1)) p.out_int[obase + u] = 0;
   }
 }
 
-hipError_t launch_raw_vals(const RawParams& p, hipStream_t s) {
+hipError_t launch_raw_vals(const RawParams& p, int64_t k_max, hipStream_t s) {
   if (p.n_strips == 0) return hipSuccess;
-  const dim3 grid((unsigned)p.n_strips), block(64);
+  const dim3 grid((unsigned)p.n_strips, (unsigned)((k_max + RAW_SEL_SPANS - 1) / RAW_SEL_SPANS)), block(64);
   if (p.rate) hipLaunchKernelGGL((k_raw_vals<false, true, true>), grid, block, 0, s, p);
   else if (p.do_long && p.do_double) hipLaunchKernelGGL((k_raw_vals<true, true, false>), grid, block, 0, s, p);
   else if (p.do_long) hipLaunchKernelGGL((k_raw_vals<true, false, false>), grid, block, 0, s, p);

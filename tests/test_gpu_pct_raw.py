@@ -104,3 +104,14 @@ def test_raw_pct_group_beyond_lds_not_implemented(eng):
     with pytest.raises(Exception) as ei:
         eng.run(q)
     assert "notimplemented" in str(ei.value).lower().replace(" ", "")
+
+
+@pytest.mark.parametrize("ops", ["1", "70000"])
+def test_raw_pct_strip_batches(eng, ops, monkeypatch):
+    """Operands are staged per strip (RAW_STRIP points x the group's spans) in batches of at
+    most TSDBHIP_SELOPS operands: one strip per batch, and several strips per batch."""
+    monkeypatch.setenv("TSDBHIP_SELOPS", ops)
+    b = random_batch(7, n_series=60, n_groups=2, span_h=3)
+    for agg in ["p95", "ep50r3", "median"]:
+        q = abi.new_query(T0, T0 + 3 * 3600 - 1, agg)
+        exact(eng.run_batch(b, q), O.run_query(b, q), agg, f"ops {ops} {agg}")

@@ -170,6 +170,7 @@ def main():
     load_s = time.perf_counter() - t
     queries = {
         "sum (raw union LERP)": abi.new_query(T0, T0 + 3599, "sum"),
+        "p99 (raw union LERP, per-point selection)": abi.new_query(T0, T0 + 3599, "p99"),
         "sum:rate{counter,4294967296,1000000}": abi.new_query(T0, T0 + 3599, "sum", rate=True, counter=True,
                                                               counter_max=1 << 32, reset_value=1000000),
     }
