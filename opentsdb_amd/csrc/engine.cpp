@@ -1813,10 +1813,6 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
       // (RAW_STRIP points x the group's spans each), in batches of at most kSelOps operands
       int64_t kSelOps = (int64_t)1 << 28;
       if (const char* e = std::getenv("TSDBHIP_SELOPS")) kSelOps = std::max<int64_t>(1, std::atoll(e));   // tests: force batches
-      for (int64_t i = 0; i < ng; i++)
-        if (grp_ser[g0 + i + 1] - grp_ser[g0 + i] > SEL_CAP)
-          return fail(TSDB_E_NOT_IMPLEMENTED, "percentile / median group-by without downsampling over a group of more than " +
-                                                  std::to_string(SEL_CAP) + " spans");
       std::vector<int64_t> soff(ns + 1, 0);
       for (int64_t t = 0; t < ns; t++) soff[t + 1] = soff[t] + (grp_ser[g0 + sg[t] + 1] - grp_ser[g0 + sg[t]]) * RAW_STRIP;
       // batches [bat[i], bat[i + 1]) of strips: at least one strip each, else <= kSelOps operands

@@ -1032,53 +1032,174 @@ __device__ __forceinline__ int64_t sel_d2l(double d) {   // Java (long) of a dou
   return (int64_t)d;
 }
 
-// One block per union point of the batch's strips: block b -> strip b / RAW_STRIP, point j.
-__global__ __launch_bounds__(256) void k_raw_sel(RawParams p) {
+// One WAVE per union point of the batch's strips (4 waves a block, no block barriers):
+// point pt -> strip pt / RAW_STRIP, position j.  Wave-local radix select: 8-bit digits, a
+// 256-bin LDS histogram per wave, the digit holding rank r found by a wave prefix sum over
+// the lanes' 4 bins; once <= 64 keys share the prefix they are ranked directly.
+constexpr int SELW = 4;
+constexpr int RAW_SEL_LDS = 4096;   // keys per wave staged in LDS (4 x 32 KB a block)
+struct SelWave {
+  uint32_t hist[256];
+  uint64_t cand[64];
+  uint32_t n;
+};
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint64_t o = shfl_u64(v, lane_id() ^ d);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ int wave_sum_int(int v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+// Key of rank r (0-based ascending) among keys[0..n); called by all 64 lanes of the wave.
+__device__ uint64_t wave_radix_select(const uint64_t* keys, int64_t ks, int n, int r, SelWave& W) {
+  const int lane = lane_id();
+  // skip the leading digits every key shares (counters, clustered values): they would put
+  // all n keys into one histogram bin, pass after pass
+  uint64_t kand = ~0ULL, kor = 0;
+  for (int j = lane; j < n; j += 64) {
+    const uint64_t k = keys[j * ks];
+    kand &= k;
+    kor |= k;
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    kand &= shfl_u64(kand, lane ^ d);
+    kor |= shfl_u64(kor, lane ^ d);
+  }
+  const uint64_t diff = kand ^ kor;
+  if (diff == 0) return kand;   // all keys equal
+  const int top = (63 - __clzll((long long)diff)) & ~7;   // lowest bit of the first differing digit
+  uint64_t mask = top == 56 ? 0 : ~((1ULL << (top + 8)) - 1ULL);
+  uint64_t prefix = kand & mask;
+  for (int shift = top; shift >= 0; shift -= 8) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) W.hist[lane * 4 + q] = 0;
+    WAVE_SYNC();
+    for (int j = lane; j < n; j += 64) {
+      const uint64_t k = keys[j * ks];
+      if ((k & mask) == prefix) atomicAdd(&W.hist[(k >> shift) & 255], 1u);
+    }
+    WAVE_SYNC();
+    uint32_t c[4], t = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) { c[q] = W.hist[lane * 4 + q]; t += c[q]; }
+    const int incl = wave_incl_sum((int)t);
+    int ex = incl - (int)t;
+    const bool found = ex <= r && r < incl;
+    int bin = 0, rr = 0, nc = 0;
+    if (found) {
+      int q = 0;
+      for (; q < 3; q++) {
+        if (r < ex + (int)c[q]) break;
+        ex += (int)c[q];
+      }
+      bin = lane * 4 + q;
+      rr = r - ex;
+      nc = (int)c[q];
+    }
+    const int src = __ffsll((long long)__ballot(found)) - 1;
+    bin = __shfl(bin, src, 64);
+    rr = __shfl(rr, src, 64);
+    nc = __shfl(nc, src, 64);
+    prefix |= (uint64_t)bin << shift;
+    mask |= 255ULL << shift;
+    r = rr;
+    WAVE_SYNC();
+    if (shift == 0) break;
+    if (nc <= 64) {
+      if (lane == 0) W.n = 0;
+      WAVE_SYNC();
+      for (int j = lane; j < n; j += 64) {
+        const uint64_t k = keys[j * ks];
+        if ((k & mask) == prefix) W.cand[atomicAdd(&W.n, 1u)] = k;
+      }
+      WAVE_SYNC();
+      const uint64_t x = lane < nc ? W.cand[lane] : ~0ULL;
+      int less = 0, eq = 0;
+      for (int q = 0; q < nc; q++) {
+        const uint64_t y = W.cand[q];
+        less += y < x;
+        eq += y == x;
+      }
+      const bool hit = lane < nc && less <= r && r < less + eq;
+      const uint64_t res = shfl_u64(x, __ffsll((long long)__ballot(hit)) - 1);
+      WAVE_SYNC();
+      return res;
+    }
+  }
+  return prefix;
+}
+
+__global__ __launch_bounds__(256) void k_raw_sel(RawParams p, int32_t kcap) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ SelShared S;
-  __shared__ unsigned long long red[2];
-  const int64_t sl = blockIdx.x / RAW_STRIP;
-  const int64_t j = blockIdx.x - sl * RAW_STRIP;
-  if (sl >= p.n_strips) return;
-  const int tid = threadIdx.x;
+  __shared__ SelWave WS[SELW];
+  const int wv = threadIdx.x >> 6;
+  const int lane = lane_id();
+  const int64_t pt = (int64_t)blockIdx.x * SELW + wv;
+  const int64_t sl = pt / RAW_STRIP;
+  const int64_t j = pt - sl * RAW_STRIP;
+  if (sl >= p.n_strips) return;   // whole waves leave; no block barrier follows
   const int64_t gi = p.strip_g[sl];
   const int64_t u = (int64_t)p.strip_t[sl] * RAW_STRIP + j;
   if (u >= p.U[gi]) return;
   const int64_t idx = p.out_off[gi] + u;
   const int64_t g = gi + p.g0;
-  const int64_t k = p.grp_ser[g + 1] - p.grp_ser[g];
+  const int k = (int)(p.grp_ser[g + 1] - p.grp_ser[g]);
   const int64_t vb = p.vals_off[sl] + j;
-  constexpr int64_t U = RAW_STRIP;   // operand stride between spans
+  constexpr int64_t US = RAW_STRIP;   // operand stride between spans
   const bool is_int = p.out_int[idx] != 0;
-  uint64_t* keys = reinterpret_cast<uint64_t*>(smem);
-  if (tid == 0) { red[0] = 0; red[1] = 0; }
-  __syncthreads();
-  int64_t m = 0;
+  SelWave& W = WS[wv];
+  // keys in LDS, or (groups beyond kcap) in place over the strided operands themselves
+  const bool in_lds = k <= kcap;
+  const int64_t ks = in_lds ? 1 : US;
+  uint64_t* keys = in_lds ? reinterpret_cast<uint64_t*>(smem) + (int64_t)wv * kcap
+                          : reinterpret_cast<uint64_t*>(is_int ? (void*)p.vals_l : (void*)p.vals_d) + vb;
+  const uint64_t below = (1ULL << lane) - 1ULL;   // lanes < lane
+  int m = 0;
   if (is_int) {
     // present long operands, compacted (their order does not matter to a selection)
-    for (int64_t i = tid; i < k; i += blockDim.x) {
-      if (p.vals_p[vb + i * U]) {
-        const uint64_t key = (uint64_t)p.vals_l[vb + i * U] ^ 0x8000000000000000ULL;
-        keys[atomicAdd(&red[0], 1ULL)] = key;
-      }
+    for (int base = 0; base < k; base += 64) {
+      const int i = base + lane;
+      const bool pres = i < k && p.vals_p[vb + i * US];
+      const uint64_t bal = (uint64_t)__ballot(pres);
+      const uint64_t key = pres ? (uint64_t)p.vals_l[vb + i * US] ^ 0x8000000000000000ULL : 0;
+      WAVE_SYNC();   // in place: every lane has read its operand before any is overwritten
+      if (pres) keys[(m + __popcll(bal & below)) * ks] = key;
+      m += __popcll(bal);
     }
-    __syncthreads();
-    m = (int64_t)red[0];
   } else {
-    uint32_t nan_local = 0;
-    for (int64_t i = tid; i < k; i += blockDim.x) {
-      const double x = p.vals_d[vb + i * U];
-      nan_local += isnan(x) ? 1u : 0u;
-      keys[i] = f2key(canon_nan(x));
+    int nan = 0;
+    for (int base = 0; base < k; base += 64) {
+      const int i = base + lane;
+      bool isn = false;
+      if (i < k) {
+        const double x = p.vals_d[vb + i * US];
+        isn = isnan(x);
+        keys[i * ks] = f2key(canon_nan(x));
+      }
+      nan += __popcll((uint64_t)__ballot(isn));
     }
-    if (nan_local) atomicAdd(&red[0], (unsigned long long)nan_local);
-    __syncthreads();
-    m = k - (int64_t)red[0];
+    m = k - nan;
   }
-  const int64_t n = is_int ? m : k;   // keys staged
+  WAVE_SYNC();
+  const int n = is_int ? m : k;   // keys staged
   const int fn = p.sel_fn;
-  // ranks r0 (and r1 = r0 + 1 when interpolating) and the weight of the estimate
-  int64_t r0 = 0, r1 = -1;
+  int r0 = 0, r1 = -1;
   double dif = 0.0;
   const int est = fn == TSDB_AGG_MEDIAN ? 0 : (is_int ? (fn - TSDB_AGG_P999) / 6 : 0);   // runDouble: LEGACY
   if (m > 1 && fn != TSDB_AGG_MEDIAN) {
@@ -1094,31 +1215,29 @@ __global__ __launch_bounds__(256) void k_raw_sel(RawParams p) {
     const double fpos = floor(pos);
     if (pos < 1) r0 = 0;
     else if (pos >= (double)m) r0 = m - 1;
-    else { r0 = (int64_t)fpos - 1; r1 = r0 + 1; dif = pos - fpos; }
+    else { r0 = (int)fpos - 1; r1 = r0 + 1; dif = pos - fpos; }
   } else if (m > 0 && fn == TSDB_AGG_MEDIAN) {
     r0 = m / 2;
   }
   uint64_t k0 = 0, k1 = 0;
   if (m > 0) {
-    k0 = radix_select(keys, n, r0, S);
+    k0 = wave_radix_select(keys, ks, n, r0, W);
     k1 = k0;
     if (r1 >= 0) {
-      if (tid == 0) { red[0] = 0; red[1] = ~0ULL; }
-      __syncthreads();
-      uint32_t le = 0;
+      // rank r0 + 1: the same key when more than r0 + 1 keys are <= k0, else the next larger key
+      int le = 0;
       uint64_t gt = ~0ULL;
-      for (int64_t j = tid; j < n; j += blockDim.x) {
-        const uint64_t kk = keys[j];
+      for (int jj = lane; jj < n; jj += 64) {
+        const uint64_t kk = keys[jj * ks];
         if (kk <= k0) le++;
         else gt = kk < gt ? kk : gt;
       }
-      atomicAdd(&red[0], (unsigned long long)le);
-      atomicMin(&red[1], (unsigned long long)gt);
-      __syncthreads();
-      k1 = (int64_t)red[0] > r1 ? k0 : red[1];
+      le = wave_sum_int(le);
+      gt = wave_min_u64(gt);
+      k1 = le > r1 ? k0 : gt;
     }
   }
-  if (tid != 0) return;
+  if (lane != 0) return;
   uint64_t bits;
   if (is_int) {
     const int64_t l0 = (int64_t)(k0 ^ 0x8000000000000000ULL), l1 = (int64_t)(k1 ^ 0x8000000000000000ULL);
@@ -1149,14 +1268,15 @@ __global__ __launch_bounds__(256) void k_raw_sel(RawParams p) {
   p.out_bits[idx] = bits;
 }
 
-// k_max: the largest group of the batch.  LDS is sized to it (not to SEL_CAP) so that groups
-// of a few thousand spans keep several blocks per CU.
+// k_max: the largest group of the batch; each wave stages k_max keys in LDS.
 hipError_t launch_raw_sel(const RawParams& p, int64_t k_max, hipStream_t s) {
   if (p.n_strips == 0) return hipSuccess;
-  const size_t lds = (size_t)std::max<int64_t>(1, std::min<int64_t>(k_max, SEL_CAP)) * 8;
-  hipError_t e = hipFuncSetAttribute((const void*)k_raw_sel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SEL_CAP * 8);
+  const int32_t kcap = (int32_t)std::max<int64_t>(1, std::min<int64_t>(k_max, RAW_SEL_LDS));
+  const size_t lds = (size_t)kcap * 8 * SELW;
+  hipError_t e = hipFuncSetAttribute((const void*)k_raw_sel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)((size_t)RAW_SEL_LDS * 8 * SELW));
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_raw_sel, dim3((unsigned)(p.n_strips * RAW_STRIP)), dim3(256), lds, s, p);
+  const int64_t pts = p.n_strips * RAW_STRIP;
+  hipLaunchKernelGGL(k_raw_sel, dim3((unsigned)((pts + SELW - 1) / SELW)), dim3(64 * SELW), lds, s, p, kcap);
   return hipGetLastError();
 }
 

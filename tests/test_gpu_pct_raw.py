@@ -97,13 +97,15 @@ def test_raw_pct_nan_members(eng):
         exact(eng.run_batch(b, q), O.run_query(b, q), agg, agg)
 
 
-def test_raw_pct_group_beyond_lds_not_implemented(eng):
-    """A group of more than SEL_CAP = 12288 spans does not fit the LDS stage of k_raw_sel."""
-    eng.synth(12300, T0, 4, 10000, 1, 1, 1000, 0x5EED)
-    q = abi.new_query(T0, T0 + 3599, "p99")
-    with pytest.raises(Exception) as ei:
-        eng.run(q)
-    assert "notimplemented" in str(ei.value).lower().replace(" ", "")
+@pytest.mark.parametrize("kind", [1, 2])
+def test_raw_pct_group_beyond_lds(eng, kind):
+    """A group of 5000 spans exceeds the per-wave LDS stage of k_raw_sel (4096 keys): the keys
+    are built in place over the strided operands (int: compacted present longs; float: all)."""
+    eng.synth(5000, T0, 6, 10000, kind, 1, 1000, 0x5EED)
+    b = eng.download()
+    for agg in ["p99", "ep50r3", "median"]:
+        q = abi.new_query(T0, T0 + 3599, agg)
+        exact(eng.run(q), O.run_query(b, q), agg, f"kind {kind} {agg}")
 
 
 @pytest.mark.parametrize("ops", ["1", "70000"])
