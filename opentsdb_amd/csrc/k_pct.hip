@@ -800,8 +800,25 @@ struct SelShared {
 };
 __device__ uint64_t radix_select(const uint64_t* keys, int64_t n, int64_t r, SelShared& S) {
   const int tid = threadIdx.x;
-  uint64_t prefix = 0, mask = 0;
-  for (int shift = 56; shift >= 0; shift -= 8) {
+  // the leading digits all keys share are skipped (clustered values would otherwise put every
+  // key into one bin, pass after pass): block AND / OR of the keys
+  uint64_t kand = ~0ULL, kor = 0;
+  for (int64_t j = tid; j < n; j += blockDim.x) {
+    kand &= keys[j];
+    kor |= keys[j];
+  }
+  if (tid == 0) { S.bin = ~0ULL; S.rr = 0; }
+  __syncthreads();
+  atomicAnd(reinterpret_cast<unsigned long long*>(&S.bin), (unsigned long long)kand);
+  atomicOr(reinterpret_cast<unsigned long long*>(&S.rr), (unsigned long long)kor);
+  __syncthreads();
+  const uint64_t band = S.bin, bor = S.rr;
+  __syncthreads();
+  if ((band ^ bor) == 0) return band;   // all keys equal
+  const int top = (63 - __clzll((long long)(band ^ bor))) & ~7;
+  uint64_t mask = top == 56 ? 0 : ~((1ULL << (top + 8)) - 1ULL);
+  uint64_t prefix = band & mask;
+  for (int shift = top; shift >= 0; shift -= 8) {
     for (int b = tid; b < 256; b += blockDim.x) S.hist[b] = 0;
     __syncthreads();
     for (int64_t j = tid; j < n; j += blockDim.x) {
