@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define TSDBHIP_ABI_VERSION 3
+#define TSDBHIP_ABI_VERSION 4
 
 /* ---- error codes: one per Java exception on the path --------------------- */
 enum {
@@ -111,10 +111,11 @@ typedef struct {
 /* Calendar units of a 'c' downsampling interval (DateTime.unitsToCalendarType,
  * src/utils/DateTime.java:616-640); the interval count is ds_interval_ms / the unit's
  * parseDuration length (ms 1, s 1e3, m 6e4, h 3.6e6, d 8.64e7, w 6.048e8, n 30 d, y 365 d).
- * The engine aligns on the UTC calendar (the DownsamplingSpecification default timezone);
- * it runs the units whose grid is one global sequence -- ms (1000 % n == 0), s / m
- * (60 % n == 0), h (24 % n == 0), d (n == 1), w (n == 1, weeks from Sunday) -- and returns
- * TSDB_E_NOT_IMPLEMENTED for months, years and intervals anchored per span. */
+ * The engine aligns on the UTC calendar (the DownsamplingSpecification default timezone).
+ * It runs the units whose grid is one global sequence -- ms (1000 % n == 0), s / m
+ * (60 % n == 0), h (24 % n == 0), d (n == 1), w (n == 1, weeks from Sunday) -- and n months
+ * (12 % n == 0) and 1 year through a per-query slot boundary table; intervals anchored per
+ * span (7sc, 2dc, 5nc, 2wc, 2yc) return TSDB_E_NOT_IMPLEMENTED. */
 enum {
   TSDB_CAL_NONE = 0, TSDB_CAL_MS, TSDB_CAL_S, TSDB_CAL_M, TSDB_CAL_H, TSDB_CAL_D, TSDB_CAL_W, TSDB_CAL_N, TSDB_CAL_Y
 };
@@ -143,6 +144,8 @@ typedef struct {
   int64_t tiles;                 /* series tiles of the query */
   int64_t redo_tiles;            /* tiles the streaming kernel handed to the general kernel */
   double fast_ms;                /* streaming kernel (k_fast) alone; 0 when not used */
+  double index_ms;               /* k_index of the last tsdbhip_load / tsdbhip_synth: row classification,
+                                    validation, certificate stats (+ the int16 value copy of vle rows) */
 } tsdbhip_timing;
 
 /* ---- library-level helpers (host logic of the reference, restated) ------- */
@@ -306,6 +309,11 @@ int tsdbhip_rollup_download(tsdbhip_ctx* ctx, int32_t* series, uint32_t* base_ti
 
 /* Device synchronisation helper for host code that does not use HIP directly. */
 int tsdbhip_sync(tsdbhip_ctx* ctx);
+
+/* Test hook (no reference counterpart): the per-row facts k_index derived for the resident
+ * batch, rows in resident order -- datapoints, RowDesc flags, exactness-certificate lsb and
+ * max |value|.  Any pointer may be null. */
+int tsdbhip_debug_rows(tsdbhip_ctx* ctx, uint32_t* ndp, uint32_t* flags, int32_t* lsb, double* absmax);
 
 #ifdef __cplusplus
 }

@@ -128,6 +128,7 @@ class Timing(C.Structure):
         ("tiles", C.c_int64),
         ("redo_tiles", C.c_int64),
         ("fast_ms", C.c_double),
+        ("index_ms", C.c_double),
     ]
 
 

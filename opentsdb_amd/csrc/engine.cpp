@@ -222,6 +222,9 @@ struct tsdbhip_ctx {
   DevBuf pa, pb, pn, pf, out_val, out_flag, gact, err, g_dense, g_pres, g_rate, redo, redo_n, redo2, redo2_n;
   DevBuf xbuf, gbuf;
   DevBuf pre_dense, pre_pres;          // percentile / median downsampling
+  DevBuf big_scratch;                  // k_pct large buckets: per-wave overflow regions
+  bool mdp_valid = false;              // series_max_dp() cache (invalidated by every load)
+  int64_t mdp_ss = 0, mdp_se = 0, mdp = 0;
   DevBuf sel_vals, sel_sorted, sel_uni, sel_gsp;   // percentile / median group-by
   DevBuf cal_bounds;                                // calendar month / year slot boundaries
   // raw path scratch
@@ -241,6 +244,7 @@ struct tsdbhip_ctx {
   const int32_t* redo_final = nullptr;   // device counter of the tiles k_fast handed to k_grid
   int64_t redo_other = 0;                // + tiles of neither row class (k_grid only)
   tsdbhip_timing timing{};
+  double index_ms = 0;                   // k_index (+ val2 pass) of the last load
   // account() cache (invalidated by every load)
   bool acct_valid = false;
   int64_t acct_ss = 0, acct_se = 0, acct_dps = 0, acct_bytes = 0;
@@ -397,6 +401,7 @@ static void release_batch(tsdbhip_ctx* c) {
     b->release();
   c->none_tiles_ready = false;
   c->acct_valid = false;
+  c->mdp_valid = false;
   c->n_series = c->n_rows = c->n_groups = 0;
 }
 
@@ -409,7 +414,8 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
                     &c->g_pres, &c->g_rate, &c->redo, &c->redo_n, &c->redo2, &c->redo2_n, &c->d_tl, &c->d_tl_n, &c->r1a, &c->r1b, &c->r2, &c->r_n, &c->xbuf, &c->gbuf, &c->r_rowpt,
                     &c->r_spoff, &c->r_spn, &c->r_grp, &c->r_pts, &c->r_rank, &c->r_bm, &c->r_wb, &c->r_U, &c->r_ooff,
                     &c->r_sg, &c->r_su, &c->r_ots, &c->r_obits, &c->r_oint, &c->r_coff, &c->r_cur, &c->r_voff, &c->r_vl, &c->r_vd, &c->r_vp, &c->pre_dense, &c->pre_pres,
-                    &c->ro_allint, &c->ro_ord, &c->ro_orig, &c->ro_cnt, &c->ro_vsz, &c->ro_coff, &c->ro_voff})
+                    &c->ro_allint, &c->ro_ord, &c->ro_orig, &c->ro_cnt, &c->ro_vsz, &c->ro_coff, &c->ro_voff,
+                    &c->big_scratch})
     b->release();
   for (auto& o : c->ro_out)
     for (DevBuf* b : {&o.series, &o.base, &o.qual, &o.voff, &o.val}) b->release();
@@ -524,12 +530,17 @@ static int build_none_tiles(tsdbhip_ctx* c) {
 static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
   // classify rows on the device, then fetch ndp for host-side accounting
   HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
+  const char* genv = std::getenv("TSDBHIP_INDEX_GENERIC");   // test hook: sequential per-datapoint path
+  HIP_OK(hipEventRecord(c->ev[0], c->stream));
   HIP_OK(launch_index(c->qual.as<uint8_t>(), c->val.as<uint8_t>(), nullptr, c->rows.as<RowDesc>(), c->n_rows,
-                      c->err.as<int32_t>(), c->stream));
+                      c->err.as<int32_t>(), c->stream, genv && genv[0] == '1'));
+  HIP_OK(hipEventRecord(c->ev[1], c->stream));
   std::vector<RowDesc> back(c->n_rows);
   if (c->n_rows)
     HIP_OK(hipMemcpyAsync(back.data(), c->rows.p, c->n_rows * sizeof(RowDesc), hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
+  float t_index = 0, t_val2 = 0;
+  (void)hipEventElapsedTime(&t_index, c->ev[0], c->ev[1]);
   // rows of the vle-integer class (2-byte qualifiers, 1-2-byte integers): a second pass
   // writes their values as int16 at the qualifier offsets (val2), the layout k_short /
   // k_fast read -- allocated only when such rows exist
@@ -539,10 +550,14 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
   c->val2.release();
   if (need_val2) {
     HIP_OK(c->val2.ensure(c->qual_bytes + BLOB_SLACK));
+    HIP_OK(hipEventRecord(c->ev[2], c->stream));
     HIP_OK(launch_index(c->qual.as<uint8_t>(), c->val.as<uint8_t>(), c->val2.as<uint8_t>(), c->rows.as<RowDesc>(),
-                        c->n_rows, c->err.as<int32_t>(), c->stream));
+                        c->n_rows, c->err.as<int32_t>(), c->stream, genv && genv[0] == '1'));
+    HIP_OK(hipEventRecord(c->ev[3], c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
+    (void)hipEventElapsedTime(&t_val2, c->ev[2], c->ev[3]);
   }
+  c->index_ms = (double)t_index + t_val2;
   (void)rd;
   c->h_ndp.resize(c->n_rows);
   c->h_base.resize(c->n_rows);
@@ -936,6 +951,22 @@ extern "C" int tsdbhip_batch_download(tsdbhip_ctx* c, int64_t* series_row_ptr, u
   return 0;
 }
 
+// Test hook: the per-row facts k_index derived (RowDesc.ndp / flags / lsb / absmax).
+extern "C" int tsdbhip_debug_rows(tsdbhip_ctx* c, uint32_t* ndp, uint32_t* flags, int32_t* lsb, double* absmax) {
+  if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  std::vector<RowDesc> rd(c->n_rows);
+  if (c->n_rows) HIP_OK(hipMemcpy(rd.data(), c->rows.p, c->n_rows * sizeof(RowDesc), hipMemcpyDeviceToHost));
+  for (int64_t r = 0; r < c->n_rows; r++) {
+    if (ndp) ndp[r] = rd[r].ndp;
+    if (flags) flags[r] = rd[r].flags;
+    if (lsb) lsb[r] = rd[r].lsb;
+    if (absmax) absmax[r] = rd[r].absmax;
+  }
+  return 0;
+}
+
 // ===========================================================================
 // query execution
 // ===========================================================================
@@ -1082,6 +1113,24 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
   return 0;
 }
 
+// Largest number of datapoints one series holds in rows with base in [ss, se) (cached per
+// scan range; the batch is resident).
+int64_t series_max_dp(tsdbhip_ctx* c, int64_t ss, int64_t se) {
+  if (c->mdp_valid && c->mdp_ss == ss && c->mdp_se == se) return c->mdp;
+  int64_t m = 0;
+  for (int64_t s = 0; s < c->n_series; s++) {
+    int64_t n = 0;
+    for (int64_t r = c->h_srp[s]; r < c->h_srp[s + 1]; r++)
+      if ((int64_t)c->h_base[r] >= ss && (int64_t)c->h_base[r] < se) n += c->h_ndp[r];
+    m = std::max(m, n);
+  }
+  c->mdp_valid = true;
+  c->mdp_ss = ss;
+  c->mdp_se = se;
+  c->mdp = m;
+  return m;
+}
+
 int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bool do_reduce) {
   const bool none = P.none;
   if (none) { int rc = build_none_tiles(c); if (rc) return rc; }
@@ -1206,10 +1255,21 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     } else {
       HIP_OK(launch_pct(gp, 0, c->n_series, c->stream));
     }
-    int32_t nbig = 0;   // series with a bucket of more than 512 values: the LDS-sort pass
+    int32_t nbig = 0;   // series with a bucket of more than 512 values: the large-bucket pass
     HIP_OK(hipMemcpyAsync(&nbig, c->redo_n.p, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
-    HIP_OK(launch_pct(gp, 2, nbig, c->stream));
+    if (nbig > 0) {
+      // persistent waves, each with an overflow region as large as the largest series' in-range
+      // datapoints (buckets above PCT_CAP values); at most ~2 GB of regions
+      const int64_t cap = std::max<int64_t>(PCT_CAP + 1, series_max_dp(c, P.ss, P.se));
+      int64_t nw = std::min<int64_t>({(int64_t)nbig, 4096, std::max<int64_t>(2, ((int64_t)2 << 30) / (cap * 8))});
+      nw = (nw + 1) & ~(int64_t)1;
+      HIP_OK(c->big_scratch.ensure(nw * cap * 8));
+      gp.big_scratch = c->big_scratch.as<double>();
+      gp.big_cap = cap;
+      gp.n_launch = nw;
+      HIP_OK(launch_pct(gp, 2, nw, c->stream));
+    }
     }
     if (!P.gsel && !P.ordered && !P.values_only)
       HIP_OK(launch_emit(gp, c->stream));   // else the caller takes the bucket values
@@ -2059,6 +2119,7 @@ extern "C" void tsdbhip_result_free(tsdbhip_result* r) { std::free(r); }
 extern "C" int tsdbhip_last_timing(tsdbhip_ctx* c, tsdbhip_timing* out) {
   if (!c || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   *out = c->timing;
+  out->index_ms = c->index_ms;
   return 0;
 }
 

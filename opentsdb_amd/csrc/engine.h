@@ -132,6 +132,10 @@ struct GridParams {
   // ([series][K], before rate and fill) instead of its SpanGroup contributions
   double* dense_out;
   uint8_t* pres_out;
+  // k_pct BIG pass: each of the n_launch waves owns big_cap values of big_scratch for buckets
+  // of more than PCT_CAP values (big_cap >= the largest series' in-range datapoints)
+  double* big_scratch;
+  int64_t big_cap;
   int32_t dbg;           // k_short profiling switches (TSDBHIP_DBG, results invalid): 1 skip series end,
                          // 2 skip chunk fold, 8 consume loads, 16 stop after the descriptors, 32 load row 0 only
 };
@@ -294,8 +298,9 @@ hipError_t rollup_scan(const uint32_t* cnt, int64_t* coff, const uint32_t* vsz, 
                        void** tmp, size_t* tmp_bytes, hipStream_t s);
 
 // launchers (kernels.hip)
+// generic: every row through the sequential per-datapoint path (test hook)
 hipError_t launch_index(const uint8_t* qual, const uint8_t* val, uint8_t* val2, RowDesc* rows, int64_t n_rows, int32_t* err,
-                        hipStream_t s);
+                        hipStream_t s, bool generic = false);
 hipError_t launch_grid(const GridParams& p, int ds_function_class, hipStream_t s);
 // k_fast: uniform float rows of one (qualifier width, value length) class; returns
 // hipErrorNotSupported when no specialisation exists for (f, qw, vl)
@@ -304,9 +309,9 @@ hipError_t launch_fast(const GridParams& p, int ds_function_class, int qw, int v
 int64_t fast_wave_lds(int64_t K, bool rate);
 hipError_t launch_reduce(const ReduceParams& p, hipStream_t s);
 // percentile / median downsampling (k_pct.hip): bucket order statistics, then group-by
-static constexpr int PCT_CAP = 4096;   // values per bucket sorted in LDS
-// pass 0: every series; 1: the series k_pct_rows handed back (tile_list); 2: the LDS-sort
-// pass over redo_list
+static constexpr int PCT_CAP = 4096;   // values per bucket sorted in LDS; larger buckets are radix-selected
+// pass 0: every series; 1: the series k_pct_rows handed back (tile_list); 2: the large-bucket
+// pass over redo_list (n = waves launched = p.n_launch)
 hipError_t launch_pct(const GridParams& p, int pass, int64_t n, hipStream_t s);
 bool pct_rows_supported(int qw, int vl);
 hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s);

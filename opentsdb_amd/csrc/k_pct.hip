@@ -203,16 +203,184 @@ __device__ __forceinline__ bool select_extreme(int fn, int n, const double* buf,
   return true;
 }
 
-// value of a finished bucket holding n non-NaN values in buf (tot values incl. NaN)
-__device__ __forceinline__ double bucket_value(const GridParams& p, double* buf, int n) {
+// ---- order-preserving keys and the wave-local radix select (k_pct's large buckets,
+//      k_raw_sel) ---------------------------------------------------------------------
+__device__ __forceinline__ double canon_nan(double v) {
+  return isnan(v) ? __longlong_as_double(0x7FF8000000000000LL) : v;   // +NaN: the largest key
+}
+
+__device__ __forceinline__ uint64_t f2key(double x) {   // ascending double order == unsigned key order
+  const uint64_t b = (uint64_t)__double_as_longlong(x);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
+}
+__device__ __forceinline__ double key2f(uint64_t k) {
+  return __longlong_as_double((long long)((k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFULL) : ~k));
+}
+
+constexpr int SELW = 4;
+constexpr int RAW_SEL_LDS = 4096;   // keys per wave staged in LDS (4 x 32 KB a block)
+struct SelWave {
+  uint32_t hist[256];
+  uint64_t cand[64];
+  uint32_t n;
+};
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint64_t o = shfl_u64(v, lane_id() ^ d);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ int wave_sum_int(int v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+// Key of rank r (0-based ascending) among keys[0..n); called by all 64 lanes of the wave.
+__device__ uint64_t wave_radix_select(const uint64_t* keys, int64_t ks, int n, int r, SelWave& W) {
+  const int lane = lane_id();
+  // skip the leading digits every key shares (counters, clustered values): they would put
+  // all n keys into one histogram bin, pass after pass
+  uint64_t kand = ~0ULL, kor = 0;
+  for (int j = lane; j < n; j += 64) {
+    const uint64_t k = keys[j * ks];
+    kand &= k;
+    kor |= k;
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    kand &= shfl_u64(kand, lane ^ d);
+    kor |= shfl_u64(kor, lane ^ d);
+  }
+  const uint64_t diff = kand ^ kor;
+  if (diff == 0) return kand;   // all keys equal
+  const int top = (63 - __clzll((long long)diff)) & ~7;   // lowest bit of the first differing digit
+  uint64_t mask = top == 56 ? 0 : ~((1ULL << (top + 8)) - 1ULL);
+  uint64_t prefix = kand & mask;
+  for (int shift = top; shift >= 0; shift -= 8) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) W.hist[lane * 4 + q] = 0;
+    WAVE_SYNC();
+    for (int j = lane; j < n; j += 64) {
+      const uint64_t k = keys[j * ks];
+      if ((k & mask) == prefix) atomicAdd(&W.hist[(k >> shift) & 255], 1u);
+    }
+    WAVE_SYNC();
+    uint32_t c[4], t = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) { c[q] = W.hist[lane * 4 + q]; t += c[q]; }
+    const int incl = wave_incl_sum((int)t);
+    int ex = incl - (int)t;
+    const bool found = ex <= r && r < incl;
+    int bin = 0, rr = 0, nc = 0;
+    if (found) {
+      int q = 0;
+      for (; q < 3; q++) {
+        if (r < ex + (int)c[q]) break;
+        ex += (int)c[q];
+      }
+      bin = lane * 4 + q;
+      rr = r - ex;
+      nc = (int)c[q];
+    }
+    const int src = __ffsll((long long)__ballot(found)) - 1;
+    bin = __shfl(bin, src, 64);
+    rr = __shfl(rr, src, 64);
+    nc = __shfl(nc, src, 64);
+    prefix |= (uint64_t)bin << shift;
+    mask |= 255ULL << shift;
+    r = rr;
+    WAVE_SYNC();
+    if (shift == 0) break;
+    if (nc <= 64) {
+      if (lane == 0) W.n = 0;
+      WAVE_SYNC();
+      for (int j = lane; j < n; j += 64) {
+        const uint64_t k = keys[j * ks];
+        if ((k & mask) == prefix) W.cand[atomicAdd(&W.n, 1u)] = k;
+      }
+      WAVE_SYNC();
+      const uint64_t x = lane < nc ? W.cand[lane] : ~0ULL;
+      int less = 0, eq = 0;
+      for (int q = 0; q < nc; q++) {
+        const uint64_t y = W.cand[q];
+        less += y < x;
+        eq += y == x;
+      }
+      const bool hit = lane < nc && less <= r && r < less + eq;
+      const uint64_t res = shfl_u64(x, __ffsll((long long)__ballot(hit)) - 1);
+      WAVE_SYNC();
+      return res;
+    }
+  }
+  return prefix;
+}
+
+
+// Ranks select_sorted reads for n sorted values (r1 = -1: one value); Median.runDouble
+// sorted[n / 2], PercentileAgg.runDouble commons-math3 LEGACY pos = p (n + 1).
+__device__ __forceinline__ void sel_ranks(int fn, int64_t n, int64_t& r0, int64_t& r1) {
+  r0 = 0;
+  r1 = -1;
+  if (fn == TSDB_AGG_MEDIAN) { r0 = n / 2; return; }
+  if (n <= 1) return;
+  const double q = pct_quantile(fn) / 100.0;
+  const double pos = (q == 0.0) ? 0.0 : (q == 1.0 ? (double)n : q * (double)(n + 1));
+  if (pos < 1) r0 = 0;
+  else if (pos >= (double)n) r0 = n - 1;
+  else { r0 = (int64_t)floor(pos) - 1; r1 = r0 + 1; }
+}
+
+// Order statistic of n > PCT_CAP values: buf[0 .. PCT_CAP) in LDS, the rest at gbuf[PCT_CAP ..)
+// (the wave's region of the global overflow buffer).  The values become order-preserving
+// keys in gbuf[0 .. n) and the one or two ranks select_sorted reads are radix-selected --
+// no sort and no size limit (the reference collects any number of values, Aggregators.java:657-708).
+__device__ double bucket_value_big(const GridParams& p, const double* buf, int64_t n, double* gbuf, SelWave& SW) {
+  const int lane = lane_id();
+  uint64_t* keys = reinterpret_cast<uint64_t*>(gbuf);
+  for (int e = lane; e < PCT_CAP; e += 64) keys[e] = f2key(buf[e]);
+  for (int64_t e = PCT_CAP + lane; e < n; e += 64) keys[e] = f2key(gbuf[e]);
+  __threadfence_block();
+  WAVE_SYNC();
+  int64_t r0, r1;
+  sel_ranks(p.sel_fn, n, r0, r1);
+  const uint64_t k0 = wave_radix_select(keys, 1, (int)n, (int)r0, SW);
+  uint64_t k1 = k0;
+  if (r1 >= 0) {
+    // rank r0 + 1: the same key when more than r0 + 1 keys are <= k0, else the next larger key
+    int le = 0;
+    uint64_t gt = ~0ULL;
+    for (int64_t j = lane; j < n; j += 64) {
+      const uint64_t kk = keys[j];
+      if (kk <= k0) le++;
+      else gt = kk < gt ? kk : gt;
+    }
+    le = wave_sum_int(le);
+    gt = wave_min_u64(gt);
+    k1 = le > r1 ? k0 : gt;
+  }
+  const double v0 = key2f(k0), v1 = key2f(k1);
+  WAVE_SYNC();
+  return select_sorted(p.sel_fn, (int)n, [&](int i) { return (int64_t)i == r0 ? v0 : v1; });
+}
+
+// value of a finished bucket holding n non-NaN values in buf (and gbuf beyond PCT_CAP)
+__device__ __forceinline__ double bucket_value(const GridParams& p, double* buf, int64_t n, double* gbuf, SelWave* SW) {
   const int lane = lane_id();
   if (n == 0) return (double)NAN;
-  if (n > PCT_CAP) {   // only the BIG pass gets here
-    if (lane == 0) set_err(p.err, TSDB_E_NOT_IMPLEMENTED);
-    return (double)NAN;
-  }
+  if (n > PCT_CAP) return bucket_value_big(p, buf, n, gbuf, *SW);   // only the BIG pass gets here
   double sel;
-  if (select_extreme(p.sel_fn, n, buf, sel)) return sel;
+  if (select_extreme(p.sel_fn, (int)n, buf, sel)) return sel;
   if (n <= CH) {
     double v[DPL];
 #pragma unroll
@@ -221,44 +389,27 @@ __device__ __forceinline__ double bucket_value(const GridParams& p, double* buf,
       v[j] = e < n ? buf[e] : (double)INFINITY;
     }
     sort512(v);
-    return select_sorted(p.sel_fn, n, [&](int i) { return reg_at(v, i); });
+    return select_sorted(p.sel_fn, (int)n, [&](int i) { return reg_at(v, i); });
   }
   int N = CH;
   while (N < n) N <<= 1;
-  for (int e = n + lane; e < N; e += 64) buf[e] = (double)INFINITY;
+  for (int e = (int)n + lane; e < N; e += 64) buf[e] = (double)INFINITY;
   WAVE_SYNC();
   sort_lds(buf, N);
-  return select_sorted(p.sel_fn, n, [&](int i) { return buf[i]; });
+  return select_sorted(p.sel_fn, (int)n, [&](int i) { return buf[i]; });
 }
 
-// Order statistics per (series, bucket).  BIG = false: every series, buckets of at most
-// CH values (register sort), 4 waves per block; a series with a larger bucket is appended
-// to p.redo_list and left to the BIG pass (one wave per listed series, LDS buffer of
-// PCT_CAP values).  Uniform rows are decoded from registers with a one-chunk prefetch
-// (load_raw / decode_raw, as k_grid); other row classes through decode_generic.
-template <bool BIG, bool LIST>
-__global__ __launch_bounds__(256) void k_pct(GridParams p) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// Order statistics per (series, bucket) of series s.  BIG = false: buckets of at most CH
+// values (register sort); false = the series has a larger bucket (left to the BIG pass).
+// BIG = true: buckets up to PCT_CAP values sorted in the LDS buffer, larger ones spill to the
+// wave's global region gbuf (p.big_cap values) and are radix-selected.  Uniform rows are
+// decoded from registers with a one-chunk prefetch (load_raw / decode_raw, as k_grid);
+// other row classes through decode_generic.
+template <bool BIG>
+__device__ bool pct_series(const GridParams& p, int64_t s, const WaveLds& W, double* buf, double* gbuf, SelWave* SW) {
   constexpr int CAP = BIG ? PCT_CAP : CH;
   const int lane = lane_id();
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  unsigned char* base = smem + (int64_t)wave * (VBUF + CAP * 8);
-  WaveLds W;
-  W.dpv = (double*)base;
-  W.vbuf = base;
-  W.mq = (uint32_t*)base;
-  W.mv = (uint32_t*)(base + CH * 4);
-  double* buf = (double*)(base + VBUF);
   const int K = (int)p.K;
-  int64_t s = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-  if (BIG) {
-    if (s >= (int64_t)*p.redo_n) return;
-    s = p.redo_list[s];
-  } else if (LIST) {   // series k_pct_rows handed back
-    if (s >= (int64_t)*p.tile_list_n) return;
-    s = p.tile_list[s];
-  }
-  if (s >= p.n_series) return;
   double* dense = p.pre_dense + s * K;
   uint8_t* pres = p.pre_pres + s * K;
   for (int k = lane; k < K; k += 64) pres[k] = 0;
@@ -268,16 +419,15 @@ __global__ __launch_bounds__(256) void k_pct(GridParams p) {
   while (ra < r1 && (int64_t)p.rows[ra].base < p.ss) ra++;
   int64_t rb = ra;
   while (rb < r1 && (int64_t)p.rows[rb].base < p.se) rb++;
-  int cur = -1;      // open bucket
-  int cnt = 0;       // its non-NaN values (in buf)
-  bool big = false;
+  int cur = -1;        // open bucket
+  int64_t cnt = 0;     // its non-NaN values (in buf / gbuf)
   Raw rc = {}, rn = {};
   RowDesc d = {};
   if (ra < rb) {
     d = p.rows[ra];
     if (row_uniform(d)) load_raw(p, d, 0, rc);
   }
-  for (int64_t r = ra; r < rb && !big; r++) {
+  for (int64_t r = ra; r < rb; r++) {
     const bool has_next = r + 1 < rb;
     RowDesc nd = {};
     if (has_next) nd = p.rows[r + 1];
@@ -290,7 +440,7 @@ __global__ __launch_bounds__(256) void k_pct(GridParams p) {
     const RowGeom g = row_geom(p, d.base);
     const bool uni = row_uniform(d);
     int64_t vcur = 0;
-    for (int64_t c0 = 0; c0 < (int64_t)d.ndp && !big; c0 += CH) {
+    for (int64_t c0 = 0; c0 < (int64_t)d.ndp; c0 += CH) {
       // prefetch the next chunk (same row, or the first chunk of the next row)
       if (c0 + CH < (int64_t)d.ndp) {
         if (uni) load_raw(p, d, c0 + CH, rn);
@@ -313,7 +463,7 @@ __global__ __launch_bounds__(256) void k_pct(GridParams p) {
         if (mn == INT32_MAX) break;
         if (mn != cur) {
           if (cur >= 0) {
-            const double x = bucket_value(p, buf, cnt);
+            const double x = bucket_value(p, buf, cnt, gbuf, SW);
             if (lane == 0) { dense[cur] = x; pres[cur] = 1; }
           }
           cur = mn;
@@ -325,35 +475,65 @@ __global__ __launch_bounds__(256) void k_pct(GridParams p) {
         for (int j = 0; j < DPL; j++) if (left[j] && slot[j] == mn && !isnan(val[j])) mine++;
         const int incl = wave_incl_sum(mine);
         const int total = __shfl(incl, 63, 64);
-        if (!BIG && cnt + total > CAP) {   // bucket too large for the register sort
-          big = true;
-          break;
-        }
-        int o = cnt + incl - mine;
+        if (!BIG && cnt + total > CAP) return false;   // bucket too large for the register sort
+        int64_t o = cnt + incl - mine;
 #pragma unroll
         for (int j = 0; j < DPL; j++) {
           if (left[j] && slot[j] == mn) {
             if (!isnan(val[j])) {
               if (o < CAP) buf[o] = val[j];
+              else if (BIG && o < p.big_cap) gbuf[o] = val[j];
               o++;
             }
             left[j] = false;
           }
         }
         cnt += total;
+        if (BIG && cnt > p.big_cap && lane == 0) set_err(p.err, TSDB_E_HIP);   // host sizing bug; never silent
         WAVE_SYNC();
       }
     }
     d = nd;
   }
-  if (big) {
-    if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)s;
-    return;
-  }
   if (cur >= 0) {
-    const double x = bucket_value(p, buf, cnt);
+    const double x = bucket_value(p, buf, cnt, gbuf, SW);
     if (lane == 0) { dense[cur] = x; pres[cur] = 1; }
   }
+  return true;
+}
+
+// BIG = false: one wave per series (LIST: the series k_pct_rows handed back), 4 waves a
+// block; a series with a bucket of more than CH values goes to p.redo_list.  BIG = true:
+// p.n_launch waves loop over p.redo_list, each with a region of p.big_cap values of
+// p.big_scratch for buckets above PCT_CAP.
+template <bool BIG, bool LIST>
+__global__ __launch_bounds__(256) void k_pct(GridParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ SelWave SWs[BIG ? 2 : 1];
+  constexpr int CAP = BIG ? PCT_CAP : CH;
+  const int lane = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  unsigned char* base = smem + (int64_t)wave * (VBUF + CAP * 8);
+  WaveLds W;
+  W.dpv = (double*)base;
+  W.vbuf = base;
+  W.mq = (uint32_t*)base;
+  W.mv = (uint32_t*)(base + CH * 4);
+  double* buf = (double*)(base + VBUF);
+  const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+  if (BIG) {
+    double* gbuf = p.big_scratch + gw * p.big_cap;
+    const int64_t n = *p.redo_n;
+    for (int64_t i = gw; i < n; i += p.n_launch) pct_series<true>(p, p.redo_list[i], W, buf, gbuf, &SWs[wave]);
+    return;
+  }
+  int64_t s = gw;
+  if (LIST) {   // series k_pct_rows handed back
+    if (s >= (int64_t)*p.tile_list_n) return;
+    s = p.tile_list[s];
+  }
+  if (s >= p.n_series) return;
+  if (!pct_series<false>(p, s, W, buf, nullptr, nullptr) && lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)s;
 }
 
 // One wave per tile: SpanGroup contributions of precomputed bucket values.
@@ -718,6 +898,7 @@ __global__ __launch_bounds__(256) void k_pct_rows(GridParams p) {
 hipError_t launch_pct(const GridParams& p, int pass, int64_t n, hipStream_t s) {
   if (n == 0) return hipSuccess;
   if (pass == 2) {
+    // n = waves (p.n_launch, even): a persistent loop over the listed series
     const size_t lds = 2 * (size_t)(VBUF + PCT_CAP * 8);
     hipError_t e = hipFuncSetAttribute((const void*)k_pct<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -744,9 +925,6 @@ bool pct_rows_supported(int qw, int vl) { return (qw == 2 || qw == 4) && (vl == 
 // LDS as order-preserving integer keys and finds the one or two order statistics
 // select_sorted needs by an 8-pass radix select -- no sort.
 
-__device__ __forceinline__ double canon_nan(double v) {
-  return isnan(v) ? __longlong_as_double(0x7FF8000000000000LL) : v;   // +NaN: the largest key
-}
 
 // One wave per tile (<= 64 series of one group).
 __global__ __launch_bounds__(256) void k_emit_vals(GridParams p) {
@@ -779,13 +957,6 @@ __global__ __launch_bounds__(256) void k_emit_vals(GridParams p) {
   if (active && lane_id() == 0) atomicOr(&p.group_active[g], 1u);
 }
 
-__device__ __forceinline__ uint64_t f2key(double x) {   // ascending double order == unsigned key order
-  const uint64_t b = (uint64_t)__double_as_longlong(x);
-  return (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
-}
-__device__ __forceinline__ double key2f(uint64_t k) {
-  return __longlong_as_double((long long)((k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFULL) : ~k));
-}
 
 // The key of rank r (0-based, ascending) among keys[0..n): MSB-first radix select, 8 bits a
 // pass; the bin holding rank r is found by wave 0 with a prefix sum over its lanes' 4 bins,
@@ -1053,115 +1224,6 @@ __device__ __forceinline__ int64_t sel_d2l(double d) {   // Java (long) of a dou
 // point pt -> strip pt / RAW_STRIP, position j.  Wave-local radix select: 8-bit digits, a
 // 256-bin LDS histogram per wave, the digit holding rank r found by a wave prefix sum over
 // the lanes' 4 bins; once <= 64 keys share the prefix they are ranked directly.
-constexpr int SELW = 4;
-constexpr int RAW_SEL_LDS = 4096;   // keys per wave staged in LDS (4 x 32 KB a block)
-struct SelWave {
-  uint32_t hist[256];
-  uint64_t cand[64];
-  uint32_t n;
-};
-
-__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
-  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
-  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
-  return ((uint64_t)hi << 32) | lo;
-}
-
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const uint64_t o = shfl_u64(v, lane_id() ^ d);
-    v = o < v ? o : v;
-  }
-  return v;
-}
-
-__device__ __forceinline__ int wave_sum_int(int v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-  return v;
-}
-
-// Key of rank r (0-based ascending) among keys[0..n); called by all 64 lanes of the wave.
-__device__ uint64_t wave_radix_select(const uint64_t* keys, int64_t ks, int n, int r, SelWave& W) {
-  const int lane = lane_id();
-  // skip the leading digits every key shares (counters, clustered values): they would put
-  // all n keys into one histogram bin, pass after pass
-  uint64_t kand = ~0ULL, kor = 0;
-  for (int j = lane; j < n; j += 64) {
-    const uint64_t k = keys[j * ks];
-    kand &= k;
-    kor |= k;
-  }
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    kand &= shfl_u64(kand, lane ^ d);
-    kor |= shfl_u64(kor, lane ^ d);
-  }
-  const uint64_t diff = kand ^ kor;
-  if (diff == 0) return kand;   // all keys equal
-  const int top = (63 - __clzll((long long)diff)) & ~7;   // lowest bit of the first differing digit
-  uint64_t mask = top == 56 ? 0 : ~((1ULL << (top + 8)) - 1ULL);
-  uint64_t prefix = kand & mask;
-  for (int shift = top; shift >= 0; shift -= 8) {
-#pragma unroll
-    for (int q = 0; q < 4; q++) W.hist[lane * 4 + q] = 0;
-    WAVE_SYNC();
-    for (int j = lane; j < n; j += 64) {
-      const uint64_t k = keys[j * ks];
-      if ((k & mask) == prefix) atomicAdd(&W.hist[(k >> shift) & 255], 1u);
-    }
-    WAVE_SYNC();
-    uint32_t c[4], t = 0;
-#pragma unroll
-    for (int q = 0; q < 4; q++) { c[q] = W.hist[lane * 4 + q]; t += c[q]; }
-    const int incl = wave_incl_sum((int)t);
-    int ex = incl - (int)t;
-    const bool found = ex <= r && r < incl;
-    int bin = 0, rr = 0, nc = 0;
-    if (found) {
-      int q = 0;
-      for (; q < 3; q++) {
-        if (r < ex + (int)c[q]) break;
-        ex += (int)c[q];
-      }
-      bin = lane * 4 + q;
-      rr = r - ex;
-      nc = (int)c[q];
-    }
-    const int src = __ffsll((long long)__ballot(found)) - 1;
-    bin = __shfl(bin, src, 64);
-    rr = __shfl(rr, src, 64);
-    nc = __shfl(nc, src, 64);
-    prefix |= (uint64_t)bin << shift;
-    mask |= 255ULL << shift;
-    r = rr;
-    WAVE_SYNC();
-    if (shift == 0) break;
-    if (nc <= 64) {
-      if (lane == 0) W.n = 0;
-      WAVE_SYNC();
-      for (int j = lane; j < n; j += 64) {
-        const uint64_t k = keys[j * ks];
-        if ((k & mask) == prefix) W.cand[atomicAdd(&W.n, 1u)] = k;
-      }
-      WAVE_SYNC();
-      const uint64_t x = lane < nc ? W.cand[lane] : ~0ULL;
-      int less = 0, eq = 0;
-      for (int q = 0; q < nc; q++) {
-        const uint64_t y = W.cand[q];
-        less += y < x;
-        eq += y == x;
-      }
-      const bool hit = lane < nc && less <= r && r < less + eq;
-      const uint64_t res = shfl_u64(x, __ffsll((long long)__ballot(hit)) - 1);
-      WAVE_SYNC();
-      return res;
-    }
-  }
-  return prefix;
-}
-
 __global__ __launch_bounds__(256) void k_raw_sel(RawParams p, int32_t kcap) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ SelWave WS[SELW];

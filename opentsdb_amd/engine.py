@@ -27,6 +27,7 @@ EXPORTS = [
     "tsdbhip_run_partials", "tsdbhip_finalize", "tsdbhip_sync", "tsdbhip_rollup_interval_parse",
     "tsdbhip_rollup_basetime", "tsdbhip_rollup_qualifier", "tsdbhip_rollup_run", "tsdbhip_rollup_download",
     "tsdbhip_sel_layout", "tsdbhip_sel_run_values", "tsdbhip_sel_select", "tsdbhip_assemble", "tsdbhip_run_multi",
+    "tsdbhip_debug_rows",
 ]
 
 
@@ -87,6 +88,7 @@ def lib():
                                                C.POINTER(abi.RollupInterval), C.c_void_p]
         L.tsdbhip_rollup_run.argtypes = [vp, C.POINTER(abi.RollupSpec), C.POINTER(C.c_int64), C.POINTER(C.c_uint64)]
         L.tsdbhip_rollup_download.argtypes = [vp] + [C.c_void_p] * 5
+        L.tsdbhip_debug_rows.argtypes = [vp] + [C.c_void_p] * 4
         _lib = L
     return _lib
 
@@ -232,6 +234,18 @@ class Engine:
 
     def sync(self):
         _check(lib().tsdbhip_sync(self.ctx))
+
+    def debug_rows(self):
+        """Test hook: k_index's per-row (ndp, flags, lsb, absmax) of the resident batch."""
+        ns, nr, qb, vb = C.c_int64(), C.c_int64(), C.c_uint64(), C.c_uint64()
+        _check(lib().tsdbhip_batch_sizes(self.ctx, C.byref(ns), C.byref(nr), C.byref(qb), C.byref(vb)))
+        n = max(1, nr.value)
+        ndp, flags = np.zeros(n, np.uint32), np.zeros(n, np.uint32)
+        lsb, amax = np.zeros(n, np.int32), np.zeros(n, np.float64)
+        _check(lib().tsdbhip_debug_rows(self.ctx, ndp.ctypes.data, flags.ctypes.data, lsb.ctypes.data,
+                                        amax.ctypes.data))
+        k = nr.value
+        return ndp[:k], flags[:k], lsb[:k], amax[:k]
 
     # ---- rollup generation (tsdbhip_rollup_run) ----
     def rollup_run(self, interval: abi.RollupInterval, start_s: int, end_s: int,

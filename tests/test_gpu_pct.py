@@ -95,13 +95,42 @@ def test_pct_large_bucket_lds_sort(eng):
     assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "max", ctx="3600/bucket")
 
 
-def test_pct_bucket_over_capacity_is_reported(eng):
-    from opentsdb_amd.engine import EngineError
-    b = synth.generate(2, T0, 7200, 1000, value_kind=0, n_groups=1, seed=9)
-    q = abi.new_query(T0, T0 + 7199, "max", ds_function=abi.AGG["p99"], ds_interval_ms=7200000)
-    with pytest.raises(EngineError) as ei:
-        eng.run_batch(b, q)
-    assert ei.value.java == "NotImplemented"
+@pytest.mark.parametrize("fn", ["p99", "median", "p50", "ep999r7"])
+def test_pct_1d_buckets_over_lds_capacity(eng, fn):
+    """1d-p99 / 1d-median over 1 day @10 s: 8640 values per bucket, above PCT_CAP (4096) --
+    the large-bucket pass spills them to its global region and radix-selects (the reference
+    has no size limit, src/core/Aggregators.java:657-708)."""
+    b = synth.generate(40, T0, 8640, 10000, value_kind=2, n_groups=3, int_mod=30000, seed=12)
+    q = abi.new_query(T0, T0 + 86399, "max", ds_function=abi.AGG[fn], ds_interval_ms=86400000)
+    assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "max", ctx=f"1d-{fn}")
+    q = abi.new_query(T0, T0 + 86399, "sum", ds_function=abi.AGG[fn], ds_interval_ms=86400000)
+    assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "sum", ctx=f"1d-{fn} sum")
+
+
+def test_pct_2h_p95_at_1s(eng):
+    """2h-p95 @1 s: 7200 values per bucket, full-mantissa doubles, ties-free."""
+    b = synth.generate(12, T0, 14400, 1000, value_kind=4, n_groups=2, seed=9)
+    for fn in ["p95", "p999", "median"]:
+        q = abi.new_query(T0, T0 + 14399, "max", ds_function=abi.AGG[fn], ds_interval_ms=7200000)
+        assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "max", ctx=f"2h-{fn}")
+
+
+def test_pct_large_buckets_with_ties_and_nans(eng):
+    """Buckets of 5000-20000 values with 7 distinct values (radix-select ties) and NaNs."""
+    rng = np.random.default_rng(21)
+    rows, gids = [], []
+    for s in range(8):
+        n = 5000 + 2000 * s
+        ts = T0 * 1000 + np.arange(n, dtype=np.int64) * 1000
+        f = rng.integers(0, 7, n).astype(np.float64)
+        f[rng.random(n) < 0.05] = np.nan
+        kind = np.full(n, 2)
+        rows.append(synth.encode_rows(ts, np.zeros(n, np.int64), f, kind, np.zeros(n, bool)))
+        gids.append(0)
+    b = synth.from_series(rows, gids)
+    for fn in ["p99", "p50", "median", "p999"]:
+        q = abi.new_query(T0, T0 + 86399, "max", ds_function=abi.AGG[fn], ds_interval_ms=86400000)
+        assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "max", ctx=f"ties {fn}")
 
 
 def test_pct_sharded(eng, day_batch):
