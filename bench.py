@@ -126,7 +126,11 @@ def pmc_traffic(args, kernel_prefix: str):
     fetch = out["FETCH_SIZE"] * 1024.0 * 2.0
     write = out["WRITE_SIZE"] * 1024.0
     return fetch + write, {"fetch_bytes": fetch, "write_bytes": write, "fetch_size_kib_raw": out["FETCH_SIZE"],
-                           "correction": "FETCH_SIZE x2 (gfx950 streaming-read undercount), KiB->B"}
+                           "write_size_kib_raw": out["WRITE_SIZE"],
+                           "traffic_uncorrected": out["FETCH_SIZE"] * 1024.0 + write,
+                           "correction": "FETCH_SIZE x2 and KiB->B, as /opt/skills/guides/MI355X_MICROARCH.md's "
+                                         "HBM / rocprofv3 section prescribes for gfx950 (FETCH_SIZE reports half "
+                                         "the bytes of 16-B-per-lane streaming reads); WRITE_SIZE exact"}
 
 
 def workload_label(args) -> str:
@@ -259,6 +263,9 @@ def main():
                 "peak": BYTES_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / BYTES_PEAK_GBS,
+                "frac_note": "kernel-only: algorithmic bytes / the dominant kernel's hipEvent time; frac_step is "
+                             "the same bytes over the whole step (decode + group-by + results to the host)",
+                "frac_step": tm.bytes / (ms_per_step / 1000.0) / 1e9 / BYTES_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_detail": traffic_note,
                 "kernel": kname + (" (streaming decode+downsample+tile group partials)" if use_fast

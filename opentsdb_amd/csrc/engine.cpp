@@ -204,6 +204,7 @@ struct tsdbhip_ctx {
   uint64_t qual_bytes = 0, val_bytes = 0;
   DevBuf rows, srp, qual, val, gid;
   DevBuf val2;                         // int16 copy of vle-integer values (k_index), at qualifier offsets
+  DevBuf hint, ilist, icnt;            // k_index scratch: row classes, rows by class, class counts
   std::vector<int64_t> h_srp;          // [n_series+1]
   std::vector<uint32_t> h_base;        // [n_rows]
   std::vector<uint32_t> h_ndp;         // [n_rows]
@@ -396,7 +397,7 @@ extern "C" int tsdbhip_init(int device, tsdbhip_ctx** out) {
 }
 
 static void release_batch(tsdbhip_ctx* c) {
-  for (DevBuf* b : {&c->rows, &c->srp, &c->qual, &c->val, &c->val2, &c->gid, &c->d_tb, &c->d_te, &c->d_tg, &c->d_gtp,
+  for (DevBuf* b : {&c->rows, &c->srp, &c->qual, &c->val, &c->val2, &c->hint, &c->ilist, &c->icnt, &c->gid, &c->d_tb, &c->d_te, &c->d_tg, &c->d_gtp,
                     &c->n_tb, &c->n_te, &c->n_tg, &c->n_gtp})
     b->release();
   c->none_tiles_ready = false;
@@ -531,28 +532,41 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
   // classify rows on the device, then fetch ndp for host-side accounting
   HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
   const char* genv = std::getenv("TSDBHIP_INDEX_GENERIC");   // test hook: sequential per-datapoint path
+  const bool generic = genv && genv[0] == '1';
+  HIP_OK(c->hint.ensure(std::max<int64_t>(1, c->n_rows)));
+  HIP_OK(c->ilist.ensure(std::max<int64_t>(1, c->n_rows) * 4));
+  HIP_OK(c->icnt.ensure(32 * 4));
+  const IndexBufs ib{c->hint.as<uint8_t>(), c->ilist.as<int32_t>(), c->icnt.as<uint32_t>()};
+  // the int16 copy of 1-2-byte integer values (val2, k_short / k_fast's vle rows) is written by
+  // the class kernels of the 2-byte-qualifier integer classes, allocated when such rows exist
+  c->val2.release();
   HIP_OK(hipEventRecord(c->ev[0], c->stream));
-  HIP_OK(launch_index(c->qual.as<uint8_t>(), c->val.as<uint8_t>(), nullptr, c->rows.as<RowDesc>(), c->n_rows,
-                      c->err.as<int32_t>(), c->stream, genv && genv[0] == '1'));
+  IndexClasses ik;
+  HIP_OK(index_classes(c->qual.as<uint8_t>(), c->rows.as<RowDesc>(), ib, c->n_rows, &ik, c->stream));
+  HIP_OK(hipEventRecord(c->ev[2], c->stream));
+  if (ik.vle_capable && !generic) HIP_OK(c->val2.ensure(c->qual_bytes + BLOB_SLACK));
+  HIP_OK(hipEventRecord(c->ev[3], c->stream));   // (the allocation is not index time)
+  HIP_OK(index_rows(c->qual.as<uint8_t>(), c->val.as<uint8_t>(), c->val2.as<uint8_t>(), c->rows.as<RowDesc>(), ib, ik,
+                    c->n_rows, c->err.as<int32_t>(), generic, c->stream));
   HIP_OK(hipEventRecord(c->ev[1], c->stream));
   std::vector<RowDesc> back(c->n_rows);
   if (c->n_rows)
     HIP_OK(hipMemcpyAsync(back.data(), c->rows.p, c->n_rows * sizeof(RowDesc), hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
-  float t_index = 0, t_val2 = 0;
-  (void)hipEventElapsedTime(&t_index, c->ev[0], c->ev[1]);
-  // rows of the vle-integer class (2-byte qualifiers, 1-2-byte integers): a second pass
-  // writes their values as int16 at the qualifier offsets (val2), the layout k_short /
-  // k_fast read -- allocated only when such rows exist
+  float t_index = 0, t_val2 = 0, t_cls = 0;
+  (void)hipEventElapsedTime(&t_cls, c->ev[0], c->ev[2]);
+  (void)hipEventElapsedTime(&t_index, c->ev[3], c->ev[1]);
+  t_index += t_cls;
   bool need_val2 = false;
   for (const RowDesc& d : back)
     if ((d.flags & (ROW_QW_MASK | ROW_ALLI | ROW_VLE2 | ROW_ERR)) == (2u | ROW_ALLI | ROW_VLE2)) { need_val2 = true; break; }
-  c->val2.release();
-  if (need_val2) {
+  if (!need_val2) {
+    c->val2.release();
+  } else if (generic) {   // test hook: the sequential path writes the copy in a second pass
     HIP_OK(c->val2.ensure(c->qual_bytes + BLOB_SLACK));
     HIP_OK(hipEventRecord(c->ev[2], c->stream));
-    HIP_OK(launch_index(c->qual.as<uint8_t>(), c->val.as<uint8_t>(), c->val2.as<uint8_t>(), c->rows.as<RowDesc>(),
-                        c->n_rows, c->err.as<int32_t>(), c->stream, genv && genv[0] == '1'));
+    HIP_OK(index_rows(c->qual.as<uint8_t>(), c->val.as<uint8_t>(), c->val2.as<uint8_t>(), c->rows.as<RowDesc>(), ib,
+                      ik, c->n_rows, c->err.as<int32_t>(), true, c->stream));
     HIP_OK(hipEventRecord(c->ev[3], c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
     (void)hipEventElapsedTime(&t_val2, c->ev[2], c->ev[3]);
@@ -1914,6 +1928,10 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
         int64_t k_max = 1;
         for (int64_t t = s0; t < s1; t++) k_max = std::max<int64_t>(k_max, grp_ser[g0 + sg[t] + 1] - grp_ser[g0 + sg[t]]);
         HIP_OK(launch_raw_vals(bp, k_max, c->stream));
+        // k_raw_sel CONSUMES this batch's operand buffers: for groups above its LDS capacity it
+        // builds the sort keys in place over r_vl / r_vd, so they hold keys, not operands,
+        // afterwards.  Every batch is staged by launch_raw_vals right before its selection;
+        // a second selection over the same batch would have to re-stage it.
         HIP_OK(launch_raw_sel(bp, k_max, c->stream));
       }
     } else {

@@ -298,9 +298,24 @@ hipError_t rollup_scan(const uint32_t* cnt, int64_t* coff, const uint32_t* vsz, 
                        void** tmp, size_t* tmp_bytes, hipStream_t s);
 
 // launchers (kernels.hip)
-// generic: every row through the sequential per-datapoint path (test hook)
-hipError_t launch_index(const uint8_t* qual, const uint8_t* val, uint8_t* val2, RowDesc* rows, int64_t n_rows, int32_t* err,
-                        hipStream_t s, bool generic = false);
+// k_index.hip: row classification (once per load).  index_classes: per-row class, class
+// counts and class row lists; index_rows: the class kernels (+ the int16 copy of 1-2-byte
+// integer values when val2 is non-null) and the sequential path for the rest (generic: every
+// row sequentially -- test hook).
+struct IndexBufs {
+  uint8_t* hint;     // [n_rows] row class
+  int32_t* list;     // [n_rows] rows by class
+  uint32_t* cnt;     // [16] class counts / list cursors
+};
+struct IndexClasses {
+  uint32_t cnt[16];
+  uint32_t off[16];
+  uint32_t vle_capable;   // rows of the 2-byte-qualifier integer classes (variable, 1-byte, 2-byte values)
+};
+hipError_t index_classes(const uint8_t* qual, const RowDesc* rows, const IndexBufs& b, int64_t n_rows,
+                         IndexClasses* out, hipStream_t s);
+hipError_t index_rows(const uint8_t* qual, const uint8_t* val, uint8_t* val2, RowDesc* rows, const IndexBufs& b,
+                      const IndexClasses& k, int64_t n_rows, int32_t* err, bool generic, hipStream_t s);
 hipError_t launch_grid(const GridParams& p, int ds_function_class, hipStream_t s);
 // k_fast: uniform float rows of one (qualifier width, value length) class; returns
 // hipErrorNotSupported when no specialisation exists for (f, qw, vl)

@@ -1,0 +1,769 @@
+// k_index.hip -- the load-time row index of libtsdbhip.
+//
+// RowSeq's per-datapoint view (src/core/RowSeq.java:233-266, 552-614; Internal.java:621-810)
+// reduced to the row facts the query kernels branch on: qualifier width, uniform value
+// length, all-float / all-integer, NaN / -0.0, offset order, malformed cells, and the
+// exactness certificate (least significant set bit, max |value|).  Written once per load into
+// RowDesc; 2-byte-qualifier rows also get their 1-2-byte integers as little-endian int16 at
+// val2 + qoff + 2 i (the same offsets as the qualifiers), the layout k_short / k_fast read for
+// vle rows.
+//
+//  * k_index_hint     one thread per row: the row's class -- qualifier width (first byte) x
+//                     value length (L when the value bytes are exactly ndp x L (+ meta byte),
+//                     else variable) -- and per-class row counts.
+//  * k_index_scatter  per-class row lists.
+//  * k_index_cls<QW,L>  one wave per row of its class (grid-stride over the list), 8 datapoints
+//                     per lane per 512-datapoint chunk.  Every lane issues the same loads for
+//                     every chunk (lanes past the row re-read its start), so the next chunk --
+//                     or the next row's first chunk -- is prefetched while this one decodes and
+//                     the wait before use covers only the older loads.  Uniform classes read
+//                     values at i x L; the variable class stages value bytes in LDS after a
+//                     wave prefix sum of the lengths (its first 1 KB prefetched).  Statistics
+//                     are kept in the integer domain (bit patterns, magnitudes).
+//  * k_index_generic  rows no class kernel takes (mixed second / millisecond qualifiers, odd or
+//                     empty qualifier arrays, a class hypothesis that failed): sequential.
+#include "kcommon.h"
+
+namespace tsdb {
+
+static constexpr int IDX_STAGE = 4224;   // bytes of value staging per wave: 512 x 8 B + alignment
+static constexpr int IDX_NCLS = 11;      // 0 generic, 1 + qwi * 5 + li (qwi: 2 / 4 bytes; li: var, 1, 2, 4, 8)
+
+struct IdxAcc {
+  bool bad, allf, alli, vmax2, nan, negz, unsorted;
+  int lsb, lmin, lmax;
+  double amax;
+};
+
+__device__ __forceinline__ void idx_acc_init(IdxAcc& a) {
+  a.bad = false; a.allf = a.alli = a.vmax2 = true; a.nan = a.negz = a.unsorted = false;
+  a.lsb = INT32_MAX; a.lmin = 99; a.lmax = -1; a.amax = 0.0;
+}
+
+// 8 bytes of the LDS stage from byte offset b (little-endian memory order)
+__device__ __forceinline__ uint64_t stage_u64(const uint32_t* s, int b) {
+  const int w = b >> 2, sh = (b & 3) * 8;
+  const uint32_t w0 = s[w], w1 = s[w + 1], w2 = s[w + 2];
+  const uint32_t lo = sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0;
+  const uint32_t hi = sh ? (w1 >> sh) | (w2 << (32 - sh)) : w1;
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __noinline__ void index_row_generic(const uint8_t* __restrict__ qual, const uint8_t* __restrict__ val,
+                                  uint8_t* __restrict__ val2, RowDesc* __restrict__ rows, int64_t r, int32_t* err) {
+  const int lane = lane_id();
+  {
+    RowDesc d = rows[r];
+    const uint8_t* q = qual + d.qoff;
+    const uint8_t* v = val + d.voff;
+    const uint32_t qlen = d.qlen;
+    // hypotheses: all 2-byte, all 4-byte
+    bool ok2 = (qlen % 2) == 0 && qlen > 0;
+    bool ok4 = (qlen % 4) == 0 && qlen > 0;
+    int lmin2 = 99, lmax2 = -1, lmin4 = 99, lmax4 = -1;
+    for (uint32_t p0 = (uint32_t)lane * 16; p0 < qlen; p0 += 64 * 16) {
+      const uint4 w = *reinterpret_cast<const uint4*>(q + p0);
+      const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int b = 0; b < 16; b += 2) {
+        if (p0 + b >= qlen) break;
+        const uint32_t b0 = (ws[b >> 2] >> ((b & 3) * 8)) & 0xFF;
+        const uint32_t b1 = (ws[(b + 1) >> 2] >> (((b + 1) & 3) * 8)) & 0xFF;
+        if ((b0 & 0xF0) == 0xF0) ok2 = false;
+        const int len = (b1 & 7) + 1;
+        lmin2 = min(lmin2, len);
+        lmax2 = max(lmax2, len);
+        if ((b & 3) == 0) {
+          if ((b0 & 0xF0) != 0xF0) ok4 = false;
+          const uint32_t b3 = (ws[(b + 3) >> 2] >> (((b + 3) & 3) * 8)) & 0xFF;
+          const int l4 = (b3 & 7) + 1;
+          lmin4 = min(lmin4, l4);
+          lmax4 = max(lmax4, l4);
+        }
+      }
+    }
+    ok2 = __all(ok2);
+    ok4 = __all(ok4);
+    lmin2 = wave_min(lmin2); lmax2 = wave_max(lmax2);
+    lmin4 = wave_min(lmin4); lmax4 = wave_max(lmax4);
+    uint32_t flags = 0, ndp = 0;
+    if (ok2) {
+      ndp = qlen / 2; flags = 2;
+      if (lmin2 == lmax2) flags |= (uint32_t)lmin2 << ROW_VL_SHIFT;
+    } else if (ok4) {
+      ndp = qlen / 4; flags = 4;
+      if (lmin4 == lmax4) flags |= (uint32_t)lmin4 << ROW_VL_SHIFT;
+    } else {
+      // mixed second/millisecond qualifiers (meta bit MS_MIXED_COMPACT): count sequentially
+      if (lane == 0) {
+        uint32_t i = 0;
+        while (i < qlen) {
+          const uint32_t w = ((q[i] & 0xF0) == 0xF0) ? 4 : 2;
+          if (i + w > qlen) break;
+          ndp++;
+          i += w;
+        }
+      }
+      ndp = __shfl(ndp, 0, 64);
+    }
+    // walk every datapoint: validate qualifier/value lengths, certificate stats
+    bool bad = qlen == 0;
+    bool allf = true, alli = true, vmax2 = true, hasnan = false, negz = false, unsorted = false;
+    int lsbmin = INT32_MAX;
+    double amax = 0.0;
+    long long vcarry = 0;
+    uint32_t qcarry = 0;
+    long long prev_off = -1;   // offset (ms) of the previous datapoint
+    for (uint32_t i0 = 0; i0 < ndp; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      const bool in = i < ndp;
+      uint32_t qpos = 0, w = 2;
+      if (flags & ROW_QW_MASK) {
+        w = flags & ROW_QW_MASK;
+        qpos = i * w;
+      } else {
+        // mixed: positions found by the sequential walk below
+      }
+      uint32_t fb = 0;
+      if (flags & ROW_QW_MASK) {
+        if (in) fb = q[qpos + w - 1];
+      } else {
+        // mixed rows are rare: lane 0 computes every width sequentially, then broadcasts through shuffles
+        uint32_t pos = qcarry, mypos = 0, myw = 2;
+        for (int t = 0; t < 64 && i0 + t < ndp; t++) {
+          const uint32_t ww = ((q[pos] & 0xF0) == 0xF0) ? 4 : 2;
+          if (t == lane) { mypos = pos; myw = ww; }
+          pos += ww;
+        }
+        qpos = mypos;
+        w = myw;
+        if (in) fb = q[qpos + w - 1];
+        qcarry = __shfl(pos, 0, 64);
+      }
+      const int len = in ? (int)(fb & 7) + 1 : 0;
+      const bool fl = (fb & 8) != 0;
+      // offset order (strictly increasing in a well-formed compacted cell)
+      long long off = -1;
+      if (in) {
+        if (w == 4) off = (long long)((((uint32_t)q[qpos] << 24) | ((uint32_t)q[qpos + 1] << 16) |
+                                       ((uint32_t)q[qpos + 2] << 8) | q[qpos + 3]) & 0x0FFFFFC0u) >> 6;
+        else off = (long long)((((uint32_t)q[qpos] << 8) | q[qpos + 1]) >> 4) * 1000;
+      }
+      long long po = __shfl_up(off, 1, 64);
+      if (lane == 0) po = prev_off;
+      if (in && off <= po) unsorted = true;
+      prev_off = __shfl(off, (int)min((uint32_t)63, ndp - 1 - i0), 64);
+      if (in && !fl) allf = false;
+      if (in && fl) alli = false;
+      if (in && len > 2) vmax2 = false;
+      if (in && (fl ? (len != 4 && len != 8) : (len == 3 || (len >= 5 && len <= 7)))) bad = true;
+      const int incl = wave_incl_sum(len);
+      const long long vo = vcarry + incl - len;
+      vcarry += __shfl(incl, 63, 64);
+      if (in && !bad && vo + len <= (long long)d.vlen) {
+        uint64_t bits = 0;
+        for (int b = 0; b < len; b++) bits = (bits << 8) | v[vo + b];
+        double x = 0.0;
+        decode_value(bits, len, fl, x);
+        if (val2 && w == 2 && (flags & ROW_QW_MASK) == 2 && !fl && len <= 2)
+          reinterpret_cast<int16_t*>(val2 + d.qoff)[i] = (int16_t)(long long)x;
+        if (isnan(x)) hasnan = true;
+        if (x == 0.0 && signbit(x)) negz = true;
+        if (!isnan(x)) {
+          const double ax = fabs(x);
+          if (ax > amax || isinf(ax)) amax = fmax(amax, ax);
+          if (x != 0.0 && !isinf(x)) lsbmin = min(lsbmin, lsb_exp(x));
+        }
+      }
+    }
+    if (vcarry > (long long)d.vlen) bad = true;
+    bad = __any(bad);
+    allf = __all(allf);
+    alli = __all(alli);
+    vmax2 = __all(vmax2);
+    hasnan = __any(hasnan);
+    negz = __any(negz);
+    unsorted = __any(unsorted);
+    lsbmin = wave_min(lsbmin);
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) amax = fmax(amax, __shfl_xor(amax, dd, 64));
+    if (lane == 0) {
+      if (bad) {
+        flags |= ROW_ERR;
+        set_err(err, TSDB_E_ILLEGAL_DATA);
+      }
+      if (allf) flags |= ROW_ALLF;
+      if (alli) flags |= ROW_ALLI;
+      if (vmax2) flags |= ROW_VLE2;
+      if (hasnan) flags |= ROW_NAN;
+      if (negz) flags |= ROW_NEGZ;
+      if (unsorted) flags |= ROW_UNSORTED;
+      flags |= d.flags & ROW_SFIRST;
+      d.ndp = ndp;
+      d.flags = flags;
+      d.lsb = lsbmin;
+      d.absmax = amax;
+      rows[r] = d;
+    }
+  }
+}
+
+
+// ---- classes ----------------------------------------------------------------------------
+__host__ __device__ constexpr int idx_cls(int qw, int L) {
+  return 1 + (qw == 4 ? 5 : 0) + (L == 0 ? 0 : L == 1 ? 1 : L == 2 ? 2 : L == 4 ? 3 : 4);
+}
+
+__global__ __launch_bounds__(256) void k_index_hint(const uint8_t* __restrict__ qual, const RowDesc* __restrict__ rows,
+                                                    int64_t n_rows, uint8_t* __restrict__ hint, uint32_t* cnt) {
+  __shared__ uint32_t h[16];
+  if (threadIdx.x < 16) h[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < n_rows) {
+    const RowDesc& d = rows[r];
+    const uint32_t qlen = d.qlen, vlen = d.vlen;
+    int cls = 0;
+    if (qlen > 0) {
+      const uint32_t w = *reinterpret_cast<const uint32_t*>(qual + d.qoff);   // qoff is 16-B aligned
+      const int qw = (w & 0xF0) == 0xF0 ? 4 : 2;
+      if (qlen % qw == 0) {
+        const uint32_t L = ((w >> (8 * (qw - 1))) & 7) + 1;
+        const uint64_t ndp = qlen / qw;
+        const bool uni = (L == 1 || L == 2 || L == 4 || L == 8) && (uint64_t)vlen == ndp * L + (ndp > 1 ? 1 : 0);
+        cls = idx_cls(qw, uni ? (int)L : 0);
+      }
+    }
+    hint[r] = (uint8_t)cls;
+    atomicAdd(&h[cls], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < IDX_NCLS && h[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], h[threadIdx.x]);
+}
+
+// cursor[c] starts at class c's list offset
+__global__ __launch_bounds__(256) void k_index_scatter(const uint8_t* __restrict__ hint, int64_t n_rows, uint32_t* cursor,
+                                                       int32_t* __restrict__ list) {
+  __shared__ uint32_t h[16], base[16];
+  if (threadIdx.x < 16) h[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int cls = 0;
+  uint32_t local = 0;
+  if (r < n_rows) {
+    cls = hint[r];
+    local = atomicAdd(&h[cls], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < IDX_NCLS && h[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], h[threadIdx.x]);
+  __syncthreads();
+  if (r < n_rows && cls) list[base[cls] + local] = (int32_t)r;
+}
+
+struct IdxRow {          // wave-uniform row state
+  int64_t r;
+  uint64_t qoff, voff;
+  uint32_t qlen, vlen, flags_in, ndp;
+};
+
+template <int QW>
+__device__ __forceinline__ IdxRow idx_row(const RowDesc* __restrict__ rows, int64_t r) {
+  IdxRow w;
+  const RowDesc& d = rows[r];
+  w.r = r;
+  w.qoff = d.qoff;
+  w.voff = d.voff;
+  w.qlen = d.qlen;
+  w.vlen = d.vlen;
+  w.flags_in = d.flags;
+  w.ndp = w.qlen / QW;
+  return w;
+}
+
+template <int QW, int L>
+struct IdxLd {           // one chunk's loads
+  uint4 q[QW / 2];
+  uint4 v[L <= 2 ? 1 : L / 2];
+};
+
+// Chunk c's loads: the same for every lane and every chunk (lanes past the row's datapoints
+// re-read its start; the variable class always loads a 16-B slice of the first 1 KB).
+template <int QW, int L>
+__device__ __forceinline__ void idx_issue(const uint8_t* __restrict__ qual, const uint8_t* __restrict__ val,
+                                          const IdxRow& w, uint32_t c, IdxLd<QW, L>& ld) {
+  const int lane = lane_id();
+  int64_t i = (int64_t)c * CH + (int64_t)lane * DPL;
+  if (i >= (int64_t)w.ndp) i = 0;
+  const uint4* q = reinterpret_cast<const uint4*>(qual + w.qoff + i * QW);
+#pragma unroll
+  for (int k = 0; k < QW / 2; k++) ld.q[k] = q[k];
+  const uint8_t* v = val + w.voff;
+  if (L == 0) {
+    ld.v[0] = *reinterpret_cast<const uint4*>(v + ((uint32_t)lane * 16 < w.vlen ? lane * 16 : 0));
+  } else if (L == 1) {
+    const uint2 t = *reinterpret_cast<const uint2*>(v + i);
+    ld.v[0] = make_uint4(t.x, t.y, 0, 0);
+  } else {
+    const uint4* p = reinterpret_cast<const uint4*>(v + i * L);
+#pragma unroll
+    for (int k = 0; k < (L <= 2 ? 1 : L / 2); k++) ld.v[k] = p[k];
+  }
+}
+
+// value statistics in the integer domain (bit patterns / magnitudes), one conversion per
+// chunk: NaN, -0.0, max |x| (Inf included, NaN excluded), least significant set bit
+__device__ __forceinline__ void idx_stats(IdxAcc& a, const uint32_t qq[DPL], const int len[DPL], const uint64_t be[DPL],
+                                          int nin, int64_t vo, uint32_t vlen) {
+  uint32_t fmax_bits = 0;      // float32 |x| bits
+  uint64_t dmax_bits = 0;      // float64 |x| bits
+  uint64_t imax = 0;           // |long|
+  int64_t o = vo;
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    if (j < nin && o + len[j] <= (int64_t)vlen) {
+      const uint64_t b = be[j];
+      if (qq[j] & 8) {
+        if (len[j] == 4) {
+          const uint32_t ab = (uint32_t)b & 0x7FFFFFFFu;
+          if (ab > 0x7F800000u) {
+            a.nan = true;
+          } else {
+            a.negz |= (uint32_t)b == 0x80000000u;
+            fmax_bits = max(fmax_bits, ab);
+            const uint32_t E = ab >> 23, M = ab & 0x7FFFFFu;
+            if (ab != 0 && E != 0xFF) a.lsb = min(a.lsb, E == 0 ? -149 + __ffs(M) - 1 : (int)E - 150 + __ffs(M | 0x800000u) - 1);
+          }
+        } else if (len[j] == 8) {
+          const uint64_t ab = b & 0x7FFFFFFFFFFFFFFFULL;
+          if (ab > 0x7FF0000000000000ULL) {
+            a.nan = true;
+          } else {
+            a.negz |= b == 0x8000000000000000ULL;
+            dmax_bits = ab > dmax_bits ? ab : dmax_bits;
+            const uint32_t E = (uint32_t)(ab >> 52);
+            const uint64_t M = ab & 0xFFFFFFFFFFFFFULL;
+            if (ab != 0 && E != 0x7FF)
+              a.lsb = min(a.lsb, E == 0 ? -1074 + __ffsll((long long)M) - 1
+                                        : (int)E - 1075 + __ffsll((long long)(M | 0x10000000000000ULL)) - 1);
+          }
+        }
+      } else {
+        const int sh = 64 - 8 * len[j];   // sign-extended integer of len bytes
+        const int64_t x = (int64_t)(b << sh) >> sh;
+        const uint64_t ax = x < 0 ? (uint64_t)0 - (uint64_t)x : (uint64_t)x;
+        imax = ax > imax ? ax : imax;
+        if (ax != 0) a.lsb = min(a.lsb, ax <= (1ULL << 53) ? __ffsll((long long)ax) - 1 : lsb_exp((double)x));
+      }
+    }
+    o += len[j];
+  }
+  a.amax = fmax(a.amax, fmax(fmax((double)__uint_as_float(fmax_bits), __longlong_as_double((long long)dmax_bits)),
+                             (double)imax));
+}
+
+// The row's offset order (Internal.compareQualifiers order of a compacted cell: strictly
+// increasing), lane-local then across lanes and chunks.
+__device__ __forceinline__ void idx_order(const int off[DPL], int nin, int64_t i0, const IdxRow& w, int& prev_off,
+                                          IdxAcc& a) {
+  const int lane = lane_id();
+  bool uns = false;
+#pragma unroll
+  for (int j = 1; j < DPL; j++) uns |= (j < nin) & (off[j] <= off[j - 1]);
+  const int last = off[max(0, nin - 1)];
+  int pl = __shfl_up(last, 1, 64);
+  if (lane == 0) pl = prev_off;
+  uns |= (nin > 0) & (off[0] <= pl);
+  a.unsorted |= uns;
+  prev_off = __shfl(last, (int)((min((int64_t)CH, (int64_t)w.ndp - i0) - 1) / DPL), 64);
+}
+
+// int16 copy of the lane's 8 values (1-2-byte integers; other lanes' slots are never read:
+// val2 is consulted only for rows whose every value is a 1-2-byte integer)
+__device__ __forceinline__ void idx_val2(uint8_t* __restrict__ val2, const IdxRow& w, int64_t i, const int len[DPL],
+                                         const uint32_t lo[DPL]) {
+  uint32_t h[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t x0 = len[2 * k] == 1 ? (uint32_t)(int32_t)(int8_t)(lo[2 * k] & 0xFF) : lo[2 * k];
+    const uint32_t x1 = len[2 * k + 1] == 1 ? (uint32_t)(int32_t)(int8_t)(lo[2 * k + 1] & 0xFF) : lo[2 * k + 1];
+    h[k] = (x0 & 0xFFFF) | (x1 << 16);
+  }
+  *reinterpret_cast<uint4*>(val2 + w.qoff + 2 * i) = make_uint4(h[0], h[1], h[2], h[3]);
+}
+
+// Statistics of the lane's integer values (sign-extended from len bytes), branch-free.
+__device__ __forceinline__ void idx_int_stats(IdxAcc& a, const uint64_t be[DPL], const int len[DPL], int nin) {
+  uint64_t imax = 0;
+  int lsb = INT32_MAX;
+  bool big = false;
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    const int sh = 64 - 8 * max(1, len[j]);
+    const int64_t x = (int64_t)(be[j] << sh) >> sh;
+    const uint64_t ax = x < 0 ? (uint64_t)0 - (uint64_t)x : (uint64_t)x;
+    const bool ok = (j < nin) & (ax != 0);
+    imax = ok && ax > imax ? ax : imax;
+    lsb = min(lsb, ok ? (int)__builtin_ctzll(ax) : INT32_MAX);
+    big |= ok & (ax > (1ULL << 53));
+  }
+  if (big) {   // |x| > 2^53: the double rounds, take its least significant bit
+    lsb = INT32_MAX;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      const int sh = 64 - 8 * max(1, len[j]);
+      const int64_t x = (int64_t)(be[j] << sh) >> sh;
+      if (j < nin && x != 0) lsb = min(lsb, lsb_exp((double)x));
+    }
+  }
+  a.lsb = min(a.lsb, lsb);
+  a.amax = fmax(a.amax, (double)imax);
+}
+
+// Chunk decode of the variable-length class: wave prefix sum of the lengths, the chunk's
+// value bytes staged in LDS (the first 1 KB from the prefetch; never past the row's
+// 16-B-aligned extent).  false: a qualifier of the other width -> the generic path.
+template <int QW, bool V2>
+__device__ __forceinline__ bool idx_chunk_var(const uint8_t* __restrict__ val, uint8_t* __restrict__ val2,
+                                              const IdxRow& w, uint32_t c, const IdxLd<QW, 0>& ld, uint32_t* stage,
+                                              int64_t& carry, int& prev_off, IdxAcc& a) {
+  const int lane = lane_id();
+  const int64_t i0 = (int64_t)c * CH;
+  const int nin = (int)min((int64_t)DPL, max((int64_t)0, (int64_t)w.ndp - i0 - (int64_t)lane * DPL));
+  uint32_t qq[DPL];
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    const uint32_t* ws = &ld.q[0].x;
+    if (QW == 2) {
+      const uint32_t b = __builtin_bswap32(ws[j >> 1]);
+      qq[j] = (j & 1) ? (b & 0xFFFF) : (b >> 16);
+    } else {
+      qq[j] = __builtin_bswap32(ws[j]);
+    }
+  }
+  bool fail = false, bad = false, vmax2 = true;
+  uint32_t fl_or = 0, fl_and = 8;
+  int len[DPL], off[DPL];
+  int lsum = 0, lmin = 99, lmax = -1;
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    const bool in = j < nin;
+    fail |= in & (QW == 2 ? (qq[j] >> 12) == 0xF : (qq[j] >> 28) != 0xF);
+    len[j] = in ? (int)(qq[j] & 7) + 1 : 0;
+    lsum += len[j];
+    const uint32_t f = qq[j] & 8;
+    fl_or |= in ? f : 0u;
+    fl_and &= in ? f : 8u;
+    lmin = min(lmin, in ? len[j] : 99);
+    lmax = max(lmax, len[j] - (in ? 0 : 1));
+    vmax2 &= len[j] <= 2;
+    bad |= in & (f ? (len[j] != 4 && len[j] != 8) : (len[j] == 3 || (len[j] >= 5 && len[j] <= 7)));
+    off[j] = QW == 2 ? (int)(qq[j] >> 4) * 1000 : (int)((qq[j] & 0x0FFFFFC0u) >> 6);
+  }
+  if (__any(fail)) return false;
+  a.allf &= fl_and != 0;
+  a.alli &= fl_or == 0;
+  a.vmax2 &= vmax2;
+  a.bad |= bad;
+  a.lmin = min(a.lmin, lmin);
+  a.lmax = max(a.lmax, lmax);
+  idx_order(off, nin, i0, w, prev_off, a);
+  // stage the chunk's value bytes
+  const uint8_t* v = val + w.voff;
+  const int incl = wave_incl_sum_dpp(lsum);
+  const int total = __builtin_amdgcn_readlane(incl, 63);
+  const int64_t a0 = carry & ~(int64_t)15;
+  const int lead = (int)(carry - a0);
+  const int64_t vlen16 = ((int64_t)w.vlen + 15) & ~(int64_t)15;
+  const int64_t nst = min((int64_t)(lead + total + 15) & ~(int64_t)15, vlen16 - a0);
+  WAVE_SYNC();
+  int64_t o0 = 0;
+  if (c == 0) {   // the prefetched first 1 KB
+    if ((int64_t)lane * 16 < nst) *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(stage) + lane * 16) = ld.v[0];
+    o0 = 64 * 16;
+  }
+  for (int64_t o = o0 + (int64_t)lane * 16; o < nst; o += 64 * 16)
+    *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(stage) + o) = *reinterpret_cast<const uint4*>(v + a0 + o);
+  WAVE_SYNC();
+  uint64_t be[DPL];
+  int b = lead + incl - lsum;
+  const int64_t vo = carry + incl - lsum;
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    const bool ok = (j < nin) & (b + len[j] <= nst);
+    const uint64_t raw = __builtin_bswap64(stage_u64(stage, min(b, IDX_STAGE - 12)));
+    be[j] = ok ? raw >> (64 - 8 * max(1, len[j])) : 0;
+    b += len[j];
+  }
+  if (V2 && nin > 0) {
+    uint32_t lo[DPL];
+#pragma unroll
+    for (int j = 0; j < DPL; j++) lo[j] = (uint32_t)be[j];
+    idx_val2(val2, w, i0 + (int64_t)lane * DPL, len, lo);
+  }
+  if (__all(fl_or == 0)) idx_int_stats(a, be, len, nin);
+  else idx_stats(a, qq, len, be, nin, vo, w.vlen);
+  carry += total;
+  return true;
+}
+
+// Branch-free chunk decode of a uniform class (every length == L): per-datapoint conditions
+// are selects, not branches, and the value statistics take the float32-only / integer-only
+// fast path when the wave's chunk allows.  false: the class hypothesis failed.
+template <int QW, int L, bool V2>
+__device__ __forceinline__ bool idx_chunk_uni(uint8_t* __restrict__ val2, const IdxRow& w, uint32_t c,
+                                              const IdxLd<QW, L>& ld, int& prev_off, IdxAcc& a) {
+  const int lane = lane_id();
+  const int64_t i0 = (int64_t)c * CH;
+  const int nin = (int)min((int64_t)DPL, max((int64_t)0, (int64_t)w.ndp - i0 - (int64_t)lane * DPL));
+  uint32_t qq[DPL];
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    const uint32_t* ws = &ld.q[0].x;
+    if (QW == 2) {
+      const uint32_t b = __builtin_bswap32(ws[j >> 1]);
+      qq[j] = (j & 1) ? (b & 0xFFFF) : (b >> 16);
+    } else {
+      qq[j] = __builtin_bswap32(ws[j]);
+    }
+  }
+  bool fail = false;
+  uint32_t fl_or = 0, fl_and = 8;
+  int off[DPL];
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    const bool in = j < nin;
+    const bool ww = QW == 2 ? (qq[j] >> 12) == 0xF : (qq[j] >> 28) != 0xF;
+    fail |= in & (ww | ((qq[j] & 7) != (uint32_t)(L - 1)));
+    const uint32_t f = qq[j] & 8;
+    fl_or |= in ? f : 0u;
+    fl_and &= in ? f : 8u;
+    off[j] = QW == 2 ? (int)(qq[j] >> 4) * 1000 : (int)((qq[j] & 0x0FFFFFC0u) >> 6);
+  }
+  if (__any(fail)) return false;
+  a.allf &= fl_and != 0;
+  a.alli &= fl_or == 0;
+  if (L <= 2) a.bad |= fl_or != 0;   // a float of 1 or 2 bytes
+  idx_order(off, nin, i0, w, prev_off, a);
+  const uint32_t* vw = &ld.v[0].x;
+  int len[DPL];
+#pragma unroll
+  for (int j = 0; j < DPL; j++) len[j] = L;
+  if (L == 8) {
+    uint64_t be[DPL];
+#pragma unroll
+    for (int j = 0; j < DPL; j++) be[j] = ((uint64_t)__builtin_bswap32(vw[2 * j]) << 32) | __builtin_bswap32(vw[2 * j + 1]);
+    if (__all(fl_or == 0)) idx_int_stats(a, be, len, nin);
+    else idx_stats(a, qq, len, be, nin, 0, 0xFFFFFFFFu);
+    return true;
+  }
+  uint32_t be[DPL];
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    if (L == 1) be[j] = (vw[j >> 2] >> ((j & 3) * 8)) & 0xFF;
+    else if (L == 2) { const uint32_t b = __builtin_bswap32(vw[j >> 1]); be[j] = (j & 1) ? (b & 0xFFFF) : (b >> 16); }
+    else be[j] = __builtin_bswap32(vw[j]);
+  }
+  if (V2 && QW == 2 && L <= 2 && nin > 0) idx_val2(val2, w, i0 + (int64_t)lane * DPL, len, be);
+  if (L == 4 && __all(fl_and != 0)) {
+    // every value of the chunk float32: bit-pattern statistics
+    uint32_t fmax_bits = 0;
+    bool nan = false, negz = false;
+    int lsb = INT32_MAX;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      const bool in = j < nin;
+      const uint32_t ab = be[j] & 0x7FFFFFFFu;
+      const bool isn = ab > 0x7F800000u;
+      const bool ok = in & !isn;
+      nan |= in & isn;
+      negz |= ok & (be[j] == 0x80000000u);
+      fmax_bits = max(fmax_bits, ok ? ab : 0u);
+      const uint32_t E = ab >> 23, M = ab & 0x7FFFFFu;
+      const int lj = E == 0 ? (int)__builtin_ctz(M | 0x80000000u) - 149 : (int)E - 150 + (int)__builtin_ctz(M | 0x800000u);
+      lsb = min(lsb, (ok & (ab != 0) & (E != 0xFF)) ? lj : INT32_MAX);
+    }
+    a.nan |= nan;
+    a.negz |= negz;
+    a.lsb = min(a.lsb, lsb);
+    a.amax = fmax(a.amax, (double)__uint_as_float(fmax_bits));
+    return true;
+  }
+  if (__all(fl_or == 0)) {
+    // integers of L <= 4 bytes: magnitude and trailing zeros (|x| <= 2^31: exact as doubles)
+    uint32_t imax = 0;
+    int lsb = INT32_MAX;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      const int sh = 32 - 8 * L;
+      const int32_t x = L == 4 ? (int32_t)be[j] : (int32_t)(be[j] << (sh & 31)) >> (sh & 31);
+      const uint32_t ax = x < 0 ? 0u - (uint32_t)x : (uint32_t)x;
+      const bool ok = (j < nin) & (ax != 0);
+      imax = max(imax, ok ? ax : 0u);
+      lsb = min(lsb, ok ? (int)__builtin_ctz(ax) : INT32_MAX);
+    }
+    a.lsb = min(a.lsb, lsb);
+    a.amax = fmax(a.amax, (double)imax);
+    return true;
+  }
+  // integers and floats mixed in the chunk
+  uint64_t be64[DPL];
+#pragma unroll
+  for (int j = 0; j < DPL; j++) be64[j] = be[j];
+  idx_stats(a, qq, len, be64, nin, 0, 0xFFFFFFFFu);
+  return true;
+}
+
+// One wave per row of class (QW, L) (grid-stride over the class list); V2: also write the
+// int16 copy of 1-2-byte integers (2-byte-qualifier integer classes, when val2 is allocated).
+// Rows whose hypothesis fails get hint 0 (k_index_generic).
+template <int QW, int L, bool V2>
+__global__ __launch_bounds__(256) void k_index_cls(const uint8_t* __restrict__ qual, const uint8_t* __restrict__ val,
+                                                   uint8_t* __restrict__ val2, RowDesc* __restrict__ rows,
+                                                   uint8_t* __restrict__ hint, const int32_t* __restrict__ list,
+                                                   int64_t n, int32_t* err) {
+  __shared__ uint32_t stage_all[4][L == 0 ? IDX_STAGE / 4 : 1];
+  const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t* stage = stage_all[wv];
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  int64_t i = (int64_t)blockIdx.x * 4 + wv;
+  if (i >= n) return;
+  IdxRow cur = idx_row<QW>(rows, list[i]);
+  IdxRow nxt = i + nw < n ? idx_row<QW>(rows, list[i + nw]) : cur;
+  IdxLd<QW, L> ld;
+  idx_issue<QW, L>(qual, val, cur, 0, ld);
+  for (;;) {
+    const bool has_next = i + nw < n;
+    const IdxRow nxt2 = i + 2 * nw < n ? idx_row<QW>(rows, list[i + 2 * nw]) : nxt;
+    IdxAcc a;
+    idx_acc_init(a);
+    int64_t carry = 0;
+    int prev_off = -1;
+    bool ok = true;
+    const uint32_t nch = (cur.ndp + CH - 1) / CH;
+    for (uint32_t c = 0; c < nch; c++) {
+      IdxLd<QW, L> nl;
+      idx_issue<QW, L>(qual, val, c + 1 < nch ? cur : nxt, c + 1 < nch ? c + 1 : 0, nl);
+      if (ok) {
+        if constexpr (L != 0) ok = idx_chunk_uni<QW, L, V2>(val2, cur, c, ld, prev_off, a);
+        else ok = idx_chunk_var<QW, V2>(val, val2, cur, c, ld, stage, carry, prev_off, a);
+      }
+      ld = nl;
+    }
+    if (!ok) {
+      if (lane == 0) hint[cur.r] = 0;   // k_index_generic takes the row
+    } else {
+      if (L == 0 && carry > (int64_t)cur.vlen) a.bad = true;   // (uniform classes: vlen matches by construction)
+      const bool bad = __any(a.bad);
+      const bool allf = __all(a.allf), alli = __all(a.alli);
+      const bool vmax2 = L != 0 ? L <= 2 : __all(a.vmax2);
+      const bool hasnan = __any(a.nan), negz = __any(a.negz), unsorted = __any(a.unsorted);
+      const int lsbmin = wave_min(a.lsb);
+      const int lmin = L != 0 ? L : wave_min(a.lmin), lmax = L != 0 ? L : wave_max(a.lmax);
+      double amax = a.amax;
+#pragma unroll
+      for (int dd = 32; dd >= 1; dd >>= 1) amax = fmax(amax, __shfl_xor(amax, dd, 64));
+      if (lane == 0) {
+        uint32_t flags = (uint32_t)QW;
+        if (lmin == lmax) flags |= (uint32_t)lmin << ROW_VL_SHIFT;
+        if (bad) {
+          flags |= ROW_ERR;
+          set_err(err, TSDB_E_ILLEGAL_DATA);
+        }
+        if (allf) flags |= ROW_ALLF;
+        if (alli) flags |= ROW_ALLI;
+        if (vmax2) flags |= ROW_VLE2;
+        if (hasnan) flags |= ROW_NAN;
+        if (negz) flags |= ROW_NEGZ;
+        if (unsorted) flags |= ROW_UNSORTED;
+        flags |= cur.flags_in & ROW_SFIRST;
+        RowDesc& o = rows[cur.r];
+        o.ndp = cur.ndp;
+        o.flags = flags;
+        o.lsb = lsbmin;
+        o.absmax = amax;
+      }
+    }
+    if (!has_next) break;
+    i += nw;
+    cur = nxt;
+    nxt = nxt2;
+  }
+}
+
+// Rows of class 0 (hint 0), or every row (all = 1: test hook), through the sequential path.
+// A wave scans 64 hints at a time and walks the rows its ballot selects.
+__global__ __launch_bounds__(256) void k_index_generic(const uint8_t* __restrict__ qual, const uint8_t* __restrict__ val,
+                                                       uint8_t* __restrict__ val2, RowDesc* __restrict__ rows,
+                                                       const uint8_t* __restrict__ hint, int64_t n_rows, int32_t* err,
+                                                       int all) {
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int lane = lane_id();
+  for (int64_t r0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64; r0 < n_rows; r0 += nw * 64) {
+    const int64_t r = r0 + lane;
+    uint64_t m = __ballot(r < n_rows && (all || hint[r] == 0));
+    while (m) {
+      const int l = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      index_row_generic(qual, val, val2, rows, r0 + l, err);
+    }
+  }
+}
+
+template <int QW, int L>
+static hipError_t launch_cls(const uint8_t* qual, const uint8_t* val, uint8_t* val2, RowDesc* rows, const IndexBufs& b,
+                             const uint32_t* off, const uint32_t* cnt, int32_t* err, hipStream_t s) {
+  const int c = idx_cls(QW, L);
+  if (!cnt[c]) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>(((int64_t)cnt[c] + 3) / 4, 8192);
+  if (QW == 2 && L <= 2 && val2)
+    hipLaunchKernelGGL((k_index_cls<QW, L, true>), dim3((unsigned)blocks), dim3(256), 0, s, qual, val, val2, rows,
+                       b.hint, b.list + off[c], (int64_t)cnt[c], err);
+  else
+    hipLaunchKernelGGL((k_index_cls<QW, L, false>), dim3((unsigned)blocks), dim3(256), 0, s, qual, val, val2, rows,
+                       b.hint, b.list + off[c], (int64_t)cnt[c], err);
+  return hipGetLastError();
+}
+
+hipError_t index_classes(const uint8_t* qual, const RowDesc* rows, const IndexBufs& b, int64_t n_rows,
+                         IndexClasses* out, hipStream_t s) {
+  *out = IndexClasses{};
+  if (n_rows == 0) return hipSuccess;
+  if (n_rows > 0x7FFFFFFFLL) return hipErrorInvalidValue;   // int32 row lists
+  hipError_t e;
+  const unsigned tb = (unsigned)((n_rows + 255) / 256);
+  if ((e = hipMemsetAsync(b.cnt, 0, 16 * 4, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_index_hint, dim3(tb), dim3(256), 0, s, qual, rows, n_rows, b.hint, b.cnt);
+  uint32_t cnt[16] = {}, cur[16] = {};
+  if ((e = hipMemcpyAsync(cnt, b.cnt, 16 * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+  for (int c = 0; c < 16; c++) out->cnt[c] = cnt[c];
+  for (int c = 2; c < IDX_NCLS; c++) out->off[c] = out->off[c - 1] + cnt[c - 1];
+  for (int c = 0; c < 16; c++) cur[c] = out->off[c];
+  if ((e = hipMemcpyAsync(b.cnt, cur, 16 * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_index_scatter, dim3(tb), dim3(256), 0, s, b.hint, n_rows, b.cnt, b.list);
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;   // `cur` leaves scope
+  out->vle_capable = cnt[idx_cls(2, 0)] + cnt[idx_cls(2, 1)] + cnt[idx_cls(2, 2)];
+  return hipGetLastError();
+}
+
+hipError_t index_rows(const uint8_t* qual, const uint8_t* val, uint8_t* val2, RowDesc* rows, const IndexBufs& b,
+                      const IndexClasses& k, int64_t n_rows, int32_t* err, bool generic, hipStream_t s) {
+  if (n_rows == 0) return hipSuccess;
+  const int64_t gblocks = std::min<int64_t>((n_rows + 3) / 4, 16384);
+  if (generic) {
+    hipLaunchKernelGGL(k_index_generic, dim3((unsigned)gblocks), dim3(256), 0, s, qual, val, val2, rows, b.hint, n_rows,
+                       err, 1);
+    return hipGetLastError();
+  }
+  hipError_t e;
+#define IDX_CLS(Q, LL) if ((e = launch_cls<Q, LL>(qual, val, val2, rows, b, k.off, k.cnt, err, s)) != hipSuccess) return e;
+  IDX_CLS(2, 0) IDX_CLS(2, 1) IDX_CLS(2, 2) IDX_CLS(2, 4) IDX_CLS(2, 8)
+  IDX_CLS(4, 0) IDX_CLS(4, 1) IDX_CLS(4, 2) IDX_CLS(4, 4) IDX_CLS(4, 8)
+#undef IDX_CLS
+  hipLaunchKernelGGL(k_index_generic, dim3((unsigned)std::min<int64_t>(gblocks, 4096)), dim3(256), 0, s, qual, val,
+                     nullptr, rows, b.hint, n_rows, err, 0);
+  return hipGetLastError();
+}
+
+}  // namespace tsdb
