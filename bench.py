@@ -40,6 +40,9 @@ def parse():
     ap.add_argument("--ds", default="avg")
     ap.add_argument("--agg", default="sum")
     ap.add_argument("--value-kind", type=int, default=0)
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: --series per GPU (each rank its own store); strong: --series in total, one global "
+                         "store split over the ranks (tsdbhip_synth_shard), e.g. config 3's 10M series 1/2/4/8 ways")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH/WRITE_SIZE child passes")
@@ -56,7 +59,7 @@ def cpu_baseline(args, target_s: float):
     from opentsdb_amd import abi, synth
     n = 256
     b = synth.generate(n, T0, args.points, args.period_ms, value_kind=args.value_kind,
-                       n_groups=min(args.groups, n), seed=0x5EED)
+                       n_groups=min(args.groups, n), int_mod=30000 if args.value_kind == 2 else 2000, seed=0x5EED)
     q = query(args)
 
     def timed(threads, budget):
@@ -135,11 +138,14 @@ def pmc_traffic(args, kernel_prefix: str):
 
 def workload_label(args) -> str:
     kind = {0: "float32", 1: "vle int", 2: "int/float32 alternating"}.get(args.value_kind, "?")
-    label = (f"{args.agg}:{args.interval}-{args.ds} group-by {args.groups} groups over {args.series} series/GPU x "
+    per = "series/GPU" if args.scaling == "weak" else "series in total (strong scaling)"
+    label = (f"{args.agg}:{args.interval}-{args.ds} group-by {args.groups} groups over {args.series} {per} x "
              f"{args.points} dp @{args.period_ms} ms ({kind})")
-    if (args.series, args.points, args.period_ms, args.groups, args.interval, args.ds, args.agg, args.value_kind) == \
-            (1_000_000, 3600, 1000, 64, "1m", "avg", "sum", 0):
+    shape = (args.series, args.points, args.period_ms, args.groups, args.interval, args.ds, args.agg, args.value_kind)
+    if shape == (1_000_000, 3600, 1000, 64, "1m", "avg", "sum", 0) and args.scaling == "weak":
         label += " -- BASELINE config 2"
+    elif shape[:4] == (10_000_000, 360, 10000, 1000) and args.value_kind == 2 and args.scaling == "strong":
+        label += " -- BASELINE config 3 (1 h window)"
     return label
 
 
@@ -168,8 +174,15 @@ def main():
 
     eng = Engine(local_rank)
     t_gen = time.perf_counter()
-    eng.synth(args.series, T0, args.points, args.period_ms, args.value_kind, args.groups, 2000,
-              0x5EED ^ (rank * 0x9E3779B97F4A7C15 & 0xFFFFFFFFFFFFFFFF))
+    int_mod = 30000 if args.value_kind == 2 else 2000
+    if args.scaling == "strong":
+        from opentsdb_amd.dist import synth_bounds
+        b = synth_bounds(args.series, world)
+        eng.synth_shard(b[rank], b[rank + 1], args.series, T0, args.points, args.period_ms, args.value_kind,
+                        args.groups, int_mod, 0x5EED)
+    else:
+        eng.synth(args.series, T0, args.points, args.period_ms, args.value_kind, args.groups, int_mod,
+                  0x5EED ^ (rank * 0x9E3779B97F4A7C15 & 0xFFFFFFFFFFFFFFFF))
     eng.sync()
     t_gen = time.perf_counter() - t_gen
     index_ms = eng.timing().index_ms   # k_index at load (row classification / validation)
@@ -217,7 +230,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed * 1000.0 / args.steps
-    dps_step = tm.datapoints * world
+    if dist is not None:   # datapoints of every rank's shard
+        import torch
+        t = torch.tensor([tm.datapoints], dtype=torch.int64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t)
+        dps_step = int(t.item())
+    else:
+        dps_step = tm.datapoints
     value = dps_step / (ms_per_step / 1000.0)
     # dominant kernel: the streaming kernel k_fast when the batch's row class allows it
     # (every tile handed back to k_grid otherwise); hipEvents on the engine stream
@@ -242,7 +261,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded splitmix64, generated in HBM with the MockBase cell encoding)",
@@ -252,7 +271,7 @@ def main():
                          "brings freshly scanned cells",
             "config": {
                 "workload": workload_label(args),
-                "series_per_gpu": args.series,
+                "series_per_gpu": args.series if args.scaling == "weak" else args.series / world,
                 "datapoints_per_gpu": tm.datapoints,
                 "groups": args.groups,
                 "parallelism": f"series-sharded x{world}",

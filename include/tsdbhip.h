@@ -85,7 +85,8 @@ typedef struct {
   const uint64_t* row_val_off;     /* [n_rows + 1] */
   const uint8_t* qual;             /* [row_qual_off[n_rows]] */
   const uint8_t* val;              /* [row_val_off[n_rows]] */
-  const int32_t* group_id;         /* [n_series]; -1 drops the series (no matching group-by tag) */
+  const int32_t* group_id;         /* [n_series]; -1: no matching group-by tag -- dropped by group-by
+                                      aggregators, still emitted by NONE (TsdbQuery.java:940-961) */
 } tsdbhip_batch;
 
 /* ---- Query: TsdbQuery state that reaches the aggregation path ------------- */
@@ -171,6 +172,19 @@ int tsdbhip_init(int device, tsdbhip_ctx** out);
 void tsdbhip_destroy(tsdbhip_ctx* ctx);
 /* Copy a host batch into HBM (re-laid out: rows 16-B aligned).  Replaces any previous batch. */
 int tsdbhip_load(tsdbhip_ctx* ctx, const tsdbhip_batch* host_batch);
+/* ---- sharding one query's spans over ranks -------------------------
+ * Byte-balanced contiguous shards, one per rank; bounds[world + 1], rank r owns
+ * [bounds[r], bounds[r + 1]) of:
+ *   TSDB_SHARD_SERIES  positions in SpanGroup order (kept series stably sorted by group id):
+ *                      a group may straddle ranks (tsdbhip_run_partials, tsdbhip_sel_*);
+ *   TSDB_SHARD_GROUPS  group ids: whole SpanGroups per rank (raw queries, no downsampler);
+ *   TSDB_SHARD_SPANS   series positions in batch order, every span (NONE aggregator: it
+ *                      ignores group-by tags, so series with group id -1 count too).
+ * tsdbhip_load_shard loads one such range of a host batch (tsdbhip_load semantics; for
+ * SPANS the shard's batch order is kept, so NONE results concatenate in rank order). */
+enum { TSDB_SHARD_SERIES = 0, TSDB_SHARD_GROUPS = 1, TSDB_SHARD_SPANS = 2 };
+int tsdbhip_shard_bounds(const tsdbhip_batch* batch, int world, int mode, int64_t* bounds);
+int tsdbhip_load_shard(tsdbhip_ctx* ctx, const tsdbhip_batch* batch, int mode, int64_t begin, int64_t end);
 /* Synthetic MockBase-equivalent store generated directly in HBM (see tsdbhip_synth_spec). */
 typedef struct {
   int64_t n_series;
@@ -183,6 +197,9 @@ typedef struct {
   uint64_t seed;
 } tsdbhip_synth_spec;
 int tsdbhip_synth(tsdbhip_ctx* ctx, const tsdbhip_synth_spec* spec);
+/* Batch positions [pos_begin, pos_end) of that store (series in group order): one rank's
+ * contiguous TSDB_SHARD_SERIES shard of the whole store, generated on its own GPU. */
+int tsdbhip_synth_shard(tsdbhip_ctx* ctx, const tsdbhip_synth_spec* spec, int64_t pos_begin, int64_t pos_end);
 /* Copy the resident batch back to host (for parity checks); host arrays sized by tsdbhip_batch_sizes. */
 int tsdbhip_batch_sizes(tsdbhip_ctx* ctx, int64_t* n_series, int64_t* n_rows, uint64_t* qual_bytes, uint64_t* val_bytes);
 int tsdbhip_batch_download(tsdbhip_ctx* ctx, int64_t* series_row_ptr, uint32_t* row_base_time,

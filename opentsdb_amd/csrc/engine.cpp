@@ -249,6 +249,7 @@ struct tsdbhip_ctx {
   // account() cache (invalidated by every load)
   bool acct_valid = false;
   int64_t acct_ss = 0, acct_se = 0, acct_dps = 0, acct_bytes = 0;
+  bool acct_none = false;
   // rollup generation: scratch and the per-function cells of the last tsdbhip_rollup_run
   DevBuf ro_allint, ro_ord, ro_orig, ro_cnt, ro_vsz, ro_coff, ro_voff;
   void* ro_tmp = nullptr;
@@ -669,7 +670,10 @@ static bool merge_cells(std::vector<uint8_t>& lq, std::vector<uint8_t>& lv, cons
   return true;
 }
 
-static int load_impl(tsdbhip_ctx* c, const tsdbhip_batch* b) {
+// Loads series cand[0 .. m) of the batch (all series when cand is null), in that order as the
+// "batch order" of the resident store (NONE results are emitted in it); series are then stably
+// sorted by group (SpanGroup membership, order inside a group kept).
+static int load_impl(tsdbhip_ctx* c, const tsdbhip_batch* b, const std::vector<int64_t>* cand = nullptr) {
   if (!c || !b) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_OK(hipSetDevice(c->device));
@@ -680,14 +684,23 @@ static int load_impl(tsdbhip_ctx* c, const tsdbhip_batch* b) {
   if (b->n_series > 0 && (b->series_row_ptr[0] != 0 || b->series_row_ptr[b->n_series] != b->n_rows))
     return fail(TSDB_E_ILLEGAL_ARGUMENT, "series_row_ptr does not cover the rows");
   release_batch(c);
-  // stable order of series by group (SpanGroup membership; order inside a group kept)
-  std::vector<int64_t> order;
+  const int64_t m = cand ? (int64_t)cand->size() : b->n_series;
+  auto ser = [&](int64_t v) { return cand ? (*cand)[v] : v; };   // virtual batch position -> batch series
+  // stable order of series by group (SpanGroup membership; order inside a group kept).
+  // Series without a group (group id -1: a group-by tag missing) stay resident after the last
+  // group, in batch order, under the sentinel group n_groups: no group-by tile visits them,
+  // but the NONE aggregator emits every span (TsdbQuery.java:940-961).
+  std::vector<int64_t> order;   // virtual positions
   int32_t maxg = -1;
-  for (int64_t s = 0; s < b->n_series; s++) {
+  for (int64_t v = 0; v < m; v++) {
+    const int64_t s = ser(v);
+    if (s < 0 || s >= b->n_series) return fail(TSDB_E_ILLEGAL_ARGUMENT, "series index out of range");
     if (b->series_row_ptr[s + 1] < b->series_row_ptr[s]) return fail(TSDB_E_ILLEGAL_ARGUMENT, "series_row_ptr not monotonic");
-    if (b->group_id[s] >= 0) { order.push_back(s); maxg = std::max(maxg, b->group_id[s]); }
+    order.push_back(v);
+    maxg = std::max(maxg, b->group_id[s]);
   }
-  std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return b->group_id[x] < b->group_id[y]; });
+  auto key = [&](int64_t v) { const int32_t g = b->group_id[ser(v)]; return g < 0 ? INT32_MAX : g; };
+  std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return key(x) < key(y); });
   c->n_series = (int64_t)order.size();
   c->n_groups = maxg + 1;
   c->h_group.resize(c->n_series);
@@ -696,8 +709,8 @@ static int load_impl(tsdbhip_ctx* c, const tsdbhip_batch* b) {
   std::vector<RowDesc> rd;
   uint64_t qtot = 0, vtot = 0;
   for (int64_t i = 0; i < c->n_series; i++) {
-    const int64_t s = order[i];
-    c->h_group[i] = b->group_id[s];
+    const int64_t s = ser(order[i]);
+    c->h_group[i] = b->group_id[s] < 0 ? (int32_t)c->n_groups : b->group_id[s];
     for (int64_t r = b->series_row_ptr[s]; r < b->series_row_ptr[s + 1]; r++) {
       RowDesc d{};
       d.base = b->row_base_time[r];
@@ -730,7 +743,7 @@ static int load_impl(tsdbhip_ctx* c, const tsdbhip_batch* b) {
     // copy rows in the order their offsets were assigned (before the per-series sort)
     uint64_t qo = 0, vo = 0;
     for (int64_t i = 0; i < c->n_series; i++) {
-      const int64_t s = order[i];
+      const int64_t s = ser(order[i]);
       for (int64_t r = b->series_row_ptr[s]; r < b->series_row_ptr[s + 1]; r++) {
         const uint64_t ql = b->row_qual_off[r + 1] - b->row_qual_off[r];
         const uint64_t vl = b->row_val_off[r + 1] - b->row_val_off[r];
@@ -761,7 +774,7 @@ static int load_impl(tsdbhip_ctx* c, const tsdbhip_batch* b) {
 // Span.addRow (src/core/Span.java:177-220): several cells of one series with the same base
 // time (salt-bucket duplicates) merge into one RowSeq (RowSeq.addRow).  Batches without such
 // rows are loaded as given; otherwise the merged batch is built first.
-extern "C" int tsdbhip_load(tsdbhip_ctx* c, const tsdbhip_batch* b) {
+static int load_with(tsdbhip_ctx* c, const tsdbhip_batch* b, const std::vector<int64_t>* cand) {
   if (!c || !b) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   bool dup = false;
   if (b->n_series > 0 && b->n_rows > 0 && b->series_row_ptr && b->row_base_time && b->row_qual_off &&
@@ -775,7 +788,7 @@ extern "C" int tsdbhip_load(tsdbhip_ctx* c, const tsdbhip_batch* b) {
       dup = std::adjacent_find(bases.begin(), bases.end()) != bases.end();
     }
   }
-  if (!dup) return load_impl(c, b);
+  if (!dup) return load_impl(c, b, cand);
   std::vector<int64_t> srp(b->n_series + 1, 0);
   std::vector<uint32_t> base;
   std::vector<uint64_t> qoff{0}, voff{0};
@@ -816,15 +829,104 @@ extern "C" int tsdbhip_load(tsdbhip_ctx* c, const tsdbhip_batch* b) {
   m.row_val_off = voff.data();
   m.qual = qual.data();
   m.val = val.data();
-  return load_impl(c, &m);
+  return load_impl(c, &m, cand);   // series indices are unchanged by the merge
 }
 
-extern "C" int tsdbhip_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp) {
+extern "C" int tsdbhip_load(tsdbhip_ctx* c, const tsdbhip_batch* b) { return load_with(c, b, nullptr); }
+
+// ---- sharding a host batch over ranks ----------------------------------------
+namespace {
+
+// Contiguous byte-balanced split of n weights over `world` parts: bounds[r] = the first index
+// whose cumulative weight reaches r / world of the total (numpy searchsorted 'left' over the
+// cumulative sums), made monotone.
+void balanced_bounds(const std::vector<double>& w, int world, int64_t* bounds) {
+  const int64_t n = (int64_t)w.size();
+  std::vector<double> cum(n + 1, 0.0);
+  for (int64_t i = 0; i < n; i++) cum[i + 1] = cum[i] + w[i];
+  const double total = cum[n];
+  bounds[0] = 0;
+  for (int r = 1; r < world; r++) {
+    int64_t b;
+    if (total > 0) b = std::lower_bound(cum.begin(), cum.end(), total * r / world) - cum.begin();
+    else b = n * r / world;
+    bounds[r] = std::max(b, bounds[r - 1]);
+  }
+  bounds[world] = n;
+}
+
+double series_bytes(const tsdbhip_batch* b, int64_t s) {
+  const int64_t r0 = b->series_row_ptr[s], r1 = b->series_row_ptr[s + 1];
+  return (double)(b->row_qual_off[r1] - b->row_qual_off[r0]) + (double)(b->row_val_off[r1] - b->row_val_off[r0]);
+}
+
+// kept series (group id >= 0) stably sorted by group: SpanGroup order
+std::vector<int64_t> group_order(const tsdbhip_batch* b) {
+  std::vector<int64_t> o;
+  for (int64_t s = 0; s < b->n_series; s++) if (b->group_id[s] >= 0) o.push_back(s);
+  std::stable_sort(o.begin(), o.end(), [&](int64_t x, int64_t y) { return b->group_id[x] < b->group_id[y]; });
+  return o;
+}
+
+int check_batch_arrays(const tsdbhip_batch* b) {
+  if (!b || b->n_series < 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad batch");
+  if (b->n_series > 0 && (!b->series_row_ptr || !b->group_id || !b->row_qual_off || !b->row_val_off))
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, "null batch arrays");
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int tsdbhip_shard_bounds(const tsdbhip_batch* b, int world, int mode, int64_t* bounds) {
+  int rc = check_batch_arrays(b);
+  if (rc) return rc;
+  if (world < 1 || !bounds) return fail(TSDB_E_ILLEGAL_ARGUMENT, "world must be >= 1");
+  std::vector<double> w;
+  if (mode == TSDB_SHARD_SERIES) {
+    for (int64_t s : group_order(b)) w.push_back(series_bytes(b, s));
+  } else if (mode == TSDB_SHARD_GROUPS) {
+    int32_t maxg = -1;
+    for (int64_t s = 0; s < b->n_series; s++) maxg = std::max(maxg, b->group_id[s]);
+    w.assign(maxg + 1, 0.0);
+    for (int64_t s = 0; s < b->n_series; s++) if (b->group_id[s] >= 0) w[b->group_id[s]] += series_bytes(b, s);
+  } else if (mode == TSDB_SHARD_SPANS) {
+    for (int64_t s = 0; s < b->n_series; s++) w.push_back(series_bytes(b, s));   // every span (NONE)
+  } else {
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad shard mode");
+  }
+  balanced_bounds(w, world, bounds);
+  return 0;
+}
+
+extern "C" int tsdbhip_load_shard(tsdbhip_ctx* c, const tsdbhip_batch* b, int mode, int64_t begin, int64_t end) {
+  int rc = check_batch_arrays(b);
+  if (rc) return rc;
+  if (begin < 0 || end < begin) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad shard range");
+  std::vector<int64_t> cand;
+  if (mode == TSDB_SHARD_SERIES) {
+    const std::vector<int64_t> o = group_order(b);
+    if (end > (int64_t)o.size()) return fail(TSDB_E_ILLEGAL_ARGUMENT, "shard range past the series");
+    cand.assign(o.begin() + begin, o.begin() + end);
+  } else if (mode == TSDB_SHARD_GROUPS) {
+    for (int64_t s : group_order(b)) if (b->group_id[s] >= begin && b->group_id[s] < end) cand.push_back(s);
+  } else if (mode == TSDB_SHARD_SPANS) {
+    if (end > b->n_series) return fail(TSDB_E_ILLEGAL_ARGUMENT, "shard range past the series");
+    for (int64_t s = begin; s < end; s++) cand.push_back(s);
+  } else {
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad shard mode");
+  }
+  return load_with(c, b, &cand);
+}
+
+// Batch positions [p0, p1) of the synthetic store (series sorted by group; group g holds
+// global series g, g + G, g + 2G, ...): one GPU's contiguous shard of the whole store.
+static int synth_impl(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp, int64_t p0, int64_t p1) {
   if (!c || !sp) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_OK(hipSetDevice(c->device));
   if (sp->n_series <= 0 || sp->n_points <= 0 || sp->period_ms <= 0 || sp->n_groups <= 0 || sp->start_s < 0)
     return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad synth spec");
+  if (p0 < 0 || p1 > sp->n_series || p0 >= p1) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad synth shard range");
   if (sp->value_kind != 0 && sp->int_mod <= 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "int_mod must be > 0");
   release_batch(c);
   const bool ms_qual = (sp->period_ms % 1000) != 0 || (sp->start_s * 1000) % 1000 != 0;
@@ -845,9 +947,10 @@ extern "C" int tsdbhip_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp) {
     k = e;
   }
   const int64_t R = (int64_t)k0.size();
-  const int64_t S = sp->n_series, G = sp->n_groups;
+  const int64_t SG = sp->n_series, G = sp->n_groups;   // the whole store
+  const int64_t S = p1 - p0;                           // this shard
   std::vector<int64_t> grp_off(G + 1, 0);
-  for (int64_t g = 0; g < G; g++) grp_off[g + 1] = grp_off[g] + S / G + (g < S % G ? 1 : 0);
+  for (int64_t g = 0; g < G; g++) grp_off[g + 1] = grp_off[g] + SG / G + (g < SG % G ? 1 : 0);
   c->n_series = S;
   c->n_rows = S * R;
   c->n_groups = G;
@@ -866,7 +969,7 @@ extern "C" int tsdbhip_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp) {
   HIP_OK(hipMemcpy(d_goff.p, grp_off.data(), (G + 1) * 8, hipMemcpyHostToDevice));
   HIP_OK(c->gid.ensure(S * 4));
   SynthParams p{};
-  p.n_series = S; p.n_groups = G; p.n_rows_per_series = R; p.n_points = sp->n_points;
+  p.n_series = S; p.n_groups = G; p.n_rows_per_series = R; p.n_points = sp->n_points; p.pos0 = p0;
   p.start_ms = start_ms; p.period_ms = sp->period_ms; p.value_kind = sp->value_kind; p.ms_qual = ms_qual;
   p.int_mod = sp->int_mod; p.seed = sp->seed;
   p.grp_off = d_goff.as<int64_t>(); p.row_k0 = d_k0.as<int64_t>(); p.row_n = d_rn.as<int32_t>();
@@ -918,10 +1021,18 @@ extern "C" int tsdbhip_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp) {
   c->h_group.resize(S);
   c->h_orig.resize(S);
   for (int64_t g = 0; g < G; g++)
-    for (int64_t i = grp_off[g]; i < grp_off[g + 1]; i++) c->h_group[i] = (int32_t)g;
+    for (int64_t i = std::max(grp_off[g], p0); i < std::min(grp_off[g + 1], p1); i++) c->h_group[i - p0] = (int32_t)g;
   std::iota(c->h_orig.begin(), c->h_orig.end(), 0);
   HIP_OK(hipStreamSynchronize(c->stream));
   return finish_load(c, rd);
+}
+
+extern "C" int tsdbhip_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp) {
+  return synth_impl(c, sp, 0, sp ? sp->n_series : 0);
+}
+
+extern "C" int tsdbhip_synth_shard(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp, int64_t pos_begin, int64_t pos_end) {
+  return synth_impl(c, sp, pos_begin, pos_end);
 }
 
 extern "C" int tsdbhip_batch_sizes(tsdbhip_ctx* c, int64_t* n_series, int64_t* n_rows, uint64_t* qual_bytes,
@@ -961,7 +1072,7 @@ extern "C" int tsdbhip_batch_download(tsdbhip_ctx* c, int64_t* series_row_ptr, u
   row_qual_off[c->n_rows] = qo;
   row_val_off[c->n_rows] = vo;
   for (int64_t s = 0; s <= c->n_series; s++) series_row_ptr[s] = c->h_srp[s];
-  for (int64_t s = 0; s < c->n_series; s++) group_id[s] = c->h_group[s];
+  for (int64_t s = 0; s < c->n_series; s++) group_id[s] = c->h_group[s] >= c->n_groups ? -1 : c->h_group[s];
   return 0;
 }
 
@@ -1420,13 +1531,14 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
 //                              + 4 B base time + 2 x 8 B CSR offsets;  per series: 4 B group id.
 // Cached per scan range (the batch is resident; the loop is O(rows)).
 void account(tsdbhip_ctx* c, const Plan& P) {
-  if (c->acct_valid && c->acct_ss == P.ss && c->acct_se == P.se) {
+  if (c->acct_valid && c->acct_ss == P.ss && c->acct_se == P.se && c->acct_none == P.none) {
     c->timing.datapoints = c->acct_dps;
     c->timing.bytes = c->acct_bytes;
     return;
   }
   int64_t dps = 0, bytes = 0;
   for (int64_t s = 0; s < c->n_series; s++) {
+    if (!P.none && c->h_group[s] >= c->n_groups) continue;   // ungrouped: only NONE reads it
     bytes += 4;
     for (int64_t r = c->h_srp[s]; r < c->h_srp[s + 1]; r++) {
       if ((int64_t)c->h_base[r] < P.ss || (int64_t)c->h_base[r] >= P.se) continue;
@@ -1435,6 +1547,7 @@ void account(tsdbhip_ctx* c, const Plan& P) {
     }
   }
   c->acct_valid = true;
+  c->acct_none = P.none;
   c->acct_ss = P.ss;
   c->acct_se = P.se;
   c->acct_dps = dps;
@@ -1525,7 +1638,8 @@ std::vector<int64_t> seg_ptr(const std::vector<int64_t>& counts) {
 // local series per group id g < G (resident order is group-sorted)
 std::vector<int64_t> local_counts(tsdbhip_ctx* c, int64_t G) {
   std::vector<int64_t> n(G, 0);
-  for (int64_t s = 0; s < c->n_series; s++) n[c->h_group[s]]++;
+  for (int64_t s = 0; s < c->n_series; s++)
+    if (c->h_group[s] < G) n[c->h_group[s]]++;   // (the sentinel group of ungrouped series is not one)
   return n;
 }
 
@@ -1981,6 +2095,10 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
   c->timing.redo_tiles = 0;
   account(c, P);
   if (err) return fail(err, "error raised by the device path");
+  if (direct && !direct_r) {   // no group chunk ran (an empty shard): an empty result
+    direct_r = make_result(0, 0);
+    if (!direct_r) return fail(TSDB_E_NOMEM, "result allocation");
+  }
   if (direct) {
     auto* gptr = const_cast<int64_t*>(direct_r->group_ptr);
     auto* gid = const_cast<int32_t*>(direct_r->group_id);
@@ -2497,7 +2615,9 @@ extern "C" int tsdbhip_rollup_run(tsdbhip_ctx* c, const tsdbhip_rollup_spec* sp,
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_OK(hipSetDevice(c->device));
   c->ro_n = 0;
-  const int64_t n = c->n_series;
+  // the series with a group (ungrouped ones -- group id -1 -- sit after them and get no rollups)
+  int64_t n = 0;
+  while (n < c->n_series && c->h_group[n] < c->n_groups) n++;
   // batch order -> sorted position, and the per-series integer flag
   {
     std::vector<int64_t> ord(n);

@@ -253,6 +253,7 @@ struct RawParams {
 
 struct SynthParams {
   int64_t n_series, n_groups, n_rows_per_series, n_points;
+  int64_t pos0;                  // global batch position of local series 0 (a shard of the store)
   int64_t start_ms, period_ms;
   int32_t value_kind, ms_qual;
   int64_t int_mod;

@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256) void k_synth_sizes(SynthParams p) {
     const int64_t pos = row / R, h = row % R;
     int64_t i;
     int32_t grp;
-    synth_series(p, pos, i, grp);
+    synth_series(p, p.pos0 + pos, i, grp);   // global batch position of the shard's series
     const int64_t k0 = p.row_k0[h];
     const int n = p.row_n[h];
     long long bytes = 0;
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void k_synth_write(SynthParams p) {
     const int64_t pos = row / R, h = row % R;
     int64_t i;
     int32_t grp;
-    synth_series(p, pos, i, grp);
+    synth_series(p, p.pos0 + pos, i, grp);
     if (h == 0 && lane == 0) p.group_id[pos] = grp;
     RowDesc d = p.rows[row];   // qoff / voff / qlen / vlen set by the host
     const int64_t k0 = p.row_k0[h];

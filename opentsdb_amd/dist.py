@@ -46,13 +46,26 @@ def group_sorted_order(batch: abi.HostBatch):
     return keep[np.argsort(g[keep], kind="stable")]
 
 
+def _ranges(starts, ends):
+    """Concatenation of arange(starts[i], ends[i]) (vectorised)."""
+    starts = np.asarray(starts, np.int64)
+    lens = np.asarray(ends, np.int64) - starts
+    if lens.sum() == 0:
+        return np.zeros(0, np.int64)
+    keep = lens > 0
+    starts, lens = starts[keep], lens[keep]
+    first = np.repeat(np.cumsum(lens) - lens, lens)
+    return np.repeat(starts, lens) + (np.arange(int(lens.sum()), dtype=np.int64) - first)
+
+
 def select_series(batch: abi.HostBatch, series) -> abi.HostBatch:
-    """A batch holding only `series` (indices, in the given order); group ids unchanged."""
+    """A batch holding only `series` (indices, in the given order); group ids unchanged.
+    Vectorised (no per-row Python); the library's tsdbhip_load_shard does the same without a
+    host copy."""
     srp = batch.series_row_ptr
     qo, vo = batch.row_qual_off.astype(np.int64), batch.row_val_off.astype(np.int64)
     series = np.asarray(series, np.int64)
-    rows = [np.arange(srp[s], srp[s + 1]) for s in series]
-    rows = np.concatenate(rows) if rows else np.zeros(0, np.int64)
+    rows = _ranges(srp[series], srp[series + 1])
     new_srp = np.zeros(len(series) + 1, np.int64)
     if len(series):
         new_srp[1:] = np.cumsum(srp[series + 1] - srp[series])
@@ -60,8 +73,8 @@ def select_series(batch: abi.HostBatch, series) -> abi.HostBatch:
     vl = vo[rows + 1] - vo[rows]
     nqo = np.concatenate([[0], np.cumsum(ql)]).astype(np.uint64)
     nvo = np.concatenate([[0], np.cumsum(vl)]).astype(np.uint64)
-    q = np.concatenate([batch.qual[qo[r]:qo[r + 1]] for r in rows]) if len(rows) else np.zeros(0, np.uint8)
-    v = np.concatenate([batch.val[vo[r]:vo[r + 1]] for r in rows]) if len(rows) else np.zeros(0, np.uint8)
+    q = batch.qual[_ranges(qo[rows], qo[rows + 1])]
+    v = batch.val[_ranges(vo[rows], vo[rows + 1])]
     return abi.HostBatch(new_srp, batch.row_base_time[rows], nqo, nvo, q, v, batch.group_id[series])
 
 
@@ -226,16 +239,18 @@ def run_distributed_sel(eng, q: abi.Query, dist, n_groups_global: int, device=No
 # one GPU does (bit-exact), and only the finished points are gathered.  No data-path
 # collective.
 
+def series_bytes(batch: abi.HostBatch):
+    srp = batch.series_row_ptr
+    qo, vo = batch.row_qual_off.astype(np.int64), batch.row_val_off.astype(np.int64)
+    return (qo[srp[1:]] - qo[srp[:-1]]) + (vo[srp[1:]] - vo[srp[:-1]])
+
+
 def group_shard_bounds(batch: abi.HostBatch, world: int):
     """world+1 group ids: rank r owns groups [b[r], b[r+1]), byte-balanced."""
     G = n_groups_of(batch)
-    srp = batch.series_row_ptr
-    qo, vo = batch.row_qual_off.astype(np.int64), batch.row_val_off.astype(np.int64)
-    gbytes = np.zeros(G, np.float64)
-    for s in range(batch.n_series):
-        g = int(batch.group_id[s])
-        if g >= 0:
-            gbytes[g] += (qo[srp[s + 1]] - qo[srp[s]]) + (vo[srp[s + 1]] - vo[srp[s]])
+    g = batch.group_id
+    keep = g >= 0
+    gbytes = np.bincount(g[keep], weights=series_bytes(batch)[keep].astype(np.float64), minlength=G)
     return shard_bounds(gbytes, world)
 
 
@@ -255,15 +270,55 @@ def merge_group_results(parts):
     return groups
 
 
-def run_distributed_raw(eng, q: abi.Query, dist):
+def gather_groups(local, dist, device=None):
+    """Every rank's result groups [(group_id, ts, bits, is_int)] on every rank, as tensor
+    all-gathers (RCCL on `device` with the nccl backend, host tensors with gloo): the sizes
+    first, then one padded int64 buffer [gid | n | ts | bits] and one uint8 buffer [is_int]
+    per rank.  Returns the per-rank group lists in rank order."""
+    import torch
+    world = dist.get_world_size()
+    dev = device if dist.get_backend() == "nccl" else "cpu"
+    ng = len(local)
+    npts = int(sum(len(g[1]) for g in local))
+    sizes = torch.tensor([ng, npts], dtype=torch.int64, device=dev)
+    sizes_all = torch.empty(2 * world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(sizes_all, sizes)
+    sz = sizes_all.cpu().numpy().reshape(world, 2)
+    L = int(max(1, (2 * sz[:, 0] + 2 * sz[:, 1]).max()))
+    P = int(max(1, sz[:, 1].max()))
+    buf = np.zeros(L, np.int64)
+    isi = np.zeros(P, np.uint8)
+    if ng:
+        buf[:ng] = [g[0] for g in local]
+        buf[ng:2 * ng] = [len(g[1]) for g in local]
+    if npts:
+        buf[2 * ng:2 * ng + npts] = np.concatenate([np.asarray(g[1], np.int64) for g in local])
+        buf[2 * ng + npts:2 * ng + 2 * npts] = np.concatenate([np.asarray(g[2], np.uint64) for g in local]).view(np.int64)
+        isi[:npts] = np.concatenate([np.asarray(g[3], np.uint8) for g in local])
+    t_all = torch.empty(world * L, dtype=torch.int64, device=dev)
+    i_all = torch.empty(world * P, dtype=torch.uint8, device=dev)
+    dist.all_gather_into_tensor(t_all, torch.from_numpy(buf).to(dev))
+    dist.all_gather_into_tensor(i_all, torch.from_numpy(isi).to(dev))
+    t_all = t_all.cpu().numpy().reshape(world, L)
+    i_all = i_all.cpu().numpy().reshape(world, P)
+    parts = []
+    for r in range(world):
+        g_n, p_n = int(sz[r, 0]), int(sz[r, 1])
+        row = t_all[r]
+        gid, cnt = row[:g_n], row[g_n:2 * g_n]
+        ts, bits = row[2 * g_n:2 * g_n + p_n], row[2 * g_n + p_n:2 * g_n + 2 * p_n].view(np.uint64)
+        cut = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+        parts.append([(int(gid[i]), ts[cut[i]:cut[i + 1]], bits[cut[i]:cut[i + 1]], i_all[r][cut[i]:cut[i + 1]])
+                      for i in range(g_n)])
+    return parts
+
+
+def run_distributed_raw(eng, q: abi.Query, dist, device=None):
     """A raw (no-downsampling) query over a group-sharded store (shard_batch_by_group):
     local evaluation, then the points of every rank gathered to every rank."""
     if q.aggregator == abi.AGG["none"]:
         raise NotImplementedError("NONE aggregator: one group per span, ids are per rank")
-    local = [(int(g), np.asarray(ts), np.asarray(bits), np.asarray(isi)) for g, ts, bits, isi in eng.run(q)]
-    parts = [None] * dist.get_world_size()
-    dist.all_gather_object(parts, local)
-    return merge_group_results(parts)
+    return merge_group_results(gather_groups(eng.run(q), dist, device))
 
 
 # ---- NONE aggregator: one SpanGroup per span ---------------------------------------------
@@ -274,8 +329,9 @@ def run_distributed_raw(eng, q: abi.Query, dist):
 # order and renumbering the groups reproduces the single-GPU result.  No data exchange.
 
 def shard_batch_spans(batch: abi.HostBatch, rank: int, world: int) -> abi.HostBatch:
-    """Contiguous, byte-balanced range of spans in batch order (NONE aggregator)."""
-    keep = np.nonzero(batch.group_id >= 0)[0]
+    """Contiguous, byte-balanced range of spans in batch order (NONE aggregator: every span,
+    group-by tags ignored, TsdbQuery.java:940-961)."""
+    keep = np.arange(batch.n_series)
     srp = batch.series_row_ptr
     qo, vo = batch.row_qual_off.astype(np.int64), batch.row_val_off.astype(np.int64)
     sbytes = [(qo[srp[s + 1]] - qo[srp[s]]) + (vo[srp[s + 1]] - vo[srp[s]]) for s in keep]
@@ -292,9 +348,27 @@ def merge_none_results(parts):
     return out
 
 
-def run_distributed_none(eng, q: abi.Query, dist):
+def run_distributed_none(eng, q: abi.Query, dist, device=None):
     """A NONE-aggregator query over a span-sharded store (shard_batch_spans)."""
-    local = [(int(g), np.asarray(ts), np.asarray(bits), np.asarray(isi)) for g, ts, bits, isi in eng.run(q)]
-    parts = [None] * dist.get_world_size()
-    dist.all_gather_object(parts, local)
-    return merge_none_results(parts)
+    return merge_none_results(gather_groups(eng.run(q), dist, device))
+
+
+# ---- the library's own sharding (no host copy) -------------------------------------------
+MODE_OF = {"series": 0, "groups": 1, "spans": 2}   # tsdbhip.h TSDB_SHARD_*
+
+
+def load_rank_shard(eng, batch: abi.HostBatch, rank: int, world: int, mode: str = "series"):
+    """tsdbhip_shard_bounds + tsdbhip_load_shard: this rank's shard of a host batch, selected
+    and copied by the library (series / groups / spans as shard_batch /
+    shard_batch_by_group / shard_batch_spans)."""
+    from . import engine
+    m = MODE_OF[mode]
+    b = engine.shard_bounds(batch, world, m)
+    eng.load_shard(batch, m, int(b[rank]), int(b[rank + 1]))
+    return b
+
+
+def synth_bounds(n_series: int, world: int):
+    """Byte-balanced shard boundaries of a uniform synthetic store (every series the same
+    size): world + 1 batch positions."""
+    return [n_series * r // world for r in range(world + 1)]

@@ -27,8 +27,10 @@ EXPORTS = [
     "tsdbhip_run_partials", "tsdbhip_finalize", "tsdbhip_sync", "tsdbhip_rollup_interval_parse",
     "tsdbhip_rollup_basetime", "tsdbhip_rollup_qualifier", "tsdbhip_rollup_run", "tsdbhip_rollup_download",
     "tsdbhip_sel_layout", "tsdbhip_sel_run_values", "tsdbhip_sel_select", "tsdbhip_assemble", "tsdbhip_run_multi",
-    "tsdbhip_debug_rows",
+    "tsdbhip_debug_rows", "tsdbhip_shard_bounds", "tsdbhip_load_shard", "tsdbhip_synth_shard",
 ]
+
+SHARD_SERIES, SHARD_GROUPS, SHARD_SPANS = 0, 1, 2   # tsdbhip.h TSDB_SHARD_*
 
 
 class EngineError(Exception):
@@ -89,6 +91,9 @@ def lib():
         L.tsdbhip_rollup_run.argtypes = [vp, C.POINTER(abi.RollupSpec), C.POINTER(C.c_int64), C.POINTER(C.c_uint64)]
         L.tsdbhip_rollup_download.argtypes = [vp] + [C.c_void_p] * 5
         L.tsdbhip_debug_rows.argtypes = [vp] + [C.c_void_p] * 4
+        L.tsdbhip_shard_bounds.argtypes = [C.POINTER(abi.Batch), C.c_int, C.c_int, C.c_void_p]
+        L.tsdbhip_load_shard.argtypes = [vp, C.POINTER(abi.Batch), C.c_int, C.c_int64, C.c_int64]
+        L.tsdbhip_synth_shard.argtypes = [vp, C.POINTER(abi.SynthSpec), C.c_int64, C.c_int64]
         _lib = L
     return _lib
 
@@ -109,6 +114,13 @@ def scan_bounds(q: abi.Query):
     s, e = C.c_int64(), C.c_int64()
     _check(lib().tsdbhip_scan_bounds(C.byref(q), C.byref(s), C.byref(e)))
     return s.value, e.value
+
+
+def shard_bounds(batch: abi.HostBatch, world: int, mode: int = SHARD_SERIES):
+    """tsdbhip_shard_bounds: world + 1 byte-balanced boundaries (host logic, no GPU needed)."""
+    b = np.zeros(world + 1, np.int64)
+    _check(lib().tsdbhip_shard_bounds(C.byref(batch.c), world, mode, b.ctypes.data))
+    return b
 
 
 def rollup_interval(interval: str, row_span: str) -> abi.RollupInterval:
@@ -192,6 +204,17 @@ class Engine:
               n_groups: int = 1, int_mod: int = 2000, seed: int = 0x5EED):
         sp = abi.SynthSpec(n_series, start_s, n_points, period_ms, value_kind, n_groups, int_mod, seed)
         _check(lib().tsdbhip_synth(self.ctx, C.byref(sp)))
+
+    def synth_shard(self, pos_begin: int, pos_end: int, n_series: int, start_s: int, n_points: int,
+                    period_ms: int, value_kind: int = 0, n_groups: int = 1, int_mod: int = 2000, seed: int = 0x5EED):
+        """Batch positions [pos_begin, pos_end) of the n_series synthetic store (one rank's shard)."""
+        sp = abi.SynthSpec(n_series, start_s, n_points, period_ms, value_kind, n_groups, int_mod, seed)
+        _check(lib().tsdbhip_synth_shard(self.ctx, C.byref(sp), pos_begin, pos_end))
+
+    def load_shard(self, batch: abi.HostBatch, mode: int, begin: int, end: int):
+        """tsdbhip_load_shard: range [begin, end) of the batch under a TSDB_SHARD_* mode."""
+        _check(lib().tsdbhip_load_shard(self.ctx, C.byref(batch.c), mode, begin, end))
+        self._batch = batch
 
     def download(self) -> abi.HostBatch:
         ns, nr, qb, vb = C.c_int64(), C.c_int64(), C.c_uint64(), C.c_uint64()

@@ -91,7 +91,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_gloo_exchange_rank_order(tmp_path, world):
     nbytes = 1000
     mp.spawn(_worker, args=(world, _free_port(), nbytes, str(tmp_path)), nprocs=world, join=True)
@@ -160,7 +160,7 @@ def test_sel_combine_takes_owner_rows():
         np.testing.assert_array_equal(got[g].numpy(), (g % world) + 10 * np.arange(g * K, g * K + K))
 
 
-def _sel_gloo_worker(rank, world, port, out):
+def _sel_gloo_worker(rank, world, port, out):  # noqa: C901
     """The collective sequence of run_distributed_sel over gloo, with the engine calls
     replaced by host arithmetic (no GPU here): every rank contributes known values, and
     the owner's gathered segments must hold every rank's values of its groups."""
@@ -188,22 +188,18 @@ def _sel_gloo_worker(rank, world, port, out):
         td.destroy_process_group()
 
 
-def test_sel_exchange_gloo_two_ranks(tmp_path):
-    import socket
-    import torch.multiprocessing as mp
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    mp.spawn(_sel_gloo_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+@pytest.mark.parametrize("world", [2, 8])
+def test_sel_exchange_gloo(tmp_path, world):
+    mp.spawn(_sel_gloo_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     G, K = 6, 3
-    for me in range(2):
+    for me in range(world):
         z = np.load(tmp_path / f"s{me}.npz")
         ca = z["counts_all"]
         want = []
         for g in range(G):
-            if g % 2 != me:
+            if g % world != me:
                 continue
-            want += [r * 1e6 + g * 1e4 + k * 1e2 + i for r in range(2) for i in range(ca[r, g]) for k in range(K)]
+            want += [r * 1e6 + g * 1e4 + k * 1e2 + i for r in range(world) for i in range(ca[r, g]) for k in range(K)]
         np.testing.assert_array_equal(z["ov"], want)
 
 
@@ -236,3 +232,86 @@ def test_shard_spans_covers_batch_in_order(world):
     assert sum(got) == b.n_series
     parts = [[(0, np.zeros(1), np.zeros(1), np.zeros(1))] * n for n in got]
     assert [g[0] for g in dist.merge_none_results(parts)] == list(range(b.n_series))
+
+
+# ---- result gathers as tensors (raw / NONE queries) ------------------------------------
+def _rank_groups(rank):
+    rng = np.random.default_rng(100 + rank)
+    out = []
+    for i in range(int(rng.integers(0, 5))):
+        n = int(rng.integers(0, 40))
+        out.append((rank * 10 + i, rng.integers(0, 1 << 40, n).astype(np.int64),
+                    rng.integers(0, 1 << 63, n, dtype=np.uint64) | np.uint64(1 << 63), rng.integers(0, 2, n).astype(np.uint8)))
+    return out
+
+
+def _gather_worker(rank, world, port, out):
+    import torch.distributed as td
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    td.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        parts = dist.gather_groups(_rank_groups(rank), td)
+        flat = [(r, g, ts, bits, isi) for r, p in enumerate(parts) for (g, ts, bits, isi) in p]
+        np.savez(os.path.join(out, f"g{rank}.npz"), rg=np.array([(f[0], f[1]) for f in flat]).reshape(-1, 2),
+                 n=np.array([len(f[2]) for f in flat]),
+                 ts=np.concatenate([f[2] for f in flat]) if flat else np.zeros(0, np.int64),
+                 bits=np.concatenate([f[3] for f in flat]) if flat else np.zeros(0, np.uint64),
+                 isi=np.concatenate([f[4] for f in flat]) if flat else np.zeros(0, np.uint8))
+    finally:
+        td.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_gather_groups_gloo(tmp_path, world):
+    """Uneven per-rank results (0..4 groups of 0..39 points, all 64 value bits used) arrive
+    on every rank, in rank order, bit for bit."""
+    mp.spawn(_gather_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    want = [(r, g) for r in range(world) for (g, _, _, _) in _rank_groups(r)]
+    wts = [x for r in range(world) for (_, ts, _, _) in _rank_groups(r) for x in ts]
+    wbits = [x for r in range(world) for (_, _, b, _) in _rank_groups(r) for x in b]
+    for me in range(world):
+        z = np.load(tmp_path / f"g{me}.npz")
+        assert [tuple(x) for x in z["rg"]] == want
+        np.testing.assert_array_equal(z["ts"], np.array(wts, np.int64))
+        np.testing.assert_array_equal(z["bits"], np.array(wbits, np.uint64))
+
+
+# ---- sharding inside the library (host logic of libtsdbhip, no GPU) ---------------------
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 8])
+def test_library_shard_bounds_match_python(world):
+    from opentsdb_amd import engine
+    b = synth.generate(57, T0, 400, 10000, value_kind=2, n_groups=6, int_mod=30000, seed=7)
+    gid = b.group_id.copy()
+    gid[::4] = (gid[::4] + 2) % 6
+    gid[7] = -1
+    b = abi.HostBatch(b.series_row_ptr, b.row_base_time, b.row_qual_off, b.row_val_off, b.qual, b.val, gid)
+    order = dist.group_sorted_order(b)
+    sb = dist.series_bytes(b)
+    assert list(engine.shard_bounds(b, world, engine.SHARD_SERIES)) == dist.shard_bounds(sb[order], world)
+    assert list(engine.shard_bounds(b, world, engine.SHARD_GROUPS)) == dist.group_shard_bounds(b, world)
+    assert list(engine.shard_bounds(b, world, engine.SHARD_SPANS)) == dist.shard_bounds(sb, world)
+
+
+def test_shard_ten_million_series_in_seconds():
+    """A 10M-series batch (config 3's series count, one 4-point row each) is sharded 8 ways
+    on the host in seconds: library bounds, and the vectorised Python selection of a shard."""
+    import time
+    from opentsdb_amd import engine
+    n = 10_000_000
+    srp = np.arange(n + 1, dtype=np.int64)
+    qo = np.arange(n + 1, dtype=np.uint64) * 8
+    vo = np.arange(n + 1, dtype=np.uint64) * 17
+    b = abi.HostBatch(srp, np.full(n, T0, np.uint32), qo, vo, np.zeros(8 * n, np.uint8), np.zeros(17 * n, np.uint8),
+                      (np.arange(n) % 1000).astype(np.int32))
+    t = time.perf_counter()
+    bounds = engine.shard_bounds(b, 8, engine.SHARD_SERIES)
+    t_bounds = time.perf_counter() - t
+    assert bounds[0] == 0 and bounds[-1] == n and np.all(np.diff(bounds) > 0)
+    assert t_bounds < 10, t_bounds
+    t = time.perf_counter()
+    order = dist.group_sorted_order(b)
+    s = dist.select_series(b, order[bounds[3]:bounds[4]])
+    t_sel = time.perf_counter() - t
+    assert s.n_series == bounds[4] - bounds[3] and len(s.qual) == 8 * s.n_series
+    assert t_sel < 20, t_sel

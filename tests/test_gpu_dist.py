@@ -25,7 +25,7 @@ T0 = 1356998400
 @pytest.fixture(scope="module")
 def engines():
     from opentsdb_amd.engine import Engine
-    es = [Engine(0) for _ in range(4)]
+    es = [Engine(0) for _ in range(8)]
     yield es
     for e in es:
         e.close()
@@ -50,7 +50,7 @@ def run_sharded(engines, b, q, world):
     return engines[0].finalize(q, G, gathered.ctypes.data, world)
 
 
-@pytest.mark.parametrize("world", [1, 2, 3, 4])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 @pytest.mark.parametrize("agg", ["sum", "avg", "min", "max", "count", "dev", "first", "last", "diff", "zimsum",
                                  "mimmax", "pfsum"])
 def test_sharded_equals_oracle(engines, batch, world, agg):
@@ -157,7 +157,7 @@ def run_sharded_sel(engines, b, q, world):
     return engines[0].assemble(q, G, val.ctypes.data, flag.ctypes.data, act.ctypes.data)
 
 
-@pytest.mark.parametrize("world", [1, 2, 3, 4])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 @pytest.mark.parametrize("agg,ds", [("p99", "avg"), ("p50", "max"), ("median", "sum"), ("p90", "p99"),
                                     ("ep95r7", "avg")])
 def test_sharded_percentile_group_equals_oracle(engines, batch, world, agg, ds):
@@ -216,7 +216,7 @@ def raw_batch():
     return random_batch(21, n_series=60, n_groups=5)
 
 
-@pytest.mark.parametrize("world", [1, 2, 3, 4])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 @pytest.mark.parametrize("agg", ["sum", "avg", "min", "max", "dev", "zimsum", "mimmax", "first", "diff", "pfsum",
                                  "p99", "ep90r3", "median"])
 def test_group_sharded_raw_equals_oracle(engines, raw_batch, world, agg):
@@ -272,7 +272,7 @@ def test_two_process_gloo_raw(tmp_path):
         assert_groups_match(got, want, "sum", tol=0.0, ctx=f"gloo raw rank {r}")
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 @pytest.mark.parametrize("agg", ["sum", "avg", "dev", "squareSum"])
 def test_sharded_ordered_bit_exact(engines, batch, world, agg):
     """TSDB_QF_ORDERED over ranks: span values to the owner, folded in rank (= span) order."""
@@ -282,9 +282,82 @@ def test_sharded_ordered_bit_exact(engines, batch, world, agg):
 
 
 # ---- NONE aggregator: span-sharded, results concatenated in rank order -----------------
-@pytest.mark.parametrize("world", [1, 2, 3, 4])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 def test_span_sharded_none_equals_oracle(engines, batch, raw_batch, world):
     for b, q in [(batch, abi.new_query(T0, T0 + 3599, "none", ds_function=abi.AGG["avg"], ds_interval_ms=60000)),
                  (raw_batch, abi.new_query(T0, T0 + 7199, "none"))]:
         parts = [engines[r].run_batch(dist.shard_batch_spans(b, r, world), q) for r in range(world)]
         assert_groups_match(dist.merge_none_results(parts), O.run_query(b, q), "none", tol=0.0, ctx=f"none x{world}")
+
+
+# ---- the library's sharding: tsdbhip_load_shard / tsdbhip_synth_shard -------------------
+def run_lib_sharded(engines, b, q, world):
+    G = dist.n_groups_of(b)
+    bufs = []
+    for r in range(world):
+        e = engines[r]
+        dist.load_rank_shard(e, b, r, world, "series")
+        lay = e.partials_layout(q, G)
+        buf = np.zeros(int(lay.bytes), np.uint8)
+        e.run_partials(q, G, buf.ctypes.data)
+        bufs.append(buf)
+    gathered = np.concatenate(bufs)   # (kept alive while finalize reads it)
+    return engines[0].finalize(q, G, gathered.ctypes.data, world)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_library_shards_equal_python_shards(engines, batch, world):
+    """tsdbhip_load_shard over the host batch == loading dist.shard_batch's copy, bit for bit
+    (run_partials + finalize), and both equal the oracle."""
+    for agg in ["sum", "max", "dev"]:
+        q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+        lib = run_lib_sharded(engines, batch, q, world)
+        py = run_sharded(engines, batch, q, world)
+        for (g1, t1, b1, i1), (g2, t2, b2, i2) in zip(lib, py):
+            assert g1 == g2
+            np.testing.assert_array_equal(b1, b2)
+        assert_groups_match(lib, O.run_query(batch, q), agg, ctx=f"lib shards {agg} x{world}")
+
+
+def test_library_group_and_span_shards(engines, raw_batch):
+    q = abi.new_query(T0, T0 + 7199, "sum")
+    parts = []
+    for r in range(4):
+        dist.load_rank_shard(engines[r], raw_batch, r, 4, "groups")
+        parts.append(engines[r].run(q))
+    assert_groups_match(dist.merge_group_results(parts), O.run_query(raw_batch, q), "sum", tol=0.0, ctx="groups")
+    qn = abi.new_query(T0, T0 + 7199, "none")
+    parts = []
+    for r in range(3):
+        dist.load_rank_shard(engines[r], raw_batch, r, 3, "spans")
+        parts.append(engines[r].run(qn))
+    assert_groups_match(dist.merge_none_results(parts), O.run_query(raw_batch, qn), "none", tol=0.0, ctx="spans")
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_synth_shards_concatenate_to_the_store(engines, world):
+    """tsdbhip_synth_shard: rank r generates batch positions [b_r, b_r+1) of the one global
+    store; the shards' bytes are the store's, and the sharded query equals the oracle."""
+    args = (203, T0, 360, 10000, 2, 7, 30000, 0x5EED)
+    engines[0].synth(*args)
+    whole = engines[0].download()
+    bounds = dist.synth_bounds(args[0], world)
+    G = args[5]
+    q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+    bufs = []
+    quals, gids = [], []
+    for r in range(world):
+        e = engines[r]
+        e.synth_shard(bounds[r], bounds[r + 1], *args)
+        sh = e.download()
+        quals.append(sh.qual)
+        gids.append(sh.group_id)
+        lay = e.partials_layout(q, G)
+        buf = np.zeros(int(lay.bytes), np.uint8)
+        e.run_partials(q, G, buf.ctypes.data)
+        bufs.append(buf)
+    np.testing.assert_array_equal(np.concatenate(quals), whole.qual)
+    np.testing.assert_array_equal(np.concatenate(gids), whole.group_id)
+    gathered = np.concatenate(bufs)
+    got = engines[0].finalize(q, G, gathered.ctypes.data, world)
+    assert_groups_match(got, O.run_query(whole, q), "sum", ctx=f"synth shards x{world}")

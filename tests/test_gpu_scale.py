@@ -251,3 +251,38 @@ def test_config2_full_size(eng):
     assert_groups_match(got, want, "sum", ctx="config2 full")
     assert_groups_match(got_ordered, want, "sum", tol=0.0, ctx="config2 full ordered (bit-exact)")
     assert_groups_match(got_max, O.run_query(host, qm, threads=16), "max", ctx="config2 full max")
+
+
+def empty_batch():
+    return abi.HostBatch(np.zeros(1, np.int64), np.zeros(0, np.uint32), np.zeros(1, np.uint64), np.zeros(1, np.uint64),
+                         np.zeros(0, np.uint8), np.zeros(0, np.uint8), np.zeros(0, np.int32))
+
+
+@pytest.mark.parametrize("kind", ["empty", "out_of_range", "dropped"])
+def test_empty_inputs_every_path(eng, kind):
+    """No series, series entirely outside the scan range, and every series dropped (group -1):
+    every path -- downsampled, percentile downsampling and group-by, ORDERED, NONE, raw union,
+    raw percentile, rate -- returns what the oracle returns (no groups / inactive groups)."""
+    if kind == "empty":
+        b = empty_batch()
+    else:
+        b = synth.generate(12, T0 + (86400 if kind == "out_of_range" else 0), 360, 10000, value_kind=2, n_groups=3,
+                           int_mod=30000)
+        if kind == "dropped":
+            b = abi.HostBatch(b.series_row_ptr, b.row_base_time, b.row_qual_off, b.row_val_off, b.qual, b.val,
+                              np.full(b.n_series, -1, np.int32))
+    queries = [
+        ("sum", dict(ds_function=abi.AGG["avg"], ds_interval_ms=60000)),
+        ("max", dict(ds_function=abi.AGG["p99"], ds_interval_ms=600000)),
+        ("p95", dict(ds_function=abi.AGG["avg"], ds_interval_ms=60000)),
+        ("sum", dict(ds_function=abi.AGG["avg"], ds_interval_ms=60000, flags=abi.QF_ORDERED)),
+        ("none", dict(ds_function=abi.AGG["avg"], ds_interval_ms=60000)),
+        ("sum", dict(ds_function=abi.AGG["sum"], ds_interval_ms=60000, ds_fill=abi.FILL_NAN)),
+        ("sum", dict()),
+        ("p99", dict()),
+        ("none", dict()),
+        ("sum", dict(rate=True, counter=True)),
+    ]
+    for agg, kw in queries:
+        q = abi.new_query(T0, T0 + 3599, agg, **kw)
+        assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), agg, tol=0.0, ctx=f"{kind} {agg} {kw}")
