@@ -173,6 +173,9 @@ def main():
     from opentsdb_amd import abi
 
     eng = Engine(local_rank)
+    # a tiny store first: loads the index kernels' code objects, so index_ms is the load of
+    # the real store alone
+    eng.synth(256, T0, args.points, args.period_ms, args.value_kind, min(args.groups, 256), 30000, 1)
     t_gen = time.perf_counter()
     int_mod = 30000 if args.value_kind == 2 else 2000
     if args.scaling == "strong":
