@@ -225,6 +225,7 @@ struct tsdbhip_ctx {
   DevBuf pre_dense, pre_pres;          // percentile / median downsampling
   DevBuf big_scratch;                  // k_pct large buckets: per-wave overflow regions
   bool mdp_valid = false;              // series_max_dp() cache (invalidated by every load)
+  bool ro_meta_valid = false;          // rollup ro_ord / ro_orig / ro_allint of the loaded batch
   int64_t mdp_ss = 0, mdp_se = 0, mdp = 0;
   DevBuf sel_vals, sel_sorted, sel_uni, sel_gsp;   // percentile / median group-by
   DevBuf cal_bounds;                                // calendar month / year slot boundaries
@@ -252,6 +253,7 @@ struct tsdbhip_ctx {
   bool acct_none = false;
   // rollup generation: scratch and the per-function cells of the last tsdbhip_rollup_run
   DevBuf ro_allint, ro_ord, ro_orig, ro_cnt, ro_vsz, ro_coff, ro_voff;
+  DevBuf ro_agg, ro_pres;              // fused rollup pass: [4][series][K] values, [series][K] presence
   void* ro_tmp = nullptr;
   size_t ro_tmp_bytes = 0;
   struct RollupOut {
@@ -404,6 +406,7 @@ static void release_batch(tsdbhip_ctx* c) {
   c->none_tiles_ready = false;
   c->acct_valid = false;
   c->mdp_valid = false;
+  c->ro_meta_valid = false;
   c->n_series = c->n_rows = c->n_groups = 0;
 }
 
@@ -417,7 +420,7 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
                     &c->r_spoff, &c->r_spn, &c->r_grp, &c->r_pts, &c->r_rank, &c->r_bm, &c->r_wb, &c->r_U, &c->r_ooff,
                     &c->r_sg, &c->r_su, &c->r_ots, &c->r_obits, &c->r_oint, &c->r_coff, &c->r_cur, &c->r_voff, &c->r_vl, &c->r_vd, &c->r_vp, &c->pre_dense, &c->pre_pres,
                     &c->ro_allint, &c->ro_ord, &c->ro_orig, &c->ro_cnt, &c->ro_vsz, &c->ro_coff, &c->ro_voff,
-                    &c->big_scratch})
+                    &c->big_scratch, &c->ro_agg, &c->ro_pres})
     b->release();
   for (auto& o : c->ro_out)
     for (DevBuf* b : {&o.series, &o.base, &o.qual, &o.voff, &o.val}) b->release();
@@ -2618,8 +2621,8 @@ extern "C" int tsdbhip_rollup_run(tsdbhip_ctx* c, const tsdbhip_rollup_spec* sp,
   // the series with a group (ungrouped ones -- group id -1 -- sit after them and get no rollups)
   int64_t n = 0;
   while (n < c->n_series && c->h_group[n] < c->n_groups) n++;
-  // batch order -> sorted position, and the per-series integer flag
-  {
+  // batch order -> sorted position, and the per-series integer flag (once per loaded batch)
+  if (!c->ro_meta_valid) {
     std::vector<int64_t> ord(n);
     std::iota(ord.begin(), ord.end(), 0);
     std::sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return c->h_orig[a] < c->h_orig[b]; });
@@ -2632,30 +2635,102 @@ extern "C" int tsdbhip_rollup_run(tsdbhip_ctx* c, const tsdbhip_rollup_spec* sp,
     }
     HIP_OK(launch_series_allint(c->rows.as<RowDesc>(), c->srp.as<int64_t>(), n, c->ro_allint.as<uint8_t>(), c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));   // `ord` leaves scope
+    c->ro_meta_valid = true;
   }
-  for (int fi = 0; fi < sp->n_funcs; fi++) {
-    // Downsampler of every series (NONE aggregator: one SpanGroup per span), fill none
-    tsdbhip_query q{};
-    q.start_time = sp->start_s;
-    q.end_time = sp->end_s - 1;
-    q.aggregator = TSDB_AGG_NONE;
-    q.ds_function = sp->func[fi];
-    q.ds_fill = TSDB_FILL_NONE;
-    q.ds_interval_ms = (int64_t)sp->interval.interval_s * 1000;
-    q.rate_counter_max = INT64_MAX;
-    Plan P;
+  // Downsampler of every series at the rollup interval (fill none; the geometry of a NONE-
+  // aggregator query): one fused pass reduces every bucket with sum, count, max and min
+  tsdbhip_query q{};
+  q.start_time = sp->start_s;
+  q.end_time = sp->end_s - 1;
+  q.aggregator = TSDB_AGG_NONE;
+  q.ds_function = TSDB_AGG_SUM;
+  q.ds_fill = TSDB_FILL_NONE;
+  q.ds_interval_ms = (int64_t)sp->interval.interval_s * 1000;
+  q.rate_counter_max = INT64_MAX;
+  Plan P;
+  {
     int rc = plan_query(c, &q, P);
     if (rc) return rc;
-    rc = run_device(c, &q, P, n, true);
-    if (rc) return rc;
+  }
+  const int64_t NS = c->n_series;
+  HIP_OK(c->ro_agg.ensure(std::max<int64_t>(1, 4 * NS * P.K) * 8));
+  HIP_OK(c->ro_pres.ensure(std::max<int64_t>(1, NS * P.K)));
+  HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
+  HIP_OK(hipEventRecord(c->ev[0], c->stream));
+  {
+    GridParams gp{};
+    gp.rows = c->rows.as<RowDesc>();
+    gp.series_row_ptr = c->srp.as<int64_t>();
+    gp.qual = c->qual.as<uint8_t>();
+    gp.val = c->val.as<uint8_t>();
+    gp.ss = P.ss;
+    gp.se = P.se;
+    gp.B0 = P.B0;
+    gp.I = P.I;
+    gp.K = P.K;
+    gp.rcpI = (float)(1.0 / (double)P.I);
+    gp.mode = MODE_GRID;
+    gp.n_series = n;
+    gp.err = c->err.as<int32_t>();
+    gp.val2 = c->val2.as<uint8_t>();
+    RollupAggParams ap{};
+    ap.out = c->ro_agg.as<double>();
+    ap.stride = NS * P.K;
+    ap.K = P.K;
+    ap.pres = c->ro_pres.as<uint8_t>();
+    // streaming kernel per row class (class A over every series, class B over what A handed
+    // back), then the general kernel over the rest
+    const char* env = std::getenv("TSDBHIP_FAST");
+    const bool fast = !(env && env[0] == '0') && c->fast_qw && n > 0 && P.I <= (1LL << 29) &&
+                      rollup_fast_lds(P.K) <= 32 * 1024;
+    const int32_t* list = nullptr;
+    const int32_t* list_n = nullptr;
+    if (fast) {
+      HIP_OK(c->r1a.ensure(n * 4));
+      HIP_OK(c->r2.ensure(n * 4));
+      HIP_OK(c->r_n.ensure(16));
+      HIP_OK(hipMemsetAsync(c->r_n.p, 0, 16, c->stream));
+      int32_t* rn = c->r_n.as<int32_t>();
+      int32_t* outs[2] = {c->r1a.as<int32_t>(), c->r2.as<int32_t>()};
+      for (int cls = 0; cls < 2; cls++) {
+        const int qw = cls ? c->fast_qw2 : c->fast_qw, vl = cls ? c->fast_vl2 : c->fast_vl;
+        if (!qw || !rollup_fast_supported(qw, vl) || (cls == 1 && !list)) continue;
+        GridParams fp = gp;
+        fp.unit_s = (qw == 2 && P.I % 1000 == 0 && P.B0 % 1000 == 0) ? 1 : 0;
+        fp.In = (int32_t)(fp.unit_s ? P.I / 1000 : P.I);
+        fp.B0n = fp.unit_s ? P.B0 / 1000 : P.B0;
+        fp.rcpn = std::nextafter(1.0 / (double)fp.In, INFINITY);
+        fp.wave_lds = (int32_t)rollup_fast_lds(P.K);
+        fp.waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / std::max<int64_t>(16, fp.wave_lds)));
+        fp.tile_list = list;
+        fp.tile_list_n = list_n;
+        fp.n_launch = n;
+        fp.redo_list = outs[cls];
+        fp.redo_n = rn + cls;
+        HIP_OK(launch_rollup_fast(fp, ap, qw, vl, c->stream));
+        list = outs[cls];
+        list_n = rn + cls;
+      }
+    }
+    if (list) {
+      gp.tile_list = list;
+      gp.tile_list_n = list_n;
+      gp.n_launch = std::min<int64_t>(n, 16384);
+    }
+    HIP_OK(launch_rollup_agg(gp, ap, c->stream));
+  }
+  HIP_OK(hipEventRecord(c->ev[1], c->stream));
+  for (int fi = 0; fi < sp->n_funcs; fi++) {
+    const int f = sp->func[fi];
+    const int fslot = f == TSDB_AGG_SUM ? 0 : f == TSDB_AGG_COUNT ? 1 : f == TSDB_AGG_MAX ? 2 : 3;
     const int64_t NK = n * P.K;
     HIP_OK(c->ro_cnt.ensure(std::max<int64_t>(1, NK) * 4));
     HIP_OK(c->ro_vsz.ensure(std::max<int64_t>(1, NK) * 4));
     HIP_OK(c->ro_coff.ensure(std::max<int64_t>(1, NK) * 8));
     HIP_OK(c->ro_voff.ensure(std::max<int64_t>(1, NK) * 8));
     RollupParams rp{};
-    rp.val = c->out_val.as<double>();
-    rp.flag = c->out_flag.as<uint8_t>();
+    rp.val = c->ro_agg.as<double>() + fslot * NS * P.K;
+    rp.flag = c->ro_pres.as<uint8_t>();
     rp.ord = c->ro_ord.as<int64_t>();
     rp.orig = c->ro_orig.as<int64_t>();
     rp.allint = c->ro_allint.as<uint8_t>();
@@ -2711,6 +2786,18 @@ extern "C" int tsdbhip_rollup_run(tsdbhip_ctx* c, const tsdbhip_rollup_spec* sp,
     HIP_OK(hipMemcpyAsync(o.voff.as<uint64_t>() + o.cells, &o.bytes, 8, hipMemcpyHostToDevice, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
     c->ro_n = fi + 1;
+  }
+  HIP_OK(hipEventRecord(c->ev[2], c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  {
+    float t01 = 0, t02 = 0;
+    (void)hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
+    (void)hipEventElapsedTime(&t02, c->ev[0], c->ev[2]);
+    c->timing.decode_downsample_ms = t01;   // the fused sum / count / max / min pass
+    c->timing.group_reduce_ms = t02 - t01;  // cell sizing, scans and writes
+    c->timing.total_ms = t02;
+    c->timing.fast_ms = 0;
+    account(c, P);
   }
   int64_t cells = 0;
   uint64_t bytes = 0;

@@ -292,6 +292,20 @@ struct RollupParams {
   uint8_t* o_val;
   int32_t* err;
 };
+// fused per-series reduction of every rollup function (k_rollup.hip): out[f * stride + s * K + k]
+// for f = 0 sum, 1 count, 2 max, 3 min; pres[s * K + k] = the bucket has a datapoint
+struct RollupAggParams {
+  double* out;
+  int64_t stride;           // n_series * K
+  int64_t K;
+  uint8_t* pres;
+};
+hipError_t launch_rollup_agg(const GridParams& p, const RollupAggParams& rp, hipStream_t s);
+// streaming variant for one uniform row class (k_fast's premises + the sum certificate);
+// series that break a premise go to p.redo_list for launch_rollup_agg (tile_list mode)
+bool rollup_fast_supported(int qw, int vl);
+int64_t rollup_fast_lds(int64_t K);
+hipError_t launch_rollup_fast(const GridParams& p, const RollupAggParams& rp, int qw, int vl, hipStream_t s);
 hipError_t launch_series_allint(const RowDesc* rows, const int64_t* srp, int64_t n, uint8_t* allint, hipStream_t s);
 hipError_t launch_rollup_size(const RollupParams& p, hipStream_t s);
 hipError_t launch_rollup_write(const RollupParams& p, hipStream_t s);

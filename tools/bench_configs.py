@@ -83,13 +83,17 @@ def rollup_bench(args, eng, n_series):
             nc, nb = eng.rollup_run(riv, T0, T0 + 86400)
             ms.append((time.perf_counter() - t) * 1000)
         step_ms = sum(ms) / len(ms)
+        rt = eng.timing()
         out_bytes = nc * (4 + 4 + 3 + 8) + nb
         line = {"config": args.config, "query": f"rollup {iv} in {span} rows x sum,count,max,min",
                 "series": n_series, "datapoints": int(tm.datapoints), "cells": nc, "value_bytes": nb,
                 "ms_per_step": step_ms, "datapoints_per_s": tm.datapoints / (step_ms / 1000),
+                "fused_pass_ms": rt.decode_downsample_ms, "cell_write_ms": rt.group_reduce_ms,
+                "fused_pass_hbm_frac_of_8tbs": in_bytes / (rt.decode_downsample_ms / 1000) / 8e12,
                 "algorithmic_bytes": in_bytes + out_bytes,
                 "hbm_frac_of_8tbs": (in_bytes + out_bytes) / (step_ms / 1000) / 8e12,
-                "note": "one downsample pass per function (4 input reads); algorithmic bytes count one"}
+                "note": "one fused input pass (k_rollup_agg: sum, count, max, min per bucket), then cell "
+                        "sizing / scans / writes per function"}
         print(json.dumps(line), flush=True)
 
 
