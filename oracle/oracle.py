@@ -15,12 +15,13 @@ import numpy as np
 from opentsdb_amd import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "librefcpu.so")
+LIB_PATH = os.environ.get("TSDB_ORACLE_LIB") or os.path.join(HERE, "build", "librefcpu.so")
 
 
 def build(force: bool = False) -> str:
     if force or not os.path.exists(LIB_PATH):
-        subprocess.run(["make", "-C", HERE], check=True, stdout=subprocess.DEVNULL)
+        target = ["san"] if LIB_PATH.endswith("_ubsan.so") else []
+        subprocess.run(["make", "-C", HERE] + target, check=True, stdout=subprocess.DEVNULL)
     return LIB_PATH
 
 

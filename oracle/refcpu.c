@@ -1431,9 +1431,11 @@ static void ai_destroy(ref_view* v) {
 }
 static const view_vt AGG_VT = {ai_has_next, ai_next, ai_seek, ai_destroy};
 
-/* Constructor :395-465 */
-static ref_view* make_aggregate(ref_view** srcs, int64_t n, int64_t start_time, int64_t end_time,
-                                int32_t aggregator, int32_t interpolation, int32_t rate) {
+/* Constructor :395-465, in two steps so that an exception thrown while priming the spans
+ * (the second step) finds the object already owned by the caller: agg_new takes ownership of
+ * the spans and cannot throw. */
+static agg_view* agg_new(ref_view** srcs, int64_t n, int64_t start_time, int64_t end_time,
+                         int32_t aggregator, int32_t interpolation, int32_t rate) {
   agg_view* a = (agg_view*)xcalloc(1, sizeof(agg_view));
   a->base.vt = &AGG_VT;
   a->k = n;
@@ -1448,6 +1450,11 @@ static ref_view* make_aggregate(ref_view** srcs, int64_t n, int64_t start_time, 
   a->rate = rate;
   a->current = 0;
   for (int64_t i = 0; i < n; i++) { a->its[i] = srcs[i]; a->owned[i] = srcs[i]; }
+  return a;
+}
+
+static void agg_start(agg_view* a) {
+  const int64_t n = a->k, start_time = a->start;
   for (int64_t i = 0; i < n; i++) {
     ref_view* it = a->its[i];
     v_seek(it, start_time);
@@ -1464,20 +1471,21 @@ static ref_view* make_aggregate(ref_view** srcs, int64_t n, int64_t start_time, 
       if (null_dp) { ai_end_reached(a, i); continue; }
       ai_put(a, n + i, &d);
     }
-    if (rate) {
+    if (a->rate) {
       if (v_has_next(it)) ai_move_to_next(a, i);
       else ai_end_reached(a, i);
     }
   }
-  return &a->base;
 }
 
 ref_view* ref_view_aggregate(ref_view** srcs, int64_t n, int64_t start_time, int64_t end_time,
                              int32_t aggregator, int32_t interpolation, int32_t rate) {
-  ref_view* r = NULL;
-  TRY { r = make_aggregate(srcs, n, start_time, end_time, aggregator, interpolation, rate); }
-  CATCH(e) { (void)e; r = NULL; } END_TRY
-  return r;
+  agg_view* a = agg_new(srcs, n, start_time, end_time, aggregator, interpolation, rate);
+  volatile int failed = 0;
+  TRY { agg_start(a); }
+  CATCH(e) { (void)e; failed = 1; } END_TRY
+  if (failed) { ai_destroy(&a->base); return NULL; }   /* the spans were handed over: freed with it */
+  return &a->base;
 }
 
 void ref_view_free(ref_view* v) { if (v) v->vt->destroy(v); }
@@ -1703,8 +1711,10 @@ static void run_group(const query_env* env, group_job* g) {
       if (q->rate) it = ref_view_rate(it, q->rate_counter, q->rate_counter_max, q->rate_reset_value, q->rate_drop_resets);
       its[k++] = it;
     }
-    ai = make_aggregate(its, k, env->scan_start_ms, env->scan_end_ms, q->aggregator, agg_interp(q->aggregator), q->rate);
+    agg_view* na = agg_new(its, k, env->scan_start_ms, env->scan_end_ms, q->aggregator, agg_interp(q->aggregator), q->rate);
+    ai = &na->base;
     k = 0;  /* ownership moved */
+    agg_start(na);
     while (v_has_next(ai)) {
       ref_dp d = v_next(ai);
       if (d.is_int) job_push(g, d.ts, 1, (uint64_t)dp_long(&d));
