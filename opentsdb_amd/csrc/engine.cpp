@@ -226,6 +226,8 @@ struct tsdbhip_ctx {
   DevBuf big_scratch;                  // k_pct large buckets: per-wave overflow regions
   bool mdp_valid = false;              // series_max_dp() cache (invalidated by every load)
   bool ro_meta_valid = false;          // rollup ro_ord / ro_orig / ro_allint of the loaded batch
+  bool lc_valid = false;               // local_counts() cache
+  std::vector<int64_t> lc;
   int64_t mdp_ss = 0, mdp_se = 0, mdp = 0;
   DevBuf sel_vals, sel_sorted, sel_uni, sel_gsp;   // percentile / median group-by
   DevBuf cal_bounds;                                // calendar month / year slot boundaries
@@ -407,6 +409,7 @@ static void release_batch(tsdbhip_ctx* c) {
   c->acct_valid = false;
   c->mdp_valid = false;
   c->ro_meta_valid = false;
+  c->lc_valid = false;
   c->n_series = c->n_rows = c->n_groups = 0;
 }
 
@@ -1110,6 +1113,7 @@ struct Plan {
   int gsel = 0;       // TSDB_AGG_* when the group-by aggregator is a percentile / median (0: none)
   bool no_inf = false;   // per-span pass feeding the percentile group-by: no +-Inf check
   bool dense_out = false;   // grid kernels write per-series bucket values to pre_dense / pre_pres
+  bool sel_direct = false;  // grid kernels write percentile group-by contributions (GridParams.sel_direct)
   std::vector<int64_t> bounds;   // MODE_TABLE: K + 1 calendar slot boundaries (ms)
   int64_t seek = 0;              // MODE_TABLE: first timestamp the spans' Downsamplers read
   bool ordered = false;          // TSDB_QF_ORDERED float reduction: run_ordered
@@ -1322,7 +1326,12 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   gp.group_active = c->gact.as<uint32_t>();
   gp.err = c->err.as<int32_t>();
   if (const char* dbg = std::getenv("TSDBHIP_DBG")) gp.dbg = std::atoi(dbg);
-  if (P.dense_out) {
+  if (P.sel_direct) {   // buffers prepared by sel_values
+    gp.sel_direct = 1;
+    gp.sel_vals = c->sel_vals.as<double>();
+    gp.sel_uni = c->sel_uni.as<uint8_t>();
+    gp.group_series_ptr = c->sel_gsp.as<int64_t>();
+  } else if (P.dense_out) {
     HIP_OK(c->pre_dense.ensure(std::max<int64_t>(1, c->n_series * K) * 8));
     HIP_OK(c->pre_pres.ensure(std::max<int64_t>(1, c->n_series * K)));
     HIP_OK(hipMemsetAsync(c->pre_pres.p, 0, std::max<int64_t>(1, c->n_series * K), c->stream));
@@ -1638,19 +1647,43 @@ std::vector<int64_t> seg_ptr(const std::vector<int64_t>& counts) {
   return gsp;
 }
 
-// local series per group id g < G (resident order is group-sorted)
-std::vector<int64_t> local_counts(tsdbhip_ctx* c, int64_t G) {
-  std::vector<int64_t> n(G, 0);
+// local series per group id g < G (resident order is group-sorted); cached per loaded batch
+const std::vector<int64_t>& local_counts(tsdbhip_ctx* c, int64_t G) {
+  if (c->lc_valid && (int64_t)c->lc.size() == G) return c->lc;
+  std::vector<int64_t>& n = c->lc;
+  n.assign(G, 0);
   for (int64_t s = 0; s < c->n_series; s++)
     if (c->h_group[s] < G) n[c->h_group[s]]++;   // (the sentinel group of ungrouped series is not one)
+  c->lc_valid = true;
   return n;
 }
 
 // Stages 1-2 of the percentile / median group-by: every local span's contribution to each
 // (group, slot) into c->sel_vals ([series][K], NaN = none), c->sel_uni [G][K], c->gact [G].
+// When the query allows it (no rate, K <= 64, not a percentile downsampling) the downsampling
+// pass writes the contributions itself (GridParams.sel_direct): no bucket values round-trip
+// through pre_dense and no k_emit_vals pass.
 int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G) {
   const int64_t S = c->n_series, K = P.K;
   if (S * K > 0x7FFFFFFFLL) return fail(TSDB_E_NOT_IMPLEMENTED, "percentile group-by over more than 2^31 (series, slot) values");
+  const char* fenv = std::getenv("TSDBHIP_SEL_FUSED");
+  if (P.f != F_SEL && !q->rate && K >= 1 && K <= 64 && !(fenv && fenv[0] == '0')) {
+    const std::vector<int64_t> gsp = seg_ptr(local_counts(c, G));
+    HIP_OK(c->sel_gsp.ensure((G + 1) * 8));
+    HIP_OK(c->sel_vals.ensure(std::max<int64_t>(1, S * K) * 8));
+    HIP_OK(c->sel_uni.ensure(std::max<int64_t>(1, G * K)));
+    HIP_OK(hipMemcpyAsync(c->sel_gsp.p, gsp.data(), (G + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    if (S * K) HIP_OK(hipMemsetD32Async((hipDeviceptr_t)c->sel_vals.p, 0x7FF87FF8, S * K * 2, c->stream));   // +NaN
+    HIP_OK(hipMemsetAsync(c->sel_uni.p, 0, std::max<int64_t>(1, G * K), c->stream));
+    Plan P2;
+    int rc = plan_query(c, q, P2);
+    if (rc) return rc;
+    P2.sel_direct = true;
+    rc = run_device(c, q, P2, G, false);   // sets c->gact like the group-by pass
+    if (rc) return rc;
+    HIP_OK(hipStreamSynchronize(c->stream));   // `gsp` leaves scope
+    return 0;
+  }
   HIP_OK(c->pre_dense.ensure(std::max<int64_t>(1, S * K) * 8));
   HIP_OK(c->pre_pres.ensure(std::max<int64_t>(1, S * K)));
   if (P.f == F_SEL) {
@@ -1730,7 +1763,7 @@ int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G)
 // Stage 3: the order statistic of every (group, slot) column of `vals` (device,
 // [series][K] with counts[g] series in group g) -> c->out_val / c->out_flag [G][K].
 int sel_select(tsdbhip_ctx* c, const Plan& P, int64_t G, double* vals, const std::vector<int64_t>& counts,
-               const uint8_t* uni) {
+               const uint8_t* uni, bool cols = false) {
   const int64_t K = P.K;
   const std::vector<int64_t> gsp = seg_ptr(counts);
   int64_t maxn = 0;
@@ -1742,6 +1775,7 @@ int sel_select(tsdbhip_ctx* c, const Plan& P, int64_t G, double* vals, const std
   HIP_OK(hipMemcpyAsync(c->sel_gsp.p, gsp.data(), (G + 1) * 8, hipMemcpyHostToDevice, c->stream));
   SelParams sp{};
   sp.vals = vals;
+  sp.cols = cols ? 1 : 0;
   sp.scratch = maxn > SEL_CAP ? c->sel_sorted.as<double>() : nullptr;
   sp.uni = uni;
   sp.group_series_ptr = c->sel_gsp.as<int64_t>();
@@ -1751,7 +1785,7 @@ int sel_select(tsdbhip_ctx* c, const Plan& P, int64_t G, double* vals, const std
   sp.out_val = c->out_val.as<double>();
   sp.out_flag = c->out_flag.as<uint8_t>();
   sp.err = c->err.as<int32_t>();
-  HIP_OK(launch_sel_seg(sp, c->stream));
+  HIP_OK(launch_sel_seg(sp, c->stream, maxn));
   return 0;
 }
 

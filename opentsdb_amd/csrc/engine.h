@@ -128,6 +128,9 @@ struct GridParams {
   double* sel_vals;
   uint8_t* sel_uni;            // [G][K]: some series contributed with a real point (emit)
   const int64_t* group_series_ptr;   // [G + 1]
+  // 1: the downsampling pass writes the contributions itself (kcommon.h sel_direct_out;
+  // K <= 64, no rate)
+  int32_t sel_direct;
   // non-null: the grid kernels write every series' bucket values / presence here
   // ([series][K], before rate and fill) instead of its SpanGroup contributions
   double* dense_out;
@@ -155,7 +158,8 @@ struct ReduceParams {
 // Order statistic per (group, slot) (percentile / median group-by aggregator): segment
 // (g, k) is vals[(gsp[g] + i) * K + k], i < gsp[g + 1] - gsp[g].
 struct SelParams {
-  const double* vals;
+  const double* vals;             // [series][K], or (cols) [gsp[g] * K + k * n_g + i]
+  int32_t cols;
   double* scratch;                // [sum n_g * K] key space for segments longer than SEL_CAP
   const uint8_t* uni;             // [G][K]
   const int64_t* group_series_ptr;
@@ -347,7 +351,7 @@ bool pct_rows_supported(int qw, int vl);
 hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s);
 hipError_t launch_emit(const GridParams& p, hipStream_t s);
 hipError_t launch_emit_vals(const GridParams& p, hipStream_t s);
-hipError_t launch_sel_seg(const SelParams& p, hipStream_t s);
+hipError_t launch_sel_seg(const SelParams& p, hipStream_t s, int64_t maxn);
 hipError_t launch_ordered(const OrdParams& p, hipStream_t s);
 hipError_t launch_rank_merge(const RankMergeParams& p, hipStream_t s);
 // per-downsample-function instantiations (k_grid.hip / k_fast.hip, one object per F)

@@ -205,10 +205,6 @@ __device__ __forceinline__ bool select_extreme(int fn, int n, const double* buf,
 
 // ---- order-preserving keys and the wave-local radix select (k_pct's large buckets,
 //      k_raw_sel) ---------------------------------------------------------------------
-__device__ __forceinline__ double canon_nan(double v) {
-  return isnan(v) ? __longlong_as_double(0x7FF8000000000000LL) : v;   // +NaN: the largest key
-}
-
 __device__ __forceinline__ uint64_t f2key(double x) {   // ascending double order == unsigned key order
   const uint64_t b = (uint64_t)__double_as_longlong(x);
   return (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
@@ -1050,7 +1046,7 @@ __device__ uint64_t radix_select(const uint64_t* keys, int64_t n, int64_t r, Sel
 
 // One block per (group, slot).  Blocks are dealt to the 8 XCDs in contiguous runs of
 // segments, so the K columns of one group (interleaved in memory) share an L2.
-__global__ __launch_bounds__(512) void k_sel_seg(SelParams p) {
+__global__ __launch_bounds__(1024) void k_sel_seg(SelParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ SelShared S;
   __shared__ unsigned long long red[2];
@@ -1069,10 +1065,26 @@ __global__ __launch_bounds__(512) void k_sel_seg(SelParams p) {
   if (tid == 0) red[0] = 0;
   __syncthreads();
   uint32_t nan_local = 0;
-  for (int64_t j = tid; j < n; j += blockDim.x) {
-    const double x = p.vals[(gs0 + j) * p.K + k];
-    nan_local += isnan(x) ? 1u : 0u;
-    keys[j] = f2key(canon_nan(x));
+  // SEL_UNROLL independent loads in flight per thread (the column is strided by K: one cache
+  // line per value, so the staging is latency-bound, not bandwidth-bound)
+  constexpr int SEL_UNROLL = 8;
+  const int bs = blockDim.x;
+  for (int64_t j0 = tid; j0 < n; j0 += (int64_t)SEL_UNROLL * bs) {
+    double x[SEL_UNROLL];
+#pragma unroll
+    for (int u = 0; u < SEL_UNROLL; u++) {
+      const int64_t j = j0 + (int64_t)u * bs;
+      const int64_t jj = j < n ? j : j0;
+      x[u] = p.cols ? p.vals[gs0 * p.K + k * n + jj] : p.vals[(gs0 + jj) * p.K + k];
+    }
+#pragma unroll
+    for (int u = 0; u < SEL_UNROLL; u++) {
+      const int64_t j = j0 + (int64_t)u * bs;
+      if (j < n) {
+        nan_local += isnan(x[u]) ? 1u : 0u;
+        keys[j] = f2key(canon_nan(x[u]));
+      }
+    }
   }
   if (nan_local) atomicAdd(&red[0], (unsigned long long)nan_local);
   __syncthreads();
@@ -1107,6 +1119,196 @@ __global__ __launch_bounds__(512) void k_sel_seg(SelParams p) {
       }
       atomicAdd(&red[0], (unsigned long long)le);
       atomicMin(&red[1], (unsigned long long)gt);
+      __syncthreads();
+      v1 = (int64_t)red[0] > r1 ? v0 : key2f(red[1]);
+    }
+  }
+  if (tid == 0) {
+    const double r = m == 0 ? (double)NAN
+                            : select_sorted(p.fn, (int)m, [&](int j) { return (int64_t)j == r0 ? v0 : v1; });
+    if (isinf(r)) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // AggregationIterator.doubleValue :640-643
+    p.out_val[i] = r;
+    p.out_flag[i] = 1;
+  }
+}
+
+// k_sel_reg: k_sel_seg for segments of at most SEL_REG_T * SEL_REG_R values, the keys held in
+// registers (SEL_REG_R per thread) instead of staged in LDS: no 96 KB LDS buffer, so two
+// blocks share a CU, and every radix pass reads registers.  Same ranks, same result.
+constexpr int SEL_REG_T = 1024;
+constexpr int SEL_REG_R = 12;
+
+__device__ __forceinline__ uint64_t wave_and_u64(uint64_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x &= shfl_u64(x, lane_id() ^ d);
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_or_u64(uint64_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x |= shfl_u64(x, lane_id() ^ d);
+  return x;
+}
+
+template <int R>
+__device__ uint64_t reg_radix_select(const uint64_t (&key)[R], uint32_t valid, int64_t r, SelShared& S,
+                                     unsigned long long* red) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  uint64_t kand = ~0ULL, kor = 0;
+#pragma unroll
+  for (int u = 0; u < R; u++) {
+    if (valid >> u & 1) {
+      kand &= key[u];
+      kor |= key[u];
+    }
+  }
+  kand = wave_and_u64(kand);
+  kor = wave_or_u64(kor);
+  if (tid == 0) { red[0] = ~0ULL; red[1] = 0; }
+  __syncthreads();
+  if (lane == 0) {
+    atomicAnd(&red[0], (unsigned long long)kand);
+    atomicOr(&red[1], (unsigned long long)kor);
+  }
+  __syncthreads();
+  const uint64_t band = red[0], bor = red[1];
+  if ((band ^ bor) == 0) return band;   // all keys equal
+  const int top = (63 - __clzll((long long)(band ^ bor))) & ~7;
+  uint64_t mask = top == 56 ? 0 : ~((1ULL << (top + 8)) - 1ULL);
+  uint64_t prefix = band & mask;
+  for (int shift = top; shift >= 0; shift -= 8) {
+    for (int b = tid; b < 256; b += blockDim.x) S.hist[b] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < R; u++)
+      if ((valid >> u & 1) && (key[u] & mask) == prefix) atomicAdd(&S.hist[(key[u] >> shift) & 255], 1u);
+    __syncthreads();
+    if (tid < 64) {
+      uint32_t c[4], t = 0;
+#pragma unroll
+      for (int q = 0; q < 4; q++) { c[q] = S.hist[tid * 4 + q]; t += c[q]; }
+      const int64_t incl = wave_incl_sum((int)t);
+      int64_t ex = incl - t;
+      if (ex <= r && r < incl) {
+        int q = 0;
+        for (; q < 3; q++) {
+          if (r < ex + c[q]) break;
+          ex += c[q];
+        }
+        S.bin = (uint64_t)(tid * 4 + q);
+        S.rr = (uint64_t)(r - ex);
+        S.ncand = c[q];
+      }
+    }
+    __syncthreads();
+    prefix |= S.bin << shift;
+    mask |= 255ULL << shift;
+    r = (int64_t)S.rr;
+    const uint32_t nc = S.ncand;
+    __syncthreads();
+    if (shift == 0) break;
+    if (nc <= SEL_FIN) {
+      if (tid == 0) S.ncand = 0;
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < R; u++)
+        if ((valid >> u & 1) && (key[u] & mask) == prefix) S.cand[atomicAdd(&S.ncand, 1u)] = key[u];
+      __syncthreads();
+      if ((uint32_t)tid < nc) {
+        const uint64_t x = S.cand[tid];
+        uint32_t less = 0, eq = 0;
+        for (uint32_t q = 0; q < nc; q++) {
+          const uint64_t y = S.cand[q];
+          less += y < x;
+          eq += y == x;
+        }
+        if ((int64_t)less <= r && r < (int64_t)(less + eq)) S.res = x;
+      }
+      __syncthreads();
+      const uint64_t res = S.res;
+      __syncthreads();
+      return res;
+    }
+  }
+  return prefix;
+}
+
+template <int OCC>
+__global__ __launch_bounds__(SEL_REG_T, OCC) void k_sel_reg(SelParams p) {
+  __shared__ SelShared S;
+  __shared__ unsigned long long red[2];
+  const int64_t nseg = p.G * p.K;
+  const int64_t per = (nseg + 7) / 8;
+  const int64_t i = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (i >= nseg) return;
+  const int tid = threadIdx.x;
+  if (!p.uni[i]) {
+    if (tid == 0) { p.out_val[i] = 0.0; p.out_flag[i] = 0; }
+    return;
+  }
+  const int64_t g = i / p.K, k = i - g * p.K;
+  const int64_t gs0 = p.group_series_ptr[g], n = p.group_series_ptr[g + 1] - gs0;
+  // all loads issued before any is consumed (strided column: latency-bound)
+  double x[SEL_REG_R];
+#pragma unroll
+  for (int u = 0; u < SEL_REG_R; u++) {
+    const int64_t j = tid + (int64_t)u * SEL_REG_T;
+    const int64_t jj = j < n ? j : 0;
+    x[u] = p.cols ? p.vals[gs0 * p.K + k * n + jj] : p.vals[(gs0 + jj) * p.K + k];
+  }
+  uint64_t key[SEL_REG_R];
+  uint32_t valid = 0;
+  int nan_local = 0;
+#pragma unroll
+  for (int u = 0; u < SEL_REG_R; u++) {
+    const bool v = tid + (int64_t)u * SEL_REG_T < n;
+    valid |= (v ? 1u : 0u) << u;
+    nan_local += (v && isnan(x[u])) ? 1 : 0;
+    key[u] = f2key(canon_nan(x[u]));
+  }
+  nan_local = wave_sum_int(nan_local);
+  if (tid == 0) red[0] = 0;
+  __syncthreads();
+  if ((tid & 63) == 0 && nan_local) atomicAdd(&red[0], (unsigned long long)nan_local);
+  __syncthreads();
+  const int64_t m = n - (int64_t)red[0];   // non-NaN values (they hold ranks 0 .. m-1)
+  __syncthreads();
+  int64_t r0 = 0, r1 = -1;
+  if (m > 0) {
+    if (p.fn == TSDB_AGG_MEDIAN) {
+      r0 = m / 2;
+    } else if (m > 1) {
+      const double q = pct_quantile(p.fn) / 100.0;
+      const double pos = (q == 0.0) ? 0.0 : (q == 1.0 ? (double)m : q * (double)(m + 1));
+      if (pos < 1) r0 = 0;
+      else if (pos >= (double)m) r0 = m - 1;
+      else { r0 = (int64_t)floor(pos) - 1; r1 = r0 + 1; }
+    }
+  }
+  double v0 = NAN, v1 = NAN;
+  if (m > 0) {
+    const uint64_t k0 = reg_radix_select<SEL_REG_R>(key, valid, r0, S, red);
+    v0 = key2f(k0);
+    if (r1 >= 0) {
+      // rank r0 + 1: the same key when more than r0 + 1 keys are <= k0, else the next larger key
+      __syncthreads();
+      if (tid == 0) { red[0] = 0; red[1] = ~0ULL; }
+      __syncthreads();
+      int le = 0;
+      uint64_t gt = ~0ULL;
+#pragma unroll
+      for (int u = 0; u < SEL_REG_R; u++) {
+        if (valid >> u & 1) {
+          if (key[u] <= k0) le++;
+          else gt = key[u] < gt ? key[u] : gt;
+        }
+      }
+      le = wave_sum_int(le);
+      gt = wave_min_u64(gt);
+      if ((tid & 63) == 0) {
+        atomicAdd(&red[0], (unsigned long long)le);
+        atomicMin(&red[1], (unsigned long long)gt);
+      }
       __syncthreads();
       v1 = (int64_t)red[0] > r1 ? v0 : key2f(red[1]);
     }
@@ -1165,14 +1367,23 @@ hipError_t launch_emit_vals(const GridParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_sel_seg(const SelParams& p, hipStream_t s) {
+hipError_t launch_sel_seg(const SelParams& p, hipStream_t s, int64_t maxn) {
   const int64_t n = p.G * p.K;
   if (n == 0) return hipSuccess;
   const int64_t per = (n + 7) / 8;
+  const char* renv = std::getenv("TSDBHIP_SEL_REG");
+  if (maxn <= (int64_t)SEL_REG_T * SEL_REG_R && !(renv && renv[0] == '0')) {
+    // two blocks per CU (8 waves / SIMD, a few spilled registers) beat one: config 3 p99
+    // 11.4 vs 13.3 ms per step
+    const char* oenv = std::getenv("TSDBHIP_SEL_OCC");
+    if (oenv && oenv[0] == '4') hipLaunchKernelGGL(k_sel_reg<4>, dim3((unsigned)(per * 8)), dim3(SEL_REG_T), 0, s, p);
+    else hipLaunchKernelGGL(k_sel_reg<8>, dim3((unsigned)(per * 8)), dim3(SEL_REG_T), 0, s, p);
+    return hipGetLastError();
+  }
   const size_t lds = (size_t)SEL_CAP * 8;
   hipError_t e = hipFuncSetAttribute((const void*)k_sel_seg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_sel_seg, dim3((unsigned)(per * 8)), dim3(512), lds, s, p);
+  hipLaunchKernelGGL(k_sel_seg, dim3((unsigned)(per * 8)), dim3(1024), lds, s, p);
   return hipGetLastError();
 }
 

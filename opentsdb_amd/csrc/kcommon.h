@@ -987,43 +987,39 @@ __device__ __forceinline__ void emit_series(const GridParams& p, const WaveLds& 
   emit_series_to(p, W, K, [&](int s, double v, bool uni) { contribute(ga, W.part, s, v, uni); });
 }
 
-// End of series s: its SpanGroup contributions, or (dense_out) its bucket values.
-__device__ __forceinline__ void series_out(const GridParams& p, const WaveLds& W, int K, int64_t s) {
-  if (p.dense_out) {
-    const int lane = lane_id();
-    WAVE_SYNC();
-    for (int k = lane; k < K; k += 64) {
-      p.dense_out[s * K + k] = W.dense[k];
-      p.pres_out[s * K + k] = W.pres[k];
-    }
-    WAVE_SYNC();
-    return;
-  }
-  emit_series(p, W, K);
-}
-
 // emit_series for K <= 64 without rate: lane k owns slot k; the series' bucket k arrives
 // in registers (pr, v) and the tile partial of slot k lives in the lane's registers, so
 // neither the bucket values nor the partials round-trip through LDS.  Same contributions,
 // same per-slot order (one per series) as emit_series.
-__device__ __forceinline__ void emit_series_reg(const GridParams& p, int K, bool pr_in, double v, RegPart& P) {
+__device__ __forceinline__ double canon_nan(double v) {
+  return isnan(v) ? __longlong_as_double(0x7FF8000000000000LL) : v;   // +NaN: the largest key
+}
+
+// The SpanGroup contribution of lane k's slot (K <= 64, no rate): the bucket value, its LERP
+// between the neighbouring present buckets, the fill value, or none (returns false).  *uni:
+// the slot holds a real bucket of the span (a union timestamp).  Called by the whole wave.
+__device__ __forceinline__ bool slot_contribution(const GridParams& p, int K, bool pr_in, double v, double& cv,
+                                                  bool& uni) {
   const int lane = lane_id();
   const bool inK = lane < K;
   const bool pr = inK && pr_in;
+  uni = false;
   if (p.fill != TSDB_FILL_NONE && p.mode != MODE_ALL) {
     // FillingDownsampler (:172-301): every slot, missing -> NaN / 0 / RuntimeException
     const double fillv = (p.fill == TSDB_FILL_ZERO) ? 0.0 : (double)NAN;
-    if (inK) {
-      if (!pr && p.fill == TSDB_FILL_SCALAR) set_err(p.err, TSDB_E_RUNTIME);
-      contribute_slot(p.ga, P, pr ? v : fillv, true);
-    }
-    return;
+    if (!inK) return false;
+    if (!pr && p.fill == TSDB_FILL_SCALAR) set_err(p.err, TSDB_E_RUNTIME);
+    if (lane == 0 && p.skip0) return false;   // before start_time: AggregationIterator ctor :424-441
+    cv = pr ? v : fillv;
+    uni = true;
+    return true;
   }
   // previous and next present slot of every lane, from the presence ballot
   const uint64_t pm = __ballot(pr);
   if (pm == (K >= 64 ? ~0ull : ((1ull << K) - 1))) {   // every slot present: no interpolation
-    if (inK) contribute_slot(p.ga, P, v, true);
-    return;
+    cv = v;
+    uni = inK;
+    return inK;
   }
   const uint64_t below = pm & ((1ull << lane) - 1);
   const uint64_t above = lane == 63 ? 0ull : (pm & ~((2ull << lane) - 1));
@@ -1035,8 +1031,61 @@ __device__ __forceinline__ void emit_series_reg(const GridParams& p, int K, bool
     y0 = __shfl(v, max(prv, 0), 64);
     y1 = __shfl(v, min(nxt, 63), 64);
   }
-  if (pr) contribute_slot(p.ga, P, v, true);
-  else if (inK && prv >= 0 && nxt < K) contribute_slot(p.ga, P, interp(p.interp, p, prv, y0, nxt, y1, lane), false);
+  if (pr) {
+    cv = v;
+    uni = true;
+    return true;
+  }
+  if (need) {
+    cv = interp(p.interp, p, prv, y0, nxt, y1, lane);
+    return true;
+  }
+  return false;
+}
+
+__device__ __forceinline__ void emit_series_reg(const GridParams& p, int K, bool pr_in, double v, RegPart& P) {
+  double cv;
+  bool uni;
+  if (slot_contribution(p, K, pr_in, v, cv, uni)) contribute_slot(p.ga, P, cv, uni);
+}
+
+// Percentile / median (and ordered) group-by, fused into the downsampling pass (p.sel_direct,
+// K <= 64, no rate): series s of group g writes its contribution to every slot straight into
+// sel_vals[s * K + k] (one coalesced row per series; the fill pattern where it has none) and
+// marks the union slots -- k_emit_vals' output without the bucket values round-tripping
+// through pre_dense.
+__device__ __forceinline__ void sel_direct_out(const GridParams& p, int K, int32_t g, int64_t s, bool pr_in,
+                                               double v) {
+  double cv = 0.0;
+  bool uni;
+  const bool has = slot_contribution(p, K, pr_in, v, cv, uni);
+  const int lane = lane_id();
+  if (lane < K) p.sel_vals[s * K + lane] = has ? canon_nan(cv) : __longlong_as_double(0x7FF87FF87FF87FF8LL);
+  if (uni) p.sel_uni[(int64_t)g * K + lane] = 1;
+}
+
+// End of series s (group g): its SpanGroup contributions, (dense_out) its bucket values, or
+// (sel_direct) its percentile group-by contributions.
+__device__ __forceinline__ void series_out(const GridParams& p, const WaveLds& W, int K, int64_t s, int32_t g) {
+  if (p.sel_direct) {   // K <= 64 (host-checked)
+    const int lane = lane_id();
+    WAVE_SYNC();
+    const bool pr = lane < K && W.pres[lane] != 0;
+    sel_direct_out(p, K, g, s, pr, pr ? W.dense[lane] : 0.0);
+    WAVE_SYNC();
+    return;
+  }
+  if (p.dense_out) {
+    const int lane = lane_id();
+    WAVE_SYNC();
+    for (int k = lane; k < K; k += 64) {
+      p.dense_out[s * K + k] = W.dense[k];
+      p.pres_out[s * K + k] = W.pres[k];
+    }
+    WAVE_SYNC();
+    return;
+  }
+  emit_series(p, W, K);
 }
 
 // Next row of the tile inside the scan range, starting at (s, r) inclusive.
@@ -1173,7 +1222,7 @@ __global__ __launch_bounds__(256) void k_grid(GridParams p) {
         }
       }
       if (slow) series_slow<F>(p, W, cs, K);
-      series_out(p, W, K, cs);
+      series_out(p, W, K, cs, p.tile_group[tile]);
       // next series
       for (int k = lane; k < K; k += 64) W.pres[k] = 0;
       WAVE_SYNC();
@@ -1599,7 +1648,7 @@ __device__ __forceinline__ double fast_bucket_value(uint32_t c, double a) {
 // K <= 64, no rate: the register-partial variant (emit_series_reg).
 template <int F>
 __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const FastLds& L, int K, int lsb, double amax,
-                                                    RegPart& P, int64_t s, uint32_t nbound = 0) {
+                                                    RegPart& P, int64_t s, int32_t g, uint32_t nbound = 0) {
   const int lane = lane_id();
   WAVE_SYNC();
   uint32_t c = 0;
@@ -1614,7 +1663,9 @@ __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const F
     const uint32_t nmax = (uint32_t)wave_max((int)c);
     if (!fast_cert<F>(nmax, lsb, amax)) return false;
   }
-  if (p.dense_out) {
+  if (p.sel_direct) {
+    sel_direct_out(p, K, g, s, c != 0, fast_bucket_value<F>(c, a));
+  } else if (p.dense_out) {
     if (lane < K) {
       p.dense_out[s * K + lane] = fast_bucket_value<F>(c, a);
       p.pres_out[s * K + lane] = c != 0;
@@ -1632,7 +1683,7 @@ __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const F
 
 template <int F>
 __device__ __forceinline__ bool fast_series_end(const GridParams& p, const FastLds& L, int K, int lsb, double amax,
-                                                int64_t s) {
+                                                int64_t s, int32_t g) {
   const int lane = lane_id();
   WAVE_SYNC();
   uint32_t nmax = 0;
@@ -1657,7 +1708,7 @@ __device__ __forceinline__ bool fast_series_end(const GridParams& p, const FastL
                                    (double)nmax * A * (1.0 + 1e-12) <= ldexp(1.0, 52 + Lb));
     if (!ok) return false;
   }
-  series_out(p, L.w, K, s);
+  series_out(p, L.w, K, s, g);
   for (int k = lane; k < K; k += 64) {
     L.acc[k] = fast_identity<F>();
     L.cnt[k] = 0;
@@ -1722,13 +1773,14 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
         if (!(mb & FM_OK) || (mb & FM_NEWSER)) {
           if (have) {
             int64_t s = -1;
-            if (p.dense_out) {   // the series of the last row folded (dense output only)
+            if (p.dense_out || p.sel_direct) {   // the series of the last row folded (dense output only)
               const int64_t row = w.r0 + last_rrel;
               s = tbeg[tile];
               while (s + 1 < tend[tile] && srp[s + 1] <= row) s++;
             }
             const bool ok =
-                KR ? fast_series_end_reg<F>(p, L, K, lsb, amax, RP, s) : fast_series_end<F>(p, L, K, lsb, amax, s);
+                KR ? fast_series_end_reg<F>(p, L, K, lsb, amax, RP, s, p.tile_group[tile])
+                   : fast_series_end<F>(p, L, K, lsb, amax, s, p.tile_group[tile]);
             if (!ok) { redo = true; done = true; }
           }
           lsb = INT32_MAX;
@@ -1894,8 +1946,8 @@ __global__ __launch_bounds__(256, SHORT_OCC) void k_short(GridParams p, const Ro
     const int lsb = __builtin_amdgcn_readlane(dlsb, j);
     const double amax = __longlong_as_double((long long)rl64(damax, j));
     const bool fine =
-        KR ? fast_series_end_reg<F>(p, L, K, lsb, amax, RP, s0 + j, (uint32_t)nv0)
-           : fast_series_end<F>(p, L, K, lsb, amax, s0 + j);
+        KR ? fast_series_end_reg<F>(p, L, K, lsb, amax, RP, s0 + j, p.tile_group[tile], (uint32_t)nv0)
+           : fast_series_end<F>(p, L, K, lsb, amax, s0 + j, p.tile_group[tile]);
     if (!fine) redo = true;
   };
   int j = 0;
