@@ -596,6 +596,9 @@ __global__ __launch_bounds__(256) void k_emit(GridParams p) {
 // p.redo_list for k_pct (which recomputes it whole).
 
 static constexpr int EXT_MAX = 24;
+#ifndef PCT_KEYS_OCC
+#define PCT_KEYS_OCC 1   // min waves / SIMD the key kernel is compiled for (8: 18.7 ms with spills vs 18.1 at 7)
+#endif
 
 // DPP int min across the wave (uniform result)
 __device__ __forceinline__ int wave_min_dpp(int x) {
@@ -759,9 +762,139 @@ __device__ __forceinline__ bool select_keep(const double val[DPL], uint32_t keep
   return true;
 }
 
+// ---- one-bucket rows of 4-byte values: order statistics over 32-bit keys ----------------
+// A 1 h bucket in a row of 4-byte values that are all float32 (or all int32): the values map
+// to order-preserving uint32 keys (NaN and absent datapoints -> 0, below every key), each lane
+// sorts its 8 keys once, and the k-th largest is found by popping the wave maximum of the lane
+// heads -- every lane holding the maximum pops it at once, so a round costs one DPP max and a
+// shift of the popped lanes' lists.  The arithmetic is 32-bit until the two selected values are
+// converted back (exact: float32 / int32 -> double), so the result equals select_keep's.
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+__device__ __forceinline__ void cas_desc(uint32_t& a, uint32_t& b) {
+  const uint32_t hi = max(a, b), lo = min(a, b);
+  a = hi;
+  b = lo;
+}
+
+// 8 keys, descending (Batcher's odd-even merge network, 19 comparators)
+__device__ __forceinline__ void sort8_desc(uint32_t k[DPL]) {
+  cas_desc(k[0], k[1]); cas_desc(k[2], k[3]); cas_desc(k[4], k[5]); cas_desc(k[6], k[7]);
+  cas_desc(k[0], k[2]); cas_desc(k[1], k[3]); cas_desc(k[4], k[6]); cas_desc(k[5], k[7]);
+  cas_desc(k[1], k[2]); cas_desc(k[5], k[6]);
+  cas_desc(k[0], k[4]); cas_desc(k[1], k[5]); cas_desc(k[2], k[6]); cas_desc(k[3], k[7]);
+  cas_desc(k[2], k[4]); cas_desc(k[3], k[5]);
+  cas_desc(k[1], k[2]); cas_desc(k[3], k[4]); cas_desc(k[5], k[6]);
+}
+
+// k-th and (k-1)-th largest key (k >= 1) of the wave's keys (0 = none); sorts k[] in place
+__device__ __forceinline__ void topk_u32(uint32_t k[DPL], int kk, uint32_t& ek, uint32_t& ek1) {
+  sort8_desc(k);
+  int cum = 0;
+  ek = ek1 = 0;
+  while (cum < kk) {
+    const uint32_t w = wave_max_u32(k[0]);
+    const bool pop = k[0] == w;
+    const int c = __popcll(__ballot(pop));
+    if (cum < kk - 1 && kk - 1 <= cum + c) ek1 = w;
+    if (kk <= cum + c) ek = w;
+    cum += c;
+    if (pop) {
+#pragma unroll
+      for (int j = 0; j < DPL - 1; j++) k[j] = k[j + 1];
+      k[DPL - 1] = 0;
+    }
+  }
+}
+
+// float32 bits / int32 -> order key (> 0); NaN -> 0
+__device__ __forceinline__ uint32_t key32(uint32_t bits, bool isf) {
+  if (!isf) return bits ^ 0x80000000u;
+  if ((bits & 0x7FFFFFFFu) > 0x7F800000u) return 0u;   // NaN
+  return (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u);
+}
+__device__ __forceinline__ double unkey32(uint32_t k, bool isf) {
+  if (!isf) return (double)(int32_t)(k ^ 0x80000000u);
+  return (double)__uint_as_float((k & 0x80000000u) ? (k ^ 0x80000000u) : ~k);
+}
+
+// The statistic of a one-bucket row of 4-byte values; false = not this path's case (mixed
+// float / int row, or the statistic too far from both ends): the caller takes select_keep.
+template <int QW>
+__device__ __forceinline__ int pct_row_keys(const GridParams& p, const RowLite& d, const RawT<QW, 4>& rw, double q,
+                                            double& x) {
+  const int i0 = lane_id() * DPL;
+  const int nv = max(0, min(DPL, (int)d.ndp - i0));
+  uint32_t key[DPL];
+  bool ok = true, anyf = false, anyi = false;
+  int n = 0;
+  const uint32_t* vw = &rw.v[0].x;
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    uint32_t off, fl;
+    if (QW == 2) {
+      const uint32_t be = __builtin_bswap32((&rw.q[0].x)[j >> 1]);
+      const uint32_t qq = (j & 1) ? (be & 0xFFFF) : (be >> 16);
+      off = (qq >> 4) * 1000u;
+      fl = qq & 0xF;
+    } else {
+      const uint32_t qq = __builtin_bswap32((&rw.q[0].x)[j]);
+      off = (qq & 0x0FFFFFC0u) >> 6;
+      fl = qq & 0xF;
+    }
+    const bool v = j < nv;
+    const bool isf = (fl & 8) != 0;
+    ok = ok && (!v || off < 3600000u);
+    anyf = anyf || (v && isf);
+    anyi = anyi || (v && !isf);
+    key[j] = v ? key32(__builtin_bswap32(vw[j]), isf) : 0u;
+    n += key[j] != 0;
+  }
+  if (__ballot(!ok)) return -1;   // offset >= 1 h: hand the series back
+  const bool wf = __ballot(anyf) != 0, wi = __ballot(anyi) != 0;
+  if (wf && wi) return 0;   // mixed row
+  n = __builtin_amdgcn_readlane(wave_incl_sum_dpp(n), 63);
+  if (n == 0) {
+    x = (double)NAN;
+    return 1;
+  }
+  // select_sorted / select_extreme: LEGACY pos = p (n + 1)
+  const double pos = q * (double)(n + 1);
+  const int ip = (int)floor(pos);
+  int lo_i, hi_i;
+  if (pos < 1) { lo_i = hi_i = 0; }
+  else if (pos >= (double)n) { lo_i = hi_i = n - 1; }
+  else { lo_i = ip - 1; hi_i = ip; }
+  const int ktop = n - lo_i, kbot = hi_i + 1;
+  if (min(ktop, kbot) > EXT_MAX) return 0;
+  double a, b;
+  uint32_t ek, ek1;
+  if (ktop <= kbot) {
+    topk_u32(key, ktop, ek, ek1);
+    a = unkey32(ek, wf);
+    b = (hi_i == lo_i) ? a : unkey32(ek1, wf);
+  } else {
+#pragma unroll
+    for (int j = 0; j < DPL; j++) key[j] = key[j] ? ~key[j] : 0u;   // ascending order as descending keys
+    topk_u32(key, kbot, ek, ek1);
+    b = unkey32(~ek, wf);
+    a = (hi_i == lo_i) ? b : unkey32(~ek1, wf);
+  }
+  x = (lo_i == hi_i) ? a : a + (pos - floor(pos)) * (b - a);
+  return 1;
+}
+
 // one in-range row: its buckets' order statistics into dense / pres; false = hand the
 // series back (offset >= 1 h, or a statistic more than EXT_MAX from both ends)
-template <int QW, int VL>
+template <int QW, int VL, bool KEYS>
 __device__ __forceinline__ bool pct_row(const GridParams& p, const RowLite& cd, const RawT<QW, VL>& rc, double q,
                                         double* dense, uint8_t* pres) {
   const int lane = lane_id();
@@ -773,6 +906,19 @@ __device__ __forceinline__ bool pct_row(const GridParams& p, const RowLite& cd, 
   const int slot0 = (int)__builtin_amdgcn_readfirstlane((int)((double)rel / (double)p.I));
   const bool one = p.I == 3600000;
   if (one && (slot0 < 0 || slot0 >= (int)p.K)) return true;   // the row's bucket is out of range
+  if constexpr (KEYS) {
+    // 1 h buckets of 4-byte values (host-checked): the key path alone, the rest to k_pct
+    if constexpr (VL == 4) {
+      if (d.ndp == 0) return true;
+      double x;
+      const int r = pct_row_keys<QW>(p, d, rc, q, x);
+      if (r <= 0) return false;
+      if (lane == 0) { dense[slot0] = x; pres[slot0] = 1; }
+      return true;
+    } else {
+      return false;
+    }
+  } else {
   int slot[DPL];
   double val[DPL];
   const bool ok = decode_row<QW, VL>(p, d, slot0, one, rc, slot, val);
@@ -815,10 +961,11 @@ __device__ __forceinline__ bool pct_row(const GridParams& p, const RowLite& cd, 
     if (lane == 0) { dense[mn] = x; pres[mn] = 1; }
   }
   return true;
+  }
 }
 
-template <int QW, int VL, int D>
-__global__ __launch_bounds__(256) void k_pct_rows(GridParams p) {
+template <int QW, int VL, int D, bool KEYS>
+__global__ __launch_bounds__(256, KEYS ? PCT_KEYS_OCC : 1) void k_pct_rows(GridParams p) {
   const int lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t s = (int64_t)blockIdx.x * 4 + wave;
@@ -878,7 +1025,7 @@ __global__ __launch_bounds__(256) void k_pct_rows(GridParams p) {
         rl[D - 1] = row_of_lane(d, lo + t + D - 1);
         load_row<QW, VL>(p, rl[D - 1], ring[D - 1]);
       }
-      if (!pct_row<QW, VL>(p, rl[0], ring[0], q, dense, pres)) {
+      if (!pct_row<QW, VL, KEYS>(p, rl[0], ring[0], q, dense, pres)) {
         if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)s;
         return;
       }
@@ -1391,12 +1538,22 @@ hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s) {
   if (p.n_series == 0) return hipSuccess;
   const dim3 grid((unsigned)((p.n_series + 3) / 4)), block(256);
   const char* denv = std::getenv("TSDBHIP_PCTD");
-  const int D = denv ? std::atoi(denv) : 3;
+  // ring depth: 3 rows for the general kernel; 2 for the key kernel (config 5 1h-p99: 18.1 /
+  // 19.7 / 22.0 ms at D = 2 / 3 / 4 -- occupancy beats depth)
+  const int D = denv ? std::atoi(denv) : (vl == 4 && p.I == 3600000 ? 2 : 3);
+  // 1 h buckets of 4-byte values: the 32-bit key kernel (its misses go to k_pct)
+  const bool keys = vl == 4 && p.I == 3600000 && !(std::getenv("TSDBHIP_PCT_KEYS") && std::getenv("TSDBHIP_PCT_KEYS")[0] == '0');
 #define PCT_ROWS_CASE(Q, V)                                                                                  \
   if (qw == Q && vl == V) {                                                                                \
-    if (D == 2) hipLaunchKernelGGL((k_pct_rows<Q, V, 2>), grid, block, 0, s, p);                          \
-    else if (D == 4) hipLaunchKernelGGL((k_pct_rows<Q, V, 4>), grid, block, 0, s, p);                     \
-    else hipLaunchKernelGGL((k_pct_rows<Q, V, 3>), grid, block, 0, s, p);                                 \
+    if (V == 4 && keys) {                                                                                  \
+      if (D == 2) hipLaunchKernelGGL((k_pct_rows<Q, V, 2, true>), grid, block, 0, s, p);                   \
+      else if (D == 4) hipLaunchKernelGGL((k_pct_rows<Q, V, 4, true>), grid, block, 0, s, p);              \
+      else hipLaunchKernelGGL((k_pct_rows<Q, V, 3, true>), grid, block, 0, s, p);                          \
+      return hipGetLastError();                                                                            \
+    }                                                                                                      \
+    if (D == 2) hipLaunchKernelGGL((k_pct_rows<Q, V, 2, false>), grid, block, 0, s, p);                    \
+    else if (D == 4) hipLaunchKernelGGL((k_pct_rows<Q, V, 4, false>), grid, block, 0, s, p);               \
+    else hipLaunchKernelGGL((k_pct_rows<Q, V, 3, false>), grid, block, 0, s, p);                           \
     return hipGetLastError();                                                                              \
   }
   PCT_ROWS_CASE(2, 1) PCT_ROWS_CASE(2, 2) PCT_ROWS_CASE(2, 4) PCT_ROWS_CASE(2, 8)
