@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define TSDBHIP_ABI_VERSION 4
+#define TSDBHIP_ABI_VERSION 5
 
 /* ---- error codes: one per Java exception on the path --------------------- */
 enum {
@@ -89,6 +89,21 @@ typedef struct {
                                       aggregators, still emitted by NONE (TsdbQuery.java:940-961) */
 } tsdbhip_batch;
 
+/* ---- Time zone of a calendar downsampling --------------------------------
+ * DownsamplingSpecification.setTimezone (src/core/DownsamplingSpecification.java:199-207):
+ * the zone's UTC offset history as a transition table that the host builds from its own
+ * time-zone database (a JVM host: ZoneId.of(id).getRules() -- getTransitions(), plus
+ * getTransitionRules() expanded over the query range), so that the engine reproduces
+ * java.util.GregorianCalendar's arithmetic in that zone (ZoneInfo.getOffsets by UTC time,
+ * getOffsetsByWall for local fields).  offset_ms[0] holds before utc_ms[0] and offset_ms[i + 1]
+ * from utc_ms[i] on; the table must cover the query's time range.  The engine reads it during
+ * tsdbhip_run only. */
+typedef struct {
+  int32_t n;                   /* transitions */
+  const int64_t* utc_ms;       /* [n] ascending instants */
+  const int32_t* offset_ms;    /* [n + 1] total offset (raw + DST), ms east of UTC */
+} tsdbhip_tz;
+
 /* ---- Query: TsdbQuery state that reaches the aggregation path ------------- */
 typedef struct {
   int64_t start_time;        /* TsdbQuery.setStartTime: unix seconds or ms (TsdbQuery.java:262-289) */
@@ -107,6 +122,7 @@ typedef struct {
   int32_t flags;             /* TSDB_QF_* */
   int64_t rate_counter_max;  /* default Long.MAX_VALUE */
   int64_t rate_reset_value;  /* default 0 */
+  const tsdbhip_tz* ds_tz;   /* calendar time zone; NULL = UTC (the DownsamplingSpecification default) */
 } tsdbhip_query;
 
 /* Calendar units of a 'c' downsampling interval (DateTime.unitsToCalendarType,

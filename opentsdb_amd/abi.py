@@ -88,6 +88,15 @@ class Batch(C.Structure):
     ]
 
 
+class TZ(C.Structure):
+    """tsdbhip_tz: a zone's UTC offset transition table (see opentsdb_amd/tz.py)."""
+    _fields_ = [
+        ("n", C.c_int32),
+        ("utc_ms", C.POINTER(C.c_int64)),
+        ("offset_ms", C.POINTER(C.c_int32)),
+    ]
+
+
 class Query(C.Structure):
     _fields_ = [
         ("start_time", C.c_int64),
@@ -104,6 +113,7 @@ class Query(C.Structure):
         ("flags", C.c_int32),
         ("rate_counter_max", C.c_int64),
         ("rate_reset_value", C.c_int64),
+        ("ds_tz", C.POINTER(TZ)),
     ]
 
 
@@ -179,7 +189,7 @@ def new_query(start_time: int, end_time: int, aggregator: str | int = "sum", *,
               ds_function: int = -1, ds_interval_ms: int = 0, ds_fill: int = FILL_NONE,
               ds_all: bool = False, rate: bool = False, counter: bool = False,
               counter_max: int = LONG_MAX, reset_value: int = 0, drop_resets: bool = False,
-              flags: int = 0) -> Query:
+              flags: int = 0, tz=None) -> Query:
     q = Query()
     q.start_time = start_time
     q.end_time = end_time
@@ -195,7 +205,19 @@ def new_query(start_time: int, end_time: int, aggregator: str | int = "sum", *,
     q.rate_counter_max = counter_max
     q.rate_reset_value = reset_value
     q.flags = flags
+    if tz is not None:
+        set_timezone(q, tz)
     return q
+
+
+def set_timezone(q: Query, tz) -> None:
+    """The calendar time zone of q: a zone id (tz.table) or a tz.TzTable; None = UTC."""
+    if tz is None:
+        q.ds_tz = C.POINTER(TZ)()
+        return
+    from . import tz as _tz
+    t = tz if isinstance(tz, _tz.TzTable) else _tz.table(tz)
+    q.ds_tz = C.pointer(t.struct)   # the struct keeps the table's arrays alive
 
 
 def _ptr(a: np.ndarray, ctype):

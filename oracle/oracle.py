@@ -43,6 +43,9 @@ def lib():
         L.ref_view_downsampler.restype = vp
         L.ref_view_downsampler.argtypes = [vp, C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_int64, C.c_int64,
                                            C.c_int64, C.c_int64, C.c_int32]
+        L.ref_view_downsampler_tz.restype = vp
+        L.ref_view_downsampler_tz.argtypes = [vp, C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_int64, C.c_int64,
+                                              C.c_int64, C.c_int64, C.c_int32, C.POINTER(abi.TZ)]
         L.ref_view_rate.restype = vp
         L.ref_view_rate.argtypes = [vp, C.c_int32, C.c_int64, C.c_int64, C.c_int32]
         L.ref_view_aggregate.restype = vp
@@ -172,14 +175,21 @@ def parse_downsample(spec: str) -> abi.Query:
 
 
 def downsampler(src: View, spec: str, start_time: int = 0, end_time: int = 0,
-                query_start: int = 0, query_end: int = abi.LONG_MAX) -> View:
-    """Downsampler (fill none) or FillingDownsampler, as Span.downsampler builds them."""
+                query_start: int = 0, query_end: int = abi.LONG_MAX, tz=None) -> View:
+    """Downsampler (fill none) or FillingDownsampler, as Span.downsampler builds them; tz: the
+    specification's time zone (a zone id or opentsdb_amd.tz.TzTable; None = UTC)."""
     q = parse_downsample(spec)
-    ptr = lib().ref_view_downsampler(src._take(), q.ds_function, q.ds_interval_ms, q.ds_fill, q.ds_all,
-                                     start_time, end_time, query_start, query_end, q.ds_calendar)
+    tzs = None
+    if tz is not None:
+        from opentsdb_amd import tz as _tz
+        tzs = (tz if isinstance(tz, _tz.TzTable) else _tz.table(tz)).struct
+    ptr = lib().ref_view_downsampler_tz(src._take(), q.ds_function, q.ds_interval_ms, q.ds_fill, q.ds_all,
+                                        start_time, end_time, query_start, query_end, q.ds_calendar,
+                                        C.byref(tzs) if tzs is not None else None)
     if not ptr:
         _err(-3)
-    return View(ptr, keep=src.keep)
+    keep = list(src.keep) + ([tzs] if tzs is not None else [])
+    return View(ptr, keep=keep)
 
 
 def downsampler_raw(src: View, function: str, interval_ms: int, fill: int = abi.FILL_NONE,

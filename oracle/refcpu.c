@@ -906,12 +906,57 @@ static int month_days(int64_t y, int m) {
   const int leap = (y % 4 == 0 && y % 100 != 0) || y % 400 == 0;
   return m == 2 ? 28 + leap : md[m - 1];
 }
-/* Calendar.add(unit, n) in UTC (fixed-length units are exact millisecond sums) */
-static int64_t cal_add(int64_t ts, int unit, int64_t n) {
-  if (unit != TSDB_CAL_N && unit != TSDB_CAL_Y) return ts + n * CAL_UNIT_MS[unit];
-  const int64_t day = cal_fdiv(ts, 86400000), tod = ts - day * 86400000;
+/* ---- time zone (ZoneInfo restated over the host's tsdbhip_tz table) ------- */
+/* ZoneInfo.getOffsets(date, UTC_TIME): the offset of the last transition at or before t */
+static int32_t tz_off_utc(const tsdbhip_tz* z, int64_t t) {
+  if (!z) return 0;
+  int lo = 0, hi = z->n - 1, idx = -1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    if (z->utc_ms[mid] <= t) { idx = mid; lo = mid + 1; }
+    else hi = mid - 1;
+  }
+  return z->offset_ms[idx + 1];
+}
+/* ZoneInfo.getOffsetsByWall (getTransitionIndex with WALL_TIME): a transition's wall time is
+ * its instant plus the offset that starts there; a wall time in a spring-forward gap takes
+ * the old offset, one in a fall-back overlap the new one */
+static int32_t tz_off_wall(const tsdbhip_tz* z, int64_t w) {
+  if (!z) return 0;
+  int lo = 0, hi = z->n - 1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    const int64_t mv = z->utc_ms[mid] + z->offset_ms[mid + 1];
+    if (mv < w) lo = mid + 1;
+    else if (mv > w) hi = mid - 1;
+    else return z->offset_ms[mid + 1];
+  }
+  if (lo >= z->n) return z->offset_ms[z->n];
+  return lo - 1 < 0 ? z->offset_ms[0] : z->offset_ms[lo];
+}
+/* GregorianCalendar.computeTime from local wall-clock fields */
+static int64_t tz_from_wall(const tsdbhip_tz* z, int64_t w) { return w - tz_off_wall(z, w); }
+
+/* GregorianCalendar.add(unit, n) in zone z: ms / s / m / h add absolute milliseconds;
+ * days keep the local time of day and re-adjust for an offset change (the previous instant if
+ * the adjustment changes the date); months / years move the local date, pin the day of month
+ * and recompute the instant from the wall-clock fields */
+static int64_t cal_add(int64_t ts, int unit, int64_t n, const tsdbhip_tz* z) {
+  if (unit != TSDB_CAL_N && unit != TSDB_CAL_Y && unit != TSDB_CAL_D) return ts + n * CAL_UNIT_MS[unit];
+  const int64_t off = tz_off_utc(z, ts);
+  const int64_t loc = ts + off;
+  int64_t fd = cal_fdiv(loc, 86400000);
+  const int64_t tod = loc - fd * 86400000;
+  if (unit == TSDB_CAL_D) {
+    fd += n;
+    const int64_t t1 = fd * 86400000 + tod - off;
+    const int64_t diff = off - tz_off_utc(z, t1);
+    if (diff == 0) return t1;
+    const int64_t t2 = t1 + diff;
+    return cal_fdiv(t2 + tz_off_utc(z, t2), 86400000) != fd ? t1 : t2;
+  }
   int64_t y; int m, d;
-  civil_from_days(day, &y, &m, &d);
+  civil_from_days(fd, &y, &m, &d);
   if (unit == TSDB_CAL_N) {
     const int64_t mm = y * 12 + (m - 1) + n;
     y = cal_fdiv(mm, 12);
@@ -921,49 +966,52 @@ static int64_t cal_add(int64_t ts, int unit, int64_t n) {
   }
   const int ml = month_days(y, m);
   if (d > ml) d = ml;   /* add() pins the day of month */
-  return days_from_civil(y, m, d) * 86400000 + tod;
+  return tz_from_wall(z, days_from_civil(y, m, d) * 86400000 + tod);
 }
 /* one Downsampler step: interval units, or interval * WEEK_LENGTH days for weeks */
-static int64_t cal_step(int64_t ts, int unit, int64_t n, int sign) {
-  if (unit == TSDB_CAL_W) return cal_add(ts, TSDB_CAL_D, sign * n * 7);
-  return cal_add(ts, unit, sign * n);
+static int64_t cal_step(int64_t ts, int unit, int64_t n, int sign, const tsdbhip_tz* z) {
+  if (unit == TSDB_CAL_W) return cal_add(ts, TSDB_CAL_D, sign * n * 7, z);
+  return cal_add(ts, unit, sign * n, z);
 }
-/* DateTime.previousInterval(ts, interval, unit, UTC) :445-606 */
-static int64_t cal_prev(int64_t ts, int64_t n, int unit) {
+/* DateTime.previousInterval(ts, interval, unit, tz) :445-606: the set() calls zero local
+ * fields (the instant is recomputed from the wall clock), the adds run in zone z */
+static int64_t cal_prev(int64_t ts, int64_t n, int unit, const tsdbhip_tz* z) {
   if (ts < 0) jthrow(TSDB_E_ILLEGAL_ARGUMENT, "Timestamp cannot be less than zero");
   if (n < 1) jthrow(TSDB_E_ILLEGAL_ARGUMENT, "Interval must be greater than zero");
   int uo = unit;
   int64_t io = n;
-  const int64_t day = cal_fdiv(ts, 86400000);
+  const int64_t loc = ts + tz_off_utc(z, ts);
+  const int64_t day = cal_fdiv(loc, 86400000);
+  const int64_t tod = loc - day * 86400000;
   int64_t y; int m, d;
   civil_from_days(day, &y, &m, &d);
   int64_t c;
   switch (unit) {
     case TSDB_CAL_MS:
-      if (1000 % n == 0) { c = ts - ts % 1000; if (n > 1000) c -= n; }
-      else c = ts - ts % 60000;
+      if (1000 % n == 0) { c = tz_from_wall(z, loc - tod % 1000); if (n > 1000) c -= n; }
+      else c = tz_from_wall(z, loc - tod % 60000);
       break;
     case TSDB_CAL_S:
-      if (60 % n == 0) { c = ts - ts % 60000; if (n > 60) c -= n * 1000; }
-      else c = ts - ts % 3600000;
+      if (60 % n == 0) { c = tz_from_wall(z, loc - tod % 60000); if (n > 60) c -= n * 1000; }
+      else c = tz_from_wall(z, loc - tod % 3600000);
       break;
     case TSDB_CAL_M:
-      if (60 % n == 0) { c = ts - ts % 3600000; if (n > 60) c -= n * 60000; }
-      else c = day * 86400000;
+      if (60 % n == 0) { c = tz_from_wall(z, loc - tod % 3600000); if (n > 60) c -= n * 60000; }
+      else c = tz_from_wall(z, day * 86400000);
       break;
     case TSDB_CAL_H:
-      if (24 % n == 0) { c = day * 86400000; if (n > 24) c -= n * 3600000; }
-      else c = days_from_civil(y, m, 1) * 86400000;
+      if (24 % n == 0) { c = tz_from_wall(z, day * 86400000); if (n > 24) c -= n * 3600000; }
+      else c = tz_from_wall(z, days_from_civil(y, m, 1) * 86400000);
       break;
     case TSDB_CAL_D:
-      if (n == 1) c = days_from_civil(y, m, 1) * 86400000;
-      else c = days_from_civil(y, 1, 1) * 86400000;
+      if (n == 1) c = tz_from_wall(z, days_from_civil(y, m, 1) * 86400000);
+      else c = tz_from_wall(z, days_from_civil(y, 1, 1) * 86400000);
       break;
     case TSDB_CAL_W:
       if (2 % n == 0) {
         /* set(DAY_OF_WEEK, SUNDAY): the Sunday of the Sunday-first week (1970-01-04 was one) */
         const int64_t dow = ((day - 3) % 7 + 7) % 7;
-        c = (day - dow) * 86400000;
+        c = tz_from_wall(z, (day - dow) * 86400000);
       } else {
         /* set(MONTH, 0) then set(DAY_OF_WEEK, ...): lenient resolution of a January week */
         jthrow(TSDB_E_NOT_IMPLEMENTED, "calendar intervals of more than 2 weeks");
@@ -972,12 +1020,12 @@ static int64_t cal_prev(int64_t ts, int64_t n, int unit) {
       io = 7;
       break;
     default:   /* MONTH, YEAR: from the top of the year */
-      c = days_from_civil(y, 1, 1) * 86400000;
+      c = tz_from_wall(z, days_from_civil(y, 1, 1) * 86400000);
       break;
   }
   if (c == ts) return c;
-  while (c <= ts) c = cal_add(c, uo, io);
-  return cal_add(c, uo, -io);
+  while (c <= ts) c = cal_add(c, uo, io, z);
+  return cal_add(c, uo, -io, z);
 }
 
 /* ======================================================================== */
@@ -1005,6 +1053,7 @@ typedef struct {
    * FillingDownsampler's own previous_calendar / next_calendar (FillingDownsampler.java:38-41) */
   int cal;
   int64_t cal_n;
+  const tsdbhip_tz* tz;   /* DownsamplingSpecification.getTimezone (NULL = UTC) */
   int64_t prev_cal, next_cal;
   int64_t fprev_cal, fnext_cal;
 } ds_view;
@@ -1038,8 +1087,8 @@ static void viv_init(ds_view* d) {  /* :327-354 */
       viv_move_to_next_value(d);
       if (!d->run_all) {
         if (d->cal) {
-          d->prev_cal = cal_prev(d->next_dp.ts, d->cal_n, d->cal);
-          d->next_cal = cal_step(d->prev_cal, d->cal, d->cal_n, 1);
+          d->prev_cal = cal_prev(d->next_dp.ts, d->cal_n, d->cal, d->tz);
+          d->next_cal = cal_step(d->prev_cal, d->cal, d->cal_n, 1, d->tz);
           d->tei = d->next_cal;
         } else {
           d->tei = ds_align(d, d->next_dp.ts) + d->interval;
@@ -1052,8 +1101,8 @@ static void viv_reset_end(ds_view* d) {  /* :388-406 */
   if (d->has_src && !d->run_all) {
     if (d->cal) {
       while (d->next_dp.ts >= d->tei) {
-        d->prev_cal = cal_step(d->prev_cal, d->cal, d->cal_n, 1);
-        d->next_cal = cal_step(d->next_cal, d->cal, d->cal_n, 1);
+        d->prev_cal = cal_step(d->prev_cal, d->cal, d->cal_n, 1, d->tz);
+        d->next_cal = cal_step(d->next_cal, d->cal, d->cal_n, 1, d->tz);
         d->tei = d->next_cal;
       }
     } else {
@@ -1066,8 +1115,8 @@ static void viv_seek(ds_view* d, int64_t ts) {  /* :415-437 */
   if (d->run_all) {
     v_seek(d->src, ts);
   } else if (d->cal) {
-    int64_t sc = cal_prev(ts, d->cal_n, d->cal);
-    if (ts > sc) sc = cal_step(sc, d->cal, d->cal_n, 1);
+    int64_t sc = cal_prev(ts, d->cal_n, d->cal, d->tz);
+    if (ts > sc) sc = cal_step(sc, d->cal, d->cal_n, 1, d->tz);
     v_seek(d->src, sc);
   } else {
     v_seek(d->src, ds_align(d, ts + d->interval - 1));
@@ -1134,8 +1183,8 @@ static ref_dp ds_next(ref_view* v) {
   }
   if (d->run_all) return dp_of_double(d->qs, d->value);
   if (d->cal) {   /* advance :280-286; timestamp() = previous_calendar :304-311 */
-    d->fprev_cal = cal_step(d->fprev_cal, d->cal, d->cal_n, 1);
-    d->fnext_cal = cal_step(d->fnext_cal, d->cal, d->cal_n, 1);
+    d->fprev_cal = cal_step(d->fprev_cal, d->cal, d->cal_n, 1, d->tz);
+    d->fnext_cal = cal_step(d->fnext_cal, d->cal, d->cal_n, 1, d->tz);
     d->timestamp = d->fnext_cal;
     return dp_of_double(d->fprev_cal, d->value);
   }
@@ -1148,13 +1197,15 @@ static const view_vt DS_VT = {ds_has_next, ds_next, ds_seek, ds_destroy};
 
 static ref_view* make_downsampler(ref_view* src, int32_t function, int64_t interval_ms, int32_t fill,
                                   int32_t run_all, int64_t start_time, int64_t end_time,
-                                  int64_t query_start, int64_t query_end, int32_t calendar) {
+                                  int64_t query_start, int64_t query_end, int32_t calendar,
+                                  const tsdbhip_tz* tz) {
   if (function == TSDB_AGG_NONE) jthrow(TSDB_E_ILLEGAL_ARGUMENT, "cannot use the NONE aggregator for downsampling");
   if (!run_all && interval_ms <= 0) jthrow(TSDB_E_ILLEGAL_ARGUMENT, "interval not > 0");
   ds_view* d = (ds_view*)xcalloc(1, sizeof(ds_view));
   d->base.vt = &DS_VT;
   d->src = src;
   d->fn = function;
+  d->tz = tz;
   d->interval = interval_ms;
   d->fill = fill;
   d->run_all = run_all;
@@ -1173,10 +1224,10 @@ static ref_view* make_downsampler(ref_view* src, int32_t function, int64_t inter
       d->timestamp = start_time;
       d->end_timestamp = end_time;
     } else if (d->cal) {   /* FillingDownsampler ctor :113-135 */
-      d->fnext_cal = cal_prev(start_time, d->cal_n, d->cal);
-      d->fprev_cal = cal_step(d->fnext_cal, d->cal, d->cal_n, -1);
-      int64_t end_cal = cal_prev(end_time, d->cal_n, d->cal);
-      if (end_cal == d->fnext_cal) end_cal = cal_step(end_cal, d->cal, d->cal_n, 1);
+      d->fnext_cal = cal_prev(start_time, d->cal_n, d->cal, d->tz);
+      d->fprev_cal = cal_step(d->fnext_cal, d->cal, d->cal_n, -1, d->tz);
+      int64_t end_cal = cal_prev(end_time, d->cal_n, d->cal, d->tz);
+      if (end_cal == d->fnext_cal) end_cal = cal_step(end_cal, d->cal, d->cal_n, 1, d->tz);
       d->timestamp = d->fnext_cal;
       d->end_timestamp = end_cal;
     } else {
@@ -1187,13 +1238,19 @@ static ref_view* make_downsampler(ref_view* src, int32_t function, int64_t inter
   return &d->base;
 }
 
+ref_view* ref_view_downsampler_tz(ref_view* src, int32_t function, int64_t interval_ms, int32_t fill,
+                                  int32_t run_all, int64_t start_time, int64_t end_time,
+                                  int64_t query_start, int64_t query_end, int32_t calendar, const tsdbhip_tz* tz) {
+  ref_view* r = NULL;
+  TRY { r = make_downsampler(src, function, interval_ms, fill, run_all, start_time, end_time, query_start, query_end, calendar, tz); }
+  CATCH(e) { (void)e; r = NULL; } END_TRY
+  return r;
+}
 ref_view* ref_view_downsampler(ref_view* src, int32_t function, int64_t interval_ms, int32_t fill,
                                int32_t run_all, int64_t start_time, int64_t end_time,
                                int64_t query_start, int64_t query_end, int32_t calendar) {
-  ref_view* r = NULL;
-  TRY { r = make_downsampler(src, function, interval_ms, fill, run_all, start_time, end_time, query_start, query_end, calendar); }
-  CATCH(e) { (void)e; r = NULL; } END_TRY
-  return r;
+  return ref_view_downsampler_tz(src, function, interval_ms, fill, run_all, start_time, end_time, query_start,
+                                 query_end, calendar, NULL);
 }
 
 /* ======================================================================== */
@@ -1706,7 +1763,8 @@ static void run_group(const query_env* env, group_job* g) {
       if (size == 0 || !(first <= env->scan_end_ms && last >= env->scan_start_ms)) { ref_view_free(it); continue; }
       if (has_downsampler(q)) {
         it = make_downsampler(it, q->ds_function, q->ds_interval_ms, q->ds_fill, q->ds_all,
-                              env->scan_start_ms, env->scan_end_ms, q->start_time, q->end_time, q->ds_calendar);
+                              env->scan_start_ms, env->scan_end_ms, q->start_time, q->end_time, q->ds_calendar,
+                              q->ds_tz);
       }
       if (q->rate) it = ref_view_rate(it, q->rate_counter, q->rate_counter_max, q->rate_reset_value, q->rate_drop_resets);
       its[k++] = it;

@@ -43,6 +43,10 @@ ref_view* ref_view_span(int64_t n_rows, const uint32_t* base_time, const uint64_
 ref_view* ref_view_downsampler(ref_view* src, int32_t function, int64_t interval_ms, int32_t fill,
                                int32_t run_all, int64_t start_time, int64_t end_time,
                                int64_t query_start, int64_t query_end, int32_t calendar);
+/* the same in a time zone (DownsamplingSpecification.setTimezone; NULL = UTC) */
+ref_view* ref_view_downsampler_tz(ref_view* src, int32_t function, int64_t interval_ms, int32_t fill,
+                                  int32_t run_all, int64_t start_time, int64_t end_time,
+                                  int64_t query_start, int64_t query_end, int32_t calendar, const tsdbhip_tz* tz);
 ref_view* ref_view_rate(ref_view* src, int32_t counter, int64_t counter_max, int64_t reset_value,
                         int32_t drop_resets);
 ref_view* ref_view_aggregate(ref_view** srcs, int64_t n, int64_t start_time, int64_t end_time,
