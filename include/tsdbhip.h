@@ -128,11 +128,15 @@ typedef struct {
 /* Calendar units of a 'c' downsampling interval (DateTime.unitsToCalendarType,
  * src/utils/DateTime.java:616-640); the interval count is ds_interval_ms / the unit's
  * parseDuration length (ms 1, s 1e3, m 6e4, h 3.6e6, d 8.64e7, w 6.048e8, n 30 d, y 365 d).
- * The engine aligns on the UTC calendar (the DownsamplingSpecification default timezone).
- * It runs the units whose grid is one global sequence -- ms (1000 % n == 0), s / m
- * (60 % n == 0), h (24 % n == 0), d (n == 1), w (n == 1, weeks from Sunday) -- and n months
- * (12 % n == 0) and 1 year through a per-query slot boundary table; intervals anchored per
- * span (7sc, 2dc, 5nc, 2wc, 2yc) return TSDB_E_NOT_IMPLEMENTED. */
+ * The calendar is the query's zone (ds_tz; UTC when NULL, the DownsamplingSpecification
+ * default).  UTC intervals whose grid is one global sequence -- ms (1000 % n == 0), s / m
+ * (60 % n == 0), h (24 % n == 0), d (n == 1), w (n == 1, weeks from Sunday) -- run on a fixed
+ * grid, n months (12 % n == 0) and 1 year on a slot boundary table.  Everything else (a time
+ * zone, or an interval anchored per span: 7sc, 2dc, 5nc, 2wc, 2yc ...) runs on the union of
+ * the spans' boundary sequences, each anchored at previousInterval(the span's first datapoint
+ * after the seek); spans whose sequences disagree (their union of timestamps is not one grid),
+ * week intervals of more than 2 weeks, and percentile / median downsampling over a boundary
+ * table return TSDB_E_NOT_IMPLEMENTED. */
 enum {
   TSDB_CAL_NONE = 0, TSDB_CAL_MS, TSDB_CAL_S, TSDB_CAL_M, TSDB_CAL_H, TSDB_CAL_D, TSDB_CAL_W, TSDB_CAL_N, TSDB_CAL_Y
 };

@@ -167,6 +167,143 @@ bool cal_months(int unit, int64_t interval_ms, int64_t* step_months) {
   return false;
 }
 
+// ---- calendar intervals in a time zone (java.util.GregorianCalendar) ----------------------
+// The host-side Calendar the general calendar plan runs (plan_query): DateTime.previousInterval
+// (src/utils/DateTime.java:445-606) and Calendar.add in the zone of the query's tsdbhip_tz
+// (UTC when none) -- ZoneInfo.getOffsets by instant, getOffsetsByWall when an instant is
+// recomputed from local fields, GregorianCalendar.add's per-unit rules.
+struct JZone {
+  const tsdbhip_tz* z = nullptr;
+  int32_t at(int64_t t) const {   // offset in effect at instant t
+    if (!z || z->n <= 0) return z ? z->offset_ms[0] : 0;
+    const int64_t* u = z->utc_ms;
+    const int64_t i = std::upper_bound(u, u + z->n, t) - u;   // transitions at or before t
+    return z->offset_ms[i];
+  }
+  int32_t by_wall(int64_t w) const {   // getTransitionIndex(WALL_TIME): gap -> old offset, overlap -> new
+    if (!z || z->n <= 0) return z ? z->offset_ms[0] : 0;
+    int lo = 0, hi = z->n - 1;
+    while (lo <= hi) {
+      const int mid = (lo + hi) >> 1;
+      const int64_t mv = z->utc_ms[mid] + z->offset_ms[mid + 1];
+      if (mv < w) lo = mid + 1;
+      else if (mv > w) hi = mid - 1;
+      else return z->offset_ms[mid + 1];
+    }
+    if (lo >= z->n) return z->offset_ms[z->n];
+    return lo == 0 ? z->offset_ms[0] : z->offset_ms[lo];
+  }
+  int64_t from_wall(int64_t w) const { return w - by_wall(w); }
+};
+
+void civil_of_day(int64_t z, int64_t& y, int& m, int& d) {
+  z += 719468;
+  const int64_t era = floor_div(z, 146097);
+  const int64_t doe = z - era * 146097;
+  const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+  const int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+  const int64_t mp = (5 * doy + 2) / 153;
+  d = (int)(doy - (153 * mp + 2) / 5 + 1);
+  m = (int)(mp < 10 ? mp + 3 : mp - 9);
+  y = yoe + era * 400 + (m <= 2);
+}
+int64_t day_of_civil(int64_t y, int m, int d) { return floor_div(month_start_ms(y * 12 + m - 1), 86400000LL) + d - 1; }
+int month_len(int64_t y, int m) {
+  static const int md[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+  const bool leap = (y % 4 == 0 && y % 100 != 0) || y % 400 == 0;
+  return m == 2 ? 28 + (leap ? 1 : 0) : md[m - 1];
+}
+
+// Calendar.add(unit, n): ms / s / m / h absolute; days keep the local time of day and correct
+// an offset change (keeping the date); months / years move the local date, pin the day of
+// month and recompute the instant from the wall clock
+int64_t jcal_add(const JZone& Z, int64_t t, int unit, int64_t n) {
+  if (unit != TSDB_CAL_D && unit != TSDB_CAL_N && unit != TSDB_CAL_Y) return t + n * CAL_UNIT_MS[unit];
+  const int64_t off = Z.at(t);
+  const int64_t loc = t + off;
+  int64_t fd = floor_div(loc, 86400000LL);
+  const int64_t tod = loc - fd * 86400000LL;
+  if (unit == TSDB_CAL_D) {
+    fd += n;
+    const int64_t t1 = fd * 86400000LL + tod - off;
+    const int64_t diff = off - Z.at(t1);
+    if (diff == 0) return t1;
+    const int64_t t2 = t1 + diff;
+    return floor_div(t2 + Z.at(t2), 86400000LL) != fd ? t1 : t2;
+  }
+  int64_t y;
+  int m, d;
+  civil_of_day(fd, y, m, d);
+  int64_t mm = y * 12 + (m - 1) + (unit == TSDB_CAL_N ? n : 12 * n);
+  y = floor_div(mm, 12);
+  m = (int)(mm - y * 12) + 1;
+  d = std::min(d, month_len(y, m));
+  return Z.from_wall(day_of_civil(y, m, d) * 86400000LL + tod);
+}
+// one Downsampler step (weeks: interval * 7 days)
+int64_t jcal_step(const JZone& Z, int64_t t, int unit, int64_t n, int sign) {
+  if (unit == TSDB_CAL_W) return jcal_add(Z, t, TSDB_CAL_D, sign * n * 7);
+  return jcal_add(Z, t, unit, sign * n);
+}
+// DateTime.previousInterval(ts, n, unit, tz) in two steps: jcal_top, the instant the set()
+// calls produce (the top of the enclosing unit, shifted back for intervals longer than it) and
+// the unit / count the walk steps by; then the walk from there to the last step <= ts.
+// false = not supported (weeks > 2)
+bool jcal_top(const JZone& Z, int64_t ts, int64_t n, int unit, int64_t& c, int& uo, int64_t& io) {
+  uo = unit;
+  io = n;
+  const int64_t loc = ts + Z.at(ts);
+  const int64_t day = floor_div(loc, 86400000LL);
+  const int64_t tod = loc - day * 86400000LL;
+  int64_t y;
+  int m, d;
+  civil_of_day(day, y, m, d);
+  switch (unit) {
+    case TSDB_CAL_MS:
+      if (1000 % n == 0) { c = Z.from_wall(loc - tod % 1000); if (n > 1000) c -= n; }
+      else c = Z.from_wall(loc - tod % 60000);
+      break;
+    case TSDB_CAL_S:
+      if (60 % n == 0) { c = Z.from_wall(loc - tod % 60000); if (n > 60) c -= n * 1000; }
+      else c = Z.from_wall(loc - tod % 3600000);
+      break;
+    case TSDB_CAL_M:
+      if (60 % n == 0) { c = Z.from_wall(loc - tod % 3600000); if (n > 60) c -= n * 60000; }
+      else c = Z.from_wall(day * 86400000LL);
+      break;
+    case TSDB_CAL_H:
+      if (24 % n == 0) { c = Z.from_wall(day * 86400000LL); if (n > 24) c -= n * 3600000LL; }
+      else c = Z.from_wall(day_of_civil(y, m, 1) * 86400000LL);
+      break;
+    case TSDB_CAL_D:
+      c = Z.from_wall(day_of_civil(y, n == 1 ? m : 1, 1) * 86400000LL);
+      break;
+    case TSDB_CAL_W: {
+      if (2 % n != 0) return false;   // set(MONTH, 0) + set(DAY_OF_WEEK): a January week
+      const int64_t dow = ((day - 3) % 7 + 7) % 7;   // Sunday-first weeks (1970-01-04 was a Sunday)
+      c = Z.from_wall((day - dow) * 86400000LL);
+      uo = TSDB_CAL_D;
+      io = 7;
+      break;
+    }
+    default:   // months, years: from the top of the year
+      c = Z.from_wall(day_of_civil(y, 1, 1) * 86400000LL);
+      break;
+  }
+  return true;
+}
+bool jcal_prev(const JZone& Z, int64_t ts, int64_t n, int unit, int64_t& out) {
+  int64_t c, io;
+  int uo;
+  if (!jcal_top(Z, ts, n, unit, c, uo, io)) return false;
+  if (c != ts) {
+    while (c <= ts) c = jcal_add(Z, c, uo, io);
+    c = jcal_add(Z, c, uo, -io);
+  }
+  out = c;
+  return true;
+}
+
 // bytes past the end of the qualifier / value blobs that kernels may read (never use):
 // k_fast's vle class loads a 1 KB value window from each row start
 constexpr int64_t BLOB_SLACK = 1024 + 64;
@@ -228,6 +365,11 @@ struct tsdbhip_ctx {
   bool ro_meta_valid = false;          // rollup ro_ord / ro_orig / ro_allint of the loaded batch
   bool lc_valid = false;               // local_counts() cache
   std::vector<int64_t> lc;
+  // general calendar plan cache (plan_calendar): key, then its boundaries / seek point
+  bool calc_valid = false;
+  std::vector<int64_t> calc_key, calc_bounds;
+  int64_t calc_seek = 0;
+  DevBuf first_ts;
   int64_t mdp_ss = 0, mdp_se = 0, mdp = 0;
   DevBuf sel_vals, sel_sorted, sel_uni, sel_gsp;   // percentile / median group-by
   DevBuf cal_bounds;                                // calendar month / year slot boundaries
@@ -410,6 +552,7 @@ static void release_batch(tsdbhip_ctx* c) {
   c->mdp_valid = false;
   c->ro_meta_valid = false;
   c->lc_valid = false;
+  c->calc_valid = false;
   c->n_series = c->n_rows = c->n_groups = 0;
 }
 
@@ -1123,6 +1266,150 @@ struct Plan {
 
 bool is_sel_agg(int a) { return a == TSDB_AGG_MEDIAN || (a >= TSDB_AGG_P999 && a < TSDB_AGG_COUNT_ALL); }
 
+// A calendar interval in a time zone, or one anchored per span (DateTime.previousInterval of the
+// span's first datapoint: 7sc, 2dc, 5nc, 2wc, 2yc ...), as a MODE_TABLE slot table.  Every
+// span's Downsampler seeks to the first boundary at or after the scan start
+// (Downsampler.seekInterval :415-437), anchors at previousInterval(its first datapoint there)
+// (:336-350) and steps by the interval (:388-406); a FillingDownsampler emits from
+// previousInterval(start) to previousInterval(end) (FillingDownsampler.java:113-135).  The
+// slots are the union of those boundary sequences, provided they agree where they overlap --
+// always for days, weeks, n months (12 % n == 0) and years, which step on the local calendar,
+// and for ms / s / m / h lattices when the zone's offsets in range are congruent modulo the
+// step; otherwise the anchors come from each series' first datapoint (k_first_ts) and spans on
+// grids that disagree return NOT_IMPLEMENTED (their union of timestamps is not one grid).
+int plan_calendar(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
+  const int unit = q->ds_calendar;
+  if (unit < TSDB_CAL_MS || unit > TSDB_CAL_Y) return fail(TSDB_E_ILLEGAL_ARGUMENT, "Unrecognized unit type");
+  const int64_t n = q->ds_interval_ms / CAL_UNIT_MS[unit];
+  if (n < 1 || n * CAL_UNIT_MS[unit] != q->ds_interval_ms || n > (1 << 30))
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, "calendar interval is not a whole number of units");
+  const JZone Z{q->ds_tz};
+  const int64_t S0 = P.ss * 1000, E0 = P.se * 1000;
+  const bool fill = q->ds_fill != TSDB_FILL_NONE;
+  // cache: the plan depends on the interval, the scan range, the fill, the zone and the batch
+  std::vector<int64_t> key = {unit, n, S0, E0, fill ? 1 : 0, (int64_t)(intptr_t)q->ds_tz,
+                              q->ds_tz ? q->ds_tz->n : -1};
+  if (q->ds_tz && q->ds_tz->n > 0) { key.push_back(q->ds_tz->utc_ms[0]); key.push_back(q->ds_tz->utc_ms[q->ds_tz->n - 1]); }
+  if (c->calc_valid && c->calc_key == key) {
+    P.bounds = c->calc_bounds;
+  } else {
+    int64_t a0;
+    if (!jcal_prev(Z, S0, n, unit, a0))
+      return fail(TSDB_E_NOT_IMPLEMENTED, "calendar week intervals of more than 2 weeks");
+    const int64_t sc = a0 == S0 ? a0 : jcal_step(Z, a0, unit, n, 1);   // seekInterval(scan start)
+    // zone-global grids: one boundary sequence whatever the anchor
+    bool global = unit == TSDB_CAL_D ? n == 1 : unit == TSDB_CAL_W ? n == 1 : unit == TSDB_CAL_N ? 12 % n == 0
+                  : unit == TSDB_CAL_Y ? n == 1 : false;
+    if (unit == TSDB_CAL_MS || unit == TSDB_CAL_S || unit == TSDB_CAL_M || unit == TSDB_CAL_H) {
+      const int64_t top = unit == TSDB_CAL_MS ? 1000 : unit == TSDB_CAL_H ? 24 : 60;
+      if (top % n == 0) {
+        global = true;
+        const int64_t step = n * CAL_UNIT_MS[unit];
+        const int32_t ref = Z.at(S0);
+        if (q->ds_tz) {
+          const tsdbhip_tz* z = q->ds_tz;
+          for (int i = 0; i <= z->n && global; i++) {
+            const int64_t from = i == 0 ? INT64_MIN : z->utc_ms[i - 1];
+            const int64_t to = i == z->n ? INT64_MAX : z->utc_ms[i];
+            if (to < S0 - 2 * 86400000LL || from > E0 + 2 * 86400000LL) continue;
+            if (((int64_t)z->offset_ms[i] - ref) % step != 0) global = false;
+          }
+        }
+      }
+    }
+    std::vector<int64_t> anchors;
+    if (global) {
+      anchors.push_back(sc);
+    } else {
+      // every series' first datapoint at or after the seek point (device), its anchor (host)
+      const int64_t NS = c->n_series;
+      std::vector<int64_t> f(std::max<int64_t>(1, NS));
+      HIP_OK(c->first_ts.ensure(std::max<int64_t>(1, NS) * 8));
+      HIP_OK(launch_first_ts(c->rows.as<RowDesc>(), c->srp.as<int64_t>(), c->qual.as<uint8_t>(), NS, P.ss, P.se, sc,
+                             c->first_ts.as<int64_t>(), c->stream));
+      if (NS) HIP_OK(hipMemcpyAsync(f.data(), c->first_ts.p, NS * 8, hipMemcpyDeviceToHost, c->stream));
+      HIP_OK(hipStreamSynchronize(c->stream));
+      f.resize(NS);
+      std::sort(f.begin(), f.end());
+      f.erase(std::unique(f.begin(), f.end()), f.end());
+      // datapoints with the same top (jcal_top) inside one bucket of that top's walk share its
+      // anchor; the walk runs once per such bucket
+      int64_t top = INT64_MIN, lo = INT64_MAX, hi = INT64_MIN;
+      for (int64_t t : f) {
+        if (t == INT64_MAX) break;
+        int64_t tp, io;
+        int uo;
+        if (!jcal_top(Z, t, n, unit, tp, uo, io)) return fail(TSDB_E_NOT_IMPLEMENTED, "calendar week intervals of more than 2 weeks");
+        if (tp == top && t >= lo && t < hi) continue;
+        int64_t a;
+        jcal_prev(Z, t, n, unit, a);
+        if (anchors.empty() || anchors.back() != a) anchors.push_back(a);
+        top = tp;
+        lo = a;
+        hi = jcal_add(Z, a, uo, io);
+      }
+      std::sort(anchors.begin(), anchors.end());
+      anchors.erase(std::unique(anchors.begin(), anchors.end()), anchors.end());
+    }
+    // each anchor's boundary sequence through the first boundary >= the scan end
+    std::vector<std::vector<int64_t>> seqs;
+    std::vector<int64_t> T;
+    for (int64_t a : anchors) {
+      std::vector<int64_t> sq{a};
+      while (sq.back() < E0) {
+        sq.push_back(jcal_step(Z, sq.back(), unit, n, 1));
+        if (sq.size() > 50000000) return fail(TSDB_E_ILLEGAL_ARGUMENT, "too many calendar buckets");
+      }
+      T.insert(T.end(), sq.begin(), sq.end());
+      seqs.push_back(std::move(sq));
+    }
+    std::vector<int64_t> F;   // FillingDownsampler: previousInterval(start) .. previousInterval(end)
+    if (fill) {
+      int64_t f0, eC;
+      jcal_prev(Z, S0, n, unit, f0);
+      jcal_prev(Z, E0, n, unit, eC);
+      if (eC == f0) eC = jcal_step(Z, eC, unit, n, 1);
+      for (int64_t t = f0; t < eC; t = jcal_step(Z, t, unit, n, 1)) {
+        F.push_back(t);
+        if (F.size() > 50000000) return fail(TSDB_E_ILLEGAL_ARGUMENT, "too many calendar buckets");
+      }
+      F.push_back(eC);
+      T.insert(T.end(), F.begin(), F.end());
+    }
+    std::sort(T.begin(), T.end());
+    T.erase(std::unique(T.begin(), T.end()), T.end());
+    // the sequences must coincide with the union wherever they run
+    auto agrees = [&](const std::vector<int64_t>& sq) {
+      const auto it = std::lower_bound(T.begin(), T.end(), sq.front());
+      const size_t i0 = it - T.begin();
+      if (i0 + sq.size() > T.size()) return false;
+      for (size_t k = 0; k < sq.size(); k++) if (T[i0 + k] != sq[k]) return false;
+      return true;
+    };
+    for (const auto& sq : seqs)
+      if (!agrees(sq))
+        return fail(TSDB_E_NOT_IMPLEMENTED, "spans on calendar grids that disagree (per-span anchors): their union of "
+                                            "timestamps is not one slot grid");
+    if (fill && !agrees(F)) return fail(TSDB_E_NOT_IMPLEMENTED, "fill grid disagrees with the spans' calendar grids");
+    P.bounds = fill ? F : T;
+    c->calc_key = key;
+    c->calc_bounds = P.bounds;
+    c->calc_seek = sc;
+    c->calc_valid = true;
+  }
+  P.mode = MODE_TABLE;
+  P.seek = c->calc_seek;
+  P.I = q->ds_interval_ms;
+  if (P.bounds.size() < 2) {
+    P.bounds.assign(1, P.bounds.empty() ? S0 : P.bounds[0]);
+    P.K = 0;
+  } else {
+    P.K = (int64_t)P.bounds.size() - 1;
+  }
+  P.B0 = P.bounds[0];
+  return 0;
+}
+
 int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
   if (q->aggregator < 0 || q->aggregator >= TSDB_AGG_COUNT_ALL) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad aggregator");
   if (q->ds_function >= TSDB_AGG_COUNT_ALL) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad downsampling function");
@@ -1142,12 +1429,12 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
   }
   if (!q->ds_all && q->ds_interval_ms <= 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "interval not > 0");
   int64_t calW = 0, calO = 0, calM = 0;
-  bool table = false;
-  if (q->ds_calendar && !q->ds_all && !cal_grid(q->ds_calendar, q->ds_interval_ms, &calW, &calO)) {
-    if (!cal_months(q->ds_calendar, q->ds_interval_ms, &calM))
-      return fail(TSDB_E_NOT_IMPLEMENTED, "calendar interval anchored per span (one that does not divide its "
-                                          "unit) is not implemented yet");
-    table = true;
+  bool table = false, general = false;
+  if (q->ds_calendar && !q->ds_all) {
+    if (q->ds_tz) general = true;   // a time zone: the general calendar plan
+    else if (cal_grid(q->ds_calendar, q->ds_interval_ms, &calW, &calO)) {}
+    else if (cal_months(q->ds_calendar, q->ds_interval_ms, &calM)) table = true;
+    else general = true;            // anchored per span
   }
   P.ga = ga_of(q->aggregator);
   P.f = f_of(q->ds_function);
@@ -1175,7 +1462,10 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
     P.mode = MODE_GRID;
     const int64_t I = q->ds_interval_ms;
     P.I = I;
-    if (table) {
+    if (general) {
+      const int rc = plan_calendar(c, q, P);
+      if (rc) return rc;
+    } else if (table) {
       // slot boundaries of the month grid: first slot = seekInterval(scan start) :420-432
       P.mode = MODE_TABLE;
       auto mprev = [&](int64_t t) {   // previousInterval: the n-month block of t, from January

@@ -305,6 +305,9 @@ struct RollupAggParams {
   uint8_t* pres;
 };
 hipError_t launch_rollup_agg(const GridParams& p, const RollupAggParams& rp, hipStream_t s);
+// each series' first datapoint >= t0 in rows with base in [ss, se) (INT64_MAX: none)
+hipError_t launch_first_ts(const RowDesc* rows, const int64_t* srp, const uint8_t* qual, int64_t n, int64_t ss,
+                           int64_t se, int64_t t0, int64_t* out, hipStream_t s);
 // streaming variant for one uniform row class (k_fast's premises + the sum certificate);
 // series that break a premise go to p.redo_list for launch_rollup_agg (tile_list mode)
 bool rollup_fast_supported(int qw, int vl);

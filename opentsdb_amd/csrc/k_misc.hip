@@ -190,6 +190,48 @@ __global__ __launch_bounds__(256) void k_synth_write(SynthParams p) {
   }
 }
 
+// ---- k_first_ts: each series' first datapoint at or after a seek point -------------------
+// The general calendar plan (engine.cpp) anchors every span's Downsampler at
+// previousInterval(first datapoint after the seek, src/core/Downsampler.java:336-350), so it
+// needs that datapoint per series: rows with base in [ss, se), in order, qualifiers walked
+// (2-byte second or 4-byte millisecond, Internal.java:621-810) until the first timestamp >= t0.
+// One thread per series; INT64_MAX when the series has none.
+__global__ void k_first_ts(const RowDesc* __restrict__ rows, const int64_t* __restrict__ srp,
+                           const uint8_t* __restrict__ qual, int64_t n, int64_t ss, int64_t se, int64_t t0,
+                           int64_t* __restrict__ out) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  int64_t res = INT64_MAX;
+  for (int64_t r = srp[s]; r < srp[s + 1] && res == INT64_MAX; r++) {
+    const RowDesc d = rows[r];
+    if ((int64_t)d.base < ss || (int64_t)d.base >= se) continue;
+    if ((int64_t)d.base * 1000 + 3600000 <= t0) continue;   // every offset is < 1 h
+    const uint8_t* q = qual + d.qoff;
+    uint32_t pos = 0;
+    for (uint32_t i = 0; i < d.ndp && pos < d.qlen; i++) {
+      int64_t off;
+      if ((q[pos] & 0xF0) == 0xF0) {
+        const uint32_t w = ((uint32_t)q[pos] << 24) | ((uint32_t)q[pos + 1] << 16) | ((uint32_t)q[pos + 2] << 8) | q[pos + 3];
+        off = (w & 0x0FFFFFC0u) >> 6;
+        pos += 4;
+      } else {
+        off = (int64_t)((((uint32_t)q[pos] << 8) | q[pos + 1]) >> 4) * 1000;
+        pos += 2;
+      }
+      const int64_t ts = (int64_t)d.base * 1000 + off;
+      if (ts >= t0) { res = ts; break; }
+    }
+  }
+  out[s] = res;
+}
+
+hipError_t launch_first_ts(const RowDesc* rows, const int64_t* srp, const uint8_t* qual, int64_t n, int64_t ss,
+                           int64_t se, int64_t t0, int64_t* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_first_ts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rows, srp, qual, n, ss, se, t0, out);
+  return hipGetLastError();
+}
+
 // ---- launchers -------------------------------------------------------------------
 hipError_t launch_grid(const GridParams& p, int f, hipStream_t s) {
   if (p.n_tiles == 0) return hipSuccess;

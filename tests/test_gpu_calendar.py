@@ -3,10 +3,11 @@ DateTime.previousInterval / the calendar Downsampler and FillingDownsampler
 (src/utils/DateTime.java:445-606, src/core/Downsampler.java:131-147,336-432,
 src/core/FillingDownsampler.java:113-135,280-286).  The oracle's calendar arithmetic is
 pinned by tests/golden/calendar.json (TestDownsampler's UTC cases); here the engine is
-checked against the oracle on multi-series stores.  The engine takes the intervals whose
-UTC grid is one global sequence: ms / s / m / h dividing their unit, 1d, 1w (fixed width),
-and n months with 12 % n == 0 or 1 year (a slot-boundary table); per-span anchored intervals
-and percentile downsampling over months return NOT_IMPLEMENTED."""
+checked against the oracle on multi-series stores.  Intervals whose UTC grid is one global
+sequence run on the fixed grid (ms / s / m / h dividing their unit, 1d, 1w) or a boundary
+table (n months with 12 % n == 0, 1 year); intervals anchored per span run on the union table
+of the spans' anchors when those agree (tests/test_gpu_calendar_tz.py covers time zones and
+disagreeing anchors); percentile downsampling over a boundary table returns NOT_IMPLEMENTED."""
 from __future__ import annotations
 
 import pytest
@@ -100,8 +101,15 @@ def test_calendar_months_rate(eng, year_batch):
     assert_groups_match(eng.run_batch(year_batch, q), O.run_query(year_batch, q), "sum", ctx="rate")
 
 
-@pytest.mark.parametrize("spec", ["7sc-sum", "2wc-sum", "2dc-sum", "5nc-sum", "2yc-sum", "1nc-p99", "1wc-p99-nan"])
-def test_calendar_without_global_grid_not_implemented(eng, hour_batch, spec):
+@pytest.mark.parametrize("spec", ["7sc-sum", "2wc-sum", "2dc-sum", "5nc-sum", "2yc-sum", "7mc-avg", "5hc-max"])
+def test_calendar_anchored_per_span(eng, hour_batch, spec):
+    # every span's first datapoint is T0: one anchor, one grid (engine.cpp plan_calendar)
+    q = q_of(spec, T0, T0 + 3599, "sum")
+    assert_groups_match(eng.run_batch(hour_batch, q), O.run_query(hour_batch, q), "sum", ctx=spec)
+
+
+@pytest.mark.parametrize("spec", ["1nc-p99", "1wc-p99-nan"])
+def test_calendar_pct_over_table_not_implemented(eng, hour_batch, spec):
     q = q_of(spec, T0, T0 + 3599, "sum")
     with pytest.raises(Exception) as ei:
         eng.run_batch(hour_batch, q)
