@@ -78,7 +78,13 @@ class DownsamplingSpecification:
     fill_policy: str = "none"
     run_all: bool = False
     use_calendar: bool = False
-    calendar_unit: int = 0     # abi.CAL_* of a 'c' interval (UTC; DateTime.unitsToCalendarType)
+    calendar_unit: int = 0     # abi.CAL_* of a 'c' interval (DateTime.unitsToCalendarType)
+    timezone: str | None = None   # setTimezone (DownsamplingSpecification.java:199-207); None = UTC
+
+    def setTimezone(self, tz: str) -> None:
+        if tz is None:
+            raise ValueError("Timezone cannot be null")
+        self.timezone = tz
 
     @classmethod
     def parse(cls, spec: str) -> "DownsamplingSpecification":
@@ -269,6 +275,8 @@ class TsdbQuery:
             drop_resets=self.rate_options.drop_resets, flags=self.flags)
         if ds and ds.use_calendar:
             q.ds_calendar = ds.calendar_unit
+            if ds.timezone is not None:
+                abi.set_timezone(q, ds.timezone)
         return q
 
     def scan_bounds(self):
