@@ -344,6 +344,34 @@ int tsdbhip_rollup_run(tsdbhip_ctx* ctx, const tsdbhip_rollup_spec* spec, int64_
 int tsdbhip_rollup_download(tsdbhip_ctx* ctx, int32_t* series, uint32_t* base_time, uint8_t* qualifier,
                             uint64_t* val_off, uint8_t* value);
 
+/* ---- rollup read path ----------------------------------
+ * A query over a rollup table (TsdbQuery with a RollupQuery, src/core/TsdbQuery.java:1293-1362;
+ * the rollup interval matched the downsampling interval).  The spans are RollupSpans of
+ * RollupSeq rows (src/rollup/RollupSeq.java:52-740): per row the cells of the queried
+ * aggregate, and -- when the group-by aggregator is avg or dev (RollupSeq.need_count) -- the
+ * count cells.  Each cell: 2-byte rollup qualifier (offset << 4 | flags, the aggregator byte or
+ * the old "sum:" string prefix stripped), value bytes (no meta byte).  A datapoint's timestamp
+ * is base + offset * interval_s (RollupUtils.getTimestampFromRollupQualifier :178-235); with
+ * counts the iterator yields only offsets present in both streams (RollupSeq.sync); offsets
+ * must increase within a row (else IllegalDataException; a repeated offset keeps the later
+ * cell when fix_duplicates).  The Downsampler then follows its rollup branches
+ * (src/core/Downsampler.java:165-221, FillingDownsampler.java:196-253): an avg downsampling
+ * of avg rollups is Σsum / Σcount per bucket (0 when Σcount is 0); count sums the counts;
+ * the other functions run on the values.  Scan bounds are the rollup's
+ * (TsdbQuery.getScanStart/EndTimeSeconds :1515-1526, 1562-1567). */
+typedef struct {
+  tsdbhip_batch cells;               /* the aggregate's cells, rows as above */
+  const uint64_t* row_cqual_off;     /* [n_rows + 1] count cells per row, or NULL (no counts) */
+  const uint64_t* row_cval_off;      /* [n_rows + 1] */
+  const uint8_t* cqual;
+  const uint8_t* cval;
+  tsdbhip_rollup_interval interval;  /* the rollup table's interval */
+  int32_t fix_duplicates;            /* tsd.storage.fix_duplicates */
+} tsdbhip_rollup_batch;
+/* Loads a rollup batch as the resident batch; tsdbhip_run then runs rollup queries over it
+ * (downsampled or not; percentile group-by, ordered and multi-GPU entry points excluded). */
+int tsdbhip_load_rollup(tsdbhip_ctx* ctx, const tsdbhip_rollup_batch* rb);
+
 /* Device synchronisation helper for host code that does not use HIP directly. */
 int tsdbhip_sync(tsdbhip_ctx* ctx);
 

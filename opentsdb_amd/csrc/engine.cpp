@@ -334,7 +334,9 @@ struct DevBuf {
 struct tsdbhip_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t copy_stream = nullptr;   // result downloads overlapped with evaluation
   hipEvent_t ev[4] = {};
+  hipEvent_t cev[8] = {};              // chunk-done events for copy_stream
   std::mutex mu;
   // resident batch (series in group-sorted order)
   int64_t n_series = 0, n_rows = 0, n_groups = 0;
@@ -537,7 +539,9 @@ extern "C" int tsdbhip_init(int device, tsdbhip_ctx** out) {
   auto* c = new tsdbhip_ctx();
   c->device = device;
   HIP_OK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIP_OK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
   for (auto& e : c->ev) HIP_OK(hipEventCreate(&e));
+  for (auto& e : c->cev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_OK(c->err.ensure(16));
   *out = c;
   return 0;
@@ -573,6 +577,8 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   if (c->ro_tmp) (void)hipFree(c->ro_tmp);
   for (DevBuf* b : {&c->sel_vals, &c->sel_sorted, &c->sel_uni, &c->sel_gsp, &c->cal_bounds}) b->release();
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->cev) if (e) (void)hipEventDestroy(e);
+  if (c->copy_stream) { (void)hipStreamSynchronize(c->copy_stream); (void)hipStreamDestroy(c->copy_stream); }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1858,12 +1864,92 @@ void account(tsdbhip_ctx* c, const Plan& P) {
   c->timing.bytes = bytes;
 }
 
+// Result blocks.  Large results are device-to-host copies of up to GBs (the raw path writes
+// the result arrays on the device): a D2H copy into pageable memory goes through a staging
+// bounce at a fraction of the link rate, so blocks of >= 1 MB come from a process-wide pool of
+// pinned (hipHostMalloc) blocks, returned to it by tsdbhip_result_free and reused by the next
+// query instead of being pinned anew.  A header before the result records the block's origin.
+struct ResultHeader {
+  uint64_t magic;       // RESULT_MAGIC
+  uint64_t capacity;    // block bytes (header included)
+  uint64_t pinned;      // 1: from the pinned pool
+  uint64_t pad;
+};
+constexpr uint64_t RESULT_MAGIC = 0x7473646268697052ULL;
+constexpr size_t PINNED_MIN = 1 << 20;
+constexpr size_t POOL_MAX = (size_t)8 << 30;   // bytes kept pinned while unused
+
+struct PinnedPool {
+  std::mutex mu;
+  std::vector<std::pair<size_t, void*>> free_blocks;   // (capacity, block)
+  size_t held = 0;
+  void* take(size_t bytes, size_t& cap) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      size_t best = SIZE_MAX;
+      for (size_t i = 0; i < free_blocks.size(); i++)
+        if (free_blocks[i].first >= bytes && (best == SIZE_MAX || free_blocks[i].first < free_blocks[best].first)) best = i;
+      if (best != SIZE_MAX && free_blocks[best].first <= 4 * bytes + PINNED_MIN) {
+        void* b = free_blocks[best].second;
+        cap = free_blocks[best].first;
+        held -= cap;
+        free_blocks.erase(free_blocks.begin() + (long)best);
+        return b;
+      }
+    }
+    cap = PINNED_MIN;
+    while (cap < bytes) cap <<= 1;
+    void* b = nullptr;
+    if (hipHostMalloc(&b, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return b;
+  }
+  void give(void* b, size_t cap) {
+    std::lock_guard<std::mutex> lk(mu);
+    while (held + cap > POOL_MAX && !free_blocks.empty()) {   // drop the oldest blocks
+      (void)hipHostFree(free_blocks.front().second);
+      held -= free_blocks.front().first;
+      free_blocks.erase(free_blocks.begin());
+    }
+    if (cap > POOL_MAX) { (void)hipHostFree(b); return; }
+    free_blocks.push_back({cap, b});
+    held += cap;
+  }
+};
+PinnedPool& pinned_pool() {
+  static PinnedPool* pool = new PinnedPool();   // never destroyed: results may outlive every context
+  return *pool;
+}
+
+void result_free(tsdbhip_result* r) {
+  if (!r) return;
+  auto* h = reinterpret_cast<ResultHeader*>(reinterpret_cast<char*>(r) - sizeof(ResultHeader));
+  if (h->magic != RESULT_MAGIC) return;   // not ours
+  h->magic = 0;
+  if (h->pinned) pinned_pool().give(h, h->capacity);
+  else std::free(h);
+}
+
 tsdbhip_result* make_result(int64_t n_groups, int64_t n_points) {
-  const size_t bytes = sizeof(tsdbhip_result) + (n_groups + 1) * 4 + (n_groups + 1) * 8 + (n_points + 1) * 8 * 2 +
-                       (n_points + 1) + 64;
-  // every array is fully written by the callers: malloc, not calloc (results can be GBs)
-  char* m = (char*)std::malloc(bytes);
-  if (!m) return nullptr;
+  const size_t bytes = sizeof(ResultHeader) + sizeof(tsdbhip_result) + (n_groups + 1) * 4 + (n_groups + 1) * 8 +
+                       (n_points + 1) * 8 * 2 + (n_points + 1) + 64;
+  // every array is fully written by the callers: no zero fill (results can be GBs)
+  size_t cap = bytes;
+  bool pinned = false;
+  char* blk = nullptr;
+  if (bytes >= PINNED_MIN) {
+    blk = (char*)pinned_pool().take(bytes, cap);
+    pinned = blk != nullptr;
+  }
+  if (!blk) {
+    cap = bytes;
+    blk = (char*)std::malloc(bytes);
+  }
+  if (!blk) return nullptr;
+  auto* h = reinterpret_cast<ResultHeader*>(blk);
+  h->magic = RESULT_MAGIC;
+  h->capacity = cap;
+  h->pinned = pinned ? 1 : 0;
+  char* m = blk + sizeof(ResultHeader);
   std::memset(m, 0, sizeof(tsdbhip_result));
   auto* r = reinterpret_cast<tsdbhip_result*>(m);
   char* p = m + sizeof(tsdbhip_result);
@@ -2270,7 +2356,7 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
   tsdbhip_result* direct_r = nullptr;
   struct Guard {
     tsdbhip_result** r;
-    ~Guard() { if (*r) std::free(*r); }
+    ~Guard() { result_free(*r); }
   } guard{&direct_r};
   for (int64_t g0 = 0; g0 < G; g0 += per_chunk) {
     const int64_t g1 = std::min(G, g0 + per_chunk);
@@ -2377,22 +2463,53 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
       }
     } else {
       HIP_OK(hipEventRecord(c->ev[3], c->stream));
-      HIP_OK(launch_raw_eval(rp, c->stream));
+      if (!direct) HIP_OK(launch_raw_eval(rp, c->stream));
     }
-    HIP_OK(hipEventRecord(c->ev[1], c->stream));
     const size_t base = res_ts.size();
     if (direct) {
-      // one chunk, groups emitted in batch order: device layout == result layout
+      // one chunk, groups emitted in batch order: device layout == result layout.  The strips
+      // are evaluated in up to 8 launches split at group boundaries; each launch's output range
+      // (its groups' union points, contiguous) downloads on copy_stream while the next one
+      // runs, into a pinned result block
       int64_t nact = 0;
       for (int64_t g = 0; g < G; g++) nact += act[g];
       direct_r = make_result(nact, nout);
       if (!direct_r) return fail(TSDB_E_NOMEM, "result allocation");
-      if (nout) {
-        HIP_OK(hipMemcpyAsync(const_cast<int64_t*>(direct_r->ts_ms), rp.out_ts, nout * 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_OK(hipMemcpyAsync(const_cast<uint64_t*>(direct_r->value_bits), rp.out_bits, nout * 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_OK(hipMemcpyAsync(const_cast<uint8_t*>(direct_r->is_int), rp.out_int, nout, hipMemcpyDeviceToHost, c->stream));
+      // chunked only for the double-only evaluation: its strips are short (config 4 rate: the
+      // download hides behind the next chunk, 36 -> 30 ms per step); the long LERP strips are
+      // long-running waves that a launch split leaves idle at every chunk's tail (94 -> 188 ms)
+      const int nch = (P.gsel || rp.do_long) ? 1 : (int)std::min<int64_t>(8, std::max<int64_t>(1, ns / 64));
+      int64_t s_lo = 0;
+      for (int ci = 0; ci < nch; ci++) {
+        int64_t s_hi = ci + 1 == nch ? ns : std::max(s_lo, ns * (ci + 1) / nch);
+        while (s_hi > s_lo && s_hi < ns && sg[s_hi] == sg[s_hi - 1]) s_hi++;   // end at a group boundary
+        if (ci + 1 == nch) s_hi = ns;
+        if (!P.gsel && s_hi > s_lo) {
+          RawParams ep = rp;
+          ep.strip_g = rp.strip_g + s_lo;
+          ep.strip_t = rp.strip_t + s_lo;
+          ep.n_strips = s_hi - s_lo;
+          HIP_OK(launch_raw_eval(ep, c->stream));
+        }
+        // output points of groups [first group of the chunk, first group of the next chunk)
+        const int64_t o0 = s_lo < ns ? ooff[sg[s_lo]] : nout;
+        const int64_t o1 = s_hi < ns ? ooff[sg[s_hi]] : nout;
+        HIP_OK(hipEventRecord(c->cev[ci], c->stream));
+        if (o1 > o0) {
+          HIP_OK(hipStreamWaitEvent(c->copy_stream, c->cev[ci], 0));
+          HIP_OK(hipMemcpyAsync(const_cast<int64_t*>(direct_r->ts_ms) + o0, rp.out_ts + o0, (o1 - o0) * 8,
+                                hipMemcpyDeviceToHost, c->copy_stream));
+          HIP_OK(hipMemcpyAsync(const_cast<uint64_t*>(direct_r->value_bits) + o0, rp.out_bits + o0, (o1 - o0) * 8,
+                                hipMemcpyDeviceToHost, c->copy_stream));
+          HIP_OK(hipMemcpyAsync(const_cast<uint8_t*>(direct_r->is_int) + o0, rp.out_int + o0, o1 - o0,
+                                hipMemcpyDeviceToHost, c->copy_stream));
+        }
+        s_lo = s_hi;
       }
+      HIP_OK(hipEventRecord(c->ev[1], c->stream));
+      HIP_OK(hipStreamSynchronize(c->copy_stream));
     } else {
+      HIP_OK(hipEventRecord(c->ev[1], c->stream));
       res_ts.resize(base + nout);
       res_bits.resize(base + nout);
       res_int.resize(base + nout);
@@ -2539,7 +2656,7 @@ extern "C" int tsdbhip_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n,
         if (!rc) rc = collect(c, &qs[i], P, P.none ? c->n_series : G, true, &outs[i]);
       }
       if (rc) {
-        for (int j = 0; j < n; j++) { std::free(outs[j]); outs[j] = nullptr; }
+        for (int j = 0; j < n; j++) { result_free(outs[j]); outs[j] = nullptr; }
         return rc;
       }
     }
@@ -2570,14 +2687,14 @@ extern "C" int tsdbhip_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n,
       }
     }
     if (rc) {
-      for (int j = 0; j < n; j++) { std::free(outs[j]); outs[j] = nullptr; }
+      for (int j = 0; j < n; j++) { result_free(outs[j]); outs[j] = nullptr; }
       return rc;
     }
   }
   return 0;
 }
 
-extern "C" void tsdbhip_result_free(tsdbhip_result* r) { std::free(r); }
+extern "C" void tsdbhip_result_free(tsdbhip_result* r) { result_free(r); }
 
 extern "C" int tsdbhip_last_timing(tsdbhip_ctx* c, tsdbhip_timing* out) {
   if (!c || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
