@@ -258,6 +258,55 @@ class HostBatch:
         return len(self.row_base_time)
 
 
+class RollupBatch(C.Structure):
+    """tsdbhip_rollup_batch: RollupSeq rows of the queried aggregate (+ count cells)."""
+    _fields_ = [
+        ("cells", Batch),
+        ("row_cqual_off", C.POINTER(C.c_uint64)),
+        ("row_cval_off", C.POINTER(C.c_uint64)),
+        ("cqual", C.POINTER(C.c_uint8)),
+        ("cval", C.POINTER(C.c_uint8)),
+        ("interval", RollupInterval),
+        ("fix_duplicates", C.c_int32),
+    ]
+
+
+class HostRollupBatch:
+    """Owns the arrays behind a :class:`RollupBatch`.  `counts` is None (no count cells:
+    RollupSeq.need_count false) or (row_cqual_off, row_cval_off, cqual, cval)."""
+
+    def __init__(self, cells: HostBatch, counts, interval: RollupInterval, fix_duplicates: bool = False):
+        self.cells = cells
+        self.interval = interval
+        self.fix_duplicates = bool(fix_duplicates)
+        self.c = RollupBatch()
+        self.c.cells = cells.c
+        self.c.interval = interval
+        self.c.fix_duplicates = int(fix_duplicates)
+        if counts is None:
+            self.counts = None
+        else:
+            cq_off, cv_off, cq, cv = counts
+            cq_off = np.ascontiguousarray(cq_off, dtype=np.uint64)
+            cv_off = np.ascontiguousarray(cv_off, dtype=np.uint64)
+            cq = np.ascontiguousarray(cq, dtype=np.uint8)
+            cv = np.ascontiguousarray(cv, dtype=np.uint8)
+            if cq.size == 0:
+                cq = np.zeros(1, np.uint8)
+            if cv.size == 0:
+                cv = np.zeros(1, np.uint8)
+            assert len(cq_off) == cells.n_rows + 1 and len(cv_off) == cells.n_rows + 1
+            self.counts = (cq_off, cv_off, cq, cv)
+            self.c.row_cqual_off = _ptr(cq_off, C.c_uint64)
+            self.c.row_cval_off = _ptr(cv_off, C.c_uint64)
+            self.c.cqual = _ptr(cq, C.c_uint8)
+            self.c.cval = _ptr(cv, C.c_uint8)
+
+    @property
+    def need_count(self) -> bool:
+        return self.counts is not None
+
+
 def _view(ptr, n: int, dtype, owner):
     """numpy view of n elements at a ctypes pointer; `owner` is kept alive by the view."""
     nbytes = n * np.dtype(dtype).itemsize

@@ -331,6 +331,21 @@ struct DevBuf {
 
 }  // namespace
 
+// One RollupSeq of a rollup batch (RollupSpan.addRow merges the cells of one row key):
+// what the query-time scan needs of it.
+struct RoSeqRow {
+  int64_t base = 0;
+  int64_t order = 0;            // scan order inside the series
+  int32_t err = 0;              // RollupSeq.append's exception for these cells (thrown when scanned)
+  std::string msg;
+  bool verr = false;            // a value the extract functions reject (thrown when read)
+  bool cerr = false;            // a count the extract functions reject (thrown by valueCount())
+  int64_t npts = 0;             // datapoints the RollupIterator yields
+  int64_t last_ts = 0;          // its last timestamp (ms)
+  int64_t pp_ts = INT64_MAX;    // first value cell after which value / count cells stop pairing one
+                                // to one (RollupIterator.seek walks them in lock step)
+};
+
 struct tsdbhip_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -408,6 +423,20 @@ struct tsdbhip_ctx {
     uint64_t bytes = 0;
   } ro_out[4];
   int ro_n = 0;
+  // rollup read path (tsdbhip_load_rollup): the resident batch holds the value series (batch
+  // positions [0, ro_nval), their groups) and, with count cells, one count series per value
+  // series (positions ro_nval + s, no group), both re-rowed into hour rows
+  bool ro_active = false, ro_counts = false;
+  tsdbhip_rollup_interval ro_iv{};
+  int64_t ro_nval = 0;
+  std::vector<int64_t> ro_rp;          // [ro_nval + 1] -> ro_rows
+  std::vector<RoSeqRow> ro_rows;
+  std::vector<std::string> ro_unsup;   // per value series: why the engine does not run it ("" = runs)
+  std::vector<int64_t> ro_res;         // batch position -> resident index
+  DevBuf ro_cmap;                      // [n_series] resident index of a value series' count series (-1: none)
+  bool ro_scan_valid = false;          // scan-active value series of the last scan range
+  int64_t ro_scan_ss = 0, ro_scan_se = 0;
+  std::vector<uint8_t> ro_scan_act;    // [n_series] resident: rollup rows in the scan range
 };
 
 // ===========================================================================
@@ -558,6 +587,14 @@ static void release_batch(tsdbhip_ctx* c) {
   c->lc_valid = false;
   c->calc_valid = false;
   c->n_series = c->n_rows = c->n_groups = 0;
+  c->ro_active = c->ro_counts = false;
+  c->ro_scan_valid = false;
+  c->ro_nval = 0;
+  c->ro_rp.clear();
+  c->ro_rows.clear();
+  c->ro_unsup.clear();
+  c->ro_res.clear();
+  c->ro_cmap.release();
 }
 
 extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
@@ -989,6 +1026,269 @@ static int load_with(tsdbhip_ctx* c, const tsdbhip_batch* b, const std::vector<i
 
 extern "C" int tsdbhip_load(tsdbhip_ctx* c, const tsdbhip_batch* b) { return load_with(c, b, nullptr); }
 
+// ---- rollup read path ---------------------------------------------
+// The host restates what the scan builds of a rollup table -- RollupSpan.addRow
+// (src/rollup/RollupSpan.java:62-80), RollupSeq.append (src/rollup/RollupSeq.java:238-318)
+// and the RollupIterator's sync (:521-555) -- and hands the device the datapoints the
+// iterators yield: each value series (its cells decoded by the resident kernels as they are)
+// and, with count cells, a count series of valueCount()s, both re-rowed into hour rows with
+// 2-byte second qualifiers.  Every hour row holds the points of one rollup row (rollup row
+// spans are whole hours), so the scan range picks the same points either way.
+namespace {
+
+struct RoCell {
+  uint32_t q;
+  const uint8_t* v;
+};
+
+int64_t ro_cell_len(uint32_t q) { return (q & 7) + 1; }   // Internal.getValueLengthFromQualifier
+
+// valueCount() of a count cell (RollupSeq.java:661-675): the integer, or (long) of the float
+bool ro_count_value(const RoCell& k, int64_t& out) {
+  const uint8_t* p = k.v;
+  auto be = [&](int n) { uint64_t x = 0; for (int i = 0; i < n; i++) x = (x << 8) | p[i]; return x; };
+  if ((k.q & 0x8) == 0) {
+    switch (k.q & 7) {
+      case 7: out = (int64_t)be(8); return true;
+      case 3: out = (int32_t)(uint32_t)be(4); return true;
+      case 1: out = (int16_t)(uint16_t)be(2); return true;
+      case 0: out = (int8_t)p[0]; return true;
+      default: return false;
+    }
+  }
+  double x;
+  if ((k.q & 7) == 7) { const uint64_t u = be(8); std::memcpy(&x, &u, 8); }
+  else if ((k.q & 7) == 3) { const uint32_t u = (uint32_t)be(4); float f; std::memcpy(&f, &u, 4); x = f; }
+  else return false;
+  out = x != x ? 0 : (x >= 9.2233720368547758e18 ? INT64_MAX : (x <= -9.2233720368547758e18 ? INT64_MIN : (int64_t)x));
+  return true;
+}
+
+bool ro_value_ok(uint32_t q) {   // extractIntegerValue / extractFloatingPointValue accept these
+  const uint32_t l = q & 7;
+  return (q & 0x8) ? (l == 3 || l == 7) : (l == 0 || l == 1 || l == 3 || l == 7);
+}
+
+// Internal.vleEncodeLong
+int vle_put(std::vector<uint8_t>& out, int64_t v) {
+  int n = (v >= -128 && v <= 127) ? 1 : (v >= -32768 && v <= 32767) ? 2 : (v >= INT32_MIN && v <= INT32_MAX) ? 4 : 8;
+  for (int i = n - 1; i >= 0; i--) out.push_back((uint8_t)((uint64_t)v >> (8 * i)));
+  return n;
+}
+
+}  // namespace
+
+extern "C" int tsdbhip_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* rb) {
+  if (!c || !rb) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  const tsdbhip_batch* b = &rb->cells;
+  const bool cnt = rb->row_cqual_off != nullptr;
+  if (cnt && (!rb->row_cval_off || !rb->cqual || !rb->cval)) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null count arrays");
+  const tsdbhip_rollup_interval iv = rb->interval;
+  if (iv.interval_s <= 0 || iv.intervals <= 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad rollup interval");
+  const int64_t NS = b->n_series;
+  if (NS < 0 || b->n_rows < 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
+  if (NS > 0 && (!b->series_row_ptr || !b->group_id)) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null batch arrays");
+  if (b->n_rows > 0 && (!b->row_base_time || !b->row_qual_off || !b->row_val_off || !b->qual || !b->val))
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, "null batch arrays");
+  if (NS > 0 && (b->series_row_ptr[0] != 0 || b->series_row_ptr[NS] != b->n_rows))
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, "series_row_ptr does not cover the rows");
+  for (int64_t s = 0; s < NS; s++)
+    if (b->series_row_ptr[s + 1] < b->series_row_ptr[s]) return fail(TSDB_E_ILLEGAL_ARGUMENT, "series_row_ptr not monotonic");
+  for (int64_t r = 0; r < b->n_rows; r++) {
+    if (b->row_qual_off[r + 1] < b->row_qual_off[r] || b->row_val_off[r + 1] < b->row_val_off[r] ||
+        (cnt && (rb->row_cqual_off[r + 1] < rb->row_cqual_off[r] || rb->row_cval_off[r + 1] < rb->row_cval_off[r])))
+      return fail(TSDB_E_ILLEGAL_ARGUMENT, "cell offsets not monotonic");
+  }
+  const int64_t iv_ms = (int64_t)iv.interval_s * 1000;
+  // the converted batch: value series [0, NS), then (cnt) count series [NS, 2 NS)
+  struct Out {
+    std::vector<int64_t> srp{0};
+    std::vector<uint32_t> base;
+    std::vector<uint64_t> qo{0}, vo{0};
+    std::vector<uint8_t> q, v;
+  } ov, oc;
+  std::vector<RoSeqRow> rows;
+  std::vector<int64_t> rp{0};
+  std::vector<std::string> unsup(NS);
+  struct Pt { int64_t ts; RoCell v; int64_t n; };
+  for (int64_t s = 0; s < NS; s++) {
+    struct Seq {
+      RoSeqRow info;
+      std::vector<RoCell> vc, cc;
+      int64_t lo = -1, lco = -1;
+    };
+    std::vector<Seq> seqs;
+    for (int64_t r = b->series_row_ptr[s]; r < b->series_row_ptr[s + 1]; r++) {
+      // RollupSpan.addRow: a row with the last row's key appends to that RollupSeq
+      if (seqs.empty() || seqs.back().info.base != (int64_t)b->row_base_time[r]) {
+        seqs.emplace_back();
+        seqs.back().info.base = b->row_base_time[r];
+        seqs.back().info.order = (int64_t)seqs.size() - 1;
+      }
+      Seq& sq = seqs.back();
+      if (sq.info.err) continue;   // the scan throws at the first bad cell of this key
+      // RollupSeq.append :238-318 per cell, value cells then count cells (qualifier order)
+      for (int pass = 0; pass < (cnt ? 2 : 1) && !sq.info.err; pass++) {
+        const bool isc = pass == 1;
+        const uint64_t* qo = isc ? rb->row_cqual_off : b->row_qual_off;
+        const uint64_t* vo = isc ? rb->row_cval_off : b->row_val_off;
+        const uint8_t* qb = isc ? rb->cqual : b->qual;
+        const uint8_t* vb = isc ? rb->cval : b->val;
+        const int64_t ql = (int64_t)(qo[r + 1] - qo[r]), vl = (int64_t)(vo[r + 1] - vo[r]);
+        if (ql % 2) { sq.info.err = TSDB_E_ILLEGAL_DATA; sq.info.msg = "rollup qualifiers are 2 bytes"; break; }
+        int64_t vi = 0;
+        for (int64_t i = 0; i < ql; i += 2) {
+          const uint32_t q = ((uint32_t)qb[qo[r] + i] << 8) | qb[qo[r] + i + 1];
+          const int64_t len = ro_cell_len(q);
+          if (vi + len > vl) { sq.info.err = TSDB_E_ILLEGAL_DATA; sq.info.msg = "rollup value bytes shorter than the qualifiers say"; break; }
+          const int64_t off = (int64_t)(q >> 4);
+          int64_t& last = isc ? sq.lco : sq.lo;
+          std::vector<RoCell>& cells = isc ? sq.cc : sq.vc;
+          if (last > -1 && off <= last) {
+            if (off == last && rb->fix_duplicates) {
+              cells.pop_back();   // the later cell replaces the earlier one (equal write timestamps)
+            } else {
+              sq.info.err = isc ? TSDB_E_ILLEGAL_ARGUMENT : TSDB_E_ILLEGAL_DATA;
+              sq.info.msg = std::string(isc ? "The count offset " : "The offset ") + std::to_string(off) +
+                            " is <= the last offset " + std::to_string(last);
+              break;
+            }
+          }
+          last = off;
+          cells.push_back({q, vb + vo[r] + vi});
+          vi += len;
+        }
+        if (!sq.info.err && vi != vl) { sq.info.err = TSDB_E_ILLEGAL_DATA; sq.info.msg = "rollup value bytes longer than the qualifiers say"; }
+      }
+    }
+    // Span.checkRowOrder: stable sort by base time; then each RollupIterator's datapoints
+    std::vector<Seq*> sorted;
+    for (auto& sq : seqs) sorted.push_back(&sq);
+    std::stable_sort(sorted.begin(), sorted.end(), [](const Seq* x, const Seq* y) { return x->info.base < y->info.base; });
+    std::vector<Pt> pts;
+    for (size_t i = 0; i < sorted.size(); i++) {
+      Seq& sq = *sorted[i];
+      if (i > 0 && sorted[i - 1]->info.base == sq.info.base && unsup[s].empty())
+        unsup[s] = "two RollupSeqs with one row key (cells of a key not adjacent in the batch)";
+      if (sq.info.err) continue;
+      int32_t basetime = 0;
+      if (tsdbhip_rollup_basetime(sq.info.base, &iv, &basetime) || basetime != sq.info.base) {
+        if (unsup[s].empty()) unsup[s] = "rollup row base time not on the table's row span";
+        continue;
+      }
+      const int64_t nv = (int64_t)sq.vc.size(), nc = (int64_t)sq.cc.size();
+      int64_t qi = 0, ci = 0;
+      auto sync = [&]() {   // RollupIterator.sync :521-555
+        while (qi < nv && ci < nc) {
+          const int64_t a = sq.vc[qi].q >> 4, d = sq.cc[ci].q >> 4;
+          if (a == d) return;
+          if (a > d) ci++; else qi++;
+        }
+      };
+      if (cnt) {
+        sync();
+        // lock-step pairing from the first matched pair (RollupIterator.seek walks both)
+        for (int64_t k = 0; qi + k < nv; k++) {
+          if (ci + k >= nc || (sq.vc[qi + k].q >> 4) != (sq.cc[ci + k].q >> 4)) {
+            sq.info.pp_ts = sq.info.base * 1000 + (int64_t)(sq.vc[qi + k].q >> 4) * iv_ms;
+            break;
+          }
+        }
+      }
+      for (;;) {
+        if (cnt) sync();
+        if (!(qi < nv && (!cnt || ci < nc))) break;
+        const RoCell& v = sq.vc[qi++];
+        int64_t n = 1;
+        if (cnt && !ro_count_value(sq.cc[ci++], n)) sq.info.cerr = true;
+        if (!ro_value_ok(v.q)) sq.info.verr = true;
+        const int64_t ts = sq.info.base * 1000 + (int64_t)(v.q >> 4) * iv_ms;
+        int32_t bt = 0;
+        if ((tsdbhip_rollup_basetime(ts / 1000, &iv, &bt) || bt != sq.info.base) && unsup[s].empty())
+          unsup[s] = "rollup offset beyond the row span";
+        pts.push_back({ts, v, n});
+        sq.info.npts++;
+        sq.info.last_ts = ts;
+      }
+    }
+    for (size_t i = 1; i < pts.size() && unsup[s].empty(); i++)
+      if (pts[i].ts <= pts[i - 1].ts) unsup[s] = "rollup datapoints out of time order across rows";
+    for (auto& sq : seqs) rows.push_back(sq.info);
+    rp.push_back((int64_t)rows.size());
+    if (!unsup[s].empty()) pts.clear();
+    // hour rows: compacted cells (2-byte qualifiers, meta byte 0 after two or more points)
+    for (size_t i = 0; i < pts.size();) {
+      const int64_t hb = (pts[i].ts / 1000) - (pts[i].ts / 1000) % 3600;
+      size_t j = i;
+      while (j < pts.size() && pts[j].ts / 1000 - hb < 3600) j++;
+      for (int side = 0; side < (cnt ? 2 : 1); side++) {
+        Out& o = side ? oc : ov;
+        o.base.push_back((uint32_t)hb);
+        for (size_t k = i; k < j; k++) {
+          const uint32_t off = (uint32_t)(pts[k].ts / 1000 - hb);
+          uint32_t q;
+          if (side == 0) {
+            q = (off << 4) | (pts[k].v.q & 0xF);
+            o.v.insert(o.v.end(), pts[k].v.v, pts[k].v.v + ro_cell_len(pts[k].v.q));
+          } else {
+            q = (off << 4) | (uint32_t)(vle_put(o.v, pts[k].n) - 1);
+          }
+          o.q.push_back((uint8_t)(q >> 8));
+          o.q.push_back((uint8_t)q);
+        }
+        if (j - i > 1) o.v.push_back(0);
+        o.qo.push_back(o.q.size());
+        o.vo.push_back(o.v.size());
+      }
+      i = j;
+    }
+    ov.srp.push_back((int64_t)ov.base.size());
+    if (cnt) oc.srp.push_back((int64_t)oc.base.size());
+  }
+  // one batch: the count series after the value series
+  const int64_t nrv = (int64_t)ov.base.size();
+  std::vector<int32_t> gid(b->group_id, b->group_id + NS);
+  if (cnt) {
+    for (size_t i = 1; i < oc.srp.size(); i++) ov.srp.push_back(nrv + oc.srp[i]);
+    const uint64_t q0 = ov.q.size(), v0 = ov.v.size();
+    ov.base.insert(ov.base.end(), oc.base.begin(), oc.base.end());
+    for (size_t i = 1; i < oc.qo.size(); i++) { ov.qo.push_back(q0 + oc.qo[i]); ov.vo.push_back(v0 + oc.vo[i]); }
+    ov.q.insert(ov.q.end(), oc.q.begin(), oc.q.end());
+    ov.v.insert(ov.v.end(), oc.v.begin(), oc.v.end());
+    gid.insert(gid.end(), NS, -1);
+  }
+  if (ov.q.empty()) ov.q.push_back(0);
+  if (ov.v.empty()) ov.v.push_back(0);
+  tsdbhip_batch m{};
+  m.n_series = cnt ? 2 * NS : NS;
+  m.series_row_ptr = ov.srp.data();
+  m.n_rows = (int64_t)ov.base.size();
+  m.row_base_time = ov.base.data();
+  m.row_qual_off = ov.qo.data();
+  m.row_val_off = ov.vo.data();
+  m.qual = ov.q.data();
+  m.val = ov.v.data();
+  m.group_id = gid.data();
+  int rc = load_impl(c, &m);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->ro_active = true;
+  c->ro_counts = cnt;
+  c->ro_iv = iv;
+  c->ro_nval = NS;
+  c->ro_rp = std::move(rp);
+  c->ro_rows = std::move(rows);
+  c->ro_unsup = std::move(unsup);
+  c->ro_res.assign(c->n_series, -1);
+  for (int64_t i = 0; i < c->n_series; i++) c->ro_res[c->h_orig[i]] = i;
+  std::vector<int64_t> cmap(std::max<int64_t>(1, c->n_series), -1);
+  if (cnt)
+    for (int64_t s = 0; s < NS; s++) cmap[c->ro_res[s]] = c->ro_res[NS + s];
+  HIP_OK(c->ro_cmap.ensure((int64_t)cmap.size() * 8));
+  HIP_OK(hipMemcpy(c->ro_cmap.p, cmap.data(), cmap.size() * 8, hipMemcpyHostToDevice));
+  return 0;
+}
+
 // ---- sharding a host batch over ranks ----------------------------------------
 namespace {
 
@@ -1192,6 +1492,7 @@ extern "C" int tsdbhip_synth_shard(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp,
 
 extern "C" int tsdbhip_batch_sizes(tsdbhip_ctx* c, int64_t* n_series, int64_t* n_rows, uint64_t* qual_bytes,
                                    uint64_t* val_bytes) {
+  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_batch_sizes over a rollup batch (tsdbhip_load_rollup)");
   if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
   uint64_t q = 0, v = 0;
   for (int64_t r = 0; r < c->n_rows; r++) { q += c->h_qlen[r]; v += c->h_vlen[r]; }
@@ -1206,6 +1507,7 @@ extern "C" int tsdbhip_batch_sizes(tsdbhip_ctx* c, int64_t* n_series, int64_t* n
 extern "C" int tsdbhip_batch_download(tsdbhip_ctx* c, int64_t* series_row_ptr, uint32_t* row_base_time,
                                       uint64_t* row_qual_off, uint64_t* row_val_off, uint8_t* qual, uint8_t* val,
                                       int32_t* group_id) {
+  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_batch_download over a rollup batch (tsdbhip_load_rollup)");
   if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_OK(hipSetDevice(c->device));
@@ -1416,6 +1718,36 @@ int plan_calendar(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
   return 0;
 }
 
+// TsdbQuery.getScanStartTimeSeconds :1515-1526 / getScanEndTimeSeconds :1562-1567 with a
+// RollupQuery: the rollup row of the start (one further back for a rate), the row of the end
+// plus one row span.
+int rollup_scan_bounds(const tsdbhip_query* q, const tsdbhip_rollup_interval& iv, int64_t& ss, int64_t& se) {
+  int64_t start = q->start_time;
+  if ((start & (int64_t)0xFFFFFFFF00000000LL) != 0) start /= 1000;
+  int32_t b = 0;
+  int rc = tsdbhip_rollup_basetime(start, &iv, &b);
+  if (rc) return rc;
+  if (q->rate) {
+    rc = tsdbhip_rollup_basetime((int64_t)b - 1, &iv, &b);
+    if (rc) return rc;
+  }
+  ss = b;
+  int64_t end = q->end_time;
+  if ((end & (int64_t)0xFFFFFFFF00000000LL) != 0) {
+    end /= 1000;
+    if (end - (end * 1000) < 1) end++;
+  }
+  rc = tsdbhip_rollup_basetime(end + (int64_t)iv.interval_s * iv.intervals, &iv, &b);
+  if (rc) return rc;
+  se = b;
+  return 0;
+}
+
+int scan_bounds_of(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t& ss, int64_t& se) {
+  if (c->ro_active) return rollup_scan_bounds(q, c->ro_iv, ss, se);
+  return tsdbhip_scan_bounds(q, &ss, &se);
+}
+
 int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
   if (q->aggregator < 0 || q->aggregator >= TSDB_AGG_COUNT_ALL) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad aggregator");
   if (q->ds_function >= TSDB_AGG_COUNT_ALL) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad downsampling function");
@@ -1430,7 +1762,7 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
     if (P.ga < 0) return fail(TSDB_E_NOT_IMPLEMENTED, std::string("group-by aggregator not implemented yet: ") + AGG_NAMES[q->aggregator]);
     P.interp = interp_of(q->aggregator);
     P.none = q->aggregator == TSDB_AGG_NONE;
-    tsdbhip_scan_bounds(q, &P.ss, &P.se);
+    { const int brc = scan_bounds_of(c, q, P.ss, P.se); if (brc) return brc; }
     return 0;
   }
   if (!q->ds_all && q->ds_interval_ms <= 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "interval not > 0");
@@ -1457,7 +1789,7 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
               (P.ga == GA_SUM || P.ga == GA_AVG || P.ga == GA_SQUARESUM || P.ga == GA_DEV || P.ga == GA_MULT);
   P.interp = interp_of(q->aggregator);
   P.none = q->aggregator == TSDB_AGG_NONE;
-  tsdbhip_scan_bounds(q, &P.ss, &P.se);
+  { const int brc = scan_bounds_of(c, q, P.ss, P.se); if (brc) return brc; }
   const int64_t S0 = P.ss * 1000, E0 = P.se * 1000;
   if (q->ds_all) {
     P.mode = MODE_ALL;
@@ -2240,6 +2572,17 @@ int collect(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bo
     const int64_t S0 = P.ss * 1000, E0 = P.se * 1000;
     if (q->start_time < S0 || q->start_time > E0) std::fill(flag.begin(), flag.end(), 0);
   }
+  if (c->ro_active && c->ro_scan_valid) {
+    // rollup: a span the scan found is a SpanGroup member (or, NONE, its own SpanGroup) even
+    // when its RollupSeqs yield no datapoint; count series are no spans of the query
+    for (int64_t i = 0; i < c->n_series; i++) {
+      if (P.none) {
+        if (i < G) act[i] = c->h_orig[i] < c->ro_nval ? (act[i] | c->ro_scan_act[i]) : 0;
+      } else if (c->ro_scan_act[i] && c->h_group[i] < G) {
+        act[c->h_group[i]] = 1;
+      }
+    }
+  }
   return assemble(c, q, P, G, val, flag, act, out);
 }
 
@@ -2594,11 +2937,122 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
 
 }  // namespace
 
+namespace {
+
+// The scan of a rollup query over the resident rollup batch: RollupSeq.append's exceptions
+// (thrown while the spans are built, in scan order), reads the engine does not restate, and
+// which value series the scan finds (cached per scan range).
+int ro_scan(tsdbhip_ctx* c, const Plan& P, bool reads_counts) {
+  for (int64_t s = 0; s < c->ro_nval; s++) {
+    const RoSeqRow* first_err = nullptr;
+    bool in = false, verr = false, cerr = false;
+    for (int64_t i = c->ro_rp[s]; i < c->ro_rp[s + 1]; i++) {
+      const RoSeqRow& r = c->ro_rows[i];
+      if (r.base < P.ss || r.base >= P.se) continue;
+      in = true;
+      if (r.err && (!first_err || r.order < first_err->order)) first_err = &r;
+      verr |= r.verr;
+      cerr |= r.cerr;
+    }
+    if (first_err) return fail(first_err->err, first_err->msg);
+    if (!in) continue;
+    if (!c->ro_unsup[s].empty()) return fail(TSDB_E_NOT_IMPLEMENTED, "rollup span: " + c->ro_unsup[s]);
+    if (verr) return fail(TSDB_E_ILLEGAL_DATA, "rollup value of a bad length");
+    if (cerr && reads_counts) return fail(TSDB_E_ILLEGAL_DATA, "rollup count of a bad length");
+  }
+  // RollupIterator.seek walks value and count cells in lock step from the first pair: past a
+  // cell where they stop pairing one to one its iteration differs from a fresh one's.  The
+  // Downsampler seeks every span to its first bucket; a RollupSeq it seeks into past such a
+  // cell is not restated.
+  const int64_t S0 = P.ss * 1000;
+  const int64_t T = P.mode == MODE_TABLE ? P.seek : (P.mode == MODE_ALL ? S0 : P.B0);
+  if (c->ro_counts && T > S0) {
+    for (int64_t s = 0; s < c->ro_nval; s++) {
+      const RoSeqRow* pick = nullptr;   // Span.seekRow: first row (by base) whose last point >= T
+      for (int64_t i = c->ro_rp[s]; i < c->ro_rp[s + 1]; i++) {
+        const RoSeqRow& r = c->ro_rows[i];
+        if (r.base < P.ss || r.base >= P.se || r.npts < 1 || r.last_ts < T) continue;
+        if (!pick || r.base < pick->base) pick = &r;
+      }
+      if (pick && pick->pp_ts < T)
+        return fail(TSDB_E_NOT_IMPLEMENTED, "rollup row whose value and count cells stop pairing before the seek point");
+    }
+  }
+  if (!(c->ro_scan_valid && c->ro_scan_ss == P.ss && c->ro_scan_se == P.se)) {
+    c->ro_scan_act.assign(std::max<int64_t>(1, c->n_series), 0);
+    for (int64_t s = 0; s < c->ro_nval; s++)
+      for (int64_t i = c->ro_rp[s]; i < c->ro_rp[s + 1]; i++)
+        if (c->ro_rows[i].base >= P.ss && c->ro_rows[i].base < P.se) { c->ro_scan_act[c->ro_res[s]] = 1; break; }
+    c->ro_scan_valid = true;
+    c->ro_scan_ss = P.ss;
+    c->ro_scan_se = P.se;
+  }
+  return 0;
+}
+
+// TsdbQuery.run with a RollupQuery (src/core/TsdbQuery.java:1665-1700 builds it from the
+// downsampler; a count group-by aggregator sums).  Avg and count downsampling of a batch with
+// count cells (Downsampler.java:165-221, FillingDownsampler.java:196-253):
+//   1. every series' SUM downsampling (value series: Σsum per bucket, count series: Σcount)
+//      into pre_dense, one NONE tile per series;
+//   2. k_rollup_combine: each value series' buckets <- Σsum / Σcount (0 when Σcount is 0) or
+//      Σcount;
+//   3. the SpanGroup step (rate, fill, LERP, group-by) over those buckets (k_emit).
+// Every other downsampling function reads only the value series: the ordinary pipeline.
+int run_rollup(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
+  if (q->ds_function < 0 || (!q->ds_all && q->ds_interval_ms <= 0))
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, "a rollup query needs a downsampling interval");
+  if (q->ds_function == TSDB_AGG_DEV)
+    return fail(TSDB_E_UNSUPPORTED, "Standard deviation over rolled up data is not supported at this time");
+  tsdbhip_query qr = *q;
+  if (qr.aggregator == TSDB_AGG_COUNT) qr.aggregator = TSDB_AGG_SUM;
+  const bool combine = c->ro_counts && (q->ds_function == TSDB_AGG_AVG || q->ds_function == TSDB_AGG_COUNT);
+  Plan P;
+  int rc = plan_query(c, &qr, P);
+  if (rc) return rc;
+  rc = ro_scan(c, P, combine);
+  if (rc) return rc;
+  const int64_t G = P.none ? c->n_series : c->n_groups;
+  if (!combine) {
+    if (P.gsel || P.ordered) {
+      rc = P.gsel ? run_sel_group(c, &qr, P, G) : run_ordered(c, &qr, P, G);
+      if (rc) return rc;
+      return collect(c, &qr, P, G, true, out);
+    }
+    rc = run_device(c, &qr, P, G, true);
+    if (rc) return rc;
+    return collect(c, &qr, P, G, true, out);
+  }
+  if (P.gsel || P.ordered)
+    return fail(TSDB_E_NOT_IMPLEMENTED, "avg / count rollup downsampling with a percentile group-by or the ordered flag");
+  tsdbhip_query q1 = qr;
+  q1.ds_function = TSDB_AGG_SUM;
+  q1.aggregator = TSDB_AGG_NONE;
+  q1.rate = 0;
+  q1.flags = 0;
+  Plan P1;
+  rc = plan_query(c, &q1, P1);
+  if (rc) return rc;
+  if (P1.K != P.K || P1.B0 != P.B0) return fail(TSDB_E_HIP, "rollup combine: plans disagree");
+  P1.dense_out = true;
+  rc = run_device(c, &q1, P1, c->n_series, false);
+  if (rc) return rc;
+  HIP_OK(launch_rollup_combine(c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->ro_cmap.as<int64_t>(),
+                               c->n_series, P.K, q->ds_function == TSDB_AGG_AVG ? 1 : 0, c->stream));
+  P.emit_only = true;
+  rc = run_device(c, &qr, P, G, true);
+  if (rc) return rc;
+  return collect(c, &qr, P, G, true, out);
+}
+
+}  // namespace
+
 extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
   if (!c || !q || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
   *out = nullptr;
   HIP_OK(hipSetDevice(c->device));
+  if (c->ro_active) return run_rollup(c, q, out);
   Plan P;
   int rc = plan_query(c, q, P);
   if (rc) return rc;
@@ -2621,6 +3075,7 @@ extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_resul
 // streaming pass.  The queries must share the time range and the downsampling specification;
 // rate, aggregator and flags may differ.
 extern "C" int tsdbhip_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_result** outs) {
+  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_run_multi over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !qs || !outs || n < 1) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad argument");
   for (int i = 0; i < n; i++) outs[i] = nullptr;
   for (int i = 1; i < n; i++) {
@@ -2739,6 +3194,7 @@ int plan_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_globa
 
 extern "C" int tsdbhip_partials_layout_get(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global,
                                            tsdbhip_partials_layout* out) {
+  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_partials_layout_get over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   Plan P;
   int rc = plan_partials(c, q, n_groups_global, P);
@@ -2750,6 +3206,7 @@ extern "C" int tsdbhip_partials_layout_get(tsdbhip_ctx* c, const tsdbhip_query* 
 }
 
 extern "C" int tsdbhip_run_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, void* partials) {
+  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_run_partials over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !partials) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_OK(hipSetDevice(c->device));
@@ -2796,6 +3253,7 @@ extern "C" int tsdbhip_run_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int6
 
 extern "C" int tsdbhip_finalize(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, const void* partials,
                                 int n_ranks, tsdbhip_result** out) {
+  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_finalize over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !partials || !out || n_ranks < 1) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad argument");
   std::lock_guard<std::mutex> lk(c->mu);
   *out = nullptr;
@@ -2848,6 +3306,7 @@ int plan_sel(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, Pl
 
 extern "C" int tsdbhip_sel_layout(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, int64_t* counts,
                                   int64_t* n_slots) {
+  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_sel_layout over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !counts || !n_slots) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   Plan P;
   int rc = plan_sel(c, q, n_groups_global, P);
@@ -2860,6 +3319,7 @@ extern "C" int tsdbhip_sel_layout(tsdbhip_ctx* c, const tsdbhip_query* q, int64_
 
 extern "C" int tsdbhip_sel_run_values(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, void* vals,
                                       void* uni, void* act) {
+  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_sel_run_values over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !vals || !uni || !act) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_OK(hipSetDevice(c->device));
@@ -2883,6 +3343,7 @@ extern "C" int tsdbhip_sel_run_values(tsdbhip_ctx* c, const tsdbhip_query* q, in
 
 extern "C" int tsdbhip_sel_select(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, const void* vals,
                                   const int64_t* counts, const void* uni, void* out_val, void* out_flag) {
+  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_sel_select over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !counts || !uni || !out_val || !out_flag) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_OK(hipSetDevice(c->device));
@@ -2936,6 +3397,7 @@ extern "C" int tsdbhip_sel_select(tsdbhip_ctx* c, const tsdbhip_query* q, int64_
 
 extern "C" int tsdbhip_assemble(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, const void* val,
                                 const void* flag, const void* act, tsdbhip_result** out) {
+  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_assemble over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !val || !flag || !act || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
   *out = nullptr;
@@ -3047,6 +3509,7 @@ extern "C" int tsdbhip_rollup_qualifier(int64_t timestamp, int32_t basetime, int
 }
 
 extern "C" int tsdbhip_rollup_run(tsdbhip_ctx* c, const tsdbhip_rollup_spec* sp, int64_t* n_cells, uint64_t* value_bytes) {
+  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_rollup_run over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !sp) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   if (!iv_valid(&sp->interval)) return fail(TSDB_E_ILLEGAL_ARGUMENT, "invalid rollup interval");
   if (sp->n_funcs < 1 || sp->n_funcs > 4) return fail(TSDB_E_ILLEGAL_ARGUMENT, "1..4 rollup functions");

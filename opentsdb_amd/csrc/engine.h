@@ -306,6 +306,10 @@ struct RollupAggParams {
 };
 hipError_t launch_rollup_agg(const GridParams& p, const RollupAggParams& rp, hipStream_t s);
 // each series' first datapoint >= t0 in rows with base in [ss, se) (INT64_MAX: none)
+// rollup read path: value series buckets <- Σsum / Σcount (avg) or Σcount, from the SUM
+// downsampling of each value series and of its count series (cmap[s], -1: none)
+hipError_t launch_rollup_combine(double* dense, const uint8_t* pres, const int64_t* cmap, int64_t n_series, int64_t K,
+                                 int avg, hipStream_t s);
 hipError_t launch_first_ts(const RowDesc* rows, const int64_t* srp, const uint8_t* qual, int64_t n, int64_t ss,
                            int64_t se, int64_t t0, int64_t* out, hipStream_t s);
 // streaming variant for one uniform row class (k_fast's premises + the sum certificate);

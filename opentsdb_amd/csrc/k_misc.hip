@@ -302,4 +302,33 @@ hipError_t launch_synth_write(const SynthParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Rollup read path: Downsampler.next's rollup branches
+// (src/core/Downsampler.java:165-221, FillingDownsampler.java:196-253) from two SUM
+// downsamplings.  dense[s][k] holds Σsum of value series s (in datapoint order, as the
+// reference's `sum += nextDoubleValue()`), dense[cmap[s]][k] Σcount of its count series; a
+// bucket with datapoints becomes Σsum / Σcount (0 when Σcount is 0) for avg, Σcount for
+// count.  The count series are never written (cmap of a count series is -1).
+__global__ __launch_bounds__(256) void k_rollup_combine(double* __restrict__ dense, const uint8_t* __restrict__ pres,
+                                                        const int64_t* __restrict__ cmap, int64_t n_series, int64_t K,
+                                                        int avg) {
+  const int64_t total = n_series * K;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = i / K;
+    const int64_t cs = cmap[s];
+    if (cs < 0 || !pres[i]) continue;
+    const double sum = dense[i];
+    const double count = dense[cs * K + (i - s * K)];
+    dense[i] = avg ? (count == 0.0 ? 0.0 : sum / count) : count;
+  }
+}
+
+hipError_t launch_rollup_combine(double* dense, const uint8_t* pres, const int64_t* cmap, int64_t n_series, int64_t K,
+                                 int avg, hipStream_t s) {
+  const int64_t total = n_series * K;
+  if (total <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_rollup_combine, dim3((unsigned)blocks), dim3(256), 0, s, dense, pres, cmap, n_series, K, avg);
+  return hipGetLastError();
+}
+
 }  // namespace tsdb

@@ -28,6 +28,7 @@ EXPORTS = [
     "tsdbhip_rollup_basetime", "tsdbhip_rollup_qualifier", "tsdbhip_rollup_run", "tsdbhip_rollup_download",
     "tsdbhip_sel_layout", "tsdbhip_sel_run_values", "tsdbhip_sel_select", "tsdbhip_assemble", "tsdbhip_run_multi",
     "tsdbhip_debug_rows", "tsdbhip_shard_bounds", "tsdbhip_load_shard", "tsdbhip_synth_shard",
+    "tsdbhip_load_rollup",
 ]
 
 SHARD_SERIES, SHARD_GROUPS, SHARD_SPANS = 0, 1, 2   # tsdbhip.h TSDB_SHARD_*
@@ -94,6 +95,7 @@ def lib():
         L.tsdbhip_shard_bounds.argtypes = [C.POINTER(abi.Batch), C.c_int, C.c_int, C.c_void_p]
         L.tsdbhip_load_shard.argtypes = [vp, C.POINTER(abi.Batch), C.c_int, C.c_int64, C.c_int64]
         L.tsdbhip_synth_shard.argtypes = [vp, C.POINTER(abi.SynthSpec), C.c_int64, C.c_int64]
+        L.tsdbhip_load_rollup.argtypes = [vp, C.POINTER(abi.RollupBatch)]
         _lib = L
     return _lib
 
@@ -200,6 +202,12 @@ class Engine:
         _check(lib().tsdbhip_load(self.ctx, C.byref(batch.c)))
         self._batch = batch
 
+    def load_rollup(self, rb: abi.HostRollupBatch):
+        """tsdbhip_load_rollup: a rollup table's scan result as the resident batch; run()
+        then answers rollup queries over it."""
+        _check(lib().tsdbhip_load_rollup(self.ctx, C.byref(rb.c)))
+        self._batch = rb
+
     def synth(self, n_series: int, start_s: int, n_points: int, period_ms: int, value_kind: int = 0,
               n_groups: int = 1, int_mod: int = 2000, seed: int = 0x5EED):
         sp = abi.SynthSpec(n_series, start_s, n_points, period_ms, value_kind, n_groups, int_mod, seed)
@@ -244,6 +252,10 @@ class Engine:
         outs = (C.POINTER(abi.Result) * n)()
         _check(lib().tsdbhip_run_multi(self.ctx, arr, n, outs))
         return [abi.result_to_groups(outs[i].contents, owner=_ResultOwner(outs[i])) for i in range(n)]
+
+    def run_rollup_batch(self, rb: abi.HostRollupBatch, q: abi.Query):
+        self.load_rollup(rb)
+        return self.run(q)
 
     def run_batch(self, batch: abi.HostBatch, q: abi.Query):
         """Runner for TsdbQuery: load the query's spans, then run."""

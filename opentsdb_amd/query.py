@@ -196,9 +196,12 @@ UNSET = -1
 class TsdbQuery:
     """Mirror of net.opentsdb.core.TsdbQuery for the aggregation path."""
 
-    def __init__(self, store: MockStore, runner=None):
+    def __init__(self, store: MockStore, runner=None, rollups=None, rollup_runner=None, fix_duplicates=False):
         self.store = store
         self.runner = runner
+        self.rollups = rollups              # rollup_read.RollupStore (tsdb.getRollupConfig() + tables)
+        self.rollup_runner = rollup_runner  # (HostRollupBatch, Query) -> groups; libtsdbhip by default
+        self.fix_duplicates = fix_duplicates
         self.start_time = UNSET
         self.end_time = UNSET
         self.metric = None
@@ -303,6 +306,76 @@ class TsdbQuery:
             e = end + (3600 - end % 3600)
         return s, e
 
+    def rollup_interval_name(self):
+        """transformDownSamplerToRollupQuery (TsdbQuery.java:1665-1700): the best-match rollup
+        table of the downsampling interval, or None (a raw scan)."""
+        ds = self.downsampler
+        if self.rollups is None or ds is None or ds.interval <= 0:
+            return None
+        from .rollup_read import NoSuchRollupForIntervalException
+        try:
+            return self.rollups.config.getRollupInterval(ds.interval // 1000)[0]
+        except NoSuchRollupForIntervalException:
+            return None
+
+    def _filters(self):
+        """Tag filters and group-by tag uids of setTimeSeries' tags (None: no series match)."""
+        tagk_ids = self.store.tagk.ids
+        tagv_ids = self.store.tagv.ids
+        filters = []   # (tagk uid, allowed tagv uid set or None)
+        group_bys = []
+        for k, v in self.tags.items():
+            if k not in tagk_ids:
+                return None
+            ku = tagk_ids[k]
+            if v == "*":
+                group_bys.append(ku)
+                filters.append((ku, None))
+            elif "|" in v:
+                allowed = {tagv_ids[x] for x in v.split("|") if x in tagv_ids}
+                group_bys.append(ku)
+                filters.append((ku, allowed))
+            else:
+                if v not in tagv_ids:
+                    return None
+                filters.append((ku, {tagv_ids[v]}))
+        group_bys.sort()
+
+        def pred(tags):
+            d = dict(tags)
+            for ku, allowed in filters:
+                if ku not in d:
+                    return False
+                if allowed is not None and d[ku] not in allowed:
+                    return False
+            return True
+        return pred, group_bys
+
+    @staticmethod
+    def _groups(spans, group_bys):
+        if not group_bys:
+            return [()], [0] * len(spans)
+        key_of = []
+        for sk, _ in spans:
+            d = dict(sk[1])
+            key_of.append(tuple(d.get(ku, -1) for ku in group_bys))
+        keys = sorted({k for k in key_of if -1 not in k})  # ByteMap order of the uid bytes
+        index = {k: i for i, k in enumerate(keys)}
+        return keys, [index.get(k, -1) for k in key_of]
+
+    def build_rollup_batch(self, name: str):
+        """The rollup scan of table `name` grouped like build_batch: (HostRollupBatch, keys)."""
+        from .rollup_read import make_rollup_batch
+        iv = self.rollups.config.intervals[name]
+        f = self._filters()
+        ds = self.downsampler
+        if f is None:
+            spans, need_count = [], False
+        else:
+            spans, need_count = self.rollups.scan_cells(name, self.metric, ds.function, self.aggregator, f[0])
+        keys, gids = self._groups(spans, f[1] if f else [])
+        return make_rollup_batch(spans, gids, iv, need_count, self.fix_duplicates), keys
+
     def build_batch(self):
         """findSpans + GroupByAndAggregateCB grouping (TsdbQuery.java:795-1049).
         Returns (HostBatch, group keys in emission order)."""
@@ -353,6 +426,21 @@ class TsdbQuery:
 
     def run(self):
         """TsdbQuery.run(): DataPoints[] of the query (one per SpanGroup)."""
+        rname = self.rollup_interval_name()
+        if rname is not None:
+            rb, keys = self.build_rollup_batch(rname)
+            q = self.to_abi()
+            runner = self.rollup_runner
+            if runner is None:
+                from .engine import default_engine
+                runner = default_engine().run_rollup_batch
+            if rb.cells.n_series == 0:
+                return []
+            out = []
+            for gid, ts, bits, isi in runner(rb, q):
+                key = keys[gid] if (self.aggregator != "none" and 0 <= gid < len(keys)) else ()
+                out.append(DataPoints(gid, ts, bits, isi, self.metric, key))
+            return out
         batch, keys = self.build_batch()
         q = self.to_abi()
         runner = self.runner

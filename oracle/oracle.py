@@ -65,6 +65,10 @@ def lib():
         L.ref_run_query_mt.argtypes = [C.POINTER(abi.Batch), C.POINTER(abi.Query), C.c_int,
                                        C.POINTER(C.POINTER(abi.Result))]
         L.ref_result_free.argtypes = [C.POINTER(abi.Result)]
+        L.ref_run_rollup_query.argtypes = [C.POINTER(abi.RollupBatch), C.POINTER(abi.Query),
+                                           C.POINTER(C.POINTER(abi.Result))]
+        L.ref_rollup_scan_bounds.argtypes = [C.POINTER(abi.Query), C.POINTER(abi.RollupInterval),
+                                             C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
         _lib = L
     return _lib
 
@@ -252,6 +256,26 @@ def parse_duration(s: str) -> int:
 def scan_bounds(q: abi.Query):
     s, e = C.c_int64(), C.c_int64()
     lib().ref_scan_bounds(C.byref(q), C.byref(s), C.byref(e))
+    return s.value, e.value
+
+
+def run_rollup_query(rb: abi.HostRollupBatch, q: abi.Query):
+    """TsdbQuery.run() with a RollupQuery (RollupSpans over rb) on the oracle."""
+    res = C.POINTER(abi.Result)()
+    rc = lib().ref_run_rollup_query(C.byref(rb.c), C.byref(q), C.byref(res))
+    if rc < 0:
+        _err(rc)
+    try:
+        return abi.result_to_groups(res.contents)
+    finally:
+        lib().ref_result_free(res)
+
+
+def rollup_scan_bounds(q: abi.Query, iv: abi.RollupInterval):
+    s, e = C.c_int64(), C.c_int64()
+    rc = lib().ref_rollup_scan_bounds(C.byref(q), C.byref(iv), C.byref(s), C.byref(e))
+    if rc < 0:
+        _err(rc)
     return s.value, e.value
 
 

@@ -116,8 +116,8 @@ static inline double dp_to_double(const ref_dp* d) {
   if (d->bad) jthrow(d->bad, "bad value at ts=%lld", (long long)d->ts);
   return d->is_int ? (double)d->lv : d->dv;
 }
-static inline ref_dp dp_of_long(int64_t ts, int64_t v) { ref_dp d = {ts, 1, 0, v, 0.0}; return d; }
-static inline ref_dp dp_of_double(int64_t ts, double v) { ref_dp d = {ts, 0, 0, 0, v}; return d; }
+static inline ref_dp dp_of_long(int64_t ts, int64_t v) { ref_dp d = {ts, 1, 0, v, 0.0, 1, 0, 0}; return d; }
+static inline ref_dp dp_of_double(int64_t ts, double v) { ref_dp d = {ts, 0, 0, 0, v, 1, 0, 0}; return d; }
 /* MutableDataPoint.reset(DataPoint) reads the value eagerly (src/core/MutableDataPoint.java) */
 static inline ref_dp dp_copy_eager(const ref_dp* d) {
   if (d->is_int) return dp_of_long(d->ts, dp_long(d));
@@ -856,6 +856,310 @@ static void span_first_last(span_view* s, int64_t* first, int64_t* last, int64_t
 }
 
 /* ======================================================================== */
+/* RollupSpan + RollupSeq (src/rollup/RollupSpan.java, src/rollup/RollupSeq.java) */
+/* ======================================================================== */
+/* A RollupSeq row: the queried aggregate's cells and (need_count) the count cells, each a
+ * 2-byte rollup qualifier (offset << 4 | flags) and its value bytes. */
+typedef struct { uint32_t q; const uint8_t* v; } ro_cell;
+typedef struct {
+  int64_t base;
+  ro_cell* vc;
+  int64_t nv, capv;
+  ro_cell* cc;
+  int64_t nc, capc;
+  int64_t last_off, last_coff;   /* RollupSeq.last_offset / last_count_offset */
+} ro_row;
+
+static inline int64_t ro_off(uint32_t q) { return (int64_t)((q & 0xFFFF) >> 4); }
+static int64_t cal_fdiv(int64_t a, int64_t b);
+static int64_t days_from_civil(int64_t y, int m, int d);
+static void civil_from_days(int64_t z, int64_t* y, int* m, int* d);
+
+/* RollupSeq.append :238-318.  The batch carries no HBase write timestamps: a repeated offset
+ * under fix_duplicates takes the "equal timestamps" branch (the later cell replaces the
+ * earlier one, :257-266 / :290-299). */
+static void ro_append(ro_row* r, uint32_t q, const uint8_t* v, int is_count, int fix_dup) {
+  const int64_t off = ro_off(q);
+  int64_t* last = is_count ? &r->last_coff : &r->last_off;
+  if (*last > -1 && off <= *last) {
+    if (off == *last && fix_dup) {
+      if (is_count) r->nc--; else r->nv--;
+    } else if (is_count) {
+      jthrow(TSDB_E_ILLEGAL_ARGUMENT, "The count offset of %lld is <= the last offset %lld", (long long)off, (long long)*last);
+    } else {
+      jthrow(TSDB_E_ILLEGAL_DATA, "The offset of %lld is <= the last offset %lld", (long long)off, (long long)*last);
+    }
+  }
+  *last = off;
+  ro_cell** a = is_count ? &r->cc : &r->vc;
+  int64_t* n = is_count ? &r->nc : &r->nv;
+  int64_t* cap = is_count ? &r->capc : &r->capv;
+  if (*n == *cap) {
+    *cap = *cap ? *cap * 2 : 16;
+    *a = (ro_cell*)realloc(*a, (size_t)*cap * sizeof(ro_cell));
+    if (!*a) jthrow(TSDB_E_NOMEM, "oom");
+  }
+  (*a)[*n].q = q;
+  (*a)[*n].v = v;
+  (*n)++;
+}
+
+/* the cells of batch row r (2-byte qualifiers, values back to back) appended to `row` */
+static void ro_append_cells(ro_row* row, const uint64_t* qoff, const uint64_t* voff, const uint8_t* qual,
+                            const uint8_t* val, int64_t r, int is_count, int fix_dup) {
+  const int64_t ql = (int64_t)(qoff[r + 1] - qoff[r]), vl = (int64_t)(voff[r + 1] - voff[r]);
+  if (ql % 2) jthrow(TSDB_E_ILLEGAL_DATA, "rollup qualifiers are 2 bytes");
+  int64_t vi = 0;
+  for (int64_t i = 0; i < ql; i += 2) {
+    const uint32_t q = be16(qual + qoff[r] + i);
+    const int64_t len = (q & 7) + 1;   /* Internal.getValueLengthFromQualifier */
+    if (vi + len > vl) jthrow(TSDB_E_ILLEGAL_DATA, "rollup value bytes shorter than the qualifiers say");
+    ro_append(row, q, val + voff[r] + vi, is_count, fix_dup);
+    vi += len;
+  }
+  if (vi != vl) jthrow(TSDB_E_ILLEGAL_DATA, "rollup value bytes longer than the qualifiers say");
+}
+
+typedef struct {
+  ref_view base;
+  ro_row* rows;
+  int64_t nrows;
+  int need_count;
+  int64_t interval_ms;
+  int64_t row_index;
+  int64_t qi, ci;   /* RollupIterator.qual_index / count_qual_index, in cells */
+} ro_span;
+
+/* RollupIterator.sync :521-555 */
+static void ro_sync(const ro_row* r, int64_t* qi, int64_t* ci) {
+  while (*qi < r->nv && *ci < r->nc) {
+    const int64_t a = ro_off(r->vc[*qi].q), b = ro_off(r->cc[*ci].q);
+    if (a == b) return;
+    if (a > b) (*ci)++;
+    else (*qi)++;
+  }
+}
+/* RollupIterator.hasNext :512-519 */
+static int ro_row_has(const ro_row* r, int need_count, int64_t* qi, int64_t* ci) {
+  if (!need_count) return *qi < r->nv;
+  ro_sync(r, qi, ci);
+  return *qi < r->nv && *ci < r->nc;
+}
+static inline int64_t ro_ts(const ro_span* s, const ro_row* r, uint32_t q) {  /* getTimestampFromRollupQualifier :193-197 */
+  return r->base * 1000 + ro_off(q) * s->interval_ms;
+}
+/* RollupIterator.next :557-572 and the DataPoint accessors :641-700 */
+static ref_dp ro_row_next(ro_span* s, const ro_row* r) {
+  if (!ro_row_has(r, s->need_count, &s->qi, &s->ci)) jthrow(TSDB_E_NO_SUCH_ELEMENT, "no more elements");
+  const ro_cell* c = &r->vc[s->qi++];
+  ref_dp d;
+  memset(&d, 0, sizeof d);
+  d.ts = ro_ts(s, r, c->q);
+  d.is_int = (c->q & 0x8) == 0;
+  const uint8_t* p = c->v;
+  if (d.is_int) {   /* Internal.extractIntegerValue */
+    switch (c->q & 7) {
+      case 7: d.lv = (int64_t)be64(p); break;
+      case 3: d.lv = (int32_t)be32(p); break;
+      case 1: d.lv = (int16_t)be16(p); break;
+      case 0: d.lv = (int8_t)p[0]; break;
+      default: d.bad = TSDB_E_ILLEGAL_DATA;
+    }
+  } else {          /* Internal.extractFloatingPointValue */
+    switch (c->q & 7) {
+      case 7: d.dv = bitsd(be64(p)); break;
+      case 3: { uint32_t u = be32(p); float f; memcpy(&f, &u, 4); d.dv = (double)f; break; }
+      default: d.bad = TSDB_E_ILLEGAL_DATA;
+    }
+  }
+  d.cnt = 1;   /* valueCount() without count cells */
+  if (s->need_count) {
+    const ro_cell* k = &r->cc[s->ci++];
+    const uint8_t* kp = k->v;
+    if ((k->q & 0x8) == 0) {
+      switch (k->q & 7) {
+        case 7: d.cnt = (int64_t)be64(kp); break;
+        case 3: d.cnt = (int32_t)be32(kp); break;
+        case 1: d.cnt = (int16_t)be16(kp); break;
+        case 0: d.cnt = (int8_t)kp[0]; break;
+        default: d.cnt_bad = TSDB_E_ILLEGAL_DATA;
+      }
+    } else {        /* (long) of the float count */
+      double x;
+      switch (k->q & 7) {
+        case 7: x = bitsd(be64(kp)); break;
+        case 3: { uint32_t u = be32(kp); float f; memcpy(&f, &u, 4); x = (double)f; break; }
+        default: x = 0; d.cnt_bad = TSDB_E_ILLEGAL_DATA;
+      }
+      /* Java's (long) of a double: NaN -> 0, saturating */
+      d.cnt = x != x ? 0 : (x >= 9.2233720368547758e18 ? INT64_MAX : (x <= -9.2233720368547758e18 ? INT64_MIN : (int64_t)x));
+    }
+  }
+  return d;
+}
+/* RollupIterator.seek :578-609: reset, then walk the value cells with the count cells in
+ * lock step (not re-synced during the walk) */
+static void ro_row_seek(ro_span* s, const ro_row* r, int64_t ts) {
+  if ((ts & (int64_t)0xFFFFFFFF00000000LL) == 0) ts *= 1000;
+  s->qi = s->ci = 0;
+  if (!ro_row_has(r, s->need_count, &s->qi, &s->ci)) return;
+  while (s->qi < r->nv && ro_ts(s, r, r->vc[s->qi].q) < ts) {
+    s->qi++;
+    if (s->need_count) s->ci++;
+  }
+}
+/* RollupSeq.size() / timestamp(size - 1) (:420-470): datapoints a fresh iterator yields */
+static int64_t ro_row_size(const ro_span* s, const ro_row* r, int64_t* last_ts, int64_t* first_ts) {
+  int64_t qi = 0, ci = 0, n = 0;
+  while (ro_row_has(r, s->need_count, &qi, &ci)) {
+    const int64_t t = ro_ts(s, r, r->vc[qi].q);
+    if (n == 0 && first_ts) *first_ts = t;
+    if (last_ts) *last_ts = t;
+    qi++;
+    if (s->need_count) ci++;
+    n++;
+  }
+  return n;
+}
+static void ro_new_row_it(ro_span* s) {   /* RollupIterator() :507-510 */
+  s->qi = s->ci = 0;
+  if (s->need_count && s->nrows) ro_sync(&s->rows[s->row_index], &s->qi, &s->ci);
+}
+static int ros_has_next(ref_view* v) {  /* Span.Iterator.hasNext :421-435 */
+  ro_span* s = (ro_span*)v;
+  if (s->nrows == 0) return 0;
+  if (ro_row_has(&s->rows[s->row_index], s->need_count, &s->qi, &s->ci)) return 1;
+  while (s->row_index < s->nrows - 1) {
+    s->row_index++;
+    ro_new_row_it(s);
+    if (ro_row_has(&s->rows[s->row_index], s->need_count, &s->qi, &s->ci)) return 1;
+  }
+  return 0;
+}
+static ref_dp ros_next(ref_view* v) {  /* :438-452 */
+  ro_span* s = (ro_span*)v;
+  if (s->nrows && ro_row_has(&s->rows[s->row_index], s->need_count, &s->qi, &s->ci))
+    return ro_row_next(s, &s->rows[s->row_index]);
+  while (s->row_index < s->nrows - 1) {
+    s->row_index++;
+    ro_new_row_it(s);
+    if (ro_row_has(&s->rows[s->row_index], s->need_count, &s->qi, &s->ci)) return ro_row_next(s, &s->rows[s->row_index]);
+  }
+  jthrow(TSDB_E_NO_SUCH_ELEMENT, "no more elements");
+}
+static void ros_seek(ref_view* v, int64_t ts) {  /* :464-471 with seekRow :360-380 */
+  ro_span* s = (ro_span*)v;
+  if (s->nrows == 0) return;
+  int64_t ri = 0;
+  for (int64_t i = 0; i < s->nrows; i++) {
+    int64_t last = 0;
+    const int64_t sz = ro_row_size(s, &s->rows[i], &last, NULL);
+    if (sz < 1) ri++;
+    else if (last < ts) ri++;
+    else break;
+  }
+  if (ri == s->nrows) --ri;
+  if (ri != s->row_index) {
+    s->row_index = ri;
+    ro_new_row_it(s);
+  }
+  ro_row_seek(s, &s->rows[s->row_index], ts);
+}
+static void ro_rows_free(ro_row* rows, int64_t n) {
+  for (int64_t i = 0; i < n; i++) { free(rows[i].vc); free(rows[i].cc); }
+  free(rows);
+}
+static void ros_destroy(ref_view* v) {
+  ro_span* s = (ro_span*)v;
+  ro_rows_free(s->rows, s->nrows);
+  free(s);
+}
+static const view_vt ROLLUP_SPAN_VT = {ros_has_next, ros_next, ros_seek, ros_destroy};
+
+/* RollupSpan.addRow :62-80 over the span's rows in scan order (a row with the last row's key
+ * appends its cells to that RollupSeq, RollupSeq.addRow :170-205), then Span.checkRowOrder's
+ * stable sort by base time.  Throws as RollupSeq.append does. */
+static ref_view* make_rollup_span(const tsdbhip_rollup_batch* rb, const int64_t* row_ids, int64_t n_rows) {
+  const tsdbhip_batch* b = &rb->cells;
+  ro_span* s = (ro_span*)xcalloc(1, sizeof(ro_span));
+  s->base.vt = &ROLLUP_SPAN_VT;
+  s->need_count = rb->row_cqual_off != NULL;
+  s->interval_ms = (int64_t)rb->interval.interval_s * 1000;
+  s->rows = (ro_row*)xcalloc((size_t)(n_rows ? n_rows : 1), sizeof(ro_row));
+  volatile int err = 0;
+  TRY {
+    for (int64_t i = 0; i < n_rows; i++) {
+      const int64_t r = row_ids[i];
+      ro_row* row;
+      if (s->nrows > 0 && s->rows[s->nrows - 1].base == (int64_t)b->row_base_time[r]) {
+        row = &s->rows[s->nrows - 1];
+      } else {
+        row = &s->rows[s->nrows++];
+        row->base = b->row_base_time[r];
+        row->last_off = row->last_coff = -1;
+      }
+      ro_append_cells(row, b->row_qual_off, b->row_val_off, b->qual, b->val, r, 0, rb->fix_duplicates);
+      if (s->need_count) ro_append_cells(row, rb->row_cqual_off, rb->row_cval_off, rb->cqual, rb->cval, r, 1, rb->fix_duplicates);
+    }
+  } CATCH(e) { err = e; } END_TRY
+  if (err) {
+    ro_rows_free(s->rows, s->nrows);
+    free(s);
+    jthrow(err, "%s", g_msg);
+  }
+  for (int64_t i = 1; i < s->nrows; i++) {   /* stable insertion sort by base */
+    ro_row t = s->rows[i];
+    int64_t j = i - 1;
+    while (j >= 0 && s->rows[j].base > t.base) { s->rows[j + 1] = s->rows[j]; j--; }
+    s->rows[j + 1] = t;
+  }
+  s->row_index = 0;
+  ro_new_row_it(s);
+  return &s->base;
+}
+
+/* Span.size() / timestamp(0) / timestamp(size - 1) of a rollup span */
+static void rollup_span_first_last(ro_span* s, int64_t* first, int64_t* last, int64_t* size) {
+  int64_t total = 0, f = 0, l = 0;
+  for (int64_t i = 0; i < s->nrows; i++) {
+    int64_t fi = 0, li = 0;
+    const int64_t n = ro_row_size(s, &s->rows[i], &li, &fi);
+    if (n == 0) continue;
+    if (total == 0) f = fi;
+    l = li;
+    total += n;
+  }
+  *size = total;
+  *first = f;
+  *last = l;
+}
+
+/* RollupUtils.getRollupBasetime :52-112 (int result) */
+static int64_t ro_basetime(int64_t ts, const tsdbhip_rollup_interval* iv) {
+  if (ts < 0) jthrow(TSDB_E_ILLEGAL_ARGUMENT, "Not supporting negative timestamps at this time: %lld", (long long)ts);
+  if (iv->units == 'h') {
+    const int64_t modulo = iv->unit_multiplier > 1 ? (int64_t)iv->unit_multiplier * 3600 : 3600;
+    const int64_t t = (ts & (int64_t)0xFFFFFFFF00000000LL) ? ts / 1000 : ts;
+    return (int32_t)(uint32_t)(t - t % modulo);
+  }
+  const int64_t ms = (ts & (int64_t)0xFFFFFFFF00000000LL) ? ts : ts * 1000;
+  const int64_t day = cal_fdiv(ms, 86400000LL);
+  const int64_t msod = ms - day * 86400000LL;
+  int64_t y;
+  int m, d;
+  civil_from_days(day, &y, &m, &d);
+  int64_t z;
+  switch (iv->units) {
+    case 'd': z = day; break;
+    case 'n': z = days_from_civil(y, m, 1); break;
+    case 'y': z = days_from_civil(y, 1, 1); break;
+    default: jthrow(TSDB_E_ILLEGAL_ARGUMENT, "Unrecogznied span");
+  }
+  /* HOUR_OF_DAY / MINUTE / SECOND zeroed, the milliseconds kept, then / 1000 */
+  return (int32_t)(uint32_t)((z * 86400000LL + msod % 1000) / 1000);
+}
+
+/* ======================================================================== */
 /* UTC calendar (java.util.GregorianCalendar in the UTC zone, default US locale: weeks   */
 /* start on Sunday) -- the arithmetic DateTime.previousInterval and the calendar          */
 /* Downsampler / FillingDownsampler use (src/utils/DateTime.java:445-606,                 */
@@ -1054,6 +1358,7 @@ typedef struct {
   int cal;
   int64_t cal_n;
   const tsdbhip_tz* tz;   /* DownsamplingSpecification.getTimezone (NULL = UTC) */
+  int32_t rollup_agg;     /* RollupQuery.getRollupAgg (-1: not a rollup query) */
   int64_t prev_cal, next_cal;
   int64_t fprev_cal, fnext_cal;
 } ds_view;
@@ -1145,6 +1450,60 @@ static double viv_nd(void* c) {  /* :474-482 */
 }
 static int64_t viv_nl(void* c) { (void)c; jthrow(TSDB_E_CLASS_CAST, "ValuesInInterval is Doubles only"); }
 
+/* Downsampler.next :165-221 / FillingDownsampler.next :196-253: the bucket value, with the
+ * rollup branches -- avg rollups: avg downsampling is Σsum / Σcount (0 when the count is 0),
+ * any other function runs on each point's sum / count; count downsampling of a rollup sums
+ * valueCount() (consuming the values) */
+static int64_t ds_value_count(ds_view* d) {   /* ValuesInInterval.nextValueCount :484-493 */
+  if (!viv_has(d)) jthrow(TSDB_E_NO_SUCH_ELEMENT, "no more values in interval");
+  if (d->next_dp.cnt_bad) jthrow(d->next_dp.cnt_bad, "bad count value");
+  return d->next_dp.cnt;
+}
+static double ds_bucket_value(ds_view* d, vals_t* vv) {
+  if (d->rollup_agg == TSDB_AGG_AVG) {
+    if (d->fn == TSDB_AGG_AVG) {
+      double sum = 0;
+      int64_t count = 0;
+      while (viv_has(d)) {
+        count += ds_value_count(d);
+        sum += viv_nd(d);
+      }
+      return count == 0 ? 0.0 : sum / (double)count;
+    }
+    double* acc = NULL;
+    int64_t n = 0, cap = 0;
+    while (viv_has(d)) {
+      const int64_t count = ds_value_count(d);
+      const double sum = viv_nd(d);
+      if (n == cap) {
+        cap = cap ? cap * 2 : 64;
+        acc = (double*)realloc(acc, (size_t)cap * 8);
+        if (!acc) jthrow(TSDB_E_NOMEM, "oom");
+      }
+      acc[n++] = count == 0 ? 0.0 : sum / (double)count;
+    }
+    arr_vals a = {NULL, acc, n, 0};
+    vals_t av = {av_has, av_nl, av_nd, &a};
+    volatile double r = 0;
+    volatile int err = 0;
+    TRY { r = agg_run_double(d->fn, &av); } CATCH(e) { err = e; } END_TRY
+    free(acc);
+    if (err) jthrow(err, "%s", g_msg);
+    return r;
+  }
+  if (d->rollup_agg == TSDB_AGG_DEV)
+    jthrow(TSDB_E_UNSUPPORTED, "Standard deviation over rolled up data is not supported at this time");
+  if (d->rollup_agg >= 0 && d->fn == TSDB_AGG_COUNT) {
+    double count = 0;
+    while (viv_has(d)) {
+      count += (double)ds_value_count(d);
+      viv_nd(d);
+    }
+    return count;
+  }
+  return agg_run_double(d->fn, vv);
+}
+
 static int ds_has_next(ref_view* v) {
   ds_view* d = (ds_view*)v;
   if (!d->filling) return viv_has(d);                 /* Downsampler.hasNext :155-157 */
@@ -1157,7 +1516,7 @@ static ref_dp ds_next(ref_view* v) {
   vals_t vv = {viv_has, viv_nl, viv_nd, d};
   if (!d->filling) {  /* Downsampler.next :163-231 (rollup branches not reachable) */
     if (!viv_has(d)) jthrow(TSDB_E_NO_SUCH_ELEMENT, "no more data points");
-    d->value = agg_run_double(d->fn, &vv);
+    d->value = ds_bucket_value(d, &vv);
     d->timestamp = viv_interval_ts(d);
     viv_move_to_next_interval(d);
     return dp_of_double(d->run_all ? d->qs : d->timestamp, d->value);
@@ -1172,7 +1531,7 @@ static ref_dp ds_next(ref_view* v) {
     actual = viv_interval_ts(d);
   }
   if (d->run_all || actual == d->timestamp) {
-    d->value = agg_run_double(d->fn, &vv);
+    d->value = ds_bucket_value(d, &vv);
     viv_move_to_next_interval(d);
   } else {
     switch (d->fill) {
@@ -1206,6 +1565,7 @@ static ref_view* make_downsampler(ref_view* src, int32_t function, int64_t inter
   d->src = src;
   d->fn = function;
   d->tz = tz;
+  d->rollup_agg = -1;
   d->interval = interval_ms;
   d->fill = fill;
   d->run_all = run_all;
@@ -1744,7 +2104,13 @@ typedef struct {
   const tsdbhip_query* q;
   span_desc* spans;
   int64_t scan_start_ms, scan_end_ms;
+  const tsdbhip_rollup_batch* rb;   /* rollup query: RollupSpans over these cells */
 } query_env;
+
+/* RollupQuery ctor :69-80: zimsum / mimmax / mimmin read the sum / max / min columns */
+static int32_t rollup_agg_of(int32_t f) {
+  return f == TSDB_AGG_ZIMSUM ? TSDB_AGG_SUM : f == TSDB_AGG_MIMMAX ? TSDB_AGG_MAX : f == TSDB_AGG_MIMMIN ? TSDB_AGG_MIN : f;
+}
 
 /* SpanGroup.iterator() :527 -> AggregationIterator.create :351-380 -> drain */
 static void run_group(const query_env* env, group_job* g) {
@@ -1756,15 +2122,22 @@ static void run_group(const query_env* env, group_job* g) {
   TRY {
     for (int64_t i = 0; i < g->nspans; i++) {
       span_desc* sd = &env->spans[g->spans[i]];
-      ref_view* it = make_span(sd->nrows, b->row_base_time, b->row_qual_off, b->row_val_off, b->qual, b->val, sd->row_ids);
-      /* SpanGroup.add :324-339: admit only spans overlapping [start, end] */
+      ref_view* it;
       int64_t first = 0, last = 0, size = 0;
-      span_first_last((span_view*)it, &first, &last, &size);
+      if (env->rb) {
+        it = make_rollup_span(env->rb, sd->row_ids, sd->nrows);
+        rollup_span_first_last((ro_span*)it, &first, &last, &size);
+      } else {
+        it = make_span(sd->nrows, b->row_base_time, b->row_qual_off, b->row_val_off, b->qual, b->val, sd->row_ids);
+        span_first_last((span_view*)it, &first, &last, &size);
+      }
+      /* SpanGroup.add :324-339: admit only spans overlapping [start, end] */
       if (size == 0 || !(first <= env->scan_end_ms && last >= env->scan_start_ms)) { ref_view_free(it); continue; }
       if (has_downsampler(q)) {
         it = make_downsampler(it, q->ds_function, q->ds_interval_ms, q->ds_fill, q->ds_all,
                               env->scan_start_ms, env->scan_end_ms, q->start_time, q->end_time, q->ds_calendar,
                               q->ds_tz);
+        if (env->rb) ((ds_view*)it)->rollup_agg = rollup_agg_of(q->ds_function);   /* Span.downsampler's rollup_query */
       }
       if (q->rate) it = ref_view_rate(it, q->rate_counter, q->rate_counter_max, q->rate_reset_value, q->rate_drop_resets);
       its[k++] = it;
@@ -1807,20 +2180,48 @@ static void* pool_worker(void* arg) {
   return NULL;
 }
 
-static int run_query_impl(const tsdbhip_batch* b, const tsdbhip_query* q, int nthreads, ref_result** out) {
+/* TsdbQuery.getScanStartTimeSeconds :1515-1526 / getScanEndTimeSeconds :1562-1567 with a
+ * rollup query */
+static void rollup_scan_bounds(const tsdbhip_query* q, const tsdbhip_rollup_interval* iv, int64_t* s_out, int64_t* e_out) {
+  int64_t start = q->start_time;
+  if ((start & (int64_t)0xFFFFFFFF00000000LL) != 0) start /= 1000;
+  int64_t base = ro_basetime(start, iv);
+  if (q->rate) base = ro_basetime(base - 1, iv);   /* one row back for the first rate */
+  *s_out = base;
+  int64_t end = q->end_time;
+  if ((end & (int64_t)0xFFFFFFFF00000000LL) != 0) {
+    end /= 1000;
+    if (end - (end * 1000) < 1) end++;
+  }
+  *e_out = ro_basetime(end + (int64_t)iv->interval_s * iv->intervals, iv);
+}
+
+static int run_query_impl(const tsdbhip_batch* b, const tsdbhip_query* q0, int nthreads, ref_result** out,
+                          const tsdbhip_rollup_batch* rb) {
   volatile int rc = 0;
   span_desc* volatile spans = NULL;
   group_job* volatile jobs = NULL;
   volatile int64_t njobs = 0, nspans = 0;
   *out = NULL;
+  tsdbhip_query qr = *q0;
+  const tsdbhip_query* q = &qr;
   TRY {
     if (has_downsampler(q)) {
       if (q->ds_function == TSDB_AGG_NONE) jthrow(TSDB_E_ILLEGAL_ARGUMENT, "cannot use the NONE aggregator for downsampling");
     }
     int64_t ss, se;
-    ref_scan_bounds(q, &ss, &se);
+    if (rb) {
+      /* TsdbQuery.transformDownSamplerToRollupQuery :1665-1700: a rollup query exists only
+       * with a downsampler; a count group-by sums the rolled-up counts */
+      if (!has_downsampler(q) || (!q->ds_all && q->ds_interval_ms <= 0))
+        jthrow(TSDB_E_ILLEGAL_ARGUMENT, "a rollup query needs a downsampling interval");
+      if (qr.aggregator == TSDB_AGG_COUNT) qr.aggregator = TSDB_AGG_SUM;
+      rollup_scan_bounds(q, &rb->interval, &ss, &se);
+    } else {
+      ref_scan_bounds(q, &ss, &se);
+    }
     /* SpanGroup ctor :270-273: seconds -> ms */
-    query_env env = {b, q, NULL, ss * 1000, se * 1000};
+    query_env env = {b, q, NULL, ss * 1000, se * 1000, rb};
     /* findSpans: rows with base_time in [scan_start, scan_end) (QueryUtil.getMetricScanner) */
     spans = (span_desc*)xcalloc((size_t)(b->n_series ? b->n_series : 1), sizeof(span_desc));
     for (int64_t s = 0; s < b->n_series; s++) {
@@ -1835,6 +2236,10 @@ static int run_query_impl(const tsdbhip_batch* b, const tsdbhip_query* q, int nt
       for (int64_t r = r0; r < r1; r++)
         if ((int64_t)b->row_base_time[r] >= ss && (int64_t)b->row_base_time[r] < se) sd->row_ids[sd->nrows++] = r;
       sd->group = b->group_id ? b->group_id[s] : 0;
+      if (rb) {   /* the scan builds every RollupSeq: RollupSeq.append throws here, in scan order */
+        ref_view* t = make_rollup_span(rb, sd->row_ids, sd->nrows);
+        ref_view_free(t);
+      }
     }
     env.spans = spans;
     if (q->aggregator == TSDB_AGG_NONE) {  /* TsdbQuery.java:941-962: one SpanGroup per span */
@@ -1915,10 +2320,19 @@ static int run_query_impl(const tsdbhip_batch* b, const tsdbhip_query* q, int nt
 }
 
 int ref_run_query(const tsdbhip_batch* b, const tsdbhip_query* q, ref_result** out) {
-  return run_query_impl(b, q, 1, out);
+  return run_query_impl(b, q, 1, out, NULL);
 }
 int ref_run_query_mt(const tsdbhip_batch* b, const tsdbhip_query* q, int nthreads, ref_result** out) {
-  return run_query_impl(b, q, nthreads, out);
+  return run_query_impl(b, q, nthreads, out, NULL);
+}
+int ref_run_rollup_query(const tsdbhip_rollup_batch* rb, const tsdbhip_query* q, ref_result** out) {
+  if (!rb || !q || !out) return TSDB_E_ILLEGAL_ARGUMENT;
+  return run_query_impl(&rb->cells, q, 1, out, rb);
+}
+int ref_rollup_scan_bounds(const tsdbhip_query* q, const tsdbhip_rollup_interval* iv, int64_t* s_out, int64_t* e_out) {
+  volatile int rc = 0;
+  TRY { rollup_scan_bounds(q, iv, s_out, e_out); } CATCH(e) { rc = e; } END_TRY
+  return rc;
 }
 void ref_result_free(ref_result* r) {
   if (!r) return;

@@ -31,6 +31,9 @@ typedef struct {
   int32_t bad;        /* nonzero: reading the value throws this TSDB_E_* code (lazy Java semantics) */
   int64_t lv;         /* longValue() when is_int */
   double dv;          /* doubleValue() when !is_int */
+  int64_t cnt;        /* RollupSeq valueCount() (rollup spans; 1 without count cells) */
+  int32_t cnt_bad;    /* nonzero: valueCount() throws this TSDB_E_* code */
+  int32_t pad_;
 } ref_dp;
 
 const char* ref_last_error(void);
@@ -83,6 +86,10 @@ int ref_run_query(const tsdbhip_batch* b, const tsdbhip_query* q, ref_result** o
 /* Same, but groups processed by nthreads std threads (CPU baseline "parallel over groups"). */
 int ref_run_query_mt(const tsdbhip_batch* b, const tsdbhip_query* q, int nthreads, ref_result** out);
 void ref_result_free(ref_result* r);
+/* TsdbQuery.run over a rollup table (RollupSpan / RollupSeq spans, the Downsampler's rollup
+ * branches, rollup scan bounds); layout as tsdbhip_load_rollup. */
+int ref_run_rollup_query(const tsdbhip_rollup_batch* rb, const tsdbhip_query* q, ref_result** out);
+int ref_rollup_scan_bounds(const tsdbhip_query* q, const tsdbhip_rollup_interval* iv, int64_t* s_out, int64_t* e_out);
 
 #ifdef __cplusplus
 }

@@ -93,3 +93,51 @@ def groups_as_points(dps_list):
             pts.append((dp.timestamp(), dp.isInteger(), dp.longValue() if dp.isInteger() else dp.doubleValue()))
         out.append(pts)
     return out
+
+
+def rollup_stores(doc, case):
+    """MockStore + RollupStore holding a rollup_queries.json case's writes."""
+    from opentsdb_amd.rollup_read import RollupConfig, RollupStore
+    raw = MockStore()
+    rs = RollupStore(RollupConfig(doc["agg_ids"], doc["intervals"]), raw)
+    for w in case["writes"]:
+        if w[0] == "raw":
+            _, metric, tags, ts, kind, value = w
+            if kind == "long":
+                raw.add_long(metric, ts, value, tags)
+            else:
+                raw.add_float(metric, ts, value, tags)
+        elif w[0] == "agg":
+            _, metric, tags, ts, kind, value, interval, agg = w
+            rs.add_aggregate_point(metric, ts, value, tags, interval, agg, kind)
+        else:
+            _, interval, metric, tags, base, qual, value = w
+            rs.add_column(interval, metric, tags, base, bytes.fromhex(qual), bytes.fromhex(value))
+    return raw, rs
+
+
+def rollup_query(doc, case, runner, rollup_runner):
+    raw, rs = rollup_stores(doc, case)
+    c = case["query"]
+    q = TsdbQuery(raw, runner=runner, rollups=rs, rollup_runner=rollup_runner,
+                  fix_duplicates=case.get("fix_duplicates", False))
+    q.setStartTime(c["start"])
+    q.setEndTime(c["end"])
+    q.setTimeSeries(c["metric"], c["tags"], c["aggregator"], c["rate"])
+    q.downsample(c["ds"])
+    return q
+
+
+def check_rollup_expect(case, dps):
+    """dps: DataPoints[] of the query; the case's stated answer."""
+    exp = case["expect"]
+    if "first" in exp:
+        dp = next(iter(dps[0]))
+        assert dp.timestamp() == exp["first"][0]
+        assert abs(dp.toDouble() - exp["first"][1]) <= 1e-4
+        return
+    groups = exp["groups"]
+    assert len(dps) == len(groups), f"{case['name']}: {len(dps)} groups, expected {len(groups)}"
+    for d, pts in zip(dps, groups):
+        got = [(dp.timestamp(), dp.isInteger(), dp.toDouble()) for dp in d]
+        assert_points(got, [[t, 0, v] for t, v in pts], case["tol"], ctx=case["name"])

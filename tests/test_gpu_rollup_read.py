@@ -1,0 +1,216 @@
+"""GPU parity of the rollup read path: tsdbhip_load_rollup + run
+(engine.cpp run_rollup: the RollupSeq restatement on the host, the value / count series on
+the device, k_rollup_combine for avg and count downsampling of rollups).
+
+  * every known answer of test/core/TestTsdbQueryRollup.java (tests/golden/rollup_queries.json)
+    through the engine, and against the oracle on the same inputs;
+  * the RollupSeq corner cases (sync, duplicates, zero counts, exceptions);
+  * randomized multi-series rollup tables with missing sum / count cells against the oracle:
+    aggregators, downsampling functions and intervals, fills, rate, NONE."""
+from __future__ import annotations
+
+import ctypes as C
+import struct
+
+import numpy as np
+import pytest
+
+from opentsdb_amd import abi, engine
+from opentsdb_amd.engine import EngineError
+from opentsdb_amd.rollup_read import make_rollup_batch
+from oracle import oracle as O
+from tests import golden_util as gu
+from tests.test_gpu_parity import assert_groups_match
+
+pytestmark = pytest.mark.gpu
+
+DOC = gu.load("rollup_queries.json")
+CASES = [c for c in DOC["cases"] if "write_error" not in c["expect"]]
+B = 1356998400
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from opentsdb_amd.engine import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_known_answers_on_gpu(eng, case):
+    q = gu.rollup_query(DOC, case, eng.run_batch, eng.run_rollup_batch)
+    if "error" in case["expect"]:
+        with pytest.raises(EngineError) as e:
+            q.run()
+        assert e.value.java == case["expect"]["error"]
+        return
+    gu.check_rollup_expect(case, q.run())
+    # the same inputs through the oracle, bit for bit
+    name = q.rollup_interval_name()
+    if name is None:
+        return
+    rb, _ = q.build_rollup_batch(name)
+    if rb.cells.n_series:
+        assert_groups_match(eng.run_rollup_batch(rb, q.to_abi()), O.run_rollup_query(rb, q.to_abi()),
+                            q.aggregator, tol=0.0, ctx=case["name"])
+
+
+def _iv(interval="10m", span="6h"):
+    return engine.rollup_interval(interval, span)
+
+
+def _batch(rows, counts=True, fix=False, groups=None, iv=None):
+    spans = []
+    for s in rows:
+        rr = []
+        for base, vals, cnts in s:
+            rr.append((base, [(struct.pack(">H", (o << 4) | f), v) for o, f, v in vals],
+                       [(struct.pack(">H", (o << 4) | f), v) for o, f, v in cnts]))
+        spans.append((None, rr))
+    return make_rollup_batch(spans, groups if groups is not None else [0] * len(spans), iv or _iv(), counts, fix)
+
+
+def _l(v):
+    return (0x7, struct.pack(">q", v))
+
+
+def _q(ds="10m-avg", agg="avg", start=B, end=B + 43200, rate=False):
+    q = abi.new_query(start, end, agg, rate=rate)
+    assert O.lib().ref_parse_downsample(ds.encode(), C.byref(q)) == 0
+    return q
+
+
+def both(eng, rb, q):
+    return eng.run_rollup_batch(rb, q), O.run_rollup_query(rb, q)
+
+
+def test_sync_count_zero(eng):
+    rb = _batch([[(B, [(0, *_l(20)), (1, *_l(40)), (3, *_l(60)), (4, *_l(9))],
+                   [(0, *_l(2)), (2, *_l(9)), (3, *_l(3)), (4, *_l(0))])]])
+    for ds in ("10m-avg", "20m-avg", "10m-count", "30m-count", "10m-sum", "10m-max", "1h-avg-zero"):
+        g, w = both(eng, rb, _q(ds))
+        assert_groups_match(g, w, "avg", tol=0.0, ctx=ds)
+
+
+def test_errors_match_oracle(eng):
+    cases = [
+        (_batch([[(B, [(2, *_l(1)), (1, *_l(2))], [])]], counts=False), _q("10m-sum", "sum")),
+        (_batch([[(B, [(1, *_l(1)), (2, *_l(2))], [(2, *_l(1)), (1, *_l(2))])]]), _q()),
+        (_batch([[(B, [(0, *_l(20))], [(0, *_l(2))])]]), _q("10m-dev", "avg")),
+    ]
+    for rb, q in cases:
+        with pytest.raises(O.OracleError) as eo:
+            O.run_rollup_query(rb, q)
+        with pytest.raises(EngineError) as ee:
+            eng.run_rollup_batch(rb, q)
+        assert ee.value.code == eo.value.code
+    # a bad row outside the scan range is never scanned
+    rb = _batch([[(B, [(0, *_l(1))], []), (B + 86400 * 3, [(2, *_l(1)), (1, *_l(2))], [])]], counts=False)
+    g, w = both(eng, rb, _q("10m-sum", "sum"))
+    assert_groups_match(g, w, "sum", tol=0.0)
+
+
+def test_duplicates_fixed(eng):
+    rb = _batch([[(B, [(1, *_l(1)), (1, 0xB, struct.pack(">f", 42.5))], [])]], counts=False, fix=True)
+    g, w = both(eng, rb, _q("10m-sum", "sum"))
+    assert_groups_match(g, w, "sum", tol=0.0)
+    assert g[0][2].view(np.float64).tolist() == [42.5]
+
+
+def test_rollup_mode_guards(eng):
+    rb = _batch([[(B, [(0, *_l(20))], [(0, *_l(2))])]])
+    eng.load_rollup(rb)
+    with pytest.raises(EngineError):
+        eng.run(abi.new_query(B, B + 3600, "sum"))   # a rollup query needs a downsampler
+    with pytest.raises(EngineError) as e:
+        eng.run_multi([_q(), _q()])
+    assert e.value.code == abi.TSDB_E_NOT_IMPLEMENTED
+
+
+def random_table(rng, n_series, n_groups, days, p_sum=0.9, p_cnt=0.9, floats=False, counts=True,
+                 interval="10m", span="6h"):
+    """Rollup rows of n_series series over `days` days with cells missing at random."""
+    iv = _iv(interval, span)
+    step = iv.interval_s
+    slots = {}   # rollup row base -> offsets, as addAggregatePoint files them
+    for t in range(B, B + days * 86400, step):
+        base = engine.rollup_basetime(t, iv)
+        slots.setdefault(base, []).append((t - base) // step)
+    rows = []
+    for s in range(n_series):
+        rr = []
+        for base, offs in slots.items():
+            n = len(offs)
+            has_v = rng.random(n) < p_sum
+            has_c = rng.random(n) < p_cnt
+            fv = rng.normal(100, 50, n)
+            iv_ = rng.integers(-1000, 100000, n)
+            cv = rng.integers(0, 40, n)
+            vals, cnts = [], []
+            for j, o in enumerate(offs):
+                if has_v[j]:
+                    vals.append((o, 0xF, struct.pack(">d", float(fv[j]))) if floats else
+                                (o, 0x7, struct.pack(">q", int(iv_[j]))))
+                if counts and has_c[j]:
+                    cnts.append((o, 0x0, struct.pack(">b", int(cv[j]))))
+            if vals or cnts:
+                rr.append((base, vals, cnts))
+        rows.append(rr)
+    groups = [int(x) for x in rng.integers(0, n_groups, n_series)]
+    return _batch(rows, counts=counts, groups=groups, iv=iv)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("floats", [False, True])
+def test_random_tables(eng, seed, floats):
+    rng = np.random.default_rng(seed * 7 + floats)
+    rb = random_table(rng, 24, 5, 3, floats=floats)
+    eng.load_rollup(rb)
+    end = B + 2 * 86400 + 3600
+    for ds in ("10m-avg", "30m-avg", "1h-count", "10m-count-zero", "20m-avg-nan", "1h-sum", "10m-max",
+               "30m-min", "1h-zimsum", "1h-avg-null", "1d-avg"):
+        for agg in ("avg", "sum", "count", "max", "none", "dev", "zimsum"):
+            for rate in (False, True):
+                q = _q(ds, agg, start=B + 1800, end=end, rate=rate)
+                g = eng.run(q)
+                w = O.run_rollup_query(rb, q)
+                fn = ds.split("-")[1]
+                exact = fn in ("max", "min", "count") and agg in ("max", "min", "none") and not rate
+                tol = 0.0 if exact else (1e-9 if agg == "dev" else 1e-12)
+                assert_groups_match(g, w, agg, tol=tol, ctx=f"{ds} {agg} rate={rate}")
+
+
+def test_no_counts_table(eng):
+    rng = np.random.default_rng(11)
+    rb = random_table(rng, 16, 3, 2, counts=False)
+    eng.load_rollup(rb)
+    for ds, agg in (("10m-avg", "sum"), ("1h-count", "sum"), ("30m-sum", "avg"), ("1h-max", "max"),
+                    ("10m-avg", "none")):
+        q = _q(ds, agg, end=B + 86400 * 2)
+        assert_groups_match(eng.run(q), O.run_rollup_query(rb, q), agg, tol=1e-12, ctx=f"{ds} {agg}")
+
+
+def test_hour_and_day_tables(eng):
+    rng = np.random.default_rng(5)
+    for interval, span, days, ds in (("1h", "1d", 6, "1h-avg"), ("1h", "1d", 6, "6h-count"), ("1d", "1n", 70, "1d-avg"),
+                                     ("1d", "1n", 70, "7d-sum")):
+        rb = random_table(rng, 8, 2, days, interval=interval, span=span)
+        q = _q(ds, "avg", start=B, end=B + days * 86400)
+        assert_groups_match(eng.run_rollup_batch(rb, q), O.run_rollup_query(rb, q), "avg", tol=1e-12,
+                            ctx=f"{interval} {ds}")
+
+
+def test_larger_table_properties(eng):
+    """1,000 series x 4 days of 10m rollups against the oracle: avg and count downsampling."""
+    rng = np.random.default_rng(99)
+    rb = random_table(rng, 1000, 40, 4, p_sum=0.97, p_cnt=0.97)
+    eng.load_rollup(rb)
+    q = _q("1h-avg", "avg", start=B, end=B + 4 * 86400)
+    got = eng.run(q)
+    want = O.run_rollup_query(rb, q)
+    assert_groups_match(got, want, "avg", tol=1e-12, ctx="1000 series")
+    q = _q("1d-count", "sum", start=B, end=B + 4 * 86400)
+    got = eng.run(q)
+    want = O.run_rollup_query(rb, q)
+    assert_groups_match(got, want, "sum", tol=0.0, ctx="1000 series count")
