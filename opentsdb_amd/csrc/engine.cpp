@@ -3030,10 +3030,15 @@ int run_rollup(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
   q1.aggregator = TSDB_AGG_NONE;
   q1.rate = 0;
   q1.flags = 0;
-  Plan P1;
-  rc = plan_query(c, &q1, P1);
-  if (rc) return rc;
-  if (P1.K != P.K || P1.B0 != P.B0) return fail(TSDB_E_HIP, "rollup combine: plans disagree");
+  // the query's own slot grid and scan range (a rate query scans one row further back)
+  Plan P1 = P;
+  P1.f = f_of(TSDB_AGG_SUM);
+  P1.ga = ga_of(TSDB_AGG_NONE);
+  P1.interp = interp_of(TSDB_AGG_NONE);
+  P1.none = true;
+  P1.gsel = 0;
+  P1.ordered = false;
+  P1.gslot = grid_wave_lds(P.K, false, false) > 40 * 1024;
   P1.dense_out = true;
   rc = run_device(c, &q1, P1, c->n_series, false);
   if (rc) return rc;
