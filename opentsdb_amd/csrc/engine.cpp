@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <mutex>
 #include <numeric>
 #include <string>
@@ -351,7 +352,7 @@ struct tsdbhip_ctx {
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;   // result downloads overlapped with evaluation
   hipEvent_t ev[4] = {};
-  hipEvent_t cev[8] = {};              // chunk-done events for copy_stream
+  hipEvent_t cev[9] = {};              // chunk-done events for copy_stream (+ timestamps final)
   std::mutex mu;
   // resident batch (series in group-sorted order)
   int64_t n_series = 0, n_rows = 0, n_groups = 0;
@@ -2593,7 +2594,26 @@ int collect(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bo
 // ---------------------------------------------------------------------------
 namespace {
 
+// TSDBHIP_TRACE=1: host wall time of a query's phases on stderr (diagnostics only)
+struct PhaseTrace {
+  bool on;
+  const char* name;
+  std::chrono::steady_clock::time_point t0, last;
+  explicit PhaseTrace(const char* n) : on(std::getenv("TSDBHIP_TRACE") != nullptr), name(n) {
+    t0 = last = std::chrono::steady_clock::now();
+  }
+  void mark(const char* what) {
+    if (!on) return;
+    const auto t = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[trace %s] %-18s %8.3f ms  (total %8.3f)\n", name, what,
+                 std::chrono::duration<double, std::milli>(t - last).count(),
+                 std::chrono::duration<double, std::milli>(t - t0).count());
+    last = t;
+  }
+};
+
 int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_result** out) {
+  PhaseTrace tr("raw");
   const int64_t S = c->n_series;
   const int64_t start = P.ss * 1000, end = P.se * 1000;
   // points of every series inside the scan range (rows with base in [ss, se), Span order)
@@ -2637,6 +2657,7 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
     }
   }
   const int64_t G = (int64_t)grp_ser.size() - 1;
+  tr.mark("host spans");
   std::vector<uint8_t> act(std::max<int64_t>(1, G), 0);
   for (int64_t g = 0; g < G; g++)
     for (int64_t s = grp_ser[g]; s < grp_ser[g + 1]; s++) if (sp_n[s] > 0) { act[g] = 1; break; }
@@ -2717,6 +2738,7 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
     std::vector<int32_t> U(ng);
     HIP_OK(hipMemcpyAsync(U.data(), rp.U, ng * 4, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
+    tr.mark("decode+union");
     std::vector<int64_t> ooff(ng + 1, 0), coff(ng + 1, 0);
     std::vector<int32_t> sg, st;
     for (int64_t i = 0; i < ng; i++) {
@@ -2818,10 +2840,18 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
       for (int64_t g = 0; g < G; g++) nact += act[g];
       direct_r = make_result(nact, nout);
       if (!direct_r) return fail(TSDB_E_NOMEM, "result allocation");
+      tr.mark("result alloc");
       // chunked only for the double-only evaluation: its strips are short (config 4 rate: the
       // download hides behind the next chunk, 36 -> 30 ms per step); the long LERP strips are
       // long-running waves that a launch split leaves idle at every chunk's tail (94 -> 188 ms)
       const int nch = (P.gsel || rp.do_long) ? 1 : (int)std::min<int64_t>(8, std::max<int64_t>(1, ns / 64));
+      // the timestamps are final once k_raw_rank ran: their download overlaps the evaluation
+      HIP_OK(hipEventRecord(c->cev[8], c->stream));
+      if (nout) {
+        HIP_OK(hipStreamWaitEvent(c->copy_stream, c->cev[8], 0));
+        HIP_OK(hipMemcpyAsync(const_cast<int64_t*>(direct_r->ts_ms), rp.out_ts, nout * 8, hipMemcpyDeviceToHost,
+                              c->copy_stream));
+      }
       int64_t s_lo = 0;
       for (int ci = 0; ci < nch; ci++) {
         int64_t s_hi = ci + 1 == nch ? ns : std::max(s_lo, ns * (ci + 1) / nch);
@@ -2840,8 +2870,6 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
         HIP_OK(hipEventRecord(c->cev[ci], c->stream));
         if (o1 > o0) {
           HIP_OK(hipStreamWaitEvent(c->copy_stream, c->cev[ci], 0));
-          HIP_OK(hipMemcpyAsync(const_cast<int64_t*>(direct_r->ts_ms) + o0, rp.out_ts + o0, (o1 - o0) * 8,
-                                hipMemcpyDeviceToHost, c->copy_stream));
           HIP_OK(hipMemcpyAsync(const_cast<uint64_t*>(direct_r->value_bits) + o0, rp.out_bits + o0, (o1 - o0) * 8,
                                 hipMemcpyDeviceToHost, c->copy_stream));
           HIP_OK(hipMemcpyAsync(const_cast<uint8_t*>(direct_r->is_int) + o0, rp.out_int + o0, o1 - o0,
@@ -2850,7 +2878,10 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
         s_lo = s_hi;
       }
       HIP_OK(hipEventRecord(c->ev[1], c->stream));
+      HIP_OK(hipStreamSynchronize(c->stream));
+      tr.mark("eval (device)");
       HIP_OK(hipStreamSynchronize(c->copy_stream));
+      tr.mark("download tail");
     } else {
       HIP_OK(hipEventRecord(c->ev[1], c->stream));
       res_ts.resize(base + nout);
@@ -2886,6 +2917,7 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
     direct_r = make_result(0, 0);
     if (!direct_r) return fail(TSDB_E_NOMEM, "result allocation");
   }
+  tr.mark("finish");
   if (direct) {
     auto* gptr = const_cast<int64_t*>(direct_r->group_ptr);
     auto* gid = const_cast<int32_t*>(direct_r->group_id);
