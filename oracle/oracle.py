@@ -65,6 +65,11 @@ def lib():
         L.ref_run_query_mt.argtypes = [C.POINTER(abi.Batch), C.POINTER(abi.Query), C.c_int,
                                        C.POINTER(C.POINTER(abi.Result))]
         L.ref_result_free.argtypes = [C.POINTER(abi.Result)]
+        L.ref_compact_row.argtypes = [C.c_int64, C.POINTER(C.c_void_p), C.POINTER(C.c_int64), C.POINTER(C.c_void_p),
+                                      C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_int,
+                                      C.POINTER(C.c_void_p), C.POINTER(C.c_int64), C.POINTER(C.c_void_p),
+                                      C.POINTER(C.c_int64)]
+        L.ref_free.argtypes = [C.c_void_p]
         L.ref_run_rollup_query.argtypes = [C.POINTER(abi.RollupBatch), C.POINTER(abi.Query),
                                            C.POINTER(C.POINTER(abi.Result))]
         L.ref_rollup_scan_bounds.argtypes = [C.POINTER(abi.Query), C.POINTER(abi.RollupInterval),
@@ -257,6 +262,33 @@ def scan_bounds(q: abi.Query):
     s, e = C.c_int64(), C.c_int64()
     lib().ref_scan_bounds(C.byref(q), C.byref(s), C.byref(e))
     return s.value, e.value
+
+
+def compact_row(columns, fix_duplicates: bool = True, timestamps=None):
+    """CompactionQueue.Compaction.compact() of one row (query time): columns = [(qualifier
+    bytes, value bytes)] in scan order, timestamps = their KeyValue timestamps (default: the
+    position).  Returns (qualifier, value), None (no datapoint) or raises OracleError."""
+    n = len(columns)
+    bufs = [(C.create_string_buffer(bytes(q), max(1, len(q))), C.create_string_buffer(bytes(v), max(1, len(v))))
+            for q, v in columns]
+    qp = (C.c_void_p * max(1, n))(*[C.cast(b[0], C.c_void_p) for b in bufs])
+    vp = (C.c_void_p * max(1, n))(*[C.cast(b[1], C.c_void_p) for b in bufs])
+    ql = (C.c_int64 * max(1, n))(*[len(q) for q, _ in columns])
+    vl = (C.c_int64 * max(1, n))(*[len(v) for _, v in columns])
+    ts = (C.c_int64 * max(1, n))(*(timestamps if timestamps is not None else range(n)))
+    oq, ov = C.c_void_p(), C.c_void_p()
+    oql, ovl = C.c_int64(), C.c_int64()
+    rc = lib().ref_compact_row(n, qp, ql, vp, vl, ts, int(fix_duplicates), C.byref(oq), C.byref(oql), C.byref(ov),
+                               C.byref(ovl))
+    if rc < 0:
+        _err(rc)
+    if rc == 0:
+        return None
+    try:
+        return C.string_at(oq, oql.value), C.string_at(ov, ovl.value)
+    finally:
+        lib().ref_free(oq)
+        lib().ref_free(ov)
 
 
 def run_rollup_query(rb: abi.HostRollupBatch, q: abi.Query):

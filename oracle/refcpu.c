@@ -856,6 +856,237 @@ static void span_first_last(span_view* s, int64_t* first, int64_t* last, int64_t
 }
 
 /* ======================================================================== */
+/* Query-time compaction: CompactionQueue.Compaction (src/core/CompactionQueue.java:267-626,  */
+/* default merge, no write-back), ColumnDatapointIterator (src/core/ColumnDatapointIterator    */
+/* .java:63-205), AppendDataPoints.parseKeyValue (src/core/AppendDataPoints.java:110-240) and  */
+/* the float / flag fixups (src/core/Internal.java:535-591).                                  */
+/* ======================================================================== */
+typedef struct {
+  uint8_t* q;          /* (fixed) qualifier, owned */
+  int64_t qlen;
+  uint8_t* v;          /* (fixed) value, owned */
+  int64_t vlen;
+  int64_t ts;          /* KeyValue.timestamp() */
+  int64_t order;       /* position in the row (tie-break of equal (offset, timestamp)) */
+  int64_t qi, vi;      /* qualifier_offset, value_offset */
+  int cur_qlen, cur_vlen, is_ms;
+  int64_t cur_off;     /* current_timestamp_offset (ms) */
+  int needs_fixup;
+} cdi;
+
+static int cdi_update(cdi* c) {   /* ColumnDatapointIterator.update :150-166 */
+  if (c->qi >= c->qlen || c->vi >= c->vlen) return 0;
+  if (in_ms(c->q[c->qi])) {
+    if (c->qi + 4 > c->qlen) jthrow(TSDB_E_ILLEGAL_DATA, "ArrayIndexOutOfBounds in a compacted qualifier");
+    c->cur_qlen = 4;
+    c->is_ms = 1;
+    c->cur_off = (int64_t)((be32(c->q + c->qi) & 0x0FFFFFC0u) >> 6);
+  } else {
+    c->cur_qlen = 2;
+    c->is_ms = 0;
+    c->cur_off = (int64_t)(be16(c->q + c->qi) >> 4) * 1000;
+  }
+  c->cur_vlen = (c->q[c->qi + c->cur_qlen - 1] & 7) + 1;
+  return 1;
+}
+static int cdi_advance(cdi* c) {   /* :141-145 */
+  c->qi += c->cur_qlen;
+  c->vi += c->cur_vlen;
+  return cdi_update(c);
+}
+/* heap order :181-189: offset ascending, column timestamp descending (the entry kept first);
+ * equal pairs by position in the row (PriorityQueue leaves them unordered) */
+static int cdi_less(const cdi* a, const cdi* b) {
+  if (a->cur_off != b->cur_off) return a->cur_off < b->cur_off;
+  if (a->ts != b->ts) return a->ts > b->ts;
+  return a->order < b->order;
+}
+
+static void cdi_init(cdi* c, const uint8_t* q, int64_t qlen, const uint8_t* v, int64_t vlen, int64_t ts, int64_t order) {
+  memset(c, 0, sizeof *c);
+  c->q = (uint8_t*)xmalloc((size_t)(qlen ? qlen : 1));
+  c->v = (uint8_t*)xmalloc((size_t)(vlen ? vlen : 1));
+  if (qlen) memcpy(c->q, q, (size_t)qlen);
+  if (vlen) memcpy(c->v, v, (size_t)vlen);
+  c->qlen = qlen;
+  c->vlen = vlen;
+  c->ts = ts;
+  c->order = order;
+  if (qlen == 2) {   /* checkForFixup :74-89 (fixups predate compaction: 2-byte qualifiers only) */
+    const uint8_t qual1 = c->q[1];
+    if ((qual1 & 0x8) && (qual1 & 7) == 3 && c->vlen == 8) {   /* floatingPointValueToFix */
+      if (c->v[0] || c->v[1] || c->v[2] || c->v[3])
+        jthrow(TSDB_E_ILLEGAL_DATA, "Corrupted floating point value -- first 4 bytes are expected to be zeros");
+      memmove(c->v, c->v + 4, 4);
+      c->vlen = 4;
+      c->needs_fixup = 1;
+    }
+    const uint8_t len_byte = (uint8_t)((qual1 & ~7) | (uint8_t)(c->vlen - 1));   /* fixQualifierFlags */
+    if (len_byte != qual1) {
+      c->q[1] = len_byte;
+      c->needs_fixup = 1;
+    }
+  }
+  cdi_update(c);
+}
+
+/* AppendDataPoints.parseKeyValue: the (qualifier, value) pairs of an append column, a later
+ * pair replacing an earlier one of the same offset, sorted by offset */
+static void parse_append(const uint8_t* v, int64_t vlen, uint8_t** oq, int64_t* oql, uint8_t** ov, int64_t* ovl) {
+  typedef struct { int64_t delta; int64_t qo, ql, vo, vl; } apc;
+  apc* cells = (apc*)xcalloc((size_t)(vlen + 1), sizeof(apc));
+  int64_t n = 0, idx = 0;
+  while (idx < vlen) {
+    const int64_t ql = in_ms(v[idx]) ? 4 : 2;
+    if (idx + ql > vlen) { free(cells); jthrow(TSDB_E_ILLEGAL_DATA, "Corrupted value: couldn't break down into individual values"); }
+    const int64_t vl = (v[idx + ql - 1] & 7) + 1;
+    if (idx + ql + vl > vlen) { free(cells); jthrow(TSDB_E_ILLEGAL_DATA, "Corrupted value: couldn't break down into individual values"); }
+    const int64_t delta = ql == 4 ? (int64_t)((be32(v + idx) & 0x0FFFFFC0u) >> 6) : (int64_t)(be16(v + idx) >> 4) * 1000;
+    int64_t j = 0;
+    for (; j < n; j++) if (cells[j].delta == delta) break;
+    cells[j].delta = delta;
+    cells[j].qo = idx;
+    cells[j].ql = ql;
+    cells[j].vo = idx + ql;
+    cells[j].vl = vl;
+    if (j == n) n++;
+    idx += ql + vl;
+  }
+  for (int64_t i = 1; i < n; i++) {   /* TreeMap order */
+    apc t = cells[i];
+    int64_t j = i - 1;
+    while (j >= 0 && cells[j].delta > t.delta) { cells[j + 1] = cells[j]; j--; }
+    cells[j + 1] = t;
+  }
+  int64_t tq = 0, tv = 0;
+  for (int64_t i = 0; i < n; i++) { tq += cells[i].ql; tv += cells[i].vl; }
+  *oq = (uint8_t*)xmalloc((size_t)(tq ? tq : 1));
+  *ov = (uint8_t*)xmalloc((size_t)(tv ? tv : 1));
+  int64_t a = 0, b = 0;
+  for (int64_t i = 0; i < n; i++) {
+    memcpy(*oq + a, v + cells[i].qo, (size_t)cells[i].ql);
+    memcpy(*ov + b, v + cells[i].vo, (size_t)cells[i].vl);
+    a += cells[i].ql;
+    b += cells[i].vl;
+  }
+  *oql = tq;
+  *ovl = tv;
+  free(cells);
+}
+
+/* Compaction.compact() as TSDB.compact(row) returns it to a query (SaltScanner.processRow
+ * :802-830).  Returns 1 with the compacted cell in out_q / out_v (malloc'd), 0 when the row
+ * has no datapoint (compacted == null), or a negative TSDB_E_* code. */
+int ref_compact_row(int64_t ncols, const uint8_t* const* quals, const int64_t* qlens, const uint8_t* const* vals,
+                    const int64_t* vlens, const int64_t* col_ts, int fix_duplicates, uint8_t** out_q,
+                    int64_t* out_qlen, uint8_t** out_v, int64_t* out_vlen) {
+  cdi* volatile cols = NULL;
+  volatile int64_t n = 0;
+  volatile int rc = 0;
+  *out_q = *out_v = NULL;
+  *out_qlen = *out_vlen = 0;
+  TRY {
+    cols = (cdi*)xcalloc((size_t)(ncols ? ncols : 1), sizeof(cdi));
+    int64_t first_dp = -1;    /* findFirstDatapointColumn :389-399 */
+    int appended = 0;
+    for (int64_t i = 0; i < ncols; i++) {   /* buildHeapProcessAnnotations :401-452 */
+      const int64_t ql = qlens[i];
+      if (ql & 1) {
+        if (ql == 3 && quals[i][0] == 0x05) {   /* AppendDataPoints.APPEND_COLUMN_PREFIX */
+          uint8_t *aq, *av;
+          int64_t aql, avl;
+          parse_append(vals[i], vlens[i], &aq, &aql, &av, &avl);
+          cdi_init(&cols[n], aq, aql, av, avl, col_ts ? col_ts[i] : 0, i);
+          free(aq);
+          free(av);
+          appended = 1;
+          first_dp = n;
+          if (cols[n].qlen > 0) n++;
+          else { free(cols[n].q); free(cols[n].v); }
+        }
+        continue;   /* annotations, histograms, unknown prefixes */
+      }
+      if (first_dp < 0 && !appended) first_dp = n;
+      cdi_init(&cols[n], quals[i], ql, vals[i], vlens[i], col_ts ? col_ts[i] : 0, i);
+      if (cols[n].qlen > 0) n++;
+      else { free(cols[n].q); free(cols[n].v); }
+    }
+    if (n == 0) {
+      rc = 0;
+    } else if (n == 1 && (cols[0].qlen == 2 || (cols[0].qlen == 4 && in_ms(cols[0].q[0]))) && !cols[0].needs_fixup) {
+      /* noMergesOrFixups :311-328: the single column as stored (or as parsed from the append) */
+      if (cols[0].vlen == 0) jthrow(TSDB_E_ILLEGAL_DATA, "empty value");
+      *out_q = (uint8_t*)xmalloc((size_t)cols[0].qlen);
+      *out_v = (uint8_t*)xmalloc((size_t)cols[0].vlen);
+      memcpy(*out_q, cols[0].q, (size_t)cols[0].qlen);
+      memcpy(*out_v, cols[0].v, (size_t)cols[0].vlen);
+      *out_qlen = cols[0].qlen;
+      *out_vlen = cols[0].vlen;
+      rc = 1;
+    } else {
+      /* defaultMergeDataPoints :512-545 over the heap of columns */
+      int64_t tq = 0, tv = 0;
+      for (int64_t i = 0; i < n; i++) { tq += cols[i].qlen; tv += cols[i].vlen; }
+      uint8_t* cq = (uint8_t*)xmalloc((size_t)tq + 1);
+      uint8_t* cv = (uint8_t*)xmalloc((size_t)tv + 2);
+      *out_q = cq;
+      *out_v = cv;
+      int64_t qo = 0, vo = 0, segs = 0, last_vo = 0, last_vl = 0, prev = -1;
+      int ms_in_row = 0, s_in_row = 0;
+      int* live = (int*)xcalloc((size_t)n, sizeof(int));
+      for (int64_t i = 0; i < n; i++) live[i] = cols[i].vlen > 0 && cols[i].qi < cols[i].qlen;
+      for (int64_t i = 0; i < n; i++)
+        if (!live[i]) { free(live); jthrow(TSDB_E_ILLEGAL_DATA, "empty value"); }
+      for (;;) {
+        int64_t best = -1;
+        for (int64_t i = 0; i < n; i++)
+          if (live[i] && (best < 0 || cdi_less(&cols[i], &cols[best]))) best = i;
+        if (best < 0) break;
+        cdi* c = &cols[best];
+        if (c->vi + c->cur_vlen > c->vlen) { free(live); jthrow(TSDB_E_ILLEGAL_DATA, "value shorter than its qualifiers"); }
+        if (c->cur_off == prev) {
+          /* getCopyOfCurrentValue vs the last segment written */
+          if (c->cur_vlen != last_vl || memcmp(c->v + c->vi, cv + last_vo, (size_t)last_vl) != 0) {
+            if (!fix_duplicates) {
+              free(live);
+              jthrow(TSDB_E_ILLEGAL_DATA, "Duplicate timestamp for key, ms_offset=%lld; set tsd.storage.fix_duplicates=true",
+                     (long long)c->cur_off);
+            }
+          }
+        } else {
+          prev = c->cur_off;
+          memcpy(cq + qo, c->q + c->qi, (size_t)c->cur_qlen);   /* writeToBuffers */
+          memcpy(cv + vo, c->v + c->vi, (size_t)c->cur_vlen);
+          last_vo = vo;
+          last_vl = c->cur_vlen;
+          qo += c->cur_qlen;
+          vo += c->cur_vlen;
+          segs++;
+          if (c->is_ms) ms_in_row = 1; else s_in_row = 1;
+        }
+        live[best] = cdi_advance(c);
+      }
+      free(live);
+      if (segs > 1) cv[vo++] = (ms_in_row && s_in_row) ? 1 : 0;   /* buildCompactedColumn :547-566 */
+      *out_qlen = qo;
+      *out_vlen = vo;
+      rc = 1;
+    }
+  } CATCH(e) {
+    rc = e;
+    free(*out_q);
+    free(*out_v);
+    *out_q = *out_v = NULL;
+  } END_TRY
+  if (cols) {
+    for (int64_t i = 0; i < n; i++) { free(cols[i].q); free(cols[i].v); }
+    free(cols);
+  }
+  return rc;
+}
+void ref_free(void* p) { free(p); }
+
+/* ======================================================================== */
 /* RollupSpan + RollupSeq (src/rollup/RollupSpan.java, src/rollup/RollupSeq.java) */
 /* ======================================================================== */
 /* A RollupSeq row: the queried aggregate's cells and (need_count) the count cells, each a

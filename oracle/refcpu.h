@@ -89,6 +89,12 @@ void ref_result_free(ref_result* r);
 /* TsdbQuery.run over a rollup table (RollupSpan / RollupSeq spans, the Downsampler's rollup
  * branches, rollup scan bounds); layout as tsdbhip_load_rollup. */
 int ref_run_rollup_query(const tsdbhip_rollup_batch* rb, const tsdbhip_query* q, ref_result** out);
+/* Compaction.compact() of one row's columns (query-time, no write-back): 1 + the compacted
+ * cell (free both with ref_free), 0 = no datapoint, < 0 = TSDB_E_* */
+int ref_compact_row(int64_t ncols, const uint8_t* const* quals, const int64_t* qlens, const uint8_t* const* vals,
+                    const int64_t* vlens, const int64_t* col_ts, int fix_duplicates, uint8_t** out_q,
+                    int64_t* out_qlen, uint8_t** out_v, int64_t* out_vlen);
+void ref_free(void* p);
 int ref_rollup_scan_bounds(const tsdbhip_query* q, const tsdbhip_rollup_interval* iv, int64_t* s_out, int64_t* e_out);
 
 #ifdef __cplusplus
