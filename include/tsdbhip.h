@@ -372,6 +372,37 @@ typedef struct {
  * (downsampled or not; percentile group-by, ordered and multi-GPU entry points excluded). */
 int tsdbhip_load_rollup(tsdbhip_ctx* ctx, const tsdbhip_rollup_batch* rb);
 
+/* ---- query-time compaction ----------------------------------
+ * The scanner's rows before TSDB.compact (src/core/SaltScanner.java:734-870): every column
+ * (KeyValue) of a row key in scan order -- single datapoints (2-byte or 4-byte ms qualifiers),
+ * earlier compactions, append columns (qualifier 0x05 0x00 0x00) and annotations / other
+ * odd-length qualifiers (skipped) -- with their HBase write timestamps.  Every row is compacted
+ * on the GPU as CompactionQueue.Compaction.compact (src/core/CompactionQueue.java:330-566,
+ * ColumnDatapointIterator.java:63-205, AppendDataPoints.java:110-240) returns it to a query:
+ * datapoints merged by offset, the newest column's kept at a repeated offset (any other value
+ * -> IllegalDataException unless fix_duplicates), 2-byte float and length fixups, the meta byte;
+ * a single column needing no fixup as stored; rows without a datapoint dropped.  The compacted
+ * rows become the resident batch.  Compaction exceptions are raised by the first query whose
+ * scan range covers the row.  NOT_IMPLEMENTED: two rows of one series with the same base time
+ * (salt buckets; tsdbhip_load merges those), more than 2^31 columns, rows or datapoints; per row,
+ * lazily: a compacted cell out of time order, a datapoint column with an empty value. */
+typedef struct {
+  int64_t n_series;
+  const int64_t* series_row_ptr;   /* [n_series + 1] */
+  int64_t n_rows;
+  const uint32_t* row_base_time;   /* [n_rows] */
+  const int64_t* row_col_ptr;      /* [n_rows + 1] columns of each row */
+  int64_t n_cols;
+  const uint64_t* col_qual_off;    /* [n_cols + 1] from 0 */
+  const uint64_t* col_val_off;     /* [n_cols + 1] from 0 */
+  const int64_t* col_timestamp;    /* [n_cols] KeyValue.timestamp(), or NULL (equal: scan order decides) */
+  const uint8_t* qual;
+  const uint8_t* val;
+  const int32_t* group_id;         /* [n_series] */
+  int32_t fix_duplicates;          /* tsd.storage.fix_duplicates */
+} tsdbhip_cell_batch;
+int tsdbhip_load_cells(tsdbhip_ctx* ctx, const tsdbhip_cell_batch* cb);
+
 /* Device synchronisation helper for host code that does not use HIP directly. */
 int tsdbhip_sync(tsdbhip_ctx* ctx);
 

@@ -258,6 +258,76 @@ class HostBatch:
         return len(self.row_base_time)
 
 
+class CellBatch(C.Structure):
+    """tsdbhip_cell_batch: a scan's rows before compaction (every column of every row)."""
+    _fields_ = [
+        ("n_series", C.c_int64),
+        ("series_row_ptr", C.POINTER(C.c_int64)),
+        ("n_rows", C.c_int64),
+        ("row_base_time", C.POINTER(C.c_uint32)),
+        ("row_col_ptr", C.POINTER(C.c_int64)),
+        ("n_cols", C.c_int64),
+        ("col_qual_off", C.POINTER(C.c_uint64)),
+        ("col_val_off", C.POINTER(C.c_uint64)),
+        ("col_timestamp", C.POINTER(C.c_int64)),
+        ("qual", C.POINTER(C.c_uint8)),
+        ("val", C.POINTER(C.c_uint8)),
+        ("group_id", C.POINTER(C.c_int32)),
+        ("fix_duplicates", C.c_int32),
+    ]
+
+
+class HostCellBatch:
+    """Owns the arrays behind a :class:`CellBatch`."""
+
+    def __init__(self, series_row_ptr, row_base_time, row_col_ptr, col_qual_off, col_val_off, qual, val, group_id,
+                 col_timestamp=None, fix_duplicates=False):
+        self.series_row_ptr = np.ascontiguousarray(series_row_ptr, dtype=np.int64)
+        self.row_base_time = np.ascontiguousarray(row_base_time, dtype=np.uint32)
+        self.row_col_ptr = np.ascontiguousarray(row_col_ptr, dtype=np.int64)
+        self.col_qual_off = np.ascontiguousarray(col_qual_off, dtype=np.uint64)
+        self.col_val_off = np.ascontiguousarray(col_val_off, dtype=np.uint64)
+        self.qual = np.ascontiguousarray(qual, dtype=np.uint8)
+        self.val = np.ascontiguousarray(val, dtype=np.uint8)
+        self.group_id = np.ascontiguousarray(group_id, dtype=np.int32)
+        self.col_timestamp = None if col_timestamp is None else np.ascontiguousarray(col_timestamp, dtype=np.int64)
+        if self.qual.size == 0:
+            self.qual = np.zeros(1, np.uint8)
+        if self.val.size == 0:
+            self.val = np.zeros(1, np.uint8)
+        ns, nr, nc = len(self.series_row_ptr) - 1, len(self.row_base_time), len(self.col_qual_off) - 1
+        assert len(self.group_id) == ns and len(self.row_col_ptr) == nr + 1 and len(self.col_val_off) == nc + 1
+        self.c = CellBatch(ns, _ptr(self.series_row_ptr, C.c_int64), nr, _ptr(self.row_base_time, C.c_uint32),
+                           _ptr(self.row_col_ptr, C.c_int64), nc, _ptr(self.col_qual_off, C.c_uint64),
+                           _ptr(self.col_val_off, C.c_uint64),
+                           C.POINTER(C.c_int64)() if self.col_timestamp is None else _ptr(self.col_timestamp, C.c_int64),
+                           _ptr(self.qual, C.c_uint8), _ptr(self.val, C.c_uint8), _ptr(self.group_id, C.c_int32),
+                           int(fix_duplicates))
+
+    @classmethod
+    def from_rows(cls, series, group_ids, fix_duplicates=False):
+        """series: [[(base_time, [(qualifier bytes, value bytes, timestamp | None), ...]), ...], ...]"""
+        srp, bases, rcp, qo, vo, ts = [0], [], [0], [0], [0], []
+        qb, vb = bytearray(), bytearray()
+        any_ts = False
+        for rows in series:
+            for base, cols in rows:
+                bases.append(base)
+                for col in cols:
+                    q, v = col[0], col[1]
+                    t = col[2] if len(col) > 2 else None
+                    any_ts |= t is not None
+                    ts.append(0 if t is None else t)
+                    qb += q
+                    vb += v
+                    qo.append(len(qb))
+                    vo.append(len(vb))
+                rcp.append(len(qo) - 1)
+            srp.append(len(bases))
+        return cls(srp, bases, rcp, qo, vo, np.frombuffer(bytes(qb), np.uint8), np.frombuffer(bytes(vb), np.uint8),
+                   group_ids, np.array(ts, np.int64) if any_ts else None, fix_duplicates)
+
+
 class RollupBatch(C.Structure):
     """tsdbhip_rollup_batch: RollupSeq rows of the queried aggregate (+ count cells)."""
     _fields_ = [

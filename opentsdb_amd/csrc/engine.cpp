@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <chrono>
+#include <functional>
 #include <mutex>
 #include <numeric>
 #include <string>
@@ -409,6 +410,7 @@ struct tsdbhip_ctx {
   int64_t redo_other = 0;                // + tiles of neither row class (k_grid only)
   tsdbhip_timing timing{};
   double index_ms = 0;                   // k_index (+ val2 pass) of the last load
+  double compact_ms = 0;                 // k_compact pipeline of the last tsdbhip_load_cells
   // account() cache (invalidated by every load)
   bool acct_valid = false;
   int64_t acct_ss = 0, acct_se = 0, acct_dps = 0, acct_bytes = 0;
@@ -435,6 +437,12 @@ struct tsdbhip_ctx {
   std::vector<std::string> ro_unsup;   // per value series: why the engine does not run it ("" = runs)
   std::vector<int64_t> ro_res;         // batch position -> resident index
   DevBuf ro_cmap;                      // [n_series] resident index of a value series' count series (-1: none)
+  // query-time compaction (tsdbhip_load_cells): rows whose compaction failed, raised when a
+  // query's scan range covers them (SaltScanner.processRow fails the scan)
+  struct CmpErr { int64_t series, row; int64_t base; int32_t code; };
+  std::vector<CmpErr> cmp_errs;
+  void* cmp_tmp = nullptr;
+  size_t cmp_tmp_bytes = 0;
   bool ro_scan_valid = false;          // scan-active value series of the last scan range
   int64_t ro_scan_ss = 0, ro_scan_se = 0;
   std::vector<uint8_t> ro_scan_act;    // [n_series] resident: rollup rows in the scan range
@@ -596,6 +604,7 @@ static void release_batch(tsdbhip_ctx* c) {
   c->ro_unsup.clear();
   c->ro_res.clear();
   c->ro_cmap.release();
+  c->cmp_errs.clear();
 }
 
 extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
@@ -613,6 +622,7 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   for (auto& o : c->ro_out)
     for (DevBuf* b : {&o.series, &o.base, &o.qual, &o.voff, &o.val}) b->release();
   if (c->ro_tmp) (void)hipFree(c->ro_tmp);
+  if (c->cmp_tmp) (void)hipFree(c->cmp_tmp);
   for (DevBuf* b : {&c->sel_vals, &c->sel_sorted, &c->sel_uni, &c->sel_gsp, &c->cal_bounds}) b->release();
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   for (auto& e : c->cev) if (e) (void)hipEventDestroy(e);
@@ -1290,6 +1300,225 @@ extern "C" int tsdbhip_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* r
   return 0;
 }
 
+// ---- query-time compaction -----------------------------------------
+// The scanner's rows before TSDB.compact: the device compacts every row (k_compact.hip), the
+// host lays the compacted rows out as the resident batch (series by group, rows by base time,
+// rows without a datapoint dropped as SaltScanner.processRow drops a null compaction).
+extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) {
+  if (!c || !cb) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  const int64_t NS = cb->n_series, NR = cb->n_rows, NC = cb->n_cols;
+  if (NS < 0 || NR < 0 || NC < 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
+  if (NS > 0 && (!cb->series_row_ptr || !cb->group_id)) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null batch arrays");
+  if (NR > 0 && (!cb->row_base_time || !cb->row_col_ptr)) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null batch arrays");
+  if (NC > 0 && (!cb->col_qual_off || !cb->col_val_off || !cb->qual || !cb->val))
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, "null batch arrays");
+  if (NS > 0 && (cb->series_row_ptr[0] != 0 || cb->series_row_ptr[NS] != NR))
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, "series_row_ptr does not cover the rows");
+  if (NR > 0 && (cb->row_col_ptr[0] != 0 || cb->row_col_ptr[NR] != NC))
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, "row_col_ptr does not cover the columns");
+  for (int64_t s = 0; s < NS; s++)
+    if (cb->series_row_ptr[s + 1] < cb->series_row_ptr[s]) return fail(TSDB_E_ILLEGAL_ARGUMENT, "series_row_ptr not monotonic");
+  for (int64_t r = 0; r < NR; r++)
+    if (cb->row_col_ptr[r + 1] < cb->row_col_ptr[r]) return fail(TSDB_E_ILLEGAL_ARGUMENT, "row_col_ptr not monotonic");
+  if (NC > 0 && (cb->col_qual_off[0] != 0 || cb->col_val_off[0] != 0))
+    return fail(TSDB_E_ILLEGAL_ARGUMENT, "column offsets must start at 0");
+  for (int64_t k = 0; k < NC; k++)
+    if (cb->col_qual_off[k + 1] < cb->col_qual_off[k] || cb->col_val_off[k + 1] < cb->col_val_off[k])
+      return fail(TSDB_E_ILLEGAL_ARGUMENT, "column offsets not monotonic");
+  if (NC >= ((int64_t)1 << 31) || NR >= ((int64_t)1 << 31))
+    return fail(TSDB_E_NOT_IMPLEMENTED, "more than 2^31 columns or rows in one compaction batch");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  release_batch(c);
+  const uint64_t qb = NC ? cb->col_qual_off[NC] : 0, vb = NC ? cb->col_val_off[NC] : 0;
+  // device copies of the scan and per-column / per-row scratch (freed at the end)
+  DevBuf d_rcp, d_cqo, d_cvo, d_cts, d_q, d_v, d_crow, d_cn, d_coff, d_cinfo, d_rheap, d_rone, d_rerr;
+  DevBuf d_key, d_key2, d_idx, d_idx2, d_ecol, d_eqo, d_evo, d_klen, d_sq, d_sv, d_sc, d_sm;
+  DevBuf d_rlo, d_rq, d_rv, d_rstate, d_rmeta, d_rdq, d_rdv;
+  auto release_all = [&]() {
+    for (DevBuf* b : {&d_rcp, &d_cqo, &d_cvo, &d_cts, &d_q, &d_v, &d_crow, &d_cn, &d_coff, &d_cinfo, &d_rheap, &d_rone,
+                      &d_rerr, &d_key, &d_key2, &d_idx, &d_idx2, &d_ecol, &d_eqo, &d_evo, &d_klen, &d_sq, &d_sv,
+                      &d_sc, &d_sm, &d_rlo, &d_rq, &d_rv, &d_rstate, &d_rmeta, &d_rdq, &d_rdv})
+      b->release();
+  };
+  struct Rel { std::function<void()> f; ~Rel() { f(); } } rel{release_all};
+  const int64_t R1 = std::max<int64_t>(1, NR), C1 = std::max<int64_t>(1, NC);
+  HIP_OK(d_rcp.ensure((NR + 1) * 8));
+  HIP_OK(d_cqo.ensure((NC + 1) * 8));
+  HIP_OK(d_cvo.ensure((NC + 1) * 8));
+  HIP_OK(d_q.ensure(std::max<uint64_t>(16, qb)));
+  HIP_OK(d_v.ensure(std::max<uint64_t>(16, vb)));
+  if (cb->col_timestamp) HIP_OK(d_cts.ensure(C1 * 8));
+  if (NR) HIP_OK(hipMemcpyAsync(d_rcp.p, cb->row_col_ptr, (NR + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  if (NC) {
+    HIP_OK(hipMemcpyAsync(d_cqo.p, cb->col_qual_off, (NC + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(d_cvo.p, cb->col_val_off, (NC + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    if (qb) HIP_OK(hipMemcpyAsync(d_q.p, cb->qual, qb, hipMemcpyHostToDevice, c->stream));
+    if (vb) HIP_OK(hipMemcpyAsync(d_v.p, cb->val, vb, hipMemcpyHostToDevice, c->stream));
+    if (cb->col_timestamp) HIP_OK(hipMemcpyAsync(d_cts.p, cb->col_timestamp, NC * 8, hipMemcpyHostToDevice, c->stream));
+  }
+  HIP_OK(d_crow.ensure(C1 * 4));
+  HIP_OK(d_cn.ensure(C1 * 8));
+  HIP_OK(d_coff.ensure((C1 + 1) * 8));
+  HIP_OK(d_cinfo.ensure(C1 * 4));
+  HIP_OK(d_rheap.ensure(R1 * 4));
+  HIP_OK(d_rone.ensure(R1 * 8));
+  HIP_OK(d_rerr.ensure(R1 * 4));
+  HIP_OK(hipMemsetAsync(d_rheap.p, 0, R1 * 4, c->stream));
+  HIP_OK(hipMemsetAsync(d_rone.p, 0, R1 * 8, c->stream));
+  HIP_OK(hipMemsetAsync(d_rerr.p, 0, R1 * 4, c->stream));
+  CmpParams p{};
+  p.n_rows = NR;
+  p.n_cols = NC;
+  p.row_col_ptr = d_rcp.as<int64_t>();
+  p.col_qo = d_cqo.as<uint64_t>();
+  p.col_vo = d_cvo.as<uint64_t>();
+  p.col_ts = cb->col_timestamp ? d_cts.as<int64_t>() : nullptr;
+  p.q = d_q.as<uint8_t>();
+  p.v = d_v.as<uint8_t>();
+  p.fix_dup = cb->fix_duplicates ? 1 : 0;
+  p.col_row = d_crow.as<int32_t>();
+  p.col_n = d_cn.as<int64_t>();
+  p.col_off = d_coff.as<int64_t>();
+  p.col_info = d_cinfo.as<uint32_t>();
+  p.row_heap = d_rheap.as<int32_t>();
+  p.row_one = d_rone.as<int64_t>();
+  p.row_err = d_rerr.as<int32_t>();
+  HIP_OK(hipEventRecord(c->ev[0], c->stream));
+  HIP_OK(cmp_analyze(p, &c->cmp_tmp, &c->cmp_tmp_bytes, c->stream));
+  int64_t n_ent = 0;
+  HIP_OK(hipMemcpyAsync(&n_ent, p.col_off + NC, 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  if (n_ent >= ((int64_t)1 << 31)) return fail(TSDB_E_NOT_IMPLEMENTED, "more than 2^31 datapoints in one compaction batch");
+  const int64_t E1 = std::max<int64_t>(1, n_ent);
+  p.n_ent = n_ent;
+  HIP_OK(d_key.ensure(E1 * 8));
+  HIP_OK(d_key2.ensure(E1 * 8));
+  HIP_OK(d_idx.ensure(E1 * 4));
+  HIP_OK(d_idx2.ensure(E1 * 4));
+  HIP_OK(d_ecol.ensure(E1 * 4));
+  HIP_OK(d_eqo.ensure(E1 * 4));
+  HIP_OK(d_evo.ensure(E1 * 4));
+  HIP_OK(d_klen.ensure(E1 * 4));
+  for (DevBuf* b : {&d_sq, &d_sv, &d_sc, &d_sm}) HIP_OK(b->ensure((E1 + 1) * 8));
+  HIP_OK(d_rlo.ensure(R1 * 8));
+  HIP_OK(d_rq.ensure(R1 * 8));
+  HIP_OK(d_rv.ensure(R1 * 8));
+  HIP_OK(d_rstate.ensure(R1 * 4));
+  HIP_OK(d_rmeta.ensure(R1));
+  p.key = d_key.as<uint64_t>();
+  p.key2 = d_key2.as<uint64_t>();
+  p.idx = d_idx.as<uint32_t>();
+  p.idx2 = d_idx2.as<uint32_t>();
+  p.ent_col = d_ecol.as<uint32_t>();
+  p.ent_qo = d_eqo.as<uint32_t>();
+  p.ent_vo = d_evo.as<uint32_t>();
+  p.klen = d_klen.as<uint32_t>();
+  p.sq = d_sq.as<int64_t>();
+  p.sv = d_sv.as<int64_t>();
+  p.sc = d_sc.as<int64_t>();
+  p.sm = d_sm.as<int64_t>();
+  p.row_lo = d_rlo.as<int64_t>();
+  p.row_q = d_rq.as<int64_t>();
+  p.row_v = d_rv.as<int64_t>();
+  p.row_state = d_rstate.as<int32_t>();
+  p.row_meta = d_rmeta.as<uint8_t>();
+  int rb = 1;
+  while (((int64_t)1 << rb) <= NR) rb++;
+  HIP_OK(cmp_entries(p, &c->cmp_tmp, &c->cmp_tmp_bytes, std::min(64, 22 + rb), c->stream));
+  std::vector<int64_t> rq(R1), rv(R1);
+  std::vector<int32_t> rstate(R1), rerr(R1);
+  if (NR) {
+    HIP_OK(hipMemcpyAsync(rq.data(), p.row_q, NR * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipMemcpyAsync(rv.data(), p.row_v, NR * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipMemcpyAsync(rstate.data(), p.row_state, NR * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipMemcpyAsync(rerr.data(), p.row_err, NR * 4, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_OK(hipStreamSynchronize(c->stream));
+  // resident layout: series stable-sorted by group, each series' kept rows by base time
+  std::vector<int64_t> order(NS);
+  int32_t maxg = -1;
+  for (int64_t s = 0; s < NS; s++) { order[s] = s; maxg = std::max(maxg, cb->group_id[s]); }
+  auto gkey = [&](int64_t s) { const int32_t g = cb->group_id[s]; return g < 0 ? INT32_MAX : g; };
+  std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return gkey(x) < gkey(y); });
+  std::vector<tsdbhip_ctx::CmpErr> errs;
+  std::vector<int64_t> rdq(R1, -1), rdv(R1, -1), srp(NS + 1, 0);
+  std::vector<RowDesc> rd;
+  std::vector<int32_t> hgroup(NS);
+  uint64_t qtot = 0, vtot = 0;
+  for (int64_t i = 0; i < NS; i++) {
+    const int64_t s = order[i];
+    hgroup[i] = cb->group_id[s] < 0 ? maxg + 1 : cb->group_id[s];
+    std::vector<int64_t> rows;
+    for (int64_t r = cb->series_row_ptr[s]; r < cb->series_row_ptr[s + 1]; r++) {
+      if (rerr[r]) errs.push_back({s, r, (int64_t)cb->row_base_time[r], rerr[r]});
+      else if (rstate[r] != 0) rows.push_back(r);
+    }
+    std::stable_sort(rows.begin(), rows.end(), [&](int64_t x, int64_t y) { return cb->row_base_time[x] < cb->row_base_time[y]; });
+    for (size_t k = 1; k < rows.size(); k++)
+      if (cb->row_base_time[rows[k]] == cb->row_base_time[rows[k - 1]])
+        return fail(TSDB_E_NOT_IMPLEMENTED, "two rows of one series with the same base time (salt buckets): load compacted cells with tsdbhip_load");
+    for (int64_t r : rows) {
+      RowDesc d{};
+      d.base = cb->row_base_time[r];
+      if (rq[r] > 0xFFFFFFFFLL || rv[r] > 0xFFFFFFFFLL) return fail(TSDB_E_ILLEGAL_ARGUMENT, "row too large");
+      d.qlen = (uint32_t)rq[r];
+      d.vlen = (uint32_t)rv[r];
+      d.qoff = qtot;
+      d.voff = vtot;
+      rdq[r] = (int64_t)qtot;
+      rdv[r] = (int64_t)vtot;
+      qtot += align16(rq[r]);
+      vtot += align16(rv[r]);
+      if (rd.size() == (size_t)srp[i]) d.flags |= ROW_SFIRST;
+      rd.push_back(d);
+    }
+    srp[i + 1] = (int64_t)rd.size();
+  }
+  std::sort(errs.begin(), errs.end(), [](const tsdbhip_ctx::CmpErr& a, const tsdbhip_ctx::CmpErr& b) {
+    return a.series != b.series ? a.series < b.series : a.row < b.row;
+  });
+  // the compacted cells, written in place
+  HIP_OK(c->qual.ensure(qtot + BLOB_SLACK));
+  HIP_OK(c->val.ensure(vtot + BLOB_SLACK));
+  HIP_OK(hipMemsetAsync(c->qual.p, 0, qtot + BLOB_SLACK, c->stream));
+  HIP_OK(hipMemsetAsync(c->val.p, 0, vtot + BLOB_SLACK, c->stream));
+  HIP_OK(d_rdq.ensure(R1 * 8));
+  HIP_OK(d_rdv.ensure(R1 * 8));
+  if (NR) {
+    HIP_OK(hipMemcpyAsync(d_rdq.p, rdq.data(), NR * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(d_rdv.p, rdv.data(), NR * 8, hipMemcpyHostToDevice, c->stream));
+  }
+  p.row_dq = d_rdq.as<int64_t>();
+  p.row_dv = d_rdv.as<int64_t>();
+  p.out_q = c->qual.as<uint8_t>();
+  p.out_v = c->val.as<uint8_t>();
+  HIP_OK(cmp_write(p, c->stream));
+  HIP_OK(hipEventRecord(c->ev[1], c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  float cmp_ms = 0;
+  (void)hipEventElapsedTime(&cmp_ms, c->ev[0], c->ev[1]);
+  // resident batch state (as load_impl)
+  c->n_series = NS;
+  c->n_groups = maxg + 1;
+  c->h_group = hgroup;
+  c->h_orig = order;
+  c->h_srp = srp;
+  c->n_rows = (int64_t)rd.size();
+  c->qual_bytes = qtot;
+  c->val_bytes = vtot;
+  HIP_OK(c->rows.ensure(std::max<size_t>(1, rd.size()) * sizeof(RowDesc)));
+  HIP_OK(c->srp.ensure((NS + 1) * 8));
+  HIP_OK(c->gid.ensure(std::max<int64_t>(1, NS) * 4));
+  if (!rd.empty()) HIP_OK(hipMemcpy(c->rows.p, rd.data(), rd.size() * sizeof(RowDesc), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(c->srp.p, srp.data(), (NS + 1) * 8, hipMemcpyHostToDevice));
+  if (NS) HIP_OK(hipMemcpy(c->gid.p, hgroup.data(), NS * 4, hipMemcpyHostToDevice));
+  const int rc = finish_load(c, rd);
+  c->cmp_errs = std::move(errs);
+  c->compact_ms = cmp_ms;
+  return rc;
+}
+
 // ---- sharding a host batch over ranks ----------------------------------------
 namespace {
 
@@ -1749,6 +1978,19 @@ int scan_bounds_of(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t& ss, int64_t&
   return tsdbhip_scan_bounds(q, &ss, &se);
 }
 
+// A row whose query-time compaction failed fails every query whose scan covers it
+// (SaltScanner.processRow :825-830 closes the scanner with the exception), in scan order.
+int cmp_scan_check(tsdbhip_ctx* c, const Plan& P) {
+  for (const auto& e : c->cmp_errs)
+    if (e.base >= P.ss && e.base < P.se)
+      return fail(e.code, e.code == TSDB_E_NOT_IMPLEMENTED
+                              ? "query-time compaction of a row this engine does not restate (a compacted cell out of "
+                                "time order, or a datapoint column without a value)"
+                              : "IllegalDataException in the query-time compaction of a row (duplicate timestamp with a "
+                                "different value, or a corrupted cell)");
+  return 0;
+}
+
 int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
   if (q->aggregator < 0 || q->aggregator >= TSDB_AGG_COUNT_ALL) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad aggregator");
   if (q->ds_function >= TSDB_AGG_COUNT_ALL) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad downsampling function");
@@ -1764,7 +2006,7 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
     P.interp = interp_of(q->aggregator);
     P.none = q->aggregator == TSDB_AGG_NONE;
     { const int brc = scan_bounds_of(c, q, P.ss, P.se); if (brc) return brc; }
-    return 0;
+    return cmp_scan_check(c, P);
   }
   if (!q->ds_all && q->ds_interval_ms <= 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "interval not > 0");
   int64_t calW = 0, calO = 0, calM = 0;
@@ -1871,7 +2113,7 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
     return fail(TSDB_E_NOT_IMPLEMENTED, "percentile downsampling over variable-width calendar slots");
   // slot arrays live in LDS when they fit next to 4 waves' worth of staging, else in HBM
   P.gslot = grid_wave_lds(P.K, q->rate != 0, false) > 40 * 1024;
-  return 0;
+  return cmp_scan_check(c, P);
 }
 
 // Largest number of datapoints one series holds in rows with base in [ss, se) (cached per

@@ -306,6 +306,57 @@ struct RollupAggParams {
 };
 hipError_t launch_rollup_agg(const GridParams& p, const RollupAggParams& rp, hipStream_t s);
 // each series' first datapoint >= t0 in rows with base in [ss, se) (INT64_MAX: none)
+// ---- query-time compaction (k_compact.hip) ----------------------------
+enum : uint32_t { CMP_IGNORE = 0, CMP_DATA = 1, CMP_APPEND = 2 };
+struct CmpParams {
+  // input: the scanner's rows, every column (KeyValue) of a row in scan order
+  int64_t n_rows, n_cols;
+  const int64_t* row_col_ptr;   // [n_rows + 1]
+  const uint64_t* col_qo;       // [n_cols + 1] qualifier bytes of each column
+  const uint64_t* col_vo;       // [n_cols + 1] value bytes
+  const int64_t* col_ts;        // [n_cols] KeyValue timestamps, or null (all equal)
+  const uint8_t* q;
+  const uint8_t* v;
+  int32_t fix_dup;
+  // per column
+  int32_t* col_row;             // [n_cols]
+  int64_t* col_n;               // [n_cols] datapoints the column contributes
+  int64_t* col_off;             // [n_cols + 1] their first entry
+  uint32_t* col_info;           // kind | 4: value starts 4 bytes in | 8: fixed up | fixed flags byte << 8
+  // per row
+  int32_t* row_heap;            // columns in the compaction heap
+  int64_t* row_one;             // one of them (the only one when row_heap == 1)
+  int32_t* row_err;             // first error: TSDB_E_ILLEGAL_DATA or TSDB_E_NOT_IMPLEMENTED
+  // entries (one per datapoint of every column)
+  int64_t n_ent;
+  uint64_t* key;                // [n_ent] row << 22 | offset (ms), then sorted
+  uint64_t* key2;
+  uint32_t* idx;                // [n_ent] entry ordinal, sorted along
+  uint32_t* idx2;
+  uint32_t* ent_col;            // [n_ent] (by ordinal)
+  uint32_t* ent_qo;             // qualifier position inside the column (append: inside its value)
+  uint32_t* ent_vo;             // value position inside the column value
+  uint32_t* klen;               // [n_ent] by sorted position: kept | ms << 1 | qlen << 2 | vlen << 8
+  int64_t* sq;                  // [n_ent + 1] exclusive sums over sorted positions of kept qualifier bytes
+  int64_t* sv;                  //   ... value bytes
+  int64_t* sc;                  //   ... kept datapoints
+  int64_t* sm;                  //   ... kept millisecond datapoints
+  // per row results
+  int64_t* row_lo;              // first sorted position of the row
+  int64_t* row_q;               // compacted qualifier bytes
+  int64_t* row_v;               // compacted value bytes (incl. the meta byte)
+  int32_t* row_state;           // 0: no cell (compacted == null, or an error), 1: merged, 2: the column as stored
+  uint8_t* row_meta;
+  // output
+  const int64_t* row_dq;        // [n_rows] destination of the row's qualifiers (-1: none)
+  const int64_t* row_dv;
+  uint8_t* out_q;
+  uint8_t* out_v;
+};
+hipError_t cmp_analyze(CmpParams& p, void** tmp, size_t* tmp_bytes, hipStream_t s);   // through k_cmp_cols, col_off
+hipError_t cmp_entries(CmpParams& p, void** tmp, size_t* tmp_bytes, int end_bit, hipStream_t s);   // explode, sort, dedup, scans, rows
+hipError_t cmp_write(const CmpParams& p, hipStream_t s);
+
 // rollup read path: value series buckets <- Σsum / Σcount (avg) or Σcount, from the SUM
 // downsampling of each value series and of its count series (cmap[s], -1: none)
 hipError_t launch_rollup_combine(double* dense, const uint8_t* pres, const int64_t* cmap, int64_t n_series, int64_t K,

@@ -1,0 +1,388 @@
+// Query-time compaction: what TSDB.compact(row) does to every row a
+// query scans (SaltScanner.processRow :802-830 -> CompactionQueue.Compaction.compact
+// :330-385), for every row at once.  The reference's per-row heap merge of column iterators
+// (defaultMergeDataPoints :512-545 over ColumnDatapointIterator :63-205) becomes:
+//   k_cmp_cols     one thread per column: its kind (datapoints / append / ignored), the 2-byte
+//                  fixups (Internal.fixFloatingPointValue / fixQualifierFlags :535-591) and its
+//                  datapoint count; errors recorded per row
+//   k_cmp_explode  one thread per column: an entry per datapoint, keyed row << 22 | offset ms
+//   radix sort     (stable: equal keys keep scan order -- column, then position)
+//   k_cmp_dedup    one thread per run of equal keys: the heap's order at one offset is newest
+//                  column first, so the kept datapoint is the newest column's; the others must
+//                  hold the same bytes unless fix_duplicates (IllegalDataException); a later
+//                  pair of the same append column replaces an earlier one
+//                  (AppendDataPoints.parseKeyValue :110-240)
+//   scans          kept qualifier / value bytes, kept and millisecond datapoints
+//   k_cmp_rows     one thread per row: its compacted size and meta byte (buildCompactedColumn
+//                  :547-566), or the single column as stored (noMergesOrFixups :311-328)
+//   k_cmp_write    one thread per kept datapoint: its bytes at the row's destination
+//   k_cmp_rowfix   one thread per row: stored single columns and meta bytes.
+// The heap merge equals the sorted merge when every column's datapoints are in time order,
+// which compactions write; a compacted column out of order is reported NOT_IMPLEMENTED.
+#include "kcommon.h"
+
+#include <hipcub/hipcub.hpp>
+
+namespace tsdb {
+
+namespace {
+
+__device__ __forceinline__ bool cmp_in_ms(uint8_t b) { return (b & 0xF0) == 0xF0; }
+__device__ __forceinline__ uint32_t cmp_be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
+__device__ __forceinline__ uint32_t cmp_be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+// Internal.getOffsetFromQualifier in ms (< 2^22 for both widths)
+__device__ __forceinline__ uint32_t cmp_off(const uint8_t* q, int eq) {
+  return eq == 4 ? ((cmp_be32(q) & 0x0FFFFFC0u) >> 6) : (cmp_be16(q) >> 4) * 1000u;
+}
+__device__ __forceinline__ void cmp_fail(int32_t* row_err, int64_t row, int32_t code) {
+  atomicCAS(&row_err[row], 0, code);
+}
+
+__global__ __launch_bounds__(256) void k_cmp_colrow(CmpParams p) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n_rows) return;
+  for (int64_t c = p.row_col_ptr[r]; c < p.row_col_ptr[r + 1]; c++) p.col_row[c] = (int32_t)r;
+}
+
+// Walk of a datapoint column (ColumnDatapointIterator.update / advance), shared by the count
+// and the explode passes.  Returns false on a malformed column.
+template <class F>
+__device__ __forceinline__ bool walk_data(const uint8_t* q, int64_t ql, int64_t vlen, uint8_t fixed_flags, F&& f) {
+  int64_t qi = 0, vi = 0;
+  while (qi < ql && vi < vlen) {
+    const int eq = cmp_in_ms(q[qi]) ? 4 : 2;
+    if (qi + eq > ql) return false;                       // ArrayIndexOutOfBounds
+    const uint8_t fl = ql == 2 ? fixed_flags : q[qi + eq - 1];
+    const int evl = (fl & 7) + 1;
+    if (vi + evl > vlen) return false;                    // value shorter than its qualifiers
+    f(qi, vi, eq, evl, cmp_off(q + qi, eq));
+    qi += eq;
+    vi += evl;
+  }
+  return true;
+}
+template <class F>
+__device__ __forceinline__ bool walk_append(const uint8_t* v, int64_t vl, F&& f) {
+  int64_t idx = 0;
+  while (idx < vl) {
+    const int eq = cmp_in_ms(v[idx]) ? 4 : 2;
+    if (idx + eq > vl) return false;
+    const int evl = (v[idx + eq - 1] & 7) + 1;
+    if (idx + eq + evl > vl) return false;
+    f(idx, idx + eq, eq, evl, cmp_off(v + idx, eq));
+    idx += eq + evl;
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(256) void k_cmp_cols(CmpParams p) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= p.n_cols) return;
+  const int64_t row = p.col_row[c];
+  const uint64_t qo = p.col_qo[c], vo = p.col_vo[c];
+  const int64_t ql = (int64_t)(p.col_qo[c + 1] - qo), vl = (int64_t)(p.col_vo[c + 1] - vo);
+  const uint8_t* q = p.q + qo;
+  const uint8_t* v = p.v + vo;
+  uint32_t kind = CMP_IGNORE, info = 0;
+  int64_t n = 0;
+  int32_t err = 0;
+  bool heap = false;
+  if (ql & 1) {
+    if (ql == 3 && q[0] == 0x05) {   // AppendDataPoints.APPEND_COLUMN_PREFIX
+      kind = CMP_APPEND;
+      if (!walk_append(v, vl, [&](int64_t, int64_t, int, int, uint32_t) { n++; })) err = TSDB_E_ILLEGAL_DATA;
+      heap = n > 0;
+    }
+    // annotations, histograms, other prefixes: not datapoints
+  } else if (ql > 0) {
+    kind = CMP_DATA;
+    heap = true;
+    int64_t vstart = 0, vlen = vl;
+    uint8_t ff = 0;
+    bool fixed = false;
+    if (ql == 2) {   // ColumnDatapointIterator.checkForFixup :74-89
+      const uint8_t q1 = q[1];
+      if ((q1 & 8) && (q1 & 7) == 3 && vl == 8) {
+        if (v[0] | v[1] | v[2] | v[3]) err = TSDB_E_ILLEGAL_DATA;   // "first 4 bytes are expected to be zeros"
+        vstart = 4;
+        vlen = 4;
+        fixed = true;
+      }
+      ff = (uint8_t)((q1 & ~7) | (uint8_t)(vlen - 1));
+      if (ff != q1) fixed = true;
+    }
+    if (vlen == 0) err = TSDB_E_NOT_IMPLEMENTED;   // a datapoint column without a value
+    uint32_t prev = 0;
+    bool sorted = true;
+    if (!err && !walk_data(q, ql, vlen, ff, [&](int64_t, int64_t, int, int, uint32_t t) {
+          if (n > 0 && t < prev) sorted = false;
+          prev = t;
+          n++;
+        }))
+      err = TSDB_E_ILLEGAL_DATA;
+    if (!err && !sorted) err = TSDB_E_NOT_IMPLEMENTED;   // a compacted column out of time order
+    info = (vstart ? 4u : 0u) | (fixed ? 8u : 0u) | ((uint32_t)ff << 8);
+  }
+  if (err) {
+    cmp_fail(p.row_err, row, err);
+    n = 0;
+  }
+  p.col_n[c] = n;
+  p.col_info[c] = kind | info;
+  if (heap) {
+    atomicAdd(&p.row_heap[row], 1);
+    atomicMax((unsigned long long*)&p.row_one[row], (unsigned long long)c);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_cmp_explode(CmpParams p) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= p.n_cols || p.col_n[c] == 0) return;
+  const uint64_t row = (uint64_t)p.col_row[c];
+  const uint64_t qo = p.col_qo[c], vo = p.col_vo[c];
+  const int64_t ql = (int64_t)(p.col_qo[c + 1] - qo), vl = (int64_t)(p.col_vo[c + 1] - vo);
+  const uint32_t info = p.col_info[c];
+  int64_t e = p.col_off[c];
+  auto put = [&](int64_t qpos, int64_t vpos, int, int, uint32_t t) {
+    p.key[e] = (row << 22) | t;
+    p.idx[e] = (uint32_t)e;
+    p.ent_col[e] = (uint32_t)c;
+    p.ent_qo[e] = (uint32_t)qpos;
+    p.ent_vo[e] = (uint32_t)vpos;
+    e++;
+  };
+  if ((info & 3) == CMP_APPEND) {
+    walk_append(p.v + vo, vl, put);
+  } else {
+    const int64_t vstart = (info & 4) ? 4 : 0;
+    walk_data(p.q + qo, ql, vl - vstart, (uint8_t)(info >> 8),
+              [&](int64_t qi, int64_t vi, int eq, int evl, uint32_t t) { put(qi, vstart + vi, eq, evl, t); });
+  }
+}
+
+// qualifier / value of entry e: pointers and lengths (fixups applied)
+struct CmpEnt {
+  const uint8_t* qp;
+  const uint8_t* vp;
+  int eq, evl;
+  uint8_t fixed_q1;   // the replacement second qualifier byte (2-byte fixed columns), else 0
+  bool fix;
+};
+__device__ __forceinline__ CmpEnt cmp_ent(const CmpParams& p, uint32_t e) {
+  CmpEnt r;
+  const uint32_t c = p.ent_col[e];
+  const uint32_t info = p.col_info[c];
+  const uint8_t* vb = p.v + p.col_vo[c];
+  const int64_t ql = (int64_t)(p.col_qo[c + 1] - p.col_qo[c]);
+  r.fix = false;
+  r.fixed_q1 = 0;
+  if ((info & 3) == CMP_APPEND) {
+    r.qp = vb + p.ent_qo[e];
+  } else {
+    r.qp = p.q + p.col_qo[c] + p.ent_qo[e];
+    if (ql == 2 && (info & 8)) { r.fix = true; r.fixed_q1 = (uint8_t)(info >> 8); }
+  }
+  r.eq = cmp_in_ms(r.qp[0]) ? 4 : 2;
+  const uint8_t fl = r.fix ? r.fixed_q1 : r.qp[r.eq - 1];
+  r.evl = (fl & 7) + 1;
+  r.vp = vb + p.ent_vo[e];
+  return r;
+}
+
+__global__ __launch_bounds__(256) void k_cmp_dedup(CmpParams p) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n_ent) return;
+  const uint64_t k = p.key2[i];
+  if (i > 0 && p.key2[i - 1] == k) return;   // not the first of its run
+  int64_t j = i + 1;
+  while (j < p.n_ent && p.key2[j] == k) j++;
+  const int64_t row = (int64_t)(k >> 22);
+  // a pair an append column repeats later is replaced (TreeMap.put); the newest column wins
+  auto superseded = [&](int64_t t) {
+    const uint32_t c = p.ent_col[p.idx2[t]];
+    return (p.col_info[c] & 3) == CMP_APPEND && t + 1 < j && p.ent_col[p.idx2[t + 1]] == c;
+  };
+  int64_t best = -1;
+  int64_t best_ts = 0;
+  for (int64_t t = i; t < j; t++) {
+    if (superseded(t)) continue;
+    const uint32_t c = p.ent_col[p.idx2[t]];
+    const int64_t ts = p.col_ts ? p.col_ts[c] : 0;
+    if (best < 0 || ts > best_ts) { best = t; best_ts = ts; }
+  }
+  const CmpEnt kb = cmp_ent(p, p.idx2[best]);
+  for (int64_t t = i; t < j; t++) {
+    if (t == best) {
+      p.klen[t] = 1u | ((kb.eq == 4 ? 1u : 0u) << 1) | ((uint32_t)kb.eq << 2) | ((uint32_t)kb.evl << 8);
+      continue;
+    }
+    p.klen[t] = 0;
+    if (superseded(t) || p.fix_dup) continue;
+    const CmpEnt o = cmp_ent(p, p.idx2[t]);   // getCopyOfCurrentValue vs the kept segment
+    bool same = o.evl == kb.evl;
+    for (int b = 0; same && b < o.evl; b++) same = o.vp[b] == kb.vp[b];
+    if (!same) cmp_fail(p.row_err, row, TSDB_E_ILLEGAL_DATA);
+  }
+}
+
+struct KeptField {
+  int f;
+  __host__ __device__ int64_t operator()(uint32_t x) const {
+    return f == 0 ? (int64_t)((x >> 2) & 7) * (x & 1) : f == 1 ? (int64_t)(x >> 8) * (x & 1)
+                  : f == 2 ? (int64_t)(x & 1) : (int64_t)((x >> 1) & 1);
+  }
+};
+
+__device__ __forceinline__ int64_t lower_bound_u64(const uint64_t* a, int64_t n, uint64_t x) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (a[m] < x) lo = m + 1;
+    else hi = m;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void k_cmp_rows(CmpParams p) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n_rows) return;
+  const int64_t lo = lower_bound_u64(p.key2, p.n_ent, (uint64_t)r << 22);
+  const int64_t hi = lower_bound_u64(p.key2, p.n_ent, (uint64_t)(r + 1) << 22);
+  p.row_lo[r] = lo;
+  p.row_meta[r] = 0;
+  p.row_q[r] = p.row_v[r] = 0;
+  if (p.row_err[r] || p.row_heap[r] == 0) { p.row_state[r] = 0; return; }
+  if (p.row_heap[r] == 1) {   // noMergesOrFixups: one 2-byte or one 4-byte ms column, no fixup
+    const int64_t c = p.row_one[r];
+    const uint32_t info = p.col_info[c];
+    const int64_t ql = (int64_t)(p.col_qo[c + 1] - p.col_qo[c]);
+    if ((info & 3) == CMP_DATA && !(info & 8) && (ql == 2 || (ql == 4 && cmp_in_ms(p.q[p.col_qo[c]])))) {
+      p.row_state[r] = 2;
+      p.row_q[r] = ql;
+      p.row_v[r] = (int64_t)(p.col_vo[c + 1] - p.col_vo[c]);
+      return;
+    }
+  }
+  const int64_t cnt = p.sc[hi] - p.sc[lo];
+  if (cnt == 0) { p.row_state[r] = 0; return; }
+  const int64_t ms = p.sm[hi] - p.sm[lo];
+  p.row_state[r] = 1;
+  p.row_q[r] = p.sq[hi] - p.sq[lo];
+  p.row_v[r] = p.sv[hi] - p.sv[lo] + (cnt > 1 ? 1 : 0);
+  p.row_meta[r] = (ms > 0 && ms < cnt) ? 1 : 0;   // Const.MS_MIXED_COMPACT
+}
+
+__global__ __launch_bounds__(256) void k_cmp_write(CmpParams p) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n_ent || !(p.klen[i] & 1)) return;
+  const int64_t r = (int64_t)(p.key2[i] >> 22);
+  if (p.row_state[r] != 1 || p.row_dq[r] < 0) return;
+  const int64_t lo = p.row_lo[r];
+  const int64_t dq = p.row_dq[r] + (p.sq[i] - p.sq[lo]);
+  const int64_t dv = p.row_dv[r] + (p.sv[i] - p.sv[lo]);
+  const CmpEnt e = cmp_ent(p, p.idx2[i]);
+  for (int b = 0; b < e.eq; b++) p.out_q[dq + b] = (e.fix && b == 1) ? e.fixed_q1 : e.qp[b];
+  for (int b = 0; b < e.evl; b++) p.out_v[dv + b] = e.vp[b];
+}
+
+__global__ __launch_bounds__(256) void k_cmp_rowfix(CmpParams p) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.n_rows || p.row_dq[r] < 0) return;
+  if (p.row_state[r] == 2) {
+    const int64_t c = p.row_one[r];
+    const uint8_t* qs = p.q + p.col_qo[c];
+    const uint8_t* vs = p.v + p.col_vo[c];
+    for (int64_t b = 0; b < p.row_q[r]; b++) p.out_q[p.row_dq[r] + b] = qs[b];
+    for (int64_t b = 0; b < p.row_v[r]; b++) p.out_v[p.row_dv[r] + b] = vs[b];
+  } else if (p.row_state[r] == 1) {
+    const int64_t lo = p.row_lo[r];
+    const int64_t hi = lower_bound_u64(p.key2, p.n_ent, (uint64_t)(r + 1) << 22);
+    if (p.sc[hi] - p.sc[lo] > 1) p.out_v[p.row_dv[r] + p.row_v[r] - 1] = p.row_meta[r];
+  }
+}
+
+inline unsigned blocks_of(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + 255) / 256); }
+
+// exclusive scan into out[0 .. n] (n + 1 values) of f(klen[i])
+hipError_t scan_field(const CmpParams& p, int f, int64_t* out, void* tmp, size_t& bytes, hipStream_t s) {
+  hipcub::TransformInputIterator<int64_t, KeptField, const uint32_t*> in(p.klen, KeptField{f});
+  if (!tmp) return hipcub::DeviceScan::InclusiveSum(nullptr, bytes, in, out + 1, (int)p.n_ent, s);
+  hipError_t e = hipMemsetAsync(out, 0, 8, s);
+  if (e != hipSuccess) return e;
+  if (p.n_ent == 0) return hipSuccess;
+  return hipcub::DeviceScan::InclusiveSum(tmp, bytes, in, out + 1, (int)p.n_ent, s);
+}
+
+}  // namespace
+
+hipError_t cmp_analyze(CmpParams& p, void** tmp, size_t* tmp_bytes, hipStream_t s) {
+  if (p.n_rows > 0) hipLaunchKernelGGL(k_cmp_colrow, dim3(blocks_of(p.n_rows)), dim3(256), 0, s, p);
+  if (p.n_cols > 0) hipLaunchKernelGGL(k_cmp_cols, dim3(blocks_of(p.n_cols)), dim3(256), 0, s, p);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  // col_off = exclusive sum of col_n (n_cols + 1 values)
+  size_t need = 0;
+  e = hipcub::DeviceScan::InclusiveSum(nullptr, need, p.col_n, p.col_off + 1, (int)std::max<int64_t>(1, p.n_cols), s);
+  if (e != hipSuccess) return e;
+  if (need > *tmp_bytes) {
+    if (*tmp) (void)hipFree(*tmp);
+    *tmp = nullptr;
+    *tmp_bytes = 0;
+    e = hipMalloc(tmp, need);
+    if (e != hipSuccess) return e;
+    *tmp_bytes = need;
+  }
+  e = hipMemsetAsync(p.col_off, 0, 8, s);
+  if (e != hipSuccess || p.n_cols == 0) return e;
+  size_t b = *tmp_bytes;
+  return hipcub::DeviceScan::InclusiveSum(*tmp, b, p.col_n, p.col_off + 1, (int)p.n_cols, s);
+}
+
+hipError_t cmp_entries(CmpParams& p, void** tmp, size_t* tmp_bytes, int end_bit, hipStream_t s) {
+  hipError_t e;
+  if (p.n_ent > 0) {
+    hipLaunchKernelGGL(k_cmp_explode, dim3(blocks_of(p.n_cols)), dim3(256), 0, s, p);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  size_t need = 0, b = 0;
+  e = hipcub::DeviceRadixSort::SortPairs(nullptr, b, p.key, p.key2, p.idx, p.idx2, (int)std::max<int64_t>(1, p.n_ent), 0,
+                                         end_bit, s);
+  if (e != hipSuccess) return e;
+  need = b;
+  for (int f = 0; f < 4; f++) {
+    b = 0;
+    if ((e = scan_field(p, f, p.sq, nullptr, b, s)) != hipSuccess) return e;
+    need = std::max(need, b);
+  }
+  if (need > *tmp_bytes) {
+    if (*tmp) (void)hipFree(*tmp);
+    *tmp = nullptr;
+    *tmp_bytes = 0;
+    if ((e = hipMalloc(tmp, need)) != hipSuccess) return e;
+    *tmp_bytes = need;
+  }
+  if (p.n_ent > 0) {
+    b = *tmp_bytes;
+    e = hipcub::DeviceRadixSort::SortPairs(*tmp, b, p.key, p.key2, p.idx, p.idx2, (int)p.n_ent, 0, end_bit, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_cmp_dedup, dim3(blocks_of(p.n_ent)), dim3(256), 0, s, p);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  int64_t* outs[4] = {p.sq, p.sv, p.sc, p.sm};
+  for (int f = 0; f < 4; f++) {
+    b = *tmp_bytes;
+    if ((e = scan_field(p, f, outs[f], *tmp, b, s)) != hipSuccess) return e;
+  }
+  if (p.n_rows > 0) hipLaunchKernelGGL(k_cmp_rows, dim3(blocks_of(p.n_rows)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t cmp_write(const CmpParams& p, hipStream_t s) {
+  if (p.n_ent > 0) hipLaunchKernelGGL(k_cmp_write, dim3(blocks_of(p.n_ent)), dim3(256), 0, s, p);
+  if (p.n_rows > 0) hipLaunchKernelGGL(k_cmp_rowfix, dim3(blocks_of(p.n_rows)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace tsdb

@@ -28,7 +28,7 @@ EXPORTS = [
     "tsdbhip_rollup_basetime", "tsdbhip_rollup_qualifier", "tsdbhip_rollup_run", "tsdbhip_rollup_download",
     "tsdbhip_sel_layout", "tsdbhip_sel_run_values", "tsdbhip_sel_select", "tsdbhip_assemble", "tsdbhip_run_multi",
     "tsdbhip_debug_rows", "tsdbhip_shard_bounds", "tsdbhip_load_shard", "tsdbhip_synth_shard",
-    "tsdbhip_load_rollup",
+    "tsdbhip_load_rollup", "tsdbhip_load_cells",
 ]
 
 SHARD_SERIES, SHARD_GROUPS, SHARD_SPANS = 0, 1, 2   # tsdbhip.h TSDB_SHARD_*
@@ -96,6 +96,7 @@ def lib():
         L.tsdbhip_load_shard.argtypes = [vp, C.POINTER(abi.Batch), C.c_int, C.c_int64, C.c_int64]
         L.tsdbhip_synth_shard.argtypes = [vp, C.POINTER(abi.SynthSpec), C.c_int64, C.c_int64]
         L.tsdbhip_load_rollup.argtypes = [vp, C.POINTER(abi.RollupBatch)]
+        L.tsdbhip_load_cells.argtypes = [vp, C.POINTER(abi.CellBatch)]
         _lib = L
     return _lib
 
@@ -201,6 +202,11 @@ class Engine:
     def load(self, batch: abi.HostBatch):
         _check(lib().tsdbhip_load(self.ctx, C.byref(batch.c)))
         self._batch = batch
+
+    def load_cells(self, cb: abi.HostCellBatch):
+        """tsdbhip_load_cells: the scan's rows compacted on the GPU become the resident batch."""
+        _check(lib().tsdbhip_load_cells(self.ctx, C.byref(cb.c)))
+        self._batch = cb
 
     def load_rollup(self, rb: abi.HostRollupBatch):
         """tsdbhip_load_rollup: a rollup table's scan result as the resident batch; run()

@@ -1,0 +1,234 @@
+"""GPU parity of query-time compaction: tsdbhip_load_cells compacts
+the scanner's rows on the device (k_compact.hip) as CompactionQueue.Compaction.compact
+returns them to a query (src/core/CompactionQueue.java:330-566).
+
+  * every TestCompactionQueue known answer of the query path (tests/golden/compaction.json):
+    the resident row's bytes after load_cells, or the exception a covering query raises;
+  * randomized rows -- individual cells in any order, earlier compactions, append columns
+    with repeats, 2-byte float / length fixups, annotations, duplicates with equal and
+    different values, mixed s / ms -- against the oracle's compaction row by row, and the
+    queries over them against the oracle's queries over its own compaction;
+  * a 3,000-series store of one-cell-per-datapoint rows in shuffled column order."""
+from __future__ import annotations
+
+import importlib.util
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from opentsdb_amd import abi
+from opentsdb_amd.engine import EngineError
+from opentsdb_amd.store import make_batch
+from oracle import oracle as O
+from tests import golden_util as gu
+from tests.test_gpu_parity import assert_groups_match
+
+pytestmark = pytest.mark.gpu
+
+DOC = gu.load("compaction.json")
+_spec = importlib.util.spec_from_file_location("make_compaction_golden",
+                                               os.path.join(gu.GOLDEN, "make_compaction_golden.py"))
+MK = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(MK)
+B = 1356998400
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from opentsdb_amd.engine import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def rows_of(batch):
+    out = []
+    for r in range(batch.n_rows):
+        q = batch.qual[int(batch.row_qual_off[r]):int(batch.row_qual_off[r + 1])].tobytes()
+        v = batch.val[int(batch.row_val_off[r]):int(batch.row_val_off[r + 1])].tobytes()
+        out.append((int(batch.row_base_time[r]), q, v))
+    return out
+
+
+@pytest.mark.parametrize("case", DOC["cases"], ids=[c["name"] for c in DOC["cases"]])
+def test_known_answers_on_gpu(eng, case):
+    cols, expect = MK.expand_columns(case)
+    cb = abi.HostCellBatch.from_rows([[(B, [(q, v, i) for i, (q, v) in enumerate(cols)])]], [0],
+                                     case["fix_duplicates"])
+    eng.load_cells(cb)
+    got = rows_of(eng.download())
+    q = abi.new_query(B, B + 3599, "sum")
+    if expect == "IllegalDataException":
+        assert got == []
+        with pytest.raises(EngineError) as e:
+            eng.run(q)
+        assert e.value.java == "IllegalDataException"
+        # a query whose scan does not cover the row never compacts it
+        eng.run(abi.new_query(B + 7200, B + 9000, "sum"))
+        return
+    if expect is None:
+        assert got == []
+        return
+    assert got == [(B, expect[0], expect[1])]
+
+
+def _cell(off_ms, ms, value, kind):
+    """One datapoint as a cell: (qualifier, value bytes)."""
+    if kind == "long":
+        v = struct.pack(">q", value)
+        fl = 7
+    elif kind == "int":
+        v = struct.pack(">i", value)
+        fl = 3
+    elif kind == "float":
+        v = struct.pack(">f", value)
+        fl = 0xB
+    else:
+        v = struct.pack(">d", value)
+        fl = 0xF
+    if ms:
+        q = struct.pack(">I", 0xF0000000 | (off_ms << 6) | fl)
+    else:
+        q = struct.pack(">H", ((off_ms // 1000) << 4) | fl)
+    return q, v
+
+
+def random_row(rng, n, dup_p=0.05, diff_p=0.3):
+    """Columns of one row: datapoints as single cells, compacted groups and appends."""
+    offs = sorted(set(int(x) for x in rng.choice(3600, size=n, replace=False) * 1000 +
+                      np.where(rng.random(n) < 0.3, rng.integers(1, 999, n), 0)))
+    pts = []
+    for o in offs:
+        kind = ["long", "int", "float", "double"][int(rng.integers(0, 4))]
+        val = float(rng.normal(0, 100)) if kind in ("float", "double") else int(rng.integers(-1000, 1000))
+        pts.append((o, o % 1000 != 0 or rng.random() < 0.2, val, kind))
+    cells = [_cell(*p) for p in pts]
+    cols = []
+    i = 0
+    while i < len(cells):
+        r = rng.random()
+        if r < 0.15 and i + 2 < len(cells):            # an earlier compaction of a few datapoints
+            k = int(rng.integers(2, 5))
+            grp = cells[i:i + k]
+            ms = any(len(q) == 4 for q, _ in grp) and any(len(q) == 2 for q, _ in grp)
+            cols.append((b"".join(q for q, _ in grp), b"".join(v for _, v in grp) + bytes([1 if ms else 0])))
+            i += k
+        elif r < 0.25 and i + 1 < len(cells):          # an append column (pairs in any order)
+            k = int(rng.integers(1, 4))
+            grp = cells[i:i + k]
+            order = rng.permutation(len(grp))
+            cols.append((bytes([5, 0, 0]), b"".join(grp[j][0] + grp[j][1] for j in order)))
+            i += k
+        else:
+            q, v = cells[i]
+            if len(q) == 2 and q[1] & 0xF == 0xB and rng.random() < 0.3:   # float stored on 8 bytes
+                v = b"\0\0\0\0" + v
+            elif len(q) == 2 and q[1] & 0xF == 0x3 and rng.random() < 0.3:  # int flagged 4, stored on 8
+                v = struct.pack(">q", struct.unpack(">i", v)[0])
+            cols.append((q, v))
+            i += 1
+        if rng.random() < dup_p and cells:             # a duplicate of some datapoint
+            q, v = cells[int(rng.integers(0, len(cells)))]
+            if rng.random() < diff_p:
+                v = bytes(b ^ 0x5A for b in v)
+            cols.append((q, v))
+        if rng.random() < 0.03:
+            cols.append((bytes([1, 0, 0]), b'{"note":1}'))   # an annotation
+    order = rng.permutation(len(cols))
+    ts = rng.permutation(len(cols) * 3)[:len(cols)]
+    return [(cols[j][0], cols[j][1], int(ts[k])) for k, j in enumerate(order)]
+
+
+@pytest.mark.parametrize("seed,fix", [(1, True), (2, True), (3, False), (4, True)])
+def test_random_rows_match_oracle(eng, seed, fix):
+    rng = np.random.default_rng(seed)
+    series, groups = [], []
+    for s in range(40):
+        rows = []
+        for h in range(int(rng.integers(1, 4))):
+            rows.append((B + 3600 * (h * 2 + int(rng.integers(0, 2))), random_row(rng, int(rng.integers(1, 60)),
+                                                                               dup_p=0.08 if fix else 0.01)))
+        series.append(rows)
+        groups.append(int(rng.integers(0, 4)))
+    order = np.argsort(groups, kind="stable")
+    series = [series[i] for i in order]
+    groups = [groups[i] for i in order]
+    cb = abi.HostCellBatch.from_rows(series, groups, fix)
+    eng.load_cells(cb)
+    got = rows_of(eng.download())
+    want, errs = [], []
+    spans = []
+    for s, rows in enumerate(series):
+        rr = []
+        for base, cols in sorted(rows, key=lambda x: x[0]):
+            try:
+                c = O.compact_row([(q, v) for q, v, _ in cols], fix, [t for _, _, t in cols])
+            except O.OracleError as e:
+                errs.append((base, e.code))
+                continue
+            if c is not None:
+                rr.append((base, c[0], c[1]))
+        want += rr
+        spans.append((s, rr))
+    assert got == want
+    # the queries over the compacted rows, against the oracle over its own compaction
+    ref = make_batch(spans, groups)
+    for agg, ds in (("sum", "1m-avg"), ("max", "10m-max"), ("none", None), ("zimsum", None)):
+        for start, end in ((B, B + 3 * 3600 * 2), (B + 7200, B + 3 * 3600 * 2)):
+            q = abi.new_query(start, end, agg)
+            if ds:
+                d = O.parse_downsample(ds)
+                q.ds_function, q.ds_interval_ms = d.ds_function, d.ds_interval_ms
+            covered = [c for b, c in errs if start // 3600 * 3600 <= b]
+            try:
+                w = O.run_query(ref, q)
+            except O.OracleError:
+                w = None
+            if covered:
+                with pytest.raises(EngineError):
+                    eng.run(q)
+                continue
+            g = eng.run(q)
+            if w is not None:
+                assert_groups_match(g, w, agg, ctx=f"{agg} {ds} {start}")
+
+
+def test_shuffled_single_cells_at_scale(eng):
+    """3,000 series x 2 rows of 3,600 one-datapoint cells in shuffled order: the compacted rows
+    are the sorted cells plus a meta byte, and the queries equal those over tsdbhip_load."""
+    rng = np.random.default_rng(7)
+    S, R, N = 3000, 2, 3600
+    nrow = S * R
+    offs = np.tile(np.arange(N, dtype=np.uint32), nrow).reshape(nrow, N)
+    perm = np.argsort(rng.random((nrow, N)), axis=1)
+    shuf = np.take_along_axis(offs, perm, axis=1)
+    quals = ((shuf << 4) | 7).astype(">u2")
+    vals = rng.integers(-10**6, 10**6, size=(nrow, N)).astype(">i8")
+    sorted_vals = np.empty_like(vals)
+    np.put_along_axis(sorted_vals, shuf.astype(np.int64), vals, axis=1)
+    qual = quals.view(np.uint8).reshape(-1)
+    val = vals.view(np.uint8).reshape(-1)
+    ncol = nrow * N
+    cb = abi.HostCellBatch(np.arange(S + 1, dtype=np.int64) * R,
+                           (B + 3600 * np.tile(np.arange(R), S)).astype(np.uint32),
+                           np.arange(nrow + 1, dtype=np.int64) * N,
+                           np.arange(ncol + 1, dtype=np.uint64) * 2, np.arange(ncol + 1, dtype=np.uint64) * 8,
+                           qual, val, np.repeat(np.arange(30), S // 30).astype(np.int32),
+                           rng.permutation(ncol).astype(np.int64), False)
+    eng.load_cells(cb)
+    got = eng.download()
+    exp_q = ((np.arange(N, dtype=np.uint32) << 4) | 7).astype(">u2").view(np.uint8)
+    assert np.array_equal(np.diff(got.row_qual_off.astype(np.int64)), np.full(nrow, 2 * N))
+    assert np.array_equal(np.diff(got.row_val_off.astype(np.int64)), np.full(nrow, 8 * N + 1))
+    gq = got.qual[:nrow * 2 * N].reshape(nrow, 2 * N)
+    assert (gq == exp_q[None, :]).all()
+    gv = got.val[:nrow * (8 * N + 1)].reshape(nrow, 8 * N + 1)
+    assert (gv[:, -1] == 0).all()
+    assert np.array_equal(gv[:, :-1], sorted_vals.view(np.uint8).reshape(nrow, 8 * N))
+    q = abi.new_query(B, B + 7199, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+    a = eng.run(q)
+    eng.load(got)
+    b = eng.run(q)
+    assert_groups_match(a, b, "sum", tol=0.0)
