@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define TSDBHIP_ABI_VERSION 5
+#define TSDBHIP_ABI_VERSION 6
 
 /* ---- error codes: one per Java exception on the path --------------------- */
 enum {
@@ -167,6 +167,7 @@ typedef struct {
   double fast_ms;                /* streaming kernel (k_fast) alone; 0 when not used */
   double index_ms;               /* k_index of the last tsdbhip_load / tsdbhip_synth: row classification,
                                     validation, certificate stats (+ the int16 value copy of vle rows) */
+  double compact_ms;             /* device compaction of the last tsdbhip_load_cells (k_compact pipeline) */
 } tsdbhip_timing;
 
 /* ---- library-level helpers (host logic of the reference, restated) ------- */

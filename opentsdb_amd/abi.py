@@ -139,6 +139,7 @@ class Timing(C.Structure):
         ("redo_tiles", C.c_int64),
         ("fast_ms", C.c_double),
         ("index_ms", C.c_double),
+        ("compact_ms", C.c_double),
     ]
 
 

@@ -77,10 +77,8 @@ __device__ __forceinline__ bool walk_append(const uint8_t* v, int64_t vl, F&& f)
   return true;
 }
 
-__global__ __launch_bounds__(256) void k_cmp_cols(CmpParams p) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= p.n_cols) return;
-  const int64_t row = p.col_row[c];
+// One column: kind, fixups, datapoint count, errors.  Returns whether it joins the heap.
+__device__ __forceinline__ bool cmp_col(const CmpParams& p, int64_t c, int64_t row) {
   const uint64_t qo = p.col_qo[c], vo = p.col_vo[c];
   const int64_t ql = (int64_t)(p.col_qo[c + 1] - qo), vl = (int64_t)(p.col_vo[c + 1] - vo);
   const uint8_t* q = p.q + qo;
@@ -131,9 +129,32 @@ __global__ __launch_bounds__(256) void k_cmp_cols(CmpParams p) {
   }
   p.col_n[c] = n;
   p.col_info[c] = kind | info;
-  if (heap) {
-    atomicAdd(&p.row_heap[row], 1);
-    atomicMax((unsigned long long*)&p.row_one[row], (unsigned long long)c);
+  return heap;
+}
+
+__global__ __launch_bounds__(256) void k_cmp_cols(CmpParams p) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = c < p.n_cols;
+  bool heap = false;
+  const int64_t row = valid ? p.col_row[c] : -1;
+  if (valid) heap = cmp_col(p, c, row);
+  // per-row heap counts, aggregated per wave: a row's columns are consecutive, so a wave
+  // covers few rows and each of them takes one atomic instead of one per column
+  const int lane = (int)(threadIdx.x & 63);
+  const int64_t prev_row = __shfl_up(row, 1);
+  const bool leader = valid && (lane == 0 || prev_row != row);
+  const uint64_t lead_mask = __ballot(leader);
+  const uint64_t heap_mask = __ballot(valid && heap);
+  if (leader) {
+    const uint64_t after = lane == 63 ? 0ull : (lead_mask & ~((2ull << lane) - 1));
+    const int end = after ? __builtin_ctzll(after) : 64;
+    const uint64_t seg = (end == 64 ? ~0ull : ((1ull << end) - 1)) & ~((1ull << lane) - 1);
+    const uint64_t hm = heap_mask & seg;
+    if (hm) {
+      atomicAdd(&p.row_heap[row], (int32_t)__popcll(hm));
+      const int top = 63 - __builtin_clzll(hm);
+      atomicMax((unsigned long long*)&p.row_one[row], (unsigned long long)(c - lane + top));
+    }
   }
 }
 

@@ -1,0 +1,67 @@
+"""Query-time compaction at scale: S series x N one-datapoint cells
+per hour row (1 s data, 8-byte values, columns in shuffled order, distinct write
+timestamps), compacted on the GPU by tsdbhip_load_cells.  Prints the wall time of the call,
+the device compaction time (k_compact pipeline, host layout excluded), k_index, and the
+algorithmic bytes rate: per cell 2 B qualifier + 8 B value + 16 B column offsets + 8 B
+timestamp read, 10 B written."""
+import json
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, ".")
+from opentsdb_amd import abi  # noqa: E402
+from opentsdb_amd.engine import Engine  # noqa: E402
+
+B = 1356998400
+
+
+def build(S, N, seed=1):
+    rng = np.random.default_rng(seed)
+    nrow = S
+    perm = np.argsort(rng.random((nrow, N)), axis=1).astype(np.uint32)
+    quals = ((perm << 4) | 7).astype(">u2")
+    vals = rng.integers(-10**6, 10**6, size=(nrow, N)).astype(">i8")
+    ncol = nrow * N
+    return abi.HostCellBatch(np.arange(S + 1, dtype=np.int64), np.full(S, B, np.uint32),
+                             np.arange(nrow + 1, dtype=np.int64) * N, np.arange(ncol + 1, dtype=np.uint64) * 2,
+                             np.arange(ncol + 1, dtype=np.uint64) * 8, quals.view(np.uint8).reshape(-1),
+                             vals.view(np.uint8).reshape(-1), (np.arange(S) * 64 // S).astype(np.int32),
+                             rng.permutation(ncol).astype(np.int64), False)
+
+
+def main():
+    S = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else 3600
+    steps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    t = time.perf_counter()
+    cb = build(S, N)
+    gen_s = time.perf_counter() - t
+    eng = Engine(0)
+    eng.load_cells(cb)
+    walls, cms, ims = [], [], []
+    for _ in range(steps):
+        t = time.perf_counter()
+        eng.load_cells(cb)
+        walls.append((time.perf_counter() - t) * 1000)
+        tm = eng.timing()
+        cms.append(tm.compact_ms)
+        ims.append(tm.index_ms)
+    cells = S * N
+    cm = sum(cms) / steps
+    q = abi.new_query(B, B + 3599, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+    eng.run(q)
+    t = time.perf_counter()
+    eng.run(q)
+    run_ms = (time.perf_counter() - t) * 1000
+    print(json.dumps({"workload": f"{S} series x {N} one-datapoint cells (shuffled), 8-byte ints",
+                      "cells": cells, "load_cells_wall_ms": sum(walls) / steps, "compact_ms": cm,
+                      "index_ms": sum(ims) / steps, "cells_per_s_device": cells / (cm / 1000),
+                      "algorithmic_GBps": cells * 44 / (cm / 1000) / 1e9, "query_ms_after": run_ms,
+                      "gen_s": gen_s}), flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
