@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define TSDBHIP_ABI_VERSION 6
+#define TSDBHIP_ABI_VERSION 7
 
 /* ---- error codes: one per Java exception on the path --------------------- */
 enum {
@@ -40,6 +40,9 @@ enum {
   TSDB_E_NO_SUCH_ELEMENT = -7,   /* NoSuchElementException (Aggregators.get, iterators) */
   TSDB_E_ASSERTION = -8,         /* AssertionError (AggregationIterator.java:701-703,769-771) */
   TSDB_E_CLASS_CAST = -9,        /* ClassCastException */
+  TSDB_E_NULL_POINTER = -10,     /* NullPointerException (a histogram downsampling function other than sum,
+                                    DownsamplingSpecification.java:153-157 -> SimpleHistogramDataPointAdapter
+                                    .mapAggregation) */
   TSDB_E_HIP = -20,              /* device/runtime failure (no reference counterpart) */
   TSDB_E_NOMEM = -21,
   TSDB_E_NOT_IMPLEMENTED = -22   /* valid reference query this engine does not run yet */
@@ -403,6 +406,81 @@ typedef struct {
   int32_t fix_duplicates;          /* tsd.storage.fix_duplicates */
 } tsdbhip_cell_batch;
 int tsdbhip_load_cells(tsdbhip_ctx* ctx, const tsdbhip_cell_batch* cb);
+
+/* ---- histogram path ----------------------------------------
+ * TsdbQuery.runHistogram (src/core/TsdbQuery.java:759-776, HistogramGroupByAndAggregateCB
+ * :1061-1255): the scanner's histogram columns (qualifier prefix 0x06, Internal.getQualifier /
+ * getTimeStampFromNonDP :1059-1074; value = [codec id][codec payload]) per row in column order,
+ * decoded by the codec HistogramCodecManager maps the id to (src/core/HistogramCodecManager.java:
+ * 148-206): SimpleHistogram (Kryo 2.21: BE16 bucket count, per bucket BE float lower / upper and a
+ * varint count, varint underflow and overflow; src/core/SimpleHistogram.java:97-122) or the
+ * reference's 8-byte long test codec (test/core/LongHistogramDataPointForTest.java).  A column
+ * that fails to decode is dropped (SaltScanner.processRow :771-778), a row without a histogram
+ * is not added.  Rows of a series become a HistogramSpan (addRow merge, :280-328); the spans of a
+ * group are merged by HistogramAggregationIterator (:91-287: union of timestamps, SUM of the
+ * histograms at equal timestamps, no interpolation) after the HistogramDownsampler (:28-403,
+ * SUM inside each interval, fill policies ignored).  Each group yields one DataPoints per
+ * requested percentile (HistogramDataPointsToDataPointsAdaptor: SimpleHistogram.percentile
+ * :133-164, the long codec data * p) and, with show_buckets, one per bucket of its first point
+ * (HistogramBucketDataPointsAdaptor).  Any group-by aggregator other than "none" is SUM
+ * (TsdbQuery.java:1132); "none" emits every span as its own group. */
+enum { TSDB_HCODEC_NONE = 0, TSDB_HCODEC_SIMPLE = 1, TSDB_HCODEC_LONG = 2 };
+typedef struct {
+  int64_t n_series;
+  const int64_t* series_row_ptr;   /* [n_series + 1] rows of each span, scan order */
+  int64_t n_rows;
+  const uint32_t* row_base_time;   /* [n_rows] seconds */
+  const int64_t* row_cell_ptr;     /* [n_rows + 1] histogram columns of each row, column order */
+  int64_t n_cells;
+  const uint64_t* cell_qual_off;   /* [n_cells + 1] from 0 */
+  const uint64_t* cell_val_off;    /* [n_cells + 1] from 0 */
+  const uint8_t* qual;
+  const uint8_t* val;
+  const int32_t* group_id;         /* [n_series] as tsdbhip_batch */
+  uint8_t codec[256];              /* codec kind (TSDB_HCODEC_*) of each codec id */
+} tsdbhip_hist_batch;
+/* Loads histogram spans as the resident histogram store (replaces the previous one; the
+ * numeric batch is unaffected). */
+int tsdbhip_load_histograms(tsdbhip_ctx* ctx, const tsdbhip_hist_batch* hb);
+
+/* Result of a histogram query, one entry per emitted HistogramSpanGroup (group order; for
+ * "none" one per span in batch order, group_id = span index).  Points of group g are
+ * [group_ptr[g], group_ptr[g + 1]).  pct[point * n_pct + j] = the j-th requested percentile.
+ * With show_buckets: the bucket dictionary (every bucket of the store, TreeMap order of
+ * HistogramBucket.compareTo: Float.compare of lower then upper bound; NaN bounds canonical), per
+ * point count[point * (n_buckets + 2) + b] (b < n_buckets: the bucket's summed count, n_buckets:
+ * underflow, n_buckets + 1: overflow) and present[point * n_buckets + b] (the bucket is in the
+ * point's histogram); codec[point] = codec kind of the point's histogram (bucket series exist for
+ * SimpleHistogram only).  The bucket series themselves (HistogramBucketDataPointsAdaptor:
+ * the first point's buckets, each looked up in every point) are built by the host from these. */
+typedef struct {
+  int64_t n_groups;
+  const int32_t* group_id;
+  const int64_t* group_ptr;
+  const int64_t* ts_ms;
+  int32_t n_pct;
+  const double* pct;
+  int32_t show_buckets;
+  int32_t n_buckets;
+  const uint32_t* bucket_lower;    /* float bits */
+  const uint32_t* bucket_upper;
+  const int64_t* count;
+  const uint8_t* present;
+  const uint8_t* codec;
+} tsdbhip_hist_result;
+/* The query's start / end, aggregator and downsampling (ds_function is ignored: histograms are
+ * always summed; -1 = no downsampling) as for tsdbhip_run; pct[n_pct] the percentiles
+ * (TsdbQuery.setPercentiles, List<Float>).  NOT_IMPLEMENTED: calendar downsampling, spans whose
+ * datapoints are not in time order, more than 4 GB of per-point state. */
+int tsdbhip_hist_run(tsdbhip_ctx* ctx, const tsdbhip_query* q, int n_pct, const float* pct, int show_buckets,
+                     tsdbhip_hist_result** out);
+/* The same over every row of the store with the HistogramSpanGroup bounds given directly (ms):
+ * HistogramAggregationIterator.create(spans, start_ms, end_ms, ...) as the reference's iterator
+ * tests call it (test/core/TestHistogramAggregationIterator.java); the query's start / end only
+ * bound "all" downsampling. */
+int tsdbhip_hist_run_range(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t start_ms, int64_t end_ms, int n_pct,
+                           const float* pct, int show_buckets, tsdbhip_hist_result** out);
+void tsdbhip_hist_result_free(tsdbhip_hist_result* r);
 
 /* Device synchronisation helper for host code that does not use HIP directly. */
 int tsdbhip_sync(tsdbhip_ctx* ctx);

@@ -20,6 +20,7 @@ TSDB_E_RUNTIME = -6
 TSDB_E_NO_SUCH_ELEMENT = -7
 TSDB_E_ASSERTION = -8
 TSDB_E_CLASS_CAST = -9
+TSDB_E_NULL_POINTER = -10
 TSDB_E_HIP = -20
 TSDB_E_NOMEM = -21
 TSDB_E_NOT_IMPLEMENTED = -22
@@ -33,6 +34,7 @@ ERROR_NAMES = {
     TSDB_E_NO_SUCH_ELEMENT: "NoSuchElementException",
     TSDB_E_ASSERTION: "AssertionError",
     TSDB_E_CLASS_CAST: "ClassCastException",
+    TSDB_E_NULL_POINTER: "NullPointerException",
     TSDB_E_HIP: "HipError",
     TSDB_E_NOMEM: "OutOfMemory",
     TSDB_E_NOT_IMPLEMENTED: "NotImplemented",

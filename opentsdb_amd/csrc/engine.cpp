@@ -446,7 +446,19 @@ struct tsdbhip_ctx {
   bool ro_scan_valid = false;          // scan-active value series of the last scan range
   int64_t ro_scan_ss = 0, ro_scan_se = 0;
   std::vector<uint8_t> ro_scan_act;    // [n_series] resident: rollup rows in the scan range
+  // histogram path (hist.cpp): the resident histogram store and its query scratch
+  void* hist = nullptr;
 };
+
+// accessors for the histogram path's translation unit (hist.cpp)
+namespace tsdb {
+hipStream_t ctx_stream(tsdbhip_ctx* c) { return c->stream; }
+int ctx_device(tsdbhip_ctx* c) { return c->device; }
+std::mutex& ctx_mutex(tsdbhip_ctx* c) { return c->mu; }
+void*& ctx_hist(tsdbhip_ctx* c) { return c->hist; }
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+void hist_release(void* h);
+}  // namespace tsdb
 
 // ===========================================================================
 // host logic restatements
@@ -624,6 +636,8 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
     for (DevBuf* b : {&o.series, &o.base, &o.qual, &o.voff, &o.val}) b->release();
   if (c->ro_tmp) (void)hipFree(c->ro_tmp);
   if (c->cmp_tmp) (void)hipFree(c->cmp_tmp);
+  tsdb::hist_release(c->hist);
+  c->hist = nullptr;
   for (DevBuf* b : {&c->sel_vals, &c->sel_sorted, &c->sel_uni, &c->sel_gsp, &c->cal_bounds}) b->release();
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   for (auto& e : c->cev) if (e) (void)hipEventDestroy(e);

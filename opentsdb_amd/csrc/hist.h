@@ -1,0 +1,93 @@
+// hist.h -- internal declarations of the histogram path shared by the
+// host side (hist.cpp) and the gfx950 kernels (k_hist.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tsdb {
+
+// Bucket dictionary: open-addressing hash set of the store's bucket keys
+// (canonical lower bits << 32 | canonical upper bits, Float.floatToIntBits canonical NaN).
+static constexpr uint64_t HK_EMPTY = ~0ull;   // never a canonical key (0xFFFFFFFF is a non-canonical NaN)
+static constexpr int HT_BITS = 16;             // 65536 slots: up to 32768 distinct buckets per store
+static constexpr int64_t HT_SIZE = 1ll << HT_BITS;
+static constexpr int HK_MAX = 1 << (HT_BITS - 1);
+
+// per-column decode status (k_hist_validate)
+enum : uint8_t { HC_DROP = 0, HC_SIMPLE = 1, HC_LONG = 2 };
+
+struct HistLoadParams {
+  int64_t n_cells;
+  const uint64_t* voff;      // [n_cells + 1]
+  const uint8_t* val;
+  const uint8_t* codec;      // [256] codec kind of each id
+  uint8_t* status;           // [n_cells] HC_*
+  uint64_t* hkey;            // [HT_SIZE]
+  int32_t* hcount;           // distinct keys inserted (overflow: > HK_MAX)
+};
+
+// Query over the resident store.  Positions are the spans' datapoints in HistogramSpan
+// iteration order (rows sorted by base time); pos_cell maps a position to its column.
+struct HistQueryParams {
+  // store
+  const uint64_t* voff;
+  const uint8_t* val;
+  const int64_t* pos_cell;   // [n_pos]
+  const int64_t* pos_ts;     // [n_pos] timestamp (ms)
+  const uint8_t* pos_kind;   // [n_pos] HC_SIMPLE / HC_LONG
+  const int64_t* row_pos;    // [n_rows + 1] positions of each (kept) row
+  const uint64_t* hkey;      // dictionary hash table
+  const int32_t* hidx;       // [HT_SIZE] dictionary index of each slot
+  const uint32_t* dict_lo;   // [D] bucket bounds (float bits) in dictionary (TreeMap) order
+  const uint32_t* dict_up;
+  int32_t D;                 // dictionary size
+  int32_t C;                 // accumulator columns: D buckets, underflow, overflow, long data
+  // present spans of the query (one thread each in k_hist_slots)
+  int64_t n_spans;
+  const int64_t* sp_rlo;     // [n_spans] in-range kept rows [rlo, rhi)
+  const int64_t* sp_rhi;
+  const int32_t* sp_out;     // [n_spans] emitted group index
+  // geometry (ms)
+  int64_t start, end;        // HistogramSpanGroup start / end (scan bounds)
+  int64_t qs, qe;            // query start / end ("all")
+  int32_t ds;                // 0 none, 1 fixed interval, 2 all
+  int32_t ds_sum;            // the downsampling function is "sum"
+  int64_t I;                 // interval
+  int64_t B0;                // slot 0 timestamp (dense modes)
+  int64_t K;                 // slots per group (dense modes)
+  // outputs of k_hist_slots
+  int32_t* pos_slot;         // [n_pos] slot (dense) or -1
+  int64_t* pos_key;          // [n_pos] sparse mode: (group << 42 | ts - start) or -1
+  int32_t* err;              // [2]: first error code, reason
+  // accumulation ([point][C] u64) -- point = group * K + slot (dense) or a union index (sparse)
+  const int32_t* pos_point;  // sparse mode: [n_pos] point of each position, -1 excluded (null: dense)
+  uint64_t* acc;
+  uint32_t* pres;            // [point][W] bucket presence bits (null: not tracked)
+  int32_t W;
+  uint32_t* pkind;           // [point] codec bits (1 simple, 2 long)
+  int64_t n_points;
+  // finalisation
+  int32_t n_pct;
+  const float* pct;          // [n_pct]
+  double* out_pct;           // [n_out * n_pct]
+  const int64_t* pt_out;     // [n_points] exclusive scan of emitted points (n_points + 1)
+  int64_t* out_ts;
+  const int64_t* pt_ts;      // sparse mode: [n_points] timestamp of each point
+  const int32_t* pt_group;   // sparse mode: [n_points] emitted group of each point
+  int32_t* out_group;        // [n_out]
+  uint8_t* out_kind;
+  int64_t* out_count;        // [n_out * (D + 2)] (show_buckets)
+  uint8_t* out_present;      // [n_out * D]
+};
+
+hipError_t hist_validate(const HistLoadParams& p, hipStream_t s);
+hipError_t hist_slots(const HistQueryParams& p, hipStream_t s);
+hipError_t hist_accum(const HistQueryParams& p, int64_t n_pos, hipStream_t s);
+hipError_t hist_flags(const HistQueryParams& p, uint32_t* flag, hipStream_t s);   // [n_points] 1 = emitted
+hipError_t hist_final(const HistQueryParams& p, hipStream_t s);
+hipError_t hist_scan(const uint32_t* flag, int64_t* out, int64_t n, void** tmp, size_t* tmp_bytes, hipStream_t s);
+hipError_t hist_sparse(const HistQueryParams& p, int64_t n_pos, uint64_t* key2, uint32_t* pos, uint32_t* pos2,
+                       uint32_t* head, int64_t* incl, int64_t* pt_ts, int32_t* pt_group, int64_t* n_points,
+                       void** tmp, size_t* tmp_bytes, hipStream_t s);
+
+}  // namespace tsdb

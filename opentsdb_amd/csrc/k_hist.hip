@@ -1,0 +1,452 @@
+// k_hist.hip -- gfx950 kernels of the histogram path.
+//
+// Reference: TsdbQuery.HistogramGroupByAndAggregateCB (src/core/TsdbQuery.java:1061-1255) over
+// HistogramSpans (src/core/HistogramSpan.java), HistogramDownsampler
+// (src/core/HistogramDownsampler.java:64-397), HistogramAggregationIterator
+// (src/core/HistogramAggregationIterator.java:91-313) and SimpleHistogram
+// (src/core/SimpleHistogram.java:97-271).
+//
+//   k_hist_validate  thread per column: the codec's decode (Kryo 2.21 layout) -- a column that
+//                    throws is dropped as SaltScanner.processRow drops it -- and every bucket key
+//                    of a SimpleHistogram into the store's dictionary hash set
+//   k_hist_slots     thread per span of the query: HistogramSpan.Iterator.seek, the
+//                    HistogramDownsampler's interval walk (or the raw datapoints) and the
+//                    aggregation iterator's per-span admission (first point >= start, stop at a
+//                    zero timestamp / past end) -> each datapoint's output slot
+//   k_hist_accum     wave of 64 consecutive datapoints: the columns are parsed in lock step (lane =
+//                    datapoint, loop = bucket position), counts are summed over the lanes that
+//                    hit the same (point, bucket) with a segmented wave scan and added once per
+//                    run (64-bit atomics: SUM of longs is exact in any order)
+//   k_hist_final     thread per (group, slot): SimpleHistogram.percentile / the long codec's
+//                    data * p, bucket counts and presence of the emitted points
+#include "hist.h"
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+
+namespace tsdb {
+
+struct HWiden {
+  __host__ __device__ int64_t operator()(uint32_t x) const { return (int64_t)x; }
+};
+
+namespace {
+
+__device__ __forceinline__ uint32_t fcanon(uint32_t b) {   // Float.floatToIntBits
+  return ((b & 0x7F800000u) == 0x7F800000u && (b & 0x007FFFFFu)) ? 0x7FC00000u : b;
+}
+__device__ __forceinline__ uint64_t hk_hash(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdULL;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ULL;
+  k ^= k >> 33;
+  return k;
+}
+__device__ __forceinline__ uint32_t be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+// Kryo Input.readLong(true): 7-bit groups, the 9th byte carries 8 bits; false = buffer underflow
+__device__ __forceinline__ bool varlong(const uint8_t* v, uint64_t n, uint64_t& i, uint64_t& out) {
+  uint64_t r = 0;
+#pragma unroll 1
+  for (int j = 0; j < 8; j++) {
+    if (i >= n) return false;
+    const uint32_t b = v[i++];
+    r |= (uint64_t)(b & 0x7F) << (7 * j);
+    if (!(b & 0x80)) { out = r; return true; }
+  }
+  if (i >= n) return false;
+  r |= (uint64_t)v[i++] << 56;
+  out = r;
+  return true;
+}
+
+// SimpleHistogram.fromHistogram(raw, true) (:97-122): count and byte length of a valid column
+__device__ bool simple_valid(const uint8_t* v, uint64_t n) {
+  if (n < 6) return false;
+  const int cnt = (int16_t)(((uint32_t)v[1] << 8) | v[2]);
+  uint64_t i = 3, c;
+#pragma unroll 1
+  for (int j = 0; j < cnt; j++) {
+    if (i + 8 > n) return false;
+    i += 8;
+    if (!varlong(v, n, i, c)) return false;
+  }
+  return varlong(v, n, i, c) && varlong(v, n, i, c);
+}
+
+__global__ void k_hist_validate(HistLoadParams p) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= p.n_cells) return;
+  const uint64_t o = p.voff[c], n = p.voff[c + 1] - o;
+  const uint8_t* v = p.val + o;
+  uint8_t st = HC_DROP;
+  if (n >= 1) {
+    const int id = (int8_t)v[0];
+    const uint8_t kind = id >= 0 ? p.codec[id] : 0;
+    if (kind == HC_LONG) st = n >= 9 ? HC_LONG : HC_DROP;             // Bytes.getLong(raw, 1)
+    else if (kind == HC_SIMPLE && simple_valid(v, n)) st = HC_SIMPLE;
+  }
+  p.status[c] = st;
+  if (st != HC_SIMPLE) return;
+  const int cnt = (int16_t)(((uint32_t)v[1] << 8) | v[2]);
+  uint64_t i = 3, cv;
+#pragma unroll 1
+  for (int j = 0; j < cnt; j++) {
+    const uint64_t key = ((uint64_t)fcanon(be32(v + i)) << 32) | fcanon(be32(v + i + 4));
+    i += 8;
+    varlong(v, n, i, cv);
+    uint64_t slot = hk_hash(key) & (uint64_t)(HT_SIZE - 1);
+#pragma unroll 1
+    for (int64_t probe = 0;; probe++) {
+      if (probe >= HT_SIZE) { atomicAdd(p.hcount, HK_MAX + 1); break; }
+      const uint64_t cur = __hip_atomic_load(&p.hkey[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == key) break;
+      if (cur == HK_EMPTY) {
+        const unsigned long long prev =
+            atomicCAS((unsigned long long*)&p.hkey[slot], (unsigned long long)HK_EMPTY, (unsigned long long)key);
+        if (prev == HK_EMPTY) { atomicAdd(p.hcount, 1); break; }
+        if (prev == key) break;
+      }
+      slot = (slot + 1) & (uint64_t)(HT_SIZE - 1);
+    }
+  }
+}
+
+__device__ __forceinline__ int32_t dict_index(const HistQueryParams& p, uint64_t key) {
+  uint64_t slot = hk_hash(key) & (uint64_t)(HT_SIZE - 1);
+#pragma unroll 1
+  for (int64_t probe = 0; probe < HT_SIZE; probe++) {
+    const uint64_t cur = p.hkey[slot];
+    if (cur == key) return p.hidx[slot];
+    if (cur == HK_EMPTY) return -1;
+    slot = (slot + 1) & (uint64_t)(HT_SIZE - 1);
+  }
+  return -1;
+}
+
+__device__ __forceinline__ void set_err(int32_t* err, int code, int why) {
+  if (atomicCAS(err, 0, code) == 0) err[1] = why;
+}
+
+// error reasons (err[1]) reported by the host
+enum { WHY_SEEK = 1, WHY_NPE = 2, WHY_UNSORTED = 3, WHY_SLOT = 4, WHY_MIXED = 5, WHY_DICT = 6 };
+
+// HistogramSpan.Iterator.seek (:525-532 with seekRow :417-437 and HistogramRowSeq.Iterator.seek
+// :357-368): the position iteration continues from
+__device__ int64_t span_seek(const HistQueryParams& p, int64_t rlo, int64_t rhi, int64_t target) {
+  int64_t ri = rlo;
+  for (int64_t r = rlo; r < rhi; r++) {
+    const int64_t a = p.row_pos[r], b = p.row_pos[r + 1];
+    if (b - a < 1 || p.pos_ts[b - 1] < target) ri++;
+    else break;
+  }
+  if (ri == rhi) --ri;
+  int64_t q = p.row_pos[ri];
+  const int64_t e = p.row_pos[ri + 1];
+  while (q < e && p.pos_ts[q] < target) ++q;
+  return q;
+}
+
+__global__ void k_hist_slots(HistQueryParams p) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= p.n_spans) return;
+  const int64_t rlo = p.sp_rlo[s], rhi = p.sp_rhi[s];
+  const int64_t p0 = p.row_pos[rlo], p1 = p.row_pos[rhi];
+  if (p1 <= p0) return;
+  // HistogramSpanGroup.add (:187-203): a datapoint of the span in [start, end]
+  int64_t first = p.pos_ts[p0], last = p.pos_ts[p1 - 1];
+  if ((first & (int64_t)0xFFFFFFFF00000000LL) == 0) first *= 1000;
+  if ((last & (int64_t)0xFFFFFFFF00000000LL) == 0) last *= 1000;
+  if (!(first <= p.end && last >= p.start)) return;
+  const int64_t g = p.sp_out[s];
+  const int64_t target = p.ds == 1 ? (p.start + p.I - 1) - (p.start + p.I - 1) % p.I : p.start;
+  if (target & (int64_t)0xFFFFF00000000000LL) { set_err(p.err, -3 /* IAE */, WHY_SEEK); return; }
+  int64_t q = span_seek(p, rlo, rhi, target);
+  if (p.ds == 0) {
+    // raw: every datapoint is an output of the span (HistogramSpan.Iterator)
+    int64_t prev = INT64_MIN;
+    for (bool firstout = true; q < p1; q++, firstout = false) {
+      const int64_t ts = p.pos_ts[q];
+      if (firstout && ts < p.start) return;   // ctor :141-151: the span ends
+      if (ts == 0 || ts > p.end) return;      // endReached / never merged again
+      if (ts <= prev) { set_err(p.err, -22, WHY_UNSORTED); return; }
+      prev = ts;
+      p.pos_key[q] = (g << 42) | (ts - p.start);
+    }
+    return;
+  }
+  if (p.ds == 2) {
+    // "all" (:251-276): skip datapoints before the query start, stop at the first one at or past
+    // the query end; one output whose timestamp() is the query start
+    int64_t n = 0;
+    int64_t r = q;
+    for (; r < p1; r++) {
+      const int64_t ts = p.pos_ts[r];
+      if (ts < p.qs) continue;
+      if (ts >= p.qe) break;
+      n++;
+    }
+    if (n == 0) return;
+    if (n >= 2 && !p.ds_sum) { set_err(p.err, -10, WHY_NPE); return; }
+    if (p.qs < p.start || p.qs == 0 || p.qs > p.end) return;
+    for (r = q; r < p1; r++) {
+      const int64_t ts = p.pos_ts[r];
+      if (ts < p.qs) continue;
+      if (ts >= p.qe) break;
+      p.pos_slot[r] = (int32_t)g;
+    }
+    return;
+  }
+  // fixed interval (:242-244, 296-297, 334-349): the interval of the first datapoint not yet
+  // consumed, every following datapoint below its end
+  int64_t prev = INT64_MIN;
+  for (bool firstout = true; q < p1; firstout = false) {
+    const int64_t a = p.pos_ts[q];
+    const int64_t tei = a - a % p.I + p.I;
+    const int64_t ots = tei - p.I;
+    int64_t e = q;
+    while (e < p1 && p.pos_ts[e] < tei) e++;
+    // the aggregation iterator pulls this interval (the HistogramDownsampler sums it now)
+    if (e - q >= 2 && !p.ds_sum) { set_err(p.err, -10, WHY_NPE); return; }
+    if (firstout && ots < p.start) return;
+    if (ots == 0 || ots > p.end) return;
+    if (ots <= prev) { set_err(p.err, -22, WHY_UNSORTED); return; }
+    prev = ots;
+    const int64_t k = (ots - p.B0) / p.I;
+    if (ots < p.B0 || k >= p.K) { set_err(p.err, -22, WHY_SLOT); return; }
+    const int32_t slot = (int32_t)(g * p.K + k);
+    for (int64_t r = q; r < e; r++) p.pos_slot[r] = slot;
+    q = e;
+  }
+}
+
+// segmented (by equal address) inclusive sum over the wave; returns true on the run's last lane
+__device__ __forceinline__ bool seg_sum(uint64_t addr, uint64_t& v) {
+  const int lane = __lane_id();
+  const uint64_t left = __shfl_up(addr, 1);
+  const bool head = lane == 0 || left != addr;
+  const uint64_t heads = __ballot(head);
+  const uint64_t upto = heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+  const int start = 63 - __builtin_clzll(upto);
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t o = __shfl_up(v, d);
+    if (lane - d >= start) v += o;
+  }
+  const uint64_t right = __shfl_down(addr, 1);
+  return lane == 63 || right != addr;
+}
+
+__global__ void __launch_bounds__(256) k_hist_accum(HistQueryParams p, int64_t n_pos) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = q < n_pos;
+  int32_t pt = -1;
+  if (in) pt = p.pos_point ? p.pos_point[q] : p.pos_slot[q];
+  if (__ballot(pt >= 0) == 0) return;
+  const uint8_t* v = nullptr;
+  uint64_t n = 0, i = 3;
+  int cnt = 0;
+  uint8_t kind = 0;
+  if (pt >= 0) {
+    const int64_t c = p.pos_cell[q];
+    const uint64_t o = p.voff[c];
+    n = p.voff[c + 1] - o;
+    v = p.val + o;
+    kind = p.pos_kind[q];
+    atomicOr(&p.pkind[pt], kind == HC_SIMPLE ? 1u : 2u);
+    if (kind == HC_SIMPLE) cnt = (int16_t)(((uint32_t)v[1] << 8) | v[2]);
+  }
+  const uint64_t base = (uint64_t)(pt >= 0 ? pt : 0) * (uint64_t)p.C;
+  // long codec data (LongHistogramDataPointForTest.aggregate: data + other)
+  {
+    uint64_t val = 0, addr = ~0ull;
+    if (pt >= 0 && kind == HC_LONG) {
+      for (int j = 1; j < 9; j++) val = (val << 8) | v[j];
+      addr = base + p.C - 1;
+    }
+    const bool tail = seg_sum(addr, val);
+    if (tail && addr != ~0ull) atomicAdd((unsigned long long*)&p.acc[addr], (unsigned long long)val);
+  }
+  int maxc = cnt;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) maxc = max(maxc, __shfl_xor(maxc, d));
+  // buckets in lock step (SimpleHistogram.aggregate :246-261: counts of equal keys add)
+#pragma unroll 1
+  for (int j = 0; j < maxc; j++) {
+    uint64_t addr = ~0ull, val = 0;
+    int32_t di = -1;
+    if (j < cnt) {
+      const uint64_t key = ((uint64_t)fcanon(be32(v + i)) << 32) | fcanon(be32(v + i + 4));
+      i += 8;
+      varlong(v, n, i, val);
+      di = dict_index(p, key);
+      if (di < 0) set_err(p.err, -22, WHY_DICT);
+      else addr = base + (uint64_t)di;
+    }
+    const bool tail = seg_sum(addr, val);
+    if (tail && addr != ~0ull) atomicAdd((unsigned long long*)&p.acc[addr], (unsigned long long)val);
+    if (p.pres && di >= 0) atomicOr(&p.pres[(uint64_t)pt * p.W + (di >> 5)], 1u << (di & 31));
+  }
+  // underflow, overflow (:256-257)
+  for (int u = 0; u < 2; u++) {
+    uint64_t addr = ~0ull, val = 0;
+    if (pt >= 0 && kind == HC_SIMPLE) {
+      varlong(v, n, i, val);
+      addr = base + (uint64_t)p.D + u;
+    }
+    const bool tail = seg_sum(addr, val);
+    if (tail && addr != ~0ull) atomicAdd((unsigned long long*)&p.acc[addr], (unsigned long long)val);
+  }
+}
+
+__global__ void k_hist_flags(HistQueryParams p, uint32_t* flag) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= p.n_points) return;
+  const uint32_t k = p.pkind[t];
+  if (k == 3u) set_err(p.err, -3, WHY_MIXED);
+  flag[t] = k ? 1u : 0u;
+}
+
+__global__ void k_hist_final(HistQueryParams p) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= p.n_points) return;
+  const uint32_t kind = p.pkind[t];
+  if (!kind) return;
+  const int64_t o = p.pt_out[t];
+  const uint64_t* a = p.acc + (uint64_t)t * p.C;
+  p.out_ts[o] = p.pt_ts ? p.pt_ts[t] : p.B0 + (t % p.K) * p.I;
+  p.out_group[o] = p.pt_group ? p.pt_group[t] : (int32_t)(t / p.K);
+  p.out_kind[o] = kind == 1u ? HC_SIMPLE : HC_LONG;
+  for (int j = 0; j < p.n_pct; j++) {
+    const double perc = (double)p.pct[j];
+    double r;
+    if (kind == 2u) {
+      r = (double)(int64_t)a[p.C - 1] * perc;   // LongHistogramDataPointForTest.percentile
+    } else if (perc < 1.0 || perc > 100.0) {
+      r = -1.0;
+    } else {   // SimpleHistogram.percentile (:133-164): int counts, bucket midpoints as float
+      int32_t sum = 0;
+      for (int b = 0; b < p.D; b++) sum = (int32_t)((uint32_t)sum + (uint32_t)a[b]);
+      int64_t running = 0;
+      r = 0.0;
+      for (int b = 0; b < p.D; b++) {
+        running += (int32_t)(uint32_t)a[b];
+        const double area = (double)running * 100.0 / (double)sum;
+        if (area >= perc) {
+          const float mid = (__uint_as_float(p.dict_lo[b]) + __uint_as_float(p.dict_up[b])) / 2;
+          r = (double)mid;
+          break;
+        }
+      }
+    }
+    p.out_pct[o * p.n_pct + j] = r;
+  }
+  if (p.out_count) {
+    for (int b = 0; b < p.D + 2; b++) p.out_count[o * (p.D + 2) + b] = (int64_t)a[b];
+    for (int b = 0; b < p.D; b++) p.out_present[o * p.D + b] = (p.pres[(uint64_t)t * p.W + (b >> 5)] >> (b & 31)) & 1u;
+  }
+}
+
+// sparse mode: sorted (group << 42 | ts - start) keys -> union points
+__global__ void k_hist_heads(const uint64_t* key, int64_t n, uint32_t* head) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  head[i] = key[i] != ~0ull && (i == 0 || key[i] != key[i - 1]) ? 1u : 0u;
+}
+__global__ void k_hist_points(const uint64_t* key, const uint32_t* pos, int64_t n, const int64_t* incl,
+                              int64_t start, int32_t* pos_point, int64_t* pt_ts, int32_t* pt_group) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || key[i] == ~0ull) return;
+  const int64_t pt = incl[i + 1] - 1;   // inclusive count of heads up to i, minus one
+  pos_point[pos[i]] = (int32_t)pt;
+  if (i == 0 || key[i] != key[i - 1]) {
+    pt_ts[pt] = start + (int64_t)(key[i] & ((1ull << 42) - 1));
+    pt_group[pt] = (int32_t)(key[i] >> 42);
+  }
+}
+__global__ void k_iota(uint32_t* v, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) v[i] = (uint32_t)i;
+}
+
+}  // namespace
+
+// exclusive scan of n flags into out[0 .. n] (out[n] = total)
+hipError_t hist_scan(const uint32_t* flag, int64_t* out, int64_t n, void** tmp, size_t* tmp_bytes, hipStream_t s) {
+  hipcub::TransformInputIterator<int64_t, HWiden, const uint32_t*> in(flag, HWiden());
+  size_t need = 0;
+  hipError_t e = hipcub::DeviceScan::InclusiveSum(nullptr, need, in, out + 1, (int)std::max<int64_t>(1, n), s);
+  if (e != hipSuccess) return e;
+  if (need > *tmp_bytes) {
+    if (*tmp) (void)hipFree(*tmp);
+    *tmp = nullptr;
+    *tmp_bytes = 0;
+    if ((e = hipMalloc(tmp, need)) != hipSuccess) return e;
+    *tmp_bytes = need;
+  }
+  if ((e = hipMemsetAsync(out, 0, 8, s)) != hipSuccess) return e;
+  if (n <= 0) return hipSuccess;
+  return hipcub::DeviceScan::InclusiveSum(*tmp, need, in, out + 1, (int)n, s);
+}
+
+// sparse (no downsampling) union: sort the datapoints' (group, timestamp) keys, one point per
+// distinct key; pos_point[position], pt_ts / pt_group[point]; returns the point count in *n_points
+hipError_t hist_sparse(const HistQueryParams& p, int64_t n_pos, uint64_t* key2, uint32_t* pos, uint32_t* pos2,
+                       uint32_t* head, int64_t* incl, int64_t* pt_ts, int32_t* pt_group, int64_t* n_points,
+                       void** tmp, size_t* tmp_bytes, hipStream_t s) {
+  hipError_t e;
+  const unsigned nb = (unsigned)((n_pos + 255) / 256);
+  hipLaunchKernelGGL(k_iota, dim3(nb), dim3(256), 0, s, pos, n_pos);
+  size_t need = 0;
+  if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, need, (const uint64_t*)p.pos_key, key2, pos, pos2, (int)n_pos, 0,
+                                              64, s)) != hipSuccess)
+    return e;
+  if (need > *tmp_bytes) {
+    if (*tmp) (void)hipFree(*tmp);
+    *tmp = nullptr;
+    *tmp_bytes = 0;
+    if ((e = hipMalloc(tmp, need)) != hipSuccess) return e;
+    *tmp_bytes = need;
+  }
+  if ((e = hipcub::DeviceRadixSort::SortPairs(*tmp, need, (const uint64_t*)p.pos_key, key2, pos, pos2, (int)n_pos, 0, 64,
+                                              s)) != hipSuccess)
+    return e;
+  hipLaunchKernelGGL(k_hist_heads, dim3(nb), dim3(256), 0, s, key2, n_pos, head);
+  if ((e = hist_scan(head, incl, n_pos, tmp, tmp_bytes, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_hist_points, dim3(nb), dim3(256), 0, s, key2, pos2, n_pos, incl, p.start,
+                     const_cast<int32_t*>(p.pos_point), pt_ts, pt_group);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = hipMemcpyAsync(n_points, incl + n_pos, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+  return hipStreamSynchronize(s);
+}
+
+hipError_t hist_validate(const HistLoadParams& p, hipStream_t s) {
+  if (p.n_cells <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hist_validate, dim3((unsigned)((p.n_cells + 255) / 256)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+hipError_t hist_slots(const HistQueryParams& p, hipStream_t s) {
+  if (p.n_spans <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hist_slots, dim3((unsigned)((p.n_spans + 127) / 128)), dim3(128), 0, s, p);
+  return hipGetLastError();
+}
+hipError_t hist_accum(const HistQueryParams& p, int64_t n_pos, hipStream_t s) {
+  if (n_pos <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hist_accum, dim3((unsigned)((n_pos + 255) / 256)), dim3(256), 0, s, p, n_pos);
+  return hipGetLastError();
+}
+hipError_t hist_flags(const HistQueryParams& p, uint32_t* flag, hipStream_t s) {
+  if (p.n_points <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hist_flags, dim3((unsigned)((p.n_points + 255) / 256)), dim3(256), 0, s, p, flag);
+  return hipGetLastError();
+}
+hipError_t hist_final(const HistQueryParams& p, hipStream_t s) {
+  if (p.n_points <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hist_final, dim3((unsigned)((p.n_points + 255) / 256)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace tsdb

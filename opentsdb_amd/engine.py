@@ -13,6 +13,7 @@ import subprocess
 import numpy as np
 
 from . import abi
+from . import histogram as H
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TSDBHIP_LIB") or os.path.join(HERE, "lib", "libtsdbhip.so")
@@ -28,7 +29,8 @@ EXPORTS = [
     "tsdbhip_rollup_basetime", "tsdbhip_rollup_qualifier", "tsdbhip_rollup_run", "tsdbhip_rollup_download",
     "tsdbhip_sel_layout", "tsdbhip_sel_run_values", "tsdbhip_sel_select", "tsdbhip_assemble", "tsdbhip_run_multi",
     "tsdbhip_debug_rows", "tsdbhip_shard_bounds", "tsdbhip_load_shard", "tsdbhip_synth_shard",
-    "tsdbhip_load_rollup", "tsdbhip_load_cells",
+    "tsdbhip_load_rollup", "tsdbhip_load_cells", "tsdbhip_load_histograms", "tsdbhip_hist_run",
+    "tsdbhip_hist_run_range", "tsdbhip_hist_result_free",
 ]
 
 SHARD_SERIES, SHARD_GROUPS, SHARD_SPANS = 0, 1, 2   # tsdbhip.h TSDB_SHARD_*
@@ -97,6 +99,12 @@ def lib():
         L.tsdbhip_synth_shard.argtypes = [vp, C.POINTER(abi.SynthSpec), C.c_int64, C.c_int64]
         L.tsdbhip_load_rollup.argtypes = [vp, C.POINTER(abi.RollupBatch)]
         L.tsdbhip_load_cells.argtypes = [vp, C.POINTER(abi.CellBatch)]
+        L.tsdbhip_load_histograms.argtypes = [vp, C.POINTER(H.HistBatch)]
+        L.tsdbhip_hist_run.argtypes = [vp, C.POINTER(abi.Query), C.c_int, C.POINTER(C.c_float), C.c_int,
+                                       C.POINTER(C.POINTER(H.HistResult))]
+        L.tsdbhip_hist_run_range.argtypes = [vp, C.POINTER(abi.Query), C.c_int64, C.c_int64, C.c_int,
+                                             C.POINTER(C.c_float), C.c_int, C.POINTER(C.POINTER(H.HistResult))]
+        L.tsdbhip_hist_result_free.argtypes = [C.POINTER(H.HistResult)]
         _lib = L
     return _lib
 
@@ -207,6 +215,28 @@ class Engine:
         """tsdbhip_load_cells: the scan's rows compacted on the GPU become the resident batch."""
         _check(lib().tsdbhip_load_cells(self.ctx, C.byref(cb.c)))
         self._batch = cb
+
+    def load_histograms(self, hb: "H.HostHistBatch"):
+        """tsdbhip_load_histograms: the resident histogram store."""
+        _check(lib().tsdbhip_load_histograms(self.ctx, C.byref(hb.c)))
+
+    def run_histogram(self, q: abi.Query, percentiles=(), show_buckets: bool = False, span_range=None):
+        """TsdbQuery.runHistogram over the resident histogram store: per emitted group the list
+        of its DataPoints (percentile series, then bucket series), see histogram.result_to_series.
+        span_range=(start_ms, end_ms): HistogramAggregationIterator bounds given directly
+        (tsdbhip_hist_run_range, every row)."""
+        pct = (C.c_float * max(1, len(percentiles)))(*[float(x) for x in percentiles])
+        res = C.POINTER(H.HistResult)()
+        if span_range is None:
+            _check(lib().tsdbhip_hist_run(self.ctx, C.byref(q), len(percentiles), pct, int(bool(show_buckets)),
+                                          C.byref(res)))
+        else:
+            _check(lib().tsdbhip_hist_run_range(self.ctx, C.byref(q), int(span_range[0]), int(span_range[1]),
+                                                len(percentiles), pct, int(bool(show_buckets)), C.byref(res)))
+        try:
+            return H.result_to_series(res.contents, [float(C.c_float(x).value) for x in percentiles])
+        finally:
+            lib().tsdbhip_hist_result_free(res)
 
     def load_rollup(self, rb: abi.HostRollupBatch):
         """tsdbhip_load_rollup: a rollup table's scan result as the resident batch; run()

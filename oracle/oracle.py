@@ -28,6 +28,23 @@ def build(force: bool = False) -> str:
 _lib = None
 
 
+class RefHistResult(C.Structure):
+    _fields_ = [
+        ("n_groups", C.c_int64),
+        ("group_id", C.POINTER(C.c_int32)),
+        ("group_ptr", C.POINTER(C.c_int64)),
+        ("ts", C.POINTER(C.c_int64)),
+        ("n_pct", C.c_int32),
+        ("pct", C.POINTER(C.c_double)),
+        ("bk_ptr", C.POINTER(C.c_int64)),
+        ("bk_type", C.POINTER(C.c_int32)),
+        ("bk_lo", C.POINTER(C.c_uint32)),
+        ("bk_up", C.POINTER(C.c_uint32)),
+        ("bk_val_off", C.POINTER(C.c_int64)),
+        ("bk_val", C.POINTER(C.c_int64)),
+    ]
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -72,6 +89,12 @@ def lib():
         L.ref_free.argtypes = [C.c_void_p]
         L.ref_run_rollup_query.argtypes = [C.POINTER(abi.RollupBatch), C.POINTER(abi.Query),
                                            C.POINTER(C.POINTER(abi.Result))]
+        L.ref_run_hist.argtypes = [C.c_void_p, C.POINTER(abi.Query), C.c_int, C.POINTER(C.c_float), C.c_int,
+                                   C.POINTER(C.POINTER(RefHistResult))]
+        L.ref_run_hist_range.argtypes = [C.c_void_p, C.POINTER(abi.Query), C.c_int64, C.c_int64, C.c_int,
+                                         C.POINTER(C.c_float), C.c_int, C.POINTER(C.POINTER(RefHistResult))]
+        L.ref_hist_result_free.argtypes = [C.POINTER(RefHistResult)]
+        L.ref_hist_value_percentile.argtypes = [C.c_char_p, C.c_int64, C.c_int, C.c_double, C.POINTER(C.c_double)]
         L.ref_rollup_scan_bounds.argtypes = [C.POINTER(abi.Query), C.POINTER(abi.RollupInterval),
                                              C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
         _lib = L
@@ -324,3 +347,50 @@ def run_query(batch: abi.HostBatch, q: abi.Query, threads: int = 1):
         return abi.result_to_groups(res.contents)
     finally:
         lib().ref_result_free(res)
+
+
+def run_hist(hb, q: abi.Query, percentiles=(), show_buckets: bool = False, span_range=None):
+    """TsdbQuery.runHistogram on the oracle (oracle/refhist.c): per emitted group the list of its
+    DataPoints (opentsdb_amd.histogram.HistogramDataPoints), percentile series then bucket series."""
+    from opentsdb_amd import histogram as H
+    pct = (C.c_float * max(1, len(percentiles)))(*[float(x) for x in percentiles])
+    res = C.POINTER(RefHistResult)()
+    if span_range is None:
+        rc = lib().ref_run_hist(C.cast(C.byref(hb.c), C.c_void_p), C.byref(q), len(percentiles), pct,
+                                int(bool(show_buckets)), C.byref(res))
+    else:
+        rc = lib().ref_run_hist_range(C.cast(C.byref(hb.c), C.c_void_p), C.byref(q), int(span_range[0]),
+                                      int(span_range[1]), len(percentiles), pct, int(bool(show_buckets)),
+                                      C.byref(res))
+    if rc < 0:
+        _err(rc)
+    try:
+        r = res.contents
+        P = len(percentiles)
+        out = []
+        for g in range(r.n_groups):
+            a, b = r.group_ptr[g], r.group_ptr[g + 1]
+            gid = r.group_id[g]
+            ts = np.array([r.ts[i] for i in range(a, b)], np.int64)
+            series = []
+            for j in range(P):
+                vals = np.array([r.pct[i * P + j] for i in range(a, b)], np.float64)
+                series.append(H.HistogramDataPoints(gid, ts, vals, np.zeros(b - a, np.uint8),
+                                                    percentile=float(pct[j])))
+            off = r.bk_val_off[g]
+            for k, bi in enumerate(range(r.bk_ptr[g], r.bk_ptr[g + 1])):
+                vals = np.array([r.bk_val[off + k * (b - a) + i] for i in range(b - a)], np.int64)
+                series.append(H.HistogramDataPoints(gid, ts, vals, np.ones(b - a, np.uint8),
+                                                    bucket=(r.bk_type[bi], r.bk_lo[bi], r.bk_up[bi])))
+            out.append(series)
+        return out
+    finally:
+        lib().ref_hist_result_free(res)
+
+
+def hist_value_percentile(value: bytes, kind: int, p: float):
+    """SimpleHistogram.percentile / the long test codec's percentile of one stored value (with
+    its codec id byte); None if the value does not decode."""
+    out = C.c_double()
+    rc = lib().ref_hist_value_percentile(value, len(value), kind, p, C.byref(out))
+    return None if rc < 0 else out.value

@@ -1563,6 +1563,21 @@ static int64_t cal_prev(int64_t ts, int64_t n, int unit, const tsdbhip_tz* z) {
   return cal_add(c, uo, -io, z);
 }
 
+int ref_cal_prev_ex(int64_t ts, int64_t n, int unit, const tsdbhip_tz* z, int64_t* out) {
+  int rc = 0;
+  TRY { *out = cal_prev(ts, n, unit, z); }
+  CATCH(code) { rc = code; }
+  END_TRY
+  return rc;
+}
+int ref_cal_step_ex(int64_t ts, int unit, int64_t n, const tsdbhip_tz* z, int64_t* out) {
+  int rc = 0;
+  TRY { *out = cal_step(ts, unit, n, 1, z); }
+  CATCH(code) { rc = code; }
+  END_TRY
+  return rc;
+}
+
 /* ======================================================================== */
 /* Downsampler / FillingDownsampler                                          */
 /* ======================================================================== */

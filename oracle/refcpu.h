@@ -95,6 +95,42 @@ int ref_compact_row(int64_t ncols, const uint8_t* const* quals, const int64_t* q
                     const int64_t* vlens, const int64_t* col_ts, int fix_duplicates, uint8_t** out_q,
                     int64_t* out_qlen, uint8_t** out_v, int64_t* out_vlen);
 void ref_free(void* p);
+/* ---- histogram path (refhist.c) ----------------------------------
+ * TsdbQuery.runHistogram over a tsdbhip_hist_batch: SaltScanner's histogram decode,
+ * HistogramSpan / HistogramRowSeq, HistogramDownsampler, HistogramAggregationIterator,
+ * SimpleHistogram and the two DataPoints adaptors.  Per emitted group: its points (ts), the
+ * percentile series values pct[point * n_pct + j], and its bucket series (the first point's
+ * getHistogramBucketsIfHas keys: type 0 underflow / 1 regular / 2 overflow, float bits) with
+ * one long per point each: bk_val[bk_val_off[g] + series * n_points_g + i]. */
+typedef struct {
+  int64_t n_groups;
+  int32_t* group_id;
+  int64_t* group_ptr;
+  int64_t* ts;
+  int32_t n_pct;
+  double* pct;
+  int64_t* bk_ptr;        /* [n_groups + 1] bucket series of each group */
+  int32_t* bk_type;
+  uint32_t* bk_lo;
+  uint32_t* bk_up;
+  int64_t* bk_val_off;    /* [n_groups + 1] */
+  int64_t* bk_val;
+} ref_hist_result;
+int ref_run_hist(const tsdbhip_hist_batch* hb, const tsdbhip_query* q, int n_pct, const float* pct,
+                 int show_buckets, ref_hist_result** out);
+/* HistogramAggregationIterator.create(spans, start_ms, end_ms, ...) over every row of the batch
+ * (the reference's iterator-level tests; query start / end feed "all" only) */
+int ref_run_hist_range(const tsdbhip_hist_batch* hb, const tsdbhip_query* q, int64_t start_ms, int64_t end_ms,
+                       int n_pct, const float* pct, int show_buckets, ref_hist_result** out);
+void ref_hist_result_free(ref_hist_result* r);
+/* SimpleHistogram.percentile / the long codec's percentile of one decoded column value
+ * (with the codec id byte); -1 = the column does not decode (it would be dropped). */
+int ref_hist_value_percentile(const uint8_t* v, int64_t n, int kind, double p, double* out);
+/* Calendar helpers of refcpu.c for refhist.c: DateTime.previousInterval and one Downsampler
+ * calendar step (weeks: interval * 7 days); 0 or a TSDB_E_* code. */
+int ref_cal_prev_ex(int64_t ts, int64_t n, int unit, const tsdbhip_tz* z, int64_t* out);
+int ref_cal_step_ex(int64_t ts, int unit, int64_t n, const tsdbhip_tz* z, int64_t* out);
+
 int ref_rollup_scan_bounds(const tsdbhip_query* q, const tsdbhip_rollup_interval* iv, int64_t* s_out, int64_t* e_out);
 
 #ifdef __cplusplus

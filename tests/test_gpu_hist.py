@@ -1,0 +1,180 @@
+"""Histogram path on the MI355X: libtsdbhip's k_hist kernels through the C
+ABI (tsdbhip_load_histograms / tsdbhip_hist_run) against the oracle (oracle/refhist.c) and the
+reference's own known answers (tests/golden/histogram.json).  Bit-exact: timestamps, percentile
+values (SimpleHistogram.percentile's int arithmetic and float bucket midpoints, the long codec's
+data * p) and bucket counts."""
+from __future__ import annotations
+
+import zlib
+
+import numpy as np
+import pytest
+
+from opentsdb_amd import histogram as H
+from opentsdb_amd.engine import Engine, EngineError
+from oracle import oracle as O
+from tests import hist_util as U
+
+pytestmark = pytest.mark.gpu
+
+G = U.golden()
+T0 = 1356998400
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("gq", G["queries"], ids=[q["name"] for q in G["queries"]])
+def test_gpu_golden_queries(eng, gq):
+    hb = U.store_batch(G["stores"][gq["store"]])
+    eng.load_histograms(hb)
+    q = U.golden_query(gq)
+    got = eng.run_histogram(q, gq["percentiles"], gq["show_buckets"], gq["span_range"])
+    U.check_golden(got, gq)
+    U.same(got, O.run_hist(hb, q, gq["percentiles"], gq["show_buckets"], gq["span_range"]), gq["name"])
+
+
+QUERIES = [
+    ("raw-sum", dict(agg="sum", ds=None)),
+    ("raw-none", dict(agg="none", ds=None)),
+    ("10s-sum", dict(agg="sum", ds="10s-sum")),
+    ("1m-sum", dict(agg="sum", ds="1m-sum")),
+    ("7m-sum", dict(agg="sum", ds="7m-sum")),
+    ("1h-sum", dict(agg="sum", ds="1h-sum")),
+    ("1m-sum-none", dict(agg="none", ds="1m-sum")),
+    ("1m-p99-groupby", dict(agg="p99", ds="1m-sum")),
+]
+PCTS = [50.0, 95.0, 99.9, 1.0, 100.0, 0.5, 150.0]
+
+
+def run_both(eng, hb, q, pcts, buckets, span_range=None):
+    eng.load_histograms(hb)
+    try:
+        want = O.run_hist(hb, q, pcts, buckets, span_range)
+    except O.OracleError as e:
+        with pytest.raises(EngineError) as ee:
+            eng.run_histogram(q, pcts, buckets, span_range)
+        return e.code, ee.value.code
+    got = eng.run_histogram(q, pcts, buckets, span_range)
+    U.same(got, want)
+    return got
+
+
+@pytest.mark.parametrize("name,kw", QUERIES, ids=[n for n, _ in QUERIES])
+@pytest.mark.parametrize("buckets", [False, True])
+def test_gpu_random_simple(eng, name, kw, buckets):
+    rng = np.random.default_rng(zlib.crc32(name.encode()) % 1000 + 17 * buckets)
+    hb = U.random_store(rng, n_series=7, n_rows=3, period_ms=10000, groups=3, layouts=3)
+    got = run_both(eng, hb, U.query(T0 + 600, T0 + 3 * 3600 - 900, kw["agg"], kw["ds"]), PCTS, buckets)
+    assert isinstance(got, list) and sum(len(g[0].ts) for g in got) > 0
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_gpu_random_wild_buckets_and_counts(eng, seed):
+    """NaN / +-inf / -0.0 bucket bounds (Float.compare order, canonical NaN keys), overlapping
+    buckets, counts above 2^31 and negative (intValue wrap in percentile, long sums), columns
+    holding a subset of their series' layout."""
+    rng = np.random.default_rng(100 + seed)
+    hb = U.random_store(rng, n_series=5, n_rows=2, period_ms=20000, groups=2, layouts=4, wild=True,
+                        big_counts=seed % 2 == 1)
+    for ds in (None, "1m-sum"):
+        run_both(eng, hb, U.query(T0, T0 + 2 * 3600, "sum", ds), PCTS, True)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_gpu_malformed_columns_dropped(eng, seed):
+    rng = np.random.default_rng(200 + seed)
+    hb = U.random_store(rng, n_series=6, n_rows=2, period_ms=15000, groups=2, bad_frac=0.3)
+    for ds in (None, "1m-sum", "0all-sum"):
+        run_both(eng, hb, U.query(T0, T0 + 7200, "sum", ds), [50.0, 99.0], True)
+
+
+def test_gpu_long_codec_and_mixed_codecs(eng):
+    rng = np.random.default_rng(7)
+    # one codec per group (series s is in group s % 2; even series long): no mixing
+    hb = U.random_store(rng, n_series=6, n_rows=2, period_ms=10000, groups=2, long_frac=0.0)
+    run_both(eng, hb, U.query(T0, T0 + 7200, "sum", "1m-sum"), [0.98, 50.0], True)
+    hb = U.random_store(rng, n_series=6, n_rows=2, period_ms=10000, groups=2, long_frac=1.0)
+    run_both(eng, hb, U.query(T0, T0 + 7200, "sum", "1m-sum"), [0.98, 50.0], True)
+    # codecs mixed inside a group: the reference's aggregate throws (ClassCastException or
+    # IllegalArgumentException by receiver); the engine raises IllegalArgumentException
+    hb = U.random_store(rng, n_series=8, n_rows=1, period_ms=10000, groups=1, long_frac=0.5)
+    r = run_both(eng, hb, U.query(T0, T0 + 3600, "sum", "1m-sum"), [50.0], False)
+    if isinstance(r, tuple):
+        assert r[0] in (-9, -3) and r[1] == -3
+
+
+def test_gpu_nonsum_downsampling_null_pointer(eng):
+    rng = np.random.default_rng(8)
+    hb = U.random_store(rng, n_series=3, n_rows=1, period_ms=10000, sparse=0.0, ms_frac=0.0)
+    r = run_both(eng, hb, U.query(T0, T0 + 3600, "sum", "1m-avg"), [50.0], False)
+    assert r == (-10, -10)
+    run_both(eng, hb, U.query(T0, T0 + 3600, "sum", "10s-max"), [50.0], False)   # one point per interval
+
+
+def test_gpu_all_downsampling_ms_query(eng):
+    """0all with millisecond query bounds (the downsampler's query start / end are TsdbQuery's as
+    set): one point per group at the query end (the clone's timestamp)."""
+    rng = np.random.default_rng(9)
+    hb = U.random_store(rng, n_series=5, n_rows=3, period_ms=10000, groups=2)
+    got = run_both(eng, hb, U.query((T0 + 1000) * 1000, (T0 + 9000) * 1000, "sum", "0all-sum"), [50.0, 99.0], True)
+    assert [list(g[0].ts) for g in got] == [[(T0 + 9000) * 1000]] * 2
+    # seconds: the "all" filter compares ms timestamps with second bounds -- nothing (reference quirk)
+    got = run_both(eng, hb, U.query(T0 + 1000, T0 + 9000, "sum", "0all-sum"), [50.0], False)
+    assert all(len(g[0].ts) == 0 for g in got)
+
+
+def test_gpu_duplicate_row_keys_merge(eng):
+    """HistogramSpan.addRow: a row whose key repeats with overlapping timestamps merges into the
+    existing HistogramRowSeq (the earlier point kept on a tie, HistogramRowSeq.addRow :66-105)."""
+    a = [(bytes([6]) + int.to_bytes(t, 2, "big"), U.encode_simple(0, [((1.0, 2.0), t)], 0, 0)) for t in range(0, 3600, 60)]
+    b = [(bytes([6]) + int.to_bytes(t, 2, "big"), U.encode_simple(0, [((1.0, 2.0), 1000 + t)], 0, 0))
+         for t in range(30, 3600, 120)]
+    c = [(bytes([6]) + int.to_bytes(t, 2, "big"), U.encode_simple(0, [((2.0, 3.0), 7)], 0, 0)) for t in range(0, 3600, 600)]
+    hb = H.HostHistBatch.from_rows([[(T0, a), (T0 + 3600, a), (T0, b), (T0, c)]], [0], {0: H.HCODEC_SIMPLE})
+    for ds in (None, "5m-sum"):
+        run_both(eng, hb, U.query(T0, T0 + 7200, "sum", ds), [50.0], True)
+
+
+def test_gpu_unsorted_row_reports_or_matches(eng):
+    """Mixed second / millisecond qualifiers in one row are iterated in column order
+    (HistogramRowSeq does not sort): the engine raises NOT_IMPLEMENTED when a span's outputs
+    leave time order, and otherwise matches."""
+    cols = [(bytes([6, 0, 10]), U.encode_simple(0, [((1.0, 2.0), 1)], 0, 0)),
+            (bytes([6, 0, 0, 0x13, 0x88]), U.encode_simple(0, [((1.0, 2.0), 2)], 0, 0)),   # 5000 ms
+            (bytes([6, 0, 20]), U.encode_simple(0, [((1.0, 2.0), 4)], 0, 0))]
+    hb = H.HostHistBatch.from_rows([[(T0, cols)]], [0], {0: H.HCODEC_SIMPLE})
+    eng.load_histograms(hb)
+    for ds in (None, "1m-sum"):
+        q = U.query(T0, T0 + 3600, "sum", ds)
+        want = O.run_hist(hb, q, [50.0], True)
+        try:
+            got = eng.run_histogram(q, [50.0], True)
+        except EngineError as e:
+            assert e.code == -22 and ds is None
+            continue
+        U.same(got, want)
+
+
+def test_gpu_group_filter_and_empty(eng):
+    """Spans without a group-by tag (-1) drop out; NONE keeps them; empty store."""
+    rng = np.random.default_rng(11)
+    hb = U.random_store(rng, n_series=4, n_rows=1, period_ms=30000, groups=2)
+    hb.group_id[1] = -1
+    for agg in ("sum", "none"):
+        run_both(eng, hb, U.query(T0, T0 + 3600, agg, "1m-sum"), [50.0], True)
+    empty = H.HostHistBatch.from_rows([], [], {0: H.HCODEC_SIMPLE})
+    assert run_both(eng, empty, U.query(T0, T0 + 3600, "sum", None), [50.0], True) == []
+
+
+def test_gpu_larger_store(eng):
+    """100 series x 2 h @ 5 s of 20-bucket histograms (144k columns), 8 groups."""
+    rng = np.random.default_rng(12)
+    hb = U.random_store(rng, n_series=100, n_rows=2, period_ms=5000, groups=8, layouts=5, nb=(18, 22),
+                        sparse=0.05, ms_frac=0.0)
+    for ds in ("1m-sum", "15m-sum", None):
+        run_both(eng, hb, U.query(T0, T0 + 2 * 3600, "sum", ds), [50.0, 90.0, 99.0], ds == "15m-sum")
