@@ -307,12 +307,15 @@ def result_to_series(res: HistResult, percentiles) -> list[list[HistogramDataPoi
     P = res.n_pct
     D = res.n_buckets
     n_all = res.group_ptr[res.n_groups] if res.n_groups else 0
-    ts_all = np.ctypeslib.as_array(res.ts_ms, (max(1, n_all),))[:n_all].copy()
-    pct_all = np.ctypeslib.as_array(res.pct, (max(1, n_all * P),))[:n_all * P].reshape(n_all, P).copy() if P else None
-    kind_all = np.ctypeslib.as_array(res.codec, (max(1, n_all),))[:n_all].copy()
-    if res.show_buckets:
-        cnt_all = np.ctypeslib.as_array(res.count, (max(1, n_all * (D + 2)),))[:n_all * (D + 2)].reshape(n_all, D + 2)
-        pres_all = np.ctypeslib.as_array(res.present, (max(1, n_all * D),))[:n_all * D].reshape(n_all, D)
+
+    def arr(ptr, n, dtype):
+        return np.ctypeslib.as_array(ptr, (n,)).copy() if n else np.zeros(0, dtype)
+    ts_all = arr(res.ts_ms, n_all, np.int64)
+    pct_all = arr(res.pct, n_all * P, np.float64).reshape(n_all, P) if P else None
+    kind_all = arr(res.codec, n_all, np.uint8)
+    if res.show_buckets and n_all:
+        cnt_all = arr(res.count, n_all * (D + 2), np.int64).reshape(n_all, D + 2)
+        pres_all = arr(res.present, n_all * D, np.uint8).reshape(n_all, D)
         lo = [res.bucket_lower[d] for d in range(D)]
         up = [res.bucket_upper[d] for d in range(D)]
     for g in range(res.n_groups):
@@ -322,7 +325,7 @@ def result_to_series(res: HistResult, percentiles) -> list[list[HistogramDataPoi
         series = []
         for j, p in enumerate(percentiles):
             series.append(HistogramDataPoints(gid, ts, pct_all[a:b, j].copy(), np.zeros(b - a, np.uint8), percentile=p))
-        if res.show_buckets and b > a and kind_all[a] == HCODEC_SIMPLE:
+        if res.show_buckets and b > a and kind_all[a] == HCODEC_SIMPLE:   # (n_all > 0 here)
             first = [d for d in range(D) if pres_all[a, d]]
             keys = [(BK_UNDER, 0, 0)] + [(BK_REG, lo[d], up[d]) for d in first] + [(BK_OVER, 0, 0)]
             vals = np.zeros((len(keys), b - a), np.int64)
