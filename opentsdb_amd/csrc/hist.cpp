@@ -56,7 +56,8 @@ struct Buf {
 struct HistStore {
   bool loaded = false;
   int64_t n_series = 0, n_cells = 0, n_pos = 0;
-  Buf val, voff, codec, status, hkey, hcount, hidx, dlo, dup;
+  Buf val, voff, codec, status, hkey, hcount, hidx, dlo, dup, lkey, lidx;
+  bool lds_dict = false;                        // the dictionary fits the LDS table of k_hist_accum
   Buf pos_cell, pos_ts, pos_kind, row_pos;
   int32_t D = 0;
   int64_t max_ts = 0;                           // largest datapoint timestamp of the store (ms)
@@ -71,7 +72,7 @@ struct HistStore {
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   void release() {
-    for (Buf* b : {&val, &voff, &codec, &status, &hkey, &hcount, &hidx, &dlo, &dup, &pos_cell, &pos_ts, &pos_kind,
+    for (Buf* b : {&val, &voff, &codec, &status, &hkey, &hcount, &hidx, &dlo, &dup, &lkey, &lidx, &pos_cell, &pos_ts, &pos_kind,
                    &row_pos, &q_rlo, &q_rhi, &q_out, &q_slot, &q_key, &q_key2, &q_pos, &q_pos2, &q_head, &q_incl,
                    &q_point, &q_ptts, &q_ptgrp, &acc, &pres, &pkind, &flag, &ptout, &err, &pct, &o_ts, &o_grp,
                    &o_kind, &o_pct, &o_cnt, &o_pres})
@@ -213,6 +214,26 @@ extern "C" int tsdbhip_load_histograms(tsdbhip_ctx* c, const tsdbhip_hist_batch*
   if (S->D) {
     HOK(hipMemcpyAsync(S->dlo.p, S->h_dlo.data(), S->D * 4, hipMemcpyHostToDevice, st));
     HOK(hipMemcpyAsync(S->dup.p, S->h_dup.data(), S->D * 4, hipMemcpyHostToDevice, st));
+  }
+  // the dictionary as the LDS hash table of k_hist_accum (same hash, HIST_LDICT slots)
+  S->lds_dict = S->D <= HIST_LDICT / 2;
+  if (S->lds_dict) {
+    std::vector<uint64_t> lk(HIST_LDICT, HK_EMPTY);
+    std::vector<int32_t> li(HIST_LDICT, -1);
+    for (int32_t d = 0; d < S->D; d++) {
+      const uint64_t key = ((uint64_t)S->h_dlo[d] << 32) | S->h_dup[d];
+      uint64_t h = key;
+      h ^= h >> 33; h *= 0xff51afd7ed558ccdULL; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ULL; h ^= h >> 33;
+      uint32_t slot = (uint32_t)(h & (HIST_LDICT - 1));
+      while (lk[slot] != HK_EMPTY) slot = (slot + 1) & (HIST_LDICT - 1);
+      lk[slot] = key;
+      li[slot] = d;
+    }
+    HOK(S->lkey.ensure(HIST_LDICT * 8));
+    HOK(S->lidx.ensure(HIST_LDICT * 4));
+    HOK(hipMemcpyAsync(S->lkey.p, lk.data(), HIST_LDICT * 8, hipMemcpyHostToDevice, st));
+    HOK(hipMemcpyAsync(S->lidx.p, li.data(), HIST_LDICT * 4, hipMemcpyHostToDevice, st));
+    HOK(hipStreamSynchronize(st));
   }
   // 3. host: spans (SaltScanner.processRow -> HistogramSpan.addRow, rows sorted by base time)
   std::vector<int64_t> pos_cell, pos_ts, row_pos{0};
@@ -436,7 +457,7 @@ int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end,
     HOK(hipMemsetAsync(S->pres.p, 0, n_points * p.W * 4 + 4, st));
     p.pres = S->pres.as<uint32_t>();
   }
-  HOK(hist_accum(p, NP, st));
+  HOK(hist_accum(p, NP, S->lds_dict ? S->lkey.as<uint64_t>() : nullptr, S->lds_dict ? S->lidx.as<int32_t>() : nullptr, st));
   HOK(S->flag.ensure(n_points * 4 + 4));
   HOK(S->ptout.ensure(n_points * 8 + 16));
   HOK(hist_flags(p, S->flag.as<uint32_t>(), st));

@@ -82,7 +82,9 @@ struct HistQueryParams {
 
 hipError_t hist_validate(const HistLoadParams& p, hipStream_t s);
 hipError_t hist_slots(const HistQueryParams& p, hipStream_t s);
-hipError_t hist_accum(const HistQueryParams& p, int64_t n_pos, hipStream_t s);
+// lkey / lidx: the dictionary as an LDICT-slot table for LDS (k_hist.hip), or null
+hipError_t hist_accum(const HistQueryParams& p, int64_t n_pos, const uint64_t* lkey, const int32_t* lidx, hipStream_t s);
+static constexpr int HIST_LDICT = 1024;
 hipError_t hist_flags(const HistQueryParams& p, uint32_t* flag, hipStream_t s);   // [n_points] 1 = emitted
 hipError_t hist_final(const HistQueryParams& p, hipStream_t s);
 hipError_t hist_scan(const uint32_t* flag, int64_t* out, int64_t n, void** tmp, size_t* tmp_bytes, hipStream_t s);

@@ -223,8 +223,11 @@ __global__ void k_hist_slots(HistQueryParams p) {
   }
 }
 
-// segmented (by equal address) inclusive sum over the wave; returns true on the run's last lane
-__device__ __forceinline__ bool seg_sum(uint64_t addr, uint64_t& v) {
+// segmented (by equal address) inclusive scan over the wave (runs of equal addr are contiguous
+// lanes in the common case; equal addresses further apart only cost extra atomics); returns true
+// on the run's last lane
+template <class T, class Op>
+__device__ __forceinline__ bool seg_scan(uint64_t addr, T& v, Op op) {
   const int lane = __lane_id();
   const uint64_t left = __shfl_up(addr, 1);
   const bool head = lane == 0 || left != addr;
@@ -233,42 +236,82 @@ __device__ __forceinline__ bool seg_sum(uint64_t addr, uint64_t& v) {
   const int start = 63 - __builtin_clzll(upto);
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t o = __shfl_up(v, d);
-    if (lane - d >= start) v += o;
+    const T o = __shfl_up(v, d);
+    if (lane - d >= start) v = op(v, o);
   }
   const uint64_t right = __shfl_down(addr, 1);
   return lane == 63 || right != addr;
 }
+struct OpAdd { __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return a + b; } };
+struct OpOr { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a | b; } };
 
-__global__ void __launch_bounds__(256) k_hist_accum(HistQueryParams p, int64_t n_pos) {
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool in = q < n_pos;
-  int32_t pt = -1;
-  if (in) pt = p.pos_point ? p.pos_point[q] : p.pos_slot[q];
-  if (__ballot(pt >= 0) == 0) return;
-  const uint8_t* v = nullptr;
-  uint64_t n = 0, i = 3;
-  int cnt = 0;
-  uint8_t kind = 0;
-  if (pt >= 0) {
-    const int64_t c = p.pos_cell[q];
-    const uint64_t o = p.voff[c];
-    n = p.voff[c + 1] - o;
-    v = p.val + o;
-    kind = p.pos_kind[q];
-    atomicOr(&p.pkind[pt], kind == HC_SIMPLE ? 1u : 2u);
-    if (kind == HC_SIMPLE) cnt = (int16_t)(((uint32_t)v[1] << 8) | v[2]);
+// byte sources of a column: the block's LDS stage or global memory
+struct SrcLds {
+  const uint8_t* b;
+  __device__ __forceinline__ uint32_t at(uint64_t i) const { return b[i]; }
+};
+struct SrcGlobal {
+  const uint8_t* b;
+  __device__ __forceinline__ uint32_t at(uint64_t i) const { return b[i]; }
+};
+template <class S>
+__device__ __forceinline__ uint32_t sbe32(const S& s, uint64_t i) {
+  return (s.at(i) << 24) | (s.at(i + 1) << 16) | (s.at(i + 2) << 8) | s.at(i + 3);
+}
+template <class S>
+__device__ __forceinline__ uint64_t svarlong(const S& s, uint64_t& i) {   // the column was validated at load
+  uint64_t r = 0;
+#pragma unroll 1
+  for (int j = 0; j < 8; j++) {
+    const uint32_t b = s.at(i++);
+    r |= (uint64_t)(b & 0x7F) << (7 * j);
+    if (!(b & 0x80)) return r;
   }
+  return r | ((uint64_t)s.at(i++) << 56);
+}
+
+static constexpr int LDICT = 1024;   // LDS dictionary slots (dictionaries of at most LDICT / 2 buckets)
+static constexpr int ATP = 128;      // positions per tile = threads per block
+static constexpr int STAGE_W = 8192; // 32 KB of column bytes staged per tile
+
+struct DictLds {
+  const uint64_t* key;
+  const int32_t* idx;
+  __device__ __forceinline__ int32_t find(uint64_t k) const {
+    uint32_t slot = (uint32_t)(hk_hash(k) & (LDICT - 1));
+#pragma unroll 1
+    for (int probe = 0; probe < LDICT; probe++) {
+      const uint64_t cur = key[slot];
+      if (cur == k) return idx[slot];
+      if (cur == HK_EMPTY) return -1;
+      slot = (slot + 1) & (LDICT - 1);
+    }
+    return -1;
+  }
+};
+struct DictGlobal {
+  const HistQueryParams* p;
+  __device__ __forceinline__ int32_t find(uint64_t k) const { return dict_index(*p, k); }
+};
+
+// One column per lane (pt < 0: no column); the wave's lanes step through their buckets together.
+template <class S, class Dict>
+__device__ __forceinline__ void accum_columns(const HistQueryParams& p, int32_t pt, const S& src, uint64_t i0,
+                                              uint8_t kind, const Dict& dict) {
+  int cnt = 0;
+  uint64_t i = i0 + 3;
+  if (pt >= 0 && kind == HC_SIMPLE) cnt = (int16_t)((src.at(i0 + 1) << 8) | src.at(i0 + 2));
   const uint64_t base = (uint64_t)(pt >= 0 ? pt : 0) * (uint64_t)p.C;
-  // long codec data (LongHistogramDataPointForTest.aggregate: data + other)
-  {
+  {  // codec bits of the point, and the long codec's data (LongHistogramDataPointForTest.aggregate)
+    uint32_t kb = pt >= 0 ? (kind == HC_SIMPLE ? 1u : 2u) : 0u;
+    const uint64_t paddr = pt >= 0 ? (uint64_t)pt : ~0ull;
+    if (seg_scan(paddr, kb, OpOr()) && pt >= 0) atomicOr(&p.pkind[pt], kb);
     uint64_t val = 0, addr = ~0ull;
     if (pt >= 0 && kind == HC_LONG) {
-      for (int j = 1; j < 9; j++) val = (val << 8) | v[j];
+      for (int j = 1; j < 9; j++) val = (val << 8) | src.at(i0 + j);
       addr = base + p.C - 1;
     }
-    const bool tail = seg_sum(addr, val);
-    if (tail && addr != ~0ull) atomicAdd((unsigned long long*)&p.acc[addr], (unsigned long long)val);
+    if (seg_scan(addr, val, OpAdd()) && addr != ~0ull) atomicAdd((unsigned long long*)&p.acc[addr], (unsigned long long)val);
   }
   int maxc = cnt;
 #pragma unroll
@@ -279,26 +322,69 @@ __global__ void __launch_bounds__(256) k_hist_accum(HistQueryParams p, int64_t n
     uint64_t addr = ~0ull, val = 0;
     int32_t di = -1;
     if (j < cnt) {
-      const uint64_t key = ((uint64_t)fcanon(be32(v + i)) << 32) | fcanon(be32(v + i + 4));
+      const uint64_t key = ((uint64_t)fcanon(sbe32(src, i)) << 32) | fcanon(sbe32(src, i + 4));
       i += 8;
-      varlong(v, n, i, val);
-      di = dict_index(p, key);
+      val = svarlong(src, i);
+      di = dict.find(key);
       if (di < 0) set_err(p.err, -22, WHY_DICT);
       else addr = base + (uint64_t)di;
     }
-    const bool tail = seg_sum(addr, val);
-    if (tail && addr != ~0ull) atomicAdd((unsigned long long*)&p.acc[addr], (unsigned long long)val);
+    if (seg_scan(addr, val, OpAdd()) && addr != ~0ull) atomicAdd((unsigned long long*)&p.acc[addr], (unsigned long long)val);
     if (p.pres && di >= 0) atomicOr(&p.pres[(uint64_t)pt * p.W + (di >> 5)], 1u << (di & 31));
   }
-  // underflow, overflow (:256-257)
-  for (int u = 0; u < 2; u++) {
+  for (int u = 0; u < 2; u++) {   // underflow, overflow (:256-257)
     uint64_t addr = ~0ull, val = 0;
     if (pt >= 0 && kind == HC_SIMPLE) {
-      varlong(v, n, i, val);
+      val = svarlong(src, i);
       addr = base + (uint64_t)p.D + u;
     }
-    const bool tail = seg_sum(addr, val);
-    if (tail && addr != ~0ull) atomicAdd((unsigned long long*)&p.acc[addr], (unsigned long long)val);
+    if (seg_scan(addr, val, OpAdd()) && addr != ~0ull) atomicAdd((unsigned long long*)&p.acc[addr], (unsigned long long)val);
+  }
+}
+
+// Persistent blocks over tiles of ATP consecutive positions.  A tile whose columns are
+// consecutive in the store and fit STAGE_W words is staged into LDS with coalesced dword loads
+// and parsed there; other tiles parse from global memory.  Small dictionaries live in LDS.
+template <bool LDSDICT>
+__global__ void __launch_bounds__(ATP) k_hist_accum(HistQueryParams p, int64_t n_pos, const uint64_t* lkey_g,
+                                                    const int32_t* lidx_g) {
+  __shared__ uint32_t stage[STAGE_W];
+  __shared__ uint64_t lkey[LDSDICT ? LDICT : 1];
+  __shared__ int32_t lidx[LDSDICT ? LDICT : 1];
+  const int tid = threadIdx.x;
+  if (LDSDICT) {
+    for (int k = tid; k < LDICT; k += ATP) { lkey[k] = lkey_g[k]; lidx[k] = lidx_g[k]; }
+  }
+  const int64_t n_tiles = (n_pos + ATP - 1) / ATP;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int64_t p0 = tile * ATP, q = p0 + tid;
+    const int64_t m = min((int64_t)ATP, n_pos - p0);
+    const bool in = tid < m;
+    int32_t pt = -1;
+    if (in) pt = p.pos_point ? p.pos_point[q] : p.pos_slot[q];
+    __syncthreads();   // the previous tile's stage is consumed (and the dictionary is loaded)
+    if (!__syncthreads_or(pt >= 0)) continue;
+    const int64_t c0 = p.pos_cell[p0];
+    const int64_t c = in ? p.pos_cell[q] : c0 + tid;
+    const bool contiguous = __syncthreads_and(c == c0 + tid);
+    const uint64_t b0 = p.voff[c0], b1 = contiguous ? p.voff[c0 + m] : b0;
+    const uint64_t w0 = b0 >> 2, w1 = (b1 + 3) >> 2;
+    const bool staged = contiguous && (w1 - w0) <= (uint64_t)STAGE_W;
+    const uint8_t kind = pt >= 0 ? p.pos_kind[q] : 0;
+    if (staged) {
+      const uint32_t* g = reinterpret_cast<const uint32_t*>(p.val) + w0;
+      for (uint64_t w = tid; w < w1 - w0; w += ATP) stage[w] = g[w];
+      __syncthreads();
+      const SrcLds src{reinterpret_cast<const uint8_t*>(stage)};
+      const uint64_t i0 = pt >= 0 ? p.voff[c] - (w0 << 2) : 0;
+      if (LDSDICT) accum_columns(p, pt, src, i0, kind, DictLds{lkey, lidx});
+      else accum_columns(p, pt, src, i0, kind, DictGlobal{&p});
+    } else {
+      const SrcGlobal src{p.val};
+      const uint64_t i0 = pt >= 0 ? p.voff[c] : 0;
+      if (LDSDICT) accum_columns(p, pt, src, i0, kind, DictLds{lkey, lidx});
+      else accum_columns(p, pt, src, i0, kind, DictGlobal{&p});
+    }
   }
 }
 
@@ -433,9 +519,14 @@ hipError_t hist_slots(const HistQueryParams& p, hipStream_t s) {
   hipLaunchKernelGGL(k_hist_slots, dim3((unsigned)((p.n_spans + 127) / 128)), dim3(128), 0, s, p);
   return hipGetLastError();
 }
-hipError_t hist_accum(const HistQueryParams& p, int64_t n_pos, hipStream_t s) {
+hipError_t hist_accum(const HistQueryParams& p, int64_t n_pos, const uint64_t* lkey, const int32_t* lidx, hipStream_t s) {
   if (n_pos <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_hist_accum, dim3((unsigned)((n_pos + 255) / 256)), dim3(256), 0, s, p, n_pos);
+  const int64_t tiles = (n_pos + ATP - 1) / ATP;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const unsigned grid = (unsigned)std::min<int64_t>(tiles, (int64_t)cus * 4);
+  if (lkey) hipLaunchKernelGGL(k_hist_accum<true>, dim3(grid), dim3(ATP), 0, s, p, n_pos, lkey, lidx);
+  else hipLaunchKernelGGL(k_hist_accum<false>, dim3(grid), dim3(ATP), 0, s, p, n_pos, lkey, lidx);
   return hipGetLastError();
 }
 hipError_t hist_flags(const HistQueryParams& p, uint32_t* flag, hipStream_t s) {

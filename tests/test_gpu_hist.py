@@ -178,3 +178,14 @@ def test_gpu_larger_store(eng):
                         sparse=0.05, ms_frac=0.0)
     for ds in ("1m-sum", "15m-sum", None):
         run_both(eng, hb, U.query(T0, T0 + 2 * 3600, "sum", ds), [50.0, 90.0, 99.0], ds == "15m-sum")
+
+
+@pytest.mark.parametrize("layouts,nb", [(70, (8, 14)), (2, (40, 60))], ids=["dict-over-lds", "wide-columns"])
+def test_gpu_accum_fallback_paths(eng, layouts, nb):
+    """k_hist_accum's other paths: a dictionary larger than its LDS table (> 512 buckets: global
+    hash lookups) and tiles whose columns overflow the 32 KB LDS stage (parsed from global)."""
+    rng = np.random.default_rng(300 + layouts)
+    hb = U.random_store(rng, n_series=layouts, n_rows=1, period_ms=20000, groups=3, layouts=layouts, nb=nb,
+                        ms_frac=0.0)
+    for ds in (None, "2m-sum"):
+        run_both(eng, hb, U.query(T0, T0 + 3600, "sum", ds), [50.0, 99.0], True)
