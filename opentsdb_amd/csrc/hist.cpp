@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <numeric>
@@ -457,6 +458,7 @@ int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end,
     HOK(hipMemsetAsync(S->pres.p, 0, n_points * p.W * 4 + 4, st));
     p.pres = S->pres.as<uint32_t>();
   }
+  if (const char* dbg = getenv("TSDBHIP_HIST_DBG")) p.dbg = atoi(dbg);
   HOK(hist_accum(p, NP, S->lds_dict ? S->lkey.as<uint64_t>() : nullptr, S->lds_dict ? S->lidx.as<int32_t>() : nullptr, st));
   HOK(S->flag.ensure(n_points * 4 + 4));
   HOK(S->ptout.ensure(n_points * 8 + 16));

@@ -78,6 +78,7 @@ struct HistQueryParams {
   uint8_t* out_kind;
   int64_t* out_count;        // [n_out * (D + 2)] (show_buckets)
   uint8_t* out_present;      // [n_out * D]
+  int32_t dbg;               // profiling switches (TSDBHIP_HIST_DBG; results invalid): 1 skip the bucket atomics
 };
 
 hipError_t hist_validate(const HistLoadParams& p, hipStream_t s);

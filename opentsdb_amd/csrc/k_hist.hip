@@ -329,7 +329,8 @@ __device__ __forceinline__ void accum_columns(const HistQueryParams& p, int32_t 
       if (di < 0) set_err(p.err, -22, WHY_DICT);
       else addr = base + (uint64_t)di;
     }
-    if (seg_scan(addr, val, OpAdd()) && addr != ~0ull) atomicAdd((unsigned long long*)&p.acc[addr], (unsigned long long)val);
+    if (seg_scan(addr, val, OpAdd()) && addr != ~0ull && !(p.dbg & 1))
+      atomicAdd((unsigned long long*)&p.acc[addr], (unsigned long long)val);
     if (p.pres && di >= 0) atomicOr(&p.pres[(uint64_t)pt * p.W + (di >> 5)], 1u << (di & 31));
   }
   for (int u = 0; u < 2; u++) {   // underflow, overflow (:256-257)
