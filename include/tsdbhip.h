@@ -482,6 +482,48 @@ int tsdbhip_hist_run_range(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t sta
                            const float* pct, int show_buckets, tsdbhip_hist_result** out);
 void tsdbhip_hist_result_free(tsdbhip_hist_result* r);
 
+/* ---- expression functions over query results ----------------------
+ * The graphite-style functions of src/query/expression/ (ExpressionFactory.java:41-63) run over
+ * the DataPoints a query returned.  Input: n_series result series as flat arrays (series i owns
+ * points [ptr[i], ptr[i + 1]) of ts / bits / is_int, the tsdbhip_result layout); output: a
+ * tsdbhip_result with one group per output series (group_id = its index).
+ *
+ * tsdbhip_expr_map, one output series per input series:
+ *   TSDB_EXPR_SCALE         Scale.scale (Scale.java:86-112): a long times an integral factor stays a
+ *                           long ((long) factor * v, Java wrap), everything else factor * v as double
+ *   TSDB_EXPR_ABSOLUTE      Absolute.abs (Absolute.java:64-83): Math.abs of the long or the double
+ *   TSDB_EXPR_SHIFT         TimeShift.shift (TimeShift.java:121-141): ts + iparam ms, longValue()
+ *                           (a double point raises ClassCastException, as MutableDataPoint does)
+ *   TSDB_EXPR_MOVING_AVG    MovingAverage (MovingAverage.java:60-123, MovingAverageAggregator
+ *                           :190-330) through a one-span AggregationIterator over [start, end]:
+ *                           the mean of the last iparam non-NaN values (fparam = 0) or of the
+ *                           points within iparam ms (fparam = 1, the first point 0), newest first
+ * tsdbhip_expr_zip: ExpressionIterator (ExpressionIterator.java:282-318) as EDPtoDPS iterates it
+ *   (EDPtoDPS.java:148-160): per joined set j the variables' series (set_series[j * n_vars + v],
+ *   -1: the variable has no series with that set's tags) are read position by position, the
+ *   timestamp is the smallest of the present series', a NaN value is the variable's fill value
+ *   (TimeSyncedIterator's NumericFillPolicy, ZERO by default), an absent variable reads 0; a
+ *   present series that ends before another raises RuntimeException ("No more elements",
+ *   TimeSyncedIterator.java:152-160).  The expression is a postfix program over doubles (JEXL 2.1.1
+ *   arithmetic on Doubles: + - * / % and negation; / and % by zero raise ArithmeticException,
+ *   reported as TSDB_E_RUNTIME). */
+enum { TSDB_EXPR_SCALE = 0, TSDB_EXPR_ABSOLUTE, TSDB_EXPR_SHIFT, TSDB_EXPR_MOVING_AVG };
+enum { TSDB_XOP_VAR = 0, TSDB_XOP_CONST, TSDB_XOP_ADD, TSDB_XOP_SUB, TSDB_XOP_MUL, TSDB_XOP_DIV, TSDB_XOP_MOD,
+       TSDB_XOP_NEG };
+typedef struct {
+  int64_t n_series;
+  const int64_t* ptr;          /* [n_series + 1] */
+  const int64_t* ts_ms;
+  const uint64_t* value_bits;  /* longValue() or doubleToRawLongBits(doubleValue()) */
+  const uint8_t* is_int;
+} tsdbhip_series_set;
+int tsdbhip_expr_map(tsdbhip_ctx* ctx, int fn, double fparam, int64_t iparam, int64_t start_ms, int64_t end_ms,
+                     const tsdbhip_series_set* in, tsdbhip_result** out);
+/* program: n_ops (op, arg) pairs -- arg = variable index (TSDB_XOP_VAR) or constant index */
+int tsdbhip_expr_zip(tsdbhip_ctx* ctx, const int32_t* program, int n_ops, const double* consts, int n_vars,
+                     int64_t n_sets, const int32_t* set_series, const double* var_fill, const tsdbhip_series_set* in,
+                     tsdbhip_result** out);
+
 /* Device synchronisation helper for host code that does not use HIP directly. */
 int tsdbhip_sync(tsdbhip_ctx* ctx);
 

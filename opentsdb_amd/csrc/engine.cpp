@@ -3449,6 +3449,11 @@ extern "C" int tsdbhip_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n,
 
 extern "C" void tsdbhip_result_free(tsdbhip_result* r) { result_free(r); }
 
+// result allocation for the expression functions' translation unit (expr.cpp)
+namespace tsdb {
+tsdbhip_result* new_result(int64_t n_groups, int64_t n_points) { return make_result(n_groups, n_points); }
+}  // namespace tsdb
+
 extern "C" int tsdbhip_last_timing(tsdbhip_ctx* c, tsdbhip_timing* out) {
   if (!c || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   *out = c->timing;

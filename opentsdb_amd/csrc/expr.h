@@ -1,0 +1,51 @@
+// expr.h -- internal declarations of the expression functions shared by
+// expr.cpp and k_expr.hip.  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tsdb {
+
+static constexpr int EXPR_STACK = 32;   // postfix program depth
+
+struct ExprMapParams {
+  int64_t n;                 // points
+  const int64_t* ts;
+  const uint64_t* bits;
+  const uint8_t* is_int;
+  const int64_t* lo;         // moving average: first emitted point of the point's series (-1: not emitted)
+  int32_t fn;
+  double fparam;
+  int32_t scale_is_int;      // Scale: factor == floor(factor) && !isInfinite(factor)
+  int32_t time_window;       // moving average: window in ms (else a point count)
+  int64_t iparam;
+  int64_t* out_ts;
+  uint64_t* out_bits;
+  uint8_t* out_int;
+  int32_t* err;
+};
+
+struct ExprZipParams {
+  const int32_t* prog;       // [2 * n_ops]
+  int32_t n_ops;
+  const double* consts;
+  int32_t n_vars;
+  int64_t n_sets;
+  const int32_t* set_series; // [n_sets * n_vars]
+  const double* var_fill;    // [n_vars]
+  const int64_t* ptr;        // input series
+  const int64_t* ts;
+  const uint64_t* bits;
+  const uint8_t* is_int;
+  const int64_t* set_off;    // [n_sets + 1] output offsets
+  int64_t n_out;
+  int64_t* out_ts;
+  uint64_t* out_bits;
+  uint8_t* out_int;
+  int32_t* err;
+};
+
+hipError_t expr_map(const ExprMapParams& p, hipStream_t s);
+hipError_t expr_zip(const ExprZipParams& p, hipStream_t s);
+
+}  // namespace tsdb

@@ -1480,7 +1480,20 @@ __global__ __launch_bounds__(256) void k_ordered(OrdParams p) {
   RegPart R;
   regpart_init(p.ga, R);
   const int64_t s1 = p.group_series_ptr[g + 1];
-  for (int64_t s = p.group_series_ptr[g]; s < s1; s++) {
+  // The fold is a dependent chain over the group's spans, and only G * K threads run it: issue
+  // ORD_U independent loads ahead of each ORD_U-step fold so the chain waits on one memory
+  // latency per ORD_U spans instead of one per span (same fold order).
+  constexpr int ORD_U = 16;
+  int64_t s = p.group_series_ptr[g];
+  for (; s + ORD_U <= s1; s += ORD_U) {
+    double v[ORD_U];
+#pragma unroll
+    for (int u = 0; u < ORD_U; u++) v[u] = p.vals[(s + u) * p.K + k];
+#pragma unroll
+    for (int u = 0; u < ORD_U; u++)
+      if ((uint64_t)__double_as_longlong(v[u]) != 0x7FF87FF87FF87FF8ULL) contribute_slot(p.ga, R, v[u], false);
+  }
+  for (; s < s1; s++) {
     const double v = p.vals[s * p.K + k];
     if ((uint64_t)__double_as_longlong(v) == 0x7FF87FF87FF87FF8ULL) continue;
     contribute_slot(p.ga, R, v, false);

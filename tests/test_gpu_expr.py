@@ -1,0 +1,159 @@
+"""Expression functions on the MI355X: k_expr through the C ABI
+(tsdbhip_expr_map / tsdbhip_expr_zip, driven by opentsdb_amd.expression) against the reference's
+known answers (tests/golden/expression.json) and the oracle (oracle/expr.py), bit for bit."""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import pytest
+
+from opentsdb_amd import expression as X
+from opentsdb_amd.engine import Engine, EngineError
+from oracle import expr as OX
+from tests import expr_util as U
+
+pytestmark = pytest.mark.gpu
+
+G = U.golden()
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def as_series(sub):
+    return [X.Series.of([tuple(p) for p in s]) for s in sub]
+
+
+def run_engine(eng, case):
+    subs = [as_series(sub) for sub in case["inputs"]]
+    fn = case["fn"]
+    if fn == "scale":
+        out = X.scale(eng, subs, case["params"])
+    elif fn == "absolute":
+        out = X.absolute(eng, subs)
+    elif fn == "movingAverage":
+        out = X.moving_average(eng, subs, case["params"], case["start"], case["end"])
+    else:
+        out = X.FUNCTIONS[fn](eng, subs)
+    return [list(zip([int(t) for t in s.ts], s.values())) for s in out]
+
+
+def same(got, want):
+    assert len(got) == len(want)
+    for g, w in zip(got, want):
+        assert len(g) == len(w)
+        for (gt, gv), (wt, wv) in zip(g, w):
+            assert gt == wt
+            assert type(gv) is type(wv) or (isinstance(gv, float) and isinstance(wv, float)), (gv, wv)
+            if isinstance(wv, float):
+                assert np.float64(gv).view(np.uint64) == np.float64(wv).view(np.uint64) or (math.isnan(gv) and math.isnan(wv)), (gv, wv)
+            else:
+                assert gv == wv
+
+
+@pytest.mark.parametrize("case", G["cases"], ids=[c["name"] for c in G["cases"]])
+def test_gpu_known_answers(eng, case):
+    got = run_engine(eng, case)
+    U.check(got, case)
+    same(got, U.oracle_run(case))
+
+
+def rand_series(rng, n, kind, t0=1356998400000, period=10000):
+    ts = t0 + np.cumsum(rng.integers(1, 3, n)) * period
+    pts = []
+    for t in ts:
+        if kind == "int":
+            v = int(rng.choice([rng.integers(-1000, 1000), rng.integers(-(1 << 62), 1 << 62)]))
+            pts.append((int(t), v))
+        else:
+            v = float(rng.choice([rng.normal(0, 100), float("nan"), 0.0, -0.0, 1e300]))
+            pts.append((int(t), v))
+    return pts
+
+
+@pytest.mark.parametrize("factor", ["2", "-3", "1.5", "0", "9223372036854775807", "-0.25"])
+def test_gpu_scale_absolute_random(eng, factor):
+    rng = np.random.default_rng(len(factor))
+    raw = [rand_series(rng, 50, "int"), rand_series(rng, 60, "dbl"), rand_series(rng, 7, "int")]
+    subs = [[X.Series.of(p) for p in raw]]
+    got = [list(zip([int(t) for t in s.ts], s.values())) for s in X.scale(eng, subs, [factor])]
+    same(got, [o for o, _ in OX.scale([(p, b"") for p in raw], float(factor))])
+    got = [list(zip([int(t) for t in s.ts], s.values())) for s in X.absolute(eng, subs)]
+    same(got, [o for o, _ in OX.absolute([(p, b"") for p in raw])])
+
+
+@pytest.mark.parametrize("param", ["1", "3", "10", "'1min'", "'5min'", "'1h'"])
+def test_gpu_moving_average_random(eng, param):
+    rng = np.random.default_rng(7 + len(param))
+    raw = [rand_series(rng, 120, "dbl"), rand_series(rng, 90, "int")]
+    t0 = raw[0][5][0]
+    t1 = raw[0][100][0]
+    subs = [[X.Series.of(p) for p in raw]]
+    got = [list(zip([int(t) for t in s.ts], s.values())) for s in X.moving_average(eng, subs, [param], t0, t1)]
+    timed = param.startswith("'")
+    cond = X._mavg_window_ms(param) if timed else int(param)
+    same(got, [o for o, _ in OX.moving_average([(p, b"") for p in raw], cond, timed, t0, t1)])
+
+
+@pytest.mark.parametrize("fn,op", [("sumSeries", "+"), ("diffSeries", "-"), ("multiplySeries", "*")])
+def test_gpu_combine_joined_sets(eng, fn, op):
+    """Three sub-queries with tag-joined series (some keys in one sub-query only: the absent
+    variable reads 0), equal lengths per set, NaN values filled with 0."""
+    rng = np.random.default_rng(len(fn))
+    keys = [b"\x00\x01", b"\x00\x02", b"\x01\x00", b"\xff"]
+    subs, osubs = [], []
+    for v in range(3):
+        lst, olst = [], []
+        for k in keys:
+            if rng.random() < 0.3:
+                continue
+            pts = rand_series(rng, 40 + keys.index(k), "dbl", t0=1356998400000 + v * 7)
+            lst.append(X.Series.of(pts, key=k))
+            olst.append((pts, k))
+        subs.append(lst)
+        osubs.append(olst)
+    got = [list(zip([int(t) for t in s.ts], s.values())) for s in X.FUNCTIONS[fn](eng, subs)]
+    want = [o for o, _ in OX.combine(op, dict(zip("abc", osubs)))]
+    same(got, want)
+
+
+def test_gpu_combine_errors_like_the_reference(eng):
+    a = [X.Series.of([(1, 1.0), (2, 2.0)])]
+    b = [X.Series.of([(1, 1.0)])]
+    with pytest.raises(EngineError) as e:
+        X.sum_series(eng, [a, b])
+    assert e.value.code == -6
+    z = [X.Series.of([(1, 0.0), (2, 1.0)])]
+    with pytest.raises(EngineError) as e:
+        X.divide_series(eng, [a, z])
+    assert e.value.code == -6
+
+
+def test_gpu_evaluate_general_expression(eng):
+    rng = np.random.default_rng(3)
+    pa, pb, pc = (rand_series(rng, 30, "dbl") for _ in range(3))
+    pb = [(t, v if v != 0 else 1.0) for t, v in pb]
+    got = X.evaluate(eng, "a * 2 + -b % 3 - (c + a) / 4", {"a": [X.Series.of(pa)], "b": [X.Series.of(pb)],
+                                                          "c": [X.Series.of(pc)]})
+    vals = got[0].values()
+    for i in range(30):
+        a, b, c = (float(x[i][1]) for x in (pa, pb, pc))
+        a, b, c = (0.0 if math.isnan(x) else x for x in (a, b, c))
+        want = a * 2.0 + math.fmod(-b, 3.0) - (c + a) / 4.0
+        assert np.float64(vals[i]).view(np.uint64) == np.float64(want).view(np.uint64) or (math.isnan(vals[i]) and math.isnan(want))
+    assert list(got[0].ts) == [min(pa[i][0], pb[i][0], pc[i][0]) for i in range(30)]
+
+
+def test_gpu_shift_series(eng):
+    sh = G["timeshift_shift"]
+    for idx, ms, want in sh["cases"]:
+        out = X.shift_series(eng, [X.Series.of([tuple(sh["points"][idx])])], ms)
+        assert int(out[0].ts[0]) == want and out[0].values()[0] == sh["points"][idx][1]
+    with pytest.raises(EngineError) as e:
+        X.shift_series(eng, [X.Series.of([(1, 1.5)])], 1000)
+    assert e.value.code == -9
