@@ -1483,7 +1483,7 @@ __global__ __launch_bounds__(256) void k_ordered(OrdParams p) {
   // The fold is a dependent chain over the group's spans, and only G * K threads run it: issue
   // ORD_U independent loads ahead of each ORD_U-step fold so the chain waits on one memory
   // latency per ORD_U spans instead of one per span (same fold order).
-  constexpr int ORD_U = 16;
+  constexpr int ORD_U = 32;
   int64_t s = p.group_series_ptr[g];
   for (; s + ORD_U <= s1; s += ORD_U) {
     double v[ORD_U];

@@ -8,11 +8,11 @@ the list of sub-query results (each a list of Series) and the string parameters,
 the reference does (IllegalArgumentException -> :class:`ExpressionError`) and run the arithmetic on
 the GPU:
 
-  scale / absolute / shift, timeShift / movingAverage      tsdbhip_expr_map
+  alias / scale / absolute / shift, timeShift / movingAverage   tsdbhip_expr_map
   sumSeries, sum / diffSeries, difference / multiplySeries,  tsdbhip_expr_zip (ExpressionIterator
   multiply / divideSeries, divide / evaluate(expression)     with a UNION of the variables)
 
-alias and highestCurrent / highestMax are not built.
+highestCurrent / highestMax are not built.
 """
 from __future__ import annotations
 
@@ -261,6 +261,21 @@ def absolute(engine, query_results, params=None):
     return _map(engine, EXPR_ABSOLUTE, _flatten(query_results))
 
 
+def alias(engine, query_results, params):
+    """Alias.evaluate (src/query/expression/Alias.java:38-85): every series renamed to the
+    comma-joined parameters -- and, as the reference does (its loop is Absolute's), with the
+    absolute value of every point."""
+    if not query_results:
+        return []
+    if not params:
+        raise ExpressionError("IllegalArgumentException", "Missing the alias")
+    out = _map(engine, EXPR_ABSOLUTE, _flatten(query_results))
+    name = ",".join(params)
+    for s in out:
+        s.name = name
+    return out
+
+
 def _mavg_window_ms(param):
     """MovingAverage.parseParam (MovingAverage.java:125-160): "'<n><unit>'"."""
     idx = 0
@@ -364,7 +379,7 @@ multiply_series = _combine("*", "multiplySeries")
 divide_series = _combine("/", "divideSeries")
 
 FUNCTIONS = {
-    "scale": scale, "absolute": absolute, "movingAverage": moving_average, "shift": shift, "timeShift": shift,
+    "alias": alias, "scale": scale, "absolute": absolute, "movingAverage": moving_average, "shift": shift, "timeShift": shift,
     "divideSeries": divide_series, "divide": divide_series, "sumSeries": sum_series, "sum": sum_series,
     "diffSeries": diff_series, "difference": diff_series, "multiplySeries": multiply_series,
     "multiply": multiply_series,

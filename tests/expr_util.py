@@ -21,8 +21,8 @@ def oracle_run(case):
     flat = [s for sub in subs for s in sub]
     if fn == "scale":
         out = OX.scale(flat, float(params[0]))
-    elif fn == "absolute":
-        out = OX.absolute(flat)
+    elif fn in ("absolute", "alias"):
+        out = OX.absolute(flat)   # Alias.java's loop is Absolute's
     elif fn == "movingAverage":
         p = params[0]
         if p.startswith("'"):

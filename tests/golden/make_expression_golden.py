@@ -8,6 +8,7 @@ assert (their loops evaluated here), with the test's tolerance.
 
   test/query/expression/TestScale.java ......... evaluateFactor* (6)
   test/query/expression/TestAbsolute.java ...... evaluate*GroupBy* (4)
+  test/query/expression/TestAlias.java ......... evaluate* (3)
   test/query/expression/TestMovingAverage.java . evaluateWindow* (9) and evaluateGroupBy
   test/query/expression/TestSumSeries.java / TestDiffSeries.java / TestMultiplySeries.java /
   TestDivideSeries.java ........................ *OneSeriesEach (4)
@@ -63,6 +64,14 @@ def main():
         [[[t, v] for t, v in zip(ts, range(1, 6))], [[t, v] for t, v in zip(ts, range(10, 15))]])
     add("evaluateNegativeGroupByDouble", "TestAbsolute.java:194-230", "absolute", [[a, gen(False, -10, -1)]], [],
         [[[t, v] for t, v in zip(ts, range(1, 6))], [[t, 10.0 + i] for i, t in enumerate(ts)]], tol=0.001)
+    # Alias: renamed, and the absolute value of every point (Alias.java's loop is Absolute's)
+    add("aliasGroupByLong", "TestAlias.java:96-132", "alias", [[a, gen(True, 10, 1)]], ["My Alias"],
+        [[[t, v] for t, v in zip(ts, range(1, 6))], [[t, v] for t, v in zip(ts, range(10, 15))]], alias_name="My Alias")
+    add("aliasGroupByDouble", "TestAlias.java:134-171", "alias", [[a, gen(False, 10, 1)]], ["My Alias"],
+        [[[t, v] for t, v in zip(ts, range(1, 6))], [[t, 10.0 + i] for i, t in enumerate(ts)]], tol=0.001,
+        alias_name="My Alias")
+    add("aliasSubQuerySeries", "TestAlias.java:172-208", "alias", [[a], [gen(True, -10, -1)]], ["My Alias"],
+        [[[t, v] for t, v in zip(ts, range(1, 6))], [[t, v] for t, v in zip(ts, range(10, 15))]], alias_name="My Alias")
     # MovingAverage over [START, START + INTERVAL * N] (the mocked TSQuery)
     win = {
         "evaluateWindow1dps": ("1", "TestMovingAverage.java:81-99", [1, 2, 3, 4, 5]),

@@ -36,6 +36,9 @@ def run_engine(eng, case):
         out = X.scale(eng, subs, case["params"])
     elif fn == "absolute":
         out = X.absolute(eng, subs)
+    elif fn == "alias":
+        out = X.alias(eng, subs, case["params"])
+        assert all(s.name == case["alias_name"] for s in out)
     elif fn == "movingAverage":
         out = X.moving_average(eng, subs, case["params"], case["start"], case["end"])
     else:
