@@ -394,7 +394,7 @@ struct tsdbhip_ctx {
   DevBuf cal_bounds;                                // calendar month / year slot boundaries
   // raw path scratch
   DevBuf r_rowpt, r_spoff, r_spn, r_grp, r_pts, r_rank, r_bm, r_wb, r_U, r_ooff, r_sg, r_su, r_ots, r_obits, r_oint,
-      r_coff, r_cur, r_voff, r_vl, r_vd, r_vp;                   // multi-GPU: this rank's partial states, gathered states
+      r_coff, r_cur, r_voff, r_vl, r_vd, r_vp, r_bnd, r_mts, r_mpos, r_mhead, r_dz;                   // multi-GPU: this rank's partial states, gathered states
   // dominant uniform row class of the batch (k_fast specialisation), 0 = none
   int fast_qw = 0, fast_vl = 0;        // dominant k_fast row class (0 = none)
   int fast_qw2 = 0, fast_vl2 = 0;      // second class, chained over the first one's redo list
@@ -2881,13 +2881,14 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
   std::vector<int64_t> row_pt(std::max<int64_t>(1, c->n_rows), -1), sp_off(S + 1, 0);
   std::vector<int32_t> sp_n(std::max<int64_t>(1, S), 0);
   bool all_s = true, any_int = false, any_float = false;
+  bool uns = false;   // a cell with unsorted datapoints: k_raw_merge walks the greedy steps
   int64_t np = 0;
   for (int64_t s = 0; s < S; s++) {
     sp_off[s] = np;
     for (int64_t r = c->h_srp[s]; r < c->h_srp[s + 1]; r++) {
       if ((int64_t)c->h_base[r] < P.ss || (int64_t)c->h_base[r] >= P.se) continue;
       const uint32_t f = c->h_flags[r];
-      if (f & ROW_UNSORTED) return fail(TSDB_E_NOT_IMPLEMENTED, "raw path over a cell with unsorted datapoints");
+      if (f & ROW_UNSORTED) uns = true;
       if ((f & ROW_QW_MASK) != 2) all_s = false;
       if (f & ROW_ALLF) any_float = true;
       else { any_int = true; if (!(f & ROW_ALLI)) any_float = true; }
@@ -2962,6 +2963,16 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
   rp.do_double = q->rate || any_float;
   if (!rp.do_long && !rp.do_double) rp.do_double = 1;
   rp.err = c->err.as<int32_t>();
+  rp.uns = uns ? 1 : 0;
+  if (uns) {
+    HIP_OK(c->r_mts.ensure(std::max<int64_t>(1, np) * 8));
+    HIP_OK(c->r_mpos.ensure(std::max<int64_t>(1, S) * 4));
+    HIP_OK(c->r_mhead.ensure(std::max<int64_t>(1, S) * 8));
+    HIP_OK(c->r_bnd.ensure((G + 1) * 8));
+    rp.mts = c->r_mts.as<int64_t>();
+    rp.m_pos = c->r_mpos.as<int32_t>();
+    rp.m_head = c->r_mhead.as<int64_t>();
+  }
   HIP_OK(hipEventRecord(c->ev[0], c->stream));
   HIP_OK(launch_raw_decode(rp, c->stream));
   if (q->rate) {
@@ -2971,7 +2982,8 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
   }
   // group chunks whose timestamp bitmaps fit the budget
   const int64_t budget = (int64_t)2 << 30;
-  const int64_t per_chunk = std::max<int64_t>(1, budget / (rp.W * 8));
+  // (the greedy merge keeps no bitmap: one chunk, its step timestamps bounded by the points)
+  const int64_t per_chunk = uns ? std::max<int64_t>(1, G) : std::max<int64_t>(1, budget / (rp.W * 8));
   std::vector<int64_t> res_ts;
   std::vector<uint64_t> res_bits;
   std::vector<uint8_t> res_int;
@@ -2988,14 +3000,27 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
     const int64_t ng = g1 - g0;
     rp.g0 = g0;
     rp.g1 = g1;
-    HIP_OK(c->r_bm.ensure(ng * rp.W * 4));
-    HIP_OK(c->r_wb.ensure(ng * rp.W * 4));
     HIP_OK(c->r_U.ensure(ng * 4));
-    rp.bitmap = c->r_bm.as<uint32_t>();
-    rp.wbase = c->r_wb.as<uint32_t>();
     rp.U = c->r_U.as<int32_t>();
-    HIP_OK(hipMemsetAsync(rp.bitmap, 0, ng * rp.W * 4, c->stream));
-    HIP_OK(launch_raw_union(rp, grp_ser[g0], grp_ser[g1], c->stream));
+    std::vector<int64_t> bnd;   // greedy merge: each group's steps are bounded by its counted points
+    if (uns) {
+      bnd.assign(ng + 1, 0);
+      const int first = q->rate ? 1 : 0;
+      for (int64_t i = 0; i < ng; i++) {
+        bnd[i + 1] = bnd[i];
+        for (int64_t s = grp_ser[g0 + i]; s < grp_ser[g0 + i + 1]; s++) bnd[i + 1] += std::max(0, sp_n[s] - first);
+      }
+      HIP_OK(hipMemcpyAsync(c->r_bnd.p, bnd.data(), (ng + 1) * 8, hipMemcpyHostToDevice, c->stream));
+      rp.bnd_off = c->r_bnd.as<int64_t>();
+      HIP_OK(launch_raw_merge(rp, c->stream));
+    } else {
+      HIP_OK(c->r_bm.ensure(ng * rp.W * 4));
+      HIP_OK(c->r_wb.ensure(ng * rp.W * 4));
+      rp.bitmap = c->r_bm.as<uint32_t>();
+      rp.wbase = c->r_wb.as<uint32_t>();
+      HIP_OK(hipMemsetAsync(rp.bitmap, 0, ng * rp.W * 4, c->stream));
+      HIP_OK(launch_raw_union(rp, grp_ser[g0], grp_ser[g1], c->stream));
+    }
     std::vector<int32_t> U(ng);
     HIP_OK(hipMemcpyAsync(U.data(), rp.U, ng * 4, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
@@ -3033,7 +3058,8 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
     rp.out_ts = c->r_ots.as<int64_t>();
     rp.out_bits = c->r_obits.as<uint64_t>();
     rp.out_int = c->r_oint.as<uint8_t>();
-    HIP_OK(launch_raw_rank(rp, grp_ser[g0], grp_ser[g1], c->stream));
+    if (uns) HIP_OK(launch_raw_merge_ts(rp, c->stream));
+    else HIP_OK(launch_raw_rank(rp, grp_ser[g0], grp_ser[g1], c->stream));
     HIP_OK(launch_raw_cursor(rp, grp_ser[g0], grp_ser[g1], c->stream));
     if (P.gsel) {
       // percentile / median: every span operand of every union point, strip by strip
@@ -3068,6 +3094,11 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
       HIP_OK(hipMemcpyAsync(c->r_voff.p, boff.data(), std::max<int64_t>(1, ns) * 8, hipMemcpyHostToDevice, c->stream));
       HIP_OK(hipStreamSynchronize(c->stream));   // `boff` leaves scope before the chunk's sync
       HIP_OK(hipMemsetAsync(rp.out_int, 1, std::max<int64_t>(1, nout), c->stream));   // isInteger until a double is seen
+      if (uns) {
+        HIP_OK(c->r_dz.ensure(std::max<int64_t>(1, nout)));
+        HIP_OK(hipMemsetAsync(c->r_dz.p, 0, std::max<int64_t>(1, nout), c->stream));
+        rp.dz = c->r_dz.as<uint8_t>();
+      }
       for (size_t bi = 0; bi + 1 < bat.size(); bi++) {
         const int64_t s0 = bat[bi], s1 = bat[bi + 1];
         const int64_t nv = soff[s1] - soff[s0];
@@ -3087,6 +3118,7 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
         // a second selection over the same batch would have to re-stage it.
         HIP_OK(launch_raw_sel(bp, k_max, c->stream));
       }
+      if (uns) HIP_OK(launch_raw_dz_check(rp, nout, c->stream));
     } else {
       HIP_OK(hipEventRecord(c->ev[3], c->stream));
       if (!direct) HIP_OK(launch_raw_eval(rp, c->stream));

@@ -253,6 +253,15 @@ struct RawParams {
   int64_t* vals_l;             // runLong operands
   double* vals_d;              // runDouble operands (NaN = no value; runDouble skips NaNs)
   uint8_t* vals_p;             // 1 = the span has a long operand at the point
+  // cells with unsorted datapoints (k_raw_merge instead of the bitmap union): the greedy
+  // AggregationIterator walk gives every point its step; the evaluation then also meets points
+  // on either end of a span's window and windows with x1 <= x0
+  int32_t uns;
+  const int64_t* bnd_off;      // [g1 - g0] offset of each group's step timestamps in mts
+  int64_t* mts;                // step timestamps, bnd_off layout (a group's points bound its steps)
+  int32_t* m_pos;              // [n_series] next point of the span
+  int64_t* m_head;             // [n_series] timestamp of that point (INT64_MAX: none)
+  uint8_t* dz;                 // [points of the chunk] a long LERP divided by zero (k_raw_vals)
 };
 
 struct SynthParams {
@@ -423,6 +432,9 @@ hipError_t launch_raw_rate(const RawParams& p, hipStream_t s);
 hipError_t launch_raw_union(const RawParams& p, int64_t s_begin, int64_t s_end, hipStream_t s);  // mark + scan
 hipError_t launch_raw_rank(const RawParams& p, int64_t s_begin, int64_t s_end, hipStream_t s);   // rank + union ts
 hipError_t launch_raw_cursor(const RawParams& p, int64_t s_begin, int64_t s_end, hipStream_t s);
+hipError_t launch_raw_merge(const RawParams& p, hipStream_t s);      // unsorted cells: steps, ranks, U
+hipError_t launch_raw_merge_ts(const RawParams& p, hipStream_t s);   // step timestamps -> out_ts
+hipError_t launch_raw_dz_check(const RawParams& p, int64_t n_out, hipStream_t s);
 hipError_t launch_raw_eval(const RawParams& p, hipStream_t s);
 hipError_t launch_raw_vals(const RawParams& p, int64_t k_max, hipStream_t s);
 hipError_t launch_raw_sel(const RawParams& p, int64_t k_max, hipStream_t s);

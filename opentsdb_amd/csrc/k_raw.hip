@@ -274,6 +274,107 @@ __global__ __launch_bounds__(256) void k_raw_cursor(RawParams p, int64_t s_begin
   }
 }
 
+// ---- greedy merge over cells with unsorted datapoints -------------------------------
+// AggregationIterator.next (src/core/AggregationIterator.java:514-567) emits the smallest next
+// timestamp of the group's spans and advances every span whose next point has it; a span's
+// points are consumed in stored order whatever their timestamps (RowSeq.Iterator.next,
+// src/core/RowSeq.java:552-568, does not sort), so over unsorted cells the emitted sequence is
+// not the sorted union and a timestamp may be emitted more than once.  One wave per group
+// walks those steps: lane l keeps the minimum next timestamp of its spans (l, l + 64, ...),
+// the wave minimum is the step's timestamp and the lanes holding it advance their spans.
+// Every counted point gets its step as rank (strictly increasing along a span), so
+// k_raw_cursor and the evaluation kernels run unchanged on top.
+__device__ __forceinline__ int64_t wave_min64(int64_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x = min(x, (int64_t)__shfl_xor((long long)x, d, 64));
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ int64_t merge_head(const RawParams& p, const RawPt* pts, int pos, int n) {
+  if (pos >= n) return INT64_MAX;
+  const int64_t t = pts[pos].tsf & RAW_TIME_MASK;
+  const int64_t bit = (t - p.start_ms) / p.gran;
+  if (t < p.start_ms || bit >= p.W * 32) set_err(p.err, TSDB_E_ILLEGAL_DATA);   // as k_raw_mark
+  return t;
+}
+
+__global__ __launch_bounds__(256) void k_raw_merge(RawParams p) {
+  const int lane = lane_id();
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int first = p.rate ? 1 : 0;   // rate: the constructor pre-advances every span (:448-459)
+  for (int64_t gi = wave; gi < p.g1 - p.g0; gi += nwaves) {
+    const int64_t g = gi + p.g0;
+    const int64_t sb = p.grp_ser[g];
+    const int64_t k = p.grp_ser[g + 1] - sb;
+    int64_t* mts = p.mts + p.bnd_off[gi];
+    if (k == 1) {   // one span: every point is a step of its own, in stored order
+      const int n = p.sp_n[sb];
+      const RawPt* pts = p.pts + p.sp_off[sb];
+      for (int j = first + lane; j < n; j += 64) {
+        mts[j - first] = merge_head(p, pts, j, n);
+        p.rank[p.sp_off[sb] + j] = j - first;
+      }
+      if (lane == 0) p.U[gi] = max(0, n - first);
+      continue;
+    }
+    int64_t lm = INT64_MAX;
+    for (int64_t i = lane; i < k; i += 64) {
+      const int64_t s = sb + i;
+      const int64_t h = merge_head(p, p.pts + p.sp_off[s], first, p.sp_n[s]);
+      p.m_pos[s] = first;
+      p.m_head[s] = h;
+      lm = min(lm, h);
+    }
+    int32_t step = 0;
+    for (;;) {
+      const int64_t m = wave_min64(lm);
+      if (m == INT64_MAX) break;
+      if (lane == 0) mts[step] = m;
+      if (lm == m) {
+        int64_t nm = INT64_MAX;
+        for (int64_t i = lane; i < k; i += 64) {
+          const int64_t s = sb + i;
+          int64_t h = p.m_head[s];
+          if (h == m) {
+            const int pos = p.m_pos[s];
+            p.rank[p.sp_off[s] + pos] = step;
+            h = merge_head(p, p.pts + p.sp_off[s], pos + 1, p.sp_n[s]);
+            p.m_pos[s] = pos + 1;
+            p.m_head[s] = h;
+          }
+          nm = min(nm, h);
+        }
+        lm = nm;
+      }
+      step++;
+    }
+    if (lane == 0) p.U[gi] = step;
+  }
+}
+
+// step timestamps from the per-group bound layout into the output layout
+__global__ __launch_bounds__(256) void k_raw_merge_ts(RawParams p) {
+  const int lane = lane_id();
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t gi = wave; gi < p.g1 - p.g0; gi += nwaves) {
+    const int64_t U = p.U[gi];
+    const int64_t* src = p.mts + p.bnd_off[gi];
+    int64_t* dst = p.out_ts + p.out_off[gi];
+    for (int64_t u = lane; u < U; u += 64) dst[u] = src[u];
+  }
+}
+
+// a long LERP that divided by zero raises ArithmeticException only where nextLongValue ran,
+// i.e. at points whose result is an integer (k_raw_vals records it per point)
+__global__ __launch_bounds__(256) void k_raw_dz_check(RawParams p, int64_t n_out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_out && p.dz[i] && p.out_int[i]) set_err(p.err, TSDB_E_ILLEGAL_STATE);
+}
+
 // ---- launchers --------------------------------------------------------------------
 static unsigned wave_blocks(int64_t n_waves) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n_waves + 3) / 4, 65536));
@@ -309,6 +410,24 @@ hipError_t launch_raw_rank(const RawParams& p, int64_t s_begin, int64_t s_end, h
   }
   const int64_t nw = (p.g1 - p.g0) * p.W;
   if (nw > 0) hipLaunchKernelGGL(k_raw_ts, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_raw_merge(const RawParams& p, hipStream_t s) {
+  if (p.g1 <= p.g0) return hipSuccess;
+  hipLaunchKernelGGL(k_raw_merge, dim3(wave_blocks(p.g1 - p.g0)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_raw_merge_ts(const RawParams& p, hipStream_t s) {
+  if (p.g1 <= p.g0) return hipSuccess;
+  hipLaunchKernelGGL(k_raw_merge_ts, dim3(wave_blocks(p.g1 - p.g0)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_raw_dz_check(const RawParams& p, int64_t n_out, hipStream_t s) {
+  if (n_out <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_raw_dz_check, dim3((unsigned)((n_out + 255) / 256)), dim3(256), 0, s, p, n_out);
   return hipGetLastError();
 }
 

@@ -66,6 +66,28 @@ __device__ __forceinline__ double dlerp(int interp, int64_t x, int64_t x0, doubl
   }
 }
 
+// nextLongValue / nextDoubleValue of a span that does not own the union point (:682-797): y0
+// at x == x0, y1 at x == x1, else the interpolation.  With points in time order x0 < x < x1
+// always holds; over cells with unsorted datapoints (RawParams.uns) x may sit on either end of
+// the window and x1 - x0 may be <= 0 (Java long division truncates; / 0 throws
+// ArithmeticException, reported through dz where the long result is the one used).
+__device__ __forceinline__ int64_t jlerp_u(int interp, int64_t x, int64_t x0, int64_t y0, int64_t x1, int64_t y1,
+                                           bool& dz) {
+  if (x == x0) return y0;
+  if (x == x1) return y1;
+  if (interp != TSDB_INTERP_LERP || x1 > x0) return jlerp(interp, x, x0, y0, x1, y1);
+  if (x1 == x0) { dz = true; return 0; }
+  const int64_t num = (int64_t)((uint64_t)(x - x0) * ((uint64_t)y1 - (uint64_t)y0));
+  const int64_t den = x1 - x0;
+  const int64_t q = (num == INT64_MIN && den == -1) ? INT64_MIN : num / den;
+  return (int64_t)((uint64_t)y0 + (uint64_t)q);
+}
+__device__ __forceinline__ double dlerp_u(int interp, int64_t x, int64_t x0, double y0, int64_t x1, double y1) {
+  if (x == x0) return y0;
+  if (x == x1) return y1;
+  return dlerp(interp, x, x0, y0, x1, y1);
+}
+
 __device__ __forceinline__ int64_t jd2l(double d) {   // Java (long) of a double
   if (isnan(d)) return 0;
   if (d >= 9223372036854775807.0) return 0x7FFFFFFFFFFFFFFFLL;
@@ -178,10 +200,15 @@ __device__ __forceinline__ int64_t racc_long_final(const RAcc& a) {
 
 // One value (exact or interpolated) of a span at union time x.
 template <int GA, bool DL, bool DD>
-__device__ __forceinline__ void feed(RAcc& acc, int interp, bool own, int64_t x, const RawPt& a, const RawPt& b) {
+__device__ __forceinline__ void feed(RAcc& acc, int interp, bool own, int64_t x, const RawPt& a, const RawPt& b,
+                                     bool uns, bool& dz) {
   if (own) {
     if (DL) racc_long<GA>(acc, (int64_t)a.bits);
     if (DD) racc_double<GA>(acc, pt_double(a.tsf, a.bits));
+  } else if (uns) {
+    const int64_t x0 = a.tsf & RAW_TIME_MASK, x1 = b.tsf & RAW_TIME_MASK;
+    if (DL) racc_long<GA>(acc, jlerp_u(interp, x, x0, (int64_t)a.bits, x1, (int64_t)b.bits, dz));
+    if (DD) racc_double<GA>(acc, dlerp_u(interp, x, x0, pt_double(a.tsf, a.bits), x1, pt_double(b.tsf, b.bits)));
   } else {
     const int64_t x0 = a.tsf & RAW_TIME_MASK, x1 = b.tsf & RAW_TIME_MASK;
     if (DL) racc_long<GA>(acc, jlerp(interp, x, x0, (int64_t)a.bits, x1, (int64_t)b.bits));
@@ -214,6 +241,8 @@ __global__ __launch_bounds__(64) void k_raw_eval(RawParams p) {
   int64_t x[RAW_W];
   RAcc acc[RAW_W];
   uint32_t flt = 0;   // bit w: some slot at union point w holds a double (isInteger, :612-625)
+  uint32_t dzm = 0;   // bit w: a long LERP at union point w divided by zero (unsorted cells)
+  const bool uns = p.uns != 0;
 #pragma unroll
   for (int w = 0; w < RAW_W; w++) {
     const int64_t u = ua + 64 * w + lane;
@@ -245,7 +274,11 @@ __global__ __launch_bounds__(64) void k_raw_eval(RawParams p) {
         const RawPt a = pts[c - 1], b = pts[c];
         if ((a.tsf | b.tsf) & RAW_FLOAT) flt = (1u << RAW_W) - 1;
 #pragma unroll
-        for (int w = 0; w < RAW_W; w++) feed<GA, DL, DD>(acc[w], interp, false, x[w], a, b);
+        for (int w = 0; w < RAW_W; w++) {
+          bool dz = false;
+          feed<GA, DL, DD>(acc[w], interp, false, x[w], a, b, uns, dz);
+          if (dz) dzm |= 1u << w;
+        }
       }
       continue;
     }
@@ -284,7 +317,9 @@ __global__ __launch_bounds__(64) void k_raw_eval(RawParams p) {
         }
         const RawPt b = pts[j + 1];
         if ((a.tsf | b.tsf) & RAW_FLOAT) flt |= 1u << w;
-        feed<GA, DL, DD>(acc[w], interp, own, x[w], a, b);
+        bool dz = false;
+        feed<GA, DL, DD>(acc[w], interp, own, x[w], a, b, uns, dz);
+        if (dz) dzm |= 1u << w;
       }
     }
     WAVE_SYNC();
@@ -307,6 +342,7 @@ __global__ __launch_bounds__(64) void k_raw_eval(RawParams p) {
       bits = (uint64_t)__double_as_longlong(r);
     }
     if (acc[w].bad) set_err(p.err, TSDB_E_ILLEGAL_DATA);   // None: "More than one value" (:454-460)
+    if (is_int && ((dzm >> w) & 1)) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // ArithmeticException: / by zero
     p.out_bits[obase + u] = bits;
     p.out_int[obase + u] = is_int ? 1 : 0;
   }
@@ -359,6 +395,7 @@ __global__ __launch_bounds__(64) void k_raw_vals(RawParams p) {
   int64_t x[RAW_W];
   bool in[RAW_W];
   uint32_t flt = 0;
+  const bool uns = p.uns != 0;
 #pragma unroll
   for (int w = 0; w < RAW_W; w++) {
     const int64_t u = ua + 64 * w + lane;
@@ -374,6 +411,19 @@ __global__ __launch_bounds__(64) void k_raw_vals(RawParams p) {
   auto put_d = [&](int i, int w, double v) {
     if (!in[w]) return;
     p.vals_d[vbase + (int64_t)i * RAW_STRIP + 64 * w + lane] = v;
+  };
+  // a non-owning span's operands (see jlerp_u); a long division by zero marks the point
+  auto put_lerp = [&](int i, int w, const RawPt& a, const RawPt& b) {
+    const int64_t x0 = a.tsf & RAW_TIME_MASK, x1 = b.tsf & RAW_TIME_MASK;
+    if (uns) {
+      bool dz = false;
+      if (DL) put_l(i, w, jlerp_u(interp, x[w], x0, (int64_t)a.bits, x1, (int64_t)b.bits, dz));
+      if (DD) put_d(i, w, dlerp_u(interp, x[w], x0, pt_double(a.tsf, a.bits), x1, pt_double(b.tsf, b.bits)));
+      if (dz && in[w]) p.dz[obase + ua + 64 * w + lane] = 1;
+    } else {
+      if (DL) put_l(i, w, jlerp(interp, x[w], x0, (int64_t)a.bits, x1, (int64_t)b.bits));
+      if (DD) put_d(i, w, dlerp(interp, x[w], x0, pt_double(a.tsf, a.bits), x1, pt_double(b.tsf, b.bits)));
+    }
   };
 
   for (int i = i0; i < i1; i++) {
@@ -398,12 +448,8 @@ __global__ __launch_bounds__(64) void k_raw_vals(RawParams p) {
         if (c == n) continue;
         const RawPt a = pts[c - 1], b = pts[c];
         if ((a.tsf | b.tsf) & RAW_FLOAT) flt = (1u << RAW_W) - 1;
-        const int64_t x0 = a.tsf & RAW_TIME_MASK, x1 = b.tsf & RAW_TIME_MASK;
 #pragma unroll
-        for (int w = 0; w < RAW_W; w++) {
-          if (DL) put_l(i, w, jlerp(interp, x[w], x0, (int64_t)a.bits, x1, (int64_t)b.bits));
-          if (DD) put_d(i, w, dlerp(interp, x[w], x0, pt_double(a.tsf, a.bits), x1, pt_double(b.tsf, b.bits)));
-        }
+        for (int w = 0; w < RAW_W; w++) put_lerp(i, w, a, b);
       }
       continue;
     }
@@ -442,9 +488,7 @@ __global__ __launch_bounds__(64) void k_raw_vals(RawParams p) {
         }
         const RawPt b = pts[j + 1];
         if ((a.tsf | b.tsf) & RAW_FLOAT) flt |= 1u << w;
-        const int64_t x0 = a.tsf & RAW_TIME_MASK, x1 = b.tsf & RAW_TIME_MASK;
-        if (DL) put_l(i, w, jlerp(interp, x[w], x0, (int64_t)a.bits, x1, (int64_t)b.bits));
-        if (DD) put_d(i, w, dlerp(interp, x[w], x0, pt_double(a.tsf, a.bits), x1, pt_double(b.tsf, b.bits)));
+        put_lerp(i, w, a, b);
       }
     }
     WAVE_SYNC();
