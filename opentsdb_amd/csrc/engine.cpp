@@ -2643,7 +2643,7 @@ int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G)
     HIP_OK(c->sel_vals.ensure(std::max<int64_t>(1, S * K) * 8));
     HIP_OK(c->sel_uni.ensure(std::max<int64_t>(1, G * K)));
     HIP_OK(hipMemcpyAsync(c->sel_gsp.p, gsp.data(), (G + 1) * 8, hipMemcpyHostToDevice, c->stream));
-    if (S * K) HIP_OK(hipMemsetD32Async((hipDeviceptr_t)c->sel_vals.p, 0x7FF87FF8, S * K * 2, c->stream));   // +NaN
+    HIP_OK(launch_fill64(c->sel_vals.as<uint64_t>(), 0x7FF87FF87FF87FF8ULL, S * K, c->stream));   // +NaN
     HIP_OK(hipMemsetAsync(c->sel_uni.p, 0, std::max<int64_t>(1, G * K), c->stream));
     Plan P2;
     int rc = plan_query(c, q, P2);
@@ -2677,7 +2677,7 @@ int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G)
   HIP_OK(c->sel_uni.ensure(std::max<int64_t>(1, G * K)));
   HIP_OK(c->gact.ensure(std::max<int64_t>(1, G) * 4));
   HIP_OK(hipMemcpyAsync(c->sel_gsp.p, gsp.data(), (G + 1) * 8, hipMemcpyHostToDevice, c->stream));
-  if (S * K) HIP_OK(hipMemsetD32Async((hipDeviceptr_t)c->sel_vals.p, 0x7FF87FF8, S * K * 2, c->stream));   // +NaN
+  HIP_OK(launch_fill64(c->sel_vals.as<uint64_t>(), 0x7FF87FF87FF87FF8ULL, S * K, c->stream));   // +NaN
   HIP_OK(hipMemsetAsync(c->sel_uni.p, 0, std::max<int64_t>(1, G * K), c->stream));
   HIP_OK(hipMemsetAsync(c->gact.p, 0, std::max<int64_t>(1, G) * 4, c->stream));
   const int64_t nt = (int64_t)c->tb.size();

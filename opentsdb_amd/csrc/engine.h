@@ -372,6 +372,8 @@ hipError_t launch_rollup_combine(double* dense, const uint8_t* pres, const int64
                                  int avg, hipStream_t s);
 hipError_t launch_first_ts(const RowDesc* rows, const int64_t* srp, const uint8_t* qual, int64_t n, int64_t ss,
                            int64_t se, int64_t t0, int64_t* out, hipStream_t s);
+// n 8-byte words of `v` from p (16-byte aligned): 16-byte non-temporal stores
+hipError_t launch_fill64(uint64_t* p, uint64_t v, int64_t n, hipStream_t s);
 // streaming variant for one uniform row class (k_fast's premises + the sum certificate);
 // series that break a premise go to p.redo_list for launch_rollup_agg (tile_list mode)
 bool rollup_fast_supported(int qw, int vl);

@@ -1473,30 +1473,50 @@ __global__ __launch_bounds__(SEL_REG_T, OCC) void k_sel_reg(SelParams p) {
 // contribute_slot over the group's spans in index order, then ps_final.  A span without a
 // value at the slot holds sel_values' fill pattern (0x7FF87FF87FF87FF8), distinct from the
 // canonical NaN of a real NaN value (which MULT / FIRST / LAST see).
+// The fold is a dependent chain over the group's spans and only G * K threads run it, so the
+// kernel is memory-latency bound: ORD_U loads per batch are issued one batch AHEAD of the fold
+// (two register buffers), and the aggregator is a template parameter so that a fold step is a
+// few instructions (the runtime switch cost more issue slots than the loads).
+constexpr int ORD_U = 32;
+
+template <int GA>
+__device__ __forceinline__ void ord_fold(RegPart& R, const double (&v)[ORD_U]) {
+#pragma unroll
+  for (int u = 0; u < ORD_U; u++)
+    if ((uint64_t)__double_as_longlong(v[u]) != 0x7FF87FF87FF87FF8ULL) contribute_slot(GA, R, v[u], false);
+}
+
+template <int GA>
 __global__ __launch_bounds__(256) void k_ordered(OrdParams p) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.G * p.K) return;
   const int64_t g = i / p.K, k = i - g * p.K;
   RegPart R;
-  regpart_init(p.ga, R);
+  regpart_init(GA, R);
   const int64_t s1 = p.group_series_ptr[g + 1];
-  // The fold is a dependent chain over the group's spans, and only G * K threads run it: issue
-  // ORD_U independent loads ahead of each ORD_U-step fold so the chain waits on one memory
-  // latency per ORD_U spans instead of one per span (same fold order).
-  constexpr int ORD_U = 32;
+  const double* col = p.vals + k;
   int64_t s = p.group_series_ptr[g];
-  for (; s + ORD_U <= s1; s += ORD_U) {
-    double v[ORD_U];
+  double va[ORD_U], vb[ORD_U];
+  if (s + ORD_U <= s1) {
 #pragma unroll
-    for (int u = 0; u < ORD_U; u++) v[u] = p.vals[(s + u) * p.K + k];
+    for (int u = 0; u < ORD_U; u++) va[u] = col[(s + u) * p.K];
+  }
+  while (s + 2 * ORD_U <= s1) {
 #pragma unroll
-    for (int u = 0; u < ORD_U; u++)
-      if ((uint64_t)__double_as_longlong(v[u]) != 0x7FF87FF87FF87FF8ULL) contribute_slot(p.ga, R, v[u], false);
+    for (int u = 0; u < ORD_U; u++) vb[u] = col[(s + ORD_U + u) * p.K];
+    ord_fold<GA>(R, va);
+#pragma unroll
+    for (int u = 0; u < ORD_U; u++) va[u] = vb[u];
+    s += ORD_U;
+  }
+  if (s + ORD_U <= s1) {
+    ord_fold<GA>(R, va);
+    s += ORD_U;
   }
   for (; s < s1; s++) {
-    const double v = p.vals[s * p.K + k];
+    const double v = col[s * p.K];
     if ((uint64_t)__double_as_longlong(v) == 0x7FF87FF87FF87FF8ULL) continue;
-    contribute_slot(p.ga, R, v, false);
+    contribute_slot(GA, R, v, false);
   }
   const bool emit = p.uni[i] != 0;
   PState S;
@@ -1504,14 +1524,22 @@ __global__ __launch_bounds__(256) void k_ordered(OrdParams p) {
   S.b = R.pb;
   S.n = R.pn;
   S.f = R.pf | (emit ? PF_UNION : 0u);
-  p.out_val[i] = emit ? ps_final(p.ga, S, p.err) : 0.0;
+  p.out_val[i] = emit ? ps_final(GA, S, p.err) : 0.0;
   p.out_flag[i] = emit ? 1 : 0;
 }
 
 hipError_t launch_ordered(const OrdParams& p, hipStream_t s) {
   const int64_t n = p.G * p.K;
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ordered, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p);
+  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  switch (p.ga) {
+#define ORD_CASE(G_) \
+  case G_: hipLaunchKernelGGL(k_ordered<G_>, grid, block, 0, s, p); break;
+    ORD_CASE(GA_SUM) ORD_CASE(GA_AVG) ORD_CASE(GA_COUNT) ORD_CASE(GA_SQUARESUM) ORD_CASE(GA_MIN) ORD_CASE(GA_MAX)
+    ORD_CASE(GA_DEV) ORD_CASE(GA_FIRST) ORD_CASE(GA_LAST) ORD_CASE(GA_DIFF) ORD_CASE(GA_MULT) ORD_CASE(GA_NONE)
+#undef ORD_CASE
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -1861,10 +1861,13 @@ __device__ __forceinline__ uint64_t rl64(uint64_t x, int l) {
 }
 
 #ifndef SHORT_OCC
-#define SHORT_OCC 5   // waves per SIMD k_short is compiled for (VGPR budget). Config 3: 3-5 -> 3.8 ms, 6 -> 4.5 ms, 8 -> 9.4 ms
+// waves per SIMD k_short is compiled for (VGPR budget). Config 3 (round 1): 3-5 -> 3.8 ms,
+// 6 -> 4.5 ms, 8 -> 9.4 ms.  Round 2: the 4- and 8-byte classes grew past 5 waves' budget and
+// spilled (48-280 B/lane of scratch): they compile for 4, the vle class (93 VGPRs) stays at 5.
+#define SHORT_OCC(VL) ((VL) == 0 ? 5 : 4)
 #endif
 template <int F, int QW, int VL, int D, bool KR>
-__global__ __launch_bounds__(256, SHORT_OCC) void k_short(GridParams p, const RowDesc* __restrict__ rows,
+__global__ __launch_bounds__(256, SHORT_OCC(VL)) void k_short(GridParams p, const RowDesc* __restrict__ rows,
                                                const int64_t* __restrict__ srp, const int64_t* __restrict__ tbeg,
                                                const int64_t* __restrict__ tend) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
