@@ -524,6 +524,21 @@ int tsdbhip_expr_zip(tsdbhip_ctx* ctx, const int32_t* program, int n_ops, const 
                      int64_t n_sets, const int32_t* set_series, const double* var_fill, const tsdbhip_series_set* in,
                      tsdbhip_result** out);
 
+/* highestMax / highestCurrent (HighestMax.java:37-150, HighestCurrent.java:37-151): the series
+ * of `in` (every sub-query's group-bys, flattened in order; each sorted by time) run through one
+ * AggregationIterator(start_ms, end_ms, LERP) with MaxCacheAggregator (HighestMax.java:182-292)
+ * or MaxLatestAggregator (HighestCurrent.java:172-283).  Those keep the operands of each point
+ * by POSITION among the spans that have a value, not by series.  The series are then ranked
+ * by TopNSortingEntry (descending Double.compare, stable).  out_index (capacity in->n_series)
+ * receives the indices into `in` of the min(topn, n) series returned, in order; *out_n their
+ * count.  HighestCurrent drops series without points first, as the reference does.
+ * topn < 1 -> TSDB_E_ILLEGAL_ARGUMENT (the host mirror parses the string parameter); series
+ * but no point in [start_ms, end_ms] -> TSDB_E_NULL_POINTER (the reference sorts null entries);
+ * a series out of time order -> TSDB_E_ILLEGAL_ARGUMENT. */
+enum { TSDB_EXPR_HIGHEST_MAX = 4, TSDB_EXPR_HIGHEST_CURRENT = 5 };
+int tsdbhip_expr_topn(tsdbhip_ctx* ctx, int fn, int32_t topn, int64_t start_ms, int64_t end_ms,
+                      const tsdbhip_series_set* in, int32_t* out_index, int32_t* out_n);
+
 /* Device synchronisation helper for host code that does not use HIP directly. */
 int tsdbhip_sync(tsdbhip_ctx* ctx);
 

@@ -2,9 +2,11 @@
 // tsdbhip_expr_map, tsdbhip_expr_zip.  Kernels in k_expr.hip; the function names, parameter
 // parsing and the union join by tags live in the host mirror (opentsdb_amd/expression.py).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -239,5 +241,177 @@ extern "C" int tsdbhip_expr_zip(tsdbhip_ctx* c, const int32_t* program, int n_op
   for (int64_t j = 0; j <= n_sets; j++) const_cast<int64_t*>(r->group_ptr)[j] = off[j];
   for (int64_t j = 0; j < n_sets; j++) const_cast<int32_t*>(r->group_id)[j] = (int32_t)j;
   *out = r;
+  return 0;
+}
+
+namespace {
+
+__global__ void k_topn_keys(const int64_t* ts, int64_t n, int64_t start, int64_t end, int64_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (ts[i] >= start && ts[i] <= end) ? ts[i] : INT64_MAX;
+}
+
+double key_double(uint64_t k) {   // inverse of k_expr.hip's dkey
+  const uint64_t b = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+  double d;
+  std::memcpy(&d, &b, 8);
+  return d;
+}
+double java_max(double a, double b) {   // Math.max(double, double)
+  if (a != a || b != b) return NAN;
+  if (a == 0.0 && b == 0.0) return std::signbit(a) ? b : a;
+  return a > b ? a : b;
+}
+int java_compare(double a, double b) {  // Double.compare
+  if (a < b) return -1;
+  if (a > b) return 1;
+  const bool na = a != a, nb = b != b;
+  if (na || nb) return na == nb ? 0 : (na ? 1 : -1);
+  const bool sa = std::signbit(a), sb = std::signbit(b);   // -0.0 < 0.0
+  return sa == sb ? 0 : (sa ? -1 : 1);
+}
+
+}  // namespace
+
+extern "C" int tsdbhip_expr_topn(tsdbhip_ctx* c, int fn, int32_t topn, int64_t start_ms, int64_t end_ms,
+                                 const tsdbhip_series_set* in, int32_t* out_index, int32_t* out_n) {
+  if (!c || !out_n || (!out_index && in && in->n_series > 0)) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  *out_n = 0;
+  if (int rc = check_set(in)) return rc;
+  if (fn != TSDB_EXPR_HIGHEST_MAX && fn != TSDB_EXPR_HIGHEST_CURRENT)
+    return set_error(TSDB_E_ILLEGAL_ARGUMENT, "unknown top-n function");
+  if (topn < 1) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "Top n value must be greater than zero");
+  const bool current = fn == TSDB_EXPR_HIGHEST_CURRENT;
+  // the series the AggregationIterator walks: all of them (HighestMax.java:75-100) or those with
+  // points (HighestCurrent.java:81-101); their points in one contiguous block each
+  std::vector<int32_t> sel;
+  std::vector<int64_t> ptr{0}, lo;
+  for (int64_t s = 0; s < in->n_series; s++) {
+    const int64_t a = in->ptr[s], b = in->ptr[s + 1];
+    if (b < a) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "malformed series set");
+    if (current && b == a) continue;
+    for (int64_t q = a + 1; q < b; q++)
+      if (in->ts_ms[q] <= in->ts_ms[q - 1]) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "series out of time order");
+    sel.push_back((int32_t)s);
+    ptr.push_back(ptr.back() + (b - a));
+    lo.push_back(std::lower_bound(in->ts_ms + a, in->ts_ms + b, start_ms) - (in->ts_ms + a));   // seek(start)
+  }
+  const int64_t S = (int64_t)sel.size(), N = ptr.back();
+  if (S == 0) return 0;
+  std::lock_guard<std::mutex> lk(ctx_mutex(c));
+  if (hipSetDevice(ctx_device(c)) != hipSuccess) return set_error(TSDB_E_HIP, "hipSetDevice");
+  hipStream_t st = ctx_stream(c);
+  Scratch sc;
+  auto release = [&]() {};
+  void *d_ptr, *d_ts, *d_bits, *d_int, *d_lo, *d_keys, *d_sorted, *d_uni, *d_nu, *d_ml, *d_md, *d_minm, *d_has, *d_last,
+      *d_err;
+  XOK(sc.alloc(&d_ptr, (S + 1) * 8));
+  XOK(sc.alloc(&d_ts, N * 8));
+  XOK(sc.alloc(&d_bits, N * 8));
+  XOK(sc.alloc(&d_int, N));
+  XOK(sc.alloc(&d_lo, S * 8));
+  XOK(sc.alloc(&d_keys, N * 8));
+  XOK(sc.alloc(&d_sorted, N * 8));
+  XOK(sc.alloc(&d_uni, N * 8));
+  XOK(sc.alloc(&d_nu, 8));
+  XOK(sc.alloc(&d_ml, S * 8));
+  XOK(sc.alloc(&d_md, S * 8));
+  XOK(sc.alloc(&d_minm, 8));
+  XOK(sc.alloc(&d_has, 8));
+  XOK(sc.alloc(&d_last, 16));
+  XOK(sc.alloc(&d_err, 16));
+  XOK(hipMemcpyAsync(d_ptr, ptr.data(), (S + 1) * 8, hipMemcpyHostToDevice, st));
+  XOK(hipMemcpyAsync(d_lo, lo.data(), S * 8, hipMemcpyHostToDevice, st));
+  for (int64_t k = 0, o = 0; k < S; k++) {   // the selected series' points, back to back
+    const int64_t a = in->ptr[sel[k]], n = in->ptr[sel[k] + 1] - a;
+    if (!n) continue;
+    XOK(hipMemcpyAsync((int64_t*)d_ts + o, in->ts_ms + a, n * 8, hipMemcpyHostToDevice, st));
+    XOK(hipMemcpyAsync((uint64_t*)d_bits + o, in->value_bits + a, n * 8, hipMemcpyHostToDevice, st));
+    XOK(hipMemcpyAsync((uint8_t*)d_int + o, in->is_int + a, n, hipMemcpyHostToDevice, st));
+    o += n;
+  }
+  // union timestamps in [start, end]: the points the iterator emits (series in time order, seek
+  // to start, hasNext while <= end), sorted and made unique on the device
+  int64_t U = 0;
+  if (N) {
+    hipLaunchKernelGGL(k_topn_keys, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, (const int64_t*)d_ts, N, start_ms,
+                       end_ms, (int64_t*)d_keys);
+    XOK(hipGetLastError());
+    size_t tmp1 = 0, tmp2 = 0;
+    XOK(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp1, (const int64_t*)d_keys, (int64_t*)d_sorted, (int)N, 0, 64, st));
+    XOK(hipcub::DeviceSelect::Unique(nullptr, tmp2, (const int64_t*)d_sorted, (int64_t*)d_uni, (int64_t*)d_nu, (int)N, st));
+    void* d_tmp;
+    XOK(sc.alloc(&d_tmp, std::max(tmp1, tmp2)));
+    size_t t1 = std::max(tmp1, tmp2), t2 = t1;
+    XOK(hipcub::DeviceRadixSort::SortKeys(d_tmp, t1, (const int64_t*)d_keys, (int64_t*)d_sorted, (int)N, 0, 64, st));
+    XOK(hipcub::DeviceSelect::Unique(d_tmp, t2, (const int64_t*)d_sorted, (int64_t*)d_uni, (int64_t*)d_nu, (int)N, st));
+    int64_t nu = 0, last = 0;
+    XOK(hipMemcpyAsync(&nu, d_nu, 8, hipMemcpyDeviceToHost, st));
+    XOK(hipStreamSynchronize(st));
+    if (nu > 0) {
+      XOK(hipMemcpyAsync(&last, (int64_t*)d_uni + nu - 1, 8, hipMemcpyDeviceToHost, st));
+      XOK(hipStreamSynchronize(st));
+    }
+    U = nu - (nu > 0 && last == INT64_MAX ? 1 : 0);
+  }
+  // MaxCacheAggregator / MaxLatestAggregator initial arrays (HighestMax.java:212-215)
+  std::vector<int64_t> ml(S, INT64_MIN);
+  std::vector<uint64_t> md(S);
+  {
+    const double dmin = 4.9e-324;   // Double.MIN_VALUE
+    uint64_t b;
+    std::memcpy(&b, &dmin, 8);
+    std::fill(md.begin(), md.end(), b | 0x8000000000000000ull);
+  }
+  const int32_t minm0[2] = {INT32_MAX, INT32_MAX}, has0[2] = {0, 0};
+  const int64_t last0[2] = {0, 0};
+  XOK(hipMemcpyAsync(d_ml, ml.data(), S * 8, hipMemcpyHostToDevice, st));
+  XOK(hipMemcpyAsync(d_md, md.data(), S * 8, hipMemcpyHostToDevice, st));
+  XOK(hipMemcpyAsync(d_minm, minm0, 8, hipMemcpyHostToDevice, st));
+  XOK(hipMemcpyAsync(d_has, has0, 8, hipMemcpyHostToDevice, st));
+  XOK(hipMemcpyAsync(d_last, last0, 16, hipMemcpyHostToDevice, st));
+  XOK(hipMemsetAsync(d_err, 0, 16, st));
+  ExprTopParams p{};
+  p.n_series = S;
+  p.ptr = (const int64_t*)d_ptr;
+  p.ts = (const int64_t*)d_ts;
+  p.bits = (const uint64_t*)d_bits;
+  p.is_int = (const uint8_t*)d_int;
+  p.lo = (const int64_t*)d_lo;
+  p.uts = (const int64_t*)d_uni;
+  p.U = U;
+  p.current = current ? 1 : 0;
+  p.max_l = (int64_t*)d_ml;
+  p.max_d = (uint64_t*)d_md;
+  p.min_m = (int32_t*)d_minm;
+  p.has = (int32_t*)d_has;
+  p.last_u = (int64_t*)d_last;
+  p.err = (int32_t*)d_err;
+  XOK(expr_topn(p, st));
+  if (current) XOK(expr_topn_at(p, st));
+  int32_t minm[2], has[2];
+  XOK(hipMemcpyAsync(ml.data(), d_ml, S * 8, hipMemcpyDeviceToHost, st));
+  XOK(hipMemcpyAsync(md.data(), d_md, S * 8, hipMemcpyDeviceToHost, st));
+  XOK(hipMemcpyAsync(minm, d_minm, 8, hipMemcpyDeviceToHost, st));
+  XOK(hipMemcpyAsync(has, d_has, 8, hipMemcpyDeviceToHost, st));
+  XOK(hipStreamSynchronize(st));
+  // the ranking over S values (HighestMax.java:118-146): positions past a point's operand count
+  // read 0 (MaxCache: Math.max with it), then (double) / Math.max of the two arrays, then
+  // TopNSortingEntry order (descending Double.compare; Arrays.sort is stable)
+  std::vector<double> val(S);
+  for (int64_t i = 0; i < S; i++) {
+    int64_t l = ml[i];
+    double d = key_double(md[i]);
+    if (!current && has[0] && i >= minm[0]) l = std::max<int64_t>(l, 0);
+    if (!current && has[1] && i >= minm[1]) d = java_max(d, 0.0);
+    val[i] = has[0] && has[1] ? java_max((double)l, d) : (has[0] ? (double)l : d);
+  }
+  if (!has[0] && !has[1]) return set_error(TSDB_E_NULL_POINTER, "no datapoint in the query range (TopNSortingEntry left null)");
+  std::vector<int32_t> order(S);
+  for (int64_t i = 0; i < S; i++) order[i] = (int32_t)i;
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return java_compare(val[a], val[b]) > 0; });
+  const int32_t cnt = (int32_t)std::min<int64_t>(topn, S);
+  for (int32_t k = 0; k < cnt; k++) out_index[k] = sel[order[k]];
+  *out_n = cnt;
   return 0;
 }

@@ -45,6 +45,28 @@ struct ExprZipParams {
   int32_t* err;
 };
 
+// highestMax / highestCurrent: an AggregationIterator (LERP) over every result series, one
+// wave per union point; operands kept by position among the spans that have a value
+struct ExprTopParams {
+  int64_t n_series;
+  const int64_t* ptr;
+  const int64_t* ts;
+  const uint64_t* bits;
+  const uint8_t* is_int;
+  const int64_t* lo;          // [n_series] first point >= start (the constructor's seek)
+  const int64_t* uts;         // [U] union timestamps in [start, end], ascending
+  int64_t U;
+  int32_t current;            // 1: MaxLatestAggregator, 0: MaxCacheAggregator
+  int64_t* max_l;             // [n_series] positional long maxima (MaxCache) / latest (MaxLatest)
+  uint64_t* max_d;            // [n_series] positional double maxima as order-preserving keys
+  int32_t* min_m;             // [2] fewest spans with a value at a long / double point
+  int32_t* has;               // [2] some long / double point ran
+  int64_t* last_u;            // [2] MaxLatest: last long / double point
+  int32_t* err;
+};
+hipError_t expr_topn(const ExprTopParams& p, hipStream_t s);      // the walk over every union point
+hipError_t expr_topn_at(const ExprTopParams& p, hipStream_t s);   // MaxLatest: operands at the last points
+
 hipError_t expr_map(const ExprMapParams& p, hipStream_t s);
 hipError_t expr_zip(const ExprZipParams& p, hipStream_t s);
 

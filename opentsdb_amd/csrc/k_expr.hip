@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "../../include/tsdbhip.h"
 #include "expr.h"
 
@@ -165,7 +167,146 @@ __global__ void k_expr_zip(ExprZipParams p) {
   p.out_int[t] = 0;
 }
 
+// ---- highestMax / highestCurrent ------------------------------------------------------
+// The state of span i at union point x, as AggregationIterator holds it after next() moved the
+// spans at x (AggregationIterator.java:514-567, slots :482-494, zeroing :521-526): lo = the
+// constructor's seek(start) position, hi = points <= x.  `flt`: a double in the span's current
+// or next slot (isInteger :612-625); `act`: hasNextValue sees the span (ts[i] != 0).
+struct TopSpan {
+  bool act, flt, own;
+  int64_t j;   // current point (act)
+};
+__device__ __forceinline__ TopSpan top_span(const ExprTopParams& p, int64_t i, int64_t x) {
+  TopSpan r = {false, false, false, 0};
+  const int64_t a = p.ptr[i], n = p.ptr[i + 1] - a, lo = p.lo[i];
+  if (lo >= n) return r;                       // ended in the constructor
+  int64_t l = lo, h = n;                       // hi = first point > x
+  while (l < h) {
+    const int64_t m = (l + h) >> 1;
+    if (p.ts[a + m] <= x) l = m + 1; else h = m;
+  }
+  if (l == lo) {                               // not started: its next slot holds point lo
+    r.flt = !p.is_int[a + lo];
+    return r;
+  }
+  r.j = l - 1;
+  r.own = p.ts[a + r.j] == x;
+  if (r.j == n - 1) {                          // no next point: ended once its last one passed
+    if (r.own) { r.act = true; r.flt = !p.is_int[a + r.j]; }
+    return r;
+  }
+  r.act = true;
+  r.flt = !p.is_int[a + r.j] || !p.is_int[a + r.j + 1];
+  return r;
+}
+
+// nextLongValue / nextDoubleValue of an active span (:682-797): its own value, else the LERP
+// between its current and next points (x0 < x < x1: the series are in time order)
+__device__ __forceinline__ int64_t top_long(const ExprTopParams& p, int64_t i, const TopSpan& t, int64_t x) {
+  const int64_t q = p.ptr[i] + t.j;
+  const int64_t y0 = (int64_t)p.bits[q];
+  if (t.own) return y0;
+  const int64_t x0 = p.ts[q], x1 = p.ts[q + 1], y1 = (int64_t)p.bits[q + 1];
+  const int64_t num = (int64_t)((uint64_t)(x - x0) * ((uint64_t)y1 - (uint64_t)y0));
+  return (int64_t)((uint64_t)y0 + (uint64_t)(num / (x1 - x0)));
+}
+__device__ __forceinline__ double top_double(const ExprTopParams& p, int64_t i, const TopSpan& t, int64_t x) {
+  const int64_t q = p.ptr[i] + t.j;
+  const double y0 = pt_double(p.bits[q], p.is_int[q]);
+  if (t.own) return y0;
+  const int64_t x0 = p.ts[q], x1 = p.ts[q + 1];
+  const double y1 = pt_double(p.bits[q + 1], p.is_int[q + 1]);
+  return y0 + (double)(x - x0) * (y1 - y0) / (double)(x1 - x0);
+}
+
+__device__ __forceinline__ uint64_t dkey(double d) {   // Math.max order: -0.0 < 0.0, NaN on top
+  uint64_t b = (uint64_t)__double_as_longlong(d);
+  if (d != d) b = 0x7FF8000000000000ull;
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+__device__ __forceinline__ int lanes_before(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// One wave per union point u: isInteger over every span's slots, then the operands in span
+// order, each at its position among the spans with a value (MaxCacheAggregator.runLong /
+// runDouble: longs[ix++], HighestMax.java:226-266), folded with Math.max per position.
+// Positions past the point's operand count read 0: min_m records the smallest count.
+__global__ __launch_bounds__(256) void k_expr_topn(ExprTopParams p) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t u = wave; u < p.U; u += nwaves) {
+    const int64_t x = p.uts[u];
+    bool flt = false;
+    for (int64_t i0 = 0; i0 < p.n_series; i0 += 64) {
+      const int64_t i = i0 + lane;
+      if (i < p.n_series && top_span(p, i, x).flt) flt = true;
+    }
+    const bool is_int = !__any(flt);
+    int64_t run = 0;
+    for (int64_t i0 = 0; i0 < p.n_series; i0 += 64) {
+      const int64_t i = i0 + lane;
+      TopSpan t = {false, false, false, 0};
+      if (i < p.n_series) t = top_span(p, i, x);
+      const uint64_t m = __ballot(t.act);
+      const int64_t pos = run + lanes_before(m);
+      if (t.act && !p.current) {
+        if (is_int) atomicMax((long long*)&p.max_l[pos], (long long)top_long(p, i, t, x));
+        else atomicMax((unsigned long long*)&p.max_d[pos], (unsigned long long)dkey(top_double(p, i, t, x)));
+      }
+      run += __popcll(m);
+    }
+    if (lane == 0) {
+      const int w = is_int ? 0 : 1;
+      atomicOr(&p.has[w], 1);
+      if (p.current) atomicMax((unsigned long long*)&p.last_u[w], (unsigned long long)u);
+      else atomicMin(&p.min_m[w], (int32_t)run);
+    }
+  }
+}
+
+// MaxLatestAggregator: `ts > latest_ts` always holds (latest_ts is never updated,
+// HighestCurrent.java:228-260), so each array is the positional operands of the LAST long /
+// double point, zeros past its operand count (System.arraycopy of the zero-filled array).
+__global__ __launch_bounds__(64) void k_expr_topn_at(ExprTopParams p) {
+  const int lane = threadIdx.x & 63;
+  const int w = blockIdx.x;   // 0: long point, 1: double point
+  if (!p.has[w]) return;
+  const int64_t u = p.last_u[w];
+  const int64_t x = p.uts[u];
+  int64_t run = 0;
+  for (int64_t i0 = 0; i0 < p.n_series; i0 += 64) {
+    const int64_t i = i0 + lane;
+    TopSpan t = {false, false, false, 0};
+    if (i < p.n_series) t = top_span(p, i, x);
+    const uint64_t m = __ballot(t.act);
+    const int64_t pos = run + lanes_before(m);
+    if (t.act) {
+      if (w == 0) p.max_l[pos] = top_long(p, i, t, x);
+      else p.max_d[pos] = dkey(top_double(p, i, t, x));
+    }
+    run += __popcll(m);
+  }
+  for (int64_t q = run + lane; q < p.n_series; q += 64) {
+    if (w == 0) p.max_l[q] = 0;
+    else p.max_d[q] = dkey(0.0);
+  }
+}
+
 }  // namespace
+
+hipError_t expr_topn(const ExprTopParams& p, hipStream_t s) {
+  if (p.U <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((p.U + 3) / 4, 65536);
+  hipLaunchKernelGGL(k_expr_topn, dim3((unsigned)blocks), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+hipError_t expr_topn_at(const ExprTopParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_expr_topn_at, dim3(2), dim3(64), 0, s, p);
+  return hipGetLastError();
+}
 
 hipError_t expr_map(const ExprMapParams& p, hipStream_t s) {
   if (p.n <= 0) return hipSuccess;

@@ -11,8 +11,8 @@ the GPU:
   alias / scale / absolute / shift, timeShift / movingAverage   tsdbhip_expr_map
   sumSeries, sum / diffSeries, difference / multiplySeries,  tsdbhip_expr_zip (ExpressionIterator
   multiply / divideSeries, divide / evaluate(expression)     with a UNION of the variables)
-
-highestCurrent / highestMax are not built.
+  highestMax / highestCurrent                                 tsdbhip_expr_topn (AggregationIterator
+                                                             over every series, positional maxima)
 """
 from __future__ import annotations
 
@@ -24,7 +24,7 @@ import numpy as np
 
 from . import abi
 
-EXPR_SCALE, EXPR_ABSOLUTE, EXPR_SHIFT, EXPR_MOVING_AVG = 0, 1, 2, 3
+EXPR_SCALE, EXPR_ABSOLUTE, EXPR_SHIFT, EXPR_MOVING_AVG, EXPR_HIGHEST_MAX, EXPR_HIGHEST_CURRENT = 0, 1, 2, 3, 4, 5
 XOP_VAR, XOP_CONST, XOP_ADD, XOP_SUB, XOP_MUL, XOP_DIV, XOP_MOD, XOP_NEG = range(8)
 
 
@@ -97,6 +97,8 @@ def _lib():
         L.tsdbhip_expr_zip.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.c_int, C.POINTER(C.c_double), C.c_int,
                                        C.c_int64, C.POINTER(C.c_int32), C.POINTER(C.c_double), C.POINTER(SeriesSet),
                                        C.POINTER(C.POINTER(abi.Result))]
+        L.tsdbhip_expr_topn.argtypes = [C.c_void_p, C.c_int, C.c_int32, C.c_int64, C.c_int64, C.POINTER(SeriesSet),
+                                        C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         L._expr_types = True
     return L, E
 
@@ -373,6 +375,48 @@ def _combine(op, fname):
     return f
 
 
+def topn_parse(params):
+    """The top-n parameter of HighestMax / HighestCurrent.evaluate (HighestMax.java:47-72)."""
+    if not params:
+        raise ExpressionError("IllegalArgumentException", "Need aggregation window for moving average")
+    p = params[0]
+    if p is None or p == "":
+        raise ExpressionError("IllegalArgumentException", "Missing top n value (number of series to return)")
+    if not re.fullmatch(r"[0-9]+", p):
+        raise ExpressionError("IllegalArgumentException", "Unparseable top n value: " + p)
+    n = int(p)
+    if n > (1 << 31) - 1:
+        raise ExpressionError("IllegalArgumentException", "Invalid parameter, must be an integer")
+    if n < 1:
+        raise ExpressionError("IllegalArgumentException", f"Top n value must be greater than zero: {n}")
+    return n
+
+
+def _highest(fn, fname):
+    def f(engine, query_results, params, start_ms, end_ms):
+        """HighestMax / HighestCurrent.evaluate with the TSQuery's start / end: the top-n series of
+        every sub-query's group-bys, as tsdbhip_expr_topn ranks them on the GPU; the series are
+        returned unchanged."""
+        if not query_results:
+            return []
+        n = topn_parse(params)
+        flat = _flatten(query_results)
+        if not flat:
+            return []
+        L, E = _lib()
+        ss, keep = _pack(flat)
+        idx = (C.c_int32 * len(flat))()
+        cnt = C.c_int32(0)
+        E._check(L.tsdbhip_expr_topn(engine.ctx, fn, n, int(start_ms), int(end_ms), C.byref(ss), idx, C.byref(cnt)))
+        del keep
+        return [flat[idx[i]] for i in range(cnt.value)]
+    f.__name__ = fname
+    return f
+
+
+highest_max = _highest(EXPR_HIGHEST_MAX, "highestMax")
+highest_current = _highest(EXPR_HIGHEST_CURRENT, "highestCurrent")
+
 sum_series = _combine("+", "sumSeries")
 diff_series = _combine("-", "diffSeries")
 multiply_series = _combine("*", "multiplySeries")
@@ -382,5 +426,5 @@ FUNCTIONS = {
     "alias": alias, "scale": scale, "absolute": absolute, "movingAverage": moving_average, "shift": shift, "timeShift": shift,
     "divideSeries": divide_series, "divide": divide_series, "sumSeries": sum_series, "sum": sum_series,
     "diffSeries": diff_series, "difference": diff_series, "multiplySeries": multiply_series,
-    "multiply": multiply_series,
+    "multiply": multiply_series, "highestMax": highest_max, "highestCurrent": highest_current,
 }

@@ -13,6 +13,9 @@ assert (their loops evaluated here), with the test's tolerance.
   test/query/expression/TestSumSeries.java / TestDiffSeries.java / TestMultiplySeries.java /
   TestDivideSeries.java ........................ *OneSeriesEach (4)
   test/query/expression/TestTimeShift.java ..... parseParam, shiftDataPoint
+  test/query/expression/TestHighestMax.java / TestHighestCurrent.java .. evaluate* (which series,
+                                                 in which order; the tests then check that the
+                                                 series come back unchanged)
 
     python tests/golden/make_expression_golden.py
 """
@@ -109,12 +112,42 @@ def main():
     shift = {"source": D + "TestTimeShift.java:72-80",
              "points": [[1356998400000, 40], [1356998400000 + 2000000, 50]],
              "cases": [[0, 60000, 1356998460000], [1, 7 * 86400000, 1357605200000], [1, 130 * 86400000, 1368232400000]]}
+    # highestMax / highestCurrent: dps = ints 1..5 (METRIC), the TSQuery over [START, START + 5 I]
+    topn = []
+    end = START + INTERVAL * N
+
+    def gen_mixed(start, inc):   # generator(..., false, start, inc, wholes_as_integer=true)
+        out, v = [], float(start)
+        for i in range(N):
+            out.append([START + i * INTERVAL, int(v) if v == int(v) else v])
+            v += inc
+        return out
+
+    for fn, src in [("highestMax", "TestHighestMax.java"), ("highestCurrent", "TestHighestCurrent.java")]:
+        def addt(name, lines, inputs, params, expect=None, raises=None):
+            topn.append({"name": f"{fn}.{name}", "source": D + src + ":" + lines, "fn": fn, "inputs": inputs,
+                         "params": params, "start": START, "end": end, "expect_index": expect, "raises": raises})
+        b = gen(True, 10, 1)
+        addt("evaluateTopN1with2SeriesLong", "83-108", [[a, b]], ["1"], [1])
+        addt("evaluateTopN2with2SeriesLong", "111-147", [[a, b]], ["2"], [1, 0])
+        addt("evaluateTopN100with2SeriesLong", "150-185", [[a, b]], ["100"], [1, 0])
+        addt("evaluateTopN100with2SubQuerySeriesLong", "188-224", [[a], [b]], ["100"], [1, 0])
+        addt("evaluateTopN2with2SeriesDouble", "227-263", [[a, gen(False, 10, 1.5)]], ["2"], [1, 0])
+        addt("evaluateTopN1with2SeriesLongDoubleMixed", "266-298", [[a, gen_mixed(10, 1.5)]], ["1"], [1])
+        if fn == "highestCurrent":
+            addt("evaluateTopN1with2SeriesDiffSpan", "301-328", [[a, gen(True, 10, 1, n=3)]], ["1"], [0])
+        addt("evaluateNullResults", "337-341", [], ["1"], [])
+        addt("evaluateEmptyResults", "349-354", [[]], ["1"], [])
+        for nm, prm in [("evaluateNullParams", None), ("evaluateEmptyParams", []), ("evaluateTopnNull", [None]),
+                        ("evaluateTopnEmpty", [""]), ("evaluateTopnZero", ["0"]),
+                        ("evaluateTopnNotaNumber", ["not a number"])]:
+            addt(nm, "343-380", [[a]], prm, None, "IllegalArgumentException")
     out = {"cases": cases, "timeshift_parse": {"source": D + "TestTimeShift.java:47-70", "cases": parse},
-           "timeshift_shift": shift}
+           "timeshift_shift": shift, "topn": topn}
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "expression.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
-    print(f"{path}: {len(cases)} cases, {len(parse)} parseParam answers")
+    print(f"{path}: {len(cases)} cases, {len(parse)} parseParam answers, {len(topn)} top-n cases")
 
 
 if __name__ == "__main__":

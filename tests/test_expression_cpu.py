@@ -77,3 +77,49 @@ def test_library_exports_expression_symbols():
     from opentsdb_amd import engine as E
     for s in ("tsdbhip_expr_map", "tsdbhip_expr_zip"):
         assert hasattr(E.lib(), s)
+
+
+# ---- highestMax / highestCurrent --------------------------------------------------------
+def _topn_oracle(case):
+    subs = [[[tuple(p) for p in s] for s in sub] for sub in case["inputs"]]
+    if not subs:
+        return []
+    n = OX.topn_parse(case["params"])
+    flat = [s for sub in subs for s in sub]
+    return OX.highest(flat, n, case["start"], case["end"], current=case["fn"] == "highestCurrent")
+
+
+@pytest.mark.parametrize("case", G["topn"], ids=[c["name"] for c in G["topn"]])
+def test_oracle_topn_known_answers(case):
+    if case["raises"]:
+        with pytest.raises(OX.OracleExprError) as e:
+            _topn_oracle(case)
+        assert e.value.java == case["raises"]
+    else:
+        assert _topn_oracle(case) == case["expect_index"]
+
+
+@pytest.mark.parametrize("case", [c for c in G["topn"] if c["raises"]], ids=lambda c: c["name"])
+def test_host_topn_parameter_checks(case):
+    """The host mirror rejects the parameters before any device call (engine None)."""
+    with pytest.raises(X.ExpressionError) as e:
+        X.FUNCTIONS[case["fn"]](None, [[X.Series.of([(1, 1)])]], case["params"], case["start"], case["end"])
+    assert e.value.java == case["raises"]
+
+
+def test_oracle_topn_positional_quirk():
+    """MaxCacheAggregator keeps operands by position among the spans with a value, not by
+    series: a series absent from the early points has its values credited to another slot."""
+    S, I = 1356998400000, 60000
+    a = [(S + 2 * I, 100)]                        # starts late
+    b = [(S, 1), (S + I, 2), (S + 2 * I, 3)]
+    # points S, S+I: only b has a value -> position 0 gets 1, 2 (and a 0 for position 1);
+    # S+2I: a=100 at position 0, b=3 at position 1 -> maxima [100, 3]: a first
+    assert OX.highest([a, b], 2, S, S + 3 * I) == [0, 1]
+    # MaxLatest takes the last point only: [100, 3] as well
+    assert OX.highest([a, b], 2, S, S + 3 * I, current=True) == [0, 1]
+    # d starts when c has ended: every point has one operand, so c's 50 and 60 land in slot 0
+    # -- d's -- and d (max 3) outranks c (max 60)
+    c = [(S, 50), (S + I, 60)]
+    d = [(S + 2 * I, 3)]
+    assert OX.highest([d, c], 1, S, S + 3 * I) == [0]

@@ -160,3 +160,75 @@ def test_gpu_shift_series(eng):
     with pytest.raises(EngineError) as e:
         X.shift_series(eng, [X.Series.of([(1, 1.5)])], 1000)
     assert e.value.code == -9
+
+
+# ---- highestMax / highestCurrent (tsdbhip_expr_topn) -------------------------------------
+def _topn_engine(eng, case):
+    subs = [as_series(sub) for sub in case["inputs"]]
+    flat = [s for sub in subs for s in sub]
+    out = X.FUNCTIONS[case["fn"]](eng, subs, case["params"], case["start"], case["end"])
+    return [next(i for i, s in enumerate(flat) if s is o) for o in out]
+
+
+def _topn_oracle(flat_pts, n, start, end, fn):
+    return OX.highest(flat_pts, n, start, end, current=fn == "highestCurrent")
+
+
+@pytest.mark.parametrize("case", [c for c in G["topn"] if not c["raises"]], ids=lambda c: c["name"])
+def test_gpu_topn_known_answers(eng, case):
+    assert _topn_engine(eng, case) == case["expect_index"]
+
+
+def _rand_topn_series(rng, k, kinds, t0=1356998400000, period=10000, npts=40):
+    out = []
+    for i in range(k):
+        n = int(rng.integers(0, npts))
+        ts = np.sort(rng.choice(np.arange(0, 3 * npts), size=n, replace=False)) * period + t0
+        kind = kinds[i % len(kinds)]
+        pts = []
+        for t in ts:
+            if kind == "int":
+                pts.append((int(t), int(rng.integers(-5000, 5000))))
+            elif kind == "float":
+                pts.append((int(t), float(rng.choice([rng.normal(0, 100), 0.0, -0.0, 1e6]))))
+            else:
+                pts.append((int(t), int(rng.integers(-50, 50)) if rng.random() < 0.5 else float(rng.normal(0, 50))))
+        out.append(pts)
+    return out
+
+
+@pytest.mark.parametrize("fn", ["highestMax", "highestCurrent"])
+@pytest.mark.parametrize("seed,k,kinds", [(1, 5, ("int",)), (2, 12, ("float",)), (3, 30, ("int", "float")),
+                                          (4, 70, ("mixed",)), (5, 130, ("int", "mixed", "float"))])
+def test_gpu_topn_random_vs_oracle(eng, fn, seed, k, kinds):
+    """Late starts, early ends, empty series, LERP between points, long / double points; more
+    series than a wave's lanes (positions carried across 64-span chunks)."""
+    rng = np.random.default_rng(seed)
+    pts = _rand_topn_series(rng, k, kinds)
+    t0 = 1356998400000
+    for start, end in [(t0, t0 + 10 ** 7), (t0 + 200000, t0 + 900000)]:
+        for n in (1, 3, k, 1000):
+            subs = [[X.Series.of(p) for p in pts[: k // 2]], [X.Series.of(p) for p in pts[k // 2:]]]
+            flat = [s for sub in subs for s in sub]
+            try:
+                want = _topn_oracle(pts, n, start, end, fn)
+                werr = None
+            except OX.OracleExprError as e:
+                want, werr = None, e.java
+            try:
+                out = X.FUNCTIONS[fn](eng, subs, [str(n)], start, end)
+                got = [next(i for i, s in enumerate(flat) if s is o) for o in out]
+                gerr = None
+            except EngineError as e:
+                got, gerr = None, e.java
+            assert gerr == werr, (fn, seed, start, n, gerr, werr)
+            assert got == want, (fn, seed, start, n)
+
+
+def test_gpu_topn_no_point_in_range_raises(eng):
+    subs = [[X.Series.of([(1000, 5)]), X.Series.of([(2000, 7)])]]
+    with pytest.raises(EngineError) as e:
+        X.highest_max(eng, subs, ["1"], 5000, 9000)
+    assert e.value.java == "NullPointerException"
+    with pytest.raises(OX.OracleExprError):
+        OX.highest([[(1000, 5)], [(2000, 7)]], 1, 5000, 9000)
