@@ -1061,7 +1061,9 @@ __device__ __forceinline__ void sel_direct_out(const GridParams& p, int K, int32
   const bool has = slot_contribution(p, K, pr_in, v, cv, uni);
   const int lane = lane_id();
   if (lane < K) p.sel_vals[s * K + lane] = has ? canon_nan(cv) : __longlong_as_double(0x7FF87FF87FF87FF8LL);
-  if (uni) p.sel_uni[(int64_t)g * K + lane] = 1;
+  // every series of a group sets the same G x K flags: store only while unset (config 2: 1M
+  // series' byte stores into 64 x 60 flags serialised on a few L2 lines, 6.5 vs 3.9 ms)
+  if (uni && !p.sel_uni[(int64_t)g * K + lane]) p.sel_uni[(int64_t)g * K + lane] = 1;
 }
 
 // End of series s (group g): its SpanGroup contributions, (dense_out) its bucket values, or
@@ -1760,6 +1762,7 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
   }
   if ((meta[0].bits & FM_OK) && !redo && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
   bool have = false;
+  int64_t scur = tbeg[tile];   // series of the rows being folded (dense_out / sel_direct)
   int lsb = INT32_MAX;
   double amax = 0.0;
   FGeom g = {0, 0};
@@ -1774,9 +1777,12 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
           if (have) {
             int64_t s = -1;
             if (p.dense_out || p.sel_direct) {   // the series of the last row folded (dense output only)
+              // rows come in series order: the cursor only moves forward (a scan from the
+              // tile's first series at every series end was quadratic in the tile's series:
+              // config 2 ordered 6.5 vs 3.9 ms)
               const int64_t row = w.r0 + last_rrel;
-              s = tbeg[tile];
-              while (s + 1 < tend[tile] && srp[s + 1] <= row) s++;
+              while (scur + 1 < tend[tile] && srp[scur + 1] <= row) scur++;
+              s = scur;
             }
             const bool ok =
                 KR ? fast_series_end_reg<F>(p, L, K, lsb, amax, RP, s, p.tile_group[tile])

@@ -31,10 +31,10 @@ sys.path.insert(0, ROOT)
 T0 = 1356998400
 
 
-def grid_config(args, eng, queries, n_series, n_points, value_kind, int_mod, groups):
+def grid_config(args, eng, queries, n_series, n_points, value_kind, int_mod, groups, period_ms=10000):
     from opentsdb_amd import abi
     t = time.perf_counter()
-    eng.synth(n_series, T0, n_points, 10000, value_kind, groups, int_mod, 0x5EED)
+    eng.synth(n_series, T0, n_points, period_ms, value_kind, groups, int_mod, 0x5EED)
     eng.sync()
     gen_s = time.perf_counter() - t
     for name, q in queries.items():
@@ -116,6 +116,18 @@ def main():
         return abi.new_query(T0, end, agg, ds_function=d.ds_function, ds_interval_ms=d.ds_interval_ms,
                              ds_fill=d.ds_fill)
 
+    if args.config == 2:   # 1M float32 series x 3600 dp @1 s, 64 groups (the bench.py workload)
+        eng = Engine(0)
+        series = args.series if args.series != 100_000 else 1_000_000
+        aggs = args.only.split(",") if args.only else ["sum", "avg", "dev"]
+        qs = {f"{a}:1m-avg": dsq(a, "1m-avg", T0 + 3599) for a in aggs}
+        if args.ordered:
+            for q in qs.values():
+                q.flags = abi.QF_ORDERED
+            qs = {k + " (ordered)": v for k, v in qs.items()}
+        grid_config(args, eng, qs, series, 3600, 0, 1, args.groups, period_ms=1000)
+        eng.close()
+        return
     if args.config == 3:
         eng = Engine(0)
         series = args.series if args.series != 100_000 else 10_000_000
