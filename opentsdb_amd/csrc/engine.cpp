@@ -391,6 +391,7 @@ struct tsdbhip_ctx {
   DevBuf first_ts;
   int64_t mdp_ss = 0, mdp_se = 0, mdp = 0;
   DevBuf sel_vals, sel_sorted, sel_uni, sel_gsp;   // percentile / median group-by
+  DevBuf sel_wr;                                    // sel_direct: rows of sel_vals written
   DevBuf cal_bounds;                                // calendar month / year slot boundaries
   // raw path scratch
   DevBuf r_rowpt, r_spoff, r_spn, r_grp, r_pts, r_rank, r_bm, r_wb, r_U, r_ooff, r_sg, r_su, r_ots, r_obits, r_oint,
@@ -2220,6 +2221,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     gp.sel_direct = 1;
     gp.sel_vals = c->sel_vals.as<double>();
     gp.sel_uni = c->sel_uni.as<uint8_t>();
+    gp.sel_wr = c->sel_wr.as<uint8_t>();
     gp.group_series_ptr = c->sel_gsp.as<int64_t>();
   } else if (P.dense_out) {
     HIP_OK(c->pre_dense.ensure(std::max<int64_t>(1, c->n_series * K) * 8));
@@ -2643,7 +2645,10 @@ int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G)
     HIP_OK(c->sel_vals.ensure(std::max<int64_t>(1, S * K) * 8));
     HIP_OK(c->sel_uni.ensure(std::max<int64_t>(1, G * K)));
     HIP_OK(hipMemcpyAsync(c->sel_gsp.p, gsp.data(), (G + 1) * 8, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(launch_fill64(c->sel_vals.as<uint64_t>(), 0x7FF87FF87FF87FF8ULL, S * K, c->stream));   // +NaN
+    // a written-row flag per series, and the no-value pattern afterwards only into the rows
+    // the pass did not write (config 3: 10 MB of flags instead of filling 4.8 GB up front)
+    HIP_OK(c->sel_wr.ensure(std::max<int64_t>(1, S)));
+    HIP_OK(hipMemsetAsync(c->sel_wr.p, 0, std::max<int64_t>(1, S), c->stream));
     HIP_OK(hipMemsetAsync(c->sel_uni.p, 0, std::max<int64_t>(1, G * K), c->stream));
     Plan P2;
     int rc = plan_query(c, q, P2);
@@ -2651,6 +2656,7 @@ int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G)
     P2.sel_direct = true;
     rc = run_device(c, q, P2, G, false);   // sets c->gact like the group-by pass
     if (rc) return rc;
+    HIP_OK(launch_fill_rows(c->sel_vals.as<uint64_t>(), c->sel_wr.as<uint8_t>(), S, K, 0x7FF87FF87FF87FF8ULL, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));   // `gsp` leaves scope
     return 0;
   }

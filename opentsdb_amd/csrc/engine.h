@@ -127,6 +127,7 @@ struct GridParams {
   // span's K values contiguous); NaN = no contribution
   double* sel_vals;
   uint8_t* sel_uni;            // [G][K]: some series contributed with a real point (emit)
+  uint8_t* sel_wr;             // [series] 1 = sel_direct wrote the series' row (null: rows pre-filled)
   const int64_t* group_series_ptr;   // [G + 1]
   // 1: the downsampling pass writes the contributions itself (kcommon.h sel_direct_out;
   // K <= 64, no rate)
@@ -374,6 +375,8 @@ hipError_t launch_first_ts(const RowDesc* rows, const int64_t* srp, const uint8_
                            int64_t se, int64_t t0, int64_t* out, hipStream_t s);
 // n 8-byte words of `v` from p (16-byte aligned): 16-byte non-temporal stores
 hipError_t launch_fill64(uint64_t* p, uint64_t v, int64_t n, hipStream_t s);
+// the rows [series][K] of `p` whose wr flag is 0 filled with `v` (after a sel_direct pass)
+hipError_t launch_fill_rows(uint64_t* p, const uint8_t* wr, int64_t n_series, int64_t K, uint64_t v, hipStream_t s);
 // streaming variant for one uniform row class (k_fast's premises + the sum certificate);
 // series that break a premise go to p.redo_list for launch_rollup_agg (tile_list mode)
 bool rollup_fast_supported(int qw, int vl);

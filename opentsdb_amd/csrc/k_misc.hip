@@ -246,6 +246,21 @@ __global__ __launch_bounds__(256) void k_fill64(uint64_t* p, uint64_t v, int64_t
   if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) p[n - 1] = v;
 }
 
+// Rows the sel_direct pass did not write (series with no row in the scan range): the no-value
+// pattern, so the whole S x K buffer need not be filled beforehand.
+__global__ __launch_bounds__(256) void k_fill_rows(uint64_t* p, const uint8_t* wr, int64_t n_series, int64_t K,
+                                                   uint64_t v) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_series || wr[s]) return;
+  for (int64_t k = 0; k < K; k++) p[s * K + k] = v;
+}
+
+hipError_t launch_fill_rows(uint64_t* p, const uint8_t* wr, int64_t n_series, int64_t K, uint64_t v, hipStream_t s) {
+  if (n_series <= 0 || K <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fill_rows, dim3((unsigned)((n_series + 255) / 256)), dim3(256), 0, s, p, wr, n_series, K, v);
+  return hipGetLastError();
+}
+
 hipError_t launch_fill64(uint64_t* p, uint64_t v, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(((n >> 1) + 255) / 256, 256 * 16));

@@ -1054,6 +1054,7 @@ __device__ __forceinline__ void emit_series_reg(const GridParams& p, int K, bool
 // sel_vals[s * K + k] (one coalesced row per series; the fill pattern where it has none) and
 // marks the union slots -- k_emit_vals' output without the bucket values round-tripping
 // through pre_dense.
+template <bool MARK = true>   // MARK: flag the row written (k_short flags its whole tile at the end)
 __device__ __forceinline__ void sel_direct_out(const GridParams& p, int K, int32_t g, int64_t s, bool pr_in,
                                                double v) {
   double cv = 0.0;
@@ -1064,6 +1065,7 @@ __device__ __forceinline__ void sel_direct_out(const GridParams& p, int K, int32
   // every series of a group sets the same G x K flags: store only while unset (config 2: 1M
   // series' byte stores into 64 x 60 flags serialised on a few L2 lines, 6.5 vs 3.9 ms)
   if (uni && !p.sel_uni[(int64_t)g * K + lane]) p.sel_uni[(int64_t)g * K + lane] = 1;
+  if (MARK && lane == 0 && p.sel_wr) p.sel_wr[s] = 1;
 }
 
 // End of series s (group g): its SpanGroup contributions, (dense_out) its bucket values, or
@@ -1648,7 +1650,7 @@ __device__ __forceinline__ double fast_bucket_value(uint32_t c, double a) {
 }
 
 // K <= 64, no rate: the register-partial variant (emit_series_reg).
-template <int F>
+template <int F, bool MARK = true>
 __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const FastLds& L, int K, int lsb, double amax,
                                                     RegPart& P, int64_t s, int32_t g, uint32_t nbound = 0) {
   const int lane = lane_id();
@@ -1666,7 +1668,7 @@ __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const F
     if (!fast_cert<F>(nmax, lsb, amax)) return false;
   }
   if (p.sel_direct) {
-    sel_direct_out(p, K, g, s, c != 0, fast_bucket_value<F>(c, a));
+    sel_direct_out<MARK>(p, K, g, s, c != 0, fast_bucket_value<F>(c, a));
   } else if (p.dense_out) {
     if (lane < K) {
       p.dense_out[s * K + lane] = fast_bucket_value<F>(c, a);
@@ -1965,7 +1967,7 @@ __global__ __launch_bounds__(256, SHORT_OCC(VL)) void k_short(GridParams p, cons
     const int lsb = __builtin_amdgcn_readlane(dlsb, j);
     const double amax = __longlong_as_double((long long)rl64(damax, j));
     const bool fine =
-        KR ? fast_series_end_reg<F>(p, L, K, lsb, amax, RP, s0 + j, p.tile_group[tile], (uint32_t)nv0)
+        KR ? fast_series_end_reg<F, false>(p, L, K, lsb, amax, RP, s0 + j, p.tile_group[tile], (uint32_t)nv0)
            : fast_series_end<F>(p, L, K, lsb, amax, s0 + j, p.tile_group[tile]);
     if (!fine) redo = true;
   };
@@ -1993,6 +1995,7 @@ __global__ __launch_bounds__(256, SHORT_OCC(VL)) void k_short(GridParams p, cons
     if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
     return;
   }
+  if (p.sel_wr && lane < ns) p.sel_wr[s0 + lane] = 1;   // sel_direct: every series of the tile was written
   WAVE_SYNC();
   double* ga_ = p.part.a + tile * K;
   double* gb_ = p.part.b + tile * K;
