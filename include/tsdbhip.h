@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define TSDBHIP_ABI_VERSION 7
+#define TSDBHIP_ABI_VERSION 8
 
 /* ---- error codes: one per Java exception on the path --------------------- */
 enum {
@@ -171,6 +171,8 @@ typedef struct {
   double index_ms;               /* k_index of the last tsdbhip_load / tsdbhip_synth: row classification,
                                     validation, certificate stats (+ the int16 value copy of vle rows) */
   double compact_ms;             /* device compaction of the last tsdbhip_load_cells (k_compact pipeline) */
+  int64_t fused_queries;         /* queries the last tsdbhip_run_multi answered from ONE fused streaming pass
+                                    (0: separate passes, or not a run_multi) */
 } tsdbhip_timing;
 
 /* ---- library-level helpers (host logic of the reference, restated) ------- */
@@ -229,13 +231,24 @@ int tsdbhip_batch_sizes(tsdbhip_ctx* ctx, int64_t* n_series, int64_t* n_rows, ui
 int tsdbhip_batch_download(tsdbhip_ctx* ctx, int64_t* series_row_ptr, uint32_t* row_base_time,
                            uint64_t* row_qual_off, uint64_t* row_val_off, uint8_t* qual, uint8_t* val,
                            int32_t* group_id);
+/* The same for resident series positions [s0, s1) only (offsets from 0; only the rows' blob span
+ * is copied, so slices of a store larger than host memory can be checked).  Any output pointer
+ * may be NULL: that part is skipped (e.g. group_id alone gives the resident group order). */
+int tsdbhip_batch_range_sizes(tsdbhip_ctx* ctx, int64_t s0, int64_t s1, int64_t* n_rows, uint64_t* qual_bytes,
+                              uint64_t* val_bytes);
+int tsdbhip_batch_download_range(tsdbhip_ctx* ctx, int64_t s0, int64_t s1, int64_t* series_row_ptr,
+                                 uint32_t* row_base_time, uint64_t* row_qual_off, uint64_t* row_val_off,
+                                 uint8_t* qual, uint8_t* val, int32_t* group_id);
 
 /* Run the query over the resident batch: TsdbQuery.run() from GroupByAndAggregateCB on. */
 int tsdbhip_run(tsdbhip_ctx* ctx, const tsdbhip_query* q, tsdbhip_result** out);
 /* n queries that share the time range and the downsampling specification (a TSQuery with
  * several sub-queries over one metric).  A percentile / median downsampling is computed once
- * and shared by the queries' group-by steps; the cheap functions run one fused pass per
- * query.  outs[i] as tsdbhip_run's result; on error none is returned. */
+ * and shared by the queries' group-by steps.  With a cheap downsampling function, decomposable
+ * group-by aggregators (sum, avg, min, max, dev, count; no rate, no flags, <= 64 output slots)
+ * share ONE fused streaming pass that keeps every aggregator's SpanGroup state -- results
+ * bit-identical to separate tsdbhip_run calls (tsdbhip_timing.fused_queries = n); any other mix
+ * runs one fused pass per query.  outs[i] as tsdbhip_run's result; on error none is returned. */
 int tsdbhip_run_multi(tsdbhip_ctx* ctx, const tsdbhip_query* qs, int n, tsdbhip_result** outs);
 void tsdbhip_result_free(tsdbhip_result* r);
 int tsdbhip_last_timing(tsdbhip_ctx* ctx, tsdbhip_timing* out);

@@ -142,6 +142,7 @@ class Timing(C.Structure):
         ("fast_ms", C.c_double),
         ("index_ms", C.c_double),
         ("compact_ms", C.c_double),
+        ("fused_queries", C.c_int64),
     ]
 
 

@@ -378,7 +378,8 @@ struct tsdbhip_ctx {
   // scratch
   DevBuf pa, pb, pn, pf, out_val, out_flag, gact, err, g_dense, g_pres, g_rate, redo, redo_n, redo2, redo2_n;
   DevBuf xbuf, gbuf;
-  DevBuf pre_dense, pre_pres;          // percentile / median downsampling
+  DevBuf m_sum, m_mn, m_mx, m_mean, m_m2, m_nl, m_nz, m_f;   // fused multi-aggregator partials
+  DevBuf pre_dense, pre_pres;         // percentile / median downsampling
   DevBuf big_scratch;                  // k_pct large buckets: per-wave overflow regions
   bool mdp_valid = false;              // series_max_dp() cache (invalidated by every load)
   bool ro_meta_valid = false;          // rollup ro_ord / ro_orig / ro_allint of the loaded batch
@@ -412,6 +413,7 @@ struct tsdbhip_ctx {
   tsdbhip_timing timing{};
   double index_ms = 0;                   // k_index (+ val2 pass) of the last load
   double compact_ms = 0;                 // k_compact pipeline of the last tsdbhip_load_cells
+  int64_t fused_n = 0;                   // queries of the fused multi-aggregator pass being collected
   // account() cache (invalidated by every load)
   bool acct_valid = false;
   int64_t acct_ss = 0, acct_se = 0, acct_dps = 0, acct_bytes = 0;
@@ -1783,6 +1785,73 @@ extern "C" int tsdbhip_batch_download(tsdbhip_ctx* c, int64_t* series_row_ptr, u
   return 0;
 }
 
+// Sizes of resident series positions [s0, s1) in the tsdbhip_batch layout.
+extern "C" int tsdbhip_batch_range_sizes(tsdbhip_ctx* c, int64_t s0, int64_t s1, int64_t* n_rows, uint64_t* qual_bytes,
+                                         uint64_t* val_bytes) {
+  if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
+  if (c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_batch_range_sizes over a rollup batch");
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (s0 < 0 || s1 < s0 || s1 > c->n_series) return fail(TSDB_E_ILLEGAL_ARGUMENT, "series range out of bounds");
+  const int64_t r0 = c->h_srp[s0], r1 = c->h_srp[s1];
+  uint64_t q = 0, v = 0;
+  for (int64_t r = r0; r < r1; r++) { q += c->h_qlen[r]; v += c->h_vlen[r]; }
+  if (n_rows) *n_rows = r1 - r0;
+  if (qual_bytes) *qual_bytes = q;
+  if (val_bytes) *val_bytes = v;
+  return 0;
+}
+
+// Resident series positions [s0, s1) back to host in the tsdbhip_batch layout (offsets from 0).
+// Only the blob span those rows occupy crosses PCIe, so a slice of a store far larger than host
+// memory can be checked.  Any output pointer may be null (that part is skipped).
+extern "C" int tsdbhip_batch_download_range(tsdbhip_ctx* c, int64_t s0, int64_t s1, int64_t* series_row_ptr,
+                                            uint32_t* row_base_time, uint64_t* row_qual_off, uint64_t* row_val_off,
+                                            uint8_t* qual, uint8_t* val, int32_t* group_id) {
+  if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
+  if (c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_batch_download_range over a rollup batch");
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (s0 < 0 || s1 < s0 || s1 > c->n_series) return fail(TSDB_E_ILLEGAL_ARGUMENT, "series range out of bounds");
+  HIP_OK(hipSetDevice(c->device));
+  const int64_t r0 = c->h_srp[s0], r1 = c->h_srp[s1], nr = r1 - r0;
+  if (series_row_ptr)
+    for (int64_t s = s0; s <= s1; s++) series_row_ptr[s - s0] = c->h_srp[s] - r0;
+  if (group_id)
+    for (int64_t s = s0; s < s1; s++) group_id[s - s0] = c->h_group[s] >= c->n_groups ? -1 : c->h_group[s];
+  if (!row_base_time && !row_qual_off && !row_val_off && !qual && !val) return 0;
+  std::vector<RowDesc> rd(nr);
+  if (nr) HIP_OK(hipMemcpy(rd.data(), (const RowDesc*)c->rows.p + r0, nr * sizeof(RowDesc), hipMemcpyDeviceToHost));
+  // the blob spans of the rows (rows of consecutive positions are laid out in order, but the
+  // span is taken from the descriptors, whatever the layout)
+  uint64_t qlo = UINT64_MAX, qhi = 0, vlo = UINT64_MAX, vhi = 0;
+  for (const RowDesc& d : rd) {
+    qlo = std::min<uint64_t>(qlo, d.qoff); qhi = std::max<uint64_t>(qhi, d.qoff + d.qlen);
+    vlo = std::min<uint64_t>(vlo, d.voff); vhi = std::max<uint64_t>(vhi, d.voff + d.vlen);
+  }
+  std::vector<uint8_t> hq, hv;
+  if (qual && qhi > qlo) {
+    hq.resize(qhi - qlo);
+    HIP_OK(hipMemcpy(hq.data(), (const uint8_t*)c->qual.p + qlo, qhi - qlo, hipMemcpyDeviceToHost));
+  }
+  if (val && vhi > vlo) {
+    hv.resize(vhi - vlo);
+    HIP_OK(hipMemcpy(hv.data(), (const uint8_t*)c->val.p + vlo, vhi - vlo, hipMemcpyDeviceToHost));
+  }
+  uint64_t qo = 0, vo = 0;
+  for (int64_t i = 0; i < nr; i++) {
+    const RowDesc& d = rd[i];
+    if (row_base_time) row_base_time[i] = d.base;
+    if (row_qual_off) row_qual_off[i] = qo;
+    if (row_val_off) row_val_off[i] = vo;
+    if (qual && d.qlen) std::memcpy(qual + qo, hq.data() + (d.qoff - qlo), d.qlen);
+    if (val && d.vlen) std::memcpy(val + vo, hv.data() + (d.voff - vlo), d.vlen);
+    qo += d.qlen;
+    vo += d.vlen;
+  }
+  if (row_qual_off) row_qual_off[nr] = qo;
+  if (row_val_off) row_val_off[nr] = vo;
+  return 0;
+}
+
 // Test hook: the per-row facts k_index derived (RowDesc.ndp / flags / lsb / absmax).
 extern "C" int tsdbhip_debug_rows(tsdbhip_ctx* c, uint32_t* ndp, uint32_t* flags, int32_t* lsb, double* absmax) {
   if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
@@ -1820,6 +1889,7 @@ struct Plan {
   bool ordered = false;          // TSDB_QF_ORDERED float reduction: run_ordered
   bool values_only = false;      // percentile downsampling pass without the group-by step
   bool emit_only = false;        // group-by step over bucket values already in pre_dense / pre_pres
+  bool multi = false;            // fused multi-aggregator pass (run_multi_fused): partials to c->mp*, no reduce
 };
 
 bool is_sel_agg(int a) { return a == TSDB_AGG_MEDIAN || (a >= TSDB_AGG_P999 && a < TSDB_AGG_COUNT_ALL); }
@@ -2154,6 +2224,17 @@ int64_t series_max_dp(tsdbhip_ctx* c, int64_t ss, int64_t se) {
   return m;
 }
 
+// The streaming kernels (k_short / k_fast) can take the query: fixed grid, a row class of the
+// batch they are specialised for, their LDS slot budget.
+bool fast_path_ok(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P) {
+  if (!(P.mode == MODE_GRID && c->fast_qw &&
+        (fast_supported(P.f, c->fast_qw, c->fast_vl) || (c->fast_qw2 && fast_supported(P.f, c->fast_qw2, c->fast_vl2))) &&
+        P.I <= (1LL << 29) && fast_wave_lds(P.K, q->rate != 0) <= 32 * 1024 && P.K > 0))
+    return false;
+  const char* env = std::getenv("TSDBHIP_FAST");
+  return !(env && env[0] == '0');
+}
+
 int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bool do_reduce) {
   const bool none = P.none;
   if (none) { int rc = build_none_tiles(c); if (rc) return rc; }
@@ -2216,6 +2297,20 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   gp.part = Partials{c->pa.as<double>(), c->pb.as<double>(), c->pn.as<uint32_t>(), c->pf.as<uint32_t>()};
   gp.group_active = c->gact.as<uint32_t>();
   gp.err = c->err.as<int32_t>();
+  if (P.multi) {   // fused multi-aggregator pass: every decomposable aggregator's tile partials
+    const int64_t n = std::max<int64_t>(1, nt * K);
+    HIP_OK(c->m_sum.ensure(n * 8));
+    HIP_OK(c->m_mn.ensure(n * 8));
+    HIP_OK(c->m_mx.ensure(n * 8));
+    HIP_OK(c->m_mean.ensure(n * 8));
+    HIP_OK(c->m_m2.ensure(n * 8));
+    HIP_OK(c->m_nl.ensure(n * 4));
+    HIP_OK(c->m_nz.ensure(n * 4));
+    HIP_OK(c->m_f.ensure(n * 4));
+    gp.multi = 1;
+    gp.mp = MultiPartials{c->m_sum.as<double>(), c->m_mn.as<double>(), c->m_mx.as<double>(), c->m_mean.as<double>(),
+                          c->m_m2.as<double>(), c->m_nl.as<uint32_t>(), c->m_nz.as<uint32_t>(), c->m_f.as<uint32_t>()};
+  }
   if (const char* dbg = std::getenv("TSDBHIP_DBG")) gp.dbg = std::atoi(dbg);
   if (P.sel_direct) {   // buffers prepared by sel_values
     gp.sel_direct = 1;
@@ -2306,14 +2401,8 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   } else {
   // streaming kernel first (when the batch's row class and the query allow it), then the
   // general kernel over the tiles it handed back
-  bool fast = false;
-  if (P.mode == MODE_GRID && c->fast_qw &&
-      (fast_supported(P.f, c->fast_qw, c->fast_vl) || (c->fast_qw2 && fast_supported(P.f, c->fast_qw2, c->fast_vl2))) &&
-      P.I <= (1LL << 29) &&
-      fast_wave_lds(K, q->rate != 0) <= 32 * 1024 && K > 0) {
-    const char* env = std::getenv("TSDBHIP_FAST");
-    fast = !(env && env[0] == '0');
-  }
+  const bool fast = fast_path_ok(c, q, P);
+  if (P.multi && !fast) return fail(TSDB_E_NOT_IMPLEMENTED, "fused multi-aggregator pass without the streaming kernels");
   c->fast_used = fast;
   HIP_OK(hipEventRecord(c->ev[0], c->stream));
   if (fast) {
@@ -2400,6 +2489,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     if (!none && !c->tl_other.empty()) to_grid.push_back({dl + c->tl_off[4], {dn + 4, (int64_t)c->tl_other.size()}});
     HIP_OK(hipEventRecord(c->ev[3], c->stream));
     for (auto& tg : to_grid) {
+      if (P.multi) break;   // the caller checks that nothing was handed back (else separate passes)
       GridParams g2 = gp;
       g2.tile_list = tg.first;
       g2.tile_list_n = tg.second.first;
@@ -2815,18 +2905,20 @@ void record_timing(tsdbhip_ctx* c, const Plan& P, int32_t redo_n) {
   c->timing.fast_ms = t03;
   c->timing.tiles = P.none ? c->n_series : (int64_t)c->tb.size();
   c->timing.redo_tiles = c->fast_used ? redo_n + c->redo_other : c->timing.tiles;
+  c->timing.fused_queries = c->fused_n;
   account(c, P);
 }
 
 // Dense [G][K] outputs on the device -> result (after the stream's work is queued).
-int collect(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bool timed, tsdbhip_result** out) {
+int collect(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bool timed, tsdbhip_result** out,
+            const void* d_val = nullptr, const void* d_flag = nullptr) {
   std::vector<double> val(G * P.K);
   std::vector<uint8_t> flag(G * P.K);
   std::vector<uint32_t> act(std::max<int64_t>(1, G));
   int32_t err = 0;
   if (G * P.K) {
-    HIP_OK(hipMemcpyAsync(val.data(), c->out_val.p, G * P.K * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipMemcpyAsync(flag.data(), c->out_flag.p, G * P.K, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipMemcpyAsync(val.data(), d_val ? d_val : c->out_val.p, G * P.K * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipMemcpyAsync(flag.data(), d_flag ? d_flag : c->out_flag.p, G * P.K, hipMemcpyDeviceToHost, c->stream));
   }
   if (G) HIP_OK(hipMemcpyAsync(act.data(), c->gact.p, G * 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
@@ -2997,10 +3089,18 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
   double eval_ms = 0.0;
   const bool direct = !P.none && per_chunk >= G;
   tsdbhip_result* direct_r = nullptr;
+  // On an early return the copy stream may still be writing into direct_r's pinned block:
+  // drain it before the block goes back to the pool.
   struct Guard {
     tsdbhip_result** r;
-    ~Guard() { result_free(*r); }
-  } guard{&direct_r};
+    hipStream_t cs;
+    ~Guard() {
+      if (*r) {
+        (void)hipStreamSynchronize(cs);
+        result_free(*r);
+      }
+    }
+  } guard{&direct_r, c->copy_stream};
   for (int64_t g0 = 0; g0 < G; g0 += per_chunk) {
     const int64_t g1 = std::min(G, g0 + per_chunk);
     const int64_t ng = g1 - g0;
@@ -3381,6 +3481,81 @@ int run_rollup(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
   return collect(c, &qr, P, G, true, out);
 }
 
+// Several decomposable group-by aggregators over one cheap downsampling, fused: ONE streaming
+// pass (k_short / k_fast, KR 2) decodes and downsamples every series once and folds each
+// series' SpanGroup contributions into the per-tile state of every aggregator at once
+// (kcommon.h MultiReg: sum / avg, min, max, dev, count); then one k_reduce per query over its
+// view of those states.  Each aggregator sees exactly the contributions -- in the same order --
+// that its own pass would feed it (AggregationIterator.nextDoubleValue :735-797 per span, per
+// timestamp), so results are bit-identical to separate queries.  Returns 1 when the queries or
+// the batch do not qualify (rate, other aggregators, flags, a row class the streaming kernels do
+// not take, K > 64) or when a tile broke a streaming premise at run time: the caller then runs
+// the queries one by one.
+int run_multi_fused(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_result** outs) {
+  const char* env = std::getenv("TSDBHIP_MULTI_FUSE");
+  if (n < 2 || (env && env[0] == '0')) return 1;
+  for (int i = 0; i < n; i++) {
+    const int a = qs[i].aggregator;
+    if (!(a == TSDB_AGG_SUM || a == TSDB_AGG_AVG || a == TSDB_AGG_MIN || a == TSDB_AGG_MAX || a == TSDB_AGG_DEV ||
+          a == TSDB_AGG_COUNT) ||
+        qs[i].rate || qs[i].flags)
+      return 1;
+  }
+  tsdbhip_query q0 = qs[0];
+  q0.aggregator = TSDB_AGG_SUM;   // LERP: the interpolation of every fused aggregator but count
+  Plan P;
+  int rc = plan_query(c, &q0, P);
+  if (rc) return rc;
+  if (P.raw || P.none || P.gsel || P.f == F_SEL || P.K > 64 || !fast_path_ok(c, &q0, P) || !c->tl_other.empty())
+    return 1;
+  for (int cls = 0; cls < 2; cls++) {
+    if (c->tl[cls][0].empty() && c->tl[cls][1].empty()) continue;
+    const int qw = cls ? c->fast_qw2 : c->fast_qw, vl = cls ? c->fast_vl2 : c->fast_vl;
+    if (!qw || !fast_supported(P.f, qw, vl)) return 1;
+  }
+  const int64_t G = c->n_groups, K = P.K;
+  P.multi = true;
+  rc = run_device(c, &q0, P, G, false);
+  if (rc) return rc;
+  int32_t handed_back = 0;
+  HIP_OK(hipMemcpyAsync(&handed_back, c->redo_final, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  if (handed_back) return 1;
+  // one k_reduce per query over its view of the fused partials, into its own output rows
+  const int64_t gk = std::max<int64_t>(1, G * K);
+  HIP_OK(c->out_val.ensure(gk * 8 * n));
+  HIP_OK(c->out_flag.ensure(gk * n));
+  std::vector<Plan> plans(n);
+  for (int i = 0; i < n; i++) {
+    rc = plan_query(c, &qs[i], plans[i]);
+    if (rc) return rc;
+    const int ga = ga_of(qs[i].aggregator);
+    ReduceParams rp{};
+    switch (qs[i].aggregator) {
+      case TSDB_AGG_MIN: rp.part = Partials{c->m_mn.as<double>(), c->m_m2.as<double>(), c->m_nl.as<uint32_t>(), c->m_f.as<uint32_t>()}; break;
+      case TSDB_AGG_MAX: rp.part = Partials{c->m_mx.as<double>(), c->m_m2.as<double>(), c->m_nl.as<uint32_t>(), c->m_f.as<uint32_t>()}; break;
+      case TSDB_AGG_DEV: rp.part = Partials{c->m_mean.as<double>(), c->m_m2.as<double>(), c->m_nl.as<uint32_t>(), c->m_f.as<uint32_t>()}; break;
+      case TSDB_AGG_COUNT: rp.part = Partials{c->m_sum.as<double>(), c->m_m2.as<double>(), c->m_nz.as<uint32_t>(), c->m_f.as<uint32_t>()}; break;
+      default: rp.part = Partials{c->m_sum.as<double>(), c->m_m2.as<double>(), c->m_nl.as<uint32_t>(), c->m_f.as<uint32_t>()};
+    }
+    rp.group_tile_ptr = c->d_gtp.as<int64_t>();
+    rp.G = G;
+    rp.K = K;
+    rp.ga = ga;
+    rp.out_val = c->out_val.as<double>() + i * gk;
+    rp.out_flag = c->out_flag.as<uint8_t>() + i * gk;
+    rp.err = c->err.as<int32_t>();
+    HIP_OK(launch_reduce(rp, c->stream));
+  }
+  HIP_OK(hipEventRecord(c->ev[2], c->stream));
+  c->fused_n = n;
+  for (int i = 0; i < n && !rc; i++)
+    rc = collect(c, &qs[i], plans[i], G, true, &outs[i], c->out_val.as<double>() + i * gk,
+                 c->out_flag.as<uint8_t>() + i * gk);
+  c->fused_n = 0;
+  return rc;
+}
+
 }  // namespace
 
 extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
@@ -3433,10 +3608,15 @@ extern "C" int tsdbhip_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n,
   if (rc) return rc;
   if (P0.raw) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_run_multi needs a downsampling specification");
   if (P0.f != F_SEL) {
-    // Cheap downsampling functions: the streaming kernels fuse decode, downsample and the
-    // group-by step in one pass that beats the generic group-by step over stored buckets
-    // (config 3, 5 aggregators: 22 ms as separate passes vs 35 ms sharing one), so each
-    // query runs its own pass.
+    // Cheap downsampling functions: decomposable aggregators (sum, avg, min, max, dev, count)
+    // share ONE streaming pass that keeps every aggregator's SpanGroup state (run_multi_fused);
+    // otherwise each query runs its own fused pass, which beats a generic group-by step over
+    // stored buckets (config 3, 5 aggregators: 22 ms as separate passes vs 35 ms sharing one).
+    rc = run_multi_fused(c, qs, n, outs);
+    if (rc <= 0) {
+      if (rc) for (int j = 0; j < n; j++) { result_free(outs[j]); outs[j] = nullptr; }
+      return rc;
+    }
     for (int i = 0; i < n; i++) {
       Plan P;
       rc = plan_query(c, &qs[i], P);

@@ -50,6 +50,14 @@ struct Partials {
 
 enum : uint32_t { PF_UNION = 1u, PF_HAS = 2u };
 
+// Per-tile partial states of the fused multi-aggregator pass (GridParams.multi), [tile][K]:
+// sum / avg (sum, nl), min (mn), max (mx), dev (mean, m2, nl), count (nz); f = union flags.
+// Aggregator x reads them as Partials (k_reduce) -- see multi_partials_of in engine.cpp.
+struct MultiPartials {
+  double *sum, *mn, *mx, *mean, *m2;
+  uint32_t *nl, *nz, *f;
+};
+
 // Kernel modes
 enum : int { MODE_GRID = 0, MODE_ALL = 1, MODE_TABLE = 2 };   // TABLE: slot k = [bounds[k], bounds[k+1]) (calendar months / years)
 
@@ -140,6 +148,10 @@ struct GridParams {
   // of more than PCT_CAP values (big_cap >= the largest series' in-range datapoints)
   double* big_scratch;
   int64_t big_cap;
+  // fused multi-aggregator pass (tsdbhip_run_multi): the register-partial kernels keep every
+  // decomposable aggregator's state and write them to mp (K <= 64, no rate, LERP + count)
+  int32_t multi;
+  MultiPartials mp;
   int32_t dbg;           // k_short profiling switches (TSDBHIP_DBG, results invalid): 1 skip series end,
                          // 2 skip chunk fold, 8 consume loads, 16 stop after the descriptors, 32 load row 0 only
 };

@@ -16,7 +16,7 @@
 
 namespace tsdb {
 
-template <int F, int QW, int VL, bool KR>
+template <int F, int QW, int VL, int KR>
 static hipError_t launch_fast_k(const GridParams& p, hipStream_t s) {
   constexpr int D = (QW * 2 + VL * 2 <= 16) ? 3 : 2;   // ring depth: chunk registers per lane
   const int64_t nl = p.n_launch > 0 ? p.n_launch : p.n_tiles;
@@ -42,10 +42,12 @@ static hipError_t launch_fast_k(const GridParams& p, hipStream_t s) {
 }
 
 // register partials when every slot has its own lane and the series emit needs no rate pass
+// (KR 1; KR 2: every decomposable aggregator's partials at once, tsdbhip_run_multi)
 template <int F, int QW, int VL>
 static hipError_t launch_fast_t(const GridParams& p, hipStream_t s) {
-  if (p.K <= 64 && !p.rate) return launch_fast_k<F, QW, VL, true>(p, s);
-  return launch_fast_k<F, QW, VL, false>(p, s);
+  if (p.K <= 64 && !p.rate) return p.multi ? launch_fast_k<F, QW, VL, 2>(p, s) : launch_fast_k<F, QW, VL, 1>(p, s);
+  if (p.multi) return hipErrorNotSupported;
+  return launch_fast_k<F, QW, VL, 0>(p, s);
 }
 
 template <>

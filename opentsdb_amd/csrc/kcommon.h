@@ -22,6 +22,7 @@
 
 #include <float.h>
 #include <math.h>
+#include <type_traits>
 
 #include "../../include/tsdbhip.h"
 
@@ -1049,6 +1050,81 @@ __device__ __forceinline__ void emit_series_reg(const GridParams& p, int K, bool
   if (slot_contribution(p, K, pr_in, v, cv, uni)) contribute_slot(p.ga, P, cv, uni);
 }
 
+// Several group-by aggregators over one downsampling in one pass (tsdbhip_run_multi,
+// p.multi): the lane's slot keeps the SpanGroup state of sum / avg (sum, nl), min, max, dev
+// (Welford mean, m2 over the same nl) and count (nz), all fed the same contribution sequence
+// contribute_slot would feed each of them alone -- so every aggregator's tile partial is
+// bit-identical to its own pass.  Count interpolates with ZIM (Aggregators.java:620-647), the
+// others with LERP: they differ only where a slot is interpolated, where count reads 0.0.
+struct MultiReg {
+  double sum, mn, mx, mean, m2;
+  uint32_t nl, nz, f;
+};
+
+__device__ __forceinline__ void rp_init(int ga, RegPart& P) { regpart_init(ga, P); }
+__device__ __forceinline__ void rp_init(int, MultiReg& M) {
+  M.sum = 0.0;
+  M.mn = INFINITY;
+  M.mx = -INFINITY;
+  M.mean = 0.0;
+  M.m2 = 0.0;
+  M.nl = 0;
+  M.nz = 0;
+  M.f = 0;
+}
+
+__device__ __forceinline__ void emit_series_reg(const GridParams& p, int K, bool pr_in, double v, MultiReg& M) {
+  double cv;
+  bool uni;
+  if (!slot_contribution(p, K, pr_in, v, cv, uni)) return;   // p.interp is LERP
+  const bool interpolated = (p.fill == TSDB_FILL_NONE || p.mode == MODE_ALL) && !(lane_id() < K && pr_in);
+  if (!isnan(cv)) {
+    M.sum += cv;
+    if (cv < M.mn) M.mn = cv;
+    if (cv > M.mx) M.mx = cv;
+    const uint32_t c = M.nl;   // contribute_slot's GA_DEV step
+    if (c == 0) {
+      M.mean = cv;
+    } else {
+      const double m = M.mean;
+      const double nm = m + (cv - m) / (double)(c + 1);
+      M.m2 += (cv - m) * (cv - nm);
+      M.mean = nm;
+    }
+    M.nl = c + 1;
+    M.nz++;
+  } else if (interpolated) {
+    M.nz++;   // ZIM reads 0.0 where LERP produced NaN
+  }
+  if (uni) M.f |= PF_UNION;
+}
+
+// the tile's partial states, lane = slot (K <= 64)
+__device__ __forceinline__ void rp_store(const GridParams& p, int64_t tile, int K, const RegPart& P) {
+  const int lane = lane_id();
+  if (lane < K) {
+    const int64_t o = tile * K + lane;
+    p.part.a[o] = P.pa;
+    p.part.b[o] = P.pb;
+    p.part.n[o] = P.pn;
+    p.part.f[o] = P.pf;
+  }
+}
+__device__ __forceinline__ void rp_store(const GridParams& p, int64_t tile, int K, const MultiReg& M) {
+  const int lane = lane_id();
+  if (lane < K) {
+    const int64_t o = tile * K + lane;
+    p.mp.sum[o] = M.sum;
+    p.mp.mn[o] = M.mn;
+    p.mp.mx[o] = M.mx;
+    p.mp.mean[o] = M.mean;
+    p.mp.m2[o] = M.m2;
+    p.mp.nl[o] = M.nl;
+    p.mp.nz[o] = M.nz;
+    p.mp.f[o] = M.f;
+  }
+}
+
 // Percentile / median (and ordered) group-by, fused into the downsampling pass (p.sel_direct,
 // K <= 64, no rate): series s of group g writes its contribution to every slot straight into
 // sel_vals[s * K + k] (one coalesced row per series; the fill pattern where it has none) and
@@ -1649,10 +1725,11 @@ __device__ __forceinline__ double fast_bucket_value(uint32_t c, double a) {
   return a == -INFINITY ? (double)NAN : a;
 }
 
-// K <= 64, no rate: the register-partial variant (emit_series_reg).
-template <int F, bool MARK = true>
+// K <= 64, no rate: the register-partial variant (emit_series_reg; RP = RegPart, or MultiReg
+// for the fused multi-aggregator pass).
+template <int F, bool MARK = true, class RP>
 __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const FastLds& L, int K, int lsb, double amax,
-                                                    RegPart& P, int64_t s, int32_t g, uint32_t nbound = 0) {
+                                                    RP& P, int64_t s, int32_t g, uint32_t nbound = 0) {
   const int lane = lane_id();
   WAVE_SYNC();
   uint32_t c = 0;
@@ -1722,7 +1799,7 @@ __device__ __forceinline__ bool fast_series_end(const GridParams& p, const FastL
   return true;
 }
 
-template <int F, int QW, int VL, int D, bool KR>
+template <int F, int QW, int VL, int D, int KR>
 __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __restrict__ rows,
                                               const int64_t* __restrict__ srp, const int64_t* __restrict__ tbeg,
                                               const int64_t* __restrict__ tend) {
@@ -1743,8 +1820,8 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
     L.cnt[k] = 0;
     L.w.pres[k] = 0;
   }
-  RegPart RP;
-  regpart_init(p.ga, RP);
+  std::conditional_t<KR == 2, MultiReg, RegPart> RP;   // KR 2: the fused multi-aggregator pass
+  rp_init(p.ga, RP);
   FWalk w;
   w.r0 = srp[tbeg[tile]];
   w.r = 0;
@@ -1832,12 +1909,7 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
   uint32_t* gn_ = p.part.n + tile * K;
   uint32_t* gf_ = p.part.f + tile * K;
   if (KR) {
-    if (lane < K) {
-      ga_[lane] = RP.pa;
-      gb_[lane] = RP.pb;
-      gn_[lane] = RP.pn;
-      gf_[lane] = RP.pf;
-    }
+    rp_store(p, tile, K, RP);
     return;
   }
   for (int k = lane; k < K; k += 64) {
@@ -1883,9 +1955,11 @@ __device__ __forceinline__ uint64_t rl64(uint64_t x, int l) {
 // 6 -> 4.5 ms, 8 -> 9.4 ms.  Round 2: the 4- and 8-byte classes grew past 5 waves' budget and
 // spilled (48-280 B/lane of scratch): they compile for 4, the vle class (93 VGPRs) stays at 5.
 #define SHORT_OCC(VL) ((VL) == 0 ? 5 : 4)
+// The fused multi-aggregator variant (KR 2, tsdbhip_run_multi) holds 13 more registers of
+// SpanGroup state: it compiles for 4 (vle at 5 spilled 20 B/lane).
 #endif
-template <int F, int QW, int VL, int D, bool KR>
-__global__ __launch_bounds__(256, SHORT_OCC(VL)) void k_short(GridParams p, const RowDesc* __restrict__ rows,
+template <int F, int QW, int VL, int D, int KR>
+__global__ __launch_bounds__(256, (KR) == 2 ? 4 : SHORT_OCC(VL)) void k_short(GridParams p, const RowDesc* __restrict__ rows,
                                                const int64_t* __restrict__ srp, const int64_t* __restrict__ tbeg,
                                                const int64_t* __restrict__ tend) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1936,8 +2010,8 @@ __global__ __launch_bounds__(256, SHORT_OCC(VL)) void k_short(GridParams p, cons
     L.cnt[k] = 0;
     L.w.pres[k] = 0;
   }
-  RegPart RP;
-  regpart_init(p.ga, RP);
+  std::conditional_t<KR == 2, MultiReg, RegPart> RP;   // KR 2: the fused multi-aggregator pass
+  rp_init(p.ga, RP);
   if (ns > 0 && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
   WAVE_SYNC();
   // The ring issues unconditionally (series index clamped to the last one) so that the
@@ -2002,12 +2076,7 @@ __global__ __launch_bounds__(256, SHORT_OCC(VL)) void k_short(GridParams p, cons
   uint32_t* gn_ = p.part.n + tile * K;
   uint32_t* gf_ = p.part.f + tile * K;
   if (KR) {
-    if (lane < K) {
-      ga_[lane] = RP.pa;
-      gb_[lane] = RP.pb;
-      gn_[lane] = RP.pn;
-      gf_[lane] = RP.pf;
-    }
+    rp_store(p, tile, K, RP);
     return;
   }
   for (int k = lane; k < K; k += 64) {

@@ -31,6 +31,7 @@ EXPORTS = [
     "tsdbhip_debug_rows", "tsdbhip_shard_bounds", "tsdbhip_load_shard", "tsdbhip_synth_shard",
     "tsdbhip_load_rollup", "tsdbhip_load_cells", "tsdbhip_load_histograms", "tsdbhip_hist_run",
     "tsdbhip_hist_run_range", "tsdbhip_hist_result_free", "tsdbhip_expr_map", "tsdbhip_expr_zip", "tsdbhip_expr_topn",
+    "tsdbhip_batch_range_sizes", "tsdbhip_batch_download_range",
 ]
 
 SHARD_SERIES, SHARD_GROUPS, SHARD_SPANS = 0, 1, 2   # tsdbhip.h TSDB_SHARD_*
@@ -72,6 +73,9 @@ def lib():
         L.tsdbhip_batch_sizes.argtypes = [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_uint64),
                                           C.POINTER(C.c_uint64)]
         L.tsdbhip_batch_download.argtypes = [vp] + [C.c_void_p] * 7
+        L.tsdbhip_batch_range_sizes.argtypes = [vp, C.c_int64, C.c_int64, C.POINTER(C.c_int64),
+                                                C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.tsdbhip_batch_download_range.argtypes = [vp, C.c_int64, C.c_int64] + [C.c_void_p] * 7
         L.tsdbhip_run.argtypes = [vp, C.POINTER(abi.Query), C.POINTER(C.POINTER(abi.Result))]
         L.tsdbhip_result_free.argtypes = [C.POINTER(abi.Result)]
         L.tsdbhip_last_timing.argtypes = [vp, C.POINTER(abi.Timing)]
@@ -273,6 +277,35 @@ class Engine:
         _check(lib().tsdbhip_batch_download(self.ctx, srp.ctypes.data, base.ctypes.data, qo.ctypes.data,
                                             vo.ctypes.data, q.ctypes.data, v.ctypes.data, g.ctypes.data))
         return abi.HostBatch(srp, base[:nr.value], qo, vo, q[:qb.value], v[:vb.value], g[:ns.value])
+
+    def n_series(self) -> int:
+        ns, nr, qb, vb = C.c_int64(), C.c_int64(), C.c_uint64(), C.c_uint64()
+        _check(lib().tsdbhip_batch_sizes(self.ctx, C.byref(ns), C.byref(nr), C.byref(qb), C.byref(vb)))
+        return ns.value
+
+    def resident_groups(self) -> np.ndarray:
+        """Group id of every resident series position (the resident order is group-sorted)."""
+        n = self.n_series()
+        g = np.zeros(max(1, n), np.int32)
+        _check(lib().tsdbhip_batch_download_range(self.ctx, 0, n, None, None, None, None, None, None,
+                                                  g.ctypes.data))
+        return g[:n]
+
+    def download_range(self, s0: int, s1: int) -> abi.HostBatch:
+        """Resident series positions [s0, s1) as a host batch (group ids kept)."""
+        nr, qb, vb = C.c_int64(), C.c_uint64(), C.c_uint64()
+        _check(lib().tsdbhip_batch_range_sizes(self.ctx, s0, s1, C.byref(nr), C.byref(qb), C.byref(vb)))
+        srp = np.zeros(s1 - s0 + 1, np.int64)
+        base = np.zeros(max(1, nr.value), np.uint32)
+        qo = np.zeros(nr.value + 1, np.uint64)
+        vo = np.zeros(nr.value + 1, np.uint64)
+        q = np.zeros(max(1, qb.value), np.uint8)
+        v = np.zeros(max(1, vb.value), np.uint8)
+        g = np.zeros(max(1, s1 - s0), np.int32)
+        _check(lib().tsdbhip_batch_download_range(self.ctx, s0, s1, srp.ctypes.data, base.ctypes.data,
+                                                  qo.ctypes.data, vo.ctypes.data, q.ctypes.data, v.ctypes.data,
+                                                  g.ctypes.data))
+        return abi.HostBatch(srp, base[:nr.value], qo, vo, q[:qb.value], v[:vb.value], g[:s1 - s0])
 
     def run(self, q: abi.Query):
         """tsdbhip_run -> [(group_id, ts, bits, is_int)]; the arrays are views into the

@@ -31,7 +31,7 @@ def test_library_exports_every_header_symbol():
 
 
 def test_abi_version():
-    assert engine.lib().tsdbhip_abi_version() == 7
+    assert engine.lib().tsdbhip_abi_version() == 8
 
 
 @pytest.mark.parametrize("name", abi.AGGREGATOR_NAMES)
