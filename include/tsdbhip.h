@@ -518,11 +518,16 @@ void tsdbhip_hist_result_free(tsdbhip_hist_result* r);
  *   (TimeSyncedIterator's NumericFillPolicy, ZERO by default), an absent variable reads 0; a
  *   present series that ends before another raises RuntimeException ("No more elements",
  *   TimeSyncedIterator.java:152-160).  The expression is a postfix program over doubles (JEXL 2.1.1
- *   arithmetic on Doubles: + - * / % and negation; / and % by zero raise ArithmeticException,
- *   reported as TSDB_E_RUNTIME). */
+ *   arithmetic on Doubles: + - * / % and negation, comparisons; a division or modulo by zero yields
+ *   0.0, the lenient JEXL interpreter's answer -- TestExpressionIterator.aDivideByZeroWithTwoSeries). */
 enum { TSDB_EXPR_SCALE = 0, TSDB_EXPR_ABSOLUTE, TSDB_EXPR_SHIFT, TSDB_EXPR_MOVING_AVG };
 enum { TSDB_XOP_VAR = 0, TSDB_XOP_CONST, TSDB_XOP_ADD, TSDB_XOP_SUB, TSDB_XOP_MUL, TSDB_XOP_DIV, TSDB_XOP_MOD,
-       TSDB_XOP_NEG };
+       TSDB_XOP_NEG,
+       /* comparisons (JexlArithmetic.lessThan & co. on doubles): 1.0 / 0.0, as ExpressionIterator maps a
+          Boolean result; NOT: negate(Boolean); IDIV / IMOD: the integer path of divide / mod (operands
+          that are Integers or Booleans: truncating division, BigInteger.mod) */
+       TSDB_XOP_LT, TSDB_XOP_GT, TSDB_XOP_LE, TSDB_XOP_GE, TSDB_XOP_EQ, TSDB_XOP_NE, TSDB_XOP_NOT, TSDB_XOP_IDIV,
+       TSDB_XOP_IMOD };
 typedef struct {
   int64_t n_series;
   const int64_t* ptr;          /* [n_series + 1] */
@@ -536,6 +541,23 @@ int tsdbhip_expr_map(tsdbhip_ctx* ctx, int fn, double fparam, int64_t iparam, in
 int tsdbhip_expr_zip(tsdbhip_ctx* ctx, const int32_t* program, int n_ops, const double* consts, int n_vars,
                      int64_t n_sets, const int32_t* set_series, const double* var_fill, const tsdbhip_series_set* in,
                      tsdbhip_result** out);
+
+/* tsdbhip_expr_sync: ExpressionIterator.next(timestamp) as /api/query/exp serializes it
+ * (src/tsd/QueryExecutor.java:668-708): the join iterator (UnionIterator / IntersectionIterator
+ * .next(), UnionIterator.java:409-419, IntersectionIterator.java:215-223) steps every sub-query's
+ * TimeSyncedIterator to the smallest next timestamp of its series (TimeSyncedIterator.java:125-158);
+ * a series without a point at that step reads its variable's fill (var_fill[v], the sub-query's
+ * NumericFillPolicy), as does a NaN value (ExpressionIterator.java:332-345); a variable without a
+ * series in a joined set (UNION's fill_dp) reads absent_value (the union's fill, 0).  The steps are the
+ * distinct timestamps of the series marked active (NULL: every series; IntersectionIterator nulls the
+ * series it kicks out, :306-349), those in [start_ms, end_ms] are emitted: one output group per
+ * joined set, one double per step.  The join itself (flattenTags keys, ByteMap order) is host logic
+ * (opentsdb_amd/expression.py).  Active series must be in strictly increasing time order (else
+ * TSDB_E_NOT_IMPLEMENTED: the reference's step walk over repeated timestamps is not restated). */
+int tsdbhip_expr_sync(tsdbhip_ctx* ctx, const int32_t* program, int n_ops, const double* consts, int n_vars,
+                      int64_t n_sets, const int32_t* set_series, const double* var_fill, double absent_value,
+                      const uint8_t* active, int64_t start_ms, int64_t end_ms, const tsdbhip_series_set* in,
+                      tsdbhip_result** out);
 
 /* highestMax / highestCurrent (HighestMax.java:37-150, HighestCurrent.java:37-151): the series
  * of `in` (every sub-query's group-bys, flattened in order; each sorted by time) run through one

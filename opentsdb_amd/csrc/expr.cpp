@@ -1,5 +1,5 @@
 // expr.cpp -- host side of the expression functions over query results:
-// tsdbhip_expr_map, tsdbhip_expr_zip.  Kernels in k_expr.hip; the function names, parameter
+// tsdbhip_expr_map, tsdbhip_expr_zip, tsdbhip_expr_sync, tsdbhip_expr_topn.  Kernels in k_expr.hip; the function names, parameter
 // parsing and the union join by tags live in the host mirror (opentsdb_amd/expression.py).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -44,6 +44,28 @@ struct Scratch {
     for (void* b : bufs) (void)hipFree(b);
   }
 };
+
+// the postfix program: stack depth, operands, indices, opcodes
+int check_program(const int32_t* program, int n_ops, int n_vars, const double* consts, int* n_consts_out) {
+  int depth = 0, maxd = 0, n_consts = 0;
+  for (int o = 0; o < n_ops; o++) {
+    const int op = program[2 * o], arg = program[2 * o + 1];
+    if (op == TSDB_XOP_VAR) { if (arg < 0 || arg >= n_vars) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "bad variable"); depth++; }
+    else if (op == TSDB_XOP_CONST) { if (arg < 0) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "bad constant"); n_consts = std::max(n_consts, arg + 1); depth++; }
+    else if (op == TSDB_XOP_NEG || op == TSDB_XOP_NOT) { if (depth < 1) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "bad program"); }
+    else if ((op >= TSDB_XOP_ADD && op <= TSDB_XOP_MOD) || (op >= TSDB_XOP_LT && op <= TSDB_XOP_NE) ||
+             op == TSDB_XOP_IDIV || op == TSDB_XOP_IMOD) {
+      if (depth < 2) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "bad program");
+      depth--;
+    } else return set_error(TSDB_E_ILLEGAL_ARGUMENT, "bad opcode");
+    maxd = std::max(maxd, depth);
+  }
+  if (depth != 1) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "bad program");
+  if (maxd > EXPR_STACK) return set_error(TSDB_E_NOT_IMPLEMENTED, "expression deeper than the evaluation stack");
+  if (n_consts && !consts) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "missing constants");
+  *n_consts_out = n_consts;
+  return 0;
+}
 
 int check_set(const tsdbhip_series_set* in) {
   if (!in || in->n_series < 0 || !in->ptr || (in->ptr[in->n_series] > 0 && (!in->ts_ms || !in->value_bits || !in->is_int)))
@@ -160,20 +182,8 @@ extern "C" int tsdbhip_expr_zip(tsdbhip_ctx* c, const int32_t* program, int n_op
     return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   *out = nullptr;
   if (int rc = check_set(in)) return rc;
-  // validate the program: stack depth, operands, indices
-  int depth = 0, maxd = 0, n_consts = 0;
-  for (int o = 0; o < n_ops; o++) {
-    const int op = program[2 * o], arg = program[2 * o + 1];
-    if (op == TSDB_XOP_VAR) { if (arg < 0 || arg >= n_vars) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "bad variable"); depth++; }
-    else if (op == TSDB_XOP_CONST) { if (arg < 0) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "bad constant"); n_consts = std::max(n_consts, arg + 1); depth++; }
-    else if (op == TSDB_XOP_NEG) { if (depth < 1) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "bad program"); }
-    else if (op >= TSDB_XOP_ADD && op <= TSDB_XOP_MOD) { if (depth < 2) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "bad program"); depth--; }
-    else return set_error(TSDB_E_ILLEGAL_ARGUMENT, "bad opcode");
-    maxd = std::max(maxd, depth);
-  }
-  if (depth != 1) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "bad program");
-  if (maxd > EXPR_STACK) return set_error(TSDB_E_NOT_IMPLEMENTED, "expression deeper than the evaluation stack");
-  if (n_consts && !consts) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "missing constants");
+  int n_consts = 0;
+  if (int rc = check_program(program, n_ops, n_vars, consts, &n_consts)) return rc;
   const int64_t S = in->n_series, N = in->ptr[S];
   for (int64_t i = 0; i < n_sets * n_vars; i++)
     if (set_series[i] >= S) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "set series out of range");
@@ -236,9 +246,128 @@ extern "C" int tsdbhip_expr_zip(tsdbhip_ctx* c, const int32_t* program, int n_op
   XOK(hipStreamSynchronize(st));
   if (err) {
     tsdbhip_result_free(r);
-    return set_error(err, "expression evaluation: a series ended before another (No more elements) or a division by zero");
+    return set_error(err, "expression evaluation: a series ended before another (No more elements)");
   }
   for (int64_t j = 0; j <= n_sets; j++) const_cast<int64_t*>(r->group_ptr)[j] = off[j];
+  for (int64_t j = 0; j < n_sets; j++) const_cast<int32_t*>(r->group_id)[j] = (int32_t)j;
+  *out = r;
+  return 0;
+}
+
+extern "C" int tsdbhip_expr_sync(tsdbhip_ctx* c, const int32_t* program, int n_ops, const double* consts, int n_vars,
+                                 int64_t n_sets, const int32_t* set_series, const double* var_fill, double absent_value,
+                                 const uint8_t* active, int64_t start_ms, int64_t end_ms, const tsdbhip_series_set* in,
+                                 tsdbhip_result** out) {
+  if (!c || !out || !program || n_ops <= 0 || n_vars <= 0 || n_sets < 0 || (n_sets && !set_series) || !var_fill)
+    return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  *out = nullptr;
+  if (int rc = check_set(in)) return rc;
+  int n_consts = 0;
+  if (int rc = check_program(program, n_ops, n_vars, consts, &n_consts)) return rc;
+  const int64_t S = in->n_series, N = in->ptr[S];
+  for (int64_t i = 0; i < n_sets * n_vars; i++)
+    if (set_series[i] >= S) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "set series out of range");
+  // per point: does its series drive the steps; the active series must be in time order
+  std::vector<uint8_t> pact(N > 0 ? N : 1, 0);
+  for (int64_t s = 0; s < S; s++) {
+    const int64_t a = in->ptr[s], b = in->ptr[s + 1];
+    if (b < a) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "malformed series set");
+    const uint8_t act = active ? active[s] : 1;
+    for (int64_t q = a; q < b; q++) {
+      pact[q] = act;
+      if (q > a && in->ts_ms[q] <= in->ts_ms[q - 1])
+        return set_error(TSDB_E_NOT_IMPLEMENTED, "time-synchronised expression over a series out of time order");
+    }
+  }
+  std::lock_guard<std::mutex> lk(ctx_mutex(c));
+  if (hipSetDevice(ctx_device(c)) != hipSuccess) return set_error(TSDB_E_HIP, "hipSetDevice");
+  hipStream_t st = ctx_stream(c);
+  Scratch sc;
+  auto release = [&]() {};
+  void *d_prog, *d_consts, *d_sets, *d_fill, *d_ptr, *d_ts, *d_bits, *d_int, *d_act, *d_keys, *d_sorted, *d_uni, *d_nu;
+  XOK(sc.alloc(&d_prog, n_ops * 8));
+  XOK(sc.alloc(&d_consts, n_consts * 8));
+  XOK(sc.alloc(&d_sets, n_sets * n_vars * 4));
+  XOK(sc.alloc(&d_fill, n_vars * 8));
+  XOK(sc.alloc(&d_ptr, (S + 1) * 8));
+  XOK(sc.alloc(&d_ts, N * 8));
+  XOK(sc.alloc(&d_bits, N * 8));
+  XOK(sc.alloc(&d_int, N));
+  XOK(sc.alloc(&d_act, N));
+  XOK(sc.alloc(&d_keys, N * 8));
+  XOK(sc.alloc(&d_sorted, N * 8));
+  XOK(sc.alloc(&d_uni, N * 8));
+  XOK(sc.alloc(&d_nu, 8));
+  XOK(hipMemcpyAsync(d_prog, program, n_ops * 8, hipMemcpyHostToDevice, st));
+  if (n_consts) XOK(hipMemcpyAsync(d_consts, consts, n_consts * 8, hipMemcpyHostToDevice, st));
+  if (n_sets) XOK(hipMemcpyAsync(d_sets, set_series, n_sets * n_vars * 4, hipMemcpyHostToDevice, st));
+  XOK(hipMemcpyAsync(d_fill, var_fill, n_vars * 8, hipMemcpyHostToDevice, st));
+  XOK(hipMemcpyAsync(d_ptr, in->ptr, (S + 1) * 8, hipMemcpyHostToDevice, st));
+  if (N) {
+    XOK(hipMemcpyAsync(d_ts, in->ts_ms, N * 8, hipMemcpyHostToDevice, st));
+    XOK(hipMemcpyAsync(d_bits, in->value_bits, N * 8, hipMemcpyHostToDevice, st));
+    XOK(hipMemcpyAsync(d_int, in->is_int, N, hipMemcpyHostToDevice, st));
+    XOK(hipMemcpyAsync(d_act, pact.data(), N, hipMemcpyHostToDevice, st));
+  }
+  ExprSyncParams p{};
+  p.prog = (const int32_t*)d_prog;
+  p.n_ops = n_ops;
+  p.consts = (const double*)d_consts;
+  p.n_vars = n_vars;
+  p.n_sets = n_sets;
+  p.set_series = (const int32_t*)d_sets;
+  p.var_fill = (const double*)d_fill;
+  p.absent = absent_value;
+  p.ptr = (const int64_t*)d_ptr;
+  p.ts = (const int64_t*)d_ts;
+  p.bits = (const uint64_t*)d_bits;
+  p.is_int = (const uint8_t*)d_int;
+  p.n_pts = N;
+  p.pt_active = (const uint8_t*)d_act;
+  p.start = start_ms;
+  p.end = end_ms;
+  // the steps: the join iterator's nextTimestamp sequence = the distinct timestamps of the
+  // active series (each in time order), sorted and made unique on the device
+  int64_t U = 0;
+  if (N) {
+    XOK(expr_sync_keys(p, (int64_t*)d_keys, st));
+    size_t tmp1 = 0, tmp2 = 0;
+    XOK(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp1, (const int64_t*)d_keys, (int64_t*)d_sorted, (int)N, 0, 64, st));
+    XOK(hipcub::DeviceSelect::Unique(nullptr, tmp2, (const int64_t*)d_sorted, (int64_t*)d_uni, (int64_t*)d_nu, (int)N, st));
+    void* d_tmp;
+    size_t t1 = std::max(tmp1, tmp2), t2 = t1;
+    XOK(sc.alloc(&d_tmp, t1));
+    XOK(hipcub::DeviceRadixSort::SortKeys(d_tmp, t1, (const int64_t*)d_keys, (int64_t*)d_sorted, (int)N, 0, 64, st));
+    XOK(hipcub::DeviceSelect::Unique(d_tmp, t2, (const int64_t*)d_sorted, (int64_t*)d_uni, (int64_t*)d_nu, (int)N, st));
+    int64_t nu = 0, last = 0;
+    XOK(hipMemcpyAsync(&nu, d_nu, 8, hipMemcpyDeviceToHost, st));
+    XOK(hipStreamSynchronize(st));
+    if (nu > 0) {
+      XOK(hipMemcpyAsync(&last, (int64_t*)d_uni + nu - 1, 8, hipMemcpyDeviceToHost, st));
+      XOK(hipStreamSynchronize(st));
+    }
+    U = nu - (nu > 0 && last == INT64_MAX ? 1 : 0);
+  }
+  const int64_t n_out = n_sets * U;
+  void *o_ts, *o_bits, *o_int;
+  XOK(sc.alloc(&o_ts, n_out * 8));
+  XOK(sc.alloc(&o_bits, n_out * 8));
+  XOK(sc.alloc(&o_int, n_out));
+  p.uts = (const int64_t*)d_uni;
+  p.U = U;
+  p.out_ts = (int64_t*)o_ts;
+  p.out_bits = (uint64_t*)o_bits;
+  p.out_int = (uint8_t*)o_int;
+  XOK(expr_sync(p, st));
+  tsdbhip_result* r = new_result(n_sets, n_out);
+  if (!r) return set_error(TSDB_E_NOMEM, "result");
+  if (n_out) {
+    XOK(hipMemcpyAsync(const_cast<int64_t*>(r->ts_ms), o_ts, n_out * 8, hipMemcpyDeviceToHost, st));
+    XOK(hipMemcpyAsync(const_cast<uint64_t*>(r->value_bits), o_bits, n_out * 8, hipMemcpyDeviceToHost, st));
+    XOK(hipMemcpyAsync(const_cast<uint8_t*>(r->is_int), o_int, n_out, hipMemcpyDeviceToHost, st));
+  }
+  XOK(hipStreamSynchronize(st));
+  for (int64_t j = 0; j <= n_sets; j++) const_cast<int64_t*>(r->group_ptr)[j] = j * U;
   for (int64_t j = 0; j < n_sets; j++) const_cast<int32_t*>(r->group_id)[j] = (int32_t)j;
   *out = r;
   return 0;

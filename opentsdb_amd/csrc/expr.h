@@ -45,6 +45,33 @@ struct ExprZipParams {
   int32_t* err;
 };
 
+// time-synchronised evaluation (tsdbhip_expr_sync): steps = distinct timestamps of the active
+// series' points in [start, end]
+struct ExprSyncParams {
+  const int32_t* prog;
+  int32_t n_ops;
+  const double* consts;
+  int32_t n_vars;
+  int64_t n_sets;
+  const int32_t* set_series; // [n_sets * n_vars]
+  const double* var_fill;    // [n_vars]
+  double absent;             // a variable without a series in the set (UnionIterator fill_dp)
+  const int64_t* ptr;        // input series
+  const int64_t* ts;
+  const uint64_t* bits;
+  const uint8_t* is_int;
+  int64_t n_pts;
+  const uint8_t* pt_active;  // [n_pts] the point's series drives the steps
+  int64_t start, end;
+  const int64_t* uts;        // [U] step timestamps
+  int64_t U;
+  int64_t* out_ts;           // [n_sets * U]
+  uint64_t* out_bits;
+  uint8_t* out_int;
+};
+hipError_t expr_sync_keys(const ExprSyncParams& p, int64_t* keys, hipStream_t s);
+hipError_t expr_sync(const ExprSyncParams& p, hipStream_t s);
+
 // highestMax / highestCurrent: an AggregationIterator (LERP) over every result series, one
 // wave per union point; operands kept by position among the spans that have a value
 struct ExprTopParams {

@@ -6,7 +6,9 @@
 //                -- the window walks back from the point, newest first, as the aggregator's
 //                LinkedList does, so the sum is the reference's in its order
 //   k_expr_zip   thread per (joined set, position): ExpressionIterator.next(index)
-//                (ExpressionIterator.java:282-318) through EDPtoDPS, the program over doubles
+//                (ExpressionIterator.java:452-485) through EDPtoDPS, the program over doubles
+//   k_expr_sync  thread per (joined set, step): ExpressionIterator.next(timestamp) (:323-358) over
+//                the join iterator's time-synchronised steps
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -108,6 +110,53 @@ __global__ void k_expr_mavg(ExprMapParams p) {
   p.out_int[i] = 0;
 }
 
+// The postfix program of one expression evaluation (JEXL 2.1.1 arithmetic, Interpreter.visit of
+// the arithmetic and comparison nodes): the operands are Doubles (variables) or constants the host
+// folded; a division or modulo error yields Double 0.0 (the lenient interpreter), comparisons give
+// Boolean -> 1.0 / 0.0 (ExpressionIterator.java:347-351).  var(v) loads variable v.
+template <class Var>
+__device__ __forceinline__ double expr_eval(const int32_t* prog, int n_ops, const double* consts, Var&& var) {
+  double stack[EXPR_STACK];
+  int sp = 0;
+  for (int o = 0; o < n_ops; o++) {
+    const int op = prog[2 * o], arg = prog[2 * o + 1];
+    if (op == TSDB_XOP_VAR) {
+      stack[sp++] = var(arg);
+    } else if (op == TSDB_XOP_CONST) {
+      stack[sp++] = consts[arg];
+    } else if (op == TSDB_XOP_NEG) {
+      stack[sp - 1] = -stack[sp - 1];
+    } else if (op == TSDB_XOP_NOT) {
+      stack[sp - 1] = stack[sp - 1] != 0.0 ? 0.0 : 1.0;
+    } else {
+      const double r = stack[--sp], l = stack[--sp];
+      double x;
+      switch (op) {
+        case TSDB_XOP_ADD: x = l + r; break;
+        case TSDB_XOP_SUB: x = l - r; break;
+        case TSDB_XOP_MUL: x = l * r; break;
+        case TSDB_XOP_DIV: x = r == 0.0 ? 0.0 : l / r; break;          // JexlArithmetic.divide
+        case TSDB_XOP_MOD: x = r == 0.0 ? 0.0 : fmod(l, r); break;     // JexlArithmetic.mod (Java %)
+        case TSDB_XOP_IDIV: x = r == 0.0 ? 0.0 : trunc(l / r); break;  // BigInteger.divide
+        case TSDB_XOP_IMOD: {                                          // BigInteger.mod: r > 0, result >= 0
+          if (r <= 0.0) { x = 0.0; break; }
+          x = fmod(l, r);
+          if (x < 0.0) x += r;
+          break;
+        }
+        case TSDB_XOP_LT: x = l < r ? 1.0 : 0.0; break;
+        case TSDB_XOP_GT: x = l > r ? 1.0 : 0.0; break;
+        case TSDB_XOP_LE: x = l <= r ? 1.0 : 0.0; break;
+        case TSDB_XOP_GE: x = l >= r ? 1.0 : 0.0; break;
+        case TSDB_XOP_EQ: x = l == r ? 1.0 : 0.0; break;
+        default: x = l != r ? 1.0 : 0.0; break;
+      }
+      stack[sp++] = x;
+    }
+  }
+  return stack[0];
+}
+
 __global__ void k_expr_zip(ExprZipParams p) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= p.n_out) return;
@@ -118,8 +167,6 @@ __global__ void k_expr_zip(ExprZipParams p) {
     if (p.set_off[m] <= t) a = m; else b = m;
   }
   const int64_t j = a, k = t - p.set_off[j];
-  double stack[EXPR_STACK];
-  int sp = 0;
   int64_t ts = INT64_MAX;
   for (int v = 0; v < p.n_vars; v++) {   // timestamps of the present series at position k
     const int32_t s = p.set_series[j * p.n_vars + v];
@@ -128,42 +175,53 @@ __global__ void k_expr_zip(ExprZipParams p) {
     if (q >= p.ptr[s + 1]) { set_err(p.err, TSDB_E_RUNTIME); return; }   // "No more elements"
     ts = min(ts, p.ts[q]);
   }
-  for (int o = 0; o < p.n_ops; o++) {
-    const int op = p.prog[2 * o], arg = p.prog[2 * o + 1];
-    if (op == TSDB_XOP_VAR) {
-      const int32_t s = p.set_series[j * p.n_vars + arg];
-      double v = 0.0;   // UnionIterator's fill_dp: a default MutableDataPoint reads 0
-      if (s >= 0) {
-        const int64_t q = p.ptr[s] + k;
-        v = pt_double(p.bits[q], p.is_int[q]);
-        if (v != v) v = p.var_fill[arg];
-      }
-      stack[sp++] = v;
-    } else if (op == TSDB_XOP_CONST) {
-      stack[sp++] = p.consts[arg];
-    } else if (op == TSDB_XOP_NEG) {
-      stack[sp - 1] = -stack[sp - 1];
-    } else {
-      const double r = stack[--sp], l = stack[--sp];
-      double x;
-      switch (op) {
-        case TSDB_XOP_ADD: x = l + r; break;
-        case TSDB_XOP_SUB: x = l - r; break;
-        case TSDB_XOP_MUL: x = l * r; break;
-        case TSDB_XOP_DIV:
-          if (r == 0.0) { set_err(p.err, TSDB_E_RUNTIME); return; }   // JexlArithmetic.divide
-          x = l / r;
-          break;
-        default:
-          if (r == 0.0) { set_err(p.err, TSDB_E_RUNTIME); return; }   // JexlArithmetic.mod
-          x = fmod(l, r);
-          break;
-      }
-      stack[sp++] = x;
+  const double r = expr_eval(p.prog, p.n_ops, p.consts, [&](int v) {
+    const int32_t s = p.set_series[j * p.n_vars + v];
+    double x = 0.0;   // UnionIterator's fill_dp: a default MutableDataPoint reads 0
+    if (s >= 0) {
+      const int64_t q = p.ptr[s] + k;
+      x = pt_double(p.bits[q], p.is_int[q]);
+      if (x != x) x = p.var_fill[v];
     }
-  }
+    return x;
+  });
   p.out_ts[t] = ts;
-  p.out_bits[t] = (uint64_t)__double_as_longlong(stack[0]);
+  p.out_bits[t] = (uint64_t)__double_as_longlong(r);
+  p.out_int[t] = 0;
+}
+
+// ---- time-synchronised evaluation (tsdbhip_expr_sync) -----------------------------------
+// keys of the step timestamps: the active series' points inside [start, end]
+__global__ void k_expr_sync_keys(ExprSyncParams p, int64_t* keys) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n_pts) return;
+  const int64_t t = p.ts[i];
+  keys[i] = (p.pt_active[i] && t >= p.start && t <= p.end) ? t : INT64_MAX;
+}
+
+// thread per (joined set, step): every variable's value at the step's timestamp -- its series'
+// point there (binary search: the series are in time order), else the variable's fill; then the
+// program (ExpressionIterator.next(long), :323-358)
+__global__ void k_expr_sync(ExprSyncParams p) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= p.n_sets * p.U) return;
+  const int64_t j = t / p.U, u = t - j * p.U;
+  const int64_t x = p.uts[u];
+  const double r = expr_eval(p.prog, p.n_ops, p.consts, [&](int v) {
+    const int32_t s = p.set_series[j * p.n_vars + v];
+    double y = p.absent;
+    if (s >= 0) {
+      int64_t lo = p.ptr[s], hi = p.ptr[s + 1];
+      while (lo < hi) {
+        const int64_t m = (lo + hi) >> 1;
+        if (p.ts[m] < x) lo = m + 1; else hi = m;
+      }
+      y = (lo < p.ptr[s + 1] && p.ts[lo] == x) ? pt_double(p.bits[lo], p.is_int[lo]) : p.var_fill[v];
+    }
+    return y != y ? p.var_fill[v] : y;
+  });
+  p.out_ts[t] = x;
+  p.out_bits[t] = (uint64_t)__double_as_longlong(r);
   p.out_int[t] = 0;
 }
 
@@ -312,6 +370,17 @@ hipError_t expr_map(const ExprMapParams& p, hipStream_t s) {
   if (p.n <= 0) return hipSuccess;
   if (p.fn == TSDB_EXPR_MOVING_AVG) hipLaunchKernelGGL(k_expr_mavg, dim3((unsigned)((p.n + 255) / 256)), dim3(256), 0, s, p);
   else hipLaunchKernelGGL(k_expr_map, dim3((unsigned)((p.n + 255) / 256)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+hipError_t expr_sync_keys(const ExprSyncParams& p, int64_t* keys, hipStream_t s) {
+  if (p.n_pts <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_expr_sync_keys, dim3((unsigned)((p.n_pts + 255) / 256)), dim3(256), 0, s, p, keys);
+  return hipGetLastError();
+}
+hipError_t expr_sync(const ExprSyncParams& p, hipStream_t s) {
+  const int64_t n = p.n_sets * p.U;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_expr_sync, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 hipError_t expr_zip(const ExprZipParams& p, hipStream_t s) {

@@ -12,8 +12,9 @@ point in the reference's order (pure-Python loops: small cases only):
                              EDPtoDPS (EDPtoDPS.java:148-160), UnionIterator.computeUnion
                              (UnionIterator.java:140-200), TimeSyncedIterator.next(int)
                              (TimeSyncedIterator.java:152-160) and JEXL 2.1.1's JexlArithmetic on
-                             Doubles (third_party/jexl/include.mk:1, not vendored: +, -, *, and /, %
-                             throwing ArithmeticException for a zero divisor)
+                             Doubles (third_party/jexl/include.mk:1, not vendored: +, -, *, /, %; a
+                             zero divisor gives 0.0 -- the lenient interpreter, pinned by
+                             TestExpressionIterator.aDivideByZeroWithTwoSeries)
   HighestMax / HighestCurrent src/query/expression/HighestMax.java:37-150, :182-292 and
                              HighestCurrent.java:37-151, :172-283: an AggregationIterator
                              (src/core/AggregationIterator.java:395-797, LERP, no rate) over every
@@ -156,7 +157,7 @@ def _jexl(op, l, r):
     if op == "*":
         return l * r
     if r == 0.0:
-        raise OracleExprError("RuntimeException", "ArithmeticException /")
+        return 0.0   # the lenient JEXL interpreter: a divide / modulo error is Double 0.0
     if op == "/":
         return l / r
     return math.fmod(l, r)

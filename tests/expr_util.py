@@ -49,3 +49,48 @@ def check(got, case):
             else:
                 assert abs(float(gv) - float(ev)) <= case["tol"] or (math.isnan(gv) and math.isnan(ev)), \
                     (case["name"], gv, ev)
+
+
+# ---- /api/query/exp join fixtures (tests/golden/expression_iter.json) --------------------------
+def uid(letter: str) -> bytes:
+    """test/core/BaseTsdbTest.java:102-110: 'A'..'Z' -> 00 00 0A.."""
+    return bytes([0, 0, 10 + ord(letter) - ord("A")])
+
+
+def num(v):
+    return math.nan if v == "NaN" else float(v)
+
+
+def result_sets(case, fill=0.0):
+    """The fixture's sub-query results as product ResultSets (opentsdb_amd.expression)."""
+    from opentsdb_amd import expression as X
+    out = []
+    for sub in case.get("results") or []:
+        series = [X.Series.of([tuple(p) for p in s["points"]], tags={uid(k): uid(v) for k, v in s["tags"].items()},
+                              agg_tags=[uid(a) for a in s["agg"]]) for s in sub["series"]]
+        out.append(X.ResultSet(series, frozenset(uid(k) for k in sub["filter_tagks"]), fill))
+    return out
+
+
+def product_expression(case):
+    """The fixture's ExpressionIterator on the product host (nested expressions included, not
+    compiled); sub-queries remapped to the case's variables with fill ZERO unless set."""
+    from opentsdb_amd import expression as X
+    fills = {k: num(v) for k, v in (case.get("fills") or {}).items()}
+    rs = result_sets(case)
+    built = {}
+    for spec in case.get("nested", []):
+        e = X.ExpressionIterator(spec["id"], spec["expression"], spec["op"], case["use_qt"], case["inc_agg"])
+        for var, src in spec["vars"].items():
+            e.add_results(var, built[src] if isinstance(src, str) else rs[src])
+        built[spec["id"]] = e
+    exp = X.ExpressionIterator("ei", case["expression"], case["op"], case["use_qt"], case["inc_agg"])
+    if case.get("null_iterator"):
+        exp.add_results(case["null_iterator"], None)
+    for var, src in case["vars"].items():
+        if isinstance(src, str):
+            exp.add_results(var, built[src])
+        else:
+            r = rs[src]
+            exp.add_results(var, X.ResultSet(r.series, r.filter_tagks, fills.get(var, 0.0)))
+    return exp, built

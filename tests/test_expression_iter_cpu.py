@@ -5,6 +5,7 @@ from __future__ import annotations
 
 import math
 
+import numpy as np
 import pytest
 
 from oracle import expr_iter as X
@@ -194,3 +195,69 @@ def test_hashmap_order_simulation():
     assert X.hashmap_order(["b", "a"]) == ["a", "b"]
     assert X.hashmap_order(["1", "0"], 2) == ["0", "1"]
     assert X.hashmap_order(["e1", "a"]) == ["a", "e1"]   # "e1".hashCode() = 3180 -> bucket 12, "a" -> 1
+
+
+# ---- the product's host half: flattenTags and the joins (no GPU) -------------------------------
+from opentsdb_amd import expression as PX  # noqa: E402
+from tests import expr_util as EU  # noqa: E402
+
+FLATTEN = [c for c in CASES if c["kind"] == "flatten" and "error" not in c and c["tags"] is not None]
+
+
+@pytest.mark.parametrize("case", FLATTEN, ids=[c["name"] for c in FLATTEN])
+def test_product_flatten_tags(case):
+    tags = {bytes(k): bytes(v) for k, v in case["tags"]}
+    agg = [bytes(a) for a in (case["agg"] or [])]
+    qt = [bytes(q) for q in case["query_tags"]]
+    assert PX.flatten_tags(case["use_qt"], case["inc_agg"], tags, agg, qt) == bytes(case["expect"])
+
+
+JOINS = [c for c in CASES if c["kind"] in ("union", "intersection") and c.get("results") is not None
+         and "next_calls" not in c]
+
+
+@pytest.mark.parametrize("case", JOINS, ids=[c["name"] for c in JOINS])
+def test_product_join_plan(case):
+    """The product's join of the fixture's results (variables v0, v1 over sub-queries 0, 1):
+    the joined set count, or the exception, as the reference test expects."""
+    rs = EU.result_sets(case, EU.num(case["fill"]))
+    exp = PX.ExpressionIterator("it", " + ".join(f"v{i}" for i in range(len(rs))) or "v0",
+                                "UNION" if case["kind"] == "union" else "INTERSECTION", case["use_qt"], case["inc_agg"])
+    for i, r in enumerate(rs):
+        exp.add_results(f"v{i}", r)
+    if "error" in case:
+        with pytest.raises(PX.ExpressionError) as ei:
+            exp.plan()
+        assert ei.value.java == case["error"]
+        return
+    flat, members, keys, joined, active, jorder = exp.plan()
+    assert len(keys) == case["series_size"]
+
+
+EXPRS = [c for c in CASES if c["kind"] == "expr" and "error" in c]
+
+
+@pytest.mark.parametrize("case", EXPRS, ids=[c["name"] for c in EXPRS])
+def test_product_expression_errors(case):
+    """Constructor / compile exceptions of TestExpressionIterator on the product host."""
+    with pytest.raises(PX.ExpressionError) as ei:
+        if case.get("ctor_only"):
+            PX.ExpressionIterator("ei", case["expression"], case["op"], False, False)
+        else:
+            exp, built = EU.product_expression(case)
+            for e in built.values():
+                e.series = []
+            exp.plan()
+    assert ei.value.java == case["error"]
+
+
+def test_product_compiler_types():
+    """JEXL literal and path rules the compiler folds: integer division truncates, Float literals
+    are float32, a division by zero is 0.0, an Integer result is refused."""
+    prog, consts, names = PX.compile_expression("(7 / 2) * a + 0.1")
+    assert consts == [3.0, float(np.float32(0.1))]
+    assert PX.compile_expression("a / 0")[1] == [0.0]
+    assert PX.compile_expression("(1 / 0) * a")[1] == [0.0]
+    with pytest.raises(PX.ExpressionError) as ei:
+        PX.compile_expression("(a > b) + 1")
+    assert ei.value.java == "IllegalStateException"

