@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH/WRITE_SIZE child passes")
+    ap.add_argument("--no-config3", action="store_true", help="skip the config-3 (10M series) block in `extra`")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -134,6 +135,62 @@ def pmc_traffic(args, kernel_prefix: str):
                            "correction": "FETCH_SIZE x2 and KiB->B, as /opt/skills/guides/MI355X_MICROARCH.md's "
                                          "HBM / rocprofv3 section prescribes for gfx950 (FETCH_SIZE reports half "
                                          "the bytes of 16-B-per-lane streaming reads); WRITE_SIZE exact"}
+
+
+def config3_block(args, device: int):
+    """BASELINE config 3's one-GPU point, the north-star target (>= 50 % of HBM for 1m-avg + sum
+    over 10M series): 10M series x 1 h @10 s (even series vle int [0, 30000), odd float32), 1000
+    groups.  Times (a) sum:1m-avg and (b) the five aggregators avg/min/max/count/dev:1m-avg
+    through one tsdbhip_run_multi (one fused streaming pass + one group reduction per query),
+    with the same barrier-free wall clock per step as the headline, plus the streaming kernels'
+    hipEvent time for the roofline."""
+    from opentsdb_amd import abi
+    from opentsdb_amd.engine import Engine
+    eng = Engine(device)
+    try:
+        eng.synth(10_000_000, T0, 360, 10000, 2, 1000, 30000, 0x5EED)
+        eng.sync()
+
+        def q(agg):
+            return abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+
+        out = {"workload": "BASELINE config 3 (1 h window): 10M series x 360 dp @10 s, int/float32 alternating, "
+                           "1000 groups, 1m-avg"}
+        qs = q("sum")
+        steps = max(3, args.steps)
+        for _ in range(2):
+            eng.run(qs)
+        eng.sync()
+        t = time.perf_counter()
+        kms = []
+        for _ in range(steps):
+            eng.run(qs)
+            kms.append(eng.timing().fast_ms)
+        eng.sync()
+        sum_ms = (time.perf_counter() - t) * 1000 / steps
+        tm = eng.timing()
+        k_ms = sum(kms) / len(kms)
+        out["sum"] = {"ms_per_step": sum_ms, "value": tm.datapoints / (sum_ms / 1000), "unit": "datapoints/s",
+                      "kernel": "k_short (both row classes)", "kernel_ms": k_ms, "bytes_per_launch": tm.bytes,
+                      "hbm_frac": tm.bytes / (k_ms / 1000) / 1e9 / BYTES_PEAK_GBS,
+                      "hbm_frac_step": tm.bytes / (sum_ms / 1000) / 1e9 / BYTES_PEAK_GBS}
+        ql = [q(a) for a in ("avg", "min", "max", "count", "dev")]
+        for _ in range(2):
+            eng.run_multi(ql)
+        eng.sync()
+        t = time.perf_counter()
+        for _ in range(steps):
+            eng.run_multi(ql)
+        eng.sync()
+        multi_ms = (time.perf_counter() - t) * 1000 / steps
+        tm = eng.timing()
+        out["multi_avg_min_max_count_dev"] = {
+            "ms_per_step": multi_ms, "fused_queries": int(tm.fused_queries),
+            "value": 5 * tm.datapoints / (multi_ms / 1000), "unit": "datapoints/s (x5 queries)",
+            "fused_pass_ms": tm.decode_downsample_ms, "ratio_to_sum_step": multi_ms / sum_ms}
+        return out
+    finally:
+        eng.close()
 
 
 def workload_label(args) -> str:
@@ -250,6 +307,10 @@ def main():
     k_avg = sum(fast_ms if use_fast else kernel_ms) / args.steps
     kname = "k_fast" if use_fast else "k_grid"
     achieved = tm.bytes / (k_avg / 1000.0) / 1e9
+    extra = None
+    if world == 1 and not args.no_config3:
+        eng.close()   # free the headline store before config 3's 18 GB
+        extra = {"config3": config3_block(args, local_rank)}
     if rank == 0:
         cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(args, args.cpu_seconds)
         traffic, traffic_note = (None, "not collected (--no-pmc or N>1)")
@@ -299,6 +360,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "synth_s": t_gen,
+            "extra": extra,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

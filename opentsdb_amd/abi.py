@@ -7,6 +7,7 @@ test-only oracle binding (oracle/oracle.py), which consumes the same boundary ty
 from __future__ import annotations
 
 import ctypes as C
+from collections.abc import Sequence
 
 import numpy as np
 
@@ -389,10 +390,43 @@ def _view(ptr, n: int, dtype, owner):
     return np.frombuffer(buf, dtype)
 
 
+class Groups(Sequence):
+    """The groups of a tsdbhip_result as a sequence of (group_id, ts, bits, is_int) tuples over
+    the result arrays (numpy views; the library's memory stays owned by `owner` while any view
+    is alive).  The tuples are built when a group is accessed -- the arrays are already complete
+    on the host -- as a JVM caller wraps the arrays as DataPoints without copying."""
+
+    def __init__(self, gid, gp, ts, bits, isi):
+        self._gid, self._gp, self._ts, self._bits, self._isi = gid, gp, ts, bits, isi
+
+    def __len__(self):
+        return len(self._gid)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        n = len(self._gid)
+        if i < 0:
+            i += n
+        if not 0 <= i < n:
+            raise IndexError(i)
+        a, b = int(self._gp[i]), int(self._gp[i + 1])
+        return (int(self._gid[i]), self._ts[a:b], self._bits[a:b], self._isi[a:b])
+
+    def __add__(self, other):
+        return list(self) + list(other)
+
+    def __eq__(self, other):
+        return list(self) == list(other)
+
+    def __repr__(self):
+        return f"Groups({len(self)} groups, {int(self._gp[-1]) if len(self._gp) else 0} points)"
+
+
 def result_to_groups(res: Result, owner=None):
-    """A tsdbhip_result / ref_result as a list of (group_id, ts[int64], bits[uint64],
-    is_int[uint8]) numpy tuples.  Without `owner` the arrays are copies; with it they are
-    views into the result memory, which `owner` frees when the last view is gone."""
+    """A tsdbhip_result / ref_result as a sequence of (group_id, ts[int64], bits[uint64],
+    is_int[uint8]) numpy tuples.  Without `owner` a list of copies; with it a lazy :class:`Groups`
+    of views into the result memory, which `owner` frees when the last view is gone."""
     groups = []
     n = res.n_groups
     if n == 0:
@@ -412,6 +446,8 @@ def result_to_groups(res: Result, owner=None):
         ts = np.zeros(0, np.int64)
         bits = np.zeros(0, np.uint64)
         isi = np.zeros(0, np.uint8)
+    if owner is not None:
+        return Groups(gid, gp, ts, bits, isi)
     for g in range(n):
         a, b = int(gp[g]), int(gp[g + 1])
         groups.append((int(gid[g]), ts[a:b], bits[a:b], isi[a:b]))

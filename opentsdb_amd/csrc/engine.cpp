@@ -1890,6 +1890,7 @@ struct Plan {
   bool values_only = false;      // percentile downsampling pass without the group-by step
   bool emit_only = false;        // group-by step over bucket values already in pre_dense / pre_pres
   bool multi = false;            // fused multi-aggregator pass (run_multi_fused): partials to c->mp*, no reduce
+  bool multi_dev = false;        //   ... with the Welford state (a dev query among them)
 };
 
 bool is_sel_agg(int a) { return a == TSDB_AGG_MEDIAN || (a >= TSDB_AGG_P999 && a < TSDB_AGG_COUNT_ALL); }
@@ -2307,7 +2308,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     HIP_OK(c->m_nl.ensure(n * 4));
     HIP_OK(c->m_nz.ensure(n * 4));
     HIP_OK(c->m_f.ensure(n * 4));
-    gp.multi = 1;
+    gp.multi = MULTI_ON | (P.multi_dev ? MULTI_DEV : 0);
     gp.mp = MultiPartials{c->m_sum.as<double>(), c->m_mn.as<double>(), c->m_mx.as<double>(), c->m_mean.as<double>(),
                           c->m_m2.as<double>(), c->m_nl.as<uint32_t>(), c->m_nz.as<uint32_t>(), c->m_f.as<uint32_t>()};
   }
@@ -3515,6 +3516,7 @@ int run_multi_fused(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_resu
   }
   const int64_t G = c->n_groups, K = P.K;
   P.multi = true;
+  for (int i = 0; i < n; i++) P.multi_dev = P.multi_dev || qs[i].aggregator == TSDB_AGG_DEV;
   rc = run_device(c, &q0, P, G, false);
   if (rc) return rc;
   int32_t handed_back = 0;
@@ -3548,12 +3550,28 @@ int run_multi_fused(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_resu
     HIP_OK(launch_reduce(rp, c->stream));
   }
   HIP_OK(hipEventRecord(c->ev[2], c->stream));
+  // every query's dense rows in one copy each (collect() per query would sync n times)
+  std::vector<double> val(gk * n);
+  std::vector<uint8_t> flag(gk * n);
+  std::vector<uint32_t> act(std::max<int64_t>(1, G));
+  int32_t err = 0, redo_n = 0;
+  HIP_OK(hipMemcpyAsync(val.data(), c->out_val.p, gk * n * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipMemcpyAsync(flag.data(), c->out_flag.p, gk * n, hipMemcpyDeviceToHost, c->stream));
+  if (G) HIP_OK(hipMemcpyAsync(act.data(), c->gact.p, G * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipMemcpyAsync(&redo_n, c->redo_final, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
   c->fused_n = n;
-  for (int i = 0; i < n && !rc; i++)
-    rc = collect(c, &qs[i], plans[i], G, true, &outs[i], c->out_val.as<double>() + i * gk,
-                 c->out_flag.as<uint8_t>() + i * gk);
+  record_timing(c, P, redo_n);
   c->fused_n = 0;
-  return rc;
+  if (err) return fail(err, "error raised by the device path");
+  for (int i = 0; i < n; i++) {
+    const std::vector<double> vi(val.begin() + i * gk, val.begin() + (i + 1) * gk);
+    const std::vector<uint8_t> fi(flag.begin() + i * gk, flag.begin() + (i + 1) * gk);
+    rc = assemble(c, &qs[i], plans[i], G, vi, fi, act, &outs[i]);
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 }  // namespace

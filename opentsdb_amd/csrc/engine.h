@@ -50,9 +50,10 @@ struct Partials {
 
 enum : uint32_t { PF_UNION = 1u, PF_HAS = 2u };
 
+enum : int32_t { MULTI_ON = 1, MULTI_DEV = 2 };
 // Per-tile partial states of the fused multi-aggregator pass (GridParams.multi), [tile][K]:
 // sum / avg (sum, nl), min (mn), max (mx), dev (mean, m2, nl), count (nz); f = union flags.
-// Aggregator x reads them as Partials (k_reduce) -- see multi_partials_of in engine.cpp.
+// Aggregator x reads them as Partials in k_reduce (the mapping is in engine.cpp run_multi_fused).
 struct MultiPartials {
   double *sum, *mn, *mx, *mean, *m2;
   uint32_t *nl, *nz, *f;
@@ -150,7 +151,7 @@ struct GridParams {
   int64_t big_cap;
   // fused multi-aggregator pass (tsdbhip_run_multi): the register-partial kernels keep every
   // decomposable aggregator's state and write them to mp (K <= 64, no rate, LERP + count)
-  int32_t multi;
+  int32_t multi;          // MULTI_ON | MULTI_DEV (the Welford state is kept only for a dev query)
   MultiPartials mp;
   int32_t dbg;           // k_short profiling switches (TSDBHIP_DBG, results invalid): 1 skip series end,
                          // 2 skip chunk fold, 8 consume loads, 16 stop after the descriptors, 32 load row 0 only

@@ -1082,14 +1082,16 @@ __device__ __forceinline__ void emit_series_reg(const GridParams& p, int K, bool
     M.sum += cv;
     if (cv < M.mn) M.mn = cv;
     if (cv > M.mx) M.mx = cv;
-    const uint32_t c = M.nl;   // contribute_slot's GA_DEV step
-    if (c == 0) {
-      M.mean = cv;
-    } else {
-      const double m = M.mean;
-      const double nm = m + (cv - m) / (double)(c + 1);
-      M.m2 += (cv - m) * (cv - nm);
-      M.mean = nm;
+    const uint32_t c = M.nl;
+    if (p.multi & MULTI_DEV) {   // contribute_slot's GA_DEV step (a division: only when asked for)
+      if (c == 0) {
+        M.mean = cv;
+      } else {
+        const double m = M.mean;
+        const double nm = m + (cv - m) / (double)(c + 1);
+        M.m2 += (cv - m) * (cv - nm);
+        M.mean = nm;
+      }
     }
     M.nl = c + 1;
     M.nz++;
@@ -1955,11 +1957,15 @@ __device__ __forceinline__ uint64_t rl64(uint64_t x, int l) {
 // 6 -> 4.5 ms, 8 -> 9.4 ms.  Round 2: the 4- and 8-byte classes grew past 5 waves' budget and
 // spilled (48-280 B/lane of scratch): they compile for 4, the vle class (93 VGPRs) stays at 5.
 #define SHORT_OCC(VL) ((VL) == 0 ? 5 : 4)
+#endif
+#ifndef SHORT_OCC2_VLE
 // The fused multi-aggregator variant (KR 2, tsdbhip_run_multi) holds 13 more registers of
 // SpanGroup state: it compiles for 4 (vle at 5 spilled 20 B/lane).
+#define SHORT_OCC2_VLE 4
 #endif
+#define SHORT_OCC2(VL) ((VL) == 0 ? SHORT_OCC2_VLE : 4)
 template <int F, int QW, int VL, int D, int KR>
-__global__ __launch_bounds__(256, (KR) == 2 ? 4 : SHORT_OCC(VL)) void k_short(GridParams p, const RowDesc* __restrict__ rows,
+__global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) void k_short(GridParams p, const RowDesc* __restrict__ rows,
                                                const int64_t* __restrict__ srp, const int64_t* __restrict__ tbeg,
                                                const int64_t* __restrict__ tend) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
