@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define TSDBHIP_ABI_VERSION 8
+#define TSDBHIP_ABI_VERSION 9
 
 /* ---- error codes: one per Java exception on the path --------------------- */
 enum {
@@ -173,6 +173,7 @@ typedef struct {
   double compact_ms;             /* device compaction of the last tsdbhip_load_cells (k_compact pipeline) */
   int64_t fused_queries;         /* queries the last tsdbhip_run_multi answered from ONE fused streaming pass
                                     (0: separate passes, or not a run_multi) */
+  double exchange_ms;            /* multi-device context: gather to devices[0] + merge (host wall time) */
 } tsdbhip_timing;
 
 /* ---- library-level helpers (host logic of the reference, restated) ------- */
@@ -193,7 +194,9 @@ int tsdbhip_scan_bounds(const tsdbhip_query* q, int64_t* scan_start_s, int64_t* 
 /* ---- engine ------------------------------------------------------------- */
 typedef struct tsdbhip_ctx tsdbhip_ctx;
 
-/* One context per GPU (hipSetDevice(device)); one process per GPU in multi-GPU runs. */
+/* One context on one GPU (hipSetDevice(device)).  Several GPUs: one process per GPU with one
+ * context each (the partials / sel exchange below), or one multi-device context
+ * (tsdbhip_init_devices). */
 int tsdbhip_init(int device, tsdbhip_ctx** out);
 void tsdbhip_destroy(tsdbhip_ctx* ctx);
 /* Copy a host batch into HBM (re-laid out: rows 16-B aligned).  Replaces any previous batch. */
@@ -313,6 +316,39 @@ int tsdbhip_sel_select(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_group
  * group-active flags (layouts as tsdbhip_sel_select / tsdbhip_sel_run_values). */
 int tsdbhip_assemble(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_global, const void* val,
                      const void* flag, const void* act, tsdbhip_result** out);
+/* ---- one process, several GPUs: a multi-device context ----------
+ * For a host that drives every GPU from one process (the TSD JVM): tsdbhip_init_devices
+ * returns ONE context over devices[0 .. n_devices) -- an engine context and HIP stream per
+ * device plus a merge context on devices[0].  tsdbhip_load / tsdbhip_synth shard the batch over
+ * the devices, tsdbhip_run / tsdbhip_run_multi run every shard on its own host thread and return
+ * what a one-GPU context returns for the same batch:
+ *   TSDB_SHARD_GROUPS  whole SpanGroups per device (byte-balanced ranges of group ids; series
+ *                      without a group on the last device): every query type runs locally and
+ *                      the results are concatenated in group order (NONE: in batch order) --
+ *                      no device exchange, bit-identical to one GPU;
+ *   TSDB_SHARD_SERIES  contiguous byte-balanced positions of the SpanGroup order (a group may
+ *                      straddle devices): the partial states are gathered to devices[0] (RCCL
+ *                      send / recv over xGMI, or device copies) and merged in device order
+ *                      (tsdbhip_finalize); percentile / median group-by and TSDB_QF_ORDERED
+ *                      gather the span contributions (tsdbhip_sel_select); raw group-by queries
+ *                      need TSDB_SHARD_GROUPS (TSDB_E_NOT_IMPLEMENTED otherwise).
+ * TSDB_SHARD_AUTO (default) picks GROUPS when the group-aligned split is within 10% of the byte
+ * balance, else SERIES; tsdbhip_md_shard_mode sets the mode of the following loads.
+ * transport: TSDB_MD_AUTO = RCCL (ncclCommInitAll) when the devices are distinct, device copies
+ * when a device repeats (several shards on one GPU); TSDB_MD_RCCL / TSDB_MD_COPY force one.
+ * Entry points bound to one device's resident store (load_shard, synth_shard, load_cells,
+ * load_rollup, the histogram path, batch downloads, the partials / sel exchange, rollup
+ * generation, debug_rows) return TSDB_E_NOT_IMPLEMENTED on such a context; the expression
+ * functions run on devices[0].  tsdbhip_last_timing: per-device stage times are the maximum over
+ * the devices, counters are summed, total_ms is the host wall time of the call and exchange_ms
+ * its gather + merge part. */
+enum { TSDB_SHARD_AUTO = -1 };
+enum { TSDB_MD_AUTO = -1, TSDB_MD_COPY = 0, TSDB_MD_RCCL = 1 };
+int tsdbhip_init_devices(const int* devices, int n_devices, int transport, tsdbhip_ctx** out);
+int tsdbhip_md_shard_mode(tsdbhip_ctx* ctx, int mode);
+/* n_devices, transport in use, shard mode of the resident batch (TSDB_SHARD_AUTO before a load)
+ * and, when shard_series is not NULL, the resident series of every device ([n_devices]). */
+int tsdbhip_md_info(tsdbhip_ctx* ctx, int* n_devices, int* transport, int* mode, int64_t* shard_series);
 /* ---- rollup generation --------------------------------
  * RollupInterval (src/rollup/RollupInterval.java:62-240): `interval` e.g. "1h", `row_span`
  * e.g. "1d"; validateAndCompile's checks and arithmetic, IllegalArgumentException ->

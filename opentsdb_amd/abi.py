@@ -144,6 +144,7 @@ class Timing(C.Structure):
         ("index_ms", C.c_double),
         ("compact_ms", C.c_double),
         ("fused_queries", C.c_int64),
+        ("exchange_ms", C.c_double),
     ]
 
 

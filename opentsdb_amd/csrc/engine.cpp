@@ -18,6 +18,7 @@
 
 #include "../../include/tsdbhip.h"
 #include "engine.h"
+#include "multi.h"
 
 using namespace tsdb;
 
@@ -451,6 +452,10 @@ struct tsdbhip_ctx {
   std::vector<uint8_t> ro_scan_act;    // [n_series] resident: rollup rows in the scan range
   // histogram path (hist.cpp): the resident histogram store and its query scratch
   void* hist = nullptr;
+  // multi-device context (multi.cpp, tsdbhip_init_devices): its devices' contexts; null on a
+  // one-device context
+  void* md = nullptr;
+  bool none_orig = false;              // NONE result groups keyed by batch position (multi.cpp merges them)
 };
 
 // accessors for the histogram path's translation unit (hist.cpp)
@@ -461,7 +466,16 @@ std::mutex& ctx_mutex(tsdbhip_ctx* c) { return c->mu; }
 void*& ctx_hist(tsdbhip_ctx* c) { return c->hist; }
 int set_error(int code, const std::string& msg) { return fail(code, msg); }
 void hist_release(void* h);
+void*& ctx_md(tsdbhip_ctx* c) { return c->md; }
+bool ctx_is_md(tsdbhip_ctx* c) { return c && c->md; }
+void ctx_set_none_orig(tsdbhip_ctx* c, bool on) { c->none_orig = on; }
 }  // namespace tsdb
+
+// Entry points bound to one device's resident store refuse a multi-device context.
+#define MD_REFUSE(c, fn)                                                                                   \
+  if ((c) && (c)->md)                                                                                      \
+  return fail(TSDB_E_NOT_IMPLEMENTED, fn " on a multi-device context (tsdbhip_init_devices): it is bound to " \
+                                         "one device's resident store")
 
 // ===========================================================================
 // host logic restatements
@@ -625,6 +639,7 @@ static void release_batch(tsdbhip_ctx* c) {
 
 extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   if (!c) return;
+  if (c->md) { tsdb::md_destroy(c->md); c->md = nullptr; }
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   release_batch(c);
@@ -651,6 +666,7 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
 
 extern "C" int tsdbhip_sync(tsdbhip_ctx* c) {
   if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
+  if (c->md) return tsdb::md_sync(c);
   HIP_OK(hipSetDevice(c->device));
   HIP_OK(hipStreamSynchronize(c->stream));
   return 0;
@@ -1053,7 +1069,10 @@ static int load_with(tsdbhip_ctx* c, const tsdbhip_batch* b, const std::vector<i
   return load_impl(c, &m, cand);   // series indices are unchanged by the merge
 }
 
-extern "C" int tsdbhip_load(tsdbhip_ctx* c, const tsdbhip_batch* b) { return load_with(c, b, nullptr); }
+extern "C" int tsdbhip_load(tsdbhip_ctx* c, const tsdbhip_batch* b) {
+  if (c && c->md) return tsdb::md_load(c, b);
+  return load_with(c, b, nullptr);
+}
 
 // ---- rollup read path ---------------------------------------------
 // The host restates what the scan builds of a rollup table -- RollupSpan.addRow
@@ -1108,6 +1127,7 @@ int vle_put(std::vector<uint8_t>& out, int64_t v) {
 }  // namespace
 
 extern "C" int tsdbhip_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* rb) {
+  MD_REFUSE(c, "tsdbhip_load_rollup");
   if (!c || !rb) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   const tsdbhip_batch* b = &rb->cells;
   const bool cnt = rb->row_cqual_off != nullptr;
@@ -1323,6 +1343,7 @@ extern "C" int tsdbhip_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* r
 // host lays the compacted rows out as the resident batch (series by group, rows by base time,
 // rows without a datapoint dropped as SaltScanner.processRow drops a null compaction).
 extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) {
+  MD_REFUSE(c, "tsdbhip_load_cells");
   if (!c || !cb) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   const int64_t NS = cb->n_series, NR = cb->n_rows, NC = cb->n_cols;
   if (NS < 0 || NR < 0 || NC < 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
@@ -1606,6 +1627,7 @@ extern "C" int tsdbhip_shard_bounds(const tsdbhip_batch* b, int world, int mode,
 }
 
 extern "C" int tsdbhip_load_shard(tsdbhip_ctx* c, const tsdbhip_batch* b, int mode, int64_t begin, int64_t end) {
+  MD_REFUSE(c, "tsdbhip_load_shard");
   int rc = check_batch_arrays(b);
   if (rc) return rc;
   if (begin < 0 || end < begin) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad shard range");
@@ -1735,15 +1757,18 @@ static int synth_impl(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp, int64_t p0, 
 }
 
 extern "C" int tsdbhip_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp) {
+  if (c && c->md) return tsdb::md_synth(c, sp);
   return synth_impl(c, sp, 0, sp ? sp->n_series : 0);
 }
 
 extern "C" int tsdbhip_synth_shard(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp, int64_t pos_begin, int64_t pos_end) {
+  MD_REFUSE(c, "tsdbhip_synth_shard");
   return synth_impl(c, sp, pos_begin, pos_end);
 }
 
 extern "C" int tsdbhip_batch_sizes(tsdbhip_ctx* c, int64_t* n_series, int64_t* n_rows, uint64_t* qual_bytes,
                                    uint64_t* val_bytes) {
+  if (c && c->md) return tsdb::md_batch_sizes(c, n_series, n_rows, qual_bytes, val_bytes);
   if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_batch_sizes over a rollup batch (tsdbhip_load_rollup)");
   if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
   uint64_t q = 0, v = 0;
@@ -1759,6 +1784,7 @@ extern "C" int tsdbhip_batch_sizes(tsdbhip_ctx* c, int64_t* n_series, int64_t* n
 extern "C" int tsdbhip_batch_download(tsdbhip_ctx* c, int64_t* series_row_ptr, uint32_t* row_base_time,
                                       uint64_t* row_qual_off, uint64_t* row_val_off, uint8_t* qual, uint8_t* val,
                                       int32_t* group_id) {
+  MD_REFUSE(c, "tsdbhip_batch_download");
   if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_batch_download over a rollup batch (tsdbhip_load_rollup)");
   if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
   std::lock_guard<std::mutex> lk(c->mu);
@@ -1788,6 +1814,7 @@ extern "C" int tsdbhip_batch_download(tsdbhip_ctx* c, int64_t* series_row_ptr, u
 // Sizes of resident series positions [s0, s1) in the tsdbhip_batch layout.
 extern "C" int tsdbhip_batch_range_sizes(tsdbhip_ctx* c, int64_t s0, int64_t s1, int64_t* n_rows, uint64_t* qual_bytes,
                                          uint64_t* val_bytes) {
+  MD_REFUSE(c, "tsdbhip_batch_range_sizes");
   if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
   if (c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_batch_range_sizes over a rollup batch");
   std::lock_guard<std::mutex> lk(c->mu);
@@ -1807,6 +1834,7 @@ extern "C" int tsdbhip_batch_range_sizes(tsdbhip_ctx* c, int64_t s0, int64_t s1,
 extern "C" int tsdbhip_batch_download_range(tsdbhip_ctx* c, int64_t s0, int64_t s1, int64_t* series_row_ptr,
                                             uint32_t* row_base_time, uint64_t* row_qual_off, uint64_t* row_val_off,
                                             uint8_t* qual, uint8_t* val, int32_t* group_id) {
+  MD_REFUSE(c, "tsdbhip_batch_download_range");
   if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
   if (c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_batch_download_range over a rollup batch");
   std::lock_guard<std::mutex> lk(c->mu);
@@ -1854,6 +1882,7 @@ extern "C" int tsdbhip_batch_download_range(tsdbhip_ctx* c, int64_t s0, int64_t 
 
 // Test hook: the per-row facts k_index derived (RowDesc.ndp / flags / lsb / absmax).
 extern "C" int tsdbhip_debug_rows(tsdbhip_ctx* c, uint32_t* ndp, uint32_t* flags, int32_t* lsb, double* absmax) {
+  MD_REFUSE(c, "tsdbhip_debug_rows");
   if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_OK(hipSetDevice(c->device));
@@ -2660,7 +2689,7 @@ int assemble(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, c
     std::vector<std::pair<int64_t, int64_t>> tmp;
     for (int64_t g = 0; g < G; g++) if (act[g]) tmp.push_back({c->h_orig[g], g});
     std::sort(tmp.begin(), tmp.end());
-    for (size_t i = 0; i < tmp.size(); i++) groups.push_back({(int64_t)i, tmp[i].second});
+    for (size_t i = 0; i < tmp.size(); i++) groups.push_back({c->none_orig ? tmp[i].first : (int64_t)i, tmp[i].second});
   } else {
     for (int64_t g = 0; g < G; g++) if (act[g]) groups.push_back({g, g});
   }
@@ -3008,7 +3037,7 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
     grp_ser.resize(S + 1);
     for (int64_t s = 0; s <= S; s++) grp_ser[s] = s;
     gid_of.assign(S, -1);
-    for (size_t i = 0; i < tmp.size(); i++) gid_of[tmp[i].second] = (int64_t)i;
+    for (size_t i = 0; i < tmp.size(); i++) gid_of[tmp[i].second] = c->none_orig ? tmp[i].first : (int64_t)i;
   } else {
     grp_ser.assign(c->n_groups + 1, 0);
     for (int64_t g = 0, s = 0; g < c->n_groups; g++) {
@@ -3577,6 +3606,7 @@ int run_multi_fused(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_resu
 }  // namespace
 
 extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
+  if (c && c->md) return tsdb::md_run(c, q, out);
   if (!c || !q || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
   *out = nullptr;
@@ -3604,6 +3634,7 @@ extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_resul
 // streaming pass.  The queries must share the time range and the downsampling specification;
 // rate, aggregator and flags may differ.
 extern "C" int tsdbhip_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_result** outs) {
+  if (c && c->md) return tsdb::md_run_multi(c, qs, n, outs);
   if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_run_multi over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !qs || !outs || n < 1) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad argument");
   for (int i = 0; i < n; i++) outs[i] = nullptr;
@@ -3688,9 +3719,26 @@ extern "C" void tsdbhip_result_free(tsdbhip_result* r) { result_free(r); }
 // result allocation for the expression functions' translation unit (expr.cpp)
 namespace tsdb {
 tsdbhip_result* new_result(int64_t n_groups, int64_t n_points) { return make_result(n_groups, n_points); }
+
+// multi.cpp: series of a host batch (batch indices, any order) as a device's resident store
+int load_series(tsdbhip_ctx* c, const tsdbhip_batch* b, const std::vector<int64_t>& series) {
+  return load_with(c, b, &series);
+}
+
+// multi.cpp: how a query crosses devices -- partial states, span contributions (percentile /
+// median group-by, TSDB_QF_ORDERED), a raw group-by, or the per-span NONE aggregator
+int query_kind(tsdbhip_ctx* c, const tsdbhip_query* q, int* kind) {
+  if (!q || !kind) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  Plan P;
+  const int rc = plan_query(c, q, P);
+  if (rc) return rc;
+  *kind = P.none ? QK_NONE : P.raw ? QK_RAW : (P.gsel || P.ordered) ? QK_SEL : QK_PARTIALS;
+  return 0;
+}
 }  // namespace tsdb
 
 extern "C" int tsdbhip_last_timing(tsdbhip_ctx* c, tsdbhip_timing* out) {
+  if (c && c->md) return tsdb::md_timing(c, out);
   if (!c || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   *out = c->timing;
   out->index_ms = c->index_ms;
@@ -3734,6 +3782,7 @@ int plan_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_globa
 
 extern "C" int tsdbhip_partials_layout_get(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global,
                                            tsdbhip_partials_layout* out) {
+  MD_REFUSE(c, "tsdbhip_partials_layout_get");
   if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_partials_layout_get over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   Plan P;
@@ -3746,6 +3795,7 @@ extern "C" int tsdbhip_partials_layout_get(tsdbhip_ctx* c, const tsdbhip_query* 
 }
 
 extern "C" int tsdbhip_run_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, void* partials) {
+  MD_REFUSE(c, "tsdbhip_run_partials");
   if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_run_partials over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !partials) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
@@ -3793,6 +3843,7 @@ extern "C" int tsdbhip_run_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int6
 
 extern "C" int tsdbhip_finalize(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, const void* partials,
                                 int n_ranks, tsdbhip_result** out) {
+  MD_REFUSE(c, "tsdbhip_finalize");
   if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_finalize over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !partials || !out || n_ranks < 1) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad argument");
   std::lock_guard<std::mutex> lk(c->mu);
@@ -3846,6 +3897,7 @@ int plan_sel(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, Pl
 
 extern "C" int tsdbhip_sel_layout(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, int64_t* counts,
                                   int64_t* n_slots) {
+  MD_REFUSE(c, "tsdbhip_sel_layout");
   if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_sel_layout over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !counts || !n_slots) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   Plan P;
@@ -3859,6 +3911,7 @@ extern "C" int tsdbhip_sel_layout(tsdbhip_ctx* c, const tsdbhip_query* q, int64_
 
 extern "C" int tsdbhip_sel_run_values(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, void* vals,
                                       void* uni, void* act) {
+  MD_REFUSE(c, "tsdbhip_sel_run_values");
   if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_sel_run_values over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !vals || !uni || !act) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
@@ -3883,6 +3936,7 @@ extern "C" int tsdbhip_sel_run_values(tsdbhip_ctx* c, const tsdbhip_query* q, in
 
 extern "C" int tsdbhip_sel_select(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, const void* vals,
                                   const int64_t* counts, const void* uni, void* out_val, void* out_flag) {
+  MD_REFUSE(c, "tsdbhip_sel_select");
   if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_sel_select over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !counts || !uni || !out_val || !out_flag) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
@@ -3937,6 +3991,7 @@ extern "C" int tsdbhip_sel_select(tsdbhip_ctx* c, const tsdbhip_query* q, int64_
 
 extern "C" int tsdbhip_assemble(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, const void* val,
                                 const void* flag, const void* act, tsdbhip_result** out) {
+  MD_REFUSE(c, "tsdbhip_assemble");
   if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_assemble over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !val || !flag || !act || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
@@ -4049,6 +4104,7 @@ extern "C" int tsdbhip_rollup_qualifier(int64_t timestamp, int32_t basetime, int
 }
 
 extern "C" int tsdbhip_rollup_run(tsdbhip_ctx* c, const tsdbhip_rollup_spec* sp, int64_t* n_cells, uint64_t* value_bytes) {
+  MD_REFUSE(c, "tsdbhip_rollup_run");
   if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_rollup_run over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !sp) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   if (!iv_valid(&sp->interval)) return fail(TSDB_E_ILLEGAL_ARGUMENT, "invalid rollup interval");
@@ -4253,6 +4309,7 @@ extern "C" int tsdbhip_rollup_run(tsdbhip_ctx* c, const tsdbhip_rollup_spec* sp,
 
 extern "C" int tsdbhip_rollup_download(tsdbhip_ctx* c, int32_t* series, uint32_t* base_time, uint8_t* qualifier,
                                        uint64_t* val_off, uint8_t* value) {
+  MD_REFUSE(c, "tsdbhip_rollup_download");
   if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_OK(hipSetDevice(c->device));

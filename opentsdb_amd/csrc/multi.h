@@ -1,0 +1,30 @@
+// Multi-device context (multi.cpp) <-> engine.cpp: the engine entry points hand a context made by
+// tsdbhip_init_devices to these; multi.cpp drives its per-device contexts through the public API
+// plus the few hooks below.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/tsdbhip.h"
+
+namespace tsdb {
+// engine.cpp
+void*& ctx_md(tsdbhip_ctx* c);                     // the MultiDev of a multi-device context (or null)
+void ctx_set_none_orig(tsdbhip_ctx* c, bool on);   // NONE results keyed by batch position, not renumbered
+int load_series(tsdbhip_ctx* c, const tsdbhip_batch* b, const std::vector<int64_t>& series);
+enum { QK_PARTIALS = 0, QK_SEL = 1, QK_RAW = 2, QK_NONE = 3 };
+int query_kind(tsdbhip_ctx* c, const tsdbhip_query* q, int* kind);   // plan_query's verdict
+int set_error(int code, const std::string& msg);
+tsdbhip_result* new_result(int64_t n_groups, int64_t n_points);
+// multi.cpp
+int md_load(tsdbhip_ctx* c, const tsdbhip_batch* b);
+int md_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp);
+int md_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out);
+int md_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_result** outs);
+int md_timing(tsdbhip_ctx* c, tsdbhip_timing* out);
+int md_sync(tsdbhip_ctx* c);
+int md_batch_sizes(tsdbhip_ctx* c, int64_t* n_series, int64_t* n_rows, uint64_t* qual_bytes, uint64_t* val_bytes);
+void md_destroy(void* md);
+}  // namespace tsdb

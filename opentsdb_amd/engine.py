@@ -31,10 +31,12 @@ EXPORTS = [
     "tsdbhip_debug_rows", "tsdbhip_shard_bounds", "tsdbhip_load_shard", "tsdbhip_synth_shard",
     "tsdbhip_load_rollup", "tsdbhip_load_cells", "tsdbhip_load_histograms", "tsdbhip_hist_run",
     "tsdbhip_hist_run_range", "tsdbhip_hist_result_free", "tsdbhip_expr_map", "tsdbhip_expr_zip", "tsdbhip_expr_topn",
-    "tsdbhip_batch_range_sizes", "tsdbhip_batch_download_range", "tsdbhip_expr_sync",
+    "tsdbhip_batch_range_sizes", "tsdbhip_batch_download_range", "tsdbhip_expr_sync", "tsdbhip_init_devices",
+    "tsdbhip_md_shard_mode", "tsdbhip_md_info",
 ]
 
-SHARD_SERIES, SHARD_GROUPS, SHARD_SPANS = 0, 1, 2   # tsdbhip.h TSDB_SHARD_*
+SHARD_AUTO, SHARD_SERIES, SHARD_GROUPS, SHARD_SPANS = -1, 0, 1, 2   # tsdbhip.h TSDB_SHARD_*
+MD_AUTO, MD_COPY, MD_RCCL = -1, 0, 1                               # tsdbhip.h TSDB_MD_*
 
 
 class EngineError(Exception):
@@ -67,6 +69,9 @@ def lib():
         L.tsdbhip_parse_downsample.argtypes = [C.c_char_p, C.POINTER(abi.Query)]
         L.tsdbhip_scan_bounds.argtypes = [C.POINTER(abi.Query), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
         L.tsdbhip_init.argtypes = [C.c_int, C.POINTER(vp)]
+        L.tsdbhip_init_devices.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(vp)]
+        L.tsdbhip_md_shard_mode.argtypes = [vp, C.c_int]
+        L.tsdbhip_md_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_void_p]
         L.tsdbhip_destroy.argtypes = [vp]
         L.tsdbhip_load.argtypes = [vp, C.POINTER(abi.Batch)]
         L.tsdbhip_synth.argtypes = [vp, C.POINTER(abi.SynthSpec)]
@@ -192,13 +197,33 @@ class _ResultOwner:
 
 
 class Engine:
-    """One tsdbhip context bound to one GPU."""
+    """One tsdbhip context bound to one GPU -- or, with `devices`, one multi-device context
+    (tsdbhip_init_devices) that shards every load over those GPUs and answers queries as one GPU
+    would."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, devices=None, transport: int = MD_AUTO):
         self.ctx = C.c_void_p()
-        _check(lib().tsdbhip_init(device, C.byref(self.ctx)))
+        if devices is None:
+            _check(lib().tsdbhip_init(device, C.byref(self.ctx)))
+        else:
+            arr = np.ascontiguousarray(devices, dtype=np.int32)
+            _check(lib().tsdbhip_init_devices(arr.ctypes.data, len(arr), transport, C.byref(self.ctx)))
+            device = int(arr[0])
         self.device = device
+        self.devices = None if devices is None else [int(d) for d in devices]
         self._batch = None
+
+    def shard_mode(self, mode: int):
+        """tsdbhip_md_shard_mode: SHARD_AUTO / SHARD_SERIES / SHARD_GROUPS for the next loads."""
+        _check(lib().tsdbhip_md_shard_mode(self.ctx, mode))
+
+    def md_info(self):
+        """tsdbhip_md_info -> (n_devices, transport, shard mode of the resident batch, series per device)."""
+        nd, tr, mode = C.c_int(), C.c_int(), C.c_int()
+        _check(lib().tsdbhip_md_info(self.ctx, C.byref(nd), C.byref(tr), C.byref(mode), None))
+        per = np.zeros(nd.value, np.int64)
+        _check(lib().tsdbhip_md_info(self.ctx, None, None, None, per.ctypes.data))
+        return nd.value, tr.value, mode.value, per
 
     def close(self):
         if self.ctx:

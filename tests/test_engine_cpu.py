@@ -31,7 +31,24 @@ def test_library_exports_every_header_symbol():
 
 
 def test_abi_version():
-    assert engine.lib().tsdbhip_abi_version() == 8
+    assert engine.lib().tsdbhip_abi_version() == 9
+
+
+def test_multi_device_context_argument_checks():
+    """tsdbhip_init_devices validates its arguments before touching a device; without a GPU the
+    context is refused with an error, never a crash."""
+    import ctypes as C
+    L = engine.lib()
+    out = C.c_void_p()
+    devs = (C.c_int * 2)(0, 0)
+    assert L.tsdbhip_init_devices(None, 2, -1, C.byref(out)) == abi.TSDB_E_ILLEGAL_ARGUMENT
+    assert L.tsdbhip_init_devices(devs, 0, -1, C.byref(out)) == abi.TSDB_E_ILLEGAL_ARGUMENT
+    assert L.tsdbhip_init_devices(devs, 2, 7, C.byref(out)) == abi.TSDB_E_ILLEGAL_ARGUMENT
+    assert L.tsdbhip_md_shard_mode(None, 0) == abi.TSDB_E_ILLEGAL_ARGUMENT
+    if not os.path.exists("/dev/kfd"):
+        with pytest.raises(engine.EngineError):
+            engine.Engine(devices=[0, 0])
+    assert abi.Timing.exchange_ms.offset == abi.Timing.fused_queries.offset + 8
 
 
 @pytest.mark.parametrize("name", abi.AGGREGATOR_NAMES)
