@@ -251,7 +251,6 @@ int64_t jcal_step(const JZone& Z, int64_t t, int unit, int64_t n, int sign) {
 // DateTime.previousInterval(ts, n, unit, tz) in two steps: jcal_top, the instant the set()
 // calls produce (the top of the enclosing unit, shifted back for intervals longer than it) and
 // the unit / count the walk steps by; then the walk from there to the last step <= ts.
-// false = not supported (weeks > 2)
 bool jcal_top(const JZone& Z, int64_t ts, int64_t n, int unit, int64_t& c, int& uo, int64_t& io) {
   uo = unit;
   io = n;
@@ -282,10 +281,18 @@ bool jcal_top(const JZone& Z, int64_t ts, int64_t n, int unit, int64_t& c, int& 
       c = Z.from_wall(day_of_civil(y, n == 1 ? m : 1, 1) * 86400000LL);
       break;
     case TSDB_CAL_W: {
-      if (2 % n != 0) return false;   // set(MONTH, 0) + set(DAY_OF_WEEK): a January week
-      const int64_t dow = ((day - 3) % 7 + 7) % 7;   // Sunday-first weeks (1970-01-04 was a Sunday)
-      c = Z.from_wall((day - dow) * 86400000LL);
-      uo = TSDB_CAL_D;
+      // Sunday-first weeks, one minimal day in the first week (the default US locale;
+      // 1970-01-04 was a Sunday)
+      auto sunday_on_or_before = [](int64_t dd) { return dd - ((dd - 3) % 7 + 7) % 7; };
+      if (2 % n == 0) {
+        c = Z.from_wall(sunday_on_or_before(day) * 86400000LL);   // set(DAY_OF_WEEK, SUNDAY)
+      } else {
+        // set(MONTH, 0) then set(DAY_OF_WEEK, SUNDAY): GregorianCalendar resolves YEAR + MONTH +
+        // WEEK_OF_MONTH (still ts's week of ITS month) + DAY_OF_WEEK, i.e. that week of January
+        const int64_t wom = (day - sunday_on_or_before(day_of_civil(y, m, 1))) / 7 + 1;
+        c = Z.from_wall((sunday_on_or_before(day_of_civil(y, 1, 1)) + 7 * (wom - 1)) * 86400000LL);
+      }
+      uo = TSDB_CAL_D;   // the walk steps 7 days whatever the interval
       io = 7;
       break;
     }
@@ -390,6 +397,9 @@ struct tsdbhip_ctx {
   bool calc_valid = false;
   std::vector<int64_t> calc_key, calc_bounds;
   int64_t calc_seek = 0;
+  bool calc_anchored = false;            // ... the spans' grids disagree: per-anchor sequences
+  std::vector<int64_t> calc_anchors;
+  std::vector<std::vector<int64_t>> calc_seqs;
   DevBuf first_ts;
   int64_t mdp_ss = 0, mdp_se = 0, mdp = 0;
   DevBuf sel_vals, sel_sorted, sel_uni, sel_gsp;   // percentile / median group-by
@@ -1920,6 +1930,11 @@ struct Plan {
   bool emit_only = false;        // group-by step over bucket values already in pre_dense / pre_pres
   bool multi = false;            // fused multi-aggregator pass (run_multi_fused): partials to c->mp*, no reduce
   bool multi_dev = false;        //   ... with the Welford state (a dev query among them)
+  // calendar grids anchored per span that disagree (plan_calendar): each anchor's boundary
+  // sequence; run_anchored downsamples every span on its own and aggregates over the union
+  bool anchored = false;
+  std::vector<int64_t> anchors;
+  std::vector<std::vector<int64_t>> seqs;
 };
 
 bool is_sel_agg(int a) { return a == TSDB_AGG_MEDIAN || (a >= TSDB_AGG_P999 && a < TSDB_AGG_COUNT_ALL); }
@@ -1935,6 +1950,28 @@ bool is_sel_agg(int a) { return a == TSDB_AGG_MEDIAN || (a >= TSDB_AGG_P999 && a
 // and for ms / s / m / h lattices when the zone's offsets in range are congruent modulo the
 // step; otherwise the anchors come from each series' first datapoint (k_first_ts) and spans on
 // grids that disagree return NOT_IMPLEMENTED (their union of timestamps is not one grid).
+// DateTime.previousInterval of every first datapoint f[i] (sorted; INT64_MAX = the series has
+// none, anchor INT64_MAX).  Datapoints with the same jcal_top inside one step of that top's walk
+// share its anchor, so the walk runs once per such step.
+void anchors_of(const JZone& Z, int64_t n, int unit, const std::vector<int64_t>& f, std::vector<int64_t>& a) {
+  a.assign(f.size(), INT64_MAX);
+  int64_t top = INT64_MIN, lo = INT64_MAX, hi = INT64_MIN, cur = 0;
+  for (size_t i = 0; i < f.size(); i++) {
+    const int64_t t = f[i];
+    if (t == INT64_MAX) break;
+    int64_t tp, io;
+    int uo;
+    jcal_top(Z, t, n, unit, tp, uo, io);
+    if (!(tp == top && t >= lo && t < hi)) {
+      jcal_prev(Z, t, n, unit, cur);
+      top = tp;
+      lo = cur;
+      hi = jcal_add(Z, cur, uo, io);
+    }
+    a[i] = cur;
+  }
+}
+
 int plan_calendar(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
   const int unit = q->ds_calendar;
   if (unit < TSDB_CAL_MS || unit > TSDB_CAL_Y) return fail(TSDB_E_ILLEGAL_ARGUMENT, "Unrecognized unit type");
@@ -1952,8 +1989,7 @@ int plan_calendar(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
     P.bounds = c->calc_bounds;
   } else {
     int64_t a0;
-    if (!jcal_prev(Z, S0, n, unit, a0))
-      return fail(TSDB_E_NOT_IMPLEMENTED, "calendar week intervals of more than 2 weeks");
+    jcal_prev(Z, S0, n, unit, a0);
     const int64_t sc = a0 == S0 ? a0 : jcal_step(Z, a0, unit, n, 1);   // seekInterval(scan start)
     // zone-global grids: one boundary sequence whatever the anchor
     bool global = unit == TSDB_CAL_D ? n == 1 : unit == TSDB_CAL_W ? n == 1 : unit == TSDB_CAL_N ? 12 % n == 0
@@ -1990,22 +2026,8 @@ int plan_calendar(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
       f.resize(NS);
       std::sort(f.begin(), f.end());
       f.erase(std::unique(f.begin(), f.end()), f.end());
-      // datapoints with the same top (jcal_top) inside one bucket of that top's walk share its
-      // anchor; the walk runs once per such bucket
-      int64_t top = INT64_MIN, lo = INT64_MAX, hi = INT64_MIN;
-      for (int64_t t : f) {
-        if (t == INT64_MAX) break;
-        int64_t tp, io;
-        int uo;
-        if (!jcal_top(Z, t, n, unit, tp, uo, io)) return fail(TSDB_E_NOT_IMPLEMENTED, "calendar week intervals of more than 2 weeks");
-        if (tp == top && t >= lo && t < hi) continue;
-        int64_t a;
-        jcal_prev(Z, t, n, unit, a);
-        if (anchors.empty() || anchors.back() != a) anchors.push_back(a);
-        top = tp;
-        lo = a;
-        hi = jcal_add(Z, a, uo, io);
-      }
+      anchors_of(Z, n, unit, f, anchors);
+      anchors.erase(std::remove(anchors.begin(), anchors.end(), INT64_MAX), anchors.end());
       std::sort(anchors.begin(), anchors.end());
       anchors.erase(std::unique(anchors.begin(), anchors.end()), anchors.end());
     }
@@ -2044,16 +2066,26 @@ int plan_calendar(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
       for (size_t k = 0; k < sq.size(); k++) if (T[i0 + k] != sq[k]) return false;
       return true;
     };
-    for (const auto& sq : seqs)
-      if (!agrees(sq))
-        return fail(TSDB_E_NOT_IMPLEMENTED, "spans on calendar grids that disagree (per-span anchors): their union of "
-                                            "timestamps is not one slot grid");
+    bool disagree = false;
+    for (const auto& sq : seqs) disagree = disagree || !agrees(sq);
+    if (disagree && fill)
+      return fail(TSDB_E_NOT_IMPLEMENTED, "a fill policy over spans on calendar grids that disagree (per-span anchors)");
     if (fill && !agrees(F)) return fail(TSDB_E_NOT_IMPLEMENTED, "fill grid disagrees with the spans' calendar grids");
     P.bounds = fill ? F : T;
     c->calc_key = key;
     c->calc_bounds = P.bounds;
     c->calc_seek = sc;
+    c->calc_anchored = disagree;
+    c->calc_anchors = disagree ? anchors : std::vector<int64_t>();
+    c->calc_seqs = disagree ? seqs : std::vector<std::vector<int64_t>>();
     c->calc_valid = true;
+  }
+  // spans on grids that disagree: their union of timestamps is no slot grid; run_anchored
+  // downsamples each anchor's spans on its own sequence and aggregates over the union
+  P.anchored = c->calc_anchored;
+  if (P.anchored) {
+    P.anchors = c->calc_anchors;
+    P.seqs = c->calc_seqs;
   }
   P.mode = MODE_TABLE;
   P.seek = c->calc_seek;
@@ -2229,8 +2261,6 @@ int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
       }
     }
   }
-  if (P.mode == MODE_TABLE && P.f == F_SEL)
-    return fail(TSDB_E_NOT_IMPLEMENTED, "percentile downsampling over variable-width calendar slots");
   // slot arrays live in LDS when they fit next to 4 waves' worth of staging, else in HBM
   P.gslot = grid_wave_lds(P.K, q->rate != 0, false) > 40 * 1024;
   return cmp_scan_check(c, P);
@@ -3001,7 +3031,17 @@ struct PhaseTrace {
   }
 };
 
-int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_result** out) {
+// Points handed to the raw evaluator instead of the resident rows' datapoints: each span's
+// Downsampler output (run_anchored).  n[s] points of series s, consecutive in pts; live[s] = the
+// span has rows in the scan range (its SpanGroup exists even when no bucket survives).
+struct RawExt {
+  std::vector<int32_t> n;
+  std::vector<RawPt> pts;
+  std::vector<uint8_t> live;
+  bool sec = true;   // every timestamp a whole second
+};
+
+int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_result** out, const RawExt* ext = nullptr) {
   PhaseTrace tr("raw");
   const int64_t S = c->n_series;
   const int64_t start = P.ss * 1000, end = P.se * 1000;
@@ -3013,6 +3053,11 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
   int64_t np = 0;
   for (int64_t s = 0; s < S; s++) {
     sp_off[s] = np;
+    if (ext) {
+      np += ext->n[s];
+      sp_n[s] = ext->n[s];
+      continue;
+    }
     for (int64_t r = c->h_srp[s]; r < c->h_srp[s + 1]; r++) {
       if ((int64_t)c->h_base[r] < P.ss || (int64_t)c->h_base[r] >= P.se) continue;
       const uint32_t f = c->h_flags[r];
@@ -3026,12 +3071,18 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
     sp_n[s] = (int32_t)(np - sp_off[s]);
   }
   sp_off[S] = np;
+  if (ext) {   // Downsampler outputs: doubles (Downsampler.isInteger :259-262)
+    all_s = ext->sec;
+    any_float = true;
+  }
+  // a span counts for its SpanGroup when it has points -- or, for Downsampler outputs, rows
+  auto span_live = [&](int64_t s) { return ext ? ext->live[s] != 0 : sp_n[s] > 0; };
   // groups: dense batch groups, or one per span for NONE (TsdbQuery.java:941-962)
   std::vector<int64_t> grp_ser;
   std::vector<int64_t> gid_of;   // result group id of each group row
   if (P.none) {
     std::vector<std::pair<int64_t, int64_t>> tmp;
-    for (int64_t s = 0; s < S; s++) if (sp_n[s] > 0) tmp.push_back({c->h_orig[s], s});
+    for (int64_t s = 0; s < S; s++) if (span_live(s)) tmp.push_back({c->h_orig[s], s});
     std::sort(tmp.begin(), tmp.end());
     // NONE groups must be contiguous series ranges: one series each, in resident order
     grp_ser.resize(S + 1);
@@ -3050,7 +3101,7 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
   tr.mark("host spans");
   std::vector<uint8_t> act(std::max<int64_t>(1, G), 0);
   for (int64_t g = 0; g < G; g++)
-    for (int64_t s = grp_ser[g]; s < grp_ser[g + 1]; s++) if (sp_n[s] > 0) { act[g] = 1; break; }
+    for (int64_t s = grp_ser[g]; s < grp_ser[g + 1]; s++) if (span_live(s)) { act[g] = 1; break; }
   // device arrays
   const int64_t R = std::max<int64_t>(1, c->n_rows);
   HIP_OK(c->r_rowpt.ensure(R * 8));
@@ -3102,7 +3153,11 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
     rp.m_head = c->r_mhead.as<int64_t>();
   }
   HIP_OK(hipEventRecord(c->ev[0], c->stream));
-  HIP_OK(launch_raw_decode(rp, c->stream));
+  if (ext) {
+    if (np) HIP_OK(hipMemcpyAsync(rp.pts, ext->pts.data(), np * sizeof(RawPt), hipMemcpyHostToDevice, c->stream));
+  } else {
+    HIP_OK(launch_raw_decode(rp, c->stream));
+  }
   if (q->rate) {
     HIP_OK(launch_raw_rate(rp, c->stream));
     HIP_OK(hipMemcpyAsync(sp_n.data(), c->r_spn.p, std::max<int64_t>(1, S) * 4, hipMemcpyDeviceToHost, c->stream));
@@ -3396,6 +3451,102 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
   return 0;
 }
 
+// Spans on calendar grids that disagree (per-span anchors: DateTime.previousInterval of each
+// span's first datapoint, src/core/Downsampler.java:336-350, src/utils/DateTime.java:445-606).
+// The reference's AggregationIterator interleaves the spans' Downsampler outputs over the union
+// of their timestamps, interpolating the spans without a point there
+// (src/core/AggregationIterator.java:500-797) -- the raw path's evaluation.  Each anchor's spans
+// are downsampled on that anchor's boundary sequence (one MODE_TABLE pass per anchor, every
+// series' bucket values in pre_dense / pre_pres), the buckets become the spans' points, and the
+// raw union evaluator (k_raw_*) aggregates them: rate, LERP, percentile group-by and NONE as for
+// raw datapoints.  Points before the SpanGroup start are dropped (AggregationIterator :416-441).
+int run_anchored(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_result** out) {
+  const int64_t S = c->n_series;
+  const int unit = q->ds_calendar;
+  const int64_t n = q->ds_interval_ms / CAL_UNIT_MS[unit];
+  const JZone Z{q->ds_tz};
+  // every series' first datapoint at or after the seek point, and its anchor
+  std::vector<int64_t> f(std::max<int64_t>(1, S), INT64_MAX);
+  HIP_OK(c->first_ts.ensure(std::max<int64_t>(1, S) * 8));
+  HIP_OK(launch_first_ts(c->rows.as<RowDesc>(), c->srp.as<int64_t>(), c->qual.as<uint8_t>(), S, P.ss, P.se, P.seek,
+                         c->first_ts.as<int64_t>(), c->stream));
+  if (S) HIP_OK(hipMemcpyAsync(f.data(), c->first_ts.p, S * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  f.resize(S);
+  std::vector<int64_t> fu(f);
+  std::sort(fu.begin(), fu.end());
+  fu.erase(std::unique(fu.begin(), fu.end()), fu.end());
+  std::vector<int64_t> au;
+  anchors_of(Z, n, unit, fu, au);
+  std::vector<int32_t> cls(S, -1);
+  for (int64_t s = 0; s < S; s++) {
+    if (f[s] == INT64_MAX) continue;
+    const int64_t a = au[std::lower_bound(fu.begin(), fu.end(), f[s]) - fu.begin()];
+    const auto it = std::lower_bound(P.anchors.begin(), P.anchors.end(), a);
+    if (it == P.anchors.end() || *it != a) return fail(TSDB_E_HIP, "calendar anchor of a series missing from the plan");
+    cls[s] = (int32_t)(it - P.anchors.begin());
+  }
+  // the spans with rows in the scan range: their SpanGroups exist
+  RawExt ext;
+  ext.n.assign(S, 0);
+  ext.live.assign(S, 0);
+  for (int64_t s = 0; s < S; s++)
+    for (int64_t r = c->h_srp[s]; r < c->h_srp[s + 1] && !ext.live[s]; r++)
+      ext.live[s] = (int64_t)c->h_base[r] >= P.ss && (int64_t)c->h_base[r] < P.se;
+  std::vector<std::vector<RawPt>> sp(S);
+  const int64_t start = P.ss * 1000;
+  tsdbhip_query q2 = *q;
+  q2.rate = 0;   // RateSpan wraps the Downsampler: the raw evaluator applies it to the buckets
+  for (size_t k = 0; k < P.anchors.size(); k++) {
+    const std::vector<int64_t>& sq = P.seqs[k];
+    if (sq.size() < 2 || std::find(cls.begin(), cls.end(), (int32_t)k) == cls.end()) continue;
+    Plan Pk = P;
+    Pk.anchored = false;
+    Pk.anchors.clear();
+    Pk.seqs.clear();
+    Pk.mode = MODE_TABLE;
+    Pk.bounds = sq;
+    Pk.K = (int64_t)sq.size() - 1;
+    Pk.B0 = sq[0];
+    Pk.none = true;   // one tile per series: ungrouped spans too
+    Pk.gsel = 0;
+    Pk.ordered = false;
+    Pk.raw = false;
+    Pk.gslot = grid_wave_lds(Pk.K, false, false) > 40 * 1024;
+    if (P.f == F_SEL) Pk.values_only = true;
+    else Pk.dense_out = true;
+    int rc = run_device(c, &q2, Pk, S, false);
+    if (rc) return rc;
+    const int64_t K = Pk.K;
+    std::vector<double> dense(std::max<int64_t>(1, S * K));
+    std::vector<uint8_t> pres(std::max<int64_t>(1, S * K));
+    int32_t err = 0;
+    if (S * K) {
+      HIP_OK(hipMemcpyAsync(dense.data(), c->pre_dense.p, S * K * 8, hipMemcpyDeviceToHost, c->stream));
+      HIP_OK(hipMemcpyAsync(pres.data(), c->pre_pres.p, S * K, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    if (err) return fail(err, "error raised by the device path");
+    for (int64_t s = 0; s < S; s++) {
+      if (cls[s] != (int32_t)k) continue;
+      for (int64_t j = 0; j < K; j++) {
+        if (!pres[s * K + j] || sq[j] < start) continue;
+        RawPt pt;
+        pt.tsf = sq[j] | RAW_FLOAT;
+        std::memcpy(&pt.bits, &dense[s * K + j], 8);
+        sp[s].push_back(pt);
+        if (sq[j] % 1000) ext.sec = false;
+      }
+    }
+  }
+  for (int64_t s = 0; s < S; s++) {
+    ext.n[s] = (int32_t)sp[s].size();
+    ext.pts.insert(ext.pts.end(), sp[s].begin(), sp[s].end());
+  }
+  return run_raw(c, q, P, out, &ext);
+}
+
 }  // namespace
 
 namespace {
@@ -3617,6 +3768,7 @@ extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_resul
   if (rc) return rc;
   const int64_t G = P.none ? c->n_series : c->n_groups;
   if (P.raw) return run_raw(c, q, P, out);
+  if (P.anchored) return run_anchored(c, q, P, out);
   if (P.gsel || P.ordered) {
     rc = P.gsel ? run_sel_group(c, q, P, G) : run_ordered(c, q, P, G);
     if (rc) return rc;
@@ -3656,7 +3808,7 @@ extern "C" int tsdbhip_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n,
   int rc = plan_query(c, &q0, P0);
   if (rc) return rc;
   if (P0.raw) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_run_multi needs a downsampling specification");
-  if (P0.f != F_SEL) {
+  if (P0.f != F_SEL || P0.anchored) {
     // Cheap downsampling functions: decomposable aggregators (sum, avg, min, max, dev, count)
     // share ONE streaming pass that keeps every aggregator's SpanGroup state (run_multi_fused);
     // otherwise each query runs its own fused pass, which beats a generic group-by step over
@@ -3671,6 +3823,7 @@ extern "C" int tsdbhip_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n,
       rc = plan_query(c, &qs[i], P);
       if (!rc) {
         if (P.raw) rc = fail(TSDB_E_ILLEGAL_ARGUMENT, "bad query");
+        else if (P.anchored) { rc = run_anchored(c, &qs[i], P, &outs[i]); if (!rc) continue; }
         else if (P.gsel || P.ordered) rc = P.gsel ? run_sel_group(c, &qs[i], P, G) : run_ordered(c, &qs[i], P, G);
         else rc = run_device(c, &qs[i], P, P.none ? c->n_series : G, true);
         if (!rc) rc = collect(c, &qs[i], P, P.none ? c->n_series : G, true, &outs[i]);
@@ -3774,6 +3927,8 @@ int plan_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_globa
   if (P.raw) return fail(TSDB_E_NOT_IMPLEMENTED, "multi-GPU raw (union LERP) queries are not implemented yet");
   if (P.gsel) return fail(TSDB_E_NOT_IMPLEMENTED, "percentile / median group-by: use the tsdbhip_sel_* exchange");
   if (P.ordered) return fail(TSDB_E_NOT_IMPLEMENTED, "TSDB_QF_ORDERED across ranks: use the tsdbhip_sel_* exchange");
+  if (P.anchored)
+    return fail(TSDB_E_NOT_IMPLEMENTED, "calendar grids anchored per span that disagree across ranks: shard by group");
   if (n_groups_global < c->n_groups) return fail(TSDB_E_ILLEGAL_ARGUMENT, "n_groups_global smaller than the local groups");
   return 0;
 }
@@ -3889,6 +4044,8 @@ int plan_sel(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, Pl
   if (rc) return rc;
   if (!P.gsel && !P.ordered)
     return fail(TSDB_E_ILLEGAL_ARGUMENT, "not a percentile / median group-by or TSDB_QF_ORDERED query");
+  if (P.anchored)
+    return fail(TSDB_E_NOT_IMPLEMENTED, "calendar grids anchored per span that disagree across ranks: shard by group");
   if (n_groups_global < c->n_groups) return fail(TSDB_E_ILLEGAL_ARGUMENT, "n_groups_global smaller than the local groups");
   return 0;
 }
@@ -4001,6 +4158,7 @@ extern "C" int tsdbhip_assemble(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t 
   int rc = plan_query(c, q, P);
   if (rc) return rc;
   if (P.raw || P.none) return fail(TSDB_E_ILLEGAL_ARGUMENT, "assemble takes downsampled group-by queries");
+  if (P.anchored) return fail(TSDB_E_NOT_IMPLEMENTED, "calendar grids anchored per span that disagree: no dense slot grid");
   const int64_t G = n_groups_global, K = P.K;
   HIP_OK(c->out_val.ensure(std::max<int64_t>(1, G * K) * 8));
   HIP_OK(c->out_flag.ensure(std::max<int64_t>(1, G * K)));

@@ -1548,8 +1548,15 @@ static int64_t cal_prev(int64_t ts, int64_t n, int unit, const tsdbhip_tz* z) {
         const int64_t dow = ((day - 3) % 7 + 7) % 7;
         c = tz_from_wall(z, (day - dow) * 86400000);
       } else {
-        /* set(MONTH, 0) then set(DAY_OF_WEEK, ...): lenient resolution of a January week */
-        jthrow(TSDB_E_NOT_IMPLEMENTED, "calendar intervals of more than 2 weeks");
+        /* set(MONTH, 0) then set(DAY_OF_WEEK, SUNDAY): GregorianCalendar.computeTime resolves
+         * YEAR + MONTH + WEEK_OF_MONTH + DAY_OF_WEEK (Calendar.selectFields: the WEEK_OF_MONTH
+         * pattern carries the newest stamp, DAY_OF_WEEK's).  WEEK_OF_MONTH is still the computed
+         * week of ts in its own month (getWeekNumber, minimal days 1): week w of January. */
+        const int64_t dow1 = ((days_from_civil(y, m, 1) - 3) % 7 + 7) % 7;
+        const int64_t wom = (day - (days_from_civil(y, m, 1) - dow1)) / 7 + 1;
+        const int64_t j1 = days_from_civil(y, 1, 1);
+        const int64_t jdow = ((j1 - 3) % 7 + 7) % 7;
+        c = tz_from_wall(z, (j1 - jdow + 7 * (wom - 1)) * 86400000);
       }
       uo = TSDB_CAL_D;   /* the loop steps 7 days whatever the interval */
       io = 7;

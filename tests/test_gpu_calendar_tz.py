@@ -117,16 +117,63 @@ def test_tz_utc_table_equals_utc(eng, dst_batch):
         assert_groups_match(a, b, "sum", ctx=spec)
 
 
-def test_anchors_disagree_not_implemented(eng):
-    # 7sc anchors at the top of each span's first hour; 3600 % 7 != 0, so spans whose first
-    # datapoints lie in different hours sit on different grids
+@pytest.fixture(scope="module")
+def staggered():
+    """Spans whose first datapoints lie in different hours: 7sc anchors each span at the top of
+    its first hour and 3600 % 7 != 0, so the spans sit on different 7 s grids."""
     T0 = 1356998400
-    b = merge(synth.generate(2, T0, 720, 5000, value_kind=0, n_groups=1, seed=1),
-              synth.generate(2, T0 + 3600, 720, 5000, value_kind=0, n_groups=1, seed=2))
-    q = q_of("7sc-sum", T0, T0 + 3 * 3600, "sum", None)
+    return merge(synth.generate(3, T0, 720, 5000, value_kind=2, n_groups=2, int_mod=900, seed=1),
+                 synth.generate(2, T0 + 3600 + 1234, 700, 5000, value_kind=0, n_groups=2, seed=2),
+                 synth.generate(3, T0 + 2 * 3600 + 17, 500, 7000, value_kind=1, n_groups=2, int_mod=300, seed=5))
+
+
+@pytest.mark.parametrize("agg", ["sum", "avg", "min", "max", "dev", "count", "zimsum", "mimmax", "first", "last",
+                                 "p90", "median", "none"])
+def test_anchors_disagree_union_evaluation(eng, staggered, agg):
+    """Per-span grids that disagree: each span's Downsampler output, aggregated over the union
+    of their timestamps (run_anchored -> the raw union evaluator)."""
+    T0 = 1356998400
+    for spec in ["7sc-sum", "11sc-avg", "7sc-max"]:
+        q = q_of(spec, T0, T0 + 3 * 3600, agg, None)
+        check(eng, staggered, q, agg, f"anchored {spec} {agg}")
+
+
+def test_anchors_disagree_rate_percentile_zone(eng, staggered):
+    T0 = 1356998400
+    q = q_of("7sc-avg", T0, T0 + 3 * 3600, "sum", None)
+    q.rate = 1
+    check(eng, staggered, q, "sum", "anchored rate")
+    q = q_of("13sc-p95", T0 + 100, T0 + 3 * 3600 - 50, "sum", None)
+    check(eng, staggered, q, "sum", "anchored p95 downsampling")
+    q = q_of("7sc-sum", T0, T0 + 3 * 3600, "sum", "Asia/Kabul")
+    check(eng, staggered, q, "sum", "anchored Kabul")
+
+
+def test_anchors_disagree_with_fill_not_implemented(eng, staggered):
+    T0 = 1356998400
+    q = q_of("7sc-sum-nan", T0, T0 + 3 * 3600, "sum", None)
     with pytest.raises(Exception) as ei:
-        eng.run_batch(b, q)
+        eng.run_batch(staggered, q)
     assert "NotImplemented" in str(ei.value)
+
+
+@pytest.mark.parametrize("tz", [None, "America/Denver", "Pacific/Fiji"])
+@pytest.mark.parametrize("spec", ["1nc-p95", "1dc-p99", "1dc-median", "2dc-p50", "1wc-ep90r7", "1dc-p75-nan"])
+def test_percentile_downsampling_over_calendar_slots(eng, dst_batch, tz, spec):
+    """Percentile / median downsampling over variable-width calendar slots (k_pct with the
+    MODE_TABLE slot lookup), across Denver's DST start and Fiji's DST end."""
+    for agg in ["sum", "max"]:
+        q = q_of(spec, TA + 2 * 86400 + 1234, TA + 66 * 86400, agg, tz)
+        check(eng, dst_batch, q, agg, f"{tz} {spec} {agg}")
+
+
+@pytest.mark.parametrize("tz", [None, "America/Denver"])
+@pytest.mark.parametrize("spec", ["3wc-sum", "5wc-avg", "4wc-max-nan", "3wc-p90"])
+def test_week_intervals_wider_than_two(eng, dst_batch, tz, spec):
+    """n > 2 weeks: previousInterval's January-week resolution, which still lands on the Sunday
+    of the span's first week (DateTime.java:559-571, TestDateTime.previousIntervalWeeks)."""
+    q = q_of(spec, TA + 2 * 86400 + 1234, TA + 66 * 86400, "sum", tz)
+    check(eng, dst_batch, q, "sum", f"{tz} {spec}")
 
 
 def test_anchors_agree_across_spans(eng):
