@@ -2415,13 +2415,17 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     HIP_OK(hipMemsetAsync(c->redo_n.p, 0, 4, c->stream));
     gp.redo_list = c->redo.as<int32_t>();
     gp.redo_n = c->redo_n.as<int32_t>();
-    // Buckets inside rows (interval | 1 h) and a statistic near the ends (p90 and up):
-    // k_pct_rows, with k_pct over the series it hands back; else k_pct over every series.
+    // Buckets inside rows (interval | 1 h): k_pct_rows, with k_pct over the series it hands
+    // back; else k_pct over every series.  Its extraction covers statistics near the ends (p90
+    // and up); 1 h buckets of 4-byte values go through its 32-bit key kernel, which ranks any
+    // statistic (median, p50, p75 by a bitwise search).
     const int sel_i = (q->ds_function - TSDB_AGG_P999) % 6;
     const char* renv = std::getenv("TSDBHIP_PCTROWS");
-    const bool rows_path = P.mode == MODE_GRID && q->ds_function != TSDB_AGG_MEDIAN && sel_i <= 3 && P.I > 0 &&
-                           3600000 % P.I == 0 && P.B0 % P.I == 0 && pct_rows_supported(c->pct_qw, c->pct_vl) &&
-                           !(renv && renv[0] == '0');
+    const char* kenv = std::getenv("TSDBHIP_PCT_KEYS");
+    const bool near_end = q->ds_function != TSDB_AGG_MEDIAN && sel_i <= 3;
+    const bool keys = c->pct_vl == 4 && P.I == 3600000 && !(kenv && kenv[0] == '0');
+    const bool rows_path = P.mode == MODE_GRID && (near_end || keys) && P.I > 0 && 3600000 % P.I == 0 &&
+                           P.B0 % P.I == 0 && pct_rows_supported(c->pct_qw, c->pct_vl) && !(renv && renv[0] == '0');
     if (rows_path) {
       HIP_OK(c->redo2.ensure(std::max<int64_t>(1, c->n_series) * 4));
       HIP_OK(c->redo2_n.ensure(16));

@@ -826,8 +826,53 @@ __device__ __forceinline__ double unkey32(uint32_t k, bool isf) {
   return (double)__uint_as_float((k & 0x80000000u) ? (k ^ 0x80000000u) : ~k);
 }
 
-// The statistic of a one-bucket row of 4-byte values; false = not this path's case (mixed
-// float / int row, or the statistic too far from both ends): the caller takes select_keep.
+// Key of rank `target` (0-based, ascending) among the wave's 512 keys (absent = 0, counted
+// first): a bitwise binary search -- per bit one compare per key and a ballot count, all on the
+// scalar unit -- starting below the prefix every present key shares.  Mid-rank statistics
+// (median, p50, p75) take it instead of popping ~n/2 wave maxima.
+__device__ __forceinline__ uint32_t kth_key32(const uint32_t key[DPL], int target) {
+  uint32_t kand = ~0u, kor = 0u;
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    if (key[j]) { kand &= key[j]; kor |= key[j]; }
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    kand &= (uint32_t)__shfl_xor((int)kand, d, 64);
+    kor |= (uint32_t)__shfl_xor((int)kor, d, 64);
+  }
+  kand = (uint32_t)__builtin_amdgcn_readfirstlane((int)kand);
+  kor = (uint32_t)__builtin_amdgcn_readfirstlane((int)kor);
+  const uint32_t diff = kand ^ kor;
+  if (diff == 0) return kand;   // every present key equal
+  const int top = 31 - __clz((int)diff);
+  uint32_t ans = top == 31 ? 0u : (kand & ~((2u << top) - 1u));
+  for (int b = top; b >= 0; b--) {
+    const uint32_t t = ans | (1u << b);
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) cnt += __popcll(__ballot(key[j] < t));
+    if (cnt <= target) ans = t;
+  }
+  return ans;
+}
+
+// The key of rank target + 1 given k0 = the key of rank target.
+__device__ __forceinline__ uint32_t next_key32(const uint32_t key[DPL], uint32_t k0, int target) {
+  int le = 0;
+  uint32_t gt = ~0u;
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    le += __popcll(__ballot(key[j] <= k0));
+    if (key[j] > k0) gt = min(gt, key[j]);
+  }
+  if (le > target + 1) return k0;
+  return ~wave_max_u32(~gt);
+}
+
+// The statistic of a one-bucket row of 4-byte values; 0 = not this path's case (mixed float /
+// int row): the caller hands the series to k_pct.  Near the ends the k largest / smallest keys
+// are popped (topk_u32); mid ranks take the bitwise search.
 template <int QW>
 __device__ __forceinline__ int pct_row_keys(const GridParams& p, const RowLite& d, const RawT<QW, 4>& rw, double q,
                                             double& x) {
@@ -866,18 +911,21 @@ __device__ __forceinline__ int pct_row_keys(const GridParams& p, const RowLite& 
     x = (double)NAN;
     return 1;
   }
-  // select_sorted / select_extreme: LEGACY pos = p (n + 1)
-  const double pos = q * (double)(n + 1);
-  const int ip = (int)floor(pos);
-  int lo_i, hi_i;
-  if (pos < 1) { lo_i = hi_i = 0; }
-  else if (pos >= (double)n) { lo_i = hi_i = n - 1; }
-  else { lo_i = ip - 1; hi_i = ip; }
+  // select_sorted: Median.runDouble sorted[n / 2]; PercentileAgg LEGACY pos = p (n + 1)
+  int64_t r0, r1;
+  sel_ranks(p.sel_fn, n, r0, r1);
+  const int lo_i = (int)r0, hi_i = r1 < 0 ? (int)r0 : (int)r1;
+  const double pos = q * (double)(n + 1);   // (percentiles only: the interpolation weight)
   const int ktop = n - lo_i, kbot = hi_i + 1;
-  if (min(ktop, kbot) > EXT_MAX) return 0;
   double a, b;
   uint32_t ek, ek1;
-  if (ktop <= kbot) {
+  if (min(ktop, kbot) > EXT_MAX) {
+    const int zeros = 64 * DPL - n;
+    const uint32_t k0 = kth_key32(key, zeros + lo_i);
+    const uint32_t k1 = hi_i == lo_i ? k0 : next_key32(key, k0, zeros + lo_i);
+    a = unkey32(k0, wf);
+    b = unkey32(k1, wf);
+  } else if (ktop <= kbot) {
     topk_u32(key, ktop, ek, ek1);
     a = unkey32(ek, wf);
     b = (hi_i == lo_i) ? a : unkey32(ek1, wf);
@@ -934,7 +982,7 @@ __device__ __forceinline__ bool pct_row(const GridParams& p, const RowLite& cd, 
     if (!__ballot(any)) return true;
     const int n = __builtin_amdgcn_readlane(wave_incl_sum_dpp(__popc(keep)), 63);
     double x = (double)NAN;
-    if (n > 0 && !select_keep(val, keep, n, q, x)) return false;
+    if (n > 0 && (q < 0 || !select_keep(val, keep, n, q, x))) return false;
     if (lane == 0) { dense[slot0] = x; pres[slot0] = 1; }
     return true;
   }
@@ -957,7 +1005,7 @@ __device__ __forceinline__ bool pct_row(const GridParams& p, const RowLite& cd, 
     }
     const int n = __builtin_amdgcn_readlane(wave_incl_sum_dpp(__popc(keep)), 63);
     double x = (double)NAN;
-    if (n > 0 && !select_keep(val, keep, n, q, x)) return false;
+    if (n > 0 && (q < 0 || !select_keep(val, keep, n, q, x))) return false;
     if (lane == 0) { dense[mn] = x; pres[mn] = 1; }
   }
   return true;
@@ -974,7 +1022,8 @@ __global__ __launch_bounds__(256, KEYS ? PCT_KEYS_OCC : 1) void k_pct_rows(GridP
   double* dense = p.pre_dense + s * K;
   uint8_t* pres = p.pre_pres + s * K;
   for (int k = lane; k < K; k += 64) pres[k] = 0;
-  const double q = pct_quantile(p.sel_fn) / 100.0;
+  // (median: no quantile; the extraction path hands such series back, the key path ranks them)
+  const double q = p.sel_fn == TSDB_AGG_MEDIAN ? -1.0 : pct_quantile(p.sel_fn) / 100.0;
   const int64_t r0 = p.series_row_ptr[s], r1 = p.series_row_ptr[s + 1];
   int64_t last_base = -1;   // base of the previous in-range row (repeated bases: redo)
   for (int64_t w0 = r0; w0 < r1; w0 += 64) {
@@ -1469,6 +1518,113 @@ __global__ __launch_bounds__(SEL_REG_T, OCC) void k_sel_reg(SelParams p) {
   }
 }
 
+// k_sel_reg2<SL>: k_sel_reg over SL adjacent slots of one group per block.  The [series][K]
+// layout puts a series' slots side by side, so one 16-B load per row serves two slots: a group's
+// row lines are read K / SL times instead of K times (k_sel_reg re-reads every line from L2 once
+// per slot block).  Keys stay in registers (SL x SEL_REG_R per thread); the slots are selected
+// one after the other with the same radix select, so the results are k_sel_reg's.
+template <int SL, int OCC>
+__global__ __launch_bounds__(SEL_REG_T, OCC) void k_sel_reg2(SelParams p) {
+  __shared__ SelShared S;
+  __shared__ unsigned long long red[2];
+  const int64_t nkc = (p.K + SL - 1) / SL;
+  const int64_t nseg = p.G * nkc;
+  const int64_t per = (nseg + 7) / 8;
+  const int64_t i = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (i >= nseg) return;
+  const int tid = threadIdx.x;
+  const int64_t g = i / nkc, k0 = (i - g * nkc) * SL;
+  const int ns = (int)min((int64_t)SL, p.K - k0);
+  bool any = false;
+#pragma unroll
+  for (int sl = 0; sl < SL; sl++) any = any || (sl < ns && p.uni[g * p.K + k0 + sl]);
+  if (!any) {
+    if (tid < ns) { p.out_val[g * p.K + k0 + tid] = 0.0; p.out_flag[g * p.K + k0 + tid] = 0; }
+    return;
+  }
+  const int64_t gs0 = p.group_series_ptr[g], n = p.group_series_ptr[g + 1] - gs0;
+  // all loads issued before any is consumed; SL = 2: one 16-B load per row when K is even
+  double x[SL][SEL_REG_R];
+  const bool vec = SL == 2 && (p.K & 1) == 0 && ns == 2;
+#pragma unroll
+  for (int u = 0; u < SEL_REG_R; u++) {
+    const int64_t j = tid + (int64_t)u * SEL_REG_T;
+    const int64_t jj = j < n ? j : 0;
+    const double* src = p.vals + (gs0 + jj) * p.K + k0;
+    if (vec) {
+      const double2 v2 = *reinterpret_cast<const double2*>(src);
+      x[0][u] = v2.x;
+      x[SL - 1][u] = v2.y;
+    } else {
+#pragma unroll
+      for (int sl = 0; sl < SL; sl++) x[sl][u] = sl < ns ? src[sl] : 0.0;
+    }
+  }
+#pragma unroll
+  for (int sl = 0; sl < SL; sl++) {
+    if (sl >= ns) break;
+    const int64_t oi = g * p.K + k0 + sl;
+    if (!p.uni[oi]) {
+      if (tid == 0) { p.out_val[oi] = 0.0; p.out_flag[oi] = 0; }
+      continue;
+    }
+    uint64_t key[SEL_REG_R];
+    uint32_t valid = 0;
+    int nan_local = 0;
+#pragma unroll
+    for (int u = 0; u < SEL_REG_R; u++) {
+      const bool v = tid + (int64_t)u * SEL_REG_T < n;
+      valid |= (v ? 1u : 0u) << u;
+      nan_local += (v && isnan(x[sl][u])) ? 1 : 0;
+      key[u] = f2key(canon_nan(x[sl][u]));
+    }
+    nan_local = wave_sum_int(nan_local);
+    __syncthreads();
+    if (tid == 0) red[0] = 0;
+    __syncthreads();
+    if ((tid & 63) == 0 && nan_local) atomicAdd(&red[0], (unsigned long long)nan_local);
+    __syncthreads();
+    const int64_t m = n - (int64_t)red[0];   // non-NaN values (they hold ranks 0 .. m-1)
+    __syncthreads();
+    int64_t r0 = 0, r1 = -1;
+    if (m > 0) sel_ranks(p.fn, m, r0, r1);
+    double v0 = NAN, v1 = NAN;
+    if (m > 0) {
+      const uint64_t kk0 = reg_radix_select<SEL_REG_R>(key, valid, r0, S, red);
+      v0 = key2f(kk0);
+      if (r1 >= 0) {
+        __syncthreads();
+        if (tid == 0) { red[0] = 0; red[1] = ~0ULL; }
+        __syncthreads();
+        int le = 0;
+        uint64_t gt = ~0ULL;
+#pragma unroll
+        for (int u = 0; u < SEL_REG_R; u++) {
+          if (valid >> u & 1) {
+            if (key[u] <= kk0) le++;
+            else gt = key[u] < gt ? key[u] : gt;
+          }
+        }
+        le = wave_sum_int(le);
+        gt = wave_min_u64(gt);
+        if ((tid & 63) == 0) {
+          atomicAdd(&red[0], (unsigned long long)le);
+          atomicMin(&red[1], (unsigned long long)gt);
+        }
+        __syncthreads();
+        v1 = (int64_t)red[0] > r1 ? v0 : key2f(red[1]);
+      }
+    }
+    if (tid == 0) {
+      const double r = m == 0 ? (double)NAN
+                              : select_sorted(p.fn, (int)m, [&](int j) { return (int64_t)j == r0 ? v0 : v1; });
+      if (isinf(r)) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // AggregationIterator.doubleValue :640-643
+      p.out_val[oi] = r;
+      p.out_flag[oi] = 1;
+    }
+  }
+}
+
 // One thread per (group, slot), consecutive slots in consecutive lanes (coalesced rows):
 // contribute_slot over the group's spans in index order, then ps_final.  A span without a
 // value at the slot holds sel_values' fill pattern (0x7FF87FF87FF87FF8), distinct from the
@@ -1564,6 +1720,15 @@ hipError_t launch_sel_seg(const SelParams& p, hipStream_t s, int64_t maxn) {
     // two blocks per CU (8 waves / SIMD, a few spilled registers) beat one: config 3 p99
     // 11.4 vs 13.3 ms per step
     const char* oenv = std::getenv("TSDBHIP_SEL_OCC");
+    const char* senv = std::getenv("TSDBHIP_SEL_SLOTS");   // slots per block (1: k_sel_reg)
+    const int sl = senv ? std::atoi(senv) : 2;
+    if (!p.cols && sl == 2) {
+      const int64_t per2 = (p.G * ((p.K + 1) / 2) + 7) / 8;
+      // one block per CU without spills (122 VGPRs); TSDBHIP_SEL_OCC=8 forces two (spilling)
+      if (oenv && oenv[0] == '8') hipLaunchKernelGGL((k_sel_reg2<2, 8>), dim3((unsigned)(per2 * 8)), dim3(SEL_REG_T), 0, s, p);
+      else hipLaunchKernelGGL((k_sel_reg2<2, 4>), dim3((unsigned)(per2 * 8)), dim3(SEL_REG_T), 0, s, p);
+      return hipGetLastError();
+    }
     if (oenv && oenv[0] == '4') hipLaunchKernelGGL(k_sel_reg<4>, dim3((unsigned)(per * 8)), dim3(SEL_REG_T), 0, s, p);
     else hipLaunchKernelGGL(k_sel_reg<8>, dim3((unsigned)(per * 8)), dim3(SEL_REG_T), 0, s, p);
     return hipGetLastError();

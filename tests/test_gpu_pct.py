@@ -152,3 +152,34 @@ def test_pct_extreme_selection_with_ties(eng, fn, interval):
     b = synth.generate(16, T0, 360, 10000, value_kind=1, n_groups=2, int_mod=5, seed=11)
     q = abi.new_query(T0, T0 + 3599, "max", ds_function=abi.AGG[fn], ds_interval_ms=interval)
     assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "max", ctx=f"{fn} {interval}")
+
+
+@pytest.mark.parametrize("fn", ["median", "p50", "p75", "ep50r7", "p90", "p999"])
+def test_pct_mid_ranks_key_kernel(eng, fn):
+    """1 h buckets of 4-byte values through k_pct_rows' 32-bit key kernel at any rank: the
+    bitwise rank search (median, p50, p75) and extraction (near the ends) on float32 rows with
+    ties, NaNs, negative values and +-0.0, and on int32 rows with few distinct values; buckets
+    of 1..360 values (points missing at random)."""
+    rng = np.random.default_rng(17)
+    rows, gids = [], []
+    for s in range(14):
+        keep = rng.random(3 * 360) < (0.9 if s % 5 else 0.01)
+        ts = T0 * 1000 + np.flatnonzero(keep).astype(np.int64) * 10000
+        n = len(ts)
+        if s % 2 == 0:
+            f = np.round(rng.normal(0, 20, n) * 2) / 2
+            f[rng.random(n) < 0.1] = np.nan
+            f[rng.random(n) < 0.05] = -0.0
+            f[rng.random(n) < 0.05] = 0.0
+            rows.append(synth.encode_rows(ts, np.zeros(n, np.int64), f, np.full(n, 1), np.zeros(n, bool)))
+        else:
+            lv = rng.integers(40000, 40006, n) * (1 if s % 3 else -1)
+            rows.append(synth.encode_rows(ts, lv, np.zeros(n), np.zeros(n, np.int64), np.zeros(n, bool)))
+        gids.append(s % 3)
+    order = sorted(range(14), key=lambda i: gids[i])
+    b = synth.from_series([rows[i] for i in order], [gids[i] for i in order])
+    for agg in ["max", "min", "count"]:
+        q = abi.new_query(T0, T0 + 3 * 3600 - 1, agg, ds_function=abi.AGG[fn], ds_interval_ms=3600000)
+        assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), agg, ctx=f"{fn} {agg}")
+    q = abi.new_query(T0, T0 + 3 * 3600 - 1, "none", ds_function=abi.AGG[fn], ds_interval_ms=3600000)
+    assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "none", tol=0.0, ctx=f"{fn} none")

@@ -107,6 +107,8 @@ def main():
     ap.add_argument("--only", default="", help="comma-separated group-by aggregators to run (config 3)")
     ap.add_argument("--ordered", action="store_true", help="TSDB_QF_ORDERED (bit-exact span-order float reductions)")
     ap.add_argument("--multi", action="store_true", help="config 3: the queries through one tsdbhip_run_multi call")
+    ap.add_argument("--fns", default="p99,ep99r7", help="config 5: comma-separated 1h downsampling functions")
+    ap.add_argument("--no-extra", action="store_true", help="config 5: skip the run_multi and rollup lines")
     args = ap.parse_args()
     from opentsdb_amd import abi, dist, synth
     from opentsdb_amd.engine import Engine, parse_downsample
@@ -161,8 +163,11 @@ def main():
     if args.config == 5:
         eng = Engine(0)
         series = args.series if args.series != 100_000 else 1_250_000
-        qs = {f"sum:1h-{f}": dsq("sum", f"1h-{f}", T0 + 86399) for f in ["p99", "ep99r7"]}
+        qs = {f"sum:1h-{f}": dsq("sum", f"1h-{f}", T0 + 86399) for f in args.fns.split(",")}
         grid_config(args, eng, qs, series, 8640, 0, 1, args.groups)
+        if args.no_extra:
+            eng.close()
+            return
         # four group-by aggregators over one 1h-p99 downsampling: shared selection pass
         ql = [dsq(a, "1h-p99", T0 + 86399) for a in ["sum", "max", "min", "avg"]]
         eng.run_multi(ql)
