@@ -920,9 +920,8 @@ static bool merge_cells(std::vector<uint8_t>& lq, std::vector<uint8_t>& lv, cons
 // Loads series cand[0 .. m) of the batch (all series when cand is null), in that order as the
 // "batch order" of the resident store (NONE results are emitted in it); series are then stably
 // sorted by group (SpanGroup membership, order inside a group kept).
-static int load_impl(tsdbhip_ctx* c, const tsdbhip_batch* b, const std::vector<int64_t>* cand = nullptr) {
-  if (!c || !b) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
-  std::lock_guard<std::mutex> lk(c->mu);
+// (the caller holds c->mu: tsdbhip_load_rollup sets its rollup state under the same lock)
+static int load_body(tsdbhip_ctx* c, const tsdbhip_batch* b, const std::vector<int64_t>* cand) {
   HIP_OK(hipSetDevice(c->device));
   if (b->n_series < 0 || b->n_rows < 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
   if (b->n_series > 0 && (!b->series_row_ptr || !b->group_id)) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null batch arrays");
@@ -1012,6 +1011,12 @@ static int load_impl(tsdbhip_ctx* c, const tsdbhip_batch* b, const std::vector<i
   HIP_OK(hipMemcpy(c->val.p, hv.data(), hv.size(), hipMemcpyHostToDevice));
   if (c->n_series) HIP_OK(hipMemcpy(c->gid.p, c->h_group.data(), c->n_series * 4, hipMemcpyHostToDevice));
   return finish_load(c, rd);
+}
+
+static int load_impl(tsdbhip_ctx* c, const tsdbhip_batch* b, const std::vector<int64_t>* cand = nullptr) {
+  if (!c || !b) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  return load_body(c, b, cand);
 }
 
 // ---------------------------------------------------------------------------
@@ -1328,9 +1333,9 @@ extern "C" int tsdbhip_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* r
   m.qual = ov.q.data();
   m.val = ov.v.data();
   m.group_id = gid.data();
-  int rc = load_impl(c, &m);
+  std::lock_guard<std::mutex> lk(c->mu);   // the batch and its rollup state in one critical section
+  int rc = load_body(c, &m, nullptr);
   if (rc) return rc;
-  std::lock_guard<std::mutex> lk(c->mu);
   c->ro_active = true;
   c->ro_counts = cnt;
   c->ro_iv = iv;
@@ -1982,9 +1987,15 @@ int plan_calendar(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
   const int64_t S0 = P.ss * 1000, E0 = P.se * 1000;
   const bool fill = q->ds_fill != TSDB_FILL_NONE;
   // cache: the plan depends on the interval, the scan range, the fill, the zone and the batch
-  std::vector<int64_t> key = {unit, n, S0, E0, fill ? 1 : 0, (int64_t)(intptr_t)q->ds_tz,
+  std::vector<int64_t> key = {unit, n, S0, E0, fill ? 1 : 0, q->ds_tz ? 1 : 0,
                               q->ds_tz ? q->ds_tz->n : -1};
-  if (q->ds_tz && q->ds_tz->n > 0) { key.push_back(q->ds_tz->utc_ms[0]); key.push_back(q->ds_tz->utc_ms[q->ds_tz->n - 1]); }
+  if (q->ds_tz) {   // the whole table (a struct reused at the same address may hold another zone)
+    uint64_t h = 1469598103934665603ULL;   // FNV-1a over the transitions and offsets
+    auto mix = [&](uint64_t v) { for (int i = 0; i < 8; i++) { h ^= (v >> (8 * i)) & 0xFF; h *= 1099511628211ULL; } };
+    for (int i = 0; i < q->ds_tz->n; i++) mix((uint64_t)q->ds_tz->utc_ms[i]);
+    for (int i = 0; i <= q->ds_tz->n; i++) mix((uint64_t)(uint32_t)q->ds_tz->offset_ms[i]);
+    key.push_back((int64_t)h);
+  }
   if (c->calc_valid && c->calc_key == key) {
     P.bounds = c->calc_bounds;
   } else {

@@ -15,6 +15,10 @@ static constexpr int HK_MAX = 1 << (HT_BITS - 1);
 
 // per-column decode status (k_hist_validate)
 enum : uint8_t { HC_DROP = 0, HC_SIMPLE = 1, HC_LONG = 2 };
+// status bit: a SimpleHistogram column whose bucket keys are not strictly increasing (it may
+// repeat a key: fromHistogram's TreeMap.put keeps the last count)
+constexpr uint8_t HC_UNSORTED = 0x80;
+constexpr uint8_t HC_KIND = 0x7F;
 
 struct HistLoadParams {
   int64_t n_cells;

@@ -93,9 +93,16 @@ __global__ void k_hist_validate(HistLoadParams p) {
   if (st != HC_SIMPLE) return;
   const int cnt = (int16_t)(((uint32_t)v[1] << 8) | v[2]);
   uint64_t i = 3, cv;
+  uint64_t prev_ord = 0;
+  bool sorted = true;   // keys in HistogramBucket.compareTo order, strictly (histogram() writes a TreeMap)
 #pragma unroll 1
   for (int j = 0; j < cnt; j++) {
     const uint64_t key = ((uint64_t)fcanon(be32(v + i)) << 32) | fcanon(be32(v + i + 4));
+    // Float.compare order of (lower, upper) as one unsigned key
+    auto ford = [](uint32_t b) { return (b & 0x80000000u) ? ~b : (b | 0x80000000u); };
+    const uint64_t ord = ((uint64_t)ford((uint32_t)(key >> 32)) << 32) | ford((uint32_t)key);
+    if (j > 0 && ord <= prev_ord) sorted = false;
+    prev_ord = ord;
     i += 8;
     varlong(v, n, i, cv);
     uint64_t slot = hk_hash(key) & (uint64_t)(HT_SIZE - 1);
@@ -113,6 +120,7 @@ __global__ void k_hist_validate(HistLoadParams p) {
       slot = (slot + 1) & (uint64_t)(HT_SIZE - 1);
     }
   }
+  if (!sorted) p.status[c] = HC_SIMPLE | HC_UNSORTED;
 }
 
 __device__ __forceinline__ int32_t dict_index(const HistQueryParams& p, uint64_t key) {
@@ -295,9 +303,25 @@ struct DictGlobal {
 };
 
 // One column per lane (pt < 0: no column); the wave's lanes step through their buckets together.
+// true when the bucket key recurs among the column's buckets [j + 1, cnt) (bytes from i on):
+// TreeMap.put keeps the last count of a key (SimpleHistogram.fromHistogram :110-113)
+template <class S>
+__device__ bool key_recurs(const S& src, uint64_t i, int j, int cnt, uint64_t key) {
+#pragma unroll 1
+  for (int k = j + 1; k < cnt; k++) {
+    const uint64_t kk = ((uint64_t)fcanon(sbe32(src, i)) << 32) | fcanon(sbe32(src, i + 4));
+    i += 8;
+    (void)svarlong(src, i);
+    if (kk == key) return true;
+  }
+  return false;
+}
+
 template <class S, class Dict>
 __device__ __forceinline__ void accum_columns(const HistQueryParams& p, int32_t pt, const S& src, uint64_t i0,
-                                              uint8_t kind, const Dict& dict) {
+                                              uint8_t kind_st, const Dict& dict) {
+  const uint8_t kind = kind_st & HC_KIND;
+  const bool unsorted = (kind_st & HC_UNSORTED) != 0;
   int cnt = 0;
   uint64_t i = i0 + 3;
   if (pt >= 0 && kind == HC_SIMPLE) cnt = (int16_t)((src.at(i0 + 1) << 8) | src.at(i0 + 2));
@@ -325,6 +349,7 @@ __device__ __forceinline__ void accum_columns(const HistQueryParams& p, int32_t 
       const uint64_t key = ((uint64_t)fcanon(sbe32(src, i)) << 32) | fcanon(sbe32(src, i + 4));
       i += 8;
       val = svarlong(src, i);
+      if (unsorted && key_recurs(src, i, j, cnt, key)) val = 0;   // a later bucket's count replaces it
       di = dict.find(key);
       if (di < 0) set_err(p.err, -22, WHY_DICT);
       else addr = base + (uint64_t)di;

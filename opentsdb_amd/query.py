@@ -306,9 +306,8 @@ class TsdbQuery:
             e = end + (3600 - end % 3600)
         return s, e
 
-    def rollup_interval_name(self):
-        """transformDownSamplerToRollupQuery (TsdbQuery.java:1665-1700): the best-match rollup
-        table of the downsampling interval, or None (a raw scan)."""
+    def _best_rollup(self):
+        """getRollupInterval's best match for the downsampling interval, or None."""
         ds = self.downsampler
         if self.rollups is None or ds is None or ds.interval <= 0:
             return None
@@ -317,6 +316,23 @@ class TsdbQuery:
             return self.rollups.config.getRollupInterval(ds.interval // 1000)[0]
         except NoSuchRollupForIntervalException:
             return None
+
+    def rollup_interval_name(self):
+        """transformDownSamplerToRollupQuery (TsdbQuery.java:1665-1700): the best-match rollup
+        table of the downsampling interval, or None (a raw scan) -- also when the best match is
+        the default interval, the raw table itself (:1694-1697)."""
+        name = self._best_rollup()
+        if name is not None and self.rollups.config.isDefaultInterval(name):
+            return None
+        return name
+
+    def _raw_aggregator_override(self):
+        """A count group-by becomes sum as soon as a rollup query is built (:1681-1683), before
+        the default-interval check drops that query: the raw scan then aggregates with sum."""
+        name = self._best_rollup()
+        if name is not None and self.rollups.config.isDefaultInterval(name) and self.aggregator == "count":
+            return "sum"
+        return None
 
     def _filters(self):
         """Tag filters and group-by tag uids of setTimeSeries' tags (None: no series match)."""
@@ -443,6 +459,8 @@ class TsdbQuery:
             return out
         batch, keys = self.build_batch()
         q = self.to_abi()
+        if self._raw_aggregator_override():
+            q.aggregator = abi.AGG[self._raw_aggregator_override()]
         runner = self.runner
         if runner is None:
             from .engine import default_engine

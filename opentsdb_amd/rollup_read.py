@@ -40,11 +40,24 @@ class RollupConfig:
     """RollupConfig: aggregator name -> id, interval name -> RollupInterval."""
 
     def __init__(self, agg_ids: dict, intervals):
+        """intervals: (interval, row_span) or (interval, row_span, is_default) -- the default
+        interval is the raw table (RollupInterval.isDefaultInterval); at most one (:93-103)."""
         from . import engine
         self.ids = {k.lower(): int(v) for k, v in agg_ids.items()}
         self.intervals = {}
-        for iv, span in intervals:
+        self.default = None
+        for item in intervals:
+            iv, span = item[0], item[1]
+            if iv in self.intervals:
+                raise ValueError(f"Only one interval of each type can be configured: {iv}")
+            if len(item) > 2 and item[2]:
+                if self.default is not None:
+                    raise ValueError(f"Multiple default intervals configured. Only one is allowed: {iv}")
+                self.default = iv
             self.intervals[iv] = engine.rollup_interval(iv, span)
+
+    def isDefaultInterval(self, name: str) -> bool:   # RollupInterval.isDefaultInterval :298-300
+        return name == self.default
 
     def getIdForAggregator(self, agg: str) -> int:   # :279-289
         if not agg:

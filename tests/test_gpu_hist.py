@@ -189,3 +189,38 @@ def test_gpu_accum_fallback_paths(eng, layouts, nb):
                         ms_frac=0.0)
     for ds in (None, "2m-sum"):
         run_both(eng, hb, U.query(T0, T0 + 3600, "sum", ds), [50.0, 99.0], True)
+
+
+def raw_simple(buckets, under=0, over=0, codec_id=0):
+    """A stored SimpleHistogram column written bucket by bucket in the given order (duplicates
+    and out-of-order keys included), as a foreign writer could store it."""
+    import struct
+    out = bytearray([codec_id]) + struct.pack(">h", len(buckets))
+    for lo, up, cnt in buckets:
+        out += struct.pack(">ff", lo, up) + H.kryo_varlong(cnt)
+    return bytes(out + H.kryo_varlong(under) + H.kryo_varlong(over))
+
+
+def test_gpu_repeated_bucket_keys_last_count_wins(eng):
+    """fromHistogram's TreeMap.put (src/core/SimpleHistogram.java:110-113): a key repeated inside
+    one column keeps its LAST count; columns with keys out of order still aggregate by key."""
+    cols = [
+        raw_simple([(0.0, 1.0, 5), (1.0, 2.0, 7), (0.0, 1.0, 11)], 1, 2),           # (0,1) -> 11
+        raw_simple([(1.0, 2.0, 3), (0.0, 1.0, 4)], 0, 1),                          # out of order
+        raw_simple([(-0.0, 1.0, 2), (0.0, 1.0, 9), (-0.0, 1.0, 6), (5.0, 6.0, 1)]),  # -0.0 != 0.0
+        raw_simple([(0.0, 1.0, 1), (0.0, 1.0, 2), (0.0, 1.0, 3), (0.0, 1.0, 4)]),   # -> 4
+    ]
+    series = []
+    for s in range(2):
+        rows = []
+        for r in range(2):
+            base = T0 + r * 3600
+            cells = []
+            for k in range(6):
+                _, q = H.histogram_qualifier(base + 10 * k + s)
+                cells.append((q, cols[(k + r + s) % len(cols)]))
+            rows.append((base, cells))
+        series.append(rows)
+    hb = H.HostHistBatch.from_rows(series, [0, 0], {0: H.HCODEC_SIMPLE})
+    for ds in (None, "1m-sum", "1h-sum"):
+        run_both(eng, hb, U.query(T0, T0 + 2 * 3600, "sum", ds), [50.0, 90.0, 10.0], True)
