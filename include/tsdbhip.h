@@ -435,10 +435,12 @@ int tsdbhip_load_rollup(tsdbhip_ctx* ctx, const tsdbhip_rollup_batch* rb);
  * datapoints merged by offset, the newest column's kept at a repeated offset (any other value
  * -> IllegalDataException unless fix_duplicates), 2-byte float and length fixups, the meta byte;
  * a single column needing no fixup as stored; rows without a datapoint dropped.  The compacted
- * rows become the resident batch.  Compaction exceptions are raised by the first query whose
- * scan range covers the row.  NOT_IMPLEMENTED: two rows of one series with the same base time
- * (salt buckets; tsdbhip_load merges those), more than 2^31 columns, rows or datapoints; per row,
- * lazily: a compacted cell out of time order, a datapoint column with an empty value. */
+ * rows become the resident batch; rows of one series with the same base time (one per salt
+ * bucket) are compacted each and then merged in scan order as Span.addRow / RowSeq.addRow merge
+ * them (src/core/Span.java:202-219).  Compaction exceptions are raised by the first query whose
+ * scan range covers the row.  NOT_IMPLEMENTED: more than 2^31 columns, rows or datapoints in one
+ * call; per row, lazily: a compacted cell out of time order, a datapoint column with an empty
+ * value. */
 typedef struct {
   int64_t n_series;
   const int64_t* series_row_ptr;   /* [n_series + 1] */

@@ -1500,6 +1500,12 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   std::vector<int64_t> rdq(R1, -1), rdv(R1, -1), srp(NS + 1, 0);
   std::vector<RowDesc> rd;
   std::vector<int32_t> hgroup(NS);
+  // Rows of one series with the same base time (salt buckets): Span.addRow merges the second
+  // compacted row into the first (RowSeq.addRow, src/core/Span.java:202-219).  Such rows are
+  // compacted into consecutive slots of one region and merged there afterwards; the merged row
+  // is never longer than the region (plus 16 bytes for a meta byte).
+  struct SaltGroup { size_t rd_index; std::vector<int64_t> rows; };
+  std::vector<SaltGroup> salt;
   uint64_t qtot = 0, vtot = 0;
   for (int64_t i = 0; i < NS; i++) {
     const int64_t s = order[i];
@@ -1510,23 +1516,34 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
       else if (rstate[r] != 0) rows.push_back(r);
     }
     std::stable_sort(rows.begin(), rows.end(), [&](int64_t x, int64_t y) { return cb->row_base_time[x] < cb->row_base_time[y]; });
-    for (size_t k = 1; k < rows.size(); k++)
-      if (cb->row_base_time[rows[k]] == cb->row_base_time[rows[k - 1]])
-        return fail(TSDB_E_NOT_IMPLEMENTED, "two rows of one series with the same base time (salt buckets): load compacted cells with tsdbhip_load");
-    for (int64_t r : rows) {
+    for (size_t k0 = 0; k0 < rows.size();) {
+      size_t k1 = k0 + 1;
+      while (k1 < rows.size() && cb->row_base_time[rows[k1]] == cb->row_base_time[rows[k0]]) k1++;
       RowDesc d{};
-      d.base = cb->row_base_time[r];
-      if (rq[r] > 0xFFFFFFFFLL || rv[r] > 0xFFFFFFFFLL) return fail(TSDB_E_ILLEGAL_ARGUMENT, "row too large");
-      d.qlen = (uint32_t)rq[r];
-      d.vlen = (uint32_t)rv[r];
+      d.base = cb->row_base_time[rows[k0]];
       d.qoff = qtot;
       d.voff = vtot;
-      rdq[r] = (int64_t)qtot;
-      rdv[r] = (int64_t)vtot;
-      qtot += align16(rq[r]);
-      vtot += align16(rv[r]);
+      uint64_t ql = 0, vl = 0;
+      for (size_t k = k0; k < k1; k++) {
+        const int64_t r = rows[k];
+        if (rq[r] > 0xFFFFFFFFLL || rv[r] > 0xFFFFFFFFLL) return fail(TSDB_E_ILLEGAL_ARGUMENT, "row too large");
+        rdq[r] = (int64_t)qtot;
+        rdv[r] = (int64_t)vtot;
+        qtot += align16(rq[r]);
+        vtot += align16(rv[r]);
+        ql += rq[r];
+        vl += rv[r];
+      }
+      if (ql > 0xFFFFFFFFull || vl > 0xFFFFFFFFull) return fail(TSDB_E_ILLEGAL_ARGUMENT, "row too large");
+      d.qlen = (uint32_t)rq[rows[k0]];
+      d.vlen = (uint32_t)rv[rows[k0]];
+      if (k1 - k0 > 1) {
+        vtot += 16;   // the merged cell's meta byte (two single-datapoint cells become a compacted one)
+        salt.push_back({rd.size(), std::vector<int64_t>(rows.begin() + k0, rows.begin() + k1)});
+      }
       if (rd.size() == (size_t)srp[i]) d.flags |= ROW_SFIRST;
       rd.push_back(d);
+      k0 = k1;
     }
     srp[i + 1] = (int64_t)rd.size();
   }
@@ -1552,6 +1569,27 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   HIP_OK(cmp_write(p, c->stream));
   HIP_OK(hipEventRecord(c->ev[1], c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
+  for (const SaltGroup& sg : salt) {   // RowSeq.addRow of each later row, in scan order
+    std::vector<uint8_t> lq, lv, q2, v2;
+    bool ok = true;
+    for (size_t k = 0; k < sg.rows.size() && ok; k++) {
+      const int64_t r = sg.rows[k];
+      std::vector<uint8_t>& tq = k ? q2 : lq;
+      std::vector<uint8_t>& tv = k ? v2 : lv;
+      tq.resize(rq[r]);
+      tv.resize(rv[r]);
+      if (rq[r]) HIP_OK(hipMemcpy(tq.data(), c->qual.as<uint8_t>() + rdq[r], rq[r], hipMemcpyDeviceToHost));
+      if (rv[r]) HIP_OK(hipMemcpy(tv.data(), c->val.as<uint8_t>() + rdv[r], rv[r], hipMemcpyDeviceToHost));
+      if (k) ok = merge_cells(lq, lv, q2.data(), q2.size(), v2.data(), v2.size());
+    }
+    if (!ok)
+      return fail(TSDB_E_NOT_IMPLEMENTED, "salt-bucket rows of one series whose compacted cells do not merge (RowSeq.addRow)");
+    RowDesc& d = rd[sg.rd_index];
+    if (!lq.empty()) HIP_OK(hipMemcpy(c->qual.as<uint8_t>() + d.qoff, lq.data(), lq.size(), hipMemcpyHostToDevice));
+    if (!lv.empty()) HIP_OK(hipMemcpy(c->val.as<uint8_t>() + d.voff, lv.data(), lv.size(), hipMemcpyHostToDevice));
+    d.qlen = (uint32_t)lq.size();
+    d.vlen = (uint32_t)lv.size();
+  }
   float t_a = 0, t_w = 0;   // device spans; the host layout between them is not counted
   (void)hipEventElapsedTime(&t_a, c->ev[0], c->ev[2]);
   (void)hipEventElapsedTime(&t_w, c->ev[3], c->ev[1]);

@@ -232,3 +232,43 @@ def test_shuffled_single_cells_at_scale(eng):
     eng.load(got)
     b = eng.run(q)
     assert_groups_match(a, b, "sum", tol=0.0)
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_salt_bucket_rows_merge(eng, seed):
+    """Two or three scanned rows of one series with the same base time (one per salt bucket):
+    each is compacted, then Span.addRow merges the later ones into the first (RowSeq.addRow,
+    src/core/Span.java:202-219).  The resident rows equal tsdbhip_load's host merge of the
+    oracle's compactions, and the queries equal the oracle's over those rows."""
+    rng = np.random.default_rng(seed)
+    series, groups, spans = [], [], []
+    for s in range(30):
+        rows, rr = [], []
+        for h in range(int(rng.integers(1, 3))):
+            base = B + 3600 * h
+            for _ in range(int(rng.integers(1, 4))):   # salt buckets holding this hour
+                cols = random_row(rng, int(rng.integers(1, 40)), dup_p=0.0)
+                rows.append((base, cols))
+                c = O.compact_row([(q, v) for q, v, _ in cols], True, [t for _, _, t in cols])
+                if c is not None:
+                    rr.append((base, c[0], c[1]))
+        series.append(rows)
+        spans.append((s, rr))
+        groups.append(s % 3)
+    order = np.argsort(groups, kind="stable")
+    series = [series[i] for i in order]
+    spans = [(k, spans[i][1]) for k, i in enumerate(order)]
+    groups = [groups[i] for i in order]
+    cb = abi.HostCellBatch.from_rows(series, groups, True)
+    eng.load_cells(cb)
+    got = rows_of(eng.download())
+    ref = make_batch(spans, groups)
+    eng.load(ref)   # the host merge of tsdbhip_load (RowSeq.addRow restated, pinned by TestRowSeq)
+    assert got == rows_of(eng.download())
+    eng.load_cells(cb)
+    for agg, ds in (("sum", "1m-avg"), ("max", "10m-max"), ("none", None), ("zimsum", None)):
+        q = abi.new_query(B, B + 2 * 3600, agg)
+        if ds:
+            d = O.parse_downsample(ds)
+            q.ds_function, q.ds_interval_ms = d.ds_function, d.ds_interval_ms
+        assert_groups_match(eng.run(q), O.run_query(ref, q), agg, ctx=f"salt {agg} {ds}")
