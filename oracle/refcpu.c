@@ -188,6 +188,14 @@ static int cmp_double(const void* a, const void* b) {
   double x = *(const double*)a, y = *(const double*)b;
   return x < y ? -1 : (x > y ? 1 : 0);
 }
+/* Double.compareTo (Collections.sort of a List<Double>): -0.0 before 0.0 (NaNs are dropped) */
+static int cmp_double_total(const void* a, const void* b) {
+  double x = *(const double*)a, y = *(const double*)b;
+  if (x < y) return -1;
+  if (x > y) return 1;
+  const int sx = signbit(x) != 0, sy = signbit(y) != 0;
+  return sx == sy ? 0 : (sx ? -1 : 1);
+}
 
 /* commons-math3 3.4.1 Percentile.evaluate with EstimationType LEGACY / R_3 / R_7
  * (index() and the shared estimate()); NaNs already removed by the caller. */
@@ -387,7 +395,7 @@ static double agg_run_double(int a, vals_t* v) {
       dvec c = {0};
       while (v->has(v->c)) { const double x = v->nd(v->c); if (!isnan(x)) dvec_push(&c, x); }
       if (c.n == 0) { free(c.a); return NAN; }
-      qsort(c.a, (size_t)c.n, sizeof(double), cmp_double);
+      qsort(c.a, (size_t)c.n, sizeof(double), cmp_double_total);   /* Collections.sort :428 */
       double r = c.a[c.n / 2];
       free(c.a);
       return r;

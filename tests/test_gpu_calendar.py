@@ -109,8 +109,7 @@ def test_calendar_anchored_per_span(eng, hour_batch, spec):
 
 
 @pytest.mark.parametrize("spec", ["1nc-p99", "1wc-p99-nan"])
-def test_calendar_pct_over_table_not_implemented(eng, hour_batch, spec):
+def test_calendar_pct_over_table(eng, hour_batch, spec):
+    """Percentile downsampling over a calendar slot table (k_pct's MODE_TABLE slot lookup)."""
     q = q_of(spec, T0, T0 + 3599, "sum")
-    with pytest.raises(Exception) as ei:
-        eng.run_batch(hour_batch, q)
-    assert "NotImplemented" in str(ei.value)
+    assert_groups_match(eng.run_batch(hour_batch, q), O.run_query(hour_batch, q), "sum", ctx=spec)

@@ -143,7 +143,8 @@ def test_series_shards(batch, single, world):
                 assert_groups_match(got, want[n], q_agg(q), ctx=f"series x{world} {n} vs one GPU")
             else:
                 bit_same(e.run(q), want[n], f"series x{world} {n}")
-        assert e.timing().exchange_ms > 0
+        e.run(QUERIES[0][1])
+        assert e.timing().exchange_ms > 0   # the gather + merge of the partial states
     finally:
         e.close()
 

@@ -158,7 +158,8 @@ def test_pct_extreme_selection_with_ties(eng, fn, interval):
 def test_pct_mid_ranks_key_kernel(eng, fn):
     """1 h buckets of 4-byte values through k_pct_rows' 32-bit key kernel at any rank: the
     bitwise rank search (median, p50, p75) and extraction (near the ends) on float32 rows with
-    ties, NaNs, negative values and +-0.0, and on int32 rows with few distinct values; buckets
+    ties, NaNs, negative values (and +-0.0 for the median), and on int32 rows with few distinct
+    values; buckets
     of 1..360 values (points missing at random)."""
     rng = np.random.default_rng(17)
     rows, gids = [], []
@@ -169,8 +170,10 @@ def test_pct_mid_ranks_key_kernel(eng, fn):
         if s % 2 == 0:
             f = np.round(rng.normal(0, 20, n) * 2) / 2
             f[rng.random(n) < 0.1] = np.nan
-            f[rng.random(n) < 0.05] = -0.0
-            f[rng.random(n) < 0.05] = 0.0
+            if fn == "median":   # Collections.sort orders -0.0 before 0.0; commons-math's
+                # KthSelector leaves the order of equal zeros to its partitioning (not restated)
+                f[rng.random(n) < 0.05] = -0.0
+                f[rng.random(n) < 0.05] = 0.0
             rows.append(synth.encode_rows(ts, np.zeros(n, np.int64), f, np.full(n, 1), np.zeros(n, bool)))
         else:
             lv = rng.integers(40000, 40006, n) * (1 if s % 3 else -1)
