@@ -231,3 +231,29 @@ def test_gpu_topn_no_point_in_range_raises(eng):
     assert e.value.java == "NullPointerException"
     with pytest.raises(OX.OracleExprError):
         OX.highest([[(1000, 5)], [(2000, 7)]], 1, 5000, 9000)
+
+
+def test_gpu_nested_expression_tree(eng):
+    """Expressions.parse + ExpressionTree.evaluate (opentsdb_amd/expression_tree.py) over the GPU
+    functions: scale(absolute(sum:a),, 2) and movingAverage(scale(sum:a,, 3),, 4) against the
+    oracle's functions composed the same way; sumSeries over two metric queries."""
+    from opentsdb_amd import expression_tree as T
+    rng = np.random.default_rng(99)
+    raw = [rand_series(rng, 80, "int"), rand_series(rng, 70, "dbl")]
+    raw_b = [rand_series(rng, 70, "dbl")]   # as long as a's last series (positional join)
+    results = [[X.Series.of(p) for p in raw], [X.Series.of(p) for p in raw_b]]
+    t0, t1 = raw[0][3][0], raw[0][70][0]
+    mq = []
+    tree = T.parse("scale(absolute(sum:a),, 2)", mq, (t0, t1))
+    assert mq == ["sum:a"] and str(tree) == "scale(absolute(a))"
+    got = [list(zip([int(t) for t in s.ts], s.values())) for s in tree.evaluate(eng, results)]
+    inner = [o for o, _ in OX.absolute([(p, b"") for p in raw])]
+    same(got, [o for o, _ in OX.scale([(p, b"") for p in inner], 2.0)])
+    tree = T.parse("movingAverage(scale(sum:a,, 3),, 4)", [], (t0, t1))
+    got = [list(zip([int(t) for t in s.ts], s.values())) for s in tree.evaluate(eng, results)]
+    inner = [o for o, _ in OX.scale([(p, b"") for p in raw], 3.0)]
+    same(got, [o for o, _ in OX.moving_average([(p, b"") for p in inner], 4, False, t0, t1)])
+    [tree] = T.parse_expressions(["sumSeries(sum:a, sum:b)"], (t0, t1), [])
+    got = [list(zip([int(t) for t in s.ts], s.values())) for s in tree.evaluate(eng, results)]
+    want = [o for o, _ in OX.combine("+", {"a": [(p, b"") for p in raw], "b": [(p, b"") for p in raw_b]})]
+    same(got, want)
