@@ -826,11 +826,33 @@ __device__ __forceinline__ double unkey32(uint32_t k, bool isf) {
   return (double)__uint_as_float((k & 0x80000000u) ? (k ^ 0x80000000u) : ~k);
 }
 
-// Key of rank `target` (0-based, ascending) among the wave's 512 keys (absent = 0, counted
-// first): a bitwise binary search -- per bit one compare per key and a ballot count, all on the
-// scalar unit -- starting below the prefix every present key shares.  Mid-rank statistics
-// (median, p50, p75) take it instead of popping ~n/2 wave maxima.
-__device__ __forceinline__ uint32_t kth_key32(const uint32_t key[DPL], int target) {
+// keys of the lane (sorted descending) below t: the keys >= t are a prefix, found by a
+// branch-free binary search over the 8 keys
+__device__ __forceinline__ int lane_below(const uint32_t key[DPL], uint32_t t) {
+  const bool c4 = key[3] >= t;
+  int ge = c4 ? 4 : 0;
+  const bool c2 = (c4 ? key[5] : key[1]) >= t;
+  ge += c2 ? 2 : 0;
+  const uint32_t x = c4 ? (c2 ? key[6] : key[4]) : (c2 ? key[2] : key[0]);
+  ge += x >= t ? 1 : 0;
+  if (key[7] >= t) ge = 8;   // (the search above resolves 0..7)
+  return DPL - ge;
+}
+
+__device__ __forceinline__ uint32_t next_key32(const uint32_t key[DPL], uint32_t k0, int target);
+
+// Keys of rank `target` and `target + 1` (0-based, ascending; k1 only when want1) among the
+// wave's 512 keys (absent = 0, counted first; each lane's 8 keys sorted descending).  Mid-rank
+// statistics (median, p50, p75) take it instead of popping ~n/2 wave maxima.
+// Phase 1, a bitwise binary search over the key bits below the prefix every present key
+// shares, narrows [ans, ans + 2^b) until it holds <= 64 keys (the counts below both ends come
+// free with each step).  Phase 2 compacts those keys one per lane through the wave's LDS row and
+// finishes the remaining bits with one compare + ballot each.  (The kernel is VALU-bound -- r03h
+// PMC: VALU issue ~100 % of SIMD cycles -- and phase 2's bits cost 1 VALU instead of ~16.)
+__device__ __forceinline__ void kth_pair32(const uint32_t key[DPL], int target, bool want1, uint32_t& k0,
+                                           uint32_t& k1) {
+  __shared__ uint32_t cand_lds[4][64];
+  uint32_t* cand_row = cand_lds[threadIdx.x >> 6];
   uint32_t kand = ~0u, kor = 0u;
 #pragma unroll
   for (int j = 0; j < DPL; j++) {
@@ -844,17 +866,53 @@ __device__ __forceinline__ uint32_t kth_key32(const uint32_t key[DPL], int targe
   kand = (uint32_t)__builtin_amdgcn_readfirstlane((int)kand);
   kor = (uint32_t)__builtin_amdgcn_readfirstlane((int)kor);
   const uint32_t diff = kand ^ kor;
-  if (diff == 0) return kand;   // every present key equal
-  const int top = 31 - __clz((int)diff);
-  uint32_t ans = top == 31 ? 0u : (kand & ~((2u << top) - 1u));
-  for (int b = top; b >= 0; b--) {
-    const uint32_t t = ans | (1u << b);
-    int cnt = 0;
+  if (diff == 0) { k0 = k1 = kand; return; }   // every present key equal
+  int b = 32 - __clz((int)diff);   // width of the open interval [ans, ans + 2^b)
+  uint32_t ans = b == 32 ? 0u : (kand & ~((1u << b) - 1u));
+  // count of keys below ans / below ans + 2^b (zeros below every present key)
+  int lowc = 0, highc = 64 * DPL;
 #pragma unroll
-    for (int j = 0; j < DPL; j++) cnt += __popcll(__ballot(key[j] < t));
-    if (cnt <= target) ans = t;
+  for (int j = 0; j < DPL; j++) lowc += __popcll(__ballot(key[j] == 0));
+  while (b > 0 && highc - lowc > 64) {
+    b--;
+    const uint32_t t = ans | (1u << b);
+    const int c = __builtin_amdgcn_readlane(wave_incl_sum_dpp(lane_below(key, t)), 63);
+    if (c <= target) { ans = t; lowc = c; } else { highc = c; }
   }
-  return ans;
+  if (b == 0) {   // more than 64 keys equal ans
+    k0 = ans;
+    k1 = want1 ? next_key32(key, ans, target) : ans;
+    return;
+  }
+  const uint32_t span = b == 32 ? ~0u : (1u << b) - 1u;   // keys in the interval: key - ans <= span
+  int m = 0;
+#pragma unroll
+  for (int j = 0; j < DPL; j++) m += (key[j] != 0 && key[j] - ans <= span) ? 1 : 0;
+  int pos = wave_incl_sum_dpp(m) - m;
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    if (key[j] != 0 && key[j] - ans <= span) cand_row[pos++] = key[j];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int M = highc - lowc;
+  const bool live = lane_id() < M;
+  const uint32_t c = live ? cand_row[lane_id()] : ~0u;
+  __builtin_amdgcn_wave_barrier();
+  const int t2 = target - lowc;   // rank among the candidates
+  while (b > 0) {
+    b--;
+    const uint32_t t = ans | (1u << b);
+    const int cnt = __popcll(__ballot(live && c < t));
+    if (cnt <= t2) ans = t;
+  }
+  k0 = ans;
+  if (!want1) { k1 = ans; return; }
+  if (__popcll(__ballot(live && c <= ans)) > t2 + 1) { k1 = ans; return; }
+  if (t2 + 1 < M) { k1 = ~wave_max_u32(live && c > ans ? ~c : 0u); return; }
+  k1 = next_key32(key, ans, target);   // rank target + 1 lies above the interval
 }
 
 // The key of rank target + 1 given k0 = the key of rank target.
@@ -873,7 +931,7 @@ __device__ __forceinline__ uint32_t next_key32(const uint32_t key[DPL], uint32_t
 // The statistic of a one-bucket row of 4-byte values; 0 = not this path's case (mixed float /
 // int row): the caller hands the series to k_pct.  Near the ends the k largest / smallest keys
 // are popped (topk_u32); mid ranks take the bitwise search.
-template <int QW>
+template <int QW, bool MID>
 __device__ __forceinline__ int pct_row_keys(const GridParams& p, const RowLite& d, const RawT<QW, 4>& rw, double q,
                                             double& x) {
   const int i0 = lane_id() * DPL;
@@ -911,18 +969,25 @@ __device__ __forceinline__ int pct_row_keys(const GridParams& p, const RowLite& 
     x = (double)NAN;
     return 1;
   }
-  // select_sorted: Median.runDouble sorted[n / 2]; PercentileAgg LEGACY pos = p (n + 1)
-  int64_t r0, r1;
-  sel_ranks(p.sel_fn, n, r0, r1);
-  const int lo_i = (int)r0, hi_i = r1 < 0 ? (int)r0 : (int)r1;
-  const double pos = q * (double)(n + 1);   // (percentiles only: the interpolation weight)
+  // select_sorted: PercentileAgg LEGACY pos = p (n + 1); Median.runDouble sorted[n / 2]
+  const double pos = q * (double)(n + 1);
+  int lo_i, hi_i;
+  if (MID && p.sel_fn == TSDB_AGG_MEDIAN) { lo_i = hi_i = n / 2; }
+  else {
+    const int ip = (int)floor(pos);
+    if (pos < 1) { lo_i = hi_i = 0; }
+    else if (pos >= (double)n) { lo_i = hi_i = n - 1; }
+    else { lo_i = ip - 1; hi_i = ip; }
+  }
   const int ktop = n - lo_i, kbot = hi_i + 1;
   double a, b;
   uint32_t ek, ek1;
   if (min(ktop, kbot) > EXT_MAX) {
+    if constexpr (!MID) return 0;   // (the near-end variant keeps its registers for the extraction)
+    sort8_desc(key);
     const int zeros = 64 * DPL - n;
-    const uint32_t k0 = kth_key32(key, zeros + lo_i);
-    const uint32_t k1 = hi_i == lo_i ? k0 : next_key32(key, k0, zeros + lo_i);
+    uint32_t k0, k1;
+    kth_pair32(key, zeros + lo_i, hi_i != lo_i, k0, k1);
     a = unkey32(k0, wf);
     b = unkey32(k1, wf);
   } else if (ktop <= kbot) {
@@ -942,7 +1007,7 @@ __device__ __forceinline__ int pct_row_keys(const GridParams& p, const RowLite& 
 
 // one in-range row: its buckets' order statistics into dense / pres; false = hand the
 // series back (offset >= 1 h, or a statistic more than EXT_MAX from both ends)
-template <int QW, int VL, bool KEYS>
+template <int QW, int VL, int KEYS>
 __device__ __forceinline__ bool pct_row(const GridParams& p, const RowLite& cd, const RawT<QW, VL>& rc, double q,
                                         double* dense, uint8_t* pres) {
   const int lane = lane_id();
@@ -959,7 +1024,7 @@ __device__ __forceinline__ bool pct_row(const GridParams& p, const RowLite& cd, 
     if constexpr (VL == 4) {
       if (d.ndp == 0) return true;
       double x;
-      const int r = pct_row_keys<QW>(p, d, rc, q, x);
+      const int r = pct_row_keys<QW, KEYS == 2>(p, d, rc, q, x);
       if (r <= 0) return false;
       if (lane == 0) { dense[slot0] = x; pres[slot0] = 1; }
       return true;
@@ -1012,7 +1077,9 @@ __device__ __forceinline__ bool pct_row(const GridParams& p, const RowLite& cd, 
   }
 }
 
-template <int QW, int VL, int D, bool KEYS>
+// KEYS: 0 = extraction over doubles; 1 = the 32-bit key kernel, statistics near the ends;
+// 2 = the key kernel ranking any statistic (median, p50, p75: the bitwise rank search)
+template <int QW, int VL, int D, int KEYS>
 __global__ __launch_bounds__(256, KEYS ? PCT_KEYS_OCC : 1) void k_pct_rows(GridParams p) {
   const int lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1721,7 +1788,9 @@ hipError_t launch_sel_seg(const SelParams& p, hipStream_t s, int64_t maxn) {
     // 11.4 vs 13.3 ms per step
     const char* oenv = std::getenv("TSDBHIP_SEL_OCC");
     const char* senv = std::getenv("TSDBHIP_SEL_SLOTS");   // slots per block (1: k_sel_reg)
-    const int sl = senv ? std::atoi(senv) : 2;
+    // 2 slots a block halves the row-line reads but measured slower on config 3 p99 (11.4 vs
+    // 10.4 ms per step, profiles/r03g): the selection, not the L2, is the limit
+    const int sl = senv ? std::atoi(senv) : 1;
     if (!p.cols && sl == 2) {
       const int64_t per2 = (p.G * ((p.K + 1) / 2) + 7) / 8;
       // one block per CU without spills (122 VGPRs); TSDBHIP_SEL_OCC=8 forces two (spilling)
@@ -1749,17 +1818,20 @@ hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s) {
   const int D = denv ? std::atoi(denv) : (vl == 4 && p.I == 3600000 ? 2 : 3);
   // 1 h buckets of 4-byte values: the 32-bit key kernel (its misses go to k_pct)
   const bool keys = vl == 4 && p.I == 3600000 && !(std::getenv("TSDBHIP_PCT_KEYS") && std::getenv("TSDBHIP_PCT_KEYS")[0] == '0');
+  const int sel_i = (p.sel_fn - TSDB_AGG_P999) % 6;
+  const bool mid = p.sel_fn == TSDB_AGG_MEDIAN || sel_i >= 4;   // median, p75, p50 (and their ep* forms)
 #define PCT_ROWS_CASE(Q, V)                                                                                  \
   if (qw == Q && vl == V) {                                                                                \
     if (V == 4 && keys) {                                                                                  \
-      if (D == 2) hipLaunchKernelGGL((k_pct_rows<Q, V, 2, true>), grid, block, 0, s, p);                   \
-      else if (D == 4) hipLaunchKernelGGL((k_pct_rows<Q, V, 4, true>), grid, block, 0, s, p);              \
-      else hipLaunchKernelGGL((k_pct_rows<Q, V, 3, true>), grid, block, 0, s, p);                          \
+      if (mid) hipLaunchKernelGGL((k_pct_rows<Q, V, 2, 2>), grid, block, 0, s, p);                        \
+      else if (D == 2) hipLaunchKernelGGL((k_pct_rows<Q, V, 2, 1>), grid, block, 0, s, p);                 \
+      else if (D == 4) hipLaunchKernelGGL((k_pct_rows<Q, V, 4, 1>), grid, block, 0, s, p);                 \
+      else hipLaunchKernelGGL((k_pct_rows<Q, V, 3, 1>), grid, block, 0, s, p);                             \
       return hipGetLastError();                                                                            \
     }                                                                                                      \
-    if (D == 2) hipLaunchKernelGGL((k_pct_rows<Q, V, 2, false>), grid, block, 0, s, p);                    \
-    else if (D == 4) hipLaunchKernelGGL((k_pct_rows<Q, V, 4, false>), grid, block, 0, s, p);               \
-    else hipLaunchKernelGGL((k_pct_rows<Q, V, 3, false>), grid, block, 0, s, p);                           \
+    if (D == 2) hipLaunchKernelGGL((k_pct_rows<Q, V, 2, 0>), grid, block, 0, s, p);                        \
+    else if (D == 4) hipLaunchKernelGGL((k_pct_rows<Q, V, 4, 0>), grid, block, 0, s, p);                   \
+    else hipLaunchKernelGGL((k_pct_rows<Q, V, 3, 0>), grid, block, 0, s, p);                               \
     return hipGetLastError();                                                                              \
   }
   PCT_ROWS_CASE(2, 1) PCT_ROWS_CASE(2, 2) PCT_ROWS_CASE(2, 4) PCT_ROWS_CASE(2, 8)

@@ -235,7 +235,7 @@ def test_gpu_topn_no_point_in_range_raises(eng):
 
 def test_gpu_nested_expression_tree(eng):
     """Expressions.parse + ExpressionTree.evaluate (opentsdb_amd/expression_tree.py) over the GPU
-    functions: scale(absolute(sum:a),, 2) and movingAverage(scale(sum:a,, 3),, 4) against the
+    functions: scale(absolute(sum:a),, 2) and movingAverage(scale(sum:a,,3),, 4) against the
     oracle's functions composed the same way; sumSeries over two metric queries."""
     from opentsdb_amd import expression_tree as T
     rng = np.random.default_rng(99)
@@ -249,7 +249,8 @@ def test_gpu_nested_expression_tree(eng):
     got = [list(zip([int(t) for t in s.ts], s.values())) for s in tree.evaluate(eng, results)]
     inner = [o for o, _ in OX.absolute([(p, b"") for p in raw])]
     same(got, [o for o, _ in OX.scale([(p, b"") for p in inner], 2.0)])
-    tree = T.parse("movingAverage(scale(sum:a,, 3),, 4)", [], (t0, t1))
+    tree = T.parse("movingAverage(scale(sum:a,,3),, 4)", [], (t0, t1))   # (a space inside a nested
+    # call ends the parameter: ExpressionReader.readNextParameter stops at whitespace)
     got = [list(zip([int(t) for t in s.ts], s.values())) for s in tree.evaluate(eng, results)]
     inner = [o for o, _ in OX.scale([(p, b"") for p in raw], 3.0)]
     same(got, [o for o, _ in OX.moving_average([(p, b"") for p in inner], 4, False, t0, t1)])

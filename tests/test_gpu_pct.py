@@ -160,14 +160,17 @@ def test_pct_mid_ranks_key_kernel(eng, fn):
     bitwise rank search (median, p50, p75) and extraction (near the ends) on float32 rows with
     ties, NaNs, negative values (and +-0.0 for the median), and on int32 rows with few distinct
     values; buckets
-    of 1..360 values (points missing at random)."""
+    of 1..360 values (points missing at random), and rows of distinct values."""
     rng = np.random.default_rng(17)
     rows, gids = [], []
-    for s in range(14):
+    for s in range(20):
         keep = rng.random(3 * 360) < (0.9 if s % 5 else 0.01)
         ts = T0 * 1000 + np.flatnonzero(keep).astype(np.int64) * 10000
         n = len(ts)
-        if s % 2 == 0:
+        if s >= 14:   # distinct values: the rank search's candidate set ends at any rank
+            f = rng.normal(0, 1e3, n) * (1 + s)
+            rows.append(synth.encode_rows(ts, np.zeros(n, np.int64), f, np.full(n, 1), np.zeros(n, bool)))
+        elif s % 2 == 0:
             f = np.round(rng.normal(0, 20, n) * 2) / 2
             f[rng.random(n) < 0.1] = np.nan
             if fn == "median":   # Collections.sort orders -0.0 before 0.0; commons-math's
@@ -179,7 +182,7 @@ def test_pct_mid_ranks_key_kernel(eng, fn):
             lv = rng.integers(40000, 40006, n) * (1 if s % 3 else -1)
             rows.append(synth.encode_rows(ts, lv, np.zeros(n), np.zeros(n, np.int64), np.zeros(n, bool)))
         gids.append(s % 3)
-    order = sorted(range(14), key=lambda i: gids[i])
+    order = sorted(range(20), key=lambda i: gids[i])
     b = synth.from_series([rows[i] for i in order], [gids[i] for i in order])
     for agg in ["max", "min", "count"]:
         q = abi.new_query(T0, T0 + 3 * 3600 - 1, agg, ds_function=abi.AGG[fn], ds_interval_ms=3600000)

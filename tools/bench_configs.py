@@ -154,6 +154,7 @@ def main():
             step = sum(ms) / len(ms)
             print(json.dumps({"config": 3, "query": "run_multi " + ",".join(qs), "series": series, "groups": groups,
                               "datapoints": int(tm.datapoints), "ms_per_step": step,
+                              "fused_queries": int(tm.fused_queries), "fast_ms": tm.fast_ms, "total_ms": tm.total_ms,
                               "separate_queries_note": "compare with the per-query ms_per_step lines",
                               "datapoints_per_s_per_query": tm.datapoints * len(ql) / (step / 1000)}), flush=True)
         else:
