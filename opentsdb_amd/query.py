@@ -191,6 +191,7 @@ class DataPoints:
 
 
 UNSET = -1
+ROLLUP_USAGES = ("ROLLUP_RAW", "ROLLUP_NOFALLBACK", "ROLLUP_FALLBACK", "ROLLUP_FALLBACK_RAW")
 
 
 class TsdbQuery:
@@ -211,6 +212,13 @@ class TsdbQuery:
         self.rate_options = RateOptions()
         self.downsampler: DownsamplingSpecification | None = None
         self.flags = 0
+        self.rollup_usage = "ROLLUP_NOFALLBACK"   # TsdbQuery.java:150
+
+    def setRollupUsage(self, usage: str | None):
+        """TSSubQuery.setRollupUsage / ROLLUP_USAGE.parse (TsdbQuery.java:207-222): an unknown
+        name means ROLLUP_NOFALLBACK."""
+        u = (usage or "").upper()
+        self.rollup_usage = u if u in ROLLUP_USAGES else "ROLLUP_NOFALLBACK"
 
     # TsdbQuery.java:262-319
     def setStartTime(self, timestamp: int):
@@ -306,33 +314,14 @@ class TsdbQuery:
             e = end + (3600 - end % 3600)
         return s, e
 
-    def _best_rollup(self):
-        """getRollupInterval's best match for the downsampling interval, or None."""
-        ds = self.downsampler
-        if self.rollups is None or ds is None or ds.interval <= 0:
-            return None
-        from .rollup_read import NoSuchRollupForIntervalException
-        try:
-            return self.rollups.config.getRollupInterval(ds.interval // 1000)[0]
-        except NoSuchRollupForIntervalException:
-            return None
-
     def rollup_interval_name(self):
         """transformDownSamplerToRollupQuery (TsdbQuery.java:1665-1700): the best-match rollup
         table of the downsampling interval, or None (a raw scan) -- also when the best match is
         the default interval, the raw table itself (:1694-1697)."""
-        name = self._best_rollup()
-        if name is not None and self.rollups.config.isDefaultInterval(name):
+        best = self._best_rollups()
+        if not best or self.rollups.config.isDefaultInterval(best[0]):
             return None
-        return name
-
-    def _raw_aggregator_override(self):
-        """A count group-by becomes sum as soon as a rollup query is built (:1681-1683), before
-        the default-interval check drops that query: the raw scan then aggregates with sum."""
-        name = self._best_rollup()
-        if name is not None and self.rollups.config.isDefaultInterval(name) and self.aggregator == "count":
-            return "sum"
-        return None
+        return best[0]
 
     def _filters(self):
         """Tag filters and group-by tag uids of setTimeSeries' tags (None: no series match)."""
@@ -440,27 +429,38 @@ class TsdbQuery:
             gids = [index.get(k, -1) for k in key_of]
         return make_batch(spans, gids), keys
 
-    def run(self):
-        """TsdbQuery.run(): DataPoints[] of the query (one per SpanGroup)."""
-        rname = self.rollup_interval_name()
-        if rname is not None:
-            rb, keys = self.build_rollup_batch(rname)
-            q = self.to_abi()
-            runner = self.rollup_runner
-            if runner is None:
-                from .engine import default_engine
-                runner = default_engine().run_rollup_batch
-            if rb.cells.n_series == 0:
-                return []
-            out = []
-            for gid, ts, bits, isi in runner(rb, q):
-                key = keys[gid] if (self.aggregator != "none" and 0 <= gid < len(keys)) else ()
-                out.append(DataPoints(gid, ts, bits, isi, self.metric, key))
-            return out
+    def _best_rollups(self):
+        """getRollupInterval's match list for the downsampling interval, best first ([] = none;
+        ROLLUP_RAW never builds a rollup query, TsdbQuery.java:480-483)."""
+        ds = self.downsampler
+        if self.rollups is None or ds is None or ds.interval <= 0 or self.rollup_usage == "ROLLUP_RAW":
+            return []
+        from .rollup_read import NoSuchRollupForIntervalException
+        try:
+            return list(self.rollups.config.getRollupInterval(ds.interval // 1000))
+        except NoSuchRollupForIntervalException:
+            return []
+
+    def _run_rollup(self, name):
+        rb, keys = self.build_rollup_batch(name)
+        q = self.to_abi()
+        runner = self.rollup_runner
+        if runner is None:
+            from .engine import default_engine
+            runner = default_engine().run_rollup_batch
+        if rb.cells.n_series == 0:
+            return []
+        out = []
+        for gid, ts, bits, isi in runner(rb, q):
+            key = keys[gid] if (self.aggregator != "none" and 0 <= gid < len(keys)) else ()
+            out.append(DataPoints(gid, ts, bits, isi, self.metric, key))
+        return out
+
+    def _run_raw(self, aggregator_override):
         batch, keys = self.build_batch()
         q = self.to_abi()
-        if self._raw_aggregator_override():
-            q.aggregator = abi.AGG[self._raw_aggregator_override()]
+        if aggregator_override:
+            q.aggregator = abi.AGG[aggregator_override]
         runner = self.runner
         if runner is None:
             from .engine import default_engine
@@ -473,3 +473,48 @@ class TsdbQuery:
             key = keys[gid] if (self.aggregator != "none" and 0 <= gid < len(keys)) else ()
             out.append(DataPoints(gid, ts, bits, isi, self.metric, key))
         return out
+
+    def _rollup_to_downsampler(self, name):
+        """transformRollupQueryToDownSampler (TsdbQuery.java:1706-1717): the raw scan downsamples
+        at the failed rollup table's interval with the rollup aggregator (zimsum / mimmax /
+        mimmin read as sum / max / min, RollupQuery.java:69-80)."""
+        from .rollup_read import normalize_agg
+        ds = self.downsampler
+        self.downsampler = DownsamplingSpecification(
+            interval=self.rollups.config.intervals[name].interval_s * 1000,
+            function=normalize_agg(ds.function), fill_policy=ds.fill_policy if ds else "zero")
+
+    def run(self):
+        """TsdbQuery.run(): DataPoints[] of the query (one per SpanGroup).  With a rollup config
+        the downsampler becomes a rollup query on the best-match table
+        (transformDownSamplerToRollupQuery, :1665-1700; a count group-by turns into sum there);
+        the default interval is the raw table.  Under ROLLUP_FALLBACK / ROLLUP_FALLBACK_RAW an
+        empty result re-runs on the next best match or on raw data
+        (FallbackRollupOnEmptyResult, :1293-1354).  The query's downsampler is restored after."""
+        best = self._best_rollups()
+        if not best:
+            return self._run_raw(None)
+        override = "sum" if self.aggregator == "count" else None
+        cur = best.pop(0)
+        if self.rollups.config.isDefaultInterval(cur):
+            return self._run_raw(override)
+        saved = self.downsampler
+        try:
+            while True:
+                out = self._run_rollup(cur)
+                if out or self.rollup_usage not in ("ROLLUP_FALLBACK", "ROLLUP_FALLBACK_RAW"):
+                    return out
+                if self.rollup_usage == "ROLLUP_FALLBACK_RAW":
+                    self._rollup_to_downsampler(cur)
+                    return self._run_raw(override)
+                if not best:
+                    return []
+                nxt = best.pop(0)
+                if self.rollups.config.isDefaultInterval(nxt):
+                    self._rollup_to_downsampler(cur)
+                    return self._run_raw(override)
+                # (the next table's interval divides the sample interval: the downsampler keeps
+                # its interval, :1331-1340)
+                cur = nxt
+        finally:
+            self.downsampler = saved

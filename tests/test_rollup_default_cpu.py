@@ -5,6 +5,7 @@ RollupConfig allows one default interval (src/rollup/RollupConfig.java:93-103). 
 test covers the default interval on the query path: these cases restate that code, unpinned."""
 from __future__ import annotations
 
+import numpy as np
 import pytest
 
 from opentsdb_amd import abi
@@ -74,3 +75,90 @@ def test_one_default_interval_only():
         RollupConfig(IDS, [("1m", "1h", True), ("1h", "1d", True)])
     with pytest.raises(ValueError, match="Only one interval of each type"):
         RollupConfig(IDS, [("1m", "1h"), ("1m", "1d")])
+
+
+# ---- FallbackRollupOnEmptyResult (src/core/TsdbQuery.java:1293-1354) -------------------------
+def fallback_query(intervals, filled, usage, agg="sum", ds="10m-zimsum"):
+    """Rollup tables `intervals`; only the tables in `filled` hold points.  Returns the query
+    and the list of scans it makes: ("rollup", table) / ("raw", aggregator, ds interval, ds fn)."""
+    st = MockStore()
+    for i in range(10):
+        st.add_long("sys.cpu", T0 + i * 60, i, {"host": "a"})
+    rs = RollupStore(RollupConfig(IDS, intervals), st)
+    for name in filled:
+        for a in ("sum", "count"):
+            rs.add_aggregate_point("sys.cpu", T0, 5, {"host": "a"}, name, a)
+    seen = []
+
+    def runner(batch, q):
+        seen.append(("raw", q.aggregator, q.ds_interval_ms, q.ds_function))
+        return []
+
+    def rollup_runner(rb, q):   # one group for a table with points
+        return [(0, np.array([T0 * 1000], np.int64), np.zeros(1, np.uint64), np.zeros(1, bool))]
+
+    class Q(TsdbQuery):
+        def build_rollup_batch(self, name):
+            seen.append(("rollup", name))
+            return super().build_rollup_batch(name)
+
+    q = Q(st, runner=runner, rollups=rs, rollup_runner=rollup_runner)
+    q.setStartTime(T0)
+    q.setEndTime(T0 + 3600)
+    q.setTimeSeries("sys.cpu", {"host": "*"}, agg, False)
+    q.downsample(ds)
+    q.setRollupUsage(usage)
+    return q, seen
+
+
+IVS = [("1m", "1h", True), ("5m", "1d"), ("10m", "1d")]
+
+
+def test_rollup_usage_parse():
+    q, _ = fallback_query(IVS, [], None)
+    assert q.rollup_usage == "ROLLUP_NOFALLBACK"
+    for u in ("rollup_fallback", "ROLLUP_FALLBACK_RAW", "Rollup_Raw"):
+        q.setRollupUsage(u)
+        assert q.rollup_usage == u.upper()
+    q.setRollupUsage("bogus")                       # unknown -> the default, with a warning
+    assert q.rollup_usage == "ROLLUP_NOFALLBACK"
+
+
+def test_no_fallback_returns_the_empty_rollup_result():
+    q, seen = fallback_query(IVS, [], "ROLLUP_NOFALLBACK")
+    assert q.run() == [] and seen == [("rollup", "10m")]
+
+
+def test_fallback_walks_the_best_matches_then_raw():
+    """10m and 5m empty: the next best match is the default interval, so the raw scan
+    downsamples at the failed table's interval (transformRollupQueryToDownSampler) with the
+    rollup aggregator (zimsum -> sum)."""
+    q, seen = fallback_query(IVS, [], "ROLLUP_FALLBACK", agg="count")
+    ds = q.downsampler
+    q.run()
+    assert seen == [("rollup", "10m"), ("rollup", "5m"),
+                    ("raw", abi.AGG["sum"], 300000, abi.AGG["sum"])]
+    assert q.downsampler is ds                      # (restored after the run)
+
+
+def test_fallback_stops_at_the_first_table_with_data():
+    q, seen = fallback_query(IVS, ["5m"], "ROLLUP_FALLBACK")
+    assert len(q.run()) == 1
+    assert seen == [("rollup", "10m"), ("rollup", "5m")]
+
+
+def test_fallback_raw_goes_straight_to_raw():
+    q, seen = fallback_query(IVS, [], "ROLLUP_FALLBACK_RAW", agg="count")
+    q.run()
+    assert seen == [("rollup", "10m"), ("raw", abi.AGG["sum"], 600000, abi.AGG["sum"])]
+
+
+def test_fallback_without_more_matches_is_empty():
+    q, seen = fallback_query([("10m", "1d")], [], "ROLLUP_FALLBACK")
+    assert q.run() == [] and seen == [("rollup", "10m")]
+
+
+def test_rollup_raw_usage_never_reads_rollups():
+    q, seen = fallback_query(IVS, ["10m"], "ROLLUP_RAW", agg="count")
+    q.run()
+    assert seen == [("raw", abi.AGG["count"], 600000, abi.AGG["zimsum"])]
