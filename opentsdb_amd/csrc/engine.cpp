@@ -647,6 +647,15 @@ static void release_batch(tsdbhip_ctx* c) {
   c->compact_ms = 0;
 }
 
+namespace tsdb {
+// multi.cpp: the merge context's resident state reset (a load that is not a rollup load)
+void ctx_drop_batch(tsdbhip_ctx* c) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  release_batch(c);
+}
+int64_t ctx_n_series(tsdbhip_ctx* c) { return c->n_series; }   // resident series (count series too)
+}  // namespace tsdb
+
 extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   if (!c) return;
   if (c->md) { tsdb::md_destroy(c->md); c->md = nullptr; }
@@ -1142,7 +1151,7 @@ int vle_put(std::vector<uint8_t>& out, int64_t v) {
 }  // namespace
 
 extern "C" int tsdbhip_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* rb) {
-  MD_REFUSE(c, "tsdbhip_load_rollup");
+  if (c && c->md) return tsdb::md_load_rollup(c, rb);
   if (!c || !rb) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   const tsdbhip_batch* b = &rb->cells;
   const bool cnt = rb->row_cqual_off != nullptr;
@@ -3023,6 +3032,8 @@ void record_timing(tsdbhip_ctx* c, const Plan& P, int32_t redo_n) {
 }
 
 // Dense [G][K] outputs on the device -> result (after the stream's work is queued).
+void ro_activity(const tsdbhip_ctx* c, const Plan& P, int64_t G, std::vector<uint32_t>& act);
+
 int collect(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bool timed, tsdbhip_result** out,
             const void* d_val = nullptr, const void* d_flag = nullptr) {
   std::vector<double> val(G * P.K);
@@ -3045,17 +3056,7 @@ int collect(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bo
     const int64_t S0 = P.ss * 1000, E0 = P.se * 1000;
     if (q->start_time < S0 || q->start_time > E0) std::fill(flag.begin(), flag.end(), 0);
   }
-  if (c->ro_active && c->ro_scan_valid) {
-    // rollup: a span the scan found is a SpanGroup member (or, NONE, its own SpanGroup) even
-    // when its RollupSeqs yield no datapoint; count series are no spans of the query
-    for (int64_t i = 0; i < c->n_series; i++) {
-      if (P.none) {
-        if (i < G) act[i] = c->h_orig[i] < c->ro_nval ? (act[i] | c->ro_scan_act[i]) : 0;
-      } else if (c->ro_scan_act[i] && c->h_group[i] < G) {
-        act[c->h_group[i]] = 1;
-      }
-    }
-  }
+  ro_activity(c, P, G, act);
   return assemble(c, q, P, G, val, flag, act, out);
 }
 
@@ -3664,30 +3665,28 @@ int ro_scan(tsdbhip_ctx* c, const Plan& P, bool reads_counts) {
 //      Σcount;
 //   3. the SpanGroup step (rate, fill, LERP, group-by) over those buckets (k_emit).
 // Every other downsampling function reads only the value series: the ordinary pipeline.
-int run_rollup(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
+// The query a rollup batch runs: a count group-by sums (the aggregator RollupQuery leaves).
+tsdbhip_query ro_query(const tsdbhip_ctx* c, const tsdbhip_query* q) {
+  tsdbhip_query r = *q;
+  if (c->ro_active && r.aggregator == TSDB_AGG_COUNT) r.aggregator = TSDB_AGG_SUM;
+  return r;
+}
+
+int ro_check(const tsdbhip_query* q) {
   if (q->ds_function < 0 || (!q->ds_all && q->ds_interval_ms <= 0))
     return fail(TSDB_E_ILLEGAL_ARGUMENT, "a rollup query needs a downsampling interval");
   if (q->ds_function == TSDB_AGG_DEV)
     return fail(TSDB_E_UNSUPPORTED, "Standard deviation over rolled up data is not supported at this time");
-  tsdbhip_query qr = *q;
-  if (qr.aggregator == TSDB_AGG_COUNT) qr.aggregator = TSDB_AGG_SUM;
+  return 0;
+}
+
+// The scan (ro_scan) and, for avg / count downsampling over count cells, steps 1-2 above: the
+// query's group-by step then runs over pre_dense (P.emit_only).  q is the caller's query, qr
+// ro_query(q), P planned from qr.
+int ro_stage(tsdbhip_ctx* c, const tsdbhip_query* q, const tsdbhip_query& qr, Plan& P) {
   const bool combine = c->ro_counts && (q->ds_function == TSDB_AGG_AVG || q->ds_function == TSDB_AGG_COUNT);
-  Plan P;
-  int rc = plan_query(c, &qr, P);
-  if (rc) return rc;
-  rc = ro_scan(c, P, combine);
-  if (rc) return rc;
-  const int64_t G = P.none ? c->n_series : c->n_groups;
-  if (!combine) {
-    if (P.gsel || P.ordered) {
-      rc = P.gsel ? run_sel_group(c, &qr, P, G) : run_ordered(c, &qr, P, G);
-      if (rc) return rc;
-      return collect(c, &qr, P, G, true, out);
-    }
-    rc = run_device(c, &qr, P, G, true);
-    if (rc) return rc;
-    return collect(c, &qr, P, G, true, out);
-  }
+  int rc = ro_scan(c, P, combine);
+  if (rc || !combine) return rc;
   if (P.gsel || P.ordered)
     return fail(TSDB_E_NOT_IMPLEMENTED, "avg / count rollup downsampling with a percentile group-by or the ordered flag");
   tsdbhip_query q1 = qr;
@@ -3710,6 +3709,37 @@ int run_rollup(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
   HIP_OK(launch_rollup_combine(c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->ro_cmap.as<int64_t>(),
                                c->n_series, P.K, q->ds_function == TSDB_AGG_AVG ? 1 : 0, c->stream));
   P.emit_only = true;
+  return 0;
+}
+
+// rollup: a span the scan found is a SpanGroup member (or, NONE, its own SpanGroup) even when
+// its RollupSeqs yield no datapoint; count series are no spans of the query
+void ro_activity(const tsdbhip_ctx* c, const Plan& P, int64_t G, std::vector<uint32_t>& act) {
+  if (!(c->ro_active && c->ro_scan_valid)) return;
+  for (int64_t i = 0; i < c->n_series; i++) {
+    if (P.none) {
+      if (i < G) act[i] = c->h_orig[i] < c->ro_nval ? (act[i] | c->ro_scan_act[i]) : 0;
+    } else if (c->ro_scan_act[i] && c->h_group[i] < G) {
+      act[c->h_group[i]] = 1;
+    }
+  }
+}
+
+int run_rollup(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
+  int rc = ro_check(q);
+  if (rc) return rc;
+  const tsdbhip_query qr = ro_query(c, q);
+  Plan P;
+  rc = plan_query(c, &qr, P);
+  if (rc) return rc;
+  rc = ro_stage(c, q, qr, P);
+  if (rc) return rc;
+  const int64_t G = P.none ? c->n_series : c->n_groups;
+  if (P.gsel || P.ordered) {
+    rc = P.gsel ? run_sel_group(c, &qr, P, G) : run_ordered(c, &qr, P, G);
+    if (rc) return rc;
+    return collect(c, &qr, P, G, true, out);
+  }
   rc = run_device(c, &qr, P, G, true);
   if (rc) return rc;
   return collect(c, &qr, P, G, true, out);
@@ -3991,10 +4021,11 @@ int plan_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_globa
 extern "C" int tsdbhip_partials_layout_get(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global,
                                            tsdbhip_partials_layout* out) {
   MD_REFUSE(c, "tsdbhip_partials_layout_get");
-  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_partials_layout_get over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  if (c->ro_active) { const int r = ro_check(q); if (r) return r; }
+  const tsdbhip_query qr = ro_query(c, q);
   Plan P;
-  int rc = plan_partials(c, q, n_groups_global, P);
+  int rc = plan_partials(c, &qr, n_groups_global, P);
   if (rc) return rc;
   out->n_groups = n_groups_global;
   out->n_slots = P.K;
@@ -4004,16 +4035,21 @@ extern "C" int tsdbhip_partials_layout_get(tsdbhip_ctx* c, const tsdbhip_query* 
 
 extern "C" int tsdbhip_run_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, void* partials) {
   MD_REFUSE(c, "tsdbhip_run_partials");
-  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_run_partials over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !partials) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_OK(hipSetDevice(c->device));
+  if (c->ro_active) { const int r = ro_check(q); if (r) return r; }
+  const tsdbhip_query qr = ro_query(c, q);
   Plan P;
-  int rc = plan_partials(c, q, n_groups_global, P);
+  int rc = plan_partials(c, &qr, n_groups_global, P);
   if (rc) return rc;
+  if (c->ro_active) {   // a rollup shard: its scan and (avg / count over counts) the combine pass
+    rc = ro_stage(c, q, qr, P);
+    if (rc) return rc;
+  }
   const int64_t G = n_groups_global, K = P.K;
   const PartLayout L = part_layout(G, K);
-  rc = run_device(c, q, P, c->n_groups, false);
+  rc = run_device(c, &qr, P, c->n_groups, false);
   if (rc) return rc;
   // merged per-(group, slot) states of this shard; groups this rank does not hold keep
   // the identity state (zero bytes except the min / max identities written below)
@@ -4037,7 +4073,16 @@ extern "C" int tsdbhip_run_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int6
     HIP_OK(hipMemcpyAsync(xb + c->n_groups * K * 8, ident.data(), ident.size() * 8, hipMemcpyHostToDevice, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
   }
-  if (c->n_groups) HIP_OK(hipMemcpyAsync(xb + L.off_act, c->gact.p, c->n_groups * 4, hipMemcpyDeviceToDevice, c->stream));
+  if (c->n_groups && c->ro_active) {   // + the groups of the spans the rollup scan found
+    std::vector<uint32_t> act(c->n_groups);
+    HIP_OK(hipMemcpyAsync(act.data(), c->gact.p, c->n_groups * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    ro_activity(c, P, c->n_groups, act);
+    HIP_OK(hipMemcpyAsync(xb + L.off_act, act.data(), c->n_groups * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+  } else if (c->n_groups) {
+    HIP_OK(hipMemcpyAsync(xb + L.off_act, c->gact.p, c->n_groups * 4, hipMemcpyDeviceToDevice, c->stream));
+  }
   HIP_OK(hipEventRecord(c->ev[2], c->stream));
   HIP_OK(hipMemcpyAsync(partials, xb, L.bytes, hipMemcpyDefault, c->stream));
   int32_t err = 0, redo_n = 0;
@@ -4052,11 +4097,14 @@ extern "C" int tsdbhip_run_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int6
 extern "C" int tsdbhip_finalize(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, const void* partials,
                                 int n_ranks, tsdbhip_result** out) {
   MD_REFUSE(c, "tsdbhip_finalize");
-  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_finalize over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !partials || !out || n_ranks < 1) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad argument");
   std::lock_guard<std::mutex> lk(c->mu);
   *out = nullptr;
   HIP_OK(hipSetDevice(c->device));
+  if (c->ro_active) { const int r = ro_check(q); if (r) return r; }
+  const tsdbhip_query qr0 = ro_query(c, q);
+  q = &qr0;
+  c->ro_scan_valid = false;   // the ranks' activity arrives in the partials (no local scan to add)
   Plan P;
   int rc = plan_partials(c, q, n_groups_global, P);
   if (rc) return rc;
@@ -4108,10 +4156,11 @@ int plan_sel(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, Pl
 extern "C" int tsdbhip_sel_layout(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, int64_t* counts,
                                   int64_t* n_slots) {
   MD_REFUSE(c, "tsdbhip_sel_layout");
-  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_sel_layout over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !counts || !n_slots) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  if (c->ro_active) { const int r = ro_check(q); if (r) return r; }
+  const tsdbhip_query qr = ro_query(c, q);
   Plan P;
-  int rc = plan_sel(c, q, n_groups_global, P);
+  int rc = plan_sel(c, &qr, n_groups_global, P);
   if (rc) return rc;
   const std::vector<int64_t> n = local_counts(c, n_groups_global);
   for (int64_t g = 0; g < n_groups_global; g++) counts[g] = n[g];
@@ -4122,35 +4171,46 @@ extern "C" int tsdbhip_sel_layout(tsdbhip_ctx* c, const tsdbhip_query* q, int64_
 extern "C" int tsdbhip_sel_run_values(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, void* vals,
                                       void* uni, void* act) {
   MD_REFUSE(c, "tsdbhip_sel_run_values");
-  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_sel_run_values over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !vals || !uni || !act) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_OK(hipSetDevice(c->device));
+  if (c->ro_active) { const int r = ro_check(q); if (r) return r; }
+  const tsdbhip_query qr = ro_query(c, q);
   Plan P;
-  int rc = plan_sel(c, q, n_groups_global, P);
+  int rc = plan_sel(c, &qr, n_groups_global, P);
   if (rc) return rc;
+  if (c->ro_active) {
+    rc = ro_stage(c, q, qr, P);
+    if (rc) return rc;
+  }
   const int64_t G = n_groups_global, K = P.K;
   HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
-  rc = sel_values(c, q, P, G);
+  rc = sel_values(c, &qr, P, G);
   if (rc) return rc;
-  const int64_t n = c->n_series * K;
+  int64_t n = 0;   // the grouped spans (ungrouped ones, and a rollup batch's count series, last)
+  for (int64_t x : local_counts(c, G)) n += x * K;
   if (n) HIP_OK(hipMemcpyAsync(vals, c->sel_vals.p, n * 8, hipMemcpyDefault, c->stream));
   if (G * K) HIP_OK(hipMemcpyAsync(uni, c->sel_uni.p, G * K, hipMemcpyDefault, c->stream));
-  if (G) HIP_OK(hipMemcpyAsync(act, c->gact.p, G * 4, hipMemcpyDefault, c->stream));
+  std::vector<uint32_t> a(std::max<int64_t>(1, G));
+  if (G) HIP_OK(hipMemcpyAsync(a.data(), c->gact.p, G * 4, hipMemcpyDeviceToHost, c->stream));
   int32_t err = 0;
   HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
   if (err) return fail(err, "error raised by the device path");
+  ro_activity(c, P, G, a);
+  if (G) HIP_OK(hipMemcpy(act, a.data(), G * 4, hipMemcpyDefault));
   return 0;
 }
 
 extern "C" int tsdbhip_sel_select(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, const void* vals,
                                   const int64_t* counts, const void* uni, void* out_val, void* out_flag) {
   MD_REFUSE(c, "tsdbhip_sel_select");
-  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_sel_select over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !counts || !uni || !out_val || !out_flag) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_OK(hipSetDevice(c->device));
+  if (c->ro_active) { const int r = ro_check(q); if (r) return r; }
+  const tsdbhip_query qr0 = ro_query(c, q);
+  q = &qr0;
   Plan P;
   int rc = plan_sel(c, q, n_groups_global, P);
   if (rc) return rc;
@@ -4202,11 +4262,13 @@ extern "C" int tsdbhip_sel_select(tsdbhip_ctx* c, const tsdbhip_query* q, int64_
 extern "C" int tsdbhip_assemble(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, const void* val,
                                 const void* flag, const void* act, tsdbhip_result** out) {
   MD_REFUSE(c, "tsdbhip_assemble");
-  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_assemble over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !q || !val || !flag || !act || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
   *out = nullptr;
   HIP_OK(hipSetDevice(c->device));
+  if (c->ro_active) { const int r = ro_check(q); if (r) return r; }
+  const tsdbhip_query qr0 = ro_query(c, q);
+  q = &qr0;
   Plan P;
   int rc = plan_query(c, q, P);
   if (rc) return rc;

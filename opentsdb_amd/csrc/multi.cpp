@@ -334,11 +334,7 @@ int run_sel_xchg(MultiDev* m, const tsdbhip_query* q, tsdbhip_result** out) {
     rc = tsdbhip_sel_layout(m->subs[d], q, G, counts[d].data(), &Kd);
     if (rc) return rc;
     if (Kd != K) return set_error(TSDB_E_NOT_IMPLEMENTED, per_span_calendar());
-    int64_t ns = 0, nr = 0;
-    uint64_t qb = 0, vb = 0;
-    rc = tsdbhip_batch_sizes(m->subs[d], &ns, &nr, &qb, &vb);
-    if (rc) return rc;
-    n_series[d] = ns;
+    n_series[d] = ctx_n_series(m->subs[d]);
   }
   std::vector<std::vector<uint8_t>> uni(n);
   std::vector<std::vector<uint32_t>> act(n);
@@ -424,6 +420,46 @@ void device_timing(MultiDev* m, double wall_ms, bool fused) {
 }  // namespace
 
 // ---- load -------------------------------------------------------------------------------
+// The batch positions each device loads: whole SpanGroups (GROUPS) or a byte-balanced split of
+// the SpanGroup order (SERIES); ungrouped series on the last device.  Sets m->live / mode state.
+std::vector<std::vector<int64_t>> shard_series(MultiDev* m, const int32_t* gid, const std::vector<double>& w, int& mode,
+                                               int64_t& G) {
+  const int n = (int)m->devices.size();
+  const int64_t S = (int64_t)w.size();
+  int32_t maxg = -1;
+  for (int64_t s = 0; s < S; s++) maxg = std::max(maxg, gid[s]);
+  G = maxg + 1;
+  std::vector<double> gw(G, 0.0);
+  for (int64_t s = 0; s < S; s++) if (gid[s] >= 0) gw[gid[s]] += w[s];
+  const std::vector<int64_t> gb = split(gw, n);
+  mode = m->mode_req;
+  if (mode == TSDB_SHARD_AUTO) mode = (n == 1 || groups_balanced(gw, gb, n)) ? TSDB_SHARD_GROUPS : TSDB_SHARD_SERIES;
+  std::vector<std::vector<int64_t>> cand(n);
+  if (mode == TSDB_SHARD_GROUPS) {
+    std::vector<int32_t> owner(G, 0);
+    for (int d = 0; d < n; d++)
+      for (int64_t g = gb[d]; g < gb[d + 1]; g++) owner[g] = d;
+    for (int64_t s = 0; s < S; s++) cand[gid[s] < 0 ? n - 1 : owner[gid[s]]].push_back(s);
+  } else {
+    std::vector<int64_t> order;   // kept series stably by group: the SpanGroup order
+    for (int64_t s = 0; s < S; s++) if (gid[s] >= 0) order.push_back(s);
+    std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return gid[x] < gid[y]; });
+    std::vector<double> ow(order.size());
+    for (size_t i = 0; i < order.size(); i++) ow[i] = w[order[i]];
+    const std::vector<int64_t> pb = split(ow, n);
+    for (int d = 0; d < n; d++) cand[d].assign(order.begin() + pb[d], order.begin() + pb[d + 1]);
+    for (int64_t s = 0; s < S; s++) if (gid[s] < 0) cand[n - 1].push_back(s);
+  }
+  m->mode = TSDB_SHARD_AUTO;
+  m->series.clear();
+  m->pos0.clear();
+  m->live.assign(n, 0);
+  bool any = false;
+  for (int d = 0; d < n; d++) { m->live[d] = !cand[d].empty(); any = any || m->live[d]; }
+  if (!any) m->live[0] = 1;   // an empty batch: device 0 holds it, as one device would
+  return cand;
+}
+
 int md_load(tsdbhip_ctx* c, const tsdbhip_batch* b) {
   MultiDev* m = md_of(c);
   if (!b) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
@@ -433,54 +469,132 @@ int md_load(tsdbhip_ctx* c, const tsdbhip_batch* b) {
   if (b->n_series > 0 && (b->series_row_ptr[0] != 0 || b->series_row_ptr[b->n_series] != b->n_rows))
     return set_error(TSDB_E_ILLEGAL_ARGUMENT, "series_row_ptr does not cover the rows");
   std::lock_guard<std::mutex> lk(ctx_mutex(c));
-  const int n = (int)m->devices.size();
   const int64_t S = b->n_series;
-  int32_t maxg = -1;
+  std::vector<double> w(S);
   for (int64_t s = 0; s < S; s++) {
     if (b->series_row_ptr[s + 1] < b->series_row_ptr[s]) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "series_row_ptr not monotonic");
-    maxg = std::max(maxg, b->group_id[s]);
-  }
-  const int64_t G = maxg + 1;
-  std::vector<double> w(S), gw(G, 0.0);
-  for (int64_t s = 0; s < S; s++) {
     const int64_t r0 = b->series_row_ptr[s], r1 = b->series_row_ptr[s + 1];
     w[s] = (double)(b->row_qual_off[r1] - b->row_qual_off[r0]) + (double)(b->row_val_off[r1] - b->row_val_off[r0]);
-    if (b->group_id[s] >= 0) gw[b->group_id[s]] += w[s];
   }
-  const std::vector<int64_t> gb = split(gw, n);
-  int mode = m->mode_req;
-  if (mode == TSDB_SHARD_AUTO) mode = (n == 1 || groups_balanced(gw, gb, n)) ? TSDB_SHARD_GROUPS : TSDB_SHARD_SERIES;
-  std::vector<std::vector<int64_t>> cand(n);
-  if (mode == TSDB_SHARD_GROUPS) {
-    std::vector<int32_t> owner(G, 0);
-    for (int d = 0; d < n; d++)
-      for (int64_t g = gb[d]; g < gb[d + 1]; g++) owner[g] = d;
-    for (int64_t s = 0; s < S; s++) cand[b->group_id[s] < 0 ? n - 1 : owner[b->group_id[s]]].push_back(s);
-  } else {
-    std::vector<int64_t> order;   // kept series stably by group: the SpanGroup order
-    for (int64_t s = 0; s < S; s++) if (b->group_id[s] >= 0) order.push_back(s);
-    std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return b->group_id[x] < b->group_id[y]; });
-    std::vector<double> ow(order.size());
-    for (size_t i = 0; i < order.size(); i++) ow[i] = w[order[i]];
-    const std::vector<int64_t> pb = split(ow, n);
-    for (int d = 0; d < n; d++) cand[d].assign(order.begin() + pb[d], order.begin() + pb[d + 1]);
-    for (int64_t s = 0; s < S; s++) if (b->group_id[s] < 0) cand[n - 1].push_back(s);
-  }
-  m->mode = TSDB_SHARD_AUTO;
-  m->series.clear();
-  m->pos0.clear();
-  m->live.assign(n, 0);
-  bool any = false;
-  for (int d = 0; d < n; d++) { m->live[d] = !cand[d].empty(); any = any || m->live[d]; }
-  if (!any) m->live[0] = 1;   // an empty batch: device 0 holds it, as one device would
+  int mode = 0;
+  int64_t G = 0;
+  const std::vector<std::vector<int64_t>> cand = shard_series(m, b->group_id, w, mode, G);
+  ctx_drop_batch(m->root);   // (a rollup load before leaves rollup state on the merge context)
   const int rc = each_device(m, [&](int d) { return load_series(m->subs[d], b, cand[d]); });
+  if (rc) {
+    m->live.assign(m->devices.size(), 0);
+    return rc;
+  }
+  m->mode = mode;
+  m->G = G;
+  m->series = cand;
+  return 0;
+}
+
+// A rollup batch: each device loads the rollup spans of its series (value and count cells copied
+// out of the caller's arrays); the merge context holds an empty rollup batch of the same table,
+// so its plans (scan bounds of the rollup interval, count group-by as sum) match the devices'.
+int md_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* rb) {
+  MultiDev* m = md_of(c);
+  if (!rb) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  const tsdbhip_batch* b = &rb->cells;
+  const bool cnt = rb->row_cqual_off != nullptr;
+  if (cnt && (!rb->row_cval_off || !rb->cqual || !rb->cval)) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null count arrays");
+  if (b->n_series < 0 || b->n_rows < 0) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
+  if (b->n_series > 0 && (!b->series_row_ptr || !b->group_id)) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null batch arrays");
+  if (b->n_rows > 0 && (!b->row_base_time || !b->row_qual_off || !b->row_val_off || !b->qual || !b->val))
+    return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null batch arrays");
+  if (b->n_series > 0 && (b->series_row_ptr[0] != 0 || b->series_row_ptr[b->n_series] != b->n_rows))
+    return set_error(TSDB_E_ILLEGAL_ARGUMENT, "series_row_ptr does not cover the rows");
+  const int64_t S = b->n_series;
+  for (int64_t s = 0; s < S; s++)
+    if (b->series_row_ptr[s + 1] < b->series_row_ptr[s]) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "series_row_ptr not monotonic");
+  for (int64_t r = 0; r < b->n_rows; r++)
+    if (b->row_qual_off[r + 1] < b->row_qual_off[r] || b->row_val_off[r + 1] < b->row_val_off[r] ||
+        (cnt && (rb->row_cqual_off[r + 1] < rb->row_cqual_off[r] || rb->row_cval_off[r + 1] < rb->row_cval_off[r])))
+      return set_error(TSDB_E_ILLEGAL_ARGUMENT, "cell offsets not monotonic");
+  std::lock_guard<std::mutex> lk(ctx_mutex(c));
+  std::vector<double> w(S);
+  auto span = [](const uint64_t* o, int64_t r0, int64_t r1) { return (double)(o[r1] - o[r0]); };
+  for (int64_t s = 0; s < S; s++) {
+    const int64_t r0 = b->series_row_ptr[s], r1 = b->series_row_ptr[s + 1];
+    w[s] = span(b->row_qual_off, r0, r1) + span(b->row_val_off, r0, r1) +
+           (cnt ? span(rb->row_cqual_off, r0, r1) + span(rb->row_cval_off, r0, r1) : 0.0);
+  }
+  int mode = 0;
+  int64_t G = 0;
+  const std::vector<std::vector<int64_t>> cand = shard_series(m, b->group_id, w, mode, G);
+  const int n = (int)m->devices.size();
+  struct Sub {
+    std::vector<int64_t> srp{0};
+    std::vector<int32_t> gid;
+    std::vector<uint32_t> base;
+    std::vector<uint64_t> qo{0}, vo{0}, cqo{0}, cvo{0};
+    std::vector<uint8_t> q, v, cq, cv;
+    tsdbhip_rollup_batch rb{};
+  };
+  std::vector<Sub> sub(n);
+  auto append = [](std::vector<uint8_t>& dst, std::vector<uint64_t>& off, const uint8_t* src, const uint64_t* o, int64_t r) {
+    dst.insert(dst.end(), src + o[r], src + o[r + 1]);
+    off.push_back(dst.size());
+  };
+  for (int d = 0; d < n; d++) {
+    Sub& u = sub[d];
+    for (int64_t s : cand[d]) {
+      for (int64_t r = b->series_row_ptr[s]; r < b->series_row_ptr[s + 1]; r++) {
+        u.base.push_back(b->row_base_time[r]);
+        append(u.q, u.qo, b->qual, b->row_qual_off, r);
+        append(u.v, u.vo, b->val, b->row_val_off, r);
+        if (cnt) {
+          append(u.cq, u.cqo, rb->cqual, rb->row_cqual_off, r);
+          append(u.cv, u.cvo, rb->cval, rb->row_cval_off, r);
+        }
+      }
+      u.srp.push_back((int64_t)u.base.size());
+      u.gid.push_back(b->group_id[s]);
+    }
+    for (auto* x : {&u.q, &u.v, &u.cq, &u.cv}) if (x->empty()) x->push_back(0);
+    if (u.gid.empty()) u.gid.push_back(-1);
+    u.rb = *rb;
+    u.rb.cells.n_series = (int64_t)cand[d].size();
+    u.rb.cells.n_rows = (int64_t)u.base.size();
+    u.rb.cells.series_row_ptr = u.srp.data();
+    u.rb.cells.group_id = u.gid.data();
+    u.rb.cells.row_base_time = u.base.empty() ? nullptr : u.base.data();
+    u.rb.cells.row_qual_off = u.qo.data();
+    u.rb.cells.row_val_off = u.vo.data();
+    u.rb.cells.qual = u.q.data();
+    u.rb.cells.val = u.v.data();
+    u.rb.row_cqual_off = cnt ? u.cqo.data() : nullptr;
+    u.rb.row_cval_off = cnt ? u.cvo.data() : nullptr;
+    u.rb.cqual = cnt ? u.cq.data() : nullptr;
+    u.rb.cval = cnt ? u.cv.data() : nullptr;
+  }
+  int rc = each_device(m, [&](int d) { return tsdbhip_load_rollup(m->subs[d], &sub[d].rb); });
+  if (!rc) {   // the merge context: an empty batch of the same rollup table
+    Sub e;
+    e.q.push_back(0);
+    e.rb = *rb;
+    e.rb.cells = tsdbhip_batch{};
+    e.rb.cells.series_row_ptr = e.srp.data();
+    e.rb.cells.row_qual_off = e.qo.data();
+    e.rb.cells.row_val_off = e.vo.data();
+    e.rb.cells.qual = e.q.data();
+    e.rb.cells.val = e.q.data();
+    if (cnt) {
+      e.rb.row_cqual_off = e.cqo.data();
+      e.rb.row_cval_off = e.cvo.data();
+      e.rb.cqual = e.rb.cval = e.q.data();
+    }
+    rc = tsdbhip_load_rollup(m->root, &e.rb);
+  }
   if (rc) {
     m->live.assign(n, 0);
     return rc;
   }
   m->mode = mode;
   m->G = G;
-  m->series = std::move(cand);
+  m->series = cand;
   return 0;
 }
 
@@ -507,6 +621,7 @@ int md_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp) {
   m->series.clear();
   m->live.assign(n, 0);
   for (int d = 0; d < n; d++) m->live[d] = p[d + 1] > p[d];
+  ctx_drop_batch(m->root);
   const int rc = each_device(m, [&](int d) { return tsdbhip_synth_shard(m->subs[d], sp, p[d], p[d + 1]); });
   if (rc) {
     m->live.assign(n, 0);
@@ -682,10 +797,15 @@ extern "C" int tsdbhip_md_info(tsdbhip_ctx* c, int* n_devices, int* transport, i
   if (mode) *mode = m->mode;
   if (shard_series) {
     for (int d = 0; d < (int)m->devices.size(); d++) {
-      int64_t ns = 0, nr = 0;
-      uint64_t qb = 0, vb = 0;
       shard_series[d] = 0;
-      if (m->live[d] && tsdbhip_batch_sizes(m->subs[d], &ns, &nr, &qb, &vb) == 0) shard_series[d] = ns;
+      if (!m->live[d]) continue;
+      if (!m->series.empty()) {   // loaded: the batch series the device holds
+        shard_series[d] = (int64_t)m->series[d].size();
+      } else {                    // synthesized
+        int64_t ns = 0, nr = 0;
+        uint64_t qb = 0, vb = 0;
+        if (tsdbhip_batch_sizes(m->subs[d], &ns, &nr, &qb, &vb) == 0) shard_series[d] = ns;
+      }
     }
   }
   return 0;

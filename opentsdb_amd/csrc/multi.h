@@ -18,9 +18,12 @@ enum { QK_PARTIALS = 0, QK_SEL = 1, QK_RAW = 2, QK_NONE = 3 };
 int query_kind(tsdbhip_ctx* c, const tsdbhip_query* q, int* kind);   // plan_query's verdict
 int set_error(int code, const std::string& msg);
 tsdbhip_result* new_result(int64_t n_groups, int64_t n_points);
+void ctx_drop_batch(tsdbhip_ctx* c);               // release the resident batch (and rollup state)
+int64_t ctx_n_series(tsdbhip_ctx* c);              // resident series, a rollup batch's count series too
 // multi.cpp
 int md_load(tsdbhip_ctx* c, const tsdbhip_batch* b);
 int md_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp);
+int md_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* rb);
 int md_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out);
 int md_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_result** outs);
 int md_timing(tsdbhip_ctx* c, tsdbhip_timing* out);

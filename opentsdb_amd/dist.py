@@ -88,6 +88,39 @@ def shard_batch(batch: abi.HostBatch, rank: int, world: int) -> abi.HostBatch:
     return select_series(batch, order[b[rank]:b[rank + 1]])
 
 
+def shard_rollup_batch(rb: abi.HostRollupBatch, rank: int, world: int, by_group: bool = False) -> abi.HostRollupBatch:
+    """The rank's shard of a rollup scan (value cells and, with RollupSeq.need_count, the count
+    cells of the same rows): series split like shard_batch / shard_batch_by_group.  Load it with
+    eng.load_rollup; run_distributed / run_distributed_sel then work over rollup shards as over
+    raw ones (the library plans a count group-by as sum on every rank)."""
+    cells = rb.cells
+    srp = cells.series_row_ptr
+    w = series_bytes(cells)
+    if rb.counts is not None:
+        cqo, cvo = rb.counts[0].astype(np.int64), rb.counts[1].astype(np.int64)
+        w = w + np.array([(cqo[srp[s + 1]] - cqo[srp[s]]) + (cvo[srp[s + 1]] - cvo[srp[s]])
+                          for s in range(cells.n_series)], np.float64)
+    if by_group:
+        gw = np.bincount(cells.group_id[cells.group_id >= 0], weights=w[cells.group_id >= 0],
+                         minlength=n_groups_of(cells))
+        b = shard_bounds(gw, world)
+        series = np.nonzero((cells.group_id >= b[rank]) & (cells.group_id < b[rank + 1]))[0]
+    else:
+        order = group_sorted_order(cells)
+        b = shard_bounds(w[order], world)
+        series = order[b[rank]:b[rank + 1]]
+    sub = select_series(cells, series)
+    counts = None
+    if rb.counts is not None:
+        cqo, cvo = rb.counts[0].astype(np.int64), rb.counts[1].astype(np.int64)
+        series = np.asarray(series, np.int64)
+        rows = _ranges(srp[series], srp[series + 1])
+        nq = np.concatenate([[0], np.cumsum(cqo[rows + 1] - cqo[rows])]).astype(np.uint64)
+        nv = np.concatenate([[0], np.cumsum(cvo[rows + 1] - cvo[rows])]).astype(np.uint64)
+        counts = (nq, nv, rb.counts[2][_ranges(cqo[rows], cqo[rows + 1])], rb.counts[3][_ranges(cvo[rows], cvo[rows + 1])])
+    return abi.HostRollupBatch(sub, counts, rb.interval, rb.fix_duplicates)
+
+
 def n_groups_of(batch: abi.HostBatch) -> int:
     return int(batch.group_id.max()) + 1 if batch.n_series else 0
 

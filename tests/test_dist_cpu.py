@@ -315,3 +315,53 @@ def test_shard_ten_million_series_in_seconds():
     t_sel = time.perf_counter() - t
     assert s.n_series == bounds[4] - bounds[3] and len(s.qual) == 8 * s.n_series
     assert t_sel < 20, t_sel
+
+
+def _rollup_batch(seed=3):
+    """A rollup scan result: value cells from synth, count cells of random length per row."""
+    b = synth.generate(37, 1356998400, 120, 60000, value_kind=2, n_groups=5, int_mod=100, seed=seed)
+    gid = b.group_id.copy()
+    gid[::7] = -1
+    rng = np.random.default_rng(seed)
+    clen = rng.integers(0, 5, b.n_rows) * 2
+    cq_off = np.concatenate([[0], np.cumsum(clen)]).astype(np.uint64)
+    cv_off = np.concatenate([[0], np.cumsum(clen // 2)]).astype(np.uint64)
+    cq = rng.integers(0, 256, int(cq_off[-1]), dtype=np.uint8)
+    cv = rng.integers(0, 256, int(cv_off[-1]), dtype=np.uint8)
+    cells = abi.HostBatch(b.series_row_ptr, b.row_base_time, b.row_qual_off, b.row_val_off, b.qual, b.val, gid)
+    return abi.HostRollupBatch(cells, (cq_off, cv_off, cq, cv), abi.RollupInterval())
+
+
+def _series_cells(rb):
+    c = rb.cells
+    srp = c.series_row_ptr
+    out = []
+    for s in range(c.n_series):
+        rows = range(srp[s], srp[s + 1])
+        cut = lambda o, buf: [bytes(buf[int(o[r]):int(o[r + 1])]) for r in rows]  # noqa: E731
+        out.append((int(c.group_id[s]), [int(c.row_base_time[r]) for r in rows], cut(c.row_qual_off, c.qual),
+                    cut(c.row_val_off, c.val), cut(rb.counts[0], rb.counts[2]), cut(rb.counts[1], rb.counts[3])))
+    return out
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("by_group", [False, True])
+def test_shard_rollup_batch_covers_groups(world, by_group):
+    """dist.shard_rollup_batch: the ranks' shards hold every grouped series once, value and count
+    cells of each row intact; series shards follow the SpanGroup order, group shards keep groups
+    whole."""
+    rb = _rollup_batch()
+    full = _series_cells(rb)
+    want = sorted([x for x in full if x[0] >= 0], key=lambda x: x[0])
+    got, owner = [], {}
+    for r in range(world):
+        sh = dist.shard_rollup_batch(rb, r, world, by_group=by_group)
+        assert sh.counts is not None and sh.interval is rb.interval
+        part = _series_cells(sh)
+        for x in part:
+            owner.setdefault(x[0], set()).add(r)
+        got.extend(part)
+    if by_group:
+        assert all(len(v) == 1 for v in owner.values())
+        got = sorted(got, key=lambda x: x[0])
+    assert got == want
