@@ -422,7 +422,10 @@ typedef struct {
   int32_t fix_duplicates;            /* tsd.storage.fix_duplicates */
 } tsdbhip_rollup_batch;
 /* Loads a rollup batch as the resident batch; tsdbhip_run then runs rollup queries over it
- * (downsampled or not; percentile group-by, ordered and multi-GPU entry points excluded). */
+ * (downsampling required; tsdbhip_run_multi excluded).  A rank's rollup shard takes part in
+ * the partials (tsdbhip_run_partials / finalize) and percentile (tsdbhip_sel_*) exchanges --
+ * every rank plans a count group-by as sum -- and a multi-device context shards a rollup batch
+ * like tsdbhip_load (value and count cells of a series stay together). */
 int tsdbhip_load_rollup(tsdbhip_ctx* ctx, const tsdbhip_rollup_batch* rb);
 
 /* ---- query-time compaction ----------------------------------
