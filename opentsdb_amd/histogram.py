@@ -315,9 +315,32 @@ def result_to_series(res: HistResult, percentiles) -> list[list[HistogramDataPoi
     kind_all = arr(res.codec, n_all, np.uint8)
     if res.show_buckets and n_all:
         cnt_all = arr(res.count, n_all * (D + 2), np.int64).reshape(n_all, D + 2)
-        pres_all = arr(res.present, n_all * D, np.uint8).reshape(n_all, D)
+        pres_all = arr(res.present, n_all * D, np.uint8).reshape(n_all, D).astype(bool)
         lo = [res.bucket_lower[d] for d in range(D)]
         up = [res.bucket_upper[d] for d in range(D)]
+        # bucket_value for every (point, dictionary bucket) at once: each dictionary bucket's
+        # rank in compareTo order, and per point the lowest / highest rank it holds
+        order = sorted(range(D), key=lambda d: (_fcmp_key(lo[d]), _fcmp_key(up[d])))
+        rank = np.empty(D, np.int64)
+        rank[order] = np.arange(D)
+        zero_key = np.array([lo[d] == 0 and up[d] == 0 for d in range(D)], bool)
+        rmin = np.where(pres_all, rank[None, :], D).min(axis=1) if D else np.zeros(n_all, np.int64)
+        rmax = np.where(pres_all, rank[None, :], -1).max(axis=1) if D else np.full(n_all, -1, np.int64)
+        simple = kind_all == HCODEC_SIMPLE
+        under_all = np.where(simple, cnt_all[:, D], 0)
+        over_all = np.where(simple, cnt_all[:, D + 1], 0)
+        reg_all = np.where(pres_all, cnt_all[:, :D], 0)
+        if zero_key.any():
+            absent = ~pres_all[:, zero_key]
+            zr = rank[zero_key][None, :]
+            none_held = (rmax < 0)[:, None]
+            below = none_held | (zr < rmin[:, None])
+            above = ~none_held & (zr > rmax[:, None])
+            reg_all[:, zero_key] = np.where(absent & below, cnt_all[:, D][:, None],
+                                            np.where(absent & above, cnt_all[:, D + 1][:, None],
+                                                     reg_all[:, zero_key]))
+        # getHistogramBucketsIfHas throws UnsupportedOperationException for other codecs: 0
+        reg_all[~simple] = 0
     for g in range(res.n_groups):
         a, b = res.group_ptr[g], res.group_ptr[g + 1]
         gid = res.group_id[g]
@@ -326,17 +349,9 @@ def result_to_series(res: HistResult, percentiles) -> list[list[HistogramDataPoi
         for j, p in enumerate(percentiles):
             series.append(HistogramDataPoints(gid, ts, pct_all[a:b, j].copy(), np.zeros(b - a, np.uint8), percentile=p))
         if res.show_buckets and b > a and kind_all[a] == HCODEC_SIMPLE:   # (n_all > 0 here)
-            first = [d for d in range(D) if pres_all[a, d]]
+            first = np.flatnonzero(pres_all[a])
             keys = [(BK_UNDER, 0, 0)] + [(BK_REG, lo[d], up[d]) for d in first] + [(BK_OVER, 0, 0)]
-            vals = np.zeros((len(keys), b - a), np.int64)
-            for i in range(a, b):
-                if kind_all[i] != HCODEC_SIMPLE:
-                    continue   # getHistogramBucketsIfHas throws UnsupportedOperationException: 0
-                present = [d for d in range(D) if pres_all[i, d]]
-                counts = {(_fcmp_key(lo[d]), _fcmp_key(up[d])): int(cnt_all[i, d]) for d in present}
-                regs = sorted(counts)
-                for kidx, key in enumerate(keys):
-                    vals[kidx, i - a] = bucket_value(key, regs, counts, int(cnt_all[i, D]), int(cnt_all[i, D + 1]))
+            vals = np.concatenate([under_all[None, a:b], reg_all[a:b, first].T, over_all[None, a:b]])
             for kidx, key in enumerate(keys):
                 series.append(HistogramDataPoints(gid, ts, vals[kidx], np.ones(b - a, np.uint8), bucket=key))
         out.append(series)

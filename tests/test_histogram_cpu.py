@@ -136,3 +136,57 @@ def test_oracle_nonsum_downsampling_raises_null_pointer():
 
 def test_percentile_struct_pack_roundtrip():
     assert struct.unpack(">f", struct.pack(">I", H.f32bits(0.98)))[0] == np.float32(0.98)
+
+
+def _loop_bucket_series(lo, up, cnt, pres, kind, a, b):
+    """The per-point, per-bucket loop over bucket_value (the closed form's definition)."""
+    D = len(lo)
+    first = [d for d in range(D) if pres[a, d]]
+    keys = [(H.BK_UNDER, 0, 0)] + [(H.BK_REG, lo[d], up[d]) for d in first] + [(H.BK_OVER, 0, 0)]
+    vals = np.zeros((len(keys), b - a), np.int64)
+    for i in range(a, b):
+        if kind[i] != H.HCODEC_SIMPLE:
+            continue
+        counts = {(H._fcmp_key(lo[d]), H._fcmp_key(up[d])): int(cnt[i, d]) for d in range(D) if pres[i, d]}
+        regs = sorted(counts)
+        for k, key in enumerate(keys):
+            vals[k, i - a] = H.bucket_value(key, regs, counts, int(cnt[i, D]), int(cnt[i, D + 1]))
+    return keys, vals
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_bucket_series_vectorised_matches_loop(seed):
+    """result_to_series builds every bucket series with array operations; it must equal the
+    per-point bucket_value loop, (+0.0, +0.0) lookups and non-simple points included."""
+    import ctypes as C
+    rng = np.random.default_rng(seed)
+    bounds = [0.0, -0.0, 1.0, 2.0, -3.0, 5.5, 1e9]
+    pairs = [(H.f32bits(x), H.f32bits(y)) for x in bounds for y in bounds if x <= y]
+    pairs = list(dict.fromkeys(pairs))
+    D = len(pairs)
+    n_groups = 4
+    sizes = rng.integers(1, 12, n_groups)
+    n_all = int(sizes.sum())
+    gptr = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    pres = (rng.random((n_all, D)) < 0.3).astype(np.uint8)
+    cnt = rng.integers(0, 1000, (n_all, D + 2)).astype(np.int64)
+    kind = np.where(rng.random(n_all) < 0.9, H.HCODEC_SIMPLE, H.HCODEC_SIMPLE + 1).astype(np.uint8)
+    kind[gptr[:-1]] = H.HCODEC_SIMPLE
+    ts = np.arange(n_all, dtype=np.int64)
+    lo = np.array([p[0] for p in pairs], np.uint32)
+    up = np.array([p[1] for p in pairs], np.uint32)
+    gid = np.arange(n_groups, dtype=np.int32)
+    keep = [gid, gptr, ts, lo, up, cnt, pres, kind]
+    r = H.HistResult()
+    r.n_groups, r.n_pct, r.show_buckets, r.n_buckets = n_groups, 0, 1, D
+    for name, a, ct in (("group_id", gid, C.c_int32), ("group_ptr", gptr, C.c_int64), ("ts_ms", ts, C.c_int64),
+                        ("bucket_lower", lo, C.c_uint32), ("bucket_upper", up, C.c_uint32),
+                        ("count", cnt, C.c_int64), ("present", pres, C.c_uint8), ("codec", kind, C.c_uint8)):
+        setattr(r, name, a.ctypes.data_as(C.POINTER(ct)))
+    out = H.result_to_series(r, [])
+    assert keep and len(out) == n_groups
+    for g in range(n_groups):
+        keys, vals = _loop_bucket_series(list(lo), list(up), cnt, pres, kind, gptr[g], gptr[g + 1])
+        assert [tuple(s.bucket) for s in out[g]] == [(k[0], int(k[1]), int(k[2])) for k in keys]
+        for s, v in zip(out[g], vals):
+            assert np.array_equal(np.asarray(s.values), v)
