@@ -441,8 +441,9 @@ int tsdbhip_load_rollup(tsdbhip_ctx* ctx, const tsdbhip_rollup_batch* rb);
  * rows become the resident batch; rows of one series with the same base time (one per salt
  * bucket) are compacted each and then merged in scan order as Span.addRow / RowSeq.addRow merge
  * them (src/core/Span.java:202-219).  Compaction exceptions are raised by the first query whose
- * scan range covers the row.  NOT_IMPLEMENTED: more than 2^31 columns, rows or datapoints in one
- * call; per row, lazily: a compacted cell out of time order, a datapoint column with an empty
+ * scan range covers the row.  Scans of more than 2^31 columns or datapoints are compacted in
+ * chunks of whole rows.  NOT_IMPLEMENTED: a row of more than 2^31 columns or datapoints, more
+ * than 2^31 rows; per row, lazily: a compacted cell out of time order, a datapoint column with an empty
  * value. */
 typedef struct {
   int64_t n_series;
@@ -614,6 +615,14 @@ int tsdbhip_expr_sync(tsdbhip_ctx* ctx, const int32_t* program, int n_ops, const
 enum { TSDB_EXPR_HIGHEST_MAX = 4, TSDB_EXPR_HIGHEST_CURRENT = 5 };
 int tsdbhip_expr_topn(tsdbhip_ctx* ctx, int fn, int32_t topn, int64_t start_ms, int64_t end_ms,
                       const tsdbhip_series_set* in, int32_t* out_index, int32_t* out_n);
+
+/* Page-locked host memory for the buffers a caller hands to the load entry points
+ * (tsdbhip_load, tsdbhip_load_cells, tsdbhip_load_histograms ...): their uploads are then DMA
+ * transfers at the link's rate instead of staged copies of pageable memory.  A JVM caller wraps
+ * the block in a direct ByteBuffer (JNI NewDirectByteBuffer) and assembles the scan into it.
+ * No reference counterpart (the JVM's scan buffers). */
+int tsdbhip_host_alloc(uint64_t bytes, void** out);
+void tsdbhip_host_free(void* p);
 
 /* Device synchronisation helper for host code that does not use HIP directly. */
 int tsdbhip_sync(tsdbhip_ctx* ctx);

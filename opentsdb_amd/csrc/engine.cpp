@@ -400,6 +400,7 @@ struct tsdbhip_ctx {
   bool calc_anchored = false;            // ... the spans' grids disagree: per-anchor sequences
   std::vector<int64_t> calc_anchors;
   std::vector<std::vector<int64_t>> calc_seqs;
+  std::vector<int64_t> calc_fill;      // FillingDownsampler's calendar sequence of an anchored plan
   DevBuf first_ts;
   int64_t mdp_ss = 0, mdp_se = 0, mdp = 0;
   DevBuf sel_vals, sel_sorted, sel_uni, sel_gsp;   // percentile / median group-by
@@ -479,6 +480,18 @@ void hist_release(void* h);
 void*& ctx_md(tsdbhip_ctx* c) { return c->md; }
 bool ctx_is_md(tsdbhip_ctx* c) { return c && c->md; }
 void ctx_set_none_orig(tsdbhip_ctx* c, bool on) { c->none_orig = on; }
+// DateTime.previousInterval and one Downsampler calendar step in a zone (null: UTC), for hist.cpp
+bool cal_prev_tz(const tsdbhip_tz* z, int64_t ts, int64_t n, int unit, int64_t* out) {
+  JZone Z;
+  Z.z = z;
+  return jcal_prev(Z, ts, n, unit, *out);
+}
+int64_t cal_step_tz(const tsdbhip_tz* z, int64_t t, int unit, int64_t n) {
+  JZone Z;
+  Z.z = z;
+  return jcal_step(Z, t, unit, n, 1);
+}
+int64_t cal_unit_ms(int unit) { return unit >= 0 && unit < 9 ? CAL_UNIT_MS[unit] : 0; }
 }  // namespace tsdb
 
 // Entry points bound to one device's resident store refuse a multi-device context.
@@ -491,6 +504,17 @@ void ctx_set_none_orig(tsdbhip_ctx* c, bool on) { c->none_orig = on; }
 // host logic restatements
 // ===========================================================================
 extern "C" int tsdbhip_abi_version(void) { return TSDBHIP_ABI_VERSION; }
+
+extern "C" int tsdbhip_host_alloc(uint64_t bytes, void** out) {
+  if (!out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  *out = nullptr;
+  HIP_OK(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocPortable));
+  return 0;
+}
+
+extern "C" void tsdbhip_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
 extern "C" const char* tsdbhip_last_error(void) { return g_last_error.c_str(); }
 
 extern "C" int tsdbhip_aggregator_get(const char* name) {
@@ -1385,120 +1409,195 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     if (cb->row_col_ptr[r + 1] < cb->row_col_ptr[r]) return fail(TSDB_E_ILLEGAL_ARGUMENT, "row_col_ptr not monotonic");
   if (NC > 0 && (cb->col_qual_off[0] != 0 || cb->col_val_off[0] != 0))
     return fail(TSDB_E_ILLEGAL_ARGUMENT, "column offsets must start at 0");
-  for (int64_t k = 0; k < NC; k++)
-    if (cb->col_qual_off[k + 1] < cb->col_qual_off[k] || cb->col_val_off[k + 1] < cb->col_val_off[k])
-      return fail(TSDB_E_ILLEGAL_ARGUMENT, "column offsets not monotonic");
-  if (NC >= ((int64_t)1 << 31) || NR >= ((int64_t)1 << 31))
-    return fail(TSDB_E_NOT_IMPLEMENTED, "more than 2^31 columns or rows in one compaction batch");
+  // The scan in chunks of whole rows, each under 2^31 columns and 2^31 datapoints: a datapoint
+  // takes at least 2 qualifier bytes, or 3 bytes of an append value, so a row holds at most
+  // (qualifier + value bytes) / 2.  The column offsets are checked on the device chunk by chunk
+  // (k_cmp_rebase), not here.  One chunk: one pass.  Several: the first pass sizes every row, the
+  // host lays the batch out, and the second pass recomputes each chunk's entries and writes them.
+  const int64_t kLim = ((int64_t)1 << 31) - 1;
+  int64_t limit = kLim;
+  if (const char* e = std::getenv("TSDBHIP_CMP_CHUNK")) limit = std::max<int64_t>(1, std::atoll(e));   // tests: force chunks
+  std::vector<int64_t> cuts{0};
+  {
+    int64_t w = 0;
+    for (int64_t r = 0; r < NR; r++) {
+      const int64_t c0 = cb->row_col_ptr[r], c1 = cb->row_col_ptr[r + 1];
+      int64_t wr = c1 - c0;
+      if (c1 > c0) {
+        const uint64_t q0 = cb->col_qual_off[c0], q1 = cb->col_qual_off[c1];
+        const uint64_t v0 = cb->col_val_off[c0], v1 = cb->col_val_off[c1];
+        if (q1 < q0 || v1 < v0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "column offsets not monotonic");
+        if (q1 - q0 + v1 - v0 >= (uint64_t)2 * kLim) wr = kLim;
+        else wr = std::max<int64_t>(wr, (int64_t)((q1 - q0 + v1 - v0) / 2));
+      }
+      if (wr >= kLim) return fail(TSDB_E_NOT_IMPLEMENTED, "a row of more than 2^31 columns or datapoints");
+      if (w + wr > limit && r > cuts.back()) {
+        cuts.push_back(r);
+        w = 0;
+      }
+      w += wr;
+    }
+    cuts.push_back(NR);
+  }
+  const int n_chunks = (int)cuts.size() - 1;
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_OK(hipSetDevice(c->device));
   release_batch(c);
-  const uint64_t qb = NC ? cb->col_qual_off[NC] : 0, vb = NC ? cb->col_val_off[NC] : 0;
-  // device copies of the scan and per-column / per-row scratch (freed at the end)
+  // device copies of one chunk of the scan and per-column / per-row scratch (freed at the end)
   DevBuf d_rcp, d_cqo, d_cvo, d_cts, d_q, d_v, d_crow, d_cn, d_coff, d_cinfo, d_rheap, d_rone, d_rerr;
   DevBuf d_key, d_key2, d_idx, d_idx2, d_ecol, d_eqo, d_evo, d_klen, d_sq, d_sv, d_sc, d_sm;
-  DevBuf d_rlo, d_rq, d_rv, d_rstate, d_rmeta, d_rdq, d_rdv;
+  DevBuf d_rlo, d_rq, d_rv, d_rstate, d_rmeta, d_rdq, d_rdv, d_raw, d_bad;
   auto release_all = [&]() {
     for (DevBuf* b : {&d_rcp, &d_cqo, &d_cvo, &d_cts, &d_q, &d_v, &d_crow, &d_cn, &d_coff, &d_cinfo, &d_rheap, &d_rone,
                       &d_rerr, &d_key, &d_key2, &d_idx, &d_idx2, &d_ecol, &d_eqo, &d_evo, &d_klen, &d_sq, &d_sv,
-                      &d_sc, &d_sm, &d_rlo, &d_rq, &d_rv, &d_rstate, &d_rmeta, &d_rdq, &d_rdv})
+                      &d_sc, &d_sm, &d_rlo, &d_rq, &d_rv, &d_rstate, &d_rmeta, &d_rdq, &d_rdv, &d_raw, &d_bad})
       b->release();
   };
   struct Rel { std::function<void()> f; ~Rel() { f(); } } rel{release_all};
-  const int64_t R1 = std::max<int64_t>(1, NR), C1 = std::max<int64_t>(1, NC);
-  HIP_OK(d_rcp.ensure((NR + 1) * 8));
-  HIP_OK(d_cqo.ensure((NC + 1) * 8));
-  HIP_OK(d_cvo.ensure((NC + 1) * 8));
-  HIP_OK(d_q.ensure(std::max<uint64_t>(16, qb)));
-  HIP_OK(d_v.ensure(std::max<uint64_t>(16, vb)));
-  if (cb->col_timestamp) HIP_OK(d_cts.ensure(C1 * 8));
-  if (NR) HIP_OK(hipMemcpyAsync(d_rcp.p, cb->row_col_ptr, (NR + 1) * 8, hipMemcpyHostToDevice, c->stream));
-  if (NC) {
-    HIP_OK(hipMemcpyAsync(d_cqo.p, cb->col_qual_off, (NC + 1) * 8, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(d_cvo.p, cb->col_val_off, (NC + 1) * 8, hipMemcpyHostToDevice, c->stream));
-    if (qb) HIP_OK(hipMemcpyAsync(d_q.p, cb->qual, qb, hipMemcpyHostToDevice, c->stream));
-    if (vb) HIP_OK(hipMemcpyAsync(d_v.p, cb->val, vb, hipMemcpyHostToDevice, c->stream));
-    if (cb->col_timestamp) HIP_OK(hipMemcpyAsync(d_cts.p, cb->col_timestamp, NC * 8, hipMemcpyHostToDevice, c->stream));
-  }
-  HIP_OK(d_crow.ensure(C1 * 4));
-  HIP_OK(d_cn.ensure(C1 * 8));
-  HIP_OK(d_coff.ensure((C1 + 1) * 8));
-  HIP_OK(d_cinfo.ensure(C1 * 4));
-  HIP_OK(d_rheap.ensure(R1 * 4));
-  HIP_OK(d_rone.ensure(R1 * 8));
-  HIP_OK(d_rerr.ensure(R1 * 4));
-  HIP_OK(hipMemsetAsync(d_rheap.p, 0, R1 * 4, c->stream));
-  HIP_OK(hipMemsetAsync(d_rone.p, 0, R1 * 8, c->stream));
-  HIP_OK(hipMemsetAsync(d_rerr.p, 0, R1 * 4, c->stream));
-  CmpParams p{};
-  p.n_rows = NR;
-  p.n_cols = NC;
-  p.row_col_ptr = d_rcp.as<int64_t>();
-  p.col_qo = d_cqo.as<uint64_t>();
-  p.col_vo = d_cvo.as<uint64_t>();
-  p.col_ts = cb->col_timestamp ? d_cts.as<int64_t>() : nullptr;
-  p.q = d_q.as<uint8_t>();
-  p.v = d_v.as<uint8_t>();
-  p.fix_dup = cb->fix_duplicates ? 1 : 0;
-  p.col_row = d_crow.as<int32_t>();
-  p.col_n = d_cn.as<int64_t>();
-  p.col_off = d_coff.as<int64_t>();
-  p.col_info = d_cinfo.as<uint32_t>();
-  p.row_heap = d_rheap.as<int32_t>();
-  p.row_one = d_rone.as<int64_t>();
-  p.row_err = d_rerr.as<int32_t>();
-  HIP_OK(hipEventRecord(c->ev[0], c->stream));
-  HIP_OK(cmp_analyze(p, &c->cmp_tmp, &c->cmp_tmp_bytes, c->stream));
-  int64_t n_ent = 0;
-  HIP_OK(hipMemcpyAsync(&n_ent, p.col_off + NC, 8, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipStreamSynchronize(c->stream));
-  if (n_ent >= ((int64_t)1 << 31)) return fail(TSDB_E_NOT_IMPLEMENTED, "more than 2^31 datapoints in one compaction batch");
-  const int64_t E1 = std::max<int64_t>(1, n_ent);
-  p.n_ent = n_ent;
-  HIP_OK(d_key.ensure(E1 * 8));
-  HIP_OK(d_key2.ensure(E1 * 8));
-  HIP_OK(d_idx.ensure(E1 * 4));
-  HIP_OK(d_idx2.ensure(E1 * 4));
-  HIP_OK(d_ecol.ensure(E1 * 4));
-  HIP_OK(d_eqo.ensure(E1 * 4));
-  HIP_OK(d_evo.ensure(E1 * 4));
-  HIP_OK(d_klen.ensure(E1 * 4));
-  for (DevBuf* b : {&d_sq, &d_sv, &d_sc, &d_sm}) HIP_OK(b->ensure((E1 + 1) * 8));
-  HIP_OK(d_rlo.ensure(R1 * 8));
-  HIP_OK(d_rq.ensure(R1 * 8));
-  HIP_OK(d_rv.ensure(R1 * 8));
-  HIP_OK(d_rstate.ensure(R1 * 4));
-  HIP_OK(d_rmeta.ensure(R1));
-  p.key = d_key.as<uint64_t>();
-  p.key2 = d_key2.as<uint64_t>();
-  p.idx = d_idx.as<uint32_t>();
-  p.idx2 = d_idx2.as<uint32_t>();
-  p.ent_col = d_ecol.as<uint32_t>();
-  p.ent_qo = d_eqo.as<uint32_t>();
-  p.ent_vo = d_evo.as<uint32_t>();
-  p.klen = d_klen.as<uint32_t>();
-  p.sq = d_sq.as<int64_t>();
-  p.sv = d_sv.as<int64_t>();
-  p.sc = d_sc.as<int64_t>();
-  p.sm = d_sm.as<int64_t>();
-  p.row_lo = d_rlo.as<int64_t>();
-  p.row_q = d_rq.as<int64_t>();
-  p.row_v = d_rv.as<int64_t>();
-  p.row_state = d_rstate.as<int32_t>();
-  p.row_meta = d_rmeta.as<uint8_t>();
-  int rb = 1;
-  while (((int64_t)1 << rb) <= NR) rb++;
-  HIP_OK(cmp_entries(p, &c->cmp_tmp, &c->cmp_tmp_bytes, std::min(64, 22 + rb), c->stream));
-  HIP_OK(hipEventRecord(c->ev[2], c->stream));
-  std::vector<int64_t> rq(R1), rv(R1);
+  const hipStream_t st = c->stream;
+  const int64_t R1 = std::max<int64_t>(1, NR);
+  std::vector<int64_t> rq(R1), rv(R1), rdq(R1, -1), rdv(R1, -1);
   std::vector<int32_t> rstate(R1), rerr(R1);
-  if (NR) {
-    HIP_OK(hipMemcpyAsync(rq.data(), p.row_q, NR * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipMemcpyAsync(rv.data(), p.row_v, NR * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipMemcpyAsync(rstate.data(), p.row_state, NR * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipMemcpyAsync(rerr.data(), p.row_err, NR * 4, hipMemcpyDeviceToHost, c->stream));
-  }
-  HIP_OK(hipStreamSynchronize(c->stream));
+  CmpParams p{};
+  p.fix_dup = cb->fix_duplicates ? 1 : 0;
+  double cmp_ms = 0;   // device spans; the uploads and the host layout between them are not counted
+  HIP_OK(d_bad.ensure(4));
+  // upload, analyze and build the entries of chunk k; its rows' sizes and states to the host
+  auto prepare = [&](int k) -> int {
+    const int64_t r0 = cuts[k], r1 = cuts[k + 1], nr = r1 - r0;
+    const int64_t c0 = NR ? cb->row_col_ptr[r0] : 0, c1 = NR ? cb->row_col_ptr[r1] : 0, nc = c1 - c0;
+    const uint64_t qa = nc ? cb->col_qual_off[c0] : 0, qz = nc ? cb->col_qual_off[c1] : 0;
+    const uint64_t va = nc ? cb->col_val_off[c0] : 0, vz = nc ? cb->col_val_off[c1] : 0;
+    const int64_t r1c = std::max<int64_t>(1, nr), c1c = std::max<int64_t>(1, nc);
+    HIP_OK(d_rcp.ensure((r1c + 1) * 8));
+    HIP_OK(d_cqo.ensure((c1c + 1) * 8));
+    HIP_OK(d_cvo.ensure((c1c + 1) * 8));
+    HIP_OK(d_raw.ensure((std::max(r1c, c1c) + 1) * 8));
+    HIP_OK(d_q.ensure(std::max<uint64_t>(16, qz - qa)));
+    HIP_OK(d_v.ensure(std::max<uint64_t>(16, vz - va)));
+    if (cb->col_timestamp) HIP_OK(d_cts.ensure(c1c * 8));
+    HIP_OK(hipMemsetAsync(d_bad.p, 0, 4, st));
+    if (nr) {
+      HIP_OK(hipMemcpyAsync(d_raw.p, cb->row_col_ptr + r0, (nr + 1) * 8, hipMemcpyHostToDevice, st));
+      HIP_OK(cmp_rebase(d_raw.as<uint64_t>(), d_rcp.as<uint64_t>(), nr + 1, (uint64_t)c0, d_bad.as<int32_t>(), st));
+    }
+    if (nc) {
+      HIP_OK(hipMemcpyAsync(d_raw.p, cb->col_qual_off + c0, (nc + 1) * 8, hipMemcpyHostToDevice, st));
+      HIP_OK(cmp_rebase(d_raw.as<uint64_t>(), d_cqo.as<uint64_t>(), nc + 1, qa, d_bad.as<int32_t>(), st));
+      HIP_OK(hipMemcpyAsync(d_raw.p, cb->col_val_off + c0, (nc + 1) * 8, hipMemcpyHostToDevice, st));
+      HIP_OK(cmp_rebase(d_raw.as<uint64_t>(), d_cvo.as<uint64_t>(), nc + 1, va, d_bad.as<int32_t>(), st));
+      if (qz > qa) HIP_OK(hipMemcpyAsync(d_q.p, cb->qual + qa, qz - qa, hipMemcpyHostToDevice, st));
+      if (vz > va) HIP_OK(hipMemcpyAsync(d_v.p, cb->val + va, vz - va, hipMemcpyHostToDevice, st));
+      if (cb->col_timestamp) HIP_OK(hipMemcpyAsync(d_cts.p, cb->col_timestamp + c0, nc * 8, hipMemcpyHostToDevice, st));
+    }
+    int32_t bad = 0;
+    HIP_OK(hipMemcpyAsync(&bad, d_bad.p, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (bad) return fail(TSDB_E_ILLEGAL_ARGUMENT, "column offsets not monotonic");
+    HIP_OK(d_crow.ensure(c1c * 4));
+    HIP_OK(d_cn.ensure(c1c * 8));
+    HIP_OK(d_coff.ensure((c1c + 1) * 8));
+    HIP_OK(d_cinfo.ensure(c1c * 4));
+    HIP_OK(d_rheap.ensure(r1c * 4));
+    HIP_OK(d_rone.ensure(r1c * 8));
+    HIP_OK(d_rerr.ensure(r1c * 4));
+    HIP_OK(hipMemsetAsync(d_rheap.p, 0, r1c * 4, st));
+    HIP_OK(hipMemsetAsync(d_rone.p, 0, r1c * 8, st));
+    HIP_OK(hipMemsetAsync(d_rerr.p, 0, r1c * 4, st));
+    p.n_rows = nr;
+    p.n_cols = nc;
+    p.row_col_ptr = d_rcp.as<int64_t>();
+    p.col_qo = d_cqo.as<uint64_t>();
+    p.col_vo = d_cvo.as<uint64_t>();
+    p.col_ts = cb->col_timestamp ? d_cts.as<int64_t>() : nullptr;
+    p.q = d_q.as<uint8_t>();
+    p.v = d_v.as<uint8_t>();
+    p.col_row = d_crow.as<int32_t>();
+    p.col_n = d_cn.as<int64_t>();
+    p.col_off = d_coff.as<int64_t>();
+    p.col_info = d_cinfo.as<uint32_t>();
+    p.row_heap = d_rheap.as<int32_t>();
+    p.row_one = d_rone.as<int64_t>();
+    p.row_err = d_rerr.as<int32_t>();
+    HIP_OK(hipEventRecord(c->ev[0], st));
+    HIP_OK(cmp_analyze(p, &c->cmp_tmp, &c->cmp_tmp_bytes, st));
+    int64_t n_ent = 0;
+    HIP_OK(hipMemcpyAsync(&n_ent, p.col_off + nc, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (n_ent >= kLim) return fail(TSDB_E_NOT_IMPLEMENTED, "more than 2^31 datapoints in one compaction chunk");
+    const int64_t E1 = std::max<int64_t>(1, n_ent);
+    p.n_ent = n_ent;
+    HIP_OK(d_key.ensure(E1 * 8));
+    HIP_OK(d_key2.ensure(E1 * 8));
+    HIP_OK(d_idx.ensure(E1 * 4));
+    HIP_OK(d_idx2.ensure(E1 * 4));
+    HIP_OK(d_ecol.ensure(E1 * 4));
+    HIP_OK(d_eqo.ensure(E1 * 4));
+    HIP_OK(d_evo.ensure(E1 * 4));
+    HIP_OK(d_klen.ensure(E1 * 4));
+    for (DevBuf* b : {&d_sq, &d_sv, &d_sc, &d_sm}) HIP_OK(b->ensure((E1 + 1) * 8));
+    HIP_OK(d_rlo.ensure(r1c * 8));
+    HIP_OK(d_rq.ensure(r1c * 8));
+    HIP_OK(d_rv.ensure(r1c * 8));
+    HIP_OK(d_rstate.ensure(r1c * 4));
+    HIP_OK(d_rmeta.ensure(r1c));
+    p.key = d_key.as<uint64_t>();
+    p.key2 = d_key2.as<uint64_t>();
+    p.idx = d_idx.as<uint32_t>();
+    p.idx2 = d_idx2.as<uint32_t>();
+    p.ent_col = d_ecol.as<uint32_t>();
+    p.ent_qo = d_eqo.as<uint32_t>();
+    p.ent_vo = d_evo.as<uint32_t>();
+    p.klen = d_klen.as<uint32_t>();
+    p.sq = d_sq.as<int64_t>();
+    p.sv = d_sv.as<int64_t>();
+    p.sc = d_sc.as<int64_t>();
+    p.sm = d_sm.as<int64_t>();
+    p.row_lo = d_rlo.as<int64_t>();
+    p.row_q = d_rq.as<int64_t>();
+    p.row_v = d_rv.as<int64_t>();
+    p.row_state = d_rstate.as<int32_t>();
+    p.row_meta = d_rmeta.as<uint8_t>();
+    int rb = 1;
+    while (((int64_t)1 << rb) <= nr) rb++;
+    HIP_OK(cmp_entries(p, &c->cmp_tmp, &c->cmp_tmp_bytes, std::min(64, 22 + rb), st));
+    HIP_OK(hipEventRecord(c->ev[2], st));
+    if (nr) {
+      HIP_OK(hipMemcpyAsync(rq.data() + r0, p.row_q, nr * 8, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipMemcpyAsync(rv.data() + r0, p.row_v, nr * 8, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipMemcpyAsync(rstate.data() + r0, p.row_state, nr * 4, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipMemcpyAsync(rerr.data() + r0, p.row_err, nr * 4, hipMemcpyDeviceToHost, st));
+    }
+    HIP_OK(hipStreamSynchronize(st));
+    float t = 0;
+    (void)hipEventElapsedTime(&t, c->ev[0], c->ev[2]);
+    cmp_ms += t;
+    return 0;
+  };
+  // chunk k (prepared last) to the resident blob at the host's layout
+  auto write = [&](int k) -> int {
+    const int64_t r0 = cuts[k], nr = cuts[k + 1] - r0;
+    HIP_OK(d_rdq.ensure(std::max<int64_t>(1, nr) * 8));
+    HIP_OK(d_rdv.ensure(std::max<int64_t>(1, nr) * 8));
+    if (nr) {
+      HIP_OK(hipMemcpyAsync(d_rdq.p, rdq.data() + r0, nr * 8, hipMemcpyHostToDevice, st));
+      HIP_OK(hipMemcpyAsync(d_rdv.p, rdv.data() + r0, nr * 8, hipMemcpyHostToDevice, st));
+    }
+    p.row_dq = d_rdq.as<int64_t>();
+    p.row_dv = d_rdv.as<int64_t>();
+    p.out_q = c->qual.as<uint8_t>();
+    p.out_v = c->val.as<uint8_t>();
+    HIP_OK(hipEventRecord(c->ev[3], st));
+    HIP_OK(cmp_write(p, st));
+    HIP_OK(hipEventRecord(c->ev[1], st));
+    HIP_OK(hipStreamSynchronize(st));
+    float t = 0;
+    (void)hipEventElapsedTime(&t, c->ev[3], c->ev[1]);
+    cmp_ms += t;
+    return 0;
+  };
+  for (int k = 0; k < n_chunks; k++)
+    if (int rc = prepare(k)) return rc;
   // resident layout: series stable-sorted by group, each series' kept rows by base time
   std::vector<int64_t> order(NS);
   int32_t maxg = -1;
@@ -1506,7 +1605,7 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   auto gkey = [&](int64_t s) { const int32_t g = cb->group_id[s]; return g < 0 ? INT32_MAX : g; };
   std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return gkey(x) < gkey(y); });
   std::vector<tsdbhip_ctx::CmpErr> errs;
-  std::vector<int64_t> rdq(R1, -1), rdv(R1, -1), srp(NS + 1, 0);
+  std::vector<int64_t> srp(NS + 1, 0);
   std::vector<RowDesc> rd;
   std::vector<int32_t> hgroup(NS);
   // Rows of one series with the same base time (salt buckets): Span.addRow merges the second
@@ -1564,20 +1663,14 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   HIP_OK(c->val.ensure(vtot + BLOB_SLACK));
   HIP_OK(hipMemsetAsync(c->qual.p, 0, qtot + BLOB_SLACK, c->stream));
   HIP_OK(hipMemsetAsync(c->val.p, 0, vtot + BLOB_SLACK, c->stream));
-  HIP_OK(d_rdq.ensure(R1 * 8));
-  HIP_OK(d_rdv.ensure(R1 * 8));
-  if (NR) {
-    HIP_OK(hipMemcpyAsync(d_rdq.p, rdq.data(), NR * 8, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(d_rdv.p, rdv.data(), NR * 8, hipMemcpyHostToDevice, c->stream));
+  if (n_chunks == 1) {
+    if (int rc = write(0)) return rc;
+  } else {
+    for (int k = 0; k < n_chunks; k++) {
+      if (int rc = prepare(k)) return rc;
+      if (int rc = write(k)) return rc;
+    }
   }
-  p.row_dq = d_rdq.as<int64_t>();
-  p.row_dv = d_rdv.as<int64_t>();
-  p.out_q = c->qual.as<uint8_t>();
-  p.out_v = c->val.as<uint8_t>();
-  HIP_OK(hipEventRecord(c->ev[3], c->stream));
-  HIP_OK(cmp_write(p, c->stream));
-  HIP_OK(hipEventRecord(c->ev[1], c->stream));
-  HIP_OK(hipStreamSynchronize(c->stream));
   for (const SaltGroup& sg : salt) {   // RowSeq.addRow of each later row, in scan order
     std::vector<uint8_t> lq, lv, q2, v2;
     bool ok = true;
@@ -1599,10 +1692,6 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     d.qlen = (uint32_t)lq.size();
     d.vlen = (uint32_t)lv.size();
   }
-  float t_a = 0, t_w = 0;   // device spans; the host layout between them is not counted
-  (void)hipEventElapsedTime(&t_a, c->ev[0], c->ev[2]);
-  (void)hipEventElapsedTime(&t_w, c->ev[3], c->ev[1]);
-  const double cmp_ms = (double)t_a + t_w;
   // resident batch state (as load_impl)
   c->n_series = NS;
   c->n_groups = maxg + 1;
@@ -1987,6 +2076,7 @@ struct Plan {
   bool anchored = false;
   std::vector<int64_t> anchors;
   std::vector<std::vector<int64_t>> seqs;
+  std::vector<int64_t> fillseq;   // anchored + fill: previousInterval(start) .. previousInterval(end)
 };
 
 bool is_sel_agg(int a) { return a == TSDB_AGG_MEDIAN || (a >= TSDB_AGG_P999 && a < TSDB_AGG_COUNT_ALL); }
@@ -2126,16 +2216,17 @@ int plan_calendar(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
     };
     bool disagree = false;
     for (const auto& sq : seqs) disagree = disagree || !agrees(sq);
-    if (disagree && fill)
-      return fail(TSDB_E_NOT_IMPLEMENTED, "a fill policy over spans on calendar grids that disagree (per-span anchors)");
-    if (fill && !agrees(F)) return fail(TSDB_E_NOT_IMPLEMENTED, "fill grid disagrees with the spans' calendar grids");
-    P.bounds = fill ? F : T;
+    // a fill over grids that disagree (with each other or with the FillingDownsampler's own
+    // sequence): every span's filled output runs through the union evaluator (run_anchored)
+    if (fill && !agrees(F)) disagree = true;
+    P.bounds = fill && !disagree ? F : T;
     c->calc_key = key;
     c->calc_bounds = P.bounds;
     c->calc_seek = sc;
     c->calc_anchored = disagree;
     c->calc_anchors = disagree ? anchors : std::vector<int64_t>();
     c->calc_seqs = disagree ? seqs : std::vector<std::vector<int64_t>>();
+    c->calc_fill = disagree && fill ? F : std::vector<int64_t>();
     c->calc_valid = true;
   }
   // spans on grids that disagree: their union of timestamps is no slot grid; run_anchored
@@ -2144,6 +2235,7 @@ int plan_calendar(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
   if (P.anchored) {
     P.anchors = c->calc_anchors;
     P.seqs = c->calc_seqs;
+    P.fillseq = c->calc_fill;
   }
   P.mode = MODE_TABLE;
   P.seek = c->calc_seek;
@@ -2837,7 +2929,9 @@ const std::vector<int64_t>& local_counts(tsdbhip_ctx* c, int64_t G) {
   std::vector<int64_t>& n = c->lc;
   n.assign(G, 0);
   for (int64_t s = 0; s < c->n_series; s++)
-    if (c->h_group[s] < G) n[c->h_group[s]]++;   // (the sentinel group of ungrouped series is not one)
+    // ungrouped series carry the LOCAL sentinel group n_groups, which can be a real group id
+    // of a wider (global) numbering: not one of its groups
+    if (c->h_group[s] < c->n_groups && c->h_group[s] < G) n[c->h_group[s]]++;
   c->lc_valid = true;
   return n;
 }
@@ -3549,6 +3643,8 @@ int run_anchored(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_
       ext.live[s] = (int64_t)c->h_base[r] >= P.ss && (int64_t)c->h_base[r] < P.se;
   std::vector<std::vector<RawPt>> sp(S);
   const int64_t start = P.ss * 1000;
+  const bool fill = q->ds_fill != TSDB_FILL_NONE;
+  if (fill && q->ds_fill == TSDB_FILL_SCALAR) return fail(TSDB_E_RUNTIME, "unhandled fill policy");
   tsdbhip_query q2 = *q;
   q2.rate = 0;   // RateSpan wraps the Downsampler: the raw evaluator applies it to the buckets
   for (size_t k = 0; k < P.anchors.size(); k++) {
@@ -3585,13 +3681,40 @@ int run_anchored(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_
     for (int64_t s = 0; s < S; s++) {
       if (cls[s] != (int32_t)k) continue;
       for (int64_t j = 0; j < K; j++) {
-        if (!pres[s * K + j] || sq[j] < start) continue;
+        if (!pres[s * K + j] || (sq[j] < start && !fill)) continue;
         RawPt pt;
         pt.tsf = sq[j] | RAW_FLOAT;
         std::memcpy(&pt.bits, &dense[s * K + j], 8);
         sp[s].push_back(pt);
         if (sq[j] % 1000) ext.sec = false;
       }
+    }
+  }
+  if (fill) {
+    // FillingDownsampler.next (src/core/FillingDownsampler.java:172-301): one output per step of
+    // its own calendar sequence, previousInterval(start) up to previousInterval(end) exclusive --
+    // the span's bucket at exactly that timestamp (earlier buckets are consumed), else the fill
+    // value; a span with rows in the scan but no bucket emits fills only
+    const double fv = q->ds_fill == TSDB_FILL_ZERO ? 0.0 : std::numeric_limits<double>::quiet_NaN();
+    uint64_t fbits;
+    std::memcpy(&fbits, &fv, 8);
+    const std::vector<int64_t>& F = P.fillseq;
+    for (int64_t s = 0; s < S; s++) {
+      std::vector<RawPt> out;
+      if (ext.live[s]) {
+        size_t b = 0;
+        for (size_t i = 0; i + 1 < F.size(); i++) {
+          const int64_t t = F[i];
+          while (b < sp[s].size() && (sp[s][b].tsf & RAW_TIME_MASK) < t) b++;
+          RawPt pt;
+          pt.tsf = t | RAW_FLOAT;
+          pt.bits = b < sp[s].size() && (sp[s][b].tsf & RAW_TIME_MASK) == t ? sp[s][b].bits : fbits;
+          if (t < start) continue;
+          out.push_back(pt);
+          if (t % 1000) ext.sec = false;
+        }
+      }
+      sp[s].swap(out);
     }
   }
   for (int64_t s = 0; s < S; s++) {
@@ -3719,7 +3842,7 @@ void ro_activity(const tsdbhip_ctx* c, const Plan& P, int64_t G, std::vector<uin
   for (int64_t i = 0; i < c->n_series; i++) {
     if (P.none) {
       if (i < G) act[i] = c->h_orig[i] < c->ro_nval ? (act[i] | c->ro_scan_act[i]) : 0;
-    } else if (c->ro_scan_act[i] && c->h_group[i] < G) {
+    } else if (c->ro_scan_act[i] && c->h_group[i] < c->n_groups && c->h_group[i] < G) {
       act[c->h_group[i]] = 1;
     }
   }

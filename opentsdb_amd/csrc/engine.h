@@ -379,6 +379,8 @@ struct CmpParams {
 hipError_t cmp_analyze(CmpParams& p, void** tmp, size_t* tmp_bytes, hipStream_t s);   // through k_cmp_cols, col_off
 hipError_t cmp_entries(CmpParams& p, void** tmp, size_t* tmp_bytes, int end_bit, hipStream_t s);   // explode, sort, dedup, scans, rows
 hipError_t cmp_write(const CmpParams& p, hipStream_t s);
+// dst = src - base over n offsets (a chunk of the scan, rebased); *bad |= 1 unless non-decreasing and >= base
+hipError_t cmp_rebase(const uint64_t* src, uint64_t* dst, int64_t n, uint64_t base, int32_t* bad, hipStream_t s);
 
 // rollup read path: value series buckets <- Σsum / Σcount (avg) or Σcount, from the SUM
 // downsampling of each value series and of its count series (cmap[s], -1: none)

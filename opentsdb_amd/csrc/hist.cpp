@@ -25,6 +25,9 @@ std::mutex& ctx_mutex(tsdbhip_ctx* c);
 void*& ctx_hist(tsdbhip_ctx* c);
 bool ctx_is_md(tsdbhip_ctx* c);
 int set_error(int code, const std::string& msg);
+bool cal_prev_tz(const tsdbhip_tz* z, int64_t ts, int64_t n, int unit, int64_t* out);
+int64_t cal_step_tz(const tsdbhip_tz* z, int64_t t, int unit, int64_t n);
+int64_t cal_unit_ms(int unit);
 
 namespace {
 
@@ -65,10 +68,13 @@ struct HistStore {
   int64_t max_ts = 0;                           // largest datapoint timestamp of the store (ms)
   std::vector<uint32_t> h_dlo, h_dup;           // dictionary bounds (float bits), TreeMap order
   std::vector<int64_t> sp_row;                  // [n_series + 1] kept rows of each span (base-time order)
+  std::vector<int64_t> h_pos_ts, h_row_pos;     // host copies (calendar anchors are planned on the host)
   std::vector<uint32_t> row_base;               // [kept rows]
   std::vector<int32_t> group;                   // [n_series]
   // query scratch
   Buf q_rlo, q_rhi, q_out, q_slot, q_key, q_key2, q_pos, q_pos2, q_head, q_incl, q_point, q_ptts, q_ptgrp;
+  Buf q_vlen, q_voff, q_vpos;   // windowed accumulation: the spans' positions in output-group order
+  Buf q_caltab, q_spcal;         // calendar downsampling: boundary runs per span anchor
   Buf acc, pres, pkind, flag, ptout, err, pct;
   Buf o_ts, o_grp, o_kind, o_pct, o_cnt, o_pres;
   void* tmp = nullptr;
@@ -76,7 +82,7 @@ struct HistStore {
   void release() {
     for (Buf* b : {&val, &voff, &codec, &status, &hkey, &hcount, &hidx, &dlo, &dup, &lkey, &lidx, &pos_cell, &pos_ts, &pos_kind,
                    &row_pos, &q_rlo, &q_rhi, &q_out, &q_slot, &q_key, &q_key2, &q_pos, &q_pos2, &q_head, &q_incl,
-                   &q_point, &q_ptts, &q_ptgrp, &acc, &pres, &pkind, &flag, &ptout, &err, &pct, &o_ts, &o_grp,
+                   &q_point, &q_ptts, &q_ptgrp, &q_vlen, &q_voff, &q_vpos, &q_caltab, &q_spcal, &acc, &pres, &pkind, &flag, &ptout, &err, &pct, &o_ts, &o_grp,
                    &o_kind, &o_pct, &o_cnt, &o_pres})
       b->release();
     if (tmp) (void)hipFree(tmp);
@@ -299,6 +305,8 @@ extern "C" int tsdbhip_load_histograms(tsdbhip_ctx* c, const tsdbhip_hist_batch*
   }
   HOK(hipMemcpyAsync(S->row_pos.p, row_pos.data(), row_pos.size() * 8, hipMemcpyHostToDevice, st));
   HOK(hipStreamSynchronize(st));
+  S->h_pos_ts.swap(pos_ts);
+  S->h_row_pos.swap(row_pos);
   S->loaded = true;
   return 0;
 }
@@ -317,7 +325,7 @@ int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end,
   int ds;
   if (q->ds_function < 0) ds = 0;
   else if (q->ds_all) ds = 2;
-  else if (q->ds_calendar) return set_error(TSDB_E_NOT_IMPLEMENTED, "calendar downsampling of histograms");
+  else if (q->ds_calendar) ds = 3;
   else ds = 1;
   if (ds == 1 && q->ds_interval_ms <= 0) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "downsampling interval must be positive");
   // the spans the scan returns (rows with base in [ss, se)) and the groups they form
@@ -357,6 +365,22 @@ int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end,
     rhi.push_back(hi[s]);
     sout.push_back(o);
   }
+  if (!none && !sout.empty()) {   // spans by output group (stable): a group's datapoints become contiguous
+    std::vector<int64_t> first(gid_of_out.size() + 1, 0);
+    for (int32_t o : sout) first[o + 1]++;
+    for (size_t g = 0; g < gid_of_out.size(); g++) first[g + 1] += first[g];
+    std::vector<int64_t> r2(rlo.size()), h2(rhi.size());
+    std::vector<int32_t> o2(sout.size());
+    for (size_t i = 0; i < sout.size(); i++) {
+      const int64_t k = first[sout[i]]++;
+      r2[k] = rlo[i];
+      h2[k] = rhi[i];
+      o2[k] = sout[i];
+    }
+    rlo.swap(r2);
+    rhi.swap(h2);
+    sout.swap(o2);
+  }
   const int64_t G = (int64_t)gid_of_out.size(), nsp = (int64_t)rlo.size();
   if (G >= ((int64_t)1 << 21)) return set_error(TSDB_E_NOT_IMPLEMENTED, "more than 2^21 histogram groups in one query");
   const int64_t NP = S->n_pos;
@@ -390,6 +414,81 @@ int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end,
     p.B0 = q->end_time;   // the clone's timestamp: HistogramDownsampler.timestamp field = the query end (:179-183, 334-345)
     p.K = 1;
   }
+  if (ds == 3) {
+    // HistogramDownsampler with a calendar interval: seekInterval's target (previousInterval of
+    // the span group start, stepped once when the start is past it), then per span the intervals
+    // from previousInterval(its first datapoint after the seek) -- one boundary run per distinct
+    // anchor, reaching past the span's last datapoint
+    const int unit = q->ds_calendar;
+    const int64_t um = cal_unit_ms(unit);
+    const int64_t n = um > 0 ? q->ds_interval_ms / um : 0;
+    if (n < 1) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "Interval must be greater than zero");
+    if (start < 0) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "Timestamp cannot be less than zero");
+    const tsdbhip_tz* z = q->ds_tz;
+    int64_t c = 0;
+    cal_prev_tz(z, start, n, unit, &c);
+    if (start > c) c = cal_step_tz(z, c, unit, n);
+    p.cal_seek = c;
+    const std::vector<int64_t>& rp = S->h_row_pos;
+    const std::vector<int64_t>& pt = S->h_pos_ts;
+    auto seek = [&](int64_t rl, int64_t rh, int64_t target) {   // k_hist.hip span_seek
+      int64_t ri = rl;
+      for (int64_t r = rl; r < rh; r++) {
+        if (rp[r + 1] - rp[r] < 1 || pt[rp[r + 1] - 1] < target) ri++;
+        else break;
+      }
+      if (ri == rh) --ri;
+      int64_t qq = rp[ri];
+      while (qq < rp[ri + 1] && pt[qq] < target) ++qq;
+      return qq;
+    };
+    std::vector<int64_t> anchor(nsp, INT64_MIN);
+    std::vector<std::pair<int64_t, int64_t>> need;   // (anchor, latest datapoint its run must pass)
+    for (int64_t i = 0; i < nsp; i++) {
+      const int64_t q0 = seek(rlo[i], rhi[i], c), p1 = rp[rhi[i]];
+      if (q0 >= p1) continue;
+      if (pt[q0] < 0) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "Timestamp cannot be less than zero");
+      cal_prev_tz(z, pt[q0], n, unit, &anchor[i]);
+      int64_t mx = pt[q0];
+      for (int64_t k = q0; k < p1; k++) mx = std::max(mx, pt[k]);
+      need.emplace_back(anchor[i], mx);
+    }
+    std::sort(need.begin(), need.end());
+    std::vector<int64_t> tab, run_a, run_off, run_n;
+    for (size_t k = 0; k < need.size();) {
+      size_t k1 = k;
+      int64_t reach = need[k].second;
+      while (k1 < need.size() && need[k1].first == need[k].first) reach = std::max(reach, need[k1++].second);
+      run_a.push_back(need[k].first);
+      run_off.push_back((int64_t)tab.size());
+      int64_t b = need[k].first;
+      tab.push_back(b);
+      while (b <= reach) {
+        b = cal_step_tz(z, b, unit, n);
+        tab.push_back(b);
+        if (tab.size() > ((size_t)1 << 27))
+          return set_error(TSDB_E_NOT_IMPLEMENTED, "more than 2^27 calendar intervals in one histogram query");
+      }
+      run_n.push_back((int64_t)tab.size() - run_off.back());
+      k = k1;
+    }
+    std::vector<int64_t> spc(2 * std::max<int64_t>(1, nsp), 0);
+    for (int64_t i = 0; i < nsp; i++) {
+      if (anchor[i] == INT64_MIN) continue;
+      const size_t r = std::lower_bound(run_a.begin(), run_a.end(), anchor[i]) - run_a.begin();
+      spc[2 * i] = run_off[r];
+      spc[2 * i + 1] = run_n[r];
+    }
+    if (tab.empty()) tab.push_back(0);
+    HOK(S->q_caltab.ensure(tab.size() * 8));
+    HOK(S->q_spcal.ensure(spc.size() * 8));
+    HOK(hipMemcpyAsync(S->q_caltab.p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice, st));
+    HOK(hipMemcpyAsync(S->q_spcal.p, spc.data(), spc.size() * 8, hipMemcpyHostToDevice, st));
+    HOK(hipStreamSynchronize(st));   // (tab / spc leave scope)
+    p.cal_tab = S->q_caltab.as<int64_t>();
+    p.sp_cal = S->q_spcal.as<int64_t>();
+  }
+  const bool sparse = ds == 0 || ds == 3;
   HOK(S->q_rlo.ensure(nsp * 8 + 8));
   HOK(S->q_rhi.ensure(nsp * 8 + 8));
   HOK(S->q_out.ensure(nsp * 4 + 4));
@@ -404,7 +503,7 @@ int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end,
   p.sp_rhi = S->q_rhi.as<int64_t>();
   p.sp_out = S->q_out.as<int32_t>();
   p.err = S->err.as<int32_t>();
-  if (ds == 0) {
+  if (sparse) {
     if (NP >= ((int64_t)1 << 31)) return set_error(TSDB_E_NOT_IMPLEMENTED, "more than 2^31 histogram datapoints without downsampling");
     HOK(S->q_key.ensure(NP * 8 + 8));
     HOK(hipMemsetAsync(S->q_key.p, 0xFF, NP * 8 + 8, st));
@@ -426,7 +525,7 @@ int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end,
   auto why = [&](int w) { return std::string(w >= 0 && w <= 6 ? WHY[w] : "?"); };
   if (err[0]) return set_error(err[0], why(err[1]));
   int64_t n_points;
-  if (ds == 0) {
+  if (sparse) {
     HOK(S->q_key2.ensure(NP * 8 + 8));
     HOK(S->q_pos.ensure(NP * 4 + 4));
     HOK(S->q_pos2.ensure(NP * 4 + 4));
@@ -463,7 +562,18 @@ int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end,
     p.pres = S->pres.as<uint32_t>();
   }
   if (const char* dbg = getenv("TSDBHIP_HIST_DBG")) p.dbg = atoi(dbg);
-  HOK(hist_accum(p, NP, S->lds_dict ? S->lkey.as<uint64_t>() : nullptr, S->lds_dict ? S->lidx.as<int32_t>() : nullptr, st));
+  const char* wenv = getenv("TSDBHIP_HIST_WINDOW");   // tests: 0 = the per-column atomic kernel
+  if (S->lds_dict && hist_window_points(p) > 0 && !(wenv && wenv[0] == '0')) {
+    HOK(S->q_vlen.ensure(nsp * 4 + 4));
+    HOK(S->q_voff.ensure(nsp * 8 + 16));
+    HOK(S->q_vpos.ensure(NP * 4 + 4));
+    int64_t nvp = 0;
+    HOK(hist_vpos(S->q_rlo.as<int64_t>(), S->q_rhi.as<int64_t>(), S->row_pos.as<int64_t>(), nsp, S->q_vlen.as<uint32_t>(),
+                  S->q_voff.as<int64_t>(), S->q_vpos.as<int32_t>(), &nvp, &S->tmp, &S->tmp_bytes, st));
+    HOK(hist_accum_window(p, S->q_vpos.as<int32_t>(), nvp, S->lkey.as<uint64_t>(), S->lidx.as<int32_t>(), st));
+  } else {
+    HOK(hist_accum(p, NP, S->lds_dict ? S->lkey.as<uint64_t>() : nullptr, S->lds_dict ? S->lidx.as<int32_t>() : nullptr, st));
+  }
   HOK(S->flag.ensure(n_points * 4 + 4));
   HOK(S->ptout.ensure(n_points * 8 + 16));
   HOK(hist_flags(p, S->flag.as<uint32_t>(), st));

@@ -54,11 +54,14 @@ struct HistQueryParams {
   // geometry (ms)
   int64_t start, end;        // HistogramSpanGroup start / end (scan bounds)
   int64_t qs, qe;            // query start / end ("all")
-  int32_t ds;                // 0 none, 1 fixed interval, 2 all
+  int32_t ds;                // 0 none, 1 fixed interval, 2 all, 3 calendar (union of per-span intervals)
   int32_t ds_sum;            // the downsampling function is "sum"
   int64_t I;                 // interval
   int64_t B0;                // slot 0 timestamp (dense modes)
   int64_t K;                 // slots per group (dense modes)
+  const int64_t* cal_tab;    // calendar: interval boundaries, one run per distinct span anchor
+  const int64_t* sp_cal;     // calendar: [n_spans][2] first boundary of the span's run, boundaries in it
+  int64_t cal_seek;          // calendar: HistogramDownsampler.seekInterval's target
   // outputs of k_hist_slots
   int32_t* pos_slot;         // [n_pos] slot (dense) or -1
   int64_t* pos_key;          // [n_pos] sparse mode: (group << 42 | ts - start) or -1
@@ -90,6 +93,15 @@ hipError_t hist_slots(const HistQueryParams& p, hipStream_t s);
 // lkey / lidx: the dictionary as an LDICT-slot table for LDS (k_hist.hip), or null
 hipError_t hist_accum(const HistQueryParams& p, int64_t n_pos, const uint64_t* lkey, const int32_t* lidx, hipStream_t s);
 static constexpr int HIST_LDICT = 1024;
+static constexpr int64_t HIST_WLDS = 80 * 1024;   // LDS of a k_hist_accw block (two blocks per CU)
+// the present spans' in-range positions in span order: vpos[off[i] .. off[i + 1]) = span i's
+hipError_t hist_vpos(const int64_t* rlo, const int64_t* rhi, const int64_t* row_pos, int64_t n_spans, uint32_t* len,
+                     int64_t* off, int32_t* vpos, int64_t* nvp, void** tmp, size_t* tmp_bytes, hipStream_t s);
+// points of the k_hist_accw LDS window for this query (0: the counters do not fit, use hist_accum)
+int hist_window_points(const HistQueryParams& p);
+// windowed accumulation over vpos (spans sorted by output group); needs the LDS dictionary
+hipError_t hist_accum_window(const HistQueryParams& p, const int32_t* vpos, int64_t nvp, const uint64_t* lkey,
+                             const int32_t* lidx, hipStream_t s);
 hipError_t hist_flags(const HistQueryParams& p, uint32_t* flag, hipStream_t s);   // [n_points] 1 = emitted
 hipError_t hist_final(const HistQueryParams& p, hipStream_t s);
 hipError_t hist_scan(const uint32_t* flag, int64_t* out, int64_t n, void** tmp, size_t* tmp_bytes, hipStream_t s);

@@ -400,6 +400,21 @@ hipError_t cmp_entries(CmpParams& p, void** tmp, size_t* tmp_bytes, int end_bit,
   return hipGetLastError();
 }
 
+// dst[i] = src[i] - base over n values; bad |= 1 when the values decrease or start below base
+__global__ __launch_bounds__(256) void k_cmp_rebase(const uint64_t* src, uint64_t* dst, int64_t n, uint64_t base,
+                                                    int32_t* bad) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t v = src[i];
+  if (v < base || (i + 1 < n && src[i + 1] < v)) atomicOr(bad, 1);
+  dst[i] = v - base;
+}
+
+hipError_t cmp_rebase(const uint64_t* src, uint64_t* dst, int64_t n, uint64_t base, int32_t* bad, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_cmp_rebase, dim3(blocks_of(n)), dim3(256), 0, s, src, dst, n, base, bad);
+  return hipGetLastError();
+}
+
 hipError_t cmp_write(const CmpParams& p, hipStream_t s) {
   if (p.n_ent > 0) hipLaunchKernelGGL(k_cmp_write, dim3(blocks_of(p.n_ent)), dim3(256), 0, s, p);
   if (p.n_rows > 0) hipLaunchKernelGGL(k_cmp_rowfix, dim3(blocks_of(p.n_rows)), dim3(256), 0, s, p);

@@ -24,6 +24,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace tsdb {
 
@@ -170,7 +171,7 @@ __global__ void k_hist_slots(HistQueryParams p) {
   if ((last & (int64_t)0xFFFFFFFF00000000LL) == 0) last *= 1000;
   if (!(first <= p.end && last >= p.start)) return;
   const int64_t g = p.sp_out[s];
-  const int64_t target = p.ds == 1 ? (p.start + p.I - 1) - (p.start + p.I - 1) % p.I : p.start;
+  const int64_t target = p.ds == 1 ? (p.start + p.I - 1) - (p.start + p.I - 1) % p.I : (p.ds == 3 ? p.cal_seek : p.start);
   if (target & (int64_t)0xFFFFF00000000000LL) { set_err(p.err, -3 /* IAE */, WHY_SEEK); return; }
   int64_t q = span_seek(p, rlo, rhi, target);
   if (p.ds == 0) {
@@ -205,6 +206,30 @@ __global__ void k_hist_slots(HistQueryParams p) {
       if (ts < p.qs) continue;
       if (ts >= p.qe) break;
       p.pos_slot[r] = (int32_t)g;
+    }
+    return;
+  }
+  if (p.ds == 3) {
+    // calendar (:219-248, 282-300, 309-331): intervals from previousInterval(the first datapoint
+    // after the seek) stepped by the calendar unit -- the host's boundary run of this span's
+    // anchor; outputs are keyed like raw datapoints and merged over the union of timestamps
+    const int64_t* tab = p.cal_tab + p.sp_cal[2 * s];
+    const int64_t nb = p.sp_cal[2 * s + 1];
+    int64_t j = 0, prev = INT64_MIN;
+    for (bool firstout = true; q < p1; firstout = false) {
+      const int64_t a = p.pos_ts[q];
+      while (j + 1 < nb && tab[j + 1] <= a) j++;
+      const int64_t ots = tab[j];
+      const int64_t tei = j + 1 < nb ? tab[j + 1] : INT64_MAX;
+      int64_t e = q;
+      while (e < p1 && p.pos_ts[e] < tei) e++;
+      if (e - q >= 2 && !p.ds_sum) { set_err(p.err, -10, WHY_NPE); return; }
+      if (firstout && ots < p.start) return;
+      if (ots == 0 || ots > p.end) return;
+      if (ots <= prev) { set_err(p.err, -22, WHY_UNSORTED); return; }
+      prev = ots;
+      for (int64_t r = q; r < e; r++) p.pos_key[r] = (g << 42) | (ots - p.start);
+      q = e;
     }
     return;
   }
@@ -484,6 +509,240 @@ __global__ void k_iota(uint32_t* v, int64_t n) {
   if (i < n) v[i] = (uint32_t)i;
 }
 
+// ---- windowed accumulation ---------------------------------------------------------------
+// The datapoints in SpanGroup order (vpos: the present spans sorted by output group, each span's
+// in-range positions), each block a contiguous chunk of them.  A group's spans all land on the
+// group's points, so a block keeps a window of WS consecutive points' [C] counters in LDS, adds
+// there with LDS atomics and flushes the window to the global accumulator (contiguous 64-bit
+// atomics, one per nonzero counter) only when a tile's points leave it.  Columns are staged in
+// LDS per run of consecutive cells (up to WRUNS runs a tile) and parsed with unaligned dword
+// reads (bucket key, one-dword varints).
+
+static constexpr int WRUNS = 8;
+
+__global__ void k_hist_vlen(const int64_t* rlo, const int64_t* rhi, const int64_t* row_pos, int64_t n, uint32_t* len) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) len[i] = (uint32_t)(row_pos[rhi[i]] - row_pos[rlo[i]]);
+}
+__global__ void k_hist_vpos(const int64_t* rlo, const int64_t* row_pos, const int64_t* off, int32_t* vpos) {
+  const int64_t sp = blockIdx.x;
+  const int64_t p0 = row_pos[rlo[sp]], o = off[sp], n = off[sp + 1] - o;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) vpos[o + i] = (int32_t)(p0 + i);
+}
+
+// little-endian dword of the bytes [i, i + 4) of a byte stream held as aligned dwords
+__device__ __forceinline__ uint32_t udw(const uint32_t* w, uint64_t i) {
+  const uint64_t k = i >> 2;
+  return __builtin_amdgcn_alignbyte(w[k + 1], w[k], (uint32_t)(i & 3));
+}
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+struct SrcW {   // LDS stage or global bytes, read as unaligned dwords
+  const uint32_t* w;
+  __device__ __forceinline__ uint32_t at(uint64_t i) const { return (udw(w, i) & 0xFF); }
+  __device__ __forceinline__ uint32_t dw(uint64_t i) const { return udw(w, i); }
+};
+
+// Kryo readLong(true) from one dword when the varint has at most 4 bytes; else byte by byte
+__device__ __forceinline__ uint64_t wvarlong(const SrcW& s, uint64_t& i) {
+  const uint32_t x = s.dw(i);
+  const uint32_t m = ~x & 0x80808080u;
+  if (m) {
+    const uint32_t L = (__builtin_ctz(m) >> 3) + 1;
+    uint32_t v = (x & 0x7Fu) | ((x >> 1) & 0x3F80u) | ((x >> 2) & 0x1FC000u) | ((x >> 3) & 0xFE00000u);
+    v &= (L == 4) ? 0x0FFFFFFFu : ((1u << (7 * L)) - 1);
+    i += L;
+    return v;
+  }
+  return svarlong(s, i);
+}
+__device__ __forceinline__ uint64_t wkey(const SrcW& s, uint64_t i) {
+  return ((uint64_t)fcanon(bswap32(s.dw(i))) << 32) | fcanon(bswap32(s.dw(i + 4)));
+}
+
+struct Window {
+  uint64_t* acc;     // [WS * C]
+  uint32_t* kind;    // [WS]
+  uint32_t* pres;    // [WS * W]
+};
+
+__device__ __forceinline__ void w_add(const HistQueryParams& p, const Window& w, int32_t local, int32_t pt, int col,
+                                      uint64_t v) {
+  if (!v) return;
+  if (local >= 0) atomicAdd((unsigned long long*)&w.acc[(uint32_t)local * (uint32_t)p.C + col], (unsigned long long)v);
+  else atomicAdd((unsigned long long*)&p.acc[(uint64_t)pt * p.C + col], (unsigned long long)v);
+}
+
+__device__ void accum_column_w(const HistQueryParams& p, const Window& w, int32_t pt, int32_t local, const SrcW& src,
+                               uint64_t i0, uint8_t kind_st, const DictLds& dict) {
+  const uint8_t kind = kind_st & HC_KIND;
+  const uint32_t kb = kind == HC_SIMPLE ? 1u : 2u;
+  if (local >= 0) atomicOr(&w.kind[local], kb);
+  else atomicOr(&p.pkind[pt], kb);
+  if (kind == HC_LONG) {   // LongHistogramDataPointForTest.aggregate: the 8-byte data adds
+    const uint64_t v = ((uint64_t)bswap32(src.dw(i0 + 1)) << 32) | bswap32(src.dw(i0 + 5));
+    w_add(p, w, local, pt, p.C - 1, v);
+    return;
+  }
+  const bool unsorted = (kind_st & HC_UNSORTED) != 0;
+  const int cnt = (int16_t)((src.at(i0 + 1) << 8) | src.at(i0 + 2));
+  uint64_t i = i0 + 3;
+#pragma unroll 1
+  for (int j = 0; j < cnt; j++) {   // SimpleHistogram.aggregate (:246-261): counts of equal keys add
+    const uint64_t key = wkey(src, i);
+    i += 8;
+    uint64_t val = wvarlong(src, i);
+    if (unsorted && key_recurs(src, i, j, cnt, key)) val = 0;   // a later bucket's count replaces it
+    const int32_t di = dict.find(key);
+    if (di < 0) {
+      set_err(p.err, -22, WHY_DICT);
+      continue;
+    }
+    if (!(p.dbg & 1)) w_add(p, w, local, pt, di, val);
+    if (p.pres) {
+      if (local >= 0) atomicOr(&w.pres[(uint32_t)local * (uint32_t)p.W + (di >> 5)], 1u << (di & 31));
+      else atomicOr(&p.pres[(uint64_t)pt * p.W + (di >> 5)], 1u << (di & 31));
+    }
+  }
+  const uint64_t under = wvarlong(src, i);   // underflow, overflow (:256-257)
+  const uint64_t over = wvarlong(src, i);
+  w_add(p, w, local, pt, p.D, under);
+  w_add(p, w, local, pt, p.D + 1, over);
+}
+
+// the window's counters to the global accumulator (points [wb, wb + WS)), zeroed for the next
+__device__ void w_flush(const HistQueryParams& p, const Window& w, int64_t wb, int WS) {
+  __syncthreads();
+  const int64_t lim = (p.n_points - wb) * p.C;   // counters of real points
+  const int nc = WS * p.C;
+  uint64_t* g = p.acc + (uint64_t)wb * p.C;
+  for (int e = threadIdx.x; e < nc; e += blockDim.x) {
+    const uint64_t v = w.acc[e];
+    if (v && e < lim) atomicAdd((unsigned long long*)&g[e], (unsigned long long)v);
+    w.acc[e] = 0;
+  }
+  for (int e = threadIdx.x; e < WS; e += blockDim.x) {
+    const uint32_t v = w.kind[e];
+    if (v && wb + e < p.n_points) atomicOr(&p.pkind[wb + e], v);
+    w.kind[e] = 0;
+  }
+  if (p.pres) {
+    const int np = WS * p.W;
+    for (int e = threadIdx.x; e < np; e += blockDim.x) {
+      const uint32_t v = w.pres[e];
+      if (v && wb + e / p.W < p.n_points) atomicOr(&p.pres[(uint64_t)wb * p.W + e], v);
+      w.pres[e] = 0;
+    }
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(ATP) k_hist_accw(HistQueryParams p, const int32_t* __restrict__ vpos, int64_t nvp,
+                                                   int64_t chunk, const uint64_t* lkey_g, const int32_t* lidx_g, int WS) {
+  extern __shared__ uint64_t smem64[];
+  uint32_t* stage = reinterpret_cast<uint32_t*>(smem64);                         // STAGE_W + 8 dwords
+  uint64_t* lkey = smem64 + (STAGE_W + 8) / 2;                                    // LDICT
+  int32_t* lidx = reinterpret_cast<int32_t*>(lkey + LDICT);                       // LDICT
+  uint64_t* wacc = reinterpret_cast<uint64_t*>(lidx + LDICT);                     // WS * C
+  uint32_t* wkind = reinterpret_cast<uint32_t*>(wacc + (size_t)WS * p.C);        // WS
+  uint32_t* wpres = wkind + WS;                                                   // WS * W
+  __shared__ int32_t red[4];
+  __shared__ int32_t wheads[2];
+  __shared__ uint64_t run_b0[WRUNS], run_b1[WRUNS];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int k = tid; k < LDICT; k += ATP) { lkey[k] = lkey_g[k]; lidx[k] = lidx_g[k]; }
+  const int nwin = WS * p.C;
+  for (int e = tid; e < nwin; e += ATP) wacc[e] = 0;
+  for (int e = tid; e < WS; e += ATP) wkind[e] = 0;
+  if (p.pres) for (int e = tid; e < WS * p.W; e += ATP) wpres[e] = 0;
+  const Window win{wacc, wkind, wpres};
+  const DictLds dict{lkey, lidx};
+  const int64_t v0 = (int64_t)blockIdx.x * chunk, v1 = min(nvp, v0 + chunk);
+  int64_t wb = -1;
+  for (int64_t t0 = v0; t0 < v1; t0 += ATP) {
+    const int64_t v = t0 + tid;
+    const bool in = v < v1;
+    const int64_t q = in ? (int64_t)vpos[v] : -1;
+    const int32_t pt = in ? (p.pos_point ? p.pos_point[q] : p.pos_slot[q]) : -1;
+    // the tile's point range
+    int32_t mn = pt >= 0 ? pt : INT32_MAX, mx = pt;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      mn = min(mn, __shfl_xor(mn, d));
+      mx = max(mx, __shfl_xor(mx, d));
+    }
+    __syncthreads();   // the previous tile's stage and descriptors are consumed
+    if (lane == 0) { red[wv * 2] = mn; red[wv * 2 + 1] = mx; }
+    // runs of consecutive cells (the stage plan)
+    const int64_t c = in ? p.pos_cell[q] : 0;
+    const int64_t cprev = __shfl_up(c, 1);
+    const bool inprev = __shfl_up((int)in, 1) != 0;
+    bool head = in && (lane == 0 || !inprev || c != cprev + 1);
+    const uint64_t hb = __ballot(head);
+    if (lane == 0) wheads[wv] = __popcll(hb);
+    __syncthreads();
+    mn = min(red[0], red[2]);
+    mx = max(red[1], red[3]);
+    if (mx < 0) continue;   // (block-uniform)
+    if (wb < 0 || mn < wb || mx >= wb + WS) {
+      if (wb >= 0) w_flush(p, win, wb, WS);
+      wb = mn;
+    }
+    // a run that crosses the wave boundary continues in wave 1's lane 0
+    const int nh0 = wheads[0], nruns = nh0 + wheads[1];
+    const int rid = (wv ? nh0 : 0) + (int)__popcll(hb & ((1ull << lane) - 1)) - (head ? 0 : 1);
+    const bool fit = nruns <= WRUNS;
+    if (fit && in) {
+      const uint64_t nxt_c = __shfl_down(c, 1);
+      const bool nxt_in = __shfl_down((int)in, 1) != 0;
+      // the last lane of a run: the next lane starts another run, is out, or is in the next wave
+      bool last = lane == 63 || !nxt_in || nxt_c != (uint64_t)c + 1;
+      if (lane == 63 && wv == 0) {
+        // continues into wave 1 only when wave 1's lane 0 is not a head: read it through LDS
+        last = true;
+      }
+      if (head) run_b0[rid] = p.voff[c];
+      if (last) run_b1[rid] = p.voff[c + 1];
+    }
+    __syncthreads();
+    // run r's dwords [w0, w1) at LDS dword base; wave 0's last run may continue in wave 1: the
+    // descriptor of a run that does not start with a head in wave 1 lane 0 is merged below
+    uint64_t my_b0 = 0;
+    uint32_t my_base = 0;
+    bool staged = fit;
+    if (fit) {
+      uint32_t base = 0;
+      for (int r = 0; r < nruns; r++) {
+        const uint64_t w0 = run_b0[r] >> 2, w1 = (run_b1[r] + 3) >> 2;
+        if (r == rid) { my_b0 = w0; my_base = base; }
+        base += (uint32_t)(w1 - w0);
+      }
+      staged = base <= (uint32_t)STAGE_W;
+      if (staged) {
+        uint32_t b = 0;
+        for (int r = 0; r < nruns; r++) {
+          const uint64_t w0 = run_b0[r] >> 2, w1 = (run_b1[r] + 3) >> 2;
+          const uint32_t* g = reinterpret_cast<const uint32_t*>(p.val) + w0;
+          const uint32_t n = (uint32_t)(w1 - w0);
+          for (uint32_t k = tid; k < n; k += ATP) stage[b + k] = g[k];
+          b += n;
+        }
+        __syncthreads();
+      }
+    }
+    if (pt < 0) continue;
+    const int32_t local = pt - wb < WS ? (int32_t)(pt - wb) : -1;
+    const uint8_t kind = p.pos_kind[q];
+    if (staged) {
+      const uint64_t i0 = (uint64_t)my_base * 4 + (p.voff[c] - my_b0 * 4);
+      accum_column_w(p, win, pt, local, SrcW{stage}, i0, kind, dict);
+    } else {
+      accum_column_w(p, win, pt, local, SrcW{reinterpret_cast<const uint32_t*>(p.val)}, p.voff[c], kind, dict);
+    }
+  }
+  if (wb >= 0) w_flush(p, win, wb, WS);
+}
+
 }  // namespace
 
 // exclusive scan of n flags into out[0 .. n] (out[n] = total)
@@ -553,6 +812,47 @@ hipError_t hist_accum(const HistQueryParams& p, int64_t n_pos, const uint64_t* l
   const unsigned grid = (unsigned)std::min<int64_t>(tiles, (int64_t)cus * 4);
   if (lkey) hipLaunchKernelGGL(k_hist_accum<true>, dim3(grid), dim3(ATP), 0, s, p, n_pos, lkey, lidx);
   else hipLaunchKernelGGL(k_hist_accum<false>, dim3(grid), dim3(ATP), 0, s, p, n_pos, lkey, lidx);
+  return hipGetLastError();
+}
+hipError_t hist_vpos(const int64_t* rlo, const int64_t* rhi, const int64_t* row_pos, int64_t n_spans, uint32_t* len,
+                     int64_t* off, int32_t* vpos, int64_t* nvp, void** tmp, size_t* tmp_bytes, hipStream_t s) {
+  *nvp = 0;
+  if (n_spans <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hist_vlen, dim3((unsigned)((n_spans + 255) / 256)), dim3(256), 0, s, rlo, rhi, row_pos, n_spans, len);
+  hipError_t e = hist_scan(len, off, n_spans, tmp, tmp_bytes, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_hist_vpos, dim3((unsigned)n_spans), dim3(256), 0, s, rlo, row_pos, off, vpos);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = hipMemcpyAsync(nvp, off + n_spans, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+  return hipStreamSynchronize(s);
+}
+
+int hist_window_points(const HistQueryParams& p) {
+  const int64_t fixed = (int64_t)(STAGE_W + 8) * 4 + (int64_t)LDICT * 12;
+  const int64_t per = (int64_t)p.C * 8 + 4 + (p.pres ? (int64_t)p.W * 4 : 0);
+  int64_t ws = (HIST_WLDS - fixed) / per;
+  if (ws < 32) return 0;
+  if (const char* e = getenv("TSDBHIP_HIST_WS")) ws = std::min<int64_t>(ws, std::max(1, atoi(e)));   // tests: tiny windows
+  return (int)std::min<int64_t>(ws, 4096);
+}
+
+hipError_t hist_accum_window(const HistQueryParams& p, const int32_t* vpos, int64_t nvp, const uint64_t* lkey,
+                             const int32_t* lidx, hipStream_t s) {
+  if (nvp <= 0) return hipSuccess;
+  const int WS = hist_window_points(p);
+  if (WS <= 0 || !lkey) return hipErrorInvalidValue;
+  const size_t lds = (size_t)(STAGE_W + 8) * 4 + (size_t)LDICT * 12 + (size_t)WS * p.C * 8 + (size_t)WS * 4 +
+                     (p.pres ? (size_t)WS * p.W * 4 : 0);
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_hist_accw), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return e;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t tiles = (nvp + ATP - 1) / ATP;
+  const int64_t want = std::min<int64_t>(tiles, (int64_t)cus * 2);
+  const int64_t chunk = ((tiles + want - 1) / want) * ATP;
+  const unsigned grid = (unsigned)((nvp + chunk - 1) / chunk);
+  hipLaunchKernelGGL(k_hist_accw, dim3(grid), dim3(ATP), lds, s, p, vpos, nvp, chunk, lkey, lidx, WS);
   return hipGetLastError();
 }
 hipError_t hist_flags(const HistQueryParams& p, uint32_t* flag, hipStream_t s) {

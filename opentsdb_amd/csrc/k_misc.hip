@@ -353,7 +353,8 @@ __global__ __launch_bounds__(256) void k_rollup_combine(double* __restrict__ den
     const int64_t cs = cmap[s];
     if (cs < 0 || !pres[i]) continue;
     const double sum = dense[i];
-    const double count = dense[cs * K + (i - s * K)];
+    const int64_t ci = cs * K + (i - s * K);
+    const double count = pres[ci] ? dense[ci] : 0.0;   // a bucket the count series left empty holds no count
     dense[i] = avg ? (count == 0.0 ? 0.0 : sum / count) : count;
   }
 }

@@ -32,11 +32,41 @@ EXPORTS = [
     "tsdbhip_load_rollup", "tsdbhip_load_cells", "tsdbhip_load_histograms", "tsdbhip_hist_run",
     "tsdbhip_hist_run_range", "tsdbhip_hist_result_free", "tsdbhip_expr_map", "tsdbhip_expr_zip", "tsdbhip_expr_topn",
     "tsdbhip_batch_range_sizes", "tsdbhip_batch_download_range", "tsdbhip_expr_sync", "tsdbhip_init_devices",
-    "tsdbhip_md_shard_mode", "tsdbhip_md_info",
+    "tsdbhip_md_shard_mode", "tsdbhip_md_info", "tsdbhip_host_alloc", "tsdbhip_host_free",
 ]
 
 SHARD_AUTO, SHARD_SERIES, SHARD_GROUPS, SHARD_SPANS = -1, 0, 1, 2   # tsdbhip.h TSDB_SHARD_*
 MD_AUTO, MD_COPY, MD_RCCL = -1, 0, 1                               # tsdbhip.h TSDB_MD_*
+
+
+class PinnedArray(np.ndarray):
+    """A numpy array over page-locked host memory (tsdbhip_host_alloc), freed with the array."""
+
+    _owner = None
+
+
+class _PinnedBlock:
+    def __init__(self, nbytes: int):
+        p = C.c_void_p()
+        _check(lib().tsdbhip_host_alloc(max(1, int(nbytes)), C.byref(p)))
+        self.ptr = p.value
+        self.nbytes = int(nbytes)
+
+    def __del__(self):
+        if getattr(self, "ptr", None) and _lib is not None:
+            _lib.tsdbhip_host_free(self.ptr)
+            self.ptr = None
+
+
+def pinned_copy(a: np.ndarray) -> np.ndarray:
+    """`a` copied into page-locked host memory (uploads from it are DMA transfers)."""
+    a = np.ascontiguousarray(a)
+    blk = _PinnedBlock(a.nbytes)
+    buf = (C.c_uint8 * max(1, a.nbytes)).from_address(blk.ptr)
+    out = np.frombuffer(buf, dtype=a.dtype, count=a.size).reshape(a.shape).view(PinnedArray)
+    out._owner = blk
+    out[...] = a
+    return out
 
 
 class EngineError(Exception):
@@ -73,6 +103,9 @@ def lib():
         L.tsdbhip_md_shard_mode.argtypes = [vp, C.c_int]
         L.tsdbhip_md_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_void_p]
         L.tsdbhip_destroy.argtypes = [vp]
+        L.tsdbhip_host_alloc.argtypes = [C.c_uint64, C.POINTER(vp)]
+        L.tsdbhip_host_free.argtypes = [vp]
+        L.tsdbhip_host_free.restype = None
         L.tsdbhip_load.argtypes = [vp, C.POINTER(abi.Batch)]
         L.tsdbhip_synth.argtypes = [vp, C.POINTER(abi.SynthSpec)]
         L.tsdbhip_batch_sizes.argtypes = [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_uint64),

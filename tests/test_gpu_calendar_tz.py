@@ -184,3 +184,21 @@ def test_anchors_agree_across_spans(eng):
     for tz in [None, "Pacific/Fiji"]:
         q = q_of("5nc-sum", T0, T0 + 200 * 86400, "sum", tz)
         check(eng, b, q, "sum", f"5nc {tz}")
+
+
+@pytest.mark.parametrize("agg", ["sum", "avg", "max", "dev", "p90", "none"])
+def test_anchors_disagree_with_fill(eng, staggered, agg):
+    """A fill policy over per-span grids that disagree: each span's FillingDownsampler emits on its
+    own calendar sequence (previousInterval(start) .. previousInterval(end)) -- its bucket where one
+    has that timestamp, else the fill -- and the union evaluator aggregates those points."""
+    T0 = 1356998400
+    for spec in ["7sc-sum-nan", "11sc-avg-zero", "7sc-max-null"]:
+        q = q_of(spec, T0 + 5, T0 + 3 * 3600 - 7, agg, None)
+        check(eng, staggered, q, agg, f"anchored fill {spec} {agg}")
+
+
+@pytest.mark.parametrize("tz", ["America/Denver", "Asia/Kabul"])
+@pytest.mark.parametrize("spec", ["2dc-sum-zero", "5nc-sum-nan", "3wc-avg-nan", "7hc-max-null"])
+def test_fill_grid_against_span_anchors(eng, dst_batch, tz, spec):
+    q = q_of(spec, TA + 2 * 86400 + 1234, TA + 66 * 86400, "sum", tz)
+    check(eng, dst_batch, q, "sum", f"{tz} {spec}")

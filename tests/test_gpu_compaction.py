@@ -272,3 +272,77 @@ def test_salt_bucket_rows_merge(eng, seed):
             d = O.parse_downsample(ds)
             q.ds_function, q.ds_interval_ms = d.ds_function, d.ds_interval_ms
         assert_groups_match(eng.run(q), O.run_query(ref, q), agg, ctx=f"salt {agg} {ds}")
+
+
+def _random_scan(seed, n_series=40, salt=False):
+    rng = np.random.default_rng(seed)
+    series, groups = [], []
+    for s in range(n_series):
+        rows = []
+        for h in range(int(rng.integers(1, 4))):
+            for _ in range(int(rng.integers(1, 3)) if salt else 1):
+                rows.append((B + 3600 * (h * 2 + int(rng.integers(0, 2))),
+                             random_row(rng, int(rng.integers(1, 60)), dup_p=0.0 if salt else 0.05)))
+        series.append(rows)
+        groups.append(int(rng.integers(-1, 4)))
+    order = np.argsort(groups, kind="stable")
+    return [series[i] for i in order], [groups[i] for i in order]
+
+
+@pytest.mark.parametrize("seed,salt", [(21, False), (22, True), (23, False)])
+@pytest.mark.parametrize("chunk", [1, 97, 2000])
+def test_chunked_compaction_equals_one_pass(eng, seed, salt, chunk):
+    """A scan over the 2^31-datapoint chunk limit is compacted in chunks of whole rows (two passes:
+    sizes, then entries + writes at the host's layout).  TSDBHIP_CMP_CHUNK lowers the limit so
+    small scans take that path: the resident batch, the lazily raised errors and the query results
+    equal the one-pass compaction's."""
+    series, groups = _random_scan(seed, salt=salt)
+    cb = abi.HostCellBatch.from_rows(series, groups, True)
+    eng.load_cells(cb)
+    want = eng.download()
+    qs = []
+    for agg, ds in (("sum", "1m-avg"), ("max", "10m-max"), ("none", None)):
+        q = abi.new_query(B, B + 6 * 3600, agg)
+        if ds:
+            d = O.parse_downsample(ds)
+            q.ds_function, q.ds_interval_ms = d.ds_function, d.ds_interval_ms
+        try:
+            qs.append((q, agg, eng.run(q)))
+        except EngineError as e:
+            qs.append((q, agg, e.code))
+    os.environ["TSDBHIP_CMP_CHUNK"] = str(chunk)
+    try:
+        eng.load_cells(cb)
+    finally:
+        del os.environ["TSDBHIP_CMP_CHUNK"]
+    got = eng.download()
+    assert rows_of(got) == rows_of(want)
+    assert np.array_equal(got.group_id, want.group_id)
+    for q, agg, w in qs:
+        if isinstance(w, int):
+            with pytest.raises(EngineError) as ei:
+                eng.run(q)
+            assert ei.value.code == w
+        else:
+            assert_groups_match(eng.run(q), w, agg, tol=0.0, ctx=f"chunk {chunk} {agg}")
+
+
+@pytest.mark.parametrize("chunk", [None, 5])
+def test_decreasing_column_offsets_rejected(eng, chunk):
+    """Column offsets are checked on the device chunk by chunk: a decreasing offset inside a row
+    is an IllegalArgumentException before any compaction kernel reads the bytes."""
+    series, groups = _random_scan(31, n_series=6)
+    cb = abi.HostCellBatch.from_rows(series, groups, True)
+    qo = cb.col_qual_off.copy()
+    k = len(qo) // 2
+    qo[k] = qo[k + 1] + 2   # column k ends before it starts
+    bad = abi.HostCellBatch(cb.series_row_ptr, cb.row_base_time, cb.row_col_ptr, qo, cb.col_val_off, cb.qual,
+                            cb.val, cb.group_id, cb.col_timestamp, True)
+    if chunk:
+        os.environ["TSDBHIP_CMP_CHUNK"] = str(chunk)
+    try:
+        with pytest.raises(EngineError) as ei:
+            eng.load_cells(bad)
+        assert ei.value.code == abi.TSDB_E_ILLEGAL_ARGUMENT
+    finally:
+        os.environ.pop("TSDBHIP_CMP_CHUNK", None)

@@ -224,3 +224,52 @@ def test_gpu_repeated_bucket_keys_last_count_wins(eng):
     hb = H.HostHistBatch.from_rows(series, [0, 0], {0: H.HCODEC_SIMPLE})
     for ds in (None, "1m-sum", "1h-sum"):
         run_both(eng, hb, U.query(T0, T0 + 2 * 3600, "sum", ds), [50.0, 90.0, 10.0], True)
+
+
+@pytest.mark.parametrize("env", [{"TSDBHIP_HIST_WINDOW": "0"}, {"TSDBHIP_HIST_WS": "1"}, {"TSDBHIP_HIST_WS": "5"},
+                                 {"TSDBHIP_HIST_WS": "64"}], ids=["atomic-kernel", "ws1", "ws5", "ws64"])
+def test_gpu_accum_window_sizes(eng, env):
+    """k_hist_accw keeps a window of consecutive points' counters in LDS; tiles whose points leave
+    it flush it, points past its end add to the global counters directly.  Windows of 1, 5 and 64
+    points (and the per-column atomic kernel) give the oracle's answers, raw unions included."""
+    import os
+    rng = np.random.default_rng(77)
+    hb = U.random_store(rng, n_series=40, n_rows=2, period_ms=5000, groups=5, layouts=4, nb=(10, 16),
+                        sparse=0.1, ms_frac=0.2)
+    os.environ.update(env)
+    try:
+        for agg, ds, b in (("sum", "1m-sum", True), ("sum", None, True), ("none", "2m-sum", False),
+                           ("p99", "30s-sum", False), ("sum", "0all-sum", True)):
+            run_both(eng, hb, U.query(T0 + 100, T0 + 2 * 3600 - 50, agg, ds), [50.0, 95.0, 99.9], b)
+    finally:
+        for k in env:
+            del os.environ[k]
+
+
+T_DST = 1457740800   # 2016-03-12 00:00 UTC: America/Denver enters daylight time on Mar 13
+
+
+@pytest.fixture(scope="module")
+def dst_store():
+    rng = np.random.default_rng(4242)
+    return U.random_store(rng, n_series=9, n_rows=80, period_ms=600000, t0=T_DST, groups=3, layouts=3, nb=(4, 9),
+                          sparse=0.15, ms_frac=0.0)
+
+
+@pytest.mark.parametrize("tz", [None, "America/Denver", "Asia/Kabul"])
+@pytest.mark.parametrize("spec", ["1dc-sum", "6hc-sum", "1wc-sum", "1nc-sum", "2dc-sum", "90mc-sum", "7sc-sum",
+                                  "1hc-avg"])
+def test_gpu_calendar_downsampling(eng, dst_store, tz, spec):
+    """HistogramDownsampler with calendar intervals (src/core/HistogramDownsampler.java:219-331):
+    intervals from DateTime.previousInterval of each span's first datapoint after the seek, in the
+    query's zone, stepped by the calendar unit; the spans' outputs merge over the union of their
+    timestamps.  7sc / 2dc / 90mc anchor per span; 1hc-avg over two datapoints raises as the
+    reference's null HistogramAggregation does."""
+    from opentsdb_amd import tz as T
+    zone = T.table(tz) if tz else None
+    for agg in ("sum", "none"):
+        q = abi.new_query(T_DST + 1800, T_DST + 3 * 86400 + 600, agg, tz=zone)
+        d = U.query(0, 1, agg, spec)
+        q.ds_function, q.ds_interval_ms, q.ds_all, q.ds_calendar, q.ds_fill = (d.ds_function, d.ds_interval_ms,
+                                                                               d.ds_all, d.ds_calendar, d.ds_fill)
+        run_both(eng, dst_store, q, [50.0, 99.0], agg == "sum")

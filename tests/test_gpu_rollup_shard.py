@@ -122,7 +122,8 @@ def run_rank_partials(engines, rb, q, world):
         buf = np.zeros(int(lay.bytes), np.uint8)
         eng.run_partials(q, G, buf.ctypes.data)
         bufs.append(buf)
-    return engines[0].finalize(q, G, np.concatenate(bufs).ctypes.data, world)
+    gathered = np.concatenate(bufs)   # (kept alive across the call: .ctypes.data is a bare address)
+    return engines[0].finalize(q, G, gathered.ctypes.data, world)
 
 
 @pytest.mark.parametrize("world", [1, 2, 4])

@@ -14,7 +14,10 @@ for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
             k = row["Kernel_Name"]
             if flt and flt not in k:
                 continue
-            acc[k.split("(")[0][:70]][row["Counter_Name"]].append(float(row["Counter_Value"]))
+            # "void tsdb::(anonymous namespace)::k_x<...>(args)" -> "tsdb::k_x<...>"
+            name = k.replace("(anonymous namespace)::", "").split("(")[0]
+            name = name[5:] if name.startswith("void ") else name
+            acc[name[:90]][row["Counter_Name"]].append(float(row["Counter_Value"]))
 for k, d in acc.items():
     print(k)
     for c, v in sorted(d.items()):
