@@ -177,7 +177,7 @@ extern "C" int tsdbhip_load_histograms(tsdbhip_ctx* c, const tsdbhip_hist_batch*
   if (NC >= ((int64_t)1 << 31)) return set_error(TSDB_E_NOT_IMPLEMENTED, "more than 2^31 histogram columns in one store");
   const uint64_t vbytes = NC ? hb->cell_val_off[NC] : 0;
   // 1. device: decode check of every column, bucket keys into the dictionary hash set
-  HOK(S->val.ensure(vbytes + 16));
+  HOK(S->val.ensure(vbytes + 64));   // (k_hist_accw stages whole 16-byte units past a column's end)
   HOK(S->voff.ensure((NC + 1) * 8));
   HOK(S->codec.ensure(256));
   HOK(S->status.ensure(NC + 1));
@@ -233,9 +233,7 @@ extern "C" int tsdbhip_load_histograms(tsdbhip_ctx* c, const tsdbhip_hist_batch*
     std::vector<int32_t> li(HIST_LDICT, -1);
     for (int32_t d = 0; d < S->D; d++) {
       const uint64_t key = ((uint64_t)S->h_dlo[d] << 32) | S->h_dup[d];
-      uint64_t h = key;
-      h ^= h >> 33; h *= 0xff51afd7ed558ccdULL; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ULL; h ^= h >> 33;
-      uint32_t slot = (uint32_t)(h & (HIST_LDICT - 1));
+      uint32_t slot = lds_dict_slot(key);
       while (lk[slot] != HK_EMPTY) slot = (slot + 1) & (HIST_LDICT - 1);
       lk[slot] = key;
       li[slot] = d;

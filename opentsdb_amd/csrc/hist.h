@@ -93,6 +93,12 @@ hipError_t hist_slots(const HistQueryParams& p, hipStream_t s);
 // lkey / lidx: the dictionary as an LDICT-slot table for LDS (k_hist.hip), or null
 hipError_t hist_accum(const HistQueryParams& p, int64_t n_pos, const uint64_t* lkey, const int32_t* lidx, hipStream_t s);
 static constexpr int HIST_LDICT = 1024;
+// slot of a bucket key in the LDS dictionary table (HIST_LDICT = 2^10 slots): two 32-bit
+// multiplies instead of the global table's 64-bit mixer (host and device must agree)
+__host__ __device__ inline uint32_t lds_dict_slot(uint64_t k) {
+  const uint32_t h = ((uint32_t)(k >> 32) * 0x9E3779B1u) ^ ((uint32_t)k * 0x85EBCA77u);
+  return (h ^ (h >> 16)) & (HIST_LDICT - 1);
+}
 static constexpr int64_t HIST_WLDS = 80 * 1024;   // LDS of a k_hist_accw block (two blocks per CU)
 // the present spans' in-range positions in span order: vpos[off[i] .. off[i + 1]) = span i's
 hipError_t hist_vpos(const int64_t* rlo, const int64_t* rhi, const int64_t* row_pos, int64_t n_spans, uint32_t* len,

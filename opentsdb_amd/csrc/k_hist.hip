@@ -311,7 +311,7 @@ struct DictLds {
   const uint64_t* key;
   const int32_t* idx;
   __device__ __forceinline__ int32_t find(uint64_t k) const {
-    uint32_t slot = (uint32_t)(hk_hash(k) & (LDICT - 1));
+    uint32_t slot = lds_dict_slot(k);
 #pragma unroll 1
     for (int probe = 0; probe < LDICT; probe++) {
       const uint64_t cur = key[slot];
@@ -639,7 +639,8 @@ __device__ void w_flush(const HistQueryParams& p, const Window& w, int64_t wb, i
 
 __global__ void __launch_bounds__(ATP) k_hist_accw(HistQueryParams p, const int32_t* __restrict__ vpos, int64_t nvp,
                                                    int64_t chunk, const uint64_t* lkey_g, const int32_t* lidx_g, int WS) {
-  extern __shared__ uint64_t smem64[];
+  extern __shared__ uint4 smem4[];   // (16-byte aligned: the stage takes 16-byte stores)
+  uint64_t* smem64 = reinterpret_cast<uint64_t*>(smem4);
   uint32_t* stage = reinterpret_cast<uint32_t*>(smem64);                         // STAGE_W + 8 dwords
   uint64_t* lkey = smem64 + (STAGE_W + 8) / 2;                                    // LDICT
   int32_t* lidx = reinterpret_cast<int32_t*>(lkey + LDICT);                       // LDICT
@@ -711,9 +712,11 @@ __global__ void __launch_bounds__(ATP) k_hist_accw(HistQueryParams p, const int3
     uint32_t my_base = 0;
     bool staged = fit;
     if (fit) {
+      // each run as whole 16-byte units (16-B aligned in HBM and in LDS): four loads in flight
+      // per thread before their stores
       uint32_t base = 0;
       for (int r = 0; r < nruns; r++) {
-        const uint64_t w0 = run_b0[r] >> 2, w1 = (run_b1[r] + 3) >> 2;
+        const uint64_t w0 = (run_b0[r] >> 2) & ~3ull, w1 = (((run_b1[r] + 3) >> 2) + 3) & ~3ull;
         if (r == rid) { my_b0 = w0; my_base = base; }
         base += (uint32_t)(w1 - w0);
       }
@@ -721,11 +724,20 @@ __global__ void __launch_bounds__(ATP) k_hist_accw(HistQueryParams p, const int3
       if (staged) {
         uint32_t b = 0;
         for (int r = 0; r < nruns; r++) {
-          const uint64_t w0 = run_b0[r] >> 2, w1 = (run_b1[r] + 3) >> 2;
-          const uint32_t* g = reinterpret_cast<const uint32_t*>(p.val) + w0;
-          const uint32_t n = (uint32_t)(w1 - w0);
-          for (uint32_t k = tid; k < n; k += ATP) stage[b + k] = g[k];
-          b += n;
+          const uint64_t w0 = (run_b0[r] >> 2) & ~3ull, w1 = (((run_b1[r] + 3) >> 2) + 3) & ~3ull;
+          const uint4* g = reinterpret_cast<const uint4*>(p.val) + (w0 >> 2);
+          uint4* st4 = reinterpret_cast<uint4*>(stage + b);
+          const uint32_t n4 = (uint32_t)((w1 - w0) >> 2);
+          uint32_t k = tid;
+          for (; k + 3 * ATP < n4; k += 4 * ATP) {
+            const uint4 a0 = g[k], a1 = g[k + ATP], a2 = g[k + 2 * ATP], a3 = g[k + 3 * ATP];
+            st4[k] = a0;
+            st4[k + ATP] = a1;
+            st4[k + 2 * ATP] = a2;
+            st4[k + 3 * ATP] = a3;
+          }
+          for (; k < n4; k += ATP) st4[k] = g[k];
+          b += (uint32_t)(w1 - w0);
         }
         __syncthreads();
       }

@@ -7,7 +7,7 @@ checked against the oracle on multi-series stores.  Intervals whose UTC grid is 
 sequence run on the fixed grid (ms / s / m / h dividing their unit, 1d, 1w) or a boundary
 table (n months with 12 % n == 0, 1 year); intervals anchored per span run on the union table
 of the spans' anchors when those agree (tests/test_gpu_calendar_tz.py covers time zones and
-disagreeing anchors); percentile downsampling over a boundary table returns NOT_IMPLEMENTED."""
+disagreeing anchors)."""
 from __future__ import annotations
 
 import pytest

@@ -149,14 +149,6 @@ def test_anchors_disagree_rate_percentile_zone(eng, staggered):
     check(eng, staggered, q, "sum", "anchored Kabul")
 
 
-def test_anchors_disagree_with_fill_not_implemented(eng, staggered):
-    T0 = 1356998400
-    q = q_of("7sc-sum-nan", T0, T0 + 3 * 3600, "sum", None)
-    with pytest.raises(Exception) as ei:
-        eng.run_batch(staggered, q)
-    assert "NotImplemented" in str(ei.value)
-
-
 @pytest.mark.parametrize("tz", [None, "America/Denver", "Pacific/Fiji"])
 @pytest.mark.parametrize("spec", ["1nc-p95", "1dc-p99", "1dc-median", "2dc-p50", "1wc-ep90r7", "1dc-p75-nan"])
 def test_percentile_downsampling_over_calendar_slots(eng, dst_batch, tz, spec):
