@@ -610,6 +610,68 @@ __device__ void accum_column_w(const HistQueryParams& p, const Window& w, int32_
   w_add(p, w, local, pt, p.D + 1, over);
 }
 
+// accum_column_w with the bucket loop software-pipelined: bucket j's dictionary probe is issued
+// together with bucket j + 1's key and count dwords, so each bucket waits for one LDS round trip
+// instead of two (the key / count reads of j + 1 do not depend on j's lookup)
+__device__ void accum_column_wp(const HistQueryParams& p, const Window& w, int32_t pt, int32_t local, const SrcW& src,
+                                uint64_t i0, uint8_t kind_st, const DictLds& dict) {
+  const uint8_t kind = kind_st & HC_KIND;
+  if ((kind_st & HC_UNSORTED) || kind != HC_SIMPLE) {
+    accum_column_w(p, w, pt, local, src, i0, kind_st, dict);
+    return;
+  }
+  if (local >= 0) atomicOr(&w.kind[local], 1u);
+  else atomicOr(&p.pkind[pt], 1u);
+  const int cnt = (int16_t)((src.at(i0 + 1) << 8) | src.at(i0 + 2));
+  uint64_t i = i0 + 3;
+  uint64_t key = 0, val = 0;
+  if (cnt > 0) {
+    key = wkey(src, i);
+    i += 8;
+    val = wvarlong(src, i);
+  }
+#pragma unroll 1
+  for (int j = 0; j < cnt; j++) {
+    const uint32_t slot = lds_dict_slot(key);
+    const uint64_t cur = dict.key[slot];
+    const int32_t cidx = dict.idx[slot];
+    uint32_t x0 = 0, x1 = 0, xv = 0;
+    const bool more = j + 1 < cnt;
+    if (more) {
+      x0 = src.dw(i);
+      x1 = src.dw(i + 4);
+      xv = src.dw(i + 8);
+    }
+    int32_t di = cur == key ? cidx : (cur == HK_EMPTY ? -1 : dict.find(key));
+    if (di < 0) set_err(p.err, -22, WHY_DICT);
+    else {
+      if (!(p.dbg & 1)) w_add(p, w, local, pt, di, val);
+      if (p.pres) {
+        if (local >= 0) atomicOr(&w.pres[(uint32_t)local * (uint32_t)p.W + (di >> 5)], 1u << (di & 31));
+        else atomicOr(&p.pres[(uint64_t)pt * p.W + (di >> 5)], 1u << (di & 31));
+      }
+    }
+    if (more) {
+      key = ((uint64_t)fcanon(bswap32(x0)) << 32) | fcanon(bswap32(x1));
+      i += 8;
+      const uint32_t m = ~xv & 0x80808080u;
+      if (m) {
+        const uint32_t L = (__builtin_ctz(m) >> 3) + 1;
+        uint32_t v = (xv & 0x7Fu) | ((xv >> 1) & 0x3F80u) | ((xv >> 2) & 0x1FC000u) | ((xv >> 3) & 0xFE00000u);
+        v &= (L == 4) ? 0x0FFFFFFFu : ((1u << (7 * L)) - 1);
+        val = v;
+        i += L;
+      } else {
+        val = svarlong(src, i);
+      }
+    }
+  }
+  const uint64_t under = wvarlong(src, i);   // underflow, overflow (:256-257)
+  const uint64_t over = wvarlong(src, i);
+  w_add(p, w, local, pt, p.D, under);
+  w_add(p, w, local, pt, p.D + 1, over);
+}
+
 // the window's counters to the global accumulator (points [wb, wb + WS)), zeroed for the next
 __device__ void w_flush(const HistQueryParams& p, const Window& w, int64_t wb, int WS) {
   __syncthreads();
@@ -637,6 +699,7 @@ __device__ void w_flush(const HistQueryParams& p, const Window& w, int64_t wb, i
   __syncthreads();
 }
 
+template <bool PIPE>
 __global__ void __launch_bounds__(ATP) k_hist_accw(HistQueryParams p, const int32_t* __restrict__ vpos, int64_t nvp,
                                                    int64_t chunk, const uint64_t* lkey_g, const int32_t* lidx_g, int WS) {
   extern __shared__ uint4 smem4[];   // (16-byte aligned: the stage takes 16-byte stores)
@@ -747,7 +810,8 @@ __global__ void __launch_bounds__(ATP) k_hist_accw(HistQueryParams p, const int3
     const uint8_t kind = p.pos_kind[q];
     if (staged) {
       const uint64_t i0 = (uint64_t)my_base * 4 + (p.voff[c] - my_b0 * 4);
-      accum_column_w(p, win, pt, local, SrcW{stage}, i0, kind, dict);
+      if (PIPE) accum_column_wp(p, win, pt, local, SrcW{stage}, i0, kind, dict);
+      else accum_column_w(p, win, pt, local, SrcW{stage}, i0, kind, dict);
     } else {
       accum_column_w(p, win, pt, local, SrcW{reinterpret_cast<const uint32_t*>(p.val)}, p.voff[c], kind, dict);
     }
@@ -855,8 +919,11 @@ hipError_t hist_accum_window(const HistQueryParams& p, const int32_t* vpos, int6
   if (WS <= 0 || !lkey) return hipErrorInvalidValue;
   const size_t lds = (size_t)(STAGE_W + 8) * 4 + (size_t)LDICT * 12 + (size_t)WS * p.C * 8 + (size_t)WS * 4 +
                      (p.pres ? (size_t)WS * p.W * 4 : 0);
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_hist_accw), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)lds);
+  const char* penv = getenv("TSDBHIP_HIST_PIPE");   // A/B: 0 = the unpipelined bucket loop
+  const bool pipe = !(penv && penv[0] == '0');
+  hipError_t e = hipFuncSetAttribute(pipe ? reinterpret_cast<const void*>(&k_hist_accw<true>)
+                                          : reinterpret_cast<const void*>(&k_hist_accw<false>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -864,7 +931,8 @@ hipError_t hist_accum_window(const HistQueryParams& p, const int32_t* vpos, int6
   const int64_t want = std::min<int64_t>(tiles, (int64_t)cus * 2);
   const int64_t chunk = ((tiles + want - 1) / want) * ATP;
   const unsigned grid = (unsigned)((nvp + chunk - 1) / chunk);
-  hipLaunchKernelGGL(k_hist_accw, dim3(grid), dim3(ATP), lds, s, p, vpos, nvp, chunk, lkey, lidx, WS);
+  if (pipe) hipLaunchKernelGGL(k_hist_accw<true>, dim3(grid), dim3(ATP), lds, s, p, vpos, nvp, chunk, lkey, lidx, WS);
+  else hipLaunchKernelGGL(k_hist_accw<false>, dim3(grid), dim3(ATP), lds, s, p, vpos, nvp, chunk, lkey, lidx, WS);
   return hipGetLastError();
 }
 hipError_t hist_flags(const HistQueryParams& p, uint32_t* flag, hipStream_t s) {
