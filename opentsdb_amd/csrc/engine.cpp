@@ -428,6 +428,9 @@ struct tsdbhip_ctx {
   int64_t fused_n = 0;                   // queries of the fused multi-aggregator pass being collected
   // account() cache (invalidated by every load)
   bool acct_valid = false;
+  bool seqd_valid = false;             // cached seq_dense_wanted answer for (seqd_ss, seqd_se)
+  bool seqd_ans = false;
+  int64_t seqd_ss = 0, seqd_se = 0;
   int64_t acct_ss = 0, acct_se = 0, acct_dps = 0, acct_bytes = 0;
   bool acct_none = false;
   // rollup generation: scratch and the per-function cells of the last tsdbhip_rollup_run
@@ -654,6 +657,7 @@ static void release_batch(tsdbhip_ctx* c) {
     b->release();
   c->none_tiles_ready = false;
   c->acct_valid = false;
+  c->seqd_valid = false;
   c->mdp_valid = false;
   c->ro_meta_valid = false;
   c->lc_valid = false;
@@ -1440,6 +1444,17 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     cuts.push_back(NR);
   }
   const int n_chunks = (int)cuts.size() - 1;
+  // TSDBHIP_TRACE=1: host wall time of the call's phases on stderr (diagnostics only)
+  const bool trace = std::getenv("TSDBHIP_TRACE") != nullptr;
+  auto t_last = std::chrono::steady_clock::now();
+  auto mark = [&](const char* what) {
+    if (!trace) return;
+    (void)hipStreamSynchronize(c->stream);
+    const auto t = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[trace load_cells] %-14s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+    t_last = t;
+  };
+  mark("validate+plan");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_OK(hipSetDevice(c->device));
   release_batch(c);
@@ -1598,6 +1613,7 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   };
   for (int k = 0; k < n_chunks; k++)
     if (int rc = prepare(k)) return rc;
+  mark("upload+entries");
   // resident layout: series stable-sorted by group, each series' kept rows by base time
   std::vector<int64_t> order(NS);
   int32_t maxg = -1;
@@ -1663,6 +1679,7 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   HIP_OK(c->val.ensure(vtot + BLOB_SLACK));
   HIP_OK(hipMemsetAsync(c->qual.p, 0, qtot + BLOB_SLACK, c->stream));
   HIP_OK(hipMemsetAsync(c->val.p, 0, vtot + BLOB_SLACK, c->stream));
+  mark("host layout");
   if (n_chunks == 1) {
     if (int rc = write(0)) return rc;
   } else {
@@ -1707,7 +1724,9 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   if (!rd.empty()) HIP_OK(hipMemcpy(c->rows.p, rd.data(), rd.size() * sizeof(RowDesc), hipMemcpyHostToDevice));
   HIP_OK(hipMemcpy(c->srp.p, srp.data(), (NS + 1) * 8, hipMemcpyHostToDevice));
   if (NS) HIP_OK(hipMemcpy(c->gid.p, hgroup.data(), NS * 4, hipMemcpyHostToDevice));
+  mark("write+merge");
   const int rc = finish_load(c, rd);
+  mark("finish_load");
   c->cmp_errs = std::move(errs);
   c->compact_ms = cmp_ms;
   return rc;
@@ -2069,6 +2088,7 @@ struct Plan {
   bool ordered = false;          // TSDB_QF_ORDERED float reduction: run_ordered
   bool values_only = false;      // percentile downsampling pass without the group-by step
   bool emit_only = false;        // group-by step over bucket values already in pre_dense / pre_pres
+  bool seq_dense = false;        // sum / avg buckets in Java's order first (k_seq_dense), then the group-by step
   bool multi = false;            // fused multi-aggregator pass (run_multi_fused): partials to c->mp*, no reduce
   bool multi_dev = false;        //   ... with the Welford state (a dev query among them)
   // calendar grids anchored per span that disagree (plan_calendar): each anchor's boundary
@@ -2536,11 +2556,17 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     gp.pres_out = c->pre_pres.as<uint8_t>();
   }
 
-  if (P.f == F_SEL || P.emit_only) {
+  if (P.f == F_SEL || P.emit_only || P.seq_dense) {
     // percentile / median: per-series bucket order statistics, then the group-by step
-    // (emit_only: the group-by step alone, over buckets a previous pass left in pre_dense)
+    // (emit_only: the group-by step alone, over buckets a previous pass left in pre_dense;
+    // seq_dense: k_seq_dense leaves them there first)
     HIP_OK(c->pre_dense.ensure(std::max<int64_t>(1, c->n_series * K) * 8));
     HIP_OK(c->pre_pres.ensure(std::max<int64_t>(1, c->n_series * K)));
+    if (P.seq_dense) {
+      HIP_OK(hipEventRecord(c->ev[0], c->stream));
+      HIP_OK(hipMemsetAsync(c->pre_pres.p, 0, std::max<int64_t>(1, c->n_series * K), c->stream));
+      HIP_OK(launch_seq_dense(gp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->n_series, c->stream));
+    }
     gp.sel_fn = q->ds_function;
     gp.n_series = c->n_series;
     gp.pre_dense = c->pre_dense.as<double>();
@@ -2558,8 +2584,8 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     }
     gp.waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / gp.wave_lds));
     c->fast_used = false;
-    HIP_OK(hipEventRecord(c->ev[0], c->stream));
-    if (!P.emit_only) {
+    if (!P.seq_dense) HIP_OK(hipEventRecord(c->ev[0], c->stream));
+    if (!P.emit_only && !P.seq_dense) {
     HIP_OK(c->redo.ensure(std::max<int64_t>(1, c->n_series) * 4));
     HIP_OK(c->redo_n.ensure(16));
     HIP_OK(hipMemsetAsync(c->redo_n.p, 0, 4, c->stream));
@@ -3806,6 +3832,8 @@ int ro_check(const tsdbhip_query* q) {
 // The scan (ro_scan) and, for avg / count downsampling over count cells, steps 1-2 above: the
 // query's group-by step then runs over pre_dense (P.emit_only).  q is the caller's query, qr
 // ro_query(q), P planned from qr.
+bool seq_dense_wanted(tsdbhip_ctx* c, const Plan& P);
+
 int ro_stage(tsdbhip_ctx* c, const tsdbhip_query* q, const tsdbhip_query& qr, Plan& P) {
   const bool combine = c->ro_counts && (q->ds_function == TSDB_AGG_AVG || q->ds_function == TSDB_AGG_COUNT);
   int rc = ro_scan(c, P, combine);
@@ -3826,7 +3854,12 @@ int ro_stage(tsdbhip_ctx* c, const tsdbhip_query* q, const tsdbhip_query& qr, Pl
   P1.gsel = 0;
   P1.ordered = false;
   P1.gslot = grid_wave_lds(P.K, false, false) > 40 * 1024;
-  P1.dense_out = true;
+  if (seq_dense_wanted(c, P1)) {   // sums that cannot add in any order: k_seq_dense, Java's order, one pass
+    P1.seq_dense = true;
+    P1.values_only = true;
+  } else {
+    P1.dense_out = true;
+  }
   rc = run_device(c, &q1, P1, c->n_series, false);
   if (rc) return rc;
   HIP_OK(launch_rollup_combine(c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->ro_cmap.as<int64_t>(),
@@ -3848,6 +3881,31 @@ void ro_activity(const tsdbhip_ctx* c, const Plan& P, int64_t G, std::vector<uin
   }
 }
 
+// Sum / avg downsampling over a scan holding rows whose values cannot add exactly in any order
+// (ROW_NOCERT): k_seq_dense computes every bucket in Java's order in one pass instead of the
+// streaming kernels handing those tiles to k_grid's sequential re-walk.  Needs rows in time
+// order throughout the scan (the cache is per scan range; the rows are resident).
+bool seq_dense_wanted(tsdbhip_ctx* c, const Plan& P) {
+  if (!(P.f == F_SUM || P.f == F_AVG) || P.raw || P.anchored || P.gsel || P.ordered || P.multi || P.emit_only ||
+      P.dense_out || P.values_only || P.sel_direct)
+    return false;
+  if (const char* e = std::getenv("TSDBHIP_SEQ")) if (e[0] == '0') return false;   // tests: the k_grid path
+  if (const char* e = std::getenv("TSDBHIP_FAST")) if (e[0] == '0') return false;  // (the general path only)
+  if (c->seqd_valid && c->seqd_ss == P.ss && c->seqd_se == P.se) return c->seqd_ans;
+  bool any = false, ok = true;
+  for (int64_t r = 0; r < c->n_rows && ok; r++) {
+    if ((int64_t)c->h_base[r] < P.ss || (int64_t)c->h_base[r] >= P.se) continue;
+    const uint32_t f = c->h_flags[r];
+    ok = !(f & ROW_UNSORTED);
+    any = any || (f & ROW_NOCERT);
+  }
+  c->seqd_valid = true;
+  c->seqd_ss = P.ss;
+  c->seqd_se = P.se;
+  c->seqd_ans = ok && any;
+  return c->seqd_ans;
+}
+
 int run_rollup(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
   int rc = ro_check(q);
   if (rc) return rc;
@@ -3858,6 +3916,7 @@ int run_rollup(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
   rc = ro_stage(c, q, qr, P);
   if (rc) return rc;
   const int64_t G = P.none ? c->n_series : c->n_groups;
+  P.seq_dense = seq_dense_wanted(c, P);
   if (P.gsel || P.ordered) {
     rc = P.gsel ? run_sel_group(c, &qr, P, G) : run_ordered(c, &qr, P, G);
     if (rc) return rc;
@@ -3980,6 +4039,7 @@ extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_resul
     if (rc) return rc;
     return collect(c, q, P, G, true, out);
   }
+  P.seq_dense = seq_dense_wanted(c, P);
   rc = run_device(c, q, P, G, true);
   if (rc) return rc;
   return collect(c, q, P, G, true, out);

@@ -38,7 +38,15 @@ enum : uint32_t {
   ROW_SFIRST = 0x200000,    // first row of its series (set by the host at load)
   ROW_ALLI = 0x400000,      // every value is an integer
   ROW_VLE2 = 0x800000,      // every value is 1 or 2 bytes long
+  ROW_NOCERT = 0x1000000,   // two of the row's values cannot add exactly (row_nocert): an order-free sum is ruled out
 };
+
+// The exactness certificate (n * absmax <= 2^(52 + lsb)) fails for any bucket of
+// two or more of this row's values: sums over them must keep Java's order (k_grid's sequential path).
+__host__ __device__ inline bool row_nocert(int lsb, double absmax) {
+  if (lsb == INT32_MAX || absmax == 0.0) return false;
+  return isinf(absmax) || 2.0 * absmax * (1.0 + 1e-12) > ldexp(1.0, 52 + lsb);
+}
 
 // Per-tile partial group state, structure of arrays, [tile][K].
 struct Partials {
@@ -437,6 +445,8 @@ hipError_t launch_pct(const GridParams& p, int pass, int64_t n, hipStream_t s);
 bool pct_rows_supported(int qw, int vl);
 hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s);
 hipError_t launch_emit(const GridParams& p, hipStream_t s);
+// sum / avg downsampling in Java's order, one series per thread, into [series][K] (k_misc.hip)
+hipError_t launch_seq_dense(const GridParams& p, int f, double* dense, uint8_t* pres, int64_t n_series, hipStream_t s);
 hipError_t launch_emit_vals(const GridParams& p, hipStream_t s);
 hipError_t launch_sel_seg(const SelParams& p, hipStream_t s, int64_t maxn);
 hipError_t launch_ordered(const OrdParams& p, hipStream_t s);

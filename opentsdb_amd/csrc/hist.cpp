@@ -64,6 +64,8 @@ struct HistStore {
   Buf val, voff, codec, status, hkey, hcount, hidx, dlo, dup, lkey, lidx;
   bool lds_dict = false;                        // the dictionary fits the LDS table of k_hist_accum
   Buf pos_cell, pos_ts, pos_kind, row_pos;
+  Buf col_lid, lay_col, lay_off, lay_di;        // bucket layouts: dictionary indices without the keys
+  int64_t n_layouts = 0;
   int32_t D = 0;
   int64_t max_ts = 0;                           // largest datapoint timestamp of the store (ms)
   std::vector<uint32_t> h_dlo, h_dup;           // dictionary bounds (float bits), TreeMap order
@@ -81,7 +83,7 @@ struct HistStore {
   size_t tmp_bytes = 0;
   void release() {
     for (Buf* b : {&val, &voff, &codec, &status, &hkey, &hcount, &hidx, &dlo, &dup, &lkey, &lidx, &pos_cell, &pos_ts, &pos_kind,
-                   &row_pos, &q_rlo, &q_rhi, &q_out, &q_slot, &q_key, &q_key2, &q_pos, &q_pos2, &q_head, &q_incl,
+                   &row_pos, &col_lid, &lay_col, &lay_off, &lay_di, &q_rlo, &q_rhi, &q_out, &q_slot, &q_key, &q_key2, &q_pos, &q_pos2, &q_head, &q_incl,
                    &q_point, &q_ptts, &q_ptgrp, &q_vlen, &q_voff, &q_vpos, &q_caltab, &q_spcal, &acc, &pres, &pkind, &flag, &ptout, &err, &pct, &o_ts, &o_grp,
                    &o_kind, &o_pct, &o_cnt, &o_pres})
       b->release();
@@ -244,6 +246,32 @@ extern "C" int tsdbhip_load_histograms(tsdbhip_ctx* c, const tsdbhip_hist_batch*
     HOK(hipMemcpyAsync(S->lidx.p, li.data(), HIST_LDICT * 4, hipMemcpyHostToDevice, st));
     HOK(hipStreamSynchronize(st));
   }
+  // bucket layouts: runs of columns with the same key bytes share one row of dictionary indices
+  {
+    Buf head, excl;
+    struct Rel { Buf* a; Buf* b; ~Rel() { a->release(); b->release(); } } rel{&head, &excl};
+    HOK(head.ensure(NC * 4 + 4));
+    HOK(excl.ensure(NC * 8 + 16));
+    HOK(S->col_lid.ensure(NC * 4 + 4));
+    HOK(S->lay_col.ensure(NC * 4 + 4));
+    HOK(hist_layout_index(NC, S->voff.as<uint64_t>(), S->val.as<uint8_t>(), S->status.as<uint8_t>(), head.as<uint32_t>(),
+                          excl.as<int64_t>(), S->col_lid.as<int32_t>(), S->lay_col.as<int32_t>(), &S->n_layouts, &S->tmp,
+                          &S->tmp_bytes, st));
+    const int64_t NL = S->n_layouts;
+    std::vector<int32_t> lcol(std::max<int64_t>(1, NL)), loff(std::max<int64_t>(1, NL) + 1, 0);
+    if (NL) HOK(hipMemcpyAsync(lcol.data(), S->lay_col.p, NL * 4, hipMemcpyDeviceToHost, st));
+    HOK(hipStreamSynchronize(st));
+    for (int64_t l = 0; l < NL; l++) {
+      const uint8_t* v = hb->val + hb->cell_val_off[lcol[l]];
+      loff[l + 1] = loff[l] + (int16_t)(((uint32_t)v[1] << 8) | v[2]);
+    }
+    HOK(S->lay_off.ensure((NL + 1) * 4));
+    HOK(S->lay_di.ensure(std::max<int64_t>(1, loff[NL]) * 4));
+    HOK(hipMemcpyAsync(S->lay_off.p, loff.data(), (NL + 1) * 4, hipMemcpyHostToDevice, st));
+    HOK(hist_layout_di(NL, S->lay_col.as<int32_t>(), S->lay_off.as<int32_t>(), S->voff.as<uint64_t>(), S->val.as<uint8_t>(),
+                       S->hkey.as<uint64_t>(), S->hidx.as<int32_t>(), S->lay_di.as<int32_t>(), st));
+    HOK(hipStreamSynchronize(st));
+  }
   // 3. host: spans (SaltScanner.processRow -> HistogramSpan.addRow, rows sorted by base time)
   std::vector<int64_t> pos_cell, pos_ts, row_pos{0};
   std::vector<uint8_t> pos_kind;
@@ -391,6 +419,11 @@ int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end,
   p.row_pos = S->row_pos.as<int64_t>();
   p.hkey = S->hkey.as<uint64_t>();
   p.hidx = S->hidx.as<int32_t>();
+  if (const char* le = getenv("TSDBHIP_HIST_LAYOUT"); !(le && le[0] == '0') && S->n_layouts > 0) {
+    p.col_lid = S->col_lid.as<int32_t>();   // (tests: 0 = every bucket through the keyed lookup)
+    p.lay_off = S->lay_off.as<int32_t>();
+    p.lay_di = S->lay_di.as<int32_t>();
+  }
   p.dict_lo = S->dlo.as<uint32_t>();
   p.dict_up = S->dup.as<uint32_t>();
   p.D = S->D;

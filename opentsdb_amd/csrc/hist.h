@@ -85,6 +85,9 @@ struct HistQueryParams {
   uint8_t* out_kind;
   int64_t* out_count;        // [n_out * (D + 2)] (show_buckets)
   uint8_t* out_present;      // [n_out * D]
+  const int32_t* col_lid;    // [n_cells] bucket layout of the column (-1: none), or null
+  const int32_t* lay_off;    // [layouts] first entry of the layout's dictionary indices in lay_di
+  const int32_t* lay_di;     // dictionary index of each bucket of each layout
   int32_t dbg;               // profiling switches (TSDBHIP_HIST_DBG; results invalid): 1 skip the bucket atomics
 };
 
@@ -108,6 +111,16 @@ int hist_window_points(const HistQueryParams& p);
 // windowed accumulation over vpos (spans sorted by output group); needs the LDS dictionary
 hipError_t hist_accum_window(const HistQueryParams& p, const int32_t* vpos, int64_t nvp, const uint64_t* lkey,
                              const int32_t* lidx, hipStream_t s);
+// Bucket layouts (load): a SimpleHistogram column with strictly increasing keys whose key bytes
+// equal the previous column's shares its layout; col_lid[c] = the layout, lay_col[l] = its first
+// column.  hist_layout_index writes col_lid / lay_col and returns the layout count;
+// hist_layout_di fills lay_di[lay_off[l] + j] = the dictionary index of layout l's bucket j.
+hipError_t hist_layout_index(int64_t n_cells, const uint64_t* voff, const uint8_t* val, const uint8_t* status,
+                             uint32_t* head, int64_t* excl, int32_t* col_lid, int32_t* lay_col, int64_t* n_layouts,
+                             void** tmp, size_t* tmp_bytes, hipStream_t s);
+hipError_t hist_layout_di(int64_t n_layouts, const int32_t* lay_col, const int32_t* lay_off, const uint64_t* voff,
+                          const uint8_t* val, const uint64_t* hkey, const int32_t* hidx, int32_t* lay_di, hipStream_t s);
+static constexpr int HIST_LAY_MAXB = 32;   // layouts of more buckets take the keyed path
 hipError_t hist_flags(const HistQueryParams& p, uint32_t* flag, hipStream_t s);   // [n_points] 1 = emitted
 hipError_t hist_final(const HistQueryParams& p, hipStream_t s);
 hipError_t hist_scan(const uint32_t* flag, int64_t* out, int64_t n, void** tmp, size_t* tmp_bytes, hipStream_t s);

@@ -509,6 +509,76 @@ __global__ void k_iota(uint32_t* v, int64_t n) {
   if (i < n) v[i] = (uint32_t)i;
 }
 
+// ---- bucket layouts (load) ------------------------------------------------------------------
+// column c shares column c - 1's layout when both are sorted SimpleHistograms of the same bucket
+// count whose key bytes are equal (the counts in between may differ in length)
+__device__ bool same_keys(const uint8_t* a, uint64_t na, const uint8_t* b, uint64_t nb) {
+  const int ca = (int16_t)(((uint32_t)a[1] << 8) | a[2]), cb = (int16_t)(((uint32_t)b[1] << 8) | b[2]);
+  if (ca != cb) return false;
+  uint64_t i = 3, k = 3, c;
+#pragma unroll 1
+  for (int j = 0; j < ca; j++) {
+    for (int t = 0; t < 8; t++)
+      if (a[i + t] != b[k + t]) return false;
+    i += 8;
+    k += 8;
+    varlong(a, na, i, c);
+    varlong(b, nb, k, c);
+  }
+  return true;
+}
+__global__ void k_hist_layhead(int64_t n, const uint64_t* voff, const uint8_t* val, const uint8_t* status, uint32_t* head) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  const bool el = status[c] == HC_SIMPLE;   // (unsorted columns carry HC_UNSORTED: not eligible)
+  bool h = false;
+  if (el) {
+    const uint64_t o = voff[c], l = voff[c + 1] - o;
+    const int cnt = (int16_t)(((uint32_t)val[o + 1] << 8) | val[o + 2]);
+    if (cnt < 0 || cnt > HIST_LAY_MAXB) h = false;
+    else h = c == 0 || status[c - 1] != HC_SIMPLE || !same_keys(val + o, l, val + voff[c - 1], voff[c] - voff[c - 1]);
+  }
+  head[c] = h ? 1u : 0u;
+}
+__global__ void k_hist_laylid(int64_t n, const uint64_t* voff, const uint8_t* val, const uint8_t* status,
+                              const uint32_t* head, const int64_t* excl, int32_t* col_lid, int32_t* lay_col) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  int32_t lid = -1;
+  if (status[c] == HC_SIMPLE) {
+    const uint64_t o = voff[c];
+    const int cnt = (int16_t)(((uint32_t)val[o + 1] << 8) | val[o + 2]);
+    // heads up to and including c, minus one: c's layout (a column past HIST_LAY_MAXB buckets has none)
+    if (cnt >= 0 && cnt <= HIST_LAY_MAXB) lid = (int32_t)(excl[c + 1] - 1);
+  }
+  col_lid[c] = lid;
+  if (head[c]) lay_col[lid] = (int32_t)c;
+}
+__global__ void k_hist_laydi(int64_t nl, const int32_t* lay_col, const int32_t* lay_off, const uint64_t* voff,
+                             const uint8_t* val, const uint64_t* hkey, const int32_t* hidx, int32_t* lay_di) {
+  const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= nl) return;
+  const int64_t c = lay_col[l];
+  const uint64_t o = voff[c], n = voff[c + 1] - o;
+  const uint8_t* v = val + o;
+  const int cnt = (int16_t)(((uint32_t)v[1] << 8) | v[2]);
+  uint64_t i = 3, cv;
+  for (int j = 0; j < cnt; j++) {
+    const uint64_t key = ((uint64_t)fcanon(be32(v + i)) << 32) | fcanon(be32(v + i + 4));
+    i += 8;
+    varlong(v, n, i, cv);
+    uint64_t slot = hk_hash(key) & (uint64_t)(HT_SIZE - 1);
+    int32_t di = -1;
+    for (int64_t probe = 0; probe < HT_SIZE; probe++) {
+      const uint64_t cur = hkey[slot];
+      if (cur == key) { di = hidx[slot]; break; }
+      if (cur == HK_EMPTY) break;
+      slot = (slot + 1) & (uint64_t)(HT_SIZE - 1);
+    }
+    lay_di[lay_off[l] + j] = di;
+  }
+}
+
 // ---- windowed accumulation ---------------------------------------------------------------
 // The datapoints in SpanGroup order (vpos: the present spans sorted by output group, each span's
 // in-range positions), each block a contiguous chunk of them.  A group's spans all land on the
@@ -614,7 +684,7 @@ __device__ void accum_column_w(const HistQueryParams& p, const Window& w, int32_
 // together with bucket j + 1's key and count dwords, so each bucket waits for one LDS round trip
 // instead of two (the key / count reads of j + 1 do not depend on j's lookup)
 __device__ void accum_column_wp(const HistQueryParams& p, const Window& w, int32_t pt, int32_t local, const SrcW& src,
-                                uint64_t i0, uint8_t kind_st, const DictLds& dict) {
+                                uint64_t i0, uint8_t kind_st, const DictLds& dict, int32_t lid) {
   const uint8_t kind = kind_st & HC_KIND;
   if ((kind_st & HC_UNSORTED) || kind != HC_SIMPLE) {
     accum_column_w(p, w, pt, local, src, i0, kind_st, dict);
@@ -624,6 +694,35 @@ __device__ void accum_column_wp(const HistQueryParams& p, const Window& w, int32
   else atomicOr(&p.pkind[pt], 1u);
   const int cnt = (int16_t)((src.at(i0 + 1) << 8) | src.at(i0 + 2));
   uint64_t i = i0 + 3;
+  if (lid >= 0) {
+    // a known layout: the dictionary indices come from the layout table, the keys are skipped
+    const int32_t* lt = p.lay_di + p.lay_off[lid];
+    int32_t dis[HIST_LAY_MAXB];
+#pragma unroll
+    for (int j = 0; j < HIST_LAY_MAXB; j++) dis[j] = j < cnt ? lt[j] : 0;
+#pragma unroll
+    for (int j = 0; j < HIST_LAY_MAXB; j++) {
+      if (j < cnt) {
+        i += 8;
+        const uint64_t val = wvarlong(src, i);
+        const int32_t di = dis[j];
+        if (di < 0) {
+          set_err(p.err, -22, WHY_DICT);
+          continue;
+        }
+        if (!(p.dbg & 1)) w_add(p, w, local, pt, di, val);
+        if (p.pres) {
+          if (local >= 0) atomicOr(&w.pres[(uint32_t)local * (uint32_t)p.W + (di >> 5)], 1u << (di & 31));
+          else atomicOr(&p.pres[(uint64_t)pt * p.W + (di >> 5)], 1u << (di & 31));
+        }
+      }
+    }
+    const uint64_t under = wvarlong(src, i);
+    const uint64_t over = wvarlong(src, i);
+    w_add(p, w, local, pt, p.D, under);
+    w_add(p, w, local, pt, p.D + 1, over);
+    return;
+  }
   uint64_t key = 0, val = 0;
   if (cnt > 0) {
     key = wkey(src, i);
@@ -810,7 +909,7 @@ __global__ void __launch_bounds__(ATP) k_hist_accw(HistQueryParams p, const int3
     const uint8_t kind = p.pos_kind[q];
     if (staged) {
       const uint64_t i0 = (uint64_t)my_base * 4 + (p.voff[c] - my_b0 * 4);
-      if (PIPE) accum_column_wp(p, win, pt, local, SrcW{stage}, i0, kind, dict);
+      if (PIPE) accum_column_wp(p, win, pt, local, SrcW{stage}, i0, kind, dict, p.col_lid ? p.col_lid[c] : -1);
       else accum_column_w(p, win, pt, local, SrcW{stage}, i0, kind, dict);
     } else {
       accum_column_w(p, win, pt, local, SrcW{reinterpret_cast<const uint32_t*>(p.val)}, p.voff[c], kind, dict);
@@ -933,6 +1032,27 @@ hipError_t hist_accum_window(const HistQueryParams& p, const int32_t* vpos, int6
   const unsigned grid = (unsigned)((nvp + chunk - 1) / chunk);
   if (pipe) hipLaunchKernelGGL(k_hist_accw<true>, dim3(grid), dim3(ATP), lds, s, p, vpos, nvp, chunk, lkey, lidx, WS);
   else hipLaunchKernelGGL(k_hist_accw<false>, dim3(grid), dim3(ATP), lds, s, p, vpos, nvp, chunk, lkey, lidx, WS);
+  return hipGetLastError();
+}
+hipError_t hist_layout_index(int64_t n_cells, const uint64_t* voff, const uint8_t* val, const uint8_t* status,
+                             uint32_t* head, int64_t* excl, int32_t* col_lid, int32_t* lay_col, int64_t* n_layouts,
+                             void** tmp, size_t* tmp_bytes, hipStream_t s) {
+  *n_layouts = 0;
+  if (n_cells <= 0) return hipSuccess;
+  const unsigned nb = (unsigned)((n_cells + 255) / 256);
+  hipLaunchKernelGGL(k_hist_layhead, dim3(nb), dim3(256), 0, s, n_cells, voff, val, status, head);
+  hipError_t e = hist_scan(head, excl, n_cells, tmp, tmp_bytes, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_hist_laylid, dim3(nb), dim3(256), 0, s, n_cells, voff, val, status, head, excl, col_lid, lay_col);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = hipMemcpyAsync(n_layouts, excl + n_cells, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+  return hipStreamSynchronize(s);
+}
+hipError_t hist_layout_di(int64_t n_layouts, const int32_t* lay_col, const int32_t* lay_off, const uint64_t* voff,
+                          const uint8_t* val, const uint64_t* hkey, const int32_t* hidx, int32_t* lay_di, hipStream_t s) {
+  if (n_layouts <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hist_laydi, dim3((unsigned)((n_layouts + 255) / 256)), dim3(256), 0, s, n_layouts, lay_col, lay_off,
+                     voff, val, hkey, hidx, lay_di);
   return hipGetLastError();
 }
 hipError_t hist_flags(const HistQueryParams& p, uint32_t* flag, hipStream_t s) {

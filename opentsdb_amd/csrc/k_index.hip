@@ -199,6 +199,7 @@ __device__ __noinline__ void index_row_generic(const uint8_t* __restrict__ qual,
       if (negz) flags |= ROW_NEGZ;
       if (unsorted) flags |= ROW_UNSORTED;
       flags |= d.flags & ROW_SFIRST;
+      if (row_nocert(lsbmin, amax)) flags |= ROW_NOCERT;
       d.ndp = ndp;
       d.flags = flags;
       d.lsb = lsbmin;
@@ -677,6 +678,7 @@ __global__ __launch_bounds__(256) void k_index_cls(const uint8_t* __restrict__ q
         if (negz) flags |= ROW_NEGZ;
         if (unsorted) flags |= ROW_UNSORTED;
         flags |= cur.flags_in & ROW_SFIRST;
+        if (row_nocert(lsbmin, amax)) flags |= ROW_NOCERT;
         RowDesc& o = rows[cur.r];
         o.ndp = cur.ndp;
         o.flags = flags;

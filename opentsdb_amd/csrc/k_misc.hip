@@ -5,6 +5,157 @@
 
 namespace tsdb {
 
+// ---- k_seq_dense: Java's bucket order, one series per thread -------------------------
+// Sum / avg downsampling of rows whose values cannot add exactly in any order (ROW_NOCERT):
+// each thread walks its series' uniform rows in stored order, adding every bucket's values one
+// after the other as Downsampler.ValuesInInterval hands them to runDouble, and writes the
+// bucket values to [series][K] (pre_dense / pre_pres) for the group-by step (k_emit).  Uniform
+// rows: 16-byte loads of qualifiers and values, eight datapoints decoded per step; other rows
+// datapoint by datapoint.
+template <int F>
+__global__ __launch_bounds__(256) void k_seq_dense(GridParams p, double* __restrict__ dense, uint8_t* __restrict__ pres,
+                                                   int64_t n_series) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_series) return;
+  const int64_t K = p.K;
+  BState st;
+  bs_init<F>(st);
+  int cur = -1;
+  auto flush = [&]() {
+    if (cur >= 0) {
+      dense[s * K + cur] = bs_final<F>(st);
+      pres[s * K + cur] = 1;
+    }
+  };
+  for (int64_t r = p.series_row_ptr[s]; r < p.series_row_ptr[s + 1]; r++) {
+    const RowDesc d = p.rows[r];
+    if ((int64_t)d.base < p.ss) continue;
+    if ((int64_t)d.base >= p.se) break;
+    if (d.flags & ROW_ERR) { set_err(p.err, TSDB_E_ILLEGAL_DATA); continue; }
+    const int qw = d.flags & ROW_QW_MASK;
+    const int vl = (d.flags & ROW_VL_MASK) >> ROW_VL_SHIFT;
+    const RowGeom g = row_geom(p, d.base);
+    const uint8_t* qb = p.qual + d.qoff;
+    const uint8_t* vb = p.val + d.voff;
+    if (!((qw == 2 || qw == 4) && (vl == 1 || vl == 2 || vl == 4 || vl == 8))) {
+      // mixed qualifier widths or variable value lengths: datapoint by datapoint
+      // (RowSeq.Iterator: the width from the qualifier's first byte, the length from its flags)
+      uint64_t qi = 0, vi = 0;
+      for (uint32_t j = 0; j < d.ndp; j++) {
+        uint32_t off, fl;
+        if ((qb[qi] & 0xF0) == 0xF0) {
+          const uint32_t qq = ((uint32_t)qb[qi] << 24) | ((uint32_t)qb[qi + 1] << 16) | ((uint32_t)qb[qi + 2] << 8) | qb[qi + 3];
+          off = (qq & 0x0FFFFFC0u) >> 6;
+          fl = qq & 0xF;
+          qi += 4;
+        } else {
+          const uint32_t qq = ((uint32_t)qb[qi] << 8) | qb[qi + 1];
+          off = (qq >> 4) * 1000u;
+          fl = qq & 0xF;
+          qi += 2;
+        }
+        const int len = (int)(fl & 7) + 1;
+        uint64_t be = 0;
+        for (int t = 0; t < len; t++) be = (be << 8) | vb[vi + t];
+        vi += len;
+        double x;
+        if (fl & 8) x = len == 4 ? (double)__uint_as_float((uint32_t)be) : __longlong_as_double((long long)be);
+        else x = (double)((long long)(be << (64 - 8 * len)) >> (64 - 8 * len));
+        const int k = slot_of(p, g, d.base, off);
+        if (k < 0) continue;
+        if (k != cur) {
+          flush();
+          bs_init<F>(st);
+          cur = k;
+        }
+        bs_add<F>(st, x);
+      }
+      continue;
+    }
+    for (int64_t i0 = 0; i0 < (int64_t)d.ndp; i0 += DPL) {
+      const int nv = (int)min((int64_t)DPL, (int64_t)d.ndp - i0);
+      uint32_t off[DPL], fl[DPL];
+      if (qw == 2) {
+        const uint4 q = *reinterpret_cast<const uint4*>(qb + i0 * 2);
+        const uint32_t ws[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int j = 0; j < DPL; j++) {
+          const uint32_t be = __builtin_bswap32(ws[j >> 1]);
+          const uint32_t qq = (j & 1) ? (be & 0xFFFF) : (be >> 16);
+          off[j] = (qq >> 4) * 1000u;
+          fl[j] = qq & 0xF;
+        }
+      } else {
+        const uint4 q0 = *reinterpret_cast<const uint4*>(qb + i0 * 4);
+        const uint4 q1 = *reinterpret_cast<const uint4*>(qb + i0 * 4 + 16);
+        const uint32_t ws[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+        for (int j = 0; j < DPL; j++) {
+          const uint32_t qq = __builtin_bswap32(ws[j]);
+          off[j] = (qq & 0x0FFFFFC0u) >> 6;
+          fl[j] = qq & 0xF;
+        }
+      }
+      double val[DPL];
+      if (vl == 8) {
+        const uint4* v = reinterpret_cast<const uint4*>(vb + i0 * 8);
+        const uint4 a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
+        const uint32_t ws[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                                 a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+#pragma unroll
+        for (int j = 0; j < DPL; j++) {
+          const uint64_t b = ((uint64_t)__builtin_bswap32(ws[2 * j]) << 32) | __builtin_bswap32(ws[2 * j + 1]);
+          val[j] = (fl[j] & 8) ? __longlong_as_double((long long)b) : (double)(long long)b;
+        }
+      } else if (vl == 4) {
+        const uint4* v = reinterpret_cast<const uint4*>(vb + i0 * 4);
+        const uint4 a0 = v[0], a1 = v[1];
+        const uint32_t ws[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+        for (int j = 0; j < DPL; j++) {
+          const uint32_t be = __builtin_bswap32(ws[j]);
+          val[j] = (fl[j] & 8) ? (double)__uint_as_float(be) : (double)(int32_t)be;
+        }
+      } else if (vl == 2) {
+        const uint4 a0 = *reinterpret_cast<const uint4*>(vb + i0 * 2);
+        const uint32_t ws[4] = {a0.x, a0.y, a0.z, a0.w};
+#pragma unroll
+        for (int j = 0; j < DPL; j++) {
+          const uint32_t be = __builtin_bswap32(ws[j >> 1]);
+          val[j] = (double)(int16_t)(uint16_t)((j & 1) ? (be & 0xFFFF) : (be >> 16));
+        }
+      } else {
+        const uint2 a0 = *reinterpret_cast<const uint2*>(vb + i0);
+        const uint32_t ws[2] = {a0.x, a0.y};
+#pragma unroll
+        for (int j = 0; j < DPL; j++) val[j] = (double)(int8_t)((ws[j >> 2] >> ((j & 3) * 8)) & 0xFF);
+      }
+#pragma unroll
+      for (int j = 0; j < DPL; j++) {
+        if (j >= nv) break;
+        const int k = slot_of(p, g, d.base, off[j]);
+        if (k < 0) continue;
+        if (k != cur) {
+          flush();
+          bs_init<F>(st);
+          cur = k;
+        }
+        bs_add<F>(st, val[j]);
+      }
+    }
+  }
+  flush();
+}
+
+hipError_t launch_seq_dense(const GridParams& p, int f, double* dense, uint8_t* pres, int64_t n_series, hipStream_t s) {
+  if (n_series <= 0) return hipSuccess;
+  const unsigned nb = (unsigned)((n_series + 255) / 256);
+  if (f == F_SUM) hipLaunchKernelGGL(k_seq_dense<F_SUM>, dim3(nb), dim3(256), 0, s, p, dense, pres, n_series);
+  else if (f == F_AVG) hipLaunchKernelGGL(k_seq_dense<F_AVG>, dim3(nb), dim3(256), 0, s, p, dense, pres, n_series);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void k_reduce(ReduceParams p) {
   __shared__ PState sh[4][64];
   const int lane = lane_id();

@@ -1207,7 +1207,13 @@ __device__ __forceinline__ void series_slow(const GridParams& p, const WaveLds& 
     for (int64_t c0 = 0; c0 < (int64_t)d.ndp; c0 += CH) {
       int slot[DPL];
       double val[DPL];
-      decode_generic(p, d, g, c0, W, vcur, slot, val);
+      if (row_uniform(d)) {   // uniform rows: the register decode (no byte staging)
+        Raw rw = {};
+        load_raw(p, d, c0, rw);
+        decode_raw(p, d, g, c0, rw, slot, val);
+      } else {
+        decode_generic(p, d, g, c0, W, vcur, slot, val);
+      }
       slow_chunk<F>(W, st, slot, val);
     }
   }
@@ -1257,12 +1263,24 @@ __global__ __launch_bounds__(256) void k_grid(GridParams p) {
   Raw rc = {};
   if (cok && !force_slow && row_uniform(cd)) load_raw(p, cd, 0, rc);
   bool row_start = true;
+  // seq: this series' first row already rules the exactness certificate out (two values of its
+  // magnitude and resolution cannot add exactly), so its chunks go straight through the
+  // sequential in-bucket order (slow_chunk) -- one pass instead of the fast pass plus a re-walk
+  bool series_first = true, seq = false;
   while (cok) {
     if (row_start) {
       if (cd.flags & ROW_ERR) { if (lane == 0) set_err(p.err, TSDB_E_ILLEGAL_DATA); }
       lsb = min(lsb, cd.lsb);
       amax = fmax(amax, cd.absmax);
       row_start = false;
+      if (series_first) {
+        series_first = false;
+        if (needs_cert<F>() && !force_slow && cd.lsb != INT32_MAX && cd.absmax != 0.0) {
+          const int L = (F == F_SQUARESUM) ? 2 * cd.lsb : cd.lsb;
+          const double A = (F == F_SQUARESUM) ? cd.absmax * cd.absmax : cd.absmax;
+          seq = isinf(A) || 2.0 * A * (1.0 + 1e-12) > ldexp(1.0, 52 + L);   // (row_nocert for sums)
+        }
+      }
     }
     const bool more_in_row = c0 + CH < (int64_t)cd.ndp;
     // prefetch the next chunk (same row, or the first chunk of the next row)
@@ -1280,7 +1298,8 @@ __global__ __launch_bounds__(256) void k_grid(GridParams p) {
       double val[DPL];
       if (row_uniform(cd)) decode_raw(p, cd, g, c0, rc, slot, val);
       else decode_generic(p, cd, g, c0, W, vcur, slot, val);
-      fast_chunk<F>(W, st, slot, val);
+      if (seq) slow_chunk<F>(W, st, slot, val);
+      else fast_chunk<F>(W, st, slot, val);
     }
     if (more_in_row) {
       c0 += CH;
@@ -1291,7 +1310,10 @@ __global__ __launch_bounds__(256) void k_grid(GridParams p) {
     const bool series_end = !nok || ns != cs;
     if (series_end) {
       bool slow = force_slow;
-      if (!slow) {
+      if (seq) {
+        if (st.carry_slot >= 0 && lane == 0) emit_bucket<F>(W, st.carry_slot, bs_final<F>(st.scarry));
+        WAVE_SYNC();
+      } else if (!slow) {
         if (st.carry_slot >= 0 && lane == 0) emit_bucket<F>(W, st.carry_slot, fs_final<F>(st.fcarry));
         if (st.carry_slot >= 0) st.nmax = max(st.nmax, st.fcarry.n);
         if (needs_cert<F>()) {
@@ -1314,6 +1336,8 @@ __global__ __launch_bounds__(256) void k_grid(GridParams p) {
       st.nmax = 0;
       lsb = INT32_MAX;
       amax = 0.0;
+      series_first = true;
+      seq = false;
     }
     cs = ns;
     cr = nr;
@@ -1421,15 +1445,17 @@ __device__ __forceinline__ void fast_fold(const FastLds& L, int k, double v, uin
 }
 
 template <int QW, int VL>
-__device__ __forceinline__ bool fast_row_ok(uint32_t flags, bool minmax) {
+__device__ __forceinline__ bool fast_row_ok(uint32_t flags, bool minmax, bool cert = false) {
+  // cert: an order-free sum (F_SUM / F_AVG) -- a row whose values can never add exactly goes
+  // to k_grid's sequential path at once instead of after a full streaming pass
   if (VL == 0) {
     const uint32_t want = (uint32_t)QW | ROW_ALLI | ROW_VLE2;
-    const uint32_t mask = ROW_QW_MASK | ROW_ALLI | ROW_VLE2 | ROW_ERR | ROW_UNSORTED;
+    const uint32_t mask = ROW_QW_MASK | ROW_ALLI | ROW_VLE2 | ROW_ERR | ROW_UNSORTED | (cert ? ROW_NOCERT : 0u);
     return (flags & mask) == want;
   }
   const uint32_t want = (uint32_t)QW | ((uint32_t)VL << ROW_VL_SHIFT) | ROW_ALLF;
   const uint32_t mask = ROW_QW_MASK | ROW_VL_MASK | ROW_ALLF | ROW_ERR | ROW_NAN | ROW_UNSORTED |
-                        (minmax ? ROW_NEGZ : 0u);
+                        (minmax ? ROW_NEGZ : 0u) | (cert ? ROW_NOCERT : 0u);
   return (flags & mask) == want;
 }
 
@@ -1472,7 +1498,7 @@ __device__ __forceinline__ int fast_issue(const GridParams& p, const RowDesc* __
     if (w.c0 == 0) {
       w.sf |= (w.d.flags & ROW_SFIRST) != 0;
       if ((int64_t)w.d.base < p.ss || (int64_t)w.d.base >= p.se) { fwalk_next_row(rows, w); continue; }
-      if (!fast_row_ok<QW, VL>(w.d.flags, F == F_MIN || F == F_MAX)) return 2;
+      if (!fast_row_ok<QW, VL>(w.d.flags, F == F_MIN || F == F_MAX, F == F_SUM || F == F_AVG)) return 2;
       if (VL == 0 && w.d.ndp > CH) return 2;
     }
     if (w.c0 < (int64_t)w.d.ndp) break;
@@ -1995,7 +2021,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     damax = (uint64_t)__double_as_longlong(x.absmax);
     const uint32_t fl = x.flags;
     ok = (int64_t)x.base >= p.ss && (int64_t)x.base < p.se && dndp >= 1 && dndp <= CH &&
-         fast_row_ok<QW, VL>(fl, F == F_MIN || F == F_MAX);
+         fast_row_ok<QW, VL>(fl, F == F_MIN || F == F_MAX, F == F_SUM || F == F_AVG);
   }
   if (!__all(ok)) {
     if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;

@@ -39,18 +39,17 @@ SHARD_AUTO, SHARD_SERIES, SHARD_GROUPS, SHARD_SPANS = -1, 0, 1, 2   # tsdbhip.h 
 MD_AUTO, MD_COPY, MD_RCCL = -1, 0, 1                               # tsdbhip.h TSDB_MD_*
 
 
-class PinnedArray(np.ndarray):
-    """A numpy array over page-locked host memory (tsdbhip_host_alloc), freed with the array."""
-
-    _owner = None
-
-
 class _PinnedBlock:
-    def __init__(self, nbytes: int):
+    """Page-locked host memory (tsdbhip_host_alloc) exposed through __array_interface__: numpy
+    arrays over it keep this object as their base (views collapse to it), so the block is freed
+    only when the last array over it is gone."""
+
+    def __init__(self, nbytes: int, dtype, shape):
         p = C.c_void_p()
         _check(lib().tsdbhip_host_alloc(max(1, int(nbytes)), C.byref(p)))
         self.ptr = p.value
-        self.nbytes = int(nbytes)
+        self.__array_interface__ = {"data": (self.ptr, False), "shape": tuple(shape),
+                                    "typestr": np.dtype(dtype).str, "version": 3}
 
     def __del__(self):
         if getattr(self, "ptr", None) and _lib is not None:
@@ -61,10 +60,7 @@ class _PinnedBlock:
 def pinned_copy(a: np.ndarray) -> np.ndarray:
     """`a` copied into page-locked host memory (uploads from it are DMA transfers)."""
     a = np.ascontiguousarray(a)
-    blk = _PinnedBlock(a.nbytes)
-    buf = (C.c_uint8 * max(1, a.nbytes)).from_address(blk.ptr)
-    out = np.frombuffer(buf, dtype=a.dtype, count=a.size).reshape(a.shape).view(PinnedArray)
-    out._owner = blk
+    out = np.asarray(_PinnedBlock(a.nbytes, a.dtype, a.shape))
     out[...] = a
     return out
 

@@ -126,3 +126,34 @@ def test_calendar_spec_units_match_oracle():
         a, b = engine.parse_downsample(spec), O.parse_downsample(spec)
         assert (a.ds_calendar, a.ds_interval_ms, a.ds_fill, a.ds_all) == (b.ds_calendar, b.ds_interval_ms, b.ds_fill,
                                                                           b.ds_all), spec
+
+
+def test_pinned_copy_keeps_its_block_alive(monkeypatch):
+    """pinned_copy's arrays (and any view numpy collapses to their base) own the page-locked
+    block: it is freed only after the last array over it is gone (a use-after-free here crashed
+    an upload from pinned memory)."""
+    import ctypes as C
+    import gc
+    freed, keep = [], {}
+
+    class FakeLib:
+        def tsdbhip_host_alloc(self, n, pp):
+            buf = C.create_string_buffer(n)
+            keep[C.addressof(buf)] = buf
+            C.cast(pp, C.POINTER(C.c_void_p))[0] = C.addressof(buf)
+            return 0
+
+        def tsdbhip_host_free(self, p):
+            freed.append(p)
+
+    fake = FakeLib()
+    monkeypatch.setattr(engine, "_lib", fake)
+    monkeypatch.setattr(engine, "lib", lambda: fake)
+    y = engine.pinned_copy(np.arange(10, dtype=np.int64))
+    v = np.ascontiguousarray(y, dtype=np.int64)[2:]
+    del y
+    gc.collect()
+    assert freed == [] and int(v.sum()) == 44
+    del v
+    gc.collect()
+    assert len(freed) == 1

@@ -141,8 +141,10 @@ def test_fast_float64_certified(eng):
         check(eng, b, q, "sum", f"f64 {ds}", expect_redo=False)
 
 
-def test_fast_float64_certificate_fails(eng):
-    """Full-mantissa doubles: the certificate fails, every tile is redone sequentially."""
+def test_fast_float64_certificate_fails(eng, monkeypatch):
+    """Full-mantissa doubles: the certificate fails, every tile is redone sequentially (k_grid; the
+    one-pass k_seq_dense route is switched off here, see test_float64_sequential_sums)."""
+    monkeypatch.setenv("TSDBHIP_SEQ", "0")
     b = synth.generate(96, T0, 3600, 1000, value_kind=4, n_groups=4, seed=9)
     q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
     check(eng, b, q, "sum", "f64 uncertified", expect_redo=True)
@@ -281,3 +283,49 @@ def test_short_kernel_mixed_row_counts(eng):
     g, tg = run_path(eng, b, q, False)
     assert_bit_equal(s, g, "mixed row counts")
     assert_groups_match(s, O.run_query(b, q), "sum", ctx="mixed row counts vs oracle")
+
+
+@pytest.mark.parametrize("ds,iv,span", [("sum", 60000, 3 * 3600 - 1), ("avg", 420000, 3 * 3600 - 1),
+                                        ("squareSum", 60000, 3599), ("avg", 86400000, 3 * 3600 - 1),
+                                        ("sum", 1000, 1799), ("avg", 60000, 3 * 3600 - 1)])
+def test_float64_sequential_sums(eng, ds, iv, span):
+    """Full-mantissa doubles over three hour rows: the rows carry ROW_NOCERT (two of their values
+    cannot add exactly).  Sum / avg downsampling then runs k_seq_dense (each bucket in Java's
+    order, one pass, then the group-by step over the stored buckets); with it switched off the
+    streaming kernels hand the tiles to k_grid, which sums them in order in one pass (slow_chunk).
+    Both equal the general path bit for bit and the oracle -- buckets inside a row, across rows
+    (7m), one a day and one a datapoint; squareSum keeps the certificate check at series end."""
+    b = synth.generate(70, T0, 3 * 3600, 1000, value_kind=4, n_groups=3, seed=17)
+    for agg in ("sum", "max", "none"):
+        q = abi.new_query(T0, T0 + span, agg, ds_function=abi.AGG[ds], ds_interval_ms=iv)
+        seq, ts = run_path(eng, b, q, True)
+        gen, _ = run_path(eng, b, q, False)
+        os.environ["TSDBHIP_SEQ"] = "0"
+        try:
+            grid, _ = run_path(eng, b, q, True)
+        finally:
+            del os.environ["TSDBHIP_SEQ"]
+        if ds in ("sum", "avg"):
+            assert ts.fast_ms == 0, "k_seq_dense expected (no streaming pass)"
+        ctx = f"f64 seq {ds} {iv} {agg}"
+        assert_bit_equal(seq, gen, ctx)
+        assert_bit_equal(grid, gen, ctx + " (k_grid)")
+        assert_groups_match(seq, O.run_query(b, q), agg, ctx=ctx)
+
+
+def test_float64_sequential_sums_mixed_rows(eng):
+    """k_seq_dense over a scan mixing full-mantissa doubles (ROW_NOCERT), vle integers and
+    millisecond rows: the non-uniform rows are walked datapoint by datapoint (width from the
+    qualifier, length from its flags); bit-exact against the general path and the oracle."""
+    from tests.test_gpu_calendar_tz import merge
+    b = merge(synth.generate(20, T0, 7200, 1000, value_kind=4, n_groups=3, seed=5),
+              synth.generate(20, T0, 7200, 1000, value_kind=1, n_groups=3, int_mod=70000, seed=6),
+              synth.generate(10, T0, 3000, 2500, value_kind=4, n_groups=3, seed=7))
+    for ds, iv in (("sum", 60000), ("avg", 300000)):
+        for agg in ("sum", "avg"):
+            q = abi.new_query(T0, T0 + 7199, agg, ds_function=abi.AGG[ds], ds_interval_ms=iv)
+            seq, ts = run_path(eng, b, q, True)
+            gen, _ = run_path(eng, b, q, False)
+            assert ts.fast_ms == 0
+            assert_bit_equal(seq, gen, f"mixed {ds} {agg}")
+            assert_groups_match(seq, O.run_query(b, q), agg, ctx=f"mixed {ds} {agg}")

@@ -228,12 +228,13 @@ def test_gpu_repeated_bucket_keys_last_count_wins(eng):
 
 
 @pytest.mark.parametrize("env", [{"TSDBHIP_HIST_WINDOW": "0"}, {"TSDBHIP_HIST_WS": "1"}, {"TSDBHIP_HIST_WS": "5"},
-                                 {"TSDBHIP_HIST_WS": "64"}, {"TSDBHIP_HIST_PIPE": "0"}],
-                         ids=["atomic-kernel", "ws1", "ws5", "ws64", "unpipelined"])
+                                 {"TSDBHIP_HIST_WS": "64"}, {"TSDBHIP_HIST_PIPE": "0"}, {"TSDBHIP_HIST_LAYOUT": "0"}],
+                         ids=["atomic-kernel", "ws1", "ws5", "ws64", "unpipelined", "keyed"])
 def test_gpu_accum_window_sizes(eng, env):
     """k_hist_accw keeps a window of consecutive points' counters in LDS; tiles whose points leave
     it flush it, points past its end add to the global counters directly.  Windows of 1, 5 and 64
-    points (and the per-column atomic kernel) give the oracle's answers, raw unions included."""
+    points, the unpipelined loop, every bucket through the keyed lookup (no layout table) and the
+    per-column atomic kernel give the oracle's answers, raw unions included."""
     import os
     rng = np.random.default_rng(77)
     hb = U.random_store(rng, n_series=40, n_rows=2, period_ms=5000, groups=5, layouts=4, nb=(10, 16),
