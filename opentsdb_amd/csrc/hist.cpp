@@ -61,7 +61,8 @@ struct Buf {
 struct HistStore {
   bool loaded = false;
   int64_t n_series = 0, n_cells = 0, n_pos = 0;
-  Buf val, voff, codec, status, hkey, hcount, hidx, dlo, dup, lkey, lidx;
+  Buf val, voff, codec, status, hkey, hcount, hidx, dlo, dup, lkey, lidx, lkey2, lidx2;
+  int lslots = 64;                              // k_hist_accw's compact LDS dictionary table
   bool lds_dict = false;                        // the dictionary fits the LDS table of k_hist_accum
   Buf pos_cell, pos_ts, pos_kind, row_pos;
   Buf col_lid, lay_col, lay_off, lay_di;        // bucket layouts: dictionary indices without the keys
@@ -82,7 +83,7 @@ struct HistStore {
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   void release() {
-    for (Buf* b : {&val, &voff, &codec, &status, &hkey, &hcount, &hidx, &dlo, &dup, &lkey, &lidx, &pos_cell, &pos_ts, &pos_kind,
+    for (Buf* b : {&val, &voff, &codec, &status, &hkey, &hcount, &hidx, &dlo, &dup, &lkey, &lidx, &lkey2, &lidx2, &pos_cell, &pos_ts, &pos_kind,
                    &row_pos, &col_lid, &lay_col, &lay_off, &lay_di, &q_rlo, &q_rhi, &q_out, &q_slot, &q_key, &q_key2, &q_pos, &q_pos2, &q_head, &q_incl,
                    &q_point, &q_ptts, &q_ptgrp, &q_vlen, &q_voff, &q_vpos, &q_caltab, &q_spcal, &acc, &pres, &pkind, &flag, &ptout, &err, &pct, &o_ts, &o_grp,
                    &o_kind, &o_pct, &o_cnt, &o_pres})
@@ -244,6 +245,21 @@ extern "C" int tsdbhip_load_histograms(tsdbhip_ctx* c, const tsdbhip_hist_batch*
     HOK(S->lidx.ensure(HIST_LDICT * 4));
     HOK(hipMemcpyAsync(S->lkey.p, lk.data(), HIST_LDICT * 8, hipMemcpyHostToDevice, st));
     HOK(hipMemcpyAsync(S->lidx.p, li.data(), HIST_LDICT * 4, hipMemcpyHostToDevice, st));
+    // the compact table k_hist_accw keeps in LDS (its window takes the space the rest leaves)
+    S->lslots = hist_lds_slots(S->D);
+    std::vector<uint64_t> ck(S->lslots, HK_EMPTY);
+    std::vector<int32_t> ci(S->lslots, -1);
+    for (int32_t d = 0; d < S->D; d++) {
+      const uint64_t key = ((uint64_t)S->h_dlo[d] << 32) | S->h_dup[d];
+      uint32_t slot = lds_dict_slot(key, (uint32_t)S->lslots - 1);
+      while (ck[slot] != HK_EMPTY) slot = (slot + 1) & (uint32_t)(S->lslots - 1);
+      ck[slot] = key;
+      ci[slot] = d;
+    }
+    HOK(S->lkey2.ensure(S->lslots * 8));
+    HOK(S->lidx2.ensure(S->lslots * 4));
+    HOK(hipMemcpyAsync(S->lkey2.p, ck.data(), S->lslots * 8, hipMemcpyHostToDevice, st));
+    HOK(hipMemcpyAsync(S->lidx2.p, ci.data(), S->lslots * 4, hipMemcpyHostToDevice, st));
     HOK(hipStreamSynchronize(st));
   }
   // bucket layouts: runs of columns with the same key bytes share one row of dictionary indices
@@ -594,14 +610,14 @@ int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end,
   }
   if (const char* dbg = getenv("TSDBHIP_HIST_DBG")) p.dbg = atoi(dbg);
   const char* wenv = getenv("TSDBHIP_HIST_WINDOW");   // tests: 0 = the per-column atomic kernel
-  if (S->lds_dict && hist_window_points(p) > 0 && !(wenv && wenv[0] == '0')) {
+  if (S->lds_dict && hist_window_points(p, S->lslots) > 0 && !(wenv && wenv[0] == '0')) {
     HOK(S->q_vlen.ensure(nsp * 4 + 4));
     HOK(S->q_voff.ensure(nsp * 8 + 16));
     HOK(S->q_vpos.ensure(NP * 4 + 4));
     int64_t nvp = 0;
     HOK(hist_vpos(S->q_rlo.as<int64_t>(), S->q_rhi.as<int64_t>(), S->row_pos.as<int64_t>(), nsp, S->q_vlen.as<uint32_t>(),
                   S->q_voff.as<int64_t>(), S->q_vpos.as<int32_t>(), &nvp, &S->tmp, &S->tmp_bytes, st));
-    HOK(hist_accum_window(p, S->q_vpos.as<int32_t>(), nvp, S->lkey.as<uint64_t>(), S->lidx.as<int32_t>(), st));
+    HOK(hist_accum_window(p, S->q_vpos.as<int32_t>(), nvp, S->lkey2.as<uint64_t>(), S->lidx2.as<int32_t>(), S->lslots, st));
   } else {
     HOK(hist_accum(p, NP, S->lds_dict ? S->lkey.as<uint64_t>() : nullptr, S->lds_dict ? S->lidx.as<int32_t>() : nullptr, st));
   }

@@ -98,19 +98,25 @@ hipError_t hist_accum(const HistQueryParams& p, int64_t n_pos, const uint64_t* l
 static constexpr int HIST_LDICT = 1024;
 // slot of a bucket key in the LDS dictionary table (HIST_LDICT = 2^10 slots): two 32-bit
 // multiplies instead of the global table's 64-bit mixer (host and device must agree)
-__host__ __device__ inline uint32_t lds_dict_slot(uint64_t k) {
+__host__ __device__ inline uint32_t lds_dict_slot(uint64_t k, uint32_t mask = HIST_LDICT - 1) {
   const uint32_t h = ((uint32_t)(k >> 32) * 0x9E3779B1u) ^ ((uint32_t)k * 0x85EBCA77u);
-  return (h ^ (h >> 16)) & (HIST_LDICT - 1);
+  return (h ^ (h >> 16)) & mask;
 }
-static constexpr int64_t HIST_WLDS = 80 * 1024;   // LDS of a k_hist_accw block (two blocks per CU)
+// slots of k_hist_accw's compact LDS table for a D-bucket dictionary (load factor <= 1/2)
+inline int hist_lds_slots(int D) {
+  int n = 64;
+  while (n < 2 * D) n <<= 1;
+  return n;
+}
+static constexpr int64_t HIST_WLDS = 52 * 1024;   // LDS of a k_hist_accw block (three blocks per CU)
 // the present spans' in-range positions in span order: vpos[off[i] .. off[i + 1]) = span i's
 hipError_t hist_vpos(const int64_t* rlo, const int64_t* rhi, const int64_t* row_pos, int64_t n_spans, uint32_t* len,
                      int64_t* off, int32_t* vpos, int64_t* nvp, void** tmp, size_t* tmp_bytes, hipStream_t s);
 // points of the k_hist_accw LDS window for this query (0: the counters do not fit, use hist_accum)
-int hist_window_points(const HistQueryParams& p);
+int hist_window_points(const HistQueryParams& p, int lslots);
 // windowed accumulation over vpos (spans sorted by output group); needs the LDS dictionary
 hipError_t hist_accum_window(const HistQueryParams& p, const int32_t* vpos, int64_t nvp, const uint64_t* lkey,
-                             const int32_t* lidx, hipStream_t s);
+                             const int32_t* lidx, int lslots, hipStream_t s);
 // Bucket layouts (load): a SimpleHistogram column with strictly increasing keys whose key bytes
 // equal the previous column's shares its layout; col_lid[c] = the layout, lay_col[l] = its first
 // column.  hist_layout_index writes col_lid / lay_col and returns the layout count;

@@ -310,14 +310,15 @@ static constexpr int STAGE_W = 8192; // 32 KB of column bytes staged per tile
 struct DictLds {
   const uint64_t* key;
   const int32_t* idx;
+  uint32_t mask = LDICT - 1;   // slots - 1
   __device__ __forceinline__ int32_t find(uint64_t k) const {
-    uint32_t slot = lds_dict_slot(k);
+    uint32_t slot = lds_dict_slot(k, mask);
 #pragma unroll 1
-    for (int probe = 0; probe < LDICT; probe++) {
+    for (uint32_t probe = 0; probe <= mask; probe++) {
       const uint64_t cur = key[slot];
       if (cur == k) return idx[slot];
       if (cur == HK_EMPTY) return -1;
-      slot = (slot + 1) & (LDICT - 1);
+      slot = (slot + 1) & mask;
     }
     return -1;
   }
@@ -731,7 +732,7 @@ __device__ void accum_column_wp(const HistQueryParams& p, const Window& w, int32
   }
 #pragma unroll 1
   for (int j = 0; j < cnt; j++) {
-    const uint32_t slot = lds_dict_slot(key);
+    const uint32_t slot = lds_dict_slot(key, dict.mask);
     const uint64_t cur = dict.key[slot];
     const int32_t cidx = dict.idx[slot];
     uint32_t x0 = 0, x1 = 0, xv = 0;
@@ -798,28 +799,29 @@ __device__ void w_flush(const HistQueryParams& p, const Window& w, int64_t wb, i
   __syncthreads();
 }
 
-template <bool PIPE>
+template <bool PIPE, int SU>
 __global__ void __launch_bounds__(ATP) k_hist_accw(HistQueryParams p, const int32_t* __restrict__ vpos, int64_t nvp,
-                                                   int64_t chunk, const uint64_t* lkey_g, const int32_t* lidx_g, int WS) {
+                                                   int64_t chunk, const uint64_t* lkey_g, const int32_t* lidx_g, int WS,
+                                                   int LS) {
   extern __shared__ uint4 smem4[];   // (16-byte aligned: the stage takes 16-byte stores)
   uint64_t* smem64 = reinterpret_cast<uint64_t*>(smem4);
   uint32_t* stage = reinterpret_cast<uint32_t*>(smem64);                         // STAGE_W + 8 dwords
-  uint64_t* lkey = smem64 + (STAGE_W + 8) / 2;                                    // LDICT
-  int32_t* lidx = reinterpret_cast<int32_t*>(lkey + LDICT);                       // LDICT
-  uint64_t* wacc = reinterpret_cast<uint64_t*>(lidx + LDICT);                     // WS * C
+  uint64_t* lkey = smem64 + (STAGE_W + 8) / 2;                                    // LS (compact table)
+  int32_t* lidx = reinterpret_cast<int32_t*>(lkey + LS);                          // LS
+  uint64_t* wacc = reinterpret_cast<uint64_t*>(lidx + LS);                        // WS * C
   uint32_t* wkind = reinterpret_cast<uint32_t*>(wacc + (size_t)WS * p.C);        // WS
   uint32_t* wpres = wkind + WS;                                                   // WS * W
   __shared__ int32_t red[4];
   __shared__ int32_t wheads[2];
   __shared__ uint64_t run_b0[WRUNS], run_b1[WRUNS];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int k = tid; k < LDICT; k += ATP) { lkey[k] = lkey_g[k]; lidx[k] = lidx_g[k]; }
+  for (int k = tid; k < LS; k += ATP) { lkey[k] = lkey_g[k]; lidx[k] = lidx_g[k]; }
   const int nwin = WS * p.C;
   for (int e = tid; e < nwin; e += ATP) wacc[e] = 0;
   for (int e = tid; e < WS; e += ATP) wkind[e] = 0;
   if (p.pres) for (int e = tid; e < WS * p.W; e += ATP) wpres[e] = 0;
   const Window win{wacc, wkind, wpres};
-  const DictLds dict{lkey, lidx};
+  const DictLds dict{lkey, lidx, (uint32_t)(LS - 1)};
   const int64_t v0 = (int64_t)blockIdx.x * chunk, v1 = min(nvp, v0 + chunk);
   int64_t wb = -1;
   for (int64_t t0 = v0; t0 < v1; t0 += ATP) {
@@ -874,8 +876,7 @@ __global__ void __launch_bounds__(ATP) k_hist_accw(HistQueryParams p, const int3
     uint32_t my_base = 0;
     bool staged = fit;
     if (fit) {
-      // each run as whole 16-byte units (16-B aligned in HBM and in LDS): four loads in flight
-      // per thread before their stores
+      // each run as whole 16-byte units (16-B aligned in HBM and in LDS)
       uint32_t base = 0;
       for (int r = 0; r < nruns; r++) {
         const uint64_t w0 = (run_b0[r] >> 2) & ~3ull, w1 = (((run_b1[r] + 3) >> 2) + 3) & ~3ull;
@@ -890,15 +891,21 @@ __global__ void __launch_bounds__(ATP) k_hist_accw(HistQueryParams p, const int3
           const uint4* g = reinterpret_cast<const uint4*>(p.val) + (w0 >> 2);
           uint4* st4 = reinterpret_cast<uint4*>(stage + b);
           const uint32_t n4 = (uint32_t)((w1 - w0) >> 2);
-          uint32_t k = tid;
-          for (; k + 3 * ATP < n4; k += 4 * ATP) {
-            const uint4 a0 = g[k], a1 = g[k + ATP], a2 = g[k + 2 * ATP], a3 = g[k + 3 * ATP];
-            st4[k] = a0;
-            st4[k + ATP] = a1;
-            st4[k + 2 * ATP] = a2;
-            st4[k + 3 * ATP] = a3;
+          // up to SU loads in flight per thread (SU 16: a whole 32 KB tile in one round trip), then
+          // the stores
+          for (uint32_t k0 = 0; k0 < n4; k0 += SU * ATP) {
+            uint4 a[SU];
+#pragma unroll
+            for (int u = 0; u < SU; u++) {
+              const uint32_t k = k0 + u * ATP + tid;
+              if (k < n4) a[u] = g[k];
+            }
+#pragma unroll
+            for (int u = 0; u < SU; u++) {
+              const uint32_t k = k0 + u * ATP + tid;
+              if (k < n4) st4[k] = a[u];
+            }
           }
-          for (; k < n4; k += ATP) st4[k] = g[k];
           b += (uint32_t)(w1 - w0);
         }
         __syncthreads();
@@ -1002,36 +1009,47 @@ hipError_t hist_vpos(const int64_t* rlo, const int64_t* rhi, const int64_t* row_
   return hipStreamSynchronize(s);
 }
 
-int hist_window_points(const HistQueryParams& p) {
-  const int64_t fixed = (int64_t)(STAGE_W + 8) * 4 + (int64_t)LDICT * 12;
+int hist_window_points(const HistQueryParams& p, int lslots) {
+  const int64_t fixed = (int64_t)(STAGE_W + 8) * 4 + (int64_t)lslots * 12 + 256;
   const int64_t per = (int64_t)p.C * 8 + 4 + (p.pres ? (int64_t)p.W * 4 : 0);
-  int64_t ws = (HIST_WLDS - fixed) / per;
+  // three blocks a CU when a 64-point window fits in HIST_WLDS, else two with 80 KB
+  int64_t budget = HIST_WLDS;
+  if (const char* e = getenv("TSDBHIP_HIST_WLDS")) budget = std::max<int64_t>(40 * 1024, (int64_t)atoi(e) * 1024);   // A/B
+  int64_t ws = (budget - fixed) / per;
+  if (ws < 64) ws = (80 * 1024 - fixed) / per;
   if (ws < 32) return 0;
   if (const char* e = getenv("TSDBHIP_HIST_WS")) ws = std::min<int64_t>(ws, std::max(1, atoi(e)));   // tests: tiny windows
   return (int)std::min<int64_t>(ws, 4096);
 }
 
 hipError_t hist_accum_window(const HistQueryParams& p, const int32_t* vpos, int64_t nvp, const uint64_t* lkey,
-                             const int32_t* lidx, hipStream_t s) {
+                             const int32_t* lidx, int lslots, hipStream_t s) {
   if (nvp <= 0) return hipSuccess;
-  const int WS = hist_window_points(p);
+  const int WS = hist_window_points(p, lslots);
   if (WS <= 0 || !lkey) return hipErrorInvalidValue;
-  const size_t lds = (size_t)(STAGE_W + 8) * 4 + (size_t)LDICT * 12 + (size_t)WS * p.C * 8 + (size_t)WS * 4 +
+  const size_t lds = (size_t)(STAGE_W + 8) * 4 + (size_t)lslots * 12 + (size_t)WS * p.C * 8 + (size_t)WS * 4 +
                      (p.pres ? (size_t)WS * p.W * 4 : 0);
   const char* penv = getenv("TSDBHIP_HIST_PIPE");   // A/B: 0 = the unpipelined bucket loop
   const bool pipe = !(penv && penv[0] == '0');
-  hipError_t e = hipFuncSetAttribute(pipe ? reinterpret_cast<const void*>(&k_hist_accw<true>)
-                                          : reinterpret_cast<const void*>(&k_hist_accw<false>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const char* uenv = getenv("TSDBHIP_HIST_SU");     // A/B: 4 = four staging loads in flight a thread
+  const bool su4 = uenv && uenv[0] == '4';
+  const void* kf = pipe ? (su4 ? reinterpret_cast<const void*>(&k_hist_accw<true, 4>)
+                               : reinterpret_cast<const void*>(&k_hist_accw<true, 16>))
+                        : (su4 ? reinterpret_cast<const void*>(&k_hist_accw<false, 4>)
+                               : reinterpret_cast<const void*>(&k_hist_accw<false, 16>));
+  hipError_t e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t tiles = (nvp + ATP - 1) / ATP;
-  const int64_t want = std::min<int64_t>(tiles, (int64_t)cus * 2);
+  const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(4, (int64_t)(160 * 1024) / (int64_t)lds));
+  const int64_t want = std::min<int64_t>(tiles, (int64_t)cus * per_cu);
   const int64_t chunk = ((tiles + want - 1) / want) * ATP;
   const unsigned grid = (unsigned)((nvp + chunk - 1) / chunk);
-  if (pipe) hipLaunchKernelGGL(k_hist_accw<true>, dim3(grid), dim3(ATP), lds, s, p, vpos, nvp, chunk, lkey, lidx, WS);
-  else hipLaunchKernelGGL(k_hist_accw<false>, dim3(grid), dim3(ATP), lds, s, p, vpos, nvp, chunk, lkey, lidx, WS);
+  if (pipe && su4) hipLaunchKernelGGL((k_hist_accw<true, 4>), dim3(grid), dim3(ATP), lds, s, p, vpos, nvp, chunk, lkey, lidx, WS, lslots);
+  else if (pipe) hipLaunchKernelGGL((k_hist_accw<true, 16>), dim3(grid), dim3(ATP), lds, s, p, vpos, nvp, chunk, lkey, lidx, WS, lslots);
+  else if (su4) hipLaunchKernelGGL((k_hist_accw<false, 4>), dim3(grid), dim3(ATP), lds, s, p, vpos, nvp, chunk, lkey, lidx, WS, lslots);
+  else hipLaunchKernelGGL((k_hist_accw<false, 16>), dim3(grid), dim3(ATP), lds, s, p, vpos, nvp, chunk, lkey, lidx, WS, lslots);
   return hipGetLastError();
 }
 hipError_t hist_layout_index(int64_t n_cells, const uint64_t* voff, const uint8_t* val, const uint8_t* status,
