@@ -429,7 +429,7 @@ struct tsdbhip_ctx {
   // account() cache (invalidated by every load)
   bool acct_valid = false;
   bool seqd_valid = false;             // cached seq_dense_wanted answer for (seqd_ss, seqd_se)
-  bool seqd_ans = false;
+  bool seqd_ok = false, seqd_nocert = false, seqd_tiny = false;
   int64_t seqd_ss = 0, seqd_se = 0;
   int64_t acct_ss = 0, acct_se = 0, acct_dps = 0, acct_bytes = 0;
   bool acct_none = false;
@@ -2089,6 +2089,7 @@ struct Plan {
   bool values_only = false;      // percentile downsampling pass without the group-by step
   bool emit_only = false;        // group-by step over bucket values already in pre_dense / pre_pres
   bool seq_dense = false;        // sum / avg buckets in Java's order first (k_seq_dense), then the group-by step
+  bool sel_cols = false;         // sel_direct in the (group, slot) column layout
   bool multi = false;            // fused multi-aggregator pass (run_multi_fused): partials to c->mp*, no reduce
   bool multi_dev = false;        //   ... with the Welford state (a dev query among them)
   // calendar grids anchored per span that disagree (plan_calendar): each anchor's boundary
@@ -2544,6 +2545,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   if (const char* dbg = std::getenv("TSDBHIP_DBG")) gp.dbg = std::atoi(dbg);
   if (P.sel_direct) {   // buffers prepared by sel_values
     gp.sel_direct = 1;
+    gp.sel_cols = P.sel_cols ? 1 : 0;
     gp.sel_vals = c->sel_vals.as<double>();
     gp.sel_uni = c->sel_uni.as<uint8_t>();
     gp.sel_wr = c->sel_wr.as<uint8_t>();
@@ -2967,7 +2969,7 @@ const std::vector<int64_t>& local_counts(tsdbhip_ctx* c, int64_t G) {
 // When the query allows it (no rate, K <= 64, not a percentile downsampling) the downsampling
 // pass writes the contributions itself (GridParams.sel_direct): no bucket values round-trip
 // through pre_dense and no k_emit_vals pass.
-int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G) {
+int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bool* cols_out = nullptr) {
   const int64_t S = c->n_series, K = P.K;
   if (S * K > 0x7FFFFFFFLL) return fail(TSDB_E_NOT_IMPLEMENTED, "percentile group-by over more than 2^31 (series, slot) values");
   const char* fenv = std::getenv("TSDBHIP_SEL_FUSED");
@@ -2986,9 +2988,14 @@ int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G)
     int rc = plan_query(c, q, P2);
     if (rc) return rc;
     P2.sel_direct = true;
+    // the caller that selects right here takes contiguous (group, slot) columns
+    const char* cenv = std::getenv("TSDBHIP_SEL_COLS");
+    P2.sel_cols = cols_out != nullptr && !(cenv && cenv[0] == '0');
     rc = run_device(c, q, P2, G, false);   // sets c->gact like the group-by pass
     if (rc) return rc;
-    HIP_OK(launch_fill_rows(c->sel_vals.as<uint64_t>(), c->sel_wr.as<uint8_t>(), S, K, 0x7FF87FF87FF87FF8ULL, c->stream));
+    HIP_OK(launch_fill_rows(c->sel_vals.as<uint64_t>(), c->sel_wr.as<uint8_t>(), S, K, 0x7FF87FF87FF87FF8ULL, c->stream,
+                            P2.sel_cols ? c->sel_gsp.as<int64_t>() : nullptr, G));
+    if (cols_out) *cols_out = P2.sel_cols;
     HIP_OK(hipStreamSynchronize(c->stream));   // `gsp` leaves scope
     return 0;
   }
@@ -3103,9 +3110,10 @@ int sel_select(tsdbhip_ctx* c, const Plan& P, int64_t G, double* vals, const std
 //  2. k_emit_vals: the SpanGroup contributions (rate, fill, LERP) per (series, slot);
 //  3. k_sel_seg: runDouble's order statistic per (group, slot) by radix select.
 int run_sel_group(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G) {
-  int rc = sel_values(c, q, P, G);
+  bool cols = false;
+  int rc = sel_values(c, q, P, G, &cols);
   if (rc) return rc;
-  rc = sel_select(c, P, G, c->sel_vals.as<double>(), local_counts(c, G), c->sel_uni.as<uint8_t>());
+  rc = sel_select(c, P, G, c->sel_vals.as<double>(), local_counts(c, G), c->sel_uni.as<uint8_t>(), cols);
   if (rc) return rc;
   HIP_OK(hipEventRecord(c->ev[1], c->stream));
   HIP_OK(hipEventRecord(c->ev[2], c->stream));
@@ -3317,6 +3325,10 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
   if (!rp.do_long && !rp.do_double) rp.do_double = 1;
   rp.err = c->err.as<int32_t>();
   rp.uns = uns ? 1 : 0;
+  {
+    const char* e = std::getenv("TSDBHIP_RAW_LERPW");
+    rp.lerp_fast = !(e && e[0] == '0');
+  }
   if (uns) {
     HIP_OK(c->r_mts.ensure(std::max<int64_t>(1, np) * 8));
     HIP_OK(c->r_mpos.ensure(std::max<int64_t>(1, S) * 4));
@@ -3885,25 +3897,34 @@ void ro_activity(const tsdbhip_ctx* c, const Plan& P, int64_t G, std::vector<uin
 // (ROW_NOCERT): k_seq_dense computes every bucket in Java's order in one pass instead of the
 // streaming kernels handing those tiles to k_grid's sequential re-walk.  Needs rows in time
 // order throughout the scan (the cache is per scan range; the rows are resident).
+// Also every other downsampling function over scans of tiny rows at scale (rollup tables read
+// as hour rows of a few cells: the streaming kernels' per-row overhead dominates there).
 bool seq_dense_wanted(tsdbhip_ctx* c, const Plan& P) {
-  if (!(P.f == F_SUM || P.f == F_AVG) || P.raw || P.anchored || P.gsel || P.ordered || P.multi || P.emit_only ||
+  if (!(P.f >= F_SUM && P.f <= F_MULT) || P.raw || P.anchored || P.gsel || P.ordered || P.multi || P.emit_only ||
       P.dense_out || P.values_only || P.sel_direct)
     return false;
   if (const char* e = std::getenv("TSDBHIP_SEQ")) if (e[0] == '0') return false;   // tests: the k_grid path
   if (const char* e = std::getenv("TSDBHIP_FAST")) if (e[0] == '0') return false;  // (the general path only)
-  if (c->seqd_valid && c->seqd_ss == P.ss && c->seqd_se == P.se) return c->seqd_ans;
-  bool any = false, ok = true;
-  for (int64_t r = 0; r < c->n_rows && ok; r++) {
-    if ((int64_t)c->h_base[r] < P.ss || (int64_t)c->h_base[r] >= P.se) continue;
-    const uint32_t f = c->h_flags[r];
-    ok = !(f & ROW_UNSORTED);
-    any = any || (f & ROW_NOCERT);
+  if (!(c->seqd_valid && c->seqd_ss == P.ss && c->seqd_se == P.se)) {
+    bool any = false, ok = true;
+    int64_t rows = 0, dps = 0;
+    for (int64_t r = 0; r < c->n_rows && ok; r++) {
+      if ((int64_t)c->h_base[r] < P.ss || (int64_t)c->h_base[r] >= P.se) continue;
+      const uint32_t f = c->h_flags[r];
+      ok = !(f & ROW_UNSORTED);
+      any = any || (f & ROW_NOCERT);
+      rows++;
+      dps += c->h_ndp[r];
+    }
+    c->seqd_valid = true;
+    c->seqd_ss = P.ss;
+    c->seqd_se = P.se;
+    c->seqd_ok = ok;
+    c->seqd_nocert = any;
+    c->seqd_tiny = rows >= 100000 && dps <= 8 * rows;
   }
-  c->seqd_valid = true;
-  c->seqd_ss = P.ss;
-  c->seqd_se = P.se;
-  c->seqd_ans = ok && any;
-  return c->seqd_ans;
+  if (!c->seqd_ok) return false;
+  return (c->seqd_nocert && (P.f == F_SUM || P.f == F_AVG)) || c->seqd_tiny;
 }
 
 int run_rollup(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {

@@ -149,6 +149,7 @@ struct GridParams {
   // 1: the downsampling pass writes the contributions itself (kcommon.h sel_direct_out;
   // K <= 64, no rate)
   int32_t sel_direct;
+  int32_t sel_cols;              // sel_direct into [gsp[g] * K + k * n_g + i] (contiguous (group, slot) columns)
   // non-null: the grid kernels write every series' bucket values / presence here
   // ([series][K], before rate and fill) instead of its SpanGroup contributions
   double* dense_out;
@@ -279,6 +280,7 @@ struct RawParams {
   // AggregationIterator walk gives every point its step; the evaluation then also meets points
   // on either end of a span's window and windows with x1 <= x0
   int32_t uns;
+  int32_t lerp_fast;           // k_raw_eval: exact double LERP for strip-wide windows (lerpw_*)
   const int64_t* bnd_off;      // [g1 - g0] offset of each group's step timestamps in mts
   int64_t* mts;                // step timestamps, bnd_off layout (a group's points bound its steps)
   int32_t* m_pos;              // [n_series] next point of the span
@@ -399,7 +401,8 @@ hipError_t launch_first_ts(const RowDesc* rows, const int64_t* srp, const uint8_
 // n 8-byte words of `v` from p (16-byte aligned): 16-byte non-temporal stores
 hipError_t launch_fill64(uint64_t* p, uint64_t v, int64_t n, hipStream_t s);
 // the rows [series][K] of `p` whose wr flag is 0 filled with `v` (after a sel_direct pass)
-hipError_t launch_fill_rows(uint64_t* p, const uint8_t* wr, int64_t n_series, int64_t K, uint64_t v, hipStream_t s);
+hipError_t launch_fill_rows(uint64_t* p, const uint8_t* wr, int64_t n_series, int64_t K, uint64_t v, hipStream_t s,
+                            const int64_t* gsp = nullptr, int64_t G = 0);   // gsp: the column layout
 // streaming variant for one uniform row class (k_fast's premises + the sum certificate);
 // series that break a premise go to p.redo_list for launch_rollup_agg (tile_list mode)
 bool rollup_fast_supported(int qw, int vl);

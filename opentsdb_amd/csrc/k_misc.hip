@@ -150,9 +150,14 @@ __global__ __launch_bounds__(256) void k_seq_dense(GridParams p, double* __restr
 hipError_t launch_seq_dense(const GridParams& p, int f, double* dense, uint8_t* pres, int64_t n_series, hipStream_t s) {
   if (n_series <= 0) return hipSuccess;
   const unsigned nb = (unsigned)((n_series + 255) / 256);
-  if (f == F_SUM) hipLaunchKernelGGL(k_seq_dense<F_SUM>, dim3(nb), dim3(256), 0, s, p, dense, pres, n_series);
-  else if (f == F_AVG) hipLaunchKernelGGL(k_seq_dense<F_AVG>, dim3(nb), dim3(256), 0, s, p, dense, pres, n_series);
-  else return hipErrorInvalidValue;
+#define SEQ_CASE(FF) \
+  case FF: hipLaunchKernelGGL(k_seq_dense<FF>, dim3(nb), dim3(256), 0, s, p, dense, pres, n_series); break;
+  switch (f) {
+    SEQ_CASE(F_SUM) SEQ_CASE(F_AVG) SEQ_CASE(F_COUNT) SEQ_CASE(F_SQUARESUM) SEQ_CASE(F_MIN) SEQ_CASE(F_MAX)
+    SEQ_CASE(F_DEV) SEQ_CASE(F_FIRST) SEQ_CASE(F_LAST) SEQ_CASE(F_DIFF) SEQ_CASE(F_MULT)
+    default: return hipErrorInvalidValue;
+  }
+#undef SEQ_CASE
   return hipGetLastError();
 }
 
@@ -400,15 +405,28 @@ __global__ __launch_bounds__(256) void k_fill64(uint64_t* p, uint64_t v, int64_t
 // Rows the sel_direct pass did not write (series with no row in the scan range): the no-value
 // pattern, so the whole S x K buffer need not be filled beforehand.
 __global__ __launch_bounds__(256) void k_fill_rows(uint64_t* p, const uint8_t* wr, int64_t n_series, int64_t K,
-                                                   uint64_t v) {
+                                                   uint64_t v, const int64_t* gsp, int64_t G) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_series || wr[s]) return;
-  for (int64_t k = 0; k < K; k++) p[s * K + k] = v;
+  if (!gsp) {
+    for (int64_t k = 0; k < K; k++) p[s * K + k] = v;
+    return;
+  }
+  // column layout: the series' group by binary search over gsp (ungrouped series have no column)
+  if (s >= gsp[G]) return;
+  int64_t lo = 0, hi = G;
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (gsp[mid] <= s) lo = mid; else hi = mid;
+  }
+  const int64_t g0 = gsp[lo], ng = gsp[lo + 1] - g0;
+  for (int64_t k = 0; k < K; k++) p[g0 * K + k * ng + (s - g0)] = v;
 }
 
-hipError_t launch_fill_rows(uint64_t* p, const uint8_t* wr, int64_t n_series, int64_t K, uint64_t v, hipStream_t s) {
+hipError_t launch_fill_rows(uint64_t* p, const uint8_t* wr, int64_t n_series, int64_t K, uint64_t v, hipStream_t s,
+                            const int64_t* gsp, int64_t G) {
   if (n_series <= 0 || K <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_fill_rows, dim3((unsigned)((n_series + 255) / 256)), dim3(256), 0, s, p, wr, n_series, K, v);
+  hipLaunchKernelGGL(k_fill_rows, dim3((unsigned)((n_series + 255) / 256)), dim3(256), 0, s, p, wr, n_series, K, v, gsp, G);
   return hipGetLastError();
 }
 

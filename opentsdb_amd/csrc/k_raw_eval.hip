@@ -55,6 +55,43 @@ __device__ __forceinline__ int64_t jlerp(int interp, int64_t x, int64_t x0, int6
   }
 }
 
+// The long LERP of one span window shared by a whole strip (k_raw_eval's m == 0 case: x0, y0,
+// x1, y1 wave-uniform, x0 < x < x1 at every lane).  When x1 - x0 < 2^32 and |y1 - y0| (x1 - x0)
+// < 2^51 the wrapping product cannot wrap and every quantity is an exact double: the product is
+// one multiply, the quotient one multiply by the window's reciprocal (off by at most one), an
+// FMA gives its exact remainder and a compare corrects it -- ~15 instructions a point instead of
+// the general path's 64-bit multiplies, IEEE division and conversions.  Same result bit for bit.
+struct LerpW {
+  double dyd, dend, rd;
+  int64_t x0, y0;
+  bool pos, ok;
+};
+__device__ __forceinline__ LerpW lerpw_init(int interp, bool uns, int64_t x0, int64_t y0, int64_t x1, int64_t y1) {
+  LerpW L;
+  const int64_t den = x1 - x0;
+  const int64_t dy = (int64_t)((uint64_t)y1 - (uint64_t)y0);
+  const uint64_t ady = dy < 0 ? (uint64_t)0 - (uint64_t)dy : (uint64_t)dy;
+  L.ok = interp == TSDB_INTERP_LERP && !uns && den > 0 && den < (1LL << 32) && ady < (1ULL << 51) &&
+         (double)ady * (double)den < 1125899906842624.0;   // 2^50 on the rounded product: the exact one < 2^51
+  L.dyd = (double)dy;
+  L.dend = (double)den;
+  L.rd = 1.0 / L.dend;
+  L.x0 = x0;
+  L.y0 = y0;
+  L.pos = dy >= 0;
+  return L;
+}
+__device__ __forceinline__ int64_t lerpw_eval(const LerpW& L, int64_t x) {
+  const double nd = (double)(uint32_t)(x - L.x0) * L.dyd;   // exact: |nd| < 2^51
+  double q = trunc(nd * L.rd);
+  const double r = fma(-q, L.dend, nd);                      // exact remainder of q
+  if (L.pos) q += (r >= L.dend ? 1.0 : 0.0) - (r < 0.0 ? 1.0 : 0.0);
+  else q += (r > 0.0 ? 1.0 : 0.0) - (r <= -L.dend ? 1.0 : 0.0);
+  // |q| < 2^51: its integer from the mantissa of q + 1.5 * 2^52
+  const int64_t qi = (int64_t)__double_as_longlong(q + 6755399441055744.0) - 0x4338000000000000LL;
+  return (int64_t)((uint64_t)L.y0 + (uint64_t)qi);
+}
+
 // nextDoubleValue (:735-797), evaluated with exactly Java's association and no FMA
 __device__ __forceinline__ double dlerp(int interp, int64_t x, int64_t x0, double y0, int64_t x1, double y1) {
   switch (interp) {
@@ -273,6 +310,18 @@ __global__ __launch_bounds__(64) void k_raw_eval(RawParams p) {
         if (c == n) continue;    // ended
         const RawPt a = pts[c - 1], b = pts[c];
         if ((a.tsf | b.tsf) & RAW_FLOAT) flt = (1u << RAW_W) - 1;
+        if (DL && p.lerp_fast) {
+          const int64_t x0 = a.tsf & RAW_TIME_MASK, x1 = b.tsf & RAW_TIME_MASK;
+          const LerpW L = lerpw_init(interp, uns, x0, (int64_t)a.bits, x1, (int64_t)b.bits);
+          if (L.ok) {
+#pragma unroll
+            for (int w = 0; w < RAW_W; w++) {
+              racc_long<GA>(acc[w], lerpw_eval(L, x[w]));
+              if (DD) racc_double<GA>(acc[w], dlerp(interp, x[w], x0, pt_double(a.tsf, a.bits), x1, pt_double(b.tsf, b.bits)));
+            }
+            continue;
+          }
+        }
 #pragma unroll
         for (int w = 0; w < RAW_W; w++) {
           bool dz = false;

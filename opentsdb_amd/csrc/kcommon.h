@@ -1139,7 +1139,14 @@ __device__ __forceinline__ void sel_direct_out(const GridParams& p, int K, int32
   bool uni;
   const bool has = slot_contribution(p, K, pr_in, v, cv, uni);
   const int lane = lane_id();
-  if (lane < K) p.sel_vals[s * K + lane] = has ? canon_nan(cv) : __longlong_as_double(0x7FF87FF87FF87FF8LL);
+  if (lane < K) {
+    int64_t at = s * K + lane;
+    if (p.sel_cols) {   // the (group, slot) column layout: each column contiguous for the select
+      const int64_t g0 = p.group_series_ptr[g], ng = p.group_series_ptr[g + 1] - g0;
+      at = g0 * K + (int64_t)lane * ng + (s - g0);
+    }
+    p.sel_vals[at] = has ? canon_nan(cv) : __longlong_as_double(0x7FF87FF87FF87FF8LL);
+  }
   // every series of a group sets the same G x K flags: store only while unset (config 2: 1M
   // series' byte stores into 64 x 60 flags serialised on a few L2 lines, 6.5 vs 3.9 ms)
   if (uni && !p.sel_uni[(int64_t)g * K + lane]) p.sel_uni[(int64_t)g * K + lane] = 1;

@@ -329,3 +329,26 @@ def test_float64_sequential_sums_mixed_rows(eng):
             assert ts.fast_ms == 0
             assert_bit_equal(seq, gen, f"mixed {ds} {agg}")
             assert_groups_match(seq, O.run_query(b, q), agg, ctx=f"mixed {ds} {agg}")
+
+
+@pytest.fixture(scope="module")
+def tiny_rows():
+    return synth.generate(100_000, T0, 8, 450000, value_kind=2, n_groups=16, int_mod=900, seed=23)
+
+
+@pytest.mark.parametrize("ds", ["sum", "avg", "min", "max", "count", "dev", "first", "last", "diff", "squareSum"])
+def test_tiny_rows_at_scale_sequential(eng, tiny_rows, ds):
+    """100k series of one 8-point row (the shape of rollup tables read as hour rows): every
+    downsampling function runs k_seq_dense (one series a thread, Java's order), bit-exact against
+    the streaming / k_grid path and the oracle."""
+    b = tiny_rows
+    q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG[ds], ds_interval_ms=900000)
+    seq, ts = run_path(eng, b, q, True)
+    os.environ["TSDBHIP_SEQ"] = "0"
+    try:
+        other, _ = run_path(eng, b, q, True)
+    finally:
+        del os.environ["TSDBHIP_SEQ"]
+    assert ts.fast_ms == 0, "k_seq_dense expected"
+    assert_bit_equal(seq, other, f"tiny {ds}")
+    assert_groups_match(seq, O.run_query(b, q), "sum", ctx=f"tiny {ds}")

@@ -126,3 +126,17 @@ def test_pct_group_segment_beyond_lds(eng):
     for agg in ["p99", "median", "p50"]:
         q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["avg"], ds_interval_ms=300000)
         assert_groups_match(eng.run(q), O.run_query(b, q), agg, tol=0.0, ctx=agg)
+
+
+@pytest.mark.parametrize("cols", ["0", "1"])
+def test_pct_group_column_layout(eng, mixed_batch, monkeypatch, cols):
+    """The fused percentile pass writes each (group, slot) column contiguously (sel_cols) or one
+    row per series (TSDBHIP_SEL_COLS=0): both feed the same select and match the oracle, incl.
+    a single group wider than a wave and the LDS-staged select."""
+    monkeypatch.setenv("TSDBHIP_SEL_COLS", cols)
+    for agg in ["p99", "median", "ep99r7"]:
+        q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+        assert_groups_match(eng.run_batch(mixed_batch, q), O.run_query(mixed_batch, q), agg, tol=0.0, ctx=agg)
+    b = synth.generate(300, T0, 360, 10000, value_kind=1, n_groups=1, int_mod=50, seed=3)
+    q = abi.new_query(T0, T0 + 3599, "p50", ds_function=abi.AGG["max"], ds_interval_ms=60000)
+    assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "p50", tol=0.0, ctx="one group")

@@ -148,3 +148,29 @@ def test_raw_spans_outside_scan_range(eng):
         for rate in (False, True):
             q = abi.new_query(T0, T0 + 3599, agg, rate=rate)
             exact(eng.run_batch(b, q), O.run_query(b, q), agg, f"{agg} rate={rate}")
+
+
+@pytest.mark.parametrize("lerpw", ["0", "1"])
+def test_raw_strip_window_lerp(eng, monkeypatch, lerpw):
+    """k_raw_eval's strip-wide long LERP (lerpw_*: reciprocal quotient + exact remainder) and the
+    general 64-bit path (TSDBHIP_RAW_LERPW=0) give the oracle's answer: counters, large-slope
+    integers that leave the fast window (|dy| (x1 - x0) >= 2^51), negative slopes, mixed groups."""
+    monkeypatch.setenv("TSDBHIP_RAW_LERPW", lerpw)
+    b = synth.generate_counters(300, T0, 360, n_groups=16, seed=0xC4)
+    for agg in ["sum", "avg", "min", "max", "dev"]:
+        q = abi.new_query(T0, T0 + 3599, agg)
+        exact(eng.run_batch(b, q), O.run_query(b, q), agg, f"counters {agg}")
+    rng = np.random.default_rng(3)
+    rows = []
+    for s in range(24):
+        ts = T0 * 1000 + np.sort(rng.choice(np.arange(0, 3600000, 13), 40, replace=False))
+        scale = [10, 1 << 30, 1 << 45, 1 << 61][s % 4]
+        lv = rng.integers(-scale, scale, 40)
+        rows.append(synth.encode_rows(ts, lv, None, np.zeros(40, np.int64), np.ones(40, bool)))
+    b = synth.from_series(rows, [s // 6 for s in range(24)])
+    for agg in ["sum", "max", "mult"]:
+        q = abi.new_query(T0, T0 + 3599, agg)
+        exact(eng.run_batch(b, q), O.run_query(b, q), agg, f"wide {agg}")
+    b = random_batch(77, n_series=60, n_groups=2)
+    q = abi.new_query(T0, T0 + 7199, "sum")
+    exact(eng.run_batch(b, q), O.run_query(b, q), "sum", "mixed")

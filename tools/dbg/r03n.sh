@@ -1,0 +1,6 @@
+set -o pipefail
+out=gpurun_out/r03n; mkdir -p $out; export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_fast.py tests/test_gpu_rollup_read.py tests/test_gpu_rollup.py tests/test_gpu_hist.py -q --timeout 300 --timeout-method thread > $out/tests.log 2>&1; rc=$?; tail -2 $out/tests.log; grep -E "^FAILED" $out/tests.log | head
+case $rc in 0|1) ;; *) exit $rc;; esac
+timeout -k 10 300 python -u tools/rollup_read_bench.py --check > $out/rollup_read.jsonl 2> $out/rr.err; rc=$?; cut -c1-250 $out/rollup_read.jsonl; [ $rc -eq 0 ] || { tail -5 $out/rr.err; exit $rc; }
+bash tools/dbg/r03l.sh
