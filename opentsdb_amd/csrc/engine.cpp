@@ -2673,6 +2673,10 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       fp.B0n = fp.unit_s ? P.B0 / 1000 : P.B0;
       fp.rcpn = std::nextafter(1.0 / (double)fp.In, INFINITY);
       fp.wave_lds = (int32_t)fast_wave_lds(K, q->rate != 0);
+      if (shortk && fp.sel_direct && fp.sel_cols && K <= 64) {   // k_short's column stage
+        fp.sel_stage = fp.wave_lds;
+        fp.wave_lds += (int32_t)align16(8 * K * 8);
+      }
       fp.waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / fp.wave_lds));
       fp.tile_list = list;
       fp.tile_list_n = list_n;

@@ -1031,8 +1031,10 @@ hipError_t hist_accum_window(const HistQueryParams& p, const int32_t* vpos, int6
                      (p.pres ? (size_t)WS * p.W * 4 : 0);
   const char* penv = getenv("TSDBHIP_HIST_PIPE");   // A/B: 0 = the unpipelined bucket loop
   const bool pipe = !(penv && penv[0] == '0');
-  const char* uenv = getenv("TSDBHIP_HIST_SU");     // A/B: 4 = four staging loads in flight a thread
-  const bool su4 = uenv && uenv[0] == '4';
+  // staging loads in flight a thread: 4 (default) or 16 (TSDBHIP_HIST_SU=16).  r03o sweep of the
+  // histogram bench query: 52 KB window + 4 in flight 2.60 ms; + 16 2.77; 80 KB 3.21 / 3.40; 160 KB 5.08
+  const char* uenv = getenv("TSDBHIP_HIST_SU");
+  const bool su4 = !(uenv && uenv[0] == '1');
   const void* kf = pipe ? (su4 ? reinterpret_cast<const void*>(&k_hist_accw<true, 4>)
                                : reinterpret_cast<const void*>(&k_hist_accw<true, 16>))
                         : (su4 ? reinterpret_cast<const void*>(&k_hist_accw<false, 4>)

@@ -1132,14 +1132,18 @@ __device__ __forceinline__ void rp_store(const GridParams& p, int64_t tile, int 
 // sel_vals[s * K + k] (one coalesced row per series; the fill pattern where it has none) and
 // marks the union slots -- k_emit_vals' output without the bucket values round-tripping
 // through pre_dense.
+// stage (k_short, column layout): the row goes to LDS and sel_cols_flush writes 8 series'
+// column pieces at once.
 template <bool MARK = true>   // MARK: flag the row written (k_short flags its whole tile at the end)
 __device__ __forceinline__ void sel_direct_out(const GridParams& p, int K, int32_t g, int64_t s, bool pr_in,
-                                               double v) {
+                                               double v, double* stage = nullptr) {
   double cv = 0.0;
   bool uni;
   const bool has = slot_contribution(p, K, pr_in, v, cv, uni);
   const int lane = lane_id();
-  if (lane < K) {
+  if (stage) {
+    if (lane < K) stage[lane] = has ? canon_nan(cv) : __longlong_as_double(0x7FF87FF87FF87FF8LL);
+  } else if (lane < K) {
     int64_t at = s * K + lane;
     if (p.sel_cols) {   // the (group, slot) column layout: each column contiguous for the select
       const int64_t g0 = p.group_series_ptr[g], ng = p.group_series_ptr[g + 1] - g0;
@@ -1151,6 +1155,29 @@ __device__ __forceinline__ void sel_direct_out(const GridParams& p, int K, int32
   // series' byte stores into 64 x 60 flags serialised on a few L2 lines, 6.5 vs 3.9 ms)
   if (uni && !p.sel_uni[(int64_t)g * K + lane]) p.sel_uni[(int64_t)g * K + lane] = 1;
   if (MARK && lane == 0 && p.sel_wr) p.sel_wr[s] = 1;
+}
+
+// The staged rows of series sa .. sa + nb - 1 (group g, nb <= 8; stage [nb][K]) into their
+// columns: lanes 8c .. 8c + 7 store column k's nb consecutive values (64 B pieces instead of one
+// 8-B store per line).
+__device__ __forceinline__ void sel_cols_flush(const GridParams& p, int K, int32_t g, int64_t sa, int nb,
+                                               const double* stage) {
+  WAVE_SYNC();
+  const int64_t g0 = p.group_series_ptr[g], ng = p.group_series_ptr[g + 1] - g0;
+  double* base = p.sel_vals + g0 * K + (sa - g0);
+  const int lane = lane_id();
+  if (nb == 8) {
+    for (int e = lane; e < 8 * K; e += 64) {
+      const int k = e >> 3, i = e & 7;
+      base[(int64_t)k * ng + i] = stage[i * K + k];
+    }
+  } else {
+    for (int e = lane; e < nb * K; e += 64) {
+      const int k = e / nb, i = e - k * nb;
+      base[(int64_t)k * ng + i] = stage[i * K + k];
+    }
+  }
+  WAVE_SYNC();
 }
 
 // End of series s (group g): its SpanGroup contributions, (dense_out) its bucket values, or
@@ -1764,7 +1791,8 @@ __device__ __forceinline__ double fast_bucket_value(uint32_t c, double a) {
 // for the fused multi-aggregator pass).
 template <int F, bool MARK = true, class RP>
 __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const FastLds& L, int K, int lsb, double amax,
-                                                    RP& P, int64_t s, int32_t g, uint32_t nbound = 0) {
+                                                    RP& P, int64_t s, int32_t g, uint32_t nbound = 0,
+                                                    double* stage = nullptr) {
   const int lane = lane_id();
   WAVE_SYNC();
   uint32_t c = 0;
@@ -1780,7 +1808,7 @@ __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const F
     if (!fast_cert<F>(nmax, lsb, amax)) return false;
   }
   if (p.sel_direct) {
-    sel_direct_out<MARK>(p, K, g, s, c != 0, fast_bucket_value<F>(c, a));
+    sel_direct_out<MARK>(p, K, g, s, c != 0, fast_bucket_value<F>(c, a), stage);
   } else if (p.dense_out) {
     if (lane < K) {
       p.dense_out[s * K + lane] = fast_bucket_value<F>(c, a);
@@ -2075,14 +2103,19 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     }
     return nv0;
   };
+  // sel_direct into the column layout: rows staged 8 series at a time (sel_cols_flush)
+  double* stage = (KR == 1 && p.sel_stage) ? (double*)(smem + (int64_t)wave * p.wave_lds + p.sel_stage) : nullptr;
   auto series_end = [&](int j, int nv0) {
     if (p.dbg & 1) return;
     const int lsb = __builtin_amdgcn_readlane(dlsb, j);
     const double amax = __longlong_as_double((long long)rl64(damax, j));
     const bool fine =
-        KR ? fast_series_end_reg<F, false>(p, L, K, lsb, amax, RP, s0 + j, p.tile_group[tile], (uint32_t)nv0)
+        KR ? fast_series_end_reg<F, false>(p, L, K, lsb, amax, RP, s0 + j, p.tile_group[tile], (uint32_t)nv0,
+                                           stage ? stage + (j & 7) * K : nullptr)
            : fast_series_end<F>(p, L, K, lsb, amax, s0 + j, p.tile_group[tile]);
     if (!fine) redo = true;
+    else if (stage && ((j & 7) == 7 || j == ns - 1))
+      sel_cols_flush(p, K, p.tile_group[tile], s0 + (j & ~7), (j & 7) + 1, stage);
   };
   int j = 0;
   for (; j + D <= ns; j += D) {

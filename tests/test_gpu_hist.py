@@ -228,8 +228,9 @@ def test_gpu_repeated_bucket_keys_last_count_wins(eng):
 
 
 @pytest.mark.parametrize("env", [{"TSDBHIP_HIST_WINDOW": "0"}, {"TSDBHIP_HIST_WS": "1"}, {"TSDBHIP_HIST_WS": "5"},
-                                 {"TSDBHIP_HIST_WS": "64"}, {"TSDBHIP_HIST_PIPE": "0"}, {"TSDBHIP_HIST_LAYOUT": "0"}],
-                         ids=["atomic-kernel", "ws1", "ws5", "ws64", "unpipelined", "keyed"])
+                                 {"TSDBHIP_HIST_WS": "64"}, {"TSDBHIP_HIST_PIPE": "0"}, {"TSDBHIP_HIST_LAYOUT": "0"},
+                                 {"TSDBHIP_HIST_SU": "16"}],
+                         ids=["atomic-kernel", "ws1", "ws5", "ws64", "unpipelined", "keyed", "su16"])
 def test_gpu_accum_window_sizes(eng, env):
     """k_hist_accw keeps a window of consecutive points' counters in LDS; tiles whose points leave
     it flush it, points past its end add to the global counters directly.  Windows of 1, 5 and 64

@@ -22,3 +22,14 @@ for k, d in acc.items():
     print(k)
     for c, v in sorted(d.items()):
         print(f"   {c:22s} {sum(v) / len(v):16.4g}   (n={len(v)})")
+    # derived (MI355X: 256 CUs x 4 SIMDs; a wave64 VALU instruction issues over 4 cycles; GRBM_GUI_ACTIVE
+    # sums the 8 XCDs' busy cycles, so / 8 is the kernel's cycle count)
+    m = {c: sum(v) / len(v) for c, v in d.items()}
+    if "SQ_INSTS_VALU" in m and m.get("GRBM_GUI_ACTIVE"):
+        cyc = m["GRBM_GUI_ACTIVE"] / 8
+        print(f"   => VALU issue utilisation {m['SQ_INSTS_VALU'] * 4 / (1024 * cyc):.3f} "
+              f"(SQ_INSTS_VALU x 4 / (1024 SIMDs x {cyc:.4g} cycles))")
+    if "SQ_WAVE_CYCLES" in m and m["SQ_WAVE_CYCLES"]:
+        for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"):
+            if c in m:
+                print(f"   => {c} / SQ_WAVE_CYCLES {m[c] / m['SQ_WAVE_CYCLES']:.3f}")

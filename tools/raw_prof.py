@@ -1,4 +1,4 @@
-"""Config 4 (raw union path) step breakdown: wall time of the C call, of the Python result
+"""Config 4 (raw union path) step breakdown (argv: series, steps, queries = sum,rate[,p99]): wall time of the C call, of the Python result
 wrapping, and the device time the library reports.  TSDBHIP_TRACE=1 adds the library's own
 phase marks on stderr."""
 import ctypes as C
@@ -21,7 +21,10 @@ def main():
     eng.load(b)
     qs = {"sum": abi.new_query(T0, T0 + 3599, "sum"),
           "rate": abi.new_query(T0, T0 + 3599, "sum", rate=True, counter=True, counter_max=1 << 32,
-                                reset_value=1000000)}
+                                reset_value=1000000),
+          "p99": abi.new_query(T0, T0 + 3599, "p99")}
+    only = sys.argv[3].split(",") if len(sys.argv) > 3 else ["sum", "rate"]
+    qs = {k: v for k, v in qs.items() if k in only}
     for name, q in qs.items():
         eng.run(q)
         call, wrap, dev = [], [], []
