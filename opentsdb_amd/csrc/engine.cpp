@@ -3484,7 +3484,8 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
         const int64_t s0 = bat[bi], s1 = bat[bi + 1];
         const int64_t nv = soff[s1] - soff[s0];
         HIP_OK(hipMemsetAsync(c->r_vp.p, 0, nv, c->stream));
-        HIP_OK(hipMemsetAsync(c->r_vd.p, 0xFF, nv * 8, c->stream));   // NaN: no operand
+        // NaN: no operand (only double points read r_vd; a long-only query never has one)
+        if (rp.do_double) HIP_OK(hipMemsetAsync(c->r_vd.p, 0xFF, nv * 8, c->stream));
         RawParams bp = rp;
         bp.strip_g = rp.strip_g + s0;
         bp.strip_t = rp.strip_t + s0;

@@ -214,6 +214,7 @@ __device__ __forceinline__ double key2f(uint64_t k) {
 }
 
 constexpr int SELW = 4;
+constexpr int RAW_SEL_B = 8;        // operand rows of 64 loaded together (k_raw_sel staging)
 constexpr int RAW_SEL_LDS = 4096;   // keys per wave staged in LDS (4 x 32 KB a block)
 struct SelWave {
   uint32_t hist[256];
@@ -1896,28 +1897,49 @@ __global__ __launch_bounds__(256) void k_raw_sel(RawParams p, int32_t kcap) {
                           : reinterpret_cast<uint64_t*>(is_int ? (void*)p.vals_l : (void*)p.vals_d) + vb;
   const uint64_t below = (1ULL << lane) - 1ULL;   // lanes < lane
   int m = 0;
+  // RAW_SEL_B rows of 64 operands loaded before any is used: the operands are strided by
+  // RAW_STRIP (one line each), so a load-use chain per row left the kernel waiting on memory
+  // latency 25 times a point for config 4's 1560-span groups
   if (is_int) {
     // present long operands, compacted (their order does not matter to a selection)
-    for (int base = 0; base < k; base += 64) {
-      const int i = base + lane;
-      const bool pres = i < k && p.vals_p[vb + i * US];
-      const uint64_t bal = (uint64_t)__ballot(pres);
-      const uint64_t key = pres ? (uint64_t)p.vals_l[vb + i * US] ^ 0x8000000000000000ULL : 0;
-      WAVE_SYNC();   // in place: every lane has read its operand before any is overwritten
-      if (pres) keys[(m + __popcll(bal & below)) * ks] = key;
-      m += __popcll(bal);
+    for (int base = 0; base < k; base += 64 * RAW_SEL_B) {
+      bool pres[RAW_SEL_B];
+      uint64_t key[RAW_SEL_B];
+#pragma unroll
+      for (int u = 0; u < RAW_SEL_B; u++) {
+        const int i = base + 64 * u + lane;
+        const int ic = i < k ? i : 0;
+        pres[u] = i < k && p.vals_p[vb + ic * US];
+        key[u] = (uint64_t)p.vals_l[vb + ic * US] ^ 0x8000000000000000ULL;
+      }
+      WAVE_SYNC();   // in place: every lane has read its operands before any is overwritten
+#pragma unroll
+      for (int u = 0; u < RAW_SEL_B; u++) {
+        const uint64_t bal = (uint64_t)__ballot(pres[u]);
+        if (pres[u]) keys[(m + __popcll(bal & below)) * ks] = key[u];
+        m += __popcll(bal);
+      }
     }
   } else {
     int nan = 0;
-    for (int base = 0; base < k; base += 64) {
-      const int i = base + lane;
-      bool isn = false;
-      if (i < k) {
-        const double x = p.vals_d[vb + i * US];
-        isn = isnan(x);
-        keys[i * ks] = f2key(canon_nan(x));
+    for (int base = 0; base < k; base += 64 * RAW_SEL_B) {
+      double x[RAW_SEL_B];
+#pragma unroll
+      for (int u = 0; u < RAW_SEL_B; u++) {
+        const int i = base + 64 * u + lane;
+        x[u] = p.vals_d[vb + (int64_t)(i < k ? i : 0) * US];
       }
-      nan += __popcll((uint64_t)__ballot(isn));
+      WAVE_SYNC();
+#pragma unroll
+      for (int u = 0; u < RAW_SEL_B; u++) {
+        const int i = base + 64 * u + lane;
+        bool isn = false;
+        if (i < k) {
+          isn = isnan(x[u]);
+          keys[i * ks] = f2key(canon_nan(x[u]));
+        }
+        nan += __popcll((uint64_t)__ballot(isn));
+      }
     }
     m = k - nan;
   }

@@ -497,6 +497,18 @@ __global__ __launch_bounds__(64) void k_raw_vals(RawParams p) {
         if (c == n) continue;
         const RawPt a = pts[c - 1], b = pts[c];
         if ((a.tsf | b.tsf) & RAW_FLOAT) flt = (1u << RAW_W) - 1;
+        if (DL && p.lerp_fast) {   // the strip-wide window (lerpw_*, as in k_raw_eval)
+          const int64_t x0 = a.tsf & RAW_TIME_MASK, x1 = b.tsf & RAW_TIME_MASK;
+          const LerpW L = lerpw_init(interp, uns, x0, (int64_t)a.bits, x1, (int64_t)b.bits);
+          if (L.ok) {
+#pragma unroll
+            for (int w = 0; w < RAW_W; w++) {
+              put_l(i, w, lerpw_eval(L, x[w]));
+              if (DD) put_d(i, w, dlerp(interp, x[w], x0, pt_double(a.tsf, a.bits), x1, pt_double(b.tsf, b.bits)));
+            }
+            continue;
+          }
+        }
 #pragma unroll
         for (int w = 0; w < RAW_W; w++) put_lerp(i, w, a, b);
       }
