@@ -1867,6 +1867,66 @@ __device__ __forceinline__ int64_t sel_d2l(double d) {   // Java (long) of a dou
   return (int64_t)d;
 }
 
+// The ranks select_sorted reads among m values at a union point (r1 = -1: one value) and the
+// interpolation weight: Median.runLong / runDouble sorted[m / 2]; PercentileAgg with its
+// estimation type for runLong, LEGACY for runDouble (src/core/Aggregators.java:403-430, :675-706).
+__device__ __forceinline__ void raw_sel_ranks(int fn, bool is_int, int m, int& r0, int& r1, double& dif) {
+  r0 = 0;
+  r1 = -1;
+  dif = 0.0;
+  const int est = fn == TSDB_AGG_MEDIAN ? 0 : (is_int ? (fn - TSDB_AGG_P999) / 6 : 0);   // runDouble: LEGACY
+  if (m > 1 && fn != TSDB_AGG_MEDIAN) {
+    const double q = pct_quantile(fn) / 100.0;
+    double pos;
+    if (est == 1) {            // R_3
+      pos = (q <= 0.5 / (double)m) ? 0.0 : rint((double)m * q);
+    } else if (est == 2) {     // R_7
+      pos = (q == 0.0) ? 0.0 : (q == 1.0 ? (double)m : 1.0 + (double)(m - 1) * q);
+    } else {                   // LEGACY
+      pos = (q == 0.0) ? 0.0 : (q == 1.0 ? (double)m : q * (double)(m + 1));
+    }
+    const double fpos = floor(pos);
+    if (pos < 1) r0 = 0;
+    else if (pos >= (double)m) r0 = m - 1;
+    else { r0 = (int)fpos - 1; r1 = r0 + 1; dif = pos - fpos; }
+  } else if (m > 0 && fn == TSDB_AGG_MEDIAN) {
+    r0 = m / 2;
+  }
+}
+
+// longValue / doubleValue of the selection (k0, k1: keys of ranks r0, r0 + 1) into out_bits.
+__device__ __forceinline__ void raw_sel_store(const RawParams& p, int64_t idx, bool is_int, int fn, int m, int r1,
+                                              double dif, uint64_t k0, uint64_t k1) {
+  uint64_t bits;
+  if (is_int) {
+    const int64_t l0 = (int64_t)(k0 ^ 0x8000000000000000ULL), l1 = (int64_t)(k1 ^ 0x8000000000000000ULL);
+    int64_t r;
+    if (fn == TSDB_AGG_MEDIAN) {
+      if (m == 0) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // "Shouldn't be here without any data"
+      r = l0;
+    } else if (m == 0) {
+      r = 0;                                               // (long) NaN
+    } else if (r1 < 0) {
+      r = sel_d2l((double)l0);
+    } else {
+      const double lower = (double)l0, upper = (double)l1;
+      r = sel_d2l(lower + dif * (upper - lower));
+    }
+    bits = (uint64_t)r;
+  } else {
+    double r;
+    if (m == 0) r = NAN;
+    else if (r1 < 0) r = key2f(k0);
+    else {
+      const double lower = key2f(k0), upper = key2f(k1);
+      r = lower + dif * (upper - lower);
+    }
+    if (isinf(r)) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // doubleValue (:640-643)
+    bits = (uint64_t)__double_as_longlong(r);
+  }
+  p.out_bits[idx] = bits;
+}
+
 // One WAVE per union point of the batch's strips (4 waves a block, no block barriers):
 // point pt -> strip pt / RAW_STRIP, position j.  Wave-local radix select: 8-bit digits, a
 // 256-bin LDS histogram per wave, the digit holding rank r found by a wave prefix sum over
@@ -1946,26 +2006,9 @@ __global__ __launch_bounds__(256) void k_raw_sel(RawParams p, int32_t kcap) {
   WAVE_SYNC();
   const int n = is_int ? m : k;   // keys staged
   const int fn = p.sel_fn;
-  int r0 = 0, r1 = -1;
-  double dif = 0.0;
-  const int est = fn == TSDB_AGG_MEDIAN ? 0 : (is_int ? (fn - TSDB_AGG_P999) / 6 : 0);   // runDouble: LEGACY
-  if (m > 1 && fn != TSDB_AGG_MEDIAN) {
-    const double q = pct_quantile(fn) / 100.0;
-    double pos;
-    if (est == 1) {            // R_3
-      pos = (q <= 0.5 / (double)m) ? 0.0 : rint((double)m * q);
-    } else if (est == 2) {     // R_7
-      pos = (q == 0.0) ? 0.0 : (q == 1.0 ? (double)m : 1.0 + (double)(m - 1) * q);
-    } else {                   // LEGACY
-      pos = (q == 0.0) ? 0.0 : (q == 1.0 ? (double)m : q * (double)(m + 1));
-    }
-    const double fpos = floor(pos);
-    if (pos < 1) r0 = 0;
-    else if (pos >= (double)m) r0 = m - 1;
-    else { r0 = (int)fpos - 1; r1 = r0 + 1; dif = pos - fpos; }
-  } else if (m > 0 && fn == TSDB_AGG_MEDIAN) {
-    r0 = m / 2;
-  }
+  int r0, r1;
+  double dif;
+  raw_sel_ranks(fn, is_int, m, r0, r1, dif);
   uint64_t k0 = 0, k1 = 0;
   if (m > 0) {
     k0 = wave_radix_select(keys, ks, n, r0, W);
@@ -1984,40 +2027,174 @@ __global__ __launch_bounds__(256) void k_raw_sel(RawParams p, int32_t kcap) {
       k1 = le > r1 ? k0 : gt;
     }
   }
-  if (lane != 0) return;
-  uint64_t bits;
-  if (is_int) {
-    const int64_t l0 = (int64_t)(k0 ^ 0x8000000000000000ULL), l1 = (int64_t)(k1 ^ 0x8000000000000000ULL);
-    int64_t r;
-    if (fn == TSDB_AGG_MEDIAN) {
-      if (m == 0) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // "Shouldn't be here without any data"
-      r = l0;
-    } else if (m == 0) {
-      r = 0;                                               // (long) NaN
-    } else if (r1 < 0) {
-      r = sel_d2l((double)l0);
-    } else {
-      const double lower = (double)l0, upper = (double)l1;
-      r = sel_d2l(lower + dif * (upper - lower));
-    }
-    bits = (uint64_t)r;
-  } else {
-    double r;
-    if (m == 0) r = NAN;
-    else if (r1 < 0) r = key2f(k0);
-    else {
-      const double lower = key2f(k0), upper = key2f(k1);
-      r = lower + dif * (upper - lower);
-    }
-    if (isinf(r)) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // doubleValue (:640-643)
-    bits = (uint64_t)__double_as_longlong(r);
+  if (lane == 0) raw_sel_store(p, idx, is_int, fn, m, r1, dif, k0, k1);
+}
+
+// Register-resident variant (groups of <= 64 KPL spans): lane l holds operands l, l + 64, ...
+// as keys (all KPL loads in flight together), a validity mask stands in for the compaction,
+// and the radix passes read registers.  The wave's LDS is the 256-bin histogram and the
+// candidate list only, so residency is set by registers (k_raw_sel: a 12.5-KB key stage per
+// wave for config 4's 1560-span groups, 3 waves a SIMD).  Same ranks, same keys, same result.
+template <int KPL>
+__device__ uint64_t wave_radix_select_reg(const uint64_t (&kr)[KPL], uint64_t vm, int r, SelWave& W) {
+  const int lane = lane_id();
+  uint64_t kand = ~0ULL, kor = 0;
+#pragma unroll
+  for (int u = 0; u < KPL; u++)
+    if ((vm >> u) & 1ULL) { kand &= kr[u]; kor |= kr[u]; }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    kand &= shfl_u64(kand, lane ^ d);
+    kor |= shfl_u64(kor, lane ^ d);
   }
-  p.out_bits[idx] = bits;
+  const uint64_t diff = kand ^ kor;
+  if (diff == 0) return kand;
+  const int top = (63 - __clzll((long long)diff)) & ~7;
+  uint64_t mask = top == 56 ? 0 : ~((1ULL << (top + 8)) - 1ULL);
+  uint64_t prefix = kand & mask;
+  for (int shift = top; shift >= 0; shift -= 8) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) W.hist[lane * 4 + q] = 0;
+    WAVE_SYNC();
+#pragma unroll
+    for (int u = 0; u < KPL; u++)
+      if (((vm >> u) & 1ULL) && (kr[u] & mask) == prefix) atomicAdd(&W.hist[(kr[u] >> shift) & 255], 1u);
+    WAVE_SYNC();
+    uint32_t c[4], t = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) { c[q] = W.hist[lane * 4 + q]; t += c[q]; }
+    const int incl = wave_incl_sum((int)t);
+    int ex = incl - (int)t;
+    const bool found = ex <= r && r < incl;
+    int bin = 0, rr = 0, nc = 0;
+    if (found) {
+      int q = 0;
+      for (; q < 3; q++) {
+        if (r < ex + (int)c[q]) break;
+        ex += (int)c[q];
+      }
+      bin = lane * 4 + q;
+      rr = r - ex;
+      nc = (int)c[q];
+    }
+    const int src = __ffsll((long long)__ballot(found)) - 1;
+    bin = __shfl(bin, src, 64);
+    rr = __shfl(rr, src, 64);
+    nc = __shfl(nc, src, 64);
+    prefix |= (uint64_t)bin << shift;
+    mask |= 255ULL << shift;
+    r = rr;
+    WAVE_SYNC();
+    if (shift == 0) break;
+    if (nc <= 64) {
+      if (lane == 0) W.n = 0;
+      WAVE_SYNC();
+#pragma unroll
+      for (int u = 0; u < KPL; u++)
+        if (((vm >> u) & 1ULL) && (kr[u] & mask) == prefix) W.cand[atomicAdd(&W.n, 1u)] = kr[u];
+      WAVE_SYNC();
+      const uint64_t x = lane < nc ? W.cand[lane] : ~0ULL;
+      int less = 0, eq = 0;
+      for (int q = 0; q < nc; q++) {
+        const uint64_t y = W.cand[q];
+        less += y < x;
+        eq += y == x;
+      }
+      const bool hit = lane < nc && less <= r && r < less + eq;
+      const uint64_t res = shfl_u64(x, __ffsll((long long)__ballot(hit)) - 1);
+      WAVE_SYNC();
+      return res;
+    }
+  }
+  return prefix;
+}
+
+template <int KPL>
+__global__ __launch_bounds__(256) void k_raw_sel_reg(RawParams p) {
+  __shared__ SelWave WS[SELW];
+  const int wv = threadIdx.x >> 6;
+  const int lane = lane_id();
+  const int64_t pt = (int64_t)blockIdx.x * SELW + wv;
+  const int64_t sl = pt / RAW_STRIP;
+  const int64_t j = pt - sl * RAW_STRIP;
+  if (sl >= p.n_strips) return;   // whole waves leave; no block barrier follows
+  const int64_t gi = p.strip_g[sl];
+  const int64_t u0 = (int64_t)p.strip_t[sl] * RAW_STRIP + j;
+  if (u0 >= p.U[gi]) return;
+  const int64_t idx = p.out_off[gi] + u0;
+  const int64_t g = gi + p.g0;
+  const int k = (int)(p.grp_ser[g + 1] - p.grp_ser[g]);   // <= 64 KPL (host-checked)
+  const int64_t vb = p.vals_off[sl] + j;
+  constexpr int64_t US = RAW_STRIP;
+  const bool is_int = p.out_int[idx] != 0;
+  SelWave& W = WS[wv];
+  uint64_t kr[KPL];
+  uint64_t vm = 0;
+  int m;
+  if (is_int) {
+    bool pr[KPL];
+#pragma unroll
+    for (int u = 0; u < KPL; u++) {
+      const int i = 64 * u + lane;
+      const int64_t ic = i < k ? i : 0;
+      pr[u] = i < k && p.vals_p[vb + ic * US];
+      kr[u] = (uint64_t)p.vals_l[vb + ic * US] ^ 0x8000000000000000ULL;
+    }
+#pragma unroll
+    for (int u = 0; u < KPL; u++) vm |= (uint64_t)pr[u] << u;
+    m = wave_sum_int(__popcll(vm));
+  } else {
+    int nan = 0;
+#pragma unroll
+    for (int u = 0; u < KPL; u++) {
+      const int i = 64 * u + lane;
+      const double x = p.vals_d[vb + (int64_t)(i < k ? i : 0) * US];
+      kr[u] = f2key(canon_nan(x));
+      if (i < k) {
+        vm |= 1ULL << u;
+        nan += isnan(x) ? 1 : 0;
+      }
+    }
+    m = k - wave_sum_int(nan);   // NaN keys sort above every number; ranks < m never reach them
+  }
+  const int fn = p.sel_fn;
+  int r0, r1;
+  double dif;
+  raw_sel_ranks(fn, is_int, m, r0, r1, dif);
+  uint64_t k0 = 0, k1 = 0;
+  if (m > 0) {
+    k0 = wave_radix_select_reg<KPL>(kr, vm, r0, W);
+    k1 = k0;
+    if (r1 >= 0) {
+      int le = 0;
+      uint64_t gt = ~0ULL;
+#pragma unroll
+      for (int u = 0; u < KPL; u++) {
+        if (!((vm >> u) & 1ULL)) continue;
+        if (kr[u] <= k0) le++;
+        else gt = kr[u] < gt ? kr[u] : gt;
+      }
+      le = wave_sum_int(le);
+      gt = wave_min_u64(gt);
+      k1 = le > r1 ? k0 : gt;
+    }
+  }
+  if (lane == 0) raw_sel_store(p, idx, is_int, fn, m, r1, dif, k0, k1);
 }
 
 // k_max: the largest group of the batch; each wave stages k_max keys in LDS.
 hipError_t launch_raw_sel(const RawParams& p, int64_t k_max, hipStream_t s) {
   if (p.n_strips == 0) return hipSuccess;
+  const char* renv = std::getenv("TSDBHIP_RAW_SEL_REG");   // A/B: 0 = the LDS-staged kernel
+  if (k_max <= 64 * 32 && !(renv && renv[0] == '0')) {
+    const dim3 grid((unsigned)((p.n_strips * RAW_STRIP + SELW - 1) / SELW)), block(64 * SELW);
+    if (k_max <= 64 * 8) hipLaunchKernelGGL(k_raw_sel_reg<8>, grid, block, 0, s, p);
+    else if (k_max <= 64 * 16) hipLaunchKernelGGL(k_raw_sel_reg<16>, grid, block, 0, s, p);
+    // 26 keys a lane (groups of <= 1664 spans, config 4's 1560) still fit 4 waves a SIMD; 32 take 3
+    else if (k_max <= 64 * 26) hipLaunchKernelGGL(k_raw_sel_reg<26>, grid, block, 0, s, p);
+    else hipLaunchKernelGGL(k_raw_sel_reg<32>, grid, block, 0, s, p);
+    return hipGetLastError();
+  }
   const int32_t kcap = (int32_t)std::max<int64_t>(1, std::min<int64_t>(k_max, RAW_SEL_LDS));
   const size_t lds = (size_t)kcap * 8 * SELW;
   hipError_t e = hipFuncSetAttribute((const void*)k_raw_sel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)((size_t)RAW_SEL_LDS * 8 * SELW));

@@ -117,3 +117,22 @@ def test_raw_pct_strip_batches(eng, ops, monkeypatch):
     for agg in ["p95", "ep50r3", "median"]:
         q = abi.new_query(T0, T0 + 3 * 3600 - 1, agg)
         exact(eng.run_batch(b, q), O.run_query(b, q), agg, f"ops {ops} {agg}")
+
+
+@pytest.mark.parametrize("reg", ["0", "1"])
+@pytest.mark.parametrize("n_spans", [40, 700, 1600, 2000])
+def test_raw_pct_register_select(eng, monkeypatch, reg, n_spans):
+    """k_raw_sel_reg (keys in registers, 8 / 16 / 26 / 32 a lane by group size) and the
+    LDS-staged k_raw_sel (TSDBHIP_RAW_SEL_REG=0) against the oracle: long points with absent
+    operands (spans not started or ended), double points with NaN members, ties."""
+    monkeypatch.setenv("TSDBHIP_RAW_SEL_REG", reg)
+    eng.synth(n_spans, T0, 4, 10000, 1, 1, 40, 0xA5 + n_spans)
+    b = eng.download()
+    for agg in ["p99", "median", "ep75r7"]:
+        q = abi.new_query(T0, T0 + 3599, agg)
+        exact(eng.run(q), O.run_query(b, q), agg, f"int {n_spans} {agg}")
+    for mixed in (False, True):
+        b = random_batch(n_spans, n_series=n_spans, n_groups=1, mixed=mixed, span_h=1)
+        for agg in ["p95", "median"]:
+            q = abi.new_query(T0, T0 + 3599, agg)
+            exact(eng.run_batch(b, q), O.run_query(b, q), agg, f"random {mixed} {n_spans} {agg}")
