@@ -462,6 +462,10 @@ struct tsdbhip_ctx {
   void* cmp_tmp = nullptr;
   size_t cmp_tmp_bytes = 0;
   bool ro_scan_valid = false;          // scan-active value series of the last scan range
+  // the last scan range whose rollup rows passed ro_scan's checks (a host walk over every row:
+  // 4 ms a query for a 1M-series table; the store is immutable until the next load)
+  bool ro_chk_valid = false, ro_chk_counts = false;
+  int64_t ro_chk_ss = 0, ro_chk_se = 0, ro_chk_T = 0;
   int64_t ro_scan_ss = 0, ro_scan_se = 0;
   std::vector<uint8_t> ro_scan_act;    // [n_series] resident: rollup rows in the scan range
   // histogram path (hist.cpp): the resident histogram store and its query scratch
@@ -665,6 +669,7 @@ static void release_batch(tsdbhip_ctx* c) {
   c->n_series = c->n_rows = c->n_groups = 0;
   c->ro_active = c->ro_counts = false;
   c->ro_scan_valid = false;
+  c->ro_chk_valid = false;
   c->ro_nval = 0;
   c->ro_rp.clear();
   c->ro_rows.clear();
@@ -1379,6 +1384,7 @@ extern "C" int tsdbhip_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* r
   c->ro_nval = NS;
   c->ro_rp = std::move(rp);
   c->ro_rows = std::move(rows);
+  c->ro_chk_valid = false;
   c->ro_unsup = std::move(unsup);
   c->ro_res.assign(c->n_series, -1);
   for (int64_t i = 0; i < c->n_series; i++) c->ro_res[c->h_orig[i]] = i;
@@ -3775,7 +3781,11 @@ namespace {
 // (thrown while the spans are built, in scan order), reads the engine does not restate, and
 // which value series the scan finds (cached per scan range).
 int ro_scan(tsdbhip_ctx* c, const Plan& P, bool reads_counts) {
-  for (int64_t s = 0; s < c->ro_nval; s++) {
+  const int64_t S0 = P.ss * 1000;
+  const int64_t T = P.mode == MODE_TABLE ? P.seek : (P.mode == MODE_ALL ? S0 : P.B0);
+  const bool checked = c->ro_chk_valid && c->ro_chk_ss == P.ss && c->ro_chk_se == P.se && c->ro_chk_T == T &&
+                       (c->ro_chk_counts || !reads_counts);
+  for (int64_t s = 0; s < c->ro_nval && !checked; s++) {
     const RoSeqRow* first_err = nullptr;
     bool in = false, verr = false, cerr = false;
     for (int64_t i = c->ro_rp[s]; i < c->ro_rp[s + 1]; i++) {
@@ -3796,9 +3806,7 @@ int ro_scan(tsdbhip_ctx* c, const Plan& P, bool reads_counts) {
   // cell where they stop pairing one to one its iteration differs from a fresh one's.  The
   // Downsampler seeks every span to its first bucket; a RollupSeq it seeks into past such a
   // cell is not restated.
-  const int64_t S0 = P.ss * 1000;
-  const int64_t T = P.mode == MODE_TABLE ? P.seek : (P.mode == MODE_ALL ? S0 : P.B0);
-  if (c->ro_counts && T > S0) {
+  if (c->ro_counts && T > S0 && !checked) {
     for (int64_t s = 0; s < c->ro_nval; s++) {
       const RoSeqRow* pick = nullptr;   // Span.seekRow: first row (by base) whose last point >= T
       for (int64_t i = c->ro_rp[s]; i < c->ro_rp[s + 1]; i++) {
@@ -3809,6 +3817,13 @@ int ro_scan(tsdbhip_ctx* c, const Plan& P, bool reads_counts) {
       if (pick && pick->pp_ts < T)
         return fail(TSDB_E_NOT_IMPLEMENTED, "rollup row whose value and count cells stop pairing before the seek point");
     }
+  }
+  if (!checked) {   // every check passed for this range (failures are not cached: they re-raise)
+    c->ro_chk_valid = true;
+    c->ro_chk_ss = P.ss;
+    c->ro_chk_se = P.se;
+    c->ro_chk_T = T;
+    c->ro_chk_counts = reads_counts;
   }
   if (!(c->ro_scan_valid && c->ro_scan_ss == P.ss && c->ro_scan_se == P.se)) {
     c->ro_scan_act.assign(std::max<int64_t>(1, c->n_series), 0);
