@@ -429,6 +429,7 @@ struct tsdbhip_ctx {
   // account() cache (invalidated by every load)
   bool acct_valid = false;
   bool seqd_valid = false;             // cached seq_dense_wanted answer for (seqd_ss, seqd_se)
+  bool seqd_uniform = false;          // every row of the cached scan range has one qualifier width and value length
   bool seqd_ok = false, seqd_nocert = false, seqd_tiny = false;
   int64_t seqd_ss = 0, seqd_se = 0;
   int64_t acct_ss = 0, acct_se = 0, acct_dps = 0, acct_bytes = 0;
@@ -2573,7 +2574,8 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     if (P.seq_dense) {
       HIP_OK(hipEventRecord(c->ev[0], c->stream));
       HIP_OK(hipMemsetAsync(c->pre_pres.p, 0, std::max<int64_t>(1, c->n_series * K), c->stream));
-      HIP_OK(launch_seq_dense(gp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->n_series, c->stream));
+      HIP_OK(launch_seq_dense(gp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->n_series, c->stream,
+                              c->seqd_uniform));
     }
     gp.sel_fn = q->ds_function;
     gp.n_series = c->n_series;
@@ -3926,13 +3928,15 @@ bool seq_dense_wanted(tsdbhip_ctx* c, const Plan& P) {
   if (const char* e = std::getenv("TSDBHIP_SEQ")) if (e[0] == '0') return false;   // tests: the k_grid path
   if (const char* e = std::getenv("TSDBHIP_FAST")) if (e[0] == '0') return false;  // (the general path only)
   if (!(c->seqd_valid && c->seqd_ss == P.ss && c->seqd_se == P.se)) {
-    bool any = false, ok = true;
+    bool any = false, ok = true, uni = true;
     int64_t rows = 0, dps = 0;
     for (int64_t r = 0; r < c->n_rows && ok; r++) {
       if ((int64_t)c->h_base[r] < P.ss || (int64_t)c->h_base[r] >= P.se) continue;
       const uint32_t f = c->h_flags[r];
       ok = !(f & ROW_UNSORTED);
       any = any || (f & ROW_NOCERT);
+      const int qw = f & ROW_QW_MASK, vl = (f & ROW_VL_MASK) >> ROW_VL_SHIFT;
+      uni = uni && (qw == 2 || qw == 4) && (vl == 1 || vl == 2 || vl == 4 || vl == 8);
       rows++;
       dps += c->h_ndp[r];
     }
@@ -3942,6 +3946,9 @@ bool seq_dense_wanted(tsdbhip_ctx* c, const Plan& P) {
     c->seqd_ok = ok;
     c->seqd_nocert = any;
     c->seqd_tiny = rows >= 100000 && dps <= 8 * rows;
+    // k_seq_wave walks a series' rows one after the other with the whole wave: worth it for long
+    // rows only (a rollup table read as one-cell rows: 144 rows a series, 47 vs 3.9 ms)
+    c->seqd_uniform = uni && dps >= 64 * rows;
   }
   if (!c->seqd_ok) return false;
   return (c->seqd_nocert && (P.f == F_SUM || P.f == F_AVG)) || c->seqd_tiny;

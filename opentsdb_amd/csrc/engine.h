@@ -450,7 +450,8 @@ bool pct_rows_supported(int qw, int vl);
 hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s);
 hipError_t launch_emit(const GridParams& p, hipStream_t s);
 // sum / avg downsampling in Java's order, one series per thread, into [series][K] (k_misc.hip)
-hipError_t launch_seq_dense(const GridParams& p, int f, double* dense, uint8_t* pres, int64_t n_series, hipStream_t s);
+hipError_t launch_seq_dense(const GridParams& p, int f, double* dense, uint8_t* pres, int64_t n_series, hipStream_t s,
+                            bool uniform = false);   // uniform: every row of one width (k_seq_wave)
 hipError_t launch_emit_vals(const GridParams& p, hipStream_t s);
 hipError_t launch_sel_seg(const SelParams& p, hipStream_t s, int64_t maxn);
 hipError_t launch_ordered(const OrdParams& p, hipStream_t s);

@@ -2,6 +2,7 @@
 // per-function dispatch of libtsdbhip (the k_grid / k_fast instantiations live in
 // k_grid.hip / k_fast.hip, compiled once per downsample function).
 #include "kcommon.h"
+#include <cstdlib>
 
 namespace tsdb {
 
@@ -147,11 +148,179 @@ __global__ __launch_bounds__(256) void k_seq_dense(GridParams p, double* __restr
   flush();
 }
 
-hipError_t launch_seq_dense(const GridParams& p, int f, double* dense, uint8_t* pres, int64_t n_series, hipStream_t s) {
+// The same sums with one WAVE per series (K <= 64): a row's datapoints are loaded by the whole
+// wave in 512-point chunks (lane l: points 8l .. 8l + 7, so the 16-byte loads of neighbouring
+// lanes are neighbouring bytes) and staged in LDS with their slots; lane b then folds bucket
+// b's values in stored order.  Slots never decrease along a sorted series, so a bucket's values
+// in a chunk are one run [start, end), found by the lanes that own its edges.  k_seq_dense's
+// one-series-per-lane walk reads 16 bytes of a different line per lane and instruction (1M
+// rollup rows: 3.9 ms).  Rows of mixed widths are decoded by lane 0, in order, into the same stage.
+constexpr int SEQW_DP = 512;
+constexpr int SEQW_WAVES = 4;
+template <int F>
+__global__ __launch_bounds__(64 * SEQW_WAVES) void k_seq_wave(GridParams p, double* __restrict__ dense,
+                                                             uint8_t* __restrict__ pres, int64_t n_series) {
+  __shared__ double sval[SEQW_WAVES][SEQW_DP];
+  __shared__ int32_t sslot[SEQW_WAVES][SEQW_DP];
+  __shared__ int32_t srun[SEQW_WAVES][2][64];
+  const int wv = threadIdx.x >> 6;
+  const int lane = lane_id();
+  const int64_t s = (int64_t)blockIdx.x * SEQW_WAVES + wv;
+  if (s >= n_series) return;   // whole waves leave; no block barrier follows
+  const int K = (int)p.K;      // <= 64 (host-checked)
+  double* V = sval[wv];
+  int32_t* S = sslot[wv];
+  int32_t* RS = srun[wv][0];
+  int32_t* RE = srun[wv][1];
+  BState st;
+  bs_init<F>(st);
+  bool has = false;
+  for (int64_t r = p.series_row_ptr[s]; r < p.series_row_ptr[s + 1]; r++) {
+    const RowDesc d = p.rows[r];
+    if ((int64_t)d.base < p.ss) continue;
+    if ((int64_t)d.base >= p.se) break;
+    if (d.flags & ROW_ERR) { if (lane == 0) set_err(p.err, TSDB_E_ILLEGAL_DATA); continue; }
+    const int qw = d.flags & ROW_QW_MASK;
+    const int vl = (d.flags & ROW_VL_MASK) >> ROW_VL_SHIFT;
+    const bool uni = (qw == 2 || qw == 4) && (vl == 1 || vl == 2 || vl == 4 || vl == 8);
+    const RowGeom g = row_geom(p, d.base);
+    const uint8_t* qb = p.qual + d.qoff;
+    const uint8_t* vb = p.val + d.voff;
+    const int64_t ndp = d.ndp;
+    uint64_t qi = 0, vi = 0;   // lane 0's cursor through a row of mixed widths
+    for (int64_t c0 = 0; c0 < ndp; c0 += SEQW_DP) {
+      const int n = (int)min((int64_t)SEQW_DP, ndp - c0);
+      if (uni) {
+        const int64_t i0 = c0 + (int64_t)lane * DPL;
+        if (lane * DPL < n) {
+          uint32_t off[DPL], fl[DPL];
+          if (qw == 2) {
+            const uint4 q = *reinterpret_cast<const uint4*>(qb + i0 * 2);
+            const uint32_t ws[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int j = 0; j < DPL; j++) {
+              const uint32_t be = __builtin_bswap32(ws[j >> 1]);
+              const uint32_t qq = (j & 1) ? (be & 0xFFFF) : (be >> 16);
+              off[j] = (qq >> 4) * 1000u;
+              fl[j] = qq & 0xF;
+            }
+          } else {
+            const uint4 q0 = *reinterpret_cast<const uint4*>(qb + i0 * 4);
+            const uint4 q1 = *reinterpret_cast<const uint4*>(qb + i0 * 4 + 16);
+            const uint32_t ws[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+            for (int j = 0; j < DPL; j++) {
+              const uint32_t qq = __builtin_bswap32(ws[j]);
+              off[j] = (qq & 0x0FFFFFC0u) >> 6;
+              fl[j] = qq & 0xF;
+            }
+          }
+          double val[DPL];
+          if (vl == 8) {
+            const uint4* v = reinterpret_cast<const uint4*>(vb + i0 * 8);
+            const uint4 a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
+            const uint32_t ws[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                                     a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+#pragma unroll
+            for (int j = 0; j < DPL; j++) {
+              const uint64_t b = ((uint64_t)__builtin_bswap32(ws[2 * j]) << 32) | __builtin_bswap32(ws[2 * j + 1]);
+              val[j] = (fl[j] & 8) ? __longlong_as_double((long long)b) : (double)(long long)b;
+            }
+          } else if (vl == 4) {
+            const uint4* v = reinterpret_cast<const uint4*>(vb + i0 * 4);
+            const uint4 a0 = v[0], a1 = v[1];
+            const uint32_t ws[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+            for (int j = 0; j < DPL; j++) {
+              const uint32_t be = __builtin_bswap32(ws[j]);
+              val[j] = (fl[j] & 8) ? (double)__uint_as_float(be) : (double)(int32_t)be;
+            }
+          } else if (vl == 2) {
+            const uint4 a0 = *reinterpret_cast<const uint4*>(vb + i0 * 2);
+            const uint32_t ws[4] = {a0.x, a0.y, a0.z, a0.w};
+#pragma unroll
+            for (int j = 0; j < DPL; j++) {
+              const uint32_t be = __builtin_bswap32(ws[j >> 1]);
+              val[j] = (double)(int16_t)(uint16_t)((j & 1) ? (be & 0xFFFF) : (be >> 16));
+            }
+          } else {
+            const uint2 a0 = *reinterpret_cast<const uint2*>(vb + i0);
+            const uint32_t ws[2] = {a0.x, a0.y};
+#pragma unroll
+            for (int j = 0; j < DPL; j++) val[j] = (double)(int8_t)((ws[j >> 2] >> ((j & 3) * 8)) & 0xFF);
+          }
+#pragma unroll
+          for (int j = 0; j < DPL; j++) {
+            const int i = lane * DPL + j;
+            if (i < n) {
+              V[i] = val[j];
+              S[i] = slot_of(p, g, d.base, off[j]);
+            }
+          }
+        }
+      } else if (lane == 0) {
+        // RowSeq.Iterator: the width from the qualifier's first byte, the length from its flags
+        for (int i = 0; i < n; i++) {
+          uint32_t off, fl;
+          if ((qb[qi] & 0xF0) == 0xF0) {
+            const uint32_t qq = ((uint32_t)qb[qi] << 24) | ((uint32_t)qb[qi + 1] << 16) | ((uint32_t)qb[qi + 2] << 8) | qb[qi + 3];
+            off = (qq & 0x0FFFFFC0u) >> 6;
+            fl = qq & 0xF;
+            qi += 4;
+          } else {
+            const uint32_t qq = ((uint32_t)qb[qi] << 8) | qb[qi + 1];
+            off = (qq >> 4) * 1000u;
+            fl = qq & 0xF;
+            qi += 2;
+          }
+          const int len = (int)(fl & 7) + 1;
+          uint64_t be = 0;
+          for (int t = 0; t < len; t++) be = (be << 8) | vb[vi + t];
+          vi += len;
+          double x;
+          if (fl & 8) x = len == 4 ? (double)__uint_as_float((uint32_t)be) : __longlong_as_double((long long)be);
+          else x = (double)((long long)(be << (64 - 8 * len)) >> (64 - 8 * len));
+          V[i] = x;
+          S[i] = slot_of(p, g, d.base, off);
+        }
+      }
+      RS[lane] = -1;
+      WAVE_SYNC();
+      // the run of each slot in this chunk: its first and one-past-last point
+      for (int i = lane; i < n; i += 64) {
+        const int k = S[i];
+        if (k < 0) continue;
+        if (i == 0 || S[i - 1] != k) RS[k] = i;
+        if (i == n - 1 || S[i + 1] != k) RE[k] = i + 1;
+      }
+      WAVE_SYNC();
+      if (lane < K && RS[lane] >= 0) {
+        for (int i = RS[lane]; i < RE[lane]; i++) bs_add<F>(st, V[i]);
+        has = true;
+      }
+      WAVE_SYNC();
+    }
+  }
+  if (lane < K && has) {
+    dense[s * K + lane] = bs_final<F>(st);
+    pres[s * K + lane] = 1;
+  }
+}
+
+hipError_t launch_seq_dense(const GridParams& p, int f, double* dense, uint8_t* pres, int64_t n_series, hipStream_t s,
+                            bool uniform) {
   if (n_series <= 0) return hipSuccess;
   const unsigned nb = (unsigned)((n_series + 255) / 256);
-#define SEQ_CASE(FF) \
-  case FF: hipLaunchKernelGGL(k_seq_dense<FF>, dim3(nb), dim3(256), 0, s, p, dense, pres, n_series); break;
+  const char* wenv = std::getenv("TSDBHIP_SEQ_WAVE");   // A/B: 0 = one series per lane
+  // uniform rows of 64+ points on average only (engine.cpp seq_dense_wanted): a row of mixed
+  // widths is decoded by one lane, and short rows leave the wave waiting on each row's descriptor
+  const bool wave = uniform && p.K <= 64 && !(wenv && wenv[0] == '0');
+  const unsigned nw = (unsigned)((n_series + SEQW_WAVES - 1) / SEQW_WAVES);
+#define SEQ_CASE(FF)                                                                                          \
+  case FF:                                                                                                    \
+    if (wave) hipLaunchKernelGGL(k_seq_wave<FF>, dim3(nw), dim3(64 * SEQW_WAVES), 0, s, p, dense, pres, n_series); \
+    else hipLaunchKernelGGL(k_seq_dense<FF>, dim3(nb), dim3(256), 0, s, p, dense, pres, n_series);           \
+    break;
   switch (f) {
     SEQ_CASE(F_SUM) SEQ_CASE(F_AVG) SEQ_CASE(F_COUNT) SEQ_CASE(F_SQUARESUM) SEQ_CASE(F_MIN) SEQ_CASE(F_MAX)
     SEQ_CASE(F_DEV) SEQ_CASE(F_FIRST) SEQ_CASE(F_LAST) SEQ_CASE(F_DIFF) SEQ_CASE(F_MULT)

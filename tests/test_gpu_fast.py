@@ -288,13 +288,15 @@ def test_short_kernel_mixed_row_counts(eng):
 @pytest.mark.parametrize("ds,iv,span", [("sum", 60000, 3 * 3600 - 1), ("avg", 420000, 3 * 3600 - 1),
                                         ("squareSum", 60000, 3599), ("avg", 86400000, 3 * 3600 - 1),
                                         ("sum", 1000, 1799), ("avg", 60000, 3 * 3600 - 1)])
-def test_float64_sequential_sums(eng, ds, iv, span):
-    """Full-mantissa doubles over three hour rows: the rows carry ROW_NOCERT (two of their values
+@pytest.mark.parametrize("seqwave", ["1", "0"])
+def test_float64_sequential_sums(eng, monkeypatch, seqwave, ds, iv, span):
+    """k_seq_wave (one wave a series, K <= 64) and k_seq_dense (TSDBHIP_SEQ_WAVE=0).  Full-mantissa doubles over three hour rows: the rows carry ROW_NOCERT (two of their values
     cannot add exactly).  Sum / avg downsampling then runs k_seq_dense (each bucket in Java's
     order, one pass, then the group-by step over the stored buckets); with it switched off the
     streaming kernels hand the tiles to k_grid, which sums them in order in one pass (slow_chunk).
     Both equal the general path bit for bit and the oracle -- buckets inside a row, across rows
     (7m), one a day and one a datapoint; squareSum keeps the certificate check at series end."""
+    monkeypatch.setenv("TSDBHIP_SEQ_WAVE", seqwave)
     b = synth.generate(70, T0, 3 * 3600, 1000, value_kind=4, n_groups=3, seed=17)
     for agg in ("sum", "max", "none"):
         q = abi.new_query(T0, T0 + span, agg, ds_function=abi.AGG[ds], ds_interval_ms=iv)
@@ -313,10 +315,12 @@ def test_float64_sequential_sums(eng, ds, iv, span):
         assert_groups_match(seq, O.run_query(b, q), agg, ctx=ctx)
 
 
-def test_float64_sequential_sums_mixed_rows(eng):
-    """k_seq_dense over a scan mixing full-mantissa doubles (ROW_NOCERT), vle integers and
+@pytest.mark.parametrize("seqwave", ["1", "0"])
+def test_float64_sequential_sums_mixed_rows(eng, monkeypatch, seqwave):
+    """Both sequential kernels (TSDBHIP_SEQ_WAVE).  k_seq_dense over a scan mixing full-mantissa doubles (ROW_NOCERT), vle integers and
     millisecond rows: the non-uniform rows are walked datapoint by datapoint (width from the
     qualifier, length from its flags); bit-exact against the general path and the oracle."""
+    monkeypatch.setenv("TSDBHIP_SEQ_WAVE", seqwave)
     from tests.test_gpu_calendar_tz import merge
     b = merge(synth.generate(20, T0, 7200, 1000, value_kind=4, n_groups=3, seed=5),
               synth.generate(20, T0, 7200, 1000, value_kind=1, n_groups=3, int_mod=70000, seed=6),
