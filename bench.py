@@ -6,9 +6,13 @@ Workload (BASELINE.json configs[1] = BASELINE.md config 2): 1,000,000 series x 1
 query sum:1m-avg grouped by a 64-valued tag.  A "step" is one full tsdbhip_run over the
 resident cells: decode -> 1m-avg downsample -> 64-group sum -> results on the host.
 
-Multi-GPU (torch.distributed.run, one process per GPU): weak scaling -- every rank holds
-its own 1M-series shard (disjoint series ids); per-(group, slot) partial states are
-all-gathered over RCCL and merged in rank order (tsdbhip_partials_* in the C ABI).
+Multi-GPU, two launch forms, both weak scaling by default (1M series per GPU):
+  * `python bench.py --gpus N` (no launcher): ONE process drives N distinct GPUs through one
+    multi-device context (tsdbhip_init_devices, the handle a TSD JVM would hold): series-sharded
+    shards, per-(group, slot) partial states gathered to devices[0] with RCCL send / recv over
+    xGMI and merged in device order.  Exits non-zero when fewer than N GPUs are visible.
+  * `torch.distributed.run --nproc-per-node N bench.py --gpus N`: one process per GPU, each
+    rank its own shard, partial states all-gathered over RCCL (tsdbhip_partials_* in the C ABI).
 
 Prints ONE JSON line on rank 0 (see README / DESIGN.md for the fields).
 """
@@ -47,6 +51,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH/WRITE_SIZE child passes")
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 (10M series) block in `extra`")
+    ap.add_argument("--transport", choices=["auto", "rccl", "copy"], default="auto",
+                    help="multi-device context (--gpus N, no launcher): RCCL send / recv or peer copies")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -214,11 +220,185 @@ def query(args):
     return q
 
 
+def visible_gpus() -> int:
+    import torch
+    return torch.cuda.device_count()   # (counts devices without initialising HIP)
+
+
+def md_engine(args, n):
+    """One multi-device context over GPUs 0..n-1, series shards.  RCCL unless --transport copy;
+    when the RCCL communicator cannot be built, peer copies (reported in the line)."""
+    from opentsdb_amd import engine as E
+    tr = {"auto": E.MD_AUTO, "rccl": E.MD_RCCL, "copy": E.MD_COPY}[args.transport]
+    note = None
+    try:
+        eng = E.Engine(devices=list(range(n)), transport=tr)
+    except E.EngineError as ex:
+        if args.transport != "auto":
+            raise
+        note = f"RCCL init failed ({ex}); peer copies used"
+        eng = E.Engine(devices=list(range(n)), transport=E.MD_COPY)
+    eng.shard_mode(E.SHARD_SERIES)
+    return eng, note
+
+
+def md_step_stats(eng, steps_stats):
+    per, ranks, moved = eng.md_stats()
+    steps_stats.append(([(t.fast_ms, t.decode_downsample_ms, t.datapoints, t.bytes) for t in per], moved))
+    return ranks
+
+
+def md_config3(args, n):
+    """BASELINE config 3 strong-scaled over the n GPUs of the context: 10M series @10 s, 1000
+    groups, int/float32 alternating -- the full 1-day store (8.64e10 dp, ~437 GB of cells) from
+    4 GPUs on, 12 h at 2 GPUs (what fits 288 GB per GPU with the int16 value copy).  Series
+    shards, so the 1000 x 1440 partial states cross devices every query (RCCL)."""
+    from opentsdb_amd import abi
+    from opentsdb_amd import engine as E
+    hours = 24 if n >= 4 else 12
+    eng, note = md_engine(args, n)
+    try:
+        t = time.perf_counter()
+        eng.synth(10_000_000, T0, hours * 360, 10000, 2, 1000, 30000, 0x5EED)
+        eng.sync()
+        synth_s = time.perf_counter() - t
+
+        def q(agg):
+            return abi.new_query(T0, T0 + hours * 3600 - 1, agg, ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+
+        out = {"workload": f"BASELINE config 3: 10M series x {hours} h @10 s (int/float32 alternating), 1000 groups, "
+                           f"1m-avg, strong-scaled over {n} GPUs (series shards, partial states over "
+                           f"{'RCCL' if eng.md_info()[1] == 1 else 'peer copies'})",
+               "hours": hours, "synth_s": synth_s, "transport_note": note}
+        steps = max(3, args.steps)
+        for name, qs in (("sum", [q("sum")]), ("p99", [q("p99")]),
+                         ("multi_avg_min_max_count_dev", [q(a) for a in ("avg", "min", "max", "count", "dev")])):
+            try:
+                for _ in range(2):
+                    eng.run_multi(qs) if len(qs) > 1 else eng.run(qs[0])
+            except E.EngineError as ex:   # e.g. more (series, slot) values per device than the select indexes
+                out[name] = {"skipped": str(ex)}
+                continue
+            eng.sync()
+            stats = []
+            t = time.perf_counter()
+            for _ in range(steps):
+                eng.run_multi(qs) if len(qs) > 1 else eng.run(qs[0])
+                md_step_stats(eng, stats)
+            eng.sync()
+            ms = (time.perf_counter() - t) * 1000 / steps
+            tm = eng.timing()
+            fast = [max(s[0][d][0] for s in stats) for d in range(n)]
+            out[name] = {"ms_per_step": ms, "value": len(qs) * tm.datapoints / (ms / 1000),
+                         "unit": "datapoints/s" + (f" (x{len(qs)} queries)" if len(qs) > 1 else ""),
+                         "exchange_ms": tm.exchange_ms, "xfer_bytes": stats[-1][1],
+                         "device_kernel_ms_max": [round(x, 4) for x in fast],
+                         "hbm_frac_step_per_gpu": tm.bytes / n / (ms / 1000) / 1e9 / BYTES_PEAK_GBS}
+        return out
+    finally:
+        eng.close()
+
+
+def main_md(args):
+    """--gpus N > 1 without a launcher: one process, one multi-device context over N GPUs."""
+    from opentsdb_amd import abi
+    n = args.gpus
+    have = visible_gpus()
+    if have < n:
+        print(f"bench.py: --gpus {n} but only {have} GPU(s) visible; refusing to report a {have}-GPU number "
+              f"as {n}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    eng, note = md_engine(args, n)
+    n_dev, transport, _, _ = eng.md_info()
+    total_series = args.series * n if args.scaling == "weak" else args.series
+    int_mod = 30000 if args.value_kind == 2 else 2000
+    t_gen = time.perf_counter()
+    eng.synth(total_series, T0, args.points, args.period_ms, args.value_kind, args.groups, int_mod, 0x5EED)
+    eng.sync()
+    t_gen = time.perf_counter() - t_gen
+    _, _, mode, per_series = eng.md_info()
+    index_ms = eng.timing().index_ms
+    q = query(args)
+    for _ in range(args.warmup):
+        eng.run(q)
+    eng.sync()
+    stats = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.run(q)
+        ranks = md_step_stats(eng, stats)
+    eng.sync()
+    elapsed = time.perf_counter() - t0
+    tm = eng.timing()
+    ms_per_step = elapsed * 1000.0 / args.steps
+    value = tm.datapoints / (ms_per_step / 1000.0)
+    # per device: its k_fast hipEvent time, its algorithmic bytes
+    dev_ms = [sum(s[0][d][0] for s in stats) / len(stats) for d in range(n)]
+    dev_bytes = [stats[-1][0][d][3] for d in range(n)]
+    dev_gbs = [b / (ms / 1000.0) / 1e9 if ms > 0 else 0.0 for b, ms in zip(dev_bytes, dev_ms)]
+    achieved = sum(dev_gbs) / n
+    eng.close()
+    extra = None if args.no_config3 else {"config3_strong": md_config3(args, n)}
+    line = {
+        "metric": "raw datapoints/sec through downsample+group-by; % of HBM BW, 1-8 GPUs",
+        "value": value,
+        "unit": "datapoints/s",
+        "n_gpus": n_dev,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": args.scaling,
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded splitmix64, generated in HBM with the MockBase cell encoding)",
+        "index_ms": index_ms,
+        "launch": "one process, one multi-device context (tsdbhip_init_devices) over GPUs 0..N-1",
+        "transport": {0: "peer copies", 1: "RCCL send/recv"}.get(transport, str(transport)),
+        "transport_note": note,
+        "rccl_ranks": ranks,
+        "exchange_ms": tm.exchange_ms,
+        "xfer_bytes_per_step": stats[-1][1],
+        "config": {
+            "workload": workload_label(args),
+            "series_per_gpu": [int(x) for x in per_series],
+            "datapoints_per_gpu": [int(stats[-1][0][d][2]) for d in range(n)],
+            "groups": args.groups,
+            "parallelism": f"series-sharded x{n} ({'series' if mode == 0 else 'groups'} shards)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": BYTES_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / BYTES_PEAK_GBS,
+            "frac_note": "per GPU (mean over the devices): each device's algorithmic bytes / its k_fast hipEvent "
+                         "time; frac_step: all bytes / (N x step time)",
+            "frac_step": tm.bytes / n / (ms_per_step / 1000.0) / 1e9 / BYTES_PEAK_GBS,
+            "per_gpu_frac": [g / BYTES_PEAK_GBS for g in dev_gbs],
+            "traffic": None,
+            "traffic_detail": "PMC passes are collected at N=1 only",
+            "kernel": "k_fast (streaming decode+downsample+tile group partials), per device",
+            "kernel_ms": dev_ms,
+            "bytes_per_launch": dev_bytes,
+        },
+        "cpu_baseline": None,
+        "synth_s": t_gen,
+        "extra": extra,
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.gpus not in (1, world):
+        print(f"bench.py: --gpus {args.gpus} under a launcher with WORLD_SIZE={world}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if world == 1 and args.gpus > 1 and not args.pmc_child:
+        return main_md(args)
     dist = None
     if world > 1:
         import torch

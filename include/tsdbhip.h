@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define TSDBHIP_ABI_VERSION 9
+#define TSDBHIP_ABI_VERSION 10
 
 /* ---- error codes: one per Java exception on the path --------------------- */
 enum {
@@ -327,15 +327,20 @@ int tsdbhip_assemble(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_
  *                      the results are concatenated in group order (NONE: in batch order) --
  *                      no device exchange, bit-identical to one GPU;
  *   TSDB_SHARD_SERIES  contiguous byte-balanced positions of the SpanGroup order (a group may
- *                      straddle devices): the partial states are gathered to devices[0] (RCCL
- *                      send / recv over xGMI, or device copies) and merged in device order
- *                      (tsdbhip_finalize); percentile / median group-by and TSDB_QF_ORDERED
- *                      gather the span contributions (tsdbhip_sel_select); raw group-by queries
- *                      need TSDB_SHARD_GROUPS (TSDB_E_NOT_IMPLEMENTED otherwise).
+ *                      straddle devices): decomposable aggregators gather their partial states
+ *                      to devices[0] (RCCL send / recv over xGMI, or peer copies) and merge them
+ *                      in device order (tsdbhip_finalize); percentile / median group-by and
+ *                      TSDB_QF_ORDERED route each group to its owner (the first device holding
+ *                      one of its spans): only the straddling groups' span rows move, every owner
+ *                      selects its groups in place, and the owners' G x K result rows go to
+ *                      devices[0]; raw group-by queries (no downsampler) run every whole group
+ *                      locally and each straddling group on its owner over a copy of all its
+ *                      spans (built once per load), so results are bit-identical to one GPU.
  * TSDB_SHARD_AUTO (default) picks GROUPS when the group-aligned split is within 10% of the byte
  * balance, else SERIES; tsdbhip_md_shard_mode sets the mode of the following loads.
- * transport: TSDB_MD_AUTO = RCCL (ncclCommInitAll) when the devices are distinct, device copies
- * when a device repeats (several shards on one GPU); TSDB_MD_RCCL / TSDB_MD_COPY force one.
+ * transport: TSDB_MD_AUTO = RCCL (ncclCommInitAll) when two or more devices are all distinct,
+ * device copies when a device repeats (several shards on one GPU); TSDB_MD_RCCL / TSDB_MD_COPY
+ * force one.
  * Entry points bound to one device's resident store (load_shard, synth_shard, load_cells,
  * load_rollup, the histogram path, batch downloads, the partials / sel exchange, rollup
  * generation, debug_rows) return TSDB_E_NOT_IMPLEMENTED on such a context; the expression
@@ -349,6 +354,10 @@ int tsdbhip_md_shard_mode(tsdbhip_ctx* ctx, int mode);
 /* n_devices, transport in use, shard mode of the resident batch (TSDB_SHARD_AUTO before a load)
  * and, when shard_series is not NULL, the resident series of every device ([n_devices]). */
 int tsdbhip_md_info(tsdbhip_ctx* ctx, int* n_devices, int* transport, int* mode, int64_t* shard_series);
+/* The last tsdbhip_run / tsdbhip_run_multi on a multi-device context: per_device[d] = device d's
+ * own timing record, n_devices entries or NULL, *rccl_ranks = ranks of the RCCL communicator
+ * (ncclCommCount; 0 with device copies), *xfer_bytes = bytes moved between devices. */
+int tsdbhip_md_stats(tsdbhip_ctx* ctx, tsdbhip_timing* per_device, int* rccl_ranks, double* xfer_bytes);
 /* ---- rollup generation --------------------------------
  * RollupInterval (src/rollup/RollupInterval.java:62-240): `interval` e.g. "1h", `row_span`
  * e.g. "1d"; validateAndCompile's checks and arithmetic, IllegalArgumentException ->

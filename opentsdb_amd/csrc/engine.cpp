@@ -2985,7 +2985,7 @@ int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   const int64_t S = c->n_series, K = P.K;
   if (S * K > 0x7FFFFFFFLL) return fail(TSDB_E_NOT_IMPLEMENTED, "percentile group-by over more than 2^31 (series, slot) values");
   const char* fenv = std::getenv("TSDBHIP_SEL_FUSED");
-  if (P.f != F_SEL && !q->rate && K >= 1 && K <= 64 && !(fenv && fenv[0] == '0')) {
+  if (P.f != F_SEL && !P.emit_only && !q->rate && K >= 1 && K <= 64 && !(fenv && fenv[0] == '0')) {
     const std::vector<int64_t> gsp = seg_ptr(local_counts(c, G));
     HIP_OK(c->sel_gsp.ensure((G + 1) * 8));
     HIP_OK(c->sel_vals.ensure(std::max<int64_t>(1, S * K) * 8));
@@ -3013,7 +3013,10 @@ int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   }
   HIP_OK(c->pre_dense.ensure(std::max<int64_t>(1, S * K) * 8));
   HIP_OK(c->pre_pres.ensure(std::max<int64_t>(1, S * K)));
-  if (P.f == F_SEL) {
+  if (P.emit_only) {
+    // the buckets are already in pre_dense / pre_pres: a rollup table's avg / count downsampling
+    // (ro_stage: Σsum / Σcount per bucket, Downsampler.java:165-221)
+  } else if (P.f == F_SEL) {
     int rc = run_device(c, q, P, G, false);   // k_pct -> pre_dense / pre_pres (no k_emit)
     if (rc) return rc;
   } else {
@@ -3872,8 +3875,8 @@ int ro_stage(tsdbhip_ctx* c, const tsdbhip_query* q, const tsdbhip_query& qr, Pl
   const bool combine = c->ro_counts && (q->ds_function == TSDB_AGG_AVG || q->ds_function == TSDB_AGG_COUNT);
   int rc = ro_scan(c, P, combine);
   if (rc || !combine) return rc;
-  if (P.gsel || P.ordered)
-    return fail(TSDB_E_NOT_IMPLEMENTED, "avg / count rollup downsampling with a percentile group-by or the ordered flag");
+  // (a percentile / median group-by or TSDB_QF_ORDERED then takes these buckets as its span
+  // values: sel_values skips its own downsampling pass under P.emit_only)
   tsdbhip_query q1 = qr;
   q1.ds_function = TSDB_AGG_SUM;
   q1.aggregator = TSDB_AGG_NONE;
@@ -4101,7 +4104,6 @@ extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_resul
 // rate, aggregator and flags may differ.
 extern "C" int tsdbhip_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_result** outs) {
   if (c && c->md) return tsdb::md_run_multi(c, qs, n, outs);
-  if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_run_multi over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !qs || !outs || n < 1) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad argument");
   for (int i = 0; i < n; i++) outs[i] = nullptr;
   for (int i = 1; i < n; i++) {
@@ -4113,6 +4115,18 @@ extern "C" int tsdbhip_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n,
   }
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_OK(hipSetDevice(c->device));
+  if (c->ro_active) {
+    // a rollup table: each query reads its own aggregate's cells (RollupQuery per sub-query,
+    // TsdbQuery.java:1665-1700), so the queries run one after the other
+    for (int i = 0; i < n; i++) {
+      const int rc = run_rollup(c, &qs[i], &outs[i]);
+      if (rc) {
+        for (int j = 0; j < n; j++) { result_free(outs[j]); outs[j] = nullptr; }
+        return rc;
+      }
+    }
+    return 0;
+  }
   const int64_t G = c->n_groups;
   tsdbhip_query q0 = qs[0];
   q0.rate = 0;
@@ -4139,7 +4153,10 @@ extern "C" int tsdbhip_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n,
         if (P.raw) rc = fail(TSDB_E_ILLEGAL_ARGUMENT, "bad query");
         else if (P.anchored) { rc = run_anchored(c, &qs[i], P, &outs[i]); if (!rc) continue; }
         else if (P.gsel || P.ordered) rc = P.gsel ? run_sel_group(c, &qs[i], P, G) : run_ordered(c, &qs[i], P, G);
-        else rc = run_device(c, &qs[i], P, P.none ? c->n_series : G, true);
+        else {
+          P.seq_dense = seq_dense_wanted(c, P);   // as tsdbhip_run: sums that cannot add in any order
+          rc = run_device(c, &qs[i], P, P.none ? c->n_series : G, true);
+        }
         if (!rc) rc = collect(c, &qs[i], P, P.none ? c->n_series : G, true, &outs[i]);
       }
       if (rc) {
@@ -4382,7 +4399,129 @@ int plan_sel(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, Pl
   return 0;
 }
 
+// Stages 1-2 on this device: the local spans' contributions stay in c->sel_vals ([span][K] rows,
+// groups in SpanGroup order, ungrouped spans last; room for `extra_rows` more rows), the emit
+// flags in c->sel_uni; `a` = the groups' active flags on the host.  Caller holds c->mu.
+int sel_values_stage(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, int64_t extra_rows, Plan& P,
+                     std::vector<uint32_t>& a) {
+  HIP_OK(hipSetDevice(c->device));
+  if (c->ro_active) { const int r = ro_check(q); if (r) return r; }
+  const tsdbhip_query qr = ro_query(c, q);
+  int rc = plan_sel(c, &qr, G, P);
+  if (rc) return rc;
+  if (c->ro_active) {
+    rc = ro_stage(c, q, qr, P);
+    if (rc) return rc;
+  }
+  if (extra_rows > 0) HIP_OK(c->sel_vals.ensure((c->n_series + extra_rows) * P.K * 8));
+  HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
+  rc = sel_values(c, &qr, P, G);
+  if (rc) return rc;
+  a.assign(std::max<int64_t>(1, G), 0);
+  if (G) HIP_OK(hipMemcpyAsync(a.data(), c->gact.p, G * 4, hipMemcpyDeviceToHost, c->stream));
+  int32_t err = 0;
+  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  if (err) return fail(err, "error raised by the device path");
+  ro_activity(c, P, G, a);
+  return 0;
+}
+
+// Stages 3-4 on this device over rows already on it (`vals`, counts[g] rows per group) and the
+// emit flags in c->sel_uni: the order statistic (or, TSDB_QF_ORDERED, the fold in row order)
+// of every (group, slot) -> c->out_val / c->out_flag [G][K].  Caller holds c->mu.
+int sel_select_stage(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, const double* vals,
+                     const std::vector<int64_t>& cnt, Plan& P) {
+  HIP_OK(hipSetDevice(c->device));
+  if (c->ro_active) { const int r = ro_check(q); if (r) return r; }
+  const tsdbhip_query qr0 = ro_query(c, q);
+  int rc = plan_sel(c, &qr0, G, P);
+  if (rc) return rc;
+  const int64_t K = P.K;
+  HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
+  if (P.ordered) {   // the owner folds each (group, slot) over the ranks' spans in rank (= span) order
+    const std::vector<int64_t> gsp = seg_ptr(cnt);
+    HIP_OK(c->sel_gsp.ensure((G + 1) * 8));
+    HIP_OK(c->out_val.ensure(std::max<int64_t>(1, G * K) * 8));
+    HIP_OK(c->out_flag.ensure(std::max<int64_t>(1, G * K)));
+    HIP_OK(hipMemcpyAsync(c->sel_gsp.p, gsp.data(), (G + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    OrdParams op{};
+    op.vals = vals;
+    op.uni = c->sel_uni.as<uint8_t>();
+    op.group_series_ptr = c->sel_gsp.as<int64_t>();
+    op.G = G;
+    op.K = K;
+    op.ga = P.ga;
+    op.out_val = c->out_val.as<double>();
+    op.out_flag = c->out_flag.as<uint8_t>();
+    op.err = c->err.as<int32_t>();
+    HIP_OK(launch_ordered(op, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));   // `gsp` leaves scope
+  } else {
+    rc = sel_select(c, P, G, const_cast<double*>(vals), cnt, c->sel_uni.as<uint8_t>());
+    if (rc) return rc;
+  }
+  int32_t err = 0;
+  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  if (err) return fail(err, "error raised by the device path");
+  return 0;
+}
+
 }  // namespace
+
+namespace tsdb {
+// multi.cpp, owner-routed percentile / ordered exchange: this device's span contributions left in
+// place (*vals, on this device) with room for extra_rows more rows after the grouped ones;
+// emit flags [G * K] and group activity [G] to the host.
+int md_sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, int64_t extra_rows, double** vals,
+                  int64_t* K, uint8_t* uni, uint32_t* act) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  Plan P;
+  std::vector<uint32_t> a;
+  int rc = sel_values_stage(c, q, G, extra_rows, P, a);
+  if (rc) return rc;
+  if (G * P.K) HIP_OK(hipMemcpy(uni, c->sel_uni.p, G * P.K, hipMemcpyDeviceToHost));
+  std::copy(a.begin(), a.begin() + G, act);
+  *vals = c->sel_vals.as<double>();
+  *K = P.K;
+  return 0;
+}
+
+// ... and the owner's selection over rows on its device: out_val / out_flag [G][K] stay on it.
+int md_sel_select(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, const double* vals, const int64_t* counts,
+                  const uint8_t* uni, double** out_val, uint8_t** out_flag) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  Plan P;
+  int rc = plan_sel(c, q, G, P);
+  if (rc) return rc;
+  HIP_OK(c->sel_uni.ensure(std::max<int64_t>(1, G * P.K)));
+  if (G * P.K) HIP_OK(hipMemcpyAsync(c->sel_uni.p, uni, G * P.K, hipMemcpyHostToDevice, c->stream));
+  rc = sel_select_stage(c, q, G, vals, std::vector<int64_t>(counts, counts + G), P);
+  if (rc) return rc;
+  *out_val = c->out_val.as<double>();
+  *out_flag = c->out_flag.as<uint8_t>();
+  return 0;
+}
+
+// local series per group id < G of the resident batch (multi.cpp: which groups straddle devices)
+std::vector<int64_t> ctx_group_counts(tsdbhip_ctx* c, int64_t G) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  return local_counts(c, G);
+}
+
+// resident positions [p0, p1) of group g (the resident order is group-sorted)
+void ctx_group_range(tsdbhip_ctx* c, int64_t g, int64_t* p0, int64_t* p1) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  *p0 = *p1 = 0;
+  if (g < 0 || g >= c->n_groups) return;   // (the local sentinel n_groups marks ungrouped series)
+  const auto lo = std::lower_bound(c->h_group.begin(), c->h_group.begin() + c->n_series, (int32_t)g);
+  const auto hi = std::upper_bound(lo, c->h_group.begin() + c->n_series, (int32_t)g);
+  *p0 = lo - c->h_group.begin();
+  *p1 = hi - c->h_group.begin();
+}
+}  // namespace tsdb
 
 extern "C" int tsdbhip_sel_layout(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, int64_t* counts,
                                   int64_t* n_slots) {
@@ -4404,31 +4543,16 @@ extern "C" int tsdbhip_sel_run_values(tsdbhip_ctx* c, const tsdbhip_query* q, in
   MD_REFUSE(c, "tsdbhip_sel_run_values");
   if (!c || !q || !vals || !uni || !act) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_OK(hipSetDevice(c->device));
-  if (c->ro_active) { const int r = ro_check(q); if (r) return r; }
-  const tsdbhip_query qr = ro_query(c, q);
   Plan P;
-  int rc = plan_sel(c, &qr, n_groups_global, P);
+  std::vector<uint32_t> a;
+  int rc = sel_values_stage(c, q, n_groups_global, 0, P, a);
   if (rc) return rc;
-  if (c->ro_active) {
-    rc = ro_stage(c, q, qr, P);
-    if (rc) return rc;
-  }
   const int64_t G = n_groups_global, K = P.K;
-  HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
-  rc = sel_values(c, &qr, P, G);
-  if (rc) return rc;
   int64_t n = 0;   // the grouped spans (ungrouped ones, and a rollup batch's count series, last)
   for (int64_t x : local_counts(c, G)) n += x * K;
   if (n) HIP_OK(hipMemcpyAsync(vals, c->sel_vals.p, n * 8, hipMemcpyDefault, c->stream));
   if (G * K) HIP_OK(hipMemcpyAsync(uni, c->sel_uni.p, G * K, hipMemcpyDefault, c->stream));
-  std::vector<uint32_t> a(std::max<int64_t>(1, G));
-  if (G) HIP_OK(hipMemcpyAsync(a.data(), c->gact.p, G * 4, hipMemcpyDeviceToHost, c->stream));
-  int32_t err = 0;
-  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
-  if (err) return fail(err, "error raised by the device path");
-  ro_activity(c, P, G, a);
   if (G) HIP_OK(hipMemcpy(act, a.data(), G * 4, hipMemcpyDefault));
   return 0;
 }
@@ -4457,36 +4581,13 @@ extern "C" int tsdbhip_sel_select(tsdbhip_ctx* c, const tsdbhip_query* q, int64_
   HIP_OK(c->sel_uni.ensure(std::max<int64_t>(1, G * K)));
   if (n) HIP_OK(hipMemcpyAsync(c->sel_vals.p, vals, n * 8, hipMemcpyDefault, c->stream));
   if (G * K) HIP_OK(hipMemcpyAsync(c->sel_uni.p, uni, G * K, hipMemcpyDefault, c->stream));
-  HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
-  if (P.ordered) {   // the owner folds each (group, slot) over the ranks' spans in rank (= span) order
-    const std::vector<int64_t> gsp = seg_ptr(cnt);
-    HIP_OK(c->sel_gsp.ensure((G + 1) * 8));
-    HIP_OK(c->out_val.ensure(std::max<int64_t>(1, G * K) * 8));
-    HIP_OK(c->out_flag.ensure(std::max<int64_t>(1, G * K)));
-    HIP_OK(hipMemcpyAsync(c->sel_gsp.p, gsp.data(), (G + 1) * 8, hipMemcpyHostToDevice, c->stream));
-    OrdParams op{};
-    op.vals = c->sel_vals.as<double>();
-    op.uni = c->sel_uni.as<uint8_t>();
-    op.group_series_ptr = c->sel_gsp.as<int64_t>();
-    op.G = G;
-    op.K = K;
-    op.ga = P.ga;
-    op.out_val = c->out_val.as<double>();
-    op.out_flag = c->out_flag.as<uint8_t>();
-    op.err = c->err.as<int32_t>();
-    HIP_OK(launch_ordered(op, c->stream));
-  } else {
-    rc = sel_select(c, P, G, c->sel_vals.as<double>(), cnt, c->sel_uni.as<uint8_t>());
-  }
+  rc = sel_select_stage(c, q, G, c->sel_vals.as<double>(), cnt, P);
   if (rc) return rc;
   if (G * K) {
     HIP_OK(hipMemcpyAsync(out_val, c->out_val.p, G * K * 8, hipMemcpyDefault, c->stream));
     HIP_OK(hipMemcpyAsync(out_flag, c->out_flag.p, G * K, hipMemcpyDefault, c->stream));
   }
-  int32_t err = 0;
-  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
-  if (err) return fail(err, "error raised by the device path");
   return 0;
 }
 

@@ -7,17 +7,25 @@
 // A multi-device context holds one ordinary engine context (stream, scratch, resident shard)
 // per device and a merge context on devices[0].  Loads split the batch by bytes:
 //   GROUPS  whole SpanGroups per device -- every query runs locally, results concatenate;
-//   SERIES  positions of the SpanGroup order -- the devices' partial states (or, for percentile /
-//           median group-by and TSDB_QF_ORDERED, their span contributions) are gathered to
-//           devices[0] over RCCL (send / recv, one rank per GPU, ncclCommInitAll) and merged in
-//           device order, which continues SpanGroup order across devices.
-// Every device runs on its own host thread; the gather is the only device-to-device traffic.
+//   SERIES  contiguous positions of the SpanGroup order, so a group may straddle devices:
+//           - decomposable aggregators: the devices' partial states are gathered to devices[0]
+//             and merged in device order, which continues SpanGroup order across devices;
+//           - percentile / median group-by and TSDB_QF_ORDERED: group g is owned by the first
+//             device holding one of its spans; only the straddling groups' span rows move (to
+//             the owner, appended in device order), every owner selects its groups in place, and
+//             the owners' dense (group, slot) rows go to devices[0];
+//           - raw group-by (no downsampler): each straddling group is assembled once per load on
+//             its owner (a side context holding the whole SpanGroup), so every group is evaluated
+//             over all its spans in SpanGroup order on one device.
+// Device-to-device bytes move over RCCL (grouped ncclSend / ncclRecv, one rank per GPU,
+// ncclCommInitAll) or peer copies.  Every device runs on its own persistent host thread.
 #include <hip/hip_runtime.h>
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <functional>
 #include <mutex>
 #include <numeric>
@@ -49,6 +57,7 @@ struct Rccl {
   std::string why;
   decltype(&ncclCommInitAll) init_all = nullptr;
   decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclCommCount) count = nullptr;
   decltype(&ncclGroupStart) group_start = nullptr;
   decltype(&ncclGroupEnd) group_end = nullptr;
   decltype(&ncclSend) send = nullptr;
@@ -69,12 +78,13 @@ Rccl& rccl() {
     }
     r.init_all = reinterpret_cast<decltype(r.init_all)>(dlsym(h, "ncclCommInitAll"));
     r.destroy = reinterpret_cast<decltype(r.destroy)>(dlsym(h, "ncclCommDestroy"));
+    r.count = reinterpret_cast<decltype(r.count)>(dlsym(h, "ncclCommCount"));
     r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(h, "ncclGroupStart"));
     r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(h, "ncclGroupEnd"));
     r.send = reinterpret_cast<decltype(r.send)>(dlsym(h, "ncclSend"));
     r.recv = reinterpret_cast<decltype(r.recv)>(dlsym(h, "ncclRecv"));
     r.err_str = reinterpret_cast<decltype(r.err_str)>(dlsym(h, "ncclGetErrorString"));
-    r.ok = r.init_all && r.destroy && r.group_start && r.group_end && r.send && r.recv && r.err_str;
+    r.ok = r.init_all && r.destroy && r.count && r.group_start && r.group_end && r.send && r.recv && r.err_str;
     if (!r.ok) r.why = "librccl.so.1 lacks the send / recv API";
   });
   return r;
@@ -108,21 +118,90 @@ struct Buf {
   }
 };
 
+// One persistent host thread per device slot but the first (slot 0's work runs on the calling
+// thread): a query's per-device calls start without a thread creation each (8 x ~30 us).
+class Workers {
+ public:
+  explicit Workers(int n) : slots_(n) {
+    for (int i = 1; i < n; i++) th_.emplace_back([this, i] { loop(i); });
+  }
+  ~Workers() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  // fn(i) for every i of idx at once; returns when all have finished
+  void run(const std::vector<int>& idx, const std::function<void(int)>& fn) {
+    // slot 0 (no worker of its own) runs here, or else the last slot of the set
+    const int inline_i = std::find(idx.begin(), idx.end(), 0) != idx.end() ? 0 : idx.back();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (int i : idx) {
+        if (i == inline_i) continue;
+        slots_[i].job = [&fn, i] { fn(i); };
+        slots_[i].has = true;
+        pending_++;
+      }
+    }
+    cv_.notify_all();
+    fn(inline_i);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [this] { return pending_ == 0; });
+  }
+
+ private:
+  struct Slot {
+    std::function<void()> job;
+    bool has = false;
+  };
+  void loop(int i) {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || slots_[i].has; });
+      if (!slots_[i].has) return;
+      std::function<void()> job = std::move(slots_[i].job);
+      lk.unlock();
+      job();
+      lk.lock();
+      slots_[i].has = false;
+      if (--pending_ == 0) done_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  std::vector<Slot> slots_;
+  std::vector<std::thread> th_;
+  int pending_ = 0;
+  bool stop_ = false;
+};
+
 struct MultiDev {
   std::vector<int> devices;
   std::vector<tsdbhip_ctx*> subs;       // one engine context per device (slot d = RCCL rank d)
   tsdbhip_ctx* root = nullptr;          // merge context on devices[0]
   int transport = TSDB_MD_COPY;
   std::vector<ncclComm_t> comms;
+  Workers* pool = nullptr;
   int mode_req = TSDB_SHARD_AUTO;       // shard mode of the next load
   int mode = TSDB_SHARD_AUTO;           // shard mode of the resident batch (AUTO: nothing loaded)
   int64_t G = 0;                        // groups of the whole batch
   std::vector<char> live;               // the device holds series
   std::vector<std::vector<int64_t>> series;   // load: batch index of each resident virtual position
   std::vector<int64_t> pos0;            // synth: first batch position of each shard
+  bool rollup = false;                  // the resident batch is a rollup table
+  // raw group-by over SERIES shards: per owner device a side context holding the whole straddling
+  // SpanGroups it owns, built at the first raw query after a load
+  bool side_valid = false;
+  std::vector<tsdbhip_ctx*> side;
+  std::vector<char> straddle;           // [G] the group's spans sit on several devices
   std::vector<Buf> xb;                  // per device: exchange source
   Buf gb, ov, of;                       // devices[0]: gathered exchange, merged values / flags
   tsdbhip_timing timing{};
+  std::vector<tsdbhip_timing> dev_timing;   // per device, last call
+  double xfer_bytes = 0;                // device-to-device bytes of the last call
 };
 
 MultiDev* md_of(tsdbhip_ctx* c) { return static_cast<MultiDev*>(ctx_md(c)); }
@@ -131,24 +210,27 @@ double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// fn(d) for every live device (all devices when `all`), each on its own host thread; the error
-// of the first failing device in device order is the call's.
-int each_device(MultiDev* m, const std::function<int(int)>& fn, bool all = false) {
-  const int n = (int)m->devices.size();
-  std::vector<int> run;
-  for (int d = 0; d < n; d++) if (all || m->live[d]) run.push_back(d);
+// fn(d) for every d of `run`, each on its device's worker; the error of the first failing device
+// in device order is the call's.
+int each_of(MultiDev* m, const std::vector<int>& run, const std::function<int(int)>& fn) {
+  if (run.empty()) return 0;
   if (run.size() == 1) return fn(run[0]);
+  const int n = (int)m->devices.size();
   std::vector<int> rc(n, 0);
   std::vector<std::string> msg(n);
-  std::vector<std::thread> th;
-  for (int d : run)
-    th.emplace_back([&, d] {
-      rc[d] = fn(d);
-      if (rc[d]) msg[d] = tsdbhip_last_error();
-    });
-  for (auto& t : th) t.join();
+  m->pool->run(run, [&](int d) {
+    rc[d] = fn(d);
+    if (rc[d]) msg[d] = tsdbhip_last_error();
+  });
   for (int d : run) if (rc[d]) return set_error(rc[d], msg[d]);
   return 0;
+}
+
+// ... for every live device (all devices when `all`)
+int each_device(MultiDev* m, const std::function<int(int)>& fn, bool all = false) {
+  std::vector<int> run;
+  for (int d = 0; d < (int)m->devices.size(); d++) if (all || m->live[d]) run.push_back(d);
+  return each_of(m, run, fn);
 }
 
 std::vector<int> live_devices(const MultiDev* m) {
@@ -183,22 +265,42 @@ bool groups_balanced(const std::vector<double>& gw, const std::vector<int64_t>& 
   return (int64_t)gw.size() >= n && worst <= 1.10 * total / n;
 }
 
-// Copies bytes[i] from src[i] (on devices[ds[i]]) to dst on devices[0], concatenated in the
-// order of ds: RCCL send / recv to rank 0, or peer copies on the merge stream.
-int gather(MultiDev* m, const std::vector<int>& ds, const std::vector<const void*>& src,
-           const std::vector<size_t>& bytes, void* dst) {
-  hipStream_t rs = ctx_stream(m->root);
-  std::vector<size_t> off(ds.size() + 1, 0);
-  for (size_t i = 0; i < ds.size(); i++) off[i + 1] = off[i] + bytes[i];
+// One device-to-device copy: bytes from slot `src` (device memory there) to slot `dst`.
+struct Xfer {
+  int src;
+  const void* sp;
+  int dst;
+  void* dp;
+  size_t n;
+};
+
+// Moves every piece: RCCL -- one grouped round of ncclSend / ncclRecv between the ranks, pieces
+// within a device as copies on its stream; COPY -- peer copies on the destination's stream.
+// Sources must be complete; returns when every destination holds its bytes.
+int transfer(MultiDev* m, const std::vector<Xfer>& xs) {
+  const int n = (int)m->devices.size();
+  std::vector<char> used(n, 0);
+  auto st = [&](int d) { return ctx_stream(m->subs[d]); };
+  for (const Xfer& x : xs) {
+    if (!x.n) continue;
+    used[x.src] = used[x.dst] = 1;
+    m->xfer_bytes += x.src != x.dst ? (double)x.n : 0.0;
+  }
   if (m->transport == TSDB_MD_RCCL) {
+    for (const Xfer& x : xs) {
+      if (!x.n || x.src != x.dst) continue;
+      MOK(hipSetDevice(m->devices[x.dst]));
+      MOK(hipMemcpyAsync(x.dp, x.sp, x.n, hipMemcpyDeviceToDevice, st(x.dst)));
+    }
     Rccl& R = rccl();
     ncclResult_t e = R.group_start();
     if (e != ncclSuccess) return rccl_fail(e, "ncclGroupStart");
-    for (size_t i = 0; i < ds.size(); i++) {
-      if (!bytes[i]) continue;
-      const int d = ds[i];
-      e = R.send(src[i], bytes[i], ncclUint8, 0, m->comms[d], d == 0 ? rs : ctx_stream(m->subs[d]));
-      if (e == ncclSuccess) e = R.recv(static_cast<char*>(dst) + off[i], bytes[i], ncclUint8, d, m->comms[0], rs);
+    for (const Xfer& x : xs) {
+      if (!x.n || x.src == x.dst) continue;
+      // the same list drives both sides, so the pieces of every (src, dst) pair are posted in
+      // the same order at the sender and at the receiver
+      e = R.send(x.sp, x.n, ncclUint8, x.dst, m->comms[x.src], st(x.src));
+      if (e == ncclSuccess) e = R.recv(x.dp, x.n, ncclUint8, x.src, m->comms[x.dst], st(x.dst));
       if (e != ncclSuccess) {
         (void)R.group_end();
         return rccl_fail(e, "ncclSend / ncclRecv");
@@ -206,19 +308,18 @@ int gather(MultiDev* m, const std::vector<int>& ds, const std::vector<const void
     }
     e = R.group_end();
     if (e != ncclSuccess) return rccl_fail(e, "ncclGroupEnd");
-    for (size_t i = 0; i < ds.size(); i++) {
-      if (!bytes[i] || ds[i] == 0) continue;
-      MOK(hipSetDevice(m->devices[ds[i]]));
-      MOK(hipStreamSynchronize(ctx_stream(m->subs[ds[i]])));
-    }
   } else {
-    MOK(hipSetDevice(m->devices[0]));
-    for (size_t i = 0; i < ds.size(); i++)
-      if (bytes[i])
-        MOK(hipMemcpyPeerAsync(static_cast<char*>(dst) + off[i], m->devices[0], src[i], m->devices[ds[i]], bytes[i], rs));
+    for (const Xfer& x : xs) {
+      if (!x.n) continue;
+      MOK(hipSetDevice(m->devices[x.dst]));
+      MOK(hipMemcpyPeerAsync(x.dp, m->devices[x.dst], x.sp, m->devices[x.src], x.n, st(x.dst)));
+    }
   }
-  MOK(hipSetDevice(m->devices[0]));
-  MOK(hipStreamSynchronize(rs));
+  for (int d = 0; d < n; d++) {
+    if (!used[d]) continue;
+    MOK(hipSetDevice(m->devices[d]));
+    MOK(hipStreamSynchronize(st(d)));
+  }
   return 0;
 }
 
@@ -227,17 +328,24 @@ int64_t batch_index(const MultiDev* m, int d, int64_t v) {
 }
 
 // One result from the devices' results: groups in group id order (whole SpanGroups per device),
-// or for NONE every span in batch order, renumbered (TsdbQuery.java:940-961).
-int merge(MultiDev* m, const std::vector<tsdbhip_result*>& parts, bool none, tsdbhip_result** out) {
-  struct E { int64_t key; int d; int64_t i; };
+// or for NONE every span in batch order, renumbered (TsdbQuery.java:940-961).  parts[i] belongs
+// to device slot i % n_devices; for i < n_skip the groups flagged in `skip` are left out (their
+// answer comes from a later part).
+int merge(MultiDev* m, const std::vector<tsdbhip_result*>& parts, bool none, tsdbhip_result** out,
+          const std::vector<char>* skip = nullptr, size_t n_skip = 0) {
+  struct E { int64_t key; int p; int64_t i; };
+  const int nd = (int)m->devices.size();
   std::vector<E> e;
   int64_t npts = 0;
-  for (int d = 0; d < (int)parts.size(); d++) {
-    const tsdbhip_result* r = parts[d];
+  for (int p = 0; p < (int)parts.size(); p++) {
+    const tsdbhip_result* r = parts[p];
     if (!r) continue;
-    for (int64_t i = 0; i < r->n_groups; i++)
-      e.push_back({none ? batch_index(m, d, r->group_id[i]) : (int64_t)r->group_id[i], d, i});
-    npts += r->group_ptr[r->n_groups];
+    for (int64_t i = 0; i < r->n_groups; i++) {
+      const int64_t key = none ? batch_index(m, p % nd, r->group_id[i]) : (int64_t)r->group_id[i];
+      if (skip && (size_t)p < n_skip && key >= 0 && key < (int64_t)skip->size() && (*skip)[key]) continue;
+      e.push_back({key, p, i});
+      npts += r->group_ptr[i + 1] - r->group_ptr[i];
+    }
   }
   std::sort(e.begin(), e.end(), [](const E& a, const E& b) { return a.key < b.key; });
   tsdbhip_result* r = new_result((int64_t)e.size(), npts);
@@ -249,7 +357,7 @@ int merge(MultiDev* m, const std::vector<tsdbhip_result*>& parts, bool none, tsd
   auto* isi = const_cast<uint8_t*>(r->is_int);
   int64_t o = 0;
   for (size_t k = 0; k < e.size(); k++) {
-    const tsdbhip_result* p = parts[e[k].d];
+    const tsdbhip_result* p = parts[e[k].p];
     const int64_t a = p->group_ptr[e[k].i], n = p->group_ptr[e[k].i + 1] - a;
     gptr[k] = o;
     gid[k] = none ? (int32_t)k : (int32_t)e[k].key;
@@ -286,8 +394,8 @@ std::string per_span_calendar() {
          "load with tsdbhip_md_shard_mode(ctx, TSDB_SHARD_GROUPS)";
 }
 
-// Decomposable group-by over straddling groups: partial states per device -> gather -> merge in
-// device order (tsdbhip_finalize on the merge context).
+// Decomposable group-by over straddling groups: partial states per device -> gather to devices[0]
+// -> merge in device order (tsdbhip_finalize on the merge context).
 int run_partials_xchg(MultiDev* m, const tsdbhip_query* q, tsdbhip_result** out) {
   const std::vector<int> ds = live_devices(m);
   tsdbhip_partials_layout L{};
@@ -299,79 +407,276 @@ int run_partials_xchg(MultiDev* m, const tsdbhip_query* q, tsdbhip_result** out)
     if (rc) return rc;
     if (Ld.bytes != L.bytes || Ld.n_slots != L.n_slots) return set_error(TSDB_E_NOT_IMPLEMENTED, per_span_calendar());
   }
+  rc = m->gb.ensure((size_t)L.bytes * ds.size());
+  if (rc) return rc;
   rc = each_device(m, [&](int d) {
     const int r = m->xb[d].ensure((size_t)L.bytes);
     return r ? r : tsdbhip_run_partials(m->subs[d], q, m->G, m->xb[d].p);
   });
   if (rc) return rc;
   const double t0 = now_ms();
-  std::vector<const void*> src;
-  std::vector<size_t> bytes;
-  for (int d : ds) { src.push_back(m->xb[d].p); bytes.push_back((size_t)L.bytes); }
-  rc = m->gb.ensure((size_t)L.bytes * ds.size());
-  if (!rc) rc = gather(m, ds, src, bytes, m->gb.p);
+  std::vector<Xfer> xs;
+  for (size_t i = 0; i < ds.size(); i++)
+    xs.push_back({ds[i], m->xb[ds[i]].p, 0, static_cast<char*>(m->gb.p) + i * (size_t)L.bytes, (size_t)L.bytes});
+  rc = transfer(m, xs);
   if (!rc) rc = tsdbhip_finalize(m->root, q, m->G, m->gb.p, (int)ds.size(), out);
   m->timing.exchange_ms = now_ms() - t0;
   return rc;
 }
 
-// Percentile / median group-by and TSDB_QF_ORDERED over straddling groups: every span's
-// contributions are gathered to devices[0] in device (= SpanGroup) order, which selects / folds
-// every (group, slot) there (tsdbhip_sel_select).
+// Percentile / median group-by and TSDB_QF_ORDERED over straddling groups (the
+// values of a non-decomposable aggregate go to the owning rank; Aggregators.java:657-708).
+// Group g's owner is the first device holding one of its spans.  SERIES shards are contiguous in
+// SpanGroup order, so on every device the groups it does not own precede the ones it owns, and
+// only its last owned group can have spans on later devices: those rows are appended to the
+// owner's rows in device order (= SpanGroup order), and each owner selects its groups over rows
+// that never left it.  Traffic: the straddling groups' rows plus G * K * 9 B of results, instead
+// of every span's contributions to devices[0].
 int run_sel_xchg(MultiDev* m, const tsdbhip_query* q, tsdbhip_result** out) {
   const std::vector<int> ds = live_devices(m);
+  const int n = (int)m->devices.size();
   const int64_t G = m->G;
   int64_t K = 0;
-  std::vector<int64_t> none_counts(std::max<int64_t>(1, G));
-  int rc = tsdbhip_sel_layout(m->root, q, G, none_counts.data(), &K);
-  if (rc) return rc;
-  const int n = (int)m->devices.size();
-  std::vector<std::vector<int64_t>> counts(n);
-  std::vector<int64_t> n_series(n, 0);
+  int rc = 0;
+  {
+    std::vector<int64_t> none_counts(std::max<int64_t>(1, G));
+    rc = tsdbhip_sel_layout(m->root, q, G, none_counts.data(), &K);   // the merge context's refusals
+    if (rc) return rc;
+  }
+  std::vector<std::vector<int64_t>> cnt(n);
   for (int d : ds) {
-    counts[d].assign(std::max<int64_t>(1, G), 0);
+    cnt[d].assign(std::max<int64_t>(1, G), 0);
     int64_t Kd = 0;
-    rc = tsdbhip_sel_layout(m->subs[d], q, G, counts[d].data(), &Kd);
+    rc = tsdbhip_sel_layout(m->subs[d], q, G, cnt[d].data(), &Kd);
     if (rc) return rc;
     if (Kd != K) return set_error(TSDB_E_NOT_IMPLEMENTED, per_span_calendar());
-    n_series[d] = ctx_n_series(m->subs[d]);
   }
+  // owners (a group without spans: the owner of the group before it, so owned ranges are contiguous)
+  std::vector<int> owner(std::max<int64_t>(1, G), ds[0]);
+  std::vector<int64_t> total(std::max<int64_t>(1, G), 0);
+  for (int64_t g = 0, prev = ds[0]; g < G; g++) {
+    int o = -1;
+    for (int d : ds) {
+      if (cnt[d][g] > 0 && o < 0) o = d;
+      total[g] += cnt[d][g];
+    }
+    owner[g] = o < 0 ? (int)prev : o;
+    prev = owner[g];
+  }
+  // per device: rows of the groups it does not own (a prefix), its rows, its last owned group
+  std::vector<int64_t> skip(n, 0), rows(n, 0), extra(n, 0), last(n, -1), ga(n, -1), gb(n, -1);
+  for (int d : ds) {
+    bool owned_seen = false;
+    for (int64_t g = 0; g < G; g++) {
+      if (owner[g] == d) {
+        if (ga[d] < 0) ga[d] = g;
+        gb[d] = g + 1;
+      }
+      if (!cnt[d][g]) continue;
+      rows[d] += cnt[d][g];
+      if (owner[g] != d) {
+        if (owned_seen) return set_error(TSDB_E_HIP, "multi-device exchange: shard not contiguous in SpanGroup order");
+        skip[d] += cnt[d][g];
+        continue;
+      }
+      if (last[d] >= 0 && total[last[d]] != cnt[d][last[d]])
+        return set_error(TSDB_E_HIP, "multi-device exchange: a straddling group inside a shard");
+      owned_seen = true;
+      last[d] = g;
+    }
+    if (last[d] >= 0) extra[d] = total[last[d]] - cnt[d][last[d]];
+  }
+  std::vector<double*> vals(n, nullptr);
   std::vector<std::vector<uint8_t>> uni(n);
   std::vector<std::vector<uint32_t>> act(n);
   for (int d : ds) {
     uni[d].assign(std::max<int64_t>(1, G * K), 0);
     act[d].assign(std::max<int64_t>(1, G), 0);
   }
-  rc = each_device(m, [&](int d) {
-    const int r = m->xb[d].ensure((size_t)(n_series[d] * K * 8));
-    return r ? r : tsdbhip_sel_run_values(m->subs[d], q, G, m->xb[d].p, uni[d].data(), act[d].data());
+  rc = each_of(m, ds, [&](int d) {
+    int64_t Kd = 0;
+    return md_sel_values(m->subs[d], q, G, extra[d], &vals[d], &Kd, uni[d].data(), act[d].data());
   });
   if (rc) return rc;
   const double t0 = now_ms();
-  std::vector<const void*> src;
-  std::vector<size_t> bytes;
-  std::vector<int64_t> total(std::max<int64_t>(1, G), 0);
-  size_t all = 0;
-  for (int d : ds) {
-    int64_t nv = 0;
-    for (int64_t g = 0; g < G; g++) { nv += counts[d][g]; total[g] += counts[d][g]; }
-    src.push_back(m->xb[d].p);
-    bytes.push_back((size_t)(nv * K * 8));   // the spans of groups (ungrouped spans come last)
-    all += bytes.back();
+  // 1. the straddling groups' rows to their owners, appended in device order
+  std::vector<Xfer> xs;
+  for (int o : ds) {
+    if (last[o] < 0 || !extra[o]) continue;
+    const int64_t g = last[o];
+    int64_t at = rows[o];
+    for (int d : ds) {
+      if (d <= o || !cnt[d][g]) continue;
+      int64_t pre = 0;   // rows before g on d
+      for (int64_t h = 0; h < g; h++) pre += cnt[d][h];
+      xs.push_back({d, vals[d] + pre * K, o, vals[o] + at * K, (size_t)(cnt[d][g] * K * 8)});
+      at += cnt[d][g];
+    }
   }
+  rc = transfer(m, xs);
+  if (rc) return rc;
+  // 2. every owner selects its groups (the rows of groups it does not own are skipped)
   std::vector<uint8_t> u(std::max<int64_t>(1, G * K), 0);
   std::vector<uint32_t> a(std::max<int64_t>(1, G), 0);
   for (int d : ds) {
     for (int64_t i = 0; i < G * K; i++) u[i] |= uni[d][i];
     for (int64_t g = 0; g < G; g++) a[g] |= act[d][g];
   }
-  rc = m->gb.ensure(all);
-  if (!rc) rc = gather(m, ds, src, bytes, m->gb.p);
+  std::vector<int> owners;
+  std::vector<std::vector<int64_t>> oc(n);
+  for (int d : ds) {
+    if (ga[d] < 0) continue;
+    owners.push_back(d);
+    oc[d].assign(std::max<int64_t>(1, G), 0);
+    for (int64_t g = ga[d]; g < gb[d]; g++) oc[d][g] = total[g];
+  }
+  std::vector<double*> ov(n, nullptr);
+  std::vector<uint8_t*> of(n, nullptr);
+  rc = each_of(m, owners, [&](int d) {
+    return md_sel_select(m->subs[d], q, G, vals[d] + skip[d] * K, oc[d].data(), u.data(), &ov[d], &of[d]);
+  });
+  // 3. the owners' dense rows to devices[0]
   if (!rc) rc = m->ov.ensure((size_t)(G * K * 8));
   if (!rc) rc = m->of.ensure((size_t)(G * K));
-  if (!rc) rc = tsdbhip_sel_select(m->root, q, G, m->gb.p, total.data(), u.data(), m->ov.p, m->of.p);
+  if (rc) return rc;
+  std::vector<Xfer> ys;
+  for (int d : owners) {
+    const int64_t r0 = ga[d] * K, nr = (gb[d] - ga[d]) * K;
+    ys.push_back({d, ov[d] + r0, 0, static_cast<double*>(m->ov.p) + r0, (size_t)(nr * 8)});
+    ys.push_back({d, of[d] + r0, 0, static_cast<uint8_t*>(m->of.p) + r0, (size_t)nr});
+  }
+  rc = transfer(m, ys);
   if (!rc) rc = tsdbhip_assemble(m->root, q, G, m->ov.p, m->of.p, a.data(), out);
   m->timing.exchange_ms = now_ms() - t0;
+  return rc;
+}
+
+void drop_side(MultiDev* m) {
+  for (tsdbhip_ctx*& s : m->side) {
+    if (s) tsdbhip_destroy(s);
+    s = nullptr;
+  }
+  m->side_valid = false;
+  m->straddle.clear();
+}
+
+// Host batch assembled from resident ranges of the devices (tsdbhip_batch_download_range).
+struct HostPieces {
+  std::vector<int64_t> srp{0};
+  std::vector<uint32_t> base;
+  std::vector<uint64_t> qo{0}, vo{0};
+  std::vector<uint8_t> q, v;
+  std::vector<int32_t> gid;
+  int add(tsdbhip_ctx* c, int64_t s0, int64_t s1) {
+    if (s1 <= s0) return 0;
+    int64_t nr = 0;
+    uint64_t qb = 0, vb = 0;
+    int rc = tsdbhip_batch_range_sizes(c, s0, s1, &nr, &qb, &vb);
+    if (rc) return rc;
+    std::vector<int64_t> p(s1 - s0 + 1);
+    std::vector<uint32_t> b(std::max<int64_t>(1, nr));
+    std::vector<uint64_t> po(nr + 1), pv(nr + 1);
+    std::vector<uint8_t> pq(std::max<uint64_t>(1, qb)), pw(std::max<uint64_t>(1, vb));
+    std::vector<int32_t> g(s1 - s0);
+    rc = tsdbhip_batch_download_range(c, s0, s1, p.data(), b.data(), po.data(), pv.data(), pq.data(), pw.data(), g.data());
+    if (rc) return rc;
+    const int64_t r0 = (int64_t)base.size();
+    const uint64_t q0 = q.size(), v0 = v.size();
+    for (int64_t i = 1; i <= s1 - s0; i++) srp.push_back(r0 + p[i]);
+    base.insert(base.end(), b.begin(), b.begin() + nr);
+    for (int64_t r = 1; r <= nr; r++) {
+      qo.push_back(q0 + po[r]);
+      vo.push_back(v0 + pv[r]);
+    }
+    q.insert(q.end(), pq.begin(), pq.begin() + qb);
+    v.insert(v.end(), pw.begin(), pw.begin() + vb);
+    gid.insert(gid.end(), g.begin(), g.end());
+    return 0;
+  }
+  tsdbhip_batch batch() {
+    if (q.empty()) q.push_back(0);
+    if (v.empty()) v.push_back(0);
+    tsdbhip_batch b{};
+    b.n_series = (int64_t)gid.size();
+    b.n_rows = (int64_t)base.size();
+    b.series_row_ptr = srp.data();
+    b.row_base_time = base.empty() ? nullptr : base.data();
+    b.row_qual_off = qo.data();
+    b.row_val_off = vo.data();
+    b.qual = q.data();
+    b.val = v.data();
+    b.group_id = gid.data();
+    return b;
+  }
+};
+
+// The side contexts of the raw path: every straddling group, whole, on its owner (the first
+// device holding one of its spans), its spans in device order = SpanGroup order.
+int build_side(MultiDev* m) {
+  if (m->side_valid) return 0;
+  drop_side(m);
+  const int n = (int)m->devices.size();
+  const int64_t G = m->G;
+  const std::vector<int> ds = live_devices(m);
+  std::vector<std::vector<int64_t>> cnt(n);
+  for (int d : ds) cnt[d] = ctx_group_counts(m->subs[d], G);
+  m->straddle.assign(std::max<int64_t>(1, G), 0);
+  std::vector<std::vector<int64_t>> own(n);
+  for (int64_t g = 0; g < G; g++) {
+    int first = -1, held = 0;
+    for (int d : ds)
+      if (cnt[d][g] > 0) {
+        if (first < 0) first = d;
+        held++;
+      }
+    if (held >= 2) {
+      m->straddle[g] = 1;
+      own[first].push_back(g);
+    }
+  }
+  m->side.assign(n, nullptr);
+  for (int o = 0; o < n; o++) {
+    if (own[o].empty()) continue;
+    HostPieces h;
+    for (int64_t g : own[o])
+      for (int d : ds) {
+        if (!cnt[d][g]) continue;
+        int64_t p0 = 0, p1 = 0;
+        ctx_group_range(m->subs[d], g, &p0, &p1);
+        const int rc = h.add(m->subs[d], p0, p1);
+        if (rc) return rc;
+      }
+    int rc = tsdbhip_init(m->devices[o], &m->side[o]);
+    if (rc) return rc;
+    const tsdbhip_batch b = h.batch();
+    rc = tsdbhip_load(m->side[o], &b);
+    if (rc) return rc;
+  }
+  m->side_valid = true;
+  return 0;
+}
+
+// Raw group-by (no downsampler) over SERIES shards: every device answers its whole groups, the
+// side contexts answer the straddling ones (AggregationIterator over all of a group's spans,
+// :514-797, on one device, so float operands keep SpanGroup order).
+int run_raw_series(MultiDev* m, const tsdbhip_query* q, tsdbhip_result** out) {
+  int rc = build_side(m);
+  if (rc) return rc;
+  const int n = (int)m->devices.size();
+  std::vector<tsdbhip_result*> parts(2 * n, nullptr);
+  std::vector<int> run = live_devices(m);
+  for (int d = 0; d < n; d++)
+    if (m->side[d] && !m->live[d]) run.push_back(d);
+  std::sort(run.begin(), run.end());
+  rc = each_of(m, run, [&](int d) {
+    int r = m->live[d] ? tsdbhip_run(m->subs[d], q, &parts[d]) : 0;
+    if (!r && m->side[d]) r = tsdbhip_run(m->side[d], q, &parts[n + d]);
+    return r;
+  });
+  const double t0 = now_ms();
+  if (!rc) rc = merge(m, parts, false, out, &m->straddle, (size_t)n);
+  m->timing.exchange_ms = now_ms() - t0;
+  free_all(parts);
   return rc;
 }
 
@@ -387,9 +692,7 @@ int run_one(MultiDev* m, const tsdbhip_query* q, tsdbhip_result** out) {
   int rc = query_kind(m->subs[first_live(m)], q, &kind);
   if (rc) return rc;
   if (m->mode == TSDB_SHARD_GROUPS || kind == QK_NONE) return run_local(m, q, kind == QK_NONE, out);
-  if (kind == QK_RAW)
-    return set_error(TSDB_E_NOT_IMPLEMENTED, "a raw (no downsampling) group-by over a series-sharded multi-device context: "
-                                             "load with tsdbhip_md_shard_mode(ctx, TSDB_SHARD_GROUPS)");
+  if (kind == QK_RAW) return m->rollup ? run_local(m, q, false, out) : run_raw_series(m, q, out);
   return kind == QK_PARTIALS ? run_partials_xchg(m, q, out) : run_sel_xchg(m, q, out);
 }
 
@@ -397,9 +700,11 @@ int run_one(MultiDev* m, const tsdbhip_query* q, tsdbhip_result** out) {
 void device_timing(MultiDev* m, double wall_ms, bool fused) {
   tsdbhip_timing t{};
   int64_t fq = -1;
+  m->dev_timing.assign(m->devices.size(), tsdbhip_timing{});
   for (int d : live_devices(m)) {
     tsdbhip_timing s{};
     if (tsdbhip_last_timing(m->subs[d], &s)) continue;
+    m->dev_timing[d] = s;
     t.decode_downsample_ms = std::max(t.decode_downsample_ms, s.decode_downsample_ms);
     t.group_reduce_ms = std::max(t.group_reduce_ms, s.group_reduce_ms);
     t.fast_ms = std::max(t.fast_ms, s.fast_ms);
@@ -415,6 +720,12 @@ void device_timing(MultiDev* m, double wall_ms, bool fused) {
   t.total_ms = wall_ms;
   t.exchange_ms = m->timing.exchange_ms;
   m->timing = t;
+}
+
+// After a load: devices without series give up what they held before.
+void drop_idle(MultiDev* m) {
+  for (int d = 0; d < (int)m->devices.size(); d++)
+    if (!m->live[d]) ctx_drop_batch(m->subs[d]);
 }
 
 }  // namespace
@@ -453,6 +764,8 @@ std::vector<std::vector<int64_t>> shard_series(MultiDev* m, const int32_t* gid, 
   m->mode = TSDB_SHARD_AUTO;
   m->series.clear();
   m->pos0.clear();
+  m->rollup = false;
+  drop_side(m);
   m->live.assign(n, 0);
   bool any = false;
   for (int d = 0; d < n; d++) { m->live[d] = !cand[d].empty(); any = any || m->live[d]; }
@@ -480,6 +793,7 @@ int md_load(tsdbhip_ctx* c, const tsdbhip_batch* b) {
   int64_t G = 0;
   const std::vector<std::vector<int64_t>> cand = shard_series(m, b->group_id, w, mode, G);
   ctx_drop_batch(m->root);   // (a rollup load before leaves rollup state on the merge context)
+  drop_idle(m);
   const int rc = each_device(m, [&](int d) { return load_series(m->subs[d], b, cand[d]); });
   if (rc) {
     m->live.assign(m->devices.size(), 0);
@@ -570,6 +884,7 @@ int md_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* rb) {
     u.rb.cqual = cnt ? u.cq.data() : nullptr;
     u.rb.cval = cnt ? u.cv.data() : nullptr;
   }
+  drop_idle(m);
   int rc = each_device(m, [&](int d) { return tsdbhip_load_rollup(m->subs[d], &sub[d].rb); });
   if (!rc) {   // the merge context: an empty batch of the same rollup table
     Sub e;
@@ -595,6 +910,7 @@ int md_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* rb) {
   m->mode = mode;
   m->G = G;
   m->series = cand;
+  m->rollup = true;
   return 0;
 }
 
@@ -619,9 +935,12 @@ int md_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp) {
   for (int d = 0; d <= n; d++) p[d] = mode == TSDB_SHARD_GROUPS ? goff[gb[d]] : SG * d / n;
   m->mode = TSDB_SHARD_AUTO;
   m->series.clear();
+  m->rollup = false;
+  drop_side(m);
   m->live.assign(n, 0);
   for (int d = 0; d < n; d++) m->live[d] = p[d + 1] > p[d];
   ctx_drop_batch(m->root);
+  drop_idle(m);
   const int rc = each_device(m, [&](int d) { return tsdbhip_synth_shard(m->subs[d], sp, p[d], p[d + 1]); });
   if (rc) {
     m->live.assign(n, 0);
@@ -639,6 +958,7 @@ int md_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
   if (!q || !out) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(ctx_mutex(c));
   *out = nullptr;
+  m->xfer_bytes = 0;
   const double t0 = now_ms();
   const int rc = run_one(m, q, out);
   if (!rc) device_timing(m, now_ms() - t0, false);
@@ -652,6 +972,7 @@ int md_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_result*
   for (int i = 0; i < n; i++) outs[i] = nullptr;
   const double t0 = now_ms();
   m->timing.exchange_ms = 0;
+  m->xfer_bytes = 0;
   int rc = 0;
   if (m->mode == TSDB_SHARD_GROUPS) {
     // whole SpanGroups per device: each device runs its own fused pass over the queries
@@ -667,7 +988,12 @@ int md_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_result*
     m->timing.exchange_ms = now_ms() - t1;
     for (auto& p : parts) free_all(p);
   } else {
-    for (int i = 0; i < n && !rc; i++) rc = run_one(m, &qs[i], &outs[i]);
+    double xm = 0;
+    for (int i = 0; i < n && !rc; i++) {
+      rc = run_one(m, &qs[i], &outs[i]);
+      xm += m->timing.exchange_ms;
+    }
+    m->timing.exchange_ms = xm;
   }
   if (rc) {
     for (int i = 0; i < n; i++) {
@@ -713,6 +1039,9 @@ int md_batch_sizes(tsdbhip_ctx* c, int64_t* n_series, int64_t* n_rows, uint64_t*
 void md_destroy(void* p) {
   auto* m = static_cast<MultiDev*>(p);
   if (!m) return;
+  delete m->pool;
+  m->pool = nullptr;
+  drop_side(m);
   for (ncclComm_t cm : m->comms) if (cm) (void)rccl().destroy(cm);
   for (Buf& b : m->xb) b.release();
   m->gb.release();
@@ -736,12 +1065,13 @@ extern "C" int tsdbhip_init_devices(const int* devices, int n_devices, int trans
   MOK(hipGetDeviceCount(&count));
   for (int d = 0; d < n_devices; d++)
     if (devices[d] < 0 || devices[d] >= count)
-      return set_error(TSDB_E_HIP, "no such HIP device " + std::to_string(devices[d]));
+      return set_error(TSDB_E_HIP, "no such HIP device " + std::to_string(devices[d]) + " (" +
+                                       std::to_string(count) + " visible)");
   const bool distinct = std::set<int>(devices, devices + n_devices).size() == (size_t)n_devices;
   if (transport == TSDB_MD_RCCL && !distinct)
     return set_error(TSDB_E_ILLEGAL_ARGUMENT, "RCCL needs distinct devices (one rank per GPU)");
   int tr = transport;
-  if (tr == TSDB_MD_AUTO) tr = distinct && rccl().ok ? TSDB_MD_RCCL : TSDB_MD_COPY;
+  if (tr == TSDB_MD_AUTO) tr = distinct && n_devices > 1 && rccl().ok ? TSDB_MD_RCCL : TSDB_MD_COPY;
   if (tr == TSDB_MD_RCCL && !rccl().ok) return set_error(TSDB_E_HIP, "RCCL unavailable: " + rccl().why);
   tsdbhip_ctx* c = nullptr;
   int rc = tsdbhip_init(devices[0], &c);
@@ -751,6 +1081,7 @@ extern "C" int tsdbhip_init_devices(const int* devices, int n_devices, int trans
   m->devices.assign(devices, devices + n_devices);
   m->transport = tr;
   m->live.assign(n_devices, 0);
+  m->pool = new Workers(n_devices);
   for (int d = 0; d < n_devices && !rc; d++) {
     tsdbhip_ctx* s = nullptr;
     rc = tsdbhip_init(devices[d], &s);
@@ -762,6 +1093,16 @@ extern "C" int tsdbhip_init_devices(const int* devices, int n_devices, int trans
   }
   if (!rc) rc = tsdbhip_init(devices[0], &m->root);
   m->gb.dev = m->ov.dev = m->of.dev = devices[0];
+  // direct peer access between distinct devices (xGMI): peer copies and RCCL's P2P path use it
+  if (!rc && distinct)
+    for (int a = 0; a < n_devices; a++)
+      for (int b = 0; b < n_devices; b++) {
+        int can = 0;
+        if (a == b || hipDeviceCanAccessPeer(&can, devices[a], devices[b]) != hipSuccess || !can) continue;
+        (void)hipSetDevice(devices[a]);
+        const hipError_t e = hipDeviceEnablePeerAccess(devices[b], 0);
+        if (e != hipSuccess) (void)hipGetLastError();   // (already enabled by someone else: fine)
+      }
   if (!rc && tr == TSDB_MD_RCCL) {
     m->comms.assign(n_devices, nullptr);
     const ncclResult_t e = rccl().init_all(m->comms.data(), n_devices, devices);
@@ -808,5 +1149,25 @@ extern "C" int tsdbhip_md_info(tsdbhip_ctx* c, int* n_devices, int* transport, i
       }
     }
   }
+  return 0;
+}
+
+extern "C" int tsdbhip_md_stats(tsdbhip_ctx* c, tsdbhip_timing* per_device, int* rccl_ranks, double* xfer_bytes) {
+  if (!c || !md_of(c)) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "not a multi-device context (tsdbhip_init_devices)");
+  MultiDev* m = md_of(c);
+  std::lock_guard<std::mutex> lk(ctx_mutex(c));
+  if (per_device)
+    for (size_t d = 0; d < m->devices.size(); d++)
+      per_device[d] = d < m->dev_timing.size() ? m->dev_timing[d] : tsdbhip_timing{};
+  if (rccl_ranks) {
+    *rccl_ranks = 0;
+    if (!m->comms.empty() && m->comms[0]) {
+      int k = 0;
+      const ncclResult_t e = rccl().count(m->comms[0], &k);
+      if (e != ncclSuccess) return rccl_fail(e, "ncclCommCount");
+      *rccl_ranks = k;
+    }
+  }
+  if (xfer_bytes) *xfer_bytes = m->xfer_bytes;
   return 0;
 }

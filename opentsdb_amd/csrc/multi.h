@@ -20,6 +20,14 @@ int set_error(int code, const std::string& msg);
 tsdbhip_result* new_result(int64_t n_groups, int64_t n_points);
 void ctx_drop_batch(tsdbhip_ctx* c);               // release the resident batch (and rollup state)
 int64_t ctx_n_series(tsdbhip_ctx* c);              // resident series, a rollup batch's count series too
+std::vector<int64_t> ctx_group_counts(tsdbhip_ctx* c, int64_t G);   // resident series of each group id < G
+void ctx_group_range(tsdbhip_ctx* c, int64_t g, int64_t* p0, int64_t* p1);   // resident positions of group g
+// owner-routed percentile / ordered exchange: span contributions left on the device (room for
+// extra_rows more rows), then the owner's selection over rows on its device
+int md_sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, int64_t extra_rows, double** vals,
+                  int64_t* K, uint8_t* uni, uint32_t* act);
+int md_sel_select(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, const double* vals, const int64_t* counts,
+                  const uint8_t* uni, double** out_val, uint8_t** out_flag);
 // multi.cpp
 int md_load(tsdbhip_ctx* c, const tsdbhip_batch* b);
 int md_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp);

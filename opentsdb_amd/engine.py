@@ -32,7 +32,7 @@ EXPORTS = [
     "tsdbhip_load_rollup", "tsdbhip_load_cells", "tsdbhip_load_histograms", "tsdbhip_hist_run",
     "tsdbhip_hist_run_range", "tsdbhip_hist_result_free", "tsdbhip_expr_map", "tsdbhip_expr_zip", "tsdbhip_expr_topn",
     "tsdbhip_batch_range_sizes", "tsdbhip_batch_download_range", "tsdbhip_expr_sync", "tsdbhip_init_devices",
-    "tsdbhip_md_shard_mode", "tsdbhip_md_info", "tsdbhip_host_alloc", "tsdbhip_host_free",
+    "tsdbhip_md_shard_mode", "tsdbhip_md_info", "tsdbhip_host_alloc", "tsdbhip_host_free", "tsdbhip_md_stats",
 ]
 
 SHARD_AUTO, SHARD_SERIES, SHARD_GROUPS, SHARD_SPANS = -1, 0, 1, 2   # tsdbhip.h TSDB_SHARD_*
@@ -98,6 +98,7 @@ def lib():
         L.tsdbhip_init_devices.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(vp)]
         L.tsdbhip_md_shard_mode.argtypes = [vp, C.c_int]
         L.tsdbhip_md_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_void_p]
+        L.tsdbhip_md_stats.argtypes = [vp, C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double)]
         L.tsdbhip_destroy.argtypes = [vp]
         L.tsdbhip_host_alloc.argtypes = [C.c_uint64, C.POINTER(vp)]
         L.tsdbhip_host_free.argtypes = [vp]
@@ -253,6 +254,15 @@ class Engine:
         per = np.zeros(nd.value, np.int64)
         _check(lib().tsdbhip_md_info(self.ctx, None, None, None, per.ctypes.data))
         return nd.value, tr.value, mode.value, per
+
+    def md_stats(self):
+        """tsdbhip_md_stats -> (per-device Timing list, RCCL communicator ranks, device-to-device
+        bytes) of the last run on a multi-device context."""
+        nd = self.md_info()[0]
+        per = (abi.Timing * nd)()
+        ranks, xb = C.c_int(), C.c_double()
+        _check(lib().tsdbhip_md_stats(self.ctx, C.cast(per, C.c_void_p), C.byref(ranks), C.byref(xb)))
+        return list(per), ranks.value, xb.value
 
     def close(self):
         if self.ctx:

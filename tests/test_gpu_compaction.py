@@ -195,6 +195,39 @@ def test_random_rows_match_oracle(eng, seed, fix):
                 assert_groups_match(g, w, agg, ctx=f"{agg} {ds} {start}")
 
 
+@pytest.mark.parametrize("seed", [5, 6])
+def test_pinned_scan_buffers(eng, seed):
+    """The scan assembled in page-locked host memory (tsdbhip_host_alloc, engine.pinned_copy --
+    the path whose use-after-free crashed in round 3): the compacted rows equal those of the
+    same scan from pageable memory, repeated loads included, and queries agree with the oracle."""
+    import gc
+
+    from opentsdb_amd.engine import pinned_copy
+    rng = np.random.default_rng(seed)
+    series, groups = [], []
+    for s in range(30):
+        series.append([(B + 3600 * h, random_row(rng, int(rng.integers(1, 50)), dup_p=0.05)) for h in range(2)])
+        groups.append(s % 3)
+    cb = abi.HostCellBatch.from_rows(series, groups, True)
+    eng.load_cells(cb)
+    want = rows_of(eng.download())
+    ref = eng.download()
+    for _ in range(3):
+        pc = abi.HostCellBatch(*(None if x is None else pinned_copy(x) for x in (cb.series_row_ptr, cb.row_base_time, cb.row_col_ptr,
+                                                           cb.col_qual_off, cb.col_val_off, cb.qual, cb.val,
+                                                           cb.group_id, cb.col_timestamp)), True)
+        eng.load_cells(pc)
+        del pc
+        gc.collect()   # the pinned blocks may go now: the engine holds its own device copy
+        assert rows_of(eng.download()) == want
+    q = abi.new_query(B, B + 7199, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+    try:
+        got = eng.run(q)
+    except EngineError:   # a compaction error of some row, raised by the covering query
+        return
+    assert_groups_match(got, O.run_query(ref, q), "sum", ctx="pinned")
+
+
 def test_shuffled_single_cells_at_scale(eng):
     """3,000 series x 2 rows of 3,600 one-datapoint cells in shuffled order: the compacted rows
     are the sorted cells plus a meta byte, and the queries equal those over tsdbhip_load."""

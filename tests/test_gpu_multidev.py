@@ -6,9 +6,11 @@ series-sharded stores (TSDB_SHARD_SERIES, partial states gathered to devices[0] 
 device order) bit for bit for order statistics / ordered folds / NONE, and within the oracle's
 tolerance for the float reductions whose association changes at the shard boundaries.
 
-The GPU box has one MI355X: N devices are emulated by repeating device 0 (the device-copy
-transport); a one-rank RCCL communicator (ncclCommInitAll over [0], send / recv to itself)
-exercises the RCCL gather.  The round-end 8-GPU run covers distinct devices through bench.py."""
+The development GPU box has one MI355X: N devices are emulated by repeating device 0 (the
+device-copy transport), and a one-rank RCCL communicator (ncclCommInitAll over [0]) exercises the
+RCCL code path without a peer.  `test_distinct_devices` runs every query kind over 2..N distinct
+GPUs with both transports when the machine has them (it skips on a one-GPU box); bench.py's
+`--gpus N` drives the same context over N distinct GPUs."""
 from __future__ import annotations
 
 import numpy as np
@@ -126,27 +128,60 @@ def test_group_shards_are_bit_identical(batch, single, world):
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_series_shards(batch, single, world):
     """Groups straddle devices: partial states gathered and merged in device order (oracle
-    tolerance for float reductions), span contributions gathered for order statistics and
-    ordered folds (bit for bit), NONE per span (bit for bit), raw group-by refused."""
+    tolerance for float reductions); order statistics and ordered folds routed to each group's
+    owner (bit for bit, only the straddling groups' rows move); NONE per span (bit for bit); raw
+    group-by with the straddling groups evaluated whole on their owners (bit for bit)."""
     _, want = single
     e = md_engine([0] * world, E.SHARD_SERIES, batch)
     try:
         assert e.md_info()[2] == E.SHARD_SERIES
         for n, q, kind in QUERIES:
-            if kind == "raw":
-                with pytest.raises(E.EngineError) as ei:
-                    e.run(q)
-                assert ei.value.code == abi.TSDB_E_NOT_IMPLEMENTED
-            elif kind == "partials":
+            if kind == "partials":
                 got = e.run(q)
                 assert_groups_match(got, O.run_query(batch, q), q_agg(q), ctx=f"series x{world} {n}")
                 assert_groups_match(got, want[n], q_agg(q), ctx=f"series x{world} {n} vs one GPU")
             else:
                 bit_same(e.run(q), want[n], f"series x{world} {n}")
+            if kind == "sel":   # owner routing: far fewer bytes than every span's rows
+                _, _, moved = e.md_stats()
+                k = 60
+                assert 0 < moved < batch.n_series * k * 8 / 2, (n, moved)
         e.run(QUERIES[0][1])
         assert e.timing().exchange_ms > 0   # the gather + merge of the partial states
+        per, ranks, _ = e.md_stats()
+        assert len(per) == world and ranks == 0 and sum(t.datapoints for t in per) == e.timing().datapoints
     finally:
         e.close()
+
+
+def device_count():
+    import torch
+    return torch.cuda.device_count()
+
+
+@pytest.mark.parametrize("transport", [E.MD_RCCL, E.MD_COPY])
+def test_distinct_devices(batch, single, transport):
+    """Every query kind over 2..N DISTINCT GPUs (series shards: partial gather, owner-routed
+    selection, ordered folds, raw side contexts, NONE), RCCL send / recv and peer copies, against
+    the one-GPU results.  Needs a multi-GPU machine."""
+    n = device_count()
+    if n < 2:
+        pytest.skip("one visible GPU: distinct-device exchange needs two or more")
+    _, want = single
+    for world in sorted({2, min(n, 8)}):
+        e = md_engine(list(range(world)), E.SHARD_SERIES, batch, transport=transport)
+        try:
+            assert e.md_info()[1] == transport
+            for name, q, kind in QUERIES:
+                got = e.run(q)
+                if kind == "partials":
+                    assert_groups_match(got, want[name], q_agg(q), ctx=f"distinct x{world} {name}")
+                else:
+                    bit_same(got, want[name], f"distinct x{world} {name}")
+            if transport == E.MD_RCCL:
+                assert e.md_stats()[1] == world
+        finally:
+            e.close()
 
 
 def q_agg(q):
@@ -162,8 +197,9 @@ def test_rccl_gather_one_rank(batch, single):
         for n, q, kind in QUERIES:
             if kind == "partials":
                 assert_groups_match(e.run(q), O.run_query(batch, q), q_agg(q), ctx=f"rccl {n}")
-            elif kind == "sel":
+            elif kind in ("sel", "raw", "none"):
                 bit_same(e.run(q), want[n], f"rccl {n}")
+        assert e.md_stats()[1] == 1   # a one-rank communicator
     finally:
         e.close()
 

@@ -123,9 +123,43 @@ def test_rollup_mode_guards(eng):
     eng.load_rollup(rb)
     with pytest.raises(EngineError):
         eng.run(abi.new_query(B, B + 3600, "sum"))   # a rollup query needs a downsampler
-    with pytest.raises(EngineError) as e:
-        eng.run_multi([_q(), _q()])
-    assert e.value.code == abi.TSDB_E_NOT_IMPLEMENTED
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_percentile_and_ordered_over_rollup_avg(eng, seed):
+    """A percentile / median group-by and TSDB_QF_ORDERED over rollup avg / count downsampling
+    (Sigma sum / Sigma count buckets, Downsampler.java:165-221, under any AggregationIterator):
+    the combined buckets are the span values of the selection / ordered fold -- bit for bit."""
+    rng = np.random.default_rng(seed)
+    rb = random_table(rng, 40, 4, 2, floats=seed == 5)
+    eng.load_rollup(rb)
+    end = B + 86400 + 7200
+    for ds in ("10m-avg", "1h-avg", "1h-count", "30m-avg-nan", "20m-count-zero"):
+        for agg, flags in (("p99", 0), ("median", 0), ("p50", 0), ("ep90r7", 0), ("sum", abi.QF_ORDERED),
+                           ("avg", abi.QF_ORDERED), ("dev", abi.QF_ORDERED)):
+            for rate in (False, True):
+                q = _q(ds, agg, start=B + 600, end=end, rate=rate)
+                q.flags = flags
+                tol = 1e-9 if agg == "dev" else 0.0
+                assert_groups_match(eng.run(q), O.run_rollup_query(rb, q), agg, tol=tol,
+                                    ctx=f"{ds} {agg} flags={flags} rate={rate}")
+
+
+def test_run_multi_over_rollup(eng):
+    """tsdbhip_run_multi over a rollup table: each sub-query as tsdbhip_run answers it."""
+    rng = np.random.default_rng(21)
+    rb = random_table(rng, 30, 3, 2)
+    eng.load_rollup(rb)
+    qs = [_q("1h-avg", a, end=B + 86400) for a in ("sum", "avg", "count", "p90", "max")]
+    got = eng.run_multi(qs)
+    for q, g in zip(qs, got):
+        w = eng.run(q)
+        assert len(g) == len(w)
+        for (g1, t1, b1, i1), (g2, t2, b2, i2) in zip(g, w):
+            assert g1 == g2
+            np.testing.assert_array_equal(t1, t2)
+            np.testing.assert_array_equal(b1, b2)
+            np.testing.assert_array_equal(i1, i2)
 
 
 def random_table(rng, n_series, n_groups, days, p_sum=0.9, p_cnt=0.9, floats=False, counts=True,
