@@ -1468,11 +1468,11 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   // device copies of one chunk of the scan and per-column / per-row scratch (freed at the end)
   DevBuf d_rcp, d_cqo, d_cvo, d_cts, d_q, d_v, d_crow, d_cn, d_coff, d_cinfo, d_rheap, d_rone, d_rerr;
   DevBuf d_key, d_key2, d_idx, d_idx2, d_ecol, d_eqo, d_evo, d_klen, d_sq, d_sv, d_sc, d_sm;
-  DevBuf d_rlo, d_rq, d_rv, d_rstate, d_rmeta, d_rdq, d_rdv, d_raw, d_bad;
+  DevBuf d_rlo, d_rq, d_rv, d_rstate, d_rmeta, d_rdq, d_rdv, d_raw, d_bad, d_rmax;
   auto release_all = [&]() {
     for (DevBuf* b : {&d_rcp, &d_cqo, &d_cvo, &d_cts, &d_q, &d_v, &d_crow, &d_cn, &d_coff, &d_cinfo, &d_rheap, &d_rone,
                       &d_rerr, &d_key, &d_key2, &d_idx, &d_idx2, &d_ecol, &d_eqo, &d_evo, &d_klen, &d_sq, &d_sv,
-                      &d_sc, &d_sm, &d_rlo, &d_rq, &d_rv, &d_rstate, &d_rmeta, &d_rdq, &d_rdv, &d_raw, &d_bad})
+                      &d_sc, &d_sm, &d_rlo, &d_rq, &d_rv, &d_rstate, &d_rmeta, &d_rdq, &d_rdv, &d_raw, &d_bad, &d_rmax})
       b->release();
   };
   struct Rel { std::function<void()> f; ~Rel() { f(); } } rel{release_all};
@@ -1482,8 +1482,16 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   std::vector<int32_t> rstate(R1), rerr(R1);
   CmpParams p{};
   p.fix_dup = cb->fix_duplicates ? 1 : 0;
-  double cmp_ms = 0;   // device spans; the uploads and the host layout between them are not counted
+  // device spans; the uploads and the host layout between them are not counted.  A scan in several
+  // chunks sizes every chunk, then recomputes each one before writing it: both passes count.
+  double cmp_ms = 0;
   HIP_OK(d_bad.ensure(4));
+  HIP_OK(d_rmax.ensure(8));
+  // the per-row LDS path (k_cmp_row) when every row of a chunk fits one block; else the global
+  // sort (TSDBHIP_CMP_ROWS=0 forces the latter)
+  const char* rows_env = std::getenv("TSDBHIP_CMP_ROWS");
+  const bool rows_ok = !(rows_env && rows_env[0] == '0');
+  std::vector<int> row_cap(n_chunks, 0);
   // upload, analyze and build the entries of chunk k; its rows' sizes and states to the host
   auto prepare = [&](int k) -> int {
     const int64_t r0 = cuts[k], r1 = cuts[k + 1], nr = r1 - r0;
@@ -1547,8 +1555,25 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     HIP_OK(hipMemcpyAsync(&n_ent, p.col_off + nc, 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     if (n_ent >= kLim) return fail(TSDB_E_NOT_IMPLEMENTED, "more than 2^31 datapoints in one compaction chunk");
-    const int64_t E1 = std::max<int64_t>(1, n_ent);
     p.n_ent = n_ent;
+    HIP_OK(d_rq.ensure(r1c * 8));
+    HIP_OK(d_rv.ensure(r1c * 8));
+    HIP_OK(d_rstate.ensure(r1c * 4));
+    HIP_OK(d_rmeta.ensure(r1c));
+    p.row_q = d_rq.as<int64_t>();
+    p.row_v = d_rv.as<int64_t>();
+    p.row_state = d_rstate.as<int32_t>();
+    p.row_meta = d_rmeta.as<uint8_t>();
+    row_cap[k] = 0;
+    if (rows_ok) {
+      hipError_t he = hipSuccess;
+      row_cap[k] = cmp_row_cap(p, d_rmax.as<uint32_t>(), st, &he);
+      HIP_OK(he);
+    }
+    if (row_cap[k]) {
+      HIP_OK(cmp_rows_fused(p, row_cap[k], false, st));
+    } else {
+    const int64_t E1 = std::max<int64_t>(1, n_ent);
     HIP_OK(d_key.ensure(E1 * 8));
     HIP_OK(d_key2.ensure(E1 * 8));
     HIP_OK(d_idx.ensure(E1 * 4));
@@ -1559,10 +1584,6 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     HIP_OK(d_klen.ensure(E1 * 4));
     for (DevBuf* b : {&d_sq, &d_sv, &d_sc, &d_sm}) HIP_OK(b->ensure((E1 + 1) * 8));
     HIP_OK(d_rlo.ensure(r1c * 8));
-    HIP_OK(d_rq.ensure(r1c * 8));
-    HIP_OK(d_rv.ensure(r1c * 8));
-    HIP_OK(d_rstate.ensure(r1c * 4));
-    HIP_OK(d_rmeta.ensure(r1c));
     p.key = d_key.as<uint64_t>();
     p.key2 = d_key2.as<uint64_t>();
     p.idx = d_idx.as<uint32_t>();
@@ -1576,13 +1597,10 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     p.sc = d_sc.as<int64_t>();
     p.sm = d_sm.as<int64_t>();
     p.row_lo = d_rlo.as<int64_t>();
-    p.row_q = d_rq.as<int64_t>();
-    p.row_v = d_rv.as<int64_t>();
-    p.row_state = d_rstate.as<int32_t>();
-    p.row_meta = d_rmeta.as<uint8_t>();
     int rb = 1;
     while (((int64_t)1 << rb) <= nr) rb++;
     HIP_OK(cmp_entries(p, &c->cmp_tmp, &c->cmp_tmp_bytes, std::min(64, 22 + rb), st));
+    }
     HIP_OK(hipEventRecord(c->ev[2], st));
     if (nr) {
       HIP_OK(hipMemcpyAsync(rq.data() + r0, p.row_q, nr * 8, hipMemcpyDeviceToHost, st));
@@ -1610,7 +1628,8 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     p.out_q = c->qual.as<uint8_t>();
     p.out_v = c->val.as<uint8_t>();
     HIP_OK(hipEventRecord(c->ev[3], st));
-    HIP_OK(cmp_write(p, st));
+    if (row_cap[k]) HIP_OK(cmp_rows_fused(p, row_cap[k], true, st));
+    else HIP_OK(cmp_write(p, st));
     HIP_OK(hipEventRecord(c->ev[1], st));
     HIP_OK(hipStreamSynchronize(st));
     float t = 0;

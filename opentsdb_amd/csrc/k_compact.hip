@@ -19,6 +19,9 @@
 //   k_cmp_rowfix   one thread per row: stored single columns and meta bytes.
 // The heap merge equals the sorted merge when every column's datapoints are in time order,
 // which compactions write; a compacted column out of order is reported NOT_IMPLEMENTED.
+// When every row of a chunk has at most 4096 datapoints (the common case: an hour row), the
+// explode / sort / dedup / scans / write steps run instead per row in one block's LDS
+// (k_cmp_row, below): no global entry arrays, no global radix sort.
 #include "kcommon.h"
 
 #include <hipcub/hipcub.hpp>
@@ -418,6 +421,273 @@ hipError_t cmp_rebase(const uint64_t* src, uint64_t* dst, int64_t n, uint64_t ba
 hipError_t cmp_write(const CmpParams& p, hipStream_t s) {
   if (p.n_ent > 0) hipLaunchKernelGGL(k_cmp_write, dim3(blocks_of(p.n_ent)), dim3(256), 0, s, p);
   if (p.n_rows > 0) hipLaunchKernelGGL(k_cmp_rowfix, dim3(blocks_of(p.n_rows)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+// ---- the per-row path ----------------------------------------------------------------------
+// A scan row holds at most a few thousand datapoints (3600 a second-resolution hour), so one
+// 256-thread block takes a whole row: its columns' datapoints are exploded into LDS as
+// (offset ms << 12 | entry) keys -- the entry ordinal keeps scan order among equal offsets, as
+// the global sort's stability does -- bitonic-sorted there, deduplicated run by run (the heap's
+// newest-column rule, append repeats, the duplicate check), prefix-summed, and (second launch,
+// after the host layout) written as the compacted cell.  No per-datapoint arrays go through
+// HBM: the sizing pass reads the columns, the write pass reads them again and writes the cell.
+constexpr int CMP_ROW_CAP = 4096;   // datapoints per row (12 bits of the key)
+constexpr int CMP_ROW_THREADS = 256;
+
+__global__ __launch_bounds__(256) void k_cmp_rowmax(CmpParams p, uint32_t* out) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t n = 0, nc = 0;
+  if (r < p.n_rows) {
+    const int64_t c0 = p.row_col_ptr[r], c1 = p.row_col_ptr[r + 1];
+    const int64_t e = p.col_off[c1] - p.col_off[c0];
+    n = (uint32_t)min<int64_t>(e, 0xFFFFFFFFll);
+    nc = (uint32_t)min<int64_t>(c1 - c0, 0xFFFFFFFFll);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    n = max(n, (uint32_t)__shfl_xor((int)n, o));
+    nc = max(nc, (uint32_t)__shfl_xor((int)nc, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(&out[0], n);
+    atomicMax(&out[1], nc);
+  }
+}
+
+__device__ __forceinline__ CmpEnt row_ent(const CmpParams& p, int64_t c, uint32_t qpos, uint32_t vpos) {
+  CmpEnt r;
+  const uint32_t info = p.col_info[c];
+  const uint8_t* vb = p.v + p.col_vo[c];
+  r.fix = false;
+  r.fixed_q1 = 0;
+  if ((info & 3) == CMP_APPEND) {
+    r.qp = vb + qpos;
+  } else {
+    r.qp = p.q + p.col_qo[c] + qpos;
+    if (p.col_qo[c + 1] - p.col_qo[c] == 2 && (info & 8)) { r.fix = true; r.fixed_q1 = (uint8_t)(info >> 8); }
+  }
+  r.eq = cmp_in_ms(r.qp[0]) ? 4 : 2;
+  const uint8_t fl = r.fix ? r.fixed_q1 : r.qp[r.eq - 1];
+  r.evl = (fl & 7) + 1;
+  r.vp = vb + vpos;
+  return r;
+}
+
+// block-wide exclusive scan of one int per thread (LDS scratch of 256 + 1 ints); returns the
+// thread's offset, *total = the block's sum
+__device__ __forceinline__ int block_excl_scan(int x, int* sh, int* total) {
+  const int t = threadIdx.x;
+  int v = x;
+  const int lane = t & 63;
+  for (int o = 1; o < 64; o <<= 1) {   // inclusive wave scan
+    const int y = __shfl_up(v, o);
+    if (lane >= o) v += y;
+  }
+  if (lane == 63) sh[t >> 6] = v;
+  __syncthreads();
+  int base = 0;
+  for (int w = 0; w < (t >> 6); w++) base += sh[w];
+  const int all = sh[0] + sh[1] + sh[2] + sh[3];
+  __syncthreads();
+  *total = all;
+  return base + v - x;
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(256) void k_cmp_row(CmpParams p, int P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  uint64_t* key = reinterpret_cast<uint64_t*>(sm);     // [P] sorted keys
+  uint16_t* ecol = reinterpret_cast<uint16_t*>(key + P);   // [P] by entry: column - c0
+  uint16_t* eqo = ecol + P;                            //          qualifier position in the column
+  uint16_t* evo = eqo + P;                             //          value position
+  uint16_t* kin = evo + P;                             // [P] by sorted position: kept | ms | eq | evl
+  __shared__ int scan_sh[8];
+  __shared__ int dup_err;   // a duplicate with different bytes in this row (the global flag may be stale in L1)
+  const int64_t r = blockIdx.x;
+  const int t = threadIdx.x;
+  if (t == 0) dup_err = 0;
+  if (WRITE) {
+    if (p.row_dq[r] < 0 || p.row_state[r] == 0) return;
+    if (p.row_state[r] == 2) {   // the single column as stored (noMergesOrFixups)
+      const int64_t c = p.row_one[r];
+      const uint8_t* qs = p.q + p.col_qo[c];
+      const uint8_t* vs = p.v + p.col_vo[c];
+      for (int64_t b = t; b < p.row_q[r]; b += CMP_ROW_THREADS) p.out_q[p.row_dq[r] + b] = qs[b];
+      for (int64_t b = t; b < p.row_v[r]; b += CMP_ROW_THREADS) p.out_v[p.row_dv[r] + b] = vs[b];
+      return;
+    }
+  } else {
+    // k_cmp_rows' verdicts that need no datapoint
+    if (p.row_err[r] || p.row_heap[r] == 0) {
+      if (t == 0) { p.row_state[r] = 0; p.row_q[r] = p.row_v[r] = 0; p.row_meta[r] = 0; }
+      return;
+    }
+    if (p.row_heap[r] == 1) {
+      const int64_t c = p.row_one[r];
+      const uint32_t info = p.col_info[c];
+      const int64_t ql = (int64_t)(p.col_qo[c + 1] - p.col_qo[c]);
+      if ((info & 3) == CMP_DATA && !(info & 8) && (ql == 2 || (ql == 4 && cmp_in_ms(p.q[p.col_qo[c]])))) {
+        if (t == 0) {
+          p.row_state[r] = 2;
+          p.row_q[r] = ql;
+          p.row_v[r] = (int64_t)(p.col_vo[c + 1] - p.col_vo[c]);
+          p.row_meta[r] = 0;
+        }
+        return;
+      }
+    }
+  }
+  const int64_t c0 = p.row_col_ptr[r], c1 = p.row_col_ptr[r + 1];
+  const int64_t e0 = p.col_off[c0];
+  const int n = (int)(p.col_off[c1] - e0);
+  // explode: one thread per column
+  for (int64_t c = c0 + t; c < c1; c += CMP_ROW_THREADS) {
+    if (p.col_n[c] == 0) continue;
+    int e = (int)(p.col_off[c] - e0);
+    const uint64_t qo = p.col_qo[c], vo = p.col_vo[c];
+    const int64_t ql = (int64_t)(p.col_qo[c + 1] - qo), vl = (int64_t)(p.col_vo[c + 1] - vo);
+    const uint32_t info = p.col_info[c];
+    auto put = [&](int64_t qpos, int64_t vpos, int, int, uint32_t off) {
+      key[e] = ((uint64_t)off << 12) | (uint64_t)e;
+      ecol[e] = (uint16_t)(c - c0);
+      eqo[e] = (uint16_t)qpos;
+      evo[e] = (uint16_t)vpos;
+      e++;
+    };
+    if ((info & 3) == CMP_APPEND) {
+      walk_append(p.v + vo, vl, put);
+    } else {
+      const int64_t vstart = (info & 4) ? 4 : 0;
+      walk_data(p.q + qo, ql, vl - vstart, (uint8_t)(info >> 8),
+                [&](int64_t qi, int64_t vi, int eq, int evl, uint32_t off) { put(qi, vstart + vi, eq, evl, off); });
+    }
+  }
+  for (int i = n + t; i < P; i += CMP_ROW_THREADS) key[i] = ~0ull;
+  __syncthreads();
+  // bitonic sort of the P keys (unique: the entry ordinal is in the low bits)
+  for (int k = 2; k <= P; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = t; i < P / 2; i += CMP_ROW_THREADS) {
+        const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));
+        const int hi = lo + j;
+        const uint64_t x = key[lo], y = key[hi];
+        if ((x > y) == ((lo & k) == 0)) {
+          key[lo] = y;
+          key[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+  // runs of one offset: the newest column's datapoint is kept (k_cmp_dedup's rules)
+  for (int i = t; i < n; i += CMP_ROW_THREADS) {
+    const uint64_t off = key[i] >> 12;
+    if (i > 0 && (key[i - 1] >> 12) == off) continue;
+    int j = i + 1;
+    while (j < n && (key[j] >> 12) == off) j++;
+    auto col_of = [&](int s) { return c0 + (int64_t)ecol[key[s] & 4095]; };
+    auto superseded = [&](int s) {
+      const int64_t c = col_of(s);
+      return (p.col_info[c] & 3) == CMP_APPEND && s + 1 < j && col_of(s + 1) == c;
+    };
+    int best = -1;
+    int64_t best_ts = 0;
+    for (int s = i; s < j; s++) {
+      if (superseded(s)) continue;
+      const int64_t ts = p.col_ts ? p.col_ts[col_of(s)] : 0;
+      if (best < 0 || ts > best_ts) { best = s; best_ts = ts; }
+    }
+    const int eb = (int)(key[best] & 4095);
+    const CmpEnt kb = row_ent(p, col_of(best), eqo[eb], evo[eb]);
+    for (int s = i; s < j; s++) {
+      if (s == best) {
+        kin[s] = (uint16_t)(1u | ((kb.eq == 4 ? 1u : 0u) << 1) | ((uint32_t)kb.eq << 2) | ((uint32_t)kb.evl << 5));
+        continue;
+      }
+      kin[s] = 0;
+      if (WRITE || superseded(s) || p.fix_dup) continue;
+      const int es = (int)(key[s] & 4095);
+      const CmpEnt o = row_ent(p, col_of(s), eqo[es], evo[es]);   // getCopyOfCurrentValue vs the kept one
+      bool same = o.evl == kb.evl;
+      for (int b = 0; same && b < o.evl; b++) same = o.vp[b] == kb.vp[b];
+      if (!same) {
+        cmp_fail(p.row_err, r, TSDB_E_ILLEGAL_DATA);
+        dup_err = 1;
+      }
+    }
+  }
+  __syncthreads();
+  // each thread a contiguous run of m sorted positions: its kept bytes / datapoints, then the
+  // block's exclusive offsets
+  const int m = P / CMP_ROW_THREADS > 0 ? P / CMP_ROW_THREADS : 1;
+  const int a0 = t * m, a1 = min(n, a0 + m);
+  int sq = 0, sv = 0, sc = 0, sms = 0;
+  for (int i = a0; i < a1; i++) {
+    const uint32_t x = kin[i];
+    if (!(x & 1)) continue;
+    sq += (x >> 2) & 7;
+    sv += (x >> 5) & 15;
+    sc++;
+    sms += (x >> 1) & 1;
+  }
+  int tq, tv, tc, tm;
+  int oq = block_excl_scan(sq, scan_sh, &tq);
+  int ov = block_excl_scan(sv, scan_sh, &tv);
+  block_excl_scan(sc, scan_sh, &tc);
+  block_excl_scan(sms, scan_sh, &tm);
+  if (!WRITE) {
+    if (t == 0) {
+      if (dup_err) {
+        p.row_state[r] = 0;
+        p.row_q[r] = p.row_v[r] = 0;
+        p.row_meta[r] = 0;
+      } else {
+        p.row_state[r] = tc ? 1 : 0;
+        p.row_q[r] = tc ? tq : 0;
+        p.row_v[r] = tc ? tv + (tc > 1 ? 1 : 0) : 0;
+        p.row_meta[r] = (tm > 0 && tm < tc) ? 1 : 0;   // Const.MS_MIXED_COMPACT
+      }
+    }
+    return;
+  }
+  uint8_t* dq = p.out_q + p.row_dq[r];
+  uint8_t* dv = p.out_v + p.row_dv[r];
+  for (int i = a0; i < a1; i++) {
+    const uint32_t x = kin[i];
+    if (!(x & 1)) continue;
+    const int e = (int)(key[i] & 4095);
+    const CmpEnt en = row_ent(p, c0 + (int64_t)ecol[e], eqo[e], evo[e]);
+    for (int b = 0; b < en.eq; b++) dq[oq + b] = (en.fix && b == 1) ? en.fixed_q1 : en.qp[b];
+    for (int b = 0; b < en.evl; b++) dv[ov + b] = en.vp[b];
+    oq += en.eq;
+    ov += en.evl;
+  }
+  if (t == 0 && tc > 1) dv[p.row_v[r] - 1] = p.row_meta[r];
+}
+
+int cmp_row_cap(const CmpParams& p, uint32_t* scratch2, hipStream_t s, hipError_t* err) {
+  *err = hipSuccess;
+  if (p.n_rows <= 0) return 64;
+  if ((*err = hipMemsetAsync(scratch2, 0, 8, s)) != hipSuccess) return 0;
+  hipLaunchKernelGGL(k_cmp_rowmax, dim3(blocks_of(p.n_rows)), dim3(256), 0, s, p, scratch2);
+  uint32_t h[2] = {0, 0};
+  if ((*err = hipMemcpyAsync(h, scratch2, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return 0;
+  if ((*err = hipStreamSynchronize(s)) != hipSuccess) return 0;
+  if (h[0] > (uint32_t)CMP_ROW_CAP || h[1] > 65535u) return 0;
+  int cap = 64;
+  while (cap < (int)h[0]) cap <<= 1;
+  return cap;
+}
+
+hipError_t cmp_rows_fused(const CmpParams& p, int cap, bool write, hipStream_t s) {
+  if (p.n_rows <= 0) return hipSuccess;
+  const size_t lds = (size_t)cap * 16;
+  const void* fn = write ? (const void*)k_cmp_row<true> : (const void*)k_cmp_row<false>;
+  if (lds > 65536) {
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  if (write) hipLaunchKernelGGL(k_cmp_row<true>, dim3((unsigned)p.n_rows), dim3(CMP_ROW_THREADS), lds, s, p, cap);
+  else hipLaunchKernelGGL(k_cmp_row<false>, dim3((unsigned)p.n_rows), dim3(CMP_ROW_THREADS), lds, s, p, cap);
   return hipGetLastError();
 }
 

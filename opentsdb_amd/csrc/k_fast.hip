@@ -42,10 +42,14 @@ static hipError_t launch_fast_k(const GridParams& p, hipStream_t s) {
 }
 
 // register partials when every slot has its own lane and the series emit needs no rate pass
-// (KR 1; KR 2: every decomposable aggregator's partials at once, tsdbhip_run_multi)
+// (KR 1: the group-by alone; KR 3: with the per-series outputs of the percentile / ordered /
+// dense paths; KR 2: every decomposable aggregator's partials at once, tsdbhip_run_multi)
 template <int F, int QW, int VL>
 static hipError_t launch_fast_t(const GridParams& p, hipStream_t s) {
-  if (p.K <= 64 && !p.rate) return p.multi ? launch_fast_k<F, QW, VL, 2>(p, s) : launch_fast_k<F, QW, VL, 1>(p, s);
+  if (p.K <= 64 && !p.rate) {
+    if (p.multi) return launch_fast_k<F, QW, VL, 2>(p, s);
+    return (p.sel_direct || p.dense_out) ? launch_fast_k<F, QW, VL, 3>(p, s) : launch_fast_k<F, QW, VL, 1>(p, s);
+  }
   if (p.multi) return hipErrorNotSupported;
   return launch_fast_k<F, QW, VL, 0>(p, s);
 }

@@ -1788,8 +1788,9 @@ __device__ __forceinline__ double fast_bucket_value(uint32_t c, double a) {
 }
 
 // K <= 64, no rate: the register-partial variant (emit_series_reg; RP = RegPart, or MultiReg
-// for the fused multi-aggregator pass).
-template <int F, bool MARK = true, class RP>
+// for the fused multi-aggregator pass).  OUT: the instantiation also serves the per-series
+// output modes (sel_direct / dense_out); without it the group-by kernels carry no such branch.
+template <int F, bool MARK = true, bool OUT = true, class RP>
 __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const FastLds& L, int K, int lsb, double amax,
                                                     RP& P, int64_t s, int32_t g, uint32_t nbound = 0,
                                                     double* stage = nullptr) {
@@ -1807,9 +1808,9 @@ __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const F
     const uint32_t nmax = (uint32_t)wave_max((int)c);
     if (!fast_cert<F>(nmax, lsb, amax)) return false;
   }
-  if (p.sel_direct) {
+  if (OUT && p.sel_direct) {
     sel_direct_out<MARK>(p, K, g, s, c != 0, fast_bucket_value<F>(c, a), stage);
-  } else if (p.dense_out) {
+  } else if (OUT && p.dense_out) {
     if (lane < K) {
       p.dense_out[s * K + lane] = fast_bucket_value<F>(c, a);
       p.pres_out[s * K + lane] = c != 0;
@@ -1862,10 +1863,13 @@ __device__ __forceinline__ bool fast_series_end(const GridParams& p, const FastL
   return true;
 }
 
+// KR: 0 = LDS partials (rate, K > 64), 1 = register partials, 2 = the fused multi-aggregator
+// registers, 3 = register partials with the per-series output modes (sel_direct / dense_out).
 template <int F, int QW, int VL, int D, int KR>
 __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __restrict__ rows,
                                               const int64_t* __restrict__ srp, const int64_t* __restrict__ tbeg,
                                               const int64_t* __restrict__ tend) {
+  constexpr bool OUT = KR == 0 || KR == 3;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (scalar) tile index
@@ -1919,7 +1923,7 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
         if (!(mb & FM_OK) || (mb & FM_NEWSER)) {
           if (have) {
             int64_t s = -1;
-            if (p.dense_out || p.sel_direct) {   // the series of the last row folded (dense output only)
+            if (OUT && (p.dense_out || p.sel_direct)) {   // the series of the last row folded (dense output only)
               // rows come in series order: the cursor only moves forward (a scan from the
               // tile's first series at every series end was quadratic in the tile's series:
               // config 2 ordered 6.5 vs 3.9 ms)
@@ -1933,10 +1937,10 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
               s = scur;
             }
             const bool ok =
-                KR ? fast_series_end_reg<F>(p, L, K, lsb, amax, RP, s, p.tile_group[tile])
+                KR ? fast_series_end_reg<F, true, OUT>(p, L, K, lsb, amax, RP, s, p.tile_group[tile])
                    : fast_series_end<F>(p, L, K, lsb, amax, s, p.tile_group[tile]);
             if (!ok) { redo = true; done = true; }
-            if (p.dense_out || p.sel_direct) {   // the next series end is a later series
+            if (OUT && (p.dense_out || p.sel_direct)) {   // the next series end is a later series
               scur++;
               snb = scur + 1 < tend[tile] ? srp[scur + 1] : INT64_MAX;
             }
@@ -1993,7 +1997,9 @@ template <int QW, int VL>
 __device__ __forceinline__ void short_issue(const GridParams& p, uint64_t qoff, uint64_t voff, int ndp,
                                             FRaw<QW, VL>& b) {
   const int lane = lane_id();
+#ifdef TSDBHIP_KDBG
   if (p.dbg & 32) { qoff = 0; voff = 0; }
+#endif
   const int64_t i0 = (lane * DPL < ndp) ? (int64_t)lane * DPL : 0;
   const uint4* q = reinterpret_cast<const uint4*>(p.qual + qoff + i0 * QW);
 #pragma unroll
@@ -2025,10 +2031,12 @@ __device__ __forceinline__ uint64_t rl64(uint64_t x, int l) {
 #define SHORT_OCC2_VLE 4
 #endif
 #define SHORT_OCC2(VL) ((VL) == 0 ? SHORT_OCC2_VLE : 4)
+// KR as k_fast.  The profiling switches of TSDBHIP_DBG exist only in a -DTSDBHIP_KDBG build.
 template <int F, int QW, int VL, int D, int KR>
 __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) void k_short(GridParams p, const RowDesc* __restrict__ rows,
                                                const int64_t* __restrict__ srp, const int64_t* __restrict__ tbeg,
                                                const int64_t* __restrict__ tend) {
+  constexpr bool OUT = KR == 0 || KR == 3;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2062,7 +2070,9 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
     return;
   }
+#ifdef TSDBHIP_KDBG
   if (p.dbg & 16) return;
+#endif
   // bucket geometry of every series' row, computed once per tile (lane = series)
   int gq0, gr0;
   {
@@ -2095,26 +2105,32 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
   auto series = [&](const FRaw<QW, VL>& b, int j) {
     const int nv0 = __builtin_amdgcn_readlane(dndp, j);
     const FGeom g = {__builtin_amdgcn_readlane(gq0, j), __builtin_amdgcn_readlane(gr0, j)};
+#ifdef TSDBHIP_KDBG
     if (!(p.dbg & 2)) {   // TSDBHIP_DBG profiling switches (results invalid when set)
       fast_chunk_any<F, QW, VL>(p, L, b, g, nv0, K);
     } else if (p.dbg & 8) {
       uint32_t x = b.q[0].x ^ b.v[0].x;
       if (x == 0x12345678u) L.cnt[0] = x;
     }
+#else
+    fast_chunk_any<F, QW, VL>(p, L, b, g, nv0, K);
+#endif
     return nv0;
   };
   // sel_direct into the column layout: rows staged 8 series at a time (sel_cols_flush)
-  double* stage = (KR == 1 && p.sel_stage) ? (double*)(smem + (int64_t)wave * p.wave_lds + p.sel_stage) : nullptr;
+  double* stage = (KR == 3 && p.sel_stage) ? (double*)(smem + (int64_t)wave * p.wave_lds + p.sel_stage) : nullptr;
   auto series_end = [&](int j, int nv0) {
+#ifdef TSDBHIP_KDBG
     if (p.dbg & 1) return;
+#endif
     const int lsb = __builtin_amdgcn_readlane(dlsb, j);
     const double amax = __longlong_as_double((long long)rl64(damax, j));
     const bool fine =
-        KR ? fast_series_end_reg<F, false>(p, L, K, lsb, amax, RP, s0 + j, p.tile_group[tile], (uint32_t)nv0,
-                                           stage ? stage + (j & 7) * K : nullptr)
+        KR ? fast_series_end_reg<F, false, OUT>(p, L, K, lsb, amax, RP, s0 + j, p.tile_group[tile], (uint32_t)nv0,
+                                                stage ? stage + (j & 7) * K : nullptr)
            : fast_series_end<F>(p, L, K, lsb, amax, s0 + j, p.tile_group[tile]);
     if (!fine) redo = true;
-    else if (stage && ((j & 7) == 7 || j == ns - 1))
+    else if (KR == 3 && stage && ((j & 7) == 7 || j == ns - 1))
       sel_cols_flush(p, K, p.tile_group[tile], s0 + (j & ~7), (j & 7) + 1, stage);
   };
   int j = 0;
@@ -2141,7 +2157,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
     return;
   }
-  if (p.sel_wr && lane < ns) p.sel_wr[s0 + lane] = 1;   // sel_direct: every series of the tile was written
+  if (OUT && p.sel_wr && lane < ns) p.sel_wr[s0 + lane] = 1;   // sel_direct: every series of the tile was written
   WAVE_SYNC();
   double* ga_ = p.part.a + tile * K;
   double* gb_ = p.part.b + tile * K;

@@ -360,6 +360,71 @@ def test_chunked_compaction_equals_one_pass(eng, seed, salt, chunk):
             assert_groups_match(eng.run(q), w, agg, tol=0.0, ctx=f"chunk {chunk} {agg}")
 
 
+def _load_with_env(eng, cb, **env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        eng.load_cells(cb)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    return eng.download()
+
+
+def _queries_and_answers(eng):
+    out = []
+    for agg, ds in (("sum", "1m-avg"), ("max", "10m-max"), ("none", None), ("zimsum", None)):
+        q = abi.new_query(B, B + 6 * 3600, agg)
+        if ds:
+            d = O.parse_downsample(ds)
+            q.ds_function, q.ds_interval_ms = d.ds_function, d.ds_interval_ms
+        try:
+            out.append((q, agg, eng.run(q)))
+        except EngineError as e:
+            out.append((q, agg, e.code))
+    return out
+
+
+@pytest.mark.parametrize("seed,salt,fix", [(41, False, True), (42, True, True), (43, False, False), (44, False, True)])
+def test_row_lds_path_equals_global_sort(eng, seed, salt, fix):
+    """The per-row LDS compaction (k_cmp_row: explode, bitonic sort, dedup and write in one block)
+    against the global-sort pipeline (TSDBHIP_CMP_ROWS=0): the same resident rows, the same
+    lazily raised errors, the same query answers -- also in chunks (TSDBHIP_CMP_CHUNK)."""
+    series, groups = _random_scan(seed, salt=salt)
+    cb = abi.HostCellBatch.from_rows(series, groups, fix)
+    want = _load_with_env(eng, cb, TSDBHIP_CMP_ROWS=0)
+    answers = _queries_and_answers(eng)
+    for env in ({}, {"TSDBHIP_CMP_CHUNK": 150}):
+        got = _load_with_env(eng, cb, **env)
+        assert rows_of(got) == rows_of(want), env
+        assert np.array_equal(got.group_id, want.group_id)
+        for q, agg, w in answers:
+            if isinstance(w, int):
+                with pytest.raises(EngineError) as ei:
+                    eng.run(q)
+                assert ei.value.code == w
+            else:
+                assert_groups_match(eng.run(q), w, agg, tol=0.0, ctx=f"rows path {env} {agg}")
+
+
+def test_row_over_lds_capacity_takes_global_sort(eng):
+    """A row of more than 4096 datapoints (ms cells of one hour) cannot be sorted in one block: the
+    chunk falls back to the global sort; both agree with the oracle's compaction."""
+    rng = np.random.default_rng(77)
+    offs = np.sort(rng.choice(3_600_000, size=5000, replace=False))
+    cols = [_cell(int(o), True, int(rng.integers(-500, 500)), "int") for o in offs]
+    order = rng.permutation(len(cols))
+    row = [(cols[j][0], cols[j][1], int(k)) for k, j in enumerate(order)]
+    small = [(B + 3600, random_row(rng, 40))]
+    cb = abi.HostCellBatch.from_rows([[(B, row)], small], [0, 1], True)
+    got = _load_with_env(eng, cb)
+    want = O.compact_row([(q, v) for q, v, _ in row], True, [t for _, _, t in row])
+    assert rows_of(got)[0] == (B, want[0], want[1])
+
+
 @pytest.mark.parametrize("chunk", [None, 5])
 def test_decreasing_column_offsets_rejected(eng, chunk):
     """Column offsets are checked on the device chunk by chunk: a decreasing offset inside a row
