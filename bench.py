@@ -221,8 +221,10 @@ def query(args):
 
 
 def visible_gpus() -> int:
-    import torch
-    return torch.cuda.device_count()   # (counts devices without initialising HIP)
+    # the library's hipGetDeviceCount: torch.cuda.device_count() would bring up torch's own
+    # HIP runtime beside the library's, which broke ncclCommInitAll in the same process
+    from opentsdb_amd import engine
+    return engine.device_count()
 
 
 def md_engine(args, n):

@@ -350,6 +350,9 @@ int tsdbhip_assemble(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_
 enum { TSDB_SHARD_AUTO = -1 };
 enum { TSDB_MD_AUTO = -1, TSDB_MD_COPY = 0, TSDB_MD_RCCL = 1 };
 int tsdbhip_init_devices(const int* devices, int n_devices, int transport, tsdbhip_ctx** out);
+/* HIP devices visible to this process (hipGetDeviceCount), for a host that sizes its device list
+ * without initialising another runtime. */
+int tsdbhip_device_count(int* n);
 int tsdbhip_md_shard_mode(tsdbhip_ctx* ctx, int mode);
 /* n_devices, transport in use, shard mode of the resident batch (TSDB_SHARD_AUTO before a load)
  * and, when shard_series is not NULL, the resident series of every device ([n_devices]). */

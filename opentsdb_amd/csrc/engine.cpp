@@ -3406,6 +3406,16 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
       }
     }
   } guard{&direct_r, c->copy_stream};
+  if (direct) {
+    // the result block, sized by the decoded points (every union point is one of them), is
+    // allocated while the device decodes: a fresh pinned block of 100s of MB costs the host
+    // longer than the evaluation itself
+    int64_t nact = 0;
+    for (int64_t g = 0; g < G; g++) nact += act[g];
+    direct_r = make_result(nact, std::max<int64_t>(0, np));
+    if (!direct_r) return fail(TSDB_E_NOMEM, "result allocation");
+    tr.mark("result alloc");
+  }
   for (int64_t g0 = 0; g0 < G; g0 += per_chunk) {
     const int64_t g1 = std::min(G, g0 + per_chunk);
     const int64_t ng = g1 - g0;
@@ -3531,9 +3541,9 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
         HIP_OK(launch_raw_sel(bp, k_max, c->stream));
       }
       if (uns) HIP_OK(launch_raw_dz_check(rp, nout, c->stream));
-    } else {
+    } else if (!direct) {
       HIP_OK(hipEventRecord(c->ev[3], c->stream));
-      if (!direct) HIP_OK(launch_raw_eval(rp, c->stream));
+      HIP_OK(launch_raw_eval(rp, c->stream));
     }
     const size_t base = res_ts.size();
     if (direct) {
@@ -3541,11 +3551,7 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
       // are evaluated in up to 8 launches split at group boundaries; each launch's output range
       // (its groups' union points, contiguous) downloads on copy_stream while the next one
       // runs, into a pinned result block
-      int64_t nact = 0;
-      for (int64_t g = 0; g < G; g++) nact += act[g];
-      direct_r = make_result(nact, nout);
-      if (!direct_r) return fail(TSDB_E_NOMEM, "result allocation");
-      tr.mark("result alloc");
+      if (!P.gsel) HIP_OK(hipEventRecord(c->ev[3], c->stream));
       // chunked only for the double-only evaluation: its strips are short (config 4 rate: the
       // download hides behind the next chunk, 36 -> 30 ms per step); the long LERP strips are
       // long-running waves that a launch split leaves idle at every chunk's tail (94 -> 188 ms)

@@ -49,9 +49,10 @@ namespace {
   } while (0)
 
 // ---- RCCL, resolved at run time -----------------------------------------------------------
-// librccl.so.1 is the copy already in the process when there is one (PyTorch's, same soname),
-// else the system's: the library itself loads without RCCL, and a context whose devices repeat
-// (several shards on one GPU) never needs it.
+// The system's librccl.so.1 (built against the same HIP runtime as this library; PyTorch's wheel
+// carries its own librccl.so and HIP runtime, which this does not bind).  Resolved at run time:
+// the library itself loads without RCCL, and a context whose devices repeat (several shards on
+// one GPU) never needs it.
 struct Rccl {
   bool ok = false;
   std::string why;
@@ -1117,6 +1118,13 @@ extern "C" int tsdbhip_init_devices(const int* devices, int n_devices, int trans
     return set_error(rc, msg);
   }
   *out = c;
+  return 0;
+}
+
+extern "C" int tsdbhip_device_count(int* n) {
+  if (!n) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  *n = 0;
+  MOK(hipGetDeviceCount(n));
   return 0;
 }
 

@@ -9,6 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 import subprocess
+import time
 
 import numpy as np
 
@@ -33,6 +34,7 @@ EXPORTS = [
     "tsdbhip_hist_run_range", "tsdbhip_hist_result_free", "tsdbhip_expr_map", "tsdbhip_expr_zip", "tsdbhip_expr_topn",
     "tsdbhip_batch_range_sizes", "tsdbhip_batch_download_range", "tsdbhip_expr_sync", "tsdbhip_init_devices",
     "tsdbhip_md_shard_mode", "tsdbhip_md_info", "tsdbhip_host_alloc", "tsdbhip_host_free", "tsdbhip_md_stats",
+    "tsdbhip_device_count",
 ]
 
 SHARD_AUTO, SHARD_SERIES, SHARD_GROUPS, SHARD_SPANS = -1, 0, 1, 2   # tsdbhip.h TSDB_SHARD_*
@@ -98,6 +100,7 @@ def lib():
         L.tsdbhip_init_devices.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(vp)]
         L.tsdbhip_md_shard_mode.argtypes = [vp, C.c_int]
         L.tsdbhip_md_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_void_p]
+        L.tsdbhip_device_count.argtypes = [C.POINTER(C.c_int)]
         L.tsdbhip_md_stats.argtypes = [vp, C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double)]
         L.tsdbhip_destroy.argtypes = [vp]
         L.tsdbhip_host_alloc.argtypes = [C.c_uint64, C.POINTER(vp)]
@@ -152,6 +155,15 @@ def _check(rc):
     if rc < 0:
         raise EngineError(rc, lib().tsdbhip_last_error().decode(errors="replace"))
     return rc
+
+
+def device_count() -> int:
+    """HIP devices visible to the library (tsdbhip_device_count).  Use this rather than
+    torch.cuda.device_count() before building an RCCL context: torch's wheel carries its own
+    HIP / HSA runtime, and initialising it beside the library's broke ncclCommInitAll here."""
+    n = C.c_int()
+    _check(lib().tsdbhip_device_count(C.byref(n)))
+    return n.value
 
 
 def parse_downsample(spec: str) -> abi.Query:
@@ -242,6 +254,7 @@ class Engine:
         self.device = device
         self.devices = None if devices is None else [int(d) for d in devices]
         self._batch = None
+        self.last_call_ms = 0.0
 
     def shard_mode(self, mode: int):
         """tsdbhip_md_shard_mode: SHARD_AUTO / SHARD_SERIES / SHARD_GROUPS for the next loads."""
@@ -375,7 +388,9 @@ class Engine:
         """tsdbhip_run -> [(group_id, ts, bits, is_int)]; the arrays are views into the
         library's result, freed when the last of them is garbage-collected."""
         res = C.POINTER(abi.Result)()
+        t = time.perf_counter()
         _check(lib().tsdbhip_run(self.ctx, C.byref(q), C.byref(res)))
+        self.last_call_ms = (time.perf_counter() - t) * 1000.0   # the C call alone (host wall time)
         return abi.result_to_groups(res.contents, owner=_ResultOwner(res))
 
     def run_multi(self, queries):

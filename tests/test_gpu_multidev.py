@@ -155,8 +155,7 @@ def test_series_shards(batch, single, world):
 
 
 def device_count():
-    import torch
-    return torch.cuda.device_count()
+    return E.device_count()   # (not torch's: its own HIP runtime beside RCCL's broke ncclCommInitAll)
 
 
 @pytest.mark.parametrize("transport", [E.MD_RCCL, E.MD_COPY])

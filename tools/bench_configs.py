@@ -201,20 +201,23 @@ def main():
         U = [len(g[1]) for g in res]
         k = [int((b.group_id == g[0]).sum()) for g in res]
         evals = sum(u * kk for u, kk in zip(U, k))
-        ms, ev = [], []
+        ms, ev, cc, dv = [], [], [], []
         for _ in range(args.steps):
             t = time.perf_counter()
             eng.run(q)
             ms.append((time.perf_counter() - t) * 1000)
             tm = eng.timing()
             ev.append(tm.group_reduce_ms)
+            dv.append(tm.decode_downsample_ms)
+            cc.append(eng.last_call_ms)
         step_ms = sum(ms) / len(ms)
         eval_ms = sum(ev) / len(ev)
         line = {
             "config": args.config, "query": name, "series": args.series, "groups": args.groups,
             "datapoints": int(tm.datapoints), "union_points": sum(U), "span_evaluations": evals,
             "ms_per_step": step_ms, "datapoints_per_s": tm.datapoints / (step_ms / 1000),
-            "k_raw_eval_ms": eval_ms, "device_ms": tm.decode_downsample_ms,
+            "k_raw_eval_ms": eval_ms, "device_ms": sum(dv) / len(dv), "c_call_ms": sum(cc) / len(cc),
+            "step_ms_median": sorted(ms)[len(ms) // 2],
             "span_evaluations_per_s": evals / (eval_ms / 1000) if eval_ms > 0 else None,
             "gen_s": gen_s, "load_s": load_s,
         }
