@@ -2182,9 +2182,135 @@ __global__ __launch_bounds__(256) void k_raw_sel_reg(RawParams p) {
   if (lane == 0) raw_sel_store(p, idx, is_int, fn, m, r1, dif, k0, k1);
 }
 
+// The order statistics near the top (p90 ... p999 of large groups; any rank of small ones):
+// one WAVE per 64 consecutive union points of a strip, lane = point.  The operands of span i
+// for those points are adjacent (k_raw_vals writes [span][RAW_STRIP points]), so every load
+// instruction reads 512 contiguous bytes -- the per-point kernels above read one 8-byte operand
+// per 4 KB line and lane, and wait on the texture path.  Each lane streams its point's k
+// operands in chunks of 8 and keeps the T largest keys in registers, sorted descending (a
+// compare-exchange chain per insertion, only for operands above the current T-th).  Ranks from
+// the top below T (host-checked bound) are then read from the registers; the keys and the
+// estimate are those of the selections above.
+template <int T>
+__device__ __forceinline__ void topk_insert(uint64_t (&b)[T], uint64_t c) {
+#pragma unroll
+  for (int t = 0; t < T; t++) {
+    const uint64_t hi = b[t] > c ? b[t] : c;
+    c = b[t] > c ? c : b[t];
+    b[t] = hi;
+  }
+}
+
+// b[i] for a lane-varying i, as masks (a select chain is turned back into a dynamically
+// indexed array, which lives in scratch)
+template <int T>
+__device__ __forceinline__ uint64_t topk_at(const uint64_t (&b)[T], int i) {
+  uint64_t r = 0;
+#pragma unroll
+  for (int t = 0; t < T; t++) r |= b[t] & (0ULL - (uint64_t)(i == t));
+  return r;
+}
+
+template <int T, int MODE>   // MODE 0: every point long, 1: every point double, 2: mixed
+__device__ __forceinline__ void topk_stream(const RawParams& p, int64_t vb, int k, bool is_int, uint64_t (&b)[T],
+                                            int& m) {
+  constexpr int64_t US = RAW_STRIP;
+  for (int i0 = 0; i0 < k; i0 += 8) {
+    uint64_t x[8];
+    uint32_t cm = 0;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int i = i0 + u;
+      const int64_t o = vb + (int64_t)(i < k ? i : k - 1) * US;
+      bool ok;
+      if (MODE == 0 || (MODE == 2 && is_int)) {
+        ok = i < k && p.vals_p[o];
+        x[u] = (uint64_t)p.vals_l[o] ^ 0x8000000000000000ULL;
+      } else {
+        const double d = p.vals_d[o];
+        ok = i < k && !isnan(d);   // runDouble drops NaN operands
+        x[u] = f2key(d);
+      }
+      m += ok ? 1 : 0;
+      if (ok && x[u] > b[T - 1]) cm |= 1u << u;
+    }
+    // insertions, operand by operand where some lane holds a candidate (static register
+    // indices: a dynamically indexed x[] went to scratch)
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (__any((cm >> u) & 1u))
+        if ((cm >> u) & 1u) topk_insert<T>(b, x[u]);
+  }
+}
+
+template <int T>
+__global__ __launch_bounds__(256) void k_raw_sel_top(RawParams p) {
+  const int wv = threadIdx.x >> 6;
+  const int lane = lane_id();
+  constexpr int WPS = RAW_STRIP / 64;   // waves per strip
+  const int64_t wid = (int64_t)blockIdx.x * 4 + wv;
+  const int64_t sl = wid / WPS;
+  if (sl >= p.n_strips) return;
+  const int64_t j = (wid - sl * WPS) * 64 + lane;   // point of the strip
+  const int64_t gi = p.strip_g[sl];
+  const int64_t u0 = (int64_t)p.strip_t[sl] * RAW_STRIP + j;
+  if (!__any(u0 < p.U[gi])) return;   // the strip's tail
+  const bool live = u0 < p.U[gi];
+  const int64_t idx = p.out_off[gi] + u0;
+  const int64_t g = gi + p.g0;
+  const int k = (int)(p.grp_ser[g + 1] - p.grp_ser[g]);
+  const int64_t vb = p.vals_off[sl] + j;
+  const bool is_int = live && p.out_int[idx] != 0;
+  uint64_t b[T];
+#pragma unroll
+  for (int t = 0; t < T; t++) b[t] = 0;   // the smallest key: pads rank below every operand
+  int m = 0;
+  if (__all(is_int || !live)) topk_stream<T, 0>(p, vb, k, true, b, m);
+  else if (__all(!is_int)) topk_stream<T, 1>(p, vb, k, false, b, m);
+  else topk_stream<T, 2>(p, vb, k, is_int, b, m);
+  if (!live) return;
+  const int fn = p.sel_fn;
+  int r0, r1;
+  double dif;
+  raw_sel_ranks(fn, is_int, m, r0, r1, dif);
+  uint64_t k0 = 0, k1 = 0;
+  if (m > 0) {
+    const int i0 = m - 1 - r0, i1 = r1 >= 0 ? m - 1 - r1 : i0;   // positions from the top
+    if (i0 >= T || i0 < 0 || i1 < 0) {
+      set_err(p.err, TSDB_E_HIP);   // planning error: the rank is not among the kept keys
+      return;
+    }
+    k0 = topk_at<T>(b, i0);
+    k1 = topk_at<T>(b, i1);
+  }
+  raw_sel_store(p, idx, is_int, fn, m, r1, dif, k0, k1);
+}
+
+// T for k_raw_sel_top when every rank it can be asked for lies within T of the top: m - 1 - r0
+// <= (1 - q) m + 1 for the LEGACY / R_3 / R_7 positions of quantile q over m <= k_max operands
+// (Median: m / 2); 0 = no.
+int raw_sel_top_t(int fn, int64_t k_max) {
+  const char* e = std::getenv("TSDBHIP_RAW_SEL_TOP");   // A/B: 0 = the per-point kernels
+  if (e && e[0] == '0') return 0;
+  for (int T : {16, 32}) {
+    if (k_max <= T) return T;
+    if (fn == TSDB_AGG_MEDIAN) continue;
+    const int i = (fn - TSDB_AGG_P999) % 6;
+    const double q = (i == 0 ? 99.9 : i == 1 ? 99.0 : i == 2 ? 95.0 : i == 3 ? 90.0 : i == 4 ? 75.0 : 50.0) / 100.0;
+    if (std::ceil((1.0 - q) * (double)k_max) + 2.0 <= (double)(T - 1)) return T;
+  }
+  return 0;
+}
+
 // k_max: the largest group of the batch; each wave stages k_max keys in LDS.
 hipError_t launch_raw_sel(const RawParams& p, int64_t k_max, hipStream_t s) {
   if (p.n_strips == 0) return hipSuccess;
+  if (const int T = raw_sel_top_t(p.sel_fn, k_max)) {
+    const dim3 grid((unsigned)((p.n_strips * (RAW_STRIP / 64) + 3) / 4)), block(256);
+    if (T == 16) hipLaunchKernelGGL(k_raw_sel_top<16>, grid, block, 0, s, p);
+    else hipLaunchKernelGGL(k_raw_sel_top<32>, grid, block, 0, s, p);
+    return hipGetLastError();
+  }
   const char* renv = std::getenv("TSDBHIP_RAW_SEL_REG");   // A/B: 0 = the LDS-staged kernel
   if (k_max <= 64 * 32 && !(renv && renv[0] == '0')) {
     const dim3 grid((unsigned)((p.n_strips * RAW_STRIP + SELW - 1) / SELW)), block(64 * SELW);

@@ -136,3 +136,24 @@ def test_raw_pct_register_select(eng, monkeypatch, reg, n_spans):
         for agg in ["p95", "median"]:
             q = abi.new_query(T0, T0 + 3599, agg)
             exact(eng.run_batch(b, q), O.run_query(b, q), agg, f"random {mixed} {n_spans} {agg}")
+
+
+@pytest.mark.parametrize("top", ["0", "1"])
+@pytest.mark.parametrize("n_spans", [12, 33, 300, 1563, 2900])
+def test_raw_pct_top_select(eng, monkeypatch, top, n_spans):
+    """k_raw_sel_top (lane = union point, the T largest keys streamed into registers; used when
+    every requested rank lies within T of the top) against the oracle and against the per-point
+    kernels (TSDBHIP_RAW_SEL_TOP=0): long and double points, absent operands, NaN members, ties,
+    every estimation type, small groups for the median."""
+    monkeypatch.setenv("TSDBHIP_RAW_SEL_TOP", top)
+    eng.synth(n_spans, T0, 4, 10000, 1, 1, 25, 0x77 + n_spans)
+    b = eng.download()
+    for agg in ["p99", "p999", "ep99r3", "ep99r7", "p95", "median", "p50"]:
+        q = abi.new_query(T0, T0 + 3599, agg)
+        exact(eng.run(q), O.run_query(b, q), agg, f"int {n_spans} {agg}")
+    for mixed in (False, True):
+        rb = random_batch(n_spans, n_series=min(n_spans, 150), n_groups=1, mixed=mixed, span_h=1)
+        for agg in ["p99", "ep999r7", "median"]:
+            q = abi.new_query(T0, T0 + 3599, agg)
+            exact(eng.run_batch(rb, q), O.run_query(rb, q), agg, f"random {mixed} {n_spans} {agg}")
+
