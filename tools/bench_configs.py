@@ -217,7 +217,8 @@ def main():
             "datapoints": int(tm.datapoints), "union_points": sum(U), "span_evaluations": evals,
             "ms_per_step": step_ms, "datapoints_per_s": tm.datapoints / (step_ms / 1000),
             "k_raw_eval_ms": eval_ms, "device_ms": sum(dv) / len(dv), "c_call_ms": sum(cc) / len(cc),
-            "step_ms_median": sorted(ms)[len(ms) // 2],
+            "step_ms_median": sorted(ms)[len(ms) // 2], "steps_ms": [round(x, 2) for x in ms],
+            "device_steps_ms": [round(x, 2) for x in dv],
             "span_evaluations_per_s": evals / (eval_ms / 1000) if eval_ms > 0 else None,
             "gen_s": gen_s, "load_s": load_s,
         }
