@@ -1468,11 +1468,11 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   // device copies of one chunk of the scan and per-column / per-row scratch (freed at the end)
   DevBuf d_rcp, d_cqo, d_cvo, d_cts, d_q, d_v, d_crow, d_cn, d_coff, d_cinfo, d_rheap, d_rone, d_rerr;
   DevBuf d_key, d_key2, d_idx, d_idx2, d_ecol, d_eqo, d_evo, d_klen, d_sq, d_sv, d_sc, d_sm;
-  DevBuf d_rlo, d_rq, d_rv, d_rstate, d_rmeta, d_rdq, d_rdv, d_raw, d_bad, d_rmax;
+  DevBuf d_rlo, d_rq, d_rv, d_rstate, d_rmeta, d_rdq, d_rdv, d_raw, d_bad, d_rmax, d_klist;
   auto release_all = [&]() {
     for (DevBuf* b : {&d_rcp, &d_cqo, &d_cvo, &d_cts, &d_q, &d_v, &d_crow, &d_cn, &d_coff, &d_cinfo, &d_rheap, &d_rone,
                       &d_rerr, &d_key, &d_key2, &d_idx, &d_idx2, &d_ecol, &d_eqo, &d_evo, &d_klen, &d_sq, &d_sv,
-                      &d_sc, &d_sm, &d_rlo, &d_rq, &d_rv, &d_rstate, &d_rmeta, &d_rdq, &d_rdv, &d_raw, &d_bad, &d_rmax})
+                      &d_sc, &d_sm, &d_rlo, &d_rq, &d_rv, &d_rstate, &d_rmeta, &d_rdq, &d_rdv, &d_raw, &d_bad, &d_rmax, &d_klist})
       b->release();
   };
   struct Rel { std::function<void()> f; ~Rel() { f(); } } rel{release_all};
@@ -1486,7 +1486,7 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   // chunks sizes every chunk, then recomputes each one before writing it: both passes count.
   double cmp_ms = 0;
   HIP_OK(d_bad.ensure(4));
-  HIP_OK(d_rmax.ensure(8));
+  HIP_OK(d_rmax.ensure(16));
   // the per-row LDS path (k_cmp_row) when every row of a chunk fits one block; else the global
   // sort (TSDBHIP_CMP_ROWS=0 forces the latter)
   const char* rows_env = std::getenv("TSDBHIP_CMP_ROWS");
@@ -1571,7 +1571,10 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
       HIP_OK(he);
     }
     if (row_cap[k]) {
-      HIP_OK(cmp_rows_fused(p, row_cap[k], false, st));
+      HIP_OK(d_rlo.ensure(r1c * 8));
+      HIP_OK(d_klist.ensure(std::max<int64_t>(1, n_ent) * 16));
+      p.row_lo = d_rlo.as<int64_t>();
+      HIP_OK(cmp_rows_fused(p, d_klist.p, row_cap[k], false, st));
     } else {
     const int64_t E1 = std::max<int64_t>(1, n_ent);
     HIP_OK(d_key.ensure(E1 * 8));
@@ -1628,7 +1631,7 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     p.out_q = c->qual.as<uint8_t>();
     p.out_v = c->val.as<uint8_t>();
     HIP_OK(hipEventRecord(c->ev[3], st));
-    if (row_cap[k]) HIP_OK(cmp_rows_fused(p, row_cap[k], true, st));
+    if (row_cap[k]) HIP_OK(cmp_rows_fused(p, d_klist.p, row_cap[k], true, st));
     else HIP_OK(cmp_write(p, st));
     HIP_OK(hipEventRecord(c->ev[1], st));
     HIP_OK(hipStreamSynchronize(st));

@@ -390,11 +390,12 @@ struct CmpParams {
 hipError_t cmp_analyze(CmpParams& p, void** tmp, size_t* tmp_bytes, hipStream_t s);   // through k_cmp_cols, col_off
 hipError_t cmp_entries(CmpParams& p, void** tmp, size_t* tmp_bytes, int end_bit, hipStream_t s);   // explode, sort, dedup, scans, rows
 hipError_t cmp_write(const CmpParams& p, hipStream_t s);
-// The per-row path (k_cmp_row): every row's datapoints sorted, deduplicated and written by one
-// block in LDS, no global entry arrays.  cmp_row_cap: the largest row's datapoints / columns of
-// the chunk (after cmp_analyze) -> the LDS capacity to launch with, 0 when a row does not fit.
-int cmp_row_cap(const CmpParams& p, uint32_t* scratch2, hipStream_t s, hipError_t* err);
-hipError_t cmp_rows_fused(const CmpParams& p, int cap, bool write, hipStream_t s);   // sizes (write=false) or bytes
+// The per-row path (k_cmp_row / k_cmp_rowwrite): every row's datapoints sorted and deduplicated
+// by one block in LDS, the kept ones listed (16 B each, klist: n_ent entries) and written after
+// the host layout.  cmp_row_cap: the largest row's datapoints / columns / bytes of the chunk
+// (after cmp_analyze) -> the LDS capacity to launch with, 0 when a row does not fit.
+int cmp_row_cap(const CmpParams& p, uint32_t* scratch3, hipStream_t s, hipError_t* err);
+hipError_t cmp_rows_fused(const CmpParams& p, void* klist, int cap, bool write, hipStream_t s);   // sizes or bytes
 // dst = src - base over n offsets (a chunk of the scan, rebased); *bad |= 1 unless non-decreasing and >= base
 hipError_t cmp_rebase(const uint64_t* src, uint64_t* dst, int64_t n, uint64_t base, int32_t* bad, hipStream_t s);
 

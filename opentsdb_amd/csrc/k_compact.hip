@@ -426,57 +426,52 @@ hipError_t cmp_write(const CmpParams& p, hipStream_t s) {
 
 // ---- the per-row path ----------------------------------------------------------------------
 // A scan row holds at most a few thousand datapoints (3600 a second-resolution hour), so one
-// 256-thread block takes a whole row: its columns' datapoints are exploded into LDS as
-// (offset ms << 12 | entry) keys -- the entry ordinal keeps scan order among equal offsets, as
-// the global sort's stability does -- bitonic-sorted there, deduplicated run by run (the heap's
-// newest-column rule, append repeats, the duplicate check), prefix-summed, and (second launch,
-// after the host layout) written as the compacted cell.  No per-datapoint arrays go through
-// HBM: the sizing pass reads the columns, the write pass reads them again and writes the cell.
+// block takes a whole row.  Sizing pass (k_cmp_row): its columns' datapoints are exploded into
+// LDS -- sort key (offset ms << 12 | entry; the entry ordinal keeps scan order among equal
+// offsets, as the global sort's stability does) and everything later steps need (source
+// offsets, lengths, fixup / append flags, column) -- bitonic-sorted there, deduplicated run by
+// run (a run of one offset is the common case and touches no global memory; longer runs apply
+// the heap's newest-column rule, append repeats and the duplicate check), prefix-summed; the
+// row's sizes go to the host and its kept datapoints, in output order with their source and
+// destination offsets, to a list (16 B each).  Write pass (k_cmp_rowwrite, after the host
+// layout): one block per row streams its list and copies the bytes.
 constexpr int CMP_ROW_CAP = 4096;   // datapoints per row (12 bits of the key)
-constexpr int CMP_ROW_THREADS = 256;
+constexpr int CMP_ROW_THREADS = 1024;
+constexpr uint64_t CMP_KEPT = 1ULL << 62;   // in a sorted key: the datapoint is kept
 
 __global__ __launch_bounds__(256) void k_cmp_rowmax(CmpParams p, uint32_t* out) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t n = 0, nc = 0;
+  uint32_t n = 0, nc = 0, span = 0;
   if (r < p.n_rows) {
     const int64_t c0 = p.row_col_ptr[r], c1 = p.row_col_ptr[r + 1];
     const int64_t e = p.col_off[c1] - p.col_off[c0];
+    const uint64_t qs = p.col_qo[c1] - p.col_qo[c0], vs = p.col_vo[c1] - p.col_vo[c0];
     n = (uint32_t)min<int64_t>(e, 0xFFFFFFFFll);
     nc = (uint32_t)min<int64_t>(c1 - c0, 0xFFFFFFFFll);
+    span = (uint32_t)min<uint64_t>(max(qs, vs), 0xFFFFFFFFull);
   }
   for (int o = 32; o > 0; o >>= 1) {
     n = max(n, (uint32_t)__shfl_xor((int)n, o));
     nc = max(nc, (uint32_t)__shfl_xor((int)nc, o));
+    span = max(span, (uint32_t)__shfl_xor((int)span, o));
   }
   if ((threadIdx.x & 63) == 0) {
     atomicMax(&out[0], n);
     atomicMax(&out[1], nc);
+    atomicMax(&out[2], span);
   }
 }
 
-__device__ __forceinline__ CmpEnt row_ent(const CmpParams& p, int64_t c, uint32_t qpos, uint32_t vpos) {
-  CmpEnt r;
-  const uint32_t info = p.col_info[c];
-  const uint8_t* vb = p.v + p.col_vo[c];
-  r.fix = false;
-  r.fixed_q1 = 0;
-  if ((info & 3) == CMP_APPEND) {
-    r.qp = vb + qpos;
-  } else {
-    r.qp = p.q + p.col_qo[c] + qpos;
-    if (p.col_qo[c + 1] - p.col_qo[c] == 2 && (info & 8)) { r.fix = true; r.fixed_q1 = (uint8_t)(info >> 8); }
-  }
-  r.eq = cmp_in_ms(r.qp[0]) ? 4 : 2;
-  const uint8_t fl = r.fix ? r.fixed_q1 : r.qp[r.eq - 1];
-  r.evl = (fl & 7) + 1;
-  r.vp = vb + vpos;
-  return r;
-}
+// per-entry flags in LDS: bit0 ms (4-byte qualifier), bits1-3 value length - 1, bit4 the
+// 2-byte qualifier's flags byte is fixed up, bit5 append column (qualifier inside the value)
+__device__ __forceinline__ int em_eq(uint32_t em) { return (em & 1) ? 4 : 2; }
+__device__ __forceinline__ int em_evl(uint32_t em) { return (int)((em >> 1) & 7) + 1; }
 
-// block-wide exclusive scan of one int per thread (LDS scratch of 256 + 1 ints); returns the
-// thread's offset, *total = the block's sum
+// block-wide exclusive scan of one int per thread (LDS scratch of >= 16 + 1 ints); returns
+// the thread's offset, *total = the block's sum
 __device__ __forceinline__ int block_excl_scan(int x, int* sh, int* total) {
   const int t = threadIdx.x;
+  const int nw = (int)(blockDim.x >> 6);
   int v = x;
   const int lane = t & 63;
   for (int o = 1; o < 64; o <<= 1) {   // inclusive wave scan
@@ -485,76 +480,84 @@ __device__ __forceinline__ int block_excl_scan(int x, int* sh, int* total) {
   }
   if (lane == 63) sh[t >> 6] = v;
   __syncthreads();
-  int base = 0;
-  for (int w = 0; w < (t >> 6); w++) base += sh[w];
-  const int all = sh[0] + sh[1] + sh[2] + sh[3];
+  int base = 0, all = 0;
+  for (int w = 0; w < nw; w++) {
+    const int sw = sh[w];
+    base += w < (t >> 6) ? sw : 0;
+    all += sw;
+  }
   __syncthreads();
   *total = all;
   return base + v - x;
 }
 
-template <bool WRITE>
-__global__ __launch_bounds__(256) void k_cmp_row(CmpParams p, int P) {
+// kept datapoint of a row, in output order (the write pass's input)
+struct CmpKept {
+  uint32_t qsrc;   // qualifier source, from the row's first column's qualifier (append: value) bytes
+  uint32_t vsrc;   // value source, from the row's first column's value bytes
+  uint32_t qdst;   // destination offset in the compacted qualifier << 8 | em
+  uint32_t vdst;   // destination offset in the compacted value
+};
+
+__global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_row(CmpParams p, CmpKept* klist, int P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
-  uint64_t* key = reinterpret_cast<uint64_t*>(sm);     // [P] sorted keys
-  uint16_t* ecol = reinterpret_cast<uint16_t*>(key + P);   // [P] by entry: column - c0
-  uint16_t* eqo = ecol + P;                            //          qualifier position in the column
-  uint16_t* evo = eqo + P;                             //          value position
-  uint16_t* kin = evo + P;                             // [P] by sorted position: kept | ms | eq | evl
-  __shared__ int scan_sh[8];
+  uint64_t* key = reinterpret_cast<uint64_t*>(sm);       // [P] sorted keys
+  uint32_t* eq_src = reinterpret_cast<uint32_t*>(key + P);   // [P] by entry: qualifier source (row-relative)
+  uint32_t* ev_src = eq_src + P;                         //          value source
+  uint16_t* eem = reinterpret_cast<uint16_t*>(ev_src + P);   //          flags (em_*)
+  uint16_t* ecol = eem + P;                              //          column - c0
+  __shared__ int scan_sh[CMP_ROW_THREADS / 64];
   __shared__ int dup_err;   // a duplicate with different bytes in this row (the global flag may be stale in L1)
   const int64_t r = blockIdx.x;
   const int t = threadIdx.x;
   if (t == 0) dup_err = 0;
-  if (WRITE) {
-    if (p.row_dq[r] < 0 || p.row_state[r] == 0) return;
-    if (p.row_state[r] == 2) {   // the single column as stored (noMergesOrFixups)
-      const int64_t c = p.row_one[r];
-      const uint8_t* qs = p.q + p.col_qo[c];
-      const uint8_t* vs = p.v + p.col_vo[c];
-      for (int64_t b = t; b < p.row_q[r]; b += CMP_ROW_THREADS) p.out_q[p.row_dq[r] + b] = qs[b];
-      for (int64_t b = t; b < p.row_v[r]; b += CMP_ROW_THREADS) p.out_v[p.row_dv[r] + b] = vs[b];
-      return;
-    }
-  } else {
-    // k_cmp_rows' verdicts that need no datapoint
-    if (p.row_err[r] || p.row_heap[r] == 0) {
-      if (t == 0) { p.row_state[r] = 0; p.row_q[r] = p.row_v[r] = 0; p.row_meta[r] = 0; }
-      return;
-    }
-    if (p.row_heap[r] == 1) {
-      const int64_t c = p.row_one[r];
-      const uint32_t info = p.col_info[c];
-      const int64_t ql = (int64_t)(p.col_qo[c + 1] - p.col_qo[c]);
-      if ((info & 3) == CMP_DATA && !(info & 8) && (ql == 2 || (ql == 4 && cmp_in_ms(p.q[p.col_qo[c]])))) {
-        if (t == 0) {
-          p.row_state[r] = 2;
-          p.row_q[r] = ql;
-          p.row_v[r] = (int64_t)(p.col_vo[c + 1] - p.col_vo[c]);
-          p.row_meta[r] = 0;
-        }
-        return;
+  // k_cmp_rows' verdicts that need no datapoint
+  if (p.row_err[r] || p.row_heap[r] == 0) {
+    if (t == 0) { p.row_state[r] = 0; p.row_q[r] = p.row_v[r] = 0; p.row_meta[r] = 0; p.row_lo[r] = 0; }
+    return;
+  }
+  if (p.row_heap[r] == 1) {
+    const int64_t c = p.row_one[r];
+    const uint32_t info = p.col_info[c];
+    const int64_t ql = (int64_t)(p.col_qo[c + 1] - p.col_qo[c]);
+    if ((info & 3) == CMP_DATA && !(info & 8) && (ql == 2 || (ql == 4 && cmp_in_ms(p.q[p.col_qo[c]])))) {
+      if (t == 0) {   // noMergesOrFixups: the single column as stored
+        p.row_state[r] = 2;
+        p.row_q[r] = ql;
+        p.row_v[r] = (int64_t)(p.col_vo[c + 1] - p.col_vo[c]);
+        p.row_meta[r] = 0;
+        p.row_lo[r] = 0;
       }
+      return;
     }
   }
   const int64_t c0 = p.row_col_ptr[r], c1 = p.row_col_ptr[r + 1];
   const int64_t e0 = p.col_off[c0];
   const int n = (int)(p.col_off[c1] - e0);
+  const uint64_t qb = p.col_qo[c0], vb = p.col_vo[c0];
+  const uint8_t* qrow = p.q + qb;
+  const uint8_t* vrow = p.v + vb;
   // explode: one thread per column
   for (int64_t c = c0 + t; c < c1; c += CMP_ROW_THREADS) {
-    if (p.col_n[c] == 0) continue;
+    const int64_t nc_ = p.col_n[c];
+    if (nc_ == 0) continue;
     int e = (int)(p.col_off[c] - e0);
     const uint64_t qo = p.col_qo[c], vo = p.col_vo[c];
     const int64_t ql = (int64_t)(p.col_qo[c + 1] - qo), vl = (int64_t)(p.col_vo[c + 1] - vo);
     const uint32_t info = p.col_info[c];
-    auto put = [&](int64_t qpos, int64_t vpos, int, int, uint32_t off) {
+    const bool app = (info & 3) == CMP_APPEND;
+    const bool fix = !app && ql == 2 && (info & 8);
+    const uint32_t qbase = (uint32_t)((app ? vo - vb : qo - qb));
+    const uint32_t vbase = (uint32_t)(vo - vb);
+    auto put = [&](int64_t qpos, int64_t vpos, int eq, int evl, uint32_t off) {
       key[e] = ((uint64_t)off << 12) | (uint64_t)e;
+      eq_src[e] = qbase + (uint32_t)qpos;
+      ev_src[e] = vbase + (uint32_t)vpos;
+      eem[e] = (uint16_t)((eq == 4 ? 1u : 0u) | ((uint32_t)(evl - 1) << 1) | (fix ? 16u : 0u) | (app ? 32u : 0u));
       ecol[e] = (uint16_t)(c - c0);
-      eqo[e] = (uint16_t)qpos;
-      evo[e] = (uint16_t)vpos;
       e++;
     };
-    if ((info & 3) == CMP_APPEND) {
+    if (app) {
       walk_append(p.v + vo, vl, put);
     } else {
       const int64_t vstart = (info & 4) ? 4 : 0;
@@ -562,7 +565,7 @@ __global__ __launch_bounds__(256) void k_cmp_row(CmpParams p, int P) {
                 [&](int64_t qi, int64_t vi, int eq, int evl, uint32_t off) { put(qi, vstart + vi, eq, evl, off); });
     }
   }
-  for (int i = n + t; i < P; i += CMP_ROW_THREADS) key[i] = ~0ull;
+  for (int i = n + t; i < P; i += CMP_ROW_THREADS) key[i] = ~0ull >> 2;   // above every key, kept bit clear
   __syncthreads();
   // bitonic sort of the P keys (unique: the entry ordinal is in the low bits)
   for (int k = 2; k <= P; k <<= 1)
@@ -578,37 +581,40 @@ __global__ __launch_bounds__(256) void k_cmp_row(CmpParams p, int P) {
       }
       __syncthreads();
     }
-  // runs of one offset: the newest column's datapoint is kept (k_cmp_dedup's rules)
+  // runs of one offset: a single datapoint is kept as is; of several, the newest column's
+  // (k_cmp_dedup's rules)
   for (int i = t; i < n; i += CMP_ROW_THREADS) {
     const uint64_t off = key[i] >> 12;
     if (i > 0 && (key[i - 1] >> 12) == off) continue;
     int j = i + 1;
     while (j < n && (key[j] >> 12) == off) j++;
-    auto col_of = [&](int s) { return c0 + (int64_t)ecol[key[s] & 4095]; };
+    if (j == i + 1) {
+      key[i] |= CMP_KEPT;
+      continue;
+    }
+    auto ent = [&](int s) { return (int)(key[s] & 4095); };
     auto superseded = [&](int s) {
-      const int64_t c = col_of(s);
-      return (p.col_info[c] & 3) == CMP_APPEND && s + 1 < j && col_of(s + 1) == c;
+      const int es = ent(s);
+      return (eem[es] & 32) && s + 1 < j && ecol[ent(s + 1)] == ecol[es];
     };
     int best = -1;
     int64_t best_ts = 0;
     for (int s = i; s < j; s++) {
       if (superseded(s)) continue;
-      const int64_t ts = p.col_ts ? p.col_ts[col_of(s)] : 0;
+      const int64_t ts = p.col_ts ? p.col_ts[c0 + ecol[ent(s)]] : 0;
       if (best < 0 || ts > best_ts) { best = s; best_ts = ts; }
     }
-    const int eb = (int)(key[best] & 4095);
-    const CmpEnt kb = row_ent(p, col_of(best), eqo[eb], evo[eb]);
+    key[best] |= CMP_KEPT;
+    if (p.fix_dup) continue;
+    const int eb = ent(best);
+    const int lb = em_evl(eem[eb]);
+    const uint8_t* vk = vrow + ev_src[eb];
     for (int s = i; s < j; s++) {
-      if (s == best) {
-        kin[s] = (uint16_t)(1u | ((kb.eq == 4 ? 1u : 0u) << 1) | ((uint32_t)kb.eq << 2) | ((uint32_t)kb.evl << 5));
-        continue;
-      }
-      kin[s] = 0;
-      if (WRITE || superseded(s) || p.fix_dup) continue;
-      const int es = (int)(key[s] & 4095);
-      const CmpEnt o = row_ent(p, col_of(s), eqo[es], evo[es]);   // getCopyOfCurrentValue vs the kept one
-      bool same = o.evl == kb.evl;
-      for (int b = 0; same && b < o.evl; b++) same = o.vp[b] == kb.vp[b];
+      if (s == best || superseded(s)) continue;
+      const int es = ent(s);   // getCopyOfCurrentValue vs the kept one
+      bool same = em_evl(eem[es]) == lb;
+      const uint8_t* vo = vrow + ev_src[es];
+      for (int b = 0; same && b < lb; b++) same = vo[b] == vk[b];
       if (!same) {
         cmp_fail(p.row_err, r, TSDB_E_ILLEGAL_DATA);
         dup_err = 1;
@@ -617,77 +623,113 @@ __global__ __launch_bounds__(256) void k_cmp_row(CmpParams p, int P) {
   }
   __syncthreads();
   // each thread a contiguous run of m sorted positions: its kept bytes / datapoints, then the
-  // block's exclusive offsets
+  // block's exclusive offsets, then the thread's list records
   const int m = P / CMP_ROW_THREADS > 0 ? P / CMP_ROW_THREADS : 1;
   const int a0 = t * m, a1 = min(n, a0 + m);
   int sq = 0, sv = 0, sc = 0, sms = 0;
   for (int i = a0; i < a1; i++) {
-    const uint32_t x = kin[i];
-    if (!(x & 1)) continue;
-    sq += (x >> 2) & 7;
-    sv += (x >> 5) & 15;
+    const uint64_t kk = key[i];
+    if (!(kk & CMP_KEPT)) continue;
+    const uint32_t em = eem[kk & 4095];
+    sq += em_eq(em);
+    sv += em_evl(em);
     sc++;
-    sms += (x >> 1) & 1;
+    sms += em & 1;
   }
   int tq, tv, tc, tm;
   int oq = block_excl_scan(sq, scan_sh, &tq);
   int ov = block_excl_scan(sv, scan_sh, &tv);
-  block_excl_scan(sc, scan_sh, &tc);
+  int oc = block_excl_scan(sc, scan_sh, &tc);
   block_excl_scan(sms, scan_sh, &tm);
-  if (!WRITE) {
-    if (t == 0) {
-      if (dup_err) {
-        p.row_state[r] = 0;
-        p.row_q[r] = p.row_v[r] = 0;
-        p.row_meta[r] = 0;
-      } else {
-        p.row_state[r] = tc ? 1 : 0;
-        p.row_q[r] = tc ? tq : 0;
-        p.row_v[r] = tc ? tv + (tc > 1 ? 1 : 0) : 0;
-        p.row_meta[r] = (tm > 0 && tm < tc) ? 1 : 0;   // Const.MS_MIXED_COMPACT
-      }
-    }
+  if (dup_err) {
+    if (t == 0) { p.row_state[r] = 0; p.row_q[r] = p.row_v[r] = 0; p.row_meta[r] = 0; p.row_lo[r] = 0; }
     return;
   }
-  uint8_t* dq = p.out_q + p.row_dq[r];
-  uint8_t* dv = p.out_v + p.row_dv[r];
+  CmpKept* out = klist + e0;
   for (int i = a0; i < a1; i++) {
-    const uint32_t x = kin[i];
-    if (!(x & 1)) continue;
-    const int e = (int)(key[i] & 4095);
-    const CmpEnt en = row_ent(p, c0 + (int64_t)ecol[e], eqo[e], evo[e]);
-    for (int b = 0; b < en.eq; b++) dq[oq + b] = (en.fix && b == 1) ? en.fixed_q1 : en.qp[b];
-    for (int b = 0; b < en.evl; b++) dv[ov + b] = en.vp[b];
-    oq += en.eq;
-    ov += en.evl;
+    const uint64_t kk = key[i];
+    if (!(kk & CMP_KEPT)) continue;
+    const int e = (int)(kk & 4095);
+    const uint32_t em = eem[e];
+    out[oc] = CmpKept{eq_src[e], ev_src[e], ((uint32_t)oq << 8) | em, (uint32_t)ov};
+    oq += em_eq(em);
+    ov += em_evl(em);
+    oc++;
   }
-  if (t == 0 && tc > 1) dv[p.row_v[r] - 1] = p.row_meta[r];
+  if (t == 0) {
+    p.row_state[r] = tc ? 1 : 0;
+    p.row_q[r] = tc ? tq : 0;
+    p.row_v[r] = tc ? tv + (tc > 1 ? 1 : 0) : 0;
+    p.row_meta[r] = (tm > 0 && tm < tc) ? 1 : 0;   // Const.MS_MIXED_COMPACT
+    p.row_lo[r] = tc;                               // kept datapoints (list length)
+  }
 }
 
-int cmp_row_cap(const CmpParams& p, uint32_t* scratch2, hipStream_t s, hipError_t* err) {
+// the compacted cell of each row at the host's layout, from the sizing pass's list
+__global__ __launch_bounds__(256) void k_cmp_rowwrite(CmpParams p, const CmpKept* klist) {
+  const int64_t r = blockIdx.x;
+  const int t = threadIdx.x;
+  if (p.row_dq[r] < 0 || p.row_state[r] == 0) return;
+  const int64_t c0 = p.row_col_ptr[r];
+  uint8_t* dq = p.out_q + p.row_dq[r];
+  uint8_t* dv = p.out_v + p.row_dv[r];
+  if (p.row_state[r] == 2) {   // the single column as stored (noMergesOrFixups)
+    const int64_t c = p.row_one[r];
+    const uint8_t* qs = p.q + p.col_qo[c];
+    const uint8_t* vs = p.v + p.col_vo[c];
+    for (int64_t b = t; b < p.row_q[r]; b += 256) dq[b] = qs[b];
+    for (int64_t b = t; b < p.row_v[r]; b += 256) dv[b] = vs[b];
+    return;
+  }
+  const uint8_t* qrow = p.q + p.col_qo[c0];
+  const uint8_t* vrow = p.v + p.col_vo[c0];
+  const CmpKept* list = klist + p.col_off[c0];
+  const int64_t nk = p.row_lo[r];
+  for (int64_t i = t; i < nk; i += 256) {
+    const CmpKept k = list[i];
+    const uint32_t em = k.qdst & 255;
+    const int eq = em_eq(em), evl = em_evl(em);
+    const uint8_t* qs = ((em & 32) ? vrow : qrow) + k.qsrc;
+    uint8_t* qd = dq + (k.qdst >> 8);
+    qd[0] = qs[0];
+    qd[1] = (em & 16) ? (uint8_t)((qs[1] & 0xF8) | (evl - 1)) : qs[1];   // checkForFixup's flags
+    if (eq == 4) {
+      qd[2] = qs[2];
+      qd[3] = qs[3];
+    }
+    const uint8_t* vs = vrow + k.vsrc;
+    uint8_t* vd = dv + k.vdst;
+    for (int b = 0; b < evl; b++) vd[b] = vs[b];
+  }
+  if (t == 0 && nk > 1) dv[p.row_v[r] - 1] = p.row_meta[r];
+}
+
+int cmp_row_cap(const CmpParams& p, uint32_t* scratch3, hipStream_t s, hipError_t* err) {
   *err = hipSuccess;
   if (p.n_rows <= 0) return 64;
-  if ((*err = hipMemsetAsync(scratch2, 0, 8, s)) != hipSuccess) return 0;
-  hipLaunchKernelGGL(k_cmp_rowmax, dim3(blocks_of(p.n_rows)), dim3(256), 0, s, p, scratch2);
-  uint32_t h[2] = {0, 0};
-  if ((*err = hipMemcpyAsync(h, scratch2, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return 0;
+  if ((*err = hipMemsetAsync(scratch3, 0, 12, s)) != hipSuccess) return 0;
+  hipLaunchKernelGGL(k_cmp_rowmax, dim3(blocks_of(p.n_rows)), dim3(256), 0, s, p, scratch3);
+  uint32_t h[3] = {0, 0, 0};
+  if ((*err = hipMemcpyAsync(h, scratch3, 12, hipMemcpyDeviceToHost, s)) != hipSuccess) return 0;
   if ((*err = hipStreamSynchronize(s)) != hipSuccess) return 0;
-  if (h[0] > (uint32_t)CMP_ROW_CAP || h[1] > 65535u) return 0;
+  if (h[0] > (uint32_t)CMP_ROW_CAP || h[1] > 65535u || h[2] >= 0x7FFFFFFFu) return 0;
   int cap = 64;
   while (cap < (int)h[0]) cap <<= 1;
   return cap;
 }
 
-hipError_t cmp_rows_fused(const CmpParams& p, int cap, bool write, hipStream_t s) {
+hipError_t cmp_rows_fused(const CmpParams& p, void* klist, int cap, bool write, hipStream_t s) {
   if (p.n_rows <= 0) return hipSuccess;
-  const size_t lds = (size_t)cap * 16;
-  const void* fn = write ? (const void*)k_cmp_row<true> : (const void*)k_cmp_row<false>;
+  if (write) {
+    hipLaunchKernelGGL(k_cmp_rowwrite, dim3((unsigned)p.n_rows), dim3(256), 0, s, p, (const CmpKept*)klist);
+    return hipGetLastError();
+  }
+  const size_t lds = (size_t)cap * 20;
   if (lds > 65536) {
-    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const hipError_t e = hipFuncSetAttribute((const void*)k_cmp_row, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  if (write) hipLaunchKernelGGL(k_cmp_row<true>, dim3((unsigned)p.n_rows), dim3(CMP_ROW_THREADS), lds, s, p, cap);
-  else hipLaunchKernelGGL(k_cmp_row<false>, dim3((unsigned)p.n_rows), dim3(CMP_ROW_THREADS), lds, s, p, cap);
+  hipLaunchKernelGGL(k_cmp_row, dim3((unsigned)p.n_rows), dim3(CMP_ROW_THREADS), lds, s, p, (CmpKept*)klist, cap);
   return hipGetLastError();
 }
 
