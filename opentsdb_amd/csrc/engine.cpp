@@ -1492,6 +1492,7 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   const char* rows_env = std::getenv("TSDBHIP_CMP_ROWS");
   const bool rows_ok = !(rows_env && rows_env[0] == '0');
   std::vector<int> row_cap(n_chunks, 0);
+  std::vector<uint32_t> row_span(n_chunks, 0);
   // upload, analyze and build the entries of chunk k; its rows' sizes and states to the host
   auto prepare = [&](int k) -> int {
     const int64_t r0 = cuts[k], r1 = cuts[k + 1], nr = r1 - r0;
@@ -1503,8 +1504,8 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     HIP_OK(d_cqo.ensure((c1c + 1) * 8));
     HIP_OK(d_cvo.ensure((c1c + 1) * 8));
     HIP_OK(d_raw.ensure((std::max(r1c, c1c) + 1) * 8));
-    HIP_OK(d_q.ensure(std::max<uint64_t>(16, qz - qa)));
-    HIP_OK(d_v.ensure(std::max<uint64_t>(16, vz - va)));
+    HIP_OK(d_q.ensure(std::max<uint64_t>(16, qz - qa) + 16));   // (+16: dword reads past the last byte)
+    HIP_OK(d_v.ensure(std::max<uint64_t>(16, vz - va) + 16));
     if (cb->col_timestamp) HIP_OK(d_cts.ensure(c1c * 8));
     HIP_OK(hipMemsetAsync(d_bad.p, 0, 4, st));
     if (nr) {
@@ -1567,14 +1568,14 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     row_cap[k] = 0;
     if (rows_ok) {
       hipError_t he = hipSuccess;
-      row_cap[k] = cmp_row_cap(p, d_rmax.as<uint32_t>(), st, &he);
+      row_cap[k] = cmp_row_cap(p, d_rmax.as<uint32_t>(), st, &he, &row_span[k]);
       HIP_OK(he);
     }
     if (row_cap[k]) {
       HIP_OK(d_rlo.ensure(r1c * 8));
       HIP_OK(d_klist.ensure(std::max<int64_t>(1, n_ent) * 16));
       p.row_lo = d_rlo.as<int64_t>();
-      HIP_OK(cmp_rows_fused(p, d_klist.p, row_cap[k], false, st));
+      HIP_OK(cmp_rows_fused(p, d_klist.p, row_cap[k], row_span[k], false, st));
     } else {
     const int64_t E1 = std::max<int64_t>(1, n_ent);
     HIP_OK(d_key.ensure(E1 * 8));
@@ -1631,7 +1632,7 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     p.out_q = c->qual.as<uint8_t>();
     p.out_v = c->val.as<uint8_t>();
     HIP_OK(hipEventRecord(c->ev[3], st));
-    if (row_cap[k]) HIP_OK(cmp_rows_fused(p, d_klist.p, row_cap[k], true, st));
+    if (row_cap[k]) HIP_OK(cmp_rows_fused(p, d_klist.p, row_cap[k], row_span[k], true, st));
     else HIP_OK(cmp_write(p, st));
     HIP_OK(hipEventRecord(c->ev[1], st));
     HIP_OK(hipStreamSynchronize(st));

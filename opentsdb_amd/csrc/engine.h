@@ -394,8 +394,9 @@ hipError_t cmp_write(const CmpParams& p, hipStream_t s);
 // by one block in LDS, the kept ones listed (16 B each, klist: n_ent entries) and written after
 // the host layout.  cmp_row_cap: the largest row's datapoints / columns / bytes of the chunk
 // (after cmp_analyze) -> the LDS capacity to launch with, 0 when a row does not fit.
-int cmp_row_cap(const CmpParams& p, uint32_t* scratch3, hipStream_t s, hipError_t* err);
-hipError_t cmp_rows_fused(const CmpParams& p, void* klist, int cap, bool write, hipStream_t s);   // sizes or bytes
+// *span: the largest row's qualifier or value bytes (the write pass's LDS stage).
+int cmp_row_cap(const CmpParams& p, uint32_t* scratch3, hipStream_t s, hipError_t* err, uint32_t* span);
+hipError_t cmp_rows_fused(const CmpParams& p, void* klist, int cap, uint32_t span, bool write, hipStream_t s);
 // dst = src - base over n offsets (a chunk of the scan, rebased); *bad |= 1 unless non-decreasing and >= base
 hipError_t cmp_rebase(const uint64_t* src, uint64_t* dst, int64_t n, uint64_t base, int32_t* bad, hipStream_t s);
 

@@ -491,6 +491,71 @@ __device__ __forceinline__ int block_excl_scan(int x, int* sh, int* total) {
   return base + v - x;
 }
 
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int m) {
+  const int lo = __shfl_xor((int)(uint32_t)x, m, 64), hi = __shfl_xor((int)(uint32_t)(x >> 32), m, 64);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+// Bitonic sort of P = 1024 E keys by a 1024-thread block, thread t holding keys t E .. t E + E - 1
+// in registers: partners within the thread are compare-exchanged in registers, within the wave
+// through lane shuffles, and only distances of 64 E and more go through LDS (10 of the 78
+// stages for 4096 keys, each a write / barrier / read / barrier).  Element i's new value is the
+// min or the max of (i, i ^ j) as ((i & j) == 0) == ((i & k) == 0).
+template <int E>
+__device__ __forceinline__ void cmp_sort_block(uint64_t* key, int P) {
+  const int t = threadIdx.x;
+  uint64_t v[E];
+#pragma unroll
+  for (int e = 0; e < E; e++) v[e] = key[t * E + e];
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= 64 * E) {
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < E; e++) key[t * E + e] = v[e];
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+          const int i = t * E + e;
+          const uint64_t y = key[i ^ j];
+          v[e] = (((i & j) == 0) == ((i & k) == 0)) ? (v[e] < y ? v[e] : y) : (v[e] > y ? v[e] : y);
+        }
+      } else if (j >= E) {
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+          const int i = t * E + e;
+          const uint64_t y = shfl_xor_u64(v[e], j / E);
+          v[e] = (((i & j) == 0) == ((i & k) == 0)) ? (v[e] < y ? v[e] : y) : (v[e] > y ? v[e] : y);
+        }
+      } else {
+        // j < E: pairs inside the thread (static register indices)
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+          const int f = e ^ j;   // (j is 1 or 2 here; E <= 4)
+          if (E >= 2 && j == 1 && (e & 1) == 0) {
+            const bool up = ((t * E + e) & k) == 0;
+            const uint64_t a = v[e], b = v[e + 1 < E ? e + 1 : e];
+            const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+            v[e] = up ? lo : hi;
+            v[e + 1 < E ? e + 1 : e] = up ? hi : lo;
+          } else if (E >= 4 && j == 2 && (e & 2) == 0) {
+            const bool up = ((t * E + e) & k) == 0;
+            const uint64_t a = v[e], b = v[e + 2 < E ? e + 2 : e];
+            const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+            v[e] = up ? lo : hi;
+            v[e + 2 < E ? e + 2 : e] = up ? hi : lo;
+          }
+          (void)f;
+        }
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < E; e++) key[t * E + e] = v[e];
+  __syncthreads();
+}
+
 // kept datapoint of a row, in output order (the write pass's input)
 struct CmpKept {
   uint32_t qsrc;   // qualifier source, from the row's first column's qualifier (append: value) bytes
@@ -567,20 +632,31 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_row(CmpParams p, CmpKep
   }
   for (int i = n + t; i < P; i += CMP_ROW_THREADS) key[i] = ~0ull >> 2;   // above every key, kept bit clear
   __syncthreads();
-  // bitonic sort of the P keys (unique: the entry ordinal is in the low bits)
-  for (int k = 2; k <= P; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = t; i < P / 2; i += CMP_ROW_THREADS) {
-        const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));
-        const int hi = lo + j;
-        const uint64_t x = key[lo], y = key[hi];
-        if ((x > y) == ((lo & k) == 0)) {
-          key[lo] = y;
-          key[hi] = x;
+  // sort the P keys (unique: the entry ordinal is in the low bits) unless the columns came in
+  // time order already -- an HBase scan returns a row's columns sorted by qualifier, which is
+  // time order for second qualifiers
+  int unsorted = 0;
+  for (int i = t + 1; i < n; i += CMP_ROW_THREADS) unsorted |= key[i - 1] > key[i] ? 1 : 0;
+  if (__syncthreads_or(unsorted)) {
+    if (P == 4096) cmp_sort_block<4>(key, P);
+    else if (P == 2048) cmp_sort_block<2>(key, P);
+    else if (P == 1024) cmp_sort_block<1>(key, P);
+    else {
+      for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          for (int i = t; i < P / 2; i += CMP_ROW_THREADS) {
+            const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));
+            const int hi = lo + j;
+            const uint64_t x = key[lo], y = key[hi];
+            if ((x > y) == ((lo & k) == 0)) {
+              key[lo] = y;
+              key[hi] = x;
+            }
+          }
+          __syncthreads();
         }
-      }
-      __syncthreads();
     }
+  }
   // runs of one offset: a single datapoint is kept as is; of several, the newest column's
   // (k_cmp_dedup's rules)
   for (int i = t; i < n; i += CMP_ROW_THREADS) {
@@ -665,46 +741,80 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_row(CmpParams p, CmpKep
   }
 }
 
-// the compacted cell of each row at the host's layout, from the sizing pass's list
-__global__ __launch_bounds__(256) void k_cmp_rowwrite(CmpParams p, const CmpKept* klist) {
+// The compacted cell of each row at the host's layout, from the sizing pass's list.  The row's
+// source bytes (its columns' qualifiers and values, contiguous) are staged in LDS with dword
+// loads when they fit, the cell is assembled in LDS byte by byte, and leaves in dwords (the
+// destination rows are 16-byte aligned).  Rows whose sources do not fit read them from HBM.
+__global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_rowwrite(CmpParams p, const CmpKept* klist, int oq_cap,
+                                                                  int ov_cap, int src_cap) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smw[];
+  uint8_t* oq = reinterpret_cast<uint8_t*>(smw);
+  uint8_t* ov = oq + oq_cap;
+  uint32_t* srcw = reinterpret_cast<uint32_t*>(ov + ov_cap);
   const int64_t r = blockIdx.x;
   const int t = threadIdx.x;
+  const int nt = CMP_ROW_THREADS;
   if (p.row_dq[r] < 0 || p.row_state[r] == 0) return;
-  const int64_t c0 = p.row_col_ptr[r];
   uint8_t* dq = p.out_q + p.row_dq[r];
   uint8_t* dv = p.out_v + p.row_dv[r];
+  const int64_t c0 = p.row_col_ptr[r], c1 = p.row_col_ptr[r + 1];
   if (p.row_state[r] == 2) {   // the single column as stored (noMergesOrFixups)
     const int64_t c = p.row_one[r];
     const uint8_t* qs = p.q + p.col_qo[c];
     const uint8_t* vs = p.v + p.col_vo[c];
-    for (int64_t b = t; b < p.row_q[r]; b += 256) dq[b] = qs[b];
-    for (int64_t b = t; b < p.row_v[r]; b += 256) dv[b] = vs[b];
+    for (int64_t b = t; b < p.row_q[r]; b += nt) dq[b] = qs[b];
+    for (int64_t b = t; b < p.row_v[r]; b += nt) dv[b] = vs[b];
     return;
   }
-  const uint8_t* qrow = p.q + p.col_qo[c0];
-  const uint8_t* vrow = p.v + p.col_vo[c0];
+  const uint64_t qb = p.col_qo[c0], vb = p.col_vo[c0];
+  const uint64_t qspan = p.col_qo[c1] - qb, vspan = p.col_vo[c1] - vb;
+  // dword windows over the sources: [qa, qa + 4 nqw) then [va, va + 4 nvw)
+  const uint64_t qa = qb & ~3ull, va = vb & ~3ull;
+  const int64_t nqw = (int64_t)((qb + qspan - qa + 3) / 4), nvw = (int64_t)((vb + vspan - va + 3) / 4);
+  const bool staged = (nqw + nvw) * 4 <= src_cap;
+  const int64_t nq = p.row_q[r], nv = p.row_v[r];
+  const int64_t nqd = (nq + 3) / 4, nvd = (nv + 3) / 4;
+  uint32_t* oqw = reinterpret_cast<uint32_t*>(oq);
+  uint32_t* ovw = reinterpret_cast<uint32_t*>(ov);
+  for (int64_t w = t; w < nqd; w += nt) oqw[w] = 0;
+  for (int64_t w = t; w < nvd; w += nt) ovw[w] = 0;
+  if (staged) {
+    const uint32_t* gq = reinterpret_cast<const uint32_t*>(p.q + qa);
+    const uint32_t* gv = reinterpret_cast<const uint32_t*>(p.v + va);
+    for (int64_t w = t; w < nqw; w += nt) srcw[w] = gq[w];
+    for (int64_t w = t; w < nvw; w += nt) srcw[nqw + w] = gv[w];
+  }
+  __syncthreads();
+  const uint8_t* sq = staged ? reinterpret_cast<const uint8_t*>(srcw) + (qb - qa) : p.q + qb;
+  const uint8_t* sv = staged ? reinterpret_cast<const uint8_t*>(srcw + nqw) + (vb - va) : p.v + vb;
   const CmpKept* list = klist + p.col_off[c0];
   const int64_t nk = p.row_lo[r];
-  for (int64_t i = t; i < nk; i += 256) {
+  for (int64_t i = t; i < nk; i += nt) {
     const CmpKept k = list[i];
     const uint32_t em = k.qdst & 255;
     const int eq = em_eq(em), evl = em_evl(em);
-    const uint8_t* qs = ((em & 32) ? vrow : qrow) + k.qsrc;
-    uint8_t* qd = dq + (k.qdst >> 8);
+    const uint8_t* qs = ((em & 32) ? sv : sq) + k.qsrc;
+    uint8_t* qd = oq + (k.qdst >> 8);
     qd[0] = qs[0];
     qd[1] = (em & 16) ? (uint8_t)((qs[1] & 0xF8) | (evl - 1)) : qs[1];   // checkForFixup's flags
     if (eq == 4) {
       qd[2] = qs[2];
       qd[3] = qs[3];
     }
-    const uint8_t* vs = vrow + k.vsrc;
-    uint8_t* vd = dv + k.vdst;
+    const uint8_t* vs = sv + k.vsrc;
+    uint8_t* vd = ov + k.vdst;
     for (int b = 0; b < evl; b++) vd[b] = vs[b];
   }
-  if (t == 0 && nk > 1) dv[p.row_v[r] - 1] = p.row_meta[r];
+  __syncthreads();
+  if (t == 0 && nk > 1) ov[nv - 1] = p.row_meta[r];
+  __syncthreads();
+  uint32_t* dqw = reinterpret_cast<uint32_t*>(dq);
+  uint32_t* dvw = reinterpret_cast<uint32_t*>(dv);
+  for (int64_t w = t; w < nqd; w += nt) dqw[w] = oqw[w];
+  for (int64_t w = t; w < nvd; w += nt) dvw[w] = ovw[w];
 }
 
-int cmp_row_cap(const CmpParams& p, uint32_t* scratch3, hipStream_t s, hipError_t* err) {
+int cmp_row_cap(const CmpParams& p, uint32_t* scratch3, hipStream_t s, hipError_t* err, uint32_t* span) {
   *err = hipSuccess;
   if (p.n_rows <= 0) return 64;
   if ((*err = hipMemsetAsync(scratch3, 0, 12, s)) != hipSuccess) return 0;
@@ -713,15 +823,23 @@ int cmp_row_cap(const CmpParams& p, uint32_t* scratch3, hipStream_t s, hipError_
   if ((*err = hipMemcpyAsync(h, scratch3, 12, hipMemcpyDeviceToHost, s)) != hipSuccess) return 0;
   if ((*err = hipStreamSynchronize(s)) != hipSuccess) return 0;
   if (h[0] > (uint32_t)CMP_ROW_CAP || h[1] > 65535u || h[2] >= 0x7FFFFFFFu) return 0;
+  *span = h[2];
   int cap = 64;
   while (cap < (int)h[0]) cap <<= 1;
   return cap;
 }
 
-hipError_t cmp_rows_fused(const CmpParams& p, void* klist, int cap, bool write, hipStream_t s) {
+hipError_t cmp_rows_fused(const CmpParams& p, void* klist, int cap, uint32_t span, bool write, hipStream_t s) {
   if (p.n_rows <= 0) return hipSuccess;
   if (write) {
-    hipLaunchKernelGGL(k_cmp_rowwrite, dim3((unsigned)p.n_rows), dim3(256), 0, s, p, (const CmpKept*)klist);
+    // output cell <= cap x (4 + 8) bytes + the meta byte; sources staged up to 96 KB a row
+    const int oq_cap = cap * 4 + 16, ov_cap = cap * 8 + 16;
+    const int src_cap = (int)std::min<uint64_t>((uint64_t)96 << 10, ((uint64_t)span * 2 + 64 + 15) & ~15ull);
+    const size_t lds = (size_t)oq_cap + ov_cap + src_cap;
+    const hipError_t e = hipFuncSetAttribute((const void*)k_cmp_rowwrite, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_cmp_rowwrite, dim3((unsigned)p.n_rows), dim3(CMP_ROW_THREADS), lds, s, p, (const CmpKept*)klist,
+                       oq_cap, ov_cap, src_cap);
     return hipGetLastError();
   }
   const size_t lds = (size_t)cap * 20;

@@ -17,10 +17,15 @@ from opentsdb_amd.engine import Engine  # noqa: E402
 B = 1356998400
 
 
-def build(S, N, seed=1):
+def build(S, N, seed=1, scan_order=False):
+    """scan_order: each row's columns in qualifier order, as an HBase scan returns them (time
+    order for second qualifiers); else shuffled (the general merge)."""
     rng = np.random.default_rng(seed)
     nrow = S
-    perm = np.argsort(rng.random((nrow, N)), axis=1).astype(np.uint32)
+    if scan_order:
+        perm = np.tile(np.arange(N, dtype=np.uint32), (nrow, 1))
+    else:
+        perm = np.argsort(rng.random((nrow, N)), axis=1).astype(np.uint32)
     quals = ((perm << 4) | 7).astype(">u2")
     vals = rng.integers(-10**6, 10**6, size=(nrow, N)).astype(">i8")
     ncol = nrow * N
@@ -45,7 +50,8 @@ def main():
     N = int(args[1]) if len(args) > 1 else 3600
     steps = int(args[2]) if len(args) > 2 else 3
     t = time.perf_counter()
-    cb = build(S, N)
+    order = "--scan-order" in sys.argv
+    cb = build(S, N, scan_order=order)
     gen_s = time.perf_counter() - t
     if "--pinned-first" in sys.argv:   # (diagnostic: page-locked buffers before the context exists)
         cb = pinned(cb)
@@ -68,7 +74,8 @@ def main():
     t = time.perf_counter()
     eng.run(q)
     run_ms = (time.perf_counter() - t) * 1000
-    print(json.dumps({"workload": f"{S} series x {N} one-datapoint cells (shuffled), 8-byte ints",
+    print(json.dumps({"workload": f"{S} series x {N} one-datapoint cells "
+                                  f"({'qualifier (scan) order' if order else 'shuffled'}), 8-byte ints",
                       "host_memory": "pinned" if any(a.startswith("--pinned") for a in sys.argv) else "pageable",
                       "cells": cells, "load_cells_wall_ms": sum(walls) / steps, "compact_ms": cm,
                       "index_ms": sum(ims) / steps, "cells_per_s_device": cells / (cm / 1000),
