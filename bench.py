@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--transport", choices=["auto", "rccl", "copy"], default="auto",
                     help="multi-device context (--gpus N, no launcher): RCCL send / recv or peer copies")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-child-config3", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -91,14 +92,15 @@ def cpu_baseline(args, target_s: float):
                       f"{repsn} reps in {dtn:.1f} s; 1 thread: {reps1} reps in {dt1:.1f} s"}
 
 
-def pmc_traffic(args, kernel_prefix: str):
-    """HBM bytes per launch of the dominant kernel from rocprofv3 PMC counters.
+def pmc_traffic(args, kernel_prefix: str, config3: bool = False):
+    """HBM bytes per step of the dominant kernel (every launch of it in the step: k_fast once;
+    config 3's k_short once per row class) from rocprofv3 PMC counters.
 
     Two separate child runs of this script (FETCH_SIZE and WRITE_SIZE cannot share a pass,
-    MI355X_MICROARCH.md "rocprofv3 PMC slots"), each profiling 3 launches of the same
+    MI355X_MICROARCH.md "rocprofv3 PMC slots"), each profiling 3 steps of the same
     workload.  FETCH_SIZE is in KiB and on gfx950 reports half the bytes of a 16-B/lane
     streaming read, so it is doubled; WRITE_SIZE is exact (same guide, "HBM").  Returns
-    (bytes_per_launch, detail) or (None, reason)."""
+    (bytes_per_step, detail) or (None, reason)."""
     import csv
     import glob
     import shutil
@@ -107,10 +109,11 @@ def pmc_traffic(args, kernel_prefix: str):
     exe = shutil.which("rocprofv3")
     if exe is None:
         return None, "rocprofv3 not found"
-    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "3", "--warmup", "0",
+    steps = 3
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", str(steps), "--warmup", "0",
              "--series", str(args.series), "--points", str(args.points), "--period-ms", str(args.period_ms),
              "--groups", str(args.groups), "--interval", args.interval, "--ds", args.ds, "--agg", args.agg,
-             "--value-kind", str(args.value_kind)]
+             "--value-kind", str(args.value_kind)] + (["--pmc-child-config3"] if config3 else [])
     out = {}
     tmp = tempfile.mkdtemp(prefix="tsdb_pmc_")
     env = dict(os.environ, TMPDIR="/tmp")
@@ -130,7 +133,7 @@ def pmc_traffic(args, kernel_prefix: str):
                             vals.append(float(row["Counter_Value"]))
             if not vals:
                 return None, f"no {ctr} rows for {kernel_prefix}"
-            out[ctr] = sum(vals) / len(vals)
+            out[ctr] = sum(vals) / steps
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     fetch = out["FETCH_SIZE"] * 1024.0 * 2.0
@@ -197,6 +200,20 @@ def config3_block(args, device: int):
         return out
     finally:
         eng.close()
+
+
+def config3_pmc_child(args, device: int):
+    """--pmc-child-config3: the config-3 sum:1m-avg step alone, args.steps times (pmc_traffic)."""
+    from opentsdb_amd import abi
+    from opentsdb_amd.engine import Engine
+    eng = Engine(device)
+    eng.synth(10_000_000, T0, 360, 10000, 2, 1000, 30000, 0x5EED)
+    eng.sync()
+    q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+    for _ in range(args.steps):
+        eng.run(q)
+    eng.sync()
+    eng.close()
 
 
 def workload_label(args) -> str:
@@ -401,6 +418,8 @@ def main():
         sys.exit(2)
     if world == 1 and args.gpus > 1 and not args.pmc_child:
         return main_md(args)
+    if args.pmc_child_config3:
+        return config3_pmc_child(args, local_rank)
     dist = None
     if world > 1:
         import torch
@@ -498,6 +517,10 @@ def main():
         traffic, traffic_note = (None, "not collected (--no-pmc or N>1)")
         if not args.no_pmc and world == 1:
             traffic, traffic_note = pmc_traffic(args, f"void tsdb::{kname}")
+            if extra is not None:   # config 3: both k_short row classes of a step
+                c3t, c3note = pmc_traffic(args, "void tsdb::k_short", config3=True)
+                extra["config3"]["sum"]["traffic"] = c3t
+                extra["config3"]["sum"]["traffic_detail"] = c3note
         line = {
             "metric": "raw datapoints/sec through downsample+group-by; % of HBM BW, 1-8 GPUs",
             "value": value,

@@ -413,6 +413,8 @@ struct tsdbhip_ctx {
   int fast_qw = 0, fast_vl = 0;        // dominant k_fast row class (0 = none)
   int fast_qw2 = 0, fast_vl2 = 0;      // second class, chained over the first one's redo list
   int pct_qw = 0, pct_vl = 0;          // dominant uniform class of one-chunk rows (k_pct_rows)
+  bool pct_vonly = false;              // every row of that class (4-byte values) all-float without NaN
+                                       // or all-integer: the key kernel reads values only
   // tile lists by k_fast row class (built at load): [class A / class B][walker / short],
   // and the tiles of neither class (general kernel only).  Short = one row per series of at
   // most CH datapoints (k_short).
@@ -729,8 +731,22 @@ extern "C" int tsdbhip_sync(tsdbhip_ctx* c) {
 static int build_tiles(tsdbhip_ctx* c) {
   const int64_t n = c->n_series;
   int64_t T = 64;
-  // keep enough waves in flight for small batches
-  while (T > 1 && (n + T - 1) / T < 8192) T >>= 1;
+  // Keep enough waves in flight for small batches (8192 tiles), and enough tiles of heavy series
+  // that the grid's last round is a small part of the launch: a tile is one wave's work and the
+  // tiles of a uniform batch cost the same, so with ~2k waves resident the idle tail is about half
+  // a tile-time per wave slot.  Config 2 (1M series of 3600 dp): 15.6k tiles of 64 series = 7.6
+  // rounds, ~6 % tail; 62.5k tiles of 16 series = 30 rounds (the per-tile partials grow to 90 MB,
+  // 0.4 % of the bytes read).  Tiles of light series (config 3's one 360-dp row) stay at 64: they
+  // are short, and k_short gives each of a tile's series a lane.  TSDBHIP_TILE_MIN /
+  // TSDBHIP_TILE_DP override the tile-count and tile-datapoint thresholds (A/B runs).
+  int64_t min_tiles = 32768, tile_dp = 40000;
+  if (const char* e = std::getenv("TSDBHIP_TILE_MIN")) min_tiles = std::max<int64_t>(1, std::atoll(e));
+  if (const char* e = std::getenv("TSDBHIP_TILE_DP")) tile_dp = std::max<int64_t>(1, std::atoll(e));
+  int64_t dps = 0;
+  for (int64_t r = 0; r < c->n_rows; r++) dps += c->h_ndp[r];
+  const double dp_per_series = n ? (double)dps / (double)n : 0.0;
+  while (T > 1 && ((n + T - 1) / T < 8192 || ((n + T - 1) / T < min_tiles && (double)T * dp_per_series > (double)tile_dp)))
+    T >>= 1;
   c->tb.clear(); c->te.clear(); c->tg.clear();
   c->gtp.assign(c->n_groups + 1, 0);
   int64_t s = 0;
@@ -872,6 +888,7 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
   int64_t cls[2][2] = {{0, 0}, {0, 0}};   // [qw 2/4][vl 4/8] uniform float rows
   int64_t cls_vle = 0;                    // 2-byte qualifiers, 1-2 byte integers, one chunk
   int64_t cls_pct[2][9] = {};             // [qw 2/4][vl]: uniform sorted rows of <= 512 dp
+  int64_t cls_vonly[2] = {};              // [qw 2/4]: those of 4-byte values, all-float without NaN or all-int
   for (int64_t r = 0; r < c->n_rows; r++) {
     c->h_ndp[r] = back[r].ndp;
     c->h_base[r] = back[r].base;
@@ -887,6 +904,9 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
     if (!(f & (ROW_ERR | ROW_UNSORTED)) && (qw == 2 || qw == 4) && (vl == 1 || vl == 2 || vl == 4 || vl == 8) &&
         back[r].ndp <= 512)
       cls_pct[qw == 4][vl] += back[r].ndp;
+    if (!(f & (ROW_ERR | ROW_UNSORTED)) && (qw == 2 || qw == 4) && vl == 4 && back[r].ndp <= 512 &&
+        (((f & ROW_ALLF) && !(f & ROW_NAN)) || (f & ROW_ALLI)))
+      cls_vonly[qw == 4] += back[r].ndp;
   }
   // the two largest k_fast row classes by datapoints
   struct Cand { int64_t n; int qw, vl; };
@@ -900,6 +920,7 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
   for (int a = 0; a < 2; a++)
     for (int v = 1; v <= 8; v++)
       if (cls_pct[a][v] > best) { best = cls_pct[a][v]; c->pct_qw = a ? 4 : 2; c->pct_vl = v; }
+  c->pct_vonly = c->pct_vl == 4 && best > 0 && cls_vonly[c->pct_qw == 4] == best;
   // malformed rows are reported lazily, when a query reads them (as the reference does)
   return build_tiles(c);
 }
@@ -2642,6 +2663,8 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       GridParams rp = gp;
       rp.redo_list = c->redo2.as<int32_t>();
       rp.redo_n = c->redo2_n.as<int32_t>();
+      const char* venv = std::getenv("TSDBHIP_PCT_VONLY");
+      rp.pct_vonly = keys && c->pct_vonly && !(venv && venv[0] == '0');
       HIP_OK(launch_pct_rows(rp, c->pct_qw, c->pct_vl, c->stream));
       int32_t nback = 0;
       HIP_OK(hipMemcpyAsync(&nback, c->redo2_n.p, 4, hipMemcpyDeviceToHost, c->stream));

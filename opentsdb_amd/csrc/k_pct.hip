@@ -600,6 +600,9 @@ static constexpr int EXT_MAX = 24;
 #ifndef PCT_KEYS_OCC
 #define PCT_KEYS_OCC 1   // min waves / SIMD the key kernel is compiled for (8: 18.7 ms with spills vs 18.1 at 7)
 #endif
+#ifndef PCT_VKEYS_OCC
+#define PCT_VKEYS_OCC 7  // the values-only key kernel (8 spills 3-10 VGPRs)
+#endif
 
 // DPP int min across the wave (uniform result)
 __device__ __forceinline__ int wave_min_dpp(int x) {
@@ -642,7 +645,7 @@ __device__ __forceinline__ void extract_masked(const double val[DPL], uint32_t k
 
 struct RowLite {
   uint64_t qoff, voff;
-  uint32_t base, ndp;
+  uint32_t base, ndp, flags;
 };
 
 __device__ __forceinline__ RowLite row_of_lane(const RowDesc& d, int l) {
@@ -651,6 +654,7 @@ __device__ __forceinline__ RowLite row_of_lane(const RowDesc& d, int l) {
   r.voff = rl64(d.voff, l);
   r.base = (uint32_t)__builtin_amdgcn_readlane((int)d.base, l);
   r.ndp = (uint32_t)__builtin_amdgcn_readlane((int)d.ndp, l);
+  r.flags = (uint32_t)__builtin_amdgcn_readlane((int)d.flags, l);
   return r;
 }
 
@@ -929,47 +933,12 @@ __device__ __forceinline__ uint32_t next_key32(const uint32_t key[DPL], uint32_t
   return ~wave_max_u32(~gt);
 }
 
-// The statistic of a one-bucket row of 4-byte values; 0 = not this path's case (mixed float /
-// int row): the caller hands the series to k_pct.  Near the ends the k largest / smallest keys
-// are popped (topk_u32); mid ranks take the bitwise search.
-template <int QW, bool MID>
-__device__ __forceinline__ int pct_row_keys(const GridParams& p, const RowLite& d, const RawT<QW, 4>& rw, double q,
-                                            double& x) {
-  const int i0 = lane_id() * DPL;
-  const int nv = max(0, min(DPL, (int)d.ndp - i0));
-  uint32_t key[DPL];
-  bool ok = true, anyf = false, anyi = false;
-  int n = 0;
-  const uint32_t* vw = &rw.v[0].x;
-#pragma unroll
-  for (int j = 0; j < DPL; j++) {
-    uint32_t off, fl;
-    if (QW == 2) {
-      const uint32_t be = __builtin_bswap32((&rw.q[0].x)[j >> 1]);
-      const uint32_t qq = (j & 1) ? (be & 0xFFFF) : (be >> 16);
-      off = (qq >> 4) * 1000u;
-      fl = qq & 0xF;
-    } else {
-      const uint32_t qq = __builtin_bswap32((&rw.q[0].x)[j]);
-      off = (qq & 0x0FFFFFC0u) >> 6;
-      fl = qq & 0xF;
-    }
-    const bool v = j < nv;
-    const bool isf = (fl & 8) != 0;
-    ok = ok && (!v || off < 3600000u);
-    anyf = anyf || (v && isf);
-    anyi = anyi || (v && !isf);
-    key[j] = v ? key32(__builtin_bswap32(vw[j]), isf) : 0u;
-    n += key[j] != 0;
-  }
-  if (__ballot(!ok)) return -1;   // offset >= 1 h: hand the series back
-  const bool wf = __ballot(anyf) != 0, wi = __ballot(anyi) != 0;
-  if (wf && wi) return 0;   // mixed row
-  n = __builtin_amdgcn_readlane(wave_incl_sum_dpp(n), 63);
-  if (n == 0) {
-    x = (double)NAN;
-    return 1;
-  }
+// The statistic of one bucket from the wave's 32-bit keys (absent = 0), n present values (n >= 1),
+// wf = the keys are float32 (else int32).  Near the ends the k largest / smallest keys are popped
+// (topk_u32); mid ranks take the bitwise search.  0 = more than EXT_MAX from both ends (near-end
+// variant): the caller hands the series back.
+template <bool MID>
+__device__ __forceinline__ int keys_stat(const GridParams& p, uint32_t key[DPL], int n, bool wf, double q, double& x) {
   // select_sorted: PercentileAgg LEGACY pos = p (n + 1); Median.runDouble sorted[n / 2]
   const double pos = q * (double)(n + 1);
   int lo_i, hi_i;
@@ -1006,15 +975,118 @@ __device__ __forceinline__ int pct_row_keys(const GridParams& p, const RowLite& 
   return 1;
 }
 
+// The statistic of a one-bucket row of 4-byte values; 0 = not this path's case (mixed float /
+// int row): the caller hands the series to k_pct.  Near the ends the k largest / smallest keys
+// are popped (topk_u32); mid ranks take the bitwise search.
+template <int QW, bool MID>
+__device__ __forceinline__ int pct_row_keys(const GridParams& p, const RowLite& d, const RawT<QW, 4>& rw, double q,
+                                            double& x) {
+  const int i0 = lane_id() * DPL;
+  const int nv = max(0, min(DPL, (int)d.ndp - i0));
+  uint32_t key[DPL];
+  bool ok = true, anyf = false, anyi = false;
+  int n = 0;
+  const uint32_t* vw = &rw.v[0].x;
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    uint32_t off, fl;
+    if (QW == 2) {
+      const uint32_t be = __builtin_bswap32((&rw.q[0].x)[j >> 1]);
+      const uint32_t qq = (j & 1) ? (be & 0xFFFF) : (be >> 16);
+      off = (qq >> 4) * 1000u;
+      fl = qq & 0xF;
+    } else {
+      const uint32_t qq = __builtin_bswap32((&rw.q[0].x)[j]);
+      off = (qq & 0x0FFFFFC0u) >> 6;
+      fl = qq & 0xF;
+    }
+    const bool v = j < nv;
+    const bool isf = (fl & 8) != 0;
+    ok = ok && (!v || off < 3600000u);
+    anyf = anyf || (v && isf);
+    anyi = anyi || (v && !isf);
+    const uint32_t bits = __builtin_bswap32(vw[j]);
+    key[j] = v ? key32(bits, isf) : 0u;
+    n += key[j] != 0;
+    ok = ok && !(v && !isf && bits == 0x80000000u);   // int32 MIN keys to 0 (= absent): not this path's
+  }
+  if (__ballot(!ok)) return -1;   // offset >= 1 h (or an int32 MIN value): hand the series back
+  const bool wf = __ballot(anyf) != 0, wi = __ballot(anyi) != 0;
+  if (wf && wi) return 0;   // mixed row
+  n = __builtin_amdgcn_readlane(wave_incl_sum_dpp(n), 63);
+  if (n == 0) {
+    x = (double)NAN;
+    return 1;
+  }
+  return keys_stat<MID>(p, key, n, wf, q, x);
+}
+
+// ---- values-only key rows (KEYS & 4) ----------------------------------------------------
+// When every row of the batch's key class was certified at load (k_index flags) as all-float32
+// without NaN or all-int32 -- sorted, 4-byte values -- a 1 h bucket needs no qualifier but the
+// row's last: offsets strictly increase, so the row lies inside its hour iff its last offset is
+// < 1 h.  The kernel then reads 4 B a datapoint (+ one qualifier a row), forms each key with a
+// byte swap and a sign flip, and n is the row's datapoint count (no NaN to drop).
+struct RawV {
+  uint4 v[2];
+  uint32_t lq;   // the row's last qualifier, as loaded (little-endian load of big-endian bytes)
+};
+
+template <int QW>
+__device__ __forceinline__ void load_row_v(const GridParams& p, const RowLite& d, RawV& rw) {
+  const uint8_t* q = p.qual + (d.ndp ? d.qoff + (uint64_t)(d.ndp - 1) * QW : 0);
+  rw.lq = QW == 2 ? (uint32_t)*reinterpret_cast<const uint16_t*>(q) : *reinterpret_cast<const uint32_t*>(q);
+  const int64_t i0 = (int64_t)lane_id() * DPL;
+  if (i0 >= (int64_t)d.ndp) return;
+  const uint4* v = reinterpret_cast<const uint4*>(p.val + d.voff + i0 * 4);
+  rw.v[0] = v[0];
+  rw.v[1] = v[1];
+}
+
+template <int QW, bool MID>
+__device__ __forceinline__ int pct_row_vkeys(const GridParams& p, const RowLite& d, const RawV& rw, double q,
+                                             double& x) {
+  const uint32_t lq = (uint32_t)__builtin_amdgcn_readfirstlane((int)rw.lq);
+  const uint32_t off = QW == 2 ? (((((lq & 0xFFu) << 8) | ((lq >> 8) & 0xFFu)) >> 4) * 1000u)
+                               : ((__builtin_bswap32(lq) & 0x0FFFFFC0u) >> 6);
+  if (off >= 3600000u) return -1;   // the row reaches past its hour: hand the series back
+  const bool isf = (d.flags & ROW_ALLF) != 0;
+  const int n = (int)d.ndp;
+  const int i0 = lane_id() * DPL;
+  uint32_t key[DPL];
+  const uint32_t* vw = &rw.v[0].x;
+  if (isf) {
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      const uint32_t b = __builtin_bswap32(vw[j]);
+      key[j] = b ^ ((uint32_t)((int32_t)b >> 31) | 0x80000000u);   // key32 of a non-NaN float32
+    }
+  } else {
+    bool mn = false;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      key[j] = __builtin_bswap32(vw[j]) ^ 0x80000000u;
+      mn = mn || (i0 + j < n && key[j] == 0u);
+    }
+    if (__ballot(mn)) return -1;   // an int32 MIN value keys to 0 (= absent)
+  }
+  if (i0 + DPL > n) {
+#pragma unroll
+    for (int j = 0; j < DPL; j++) key[j] = i0 + j < n ? key[j] : 0u;
+  }
+  return keys_stat<MID>(p, key, n, isf, q, x);
+}
+
 // one in-range row: its buckets' order statistics into dense / pres; false = hand the
 // series back (offset >= 1 h, or a statistic more than EXT_MAX from both ends)
-template <int QW, int VL, int KEYS>
-__device__ __forceinline__ bool pct_row(const GridParams& p, const RowLite& cd, const RawT<QW, VL>& rc, double q,
+template <int QW, int VL, int KEYS, class R>
+__device__ __forceinline__ bool pct_row(const GridParams& p, const RowLite& cd, const R& rc, double q,
                                         double* dense, uint8_t* pres) {
   const int lane = lane_id();
   RowLite d;
   d.base = (uint32_t)__builtin_amdgcn_readfirstlane((int)cd.base);
   d.ndp = (uint32_t)__builtin_amdgcn_readfirstlane((int)cd.ndp);
+  d.flags = (uint32_t)__builtin_amdgcn_readfirstlane((int)cd.flags);
   // slot of the row base: (base * 1000 - B0) / I, an exact multiple (double division exact)
   const int64_t rel = (int64_t)d.base * 1000 - p.B0;
   const int slot0 = (int)__builtin_amdgcn_readfirstlane((int)((double)rel / (double)p.I));
@@ -1025,7 +1097,9 @@ __device__ __forceinline__ bool pct_row(const GridParams& p, const RowLite& cd, 
     if constexpr (VL == 4) {
       if (d.ndp == 0) return true;
       double x;
-      const int r = pct_row_keys<QW, KEYS == 2>(p, d, rc, q, x);
+      int r;
+      if constexpr ((KEYS & 4) != 0) r = pct_row_vkeys<QW, (KEYS & 3) == 2>(p, d, rc, q, x);
+      else r = pct_row_keys<QW, (KEYS & 3) == 2>(p, d, rc, q, x);
       if (r <= 0) return false;
       if (lane == 0) { dense[slot0] = x; pres[slot0] = 1; }
       return true;
@@ -1033,6 +1107,7 @@ __device__ __forceinline__ bool pct_row(const GridParams& p, const RowLite& cd, 
       return false;
     }
   } else {
+  static_assert(std::is_same<R, RawT<QW, VL>>::value, "extraction rows are raw qualifier + value registers");
   int slot[DPL];
   double val[DPL];
   const bool ok = decode_row<QW, VL>(p, d, slot0, one, rc, slot, val);
@@ -1079,9 +1154,19 @@ __device__ __forceinline__ bool pct_row(const GridParams& p, const RowLite& cd, 
 }
 
 // KEYS: 0 = extraction over doubles; 1 = the 32-bit key kernel, statistics near the ends;
-// 2 = the key kernel ranking any statistic (median, p50, p75: the bitwise rank search)
+// 2 = the key kernel ranking any statistic (median, p50, p75: the bitwise rank search);
+// | 4 = the key kernel over load-certified rows, values read alone (RawV)
+template <int QW, int VL, int KEYS>
+__device__ __forceinline__ void load_ring_row(const GridParams& p, const RowLite& d, RawT<QW, VL>& rw) {
+  load_row<QW, VL>(p, d, rw);
+}
+template <int QW, int VL, int KEYS>
+__device__ __forceinline__ void load_ring_row(const GridParams& p, const RowLite& d, RawV& rw) {
+  load_row_v<QW>(p, d, rw);
+}
+
 template <int QW, int VL, int D, int KEYS>
-__global__ __launch_bounds__(256, KEYS ? PCT_KEYS_OCC : 1) void k_pct_rows(GridParams p) {
+__global__ __launch_bounds__(256, (KEYS & 4) ? PCT_VKEYS_OCC : KEYS ? PCT_KEYS_OCC : 1) void k_pct_rows(GridParams p) {
   const int lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t s = (int64_t)blockIdx.x * 4 + wave;
@@ -1109,6 +1194,7 @@ __global__ __launch_bounds__(256, KEYS ? PCT_KEYS_OCC : 1) void k_pct_rows(GridP
       const uint32_t f = d.flags;
       bad = in && ((f & (ROW_ERR | ROW_UNSORTED)) || (d.base % 3600u) != 0 || (int)(f & ROW_QW_MASK) != QW ||
                    (int)((f & ROW_VL_MASK) >> ROW_VL_SHIFT) != VL || d.ndp > (uint32_t)CH);
+      if ((KEYS & 4) != 0) bad = bad || (in && !(((f & ROW_ALLF) && !(f & ROW_NAN)) || (f & ROW_ALLI)));
     }
     // strictly increasing bases (rows of one series are in base order; equal = two cells)
     const int prev = __shfl_up((int)d.base, 1, 64);
@@ -1127,20 +1213,21 @@ __global__ __launch_bounds__(256, KEYS ? PCT_KEYS_OCC : 1) void k_pct_rows(GridP
     const int nin = hi - lo + 1;
     // D-deep ring, shifted by one row per step: ring[0] is row t, ring[1 .. D-1] rows
     // t+1 .. t+D-1 in flight
-    RawT<QW, VL> ring[D];
+    using Ring = typename std::conditional<(KEYS & 4) != 0, RawV, RawT<QW, VL>>::type;
+    Ring ring[D];
     RowLite rl[D];
 #pragma unroll
     for (int u = 0; u < D; u++) {
       ring[u] = {};
       if (u < D - 1 && u < nin) {
         rl[u] = row_of_lane(d, lo + u);
-        load_row<QW, VL>(p, rl[u], ring[u]);
+        load_ring_row<QW, VL, KEYS>(p, rl[u], ring[u]);
       }
     }
     for (int t = 0; t < nin; t++) {
       if (t + D - 1 < nin) {
         rl[D - 1] = row_of_lane(d, lo + t + D - 1);
-        load_row<QW, VL>(p, rl[D - 1], ring[D - 1]);
+        load_ring_row<QW, VL, KEYS>(p, rl[D - 1], ring[D - 1]);
       }
       if (!pct_row<QW, VL, KEYS>(p, rl[0], ring[0], q, dense, pres)) {
         if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)s;
@@ -1821,8 +1908,17 @@ hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s) {
   const bool keys = vl == 4 && p.I == 3600000 && !(std::getenv("TSDBHIP_PCT_KEYS") && std::getenv("TSDBHIP_PCT_KEYS")[0] == '0');
   const int sel_i = (p.sel_fn - TSDB_AGG_P999) % 6;
   const bool mid = p.sel_fn == TSDB_AGG_MEDIAN || sel_i >= 4;   // median, p75, p50 (and their ep* forms)
+  // values-only key rows: ring depth (TSDBHIP_PCTDV; half the registers of a raw row)
+  const char* dvenv = std::getenv("TSDBHIP_PCTDV");
+  const int DV = dvenv ? std::atoi(dvenv) : 2;
 #define PCT_ROWS_CASE(Q, V)                                                                                  \
   if (qw == Q && vl == V) {                                                                                \
+    if (V == 4 && keys && p.pct_vonly) {                                                                   \
+      if (mid) hipLaunchKernelGGL((k_pct_rows<Q, V, 2, 6>), grid, block, 0, s, p);                        \
+      else if (DV == 3) hipLaunchKernelGGL((k_pct_rows<Q, V, 3, 5>), grid, block, 0, s, p);               \
+      else hipLaunchKernelGGL((k_pct_rows<Q, V, 2, 5>), grid, block, 0, s, p);                             \
+      return hipGetLastError();                                                                            \
+    }                                                                                                      \
     if (V == 4 && keys) {                                                                                  \
       if (mid) hipLaunchKernelGGL((k_pct_rows<Q, V, 2, 2>), grid, block, 0, s, p);                        \
       else if (D == 2) hipLaunchKernelGGL((k_pct_rows<Q, V, 2, 1>), grid, block, 0, s, p);                 \

@@ -189,3 +189,55 @@ def test_pct_mid_ranks_key_kernel(eng, fn):
         assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), agg, ctx=f"{fn} {agg}")
     q = abi.new_query(T0, T0 + 3 * 3600 - 1, "none", ds_function=abi.AGG[fn], ds_interval_ms=3600000)
     assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "none", tol=0.0, ctx=f"{fn} none")
+
+
+def _vonly_batch(seed=23):
+    """Rows k_index certifies for the values-only key kernel (every row 4-byte values, all float32
+    without NaN or all int32, sorted) plus the cases it must hand back to k_pct: an int32 MIN value
+    (keys to 0 = absent), and a row whose last offset is past its hour (2-byte qualifiers reach
+    4095 s).  Buckets of 1..360 values, rows of any length (partial lanes)."""
+    rng = np.random.default_rng(seed)
+    rows, gids = [], []
+    for s in range(18):
+        keep = rng.random(3 * 360) < (0.85 if s % 4 else 0.02)
+        ts = T0 * 1000 + np.flatnonzero(keep).astype(np.int64) * 10000
+        n = len(ts)
+        if s % 2 == 0:   # float32, ties and negatives, no NaN
+            f = np.round(rng.normal(0, 50, n) * 4) / 4 + (1 + s) * 0.5
+            rows.append(synth.encode_rows(ts, np.zeros(n, np.int64), f, np.full(n, 1), np.zeros(n, bool)))
+        else:            # int32 (4-byte vle), few distinct values, both signs
+            lv = rng.integers(70000, 70009, n) * (1 if s % 3 else -1) * (1 + s)
+            if s == 5:
+                lv[rng.random(n) < 0.1] = -(1 << 31)   # int32 MIN: handed back to k_pct
+            if s == 7:
+                lv[:] = rng.integers(-(1 << 31) + 1, (1 << 31) - 1, n)
+            rows.append(synth.encode_rows(ts, lv, np.zeros(n), np.zeros(n, np.int64), np.zeros(n, bool)))
+        gids.append(s % 3)
+    # series 9: its first hour row carries 20 more int32 points at offsets 3600..3790 s (the
+    # next hour's bucket), as a row may under 2-byte qualifiers
+    base, q, v = rows[9][0]
+    extra_q = b"".join((((3600 + 10 * k) << 4) | 3).to_bytes(2, "big") for k in range(20))
+    extra_v = b"".join(int(-90000 - k).to_bytes(4, "big", signed=True) for k in range(20))
+    meta = v[-1:] if len(v) % 4 == 1 else b"\x00"
+    body = v[:len(v) - len(meta)]
+    rows[9][0] = (base, q + extra_q, body + extra_v + meta)
+    order = sorted(range(18), key=lambda i: gids[i])
+    return synth.from_series([rows[i] for i in order], [gids[i] for i in order])
+
+
+@pytest.mark.parametrize("fn", ["p99", "p999", "p90", "ep99r7", "p75", "p50", "median"])
+def test_pct_values_only_key_rows(eng, fn, monkeypatch):
+    """k_pct_rows' values-only key kernel (rows certified at load read 4 B a datapoint, one
+    qualifier a row) against the oracle, and bit-identical to the qualifier-reading key kernel
+    (TSDBHIP_PCT_VONLY=0)."""
+    b = _vonly_batch()
+    res = {}
+    for vonly in ("1", "0"):
+        monkeypatch.setenv("TSDBHIP_PCT_VONLY", vonly)
+        for agg in ["max", "min", "none"]:
+            q = abi.new_query(T0, T0 + 3 * 3600 - 1, agg, ds_function=abi.AGG[fn], ds_interval_ms=3600000)
+            got = eng.run_batch(b, q)
+            assert_groups_match(got, O.run_query(b, q), agg, tol=0.0, ctx=f"{fn} {agg} vonly={vonly}")
+            res[(vonly, agg)] = got
+    for agg in ["max", "min", "none"]:
+        assert_groups_match(res[("1", agg)], res[("0", agg)], agg, tol=0.0, ctx=f"{fn} {agg} vonly vs keys")
