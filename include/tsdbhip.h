@@ -537,8 +537,9 @@ typedef struct {
 } tsdbhip_hist_result;
 /* The query's start / end, aggregator and downsampling (ds_function is ignored: histograms are
  * always summed; -1 = no downsampling) as for tsdbhip_run; pct[n_pct] the percentiles
- * (TsdbQuery.setPercentiles, List<Float>).  NOT_IMPLEMENTED: calendar downsampling, spans whose
- * datapoints are not in time order, more than 4 GB of per-point state. */
+ * (TsdbQuery.setPercentiles, List<Float>).  Calendar downsampling (UTC, ds_tz, per-span anchors)
+ * included.  NOT_IMPLEMENTED: spans whose datapoints are not in time order, more than 32 GB of
+ * per-point state, more than 32768 distinct buckets. */
 int tsdbhip_hist_run(tsdbhip_ctx* ctx, const tsdbhip_query* q, int n_pct, const float* pct, int show_buckets,
                      tsdbhip_hist_result** out);
 /* The same over every row of the store with the HistogramSpanGroup bounds given directly (ms):

@@ -2162,8 +2162,9 @@ bool is_sel_agg(int a) { return a == TSDB_AGG_MEDIAN || (a >= TSDB_AGG_P999 && a
 // slots are the union of those boundary sequences, provided they agree where they overlap --
 // always for days, weeks, n months (12 % n == 0) and years, which step on the local calendar,
 // and for ms / s / m / h lattices when the zone's offsets in range are congruent modulo the
-// step; otherwise the anchors come from each series' first datapoint (k_first_ts) and spans on
-// grids that disagree return NOT_IMPLEMENTED (their union of timestamps is not one grid).
+// step; otherwise the anchors come from each series' first datapoint (k_first_ts), and spans on
+// grids that disagree run per anchor and aggregate over the union of their timestamps
+// (run_anchored: the raw union evaluator, fills included).
 // DateTime.previousInterval of every first datapoint f[i] (sorted; INT64_MAX = the series has
 // none, anchor INT64_MAX).  Datapoints with the same jcal_top inside one step of that top's walk
 // share its anchor, so the walk runs once per such step.
