@@ -471,6 +471,7 @@ struct tsdbhip_ctx {
   int64_t ro_chk_ss = 0, ro_chk_se = 0, ro_chk_T = 0;
   int64_t ro_scan_ss = 0, ro_scan_se = 0;
   std::vector<uint8_t> ro_scan_act;    // [n_series] resident: rollup rows in the scan range
+  std::vector<int32_t> ro_scan_gact;   // the groups holding such a series (with ro_scan_act)
   // histogram path (hist.cpp): the resident histogram store and its query scratch
   void* hist = nullptr;
   // multi-device context (multi.cpp, tsdbhip_init_devices): its devices' contexts; null on a
@@ -3224,39 +3225,6 @@ void record_timing(tsdbhip_ctx* c, const Plan& P, int32_t redo_n) {
 // Dense [G][K] outputs on the device -> result (after the stream's work is queued).
 void ro_activity(const tsdbhip_ctx* c, const Plan& P, int64_t G, std::vector<uint32_t>& act);
 
-int collect(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bool timed, tsdbhip_result** out,
-            const void* d_val = nullptr, const void* d_flag = nullptr) {
-  std::vector<double> val(G * P.K);
-  std::vector<uint8_t> flag(G * P.K);
-  std::vector<uint32_t> act(std::max<int64_t>(1, G));
-  int32_t err = 0;
-  if (G * P.K) {
-    HIP_OK(hipMemcpyAsync(val.data(), d_val ? d_val : c->out_val.p, G * P.K * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipMemcpyAsync(flag.data(), d_flag ? d_flag : c->out_flag.p, G * P.K, hipMemcpyDeviceToHost, c->stream));
-  }
-  if (G) HIP_OK(hipMemcpyAsync(act.data(), c->gact.p, G * 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
-  int32_t redo_n = 0;
-  if (timed && c->fast_used) HIP_OK(hipMemcpyAsync(&redo_n, c->redo_final, 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipStreamSynchronize(c->stream));
-  if (timed) record_timing(c, P, redo_n);
-  if (err) return fail(err, "error raised by the device path");
-  if (P.mode == MODE_ALL) {
-    // AggregationIterator ctor: the single "all" point is skipped unless start_time <= qs <= end_time
-    const int64_t S0 = P.ss * 1000, E0 = P.se * 1000;
-    if (q->start_time < S0 || q->start_time > E0) std::fill(flag.begin(), flag.end(), 0);
-  }
-  ro_activity(c, P, G, act);
-  return assemble(c, q, P, G, val, flag, act, out);
-}
-
-}  // namespace
-
-// ---------------------------------------------------------------------------
-// raw path (k_raw.hip): no downsampling
-// ---------------------------------------------------------------------------
-namespace {
-
 // TSDBHIP_TRACE=1: host wall time of a query's phases on stderr (diagnostics only)
 struct PhaseTrace {
   bool on;
@@ -3274,6 +3242,45 @@ struct PhaseTrace {
     last = t;
   }
 };
+
+int collect(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bool timed, tsdbhip_result** out,
+            const void* d_val = nullptr, const void* d_flag = nullptr) {
+  std::vector<double> val(G * P.K);
+  std::vector<uint8_t> flag(G * P.K);
+  std::vector<uint32_t> act(std::max<int64_t>(1, G));
+  int32_t err = 0;
+  if (G * P.K) {
+    HIP_OK(hipMemcpyAsync(val.data(), d_val ? d_val : c->out_val.p, G * P.K * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipMemcpyAsync(flag.data(), d_flag ? d_flag : c->out_flag.p, G * P.K, hipMemcpyDeviceToHost, c->stream));
+  }
+  if (G) HIP_OK(hipMemcpyAsync(act.data(), c->gact.p, G * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
+  int32_t redo_n = 0;
+  if (timed && c->fast_used) HIP_OK(hipMemcpyAsync(&redo_n, c->redo_final, 4, hipMemcpyDeviceToHost, c->stream));
+  PhaseTrace tr("collect");
+  HIP_OK(hipStreamSynchronize(c->stream));
+  tr.mark("device + d2h");
+  if (timed) record_timing(c, P, redo_n);
+  if (err) return fail(err, "error raised by the device path");
+  if (P.mode == MODE_ALL) {
+    // AggregationIterator ctor: the single "all" point is skipped unless start_time <= qs <= end_time
+    const int64_t S0 = P.ss * 1000, E0 = P.se * 1000;
+    if (q->start_time < S0 || q->start_time > E0) std::fill(flag.begin(), flag.end(), 0);
+  }
+  ro_activity(c, P, G, act);
+  tr.mark("ro_activity");
+  const int rc = assemble(c, q, P, G, val, flag, act, out);
+  tr.mark("assemble");
+  return rc;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// raw path (k_raw.hip): no downsampling
+// ---------------------------------------------------------------------------
+namespace {
+
 
 // Points handed to the raw evaluator instead of the resident rows' datapoints: each span's
 // Downsampler output (run_anchored).  n[s] points of series s, consecutive in pts; live[s] = the
@@ -3888,6 +3895,13 @@ int ro_scan(tsdbhip_ctx* c, const Plan& P, bool reads_counts) {
     for (int64_t s = 0; s < c->ro_nval; s++)
       for (int64_t i = c->ro_rp[s]; i < c->ro_rp[s + 1]; i++)
         if (c->ro_rows[i].base >= P.ss && c->ro_rows[i].base < P.se) { c->ro_scan_act[c->ro_res[s]] = 1; break; }
+    // the groups those series belong to, once per scan range (not a pass over every series per query)
+    std::vector<uint8_t> seen(std::max<int64_t>(1, c->n_groups), 0);
+    c->ro_scan_gact.clear();
+    for (int64_t i = 0; i < c->n_series; i++) {
+      const int64_t g = c->h_group[i];
+      if (c->ro_scan_act[i] && g < c->n_groups && !seen[g]) { seen[g] = 1; c->ro_scan_gact.push_back((int32_t)g); }
+    }
     c->ro_scan_valid = true;
     c->ro_scan_ss = P.ss;
     c->ro_scan_se = P.se;
@@ -3962,13 +3976,13 @@ int ro_stage(tsdbhip_ctx* c, const tsdbhip_query* q, const tsdbhip_query& qr, Pl
 // its RollupSeqs yield no datapoint; count series are no spans of the query
 void ro_activity(const tsdbhip_ctx* c, const Plan& P, int64_t G, std::vector<uint32_t>& act) {
   if (!(c->ro_active && c->ro_scan_valid)) return;
-  for (int64_t i = 0; i < c->n_series; i++) {
-    if (P.none) {
-      if (i < G) act[i] = c->h_orig[i] < c->ro_nval ? (act[i] | c->ro_scan_act[i]) : 0;
-    } else if (c->ro_scan_act[i] && c->h_group[i] < c->n_groups && c->h_group[i] < G) {
-      act[c->h_group[i]] = 1;
-    }
+  if (!P.none) {
+    for (const int32_t g : c->ro_scan_gact)
+      if (g < G) act[g] = 1;
+    return;
   }
+  for (int64_t i = 0; i < std::min<int64_t>(G, c->n_series); i++)
+    act[i] = c->h_orig[i] < c->ro_nval ? (act[i] | c->ro_scan_act[i]) : 0;
 }
 
 // Sum / avg downsampling over a scan holding rows whose values cannot add exactly in any order
@@ -4011,16 +4025,20 @@ bool seq_dense_wanted(tsdbhip_ctx* c, const Plan& P) {
 }
 
 int run_rollup(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
+  PhaseTrace tr("rollup");
   int rc = ro_check(q);
   if (rc) return rc;
   const tsdbhip_query qr = ro_query(c, q);
   Plan P;
   rc = plan_query(c, &qr, P);
   if (rc) return rc;
+  tr.mark("plan");
   rc = ro_stage(c, q, qr, P);
   if (rc) return rc;
+  tr.mark("scan + stage");
   const int64_t G = P.none ? c->n_series : c->n_groups;
   P.seq_dense = seq_dense_wanted(c, P);
+  tr.mark("seq_dense_wanted");
   if (P.gsel || P.ordered) {
     rc = P.gsel ? run_sel_group(c, &qr, P, G) : run_ordered(c, &qr, P, G);
     if (rc) return rc;
@@ -4028,6 +4046,7 @@ int run_rollup(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
   }
   rc = run_device(c, &qr, P, G, true);
   if (rc) return rc;
+  tr.mark("device launches");
   return collect(c, &qr, P, G, true, out);
 }
 
