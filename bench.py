@@ -55,6 +55,9 @@ def parse():
                     help="multi-device context (--gpus N, no launcher): RCCL send / recv or peer copies")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--pmc-child-config3", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--md-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--md-timeout", type=float, default=480.0,
+                    help="--gpus N > 1: seconds the multi-device run may take before it is retried over peer copies")
     return ap.parse_args()
 
 
@@ -241,7 +244,10 @@ def visible_gpus() -> int:
     # the library's hipGetDeviceCount: torch.cuda.device_count() would bring up torch's own
     # HIP runtime beside the library's, which broke ncclCommInitAll in the same process
     from opentsdb_amd import engine
-    return engine.device_count()
+    try:
+        return engine.device_count()
+    except engine.EngineError:   # no ROCm device at all
+        return 0
 
 
 def md_engine(args, n):
@@ -316,6 +322,43 @@ def md_config3(args, n):
         return out
     finally:
         eng.close()
+
+
+def md_supervise(args):
+    """--gpus N > 1: the multi-device run in a child process (this one touches no GPU), under a time
+    limit.  RCCL between distinct GPUs is first exercised on the node the driver runs this on; if
+    the child fails or hangs over RCCL (transport auto), it is run once more over peer copies and the
+    line says so.  A child that refuses the GPU count (exit 2) is final."""
+    import subprocess
+    argv = [a for a in sys.argv[1:]]
+
+    def child(extra):
+        cmd = [sys.executable, os.path.abspath(__file__)] + argv + ["--md-child"] + extra
+        try:
+            r = subprocess.run(cmd, stdout=subprocess.PIPE, timeout=args.md_timeout, cwd=ROOT)
+        except subprocess.TimeoutExpired:
+            return None, f"timed out after {args.md_timeout:.0f} s"
+        lines = [ln for ln in r.stdout.decode(errors="replace").splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not lines:
+            return r.returncode, f"exited {r.returncode}"
+        return 0, lines[-1]
+
+    rc, out = child([])
+    if rc == 0:
+        print(out, flush=True)
+        return
+    if rc == 2 or args.transport != "auto":
+        print(f"bench.py: multi-device run failed ({out})", file=sys.stderr, flush=True)
+        sys.exit(rc if rc else 1)
+    first = out
+    rc, out = child(["--transport", "copy"])
+    if rc != 0:
+        print(f"bench.py: multi-device run failed over RCCL ({first}) and over peer copies ({out})",
+              file=sys.stderr, flush=True)
+        sys.exit(rc if rc else 1)
+    line = json.loads(out)
+    line["transport_note"] = f"the RCCL run {first}; this line is the peer-copy rerun"
+    print(json.dumps(line), flush=True)
 
 
 def main_md(args):
@@ -417,7 +460,7 @@ def main():
         print(f"bench.py: --gpus {args.gpus} under a launcher with WORLD_SIZE={world}", file=sys.stderr, flush=True)
         sys.exit(2)
     if world == 1 and args.gpus > 1 and not args.pmc_child:
-        return main_md(args)
+        return main_md(args) if args.md_child else md_supervise(args)
     if args.pmc_child_config3:
         return config3_pmc_child(args, local_rank)
     dist = None
