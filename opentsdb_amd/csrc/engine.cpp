@@ -415,6 +415,7 @@ struct tsdbhip_ctx {
   int pct_qw = 0, pct_vl = 0;          // dominant uniform class of one-chunk rows (k_pct_rows)
   bool pct_vonly = false;              // every row of that class (4-byte values) all-float without NaN
                                        // or all-integer: the key kernel reads values only
+  bool pct_v6 = false;                 // ... and none over 384 values (6 values a lane)
   // tile lists by k_fast row class (built at load): [class A / class B][walker / short],
   // and the tiles of neither class (general kernel only).  Short = one row per series of at
   // most CH datapoints (k_short).
@@ -890,6 +891,7 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
   int64_t cls_vle = 0;                    // 2-byte qualifiers, 1-2 byte integers, one chunk
   int64_t cls_pct[2][9] = {};             // [qw 2/4][vl]: uniform sorted rows of <= 512 dp
   int64_t cls_vonly[2] = {};              // [qw 2/4]: those of 4-byte values, all-float without NaN or all-int
+  uint32_t vonly_max[2] = {};             // [qw 2/4]: their longest row
   for (int64_t r = 0; r < c->n_rows; r++) {
     c->h_ndp[r] = back[r].ndp;
     c->h_base[r] = back[r].base;
@@ -906,8 +908,10 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
         back[r].ndp <= 512)
       cls_pct[qw == 4][vl] += back[r].ndp;
     if (!(f & (ROW_ERR | ROW_UNSORTED)) && (qw == 2 || qw == 4) && vl == 4 && back[r].ndp <= 512 &&
-        (((f & ROW_ALLF) && !(f & ROW_NAN)) || (f & ROW_ALLI)))
+        (((f & ROW_ALLF) && !(f & ROW_NAN)) || (f & ROW_ALLI))) {
       cls_vonly[qw == 4] += back[r].ndp;
+      vonly_max[qw == 4] = std::max(vonly_max[qw == 4], back[r].ndp);
+    }
   }
   // the two largest k_fast row classes by datapoints
   struct Cand { int64_t n; int qw, vl; };
@@ -922,6 +926,7 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
     for (int v = 1; v <= 8; v++)
       if (cls_pct[a][v] > best) { best = cls_pct[a][v]; c->pct_qw = a ? 4 : 2; c->pct_vl = v; }
   c->pct_vonly = c->pct_vl == 4 && best > 0 && cls_vonly[c->pct_qw == 4] == best;
+  c->pct_v6 = c->pct_vonly && vonly_max[c->pct_qw == 4] <= 384;
   // malformed rows are reported lazily, when a query reads them (as the reference does)
   return build_tiles(c);
 }
@@ -2667,6 +2672,8 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       rp.redo_n = c->redo2_n.as<int32_t>();
       const char* venv = std::getenv("TSDBHIP_PCT_VONLY");
       rp.pct_vonly = keys && c->pct_vonly && !(venv && venv[0] == '0');
+      const char* v6env = std::getenv("TSDBHIP_PCT_V6");
+      rp.pct_v6 = rp.pct_vonly && c->pct_v6 && !(v6env && v6env[0] == '0');
       HIP_OK(launch_pct_rows(rp, c->pct_qw, c->pct_vl, c->stream));
       int32_t nback = 0;
       HIP_OK(hipMemcpyAsync(&nback, c->redo2_n.p, 4, hipMemcpyDeviceToHost, c->stream));

@@ -136,6 +136,7 @@ struct GridParams {
   // k_pct / k_emit: per-series bucket values computed before the group-by step
   int32_t sel_fn;        // TSDB_AGG_* of the percentile / median downsample function
   bool pct_vonly;        // k_pct_rows key kernel: rows certified at load, values read alone
+  bool pct_v6;           // ... and no such row over 384 values: 6 values a lane
   int64_t n_series;
   double* pre_dense;     // [n_series][K]
   uint8_t* pre_pres;     // [n_series][K]

@@ -800,9 +800,28 @@ __device__ __forceinline__ void sort8_desc(uint32_t k[DPL]) {
   cas_desc(k[1], k[2]); cas_desc(k[3], k[4]); cas_desc(k[5], k[6]);
 }
 
+// 6 keys, descending (the optimal 12-comparator network, depth 5)
+__device__ __forceinline__ void sort6_desc(uint32_t k[6]) {
+  cas_desc(k[0], k[5]); cas_desc(k[1], k[3]); cas_desc(k[2], k[4]);
+  cas_desc(k[1], k[2]); cas_desc(k[3], k[4]);
+  cas_desc(k[0], k[3]); cas_desc(k[2], k[5]);
+  cas_desc(k[0], k[1]); cas_desc(k[2], k[3]); cas_desc(k[4], k[5]);
+  cas_desc(k[1], k[2]); cas_desc(k[3], k[4]);
+}
+
+// N keys a lane (8, or 6 for rows of <= 384 values: 60 lanes of a 360-value hour row busy
+// instead of 45)
+template <int N>
+__device__ __forceinline__ void sortN_desc(uint32_t k[N]) {
+  static_assert(N == 8 || N == 6, "8 or 6 keys a lane");
+  if constexpr (N == 8) sort8_desc(k);
+  else sort6_desc(k);
+}
+
 // k-th and (k-1)-th largest key (k >= 1) of the wave's keys (0 = none); sorts k[] in place
-__device__ __forceinline__ void topk_u32(uint32_t k[DPL], int kk, uint32_t& ek, uint32_t& ek1) {
-  sort8_desc(k);
+template <int N = DPL>
+__device__ __forceinline__ void topk_u32(uint32_t k[N], int kk, uint32_t& ek, uint32_t& ek1) {
+  sortN_desc<N>(k);
   int cum = 0;
   ek = ek1 = 0;
   while (cum < kk) {
@@ -814,8 +833,8 @@ __device__ __forceinline__ void topk_u32(uint32_t k[DPL], int kk, uint32_t& ek, 
     cum += c;
     if (pop) {
 #pragma unroll
-      for (int j = 0; j < DPL - 1; j++) k[j] = k[j + 1];
-      k[DPL - 1] = 0;
+      for (int j = 0; j < N - 1; j++) k[j] = k[j + 1];
+      k[N - 1] = 0;
     }
   }
 }
@@ -832,8 +851,17 @@ __device__ __forceinline__ double unkey32(uint32_t k, bool isf) {
 }
 
 // keys of the lane (sorted descending) below t: the keys >= t are a prefix, found by a
-// branch-free binary search over the 8 keys
-__device__ __forceinline__ int lane_below(const uint32_t key[DPL], uint32_t t) {
+// branch-free binary search over the N keys
+template <int N = DPL>
+__device__ __forceinline__ int lane_below(const uint32_t key[N], uint32_t t) {
+  if constexpr (N == 6) {
+    const bool c3 = key[2] >= t;
+    const bool c2 = (c3 ? key[4] : key[0]) >= t;
+    int ge = c3 ? (c2 ? 5 : 3) : (c2 ? 1 : 0);
+    const uint32_t x = c3 ? (c2 ? key[5] : key[3]) : (c2 ? key[1] : key[0]);
+    ge += (c2 || c3) && x >= t ? 1 : 0;
+    return N - ge;
+  }
   const bool c4 = key[3] >= t;
   int ge = c4 ? 4 : 0;
   const bool c2 = (c4 ? key[5] : key[1]) >= t;
@@ -844,7 +872,8 @@ __device__ __forceinline__ int lane_below(const uint32_t key[DPL], uint32_t t) {
   return DPL - ge;
 }
 
-__device__ __forceinline__ uint32_t next_key32(const uint32_t key[DPL], uint32_t k0, int target);
+template <int N = DPL>
+__device__ __forceinline__ uint32_t next_key32(const uint32_t key[N], uint32_t k0, int target);
 
 // Keys of rank `target` and `target + 1` (0-based, ascending; k1 only when want1) among the
 // wave's 512 keys (absent = 0, counted first; each lane's 8 keys sorted descending).  Mid-rank
@@ -854,13 +883,14 @@ __device__ __forceinline__ uint32_t next_key32(const uint32_t key[DPL], uint32_t
 // free with each step).  Phase 2 compacts those keys one per lane through the wave's LDS row and
 // finishes the remaining bits with one compare + ballot each.  (The kernel is VALU-bound -- r03h
 // PMC: VALU issue ~100 % of SIMD cycles -- and phase 2's bits cost 1 VALU instead of ~16.)
-__device__ __forceinline__ void kth_pair32(const uint32_t key[DPL], int target, bool want1, uint32_t& k0,
+template <int N = DPL>
+__device__ __forceinline__ void kth_pair32(const uint32_t key[N], int target, bool want1, uint32_t& k0,
                                            uint32_t& k1) {
   __shared__ uint32_t cand_lds[4][64];
   uint32_t* cand_row = cand_lds[threadIdx.x >> 6];
   uint32_t kand = ~0u, kor = 0u;
 #pragma unroll
-  for (int j = 0; j < DPL; j++) {
+  for (int j = 0; j < N; j++) {
     if (key[j]) { kand &= key[j]; kor |= key[j]; }
   }
 #pragma unroll
@@ -875,28 +905,28 @@ __device__ __forceinline__ void kth_pair32(const uint32_t key[DPL], int target, 
   int b = 32 - __clz((int)diff);   // width of the open interval [ans, ans + 2^b)
   uint32_t ans = b == 32 ? 0u : (kand & ~((1u << b) - 1u));
   // count of keys below ans / below ans + 2^b (zeros below every present key)
-  int lowc = 0, highc = 64 * DPL;
+  int lowc = 0, highc = 64 * N;
 #pragma unroll
-  for (int j = 0; j < DPL; j++) lowc += __popcll(__ballot(key[j] == 0));
+  for (int j = 0; j < N; j++) lowc += __popcll(__ballot(key[j] == 0));
   while (b > 0 && highc - lowc > 64) {
     b--;
     const uint32_t t = ans | (1u << b);
-    const int c = __builtin_amdgcn_readlane(wave_incl_sum_dpp(lane_below(key, t)), 63);
+    const int c = __builtin_amdgcn_readlane(wave_incl_sum_dpp(lane_below<N>(key, t)), 63);
     if (c <= target) { ans = t; lowc = c; } else { highc = c; }
   }
   if (b == 0) {   // more than 64 keys equal ans
     k0 = ans;
-    k1 = want1 ? next_key32(key, ans, target) : ans;
+    k1 = want1 ? next_key32<N>(key, ans, target) : ans;
     return;
   }
   const uint32_t span = b == 32 ? ~0u : (1u << b) - 1u;   // keys in the interval: key - ans <= span
   int m = 0;
 #pragma unroll
-  for (int j = 0; j < DPL; j++) m += (key[j] != 0 && key[j] - ans <= span) ? 1 : 0;
+  for (int j = 0; j < N; j++) m += (key[j] != 0 && key[j] - ans <= span) ? 1 : 0;
   int pos = wave_incl_sum_dpp(m) - m;
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
-  for (int j = 0; j < DPL; j++) {
+  for (int j = 0; j < N; j++) {
     if (key[j] != 0 && key[j] - ans <= span) cand_row[pos++] = key[j];
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -917,15 +947,16 @@ __device__ __forceinline__ void kth_pair32(const uint32_t key[DPL], int target, 
   if (!want1) { k1 = ans; return; }
   if (__popcll(__ballot(live && c <= ans)) > t2 + 1) { k1 = ans; return; }
   if (t2 + 1 < M) { k1 = ~wave_max_u32(live && c > ans ? ~c : 0u); return; }
-  k1 = next_key32(key, ans, target);   // rank target + 1 lies above the interval
+  k1 = next_key32<N>(key, ans, target);   // rank target + 1 lies above the interval
 }
 
 // The key of rank target + 1 given k0 = the key of rank target.
-__device__ __forceinline__ uint32_t next_key32(const uint32_t key[DPL], uint32_t k0, int target) {
+template <int N>
+__device__ __forceinline__ uint32_t next_key32(const uint32_t key[N], uint32_t k0, int target) {
   int le = 0;
   uint32_t gt = ~0u;
 #pragma unroll
-  for (int j = 0; j < DPL; j++) {
+  for (int j = 0; j < N; j++) {
     le += __popcll(__ballot(key[j] <= k0));
     if (key[j] > k0) gt = min(gt, key[j]);
   }
@@ -937,8 +968,8 @@ __device__ __forceinline__ uint32_t next_key32(const uint32_t key[DPL], uint32_t
 // wf = the keys are float32 (else int32).  Near the ends the k largest / smallest keys are popped
 // (topk_u32); mid ranks take the bitwise search.  0 = more than EXT_MAX from both ends (near-end
 // variant): the caller hands the series back.
-template <bool MID>
-__device__ __forceinline__ int keys_stat(const GridParams& p, uint32_t key[DPL], int n, bool wf, double q, double& x) {
+template <bool MID, int N = DPL>
+__device__ __forceinline__ int keys_stat(const GridParams& p, uint32_t key[N], int n, bool wf, double q, double& x) {
   // select_sorted: PercentileAgg LEGACY pos = p (n + 1); Median.runDouble sorted[n / 2]
   const double pos = q * (double)(n + 1);
   int lo_i, hi_i;
@@ -954,20 +985,20 @@ __device__ __forceinline__ int keys_stat(const GridParams& p, uint32_t key[DPL],
   uint32_t ek, ek1;
   if (min(ktop, kbot) > EXT_MAX) {
     if constexpr (!MID) return 0;   // (the near-end variant keeps its registers for the extraction)
-    sort8_desc(key);
-    const int zeros = 64 * DPL - n;
+    sortN_desc<N>(key);
+    const int zeros = 64 * N - n;
     uint32_t k0, k1;
-    kth_pair32(key, zeros + lo_i, hi_i != lo_i, k0, k1);
+    kth_pair32<N>(key, zeros + lo_i, hi_i != lo_i, k0, k1);
     a = unkey32(k0, wf);
     b = unkey32(k1, wf);
   } else if (ktop <= kbot) {
-    topk_u32(key, ktop, ek, ek1);
+    topk_u32<N>(key, ktop, ek, ek1);
     a = unkey32(ek, wf);
     b = (hi_i == lo_i) ? a : unkey32(ek1, wf);
   } else {
 #pragma unroll
-    for (int j = 0; j < DPL; j++) key[j] = key[j] ? ~key[j] : 0u;   // ascending order as descending keys
-    topk_u32(key, kbot, ek, ek1);
+    for (int j = 0; j < N; j++) key[j] = key[j] ? ~key[j] : 0u;   // ascending order as descending keys
+    topk_u32<N>(key, kbot, ek, ek1);
     b = unkey32(~ek, wf);
     a = (hi_i == lo_i) ? b : unkey32(~ek1, wf);
   }
@@ -1043,8 +1074,26 @@ __device__ __forceinline__ void load_row_v(const GridParams& p, const RowLite& d
   rw.v[1] = v[1];
 }
 
-template <int QW, bool MID>
-__device__ __forceinline__ int pct_row_vkeys(const GridParams& p, const RowLite& d, const RawV& rw, double q,
+// 6 values a lane (KEYS & 8): rows of <= 384 values, 24 B a lane
+struct RawV6 {
+  uint2 v[3];
+  uint32_t lq;
+};
+
+template <int QW>
+__device__ __forceinline__ void load_row_v6(const GridParams& p, const RowLite& d, RawV6& rw) {
+  const uint8_t* q = p.qual + (d.ndp ? d.qoff + (uint64_t)(d.ndp - 1) * QW : 0);
+  rw.lq = QW == 2 ? (uint32_t)*reinterpret_cast<const uint16_t*>(q) : *reinterpret_cast<const uint32_t*>(q);
+  const int64_t i0 = (int64_t)lane_id() * 6;
+  if (i0 >= (int64_t)d.ndp) return;
+  const uint2* v = reinterpret_cast<const uint2*>(p.val + d.voff + i0 * 4);
+  rw.v[0] = v[0];
+  rw.v[1] = v[1];
+  rw.v[2] = v[2];
+}
+
+template <int QW, bool MID, int N = DPL, class R>
+__device__ __forceinline__ int pct_row_vkeys(const GridParams& p, const RowLite& d, const R& rw, double q,
                                              double& x) {
   const uint32_t lq = (uint32_t)__builtin_amdgcn_readfirstlane((int)rw.lq);
   const uint32_t off = QW == 2 ? (((((lq & 0xFFu) << 8) | ((lq >> 8) & 0xFFu)) >> 4) * 1000u)
@@ -1052,29 +1101,29 @@ __device__ __forceinline__ int pct_row_vkeys(const GridParams& p, const RowLite&
   if (off >= 3600000u) return -1;   // the row reaches past its hour: hand the series back
   const bool isf = (d.flags & ROW_ALLF) != 0;
   const int n = (int)d.ndp;
-  const int i0 = lane_id() * DPL;
-  uint32_t key[DPL];
+  const int i0 = lane_id() * N;
+  uint32_t key[N];
   const uint32_t* vw = &rw.v[0].x;
   if (isf) {
 #pragma unroll
-    for (int j = 0; j < DPL; j++) {
+    for (int j = 0; j < N; j++) {
       const uint32_t b = __builtin_bswap32(vw[j]);
       key[j] = b ^ ((uint32_t)((int32_t)b >> 31) | 0x80000000u);   // key32 of a non-NaN float32
     }
   } else {
     bool mn = false;
 #pragma unroll
-    for (int j = 0; j < DPL; j++) {
+    for (int j = 0; j < N; j++) {
       key[j] = __builtin_bswap32(vw[j]) ^ 0x80000000u;
       mn = mn || (i0 + j < n && key[j] == 0u);
     }
     if (__ballot(mn)) return -1;   // an int32 MIN value keys to 0 (= absent)
   }
-  if (i0 + DPL > n) {
+  if (i0 + N > n) {
 #pragma unroll
-    for (int j = 0; j < DPL; j++) key[j] = i0 + j < n ? key[j] : 0u;
+    for (int j = 0; j < N; j++) key[j] = i0 + j < n ? key[j] : 0u;
   }
-  return keys_stat<MID>(p, key, n, isf, q, x);
+  return keys_stat<MID, N>(p, key, n, isf, q, x);
 }
 
 // one in-range row: its buckets' order statistics into dense / pres; false = hand the
@@ -1098,7 +1147,8 @@ __device__ __forceinline__ bool pct_row(const GridParams& p, const RowLite& cd, 
       if (d.ndp == 0) return true;
       double x;
       int r;
-      if constexpr ((KEYS & 4) != 0) r = pct_row_vkeys<QW, (KEYS & 3) == 2>(p, d, rc, q, x);
+      if constexpr ((KEYS & 8) != 0) r = pct_row_vkeys<QW, (KEYS & 3) == 2, 6>(p, d, rc, q, x);
+      else if constexpr ((KEYS & 4) != 0) r = pct_row_vkeys<QW, (KEYS & 3) == 2>(p, d, rc, q, x);
       else r = pct_row_keys<QW, (KEYS & 3) == 2>(p, d, rc, q, x);
       if (r <= 0) return false;
       if (lane == 0) { dense[slot0] = x; pres[slot0] = 1; }
@@ -1155,7 +1205,8 @@ __device__ __forceinline__ bool pct_row(const GridParams& p, const RowLite& cd, 
 
 // KEYS: 0 = extraction over doubles; 1 = the 32-bit key kernel, statistics near the ends;
 // 2 = the key kernel ranking any statistic (median, p50, p75: the bitwise rank search);
-// | 4 = the key kernel over load-certified rows, values read alone (RawV)
+// | 4 = the key kernel over load-certified rows, values read alone (RawV); | 8 as well, 6 values a
+// lane (RawV6, rows of <= 384 values)
 template <int QW, int VL, int KEYS>
 __device__ __forceinline__ void load_ring_row(const GridParams& p, const RowLite& d, RawT<QW, VL>& rw) {
   load_row<QW, VL>(p, d, rw);
@@ -1163,6 +1214,10 @@ __device__ __forceinline__ void load_ring_row(const GridParams& p, const RowLite
 template <int QW, int VL, int KEYS>
 __device__ __forceinline__ void load_ring_row(const GridParams& p, const RowLite& d, RawV& rw) {
   load_row_v<QW>(p, d, rw);
+}
+template <int QW, int VL, int KEYS>
+__device__ __forceinline__ void load_ring_row(const GridParams& p, const RowLite& d, RawV6& rw) {
+  load_row_v6<QW>(p, d, rw);
 }
 
 template <int QW, int VL, int D, int KEYS>
@@ -1195,6 +1250,7 @@ __global__ __launch_bounds__(256, (KEYS & 4) ? PCT_VKEYS_OCC : KEYS ? PCT_KEYS_O
       bad = in && ((f & (ROW_ERR | ROW_UNSORTED)) || (d.base % 3600u) != 0 || (int)(f & ROW_QW_MASK) != QW ||
                    (int)((f & ROW_VL_MASK) >> ROW_VL_SHIFT) != VL || d.ndp > (uint32_t)CH);
       if ((KEYS & 4) != 0) bad = bad || (in && !(((f & ROW_ALLF) && !(f & ROW_NAN)) || (f & ROW_ALLI)));
+      if ((KEYS & 8) != 0) bad = bad || (in && d.ndp > 384u);
     }
     // strictly increasing bases (rows of one series are in base order; equal = two cells)
     const int prev = __shfl_up((int)d.base, 1, 64);
@@ -1213,7 +1269,8 @@ __global__ __launch_bounds__(256, (KEYS & 4) ? PCT_VKEYS_OCC : KEYS ? PCT_KEYS_O
     const int nin = hi - lo + 1;
     // D-deep ring, shifted by one row per step: ring[0] is row t, ring[1 .. D-1] rows
     // t+1 .. t+D-1 in flight
-    using Ring = typename std::conditional<(KEYS & 4) != 0, RawV, RawT<QW, VL>>::type;
+    using Ring = typename std::conditional<(KEYS & 8) != 0, RawV6,
+                                           typename std::conditional<(KEYS & 4) != 0, RawV, RawT<QW, VL>>::type>::type;
     Ring ring[D];
     RowLite rl[D];
 #pragma unroll
@@ -1913,6 +1970,11 @@ hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s) {
   const int DV = dvenv ? std::atoi(dvenv) : 2;
 #define PCT_ROWS_CASE(Q, V)                                                                                  \
   if (qw == Q && vl == V) {                                                                                \
+    if (V == 4 && keys && p.pct_vonly && p.pct_v6) {                                                       \
+      if (mid) hipLaunchKernelGGL((k_pct_rows<Q, V, 2, 14>), grid, block, 0, s, p);                       \
+      else hipLaunchKernelGGL((k_pct_rows<Q, V, 2, 13>), grid, block, 0, s, p);                            \
+      return hipGetLastError();                                                                            \
+    }                                                                                                      \
     if (V == 4 && keys && p.pct_vonly) {                                                                   \
       if (mid) hipLaunchKernelGGL((k_pct_rows<Q, V, 2, 6>), grid, block, 0, s, p);                        \
       else if (DV == 3) hipLaunchKernelGGL((k_pct_rows<Q, V, 3, 5>), grid, block, 0, s, p);               \

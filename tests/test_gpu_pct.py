@@ -228,16 +228,19 @@ def _vonly_batch(seed=23):
 @pytest.mark.parametrize("fn", ["p99", "p999", "p90", "ep99r7", "p75", "p50", "median"])
 def test_pct_values_only_key_rows(eng, fn, monkeypatch):
     """k_pct_rows' values-only key kernel (rows certified at load read 4 B a datapoint, one
-    qualifier a row) against the oracle, and bit-identical to the qualifier-reading key kernel
-    (TSDBHIP_PCT_VONLY=0)."""
+    qualifier a row; 6 values a lane when no row exceeds 384, else 8) against the oracle, and
+    bit-identical to the qualifier-reading key kernel (TSDBHIP_PCT_VONLY=0)."""
     b = _vonly_batch()
     res = {}
-    for vonly in ("1", "0"):
+    modes = [("1", "1"), ("1", "0"), ("0", "1")]   # (TSDBHIP_PCT_VONLY, TSDBHIP_PCT_V6)
+    for vonly, v6 in modes:
         monkeypatch.setenv("TSDBHIP_PCT_VONLY", vonly)
+        monkeypatch.setenv("TSDBHIP_PCT_V6", v6)
         for agg in ["max", "min", "none"]:
             q = abi.new_query(T0, T0 + 3 * 3600 - 1, agg, ds_function=abi.AGG[fn], ds_interval_ms=3600000)
             got = eng.run_batch(b, q)
-            assert_groups_match(got, O.run_query(b, q), agg, tol=0.0, ctx=f"{fn} {agg} vonly={vonly}")
-            res[(vonly, agg)] = got
+            assert_groups_match(got, O.run_query(b, q), agg, tol=0.0, ctx=f"{fn} {agg} vonly={vonly} v6={v6}")
+            res[(vonly, v6, agg)] = got
     for agg in ["max", "min", "none"]:
-        assert_groups_match(res[("1", agg)], res[("0", agg)], agg, tol=0.0, ctx=f"{fn} {agg} vonly vs keys")
+        for m in modes[1:]:
+            assert_groups_match(res[modes[0] + (agg,)], res[m + (agg,)], agg, tol=0.0, ctx=f"{fn} {agg} {m}")
