@@ -388,6 +388,8 @@ struct tsdbhip_ctx {
   DevBuf xbuf, gbuf;
   DevBuf m_sum, m_mn, m_mx, m_mean, m_m2, m_nl, m_nz, m_f;   // fused multi-aggregator partials
   DevBuf pre_dense, pre_pres;         // percentile / median downsampling
+  DevBuf row_ser, sr_list, sr_n, sr_mark;   // k_seq_rows: series of each row, handed-back series
+  bool row_ser_valid = false;
   DevBuf big_scratch;                  // k_pct large buckets: per-wave overflow regions
   bool mdp_valid = false;              // series_max_dp() cache (invalidated by every load)
   bool ro_meta_valid = false;          // rollup ro_ord / ro_orig / ro_allint of the loaded batch
@@ -667,6 +669,7 @@ static void release_batch(tsdbhip_ctx* c) {
   c->none_tiles_ready = false;
   c->acct_valid = false;
   c->seqd_valid = false;
+  c->row_ser_valid = false;
   c->mdp_valid = false;
   c->ro_meta_valid = false;
   c->lc_valid = false;
@@ -704,6 +707,7 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
                     &c->g_pres, &c->g_rate, &c->redo, &c->redo_n, &c->redo2, &c->redo2_n, &c->d_tl, &c->d_tl_n, &c->r1a, &c->r1b, &c->r2, &c->r_n, &c->xbuf, &c->gbuf, &c->r_rowpt,
                     &c->r_spoff, &c->r_spn, &c->r_grp, &c->r_pts, &c->r_rank, &c->r_bm, &c->r_wb, &c->r_U, &c->r_ooff,
                     &c->r_sg, &c->r_su, &c->r_ots, &c->r_obits, &c->r_oint, &c->r_coff, &c->r_cur, &c->r_voff, &c->r_vl, &c->r_vd, &c->r_vp, &c->pre_dense, &c->pre_pres,
+                    &c->row_ser, &c->sr_list, &c->sr_n, &c->sr_mark,
                     &c->ro_allint, &c->ro_ord, &c->ro_orig, &c->ro_cnt, &c->ro_vsz, &c->ro_coff, &c->ro_voff,
                     &c->big_scratch, &c->ro_agg, &c->ro_pres})
     b->release();
@@ -733,15 +737,12 @@ extern "C" int tsdbhip_sync(tsdbhip_ctx* c) {
 static int build_tiles(tsdbhip_ctx* c) {
   const int64_t n = c->n_series;
   int64_t T = 64;
-  // Keep enough waves in flight for small batches (8192 tiles), and enough tiles of heavy series
-  // that the grid's last round is a small part of the launch: a tile is one wave's work and the
-  // tiles of a uniform batch cost the same, so with ~2k waves resident the idle tail is about half
-  // a tile-time per wave slot.  Config 2 (1M series of 3600 dp): 15.6k tiles of 64 series = 7.6
-  // rounds, ~6 % tail; 62.5k tiles of 16 series = 30 rounds (the per-tile partials grow to 90 MB,
-  // 0.4 % of the bytes read).  Tiles of light series (config 3's one 360-dp row) stay at 64: they
-  // are short, and k_short gives each of a tile's series a lane.  TSDBHIP_TILE_MIN /
-  // TSDBHIP_TILE_DP override the tile-count and tile-datapoint thresholds (A/B runs).
-  int64_t min_tiles = 32768, tile_dp = 40000;
+  // Keep enough waves in flight for small batches (8192 tiles).  TSDBHIP_TILE_MIN raises the tile
+  // count for batches of heavy series (more than TSDBHIP_TILE_DP datapoints a tile): measured on
+  // config 2 (1M series of 3600 dp), 62.5k tiles of 16 series instead of 15.6k of 64 gave k_fast
+  // 3.79 vs 3.82 ms but k_reduce 0.13 vs 0.04 ms over 4x the partials -- a slower step
+  // (profiles/r04e), so the default stays at 8192.
+  int64_t min_tiles = 8192, tile_dp = 40000;
   if (const char* e = std::getenv("TSDBHIP_TILE_MIN")) min_tiles = std::max<int64_t>(1, std::atoll(e));
   if (const char* e = std::getenv("TSDBHIP_TILE_DP")) tile_dp = std::max<int64_t>(1, std::atoll(e));
   int64_t dps = 0;
@@ -2524,6 +2525,28 @@ bool fast_path_ok(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P) {
   return !(env && env[0] == '0');
 }
 
+// The series of every row, on the device (k_seq_rows), once per resident batch.
+int ensure_row_series(tsdbhip_ctx* c) {
+  if (c->row_ser_valid) return 0;
+  std::vector<int32_t> rs(std::max<int64_t>(1, c->n_rows));
+  for (int64_t s = 0; s < c->n_series; s++)
+    for (int64_t r = c->h_srp[s]; r < c->h_srp[s + 1]; r++) rs[r] = (int32_t)s;
+  HIP_OK(c->row_ser.ensure(rs.size() * 4));
+  HIP_OK(hipMemcpy(c->row_ser.p, rs.data(), rs.size() * 4, hipMemcpyHostToDevice));
+  c->row_ser_valid = true;
+  return 0;
+}
+
+// k_seq_rows takes a sequential (Java-order) downsampling when the interval divides one hour
+// and slot 0 is interval-aligned (then a bucket of an hour row aligned to the hour holds only
+// that row's datapoints; the kernel checks the rows), over rows short enough that one thread a
+// row beats k_seq_wave's wave a series (fewer than 64 datapoints a row on average).
+bool seq_rows_ok(tsdbhip_ctx* c, const Plan& P) {
+  if (const char* e = std::getenv("TSDBHIP_SEQ_ROWS")) if (e[0] == '0') return false;
+  return P.mode == MODE_GRID && P.I > 0 && 3600000 % P.I == 0 && P.B0 % P.I == 0 && P.K > 0 && !c->seqd_uniform &&
+         c->n_rows < ((int64_t)1 << 31);
+}
+
 int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bool do_reduce) {
   const bool none = P.none;
   if (none) { int rc = build_none_tiles(c); if (rc) return rc; }
@@ -2625,8 +2648,31 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     if (P.seq_dense) {
       HIP_OK(hipEventRecord(c->ev[0], c->stream));
       HIP_OK(hipMemsetAsync(c->pre_pres.p, 0, std::max<int64_t>(1, c->n_series * K), c->stream));
-      HIP_OK(launch_seq_dense(gp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->n_series, c->stream,
-                              c->seqd_uniform));
+      if (seq_rows_ok(c, P)) {
+        // every bucket inside one hour row: a thread a row, then k_seq_dense over the series
+        // whose rows broke that premise
+        int rc = ensure_row_series(c);
+        if (rc) return rc;
+        HIP_OK(c->sr_list.ensure(std::max<int64_t>(1, c->n_series) * 4));
+        HIP_OK(c->sr_mark.ensure(std::max<int64_t>(1, c->n_series) * 4));
+        HIP_OK(c->sr_n.ensure(16));
+        HIP_OK(hipMemsetAsync(c->sr_mark.p, 0, std::max<int64_t>(1, c->n_series) * 4, c->stream));
+        HIP_OK(hipMemsetAsync(c->sr_n.p, 0, 4, c->stream));
+        GridParams rp = gp;
+        rp.row_series = c->row_ser.as<int32_t>();
+        rp.redo_list = c->sr_list.as<int32_t>();
+        rp.redo_n = c->sr_n.as<int32_t>();
+        rp.redo_mark = c->sr_mark.as<uint32_t>();
+        HIP_OK(launch_seq_rows(rp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->n_rows, c->stream));
+        GridParams dp = gp;
+        dp.tile_list = c->sr_list.as<int32_t>();
+        dp.tile_list_n = c->sr_n.as<int32_t>();
+        HIP_OK(launch_seq_dense(dp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->n_series, c->stream,
+                                false));
+      } else {
+        HIP_OK(launch_seq_dense(gp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->n_series, c->stream,
+                                c->seqd_uniform));
+      }
     }
     gp.sel_fn = q->ds_function;
     gp.n_series = c->n_series;

@@ -125,6 +125,8 @@ struct GridParams {
   // k_grid over a tile list (tiles k_fast handed back): tile = tile_list[i], i < *tile_list_n
   const int32_t* tile_list;
   const int32_t* tile_list_n;
+  const int32_t* row_series;   // [n_rows] series of each row (k_seq_rows)
+  uint32_t* redo_mark;         // [n_series] a series is on redo_list (k_seq_rows)
   // k_fast: geometry in "n-units" (seconds when every row has second qualifiers and the
   // interval / slot origin are whole seconds, else milliseconds) and the redo list
   int32_t unit_s;        // 1: n-units are seconds
@@ -459,6 +461,9 @@ bool pct_rows_supported(int qw, int vl);
 hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s);
 hipError_t launch_emit(const GridParams& p, hipStream_t s);
 // sum / avg downsampling in Java's order, one series per thread, into [series][K] (k_misc.hip)
+// sum / avg downsampling in Java's order, one row per thread, when every bucket lies inside one
+// hour row; series that break the premise go to redo_list for k_seq_dense (k_misc.hip)
+hipError_t launch_seq_rows(const GridParams& p, int f, double* dense, uint8_t* pres, int64_t n_rows, hipStream_t s);
 hipError_t launch_seq_dense(const GridParams& p, int f, double* dense, uint8_t* pres, int64_t n_series, hipStream_t s,
                             bool uniform = false);   // uniform: every row of one width (k_seq_wave)
 hipError_t launch_emit_vals(const GridParams& p, hipStream_t s);

@@ -600,7 +600,6 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_row(CmpParams p, CmpKep
   const int64_t e0 = p.col_off[c0];
   const int n = (int)(p.col_off[c1] - e0);
   const uint64_t qb = p.col_qo[c0], vb = p.col_vo[c0];
-  const uint8_t* qrow = p.q + qb;
   const uint8_t* vrow = p.v + vb;
   // explode: one thread per column
   for (int64_t c = c0 + t; c < c1; c += CMP_ROW_THREADS) {

@@ -6,6 +6,43 @@
 
 namespace tsdb {
 
+// values of datapoints i0 .. i0 + 7 of a uniform row (value length vl; fl: the qualifier flags)
+__device__ __forceinline__ void seq_values(const uint8_t* vb, int64_t i0, int vl, const uint32_t fl[DPL], double val[DPL]) {
+  if (vl == 8) {
+    const uint4* v = reinterpret_cast<const uint4*>(vb + i0 * 8);
+    const uint4 a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
+    const uint32_t ws[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                             a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      const uint64_t b = ((uint64_t)__builtin_bswap32(ws[2 * j]) << 32) | __builtin_bswap32(ws[2 * j + 1]);
+      val[j] = (fl[j] & 8) ? __longlong_as_double((long long)b) : (double)(long long)b;
+    }
+  } else if (vl == 4) {
+    const uint4* v = reinterpret_cast<const uint4*>(vb + i0 * 4);
+    const uint4 a0 = v[0], a1 = v[1];
+    const uint32_t ws[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      const uint32_t be = __builtin_bswap32(ws[j]);
+      val[j] = (fl[j] & 8) ? (double)__uint_as_float(be) : (double)(int32_t)be;
+    }
+  } else if (vl == 2) {
+    const uint4 a0 = *reinterpret_cast<const uint4*>(vb + i0 * 2);
+    const uint32_t ws[4] = {a0.x, a0.y, a0.z, a0.w};
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      const uint32_t be = __builtin_bswap32(ws[j >> 1]);
+      val[j] = (double)(int16_t)(uint16_t)((j & 1) ? (be & 0xFFFF) : (be >> 16));
+    }
+  } else {
+    const uint2 a0 = *reinterpret_cast<const uint2*>(vb + i0);
+    const uint32_t ws[2] = {a0.x, a0.y};
+#pragma unroll
+    for (int j = 0; j < DPL; j++) val[j] = (double)(int8_t)((ws[j >> 2] >> ((j & 3) * 8)) & 0xFF);
+  }
+}
+
 // ---- k_seq_dense: Java's bucket order, one series per thread -------------------------
 // Sum / avg downsampling of rows whose values cannot add exactly in any order (ROW_NOCERT):
 // each thread walks its series' uniform rows in stored order, adding every bucket's values one
@@ -16,8 +53,12 @@ namespace tsdb {
 template <int F>
 __global__ __launch_bounds__(256) void k_seq_dense(GridParams p, double* __restrict__ dense, uint8_t* __restrict__ pres,
                                                    int64_t n_series) {
-  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_series) return;
+  if (p.tile_list) {   // the series k_seq_rows handed back
+    if (s >= (int64_t)*p.tile_list_n) return;
+    s = p.tile_list[s];
+  }
   const int64_t K = p.K;
   BState st;
   bs_init<F>(st);
@@ -98,39 +139,7 @@ __global__ __launch_bounds__(256) void k_seq_dense(GridParams p, double* __restr
         }
       }
       double val[DPL];
-      if (vl == 8) {
-        const uint4* v = reinterpret_cast<const uint4*>(vb + i0 * 8);
-        const uint4 a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
-        const uint32_t ws[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
-                                 a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
-#pragma unroll
-        for (int j = 0; j < DPL; j++) {
-          const uint64_t b = ((uint64_t)__builtin_bswap32(ws[2 * j]) << 32) | __builtin_bswap32(ws[2 * j + 1]);
-          val[j] = (fl[j] & 8) ? __longlong_as_double((long long)b) : (double)(long long)b;
-        }
-      } else if (vl == 4) {
-        const uint4* v = reinterpret_cast<const uint4*>(vb + i0 * 4);
-        const uint4 a0 = v[0], a1 = v[1];
-        const uint32_t ws[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-#pragma unroll
-        for (int j = 0; j < DPL; j++) {
-          const uint32_t be = __builtin_bswap32(ws[j]);
-          val[j] = (fl[j] & 8) ? (double)__uint_as_float(be) : (double)(int32_t)be;
-        }
-      } else if (vl == 2) {
-        const uint4 a0 = *reinterpret_cast<const uint4*>(vb + i0 * 2);
-        const uint32_t ws[4] = {a0.x, a0.y, a0.z, a0.w};
-#pragma unroll
-        for (int j = 0; j < DPL; j++) {
-          const uint32_t be = __builtin_bswap32(ws[j >> 1]);
-          val[j] = (double)(int16_t)(uint16_t)((j & 1) ? (be & 0xFFFF) : (be >> 16));
-        }
-      } else {
-        const uint2 a0 = *reinterpret_cast<const uint2*>(vb + i0);
-        const uint32_t ws[2] = {a0.x, a0.y};
-#pragma unroll
-        for (int j = 0; j < DPL; j++) val[j] = (double)(int8_t)((ws[j >> 2] >> ((j & 3) * 8)) & 0xFF);
-      }
+      seq_values(vb, i0, vl, fl, val);
 #pragma unroll
       for (int j = 0; j < DPL; j++) {
         if (j >= nv) break;
@@ -305,6 +314,116 @@ __global__ __launch_bounds__(64 * SEQW_WAVES) void k_seq_wave(GridParams p, doub
     dense[s * K + lane] = bs_final<F>(st);
     pres[s * K + lane] = 1;
   }
+}
+
+// ---- k_seq_rows: Java's bucket order, one row per thread ---------------------------------
+// When the interval divides one hour and slot 0 is interval-aligned, a bucket of an hour row
+// holds only that row's datapoints -- unless the row starts off the hour, reaches past it
+// (2-byte qualifiers go to 4095 s), repeats the previous row's base (two cells of one hour),
+// or is not uniform / sorted.  Each row is then its own sequential walk: the thread adds its
+// buckets' values in stored order (ValuesInInterval -> runDouble) and writes them to
+// [series][K].  Neighbouring threads read neighbouring descriptors and cells, and write
+// neighbouring buckets, where k_seq_dense's one-series-a-thread walk reads one row after the
+// other (rollup tables read as hour rows: 24 rows of a few cells a series).  A row that breaks
+// the premise hands its series back (redo_list, once per series: redo_mark), and k_seq_dense
+// recomputes those series whole afterwards, overwriting every bucket they hold.
+template <int F>
+__global__ __launch_bounds__(256) void k_seq_rows(GridParams p, double* __restrict__ dense, uint8_t* __restrict__ pres,
+                                                  int64_t n_rows) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rows) return;
+  const RowDesc d = p.rows[r];
+  if ((int64_t)d.base < p.ss || (int64_t)d.base >= p.se) return;
+  const int64_t s = p.row_series[r];
+  const int qw = d.flags & ROW_QW_MASK;
+  const int vl = (d.flags & ROW_VL_MASK) >> ROW_VL_SHIFT;
+  bool back = (d.flags & (ROW_ERR | ROW_UNSORTED)) || (d.base % 3600u) != 0 ||
+              !((qw == 2 || qw == 4) && (vl == 1 || vl == 2 || vl == 4 || vl == 8));
+  if (!back && r > p.series_row_ptr[s] && p.rows[r - 1].base == d.base) back = true;   // two cells of one hour
+  if (back) {
+    if (atomicExch(&p.redo_mark[s], 1u) == 0u) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)s;
+    return;
+  }
+  const int64_t K = p.K;
+  const RowGeom g = row_geom(p, d.base);
+  const uint8_t* qb = p.qual + d.qoff;
+  const uint8_t* vb = p.val + d.voff;
+  // pass 1: every offset inside the row's hour (sorted: the last one decides)
+  {
+    const uint32_t j = d.ndp - 1;
+    uint32_t off;
+    if (qw == 2) off = ((((uint32_t)qb[2 * j] << 8) | qb[2 * j + 1]) >> 4) * 1000u;
+    else off = ((((uint32_t)qb[4 * j] << 24) | ((uint32_t)qb[4 * j + 1] << 16) | ((uint32_t)qb[4 * j + 2] << 8) | qb[4 * j + 3]) & 0x0FFFFFC0u) >> 6;
+    if (d.ndp && off >= 3600000u) {
+      if (atomicExch(&p.redo_mark[s], 1u) == 0u) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)s;
+      return;
+    }
+  }
+  BState st;
+  bs_init<F>(st);
+  int cur = -1;
+  for (int64_t i0 = 0; i0 < (int64_t)d.ndp; i0 += DPL) {
+    const int nv = (int)min((int64_t)DPL, (int64_t)d.ndp - i0);
+    uint32_t off[DPL], fl[DPL];
+    if (qw == 2) {
+      const uint4 q = *reinterpret_cast<const uint4*>(qb + i0 * 2);
+      const uint32_t ws[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int j = 0; j < DPL; j++) {
+        const uint32_t be = __builtin_bswap32(ws[j >> 1]);
+        const uint32_t qq = (j & 1) ? (be & 0xFFFF) : (be >> 16);
+        off[j] = (qq >> 4) * 1000u;
+        fl[j] = qq & 0xF;
+      }
+    } else {
+      const uint4 q0 = *reinterpret_cast<const uint4*>(qb + i0 * 4);
+      const uint4 q1 = *reinterpret_cast<const uint4*>(qb + i0 * 4 + 16);
+      const uint32_t ws[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+      for (int j = 0; j < DPL; j++) {
+        const uint32_t qq = __builtin_bswap32(ws[j]);
+        off[j] = (qq & 0x0FFFFFC0u) >> 6;
+        fl[j] = qq & 0xF;
+      }
+    }
+    double val[DPL];
+    seq_values(vb, i0, vl, fl, val);
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      if (j >= nv) break;
+      const int k = slot_of(p, g, d.base, off[j]);
+      if (k < 0) continue;
+      if (k != cur) {
+        if (cur >= 0) {
+          dense[s * K + cur] = bs_final<F>(st);
+          pres[s * K + cur] = 1;
+        }
+        bs_init<F>(st);
+        cur = k;
+      }
+      bs_add<F>(st, val[j]);
+    }
+  }
+  if (cur >= 0) {
+    dense[s * K + cur] = bs_final<F>(st);
+    pres[s * K + cur] = 1;
+  }
+}
+
+hipError_t launch_seq_rows(const GridParams& p, int f, double* dense, uint8_t* pres, int64_t n_rows, hipStream_t s) {
+  if (n_rows <= 0) return hipSuccess;
+  const unsigned nb = (unsigned)((n_rows + 255) / 256);
+#define SEQR_CASE(FF)                                                                          \
+  case FF:                                                                                     \
+    hipLaunchKernelGGL(k_seq_rows<FF>, dim3(nb), dim3(256), 0, s, p, dense, pres, n_rows);     \
+    break;
+  switch (f) {
+    SEQR_CASE(F_SUM) SEQR_CASE(F_AVG) SEQR_CASE(F_COUNT) SEQR_CASE(F_SQUARESUM) SEQR_CASE(F_MIN) SEQR_CASE(F_MAX)
+    SEQR_CASE(F_DEV) SEQR_CASE(F_FIRST) SEQR_CASE(F_LAST) SEQR_CASE(F_DIFF) SEQR_CASE(F_MULT)
+    default: return hipErrorInvalidValue;
+  }
+#undef SEQR_CASE
+  return hipGetLastError();
 }
 
 hipError_t launch_seq_dense(const GridParams& p, int f, double* dense, uint8_t* pres, int64_t n_series, hipStream_t s,

@@ -356,3 +356,54 @@ def test_tiny_rows_at_scale_sequential(eng, tiny_rows, ds):
     assert ts.fast_ms == 0, "k_seq_dense expected"
     assert_bit_equal(seq, other, f"tiny {ds}")
     assert_groups_match(seq, O.run_query(b, q), "sum", ctx=f"tiny {ds}")
+
+
+def _short_rows_with_breaks():
+    """300 series of full-mantissa doubles in short hour rows (6 points an hour, 24 hours) -- the
+    shape of a rollup table read as hour rows -- plus rows k_seq_rows must hand back: series 3's
+    sixth row reaches 160 s past its hour (2-byte qualifiers go to 4095 s), series 7 holds two
+    cells of one hour (a repeated base), series 11 mixes 2-byte integers into its rows."""
+    rng = np.random.default_rng(31)
+    rows, gids = [], []
+    for s in range(300):
+        ts = T0 * 1000 + np.arange(24 * 6, dtype=np.int64) * 600000 + rng.integers(0, 599, 24 * 6) * 1000
+        f = rng.normal(50, 10, len(ts)) * (1 + 1e-9 * s)
+        kind = np.full(len(ts), 2)
+        lv = np.zeros(len(ts), np.int64)
+        if s == 11:
+            kind[::5] = 0
+            lv[::5] = rng.integers(-30000, 30000, len(lv[::5]))
+        r = synth.encode_rows(ts, lv, f, kind, np.zeros(len(ts), bool))
+        if s == 3:
+            base, q, v = r[5]
+            extra = [(3600 + 40 * k, float(rng.normal(50, 10))) for k in range(5)]   # (< 3840: 0xF0.. is a ms qualifier)
+            q += b"".join(((off << 4) | 0xF).to_bytes(2, "big") for off, _ in extra)
+            v = v[:-1] + b"".join(np.array([x], ">f8").tobytes() for _, x in extra) + v[-1:]
+            r[5] = (base, q, v)
+        if s == 7:
+            base, q, v = r[8]
+            r.insert(9, (base, ((3599 << 4) | 0xF).to_bytes(2, "big"), np.array([12.375], ">f8").tobytes()))
+        rows.append(r)
+        gids.append(s % 5)
+    order = sorted(range(300), key=lambda i: gids[i])
+    return synth.from_series([rows[i] for i in order], [gids[i] for i in order])
+
+
+@pytest.mark.parametrize("ds,iv", [("sum", 600000), ("avg", 3600000), ("dev", 1200000), ("first", 600000),
+                                   ("sum", 420000), ("avg", 86400000)])
+def test_sequential_rows_kernel(eng, monkeypatch, ds, iv):
+    """k_seq_rows (one thread a short hour row, Java's order inside each bucket) against
+    k_seq_dense (TSDBHIP_SEQ_ROWS=0) bit for bit and the oracle, including the series it hands
+    back (a row past its hour, two cells of one hour, mixed value kinds) and intervals it does not
+    take (7m buckets crossing rows, 1d)."""
+    b = _short_rows_with_breaks()
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("TSDBHIP_SEQ_ROWS", mode)
+        for agg in ("sum", "none"):
+            q = abi.new_query(T0, T0 + 86399, agg, ds_function=abi.AGG[ds], ds_interval_ms=iv)
+            got, tm = run_path(eng, b, q, True)
+            assert_groups_match(got, O.run_query(b, q), agg, ctx=f"{ds} {iv} {agg} rows={mode}")
+            res[(mode, agg)] = got
+    for agg in ("sum", "none"):
+        assert_bit_equal(res[("1", agg)], res[("0", agg)], f"{ds} {iv} {agg} k_seq_rows vs k_seq_dense")
