@@ -851,25 +851,31 @@ __device__ __forceinline__ double unkey32(uint32_t k, bool isf) {
 }
 
 // keys of the lane (sorted descending) below t: the keys >= t are a prefix, found by a
-// branch-free binary search over the N keys
+// branch-free binary search over the N keys.  (The keys are copied to values first: a
+// conditional over two array elements is an lvalue in C++, so clang selects between their
+// addresses, and the AMDGPU backend then moved the whole key array to LDS for the indexed load --
+// one ds_write per key and a ds_read per search step, seen in the ISA.)
 template <int N = DPL>
 __device__ __forceinline__ int lane_below(const uint32_t key[N], uint32_t t) {
   if constexpr (N == 6) {
-    const bool c3 = key[2] >= t;
-    const bool c2 = (c3 ? key[4] : key[0]) >= t;
-    int ge = c3 ? (c2 ? 5 : 3) : (c2 ? 1 : 0);
-    const uint32_t x = c3 ? (c2 ? key[5] : key[3]) : (c2 ? key[1] : key[0]);
-    ge += (c2 || c3) && x >= t ? 1 : 0;
+    const uint32_t k0 = key[0], k1 = key[1], k2 = key[2], k3 = key[3], k4 = key[4], k5 = key[5];
+    const bool c3 = k2 >= t;
+    const bool c2 = (c3 ? k4 : k0) >= t;
+    const int ge = c3 ? (c2 ? 5 : 3) : (c2 ? 1 : 0);
+    const uint32_t x = c3 ? (c2 ? k5 : k3) : (c2 ? k1 : k0);
+    return N - (ge + ((c2 || c3) && x >= t ? 1 : 0));
+  } else {
+    const uint32_t k0 = key[0], k1 = key[1], k2 = key[2], k3 = key[3], k4 = key[4], k5 = key[5], k6 = key[6],
+                   k7 = key[7];
+    const bool c4 = k3 >= t;
+    int ge = c4 ? 4 : 0;
+    const bool c2 = (c4 ? k5 : k1) >= t;
+    ge += c2 ? 2 : 0;
+    const uint32_t x = c4 ? (c2 ? k6 : k4) : (c2 ? k2 : k0);
+    ge += x >= t ? 1 : 0;
+    if (k7 >= t) ge = 8;   // (the search above resolves 0..7)
     return N - ge;
   }
-  const bool c4 = key[3] >= t;
-  int ge = c4 ? 4 : 0;
-  const bool c2 = (c4 ? key[5] : key[1]) >= t;
-  ge += c2 ? 2 : 0;
-  const uint32_t x = c4 ? (c2 ? key[6] : key[4]) : (c2 ? key[2] : key[0]);
-  ge += x >= t ? 1 : 0;
-  if (key[7] >= t) ge = 8;   // (the search above resolves 0..7)
-  return DPL - ge;
 }
 
 template <int N = DPL>
@@ -937,11 +943,12 @@ __device__ __forceinline__ void kth_pair32(const uint32_t key[N], int target, bo
   const uint32_t c = live ? cand_row[lane_id()] : ~0u;
   __builtin_amdgcn_wave_barrier();
   const int t2 = target - lowc;   // rank among the candidates
-  while (b > 0) {
-    b--;
-    const uint32_t t = ans | (1u << b);
-    const int cnt = __popcll(__ballot(live && c < t));
-    if (cnt <= t2) ans = t;
+  // (lanes past the candidates hold ~0u, never below a threshold: one compare and one popcount
+  // a bit, no lane mask)
+  for (uint32_t m = 1u << (b - 1); m != 0u; m >>= 1) {
+    const uint32_t t = ans | m;
+    const int cnt = __popcll(__ballot(c < t));
+    ans = cnt <= t2 ? t : ans;
   }
   k0 = ans;
   if (!want1) { k1 = ans; return; }
