@@ -390,6 +390,8 @@ struct tsdbhip_ctx {
   DevBuf pre_dense, pre_pres;         // percentile / median downsampling
   DevBuf row_ser, sr_list, sr_n, sr_mark;   // k_seq_rows: series of each row, handed-back series
   bool row_ser_valid = false;
+  int64_t n_grouped = -1;              // series before the first ungrouped one, when every later one
+                                       // is ungrouped (else n_series); -1 = not computed
   DevBuf big_scratch;                  // k_pct large buckets: per-wave overflow regions
   bool mdp_valid = false;              // series_max_dp() cache (invalidated by every load)
   bool ro_meta_valid = false;          // rollup ro_ord / ro_orig / ro_allint of the loaded batch
@@ -670,6 +672,7 @@ static void release_batch(tsdbhip_ctx* c) {
   c->acct_valid = false;
   c->seqd_valid = false;
   c->row_ser_valid = false;
+  c->n_grouped = -1;
   c->mdp_valid = false;
   c->ro_meta_valid = false;
   c->lc_valid = false;
@@ -2537,6 +2540,18 @@ int ensure_row_series(tsdbhip_ctx* c) {
   return 0;
 }
 
+// Series a grouped query reads: the ungrouped ones (a rollup batch's count series, spans without
+// a group) sort last and only NONE reads them, so the sequential kernels stop before them.
+int64_t grouped_prefix(tsdbhip_ctx* c) {
+  if (c->n_grouped >= 0) return c->n_grouped;
+  int64_t n = 0;
+  while (n < c->n_series && c->h_group[n] < c->n_groups) n++;
+  for (int64_t i = n; i < c->n_series; i++)
+    if (c->h_group[i] < c->n_groups) { n = c->n_series; break; }
+  c->n_grouped = n;
+  return n;
+}
+
 // k_seq_rows takes a sequential (Java-order) downsampling when the interval divides one hour
 // and slot 0 is interval-aligned (then a bucket of an hour row aligned to the hour holds only
 // that row's datapoints; the kernel checks the rows), over rows short enough that one thread a
@@ -2648,6 +2663,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     if (P.seq_dense) {
       HIP_OK(hipEventRecord(c->ev[0], c->stream));
       HIP_OK(hipMemsetAsync(c->pre_pres.p, 0, std::max<int64_t>(1, c->n_series * K), c->stream));
+      const int64_t ns = P.none ? c->n_series : grouped_prefix(c);   // series the query reads
       if (seq_rows_ok(c, P)) {
         // every bucket inside one hour row: a thread a row, then k_seq_dense over the series
         // whose rows broke that premise
@@ -2663,14 +2679,13 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
         rp.redo_list = c->sr_list.as<int32_t>();
         rp.redo_n = c->sr_n.as<int32_t>();
         rp.redo_mark = c->sr_mark.as<uint32_t>();
-        HIP_OK(launch_seq_rows(rp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->n_rows, c->stream));
+        HIP_OK(launch_seq_rows(rp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->h_srp[ns], c->stream));
         GridParams dp = gp;
         dp.tile_list = c->sr_list.as<int32_t>();
         dp.tile_list_n = c->sr_n.as<int32_t>();
-        HIP_OK(launch_seq_dense(dp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->n_series, c->stream,
-                                false));
+        HIP_OK(launch_seq_dense(dp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), ns, c->stream, false));
       } else {
-        HIP_OK(launch_seq_dense(gp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->n_series, c->stream,
+        HIP_OK(launch_seq_dense(gp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), ns, c->stream,
                                 c->seqd_uniform));
       }
     }

@@ -583,6 +583,49 @@ __global__ __launch_bounds__(256) void k_emit(GridParams p) {
   }
 }
 
+// k_emit for K <= 64 without rate: lane k owns slot k (emit_series_reg, as k_fast's register
+// partials), the tile's series are checked for scan-range rows one a lane up front, and the
+// next series' buckets are loaded while the current one is folded -- k_emit walks each series'
+// rows for that check and stages the partials in LDS (0.62 ms over a 1M-series rollup table).
+__global__ __launch_bounds__(256) void k_emit_reg(GridParams p) {
+  const int lane = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t tile = (int64_t)blockIdx.x * p.waves + wave;
+  if (tile >= p.n_tiles) return;
+  const int K = (int)p.K;
+  const int64_t s0 = p.tile_begin[tile], s1 = p.tile_end[tile];
+  bool mine = false;   // lane i: series s0 + i has a row in the scan range (tiles hold <= 64 series)
+  if (s0 + lane < s1) {
+    const int64_t s = s0 + lane;
+    for (int64_t r = p.series_row_ptr[s]; r < p.series_row_ptr[s + 1]; r++) {
+      const uint32_t base = p.rows[r].base;
+      if ((int64_t)base >= p.ss && (int64_t)base < p.se) { mine = true; break; }
+    }
+  }
+  const uint64_t act = __ballot(mine);
+  if (act && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
+  RegPart RP;
+  rp_init(p.ga, RP);
+  const bool inK = lane < K;
+  int64_t s = s0;
+  while (s < s1 && !((act >> (s - s0)) & 1)) s++;
+  bool pr = false;
+  double v = 0.0;
+  if (s < s1 && inK) { pr = p.pre_pres[s * K + lane] != 0; v = p.pre_dense[s * K + lane]; }
+  while (s < s1) {
+    int64_t sn = s + 1;
+    while (sn < s1 && !((act >> (sn - s0)) & 1)) sn++;
+    bool prn = false;
+    double vn = 0.0;
+    if (sn < s1 && inK) { prn = p.pre_pres[sn * K + lane] != 0; vn = p.pre_dense[sn * K + lane]; }
+    emit_series_reg(p, K, pr, v, RP);
+    s = sn;
+    pr = prn;
+    v = vn;
+  }
+  rp_store(p, tile, K, RP);
+}
+
 // ---- k_pct_rows: buckets inside rows, order statistics near the ends ------------------
 //
 // When the interval divides one hour (and slot 0 is interval-aligned, as the Downsampler's
@@ -2008,6 +2051,13 @@ hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s) {
 
 hipError_t launch_emit(const GridParams& p, hipStream_t s) {
   if (p.n_tiles == 0) return hipSuccess;
+  const char* renv = std::getenv("TSDBHIP_EMIT_REG");
+  if (p.K <= 64 && !p.rate && !(renv && renv[0] == '0')) {
+    GridParams q = p;
+    q.waves = 4;
+    hipLaunchKernelGGL(k_emit_reg, dim3((unsigned)((p.n_tiles + 3) / 4)), dim3(256), 0, s, q);
+    return hipGetLastError();
+  }
   const int64_t blocks = (p.n_tiles + p.waves - 1) / p.waves;
   const size_t lds = (size_t)p.wave_lds * p.waves;
   if (lds > 65536) {
