@@ -636,7 +636,45 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_row(CmpParams p, CmpKep
   // time order for second qualifiers
   int unsorted = 0;
   for (int i = t + 1; i < n; i += CMP_ROW_THREADS) unsorted |= key[i - 1] > key[i] ? 1 : 0;
-  if (__syncthreads_or(unsorted)) {
+  bool placed = false;
+  if (__syncthreads_or(unsorted) && P == 4096) {
+    // Columns out of time order whose datapoints all sit on distinct whole seconds (a second-
+    // resolution hour row of single-datapoint columns): each entry goes straight to its second
+    // -- a bitmap of the seconds (a second hit twice means duplicates: the sort below), the
+    // entries by second in ecol's space (only runs of several datapoints read ecol), then one
+    // block scan over the bitmap gives every entry its sorted position.  The same order the
+    // sort gives: the keys are distinct, so the entry bits never decide.
+    __shared__ uint32_t secmap[4096 / 32];
+    __shared__ int place_fail;
+    for (int i = t; i < 4096 / 32; i += CMP_ROW_THREADS) secmap[i] = 0;
+    if (t == 0) place_fail = 0;
+    __syncthreads();
+    for (int i = t; i < n; i += CMP_ROW_THREADS) {
+      const uint64_t off = key[i] >> 12;
+      if (off % 1000u != 0 || off >= 4096000u) { place_fail = 1; continue; }
+      const uint32_t sec = (uint32_t)(off / 1000u);
+      const uint32_t bit = 1u << (sec & 31);
+      if (atomicOr(&secmap[sec >> 5], bit) & bit) place_fail = 1;
+    }
+    __syncthreads();
+    if (!place_fail) {
+      uint16_t* by_sec = ecol;   // [4096]: the entry on each occupied second
+      for (int i = t; i < n; i += CMP_ROW_THREADS) by_sec[(uint32_t)((key[i] >> 12) / 1000u)] = (uint16_t)i;
+      const uint32_t bits = (secmap[t >> 3] >> ((t & 7) * 4)) & 0xFu;   // seconds 4t .. 4t + 3
+      int total;
+      int pos = block_excl_scan(__popc(bits), scan_sh, &total);   // (its barriers order the writes above)
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if ((bits >> j) & 1u) {
+          const uint32_t sec = 4u * (uint32_t)t + (uint32_t)j;
+          key[pos++] = ((uint64_t)(sec * 1000u) << 12) | by_sec[sec];
+        }
+      }
+      __syncthreads();
+      placed = true;
+    }
+  }
+  if (!placed && __syncthreads_or(unsorted)) {
     if (P == 4096) cmp_sort_block<4>(key, P);
     else if (P == 2048) cmp_sort_block<2>(key, P);
     else if (P == 1024) cmp_sort_block<1>(key, P);
