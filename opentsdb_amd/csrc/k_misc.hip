@@ -339,26 +339,32 @@ __global__ __launch_bounds__(256) void k_seq_rows(GridParams p, double* __restri
   const int vl = (d.flags & ROW_VL_MASK) >> ROW_VL_SHIFT;
   bool back = (d.flags & (ROW_ERR | ROW_UNSORTED)) || (d.base % 3600u) != 0 ||
               !((qw == 2 || qw == 4) && (vl == 1 || vl == 2 || vl == 4 || vl == 8));
-  if (!back && r > p.series_row_ptr[s] && p.rows[r - 1].base == d.base) back = true;   // two cells of one hour
+  // two cells of one hour: the previous row of the series has the same base (ROW_SFIRST: none)
+  if (!back && r > 0 && !(d.flags & ROW_SFIRST) && p.rows[r - 1].base == d.base) back = true;
   if (back) {
     if (atomicExch(&p.redo_mark[s], 1u) == 0u) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)s;
     return;
   }
   const int64_t K = p.K;
-  const RowGeom g = row_geom(p, d.base);
-  const uint8_t* qb = p.qual + d.qoff;
-  const uint8_t* vb = p.val + d.voff;
-  // pass 1: every offset inside the row's hour (sorted: the last one decides)
+  // slot of the row base without a 64-bit division: rel and I are exact doubles, the quotient
+  // is corrected to the exact one
+  RowGeom g;
   {
-    const uint32_t j = d.ndp - 1;
-    uint32_t off;
-    if (qw == 2) off = ((((uint32_t)qb[2 * j] << 8) | qb[2 * j + 1]) >> 4) * 1000u;
-    else off = ((((uint32_t)qb[4 * j] << 24) | ((uint32_t)qb[4 * j + 1] << 16) | ((uint32_t)qb[4 * j + 2] << 8) | qb[4 * j + 3]) & 0x0FFFFFC0u) >> 6;
-    if (d.ndp && off >= 3600000u) {
-      if (atomicExch(&p.redo_mark[s], 1u) == 0u) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)s;
-      return;
+    const int64_t rel = (int64_t)d.base * 1000 - p.B0;
+    if (rel >= 0) {
+      int64_t q0 = (int64_t)((double)rel / (double)p.I);
+      int64_t r0 = rel - q0 * p.I;
+      if (r0 < 0) { q0--; r0 += p.I; }
+      if (r0 >= p.I) { q0++; r0 -= p.I; }
+      g.q0 = q0;
+      g.r0 = r0;
+    } else {
+      g.q0 = 0;
+      g.r0 = rel;
     }
   }
+  const uint8_t* qb = p.qual + d.qoff;
+  const uint8_t* vb = p.val + d.voff;
   BState st;
   bs_init<F>(st);
   int cur = -1;
@@ -388,6 +394,16 @@ __global__ __launch_bounds__(256) void k_seq_rows(GridParams p, double* __restri
     }
     double val[DPL];
     seq_values(vb, i0, vl, fl, val);
+    // a datapoint past the row's hour (2-byte qualifiers reach 4095 s): its bucket takes the next
+    // row's datapoints too, so the series goes to k_seq_dense, which rewrites every bucket of it
+    // (the ones this row wrote already included)
+    bool past = false;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) past = past || (j < nv && off[j] >= 3600000u);
+    if (past) {
+      if (atomicExch(&p.redo_mark[s], 1u) == 0u) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)s;
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < DPL; j++) {
       if (j >= nv) break;
