@@ -934,7 +934,7 @@ __device__ __forceinline__ uint32_t next_key32(const uint32_t key[N], uint32_t k
 // PMC: VALU issue ~100 % of SIMD cycles -- and phase 2's bits cost 1 VALU instead of ~16.)
 template <int N = DPL>
 __device__ __forceinline__ void kth_pair32(const uint32_t key[N], int target, bool want1, uint32_t& k0,
-                                           uint32_t& k1) {
+                                           uint32_t& k1, int zeros) {
   __shared__ uint32_t cand_lds[4][64];
   uint32_t* cand_row = cand_lds[threadIdx.x >> 6];
   uint32_t kand = ~0u, kor = 0u;
@@ -953,14 +953,16 @@ __device__ __forceinline__ void kth_pair32(const uint32_t key[N], int target, bo
   if (diff == 0) { k0 = k1 = kand; return; }   // every present key equal
   int b = 32 - __clz((int)diff);   // width of the open interval [ans, ans + 2^b)
   uint32_t ans = b == 32 ? 0u : (kand & ~((1u << b) - 1u));
-  // count of keys below ans / below ans + 2^b (zeros below every present key)
-  int lowc = 0, highc = 64 * N;
-#pragma unroll
-  for (int j = 0; j < N; j++) lowc += __popcll(__ballot(key[j] == 0));
+  // count of keys below ans / below ans + 2^b (the absent keys, 0, below every present key)
+  int lowc = zeros, highc = 64 * N;
   while (b > 0 && highc - lowc > 64) {
     b--;
     const uint32_t t = ans | (1u << b);
-    const int c = __builtin_amdgcn_readlane(wave_incl_sum_dpp(lane_below<N>(key, t)), 63);
+    // keys below t: one compare and one popcount a key slot (the scalar unit adds; a DPP sum
+    // of per-lane counts cost ~15 more VALU instructions a step)
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < N; j++) c += __popcll(__ballot(key[j] < t));
     if (c <= target) { ans = t; lowc = c; } else { highc = c; }
   }
   if (b == 0) {   // more than 64 keys equal ans
@@ -987,9 +989,9 @@ __device__ __forceinline__ void kth_pair32(const uint32_t key[N], int target, bo
   __builtin_amdgcn_wave_barrier();
   const int t2 = target - lowc;   // rank among the candidates
   // (lanes past the candidates hold ~0u, never below a threshold: one compare and one popcount
-  // a bit, no lane mask)
-  for (uint32_t m = 1u << (b - 1); m != 0u; m >>= 1) {
-    const uint32_t t = ans | m;
+  // a bit, no lane mask; two bits a step with three thresholds took more scalar instructions)
+  for (uint32_t bit = 1u << (b - 1); bit != 0u; bit >>= 1) {
+    const uint32_t t = ans | bit;
     const int cnt = __popcll(__ballot(c < t));
     ans = cnt <= t2 ? t : ans;
   }
@@ -1038,7 +1040,7 @@ __device__ __forceinline__ int keys_stat(const GridParams& p, uint32_t key[N], i
     sortN_desc<N>(key);
     const int zeros = 64 * N - n;
     uint32_t k0, k1;
-    kth_pair32<N>(key, zeros + lo_i, hi_i != lo_i, k0, k1);
+    kth_pair32<N>(key, zeros + lo_i, hi_i != lo_i, k0, k1, zeros);
     a = unkey32(k0, wf);
     b = unkey32(k1, wf);
   } else if (ktop <= kbot) {
