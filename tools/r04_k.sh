@@ -20,9 +20,9 @@ import json
 for l in open('$out/rollup.jsonl'):
     d=json.loads(l); print(d['query'], round(d['ms_per_step'],3), d.get('check'))"
 find $out/prof_ro -name '*kernel_stats.csv' -exec cp {} $out/rollup_kernel_stats.csv \;
-python3 - <<'PY'
-import csv
-for r in list(csv.DictReader(open("gpurun_out/r04k/rollup_kernel_stats.csv")))[:8]:
+python3 - "$out" <<'PY'
+import csv, sys
+for r in list(csv.DictReader(open(sys.argv[1] + "/rollup_kernel_stats.csv")))[:8]:
     print(f"  {r['Name'][:60]:60s} calls={r['Calls']:>5s} avg_us={float(r['AverageNs'])/1e3:10.1f}")
 PY
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof_cmp -o run -- \
@@ -31,8 +31,8 @@ cat $out/compact.jsonl
 find $out/prof_cmp -name '*kernel_stats.csv' -exec cp {} $out/compact_kernel_stats.csv \;
 timeout -k 10 300 python3 tools/compact_bench.py 20000 3600 3 --scan-order > $out/compact_scan.jsonl 2> $out/compact_scan.err || exit 1
 cat $out/compact_scan.jsonl
-python3 - <<'PY'
-import csv
-for r in list(csv.DictReader(open("gpurun_out/r04k/compact_kernel_stats.csv")))[:8]:
+python3 - "$out" <<'PY'
+import csv, sys
+for r in list(csv.DictReader(open(sys.argv[1] + "/compact_kernel_stats.csv")))[:8]:
     print(f"  {r['Name'][:60]:60s} calls={r['Calls']:>5s} avg_us={float(r['AverageNs'])/1e3:10.1f}")
 PY
