@@ -43,10 +43,13 @@ __device__ __forceinline__ void cmp_fail(int32_t* row_err, int64_t row, int32_t 
   atomicCAS(&row_err[row], 0, code);
 }
 
+// the row of every column: one wave a row, its lanes striding over the row's columns (coalesced
+// stores; a thread a row wrote an hour row's 3600 entries one after the other)
 __global__ __launch_bounds__(256) void k_cmp_colrow(CmpParams p) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= p.n_rows) return;
-  for (int64_t c = p.row_col_ptr[r]; c < p.row_col_ptr[r + 1]; c++) p.col_row[c] = (int32_t)r;
+  const int64_t c1 = p.row_col_ptr[r + 1];
+  for (int64_t c = p.row_col_ptr[r] + (threadIdx.x & 63); c < c1; c += 64) p.col_row[c] = (int32_t)r;
 }
 
 // Walk of a datapoint column (ColumnDatapointIterator.update / advance), shared by the count
@@ -342,7 +345,7 @@ hipError_t scan_field(const CmpParams& p, int f, int64_t* out, void* tmp, size_t
 }  // namespace
 
 hipError_t cmp_analyze(CmpParams& p, void** tmp, size_t* tmp_bytes, hipStream_t s) {
-  if (p.n_rows > 0) hipLaunchKernelGGL(k_cmp_colrow, dim3(blocks_of(p.n_rows)), dim3(256), 0, s, p);
+  if (p.n_rows > 0) hipLaunchKernelGGL(k_cmp_colrow, dim3((unsigned)((p.n_rows + 3) / 4)), dim3(256), 0, s, p);
   if (p.n_cols > 0) hipLaunchKernelGGL(k_cmp_cols, dim3(blocks_of(p.n_cols)), dim3(256), 0, s, p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
