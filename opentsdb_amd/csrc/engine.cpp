@@ -2150,6 +2150,7 @@ struct Plan {
   bool values_only = false;      // percentile downsampling pass without the group-by step
   bool emit_only = false;        // group-by step over bucket values already in pre_dense / pre_pres
   bool seq_dense = false;        // sum / avg buckets in Java's order first (k_seq_dense), then the group-by step
+  int ro_fuse = 0;               // rollup avg (1) / count (2) stage: value rows with their count rows (k_seq_rows_ro)
   bool sel_cols = false;         // sel_direct in the (group, slot) column layout
   bool multi = false;            // fused multi-aggregator pass (run_multi_fused): partials to c->mp*, no reduce
   bool multi_dev = false;        //   ... with the Welford state (a dev query among them)
@@ -2664,7 +2665,33 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       HIP_OK(hipEventRecord(c->ev[0], c->stream));
       HIP_OK(hipMemsetAsync(c->pre_pres.p, 0, std::max<int64_t>(1, c->n_series * K), c->stream));
       const int64_t ns = P.none ? c->n_series : grouped_prefix(c);   // series the query reads
-      if (seq_rows_ok(c, P)) {
+      if (P.ro_fuse && seq_rows_ok(c, P)) {
+        // rollup avg / count: a thread a value row with its count row, combined in place; the
+        // handed-back series (value and count) through k_seq_dense, then combined
+        int rc = ensure_row_series(c);
+        if (rc) return rc;
+        HIP_OK(c->sr_list.ensure(std::max<int64_t>(1, c->n_series) * 4));
+        HIP_OK(c->sr_mark.ensure(std::max<int64_t>(1, c->n_series) * 4));
+        HIP_OK(c->sr_n.ensure(16));
+        HIP_OK(hipMemsetAsync(c->sr_mark.p, 0, std::max<int64_t>(1, c->n_series) * 4, c->stream));
+        HIP_OK(hipMemsetAsync(c->sr_n.p, 0, 4, c->stream));
+        GridParams rp = gp;
+        rp.row_series = c->row_ser.as<int32_t>();
+        rp.redo_list = c->sr_list.as<int32_t>();
+        rp.redo_n = c->sr_n.as<int32_t>();
+        rp.redo_mark = c->sr_mark.as<uint32_t>();
+        const int avg = P.ro_fuse == 1 ? 1 : 0;
+        HIP_OK(launch_seq_rows_ro(rp, avg, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->ro_cmap.as<int64_t>(),
+                                  c->n_rows, c->stream));
+        GridParams dp = gp;
+        dp.tile_list = c->sr_list.as<int32_t>();
+        dp.tile_list_n = c->sr_n.as<int32_t>();
+        HIP_OK(launch_seq_dense(dp, F_SUM, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->n_series, c->stream,
+                                false));
+        HIP_OK(launch_rollup_combine_list(c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->ro_cmap.as<int64_t>(),
+                                          c->sr_list.as<int32_t>(), c->sr_n.as<int32_t>(), c->n_series, K, avg,
+                                          c->stream));
+      } else if (seq_rows_ok(c, P)) {
         // every bucket inside one hour row: a thread a row, then k_seq_dense over the series
         // whose rows broke that premise
         int rc = ensure_row_series(c);
@@ -4026,16 +4053,24 @@ int ro_stage(tsdbhip_ctx* c, const tsdbhip_query* q, const tsdbhip_query& qr, Pl
   P1.gsel = 0;
   P1.ordered = false;
   P1.gslot = grid_wave_lds(P.K, false, false) > 40 * 1024;
+  bool fused = false;
   if (seq_dense_wanted(c, P1)) {   // sums that cannot add in any order: k_seq_dense, Java's order, one pass
     P1.seq_dense = true;
     P1.values_only = true;
+    // value rows with their lock-step count rows in one pass (k_seq_rows_ro), combined in place
+    const char* fenv = std::getenv("TSDBHIP_RO_FUSE");
+    if (seq_rows_ok(c, P1) && !(fenv && fenv[0] == '0')) {
+      P1.ro_fuse = q->ds_function == TSDB_AGG_AVG ? 1 : 2;
+      fused = true;
+    }
   } else {
     P1.dense_out = true;
   }
   rc = run_device(c, &q1, P1, c->n_series, false);
   if (rc) return rc;
-  HIP_OK(launch_rollup_combine(c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->ro_cmap.as<int64_t>(),
-                               c->n_series, P.K, q->ds_function == TSDB_AGG_AVG ? 1 : 0, c->stream));
+  if (!fused)
+    HIP_OK(launch_rollup_combine(c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->ro_cmap.as<int64_t>(),
+                                 c->n_series, P.K, q->ds_function == TSDB_AGG_AVG ? 1 : 0, c->stream));
   P.emit_only = true;
   return 0;
 }

@@ -464,6 +464,11 @@ hipError_t launch_emit(const GridParams& p, hipStream_t s);
 // sum / avg downsampling in Java's order, one row per thread, when every bucket lies inside one
 // hour row; series that break the premise go to redo_list for k_seq_dense (k_misc.hip)
 hipError_t launch_seq_rows(const GridParams& p, int f, double* dense, uint8_t* pres, int64_t n_rows, hipStream_t s);
+// rollup avg / count: a value row with its lock-step count row, combined in place (k_misc.hip)
+hipError_t launch_seq_rows_ro(const GridParams& p, int avg, double* dense, uint8_t* pres, const int64_t* cmap, int64_t n_rows,
+                              hipStream_t s);
+hipError_t launch_rollup_combine_list(double* dense, const uint8_t* pres, const int64_t* cmap, const int32_t* list,
+                                      const int32_t* list_n, int64_t n_max, int64_t K, int avg, hipStream_t s);
 hipError_t launch_seq_dense(const GridParams& p, int f, double* dense, uint8_t* pres, int64_t n_series, hipStream_t s,
                             bool uniform = false);   // uniform: every row of one width (k_seq_wave)
 hipError_t launch_emit_vals(const GridParams& p, hipStream_t s);

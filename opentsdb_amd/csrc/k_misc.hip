@@ -442,6 +442,168 @@ hipError_t launch_seq_rows(const GridParams& p, int f, double* dense, uint8_t* p
   return hipGetLastError();
 }
 
+// ---- k_seq_rows_ro: rollup avg / count downsampling, a value row with its count row ------
+// A rollup batch with count cells holds, for every value series, a count series whose hour rows
+// the load wrote in lock step with the value rows (tsdbhip_load_rollup: same bases, same
+// offsets).  With k_seq_rows' premise (buckets inside hour rows), one thread takes a value row
+// and its count row: Σsum in Java's order (the SUM downsampler over the value cells), Σcount
+// (exact integer sums), and writes the bucket as k_rollup_combine would: Σsum / Σcount (0 when
+// Σcount is 0) for avg, Σcount for count.  No thread for the count rows, no combine pass.  A row
+// pair that breaks a premise (k_seq_rows' checks, rows out of lock step, a count row that is not
+// uniform integers) hands both series to k_seq_dense, and k_rollup_combine_list combines them.
+template <int AVG>
+__global__ __launch_bounds__(256) void k_seq_rows_ro(GridParams p, double* __restrict__ dense, uint8_t* __restrict__ pres,
+                                                     const int64_t* __restrict__ cmap, int64_t n_rows) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rows) return;
+  const int64_t s = p.row_series[r];
+  const int64_t cs = cmap[s];
+  if (cs < 0) return;   // a count row: its value row takes it
+  const RowDesc d = p.rows[r];
+  if ((int64_t)d.base < p.ss || (int64_t)d.base >= p.se) return;
+  const int64_t rc = p.series_row_ptr[cs] + (r - p.series_row_ptr[s]);
+  const int qw = d.flags & ROW_QW_MASK;
+  const int vl = (d.flags & ROW_VL_MASK) >> ROW_VL_SHIFT;
+  auto hand_back = [&]() {
+    if (atomicExch(&p.redo_mark[s], 1u) == 0u) {
+      const int32_t at = atomicAdd(p.redo_n, 2);
+      p.redo_list[at] = (int32_t)s;
+      p.redo_list[at + 1] = (int32_t)cs;
+    }
+  };
+  bool back = (d.flags & (ROW_ERR | ROW_UNSORTED)) || (d.base % 3600u) != 0 ||
+              !((qw == 2 || qw == 4) && (vl == 1 || vl == 2 || vl == 4 || vl == 8));
+  if (!back && r > 0 && !(d.flags & ROW_SFIRST) && p.rows[r - 1].base == d.base) back = true;
+  RowDesc dc{};
+  if (!back) {
+    if (rc >= p.series_row_ptr[cs + 1]) back = true;
+    else dc = p.rows[rc];
+  }
+  const int qwc = dc.flags & ROW_QW_MASK;
+  const int vlc = (dc.flags & ROW_VL_MASK) >> ROW_VL_SHIFT;
+  if (!back && (dc.base != d.base || dc.ndp != d.ndp || (dc.flags & (ROW_ERR | ROW_UNSORTED)) || !(dc.flags & ROW_ALLI) ||
+                qwc != 2 || !(vlc == 1 || vlc == 2 || vlc == 4 || vlc == 8)))
+    back = true;
+  if (back) {
+    hand_back();
+    return;
+  }
+  const int64_t K = p.K;
+  RowGeom g;
+  {
+    const int64_t rel = (int64_t)d.base * 1000 - p.B0;
+    if (rel >= 0) {
+      int64_t q0 = (int64_t)((double)rel / (double)p.I);
+      int64_t r0 = rel - q0 * p.I;
+      if (r0 < 0) { q0--; r0 += p.I; }
+      if (r0 >= p.I) { q0++; r0 -= p.I; }
+      g.q0 = q0;
+      g.r0 = r0;
+    } else {
+      g.q0 = 0;
+      g.r0 = rel;
+    }
+  }
+  const uint8_t* qb = p.qual + d.qoff;
+  const uint8_t* vb = p.val + d.voff;
+  const uint8_t* vbc = p.val + dc.voff;
+  BState sv, sc;
+  bs_init<F_SUM>(sv);
+  bs_init<F_SUM>(sc);
+  int cur = -1;
+  auto flush = [&]() {
+    if (cur < 0) return;
+    const double sum = bs_final<F_SUM>(sv), count = bs_final<F_SUM>(sc);
+    dense[s * K + cur] = AVG ? (count == 0.0 ? 0.0 : sum / count) : count;
+    pres[s * K + cur] = 1;
+  };
+  const uint32_t fl_int[DPL] = {0, 0, 0, 0, 0, 0, 0, 0};   // count cells: integers
+  for (int64_t i0 = 0; i0 < (int64_t)d.ndp; i0 += DPL) {
+    const int nv = (int)min((int64_t)DPL, (int64_t)d.ndp - i0);
+    uint32_t off[DPL], fl[DPL];
+    if (qw == 2) {
+      const uint4 q = *reinterpret_cast<const uint4*>(qb + i0 * 2);
+      const uint32_t ws[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int j = 0; j < DPL; j++) {
+        const uint32_t be = __builtin_bswap32(ws[j >> 1]);
+        const uint32_t qq = (j & 1) ? (be & 0xFFFF) : (be >> 16);
+        off[j] = (qq >> 4) * 1000u;
+        fl[j] = qq & 0xF;
+      }
+    } else {
+      const uint4 q0 = *reinterpret_cast<const uint4*>(qb + i0 * 4);
+      const uint4 q1 = *reinterpret_cast<const uint4*>(qb + i0 * 4 + 16);
+      const uint32_t ws[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+      for (int j = 0; j < DPL; j++) {
+        const uint32_t qq = __builtin_bswap32(ws[j]);
+        off[j] = (qq & 0x0FFFFFC0u) >> 6;
+        fl[j] = qq & 0xF;
+      }
+    }
+    bool past = false;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) past = past || (j < nv && off[j] >= 3600000u);
+    if (past) {
+      hand_back();
+      return;
+    }
+    double val[DPL], cnt[DPL];
+    seq_values(vb, i0, vl, fl, val);
+    seq_values(vbc, i0, vlc, fl_int, cnt);
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      if (j >= nv) break;
+      const int k = slot_of(p, g, d.base, off[j]);
+      if (k < 0) continue;
+      if (k != cur) {
+        flush();
+        bs_init<F_SUM>(sv);
+        bs_init<F_SUM>(sc);
+        cur = k;
+      }
+      bs_add<F_SUM>(sv, val[j]);
+      bs_add<F_SUM>(sc, cnt[j]);
+    }
+  }
+  flush();
+}
+
+// k_rollup_combine over the listed series (the ones k_seq_rows_ro handed back; count series in
+// the list have no count map entry and are skipped)
+__global__ __launch_bounds__(256) void k_rollup_combine_list(double* __restrict__ dense, const uint8_t* __restrict__ pres,
+                                                             const int64_t* __restrict__ cmap, const int32_t* __restrict__ list,
+                                                             const int32_t* __restrict__ list_n, int64_t K, int avg) {
+  const int64_t n = *list_n;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n * K; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = list[i / K];
+    const int64_t cs = cmap[s];
+    const int64_t k = i % K;
+    if (cs < 0 || !pres[s * K + k]) continue;
+    const double sum = dense[s * K + k];
+    const double count = pres[cs * K + k] ? dense[cs * K + k] : 0.0;
+    dense[s * K + k] = avg ? (count == 0.0 ? 0.0 : sum / count) : count;
+  }
+}
+
+hipError_t launch_seq_rows_ro(const GridParams& p, int avg, double* dense, uint8_t* pres, const int64_t* cmap, int64_t n_rows,
+                              hipStream_t s) {
+  if (n_rows <= 0) return hipSuccess;
+  const unsigned nb = (unsigned)((n_rows + 255) / 256);
+  if (avg) hipLaunchKernelGGL(k_seq_rows_ro<1>, dim3(nb), dim3(256), 0, s, p, dense, pres, cmap, n_rows);
+  else hipLaunchKernelGGL(k_seq_rows_ro<0>, dim3(nb), dim3(256), 0, s, p, dense, pres, cmap, n_rows);
+  return hipGetLastError();
+}
+
+hipError_t launch_rollup_combine_list(double* dense, const uint8_t* pres, const int64_t* cmap, const int32_t* list,
+                                      const int32_t* list_n, int64_t n_max, int64_t K, int avg, hipStream_t s) {
+  if (n_max * K <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((n_max * K + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_rollup_combine_list, dim3((unsigned)blocks), dim3(256), 0, s, dense, pres, cmap, list, list_n, K, avg);
+  return hipGetLastError();
+}
+
 hipError_t launch_seq_dense(const GridParams& p, int f, double* dense, uint8_t* pres, int64_t n_series, hipStream_t s,
                             bool uniform) {
   if (n_series <= 0) return hipSuccess;

@@ -163,7 +163,7 @@ def test_run_multi_over_rollup(eng):
 
 
 def random_table(rng, n_series, n_groups, days, p_sum=0.9, p_cnt=0.9, floats=False, counts=True,
-                 interval="10m", span="6h"):
+                 interval="10m", span="6h", cnt_hi=40):
     """Rollup rows of n_series series over `days` days with cells missing at random."""
     iv = _iv(interval, span)
     step = iv.interval_s
@@ -180,14 +180,15 @@ def random_table(rng, n_series, n_groups, days, p_sum=0.9, p_cnt=0.9, floats=Fal
             has_c = rng.random(n) < p_cnt
             fv = rng.normal(100, 50, n)
             iv_ = rng.integers(-1000, 100000, n)
-            cv = rng.integers(0, 40, n)
+            cv = rng.integers(0, cnt_hi, n)
             vals, cnts = [], []
             for j, o in enumerate(offs):
                 if has_v[j]:
                     vals.append((o, 0xF, struct.pack(">d", float(fv[j]))) if floats else
                                 (o, 0x7, struct.pack(">q", int(iv_[j]))))
                 if counts and has_c[j]:
-                    cnts.append((o, 0x0, struct.pack(">b", int(cv[j]))))
+                    cnts.append((o, 0x0, struct.pack(">b", int(cv[j]))) if cv[j] < 128 else
+                                (o, 0x1, struct.pack(">h", int(cv[j]))))
             if vals or cnts:
                 rr.append((base, vals, cnts))
         rows.append(rr)
@@ -248,3 +249,28 @@ def test_larger_table_properties(eng):
     got = eng.run(q)
     want = O.run_rollup_query(rb, q)
     assert_groups_match(got, want, "sum", tol=0.0, ctx="1000 series count")
+
+
+@pytest.mark.parametrize("cnt_hi", [40, 3000])
+def test_fused_avg_count_stage(eng, monkeypatch, cnt_hi):
+    """Rollup avg / count downsampling over full-mantissa sums: k_seq_rows_ro (a value row with its
+    lock-step count row, combined in place) bit-identical to the separate passes + k_rollup_combine
+    (TSDBHIP_RO_FUSE=0) and within the oracle's tolerance; counts up to 3000 make count rows of
+    mixed 1- and 2-byte cells, which hand their series back (k_seq_dense + the list combine)."""
+    rng = np.random.default_rng(17 + cnt_hi)
+    rb = random_table(rng, 40, 4, 2, floats=True, cnt_hi=cnt_hi)
+    eng.load_rollup(rb)
+    for ds in ("10m-avg", "1h-avg", "30m-count", "20m-avg-nan", "1d-avg"):
+        for agg in ("sum", "none", "p90"):
+            q = _q(ds, agg, start=B + 1800, end=B + 2 * 86400)
+            res = {}
+            for fuse in ("1", "0"):
+                monkeypatch.setenv("TSDBHIP_RO_FUSE", fuse)
+                res[fuse] = eng.run(q)
+            assert len(res["1"]) == len(res["0"])
+            for (g1, t1, b1, i1), (g2, t2, b2, i2) in zip(res["1"], res["0"]):
+                assert g1 == g2
+                np.testing.assert_array_equal(t1, t2, err_msg=f"{ds} {agg}")
+                np.testing.assert_array_equal(b1, b2, err_msg=f"{ds} {agg}: fused vs separate passes")
+                np.testing.assert_array_equal(i1, i2, err_msg=f"{ds} {agg}")
+            assert_groups_match(res["1"], O.run_rollup_query(rb, q), agg, tol=1e-12, ctx=f"{ds} {agg}")
