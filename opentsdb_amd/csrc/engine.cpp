@@ -463,6 +463,7 @@ struct tsdbhip_ctx {
   std::vector<std::string> ro_unsup;   // per value series: why the engine does not run it ("" = runs)
   std::vector<int64_t> ro_res;         // batch position -> resident index
   DevBuf ro_cmap;                      // [n_series] resident index of a value series' count series (-1: none)
+  DevBuf ro_partner;                   // [n_rows] a value row's lock-step count row (GridParams.ro_partner)
   // query-time compaction (tsdbhip_load_cells): rows whose compaction failed, raised when a
   // query's scan range covers them (SaltScanner.processRow fails the scan)
   struct CmpErr { int64_t series, row; int64_t base; int32_t code; };
@@ -687,6 +688,7 @@ static void release_batch(tsdbhip_ctx* c) {
   c->ro_unsup.clear();
   c->ro_res.clear();
   c->ro_cmap.release();
+  c->ro_partner.release();
   c->cmp_errs.clear();
   c->compact_ms = 0;
 }
@@ -1425,6 +1427,18 @@ extern "C" int tsdbhip_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* r
     for (int64_t s = 0; s < NS; s++) cmap[c->ro_res[s]] = c->ro_res[NS + s];
   HIP_OK(c->ro_cmap.ensure((int64_t)cmap.size() * 8));
   HIP_OK(hipMemcpy(c->ro_cmap.p, cmap.data(), cmap.size() * 8, hipMemcpyHostToDevice));
+  if (cnt) {   // each value row's count row: the load wrote them in lock step
+    std::vector<int32_t> partner(std::max<int64_t>(1, c->n_rows), -1);
+    for (int64_t s = 0; s < c->n_series; s++) {
+      const int64_t cs = cmap[s];
+      if (cs < 0) continue;
+      const int64_t n = c->h_srp[s + 1] - c->h_srp[s];
+      const bool mirror = c->h_srp[cs + 1] - c->h_srp[cs] == n;
+      for (int64_t k = 0; k < n; k++) partner[c->h_srp[s] + k] = mirror ? (int32_t)(c->h_srp[cs] + k) : -2;
+    }
+    HIP_OK(c->ro_partner.ensure((int64_t)partner.size() * 4));
+    HIP_OK(hipMemcpy(c->ro_partner.p, partner.data(), partner.size() * 4, hipMemcpyHostToDevice));
+  }
   return 0;
 }
 
@@ -2680,6 +2694,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
         rp.redo_list = c->sr_list.as<int32_t>();
         rp.redo_n = c->sr_n.as<int32_t>();
         rp.redo_mark = c->sr_mark.as<uint32_t>();
+        rp.ro_partner = c->ro_partner.as<int32_t>();
         const int avg = P.ro_fuse == 1 ? 1 : 0;
         HIP_OK(launch_seq_rows_ro(rp, avg, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->ro_cmap.as<int64_t>(),
                                   c->n_rows, c->stream));
@@ -4059,7 +4074,7 @@ int ro_stage(tsdbhip_ctx* c, const tsdbhip_query* q, const tsdbhip_query& qr, Pl
     P1.values_only = true;
     // value rows with their lock-step count rows in one pass (k_seq_rows_ro), combined in place
     const char* fenv = std::getenv("TSDBHIP_RO_FUSE");
-    if (seq_rows_ok(c, P1) && !(fenv && fenv[0] == '0')) {
+    if (seq_rows_ok(c, P1) && c->ro_partner.p && !(fenv && fenv[0] == '0')) {
       P1.ro_fuse = q->ds_function == TSDB_AGG_AVG ? 1 : 2;
       fused = true;
     }

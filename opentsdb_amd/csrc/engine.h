@@ -127,6 +127,8 @@ struct GridParams {
   const int32_t* tile_list_n;
   const int32_t* row_series;   // [n_rows] series of each row (k_seq_rows)
   uint32_t* redo_mark;         // [n_series] a series is on redo_list (k_seq_rows)
+  const int32_t* ro_partner;   // [n_rows] rollup batch: a value row's count row (-1: a count row,
+                               // -2: the count series does not mirror the value series' rows)
   // k_fast: geometry in "n-units" (seconds when every row has second qualifiers and the
   // interval / slot origin are whole seconds, else milliseconds) and the redo list
   int32_t unit_s;        // 1: n-units are seconds

@@ -456,29 +456,25 @@ __global__ __launch_bounds__(256) void k_seq_rows_ro(GridParams p, double* __res
                                                      const int64_t* __restrict__ cmap, int64_t n_rows) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n_rows) return;
+  const int32_t rc = p.ro_partner[r];   // the count row (loaded beside the series and descriptor)
   const int64_t s = p.row_series[r];
-  const int64_t cs = cmap[s];
-  if (cs < 0) return;   // a count row: its value row takes it
+  if (rc == -1) return;                 // a count row: its value row takes it
   const RowDesc d = p.rows[r];
   if ((int64_t)d.base < p.ss || (int64_t)d.base >= p.se) return;
-  const int64_t rc = p.series_row_ptr[cs] + (r - p.series_row_ptr[s]);
   const int qw = d.flags & ROW_QW_MASK;
   const int vl = (d.flags & ROW_VL_MASK) >> ROW_VL_SHIFT;
   auto hand_back = [&]() {
     if (atomicExch(&p.redo_mark[s], 1u) == 0u) {
       const int32_t at = atomicAdd(p.redo_n, 2);
       p.redo_list[at] = (int32_t)s;
-      p.redo_list[at + 1] = (int32_t)cs;
+      p.redo_list[at + 1] = (int32_t)cmap[s];
     }
   };
-  bool back = (d.flags & (ROW_ERR | ROW_UNSORTED)) || (d.base % 3600u) != 0 ||
+  bool back = rc < 0 || (d.flags & (ROW_ERR | ROW_UNSORTED)) || (d.base % 3600u) != 0 ||
               !((qw == 2 || qw == 4) && (vl == 1 || vl == 2 || vl == 4 || vl == 8));
   if (!back && r > 0 && !(d.flags & ROW_SFIRST) && p.rows[r - 1].base == d.base) back = true;
   RowDesc dc{};
-  if (!back) {
-    if (rc >= p.series_row_ptr[cs + 1]) back = true;
-    else dc = p.rows[rc];
-  }
+  if (!back) dc = p.rows[rc];
   const int qwc = dc.flags & ROW_QW_MASK;
   const int vlc = (dc.flags & ROW_VL_MASK) >> ROW_VL_SHIFT;
   if (!back && (dc.base != d.base || dc.ndp != d.ndp || (dc.flags & (ROW_ERR | ROW_UNSORTED)) || !(dc.flags & ROW_ALLI) ||
