@@ -942,13 +942,21 @@ __device__ __forceinline__ void kth_pair32(const uint32_t key[N], int target, bo
   for (int j = 0; j < N; j++) {
     if (key[j]) { kand &= key[j]; kor |= key[j]; }
   }
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    kand &= (uint32_t)__shfl_xor((int)kand, d, 64);
-    kor |= (uint32_t)__shfl_xor((int)kor, d, 64);
-  }
-  kand = (uint32_t)__builtin_amdgcn_readfirstlane((int)kand);
-  kor = (uint32_t)__builtin_amdgcn_readfirstlane((int)kor);
+  // wave AND / OR by DPP (row shifts, then the row broadcasts; lane 63 ends with the whole wave)
+  kand &= (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)kand, 0x111, 0xF, 0xF, false);
+  kor |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kor, 0x111, 0xF, 0xF, false);
+  kand &= (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)kand, 0x112, 0xF, 0xF, false);
+  kor |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kor, 0x112, 0xF, 0xF, false);
+  kand &= (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)kand, 0x114, 0xF, 0xF, false);
+  kor |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kor, 0x114, 0xF, 0xF, false);
+  kand &= (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)kand, 0x118, 0xF, 0xF, false);
+  kor |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kor, 0x118, 0xF, 0xF, false);
+  kand &= (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)kand, 0x142, 0xA, 0xF, false);
+  kor |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kor, 0x142, 0xA, 0xF, false);
+  kand &= (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)kand, 0x143, 0xC, 0xF, false);
+  kor |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kor, 0x143, 0xC, 0xF, false);
+  kand = (uint32_t)__builtin_amdgcn_readlane((int)kand, 63);
+  kor = (uint32_t)__builtin_amdgcn_readlane((int)kor, 63);
   const uint32_t diff = kand ^ kor;
   if (diff == 0) { k0 = k1 = kand; return; }   // every present key equal
   int b = 32 - __clz((int)diff);   // width of the open interval [ans, ans + 2^b)
@@ -988,18 +996,26 @@ __device__ __forceinline__ void kth_pair32(const uint32_t key[N], int target, bo
   const uint32_t c = live ? cand_row[lane_id()] : ~0u;
   __builtin_amdgcn_wave_barrier();
   const int t2 = target - lowc;   // rank among the candidates
-  // (lanes past the candidates hold ~0u, never below a threshold: one compare and one popcount
-  // a bit, no lane mask; two bits a step with three thresholds took more scalar instructions)
-  for (uint32_t bit = 1u << (b - 1); bit != 0u; bit >>= 1) {
-    const uint32_t t = ans | bit;
-    const int cnt = __popcll(__ballot(c < t));
-    ans = cnt <= t2 ? t : ans;
+  // The candidates sorted across the wave (bitonic, one per lane; lanes past them hold ~0u and
+  // sort last): ranks t2 and t2 + 1 are lanes t2 and t2 + 1.  21 compare-exchange steps of a
+  // shuffle, a min and a max -- the bit-by-bit search it replaces cost one compare and ~8 scalar
+  // instructions for each of the ~20 open key bits, and the kernel is bound by the scalar unit.
+  const int lane = lane_id();
+  uint32_t v = c;
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const uint32_t o = (uint32_t)__shfl_xor((int)v, j, 64);
+      const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+      v = keep_min ? min(v, o) : max(v, o);
+    }
   }
-  k0 = ans;
-  if (!want1) { k1 = ans; return; }
-  if (__popcll(__ballot(live && c <= ans)) > t2 + 1) { k1 = ans; return; }
-  if (t2 + 1 < M) { k1 = ~wave_max_u32(live && c > ans ? ~c : 0u); return; }
-  k1 = next_key32<N>(key, ans, target);   // rank target + 1 lies above the interval
+  (void)ans;
+  k0 = (uint32_t)__builtin_amdgcn_readlane((int)v, t2);
+  if (!want1) { k1 = k0; return; }
+  if (t2 + 1 < M) { k1 = (uint32_t)__builtin_amdgcn_readlane((int)v, t2 + 1); return; }
+  k1 = next_key32<N>(key, k0, target);   // rank target + 1 lies above the interval
 }
 
 // The key of rank target + 1 given k0 = the key of rank target.
