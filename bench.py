@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--pmc-child-config3", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--md-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--c3-series", type=int, default=10_000_000, help=argparse.SUPPRESS)   # rehearsals only
     ap.add_argument("--md-timeout", type=float, default=480.0,
                     help="--gpus N > 1: seconds the multi-device run may take before it is retried over peer copies")
     return ap.parse_args()
@@ -250,6 +251,18 @@ def visible_gpus() -> int:
         return 0
 
 
+def md_devices(n):
+    """GPUs 0..n-1; TSDBHIP_BENCH_DEVICES="0,0" (rehearsal hook) repeats devices so the
+    multi-device bench path runs on a one-GPU box (peer copies between shards of one GPU)."""
+    env = os.environ.get("TSDBHIP_BENCH_DEVICES")
+    if env:
+        devs = [int(x) for x in env.split(",") if x.strip()]
+        if len(devs) != n:
+            raise SystemExit(f"bench.py: TSDBHIP_BENCH_DEVICES lists {len(devs)} devices, --gpus {n}")
+        return devs
+    return list(range(n))
+
+
 def md_engine(args, n):
     """One multi-device context over GPUs 0..n-1, series shards.  RCCL unless --transport copy;
     when the RCCL communicator cannot be built, peer copies (reported in the line)."""
@@ -257,12 +270,12 @@ def md_engine(args, n):
     tr = {"auto": E.MD_AUTO, "rccl": E.MD_RCCL, "copy": E.MD_COPY}[args.transport]
     note = None
     try:
-        eng = E.Engine(devices=list(range(n)), transport=tr)
+        eng = E.Engine(devices=md_devices(n), transport=tr)
     except E.EngineError as ex:
         if args.transport != "auto":
             raise
         note = f"RCCL init failed ({ex}); peer copies used"
-        eng = E.Engine(devices=list(range(n)), transport=E.MD_COPY)
+        eng = E.Engine(devices=md_devices(n), transport=E.MD_COPY)
     eng.shard_mode(E.SHARD_SERIES)
     return eng, note
 
@@ -284,14 +297,14 @@ def md_config3(args, n):
     eng, note = md_engine(args, n)
     try:
         t = time.perf_counter()
-        eng.synth(10_000_000, T0, hours * 360, 10000, 2, 1000, 30000, 0x5EED)
+        eng.synth(args.c3_series, T0, hours * 360, 10000, 2, 1000, 30000, 0x5EED)
         eng.sync()
         synth_s = time.perf_counter() - t
 
         def q(agg):
             return abi.new_query(T0, T0 + hours * 3600 - 1, agg, ds_function=abi.AGG["avg"], ds_interval_ms=60000)
 
-        out = {"workload": f"BASELINE config 3: 10M series x {hours} h @10 s (int/float32 alternating), 1000 groups, "
+        out = {"workload": f"BASELINE config 3: {args.c3_series / 1e6:g}M series x {hours} h @10 s (int/float32 alternating), 1000 groups, "
                            f"1m-avg, strong-scaled over {n} GPUs (series shards, partial states over "
                            f"{'RCCL' if eng.md_info()[1] == 1 else 'peer copies'})",
                "hours": hours, "synth_s": synth_s, "transport_note": note}
@@ -366,7 +379,7 @@ def main_md(args):
     from opentsdb_amd import abi
     n = args.gpus
     have = visible_gpus()
-    if have < n:
+    if have <= max(md_devices(n)):
         print(f"bench.py: --gpus {n} but only {have} GPU(s) visible; refusing to report a {have}-GPU number "
               f"as {n}", file=sys.stderr, flush=True)
         sys.exit(2)
@@ -416,6 +429,7 @@ def main_md(args):
         "data": "synthetic (seeded splitmix64, generated in HBM with the MockBase cell encoding)",
         "index_ms": index_ms,
         "launch": "one process, one multi-device context (tsdbhip_init_devices) over GPUs 0..N-1",
+        "devices": md_devices(n),
         "transport": {0: "peer copies", 1: "RCCL send/recv"}.get(transport, str(transport)),
         "transport_note": note,
         "rccl_ranks": ranks,
