@@ -2534,10 +2534,18 @@ int64_t series_max_dp(tsdbhip_ctx* c, int64_t ss, int64_t se) {
 
 // The streaming kernels (k_short / k_fast) can take the query: fixed grid, a row class of the
 // batch they are specialised for, their LDS slot budget.
+// LDS a streaming-kernel wave takes: KR 0 writing the buckets to HBM (dense_out, K > 64 or rate)
+// keeps no partials or rate values
+int64_t fast_lds_of(const tsdbhip_query* q, const Plan& P) {
+  const bool rate = q->rate != 0;
+  const bool dense0 = P.dense_out && !(P.K <= 64 && !rate);
+  return fast_wave_lds(P.K, rate && !dense0, !dense0);
+}
+
 bool fast_path_ok(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P) {
   if (!(P.mode == MODE_GRID && c->fast_qw &&
         (fast_supported(P.f, c->fast_qw, c->fast_vl) || (c->fast_qw2 && fast_supported(P.f, c->fast_qw2, c->fast_vl2))) &&
-        P.I <= (1LL << 29) && fast_wave_lds(P.K, q->rate != 0) <= 32 * 1024 && P.K > 0))
+        P.I <= (1LL << 29) && fast_lds_of(q, P) <= 32 * 1024 && P.K > 0))
     return false;
   const char* env = std::getenv("TSDBHIP_FAST");
   return !(env && env[0] == '0');
@@ -2577,7 +2585,33 @@ bool seq_rows_ok(tsdbhip_ctx* c, const Plan& P) {
          c->n_rows < ((int64_t)1 << 31);
 }
 
+// A grid query whose streaming-kernel LDS (the per-slot partials of K buckets) exceeds a wave's
+// budget -- a day of 1m buckets: K = 1440 -- would run k_grid's general path with slot arrays in
+// HBM (5 % of HBM on config 3's day, c3day_bench).  Split it instead: the streaming kernels write
+// every series' buckets to HBM (dense_out, no partials in LDS), then the group-by step runs over
+// them (emit_only: k_emit + k_reduce), as the percentile functions do.
+bool dense_split_wanted(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P) {
+  if (P.dense_out || P.emit_only || P.values_only || P.sel_direct || P.multi || P.seq_dense || P.raw || P.anchored ||
+      P.f == F_SEL || P.mode != MODE_GRID || P.K <= 64)
+    return false;
+  if (const char* e = std::getenv("TSDBHIP_DENSE_SPLIT")) if (e[0] == '0') return false;
+  if (fast_wave_lds(P.K, q->rate != 0, true) <= 32 * 1024) return false;   // the fused pass fits
+  Plan Pd = P;
+  Pd.dense_out = true;
+  if (!fast_path_ok(c, q, Pd)) return false;
+  return (double)c->n_series * (double)P.K * 9.0 <= 64.0 * (1ull << 30);   // [series][K] values + presence
+}
+
 int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bool do_reduce) {
+  if (dense_split_wanted(c, q, P)) {
+    Plan P1 = P;
+    P1.dense_out = true;
+    int rc = run_device(c, q, P1, G, false);
+    if (rc) return rc;
+    Plan P2 = P;
+    P2.emit_only = true;
+    return run_device(c, q, P2, G, do_reduce);
+  }
   const bool none = P.none;
   if (none) { int rc = build_none_tiles(c); if (rc) return rc; }
   const int64_t nt = none ? c->n_series : (int64_t)c->tb.size();
@@ -2838,7 +2872,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       fp.In = (int32_t)(fp.unit_s ? P.I / 1000 : P.I);
       fp.B0n = fp.unit_s ? P.B0 / 1000 : P.B0;
       fp.rcpn = std::nextafter(1.0 / (double)fp.In, INFINITY);
-      fp.wave_lds = (int32_t)fast_wave_lds(K, q->rate != 0);
+      fp.wave_lds = (int32_t)fast_lds_of(q, P);
       if (shortk && fp.sel_direct && fp.sel_cols && K <= 64) {   // k_short's column stage
         fp.sel_stage = fp.wave_lds;
         fp.wave_lds += (int32_t)align16(8 * K * 8);

@@ -452,7 +452,7 @@ hipError_t launch_grid(const GridParams& p, int ds_function_class, hipStream_t s
 // hipErrorNotSupported when no specialisation exists for (f, qw, vl)
 bool fast_supported(int ds_function_class, int qw, int vl);
 hipError_t launch_fast(const GridParams& p, int ds_function_class, int qw, int vl, hipStream_t s);
-int64_t fast_wave_lds(int64_t K, bool rate);
+int64_t fast_wave_lds(int64_t K, bool rate, bool part = true);   // part = false: KR 0 with dense_out
 hipError_t launch_reduce(const ReduceParams& p, hipStream_t s);
 // percentile / median downsampling (k_pct.hip): bucket order statistics, then group-by
 static constexpr int PCT_CAP = 4096;   // values per bucket sorted in LDS; larger buckets are radix-selected

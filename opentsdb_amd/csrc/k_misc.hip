@@ -936,7 +936,7 @@ hipError_t launch_fast(const GridParams& p, int f, int qw, int vl, hipStream_t s
   return hipErrorNotSupported;
 }
 
-int64_t fast_wave_lds(int64_t K, bool rate) { return align16(1024 + fast_slot_bytes(K, rate)); }   // + VL==0 value stage
+int64_t fast_wave_lds(int64_t K, bool rate, bool part) { return align16(1024 + fast_slot_bytes(K, rate, part)); }   // + VL==0 value stage
 
 int64_t grid_wave_lds(int64_t K, bool rate, bool gslot) {
   return align16(fixed_lds_bytes() + (gslot ? 0 : slot_lds_bytes(K, rate)));

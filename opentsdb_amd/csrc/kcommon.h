@@ -1433,10 +1433,11 @@ __device__ __forceinline__ constexpr bool fast_f() {
   return F == F_SUM || F == F_AVG || F == F_COUNT || F == F_SQUARESUM || F == F_MIN || F == F_MAX;
 }
 
-__host__ __device__ inline int64_t fast_slot_bytes(int64_t K, bool rate) {
-  // acc (f64, also the dense bucket values), cnt (u32), pres (u8), [rate f64], partials
-  return align16(K * 8) + align16(K * 4) + align16(K) + (rate ? align16(K * 8) : 0) + align16(K * 8) * 2 +
-         align16(K * 4) * 2;
+__host__ __device__ inline int64_t fast_slot_bytes(int64_t K, bool rate, bool part = true) {
+  // acc (f64, also the dense bucket values), cnt (u32), pres (u8), [rate f64], [partials: not
+  // when the kernel writes the series' buckets to HBM for a later group-by step (dense_out)]
+  return align16(K * 8) + align16(K * 4) + align16(K) + (rate ? align16(K * 8) : 0) +
+         (part ? align16(K * 8) * 2 + align16(K * 4) * 2 : 0);
 }
 
 struct FastLds {
@@ -1446,7 +1447,7 @@ struct FastLds {
   uint8_t* vstage;    // VL == 0: the row's value bytes (64 lanes x 16 B)
 };
 
-__device__ __forceinline__ FastLds fast_carve(unsigned char* base, int64_t K, bool rate) {
+__device__ __forceinline__ FastLds fast_carve(unsigned char* base, int64_t K, bool rate, bool part = true) {
   FastLds f;
   int64_t o = 0;
   f.vstage = base;    // used only by the VL == 0 instantiations (fast_wave_lds reserves it)
@@ -1456,10 +1457,15 @@ __device__ __forceinline__ FastLds fast_carve(unsigned char* base, int64_t K, bo
   f.w.dense = f.acc;
   f.w.pres = base + o; o += align16(K);
   if (rate) { f.w.rate = (double*)(base + o); o += align16(K * 8); } else { f.w.rate = nullptr; }
-  f.w.part.a = (double*)(base + o); o += align16(K * 8);
-  f.w.part.b = (double*)(base + o); o += align16(K * 8);
-  f.w.part.n = (uint32_t*)(base + o); o += align16(K * 4);
-  f.w.part.f = (uint32_t*)(base + o); o += align16(K * 4);
+  if (part) {
+    f.w.part.a = (double*)(base + o); o += align16(K * 8);
+    f.w.part.b = (double*)(base + o); o += align16(K * 8);
+    f.w.part.n = (uint32_t*)(base + o); o += align16(K * 4);
+    f.w.part.f = (uint32_t*)(base + o); o += align16(K * 4);
+  } else {
+    f.w.part.a = f.w.part.b = nullptr;
+    f.w.part.n = f.w.part.f = nullptr;
+  }
   f.w.dpv = nullptr; f.w.vbuf = nullptr; f.w.mq = nullptr; f.w.mv = nullptr;
   f.w.seg_slot = nullptr; f.w.seg_start = nullptr;
   return f;
@@ -1880,9 +1886,12 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
   }
   if (tile >= p.n_tiles) return;
   const int K = (int)p.K;
-  const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0);
+  // KR 0 writing the series' buckets to HBM (dense_out: a group-by step over them follows) keeps
+  // no partials or rate values in LDS, so large K (a day of 1m buckets) fits the streaming kernels
+  const bool dense0 = KR == 0 && p.dense_out != nullptr;
+  const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0 && !dense0, !dense0);
   for (int k = lane; k < K; k += 64) {
-    if (!KR) part_init(p.ga, L.w.part, k);
+    if (!KR && !dense0) part_init(p.ga, L.w.part, k);
     L.acc[k] = fast_identity<F>();
     L.cnt[k] = 0;
     L.w.pres[k] = 0;
@@ -1979,6 +1988,7 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
     rp_store(p, tile, K, RP);
     return;
   }
+  if (dense0) return;   // (the buckets went to dense_out; no tile partials)
   for (int k = lane; k < K; k += 64) {
     ga_[k] = L.w.part.a[k];
     gb_[k] = L.w.part.b[k];
@@ -2080,9 +2090,12 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     gq0 = g.q0;
     gr0 = g.r0;
   }
-  const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0);
+  // KR 0 writing the series' buckets to HBM (dense_out: a group-by step over them follows) keeps
+  // no partials or rate values in LDS, so large K (a day of 1m buckets) fits the streaming kernels
+  const bool dense0 = KR == 0 && p.dense_out != nullptr;
+  const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0 && !dense0, !dense0);
   for (int k = lane; k < K; k += 64) {
-    if (!KR) part_init(p.ga, L.w.part, k);
+    if (!KR && !dense0) part_init(p.ga, L.w.part, k);
     L.acc[k] = fast_identity<F>();
     L.cnt[k] = 0;
     L.w.pres[k] = 0;
@@ -2167,6 +2180,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     rp_store(p, tile, K, RP);
     return;
   }
+  if (dense0) return;   // (the buckets went to dense_out; no tile partials)
   for (int k = lane; k < K; k += 64) {
     ga_[k] = L.w.part.a[k];
     gb_[k] = L.w.part.b[k];
