@@ -626,6 +626,99 @@ __global__ __launch_bounds__(256) void k_emit_reg(GridParams p) {
   rp_store(p, tile, K, RP);
 }
 
+// k_emit for K > 64 without rate (a day of 1m buckets: K = 1440): one wave per (tile, window of
+// 64 slots), lane = slot, the window's tile partials in registers -- k_emit keeps K slots of
+// partials in LDS (35 KB a wave at K = 1440: one wave a block, four a CU).  The contributions of
+// a slot still arrive in series order.  A missing slot interpolates between the nearest present
+// buckets of its series as emit_series_to does (both must exist); when one lies outside the
+// window the wave finds it by scanning the series' presence bytes 64 at a time.
+__device__ __forceinline__ int pres_prev(const uint8_t* pres, int k) {   // last present slot < k, -1 if none
+  for (int b = k - 64; b > -64; b -= 64) {
+    const int j = b + lane_id();
+    const uint64_t m = __ballot(j >= 0 && j < k && pres[j] != 0);
+    if (m) return b + 63 - __clzll((long long)m);
+  }
+  return -1;
+}
+__device__ __forceinline__ int pres_next(const uint8_t* pres, int k, int K) {   // first present slot >= k, K if none
+  for (int b = k; b < K; b += 64) {
+    const int j = b + lane_id();
+    const uint64_t m = __ballot(j < K && pres[j] != 0);
+    if (m) return b + __ffsll((long long)m) - 1;
+  }
+  return K;
+}
+
+__global__ __launch_bounds__(256) void k_emit_win(GridParams p, int nwin) {
+  const int lane = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t gw = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t tile = gw / nwin;
+  if (tile >= p.n_tiles) return;
+  const int K = (int)p.K;
+  const int w0 = (int)(gw % nwin) * 64;
+  const int k = w0 + lane;
+  const bool inK = k < K;
+  const int64_t s0 = p.tile_begin[tile], s1 = p.tile_end[tile];
+  bool mine = false;   // lane i: series s0 + i has a row in the scan range (tiles hold <= 64 series)
+  if (s0 + lane < s1) {
+    const int64_t s = s0 + lane;
+    for (int64_t r = p.series_row_ptr[s]; r < p.series_row_ptr[s + 1]; r++) {
+      const uint32_t base = p.rows[r].base;
+      if ((int64_t)base >= p.ss && (int64_t)base < p.se) { mine = true; break; }
+    }
+  }
+  const uint64_t act = __ballot(mine);
+  if (act && w0 == 0 && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
+  RegPart RP;
+  rp_init(p.ga, RP);
+  const bool fill = p.fill != TSDB_FILL_NONE && p.mode != MODE_ALL;
+  const double fillv = (p.fill == TSDB_FILL_ZERO) ? 0.0 : (double)NAN;
+  const uint64_t win_mask = K - w0 >= 64 ? ~0ull : ((1ull << (K - w0)) - 1);
+  for (int64_t s = s0; s < s1; s++) {
+    if (!((act >> (s - s0)) & 1)) continue;
+    const uint8_t* pres = p.pre_pres + s * K;
+    const double* dense = p.pre_dense + s * K;
+    const bool pr = inK && pres[k] != 0;
+    const double v = inK ? dense[k] : 0.0;
+    if (fill) {   // FillingDownsampler: every slot, missing -> NaN / 0 / RuntimeException
+      if (inK) {
+        if (!pr && p.fill == TSDB_FILL_SCALAR) set_err(p.err, TSDB_E_RUNTIME);
+        if (!(k == 0 && p.skip0)) contribute_slot(p.ga, RP, pr ? v : fillv, true);
+      }
+      continue;
+    }
+    const uint64_t pm = __ballot(pr);
+    if (pm == win_mask) {   // every slot of the window present: no interpolation
+      if (inK) contribute_slot(p.ga, RP, v, true);
+      continue;
+    }
+    // nearest present slots in the window, else outside it (scanned only when a lane needs them)
+    const uint64_t below = pm & ((1ull << lane) - 1);
+    const uint64_t above = lane == 63 ? 0ull : (pm & ~((2ull << lane) - 1));
+    int prv = below ? w0 + 63 - __clzll((long long)below) : -2;
+    int nxt = above ? w0 + __ffsll((long long)above) - 1 : -2;
+    const bool miss = inK && !pr;
+    if (__ballot(miss && prv == -2)) { const int q = pres_prev(pres, w0); if (prv == -2) prv = q; }
+    if (__ballot(miss && nxt == -2)) { const int q = pres_next(pres, w0 + 64, K); if (nxt == -2) nxt = q; }
+    const bool need = miss && prv >= 0 && nxt >= 0 && nxt < K;
+    double y0 = 0.0, y1 = 0.0;
+    if (need) {
+      y0 = dense[prv];
+      y1 = dense[nxt];
+    }
+    if (pr) contribute_slot(p.ga, RP, v, true);
+    else if (need) contribute_slot(p.ga, RP, interp(p.interp, p, prv, y0, nxt, y1, k), false);
+  }
+  if (inK) {
+    const int64_t o = tile * K + k;
+    p.part.a[o] = RP.pa;
+    p.part.b[o] = RP.pb;
+    p.part.n[o] = RP.pn;
+    p.part.f[o] = RP.pf;
+  }
+}
+
 // ---- k_pct_rows: buckets inside rows, order statistics near the ends ------------------
 //
 // When the interval divides one hour (and slot 0 is interval-aligned, as the Downsampler's
@@ -2074,6 +2167,12 @@ hipError_t launch_emit(const GridParams& p, hipStream_t s) {
     GridParams q = p;
     q.waves = 4;
     hipLaunchKernelGGL(k_emit_reg, dim3((unsigned)((p.n_tiles + 3) / 4)), dim3(256), 0, s, q);
+    return hipGetLastError();
+  }
+  if (p.K > 64 && !p.rate && !(renv && renv[0] == '0')) {
+    const int nwin = (int)((p.K + 63) / 64);
+    const int64_t waves = p.n_tiles * nwin;
+    hipLaunchKernelGGL(k_emit_win, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, p, nwin);
     return hipGetLastError();
   }
   const int64_t blocks = (p.n_tiles + p.waves - 1) / p.waves;
