@@ -420,12 +420,12 @@ struct tsdbhip_ctx {
   bool pct_vonly = false;              // every row of that class (4-byte values) all-float without NaN
                                        // or all-integer: the key kernel reads values only
   bool pct_v6 = false;                 // ... and none over 384 values (6 values a lane)
-  // tile lists by k_fast row class (built at load): [class A / class B][walker / short],
-  // and the tiles of neither class (general kernel only).  Short = one row per series of at
-  // most CH datapoints (k_short).
-  std::vector<int32_t> tl[2][2], tl_other;
-  DevBuf d_tl, d_tl_n, r1a, r1b, r2, r_n;   // device copies; k_short / k_fast redo lists
-  int64_t tl_off[5] = {};
+  // tile lists by k_fast row class (built at load): [class A / class B][walker / short /
+  // rows], and the tiles of neither class (general kernel only).  Short = one row per series
+  // of at most CH datapoints (k_short); rows = several rows per series, none over CH (k_rows).
+  std::vector<int32_t> tl[2][3], tl_other;
+  DevBuf d_tl, d_tl_n, r1a, r1b, r3a, r3b, r2, r_n;   // device copies; k_short / k_rows / k_fast redo lists
+  int64_t tl_off[7] = {};
   bool fast_used = false;
   const int32_t* redo_final = nullptr;   // device counter of the tiles k_fast handed to k_grid
   int64_t redo_other = 0;                // + tiles of neither row class (k_grid only)
@@ -709,7 +709,7 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   release_batch(c);
   for (DevBuf* b : {&c->pa, &c->pb, &c->pn, &c->pf, &c->out_val, &c->out_flag, &c->gact, &c->err, &c->g_dense,
-                    &c->g_pres, &c->g_rate, &c->redo, &c->redo_n, &c->redo2, &c->redo2_n, &c->d_tl, &c->d_tl_n, &c->r1a, &c->r1b, &c->r2, &c->r_n, &c->xbuf, &c->gbuf, &c->r_rowpt,
+                    &c->g_pres, &c->g_rate, &c->redo, &c->redo_n, &c->redo2, &c->redo2_n, &c->d_tl, &c->d_tl_n, &c->r1a, &c->r1b, &c->r3a, &c->r3b, &c->r2, &c->r_n, &c->xbuf, &c->gbuf, &c->r_rowpt,
                     &c->r_spoff, &c->r_spn, &c->r_grp, &c->r_pts, &c->r_rank, &c->r_bm, &c->r_wb, &c->r_U, &c->r_ooff,
                     &c->r_sg, &c->r_su, &c->r_ots, &c->r_obits, &c->r_oint, &c->r_coff, &c->r_cur, &c->r_voff, &c->r_vl, &c->r_vd, &c->r_vp, &c->pre_dense, &c->pre_pres,
                     &c->row_ser, &c->sr_list, &c->sr_n, &c->sr_mark,
@@ -791,22 +791,24 @@ static int build_tiles(tsdbhip_ctx* c) {
       if (all) cls = k;
     }
     if (cls < 0) { c->tl_other.push_back((int32_t)t); continue; }
-    bool shrt = r1 - r0 == c->te[t] - c->tb[t];
-    for (int64_t r = r0; r < r1 && shrt; r++) shrt = c->h_ndp[r] <= (uint32_t)CH_ROWS;
-    c->tl[cls][shrt ? 1 : 0].push_back((int32_t)t);
+    bool chunk = true;   // every row one chunk
+    for (int64_t r = r0; r < r1 && chunk; r++) chunk = c->h_ndp[r] <= (uint32_t)CH_ROWS;
+    const bool shrt = chunk && r1 - r0 == c->te[t] - c->tb[t];
+    c->tl[cls][shrt ? 1 : (chunk && c->te[t] - c->tb[t] <= 64) ? 2 : 0].push_back((int32_t)t);
   }
   {
     std::vector<int32_t> all, cnt;
-    const std::vector<int32_t>* parts[5] = {&c->tl[0][0], &c->tl[0][1], &c->tl[1][0], &c->tl[1][1], &c->tl_other};
-    for (int i = 0; i < 5; i++) {
+    const std::vector<int32_t>* parts[7] = {&c->tl[0][0], &c->tl[0][1], &c->tl[0][2], &c->tl[1][0],
+                                            &c->tl[1][1], &c->tl[1][2], &c->tl_other};
+    for (int i = 0; i < 7; i++) {
       c->tl_off[i] = (int64_t)all.size();
       all.insert(all.end(), parts[i]->begin(), parts[i]->end());
       cnt.push_back((int32_t)parts[i]->size());
     }
     HIP_OK(c->d_tl.ensure(std::max<size_t>(1, all.size()) * 4));
-    HIP_OK(c->d_tl_n.ensure(5 * 4));
+    HIP_OK(c->d_tl_n.ensure(7 * 4));
     if (!all.empty()) HIP_OK(hipMemcpy(c->d_tl.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(c->d_tl_n.p, cnt.data(), 5 * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(c->d_tl_n.p, cnt.data(), 7 * 4, hipMemcpyHostToDevice));
   }
   HIP_OK(c->d_tb.ensure(nt * 8));
   HIP_OK(c->d_te.ensure(nt * 8));
@@ -2163,6 +2165,7 @@ struct Plan {
   bool ordered = false;          // TSDB_QF_ORDERED float reduction: run_ordered
   bool values_only = false;      // percentile downsampling pass without the group-by step
   bool emit_only = false;        // group-by step over bucket values already in pre_dense / pre_pres
+  bool split2 = false;           // ... the second pass of a dense split: the first pass's timing stands
   bool seq_dense = false;        // sum / avg buckets in Java's order first (k_seq_dense), then the group-by step
   int ro_fuse = 0;               // rollup avg (1) / count (2) stage: value rows with their count rows (k_seq_rows_ro)
   bool sel_cols = false;         // sel_direct in the (group, slot) column layout
@@ -2610,6 +2613,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     if (rc) return rc;
     Plan P2 = P;
     P2.emit_only = true;
+    P2.split2 = true;
     return run_device(c, q, P2, G, do_reduce);
   }
   const bool none = P.none;
@@ -2781,8 +2785,8 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       gp.wave_lds = (int32_t)std::max<int64_t>(16, elds);
     }
     gp.waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / gp.wave_lds));
-    c->fast_used = false;
-    if (!P.seq_dense) HIP_OK(hipEventRecord(c->ev[0], c->stream));
+    if (!P.split2) c->fast_used = false;   // (split: ev[0] and the k_fast state of the first pass stand)
+    if (!P.seq_dense && !P.split2) HIP_OK(hipEventRecord(c->ev[0], c->stream));
     if (!P.emit_only && !P.seq_dense) {
     HIP_OK(c->redo.ensure(std::max<int64_t>(1, c->n_series) * 4));
     HIP_OK(c->redo_n.ensure(16));
@@ -2848,20 +2852,25 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   c->fast_used = fast;
   HIP_OK(hipEventRecord(c->ev[0], c->stream));
   if (fast) {
-    // Per row class (A, B): k_short over its one-row-series tiles, k_fast over its other
-    // tiles and over what k_short handed back; k_grid over what k_fast handed back and over
-    // the tiles of neither class.  Lists by class are built at load (no per-tile appends
-    // for class mismatches); only tiles that break a premise at run time are appended.
+    // Per row class (A, B): k_short over its one-row-series tiles, k_rows over its tiles of
+    // one-chunk rows, k_fast over its other tiles and over what those two handed back; k_grid
+    // over what k_fast handed back and over the tiles of neither class.  Lists by class are
+    // built at load (no per-tile appends for class mismatches); only tiles that break a
+    // premise at run time are appended.
     const char* senv = std::getenv("TSDBHIP_SHORT");
     const bool use_short = !(senv && senv[0] == '0');
+    const char* renv = std::getenv("TSDBHIP_ROWS");
+    const bool use_rows = !(renv && renv[0] == '0');
     const int32_t* dl = c->d_tl.as<int32_t>();
     const int32_t* dn = c->d_tl_n.as<int32_t>();
     HIP_OK(c->r1a.ensure(std::max<int64_t>(1, nt) * 4));
     HIP_OK(c->r1b.ensure(std::max<int64_t>(1, nt) * 4));
+    HIP_OK(c->r3a.ensure(std::max<int64_t>(1, nt) * 4));
+    HIP_OK(c->r3b.ensure(std::max<int64_t>(1, nt) * 4));
     HIP_OK(c->r2.ensure(std::max<int64_t>(1, nt) * 4));
-    HIP_OK(c->r_n.ensure(16));
-    HIP_OK(hipMemsetAsync(c->r_n.p, 0, 16, c->stream));
-    int32_t* rn = c->r_n.as<int32_t>();   // [0] r1a, [1] r1b, [2] r2
+    HIP_OK(c->r_n.ensure(32));
+    HIP_OK(hipMemsetAsync(c->r_n.p, 0, 32, c->stream));
+    int32_t* rn = c->r_n.as<int32_t>();   // [0] r1a, [1] r1b, [2] r2, [3] r3a, [4] r3b
     auto fast_launch = [&](int cls, int shortk, const int32_t* list, const int32_t* list_n, int64_t cap,
                            int32_t* out, int32_t* out_n) -> int {
       const int qw = cls ? c->fast_qw2 : c->fast_qw, vl = cls ? c->fast_vl2 : c->fast_vl;
@@ -2873,7 +2882,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       fp.B0n = fp.unit_s ? P.B0 / 1000 : P.B0;
       fp.rcpn = std::nextafter(1.0 / (double)fp.In, INFINITY);
       fp.wave_lds = (int32_t)fast_lds_of(q, P);
-      if (shortk && fp.sel_direct && fp.sel_cols && K <= 64) {   // k_short's column stage
+      if (shortk == 1 && fp.sel_direct && fp.sel_cols && K <= 64) {   // k_short's column stage
         fp.sel_stage = fp.wave_lds;
         fp.wave_lds += (int32_t)align16(8 * K * 8);
       }
@@ -2890,6 +2899,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     // lists that no fast kernel takes go to k_grid: collect them
     std::vector<std::pair<const int32_t*, std::pair<const int32_t*, int64_t>>> to_grid;
     int32_t* r1[2] = {c->r1a.as<int32_t>(), c->r1b.as<int32_t>()};
+    int32_t* r3[2] = {c->r3a.as<int32_t>(), c->r3b.as<int32_t>()};
     int64_t routed = 0;   // tiles of host lists sent straight to k_grid
     if (none) {
       // NONE aggregator: one tile per series (not the group tiles the lists index) --
@@ -2906,33 +2916,54 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     }
     for (int cls = 0; cls < 2 && !none; cls++) {
       const int64_t n0 = (int64_t)c->tl[cls][0].size(), n1 = (int64_t)c->tl[cls][1].size();
-      const int32_t* l0 = dl + c->tl_off[2 * cls];
-      const int32_t* l1 = dl + c->tl_off[2 * cls + 1];
+      const int64_t n2 = (int64_t)c->tl[cls][2].size();
+      const int32_t* l0 = dl + c->tl_off[3 * cls];
+      const int32_t* l1 = dl + c->tl_off[3 * cls + 1];
+      const int32_t* l2 = dl + c->tl_off[3 * cls + 2];
+      const int32_t* dn0 = dn + 3 * cls;
+      const int32_t* dn1 = dn + 3 * cls + 1;
+      const int32_t* dn2 = dn + 3 * cls + 2;
       int rc;
+      if (use_rows && n2) {
+        rc = fast_launch(cls, 2, l2, dn2, n2, r3[cls], rn + 3 + cls);
+        if (rc < 0) return rc;
+        if (rc == 0) {
+          rc = fast_launch(cls, 0, r3[cls], rn + 3 + cls, n2, c->r2.as<int32_t>(), rn + 2);
+          if (rc < 0) return rc;
+          if (rc == 1) to_grid.push_back({r3[cls], {rn + 3 + cls, n2}});
+        } else {
+          to_grid.push_back({l2, {dn2, n2}});
+          routed += n2;
+        }
+      } else if (n2) {
+        rc = fast_launch(cls, 0, l2, dn2, n2, c->r2.as<int32_t>(), rn + 2);
+        if (rc < 0) return rc;
+        if (rc == 1) { to_grid.push_back({l2, {dn2, n2}}); routed += n2; }
+      }
       if (use_short && n1) {
-        rc = fast_launch(cls, 1, l1, dn + 2 * cls + 1, n1, r1[cls], rn + cls);
+        rc = fast_launch(cls, 1, l1, dn1, n1, r1[cls], rn + cls);
         if (rc < 0) return rc;
         if (rc == 0) {
           rc = fast_launch(cls, 0, r1[cls], rn + cls, n1, c->r2.as<int32_t>(), rn + 2);
           if (rc < 0) return rc;
           if (rc == 1) to_grid.push_back({r1[cls], {rn + cls, n1}});
         } else {
-          to_grid.push_back({l1, {dn + 2 * cls + 1, n1}});
+          to_grid.push_back({l1, {dn1, n1}});
           routed += n1;
         }
       } else if (n1) {
-        rc = fast_launch(cls, 0, l1, dn + 2 * cls + 1, n1, c->r2.as<int32_t>(), rn + 2);
+        rc = fast_launch(cls, 0, l1, dn1, n1, c->r2.as<int32_t>(), rn + 2);
         if (rc < 0) return rc;
-        if (rc == 1) { to_grid.push_back({l1, {dn + 2 * cls + 1, n1}}); routed += n1; }
+        if (rc == 1) { to_grid.push_back({l1, {dn1, n1}}); routed += n1; }
       }
       if (n0) {
-        rc = fast_launch(cls, 0, l0, dn + 2 * cls, n0, c->r2.as<int32_t>(), rn + 2);
+        rc = fast_launch(cls, 0, l0, dn0, n0, c->r2.as<int32_t>(), rn + 2);
         if (rc < 0) return rc;
-        if (rc == 1) { to_grid.push_back({l0, {dn + 2 * cls, n0}}); routed += n0; }
+        if (rc == 1) { to_grid.push_back({l0, {dn0, n0}}); routed += n0; }
       }
     }
     to_grid.push_back({c->r2.as<int32_t>(), {rn + 2, nt}});
-    if (!none && !c->tl_other.empty()) to_grid.push_back({dl + c->tl_off[4], {dn + 4, (int64_t)c->tl_other.size()}});
+    if (!none && !c->tl_other.empty()) to_grid.push_back({dl + c->tl_off[6], {dn + 6, (int64_t)c->tl_other.size()}});
     HIP_OK(hipEventRecord(c->ev[3], c->stream));
     for (auto& tg : to_grid) {
       if (P.multi) break;   // the caller checks that nothing was handed back (else separate passes)
@@ -4230,7 +4261,7 @@ int run_multi_fused(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_resu
   if (P.raw || P.none || P.gsel || P.f == F_SEL || P.K > 64 || !fast_path_ok(c, &q0, P) || !c->tl_other.empty())
     return 1;
   for (int cls = 0; cls < 2; cls++) {
-    if (c->tl[cls][0].empty() && c->tl[cls][1].empty()) continue;
+    if (c->tl[cls][0].empty() && c->tl[cls][1].empty() && c->tl[cls][2].empty()) continue;
     const int qw = cls ? c->fast_qw2 : c->fast_qw, vl = cls ? c->fast_vl2 : c->fast_vl;
     if (!qw || !fast_supported(P.f, qw, vl)) return 1;
   }

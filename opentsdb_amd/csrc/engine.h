@@ -144,7 +144,7 @@ struct GridParams {
   int64_t n_series;
   double* pre_dense;     // [n_series][K]
   uint8_t* pre_pres;     // [n_series][K]
-  int32_t shortk;        // k_fast launch runs k_short (one row per series, descriptors up front)
+  int32_t shortk;        // k_fast launch runs k_short (1: one row per series) / k_rows (2: rows <= CH)
   // percentile / median as the group-by aggregator (k_emit_vals, k_sel_seg): the value of
   // span i of group g at slot k goes to sel_vals[(gsp[g] + i) * K + k] ([series][slot], the
   // span's K values contiguous); NaN = no contribution

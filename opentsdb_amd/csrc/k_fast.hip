@@ -13,6 +13,9 @@
 #ifndef SHORT_D
 #define SHORT_D 2      // k_short ring depth, 4-byte float class
 #endif
+#ifndef ROWS_D
+#define ROWS_D 2       // k_rows ring depth (a power of two: 64 rows per descriptor batch)
+#endif
 
 namespace tsdb {
 
@@ -22,6 +25,16 @@ static hipError_t launch_fast_k(const GridParams& p, hipStream_t s) {
   const int64_t nl = p.n_launch > 0 ? p.n_launch : p.n_tiles;
   const int64_t blocks = (nl + p.waves - 1) / p.waves;
   const size_t lds = (size_t)p.wave_lds * p.waves;
+  if (p.shortk == 2) {   // k_rows: multi-row series of rows <= CH (a batch is 64 / DR ring turns)
+    constexpr int DR = ROWS_D;
+    if (lds > 65536) {
+      hipError_t e = hipFuncSetAttribute((const void*)k_rows<F, QW, VL, DR, KR>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((k_rows<F, QW, VL, DR, KR>), dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p, p.rows,
+                       p.series_row_ptr, p.tile_begin, p.tile_end);
+    return hipGetLastError();
+  }
   if (p.shortk) {
     constexpr int DS = VL == 0 ? SHORT_D0 : (QW * 2 + VL * 2 <= 16) ? SHORT_D : 2;
     if (lds > 65536) {

@@ -2189,6 +2189,158 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
   }
 }
 
+// ---- k_rows: tiles whose series have several rows, each at most CH datapoints -------------
+// A day of 10 s points kept as hour rows (24 rows of 360 per series): k_fast's walker reads
+// every row's descriptor with a dependent scalar load before it can issue the row's chunk.
+// Here the descriptors come in batches of 64 rows, lane i holding row b*64 + i, two batches
+// in registers (the one being folded and the next), so the D-deep ring issues across rows
+// and series with no walker.  A series ends at the row where some series' row range ends
+// (a ballot over the tile's series ends, lane = series).  Same chunk fold, certificate and
+// series end as k_fast (bit-identical partials); a tile that breaks a premise is handed back.
+struct RowBatch {
+  uint64_t qoff, voff, amax;
+  int ndp;    // > 0 in the scan range, 0 out of it (or past the tile), -1 not this kernel's row
+  uint32_t base;
+  int lsb;
+};
+
+template <int F, int QW, int VL>
+__device__ __forceinline__ void rows_batch(const GridParams& p, const RowDesc* __restrict__ rows, int64_t r0,
+                                           int nr, int b, RowBatch& B) {
+  const int jr = b * 64 + lane_id();
+  const RowDesc& x = rows[r0 + min(jr, nr - 1)];
+  B.qoff = x.qoff;
+  B.voff = x.voff;
+  B.base = x.base;
+  B.lsb = x.lsb;
+  B.amax = (uint64_t)__double_as_longlong(x.absmax);
+  const int n = (int)x.ndp;
+  const uint32_t fl = x.flags;   // (no short-circuit: a lane-conditional load waits for all loads)
+  const bool in = (jr < nr) & ((int64_t)x.base >= p.ss) & ((int64_t)x.base < p.se);
+  const bool ok = (n <= CH) & fast_row_ok<QW, VL>(fl, F == F_MIN || F == F_MAX, F == F_SUM || F == F_AVG);
+  B.ndp = !in ? 0 : (ok ? n : -1);
+}
+
+template <int F, int QW, int VL, int D, int KR>
+__global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) void k_rows(GridParams p, const RowDesc* __restrict__ rows,
+                                              const int64_t* __restrict__ srp, const int64_t* __restrict__ tbeg,
+                                              const int64_t* __restrict__ tend) {
+  static_assert(64 % D == 0, "a batch is a whole number of ring turns");
+  constexpr bool OUT = KR == 0 || KR == 3;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int64_t tile = (int64_t)blockIdx.x * p.waves + wave;
+  if (p.tile_list) {
+    if (tile >= (int64_t)*p.tile_list_n) return;
+    tile = p.tile_list[tile];
+  }
+  if (tile >= p.n_tiles) return;
+  const int K = (int)p.K;
+  const int64_t s0 = tbeg[tile];
+  const int ns = (int)(tend[tile] - s0);
+  const int64_t r0 = srp[s0];
+  const int64_t nr64 = srp[s0 + ns] - r0;
+  if (ns > 64 || nr64 <= 0 || nr64 > INT32_MAX) {
+    if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
+    return;
+  }
+  const int nr = (int)nr64;
+  const int nb = (nr + 63) >> 6;
+  // lane = series of the tile: the end of its rows (tile-relative)
+  int send = lane < ns ? (int)(srp[s0 + lane + 1] - r0) : INT32_MAX;
+  asm volatile("" : "+v"(send));   // kept in its register (not re-loaded from srp at every series end)
+  RowBatch cur, nxt;
+  rows_batch<F, QW, VL>(p, rows, r0, nr, 0, cur);
+  rows_batch<F, QW, VL>(p, rows, r0, nr, min(1, nb - 1), nxt);
+  const bool dense0 = KR == 0 && p.dense_out != nullptr;
+  const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0 && !dense0, !dense0);
+  for (int k = lane; k < K; k += 64) {
+    if (!KR && !dense0) part_init(p.ga, L.w.part, k);
+    L.acc[k] = fast_identity<F>();
+    L.cnt[k] = 0;
+    L.w.pres[k] = 0;
+  }
+  std::conditional_t<KR == 2, MultiReg, RegPart> RP;
+  rp_init(p.ga, RP);
+  WAVE_SYNC();
+  // ring: rows issued unconditionally (past the tile: its last row, 0 datapoints)
+  FRaw<QW, VL> buf[D];
+  // (in ring order: the scheduler is kept from issuing buf[1] before buf[0], which made the
+  // first fold in the loop wait for every load)
+#pragma unroll
+  for (int i = 0; i < D; i++) {
+    short_issue<QW, VL>(p, rl64(cur.qoff, i), rl64(cur.voff, i), max(0, __builtin_amdgcn_readlane(cur.ndp, i)), buf[i]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  bool redo = false, have = false, any = false;
+  int lsb = INT32_MAX;
+  double amax = 0.0;
+  uint32_t nser = 0;
+  // One loop over the rows (D a turn); the next batch is loaded when a batch is finished.  (A
+  // nested batch/row loop was rotated by the compiler so that the loads at the loop's entry
+  // made it wait for every outstanding load -- vmcnt(0) -- on every row: no ring at all.)
+  for (int j = 0; j < nr && !redo; j += D) {
+#pragma unroll
+    for (int i = 0; i < D; i++) {
+      const int jr = j + i, jl = jr & 63;
+      const int nd = __builtin_amdgcn_readlane(cur.ndp, jl);
+      if (jr < nr && nd < 0) redo = true;
+      if (jr < nr && nd > 0) {
+        const FGeom g = fgeom(p, (uint32_t)__builtin_amdgcn_readlane((int)cur.base, jl));
+        fast_chunk_any<F, QW, VL>(p, L, buf[i], g, nd, K);
+        have = true;
+        lsb = min(lsb, __builtin_amdgcn_readlane(cur.lsb, jl));
+        amax = fmax(amax, __longlong_as_double((long long)rl64(cur.amax, jl)));
+        nser += (uint32_t)nd;
+      }
+      const int jn = jl + D;   // the ring's next row: this batch or the next
+      const uint64_t iq = jn < 64 ? rl64(cur.qoff, jn) : rl64(nxt.qoff, jn - 64);
+      const uint64_t iv = jn < 64 ? rl64(cur.voff, jn) : rl64(nxt.voff, jn - 64);
+      const int in = jn < 64 ? __builtin_amdgcn_readlane(cur.ndp, jn) : __builtin_amdgcn_readlane(nxt.ndp, jn - 64);
+      short_issue<QW, VL>(p, iq, iv, max(0, in), buf[i]);
+      if (jr < nr && !redo && __ballot(send == jr + 1) != 0) {   // the last row of its series
+        if (have) {
+          const int64_t s = s0 + __popcll(__ballot(send <= jr));
+          const bool fine = KR ? fast_series_end_reg<F, true, OUT>(p, L, K, lsb, amax, RP, s, p.tile_group[tile], nser)
+                               : fast_series_end<F>(p, L, K, lsb, amax, s, p.tile_group[tile]);
+          if (!fine) redo = true;
+          any = true;
+        }
+        have = false;
+        lsb = INT32_MAX;
+        amax = 0.0;
+        nser = 0;
+      }
+    }
+    if (((j + D) & 63) == 0) {
+      cur = nxt;
+      rows_batch<F, QW, VL>(p, rows, r0, nr, min(((j + D) >> 6) + 1, nb - 1), nxt);
+    }
+  }
+  if (redo) {
+    if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
+    return;
+  }
+  if (any && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
+  WAVE_SYNC();
+  if (KR) {
+    rp_store(p, tile, K, RP);
+    return;
+  }
+  if (dense0) return;
+  double* ga_ = p.part.a + tile * K;
+  double* gb_ = p.part.b + tile * K;
+  uint32_t* gn_ = p.part.n + tile * K;
+  uint32_t* gf_ = p.part.f + tile * K;
+  for (int k = lane; k < K; k += 64) {
+    ga_[k] = L.w.part.a[k];
+    gb_[k] = L.w.part.b[k];
+    gn_[k] = L.w.part.n[k];
+    gf_[k] = L.w.part.f[k];
+  }
+}
+
 // ---- k_reduce -------------------------------------------------------------------
 struct PState {
   double a, b;
