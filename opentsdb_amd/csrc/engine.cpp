@@ -1688,15 +1688,163 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     cmp_ms += t;
     return 0;
   };
-  for (int k = 0; k < n_chunks; k++)
-    if (int rc = prepare(k)) return rc;
-  mark("upload+entries");
   // resident layout: series stable-sorted by group, each series' kept rows by base time
   std::vector<int64_t> order(NS);
   int32_t maxg = -1;
   for (int64_t s = 0; s < NS; s++) { order[s] = s; maxg = std::max(maxg, cb->group_id[s]); }
   auto gkey = [&](int64_t s) { const int32_t g = cb->group_id[s]; return g < 0 ? INT32_MAX : g; };
   std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return gkey(x) < gkey(y); });
+  // One chunk whose rows all fit a block: the one-pass path.  k_cmp_cols sums every row's
+  // datapoints and byte bounds; the host lays the rows out from the bounds (the layout below, with
+  // each row's region reserved whether or not it keeps a cell); k_cmp_rowone compacts every row
+  // straight into its region.  TSDBHIP_CMP_ONEPASS=0: the sizing pass + write pass below.
+  uint64_t op_qtot = 0, op_vtot = 0;
+  auto onepass = [&]() -> int {   // 0: compacted in place, 1: not taken (nothing kept), < 0: error
+    const int64_t nr = NR, nc = NC;
+    const uint64_t qz = nc ? cb->col_qual_off[nc] : 0, vz = nc ? cb->col_val_off[nc] : 0;
+    const int64_t r1c = std::max<int64_t>(1, nr), c1c = std::max<int64_t>(1, nc);
+    HIP_OK(d_rcp.ensure((r1c + 1) * 8));
+    HIP_OK(d_cqo.ensure((c1c + 1) * 8));
+    HIP_OK(d_cvo.ensure((c1c + 1) * 8));
+    HIP_OK(d_q.ensure(std::max<uint64_t>(16, qz) + 16));
+    HIP_OK(d_v.ensure(std::max<uint64_t>(16, vz) + 16));
+    if (cb->col_timestamp) HIP_OK(d_cts.ensure(c1c * 8));
+    HIP_OK(d_raw.ensure((std::max(r1c, c1c) + 1) * 8));
+    HIP_OK(hipMemsetAsync(d_bad.p, 0, 4, st));
+    if (nr) {   // (rebase 0: the monotonicity check; the offsets are used as given)
+      HIP_OK(hipMemcpyAsync(d_raw.p, cb->row_col_ptr, (nr + 1) * 8, hipMemcpyHostToDevice, st));
+      HIP_OK(cmp_rebase(d_raw.as<uint64_t>(), d_rcp.as<uint64_t>(), nr + 1, 0, d_bad.as<int32_t>(), st));
+    }
+    if (nc) {
+      HIP_OK(hipMemcpyAsync(d_raw.p, cb->col_qual_off, (nc + 1) * 8, hipMemcpyHostToDevice, st));
+      HIP_OK(cmp_rebase(d_raw.as<uint64_t>(), d_cqo.as<uint64_t>(), nc + 1, 0, d_bad.as<int32_t>(), st));
+      HIP_OK(hipMemcpyAsync(d_raw.p, cb->col_val_off, (nc + 1) * 8, hipMemcpyHostToDevice, st));
+      HIP_OK(cmp_rebase(d_raw.as<uint64_t>(), d_cvo.as<uint64_t>(), nc + 1, 0, d_bad.as<int32_t>(), st));
+      if (qz) HIP_OK(hipMemcpyAsync(d_q.p, cb->qual, qz, hipMemcpyHostToDevice, st));
+      if (vz) HIP_OK(hipMemcpyAsync(d_v.p, cb->val, vz, hipMemcpyHostToDevice, st));
+      if (cb->col_timestamp) HIP_OK(hipMemcpyAsync(d_cts.p, cb->col_timestamp, nc * 8, hipMemcpyHostToDevice, st));
+    }
+    int32_t bad = 0;
+    HIP_OK(hipMemcpyAsync(&bad, d_bad.p, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (bad) return fail(TSDB_E_ILLEGAL_ARGUMENT, "column offsets not monotonic");
+    HIP_OK(d_crow.ensure(c1c * 4));
+    HIP_OK(d_cn.ensure(c1c * 8));
+    HIP_OK(d_cinfo.ensure(c1c * 4));
+    for (DevBuf* b : {&d_rheap, &d_rerr}) HIP_OK(b->ensure(r1c * 4));
+    for (DevBuf* b : {&d_rone, &d_rlo, &d_rq, &d_rv, &d_sq, &d_sv, &d_sc}) HIP_OK(b->ensure(r1c * 8));
+    HIP_OK(d_rstate.ensure(r1c * 4));
+    HIP_OK(d_rmeta.ensure(r1c));
+    HIP_OK(hipMemsetAsync(d_rheap.p, 0, r1c * 4, st));
+    HIP_OK(hipMemsetAsync(d_rone.p, 0, r1c * 8, st));
+    HIP_OK(hipMemsetAsync(d_rerr.p, 0, r1c * 4, st));
+    for (DevBuf* b : {&d_sq, &d_sv, &d_sc}) HIP_OK(hipMemsetAsync(b->p, 0, r1c * 8, st));
+    p.n_rows = nr;
+    p.n_cols = nc;
+    p.row_col_ptr = d_rcp.as<int64_t>();
+    p.col_qo = d_cqo.as<uint64_t>();
+    p.col_vo = d_cvo.as<uint64_t>();
+    p.col_ts = cb->col_timestamp ? d_cts.as<int64_t>() : nullptr;
+    p.q = d_q.as<uint8_t>();
+    p.v = d_v.as<uint8_t>();
+    p.col_row = d_crow.as<int32_t>();
+    p.col_n = d_cn.as<int64_t>();
+    p.col_off = nullptr;
+    p.col_info = d_cinfo.as<uint32_t>();
+    p.row_heap = d_rheap.as<int32_t>();
+    p.row_one = d_rone.as<int64_t>();
+    p.row_err = d_rerr.as<int32_t>();
+    p.row_n = d_sc.as<int64_t>();
+    p.row_qb = d_sq.as<int64_t>();
+    p.row_vb = d_sv.as<int64_t>();
+    p.row_lo = d_rlo.as<int64_t>();
+    p.row_q = d_rq.as<int64_t>();
+    p.row_v = d_rv.as<int64_t>();
+    p.row_state = d_rstate.as<int32_t>();
+    p.row_meta = d_rmeta.as<uint8_t>();
+    HIP_OK(hipEventRecord(c->ev[0], st));
+    HIP_OK(cmp_cols_rows(p, st));
+    HIP_OK(hipEventRecord(c->ev[2], st));
+    hipError_t he = hipSuccess;
+    const int cap = cmp_onepass_cap(p, d_rmax.as<uint32_t>(), st, &he);   // (synchronises)
+    HIP_OK(he);
+    float t_cols = 0;
+    (void)hipEventElapsedTime(&t_cols, c->ev[0], c->ev[2]);
+    if (!cap) {
+      p.row_n = p.row_qb = p.row_vb = nullptr;
+      return 1;
+    }
+    std::vector<int64_t> qbv(r1c, 0), vbv(r1c, 0);
+    if (nr) {
+      HIP_OK(hipMemcpyAsync(qbv.data(), p.row_qb, nr * 8, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipMemcpyAsync(vbv.data(), p.row_vb, nr * 8, hipMemcpyDeviceToHost, st));
+    }
+    HIP_OK(hipStreamSynchronize(st));
+    // regions: series in resident order, each series' rows by base time; rows of one base time
+    // (salt buckets) adjacent, with 16 more bytes for the merged cell's meta byte
+    uint64_t qt = 0, vt = 0;
+    for (int64_t i = 0; i < NS; i++) {
+      const int64_t s = order[i];
+      std::vector<int64_t> rows;
+      for (int64_t r = cb->series_row_ptr[s]; r < cb->series_row_ptr[s + 1]; r++) rows.push_back(r);
+      std::stable_sort(rows.begin(), rows.end(), [&](int64_t x, int64_t y) { return cb->row_base_time[x] < cb->row_base_time[y]; });
+      for (size_t k0 = 0; k0 < rows.size();) {
+        size_t k1 = k0 + 1;
+        while (k1 < rows.size() && cb->row_base_time[rows[k1]] == cb->row_base_time[rows[k0]]) k1++;
+        for (size_t k = k0; k < k1; k++) {
+          const int64_t r = rows[k];
+          rdq[r] = (int64_t)qt;
+          rdv[r] = (int64_t)vt;
+          qt += align16((uint64_t)qbv[r]);
+          vt += align16((uint64_t)vbv[r] + 1);
+        }
+        if (k1 - k0 > 1) vt += 16;
+        k0 = k1;
+      }
+    }
+    op_qtot = qt;
+    op_vtot = vt;
+    HIP_OK(c->qual.ensure(qt + BLOB_SLACK));
+    HIP_OK(c->val.ensure(vt + BLOB_SLACK));
+    HIP_OK(hipMemsetAsync(c->qual.p, 0, qt + BLOB_SLACK, st));
+    HIP_OK(hipMemsetAsync(c->val.p, 0, vt + BLOB_SLACK, st));
+    HIP_OK(d_rdq.ensure(r1c * 8));
+    HIP_OK(d_rdv.ensure(r1c * 8));
+    if (nr) {
+      HIP_OK(hipMemcpyAsync(d_rdq.p, rdq.data(), nr * 8, hipMemcpyHostToDevice, st));
+      HIP_OK(hipMemcpyAsync(d_rdv.p, rdv.data(), nr * 8, hipMemcpyHostToDevice, st));
+    }
+    p.row_dq = d_rdq.as<int64_t>();
+    p.row_dv = d_rdv.as<int64_t>();
+    p.out_q = c->qual.as<uint8_t>();
+    p.out_v = c->val.as<uint8_t>();
+    HIP_OK(hipEventRecord(c->ev[3], st));
+    HIP_OK(cmp_rows_onepass(p, cap, st));
+    HIP_OK(hipEventRecord(c->ev[1], st));
+    if (nr) {
+      HIP_OK(hipMemcpyAsync(rq.data(), p.row_q, nr * 8, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipMemcpyAsync(rv.data(), p.row_v, nr * 8, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipMemcpyAsync(rstate.data(), p.row_state, nr * 4, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipMemcpyAsync(rerr.data(), p.row_err, nr * 4, hipMemcpyDeviceToHost, st));
+    }
+    HIP_OK(hipStreamSynchronize(st));
+    float t_rows = 0;
+    (void)hipEventElapsedTime(&t_rows, c->ev[3], c->ev[1]);
+    cmp_ms = t_cols + t_rows;
+    return 0;
+  };
+  int op = 1;
+  {
+    const char* op_env = std::getenv("TSDBHIP_CMP_ONEPASS");
+    if (n_chunks == 1 && rows_ok && !(op_env && op_env[0] == '0')) {
+      op = onepass();
+      if (op < 0) return op;
+    }
+  }
+  if (op)
+    for (int k = 0; k < n_chunks; k++)
+      if (int rc = prepare(k)) return rc;
+  mark("upload+entries");
   std::vector<tsdbhip_ctx::CmpErr> errs;
   std::vector<int64_t> srp(NS + 1, 0);
   std::vector<RowDesc> rd;
@@ -1722,16 +1870,18 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
       while (k1 < rows.size() && cb->row_base_time[rows[k1]] == cb->row_base_time[rows[k0]]) k1++;
       RowDesc d{};
       d.base = cb->row_base_time[rows[k0]];
-      d.qoff = qtot;
-      d.voff = vtot;
+      d.qoff = op ? qtot : (uint64_t)rdq[rows[k0]];   // (one-pass: the regions laid out before the kernel)
+      d.voff = op ? vtot : (uint64_t)rdv[rows[k0]];
       uint64_t ql = 0, vl = 0;
       for (size_t k = k0; k < k1; k++) {
         const int64_t r = rows[k];
         if (rq[r] > 0xFFFFFFFFLL || rv[r] > 0xFFFFFFFFLL) return fail(TSDB_E_ILLEGAL_ARGUMENT, "row too large");
-        rdq[r] = (int64_t)qtot;
-        rdv[r] = (int64_t)vtot;
-        qtot += align16(rq[r]);
-        vtot += align16(rv[r]);
+        if (op) {
+          rdq[r] = (int64_t)qtot;
+          rdv[r] = (int64_t)vtot;
+          qtot += align16(rq[r]);
+          vtot += align16(rv[r]);
+        }
         ql += rq[r];
         vl += rv[r];
       }
@@ -1739,7 +1889,7 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
       d.qlen = (uint32_t)rq[rows[k0]];
       d.vlen = (uint32_t)rv[rows[k0]];
       if (k1 - k0 > 1) {
-        vtot += 16;   // the merged cell's meta byte (two single-datapoint cells become a compacted one)
+        if (op) vtot += 16;   // the merged cell's meta byte (two single-datapoint cells become a compacted one)
         salt.push_back({rd.size(), std::vector<int64_t>(rows.begin() + k0, rows.begin() + k1)});
       }
       if (rd.size() == (size_t)srp[i]) d.flags |= ROW_SFIRST;
@@ -1752,12 +1902,18 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     return a.series != b.series ? a.series < b.series : a.row < b.row;
   });
   // the compacted cells, written in place
-  HIP_OK(c->qual.ensure(qtot + BLOB_SLACK));
-  HIP_OK(c->val.ensure(vtot + BLOB_SLACK));
-  HIP_OK(hipMemsetAsync(c->qual.p, 0, qtot + BLOB_SLACK, c->stream));
-  HIP_OK(hipMemsetAsync(c->val.p, 0, vtot + BLOB_SLACK, c->stream));
+  if (!op) {
+    qtot = op_qtot;
+    vtot = op_vtot;
+  } else {
+    HIP_OK(c->qual.ensure(qtot + BLOB_SLACK));
+    HIP_OK(c->val.ensure(vtot + BLOB_SLACK));
+    HIP_OK(hipMemsetAsync(c->qual.p, 0, qtot + BLOB_SLACK, c->stream));
+    HIP_OK(hipMemsetAsync(c->val.p, 0, vtot + BLOB_SLACK, c->stream));
+  }
   mark("host layout");
-  if (n_chunks == 1) {
+  if (!op) {
+  } else if (n_chunks == 1) {
     if (int rc = write(0)) return rc;
   } else {
     for (int k = 0; k < n_chunks; k++) {
@@ -2881,6 +3037,8 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       fp.In = (int32_t)(fp.unit_s ? P.I / 1000 : P.I);
       fp.B0n = fp.unit_s ? P.B0 / 1000 : P.B0;
       fp.rcpn = std::nextafter(1.0 / (double)fp.In, INFINITY);
+      const char* oenv = std::getenv("TSDBHIP_ONEB");
+      fp.oneb = P.I >= 3600000 && !(oenv && oenv[0] == '0') ? 1 : 0;   // (an hour row's chunk in one bucket)
       fp.wave_lds = (int32_t)fast_lds_of(q, P);
       if (shortk == 1 && fp.sel_direct && fp.sel_cols && K <= 64) {   // k_short's column stage
         fp.sel_stage = fp.wave_lds;

@@ -145,6 +145,7 @@ struct GridParams {
   double* pre_dense;     // [n_series][K]
   uint8_t* pre_pres;     // [n_series][K]
   int32_t shortk;        // k_fast launch runs k_short (1: one row per series) / k_rows (2: rows <= CH)
+  int32_t oneb;          // streaming kernels: buckets of an hour or more -- try the one-bucket chunk fold
   // percentile / median as the group-by aggregator (k_emit_vals, k_sel_seg): the value of
   // span i of group g at slot k goes to sel_vals[(gsp[g] + i) * K + k] ([series][slot], the
   // span's K values contiguous); NaN = no contribution
@@ -367,6 +368,9 @@ struct CmpParams {
   int32_t* row_heap;            // columns in the compaction heap
   int64_t* row_one;             // one of them (the only one when row_heap == 1)
   int32_t* row_err;             // first error: TSDB_E_ILLEGAL_DATA or TSDB_E_NOT_IMPLEMENTED
+  int64_t* row_n;               // one-pass path (k_cmp_cols_rowwave): datapoints of the row,
+  int64_t* row_qb;              //   bounds of its compacted qualifier bytes
+  int64_t* row_vb;              //   and value bytes (before the meta byte)
   // entries (one per datapoint of every column)
   int64_t n_ent;
   uint64_t* key;                // [n_ent] row << 22 | offset (ms), then sorted
@@ -403,6 +407,15 @@ hipError_t cmp_write(const CmpParams& p, hipStream_t s);
 // *span: the largest row's qualifier or value bytes (the write pass's LDS stage).
 int cmp_row_cap(const CmpParams& p, uint32_t* scratch3, hipStream_t s, hipError_t* err, uint32_t* span);
 hipError_t cmp_rows_fused(const CmpParams& p, void* klist, int cap, uint32_t span, bool write, hipStream_t s);
+// One-pass per-row compaction (a chunk whose rows all fit a block): cmp_cols_rows = k_cmp_cols'
+// analysis a wave per row, with the per-row heap count, datapoints and byte bounds (p.row_heap /
+// row_one / row_n / row_qb / row_vb), no column offsets; cmp_onepass_cap = the LDS capacity (0: a
+// row does not fit);
+// cmp_rows_onepass = k_cmp_rowone: sort, deduplicate and write every row at p.row_dq / row_dv
+// (laid out by the host from the bounds) in one kernel.
+hipError_t cmp_cols_rows(const CmpParams& p, hipStream_t s);
+int cmp_onepass_cap(const CmpParams& p, uint32_t* scratch3, hipStream_t s, hipError_t* err);
+hipError_t cmp_rows_onepass(const CmpParams& p, int cap, hipStream_t s);
 // dst = src - base over n offsets (a chunk of the scan, rebased); *bad |= 1 unless non-decreasing and >= base
 hipError_t cmp_rebase(const uint64_t* src, uint64_t* dst, int64_t n, uint64_t base, int32_t* bad, hipStream_t s);
 

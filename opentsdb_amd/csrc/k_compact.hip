@@ -83,8 +83,11 @@ __device__ __forceinline__ bool walk_append(const uint8_t* v, int64_t vl, F&& f)
   return true;
 }
 
-// One column: kind, fixups, datapoint count, errors.  Returns whether it joins the heap.
-__device__ __forceinline__ bool cmp_col(const CmpParams& p, int64_t c, int64_t row) {
+// One column: kind, fixups, datapoint count, errors.  Returns whether it joins the heap.  *qb /
+// *vb: bounds of the compacted bytes it can contribute (a data column keeps its qualifier width
+// and value bytes; an append column's qualifiers and values both come out of its value)
+__device__ __forceinline__ bool cmp_col(const CmpParams& p, int64_t c, int64_t row, int64_t* qb = nullptr,
+                                        int64_t* vb = nullptr, int64_t* nout = nullptr) {
   const uint64_t qo = p.col_qo[c], vo = p.col_vo[c];
   const int64_t ql = (int64_t)(p.col_qo[c + 1] - qo), vl = (int64_t)(p.col_vo[c + 1] - vo);
   const uint8_t* q = p.q + qo;
@@ -135,6 +138,11 @@ __device__ __forceinline__ bool cmp_col(const CmpParams& p, int64_t c, int64_t r
   }
   p.col_n[c] = n;
   p.col_info[c] = kind | info;
+  if (nout) *nout = n;
+  if (qb) {
+    *qb = n == 0 ? 0 : (kind == CMP_APPEND ? vl : ql);
+    *vb = n == 0 ? 0 : (kind == CMP_APPEND ? vl : vl - ((info & 4) ? 4 : 0));
+  }
   return heap;
 }
 
@@ -475,12 +483,8 @@ __device__ __forceinline__ int em_evl(uint32_t em) { return (int)((em >> 1) & 7)
 __device__ __forceinline__ int block_excl_scan(int x, int* sh, int* total) {
   const int t = threadIdx.x;
   const int nw = (int)(blockDim.x >> 6);
-  int v = x;
   const int lane = t & 63;
-  for (int o = 1; o < 64; o <<= 1) {   // inclusive wave scan
-    const int y = __shfl_up(v, o);
-    if (lane >= o) v += y;
-  }
+  const int v = wave_incl_sum_dpp(x);   // inclusive wave scan (DPP: no LDS permutes)
   if (lane == 63) sh[t >> 6] = v;
   __syncthreads();
   int base = 0, all = 0;
@@ -852,6 +856,371 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_rowwrite(CmpParams p, c
   uint32_t* dvw = reinterpret_cast<uint32_t*>(dv);
   for (int64_t w = t; w < nqd; w += nt) dqw[w] = oqw[w];
   for (int64_t w = t; w < nvd; w += nt) dvw[w] = ovw[w];
+}
+
+// ---- the one-pass per-row path ------------------------------------------------------------
+// The host lays every row out from k_cmp_cols' byte bounds before any datapoint is sorted, so the
+// row kernel can write the compacted cell itself: no kept-datapoint list through HBM, no second
+// read of the sources, no scan over the column counts (a block scan gives the row's entry
+// offsets).  Same explode / order / dedup as k_cmp_row; the cell is assembled in the LDS the
+// sort used and leaves in dwords.
+__global__ __launch_bounds__(256) void k_cmp_rowmax2(CmpParams p, uint32_t* out) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t n = 0, nc = 0;
+  if (r < p.n_rows) {
+    n = (uint32_t)min<int64_t>(p.row_n[r], 0xFFFFFFFFll);
+    nc = (uint32_t)min<int64_t>(p.row_col_ptr[r + 1] - p.row_col_ptr[r], 0xFFFFFFFFll);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    n = max(n, (uint32_t)__shfl_xor((int)n, o));
+    nc = max(nc, (uint32_t)__shfl_xor((int)nc, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(&out[0], n);
+    atomicMax(&out[1], nc);
+  }
+}
+
+// bytes [s, s + n) of src to dst (16-byte aligned) in dwords: each output dword from the two
+// aligned source dwords it straddles
+__device__ __forceinline__ void cmp_copy_to_aligned(uint8_t* dst, const uint8_t* src, int64_t n, int t, int nt) {
+  const uintptr_t sa = (uintptr_t)src;
+  const uint32_t* s4 = reinterpret_cast<const uint32_t*>(sa & ~(uintptr_t)3);
+  const int sh = (int)(sa & 3) * 8;
+  uint32_t* d4 = reinterpret_cast<uint32_t*>(dst);
+  const int64_t nw = n >> 2;
+  for (int64_t w = t; w < nw; w += nt) {
+    const uint32_t lo = s4[w];
+    const uint32_t hi = sh ? s4[w + 1] : 0u;   // (the sources carry 16 bytes of slack)
+    d4[w] = sh ? ((lo >> sh) | (hi << (32 - sh))) : lo;
+  }
+  for (int64_t b = (nw << 2) + t; b < n; b += nt) dst[b] = src[b];
+}
+
+__global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_rowone(CmpParams p, int P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  uint64_t* key = reinterpret_cast<uint64_t*>(sm);
+  uint32_t* eq_src = reinterpret_cast<uint32_t*>(key + P);
+  uint32_t* ev_src = eq_src + P;
+  uint16_t* eem = reinterpret_cast<uint16_t*>(ev_src + P);
+  uint16_t* ecol = eem + P;
+  __shared__ int scan_sh[CMP_ROW_THREADS / 64];
+  __shared__ int dup_err;
+  const int64_t r = blockIdx.x;
+  const int t = threadIdx.x;
+  if (t == 0) dup_err = 0;
+  auto no_cell = [&]() {
+    if (t == 0) { p.row_state[r] = 0; p.row_q[r] = p.row_v[r] = 0; p.row_meta[r] = 0; p.row_lo[r] = 0; }
+  };
+  if (p.row_err[r] || p.row_heap[r] == 0) { no_cell(); return; }
+  if (p.row_heap[r] == 1) {
+    const int64_t c = p.row_one[r];
+    const uint32_t info = p.col_info[c];
+    const int64_t ql = (int64_t)(p.col_qo[c + 1] - p.col_qo[c]);
+    if ((info & 3) == CMP_DATA && !(info & 8) && (ql == 2 || (ql == 4 && cmp_in_ms(p.q[p.col_qo[c]])))) {
+      const int64_t vl = (int64_t)(p.col_vo[c + 1] - p.col_vo[c]);   // noMergesOrFixups: as stored
+      if (ql > p.row_qb[r] || vl > p.row_vb[r]) {
+        if (t == 0) cmp_fail(p.row_err, r, TSDB_E_ILLEGAL_STATE);
+        no_cell();
+        return;
+      }
+      cmp_copy_to_aligned(p.out_q + p.row_dq[r], p.q + p.col_qo[c], ql, t, CMP_ROW_THREADS);
+      cmp_copy_to_aligned(p.out_v + p.row_dv[r], p.v + p.col_vo[c], vl, t, CMP_ROW_THREADS);
+      if (t == 0) { p.row_state[r] = 2; p.row_q[r] = ql; p.row_v[r] = vl; p.row_meta[r] = 0; p.row_lo[r] = 0; }
+      return;
+    }
+  }
+  const int64_t c0 = p.row_col_ptr[r], c1 = p.row_col_ptr[r + 1];
+  const uint64_t qb = p.col_qo[c0], vb = p.col_vo[c0];
+  const uint8_t* qrow = p.q + qb;
+  const uint8_t* vrow = p.v + vb;
+  // explode, 1024 columns a round: the entry offsets of a round from a block scan of its counts
+  int n = 0;
+  for (int64_t cr = c0; cr < c1; cr += CMP_ROW_THREADS) {
+    const int64_t c = cr + t;
+    const int nc_ = c < c1 ? (int)p.col_n[c] : 0;
+    int tot;
+    int e = n + block_excl_scan(nc_, scan_sh, &tot);
+    n += tot;
+    if (nc_ == 0) continue;
+    const uint64_t qo = p.col_qo[c], vo = p.col_vo[c];
+    const int64_t ql = (int64_t)(p.col_qo[c + 1] - qo), vl = (int64_t)(p.col_vo[c + 1] - vo);
+    const uint32_t info = p.col_info[c];
+    const bool app = (info & 3) == CMP_APPEND;
+    const bool fix = !app && ql == 2 && (info & 8);
+    const uint32_t qbase = (uint32_t)((app ? vo - vb : qo - qb));
+    const uint32_t vbase = (uint32_t)(vo - vb);
+    auto put = [&](int64_t qpos, int64_t vpos, int eq, int evl, uint32_t off) {
+      key[e] = ((uint64_t)off << 12) | (uint64_t)e;
+      eq_src[e] = qbase + (uint32_t)qpos;
+      ev_src[e] = vbase + (uint32_t)vpos;
+      eem[e] = (uint16_t)((eq == 4 ? 1u : 0u) | ((uint32_t)(evl - 1) << 1) | (fix ? 16u : 0u) | (app ? 32u : 0u));
+      ecol[e] = (uint16_t)(c - c0);
+      e++;
+    };
+    if (app) {
+      walk_append(p.v + vo, vl, put);
+    } else {
+      const int64_t vstart = (info & 4) ? 4 : 0;
+      walk_data(p.q + qo, ql, vl - vstart, (uint8_t)(info >> 8),
+                [&](int64_t qi, int64_t vi, int eq, int evl, uint32_t off) { put(qi, vstart + vi, eq, evl, off); });
+    }
+  }
+  for (int i = n + t; i < P; i += CMP_ROW_THREADS) key[i] = ~0ull >> 2;
+  __syncthreads();
+  int unsorted = 0;
+  for (int i = t + 1; i < n; i += CMP_ROW_THREADS) unsorted |= key[i - 1] > key[i] ? 1 : 0;
+  bool placed = false;
+  if (__syncthreads_or(unsorted) && P == 4096) {   // distinct whole seconds: placed by second (k_cmp_row)
+    __shared__ uint32_t secmap[4096 / 32];
+    __shared__ int place_fail;
+    for (int i = t; i < 4096 / 32; i += CMP_ROW_THREADS) secmap[i] = 0;
+    if (t == 0) place_fail = 0;
+    __syncthreads();
+    for (int i = t; i < n; i += CMP_ROW_THREADS) {
+      const uint64_t off = key[i] >> 12;
+      if (off % 1000u != 0 || off >= 4096000u) { place_fail = 1; continue; }
+      const uint32_t sec = (uint32_t)(off / 1000u);
+      const uint32_t bit = 1u << (sec & 31);
+      if (atomicOr(&secmap[sec >> 5], bit) & bit) place_fail = 1;
+    }
+    __syncthreads();
+    if (!place_fail) {
+      uint16_t* by_sec = ecol;
+      for (int i = t; i < n; i += CMP_ROW_THREADS) by_sec[(uint32_t)((key[i] >> 12) / 1000u)] = (uint16_t)i;
+      const uint32_t bits = (secmap[t >> 3] >> ((t & 7) * 4)) & 0xFu;
+      int total;
+      int pos = block_excl_scan(__popc(bits), scan_sh, &total);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if ((bits >> j) & 1u) {
+          const uint32_t sec = 4u * (uint32_t)t + (uint32_t)j;
+          key[pos++] = ((uint64_t)(sec * 1000u) << 12) | by_sec[sec];
+        }
+      }
+      __syncthreads();
+      placed = true;
+    }
+  }
+  if (!placed && __syncthreads_or(unsorted)) {
+    if (P == 4096) cmp_sort_block<4>(key, P);
+    else if (P == 2048) cmp_sort_block<2>(key, P);
+    else if (P == 1024) cmp_sort_block<1>(key, P);
+    else {
+      for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          for (int i = t; i < P / 2; i += CMP_ROW_THREADS) {
+            const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));
+            const int hi = lo + j;
+            const uint64_t x = key[lo], y = key[hi];
+            if ((x > y) == ((lo & k) == 0)) {
+              key[lo] = y;
+              key[hi] = x;
+            }
+          }
+          __syncthreads();
+        }
+    }
+  }
+  // runs of one offset (k_cmp_row's rules)
+  for (int i = t; i < n; i += CMP_ROW_THREADS) {
+    const uint64_t off = key[i] >> 12;
+    if (i > 0 && (key[i - 1] >> 12) == off) continue;
+    int j = i + 1;
+    while (j < n && (key[j] >> 12) == off) j++;
+    if (j == i + 1) {
+      key[i] |= CMP_KEPT;
+      continue;
+    }
+    auto ent = [&](int s) { return (int)(key[s] & 4095); };
+    auto superseded = [&](int s) {
+      const int es = ent(s);
+      return (eem[es] & 32) && s + 1 < j && ecol[ent(s + 1)] == ecol[es];
+    };
+    int best = -1;
+    int64_t best_ts = 0;
+    for (int s = i; s < j; s++) {
+      if (superseded(s)) continue;
+      const int64_t ts = p.col_ts ? p.col_ts[c0 + ecol[ent(s)]] : 0;
+      if (best < 0 || ts > best_ts) { best = s; best_ts = ts; }
+    }
+    key[best] |= CMP_KEPT;
+    if (p.fix_dup) continue;
+    const int eb = ent(best);
+    const int lb = em_evl(eem[eb]);
+    const uint8_t* vk = vrow + ev_src[eb];
+    for (int s = i; s < j; s++) {
+      if (s == best || superseded(s)) continue;
+      const int es = ent(s);
+      bool same = em_evl(eem[es]) == lb;
+      const uint8_t* vo = vrow + ev_src[es];
+      for (int b = 0; same && b < lb; b++) same = vo[b] == vk[b];
+      if (!same) {
+        cmp_fail(p.row_err, r, TSDB_E_ILLEGAL_DATA);
+        dup_err = 1;
+      }
+    }
+  }
+  __syncthreads();
+  // each thread m consecutive sorted positions (m <= 4): its kept entries into registers, two
+  // block scans of packed sums (qualifier | value bytes, datapoints | ms datapoints)
+  constexpr int MMAX = CMP_ROW_CAP / CMP_ROW_THREADS;
+  const int m = P / CMP_ROW_THREADS > 0 ? P / CMP_ROW_THREADS : 1;
+  const int a0 = t * m, a1 = min(n, a0 + m);
+  uint32_t kq[MMAX], kv[MMAX], kem[MMAX];
+  int kc = 0, sq = 0, sv = 0, sms = 0;
+#pragma unroll
+  for (int x = 0; x < MMAX; x++) {
+    const int i = a0 + x;
+    kq[x] = kv[x] = kem[x] = 0;
+    if (x < m && i < a1) {
+      const uint64_t kk = key[i];
+      if (kk & CMP_KEPT) {
+        const int e = (int)(kk & 4095);
+        const uint32_t em = eem[e];
+        kq[x] = eq_src[e];
+        kv[x] = ev_src[e];
+        kem[x] = em | 0x10000u;   // (bit 16: kept)
+        sq += em_eq(em);
+        sv += em_evl(em);
+        kc++;
+        sms += em & 1;
+      }
+    }
+  }
+  int tqv, tcm;
+  const int oqv = block_excl_scan((sq << 16) | sv, scan_sh, &tqv);   // (sq <= 16384, sv <= 32768 a row)
+  const int ocm = block_excl_scan((kc << 16) | sms, scan_sh, &tcm);
+  const int tq = tqv >> 16, tv = tqv & 0xFFFF, tc = tcm >> 16, tm = tcm & 0xFFFF;
+  if (dup_err) { no_cell(); return; }
+  if (tc == 0) { no_cell(); return; }
+  const int nv = tv + (tc > 1 ? 1 : 0);   // + the meta byte
+  if (tq > p.row_qb[r] || tv > p.row_vb[r]) {   // (the host's region is too small: cannot happen)
+    if (t == 0) cmp_fail(p.row_err, r, TSDB_E_ILLEGAL_STATE);
+    no_cell();
+    return;
+  }
+  // the cell in LDS (the sort's space is free: every thread's entries are in registers)
+  uint8_t* oq = sm;
+  uint8_t* ov = sm + ((tq + 15) & ~15);
+  const int nqd = (tq + 3) >> 2, nvd = (nv + 3) >> 2;
+  uint32_t* oqw = reinterpret_cast<uint32_t*>(oq);
+  uint32_t* ovw = reinterpret_cast<uint32_t*>(ov);
+  for (int w = t; w < nqd; w += CMP_ROW_THREADS) oqw[w] = 0;
+  for (int w = t; w < nvd; w += CMP_ROW_THREADS) ovw[w] = 0;
+  __syncthreads();
+  int q_at = oqv >> 16, v_at = oqv & 0xFFFF;
+#pragma unroll
+  for (int x = 0; x < MMAX; x++) {
+    if (kem[x] & 0x10000u) {
+      const uint32_t em = kem[x];
+      const int eq = em_eq(em), evl = em_evl(em);
+      const uint8_t* qs = ((em & 32) ? vrow : qrow) + kq[x];
+      uint8_t* qd = oq + q_at;
+      if (eq == 2 && !(((uintptr_t)qs | (uintptr_t)qd) & 1)) {   // a 2-byte qualifier: one 16-bit move
+        uint32_t w = *reinterpret_cast<const uint16_t*>(qs);   // (little-endian: byte 1 is the high half)
+        if (em & 16) w = (w & 0x00FFu) | ((((w >> 8) & 0xF8u) | (uint32_t)(evl - 1)) << 8);   // checkForFixup's flags
+        *reinterpret_cast<uint16_t*>(qd) = (uint16_t)w;
+      } else {
+        qd[0] = qs[0];
+        qd[1] = (em & 16) ? (uint8_t)((qs[1] & 0xF8) | (evl - 1)) : qs[1];   // checkForFixup's flags
+        if (eq == 4) {
+          qd[2] = qs[2];
+          qd[3] = qs[3];
+        }
+      }
+      const uint8_t* vs = vrow + kv[x];
+      uint8_t* vd = ov + v_at;
+      if ((evl == 8 || evl == 4) && !(((uintptr_t)vs | (uintptr_t)vd) & 3)) {   // dword moves
+        *reinterpret_cast<uint32_t*>(vd) = *reinterpret_cast<const uint32_t*>(vs);
+        if (evl == 8) *reinterpret_cast<uint32_t*>(vd + 4) = *reinterpret_cast<const uint32_t*>(vs + 4);
+      } else {
+        for (int b = 0; b < evl; b++) vd[b] = vs[b];
+      }
+      q_at += eq;
+      v_at += evl;
+    }
+  }
+  const uint8_t meta = (tm > 0 && tm < tc) ? 1 : 0;   // Const.MS_MIXED_COMPACT
+  __syncthreads();
+  if (t == 0 && tc > 1) ov[nv - 1] = meta;
+  __syncthreads();
+  uint32_t* dqw = reinterpret_cast<uint32_t*>(p.out_q + p.row_dq[r]);
+  uint32_t* dvw = reinterpret_cast<uint32_t*>(p.out_v + p.row_dv[r]);
+  for (int w = t; w < nqd; w += CMP_ROW_THREADS) dqw[w] = oqw[w];
+  for (int w = t; w < nvd; w += CMP_ROW_THREADS) dvw[w] = ovw[w];
+  if (t == 0) {
+    p.row_state[r] = 1;
+    p.row_q[r] = tq;
+    p.row_v[r] = nv;
+    p.row_meta[r] = meta;
+    p.row_lo[r] = tc;
+  }
+  (void)ocm;
+}
+
+// k_cmp_cols for the one-pass path: one wave a row, its lanes striding over the row's columns
+// (coalesced), the row's heap count / datapoints / byte bounds reduced in the wave and stored
+// once -- no per-column row index, no atomics (k_cmp_cols' per-row atomics from every wave of a
+// 3600-column row serialised in L2: 1.1 ms for 72M columns against 0.78 without the sums).
+__global__ __launch_bounds__(256) void k_cmp_cols_rowwave(CmpParams p) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= p.n_rows) return;
+  const int lane = (int)(threadIdx.x & 63);
+  const int64_t c0 = p.row_col_ptr[r], c1 = p.row_col_ptr[r + 1];
+  long long heap = 0, n = 0, qs = 0, vs = 0;
+  int64_t top = -1;
+  for (int64_t c = c0 + lane; c < c1; c += 64) {
+    int64_t qb = 0, vb = 0, nc = 0;
+    if (cmp_col(p, c, r, &qb, &vb, &nc)) { heap++; top = c; }
+    n += nc;
+    qs += qb;
+    vs += vb;
+  }
+  heap = wave_sum64(heap);
+  n = wave_sum64(n);
+  qs = wave_sum64(qs);
+  vs = wave_sum64(vs);
+  long long t = (long long)top;
+  for (int d = 32; d >= 1; d >>= 1) t = max(t, (long long)__shfl_xor(t, d, 64));
+  if (lane == 0) {
+    p.row_heap[r] = (int32_t)heap;
+    p.row_one[r] = t < 0 ? 0 : (int64_t)t;
+    p.row_n[r] = n;
+    p.row_qb[r] = qs;
+    p.row_vb[r] = vs;
+  }
+}
+
+hipError_t cmp_cols_rows(const CmpParams& p, hipStream_t s) {
+  if (p.n_rows > 0) hipLaunchKernelGGL(k_cmp_cols_rowwave, dim3((unsigned)((p.n_rows + 3) / 4)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+int cmp_onepass_cap(const CmpParams& p, uint32_t* scratch3, hipStream_t s, hipError_t* err) {
+  *err = hipSuccess;
+  if (p.n_rows <= 0) return 64;
+  if ((*err = hipMemsetAsync(scratch3, 0, 12, s)) != hipSuccess) return 0;
+  hipLaunchKernelGGL(k_cmp_rowmax2, dim3(blocks_of(p.n_rows)), dim3(256), 0, s, p, scratch3);
+  uint32_t h[3] = {0, 0, 0};
+  if ((*err = hipMemcpyAsync(h, scratch3, 12, hipMemcpyDeviceToHost, s)) != hipSuccess) return 0;
+  if ((*err = hipStreamSynchronize(s)) != hipSuccess) return 0;
+  if (h[0] > (uint32_t)CMP_ROW_CAP || h[1] > 65535u) return 0;
+  int cap = 64;
+  while (cap < (int)h[0]) cap <<= 1;
+  return cap;
+}
+
+hipError_t cmp_rows_onepass(const CmpParams& p, int cap, hipStream_t s) {
+  if (p.n_rows <= 0) return hipSuccess;
+  // the sort's arrays (20 B an entry); the cell assembled in the same space needs <= 12 B an entry
+  const size_t lds = (size_t)cap * 20;
+  if (lds > 65536) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_cmp_rowone, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_cmp_rowone, dim3((unsigned)p.n_rows), dim3(CMP_ROW_THREADS), lds, s, p, cap);
+  return hipGetLastError();
 }
 
 int cmp_row_cap(const CmpParams& p, uint32_t* scratch3, hipStream_t s, hipError_t* err, uint32_t* span) {

@@ -1018,7 +1018,7 @@ template <int N = DPL>
 __device__ __forceinline__ uint32_t next_key32(const uint32_t key[N], uint32_t k0, int target);
 
 // Keys of rank `target` and `target + 1` (0-based, ascending; k1 only when want1) among the
-// wave's 512 keys (absent = 0, counted first; each lane's 8 keys sorted descending).  Mid-rank
+// wave's 512 keys (absent = 0, counted first; any order in a lane).  Mid-rank
 // statistics (median, p50, p75) take it instead of popping ~n/2 wave maxima.
 // Phase 1, a bitwise binary search over the key bits below the prefix every present key
 // shares, narrows [ans, ans + 2^b) until it holds <= 64 keys (the counts below both ends come
@@ -1146,7 +1146,7 @@ __device__ __forceinline__ int keys_stat(const GridParams& p, uint32_t key[N], i
   uint32_t ek, ek1;
   if (min(ktop, kbot) > EXT_MAX) {
     if constexpr (!MID) return 0;   // (the near-end variant keeps its registers for the extraction)
-    sortN_desc<N>(key);
+    // (kth_pair32 needs no per-lane order: its counts, candidate list and next key compare every slot)
     const int zeros = 64 * N - n;
     uint32_t k0, k1;
     kth_pair32<N>(key, zeros + lo_i, hi_i != lo_i, k0, k1, zeros);

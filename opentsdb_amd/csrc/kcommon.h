@@ -104,6 +104,39 @@ __device__ __forceinline__ long long wave_sum64(long long x) {
 // value of lane l (uniform result)
 __device__ __forceinline__ int lane_bcast(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
 
+// Wave reduction by DPP (the inclusive-scan pattern of wave_incl_sum_dpp; lane 63 ends with the
+// whole wave, returned as a uniform value).  op(a, b) combines, id is its identity; every lane
+// must be active.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_mov_f64(double x, double id) {
+  const long long b = __double_as_longlong(x), ib = __double_as_longlong(id);
+  const int lo = __builtin_amdgcn_update_dpp((int)ib, (int)b, CTRL, ROWS, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(ib >> 32), (int)(b >> 32), CTRL, ROWS, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+template <class Op>
+__device__ __forceinline__ double wave_reduce_f64(double x, double id, Op op) {
+  x = op(x, dpp_mov_f64<0x111, 0xF>(x, id));
+  x = op(x, dpp_mov_f64<0x112, 0xF>(x, id));
+  x = op(x, dpp_mov_f64<0x114, 0xF>(x, id));
+  x = op(x, dpp_mov_f64<0x118, 0xF>(x, id));
+  x = op(x, dpp_mov_f64<0x142, 0xA>(x, id));
+  x = op(x, dpp_mov_f64<0x143, 0xC>(x, id));
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+template <class Op>
+__device__ __forceinline__ int wave_reduce_i32(int x, int id, Op op) {
+  x = op(x, __builtin_amdgcn_update_dpp(id, x, 0x111, 0xF, 0xF, false));
+  x = op(x, __builtin_amdgcn_update_dpp(id, x, 0x112, 0xF, 0xF, false));
+  x = op(x, __builtin_amdgcn_update_dpp(id, x, 0x114, 0xF, 0xF, false));
+  x = op(x, __builtin_amdgcn_update_dpp(id, x, 0x118, 0xF, 0xF, false));
+  x = op(x, __builtin_amdgcn_update_dpp(id, x, 0x142, 0xA, 0xF, false));
+  x = op(x, __builtin_amdgcn_update_dpp(id, x, 0x143, 0xC, 0xF, false));
+  return __builtin_amdgcn_readlane(x, 63);
+}
+
 // ---- big-endian value decode (RowSeq.extractIntegerValue / extractFloatingPointValue,
 //      src/core/RowSeq.java:233-266); returns false on an illegal length -------------
 __device__ __forceinline__ bool decode_value(uint64_t be_bits, int len, bool is_float, double& out) {
@@ -1761,11 +1794,65 @@ __device__ __forceinline__ void fast_chunk(const GridParams& p, const FastLds& L
   }
 }
 
+// The whole chunk in one bucket (an hour bucket over an hour row, GridParams.oneb): one wave
+// reduction and one fold.  A fold a lane would serialise ~45 LDS atomics on one slot.  Any
+// association is exact here (the series' certificate covers every partial sum), min / max are
+// order-free.  Called by the whole wave; false = not one bucket (nothing folded).
+template <int F, int QW, int VL>
+__device__ __forceinline__ bool fast_chunk_oneb(const GridParams& p, const FastLds& L, const FRaw<QW, VL>& b,
+                                                const FGeom& m, int nv0, int K) {
+  const int lane = lane_id();
+  const int n = min(nv0, CH);
+  const int nvl = max(0, min(DPL, n - lane * DPL));
+  const int uq = (QW == 2 && !p.unit_s) ? 1000 : 1;
+  const int ll = (n - 1) / DPL, jl = (n - 1) % DPL;   // the chunk's last datapoint: lane, slot
+  uint32_t fl = 0;
+#pragma unroll
+  for (int j = 0; j < DPL; j++) if (j == jl) fl = f_field<QW, VL>(b, j);
+  const int n0 = m.r0 + (int)__builtin_amdgcn_readfirstlane((int)f_field<QW, VL>(b, 0)) * uq;
+  const int nl = m.r0 + (int)__builtin_amdgcn_readlane((int)fl, ll) * uq;
+  if (n0 < 0) return false;
+  const int s0 = f_slot(p, m, n0);
+  if (f_slot(p, m, nl) != s0 || s0 >= K) return false;
+  const uint32_t cnt = (uint32_t)n;
+  if constexpr (F == F_COUNT) {
+    if (lane == 0) fast_fold<F>(L, s0, 0.0, cnt);
+  } else if constexpr (VL == 0 && F != F_SQUARESUM) {   // vle integers: |x| < 2^15, 512 of them add in int32
+    constexpr int ID = F == F_MIN ? INT32_MAX : (F == F_MAX ? INT32_MIN : 0);
+    int P = ID;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      const int x = j < nvl ? f_int16<QW, VL>(b, j) : ID;
+      P = F == F_MIN ? min(P, x) : (F == F_MAX ? max(P, x) : P + x);
+    }
+    const int tot = wave_reduce_i32(P, ID, [](int a, int c) { return F == F_MIN ? min(a, c) : (F == F_MAX ? max(a, c) : a + c); });
+    if (lane == 0) fast_fold<F>(L, s0, (double)tot, cnt);
+  } else {
+    const double ID = fast_identity<F>();
+    double P = ID;
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      double x = VL == 0 ? (double)f_int16<QW, VL>(b, j) : f_value<QW, VL>(b, j);
+      if (F == F_SQUARESUM) x = x * x;
+      if (j >= nvl) x = ID;
+      P = F == F_MIN ? fmin(P, x) : (F == F_MAX ? fmax(P, x) : P + x);
+    }
+    const double tot = wave_reduce_f64(P, ID, [](double a, double c) {
+      return F == F_MIN ? fmin(a, c) : (F == F_MAX ? fmax(a, c) : a + c);
+    });
+    if (lane == 0) fast_fold<F>(L, s0, tot, cnt);
+  }
+  return true;
+}
+
 // A chunk of a row shorter than CH: when every lane is either full or empty (a row of a
 // multiple of 8 datapoints, e.g. 360), the full-lane code runs on the non-empty lanes.
 template <int F, int QW, int VL>
 __device__ __forceinline__ void fast_chunk_any(const GridParams& p, const FastLds& L, const FRaw<QW, VL>& b,
                                                const FGeom& m, int nv0, int K) {
+#ifndef TSDBHIP_NO_ONEB
+  if (p.oneb && fast_chunk_oneb<F, QW, VL>(p, L, b, m, nv0, K)) return;
+#endif
   const int nvl = max(0, min(DPL, nv0 - lane_id() * DPL));
   if (__all(nvl == 0 || nvl == DPL)) {
     if (nvl) fast_chunk<F, QW, VL, true>(p, L, b, m, nv0, K);
@@ -1968,6 +2055,10 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
             g = fgeom(p, x.base);
           }
           const int nv0 = (int)(mb & FM_NV);
+#ifndef TSDBHIP_NO_ONEB
+          if (p.oneb && fast_chunk_oneb<F, QW, VL>(p, L, buf[i], g, nv0, K)) {
+          } else
+#endif
           if (nv0 >= CH) fast_chunk<F, QW, VL, true>(p, L, buf[i], g, nv0, K);
           else fast_chunk<F, QW, VL, false>(p, L, buf[i], g, nv0, K);
           if (fast_issue<F, QW, VL>(p, rows, w, buf[i], meta[i]) == 2) { redo = true; done = true; }

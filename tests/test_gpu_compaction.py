@@ -390,14 +390,16 @@ def _queries_and_answers(eng):
 
 @pytest.mark.parametrize("seed,salt,fix", [(41, False, True), (42, True, True), (43, False, False), (44, False, True)])
 def test_row_lds_path_equals_global_sort(eng, seed, salt, fix):
-    """The per-row LDS compaction (k_cmp_row: explode, bitonic sort, dedup and write in one block)
-    against the global-sort pipeline (TSDBHIP_CMP_ROWS=0): the same resident rows, the same
-    lazily raised errors, the same query answers -- also in chunks (TSDBHIP_CMP_CHUNK)."""
+    """The per-row LDS compaction -- one pass (k_cmp_rowone: explode, sort, dedup and the cell
+    written into the region the host laid out from k_cmp_cols' bounds), and the sizing + write
+    passes (k_cmp_row / k_cmp_rowwrite, TSDBHIP_CMP_ONEPASS=0, and in chunks) -- against the
+    global-sort pipeline (TSDBHIP_CMP_ROWS=0): the same resident rows, the same lazily raised
+    errors, the same query answers."""
     series, groups = _random_scan(seed, salt=salt)
     cb = abi.HostCellBatch.from_rows(series, groups, fix)
     want = _load_with_env(eng, cb, TSDBHIP_CMP_ROWS=0)
     answers = _queries_and_answers(eng)
-    for env in ({}, {"TSDBHIP_CMP_CHUNK": 150}):
+    for env in ({}, {"TSDBHIP_CMP_ONEPASS": 0}, {"TSDBHIP_CMP_CHUNK": 150}):
         got = _load_with_env(eng, cb, **env)
         assert rows_of(got) == rows_of(want), env
         assert np.array_equal(got.group_id, want.group_id)

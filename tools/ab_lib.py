@@ -39,12 +39,19 @@ def run(lib_path, cfg, fns, steps):
     if cfg == 5:
         sp = abi.SynthSpec(1_250_000, T0, 8640, 10000, 0, 64, 2000, 0x5EED)
         end, interval = T0 + 86399, 3600000
+    elif cfg == 2:
+        sp = abi.SynthSpec(1_000_000, T0, 3600, 1000, 0, 64, 1, 0x5EED)
+        end, interval = T0 + 3599, 60000
     else:
         sp = abi.SynthSpec(10_000_000, T0, 360, 10000, 2, 1000, 30000, 0x5EED)
         end, interval = T0 + 3599, 60000
     assert L.tsdbhip_synth(ctx, C.byref(sp)) == 0
     for fn in fns:
         agg, ds = ("sum", fn) if cfg == 5 else (fn, "avg")
+        if cfg == 2 and ":" in fn:
+            agg, ds = fn.split(":")
+            interval = {"1m": 60000, "1h": 3600000}[ds.split("-")[0]]
+            ds = ds.split("-")[1]
         q = abi.new_query(T0, end, agg, ds_function=abi.AGG[ds], ds_interval_ms=interval)
         res = C.POINTER(abi.Result)()
         for _ in range(2):
