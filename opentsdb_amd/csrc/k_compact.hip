@@ -498,6 +498,29 @@ __device__ __forceinline__ int block_excl_scan(int x, int* sh, int* total) {
   return base + v - x;
 }
 
+// two block-wide exclusive scans sharing one pair of barriers (LDS scratch >= 2 x 16 ints)
+__device__ __forceinline__ int block_excl_scan2(int x, int y, int* sh, int* totx, int* oy, int* toty) {
+  const int t = threadIdx.x;
+  const int nw = (int)(blockDim.x >> 6);
+  const int lane = t & 63;
+  const int vx = wave_incl_sum_dpp(x), vy = wave_incl_sum_dpp(y);
+  if (lane == 63) { sh[t >> 6] = vx; sh[16 + (t >> 6)] = vy; }
+  __syncthreads();
+  int bx = 0, ax = 0, by = 0, ay = 0;
+  for (int w = 0; w < nw; w++) {
+    const int sx = sh[w], sy = sh[16 + w];
+    bx += w < (t >> 6) ? sx : 0;
+    by += w < (t >> 6) ? sy : 0;
+    ax += sx;
+    ay += sy;
+  }
+  __syncthreads();
+  *totx = ax;
+  *toty = ay;
+  *oy = by + vy - y;
+  return bx + vx - x;
+}
+
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int m) {
   const int lo = __shfl_xor((int)(uint32_t)x, m, 64), hi = __shfl_xor((int)(uint32_t)(x >> 32), m, 64);
   return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
@@ -904,7 +927,7 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_rowone(CmpParams p, int
   uint32_t* ev_src = eq_src + P;
   uint16_t* eem = reinterpret_cast<uint16_t*>(ev_src + P);
   uint16_t* ecol = eem + P;
-  __shared__ int scan_sh[CMP_ROW_THREADS / 64];
+  __shared__ int scan_sh[2 * CMP_ROW_THREADS / 64];
   __shared__ int dup_err;
   const int64_t r = blockIdx.x;
   const int t = threadIdx.x;
@@ -934,36 +957,47 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_rowone(CmpParams p, int
   const uint64_t qb = p.col_qo[c0], vb = p.col_vo[c0];
   const uint8_t* qrow = p.q + qb;
   const uint8_t* vrow = p.v + vb;
-  // explode, 1024 columns a round: the entry offsets of a round from a block scan of its counts
+  // explode, 4096 columns a round (4 consecutive a thread, in scan order): the entry offsets of a
+  // round from one block scan of the threads' counts
+  constexpr int CPT = 4;
   int n = 0;
-  for (int64_t cr = c0; cr < c1; cr += CMP_ROW_THREADS) {
-    const int64_t c = cr + t;
-    const int nc_ = c < c1 ? (int)p.col_n[c] : 0;
+  for (int64_t cr = c0; cr < c1; cr += CMP_ROW_THREADS * CPT) {
+    const int64_t cb = cr + (int64_t)t * CPT;
+    int ncs[CPT], sum = 0;
+#pragma unroll
+    for (int j = 0; j < CPT; j++) {
+      ncs[j] = cb + j < c1 ? (int)p.col_n[cb + j] : 0;
+      sum += ncs[j];
+    }
     int tot;
-    int e = n + block_excl_scan(nc_, scan_sh, &tot);
+    int e = n + block_excl_scan(sum, scan_sh, &tot);
     n += tot;
-    if (nc_ == 0) continue;
-    const uint64_t qo = p.col_qo[c], vo = p.col_vo[c];
-    const int64_t ql = (int64_t)(p.col_qo[c + 1] - qo), vl = (int64_t)(p.col_vo[c + 1] - vo);
-    const uint32_t info = p.col_info[c];
-    const bool app = (info & 3) == CMP_APPEND;
-    const bool fix = !app && ql == 2 && (info & 8);
-    const uint32_t qbase = (uint32_t)((app ? vo - vb : qo - qb));
-    const uint32_t vbase = (uint32_t)(vo - vb);
-    auto put = [&](int64_t qpos, int64_t vpos, int eq, int evl, uint32_t off) {
-      key[e] = ((uint64_t)off << 12) | (uint64_t)e;
-      eq_src[e] = qbase + (uint32_t)qpos;
-      ev_src[e] = vbase + (uint32_t)vpos;
-      eem[e] = (uint16_t)((eq == 4 ? 1u : 0u) | ((uint32_t)(evl - 1) << 1) | (fix ? 16u : 0u) | (app ? 32u : 0u));
-      ecol[e] = (uint16_t)(c - c0);
-      e++;
-    };
-    if (app) {
-      walk_append(p.v + vo, vl, put);
-    } else {
-      const int64_t vstart = (info & 4) ? 4 : 0;
-      walk_data(p.q + qo, ql, vl - vstart, (uint8_t)(info >> 8),
-                [&](int64_t qi, int64_t vi, int eq, int evl, uint32_t off) { put(qi, vstart + vi, eq, evl, off); });
+#pragma unroll
+    for (int j = 0; j < CPT; j++) {
+      if (ncs[j] == 0) continue;
+      const int64_t c = cb + j;
+      const uint64_t qo = p.col_qo[c], vo = p.col_vo[c];
+      const int64_t ql = (int64_t)(p.col_qo[c + 1] - qo), vl = (int64_t)(p.col_vo[c + 1] - vo);
+      const uint32_t info = p.col_info[c];
+      const bool app = (info & 3) == CMP_APPEND;
+      const bool fix = !app && ql == 2 && (info & 8);
+      const uint32_t qbase = (uint32_t)((app ? vo - vb : qo - qb));
+      const uint32_t vbase = (uint32_t)(vo - vb);
+      auto put = [&](int64_t qpos, int64_t vpos, int eq, int evl, uint32_t off) {
+        key[e] = ((uint64_t)off << 12) | (uint64_t)e;
+        eq_src[e] = qbase + (uint32_t)qpos;
+        ev_src[e] = vbase + (uint32_t)vpos;
+        eem[e] = (uint16_t)((eq == 4 ? 1u : 0u) | ((uint32_t)(evl - 1) << 1) | (fix ? 16u : 0u) | (app ? 32u : 0u));
+        ecol[e] = (uint16_t)(c - c0);
+        e++;
+      };
+      if (app) {
+        walk_append(p.v + vo, vl, put);
+      } else {
+        const int64_t vstart = (info & 4) ? 4 : 0;
+        walk_data(p.q + qo, ql, vl - vstart, (uint8_t)(info >> 8),
+                  [&](int64_t qi, int64_t vi, int eq, int evl, uint32_t off) { put(qi, vstart + vi, eq, evl, off); });
+      }
     }
   }
   for (int i = n + t; i < P; i += CMP_ROW_THREADS) key[i] = ~0ull >> 2;
@@ -1088,9 +1122,8 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_rowone(CmpParams p, int
       }
     }
   }
-  int tqv, tcm;
-  const int oqv = block_excl_scan((sq << 16) | sv, scan_sh, &tqv);   // (sq <= 16384, sv <= 32768 a row)
-  const int ocm = block_excl_scan((kc << 16) | sms, scan_sh, &tcm);
+  int tqv, tcm, ocm;
+  const int oqv = block_excl_scan2((sq << 16) | sv, (kc << 16) | sms, scan_sh, &tqv, &ocm, &tcm);   // (sq <= 16384, sv <= 32768 a row)
   const int tq = tqv >> 16, tv = tqv & 0xFFFF, tc = tcm >> 16, tm = tcm & 0xFFFF;
   if (dup_err) { no_cell(); return; }
   if (tc == 0) { no_cell(); return; }
@@ -1106,9 +1139,10 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_rowone(CmpParams p, int
   const int nqd = (tq + 3) >> 2, nvd = (nv + 3) >> 2;
   uint32_t* oqw = reinterpret_cast<uint32_t*>(oq);
   uint32_t* ovw = reinterpret_cast<uint32_t*>(ov);
-  for (int w = t; w < nqd; w += CMP_ROW_THREADS) oqw[w] = 0;
-  for (int w = t; w < nvd; w += CMP_ROW_THREADS) ovw[w] = 0;
-  __syncthreads();
+  const uint8_t meta = (tm > 0 && tm < tc) ? 1 : 0;   // Const.MS_MIXED_COMPACT
+  // (no zero pass: the cell's bytes are each written once below; the thread holding the last kept
+  // datapoint writes the meta byte and zeroes the rest of the last dwords)
+  const bool last_owner = kc > 0 && (ocm >> 16) + kc == tc;
   int q_at = oqv >> 16, v_at = oqv & 0xFFFF;
 #pragma unroll
   for (int x = 0; x < MMAX; x++) {
@@ -1141,9 +1175,11 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_rowone(CmpParams p, int
       v_at += evl;
     }
   }
-  const uint8_t meta = (tm > 0 && tm < tc) ? 1 : 0;   // Const.MS_MIXED_COMPACT
-  __syncthreads();
-  if (t == 0 && tc > 1) ov[nv - 1] = meta;
+  if (last_owner) {
+    if (tc > 1) ov[nv - 1] = meta;
+    for (int b = tq; b < nqd * 4; b++) oq[b] = 0;
+    for (int b = nv; b < nvd * 4; b++) ov[b] = 0;
+  }
   __syncthreads();
   uint32_t* dqw = reinterpret_cast<uint32_t*>(p.out_q + p.row_dq[r]);
   uint32_t* dvw = reinterpret_cast<uint32_t*>(p.out_v + p.row_dv[r]);
@@ -1156,7 +1192,6 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_rowone(CmpParams p, int
     p.row_meta[r] = meta;
     p.row_lo[r] = tc;
   }
-  (void)ocm;
 }
 
 // k_cmp_cols for the one-pass path: one wave a row, its lanes striding over the row's columns
