@@ -2749,7 +2749,33 @@ bool seq_rows_ok(tsdbhip_ctx* c, const Plan& P) {
 // HBM (5 % of HBM on config 3's day, c3day_bench).  Split it instead: the streaming kernels write
 // every series' buckets to HBM (dense_out, no partials in LDS), then the group-by step runs over
 // them (emit_only: k_emit + k_reduce), as the percentile functions do.
+// k_hwin takes the query: a fixed grid of K > 64 buckets dividing the hour with slot 0 on an
+// hour (every hour row in one window of W = 1 h / interval <= 64 slots), no rate, an order-free
+// function, and every tile of one streaming class with one-chunk rows.
+int hwin_slots(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P) {
+  if (const char* e = std::getenv("TSDBHIP_HWIN")) if (e[0] == '0') return 0;
+  // (fill policies need every participating series' fill values in windows where it has no row:
+  // left to the dense split)
+  if (P.mode != MODE_GRID || q->rate || q->ds_fill != TSDB_FILL_NONE || P.K <= 64 || P.I <= 0 || 3600000 % P.I != 0 || 3600000 / P.I > 64 ||
+      ((P.B0 % 3600000) + 3600000) % 3600000 != 0 || P.dense_out || P.emit_only || P.values_only || P.sel_direct ||
+      P.multi || P.seq_dense || P.raw || P.anchored || P.none || P.f == F_SEL || !c->fast_qw || !c->tl_other.empty())
+    return 0;
+  for (int cls = 0; cls < 2; cls++) {
+    if (!c->tl[cls][0].empty()) return 0;
+    if (c->tl[cls][1].empty() && c->tl[cls][2].empty()) continue;
+    const int qw = cls ? c->fast_qw2 : c->fast_qw, vl = cls ? c->fast_vl2 : c->fast_vl;
+    if (!qw || !fast_supported(P.f, qw, vl)) return 0;
+  }
+  const char* env = std::getenv("TSDBHIP_FAST");
+  if (env && env[0] == '0') return 0;
+  // only where the one-pass streaming kernels' slot LDS does not fit (the dense split's case):
+  // with a handful of slots a window (10m: 6) k_rows' fused pass is faster (profiles/r04x)
+  if (fast_wave_lds(P.K, false, true) <= 32 * 1024) return 0;
+  return (int)(3600000 / P.I);
+}
+
 bool dense_split_wanted(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P) {
+  if (hwin_slots(c, q, P)) return false;   // (k_hwin needs no bucket store)
   if (P.dense_out || P.emit_only || P.values_only || P.sel_direct || P.multi || P.seq_dense || P.raw || P.anchored ||
       P.f == F_SEL || P.mode != MODE_GRID || P.K <= 64)
     return false;
@@ -3003,7 +3029,8 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   } else {
   // streaming kernel first (when the batch's row class and the query allow it), then the
   // general kernel over the tiles it handed back
-  const bool fast = fast_path_ok(c, q, P);
+  const int hwin = hwin_slots(c, q, P);
+  const bool fast = hwin || fast_path_ok(c, q, P);
   if (P.multi && !fast) return fail(TSDB_E_NOT_IMPLEMENTED, "fused multi-aggregator pass without the streaming kernels");
   c->fast_used = fast;
   HIP_OK(hipEventRecord(c->ev[0], c->stream));
@@ -3039,7 +3066,8 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       fp.rcpn = std::nextafter(1.0 / (double)fp.In, INFINITY);
       const char* oenv = std::getenv("TSDBHIP_ONEB");
       fp.oneb = P.I >= 3600000 && !(oenv && oenv[0] == '0') ? 1 : 0;   // (an hour row's chunk in one bucket)
-      fp.wave_lds = (int32_t)fast_lds_of(q, P);
+      fp.wave_lds = (int32_t)(shortk == 3 ? fast_wave_lds(hwin, false, false) : fast_lds_of(q, P));
+      fp.win_w = hwin;
       if (shortk == 1 && fp.sel_direct && fp.sel_cols && K <= 64) {   // k_short's column stage
         fp.sel_stage = fp.wave_lds;
         fp.wave_lds += (int32_t)align16(8 * K * 8);
@@ -3082,6 +3110,16 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       const int32_t* dn1 = dn + 3 * cls + 1;
       const int32_t* dn2 = dn + 3 * cls + 2;
       int rc;
+      if (hwin) {   // k_hwin over the one-chunk-row tiles (hwin_slots: no other tiles); k_grid takes what it hands back
+        for (int part = 1; part <= 2; part++) {
+          const int64_t nn = part == 1 ? n1 : n2;
+          if (!nn) continue;
+          rc = fast_launch(cls, 3, part == 1 ? l1 : l2, part == 1 ? dn1 : dn2, nn, c->r2.as<int32_t>(), rn + 2);
+          if (rc < 0) return rc;
+          if (rc == 1) { to_grid.push_back({part == 1 ? l1 : l2, {part == 1 ? dn1 : dn2, nn}}); routed += nn; }
+        }
+        continue;
+      }
       if (use_rows && n2) {
         rc = fast_launch(cls, 2, l2, dn2, n2, r3[cls], rn + 3 + cls);
         if (rc < 0) return rc;

@@ -59,6 +59,14 @@ static hipError_t launch_fast_k(const GridParams& p, hipStream_t s) {
 // dense paths; KR 2: every decomposable aggregator's partials at once, tsdbhip_run_multi)
 template <int F, int QW, int VL>
 static hipError_t launch_fast_t(const GridParams& p, hipStream_t s) {
+  if (p.shortk == 3) {   // k_hwin: K > 64 buckets tiling the hour, window by window
+    const int64_t nl = p.n_launch > 0 ? p.n_launch : p.n_tiles;
+    const int64_t blocks = (nl + p.waves - 1) / p.waves;
+    const size_t lds = (size_t)p.wave_lds * p.waves;
+    hipLaunchKernelGGL((k_hwin<F, QW, VL, 2>), dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p, p.rows,
+                       p.series_row_ptr, p.tile_begin, p.tile_end);
+    return hipGetLastError();
+  }
   if (p.K <= 64 && !p.rate) {
     if (p.multi) return launch_fast_k<F, QW, VL, 2>(p, s);
     return (p.sel_direct || p.dense_out) ? launch_fast_k<F, QW, VL, 3>(p, s) : launch_fast_k<F, QW, VL, 1>(p, s);

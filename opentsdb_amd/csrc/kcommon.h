@@ -2432,6 +2432,150 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
   }
 }
 
+// ---- k_hwin: K > 64 buckets that tile the hour (a day of 1m buckets over hour rows) ---------
+// Buckets dividing the hour with slot 0 on an hour (GridParams.win_w = W = 3600 s / interval
+// <= 64 slots): every hour row falls in one window of W slots.  The tile is walked window by
+// window; in a window every series contributes at most its one row, so the series' buckets and
+// the tile's partials of the window fit the wave (registers, KR 1's emit) -- no [series][K]
+// bucket store and no group-by pass over it (the dense split).  LERP needs neighbours across
+// windows, so a series with a bucket missing inside its data span hands the tile back (the
+// general kernel takes it); regular data never does.
+template <int F, int QW, int VL, int D>
+__global__ __launch_bounds__(256, SHORT_OCC(VL)) void k_hwin(GridParams p, const RowDesc* __restrict__ rows,
+                                                             const int64_t* __restrict__ srp, const int64_t* __restrict__ tbeg,
+                                                             const int64_t* __restrict__ tend) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int64_t tile = (int64_t)blockIdx.x * p.waves + wave;
+  if (p.tile_list) {
+    if (tile >= (int64_t)*p.tile_list_n) return;
+    tile = p.tile_list[tile];
+  }
+  if (tile >= p.n_tiles) return;
+  const int K = (int)p.K;
+  const int W = p.win_w;
+  const int NW = (K + W - 1) / W;
+  const int64_t s0 = tbeg[tile];
+  const int ns = (int)(tend[tile] - s0);
+  if (ns > 64) {
+    if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
+    return;
+  }
+  int64_t cur = lane < ns ? srp[s0 + lane] : 0;
+  const int64_t end = lane < ns ? srp[s0 + lane + 1] : 0;
+  const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, W, false, false);
+  for (int k = lane; k < W; k += 64) {
+    L.acc[k] = fast_identity<F>();
+    L.cnt[k] = 0;
+  }
+  RegPart RP;
+  rp_init(p.ga, RP);
+  WAVE_SYNC();
+  bool redo = false, any = false;
+  bool seen = false;   // the lane's series had a row in an earlier window
+  const bool lerp = p.fill == TSDB_FILL_NONE;   // (the host routes fill policies elsewhere)
+  for (int h = 0; h < NW && !redo; h++) {
+    const int Wh = min(W, K - h * W);
+    // the lane's row of window h: rows outside the scan range or before slot 0 are passed over
+    bool has = false, bad = false;
+    uint64_t dq = 0, dv = 0, damax = 0;
+    int dndp = 0, dlsb = INT32_MAX, gr0 = 0;
+    while (cur < end) {
+      const RowDesc& x = rows[cur];
+      const int64_t base = (int64_t)x.base;
+      const int64_t rel = p.unit_s ? base - p.B0n : base * 1000 - p.B0n;
+      if (base < p.ss || base >= p.se || rel < 0) { cur++; continue; }
+      const FGeom g = fgeom(p, (uint32_t)base);
+      if (g.r0 != 0 || g.q0 % W != 0) { bad = true; break; }   // (host-checked alignment)
+      const int wi = g.q0 / W;
+      if (wi < h) { cur++; continue; }
+      if (wi == h) {
+        has = true;
+        dq = x.qoff;
+        dv = x.voff;
+        dndp = (int)x.ndp;
+        dlsb = x.lsb;
+        damax = (uint64_t)__double_as_longlong(x.absmax);
+        gr0 = g.r0;
+        bad = !(dndp >= 1 && dndp <= CH &&
+                fast_row_ok<QW, VL>(x.flags, F == F_MIN || F == F_MAX, F == F_SUM || F == F_AVG));
+      }
+      break;
+    }
+    // a series without a row here but with rows on both sides: LERP would fill this window
+    if (lerp && !has && seen && cur < end) bad = true;
+    if (__ballot(bad)) { redo = true; break; }
+    uint64_t act = __ballot(has);
+    if (act) any = true;
+    // the window's series, in order: the ring over them
+    FRaw<QW, VL> buf[D];
+    int lanes_[D];
+    uint64_t rest = act;
+#pragma unroll
+    for (int i = 0; i < D; i++) {
+      const int ln = rest ? (int)__builtin_ctzll(rest) : -1;
+      if (rest) rest &= rest - 1;
+      lanes_[i] = ln;
+      const int l2 = ln < 0 ? 0 : ln;
+      short_issue<QW, VL>(p, rl64(dq, l2), rl64(dv, l2), ln < 0 ? 0 : __builtin_amdgcn_readlane(dndp, l2), buf[i]);
+    }
+    const int nact = __popcll(act);
+    for (int j = 0; j < nact && !redo; j += D) {
+#pragma unroll
+      for (int i = 0; i < D; i++) {
+        const int ln = lanes_[i];
+        if (j + i < nact) {
+          const int nv0 = __builtin_amdgcn_readlane(dndp, ln);
+          const FGeom g = {0, __builtin_amdgcn_readlane(gr0, ln)};   // window-relative: the row starts at slot 0
+          // the row's last datapoint inside the window (a second qualifier can reach 4095 s)
+          const int ll = (nv0 - 1) >> 3, jl = (nv0 - 1) & 7;
+          uint32_t fl = 0;
+#pragma unroll
+          for (int jj = 0; jj < DPL; jj++) if (jj == jl) fl = f_field<QW, VL>(buf[i], jj);
+          const int uq = (QW == 2 && !p.unit_s) ? 1000 : 1;
+          const int64_t lastn = (int64_t)g.r0 + (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)fl, ll) * uq;
+          if (lastn >= (int64_t)W * p.In) redo = true;
+          if (!redo) {
+            fast_chunk_any<F, QW, VL>(p, L, buf[i], g, nv0, Wh);
+            WAVE_SYNC();
+            // every bucket of the window present, or fill: the window's emit needs no neighbour
+            // from another window
+            if (lerp && __ballot(lane < Wh && L.cnt[lane] == 0)) redo = true;
+            const int lsb = __builtin_amdgcn_readlane(dlsb, ln);
+            const double amax = __longlong_as_double((long long)rl64(damax, ln));
+            if (!redo && !fast_series_end_reg<F, false, false>(p, L, Wh, lsb, amax, RP, s0 + ln, p.tile_group[tile],
+                                                               (uint32_t)nv0))
+              redo = true;
+          }
+        }
+        // next series of the window into this ring slot (issued unconditionally)
+        const int ln2 = rest ? (int)__builtin_ctzll(rest) : -1;
+        if (rest) rest &= rest - 1;
+        lanes_[i] = ln2;
+        const int l2 = ln2 < 0 ? 0 : ln2;
+        short_issue<QW, VL>(p, rl64(dq, l2), rl64(dv, l2), ln2 < 0 ? 0 : __builtin_amdgcn_readlane(dndp, l2), buf[i]);
+      }
+    }
+    if (redo) break;
+    // the window's partials: slots h W .. h W + Wh - 1 of the tile
+    if (lane < Wh) {
+      const int64_t o = tile * K + (int64_t)h * W + lane;
+      p.part.a[o] = RP.pa;
+      p.part.b[o] = RP.pb;
+      p.part.n[o] = RP.pn;
+      p.part.f[o] = RP.pf;
+    }
+    rp_init(p.ga, RP);
+    if (has) { seen = true; cur++; }
+  }
+  if (redo) {
+    if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
+    return;
+  }
+  if (any && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
+}
+
 // ---- k_reduce -------------------------------------------------------------------
 struct PState {
   double a, b;

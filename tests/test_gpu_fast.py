@@ -429,7 +429,9 @@ def run_rows(eng, batch, q, rows: bool, monkeypatch):
 def test_rows_kernel_matches_walker(eng, monkeypatch, agg, ds, iv, win, rate):
     """k_rows (series of several one-chunk rows, descriptors in 64-row batches) against k_fast's
     row walker (TSDBHIP_ROWS=0) and k_grid, bit for bit: 40000 series of 24 hour rows (4 series a
-    tile, 96 rows: the batch refill), int and float series (two row classes)."""
+    tile, 96 rows: the batch refill), int and float series (two row classes).  (k_hwin off: the
+    1m case runs the dense split; its buckets are one datapoint in 100 s, LERP fills between.)"""
+    monkeypatch.setenv("TSDBHIP_HWIN", "0")
     eng.synth(40000, T0, 24 * 36, 100000, 2, 1000, 30000, 0x5EED)
     q = abi.new_query(T0 + win[0], T0 + win[1], agg, ds_function=abi.AGG[ds], ds_interval_ms=iv, rate=rate)
     r, tr = run_rows(eng, None, q, True, monkeypatch)
@@ -478,3 +480,57 @@ def test_rows_kernel_irregular(eng, monkeypatch):
         assert_bit_equal(r, w, ctx + " rows vs walker")
         assert_bit_equal(r, g, ctx + " rows vs general")
         assert_groups_match(r, O.run_query(b, q), agg, ctx=ctx)
+
+
+def run_hwin(eng, batch, q, on: bool, monkeypatch):
+    monkeypatch.setenv("TSDBHIP_HWIN", "1" if on else "0")
+    try:
+        return run_path(eng, batch, q, True)
+    finally:
+        monkeypatch.delenv("TSDBHIP_HWIN")
+
+
+@pytest.mark.parametrize("agg,ds,iv,win,fill", [
+    ("sum", "avg", 60000, (0, 86399), abi.FILL_NONE),        # K 1440 (config 3's day)
+    ("avg", "sum", 60000, (7200, 79199), abi.FILL_NONE),     # K 1200, window inside the data
+    ("max", "min", 60000, (0, 86399), abi.FILL_NONE),
+    ("dev", "avg", 60000, (3600, 86399), abi.FILL_NONE),
+    ("count", "count", 60000, (0, 86399), abi.FILL_NONE),
+    ("sum", "squareSum", 60000, (0, 86399), abi.FILL_NONE),  # squares rarely certify: handed back
+    ("sum", "avg", 60000, (-3600, 90000 - 1), abi.FILL_NONE),   # window wider than the data
+])
+def test_hwin_matches_dense_split(eng, monkeypatch, agg, ds, iv, win, fill):
+    """k_hwin (K > 64 buckets tiling the hour, walked window by window with register partials; the
+    queries whose one-pass slot LDS does not fit, K >= 859) against the dense split (TSDBHIP_HWIN=0: buckets stored, then k_emit_win) and the general
+    kernel, bit for bit: 40000 series x a day of 10 s points (24 hour rows), int and float series."""
+    eng.synth(40000, T0, 24 * 360, 10000, 2, 1000, 30000, 0x5EED)
+    q = abi.new_query(T0 + win[0], T0 + win[1], agg, ds_function=abi.AGG[ds], ds_interval_ms=iv, ds_fill=fill)
+    h, th = run_hwin(eng, None, q, True, monkeypatch)
+    d, td = run_hwin(eng, None, q, False, monkeypatch)
+    g, tg = run_path(eng, None, q, False)
+    ctx = f"hwin {agg}:{ds} {iv} {win} fill {fill}"
+    assert th.fast_ms > 0, ctx
+    if ds != "squareSum":
+        assert th.redo_tiles == 0, f"{ctx}: {th.redo_tiles} tiles handed back"
+    assert_bit_equal(h, d, ctx + " hwin vs split")
+    assert_bit_equal(h, g, ctx + " hwin vs general")
+
+
+def test_hwin_holes_handed_back(eng, monkeypatch):
+    """Buckets missing inside a series' span (100 s points in 1m buckets; a series missing an hour):
+    LERP needs neighbours from other windows, so k_hwin hands those tiles to the general kernel --
+    same answers as the general path and the oracle."""
+    b = _irregular_rows(seed=9, n=120)
+    for agg, ds, iv in [("sum", "avg", 60000), ("avg", "max", 120000)]:
+        q = abi.new_query(T0, T0 + 30 * 3600 - 1, agg, ds_function=abi.AGG[ds], ds_interval_ms=iv)
+        h, th = run_hwin(eng, b, q, True, monkeypatch)
+        g, tg = run_path(eng, b, q, False)
+        ctx = f"hwin holes {agg}:{ds} {iv}"
+        assert_bit_equal(h, g, ctx)
+        assert_groups_match(h, O.run_query(b, q), agg, ctx=ctx)
+    eng.synth(4000, T0, 24 * 36, 100000, 0, 16, 1, 3)
+    q = abi.new_query(T0, T0 + 86399, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+    h, th = run_hwin(eng, None, q, True, monkeypatch)
+    g, tg = run_path(eng, None, q, False)
+    assert th.redo_tiles > 0
+    assert_bit_equal(h, g, "hwin 100 s points")
