@@ -1030,30 +1030,33 @@ __device__ __forceinline__ void kth_pair32(const uint32_t key[N], int target, bo
                                            uint32_t& k1, int zeros) {
   __shared__ uint32_t cand_lds[4][64];
   uint32_t* cand_row = cand_lds[threadIdx.x >> 6];
-  uint32_t kand = ~0u, kor = 0u;
+  // the prefix every present key shares = the common prefix of the smallest and largest present
+  // key (absent keys are 0: the max ignores them, the min of key - 1 wraps them to the top)
+  uint32_t kmx = 0u, kmn1 = ~0u;
 #pragma unroll
   for (int j = 0; j < N; j++) {
-    if (key[j]) { kand &= key[j]; kor |= key[j]; }
+    kmx = max(kmx, key[j]);
+    kmn1 = min(kmn1, key[j] - 1u);
   }
-  // wave AND / OR by DPP (row shifts, then the row broadcasts; lane 63 ends with the whole wave)
-  kand &= (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)kand, 0x111, 0xF, 0xF, false);
-  kor |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kor, 0x111, 0xF, 0xF, false);
-  kand &= (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)kand, 0x112, 0xF, 0xF, false);
-  kor |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kor, 0x112, 0xF, 0xF, false);
-  kand &= (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)kand, 0x114, 0xF, 0xF, false);
-  kor |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kor, 0x114, 0xF, 0xF, false);
-  kand &= (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)kand, 0x118, 0xF, 0xF, false);
-  kor |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kor, 0x118, 0xF, 0xF, false);
-  kand &= (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)kand, 0x142, 0xA, 0xF, false);
-  kor |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kor, 0x142, 0xA, 0xF, false);
-  kand &= (uint32_t)__builtin_amdgcn_update_dpp(~0, (int)kand, 0x143, 0xC, 0xF, false);
-  kor |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kor, 0x143, 0xC, 0xF, false);
-  kand = (uint32_t)__builtin_amdgcn_readlane((int)kand, 63);
-  kor = (uint32_t)__builtin_amdgcn_readlane((int)kor, 63);
-  const uint32_t diff = kand ^ kor;
-  if (diff == 0) { k0 = k1 = kand; return; }   // every present key equal
+  // wave max / min by DPP (row shifts, then the row broadcasts; lane 63 ends with the whole wave)
+  kmx = max(kmx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kmx, 0x111, 0xF, 0xF, false));
+  kmn1 = min(kmn1, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)kmn1, 0x111, 0xF, 0xF, false));
+  kmx = max(kmx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kmx, 0x112, 0xF, 0xF, false));
+  kmn1 = min(kmn1, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)kmn1, 0x112, 0xF, 0xF, false));
+  kmx = max(kmx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kmx, 0x114, 0xF, 0xF, false));
+  kmn1 = min(kmn1, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)kmn1, 0x114, 0xF, 0xF, false));
+  kmx = max(kmx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kmx, 0x118, 0xF, 0xF, false));
+  kmn1 = min(kmn1, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)kmn1, 0x118, 0xF, 0xF, false));
+  kmx = max(kmx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kmx, 0x142, 0xA, 0xF, false));
+  kmn1 = min(kmn1, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)kmn1, 0x142, 0xA, 0xF, false));
+  kmx = max(kmx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kmx, 0x143, 0xC, 0xF, false));
+  kmn1 = min(kmn1, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)kmn1, 0x143, 0xC, 0xF, false));
+  kmx = (uint32_t)__builtin_amdgcn_readlane((int)kmx, 63);
+  const uint32_t kmn = (uint32_t)__builtin_amdgcn_readlane((int)kmn1, 63) + 1u;   // (n >= 1 present keys)
+  const uint32_t diff = kmn ^ kmx;
+  if (diff == 0) { k0 = k1 = kmn; return; }   // every present key equal
   int b = 32 - __clz((int)diff);   // width of the open interval [ans, ans + 2^b)
-  uint32_t ans = b == 32 ? 0u : (kand & ~((1u << b) - 1u));
+  uint32_t ans = b == 32 ? 0u : (kmn & ~((1u << b) - 1u));
   // count of keys below ans / below ans + 2^b (the absent keys, 0, below every present key)
   int lowc = zeros, highc = 64 * N;
   while (b > 0 && highc - lowc > 64) {
@@ -1072,14 +1075,17 @@ __device__ __forceinline__ void kth_pair32(const uint32_t key[N], int target, bo
     return;
   }
   const uint32_t span = b == 32 ? ~0u : (1u << b) - 1u;   // keys in the interval: key - ans <= span
+  // present keys in [ans, ans + span] with one compare: key - lo <= hb, lo = max(ans, 1) keeps the
+  // absent keys (0) out when ans is 0
+  const uint32_t lo = ans ? ans : 1u, hb = span - (lo - ans);
   int m = 0;
 #pragma unroll
-  for (int j = 0; j < N; j++) m += (key[j] != 0 && key[j] - ans <= span) ? 1 : 0;
+  for (int j = 0; j < N; j++) m += (key[j] - lo <= hb) ? 1 : 0;
   int pos = wave_incl_sum_dpp(m) - m;
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int j = 0; j < N; j++) {
-    if (key[j] != 0 && key[j] - ans <= span) cand_row[pos++] = key[j];
+    if (key[j] - lo <= hb) cand_row[pos++] = key[j];
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
