@@ -1101,12 +1101,16 @@ __device__ __forceinline__ void kth_pair32(const uint32_t key[N], int target, bo
   // instructions for each of the ~20 open key bits, and the kernel is bound by the scalar unit.
   const int lane = lane_id();
   uint32_t v = c;
+  // (the flip form: each stage starts by comparing lane l with l ^ (k - 1), then half-cleaners
+  // with l ^ j; the lower lane always keeps the minimum, so the lane predicate is one bit of the
+  // lane id -- six wave-constant masks -- instead of two)
 #pragma unroll
   for (int k = 2; k <= 64; k <<= 1) {
 #pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
-      const uint32_t o = (uint32_t)__shfl_xor((int)v, j, 64);
-      const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+      const int x = j == (k >> 1) ? k - 1 : j;
+      const uint32_t o = (uint32_t)__shfl_xor((int)v, x, 64);
+      const bool keep_min = (lane & j) == 0;
       v = keep_min ? min(v, o) : max(v, o);
     }
   }
