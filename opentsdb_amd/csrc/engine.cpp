@@ -3068,6 +3068,10 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       fp.oneb = P.I >= 3600000 && !(oenv && oenv[0] == '0') ? 1 : 0;   // (an hour row's chunk in one bucket)
       fp.wave_lds = (int32_t)(shortk == 3 ? fast_wave_lds(hwin, false, false) : fast_lds_of(q, P));
       fp.win_w = hwin;
+      {
+        const char* e6 = std::getenv("TSDBHIP_SHORT6");
+        fp.short6 = (shortk == 1 && !(e6 && e6[0] == '0')) ? 1 : 0;
+      }
       if (shortk == 1 && fp.sel_direct && fp.sel_cols && K <= 64) {   // k_short's column stage
         fp.sel_stage = fp.wave_lds;
         fp.wave_lds += (int32_t)align16(8 * K * 8);

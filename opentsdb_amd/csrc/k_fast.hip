@@ -37,6 +37,17 @@ static hipError_t launch_fast_k(const GridParams& p, hipStream_t s) {
   }
   if (p.shortk) {
     constexpr int DS = VL == 0 ? SHORT_D0 : (QW * 2 + VL * 2 <= 16) ? SHORT_D : 2;
+    if constexpr (QW == 2 && VL == 0) {
+      if (p.short6) {   // vle rows of <= 384 points: 6 a lane (the kernel hands longer rows back)
+        if (lds > 65536) {
+          hipError_t e = hipFuncSetAttribute((const void*)k_short<F, QW, VL, DS, KR, 6>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+          if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL((k_short<F, QW, VL, DS, KR, 6>), dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p, p.rows,
+                           p.series_row_ptr, p.tile_begin, p.tile_end);
+        return hipGetLastError();
+      }
+    }
     if (lds > 65536) {
       hipError_t e = hipFuncSetAttribute((const void*)k_short<F, QW, VL, DS, KR>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) return e;

@@ -1656,10 +1656,10 @@ __device__ __forceinline__ void f_values_vle(const FastLds& L, const FRaw<QW, VL
   for (int j = 0; j < DPL; j++) xs[j] = (double)f_int16<QW, VL>(b, j);
 }
 
-template <int QW, int VL>
-__device__ __forceinline__ void f_values_vle_i(const FastLds& L, const FRaw<QW, VL>& b, int nvl, int xi[DPL]) {
+template <int QW, int VL, int NP = DPL>
+__device__ __forceinline__ void f_values_vle_i(const FastLds& L, const FRaw<QW, VL>& b, int nvl, int xi[NP]) {
 #pragma unroll
-  for (int j = 0; j < DPL; j++) xi[j] = f_int16<QW, VL>(b, j);
+  for (int j = 0; j < NP; j++) xi[j] = f_int16<QW, VL>(b, j);
 }
 
 struct FGeom {
@@ -1684,34 +1684,34 @@ __device__ __forceinline__ int f_slot(const GridParams& p, const FGeom& m, int n
 }
 
 // Folds one chunk into the series' slot accumulators.
-template <int F, int QW, int VL, bool FULL>
+template <int F, int QW, int VL, bool FULL, int NP = DPL>
 __device__ __forceinline__ void fast_chunk(const GridParams& p, const FastLds& L, const FRaw<QW, VL>& b,
                                            const FGeom& m, int nv0, int K) {
   const int lane = lane_id();
-  const int nvl = FULL ? DPL : max(0, min(DPL, nv0 - lane * DPL));
+  const int nvl = FULL ? NP : max(0, min(NP, nv0 - lane * NP));
   const int uq = (QW == 2 && !p.unit_s) ? 1000 : 1;
-  uint32_t fld[DPL];
+  uint32_t fld[NP];
 #pragma unroll
-  for (int j = 0; j < DPL; j++) fld[j] = f_field<QW, VL>(b, j);
+  for (int j = 0; j < NP; j++) fld[j] = f_field<QW, VL>(b, j);
   // vle integers (1-2 bytes): the in-lane runs are folded in int32 (8 values of |x| < 2^15
   // sum exactly) and converted once per run; squareSum stays in double
   constexpr bool IP = (VL == 0) && (F != F_SQUARESUM);
-  double xs[DPL];
-  int xi[DPL];
+  double xs[NP];
+  int xi[NP];
   if (VL == 0) {
-    f_values_vle_i<QW, VL>(L, b, nvl, xi);
+    f_values_vle_i<QW, VL, NP>(L, b, nvl, xi);
     if (!IP) {
 #pragma unroll
-      for (int j = 0; j < DPL; j++) xs[j] = (double)xi[j];
+      for (int j = 0; j < NP; j++) xs[j] = (double)xi[j];
     }
   } else {
 #pragma unroll
-    for (int j = 0; j < DPL; j++) xs[j] = f_value<QW, VL>(b, j);
+    for (int j = 0; j < NP; j++) xs[j] = f_value<QW, VL>(b, j);
   }
-  uint32_t flast = fld[DPL - 1];
+  uint32_t flast = fld[NP - 1];
   if (!FULL) {
 #pragma unroll
-    for (int j = 0; j < DPL - 1; j++) if (j == nvl - 1) flast = fld[j];
+    for (int j = 0; j < NP - 1; j++) if (j == nvl - 1) flast = fld[j];
   }
   const int n0 = m.r0 + (int)fld[0] * uq;
   const int nl = m.r0 + (int)flast * uq;
@@ -1729,7 +1729,7 @@ __device__ __forceinline__ void fast_chunk(const GridParams& p, const FastLds& L
       constexpr int ID = F == F_MIN ? INT32_MAX : (F == F_MAX ? INT32_MIN : 0);
       int P = ID, sF = 0, mL = ID, cF = 0;
 #pragma unroll
-      for (int j = 0; j < DPL; j++) {
+      for (int j = 0; j < NP; j++) {
         const bool valid = FULL || j < nvl;
         const bool inF = valid && fld[j] < Tf;
         const int x = xi[j];
@@ -1753,7 +1753,7 @@ __device__ __forceinline__ void fast_chunk(const GridParams& p, const FastLds& L
     double P = fast_identity<F>(), sF = 0.0, mL = fast_identity<F>();
     int cF = 0;
 #pragma unroll
-    for (int j = 0; j < DPL; j++) {
+    for (int j = 0; j < NP; j++) {
       const bool valid = FULL || j < nvl;
       const bool inF = valid && fld[j] < Tf;
       double x = xs[j];
@@ -1778,7 +1778,7 @@ __device__ __forceinline__ void fast_chunk(const GridParams& p, const FastLds& L
   } else {
     // some lane spans more than two buckets or the edge of the slot range: per datapoint
 #pragma unroll
-    for (int j = 0; j < DPL; j++) {
+    for (int j = 0; j < NP; j++) {
       if (j < nvl) {
         const int n = m.r0 + (int)fld[j] * uq;
         if (n >= 0) {
@@ -1798,17 +1798,17 @@ __device__ __forceinline__ void fast_chunk(const GridParams& p, const FastLds& L
 // reduction and one fold.  A fold a lane would serialise ~45 LDS atomics on one slot.  Any
 // association is exact here (the series' certificate covers every partial sum), min / max are
 // order-free.  Called by the whole wave; false = not one bucket (nothing folded).
-template <int F, int QW, int VL>
+template <int F, int QW, int VL, int NP = DPL>
 __device__ __forceinline__ bool fast_chunk_oneb(const GridParams& p, const FastLds& L, const FRaw<QW, VL>& b,
                                                 const FGeom& m, int nv0, int K) {
   const int lane = lane_id();
-  const int n = min(nv0, CH);
-  const int nvl = max(0, min(DPL, n - lane * DPL));
+  const int n = min(nv0, 64 * NP);
+  const int nvl = max(0, min(NP, n - lane * NP));
   const int uq = (QW == 2 && !p.unit_s) ? 1000 : 1;
-  const int ll = (n - 1) / DPL, jl = (n - 1) % DPL;   // the chunk's last datapoint: lane, slot
+  const int ll = (n - 1) / NP, jl = (n - 1) % NP;   // the chunk's last datapoint: lane, slot
   uint32_t fl = 0;
 #pragma unroll
-  for (int j = 0; j < DPL; j++) if (j == jl) fl = f_field<QW, VL>(b, j);
+  for (int j = 0; j < NP; j++) if (j == jl) fl = f_field<QW, VL>(b, j);
   const int n0 = m.r0 + (int)__builtin_amdgcn_readfirstlane((int)f_field<QW, VL>(b, 0)) * uq;
   const int nl = m.r0 + (int)__builtin_amdgcn_readlane((int)fl, ll) * uq;
   if (n0 < 0) return false;
@@ -1821,7 +1821,7 @@ __device__ __forceinline__ bool fast_chunk_oneb(const GridParams& p, const FastL
     constexpr int ID = F == F_MIN ? INT32_MAX : (F == F_MAX ? INT32_MIN : 0);
     int P = ID;
 #pragma unroll
-    for (int j = 0; j < DPL; j++) {
+    for (int j = 0; j < NP; j++) {
       const int x = j < nvl ? f_int16<QW, VL>(b, j) : ID;
       P = F == F_MIN ? min(P, x) : (F == F_MAX ? max(P, x) : P + x);
     }
@@ -1831,7 +1831,7 @@ __device__ __forceinline__ bool fast_chunk_oneb(const GridParams& p, const FastL
     const double ID = fast_identity<F>();
     double P = ID;
 #pragma unroll
-    for (int j = 0; j < DPL; j++) {
+    for (int j = 0; j < NP; j++) {
       double x = VL == 0 ? (double)f_int16<QW, VL>(b, j) : f_value<QW, VL>(b, j);
       if (F == F_SQUARESUM) x = x * x;
       if (j >= nvl) x = ID;
@@ -1847,17 +1847,17 @@ __device__ __forceinline__ bool fast_chunk_oneb(const GridParams& p, const FastL
 
 // A chunk of a row shorter than CH: when every lane is either full or empty (a row of a
 // multiple of 8 datapoints, e.g. 360), the full-lane code runs on the non-empty lanes.
-template <int F, int QW, int VL>
+template <int F, int QW, int VL, int NP = DPL>
 __device__ __forceinline__ void fast_chunk_any(const GridParams& p, const FastLds& L, const FRaw<QW, VL>& b,
                                                const FGeom& m, int nv0, int K) {
 #ifndef TSDBHIP_NO_ONEB
-  if (p.oneb && fast_chunk_oneb<F, QW, VL>(p, L, b, m, nv0, K)) return;
+  if (p.oneb && fast_chunk_oneb<F, QW, VL, NP>(p, L, b, m, nv0, K)) return;
 #endif
-  const int nvl = max(0, min(DPL, nv0 - lane_id() * DPL));
-  if (__all(nvl == 0 || nvl == DPL)) {
-    if (nvl) fast_chunk<F, QW, VL, true>(p, L, b, m, nv0, K);
+  const int nvl = max(0, min(NP, nv0 - lane_id() * NP));
+  if (__all(nvl == 0 || nvl == NP)) {
+    if (nvl) fast_chunk<F, QW, VL, true, NP>(p, L, b, m, nv0, K);
   } else {
-    fast_chunk<F, QW, VL, false>(p, L, b, m, nv0, K);
+    fast_chunk<F, QW, VL, false, NP>(p, L, b, m, nv0, K);
   }
 }
 
@@ -2114,6 +2114,24 @@ __device__ __forceinline__ void short_issue(const GridParams& p, uint64_t qoff, 
   }
 }
 
+// NP = 6 (vle class, rows of <= 384 datapoints): 6 datapoints a lane, 12 bytes of qualifiers and
+// 12 of int16 values (dwordx3 loads at lane * 12), so a 360-point row keeps 60 lanes busy, not 45
+template <int QW, int VL, int NP>
+__device__ __forceinline__ void short_issue_np(const GridParams& p, uint64_t qoff, uint64_t voff, int ndp,
+                                               FRaw<QW, VL>& b) {
+  if constexpr (NP == DPL) {
+    short_issue<QW, VL>(p, qoff, voff, ndp, b);
+  } else {
+    static_assert(NP == 6 && QW == 2 && VL == 0, "6 a lane: the 2-byte-qualifier vle class");
+    const int lane = lane_id();
+    const int64_t i0 = (lane * NP < ndp) ? (int64_t)lane * NP : 0;
+    const uint3 q = *reinterpret_cast<const uint3*>(p.qual + qoff + i0 * 2);
+    const uint3 v = *reinterpret_cast<const uint3*>(p.val2 + qoff + i0 * 2);
+    b.q[0] = make_uint4(q.x, q.y, q.z, 0u);
+    b.v[0] = make_uint4(v.x, v.y, v.z, 0u);
+  }
+}
+
 __device__ __forceinline__ uint64_t rl64(uint64_t x, int l) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
@@ -2133,7 +2151,7 @@ __device__ __forceinline__ uint64_t rl64(uint64_t x, int l) {
 #endif
 #define SHORT_OCC2(VL) ((VL) == 0 ? SHORT_OCC2_VLE : 4)
 // KR as k_fast.  The profiling switches of TSDBHIP_DBG exist only in a -DTSDBHIP_KDBG build.
-template <int F, int QW, int VL, int D, int KR>
+template <int F, int QW, int VL, int D, int KR, int NP = DPL>
 __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) void k_short(GridParams p, const RowDesc* __restrict__ rows,
                                                const int64_t* __restrict__ srp, const int64_t* __restrict__ tbeg,
                                                const int64_t* __restrict__ tend) {
@@ -2164,7 +2182,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     dlsb = x.lsb;
     damax = (uint64_t)__double_as_longlong(x.absmax);
     const uint32_t fl = x.flags;
-    ok = (int64_t)x.base >= p.ss && (int64_t)x.base < p.se && dndp >= 1 && dndp <= CH &&
+    ok = (int64_t)x.base >= p.ss && (int64_t)x.base < p.se && dndp >= 1 && dndp <= 64 * NP &&
          fast_row_ok<QW, VL>(fl, F == F_MIN || F == F_MAX, F == F_SUM || F == F_AVG);
   }
   if (!__all(ok)) {
@@ -2203,7 +2221,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
 #pragma unroll
   for (int i = 0; i < D; i++) {
     const int jn = min(i, nlast);
-    short_issue<QW, VL>(p, rl64(dq, jn), rl64(dv, jn), __builtin_amdgcn_readlane(dndp, jn), buf[i]);
+    short_issue_np<QW, VL, NP>(p, rl64(dq, jn), rl64(dv, jn), __builtin_amdgcn_readlane(dndp, jn), buf[i]);
   }
   bool redo = false;
   auto series = [&](const FRaw<QW, VL>& b, int j) {
@@ -2211,13 +2229,13 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     const FGeom g = {__builtin_amdgcn_readlane(gq0, j), __builtin_amdgcn_readlane(gr0, j)};
 #ifdef TSDBHIP_KDBG
     if (!(p.dbg & 2)) {   // TSDBHIP_DBG profiling switches (results invalid when set)
-      fast_chunk_any<F, QW, VL>(p, L, b, g, nv0, K);
+      fast_chunk_any<F, QW, VL, NP>(p, L, b, g, nv0, K);
     } else if (p.dbg & 8) {
       uint32_t x = b.q[0].x ^ b.v[0].x;
       if (x == 0x12345678u) L.cnt[0] = x;
     }
 #else
-    fast_chunk_any<F, QW, VL>(p, L, b, g, nv0, K);
+    fast_chunk_any<F, QW, VL, NP>(p, L, b, g, nv0, K);
 #endif
     return nv0;
   };
@@ -2243,7 +2261,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     for (int i = 0; i < D; i++) {
       const int nv0 = series(buf[i], j + i);
       const int jn = min(j + i + D, nlast);
-      short_issue<QW, VL>(p, rl64(dq, jn), rl64(dv, jn), __builtin_amdgcn_readlane(dndp, jn), buf[i]);
+      short_issue_np<QW, VL, NP>(p, rl64(dq, jn), rl64(dv, jn), __builtin_amdgcn_readlane(dndp, jn), buf[i]);
       series_end(j + i, nv0);
     }
     if (redo) break;
