@@ -13,6 +13,9 @@
 #ifndef SHORT_D
 #define SHORT_D 2      // k_short ring depth, 4-byte float class
 #endif
+#ifndef SHORT6_VL4
+#define SHORT6_VL4 0   // 4: the float32 class takes 6 a lane too (measured no faster: profiles/r04ab)
+#endif
 #ifndef ROWS_D
 #define ROWS_D 2       // k_rows ring depth (a power of two: 64 rows per descriptor batch)
 #endif
@@ -37,8 +40,8 @@ static hipError_t launch_fast_k(const GridParams& p, hipStream_t s) {
   }
   if (p.shortk) {
     constexpr int DS = VL == 0 ? SHORT_D0 : (QW * 2 + VL * 2 <= 16) ? SHORT_D : 2;
-    if constexpr (QW == 2 && VL == 0) {
-      if (p.short6) {   // vle rows of <= 384 points: 6 a lane (the kernel hands longer rows back)
+    if constexpr (QW == 2 && (VL == 0 || VL == SHORT6_VL4)) {
+      if (p.short6) {   // rows of <= 384 points: 6 a lane (the kernel hands longer rows back)
         if (lds > 65536) {
           hipError_t e = hipFuncSetAttribute((const void*)k_short<F, QW, VL, DS, KR, 6>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
           if (e != hipSuccess) return e;

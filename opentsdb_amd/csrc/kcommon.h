@@ -2122,13 +2122,20 @@ __device__ __forceinline__ void short_issue_np(const GridParams& p, uint64_t qof
   if constexpr (NP == DPL) {
     short_issue<QW, VL>(p, qoff, voff, ndp, b);
   } else {
-    static_assert(NP == 6 && QW == 2 && VL == 0, "6 a lane: the 2-byte-qualifier vle class");
+    static_assert(NP == 6 && QW == 2 && (VL == 0 || VL == 4), "6 a lane: 2-byte qualifiers, vle or 4-byte values");
     const int lane = lane_id();
     const int64_t i0 = (lane * NP < ndp) ? (int64_t)lane * NP : 0;
     const uint3 q = *reinterpret_cast<const uint3*>(p.qual + qoff + i0 * 2);
-    const uint3 v = *reinterpret_cast<const uint3*>(p.val2 + qoff + i0 * 2);
     b.q[0] = make_uint4(q.x, q.y, q.z, 0u);
-    b.v[0] = make_uint4(v.x, v.y, v.z, 0u);
+    if constexpr (VL == 0) {
+      const uint3 v = *reinterpret_cast<const uint3*>(p.val2 + qoff + i0 * 2);
+      b.v[0] = make_uint4(v.x, v.y, v.z, 0u);
+    } else {   // 24 bytes of float32 values at lane * 24 (16-byte and 8-byte loads)
+      const uint8_t* vp = p.val + voff + i0 * 4;
+      b.v[0] = *reinterpret_cast<const uint4*>(vp);
+      const uint2 t = *reinterpret_cast<const uint2*>(vp + 16);
+      b.v[1] = make_uint4(t.x, t.y, 0u, 0u);
+    }
   }
 }
 
