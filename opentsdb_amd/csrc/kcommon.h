@@ -2320,7 +2320,7 @@ struct RowBatch {
   int lsb;
 };
 
-template <int F, int QW, int VL>
+template <int F, int QW, int VL, int NP = DPL>
 __device__ __forceinline__ void rows_batch(const GridParams& p, const RowDesc* __restrict__ rows, int64_t r0,
                                            int nr, int b, RowBatch& B) {
   const int jr = b * 64 + lane_id();
@@ -2333,11 +2333,11 @@ __device__ __forceinline__ void rows_batch(const GridParams& p, const RowDesc* _
   const int n = (int)x.ndp;
   const uint32_t fl = x.flags;   // (no short-circuit: a lane-conditional load waits for all loads)
   const bool in = (jr < nr) & ((int64_t)x.base >= p.ss) & ((int64_t)x.base < p.se);
-  const bool ok = (n <= CH) & fast_row_ok<QW, VL>(fl, F == F_MIN || F == F_MAX, F == F_SUM || F == F_AVG);
+  const bool ok = (n <= 64 * NP) & fast_row_ok<QW, VL>(fl, F == F_MIN || F == F_MAX, F == F_SUM || F == F_AVG);
   B.ndp = !in ? 0 : (ok ? n : -1);
 }
 
-template <int F, int QW, int VL, int D, int KR>
+template <int F, int QW, int VL, int D, int KR, int NP = DPL>
 __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) void k_rows(GridParams p, const RowDesc* __restrict__ rows,
                                               const int64_t* __restrict__ srp, const int64_t* __restrict__ tbeg,
                                               const int64_t* __restrict__ tend) {
@@ -2367,8 +2367,8 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
   int send = lane < ns ? (int)(srp[s0 + lane + 1] - r0) : INT32_MAX;
   asm volatile("" : "+v"(send));   // kept in its register (not re-loaded from srp at every series end)
   RowBatch cur, nxt;
-  rows_batch<F, QW, VL>(p, rows, r0, nr, 0, cur);
-  rows_batch<F, QW, VL>(p, rows, r0, nr, min(1, nb - 1), nxt);
+  rows_batch<F, QW, VL, NP>(p, rows, r0, nr, 0, cur);
+  rows_batch<F, QW, VL, NP>(p, rows, r0, nr, min(1, nb - 1), nxt);
   const bool dense0 = KR == 0 && p.dense_out != nullptr;
   const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0 && !dense0, !dense0);
   for (int k = lane; k < K; k += 64) {
@@ -2386,7 +2386,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
   // first fold in the loop wait for every load)
 #pragma unroll
   for (int i = 0; i < D; i++) {
-    short_issue<QW, VL>(p, rl64(cur.qoff, i), rl64(cur.voff, i), max(0, __builtin_amdgcn_readlane(cur.ndp, i)), buf[i]);
+    short_issue_np<QW, VL, NP>(p, rl64(cur.qoff, i), rl64(cur.voff, i), max(0, __builtin_amdgcn_readlane(cur.ndp, i)), buf[i]);
     __builtin_amdgcn_sched_barrier(0);
   }
   bool redo = false, have = false, any = false;
@@ -2404,7 +2404,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
       if (jr < nr && nd < 0) redo = true;
       if (jr < nr && nd > 0) {
         const FGeom g = fgeom(p, (uint32_t)__builtin_amdgcn_readlane((int)cur.base, jl));
-        fast_chunk_any<F, QW, VL>(p, L, buf[i], g, nd, K);
+        fast_chunk_any<F, QW, VL, NP>(p, L, buf[i], g, nd, K);
         have = true;
         lsb = min(lsb, __builtin_amdgcn_readlane(cur.lsb, jl));
         amax = fmax(amax, __longlong_as_double((long long)rl64(cur.amax, jl)));
@@ -2414,7 +2414,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
       const uint64_t iq = jn < 64 ? rl64(cur.qoff, jn) : rl64(nxt.qoff, jn - 64);
       const uint64_t iv = jn < 64 ? rl64(cur.voff, jn) : rl64(nxt.voff, jn - 64);
       const int in = jn < 64 ? __builtin_amdgcn_readlane(cur.ndp, jn) : __builtin_amdgcn_readlane(nxt.ndp, jn - 64);
-      short_issue<QW, VL>(p, iq, iv, max(0, in), buf[i]);
+      short_issue_np<QW, VL, NP>(p, iq, iv, max(0, in), buf[i]);
       if (jr < nr && !redo && __ballot(send == jr + 1) != 0) {   // the last row of its series
         if (have) {
           const int64_t s = s0 + __popcll(__ballot(send <= jr));
@@ -2431,7 +2431,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     }
     if (((j + D) & 63) == 0) {
       cur = nxt;
-      rows_batch<F, QW, VL>(p, rows, r0, nr, min(((j + D) >> 6) + 1, nb - 1), nxt);
+      rows_batch<F, QW, VL, NP>(p, rows, r0, nr, min(((j + D) >> 6) + 1, nb - 1), nxt);
     }
   }
   if (redo) {
@@ -2465,7 +2465,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
 // bucket store and no group-by pass over it (the dense split).  LERP needs neighbours across
 // windows, so a series with a bucket missing inside its data span hands the tile back (the
 // general kernel takes it); regular data never does.
-template <int F, int QW, int VL, int D>
+template <int F, int QW, int VL, int D, int NP = DPL>
 __global__ __launch_bounds__(256, SHORT_OCC(VL)) void k_hwin(GridParams p, const RowDesc* __restrict__ rows,
                                                              const int64_t* __restrict__ srp, const int64_t* __restrict__ tbeg,
                                                              const int64_t* __restrict__ tend) {
@@ -2523,7 +2523,7 @@ __global__ __launch_bounds__(256, SHORT_OCC(VL)) void k_hwin(GridParams p, const
         dlsb = x.lsb;
         damax = (uint64_t)__double_as_longlong(x.absmax);
         gr0 = g.r0;
-        bad = !(dndp >= 1 && dndp <= CH &&
+        bad = !(dndp >= 1 && dndp <= 64 * NP &&
                 fast_row_ok<QW, VL>(x.flags, F == F_MIN || F == F_MAX, F == F_SUM || F == F_AVG));
       }
       break;
@@ -2543,7 +2543,7 @@ __global__ __launch_bounds__(256, SHORT_OCC(VL)) void k_hwin(GridParams p, const
       if (rest) rest &= rest - 1;
       lanes_[i] = ln;
       const int l2 = ln < 0 ? 0 : ln;
-      short_issue<QW, VL>(p, rl64(dq, l2), rl64(dv, l2), ln < 0 ? 0 : __builtin_amdgcn_readlane(dndp, l2), buf[i]);
+      short_issue_np<QW, VL, NP>(p, rl64(dq, l2), rl64(dv, l2), ln < 0 ? 0 : __builtin_amdgcn_readlane(dndp, l2), buf[i]);
     }
     const int nact = __popcll(act);
     for (int j = 0; j < nact && !redo; j += D) {
@@ -2554,15 +2554,15 @@ __global__ __launch_bounds__(256, SHORT_OCC(VL)) void k_hwin(GridParams p, const
           const int nv0 = __builtin_amdgcn_readlane(dndp, ln);
           const FGeom g = {0, __builtin_amdgcn_readlane(gr0, ln)};   // window-relative: the row starts at slot 0
           // the row's last datapoint inside the window (a second qualifier can reach 4095 s)
-          const int ll = (nv0 - 1) >> 3, jl = (nv0 - 1) & 7;
+          const int ll = (nv0 - 1) / NP, jl = (nv0 - 1) % NP;
           uint32_t fl = 0;
 #pragma unroll
-          for (int jj = 0; jj < DPL; jj++) if (jj == jl) fl = f_field<QW, VL>(buf[i], jj);
+          for (int jj = 0; jj < NP; jj++) if (jj == jl) fl = f_field<QW, VL>(buf[i], jj);
           const int uq = (QW == 2 && !p.unit_s) ? 1000 : 1;
           const int64_t lastn = (int64_t)g.r0 + (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)fl, ll) * uq;
           if (lastn >= (int64_t)W * p.In) redo = true;
           if (!redo) {
-            fast_chunk_any<F, QW, VL>(p, L, buf[i], g, nv0, Wh);
+            fast_chunk_any<F, QW, VL, NP>(p, L, buf[i], g, nv0, Wh);
             WAVE_SYNC();
             // every bucket of the window present, or fill: the window's emit needs no neighbour
             // from another window
@@ -2579,7 +2579,7 @@ __global__ __launch_bounds__(256, SHORT_OCC(VL)) void k_hwin(GridParams p, const
         if (rest) rest &= rest - 1;
         lanes_[i] = ln2;
         const int l2 = ln2 < 0 ? 0 : ln2;
-        short_issue<QW, VL>(p, rl64(dq, l2), rl64(dv, l2), ln2 < 0 ? 0 : __builtin_amdgcn_readlane(dndp, l2), buf[i]);
+        short_issue_np<QW, VL, NP>(p, rl64(dq, l2), rl64(dv, l2), ln2 < 0 ? 0 : __builtin_amdgcn_readlane(dndp, l2), buf[i]);
       }
     }
     if (redo) break;
