@@ -87,7 +87,8 @@ __device__ __forceinline__ bool walk_append(const uint8_t* v, int64_t vl, F&& f)
 // *vb: bounds of the compacted bytes it can contribute (a data column keeps its qualifier width
 // and value bytes; an append column's qualifiers and values both come out of its value)
 __device__ __forceinline__ bool cmp_col(const CmpParams& p, int64_t c, int64_t row, int64_t* qb = nullptr,
-                                        int64_t* vb = nullptr, int64_t* nout = nullptr) {
+                                        int64_t* vb = nullptr, int64_t* nout = nullptr, bool store = true,
+                                        uint32_t* info_out = nullptr) {
   const uint64_t qo = p.col_qo[c], vo = p.col_vo[c];
   const int64_t ql = (int64_t)(p.col_qo[c + 1] - qo), vl = (int64_t)(p.col_vo[c + 1] - vo);
   const uint8_t* q = p.q + qo;
@@ -136,8 +137,11 @@ __device__ __forceinline__ bool cmp_col(const CmpParams& p, int64_t c, int64_t r
     cmp_fail(p.row_err, row, err);
     n = 0;
   }
-  p.col_n[c] = n;
-  p.col_info[c] = kind | info;
+  if (store) {
+    p.col_n[c] = n;
+    p.col_info[c] = kind | info;
+  }
+  if (info_out) *info_out = kind | info;
   if (nout) *nout = n;
   if (qb) {
     *qb = n == 0 ? 0 : (kind == CMP_APPEND ? vl : ql);
@@ -938,7 +942,8 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_rowone(CmpParams p, int
   if (p.row_err[r] || p.row_heap[r] == 0) { no_cell(); return; }
   if (p.row_heap[r] == 1) {
     const int64_t c = p.row_one[r];
-    const uint32_t info = p.col_info[c];
+    uint32_t info = 0;
+    cmp_col(p, c, r, nullptr, nullptr, nullptr, false, &info);
     const int64_t ql = (int64_t)(p.col_qo[c + 1] - p.col_qo[c]);
     if ((info & 3) == CMP_DATA && !(info & 8) && (ql == 2 || (ql == 4 && cmp_in_ms(p.q[p.col_qo[c]])))) {
       const int64_t vl = (int64_t)(p.col_vo[c + 1] - p.col_vo[c]);   // noMergesOrFixups: as stored
@@ -964,9 +969,13 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_rowone(CmpParams p, int
   for (int64_t cr = c0; cr < c1; cr += CMP_ROW_THREADS * CPT) {
     const int64_t cb = cr + (int64_t)t * CPT;
     int ncs[CPT], sum = 0;
+    uint32_t infos[CPT];
 #pragma unroll
     for (int j = 0; j < CPT; j++) {
-      ncs[j] = cb + j < c1 ? (int)p.col_n[cb + j] : 0;
+      int64_t nn = 0;
+      infos[j] = 0;
+      if (cb + j < c1) cmp_col(p, cb + j, r, nullptr, nullptr, &nn, false, &infos[j]);
+      ncs[j] = (int)nn;
       sum += ncs[j];
     }
     int tot;
@@ -978,7 +987,7 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_rowone(CmpParams p, int
       const int64_t c = cb + j;
       const uint64_t qo = p.col_qo[c], vo = p.col_vo[c];
       const int64_t ql = (int64_t)(p.col_qo[c + 1] - qo), vl = (int64_t)(p.col_vo[c + 1] - vo);
-      const uint32_t info = p.col_info[c];
+      const uint32_t info = infos[j];
       const bool app = (info & 3) == CMP_APPEND;
       const bool fix = !app && ql == 2 && (info & 8);
       const uint32_t qbase = (uint32_t)((app ? vo - vb : qo - qb));
@@ -1207,7 +1216,9 @@ __global__ __launch_bounds__(256) void k_cmp_cols_rowwave(CmpParams p) {
   int64_t top = -1;
   for (int64_t c = c0 + lane; c < c1; c += 64) {
     int64_t qb = 0, vb = 0, nc = 0;
-    if (cmp_col(p, c, r, &qb, &vb, &nc)) { heap++; top = c; }
+    // (no per-column arrays: k_cmp_rowone recomputes a column's count and kind from its bytes,
+    // cheaper than writing and re-reading 12 bytes a column)
+    if (cmp_col(p, c, r, &qb, &vb, &nc, false)) { heap++; top = c; }
     n += nc;
     qs += qb;
     vs += vb;
