@@ -1538,11 +1538,11 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   // device copies of one chunk of the scan and per-column / per-row scratch (freed at the end)
   DevBuf d_rcp, d_cqo, d_cvo, d_cts, d_q, d_v, d_crow, d_cn, d_coff, d_cinfo, d_rheap, d_rone, d_rerr;
   DevBuf d_key, d_key2, d_idx, d_idx2, d_ecol, d_eqo, d_evo, d_klen, d_sq, d_sv, d_sc, d_sm;
-  DevBuf d_rlo, d_rq, d_rv, d_rstate, d_rmeta, d_rdq, d_rdv, d_raw, d_bad, d_rmax, d_klist;
+  DevBuf d_rlo, d_rq, d_rv, d_rstate, d_rmeta, d_rdq, d_rdv, d_raw, d_bad, d_rmax, d_klist, d_cq32, d_cv32;
   auto release_all = [&]() {
     for (DevBuf* b : {&d_rcp, &d_cqo, &d_cvo, &d_cts, &d_q, &d_v, &d_crow, &d_cn, &d_coff, &d_cinfo, &d_rheap, &d_rone,
                       &d_rerr, &d_key, &d_key2, &d_idx, &d_idx2, &d_ecol, &d_eqo, &d_evo, &d_klen, &d_sq, &d_sv,
-                      &d_sc, &d_sm, &d_rlo, &d_rq, &d_rv, &d_rstate, &d_rmeta, &d_rdq, &d_rdv, &d_raw, &d_bad, &d_rmax, &d_klist})
+                      &d_sc, &d_sm, &d_rlo, &d_rq, &d_rv, &d_rstate, &d_rmeta, &d_rdq, &d_rdv, &d_raw, &d_bad, &d_rmax, &d_klist, &d_cq32, &d_cv32})
       b->release();
   };
   struct Rel { std::function<void()> f; ~Rel() { f(); } } rel{release_all};
@@ -1738,11 +1738,20 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
       HIP_OK(hipMemcpyAsync(d_raw.p, cb->row_col_ptr, (nr + 1) * 8, hipMemcpyHostToDevice, st));
       HIP_OK(cmp_rebase(d_raw.as<uint64_t>(), d_rcp.as<uint64_t>(), nr + 1, 0, d_bad.as<int32_t>(), st));
     }
+    // 32-bit copies of the column offsets when the blobs are under 4 GB (written by the same
+    // checking pass; the one-pass kernels read 4 bytes an offset instead of 8)
+    const bool w32 = nc && qz < ((uint64_t)1 << 32) && vz < ((uint64_t)1 << 32);
+    if (w32) {
+      HIP_OK(d_cq32.ensure((c1c + 1) * 4));
+      HIP_OK(d_cv32.ensure((c1c + 1) * 4));
+    }
     if (nc) {
       HIP_OK(hipMemcpyAsync(d_raw.p, cb->col_qual_off, (nc + 1) * 8, hipMemcpyHostToDevice, st));
-      HIP_OK(cmp_rebase(d_raw.as<uint64_t>(), d_cqo.as<uint64_t>(), nc + 1, 0, d_bad.as<int32_t>(), st));
+      HIP_OK(cmp_rebase(d_raw.as<uint64_t>(), d_cqo.as<uint64_t>(), nc + 1, 0, d_bad.as<int32_t>(), st,
+                        w32 ? d_cq32.as<uint32_t>() : nullptr));
       HIP_OK(hipMemcpyAsync(d_raw.p, cb->col_val_off, (nc + 1) * 8, hipMemcpyHostToDevice, st));
-      HIP_OK(cmp_rebase(d_raw.as<uint64_t>(), d_cvo.as<uint64_t>(), nc + 1, 0, d_bad.as<int32_t>(), st));
+      HIP_OK(cmp_rebase(d_raw.as<uint64_t>(), d_cvo.as<uint64_t>(), nc + 1, 0, d_bad.as<int32_t>(), st,
+                        w32 ? d_cv32.as<uint32_t>() : nullptr));
       if (qz) HIP_OK(hipMemcpyAsync(d_q.p, cb->qual, qz, hipMemcpyHostToDevice, st));
       if (vz) HIP_OK(hipMemcpyAsync(d_v.p, cb->val, vz, hipMemcpyHostToDevice, st));
       if (cb->col_timestamp) HIP_OK(hipMemcpyAsync(d_cts.p, cb->col_timestamp, nc * 8, hipMemcpyHostToDevice, st));
@@ -1767,6 +1776,8 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     p.row_col_ptr = d_rcp.as<int64_t>();
     p.col_qo = d_cqo.as<uint64_t>();
     p.col_vo = d_cvo.as<uint64_t>();
+    p.col_qo32 = w32 ? d_cq32.as<uint32_t>() : nullptr;
+    p.col_vo32 = w32 ? d_cv32.as<uint32_t>() : nullptr;
     p.col_ts = cb->col_timestamp ? d_cts.as<int64_t>() : nullptr;
     p.q = d_q.as<uint8_t>();
     p.v = d_v.as<uint8_t>();
@@ -1795,6 +1806,7 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     (void)hipEventElapsedTime(&t_cols, c->ev[0], c->ev[2]);
     if (!cap) {
       p.row_n = p.row_qb = p.row_vb = nullptr;
+      p.col_qo32 = p.col_vo32 = nullptr;
       return 1;
     }
     std::vector<int64_t> qbv(r1c, 0), vbv(r1c, 0);

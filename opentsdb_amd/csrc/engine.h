@@ -357,6 +357,8 @@ struct CmpParams {
   const int64_t* row_col_ptr;   // [n_rows + 1]
   const uint64_t* col_qo;       // [n_cols + 1] qualifier bytes of each column
   const uint64_t* col_vo;       // [n_cols + 1] value bytes
+  const uint32_t* col_qo32;     // the same in 32 bits (one-pass path, blobs under 4 GB), else null
+  const uint32_t* col_vo32;
   const int64_t* col_ts;        // [n_cols] KeyValue timestamps, or null (all equal)
   const uint8_t* q;
   const uint8_t* v;
@@ -419,7 +421,8 @@ hipError_t cmp_cols_rows(const CmpParams& p, hipStream_t s);
 int cmp_onepass_cap(const CmpParams& p, uint32_t* scratch3, hipStream_t s, hipError_t* err);
 hipError_t cmp_rows_onepass(const CmpParams& p, int cap, hipStream_t s);
 // dst = src - base over n offsets (a chunk of the scan, rebased); *bad |= 1 unless non-decreasing and >= base
-hipError_t cmp_rebase(const uint64_t* src, uint64_t* dst, int64_t n, uint64_t base, int32_t* bad, hipStream_t s);
+hipError_t cmp_rebase(const uint64_t* src, uint64_t* dst, int64_t n, uint64_t base, int32_t* bad, hipStream_t s,
+                      uint32_t* dst32 = nullptr);   // dst32: also a 32-bit copy (the one-pass path)
 
 // rollup read path: value series buckets <- Σsum / Σcount (avg) or Σcount, from the SUM
 // downsampling of each value series and of its count series (cmap[s], -1: none)

@@ -83,14 +83,27 @@ __device__ __forceinline__ bool walk_append(const uint8_t* v, int64_t vl, F&& f)
   return true;
 }
 
+// column offsets: 64-bit, or (W32, the one-pass path when a chunk's blobs are under 4 GB) 32-bit
+template <bool W32>
+__device__ __forceinline__ uint64_t col_q(const CmpParams& p, int64_t c) {
+  if constexpr (W32) return (uint64_t)p.col_qo32[c];
+  else return p.col_qo[c];
+}
+template <bool W32>
+__device__ __forceinline__ uint64_t col_v(const CmpParams& p, int64_t c) {
+  if constexpr (W32) return (uint64_t)p.col_vo32[c];
+  else return p.col_vo[c];
+}
+
 // One column: kind, fixups, datapoint count, errors.  Returns whether it joins the heap.  *qb /
 // *vb: bounds of the compacted bytes it can contribute (a data column keeps its qualifier width
 // and value bytes; an append column's qualifiers and values both come out of its value)
+template <bool W32 = false>
 __device__ __forceinline__ bool cmp_col(const CmpParams& p, int64_t c, int64_t row, int64_t* qb = nullptr,
                                         int64_t* vb = nullptr, int64_t* nout = nullptr, bool store = true,
                                         uint32_t* info_out = nullptr) {
-  const uint64_t qo = p.col_qo[c], vo = p.col_vo[c];
-  const int64_t ql = (int64_t)(p.col_qo[c + 1] - qo), vl = (int64_t)(p.col_vo[c + 1] - vo);
+  const uint64_t qo = col_q<W32>(p, c), vo = col_v<W32>(p, c);
+  const int64_t ql = (int64_t)(col_q<W32>(p, c + 1) - qo), vl = (int64_t)(col_v<W32>(p, c + 1) - vo);
   const uint8_t* q = p.q + qo;
   const uint8_t* v = p.v + vo;
   uint32_t kind = CMP_IGNORE, info = 0;
@@ -420,16 +433,18 @@ hipError_t cmp_entries(CmpParams& p, void** tmp, size_t* tmp_bytes, int end_bit,
 
 // dst[i] = src[i] - base over n values; bad |= 1 when the values decrease or start below base
 __global__ __launch_bounds__(256) void k_cmp_rebase(const uint64_t* src, uint64_t* dst, int64_t n, uint64_t base,
-                                                    int32_t* bad) {
+                                                    int32_t* bad, uint32_t* dst32) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t v = src[i];
   if (v < base || (i + 1 < n && src[i + 1] < v)) atomicOr(bad, 1);
   dst[i] = v - base;
+  if (dst32) dst32[i] = (uint32_t)(v - base);   // (the caller checked the chunk's bytes fit 32 bits)
 }
 
-hipError_t cmp_rebase(const uint64_t* src, uint64_t* dst, int64_t n, uint64_t base, int32_t* bad, hipStream_t s) {
-  if (n > 0) hipLaunchKernelGGL(k_cmp_rebase, dim3(blocks_of(n)), dim3(256), 0, s, src, dst, n, base, bad);
+hipError_t cmp_rebase(const uint64_t* src, uint64_t* dst, int64_t n, uint64_t base, int32_t* bad, hipStream_t s,
+                      uint32_t* dst32) {
+  if (n > 0) hipLaunchKernelGGL(k_cmp_rebase, dim3(blocks_of(n)), dim3(256), 0, s, src, dst, n, base, bad, dst32);
   return hipGetLastError();
 }
 
@@ -924,6 +939,7 @@ __device__ __forceinline__ void cmp_copy_to_aligned(uint8_t* dst, const uint8_t*
   for (int64_t b = (nw << 2) + t; b < n; b += nt) dst[b] = src[b];
 }
 
+template <bool W32>
 __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_rowone(CmpParams p, int P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   uint64_t* key = reinterpret_cast<uint64_t*>(sm);
@@ -943,23 +959,23 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_rowone(CmpParams p, int
   if (p.row_heap[r] == 1) {
     const int64_t c = p.row_one[r];
     uint32_t info = 0;
-    cmp_col(p, c, r, nullptr, nullptr, nullptr, false, &info);
-    const int64_t ql = (int64_t)(p.col_qo[c + 1] - p.col_qo[c]);
-    if ((info & 3) == CMP_DATA && !(info & 8) && (ql == 2 || (ql == 4 && cmp_in_ms(p.q[p.col_qo[c]])))) {
-      const int64_t vl = (int64_t)(p.col_vo[c + 1] - p.col_vo[c]);   // noMergesOrFixups: as stored
+    cmp_col<W32>(p, c, r, nullptr, nullptr, nullptr, false, &info);
+    const int64_t ql = (int64_t)(col_q<W32>(p, c + 1) - col_q<W32>(p, c));
+    if ((info & 3) == CMP_DATA && !(info & 8) && (ql == 2 || (ql == 4 && cmp_in_ms(p.q[col_q<W32>(p, c)])))) {
+      const int64_t vl = (int64_t)(col_v<W32>(p, c + 1) - col_v<W32>(p, c));   // noMergesOrFixups: as stored
       if (ql > p.row_qb[r] || vl > p.row_vb[r]) {
         if (t == 0) cmp_fail(p.row_err, r, TSDB_E_ILLEGAL_STATE);
         no_cell();
         return;
       }
-      cmp_copy_to_aligned(p.out_q + p.row_dq[r], p.q + p.col_qo[c], ql, t, CMP_ROW_THREADS);
-      cmp_copy_to_aligned(p.out_v + p.row_dv[r], p.v + p.col_vo[c], vl, t, CMP_ROW_THREADS);
+      cmp_copy_to_aligned(p.out_q + p.row_dq[r], p.q + col_q<W32>(p, c), ql, t, CMP_ROW_THREADS);
+      cmp_copy_to_aligned(p.out_v + p.row_dv[r], p.v + col_v<W32>(p, c), vl, t, CMP_ROW_THREADS);
       if (t == 0) { p.row_state[r] = 2; p.row_q[r] = ql; p.row_v[r] = vl; p.row_meta[r] = 0; p.row_lo[r] = 0; }
       return;
     }
   }
   const int64_t c0 = p.row_col_ptr[r], c1 = p.row_col_ptr[r + 1];
-  const uint64_t qb = p.col_qo[c0], vb = p.col_vo[c0];
+  const uint64_t qb = col_q<W32>(p, c0), vb = col_v<W32>(p, c0);
   const uint8_t* qrow = p.q + qb;
   const uint8_t* vrow = p.v + vb;
   // explode, 4096 columns a round (4 consecutive a thread, in scan order): the entry offsets of a
@@ -974,7 +990,7 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_rowone(CmpParams p, int
     for (int j = 0; j < CPT; j++) {
       int64_t nn = 0;
       infos[j] = 0;
-      if (cb + j < c1) cmp_col(p, cb + j, r, nullptr, nullptr, &nn, false, &infos[j]);
+      if (cb + j < c1) cmp_col<W32>(p, cb + j, r, nullptr, nullptr, &nn, false, &infos[j]);
       ncs[j] = (int)nn;
       sum += ncs[j];
     }
@@ -985,8 +1001,8 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_rowone(CmpParams p, int
     for (int j = 0; j < CPT; j++) {
       if (ncs[j] == 0) continue;
       const int64_t c = cb + j;
-      const uint64_t qo = p.col_qo[c], vo = p.col_vo[c];
-      const int64_t ql = (int64_t)(p.col_qo[c + 1] - qo), vl = (int64_t)(p.col_vo[c + 1] - vo);
+      const uint64_t qo = col_q<W32>(p, c), vo = col_v<W32>(p, c);
+      const int64_t ql = (int64_t)(col_q<W32>(p, c + 1) - qo), vl = (int64_t)(col_v<W32>(p, c + 1) - vo);
       const uint32_t info = infos[j];
       const bool app = (info & 3) == CMP_APPEND;
       const bool fix = !app && ql == 2 && (info & 8);
@@ -1207,6 +1223,7 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_rowone(CmpParams p, int
 // (coalesced), the row's heap count / datapoints / byte bounds reduced in the wave and stored
 // once -- no per-column row index, no atomics (k_cmp_cols' per-row atomics from every wave of a
 // 3600-column row serialised in L2: 1.1 ms for 72M columns against 0.78 without the sums).
+template <bool W32>
 __global__ __launch_bounds__(256) void k_cmp_cols_rowwave(CmpParams p) {
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= p.n_rows) return;
@@ -1218,7 +1235,7 @@ __global__ __launch_bounds__(256) void k_cmp_cols_rowwave(CmpParams p) {
     int64_t qb = 0, vb = 0, nc = 0;
     // (no per-column arrays: k_cmp_rowone recomputes a column's count and kind from its bytes,
     // cheaper than writing and re-reading 12 bytes a column)
-    if (cmp_col(p, c, r, &qb, &vb, &nc, false)) { heap++; top = c; }
+    if (cmp_col<W32>(p, c, r, &qb, &vb, &nc, false)) { heap++; top = c; }
     n += nc;
     qs += qb;
     vs += vb;
@@ -1239,9 +1256,13 @@ __global__ __launch_bounds__(256) void k_cmp_cols_rowwave(CmpParams p) {
 }
 
 hipError_t cmp_cols_rows(const CmpParams& p, hipStream_t s) {
-  if (p.n_rows > 0) hipLaunchKernelGGL(k_cmp_cols_rowwave, dim3((unsigned)((p.n_rows + 3) / 4)), dim3(256), 0, s, p);
+  if (p.n_rows > 0) {
+    if (p.col_qo32) hipLaunchKernelGGL(k_cmp_cols_rowwave<true>, dim3((unsigned)((p.n_rows + 3) / 4)), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(k_cmp_cols_rowwave<false>, dim3((unsigned)((p.n_rows + 3) / 4)), dim3(256), 0, s, p);
+  }
   return hipGetLastError();
 }
+
 
 int cmp_onepass_cap(const CmpParams& p, uint32_t* scratch3, hipStream_t s, hipError_t* err) {
   *err = hipSuccess;
@@ -1261,11 +1282,13 @@ hipError_t cmp_rows_onepass(const CmpParams& p, int cap, hipStream_t s) {
   if (p.n_rows <= 0) return hipSuccess;
   // the sort's arrays (20 B an entry); the cell assembled in the same space needs <= 12 B an entry
   const size_t lds = (size_t)cap * 20;
+  const void* kf = p.col_qo32 ? (const void*)k_cmp_rowone<true> : (const void*)k_cmp_rowone<false>;
   if (lds > 65536) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k_cmp_rowone, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const hipError_t e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_cmp_rowone, dim3((unsigned)p.n_rows), dim3(CMP_ROW_THREADS), lds, s, p, cap);
+  if (p.col_qo32) hipLaunchKernelGGL(k_cmp_rowone<true>, dim3((unsigned)p.n_rows), dim3(CMP_ROW_THREADS), lds, s, p, cap);
+  else hipLaunchKernelGGL(k_cmp_rowone<false>, dim3((unsigned)p.n_rows), dim3(CMP_ROW_THREADS), lds, s, p, cap);
   return hipGetLastError();
 }
 
