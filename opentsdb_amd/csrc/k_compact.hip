@@ -978,6 +978,113 @@ __global__ __launch_bounds__(CMP_ROW_THREADS) void k_cmp_rowone(CmpParams p, int
   const uint64_t qb = col_q<W32>(p, c0), vb = col_v<W32>(p, c0);
   const uint8_t* qrow = p.q + qb;
   const uint8_t* vrow = p.v + vb;
+  // Fast path: every column one datapoint with a 2-byte (second) qualifier, no two on one
+  // second -- an hour row of single-datapoint cells.  Each column goes straight to its second (a
+  // 4096-bit map and a second -> column map at the top of the LDS); one dual block scan over the
+  // map gives the output positions; the cell is assembled as below.  No entry arrays, sort or
+  // dedup.  Anything else (a compacted column, an append, ms qualifiers, a second hit twice)
+  // falls through to the general path.
+  if (P >= 2048 && c1 - c0 <= 4096) {
+    __shared__ int fp_fail;
+    uint16_t* scol = reinterpret_cast<uint16_t*>(sm + (size_t)P * 20 - 12800);   // [4096] column - c0, 0xFFFF none
+    uint8_t* sinf = reinterpret_cast<uint8_t*>(scol + 4096);                      // [4096] fix | vstart | evl - 1
+    if (t == 0) fp_fail = 0;
+    for (int i = t; i < 2048; i += CMP_ROW_THREADS) reinterpret_cast<uint32_t*>(scol)[i] = 0xFFFFFFFFu;
+    __syncthreads();
+    // (no atomics: every column stores its index at its second, then checks it is still there --
+    // a second two columns hit keeps one of them, and the other one sees it)
+    uint32_t mysec[4];
+    int nmine = 0;
+    for (int64_t c = c0 + t; c < c1; c += CMP_ROW_THREADS) {
+      int64_t nn = 0;
+      uint32_t info = 0;
+      cmp_col<W32>(p, c, r, nullptr, nullptr, &nn, false, &info);
+      const int64_t ql = (int64_t)(col_q<W32>(p, c + 1) - col_q<W32>(p, c));
+      if ((info & 3) != CMP_DATA || ql != 2 || nn != 1) { fp_fail = 1; continue; }
+      const uint8_t* q = p.q + col_q<W32>(p, c);
+      const uint32_t sec = (((uint32_t)q[0] << 8) | q[1]) >> 4;
+      scol[sec] = (uint16_t)(c - c0);
+      const uint32_t evl1 = (info >> 8) & 7;   // (the fixed flags byte's length)
+      sinf[sec] = (uint8_t)(evl1 | ((info & 4) ? 8u : 0u) | ((info & 8) ? 16u : 0u));
+      if (nmine < 4) mysec[nmine] = sec | ((uint32_t)(c - c0) << 12);
+      nmine++;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (j < nmine && scol[mysec[j] & 4095] != (uint16_t)(mysec[j] >> 12)) fp_fail = 1;   // a second hit twice
+    __syncthreads();
+    if (!fp_fail) {
+      uint32_t bits = 0;   // seconds 4t .. 4t + 3 present
+#pragma unroll
+      for (int j = 0; j < 4; j++) bits |= (scol[4 * t + j] != 0xFFFFu ? 1u : 0u) << j;
+      int sv = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if ((bits >> j) & 1u) sv += (sinf[4 * t + j] & 7) + 1;
+      const int kc = __popc(bits);
+      int tcn, tvb, ovb;
+      const int ocn = block_excl_scan2(kc, sv, scan_sh, &tcn, &ovb, &tvb);
+      const int tq = 2 * tcn, nv = tvb + (tcn > 1 ? 1 : 0);
+      if (tq > p.row_qb[r] || tvb > p.row_vb[r]) {
+        if (t == 0) cmp_fail(p.row_err, r, TSDB_E_ILLEGAL_STATE);
+        no_cell();
+        return;
+      }
+      uint8_t* oq = sm;
+      uint8_t* ov = sm + ((tq + 15) & ~15);
+      int q_at = 2 * ocn, v_at = ovb;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if ((bits >> j) & 1u) {
+          const uint32_t sec = 4u * (uint32_t)t + (uint32_t)j;
+          const int64_t c = c0 + scol[sec];
+          const uint32_t f = sinf[sec];
+          const int evl = (int)(f & 7) + 1;
+          const uint8_t* qs = p.q + col_q<W32>(p, c);
+          const uint8_t* vs = p.v + col_v<W32>(p, c) + ((f & 8) ? 4 : 0);
+          if (!(((uintptr_t)qs | (uintptr_t)(oq + q_at)) & 1)) {
+            uint32_t w = *reinterpret_cast<const uint16_t*>(qs);
+            if (f & 16) w = (w & 0x00FFu) | ((((w >> 8) & 0xF8u) | (uint32_t)(evl - 1)) << 8);   // checkForFixup's flags
+            *reinterpret_cast<uint16_t*>(oq + q_at) = (uint16_t)w;
+          } else {
+            oq[q_at] = qs[0];
+            oq[q_at + 1] = (f & 16) ? (uint8_t)((qs[1] & 0xF8) | (evl - 1)) : qs[1];
+          }
+          if ((evl == 8 || evl == 4) && !(((uintptr_t)vs | (uintptr_t)(ov + v_at)) & 3)) {
+            *reinterpret_cast<uint32_t*>(ov + v_at) = *reinterpret_cast<const uint32_t*>(vs);
+            if (evl == 8) *reinterpret_cast<uint32_t*>(ov + v_at + 4) = *reinterpret_cast<const uint32_t*>(vs + 4);
+          } else {
+            for (int b2 = 0; b2 < evl; b2++) ov[v_at + b2] = vs[b2];
+          }
+          q_at += 2;
+          v_at += evl;
+        }
+      }
+      const int nqd = (tq + 3) >> 2, nvd = (nv + 3) >> 2;
+      if (kc > 0 && ocn + kc == tcn) {   // the last datapoint's thread: meta byte (seconds only: 0), padding
+        if (tcn > 1) ov[nv - 1] = 0;
+        for (int b2 = tq; b2 < nqd * 4; b2++) oq[b2] = 0;
+        for (int b2 = nv; b2 < nvd * 4; b2++) ov[b2] = 0;
+      }
+      __syncthreads();
+      const uint32_t* oqw = reinterpret_cast<const uint32_t*>(oq);
+      const uint32_t* ovw = reinterpret_cast<const uint32_t*>(ov);
+      uint32_t* dqw = reinterpret_cast<uint32_t*>(p.out_q + p.row_dq[r]);
+      uint32_t* dvw = reinterpret_cast<uint32_t*>(p.out_v + p.row_dv[r]);
+      for (int w = t; w < nqd; w += CMP_ROW_THREADS) dqw[w] = oqw[w];
+      for (int w = t; w < nvd; w += CMP_ROW_THREADS) dvw[w] = ovw[w];
+      if (t == 0) {
+        p.row_state[r] = tcn ? 1 : 0;
+        p.row_q[r] = tcn ? tq : 0;
+        p.row_v[r] = tcn ? nv : 0;
+        p.row_meta[r] = 0;
+        p.row_lo[r] = tcn;
+      }
+      return;
+    }
+    __syncthreads();   // (the general path below reuses the LDS)
+  }
   // explode, 4096 columns a round (4 consecutive a thread, in scan order): the entry offsets of a
   // round from one block scan of the threads' counts
   constexpr int CPT = 4;
