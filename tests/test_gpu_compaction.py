@@ -446,3 +446,47 @@ def test_decreasing_column_offsets_rejected(eng, chunk):
         assert ei.value.code == abi.TSDB_E_ILLEGAL_ARGUMENT
     finally:
         os.environ.pop("TSDBHIP_CMP_CHUNK", None)
+
+
+def _single_second_rows(rng, n_rows, dup_row=None, fix_rows=()):
+    """Rows of one-datapoint second cells in shuffled order (the one-pass kernel's fast path):
+    mixed value kinds; in fix_rows some floats stored as 8 bytes with a 4-byte flag (the
+    checkForFixup cases); in dup_row two cells on one second (the general path's dedup)."""
+    rows = []
+    for r in range(n_rows):
+        n = int(rng.integers(1200, 3600))
+        secs = np.sort(rng.choice(3600, size=n, replace=False))
+        cells = []
+        for k, s_ in enumerate(secs):
+            kind = ["long", "int", "float", "double"][int(rng.integers(0, 4))]
+            val = float(rng.normal(0, 100)) if kind in ("float", "double") else int(rng.integers(-1000, 1000))
+            q, v = _cell(int(s_) * 1000, False, val, kind)
+            if r in fix_rows and kind == "float" and k % 3 == 0:
+                v = b"\x00\x00\x00\x00" + v          # 8 value bytes under a 4-byte float flag
+                q = struct.pack(">H", (int(s_) << 4) | 0xB)
+            if r in fix_rows and kind == "long" and k % 5 == 0:
+                q = struct.pack(">H", (int(s_) << 4) | 0x3)   # flags say 4 bytes, 8 stored: fixed to 8
+            cells.append((q, v))
+        if r == dup_row:
+            cells.append(cells[len(cells) // 2])     # a second cell on one second (same bytes)
+        order = rng.permutation(len(cells))
+        rows.append((B + 3600 * r, [(cells[j][0], cells[j][1], int(t)) for t, j in enumerate(order)]))
+    return rows
+
+
+@pytest.mark.parametrize("fix", [True, False])
+def test_single_cell_fast_path(eng, fix):
+    """k_cmp_rowone's fast path (each column at its second) against the global-sort pipeline and
+    the oracle's compaction, with fixups and a row whose duplicate second sends it to the general
+    path."""
+    rng = np.random.default_rng(31)
+    rows = _single_second_rows(rng, 6, dup_row=2, fix_rows=(1, 4))
+    cb = abi.HostCellBatch.from_rows([rows], [0], fix)
+    want = _load_with_env(eng, cb, TSDBHIP_CMP_ROWS=0)
+    got = _load_with_env(eng, cb)
+    two = _load_with_env(eng, cb, TSDBHIP_CMP_ONEPASS=0)
+    assert rows_of(got) == rows_of(want)
+    assert rows_of(two) == rows_of(want)
+    for (base, cells), (gb, gq, gv) in zip(rows, rows_of(got)):
+        exp = O.compact_row([(q, v) for q, v, _ in cells], fix, [t for _, _, t in cells])
+        assert (gb, gq, gv) == (base, exp[0], exp[1])
