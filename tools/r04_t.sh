@@ -2,7 +2,7 @@
 # compaction one-pass (word-wide cell assembly, 32-bit row sums) + A/B of the one-bucket fold code
 # on configs 2 / 3 (libtsdbhip vs a build without it)
 set -o pipefail
-out=gpurun_out/r04aj; mkdir -p $out
+out=gpurun_out/r04ak; mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_compaction.py -x -q --timeout 300 --timeout-method thread > $out/pytest.log 2>&1
 rc=$?; tail -3 $out/pytest.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $out/pytest.log | head -30; exit $rc; }
