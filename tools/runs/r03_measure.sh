@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-3 measurement pass on one MI355X: the bench line, configs 3/4/5, the f-row benches and a
-# kernel trace of the bench.   usage: tools/r03_measure.sh <tag>   (outputs under gpurun_out/<tag>/)
+# kernel trace of the bench.   usage: tools/runs/r03_measure.sh <tag>   (outputs under gpurun_out/<tag>/)
 set -o pipefail
 tag=${1:-r03m}; out=gpurun_out/$tag; mkdir -p $out
 export TMPDIR=/tmp

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-3 PMC passes (each counter group its own run, kernel trace only): config 4's raw union
 # kernels, config 3's percentile group-by selection, the windowed histogram accumulation.
-# usage: tools/r03_pmc.sh <tag>   (outputs under gpurun_out/pmc_<tag>_*/, summaries printed)
+# usage: tools/runs/r03_pmc.sh <tag>   (outputs under gpurun_out/pmc_<tag>_*/, summaries printed)
 set -o pipefail
 tag=${1:-r03}
 export TMPDIR=/tmp
