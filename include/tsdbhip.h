@@ -607,8 +607,9 @@ int tsdbhip_expr_zip(tsdbhip_ctx* ctx, const int32_t* program, int n_ops, const 
  * distinct timestamps of the series marked active (NULL: every series; IntersectionIterator nulls the
  * series it kicks out, :306-349), those in [start_ms, end_ms] are emitted: one output group per
  * joined set, one double per step.  The join itself (flattenTags keys, ByteMap order) is host logic
- * (opentsdb_amd/expression.py).  Active series must be in strictly increasing time order (else
- * TSDB_E_NOT_IMPLEMENTED: the reference's step walk over repeated timestamps is not restated). */
+ * (opentsdb_amd/expression.py).  A series may repeat a timestamp: the step walk then steps it as
+ * often as the series holding most copies of it, the j-th step reading each series' j-th copy (or
+ * its fill).  A series out of time order (a decreasing timestamp) -> TSDB_E_NOT_IMPLEMENTED. */
 int tsdbhip_expr_sync(tsdbhip_ctx* ctx, const int32_t* program, int n_ops, const double* consts, int n_vars,
                       int64_t n_sets, const int32_t* set_series, const double* var_fill, double absent_value,
                       const uint8_t* active, int64_t start_ms, int64_t end_ms, const tsdbhip_series_set* in,

@@ -267,18 +267,40 @@ extern "C" int tsdbhip_expr_sync(tsdbhip_ctx* c, const int32_t* program, int n_o
   const int64_t S = in->n_series, N = in->ptr[S];
   for (int64_t i = 0; i < n_sets * n_vars; i++)
     if (set_series[i] >= S) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "set series out of range");
-  // per point: does its series drive the steps; the active series must be in time order
+  // per point: does its series drive the steps, and its rank among the series' points at the
+  // same timestamp.  Series may repeat a timestamp (non-decreasing); a decreasing one is refused.
+  // The step walk over repeats (TimeSyncedIterator.next(long) :125-144 consumes one point per
+  // series and step, nextTimestamp :147-158 the smallest current one): timestamp t is stepped
+  // R_t times, R_t = the most copies of t any active series holds; at its j-th step a series
+  // reads its j-th copy of t, else its fill.
   std::vector<uint8_t> pact(N > 0 ? N : 1, 0);
+  std::vector<int32_t> prank;
+  int64_t rep = 1, tmin = INT64_MAX, tmax = INT64_MIN;
   for (int64_t s = 0; s < S; s++) {
     const int64_t a = in->ptr[s], b = in->ptr[s + 1];
     if (b < a) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "malformed series set");
     const uint8_t act = active ? active[s] : 1;
+    int64_t run = 0;
     for (int64_t q = a; q < b; q++) {
       pact[q] = act;
-      if (q > a && in->ts_ms[q] <= in->ts_ms[q - 1])
+      const int64_t t = in->ts_ms[q];
+      if (q > a && t < in->ts_ms[q - 1])
         return set_error(TSDB_E_NOT_IMPLEMENTED, "time-synchronised expression over a series out of time order");
+      run = (q > a && t == in->ts_ms[q - 1]) ? run + 1 : 0;
+      if (run) {
+        if (prank.empty()) prank.assign(N, 0);
+        prank[q] = (int32_t)std::min<int64_t>(run, INT32_MAX);
+      }
+      if (act && t >= start_ms && t <= end_ms) {
+        rep = std::max(rep, run + 1);
+        tmin = std::min(tmin, t);
+        tmax = std::max(tmax, t);
+      }
     }
   }
+  // repeats: step key (t - tmin) * rep + rank, below the INT64_MAX sentinel
+  if (rep > 1 && ((uint64_t)tmax - (uint64_t)tmin) > (uint64_t)((INT64_MAX - rep) / rep))
+    return set_error(TSDB_E_NOT_IMPLEMENTED, "repeated timestamps over a time range too wide for the step keys");
   std::lock_guard<std::mutex> lk(ctx_mutex(c));
   if (hipSetDevice(ctx_device(c)) != hipSuccess) return set_error(TSDB_E_HIP, "hipSetDevice");
   hipStream_t st = ctx_stream(c);
@@ -298,6 +320,11 @@ extern "C" int tsdbhip_expr_sync(tsdbhip_ctx* c, const int32_t* program, int n_o
   XOK(sc.alloc(&d_sorted, N * 8));
   XOK(sc.alloc(&d_uni, N * 8));
   XOK(sc.alloc(&d_nu, 8));
+  void* d_rank = nullptr;
+  if (rep > 1) {
+    XOK(sc.alloc(&d_rank, N * 4));
+    XOK(hipMemcpyAsync(d_rank, prank.data(), N * 4, hipMemcpyHostToDevice, st));
+  }
   XOK(hipMemcpyAsync(d_prog, program, n_ops * 8, hipMemcpyHostToDevice, st));
   if (n_consts) XOK(hipMemcpyAsync(d_consts, consts, n_consts * 8, hipMemcpyHostToDevice, st));
   if (n_sets) XOK(hipMemcpyAsync(d_sets, set_series, n_sets * n_vars * 4, hipMemcpyHostToDevice, st));
@@ -326,8 +353,12 @@ extern "C" int tsdbhip_expr_sync(tsdbhip_ctx* c, const int32_t* program, int n_o
   p.pt_active = (const uint8_t*)d_act;
   p.start = start_ms;
   p.end = end_ms;
+  p.rank = (const int32_t*)d_rank;
+  p.rep = rep;
+  p.base = rep > 1 ? tmin : 0;
   // the steps: the join iterator's nextTimestamp sequence = the distinct timestamps of the
-  // active series (each in time order), sorted and made unique on the device
+  // active series (each in time order; with repeats the distinct (timestamp, rank) keys), sorted
+  // and made unique on the device
   int64_t U = 0;
   if (N) {
     XOK(expr_sync_keys(p, (int64_t*)d_keys, st));

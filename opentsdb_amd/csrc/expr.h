@@ -63,7 +63,9 @@ struct ExprSyncParams {
   int64_t n_pts;
   const uint8_t* pt_active;  // [n_pts] the point's series drives the steps
   int64_t start, end;
-  const int64_t* uts;        // [U] step timestamps
+  const int32_t* rank;       // [n_pts] copies of the point's timestamp before it in its series (rep > 1)
+  int64_t rep, base;         // rep > 1: step key = (ts - base) * rep + rank; rep == 1: key = ts
+  const int64_t* uts;        // [U] step keys
   int64_t U;
   int64_t* out_ts;           // [n_sets * U]
   uint64_t* out_bits;

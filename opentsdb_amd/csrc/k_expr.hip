@@ -196,17 +196,21 @@ __global__ void k_expr_sync_keys(ExprSyncParams p, int64_t* keys) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.n_pts) return;
   const int64_t t = p.ts[i];
-  keys[i] = (p.pt_active[i] && t >= p.start && t <= p.end) ? t : INT64_MAX;
+  const bool in = p.pt_active[i] && t >= p.start && t <= p.end;
+  keys[i] = !in ? INT64_MAX : p.rep == 1 ? t : (t - p.base) * p.rep + p.rank[i];
 }
 
 // thread per (joined set, step): every variable's value at the step's timestamp -- its series'
-// point there (binary search: the series are in time order), else the variable's fill; then the
+// point there (binary search: the series are in time order; the step's copy of a repeated
+// timestamp), else the variable's fill; then the
 // program (ExpressionIterator.next(long), :323-358)
 __global__ void k_expr_sync(ExprSyncParams p) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= p.n_sets * p.U) return;
   const int64_t j = t / p.U, u = t - j * p.U;
-  const int64_t x = p.uts[u];
+  const int64_t key = p.uts[u];
+  const int64_t x = p.rep == 1 ? key : p.base + key / p.rep;   // the step's timestamp
+  const int64_t c = p.rep == 1 ? 0 : key % p.rep;              // and copy of it
   const double r = expr_eval(p.prog, p.n_ops, p.consts, [&](int v) {
     const int32_t s = p.set_series[j * p.n_vars + v];
     double y = p.absent;
@@ -216,6 +220,7 @@ __global__ void k_expr_sync(ExprSyncParams p) {
         const int64_t m = (lo + hi) >> 1;
         if (p.ts[m] < x) lo = m + 1; else hi = m;
       }
+      lo += c;
       y = (lo < p.ptr[s + 1] && p.ts[lo] == x) ? pt_double(p.bits[lo], p.is_int[lo]) : p.var_fill[v];
     }
     return y != y ? p.var_fill[v] : y;

@@ -218,3 +218,76 @@ def test_large_join_on_the_device(eng):
         t, vals = want[k]
         for j in range(0, len(vals), 53):
             assert bit_equal(out[j].values()[k], vals[j])
+
+
+def with_repeats(rng, subs, p_dup=0.25, max_extra=3):
+    """Copies of random points (the same timestamp, a new value) in every series: the step walk
+    over repeated timestamps (TimeSyncedIterator.next(long) :125-144 takes one point per step)."""
+    out = []
+    for ser in subs:
+        ns = []
+        for s in ser:
+            pts = []
+            for t, v in s["points"]:
+                pts.append((t, v))
+                if rng.random() < p_dup:
+                    for _ in range(int(rng.integers(1, max_extra + 1))):
+                        pts.append((t, int(rng.integers(-50, 50)) if isinstance(v, int) else float(rng.normal(0, 9))))
+            ns.append({**s, "points": pts})
+        out.append(ns)
+    return out
+
+
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("op", ["UNION", "INTERSECTION"])
+def test_repeated_timestamps_vs_oracle(eng, seed, op):
+    """Series repeating timestamps: each timestamp is stepped as often as the series with the most
+    copies holds it, the j-th step reading every series' j-th copy or its fill -- against the
+    oracle's literal step walk, bit for bit, with and without a query range."""
+    rng = np.random.default_rng(100 + seed)
+    subs = with_repeats(rng, rand_store(rng, 3, 10, 30))
+    for ex in ["v0 + v1 * v2", "(v0 - v1) / v2", "v0 > v1"]:
+        fills = [[0.0, math.nan, 1.5][int(rng.integers(0, 3))] for _ in subs]
+        for start, end in [(0, 1 << 62), (1431561600000 + 5 * 60000, 1431561600000 + 21 * 60000)]:
+            pe, oe = build_both(subs, ex, op, False, True, fills)
+            try:
+                oe.compile()
+                want = OI.serialize(oe, start, end)
+            except OI.JavaError as e:
+                with pytest.raises(X.ExpressionError) as ei:
+                    pe.compile(eng, start, end)
+                assert ei.value.java == e.java
+                continue
+            out = pe.compile(eng, start, end)
+            ctx = f"{seed} {op} {ex} [{start}, {end}]"
+            assert [int(t) for t in pe.steps] == [r[0] for r in want], ctx
+            assert len(set(r[0] for r in want)) < len(want) or not want, ctx   # repeats were stepped
+            for k, (t, vals) in enumerate(want):
+                for j, w in enumerate(vals):
+                    assert bit_equal(out[j].values()[k], w), (ctx, k, j, out[j].values()[k], w)
+
+
+def test_repeated_timestamps_nested(eng):
+    """A nested expression's output repeats the steps its inputs repeat; the outer one walks them."""
+    rng = np.random.default_rng(21)
+    subs = with_repeats(rng, rand_store(rng, 2, 6, 20, gaps=0.0, nan=0.0))
+    pe, oe = build_both(subs, "v0 * v1 + 1", "UNION", False, False, [0.0, 0.0])
+    outer_p = X.ExpressionIterator("o", "x / 2 - x", "UNION", False, False)
+    outer_p.add_results("x", pe)
+    outer_o = OI.ExpressionIterator("o", "x / 2 - x", "UNION", False, False)
+    outer_o.add_results("x", oe)
+    outer_o.compile()
+    want = OI.serialize(outer_o, 0, 1 << 62)
+    out = outer_p.compile(eng)
+    assert [int(t) for t in outer_p.steps] == [r[0] for r in want]
+    for k, (t, vals) in enumerate(want):
+        for j, w in enumerate(vals):
+            assert bit_equal(out[j].values()[k], w)
+
+
+def test_decreasing_timestamps_refused(eng):
+    from opentsdb_amd.engine import EngineError
+    subs = [[{"points": [(2000, 1.0), (1000, 2.0)], "tags": {"D": "A"}, "agg": []}]]
+    pe, _ = build_both(subs, "v0 + 1", "UNION", False, False, [0.0])
+    with pytest.raises(EngineError, match="out of time order"):
+        pe.compile(eng)
