@@ -23,7 +23,6 @@ hipStream_t ctx_stream(tsdbhip_ctx* c);
 int ctx_device(tsdbhip_ctx* c);
 std::mutex& ctx_mutex(tsdbhip_ctx* c);
 void*& ctx_hist(tsdbhip_ctx* c);
-bool ctx_is_md(tsdbhip_ctx* c);
 int set_error(int code, const std::string& msg);
 bool cal_prev_tz(const tsdbhip_tz* z, int64_t ts, int64_t n, int unit, int64_t* out);
 int64_t cal_step_tz(const tsdbhip_tz* z, int64_t t, int unit, int64_t n);
@@ -161,10 +160,10 @@ void hist_release(void* h) {
 
 using namespace tsdb;
 
+// On a multi-device context (tsdbhip_init_devices) the histogram store is resident on its first
+// device: the context is itself an engine context on devices[0] (multi.cpp), whose store, stream
+// and lock serve the histogram entry points; the numeric batch stays sharded over the devices.
 extern "C" int tsdbhip_load_histograms(tsdbhip_ctx* c, const tsdbhip_hist_batch* hb) {
-  if (ctx_is_md(c))
-    return set_error(TSDB_E_NOT_IMPLEMENTED, "the histogram path on a multi-device context (tsdbhip_init_devices): it is "
-                                             "bound to one device's resident store");
   if (!c || !hb) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(ctx_mutex(c));
   HOK(hipSetDevice(ctx_device(c)));
@@ -698,9 +697,6 @@ int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end,
 
 extern "C" int tsdbhip_hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int n_pct, const float* pct, int show_buckets,
                                 tsdbhip_hist_result** out) {
-  if (ctx_is_md(c))
-    return set_error(TSDB_E_NOT_IMPLEMENTED, "the histogram path on a multi-device context (tsdbhip_init_devices): it is "
-                                             "bound to one device's resident store");
   int64_t ss, se;
   const int rc = q ? tsdbhip_scan_bounds(q, &ss, &se) : TSDB_E_ILLEGAL_ARGUMENT;
   if (rc) return rc == TSDB_E_ILLEGAL_ARGUMENT && !q ? set_error(rc, "null query") : rc;
@@ -711,9 +707,6 @@ extern "C" int tsdbhip_hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int n_pc
 
 extern "C" int tsdbhip_hist_run_range(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start_ms, int64_t end_ms,
                                       int n_pct, const float* pct, int show_buckets, tsdbhip_hist_result** out) {
-  if (ctx_is_md(c))
-    return set_error(TSDB_E_NOT_IMPLEMENTED, "the histogram path on a multi-device context (tsdbhip_init_devices): it is "
-                                             "bound to one device's resident store");
   return hist_run(c, q, start_ms, end_ms, 0, (int64_t)UINT32_MAX + 1, n_pct, pct, show_buckets, out);
 }
 

@@ -277,3 +277,25 @@ def test_gpu_calendar_downsampling(eng, dst_store, tz, spec):
         q.ds_function, q.ds_interval_ms, q.ds_all, q.ds_calendar, q.ds_fill = (d.ds_function, d.ds_interval_ms,
                                                                                d.ds_all, d.ds_calendar, d.ds_fill)
         run_both(eng, dst_store, q, [50.0, 99.0], agg == "sum")
+
+
+def test_gpu_multi_device_context_runs_histograms(eng):
+    """A multi-device context (tsdbhip_init_devices; the one-GPU box repeats device 0) serves the
+    histogram path from its first device: the same answers as one device and the oracle, for
+    golden and random stores, beside a numeric batch sharded over its devices."""
+    md = Engine(devices=[0, 0])
+    try:
+        for gq in G["queries"][:6]:
+            hb = U.store_batch(G["stores"][gq["store"]])
+            md.load_histograms(hb)
+            q = U.golden_query(gq)
+            got = md.run_histogram(q, gq["percentiles"], gq["show_buckets"], gq["span_range"])
+            U.check_golden(got, gq)
+        rng = np.random.default_rng(31)
+        hb = U.random_store(rng, n_series=20, n_rows=2, period_ms=10000, groups=4, layouts=3)
+        for agg, ds in [("sum", "1m-sum"), ("none", None), ("p99", "5m-sum")]:
+            q = U.query(T0, T0 + 2 * 3600, agg, ds)
+            got = run_both(md, hb, q, PCTS, True)
+            U.same(got, run_both(eng, hb, q, PCTS, True))
+    finally:
+        md.close()
