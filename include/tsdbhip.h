@@ -342,9 +342,10 @@ int tsdbhip_assemble(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_
  * device copies when a device repeats (several shards on one GPU); TSDB_MD_RCCL / TSDB_MD_COPY
  * force one.
  * Entry points bound to one device's resident store (load_shard, synth_shard, load_cells,
- * load_rollup, the histogram path, batch downloads, the partials / sel exchange, rollup
- * generation, debug_rows) return TSDB_E_NOT_IMPLEMENTED on such a context; the expression
- * functions run on devices[0].  tsdbhip_last_timing: per-device stage times are the maximum over
+ * batch downloads, the partials / sel exchange, rollup generation, debug_rows) return
+ * TSDB_E_NOT_IMPLEMENTED on such a context; tsdbhip_load_rollup shards a rollup batch; the
+ * histogram path (its store resident on devices[0], unsharded) and the expression functions
+ * run on devices[0].  tsdbhip_last_timing: per-device stage times are the maximum over
  * the devices, counters are summed, total_ms is the host wall time of the call and exchange_ms
  * its gather + merge part. */
 enum { TSDB_SHARD_AUTO = -1 };
