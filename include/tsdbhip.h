@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define TSDBHIP_ABI_VERSION 10
+#define TSDBHIP_ABI_VERSION 11
 
 /* ---- error codes: one per Java exception on the path --------------------- */
 enum {
@@ -336,6 +336,11 @@ int tsdbhip_assemble(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_
  *                      devices[0]; raw group-by queries (no downsampler) run every whole group
  *                      locally and each straddling group on its owner over a copy of all its
  *                      spans (built once per load), so results are bit-identical to one GPU.
+ *                      VERIFICATION STATUS: the exchange has been tested over one GPU repeated
+ *                      as 2-8 devices (peer copies) and a one-rank RCCL communicator only; the
+ *                      rank-to-rank moves between DISTINCT GPUs (RCCL send / recv, peer copies
+ *                      over xGMI) are unverified on hardware until tests/test_gpu_multidev.py::
+ *                      test_distinct_devices has run on a multi-GPU node.
  * TSDB_SHARD_AUTO (default) picks GROUPS when the group-aligned split is within 10% of the byte
  * balance, else SERIES; tsdbhip_md_shard_mode sets the mode of the following loads.
  * transport: TSDB_MD_AUTO = RCCL (ncclCommInitAll) when two or more devices are all distinct,
@@ -457,7 +462,17 @@ int tsdbhip_load_rollup(tsdbhip_ctx* ctx, const tsdbhip_rollup_batch* rb);
  * scan range covers the row.  Scans of more than 2^31 columns or datapoints are compacted in
  * chunks of whole rows.  NOT_IMPLEMENTED: a row of more than 2^31 columns or datapoints, more
  * than 2^31 rows; per row, lazily: a compacted cell out of time order, a datapoint column with an empty
- * value. */
+ * value.
+ * use_otsdb_timestamp (Config.java:621, default false) switches the merge to dtcsMergeDataPoints
+ * (CompactionQueue.java:500-547): at a repeated offset the datapoint with the greatest value
+ * (use_max_value, Config.java:622, default true) or the smallest (false), by
+ * ColumnDatapointIterator.getCellValueAsDouble, is kept -- the first in heap order (newest column
+ * first) on a tie, the heap's head when its value is NaN -- with no duplicate exception; a merged
+ * row holding a value that getCellValueAsDouble cannot read (a float of 1, 2, 3, 5, 6 or 7 bytes,
+ * an integer of 3, 5, 6 or 7) raises TSDB_E_RUNTIME (BufferUnderflowException); the meta byte
+ * follows the reference's isMilliseconds() read after the kept column advanced.  The HBase scan
+ * time range that flag also sets (TsdbQuery.java:1401-1409) is the caller's scan.  Such batches
+ * run the global-sort compaction path. */
 typedef struct {
   int64_t n_series;
   const int64_t* series_row_ptr;   /* [n_series + 1] */
@@ -472,6 +487,8 @@ typedef struct {
   const uint8_t* val;
   const int32_t* group_id;         /* [n_series] */
   int32_t fix_duplicates;          /* tsd.storage.fix_duplicates */
+  int32_t use_otsdb_timestamp;     /* tsd.storage.use_otsdb_timestamp: dtcsMergeDataPoints */
+  int32_t use_max_value;           /* tsd.storage.use_max_value (with use_otsdb_timestamp) */
 } tsdbhip_cell_batch;
 int tsdbhip_load_cells(tsdbhip_ctx* ctx, const tsdbhip_cell_batch* cb);
 

@@ -280,6 +280,8 @@ class CellBatch(C.Structure):
         ("val", C.POINTER(C.c_uint8)),
         ("group_id", C.POINTER(C.c_int32)),
         ("fix_duplicates", C.c_int32),
+        ("use_otsdb_timestamp", C.c_int32),
+        ("use_max_value", C.c_int32),
     ]
 
 
@@ -287,7 +289,7 @@ class HostCellBatch:
     """Owns the arrays behind a :class:`CellBatch`."""
 
     def __init__(self, series_row_ptr, row_base_time, row_col_ptr, col_qual_off, col_val_off, qual, val, group_id,
-                 col_timestamp=None, fix_duplicates=False):
+                 col_timestamp=None, fix_duplicates=False, use_otsdb_timestamp=False, use_max_value=True):
         self.series_row_ptr = np.ascontiguousarray(series_row_ptr, dtype=np.int64)
         self.row_base_time = np.ascontiguousarray(row_base_time, dtype=np.uint32)
         self.row_col_ptr = np.ascontiguousarray(row_col_ptr, dtype=np.int64)
@@ -308,10 +310,10 @@ class HostCellBatch:
                            _ptr(self.col_val_off, C.c_uint64),
                            C.POINTER(C.c_int64)() if self.col_timestamp is None else _ptr(self.col_timestamp, C.c_int64),
                            _ptr(self.qual, C.c_uint8), _ptr(self.val, C.c_uint8), _ptr(self.group_id, C.c_int32),
-                           int(fix_duplicates))
+                           int(fix_duplicates), int(use_otsdb_timestamp), int(use_max_value))
 
     @classmethod
-    def from_rows(cls, series, group_ids, fix_duplicates=False):
+    def from_rows(cls, series, group_ids, fix_duplicates=False, use_otsdb_timestamp=False, use_max_value=True):
         """series: [[(base_time, [(qualifier bytes, value bytes, timestamp | None), ...]), ...], ...]"""
         srp, bases, rcp, qo, vo, ts = [0], [], [0], [0], [0], []
         qb, vb = bytearray(), bytearray()
@@ -331,7 +333,8 @@ class HostCellBatch:
                 rcp.append(len(qo) - 1)
             srp.append(len(bases))
         return cls(srp, bases, rcp, qo, vo, np.frombuffer(bytes(qb), np.uint8), np.frombuffer(bytes(vb), np.uint8),
-                   group_ids, np.array(ts, np.int64) if any_ts else None, fix_duplicates)
+                   group_ids, np.array(ts, np.int64) if any_ts else None, fix_duplicates, use_otsdb_timestamp,
+                   use_max_value)
 
 
 class RollupBatch(C.Structure):

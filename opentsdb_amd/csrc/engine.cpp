@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <chrono>
+#include <condition_variable>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -1552,6 +1553,7 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   std::vector<int32_t> rstate(R1), rerr(R1);
   CmpParams p{};
   p.fix_dup = cb->fix_duplicates ? 1 : 0;
+  p.dtcs = cb->use_otsdb_timestamp ? (cb->use_max_value ? 1 : 2) : 0;
   // device spans; the uploads and the host layout between them are not counted.  A scan in several
   // chunks sizes every chunk, then recomputes each one before writing it: both passes count.
   double cmp_ms = 0;
@@ -1560,7 +1562,8 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   // the per-row LDS path (k_cmp_row) when every row of a chunk fits one block; else the global
   // sort (TSDBHIP_CMP_ROWS=0 forces the latter)
   const char* rows_env = std::getenv("TSDBHIP_CMP_ROWS");
-  const bool rows_ok = !(rows_env && rows_env[0] == '0');
+  // (dtcsMergeDataPoints, a non-default configuration, is restated in k_cmp_dedup only)
+  const bool rows_ok = !(rows_env && rows_env[0] == '0') && !p.dtcs;
   std::vector<int> row_cap(n_chunks, 0);
   std::vector<uint32_t> row_span(n_chunks, 0);
   // upload, analyze and build the entries of chunk k; its rows' sizes and states to the host
@@ -3362,22 +3365,82 @@ tsdbhip_result* make_result(int64_t n_groups, int64_t n_points) {
   return r;
 }
 
+// Persistent host helpers of the result assembly, one pool per process: a multi-device context
+// assembles on every device worker at once, and spawning up to 8 threads per call there meant up
+// to 64 thread creations a query (and a std::system_error across the C ABI when one failed).  One
+// caller uses the pool at a time; a concurrent caller, or any caller when no helper thread could
+// be created, runs its items inline.
+class AssemblyPool {
+ public:
+  static AssemblyPool& get() {
+    static AssemblyPool p;
+    return p;
+  }
+  // fn(t) for t in [0, nt) with t = 0 on the calling thread; false when the pool is busy
+  bool run(int nt, const std::function<void(int)>& fn) {
+    std::unique_lock<std::mutex> call(call_mu_, std::try_to_lock);
+    if (!call.owns_lock()) return false;
+    nt = std::min<int>(nt, 1 + (int)th_.size());
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = &fn;
+      nt_ = nt;
+      pending_ = nt - 1;
+      gen_++;
+    }
+    cv_.notify_all();
+    fn(0);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [this] { return pending_ == 0; });
+    job_ = nullptr;
+    return true;
+  }
+  int width() const { return 1 + (int)th_.size(); }
+
+ private:
+  AssemblyPool() {
+    const int hw = std::max(1, std::min(8, (int)std::thread::hardware_concurrency()));
+    try {
+      for (int t = 1; t < hw; t++) th_.emplace_back([this, t] { loop(t); });
+    } catch (const std::exception&) {   // fewer helpers (or none): run() narrows nt
+    }
+    for (auto& t : th_) t.detach();   // process lifetime (no join at static destruction)
+  }
+  void loop(int t) {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return gen_ != seen; });
+      seen = gen_;
+      if (t >= nt_) continue;
+      const std::function<void(int)>* fn = job_;
+      lk.unlock();
+      (*fn)(t);
+      lk.lock();
+      if (--pending_ == 0) done_.notify_all();
+    }
+  }
+  std::mutex call_mu_, mu_;
+  std::condition_variable cv_, done_;
+  std::vector<std::thread> th_;
+  const std::function<void(int)>* job_ = nullptr;
+  int nt_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+};
+
 // n work items over up to 8 host threads when the work is large (a day of 1m buckets over 1000
 // groups is 1.4M points: 1.6 ms single-threaded), else inline
 template <class Fn>
 void par_groups(int64_t n, int64_t work, Fn&& fn) {
-  const int64_t hw = std::max<int64_t>(1, std::min<int64_t>(8, (int64_t)std::thread::hardware_concurrency()));
-  const int64_t nt = work >= (1 << 18) ? std::min<int64_t>(hw, n) : 1;
-  if (nt <= 1) {
-    for (int64_t i = 0; i < n; i++) fn(i);
-    return;
-  }
-  std::vector<std::thread> th;
-  for (int64_t t = 0; t < nt; t++)
-    th.emplace_back([&, t]() {
+  AssemblyPool& pool = AssemblyPool::get();
+  const int64_t nt = work >= (1 << 18) ? std::min<int64_t>(pool.width(), n) : 1;
+  if (nt > 1) {
+    const std::function<void(int)> chunk = [&](int t) {
       for (int64_t i = t * n / nt; i < (t + 1) * n / nt; i++) fn(i);
-    });
-  for (auto& x : th) x.join();
+    };
+    if (pool.run((int)nt, chunk)) return;
+  }
+  for (int64_t i = 0; i < n; i++) fn(i);
 }
 
 int assemble(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, const double* val,

@@ -363,6 +363,7 @@ struct CmpParams {
   const uint8_t* q;
   const uint8_t* v;
   int32_t fix_dup;
+  int32_t dtcs;                 // 0: defaultMergeDataPoints; 1 / 2: dtcsMergeDataPoints keeping the max / min
   // per column
   int32_t* col_row;             // [n_cols]
   int64_t* col_n;               // [n_cols] datapoints the column contributes

@@ -243,6 +243,111 @@ __device__ __forceinline__ CmpEnt cmp_ent(const CmpParams& p, uint32_t e) {
   return r;
 }
 
+// ColumnDatapointIterator.getCellValueAsDouble (:201-211) of an entry: false where ByteBuffer would
+// read past the value (a float of a length other than 4 / 8, an integer of 3, 5, 6 or 7 bytes)
+__device__ __forceinline__ bool cmp_dval(const CmpEnt& e, double* out) {
+  const uint8_t fl = e.fix ? e.fixed_q1 : e.qp[e.eq - 1];
+  const uint8_t* v = e.vp;
+  uint64_t b = 0;
+  for (int i = 0; i < e.evl; i++) b = (b << 8) | v[i];
+  if (fl & 8) {
+    if (e.evl == 4) { *out = (double)__uint_as_float((uint32_t)b); return true; }
+    if (e.evl == 8) { *out = __longlong_as_double((long long)b); return true; }
+    return false;
+  }
+  if (e.evl == 1) *out = (double)(int8_t)b;
+  else if (e.evl == 2) *out = (double)(int16_t)b;
+  else if (e.evl == 4) *out = (double)(int32_t)b;
+  else if (e.evl == 8) *out = (double)(int64_t)b;
+  else return false;
+  return true;
+}
+
+// the single column a row keeps as stored (noMergesOrFixups :311-328): no merge, no value read
+__device__ __forceinline__ bool cmp_as_stored(const CmpParams& p, int64_t r) {
+  if (p.row_heap[r] != 1) return false;
+  const int64_t c = p.row_one[r];
+  const uint32_t info = p.col_info[c];
+  const int64_t ql = (int64_t)(p.col_qo[c + 1] - p.col_qo[c]);
+  return (info & 3) == CMP_DATA && !(info & 8) && (ql == 2 || (ql == 4 && cmp_in_ms(p.q[p.col_qo[c]])));
+}
+
+// dtcsMergeDataPoints (CompactionQueue.java:508-547) over one run [i, j) of equal keys.  The heap
+// visits the run newest column first (equal write timestamps: scan order); the head's value is
+// replaced by each later one that is strictly greater (p.dtcs 1, use_max_value) / smaller (2).
+// So the kept entry is the head when its value is NaN, else the first in heap order holding the
+// extreme of the non-NaN values.  No duplicate exception.  The meta byte reads the kept
+// column's isMilliseconds() after the run advanced it (:544-545): the resolution of the column's
+// datapoint after its last one in the run (or of that one when it was the column's last); klen
+// bit 1 carries that flag instead of the kept entry's own width.
+__device__ void cmp_dedup_dtcs(const CmpParams& p, int64_t i, int64_t j, int64_t row) {
+  const bool merged = !cmp_as_stored(p, row);
+  auto superseded = [&](int64_t t) {
+    const uint32_t c = p.ent_col[p.idx2[t]];
+    return (p.col_info[c] & 3) == CMP_APPEND && t + 1 < j && p.ent_col[p.idx2[t + 1]] == c;
+  };
+  // heap rank of t over u: newer column, then scan order
+  auto before = [&](int64_t t, int64_t u) {
+    const int64_t a = p.col_ts ? p.col_ts[p.ent_col[p.idx2[t]]] : 0, b = p.col_ts ? p.col_ts[p.ent_col[p.idx2[u]]] : 0;
+    return a != b ? a > b : t < u;
+  };
+  int64_t head = -1, best = -1;
+  double ext = 0;
+  bool any = false, bad = false;
+  for (int64_t t = i; t < j; t++) {
+    p.klen[t] = 0;
+    if (superseded(t)) continue;
+    double x = 0;
+    if (!cmp_dval(cmp_ent(p, p.idx2[t]), &x)) { bad = true; continue; }
+    if (head < 0 || before(t, head)) head = t;
+    if (x != x) continue;
+    if (!any || (p.dtcs == 1 ? x > ext : x < ext)) { ext = x; any = true; }
+  }
+  if (bad && merged) cmp_fail(p.row_err, row, TSDB_E_RUNTIME);   // BufferUnderflowException
+  if (head < 0) return;
+  double hv = 0;
+  (void)cmp_dval(cmp_ent(p, p.idx2[head]), &hv);
+  if (hv != hv || !any) {
+    best = head;
+  } else {
+    for (int64_t t = i; t < j; t++) {
+      if (superseded(t)) continue;
+      double x = 0;
+      if (!cmp_dval(cmp_ent(p, p.idx2[t]), &x) || !(x == ext)) continue;
+      if (best < 0 || before(t, best)) best = t;
+    }
+  }
+  const uint32_t e = p.idx2[best];
+  const uint32_t c = p.ent_col[e];
+  const CmpEnt kb = cmp_ent(p, e);
+  // the kept column's last entry in the run, then its next datapoint
+  int64_t last = best;
+  for (int64_t t = i; t < j; t++)
+    if (p.ent_col[p.idx2[t]] == c && p.ent_qo[p.idx2[t]] > p.ent_qo[p.idx2[last]]) last = t;
+  const uint32_t el = p.idx2[last];
+  const CmpEnt kl = cmp_ent(p, el);
+  bool ms = kl.eq == 4;
+  const uint32_t info = p.col_info[c];
+  if ((info & 3) == CMP_APPEND) {
+    // the parsed append column iterates its pairs by offset: the column's next entry in key order
+    for (int64_t t = j; t < p.n_ent && (int64_t)(p.key2[t] >> 22) == row; t++)
+      if (p.ent_col[p.idx2[t]] == c) {
+        int64_t u = t;   // (the surviving pair of that offset: the column's last one there)
+        while (u + 1 < p.n_ent && p.key2[u + 1] == p.key2[t] && p.ent_col[p.idx2[u + 1]] == c) u++;
+        ms = cmp_ent(p, p.idx2[u]).eq == 4;
+        break;
+      }
+  } else {
+    const uint64_t qo = p.col_qo[c];
+    const int64_t ql = (int64_t)(p.col_qo[c + 1] - qo);
+    const int64_t vstart = (info & 4) ? 4 : 0;
+    const int64_t vlen = (int64_t)(p.col_vo[c + 1] - p.col_vo[c]) - vstart;
+    const int64_t qn = (int64_t)p.ent_qo[el] + kl.eq, vn = (int64_t)p.ent_vo[el] - vstart + kl.evl;
+    if (qn < ql && vn < vlen) ms = cmp_in_ms(p.q[qo + qn]);
+  }
+  p.klen[best] = 1u | ((ms ? 1u : 0u) << 1) | ((uint32_t)kb.eq << 2) | ((uint32_t)kb.evl << 8);
+}
+
 __global__ __launch_bounds__(256) void k_cmp_dedup(CmpParams p) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.n_ent) return;
@@ -251,6 +356,10 @@ __global__ __launch_bounds__(256) void k_cmp_dedup(CmpParams p) {
   int64_t j = i + 1;
   while (j < p.n_ent && p.key2[j] == k) j++;
   const int64_t row = (int64_t)(k >> 22);
+  if (p.dtcs) {
+    cmp_dedup_dtcs(p, i, j, row);
+    return;
+  }
   // a pair an append column repeats later is replaced (TreeMap.put); the newest column wins
   auto superseded = [&](int64_t t) {
     const uint32_t c = p.ent_col[p.idx2[t]];

@@ -134,8 +134,10 @@ class Workers {
     cv_.notify_all();
     for (auto& t : th_) t.join();
   }
-  // fn(i) for every i of idx at once; returns when all have finished
+  // fn(i) for every i of idx at once; returns when all have finished.  Callers are serialized
+  // (call_mu_): the slots and pending_ belong to one call at a time.
   void run(const std::vector<int>& idx, const std::function<void(int)>& fn) {
+    std::lock_guard<std::mutex> call(call_mu_);
     // slot 0 (no worker of its own) runs here, or else the last slot of the set
     const int inline_i = std::find(idx.begin(), idx.end(), 0) != idx.end() ? 0 : idx.back();
     {
@@ -171,7 +173,7 @@ class Workers {
       if (--pending_ == 0) done_.notify_all();
     }
   }
-  std::mutex mu_;
+  std::mutex call_mu_, mu_;
   std::condition_variable cv_, done_;
   std::vector<Slot> slots_;
   std::vector<std::thread> th_;
@@ -1015,6 +1017,7 @@ int md_timing(tsdbhip_ctx* c, tsdbhip_timing* out) {
 
 int md_sync(tsdbhip_ctx* c) {
   MultiDev* m = md_of(c);
+  std::lock_guard<std::mutex> lk(ctx_mutex(c));
   return each_device(m, [&](int d) { return tsdbhip_sync(m->subs[d]); }, true);
 }
 

@@ -83,7 +83,7 @@ def lib():
                                        C.POINTER(C.POINTER(abi.Result))]
         L.ref_result_free.argtypes = [C.POINTER(abi.Result)]
         L.ref_compact_row.argtypes = [C.c_int64, C.POINTER(C.c_void_p), C.POINTER(C.c_int64), C.POINTER(C.c_void_p),
-                                      C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_int,
+                                      C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_int, C.c_int,
                                       C.POINTER(C.c_void_p), C.POINTER(C.c_int64), C.POINTER(C.c_void_p),
                                       C.POINTER(C.c_int64)]
         L.ref_free.argtypes = [C.c_void_p]
@@ -287,10 +287,13 @@ def scan_bounds(q: abi.Query):
     return s.value, e.value
 
 
-def compact_row(columns, fix_duplicates: bool = True, timestamps=None):
+def compact_row(columns, fix_duplicates: bool = True, timestamps=None, use_otsdb_timestamp: bool = False,
+                use_max_value: bool = True):
     """CompactionQueue.Compaction.compact() of one row (query time): columns = [(qualifier
     bytes, value bytes)] in scan order, timestamps = their KeyValue timestamps (default: the
-    position).  Returns (qualifier, value), None (no datapoint) or raises OracleError."""
+    position).  use_otsdb_timestamp selects dtcsMergeDataPoints (CompactionQueue.java:508-547),
+    keeping the max (use_max_value) or min value at a repeated offset.  Returns (qualifier,
+    value), None (no datapoint) or raises OracleError."""
     n = len(columns)
     bufs = [(C.create_string_buffer(bytes(q), max(1, len(q))), C.create_string_buffer(bytes(v), max(1, len(v))))
             for q, v in columns]
@@ -301,7 +304,8 @@ def compact_row(columns, fix_duplicates: bool = True, timestamps=None):
     ts = (C.c_int64 * max(1, n))(*(timestamps if timestamps is not None else range(n)))
     oq, ov = C.c_void_p(), C.c_void_p()
     oql, ovl = C.c_int64(), C.c_int64()
-    rc = lib().ref_compact_row(n, qp, ql, vp, vl, ts, int(fix_duplicates), C.byref(oq), C.byref(oql), C.byref(ov),
+    rc = lib().ref_compact_row(n, qp, ql, vp, vl, ts, int(fix_duplicates),
+                               (1 if use_max_value else 2) if use_otsdb_timestamp else 0, C.byref(oq), C.byref(oql), C.byref(ov),
                                C.byref(ovl))
     if rc < 0:
         _err(rc)

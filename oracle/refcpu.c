@@ -985,8 +985,42 @@ static void parse_append(const uint8_t* v, int64_t vlen, uint8_t** oq, int64_t* 
 /* Compaction.compact() as TSDB.compact(row) returns it to a query (SaltScanner.processRow
  * :802-830).  Returns 1 with the compacted cell in out_q / out_v (malloc'd), 0 when the row
  * has no datapoint (compacted == null), or a negative TSDB_E_* code. */
+/* ColumnDatapointIterator.getCellValueAsDouble :201-211 of the current datapoint (fixups applied):
+ * ByteBuffer.getFloat / getDouble / get / getShort / getInt / getLong by its value length; a float of
+ * a length other than 4 or 8, or an integer of 3, 5, 6 or 7 bytes, reads past the copy
+ * (BufferUnderflowException, a RuntimeException) */
+static int cdi_dval(const cdi* c, double* out) {
+  const uint8_t* v = c->v + c->vi;
+  const int64_t n = c->cur_vlen;
+  if (c->q[c->qi + c->cur_qlen - 1] & 0x8) {   /* Internal.isFloat of the current qualifier */
+    if (n == 4) {
+      const uint32_t b = be32(v);
+      float f;
+      memcpy(&f, &b, 4);
+      *out = (double)f;
+      return 1;
+    }
+    if (n == 8) {
+      const uint64_t b = ((uint64_t)be32(v) << 32) | be32(v + 4);
+      memcpy(out, &b, 8);
+      return 1;
+    }
+    return 0;
+  }
+  if (n == 1) *out = (double)(int8_t)v[0];
+  else if (n == 2) *out = (double)(int16_t)be16(v);
+  else if (n == 4) *out = (double)(int32_t)be32(v);
+  else if (n == 8) *out = (double)(int64_t)(((uint64_t)be32(v) << 32) | be32(v + 4));
+  else return 0;
+  return 1;
+}
+#define DTCS_UNDERFLOW(c) \
+  do { free(live); jthrow(TSDB_E_RUNTIME, "BufferUnderflowException: a %lld-byte value in getCellValueAsDouble", (long long)(c)->cur_vlen); } while (0)
+
+/* dtcs: 0 = defaultMergeDataPoints; 1 / 2 = dtcsMergeDataPoints (tsd.storage.use_otsdb_timestamp)
+ * keeping the max / the min value (tsd.storage.use_max_value true / false) */
 int ref_compact_row(int64_t ncols, const uint8_t* const* quals, const int64_t* qlens, const uint8_t* const* vals,
-                    const int64_t* vlens, const int64_t* col_ts, int fix_duplicates, uint8_t** out_q,
+                    const int64_t* vlens, const int64_t* col_ts, int fix_duplicates, int dtcs, uint8_t** out_q,
                     int64_t* out_qlen, uint8_t** out_v, int64_t* out_vlen) {
   cdi* volatile cols = NULL;
   volatile int64_t n = 0;
@@ -1045,7 +1079,47 @@ int ref_compact_row(int64_t ncols, const uint8_t* const* quals, const int64_t* q
       for (int64_t i = 0; i < n; i++) live[i] = cols[i].vlen > 0 && cols[i].qi < cols[i].qlen;
       for (int64_t i = 0; i < n; i++)
         if (!live[i]) { free(live); jthrow(TSDB_E_ILLEGAL_DATA, "empty value"); }
-      for (;;) {
+      if (dtcs) {
+        /* dtcsMergeDataPoints :508-547.  col1 = the heap's head; its value and position are taken
+         * before it advances; every further column at the same offset (heap order: newest column
+         * first) replaces it when its value is strictly greater (use_max_value) / smaller.  No
+         * duplicate exception.  ms_in_row / s_in_row read the winner's isMilliseconds() AFTER it
+         * advanced (:544-545): the resolution of its next datapoint, or of its last one. */
+        for (;;) {
+          int64_t best = -1;
+          for (int64_t i = 0; i < n; i++)
+            if (live[i] && (best < 0 || cdi_less(&cols[i], &cols[best]))) best = i;
+          if (best < 0) break;
+          cdi* c1 = &cols[best];
+          if (c1->vi + c1->cur_vlen > c1->vlen) { free(live); jthrow(TSDB_E_ILLEGAL_DATA, "value shorter than its qualifiers"); }
+          int64_t w = best, wqi = c1->qi, wvi = c1->vi, wql = c1->cur_qlen, wvl = c1->cur_vlen;
+          const int64_t ts1 = c1->cur_off;
+          double v1 = 0, v2 = 0;
+          if (!cdi_dval(c1, &v1)) DTCS_UNDERFLOW(c1);
+          live[best] = cdi_advance(c1);
+          for (;;) {
+            int64_t b2 = -1;
+            for (int64_t i = 0; i < n; i++)
+              if (live[i] && (b2 < 0 || cdi_less(&cols[i], &cols[b2]))) b2 = i;
+            if (b2 < 0 || cols[b2].cur_off != ts1) break;
+            cdi* c2 = &cols[b2];
+            if (c2->vi + c2->cur_vlen > c2->vlen) { free(live); jthrow(TSDB_E_ILLEGAL_DATA, "value shorter than its qualifiers"); }
+            if (!cdi_dval(c2, &v2)) DTCS_UNDERFLOW(c2);
+            if ((dtcs == 1 && v2 > v1) || (dtcs != 1 && v1 > v2)) {
+              w = b2; v1 = v2;
+              wqi = c2->qi; wvi = c2->vi; wql = c2->cur_qlen; wvl = c2->cur_vlen;
+            }
+            live[b2] = cdi_advance(c2);
+          }
+          memcpy(cq + qo, cols[w].q + wqi, (size_t)wql);   /* writeToBuffersFromOffset */
+          memcpy(cv + vo, cols[w].v + wvi, (size_t)wvl);
+          qo += wql;
+          vo += wvl;
+          segs++;
+          if (cols[w].is_ms) ms_in_row = 1; else s_in_row = 1;
+        }
+      }
+      for (; !dtcs;) {
         int64_t best = -1;
         for (int64_t i = 0; i < n; i++)
           if (live[i] && (best < 0 || cdi_less(&cols[i], &cols[best]))) best = i;

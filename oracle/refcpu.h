@@ -92,7 +92,7 @@ int ref_run_rollup_query(const tsdbhip_rollup_batch* rb, const tsdbhip_query* q,
 /* Compaction.compact() of one row's columns (query-time, no write-back): 1 + the compacted
  * cell (free both with ref_free), 0 = no datapoint, < 0 = TSDB_E_* */
 int ref_compact_row(int64_t ncols, const uint8_t* const* quals, const int64_t* qlens, const uint8_t* const* vals,
-                    const int64_t* vlens, const int64_t* col_ts, int fix_duplicates, uint8_t** out_q,
+                    const int64_t* vlens, const int64_t* col_ts, int fix_duplicates, int dtcs, uint8_t** out_q,
                     int64_t* out_qlen, uint8_t** out_v, int64_t* out_vlen);
 void ref_free(void* p);
 /* ---- histogram path (refhist.c) ----------------------------------

@@ -5,8 +5,11 @@ Each case is one row: its columns in the order the test adds them (qualifier and
 the column timestamp is the test's makekv sequence number, i.e. the position), the
 fix_duplicates setting (the test class sets true; the "expected = IllegalDataException"
 tests set false) and the compacted cell compactionq.compact() returns (qualifier, value),
-null, or the exception class.  useMaxTsWhileCompacting runs the tsd.storage.use_otsdb_timestamp
-merge (dtcsMergeDataPoints), which is outside the query path and is not transcribed.
+null, or the exception class.  useMaxTsWhileCompacting (:108-131) sets
+tsd.storage.use_otsdb_timestamp, whose merge (dtcsMergeDataPoints, CompactionQueue.java:508-547)
+is on the query path too (SaltScanner.processRow -> TSDB.compact); its columns carry random
+write timestamps (Math.abs(rnd.nextLong())), transcribed as three fixed ones -- the expected
+cell does not depend on them, since no offset repeats.
 
     python tests/golden/make_compaction_golden.py
 """
@@ -44,14 +47,17 @@ def F32(x):
 def cases():
     out = []
 
-    def add(name, lines, cols, expect, fix=True):
+    def add(name, lines, cols, expect, fix=True, **extra):
         out.append({"name": name, "source": f"{SRC}:{lines}", "fix_duplicates": fix,
                     "columns": [[q.hex(), v.hex()] for q, v in cols],
                     "expect": expect if isinstance(expect, (str, type(None))) else
-                    {"qualifier": expect[0].hex(), "value": expect[1].hex()}})
+                    {"qualifier": expect[0].hex(), "value": expect[1].hex()}, **extra})
 
     q07, q17, q27, q37, q47, q57, q67 = (bytes([0, x]) for x in (0x07, 0x17, 0x27, 0x37, 0x47, 0x57, 0x67))
     m0, m1, m2 = (bytes([0xF0, 0, x, 0x07]) for x in (0x00, 0x01, 0x02))
+    add("useMaxTsWhileCompacting", "108-131", [(m0, L(4)), (m1, L(5)), (m2, L(2))],
+        (m0 + m1 + m2, L(4) + L(5) + L(2) + ZERO), use_otsdb_timestamp=True,
+        timestamps=[6917529027641081857, 1234567890123456789, 4611686018427387905])
     add("emptyRow", "133-145", [], None)
     add("oneCellRow", "147-163", [(q07, L(42))], (q07, L(42)))
     add("oneCellAppend", "165-182", [(APPEND, q07 + L(42))], (q07, L(42)))

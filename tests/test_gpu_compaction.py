@@ -8,7 +8,9 @@ returns them to a query (src/core/CompactionQueue.java:330-566).
     with repeats, 2-byte float / length fixups, annotations, duplicates with equal and
     different values, mixed s / ms -- against the oracle's compaction row by row, and the
     queries over them against the oracle's queries over its own compaction;
-  * a 3,000-series store of one-cell-per-datapoint rows in shuffled column order."""
+  * a 3,000-series store of one-cell-per-datapoint rows in shuffled column order;
+  * tsd.storage.use_otsdb_timestamp (dtcsMergeDataPoints, CompactionQueue.java:508-547): every
+    known-answer row and randomized rows with repeated offsets against the oracle."""
 from __future__ import annotations
 
 import importlib.util
@@ -55,8 +57,9 @@ def rows_of(batch):
 @pytest.mark.parametrize("case", DOC["cases"], ids=[c["name"] for c in DOC["cases"]])
 def test_known_answers_on_gpu(eng, case):
     cols, expect = MK.expand_columns(case)
-    cb = abi.HostCellBatch.from_rows([[(B, [(q, v, i) for i, (q, v) in enumerate(cols)])]], [0],
-                                     case["fix_duplicates"])
+    ts = case.get("timestamps") or list(range(len(cols)))
+    cb = abi.HostCellBatch.from_rows([[(B, [(q, v, t) for t, (q, v) in zip(ts, cols)])]], [0],
+                                     case["fix_duplicates"], case.get("use_otsdb_timestamp", False))
     eng.load_cells(cb)
     got = rows_of(eng.download())
     q = abi.new_query(B, B + 3599, "sum")
@@ -193,6 +196,79 @@ def test_random_rows_match_oracle(eng, seed, fix):
             g = eng.run(q)
             if w is not None:
                 assert_groups_match(g, w, agg, ctx=f"{agg} {ds} {start}")
+
+
+@pytest.mark.parametrize("use_max", [True, False])
+@pytest.mark.parametrize("case", DOC["cases"], ids=[c["name"] for c in DOC["cases"]])
+def test_known_answer_rows_dtcs_on_gpu(eng, case, use_max):
+    """Every known-answer row under tsd.storage.use_otsdb_timestamp (dtcsMergeDataPoints,
+    CompactionQueue.java:508-547) with use_max_value true / false: the GPU's cell equals the
+    oracle's (no duplicate exception under this merge)."""
+    cols, _ = MK.expand_columns(case)
+    ts = case.get("timestamps") or list(range(len(cols)))
+    cb = abi.HostCellBatch.from_rows([[(B, [(q, v, t) for t, (q, v) in zip(ts, cols)])]], [0],
+                                     case["fix_duplicates"], True, use_max)
+    eng.load_cells(cb)
+    got = rows_of(eng.download())
+    try:
+        want = O.compact_row(cols, case["fix_duplicates"], ts, use_otsdb_timestamp=True, use_max_value=use_max)
+    except O.OracleError as e:
+        assert got == []
+        with pytest.raises(EngineError) as ge:
+            eng.run(abi.new_query(B, B + 3599, "sum"))
+        assert ge.value.code == e.code
+        return
+    assert got == ([] if want is None else [(B, want[0], want[1])])
+
+
+def random_row_dtcs(rng, n):
+    """random_row with many repeated offsets: equal and different values of every width, NaN
+    floats, second / millisecond duplicates of one offset, and now and then a value
+    getCellValueAsDouble cannot read (a 3-byte integer)."""
+    cols = random_row(rng, n, dup_p=0.35, diff_p=0.6)
+    out = []
+    for q, v, t in cols:
+        r = rng.random()
+        if len(q) == 2 and not (q[1] & 8) and r < 0.05:       # the same second as a ms qualifier
+            off = (int.from_bytes(q, "big") >> 4) * 1000
+            q2, v2 = _cell(off, True, int(rng.integers(-50, 50)), "int")
+            out.append((q2, v2, int(rng.integers(0, 10**6))))
+        elif len(q) == 2 and (q[1] & 0xB) == 0xB and r < 0.1:  # a NaN float duplicate
+            out.append((q, struct.pack(">f", float("nan")), int(rng.integers(0, 10**6))))
+        elif r < 0.004:                                       # an unreadable 3-byte integer
+            out.append((bytes([q[0], (q[1] & 0xF0) | 2]) if len(q) == 2 else q, b"\x00\x01\x02", t))
+            continue
+        out.append((q, v, t))
+    return out
+
+
+@pytest.mark.parametrize("seed,use_max", [(61, True), (62, False), (63, True), (64, False)])
+def test_random_rows_dtcs_match_oracle(eng, seed, use_max):
+    """Randomized scans with repeated offsets under dtcsMergeDataPoints against the oracle, row by
+    row; rows the oracle rejects raise the same exception from a covering query."""
+    rng = np.random.default_rng(seed)
+    series, groups = [], []
+    for s in range(40):
+        series.append([(B + 3600 * h, random_row_dtcs(rng, int(rng.integers(1, 60)))) for h in range(2)])
+        groups.append(s // 10)
+    cb = abi.HostCellBatch.from_rows(series, groups, False, True, use_max)
+    eng.load_cells(cb)
+    got = rows_of(eng.download())
+    want, errs = [], []
+    for rows in series:
+        for base, cols in rows:
+            try:
+                c = O.compact_row([(q, v) for q, v, _ in cols], False, [t for _, _, t in cols],
+                                  use_otsdb_timestamp=True, use_max_value=use_max)
+            except O.OracleError as e:
+                errs.append((base, e.code))
+                continue
+            if c is not None:
+                want.append((base, c[0], c[1]))
+    assert got == want
+    if errs:
+        with pytest.raises(EngineError):
+            eng.run(abi.new_query(B, B + 7199, "sum"))
 
 
 @pytest.mark.parametrize("seed", [5, 6])
