@@ -173,7 +173,17 @@ typedef struct {
   double compact_ms;             /* device compaction of the last tsdbhip_load_cells (k_compact pipeline) */
   int64_t fused_queries;         /* queries the last tsdbhip_run_multi answered from ONE fused streaming pass
                                     (0: separate passes, or not a run_multi) */
-  double exchange_ms;            /* multi-device context: gather to devices[0] + merge (host wall time) */
+  double exchange_ms;            /* multi-device context: xfer_ms + select_ms + assemble_ms (host wall time) */
+  /* multi-device context, host wall time of the call's stages (they sum to total_ms up to bookkeeping):
+   * devices_ms   every device's own pass over its shard (in parallel; per-device kernel times in
+   *              tsdbhip_md_stats), partial states / span values left on the devices;
+   * xfer_ms      device-to-device moves (transfer(): RCCL send / recv or peer copies, to completion);
+   * select_ms    owners' merge of straddling groups + finalisation, or their percentile selection;
+   * assemble_ms  the result on the host from devices[0]'s dense rows (or the devices' results merged). */
+  double devices_ms;
+  double xfer_ms;
+  double select_ms;
+  double assemble_ms;
 } tsdbhip_timing;
 
 /* ---- library-level helpers (host logic of the reference, restated) ------- */
@@ -284,6 +294,12 @@ int tsdbhip_partials_layout_get(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_
                                 tsdbhip_partials_layout* out);
 /* Computes this shard's partial states into `partials` (device or host memory, layout above). */
 int tsdbhip_run_partials(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_global, void* partials);
+/* n queries sharing the time range and downsampling (a TSQuery's sub-queries over one metric,
+ * TsdbQuery.java:916-1049 once per sub-query): query i's partial states at partials + i * bytes.
+ * sum / avg / min / max / dev / count without rate come from ONE fused streaming pass over the
+ * shard (bit-identical to n tsdbhip_run_partials calls); any other mix runs query by query. */
+int tsdbhip_run_partials_multi(tsdbhip_ctx* ctx, const tsdbhip_query* qs, int n, int64_t n_groups_global,
+                               void* partials);
 /* Merges n_ranks rank-ordered partial buffers (device or host memory) and builds the result. */
 int tsdbhip_finalize(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_global,
                      const void* partials, int n_ranks, tsdbhip_result** out);

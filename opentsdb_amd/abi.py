@@ -145,6 +145,10 @@ class Timing(C.Structure):
         ("compact_ms", C.c_double),
         ("fused_queries", C.c_int64),
         ("exchange_ms", C.c_double),
+        ("devices_ms", C.c_double),
+        ("xfer_ms", C.c_double),
+        ("select_ms", C.c_double),
+        ("assemble_ms", C.c_double),
     ]
 
 

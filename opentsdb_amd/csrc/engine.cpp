@@ -2,6 +2,7 @@
 // planning the reference does on the host (scan bounds, downsample spec parsing,
 // SpanGroup membership), HBM layout of the loaded Spans, and result assembly.
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cctype>
@@ -2796,7 +2797,7 @@ int hwin_slots(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P) {
   // left to the dense split)
   if (P.mode != MODE_GRID || q->rate || q->ds_fill != TSDB_FILL_NONE || P.K <= 64 || P.I <= 0 || 3600000 % P.I != 0 || 3600000 / P.I > 64 ||
       ((P.B0 % 3600000) + 3600000) % 3600000 != 0 || P.dense_out || P.emit_only || P.values_only || P.sel_direct ||
-      P.multi || P.seq_dense || P.raw || P.anchored || P.none || P.f == F_SEL || !c->fast_qw || !c->tl_other.empty())
+      P.seq_dense || P.raw || P.anchored || P.none || P.f == F_SEL || !c->fast_qw || !c->tl_other.empty())
     return 0;
   for (int cls = 0; cls < 2; cls++) {
     if (!c->tl[cls][0].empty()) return 0;
@@ -3108,7 +3109,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       fp.win_w = hwin;
       {
         const char* e6 = std::getenv("TSDBHIP_SHORT6");
-        fp.short6 = (shortk == 1 && !(e6 && e6[0] == '0')) ? 1 : 0;
+        fp.short6 = ((shortk == 1 || shortk == 3) && !(e6 && e6[0] == '0')) ? 1 : 0;
       }
       if (shortk == 1 && fp.sel_direct && fp.sel_cols && K <= 64) {   // k_short's column stage
         fp.sel_stage = fp.wave_lds;
@@ -3373,11 +3374,14 @@ tsdbhip_result* make_result(int64_t n_groups, int64_t n_points) {
 class AssemblyPool {
  public:
   static AssemblyPool& get() {
-    static AssemblyPool p;
-    return p;
+    // never destroyed: a condition variable destroyed at exit while the detached helpers wait on
+    // it blocks the exiting process (glibc pthread_cond_destroy)
+    static AssemblyPool* p = new AssemblyPool();
+    return *p;
   }
   // fn(t) for t in [0, nt) with t = 0 on the calling thread; false when the pool is busy
   bool run(int nt, const std::function<void(int)>& fn) {
+    if (getpid() != pid_) return false;   // a forked child: the helpers live in the parent only
     std::unique_lock<std::mutex> call(call_mu_, std::try_to_lock);
     if (!call.owns_lock()) return false;
     nt = std::min<int>(nt, 1 + (int)th_.size());
@@ -3398,7 +3402,7 @@ class AssemblyPool {
   int width() const { return 1 + (int)th_.size(); }
 
  private:
-  AssemblyPool() {
+  AssemblyPool() : pid_(getpid()) {
     const int hw = std::max(1, std::min(8, (int)std::thread::hardware_concurrency()));
     try {
       for (int t = 1; t < hw; t++) th_.emplace_back([this, t] { loop(t); });
@@ -3426,6 +3430,7 @@ class AssemblyPool {
   const std::function<void(int)>* job_ = nullptr;
   int nt_ = 0, pending_ = 0;
   uint64_t gen_ = 0;
+  const pid_t pid_;
 };
 
 // n work items over up to 8 host threads when the work is large (a day of 1m buckets over 1000
@@ -4561,17 +4566,10 @@ int run_rollup(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
   return collect(c, &qr, P, G, true, out);
 }
 
-// Several decomposable group-by aggregators over one cheap downsampling, fused: ONE streaming
-// pass (k_short / k_fast, KR 2) decodes and downsamples every series once and folds each
-// series' SpanGroup contributions into the per-tile state of every aggregator at once
-// (kcommon.h MultiReg: sum / avg, min, max, dev, count); then one k_reduce per query over its
-// view of those states.  Each aggregator sees exactly the contributions -- in the same order --
-// that its own pass would feed it (AggregationIterator.nextDoubleValue :735-797 per span, per
-// timestamp), so results are bit-identical to separate queries.  Returns 1 when the queries or
-// the batch do not qualify (rate, other aggregators, flags, a row class the streaming kernels do
-// not take, K > 64) or when a tile broke a streaming premise at run time: the caller then runs
-// the queries one by one.
-int run_multi_fused(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_result** outs) {
+// The fused streaming pass of run_multi_fused / tsdbhip_run_partials_multi: every decomposable
+// aggregator's tile partials in c->m_* (MultiPartials).  1: the queries or the batch do not
+// qualify, or a tile broke a streaming premise (the caller runs the queries one by one).
+int fused_pass(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, Plan& P) {
   const char* env = std::getenv("TSDBHIP_MULTI_FUSE");
   if (n < 2 || (env && env[0] == '0')) return 1;
   for (int i = 0; i < n; i++) {
@@ -4583,25 +4581,52 @@ int run_multi_fused(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_resu
   }
   tsdbhip_query q0 = qs[0];
   q0.aggregator = TSDB_AGG_SUM;   // LERP: the interpolation of every fused aggregator but count
-  Plan P;
   int rc = plan_query(c, &q0, P);
   if (rc) return rc;
-  if (P.raw || P.none || P.gsel || P.f == F_SEL || P.K > 64 || !fast_path_ok(c, &q0, P) || !c->tl_other.empty())
-    return 1;
+  if (P.raw || P.none || P.gsel || P.f == F_SEL || !c->tl_other.empty()) return 1;
+  // K <= 64: k_short / k_rows / k_fast (KR 2); K > 64 (a day of 1m buckets): k_hwin's MULTI variant
+  if (!hwin_slots(c, &q0, P) && (P.K > 64 || !fast_path_ok(c, &q0, P))) return 1;
   for (int cls = 0; cls < 2; cls++) {
     if (c->tl[cls][0].empty() && c->tl[cls][1].empty() && c->tl[cls][2].empty()) continue;
     const int qw = cls ? c->fast_qw2 : c->fast_qw, vl = cls ? c->fast_vl2 : c->fast_vl;
     if (!qw || !fast_supported(P.f, qw, vl)) return 1;
   }
-  const int64_t G = c->n_groups, K = P.K;
   P.multi = true;
   for (int i = 0; i < n; i++) P.multi_dev = P.multi_dev || qs[i].aggregator == TSDB_AGG_DEV;
-  rc = run_device(c, &q0, P, G, false);
+  rc = run_device(c, &q0, P, c->n_groups, false);
   if (rc) return rc;
   int32_t handed_back = 0;
   HIP_OK(hipMemcpyAsync(&handed_back, c->redo_final, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
-  if (handed_back) return 1;
+  return handed_back ? 1 : 0;
+}
+
+// aggregator agg's view of the fused pass's tile partials (as k_reduce reads its own pass's)
+Partials multi_view(tsdbhip_ctx* c, int agg) {
+  switch (agg) {
+    case TSDB_AGG_MIN: return Partials{c->m_mn.as<double>(), c->m_m2.as<double>(), c->m_nl.as<uint32_t>(), c->m_f.as<uint32_t>()};
+    case TSDB_AGG_MAX: return Partials{c->m_mx.as<double>(), c->m_m2.as<double>(), c->m_nl.as<uint32_t>(), c->m_f.as<uint32_t>()};
+    case TSDB_AGG_DEV: return Partials{c->m_mean.as<double>(), c->m_m2.as<double>(), c->m_nl.as<uint32_t>(), c->m_f.as<uint32_t>()};
+    case TSDB_AGG_COUNT: return Partials{c->m_sum.as<double>(), c->m_m2.as<double>(), c->m_nz.as<uint32_t>(), c->m_f.as<uint32_t>()};
+    default: return Partials{c->m_sum.as<double>(), c->m_m2.as<double>(), c->m_nl.as<uint32_t>(), c->m_f.as<uint32_t>()};
+  }
+}
+
+// Several decomposable group-by aggregators over one cheap downsampling, fused: ONE streaming
+// pass (k_short / k_fast / k_rows KR 2, or k_hwin's MULTI variant for K > 64) decodes and
+// downsamples every series once and folds each series' SpanGroup contributions into the
+// per-tile state of every aggregator at once (kcommon.h MultiReg: sum / avg, min, max, dev,
+// count); then one k_reduce per query over its view of those states.  Each aggregator sees
+// exactly the contributions -- in the same order -- that its own pass would feed it
+// (AggregationIterator.nextDoubleValue :735-797 per span, per timestamp), so results are
+// bit-identical to separate queries.  Returns 1 when the queries or the batch do not qualify
+// (rate, other aggregators, flags, a row class the streaming kernels do not take) or when a
+// tile broke a streaming premise at run time: the caller then runs the queries one by one.
+int run_multi_fused(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_result** outs) {
+  Plan P;
+  int rc = fused_pass(c, qs, n, P);
+  if (rc) return rc;
+  const int64_t G = c->n_groups, K = P.K;
   // one k_reduce per query over its view of the fused partials, into its own output rows
   const int64_t gk = std::max<int64_t>(1, G * K);
   HIP_OK(c->out_val.ensure(gk * 8 * n));
@@ -4612,13 +4637,7 @@ int run_multi_fused(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_resu
     if (rc) return rc;
     const int ga = ga_of(qs[i].aggregator);
     ReduceParams rp{};
-    switch (qs[i].aggregator) {
-      case TSDB_AGG_MIN: rp.part = Partials{c->m_mn.as<double>(), c->m_m2.as<double>(), c->m_nl.as<uint32_t>(), c->m_f.as<uint32_t>()}; break;
-      case TSDB_AGG_MAX: rp.part = Partials{c->m_mx.as<double>(), c->m_m2.as<double>(), c->m_nl.as<uint32_t>(), c->m_f.as<uint32_t>()}; break;
-      case TSDB_AGG_DEV: rp.part = Partials{c->m_mean.as<double>(), c->m_m2.as<double>(), c->m_nl.as<uint32_t>(), c->m_f.as<uint32_t>()}; break;
-      case TSDB_AGG_COUNT: rp.part = Partials{c->m_sum.as<double>(), c->m_m2.as<double>(), c->m_nz.as<uint32_t>(), c->m_f.as<uint32_t>()}; break;
-      default: rp.part = Partials{c->m_sum.as<double>(), c->m_m2.as<double>(), c->m_nl.as<uint32_t>(), c->m_f.as<uint32_t>()};
-    }
+    rp.part = multi_view(c, qs[i].aggregator);
     rp.group_tile_ptr = c->d_gtp.as<int64_t>();
     rp.G = G;
     rp.K = K;
@@ -4862,10 +4881,9 @@ extern "C" int tsdbhip_partials_layout_get(tsdbhip_ctx* c, const tsdbhip_query* 
   return 0;
 }
 
-extern "C" int tsdbhip_run_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, void* partials) {
-  MD_REFUSE(c, "tsdbhip_run_partials");
-  if (!c || !q || !partials) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
-  std::lock_guard<std::mutex> lk(c->mu);
+namespace {
+// tsdbhip_run_partials with c->mu held
+int run_partials_locked(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, void* partials) {
   HIP_OK(hipSetDevice(c->device));
   if (c->ro_active) { const int r = ro_check(q); if (r) return r; }
   const tsdbhip_query qr = ro_query(c, q);
@@ -4920,6 +4938,100 @@ extern "C" int tsdbhip_run_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int6
   HIP_OK(hipStreamSynchronize(c->stream));
   record_timing(c, P, redo_n);
   if (err) return fail(err, "error raised by the device path");
+  return 0;
+}
+
+// The fused pass's per-query partial states (tsdbhip_run_partials_multi): query i's merged
+// (group, slot) states at partials + i * L.bytes.  1: not fusable (the caller loops).
+int run_partials_fused(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, int64_t n_groups_global, void* partials) {
+  if (c->ro_active) return 1;   // (a rollup shard stages each aggregate's own cells)
+  for (int i = 0; i < n; i++) {
+    Plan Pi;
+    const int rc = plan_partials(c, &qs[i], n_groups_global, Pi);
+    if (rc) return rc;
+  }
+  Plan P;
+  int rc = fused_pass(c, qs, n, P);
+  if (rc) return rc;
+  const int64_t G = n_groups_global, K = P.K, GL = c->n_groups;
+  const PartLayout L = part_layout(G, K);
+  HIP_OK(c->xbuf.ensure(L.bytes * n));
+  unsigned char* xb0 = c->xbuf.as<unsigned char>();
+  HIP_OK(hipMemsetAsync(xb0, 0, L.bytes * n, c->stream));
+  std::vector<double> ident;
+  for (int i = 0; i < n; i++) {
+    unsigned char* xb = xb0 + (int64_t)i * L.bytes;
+    const int ga = ga_of(qs[i].aggregator);
+    if (GL * K) {
+      ReduceParams rp{};
+      rp.part = multi_view(c, qs[i].aggregator);
+      rp.group_tile_ptr = c->d_gtp.as<int64_t>();
+      rp.G = GL;
+      rp.K = K;
+      rp.ga = ga;
+      rp.err = c->err.as<int32_t>();
+      rp.state = Partials{reinterpret_cast<double*>(xb), reinterpret_cast<double*>(xb + L.off_b),
+                          reinterpret_cast<uint32_t*>(xb + L.off_n), reinterpret_cast<uint32_t*>(xb + L.off_f)};
+      HIP_OK(launch_reduce(rp, c->stream));
+    }
+    if (G > GL && (ga == GA_MIN || ga == GA_MAX)) {   // identity states of the groups this shard lacks
+      ident.assign((G - GL) * K, ga == GA_MIN ? INFINITY : -INFINITY);
+      HIP_OK(hipMemcpyAsync(xb + GL * K * 8, ident.data(), ident.size() * 8, hipMemcpyHostToDevice, c->stream));
+      HIP_OK(hipStreamSynchronize(c->stream));
+    }
+    if (GL) HIP_OK(hipMemcpyAsync(xb + L.off_act, c->gact.p, GL * 4, hipMemcpyDeviceToDevice, c->stream));
+  }
+  HIP_OK(hipEventRecord(c->ev[2], c->stream));
+  HIP_OK(hipMemcpyAsync(partials, xb0, L.bytes * n, hipMemcpyDefault, c->stream));
+  int32_t err = 0, redo_n = 0;
+  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipMemcpyAsync(&redo_n, c->redo_final, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  c->fused_n = n;
+  record_timing(c, P, redo_n);
+  c->fused_n = 0;
+  if (err) return fail(err, "error raised by the device path");
+  return 0;
+}
+}  // namespace
+
+extern "C" int tsdbhip_run_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, void* partials) {
+  MD_REFUSE(c, "tsdbhip_run_partials");
+  if (!c || !q || !partials) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  return run_partials_locked(c, q, n_groups_global, partials);
+}
+
+// Several queries' partial states from one fused streaming pass (a TSQuery's sub-queries over
+// one metric on a rank's shard): as n tsdbhip_run_partials calls, query i's layout at
+// partials + i * tsdbhip_partials_layout.bytes.
+extern "C" int tsdbhip_run_partials_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, int64_t n_groups_global,
+                                          void* partials) {
+  MD_REFUSE(c, "tsdbhip_run_partials_multi");
+  if (!c || !qs || !partials || n < 1) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad argument");
+  for (int i = 1; i < n; i++) {
+    const tsdbhip_query &a = qs[0], &b = qs[i];
+    if (a.start_time != b.start_time || a.end_time != b.end_time || a.ds_function != b.ds_function ||
+        a.ds_interval_ms != b.ds_interval_ms || a.ds_fill != b.ds_fill || a.ds_all != b.ds_all ||
+        a.ds_calendar != b.ds_calendar)
+      return fail(TSDB_E_ILLEGAL_ARGUMENT, "tsdbhip_run_partials_multi: the queries must share the time range and downsampling");
+  }
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  int rc = run_partials_fused(c, qs, n, n_groups_global, partials);
+  if (rc <= 0) return rc;
+  tsdbhip_partials_layout L{};
+  {
+    const tsdbhip_query qr = ro_query(c, &qs[0]);
+    Plan P;
+    rc = plan_partials(c, &qr, n_groups_global, P);
+    if (rc) return rc;
+    L.bytes = part_layout(n_groups_global, P.K).bytes;
+  }
+  for (int i = 0; i < n; i++) {
+    rc = run_partials_locked(c, &qs[i], n_groups_global, static_cast<unsigned char*>(partials) + (int64_t)i * L.bytes);
+    if (rc) return rc;
+  }
   return 0;
 }
 
@@ -5083,6 +5195,71 @@ int md_sel_select(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, const doubl
   if (rc) return rc;
   *out_val = c->out_val.as<double>();
   *out_flag = c->out_flag.as<uint8_t>();
+  return 0;
+}
+
+// multi.cpp, owner-routed partials: the byte offsets of a partials buffer's parts
+void partials_offsets(int64_t G, int64_t K, int64_t* off_b, int64_t* off_n, int64_t* off_f, int64_t* off_act,
+                      int64_t* bytes) {
+  const PartLayout L = part_layout(G, K);
+  *off_b = L.off_b;
+  *off_n = L.off_n;
+  *off_f = L.off_f;
+  *off_act = L.off_act;
+  *bytes = L.bytes;
+}
+
+// ... the owner's step: the states of group g_fold that n_mini later devices hold (mini_state
+// layout, in device order) folded into its own state of g_fold (SpanGroup order continues
+// across devices), then every group of its buffer finalised -- dense value / emit rows and
+// activity in out_val / out_flag / out_act (device memory of this context).
+int md_partials_finish(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, unsigned char* state, int64_t g_fold,
+                       const unsigned char* mini, int n_mini, double* out_val, uint8_t* out_flag, uint32_t* out_act) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_OK(hipSetDevice(c->device));
+  if (c->ro_active) { const int r = ro_check(q); if (r) return r; }
+  const tsdbhip_query qr = ro_query(c, q);
+  Plan P;
+  int rc = plan_partials(c, &qr, G, P);
+  if (rc) return rc;
+  const int64_t K = P.K;
+  const PartLayout L = part_layout(G, K);
+  HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
+  if (n_mini > 0 && g_fold >= 0 && K > 0) {
+    StateFoldParams fp{};
+    fp.state = state;
+    fp.off_b = L.off_b;
+    fp.off_n = L.off_n;
+    fp.off_f = L.off_f;
+    fp.off_act = L.off_act;
+    fp.g = g_fold;
+    fp.K = K;
+    fp.ga = P.ga;
+    fp.mini = mini;
+    fp.mini_stride = mini_state_stride(K);
+    fp.n_mini = n_mini;
+    HIP_OK(launch_state_fold(fp, c->stream));
+  }
+  RankMergeParams mp{};
+  mp.base = state;
+  mp.stride = L.bytes;
+  mp.off_b = L.off_b;
+  mp.off_n = L.off_n;
+  mp.off_f = L.off_f;
+  mp.off_act = L.off_act;
+  mp.n_ranks = 1;
+  mp.G = G;
+  mp.K = K;
+  mp.ga = P.ga;
+  mp.out_val = out_val;
+  mp.out_flag = out_flag;
+  mp.out_act = out_act;
+  mp.err = c->err.as<int32_t>();
+  HIP_OK(launch_rank_merge(mp, c->stream));
+  int32_t err = 0;
+  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  if (err) return fail(err, "error raised by the device path");
   return 0;
 }
 

@@ -230,6 +230,19 @@ struct RankMergeParams {
   int32_t* err;
 };
 
+// Multi-device owner merge (multi.cpp): the partial states of group g (K slots) that n_mini later
+// devices hold, gathered in device order as mini states ([a K f64 | b K f64 | n K u32 | f K u32 |
+// act u32], mini_state_stride(K) bytes each, multi.h), folded into the owner's state of g in that order.
+struct StateFoldParams {
+  unsigned char* state;           // the owner's partials buffer (tsdbhip_partials layout)
+  int64_t off_b, off_n, off_f, off_act;
+  int64_t g, K;
+  int32_t ga;
+  const unsigned char* mini;
+  int64_t mini_stride;
+  int32_t n_mini;
+};
+
 // ---- raw path (no downsampling): AggregationIterator over the timestamp union ----
 // A decoded datapoint: tsf = timestamp (ms) | RAW_FLOAT when the value bits are a double
 // (AggregationIterator keeps exactly this FLAG_FLOAT encoding, src/core/AggregationIterator.java:112-118).
@@ -496,6 +509,7 @@ hipError_t launch_emit_vals(const GridParams& p, hipStream_t s);
 hipError_t launch_sel_seg(const SelParams& p, hipStream_t s, int64_t maxn);
 hipError_t launch_ordered(const OrdParams& p, hipStream_t s);
 hipError_t launch_rank_merge(const RankMergeParams& p, hipStream_t s);
+hipError_t launch_state_fold(const StateFoldParams& p, hipStream_t s);
 // per-downsample-function instantiations (k_grid.hip / k_fast.hip, one object per F)
 template <int F> hipError_t launch_grid_inst(const GridParams& p, hipStream_t s);
 template <int F> hipError_t launch_fast_inst(const GridParams& p, int qw, int vl, hipStream_t s);

@@ -693,6 +693,40 @@ __global__ __launch_bounds__(256) void k_rank_merge(RankMergeParams p) {
   }
 }
 
+// Owner merge of a group that straddles devices (multi.cpp): thread k folds the later devices'
+// states of slot k into the owner's, in device order (= SpanGroup order).
+__global__ __launch_bounds__(256) void k_state_fold(StateFoldParams p) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned char* b = p.state;
+  if (k < p.K) {
+    const int64_t i = p.g * p.K + k;
+    PState S;
+    S.a = reinterpret_cast<const double*>(b)[i];
+    S.b = reinterpret_cast<const double*>(b + p.off_b)[i];
+    S.n = reinterpret_cast<const uint32_t*>(b + p.off_n)[i];
+    S.f = reinterpret_cast<const uint32_t*>(b + p.off_f)[i];
+    for (int m = 0; m < p.n_mini; m++) {
+      const unsigned char* x = p.mini + (int64_t)m * p.mini_stride;
+      PState X;
+      X.a = reinterpret_cast<const double*>(x)[k];
+      X.b = reinterpret_cast<const double*>(x + 8 * p.K)[k];
+      X.n = reinterpret_cast<const uint32_t*>(x + 16 * p.K)[k];
+      X.f = reinterpret_cast<const uint32_t*>(x + 20 * p.K)[k];
+      S = ps_merge(p.ga, S, X);
+    }
+    reinterpret_cast<double*>(b)[i] = S.a;
+    reinterpret_cast<double*>(b + p.off_b)[i] = S.b;
+    reinterpret_cast<uint32_t*>(b + p.off_n)[i] = S.n;
+    reinterpret_cast<uint32_t*>(b + p.off_f)[i] = S.f;
+  }
+  if (k == 0) {
+    uint32_t act = reinterpret_cast<const uint32_t*>(b + p.off_act)[p.g];
+    for (int m = 0; m < p.n_mini; m++)
+      act |= reinterpret_cast<const uint32_t*>(p.mini + (int64_t)m * p.mini_stride + 24 * p.K)[0];
+    reinterpret_cast<uint32_t*>(b + p.off_act)[p.g] = act;
+  }
+}
+
 // ---- synthetic MockBase-equivalent store, generated in HBM -------------------------
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   uint64_t z = x + 0x9e3779b97f4a7c15ULL;
@@ -952,6 +986,11 @@ hipError_t launch_rank_merge(const RankMergeParams& p, hipStream_t s) {
   const int64_t n = std::max(p.G * p.K, p.G);
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_rank_merge, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_state_fold(const StateFoldParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_state_fold, dim3((unsigned)((p.K + 255) / 256)), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 

@@ -2465,8 +2465,10 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
 // bucket store and no group-by pass over it (the dense split).  LERP needs neighbours across
 // windows, so a series with a bucket missing inside its data span hands the tile back (the
 // general kernel takes it); regular data never does.
-template <int F, int QW, int VL, int D, int NP = DPL>
-__global__ __launch_bounds__(256, SHORT_OCC(VL)) void k_hwin(GridParams p, const RowDesc* __restrict__ rows,
+// MULTI: the fused multi-aggregator pass (tsdbhip_run_multi, p.multi): every decomposable
+// aggregator's window partials at once (MultiReg, as k_short / k_rows KR 2).
+template <int F, int QW, int VL, int D, bool MULTI = false, int NP = DPL>
+__global__ __launch_bounds__(256, MULTI ? SHORT_OCC2(VL) : SHORT_OCC(VL)) void k_hwin(GridParams p, const RowDesc* __restrict__ rows,
                                                              const int64_t* __restrict__ srp, const int64_t* __restrict__ tbeg,
                                                              const int64_t* __restrict__ tend) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2494,7 +2496,7 @@ __global__ __launch_bounds__(256, SHORT_OCC(VL)) void k_hwin(GridParams p, const
     L.acc[k] = fast_identity<F>();
     L.cnt[k] = 0;
   }
-  RegPart RP;
+  std::conditional_t<MULTI, MultiReg, RegPart> RP;
   rp_init(p.ga, RP);
   WAVE_SYNC();
   bool redo = false, any = false;
@@ -2586,10 +2588,21 @@ __global__ __launch_bounds__(256, SHORT_OCC(VL)) void k_hwin(GridParams p, const
     // the window's partials: slots h W .. h W + Wh - 1 of the tile
     if (lane < Wh) {
       const int64_t o = tile * K + (int64_t)h * W + lane;
-      p.part.a[o] = RP.pa;
-      p.part.b[o] = RP.pb;
-      p.part.n[o] = RP.pn;
-      p.part.f[o] = RP.pf;
+      if constexpr (MULTI) {
+        p.mp.sum[o] = RP.sum;
+        p.mp.mn[o] = RP.mn;
+        p.mp.mx[o] = RP.mx;
+        p.mp.mean[o] = RP.mean;
+        p.mp.m2[o] = RP.m2;
+        p.mp.nl[o] = RP.nl;
+        p.mp.nz[o] = RP.nz;
+        p.mp.f[o] = RP.f;
+      } else {
+        p.part.a[o] = RP.pa;
+        p.part.b[o] = RP.pb;
+        p.part.n[o] = RP.pn;
+        p.part.f[o] = RP.pf;
+      }
     }
     rp_init(p.ga, RP);
     if (has) { seen = true; cur++; }

@@ -200,8 +200,15 @@ struct MultiDev {
   bool side_valid = false;
   std::vector<tsdbhip_ctx*> side;
   std::vector<char> straddle;           // [G] the group's spans sit on several devices
-  std::vector<Buf> xb;                  // per device: exchange source
-  Buf gb, ov, of;                       // devices[0]: gathered exchange, merged values / flags
+  std::vector<Buf> xb;                  // per device: exchange source (partial states)
+  std::vector<Buf> mb;                  // per device: straddling groups' states from later devices
+  std::vector<Buf> dv, df, da;          // per device: owned groups' dense values / emit flags / activity
+  Buf ov, of, oa;                       // devices[0]: the owners' dense rows gathered
+  // resident series of each group on each device, per load (owner-routed partials)
+  bool gcnt_valid = false;
+  std::vector<std::vector<int64_t>> gcnt;
+  // stage wall times of the current call (tsdbhip_timing devices / xfer / select / assemble_ms)
+  double t_dev = 0, t_xfer = 0, t_sel = 0, t_asm = 0;
   tsdbhip_timing timing{};
   std::vector<tsdbhip_timing> dev_timing;   // per device, last call
   double xfer_bytes = 0;                // device-to-device bytes of the last call
@@ -280,7 +287,14 @@ struct Xfer {
 // Moves every piece: RCCL -- one grouped round of ncclSend / ncclRecv between the ranks, pieces
 // within a device as copies on its stream; COPY -- peer copies on the destination's stream.
 // Sources must be complete; returns when every destination holds its bytes.
+int transfer_(MultiDev* m, const std::vector<Xfer>& xs);
 int transfer(MultiDev* m, const std::vector<Xfer>& xs) {
+  const double t0 = now_ms();
+  const int rc = transfer_(m, xs);
+  m->t_xfer += now_ms() - t0;
+  return rc;
+}
+int transfer_(MultiDev* m, const std::vector<Xfer>& xs) {
   const int n = (int)m->devices.size();
   std::vector<char> used(n, 0);
   auto st = [&](int d) { return ctx_stream(m->subs[d]); };
@@ -384,10 +398,12 @@ void free_all(std::vector<tsdbhip_result*>& v) {
 // Every device answers the query over its shard; the results merge.
 int run_local(MultiDev* m, const tsdbhip_query* q, bool none, tsdbhip_result** out) {
   std::vector<tsdbhip_result*> parts(m->devices.size(), nullptr);
+  double t0 = now_ms();
   int rc = each_device(m, [&](int d) { return tsdbhip_run(m->subs[d], q, &parts[d]); });
-  const double t0 = now_ms();
+  m->t_dev += now_ms() - t0;
+  t0 = now_ms();
   if (!rc) rc = merge(m, parts, none, out);
-  m->timing.exchange_ms = now_ms() - t0;
+  m->t_asm += now_ms() - t0;
   free_all(parts);
   return rc;
 }
@@ -397,44 +413,188 @@ std::string per_span_calendar() {
          "load with tsdbhip_md_shard_mode(ctx, TSDB_SHARD_GROUPS)";
 }
 
-// Decomposable group-by over straddling groups: partial states per device -> gather to devices[0]
-// -> merge in device order (tsdbhip_finalize on the merge context).
-int run_partials_xchg(MultiDev* m, const tsdbhip_query* q, tsdbhip_result** out) {
+// Group ownership over SERIES shards: group g is owned by the first device holding one of its
+// spans (a group without spans: the owner of the group before it, so owned ranges are
+// contiguous).  Shards are contiguous in SpanGroup order, so a device's groups it does not own
+// precede the ones it owns, and only its last owned group can continue on later devices.
+struct Owners {
+  std::vector<int> owner;                // [G]
+  std::vector<int64_t> total;            // [G] spans over every device
+  std::vector<int64_t> skip, rows;       // [n] spans of groups the device does not own (a prefix); all its spans
+  std::vector<int64_t> last, extra;      // [n] its last owned group, and that group's spans on later devices
+  std::vector<int64_t> ga, gb;           // [n] owned group range [ga, gb) (-1: owns none)
+  std::vector<std::vector<int>> later;   // [n] the later devices holding spans of last[o], in device order
+};
+
+int owners_of(const MultiDev* m, const std::vector<int>& ds, const std::vector<std::vector<int64_t>>& cnt, Owners& O) {
+  const int n = (int)m->devices.size();
+  const int64_t G = m->G;
+  O.owner.assign(std::max<int64_t>(1, G), ds[0]);
+  O.total.assign(std::max<int64_t>(1, G), 0);
+  for (int64_t g = 0, prev = ds[0]; g < G; g++) {
+    int o = -1;
+    for (int d : ds) {
+      if (cnt[d][g] > 0 && o < 0) o = d;
+      O.total[g] += cnt[d][g];
+    }
+    O.owner[g] = o < 0 ? (int)prev : o;
+    prev = O.owner[g];
+  }
+  O.skip.assign(n, 0);
+  O.rows.assign(n, 0);
+  O.extra.assign(n, 0);
+  O.last.assign(n, -1);
+  O.ga.assign(n, -1);
+  O.gb.assign(n, -1);
+  O.later.assign(n, {});
+  for (int d : ds) {
+    bool owned_seen = false;
+    for (int64_t g = 0; g < G; g++) {
+      if (O.owner[g] == d) {
+        if (O.ga[d] < 0) O.ga[d] = g;
+        O.gb[d] = g + 1;
+      }
+      if (!cnt[d][g]) continue;
+      O.rows[d] += cnt[d][g];
+      if (O.owner[g] != d) {
+        if (owned_seen) return set_error(TSDB_E_HIP, "multi-device exchange: shard not contiguous in SpanGroup order");
+        O.skip[d] += cnt[d][g];
+        continue;
+      }
+      if (O.last[d] >= 0 && O.total[O.last[d]] != cnt[d][O.last[d]])
+        return set_error(TSDB_E_HIP, "multi-device exchange: a straddling group inside a shard");
+      owned_seen = true;
+      O.last[d] = g;
+    }
+    if (O.last[d] >= 0) {
+      O.extra[d] = O.total[O.last[d]] - cnt[d][O.last[d]];
+      for (int e : ds)
+        if (e > d && cnt[e][O.last[d]] > 0) O.later[d].push_back(e);
+    }
+  }
+  return 0;
+}
+
+// resident series of every group on every live device, once per load
+const std::vector<std::vector<int64_t>>& group_counts(MultiDev* m) {
+  if (!m->gcnt_valid) {
+    m->gcnt.assign(m->devices.size(), {});
+    for (int d : live_devices(m)) m->gcnt[d] = ctx_group_counts(m->subs[d], m->G);
+    m->gcnt_valid = true;
+  }
+  return m->gcnt;
+}
+
+// Decomposable group-by over straddling groups (sum, count, min, max, avg, dev
+// partials), owner-routed: every device reduces its shard to per-(group, slot) partial states
+// (n queries from one fused pass when they share the downsampling, tsdbhip_run_partials_multi);
+// only the straddling groups' K-slot states move, to their owners, which fold them in device
+// order (= SpanGroup order, TsdbQuery.java:916-1049's one AggregationIterator per group) and
+// finalise their groups in place; the owners' dense (group, slot) rows (G x K x 9 B a query)
+// go to devices[0] for the result.  No device receives every device's G x K states.
+int run_partials_owner(MultiDev* m, const tsdbhip_query* qs, int nq, tsdbhip_result** outs) {
   const std::vector<int> ds = live_devices(m);
+  const int64_t G = m->G;
   tsdbhip_partials_layout L{};
-  int rc = tsdbhip_partials_layout_get(m->root, q, m->G, &L);
+  int rc = tsdbhip_partials_layout_get(m->root, &qs[0], G, &L);
   if (rc) return rc;
   for (int d : ds) {
     tsdbhip_partials_layout Ld{};
-    rc = tsdbhip_partials_layout_get(m->subs[d], q, m->G, &Ld);
+    rc = tsdbhip_partials_layout_get(m->subs[d], &qs[0], G, &Ld);
     if (rc) return rc;
     if (Ld.bytes != L.bytes || Ld.n_slots != L.n_slots) return set_error(TSDB_E_NOT_IMPLEMENTED, per_span_calendar());
   }
-  rc = m->gb.ensure((size_t)L.bytes * ds.size());
+  const int64_t K = L.n_slots;
+  int64_t off_b = 0, off_n = 0, off_f = 0, off_act = 0, bytes = 0;
+  partials_offsets(G, K, &off_b, &off_n, &off_f, &off_act, &bytes);
+  Owners O;
+  rc = owners_of(m, ds, group_counts(m), O);
   if (rc) return rc;
+  // 1. every device's partial states, nq queries' buffers back to back
+  double t0 = now_ms();
   rc = each_device(m, [&](int d) {
-    const int r = m->xb[d].ensure((size_t)L.bytes);
-    return r ? r : tsdbhip_run_partials(m->subs[d], q, m->G, m->xb[d].p);
+    const int r = m->xb[d].ensure((size_t)L.bytes * nq);
+    if (r) return r;
+    return nq > 1 ? tsdbhip_run_partials_multi(m->subs[d], qs, nq, G, m->xb[d].p)
+                  : tsdbhip_run_partials(m->subs[d], &qs[0], G, m->xb[d].p);
   });
+  m->t_dev += now_ms() - t0;
   if (rc) return rc;
-  const double t0 = now_ms();
+  // 2. the straddling groups' states to their owners (mini states, in device order)
+  const int64_t ms = mini_state_stride(K);
   std::vector<Xfer> xs;
-  for (size_t i = 0; i < ds.size(); i++)
-    xs.push_back({ds[i], m->xb[ds[i]].p, 0, static_cast<char*>(m->gb.p) + i * (size_t)L.bytes, (size_t)L.bytes});
+  for (int o : ds) {
+    const int nm = (int)O.later[o].size();
+    if (!nm) continue;
+    rc = m->mb[o].ensure((size_t)(ms * nm * nq));
+    if (rc) return rc;
+    const int64_t g = O.last[o];
+    for (int i = 0; i < nq; i++)
+      for (int j = 0; j < nm; j++) {
+        const int d = O.later[o][j];
+        const char* src = static_cast<const char*>(m->xb[d].p) + (int64_t)i * L.bytes;
+        char* dst = static_cast<char*>(m->mb[o].p) + ((int64_t)i * nm + j) * ms;
+        xs.push_back({d, src + g * K * 8, o, dst, (size_t)(K * 8)});
+        xs.push_back({d, src + off_b + g * K * 8, o, dst + 8 * K, (size_t)(K * 8)});
+        xs.push_back({d, src + off_n + g * K * 4, o, dst + 16 * K, (size_t)(K * 4)});
+        xs.push_back({d, src + off_f + g * K * 4, o, dst + 20 * K, (size_t)(K * 4)});
+        xs.push_back({d, src + off_act + g * 4, o, dst + 24 * K, 4});
+      }
+  }
   rc = transfer(m, xs);
-  if (!rc) rc = tsdbhip_finalize(m->root, q, m->G, m->gb.p, (int)ds.size(), out);
-  m->timing.exchange_ms = now_ms() - t0;
+  if (rc) return rc;
+  // 3. every owner folds its straddling group and finalises its groups: dense rows on the device
+  std::vector<int> owners;
+  for (int d : ds) if (O.ga[d] >= 0) owners.push_back(d);
+  const int64_t gk = std::max<int64_t>(1, G * K);
+  t0 = now_ms();
+  rc = each_of(m, owners, [&](int o) {
+    int r = m->dv[o].ensure((size_t)(gk * 8 * nq));
+    if (!r) r = m->df[o].ensure((size_t)(gk * nq));
+    if (!r) r = m->da[o].ensure((size_t)(std::max<int64_t>(1, G) * 4 * nq));
+    for (int i = 0; i < nq && !r; i++)
+      r = md_partials_finish(m->subs[o], &qs[i], G, static_cast<unsigned char*>(m->xb[o].p) + (int64_t)i * L.bytes,
+                             O.last[o], static_cast<const unsigned char*>(m->mb[o].p) + (int64_t)i * O.later[o].size() * ms,
+                             (int)O.later[o].size(), static_cast<double*>(m->dv[o].p) + i * gk,
+                             static_cast<uint8_t*>(m->df[o].p) + i * gk,
+                             static_cast<uint32_t*>(m->da[o].p) + i * std::max<int64_t>(1, G));
+    return r;
+  });
+  m->t_sel += now_ms() - t0;
+  if (rc) return rc;
+  // 4. the owners' rows to devices[0]
+  rc = m->ov.ensure((size_t)(gk * 8 * nq));
+  if (!rc) rc = m->of.ensure((size_t)(gk * nq));
+  if (!rc) rc = m->oa.ensure((size_t)(std::max<int64_t>(1, G) * 4 * nq));
+  if (rc) return rc;
+  std::vector<Xfer> ys;
+  for (int i = 0; i < nq; i++)
+    for (int o : owners) {
+      const int64_t r0 = O.ga[o] * K, nr = (O.gb[o] - O.ga[o]) * K;
+      const int64_t vo = i * gk + r0, ao = i * std::max<int64_t>(1, G) + O.ga[o];
+      ys.push_back({o, static_cast<double*>(m->dv[o].p) + vo, 0, static_cast<double*>(m->ov.p) + vo, (size_t)(nr * 8)});
+      ys.push_back({o, static_cast<uint8_t*>(m->df[o].p) + vo, 0, static_cast<uint8_t*>(m->of.p) + vo, (size_t)nr});
+      ys.push_back({o, static_cast<uint32_t*>(m->da[o].p) + ao, 0, static_cast<uint32_t*>(m->oa.p) + ao,
+                    (size_t)((O.gb[o] - O.ga[o]) * 4)});
+    }
+  rc = transfer(m, ys);
+  if (rc) return rc;
+  // 5. the results on the host
+  t0 = now_ms();
+  for (int i = 0; i < nq && !rc; i++)
+    rc = tsdbhip_assemble(m->root, &qs[i], G, static_cast<double*>(m->ov.p) + i * gk,
+                          static_cast<uint8_t*>(m->of.p) + i * gk, static_cast<uint32_t*>(m->oa.p) + i * std::max<int64_t>(1, G),
+                          &outs[i]);
+  m->t_asm += now_ms() - t0;
   return rc;
 }
 
 // Percentile / median group-by and TSDB_QF_ORDERED over straddling groups (the
 // values of a non-decomposable aggregate go to the owning rank; Aggregators.java:657-708).
-// Group g's owner is the first device holding one of its spans.  SERIES shards are contiguous in
-// SpanGroup order, so on every device the groups it does not own precede the ones it owns, and
-// only its last owned group can have spans on later devices: those rows are appended to the
-// owner's rows in device order (= SpanGroup order), and each owner selects its groups over rows
-// that never left it.  Traffic: the straddling groups' rows plus G * K * 9 B of results, instead
-// of every span's contributions to devices[0].
+// Group g's owner is the first device holding one of its spans (Owners).  The straddling groups'
+// rows are appended to their owner's rows in device order (= SpanGroup order), and each owner
+// selects its groups over rows that never left it.  Traffic: the straddling groups' rows plus
+// G * K * 9 B of results, instead of every span's contributions to devices[0].
 int run_sel_xchg(MultiDev* m, const tsdbhip_query* q, tsdbhip_result** out) {
   const std::vector<int> ds = live_devices(m);
   const int n = (int)m->devices.size();
@@ -454,41 +614,9 @@ int run_sel_xchg(MultiDev* m, const tsdbhip_query* q, tsdbhip_result** out) {
     if (rc) return rc;
     if (Kd != K) return set_error(TSDB_E_NOT_IMPLEMENTED, per_span_calendar());
   }
-  // owners (a group without spans: the owner of the group before it, so owned ranges are contiguous)
-  std::vector<int> owner(std::max<int64_t>(1, G), ds[0]);
-  std::vector<int64_t> total(std::max<int64_t>(1, G), 0);
-  for (int64_t g = 0, prev = ds[0]; g < G; g++) {
-    int o = -1;
-    for (int d : ds) {
-      if (cnt[d][g] > 0 && o < 0) o = d;
-      total[g] += cnt[d][g];
-    }
-    owner[g] = o < 0 ? (int)prev : o;
-    prev = owner[g];
-  }
-  // per device: rows of the groups it does not own (a prefix), its rows, its last owned group
-  std::vector<int64_t> skip(n, 0), rows(n, 0), extra(n, 0), last(n, -1), ga(n, -1), gb(n, -1);
-  for (int d : ds) {
-    bool owned_seen = false;
-    for (int64_t g = 0; g < G; g++) {
-      if (owner[g] == d) {
-        if (ga[d] < 0) ga[d] = g;
-        gb[d] = g + 1;
-      }
-      if (!cnt[d][g]) continue;
-      rows[d] += cnt[d][g];
-      if (owner[g] != d) {
-        if (owned_seen) return set_error(TSDB_E_HIP, "multi-device exchange: shard not contiguous in SpanGroup order");
-        skip[d] += cnt[d][g];
-        continue;
-      }
-      if (last[d] >= 0 && total[last[d]] != cnt[d][last[d]])
-        return set_error(TSDB_E_HIP, "multi-device exchange: a straddling group inside a shard");
-      owned_seen = true;
-      last[d] = g;
-    }
-    if (last[d] >= 0) extra[d] = total[last[d]] - cnt[d][last[d]];
-  }
+  Owners O;
+  rc = owners_of(m, ds, cnt, O);
+  if (rc) return rc;
   std::vector<double*> vals(n, nullptr);
   std::vector<std::vector<uint8_t>> uni(n);
   std::vector<std::vector<uint32_t>> act(n);
@@ -496,20 +624,20 @@ int run_sel_xchg(MultiDev* m, const tsdbhip_query* q, tsdbhip_result** out) {
     uni[d].assign(std::max<int64_t>(1, G * K), 0);
     act[d].assign(std::max<int64_t>(1, G), 0);
   }
+  double t0 = now_ms();
   rc = each_of(m, ds, [&](int d) {
     int64_t Kd = 0;
-    return md_sel_values(m->subs[d], q, G, extra[d], &vals[d], &Kd, uni[d].data(), act[d].data());
+    return md_sel_values(m->subs[d], q, G, O.extra[d], &vals[d], &Kd, uni[d].data(), act[d].data());
   });
+  m->t_dev += now_ms() - t0;
   if (rc) return rc;
-  const double t0 = now_ms();
   // 1. the straddling groups' rows to their owners, appended in device order
   std::vector<Xfer> xs;
   for (int o : ds) {
-    if (last[o] < 0 || !extra[o]) continue;
-    const int64_t g = last[o];
-    int64_t at = rows[o];
-    for (int d : ds) {
-      if (d <= o || !cnt[d][g]) continue;
+    if (O.last[o] < 0 || !O.extra[o]) continue;
+    const int64_t g = O.last[o];
+    int64_t at = O.rows[o];
+    for (int d : O.later[o]) {
       int64_t pre = 0;   // rows before g on d
       for (int64_t h = 0; h < g; h++) pre += cnt[d][h];
       xs.push_back({d, vals[d] + pre * K, o, vals[o] + at * K, (size_t)(cnt[d][g] * K * 8)});
@@ -518,39 +646,44 @@ int run_sel_xchg(MultiDev* m, const tsdbhip_query* q, tsdbhip_result** out) {
   }
   rc = transfer(m, xs);
   if (rc) return rc;
-  // 2. every owner selects its groups (the rows of groups it does not own are skipped)
-  std::vector<uint8_t> u(std::max<int64_t>(1, G * K), 0);
+  // 2. every owner selects its groups (the rows of groups it does not own are skipped).  Its emit
+  // flags are its own, OR-ed with the later devices' flags of its straddling group (K bytes each);
+  // group activity over every device (G words each)
+  t0 = now_ms();
   std::vector<uint32_t> a(std::max<int64_t>(1, G), 0);
-  for (int d : ds) {
-    for (int64_t i = 0; i < G * K; i++) u[i] |= uni[d][i];
+  for (int d : ds)
     for (int64_t g = 0; g < G; g++) a[g] |= act[d][g];
-  }
   std::vector<int> owners;
   std::vector<std::vector<int64_t>> oc(n);
   for (int d : ds) {
-    if (ga[d] < 0) continue;
+    if (O.ga[d] < 0) continue;
     owners.push_back(d);
     oc[d].assign(std::max<int64_t>(1, G), 0);
-    for (int64_t g = ga[d]; g < gb[d]; g++) oc[d][g] = total[g];
+    for (int64_t g = O.ga[d]; g < O.gb[d]; g++) oc[d][g] = O.total[g];
+    if (O.last[d] >= 0)
+      for (int e : O.later[d])
+        for (int64_t k = 0; k < K; k++) uni[d][O.last[d] * K + k] |= uni[e][O.last[d] * K + k];
   }
   std::vector<double*> ov(n, nullptr);
   std::vector<uint8_t*> of(n, nullptr);
   rc = each_of(m, owners, [&](int d) {
-    return md_sel_select(m->subs[d], q, G, vals[d] + skip[d] * K, oc[d].data(), u.data(), &ov[d], &of[d]);
+    return md_sel_select(m->subs[d], q, G, vals[d] + O.skip[d] * K, oc[d].data(), uni[d].data(), &ov[d], &of[d]);
   });
+  m->t_sel += now_ms() - t0;
   // 3. the owners' dense rows to devices[0]
   if (!rc) rc = m->ov.ensure((size_t)(G * K * 8));
   if (!rc) rc = m->of.ensure((size_t)(G * K));
   if (rc) return rc;
   std::vector<Xfer> ys;
   for (int d : owners) {
-    const int64_t r0 = ga[d] * K, nr = (gb[d] - ga[d]) * K;
+    const int64_t r0 = O.ga[d] * K, nr = (O.gb[d] - O.ga[d]) * K;
     ys.push_back({d, ov[d] + r0, 0, static_cast<double*>(m->ov.p) + r0, (size_t)(nr * 8)});
     ys.push_back({d, of[d] + r0, 0, static_cast<uint8_t*>(m->of.p) + r0, (size_t)nr});
   }
   rc = transfer(m, ys);
+  t0 = now_ms();
   if (!rc) rc = tsdbhip_assemble(m->root, q, G, m->ov.p, m->of.p, a.data(), out);
-  m->timing.exchange_ms = now_ms() - t0;
+  m->t_asm += now_ms() - t0;
   return rc;
 }
 
@@ -671,14 +804,16 @@ int run_raw_series(MultiDev* m, const tsdbhip_query* q, tsdbhip_result** out) {
   for (int d = 0; d < n; d++)
     if (m->side[d] && !m->live[d]) run.push_back(d);
   std::sort(run.begin(), run.end());
+  double t0 = now_ms();
   rc = each_of(m, run, [&](int d) {
     int r = m->live[d] ? tsdbhip_run(m->subs[d], q, &parts[d]) : 0;
     if (!r && m->side[d]) r = tsdbhip_run(m->side[d], q, &parts[n + d]);
     return r;
   });
-  const double t0 = now_ms();
+  m->t_dev += now_ms() - t0;
+  t0 = now_ms();
   if (!rc) rc = merge(m, parts, false, out, &m->straddle, (size_t)n);
-  m->timing.exchange_ms = now_ms() - t0;
+  m->t_asm += now_ms() - t0;
   free_all(parts);
   return rc;
 }
@@ -689,14 +824,18 @@ int first_live(const MultiDev* m) {
 }
 
 int run_one(MultiDev* m, const tsdbhip_query* q, tsdbhip_result** out) {
-  m->timing.exchange_ms = 0;
   if (m->mode == TSDB_SHARD_AUTO) return tsdbhip_run(m->root, q, out);   // nothing loaded: as one empty device
   int kind = 0;
   int rc = query_kind(m->subs[first_live(m)], q, &kind);
   if (rc) return rc;
   if (m->mode == TSDB_SHARD_GROUPS || kind == QK_NONE) return run_local(m, q, kind == QK_NONE, out);
   if (kind == QK_RAW) return m->rollup ? run_local(m, q, false, out) : run_raw_series(m, q, out);
-  return kind == QK_PARTIALS ? run_partials_xchg(m, q, out) : run_sel_xchg(m, q, out);
+  return kind == QK_PARTIALS ? run_partials_owner(m, q, 1, out) : run_sel_xchg(m, q, out);
+}
+
+void reset_stages(MultiDev* m) {
+  m->t_dev = m->t_xfer = m->t_sel = m->t_asm = 0;
+  m->xfer_bytes = 0;
 }
 
 // Per-device stage times: maximum over the devices; counters: summed.
@@ -721,7 +860,11 @@ void device_timing(MultiDev* m, double wall_ms, bool fused) {
   }
   t.fused_queries = fused && fq > 0 ? fq : 0;
   t.total_ms = wall_ms;
-  t.exchange_ms = m->timing.exchange_ms;
+  t.devices_ms = m->t_dev;
+  t.xfer_ms = m->t_xfer;
+  t.select_ms = m->t_sel;
+  t.assemble_ms = m->t_asm;
+  t.exchange_ms = m->t_xfer + m->t_sel + m->t_asm;
   m->timing = t;
 }
 
@@ -768,6 +911,7 @@ std::vector<std::vector<int64_t>> shard_series(MultiDev* m, const int32_t* gid, 
   m->series.clear();
   m->pos0.clear();
   m->rollup = false;
+  m->gcnt_valid = false;
   drop_side(m);
   m->live.assign(n, 0);
   bool any = false;
@@ -939,6 +1083,7 @@ int md_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp) {
   m->mode = TSDB_SHARD_AUTO;
   m->series.clear();
   m->rollup = false;
+  m->gcnt_valid = false;
   drop_side(m);
   m->live.assign(n, 0);
   for (int d = 0; d < n; d++) m->live[d] = p[d + 1] > p[d];
@@ -961,7 +1106,7 @@ int md_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
   if (!q || !out) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> lk(ctx_mutex(c));
   *out = nullptr;
-  m->xfer_bytes = 0;
+  reset_stages(m);
   const double t0 = now_ms();
   const int rc = run_one(m, q, out);
   if (!rc) device_timing(m, now_ms() - t0, false);
@@ -974,29 +1119,40 @@ int md_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_result*
   std::lock_guard<std::mutex> lk(ctx_mutex(c));
   for (int i = 0; i < n; i++) outs[i] = nullptr;
   const double t0 = now_ms();
-  m->timing.exchange_ms = 0;
-  m->xfer_bytes = 0;
+  reset_stages(m);
   int rc = 0;
+  bool fused = false;
   if (m->mode == TSDB_SHARD_GROUPS) {
     // whole SpanGroups per device: each device runs its own fused pass over the queries
     const int nd = (int)m->devices.size();
     std::vector<std::vector<tsdbhip_result*>> parts(nd, std::vector<tsdbhip_result*>(n, nullptr));
+    double t1 = now_ms();
     rc = each_device(m, [&](int d) { return tsdbhip_run_multi(m->subs[d], qs, n, parts[d].data()); });
-    const double t1 = now_ms();
+    m->t_dev += now_ms() - t1;
+    t1 = now_ms();
     for (int i = 0; i < n && !rc; i++) {
       std::vector<tsdbhip_result*> pi(nd, nullptr);
       for (int d = 0; d < nd; d++) pi[d] = parts[d][i];
       rc = merge(m, pi, qs[i].aggregator == TSDB_AGG_NONE, &outs[i]);
     }
-    m->timing.exchange_ms = now_ms() - t1;
+    m->t_asm += now_ms() - t1;
     for (auto& p : parts) free_all(p);
+    fused = true;
   } else {
-    double xm = 0;
-    for (int i = 0; i < n && !rc; i++) {
-      rc = run_one(m, &qs[i], &outs[i]);
-      xm += m->timing.exchange_ms;
+    // series shards: queries that all exchange partial states share one fused pass per device
+    // (tsdbhip_run_partials_multi) and one owner-routed exchange; any other mix runs one by one
+    bool all_partials = m->mode != TSDB_SHARD_AUTO && n > 1;
+    for (int i = 0; i < n && all_partials && !rc; i++) {
+      int kind = 0;
+      rc = query_kind(m->subs[first_live(m)], &qs[i], &kind);
+      all_partials = kind == QK_PARTIALS;
     }
-    m->timing.exchange_ms = xm;
+    if (!rc && all_partials) {
+      rc = run_partials_owner(m, qs, n, outs);
+      fused = true;
+    } else {
+      for (int i = 0; i < n && !rc; i++) rc = run_one(m, &qs[i], &outs[i]);
+    }
   }
   if (rc) {
     for (int i = 0; i < n; i++) {
@@ -1005,7 +1161,7 @@ int md_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_result*
     }
     return rc;
   }
-  device_timing(m, now_ms() - t0, m->mode == TSDB_SHARD_GROUPS);
+  device_timing(m, now_ms() - t0, fused);
   return 0;
 }
 
@@ -1047,10 +1203,11 @@ void md_destroy(void* p) {
   m->pool = nullptr;
   drop_side(m);
   for (ncclComm_t cm : m->comms) if (cm) (void)rccl().destroy(cm);
-  for (Buf& b : m->xb) b.release();
-  m->gb.release();
+  for (auto* v : {&m->xb, &m->mb, &m->dv, &m->df, &m->da})
+    for (Buf& b : *v) b.release();
   m->ov.release();
   m->of.release();
+  m->oa.release();
   for (tsdbhip_ctx* s : m->subs) tsdbhip_destroy(s);
   if (m->root) tsdbhip_destroy(m->root);
   delete m;
@@ -1092,11 +1249,11 @@ extern "C" int tsdbhip_init_devices(const int* devices, int n_devices, int trans
     if (!rc) {
       ctx_set_none_orig(s, true);
       m->subs.push_back(s);
-      m->xb.push_back(Buf{devices[d]});
+      for (auto* v : {&m->xb, &m->mb, &m->dv, &m->df, &m->da}) v->push_back(Buf{devices[d]});
     }
   }
   if (!rc) rc = tsdbhip_init(devices[0], &m->root);
-  m->gb.dev = m->ov.dev = m->of.dev = devices[0];
+  m->ov.dev = m->of.dev = m->oa.dev = devices[0];
   // direct peer access between distinct devices (xGMI): peer copies and RCCL's P2P path use it
   if (!rc && distinct)
     for (int a = 0; a < n_devices; a++)

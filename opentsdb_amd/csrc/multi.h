@@ -28,6 +28,15 @@ int md_sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, int64_t ext
                   int64_t* K, uint8_t* uni, uint32_t* act);
 int md_sel_select(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, const double* vals, const int64_t* counts,
                   const uint8_t* uni, double** out_val, uint8_t** out_flag);
+// owner-routed partials (decomposable group-by over series shards): a partials buffer's part
+// offsets, and the owner's fold of a straddling group + finalisation of its groups
+// a straddling group's K-slot state as one device sends it to the owner:
+// [a K f64 | b K f64 | n K u32 | f K u32 | act u32], 16-byte aligned
+inline int64_t mini_state_stride(int64_t K) { return ((K * 24 + 4) + 15) & ~(int64_t)15; }
+void partials_offsets(int64_t G, int64_t K, int64_t* off_b, int64_t* off_n, int64_t* off_f, int64_t* off_act,
+                      int64_t* bytes);
+int md_partials_finish(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, unsigned char* state, int64_t g_fold,
+                       const unsigned char* mini, int n_mini, double* out_val, uint8_t* out_flag, uint32_t* out_act);
 // multi.cpp
 int md_load(tsdbhip_ctx* c, const tsdbhip_batch* b);
 int md_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp);

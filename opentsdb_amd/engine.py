@@ -26,7 +26,7 @@ EXPORTS = [
     "tsdbhip_parse_duration", "tsdbhip_parse_downsample", "tsdbhip_scan_bounds", "tsdbhip_init",
     "tsdbhip_destroy", "tsdbhip_load", "tsdbhip_synth", "tsdbhip_batch_sizes", "tsdbhip_batch_download",
     "tsdbhip_run", "tsdbhip_result_free", "tsdbhip_last_timing", "tsdbhip_partials_layout_get",
-    "tsdbhip_run_partials", "tsdbhip_finalize", "tsdbhip_sync", "tsdbhip_rollup_interval_parse",
+    "tsdbhip_run_partials", "tsdbhip_run_partials_multi", "tsdbhip_finalize", "tsdbhip_sync", "tsdbhip_rollup_interval_parse",
     "tsdbhip_rollup_basetime", "tsdbhip_rollup_qualifier", "tsdbhip_rollup_run", "tsdbhip_rollup_download",
     "tsdbhip_sel_layout", "tsdbhip_sel_run_values", "tsdbhip_sel_select", "tsdbhip_assemble", "tsdbhip_run_multi",
     "tsdbhip_debug_rows", "tsdbhip_shard_bounds", "tsdbhip_load_shard", "tsdbhip_synth_shard",
@@ -119,6 +119,7 @@ def lib():
         L.tsdbhip_last_timing.argtypes = [vp, C.POINTER(abi.Timing)]
         L.tsdbhip_partials_layout_get.argtypes = [vp, C.POINTER(abi.Query), C.c_int64, C.POINTER(abi.PartialsLayout)]
         L.tsdbhip_run_partials.argtypes = [vp, C.POINTER(abi.Query), C.c_int64, C.c_void_p]
+        L.tsdbhip_run_partials_multi.argtypes = [vp, C.POINTER(abi.Query), C.c_int, C.c_int64, C.c_void_p]
         L.tsdbhip_finalize.argtypes = [vp, C.POINTER(abi.Query), C.c_int64, C.c_void_p, C.c_int,
                                        C.POINTER(C.POINTER(abi.Result))]
         L.tsdbhip_sync.argtypes = [vp]
@@ -470,6 +471,13 @@ class Engine:
     def run_partials(self, q: abi.Query, n_groups_global: int, ptr: int):
         """This shard's per-(group, slot) partial states into `ptr` (device or host memory)."""
         _check(lib().tsdbhip_run_partials(self.ctx, C.byref(q), n_groups_global, C.c_void_p(ptr)))
+
+    def run_partials_multi(self, queries, n_groups_global: int, ptr: int):
+        """Partial states of several queries sharing the downsampling, from one fused pass: query
+        i's buffer at ptr + i * partials_layout(queries[i]).bytes."""
+        n = len(queries)
+        arr = (abi.Query * n)(*queries)
+        _check(lib().tsdbhip_run_partials_multi(self.ctx, arr, n, n_groups_global, C.c_void_p(ptr)))
 
     def finalize(self, q: abi.Query, n_groups_global: int, ptr: int, n_ranks: int):
         """Rank-ordered merge of n_ranks gathered partial buffers at `ptr` -> groups."""

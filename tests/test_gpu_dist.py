@@ -58,6 +58,30 @@ def test_sharded_equals_oracle(engines, batch, world, agg):
     assert_groups_match(run_sharded(engines, batch, q, world), O.run_query(batch, q), agg, ctx=f"{agg} x{world}")
 
 
+@pytest.mark.parametrize("world", [1, 3])
+@pytest.mark.parametrize("ds_ms", [60000, 600000])
+def test_run_partials_multi_equals_separate(engines, batch, world, ds_ms):
+    """tsdbhip_run_partials_multi: the shard's partial states of six queries from one fused pass,
+    byte for byte those of six tsdbhip_run_partials calls; a mix the fused pass does not take
+    (first, a rate) runs query by query with the same bytes."""
+    G = dist.n_groups_of(batch)
+    mixes = [["sum", "avg", "min", "max", "count", "dev"], ["sum", "first", "dev"]]
+    for aggs in mixes:
+        qs = [abi.new_query(T0, T0 + 3599, a, ds_function=abi.AGG["avg"], ds_interval_ms=ds_ms) for a in aggs]
+        for r in range(world):
+            e = engines[r]
+            e.load(dist.shard_batch(batch, r, world))
+            nb = int(e.partials_layout(qs[0], G).bytes)
+            sep = np.zeros(nb * len(qs), np.uint8)
+            for i, q in enumerate(qs):
+                e.run_partials(q, G, sep.ctypes.data + i * nb)
+            fused = np.full(nb * len(qs), 0xAB, np.uint8)
+            e.run_partials_multi(qs, G, fused.ctypes.data)
+            if aggs == mixes[0]:
+                assert e.timing().fused_queries == len(qs)
+            np.testing.assert_array_equal(fused, sep, err_msg=f"{aggs} rank {r}/{world}")
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_sharded_fill_rate_all(engines, batch, world):
     cases = [

@@ -118,6 +118,41 @@ def test_config3_full_size(eng):
             check_groups(ordered, want, a, C3_GROUPS, tol=0.0, ctx="config3 ordered sum (bit-exact)")
 
 
+# ---- config 3's day on one GPU of eight: 1.25M series x 8640 dp, 1000 groups ------------------
+def test_config3_day_shard_full_size(eng):
+    """The per-GPU workload of strong-scaled config 3 (bench.py config3_strong at 8 GPUs): 1.25M
+    series x 1 day @10 s kept as hour rows (54.6 GB), int/float alternating, 1000 groups.
+    {sum,avg,min,max,count,dev}:1m-avg take k_hwin (K = 1440 slots, window by window), the fused
+    run_multi takes its MULTI variant and must equal the separate queries bit for bit;
+    sum:10m-avg and sum:1h-avg take k_rows.  A strided slice of whole groups against the oracle."""
+    eng.synth(1_250_000, T0, 8640, 10000, 2, 1000, 30000, 0x5EED)
+    end = T0 + 86400 - 1
+    aggs = ["sum", "avg", "min", "max", "count", "dev"]
+    got = {}
+    for a in aggs:
+        got[a] = eng.run(dsq(a, "1m-avg", end))
+        t = eng.timing()
+        assert t.datapoints == 1_250_000 * 8640 and t.redo_tiles == 0 and t.fast_ms > 0, (a, t.redo_tiles)
+    multi = eng.run_multi([dsq(a, "1m-avg", end) for a in aggs])
+    assert eng.timing().fused_queries == len(aggs)   # one k_hwin MULTI pass
+    for a, m in zip(aggs, multi):
+        check_groups(m, got[a], a, sorted(set(r[0] for r in got[a])), tol=0.0, ctx=f"day run_multi {a} vs own pass")
+    for spec in ("10m-avg", "1h-avg"):
+        got["sum:" + spec] = eng.run(dsq("sum", spec, end))
+        assert eng.timing().redo_tiles == 0
+    host = group_slice(eng, C3_GROUPS)
+    assert host.n_series == 1250 * len(C3_GROUPS)
+    for a in aggs:
+        want = O.run_query(host, dsq(a, "1m-avg", end), threads=16)
+        assert all(len(w[1]) == 1440 for w in want)
+        check_groups(got[a], want, a, C3_GROUPS, tol=0.0 if a in ("min", "max", "count") else None,
+                     ctx=f"config3 day {a}")
+    for spec, k in (("10m-avg", 144), ("1h-avg", 24)):
+        want = O.run_query(host, dsq("sum", spec, end), threads=16)
+        assert all(len(w[1]) == k for w in want)
+        check_groups(got["sum:" + spec], want, "sum", C3_GROUPS, ctx=f"config3 day sum:{spec}")
+
+
 # ---- config 4: 100k jittered counters x 1 h, 64 groups --------------------------------------
 def test_config4_full_size(eng):
     b = synth.generate_counters(100_000, T0, 360, n_groups=64, seed=0x5EED)

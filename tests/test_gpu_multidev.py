@@ -147,7 +147,8 @@ def test_series_shards(batch, single, world):
                 k = 60
                 assert 0 < moved < batch.n_series * k * 8 / 2, (n, moved)
         e.run(QUERIES[0][1])
-        assert e.timing().exchange_ms > 0   # the gather + merge of the partial states
+        t = e.timing()
+        assert t.exchange_ms > 0 and t.devices_ms > 0   # the owner-routed exchange, the devices' passes
         per, ranks, _ = e.md_stats()
         assert len(per) == world and ranks == 0 and sum(t.datapoints for t in per) == e.timing().datapoints
     finally:
@@ -265,6 +266,68 @@ def test_run_multi_fused_on_every_device(batch, single):
         assert e.timing().fused_queries == fused_one
     finally:
         e.close()
+
+
+MULTI_AGGS = ["sum", "avg", "min", "max", "count", "dev"]
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_series_shards_run_multi_fused(batch, single, world):
+    """tsdbhip_run_multi on series shards: one fused pass per device (tsdbhip_run_partials_multi)
+    and one owner-routed exchange for all the queries; each result as the one-GPU run_multi's
+    (the oracle's tolerance: float sums associate per device) and bit for bit for min / max /
+    count.  The stage times of the call add up to its wall time."""
+    one, _ = single
+    qs = [q_ds(a, "avg") for a in MULTI_AGGS]
+    want = one.run_multi(qs)
+    e = md_engine([0] * world, E.SHARD_SERIES, batch)
+    try:
+        got = e.run_multi(qs)
+        t = e.timing()
+        assert t.fused_queries == len(qs)
+        for a, g, w in zip(MULTI_AGGS, got, want):
+            assert_groups_match(g, w, a, tol=0.0 if a in ("min", "max", "count") else None, ctx=f"x{world} {a}")
+            assert_groups_match(g, O.run_query(batch, q_ds(a, "avg")), a, ctx=f"x{world} {a} oracle")
+        stages = t.devices_ms + t.xfer_ms + t.select_ms + t.assemble_ms
+        assert 0 < stages <= t.total_ms * 1.001 and stages >= 0.5 * t.total_ms, (stages, t.total_ms)
+        assert abs(t.exchange_ms - (t.xfer_ms + t.select_ms + t.assemble_ms)) < 1e-9
+        # owner routing: the straddling groups' K-slot states and the owners' dense rows move, not
+        # every device's G x K partial states
+        _, _, moved = e.md_stats()
+        G, K = 7, 60
+        assert 0 < moved < len(qs) * (world * G * K * 24) / 2, moved
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_series_shards_day_of_minute_buckets(world):
+    """A day of 1m buckets (K = 1440, k_hwin) on series shards: single queries and the fused
+    run_multi (k_hwin's MULTI variant on every device) against one GPU."""
+    args = (2400, T0, 8640, 10000, 2, 13, 30000)
+    one = E.Engine(0)
+    e = E.Engine(devices=[0] * world)
+    try:
+        one.synth(*args)
+        e.shard_mode(E.SHARD_SERIES)
+        e.synth(*args)
+        qs = [abi.new_query(T0, T0 + 86399, a, ds_function=abi.AGG["avg"], ds_interval_ms=60000) for a in MULTI_AGGS]
+        want = [one.run(q) for q in qs]
+        assert all(len(w[0][1]) == 1440 for w in want)
+        got = e.run_multi(qs)
+        assert e.timing().fused_queries == len(qs)
+        for a, g, w in zip(MULTI_AGGS, got, want):
+            assert_groups_match(g, w, a, tol=0.0 if a in ("min", "max", "count") else None, ctx=f"day x{world} {a}")
+        for a, q, w in zip(MULTI_AGGS, qs, want):
+            assert_groups_match(e.run(q), w, a, tol=0.0 if a in ("min", "max", "count") else None,
+                                ctx=f"day x{world} {a} single")
+        fused_one = one.run_multi(qs)
+        assert one.timing().fused_queries == len(qs)
+        for a, g, w in zip(MULTI_AGGS, fused_one, want):
+            bit_same(g, w, f"one GPU day run_multi {a}")
+    finally:
+        e.close()
+        one.close()
 
 
 def test_store_bound_entry_points_refuse(batch):

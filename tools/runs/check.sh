@@ -9,7 +9,7 @@ out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
 sel=("$@"); [ ${#sel[@]} -eq 0 ] && sel=(tests)
-timeout -k 10 ${PYTEST_LIMIT:-1500} python -u -m pytest "${sel[@]}" -m gpu -x -q --timeout 400 --timeout-method thread \
+timeout -k 10 ${PYTEST_LIMIT:-1500} python -u -m pytest "${sel[@]}" -m gpu -x -q --timeout ${TEST_TIMEOUT:-150} --timeout-method thread \
   > $out/pytest_gpu.log 2>&1
 rc=$?; tail -3 $out/pytest_gpu.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error" $out/pytest_gpu.log | head -20; exit $rc; }
 if [ "${BENCH:-0}" = 1 ]; then
