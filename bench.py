@@ -329,10 +329,24 @@ def md_engine(args, n):
     return eng, note
 
 
+STAGES = ("devices_ms", "xfer_ms", "select_ms", "assemble_ms")
+
+
 def md_step_stats(eng, steps_stats):
     per, ranks, moved = eng.md_stats()
-    steps_stats.append(([(t.fast_ms, t.decode_downsample_ms, t.datapoints, t.bytes) for t in per], moved))
+    tm = eng.timing()
+    steps_stats.append(([(t.fast_ms, t.decode_downsample_ms, t.datapoints, t.bytes) for t in per], moved,
+                        {k: getattr(tm, k) for k in STAGES + ("total_ms",)}))
     return ranks
+
+
+def md_stages(stats):
+    """Mean per-stage host wall times of the timed calls (tsdbhip_timing, multi-device context):
+    the devices' own passes, device-to-device moves, the owners' merge / selection, the result on
+    the host -- and their sum against the call's wall time."""
+    out = {k: sum(s[2][k] for s in stats) / len(stats) for k in STAGES + ("total_ms",)}
+    out["sum_of_stages_ms"] = sum(out[k] for k in STAGES)
+    return out
 
 
 def md_config3(args, n):
@@ -378,9 +392,13 @@ def md_config3(args, n):
             fast = [max(s[0][d][0] for s in stats) for d in range(n)]
             out[name] = {"ms_per_step": ms, "value": len(qs) * tm.datapoints / (ms / 1000),
                          "unit": "datapoints/s" + (f" (x{len(qs)} queries)" if len(qs) > 1 else ""),
+                         "fused_queries": int(tm.fused_queries), "stages": md_stages(stats),
                          "exchange_ms": tm.exchange_ms, "xfer_bytes": stats[-1][1],
                          "device_kernel_ms_max": [round(x, 4) for x in fast],
                          "hbm_frac_step_per_gpu": tm.bytes / n / (ms / 1000) / 1e9 / BYTES_PEAK_GBS}
+        m5, s1 = out.get("multi_avg_min_max_count_dev", {}), out.get("sum", {})
+        if "ms_per_step" in m5 and "ms_per_step" in s1:
+            out["multi_ratio_to_sum_step"] = m5["ms_per_step"] / s1["ms_per_step"]
         return out
     finally:
         eng.close()
@@ -483,6 +501,7 @@ def main_md(args):
         "transport_note": note,
         "rccl_ranks": ranks,
         "exchange_ms": tm.exchange_ms,
+        "stages": md_stages(stats),
         "xfer_bytes_per_step": stats[-1][1],
         "config": {
             "workload": workload_label(args),

@@ -1,0 +1,36 @@
+#!/bin/bash
+# Measurement pass: bash tools/runs/measure.sh TAG [c3day] [md] [pmc_hwin]
+#   c3day     tools/c3day_bench.py --multi (config 3's day on one GPU's share)  -> c3day.jsonl
+#   md        bench.py --gpus 2 / 4 over repeated device 0 (the multi-device context rehearsal,
+#             config 2 weak + config 3 strong at 1M series)                     -> md2.jsonl, md4.jsonl
+#   pmc_hwin  rocprofv3 PMC passes over the day's sum:1m-avg (k_hwin)           -> pmc_hwin/summary.txt
+# Every GPU step under its own timeout; the first failure ends the pass.
+set -o pipefail
+tag=$1; shift
+out=gpurun_out/$tag
+mkdir -p $out
+export TMPDIR=/tmp
+for step in "$@"; do
+  case $step in
+    c3day)
+      timeout -k 10 400 python3 -u tools/c3day_bench.py --multi > $out/c3day.jsonl 2> $out/c3day.err \
+        || { tail -20 $out/c3day.err; exit 1; }
+      cat $out/c3day.jsonl ;;
+    md)
+      for n in 2 4; do
+        devs=$(python3 -c "print(','.join(['0']*$n))")
+        TSDBHIP_BENCH_DEVICES=$devs timeout -k 10 600 python3 -u bench.py --gpus $n --steps 5 --warmup 2 \
+          --c3-series 1000000 --no-cpu-baseline --no-pmc > $out/md$n.jsonl 2> $out/md$n.err \
+          || { tail -20 $out/md$n.err; exit 1; }
+        python3 -c "
+import json
+d=json.loads(open('$out/md$n.jsonl').read().strip().splitlines()[-1])
+print($n, 'value', d['value'], 'ms', d['ms_per_step'], 'stages', d.get('stages'))
+for k,v in d['extra']['config3_strong'].items():
+    if isinstance(v, dict): print('  ', k, json.dumps(v))"
+      done ;;
+    pmc_hwin)
+      bash tools/pmc_run.sh ${tag}_hwin python3 tools/c3day_bench.py --only 1m --steps 1 || exit $?
+      python3 tools/pmc_summary.py gpurun_out/pmc_${tag}_hwin k_hwin | tee $out/pmc_hwin_summary.txt ;;
+  esac
+done
