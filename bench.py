@@ -335,8 +335,9 @@ STAGES = ("devices_ms", "xfer_ms", "select_ms", "assemble_ms")
 def md_step_stats(eng, steps_stats):
     per, ranks, moved = eng.md_stats()
     tm = eng.timing()
-    steps_stats.append(([(t.fast_ms, t.decode_downsample_ms, t.datapoints, t.bytes) for t in per], moved,
-                        {k: getattr(tm, k) for k in STAGES + ("total_ms",)}))
+    st = {k: getattr(tm, k) for k in STAGES + ("total_ms",)}
+    st["c_call_ms"] = getattr(eng, "last_call_ms", 0.0)
+    steps_stats.append(([(t.fast_ms, t.decode_downsample_ms, t.datapoints, t.bytes) for t in per], moved, st))
     return ranks
 
 
@@ -344,7 +345,7 @@ def md_stages(stats):
     """Mean per-stage host wall times of the timed calls (tsdbhip_timing, multi-device context):
     the devices' own passes, device-to-device moves, the owners' merge / selection, the result on
     the host -- and their sum against the call's wall time."""
-    out = {k: sum(s[2][k] for s in stats) / len(stats) for k in STAGES + ("total_ms",)}
+    out = {k: sum(s[2][k] for s in stats) / len(stats) for k in STAGES + ("total_ms", "c_call_ms")}
     out["sum_of_stages_ms"] = sum(out[k] for k in STAGES)
     return out
 

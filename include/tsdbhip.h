@@ -572,8 +572,10 @@ typedef struct {
 /* The query's start / end, aggregator and downsampling (ds_function is ignored: histograms are
  * always summed; -1 = no downsampling) as for tsdbhip_run; pct[n_pct] the percentiles
  * (TsdbQuery.setPercentiles, List<Float>).  Calendar downsampling (UTC, ds_tz, per-span anchors)
- * included.  NOT_IMPLEMENTED: spans whose datapoints are not in time order, more than 32 GB of
- * per-point state, more than 32768 distinct buckets. */
+ * included.  Raw group-by over spans whose datapoints are not in time order (a row mixing second
+ * and millisecond qualifiers is iterated in column order) follows HistogramAggregationIterator.next's
+ * greedy walk (:240-292): repeated and receding timestamps, points merged only when current together.
+ * NOT_IMPLEMENTED: more than 32 GB of per-point state, more than 32768 distinct buckets. */
 int tsdbhip_hist_run(tsdbhip_ctx* ctx, const tsdbhip_query* q, int n_pct, const float* pct, int show_buckets,
                      tsdbhip_hist_result** out);
 /* The same over every row of the store with the HistogramSpanGroup bounds given directly (ms):

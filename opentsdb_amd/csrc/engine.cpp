@@ -2126,9 +2126,13 @@ static int synth_impl(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp, int64_t p0, 
   c->n_rows = S * R;
   c->n_groups = G;
   // qualifier offsets (identical layout for every series)
+  // row starts 16-byte aligned (TSDBHIP_ROW_ALIGN: another power of two >= 16, layout experiments)
+  int64_t ra = 16;
+  if (const char* e = std::getenv("TSDBHIP_ROW_ALIGN")) ra = std::max<int64_t>(16, std::atoll(e));
+  auto alignr = [ra](int64_t x) { return (x + ra - 1) / ra * ra; };
   std::vector<int64_t> rq(R);
   int64_t QS = 0;
-  for (int64_t h = 0; h < R; h++) { rq[h] = QS; QS += align16((int64_t)rn[h] * qw); }
+  for (int64_t h = 0; h < R; h++) { rq[h] = QS; QS += alignr((int64_t)rn[h] * qw); }
   DevBuf d_k0, d_rn, d_rbase, d_goff, d_vbytes;
   HIP_OK(d_k0.ensure(R * 8));
   HIP_OK(d_rn.ensure(R * 4));
@@ -2170,7 +2174,7 @@ static int synth_impl(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp, int64_t p0, 
       d.voff = vtot;
       d.vlen = vbytes[s * R + h];
       d.flags = h == 0 ? ROW_SFIRST : 0;
-      vtot += align16(d.vlen);
+      vtot += alignr(d.vlen);
     }
   }
   c->qual_bytes = (uint64_t)(S * QS);
@@ -2791,7 +2795,7 @@ bool seq_rows_ok(tsdbhip_ctx* c, const Plan& P) {
 // k_hwin takes the query: a fixed grid of K > 64 buckets dividing the hour with slot 0 on an
 // hour (every hour row in one window of W = 1 h / interval <= 64 slots), no rate, an order-free
 // function, and every tile of one streaming class with one-chunk rows.
-int hwin_slots(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P) {
+int hwin_slots(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, bool for_multi = false) {
   if (const char* e = std::getenv("TSDBHIP_HWIN")) if (e[0] == '0') return 0;
   // (fill policies need every participating series' fill values in windows where it has no row:
   // left to the dense split)
@@ -2808,8 +2812,10 @@ int hwin_slots(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P) {
   const char* env = std::getenv("TSDBHIP_FAST");
   if (env && env[0] == '0') return 0;
   // only where the one-pass streaming kernels' slot LDS does not fit (the dense split's case):
-  // with a handful of slots a window (10m: 6) k_rows' fused pass is faster (profiles/r04x)
-  if (fast_wave_lds(P.K, false, true) <= 32 * 1024) return 0;
+  // with a handful of slots a window (10m: 6) k_rows' fused pass is faster (profiles/r04x).  The
+  // fused multi-aggregator pass has no K > 64 variant of those kernels: k_hwin takes every K > 64
+  // that tiles the hour.
+  if (!(for_multi || P.multi) && fast_wave_lds(P.K, false, true) <= 32 * 1024) return 0;
   return (int)(3600000 / P.I);
 }
 
@@ -3107,6 +3113,15 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       fp.oneb = P.I >= 3600000 && !(oenv && oenv[0] == '0') ? 1 : 0;   // (an hour row's chunk in one bucket)
       fp.wave_lds = (int32_t)(shortk == 3 ? fast_wave_lds(hwin, false, false) : fast_lds_of(q, P));
       fp.win_w = hwin;
+      if (shortk == 3) {
+        // k_hwin: one work item a (tile, hour window) -- a tile's 24 windows as one item left the
+        // last round of the launch mostly idle; items of fewer windows measured 13.6 (whole tiles)
+        // -> 12.6 (4) -> 12.2 (6) -> 11.9 (12) -> 11.4 ms (24) on config 3's day shard
+        // (profiles/r05h/split*.jsonl).  TSDBHIP_HWIN_SPLIT: items a tile.
+        const int nw = (int)((K + hwin - 1) / hwin);
+        const char* se = std::getenv("TSDBHIP_HWIN_SPLIT");
+        fp.win_split = se ? std::max(1, std::min(nw, std::atoi(se))) : nw;
+      }
       {
         const char* e6 = std::getenv("TSDBHIP_SHORT6");
         fp.short6 = ((shortk == 1 || shortk == 3) && !(e6 && e6[0] == '0')) ? 1 : 0;
@@ -4585,7 +4600,7 @@ int fused_pass(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, Plan& P) {
   if (rc) return rc;
   if (P.raw || P.none || P.gsel || P.f == F_SEL || !c->tl_other.empty()) return 1;
   // K <= 64: k_short / k_rows / k_fast (KR 2); K > 64 (a day of 1m buckets): k_hwin's MULTI variant
-  if (!hwin_slots(c, &q0, P) && (P.K > 64 || !fast_path_ok(c, &q0, P))) return 1;
+  if (!hwin_slots(c, &q0, P, true) && (P.K > 64 || !fast_path_ok(c, &q0, P))) return 1;
   for (int cls = 0; cls < 2; cls++) {
     if (c->tl[cls][0].empty() && c->tl[cls][1].empty() && c->tl[cls][2].empty()) continue;
     const int qw = cls ? c->fast_qw2 : c->fast_qw, vl = cls ? c->fast_vl2 : c->fast_vl;
@@ -4623,9 +4638,11 @@ Partials multi_view(tsdbhip_ctx* c, int agg) {
 // (rate, other aggregators, flags, a row class the streaming kernels do not take) or when a
 // tile broke a streaming premise at run time: the caller then runs the queries one by one.
 int run_multi_fused(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_result** outs) {
+  PhaseTrace tr("run_multi_fused");
   Plan P;
   int rc = fused_pass(c, qs, n, P);
   if (rc) return rc;
+  tr.mark("fused pass (synchronised)");
   const int64_t G = c->n_groups, K = P.K;
   // one k_reduce per query over its view of the fused partials, into its own output rows
   const int64_t gk = std::max<int64_t>(1, G * K);
@@ -4648,25 +4665,29 @@ int run_multi_fused(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_resu
     HIP_OK(launch_reduce(rp, c->stream));
   }
   HIP_OK(hipEventRecord(c->ev[2], c->stream));
-  // every query's dense rows in one copy each (collect() per query would sync n times)
-  std::vector<double> val(gk * n);
-  std::vector<uint8_t> flag(gk * n);
+  // every query's dense rows in one copy each (collect() per query would sync n times), into the
+  // context's page-locked staging (a day of 1m buckets over 1000 groups: 13 MB a query)
+  HIP_OK(c->h_stage.ensure(std::max<int64_t>(16, gk * 9 * n + 16)));
+  double* val = reinterpret_cast<double*>(c->h_stage.p);
+  uint8_t* flag = reinterpret_cast<uint8_t*>(c->h_stage.p) + gk * 8 * n;
   std::vector<uint32_t> act(std::max<int64_t>(1, G));
   int32_t err = 0, redo_n = 0;
-  HIP_OK(hipMemcpyAsync(val.data(), c->out_val.p, gk * n * 8, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipMemcpyAsync(flag.data(), c->out_flag.p, gk * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipMemcpyAsync(val, c->out_val.p, gk * n * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipMemcpyAsync(flag, c->out_flag.p, gk * n, hipMemcpyDeviceToHost, c->stream));
   if (G) HIP_OK(hipMemcpyAsync(act.data(), c->gact.p, G * 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipMemcpyAsync(&redo_n, c->redo_final, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
+  tr.mark("reduce x n + d2h");
   c->fused_n = n;
   record_timing(c, P, redo_n);
   c->fused_n = 0;
   if (err) return fail(err, "error raised by the device path");
   for (int i = 0; i < n; i++) {
-    rc = assemble(c, &qs[i], plans[i], G, val.data() + i * gk, flag.data() + i * gk, act, &outs[i]);
+    rc = assemble(c, &qs[i], plans[i], G, val + i * gk, flag + i * gk, act, &outs[i]);
     if (rc) return rc;
   }
+  tr.mark("assemble x n");
   return 0;
 }
 

@@ -147,6 +147,7 @@ struct GridParams {
   int32_t shortk;        // k_fast launch runs k_short (1: one row per series) / k_rows (2: rows <= CH)
   int32_t oneb;          // streaming kernels: buckets of an hour or more -- try the one-bucket chunk fold
   int32_t win_w;         // k_hwin: slots a window (3600 s / interval; windows start on slot multiples of it)
+  int32_t win_split;     // k_hwin: work items a tile (each a contiguous range of its windows); 0/1 = whole tiles
   int32_t short6;        // k_short, vle class: 6 datapoints a lane (rows of <= 384 points)
   // percentile / median as the group-by aggregator (k_emit_vals, k_sel_seg): the value of
   // span i of group g at slot k goes to sel_vals[(gsp[g] + i) * K + k] ([series][slot], the

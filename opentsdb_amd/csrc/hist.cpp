@@ -77,6 +77,7 @@ struct HistStore {
   Buf q_rlo, q_rhi, q_out, q_slot, q_key, q_key2, q_pos, q_pos2, q_head, q_incl, q_point, q_ptts, q_ptgrp;
   Buf q_vlen, q_voff, q_vpos;   // windowed accumulation: the spans' positions in output-group order
   Buf q_caltab, q_spcal;         // calendar downsampling: boundary runs per span anchor
+  Buf q_gsp, q_spq, q_spts;      // greedy walk over spans out of time order (k_hist_walk)
   Buf acc, pres, pkind, flag, ptout, err, pct;
   Buf o_ts, o_grp, o_kind, o_pct, o_cnt, o_pres;
   void* tmp = nullptr;
@@ -84,7 +85,7 @@ struct HistStore {
   void release() {
     for (Buf* b : {&val, &voff, &codec, &status, &hkey, &hcount, &hidx, &dlo, &dup, &lkey, &lidx, &lkey2, &lidx2, &pos_cell, &pos_ts, &pos_kind,
                    &row_pos, &col_lid, &lay_col, &lay_off, &lay_di, &q_rlo, &q_rhi, &q_out, &q_slot, &q_key, &q_key2, &q_pos, &q_pos2, &q_head, &q_incl,
-                   &q_point, &q_ptts, &q_ptgrp, &q_vlen, &q_voff, &q_vpos, &q_caltab, &q_spcal, &acc, &pres, &pkind, &flag, &ptout, &err, &pct, &o_ts, &o_grp,
+                   &q_point, &q_ptts, &q_ptgrp, &q_vlen, &q_voff, &q_vpos, &q_caltab, &q_spcal, &q_gsp, &q_spq, &q_spts, &acc, &pres, &pkind, &flag, &ptout, &err, &pct, &o_ts, &o_grp,
                    &o_kind, &o_pct, &o_cnt, &o_pres})
       b->release();
     if (tmp) (void)hipFree(tmp);
@@ -563,6 +564,23 @@ int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end,
   int32_t err[2] = {0, 0};
   HOK(hipMemcpyAsync(err, S->err.p, 8, hipMemcpyDeviceToHost, st));
   HOK(hipStreamSynchronize(st));
+  if (ds == 0 && err[0] == TSDB_E_NOT_IMPLEMENTED && err[1] == 3 /* WHY_UNSORTED */) {
+    // a span out of time order: the aggregation iterator's greedy walk labels the points instead
+    // of the union of timestamps (k_hist_walk); spans of a group are consecutive in sp_*
+    std::vector<int64_t> gsp(G + 1, 0);
+    for (int32_t o : sout) gsp[o + 1]++;
+    for (int64_t g = 0; g < G; g++) gsp[g + 1] += gsp[g];
+    HOK(S->q_gsp.ensure((G + 1) * 8));
+    HOK(S->q_spq.ensure(nsp * 8 + 8));
+    HOK(S->q_spts.ensure(nsp * 8 + 8));
+    HOK(hipMemcpyAsync(S->q_gsp.p, gsp.data(), (G + 1) * 8, hipMemcpyHostToDevice, st));
+    HOK(hipMemsetAsync(S->q_key.p, 0xFF, NP * 8 + 8, st));
+    HOK(hipMemsetAsync(S->err.p, 0, 16, st));
+    HOK(hist_walk(p, S->q_gsp.as<int64_t>(), G, S->q_spq.as<int64_t>(), S->q_spts.as<int64_t>(), st));
+    HOK(hipMemcpyAsync(err, S->err.p, 8, hipMemcpyDeviceToHost, st));
+    HOK(hipStreamSynchronize(st));   // (gsp leaves scope)
+    p.greedy = 1;
+  }
   static const char* const WHY[] = {"", "invalid seek timestamp",
                                     "a histogram downsampling function other than sum aggregates two datapoints "
                                     "(HistogramAggregation null)",

@@ -64,7 +64,9 @@ struct HistQueryParams {
   int64_t cal_seek;          // calendar: HistogramDownsampler.seekInterval's target
   // outputs of k_hist_slots
   int32_t* pos_slot;         // [n_pos] slot (dense) or -1
-  int64_t* pos_key;          // [n_pos] sparse mode: (group << 42 | ts - start) or -1
+  int64_t* pos_key;          // [n_pos] sparse mode: (group << 42 | ts - start) or -1; after the
+                             // greedy walk (spans out of time order): (group << 42 | step)
+  int32_t greedy;            // pos_key holds walk steps: a point's timestamp is its positions' pos_ts
   int32_t* err;              // [2]: first error code, reason
   // accumulation ([point][C] u64) -- point = group * K + slot (dense) or a union index (sparse)
   const int32_t* pos_point;  // sparse mode: [n_pos] point of each position, -1 excluded (null: dense)
@@ -130,6 +132,9 @@ static constexpr int HIST_LAY_MAXB = 32;   // layouts of more buckets take the k
 hipError_t hist_flags(const HistQueryParams& p, uint32_t* flag, hipStream_t s);   // [n_points] 1 = emitted
 hipError_t hist_final(const HistQueryParams& p, hipStream_t s);
 hipError_t hist_scan(const uint32_t* flag, int64_t* out, int64_t n, void** tmp, size_t* tmp_bytes, hipStream_t s);
+// HistogramAggregationIterator.next()'s walk over raw spans some of which are out of time order
+// (one wave a group; span state in sp_q / sp_ts, [n_spans] scratch); gsp[G + 1]: the group's spans
+hipError_t hist_walk(const HistQueryParams& p, const int64_t* gsp, int64_t G, int64_t* sp_q, int64_t* sp_ts, hipStream_t s);
 hipError_t hist_sparse(const HistQueryParams& p, int64_t n_pos, uint64_t* key2, uint32_t* pos, uint32_t* pos2,
                        uint32_t* head, int64_t* incl, int64_t* pt_ts, int32_t* pt_group, int64_t* n_points,
                        void** tmp, size_t* tmp_bytes, hipStream_t s);

@@ -74,7 +74,7 @@ static hipError_t launch_fast_k(const GridParams& p, hipStream_t s) {
 template <int F, int QW, int VL>
 static hipError_t launch_fast_t(const GridParams& p, hipStream_t s) {
   if (p.shortk == 3) {   // k_hwin: K > 64 buckets tiling the hour, window by window
-    const int64_t nl = p.n_launch > 0 ? p.n_launch : p.n_tiles;
+    const int64_t nl = (p.n_launch > 0 ? p.n_launch : p.n_tiles) * std::max(1, (int)p.win_split);
     const int64_t blocks = (nl + p.waves - 1) / p.waves;
     const size_t lds = (size_t)p.wave_lds * p.waves;
     if constexpr (QW == 2 && VL == 0) {

@@ -256,6 +256,64 @@ __global__ void k_hist_slots(HistQueryParams p) {
   }
 }
 
+// Raw group-by over spans some of which are out of time order (a row mixing second and
+// millisecond qualifiers is iterated in column order: HistogramRowSeq does not sort).
+// HistogramAggregationIterator (src/core/HistogramAggregationIterator.java:118-160 ctor, :240-292
+// next) is then a greedy walk, not the union of timestamps: each step takes the smallest current
+// timestamp t among the spans whose current one is neither 0 (endReached) nor past the end, sums
+// every span's current histogram at t (the first such span's value aggregated with the others in
+// span order -- integer bucket counts, order-free) and advances exactly those spans; a span can
+// come back below t later.  One wave a group: lane l holds spans l, l + 64, ...; a step is a wave
+// min, then the lanes holding it label their spans' current positions with the step and advance
+// them.  The ctor's rules: HistogramSpanGroup.add's [start, end] overlap (k_hist_slots), the seek
+// to the start, a first datapoint before the start ends the span.
+__global__ void k_hist_walk(HistQueryParams p, const int64_t* gsp, int64_t G, int64_t* sp_q, int64_t* sp_ts) {
+  const int64_t g = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (g >= G) return;
+  const int lane = __lane_id();
+  const int64_t a = gsp[g], b = gsp[g + 1];
+  // ctor: the first datapoint of every span (0 = ended)
+  for (int64_t s = a + lane; s < b; s += 64) {
+    int64_t ts = 0, q = 0;
+    const int64_t rlo = p.sp_rlo[s], rhi = p.sp_rhi[s];
+    const int64_t p0 = p.row_pos[rlo], p1 = p.row_pos[rhi];
+    if (p1 > p0) {
+      int64_t first = p.pos_ts[p0], last = p.pos_ts[p1 - 1];
+      if ((first & (int64_t)0xFFFFFFFF00000000LL) == 0) first *= 1000;
+      if ((last & (int64_t)0xFFFFFFFF00000000LL) == 0) last *= 1000;
+      if (first <= p.end && last >= p.start) {
+        q = span_seek(p, rlo, rhi, p.start);
+        if (q < p1 && p.pos_ts[q] >= p.start) ts = p.pos_ts[q];
+      }
+    }
+    sp_q[s] = q;
+    sp_ts[s] = ts;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __threadfence_block();
+  for (int64_t step = 0;; step++) {
+    int64_t m = INT64_MAX;
+    for (int64_t s = a + lane; s < b; s += 64) {
+      const int64_t t = sp_ts[s];
+      if (t != 0 && t <= p.end && t < m) m = t;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      const int64_t o = __shfl_xor(m, d);
+      m = o < m ? o : m;
+    }
+    if (m == INT64_MAX) break;
+    for (int64_t s = a + lane; s < b; s += 64) {
+      if (sp_ts[s] != m) continue;
+      const int64_t q = sp_q[s];
+      p.pos_key[q] = (g << 42) | step;
+      const int64_t p1 = p.row_pos[p.sp_rhi[s]];
+      sp_q[s] = q + 1;
+      sp_ts[s] = q + 1 < p1 ? p.pos_ts[q + 1] : 0;   // (a datapoint at 0 ends the span, as endReached)
+    }
+  }
+}
+
 // segmented (by equal address) inclusive scan over the wave (runs of equal addr are contiguous
 // lanes in the common case; equal addresses further apart only cost extra atomics); returns true
 // on the run's last lane
@@ -495,13 +553,14 @@ __global__ void k_hist_heads(const uint64_t* key, int64_t n, uint32_t* head) {
   head[i] = key[i] != ~0ull && (i == 0 || key[i] != key[i - 1]) ? 1u : 0u;
 }
 __global__ void k_hist_points(const uint64_t* key, const uint32_t* pos, int64_t n, const int64_t* incl,
-                              int64_t start, int32_t* pos_point, int64_t* pt_ts, int32_t* pt_group) {
+                              int64_t start, int32_t* pos_point, int64_t* pt_ts, int32_t* pt_group,
+                              const int64_t* greedy_ts) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || key[i] == ~0ull) return;
   const int64_t pt = incl[i + 1] - 1;   // inclusive count of heads up to i, minus one
   pos_point[pos[i]] = (int32_t)pt;
   if (i == 0 || key[i] != key[i - 1]) {
-    pt_ts[pt] = start + (int64_t)(key[i] & ((1ull << 42) - 1));
+    pt_ts[pt] = greedy_ts ? greedy_ts[pos[i]] : start + (int64_t)(key[i] & ((1ull << 42) - 1));
     pt_group[pt] = (int32_t)(key[i] >> 42);
   }
 }
@@ -970,7 +1029,7 @@ hipError_t hist_sparse(const HistQueryParams& p, int64_t n_pos, uint64_t* key2, 
   hipLaunchKernelGGL(k_hist_heads, dim3(nb), dim3(256), 0, s, key2, n_pos, head);
   if ((e = hist_scan(head, incl, n_pos, tmp, tmp_bytes, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_hist_points, dim3(nb), dim3(256), 0, s, key2, pos2, n_pos, incl, p.start,
-                     const_cast<int32_t*>(p.pos_point), pt_ts, pt_group);
+                     const_cast<int32_t*>(p.pos_point), pt_ts, pt_group, p.greedy ? p.pos_ts : nullptr);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if ((e = hipMemcpyAsync(n_points, incl + n_pos, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
   return hipStreamSynchronize(s);
@@ -979,6 +1038,11 @@ hipError_t hist_sparse(const HistQueryParams& p, int64_t n_pos, uint64_t* key2, 
 hipError_t hist_validate(const HistLoadParams& p, hipStream_t s) {
   if (p.n_cells <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_hist_validate, dim3((unsigned)((p.n_cells + 255) / 256)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+hipError_t hist_walk(const HistQueryParams& p, const int64_t* gsp, int64_t G, int64_t* sp_q, int64_t* sp_ts, hipStream_t s) {
+  if (G <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hist_walk, dim3((unsigned)((G + 3) / 4)), dim3(256), 0, s, p, gsp, G, sp_q, sp_ts);
   return hipGetLastError();
 }
 hipError_t hist_slots(const HistQueryParams& p, hipStream_t s) {

@@ -2474,7 +2474,12 @@ __global__ __launch_bounds__(256, MULTI ? SHORT_OCC2(VL) : SHORT_OCC(VL)) void k
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int64_t tile = (int64_t)blockIdx.x * p.waves + wave;
+  // a work item is a contiguous range of one tile's windows (p.win_split items a tile): the
+  // launch's last round of whole tiles left most of the GPU idle (a day: 24 windows a tile)
+  const int S = max(1, p.win_split);
+  const int64_t item = (int64_t)blockIdx.x * p.waves + wave;
+  int64_t tile = item / S;
+  const int part = (int)(item - tile * S);
   if (p.tile_list) {
     if (tile >= (int64_t)*p.tile_list_n) return;
     tile = p.tile_list[tile];
@@ -2483,6 +2488,7 @@ __global__ __launch_bounds__(256, MULTI ? SHORT_OCC2(VL) : SHORT_OCC(VL)) void k
   const int K = (int)p.K;
   const int W = p.win_w;
   const int NW = (K + W - 1) / W;
+  const int h0 = (int)((int64_t)part * NW / S), h1 = (int)((int64_t)(part + 1) * NW / S);
   const int64_t s0 = tbeg[tile];
   const int ns = (int)(tend[tile] - s0);
   if (ns > 64) {
@@ -2491,6 +2497,28 @@ __global__ __launch_bounds__(256, MULTI ? SHORT_OCC2(VL) : SHORT_OCC(VL)) void k
   }
   int64_t cur = lane < ns ? srp[s0 + lane] : 0;
   const int64_t end = lane < ns ? srp[s0 + lane + 1] : 0;
+  bool seen = false;   // the lane's series had a row in an earlier window (of this item or before it)
+  if (h0 > 0 && cur < end) {
+    // a later item: jump to the series' row of window h0 (one row an hour: first row + h0 - its
+    // window), kept when the row before the jump lies in an earlier window; else the window
+    // loop below walks the rows from the first
+    const RowDesc& x0 = rows[cur];
+    const int64_t b0 = (int64_t)x0.base;
+    const int64_t rel0 = p.unit_s ? b0 - p.B0n : b0 * 1000 - p.B0n;
+    if (b0 >= p.ss && b0 < p.se && rel0 >= 0) {
+      const FGeom g0 = fgeom(p, (uint32_t)b0);
+      const int w0 = g0.q0 / W;
+      const int64_t guess = cur + (h0 - w0);
+      if (g0.r0 == 0 && g0.q0 % W == 0 && w0 < h0 && guess <= end) {
+        const int64_t bp = (int64_t)rows[guess - 1].base;
+        const FGeom gp = fgeom(p, (uint32_t)bp);
+        if (bp < p.se && gp.q0 / W < h0) {
+          cur = guess;
+          seen = true;
+        }
+      }
+    }
+  }
   const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, W, false, false);
   for (int k = lane; k < W; k += 64) {
     L.acc[k] = fast_identity<F>();
@@ -2500,9 +2528,8 @@ __global__ __launch_bounds__(256, MULTI ? SHORT_OCC2(VL) : SHORT_OCC(VL)) void k
   rp_init(p.ga, RP);
   WAVE_SYNC();
   bool redo = false, any = false;
-  bool seen = false;   // the lane's series had a row in an earlier window
   const bool lerp = p.fill == TSDB_FILL_NONE;   // (the host routes fill policies elsewhere)
-  for (int h = 0; h < NW && !redo; h++) {
+  for (int h = h0; h < h1 && !redo; h++) {
     const int Wh = min(W, K - h * W);
     // the lane's row of window h: rows outside the scan range or before slot 0 are passed over
     bool has = false, bad = false;
@@ -2516,7 +2543,7 @@ __global__ __launch_bounds__(256, MULTI ? SHORT_OCC2(VL) : SHORT_OCC(VL)) void k
       const FGeom g = fgeom(p, (uint32_t)base);
       if (g.r0 != 0 || g.q0 % W != 0) { bad = true; break; }   // (host-checked alignment)
       const int wi = g.q0 / W;
-      if (wi < h) { cur++; continue; }
+      if (wi < h) { seen = true; cur++; continue; }   // (a row of a window before this item's)
       if (wi == h) {
         has = true;
         dq = x.qoff;

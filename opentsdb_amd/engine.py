@@ -399,7 +399,9 @@ class Engine:
         n = len(queries)
         arr = (abi.Query * n)(*queries)
         outs = (C.POINTER(abi.Result) * n)()
+        t = time.perf_counter()
         _check(lib().tsdbhip_run_multi(self.ctx, arr, n, outs))
+        self.last_call_ms = (time.perf_counter() - t) * 1000.0   # the C call alone (host wall time)
         return [abi.result_to_groups(outs[i].contents, owner=_ResultOwner(outs[i])) for i in range(n)]
 
     def run_rollup_batch(self, rb: abi.HostRollupBatch, q: abi.Query):

@@ -141,10 +141,10 @@ def test_gpu_duplicate_row_keys_merge(eng):
         run_both(eng, hb, U.query(T0, T0 + 7200, "sum", ds), [50.0], True)
 
 
-def test_gpu_unsorted_row_reports_or_matches(eng):
+def test_gpu_unsorted_row_matches(eng):
     """Mixed second / millisecond qualifiers in one row are iterated in column order
-    (HistogramRowSeq does not sort): the engine raises NOT_IMPLEMENTED when a span's outputs
-    leave time order, and otherwise matches."""
+    (HistogramRowSeq does not sort): the raw group-by then follows the aggregation iterator's
+    greedy walk (HistogramAggregationIterator.next :240-292, k_hist_walk)."""
     cols = [(bytes([6, 0, 10]), U.encode_simple(0, [((1.0, 2.0), 1)], 0, 0)),
             (bytes([6, 0, 0, 0x13, 0x88]), U.encode_simple(0, [((1.0, 2.0), 2)], 0, 0)),   # 5000 ms
             (bytes([6, 0, 20]), U.encode_simple(0, [((1.0, 2.0), 4)], 0, 0))]
@@ -152,13 +152,40 @@ def test_gpu_unsorted_row_reports_or_matches(eng):
     eng.load_histograms(hb)
     for ds in (None, "1m-sum"):
         q = U.query(T0, T0 + 3600, "sum", ds)
-        want = O.run_hist(hb, q, [50.0], True)
-        try:
-            got = eng.run_histogram(q, [50.0], True)
-        except EngineError as e:
-            assert e.code == -22 and ds is None
-            continue
-        U.same(got, want)
+        U.same(eng.run_histogram(q, [50.0], True), O.run_hist(hb, q, [50.0], True))
+
+
+def _shuffled_rows(hb_rows, rng, frac):
+    return [[(base, [cols[i] for i in rng.permutation(len(cols))] if rng.random() < frac else cols)
+             for base, cols in rows] for rows in hb_rows]
+
+
+@pytest.mark.parametrize("seed", [31, 32, 33])
+def test_gpu_raw_spans_out_of_order_walk(eng, seed):
+    """Raw (no downsampler) group-by over spans some of whose rows hold their columns out of time
+    order: the greedy walk across the group's spans -- repeated and receding timestamps, points of
+    several spans merged only when they are current together -- against the oracle's literal
+    iterator, for sum and none, with queries that cut the spans at both ends."""
+    rng = np.random.default_rng(seed)
+    series = []
+    for s in range(7):
+        rows = []
+        for r in range(2):
+            cols = []
+            for off in rng.choice(3600, size=int(rng.integers(3, 40)), replace=False):
+                ms = rng.random() < 0.3
+                q = bytes([6]) + (int(off) * 1000 + int(rng.integers(0, 999))).to_bytes(4, "big") if ms else \
+                    bytes([6]) + int(off).to_bytes(2, "big")
+                cols.append((q, U.encode_simple(0, [((1.0, 2.0), int(rng.integers(0, 9))),
+                                                    ((2.0, 4.0), int(rng.integers(0, 9)))], 0, int(rng.integers(0, 3)))))
+            cols.sort(key=lambda c: c[0])            # HBase's qualifier-byte order: s / ms mixed out of time order
+            rows.append((T0 + 3600 * r, cols))
+        series.append(rows)
+    series = _shuffled_rows(series, rng, 0.3)        # and some rows in no order at all
+    hb = H.HostHistBatch.from_rows(series, [s % 3 for s in range(7)], {0: H.HCODEC_SIMPLE})
+    for agg in ("sum", "none"):
+        for t0, t1 in ((T0, T0 + 7200), (T0 + 600, T0 + 5000)):
+            run_both(eng, hb, U.query(t0, t1, agg, None), [50.0, 95.0], True)
 
 
 def test_gpu_group_filter_and_empty(eng):
