@@ -448,6 +448,7 @@ struct tsdbhip_ctx {
   // of at most CH datapoints (k_short); rows = several rows per series, none over CH (k_rows).
   std::vector<int32_t> tl[2][3], tl_other;
   DevBuf d_tl, d_tl_n, r1a, r1b, r3a, r3b, r2, r_n;   // device copies; k_short / k_rows / k_fast redo lists
+  DevBuf hw_mark;                                      // k_hwin: a tile is on the redo list (one word a tile)
   int64_t tl_off[7] = {};
   bool fast_used = false;
   HostBuf h_stage;   // collect(): the dense [G][K] values and flags, page-locked
@@ -747,7 +748,9 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   if (c->cmp_tmp) (void)hipFree(c->cmp_tmp);
   tsdb::hist_release(c->hist);
   c->hist = nullptr;
-  for (DevBuf* b : {&c->sel_vals, &c->sel_sorted, &c->sel_uni, &c->sel_gsp, &c->cal_bounds}) b->release();
+  for (DevBuf* b : {&c->sel_vals, &c->sel_sorted, &c->sel_uni, &c->sel_gsp, &c->cal_bounds, &c->sel_wr, &c->first_ts,
+                    &c->hw_mark, &c->m_sum, &c->m_mn, &c->m_mx, &c->m_mean, &c->m_m2, &c->m_nl, &c->m_nz, &c->m_f})
+    b->release();
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   for (auto& e : c->cev) if (e) (void)hipEventDestroy(e);
   if (c->copy_stream) { (void)hipStreamSynchronize(c->copy_stream); (void)hipStreamDestroy(c->copy_stream); }
@@ -1744,6 +1747,7 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     }
     // 32-bit copies of the column offsets when the blobs are under 4 GB (written by the same
     // checking pass; the one-pass kernels read 4 bytes an offset instead of 8)
+    mark("onepass alloc");
     const bool w32 = nc && qz < ((uint64_t)1 << 32) && vz < ((uint64_t)1 << 32);
     if (w32) {
       HIP_OK(d_cq32.ensure((c1c + 1) * 4));
@@ -1763,6 +1767,7 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     int32_t bad = 0;
     HIP_OK(hipMemcpyAsync(&bad, d_bad.p, 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
+    mark("onepass H2D");
     if (bad) return fail(TSDB_E_ILLEGAL_ARGUMENT, "column offsets not monotonic");
     HIP_OK(d_crow.ensure(c1c * 4));
     HIP_OK(d_cn.ensure(c1c * 8));
@@ -1806,6 +1811,7 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     hipError_t he = hipSuccess;
     const int cap = cmp_onepass_cap(p, d_rmax.as<uint32_t>(), st, &he);   // (synchronises)
     HIP_OK(he);
+    mark("onepass cols");
     float t_cols = 0;
     (void)hipEventElapsedTime(&t_cols, c->ev[0], c->ev[2]);
     if (!cap) {
@@ -1843,6 +1849,7 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     }
     op_qtot = qt;
     op_vtot = vt;
+    mark("onepass layout");
     HIP_OK(c->qual.ensure(qt + BLOB_SLACK));
     HIP_OK(c->val.ensure(vt + BLOB_SLACK));
     HIP_OK(hipMemsetAsync(c->qual.p, 0, qt + BLOB_SLACK, st));
@@ -1867,6 +1874,7 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
       HIP_OK(hipMemcpyAsync(rerr.data(), p.row_err, nr * 4, hipMemcpyDeviceToHost, st));
     }
     HIP_OK(hipStreamSynchronize(st));
+    mark("onepass rows");
     float t_rows = 0;
     (void)hipEventElapsedTime(&t_rows, c->ev[3], c->ev[1]);
     cmp_ms = t_cols + t_rows;
@@ -2796,7 +2804,9 @@ bool seq_rows_ok(tsdbhip_ctx* c, const Plan& P) {
 // hour (every hour row in one window of W = 1 h / interval <= 64 slots), no rate, an order-free
 // function, and every tile of one streaming class with one-chunk rows.
 int hwin_slots(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, bool for_multi = false) {
-  if (const char* e = std::getenv("TSDBHIP_HWIN")) if (e[0] == '0') return 0;
+  const char* he = std::getenv("TSDBHIP_HWIN");   // 0: never; 2: wherever it applies (A/B)
+  if (he && he[0] == '0') return 0;
+  if (he && he[0] == '2') for_multi = true;
   // (fill policies need every participating series' fill values in windows where it has no row:
   // left to the dense split)
   if (P.mode != MODE_GRID || q->rate || q->ds_fill != TSDB_FILL_NONE || P.K <= 64 || P.I <= 0 || 3600000 % P.I != 0 || 3600000 / P.I > 64 ||
@@ -2811,11 +2821,12 @@ int hwin_slots(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, bool for_m
   }
   const char* env = std::getenv("TSDBHIP_FAST");
   if (env && env[0] == '0') return 0;
-  // only where the one-pass streaming kernels' slot LDS does not fit (the dense split's case):
-  // with a handful of slots a window (10m: 6) k_rows' fused pass is faster (profiles/r04x).  The
-  // fused multi-aggregator pass has no K > 64 variant of those kernels: k_hwin takes every K > 64
-  // that tiles the hour.
-  if (!(for_multi || P.multi) && fast_wave_lds(P.K, false, true) <= 32 * 1024) return 0;
+  // Every K > 64 that tiles the hour, since k_hwin runs a work item a (tile, window): 12 h of 1m
+  // buckets (K = 720, whose slots fit the fused kernels' LDS) 50.6 ms through k_rows vs 11.4 ms
+  // here, 10m buckets of a day (K = 144) 11.8 vs 11.3 ms (profiles/r05j/).  (Before the per-window
+  // items, k_rows won at 10m: profiles/r04x.)  The fused multi-aggregator pass has no K > 64
+  // variant of the other kernels either.
+  (void)for_multi;
   return (int)(3600000 / P.I);
 }
 
@@ -3113,6 +3124,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       fp.oneb = P.I >= 3600000 && !(oenv && oenv[0] == '0') ? 1 : 0;   // (an hour row's chunk in one bucket)
       fp.wave_lds = (int32_t)(shortk == 3 ? fast_wave_lds(hwin, false, false) : fast_lds_of(q, P));
       fp.win_w = hwin;
+      if (shortk == 3) fp.redo_mark = c->hw_mark.as<uint32_t>();
       if (shortk == 3) {
         // k_hwin: one work item a (tile, hour window) -- a tile's 24 windows as one item left the
         // last round of the launch mostly idle; items of fewer windows measured 13.6 (whole tiles)
@@ -3169,6 +3181,10 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       const int32_t* dn2 = dn + 3 * cls + 2;
       int rc;
       if (hwin) {   // k_hwin over the one-chunk-row tiles (hwin_slots: no other tiles); k_grid takes what it hands back
+        if (cls == 0) {   // (a tile's work items hand it back once: zeroed marks for both classes' launches)
+          HIP_OK(c->hw_mark.ensure(std::max<int64_t>(1, nt) * 4));
+          HIP_OK(hipMemsetAsync(c->hw_mark.p, 0, std::max<int64_t>(1, nt) * 4, c->stream));
+        }
         for (int part = 1; part <= 2; part++) {
           const int64_t nn = part == 1 ? n1 : n2;
           if (!nn) continue;
@@ -3295,6 +3311,7 @@ struct ResultHeader {
 constexpr uint64_t RESULT_MAGIC = 0x7473646268697052ULL;
 constexpr size_t PINNED_MIN = 1 << 20;
 constexpr size_t POOL_MAX = (size_t)8 << 30;   // bytes kept pinned while unused
+constexpr size_t PIN_ASYNC_MIN = (size_t)64 << 20;   // blocks pinned by a helper thread instead of in the call
 
 struct PinnedPool {
   std::mutex mu;
@@ -3316,10 +3333,37 @@ struct PinnedPool {
     }
     cap = PINNED_MIN;
     while (cap < bytes) cap <<= 1;
+    if (cap >= PIN_ASYNC_MIN) {
+      // pinning hundreds of MB takes ~0.5 ms a MB (a config-4 raw result, 570 MB: 250 ms in the
+      // call): this result takes pageable memory, and a helper thread pins a block of its size
+      // for the pool, so the following queries find one
+      pin_async(cap);
+      return nullptr;
+    }
     void* b = nullptr;
     if (hipHostMalloc(&b, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
     return b;
   }
+  void pin_async(size_t cap) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      if (pinning) return;   // one at a time
+      pinning = true;
+    }
+    try {
+      std::thread([this, cap] {
+        void* b = nullptr;
+        const bool ok = hipHostMalloc(&b, cap, hipHostMallocDefault) == hipSuccess;
+        if (ok) give(b, cap);
+        std::lock_guard<std::mutex> lk(mu);
+        pinning = false;
+      }).detach();
+    } catch (const std::exception&) {
+      std::lock_guard<std::mutex> lk(mu);
+      pinning = false;
+    }
+  }
+  bool pinning = false;
   void give(void* b, size_t cap) {
     std::lock_guard<std::mutex> lk(mu);
     while (held + cap > POOL_MAX && !free_blocks.empty()) {   // drop the oldest blocks

@@ -2491,8 +2491,13 @@ __global__ __launch_bounds__(256, MULTI ? SHORT_OCC2(VL) : SHORT_OCC(VL)) void k
   const int h0 = (int)((int64_t)part * NW / S), h1 = (int)((int64_t)(part + 1) * NW / S);
   const int64_t s0 = tbeg[tile];
   const int ns = (int)(tend[tile] - s0);
+  // a tile goes on the redo list once, whichever of its items hands it back (p.redo_mark: a
+  // zeroed word a tile; the list holds one entry a tile)
+  auto hand_back = [&]() {
+    if (lane == 0 && atomicOr(&p.redo_mark[tile], 1u) == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
+  };
   if (ns > 64) {
-    if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
+    hand_back();
     return;
   }
   int64_t cur = lane < ns ? srp[s0 + lane] : 0;
@@ -2635,7 +2640,7 @@ __global__ __launch_bounds__(256, MULTI ? SHORT_OCC2(VL) : SHORT_OCC(VL)) void k
     if (has) { seen = true; cur++; }
   }
   if (redo) {
-    if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
+    hand_back();
     return;
   }
   if (any && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);

@@ -1311,9 +1311,7 @@ extern "C" int tsdbhip_md_info(tsdbhip_ctx* c, int* n_devices, int* transport, i
       if (!m->series.empty()) {   // loaded: the batch series the device holds
         shard_series[d] = (int64_t)m->series[d].size();
       } else {                    // synthesized
-        int64_t ns = 0, nr = 0;
-        uint64_t qb = 0, vb = 0;
-        if (tsdbhip_batch_sizes(m->subs[d], &ns, &nr, &qb, &vb) == 0) shard_series[d] = ns;
+        shard_series[d] = ctx_n_series(m->subs[d]);
       }
     }
   }

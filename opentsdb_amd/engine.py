@@ -272,7 +272,9 @@ class Engine:
     def md_stats(self):
         """tsdbhip_md_stats -> (per-device Timing list, RCCL communicator ranks, device-to-device
         bytes) of the last run on a multi-device context."""
-        nd = self.md_info()[0]
+        nd = C.c_int()   # (n_devices only: md_info's per-device series walks the shards)
+        _check(lib().tsdbhip_md_info(self.ctx, C.byref(nd), None, None, None))
+        nd = nd.value
         per = (abi.Timing * nd)()
         ranks, xb = C.c_int(), C.c_double()
         _check(lib().tsdbhip_md_stats(self.ctx, C.cast(per, C.c_void_p), C.byref(ranks), C.byref(xb)))

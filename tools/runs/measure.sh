@@ -1,8 +1,9 @@
 #!/bin/bash
-# Measurement pass: bash tools/runs/measure.sh TAG [c3day] [md] [pmc_hwin]
+# Measurement pass: bash tools/runs/measure.sh TAG [c3day] [md] [c4] [pmc_hwin]
 #   c3day     tools/c3day_bench.py --multi (config 3's day on one GPU's share)  -> c3day.jsonl
 #   md        bench.py --gpus 2 / 4 over repeated device 0 (the multi-device context rehearsal,
 #             config 2 weak + config 3 strong at 1M series)                     -> md2.jsonl, md4.jsonl
+#   c4        tools/bench_configs.py --config 4 (steps listed) and a TSDBHIP_TRACE=1 rerun -> c4*.jsonl
 #   pmc_hwin  rocprofv3 PMC passes over the day's sum:1m-avg (k_hwin)           -> pmc_hwin/summary.txt
 # Every GPU step under its own timeout; the first failure ends the pass.
 set -o pipefail
@@ -29,6 +30,15 @@ print($n, 'value', d['value'], 'ms', d['ms_per_step'], 'stages', d.get('stages')
 for k,v in d['extra']['config3_strong'].items():
     if isinstance(v, dict): print('  ', k, json.dumps(v))"
       done ;;
+    c4)
+      timeout -k 10 400 python3 -u tools/bench_configs.py --config 4 --steps 10 > $out/c4.jsonl 2> $out/c4.err \
+        || { tail -20 $out/c4.err; exit 1; }
+      TSDBHIP_TRACE=1 timeout -k 10 400 python3 -u tools/bench_configs.py --config 4 --steps 6 > $out/c4_trace.jsonl \
+        2> $out/c4_trace.txt || { tail -20 $out/c4_trace.txt; exit 1; }
+      python3 -c "
+import json
+for l in open('$out/c4.jsonl'):
+    d=json.loads(l); print(d['query'], 'mean', round(d['ms_per_step'],1), 'median', round(d['step_ms_median'],1), 'eval', round(d['k_raw_eval_ms'],1), 'steps', d['steps_ms'], 'dev', d['device_steps_ms'])" ;;
     pmc_hwin)
       bash tools/pmc_run.sh ${tag}_hwin python3 tools/c3day_bench.py --only 1m --steps 1 || exit $?
       python3 tools/pmc_summary.py gpurun_out/pmc_${tag}_hwin k_hwin | tee $out/pmc_hwin_summary.txt ;;
