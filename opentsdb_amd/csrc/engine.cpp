@@ -452,6 +452,9 @@ struct tsdbhip_ctx {
   int64_t tl_off[7] = {};
   bool fast_used = false;
   HostBuf h_stage;   // collect(): the dense [G][K] values and flags, page-locked
+  void* up_stage[2] = {nullptr, nullptr};   // h2d: page-locked staging of pageable uploads (UP_CHUNK each)
+  hipEvent_t up_ev[2] = {nullptr, nullptr};
+  bool up_busy[2] = {false, false};
   const int32_t* redo_final = nullptr;   // device counter of the tiles k_fast handed to k_grid
   int64_t redo_other = 0;                // + tiles of neither row class (k_grid only)
   tsdbhip_timing timing{};
@@ -546,6 +549,10 @@ int64_t cal_unit_ms(int unit) { return unit >= 0 && unit < 9 ? CAL_UNIT_MS[unit]
 // host logic restatements
 // ===========================================================================
 extern "C" int tsdbhip_abi_version(void) { return TSDBHIP_ABI_VERSION; }
+
+namespace tsdb {
+hipError_t h2d(tsdbhip_ctx* c, void* dst, const void* src, size_t n, hipStream_t st);   // (defined at the end)
+}  // namespace tsdb
 
 extern "C" int tsdbhip_host_alloc(uint64_t bytes, void** out) {
   if (!out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
@@ -751,6 +758,10 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
   for (DevBuf* b : {&c->sel_vals, &c->sel_sorted, &c->sel_uni, &c->sel_gsp, &c->cal_bounds, &c->sel_wr, &c->first_ts,
                     &c->hw_mark, &c->m_sum, &c->m_mn, &c->m_mx, &c->m_mean, &c->m_m2, &c->m_nl, &c->m_nz, &c->m_f})
     b->release();
+  for (int i = 0; i < 2; i++) {
+    if (c->up_ev[i]) (void)hipEventDestroy(c->up_ev[i]);
+    if (c->up_stage[i]) (void)hipHostFree(c->up_stage[i]);
+  }
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   for (auto& e : c->cev) if (e) (void)hipEventDestroy(e);
   if (c->copy_stream) { (void)hipStreamSynchronize(c->copy_stream); (void)hipStreamDestroy(c->copy_stream); }
@@ -1113,8 +1124,9 @@ static int load_body(tsdbhip_ctx* c, const tsdbhip_batch* b, const std::vector<i
   HIP_OK(c->gid.ensure(std::max<int64_t>(1, c->n_series) * 4));
   if (!rd.empty()) HIP_OK(hipMemcpy(c->rows.p, rd.data(), rd.size() * sizeof(RowDesc), hipMemcpyHostToDevice));
   HIP_OK(hipMemcpy(c->srp.p, c->h_srp.data(), (c->n_series + 1) * 8, hipMemcpyHostToDevice));
-  HIP_OK(hipMemcpy(c->qual.p, hq.data(), hq.size(), hipMemcpyHostToDevice));
-  HIP_OK(hipMemcpy(c->val.p, hv.data(), hv.size(), hipMemcpyHostToDevice));
+  HIP_OK(h2d(c, c->qual.p, hq.data(), hq.size(), c->stream));   // (the GPU pulls staged chunks: see h2d)
+  HIP_OK(h2d(c, c->val.p, hv.data(), hv.size(), c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
   if (c->n_series) HIP_OK(hipMemcpy(c->gid.p, c->h_group.data(), c->n_series * 4, hipMemcpyHostToDevice));
   return finish_load(c, rd);
 }
@@ -1590,13 +1602,13 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
       HIP_OK(cmp_rebase(d_raw.as<uint64_t>(), d_rcp.as<uint64_t>(), nr + 1, (uint64_t)c0, d_bad.as<int32_t>(), st));
     }
     if (nc) {
-      HIP_OK(hipMemcpyAsync(d_raw.p, cb->col_qual_off + c0, (nc + 1) * 8, hipMemcpyHostToDevice, st));
+      HIP_OK(h2d(c, d_raw.p, cb->col_qual_off + c0, (nc + 1) * 8, st));
       HIP_OK(cmp_rebase(d_raw.as<uint64_t>(), d_cqo.as<uint64_t>(), nc + 1, qa, d_bad.as<int32_t>(), st));
-      HIP_OK(hipMemcpyAsync(d_raw.p, cb->col_val_off + c0, (nc + 1) * 8, hipMemcpyHostToDevice, st));
+      HIP_OK(h2d(c, d_raw.p, cb->col_val_off + c0, (nc + 1) * 8, st));
       HIP_OK(cmp_rebase(d_raw.as<uint64_t>(), d_cvo.as<uint64_t>(), nc + 1, va, d_bad.as<int32_t>(), st));
-      if (qz > qa) HIP_OK(hipMemcpyAsync(d_q.p, cb->qual + qa, qz - qa, hipMemcpyHostToDevice, st));
-      if (vz > va) HIP_OK(hipMemcpyAsync(d_v.p, cb->val + va, vz - va, hipMemcpyHostToDevice, st));
-      if (cb->col_timestamp) HIP_OK(hipMemcpyAsync(d_cts.p, cb->col_timestamp + c0, nc * 8, hipMemcpyHostToDevice, st));
+      if (qz > qa) HIP_OK(h2d(c, d_q.p, cb->qual + qa, qz - qa, st));
+      if (vz > va) HIP_OK(h2d(c, d_v.p, cb->val + va, vz - va, st));
+      if (cb->col_timestamp) HIP_OK(h2d(c, d_cts.p, cb->col_timestamp + c0, nc * 8, st));
     }
     int32_t bad = 0;
     HIP_OK(hipMemcpyAsync(&bad, d_bad.p, 4, hipMemcpyDeviceToHost, st));
@@ -1754,15 +1766,15 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
       HIP_OK(d_cv32.ensure((c1c + 1) * 4));
     }
     if (nc) {
-      HIP_OK(hipMemcpyAsync(d_raw.p, cb->col_qual_off, (nc + 1) * 8, hipMemcpyHostToDevice, st));
+      HIP_OK(h2d(c, d_raw.p, cb->col_qual_off, (nc + 1) * 8, st));
       HIP_OK(cmp_rebase(d_raw.as<uint64_t>(), d_cqo.as<uint64_t>(), nc + 1, 0, d_bad.as<int32_t>(), st,
                         w32 ? d_cq32.as<uint32_t>() : nullptr));
-      HIP_OK(hipMemcpyAsync(d_raw.p, cb->col_val_off, (nc + 1) * 8, hipMemcpyHostToDevice, st));
+      HIP_OK(h2d(c, d_raw.p, cb->col_val_off, (nc + 1) * 8, st));
       HIP_OK(cmp_rebase(d_raw.as<uint64_t>(), d_cvo.as<uint64_t>(), nc + 1, 0, d_bad.as<int32_t>(), st,
                         w32 ? d_cv32.as<uint32_t>() : nullptr));
-      if (qz) HIP_OK(hipMemcpyAsync(d_q.p, cb->qual, qz, hipMemcpyHostToDevice, st));
-      if (vz) HIP_OK(hipMemcpyAsync(d_v.p, cb->val, vz, hipMemcpyHostToDevice, st));
-      if (cb->col_timestamp) HIP_OK(hipMemcpyAsync(d_cts.p, cb->col_timestamp, nc * 8, hipMemcpyHostToDevice, st));
+      if (qz) HIP_OK(h2d(c, d_q.p, cb->qual, qz, st));
+      if (vz) HIP_OK(h2d(c, d_v.p, cb->val, vz, st));
+      if (cb->col_timestamp) HIP_OK(h2d(c, d_cts.p, cb->col_timestamp, nc * 8, st));
     }
     int32_t bad = 0;
     HIP_OK(hipMemcpyAsync(&bad, d_bad.p, 4, hipMemcpyDeviceToHost, st));
@@ -5761,3 +5773,60 @@ extern "C" int tsdbhip_rollup_download(tsdbhip_ctx* c, int32_t* series, uint32_t
   if (val_off) val_off[cell0] = byte0;
   return 0;
 }
+
+namespace tsdb {
+// Host -> device upload of a scan's arrays (tsdbhip_load_cells).  The queue's copy engine ran these
+// uploads at half the PCIe rate on every call after the first (576 MB in 19 ms against 10 ms; blit
+// copies 10 ms: profiles/r05n, r05o), so the GPU pulls the bytes itself (k_pull, 16-byte loads
+// over the device mapping of page-locked memory):
+//   - page-locked sources (tsdbhip_host_alloc, registered memory): pulled directly;
+//   - pageable sources: copied into two page-locked staging chunks of the context by the host's
+//     assembly threads, each chunk pulled while the next one is copied (hipEvents order the reuse).
+// Small or misaligned copies, and TSDBHIP_PULL=0, take hipMemcpyAsync.
+constexpr size_t UP_CHUNK = (size_t)32 << 20;
+hipError_t h2d(tsdbhip_ctx* c, void* dst, const void* src, size_t n, hipStream_t st) {
+  static const bool pull_ok = [] {
+    const char* e = std::getenv("TSDBHIP_PULL");
+    return !(e && e[0] == '0');
+  }();
+  if (!pull_ok || n < ((size_t)1 << 20) || ((uintptr_t)dst & 15) != 0) return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st);
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, src) == hipSuccess && a.type == hipMemoryTypeHost && a.devicePointer) {
+    if ((((uintptr_t)src ^ (uintptr_t)dst) & 15) != 0) return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st);
+    const size_t off = a.hostPointer ? (size_t)((const char*)src - (const char*)a.hostPointer) : 0;
+    return launch_pull(dst, (const char*)a.devicePointer + off, n, st);
+  }
+  (void)hipGetLastError();   // (pageable memory: no attributes)
+  for (int i = 0; i < 2; i++) {
+    if (!c->up_stage[i]) {
+      hipError_t e = hipHostMalloc(&c->up_stage[i], UP_CHUNK, hipHostMallocDefault);
+      if (e != hipSuccess) { c->up_stage[i] = nullptr; return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st); }
+      e = hipEventCreateWithFlags(&c->up_ev[i], hipEventDisableTiming);
+      if (e != hipSuccess) return e;
+    }
+  }
+  AssemblyPool& pool = AssemblyPool::get();
+  const char* s8 = static_cast<const char*>(src);
+  char* d8 = static_cast<char*>(dst);
+  for (size_t off = 0, i = 0; off < n; off += UP_CHUNK, i++) {
+    const int b = (int)(i & 1);
+    const size_t len = std::min(UP_CHUNK, n - off);
+    if (c->up_busy[b]) {
+      const hipError_t e = hipEventSynchronize(c->up_ev[b]);
+      if (e != hipSuccess) return e;
+    }
+    char* stage = static_cast<char*>(c->up_stage[b]);
+    const int nt = len >= ((size_t)8 << 20) ? pool.width() : 1;
+    const std::function<void(int)> part = [&](int t) {
+      const size_t a0 = (len * t / nt) & ~(size_t)63, a1 = t + 1 == nt ? len : (len * (t + 1) / nt) & ~(size_t)63;
+      std::memcpy(stage + a0, s8 + off + a0, a1 - a0);
+    };
+    if (nt <= 1 || !pool.run(nt, part)) std::memcpy(stage, s8 + off, len);
+    hipError_t e = launch_pull(d8 + off, stage, len, st);   // (page-locked memory: the host pointer maps)
+    if (e == hipSuccess) e = hipEventRecord(c->up_ev[b], st);
+    if (e != hipSuccess) return e;
+    c->up_busy[b] = true;
+  }
+  return hipSuccess;
+}
+}  // namespace tsdb

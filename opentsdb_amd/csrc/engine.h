@@ -511,6 +511,7 @@ hipError_t launch_sel_seg(const SelParams& p, hipStream_t s, int64_t maxn);
 hipError_t launch_ordered(const OrdParams& p, hipStream_t s);
 hipError_t launch_rank_merge(const RankMergeParams& p, hipStream_t s);
 hipError_t launch_state_fold(const StateFoldParams& p, hipStream_t s);
+hipError_t launch_pull(void* dst, const void* src, size_t n, hipStream_t s);   // device pointer of page-locked host src
 // per-downsample-function instantiations (k_grid.hip / k_fast.hip, one object per F)
 template <int F> hipError_t launch_grid_inst(const GridParams& p, hipStream_t s);
 template <int F> hipError_t launch_fast_inst(const GridParams& p, int qw, int vl, hipStream_t s);
