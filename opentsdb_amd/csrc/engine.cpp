@@ -2613,6 +2613,12 @@ int cmp_scan_check(tsdbhip_ctx* c, const Plan& P) {
   return 0;
 }
 
+// The point every span's Downsampler seeks to (Downsampler.seekInterval :415-437; ds_all: the
+// scan start), for the kernels' stream-order row skip (kcommon.h so_row_skip)
+int64_t seek_point(const Plan& P) {
+  return P.mode == MODE_ALL ? P.ss * 1000 : P.mode == MODE_TABLE ? P.seek : P.B0;
+}
+
 int plan_query(tsdbhip_ctx* c, const tsdbhip_query* q, Plan& P) {
   if (q->aggregator < 0 || q->aggregator >= TSDB_AGG_COUNT_ALL) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad aggregator");
   if (q->ds_function >= TSDB_AGG_COUNT_ALL) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad downsampling function");
@@ -2898,6 +2904,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   gp.qe = q->end_time;
   gp.rcpI = (float)(1.0 / (double)P.I);
   gp.mode = P.mode;
+  gp.seek_any = seek_point(P);
   gp.ga = P.ga;
   gp.interp = P.interp;
   gp.fill = q->ds_fill;
@@ -3679,6 +3686,7 @@ int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   gp.qs = q->start_time;
   gp.qe = q->end_time;
   gp.mode = P.mode;
+  gp.seek_any = seek_point(P);
   gp.ga = P.ga;
   gp.interp = P.interp;
   gp.fill = q->ds_fill;
@@ -5610,6 +5618,7 @@ extern "C" int tsdbhip_rollup_run(tsdbhip_ctx* c, const tsdbhip_rollup_spec* sp,
     gp.K = P.K;
     gp.rcpI = (float)(1.0 / (double)P.I);
     gp.mode = MODE_GRID;
+    gp.seek_any = P.B0;
     gp.n_series = n;
     gp.err = c->err.as<int32_t>();
     gp.val2 = c->val2.as<uint8_t>();

@@ -103,6 +103,7 @@ struct GridParams {
   int64_t qs, qe;        // "all" bounds (raw query start/end)
   const int64_t* bounds; // MODE_TABLE: K + 1 slot boundaries (ms)
   int64_t seek_ms;       // MODE_TABLE: points before this are skipped (Downsampler.seekInterval)
+  int64_t seek_any;      // the point every span's Downsampler seeks to (any mode; stream order, so_row_skip)
   int32_t skip0;         // MODE_TABLE: slot 0 lies before the SpanGroup start (a filled leading
                          // bucket): it feeds RateSpan but AggregationIterator drops it
   float rcpI;            // 1/I as float (slot division)

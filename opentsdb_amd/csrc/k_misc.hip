@@ -847,7 +847,9 @@ __global__ __launch_bounds__(256) void k_synth_write(SynthParams p) {
 // previousInterval(first datapoint after the seek, src/core/Downsampler.java:336-350), so it
 // needs that datapoint per series: rows with base in [ss, se), in order, qualifiers walked
 // (2-byte second or 4-byte millisecond, Internal.java:621-810) until the first timestamp >= t0.
-// One thread per series; INT64_MAX when the series has none.
+// One thread per series; INT64_MAX when the series has none.  Span.seekRow passes over a row
+// whose last cell is before t0 (Span.java:360-380): for a row out of order (ROW_UNSORTED) that
+// is not the last of the scan, its first cell at or past t0 does not count.
 __global__ void k_first_ts(const RowDesc* __restrict__ rows, const int64_t* __restrict__ srp,
                            const uint8_t* __restrict__ qual, int64_t n, int64_t ss, int64_t se, int64_t t0,
                            int64_t* __restrict__ out) {
@@ -857,7 +859,10 @@ __global__ void k_first_ts(const RowDesc* __restrict__ rows, const int64_t* __re
   for (int64_t r = srp[s]; r < srp[s + 1] && res == INT64_MAX; r++) {
     const RowDesc d = rows[r];
     if ((int64_t)d.base < ss || (int64_t)d.base >= se) continue;
-    if ((int64_t)d.base * 1000 + 3600000 <= t0) continue;   // every offset is < 1 h
+    if ((int64_t)d.base * 1000 + 4194304 <= t0) continue;   // every offset is < 2^22 ms
+    const bool last_row = r + 1 >= srp[s + 1] || (int64_t)rows[r + 1].base >= se;
+    const bool whole = (d.flags & ROW_UNSORTED) && !last_row;   // the last cell decides
+    int64_t first = INT64_MAX, last = INT64_MIN;
     const uint8_t* q = qual + d.qoff;
     uint32_t pos = 0;
     for (uint32_t i = 0; i < d.ndp && pos < d.qlen; i++) {
@@ -871,8 +876,13 @@ __global__ void k_first_ts(const RowDesc* __restrict__ rows, const int64_t* __re
         pos += 2;
       }
       const int64_t ts = (int64_t)d.base * 1000 + off;
-      if (ts >= t0) { res = ts; break; }
+      last = ts;
+      if (ts >= t0 && first == INT64_MAX) {
+        first = ts;
+        if (!whole) break;
+      }
     }
+    if (!whole || last >= t0) res = first;
   }
   out[s] = res;
 }

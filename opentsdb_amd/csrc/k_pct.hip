@@ -418,6 +418,7 @@ __device__ bool pct_series(const GridParams& p, int64_t s, const WaveLds& W, dou
   while (rb < r1 && (int64_t)p.rows[rb].base < p.se) rb++;
   int cur = -1;        // open bucket
   int64_t cnt = 0;     // its non-NaN values (in buf / gbuf)
+  StreamOrd so{-1};    // stored order (kcommon.h so_apply)
   Raw rc = {}, rn = {};
   RowDesc d = {};
   if (ra < rb) {
@@ -436,6 +437,7 @@ __device__ bool pct_series(const GridParams& p, int64_t s, const WaveLds& W, dou
     }
     const RowGeom g = row_geom(p, d.base);
     const bool uni = row_uniform(d);
+    const bool skip = so_row_skip(p, so, d, !has_next);
     int64_t vcur = 0;
     for (int64_t c0 = 0; c0 < (int64_t)d.ndp; c0 += CH) {
       // prefetch the next chunk (same row, or the first chunk of the next row)
@@ -446,8 +448,9 @@ __device__ bool pct_series(const GridParams& p, int64_t s, const WaveLds& W, dou
       }
       int slot[DPL];
       double val[DPL];
-      if (uni) decode_raw(p, d, g, c0, rc, slot, val);
-      else decode_generic(p, d, g, c0, W, vcur, slot, val);
+      if (uni) decode_raw<true>(p, d, g, c0, rc, slot, val);
+      else decode_generic<true>(p, d, g, c0, W, vcur, slot, val);
+      so_apply(p, so, slot, skip);
       rc = rn;
       bool left[DPL];
 #pragma unroll

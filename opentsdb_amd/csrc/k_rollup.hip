@@ -239,6 +239,7 @@ __device__ __forceinline__ void rollup_series(const GridParams& p, const RollupA
   int carry_slot = -1;
   RAcc carry;
   racc_init(carry);
+  StreamOrd so{-1};   // stored order (kcommon.h so_apply)
   Raw rc = {}, rn = {};
   RowDesc d = {};
   if (ra < rb) {
@@ -257,6 +258,7 @@ __device__ __forceinline__ void rollup_series(const GridParams& p, const RollupA
     }
     const RowGeom g = row_geom(p, d.base);
     const bool uni = row_uniform(d);
+    const bool skip = so_row_skip(p, so, d, !has_next);
     int64_t vcur = 0;
     for (int64_t c0 = 0; c0 < (int64_t)d.ndp; c0 += CH) {
       if (c0 + CH < (int64_t)d.ndp) {
@@ -266,8 +268,9 @@ __device__ __forceinline__ void rollup_series(const GridParams& p, const RollupA
       }
       int slot[DPL];
       double val[DPL];
-      if (uni) decode_raw(p, d, g, c0, rc, slot, val);
-      else decode_generic(p, d, g, c0, W, vcur, slot, val);
+      if (uni) decode_raw<true>(p, d, g, c0, rc, slot, val);
+      else decode_generic<true>(p, d, g, c0, W, vcur, slot, val);
+      so_apply(p, so, slot, skip);
       rc = rn;
       if (fast) rfast_chunk(rp, s, carry_slot, carry, slot, val);
       else rslow_chunk(rp, W, s, carry_slot, carry, slot, val);

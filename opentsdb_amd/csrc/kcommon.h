@@ -174,15 +174,17 @@ __device__ __forceinline__ RowGeom row_geom(const GridParams& p, uint32_t base) 
   return g;
 }
 
-// slot of offset off_ms inside the row, -1 if before slot 0 or at/after K
-__device__ __forceinline__ int slot_of(const GridParams& p, const RowGeom& g, uint32_t base, uint32_t off_ms) {
+// slot code of offset off_ms inside the row: its slot, -1 before slot 0 (before the seek point;
+// ds_all: before the start), K at or after the last slot's end (ds_all: at or past the end)
+__device__ __forceinline__ int slot_code(const GridParams& p, const RowGeom& g, uint32_t base, uint32_t off_ms) {
   if (p.mode == MODE_ALL) {
     const int64_t ts = (int64_t)base * 1000 + off_ms;
-    return (ts >= p.qs && ts < p.qe) ? 0 : -1;
+    return ts < p.qs ? -1 : ts < p.qe ? 0 : 1;
   }
   if (p.mode == MODE_TABLE) {   // variable-width calendar slots: bounds[lo] <= ts < bounds[lo + 1]
     const int64_t ts = (int64_t)base * 1000 + off_ms;
-    if (ts < p.seek_ms || ts < p.bounds[0] || ts >= p.bounds[p.K]) return -1;
+    if (ts < p.seek_ms || ts < p.bounds[0]) return -1;
+    if (ts >= p.bounds[p.K]) return (int)p.K;
     int lo = 0, hi = (int)p.K;
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
@@ -207,7 +209,96 @@ __device__ __forceinline__ int slot_of(const GridParams& p, const RowGeom& g, ui
     q = n / p.I;
   }
   const int64_t s = g.q0 + q;
-  return s < p.K ? (int)s : -1;
+  return s < p.K ? (int)s : (int)p.K;
+}
+
+// slot of offset off_ms inside the row, -1 if before slot 0 or at/after K
+__device__ __forceinline__ int slot_of(const GridParams& p, const RowGeom& g, uint32_t base, uint32_t off_ms) {
+  const int k = slot_code(p, g, base, off_ms);
+  return k < p.K ? k : -1;
+}
+
+// ---- stream order -----------------------------------------------------------------
+// A span yields its datapoints as stored: Span.Iterator the rows in base-time order
+// (Span.java:420-452), RowSeq.Iterator a row's cells in column order (RowSeq.java:552-568).
+// ValuesInInterval takes every next value below the current interval's end
+// (Downsampler.java:464-471) and otherwise moves the end past the value (:388-406), so a
+// datapoint falls in the interval of the LARGEST timestamp its span has yielded so far: its own
+// when the points are in time order, the one it follows when it recedes (cells out of order).
+// Over slot codes (slot_code) that is a running max along the stored order.  The span starts at
+// the seek point (Span.seekRow :360-380: the first row whose LAST cell is at or past it, then
+// RowSeq.Iterator.seek :612-636: the first cell there that is): the max turns >= 0 at that
+// cell, and so_row_skip drops the rows seekRow passes over.  Once the max reaches K the span
+// has ended for the query.  ds_all (MODE_ALL) filters each value by [start, end) instead and
+// ends the span at the first value past the end (ValuesInInterval.moveToNextValue :357-382).
+// Over sorted rows every code is its own running max: the transform is the identity.
+#define SLOT_NONE INT32_MIN   // no datapoint (lane past the row's end)
+struct StreamOrd {
+  int smax;   // running max slot code of the span's points so far (-1: not started)
+};
+
+// Timestamp (ms) of row d's last cell in column order (Internal.inMilliseconds per qualifier).
+__device__ __forceinline__ int64_t row_last_ms(const GridParams& p, const RowDesc& d) {
+  const uint8_t* q = p.qual + d.qoff;
+  const int qw = d.flags & ROW_QW_MASK;
+  uint32_t pos = 0;
+  if (qw == 2 || qw == 4) {
+    pos = (d.ndp - 1) * (uint32_t)qw;
+  } else {
+    uint32_t at = 0;
+    for (uint32_t i = 0; i < d.ndp && at < d.qlen; i++) {
+      pos = at;
+      at += (q[at] & 0xF0) == 0xF0 ? 4 : 2;
+    }
+  }
+  int64_t off;
+  if (qw == 4 || (qw != 2 && (q[pos] & 0xF0) == 0xF0)) {
+    const uint32_t w = ((uint32_t)q[pos] << 24) | ((uint32_t)q[pos + 1] << 16) | ((uint32_t)q[pos + 2] << 8) | q[pos + 3];
+    off = (w & 0x0FFFFFC0u) >> 6;
+  } else {
+    off = (int64_t)(((((uint32_t)q[pos] << 8) | q[pos + 1]) >> 4) & 0xFFF) * 1000;
+  }
+  return (int64_t)d.base * 1000 + off;
+}
+
+// true: Span.seekRow passes over row d (the span has not started, d is not its last row in the
+// scan, and d's last cell lies before the seek point -- only a row out of order can hold a cell
+// at or past the seek point before that one)
+__device__ __forceinline__ bool so_row_skip(const GridParams& p, const StreamOrd& so, const RowDesc& d,
+                                            bool last_row) {
+  if (so.smax >= 0 || last_row || !(d.flags & ROW_UNSORTED) || d.ndp == 0) return false;
+  return row_last_ms(p, d) < p.seek_any;
+}
+
+// Slot codes of the lane's DPL consecutive points (lanes in stored order) -> slots (-1: none).
+__device__ __forceinline__ void so_apply(const GridParams& p, StreamOrd& so, int slot[DPL], bool skip_row) {
+  const int K = (int)p.K;
+  const int lane = lane_id();
+  int run[DPL];
+  int m = INT32_MIN;
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    if (skip_row) slot[j] = SLOT_NONE;
+    if (slot[j] != SLOT_NONE) m = max(m, slot[j]);
+    run[j] = m;
+  }
+  int incl = m;   // inclusive max scan over the lanes
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl = max(incl, y);
+  }
+  int excl = __shfl_up(incl, 1, 64);
+  if (lane == 0) excl = INT32_MIN;
+  excl = max(excl, so.smax);
+#pragma unroll
+  for (int j = 0; j < DPL; j++) {
+    if (slot[j] == SLOT_NONE) { slot[j] = -1; continue; }
+    const int e = max(excl, run[j]);
+    if (p.mode == MODE_ALL) slot[j] = (slot[j] == 0 && e < K) ? 0 : -1;
+    else slot[j] = (e >= 0 && e < K) ? e : -1;
+  }
+  so.smax = max(so.smax, __shfl(incl, 63, 64));
 }
 
 // ---- per-bucket downsample state (Aggregator.runDouble over a bucket, in order) ----
@@ -519,6 +610,8 @@ __device__ __forceinline__ void load_raw(const GridParams& p, const RowDesc& d, 
 }
 
 // Decodes the lane's 8 datapoints of a uniform row from raw registers into (slot, value).
+// CODE: slot codes (slot_code, SLOT_NONE past the row's end) for so_apply, else slots
+template <bool CODE = false>
 __device__ __forceinline__ void decode_raw(const GridParams& p, const RowDesc& d, const RowGeom& g, int64_t c0,
                                            const Raw& rw, int slot[DPL], double val[DPL]) {
   const int lane = lane_id();
@@ -574,10 +667,12 @@ __device__ __forceinline__ void decode_raw(const GridParams& p, const RowDesc& d
     for (int j = 0; j < DPL; j++) val[j] = (double)(int8_t)((ws[j >> 2] >> ((j & 3) * 8)) & 0xFF);
   }
 #pragma unroll
-  for (int j = 0; j < DPL; j++) slot[j] = (j < nv) ? slot_of(p, g, d.base, off[j]) : -1;
+  for (int j = 0; j < DPL; j++)
+    slot[j] = (j < nv) ? (CODE ? slot_code(p, g, d.base, off[j]) : slot_of(p, g, d.base, off[j])) : (CODE ? SLOT_NONE : -1);
 }
 
 // Generic decode (variable-length values, mixed qualifier widths); loads inside.
+template <bool CODE = false>
 __device__ __forceinline__ void decode_generic(const GridParams& p, const RowDesc& d, const RowGeom& g, int64_t c0,
                                const WaveLds& W, int64_t& vcur, int slot[DPL], double val[DPL]) {
   const int lane = lane_id();
@@ -588,7 +683,7 @@ __device__ __forceinline__ void decode_generic(const GridParams& p, const RowDes
   const uint8_t* v = p.val + d.voff;
   uint32_t off[DPL], fl[DPL];
 #pragma unroll
-  for (int j = 0; j < DPL; j++) { off[j] = 0; fl[j] = 0; slot[j] = -1; val[j] = 0.0; }
+  for (int j = 0; j < DPL; j++) { off[j] = 0; fl[j] = 0; slot[j] = CODE ? SLOT_NONE : -1; val[j] = 0.0; }
   WAVE_SYNC();
   if (qw == 2 || qw == 4) {
     if (nv > 0) {
@@ -641,7 +736,7 @@ __device__ __forceinline__ void decode_generic(const GridParams& p, const RowDes
         double x = 0.0;
         if (!decode_value(bits, len[j], (fl[j] & 8) != 0, x)) set_err(p.err, TSDB_E_ILLEGAL_DATA);
         val[j] = x;
-        slot[j] = slot_of(p, g, d.base, off[j]);
+        slot[j] = CODE ? slot_code(p, g, d.base, off[j]) : slot_of(p, g, d.base, off[j]);
       }
       o += len[j];
     }
@@ -677,7 +772,7 @@ __device__ __forceinline__ void decode_generic(const GridParams& p, const RowDes
         double x = 0.0;
         if (!decode_value(bits, len, (mvv >> 31) != 0, x)) set_err(p.err, TSDB_E_ILLEGAL_DATA);
         val[j] = x;
-        slot[j] = slot_of(p, g, d.base, W.mq[t]);
+        slot[j] = CODE ? slot_code(p, g, d.base, W.mq[t]) : slot_of(p, g, d.base, W.mq[t]);
       }
     }
   }
@@ -1167,9 +1262,12 @@ __device__ __forceinline__ void rp_store(const GridParams& p, int64_t tile, int 
 // through pre_dense.
 // stage (k_short, column layout): the row goes to LDS and sel_cols_flush writes 8 series'
 // column pieces at once.
+// uacc: the caller's per-lane union flag for the tile (all its series are of group g), stored
+// once at the tile's end (sel_uni_flush) -- a load of the flag at every series end makes the wave
+// wait for every load issued before it, the streaming kernels' whole ring of rows.
 template <bool MARK = true>   // MARK: flag the row written (k_short flags its whole tile at the end)
 __device__ __forceinline__ void sel_direct_out(const GridParams& p, int K, int32_t g, int64_t s, bool pr_in,
-                                               double v, double* stage = nullptr) {
+                                               double v, double* stage = nullptr, bool* uacc = nullptr) {
   double cv = 0.0;
   bool uni;
   const bool has = slot_contribution(p, K, pr_in, v, cv, uni);
@@ -1186,8 +1284,14 @@ __device__ __forceinline__ void sel_direct_out(const GridParams& p, int K, int32
   }
   // every series of a group sets the same G x K flags: store only while unset (config 2: 1M
   // series' byte stores into 64 x 60 flags serialised on a few L2 lines, 6.5 vs 3.9 ms)
-  if (uni && !p.sel_uni[(int64_t)g * K + lane]) p.sel_uni[(int64_t)g * K + lane] = 1;
+  if (uacc) *uacc |= uni;
+  else if (uni && !p.sel_uni[(int64_t)g * K + lane]) p.sel_uni[(int64_t)g * K + lane] = 1;
   if (MARK && lane == 0 && p.sel_wr) p.sel_wr[s] = 1;
+}
+
+__device__ __forceinline__ void sel_uni_flush(const GridParams& p, int K, int32_t g, bool uacc) {
+  const int lane = lane_id();
+  if (uacc && lane < K && !p.sel_uni[(int64_t)g * K + lane]) p.sel_uni[(int64_t)g * K + lane] = 1;
 }
 
 // The staged rows of series sa .. sa + nb - 1 (group g, nb <= 8; stage [nb][K]) into their
@@ -1263,6 +1367,7 @@ __device__ __forceinline__ void series_slow(const GridParams& p, const WaveLds& 
   SeriesState st;
   st.carry_slot = -1;
   bs_init<F>(st.scarry);
+  StreamOrd so{-1};
   const int64_t r0 = p.series_row_ptr[s], r1 = p.series_row_ptr[s + 1];
   for (int64_t r = r0; r < r1; r++) {
     const RowDesc d = p.rows[r];
@@ -1270,6 +1375,7 @@ __device__ __forceinline__ void series_slow(const GridParams& p, const WaveLds& 
     if ((int64_t)d.base >= p.se) break;
     if (d.flags & ROW_ERR) { if (lane == 0) set_err(p.err, TSDB_E_ILLEGAL_DATA); continue; }
     const RowGeom g = row_geom(p, d.base);
+    const bool skip = so_row_skip(p, so, d, r + 1 >= r1 || (int64_t)p.rows[r + 1].base >= p.se);
     int64_t vcur = 0;
     for (int64_t c0 = 0; c0 < (int64_t)d.ndp; c0 += CH) {
       int slot[DPL];
@@ -1277,10 +1383,11 @@ __device__ __forceinline__ void series_slow(const GridParams& p, const WaveLds& 
       if (row_uniform(d)) {   // uniform rows: the register decode (no byte staging)
         Raw rw = {};
         load_raw(p, d, c0, rw);
-        decode_raw(p, d, g, c0, rw, slot, val);
+        decode_raw<true>(p, d, g, c0, rw, slot, val);
       } else {
-        decode_generic(p, d, g, c0, W, vcur, slot, val);
+        decode_generic<true>(p, d, g, c0, W, vcur, slot, val);
       }
+      so_apply(p, so, slot, skip);
       slow_chunk<F>(W, st, slot, val);
     }
   }
@@ -1334,12 +1441,15 @@ __global__ __launch_bounds__(256) void k_grid(GridParams p) {
   // magnitude and resolution cannot add exactly), so its chunks go straight through the
   // sequential in-bucket order (slow_chunk) -- one pass instead of the fast pass plus a re-walk
   bool series_first = true, seq = false;
+  StreamOrd so{-1};
+  bool skip_row = false;
   while (cok) {
     if (row_start) {
       if (cd.flags & ROW_ERR) { if (lane == 0) set_err(p.err, TSDB_E_ILLEGAL_DATA); }
       lsb = min(lsb, cd.lsb);
       amax = fmax(amax, cd.absmax);
       row_start = false;
+      skip_row = !force_slow && so_row_skip(p, so, cd, !nok || ns != cs);
       if (series_first) {
         series_first = false;
         if (needs_cert<F>() && !force_slow && cd.lsb != INT32_MAX && cd.absmax != 0.0) {
@@ -1363,8 +1473,9 @@ __global__ __launch_bounds__(256) void k_grid(GridParams p) {
       const RowGeom g = row_geom(p, cd.base);
       int slot[DPL];
       double val[DPL];
-      if (row_uniform(cd)) decode_raw(p, cd, g, c0, rc, slot, val);
-      else decode_generic(p, cd, g, c0, W, vcur, slot, val);
+      if (row_uniform(cd)) decode_raw<true>(p, cd, g, c0, rc, slot, val);
+      else decode_generic<true>(p, cd, g, c0, W, vcur, slot, val);
+      so_apply(p, so, slot, skip_row);
       if (seq) slow_chunk<F>(W, st, slot, val);
       else fast_chunk<F>(W, st, slot, val);
     }
@@ -1405,6 +1516,7 @@ __global__ __launch_bounds__(256) void k_grid(GridParams p) {
       amax = 0.0;
       series_first = true;
       seq = false;
+      so.smax = -1;
     }
     cs = ns;
     cr = nr;
@@ -1886,7 +1998,7 @@ __device__ __forceinline__ double fast_bucket_value(uint32_t c, double a) {
 template <int F, bool MARK = true, bool OUT = true, class RP>
 __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const FastLds& L, int K, int lsb, double amax,
                                                     RP& P, int64_t s, int32_t g, uint32_t nbound = 0,
-                                                    double* stage = nullptr) {
+                                                    double* stage = nullptr, bool* uacc = nullptr) {
   const int lane = lane_id();
   WAVE_SYNC();
   uint32_t c = 0;
@@ -1902,7 +2014,7 @@ __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const F
     if (!fast_cert<F>(nmax, lsb, amax)) return false;
   }
   if (OUT && p.sel_direct) {
-    sel_direct_out<MARK>(p, K, g, s, c != 0, fast_bucket_value<F>(c, a), stage);
+    sel_direct_out<MARK>(p, K, g, s, c != 0, fast_bucket_value<F>(c, a), stage, uacc);
   } else if (OUT && p.dense_out) {
     if (lane < K) {
       p.dense_out[s * K + lane] = fast_bucket_value<F>(c, a);
@@ -1984,6 +2096,7 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
     L.w.pres[k] = 0;
   }
   std::conditional_t<KR == 2, MultiReg, RegPart> RP;   // KR 2: the fused multi-aggregator pass
+  bool uacc = false;   // sel_direct: this tile's union flags (sel_uni_flush)
   rp_init(p.ga, RP);
   FWalk w;
   w.r0 = srp[tbeg[tile]];
@@ -2033,7 +2146,7 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
               s = scur;
             }
             const bool ok =
-                KR ? fast_series_end_reg<F, true, OUT>(p, L, K, lsb, amax, RP, s, p.tile_group[tile])
+                KR ? fast_series_end_reg<F, true, OUT>(p, L, K, lsb, amax, RP, s, p.tile_group[tile], 0, nullptr, &uacc)
                    : fast_series_end<F>(p, L, K, lsb, amax, s, p.tile_group[tile]);
             if (!ok) { redo = true; done = true; }
             if (OUT && (p.dense_out || p.sel_direct)) {   // the next series end is a later series
@@ -2070,6 +2183,7 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
     if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
     return;
   }
+  if (OUT && p.sel_direct) sel_uni_flush(p, K, p.tile_group[tile], uacc);
   WAVE_SYNC();
   double* ga_ = p.part.a + tile * K;
   double* gb_ = p.part.b + tile * K;
@@ -2248,6 +2362,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
   };
   // sel_direct into the column layout: rows staged 8 series at a time (sel_cols_flush)
   double* stage = (KR == 3 && p.sel_stage) ? (double*)(smem + (int64_t)wave * p.wave_lds + p.sel_stage) : nullptr;
+  bool uacc = false;
   auto series_end = [&](int j, int nv0) {
 #ifdef TSDBHIP_KDBG
     if (p.dbg & 1) return;
@@ -2256,7 +2371,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     const double amax = __longlong_as_double((long long)rl64(damax, j));
     const bool fine =
         KR ? fast_series_end_reg<F, false, OUT>(p, L, K, lsb, amax, RP, s0 + j, p.tile_group[tile], (uint32_t)nv0,
-                                                stage ? stage + (j & 7) * K : nullptr)
+                                                stage ? stage + (j & 7) * K : nullptr, &uacc)
            : fast_series_end<F>(p, L, K, lsb, amax, s0 + j, p.tile_group[tile]);
     if (!fine) redo = true;
     else if (KR == 3 && stage && ((j & 7) == 7 || j == ns - 1))
@@ -2287,6 +2402,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     return;
   }
   if (OUT && p.sel_wr && lane < ns) p.sel_wr[s0 + lane] = 1;   // sel_direct: every series of the tile was written
+  if (OUT && p.sel_direct) sel_uni_flush(p, K, p.tile_group[tile], uacc);
   WAVE_SYNC();
   double* ga_ = p.part.a + tile * K;
   double* gb_ = p.part.b + tile * K;
@@ -2378,6 +2494,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     L.w.pres[k] = 0;
   }
   std::conditional_t<KR == 2, MultiReg, RegPart> RP;
+  bool uacc = false;
   rp_init(p.ga, RP);
   WAVE_SYNC();
   // ring: rows issued unconditionally (past the tile: its last row, 0 datapoints)
@@ -2418,7 +2535,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
       if (jr < nr && !redo && __ballot(send == jr + 1) != 0) {   // the last row of its series
         if (have) {
           const int64_t s = s0 + __popcll(__ballot(send <= jr));
-          const bool fine = KR ? fast_series_end_reg<F, true, OUT>(p, L, K, lsb, amax, RP, s, p.tile_group[tile], nser)
+          const bool fine = KR ? fast_series_end_reg<F, true, OUT>(p, L, K, lsb, amax, RP, s, p.tile_group[tile], nser, nullptr, &uacc)
                                : fast_series_end<F>(p, L, K, lsb, amax, s, p.tile_group[tile]);
           if (!fine) redo = true;
           any = true;
@@ -2439,6 +2556,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     return;
   }
   if (any && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
+  if (OUT && p.sel_direct) sel_uni_flush(p, K, p.tile_group[tile], uacc);
   WAVE_SYNC();
   if (KR) {
     rp_store(p, tile, K, RP);

@@ -172,6 +172,32 @@ def test_unsorted_long_division_by_zero(eng):
         check(eng, b, abi.new_query(T0, T0 + 3599, agg), agg, f"double / 0 {agg}")
 
 
+@pytest.mark.parametrize("seed", [51, 52])
+@pytest.mark.parametrize("agg,ds,iv", [("sum", "sum", 60), ("sum", "avg", 60), ("max", "min", 600), ("avg", "count", 300),
+                                       ("sum", "last", 60), ("p99", "avg", 60), ("none", "sum", 60)])
+def test_unsorted_downsampled(eng, seed, agg, ds, iv):
+    """With a downsampler the cells' stored order decides the intervals: ValuesInInterval takes
+    every next value below the current interval's end (Downsampler.java:464-471), so a point
+    that recedes joins the interval it follows, not its own (RowSeq.Iterator does not sort)."""
+    b = unsorted_batch(seed, swap_p=0.25, dup_p=0.05)
+    q = abi.new_query(T0 + 600, T0 + 6599, agg, ds_function=abi.AGG[ds], ds_interval_ms=iv * 1000)
+    assert check(eng, b, q, agg, f"ds {seed} {agg} {iv}s-{ds}")
+
+
+def test_unsorted_downsampled_known(eng):
+    """One series stored [70 s, 10 s, 130 s, 125 s] under 1m-sum: intervals 60 (70 + 10) and
+    120 (130 + 125), not 0 / 60 / 120."""
+    z = [False] * 4
+    b = synth.from_series([synth.encode_rows([(T0 + t) * 1000 for t in (70, 10, 130, 125)], [1, 2, 4, 8], None,
+                                             [0] * 4, z)], [0])
+    q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG["sum"], ds_interval_ms=60000)
+    got = eng.run_batch(b, q)
+    assert_groups_match(got, O.run_query(b, q), "sum", tol=0.0, ctx="known ds")
+    (_, ts, bits, _), = got
+    assert list(ts) == [(T0 + 60) * 1000, (T0 + 120) * 1000]
+    assert [float(v) for v in bits.view(np.float64)] == [3.0, 12.0]
+
+
 def test_unsorted_known_walk(eng):
     """A = [10 s, 5 s], B = [5 s, 20 s] (long values): steps 5 (B), 10 (A), 5 (A), 20 (B).  At
     the third step B's window is (5 s, 20 s) with x == x0: B's own value 2, not a LERP."""

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Measurement pass: bash tools/runs/measure.sh TAG [c3day] [md] [c4] [pmc_hwin]
+# Measurement pass: bash tools/runs/measure.sh TAG [c3] [c3day] [md] [c4] [pmc_hwin]
+#   c3        tools/bench_configs.py --config 3 --only sum,p99,median (10M series x 1 h)  -> c3.jsonl
 #   c3day     tools/c3day_bench.py --multi (config 3's day on one GPU's share)  -> c3day.jsonl
 #   md        bench.py --gpus 2 / 4 over repeated device 0 (the multi-device context rehearsal,
 #             config 2 weak + config 3 strong at 1M series)                     -> md2.jsonl, md4.jsonl
@@ -13,6 +14,13 @@ mkdir -p $out
 export TMPDIR=/tmp
 for step in "$@"; do
   case $step in
+    c3)
+      timeout -k 10 400 python3 -u tools/bench_configs.py --config 3 --only sum,p99,median --steps 10 \
+        > $out/c3.jsonl 2> $out/c3.err || { tail -20 $out/c3.err; exit 1; }
+      python3 -c "
+import json
+for l in open('$out/c3.jsonl'):
+    d=json.loads(l); print(d['query'], 'ms', round(d['ms_per_step'],3), 'kernel', round(d.get('kernel_ms',0),3))" ;;
     c3day)
       timeout -k 10 400 python3 -u tools/c3day_bench.py --multi > $out/c3day.jsonl 2> $out/c3day.err \
         || { tail -20 $out/c3day.err; exit 1; }
