@@ -22,6 +22,7 @@
 #include "../../include/tsdbhip.h"
 #include "engine.h"
 #include "multi.h"
+#include "ksel.h"
 
 using namespace tsdb;
 
@@ -3953,6 +3954,7 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
   HIP_OK(hipMemcpyAsync(c->r_spn.p, sp_n.data(), std::max<int64_t>(1, S) * 4, hipMemcpyHostToDevice, c->stream));
   HIP_OK(hipMemcpyAsync(c->r_grp.p, grp_ser.data(), (G + 1) * 8, hipMemcpyHostToDevice, c->stream));
   HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
+  tr.mark("device arrays + H2D");
   RawParams rp{};
   rp.rows = c->rows.as<RowDesc>();
   rp.qual = c->qual.as<uint8_t>();
@@ -4000,6 +4002,7 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
   } else {
     HIP_OK(launch_raw_decode(rp, c->stream));
   }
+  tr.mark("decode launch");
   if (q->rate) {
     HIP_OK(launch_raw_rate(rp, c->stream));
     HIP_OK(hipMemcpyAsync(sp_n.data(), c->r_spn.p, std::max<int64_t>(1, S) * 4, hipMemcpyDeviceToHost, c->stream));
@@ -4104,7 +4107,30 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
     if (uns) HIP_OK(launch_raw_merge_ts(rp, c->stream));
     else HIP_OK(launch_raw_rank(rp, grp_ser[g0], grp_ser[g1], c->stream));
     HIP_OK(launch_raw_cursor(rp, grp_ser[g0], grp_ser[g1], c->stream));
+    // percentile / median with every rank asked for within 32 of the top (p90 ... p999 of
+    // large groups, any rank of small ones): k_raw_top folds each span operand into its point's
+    // top keys as it evaluates it -- no operand arrays
+    int top_t = 0;
     if (P.gsel) {
+      const char* e = std::getenv("TSDBHIP_RAW_TOP");   // A/B: 0 = operand arrays + selection
+      if (!(e && e[0] == '0')) {
+        int64_t k_all = 1;
+        for (int64_t g = g0; g < g1; g++) k_all = std::max<int64_t>(k_all, grp_ser[g + 1] - grp_ser[g]);
+        const int need = raw_top_need(P.gsel, k_all, 32);
+        top_t = need <= 8 ? 8 : need <= 16 ? 16 : need <= 32 ? 32 : 0;
+      }
+    }
+    if (top_t) {
+      rp.sel_fn = P.gsel;
+      HIP_OK(hipEventRecord(c->ev[3], c->stream));
+      if (uns) {
+        HIP_OK(c->r_dz.ensure(std::max<int64_t>(1, nout)));
+        HIP_OK(hipMemsetAsync(c->r_dz.p, 0, std::max<int64_t>(1, nout), c->stream));
+        rp.dz = c->r_dz.as<uint8_t>();
+      }
+      HIP_OK(launch_raw_top(rp, top_t, c->stream));
+      if (uns) HIP_OK(launch_raw_dz_check(rp, nout, c->stream));
+    } else if (P.gsel) {
       // percentile / median: every span operand of every union point, strip by strip
       // (RAW_STRIP points x the group's spans each), in batches of at most kSelOps operands
       int64_t kSelOps = (int64_t)1 << 28;

@@ -530,6 +530,7 @@ hipError_t launch_raw_dz_check(const RawParams& p, int64_t n_out, hipStream_t s)
 hipError_t launch_raw_eval(const RawParams& p, hipStream_t s);
 hipError_t launch_raw_vals(const RawParams& p, int64_t k_max, hipStream_t s);
 hipError_t launch_raw_sel(const RawParams& p, int64_t k_max, hipStream_t s);
+hipError_t launch_raw_top(const RawParams& p, int T, hipStream_t s);   // fused operands + selection (k_raw_eval.hip)
 template <int GA> hipError_t launch_raw_eval_inst(const RawParams& p, hipStream_t s);   // k_raw_eval.hip
 hipError_t launch_synth_write(const SynthParams& p, hipStream_t s);
 

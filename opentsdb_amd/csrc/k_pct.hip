@@ -12,7 +12,7 @@
 //            percentile uses commons-math3 3.4.1 LEGACY: pos = p (n + 1).
 //  * k_emit  one wave per tile: the bucket values -> SpanGroup contributions (LERP, fill,
 //            rate), exactly emit_series of k_grid, into tile partials for k_reduce.
-#include "kcommon.h"
+#include "ksel.h"
 
 #include <cstdlib>
 
@@ -74,11 +74,6 @@ __device__ __forceinline__ void sort_lds(double* buf, int N) {
       WAVE_SYNC();
     }
   }
-}
-
-__device__ __forceinline__ double pct_quantile(int fn) {
-  const int i = (fn - TSDB_AGG_P999) % 6;
-  return i == 0 ? 99.9 : i == 1 ? 99.0 : i == 2 ? 95.0 : i == 3 ? 90.0 : i == 4 ? 75.0 : 50.0;
 }
 
 // Order statistic of the n sorted values; get(i) returns element i (wave-uniform i).
@@ -203,15 +198,8 @@ __device__ __forceinline__ bool select_extreme(int fn, int n, const double* buf,
   return true;
 }
 
-// ---- order-preserving keys and the wave-local radix select (k_pct's large buckets,
+// ---- the wave-local radix select (k_pct's large buckets, keys from ksel.h,
 //      k_raw_sel) ---------------------------------------------------------------------
-__device__ __forceinline__ uint64_t f2key(double x) {   // ascending double order == unsigned key order
-  const uint64_t b = (uint64_t)__double_as_longlong(x);
-  return (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
-}
-__device__ __forceinline__ double key2f(uint64_t k) {
-  return __longlong_as_double((long long)((k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFULL) : ~k));
-}
 
 constexpr int SELW = 4;
 constexpr int RAW_SEL_B = 8;        // operand rows of 64 loaded together (k_raw_sel staging)
@@ -2205,72 +2193,6 @@ hipError_t launch_emit(const GridParams& p, hipStream_t s) {
 //   runLong   (src/core/Aggregators.java:403-413 Median, :675-686 PercentileAgg): every span
 //             operand, the estimation type honoured (LEGACY / R_3 / R_7), (long) of the estimate;
 //   runDouble (:416-430, :689-706): NaNs skipped, LEGACY always.
-__device__ __forceinline__ int64_t sel_d2l(double d) {   // Java (long) of a double
-  if (isnan(d)) return 0;
-  if (d >= 9223372036854775807.0) return 0x7FFFFFFFFFFFFFFFLL;
-  if (d <= -9223372036854775808.0) return (int64_t)0x8000000000000000ULL;
-  return (int64_t)d;
-}
-
-// The ranks select_sorted reads among m values at a union point (r1 = -1: one value) and the
-// interpolation weight: Median.runLong / runDouble sorted[m / 2]; PercentileAgg with its
-// estimation type for runLong, LEGACY for runDouble (src/core/Aggregators.java:403-430, :675-706).
-__device__ __forceinline__ void raw_sel_ranks(int fn, bool is_int, int m, int& r0, int& r1, double& dif) {
-  r0 = 0;
-  r1 = -1;
-  dif = 0.0;
-  const int est = fn == TSDB_AGG_MEDIAN ? 0 : (is_int ? (fn - TSDB_AGG_P999) / 6 : 0);   // runDouble: LEGACY
-  if (m > 1 && fn != TSDB_AGG_MEDIAN) {
-    const double q = pct_quantile(fn) / 100.0;
-    double pos;
-    if (est == 1) {            // R_3
-      pos = (q <= 0.5 / (double)m) ? 0.0 : rint((double)m * q);
-    } else if (est == 2) {     // R_7
-      pos = (q == 0.0) ? 0.0 : (q == 1.0 ? (double)m : 1.0 + (double)(m - 1) * q);
-    } else {                   // LEGACY
-      pos = (q == 0.0) ? 0.0 : (q == 1.0 ? (double)m : q * (double)(m + 1));
-    }
-    const double fpos = floor(pos);
-    if (pos < 1) r0 = 0;
-    else if (pos >= (double)m) r0 = m - 1;
-    else { r0 = (int)fpos - 1; r1 = r0 + 1; dif = pos - fpos; }
-  } else if (m > 0 && fn == TSDB_AGG_MEDIAN) {
-    r0 = m / 2;
-  }
-}
-
-// longValue / doubleValue of the selection (k0, k1: keys of ranks r0, r0 + 1) into out_bits.
-__device__ __forceinline__ void raw_sel_store(const RawParams& p, int64_t idx, bool is_int, int fn, int m, int r1,
-                                              double dif, uint64_t k0, uint64_t k1) {
-  uint64_t bits;
-  if (is_int) {
-    const int64_t l0 = (int64_t)(k0 ^ 0x8000000000000000ULL), l1 = (int64_t)(k1 ^ 0x8000000000000000ULL);
-    int64_t r;
-    if (fn == TSDB_AGG_MEDIAN) {
-      if (m == 0) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // "Shouldn't be here without any data"
-      r = l0;
-    } else if (m == 0) {
-      r = 0;                                               // (long) NaN
-    } else if (r1 < 0) {
-      r = sel_d2l((double)l0);
-    } else {
-      const double lower = (double)l0, upper = (double)l1;
-      r = sel_d2l(lower + dif * (upper - lower));
-    }
-    bits = (uint64_t)r;
-  } else {
-    double r;
-    if (m == 0) r = NAN;
-    else if (r1 < 0) r = key2f(k0);
-    else {
-      const double lower = key2f(k0), upper = key2f(k1);
-      r = lower + dif * (upper - lower);
-    }
-    if (isinf(r)) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // doubleValue (:640-643)
-    bits = (uint64_t)__double_as_longlong(r);
-  }
-  p.out_bits[idx] = bits;
-}
 
 // One WAVE per union point of the batch's strips (4 waves a block, no block barriers):
 // point pt -> strip pt / RAW_STRIP, position j.  Wave-local radix select: 8-bit digits, a
@@ -2536,26 +2458,6 @@ __global__ __launch_bounds__(256) void k_raw_sel_reg(RawParams p) {
 // compare-exchange chain per insertion, only for operands above the current T-th).  Ranks from
 // the top below T (host-checked bound) are then read from the registers; the keys and the
 // estimate are those of the selections above.
-template <int T>
-__device__ __forceinline__ void topk_insert(uint64_t (&b)[T], uint64_t c) {
-#pragma unroll
-  for (int t = 0; t < T; t++) {
-    const uint64_t hi = b[t] > c ? b[t] : c;
-    c = b[t] > c ? c : b[t];
-    b[t] = hi;
-  }
-}
-
-// b[i] for a lane-varying i, as masks (a select chain is turned back into a dynamically
-// indexed array, which lives in scratch)
-template <int T>
-__device__ __forceinline__ uint64_t topk_at(const uint64_t (&b)[T], int i) {
-  uint64_t r = 0;
-#pragma unroll
-  for (int t = 0; t < T; t++) r |= b[t] & (0ULL - (uint64_t)(i == t));
-  return r;
-}
-
 template <int T, int MODE>   // MODE 0: every point long, 1: every point double, 2: mixed
 __device__ __forceinline__ void topk_stream(const RawParams& p, int64_t vb, int k, bool is_int, uint64_t (&b)[T],
                                             int& m) {
@@ -2631,20 +2533,13 @@ __global__ __launch_bounds__(256) void k_raw_sel_top(RawParams p) {
   raw_sel_store(p, idx, is_int, fn, m, r1, dif, k0, k1);
 }
 
-// T for k_raw_sel_top when every rank it can be asked for lies within T of the top: m - 1 - r0
-// <= (1 - q) m + 1 for the LEGACY / R_3 / R_7 positions of quantile q over m <= k_max operands
-// (Median: m / 2); 0 = no.
+// T for k_raw_sel_top when every rank it can be asked for lies within T of the top (ksel.h
+// raw_top_need over m <= k_max operands, both reducers); 0 = no.
 int raw_sel_top_t(int fn, int64_t k_max) {
   const char* e = std::getenv("TSDBHIP_RAW_SEL_TOP");   // A/B: 0 = the per-point kernels
   if (e && e[0] == '0') return 0;
-  for (int T : {16, 32}) {
-    if (k_max <= T) return T;
-    if (fn == TSDB_AGG_MEDIAN) continue;
-    const int i = (fn - TSDB_AGG_P999) % 6;
-    const double q = (i == 0 ? 99.9 : i == 1 ? 99.0 : i == 2 ? 95.0 : i == 3 ? 90.0 : i == 4 ? 75.0 : 50.0) / 100.0;
-    if (std::ceil((1.0 - q) * (double)k_max) + 2.0 <= (double)(T - 1)) return T;
-  }
-  return 0;
+  const int need = raw_top_need(fn, k_max, 32);
+  return need <= 16 ? 16 : need <= 32 ? 32 : 0;
 }
 
 // k_max: the largest group of the batch; each wave stages k_max keys in LDS.

@@ -14,7 +14,7 @@
 // its two end points are wave-uniform loads and every window is a plain LERP.
 // m > 0: the span's in-strip ranks are OR-ed into RAW_W 64-bit window masks in LDS; a
 // lane's segment is cursor + popcount(mask bits at or below its position).
-#include "kcommon.h"
+#include "ksel.h"
 
 #ifndef GA_ID
 #error "compile with -DGA_ID=<group aggregator class>"
@@ -562,6 +562,230 @@ __global__ __launch_bounds__(64) void k_raw_vals(RawParams p) {
     // out_int starts at 1; any run of spans that sees a double at the point clears it
     if (RATE || ((flt >> w) & 1)) p.out_int[obase + u] = 0;
   }
+}
+
+// Percentile / median group-by without downsampling, fused (config 4 p99): k_raw_vals'
+// traversal, but each span operand goes into its union point's T largest keys, held in
+// registers (ksel.h topk_insert), instead of the operand arrays -- 9 to 17 B a (span, point),
+// 5e10 operands in config 4, written by k_raw_vals and read back by k_raw_sel_top.  A wave
+// covers RW of a strip's RAW_W windows (64 x RW points; lane l: points ua + 64 (q RW + w) + l),
+// so one strip is RAW_W / RW waves; a span's in-strip ranks still come from the whole strip's
+// window masks.  Valid when every rank the query can ask for lies within T of the top
+// (host: raw_top_need); keys, counts, ranks and estimate are k_raw_sel_top's (runLong keys
+// for long points, runDouble's NaN-free double keys otherwise), so results are bit-identical.
+// MODE 0: long operands only, 1: double only (rate too), 2: both (a key list each).
+template <int T, int RW, int MODE, bool RATE>
+__global__ __launch_bounds__(64) void k_raw_top(RawParams p) {
+  constexpr bool DL = MODE != 1, DD = MODE != 0;
+  constexpr int NL = DL ? T : 1, ND = DD ? T : 1;
+  static_assert(RAW_W % RW == 0, "a strip is a whole number of waves");
+  __shared__ uint64_t wmask[RAW_W];
+  const int lane = lane_id();
+  constexpr int SUB = RAW_W / RW;
+  const int64_t strip = blockIdx.x / SUB;
+  if (strip >= p.n_strips) return;
+  const int q = (int)(blockIdx.x % SUB);
+  const int64_t gi = p.strip_g[strip];
+  const int64_t t = p.strip_t[strip];
+  const int64_t g = gi + p.g0;
+  const int64_t U = p.U[gi];
+  const int64_t ns = (U + RAW_STRIP - 1) / RAW_STRIP;
+  const int64_t ua = t * RAW_STRIP;
+  const int64_t ub = min(U, ua + (int64_t)RAW_STRIP);
+  const int64_t uq = ua + 64 * q * RW;   // this wave's first point
+  if (uq >= ub) return;
+  const int64_t sb = p.grp_ser[g];
+  const int k = (int)(p.grp_ser[g + 1] - sb);
+  constexpr int first = RATE ? 1 : 0;
+  const int interp = p.interp;
+  const int32_t* crow = p.cur + p.cur_off[gi] + t * k;
+  const int32_t* cnext = (t + 1 < ns) ? crow + k : nullptr;
+  const int64_t obase = p.out_off[gi];
+  const uint64_t below = (lane == 63) ? ~0ULL : ((2ULL << lane) - 1ULL);
+  const bool uns = p.uns != 0;
+
+  int64_t x[RW];
+  bool in[RW];
+  uint64_t bl[RW][NL], bd[RW][ND];
+  int ml[RW], md[RW];
+  uint32_t flt = 0, dzm = 0;
+#pragma unroll
+  for (int w = 0; w < RW; w++) {
+    const int64_t u = uq + 64 * w + lane;
+    in[w] = u < ub;
+    x[w] = in[w] ? p.out_ts[obase + u] : 0;
+    ml[w] = md[w] = 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) bl[w][j] = 0;
+#pragma unroll
+    for (int j = 0; j < ND; j++) bd[w][j] = 0;
+  }
+  // one operand of span i at window w (every lane: a lane without one passes ok = false)
+  auto put_l = [&](int w, int64_t v, bool ok) {
+    if (!DL) return;
+    ok = ok && in[w];
+    const uint64_t key = (uint64_t)v ^ 0x8000000000000000ULL;
+    const bool cand = ok && key > bl[w][NL - 1];
+    ml[w] += ok ? 1 : 0;
+    if (__any(cand)) topk_insert<NL>(bl[w], cand ? key : 0);
+  };
+  auto put_d = [&](int w, double v, bool ok) {
+    if (!DD) return;
+    ok = ok && in[w] && !isnan(v);   // runDouble drops NaN operands
+    const uint64_t key = f2key(v);
+    const bool cand = ok && key > bd[w][ND - 1];
+    md[w] += ok ? 1 : 0;
+    if (__any(cand)) topk_insert<ND>(bd[w], cand ? key : 0);
+  };
+  auto put_lerp = [&](int w, const RawPt& a, const RawPt& b, bool ok) {
+    const int64_t x0 = a.tsf & RAW_TIME_MASK, x1 = b.tsf & RAW_TIME_MASK;
+    if (uns) {
+      bool dz = false;
+      if (DL) put_l(w, jlerp_u(interp, x[w], x0, (int64_t)a.bits, x1, (int64_t)b.bits, dz), ok);
+      if (DD) put_d(w, dlerp_u(interp, x[w], x0, pt_double(a.tsf, a.bits), x1, pt_double(b.tsf, b.bits)), ok);
+      if (dz && ok) dzm |= 1u << w;
+    } else {
+      if (DL) put_l(w, jlerp(interp, x[w], x0, (int64_t)a.bits, x1, (int64_t)b.bits), ok);
+      if (DD) put_d(w, dlerp(interp, x[w], x0, pt_double(a.tsf, a.bits), x1, pt_double(b.tsf, b.bits)), ok);
+    }
+  };
+
+  for (int i = 0; i < k; i++) {
+    const int64_t s = sb + i;
+    const int n = p.sp_n[s];
+    if (n < (RATE ? 2 : 1)) continue;
+    const int nc = n - first;
+    const RawPt* pts = p.pts + p.sp_off[s];
+    const int c = crow[i];
+    const int m = (cnext ? cnext[i] : nc) - c;
+    if (m == 0) {
+      if (RATE) {
+        if (c == nc) continue;
+        const double y = __longlong_as_double((long long)pts[c].bits);
+#pragma unroll
+        for (int w = 0; w < RW; w++) put_d(w, y, true);
+      } else {
+        if (c == 0) {
+          if (pts[0].tsf & RAW_FLOAT) flt = (1u << RW) - 1;
+          continue;
+        }
+        if (c == n) continue;
+        const RawPt a = pts[c - 1], b = pts[c];
+        if ((a.tsf | b.tsf) & RAW_FLOAT) flt = (1u << RW) - 1;
+        if (DL && p.lerp_fast) {   // the strip-wide window (lerpw_*, as in k_raw_eval)
+          const int64_t x0 = a.tsf & RAW_TIME_MASK, x1 = b.tsf & RAW_TIME_MASK;
+          const LerpW L = lerpw_init(interp, uns, x0, (int64_t)a.bits, x1, (int64_t)b.bits);
+          if (L.ok) {
+#pragma unroll
+            for (int w = 0; w < RW; w++) {
+              put_l(w, lerpw_eval(L, x[w]), true);
+              if (DD) put_d(w, dlerp(interp, x[w], x0, pt_double(a.tsf, a.bits), x1, pt_double(b.tsf, b.bits)), true);
+            }
+            continue;
+          }
+        }
+#pragma unroll
+        for (int w = 0; w < RW; w++) put_lerp(w, a, b, true);
+      }
+      continue;
+    }
+    if (lane < RAW_W) wmask[lane] = 0;
+    WAVE_SYNC();
+    const int32_t* rk = p.rank + p.sp_off[s] + first + c;
+    for (int l = lane; l < m; l += 64) {
+      const int64_t o = rk[l] - ua;
+      __hip_atomic_fetch_or(&wmask[o >> 6], 1ULL << (o & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    WAVE_SYNC();
+    int tb = 0;
+    for (int w2 = 0; w2 < q * RW; w2++) tb += __popcll(wmask[w2]);   // the span's ranks before this wave's points
+#pragma unroll
+    for (int w = 0; w < RW; w++) {
+      const uint64_t M = wmask[q * RW + w];
+      const int cnt = c + tb + __popcll(M & below);
+      const bool own = (M >> lane) & 1ULL;
+      tb += __popcll(M);
+      if (RATE) {
+        const bool ok = !(cnt == nc && !own);
+        put_d(w, ok ? __longlong_as_double((long long)pts[min(cnt, nc - 1)].bits) : 0.0, ok);
+      } else {
+        if (cnt == 0) {
+          if (pts[0].tsf & RAW_FLOAT) flt |= 1u << w;
+          put_l(w, 0, false);
+          put_d(w, 0.0, false);
+          continue;
+        }
+        const int j = cnt - 1;
+        const RawPt a = pts[j];
+        const bool exact = j == n - 1 || own;   // the span's own point (or its last one)
+        const bool ok = !(j == n - 1 && !own);
+        if (exact) {
+          if (ok) {
+            if (a.tsf & RAW_FLOAT) flt |= 1u << w;
+            if (j < n - 1 && (pts[j + 1].tsf & RAW_FLOAT)) flt |= 1u << w;
+          }
+          put_l(w, (int64_t)a.bits, ok);
+          put_d(w, pt_double(a.tsf, a.bits), ok);
+          continue;
+        }
+        const RawPt b = pts[j + 1];
+        if ((a.tsf | b.tsf) & RAW_FLOAT) flt |= 1u << w;
+        put_lerp(w, a, b, true);
+      }
+    }
+    WAVE_SYNC();
+  }
+
+  const int fn = p.sel_fn;
+#pragma unroll
+  for (int w = 0; w < RW; w++) {
+    if (!in[w]) continue;
+    const int64_t idx = obase + uq + 64 * w + lane;
+    const bool is_int = !RATE && !((flt >> w) & 1);
+    if (uns && ((dzm >> w) & 1)) p.dz[idx] = 1;
+    const int m = is_int ? ml[w] : md[w];
+    int r0, r1;
+    double dif;
+    raw_sel_ranks(fn, is_int, m, r0, r1, dif);
+    uint64_t k0 = 0, k1 = 0;
+    if (m > 0) {
+      const int i0 = m - 1 - r0, i1 = r1 >= 0 ? m - 1 - r1 : i0;   // positions from the top
+      if (i0 >= T || i0 < 0 || i1 < 0) {
+        set_err(p.err, TSDB_E_HIP);   // planning error: the rank is not among the kept keys
+        continue;
+      }
+      if (is_int) {
+        if (DL) { k0 = topk_at<NL>(bl[w], i0); k1 = topk_at<NL>(bl[w], i1); }
+        else set_err(p.err, TSDB_E_HIP);   // planning error: an integer point without long operands
+      } else {
+        if (DD) { k0 = topk_at<ND>(bd[w], i0); k1 = topk_at<ND>(bd[w], i1); }
+        else set_err(p.err, TSDB_E_HIP);
+      }
+    }
+    raw_sel_store(p, idx, is_int, fn, m, r1, dif, k0, k1);
+    p.out_int[idx] = is_int ? 1 : 0;
+  }
+}
+
+// T: keys kept a point (8 / 16 / 32, >= raw_top_need); 0 when the query is not fused
+hipError_t launch_raw_top(const RawParams& p, int T, hipStream_t s) {
+  if (p.n_strips == 0) return hipSuccess;
+  const int mode = p.rate ? 1 : (p.do_long && p.do_double) ? 2 : p.do_long ? 0 : 1;
+#define RAW_TOP(TT, RW)                                                                                        \
+  do {                                                                                                        \
+    const dim3 grid((unsigned)(p.n_strips * (RAW_W / (RW)))), block(64);                                     \
+    if (p.rate) hipLaunchKernelGGL((k_raw_top<TT, RW, 1, true>), grid, block, 0, s, p);                       \
+    else if (mode == 0) hipLaunchKernelGGL((k_raw_top<TT, RW, 0, false>), grid, block, 0, s, p);              \
+    else if (mode == 1) hipLaunchKernelGGL((k_raw_top<TT, RW, 1, false>), grid, block, 0, s, p);              \
+    else hipLaunchKernelGGL((k_raw_top<TT, (RW > 1 ? RW / 2 : 1), 2, false>),                                \
+                            dim3((unsigned)(p.n_strips * (RAW_W / (RW > 1 ? RW / 2 : 1)))), block, 0, s, p);  \
+  } while (0)
+  if (T == 8) RAW_TOP(8, 4);
+  else if (T == 16) RAW_TOP(16, 2);
+  else if (T == 32) RAW_TOP(32, 1);
+  else return hipErrorInvalidValue;
+#undef RAW_TOP
+  return hipGetLastError();
 }
 
 hipError_t launch_raw_vals(const RawParams& p, int64_t k_max, hipStream_t s) {

@@ -75,13 +75,14 @@ def outcome(fn):
         return None, e.java
 
 
-def check(eng, b, q, agg, ctx):
-    """Same result bit for bit, or the same Java exception; returns whether a result came back."""
+def check(eng, b, q, agg, ctx, tol=0.0):
+    """Same result bit for bit (tol None: the downsampled path's group-by tolerance),
+    or the same Java exception; returns whether a result came back."""
     want, werr = outcome(lambda: O.run_query(b, q))
     got, gerr = outcome(lambda: eng.run_batch(b, q))
     assert gerr == werr, f"{ctx}: engine {gerr} vs oracle {werr}"
     if werr is None:
-        assert_groups_match(got, want, agg, tol=0.0, ctx=ctx)
+        assert_groups_match(got, want, agg, tol=tol, ctx=ctx)
     return werr is None
 
 
@@ -181,7 +182,9 @@ def test_unsorted_downsampled(eng, seed, agg, ds, iv):
     that recedes joins the interval it follows, not its own (RowSeq.Iterator does not sort)."""
     b = unsorted_batch(seed, swap_p=0.25, dup_p=0.05)
     q = abi.new_query(T0 + 600, T0 + 6599, agg, ds_function=abi.AGG[ds], ds_interval_ms=iv * 1000)
-    assert check(eng, b, q, agg, f"ds {seed} {agg} {iv}s-{ds}")
+    # timestamps and the per-span buckets exact; float sums across spans in any order (the
+    # partials path) within REL_TOL unless the aggregator is order-free
+    assert check(eng, b, q, agg, f"ds {seed} {agg} {iv}s-{ds}", tol=None)
 
 
 def test_unsorted_downsampled_known(eng):
@@ -196,6 +199,23 @@ def test_unsorted_downsampled_known(eng):
     (_, ts, bits, _), = got
     assert list(ts) == [(T0 + 60) * 1000, (T0 + 120) * 1000]
     assert [float(v) for v in bits.view(np.float64)] == [3.0, 12.0]
+
+
+@pytest.mark.parametrize("pts,want", [([12930, 12890], 7.0), ([12890, 12930], 9.0), ([12930, 12890, 12940], 15.0)])
+def test_unsorted_seek_row_skip(eng, pts, want):
+    """A 3h1m interval puts the Downsampler's seek point S = T0 + 12900 s inside the scan's first
+    hour row.  Span.seekRow passes over a row whose LAST cell is before S (Span.java:360-380): row
+    [S + 30, S - 10] yields nothing (7 = the next row's 3 + 4), row [S - 10, S + 30] is entered at
+    its first cell at or past S (9), and row [S + 30, S - 10, S + 40] from S + 30 on, the receding
+    S - 10 included (15)."""
+    n = len(pts) + 2
+    b = synth.from_series([synth.encode_rows([(T0 + t) * 1000 for t in pts + [14500, 14600]], list(range(1, n + 1)),
+                                             None, [0] * n, [False] * n)], [0])
+    q = abi.new_query(T0 + 4 * 3600, T0 + 30 * 3600, "sum", ds_function=abi.AGG["sum"], ds_interval_ms=10860 * 1000)
+    got = eng.run_batch(b, q)
+    assert_groups_match(got, O.run_query(b, q), "sum", tol=0.0, ctx=f"seek {pts}")
+    (_, ts, bits, _), = got
+    assert list(ts) == [(T0 + 12900) * 1000] and float(bits.view(np.float64)[0]) == want
 
 
 def test_unsorted_known_walk(eng):
