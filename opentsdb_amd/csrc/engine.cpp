@@ -493,6 +493,8 @@ struct tsdbhip_ctx {
   std::vector<int64_t> ro_res;         // batch position -> resident index
   DevBuf ro_cmap;                      // [n_series] resident index of a value series' count series (-1: none)
   DevBuf ro_partner;                   // [n_rows] a value row's lock-step count row (GridParams.ro_partner)
+  DevBuf ro_pairs;                     // [ro_npairs] the packed value / count row pairs (k_ro_pairs)
+  int64_t ro_npairs = 0;
   // query-time compaction (tsdbhip_load_cells): rows whose compaction failed, raised when a
   // query's scan range covers them (SaltScanner.processRow fails the scan)
   struct CmpErr { int64_t series, row; int64_t base; int32_t code; };
@@ -722,6 +724,8 @@ static void release_batch(tsdbhip_ctx* c) {
   c->ro_res.clear();
   c->ro_cmap.release();
   c->ro_partner.release();
+  c->ro_pairs.release();
+  c->ro_npairs = 0;
   c->cmp_errs.clear();
   c->compact_ms = 0;
 }
@@ -1481,6 +1485,31 @@ extern "C" int tsdbhip_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* r
     }
     HIP_OK(c->ro_partner.ensure((int64_t)partner.size() * 4));
     HIP_OK(hipMemcpy(c->ro_partner.p, partner.data(), partner.size() * 4, hipMemcpyHostToDevice));
+    // the value rows packed with their count rows (k_ro_pack), for avg / count downsampling
+    std::vector<int32_t> vrows, vser;
+    for (int64_t s = 0; s < c->n_series; s++)
+      for (int64_t r = c->h_srp[s]; r < c->h_srp[s + 1]; r++)
+        if (partner[r] != -1) {
+          vrows.push_back((int32_t)r);
+          vser.push_back((int32_t)s);
+        }
+    c->ro_npairs = (int64_t)vrows.size();
+    if (c->ro_npairs && c->n_rows < ((int64_t)1 << 31)) {
+      DevBuf dv, ds;
+      HIP_OK(dv.ensure(c->ro_npairs * 4));
+      HIP_OK(ds.ensure(c->ro_npairs * 4));
+      HIP_OK(hipMemcpy(dv.p, vrows.data(), c->ro_npairs * 4, hipMemcpyHostToDevice));
+      HIP_OK(hipMemcpy(ds.p, vser.data(), c->ro_npairs * 4, hipMemcpyHostToDevice));
+      HIP_OK(c->ro_pairs.ensure(c->ro_npairs * (int64_t)sizeof(RoPair)));
+      HIP_OK(launch_ro_pack(c->rows.as<RowDesc>(), c->ro_partner.as<int32_t>(), dv.as<int32_t>(), ds.as<int32_t>(),
+                            c->qual.as<uint8_t>(), c->ro_npairs, c->ro_pairs.as<RoPair>(), c->stream));
+      const hipError_t e = hipStreamSynchronize(c->stream);
+      dv.release();   // (DevBuf frees nothing on its own)
+      ds.release();
+      HIP_OK(e);
+    } else {
+      c->ro_npairs = 0;
+    }
   }
   return 0;
 }
@@ -2992,8 +3021,15 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
         rp.redo_mark = c->sr_mark.as<uint32_t>();
         rp.ro_partner = c->ro_partner.as<int32_t>();
         const int avg = P.ro_fuse == 1 ? 1 : 0;
-        HIP_OK(launch_seq_rows_ro(rp, avg, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->ro_cmap.as<int64_t>(),
-                                  c->n_rows, c->stream));
+        const char* pe = std::getenv("TSDBHIP_RO_PACK");   // A/B: 0 = k_seq_rows_ro over the rows
+        if (c->ro_npairs > 0 && !(pe && pe[0] == '0')) {
+          rp.ro_pairs = c->ro_pairs.as<RoPair>();
+          HIP_OK(launch_ro_pairs(rp, avg, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->ro_cmap.as<int64_t>(),
+                                 c->ro_npairs, c->stream));
+        } else {
+          HIP_OK(launch_seq_rows_ro(rp, avg, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->ro_cmap.as<int64_t>(),
+                                    c->n_rows, c->stream));
+        }
         GridParams dp = gp;
         dp.tile_list = c->sr_list.as<int32_t>();
         dp.tile_list_n = c->sr_n.as<int32_t>();

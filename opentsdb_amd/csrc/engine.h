@@ -48,6 +48,20 @@ __host__ __device__ inline bool row_nocert(int lsb, double absmax) {
   return isinf(absmax) || 2.0 * absmax * (1.0 + 1e-12) > ldexp(1.0, 52 + lsb);
 }
 
+// A rollup value row with its lock-step count row, packed once per rollup batch (k_ro_pack) for
+// k_ro_pairs: 24 B a pair where k_seq_rows_ro reads two 48-B RowDescs, the partner and the
+// series of every row, count rows included.
+struct RoPair {
+  uint32_t base;    // the rows' base time (s)
+  uint32_t qoff;    // value row: qualifier bytes offset
+  uint32_t voff;    // value row: value bytes offset
+  uint32_t cvoff;   // count row: value bytes offset
+  uint32_t meta;    // ndp | log2 vl << 16 | log2 count vl << 18 | 4-byte qualifiers << 20 | RP_OK
+  int32_t series;   // the value series (resident position)
+};
+static_assert(sizeof(RoPair) == 24, "RoPair layout");
+enum : uint32_t { RP_OK = 0x80000000u };   // k_seq_rows_ro's premises hold for the pair
+
 // Per-tile partial group state, structure of arrays, [tile][K].
 struct Partials {
   double* a;
@@ -130,6 +144,7 @@ struct GridParams {
   uint32_t* redo_mark;         // [n_series] a series is on redo_list (k_seq_rows)
   const int32_t* ro_partner;   // [n_rows] rollup batch: a value row's count row (-1: a count row,
                                // -2: the count series does not mirror the value series' rows)
+  const RoPair* ro_pairs;      // rollup batch: the packed value / count row pairs (k_ro_pairs)
   // k_fast: geometry in "n-units" (seconds when every row has second qualifiers and the
   // interval / slot origin are whole seconds, else milliseconds) and the redo list
   int32_t unit_s;        // 1: n-units are seconds
@@ -530,7 +545,11 @@ hipError_t launch_raw_dz_check(const RawParams& p, int64_t n_out, hipStream_t s)
 hipError_t launch_raw_eval(const RawParams& p, hipStream_t s);
 hipError_t launch_raw_vals(const RawParams& p, int64_t k_max, hipStream_t s);
 hipError_t launch_raw_sel(const RawParams& p, int64_t k_max, hipStream_t s);
-hipError_t launch_raw_top(const RawParams& p, int T, hipStream_t s);   // fused operands + selection (k_raw_eval.hip)
+hipError_t launch_raw_top(const RawParams& p, int T, hipStream_t s);
+hipError_t launch_ro_pack(const RowDesc* rows, const int32_t* partner, const int32_t* vrows, const int32_t* vser,
+                          const uint8_t* qual, int64_t n, RoPair* out, hipStream_t s);
+hipError_t launch_ro_pairs(const GridParams& p, int avg, double* dense, uint8_t* pres, const int64_t* cmap, int64_t n,
+                           hipStream_t s);   // fused operands + selection (k_raw_eval.hip)
 template <int GA> hipError_t launch_raw_eval_inst(const RawParams& p, hipStream_t s);   // k_raw_eval.hip
 hipError_t launch_synth_write(const SynthParams& p, hipStream_t s);
 

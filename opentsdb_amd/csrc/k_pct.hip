@@ -1719,7 +1719,22 @@ __device__ __forceinline__ uint64_t wave_or_u64(uint64_t x) {
   return x;
 }
 
-template <int R>
+// One LDS histogram increment per lane with `in`: the lanes whose bin is the first such lane's
+// add as one atomic of their count, the others one by one.  A column of similar values shares its
+// leading digits, so a pass's keys pile into a few bins and a plain per-lane atomic serialises
+// up to 64 same-address updates per instruction.
+__device__ __forceinline__ void hist_add_agg(uint32_t* hist, bool in, uint32_t bin) {
+  const uint64_t act = __ballot(in);
+  if (!act) return;
+  const int leader = __ffsll((long long)act) - 1;
+  const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bin, leader);
+  const bool same = in && bin == b0;
+  const uint64_t sm = __ballot(same);
+  if (lane_id() == leader) atomicAdd(&hist[b0], (uint32_t)__popcll(sm));
+  if (in && !same) atomicAdd(&hist[bin], 1u);
+}
+
+template <int R, bool AGG = true>
 __device__ uint64_t reg_radix_select(const uint64_t (&key)[R], uint32_t valid, int64_t r, SelShared& S,
                                      unsigned long long* red) {
   const int tid = threadIdx.x;
@@ -1750,8 +1765,11 @@ __device__ uint64_t reg_radix_select(const uint64_t (&key)[R], uint32_t valid, i
     for (int b = tid; b < 256; b += blockDim.x) S.hist[b] = 0;
     __syncthreads();
 #pragma unroll
-    for (int u = 0; u < R; u++)
-      if ((valid >> u & 1) && (key[u] & mask) == prefix) atomicAdd(&S.hist[(key[u] >> shift) & 255], 1u);
+    for (int u = 0; u < R; u++) {
+      const bool in = (valid >> u & 1) && (key[u] & mask) == prefix;
+      if (AGG) hist_add_agg(S.hist, in, (uint32_t)(key[u] >> shift) & 255u);
+      else if (in) atomicAdd(&S.hist[(key[u] >> shift) & 255], 1u);
+    }
     __syncthreads();
     if (tid < 64) {
       uint32_t c[4], t = 0;
@@ -1803,7 +1821,7 @@ __device__ uint64_t reg_radix_select(const uint64_t (&key)[R], uint32_t valid, i
   return prefix;
 }
 
-template <int OCC>
+template <int OCC, bool AGG = true>
 __global__ __launch_bounds__(SEL_REG_T, OCC) void k_sel_reg(SelParams p) {
   __shared__ SelShared S;
   __shared__ unsigned long long red[2];
@@ -1857,7 +1875,7 @@ __global__ __launch_bounds__(SEL_REG_T, OCC) void k_sel_reg(SelParams p) {
   }
   double v0 = NAN, v1 = NAN;
   if (m > 0) {
-    const uint64_t k0 = reg_radix_select<SEL_REG_R>(key, valid, r0, S, red);
+    const uint64_t k0 = reg_radix_select<SEL_REG_R, AGG>(key, valid, r0, S, red);
     v0 = key2f(k0);
     if (r1 >= 0) {
       // rank r0 + 1: the same key when more than r0 + 1 keys are <= k0, else the next larger key
@@ -2105,7 +2123,9 @@ hipError_t launch_sel_seg(const SelParams& p, hipStream_t s, int64_t maxn) {
       else hipLaunchKernelGGL((k_sel_reg2<2, 4>), dim3((unsigned)(per2 * 8)), dim3(SEL_REG_T), 0, s, p);
       return hipGetLastError();
     }
+    const char* aenv = std::getenv("TSDBHIP_SEL_AGG");   // A/B: 0 = one histogram atomic per key
     if (oenv && oenv[0] == '4') hipLaunchKernelGGL(k_sel_reg<4>, dim3((unsigned)(per * 8)), dim3(SEL_REG_T), 0, s, p);
+    else if (aenv && aenv[0] == '0') hipLaunchKernelGGL((k_sel_reg<8, false>), dim3((unsigned)(per * 8)), dim3(SEL_REG_T), 0, s, p);
     else hipLaunchKernelGGL(k_sel_reg<8>, dim3((unsigned)(per * 8)), dim3(SEL_REG_T), 0, s, p);
     return hipGetLastError();
   }

@@ -30,6 +30,9 @@ for k, d in acc.items():
         print(f"   => VALU issue utilisation {m['SQ_INSTS_VALU'] * 4 / (1024 * cyc):.3f} "
               f"(SQ_INSTS_VALU x 4 / (1024 SIMDs x {cyc:.4g} cycles))")
     if "SQ_WAVE_CYCLES" in m and m["SQ_WAVE_CYCLES"]:
-        for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"):
+        for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_WAIT_INST_LDS",
+                  "SQ_ACTIVE_INST_LDS"):
             if c in m:
                 print(f"   => {c} / SQ_WAVE_CYCLES {m[c] / m['SQ_WAVE_CYCLES']:.3f}")
+    if m.get("SQ_INSTS_LDS") and "SQ_LDS_BANK_CONFLICT" in m:
+        print(f"   => SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS {m['SQ_LDS_BANK_CONFLICT'] / m['SQ_INSTS_LDS']:.3f} cycles")

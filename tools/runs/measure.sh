@@ -6,6 +6,8 @@
 #             config 2 weak + config 3 strong at 1M series)                     -> md2.jsonl, md4.jsonl
 #   c4        tools/bench_configs.py --config 4 (steps listed) and a TSDBHIP_TRACE=1 rerun -> c4*.jsonl
 #   pmc_hwin  rocprofv3 PMC passes over the day's sum:1m-avg (k_hwin)           -> pmc_hwin/summary.txt
+#   ro        tools/rollup_read_bench.py --check (default and TSDBHIP_RO_PACK=0), traced rerun -> ro*.jsonl
+#   pmc_c3p99 PMC passes (LDS pass included) over config 3's sum / p99:1m-avg   -> pmc_c3p99_summary.txt
 # Every GPU step under its own timeout; the first failure ends the pass.
 set -o pipefail
 tag=$1; shift
@@ -47,6 +49,22 @@ for k,v in d['extra']['config3_strong'].items():
 import json
 for l in open('$out/c4.jsonl'):
     d=json.loads(l); print(d['query'], 'mean', round(d['ms_per_step'],1), 'median', round(d['step_ms_median'],1), 'eval', round(d['k_raw_eval_ms'],1), 'steps', d['steps_ms'], 'dev', d['device_steps_ms'])" ;;
+    ro)
+      timeout -k 10 300 python3 -u tools/rollup_read_bench.py --check > $out/ro.jsonl 2> $out/ro.err \
+        || { tail -20 $out/ro.err; exit 1; }
+      TSDBHIP_RO_PACK=0 timeout -k 10 300 python3 -u tools/rollup_read_bench.py > $out/ro_nopack.jsonl 2> $out/ro_nopack.err \
+        || { tail -20 $out/ro_nopack.err; exit 1; }
+      TSDBHIP_TRACE=1 timeout -k 10 300 python3 -u tools/rollup_read_bench.py --steps 3 > $out/ro_trace.jsonl \
+        2> $out/ro_trace.txt || { tail -20 $out/ro_trace.txt; exit 1; }
+      python3 -c "
+import json
+for f in ('ro', 'ro_nopack'):
+    for l in open('$out/' + f + '.jsonl'):
+        d=json.loads(l); print(f, d['query'], 'ms', round(d['ms_per_step'],3), 'dev', round(d.get('device_decode_downsample_ms',0),3), d.get('check',''))" ;;
+    pmc_c3p99)
+      PMC_LDS=1 bash tools/pmc_run.sh ${tag}_c3p99 python3 tools/bench_configs.py --config 3 --only sum,p99 --steps 1 \
+        || exit $?
+      python3 tools/pmc_summary.py gpurun_out/pmc_${tag}_c3p99 | tee $out/pmc_c3p99_summary.txt ;;
     pmc_hwin)
       bash tools/pmc_run.sh ${tag}_hwin python3 tools/c3day_bench.py --only 1m --steps 1 || exit $?
       python3 tools/pmc_summary.py gpurun_out/pmc_${tag}_hwin k_hwin | tee $out/pmc_hwin_summary.txt ;;
