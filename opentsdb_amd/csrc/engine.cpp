@@ -909,6 +909,7 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
   HIP_OK(hipEventRecord(c->ev[3], c->stream));   // (the allocation is not index time)
   HIP_OK(index_rows(c->qual.as<uint8_t>(), c->val.as<uint8_t>(), c->val2.as<uint8_t>(), c->rows.as<RowDesc>(), ib, ik,
                     c->n_rows, c->err.as<int32_t>(), generic, c->stream));
+  HIP_OK(index_recede(c->rows.as<RowDesc>(), c->srp.as<int64_t>(), c->qual.as<uint8_t>(), c->n_series, c->stream));
   HIP_OK(hipEventRecord(c->ev[1], c->stream));
   std::vector<RowDesc> back(c->n_rows);
   if (c->n_rows)

@@ -496,6 +496,8 @@ hipError_t index_classes(const uint8_t* qual, const RowDesc* rows, const IndexBu
                          IndexClasses* out, hipStream_t s);
 hipError_t index_rows(const uint8_t* qual, const uint8_t* val, uint8_t* val2, RowDesc* rows, const IndexBufs& b,
                       const IndexClasses& k, int64_t n_rows, int32_t* err, bool generic, hipStream_t s);
+// rows whose first datapoint is not after the series' earlier rows' datapoints: ROW_UNSORTED
+hipError_t index_recede(RowDesc* rows, const int64_t* srp, const uint8_t* qual, int64_t n_series, hipStream_t s);
 hipError_t launch_grid(const GridParams& p, int ds_function_class, hipStream_t s);
 // k_fast: uniform float rows of one (qualifier width, value length) class; returns
 // hipErrorNotSupported when no specialisation exists for (f, qw, vl)

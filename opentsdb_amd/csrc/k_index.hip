@@ -768,4 +768,56 @@ hipError_t index_rows(const uint8_t* qual, const uint8_t* val, uint8_t* val2, Ro
   return hipGetLastError();
 }
 
+// ---- k_recede: datapoints going back in time across a series' rows -------------------------
+// Span.Iterator yields a series' rows in base-time order and each row's cells in column order;
+// the downsamplers and AggregationIterator read that stream as it comes (kcommon.h "stream
+// order").  A row whose first datapoint is not after every datapoint of the series' earlier rows
+// (two rows of one hour, an offset past the hour in the row before) breaks the time order
+// across rows as an unsorted cell does inside one, so it is flagged ROW_UNSORTED too: every
+// streaming kernel hands it to the stored-order paths (k_grid's running max, k_raw_merge's
+// greedy walk).  One thread a series, rows in their (sorted) order.
+__device__ __forceinline__ int64_t qual_ms_at(const uint8_t* q, uint32_t pos, int qw) {
+  if (qw == 4 || (qw != 2 && (q[pos] & 0xF0) == 0xF0)) {
+    const uint32_t w = ((uint32_t)q[pos] << 24) | ((uint32_t)q[pos + 1] << 16) | ((uint32_t)q[pos + 2] << 8) | q[pos + 3];
+    return (w & 0x0FFFFFC0u) >> 6;
+  }
+  return (int64_t)(((((uint32_t)q[pos] << 8) | q[pos + 1]) >> 4) & 0xFFF) * 1000;
+}
+
+__global__ __launch_bounds__(256) void k_recede(RowDesc* __restrict__ rows, const int64_t* __restrict__ srp,
+                                                const uint8_t* __restrict__ qual, int64_t n_series) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_series) return;
+  int64_t M = INT64_MIN;   // latest datapoint of the earlier rows
+  for (int64_t r = srp[s]; r < srp[s + 1]; r++) {
+    const RowDesc d = rows[r];
+    if ((d.flags & ROW_ERR) || d.ndp == 0) continue;
+    const uint8_t* q = qual + d.qoff;
+    const int qw = d.flags & ROW_QW_MASK;
+    const int64_t b = (int64_t)d.base * 1000;
+    const int64_t first = b + qual_ms_at(q, 0, qw);
+    int64_t mx;
+    if (!(d.flags & ROW_UNSORTED) && (qw == 2 || qw == 4)) {
+      mx = b + qual_ms_at(q, (d.ndp - 1) * (uint32_t)qw, qw);
+    } else {   // a mixed-width row: walk to its last cell; a row out of order: its latest cell
+      mx = INT64_MIN;
+      uint32_t pos = 0;
+      for (uint32_t i = 0; i < d.ndp && pos < d.qlen; i++) {
+        const int w = qw ? qw : ((q[pos] & 0xF0) == 0xF0 ? 4 : 2);
+        const int64_t t = b + qual_ms_at(q, pos, qw);
+        mx = (d.flags & ROW_UNSORTED) ? max(mx, t) : t;
+        pos += w;
+      }
+    }
+    if (first <= M) rows[r].flags = d.flags | ROW_UNSORTED;
+    M = max(M, mx);
+  }
+}
+
+hipError_t index_recede(RowDesc* rows, const int64_t* srp, const uint8_t* qual, int64_t n_series, hipStream_t s) {
+  if (n_series <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_recede, dim3((unsigned)((n_series + 255) / 256)), dim3(256), 0, s, rows, srp, qual, n_series);
+  return hipGetLastError();
+}
+
 }  // namespace tsdb

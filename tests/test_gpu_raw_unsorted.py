@@ -218,6 +218,32 @@ def test_unsorted_seek_row_skip(eng, pts, want):
     assert list(ts) == [(T0 + 12900) * 1000] and float(bits.view(np.float64)[0]) == want
 
 
+def _row(base, pts):
+    """One hour row of 2-byte second qualifiers and 1-byte integers, offsets as given (up to
+    4095 s: Internal.java's 12-bit offset)."""
+    q = b"".join(((off << 4) | 0x0).to_bytes(2, "big") for off, _ in pts)
+    v = b"".join(int(x).to_bytes(1, "big", signed=True) for _, x in pts)
+    return (base, q, v)
+
+
+@pytest.mark.parametrize("agg,ds", [("sum", "sum"), ("sum", "avg"), ("count", "count"), ("sum", None), ("p50", None),
+                                    ("avg", None), ("sum", "last")])
+def test_rows_recede_across_hour(eng, agg, ds):
+    """Row T0 holds an offset past its hour (3700 s, a 2-byte qualifier reaches 4095 s); the next
+    row's first datapoint (3650 s) lies before it.  Span.Iterator yields rows in order, so the
+    stream goes back in time across the rows: k_recede flags the second row, and the downsampled
+    path (stored order: 3650 joins the interval of 3700) and the raw greedy walk take it.  A
+    second span keeps the group-by honest."""
+    a = [_row(T0, [(100, 1), (3700, 2)]), _row(T0 + 3600, [(50, 4), (200, 8)])]
+    b = [_row(T0, [(30, 16), (3000, 32)]), _row(T0 + 3600, [(60, 64), (300, 96)])]
+    batch = synth.from_series([a, b], [0, 0])
+    if ds:
+        q = abi.new_query(T0, T0 + 7199, agg, ds_function=abi.AGG[ds], ds_interval_ms=60000)
+    else:
+        q = abi.new_query(T0, T0 + 7199, agg)
+    assert check(eng, batch, q, agg, f"recede {agg} {ds}", tol=None if ds else 0.0)
+
+
 def test_unsorted_known_walk(eng):
     """A = [10 s, 5 s], B = [5 s, 20 s] (long values): steps 5 (B), 10 (A), 5 (A), 20 (B).  At
     the third step B's window is (5 s, 20 s) with x == x0: B's own value 2, not a LERP."""
