@@ -707,7 +707,7 @@ __global__ __launch_bounds__(64) void k_raw_top(RawParams p) {
       tb += __popcll(M);
       if (RATE) {
         const bool ok = !(cnt == nc && !own);
-        put_d(w, ok ? __longlong_as_double((long long)pts[min(cnt, nc - 1)].bits) : 0.0, ok);
+        put_d(w, ok ? __longlong_as_double((long long)pts[cnt].bits) : 0.0, ok);   // (n = nc + 1 points)
       } else {
         if (cnt == 0) {
           if (pts[0].tsf & RAW_FLOAT) flt |= 1u << w;
