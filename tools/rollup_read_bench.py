@@ -93,8 +93,10 @@ def main():
             eng.run(q)
         eng.sync()
         t = time.perf_counter()
+        cc = 0.0
         for _ in range(a.steps):
             eng.run(q)
+            cc += eng.last_call_ms
         eng.sync()
         ms = (time.perf_counter() - t) * 1000 / a.steps
         tm = eng.timing()
@@ -108,6 +110,7 @@ def main():
                 "cells_per_s": n_cells / (ms / 1000), "algorithmic_bytes": alg,
                 "algorithmic_GBps": alg / (ms / 1000) / 1e9, "hbm_frac_of_8tbs": alg / (ms / 1000) / 8e12,
                 "device_decode_downsample_ms": tm.decode_downsample_ms, "group_reduce_ms": tm.group_reduce_ms,
+                "c_call_ms": cc / a.steps, "device_total_ms": tm.total_ms,
                 "gen_s": gen_s, "load_s": load_s}
         if a.check:
             from oracle import oracle as O
