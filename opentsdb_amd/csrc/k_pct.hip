@@ -210,21 +210,6 @@ struct SelWave {
   uint32_t n;
 };
 
-__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
-  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
-  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
-  return ((uint64_t)hi << 32) | lo;
-}
-
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const uint64_t o = shfl_u64(v, lane_id() ^ d);
-    v = o < v ? o : v;
-  }
-  return v;
-}
-
 __device__ __forceinline__ int wave_sum_int(int v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);

@@ -574,8 +574,6 @@ __global__ __launch_bounds__(64) void k_raw_vals(RawParams p) {
 // (host: raw_top_need); keys, counts, ranks and estimate are k_raw_sel_top's (runLong keys
 // for long points, runDouble's NaN-free double keys otherwise), so results are bit-identical.
 // MODE 0: long operands only, 1: double only (rate too), 2: both (a key list each).
-constexpr uint32_t RAW_TOP_CB = 8;   // candidate keys a lane buffers per window before a fold
-
 template <int T, int RW, int MODE, bool RATE>
 __global__ __launch_bounds__(64) void k_raw_top(RawParams p) {
   constexpr bool DL = MODE != 1, DD = MODE != 0;
@@ -609,7 +607,6 @@ __global__ __launch_bounds__(64) void k_raw_top(RawParams p) {
   int64_t x[RW];
   bool in[RW];
   uint64_t bl[RW][NL], bd[RW][ND];
-  __shared__ uint64_t cbl[DL ? RW : 1][DL ? 64 * RAW_TOP_CB : 1], cbd[DD ? RW : 1][DD ? 64 * RAW_TOP_CB : 1];   // [w][slot][lane]
   int ml[RW], md[RW];
   uint32_t flt = 0, dzm = 0;
 #pragma unroll
@@ -624,27 +621,27 @@ __global__ __launch_bounds__(64) void k_raw_top(RawParams p) {
     for (int j = 0; j < ND; j++) bd[w][j] = 0;
   }
   // one operand of span i at window w (every lane: a lane without one passes ok = false)
-  // A key above the lane's current T-th goes to the lane's candidate buffer in LDS; the buffer is
-  // folded into the registers (topk_insert, ~5 VALU a kept key) when full and at the end.  An
-  // insertion straight into the registers costs the whole wave whenever ANY lane has a candidate
-  // -- at most spans of a 1563-span group some lane of 64 does -- where the buffered fold costs
-  // each lane only its own candidates (~6 % of the operands for p99).
-  uint32_t cl[RW], cd[RW];   // buffered candidates a window
+  // thr: the wave's smallest T-th key over its points (wave-uniform, refreshed after an
+  // insertion): a span whose operands all lie below it cannot enter any point's top T
+  uint64_t thr = 0;
+  auto refresh = [&]() {
+    uint64_t t = ~0ULL;
 #pragma unroll
-  for (int w = 0; w < RW; w++) cl[w] = cd[w] = 0;
-  auto fold = [&](uint64_t (&b)[T], const uint64_t* buf, uint32_t& cnt) {
-    for (uint32_t t = 0; t < cnt; t++) topk_insert<T>(b, buf[t * 64]);
-    cnt = 0;
+    for (int w = 0; w < RW; w++) {
+      if (DL && in[w]) t = min(t, bl[w][NL - 1]);
+      if (DD && in[w]) t = min(t, bd[w][ND - 1]);
+    }
+    thr = wave_min_u64(t);
   };
   auto put_l = [&](int w, int64_t v, bool ok) {
     if constexpr (DL) {
       ok = ok && in[w];
       const uint64_t key = (uint64_t)v ^ 0x8000000000000000ULL;
+      const bool cand = ok && key > bl[w][NL - 1];
       ml[w] += ok ? 1 : 0;
-      if (ok && key > bl[w][NL - 1]) {
-        uint64_t* buf = &cbl[w][lane];
-        buf[cl[w] * 64] = key;
-        if (++cl[w] == RAW_TOP_CB) fold(bl[w], buf, cl[w]);
+      if (__any(cand)) {
+        topk_insert<NL>(bl[w], cand ? key : 0);
+        refresh();
       }
     }
   };
@@ -652,12 +649,20 @@ __global__ __launch_bounds__(64) void k_raw_top(RawParams p) {
     if constexpr (DD) {
       ok = ok && in[w] && !isnan(v);   // runDouble drops NaN operands
       const uint64_t key = f2key(v);
+      const bool cand = ok && key > bd[w][ND - 1];
       md[w] += ok ? 1 : 0;
-      if (ok && key > bd[w][ND - 1]) {
-        uint64_t* buf = &cbd[w][lane];
-        buf[cd[w] * 64] = key;
-        if (++cd[w] == RAW_TOP_CB) fold(bd[w], buf, cd[w]);
+      if (__any(cand)) {
+        topk_insert<ND>(bd[w], cand ? key : 0);
+        refresh();
       }
+    }
+  };
+  // every point of the wave takes one operand of this span, none of which can enter a top T
+  auto skip_all = [&](bool count_l, bool count_d) {
+#pragma unroll
+    for (int w = 0; w < RW; w++) {
+      if (count_l) ml[w] += in[w] ? 1 : 0;
+      if (count_d) md[w] += in[w] ? 1 : 0;
     }
   };
   auto put_lerp = [&](int w, const RawPt& a, const RawPt& b, bool ok) {
@@ -685,6 +690,7 @@ __global__ __launch_bounds__(64) void k_raw_top(RawParams p) {
       if (RATE) {
         if (c == nc) continue;
         const double y = __longlong_as_double((long long)pts[c].bits);
+        if (!isnan(y) && f2key(y) < thr) { skip_all(false, true); continue; }   // (the same operand at every point)
 #pragma unroll
         for (int w = 0; w < RW; w++) put_d(w, y, true);
       } else {
@@ -695,9 +701,21 @@ __global__ __launch_bounds__(64) void k_raw_top(RawParams p) {
         if (c == n) continue;
         const RawPt a = pts[c - 1], b = pts[c];
         if ((a.tsf | b.tsf) & RAW_FLOAT) flt = (1u << RW) - 1;
+        const int64_t x0 = a.tsf & RAW_TIME_MASK, x1 = b.tsf & RAW_TIME_MASK;
+        if (MODE == 1 && !uns && interp == TSDB_INTERP_LERP) {
+          // a double LERP strictly inside (x0, x1) stays within [y0, y1] up to a few ulps of
+          // rounding: skipped when even 8 key steps (ulps) above the larger end lie below thr
+          const double y0 = pt_double(a.tsf, a.bits), y1 = pt_double(b.tsf, b.bits);
+          if (isfinite(y0) && isfinite(y1) && f2key(fmax(y0, y1)) + 8 < thr) { skip_all(false, true); continue; }
+        }
         if (DL && p.lerp_fast) {   // the strip-wide window (lerpw_*, as in k_raw_eval)
-          const int64_t x0 = a.tsf & RAW_TIME_MASK, x1 = b.tsf & RAW_TIME_MASK;
           const LerpW L = lerpw_init(interp, uns, x0, (int64_t)a.bits, x1, (int64_t)b.bits);
+          // exact long LERP strictly inside the window: y0 + trunc((x - x0) dy / (x1 - x0)) lies
+          // within [y0, y1]
+          if (MODE == 0 && L.ok && ((uint64_t)max((int64_t)a.bits, (int64_t)b.bits) ^ 0x8000000000000000ULL) < thr) {
+            skip_all(true, false);
+            continue;
+          }
           if (L.ok) {
 #pragma unroll
             for (int w = 0; w < RW; w++) {
@@ -759,11 +777,6 @@ __global__ __launch_bounds__(64) void k_raw_top(RawParams p) {
     WAVE_SYNC();
   }
 
-#pragma unroll
-  for (int w = 0; w < RW; w++) {   // the buffered candidates left
-    if constexpr (DL) fold(bl[w], &cbl[w][lane], cl[w]);
-    if constexpr (DD) fold(bd[w], &cbd[w][lane], cd[w]);
-  }
   const int fn = p.sel_fn;
 #pragma unroll
   for (int w = 0; w < RW; w++) {

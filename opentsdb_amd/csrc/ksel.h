@@ -88,6 +88,22 @@ __device__ __forceinline__ void raw_sel_store(const RawParams& p, int64_t idx, b
   p.out_bits[idx] = bits;
 }
 
+// 64-bit shuffles and the wave minimum of 64-bit keys
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint64_t o = shfl_u64(v, lane_id() ^ d);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
 // The T largest keys seen, sorted descending (k_raw_sel_top, k_raw_top): insertion is a
 // compare-exchange chain; inserting key 0 (below every operand's key) changes nothing.
 template <int T>
