@@ -1719,9 +1719,14 @@ __device__ __forceinline__ void hist_add_agg(uint32_t* hist, bool in, uint32_t b
   if (in && !same) atomicAdd(&hist[bin], 1u);
 }
 
-template <int R, bool AGG = true>
+// WIDE: the first digit is the 12 bits below the prefix every key shares (a 4096-bin histogram,
+// H, in LDS; WT: the 16 waves' totals of its block-wide scan), then 8-bit digits as before.  A
+// column of similar doubles differs first in its exponent: the 12 bits take the exponent and the
+// leading mantissa bits in one pass, and the bin of rank r usually holds few enough keys to rank
+// directly -- one histogram pass instead of three.
+template <int R, bool AGG = false, bool WIDE = false>
 __device__ uint64_t reg_radix_select(const uint64_t (&key)[R], uint32_t valid, int64_t r, SelShared& S,
-                                     unsigned long long* red) {
+                                     unsigned long long* red, uint32_t* H = nullptr, int* WT = nullptr) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   uint64_t kand = ~0ULL, kor = 0;
@@ -1743,10 +1748,76 @@ __device__ uint64_t reg_radix_select(const uint64_t (&key)[R], uint32_t valid, i
   __syncthreads();
   const uint64_t band = red[0], bor = red[1];
   if ((band ^ bor) == 0) return band;   // all keys equal
-  const int top = (63 - __clzll((long long)(band ^ bor))) & ~7;
-  uint64_t mask = top == 56 ? 0 : ~((1ULL << (top + 8)) - 1ULL);
-  uint64_t prefix = band & mask;
-  for (int shift = top; shift >= 0; shift -= 8) {
+  // the keys sharing the selected prefix, ranked directly (nc <= SEL_FIN of them)
+  auto gather_rank = [&](uint64_t mask, uint64_t prefix, int64_t rr, uint32_t nc) {
+    if (tid == 0) S.ncand = 0;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < R; u++)
+      if ((valid >> u & 1) && (key[u] & mask) == prefix) S.cand[atomicAdd(&S.ncand, 1u)] = key[u];
+    __syncthreads();
+    if ((uint32_t)tid < nc) {
+      const uint64_t x = S.cand[tid];
+      uint32_t less = 0, eq = 0;
+      for (uint32_t q = 0; q < nc; q++) {
+        const uint64_t y = S.cand[q];
+        less += y < x;
+        eq += y == x;
+      }
+      if ((int64_t)less <= rr && rr < (int64_t)(less + eq)) S.res = x;
+    }
+    __syncthreads();
+    const uint64_t res = S.res;
+    __syncthreads();
+    return res;
+  };
+  int shift;
+  uint64_t mask, prefix;
+  if constexpr (WIDE) {
+    const int h = 63 - __clzll((long long)(band ^ bor));   // the highest bit the keys differ in
+    const int sw = h >= 11 ? h - 11 : 0;                   // digit [sw, sw + 12) (bits above h shared)
+    const uint64_t above = h == 63 ? 0 : ~((1ULL << (h + 1)) - 1ULL);
+    prefix = band & above;
+    reinterpret_cast<uint4*>(H)[tid] = make_uint4(0u, 0u, 0u, 0u);   // (SEL_REG_T x 4 = 4096 bins)
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < R; u++)
+      if (valid >> u & 1) atomicAdd(&H[(key[u] >> sw) & 0xFFFu], 1u);
+    __syncthreads();
+    const uint4 c4 = reinterpret_cast<const uint4*>(H)[tid];
+    const uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
+    const uint32_t t = c[0] + c[1] + c[2] + c[3];
+    const int incl = (int)wave_incl_sum((int)t);
+    if (lane == 63) WT[tid >> 6] = incl;
+    __syncthreads();
+    int woff = 0;
+    for (int w2 = 0; w2 < (tid >> 6); w2++) woff += WT[w2];
+    int64_t ex = (int64_t)woff + incl - t;
+    if (ex <= r && r < ex + (int64_t)t) {
+      int q = 0;
+      for (; q < 3; q++) {
+        if (r < ex + c[q]) break;
+        ex += c[q];
+      }
+      S.bin = (uint64_t)(tid * 4 + q);
+      S.rr = (uint64_t)(r - ex);
+      S.ncand = c[q];
+    }
+    __syncthreads();
+    prefix |= S.bin << sw;
+    mask = above | (0xFFFULL << sw);
+    r = (int64_t)S.rr;
+    const uint32_t nc = S.ncand;
+    __syncthreads();
+    if (sw == 0) return prefix;
+    if (nc <= SEL_FIN) return gather_rank(mask, prefix, r, nc);
+    shift = sw >= 8 ? sw - 8 : 0;   // (below 8: bits [sw, 8) of the next digit are already fixed)
+  } else {
+    shift = (63 - __clzll((long long)(band ^ bor))) & ~7;
+    mask = shift == 56 ? 0 : ~((1ULL << (shift + 8)) - 1ULL);
+    prefix = band & mask;
+  }
+  for (; shift >= 0; shift -= 8) {
     for (int b = tid; b < 256; b += blockDim.x) S.hist[b] = 0;
     __syncthreads();
 #pragma unroll
@@ -1780,36 +1851,17 @@ __device__ uint64_t reg_radix_select(const uint64_t (&key)[R], uint32_t valid, i
     const uint32_t nc = S.ncand;
     __syncthreads();
     if (shift == 0) break;
-    if (nc <= SEL_FIN) {
-      if (tid == 0) S.ncand = 0;
-      __syncthreads();
-#pragma unroll
-      for (int u = 0; u < R; u++)
-        if ((valid >> u & 1) && (key[u] & mask) == prefix) S.cand[atomicAdd(&S.ncand, 1u)] = key[u];
-      __syncthreads();
-      if ((uint32_t)tid < nc) {
-        const uint64_t x = S.cand[tid];
-        uint32_t less = 0, eq = 0;
-        for (uint32_t q = 0; q < nc; q++) {
-          const uint64_t y = S.cand[q];
-          less += y < x;
-          eq += y == x;
-        }
-        if ((int64_t)less <= r && r < (int64_t)(less + eq)) S.res = x;
-      }
-      __syncthreads();
-      const uint64_t res = S.res;
-      __syncthreads();
-      return res;
-    }
+    if (nc <= SEL_FIN) return gather_rank(mask, prefix, r, nc);
   }
   return prefix;
 }
 
-template <int OCC, bool AGG = true>
+template <int OCC, bool AGG = false, bool WIDE = true>
 __global__ __launch_bounds__(SEL_REG_T, OCC) void k_sel_reg(SelParams p) {
   __shared__ SelShared S;
   __shared__ unsigned long long red[2];
+  __shared__ uint32_t H[WIDE ? 4 * SEL_REG_T : 1];
+  __shared__ int WT[SEL_REG_T / 64];
   const int64_t nseg = p.G * p.K;
   const int64_t per = (nseg + 7) / 8;
   const int64_t i = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
@@ -1860,7 +1912,7 @@ __global__ __launch_bounds__(SEL_REG_T, OCC) void k_sel_reg(SelParams p) {
   }
   double v0 = NAN, v1 = NAN;
   if (m > 0) {
-    const uint64_t k0 = reg_radix_select<SEL_REG_R, AGG>(key, valid, r0, S, red);
+    const uint64_t k0 = reg_radix_select<SEL_REG_R, AGG, WIDE>(key, valid, r0, S, red, H, WT);
     v0 = key2f(k0);
     if (r1 >= 0) {
       // rank r0 + 1: the same key when more than r0 + 1 keys are <= k0, else the next larger key
@@ -2108,9 +2160,10 @@ hipError_t launch_sel_seg(const SelParams& p, hipStream_t s, int64_t maxn) {
       else hipLaunchKernelGGL((k_sel_reg2<2, 4>), dim3((unsigned)(per2 * 8)), dim3(SEL_REG_T), 0, s, p);
       return hipGetLastError();
     }
-    const char* aenv = std::getenv("TSDBHIP_SEL_AGG");   // A/B: 0 = one histogram atomic per key
+    // (wave-aggregated histogram atomics, hist_add_agg, measured no faster: profiles/r05s)
+    const char* wenv = std::getenv("TSDBHIP_SEL_WIDE");   // A/B: 0 = 8-bit digits from the top
     if (oenv && oenv[0] == '4') hipLaunchKernelGGL(k_sel_reg<4>, dim3((unsigned)(per * 8)), dim3(SEL_REG_T), 0, s, p);
-    else if (aenv && aenv[0] == '0') hipLaunchKernelGGL((k_sel_reg<8, false>), dim3((unsigned)(per * 8)), dim3(SEL_REG_T), 0, s, p);
+    else if (wenv && wenv[0] == '0') hipLaunchKernelGGL((k_sel_reg<8, false, false>), dim3((unsigned)(per * 8)), dim3(SEL_REG_T), 0, s, p);
     else hipLaunchKernelGGL(k_sel_reg<8>, dim3((unsigned)(per * 8)), dim3(SEL_REG_T), 0, s, p);
     return hipGetLastError();
   }

@@ -1297,10 +1297,11 @@ __device__ __forceinline__ void sel_uni_flush(const GridParams& p, int K, int32_
 // The staged rows of series sa .. sa + nb - 1 (group g, nb <= 8; stage [nb][K]) into their
 // columns: lanes 8c .. 8c + 7 store column k's nb consecutive values (64 B pieces instead of one
 // 8-B store per line).
-__device__ __forceinline__ void sel_cols_flush(const GridParams& p, int K, int32_t g, int64_t sa, int nb,
+// (g0, ng: the group's first series and its series count, loaded by the caller before its load
+// ring starts -- a global load here, consumed at once, would wait for every ring load in flight)
+__device__ __forceinline__ void sel_cols_flush(const GridParams& p, int K, int64_t g0, int64_t ng, int64_t sa, int nb,
                                                const double* stage) {
   WAVE_SYNC();
-  const int64_t g0 = p.group_series_ptr[g], ng = p.group_series_ptr[g + 1] - g0;
   double* base = p.sel_vals + g0 * K + (sa - g0);
   const int lane = lane_id();
   if (nb == 8) {
@@ -2095,6 +2096,7 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
     L.cnt[k] = 0;
     L.w.pres[k] = 0;
   }
+  const int32_t tgrp = p.tile_group[tile];   // (loaded once: see k_short)
   std::conditional_t<KR == 2, MultiReg, RegPart> RP;   // KR 2: the fused multi-aggregator pass
   bool uacc = false;   // sel_direct: this tile's union flags (sel_uni_flush)
   rp_init(p.ga, RP);
@@ -2115,7 +2117,7 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
   for (int i = 0; i < D; i++) {
     if (fast_issue<F, QW, VL>(p, rows, w, buf[i], meta[i]) == 2) redo = true;
   }
-  if ((meta[0].bits & FM_OK) && !redo && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
+  if ((meta[0].bits & FM_OK) && !redo && lane == 0) atomicOr(&p.group_active[tgrp], 1u);
   bool have = false;
   int64_t scur = tbeg[tile];   // series of the rows being folded (dense_out / sel_direct)
   int64_t snb = scur + 1 < tend[tile] ? srp[scur + 1] : INT64_MAX;
@@ -2146,8 +2148,8 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
               s = scur;
             }
             const bool ok =
-                KR ? fast_series_end_reg<F, true, OUT>(p, L, K, lsb, amax, RP, s, p.tile_group[tile], 0, nullptr, &uacc)
-                   : fast_series_end<F>(p, L, K, lsb, amax, s, p.tile_group[tile]);
+                KR ? fast_series_end_reg<F, true, OUT>(p, L, K, lsb, amax, RP, s, tgrp, 0, nullptr, &uacc)
+                   : fast_series_end<F>(p, L, K, lsb, amax, s, tgrp);
             if (!ok) { redo = true; done = true; }
             if (OUT && (p.dense_out || p.sel_direct)) {   // the next series end is a later series
               scur++;
@@ -2183,7 +2185,7 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
     if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
     return;
   }
-  if (OUT && p.sel_direct) sel_uni_flush(p, K, p.tile_group[tile], uacc);
+  if (OUT && p.sel_direct) sel_uni_flush(p, K, tgrp, uacc);
   WAVE_SYNC();
   double* ga_ = p.part.a + tile * K;
   double* gb_ = p.part.b + tile * K;
@@ -2290,6 +2292,16 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
   const int64_t s0 = tbeg[tile];
   const int ns = (int)(tend[tile] - s0);
   const int64_t r0 = srp[s0];
+  // the tile's group bounds for the column layout, loaded before the ring starts (a global load
+  // consumed inside the loop waits for every ring load issued before it)
+  // (and the tile's group: p.tile_group[tile] read inside the loop is reloaded after every store
+  // the compiler cannot tell apart from it -- a load consumed at once, behind the whole ring)
+  const int32_t tgrp = p.tile_group[tile];
+  int64_t cg0 = 0, cgn = 0;
+  if (KR == 3 && p.sel_stage) {
+    cg0 = p.group_series_ptr[tgrp];
+    cgn = p.group_series_ptr[tgrp + 1] - cg0;
+  }
   // premise: one row per series, in the scan range, of this kernel's class, one chunk long
   bool ok = ns <= 64 && srp[s0 + ns] - r0 == ns;
   uint64_t dq = 0, dv = 0, damax = 0;
@@ -2332,7 +2344,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
   }
   std::conditional_t<KR == 2, MultiReg, RegPart> RP;   // KR 2: the fused multi-aggregator pass
   rp_init(p.ga, RP);
-  if (ns > 0 && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
+  if (ns > 0 && lane == 0) atomicOr(&p.group_active[tgrp], 1u);
   WAVE_SYNC();
   // The ring issues unconditionally (series index clamped to the last one) so that the
   // compiler's vmcnt bookkeeping stays exact: a conditional issue makes it wait for every
@@ -2370,12 +2382,12 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     const int lsb = __builtin_amdgcn_readlane(dlsb, j);
     const double amax = __longlong_as_double((long long)rl64(damax, j));
     const bool fine =
-        KR ? fast_series_end_reg<F, false, OUT>(p, L, K, lsb, amax, RP, s0 + j, p.tile_group[tile], (uint32_t)nv0,
+        KR ? fast_series_end_reg<F, false, OUT>(p, L, K, lsb, amax, RP, s0 + j, tgrp, (uint32_t)nv0,
                                                 stage ? stage + (j & 7) * K : nullptr, &uacc)
-           : fast_series_end<F>(p, L, K, lsb, amax, s0 + j, p.tile_group[tile]);
+           : fast_series_end<F>(p, L, K, lsb, amax, s0 + j, tgrp);
     if (!fine) redo = true;
     else if (KR == 3 && stage && ((j & 7) == 7 || j == ns - 1))
-      sel_cols_flush(p, K, p.tile_group[tile], s0 + (j & ~7), (j & 7) + 1, stage);
+      sel_cols_flush(p, K, cg0, cgn, s0 + (j & ~7), (j & 7) + 1, stage);
   };
   int j = 0;
   for (; j + D <= ns; j += D) {
@@ -2402,7 +2414,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     return;
   }
   if (OUT && p.sel_wr && lane < ns) p.sel_wr[s0 + lane] = 1;   // sel_direct: every series of the tile was written
-  if (OUT && p.sel_direct) sel_uni_flush(p, K, p.tile_group[tile], uacc);
+  if (OUT && p.sel_direct) sel_uni_flush(p, K, tgrp, uacc);
   WAVE_SYNC();
   double* ga_ = p.part.a + tile * K;
   double* gb_ = p.part.b + tile * K;
@@ -2493,6 +2505,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     L.cnt[k] = 0;
     L.w.pres[k] = 0;
   }
+  const int32_t tgrp = p.tile_group[tile];   // (loaded once: see k_short)
   std::conditional_t<KR == 2, MultiReg, RegPart> RP;
   bool uacc = false;
   rp_init(p.ga, RP);
@@ -2535,8 +2548,8 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
       if (jr < nr && !redo && __ballot(send == jr + 1) != 0) {   // the last row of its series
         if (have) {
           const int64_t s = s0 + __popcll(__ballot(send <= jr));
-          const bool fine = KR ? fast_series_end_reg<F, true, OUT>(p, L, K, lsb, amax, RP, s, p.tile_group[tile], nser, nullptr, &uacc)
-                               : fast_series_end<F>(p, L, K, lsb, amax, s, p.tile_group[tile]);
+          const bool fine = KR ? fast_series_end_reg<F, true, OUT>(p, L, K, lsb, amax, RP, s, tgrp, nser, nullptr, &uacc)
+                               : fast_series_end<F>(p, L, K, lsb, amax, s, tgrp);
           if (!fine) redo = true;
           any = true;
         }
@@ -2555,8 +2568,8 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
     return;
   }
-  if (any && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
-  if (OUT && p.sel_direct) sel_uni_flush(p, K, p.tile_group[tile], uacc);
+  if (any && lane == 0) atomicOr(&p.group_active[tgrp], 1u);
+  if (OUT && p.sel_direct) sel_uni_flush(p, K, tgrp, uacc);
   WAVE_SYNC();
   if (KR) {
     rp_store(p, tile, K, RP);
