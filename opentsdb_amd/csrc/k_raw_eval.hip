@@ -708,14 +708,20 @@ __global__ __launch_bounds__(64) void k_raw_top(RawParams p) {
           const double y0 = pt_double(a.tsf, a.bits), y1 = pt_double(b.tsf, b.bits);
           if (isfinite(y0) && isfinite(y1) && f2key(fmax(y0, y1)) + 8 < thr) { skip_all(false, true); continue; }
         }
-        if (DL && p.lerp_fast) {   // the strip-wide window (lerpw_*, as in k_raw_eval)
-          const LerpW L = lerpw_init(interp, uns, x0, (int64_t)a.bits, x1, (int64_t)b.bits);
-          // exact long LERP strictly inside the window: y0 + trunc((x - x0) dy / (x1 - x0)) lies
-          // within [y0, y1]
-          if (MODE == 0 && L.ok && ((uint64_t)max((int64_t)a.bits, (int64_t)b.bits) ^ 0x8000000000000000ULL) < thr) {
+        if (MODE == 0 && !uns && interp == TSDB_INTERP_LERP && x1 > x0) {
+          // a long LERP strictly inside the window whose product (x - x0) dy cannot wrap:
+          // y0 + trunc((x - x0) dy / (x1 - x0)) lies within [y0, y1] (wave-uniform test, before
+          // any per-lane work)
+          const int64_t ya = (int64_t)a.bits, yb = (int64_t)b.bits;
+          int64_t dy, prod;
+          if (((uint64_t)max(ya, yb) ^ 0x8000000000000000ULL) < thr && !__builtin_sub_overflow(yb, ya, &dy) &&
+              !__builtin_mul_overflow(dy, x1 - x0, &prod)) {
             skip_all(true, false);
             continue;
           }
+        }
+        if (DL && p.lerp_fast) {   // the strip-wide window (lerpw_*, as in k_raw_eval)
+          const LerpW L = lerpw_init(interp, uns, x0, (int64_t)a.bits, x1, (int64_t)b.bits);
           if (L.ok) {
 #pragma unroll
             for (int w = 0; w < RW; w++) {
