@@ -1486,14 +1486,18 @@ extern "C" int tsdbhip_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* r
     }
     HIP_OK(c->ro_partner.ensure((int64_t)partner.size() * 4));
     HIP_OK(hipMemcpy(c->ro_partner.p, partner.data(), partner.size() * 4, hipMemcpyHostToDevice));
-    // the value rows packed with their count rows (k_ro_pack), for avg / count downsampling
+  }
+  // the value rows packed (with their count rows when the table has count cells): k_ro_pack,
+  // for k_ro_pairs (avg / count downsampling) and k_ro_rows (the other functions)
+  {
     std::vector<int32_t> vrows, vser;
-    for (int64_t s = 0; s < c->n_series; s++)
-      for (int64_t r = c->h_srp[s]; r < c->h_srp[s + 1]; r++)
-        if (partner[r] != -1) {
-          vrows.push_back((int32_t)r);
-          vser.push_back((int32_t)s);
-        }
+    for (int64_t s = 0; s < c->n_series; s++) {
+      if (c->h_orig[s] >= NS) continue;   // a count series
+      for (int64_t r = c->h_srp[s]; r < c->h_srp[s + 1]; r++) {
+        vrows.push_back((int32_t)r);
+        vser.push_back((int32_t)s);
+      }
+    }
     c->ro_npairs = (int64_t)vrows.size();
     if (c->ro_npairs && c->n_rows < ((int64_t)1 << 31)) {
       DevBuf dv, ds;
@@ -1502,8 +1506,8 @@ extern "C" int tsdbhip_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* r
       HIP_OK(hipMemcpy(dv.p, vrows.data(), c->ro_npairs * 4, hipMemcpyHostToDevice));
       HIP_OK(hipMemcpy(ds.p, vser.data(), c->ro_npairs * 4, hipMemcpyHostToDevice));
       HIP_OK(c->ro_pairs.ensure(c->ro_npairs * (int64_t)sizeof(RoPair)));
-      HIP_OK(launch_ro_pack(c->rows.as<RowDesc>(), c->ro_partner.as<int32_t>(), dv.as<int32_t>(), ds.as<int32_t>(),
-                            c->qual.as<uint8_t>(), c->ro_npairs, c->ro_pairs.as<RoPair>(), c->stream));
+      HIP_OK(launch_ro_pack(c->rows.as<RowDesc>(), cnt ? c->ro_partner.as<int32_t>() : nullptr, dv.as<int32_t>(),
+                            ds.as<int32_t>(), c->qual.as<uint8_t>(), c->ro_npairs, c->ro_pairs.as<RoPair>(), c->stream));
       const hipError_t e = hipStreamSynchronize(c->stream);
       dv.release();   // (DevBuf frees nothing on its own)
       ds.release();
@@ -3054,7 +3058,13 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
         rp.redo_list = c->sr_list.as<int32_t>();
         rp.redo_n = c->sr_n.as<int32_t>();
         rp.redo_mark = c->sr_mark.as<uint32_t>();
-        HIP_OK(launch_seq_rows(rp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->h_srp[ns], c->stream));
+        const char* pe = std::getenv("TSDBHIP_RO_PACK");   // A/B: 0 = k_seq_rows over the rows
+        if (c->ro_active && c->ro_npairs > 0 && !P.none && !(pe && pe[0] == '0')) {
+          rp.ro_pairs = c->ro_pairs.as<RoPair>();   // a rollup batch's value rows, packed (k_ro_rows)
+          HIP_OK(launch_ro_rows(rp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->ro_npairs, c->stream));
+        } else {
+          HIP_OK(launch_seq_rows(rp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->h_srp[ns], c->stream));
+        }
         GridParams dp = gp;
         dp.tile_list = c->sr_list.as<int32_t>();
         dp.tile_list_n = c->sr_n.as<int32_t>();

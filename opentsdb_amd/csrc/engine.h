@@ -60,7 +60,10 @@ struct RoPair {
   int32_t series;   // the value series (resident position)
 };
 static_assert(sizeof(RoPair) == 24, "RoPair layout");
-enum : uint32_t { RP_OK = 0x80000000u };   // k_seq_rows_ro's premises hold for the pair
+enum : uint32_t {
+  RP_OK = 0x80000000u,    // k_seq_rows_ro's premises hold for the pair
+  RP_VOK = 0x40000000u,   // k_seq_rows' premises hold for the value row alone
+};
 
 // Per-tile partial group state, structure of arrays, [tile][K].
 struct Partials {
@@ -547,11 +550,12 @@ hipError_t launch_raw_dz_check(const RawParams& p, int64_t n_out, hipStream_t s)
 hipError_t launch_raw_eval(const RawParams& p, hipStream_t s);
 hipError_t launch_raw_vals(const RawParams& p, int64_t k_max, hipStream_t s);
 hipError_t launch_raw_sel(const RawParams& p, int64_t k_max, hipStream_t s);
-hipError_t launch_raw_top(const RawParams& p, int T, hipStream_t s);
+hipError_t launch_raw_top(const RawParams& p, int T, hipStream_t s);   // fused operands + selection (k_raw_eval.hip)
 hipError_t launch_ro_pack(const RowDesc* rows, const int32_t* partner, const int32_t* vrows, const int32_t* vser,
                           const uint8_t* qual, int64_t n, RoPair* out, hipStream_t s);
 hipError_t launch_ro_pairs(const GridParams& p, int avg, double* dense, uint8_t* pres, const int64_t* cmap, int64_t n,
-                           hipStream_t s);   // fused operands + selection (k_raw_eval.hip)
+                           hipStream_t s);
+hipError_t launch_ro_rows(const GridParams& p, int f, double* dense, uint8_t* pres, int64_t n, hipStream_t s);
 template <int GA> hipError_t launch_raw_eval_inst(const RawParams& p, hipStream_t s);   // k_raw_eval.hip
 hipError_t launch_synth_write(const SynthParams& p, hipStream_t s);
 

@@ -581,36 +581,39 @@ __global__ __launch_bounds__(256) void k_ro_pack(const RowDesc* __restrict__ row
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t r = vrows[i];
-  const int32_t rc = partner[r];
+  const int32_t rc = partner ? partner[r] : -2;   // (a table without count cells: value rows alone)
   const RowDesc d = rows[r];
   const int qw = d.flags & ROW_QW_MASK;
   const int vl = (d.flags & ROW_VL_MASK) >> ROW_VL_SHIFT;
-  bool ok = rc >= 0 && !(d.flags & (ROW_ERR | ROW_UNSORTED)) && (d.base % 3600u) == 0 && (qw == 2 || qw == 4) &&
-            (vl == 1 || vl == 2 || vl == 4 || vl == 8) && d.ndp < 65536 && d.qoff < (1ULL << 32) && d.voff < (1ULL << 32);
-  if (ok && r > 0 && !(d.flags & ROW_SFIRST) && rows[r - 1].base == d.base) ok = false;   // two rows of one hour
+  // vok: k_seq_rows' premises for the value row alone; ok: k_seq_rows_ro's for the pair
+  bool vok = !(d.flags & (ROW_ERR | ROW_UNSORTED)) && (d.base % 3600u) == 0 && (qw == 2 || qw == 4) &&
+             (vl == 1 || vl == 2 || vl == 4 || vl == 8) && d.ndp < 65536 && d.qoff < (1ULL << 32) && d.voff < (1ULL << 32);
+  if (vok && r > 0 && !(d.flags & ROW_SFIRST) && rows[r - 1].base == d.base) vok = false;   // two rows of one hour
+  if (vok) {   // an offset past the hour (2-byte qualifiers reach 4095 s): the walk hands the series back
+    const uint8_t* q = qual + d.qoff;
+    for (uint32_t j = 0; j < d.ndp && vok; j++) {
+      uint32_t off;
+      if (qw == 2) off = ((((uint32_t)q[2 * j] << 8) | q[2 * j + 1]) >> 4) * 1000u;
+      else off = ((((uint32_t)q[4 * j] << 24) | ((uint32_t)q[4 * j + 1] << 16) | ((uint32_t)q[4 * j + 2] << 8) | q[4 * j + 3]) &
+                  0x0FFFFFC0u) >> 6;
+      if (off >= 3600000u) vok = false;
+    }
+  }
+  bool ok = vok && rc >= 0;
   RowDesc dc{};
   if (ok) dc = rows[rc];
   const int vlc = (dc.flags & ROW_VL_MASK) >> ROW_VL_SHIFT;
   if (ok && (dc.base != d.base || dc.ndp != d.ndp || (dc.flags & (ROW_ERR | ROW_UNSORTED)) || !(dc.flags & ROW_ALLI) ||
              (dc.flags & ROW_QW_MASK) != 2 || !(vlc == 1 || vlc == 2 || vlc == 4 || vlc == 8) || dc.voff >= (1ULL << 32)))
     ok = false;
-  if (ok) {   // an offset past the hour (2-byte qualifiers reach 4095 s): the walk hands the series back
-    const uint8_t* q = qual + d.qoff;
-    for (uint32_t j = 0; j < d.ndp && ok; j++) {
-      uint32_t off;
-      if (qw == 2) off = ((((uint32_t)q[2 * j] << 8) | q[2 * j + 1]) >> 4) * 1000u;
-      else off = ((((uint32_t)q[4 * j] << 24) | ((uint32_t)q[4 * j + 1] << 16) | ((uint32_t)q[4 * j + 2] << 8) | q[4 * j + 3]) &
-                  0x0FFFFFC0u) >> 6;
-      if (off >= 3600000u) ok = false;
-    }
-  }
   auto lg = [](int v) { return v == 1 ? 0u : v == 2 ? 1u : v == 4 ? 2u : 3u; };
   RoPair o;
   o.base = d.base;
   o.qoff = (uint32_t)d.qoff;
   o.voff = (uint32_t)d.voff;
   o.cvoff = (uint32_t)dc.voff;
-  o.meta = (d.ndp & 0xFFFFu) | (lg(vl) << 16) | (lg(vlc) << 18) | (qw == 4 ? 1u << 20 : 0u) | (ok ? RP_OK : 0u);
+  o.meta = (d.ndp & 0xFFFFu) | (lg(vl) << 16) | (lg(vlc) << 18) | (qw == 4 ? 1u << 20 : 0u) | (ok ? RP_OK : 0u) |
+           (vok ? RP_VOK : 0u);
   o.series = vser[i];
   out[i] = o;
 }
@@ -715,6 +718,108 @@ __global__ __launch_bounds__(256) void k_ro_pairs(GridParams p, double* __restri
     }
   }
   flush();
+}
+
+// k_seq_rows over a rollup batch's packed value rows (sum / min / max ... downsampling reads the
+// value series alone): the pair table's value fields, RP_VOK for k_seq_rows' premises.
+template <int F>
+__global__ __launch_bounds__(256) void k_ro_rows(GridParams p, double* __restrict__ dense, uint8_t* __restrict__ pres,
+                                                 int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const RoPair P = p.ro_pairs[i];
+  if ((int64_t)P.base < p.ss || (int64_t)P.base >= p.se) return;
+  const int64_t s = P.series;
+  if (!(P.meta & RP_VOK)) {
+    if (atomicExch(&p.redo_mark[s], 1u) == 0u) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)s;
+    return;
+  }
+  const int ndp = (int)(P.meta & 0xFFFFu);
+  const int vl = 1 << ((P.meta >> 16) & 3);
+  const bool q4 = (P.meta >> 20) & 1;
+  const int64_t K = p.K;
+  RowGeom g;
+  {
+    const int64_t rel = (int64_t)P.base * 1000 - p.B0;
+    if (rel >= 0) {
+      int64_t q0 = (int64_t)((double)rel / (double)p.I);
+      int64_t r0 = rel - q0 * p.I;
+      if (r0 < 0) { q0--; r0 += p.I; }
+      if (r0 >= p.I) { q0++; r0 -= p.I; }
+      g.q0 = q0;
+      g.r0 = r0;
+    } else {
+      g.q0 = 0;
+      g.r0 = rel;
+    }
+  }
+  const uint8_t* qb = p.qual + P.qoff;
+  const uint8_t* vb = p.val + P.voff;
+  BState st;
+  bs_init<F>(st);
+  int cur = -1;
+  for (int64_t i0 = 0; i0 < (int64_t)ndp; i0 += DPL) {
+    const int nv = (int)min((int64_t)DPL, (int64_t)ndp - i0);
+    uint32_t off[DPL], fl[DPL];
+    if (!q4) {
+      const uint4 q = *reinterpret_cast<const uint4*>(qb + i0 * 2);
+      const uint32_t ws[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int j = 0; j < DPL; j++) {
+        const uint32_t be = __builtin_bswap32(ws[j >> 1]);
+        const uint32_t qq = (j & 1) ? (be & 0xFFFF) : (be >> 16);
+        off[j] = (qq >> 4) * 1000u;
+        fl[j] = qq & 0xF;
+      }
+    } else {
+      const uint4 q0 = *reinterpret_cast<const uint4*>(qb + i0 * 4);
+      const uint4 q1 = *reinterpret_cast<const uint4*>(qb + i0 * 4 + 16);
+      const uint32_t ws[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+      for (int j = 0; j < DPL; j++) {
+        const uint32_t qq = __builtin_bswap32(ws[j]);
+        off[j] = (qq & 0x0FFFFFC0u) >> 6;
+        fl[j] = qq & 0xF;
+      }
+    }
+    double val[DPL];
+    seq_values(vb, i0, vl, fl, val);
+#pragma unroll
+    for (int j = 0; j < DPL; j++) {
+      if (j >= nv) break;
+      const int k = slot_of(p, g, P.base, off[j]);
+      if (k < 0) continue;
+      if (k != cur) {
+        if (cur >= 0) {
+          dense[s * K + cur] = bs_final<F>(st);
+          pres[s * K + cur] = 1;
+        }
+        bs_init<F>(st);
+        cur = k;
+      }
+      bs_add<F>(st, val[j]);
+    }
+  }
+  if (cur >= 0) {
+    dense[s * K + cur] = bs_final<F>(st);
+    pres[s * K + cur] = 1;
+  }
+}
+
+hipError_t launch_ro_rows(const GridParams& p, int f, double* dense, uint8_t* pres, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const unsigned nb = (unsigned)((n + 255) / 256);
+#define RORO_CASE(FF)                                                                    \
+  case FF:                                                                               \
+    hipLaunchKernelGGL(k_ro_rows<FF>, dim3(nb), dim3(256), 0, s, p, dense, pres, n);     \
+    break;
+  switch (f) {
+    RORO_CASE(F_SUM) RORO_CASE(F_AVG) RORO_CASE(F_COUNT) RORO_CASE(F_SQUARESUM) RORO_CASE(F_MIN) RORO_CASE(F_MAX)
+    RORO_CASE(F_DEV) RORO_CASE(F_FIRST) RORO_CASE(F_LAST) RORO_CASE(F_DIFF) RORO_CASE(F_MULT)
+    default: return hipErrorInvalidValue;
+  }
+#undef RORO_CASE
+  return hipGetLastError();
 }
 
 hipError_t launch_ro_pairs(const GridParams& p, int avg, double* dense, uint8_t* pres, const int64_t* cmap, int64_t n,

@@ -736,6 +736,25 @@ __global__ __launch_bounds__(64) void k_raw_top(RawParams p) {
       }
       continue;
     }
+    if (!RATE && MODE == 0 && !uns && interp == TSDB_INTERP_LERP && c >= 1 && c + m <= n - 1) {
+      // points inside the strip, with one before and one after it: every point of the wave takes an
+      // operand (its own value, or a LERP between two of pts[c - 1 .. c + m]); below thr when the
+      // largest of those values is and no LERP product can wrap
+      int64_t ymax = INT64_MIN;
+      bool safe = true;
+      for (int t = c - 1; t < c + m && safe; t++) {
+        const RawPt a = pts[t], b = pts[t + 1];
+        const int64_t ya = (int64_t)a.bits, yb = (int64_t)b.bits;
+        const int64_t xa = a.tsf & RAW_TIME_MASK, xb = b.tsf & RAW_TIME_MASK;
+        int64_t dy, prod;
+        safe = xb > xa && !__builtin_sub_overflow(yb, ya, &dy) && !__builtin_mul_overflow(dy, xb - xa, &prod);
+        ymax = max(ymax, max(ya, yb));
+      }
+      if (safe && ((uint64_t)ymax ^ 0x8000000000000000ULL) < thr) {
+        skip_all(true, false);
+        continue;
+      }
+    }
     if (lane < RAW_W) wmask[lane] = 0;
     WAVE_SYNC();
     const int32_t* rk = p.rank + p.sp_off[s] + first + c;

@@ -7,6 +7,8 @@
 #   c4        tools/bench_configs.py --config 4 (steps listed) and a TSDBHIP_TRACE=1 rerun -> c4*.jsonl
 #   pmc_hwin  rocprofv3 PMC passes over the day's sum:1m-avg (k_hwin)           -> pmc_hwin/summary.txt
 #   ro        tools/rollup_read_bench.py --check (default and TSDBHIP_RO_PACK=0), traced rerun -> ro*.jsonl
+#   ro_prof   rocprofv3 --kernel-trace --stats over tools/rollup_read_bench.py    -> ro_prof/
+#   c4_prof   rocprofv3 --kernel-trace --stats over config 4 (sum, p99)           -> c4_prof/
 #   pmc_c3p99 PMC passes (LDS pass included) over config 3's sum / p99:1m-avg   -> pmc_c3p99_summary.txt
 # Every GPU step under its own timeout; the first failure ends the pass.
 set -o pipefail
@@ -61,6 +63,14 @@ import json
 for f in ('ro', 'ro_nopack'):
     for l in open('$out/' + f + '.jsonl'):
         d=json.loads(l); print(f, d['query'], 'ms', round(d['ms_per_step'],3), 'dev', round(d.get('device_decode_downsample_ms',0),3), d.get('check',''))" ;;
+    ro_prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/ro_prof -o run -- python3 tools/rollup_read_bench.py \
+        --steps 5 > $out/ro_prof.log 2>&1 || { tail -20 $out/ro_prof.log; exit 1; }
+      python3 tools/prof_top.py $out/ro_prof 12 ;;
+    c4_prof)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/c4_prof -o run -- python3 tools/bench_configs.py \
+        --config 4 --steps 3 > $out/c4_prof.log 2>&1 || { tail -20 $out/c4_prof.log; exit 1; }
+      python3 tools/prof_top.py $out/c4_prof 12 ;;
     pmc_c3p99)
       PMC_LDS=1 bash tools/pmc_run.sh ${tag}_c3p99 python3 tools/bench_configs.py --config 3 --only sum,p99 --steps 1 \
         || exit $?
