@@ -3208,7 +3208,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       const char* sge = std::getenv("TSDBHIP_SEL_STAGE");   // A/B: 0 = each series' column values stored directly
       if (shortk == 1 && fp.sel_direct && fp.sel_cols && K <= 64 && !(sge && sge[0] == '0')) {   // k_short's column stage
         fp.sel_stage = fp.wave_lds;
-        fp.wave_lds += (int32_t)align16(8 * K * 8);
+        fp.wave_lds += (int32_t)align16(2 * 8 * K * 8);   // two stages of 8 series (k_short KR 4)
       }
       fp.waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / fp.wave_lds));
       fp.tile_list = list;

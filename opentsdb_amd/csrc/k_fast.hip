@@ -28,6 +28,28 @@ static hipError_t launch_fast_k(const GridParams& p, hipStream_t s) {
   const int64_t nl = p.n_launch > 0 ? p.n_launch : p.n_tiles;
   const int64_t blocks = (nl + p.waves - 1) / p.waves;
   const size_t lds = (size_t)p.wave_lds * p.waves;
+  if constexpr (KR == 4) {   // the staged column layout: k_short only (host: sel_stage set for shortk 1)
+    if (p.shortk != 1) return hipErrorNotSupported;
+    constexpr int DS = VL == 0 ? SHORT_D0 : (QW * 2 + VL * 2 <= 16) ? SHORT_D : 2;
+    if constexpr (QW == 2 && (VL == 0 || VL == SHORT6_VL4)) {
+      if (p.short6) {
+        if (lds > 65536) {
+          hipError_t e = hipFuncSetAttribute((const void*)k_short<F, QW, VL, DS, KR, 6>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+          if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL((k_short<F, QW, VL, DS, KR, 6>), dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p, p.rows,
+                           p.series_row_ptr, p.tile_begin, p.tile_end);
+        return hipGetLastError();
+      }
+    }
+    if (lds > 65536) {
+      hipError_t e = hipFuncSetAttribute((const void*)k_short<F, QW, VL, DS, KR>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((k_short<F, QW, VL, DS, KR>), dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p, p.rows,
+                       p.series_row_ptr, p.tile_begin, p.tile_end);
+    return hipGetLastError();
+  } else {
   if (p.shortk == 2) {   // k_rows: multi-row series of rows <= CH (a batch is 64 / DR ring turns)
     constexpr int DR = ROWS_D;
     if (lds > 65536) {
@@ -66,6 +88,7 @@ static hipError_t launch_fast_k(const GridParams& p, hipStream_t s) {
   hipLaunchKernelGGL((k_fast<F, QW, VL, D, KR>), dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p, p.rows,
                      p.series_row_ptr, p.tile_begin, p.tile_end);
   return hipGetLastError();
+  }
 }
 
 // register partials when every slot has its own lane and the series emit needs no rate pass
@@ -98,6 +121,7 @@ static hipError_t launch_fast_t(const GridParams& p, hipStream_t s) {
   }
   if (p.K <= 64 && !p.rate) {
     if (p.multi) return launch_fast_k<F, QW, VL, 2>(p, s);
+    if (p.sel_direct && p.sel_stage) return launch_fast_k<F, QW, VL, 4>(p, s);   // (k_short, staged columns)
     return (p.sel_direct || p.dense_out) ? launch_fast_k<F, QW, VL, 3>(p, s) : launch_fast_k<F, QW, VL, 1>(p, s);
   }
   if (p.multi) return hipErrorNotSupported;

@@ -583,21 +583,34 @@ __global__ __launch_bounds__(256) void k_emit_reg(GridParams p) {
   RegPart RP;
   rp_init(p.ga, RP);
   const bool inK = lane < K;
-  int64_t s = s0;
-  while (s < s1 && !((act >> (s - s0)) & 1)) s++;
-  bool pr = false;
-  double v = 0.0;
-  if (s < s1 && inK) { pr = p.pre_pres[s * K + lane] != 0; v = p.pre_dense[s * K + lane]; }
-  while (s < s1) {
-    int64_t sn = s + 1;
-    while (sn < s1 && !((act >> (sn - s0)) & 1)) sn++;
-    bool prn = false;
-    double vn = 0.0;
-    if (sn < s1 && inK) { prn = p.pre_pres[sn * K + lane] != 0; vn = p.pre_dense[sn * K + lane]; }
-    emit_series_reg(p, K, pr, v, RP);
-    s = sn;
-    pr = prn;
-    v = vn;
+  // the tile's active series in order, EMIT_D of them loaded ahead (a series' K buckets are one
+  // small load each: one series in flight left the wave waiting on every one -- rollup tables,
+  // 1M series x 24 buckets)
+  constexpr int EMIT_D = 4;
+  uint64_t rem = act;
+  bool pr[EMIT_D];
+  double v[EMIT_D];
+  bool live[EMIT_D];
+  auto fetch = [&](bool& pr_, double& v_, bool& live_) {
+    live_ = rem != 0;
+    pr_ = false;
+    v_ = 0.0;
+    if (!live_) return;
+    const int64_t s = s0 + (__ffsll((long long)rem) - 1);
+    rem &= rem - 1;
+    if (inK) { pr_ = p.pre_pres[s * K + lane] != 0; v_ = p.pre_dense[s * K + lane]; }
+  };
+#pragma unroll
+  for (int d = 0; d < EMIT_D; d++) fetch(pr[d], v[d], live[d]);
+  while (live[0]) {
+    emit_series_reg(p, K, pr[0], v[0], RP);
+#pragma unroll
+    for (int d = 0; d < EMIT_D - 1; d++) {
+      pr[d] = pr[d + 1];
+      v[d] = v[d + 1];
+      live[d] = live[d + 1];
+    }
+    fetch(pr[EMIT_D - 1], v[EMIT_D - 1], live[EMIT_D - 1]);
   }
   rp_store(p, tile, K, RP);
 }

@@ -678,28 +678,65 @@ __global__ __launch_bounds__(64) void k_raw_top(RawParams p) {
     }
   };
 
-  for (int i = 0; i < k; i++) {
+  // A span's cursors and window ends are loads that depend on each other (cursor, then the
+  // points at it), and with RAW_W / RW waves a strip each wave has few points to work on between
+  // them: the next span's points and the one after's cursors are loaded a step ahead.
+  struct SpanPre {
+    int n, c, m;
+    const RawPt* pts;
+  };
+  auto meta = [&](int i) {
+    SpanPre M;
     const int64_t s = sb + i;
-    const int n = p.sp_n[s];
+    M.n = p.sp_n[s];
+    M.pts = p.pts + p.sp_off[s];
+    M.c = crow[i];
+    M.m = (cnext ? cnext[i] : M.n - first) - M.c;
+    return M;
+  };
+  auto ends = [&](const SpanPre& M, RawPt& A, RawPt& B) {   // pts[c - 1], pts[c] (clamped)
+    const int hi = max(M.n - 1, 0);
+    const RawPt* base = M.n > 0 ? M.pts : p.pts;
+    A = base[min(max(M.c - 1, 0), hi)];
+    B = base[min(max(M.c, 0), hi)];
+  };
+  SpanPre M0{}, M1{};
+  RawPt A0{}, B0{}, A1{}, B1{};
+  if (k > 0) {
+    M0 = meta(0);
+    M1 = k > 1 ? meta(1) : M0;
+    ends(M0, A0, B0);
+  }
+  for (int i = 0; i < k; i++) {
+    const SpanPre cur = M0;
+    const RawPt ea = A0, eb = B0;
+    if (i + 1 < k) ends(M1, A1, B1);
+    SpanPre M2 = M1;
+    if (i + 2 < k) M2 = meta(i + 2);
+    M0 = M1;
+    A0 = A1;
+    B0 = B1;
+    M1 = M2;
+    const int n = cur.n;
     if (n < (RATE ? 2 : 1)) continue;
     const int nc = n - first;
-    const RawPt* pts = p.pts + p.sp_off[s];
-    const int c = crow[i];
-    const int m = (cnext ? cnext[i] : nc) - c;
+    const RawPt* pts = cur.pts;
+    const int c = cur.c;
+    const int m = cur.m;
     if (m == 0) {
       if (RATE) {
         if (c == nc) continue;
-        const double y = __longlong_as_double((long long)pts[c].bits);
+        const double y = __longlong_as_double((long long)eb.bits);   // pts[c]
         if (!isnan(y) && f2key(y) < thr) { skip_all(false, true); continue; }   // (the same operand at every point)
 #pragma unroll
         for (int w = 0; w < RW; w++) put_d(w, y, true);
       } else {
         if (c == 0) {
-          if (pts[0].tsf & RAW_FLOAT) flt = (1u << RW) - 1;
+          if (eb.tsf & RAW_FLOAT) flt = (1u << RW) - 1;   // pts[0]
           continue;
         }
         if (c == n) continue;
-        const RawPt a = pts[c - 1], b = pts[c];
+        const RawPt a = ea, b = eb;   // pts[c - 1], pts[c]
         if ((a.tsf | b.tsf) & RAW_FLOAT) flt = (1u << RW) - 1;
         const int64_t x0 = a.tsf & RAW_TIME_MASK, x1 = b.tsf & RAW_TIME_MASK;
         if (MODE == 1 && !uns && interp == TSDB_INTERP_LERP) {
@@ -757,7 +794,7 @@ __global__ __launch_bounds__(64) void k_raw_top(RawParams p) {
     }
     if (lane < RAW_W) wmask[lane] = 0;
     WAVE_SYNC();
-    const int32_t* rk = p.rank + p.sp_off[s] + first + c;
+    const int32_t* rk = p.rank + (pts - p.pts) + first + c;   // (sp_off[s] + ...)
     for (int l = lane; l < m; l += 64) {
       const int64_t o = rk[l] - ua;
       __hip_atomic_fetch_or(&wmask[o >> 6], 1ULL << (o & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);

@@ -2278,7 +2278,9 @@ template <int F, int QW, int VL, int D, int KR, int NP = DPL>
 __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) void k_short(GridParams p, const RowDesc* __restrict__ rows,
                                                const int64_t* __restrict__ srp, const int64_t* __restrict__ tbeg,
                                                const int64_t* __restrict__ tend) {
-  constexpr bool OUT = KR == 0 || KR == 3;
+  constexpr bool OUT = KR == 0 || KR == 3 || KR == 4;
+  // KR 4: KR 3's percentile output in the (group, slot) column layout, staged in LDS (COLS)
+  constexpr bool COLS = KR == 4;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2298,7 +2300,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
   // the compiler cannot tell apart from it -- a load consumed at once, behind the whole ring)
   const int32_t tgrp = p.tile_group[tile];
   int64_t cg0 = 0, cgn = 0;
-  if (KR == 3 && p.sel_stage) {
+  if (COLS) {
     cg0 = p.group_series_ptr[tgrp];
     cgn = p.group_series_ptr[tgrp + 1] - cg0;
   }
@@ -2372,8 +2374,20 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
 #endif
     return nv0;
   };
-  // sel_direct into the column layout: rows staged 8 series at a time (sel_cols_flush)
-  double* stage = (KR == 3 && p.sel_stage) ? (double*)(smem + (int64_t)wave * p.wave_lds + p.sel_stage) : nullptr;
+  // sel_direct into the column layout (COLS): two LDS stages of 8 series' rows.  Every series end
+  // stores one slice (8 columns x 8 series: 64-B pieces) of the previous 8 series' stage, so
+  // each iteration issues exactly one store: a store only every 8th series made the compiler's
+  // vmcnt count assume none, and the waits for the ring's loads then also waited for the stores
+  // (68 % of wave cycles waiting, profiles/r05t).  Before the first 8 are staged the slice stores
+  // go to the first 8 series' own entries (rewritten later), masked to this tile.
+  double* stage = COLS ? (double*)(smem + (int64_t)wave * p.wave_lds + p.sel_stage) : nullptr;
+  const int sl_c = lane >> 3, sl_i = lane & 7;   // a slice lane: column 8 t + sl_c, series sl_i
+  double* colbase = COLS ? p.sel_vals + cg0 * K + (s0 - cg0) : nullptr;
+  auto slice = [&](int t, int grp, int nrow) {   // slice t of 8-series group grp (rows < nrow)
+    const int k = 8 * t + sl_c;
+    const double v = stage[((grp & 1) * 8 + sl_i) * K + min(k, K - 1)];
+    if (k < K && sl_i < nrow) colbase[(int64_t)k * cgn + grp * 8 + sl_i] = v;
+  };
   bool uacc = false;
   auto series_end = [&](int j, int nv0) {
 #ifdef TSDBHIP_KDBG
@@ -2383,11 +2397,14 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     const double amax = __longlong_as_double((long long)rl64(damax, j));
     const bool fine =
         KR ? fast_series_end_reg<F, false, OUT>(p, L, K, lsb, amax, RP, s0 + j, tgrp, (uint32_t)nv0,
-                                                stage ? stage + (j & 7) * K : nullptr, &uacc)
+                                                COLS ? stage + (((j >> 3) & 1) * 8 + (j & 7)) * K : nullptr, &uacc)
            : fast_series_end<F>(p, L, K, lsb, amax, s0 + j, tgrp);
     if (!fine) redo = true;
-    else if (KR == 3 && stage && ((j & 7) == 7 || j == ns - 1))
-      sel_cols_flush(p, K, cg0, cgn, s0 + (j & ~7), (j & 7) + 1, stage);
+    if constexpr (COLS) {
+      WAVE_SYNC();
+      const int g = (j >> 3) - 1;   // the previous group (-1: none yet)
+      slice(j & 7, max(g, 0), g >= 0 ? 8 : min(8, ns));
+    }
   };
   int j = 0;
   for (; j + D <= ns; j += D) {
@@ -2412,6 +2429,13 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
   if (redo) {
     if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
     return;
+  }
+  if constexpr (COLS) {   // the slices left: the last full group's rest, then the last group whole
+    WAVE_SYNC();
+    const int last = (ns - 1) >> 3, nb = ns - 8 * last;
+    if (last >= 1)
+      for (int t = nb; t < 8; t++) slice(t, last - 1, 8);
+    for (int t = 0; t < 8; t++) slice(t, last, nb);
   }
   if (OUT && p.sel_wr && lane < ns) p.sel_wr[s0 + lane] = 1;   // sel_direct: every series of the tile was written
   if (OUT && p.sel_direct) sel_uni_flush(p, K, tgrp, uacc);

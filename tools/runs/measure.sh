@@ -64,11 +64,11 @@ for f in ('ro', 'ro_nopack'):
     for l in open('$out/' + f + '.jsonl'):
         d=json.loads(l); print(f, d['query'], 'ms', round(d['ms_per_step'],3), 'dev', round(d.get('device_decode_downsample_ms',0),3), d.get('check',''))" ;;
     ro_prof)
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/ro_prof -o run -- python3 tools/rollup_read_bench.py \
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/ro_prof -o run -- python3 tools/rollup_read_bench.py \
         --steps 5 > $out/ro_prof.log 2>&1 || { tail -20 $out/ro_prof.log; exit 1; }
       python3 tools/prof_top.py $out/ro_prof 12 ;;
     c4_prof)
-      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/c4_prof -o run -- python3 tools/bench_configs.py \
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/c4_prof -o run -- python3 tools/bench_configs.py \
         --config 4 --steps 3 > $out/c4_prof.log 2>&1 || { tail -20 $out/c4_prof.log; exit 1; }
       python3 tools/prof_top.py $out/c4_prof 12 ;;
     pmc_c3p99)
