@@ -2430,7 +2430,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     if (lane == 0) p.redo_list[atomicAdd(p.redo_n, 1)] = (int32_t)tile;
     return;
   }
-  if constexpr (COLS) {   // the slices left: the last full group's rest, then the last group whole
+  if (COLS && ns > 0) {   // the slices left: the last full group's rest, then the last group whole
     WAVE_SYNC();
     const int last = (ns - 1) >> 3, nb = ns - 8 * last;
     if (last >= 1)
