@@ -9,6 +9,7 @@
 #   ro        tools/rollup_read_bench.py --check (default and TSDBHIP_RO_PACK=0), traced rerun -> ro*.jsonl
 #   ro_prof   rocprofv3 --kernel-trace --stats over tools/rollup_read_bench.py    -> ro_prof/
 #   c4_prof   rocprofv3 --kernel-trace --stats over config 4 (sum, p99)           -> c4_prof/
+#   pmc_c4    PMC passes (LDS pass included) over config 4 (k_raw_top, k_raw_eval)     -> pmc_c4_summary.txt
 #   pmc_c3p99 PMC passes (LDS pass included) over config 3's sum / p99:1m-avg   -> pmc_c3p99_summary.txt
 # Every GPU step under its own timeout; the first failure ends the pass.
 set -o pipefail
@@ -71,6 +72,9 @@ for f in ('ro', 'ro_nopack'):
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/c4_prof -o run -- python3 tools/bench_configs.py \
         --config 4 --steps 3 > $out/c4_prof.log 2>&1 || { tail -20 $out/c4_prof.log; exit 1; }
       python3 tools/prof_top.py $out/c4_prof 12 ;;
+    pmc_c4)
+      PMC_LDS=1 bash tools/pmc_run.sh ${tag}_c4 python3 tools/bench_configs.py --config 4 --steps 1 || exit $?
+      python3 tools/pmc_summary.py gpurun_out/pmc_${tag}_c4 k_raw | tee $out/pmc_c4_summary.txt ;;
     pmc_c3p99)
       PMC_LDS=1 bash tools/pmc_run.sh ${tag}_c3p99 python3 tools/bench_configs.py --config 3 --only sum,p99 --steps 1 \
         || exit $?
