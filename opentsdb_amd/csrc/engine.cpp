@@ -453,6 +453,11 @@ struct tsdbhip_ctx {
   int64_t tl_off[7] = {};
   bool fast_used = false;
   HostBuf h_stage;   // collect(): the dense [G][K] values and flags, page-locked
+  HostBuf h_small;   // collect(): the group activity flags, error code and hand-back count, page-locked
+  HostBuf h_scal;    // d2h_small: 16 page-locked 8-byte slots for scalars read back
+  void* small_dst[16] = {};
+  int small_len[16] = {};
+  int small_n = 0;
   void* up_stage[2] = {nullptr, nullptr};   // h2d: page-locked staging of pageable uploads (UP_CHUNK each)
   hipEvent_t up_ev[2] = {nullptr, nullptr};
   bool up_busy[2] = {false, false};
@@ -522,6 +527,40 @@ namespace tsdb {
 hipStream_t ctx_stream(tsdbhip_ctx* c) { return c->stream; }
 int ctx_device(tsdbhip_ctx* c) { return c->device; }
 std::mutex& ctx_mutex(tsdbhip_ctx* c) { return c->mu; }
+
+// Scalars read back from the device go through page-locked slots of the context: a copy into
+// pageable memory blocks in the runtime until the stream drains, and measured ~0.85 ms a call
+// however little was left to run (profiles/r05ad/ro_api: rollup avg:1h-avg, 0.27 ms of kernels in
+// a 0.99 ms call).  d2h_small queues the copy into a slot; sync_small synchronises the stream and
+// hands the slots' values to their destinations.
+int d2h_small(tsdbhip_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
+  if (bytes > 8 || c->small_n >= (int)(sizeof(c->small_dst) / sizeof(c->small_dst[0]))) {
+    HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+    return 0;
+  }
+  HIP_OK(c->h_scal.ensure(8 * 16));
+  char* slot = reinterpret_cast<char*>(c->h_scal.p) + 8 * c->small_n;
+  HIP_OK(hipMemcpyAsync(slot, src, bytes, hipMemcpyDeviceToHost, st));
+  c->small_dst[c->small_n] = dst;
+  c->small_len[c->small_n] = (int)bytes;
+  c->small_n++;
+  return 0;
+}
+int sync_small(tsdbhip_ctx* c, hipStream_t st) {
+  const hipError_t e = hipStreamSynchronize(st);
+  for (int i = 0; i < c->small_n; i++)
+    std::memcpy(c->small_dst[i], reinterpret_cast<char*>(c->h_scal.p) + 8 * i, (size_t)c->small_len[i]);
+  c->small_n = 0;
+  if (e != hipSuccess) return fail(TSDB_E_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
+  return 0;
+}
+
+// The context's lock for an entry point; also drops d2h_small copies an earlier call left
+// pending when it returned on an error between the copy and its sync_small.
+struct CtxLock {
+  std::lock_guard<std::mutex> g;
+  explicit CtxLock(tsdbhip_ctx* c) : g(c->mu) { c->small_n = 0; }
+};
 void*& ctx_hist(tsdbhip_ctx* c) { return c->hist; }
 int set_error(int code, const std::string& msg) { return fail(code, msg); }
 void hist_release(void* h);
@@ -733,7 +772,7 @@ static void release_batch(tsdbhip_ctx* c) {
 namespace tsdb {
 // multi.cpp: the merge context's resident state reset (a load that is not a rollup load)
 void ctx_drop_batch(tsdbhip_ctx* c) {
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   release_batch(c);
 }
 int64_t ctx_n_series(tsdbhip_ctx* c) { return c->n_series; }   // resident series (count series too)
@@ -754,6 +793,8 @@ extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
                     &c->big_scratch, &c->ro_agg, &c->ro_pres})
     b->release();
   c->h_stage.release();
+  c->h_small.release();
+  c->h_scal.release();
   for (auto& o : c->ro_out)
     for (DevBuf* b : {&o.series, &o.base, &o.qual, &o.voff, &o.val}) b->release();
   if (c->ro_tmp) (void)hipFree(c->ro_tmp);
@@ -1139,7 +1180,7 @@ static int load_body(tsdbhip_ctx* c, const tsdbhip_batch* b, const std::vector<i
 
 static int load_impl(tsdbhip_ctx* c, const tsdbhip_batch* b, const std::vector<int64_t>* cand = nullptr) {
   if (!c || !b) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   return load_body(c, b, cand);
 }
 
@@ -1457,7 +1498,7 @@ extern "C" int tsdbhip_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* r
   m.qual = ov.q.data();
   m.val = ov.v.data();
   m.group_id = gid.data();
-  std::lock_guard<std::mutex> lk(c->mu);   // the batch and its rollup state in one critical section
+  CtxLock lk(c);   // the batch and its rollup state in one critical section
   int rc = load_body(c, &m, nullptr);
   if (rc) return rc;
   c->ro_active = true;
@@ -1584,7 +1625,7 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     t_last = t;
   };
   mark("validate+plan");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_OK(hipSetDevice(c->device));
   release_batch(c);
   // device copies of one chunk of the scan and per-column / per-row scratch (freed at the end)
@@ -1646,8 +1687,8 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
       if (cb->col_timestamp) HIP_OK(h2d(c, d_cts.p, cb->col_timestamp + c0, nc * 8, st));
     }
     int32_t bad = 0;
-    HIP_OK(hipMemcpyAsync(&bad, d_bad.p, 4, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
+    { int rc_ = d2h_small(c, &bad, d_bad.p, 4, st); if (rc_) return rc_; }
+    { int rc_ = sync_small(c, st); if (rc_) return rc_; }
     if (bad) return fail(TSDB_E_ILLEGAL_ARGUMENT, "column offsets not monotonic");
     HIP_OK(d_crow.ensure(c1c * 4));
     HIP_OK(d_cn.ensure(c1c * 8));
@@ -1677,8 +1718,8 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     HIP_OK(hipEventRecord(c->ev[0], st));
     HIP_OK(cmp_analyze(p, &c->cmp_tmp, &c->cmp_tmp_bytes, st));
     int64_t n_ent = 0;
-    HIP_OK(hipMemcpyAsync(&n_ent, p.col_off + nc, 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
+    { int rc_ = d2h_small(c, &n_ent, p.col_off + nc, 8, st); if (rc_) return rc_; }
+    { int rc_ = sync_small(c, st); if (rc_) return rc_; }
     if (n_ent >= kLim) return fail(TSDB_E_NOT_IMPLEMENTED, "more than 2^31 datapoints in one compaction chunk");
     p.n_ent = n_ent;
     HIP_OK(d_rq.ensure(r1c * 8));
@@ -1812,8 +1853,8 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
       if (cb->col_timestamp) HIP_OK(h2d(c, d_cts.p, cb->col_timestamp, nc * 8, st));
     }
     int32_t bad = 0;
-    HIP_OK(hipMemcpyAsync(&bad, d_bad.p, 4, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
+    { int rc_ = d2h_small(c, &bad, d_bad.p, 4, st); if (rc_) return rc_; }
+    { int rc_ = sync_small(c, st); if (rc_) return rc_; }
     mark("onepass H2D");
     if (bad) return fail(TSDB_E_ILLEGAL_ARGUMENT, "column offsets not monotonic");
     HIP_OK(d_crow.ensure(c1c * 4));
@@ -2148,7 +2189,7 @@ extern "C" int tsdbhip_load_shard(tsdbhip_ctx* c, const tsdbhip_batch* b, int mo
 // global series g, g + G, g + 2G, ...): one GPU's contiguous shard of the whole store.
 static int synth_impl(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp, int64_t p0, int64_t p1) {
   if (!c || !sp) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_OK(hipSetDevice(c->device));
   if (sp->n_series <= 0 || sp->n_points <= 0 || sp->period_ms <= 0 || sp->n_groups <= 0 || sp->start_s < 0)
     return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad synth spec");
@@ -2288,7 +2329,7 @@ extern "C" int tsdbhip_batch_download(tsdbhip_ctx* c, int64_t* series_row_ptr, u
   MD_REFUSE(c, "tsdbhip_batch_download");
   if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_batch_download over a rollup batch (tsdbhip_load_rollup)");
   if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_OK(hipSetDevice(c->device));
   std::vector<RowDesc> rd(c->n_rows);
   if (c->n_rows) HIP_OK(hipMemcpy(rd.data(), c->rows.p, c->n_rows * sizeof(RowDesc), hipMemcpyDeviceToHost));
@@ -2318,7 +2359,7 @@ extern "C" int tsdbhip_batch_range_sizes(tsdbhip_ctx* c, int64_t s0, int64_t s1,
   MD_REFUSE(c, "tsdbhip_batch_range_sizes");
   if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
   if (c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_batch_range_sizes over a rollup batch");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   if (s0 < 0 || s1 < s0 || s1 > c->n_series) return fail(TSDB_E_ILLEGAL_ARGUMENT, "series range out of bounds");
   const int64_t r0 = c->h_srp[s0], r1 = c->h_srp[s1];
   uint64_t q = 0, v = 0;
@@ -2338,7 +2379,7 @@ extern "C" int tsdbhip_batch_download_range(tsdbhip_ctx* c, int64_t s0, int64_t 
   MD_REFUSE(c, "tsdbhip_batch_download_range");
   if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
   if (c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_batch_download_range over a rollup batch");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   if (s0 < 0 || s1 < s0 || s1 > c->n_series) return fail(TSDB_E_ILLEGAL_ARGUMENT, "series range out of bounds");
   HIP_OK(hipSetDevice(c->device));
   const int64_t r0 = c->h_srp[s0], r1 = c->h_srp[s1], nr = r1 - r0;
@@ -2385,7 +2426,7 @@ extern "C" int tsdbhip_batch_download_range(tsdbhip_ctx* c, int64_t s0, int64_t 
 extern "C" int tsdbhip_debug_rows(tsdbhip_ctx* c, uint32_t* ndp, uint32_t* flags, int32_t* lsb, double* absmax) {
   MD_REFUSE(c, "tsdbhip_debug_rows");
   if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_OK(hipSetDevice(c->device));
   std::vector<RowDesc> rd(c->n_rows);
   if (c->n_rows) HIP_OK(hipMemcpy(rd.data(), c->rows.p, c->n_rows * sizeof(RowDesc), hipMemcpyDeviceToHost));
@@ -2798,11 +2839,14 @@ int64_t series_max_dp(tsdbhip_ctx* c, int64_t ss, int64_t se) {
 // The streaming kernels (k_short / k_fast) can take the query: fixed grid, a row class of the
 // batch they are specialised for, their LDS slot budget.
 // LDS a streaming-kernel wave takes: KR 0 writing the buckets to HBM (dense_out, K > 64 or rate)
-// keeps no partials or rate values
+// keeps no partials or rate values; the register-partial variants (KR != 0: K <= 64, no rate) keep
+// their partials in registers (k_short's staged column variant then fits 4 waves a SIMD: 10.9 ->
+// 9.5 KB a wave)
 int64_t fast_lds_of(const tsdbhip_query* q, const Plan& P) {
   const bool rate = q->rate != 0;
-  const bool dense0 = P.dense_out && !(P.K <= 64 && !rate);
-  return fast_wave_lds(P.K, rate && !dense0, !dense0);
+  const bool kr = P.K <= 64 && !rate;
+  const bool dense0 = P.dense_out && !kr;
+  return fast_wave_lds(P.K, rate && !dense0, !dense0 && !kr);
 }
 
 bool fast_path_ok(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P) {
@@ -3122,8 +3166,8 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       rp.pct_v6 = rp.pct_vonly && c->pct_v6 && !(v6env && v6env[0] == '0');
       HIP_OK(launch_pct_rows(rp, c->pct_qw, c->pct_vl, c->stream));
       int32_t nback = 0;
-      HIP_OK(hipMemcpyAsync(&nback, c->redo2_n.p, 4, hipMemcpyDeviceToHost, c->stream));
-      HIP_OK(hipStreamSynchronize(c->stream));
+      { int rc_ = d2h_small(c, &nback, c->redo2_n.p, 4, c->stream); if (rc_) return rc_; }
+      { int rc_ = sync_small(c, c->stream); if (rc_) return rc_; }
       gp.tile_list = c->redo2.as<int32_t>();
       gp.tile_list_n = c->redo2_n.as<int32_t>();
       HIP_OK(launch_pct(gp, 1, nback, c->stream));
@@ -3131,8 +3175,8 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       HIP_OK(launch_pct(gp, 0, c->n_series, c->stream));
     }
     int32_t nbig = 0;   // series with a bucket of more than 512 values: the large-bucket pass
-    HIP_OK(hipMemcpyAsync(&nbig, c->redo_n.p, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
+    { int rc_ = d2h_small(c, &nbig, c->redo_n.p, 4, c->stream); if (rc_) return rc_; }
+    { int rc_ = sync_small(c, c->stream); if (rc_) return rc_; }
     if (nbig > 0) {
       // persistent waves, each with an overflow region as large as the largest series' in-range
       // datapoints (buckets above PCT_CAP values); at most ~2 GB of regions
@@ -3875,6 +3919,30 @@ struct PhaseTrace {
   }
 };
 
+// The group activity flags, the error code and the hand-back count of a query into page-locked
+// memory kept by the context.  (A copy into pageable memory blocks in the runtime until the stream
+// has drained, and measured ~0.85 ms a call however little was left to run: rollup avg:1h-avg,
+// 0.27 ms of kernels in a 0.99 ms call, profiles/r05ad/ro_api.)
+struct SmallD2H {
+  uint32_t* act;
+  int32_t* err;
+  int32_t* redo;
+};
+int small_d2h(tsdbhip_ctx* c, int64_t G, bool redo, SmallD2H& o) {
+  const int64_t g4 = (std::max<int64_t>(1, G) * 4 + 15) & ~(int64_t)15;
+  HIP_OK(c->h_small.ensure(g4 + 16));
+  char* b = reinterpret_cast<char*>(c->h_small.p);
+  o.act = reinterpret_cast<uint32_t*>(b);
+  o.err = reinterpret_cast<int32_t*>(b + g4);
+  o.redo = o.err + 1;
+  *o.err = 0;
+  *o.redo = 0;
+  if (G) HIP_OK(hipMemcpyAsync(o.act, c->gact.p, G * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipMemcpyAsync(o.err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
+  if (redo) HIP_OK(hipMemcpyAsync(o.redo, c->redo_final, 4, hipMemcpyDeviceToHost, c->stream));
+  return 0;
+}
+
 int collect(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bool timed, tsdbhip_result** out,
             const void* d_val = nullptr, const void* d_flag = nullptr) {
   // the dense [G][K] rows land in page-locked staging kept by the context (no zero fill, DMA
@@ -3883,18 +3951,17 @@ int collect(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bo
   HIP_OK(c->h_stage.ensure(std::max<int64_t>(16, gk * 9 + 16)));
   double* val = reinterpret_cast<double*>(c->h_stage.p);
   uint8_t* flag = reinterpret_cast<uint8_t*>(c->h_stage.p) + gk * 8;
-  std::vector<uint32_t> act(std::max<int64_t>(1, G));
-  int32_t err = 0;
   if (gk) {
     HIP_OK(hipMemcpyAsync(val, d_val ? d_val : c->out_val.p, gk * 8, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipMemcpyAsync(flag, d_flag ? d_flag : c->out_flag.p, gk, hipMemcpyDeviceToHost, c->stream));
   }
-  if (G) HIP_OK(hipMemcpyAsync(act.data(), c->gact.p, G * 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
-  int32_t redo_n = 0;
-  if (timed && c->fast_used) HIP_OK(hipMemcpyAsync(&redo_n, c->redo_final, 4, hipMemcpyDeviceToHost, c->stream));
+  SmallD2H sm;
+  int rc0 = small_d2h(c, G, timed && c->fast_used, sm);
+  if (rc0) return rc0;
   PhaseTrace tr("collect");
   HIP_OK(hipStreamSynchronize(c->stream));
+  std::vector<uint32_t> act(sm.act, sm.act + std::max<int64_t>(1, G));
+  const int32_t err = *sm.err, redo_n = *sm.redo;
   tr.mark("device + d2h");
   if (timed) record_timing(c, P, redo_n);
   if (err) return fail(err, "error raised by the device path");
@@ -4307,8 +4374,8 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
     for (int64_t i = 0; i < ng; i++) g_ptr[g0 + i + 1] = (int64_t)base + ooff[i + 1];
   }
   int32_t err = 0;
-  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipStreamSynchronize(c->stream));
+  { int rc_ = d2h_small(c, &err, c->err.p, 4, c->stream); if (rc_) return rc_; }
+  { int rc_ = sync_small(c, c->stream); if (rc_) return rc_; }
   float t01 = 0;
   (void)hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
   c->fast_used = false;
@@ -4450,8 +4517,8 @@ int run_anchored(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_
       HIP_OK(hipMemcpyAsync(dense.data(), c->pre_dense.p, S * K * 8, hipMemcpyDeviceToHost, c->stream));
       HIP_OK(hipMemcpyAsync(pres.data(), c->pre_pres.p, S * K, hipMemcpyDeviceToHost, c->stream));
     }
-    HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
+    { int rc_ = d2h_small(c, &err, c->err.p, 4, c->stream); if (rc_) return rc_; }
+    { int rc_ = sync_small(c, c->stream); if (rc_) return rc_; }
     if (err) return fail(err, "error raised by the device path");
     for (int64_t s = 0; s < S; s++) {
       if (cls[s] != (int32_t)k) continue;
@@ -4749,8 +4816,8 @@ int fused_pass(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, Plan& P) {
   rc = run_device(c, &q0, P, c->n_groups, false);
   if (rc) return rc;
   int32_t handed_back = 0;
-  HIP_OK(hipMemcpyAsync(&handed_back, c->redo_final, 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipStreamSynchronize(c->stream));
+  { int rc_ = d2h_small(c, &handed_back, c->redo_final, 4, c->stream); if (rc_) return rc_; }
+  { int rc_ = sync_small(c, c->stream); if (rc_) return rc_; }
   return handed_back ? 1 : 0;
 }
 
@@ -4808,14 +4875,14 @@ int run_multi_fused(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_resu
   HIP_OK(c->h_stage.ensure(std::max<int64_t>(16, gk * 9 * n + 16)));
   double* val = reinterpret_cast<double*>(c->h_stage.p);
   uint8_t* flag = reinterpret_cast<uint8_t*>(c->h_stage.p) + gk * 8 * n;
-  std::vector<uint32_t> act(std::max<int64_t>(1, G));
-  int32_t err = 0, redo_n = 0;
   HIP_OK(hipMemcpyAsync(val, c->out_val.p, gk * n * 8, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipMemcpyAsync(flag, c->out_flag.p, gk * n, hipMemcpyDeviceToHost, c->stream));
-  if (G) HIP_OK(hipMemcpyAsync(act.data(), c->gact.p, G * 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipMemcpyAsync(&redo_n, c->redo_final, 4, hipMemcpyDeviceToHost, c->stream));
+  SmallD2H sm;
+  rc = small_d2h(c, G, true, sm);
+  if (rc) return rc;
   HIP_OK(hipStreamSynchronize(c->stream));
+  std::vector<uint32_t> act(sm.act, sm.act + std::max<int64_t>(1, G));
+  const int32_t err = *sm.err, redo_n = *sm.redo;
   tr.mark("reduce x n + d2h");
   c->fused_n = n;
   record_timing(c, P, redo_n);
@@ -4834,7 +4901,7 @@ int run_multi_fused(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_resu
 extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
   if (c && c->md) return tsdb::md_run(c, q, out);
   if (!c || !q || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   *out = nullptr;
   HIP_OK(hipSetDevice(c->device));
   if (c->ro_active) return run_rollup(c, q, out);
@@ -4872,7 +4939,7 @@ extern "C" int tsdbhip_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n,
         a.ds_calendar != b.ds_calendar)
       return fail(TSDB_E_ILLEGAL_ARGUMENT, "tsdbhip_run_multi: the queries must share the time range and downsampling");
   }
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_OK(hipSetDevice(c->device));
   if (c->ro_active) {
     // a rollup table: each query reads its own aggregate's cells (RollupQuery per sub-query,
@@ -4930,8 +4997,8 @@ extern "C" int tsdbhip_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n,
   rc = run_device(c, &q0, P0, G, false);
   if (rc) return rc;
   int32_t err = 0;
-  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipStreamSynchronize(c->stream));
+  { int rc_ = d2h_small(c, &err, c->err.p, 4, c->stream); if (rc_) return rc_; }
+  { int rc_ = sync_small(c, c->stream); if (rc_) return rc_; }
   if (err) return fail(err, "error raised by the device path");
   for (int i = 0; i < n; i++) {
     Plan P;
@@ -5092,9 +5159,9 @@ int run_partials_locked(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups
   HIP_OK(hipEventRecord(c->ev[2], c->stream));
   HIP_OK(hipMemcpyAsync(partials, xb, L.bytes, hipMemcpyDefault, c->stream));
   int32_t err = 0, redo_n = 0;
-  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
-  if (c->fast_used) HIP_OK(hipMemcpyAsync(&redo_n, c->redo_final, 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipStreamSynchronize(c->stream));
+  { int rc_ = d2h_small(c, &err, c->err.p, 4, c->stream); if (rc_) return rc_; }
+  if (c->fast_used) { int rc_ = d2h_small(c, &redo_n, c->redo_final, 4, c->stream); if (rc_) return rc_; }
+  { int rc_ = sync_small(c, c->stream); if (rc_) return rc_; }
   record_timing(c, P, redo_n);
   if (err) return fail(err, "error raised by the device path");
   return 0;
@@ -5143,9 +5210,9 @@ int run_partials_fused(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, int64_t n
   HIP_OK(hipEventRecord(c->ev[2], c->stream));
   HIP_OK(hipMemcpyAsync(partials, xb0, L.bytes * n, hipMemcpyDefault, c->stream));
   int32_t err = 0, redo_n = 0;
-  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipMemcpyAsync(&redo_n, c->redo_final, 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipStreamSynchronize(c->stream));
+  { int rc_ = d2h_small(c, &err, c->err.p, 4, c->stream); if (rc_) return rc_; }
+  { int rc_ = d2h_small(c, &redo_n, c->redo_final, 4, c->stream); if (rc_) return rc_; }
+  { int rc_ = sync_small(c, c->stream); if (rc_) return rc_; }
   c->fused_n = n;
   record_timing(c, P, redo_n);
   c->fused_n = 0;
@@ -5157,7 +5224,7 @@ int run_partials_fused(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, int64_t n
 extern "C" int tsdbhip_run_partials(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t n_groups_global, void* partials) {
   MD_REFUSE(c, "tsdbhip_run_partials");
   if (!c || !q || !partials) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   return run_partials_locked(c, q, n_groups_global, partials);
 }
 
@@ -5175,7 +5242,7 @@ extern "C" int tsdbhip_run_partials_multi(tsdbhip_ctx* c, const tsdbhip_query* q
         a.ds_calendar != b.ds_calendar)
       return fail(TSDB_E_ILLEGAL_ARGUMENT, "tsdbhip_run_partials_multi: the queries must share the time range and downsampling");
   }
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_OK(hipSetDevice(c->device));
   int rc = run_partials_fused(c, qs, n, n_groups_global, partials);
   if (rc <= 0) return rc;
@@ -5198,7 +5265,7 @@ extern "C" int tsdbhip_finalize(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t 
                                 int n_ranks, tsdbhip_result** out) {
   MD_REFUSE(c, "tsdbhip_finalize");
   if (!c || !q || !partials || !out || n_ranks < 1) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad argument");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   *out = nullptr;
   HIP_OK(hipSetDevice(c->device));
   if (c->ro_active) { const int r = ro_check(q); if (r) return r; }
@@ -5272,8 +5339,8 @@ int sel_values_stage(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, int64_t 
   a.assign(std::max<int64_t>(1, G), 0);
   if (G) HIP_OK(hipMemcpyAsync(a.data(), c->gact.p, G * 4, hipMemcpyDeviceToHost, c->stream));
   int32_t err = 0;
-  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipStreamSynchronize(c->stream));
+  { int rc_ = d2h_small(c, &err, c->err.p, 4, c->stream); if (rc_) return rc_; }
+  { int rc_ = sync_small(c, c->stream); if (rc_) return rc_; }
   if (err) return fail(err, "error raised by the device path");
   ro_activity(c, P, G, a);
   return 0;
@@ -5314,8 +5381,8 @@ int sel_select_stage(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, const do
     if (rc) return rc;
   }
   int32_t err = 0;
-  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipStreamSynchronize(c->stream));
+  { int rc_ = d2h_small(c, &err, c->err.p, 4, c->stream); if (rc_) return rc_; }
+  { int rc_ = sync_small(c, c->stream); if (rc_) return rc_; }
   if (err) return fail(err, "error raised by the device path");
   return 0;
 }
@@ -5328,7 +5395,7 @@ namespace tsdb {
 // emit flags [G * K] and group activity [G] to the host.
 int md_sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, int64_t extra_rows, double** vals,
                   int64_t* K, uint8_t* uni, uint32_t* act) {
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   Plan P;
   std::vector<uint32_t> a;
   int rc = sel_values_stage(c, q, G, extra_rows, P, a);
@@ -5343,7 +5410,7 @@ int md_sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, int64_t ext
 // ... and the owner's selection over rows on its device: out_val / out_flag [G][K] stay on it.
 int md_sel_select(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, const double* vals, const int64_t* counts,
                   const uint8_t* uni, double** out_val, uint8_t** out_flag) {
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_OK(hipSetDevice(c->device));
   Plan P;
   int rc = plan_sel(c, q, G, P);
@@ -5374,7 +5441,7 @@ void partials_offsets(int64_t G, int64_t K, int64_t* off_b, int64_t* off_n, int6
 // activity in out_val / out_flag / out_act (device memory of this context).
 int md_partials_finish(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, unsigned char* state, int64_t g_fold,
                        const unsigned char* mini, int n_mini, double* out_val, uint8_t* out_flag, uint32_t* out_act) {
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_OK(hipSetDevice(c->device));
   if (c->ro_active) { const int r = ro_check(q); if (r) return r; }
   const tsdbhip_query qr = ro_query(c, q);
@@ -5416,21 +5483,21 @@ int md_partials_finish(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, unsign
   mp.err = c->err.as<int32_t>();
   HIP_OK(launch_rank_merge(mp, c->stream));
   int32_t err = 0;
-  HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipStreamSynchronize(c->stream));
+  { int rc_ = d2h_small(c, &err, c->err.p, 4, c->stream); if (rc_) return rc_; }
+  { int rc_ = sync_small(c, c->stream); if (rc_) return rc_; }
   if (err) return fail(err, "error raised by the device path");
   return 0;
 }
 
 // local series per group id < G of the resident batch (multi.cpp: which groups straddle devices)
 std::vector<int64_t> ctx_group_counts(tsdbhip_ctx* c, int64_t G) {
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   return local_counts(c, G);
 }
 
 // resident positions [p0, p1) of group g (the resident order is group-sorted)
 void ctx_group_range(tsdbhip_ctx* c, int64_t g, int64_t* p0, int64_t* p1) {
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   *p0 = *p1 = 0;
   if (g < 0 || g >= c->n_groups) return;   // (the local sentinel n_groups marks ungrouped series)
   const auto lo = std::lower_bound(c->h_group.begin(), c->h_group.begin() + c->n_series, (int32_t)g);
@@ -5459,7 +5526,7 @@ extern "C" int tsdbhip_sel_run_values(tsdbhip_ctx* c, const tsdbhip_query* q, in
                                       void* uni, void* act) {
   MD_REFUSE(c, "tsdbhip_sel_run_values");
   if (!c || !q || !vals || !uni || !act) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   Plan P;
   std::vector<uint32_t> a;
   int rc = sel_values_stage(c, q, n_groups_global, 0, P, a);
@@ -5478,7 +5545,7 @@ extern "C" int tsdbhip_sel_select(tsdbhip_ctx* c, const tsdbhip_query* q, int64_
                                   const int64_t* counts, const void* uni, void* out_val, void* out_flag) {
   MD_REFUSE(c, "tsdbhip_sel_select");
   if (!c || !q || !counts || !uni || !out_val || !out_flag) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_OK(hipSetDevice(c->device));
   if (c->ro_active) { const int r = ro_check(q); if (r) return r; }
   const tsdbhip_query qr0 = ro_query(c, q);
@@ -5512,7 +5579,7 @@ extern "C" int tsdbhip_assemble(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t 
                                 const void* flag, const void* act, tsdbhip_result** out) {
   MD_REFUSE(c, "tsdbhip_assemble");
   if (!c || !q || !val || !flag || !act || !out) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   *out = nullptr;
   HIP_OK(hipSetDevice(c->device));
   if (c->ro_active) { const int r = ro_check(q); if (r) return r; }
@@ -5637,7 +5704,7 @@ extern "C" int tsdbhip_rollup_run(tsdbhip_ctx* c, const tsdbhip_rollup_spec* sp,
     if (f != TSDB_AGG_SUM && f != TSDB_AGG_COUNT && f != TSDB_AGG_MAX && f != TSDB_AGG_MIN)
       return fail(TSDB_E_ILLEGAL_ARGUMENT, "rollup functions are sum, count, max and min");
   }
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_OK(hipSetDevice(c->device));
   c->ro_n = 0;
   // the series with a group (ungrouped ones -- group id -1 -- sit after them and get no rollups)
@@ -5781,13 +5848,13 @@ extern "C" int tsdbhip_rollup_run(tsdbhip_ctx* c, const tsdbhip_rollup_spec* sp,
     uint32_t last_c = 0, last_v = 0;
     int32_t err = 0;
     if (NK) {
-      HIP_OK(hipMemcpyAsync(&last_off, c->ro_coff.as<int64_t>() + NK - 1, 8, hipMemcpyDeviceToHost, c->stream));
-      HIP_OK(hipMemcpyAsync(&last_voff, c->ro_voff.as<uint64_t>() + NK - 1, 8, hipMemcpyDeviceToHost, c->stream));
-      HIP_OK(hipMemcpyAsync(&last_c, rp.cnt + NK - 1, 4, hipMemcpyDeviceToHost, c->stream));
-      HIP_OK(hipMemcpyAsync(&last_v, rp.vsz + NK - 1, 4, hipMemcpyDeviceToHost, c->stream));
+      { int rc_ = d2h_small(c, &last_off, c->ro_coff.as<int64_t>() + NK - 1, 8, c->stream); if (rc_) return rc_; }
+      { int rc_ = d2h_small(c, &last_voff, c->ro_voff.as<uint64_t>() + NK - 1, 8, c->stream); if (rc_) return rc_; }
+      { int rc_ = d2h_small(c, &last_c, rp.cnt + NK - 1, 4, c->stream); if (rc_) return rc_; }
+      { int rc_ = d2h_small(c, &last_v, rp.vsz + NK - 1, 4, c->stream); if (rc_) return rc_; }
     }
-    HIP_OK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
+    { int rc_ = d2h_small(c, &err, c->err.p, 4, c->stream); if (rc_) return rc_; }
+    { int rc_ = sync_small(c, c->stream); if (rc_) return rc_; }
     // an infinite bucket value trips AggregationIterator's Inf check (IllegalStateException)
     // in the NONE-aggregator pass; for a rollup it is addAggregatePoint's rejection
     if (err == TSDB_E_ILLEGAL_STATE) err = TSDB_E_ILLEGAL_ARGUMENT;
@@ -5834,7 +5901,7 @@ extern "C" int tsdbhip_rollup_download(tsdbhip_ctx* c, int32_t* series, uint32_t
                                        uint64_t* val_off, uint8_t* value) {
   MD_REFUSE(c, "tsdbhip_rollup_download");
   if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_OK(hipSetDevice(c->device));
   int64_t cell0 = 0;
   uint64_t byte0 = 0;

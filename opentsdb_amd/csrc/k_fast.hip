@@ -42,6 +42,14 @@ static hipError_t launch_fast_k(const GridParams& p, hipStream_t s) {
         return hipGetLastError();
       }
     }
+    if constexpr (VL == 4 && QW == 2) {
+      static const char* d4 = std::getenv("TSDBHIP_SHORT_D4");   // A/B: ring depth 3 for the float class
+      if (d4 && d4[0] == '3') {
+        hipLaunchKernelGGL((k_short<F, QW, VL, 3, KR>), dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p, p.rows,
+                           p.series_row_ptr, p.tile_begin, p.tile_end);
+        return hipGetLastError();
+      }
+    }
     if (lds > 65536) {
       hipError_t e = hipFuncSetAttribute((const void*)k_short<F, QW, VL, DS, KR>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) return e;

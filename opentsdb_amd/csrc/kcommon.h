@@ -1996,7 +1996,9 @@ __device__ __forceinline__ double fast_bucket_value(uint32_t c, double a) {
 // K <= 64, no rate: the register-partial variant (emit_series_reg; RP = RegPart, or MultiReg
 // for the fused multi-aggregator pass).  OUT: the instantiation also serves the per-series
 // output modes (sel_direct / dense_out); without it the group-by kernels carry no such branch.
-template <int F, bool MARK = true, bool OUT = true, class RP>
+// (OUT 2: the per-series select output only -- k_short KR 4 -- without the other branches'
+// registers)
+template <int F, bool MARK = true, int OUT = 1, class RP>
 __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const FastLds& L, int K, int lsb, double amax,
                                                     RP& P, int64_t s, int32_t g, uint32_t nbound = 0,
                                                     double* stage = nullptr, bool* uacc = nullptr) {
@@ -2014,8 +2016,9 @@ __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const F
     const uint32_t nmax = (uint32_t)wave_max((int)c);
     if (!fast_cert<F>(nmax, lsb, amax)) return false;
   }
-  if (OUT && p.sel_direct) {
+  if (OUT == 2 || (OUT && p.sel_direct)) {
     sel_direct_out<MARK>(p, K, g, s, c != 0, fast_bucket_value<F>(c, a), stage, uacc);
+  } else if (OUT == 2) {
   } else if (OUT && p.dense_out) {
     if (lane < K) {
       p.dense_out[s * K + lane] = fast_bucket_value<F>(c, a);
@@ -2089,7 +2092,7 @@ __global__ __launch_bounds__(256) void k_fast(GridParams p, const RowDesc* __res
   // KR 0 writing the series' buckets to HBM (dense_out: a group-by step over them follows) keeps
   // no partials or rate values in LDS, so large K (a day of 1m buckets) fits the streaming kernels
   const bool dense0 = KR == 0 && p.dense_out != nullptr;
-  const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0 && !dense0, !dense0);
+  const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0 && !dense0, !KR && !dense0);
   for (int k = lane; k < K; k += 64) {
     if (!KR && !dense0) part_init(p.ga, L.w.part, k);
     L.acc[k] = fast_identity<F>();
@@ -2337,7 +2340,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
   // KR 0 writing the series' buckets to HBM (dense_out: a group-by step over them follows) keeps
   // no partials or rate values in LDS, so large K (a day of 1m buckets) fits the streaming kernels
   const bool dense0 = KR == 0 && p.dense_out != nullptr;
-  const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0 && !dense0, !dense0);
+  const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0 && !dense0, !KR && !dense0);
   for (int k = lane; k < K; k += 64) {
     if (!KR && !dense0) part_init(p.ga, L.w.part, k);
     L.acc[k] = fast_identity<F>();
@@ -2396,7 +2399,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     const int lsb = __builtin_amdgcn_readlane(dlsb, j);
     const double amax = __longlong_as_double((long long)rl64(damax, j));
     const bool fine =
-        KR ? fast_series_end_reg<F, false, OUT>(p, L, K, lsb, amax, RP, s0 + j, tgrp, (uint32_t)nv0,
+        KR ? fast_series_end_reg<F, false, KR == 4 ? 2 : (int)OUT>(p, L, K, lsb, amax, RP, s0 + j, tgrp, (uint32_t)nv0,
                                                 COLS ? stage + (((j >> 3) & 1) * 8 + (j & 7)) * K : nullptr, &uacc)
            : fast_series_end<F>(p, L, K, lsb, amax, s0 + j, tgrp);
     if (!fine) redo = true;
@@ -2522,7 +2525,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
   rows_batch<F, QW, VL, NP>(p, rows, r0, nr, 0, cur);
   rows_batch<F, QW, VL, NP>(p, rows, r0, nr, min(1, nb - 1), nxt);
   const bool dense0 = KR == 0 && p.dense_out != nullptr;
-  const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0 && !dense0, !dense0);
+  const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0 && !dense0, !KR && !dense0);
   for (int k = lane; k < K; k += 64) {
     if (!KR && !dense0) part_init(p.ga, L.w.part, k);
     L.acc[k] = fast_identity<F>();

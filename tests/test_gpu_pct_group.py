@@ -140,3 +140,22 @@ def test_pct_group_column_layout(eng, mixed_batch, monkeypatch, cols):
     b = synth.generate(300, T0, 360, 10000, value_kind=1, n_groups=1, int_mod=50, seed=3)
     q = abi.new_query(T0, T0 + 3599, "p50", ds_function=abi.AGG["max"], ds_interval_ms=60000)
     assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "p50", tol=0.0, ctx="one group")
+
+
+@pytest.mark.parametrize("variant", [{}, {"TSDBHIP_SEL_T": "1024"}, {"TSDBHIP_SEL_T": "256"},
+                                     {"TSDBHIP_SEL_HL": "1"}, {"TSDBHIP_SEL_HL": "1", "TSDBHIP_SEL_COLS": "0"}])
+def test_pct_group_select_kernels(eng, monkeypatch, variant):
+    """The register-resident select's block shapes (512 x 24 keys, 1024 x 12, 256 x 48) and the
+    upper-word variant (k_sel_hl: 32-bit keys of the upper words, the rank resolved by the lower
+    words of the values sharing the selected one) against the oracle: segments of a few values,
+    ~3000 values with clustered integers (ties in the upper and the lower words: several radix
+    digits, the lower-word passes), negative rates, members without a value, both layouts."""
+    for k, v in variant.items():
+        monkeypatch.setenv(k, v)
+    mixed = synth.generate(70, T0, 720, 5000, value_kind=2, n_groups=3, int_mod=30000, seed=11)
+    ties = synth.generate(3000, T0, 360, 10000, value_kind=1, n_groups=1, int_mod=7, seed=5)
+    for b, ds, rate in ((mixed, "avg", False), (ties, "max", False), (ties, "avg", False), (ties, "avg", True)):
+        for agg in ["p999", "p99", "median", "p50", "ep90r7"]:
+            # (rate over u mod 7: negative and positive rates of equal magnitude)
+            q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG[ds], ds_interval_ms=60000, rate=rate)
+            assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), agg, tol=0.0, ctx=f"{agg} {ds} {variant}")

@@ -8,6 +8,8 @@
 #   pmc_hwin  rocprofv3 PMC passes over the day's sum:1m-avg (k_hwin)           -> pmc_hwin/summary.txt
 #   ro        tools/rollup_read_bench.py --check (default and TSDBHIP_RO_PACK=0), traced rerun -> ro*.jsonl
 #   ro_prof   rocprofv3 --kernel-trace --stats over tools/rollup_read_bench.py    -> ro_prof/
+#   ro_api    rocprofv3 --hip-trace --stats over tools/rollup_read_bench.py (host API time) -> ro_api/
+#   c3_prof   rocprofv3 --kernel-trace --stats over config 3 p99:1m-avg            -> c3_prof/
 #   c4_prof   rocprofv3 --kernel-trace --stats over config 4 (sum, p99)           -> c4_prof/
 #   pmc_c4    PMC passes (LDS pass included) over config 4 (k_raw_top, k_raw_eval)     -> pmc_c4_summary.txt
 #   pmc_c3p99 PMC passes (LDS pass included) over config 3's sum / p99:1m-avg   -> pmc_c3p99_summary.txt
@@ -68,6 +70,14 @@ for f in ('ro', 'ro_nopack'):
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/ro_prof -o run -- python3 tools/rollup_read_bench.py \
         --steps 5 > $out/ro_prof.log 2>&1 || { tail -20 $out/ro_prof.log; exit 1; }
       python3 tools/prof_top.py $out/ro_prof 12 ;;
+    ro_api)
+      timeout -k 10 300 rocprofv3 --hip-trace --stats --output-format csv -d $out/ro_api -o run -- python3 tools/rollup_read_bench.py \
+        --steps 20 > $out/ro_api.log 2>&1 || { tail -20 $out/ro_api.log; exit 1; }
+      head -25 $out/ro_api/run_hip_api_stats.csv ;;
+    c3_prof)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/c3_prof -o run -- python3 tools/bench_configs.py \
+        --config 3 --only p99 --steps 5 > $out/c3_prof.log 2>&1 || { tail -20 $out/c3_prof.log; exit 1; }
+      python3 tools/prof_top.py $out/c3_prof 12 ;;
     c4_prof)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/c4_prof -o run -- python3 tools/bench_configs.py \
         --config 4 --steps 3 > $out/c4_prof.log 2>&1 || { tail -20 $out/c4_prof.log; exit 1; }
