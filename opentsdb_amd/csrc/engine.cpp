@@ -2460,7 +2460,7 @@ struct Plan {
   bool ordered = false;          // TSDB_QF_ORDERED float reduction: run_ordered
   bool values_only = false;      // percentile downsampling pass without the group-by step
   bool emit_only = false;        // group-by step over bucket values already in pre_dense / pre_pres
-  bool split2 = false;           // ... the second pass of a dense split: the first pass's timing stands
+  bool split2 = false;           // ... the second pass of a dense split (or after a rollup's staged pass): the first pass's timing stands
   bool seq_dense = false;        // sum / avg buckets in Java's order first (k_seq_dense), then the group-by step
   int ro_fuse = 0;               // rollup avg (1) / count (2) stage: value rows with their count rows (k_seq_rows_ro)
   bool sel_cols = false;         // sel_direct in the (group, slot) column layout
@@ -3253,6 +3253,8 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       if (shortk == 1 && fp.sel_direct && fp.sel_cols && K <= 64 && !(sge && sge[0] == '0')) {   // k_short's column stage
         fp.sel_stage = fp.wave_lds;
         fp.wave_lds += (int32_t)align16(2 * 8 * K * 8);   // two stages of 8 series (k_short KR 4)
+        const char* nte = std::getenv("TSDBHIP_SEL_NT");
+        fp.sel_nt = nte && nte[0] == '1' ? 1 : 0;
       }
       fp.waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / fp.wave_lds));
       fp.tile_list = list;
@@ -4705,6 +4707,7 @@ int ro_stage(tsdbhip_ctx* c, const tsdbhip_query* q, const tsdbhip_query& qr, Pl
     HIP_OK(launch_rollup_combine(c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->ro_cmap.as<int64_t>(),
                                  c->n_series, P.K, q->ds_function == TSDB_AGG_AVG ? 1 : 0, c->stream));
   P.emit_only = true;
+  P.split2 = true;   // the query's device time starts with this pass (its ev[0] stands)
   return 0;
 }
 

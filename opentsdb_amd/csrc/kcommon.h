@@ -2381,7 +2381,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
   // stores one slice (8 columns x 8 series: 64-B pieces) of the previous 8 series' stage, so
   // each iteration issues exactly one store: a store only every 8th series made the compiler's
   // vmcnt count assume none, and the waits for the ring's loads then also waited for the stores
-  // (68 % of wave cycles waiting, profiles/r05t).  Before the first 8 are staged the slice stores
+  // (68 % of wave cycles waiting, round-5 PMC).  Before the first 8 are staged the slice stores
   // go to the first 8 series' own entries (rewritten later), masked to this tile.
   double* stage = COLS ? (double*)(smem + (int64_t)wave * p.wave_lds + p.sel_stage) : nullptr;
   const int sl_c = lane >> 3, sl_i = lane & 7;   // a slice lane: column 8 t + sl_c, series sl_i
@@ -2389,7 +2389,10 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
   auto slice = [&](int t, int grp, int nrow) {   // slice t of 8-series group grp (rows < nrow)
     const int k = 8 * t + sl_c;
     const double v = stage[((grp & 1) * 8 + sl_i) * K + min(k, K - 1)];
-    if (k < K && sl_i < nrow) colbase[(int64_t)k * cgn + grp * 8 + sl_i] = v;
+    if (k < K && sl_i < nrow) {
+      if (p.sel_nt) __builtin_nontemporal_store(v, colbase + (int64_t)k * cgn + grp * 8 + sl_i);
+      else colbase[(int64_t)k * cgn + grp * 8 + sl_i] = v;
+    }
   };
   bool uacc = false;
   auto series_end = [&](int j, int nv0) {
