@@ -3253,8 +3253,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       if (shortk == 1 && fp.sel_direct && fp.sel_cols && K <= 64 && !(sge && sge[0] == '0')) {   // k_short's column stage
         fp.sel_stage = fp.wave_lds;
         fp.wave_lds += (int32_t)align16(2 * 8 * K * 8);   // two stages of 8 series (k_short KR 4)
-        const char* nte = std::getenv("TSDBHIP_SEL_NT");
-        fp.sel_nt = nte && nte[0] == '1' ? 1 : 0;
+
       }
       fp.waves = (int)std::max<int64_t>(1, std::min<int64_t>(4, (64 * 1024) / fp.wave_lds));
       fp.tile_list = list;

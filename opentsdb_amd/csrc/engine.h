@@ -180,7 +180,6 @@ struct GridParams {
   int32_t sel_direct;
   int32_t sel_cols;              // sel_direct into [gsp[g] * K + k * n_g + i] (contiguous (group, slot) columns)
   int32_t sel_stage;             // k_short + sel_cols: byte offset of an 8-series x K stage in the wave's LDS (0: none)
-  int32_t sel_nt;                // k_short KR 4: the column slices stored non-temporally (A/B)
   // non-null: the grid kernels write every series' bucket values / presence here
   // ([series][K], before rate and fill) instead of its SpanGroup contributions
   double* dense_out;

@@ -2389,10 +2389,7 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
   auto slice = [&](int t, int grp, int nrow) {   // slice t of 8-series group grp (rows < nrow)
     const int k = 8 * t + sl_c;
     const double v = stage[((grp & 1) * 8 + sl_i) * K + min(k, K - 1)];
-    if (k < K && sl_i < nrow) {
-      if (p.sel_nt) __builtin_nontemporal_store(v, colbase + (int64_t)k * cgn + grp * 8 + sl_i);
-      else colbase[(int64_t)k * cgn + grp * 8 + sl_i] = v;
-    }
+    if (k < K && sl_i < nrow) colbase[(int64_t)k * cgn + grp * 8 + sl_i] = v;
   };
   bool uacc = false;
   auto series_end = [&](int j, int nv0) {
