@@ -682,6 +682,11 @@ int tsdbhip_sync(tsdbhip_ctx* ctx);
  * max |value|.  Any pointer may be null. */
 int tsdbhip_debug_rows(tsdbhip_ctx* ctx, uint32_t* ndp, uint32_t* flags, int32_t* lsb, double* absmax);
 
+/* Test hook (no reference counterpart): how many percentile / median group-by queries took the
+ * sampled-window select, and how many of those fell back to the full path (a window that missed
+ * its ranks, a handed-back tile). */
+int tsdbhip_debug_sel_window(tsdbhip_ctx* ctx, int64_t* runs, int64_t* misses);
+
 #ifdef __cplusplus
 }
 #endif

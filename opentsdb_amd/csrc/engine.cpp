@@ -433,6 +433,12 @@ struct tsdbhip_ctx {
   int64_t mdp_ss = 0, mdp_se = 0, mdp = 0;
   DevBuf sel_vals, sel_sorted, sel_uni, sel_gsp;   // percentile / median group-by
   DevBuf sel_wr;                                    // sel_direct: rows of sel_vals written
+  // the sampled-window select (sel_window): window bounds [G][K], per (tile, slot) counts and
+  // values, the fail flag, the sampled tiles (by group, and as class lists for run_device)
+  DevBuf win_lo, win_hi, win_val, win_gcnt, win_cur, win_cand, win_fail, samp_tiles, samp_ptr, samp_tl, samp_tl_n;
+  int64_t win_runs = 0, win_misses = 0;        // sel_window runs, and those that fell back to the full path (tests)
+  const int32_t* tl_dev_override = nullptr;    // run_device: these class lists instead of d_tl / d_tl_n
+  const int32_t* tln_dev_override = nullptr;
   DevBuf cal_bounds;                                // calendar month / year slot boundaries
   // raw path scratch
   DevBuf r_rowpt, r_spoff, r_spn, r_grp, r_pts, r_rank, r_bm, r_wb, r_U, r_ooff, r_sg, r_su, r_ots, r_obits, r_oint,
@@ -2422,6 +2428,16 @@ extern "C" int tsdbhip_batch_download_range(tsdbhip_ctx* c, int64_t s0, int64_t 
   return 0;
 }
 
+// Test hook: sampled-window select runs and fall-backs (sel_window).
+extern "C" int tsdbhip_debug_sel_window(tsdbhip_ctx* c, int64_t* runs, int64_t* misses) {
+  MD_REFUSE(c, "tsdbhip_debug_sel_window");
+  if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
+  CtxLock lk(c);
+  if (runs) *runs = c->win_runs;
+  if (misses) *misses = c->win_misses;
+  return 0;
+}
+
 // Test hook: the per-row facts k_index derived (RowDesc.ndp / flags / lsb / absmax).
 extern "C" int tsdbhip_debug_rows(tsdbhip_ctx* c, uint32_t* ndp, uint32_t* flags, int32_t* lsb, double* absmax) {
   MD_REFUSE(c, "tsdbhip_debug_rows");
@@ -2464,6 +2480,7 @@ struct Plan {
   bool seq_dense = false;        // sum / avg buckets in Java's order first (k_seq_dense), then the group-by step
   int ro_fuse = 0;               // rollup avg (1) / count (2) stage: value rows with their count rows (k_seq_rows_ro)
   bool sel_cols = false;         // sel_direct in the (group, slot) column layout
+  bool sel_win = false;          // sel_direct through the sampled window (k_short KR 5, sel_window)
   bool multi = false;            // fused multi-aggregator pass (run_multi_fused): partials to c->mp*, no reduce
   bool multi_dev = false;        //   ... with the Welford state (a dev query among them)
   // calendar grids anchored per span that disagree (plan_calendar): each anchor's boundary
@@ -3030,6 +3047,15 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   if (const char* dbg = std::getenv("TSDBHIP_DBG")) gp.dbg = std::atoi(dbg);
   if (P.sel_direct) {   // buffers prepared by sel_values
     gp.sel_direct = 1;
+    if (P.sel_win) {   // (sel_window)
+      gp.sel_win = 1;
+      gp.win_lo = c->win_lo.as<double>();
+      gp.win_hi = c->win_hi.as<double>();
+      gp.win_val = c->win_val.as<double>();
+      gp.win_gcnt = c->win_gcnt.as<unsigned long long>();
+      gp.win_cur = c->win_cur.as<uint32_t>();
+      gp.win_cand = c->win_cand.as<double>();
+    }
     gp.sel_cols = P.sel_cols ? 1 : 0;
     gp.sel_vals = c->sel_vals.as<double>();
     gp.sel_uni = c->sel_uni.as<uint8_t>();
@@ -3200,7 +3226,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   const bool fast = hwin || fast_path_ok(c, q, P);
   if (P.multi && !fast) return fail(TSDB_E_NOT_IMPLEMENTED, "fused multi-aggregator pass without the streaming kernels");
   c->fast_used = fast;
-  HIP_OK(hipEventRecord(c->ev[0], c->stream));
+  if (!P.split2) HIP_OK(hipEventRecord(c->ev[0], c->stream));   // (split2: an earlier pass's start stands)
   if (fast) {
     // Per row class (A, B): k_short over its one-row-series tiles, k_rows over its tiles of
     // one-chunk rows, k_fast over its other tiles and over what those two handed back; k_grid
@@ -3211,8 +3237,8 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     const bool use_short = !(senv && senv[0] == '0');
     const char* renv = std::getenv("TSDBHIP_ROWS");
     const bool use_rows = !(renv && renv[0] == '0');
-    const int32_t* dl = c->d_tl.as<int32_t>();
-    const int32_t* dn = c->d_tl_n.as<int32_t>();
+    const int32_t* dl = c->tl_dev_override ? c->tl_dev_override : c->d_tl.as<int32_t>();
+    const int32_t* dn = c->tln_dev_override ? c->tln_dev_override : c->d_tl_n.as<int32_t>();
     HIP_OK(c->r1a.ensure(std::max<int64_t>(1, nt) * 4));
     HIP_OK(c->r1b.ensure(std::max<int64_t>(1, nt) * 4));
     HIP_OK(c->r3a.ensure(std::max<int64_t>(1, nt) * 4));
@@ -3250,7 +3276,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
         fp.short6 = ((shortk == 1 || shortk == 3) && !(e6 && e6[0] == '0')) ? 1 : 0;
       }
       const char* sge = std::getenv("TSDBHIP_SEL_STAGE");   // A/B: 0 = each series' column values stored directly
-      if (shortk == 1 && fp.sel_direct && fp.sel_cols && K <= 64 && !(sge && sge[0] == '0')) {   // k_short's column stage
+      if (shortk == 1 && fp.sel_direct && fp.sel_cols && !fp.sel_win && K <= 64 && !(sge && sge[0] == '0')) {   // k_short's column stage
         fp.sel_stage = fp.wave_lds;
         fp.wave_lds += (int32_t)align16(2 * 8 * K * 8);   // two stages of 8 series (k_short KR 4)
 
@@ -3844,17 +3870,198 @@ int sel_select(tsdbhip_ctx* c, const Plan& P, int64_t G, double* vals, const std
   return 0;
 }
 
+// The sampled window (percentile / median group-by over the streaming kernels' short tiles, §5.5):
+//  1. the sample pass: k_short KR 4 over every stride-th tile of each group (the column layout at
+//     those tiles' positions; ~max(640, n_g / 16) sampled series a group);
+//  2. k_win_bounds: per (group, slot) column, a window [lo, hi] around the target ranks from the
+//     sample (binomial margin);
+//  3. the main pass: k_short KR 5 over every tile: each contribution counted below / above the
+//     window, or kept; at the tile's end its counts go to the column's (atomics) and its kept
+//     values to the column's candidates (a cursor, at most WIN_CCAP a column);
+//  4. k_win_select: exact counts -> the ranks; where the window holds them, the select over the
+//     kept values -- the full path's values and ranks, so its result.
+// *done = false: the batch or query does not qualify, a tile was handed back, or a column's
+// window missed (k_win_select's fail flag): the caller runs the full path.
+// the quantile of a percentile function id (ksel.h pct_quantile)
+double pct_quantile_host(int fn) {
+  const int i = (fn - TSDB_AGG_P999) % 6;
+  return i == 0 ? 99.9 : i == 1 ? 99.0 : i == 2 ? 95.0 : i == 3 ? 90.0 : i == 4 ? 75.0 : 50.0;
+}
+
+int sel_window(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bool* done) {
+  *done = false;
+  const char* wenv = std::getenv("TSDBHIP_SEL_WIN");   // 0: never; 2: also for small groups (tests)
+  if (wenv && wenv[0] == '0') return 0;
+  const int64_t S = c->n_series, K = P.K;
+  if (P.f == F_SEL || P.emit_only || q->rate || K < 1 || K > 64 || P.none || !P.gsel || G < 1) return 0;
+  // ranks near the ends only (p90 and up): a window around the median keeps ~a quarter of the
+  // values and measured slower than the full path (config 3 median:1m-avg 8.85 vs 7.24 ms)
+  if (!(P.gsel != TSDB_AGG_MEDIAN && pct_quantile_host(P.gsel) >= 90.0) && !(wenv && wenv[0] == '2')) return 0;
+  if (!c->tl_other.empty()) return 0;
+  int64_t nshort = 0;
+  for (int cls = 0; cls < 2; cls++) {
+    if (!c->tl[cls][0].empty() || !c->tl[cls][2].empty()) return 0;
+    nshort += (int64_t)c->tl[cls][1].size();
+  }
+  if (nshort == 0 || nshort != (int64_t)c->tb.size()) return 0;
+  const std::vector<int64_t> counts = local_counts(c, G);
+  int64_t maxn = 0;
+  for (int64_t g = 0; g < G; g++) maxn = std::max(maxn, counts[g]);
+  if (maxn < 4096 && !(wenv && wenv[0] == '2')) return 0;   // small groups: the full path is cheap
+  Plan P2;
+  int rc = plan_query(c, q, P2);
+  if (rc) return rc;
+  P2.sel_direct = true;
+  P2.sel_cols = true;
+  if (!fast_path_ok(c, q, P2)) return 0;
+  // sampled tiles, by group and by class (a short tile is in one class list)
+  const int64_t nt = (int64_t)c->tb.size();
+  // every stride-th tile of a group, the stride set for ~max(640, n_g / 16) sampled series (at
+  // most WIN_SCAP positions a group go to the bounds)
+  std::vector<uint8_t> samp(nt, 0);
+  std::vector<int32_t> sptr(G + 1, 0), spos;
+  for (int64_t g = 0; g < G; g++) {
+    sptr[g] = (int32_t)spos.size();
+    const int64_t a = c->gtp[g], b = c->gtp[g + 1], ntg = b - a;
+    if (ntg <= 0) continue;
+    const int64_t g0 = c->tb[a], ng = c->te[b - 1] - g0;
+    const int64_t target = std::min<int64_t>(WIN_SCAP, std::max<int64_t>(640, ng / 16));
+    const int64_t stride = std::max<int64_t>(1, ng / std::max<int64_t>(1, target));
+    int64_t kept = 0;
+    for (int64_t t = a; t < b && kept < WIN_SCAP; t += stride) {
+      samp[t] = 1;
+      for (int64_t s = c->tb[t]; s < c->te[t] && kept < WIN_SCAP; s++, kept++) spos.push_back((int32_t)(s - g0));
+    }
+  }
+  sptr[G] = (int32_t)spos.size();
+  std::vector<int32_t> sl[2];
+  for (int cls = 0; cls < 2; cls++)
+    for (const int32_t t : c->tl[cls][1])
+      if (samp[t]) sl[cls].push_back(t);
+  std::vector<int32_t> all(sl[0]);
+  all.insert(all.end(), sl[1].begin(), sl[1].end());
+  const int32_t ncnt[7] = {0, (int32_t)sl[0].size(), 0, 0, (int32_t)sl[1].size(), 0, 0};
+  HIP_OK(c->samp_tl.ensure(std::max<size_t>(1, all.size()) * 4));
+  HIP_OK(c->samp_tl_n.ensure(8 * 4));
+  HIP_OK(c->samp_tiles.ensure(std::max<size_t>(1, spos.size()) * 4));
+  HIP_OK(c->samp_ptr.ensure((G + 1) * 4));
+  if (!all.empty()) HIP_OK(hipMemcpyAsync(c->samp_tl.p, all.data(), all.size() * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipMemcpyAsync(c->samp_tl_n.p, ncnt, 7 * 4, hipMemcpyHostToDevice, c->stream));
+  if (!spos.empty()) HIP_OK(hipMemcpyAsync(c->samp_tiles.p, spos.data(), spos.size() * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipMemcpyAsync(c->samp_ptr.p, sptr.data(), (G + 1) * 4, hipMemcpyHostToDevice, c->stream));
+  // the sample pass's buffers (as sel_values)
+  const std::vector<int64_t> gsp = seg_ptr(counts);
+  HIP_OK(c->sel_gsp.ensure((G + 1) * 8));
+  HIP_OK(c->sel_vals.ensure(std::max<int64_t>(1, S * K) * 8));
+  HIP_OK(c->sel_uni.ensure(std::max<int64_t>(1, G * K)));
+  HIP_OK(c->sel_wr.ensure(std::max<int64_t>(1, S)));
+  HIP_OK(hipMemcpyAsync(c->sel_gsp.p, gsp.data(), (G + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(hipMemsetAsync(c->sel_wr.p, 0, std::max<int64_t>(1, S), c->stream));
+  HIP_OK(hipMemsetAsync(c->sel_uni.p, 0, std::max<int64_t>(1, G * K), c->stream));
+  {
+    // run_device over the sampled tiles: the class lists swapped for the sample's
+    std::vector<int32_t> keep[2][3], keep_other;
+    int64_t keep_off[7];
+    for (int cls = 0; cls < 2; cls++)
+      for (int j = 0; j < 3; j++) keep[cls][j].swap(c->tl[cls][j]);
+    keep_other.swap(c->tl_other);
+    std::memcpy(keep_off, c->tl_off, sizeof(keep_off));
+    c->tl[0][1] = sl[0];
+    c->tl[1][1] = sl[1];
+    const int64_t off[7] = {0, 0, (int64_t)sl[0].size(), (int64_t)sl[0].size(), (int64_t)sl[0].size(),
+                            (int64_t)all.size(), (int64_t)all.size()};
+    std::memcpy(c->tl_off, off, sizeof(off));
+    c->tl_dev_override = c->samp_tl.as<int32_t>();
+    c->tln_dev_override = c->samp_tl_n.as<int32_t>();
+    rc = run_device(c, q, P2, G, false);
+    c->tl_dev_override = nullptr;
+    c->tln_dev_override = nullptr;
+    for (int cls = 0; cls < 2; cls++)
+      for (int j = 0; j < 3; j++) keep[cls][j].swap(c->tl[cls][j]);
+    keep_other.swap(c->tl_other);
+    std::memcpy(c->tl_off, keep_off, sizeof(keep_off));
+    if (rc) return rc;
+  }
+  // the windows
+  c->win_runs++;
+  HIP_OK(c->win_lo.ensure(std::max<int64_t>(1, G * K) * 8));
+  HIP_OK(c->win_hi.ensure(std::max<int64_t>(1, G * K) * 8));
+  HIP_OK(c->win_val.ensure(std::max<int64_t>(1, nt * K * WIN_CAP) * 8));
+  HIP_OK(c->win_gcnt.ensure(std::max<int64_t>(1, G * K) * 8));
+  HIP_OK(c->win_cur.ensure(std::max<int64_t>(1, G * K) * 4));
+  HIP_OK(c->win_cand.ensure(std::max<int64_t>(1, G * K * WIN_CCAP) * 8));
+  HIP_OK(c->win_fail.ensure(16));
+  HIP_OK(c->out_val.ensure(std::max<int64_t>(1, G * K) * 8));
+  HIP_OK(c->out_flag.ensure(std::max<int64_t>(1, G * K)));
+  WinParams wp{};
+  wp.vals = c->sel_vals.as<double>();
+  wp.wr = c->sel_wr.as<uint8_t>();
+  wp.group_series_ptr = c->sel_gsp.as<int64_t>();
+  wp.tile_begin = c->d_tb.as<int64_t>();
+  wp.tile_end = c->d_te.as<int64_t>();
+  wp.samp_ptr = c->samp_ptr.as<int32_t>();
+  wp.samp_pos = c->samp_tiles.as<int32_t>();
+  wp.group_tile_ptr = c->d_gtp.as<int64_t>();
+  wp.uni = c->sel_uni.as<uint8_t>();
+  wp.lo = c->win_lo.as<double>();
+  wp.hi = c->win_hi.as<double>();
+  wp.gcnt = c->win_gcnt.as<unsigned long long>();
+  wp.cur = c->win_cur.as<uint32_t>();
+  wp.cand = c->win_cand.as<double>();
+  wp.G = G;
+  wp.K = K;
+  wp.fn = P.gsel;
+  wp.out_val = c->out_val.as<double>();
+  wp.out_flag = c->out_flag.as<uint8_t>();
+  wp.err = c->err.as<int32_t>();
+  wp.fail = c->win_fail.as<int32_t>();
+
+  HIP_OK(launch_win_bounds(wp, c->stream));
+  // the main pass (its union flags and activity afresh; the sample pass's start event stands)
+  HIP_OK(hipMemsetAsync(c->sel_uni.p, 0, std::max<int64_t>(1, G * K), c->stream));
+  HIP_OK(hipMemsetAsync(c->win_fail.p, 0, 4, c->stream));
+  HIP_OK(hipMemsetAsync(c->win_gcnt.p, 0, std::max<int64_t>(1, G * K) * 8, c->stream));
+  HIP_OK(hipMemsetAsync(c->win_cur.p, 0, std::max<int64_t>(1, G * K) * 4, c->stream));
+  Plan P3 = P2;
+  P3.sel_win = true;
+  P3.split2 = true;
+  rc = run_device(c, q, P3, G, false);
+  if (rc) return rc;
+  const int64_t routed = c->redo_other;
+  HIP_OK(launch_win_select(wp, c->stream));
+  int32_t fail = 0, hb0 = 0, hb1 = 0;
+  {
+    int rc_ = d2h_small(c, &fail, c->win_fail.p, 4, c->stream);
+    if (!rc_) rc_ = d2h_small(c, &hb0, c->r_n.as<int32_t>() + 0, 4, c->stream);
+    if (!rc_) rc_ = d2h_small(c, &hb1, c->r_n.as<int32_t>() + 1, 4, c->stream);
+    if (!rc_) rc_ = sync_small(c, c->stream);
+    if (rc_) return rc_;
+  }
+  // (a tile k_short handed back was re-run by k_fast, which writes the column layout, not windows)
+  if (fail || hb0 || hb1 || routed) {
+    c->win_misses++;
+    return 0;
+  }
+  *done = true;
+  return 0;
+}
+
 // Percentile / median as the group-by aggregator (downsampled queries):
 //  1. every series' bucket values: k_pct for a percentile / median downsample function,
 //     else a NONE-aggregator pass without rate (= each span's Downsampler output);
 //  2. k_emit_vals: the SpanGroup contributions (rate, fill, LERP) per (series, slot);
 //  3. k_sel_seg: runDouble's order statistic per (group, slot) by radix select.
 int run_sel_group(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G) {
-  bool cols = false;
-  int rc = sel_values(c, q, P, G, &cols);
+  bool done = false;
+  int rc = sel_window(c, q, P, G, &done);
   if (rc) return rc;
-  rc = sel_select(c, P, G, c->sel_vals.as<double>(), local_counts(c, G), c->sel_uni.as<uint8_t>(), cols);
-  if (rc) return rc;
+  if (!done) {
+    bool cols = false;
+    rc = sel_values(c, q, P, G, &cols);
+    if (rc) return rc;
+    rc = sel_select(c, P, G, c->sel_vals.as<double>(), local_counts(c, G), c->sel_uni.as<uint8_t>(), cols);
+    if (rc) return rc;
+  }
   HIP_OK(hipEventRecord(c->ev[1], c->stream));
   HIP_OK(hipEventRecord(c->ev[2], c->stream));
   return 0;

@@ -180,6 +180,17 @@ struct GridParams {
   int32_t sel_direct;
   int32_t sel_cols;              // sel_direct into [gsp[g] * K + k * n_g + i] (contiguous (group, slot) columns)
   int32_t sel_stage;             // k_short + sel_cols: byte offset of an 8-series x K stage in the wave's LDS (0: none)
+  // sampled window (k_short KR 5, kcommon.h sel_window_out): each (group, slot) column's window
+  // [win_lo, win_hi] ([G][K]); the tile's values inside go to win_val ([tile][K][WIN_CAP], a
+  // tile's whole column) and at the tile's end to the column's candidates (win_cand
+  // [G][K][WIN_CCAP], at win_cur's cursor); the column's counts below | above << 32 in win_gcnt
+  int32_t sel_win;
+  const double* win_lo;
+  const double* win_hi;
+  double* win_val;
+  unsigned long long* win_gcnt;
+  uint32_t* win_cur;
+  double* win_cand;
   // non-null: the grid kernels write every series' bucket values / presence here
   // ([series][K], before rate and fill) instead of its SpanGroup contributions
   double* dense_out;
@@ -223,6 +234,37 @@ struct SelParams {
   int32_t* err;
 };
 static constexpr int SEL_CAP = 12288;   // values of one segment staged in LDS (96 KB)
+static constexpr int WIN_CAP = 64;      // window values kept a (tile, slot) (k_short KR 5): a tile's whole column
+static constexpr int WIN_SCAP = 2048;   // sample values a column (k_win_bounds)
+static constexpr int WIN_CCAP = 4096;   // window values a column (k_win_select)
+
+// The sampled-window select (engine.cpp sel_window): the sample pass's values of each (group,
+// slot) column (the sampled tiles' positions of the column layout) -> the window bounds; then
+// the counts and window values of the main pass -> the order statistics.
+struct WinParams {
+  const double* vals;             // the column layout (sample pass)
+  const uint8_t* wr;              // [series] written by the sample pass (other positions are stale)
+  const int64_t* group_series_ptr;
+  const int64_t* tile_begin;
+  const int64_t* tile_end;
+  const int32_t* samp_ptr;        // [G + 1] into samp_pos
+  const int32_t* samp_pos;        // the sampled positions of each group (series - group's first, <= WIN_SCAP)
+  const int64_t* group_tile_ptr;  // [G + 1] the group's tiles
+  const uint8_t* uni;             // [G][K]
+  double* lo;                     // [G][K]
+  double* hi;
+  const unsigned long long* gcnt; // [G][K] below | above << 32
+  const uint32_t* cur;            // [G][K] values inside (the candidates' cursor)
+  const double* cand;             // [G][K][WIN_CCAP] the values inside
+  int64_t G, K;
+  int32_t fn;
+  double* out_val;
+  uint8_t* out_flag;
+  int32_t* err;
+  int32_t* fail;                  // set when a column's window misses its ranks (the caller redoes the query)
+};
+hipError_t launch_win_bounds(const WinParams& p, hipStream_t s);
+hipError_t launch_win_select(const WinParams& p, hipStream_t s);
 
 // Ordered (TSDB_QF_ORDERED) reduction of the span values per (group, slot).
 struct OrdParams {

@@ -28,7 +28,7 @@ static hipError_t launch_fast_k(const GridParams& p, hipStream_t s) {
   const int64_t nl = p.n_launch > 0 ? p.n_launch : p.n_tiles;
   const int64_t blocks = (nl + p.waves - 1) / p.waves;
   const size_t lds = (size_t)p.wave_lds * p.waves;
-  if constexpr (KR == 4) {   // the staged column layout: k_short only (host: sel_stage set for shortk 1)
+  if constexpr (KR == 4 || KR == 5) {   // the staged column layout / the sampled window: k_short only (shortk 1)
     if (p.shortk != 1) return hipErrorNotSupported;
     constexpr int DS = VL == 0 ? SHORT_D0 : (QW * 2 + VL * 2 <= 16) ? SHORT_D : 2;
     if constexpr (QW == 2 && (VL == 0 || VL == SHORT6_VL4)) {
@@ -38,14 +38,6 @@ static hipError_t launch_fast_k(const GridParams& p, hipStream_t s) {
           if (e != hipSuccess) return e;
         }
         hipLaunchKernelGGL((k_short<F, QW, VL, DS, KR, 6>), dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p, p.rows,
-                           p.series_row_ptr, p.tile_begin, p.tile_end);
-        return hipGetLastError();
-      }
-    }
-    if constexpr (VL == 4 && QW == 2) {
-      static const char* d4 = std::getenv("TSDBHIP_SHORT_D4");   // A/B: ring depth 3 for the float class
-      if (d4 && d4[0] == '3') {
-        hipLaunchKernelGGL((k_short<F, QW, VL, 3, KR>), dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p, p.rows,
                            p.series_row_ptr, p.tile_begin, p.tile_end);
         return hipGetLastError();
       }
@@ -129,6 +121,7 @@ static hipError_t launch_fast_t(const GridParams& p, hipStream_t s) {
   }
   if (p.K <= 64 && !p.rate) {
     if (p.multi) return launch_fast_k<F, QW, VL, 2>(p, s);
+    if (p.sel_direct && p.sel_win && p.shortk == 1) return launch_fast_k<F, QW, VL, 5>(p, s);   // (k_short, sampled window)
     if (p.sel_direct && p.sel_stage) return launch_fast_k<F, QW, VL, 4>(p, s);   // (k_short, staged columns)
     return (p.sel_direct || p.dense_out) ? launch_fast_k<F, QW, VL, 3>(p, s) : launch_fast_k<F, QW, VL, 1>(p, s);
   }

@@ -627,11 +627,8 @@ hipError_t launch_ro_pack(const RowDesc* rows, const int32_t* partner, const int
 }
 
 template <int AVG>
-__global__ __launch_bounds__(256) void k_ro_pairs(GridParams p, double* __restrict__ dense, uint8_t* __restrict__ pres,
-                                                  const int64_t* __restrict__ cmap, int64_t n) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const RoPair P = p.ro_pairs[i];
+__device__ __forceinline__ void ro_pair(const GridParams& p, double* __restrict__ dense, uint8_t* __restrict__ pres,
+                                        const int64_t* __restrict__ cmap, const RoPair& P) {
   if ((int64_t)P.base < p.ss || (int64_t)P.base >= p.se) return;
   const int64_t s = P.series;
   if (!(P.meta & RP_OK)) {   // as k_seq_rows_ro: both series to k_seq_dense, then k_rollup_combine_list
@@ -718,6 +715,23 @@ __global__ __launch_bounds__(256) void k_ro_pairs(GridParams p, double* __restri
     }
   }
   flush();
+}
+
+template <int AVG, int U>
+__global__ __launch_bounds__(256) void k_ro_pairs(GridParams p, double* __restrict__ dense, uint8_t* __restrict__ pres,
+                                                  const int64_t* __restrict__ cmap, int64_t n) {
+  // U pairs a thread, blocks of U x 256 consecutive pairs (lane-contiguous for each u): every
+  // pair's descriptor loaded before any is walked
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x * U + threadIdx.x;
+  RoPair P[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const int64_t i = i0 + (int64_t)u * blockDim.x;
+    if (i < n) P[u] = p.ro_pairs[i];
+    else P[u].base = 0xFFFFFFFFu;   // (outside every scan range)
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) ro_pair<AVG>(p, dense, pres, cmap, P[u]);
 }
 
 // k_seq_rows over a rollup batch's packed value rows (sum / min / max ... downsampling reads the
@@ -825,9 +839,21 @@ hipError_t launch_ro_rows(const GridParams& p, int f, double* dense, uint8_t* pr
 hipError_t launch_ro_pairs(const GridParams& p, int avg, double* dense, uint8_t* pres, const int64_t* cmap, int64_t n,
                            hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  const unsigned nb = (unsigned)((n + 255) / 256);
-  if (avg) hipLaunchKernelGGL(k_ro_pairs<1>, dim3(nb), dim3(256), 0, s, p, dense, pres, cmap, n);
-  else hipLaunchKernelGGL(k_ro_pairs<0>, dim3(nb), dim3(256), 0, s, p, dense, pres, cmap, n);
+  static const char* ue = std::getenv("TSDBHIP_RO_U");   // A/B: pairs a thread (1 / 2 / 4)
+  const int U = ue ? std::atoi(ue) : 1;
+  if (U >= 4) {
+    const unsigned nb = (unsigned)((n + 1023) / 1024);
+    if (avg) hipLaunchKernelGGL((k_ro_pairs<1, 4>), dim3(nb), dim3(256), 0, s, p, dense, pres, cmap, n);
+    else hipLaunchKernelGGL((k_ro_pairs<0, 4>), dim3(nb), dim3(256), 0, s, p, dense, pres, cmap, n);
+  } else if (U == 2) {
+    const unsigned nb = (unsigned)((n + 511) / 512);
+    if (avg) hipLaunchKernelGGL((k_ro_pairs<1, 2>), dim3(nb), dim3(256), 0, s, p, dense, pres, cmap, n);
+    else hipLaunchKernelGGL((k_ro_pairs<0, 2>), dim3(nb), dim3(256), 0, s, p, dense, pres, cmap, n);
+  } else {
+    const unsigned nb = (unsigned)((n + 255) / 256);
+    if (avg) hipLaunchKernelGGL((k_ro_pairs<1, 1>), dim3(nb), dim3(256), 0, s, p, dense, pres, cmap, n);
+    else hipLaunchKernelGGL((k_ro_pairs<0, 1>), dim3(nb), dim3(256), 0, s, p, dense, pres, cmap, n);
+  }
   return hipGetLastError();
 }
 

@@ -1289,6 +1289,30 @@ __device__ __forceinline__ void sel_direct_out(const GridParams& p, int K, int32
   if (MARK && lane == 0 && p.sel_wr) p.sel_wr[s] = 1;
 }
 
+// Sampled window (KR 5): the series' contribution to lane k's column is counted below / above
+// the column's window [lo, hi] (w.pa, w.pb: loaded once a tile) or kept among the tile's window
+// values (wv: the tile's [K][WIN_CAP] block, WIN_CAP = 64 holds a tile's whole column); w.pn =
+// below | above << 8, w.pf = values inside.  NaN and
+// no contribution count nowhere (runDouble drops NaN; the full path's fill pattern is NaN).
+__device__ __forceinline__ void sel_window_out(const GridParams& p, int K, bool pr_in, double v, RegPart& w,
+                                               double* wv, bool* uacc) {
+  double cv = 0.0;
+  bool uni;
+  const bool has = slot_contribution(p, K, pr_in, v, cv, uni);
+  *uacc |= uni;
+  const int lane = lane_id();
+  if (has && lane < K && !isnan(cv)) {
+    if (cv < w.pa) {
+      w.pn += 1u;
+    } else if (cv > w.pb) {
+      w.pn += 1u << 8;
+    } else {
+      if (w.pf < (uint32_t)WIN_CAP) wv[lane * WIN_CAP + w.pf] = cv;
+      w.pf++;
+    }
+  }
+}
+
 __device__ __forceinline__ void sel_uni_flush(const GridParams& p, int K, int32_t g, bool uacc) {
   const int lane = lane_id();
   if (uacc && lane < K && !p.sel_uni[(int64_t)g * K + lane]) p.sel_uni[(int64_t)g * K + lane] = 1;
@@ -1997,7 +2021,7 @@ __device__ __forceinline__ double fast_bucket_value(uint32_t c, double a) {
 // for the fused multi-aggregator pass).  OUT: the instantiation also serves the per-series
 // output modes (sel_direct / dense_out); without it the group-by kernels carry no such branch.
 // (OUT 2: the per-series select output only -- k_short KR 4 -- without the other branches'
-// registers)
+// registers; OUT 3: the sampled window's counts and values -- KR 5)
 template <int F, bool MARK = true, int OUT = 1, class RP>
 __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const FastLds& L, int K, int lsb, double amax,
                                                     RP& P, int64_t s, int32_t g, uint32_t nbound = 0,
@@ -2016,7 +2040,9 @@ __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const F
     const uint32_t nmax = (uint32_t)wave_max((int)c);
     if (!fast_cert<F>(nmax, lsb, amax)) return false;
   }
-  if (OUT == 2 || (OUT && p.sel_direct)) {
+  if constexpr (OUT == 3) {   // (KR 5: P holds the window state, stage the tile's window values)
+    if constexpr (std::is_same_v<RP, RegPart>) sel_window_out(p, K, c != 0, fast_bucket_value<F>(c, a), P, stage, uacc);
+  } else if (OUT == 2 || (OUT && p.sel_direct)) {
     sel_direct_out<MARK>(p, K, g, s, c != 0, fast_bucket_value<F>(c, a), stage, uacc);
   } else if (OUT == 2) {
   } else if (OUT && p.dense_out) {
@@ -2281,7 +2307,7 @@ template <int F, int QW, int VL, int D, int KR, int NP = DPL>
 __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) void k_short(GridParams p, const RowDesc* __restrict__ rows,
                                                const int64_t* __restrict__ srp, const int64_t* __restrict__ tbeg,
                                                const int64_t* __restrict__ tend) {
-  constexpr bool OUT = KR == 0 || KR == 3 || KR == 4;
+  constexpr bool OUT = KR == 0 || KR == 3 || KR == 4 || KR == 5;
   // KR 4: KR 3's percentile output in the (group, slot) column layout, staged in LDS (COLS)
   constexpr bool COLS = KR == 4;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2306,6 +2332,16 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
   if (COLS) {
     cg0 = p.group_series_ptr[tgrp];
     cgn = p.group_series_ptr[tgrp + 1] - cg0;
+  }
+  // KR 5: lane k's window of column (tgrp, k), loaded before the ring as the group bounds above
+  double wlo = 0.0, whi = 0.0;
+  double* wbase = nullptr;
+  if constexpr (KR == 5) {
+    if (lane < K) {
+      wlo = p.win_lo[(int64_t)tgrp * K + lane];
+      whi = p.win_hi[(int64_t)tgrp * K + lane];
+    }
+    wbase = p.win_val + tile * K * WIN_CAP;
   }
   // premise: one row per series, in the scan range, of this kernel's class, one chunk long
   bool ok = ns <= 64 && srp[s0 + ns] - r0 == ns;
@@ -2349,6 +2385,12 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
   }
   std::conditional_t<KR == 2, MultiReg, RegPart> RP;   // KR 2: the fused multi-aggregator pass
   rp_init(p.ga, RP);
+  if constexpr (KR == 5) {   // the window state (sel_window_out)
+    RP.pa = wlo;
+    RP.pb = whi;
+    RP.pn = 0;
+    RP.pf = 0;
+  }
   if (ns > 0 && lane == 0) atomicOr(&p.group_active[tgrp], 1u);
   WAVE_SYNC();
   // The ring issues unconditionally (series index clamped to the last one) so that the
@@ -2399,8 +2441,8 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     const int lsb = __builtin_amdgcn_readlane(dlsb, j);
     const double amax = __longlong_as_double((long long)rl64(damax, j));
     const bool fine =
-        KR ? fast_series_end_reg<F, false, KR == 4 ? 2 : (int)OUT>(p, L, K, lsb, amax, RP, s0 + j, tgrp, (uint32_t)nv0,
-                                                COLS ? stage + (((j >> 3) & 1) * 8 + (j & 7)) * K : nullptr, &uacc)
+        KR ? fast_series_end_reg<F, false, KR == 5 ? 3 : KR == 4 ? 2 : (int)OUT>(p, L, K, lsb, amax, RP, s0 + j, tgrp, (uint32_t)nv0,
+                                                COLS ? stage + (((j >> 3) & 1) * 8 + (j & 7)) * K : wbase, &uacc)
            : fast_series_end<F>(p, L, K, lsb, amax, s0 + j, tgrp);
     if (!fine) redo = true;
     if constexpr (COLS) {
@@ -2439,6 +2481,22 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
     if (last >= 1)
       for (int t = nb; t < 8; t++) slice(t, last - 1, 8);
     for (int t = 0; t < 8; t++) slice(t, last, nb);
+  }
+  if constexpr (KR == 5) {   // the tile's window counts into its column's, its values inside to the candidates
+    if (lane < K && ns > 0) {
+      const int64_t col = (int64_t)tgrp * K + lane;
+      const uint32_t nin = RP.pf;
+      const unsigned long long ba = (unsigned long long)(RP.pn & 0xFFu) | ((unsigned long long)(RP.pn >> 8) << 32);
+      if (ba) atomicAdd(&p.win_gcnt[col], ba);
+      if (nin) {
+        const uint32_t at = atomicAdd(&p.win_cur[col], nin);
+        const double* src = wbase + lane * WIN_CAP;
+        double* dst = p.win_cand + col * WIN_CCAP;
+        for (uint32_t e = 0; e < nin && at + e < (uint32_t)WIN_CCAP; e++) dst[at + e] = src[e];
+      }
+    }
+    sel_uni_flush(p, K, tgrp, uacc);
+    return;
   }
   if (OUT && p.sel_wr && lane < ns) p.sel_wr[s0 + lane] = 1;   // sel_direct: every series of the tile was written
   if (OUT && p.sel_direct) sel_uni_flush(p, K, tgrp, uacc);

@@ -29,7 +29,7 @@ EXPORTS = [
     "tsdbhip_run_partials", "tsdbhip_run_partials_multi", "tsdbhip_finalize", "tsdbhip_sync", "tsdbhip_rollup_interval_parse",
     "tsdbhip_rollup_basetime", "tsdbhip_rollup_qualifier", "tsdbhip_rollup_run", "tsdbhip_rollup_download",
     "tsdbhip_sel_layout", "tsdbhip_sel_run_values", "tsdbhip_sel_select", "tsdbhip_assemble", "tsdbhip_run_multi",
-    "tsdbhip_debug_rows", "tsdbhip_shard_bounds", "tsdbhip_load_shard", "tsdbhip_synth_shard",
+    "tsdbhip_debug_rows", "tsdbhip_debug_sel_window", "tsdbhip_shard_bounds", "tsdbhip_load_shard", "tsdbhip_synth_shard",
     "tsdbhip_load_rollup", "tsdbhip_load_cells", "tsdbhip_load_histograms", "tsdbhip_hist_run",
     "tsdbhip_hist_run_range", "tsdbhip_hist_result_free", "tsdbhip_expr_map", "tsdbhip_expr_zip", "tsdbhip_expr_topn",
     "tsdbhip_batch_range_sizes", "tsdbhip_batch_download_range", "tsdbhip_expr_sync", "tsdbhip_init_devices",
@@ -137,6 +137,7 @@ def lib():
         L.tsdbhip_rollup_run.argtypes = [vp, C.POINTER(abi.RollupSpec), C.POINTER(C.c_int64), C.POINTER(C.c_uint64)]
         L.tsdbhip_rollup_download.argtypes = [vp] + [C.c_void_p] * 5
         L.tsdbhip_debug_rows.argtypes = [vp] + [C.c_void_p] * 4
+        L.tsdbhip_debug_sel_window.argtypes = [vp, C.c_void_p, C.c_void_p]
         L.tsdbhip_shard_bounds.argtypes = [C.POINTER(abi.Batch), C.c_int, C.c_int, C.c_void_p]
         L.tsdbhip_load_shard.argtypes = [vp, C.POINTER(abi.Batch), C.c_int, C.c_int64, C.c_int64]
         L.tsdbhip_synth_shard.argtypes = [vp, C.POINTER(abi.SynthSpec), C.c_int64, C.c_int64]
@@ -434,6 +435,12 @@ class Engine:
                                         amax.ctypes.data))
         k = nr.value
         return ndp[:k], flags[:k], lsb[:k], amax[:k]
+
+    def debug_sel_window(self):
+        """Test hook: (runs, misses) of the sampled-window percentile group-by select."""
+        runs, misses = C.c_int64(), C.c_int64()
+        _check(lib().tsdbhip_debug_sel_window(self.ctx, C.byref(runs), C.byref(misses)))
+        return runs.value, misses.value
 
     # ---- rollup generation (tsdbhip_rollup_run) ----
     def rollup_run(self, interval: abi.RollupInterval, start_s: int, end_s: int,

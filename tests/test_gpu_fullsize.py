@@ -103,8 +103,11 @@ def test_config3_full_size(eng):
     assert t.datapoints == 3_600_000_000
     multi = eng.run_multi([dsq(a, "1m-avg", end) for a in aggs[1:]])
     assert eng.timing().fused_queries == len(aggs) - 1   # one fused streaming pass
+    w0 = eng.debug_sel_window()
     got["p99"] = eng.run(dsq("p99", "1m-avg", end))
     got["median"] = eng.run(dsq("median", "1m-avg", end))
+    w1 = eng.debug_sel_window()
+    assert (w1[0] - w0[0], w1[1] - w0[1]) == (1, 0), f"sampled-window select runs / misses {w0} -> {w1}"   # (p99; the median keeps the full path)
     ordered = eng.run(dsq("sum", "1m-avg", end, flags=abi.QF_ORDERED))
     host = group_slice(eng, C3_GROUPS)
     assert host.n_series == 10_000 * len(C3_GROUPS)

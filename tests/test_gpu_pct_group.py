@@ -159,3 +159,58 @@ def test_pct_group_select_kernels(eng, monkeypatch, variant):
             # (rate over u mod 7: negative and positive rates of equal magnitude)
             q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG[ds], ds_interval_ms=60000, rate=rate)
             assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), agg, tol=0.0, ctx=f"{agg} {ds} {variant}")
+
+
+def test_pct_group_sampled_window(eng, monkeypatch):
+    """The sampled-window select (groups of >= 4096 spans on the short streaming tiles): a sample
+    pass over every stride-th tile bounds a window around the target ranks of each (group, slot)
+    column, the main pass keeps only the values inside it, and the select ranks them with exact
+    counts -- bit-exact against the oracle, and taken without falling back on regular data."""
+    eng.synth(60_000, T0, 360, 10000, 2, 6, 30000, 0x5EED)
+    b = eng.download()
+    r0 = eng.debug_sel_window()
+    n = 0
+    for agg in ["p99", "p999", "p95", "ep90r7", "ep99r7"]:
+        q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+        assert_groups_match(eng.run(q), O.run_query(b, q, threads=8), agg, tol=0.0, ctx=f"window {agg}")
+        n += 1
+    r1 = eng.debug_sel_window()
+    assert (r1[0] - r0[0], r1[1] - r0[1]) == (n, 0), f"window runs / misses {r0} -> {r1}"
+    # mid ranks keep the full path; TSDBHIP_SEL_WIN=2 takes the window for them too
+    q = abi.new_query(T0, T0 + 3599, "median", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+    assert_groups_match(eng.run(q), O.run_query(b, q, threads=8), "median", tol=0.0, ctx="median full path")
+    assert eng.debug_sel_window()[0] == r1[0]
+    monkeypatch.setenv("TSDBHIP_SEL_WIN", "2")
+    for agg in ["median", "p75"]:
+        q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+        assert_groups_match(eng.run(q), O.run_query(b, q, threads=8), agg, tol=0.0, ctx=f"window {agg}")
+    r2 = eng.debug_sel_window()
+    assert (r2[0] - r1[0], r2[1] - r1[1]) == (2, 0), f"window runs / misses {r1} -> {r2}"
+    # TSDBHIP_SEL_WIN=0: the full path, the same results
+    monkeypatch.setenv("TSDBHIP_SEL_WIN", "0")
+    q = abi.new_query(T0, T0 + 3599, "p99", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+    assert_groups_match(eng.run(q), O.run_query(b, q, threads=8), "p99", tol=0.0, ctx="full path")
+    assert eng.debug_sel_window()[0] == r2[0]
+
+
+@pytest.mark.parametrize("kind", ["ties", "small"])
+def test_pct_group_sampled_window_fallback(eng, monkeypatch, kind):
+    """Windows that miss (a few distinct values tie across the window: more kept values than a
+    (tile, slot) holds) and small groups forced through the window (TSDBHIP_SEL_WIN=2, sparse
+    samples): the query falls back to the full path where a column misses -- the oracle's answers
+    either way."""
+    if kind == "ties":
+        eng.synth(20_000, T0, 360, 10000, 1, 2, 3, 0x51)
+    else:
+        eng.synth(3_000, T0, 360, 10000, 2, 7, 30000, 0x52)
+    b = eng.download()
+    # (also the full path: ties of more than 256 equal keys resolved to the last bit, a round-5 fix
+    # of the 12-bit first digit -- these keys' low 3 bits were left unresolved)
+    for win in ["2", "0"]:
+        monkeypatch.setenv("TSDBHIP_SEL_WIN", win)
+        for agg in ["p99", "median", "p50"]:
+            for ds in ["avg", "max"]:
+                q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG[ds], ds_interval_ms=60000)
+                assert_groups_match(eng.run(q), O.run_query(b, q, threads=8), agg, tol=0.0,
+                                    ctx=f"{kind} {agg} {ds} win={win}")
+    assert eng.debug_sel_window()[0] > 0
