@@ -3918,6 +3918,18 @@ int sel_window(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   const int64_t nt = (int64_t)c->tb.size();
   // every stride-th tile of a group, the stride set for ~max(640, n_g / 16) sampled series (at
   // most WIN_SCAP positions a group go to the bounds)
+  // (groups whose window would keep more values than a column holds -- the window's width is
+  // ~2 x (6 sd + 2) of ~WIN_SCAP sampled ranks: large groups, p95 / p90 -- would fall back every time)
+  {
+    const double f = pct_quantile_host(P.gsel) / 100.0;
+    for (int64_t g = 0; g < G; g++) {
+      const double ng = (double)counts[g];
+      const double ns = std::min<double>(WIN_SCAP, std::max<double>(640.0, ng / 16.0));
+      if (ng >= 64 && ng * 2.0 * (6.0 * std::sqrt(ns * f * (1.0 - f)) + 2.0) / ns > 0.7 * WIN_CCAP &&
+          !(wenv && wenv[0] == '2'))
+        return 0;
+    }
+  }
   std::vector<uint8_t> samp(nt, 0);
   std::vector<int32_t> sptr(G + 1, 0), spos;
   for (int64_t g = 0; g < G; g++) {

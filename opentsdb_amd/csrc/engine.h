@@ -235,8 +235,8 @@ struct SelParams {
 };
 static constexpr int SEL_CAP = 12288;   // values of one segment staged in LDS (96 KB)
 static constexpr int WIN_CAP = 64;      // window values kept a (tile, slot) (k_short KR 5): a tile's whole column
-static constexpr int WIN_SCAP = 2048;   // sample values a column (k_win_bounds)
-static constexpr int WIN_CCAP = 4096;   // window values a column (k_win_select)
+static constexpr int WIN_SCAP = 1024;   // sample values a column (k_win_bounds)
+static constexpr int WIN_CCAP = 1024;   // window values a column (k_win_select)
 
 // The sampled-window select (engine.cpp sel_window): the sample pass's values of each (group,
 // slot) column (the sampled tiles' positions of the column layout) -> the window bounds; then

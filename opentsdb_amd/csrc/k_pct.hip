@@ -2308,63 +2308,55 @@ __global__ __launch_bounds__(T, OCC) void k_sel_hl(SelParams p) {
   }
 }
 
+template <int KPL>
+__device__ uint64_t wave_radix_select_reg(const uint64_t (&kr)[KPL], uint64_t vm, int r, SelWave& W);
+
 // ---- the sampled-window select (engine.cpp sel_window) ------------------------------------
-// k_win_bounds: one block a (group, slot) column over the sample pass's values (the sampled
-// tiles' positions of the column layout, at most WIN_SCAP): the window [lo, hi] holds the sample
-// ranks around the estimated target ranks with a binomial margin of 6 standard deviations (+2:
-// ~1e-9 a column and side, so a 60000-column query falls back about once in 10^4);
-// an end past the sample is unbounded (-inf / +inf), as is a column with fewer than 32 sampled
-// values.  The window only decides which values the main pass keeps: k_win_select checks with
-// exact counts that it holds the ranks, and a miss redoes the query on the full path.
-constexpr int WIN_T = 256;
-__global__ __launch_bounds__(WIN_T) void k_win_bounds(WinParams p) {
-  __shared__ SelShared S;
-  __shared__ unsigned long long red[2];
-  __shared__ uint32_t H[4096];
-  __shared__ int WT[WIN_T / 64];
-  __shared__ uint32_t cnt[2];
-  constexpr int R = WIN_SCAP / WIN_T;   // 8 sample positions a thread
-  const int64_t nseg = p.G * p.K;
-  const int64_t per = (nseg + 7) / 8;
-  const int64_t i = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
-  if (i >= nseg) return;
-  const int tid = threadIdx.x;
+// One wave a (group, slot) column, four a block, no block barriers: the sample and the kept values
+// are at most WIN_SCAP / WIN_CCAP = 1024, 16 keys a lane, and wave_radix_select_reg (k_raw_sel's
+// register select) ranks them.  (A block of 256 a column with k_sel_reg's select, barrier-bound:
+// bounds 0.47 ms + select 0.46 ms over config 3's 60000 columns, profiles/r05ao.)
+constexpr int WIN_KPL = 16;   // keys a lane
+__device__ __forceinline__ int64_t win_column(int64_t nseg) {
+  const int64_t nblk = (nseg + 3) / 4;
+  const int64_t per = (nblk + 7) / 8;   // blocks dealt to the XCDs in contiguous runs
+  return ((int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8) * 4 + (threadIdx.x >> 6);
+}
+
+// k_win_bounds: the window [lo, hi] of each column from the sample pass's values (the sampled
+// positions of the column layout): the sample ranks around the target ranks (estimated from the
+// sample's non-NaN fraction) with a binomial margin of 6 standard deviations + 2 (~1e-9 a column
+// and side: a 60000-column query falls back about once in 10^4); an end past the sample is
+// unbounded, as are both for fewer than 32 sampled values.  The window only decides which values
+// the main pass keeps: k_win_select checks with exact counts that it holds the ranks.
+__global__ __launch_bounds__(256) void k_win_bounds(WinParams p) {
+  __shared__ SelWave WS[4];
+  const int64_t i = win_column(p.G * p.K);
+  if (i >= p.G * p.K) return;   // (whole waves)
+  const int lane = lane_id();
+  SelWave& W = WS[threadIdx.x >> 6];
   const int64_t g = i / p.K, k = i - g * p.K;
   const int64_t g0 = p.group_series_ptr[g], n = p.group_series_ptr[g + 1] - g0;
-  const int32_t sa = p.samp_ptr[g], np = min(p.samp_ptr[g + 1] - sa, WIN_SCAP);
+  const int32_t sa = p.samp_ptr[g], np = min(p.samp_ptr[g + 1] - sa, 64 * WIN_KPL);
   const double* col = p.vals + g0 * p.K + k * n;
-  uint64_t key[R];
-  uint32_t valid = 0;
-  int nv = 0, ns = 0;
+  uint64_t kr[WIN_KPL];
+  uint64_t vm = 0;
+  int nv = 0;
 #pragma unroll
-  for (int u = 0; u < R; u++) {
-    const int j = tid + u * WIN_T;
-    bool in = false;
-    double x = 0.0;
-    if (j < np) {
-      const int32_t o = p.samp_pos[sa + j];
-      if (p.wr[g0 + o]) {   // (a sampled series without rows in the scan range was not written)
-        in = true;
-        x = col[o];
-      }
-    }
-    ns += j < np ? 1 : 0;
-    const bool v = in && !isnan(x);
+  for (int u = 0; u < WIN_KPL; u++) {
+    const int j = lane + 64 * u;
+    // (a sampled position the sample pass did not write -- a handed-back tile's series without
+    // rows in the scan range -- holds a stale value: it only shifts the window)
+    const double x = j < np ? col[p.samp_pos[sa + j]] : 0.0;
+    const bool v = j < np && !isnan(x);
+    vm |= (uint64_t)v << u;
     nv += v ? 1 : 0;
-    valid |= (v ? 1u : 0u) << u;
-    key[u] = v ? f2key(x) : ~0ULL;
+    kr[u] = f2key(x);
   }
-  nv = wave_sum_int(nv);
-  ns = wave_sum_int(ns);
-  if (tid == 0) { cnt[0] = 0; cnt[1] = 0; }
-  __syncthreads();
-  if ((tid & 63) == 0) { atomicAdd(&cnt[0], (uint32_t)nv); atomicAdd(&cnt[1], (uint32_t)ns); }
-  __syncthreads();
-  const int64_t nsv = cnt[0], nss = cnt[1];
+  const int64_t nsv = wave_sum_int(nv);
   double lo = -(double)INFINITY, hi = (double)INFINITY;
   if (nsv >= 32) {
-    // the target ranks over the whole column's estimated m, as fractions, mapped onto the sample
-    const double m_est = (double)nsv * (double)n / (double)max<int64_t>(1, nss);
+    const double m_est = (double)nsv * (double)n / (double)max(1, np);
     int64_t r0, r1;
     sel_ranks(p.fn, max<int64_t>(1, (int64_t)llround(m_est)), r0, r1);
     const double me = max(1.0, m_est);
@@ -2372,88 +2364,80 @@ __global__ __launch_bounds__(WIN_T) void k_win_bounds(WinParams p) {
     const double sd0 = sqrt((double)nsv * f0 * (1.0 - f0)), sd1 = sqrt((double)nsv * f1 * (1.0 - f1));
     const int64_t q0 = (int64_t)floor(f0 * (double)nsv - 6.0 * sd0 - 2.0);
     const int64_t q1 = (int64_t)ceil(f1 * (double)nsv + 6.0 * sd1 + 2.0);
-    if (q0 >= 0) lo = key2f(reg_radix_select<R, false, true, WIN_T>(key, valid, min(q0, nsv - 1), S, red, H, WT));
-    __syncthreads();
-    if (q1 < nsv) hi = key2f(reg_radix_select<R, false, true, WIN_T>(key, valid, max<int64_t>(q1, 0), S, red, H, WT));
+    if (q0 >= 0) lo = key2f(wave_radix_select_reg<WIN_KPL>(kr, vm, (int)min(q0, nsv - 1), W));
+    if (q1 < nsv) hi = key2f(wave_radix_select_reg<WIN_KPL>(kr, vm, (int)max<int64_t>(q1, 0), W));
   }
-  if (tid == 0) {
+  if (lane == 0) {
     p.lo[i] = lo;
     p.hi[i] = hi;
   }
 }
 
-// k_win_select: one block a column over its window counts and values (the main pass, k_short KR 5,
-// adds each tile's counts and appends its values inside): m = below + above + inside (the non-NaN contributions, as the full path's m), the ranks
-// select_sorted reads (as k_sel_reg), and when the window holds them (below <= r0, the upper rank
-// < below + inside, inside <= WIN_CCAP) their keys among the inside values by k_sel_reg's register
-// radix select -- the full path's keys, so its result; else the column sets p.fail.
-__global__ __launch_bounds__(WIN_T) void k_win_select(WinParams p) {
-  __shared__ SelShared S;
-  __shared__ unsigned long long red[2];
-  __shared__ uint32_t H[4096];
-  __shared__ int WT[WIN_T / 64];
-  constexpr int R = WIN_CCAP / WIN_T;   // 16 keys a thread
-  const int64_t nseg = p.G * p.K;
-  const int64_t per = (nseg + 7) / 8;
-  const int64_t i = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
-  if (i >= nseg) return;
-  const int tid = threadIdx.x;
-  if (!p.uni[i]) {
-    if (tid == 0) { p.out_val[i] = 0.0; p.out_flag[i] = 0; }
+// k_win_select: one wave a column over its window counts and values (the main pass, k_short KR 5,
+// adds each tile's counts and appends its values inside): m = below + above + inside (the non-NaN
+// contributions, as the full path's m), the ranks select_sorted reads (as k_sel_reg), and when the
+// window holds them (below <= r0, the upper rank < below + inside, inside <= WIN_CCAP) their keys
+// among the inside values -- the full path's keys, so its result; else the column sets p.fail.
+__global__ __launch_bounds__(256) void k_win_select(WinParams p) {
+  __shared__ SelWave WS[4];
+  const int64_t i = win_column(p.G * p.K);
+  if (i >= p.G * p.K) return;   // (whole waves)
+  const int lane = lane_id();
+  SelWave& W = WS[threadIdx.x >> 6];
+  // the flags, counts and values loaded together (the column's region holds WIN_CCAP values)
+  const double* cand = p.cand + i * WIN_CCAP;
+  const uint8_t un = p.uni[i];
+  const unsigned long long ba = p.gcnt[i];
+  const uint32_t cc = p.cur[i];
+  double x[WIN_KPL];
+#pragma unroll
+  for (int u = 0; u < 4; u++) x[u] = cand[lane + 64 * u];   // (typical p99 columns keep ~450)
+  if (!un) {
+    if (lane == 0) { p.out_val[i] = 0.0; p.out_flag[i] = 0; }
     return;
   }
-  const unsigned long long ba = p.gcnt[i];
-  const int64_t B = (int64_t)(ba & 0xFFFFFFFFull), C = p.cur[i];
+  const int64_t B = (int64_t)(ba & 0xFFFFFFFFull), C = cc;
   const int64_t m = B + (int64_t)(ba >> 32) + C;
   if (m == 0) {
-    if (tid == 0) { p.out_val[i] = (double)NAN; p.out_flag[i] = 1; }
+    if (lane == 0) { p.out_val[i] = (double)NAN; p.out_flag[i] = 1; }
     return;
   }
   int64_t r0, r1;
   sel_ranks(p.fn, m, r0, r1);
   const int64_t rhi = r1 >= 0 ? r1 : r0;
   if (C > WIN_CCAP || r0 < B || rhi >= B + C) {
-    if (tid == 0) atomicOr(p.fail, 1);
+    if (lane == 0) atomicOr(p.fail, 1);
     return;
   }
-  // the column's values inside (any order: the select only ranks them), k_sel_reg's register select
-  const double* cand = p.cand + i * WIN_CCAP;
-  uint64_t key[R];
-  uint32_t valid = 0;
 #pragma unroll
-  for (int u = 0; u < R; u++) {
-    const int j = tid + u * WIN_T;
-    const bool v = j < C;
-    valid |= (v ? 1u : 0u) << u;
-    key[u] = v ? f2key(cand[j]) : ~0ULL;
+  for (int u = 4; u < WIN_KPL; u++) x[u] = lane + 64 * u < C ? cand[lane + 64 * u] : 0.0;
+  uint64_t kr[WIN_KPL];
+  uint64_t vm = 0;
+#pragma unroll
+  for (int u = 0; u < WIN_KPL; u++) {
+    const bool v = lane + 64 * u < C;
+    vm |= (uint64_t)v << u;
+    kr[u] = v ? f2key(x[u]) : ~0ULL;
   }
-  const uint64_t k0 = reg_radix_select<R, false, true, WIN_T>(key, valid, r0 - B, S, red, H, WT);
+  const uint64_t k0 = wave_radix_select_reg<WIN_KPL>(kr, vm, (int)(r0 - B), W);
   const double v0 = key2f(k0);
   double v1 = v0;
   if (r1 >= 0) {
     // rank r1 = r0 + 1: the same key when more than r1 - B kept keys are <= k0, else the next larger
-    __syncthreads();
-    if (tid == 0) { red[0] = 0; red[1] = ~0ULL; }
-    __syncthreads();
     int le = 0;
     uint64_t gt = ~0ULL;
 #pragma unroll
-    for (int u = 0; u < R; u++) {
-      if (valid >> u & 1) {
-        if (key[u] <= k0) le++;
-        else gt = key[u] < gt ? key[u] : gt;
+    for (int u = 0; u < WIN_KPL; u++) {
+      if ((vm >> u) & 1ULL) {
+        if (kr[u] <= k0) le++;
+        else gt = kr[u] < gt ? kr[u] : gt;
       }
     }
     le = wave_sum_int(le);
     gt = wave_min_u64(gt);
-    if ((tid & 63) == 0) {
-      atomicAdd(&red[0], (unsigned long long)le);
-      atomicMin(&red[1], (unsigned long long)gt);
-    }
-    __syncthreads();
-    v1 = (int64_t)red[0] > r1 - B ? v0 : key2f(red[1]);
+    v1 = (int64_t)le > r1 - B ? v0 : key2f(gt);
   }
-  if (tid == 0) {
+  if (lane == 0) {
     const double r = select_sorted(p.fn, (int)m, [&](int j) { return (int64_t)j == r0 ? v0 : v1; });
     if (isinf(r)) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // AggregationIterator.doubleValue :640-643
     p.out_val[i] = r;
@@ -2464,14 +2448,16 @@ __global__ __launch_bounds__(WIN_T) void k_win_select(WinParams p) {
 hipError_t launch_win_bounds(const WinParams& p, hipStream_t s) {
   const int64_t n = p.G * p.K;
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_win_bounds, dim3((unsigned)(((n + 7) / 8) * 8)), dim3(WIN_T), 0, s, p);
+  const int64_t nblk = (n + 3) / 4;
+  hipLaunchKernelGGL(k_win_bounds, dim3((unsigned)(((nblk + 7) / 8) * 8)), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
 hipError_t launch_win_select(const WinParams& p, hipStream_t s) {
   const int64_t n = p.G * p.K;
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_win_select, dim3((unsigned)(((n + 7) / 8) * 8)), dim3(WIN_T), 0, s, p);
+  const int64_t nblk = (n + 3) / 4;
+  hipLaunchKernelGGL(k_win_select, dim3((unsigned)(((nblk + 7) / 8) * 8)), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
