@@ -3275,6 +3275,10 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
         const char* e6 = std::getenv("TSDBHIP_SHORT6");
         fp.short6 = ((shortk == 1 || shortk == 3) && !(e6 && e6[0] == '0')) ? 1 : 0;
       }
+      if (shortk == 1 && fp.sel_direct && fp.sel_win) {   // k_short KR 5's stage of kept values
+        fp.win_stage = fp.wave_lds;
+        fp.wave_lds += (int32_t)align16(64 * WIN_LDS * 8);
+      }
       const char* sge = std::getenv("TSDBHIP_SEL_STAGE");   // A/B: 0 = each series' column values stored directly
       if (shortk == 1 && fp.sel_direct && fp.sel_cols && !fp.sel_win && K <= 64 && !(sge && sge[0] == '0')) {   // k_short's column stage
         fp.sel_stage = fp.wave_lds;

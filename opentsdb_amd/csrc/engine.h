@@ -185,6 +185,7 @@ struct GridParams {
   // tile's whole column) and at the tile's end to the column's candidates (win_cand
   // [G][K][WIN_CCAP], at win_cur's cursor); the column's counts below | above << 32 in win_gcnt
   int32_t sel_win;
+  int32_t win_stage;             // KR 5: byte offset of the wave's LDS stage of kept values (WIN_LDS a lane)
   const double* win_lo;
   const double* win_hi;
   double* win_val;
@@ -235,6 +236,7 @@ struct SelParams {
 };
 static constexpr int SEL_CAP = 12288;   // values of one segment staged in LDS (96 KB)
 static constexpr int WIN_CAP = 64;      // window values kept a (tile, slot) (k_short KR 5): a tile's whole column
+static constexpr int WIN_LDS = 8;       // ... of which the first WIN_LDS a lane in LDS (no global store in the ring)
 static constexpr int WIN_SCAP = 1024;   // sample values a column (k_win_bounds)
 static constexpr int WIN_CCAP = 1024;   // window values a column (k_win_select)
 

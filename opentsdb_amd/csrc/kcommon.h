@@ -1295,7 +1295,7 @@ __device__ __forceinline__ void sel_direct_out(const GridParams& p, int K, int32
 // below | above << 8, w.pf = values inside.  NaN and
 // no contribution count nowhere (runDouble drops NaN; the full path's fill pattern is NaN).
 __device__ __forceinline__ void sel_window_out(const GridParams& p, int K, bool pr_in, double v, RegPart& w,
-                                               double* wv, bool* uacc) {
+                                               double* wv, double* ws, bool* uacc) {
   double cv = 0.0;
   bool uni;
   const bool has = slot_contribution(p, K, pr_in, v, cv, uni);
@@ -1307,7 +1307,9 @@ __device__ __forceinline__ void sel_window_out(const GridParams& p, int K, bool 
     } else if (cv > w.pb) {
       w.pn += 1u << 8;
     } else {
-      if (w.pf < (uint32_t)WIN_CAP) wv[lane * WIN_CAP + w.pf] = cv;
+      // the first WIN_LDS a lane in the wave's LDS stage, the rest in the tile's global slot
+      if (w.pf < (uint32_t)WIN_LDS) ws[lane * WIN_LDS + w.pf] = cv;
+      else if (w.pf < (uint32_t)WIN_CAP) wv[lane * WIN_CAP + w.pf] = cv;
       w.pf++;
     }
   }
@@ -1615,6 +1617,7 @@ struct FastLds {
   uint32_t* cnt;
   WaveLds w;          // dense == acc, pres, rate, part
   uint8_t* vstage;    // VL == 0: the row's value bytes (64 lanes x 16 B)
+  double* wstage;     // KR 5: the kept values, WIN_LDS a lane (sel_window_out)
 };
 
 __device__ __forceinline__ FastLds fast_carve(unsigned char* base, int64_t K, bool rate, bool part = true) {
@@ -1638,6 +1641,7 @@ __device__ __forceinline__ FastLds fast_carve(unsigned char* base, int64_t K, bo
   }
   f.w.dpv = nullptr; f.w.vbuf = nullptr; f.w.mq = nullptr; f.w.mv = nullptr;
   f.w.seg_slot = nullptr; f.w.seg_start = nullptr;
+  f.wstage = nullptr;
   return f;
 }
 
@@ -2041,7 +2045,7 @@ __device__ __forceinline__ bool fast_series_end_reg(const GridParams& p, const F
     if (!fast_cert<F>(nmax, lsb, amax)) return false;
   }
   if constexpr (OUT == 3) {   // (KR 5: P holds the window state, stage the tile's window values)
-    if constexpr (std::is_same_v<RP, RegPart>) sel_window_out(p, K, c != 0, fast_bucket_value<F>(c, a), P, stage, uacc);
+    if constexpr (std::is_same_v<RP, RegPart>) sel_window_out(p, K, c != 0, fast_bucket_value<F>(c, a), P, stage, L.wstage, uacc);
   } else if (OUT == 2 || (OUT && p.sel_direct)) {
     sel_direct_out<MARK>(p, K, g, s, c != 0, fast_bucket_value<F>(c, a), stage, uacc);
   } else if (OUT == 2) {
@@ -2376,7 +2380,8 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
   // KR 0 writing the series' buckets to HBM (dense_out: a group-by step over them follows) keeps
   // no partials or rate values in LDS, so large K (a day of 1m buckets) fits the streaming kernels
   const bool dense0 = KR == 0 && p.dense_out != nullptr;
-  const FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0 && !dense0, !KR && !dense0);
+  FastLds L = fast_carve(smem + (int64_t)wave * p.wave_lds, K, p.rate != 0 && !dense0, !KR && !dense0);
+  if constexpr (KR == 5) L.wstage = (double*)(smem + (int64_t)wave * p.wave_lds + p.win_stage);
   for (int k = lane; k < K; k += 64) {
     if (!KR && !dense0) part_init(p.ga, L.w.part, k);
     L.acc[k] = fast_identity<F>();
@@ -2491,8 +2496,9 @@ __global__ __launch_bounds__(256, (KR) == 2 ? SHORT_OCC2(VL) : SHORT_OCC(VL)) vo
       if (nin) {
         const uint32_t at = atomicAdd(&p.win_cur[col], nin);
         const double* src = wbase + lane * WIN_CAP;
+        const double* sl = L.wstage + lane * WIN_LDS;
         double* dst = p.win_cand + col * WIN_CCAP;
-        for (uint32_t e = 0; e < nin && at + e < (uint32_t)WIN_CCAP; e++) dst[at + e] = src[e];
+        for (uint32_t e = 0; e < nin && at + e < (uint32_t)WIN_CCAP; e++) dst[at + e] = e < (uint32_t)WIN_LDS ? sl[e] : src[e];
       }
     }
     sel_uni_flush(p, K, tgrp, uacc);
