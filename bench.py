@@ -196,8 +196,9 @@ def pmc_traffic(args, kernel_prefix: str, config3: bool = False):
 def config3_block(args, device: int):
     """BASELINE config 3's one-GPU point, the north-star target (>= 50 % of HBM for 1m-avg + sum
     over 10M series): 10M series x 1 h @10 s (even series vle int [0, 30000), odd float32), 1000
-    groups.  Times (a) sum:1m-avg and (b) the five aggregators avg/min/max/count/dev:1m-avg
-    through one tsdbhip_run_multi (one fused streaming pass + one group reduction per query),
+    groups.  Times (a) sum:1m-avg, (b) the five aggregators avg/min/max/count/dev:1m-avg
+    through one tsdbhip_run_multi (one fused streaming pass + one group reduction per query) and
+    (c) p99:1m-avg (percentile group-by),
     with the same barrier-free wall clock per step as the headline, plus the streaming kernels'
     hipEvent time for the roofline."""
     from opentsdb_amd import abi
@@ -250,6 +251,22 @@ def config3_block(args, device: int):
             "ms_per_step": multi_ms, "fused_queries": int(tm.fused_queries),
             "value": 5 * tm.datapoints / (multi_ms / 1000), "unit": "datapoints/s (x5 queries)",
             "fused_pass_ms": tm.decode_downsample_ms, "ratio_to_sum_step": multi_ms / sum_ms}
+        # (c) p99 as the group-by aggregator (PercentileAgg over each (group, slot)'s 10000 span
+        # values: the sampled-window select)
+        qp = q("p99")
+        w0 = eng.debug_sel_window()
+        for _ in range(2):
+            eng.run(qp)
+        eng.sync()
+        t = time.perf_counter()
+        for _ in range(steps):
+            eng.run(qp)
+        eng.sync()
+        p99_ms = (time.perf_counter() - t) * 1000 / steps
+        w1 = eng.debug_sel_window()
+        out["p99"] = {"ms_per_step": p99_ms, "value": tm.datapoints / (p99_ms / 1000), "unit": "datapoints/s",
+                      "ratio_to_sum_step": p99_ms / sum_ms, "window_runs": w1[0] - w0[0],
+                      "window_fallbacks": w1[1] - w0[1]}
         return out
     finally:
         eng.close()

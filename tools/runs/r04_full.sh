@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-4 closing pass: full GPU suite, smoke, the driver's bench command, kernel trace of the bench
+# closing pass (rounds 4-5): full GPU suite, smoke, the driver's bench command, kernel trace of the bench
 set -o pipefail
 tag=${1:-r04full}; out=gpurun_out/$tag
 mkdir -p $out
@@ -13,7 +13,7 @@ python3 -c "
 import json
 d=json.loads(open('$out/bench.jsonl').read().strip().splitlines()[-1])
 print('value', d['value'], 'ms', d['ms_per_step'], 'frac', d['roofline']['frac'], 'traffic', d['roofline']['traffic'])
-print('c3', json.dumps(d['extra']['config3']['sum']))"
+print('c3', json.dumps(d['extra']['config3']['sum'])); print('c3 p99', json.dumps(d['extra']['config3'].get('p99')))"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o run -- \
   python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pmc > $out/prof_bench.jsonl 2> $out/prof.err || { tail -20 $out/prof.err; exit 1; }
 find $out/prof -name '*kernel_stats.csv' -exec cp {} $out/bench_kernel_stats.csv \;
