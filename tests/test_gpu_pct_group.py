@@ -56,8 +56,10 @@ def test_pct_group_single_group_many_series(eng):
         assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), agg, tol=0.0, ctx=agg)
 
 
+@pytest.mark.parametrize("win", ["1", "2"])   # (2: the sampled window for any group size)
 @pytest.mark.parametrize("fill", [abi.FILL_NAN, abi.FILL_ZERO, abi.FILL_NULL])
-def test_pct_group_fill(eng, fill):
+def test_pct_group_fill(eng, monkeypatch, fill, win):
+    monkeypatch.setenv("TSDBHIP_SEL_WIN", win)
     b = synth.generate(20, T0 + 1800, 200, 10000, value_kind=2, n_groups=2, int_mod=1000, seed=4)
     q = abi.new_query(T0, T0 + 7199, "p90", ds_function=abi.AGG["avg"], ds_interval_ms=300000, ds_fill=fill)
     assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "p90", tol=0.0, ctx=f"fill {fill}")
@@ -76,8 +78,11 @@ def test_pct_group_all(eng, mixed_batch):
     assert_groups_match(eng.run_batch(mixed_batch, q), O.run_query(mixed_batch, q), "p75", tol=0.0, ctx="all")
 
 
-def test_pct_group_sparse_lerp(eng):
-    """Series with missing buckets and different extents: LERP-interpolated members."""
+@pytest.mark.parametrize("win", ["1", "2"])
+def test_pct_group_sparse_lerp(eng, monkeypatch, win):
+    """Series with missing buckets and different extents: LERP-interpolated members (TSDBHIP_SEL_WIN=2:
+    through the sampled window where the batch qualifies)."""
+    monkeypatch.setenv("TSDBHIP_SEL_WIN", win)
     rng = np.random.default_rng(17)
     from opentsdb_amd.store import MockStore
     st = MockStore()
@@ -98,9 +103,11 @@ def test_pct_group_sparse_lerp(eng):
         assert_groups_match(eng.run_batch(batch, q.to_abi()), O.run_query(batch, q.to_abi()), agg, tol=0.0, ctx=agg)
 
 
-def test_pct_group_nan_members(eng):
+@pytest.mark.parametrize("win", ["1", "2"])
+def test_pct_group_nan_members(eng, monkeypatch, win):
     """Buckets of NaNs (present, value NaN) are dropped by runDouble; a slot whose members
-    are all NaN yields NaN."""
+    are all NaN yields NaN (TSDBHIP_SEL_WIN=2: also through the sampled window)."""
+    monkeypatch.setenv("TSDBHIP_SEL_WIN", win)
     rng = np.random.default_rng(5)
     rows, gids = [], []
     for s in range(12):
