@@ -2445,6 +2445,75 @@ __global__ __launch_bounds__(256) void k_win_select(WinParams p) {
   }
 }
 
+// k_sel_wave<KPL>: k_sel_reg for columns of at most 64 KPL values -- one wave a (group, slot)
+// column, four a block (adjacent columns: in the [series][K] layout they read the same row lines),
+// the keys in registers and wave_radix_select_reg, no block barriers.  k_sel_reg spends a
+// 512-thread block and a 4096-bin histogram on each column, whatever its size: the multi-device
+// owners' selection (a day of 1m slots, ~250-1000 spans a column) ran at ~12 G values/s on it.
+// NaN contributions (no value) are left out of the mask: they are the largest keys, so ranks
+// 0 .. m-1 of the non-NaN values are k_sel_reg's, and so is the result.
+template <int KPL>
+__global__ __launch_bounds__(256) void k_sel_wave(SelParams p) {
+  __shared__ SelWave WS[4];
+  const int64_t i = win_column(p.G * p.K);
+  if (i >= p.G * p.K) return;   // (whole waves)
+  const int lane = lane_id();
+  SelWave& W = WS[threadIdx.x >> 6];
+  if (!p.uni[i]) {
+    if (lane == 0) { p.out_val[i] = 0.0; p.out_flag[i] = 0; }
+    return;
+  }
+  const int64_t g = i / p.K, k = i - g * p.K;
+  const int64_t gs0 = p.group_series_ptr[g], n = p.group_series_ptr[g + 1] - gs0;
+  double x[KPL];
+#pragma unroll
+  for (int u = 0; u < KPL; u++) {
+    const int64_t j = lane + 64 * u;
+    x[u] = j < n ? (p.cols ? p.vals[gs0 * p.K + k * n + j] : p.vals[(gs0 + j) * p.K + k]) : (double)NAN;
+  }
+  uint64_t kr[KPL];
+  uint64_t vm = 0;
+  int nv = 0;
+#pragma unroll
+  for (int u = 0; u < KPL; u++) {
+    const bool v = !isnan(x[u]);
+    vm |= (uint64_t)v << u;
+    nv += v ? 1 : 0;
+    kr[u] = v ? f2key(x[u]) : ~0ULL;
+  }
+  const int64_t m = wave_sum_int(nv);
+  if (m == 0) {
+    if (lane == 0) { p.out_val[i] = (double)NAN; p.out_flag[i] = 1; }
+    return;
+  }
+  int64_t r0, r1;
+  sel_ranks(p.fn, m, r0, r1);
+  const uint64_t k0 = wave_radix_select_reg<KPL>(kr, vm, (int)r0, W);
+  const double v0 = key2f(k0);
+  double v1 = v0;
+  if (r1 >= 0) {
+    // rank r1 = r0 + 1: the same key when more than r1 keys are <= k0, else the next larger key
+    int le = 0;
+    uint64_t gt = ~0ULL;
+#pragma unroll
+    for (int u = 0; u < KPL; u++) {
+      if ((vm >> u) & 1ULL) {
+        if (kr[u] <= k0) le++;
+        else gt = kr[u] < gt ? kr[u] : gt;
+      }
+    }
+    le = wave_sum_int(le);
+    gt = wave_min_u64(gt);
+    v1 = (int64_t)le > r1 ? v0 : key2f(gt);
+  }
+  if (lane == 0) {
+    const double r = select_sorted(p.fn, (int)m, [&](int j) { return (int64_t)j == r0 ? v0 : v1; });
+    if (isinf(r)) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // AggregationIterator.doubleValue :640-643
+    p.out_val[i] = r;
+    p.out_flag[i] = 1;
+  }
+}
+
 hipError_t launch_win_bounds(const WinParams& p, hipStream_t s) {
   const int64_t n = p.G * p.K;
   if (n == 0) return hipSuccess;
@@ -2658,6 +2727,16 @@ hipError_t launch_sel_seg(const SelParams& p, hipStream_t s, int64_t maxn) {
   const int64_t n = p.G * p.K;
   if (n == 0) return hipSuccess;
   const int64_t per = (n + 7) / 8;
+  // columns of at most 2048 values: a wave each (k_sel_wave); TSDBHIP_SEL_WAVE=0 keeps the block
+  const char* venv = std::getenv("TSDBHIP_SEL_WAVE");
+  if (maxn <= 64 * 32 && !(venv && venv[0] == '0')) {
+    const int64_t nblk = (n + 3) / 4;
+    const dim3 grid((unsigned)(((nblk + 7) / 8) * 8));
+    if (maxn <= 64 * 4) hipLaunchKernelGGL(k_sel_wave<4>, grid, dim3(256), 0, s, p);
+    else if (maxn <= 64 * 16) hipLaunchKernelGGL(k_sel_wave<16>, grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(k_sel_wave<32>, grid, dim3(256), 0, s, p);
+    return hipGetLastError();
+  }
   const char* renv = std::getenv("TSDBHIP_SEL_REG");
   if (maxn <= (int64_t)SEL_REG_T * SEL_REG_R && !(renv && renv[0] == '0')) {
     // two blocks per CU (8 waves / SIMD, a few spilled registers) beat one: config 3 p99

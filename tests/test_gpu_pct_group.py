@@ -159,6 +159,8 @@ def test_pct_group_select_kernels(eng, monkeypatch, variant):
     digits, the lower-word passes), negative rates, members without a value, both layouts."""
     for k, v in variant.items():
         monkeypatch.setenv(k, v)
+    if variant:   # (the block kernels also for the small segments k_sel_wave takes by default)
+        monkeypatch.setenv("TSDBHIP_SEL_WAVE", "0")
     mixed = synth.generate(70, T0, 720, 5000, value_kind=2, n_groups=3, int_mod=30000, seed=11)
     ties = synth.generate(3000, T0, 360, 10000, value_kind=1, n_groups=1, int_mod=7, seed=5)
     for b, ds, rate in ((mixed, "avg", False), (ties, "max", False), (ties, "avg", False), (ties, "avg", True)):
@@ -166,6 +168,29 @@ def test_pct_group_select_kernels(eng, monkeypatch, variant):
             # (rate over u mod 7: negative and positive rates of equal magnitude)
             q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG[ds], ds_interval_ms=60000, rate=rate)
             assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), agg, tol=0.0, ctx=f"{agg} {ds} {variant}")
+
+
+@pytest.mark.parametrize("n", [256, 1000, 2048, 2049])
+@pytest.mark.parametrize("kind", ["ties", "mixed"])
+def test_pct_group_wave_select(eng, monkeypatch, n, kind):
+    """k_sel_wave (a wave a column, columns of at most 64 x 4 / 16 / 32 values; 2049 takes the
+    block kernel) against the oracle at each size class's edge, with clustered integers (long
+    runs of equal keys) or mixed integer / float spans (empty slots past the data's end), both
+    layouts, and TSDBHIP_SEL_WAVE=0 alike.  (Members without a value: the NaN-member and sparse
+    LERP tests above, whose groups are small, so they take k_sel_wave.)"""
+    if kind == "ties":
+        eng.synth(n, T0 + 60, 300, 20000, 1, 1, 7, 0x60 + n)
+    else:
+        eng.synth(n, T0 + 60, 300, 20000, 2, 1, 30000, 0x61 + n)
+    b = eng.download()
+    for wave in ["1", "0"]:
+        monkeypatch.setenv("TSDBHIP_SEL_WAVE", wave)
+        for cols in ["1", "0"]:
+            monkeypatch.setenv("TSDBHIP_SEL_COLS", cols)
+            for agg in ["p999", "p99", "median", "p50", "ep90r7"]:
+                q = abi.new_query(T0, T0 + 7199, agg, ds_function=abi.AGG["avg"], ds_interval_ms=300000)
+                assert_groups_match(eng.run(q), O.run_query(b, q, threads=8), agg, tol=0.0,
+                                    ctx=f"{kind} n={n} {agg} wave={wave} cols={cols}")
 
 
 def test_pct_group_sampled_window(eng, monkeypatch):
