@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH/WRITE_SIZE child passes")
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 (10M series) block in `extra`")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the parity checks against the one-GPU reference (exploratory runs only)")
     ap.add_argument("--transport", choices=["auto", "rccl", "copy"], default="auto",
                     help="multi-device context (--gpus N, no launcher): RCCL send / recv or peer copies")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
@@ -205,7 +207,8 @@ def config3_block(args, device: int):
     from opentsdb_amd.engine import Engine
     eng = Engine(device)
     try:
-        eng.synth(10_000_000, T0, 360, 10000, 2, 1000, 30000, 0x5EED)
+        spec = c3_spec(args, 1)
+        eng.synth(*spec)
         eng.sync()
         index_ms = eng.timing().index_ms   # k_index at load: row classes, certificate, the vle -> int16 copy
 
@@ -216,6 +219,9 @@ def config3_block(args, device: int):
                            "1000 groups, 1m-avg", "index_ms": index_ms,
                "index_note": "load-time k_index pass (untimed in ms_per_step): row classification, the exactness "
                              "certificate and the int16 copy of the vle integer values that k_short reads"}
+        if not args.no_parity:
+            out["parity"] = md_parity(eng, device, spec, parity_queries(T0, T0 + 3599, 60000),
+                                      "config 3, 1 h store", bounds=[0, spec[0]])
         qs = q("sum")
         steps = max(3, args.steps)
         for _ in range(2):
@@ -264,6 +270,7 @@ def config3_block(args, device: int):
         eng.sync()
         p99_ms = (time.perf_counter() - t) * 1000 / steps
         w1 = eng.debug_sel_window()
+        tm = eng.timing()
         out["p99"] = {"ms_per_step": p99_ms, "value": tm.datapoints / (p99_ms / 1000), "unit": "datapoints/s",
                       "ratio_to_sum_step": p99_ms / sum_ms, "window_runs": w1[0] - w0[0],
                       "window_fallbacks": w1[1] - w0[1]}
@@ -284,6 +291,229 @@ def config3_pmc_child(args, device: int):
         eng.run(q)
     eng.sync()
     eng.close()
+
+
+# ---- parity: the timed answer against an independent one-GPU answer ----------------------
+#
+# The multi-GPU exchange between DISTINCT GPUs (RCCL all-gather / all-to-all under the launcher,
+# RCCL send / recv or peer copies in the one-process context) runs nowhere but on the node the
+# driver benches on, so every bench run checks its own answer before the timed loop: the same
+# queries through the same (sharded, exchanged) path, against the one-GPU engine over each
+# checked group's series synthesized ALONE (tsdbhip_synth_shard of the group's batch positions:
+# one context, no partial states, no exchange).  That engine is itself held to the oracle at
+# full size (tests/test_gpu_scale.py, tests/test_gpu_fullsize.py).  A group the reference fills
+# one span at a time is one SpanGroup aggregated in span order (TsdbQuery.java:916-1049).
+# Bar: timestamps, is_int flags, integer values bit for bit; order statistics, min/max/count and
+# TSDB_QF_ORDERED folds bit for bit; float sums / avg relative 1e-12 and dev 1e-9 (their tiles
+# associate differently over a smaller store).  A mismatch makes bench.py exit 1 after its line.
+
+PARITY_TOL = {"sum": 1e-12, "avg": 1e-12, "zimsum": 1e-12, "dev": 1e-9}
+PARITY_REF = ("one-GPU engine (one context, tsdbhip_run) over each checked group's series synthesized alone: "
+              "no partial states, no exchange")
+
+
+def group_span(n_series: int, n_groups: int, g: int):
+    """Batch positions [p0, p1) of group g in the group-major synthetic store (series i in
+    group i % n_groups, synth.series_order)."""
+    base, extra = divmod(n_series, n_groups)
+    p0 = g * base + min(g, extra)
+    return p0, p0 + base + (1 if g < extra else 0)
+
+
+def group_at(n_series: int, n_groups: int, pos: int) -> int:
+    base, extra = divmod(n_series, n_groups)
+    if pos < extra * (base + 1):
+        return pos // (base + 1)
+    return extra + (pos - extra * (base + 1)) // max(1, base)
+
+
+def checked_groups(n_series: int, n_groups: int, bounds, k: int = 4, cap: int = 10):
+    """Every group a shard boundary cuts or touches (both sides), then k strided groups and the
+    last one, at most `cap` in all."""
+    edge = []
+    for b in list(bounds)[1:-1]:
+        for p in (b - 1, b):
+            if 0 <= p < n_series:
+                g = group_at(n_series, n_groups, p)
+                if g not in edge:
+                    edge.append(g)
+    stride = [g for g in list(range(0, n_groups, max(1, n_groups // k))) + [n_groups - 1] if g not in edge]
+    out = edge[:cap] + stride[:max(0, cap - len(edge[:cap]))]
+    return sorted(set(out))
+
+
+def parity_queries(t0: int, t1: int, ds_ms: int, head=None, ordered: bool = True):
+    """[(name, aggregator, query, route)]; route: "partials" (decomposable, partial states),
+    "sel" (percentile group-by / ordered fold: values to the owner), "multi" (one fused pass)."""
+    from opentsdb_amd import abi
+
+    def q(agg, **kw):
+        return abi.new_query(t0, t1, agg, ds_function=abi.AGG["avg"], ds_interval_ms=ds_ms, **kw)
+    out = []
+    if head is not None:
+        out.append(("headline", head[0], head[1], "sel" if head[0].startswith(("p", "ep", "median")) else "partials"))
+    else:
+        out.append(("sum", "sum", q("sum"), "partials"))
+    out.append(("p99", "p99", q("p99"), "sel"))
+    if ordered:
+        out.append(("ordered_sum", "sum", q("sum", flags=abi.QF_ORDERED), "sel"))
+    for a in ("avg", "min", "max", "count", "dev"):
+        out.append(("multi." + a, a, q(a), "multi"))
+    return out
+
+
+def groups_map(groups, keep=None):
+    """{group id: (ts, bits, is_int)} copies of a result (only the ids in `keep`)."""
+    import numpy as np
+    out = {}
+    for g, ts, bits, isi in groups:
+        if keep is None or int(g) in keep:
+            out[int(g)] = (np.array(ts), np.array(bits), np.array(isi))
+    return out
+
+
+def compare_groups(got: dict, want: dict, agg: str, exact: bool = False):
+    """Per-query parity stats of `got` against `want` over want's groups."""
+    import numpy as np
+    tol = 0.0 if exact or agg not in PARITY_TOL else PARITY_TOL[agg]
+    st = {"groups": 0, "points": 0, "bit_exact_points": 0, "max_rel_err": 0.0, "tol": tol, "mismatch": []}
+    for g, (ts2, b2, i2) in sorted(want.items()):
+        st["groups"] += 1
+        if g not in got:
+            st["mismatch"].append(f"group {g} missing")
+            continue
+        ts1, b1, i1 = got[g]
+        st["points"] += len(ts2)
+        if len(ts1) != len(ts2) or not np.array_equal(ts1, ts2):
+            st["mismatch"].append(f"group {g}: timestamps differ ({len(ts1)} vs {len(ts2)} points)")
+            continue
+        if not np.array_equal(i1, i2):
+            st["mismatch"].append(f"group {g}: is_int flags differ")
+            continue
+        st["bit_exact_points"] += int(np.count_nonzero(b1 == b2))
+        ints = i2.astype(bool)
+        if not np.array_equal(b1[ints], b2[ints]):
+            st["mismatch"].append(f"group {g}: integer values differ")
+        d1, d2 = b1[~ints].view(np.float64), b2[~ints].view(np.float64)
+        n1, n2 = np.isnan(d1), np.isnan(d2)
+        if not np.array_equal(n1, n2):
+            st["mismatch"].append(f"group {g}: NaN positions differ")
+            continue
+        a, b = d1[~n1], d2[~n2]
+        if a.size:
+            with np.errstate(invalid="ignore", divide="ignore"):
+                rel = np.where(a == b, 0.0, np.abs(a - b) / np.maximum(np.abs(b), np.finfo(np.float64).tiny))
+            m = float(rel.max())
+            st["max_rel_err"] = max(st["max_rel_err"], m)
+            if m > tol:
+                st["mismatch"].append(f"group {g}: max relative error {m:.3g} > {tol:g}")
+    return st
+
+
+def reference_results(device: int, spec, groups, named):
+    """The independent answer: for each checked group, a one-GPU context over that group's
+    series alone (tsdbhip_synth_shard of its batch positions), every named query through
+    tsdbhip_run.  spec = tsdbhip_synth arguments (n_series, start_s, n_points, period_ms,
+    value_kind, n_groups, int_mod, seed).  Returns {name: {group: (ts, bits, is_int)}}."""
+    from opentsdb_amd.engine import Engine
+    out = {name: {} for name, _, _, _ in named}
+    ref = Engine(device)
+    try:
+        for g in groups:
+            p0, p1 = group_span(spec[0], spec[5], g)
+            ref.synth_shard(p0, p1, *spec)
+            for name, _, q, _ in named:
+                out[name].update(groups_map(ref.run(q), {g}))
+    finally:
+        ref.close()
+    return out
+
+
+def run_named(named, run_one, run_many, want_ids=None):
+    """The named queries through the path under test: run_one(q, route) -> groups,
+    run_many(qs) -> [groups] for the "multi" ones (one fused call).  Returns {name: map} and
+    {name: error string} for queries the path refused."""
+    got, errs = {}, {}
+    for name, _, q, route in named:
+        if route == "multi":
+            continue
+        try:
+            got[name] = groups_map(run_one(q, route), want_ids)
+        except Exception as ex:   # noqa: BLE001 (an engine refusal, recorded and reported)
+            errs[name] = str(ex)
+    multi = [(name, q) for name, _, q, route in named if route == "multi"]
+    if multi:
+        try:
+            res = run_many([q for _, q in multi])
+            for (name, _), r in zip(multi, res):
+                got[name] = groups_map(r, want_ids)
+        except Exception as ex:   # noqa: BLE001
+            for name, _ in multi:
+                errs[name] = str(ex)
+    return got, errs
+
+
+def parity_stats(named, got, errs, want):
+    """{name: stats} of the checked queries; refused ones carry "skipped"."""
+    out = {}
+    for name, agg, q, route in named:
+        if name in errs:
+            out[name] = {"skipped": errs[name]}
+            continue
+        from opentsdb_amd import abi
+        exact = route == "sel" or (q.flags & abi.QF_ORDERED) != 0
+        out[name] = compare_groups(got.get(name, {}), want.get(name, {}), agg, exact=exact)
+    return out
+
+
+def parity_block(stats: dict, groups, what: str, extra=None):
+    """The line's parity block: ok unless some checked query mismatched (a query the path under
+    test refused is listed, and does not count as checked)."""
+    checked = {k: v for k, v in stats.items() if "skipped" not in v}
+    bad = {k: v["mismatch"][:4] for k, v in checked.items() if v["mismatch"]}
+    blk = {"ok": not bad and bool(checked), "checked": sorted(checked), "groups": [int(g) for g in groups],
+           "what": what, "reference": PARITY_REF,
+           "bit_exact_ok": all(v["bit_exact_points"] == v["points"] for k, v in checked.items() if v["tol"] == 0.0),
+           "max_rel_err": max([v["max_rel_err"] for v in checked.values()] or [0.0]),
+           "queries": {k: ({kk: vv for kk, vv in v.items() if kk != "mismatch"} if "skipped" not in v else v)
+                       for k, v in stats.items()}}
+    if bad:
+        blk["mismatch"] = bad
+    if extra:
+        blk.update(extra)
+    return blk
+
+
+def merge_rank_stats(dist, dev, stats: dict):
+    """Sum the ranks' per-query stats (each rank checked its share of the groups), max of the
+    errors; mismatch messages stay on the rank that saw them (printed to its stderr) and are
+    counted here."""
+    import torch
+    names = sorted(stats)
+    s = torch.zeros(max(1, len(names)) * 5, dtype=torch.float64, device=dev)
+    m = torch.zeros(max(1, len(names)), dtype=torch.float64, device=dev)
+    for i, k in enumerate(names):
+        v = stats[k]
+        if "skipped" in v:
+            s[5 * i + 4] = 1
+            continue
+        s[5 * i:5 * i + 4] = torch.tensor([v["groups"], v["points"], v["bit_exact_points"], len(v["mismatch"])],
+                                          dtype=torch.float64)
+        m[i] = v["max_rel_err"]
+    dist.all_reduce(s)
+    dist.all_reduce(m, op=dist.ReduceOp.MAX)
+    s, m = s.cpu().tolist(), m.cpu().tolist()
+    out = {}
+    for i, k in enumerate(names):
+        v = stats[k]
+        if s[5 * i + 4] > 0:
+            out[k] = v if "skipped" in v else {"skipped": "refused on some rank"}
+            continue
+        out[k] = {"groups": int(s[5 * i]), "points": int(s[5 * i + 1]), "bit_exact_points": int(s[5 * i + 2]),
+                  "max_rel_err": m[i], "tol": v["tol"],
+                  "mismatch": v["mismatch"] + [f"{int(s[5 * i + 3]) - len(v['mismatch'])} on other ranks"]
+                  if int(s[5 * i + 3]) > len(v["mismatch"]) else v["mismatch"]}
+    return out
 
 
 def workload_label(args) -> str:
@@ -367,18 +597,80 @@ def md_stages(stats):
     return out
 
 
+SEL_LIMIT = 0x7FFFFFFF   # (series, slot) values one context's percentile group-by indexes (engine.cpp sel_values)
+
+
+def c3_spec(args, hours: int):
+    """tsdbhip_synth arguments of BASELINE config 3's store: 10M series @10 s, int/float32
+    alternating, 1000 groups."""
+    return (args.c3_series, T0, hours * 360, 10000, 2, 1000, 30000, 0x5EED)
+
+
+STRADDLE_SPEC = (48_000, T0, 360, 10000, 2, 61, 30000, 0x5EED ^ 0x5171)
+
+
+def straddle_note(bounds):
+    return (f"{STRADDLE_SPEC[0]} series x 1 h @10 s over {STRADDLE_SPEC[5]} groups, shards at batch positions "
+            f"{list(bounds)}: groups straddle the shard edges, so partial states merge across GPUs and the "
+            "straddling groups' span values move to their owners; every group against one GPU over the whole store")
+
+
+def straddle_reference(device: int, named):
+    """One context over the whole small straddle store: {name: {group: ...}} of every group."""
+    from opentsdb_amd.engine import Engine
+    ref = Engine(device)
+    try:
+        ref.synth(*STRADDLE_SPEC)
+        return {name: groups_map(ref.run(q)) for name, _, q, _ in named}
+    finally:
+        ref.close()
+
+
+def md_parity(eng, ref_device: int, spec, named, what: str, bounds=None):
+    """The context's answers (tsdbhip_run / tsdbhip_run_multi; on a multi-device context over
+    its shards, the exchange included) for the checked groups against the one-GPU reference."""
+    if bounds is None:
+        per = eng.md_info()[3]
+        bounds = [0] + [int(x) for x in __import__("numpy").cumsum(per)]
+    groups = checked_groups(spec[0], spec[5], bounds)
+    got, errs = run_named(named, lambda q, route: eng.run(q), eng.run_multi, set(groups))
+    want = reference_results(ref_device, spec, groups, named)
+    return parity_block(parity_stats(named, got, errs, want), groups, what,
+                        {"shard_bounds": bounds})
+
+
+def md_straddle(args, n, ref_device: int):
+    """The small straddle store on a fresh multi-device context (series shards), every group
+    against one GPU over the whole store."""
+    eng, _ = md_engine(args, n)
+    try:
+        eng.synth(*STRADDLE_SPEC)
+        named = parity_queries(T0, T0 + 3599, 60000)
+        per = eng.md_info()[3]
+        bounds = [0] + [int(x) for x in __import__("numpy").cumsum(per)]
+        got, errs = run_named(named, lambda q, route: eng.run(q), eng.run_multi)
+        _, _, moved = eng.md_stats()
+    finally:
+        eng.close()
+    want = straddle_reference(ref_device, named)
+    return parity_block(parity_stats(named, got, errs, want), sorted(next(iter(want.values()))),
+                        straddle_note(bounds), {"xfer_bytes_last_query": moved})
+
+
 def md_config3(args, n):
     """BASELINE config 3 strong-scaled over the n GPUs of the context: 10M series @10 s, 1000
     groups, int/float32 alternating -- the full 1-day store (8.64e10 dp, ~437 GB of cells) from
     4 GPUs on, 12 h at 2 GPUs (what fits 288 GB per GPU with the int16 value copy).  Series
-    shards, so the 1000 x 1440 partial states cross devices every query (RCCL)."""
+    shards, so the 1000 x 1440 partial states cross devices every query (RCCL).  Checked against
+    one GPU on strided / shard-edge groups before the timed queries (`parity`)."""
     from opentsdb_amd import abi
     from opentsdb_amd import engine as E
     hours = 24 if n >= 4 else 12
+    spec = c3_spec(args, hours)
     eng, note = md_engine(args, n)
     try:
         t = time.perf_counter()
-        eng.synth(args.c3_series, T0, hours * 360, 10000, 2, 1000, 30000, 0x5EED)
+        eng.synth(*spec)
         eng.sync()
         synth_s = time.perf_counter() - t
 
@@ -389,6 +681,10 @@ def md_config3(args, n):
                            f"1m-avg, strong-scaled over {n} GPUs (series shards, partial states over "
                            f"{'RCCL' if eng.md_info()[1] == 1 else 'peer copies'})",
                "hours": hours, "synth_s": synth_s, "transport_note": note}
+        if not args.no_parity:
+            out["parity"] = md_parity(eng, md_devices(n)[0], spec,
+                                      parity_queries(T0, T0 + hours * 3600 - 1, 60000, ordered=False),
+                                      f"config 3 strong, {hours} h store")
         steps = max(3, args.steps)
         for name, qs in (("sum", [q("sum")]), ("p99", [q("p99")]),
                          ("multi_avg_min_max_count_dev", [q(a) for a in ("avg", "min", "max", "count", "dev")])):
@@ -422,46 +718,66 @@ def md_config3(args, n):
         eng.close()
 
 
-def md_supervise(args):
-    """--gpus N > 1: the multi-device run in a child process (this one touches no GPU), under a time
-    limit.  RCCL between distinct GPUs is first exercised on the node the driver runs this on; if
-    the child fails or hangs over RCCL (transport auto), it is run once more over peer copies and the
-    line says so.  A child that refuses the GPU count (exit 2) is final."""
+def run_child(cmd, timeout):
+    """One bench child: (returncode or None on a time-out, its last JSON line or None, stderr tail).
+    Its stderr is passed through."""
     import subprocess
+    try:
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=timeout, cwd=ROOT)
+    except subprocess.TimeoutExpired as ex:
+        err = (ex.stderr or b"").decode(errors="replace")
+        sys.stderr.write(err)
+        return None, None, f"timed out after {timeout:.0f} s; " + err[-600:]
+    err = r.stderr.decode(errors="replace")
+    sys.stderr.write(err)
+    lines = [ln for ln in r.stdout.decode(errors="replace").splitlines() if ln.startswith("{")]
+    return r.returncode, (lines[-1] if lines else None), err[-600:]
+
+
+def md_supervise(args, child=None):
+    """--gpus N > 1: the multi-device run in a child process (this one touches no GPU), under a
+    time limit.  RCCL between distinct GPUs is first exercised on the node the driver runs this on.
+    Outcomes:
+      * the child prints its line and exits 0 -> that line;
+      * it exits 1 WITH a line -> its parity check failed: the line (parity.ok false), exit 1 --
+        a wrong answer is never retried over another transport;
+      * it refuses the GPU count (exit 2), or the transport was forced -> exit with its status;
+      * it fails or hangs over RCCL (transport auto) -> ONE fresh child over peer copies (never a
+        re-exec); that line is printed with `rccl_failed: true` and the RCCL error at top level
+        (its own parity block checks the peer-copy answers)."""
     argv = [a for a in sys.argv[1:]]
-
-    def child(extra):
-        cmd = [sys.executable, os.path.abspath(__file__)] + argv + ["--md-child"] + extra
-        try:
-            r = subprocess.run(cmd, stdout=subprocess.PIPE, timeout=args.md_timeout, cwd=ROOT)
-        except subprocess.TimeoutExpired:
-            return None, f"timed out after {args.md_timeout:.0f} s"
-        lines = [ln for ln in r.stdout.decode(errors="replace").splitlines() if ln.startswith("{")]
-        if r.returncode != 0 or not lines:
-            return r.returncode, f"exited {r.returncode}"
-        return 0, lines[-1]
-
-    rc, out = child([])
-    if rc == 0:
-        print(out, flush=True)
-        return
-    if rc == 2 or args.transport != "auto":
-        print(f"bench.py: multi-device run failed ({out})", file=sys.stderr, flush=True)
-        sys.exit(rc if rc else 1)
-    first = out
-    rc, out = child(["--transport", "copy"])
-    if rc != 0:
-        print(f"bench.py: multi-device run failed over RCCL ({first}) and over peer copies ({out})",
+    if child is None:
+        def child(extra):
+            return run_child([sys.executable, os.path.abspath(__file__)] + argv + ["--md-child"] + extra,
+                             args.md_timeout)
+    rc, line, err = child([])
+    if rc == 0 and line:
+        print(line, flush=True)
+        return 0
+    if rc == 1 and line:
+        print(line, flush=True)
+        print("bench.py: the multi-device answer does not match the one-GPU reference (parity block)",
               file=sys.stderr, flush=True)
-        sys.exit(rc if rc else 1)
-    line = json.loads(out)
-    line["transport_note"] = f"the RCCL run {first}; this line is the peer-copy rerun"
-    print(json.dumps(line), flush=True)
+        return 1
+    if rc == 2 or args.transport != "auto":
+        print(f"bench.py: multi-device run failed (exit {rc}): {err}", file=sys.stderr, flush=True)
+        return rc if rc else 1
+    first = f"exit {rc}" if rc is not None else "time-out"
+    rc2, line2, err2 = child(["--transport", "copy"])
+    if rc2 not in (0, 1) or not line2:
+        print(f"bench.py: multi-device run failed over RCCL ({first}: {err}) and over peer copies "
+              f"(exit {rc2}: {err2})", file=sys.stderr, flush=True)
+        return rc2 if rc2 else 1
+    d = json.loads(line2)
+    d["rccl_failed"] = True
+    d["rccl_error"] = f"{first}: {err[-400:]}"
+    d["transport_note"] = "the RCCL child failed (rccl_error); this line is the fresh peer-copy child's"
+    print(json.dumps(d), flush=True)
+    return rc2
 
 
 def main_md(args):
     """--gpus N > 1 without a launcher: one process, one multi-device context over N GPUs."""
-    from opentsdb_amd import abi
     n = args.gpus
     have = visible_gpus()
     if have <= max(md_devices(n)):
@@ -472,13 +788,19 @@ def main_md(args):
     n_dev, transport, _, _ = eng.md_info()
     total_series = args.series * n if args.scaling == "weak" else args.series
     int_mod = 30000 if args.value_kind == 2 else 2000
+    spec = (total_series, T0, args.points, args.period_ms, args.value_kind, args.groups, int_mod, 0x5EED)
     t_gen = time.perf_counter()
-    eng.synth(total_series, T0, args.points, args.period_ms, args.value_kind, args.groups, int_mod, 0x5EED)
+    eng.synth(*spec)
     eng.sync()
     t_gen = time.perf_counter() - t_gen
     _, _, mode, per_series = eng.md_info()
     index_ms = eng.timing().index_ms
     q = query(args)
+    parity = None
+    if not args.no_parity:
+        t1 = T0 + args.points * args.period_ms // 1000 - 1
+        parity = md_parity(eng, md_devices(n)[0], spec,
+                           parity_queries(T0, t1, q.ds_interval_ms, head=(args.agg, q)), "headline store")
     for _ in range(args.warmup):
         eng.run(q)
     eng.sync()
@@ -498,7 +820,10 @@ def main_md(args):
     dev_gbs = [b / (ms / 1000.0) / 1e9 if ms > 0 else 0.0 for b, ms in zip(dev_bytes, dev_ms)]
     achieved = sum(dev_gbs) / n
     eng.close()
+    if parity is not None:
+        parity["straddle"] = md_straddle(args, n, md_devices(n)[0])
     extra = None if args.no_config3 else {"config3_strong": md_config3(args, n)}
+    ok = parity_all_ok(parity, extra)
     line = {
         "metric": "raw datapoints/sec through downsample+group-by; % of HBM BW, 1-8 GPUs",
         "value": value,
@@ -517,7 +842,10 @@ def main_md(args):
         "devices": md_devices(n),
         "transport": {0: "peer copies", 1: "RCCL send/recv"}.get(transport, str(transport)),
         "transport_note": note,
+        "rccl_failed": False,
         "rccl_ranks": ranks,
+        "parity_ok": ok,
+        "parity": parity,
         "exchange_ms": tm.exchange_ms,
         "stages": md_stages(stats),
         "xfer_bytes_per_step": stats[-1][1],
@@ -549,54 +877,260 @@ def main_md(args):
         "extra": extra,
     }
     print(json.dumps(line), flush=True)
+    if not ok:
+        sys.exit(1)
+
+
+def parity_all_ok(parity, extra) -> bool:
+    """Every parity block of the line (headline, straddle, config 3) is ok."""
+    blocks = []
+    if parity is not None:
+        blocks.append(parity)
+        if parity.get("straddle") is not None:
+            blocks.append(parity["straddle"])
+    for v in (extra or {}).values():
+        if isinstance(v, dict) and v.get("parity") is not None:
+            blocks.append(v["parity"])
+    return all(b.get("ok") for b in blocks)
+
+
+# ---- one process per GPU (torch.distributed.run) ------------------------------------------
+class Launch:
+    """This rank under torch.distributed.run: RANK / WORLD_SIZE / LOCAL_RANK from the env; the
+    backend is RCCL ("nccl").  Rehearsal hooks for a one-GPU box: TSDBHIP_BENCH_DIST=gloo (host
+    tensors; several ranks may share a GPU), TSDBHIP_BENCH_DEVICES="0,0" (GPU per local rank),
+    TSDBHIP_BENCH_FORCE_DIST=1 (the distributed path at WORLD_SIZE 1: a one-rank RCCL
+    communicator)."""
+
+    def __init__(self):
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        devs = os.environ.get("TSDBHIP_BENCH_DEVICES")
+        self.device = int(devs.split(",")[self.local_rank]) if devs else self.local_rank
+        self.backend = os.environ.get("TSDBHIP_BENCH_DIST", "nccl")
+        self.dist = None
+        self.tdev = "cpu"
+
+    def init(self):
+        if self.world > 1 or os.environ.get("TSDBHIP_BENCH_FORCE_DIST") == "1":
+            import torch
+            import torch.distributed as td
+            if self.backend == "nccl":
+                torch.cuda.set_device(self.device)
+                self.tdev = f"cuda:{self.device}"
+            td.init_process_group(self.backend)
+            self.dist = td
+        return self
+
+    def sync(self, eng=None):
+        if eng is not None:
+            eng.sync()
+        if self.dist is not None:
+            import torch
+            if self.backend == "nccl":
+                torch.cuda.synchronize(self.device)
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if self.dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device=self.tdev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x: int) -> int:
+        if self.dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.int64, device=self.tdev)
+        self.dist.all_reduce(t)
+        return int(t.item())
+
+    def runner(self, eng, n_groups: int):
+        """(run_one(q, route), run_many(qs)) through this launch's path: the one-GPU calls without
+        a process group; the exchange of opentsdb_amd.dist with one."""
+        from opentsdb_amd import dist as D
+        if self.dist is None:
+            return (lambda q, route: eng.run(q)), eng.run_multi
+        gdev = self.tdev if self.backend == "nccl" else None
+
+        def one(q, route):
+            if route == "sel":
+                return D.run_distributed_sel(eng, q, self.dist, n_groups, device=gdev)
+            return D.run_distributed(eng, q, self.dist, n_groups, device=gdev)
+        return one, (lambda qs: D.run_distributed_multi(eng, qs, self.dist, n_groups, device=gdev))
+
+
+def sel_fits(bounds, n_slots: int) -> bool:
+    """Every shard's percentile group-by fits one context's select index (the same answer on
+    every rank, so no rank enters a collective the others skip)."""
+    return max(b1 - b0 for b0, b1 in zip(bounds[:-1], bounds[1:])) * n_slots <= SEL_LIMIT
+
+
+def launch_parity(L: Launch, eng, spec, bounds, named, what: str):
+    """The launch's answers for the checked groups (every rank runs every query: collectives),
+    each rank checking its share of the groups against the one-GPU reference on its own GPU."""
+    groups = checked_groups(spec[0], spec[5], bounds)
+    one, many = L.runner(eng, spec[5])
+    got, errs = run_named(named, one, many, set(groups))
+    mine = groups[L.rank::L.world]
+    want = reference_results(L.device, spec, mine, named)
+    stats = parity_stats(named, got, errs, want)
+    for k, v in stats.items():
+        for m in v.get("mismatch", []):
+            print(f"bench.py rank {L.rank}: parity {what} {k}: {m}", file=sys.stderr, flush=True)
+    if L.dist is not None:
+        stats = merge_rank_stats(L.dist, L.tdev, stats)
+    return parity_block(stats, groups, what, {"shard_bounds": [int(b) for b in bounds]})
+
+
+def launch_straddle(L: Launch):
+    """The small straddle store split over the ranks; every rank checks every group against
+    one GPU over the whole store."""
+    from opentsdb_amd.dist import synth_bounds
+    from opentsdb_amd.engine import Engine
+    bounds = synth_bounds(STRADDLE_SPEC[0], L.world)
+    named = parity_queries(T0, T0 + 3599, 60000)
+    eng = Engine(L.device)
+    try:
+        eng.synth_shard(bounds[L.rank], bounds[L.rank + 1], *STRADDLE_SPEC)
+        one, many = L.runner(eng, STRADDLE_SPEC[5])
+        got, errs = run_named(named, one, many)
+    finally:
+        eng.close()
+    want = straddle_reference(L.device, named)
+    stats = parity_stats(named, got, errs, want)
+    bad = sum(len(v.get("mismatch", [])) for v in stats.values())
+    if L.dist is not None:   # every rank compared the same groups: agree on the verdict
+        import torch
+        t = torch.tensor([bad], dtype=torch.int64, device=L.tdev)
+        L.dist.all_reduce(t)
+        if int(t.item()) and not bad:
+            stats["_other_ranks"] = {"groups": 0, "points": 0, "bit_exact_points": 0, "max_rel_err": 0.0,
+                                     "tol": 0.0, "mismatch": [f"{int(t.item())} mismatches on other ranks"]}
+    return parity_block(stats, sorted(next(iter(want.values()))), straddle_note(bounds))
+
+
+def launch_config3(args, L: Launch):
+    """BASELINE config 3 strong-scaled over the launch's ranks (one process per GPU): the global
+    10M-series store, rank r synthesizing its contiguous shard (tsdbhip_synth_shard) -- the full
+    day from 4 GPUs on, 12 h at 2 -- sum through the partial-state all-gather, p99 through the
+    owner exchange, avg/min/max/count/dev through one fused pass and one all-gather.  Checked
+    against one GPU on strided / shard-edge groups first."""
+    from opentsdb_amd import abi
+    from opentsdb_amd.dist import synth_bounds
+    from opentsdb_amd.engine import Engine, EngineError
+    hours = 24 if L.world >= 4 else 12
+    spec = c3_spec(args, hours)
+    bounds = synth_bounds(spec[0], L.world)
+    t1 = T0 + hours * 3600 - 1
+    K = hours * 60
+    eng = Engine(L.device)
+    try:
+        t = time.perf_counter()
+        eng.synth_shard(bounds[L.rank], bounds[L.rank + 1], *spec)
+        eng.sync()
+        synth_s = L.max(time.perf_counter() - t)
+        index_ms = L.max(eng.timing().index_ms)
+        fits = sel_fits(bounds, K)
+        out = {"workload": f"BASELINE config 3: {spec[0] / 1e6:g}M series x {hours} h @10 s (int/float32 alternating), "
+                           f"1000 groups, 1m-avg, strong-scaled over {L.world} ranks (one process per GPU, series shards, "
+                           f"{'RCCL' if L.backend == 'nccl' else L.backend} collectives)",
+               "hours": hours, "synth_s": synth_s, "index_ms_max": index_ms}
+        named = parity_queries(T0, t1, 60000, ordered=False)
+        if not fits:
+            named = [x for x in named if x[3] != "sel"]
+        if not args.no_parity:
+            out["parity"] = launch_parity(L, eng, spec, bounds, named, f"config 3 strong, {hours} h store")
+            if not fits:
+                out["parity"]["queries"]["p99"] = {"skipped": "more (series, slot) values per rank than the select indexes"}
+
+        def q(agg):
+            return abi.new_query(T0, t1, agg, ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+        one, many = L.runner(eng, 1000)
+        steps = max(3, args.steps)
+        plan = [("sum", [q("sum")], "partials"), ("p99", [q("p99")], "sel"),
+                ("multi_avg_min_max_count_dev", [q(a) for a in ("avg", "min", "max", "count", "dev")], "multi")]
+        for name, qs, route in plan:
+            if route == "sel" and not fits:
+                out[name] = {"skipped": f"{max(b1 - b0 for b0, b1 in zip(bounds[:-1], bounds[1:]))} series x {K} "
+                                        "slots per rank exceed the select index (2^31)"}
+                continue
+
+            def step():
+                return many(qs) if route == "multi" else one(qs[0], route)
+            try:
+                for _ in range(2):
+                    step()
+            except EngineError as ex:
+                out[name] = {"skipped": str(ex)}
+                continue
+            L.sync(eng)
+            kms = []
+            t = time.perf_counter()
+            for _ in range(steps):
+                step()
+                kms.append(eng.timing().decode_downsample_ms)
+            L.sync(eng)
+            ms = L.max((time.perf_counter() - t) * 1000 / steps)
+            tm = eng.timing()
+            dps = L.sum(int(tm.datapoints))
+            byts = L.sum(int(tm.bytes))
+            out[name] = {"ms_per_step": ms, "value": len(qs) * dps / (ms / 1000),
+                         "unit": "datapoints/s" + (f" (x{len(qs)} queries)" if len(qs) > 1 else ""),
+                         "device_pass_ms_max": L.max(sum(kms) / len(kms)),
+                         "hbm_frac_step_per_gpu": byts / L.world / (ms / 1000) / 1e9 / BYTES_PEAK_GBS}
+        m5, s1 = out.get("multi_avg_min_max_count_dev", {}), out.get("sum", {})
+        if "ms_per_step" in m5 and "ms_per_step" in s1:
+            out["multi_ratio_to_sum_step"] = m5["ms_per_step"] / s1["ms_per_step"]
+        return out
+    finally:
+        eng.close()
 
 
 def main():
     args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and args.gpus not in (1, world):
-        print(f"bench.py: --gpus {args.gpus} under a launcher with WORLD_SIZE={world}", file=sys.stderr, flush=True)
+    L = Launch()
+    if L.world > 1 and args.gpus not in (1, L.world):
+        print(f"bench.py: --gpus {args.gpus} under a launcher with WORLD_SIZE={L.world}", file=sys.stderr, flush=True)
         sys.exit(2)
-    if world == 1 and args.gpus > 1 and not args.pmc_child:
-        return main_md(args) if args.md_child else md_supervise(args)
+    if L.world == 1 and args.gpus > 1 and not args.pmc_child:
+        if args.md_child:
+            return main_md(args)
+        sys.exit(md_supervise(args))
     if args.pmc_child_config3:
-        return config3_pmc_child(args, local_rank)
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist_
-        torch.cuda.set_device(local_rank)
-        dist_.init_process_group("nccl")
-        dist = dist_
+        return config3_pmc_child(args, L.device)
+    L.init()
+    rank, world = L.rank, L.world
     from opentsdb_amd.engine import Engine
-    from opentsdb_amd import abi
+    from opentsdb_amd.dist import synth_bounds
 
-    eng = Engine(local_rank)
+    eng = Engine(L.device)
     # a tiny store first: loads the index kernels' code objects, so index_ms is the load of
     # the real store alone
     eng.synth(256, T0, args.points, args.period_ms, args.value_kind, min(args.groups, 256), 30000, 1)
-    t_gen = time.perf_counter()
     int_mod = 30000 if args.value_kind == 2 else 2000
-    if args.scaling == "strong":
-        from opentsdb_amd.dist import synth_bounds
-        b = synth_bounds(args.series, world)
-        eng.synth_shard(b[rank], b[rank + 1], args.series, T0, args.points, args.period_ms, args.value_kind,
-                        args.groups, int_mod, 0x5EED)
+    # one global store (series i in group i % G, batch group-major): weak scaling gives every rank
+    # --series of it, strong scaling splits --series over the ranks; rank r synthesizes its
+    # contiguous shard of batch positions (tsdbhip_synth_shard), the same bytes a one-GPU store has
+    total = args.series * world if args.scaling == "weak" else args.series
+    spec = (total, T0, args.points, args.period_ms, args.value_kind, args.groups, int_mod, 0x5EED)
+    bounds = synth_bounds(total, world)
+    t_gen = time.perf_counter()
+    if world == 1:
+        eng.synth(*spec)
     else:
-        eng.synth(args.series, T0, args.points, args.period_ms, args.value_kind, args.groups, int_mod,
-                  0x5EED ^ (rank * 0x9E3779B97F4A7C15 & 0xFFFFFFFFFFFFFFFF))
+        eng.synth_shard(bounds[rank], bounds[rank + 1], *spec)
     eng.sync()
     t_gen = time.perf_counter() - t_gen
     index_ms = eng.timing().index_ms   # k_index at load (row classification / validation)
     q = query(args)
+    one, _ = L.runner(eng, args.groups)
 
     def step():
-        if dist is None:
-            return eng.run(q)
-        from opentsdb_amd.dist import run_distributed
-        return run_distributed(eng, q, dist, args.groups, device=f"cuda:{local_rank}")
+        return one(q, "sel" if args.agg.startswith(("p", "ep", "median")) else "partials")
 
     if args.pmc_child:
         for _ in range(args.steps):
@@ -604,13 +1138,15 @@ def main():
         eng.sync()
         eng.close()
         return
+    parity = None
+    if not args.no_parity:
+        named = parity_queries(T0, T0 + args.points * args.period_ms // 1000 - 1, q.ds_interval_ms, head=(args.agg, q))
+        if not sel_fits(bounds, max(1, args.points * args.period_ms // max(1, q.ds_interval_ms))):
+            named = [x for x in named if x[3] != "sel"]
+        parity = launch_parity(L, eng, spec, bounds, named, "headline store")
     for _ in range(args.warmup):
         step()
-    if dist is not None:
-        import torch
-        dist.barrier()
-        torch.cuda.synchronize()
-    eng.sync()
+    L.sync(eng)
     kernel_ms = []
     fast_ms = []
     reduce_ms = []
@@ -621,46 +1157,34 @@ def main():
         kernel_ms.append(tm.decode_downsample_ms)
         fast_ms.append(tm.fast_ms)
         reduce_ms.append(tm.group_reduce_ms)
-    eng.sync()
-    if dist is not None:
-        import torch
-        torch.cuda.synchronize()
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    L.sync(eng)
+    elapsed = L.max(time.perf_counter() - t0)
     tm = eng.timing()
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
     ms_per_step = elapsed * 1000.0 / args.steps
-    if dist is not None:   # datapoints of every rank's shard
-        import torch
-        t = torch.tensor([tm.datapoints], dtype=torch.int64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t)
-        dps_step = int(t.item())
-    else:
-        dps_step = tm.datapoints
+    dps_step = L.sum(int(tm.datapoints))   # datapoints of every rank's shard
     value = dps_step / (ms_per_step / 1000.0)
     # dominant kernel: the streaming kernel k_fast when the batch's row class allows it
     # (every tile handed back to k_grid otherwise); hipEvents on the engine stream
     use_fast = min(fast_ms) > 0 and tm.redo_tiles == 0
     # a reference query arrives with freshly scanned Spans (TsdbQuery.java:916-1049): "cold"
     # = the load-time row index + one step, per query
-    cold_value = dps_step / ((index_ms + ms_per_step) / 1000.0)
+    cold_value = dps_step / ((L.max(index_ms) + ms_per_step) / 1000.0)
     k_avg = sum(fast_ms if use_fast else kernel_ms) / args.steps
     kname = "k_fast" if use_fast else "k_grid"
     achieved = tm.bytes / (k_avg / 1000.0) / 1e9
+    eng.close()   # free the headline store before config 3
+    if parity is not None and L.dist is not None:
+        parity["straddle"] = launch_straddle(L)
     extra = None
-    if world == 1 and not args.no_config3:
-        eng.close()   # free the headline store before config 3's 18 GB
-        extra = {"config3": config3_block(args, local_rank)}
+    if not args.no_config3:
+        extra = {"config3": config3_block(args, L.device)} if L.dist is None else {"config3_strong": launch_config3(args, L)}
+    ok = parity_all_ok(parity, extra)
     if rank == 0:
         cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(args, args.cpu_seconds)
         traffic, traffic_note = (None, "not collected (--no-pmc or N>1)")
         if not args.no_pmc and world == 1:
             traffic, traffic_note = pmc_traffic(args, f"void tsdb::{kname}")
-            if extra is not None:   # config 3: both k_short row classes of a step
+            if extra is not None and "config3" in extra:   # config 3: both k_short row classes of a step
                 c3t, c3note = pmc_traffic(args, "void tsdb::k_short", config3=True)
                 extra["config3"]["sum"]["traffic"] = c3t
                 extra["config3"]["sum"]["traffic_detail"] = c3note
@@ -681,6 +1205,10 @@ def main():
             "cold_value": cold_value,
             "cold_note": "datapoints / (k_index at load + one step): the per-query rate when every query "
                          "brings freshly scanned cells",
+            "launch": ("one process per GPU (torch.distributed.run), partial states all-gathered over "
+                       f"{'RCCL' if L.backend == 'nccl' else L.backend}") if L.dist is not None else "one process, one GPU",
+            "parity_ok": ok,
+            "parity": parity,
             "config": {
                 "workload": workload_label(args),
                 "series_per_gpu": args.series if args.scaling == "weak" else args.series / world,
@@ -711,9 +1239,11 @@ def main():
             "extra": extra,
         }
         print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
-    eng.close()
+    if L.dist is not None:
+        L.dist.destroy_process_group()
+    if not ok:
+        print(f"bench.py rank {rank}: parity check FAILED (see the line's parity blocks)", file=sys.stderr, flush=True)
+        sys.exit(1)
 
 
 if __name__ == "__main__":

@@ -146,71 +146,123 @@ def run_distributed(eng, q: abi.Query, dist, n_groups_global: int, device=None):
     return eng.finalize(q, n_groups_global, gathered.data_ptr(), world)
 
 
+def run_distributed_multi(eng, qs, dist, n_groups_global: int, device=None):
+    """Several decomposable queries sharing the time range and downsampling (a TSQuery's
+    sub-queries over one metric, TsdbQuery.java:916-1049 once each): ONE fused pass over the
+    shard for all of them (tsdbhip_run_partials_multi), ONE all-gather of the concatenated
+    partial states, then the rank-ordered merge per query.  Returns one group list per query."""
+    import torch
+
+    world = dist.get_world_size()
+    sizes = [int(eng.partials_layout(q, n_groups_global).bytes) for q in qs]
+    if len(set(sizes)) != 1:
+        raise ValueError("run_distributed_multi: the queries must share the time range and downsampling")
+    total = sum(sizes)
+    on_gpu = dist.get_backend() == "nccl"
+    dev = device if on_gpu else "cpu"
+    mine = torch.empty(total, dtype=torch.uint8, device=dev)
+    eng.run_partials_multi(qs, n_groups_global, mine.data_ptr())
+    gathered = torch.empty(world * total, dtype=torch.uint8, device=dev)
+    dist.all_gather_into_tensor(gathered, mine)
+    per_q = gathered.view(world, len(qs), sizes[0]).transpose(0, 1).contiguous()   # [query][rank][bytes]
+    if on_gpu:
+        torch.cuda.current_stream(dev).synchronize()
+    return [eng.finalize(q, n_groups_global, per_q[i].data_ptr(), world) for i, q in enumerate(qs)]
+
+
 # ---- percentile / median as the group-by aggregator: values to the owning rank --------
 #
 # PercentileAgg / Median.runDouble need every span's value of a (group, slot) at once
 # (src/core/Aggregators.java:397-431, 657-708): there is no partial state to all-gather.
-# Group g is owned by rank g % world; every rank sends its spans' contributions of g to
-# that rank (one all-to-all over RCCL), the owner sorts and selects, and the owners' dense
-# rows are all-gathered (G x K x 9 B) so every rank can build the full result.
+# Group g is owned by the FIRST rank holding one of its spans (as the one-process multi-device
+# context does, multi.cpp): with contiguous series shards a group lives on one rank or straddles
+# a boundary, so only the straddling groups' values move.  Every rank sends its spans'
+# contributions of g to the owner (one all-to-all over RCCL), the owner sorts and selects, and
+# the owners' dense rows are all-gathered (G x K x 9 B) so every rank can build the full result.
 
-def sel_owner(n_groups: int, world: int):
-    return np.arange(n_groups) % world
+def sel_owner(counts_all):
+    """Owning rank per group from every rank's span counts ([world, G]): the first rank with a
+    span of the group (rank 0 for a group without spans)."""
+    counts_all = np.asarray(counts_all, np.int64)
+    if counts_all.ndim != 2 or counts_all.shape[1] == 0:
+        return np.zeros(counts_all.shape[-1] if counts_all.ndim else 0, np.int64)
+    has = counts_all > 0
+    return np.where(has.any(axis=0), has.argmax(axis=0), 0).astype(np.int64)
 
 
-def sel_pack(vals, counts, K: int, world: int):
-    """This rank's [span][slot] contribution buffer (spans group by group) reordered by
-    owning rank.
+def sel_pack(vals, counts, K: int, own, me: int, world: int):
+    """This rank's [span][slot] contributions (spans group by group) of the groups OTHER ranks
+    own (`own` = sel_owner(counts_all)), ordered by owning rank; the groups `me` owns stay put.
 
-    Returns (send, in_splits): `send` holds, for owner 0, 1, ..., the blocks of the groups
-    it owns in increasing group order; in_splits[o] is the element count for owner o."""
+    Returns (send, in_splits): `send` holds, for owner 0, 1, ... (never `me`), the blocks of
+    the groups it owns in increasing group order; in_splits[o] is the element count for o."""
     import torch
     counts = np.asarray(counts, np.int64)
     off = np.concatenate([[0], np.cumsum(counts * K)])
-    own = sel_owner(len(counts), world)
+    own = np.asarray(own, np.int64)
     pieces, splits = [], []
     for o in range(world):
-        gs = np.nonzero(own == o)[0]
-        splits.append(int(sum(counts[g] * K for g in gs)))
-        pieces += [vals[int(off[g]):int(off[g + 1])] for g in gs if counts[g]]
+        gs = np.nonzero((own == o) & (counts > 0))[0] if o != me else np.zeros(0, np.int64)
+        splits.append(int(counts[gs].sum() * K))
+        pieces += [vals[int(off[g]):int(off[g + 1])] for g in gs]
     send = torch.cat(pieces) if pieces else vals[:0]
     return send, splits
 
 
-def sel_unpack(recv, counts_all, K: int, me: int):
-    """The owner's side: `recv` holds, per source rank r (in rank order), r's blocks of the
-    groups `me` owns ([n_rg][K] each, increasing g).  Returns (vals, seg_counts): per owned
-    group every rank's spans one after the other ([g][j][k], j over all ranks' spans -- rank
-    order is SpanGroup order), and the per-group span counts (0 for groups owned elsewhere)."""
+def sel_recv_splits(counts_all, K: int, own, me: int):
+    """Element counts the owner `me` receives from each rank (0 from itself)."""
+    counts_all = np.asarray(counts_all, np.int64)
+    mine = np.asarray(own) == me
+    return [0 if r == me else int(counts_all[r, mine].sum() * K) for r in range(counts_all.shape[0])]
+
+
+def sel_unpack(recv, counts_all, K: int, me: int, local_vals):
+    """The owner's side.  `recv` holds, per source rank r != me (in rank order), r's blocks of
+    the groups `me` owns ([n_rg][K] each, increasing g); `local_vals` is this rank's own
+    contribution buffer (sel_run_values).  Returns (vals, seg_counts): per owned group every
+    rank's spans one after the other in rank order ([g][j][k] -- rank order is SpanGroup
+    order), and the per-group span counts (0 for groups owned elsewhere).  When nothing arrives
+    and every local group is owned here (whole groups per rank), `local_vals` is returned as is."""
     import torch
     counts_all = np.asarray(counts_all, np.int64)
     world, G = counts_all.shape
-    own = sel_owner(G, world)
+    own = sel_owner(counts_all)
     mine = np.nonzero(own == me)[0]
-    blocks = {}
+    local = counts_all[me]
+    if recv.numel() == 0 and not np.any((local > 0) & (own != me)):
+        seg = np.where(own == me, local, 0).astype(np.int64)
+        return local_vals[:int(local.sum()) * K], seg
+    loff = np.concatenate([[0], np.cumsum(local * K)])
+    blocks = {int(g): [None] * world for g in mine}
     pos = 0
     for r in range(world):
         for g in mine:
             n = int(counts_all[r, g])
-            if n:
-                blocks.setdefault(int(g), []).append(recv[pos:pos + n * K])
+            if not n:
+                continue
+            if r == me:
+                blocks[int(g)][r] = local_vals[int(loff[g]):int(loff[g + 1])]
+            else:
+                blocks[int(g)][r] = recv[pos:pos + n * K]
                 pos += n * K
     seg = np.zeros(G, np.int64)
     out = []
     for g in mine:
-        if int(g) in blocks:
-            b = torch.cat(blocks[int(g)])
+        parts = [b for b in blocks[int(g)] if b is not None]
+        if parts:
+            b = torch.cat(parts)
             seg[g] = b.numel() // K
             out.append(b)
     vals = torch.cat(out) if out else recv[:0]
     return vals, seg
 
 
-def sel_combine(rows_all, G: int, K: int, world: int):
+def sel_combine(rows_all, G: int, K: int, own):
     """Row g of the dense [G][K] outputs from its owner (rows_all: [world, G * K])."""
-    own = sel_owner(G, world)
-    r = rows_all.reshape(world, G, K)
     import torch
+    own = np.asarray(own, np.int64)
+    world = rows_all.numel() // max(1, G * K)
+    r = rows_all.reshape(world, G, K)
     idx = torch.as_tensor(own, device=r.device)
     return r[idx, torch.arange(G, device=r.device)].reshape(-1)
 
@@ -218,8 +270,8 @@ def sel_combine(rows_all, G: int, K: int, world: int):
 def run_distributed_sel(eng, q: abi.Query, dist, n_groups_global: int, device=None):
     """A percentile / median group-by query -- or a TSDB_QF_ORDERED one, whose owner folds
     the spans in rank (= SpanGroup) order -- over the sharded store:
-    local contributions -> all-to-all to the owning ranks -> sort + select on the owners ->
-    all-gather of the owners' rows -> result on every rank."""
+    local contributions -> the straddling groups' values to their owners (all-to-all) ->
+    sort + select on the owners -> all-gather of the owners' rows -> result on every rank."""
     import torch
 
     world, me = dist.get_world_size(), dist.get_rank()
@@ -231,19 +283,18 @@ def run_distributed_sel(eng, q: abi.Query, dist, n_groups_global: int, device=No
     uni = torch.empty(max(1, G * K), dtype=torch.uint8, device=dev)
     act = torch.empty(max(1, G), dtype=torch.int32, device=dev)
     eng.sel_run_values(q, G, vals.data_ptr(), uni.data_ptr(), act.data_ptr())
-    vals = vals[:int(counts.sum()) * K]
     c_mine = torch.as_tensor(counts, dtype=torch.int64, device=dev)
     c_all = torch.empty(world * G, dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(c_all, c_mine)
     counts_all = c_all.cpu().numpy().reshape(world, G)
-    send, in_splits = sel_pack(vals, counts, K, world)
-    own = sel_owner(G, world)
-    out_splits = [int(sum(counts_all[r, g] * K for g in np.nonzero(own == me)[0])) for r in range(world)]
+    own = sel_owner(counts_all)
+    send, in_splits = sel_pack(vals, counts, K, own, me, world)
+    out_splits = sel_recv_splits(counts_all, K, own, me)
     recv = torch.empty(sum(out_splits), dtype=torch.float64, device=dev)
     dist.all_to_all_single(recv, send.contiguous(), out_splits, in_splits)
     dist.all_reduce(uni, op=dist.ReduceOp.MAX)
     dist.all_reduce(act, op=dist.ReduceOp.MAX)
-    ovals, seg = sel_unpack(recv, counts_all, K, me)
+    ovals, seg = sel_unpack(recv, counts_all, K, me, vals)
     ovals = ovals.contiguous()
     ov = torch.empty(max(1, G * K), dtype=torch.float64, device=dev)
     of = torch.empty(max(1, G * K), dtype=torch.uint8, device=dev)
@@ -254,8 +305,8 @@ def run_distributed_sel(eng, q: abi.Query, dist, n_groups_global: int, device=No
     of_all = torch.empty(world * of.numel(), dtype=torch.uint8, device=dev)
     dist.all_gather_into_tensor(ov_all, ov)
     dist.all_gather_into_tensor(of_all, of)
-    val = sel_combine(ov_all, G, K, world).contiguous() if G * K else ov
-    flag = sel_combine(of_all, G, K, world).contiguous() if G * K else of
+    val = sel_combine(ov_all, G, K, own).contiguous() if G * K else ov
+    flag = sel_combine(of_all, G, K, own).contiguous() if G * K else of
     if on_gpu:
         torch.cuda.current_stream(dev).synchronize()
     return eng.assemble(q, G, val.data_ptr(), flag.data_ptr(), act.data_ptr())

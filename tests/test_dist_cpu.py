@@ -105,8 +105,9 @@ def _emulate_sel_exchange(per_rank_vals, per_rank_counts, K):
     """all-to-all of sel_pack outputs, in-process: recv[me] = concat over r of r's piece for me."""
     import torch
     world = len(per_rank_vals)
-    sends = [dist.sel_pack(per_rank_vals[r], per_rank_counts[r], K, world) for r in range(world)]
     counts_all = np.stack(per_rank_counts)
+    own = dist.sel_owner(counts_all)
+    sends = [dist.sel_pack(per_rank_vals[r], per_rank_counts[r], K, own, r, world) for r in range(world)]
     outs = []
     for me in range(world):
         pieces = []
@@ -115,29 +116,30 @@ def _emulate_sel_exchange(per_rank_vals, per_rank_counts, K):
             off = int(sum(splits[:me]))
             pieces.append(send[off:off + splits[me]])
         recv = torch.cat(pieces)
-        outs.append(dist.sel_unpack(recv, counts_all, K, me))
-    return outs
+        assert recv.numel() == sum(dist.sel_recv_splits(counts_all, K, own, me))
+        outs.append(dist.sel_unpack(recv, counts_all, K, me, per_rank_vals[me]))
+    return outs, own
 
 
-@pytest.mark.parametrize("world", [1, 2, 3, 4])
-def test_sel_pack_unpack_routes_every_value(world):
+def _rank_values(counts, K, world):
     import torch
-    rng = np.random.default_rng(world)
-    G, K = 7, 5
-    counts = [rng.integers(0, 4, G) for _ in range(world)]
     vals = []
     for r in range(world):
         v = []
-        for g in range(G):
+        for g in range(len(counts[r])):
             for i in range(counts[r][g]):
                 for k in range(K):
                     v.append(r * 1e6 + g * 1e4 + k * 1e2 + i)
         vals.append(torch.tensor(v, dtype=torch.float64))
-    outs = _emulate_sel_exchange(vals, counts, K)
+    return vals
+
+
+def _check_owned(outs, own, counts, K, world):
+    G = len(own)
     for me, (ov, seg) in enumerate(outs):
         pos = 0
         for g in range(G):
-            if g % world != me:
+            if own[g] != me:
                 assert seg[g] == 0
                 continue
             n = sum(int(counts[r][g]) for r in range(world))
@@ -149,15 +151,44 @@ def test_sel_pack_unpack_routes_every_value(world):
         assert pos == ov.numel()
 
 
+def test_sel_owner_is_first_rank_with_spans():
+    ca = np.array([[0, 2, 0, 1], [3, 1, 0, 0], [1, 0, 0, 4]])
+    np.testing.assert_array_equal(dist.sel_owner(ca), [1, 0, 0, 0])
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+def test_sel_pack_unpack_routes_every_value(world):
+    rng = np.random.default_rng(world)
+    G, K = 7, 5
+    counts = [rng.integers(0, 4, G) for _ in range(world)]
+    vals = _rank_values(counts, K, world)
+    outs, own = _emulate_sel_exchange(vals, counts, K)
+    _check_owned(outs, own, counts, K, world)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sel_whole_groups_move_nothing(world):
+    """Contiguous series shards with whole groups per rank: no value leaves its rank and each
+    owner selects over its own contribution buffer in place."""
+    G, K = 8, 3
+    counts = [np.array([3 if g * world // G == r else 0 for g in range(G)]) for r in range(world)]
+    vals = _rank_values(counts, K, world)
+    outs, own = _emulate_sel_exchange(vals, counts, K)
+    _check_owned(outs, own, counts, K, world)
+    for me, (ov, _) in enumerate(outs):
+        assert ov.data_ptr() == vals[me].data_ptr()   # no copy
+
+
 def test_sel_combine_takes_owner_rows():
     import torch
     world, G, K = 3, 5, 2
     rows = torch.zeros(world, G * K, dtype=torch.float64)
     for r in range(world):
         rows[r] = r + 10 * torch.arange(G * K)
-    got = dist.sel_combine(rows.reshape(-1), G, K, world).reshape(G, K)
+    own = np.array([2, 0, 1, 1, 0])
+    got = dist.sel_combine(rows.reshape(-1), G, K, own).reshape(G, K)
     for g in range(G):
-        np.testing.assert_array_equal(got[g].numpy(), (g % world) + 10 * np.arange(g * K, g * K + K))
+        np.testing.assert_array_equal(got[g].numpy(), own[g] + 10 * np.arange(g * K, g * K + K))
 
 
 def _sel_gloo_worker(rank, world, port, out):  # noqa: C901
@@ -177,12 +208,12 @@ def _sel_gloo_worker(rank, world, port, out):  # noqa: C901
         c_all = torch.empty(world * G, dtype=torch.int64)
         td.all_gather_into_tensor(c_all, torch.as_tensor(counts))
         counts_all = c_all.numpy().reshape(world, G)
-        send, in_splits = dist.sel_pack(vals, counts, K, world)
-        own = dist.sel_owner(G, world)
-        out_splits = [int(sum(counts_all[r, g] * K for g in np.nonzero(own == rank)[0])) for r in range(world)]
+        own = dist.sel_owner(counts_all)
+        send, in_splits = dist.sel_pack(vals, counts, K, own, rank, world)
+        out_splits = dist.sel_recv_splits(counts_all, K, own, rank)
         recv = torch.empty(sum(out_splits), dtype=torch.float64)
         td.all_to_all_single(recv, send.contiguous(), out_splits, in_splits)
-        ov, seg = dist.sel_unpack(recv, counts_all, K, rank)
+        ov, seg = dist.sel_unpack(recv, counts_all, K, rank, vals)
         np.savez(os.path.join(out, f"s{rank}.npz"), ov=ov.numpy(), seg=seg, counts_all=counts_all)
     finally:
         td.destroy_process_group()
@@ -195,9 +226,10 @@ def test_sel_exchange_gloo(tmp_path, world):
     for me in range(world):
         z = np.load(tmp_path / f"s{me}.npz")
         ca = z["counts_all"]
+        own = dist.sel_owner(ca)
         want = []
         for g in range(G):
-            if g % world != me:
+            if own[g] != me:
                 continue
             want += [r * 1e6 + g * 1e4 + k * 1e2 + i for r in range(world) for i in range(ca[r, g]) for k in range(K)]
         np.testing.assert_array_equal(z["ov"], want)

@@ -115,12 +115,29 @@ def _worker(rank, world, port, out):
         eng.load(dist.shard_batch(b, rank, world))
         q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
         groups = dist.run_distributed(eng, q, td, dist.n_groups_of(b))
-        np.savez(os.path.join(out, f"r{rank}.npz"), gid=np.array([g[0] for g in groups]),
-                 n=np.array([len(g[1]) for g in groups]), ts=np.concatenate([g[1] for g in groups]),
-                 bits=np.concatenate([g[2] for g in groups]), isi=np.concatenate([g[3] for g in groups]))
+        _save(os.path.join(out, f"r{rank}.npz"), groups)
+        qs = [abi.new_query(T0, T0 + 3599, a, ds_function=abi.AGG["avg"], ds_interval_ms=60000) for a in MULTI]
+        for a, gs in zip(MULTI, dist.run_distributed_multi(eng, qs, td, dist.n_groups_of(b))):
+            _save(os.path.join(out, f"r{rank}_{a}.npz"), gs)
     finally:
         eng.close()
         td.destroy_process_group()
+
+
+MULTI = ["avg", "min", "max", "count", "dev"]
+
+
+def _save(path, groups):
+    np.savez(path, gid=np.array([g[0] for g in groups]), n=np.array([len(g[1]) for g in groups]),
+             ts=np.concatenate([g[1] for g in groups]), bits=np.concatenate([g[2] for g in groups]),
+             isi=np.concatenate([g[3] for g in groups]))
+
+
+def _load(path):
+    z = np.load(path)
+    cut = np.concatenate([[0], np.cumsum(z["n"])])
+    return [(int(z["gid"][i]), z["ts"][cut[i]:cut[i + 1]], z["bits"][cut[i]:cut[i + 1]], z["isi"][cut[i]:cut[i + 1]])
+            for i in range(len(z["gid"]))]
 
 
 def test_two_process_gloo(tmp_path, batch):
@@ -132,11 +149,11 @@ def test_two_process_gloo(tmp_path, batch):
     q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
     want = O.run_query(batch, q)
     for r in range(2):
-        z = np.load(tmp_path / f"r{r}.npz")
-        cut = np.concatenate([[0], np.cumsum(z["n"])])
-        got = [(int(z["gid"][i]), z["ts"][cut[i]:cut[i + 1]], z["bits"][cut[i]:cut[i + 1]], z["isi"][cut[i]:cut[i + 1]])
-               for i in range(len(z["gid"]))]
-        assert_groups_match(got, want, "sum", ctx=f"gloo rank {r}")
+        assert_groups_match(_load(tmp_path / f"r{r}.npz"), want, "sum", ctx=f"gloo rank {r}")
+        # run_distributed_multi: one fused pass + one all-gather for the five queries
+        for a in MULTI:
+            qa = abi.new_query(T0, T0 + 3599, a, ds_function=abi.AGG["avg"], ds_interval_ms=60000)
+            assert_groups_match(_load(tmp_path / f"r{r}_{a}.npz"), O.run_query(batch, qa), a, ctx=f"gloo multi {a} rank {r}")
 
 
 # ---- percentile / median group-by: values to the owning rank ----------
@@ -160,8 +177,9 @@ def run_sharded_sel(engines, b, q, world):
         acts.append(a)
     uni = np.maximum.reduce(unis)
     act = np.maximum.reduce(acts)
-    sends = [dist.sel_pack(vals[r], counts[r], K, world) for r in range(world)]
     counts_all = np.stack(counts)
+    own = dist.sel_owner(counts_all)
+    sends = [dist.sel_pack(vals[r], counts[r], K, own, r, world) for r in range(world)]
     rows_v, rows_f = [], []
     for me in range(world):
         pieces = []
@@ -169,15 +187,15 @@ def run_sharded_sel(engines, b, q, world):
             send, splits = sends[r]
             off = int(sum(splits[:me]))
             pieces.append(send[off:off + splits[me]])
-        ov, seg = dist.sel_unpack(torch.cat(pieces), counts_all, K, me)
+        ov, seg = dist.sel_unpack(torch.cat(pieces), counts_all, K, me, vals[me])
         ov = np.ascontiguousarray(ov.numpy())
         out_v = np.zeros(max(1, G * K))
         out_f = np.zeros(max(1, G * K), np.uint8)
         engines[me].sel_select(q, G, ov.ctypes.data, seg, uni.ctypes.data, out_v.ctypes.data, out_f.ctypes.data)
         rows_v.append(out_v)
         rows_f.append(out_f)
-    val = np.ascontiguousarray(dist.sel_combine(torch.from_numpy(np.stack(rows_v)), G, K, world).numpy())
-    flag = np.ascontiguousarray(dist.sel_combine(torch.from_numpy(np.stack(rows_f)), G, K, world).numpy())
+    val = np.ascontiguousarray(dist.sel_combine(torch.from_numpy(np.stack(rows_v)).reshape(-1), G, K, own).numpy())
+    flag = np.ascontiguousarray(dist.sel_combine(torch.from_numpy(np.stack(rows_f)).reshape(-1), G, K, own).numpy())
     return engines[0].assemble(q, G, val.ctypes.data, flag.ctypes.data, act.ctypes.data)
 
 
