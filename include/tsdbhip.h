@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define TSDBHIP_ABI_VERSION 11
+#define TSDBHIP_ABI_VERSION 12
 
 /* ---- error codes: one per Java exception on the path --------------------- */
 enum {
@@ -135,11 +135,13 @@ typedef struct {
  * default).  UTC intervals whose grid is one global sequence -- ms (1000 % n == 0), s / m
  * (60 % n == 0), h (24 % n == 0), d (n == 1), w (n == 1, weeks from Sunday) -- run on a fixed
  * grid, n months (12 % n == 0) and 1 year on a slot boundary table.  Everything else (a time
- * zone, or an interval anchored per span: 7sc, 2dc, 5nc, 2wc, 2yc ...) runs on the union of
- * the spans' boundary sequences, each anchored at previousInterval(the span's first datapoint
- * after the seek); spans whose sequences disagree (their union of timestamps is not one grid),
- * week intervals of more than 2 weeks, and percentile / median downsampling over a boundary
- * table return TSDB_E_NOT_IMPLEMENTED. */
+ * zone, or an interval anchored per span: 7sc, 2dc, 5nc, 2wc, 3wc, 2yc ...) runs on the union
+ * of the spans' boundary sequences, each anchored at previousInterval(the span's first
+ * datapoint after the seek).  Spans whose sequences disagree run per anchor and aggregate over
+ * the union of their timestamps; percentile / median downsampling runs over boundary tables as
+ * well.  Refused (TSDB_E_NOT_IMPLEMENTED): the per-rank exchange entry points
+ * (tsdbhip_run_partials / tsdbhip_sel_*) when the anchored grids disagree across ranks -- shard
+ * such queries by group. */
 enum {
   TSDB_CAL_NONE = 0, TSDB_CAL_MS, TSDB_CAL_S, TSDB_CAL_M, TSDB_CAL_H, TSDB_CAL_D, TSDB_CAL_W, TSDB_CAL_N, TSDB_CAL_Y
 };
@@ -189,6 +191,18 @@ typedef struct {
 /* ---- library-level helpers (host logic of the reference, restated) ------- */
 int tsdbhip_abi_version(void);
 const char* tsdbhip_last_error(void);
+/* Developer options (no reference counterpart): kernel-choice switches that the parity tests
+ * use to force an alternative kernel onto the same data (the general kernel, a sequential path,
+ * small compaction chunks, ...), by name without a prefix: FAST, SHORT, ROWS, HWIN, SEQ,
+ * SEQ_ROWS, SEQ_WAVE, INDEX_GENERIC, CMP_CHUNK, CMP_ROWS, CMP_ONEPASS, PCT_ROWS, PCT_KEYS,
+ * PCT_VONLY, PCT_V6, SEL_FUSED, SEL_COLS, SEL_WIN, SEL_WAVE, SEL_REG, SELOPS, RAW_LERPW,
+ * RAW_SEL_TOP, RAW_SEL_REG, RO_FUSE, MULTI_FUSE, HIST_WINDOW, HIST_WS, HIST_LAYOUT, TRACE, DBG
+ * (opentsdb_amd/csrc/opts.h says what each value does).  Process-wide; -1 resets an option to
+ * its production choice, which is every option's initial state.  The library reads no
+ * environment variable: an inherited environment cannot change its kernels.  DBG is honoured
+ * only by a -DTSDBHIP_KDBG profiling build.  Unknown names -> TSDB_E_ILLEGAL_ARGUMENT. */
+int tsdbhip_set_option(const char* name, int64_t value);
+int tsdbhip_get_option(const char* name, int64_t* value);
 /* Aggregators.get(name) (src/core/Aggregators.java:222-228); returns id or TSDB_E_NO_SUCH_ELEMENT */
 int tsdbhip_aggregator_get(const char* name);
 /* Aggregator.interpolationMethod() */

@@ -5,6 +5,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cctype>
 #include <cmath>
 #include <cstdio>
@@ -598,6 +599,41 @@ int64_t cal_unit_ms(int unit) { return unit >= 0 && unit < 9 ? CAL_UNIT_MS[unit]
 // ===========================================================================
 extern "C" int tsdbhip_abi_version(void) { return TSDBHIP_ABI_VERSION; }
 
+// ---- developer options (opts.h): set through the C ABI only, never from the environment ----
+namespace tsdb {
+namespace {
+// stored as value + 1 so that the zero-initialised table means "every option unset"
+std::atomic<int64_t> g_opts[OPT_COUNT];
+const char* const kOptNames[OPT_COUNT] = {
+    "FAST", "SHORT", "ROWS", "HWIN", "SEQ", "SEQ_ROWS", "SEQ_WAVE", "INDEX_GENERIC", "CMP_CHUNK", "CMP_ROWS",
+    "CMP_ONEPASS", "PCT_ROWS", "PCT_KEYS", "PCT_VONLY", "PCT_V6", "SEL_FUSED", "SEL_COLS", "SEL_WIN", "SEL_WAVE",
+    "SEL_REG", "SELOPS", "RAW_LERPW", "RAW_SEL_TOP", "RAW_SEL_REG", "RO_FUSE", "MULTI_FUSE", "HIST_WINDOW",
+    "HIST_WS", "HIST_LAYOUT", "TRACE", "DBG"};
+int opt_index(const char* name) {
+  if (!name) return -1;
+  for (int i = 0; i < OPT_COUNT; i++)
+    if (std::strcmp(name, kOptNames[i]) == 0) return i;
+  return -1;
+}
+}  // namespace
+int64_t opt(Opt o) { return g_opts[o].load(std::memory_order_relaxed) - 1; }
+}  // namespace tsdb
+
+extern "C" int tsdbhip_set_option(const char* name, int64_t value) {
+  const int i = tsdb::opt_index(name);
+  if (i < 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, std::string("unknown option: ") + (name ? name : "(null)"));
+  if (value < -1) return fail(TSDB_E_ILLEGAL_ARGUMENT, "option values are >= 0 (-1 resets)");
+  tsdb::g_opts[i].store(value + 1, std::memory_order_relaxed);
+  return 0;
+}
+
+extern "C" int tsdbhip_get_option(const char* name, int64_t* value) {
+  const int i = tsdb::opt_index(name);
+  if (i < 0 || !value) return fail(TSDB_E_ILLEGAL_ARGUMENT, std::string("unknown option: ") + (name ? name : "(null)"));
+  *value = tsdb::opt((tsdb::Opt)i);
+  return 0;
+}
+
 namespace tsdb {
 hipError_t h2d(tsdbhip_ctx* c, void* dst, const void* src, size_t n, hipStream_t st);   // (defined at the end)
 }  // namespace tsdb
@@ -839,8 +875,6 @@ static int build_tiles(tsdbhip_ctx* c) {
   // 3.79 vs 3.82 ms but k_reduce 0.13 vs 0.04 ms over 4x the partials -- a slower step
   // (profiles/r04e), so the default stays at 8192.
   int64_t min_tiles = 8192, tile_dp = 40000;
-  if (const char* e = std::getenv("TSDBHIP_TILE_MIN")) min_tiles = std::max<int64_t>(1, std::atoll(e));
-  if (const char* e = std::getenv("TSDBHIP_TILE_DP")) tile_dp = std::max<int64_t>(1, std::atoll(e));
   int64_t dps = 0;
   for (int64_t r = 0; r < c->n_rows; r++) dps += c->h_ndp[r];
   const double dp_per_series = n ? (double)dps / (double)n : 0.0;
@@ -939,8 +973,7 @@ static int build_none_tiles(tsdbhip_ctx* c) {
 static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
   // classify rows on the device, then fetch ndp for host-side accounting
   HIP_OK(hipMemsetAsync(c->err.p, 0, 4, c->stream));
-  const char* genv = std::getenv("TSDBHIP_INDEX_GENERIC");   // test hook: sequential per-datapoint path
-  const bool generic = genv && genv[0] == '1';
+  const bool generic = opt_is(OPT_INDEX_GENERIC, 1);   // test hook: sequential per-datapoint path
   HIP_OK(c->hint.ensure(std::max<int64_t>(1, c->n_rows)));
   HIP_OK(c->ilist.ensure(std::max<int64_t>(1, c->n_rows) * 4));
   HIP_OK(c->icnt.ensure(32 * 4));
@@ -1596,7 +1629,7 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   // host lays the batch out, and the second pass recomputes each chunk's entries and writes them.
   const int64_t kLim = ((int64_t)1 << 31) - 1;
   int64_t limit = kLim;
-  if (const char* e = std::getenv("TSDBHIP_CMP_CHUNK")) limit = std::max<int64_t>(1, std::atoll(e));   // tests: force chunks
+  if (opt(OPT_CMP_CHUNK) > 0) limit = opt(OPT_CMP_CHUNK);   // tests: force chunks
   std::vector<int64_t> cuts{0};
   {
     int64_t w = 0;
@@ -1620,8 +1653,8 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
     cuts.push_back(NR);
   }
   const int n_chunks = (int)cuts.size() - 1;
-  // TSDBHIP_TRACE=1: host wall time of the call's phases on stderr (diagnostics only)
-  const bool trace = std::getenv("TSDBHIP_TRACE") != nullptr;
+  // option TRACE = 1: host wall time of the call's phases on stderr (diagnostics only)
+  const bool trace = opt_is(OPT_TRACE, 1);
   auto t_last = std::chrono::steady_clock::now();
   auto mark = [&](const char* what) {
     if (!trace) return;
@@ -1658,10 +1691,9 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   HIP_OK(d_bad.ensure(4));
   HIP_OK(d_rmax.ensure(16));
   // the per-row LDS path (k_cmp_row) when every row of a chunk fits one block; else the global
-  // sort (TSDBHIP_CMP_ROWS=0 forces the latter)
-  const char* rows_env = std::getenv("TSDBHIP_CMP_ROWS");
+  // sort (option CMP_ROWS = 0 forces the latter)
   // (dtcsMergeDataPoints, a non-default configuration, is restated in k_cmp_dedup only)
-  const bool rows_ok = !(rows_env && rows_env[0] == '0') && !p.dtcs;
+  const bool rows_ok = !opt_off(OPT_CMP_ROWS) && !p.dtcs;
   std::vector<int> row_cap(n_chunks, 0);
   std::vector<uint32_t> row_span(n_chunks, 0);
   // upload, analyze and build the entries of chunk k; its rows' sizes and states to the host
@@ -1976,8 +2008,7 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   };
   int op = 1;
   {
-    const char* op_env = std::getenv("TSDBHIP_CMP_ONEPASS");
-    if (n_chunks == 1 && rows_ok && !(op_env && op_env[0] == '0')) {
+    if (n_chunks == 1 && rows_ok && !opt_off(OPT_CMP_ONEPASS)) {
       op = onepass();
       if (op < 0) return op;
     }
@@ -2228,10 +2259,9 @@ static int synth_impl(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp, int64_t p0, 
   c->n_rows = S * R;
   c->n_groups = G;
   // qualifier offsets (identical layout for every series)
-  // row starts 16-byte aligned (TSDBHIP_ROW_ALIGN: another power of two >= 16, layout experiments)
-  int64_t ra = 16;
-  if (const char* e = std::getenv("TSDBHIP_ROW_ALIGN")) ra = std::max<int64_t>(16, std::atoll(e));
-  auto alignr = [ra](int64_t x) { return (x + ra - 1) / ra * ra; };
+  // row starts 16-byte aligned (a 128-B alignment moved k_hwin by 1 % and slowed k_rows / k_short by 3 %,
+  // profiles/r05d)
+  auto alignr = [](int64_t x) { return (x + 15) / 16 * 16; };
   std::vector<int64_t> rq(R);
   int64_t QS = 0;
   for (int64_t h = 0; h < R; h++) { rq[h] = QS; QS += alignr((int64_t)rn[h] * qw); }
@@ -2871,8 +2901,7 @@ bool fast_path_ok(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P) {
         (fast_supported(P.f, c->fast_qw, c->fast_vl) || (c->fast_qw2 && fast_supported(P.f, c->fast_qw2, c->fast_vl2))) &&
         P.I <= (1LL << 29) && fast_lds_of(q, P) <= 32 * 1024 && P.K > 0))
     return false;
-  const char* env = std::getenv("TSDBHIP_FAST");
-  return !(env && env[0] == '0');
+  return !opt_off(OPT_FAST);
 }
 
 // The series of every row, on the device (k_seq_rows), once per resident batch.
@@ -2904,7 +2933,7 @@ int64_t grouped_prefix(tsdbhip_ctx* c) {
 // that row's datapoints; the kernel checks the rows), over rows short enough that one thread a
 // row beats k_seq_wave's wave a series (fewer than 64 datapoints a row on average).
 bool seq_rows_ok(tsdbhip_ctx* c, const Plan& P) {
-  if (const char* e = std::getenv("TSDBHIP_SEQ_ROWS")) if (e[0] == '0') return false;
+  if (opt_off(OPT_SEQ_ROWS)) return false;
   return P.mode == MODE_GRID && P.I > 0 && 3600000 % P.I == 0 && P.B0 % P.I == 0 && P.K > 0 && !c->seqd_uniform &&
          c->n_rows < ((int64_t)1 << 31);
 }
@@ -2918,9 +2947,8 @@ bool seq_rows_ok(tsdbhip_ctx* c, const Plan& P) {
 // hour (every hour row in one window of W = 1 h / interval <= 64 slots), no rate, an order-free
 // function, and every tile of one streaming class with one-chunk rows.
 int hwin_slots(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, bool for_multi = false) {
-  const char* he = std::getenv("TSDBHIP_HWIN");   // 0: never; 2: wherever it applies (A/B)
-  if (he && he[0] == '0') return 0;
-  if (he && he[0] == '2') for_multi = true;
+  if (opt_off(OPT_HWIN)) return 0;   // option HWIN: 0 never; 2 wherever it applies (A/B)
+  if (opt_is(OPT_HWIN, 2)) for_multi = true;
   // (fill policies need every participating series' fill values in windows where it has no row:
   // left to the dense split)
   if (P.mode != MODE_GRID || q->rate || q->ds_fill != TSDB_FILL_NONE || P.K <= 64 || P.I <= 0 || 3600000 % P.I != 0 || 3600000 / P.I > 64 ||
@@ -2933,8 +2961,7 @@ int hwin_slots(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, bool for_m
     const int qw = cls ? c->fast_qw2 : c->fast_qw, vl = cls ? c->fast_vl2 : c->fast_vl;
     if (!qw || !fast_supported(P.f, qw, vl)) return 0;
   }
-  const char* env = std::getenv("TSDBHIP_FAST");
-  if (env && env[0] == '0') return 0;
+  if (opt_off(OPT_FAST)) return 0;
   // Every K > 64 that tiles the hour, since k_hwin runs a work item a (tile, window): 12 h of 1m
   // buckets (K = 720, whose slots fit the fused kernels' LDS) 50.6 ms through k_rows vs 11.4 ms
   // here, 10m buckets of a day (K = 144) 11.8 vs 11.3 ms (profiles/r05j/).  (Before the per-window
@@ -2949,7 +2976,6 @@ bool dense_split_wanted(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P) {
   if (P.dense_out || P.emit_only || P.values_only || P.sel_direct || P.multi || P.seq_dense || P.raw || P.anchored ||
       P.f == F_SEL || P.mode != MODE_GRID || P.K <= 64)
     return false;
-  if (const char* e = std::getenv("TSDBHIP_DENSE_SPLIT")) if (e[0] == '0') return false;
   if (fast_wave_lds(P.K, q->rate != 0, true) <= 32 * 1024) return false;   // the fused pass fits
   Plan Pd = P;
   Pd.dense_out = true;
@@ -3044,7 +3070,9 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     gp.mp = MultiPartials{c->m_sum.as<double>(), c->m_mn.as<double>(), c->m_mx.as<double>(), c->m_mean.as<double>(),
                           c->m_m2.as<double>(), c->m_nl.as<uint32_t>(), c->m_nz.as<uint32_t>(), c->m_f.as<uint32_t>()};
   }
-  if (const char* dbg = std::getenv("TSDBHIP_DBG")) gp.dbg = std::atoi(dbg);
+#ifdef TSDBHIP_KDBG
+  if (opt(OPT_DBG) > 0) gp.dbg = (int32_t)opt(OPT_DBG);   // profiling build only
+#endif
   if (P.sel_direct) {   // buffers prepared by sel_values
     gp.sel_direct = 1;
     if (P.sel_win) {   // (sel_window)
@@ -3096,8 +3124,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
         rp.redo_mark = c->sr_mark.as<uint32_t>();
         rp.ro_partner = c->ro_partner.as<int32_t>();
         const int avg = P.ro_fuse == 1 ? 1 : 0;
-        const char* pe = std::getenv("TSDBHIP_RO_PACK");   // A/B: 0 = k_seq_rows_ro over the rows
-        if (c->ro_npairs > 0 && !(pe && pe[0] == '0')) {
+        if (c->ro_npairs > 0) {
           rp.ro_pairs = c->ro_pairs.as<RoPair>();
           HIP_OK(launch_ro_pairs(rp, avg, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->ro_cmap.as<int64_t>(),
                                  c->ro_npairs, c->stream));
@@ -3128,8 +3155,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
         rp.redo_list = c->sr_list.as<int32_t>();
         rp.redo_n = c->sr_n.as<int32_t>();
         rp.redo_mark = c->sr_mark.as<uint32_t>();
-        const char* pe = std::getenv("TSDBHIP_RO_PACK");   // A/B: 0 = k_seq_rows over the rows
-        if (c->ro_active && c->ro_npairs > 0 && !P.none && !(pe && pe[0] == '0')) {
+        if (c->ro_active && c->ro_npairs > 0 && !P.none) {
           rp.ro_pairs = c->ro_pairs.as<RoPair>();   // a rollup batch's value rows, packed (k_ro_rows)
           HIP_OK(launch_ro_rows(rp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->ro_npairs, c->stream));
         } else {
@@ -3173,12 +3199,10 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     // and up); 1 h buckets of 4-byte values go through its 32-bit key kernel, which ranks any
     // statistic (median, p50, p75 by a bitwise search).
     const int sel_i = (q->ds_function - TSDB_AGG_P999) % 6;
-    const char* renv = std::getenv("TSDBHIP_PCTROWS");
-    const char* kenv = std::getenv("TSDBHIP_PCT_KEYS");
     const bool near_end = q->ds_function != TSDB_AGG_MEDIAN && sel_i <= 3;
-    const bool keys = c->pct_vl == 4 && P.I == 3600000 && !(kenv && kenv[0] == '0');
+    const bool keys = c->pct_vl == 4 && P.I == 3600000 && !opt_off(OPT_PCT_KEYS);
     const bool rows_path = P.mode == MODE_GRID && (near_end || keys) && P.I > 0 && 3600000 % P.I == 0 &&
-                           P.B0 % P.I == 0 && pct_rows_supported(c->pct_qw, c->pct_vl) && !(renv && renv[0] == '0');
+                           P.B0 % P.I == 0 && pct_rows_supported(c->pct_qw, c->pct_vl) && !opt_off(OPT_PCT_ROWS);
     if (rows_path) {
       HIP_OK(c->redo2.ensure(std::max<int64_t>(1, c->n_series) * 4));
       HIP_OK(c->redo2_n.ensure(16));
@@ -3186,10 +3210,8 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       GridParams rp = gp;
       rp.redo_list = c->redo2.as<int32_t>();
       rp.redo_n = c->redo2_n.as<int32_t>();
-      const char* venv = std::getenv("TSDBHIP_PCT_VONLY");
-      rp.pct_vonly = keys && c->pct_vonly && !(venv && venv[0] == '0');
-      const char* v6env = std::getenv("TSDBHIP_PCT_V6");
-      rp.pct_v6 = rp.pct_vonly && c->pct_v6 && !(v6env && v6env[0] == '0');
+      rp.pct_vonly = keys && c->pct_vonly && !opt_off(OPT_PCT_VONLY);
+      rp.pct_v6 = rp.pct_vonly && c->pct_v6 && !opt_off(OPT_PCT_V6);
       HIP_OK(launch_pct_rows(rp, c->pct_qw, c->pct_vl, c->stream));
       int32_t nback = 0;
       { int rc_ = d2h_small(c, &nback, c->redo2_n.p, 4, c->stream); if (rc_) return rc_; }
@@ -3233,10 +3255,8 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     // over what k_fast handed back and over the tiles of neither class.  Lists by class are
     // built at load (no per-tile appends for class mismatches); only tiles that break a
     // premise at run time are appended.
-    const char* senv = std::getenv("TSDBHIP_SHORT");
-    const bool use_short = !(senv && senv[0] == '0');
-    const char* renv = std::getenv("TSDBHIP_ROWS");
-    const bool use_rows = !(renv && renv[0] == '0');
+    const bool use_short = !opt_off(OPT_SHORT);
+    const bool use_rows = !opt_off(OPT_ROWS);
     const int32_t* dl = c->tl_dev_override ? c->tl_dev_override : c->d_tl.as<int32_t>();
     const int32_t* dn = c->tln_dev_override ? c->tln_dev_override : c->d_tl_n.as<int32_t>();
     HIP_OK(c->r1a.ensure(std::max<int64_t>(1, nt) * 4));
@@ -3257,8 +3277,7 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       fp.In = (int32_t)(fp.unit_s ? P.I / 1000 : P.I);
       fp.B0n = fp.unit_s ? P.B0 / 1000 : P.B0;
       fp.rcpn = std::nextafter(1.0 / (double)fp.In, INFINITY);
-      const char* oenv = std::getenv("TSDBHIP_ONEB");
-      fp.oneb = P.I >= 3600000 && !(oenv && oenv[0] == '0') ? 1 : 0;   // (an hour row's chunk in one bucket)
+      fp.oneb = P.I >= 3600000 ? 1 : 0;   // (an hour row's chunk in one bucket)
       fp.wave_lds = (int32_t)(shortk == 3 ? fast_wave_lds(hwin, false, false) : fast_lds_of(q, P));
       fp.win_w = hwin;
       if (shortk == 3) fp.redo_mark = c->hw_mark.as<uint32_t>();
@@ -3268,19 +3287,14 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
         // -> 12.6 (4) -> 12.2 (6) -> 11.9 (12) -> 11.4 ms (24) on config 3's day shard
         // (profiles/r05h/split*.jsonl).  TSDBHIP_HWIN_SPLIT: items a tile.
         const int nw = (int)((K + hwin - 1) / hwin);
-        const char* se = std::getenv("TSDBHIP_HWIN_SPLIT");
-        fp.win_split = se ? std::max(1, std::min(nw, std::atoi(se))) : nw;
+        fp.win_split = nw;
       }
-      {
-        const char* e6 = std::getenv("TSDBHIP_SHORT6");
-        fp.short6 = ((shortk == 1 || shortk == 3) && !(e6 && e6[0] == '0')) ? 1 : 0;
-      }
+      fp.short6 = (shortk == 1 || shortk == 3) ? 1 : 0;
       if (shortk == 1 && fp.sel_direct && fp.sel_win) {   // k_short KR 5's stage of kept values
         fp.win_stage = fp.wave_lds;
         fp.wave_lds += (int32_t)align16(64 * WIN_LDS * 8);
       }
-      const char* sge = std::getenv("TSDBHIP_SEL_STAGE");   // A/B: 0 = each series' column values stored directly
-      if (shortk == 1 && fp.sel_direct && fp.sel_cols && !fp.sel_win && K <= 64 && !(sge && sge[0] == '0')) {   // k_short's column stage
+      if (shortk == 1 && fp.sel_direct && fp.sel_cols && !fp.sel_win && K <= 64) {   // k_short's column stage
         fp.sel_stage = fp.wave_lds;
         fp.wave_lds += (int32_t)align16(2 * 8 * K * 8);   // two stages of 8 series (k_short KR 4)
 
@@ -3738,8 +3752,7 @@ const std::vector<int64_t>& local_counts(tsdbhip_ctx* c, int64_t G) {
 int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bool* cols_out = nullptr) {
   const int64_t S = c->n_series, K = P.K;
   if (S * K > 0x7FFFFFFFLL) return fail(TSDB_E_NOT_IMPLEMENTED, "percentile group-by over more than 2^31 (series, slot) values");
-  const char* fenv = std::getenv("TSDBHIP_SEL_FUSED");
-  if (P.f != F_SEL && !P.emit_only && !q->rate && K >= 1 && K <= 64 && !(fenv && fenv[0] == '0')) {
+  if (P.f != F_SEL && !P.emit_only && !q->rate && K >= 1 && K <= 64 && !opt_off(OPT_SEL_FUSED)) {
     const std::vector<int64_t> gsp = seg_ptr(local_counts(c, G));
     HIP_OK(c->sel_gsp.ensure((G + 1) * 8));
     HIP_OK(c->sel_vals.ensure(std::max<int64_t>(1, S * K) * 8));
@@ -3755,8 +3768,7 @@ int sel_values(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
     if (rc) return rc;
     P2.sel_direct = true;
     // the caller that selects right here takes contiguous (group, slot) columns
-    const char* cenv = std::getenv("TSDBHIP_SEL_COLS");
-    P2.sel_cols = cols_out != nullptr && !(cenv && cenv[0] == '0');
+    P2.sel_cols = cols_out != nullptr && !opt_off(OPT_SEL_COLS);
     rc = run_device(c, q, P2, G, false);   // sets c->gact like the group-by pass
     if (rc) return rc;
     HIP_OK(launch_fill_rows(c->sel_vals.as<uint64_t>(), c->sel_wr.as<uint8_t>(), S, K, 0x7FF87FF87FF87FF8ULL, c->stream,
@@ -3894,13 +3906,12 @@ double pct_quantile_host(int fn) {
 
 int sel_window(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, bool* done) {
   *done = false;
-  const char* wenv = std::getenv("TSDBHIP_SEL_WIN");   // 0: never; 2: also for small groups (tests)
-  if (wenv && wenv[0] == '0') return 0;
+  if (opt_off(OPT_SEL_WIN)) return 0;   // option SEL_WIN: 0 never; 2 also for small groups (tests)
   const int64_t S = c->n_series, K = P.K;
   if (P.f == F_SEL || P.emit_only || q->rate || K < 1 || K > 64 || P.none || !P.gsel || G < 1) return 0;
   // ranks near the ends only (p90 and up): a window around the median keeps ~a quarter of the
   // values and measured slower than the full path (config 3 median:1m-avg 8.85 vs 7.24 ms)
-  if (!(P.gsel != TSDB_AGG_MEDIAN && pct_quantile_host(P.gsel) >= 90.0) && !(wenv && wenv[0] == '2')) return 0;
+  if (!(P.gsel != TSDB_AGG_MEDIAN && pct_quantile_host(P.gsel) >= 90.0) && !opt_is(OPT_SEL_WIN, 2)) return 0;
   if (!c->tl_other.empty()) return 0;
   int64_t nshort = 0;
   for (int cls = 0; cls < 2; cls++) {
@@ -3911,7 +3922,7 @@ int sel_window(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
   const std::vector<int64_t> counts = local_counts(c, G);
   int64_t maxn = 0;
   for (int64_t g = 0; g < G; g++) maxn = std::max(maxn, counts[g]);
-  if (maxn < 4096 && !(wenv && wenv[0] == '2')) return 0;   // small groups: the full path is cheap
+  if (maxn < 4096 && !opt_is(OPT_SEL_WIN, 2)) return 0;   // small groups: the full path is cheap
   Plan P2;
   int rc = plan_query(c, q, P2);
   if (rc) return rc;
@@ -3930,7 +3941,7 @@ int sel_window(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
       const double ng = (double)counts[g];
       const double ns = std::min<double>(WIN_SCAP, std::max<double>(640.0, ng / 16.0));
       if (ng >= 64 && ng * 2.0 * (6.0 * std::sqrt(ns * f * (1.0 - f)) + 2.0) / ns > 0.7 * WIN_CCAP &&
-          !(wenv && wenv[0] == '2'))
+          !opt_is(OPT_SEL_WIN, 2))
         return 0;
     }
   }
@@ -4130,7 +4141,7 @@ struct PhaseTrace {
   bool on;
   const char* name;
   std::chrono::steady_clock::time_point t0, last;
-  explicit PhaseTrace(const char* n) : on(std::getenv("TSDBHIP_TRACE") != nullptr), name(n) {
+  explicit PhaseTrace(const char* n) : on(opt_is(OPT_TRACE, 1)), name(n) {
     t0 = last = std::chrono::steady_clock::now();
   }
   void mark(const char* what) {
@@ -4322,10 +4333,7 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
   if (!rp.do_long && !rp.do_double) rp.do_double = 1;
   rp.err = c->err.as<int32_t>();
   rp.uns = uns ? 1 : 0;
-  {
-    const char* e = std::getenv("TSDBHIP_RAW_LERPW");
-    rp.lerp_fast = !(e && e[0] == '0');
-  }
+  rp.lerp_fast = !opt_off(OPT_RAW_LERPW);
   if (uns) {
     HIP_OK(c->r_mts.ensure(std::max<int64_t>(1, np) * 8));
     HIP_OK(c->r_mpos.ensure(std::max<int64_t>(1, S) * 4));
@@ -4451,8 +4459,7 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
     // top keys as it evaluates it -- no operand arrays
     int top_t = 0;
     if (P.gsel) {
-      const char* e = std::getenv("TSDBHIP_RAW_TOP");   // A/B: 0 = operand arrays + selection
-      if (!(e && e[0] == '0')) {
+      {
         int64_t k_all = 1;
         for (int64_t g = g0; g < g1; g++) k_all = std::max<int64_t>(k_all, grp_ser[g + 1] - grp_ser[g]);
         const int need = raw_top_need(P.gsel, k_all, 32);
@@ -4473,7 +4480,7 @@ int run_raw(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, tsdbhip_resul
       // percentile / median: every span operand of every union point, strip by strip
       // (RAW_STRIP points x the group's spans each), in batches of at most kSelOps operands
       int64_t kSelOps = (int64_t)1 << 28;
-      if (const char* e = std::getenv("TSDBHIP_SELOPS")) kSelOps = std::max<int64_t>(1, std::atoll(e));   // tests: force batches
+      if (opt(OPT_SELOPS) > 0) kSelOps = opt(OPT_SELOPS);   // tests: force batches
       std::vector<int64_t> soff(ns + 1, 0);
       for (int64_t t = 0; t < ns; t++) soff[t + 1] = soff[t] + (grp_ser[g0 + sg[t] + 1] - grp_ser[g0 + sg[t]]) * RAW_STRIP;
       // batches [bat[i], bat[i + 1]) of strips: at least one strip each, else <= kSelOps operands
@@ -4915,8 +4922,7 @@ int ro_stage(tsdbhip_ctx* c, const tsdbhip_query* q, const tsdbhip_query& qr, Pl
     P1.seq_dense = true;
     P1.values_only = true;
     // value rows with their lock-step count rows in one pass (k_seq_rows_ro), combined in place
-    const char* fenv = std::getenv("TSDBHIP_RO_FUSE");
-    if (seq_rows_ok(c, P1) && c->ro_partner.p && !(fenv && fenv[0] == '0')) {
+    if (seq_rows_ok(c, P1) && c->ro_partner.p && !opt_off(OPT_RO_FUSE)) {
       P1.ro_fuse = q->ds_function == TSDB_AGG_AVG ? 1 : 2;
       fused = true;
     }
@@ -4956,8 +4962,7 @@ bool seq_dense_wanted(tsdbhip_ctx* c, const Plan& P) {
   if (!(P.f >= F_SUM && P.f <= F_MULT) || P.raw || P.anchored || P.gsel || P.ordered || P.multi || P.emit_only ||
       P.dense_out || P.values_only || P.sel_direct)
     return false;
-  if (const char* e = std::getenv("TSDBHIP_SEQ")) if (e[0] == '0') return false;   // tests: the k_grid path
-  if (const char* e = std::getenv("TSDBHIP_FAST")) if (e[0] == '0') return false;  // (the general path only)
+  if (opt_off(OPT_SEQ) || opt_off(OPT_FAST)) return false;   // tests: the k_grid path (the general path only)
   if (!(c->seqd_valid && c->seqd_ss == P.ss && c->seqd_se == P.se)) {
     bool any = false, ok = true, uni = true;
     int64_t rows = 0, dps = 0;
@@ -5015,8 +5020,7 @@ int run_rollup(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out) {
 // aggregator's tile partials in c->m_* (MultiPartials).  1: the queries or the batch do not
 // qualify, or a tile broke a streaming premise (the caller runs the queries one by one).
 int fused_pass(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, Plan& P) {
-  const char* env = std::getenv("TSDBHIP_MULTI_FUSE");
-  if (n < 2 || (env && env[0] == '0')) return 1;
+  if (n < 2 || opt_off(OPT_MULTI_FUSE)) return 1;
   for (int i = 0; i < n; i++) {
     const int a = qs[i].aggregator;
     if (!(a == TSDB_AGG_SUM || a == TSDB_AGG_AVG || a == TSDB_AGG_MIN || a == TSDB_AGG_MAX || a == TSDB_AGG_DEV ||
@@ -5995,8 +5999,7 @@ extern "C" int tsdbhip_rollup_run(tsdbhip_ctx* c, const tsdbhip_rollup_spec* sp,
     ap.pres = c->ro_pres.as<uint8_t>();
     // streaming kernel per row class (class A over every series, class B over what A handed
     // back), then the general kernel over the rest
-    const char* env = std::getenv("TSDBHIP_FAST");
-    const bool fast = !(env && env[0] == '0') && c->fast_qw && n > 0 && P.I <= (1LL << 29) &&
+    const bool fast = !opt_off(OPT_FAST) && c->fast_qw && n > 0 && P.I <= (1LL << 29) &&
                       rollup_fast_lds(P.K) <= 32 * 1024;
     const int32_t* list = nullptr;
     const int32_t* list_n = nullptr;
@@ -6160,11 +6163,7 @@ namespace tsdb {
 // Small or misaligned copies, and TSDBHIP_PULL=0, take hipMemcpyAsync.
 constexpr size_t UP_CHUNK = (size_t)32 << 20;
 hipError_t h2d(tsdbhip_ctx* c, void* dst, const void* src, size_t n, hipStream_t st) {
-  static const bool pull_ok = [] {
-    const char* e = std::getenv("TSDBHIP_PULL");
-    return !(e && e[0] == '0');
-  }();
-  if (!pull_ok || n < ((size_t)1 << 20) || ((uintptr_t)dst & 15) != 0) return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st);
+  if (n < ((size_t)1 << 20) || ((uintptr_t)dst & 15) != 0) return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st);
   hipPointerAttribute_t a{};
   if (hipPointerGetAttributes(&a, src) == hipSuccess && a.type == hipMemoryTypeHost && a.devicePointer) {
     if ((((uintptr_t)src ^ (uintptr_t)dst) & 15) != 0) return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st);

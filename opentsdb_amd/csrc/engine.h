@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "rollup_codec.h"
+#include "opts.h"
 #include <stdint.h>
 
 namespace tsdb {

@@ -435,8 +435,8 @@ int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end,
   p.row_pos = S->row_pos.as<int64_t>();
   p.hkey = S->hkey.as<uint64_t>();
   p.hidx = S->hidx.as<int32_t>();
-  if (const char* le = getenv("TSDBHIP_HIST_LAYOUT"); !(le && le[0] == '0') && S->n_layouts > 0) {
-    p.col_lid = S->col_lid.as<int32_t>();   // (tests: 0 = every bucket through the keyed lookup)
+  if (!opt_off(OPT_HIST_LAYOUT) && S->n_layouts > 0) {
+    p.col_lid = S->col_lid.as<int32_t>();   // (option HIST_LAYOUT = 0: every bucket through the keyed lookup)
     p.lay_off = S->lay_off.as<int32_t>();
     p.lay_di = S->lay_di.as<int32_t>();
   }
@@ -625,9 +625,11 @@ int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end,
     HOK(hipMemsetAsync(S->pres.p, 0, n_points * p.W * 4 + 4, st));
     p.pres = S->pres.as<uint32_t>();
   }
-  if (const char* dbg = getenv("TSDBHIP_HIST_DBG")) p.dbg = atoi(dbg);
-  const char* wenv = getenv("TSDBHIP_HIST_WINDOW");   // tests: 0 = the per-column atomic kernel
-  if (S->lds_dict && hist_window_points(p, S->lslots) > 0 && !(wenv && wenv[0] == '0')) {
+#ifdef TSDBHIP_KDBG
+  if (opt(OPT_DBG) > 0) p.dbg = (int32_t)opt(OPT_DBG);   // profiling build only (results invalid)
+#endif
+  // option HIST_WINDOW = 0 (tests): the per-column atomic kernel
+  if (S->lds_dict && hist_window_points(p, S->lslots) > 0 && !opt_off(OPT_HIST_WINDOW)) {
     HOK(S->q_vlen.ensure(nsp * 4 + 4));
     HOK(S->q_voff.ensure(nsp * 8 + 16));
     HOK(S->q_vpos.ensure(NP * 4 + 4));

@@ -4,6 +4,15 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "opts.h"
+
+// the bucket-atomics skip of the profiling bits exists only in a -DTSDBHIP_KDBG build
+#ifdef TSDBHIP_KDBG
+#define HIST_SKIP_ADD(p) (((p).dbg & 1) != 0)
+#else
+#define HIST_SKIP_ADD(p) false
+#endif
+
 namespace tsdb {
 
 // Bucket dictionary: open-addressing hash set of the store's bucket keys
@@ -90,7 +99,7 @@ struct HistQueryParams {
   const int32_t* col_lid;    // [n_cells] bucket layout of the column (-1: none), or null
   const int32_t* lay_off;    // [layouts] first entry of the layout's dictionary indices in lay_di
   const int32_t* lay_di;     // dictionary index of each bucket of each layout
-  int32_t dbg;               // profiling switches (TSDBHIP_HIST_DBG; results invalid): 1 skip the bucket atomics
+  int32_t dbg;               // profiling bits (option DBG, a -DTSDBHIP_KDBG build only; results invalid): 1 skip the bucket atomics
 };
 
 hipError_t hist_validate(const HistLoadParams& p, hipStream_t s);

@@ -438,7 +438,7 @@ __device__ __forceinline__ void accum_columns(const HistQueryParams& p, int32_t 
       if (di < 0) set_err(p.err, -22, WHY_DICT);
       else addr = base + (uint64_t)di;
     }
-    if (seg_scan(addr, val, OpAdd()) && addr != ~0ull && !(p.dbg & 1))
+    if (seg_scan(addr, val, OpAdd()) && addr != ~0ull && !HIST_SKIP_ADD(p))
       atomicAdd((unsigned long long*)&p.acc[addr], (unsigned long long)val);
     if (p.pres && di >= 0) atomicOr(&p.pres[(uint64_t)pt * p.W + (di >> 5)], 1u << (di & 31));
   }
@@ -728,7 +728,7 @@ __device__ void accum_column_w(const HistQueryParams& p, const Window& w, int32_
       set_err(p.err, -22, WHY_DICT);
       continue;
     }
-    if (!(p.dbg & 1)) w_add(p, w, local, pt, di, val);
+    if (!HIST_SKIP_ADD(p)) w_add(p, w, local, pt, di, val);
     if (p.pres) {
       if (local >= 0) atomicOr(&w.pres[(uint32_t)local * (uint32_t)p.W + (di >> 5)], 1u << (di & 31));
       else atomicOr(&p.pres[(uint64_t)pt * p.W + (di >> 5)], 1u << (di & 31));
@@ -770,7 +770,7 @@ __device__ void accum_column_wp(const HistQueryParams& p, const Window& w, int32
           set_err(p.err, -22, WHY_DICT);
           continue;
         }
-        if (!(p.dbg & 1)) w_add(p, w, local, pt, di, val);
+        if (!HIST_SKIP_ADD(p)) w_add(p, w, local, pt, di, val);
         if (p.pres) {
           if (local >= 0) atomicOr(&w.pres[(uint32_t)local * (uint32_t)p.W + (di >> 5)], 1u << (di & 31));
           else atomicOr(&p.pres[(uint64_t)pt * p.W + (di >> 5)], 1u << (di & 31));
@@ -804,7 +804,7 @@ __device__ void accum_column_wp(const HistQueryParams& p, const Window& w, int32
     int32_t di = cur == key ? cidx : (cur == HK_EMPTY ? -1 : dict.find(key));
     if (di < 0) set_err(p.err, -22, WHY_DICT);
     else {
-      if (!(p.dbg & 1)) w_add(p, w, local, pt, di, val);
+      if (!HIST_SKIP_ADD(p)) w_add(p, w, local, pt, di, val);
       if (p.pres) {
         if (local >= 0) atomicOr(&w.pres[(uint32_t)local * (uint32_t)p.W + (di >> 5)], 1u << (di & 31));
         else atomicOr(&p.pres[(uint64_t)pt * p.W + (di >> 5)], 1u << (di & 31));
@@ -1077,12 +1077,11 @@ int hist_window_points(const HistQueryParams& p, int lslots) {
   const int64_t fixed = (int64_t)(STAGE_W + 8) * 4 + (int64_t)lslots * 12 + 256;
   const int64_t per = (int64_t)p.C * 8 + 4 + (p.pres ? (int64_t)p.W * 4 : 0);
   // three blocks a CU when a 64-point window fits in HIST_WLDS, else two with 80 KB
-  int64_t budget = HIST_WLDS;
-  if (const char* e = getenv("TSDBHIP_HIST_WLDS")) budget = std::max<int64_t>(40 * 1024, (int64_t)atoi(e) * 1024);   // A/B
+  const int64_t budget = HIST_WLDS;
   int64_t ws = (budget - fixed) / per;
   if (ws < 64) ws = (80 * 1024 - fixed) / per;
   if (ws < 32) return 0;
-  if (const char* e = getenv("TSDBHIP_HIST_WS")) ws = std::min<int64_t>(ws, std::max(1, atoi(e)));   // tests: tiny windows
+  if (opt(OPT_HIST_WS) > 0) ws = std::min<int64_t>(ws, opt(OPT_HIST_WS));   // tests: tiny windows
   return (int)std::min<int64_t>(ws, 4096);
 }
 
@@ -1093,16 +1092,10 @@ hipError_t hist_accum_window(const HistQueryParams& p, const int32_t* vpos, int6
   if (WS <= 0 || !lkey) return hipErrorInvalidValue;
   const size_t lds = (size_t)(STAGE_W + 8) * 4 + (size_t)lslots * 12 + (size_t)WS * p.C * 8 + (size_t)WS * 4 +
                      (p.pres ? (size_t)WS * p.W * 4 : 0);
-  const char* penv = getenv("TSDBHIP_HIST_PIPE");   // A/B: 0 = the unpipelined bucket loop
-  const bool pipe = !(penv && penv[0] == '0');
-  // staging loads in flight a thread: 4 (default) or 16 (TSDBHIP_HIST_SU=16).  r03o sweep of the
-  // histogram bench query: 52 KB window + 4 in flight 2.60 ms; + 16 2.77; 80 KB 3.21 / 3.40; 160 KB 5.08
-  const char* uenv = getenv("TSDBHIP_HIST_SU");
-  const bool su4 = !(uenv && uenv[0] == '1');
-  const void* kf = pipe ? (su4 ? reinterpret_cast<const void*>(&k_hist_accw<true, 4>)
-                               : reinterpret_cast<const void*>(&k_hist_accw<true, 16>))
-                        : (su4 ? reinterpret_cast<const void*>(&k_hist_accw<false, 4>)
-                               : reinterpret_cast<const void*>(&k_hist_accw<false, 16>));
+  // the pipelined bucket loop with 4 staging loads in flight a thread.  r03o sweep of the
+  // histogram bench query: 52 KB window + 4 in flight 2.60 ms; + 16 2.77; 80 KB 3.21 / 3.40; 160 KB
+  // 5.08; the unpipelined loop lost as well (those variants are gone)
+  const void* kf = reinterpret_cast<const void*>(&k_hist_accw<true, 4>);
   hipError_t e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   int dev = 0, cus = 256;
@@ -1112,10 +1105,7 @@ hipError_t hist_accum_window(const HistQueryParams& p, const int32_t* vpos, int6
   const int64_t want = std::min<int64_t>(tiles, (int64_t)cus * per_cu);
   const int64_t chunk = ((tiles + want - 1) / want) * ATP;
   const unsigned grid = (unsigned)((nvp + chunk - 1) / chunk);
-  if (pipe && su4) hipLaunchKernelGGL((k_hist_accw<true, 4>), dim3(grid), dim3(ATP), lds, s, p, vpos, nvp, chunk, lkey, lidx, WS, lslots);
-  else if (pipe) hipLaunchKernelGGL((k_hist_accw<true, 16>), dim3(grid), dim3(ATP), lds, s, p, vpos, nvp, chunk, lkey, lidx, WS, lslots);
-  else if (su4) hipLaunchKernelGGL((k_hist_accw<false, 4>), dim3(grid), dim3(ATP), lds, s, p, vpos, nvp, chunk, lkey, lidx, WS, lslots);
-  else hipLaunchKernelGGL((k_hist_accw<false, 16>), dim3(grid), dim3(ATP), lds, s, p, vpos, nvp, chunk, lkey, lidx, WS, lslots);
+  hipLaunchKernelGGL((k_hist_accw<true, 4>), dim3(grid), dim3(ATP), lds, s, p, vpos, nvp, chunk, lkey, lidx, WS, lslots);
   return hipGetLastError();
 }
 hipError_t hist_layout_index(int64_t n_cells, const uint64_t* voff, const uint8_t* val, const uint8_t* status,

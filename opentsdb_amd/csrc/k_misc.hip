@@ -884,10 +884,9 @@ hipError_t launch_seq_dense(const GridParams& p, int f, double* dense, uint8_t* 
                             bool uniform) {
   if (n_series <= 0) return hipSuccess;
   const unsigned nb = (unsigned)((n_series + 255) / 256);
-  const char* wenv = std::getenv("TSDBHIP_SEQ_WAVE");   // A/B: 0 = one series per lane
-  // uniform rows of 64+ points on average only (engine.cpp seq_dense_wanted): a row of mixed
+  // (option SEQ_WAVE = 0: one series per lane) uniform rows of 64+ points on average only (engine.cpp seq_dense_wanted): a row of mixed
   // widths is decoded by one lane, and short rows leave the wave waiting on each row's descriptor
-  const bool wave = uniform && p.K <= 64 && !(wenv && wenv[0] == '0');
+  const bool wave = uniform && p.K <= 64 && !opt_off(OPT_SEQ_WAVE);
   const unsigned nw = (unsigned)((n_series + SEQW_WAVES - 1) / SEQW_WAVES);
 #define SEQ_CASE(FF)                                                                                          \
   case FF:                                                                                                    \

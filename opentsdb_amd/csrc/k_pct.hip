@@ -1975,338 +1975,6 @@ __global__ __launch_bounds__(T, OCC) void k_sel_reg(SelParams p) {
   }
 }
 
-// k_sel_hl: k_sel_reg over 32-bit keys of the values' upper words.  The select is VALU-bound
-// (config 3 p99, k_sel_reg: VALU issue 0.74, ~50 VALU instructions a key on 64-bit keys), and
-// the upper word of a double orders distinct upper words exactly as the doubles: the rank is
-// found among the upper-word keys, then resolved among the few values that share the selected
-// upper word by their lower words (loaded only for those), so the result is k_sel_reg's.
-// Premise: the NaNs in vals are the canonical +NaN or the fill pattern (sel_direct_out /
-// k_emit_vals write canon_nan values): their upper-word keys lie above +inf's, as in f2key order.
-__device__ __forceinline__ uint32_t hkey(uint32_t h) { return (h >> 31) ? ~h : (h | 0x80000000u); }
-__device__ __forceinline__ uint32_t unhkey(uint32_t k) { return (k >> 31) ? (k & 0x7FFFFFFFu) : ~k; }
-constexpr uint32_t HKEY_INF = 0xFFF00000u;   // hkey of +inf's upper word: keys above it are NaN / absent
-
-struct SelHL {
-  uint32_t cand[SEL_FIN];
-  uint32_t bin, rr, nc, ex, res, res1, lt, eq, hi2, m, kmin, kmax;
-};
-
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) { return ~wave_max_u32(~x); }
-
-template <int T, int R, int OCC>
-__global__ __launch_bounds__(T, OCC) void k_sel_hl(SelParams p) {
-  __shared__ uint32_t H[4096];
-  __shared__ int WT[T / 64];
-  __shared__ SelHL S;
-  constexpr int BPT = 4096 / T;   // histogram bins a thread scans
-  const int64_t nseg = p.G * p.K;
-  const int64_t per = (nseg + 7) / 8;
-  const int64_t i = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;   // (XCD-contiguous runs)
-  if (i >= nseg) return;
-  const int tid = threadIdx.x, lane = tid & 63;
-  if (!p.uni[i]) {
-    if (tid == 0) { p.out_val[i] = 0.0; p.out_flag[i] = 0; }
-    return;
-  }
-  const int64_t g = i / p.K, k = i - g * p.K;
-  const int64_t gs0 = p.group_series_ptr[g], n = p.group_series_ptr[g + 1] - gs0;
-  // the column through buffer descriptors (lower words, upper words): a load is a 32-bit offset,
-  // no 64-bit address a load (the host keeps n * stride * 4 below 2^31); elements past the column
-  // read 0 (range check) and are masked below
-  const char* col = reinterpret_cast<const char*>(p.vals + (p.cols ? gs0 * p.K + k * n : gs0 * p.K + k));
-  const uint32_t sb = p.cols ? 8u : (uint32_t)(8 * p.K);   // bytes from element j to j + 1
-  const int nb = (int)((n - 1) * sb + 8);
-  const auto rs_lo = __builtin_amdgcn_make_buffer_rsrc((void*)col, 0, nb, 0x00020000);
-  const auto rs_hi = __builtin_amdgcn_make_buffer_rsrc((void*)(col + 4), 0, nb - 4, 0x00020000);
-  auto word = [&](int t, int u, bool hi) {   // element t + u * T
-    // (the whole offset in voffset: the range check covers voffset, not soffset)
-    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(hi ? rs_hi : rs_lo, (int)((uint32_t)(t + u * T) * sb), 0, 0);
-  };
-  uint32_t key[R];
-#pragma unroll
-  for (int u = 0; u < R; u++) key[u] = word(tid, u, true);   // every load issued before any is used
-  if (tid == 0) { S.m = 0; S.kmin = ~0u; S.kmax = 0; }
-  int mloc = 0;
-  uint32_t kmn = ~0u, kmx = 0;
-#pragma unroll
-  for (int u = 0; u < R; u++) {
-    const uint32_t x = tid + (int64_t)u * T < n ? hkey(key[u]) : ~0u;   // absent: above every NaN key
-    key[u] = x;
-    const bool real = x <= HKEY_INF;
-    mloc += real ? 1 : 0;
-    kmn = min(kmn, x);
-    kmx = max(kmx, real ? x : 0u);
-  }
-  mloc = wave_sum_int(mloc);
-  kmn = wave_min_u32(kmn);
-  kmx = wave_max_u32(kmx);
-  __syncthreads();
-  if (lane == 0) {
-    atomicAdd(&S.m, (uint32_t)mloc);
-    atomicMin(&S.kmin, kmn);
-    atomicMax(&S.kmax, kmx);
-  }
-  __syncthreads();
-  const int64_t m = S.m;   // the non-NaN values: ranks 0 .. m - 1
-  if (m == 0) {
-    if (tid == 0) { p.out_val[i] = (double)NAN; p.out_flag[i] = 1; }
-    return;
-  }
-  const uint32_t kmin = S.kmin, kmax = S.kmax;
-  int64_t r0, r1;
-  sel_ranks(p.fn, m, r0, r1);
-  // ---- the upper-word key of rank r0 (NaN / absent keys clamped to kmax: they tie at the top,
-  // above every rank < m) ----
-  uint32_t hs = kmin;
-  int64_t lt = 0;   // keys below hs
-  if (kmin != kmax) {
-    const int h = 31 - __clz((int)(kmin ^ kmax));   // the highest bit the keys differ in
-    int sw = h >= 11 ? h - 11 : 0;                  // first digit: bits [sw, sw + 12)
-    uint32_t prefix = h == 31 ? 0u : (kmin & ~((2u << h) - 1u));
-#pragma unroll
-    for (int b = 0; b < BPT / 4; b++) reinterpret_cast<uint4*>(H)[tid * (BPT / 4) + b] = make_uint4(0u, 0u, 0u, 0u);
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < R; u++) atomicAdd(&H[(min(key[u], kmax) >> sw) & 0xFFFu], 1u);
-    __syncthreads();
-    int64_t r = r0;
-    uint32_t c[BPT];
-#pragma unroll
-    for (int b = 0; b < BPT / 4; b++) {
-      const uint4 c4 = reinterpret_cast<const uint4*>(H)[tid * (BPT / 4) + b];
-      c[4 * b] = c4.x; c[4 * b + 1] = c4.y; c[4 * b + 2] = c4.z; c[4 * b + 3] = c4.w;
-    }
-    uint32_t t = 0;
-#pragma unroll
-    for (int q = 0; q < BPT; q++) t += c[q];
-    const int incl = (int)wave_incl_sum((int)t);
-    if (lane == 63) WT[tid >> 6] = incl;
-    __syncthreads();
-    int woff = 0;
-    for (int w2 = 0; w2 < (tid >> 6); w2++) woff += WT[w2];
-    {
-      int64_t ex = (int64_t)woff + incl - t;
-      if (ex <= r && r < ex + (int64_t)t) {
-        int q = 0;
-        for (; q < BPT - 1; q++) {
-          if (r < ex + c[q]) break;
-          ex += c[q];
-        }
-        S.bin = (uint32_t)(tid * BPT + q);
-        S.rr = (uint32_t)(r - ex);
-        S.nc = c[q];
-        S.ex = (uint32_t)ex;
-      }
-    }
-    __syncthreads();
-    prefix |= S.bin << sw;
-    uint32_t mask = sw + 12 >= 32 ? ~0u << sw : (~0u << sw) & ~(~0u << (sw + 12));
-    mask |= h == 31 ? 0u : ~((2u << h) - 1u);
-    r = S.rr;
-    lt = S.ex;
-    uint32_t nc = S.nc;
-    __syncthreads();
-    // 8-bit digits below while the bin holds more than SEL_FIN keys (values sharing their upper
-    // 20+ bits: rare)
-    while (sw > 0 && nc > (uint32_t)SEL_FIN) {
-      sw = sw >= 8 ? sw - 8 : 0;
-      const uint32_t dm = (sw + 8 >= 32 ? ~0u : ((1u << (sw + 8)) - 1u)) & ~((1u << sw) - 1u) & ~mask;   // this digit's bits
-      for (int b = tid; b < 256; b += T) H[b] = 0;
-      __syncthreads();
-#pragma unroll
-      for (int u = 0; u < R; u++) {
-        const uint32_t x = min(key[u], kmax);
-        if ((x & mask) == prefix) atomicAdd(&H[((x & dm) >> sw) & 255u], 1u);
-      }
-      __syncthreads();
-      if (tid < 64) {
-        uint32_t cc[4], tt = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) { cc[q] = H[tid * 4 + q]; tt += cc[q]; }
-        const int64_t in2 = wave_incl_sum((int)tt);
-        int64_t ex = in2 - tt;
-        if (ex <= r && r < in2) {
-          int q = 0;
-          for (; q < 3; q++) {
-            if (r < ex + cc[q]) break;
-            ex += cc[q];
-          }
-          S.bin = (uint32_t)(tid * 4 + q);
-          S.rr = (uint32_t)(r - ex);
-          S.nc = cc[q];
-          S.ex = (uint32_t)ex;
-        }
-      }
-      __syncthreads();
-      prefix |= S.bin << sw;
-      mask |= dm;
-      r = S.rr;
-      lt += S.ex;
-      nc = S.nc;
-      __syncthreads();
-    }
-    if (sw == 0) {
-      hs = prefix;
-    } else {   // <= SEL_FIN keys share the prefix: gathered and ranked directly
-      if (tid == 0) S.nc = 0;
-      __syncthreads();
-#pragma unroll
-      for (int u = 0; u < R; u++) {
-        const uint32_t x = min(key[u], kmax);
-        if ((x & mask) == prefix) S.cand[atomicAdd(&S.nc, 1u)] = x;
-      }
-      __syncthreads();
-      const uint32_t ncg = S.nc;
-      if ((uint32_t)tid < ncg) {
-        const uint32_t x = S.cand[tid];
-        uint32_t less = 0, eq = 0;
-        for (uint32_t q = 0; q < ncg; q++) {
-          const uint32_t y = S.cand[q];
-          less += y < x;
-          eq += y == x;
-        }
-        if ((int64_t)less <= r && r < (int64_t)(less + eq)) { S.res = x; S.lt = less; }
-      }
-      __syncthreads();
-      hs = S.res;
-      lt += S.lt;
-      __syncthreads();
-    }
-  }
-  // ---- the values whose upper word is hs: how many, and the next upper-word key above ----
-  {
-    int e = 0;
-    uint32_t nx = ~0u;
-#pragma unroll
-    for (int u = 0; u < R; u++) {
-      e += key[u] == hs ? 1 : 0;
-      nx = min(nx, key[u] > hs ? key[u] : ~0u);
-    }
-    e = wave_sum_int(e);
-    nx = wave_min_u32(nx);
-    if (tid == 0) { S.eq = 0; S.hi2 = ~0u; }
-    __syncthreads();
-    if (lane == 0) {
-      atomicAdd(&S.eq, (uint32_t)e);
-      atomicMin(&S.hi2, nx);
-    }
-    __syncthreads();
-  }
-  const uint32_t eqn = S.eq, hi2 = S.hi2;
-  const int64_t rr0 = r0 - lt;   // rank among the values of upper word hs
-  const bool want1 = r1 >= 0 && rr0 + 1 < (int64_t)eqn;
-  // lower-word keys: a negative double's value falls as its lower word rises
-  const bool neg_s = (hs >> 31) == 0;
-  uint32_t lo0 = 0, lo1 = 0;
-  if (eqn <= (uint32_t)SEL_FIN) {
-    __syncthreads();
-    if (tid == 0) S.nc = 0;
-    __syncthreads();
-    int t2 = tid;
-    asm volatile("" : "+v"(t2));   // (addresses recomputed here, not kept live from the loads above)
-#pragma unroll
-    for (int u = 0; u < R; u++) {
-      if (key[u] == hs) {
-        const uint32_t lw = word(t2, u, false);
-        S.cand[atomicAdd(&S.nc, 1u)] = neg_s ? ~lw : lw;
-      }
-    }
-    __syncthreads();
-    if ((uint32_t)tid < eqn) {
-      const uint32_t x = S.cand[tid];
-      uint32_t less = 0, eq = 0;
-      for (uint32_t q = 0; q < eqn; q++) {
-        const uint32_t y = S.cand[q];
-        less += y < x;
-        eq += y == x;
-      }
-      if ((int64_t)less <= rr0 && rr0 < (int64_t)(less + eq)) S.res = x;
-      if (want1 && (int64_t)less <= rr0 + 1 && rr0 + 1 < (int64_t)(less + eq)) S.res1 = x;
-    }
-    __syncthreads();
-    lo0 = S.res;
-    lo1 = S.res1;
-  } else {
-    // more than SEL_FIN values share the upper word: 8-bit digits of the lower-word keys, the
-    // lower words re-read from memory for each digit (L2-resident)
-    auto lo_rank = [&](int64_t rr) {
-      uint32_t pre = 0, msk = 0;
-      int t2 = tid;
-      asm volatile("" : "+v"(t2));
-      for (int sh = 24; sh >= 0; sh -= 8) {
-        __syncthreads();
-        for (int b = tid; b < 256; b += T) H[b] = 0;
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < R; u++) {
-          if (key[u] == hs) {
-            const uint32_t lw = word(t2, u, false);
-            const uint32_t x = neg_s ? ~lw : lw;
-            if ((x & msk) == pre) atomicAdd(&H[(x >> sh) & 255u], 1u);
-          }
-        }
-        __syncthreads();
-        if (tid < 64) {
-          uint32_t cc[4], tt = 0;
-#pragma unroll
-          for (int q = 0; q < 4; q++) { cc[q] = H[tid * 4 + q]; tt += cc[q]; }
-          const int64_t in2 = wave_incl_sum((int)tt);
-          int64_t ex = in2 - tt;
-          if (ex <= rr && rr < in2) {
-            int q = 0;
-            for (; q < 3; q++) {
-              if (rr < ex + cc[q]) break;
-              ex += cc[q];
-            }
-            S.bin = (uint32_t)(tid * 4 + q);
-            S.ex = (uint32_t)ex;
-          }
-        }
-        __syncthreads();
-        pre |= S.bin << sh;
-        msk |= 255u << sh;
-        rr -= S.ex;
-      }
-      return pre;
-    };
-    lo0 = lo_rank(rr0);
-    if (want1) lo1 = lo_rank(rr0 + 1);
-  }
-  const double v0 = __longlong_as_double((long long)(((uint64_t)unhkey(hs) << 32) | (neg_s ? ~lo0 : lo0)));
-  double v1 = v0;
-  if (r1 >= 0) {
-    if (want1) {
-      v1 = __longlong_as_double((long long)(((uint64_t)unhkey(hs) << 32) | (neg_s ? ~lo1 : lo1)));
-    } else {
-      // rank r0 + 1 lies in the next upper word: its smallest lower-word key
-      const bool neg2 = (hi2 >> 31) == 0;
-      uint32_t mn = ~0u;
-      int t2 = tid;
-      asm volatile("" : "+v"(t2));
-#pragma unroll
-      for (int u = 0; u < R; u++) {
-        if (key[u] == hi2) {
-          const uint32_t lw = word(t2, u, false);
-          mn = min(mn, neg2 ? ~lw : lw);
-        }
-      }
-      mn = wave_min_u32(mn);
-      __syncthreads();
-      if (tid == 0) S.res = ~0u;
-      __syncthreads();
-      if (lane == 0) atomicMin(&S.res, mn);
-      __syncthreads();
-      const uint32_t l2 = S.res;
-      v1 = __longlong_as_double((long long)(((uint64_t)unhkey(hi2) << 32) | (neg2 ? ~l2 : l2)));
-    }
-  }
-  if (tid == 0) {
-    const double r = select_sorted(p.fn, (int)m, [&](int j) { return (int64_t)j == r0 ? v0 : v1; });
-    if (isinf(r)) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // AggregationIterator.doubleValue :640-643
-    p.out_val[i] = r;
-    p.out_flag[i] = 1;
-  }
-}
 
 template <int KPL>
 __device__ uint64_t wave_radix_select_reg(const uint64_t (&kr)[KPL], uint64_t vm, int r, SelWave& W);
@@ -2530,112 +2198,6 @@ hipError_t launch_win_select(const WinParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-// k_sel_reg2<SL>: k_sel_reg over SL adjacent slots of one group per block.  The [series][K]
-// layout puts a series' slots side by side, so one 16-B load per row serves two slots: a group's
-// row lines are read K / SL times instead of K times (k_sel_reg re-reads every line from L2 once
-// per slot block).  Keys stay in registers (SL x SEL_REG_R per thread); the slots are selected
-// one after the other with the same radix select, so the results are k_sel_reg's.
-template <int SL, int OCC>
-__global__ __launch_bounds__(SEL_REG_T, OCC) void k_sel_reg2(SelParams p) {
-  __shared__ SelShared S;
-  __shared__ unsigned long long red[2];
-  const int64_t nkc = (p.K + SL - 1) / SL;
-  const int64_t nseg = p.G * nkc;
-  const int64_t per = (nseg + 7) / 8;
-  const int64_t i = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
-  if (i >= nseg) return;
-  const int tid = threadIdx.x;
-  const int64_t g = i / nkc, k0 = (i - g * nkc) * SL;
-  const int ns = (int)min((int64_t)SL, p.K - k0);
-  bool any = false;
-#pragma unroll
-  for (int sl = 0; sl < SL; sl++) any = any || (sl < ns && p.uni[g * p.K + k0 + sl]);
-  if (!any) {
-    if (tid < ns) { p.out_val[g * p.K + k0 + tid] = 0.0; p.out_flag[g * p.K + k0 + tid] = 0; }
-    return;
-  }
-  const int64_t gs0 = p.group_series_ptr[g], n = p.group_series_ptr[g + 1] - gs0;
-  // all loads issued before any is consumed; SL = 2: one 16-B load per row when K is even
-  double x[SL][SEL_REG_R];
-  const bool vec = SL == 2 && (p.K & 1) == 0 && ns == 2;
-#pragma unroll
-  for (int u = 0; u < SEL_REG_R; u++) {
-    const int64_t j = tid + (int64_t)u * SEL_REG_T;
-    const int64_t jj = j < n ? j : 0;
-    const double* src = p.vals + (gs0 + jj) * p.K + k0;
-    if (vec) {
-      const double2 v2 = *reinterpret_cast<const double2*>(src);
-      x[0][u] = v2.x;
-      x[SL - 1][u] = v2.y;
-    } else {
-#pragma unroll
-      for (int sl = 0; sl < SL; sl++) x[sl][u] = sl < ns ? src[sl] : 0.0;
-    }
-  }
-#pragma unroll
-  for (int sl = 0; sl < SL; sl++) {
-    if (sl >= ns) break;
-    const int64_t oi = g * p.K + k0 + sl;
-    if (!p.uni[oi]) {
-      if (tid == 0) { p.out_val[oi] = 0.0; p.out_flag[oi] = 0; }
-      continue;
-    }
-    uint64_t key[SEL_REG_R];
-    uint32_t valid = 0;
-    int nan_local = 0;
-#pragma unroll
-    for (int u = 0; u < SEL_REG_R; u++) {
-      const bool v = tid + (int64_t)u * SEL_REG_T < n;
-      valid |= (v ? 1u : 0u) << u;
-      nan_local += (v && isnan(x[sl][u])) ? 1 : 0;
-      key[u] = f2key(canon_nan(x[sl][u]));
-    }
-    nan_local = wave_sum_int(nan_local);
-    __syncthreads();
-    if (tid == 0) red[0] = 0;
-    __syncthreads();
-    if ((tid & 63) == 0 && nan_local) atomicAdd(&red[0], (unsigned long long)nan_local);
-    __syncthreads();
-    const int64_t m = n - (int64_t)red[0];   // non-NaN values (they hold ranks 0 .. m-1)
-    __syncthreads();
-    int64_t r0 = 0, r1 = -1;
-    if (m > 0) sel_ranks(p.fn, m, r0, r1);
-    double v0 = NAN, v1 = NAN;
-    if (m > 0) {
-      const uint64_t kk0 = reg_radix_select<SEL_REG_R>(key, valid, r0, S, red);
-      v0 = key2f(kk0);
-      if (r1 >= 0) {
-        __syncthreads();
-        if (tid == 0) { red[0] = 0; red[1] = ~0ULL; }
-        __syncthreads();
-        int le = 0;
-        uint64_t gt = ~0ULL;
-#pragma unroll
-        for (int u = 0; u < SEL_REG_R; u++) {
-          if (valid >> u & 1) {
-            if (key[u] <= kk0) le++;
-            else gt = key[u] < gt ? key[u] : gt;
-          }
-        }
-        le = wave_sum_int(le);
-        gt = wave_min_u64(gt);
-        if ((tid & 63) == 0) {
-          atomicAdd(&red[0], (unsigned long long)le);
-          atomicMin(&red[1], (unsigned long long)gt);
-        }
-        __syncthreads();
-        v1 = (int64_t)red[0] > r1 ? v0 : key2f(red[1]);
-      }
-    }
-    if (tid == 0) {
-      const double r = m == 0 ? (double)NAN
-                              : select_sorted(p.fn, (int)m, [&](int j) { return (int64_t)j == r0 ? v0 : v1; });
-      if (isinf(r)) set_err(p.err, TSDB_E_ILLEGAL_STATE);   // AggregationIterator.doubleValue :640-643
-      p.out_val[oi] = r;
-      p.out_flag[oi] = 1;
-    }
-  }
-}
 
 // One thread per (group, slot), consecutive slots in consecutive lanes (coalesced rows):
 // contribute_slot over the group's spans in index order, then ps_final.  A span without a
@@ -2727,9 +2289,8 @@ hipError_t launch_sel_seg(const SelParams& p, hipStream_t s, int64_t maxn) {
   const int64_t n = p.G * p.K;
   if (n == 0) return hipSuccess;
   const int64_t per = (n + 7) / 8;
-  // columns of at most 2048 values: a wave each (k_sel_wave); TSDBHIP_SEL_WAVE=0 keeps the block
-  const char* venv = std::getenv("TSDBHIP_SEL_WAVE");
-  if (maxn <= 64 * 32 && !(venv && venv[0] == '0')) {
+  // columns of at most 2048 values: a wave each (k_sel_wave); option SEL_WAVE = 0 keeps the block
+  if (maxn <= 64 * 32 && !opt_off(OPT_SEL_WAVE)) {
     const int64_t nblk = (n + 3) / 4;
     const dim3 grid((unsigned)(((nblk + 7) / 8) * 8));
     if (maxn <= 64 * 4) hipLaunchKernelGGL(k_sel_wave<4>, grid, dim3(256), 0, s, p);
@@ -2737,45 +2298,12 @@ hipError_t launch_sel_seg(const SelParams& p, hipStream_t s, int64_t maxn) {
     else hipLaunchKernelGGL(k_sel_wave<32>, grid, dim3(256), 0, s, p);
     return hipGetLastError();
   }
-  const char* renv = std::getenv("TSDBHIP_SEL_REG");
-  if (maxn <= (int64_t)SEL_REG_T * SEL_REG_R && !(renv && renv[0] == '0')) {
-    // two blocks per CU (8 waves / SIMD, a few spilled registers) beat one: config 3 p99
-    // 11.4 vs 13.3 ms per step
-    const char* oenv = std::getenv("TSDBHIP_SEL_OCC");
-    const char* senv = std::getenv("TSDBHIP_SEL_SLOTS");   // slots per block (1: k_sel_reg)
-    // 2 slots a block halves the row-line reads but measured slower on config 3 p99 (11.4 vs
-    // 10.4 ms per step, profiles/r03g): the selection, not the L2, is the limit
-    const int sl = senv ? std::atoi(senv) : 1;
-    if (!p.cols && sl == 2) {
-      const int64_t per2 = (p.G * ((p.K + 1) / 2) + 7) / 8;
-      // one block per CU without spills (122 VGPRs); TSDBHIP_SEL_OCC=8 forces two (spilling)
-      if (oenv && oenv[0] == '8') hipLaunchKernelGGL((k_sel_reg2<2, 8>), dim3((unsigned)(per2 * 8)), dim3(SEL_REG_T), 0, s, p);
-      else hipLaunchKernelGGL((k_sel_reg2<2, 4>), dim3((unsigned)(per2 * 8)), dim3(SEL_REG_T), 0, s, p);
-      return hipGetLastError();
-    }
-    // (wave-aggregated histogram atomics, hist_add_agg, measured no faster: profiles/r05s)
-    const char* wenv = std::getenv("TSDBHIP_SEL_WIDE");   // A/B: 0 = 8-bit digits from the top
-    // 512 threads x 24 keys, two blocks a CU without spills, beat 1024 x 12 at two blocks a CU
-    // (8 waves a SIMD, 22 registers spilled): config 3 p99:1m-avg 7.90 -> 7.40 ms a step; 512 x 24 at
-    // three blocks (38 spilled) 7.72, 256 x 48 (59 spilled) 7.58, 1024 x 12 unspilled (one block) 8.54
-    // (profiles/r05z)
-    const char* tenv = std::getenv("TSDBHIP_SEL_T");      // A/B: threads a block (512 / 1024 / 256)
-    const int T = tenv ? std::atoi(tenv) : 512;
-    const int occ = oenv ? std::atoi(oenv) : 0;
-    // TSDBHIP_SEL_HL=1: k_sel_hl (32-bit keys of the upper words).  It measured no faster than
-    // k_sel_reg 512 x 24 (config 3 p99:1m-avg 7.44 ms at 3 blocks a CU, 7.64 at 4 with spills,
-    // 7.50 for 256 x 48, vs 7.40; profiles/r05ad), so the 64-bit kernel stays the default.
-    const char* henv = std::getenv("TSDBHIP_SEL_HL");
-    if (henv && henv[0] == '1' && maxn * 8 * (p.cols ? 1 : p.K) < (int64_t)1 << 31) {
-      hipLaunchKernelGGL((k_sel_hl<512, 24, 6>), dim3((unsigned)(per * 8)), dim3(512), 0, s, p);
-      return hipGetLastError();
-    }
-    if (occ == 4 && T == 1024) hipLaunchKernelGGL(k_sel_reg<4>, dim3((unsigned)(per * 8)), dim3(SEL_REG_T), 0, s, p);
-    else if (wenv && wenv[0] == '0') hipLaunchKernelGGL((k_sel_reg<8, false, false>), dim3((unsigned)(per * 8)), dim3(SEL_REG_T), 0, s, p);
-    else if (T == 512 && occ == 6) hipLaunchKernelGGL((k_sel_reg<6, false, true, 512, 24>), dim3((unsigned)(per * 8)), dim3(512), 0, s, p);
-    else if (T == 512) hipLaunchKernelGGL((k_sel_reg<4, false, true, 512, 24>), dim3((unsigned)(per * 8)), dim3(512), 0, s, p);
-    else if (T == 256) hipLaunchKernelGGL((k_sel_reg<4, false, true, 256, 48>), dim3((unsigned)(per * 8)), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL(k_sel_reg<8>, dim3((unsigned)(per * 8)), dim3(SEL_REG_T), 0, s, p);
+  if (maxn <= (int64_t)SEL_REG_T * SEL_REG_R && !opt_off(OPT_SEL_REG)) {
+    // 512 threads x 24 keys, two blocks a CU without spills: config 3 p99:1m-avg 7.40 ms a step,
+    // against 7.90 for 1024 x 12 at two blocks (spilling), 7.72 for 512 x 24 at three, 7.58 for
+    // 256 x 48, 8.54 for 1024 x 12 unspilled, 7.44 for 32-bit keys of the upper words (k_sel_hl),
+    // 10.4 -> 11.4 for two slots a block (profiles/r03g, r05z, r05ad); those variants are gone
+    hipLaunchKernelGGL((k_sel_reg<4, false, true, 512, 24>), dim3((unsigned)(per * 8)), dim3(512), 0, s, p);
     return hipGetLastError();
   }
   const size_t lds = (size_t)SEL_CAP * 8;
@@ -2788,17 +2316,13 @@ hipError_t launch_sel_seg(const SelParams& p, hipStream_t s, int64_t maxn) {
 hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s) {
   if (p.n_series == 0) return hipSuccess;
   const dim3 grid((unsigned)((p.n_series + 3) / 4)), block(256);
-  const char* denv = std::getenv("TSDBHIP_PCTD");
   // ring depth: 3 rows for the general kernel; 2 for the key kernel (config 5 1h-p99: 18.1 /
   // 19.7 / 22.0 ms at D = 2 / 3 / 4 -- occupancy beats depth)
-  const int D = denv ? std::atoi(denv) : (vl == 4 && p.I == 3600000 ? 2 : 3);
+  const int D = vl == 4 && p.I == 3600000 ? 2 : 3;
   // 1 h buckets of 4-byte values: the 32-bit key kernel (its misses go to k_pct)
-  const bool keys = vl == 4 && p.I == 3600000 && !(std::getenv("TSDBHIP_PCT_KEYS") && std::getenv("TSDBHIP_PCT_KEYS")[0] == '0');
+  const bool keys = vl == 4 && p.I == 3600000 && !opt_off(OPT_PCT_KEYS);
   const int sel_i = (p.sel_fn - TSDB_AGG_P999) % 6;
   const bool mid = p.sel_fn == TSDB_AGG_MEDIAN || sel_i >= 4;   // median, p75, p50 (and their ep* forms)
-  // values-only key rows: ring depth (TSDBHIP_PCTDV; half the registers of a raw row)
-  const char* dvenv = std::getenv("TSDBHIP_PCTDV");
-  const int DV = dvenv ? std::atoi(dvenv) : 2;
 #define PCT_ROWS_CASE(Q, V)                                                                                  \
   if (qw == Q && vl == V) {                                                                                \
     if (V == 4 && keys && p.pct_vonly && p.pct_v6) {                                                       \
@@ -2808,19 +2332,15 @@ hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s) {
     }                                                                                                      \
     if (V == 4 && keys && p.pct_vonly) {                                                                   \
       if (mid) hipLaunchKernelGGL((k_pct_rows<Q, V, 2, 6>), grid, block, 0, s, p);                        \
-      else if (DV == 3) hipLaunchKernelGGL((k_pct_rows<Q, V, 3, 5>), grid, block, 0, s, p);               \
       else hipLaunchKernelGGL((k_pct_rows<Q, V, 2, 5>), grid, block, 0, s, p);                             \
       return hipGetLastError();                                                                            \
     }                                                                                                      \
     if (V == 4 && keys) {                                                                                  \
       if (mid) hipLaunchKernelGGL((k_pct_rows<Q, V, 2, 2>), grid, block, 0, s, p);                        \
-      else if (D == 2) hipLaunchKernelGGL((k_pct_rows<Q, V, 2, 1>), grid, block, 0, s, p);                 \
-      else if (D == 4) hipLaunchKernelGGL((k_pct_rows<Q, V, 4, 1>), grid, block, 0, s, p);                 \
-      else hipLaunchKernelGGL((k_pct_rows<Q, V, 3, 1>), grid, block, 0, s, p);                             \
+      else hipLaunchKernelGGL((k_pct_rows<Q, V, 2, 1>), grid, block, 0, s, p);                             \
       return hipGetLastError();                                                                            \
     }                                                                                                      \
     if (D == 2) hipLaunchKernelGGL((k_pct_rows<Q, V, 2, 0>), grid, block, 0, s, p);                        \
-    else if (D == 4) hipLaunchKernelGGL((k_pct_rows<Q, V, 4, 0>), grid, block, 0, s, p);                   \
     else hipLaunchKernelGGL((k_pct_rows<Q, V, 3, 0>), grid, block, 0, s, p);                               \
     return hipGetLastError();                                                                              \
   }
@@ -2832,14 +2352,13 @@ hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s) {
 
 hipError_t launch_emit(const GridParams& p, hipStream_t s) {
   if (p.n_tiles == 0) return hipSuccess;
-  const char* renv = std::getenv("TSDBHIP_EMIT_REG");
-  if (p.K <= 64 && !p.rate && !(renv && renv[0] == '0')) {
+  if (p.K <= 64 && !p.rate) {
     GridParams q = p;
     q.waves = 4;
     hipLaunchKernelGGL(k_emit_reg, dim3((unsigned)((p.n_tiles + 3) / 4)), dim3(256), 0, s, q);
     return hipGetLastError();
   }
-  if (p.K > 64 && !p.rate && !(renv && renv[0] == '0')) {
+  if (p.K > 64 && !p.rate) {
     const int nwin = (int)((p.K + 63) / 64);
     const int64_t waves = p.n_tiles * nwin;
     hipLaunchKernelGGL(k_emit_win, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, p, nwin);
@@ -3205,8 +2724,7 @@ __global__ __launch_bounds__(256) void k_raw_sel_top(RawParams p) {
 // T for k_raw_sel_top when every rank it can be asked for lies within T of the top (ksel.h
 // raw_top_need over m <= k_max operands, both reducers); 0 = no.
 int raw_sel_top_t(int fn, int64_t k_max) {
-  const char* e = std::getenv("TSDBHIP_RAW_SEL_TOP");   // A/B: 0 = the per-point kernels
-  if (e && e[0] == '0') return 0;
+  if (opt_off(OPT_RAW_SEL_TOP)) return 0;   // option RAW_SEL_TOP = 0: the per-point kernels
   const int need = raw_top_need(fn, k_max, 32);
   return need <= 16 ? 16 : need <= 32 ? 32 : 0;
 }
@@ -3220,8 +2738,7 @@ hipError_t launch_raw_sel(const RawParams& p, int64_t k_max, hipStream_t s) {
     else hipLaunchKernelGGL(k_raw_sel_top<32>, grid, block, 0, s, p);
     return hipGetLastError();
   }
-  const char* renv = std::getenv("TSDBHIP_RAW_SEL_REG");   // A/B: 0 = the LDS-staged kernel
-  if (k_max <= 64 * 32 && !(renv && renv[0] == '0')) {
+  if (k_max <= 64 * 32 && !opt_off(OPT_RAW_SEL_REG)) {   // option RAW_SEL_REG = 0: the LDS-staged kernel
     const dim3 grid((unsigned)((p.n_strips * RAW_STRIP + SELW - 1) / SELW)), block(64 * SELW);
     if (k_max <= 64 * 8) hipLaunchKernelGGL(k_raw_sel_reg<8>, grid, block, 0, s, p);
     else if (k_max <= 64 * 16) hipLaunchKernelGGL(k_raw_sel_reg<16>, grid, block, 0, s, p);

@@ -34,8 +34,14 @@ EXPORTS = [
     "tsdbhip_hist_run_range", "tsdbhip_hist_result_free", "tsdbhip_expr_map", "tsdbhip_expr_zip", "tsdbhip_expr_topn",
     "tsdbhip_batch_range_sizes", "tsdbhip_batch_download_range", "tsdbhip_expr_sync", "tsdbhip_init_devices",
     "tsdbhip_md_shard_mode", "tsdbhip_md_info", "tsdbhip_host_alloc", "tsdbhip_host_free", "tsdbhip_md_stats",
-    "tsdbhip_device_count",
+    "tsdbhip_device_count", "tsdbhip_set_option", "tsdbhip_get_option",
 ]
+
+# developer options (tsdbhip_set_option, opentsdb_amd/csrc/opts.h)
+OPTIONS = ["FAST", "SHORT", "ROWS", "HWIN", "SEQ", "SEQ_ROWS", "SEQ_WAVE", "INDEX_GENERIC", "CMP_CHUNK", "CMP_ROWS",
+           "CMP_ONEPASS", "PCT_ROWS", "PCT_KEYS", "PCT_VONLY", "PCT_V6", "SEL_FUSED", "SEL_COLS", "SEL_WIN", "SEL_WAVE",
+           "SEL_REG", "SELOPS", "RAW_LERPW", "RAW_SEL_TOP", "RAW_SEL_REG", "RO_FUSE", "MULTI_FUSE", "HIST_WINDOW",
+           "HIST_WS", "HIST_LAYOUT", "TRACE", "DBG"]
 
 SHARD_AUTO, SHARD_SERIES, SHARD_GROUPS, SHARD_SPANS = -1, 0, 1, 2   # tsdbhip.h TSDB_SHARD_*
 MD_AUTO, MD_COPY, MD_RCCL = -1, 0, 1                               # tsdbhip.h TSDB_MD_*
@@ -101,6 +107,8 @@ def lib():
         L.tsdbhip_md_shard_mode.argtypes = [vp, C.c_int]
         L.tsdbhip_md_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_void_p]
         L.tsdbhip_device_count.argtypes = [C.POINTER(C.c_int)]
+        L.tsdbhip_set_option.argtypes = [C.c_char_p, C.c_int64]
+        L.tsdbhip_get_option.argtypes = [C.c_char_p, C.POINTER(C.c_int64)]
         L.tsdbhip_md_stats.argtypes = [vp, C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double)]
         L.tsdbhip_destroy.argtypes = [vp]
         L.tsdbhip_host_alloc.argtypes = [C.c_uint64, C.POINTER(vp)]
@@ -166,6 +174,40 @@ def device_count() -> int:
     n = C.c_int()
     _check(lib().tsdbhip_device_count(C.byref(n)))
     return n.value
+
+
+def set_option(name: str, value) -> None:
+    """tsdbhip_set_option: a developer option (kernel choice for tests / A/B runs), process-wide;
+    None or -1 resets it to the production choice."""
+    _check(lib().tsdbhip_set_option(name.encode(), -1 if value is None else int(value)))
+
+
+def get_option(name: str) -> int:
+    v = C.c_int64()
+    _check(lib().tsdbhip_get_option(name.encode(), C.byref(v)))
+    return v.value
+
+
+def reset_options() -> None:
+    for n in OPTIONS:
+        set_option(n, -1)
+
+
+class options:
+    """Context manager: developer options set for the block, reset after it."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            set_option(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k in self.kw:
+            set_option(k, -1)
+        return False
 
 
 def parse_downsample(spec: str) -> abi.Query:

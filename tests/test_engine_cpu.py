@@ -31,7 +31,7 @@ def test_library_exports_every_header_symbol():
 
 
 def test_abi_version():
-    assert engine.lib().tsdbhip_abi_version() == 11
+    assert engine.lib().tsdbhip_abi_version() == 12
 
 
 def test_multi_device_context_argument_checks():

@@ -21,6 +21,7 @@ import numpy as np
 import pytest
 
 from opentsdb_amd import abi
+from opentsdb_amd.engine import get_option, set_option
 from opentsdb_amd.engine import EngineError
 from opentsdb_amd.store import make_batch
 from oracle import oracle as O
@@ -402,7 +403,7 @@ def _random_scan(seed, n_series=40, salt=False):
 @pytest.mark.parametrize("chunk", [1, 97, 2000])
 def test_chunked_compaction_equals_one_pass(eng, seed, salt, chunk):
     """A scan over the 2^31-datapoint chunk limit is compacted in chunks of whole rows (two passes:
-    sizes, then entries + writes at the host's layout).  TSDBHIP_CMP_CHUNK lowers the limit so
+    sizes, then entries + writes at the host's layout).  option CMP_CHUNK  lowers the limit so
     small scans take that path: the resident batch, the lazily raised errors and the query results
     equal the one-pass compaction's."""
     series, groups = _random_scan(seed, salt=salt)
@@ -419,11 +420,11 @@ def test_chunked_compaction_equals_one_pass(eng, seed, salt, chunk):
             qs.append((q, agg, eng.run(q)))
         except EngineError as e:
             qs.append((q, agg, e.code))
-    os.environ["TSDBHIP_CMP_CHUNK"] = str(chunk)
+    set_option("CMP_CHUNK", chunk)
     try:
         eng.load_cells(cb)
     finally:
-        del os.environ["TSDBHIP_CMP_CHUNK"]
+        set_option("CMP_CHUNK", None)
     got = eng.download()
     assert rows_of(got) == rows_of(want)
     assert np.array_equal(got.group_id, want.group_id)
@@ -436,17 +437,14 @@ def test_chunked_compaction_equals_one_pass(eng, seed, salt, chunk):
             assert_groups_match(eng.run(q), w, agg, tol=0.0, ctx=f"chunk {chunk} {agg}")
 
 
-def _load_with_env(eng, cb, **env):
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update({k: str(v) for k, v in env.items()})
+def _load_with_opts(eng, cb, **opts):
+    for k, v in opts.items():
+        set_option(k, v)
     try:
         eng.load_cells(cb)
     finally:
-        for k, v in old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
+        for k in opts:
+            set_option(k, None)
     return eng.download()
 
 
@@ -468,15 +466,15 @@ def _queries_and_answers(eng):
 def test_row_lds_path_equals_global_sort(eng, seed, salt, fix):
     """The per-row LDS compaction -- one pass (k_cmp_rowone: explode, sort, dedup and the cell
     written into the region the host laid out from k_cmp_cols' bounds), and the sizing + write
-    passes (k_cmp_row / k_cmp_rowwrite, TSDBHIP_CMP_ONEPASS=0, and in chunks) -- against the
-    global-sort pipeline (TSDBHIP_CMP_ROWS=0): the same resident rows, the same lazily raised
+    passes (k_cmp_row / k_cmp_rowwrite, option CMP_ONEPASS = 0, and in chunks) -- against the
+    global-sort pipeline (option CMP_ROWS = 0): the same resident rows, the same lazily raised
     errors, the same query answers."""
     series, groups = _random_scan(seed, salt=salt)
     cb = abi.HostCellBatch.from_rows(series, groups, fix)
-    want = _load_with_env(eng, cb, TSDBHIP_CMP_ROWS=0)
+    want = _load_with_opts(eng, cb, CMP_ROWS=0)
     answers = _queries_and_answers(eng)
-    for env in ({}, {"TSDBHIP_CMP_ONEPASS": 0}, {"TSDBHIP_CMP_CHUNK": 150}):
-        got = _load_with_env(eng, cb, **env)
+    for env in ({}, {"CMP_ONEPASS": 0}, {"CMP_CHUNK": 150}):
+        got = _load_with_opts(eng, cb, **env)
         assert rows_of(got) == rows_of(want), env
         assert np.array_equal(got.group_id, want.group_id)
         for q, agg, w in answers:
@@ -498,7 +496,7 @@ def test_row_over_lds_capacity_takes_global_sort(eng):
     row = [(cols[j][0], cols[j][1], int(k)) for k, j in enumerate(order)]
     small = [(B + 3600, random_row(rng, 40))]
     cb = abi.HostCellBatch.from_rows([[(B, row)], small], [0, 1], True)
-    got = _load_with_env(eng, cb)
+    got = _load_with_opts(eng, cb)
     want = O.compact_row([(q, v) for q, v, _ in row], True, [t for _, _, t in row])
     assert rows_of(got)[0] == (B, want[0], want[1])
 
@@ -515,13 +513,13 @@ def test_decreasing_column_offsets_rejected(eng, chunk):
     bad = abi.HostCellBatch(cb.series_row_ptr, cb.row_base_time, cb.row_col_ptr, qo, cb.col_val_off, cb.qual,
                             cb.val, cb.group_id, cb.col_timestamp, True)
     if chunk:
-        os.environ["TSDBHIP_CMP_CHUNK"] = str(chunk)
+        set_option("CMP_CHUNK", chunk)
     try:
         with pytest.raises(EngineError) as ei:
             eng.load_cells(bad)
         assert ei.value.code == abi.TSDB_E_ILLEGAL_ARGUMENT
     finally:
-        os.environ.pop("TSDBHIP_CMP_CHUNK", None)
+        set_option("CMP_CHUNK", None)
 
 
 def _single_second_rows(rng, n_rows, dup_row=None, fix_rows=()):
@@ -558,9 +556,9 @@ def test_single_cell_fast_path(eng, fix):
     rng = np.random.default_rng(31)
     rows = _single_second_rows(rng, 6, dup_row=2, fix_rows=(1, 4))
     cb = abi.HostCellBatch.from_rows([rows], [0], fix)
-    want = _load_with_env(eng, cb, TSDBHIP_CMP_ROWS=0)
-    got = _load_with_env(eng, cb)
-    two = _load_with_env(eng, cb, TSDBHIP_CMP_ONEPASS=0)
+    want = _load_with_opts(eng, cb, CMP_ROWS=0)
+    got = _load_with_opts(eng, cb)
+    two = _load_with_opts(eng, cb, CMP_ONEPASS=0)
     assert rows_of(got) == rows_of(want)
     assert rows_of(two) == rows_of(want)
     for (base, cells), (gb, gq, gv) in zip(rows, rows_of(got)):

@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 
 from opentsdb_amd import abi, synth
+from opentsdb_amd.engine import get_option, set_option
 from oracle import oracle as O
 from tests.test_gpu_parity import assert_groups_match, T0
 
@@ -31,16 +32,13 @@ def eng():
 
 
 def run_path(eng, batch, q, fast: bool):
-    old = os.environ.get("TSDBHIP_FAST")
-    os.environ["TSDBHIP_FAST"] = "1" if fast else "0"
+    old = get_option("FAST")
+    set_option("FAST", 1 if fast else 0)
     try:
         got = eng.run_batch(batch, q) if batch is not None else eng.run(q)
         return got, eng.timing()
     finally:
-        if old is None:
-            del os.environ["TSDBHIP_FAST"]
-        else:
-            os.environ["TSDBHIP_FAST"] = old
+        set_option("FAST", old)
 
 
 def assert_bit_equal(a, b, ctx):
@@ -144,7 +142,7 @@ def test_fast_float64_certified(eng):
 def test_fast_float64_certificate_fails(eng, monkeypatch):
     """Full-mantissa doubles: the certificate fails, every tile is redone sequentially (k_grid; the
     one-pass k_seq_dense route is switched off here, see test_float64_sequential_sums)."""
-    monkeypatch.setenv("TSDBHIP_SEQ", "0")
+    set_option("SEQ", "0")
     b = synth.generate(96, T0, 3600, 1000, value_kind=4, n_groups=4, seed=9)
     q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
     check(eng, b, q, "sum", "f64 uncertified", expect_redo=True)
@@ -240,15 +238,12 @@ def test_fast_multi_row_series_window_refill(eng):
 
 
 def run_short(eng, batch, q, short: bool):
-    old = os.environ.get("TSDBHIP_SHORT")
-    os.environ["TSDBHIP_SHORT"] = "1" if short else "0"
+    old = get_option("SHORT")
+    set_option("SHORT", 1 if short else 0)
     try:
         return run_path(eng, batch, q, True)
     finally:
-        if old is None:
-            del os.environ["TSDBHIP_SHORT"]
-        else:
-            os.environ["TSDBHIP_SHORT"] = old
+        set_option("SHORT", old)
 
 
 @pytest.mark.parametrize("agg,ds", [("sum", "avg"), ("avg", "sum"), ("dev", "avg"), ("min", "max"), ("max", "min"),
@@ -290,23 +285,23 @@ def test_short_kernel_mixed_row_counts(eng):
                                         ("sum", 1000, 1799), ("avg", 60000, 3 * 3600 - 1)])
 @pytest.mark.parametrize("seqwave", ["1", "0"])
 def test_float64_sequential_sums(eng, monkeypatch, seqwave, ds, iv, span):
-    """k_seq_wave (one wave a series, K <= 64) and k_seq_dense (TSDBHIP_SEQ_WAVE=0).  Full-mantissa doubles over three hour rows: the rows carry ROW_NOCERT (two of their values
+    """k_seq_wave (one wave a series, K <= 64) and k_seq_dense (option SEQ_WAVE = 0).  Full-mantissa doubles over three hour rows: the rows carry ROW_NOCERT (two of their values
     cannot add exactly).  Sum / avg downsampling then runs k_seq_dense (each bucket in Java's
     order, one pass, then the group-by step over the stored buckets); with it switched off the
     streaming kernels hand the tiles to k_grid, which sums them in order in one pass (slow_chunk).
     Both equal the general path bit for bit and the oracle -- buckets inside a row, across rows
     (7m), one a day and one a datapoint; squareSum keeps the certificate check at series end."""
-    monkeypatch.setenv("TSDBHIP_SEQ_WAVE", seqwave)
+    set_option("SEQ_WAVE", seqwave)
     b = synth.generate(70, T0, 3 * 3600, 1000, value_kind=4, n_groups=3, seed=17)
     for agg in ("sum", "max", "none"):
         q = abi.new_query(T0, T0 + span, agg, ds_function=abi.AGG[ds], ds_interval_ms=iv)
         seq, ts = run_path(eng, b, q, True)
         gen, _ = run_path(eng, b, q, False)
-        os.environ["TSDBHIP_SEQ"] = "0"
+        set_option("SEQ", 0)
         try:
             grid, _ = run_path(eng, b, q, True)
         finally:
-            del os.environ["TSDBHIP_SEQ"]
+            set_option("SEQ", None)
         if ds in ("sum", "avg"):
             assert ts.fast_ms == 0, "k_seq_dense expected (no streaming pass)"
         ctx = f"f64 seq {ds} {iv} {agg}"
@@ -317,10 +312,10 @@ def test_float64_sequential_sums(eng, monkeypatch, seqwave, ds, iv, span):
 
 @pytest.mark.parametrize("seqwave", ["1", "0"])
 def test_float64_sequential_sums_mixed_rows(eng, monkeypatch, seqwave):
-    """Both sequential kernels (TSDBHIP_SEQ_WAVE).  k_seq_dense over a scan mixing full-mantissa doubles (ROW_NOCERT), vle integers and
+    """Both sequential kernels (option SEQ_WAVE).  k_seq_dense over a scan mixing full-mantissa doubles (ROW_NOCERT), vle integers and
     millisecond rows: the non-uniform rows are walked datapoint by datapoint (width from the
     qualifier, length from its flags); bit-exact against the general path and the oracle."""
-    monkeypatch.setenv("TSDBHIP_SEQ_WAVE", seqwave)
+    set_option("SEQ_WAVE", seqwave)
     from tests.test_gpu_calendar_tz import merge
     b = merge(synth.generate(20, T0, 7200, 1000, value_kind=4, n_groups=3, seed=5),
               synth.generate(20, T0, 7200, 1000, value_kind=1, n_groups=3, int_mod=70000, seed=6),
@@ -348,11 +343,11 @@ def test_tiny_rows_at_scale_sequential(eng, tiny_rows, ds):
     b = tiny_rows
     q = abi.new_query(T0, T0 + 3599, "sum", ds_function=abi.AGG[ds], ds_interval_ms=900000)
     seq, ts = run_path(eng, b, q, True)
-    os.environ["TSDBHIP_SEQ"] = "0"
+    set_option("SEQ", 0)
     try:
         other, _ = run_path(eng, b, q, True)
     finally:
-        del os.environ["TSDBHIP_SEQ"]
+        set_option("SEQ", None)
     assert ts.fast_ms == 0, "k_seq_dense expected"
     assert_bit_equal(seq, other, f"tiny {ds}")
     assert_groups_match(seq, O.run_query(b, q), "sum", ctx=f"tiny {ds}")
@@ -393,13 +388,13 @@ def _short_rows_with_breaks():
                                    ("sum", 420000), ("avg", 86400000)])
 def test_sequential_rows_kernel(eng, monkeypatch, ds, iv):
     """k_seq_rows (one thread a short hour row, Java's order inside each bucket) against
-    k_seq_dense (TSDBHIP_SEQ_ROWS=0) bit for bit and the oracle, including the series it hands
+    k_seq_dense (option SEQ_ROWS = 0) bit for bit and the oracle, including the series it hands
     back (a row past its hour, two cells of one hour, mixed value kinds) and intervals it does not
     take (7m buckets crossing rows, 1d)."""
     b = _short_rows_with_breaks()
     res = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("TSDBHIP_SEQ_ROWS", mode)
+        set_option("SEQ_ROWS", mode)
         for agg in ("sum", "none"):
             q = abi.new_query(T0, T0 + 86399, agg, ds_function=abi.AGG[ds], ds_interval_ms=iv)
             got, tm = run_path(eng, b, q, True)
@@ -410,11 +405,11 @@ def test_sequential_rows_kernel(eng, monkeypatch, ds, iv):
 
 
 def run_rows(eng, batch, q, rows: bool, monkeypatch):
-    monkeypatch.setenv("TSDBHIP_ROWS", "1" if rows else "0")
+    set_option("ROWS", "1" if rows else "0")
     try:
         return run_path(eng, batch, q, True)
     finally:
-        monkeypatch.delenv("TSDBHIP_ROWS")
+        set_option("ROWS", None)
 
 
 @pytest.mark.parametrize("agg,ds,iv,win,rate", [
@@ -428,10 +423,10 @@ def run_rows(eng, batch, q, rows: bool, monkeypatch):
 ])
 def test_rows_kernel_matches_walker(eng, monkeypatch, agg, ds, iv, win, rate):
     """k_rows (series of several one-chunk rows, descriptors in 64-row batches) against k_fast's
-    row walker (TSDBHIP_ROWS=0) and k_grid, bit for bit: 40000 series of 24 hour rows (4 series a
+    row walker (option ROWS = 0) and k_grid, bit for bit: 40000 series of 24 hour rows (4 series a
     tile, 96 rows: the batch refill), int and float series (two row classes).  (k_hwin off: the
     1m case runs the dense split; its buckets are one datapoint in 100 s, LERP fills between.)"""
-    monkeypatch.setenv("TSDBHIP_HWIN", "0")
+    set_option("HWIN", "0")
     eng.synth(40000, T0, 24 * 36, 100000, 2, 1000, 30000, 0x5EED)
     q = abi.new_query(T0 + win[0], T0 + win[1], agg, ds_function=abi.AGG[ds], ds_interval_ms=iv, rate=rate)
     r, tr = run_rows(eng, None, q, True, monkeypatch)
@@ -483,11 +478,11 @@ def test_rows_kernel_irregular(eng, monkeypatch):
 
 
 def run_hwin(eng, batch, q, on: bool, monkeypatch):
-    monkeypatch.setenv("TSDBHIP_HWIN", "1" if on else "0")
+    set_option("HWIN", "1" if on else "0")
     try:
         return run_path(eng, batch, q, True)
     finally:
-        monkeypatch.delenv("TSDBHIP_HWIN")
+        set_option("HWIN", None)
 
 
 @pytest.mark.parametrize("agg,ds,iv,win,fill", [
@@ -501,7 +496,7 @@ def run_hwin(eng, batch, q, on: bool, monkeypatch):
 ])
 def test_hwin_matches_dense_split(eng, monkeypatch, agg, ds, iv, win, fill):
     """k_hwin (K > 64 buckets tiling the hour, walked window by window with register partials; the
-    queries whose one-pass slot LDS does not fit, K >= 859) against the dense split (TSDBHIP_HWIN=0: buckets stored, then k_emit_win) and the general
+    queries whose one-pass slot LDS does not fit, K >= 859) against the dense split (option HWIN = 0: buckets stored, then k_emit_win) and the general
     kernel, bit for bit: 40000 series x a day of 10 s points (24 hour rows), int and float series."""
     eng.synth(40000, T0, 24 * 360, 10000, 2, 1000, 30000, 0x5EED)
     q = abi.new_query(T0 + win[0], T0 + win[1], agg, ds_function=abi.AGG[ds], ds_interval_ms=iv, ds_fill=fill)

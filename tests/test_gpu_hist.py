@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 from opentsdb_amd import abi
+from opentsdb_amd.engine import get_option, set_option
 from opentsdb_amd import histogram as H
 from opentsdb_amd.engine import Engine, EngineError
 from oracle import oracle as O
@@ -254,27 +255,26 @@ def test_gpu_repeated_bucket_keys_last_count_wins(eng):
         run_both(eng, hb, U.query(T0, T0 + 2 * 3600, "sum", ds), [50.0, 90.0, 10.0], True)
 
 
-@pytest.mark.parametrize("env", [{"TSDBHIP_HIST_WINDOW": "0"}, {"TSDBHIP_HIST_WS": "1"}, {"TSDBHIP_HIST_WS": "5"},
-                                 {"TSDBHIP_HIST_WS": "64"}, {"TSDBHIP_HIST_PIPE": "0"}, {"TSDBHIP_HIST_LAYOUT": "0"},
-                                 {"TSDBHIP_HIST_SU": "16"}],
-                         ids=["atomic-kernel", "ws1", "ws5", "ws64", "unpipelined", "keyed", "su16"])
+@pytest.mark.parametrize("env", [{"HIST_WINDOW": 0}, {"HIST_WS": 1}, {"HIST_WS": 5}, {"HIST_WS": 64},
+                                 {"HIST_LAYOUT": 0}],
+                         ids=["atomic-kernel", "ws1", "ws5", "ws64", "keyed"])
 def test_gpu_accum_window_sizes(eng, env):
     """k_hist_accw keeps a window of consecutive points' counters in LDS; tiles whose points leave
     it flush it, points past its end add to the global counters directly.  Windows of 1, 5 and 64
-    points, the unpipelined loop, every bucket through the keyed lookup (no layout table) and the
-    per-column atomic kernel give the oracle's answers, raw unions included."""
-    import os
+    points, every bucket through the keyed lookup (no layout table) and the per-column atomic
+    kernel give the oracle's answers, raw unions included (developer options)."""
     rng = np.random.default_rng(77)
     hb = U.random_store(rng, n_series=40, n_rows=2, period_ms=5000, groups=5, layouts=4, nb=(10, 16),
                         sparse=0.1, ms_frac=0.2)
-    os.environ.update(env)
+    for k, v in env.items():
+        set_option(k, v)
     try:
         for agg, ds, b in (("sum", "1m-sum", True), ("sum", None, True), ("none", "2m-sum", False),
                            ("p99", "30s-sum", False), ("sum", "0all-sum", True)):
             run_both(eng, hb, U.query(T0 + 100, T0 + 2 * 3600 - 50, agg, ds), [50.0, 95.0, 99.9], b)
     finally:
         for k in env:
-            del os.environ[k]
+            set_option(k, None)
 
 
 T_DST = 1457740800   # 2016-03-12 00:00 UTC: America/Denver enters daylight time on Mar 13

@@ -7,6 +7,7 @@ from __future__ import annotations
 import pytest
 
 from opentsdb_amd import abi, synth
+from opentsdb_amd.engine import get_option, set_option
 from oracle import oracle as O
 from tests.test_gpu_parity import assert_groups_match
 
@@ -79,16 +80,11 @@ FUSABLE = ["sum", "avg", "min", "max", "count", "dev"]
 
 def run_separate(eng, qs):
     """The same queries with the fused pass switched off (one streaming pass per query)."""
-    import os
-    old = os.environ.get("TSDBHIP_MULTI_FUSE")
-    os.environ["TSDBHIP_MULTI_FUSE"] = "0"
+    set_option("MULTI_FUSE", 0)
     try:
         return eng.run_multi(qs)
     finally:
-        if old is None:
-            del os.environ["TSDBHIP_MULTI_FUSE"]
-        else:
-            os.environ["TSDBHIP_MULTI_FUSE"] = old
+        set_option("MULTI_FUSE", None)
 
 
 def sparse_batch(seed, n_series=240, n_groups=5, span_s=3600, period_s=10):

@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 from opentsdb_amd import abi, synth
+from opentsdb_amd.engine import set_option
 from oracle import oracle as O
 from tests.test_gpu_parity import assert_groups_match
 
@@ -229,13 +230,13 @@ def _vonly_batch(seed=23):
 def test_pct_values_only_key_rows(eng, fn, monkeypatch):
     """k_pct_rows' values-only key kernel (rows certified at load read 4 B a datapoint, one
     qualifier a row; 6 values a lane when no row exceeds 384, else 8) against the oracle, and
-    bit-identical to the qualifier-reading key kernel (TSDBHIP_PCT_VONLY=0)."""
+    bit-identical to the qualifier-reading key kernel (option PCT_VONLY = 0)."""
     b = _vonly_batch()
     res = {}
-    modes = [("1", "1"), ("1", "0"), ("0", "1")]   # (TSDBHIP_PCT_VONLY, TSDBHIP_PCT_V6)
+    modes = [("1", "1"), ("1", "0"), ("0", "1")]   # (option PCT_VONLY, option PCT_V6)
     for vonly, v6 in modes:
-        monkeypatch.setenv("TSDBHIP_PCT_VONLY", vonly)
-        monkeypatch.setenv("TSDBHIP_PCT_V6", v6)
+        set_option("PCT_VONLY", vonly)
+        set_option("PCT_V6", v6)
         for agg in ["max", "min", "none"]:
             q = abi.new_query(T0, T0 + 3 * 3600 - 1, agg, ds_function=abi.AGG[fn], ds_interval_ms=3600000)
             got = eng.run_batch(b, q)

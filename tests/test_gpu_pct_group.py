@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 from opentsdb_amd import abi, synth
+from opentsdb_amd.engine import set_option
 from opentsdb_amd.query import TsdbQuery
 from oracle import oracle as O
 from tests.test_gpu_parity import assert_groups_match
@@ -59,7 +60,7 @@ def test_pct_group_single_group_many_series(eng):
 @pytest.mark.parametrize("win", ["1", "2"])   # (2: the sampled window for any group size)
 @pytest.mark.parametrize("fill", [abi.FILL_NAN, abi.FILL_ZERO, abi.FILL_NULL])
 def test_pct_group_fill(eng, monkeypatch, fill, win):
-    monkeypatch.setenv("TSDBHIP_SEL_WIN", win)
+    set_option("SEL_WIN", win)
     b = synth.generate(20, T0 + 1800, 200, 10000, value_kind=2, n_groups=2, int_mod=1000, seed=4)
     q = abi.new_query(T0, T0 + 7199, "p90", ds_function=abi.AGG["avg"], ds_interval_ms=300000, ds_fill=fill)
     assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "p90", tol=0.0, ctx=f"fill {fill}")
@@ -80,9 +81,9 @@ def test_pct_group_all(eng, mixed_batch):
 
 @pytest.mark.parametrize("win", ["1", "2"])
 def test_pct_group_sparse_lerp(eng, monkeypatch, win):
-    """Series with missing buckets and different extents: LERP-interpolated members (TSDBHIP_SEL_WIN=2:
+    """Series with missing buckets and different extents: LERP-interpolated members (option SEL_WIN = 2:
     through the sampled window where the batch qualifies)."""
-    monkeypatch.setenv("TSDBHIP_SEL_WIN", win)
+    set_option("SEL_WIN", win)
     rng = np.random.default_rng(17)
     from opentsdb_amd.store import MockStore
     st = MockStore()
@@ -106,8 +107,8 @@ def test_pct_group_sparse_lerp(eng, monkeypatch, win):
 @pytest.mark.parametrize("win", ["1", "2"])
 def test_pct_group_nan_members(eng, monkeypatch, win):
     """Buckets of NaNs (present, value NaN) are dropped by runDouble; a slot whose members
-    are all NaN yields NaN (TSDBHIP_SEL_WIN=2: also through the sampled window)."""
-    monkeypatch.setenv("TSDBHIP_SEL_WIN", win)
+    are all NaN yields NaN (option SEL_WIN = 2: also through the sampled window)."""
+    set_option("SEL_WIN", win)
     rng = np.random.default_rng(5)
     rows, gids = [], []
     for s in range(12):
@@ -138,9 +139,9 @@ def test_pct_group_segment_beyond_lds(eng):
 @pytest.mark.parametrize("cols", ["0", "1"])
 def test_pct_group_column_layout(eng, mixed_batch, monkeypatch, cols):
     """The fused percentile pass writes each (group, slot) column contiguously (sel_cols) or one
-    row per series (TSDBHIP_SEL_COLS=0): both feed the same select and match the oracle, incl.
+    row per series (option SEL_COLS = 0): both feed the same select and match the oracle, incl.
     a single group wider than a wave and the LDS-staged select."""
-    monkeypatch.setenv("TSDBHIP_SEL_COLS", cols)
+    set_option("SEL_COLS", cols)
     for agg in ["p99", "median", "ep99r7"]:
         q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["avg"], ds_interval_ms=60000)
         assert_groups_match(eng.run_batch(mixed_batch, q), O.run_query(mixed_batch, q), agg, tol=0.0, ctx=agg)
@@ -149,18 +150,16 @@ def test_pct_group_column_layout(eng, mixed_batch, monkeypatch, cols):
     assert_groups_match(eng.run_batch(b, q), O.run_query(b, q), "p50", tol=0.0, ctx="one group")
 
 
-@pytest.mark.parametrize("variant", [{}, {"TSDBHIP_SEL_T": "1024"}, {"TSDBHIP_SEL_T": "256"},
-                                     {"TSDBHIP_SEL_HL": "1"}, {"TSDBHIP_SEL_HL": "1", "TSDBHIP_SEL_COLS": "0"}])
-def test_pct_group_select_kernels(eng, monkeypatch, variant):
-    """The register-resident select's block shapes (512 x 24 keys, 1024 x 12, 256 x 48) and the
-    upper-word variant (k_sel_hl: 32-bit keys of the upper words, the rank resolved by the lower
-    words of the values sharing the selected one) against the oracle: segments of a few values,
-    ~3000 values with clustered integers (ties in the upper and the lower words: several radix
-    digits, the lower-word passes), negative rates, members without a value, both layouts."""
+@pytest.mark.parametrize("variant", [{}, {"SEL_WAVE": 0}, {"SEL_WAVE": 0, "SEL_COLS": 0}, {"SEL_REG": 0, "SEL_WAVE": 0}])
+def test_pct_group_select_kernels(eng, variant):
+    """The select kernels -- k_sel_wave (columns of <= 2048 values), the register-resident block
+    select k_sel_reg (512 x 24 keys) and the LDS k_sel_seg -- against the oracle: segments of a
+    few values, ~3000 values with clustered integers (ties: several radix digits), negative
+    rates, members without a value, both layouts."""
     for k, v in variant.items():
-        monkeypatch.setenv(k, v)
+        set_option(k, v)
     if variant:   # (the block kernels also for the small segments k_sel_wave takes by default)
-        monkeypatch.setenv("TSDBHIP_SEL_WAVE", "0")
+        set_option("SEL_WAVE", "0")
     mixed = synth.generate(70, T0, 720, 5000, value_kind=2, n_groups=3, int_mod=30000, seed=11)
     ties = synth.generate(3000, T0, 360, 10000, value_kind=1, n_groups=1, int_mod=7, seed=5)
     for b, ds, rate in ((mixed, "avg", False), (ties, "max", False), (ties, "avg", False), (ties, "avg", True)):
@@ -176,7 +175,7 @@ def test_pct_group_wave_select(eng, monkeypatch, n, kind):
     """k_sel_wave (a wave a column, columns of at most 64 x 4 / 16 / 32 values; 2049 takes the
     block kernel) against the oracle at each size class's edge, with clustered integers (long
     runs of equal keys) or mixed integer / float spans (empty slots past the data's end), both
-    layouts, and TSDBHIP_SEL_WAVE=0 alike.  (Members without a value: the NaN-member and sparse
+    layouts, and option SEL_WAVE = 0 alike.  (Members without a value: the NaN-member and sparse
     LERP tests above, whose groups are small, so they take k_sel_wave.)"""
     if kind == "ties":
         eng.synth(n, T0 + 60, 300, 20000, 1, 1, 7, 0x60 + n)
@@ -184,9 +183,9 @@ def test_pct_group_wave_select(eng, monkeypatch, n, kind):
         eng.synth(n, T0 + 60, 300, 20000, 2, 1, 30000, 0x61 + n)
     b = eng.download()
     for wave in ["1", "0"]:
-        monkeypatch.setenv("TSDBHIP_SEL_WAVE", wave)
+        set_option("SEL_WAVE", wave)
         for cols in ["1", "0"]:
-            monkeypatch.setenv("TSDBHIP_SEL_COLS", cols)
+            set_option("SEL_COLS", cols)
             for agg in ["p999", "p99", "median", "p50", "ep90r7"]:
                 q = abi.new_query(T0, T0 + 7199, agg, ds_function=abi.AGG["avg"], ds_interval_ms=300000)
                 assert_groups_match(eng.run(q), O.run_query(b, q, threads=8), agg, tol=0.0,
@@ -206,18 +205,18 @@ def test_pct_group_sampled_window(eng, monkeypatch):
         assert_groups_match(eng.run(q), O.run_query(b, q, threads=8), agg, tol=0.0, ctx=f"window {agg}")
     r1 = eng.debug_sel_window()
     assert (r1[0] - r0[0], r1[1] - r0[1]) == (3, 0), f"window runs / misses {r0} -> {r1}"
-    # mid ranks keep the full path; TSDBHIP_SEL_WIN=2 takes the window for them too
+    # mid ranks keep the full path; option SEL_WIN = 2 takes the window for them too
     q = abi.new_query(T0, T0 + 3599, "median", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
     assert_groups_match(eng.run(q), O.run_query(b, q, threads=8), "median", tol=0.0, ctx="median full path")
     assert eng.debug_sel_window()[0] == r1[0]
-    monkeypatch.setenv("TSDBHIP_SEL_WIN", "2")   # (windows wider than a column holds: they fall back)
+    set_option("SEL_WIN", "2")   # (windows wider than a column holds: they fall back)
     for agg in ["median", "p75", "p95"]:
         q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["avg"], ds_interval_ms=60000)
         assert_groups_match(eng.run(q), O.run_query(b, q, threads=8), agg, tol=0.0, ctx=f"window {agg}")
     r2 = eng.debug_sel_window()
     assert r2[0] - r1[0] == 3, f"window runs {r1} -> {r2}"
-    # TSDBHIP_SEL_WIN=0: the full path, the same results
-    monkeypatch.setenv("TSDBHIP_SEL_WIN", "0")
+    # option SEL_WIN = 0: the full path, the same results
+    set_option("SEL_WIN", "0")
     q = abi.new_query(T0, T0 + 3599, "p99", ds_function=abi.AGG["avg"], ds_interval_ms=60000)
     assert_groups_match(eng.run(q), O.run_query(b, q, threads=8), "p99", tol=0.0, ctx="full path")
     assert eng.debug_sel_window()[0] == r2[0]
@@ -226,7 +225,7 @@ def test_pct_group_sampled_window(eng, monkeypatch):
 @pytest.mark.parametrize("kind", ["ties", "small"])
 def test_pct_group_sampled_window_fallback(eng, monkeypatch, kind):
     """Windows that miss (a few distinct values tie across the window: more kept values than a
-    (tile, slot) holds) and small groups forced through the window (TSDBHIP_SEL_WIN=2, sparse
+    (tile, slot) holds) and small groups forced through the window (option SEL_WIN = 2, sparse
     samples): the query falls back to the full path where a column misses -- the oracle's answers
     either way."""
     if kind == "ties":
@@ -237,7 +236,7 @@ def test_pct_group_sampled_window_fallback(eng, monkeypatch, kind):
     # (also the full path: ties of more than 256 equal keys resolved to the last bit, a round-5 fix
     # of the 12-bit first digit -- these keys' low 3 bits were left unresolved)
     for win in ["2", "0"]:
-        monkeypatch.setenv("TSDBHIP_SEL_WIN", win)
+        set_option("SEL_WIN", win)
         for agg in ["p99", "median", "p50"]:
             for ds in ["avg", "max"]:
                 q = abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG[ds], ds_interval_ms=60000)

@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 from opentsdb_amd import abi, synth
+from opentsdb_amd.engine import set_option
 from oracle import oracle as O
 from tests.test_gpu_parity import assert_groups_match
 from tests.test_gpu_raw import random_batch
@@ -111,8 +112,8 @@ def test_raw_pct_group_beyond_lds(eng, kind):
 @pytest.mark.parametrize("ops", ["1", "70000"])
 def test_raw_pct_strip_batches(eng, ops, monkeypatch):
     """Operands are staged per strip (RAW_STRIP points x the group's spans) in batches of at
-    most TSDBHIP_SELOPS operands: one strip per batch, and several strips per batch."""
-    monkeypatch.setenv("TSDBHIP_SELOPS", ops)
+    most option SELOPS  operands: one strip per batch, and several strips per batch."""
+    set_option("SELOPS", ops)
     b = random_batch(7, n_series=60, n_groups=2, span_h=3)
     for agg in ["p95", "ep50r3", "median"]:
         q = abi.new_query(T0, T0 + 3 * 3600 - 1, agg)
@@ -123,9 +124,9 @@ def test_raw_pct_strip_batches(eng, ops, monkeypatch):
 @pytest.mark.parametrize("n_spans", [40, 700, 1600, 2000])
 def test_raw_pct_register_select(eng, monkeypatch, reg, n_spans):
     """k_raw_sel_reg (keys in registers, 8 / 16 / 26 / 32 a lane by group size) and the
-    LDS-staged k_raw_sel (TSDBHIP_RAW_SEL_REG=0) against the oracle: long points with absent
+    LDS-staged k_raw_sel (option RAW_SEL_REG = 0) against the oracle: long points with absent
     operands (spans not started or ended), double points with NaN members, ties."""
-    monkeypatch.setenv("TSDBHIP_RAW_SEL_REG", reg)
+    set_option("RAW_SEL_REG", reg)
     eng.synth(n_spans, T0, 4, 10000, 1, 1, 40, 0xA5 + n_spans)
     b = eng.download()
     for agg in ["p99", "median", "ep75r7"]:
@@ -143,9 +144,9 @@ def test_raw_pct_register_select(eng, monkeypatch, reg, n_spans):
 def test_raw_pct_top_select(eng, monkeypatch, top, n_spans):
     """k_raw_sel_top (lane = union point, the T largest keys streamed into registers; used when
     every requested rank lies within T of the top) against the oracle and against the per-point
-    kernels (TSDBHIP_RAW_SEL_TOP=0): long and double points, absent operands, NaN members, ties,
+    kernels (option RAW_SEL_TOP = 0): long and double points, absent operands, NaN members, ties,
     every estimation type, small groups for the median."""
-    monkeypatch.setenv("TSDBHIP_RAW_SEL_TOP", top)
+    set_option("RAW_SEL_TOP", top)
     eng.synth(n_spans, T0, 4, 10000, 1, 1, 25, 0x77 + n_spans)
     b = eng.download()
     for agg in ["p99", "p999", "ep99r3", "ep99r7", "p95", "median", "p50"]:

@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 from opentsdb_amd import abi, synth
+from opentsdb_amd.engine import set_option
 from oracle import oracle as O
 from tests.test_gpu_parity import assert_groups_match
 
@@ -153,9 +154,9 @@ def test_raw_spans_outside_scan_range(eng):
 @pytest.mark.parametrize("lerpw", ["0", "1"])
 def test_raw_strip_window_lerp(eng, monkeypatch, lerpw):
     """k_raw_eval's strip-wide long LERP (lerpw_*: reciprocal quotient + exact remainder) and the
-    general 64-bit path (TSDBHIP_RAW_LERPW=0) give the oracle's answer: counters, large-slope
+    general 64-bit path (option RAW_LERPW = 0) give the oracle's answer: counters, large-slope
     integers that leave the fast window (|dy| (x1 - x0) >= 2^51), negative slopes, mixed groups."""
-    monkeypatch.setenv("TSDBHIP_RAW_LERPW", lerpw)
+    set_option("RAW_LERPW", lerpw)
     b = synth.generate_counters(300, T0, 360, n_groups=16, seed=0xC4)
     for agg in ["sum", "avg", "min", "max", "dev"]:
         q = abi.new_query(T0, T0 + 3599, agg)

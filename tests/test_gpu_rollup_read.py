@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 
 from opentsdb_amd import abi, engine
+from opentsdb_amd.engine import set_option
 from opentsdb_amd.engine import EngineError
 from opentsdb_amd.rollup_read import make_rollup_batch
 from oracle import oracle as O
@@ -255,7 +256,7 @@ def test_larger_table_properties(eng):
 def test_fused_avg_count_stage(eng, monkeypatch, cnt_hi):
     """Rollup avg / count downsampling over full-mantissa sums: k_seq_rows_ro (a value row with its
     lock-step count row, combined in place) bit-identical to the separate passes + k_rollup_combine
-    (TSDBHIP_RO_FUSE=0) and within the oracle's tolerance; counts up to 3000 make count rows of
+    (option RO_FUSE = 0) and within the oracle's tolerance; counts up to 3000 make count rows of
     mixed 1- and 2-byte cells, which hand their series back (k_seq_dense + the list combine)."""
     rng = np.random.default_rng(17 + cnt_hi)
     rb = random_table(rng, 40, 4, 2, floats=True, cnt_hi=cnt_hi)
@@ -265,7 +266,7 @@ def test_fused_avg_count_stage(eng, monkeypatch, cnt_hi):
             q = _q(ds, agg, start=B + 1800, end=B + 2 * 86400)
             res = {}
             for fuse in ("1", "0"):
-                monkeypatch.setenv("TSDBHIP_RO_FUSE", fuse)
+                set_option("RO_FUSE", fuse)
                 res[fuse] = eng.run(q)
             assert len(res["1"]) == len(res["0"])
             for (g1, t1, b1, i1), (g2, t2, b2, i2) in zip(res["1"], res["0"]):

@@ -1,7 +1,7 @@
 """GPU parity at the BASELINE configs' real sizes, and the load-time row index.
 
 * k_index (vectorised, one pass, 8 datapoints per lane) against the sequential per-datapoint
-  path it replaced (TSDBHIP_INDEX_GENERIC=1), row descriptor by row descriptor, over fuzzed
+  path it replaced (option INDEX_GENERIC = 1), row descriptor by row descriptor, over fuzzed
   cells of every class: 2-byte / 4-byte / mixed qualifiers, vle integers, float32 / float64,
   NaN / -0.0 / Inf, unsorted offsets, malformed lengths, short value arrays, long rows.
 * BASELINE config 1 at its exact size (1k series x 1 day @10 s, vle integers, 24 rows per
@@ -20,6 +20,7 @@ import numpy as np
 import pytest
 
 from opentsdb_amd import abi, synth
+from opentsdb_amd.engine import get_option, set_option
 from oracle import oracle as O
 from tests.test_gpu_fast import assert_bit_equal
 from tests.test_gpu_parity import assert_groups_match, T0
@@ -42,14 +43,11 @@ def eng():
 def _with_generic(flag: bool):
     class Ctx:
         def __enter__(self):
-            self.old = os.environ.get("TSDBHIP_INDEX_GENERIC")
-            os.environ["TSDBHIP_INDEX_GENERIC"] = "1" if flag else "0"
+            self.old = get_option("INDEX_GENERIC")
+            set_option("INDEX_GENERIC", 1 if flag else 0)
 
         def __exit__(self, *a):
-            if self.old is None:
-                del os.environ["TSDBHIP_INDEX_GENERIC"]
-            else:
-                os.environ["TSDBHIP_INDEX_GENERIC"] = self.old
+            set_option("INDEX_GENERIC", self.old)
     return Ctx()
 
 

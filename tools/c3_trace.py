@@ -1,4 +1,4 @@
-"""Config 3 (10M x 360, 1000 groups) sum:1m-avg with TSDBHIP_TRACE phase marks: where the host
+"""Config 3 (10M x 360, 1000 groups) sum:1m-avg with the TRACE option's phase marks: where the host
 time of a step goes beyond the streaming kernels."""
 import os
 import sys
@@ -8,6 +8,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 T0 = 1356998400
 from opentsdb_amd import abi  # noqa: E402
 from opentsdb_amd.engine import Engine  # noqa: E402
+from opentsdb_amd.engine import set_option  # noqa: E402
+
+set_option("TRACE", 1)   # the library's phase marks on stderr
 
 eng = Engine(0)
 eng.synth(10_000_000, T0, 360, 10000, 2, 1000, 30000, 0x5EED)

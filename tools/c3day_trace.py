@@ -1,4 +1,4 @@
-"""Config 3's day shard, sum:1m-avg only, with TSDBHIP_TRACE phase marks (host wall time of the
+"""Config 3's day shard, sum:1m-avg only, with the TRACE option's phase marks (host wall time of the
 call's phases on stderr) and the Python-side result conversion timed separately."""
 import os
 import sys
@@ -8,6 +8,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 T0 = 1356998400
 from opentsdb_amd import abi  # noqa: E402
 from opentsdb_amd.engine import Engine  # noqa: E402
+from opentsdb_amd.engine import set_option  # noqa: E402
+
+set_option("TRACE", 1)   # the library's phase marks on stderr
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_250_000
 eng = Engine(0)

@@ -1,5 +1,5 @@
 """Config 4 (raw union path) step breakdown (argv: series, steps, queries = sum,rate[,p99]): wall time of the C call, of the Python result
-wrapping, and the device time the library reports.  TSDBHIP_TRACE=1 adds the library's own
+wrapping, and the device time the library reports.  the TRACE option adds the library's own
 phase marks on stderr."""
 import ctypes as C
 import json
@@ -9,6 +9,9 @@ import time
 sys.path.insert(0, ".")
 from opentsdb_amd import abi, synth  # noqa: E402
 from opentsdb_amd.engine import Engine, lib, _check  # noqa: E402
+from opentsdb_amd.engine import set_option  # noqa: E402
+
+set_option("TRACE", 1)   # the library's phase marks on stderr
 
 T0 = 1356998400
 
