@@ -390,6 +390,7 @@ struct tsdbhip_ctx {
   std::mutex mu;
   // resident batch (series in group-sorted order)
   int64_t n_series = 0, n_rows = 0, n_groups = 0;
+  int64_t max_series_rows = INT64_MAX; // most rows of one series in the resident batch (k_recede when > 1)
   uint64_t qual_bytes = 0, val_bytes = 0;
   DevBuf rows, srp, qual, val, gid;
   DevBuf val2;                         // int16 copy of vle-integer values (k_index), at qualifier offsets
@@ -795,6 +796,7 @@ static void release_batch(tsdbhip_ctx* c) {
   c->lc_valid = false;
   c->calc_valid = false;
   c->n_series = c->n_rows = c->n_groups = 0;
+  c->max_series_rows = INT64_MAX;   // (unknown until a load sets it: k_recede runs)
   c->ro_active = c->ro_counts = false;
   c->ro_scan_valid = false;
   c->ro_chk_valid = false;
@@ -989,7 +991,8 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
   HIP_OK(hipEventRecord(c->ev[3], c->stream));   // (the allocation is not index time)
   HIP_OK(index_rows(c->qual.as<uint8_t>(), c->val.as<uint8_t>(), c->val2.as<uint8_t>(), c->rows.as<RowDesc>(), ib, ik,
                     c->n_rows, c->err.as<int32_t>(), generic, c->stream));
-  HIP_OK(index_recede(c->rows.as<RowDesc>(), c->srp.as<int64_t>(), c->qual.as<uint8_t>(), c->n_series, c->stream));
+  if (c->max_series_rows > 1)   // (rows going back in time need two rows of one series)
+    HIP_OK(index_recede(c->rows.as<RowDesc>(), c->srp.as<int64_t>(), c->qual.as<uint8_t>(), c->n_series, c->stream));
   HIP_OK(hipEventRecord(c->ev[1], c->stream));
   std::vector<RowDesc> back(c->n_rows);
   if (c->n_rows)
@@ -1155,6 +1158,7 @@ static int load_body(tsdbhip_ctx* c, const tsdbhip_batch* b, const std::vector<i
   c->h_group.resize(c->n_series);
   c->h_orig = order;
   c->h_srp.assign(c->n_series + 1, 0);
+  c->max_series_rows = 0;
   std::vector<RowDesc> rd;
   uint64_t qtot = 0, vtot = 0;
   for (int64_t i = 0; i < c->n_series; i++) {
@@ -1175,6 +1179,7 @@ static int load_body(tsdbhip_ctx* c, const tsdbhip_batch* b, const std::vector<i
       rd.push_back(d);
     }
     c->h_srp[i + 1] = (int64_t)rd.size();
+    c->max_series_rows = std::max<int64_t>(c->max_series_rows, c->h_srp[i + 1] - c->h_srp[i]);
   }
   // rows of a series must be in base-time order (Span.checkRowOrder): stable sort per series
   for (int64_t i = 0; i < c->n_series; i++) {
@@ -2120,6 +2125,8 @@ extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) 
   c->h_group = hgroup;
   c->h_orig = order;
   c->h_srp = srp;
+  c->max_series_rows = 0;
+  for (int64_t s = 0; s < NS; s++) c->max_series_rows = std::max<int64_t>(c->max_series_rows, srp[s + 1] - srp[s]);
   c->n_rows = (int64_t)rd.size();
   c->qual_bytes = qtot;
   c->val_bytes = vtot;
@@ -2258,6 +2265,7 @@ static int synth_impl(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp, int64_t p0, 
   c->n_series = S;
   c->n_rows = S * R;
   c->n_groups = G;
+  c->max_series_rows = S ? R : 0;
   // qualifier offsets (identical layout for every series)
   // row starts 16-byte aligned (a 128-B alignment moved k_hwin by 1 % and slowed k_rows / k_short by 3 %,
   // profiles/r05d)

@@ -20,6 +20,12 @@
 //                     values at i x L; the variable class stages value bytes in LDS after a
 //                     wave prefix sum of the lengths (its first 1 KB prefetched).  Statistics
 //                     are kept in the integer domain (bit patterns, magnitudes).
+//  * k_index_short    rows of 2-byte qualifiers that fit one chunk (<= 512 datapoints) with
+//                     4-byte values or 1-2-byte integers (config 3's hour rows of 10 s points),
+//                     hinted by k_index_hint: no row lists, a 64-row descriptor batch per wave
+//                     (lane l loads row l's descriptor, the row loop reads them with readlane),
+//                     the next row's loads in flight while one decodes, each row's results kept
+//                     in its own lane and stored with the batch.
 //  * k_index_generic  rows no class kernel takes (mixed second / millisecond qualifiers, odd or
 //                     empty qualifier arrays, a class hypothesis that failed): sequential.
 #include "kcommon.h"
@@ -28,6 +34,10 @@ namespace tsdb {
 
 static constexpr int IDX_STAGE = 4224;   // bytes of value staging per wave: 512 x 8 B + alignment
 static constexpr int IDX_NCLS = 11;      // 0 generic, 1 + qwi * 5 + li (qwi: 2 / 4 bytes; li: var, 1, 2, 4, 8)
+static constexpr uint8_t HINT_SHORT = 0x80;   // hint bit: the row is k_index_short's (low bits: its class)
+// IndexBufs.cnt slots past the classes: k_index_short's rows (4-byte values / 1-2-byte integers)
+// and the rows it handed back to k_index_generic
+static constexpr int IDX_C_SHORT4 = 12, IDX_C_SHORTV = 13, IDX_C_FAIL = 14;
 
 struct IdxAcc {
   bool bad, allf, alli, vmax2, nan, negz, unsorted;
@@ -215,16 +225,26 @@ __host__ __device__ constexpr int idx_cls(int qw, int L) {
   return 1 + (qw == 4 ? 5 : 0) + (L == 0 ? 0 : L == 1 ? 1 : L == 2 ? 2 : L == 4 ? 3 : 4);
 }
 
+// A row fits k_index_short: 2-byte qualifiers (by its first one), one chunk, 4-byte values or
+// 1-2-byte-integer value bytes (uniform 1 / 2 or variable within ndp .. 2 ndp + meta).
+__device__ __forceinline__ bool idx_short_ok(int qw, uint32_t L, uint64_t ndp, uint32_t vlen, bool uni) {
+  if (qw != 2 || ndp == 0 || ndp > (uint64_t)CH) return false;
+  if (uni) return L == 1 || L == 2 || L == 4;
+  return (uint64_t)vlen >= ndp && (uint64_t)vlen <= 2 * ndp + 1;
+}
+
 __global__ __launch_bounds__(256) void k_index_hint(const uint8_t* __restrict__ qual, const RowDesc* __restrict__ rows,
                                                     int64_t n_rows, uint8_t* __restrict__ hint, uint32_t* cnt) {
   __shared__ uint32_t h[16];
   if (threadIdx.x < 16) h[threadIdx.x] = 0;
   __syncthreads();
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int cls = -1, slot = -1;
   if (r < n_rows) {
     const RowDesc& d = rows[r];
     const uint32_t qlen = d.qlen, vlen = d.vlen;
-    int cls = 0;
+    cls = 0;
+    bool sh = false;
     if (qlen > 0) {
       const uint32_t w = *reinterpret_cast<const uint32_t*>(qual + d.qoff);   // qoff is 16-B aligned
       const int qw = (w & 0xF0) == 0xF0 ? 4 : 2;
@@ -233,13 +253,20 @@ __global__ __launch_bounds__(256) void k_index_hint(const uint8_t* __restrict__ 
         const uint64_t ndp = qlen / qw;
         const bool uni = (L == 1 || L == 2 || L == 4 || L == 8) && (uint64_t)vlen == ndp * L + (ndp > 1 ? 1 : 0);
         cls = idx_cls(qw, uni ? (int)L : 0);
+        sh = idx_short_ok(qw, L, ndp, vlen, uni);
       }
     }
-    hint[r] = (uint8_t)cls;
-    atomicAdd(&h[cls], 1u);
+    hint[r] = (uint8_t)(cls | (sh ? HINT_SHORT : 0));
+    slot = sh ? (cls == idx_cls(2, 4) ? IDX_C_SHORT4 : IDX_C_SHORTV) : cls;
+  }
+  // wave-aggregated counts (a class per ballot): one LDS atomic per class present in the wave
+  const int lane = lane_id();
+  for (int c = 0; c < 16; c++) {
+    const uint64_t m = __ballot(slot == c);
+    if (m && lane == 0) atomicAdd(&h[c], (uint32_t)__popcll(m));
   }
   __syncthreads();
-  if (threadIdx.x < IDX_NCLS && h[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], h[threadIdx.x]);
+  if (threadIdx.x < 16 && h[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], h[threadIdx.x]);
 }
 
 // cursor[c] starts at class c's list offset
@@ -253,6 +280,7 @@ __global__ __launch_bounds__(256) void k_index_scatter(const uint8_t* __restrict
   uint32_t local = 0;
   if (r < n_rows) {
     cls = hint[r];
+    if (cls & HINT_SHORT) cls = 0;   // (k_index_short's: not listed)
     local = atomicAdd(&h[cls], 1u);
   }
   __syncthreads();
@@ -693,12 +721,260 @@ __global__ __launch_bounds__(256) void k_index_cls(const uint8_t* __restrict__ q
   }
 }
 
+
+// ---- k_index_short: one-chunk rows of 2-byte qualifiers (config 3's hour rows) ----------
+//
+// A wave takes 64 consecutive rows.  Lane l loads row l's descriptor once (one 48-B line a lane),
+// the rows the hint marks short are walked in order with their fields read by readlane (no
+// dependent descriptor load in the loop), and the next row's qualifier / value loads are issued
+// before the current row decodes.  Lane i covers datapoints 8i .. 8i + 7 (45 lanes for 360):
+//   * 4-byte values (float32, or int32 vle): 32 B of values a lane at 4 x its first datapoint;
+//   * 1-2-byte integers (uniform or variable): the row's value bytes (<= 1 KB) staged in LDS
+//     by 16-B lane slices, each lane's start from a DPP prefix sum of its lengths, its <= 16
+//     bytes read as three 8-B LDS words and consumed value by value from a 128-bit window;
+//     the int16 copy (val2) is one 16-B store a lane.
+// A row breaking a premise (a 4-byte qualifier inside, a float of 1-2 bytes, a 4- or 8-byte
+// integer among the short ones, 4-byte values mixing floats and integers) is handed to
+// k_index_generic (hint 0).  Results are k_index_cls's for the same row: the same flags, lsb and
+// max |value| (tests/test_gpu_scale.py checks every RowDesc against the generic path).
+struct ShortLd {
+  uint4 q;       // qualifiers of the lane's 8 datapoints
+  uint4 v0, v1;  // 4-byte values: 32 B at 4 x 8 lane; 1-2-byte values: v0 = bytes 16 lane .. + 15
+};
+
+__device__ __forceinline__ void short_issue(const uint8_t* __restrict__ qual, const uint8_t* __restrict__ val,
+                                            uint64_t qoff, uint64_t voff, uint32_t ndp, bool u4, ShortLd& ld) {
+  const int lane = lane_id();
+  const uint32_t i = (uint32_t)lane * DPL < ndp ? (uint32_t)lane * DPL : 0u;   // lanes past the row re-read its start
+  ld.q = *reinterpret_cast<const uint4*>(qual + qoff + 2 * (uint64_t)i);
+  const uint64_t vb = voff + (u4 ? 4 * (uint64_t)i : 2 * (uint64_t)i);
+  ld.v0 = *reinterpret_cast<const uint4*>(val + vb);
+  ld.v1 = *reinterpret_cast<const uint4*>(val + vb + (u4 ? 16 : 0));
+}
+
+__global__ __launch_bounds__(256) void k_index_short(const uint8_t* __restrict__ qual, const uint8_t* __restrict__ val,
+                                                     uint8_t* __restrict__ val2, RowDesc* __restrict__ rows,
+                                                     uint8_t* __restrict__ hint, int64_t n_rows, uint32_t* fails,
+                                                     int32_t* err) {
+  __shared__ uint4 stage_all[4][66];   // per wave: 1 KB of value bytes + a 32-B tail
+  const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint4* stage = stage_all[wv];
+  const uint8_t* st8 = reinterpret_cast<const uint8_t*>(stage);
+  if (lane < 2) stage[64 + lane] = make_uint4(0, 0, 0, 0);
+  const int64_t n_tiles = (n_rows + 63) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + wv; t < n_tiles; t += nw) {
+    const int64_t r = (t << 6) + lane;
+    const uint8_t h = r < n_rows ? hint[r] : 0;
+    const bool mine = (h & HINT_SHORT) != 0;
+    uint64_t qoff = 0, voff = 0;
+    uint32_t qlen = 0, vlen = 0, fin = 0;
+    if (mine) {
+      const RowDesc& d = rows[r];
+      qoff = d.qoff;
+      voff = d.voff;
+      qlen = d.qlen;
+      vlen = d.vlen;
+      fin = d.flags;
+    }
+    const uint32_t u4m = (uint32_t)((h & 0x7F) == idx_cls(2, 4));
+    uint64_t todo = __ballot(mine);
+    // this lane's row's results
+    uint32_t o_flags = 0;
+    int32_t o_lsb = INT32_MAX;
+    double o_amax = 0.0;
+    bool o_fail = false;
+    if (todo) {
+      int j = __ffsll((long long)todo) - 1;
+      auto fields = [&](int jj, uint64_t& qo, uint64_t& vo, uint32_t& nd, uint32_t& vl, bool& u4) {
+        qo = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(qoff >> 32), jj) << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)qoff, jj);
+        vo = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(voff >> 32), jj) << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)voff, jj);
+        nd = (uint32_t)__builtin_amdgcn_readlane((int)qlen, jj) >> 1;
+        vl = (uint32_t)__builtin_amdgcn_readlane((int)vlen, jj);
+        u4 = __builtin_amdgcn_readlane((int)u4m, jj) != 0;
+      };
+      uint64_t cq, cv;
+      uint32_t cn, cvl;
+      bool cu4;
+      fields(j, cq, cv, cn, cvl, cu4);
+      ShortLd ld;
+      short_issue(qual, val, cq, cv, cn, cu4, ld);
+      for (;;) {
+        todo &= todo - 1;
+        const int jn = todo ? __ffsll((long long)todo) - 1 : j;
+        uint64_t nq, nv;
+        uint32_t nn, nvl;
+        bool nu4;
+        fields(jn, nq, nv, nn, nvl, nu4);
+        ShortLd nl;
+        short_issue(qual, val, nq, nv, nn, nu4, nl);
+        // ---- row j: qualifiers
+        const int i0 = lane * DPL;
+        const int nin = min(DPL, max(0, (int)cn - i0));
+        uint32_t qq[DPL];
+        {
+          const uint32_t ws[4] = {ld.q.x, ld.q.y, ld.q.z, ld.q.w};
+#pragma unroll
+          for (int k = 0; k < DPL; k++) {
+            const uint32_t b = __builtin_bswap32(ws[k >> 1]);
+            qq[k] = (k & 1) ? (b & 0xFFFF) : (b >> 16);
+          }
+        }
+        bool fail = false, bad = false, uns = false;
+        uint32_t fl_or = 0, fl_and = 8;
+        int len[DPL], lsum = 0, lmin = 99, lmax = -1;
+        int prev = -1;
+#pragma unroll
+        for (int k = 0; k < DPL; k++) {
+          const bool in = k < nin;
+          const uint32_t f = qq[k] & 8;
+          len[k] = in ? (int)(qq[k] & 7) + 1 : 0;
+          fail |= in & ((qq[k] >> 12) == 0xF);                    // a 4-byte qualifier inside
+          fl_or |= in ? f : 0u;
+          fl_and &= in ? f : 8u;
+          lsum += len[k];
+          lmin = min(lmin, in ? len[k] : 99);
+          lmax = max(lmax, in ? len[k] : -1);
+          const int off = (int)(qq[k] >> 4);                       // seconds: strictly increasing
+          uns |= in & (k > 0) & (off <= prev);
+          prev = in ? off : prev;
+        }
+        {   // order across lanes: this lane's first offset against the previous lane's last
+          const int last = (int)(qq[max(0, nin - 1)] >> 4);
+          const int pl = __shfl_up(nin > 0 ? last : -1, 1, 64);
+          uns |= (lane > 0) & (nin > 0) & ((int)(qq[0] >> 4) <= pl);
+        }
+        uint32_t flags = 2;
+        int lsb = INT32_MAX;
+        uint32_t amax_bits = 0;   // float32 |x| bits, or |int32|
+        bool isf = false, nan = false, negz = false;
+        if (cu4) {
+          // ---- 4-byte values: float32 or int32
+#pragma unroll
+          for (int k = 0; k < DPL; k++) fail |= (k < nin) & (len[k] != 4);
+          const bool allf = __all(fl_and != 0), alli = __all(fl_or == 0);
+          fail |= !allf && !alli;                                  // floats and integers mixed: generic
+          isf = allf;
+          const uint32_t vw[8] = {ld.v0.x, ld.v0.y, ld.v0.z, ld.v0.w, ld.v1.x, ld.v1.y, ld.v1.z, ld.v1.w};
+#pragma unroll
+          for (int k = 0; k < DPL; k++) {
+            const bool in = k < nin;
+            const uint32_t be = __builtin_bswap32(vw[k]);
+            if (allf) {
+              const uint32_t ab = be & 0x7FFFFFFFu;
+              const bool isn = ab > 0x7F800000u;
+              const bool ok = in & !isn;
+              nan |= in & isn;
+              negz |= ok & (be == 0x80000000u);
+              amax_bits = max(amax_bits, ok ? ab : 0u);
+              const uint32_t E = ab >> 23, M = ab & 0x7FFFFFu;
+              const int lj = E == 0 ? (int)__builtin_ctz(M | 0x80000000u) - 149 : (int)E - 150 + (int)__builtin_ctz(M | 0x800000u);
+              lsb = min(lsb, (ok & (ab != 0) & (E != 0xFF)) ? lj : INT32_MAX);
+            } else {
+              const int32_t x = (int32_t)be;
+              const uint32_t ax = x < 0 ? 0u - (uint32_t)x : (uint32_t)x;
+              const bool ok = in & (ax != 0);
+              amax_bits = max(amax_bits, ok ? ax : 0u);
+              lsb = min(lsb, ok ? (int)__builtin_ctz(ax) : INT32_MAX);
+            }
+          }
+          flags |= (4u << ROW_VL_SHIFT) | (allf ? ROW_ALLF : 0u) | (alli ? ROW_ALLI : 0u);
+        } else {
+          // ---- 1-2-byte integers: stage the value bytes, each lane's start by prefix sum
+          fail |= (fl_or != 0) | (lmax > 2);
+          const int incl = wave_incl_sum_dpp(lsum);
+          const int total = __builtin_amdgcn_readlane(incl, 63);
+          bad |= lane == 0 && (uint32_t)total > cvl;              // values past the row's value bytes
+          WAVE_SYNC();
+          stage[lane] = ld.v0;
+          WAVE_SYNC();
+          const int b = min(incl - lsum, 1024);
+          const int b8 = b & ~7, d = (b - b8) * 8;
+          const uint64_t x0 = *reinterpret_cast<const uint64_t*>(st8 + b8);
+          const uint64_t x1 = *reinterpret_cast<const uint64_t*>(st8 + b8 + 8);
+          const uint64_t x2 = *reinterpret_cast<const uint64_t*>(st8 + b8 + 16);
+          uint64_t lo = d ? (x0 >> d) | (x1 << (64 - d)) : x0;
+          uint64_t hi = d ? (x1 >> d) | (x2 << (64 - d)) : x1;
+          uint32_t h16[4] = {0, 0, 0, 0};
+          uint32_t imax = 0;
+          const int vend = (int)((cvl + 15) & ~15u);   // (k_index_cls decodes up to the 16-B-aligned extent)
+          int pos = b;
+#pragma unroll
+          for (int k = 0; k < DPL; k++) {
+            const int L = len[k];
+            // big-endian: first byte most significant
+            const uint32_t b0 = (uint32_t)lo & 0xFF, b1 = (uint32_t)(lo >> 8) & 0xFF;
+            const int32_t xv = L == 2 ? (int32_t)(int16_t)(uint16_t)((b0 << 8) | b1) : (int32_t)(int8_t)(uint8_t)b0;
+            const int32_t x = pos + L <= vend ? xv : 0;
+            pos += L;
+            const uint32_t ax = x < 0 ? 0u - (uint32_t)x : (uint32_t)x;
+            const bool ok = (k < nin) & (ax != 0);
+            imax = max(imax, ok ? ax : 0u);
+            lsb = min(lsb, ok ? (int)__builtin_ctz(ax) : INT32_MAX);
+            h16[k >> 1] |= ((uint32_t)x & 0xFFFF) << ((k & 1) * 16);
+            const int sh = 8 * max(L, 1);
+            if (L) {
+              lo = (lo >> sh) | (hi << (64 - sh));
+              hi >>= sh;
+            }
+          }
+          amax_bits = imax;
+          if (val2 && nin > 0)
+            *reinterpret_cast<uint4*>(val2 + cq + 2 * (uint64_t)i0) = make_uint4(h16[0], h16[1], h16[2], h16[3]);
+          const int wl = wave_min(lmin), wh = wave_max(lmax);
+          flags |= ROW_ALLI | ROW_VLE2 | (wl == wh ? (uint32_t)wl << ROW_VL_SHIFT : 0u);
+        }
+        // ---- row results
+        const bool rfail = __any(fail);
+        const int wlsb = wave_reduce_i32(lsb, INT32_MAX, [](int a, int c) { return min(a, c); });
+        const uint32_t wmax = (uint32_t)wave_reduce_i32((int)amax_bits, 0,
+                                                        [](int a, int c) { return (int)max((uint32_t)a, (uint32_t)c); });
+        const double amax = isf ? (double)__uint_as_float(wmax) : (double)wmax;
+        if (__any(bad)) flags |= ROW_ERR;
+        if (__any(nan)) flags |= ROW_NAN;
+        if (__any(negz)) flags |= ROW_NEGZ;
+        if (__any(uns)) flags |= ROW_UNSORTED;
+        if (row_nocert(wlsb, amax)) flags |= ROW_NOCERT;
+        if (lane == j) {
+          o_flags = flags | (fin & ROW_SFIRST);
+          o_lsb = wlsb;
+          o_amax = amax;
+          o_fail = rfail;
+        }
+        if (!todo) break;
+        j = jn;
+        cq = nq; cv = nv; cn = nn; cvl = nvl; cu4 = nu4;
+        ld = nl;
+      }
+    }
+    if (mine) {
+      if (o_fail) {
+        hint[r] = 0;   // k_index_generic takes the row
+        atomicAdd(fails, 1u);
+      } else {
+        RowDesc& o = rows[r];
+        o.ndp = qlen >> 1;
+        o.flags = o_flags;
+        o.lsb = o_lsb;
+        o.absmax = o_amax;
+        if (o_flags & ROW_ERR) set_err(err, TSDB_E_ILLEGAL_DATA);
+      }
+    }
+  }
+}
+
 // Rows of class 0 (hint 0), or every row (all = 1: test hook), through the sequential path.
 // A wave scans 64 hints at a time and walks the rows its ballot selects.
 __global__ __launch_bounds__(256) void k_index_generic(const uint8_t* __restrict__ qual, const uint8_t* __restrict__ val,
                                                        uint8_t* __restrict__ val2, RowDesc* __restrict__ rows,
                                                        const uint8_t* __restrict__ hint, int64_t n_rows, int32_t* err,
-                                                       int all) {
+                                                       int all, const uint32_t* need) {
+  // need (non-null): the count of rows handed back by k_index_short -- the only rows left to
+  // this kernel when no class kernel ran and k_index_hint found none for it
+  if (need && *need == 0) return;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int lane = lane_id();
   for (int64_t r0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64; r0 < n_rows; r0 += nw * 64) {
@@ -729,6 +1005,8 @@ static hipError_t launch_cls(const uint8_t* qual, const uint8_t* val, uint8_t* v
 
 hipError_t index_classes(const uint8_t* qual, const RowDesc* rows, const IndexBufs& b, int64_t n_rows,
                          IndexClasses* out, hipStream_t s) {
+  // (k_index_hint's counts: classes 0 .. IDX_NCLS - 1 for the listed rows and k_index_generic,
+  // IDX_C_SHORT4 / IDX_C_SHORTV for k_index_short's rows)
   *out = IndexClasses{};
   if (n_rows == 0) return hipSuccess;
   if (n_rows > 0x7FFFFFFFLL) return hipErrorInvalidValue;   // int32 row lists
@@ -741,11 +1019,17 @@ hipError_t index_classes(const uint8_t* qual, const RowDesc* rows, const IndexBu
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
   for (int c = 0; c < 16; c++) out->cnt[c] = cnt[c];
   for (int c = 2; c < IDX_NCLS; c++) out->off[c] = out->off[c - 1] + cnt[c - 1];
-  for (int c = 0; c < 16; c++) cur[c] = out->off[c];
-  if ((e = hipMemcpyAsync(b.cnt, cur, 16 * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_index_scatter, dim3(tb), dim3(256), 0, s, b.hint, n_rows, b.cnt, b.list);
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;   // `cur` leaves scope
-  out->vle_capable = cnt[idx_cls(2, 0)] + cnt[idx_cls(2, 1)] + cnt[idx_cls(2, 2)];
+  for (int c = 1; c < IDX_NCLS; c++) out->listed += cnt[c];
+  out->short_rows = cnt[IDX_C_SHORT4] + cnt[IDX_C_SHORTV];
+  out->vle_capable = cnt[idx_cls(2, 0)] + cnt[idx_cls(2, 1)] + cnt[idx_cls(2, 2)] + cnt[IDX_C_SHORTV];
+  if (out->listed) {   // class row lists (the cursors; k_index_short's hand-back counter at 0)
+    for (int c = 0; c < 16; c++) cur[c] = out->off[c];
+    if ((e = hipMemcpyAsync(b.cnt, cur, 16 * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_index_scatter, dim3(tb), dim3(256), 0, s, b.hint, n_rows, b.cnt, b.list);
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;   // `cur` leaves scope
+  } else if ((e = hipMemsetAsync(b.cnt + IDX_C_FAIL, 0, 4, s)) != hipSuccess) {
+    return e;
+  }
   return hipGetLastError();
 }
 
@@ -755,16 +1039,25 @@ hipError_t index_rows(const uint8_t* qual, const uint8_t* val, uint8_t* val2, Ro
   const int64_t gblocks = std::min<int64_t>((n_rows + 3) / 4, 16384);
   if (generic) {
     hipLaunchKernelGGL(k_index_generic, dim3((unsigned)gblocks), dim3(256), 0, s, qual, val, val2, rows, b.hint, n_rows,
-                       err, 1);
+                       err, 1, nullptr);
     return hipGetLastError();
   }
   hipError_t e;
+  if (k.short_rows) {
+    const int64_t tiles = (n_rows + 63) / 64;
+    hipLaunchKernelGGL(k_index_short, dim3((unsigned)std::min<int64_t>((tiles + 3) / 4, 16384)), dim3(256), 0, s, qual,
+                       val, val2, rows, b.hint, n_rows, b.cnt + IDX_C_FAIL, err);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
 #define IDX_CLS(Q, LL) if ((e = launch_cls<Q, LL>(qual, val, val2, rows, b, k.off, k.cnt, err, s)) != hipSuccess) return e;
   IDX_CLS(2, 0) IDX_CLS(2, 1) IDX_CLS(2, 2) IDX_CLS(2, 4) IDX_CLS(2, 8)
   IDX_CLS(4, 0) IDX_CLS(4, 1) IDX_CLS(4, 2) IDX_CLS(4, 4) IDX_CLS(4, 8)
 #undef IDX_CLS
+  // rows of no class, or handed back by a class kernel: known only on the device when just
+  // k_index_short ran (its hand-back counter); otherwise the kernel scans every hint
+  const bool early_out = k.cnt[0] == 0 && k.listed == 0;
   hipLaunchKernelGGL(k_index_generic, dim3((unsigned)std::min<int64_t>(gblocks, 4096)), dim3(256), 0, s, qual, val,
-                     nullptr, rows, b.hint, n_rows, err, 0);
+                     nullptr, rows, b.hint, n_rows, err, 0, early_out ? b.cnt + IDX_C_FAIL : nullptr);
   return hipGetLastError();
 }
 
