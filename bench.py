@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH/WRITE_SIZE child passes")
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 (10M series) block in `extra`")
+    ap.add_argument("--no-config5", action="store_true", help="--gpus N > 1: skip the config-5 block in `extra`")
+    ap.add_argument("--c5-series", type=int, default=10_000_000, help=argparse.SUPPRESS)   # rehearsals only
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the parity checks against the one-GPU reference (exploratory runs only)")
     ap.add_argument("--transport", choices=["auto", "rccl", "copy"], default="auto",
@@ -718,6 +720,151 @@ def md_config3(args, n):
         eng.close()
 
 
+# ---- BASELINE config 5 at N GPUs: percentile downsampling + rollup generation ----------------
+C5_FNS = ("p99", "ep99r7")
+C5_ROLLUPS = (("1h", "1d"), ("1d", "1n"))
+
+
+def c5_spec(args, hours: int):
+    """Config 5's store: 10M float32 series @10 s, 64 groups (the 1-GPU shard in
+    tools/bench_configs.py --config 5 is 1.25M series of it)."""
+    return (args.c5_series, T0, hours * 360, 10000, 0, 64, 1, 0x5EED)
+
+
+def c5_queries(t1: int):
+    """sum:1h-p99 and sum:1h-ep99r7 (PercentileAgg downsampling, Aggregators.java:397-431,
+    657-708; the group-by a decomposable sum)."""
+    from opentsdb_amd import abi
+    return [(f"sum:1h-{f}", abi.new_query(T0, t1, "sum", ds_function=abi.AGG[f], ds_interval_ms=3600000)) for f in C5_FNS]
+
+
+def c5_parity_named(t1: int):
+    return [(name.replace(":", "_"), "sum", q, "partials") for name, q in c5_queries(t1)]
+
+
+def rollup_cells_equal(a, b) -> bool:
+    import numpy as np
+    return all(np.array_equal(getattr(a, f), getattr(b, f)) for f in ("series", "base_time", "qualifier", "val_off", "value"))
+
+
+def c5_rollup_timing(eng, hours: int, steps: int, L=None):
+    """tsdbhip_rollup_run over the resident store per (interval, row span): sum, count, max, min
+    cells (RollupUtils.java:52-171) left on the device(s).  Max over ranks under a launcher."""
+    from opentsdb_amd import engine as E
+    out = {}
+    for iv, span in C5_ROLLUPS:
+        riv = E.rollup_interval(iv, span)
+        nc, nb = eng.rollup_run(riv, T0, T0 + hours * 3600)
+        if L is not None:
+            L.sync(eng)
+        t = time.perf_counter()
+        for _ in range(steps):
+            nc, nb = eng.rollup_run(riv, T0, T0 + hours * 3600)
+        if L is not None:
+            L.sync(eng)
+        ms = (time.perf_counter() - t) * 1000 / steps
+        if L is not None:
+            ms, nc, nb = L.max(ms), L.sum(int(nc)), L.sum(int(nb))
+        out[f"rollup {iv} in {span} rows x sum,count,max,min"] = {"ms_per_step": ms, "cells": int(nc), "value_bytes": int(nb)}
+    return out
+
+
+def md_config5(args, n):
+    """BASELINE config 5 over the n GPUs of one multi-device context: 10M float32 series x 1 day
+    @10 s (12 h at 2 GPUs), 64 groups, series shards -- sum:1h-p99 and sum:1h-ep99r7 (parity vs
+    one GPU on shard-edge / strided groups), then 1h/1d and 1d/1n rollup generation over the
+    store (each device its series; parity of the cells vs one GPU on the straddle store)."""
+    from opentsdb_amd import engine as E
+    hours = 24 if n >= 4 else 12
+    spec = c5_spec(args, hours)
+    t1 = T0 + hours * 3600 - 1
+    eng, note = md_engine(args, n)
+    try:
+        t = time.perf_counter()
+        eng.synth(*spec)
+        eng.sync()
+        out = {"workload": f"BASELINE config 5: {spec[0] / 1e6:g}M float32 series x {hours} h @10 s, 64 groups, over {n} "
+                           "GPUs (series shards)", "hours": hours, "synth_s": time.perf_counter() - t, "transport_note": note}
+        if not args.no_parity:
+            out["parity"] = md_parity(eng, md_devices(n)[0], spec, c5_parity_named(t1), f"config 5, {hours} h store")
+        steps = max(3, args.steps)
+        for name, q in c5_queries(t1):
+            try:
+                eng.run(q)
+            except E.EngineError as ex:
+                out[name] = {"skipped": str(ex)}
+                continue
+            eng.sync()
+            t = time.perf_counter()
+            for _ in range(steps):
+                eng.run(q)
+            eng.sync()
+            ms = (time.perf_counter() - t) * 1000 / steps
+            tm = eng.timing()
+            out[name] = {"ms_per_step": ms, "value": tm.datapoints / (ms / 1000), "unit": "datapoints/s",
+                         "devices_ms": tm.devices_ms, "exchange_ms": tm.exchange_ms}
+        out.update(c5_rollup_timing(eng, hours, steps))
+    finally:
+        eng.close()
+    if not args.no_parity:   # rollup cells, byte for byte, on the straddle store
+        md, _ = md_engine(args, n)
+        one = E.Engine(md_devices(n)[0])
+        try:
+            ok = True
+            for x in (md, one):
+                x.synth(*STRADDLE_SPEC)
+            for iv, span in C5_ROLLUPS:
+                riv = E.rollup_interval(iv, span)
+                ok = ok and rollup_cells_equal(md.rollup(riv, T0, T0 + 3600), one.rollup(riv, T0, T0 + 3600))
+            out["rollup_parity"] = {"ok": bool(ok), "what": "straddle store, 1h/1d and 1d/1n cells byte for byte vs one GPU"}
+        finally:
+            md.close()
+            one.close()
+    return out
+
+
+def launch_config5(args, L):
+    """BASELINE config 5 over the launch's ranks (one process per GPU): rank r synthesizes its
+    contiguous shard of the 10M-series store; sum:1h-p99 / ep99r7 through the partial-state
+    all-gather; rollup generation per rank over its own series (no exchange)."""
+    from opentsdb_amd.dist import synth_bounds
+    from opentsdb_amd.engine import Engine, EngineError
+    hours = 24 if L.world >= 4 else 12
+    spec = c5_spec(args, hours)
+    bounds = synth_bounds(spec[0], L.world)
+    t1 = T0 + hours * 3600 - 1
+    eng = Engine(L.device)
+    try:
+        t = time.perf_counter()
+        eng.synth_shard(bounds[L.rank], bounds[L.rank + 1], *spec)
+        eng.sync()
+        out = {"workload": f"BASELINE config 5: {spec[0] / 1e6:g}M float32 series x {hours} h @10 s, 64 groups, over "
+                           f"{L.world} ranks (one process per GPU, series shards)", "hours": hours,
+               "synth_s": L.max(time.perf_counter() - t)}
+        if not args.no_parity:
+            out["parity"] = launch_parity(L, eng, spec, bounds, c5_parity_named(t1), f"config 5, {hours} h store")
+        one, _ = L.runner(eng, spec[5])
+        steps = max(3, args.steps)
+        for name, q in c5_queries(t1):
+            try:
+                one(q, "partials")
+            except EngineError as ex:
+                out[name] = {"skipped": str(ex)}
+                continue
+            L.sync(eng)
+            t = time.perf_counter()
+            for _ in range(steps):
+                one(q, "partials")
+            L.sync(eng)
+            ms = L.max((time.perf_counter() - t) * 1000 / steps)
+            dps = L.sum(int(eng.timing().datapoints))
+            out[name] = {"ms_per_step": ms, "value": dps / (ms / 1000), "unit": "datapoints/s"}
+        out.update(c5_rollup_timing(eng, hours, steps, L))
+        return out
+    finally:
+        eng.close()
+
+
 def run_child(cmd, timeout):
     """One bench child: (returncode or None on a time-out, its last JSON line or None, stderr tail).
     Its stderr is passed through."""
@@ -823,6 +970,8 @@ def main_md(args):
     if parity is not None:
         parity["straddle"] = md_straddle(args, n, md_devices(n)[0])
     extra = None if args.no_config3 else {"config3_strong": md_config3(args, n)}
+    if not args.no_config5:
+        extra = dict(extra or {}, config5=md_config5(args, n))
     ok = parity_all_ok(parity, extra)
     line = {
         "metric": "raw datapoints/sec through downsample+group-by; % of HBM BW, 1-8 GPUs",
@@ -891,6 +1040,8 @@ def parity_all_ok(parity, extra) -> bool:
     for v in (extra or {}).values():
         if isinstance(v, dict) and v.get("parity") is not None:
             blocks.append(v["parity"])
+        if isinstance(v, dict) and v.get("rollup_parity") is not None:
+            blocks.append(v["rollup_parity"])
     return all(b.get("ok") for b in blocks)
 
 
@@ -1178,6 +1329,8 @@ def main():
     extra = None
     if not args.no_config3:
         extra = {"config3": config3_block(args, L.device)} if L.dist is None else {"config3_strong": launch_config3(args, L)}
+    if L.dist is not None and not args.no_config5:
+        extra = dict(extra or {}, config5=launch_config5(args, L))
     ok = parity_all_ok(parity, extra)
     if rank == 0:
         cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(args, args.cpu_seconds)

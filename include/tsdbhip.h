@@ -376,11 +376,14 @@ int tsdbhip_assemble(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_
  * transport: TSDB_MD_AUTO = RCCL (ncclCommInitAll) when two or more devices are all distinct,
  * device copies when a device repeats (several shards on one GPU); TSDB_MD_RCCL / TSDB_MD_COPY
  * force one.
- * Entry points bound to one device's resident store (load_shard, synth_shard, load_cells,
- * batch downloads, the partials / sel exchange, rollup generation, debug_rows) return
- * TSDB_E_NOT_IMPLEMENTED on such a context; tsdbhip_load_rollup shards a rollup batch; the
- * histogram path (its store resident on devices[0], unsharded) and the expression functions
- * run on devices[0].  tsdbhip_last_timing: per-device stage times are the maximum over
+ * Entry points bound to one device's resident store (load_shard, synth_shard, batch
+ * downloads, the per-rank partials / sel exchange, debug_rows) return TSDB_E_NOT_IMPLEMENTED on
+ * such a context.  tsdbhip_load_rollup shards a rollup batch and tsdbhip_load_cells a compaction
+ * scan (each device compacts its series' rows) as tsdbhip_load shards a batch;
+ * tsdbhip_rollup_run generates every device's series' rollup cells on that device and
+ * tsdbhip_rollup_download returns them in the one-GPU order (function, batch series, time),
+ * byte for byte the one-GPU cells.  The histogram path (its store resident on devices[0],
+ * unsharded) and the expression functions run on devices[0].  tsdbhip_last_timing: per-device stage times are the maximum over
  * the devices, counters are summed, total_ms is the host wall time of the call and exchange_ms
  * its gather + merge part. */
 enum { TSDB_SHARD_AUTO = -1 };
@@ -502,7 +505,12 @@ int tsdbhip_load_rollup(tsdbhip_ctx* ctx, const tsdbhip_rollup_batch* rb);
  * an integer of 3, 5, 6 or 7) raises TSDB_E_RUNTIME (BufferUnderflowException); the meta byte
  * follows the reference's isMilliseconds() read after the kept column advanced.  The HBase scan
  * time range that flag also sets (TsdbQuery.java:1401-1409) is the caller's scan.  Such batches
- * run the global-sort compaction path. */
+ * run the global-sort compaction path.
+ * Documented approximation (parity unpinned): columns with EQUAL HBase write timestamps are taken
+ * in scan order, here and in the oracle.  The reference's ColumnDatapointIterator.compareTo returns
+ * 0 for them and java.util.PriorityQueue is not stable, so which of two such columns heads the heap
+ * -- the one whose datapoint a DTCS tie keeps (int 5 vs float 5.0, a NaN head) -- is not defined by
+ * the reference; give such columns distinct col_timestamp values for a defined answer. */
 typedef struct {
   int64_t n_series;
   const int64_t* series_row_ptr;   /* [n_series + 1] */

@@ -820,6 +820,14 @@ void ctx_drop_batch(tsdbhip_ctx* c) {
   release_batch(c);
 }
 int64_t ctx_n_series(tsdbhip_ctx* c) { return c->n_series; }   // resident series (count series too)
+// the last tsdbhip_rollup_run's cells / value bytes per function (its output order)
+int ctx_rollup_parts(tsdbhip_ctx* c, int64_t* cells, uint64_t* bytes) {
+  for (int i = 0; i < c->ro_n; i++) {
+    cells[i] = c->ro_out[i].cells;
+    bytes[i] = c->ro_out[i].bytes;
+  }
+  return c->ro_n;
+}
 }  // namespace tsdb
 
 extern "C" void tsdbhip_destroy(tsdbhip_ctx* c) {
@@ -1609,8 +1617,8 @@ extern "C" int tsdbhip_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* r
 // host lays the compacted rows out as the resident batch (series by group, rows by base time,
 // rows without a datapoint dropped as SaltScanner.processRow drops a null compaction).
 extern "C" int tsdbhip_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) {
-  MD_REFUSE(c, "tsdbhip_load_cells");
   if (!c || !cb) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  if (c->md) return tsdb::md_load_cells(c, cb);
   const int64_t NS = cb->n_series, NR = cb->n_rows, NC = cb->n_cols;
   if (NS < 0 || NR < 0 || NC < 0) return fail(TSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
   if (NS > 0 && (!cb->series_row_ptr || !cb->group_id)) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null batch arrays");
@@ -5166,9 +5174,9 @@ extern "C" int tsdbhip_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_resul
 // streaming pass.  The queries must share the time range and the downsampling specification;
 // rate, aggregator and flags may differ.
 extern "C" int tsdbhip_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_result** outs) {
-  if (c && c->md) return tsdb::md_run_multi(c, qs, n, outs);
   if (!c || !qs || !outs || n < 1) return fail(TSDB_E_ILLEGAL_ARGUMENT, "bad argument");
   for (int i = 0; i < n; i++) outs[i] = nullptr;
+  // (checked before the multi-device dispatch too: every context refuses the same batches)
   for (int i = 1; i < n; i++) {
     const tsdbhip_query &a = qs[0], &b = qs[i];
     if (a.start_time != b.start_time || a.end_time != b.end_time || a.ds_function != b.ds_function ||
@@ -5176,6 +5184,7 @@ extern "C" int tsdbhip_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n,
         a.ds_calendar != b.ds_calendar)
       return fail(TSDB_E_ILLEGAL_ARGUMENT, "tsdbhip_run_multi: the queries must share the time range and downsampling");
   }
+  if (c->md) return tsdb::md_run_multi(c, qs, n, outs);
   CtxLock lk(c);
   HIP_OK(hipSetDevice(c->device));
   if (c->ro_active) {
@@ -5930,7 +5939,7 @@ extern "C" int tsdbhip_rollup_qualifier(int64_t timestamp, int32_t basetime, int
 }
 
 extern "C" int tsdbhip_rollup_run(tsdbhip_ctx* c, const tsdbhip_rollup_spec* sp, int64_t* n_cells, uint64_t* value_bytes) {
-  MD_REFUSE(c, "tsdbhip_rollup_run");
+  if (c && c->md) return tsdb::md_rollup_run(c, sp, n_cells, value_bytes);
   if (c && c->ro_active) return fail(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_rollup_run over a rollup batch (tsdbhip_load_rollup)");
   if (!c || !sp) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   if (!iv_valid(&sp->interval)) return fail(TSDB_E_ILLEGAL_ARGUMENT, "invalid rollup interval");
@@ -6135,7 +6144,7 @@ extern "C" int tsdbhip_rollup_run(tsdbhip_ctx* c, const tsdbhip_rollup_spec* sp,
 
 extern "C" int tsdbhip_rollup_download(tsdbhip_ctx* c, int32_t* series, uint32_t* base_time, uint8_t* qualifier,
                                        uint64_t* val_off, uint8_t* value) {
-  MD_REFUSE(c, "tsdbhip_rollup_download");
+  if (c && c->md) return tsdb::md_rollup_download(c, series, base_time, qualifier, val_off, value);
   if (!c) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null ctx");
   CtxLock lk(c);
   HIP_OK(hipSetDevice(c->device));

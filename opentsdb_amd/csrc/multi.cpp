@@ -212,6 +212,12 @@ struct MultiDev {
   tsdbhip_timing timing{};
   std::vector<tsdbhip_timing> dev_timing;   // per device, last call
   double xfer_bytes = 0;                // device-to-device bytes of the last call
+  // the last rollup generation: per device, per function, its cells / value bytes (on the device
+  // until tsdbhip_rollup_download)
+  bool ro_valid = false;
+  int ro_nf = 0;
+  std::vector<std::vector<int64_t>> ro_cells;
+  std::vector<std::vector<uint64_t>> ro_bytes;
 };
 
 MultiDev* md_of(tsdbhip_ctx* c) { return static_cast<MultiDev*>(ctx_md(c)); }
@@ -922,6 +928,7 @@ std::vector<std::vector<int64_t>> shard_series(MultiDev* m, const int32_t* gid, 
 
 int md_load(tsdbhip_ctx* c, const tsdbhip_batch* b) {
   MultiDev* m = md_of(c);
+  m->ro_valid = false;
   if (!b) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   if (b->n_series < 0 || b->n_rows < 0) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
   if (b->n_series > 0 && (!b->series_row_ptr || !b->group_id || !b->row_qual_off || !b->row_val_off))
@@ -957,6 +964,7 @@ int md_load(tsdbhip_ctx* c, const tsdbhip_batch* b) {
 // so its plans (scan bounds of the rollup interval, count group-by as sum) match the devices'.
 int md_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* rb) {
   MultiDev* m = md_of(c);
+  m->ro_valid = false;
   if (!rb) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   const tsdbhip_batch* b = &rb->cells;
   const bool cnt = rb->row_cqual_off != nullptr;
@@ -1063,6 +1071,7 @@ int md_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* rb) {
 
 int md_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp) {
   MultiDev* m = md_of(c);
+  m->ro_valid = false;
   if (!sp) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   if (sp->n_series <= 0 || sp->n_groups <= 0) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "bad synth spec");
   std::lock_guard<std::mutex> lk(ctx_mutex(c));
@@ -1097,6 +1106,197 @@ int md_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp) {
   m->pos0.assign(p.begin(), p.end() - 1);
   m->mode = mode;
   m->G = G;
+  return 0;
+}
+
+
+// A compaction scan (tsdbhip_load_cells): the scan's series split as md_load splits a batch (by
+// their column bytes), each device compacting its series' rows (copied out of the caller's arrays)
+// into its resident shard; compaction exceptions surface lazily from the device holding the row.
+int md_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb) {
+  MultiDev* m = md_of(c);
+  m->ro_valid = false;
+  const int64_t S = cb->n_series, NR = cb->n_rows, NC = cb->n_cols;
+  if (S < 0 || NR < 0 || NC < 0) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
+  if (S > 0 && (!cb->series_row_ptr || !cb->group_id)) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null batch arrays");
+  if (NR > 0 && (!cb->row_base_time || !cb->row_col_ptr)) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null batch arrays");
+  if (NC > 0 && (!cb->col_qual_off || !cb->col_val_off || !cb->qual || !cb->val))
+    return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null batch arrays");
+  if (S > 0 && (cb->series_row_ptr[0] != 0 || cb->series_row_ptr[S] != NR))
+    return set_error(TSDB_E_ILLEGAL_ARGUMENT, "series_row_ptr does not cover the rows");
+  if (NR > 0 && (cb->row_col_ptr[0] != 0 || cb->row_col_ptr[NR] != NC))
+    return set_error(TSDB_E_ILLEGAL_ARGUMENT, "row_col_ptr does not cover the columns");
+  for (int64_t s = 0; s < S; s++)
+    if (cb->series_row_ptr[s + 1] < cb->series_row_ptr[s]) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "series_row_ptr not monotonic");
+  for (int64_t r = 0; r < NR; r++)
+    if (cb->row_col_ptr[r + 1] < cb->row_col_ptr[r]) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "row_col_ptr not monotonic");
+  for (int64_t k = 0; k < NC; k++)
+    if (cb->col_qual_off[k + 1] < cb->col_qual_off[k] || cb->col_val_off[k + 1] < cb->col_val_off[k])
+      return set_error(TSDB_E_ILLEGAL_ARGUMENT, "column offsets not monotonic");
+  std::lock_guard<std::mutex> lk(ctx_mutex(c));
+  std::vector<double> w(S);
+  for (int64_t s = 0; s < S; s++) {
+    const int64_t k0 = cb->row_col_ptr[cb->series_row_ptr[s]], k1 = cb->row_col_ptr[cb->series_row_ptr[s + 1]];
+    w[s] = (double)(cb->col_qual_off[k1] - cb->col_qual_off[k0]) + (double)(cb->col_val_off[k1] - cb->col_val_off[k0]);
+  }
+  int mode = 0;
+  int64_t G = 0;
+  const std::vector<std::vector<int64_t>> cand = shard_series(m, cb->group_id, w, mode, G);
+  const int n = (int)m->devices.size();
+  struct Sub {
+    std::vector<int64_t> srp{0}, rcp{0}, ts;
+    std::vector<int32_t> gid;
+    std::vector<uint32_t> base;
+    std::vector<uint64_t> qo{0}, vo{0};
+    std::vector<uint8_t> q, v;
+    tsdbhip_cell_batch cb{};
+  };
+  std::vector<Sub> sub(n);
+  for (int d = 0; d < n; d++) {
+    Sub& u = sub[d];
+    for (int64_t s : cand[d]) {
+      for (int64_t r = cb->series_row_ptr[s]; r < cb->series_row_ptr[s + 1]; r++) {
+        u.base.push_back(cb->row_base_time[r]);
+        for (int64_t k = cb->row_col_ptr[r]; k < cb->row_col_ptr[r + 1]; k++) {
+          u.q.insert(u.q.end(), cb->qual + cb->col_qual_off[k], cb->qual + cb->col_qual_off[k + 1]);
+          u.v.insert(u.v.end(), cb->val + cb->col_val_off[k], cb->val + cb->col_val_off[k + 1]);
+          u.qo.push_back(u.q.size());
+          u.vo.push_back(u.v.size());
+          if (cb->col_timestamp) u.ts.push_back(cb->col_timestamp[k]);
+        }
+        u.rcp.push_back((int64_t)u.qo.size() - 1);
+      }
+      u.srp.push_back((int64_t)u.base.size());
+      u.gid.push_back(cb->group_id[s]);
+    }
+    for (auto* x : {&u.q, &u.v}) if (x->empty()) x->push_back(0);
+    if (u.gid.empty()) u.gid.push_back(-1);
+    u.cb = *cb;
+    u.cb.n_series = (int64_t)cand[d].size();
+    u.cb.series_row_ptr = u.srp.data();
+    u.cb.n_rows = (int64_t)u.base.size();
+    u.cb.row_base_time = u.base.empty() ? nullptr : u.base.data();
+    u.cb.row_col_ptr = u.rcp.data();
+    u.cb.n_cols = (int64_t)u.qo.size() - 1;
+    u.cb.col_qual_off = u.qo.data();
+    u.cb.col_val_off = u.vo.data();
+    u.cb.col_timestamp = cb->col_timestamp ? (u.ts.empty() ? u.srp.data() : u.ts.data()) : nullptr;
+    u.cb.qual = u.q.data();
+    u.cb.val = u.v.data();
+    u.cb.group_id = u.gid.data();
+  }
+  ctx_drop_batch(m->root);
+  drop_idle(m);
+  const int rc = each_device(m, [&](int d) { return tsdbhip_load_cells(m->subs[d], &sub[d].cb); });
+  if (rc) {
+    m->live.assign(n, 0);
+    return rc;
+  }
+  m->mode = mode;
+  m->G = G;
+  m->series = cand;
+  return 0;
+}
+
+// Rollup generation (tsdbhip_rollup_run): every device writes the rollup cells of its series
+// (RollupUtils / TSDB.addAggregatePoint's cells, per series -- no exchange); the cells stay on the
+// devices until tsdbhip_rollup_download puts them in the one-GPU order (function, batch series,
+// time).  The spec checks are the one-GPU entry point's (each device applies them).
+int md_rollup_run(tsdbhip_ctx* c, const tsdbhip_rollup_spec* sp, int64_t* n_cells, uint64_t* value_bytes) {
+  MultiDev* m = md_of(c);
+  if (!sp) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  std::lock_guard<std::mutex> lk(ctx_mutex(c));
+  if (m->rollup) return set_error(TSDB_E_NOT_IMPLEMENTED, "tsdbhip_rollup_run over a rollup batch (tsdbhip_load_rollup)");
+  const int n = (int)m->devices.size();
+  reset_stages(m);
+  const double t0 = now_ms();
+  m->ro_valid = false;
+  std::vector<int64_t> nc(n, 0);
+  std::vector<uint64_t> nb(n, 0);
+  const int rc = each_device(m, [&](int d) { return tsdbhip_rollup_run(m->subs[d], sp, &nc[d], &nb[d]); });
+  m->t_dev += now_ms() - t0;
+  if (rc) return rc;
+  m->ro_nf = sp->n_funcs;
+  m->ro_cells.assign(n, std::vector<int64_t>(4, 0));
+  m->ro_bytes.assign(n, std::vector<uint64_t>(4, 0));
+  int64_t cells = 0;
+  uint64_t bytes = 0;
+  for (int d = 0; d < n; d++) {
+    if (!m->live[d]) continue;
+    const int nf = ctx_rollup_parts(m->subs[d], m->ro_cells[d].data(), m->ro_bytes[d].data());
+    if (nf != sp->n_funcs) return set_error(TSDB_E_HIP, "rollup function count differs on a device");
+    cells += nc[d];
+    bytes += nb[d];
+  }
+  m->ro_valid = true;
+  if (n_cells) *n_cells = cells;
+  if (value_bytes) *value_bytes = bytes;
+  device_timing(m, now_ms() - t0, false);
+  return 0;
+}
+
+int md_rollup_download(tsdbhip_ctx* c, int32_t* series, uint32_t* base_time, uint8_t* qualifier, uint64_t* val_off,
+                       uint8_t* value) {
+  MultiDev* m = md_of(c);
+  std::lock_guard<std::mutex> lk(ctx_mutex(c));
+  if (!m->ro_valid) return set_error(TSDB_E_ILLEGAL_STATE, "tsdbhip_rollup_download before tsdbhip_rollup_run");
+  const int n = (int)m->devices.size();
+  struct Part {
+    std::vector<int32_t> ser;
+    std::vector<uint32_t> base;
+    std::vector<uint8_t> qual, val;
+    std::vector<uint64_t> voff;
+  };
+  std::vector<Part> part(n);
+  int rc = each_device(m, [&](int d) {
+    Part& p = part[d];
+    int64_t cells = 0;
+    uint64_t bytes = 0;
+    for (int i = 0; i < m->ro_nf; i++) { cells += m->ro_cells[d][i]; bytes += m->ro_bytes[d][i]; }
+    p.ser.resize(std::max<int64_t>(1, cells));
+    p.base.resize(std::max<int64_t>(1, cells));
+    p.qual.resize(std::max<int64_t>(1, 3 * cells));
+    p.voff.resize(cells + 1);
+    p.val.resize(std::max<uint64_t>(1, bytes));
+    return tsdbhip_rollup_download(m->subs[d], p.ser.data(), p.base.data(), p.qual.data(), p.voff.data(), p.val.data());
+  });
+  if (rc) return rc;
+  // per function, the devices' runs of one series' cells, in global batch-series order (synth
+  // shards and group shards are already in device order; loaded shards interleave batch indices)
+  struct Run { int64_t g; int d; int64_t c0, c1; };
+  int64_t out_c = 0;
+  uint64_t out_b = 0;
+  std::vector<int64_t> f0(n, 0);   // first cell of the current function on each device
+  for (int i = 0; i < m->ro_nf; i++) {
+    std::vector<Run> runs;
+    for (int d = 0; d < n; d++) {
+      if (!m->live[d]) continue;
+      const Part& p = part[d];
+      const int64_t a = f0[d], b = a + m->ro_cells[d][i];
+      for (int64_t k = a; k < b;) {
+        int64_t e = k + 1;
+        while (e < b && p.ser[e] == p.ser[k]) e++;
+        runs.push_back({batch_index(m, d, p.ser[k]), d, k, e});
+        k = e;
+      }
+      f0[d] = b;
+    }
+    if (!m->series.empty())
+      std::stable_sort(runs.begin(), runs.end(), [](const Run& x, const Run& y) { return x.g < y.g; });
+    for (const Run& r : runs) {
+      const Part& p = part[r.d];
+      const int64_t k = r.c1 - r.c0;
+      const uint64_t b0 = p.voff[r.c0], nbytes = p.voff[r.c1] - b0;
+      if (series) for (int64_t j = 0; j < k; j++) series[out_c + j] = (int32_t)r.g;
+      if (base_time) std::copy(p.base.begin() + r.c0, p.base.begin() + r.c1, base_time + out_c);
+      if (qualifier) std::copy(p.qual.begin() + 3 * r.c0, p.qual.begin() + 3 * r.c1, qualifier + 3 * out_c);
+      if (val_off) for (int64_t j = 0; j < k; j++) val_off[out_c + j] = out_b + (p.voff[r.c0 + j] - b0);
+      if (value && nbytes) std::copy(p.val.begin() + b0, p.val.begin() + b0 + nbytes, value + out_b);
+      out_c += k;
+      out_b += nbytes;
+    }
+  }
+  if (val_off) val_off[out_c] = out_b;
   return 0;
 }
 

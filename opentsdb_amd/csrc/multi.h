@@ -20,6 +20,7 @@ int set_error(int code, const std::string& msg);
 tsdbhip_result* new_result(int64_t n_groups, int64_t n_points);
 void ctx_drop_batch(tsdbhip_ctx* c);               // release the resident batch (and rollup state)
 int64_t ctx_n_series(tsdbhip_ctx* c);              // resident series, a rollup batch's count series too
+int ctx_rollup_parts(tsdbhip_ctx* c, int64_t* cells, uint64_t* bytes);   // last rollup_run per function
 std::vector<int64_t> ctx_group_counts(tsdbhip_ctx* c, int64_t G);   // resident series of each group id < G
 void ctx_group_range(tsdbhip_ctx* c, int64_t g, int64_t* p0, int64_t* p1);   // resident positions of group g
 // owner-routed percentile / ordered exchange: span contributions left on the device (room for
@@ -41,6 +42,10 @@ int md_partials_finish(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, unsign
 int md_load(tsdbhip_ctx* c, const tsdbhip_batch* b);
 int md_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp);
 int md_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* rb);
+int md_load_cells(tsdbhip_ctx* c, const tsdbhip_cell_batch* cb);
+int md_rollup_run(tsdbhip_ctx* c, const tsdbhip_rollup_spec* sp, int64_t* n_cells, uint64_t* value_bytes);
+int md_rollup_download(tsdbhip_ctx* c, int32_t* series, uint32_t* base_time, uint8_t* qualifier, uint64_t* val_off,
+                       uint8_t* value);
 int md_run(tsdbhip_ctx* c, const tsdbhip_query* q, tsdbhip_result** out);
 int md_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_result** outs);
 int md_timing(tsdbhip_ctx* c, tsdbhip_timing* out);

@@ -12,7 +12,7 @@ out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
 TR="python -u -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
-C="--steps 5 --warmup 2 --no-pmc --no-cpu-baseline --c3-series 2000000"
+C="--steps 5 --warmup 2 --no-pmc --no-cpu-baseline --c3-series 2000000 --c5-series 1000000"
 for s in $steps; do
   echo "== $s"
   case $s in

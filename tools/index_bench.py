@@ -13,6 +13,9 @@ CONFIGS = {
     "config2": (1_000_000, T0, 3600, 1000, 0, 64, 1),
     "config3_1h": (10_000_000, T0, 360, 10000, 2, 1000, 30000),
     "config1": (1000, T0, 8640, 10000, 1, 1, 2000),
+    # config 3's two row kinds alone (5M one-hour rows each): float32 / vle integers
+    "c3_float": (5_000_000, T0, 360, 10000, 0, 1000, 1),
+    "c3_vle": (5_000_000, T0, 360, 10000, 1, 1000, 30000),
 }
 eng = Engine(0)
 for name in (sys.argv[1:] or CONFIGS):
