@@ -991,11 +991,26 @@ static int finish_load(tsdbhip_ctx* c, const std::vector<RowDesc>& rd) {
   // the int16 copy of 1-2-byte integer values (val2, k_short / k_fast's vle rows) is written by
   // the class kernels of the 2-byte-qualifier integer classes, allocated when such rows exist
   c->val2.release();
+  // val2 allocated up front when it fits beside the batch with room to spare: the short rows are
+  // then indexed by the classifying pass itself (index_fused, no separate k_index_hint); else the
+  // classes first, val2 only when some row can need it (a 216-GB store has no room for a spare 72)
+  bool fused = false;
+  if (!generic) {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > c->qual_bytes + BLOB_SLACK + ((size_t)8 << 30)) {
+      HIP_OK(c->val2.ensure(c->qual_bytes + BLOB_SLACK));
+      fused = true;
+    }
+  }
   HIP_OK(hipEventRecord(c->ev[0], c->stream));
   IndexClasses ik;
-  HIP_OK(index_classes(c->qual.as<uint8_t>(), c->rows.as<RowDesc>(), ib, c->n_rows, &ik, c->stream));
+  if (fused)
+    HIP_OK(index_fused(c->qual.as<uint8_t>(), c->val.as<uint8_t>(), c->val2.as<uint8_t>(), c->rows.as<RowDesc>(), ib,
+                       c->n_rows, c->err.as<int32_t>(), &ik, c->stream));
+  else
+    HIP_OK(index_classes(c->qual.as<uint8_t>(), c->rows.as<RowDesc>(), ib, c->n_rows, &ik, c->stream));
   HIP_OK(hipEventRecord(c->ev[2], c->stream));
-  if (ik.vle_capable && !generic) HIP_OK(c->val2.ensure(c->qual_bytes + BLOB_SLACK));
+  if (!fused && ik.vle_capable && !generic) HIP_OK(c->val2.ensure(c->qual_bytes + BLOB_SLACK));
   HIP_OK(hipEventRecord(c->ev[3], c->stream));   // (the allocation is not index time)
   HIP_OK(index_rows(c->qual.as<uint8_t>(), c->val.as<uint8_t>(), c->val2.as<uint8_t>(), c->rows.as<RowDesc>(), ib, ik,
                     c->n_rows, c->err.as<int32_t>(), generic, c->stream));

@@ -541,7 +541,10 @@ struct IndexClasses {
   uint32_t vle_capable;   // rows of the 2-byte-qualifier integer classes (variable, 1-byte, 2-byte values)
   uint32_t listed;        // rows in the class lists (the class kernels')
   uint32_t short_rows;    // rows k_index_short takes (one chunk, 2-byte qualifiers, 4-byte or 1-2-byte values)
+  bool short_done;        // index_fused: k_index_short has run (classification included)
 };
+hipError_t index_fused(const uint8_t* qual, const uint8_t* val, uint8_t* val2, RowDesc* rows, const IndexBufs& b,
+                       int64_t n_rows, int32_t* err, IndexClasses* out, hipStream_t s);
 hipError_t index_classes(const uint8_t* qual, const RowDesc* rows, const IndexBufs& b, int64_t n_rows,
                          IndexClasses* out, hipStream_t s);
 hipError_t index_rows(const uint8_t* qual, const uint8_t* val, uint8_t* val2, RowDesc* rows, const IndexBufs& b,

@@ -38,6 +38,12 @@ static constexpr uint8_t HINT_SHORT = 0x80;   // hint bit: the row is k_index_sh
 // IndexBufs.cnt slots past the classes: k_index_short's rows (4-byte values / 1-2-byte integers)
 // and the rows it handed back to k_index_generic
 static constexpr int IDX_C_SHORT4 = 12, IDX_C_SHORTV = 13, IDX_C_FAIL = 14;
+#ifndef IDX_SHORT_D
+#define IDX_SHORT_D 2   // k_index_short's load ring depth
+#endif
+#ifndef IDX_SHORT_BLOCKS
+#define IDX_SHORT_BLOCKS 16384   // k_index_short's grid cap (4 waves a block, 64-row batches grid-strided)
+#endif
 
 struct IdxAcc {
   bool bad, allf, alli, vmax2, nan, negz, unsorted;
@@ -752,10 +758,284 @@ __device__ __forceinline__ void short_issue(const uint8_t* __restrict__ qual, co
   ld.v1 = *reinterpret_cast<const uint4*>(val + vb + (u4 ? 16 : 0));
 }
 
+// Row j's results (every lane calls it; the values are wave-uniform).
+static constexpr uint32_t SHORT_FAIL = 0x80000000u;   // (a result flag of k_index_short's batch, not a RowDesc flag)
+struct ShortRes {
+  uint32_t flags;
+  int32_t lsb;
+  double amax;
+  bool fail;
+};
+
+__device__ __forceinline__ ShortRes short_row_general(const ShortLd& ld, uint8_t* __restrict__ val2, const uint8_t* st8,
+                                                      uint4* stage, uint64_t cq, uint32_t cn, uint32_t cvl, bool cu4) {
+  const int lane = lane_id();
+  const int i0 = lane * DPL;
+  const int nin = min(DPL, max(0, (int)cn - i0));
+  uint32_t qq[DPL];
+  {
+    const uint32_t ws[4] = {ld.q.x, ld.q.y, ld.q.z, ld.q.w};
+#pragma unroll
+    for (int k = 0; k < DPL; k++) {
+      const uint32_t b = __builtin_bswap32(ws[k >> 1]);
+      qq[k] = (k & 1) ? (b & 0xFFFF) : (b >> 16);
+    }
+  }
+  bool fail = false, bad = false, uns = false;
+  uint32_t fl_or = 0, fl_and = 8;
+  int len[DPL], lsum = 0, lmin = 99, lmax = -1;
+  int prev = -1;
+#pragma unroll
+  for (int k = 0; k < DPL; k++) {
+    const bool in = k < nin;
+    const uint32_t f = qq[k] & 8;
+    len[k] = in ? (int)(qq[k] & 7) + 1 : 0;
+    fail |= in & ((qq[k] >> 12) == 0xF);                    // a 4-byte qualifier inside
+    fl_or |= in ? f : 0u;
+    fl_and &= in ? f : 8u;
+    lsum += len[k];
+    lmin = min(lmin, in ? len[k] : 99);
+    lmax = max(lmax, in ? len[k] : -1);
+    const int off = (int)(qq[k] >> 4);                       // seconds: strictly increasing
+    uns |= in & (k > 0) & (off <= prev);
+    prev = in ? off : prev;
+  }
+  {   // order across lanes: this lane's first offset against the previous lane's last
+    const int last = (int)(qq[max(0, nin - 1)] >> 4);
+    const int pl = __builtin_amdgcn_update_dpp(-1, nin > 0 ? last : -1, 0x138, 0xF, 0xF, false);   // wave_shr:1
+    uns |= (lane > 0) & (nin > 0) & ((int)(qq[0] >> 4) <= pl);
+  }
+  uint32_t flags = 2;
+  int lsb = INT32_MAX;
+  uint32_t amax_bits = 0;   // float32 |x| bits, or |int32|
+  bool isf = false, nan = false, negz = false;
+  if (cu4) {
+    // ---- 4-byte values: float32 or int32
+#pragma unroll
+    for (int k = 0; k < DPL; k++) fail |= (k < nin) & (len[k] != 4);
+    const bool allf = __all(fl_and != 0), alli = __all(fl_or == 0);
+    fail |= !allf && !alli;                                  // floats and integers mixed: generic
+    isf = allf;
+    const uint32_t vw[8] = {ld.v0.x, ld.v0.y, ld.v0.z, ld.v0.w, ld.v1.x, ld.v1.y, ld.v1.z, ld.v1.w};
+#pragma unroll
+    for (int k = 0; k < DPL; k++) {
+      const bool in = k < nin;
+      const uint32_t be = __builtin_bswap32(vw[k]);
+      // float32: bit-pattern statistics; int32: magnitude and trailing zeros (branch-free select)
+      const uint32_t ab = be & 0x7FFFFFFFu;
+      const bool isn = allf & (ab > 0x7F800000u);
+      const uint32_t E = ab >> 23, M = ab & 0x7FFFFFu;
+      const int lf = E == 0 ? (int)__builtin_ctz(M | 0x80000000u) - 149 : (int)E - 150 + (int)__builtin_ctz(M | 0x800000u);
+      const uint32_t ai = (int32_t)be < 0 ? 0u - be : be;
+      const uint32_t mag = allf ? ab : ai;
+      const bool ok = in & !isn & (mag != 0) & (!allf | (E != 0xFF));
+      nan |= in & isn;
+      negz |= allf & in & (be == 0x80000000u);
+      amax_bits = max(amax_bits, (in & !isn) ? mag : 0u);
+      lsb = min(lsb, ok ? (allf ? lf : (int)__builtin_ctz(ai)) : INT32_MAX);
+    }
+    flags |= (4u << ROW_VL_SHIFT) | (allf ? ROW_ALLF : 0u) | (alli ? ROW_ALLI : 0u);
+  } else {
+    // ---- 1-2-byte integers: stage the value bytes, each lane's start by prefix sum
+    fail |= (fl_or != 0) | (lmax > 2);
+    const int incl = wave_incl_sum_dpp(lsum);
+    const int total = __builtin_amdgcn_readlane(incl, 63);
+    bad |= lane == 0 && (uint32_t)total > cvl;              // values past the row's value bytes
+    // (LDS order within the wave: the previous row's reads are done before this write lands,
+    // and the write before the reads below -- lgkmcnt waits, no memory fence)
+    __builtin_amdgcn_wave_barrier();
+    stage[lane] = ld.v0;
+    __builtin_amdgcn_s_waitcnt(0xC07F);                     // lgkmcnt(0), vmcnt / expcnt untouched
+    __builtin_amdgcn_wave_barrier();
+    const int b = min(incl - lsum, 1024);
+    const int b8 = b & ~7, d = (b - b8) * 8;
+    const uint64_t x0 = *reinterpret_cast<const uint64_t*>(st8 + b8);
+    const uint64_t x1 = *reinterpret_cast<const uint64_t*>(st8 + b8 + 8);
+    const uint64_t x2 = *reinterpret_cast<const uint64_t*>(st8 + b8 + 16);
+    uint64_t lo = d ? (x0 >> d) | (x1 << (64 - d)) : x0;
+    uint64_t hi = d ? (x1 >> d) | (x2 << (64 - d)) : x1;
+    uint32_t h16[4] = {0, 0, 0, 0};
+    uint32_t imax = 0;
+    const int vend = (int)((cvl + 15) & ~15u);   // (k_index_cls decodes up to the 16-B-aligned extent)
+    int pos = b;
+#pragma unroll
+    for (int k = 0; k < DPL; k++) {
+      const int L = len[k];
+      // big-endian: first byte most significant
+      const uint32_t b0 = (uint32_t)lo & 0xFF, b1 = (uint32_t)(lo >> 8) & 0xFF;
+      const int32_t xv = L == 2 ? (int32_t)(int16_t)(uint16_t)((b0 << 8) | b1) : (int32_t)(int8_t)(uint8_t)b0;
+      const int32_t x = pos + L <= vend ? xv : 0;
+      pos += L;
+      const uint32_t ax = x < 0 ? 0u - (uint32_t)x : (uint32_t)x;
+      const bool ok = (k < nin) & (ax != 0);
+      imax = max(imax, ok ? ax : 0u);
+      lsb = min(lsb, ok ? (int)__builtin_ctz(ax) : INT32_MAX);
+      h16[k >> 1] |= ((uint32_t)x & 0xFFFF) << ((k & 1) * 16);
+      const int sh = 8 * max(L, 1);
+      if (L) {
+        lo = (lo >> sh) | (hi << (64 - sh));
+        hi >>= sh;
+      }
+    }
+    amax_bits = imax;
+    if (val2 && nin > 0)
+      *reinterpret_cast<uint4*>(val2 + cq + 2 * (uint64_t)i0) = make_uint4(h16[0], h16[1], h16[2], h16[3]);
+    const int wl = wave_reduce_i32(lmin, 99, [](int a, int c) { return min(a, c); });
+    const int wh = wave_reduce_i32(lmax, -1, [](int a, int c) { return max(a, c); });
+    flags |= ROW_ALLI | ROW_VLE2 | (wl == wh ? (uint32_t)wl << ROW_VL_SHIFT : 0u);
+  }
+  ShortRes R;
+  R.fail = __any(fail);
+  R.lsb = wave_reduce_i32(lsb, INT32_MAX, [](int a, int c) { return min(a, c); });
+  const uint32_t wmax = (uint32_t)wave_reduce_i32((int)amax_bits, 0,
+                                                  [](int a, int c) { return (int)max((uint32_t)a, (uint32_t)c); });
+  R.amax = isf ? (double)__uint_as_float(wmax) : (double)wmax;
+  if (__any(bad)) flags |= ROW_ERR;
+  if (__any(nan)) flags |= ROW_NAN;
+  if (__any(negz)) flags |= ROW_NEGZ;
+  if (__any(uns)) flags |= ROW_UNSORTED;
+  R.flags = flags;   // (ROW_NOCERT: k_index_short, per lane at the batch end)
+  return R;
+}
+
+
+// ---- full-lane fast paths: every lane 0 or 8 datapoints (rows of a multiple of 8, 360 among them)
+// The common rows' premises checked on packed qualifier words (two 2-byte qualifiers a word)
+// and value bit patterns; false = a premise fails (a flag nibble off the class, offsets not
+// strictly increasing or a 4-byte qualifier, NaN, a denormal, values past the row, ...) and
+// short_row_general decodes the row -- whose results these equal wherever they return true.
+__device__ __forceinline__ bool short_full_order(const uint32_t t[4], bool act) {
+  uint32_t o[DPL];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    o[2 * i] = t[i] >> 20;
+    o[2 * i + 1] = (t[i] >> 4) & 0xFFF;
+  }
+  bool inc = true;
+#pragma unroll
+  for (int k = 1; k < DPL; k++) inc &= o[k - 1] < o[k];
+  const int pl = __builtin_amdgcn_update_dpp(-1, act ? (int)o[DPL - 1] : -1, 0x138, 0xF, 0xF, false);   // wave_shr:1
+  // (a 2-byte qualifier's offset field is below 0xF00: a top nibble 0xF is a 4-byte qualifier)
+  return inc & ((int)o[0] > pl) & (o[DPL - 1] < 0xF00u);
+}
+
+__device__ __forceinline__ bool short_full_u4(const ShortLd& ld, bool act, ShortRes& R) {
+  const uint32_t t[4] = {__builtin_bswap32(ld.q.x), __builtin_bswap32(ld.q.y), __builtin_bswap32(ld.q.z),
+                         __builtin_bswap32(ld.q.w)};
+  // float32 of 4 bytes everywhere: flag nibble 0xB
+  const uint32_t fx = ((t[0] ^ 0x000B000Bu) | (t[1] ^ 0x000B000Bu) | (t[2] ^ 0x000B000Bu) | (t[3] ^ 0x000B000Bu)) & 0x000F000Fu;
+  const bool ord = short_full_order(t, act);   // (every lane: a DPP step inside)
+  if (!__all(!act || (fx == 0 && ord))) return false;
+  const uint32_t vw[8] = {ld.v0.x, ld.v0.y, ld.v0.z, ld.v0.w, ld.v1.x, ld.v1.y, ld.v1.z, ld.v1.w};
+  uint32_t amax = 0, lsbk = 0xFFFFFFFFu;
+  bool odd = false;
+#pragma unroll
+  for (int k = 0; k < DPL; k++) {
+    const uint32_t be = __builtin_bswap32(vw[k]);
+    const uint32_t ab = be & 0x7FFFFFFFu;
+    const uint32_t E = ab >> 23;
+    amax = max(amax, ab);
+    // normal numbers only: a zero (-0.0 included), a denormal, an infinity or a NaN sends the row
+    // to the general path; the least significant set bit as E + its place in the significand
+    // (-150 once at the end)
+    odd |= (E - 1u) >= 254u;
+    lsbk = min(lsbk, E + (uint32_t)__builtin_ctz(be | 0x00800000u));
+  }
+  if (!act) { amax = 0; lsbk = 0xFFFFFFFFu; odd = false; }
+  if (__any(odd)) return false;
+  const uint32_t wmax = (uint32_t)wave_reduce_i32((int)amax, 0, [](int a, int c) { return (int)max((uint32_t)a, (uint32_t)c); });
+  const uint32_t wl = (uint32_t)wave_reduce_i32((int)lsbk, -1, [](int a, int c) { return (int)min((uint32_t)a, (uint32_t)c); });
+  R.fail = false;
+  R.lsb = wl == 0xFFFFFFFFu ? INT32_MAX : (int)wl - 150;
+  R.amax = (double)__uint_as_float(wmax);
+  R.flags = 2u | (4u << ROW_VL_SHIFT) | ROW_ALLF;
+  return true;
+}
+
+__device__ __forceinline__ bool short_full_vle(const ShortLd& ld, uint8_t* __restrict__ val2, const uint8_t* st8,
+                                               uint4* stage, uint64_t cq, uint32_t cvl, bool act, ShortRes& R) {
+  const int lane = lane_id();
+  const uint32_t t[4] = {__builtin_bswap32(ld.q.x), __builtin_bswap32(ld.q.y), __builtin_bswap32(ld.q.z),
+                         __builtin_bswap32(ld.q.w)};
+  // integers of 1 or 2 bytes everywhere: flag nibble 0 or 1
+  const uint32_t fx = (t[0] | t[1] | t[2] | t[3]) & 0x000E000Eu;
+  const bool ord = short_full_order(t, act);   // (every lane: a DPP step inside)
+  if (!__all(!act || (fx == 0 && ord))) return false;
+  // 2-byte values: bit k of lb (datapoint k of the lane)
+  uint32_t lb = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) lb |= (((t[i] >> 16) & 1u) << (2 * i)) | ((t[i] & 1u) << (2 * i + 1));
+  const int lsum = act ? DPL + __builtin_popcount(lb) : 0;
+  const int incl = wave_incl_sum_dpp(lsum);
+  const int total = __builtin_amdgcn_readlane(incl, 63);
+  if ((uint32_t)total > cvl) return false;   // values past the row's bytes: the general path flags the row
+  __builtin_amdgcn_wave_barrier();
+  stage[lane] = ld.v0;
+  __builtin_amdgcn_s_waitcnt(0xC07F);        // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  // the lane's 16 value bytes from byte b: five staged dwords, funnel-shifted by b & 3
+  const int b = min(incl - lsum, 1024);
+  const uint32_t* sw = reinterpret_cast<const uint32_t*>(st8) + (b >> 2);
+  const uint32_t sh = (uint32_t)(b & 3);
+  const uint32_t d0 = sw[0], d1 = sw[1], d2 = sw[2], d3 = sw[3], d4 = sw[4];
+  uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+  uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh), w3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+  int32_t mx = INT32_MIN, mn = INT32_MAX, xp = 0;
+  uint32_t ox = 0, h16[4];
+#pragma unroll
+  for (int k = 0; k < DPL; k++) {
+    const uint32_t two = (lb >> k) & 1u;
+    // big-endian: one byte, or two with the first the more significant
+    const int32_t x1 = (int32_t)(int8_t)(uint8_t)w0;
+    const int32_t x2 = (int32_t)(int16_t)(uint16_t)__builtin_amdgcn_perm(w0, w0, 0x0C0C0001u);
+    const int32_t x = two ? x2 : x1;
+    ox |= (uint32_t)x;          // ctz of the OR = the least significant set bit over the values
+    mx = max(mx, x);
+    mn = min(mn, x);
+    if (k & 1) h16[k >> 1] = __builtin_amdgcn_perm((uint32_t)x, (uint32_t)xp, 0x05040100u);   // (x << 16) | (xp & 0xFFFF)
+    xp = x;
+    // consume 1 or 2 bytes (the upper words only while later values can still reach them)
+    const uint32_t s = 1u + two;
+    w0 = __builtin_amdgcn_alignbyte(w1, w0, s);
+    if (k < 6) w1 = __builtin_amdgcn_alignbyte(w2, w1, s);
+    if (k < 4) w2 = __builtin_amdgcn_alignbyte(w3, w2, s);
+    if (k < 2) w3 = w3 >> (8 * s);
+  }
+  if (val2 && act)
+    *reinterpret_cast<uint4*>(val2 + cq + 16 * (uint64_t)lane) = make_uint4(h16[0], h16[1], h16[2], h16[3]);
+  uint32_t imax = (uint32_t)max(mx, -mn);   // |x| <= 32768
+  uint32_t lsbk = ox ? (uint32_t)__builtin_ctz(ox) : 0xFFFFFFFFu;
+  if (!act) { imax = 0; lsbk = 0xFFFFFFFFu; }
+  const uint32_t wmax = (uint32_t)wave_reduce_i32((int)imax, 0, [](int a, int c) { return (int)max((uint32_t)a, (uint32_t)c); });
+  const uint32_t wl = (uint32_t)wave_reduce_i32((int)lsbk, -1, [](int a, int c) { return (int)min((uint32_t)a, (uint32_t)c); });
+  const bool all1 = __all(!act || lb == 0), all2 = __all(!act || lb == 0xFFu);
+  R.fail = false;
+  R.lsb = wl == 0xFFFFFFFFu ? INT32_MAX : (int)wl;
+  R.amax = (double)wmax;
+  R.flags = 2u | ROW_ALLI | ROW_VLE2 | (all1 ? 1u << ROW_VL_SHIFT : all2 ? 2u << ROW_VL_SHIFT : 0u);
+  return true;
+}
+
+__device__ __forceinline__ ShortRes short_row(const ShortLd& ld, uint8_t* __restrict__ val2, const uint8_t* st8,
+                                              uint4* stage, uint64_t cq, uint32_t cn, uint32_t cvl, bool cu4) {
+  const int nin = min(DPL, max(0, (int)cn - lane_id() * DPL));
+  ShortRes R;
+  if (__all(nin == 0 || nin == DPL)) {
+    if (cu4 ? short_full_u4(ld, nin > 0, R) : short_full_vle(ld, val2, st8, stage, cq, cvl, nin > 0, R)) return R;
+  }
+  return short_row_general(ld, val2, st8, stage, cq, cn, cvl, cu4);
+}
+
+// SD: the load ring's depth (rows in flight while one decodes); 64 is a multiple of it.
+// CLS: the kernel classifies every row itself (k_index_hint's rule, from the batch's descriptors
+// already in its lanes) and writes every hint and class count (cnt) -- no separate hint pass.
+template <int SD, bool CLS>
 __global__ __launch_bounds__(256) void k_index_short(const uint8_t* __restrict__ qual, const uint8_t* __restrict__ val,
                                                      uint8_t* __restrict__ val2, RowDesc* __restrict__ rows,
-                                                     uint8_t* __restrict__ hint, int64_t n_rows, uint32_t* fails,
+                                                     uint8_t* __restrict__ hint, int64_t n_rows, uint32_t* cnt,
                                                      int32_t* err) {
+  uint32_t* fails = cnt + IDX_C_FAIL;
+  static_assert(64 % SD == 0, "ring depth divides the 64-row batch");
   __shared__ uint4 stage_all[4][66];   // per wave: 1 KB of value bytes + a 32-B tail
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -766,11 +1046,13 @@ __global__ __launch_bounds__(256) void k_index_short(const uint8_t* __restrict__
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t t = (int64_t)blockIdx.x * 4 + wv; t < n_tiles; t += nw) {
     const int64_t r = (t << 6) + lane;
-    const uint8_t h = r < n_rows ? hint[r] : 0;
-    const bool mine = (h & HINT_SHORT) != 0;
+    uint8_t h = (!CLS && r < n_rows) ? hint[r] : 0;
+    if (!CLS && !__any(h & HINT_SHORT)) continue;
+    // lane l: row l's descriptor (rows not this kernel's keep their own valid offsets: the ring
+    // issues their loads too, unused, so that every slot issues the same loads)
     uint64_t qoff = 0, voff = 0;
     uint32_t qlen = 0, vlen = 0, fin = 0;
-    if (mine) {
+    if (r < n_rows) {
       const RowDesc& d = rows[r];
       qoff = d.qoff;
       voff = d.voff;
@@ -778,188 +1060,82 @@ __global__ __launch_bounds__(256) void k_index_short(const uint8_t* __restrict__
       vlen = d.vlen;
       fin = d.flags;
     }
+    if constexpr (CLS) {   // k_index_hint's classification, and the batch's class counts
+      int slot = -1;
+      if (r < n_rows) {
+        int cls = 0;
+        bool sh = false;
+        if (qlen > 0) {
+          const uint32_t w = *reinterpret_cast<const uint32_t*>(qual + qoff);   // qoff is 16-B aligned
+          const int qw = (w & 0xF0) == 0xF0 ? 4 : 2;
+          if (qlen % qw == 0) {
+            const uint32_t L = ((w >> (8 * (qw - 1))) & 7) + 1;
+            const uint64_t ndp = qlen / qw;
+            const bool uni = (L == 1 || L == 2 || L == 4 || L == 8) && (uint64_t)vlen == ndp * L + (ndp > 1 ? 1 : 0);
+            cls = idx_cls(qw, uni ? (int)L : 0);
+            sh = idx_short_ok(qw, L, ndp, vlen, uni);
+          }
+        }
+        h = (uint8_t)(cls | (sh ? HINT_SHORT : 0));
+        slot = sh ? (cls == idx_cls(2, 4) ? IDX_C_SHORT4 : IDX_C_SHORTV) : cls;
+      }
+      for (int c = 0; c < 16; c++) {
+        const uint64_t m = __ballot(slot == c);
+        if (m && lane == 0) atomicAdd(&cnt[c], (uint32_t)__popcll(m));
+      }
+      if (r < n_rows && !(h & HINT_SHORT)) hint[r] = h;
+    }
+    const bool mine = (h & HINT_SHORT) != 0;
+    const uint64_t todo = __ballot(mine);
+    if (CLS && !todo) continue;
+    if (!mine) qlen = 0;
     const uint32_t u4m = (uint32_t)((h & 0x7F) == idx_cls(2, 4));
-    uint64_t todo = __ballot(mine);
-    // this lane's row's results
-    uint32_t o_flags = 0;
+    uint32_t o_flags = 0, o_alo = 0, o_ahi = 0;
     int32_t o_lsb = INT32_MAX;
-    double o_amax = 0.0;
-    bool o_fail = false;
-    if (todo) {
-      int j = __ffsll((long long)todo) - 1;
-      auto fields = [&](int jj, uint64_t& qo, uint64_t& vo, uint32_t& nd, uint32_t& vl, bool& u4) {
-        qo = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(qoff >> 32), jj) << 32) |
-             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)qoff, jj);
-        vo = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(voff >> 32), jj) << 32) |
-             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)voff, jj);
-        nd = (uint32_t)__builtin_amdgcn_readlane((int)qlen, jj) >> 1;
-        vl = (uint32_t)__builtin_amdgcn_readlane((int)vlen, jj);
-        u4 = __builtin_amdgcn_readlane((int)u4m, jj) != 0;
-      };
-      uint64_t cq, cv;
-      uint32_t cn, cvl;
-      bool cu4;
-      fields(j, cq, cv, cn, cvl, cu4);
-      ShortLd ld;
-      short_issue(qual, val, cq, cv, cn, cu4, ld);
-      for (;;) {
-        todo &= todo - 1;
-        const int jn = todo ? __ffsll((long long)todo) - 1 : j;
-        uint64_t nq, nv;
-        uint32_t nn, nvl;
-        bool nu4;
-        fields(jn, nq, nv, nn, nvl, nu4);
-        ShortLd nl;
-        short_issue(qual, val, nq, nv, nn, nu4, nl);
-        // ---- row j: qualifiers
-        const int i0 = lane * DPL;
-        const int nin = min(DPL, max(0, (int)cn - i0));
-        uint32_t qq[DPL];
-        {
-          const uint32_t ws[4] = {ld.q.x, ld.q.y, ld.q.z, ld.q.w};
+    auto issue = [&](int jj, ShortLd& ld) {
+      const uint64_t qo = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(qoff >> 32), jj) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)qoff, jj);
+      const uint64_t vo = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(voff >> 32), jj) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)voff, jj);
+      short_issue(qual, val, qo, vo, (uint32_t)__builtin_amdgcn_readlane((int)qlen, jj) >> 1,
+                  __builtin_amdgcn_readlane((int)u4m, jj) != 0, ld);
+    };
+    ShortLd buf[SD];
 #pragma unroll
-          for (int k = 0; k < DPL; k++) {
-            const uint32_t b = __builtin_bswap32(ws[k >> 1]);
-            qq[k] = (k & 1) ? (b & 0xFFFF) : (b >> 16);
-          }
-        }
-        bool fail = false, bad = false, uns = false;
-        uint32_t fl_or = 0, fl_and = 8;
-        int len[DPL], lsum = 0, lmin = 99, lmax = -1;
-        int prev = -1;
+    for (int i = 0; i < SD; i++) issue(i, buf[i]);
+    for (int j0 = 0; j0 < 64; j0 += SD) {
 #pragma unroll
-        for (int k = 0; k < DPL; k++) {
-          const bool in = k < nin;
-          const uint32_t f = qq[k] & 8;
-          len[k] = in ? (int)(qq[k] & 7) + 1 : 0;
-          fail |= in & ((qq[k] >> 12) == 0xF);                    // a 4-byte qualifier inside
-          fl_or |= in ? f : 0u;
-          fl_and &= in ? f : 8u;
-          lsum += len[k];
-          lmin = min(lmin, in ? len[k] : 99);
-          lmax = max(lmax, in ? len[k] : -1);
-          const int off = (int)(qq[k] >> 4);                       // seconds: strictly increasing
-          uns |= in & (k > 0) & (off <= prev);
-          prev = in ? off : prev;
+      for (int i = 0; i < SD; i++) {
+        const int j = j0 + i;
+        if ((todo >> j) & 1) {   // (wave-uniform)
+          const uint64_t cq = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(qoff >> 32), j) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)qoff, j);
+          const ShortRes R = short_row(buf[i], val2, st8, stage, cq, (uint32_t)__builtin_amdgcn_readlane((int)qlen, j) >> 1,
+                                       (uint32_t)__builtin_amdgcn_readlane((int)vlen, j),
+                                       __builtin_amdgcn_readlane((int)u4m, j) != 0);
+          // the row's (uniform) results into lane j
+          const uint64_t ab = (uint64_t)__double_as_longlong(R.amax);
+          const bool me = lane == j;
+          o_flags = me ? (R.flags | (R.fail ? SHORT_FAIL : 0u)) : o_flags;
+          o_lsb = me ? R.lsb : o_lsb;
+          o_alo = me ? (uint32_t)ab : o_alo;
+          o_ahi = me ? (uint32_t)(ab >> 32) : o_ahi;
         }
-        {   // order across lanes: this lane's first offset against the previous lane's last
-          const int last = (int)(qq[max(0, nin - 1)] >> 4);
-          const int pl = __shfl_up(nin > 0 ? last : -1, 1, 64);
-          uns |= (lane > 0) & (nin > 0) & ((int)(qq[0] >> 4) <= pl);
-        }
-        uint32_t flags = 2;
-        int lsb = INT32_MAX;
-        uint32_t amax_bits = 0;   // float32 |x| bits, or |int32|
-        bool isf = false, nan = false, negz = false;
-        if (cu4) {
-          // ---- 4-byte values: float32 or int32
-#pragma unroll
-          for (int k = 0; k < DPL; k++) fail |= (k < nin) & (len[k] != 4);
-          const bool allf = __all(fl_and != 0), alli = __all(fl_or == 0);
-          fail |= !allf && !alli;                                  // floats and integers mixed: generic
-          isf = allf;
-          const uint32_t vw[8] = {ld.v0.x, ld.v0.y, ld.v0.z, ld.v0.w, ld.v1.x, ld.v1.y, ld.v1.z, ld.v1.w};
-#pragma unroll
-          for (int k = 0; k < DPL; k++) {
-            const bool in = k < nin;
-            const uint32_t be = __builtin_bswap32(vw[k]);
-            if (allf) {
-              const uint32_t ab = be & 0x7FFFFFFFu;
-              const bool isn = ab > 0x7F800000u;
-              const bool ok = in & !isn;
-              nan |= in & isn;
-              negz |= ok & (be == 0x80000000u);
-              amax_bits = max(amax_bits, ok ? ab : 0u);
-              const uint32_t E = ab >> 23, M = ab & 0x7FFFFFu;
-              const int lj = E == 0 ? (int)__builtin_ctz(M | 0x80000000u) - 149 : (int)E - 150 + (int)__builtin_ctz(M | 0x800000u);
-              lsb = min(lsb, (ok & (ab != 0) & (E != 0xFF)) ? lj : INT32_MAX);
-            } else {
-              const int32_t x = (int32_t)be;
-              const uint32_t ax = x < 0 ? 0u - (uint32_t)x : (uint32_t)x;
-              const bool ok = in & (ax != 0);
-              amax_bits = max(amax_bits, ok ? ax : 0u);
-              lsb = min(lsb, ok ? (int)__builtin_ctz(ax) : INT32_MAX);
-            }
-          }
-          flags |= (4u << ROW_VL_SHIFT) | (allf ? ROW_ALLF : 0u) | (alli ? ROW_ALLI : 0u);
-        } else {
-          // ---- 1-2-byte integers: stage the value bytes, each lane's start by prefix sum
-          fail |= (fl_or != 0) | (lmax > 2);
-          const int incl = wave_incl_sum_dpp(lsum);
-          const int total = __builtin_amdgcn_readlane(incl, 63);
-          bad |= lane == 0 && (uint32_t)total > cvl;              // values past the row's value bytes
-          WAVE_SYNC();
-          stage[lane] = ld.v0;
-          WAVE_SYNC();
-          const int b = min(incl - lsum, 1024);
-          const int b8 = b & ~7, d = (b - b8) * 8;
-          const uint64_t x0 = *reinterpret_cast<const uint64_t*>(st8 + b8);
-          const uint64_t x1 = *reinterpret_cast<const uint64_t*>(st8 + b8 + 8);
-          const uint64_t x2 = *reinterpret_cast<const uint64_t*>(st8 + b8 + 16);
-          uint64_t lo = d ? (x0 >> d) | (x1 << (64 - d)) : x0;
-          uint64_t hi = d ? (x1 >> d) | (x2 << (64 - d)) : x1;
-          uint32_t h16[4] = {0, 0, 0, 0};
-          uint32_t imax = 0;
-          const int vend = (int)((cvl + 15) & ~15u);   // (k_index_cls decodes up to the 16-B-aligned extent)
-          int pos = b;
-#pragma unroll
-          for (int k = 0; k < DPL; k++) {
-            const int L = len[k];
-            // big-endian: first byte most significant
-            const uint32_t b0 = (uint32_t)lo & 0xFF, b1 = (uint32_t)(lo >> 8) & 0xFF;
-            const int32_t xv = L == 2 ? (int32_t)(int16_t)(uint16_t)((b0 << 8) | b1) : (int32_t)(int8_t)(uint8_t)b0;
-            const int32_t x = pos + L <= vend ? xv : 0;
-            pos += L;
-            const uint32_t ax = x < 0 ? 0u - (uint32_t)x : (uint32_t)x;
-            const bool ok = (k < nin) & (ax != 0);
-            imax = max(imax, ok ? ax : 0u);
-            lsb = min(lsb, ok ? (int)__builtin_ctz(ax) : INT32_MAX);
-            h16[k >> 1] |= ((uint32_t)x & 0xFFFF) << ((k & 1) * 16);
-            const int sh = 8 * max(L, 1);
-            if (L) {
-              lo = (lo >> sh) | (hi << (64 - sh));
-              hi >>= sh;
-            }
-          }
-          amax_bits = imax;
-          if (val2 && nin > 0)
-            *reinterpret_cast<uint4*>(val2 + cq + 2 * (uint64_t)i0) = make_uint4(h16[0], h16[1], h16[2], h16[3]);
-          const int wl = wave_min(lmin), wh = wave_max(lmax);
-          flags |= ROW_ALLI | ROW_VLE2 | (wl == wh ? (uint32_t)wl << ROW_VL_SHIFT : 0u);
-        }
-        // ---- row results
-        const bool rfail = __any(fail);
-        const int wlsb = wave_reduce_i32(lsb, INT32_MAX, [](int a, int c) { return min(a, c); });
-        const uint32_t wmax = (uint32_t)wave_reduce_i32((int)amax_bits, 0,
-                                                        [](int a, int c) { return (int)max((uint32_t)a, (uint32_t)c); });
-        const double amax = isf ? (double)__uint_as_float(wmax) : (double)wmax;
-        if (__any(bad)) flags |= ROW_ERR;
-        if (__any(nan)) flags |= ROW_NAN;
-        if (__any(negz)) flags |= ROW_NEGZ;
-        if (__any(uns)) flags |= ROW_UNSORTED;
-        if (row_nocert(wlsb, amax)) flags |= ROW_NOCERT;
-        if (lane == j) {
-          o_flags = flags | (fin & ROW_SFIRST);
-          o_lsb = wlsb;
-          o_amax = amax;
-          o_fail = rfail;
-        }
-        if (!todo) break;
-        j = jn;
-        cq = nq; cv = nv; cn = nn; cvl = nvl; cu4 = nu4;
-        ld = nl;
+        issue(min(j + SD, 63), buf[i]);
       }
     }
     if (mine) {
-      if (o_fail) {
+      if (o_flags & SHORT_FAIL) {
         hint[r] = 0;   // k_index_generic takes the row
         atomicAdd(fails, 1u);
       } else {
+        if (CLS) hint[r] = h;
+        const double amax = __longlong_as_double((long long)(((uint64_t)o_ahi << 32) | o_alo));
         RowDesc& o = rows[r];
         o.ndp = qlen >> 1;
-        o.flags = o_flags;
+        o.flags = (o_flags | (fin & ROW_SFIRST)) | (row_nocert(o_lsb, amax) ? ROW_NOCERT : 0u);
         o.lsb = o_lsb;
-        o.absmax = o_amax;
+        o.absmax = amax;
         if (o_flags & ROW_ERR) set_err(err, TSDB_E_ILLEGAL_DATA);
       }
     }
@@ -1033,6 +1209,40 @@ hipError_t index_classes(const uint8_t* qual, const RowDesc* rows, const IndexBu
   return hipGetLastError();
 }
 
+// index_classes + k_index_short in one pass over the batch (val2 allocated up front): the short
+// rows indexed while the rest are classified; then, only if some row is not short, the class
+// row lists.  index_rows runs the rest (class kernels, k_index_generic).
+hipError_t index_fused(const uint8_t* qual, const uint8_t* val, uint8_t* val2, RowDesc* rows, const IndexBufs& b,
+                       int64_t n_rows, int32_t* err, IndexClasses* out, hipStream_t s) {
+  *out = IndexClasses{};
+  if (n_rows == 0) return hipSuccess;
+  if (n_rows > 0x7FFFFFFFLL) return hipErrorInvalidValue;   // int32 row lists
+  hipError_t e;
+  if ((e = hipMemsetAsync(b.cnt, 0, 16 * 4, s)) != hipSuccess) return e;
+  const int64_t tiles = (n_rows + 63) / 64;
+  hipLaunchKernelGGL((k_index_short<IDX_SHORT_D, true>), dim3((unsigned)std::min<int64_t>((tiles + 3) / 4, IDX_SHORT_BLOCKS)),
+                     dim3(256), 0, s, qual, val, val2, rows, b.hint, n_rows, b.cnt, err);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  uint32_t cnt[16] = {}, cur[16] = {};
+  if ((e = hipMemcpyAsync(cnt, b.cnt, 16 * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+  for (int c = 0; c < 16; c++) out->cnt[c] = cnt[c];
+  for (int c = 2; c < IDX_NCLS; c++) out->off[c] = out->off[c - 1] + cnt[c - 1];
+  for (int c = 1; c < IDX_NCLS; c++) out->listed += cnt[c];
+  out->short_rows = cnt[IDX_C_SHORT4] + cnt[IDX_C_SHORTV];
+  out->short_done = true;
+  out->vle_capable = cnt[idx_cls(2, 0)] + cnt[idx_cls(2, 1)] + cnt[idx_cls(2, 2)] + cnt[IDX_C_SHORTV];
+  if (out->listed) {   // class row lists; the hand-back counter (k_index_generic's early-out) kept
+    for (int c = 0; c < 16; c++) cur[c] = out->off[c];
+    cur[IDX_C_FAIL] = cnt[IDX_C_FAIL];
+    if ((e = hipMemcpyAsync(b.cnt, cur, 16 * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    const unsigned tb = (unsigned)((n_rows + 255) / 256);
+    hipLaunchKernelGGL(k_index_scatter, dim3(tb), dim3(256), 0, s, b.hint, n_rows, b.cnt, b.list);
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;   // `cur` leaves scope
+  }
+  return hipGetLastError();
+}
+
 hipError_t index_rows(const uint8_t* qual, const uint8_t* val, uint8_t* val2, RowDesc* rows, const IndexBufs& b,
                       const IndexClasses& k, int64_t n_rows, int32_t* err, bool generic, hipStream_t s) {
   if (n_rows == 0) return hipSuccess;
@@ -1043,10 +1253,10 @@ hipError_t index_rows(const uint8_t* qual, const uint8_t* val, uint8_t* val2, Ro
     return hipGetLastError();
   }
   hipError_t e;
-  if (k.short_rows) {
+  if (k.short_rows && !k.short_done) {
     const int64_t tiles = (n_rows + 63) / 64;
-    hipLaunchKernelGGL(k_index_short, dim3((unsigned)std::min<int64_t>((tiles + 3) / 4, 16384)), dim3(256), 0, s, qual,
-                       val, val2, rows, b.hint, n_rows, b.cnt + IDX_C_FAIL, err);
+    hipLaunchKernelGGL((k_index_short<IDX_SHORT_D, false>), dim3((unsigned)std::min<int64_t>((tiles + 3) / 4, IDX_SHORT_BLOCKS)),
+                       dim3(256), 0, s, qual, val, val2, rows, b.hint, n_rows, b.cnt, err);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
 #define IDX_CLS(Q, LL) if ((e = launch_cls<Q, LL>(qual, val, val2, rows, b, k.off, k.cnt, err, s)) != hipSuccess) return e;
