@@ -108,10 +108,13 @@ def main():
     ap.add_argument("--ordered", action="store_true", help="TSDB_QF_ORDERED (bit-exact span-order float reductions)")
     ap.add_argument("--multi", action="store_true", help="config 3: the queries through one tsdbhip_run_multi call")
     ap.add_argument("--fns", default="p99,ep99r7", help="config 5: comma-separated 1h downsampling functions")
+    ap.add_argument("--dbg", type=int, default=0, help="developer option DBG (profiling switches; -DTSDBHIP_KDBG builds only)")
     ap.add_argument("--no-extra", action="store_true", help="config 5: skip the run_multi and rollup lines")
     args = ap.parse_args()
     from opentsdb_amd import abi, dist, synth
-    from opentsdb_amd.engine import Engine, parse_downsample
+    from opentsdb_amd.engine import Engine, parse_downsample, set_option
+    if args.dbg:
+        set_option("DBG", args.dbg)
 
     def dsq(agg, spec, end):
         d = parse_downsample(spec)
