@@ -3731,6 +3731,12 @@ int assemble(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G, c
     const int64_t row = groups[i].second;
     const uint8_t* f = flag + row * K;
     const double* v = val + row * K;
+    if (off[i + 1] - o == K && P.mode != MODE_ALL && P.mode != MODE_TABLE) {   // every slot emitted: straight copies
+      std::memcpy(&vb[o], v, K * 8);
+      for (int64_t k = 0; k < K; k++) ts[o + k] = P.B0 + k * P.I;
+      std::memset(&isi[o], 0, K);
+      return;
+    }
     for (int64_t k = 0; k < K; k++) {
       if (!f[k]) continue;
       // only points inside [start_time, end_time] of the SpanGroup are produced (x <= end_time)
@@ -5863,6 +5869,96 @@ extern "C" int tsdbhip_assemble(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t 
   if (G) HIP_OK(hipMemcpyAsync(c->gact.p, act, G * 4, hipMemcpyDefault, c->stream));
   return collect(c, q, P, G, false, out);
 }
+
+namespace tsdb {
+// multi.cpp's result step: nq queries' dense [G][K] rows gathered on this context's device (query
+// i's values / flags at i * stride, its activity words at i * max(1, G)) -> nq results.  One copy
+// of each array into the context's page-locked staging and one synchronisation for the whole
+// query list, then the queries' host assembly side by side on the assembly pool.  Per query the
+// same steps as tsdbhip_assemble + collect (rollup rewrite, "all" window check, activity, rows).
+int md_assemble(tsdbhip_ctx* c, const tsdbhip_query* qs, int nq, int64_t G, int64_t stride, const void* val,
+                const void* flag, const void* act, tsdbhip_result** outs) {
+  if (!c || !qs || nq < 1 || !val || !flag || !act || !outs) return fail(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  CtxLock lk(c);
+  PhaseTrace tr("md_assemble");
+  for (int i = 0; i < nq; i++) outs[i] = nullptr;
+  HIP_OK(hipSetDevice(c->device));
+  std::vector<tsdbhip_query> qr(nq);
+  std::vector<Plan> P(nq);
+  for (int i = 0; i < nq; i++) {
+    if (c->ro_active) { const int r = ro_check(&qs[i]); if (r) return r; }
+    qr[i] = ro_query(c, &qs[i]);
+    const int rc = plan_query(c, &qr[i], P[i]);
+    if (rc) return rc;
+    if (P[i].raw || P[i].none) return fail(TSDB_E_ILLEGAL_ARGUMENT, "assemble takes downsampled group-by queries");
+    if (P[i].anchored) return fail(TSDB_E_NOT_IMPLEMENTED, "calendar grids anchored per span that disagree: no dense slot grid");
+    if (G * P[i].K > stride) return fail(TSDB_E_ILLEGAL_ARGUMENT, "dense rows wider than the query stride");
+  }
+  tr.mark("plans");
+  const int64_t ga = std::max<int64_t>(1, G);
+  const int64_t vb = nq * stride * 8, fb = (nq * stride + 15) & ~(int64_t)15;
+  HIP_OK(c->h_stage.ensure(std::max<int64_t>(16, vb + fb + nq * ga * 4)));
+  double* hv = reinterpret_cast<double*>(c->h_stage.p);
+  uint8_t* hf = reinterpret_cast<uint8_t*>(c->h_stage.p) + vb;
+  uint32_t* ha = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->h_stage.p) + vb + fb);
+  // query by query, each copy followed by its event: the host rows of query i are built while
+  // the later queries' rows are still on the link
+  std::vector<hipEvent_t> ev(nq, nullptr);
+  int rc = 0;
+  for (int i = 0; i < nq && !rc; i++) {
+    if (stride) {
+      if (hipMemcpyAsync(hv + i * stride, static_cast<const double*>(val) + i * stride, stride * 8, hipMemcpyDefault,
+                         c->stream) != hipSuccess ||
+          hipMemcpyAsync(hf + i * stride, static_cast<const uint8_t*>(flag) + i * stride, stride, hipMemcpyDefault,
+                         c->stream) != hipSuccess)
+        rc = fail(TSDB_E_HIP, "result rows to the host");
+    }
+    if (!rc && G && hipMemcpyAsync(ha + i * ga, static_cast<const uint32_t*>(act) + i * ga, ga * 4, hipMemcpyDefault,
+                                   c->stream) != hipSuccess)
+      rc = fail(TSDB_E_HIP, "result activity to the host");
+    if (!rc && (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess ||
+                hipEventRecord(ev[i], c->stream) != hipSuccess))
+      rc = fail(TSDB_E_HIP, "result copy event");
+  }
+  if (rc) {
+    (void)hipStreamSynchronize(c->stream);
+    for (hipEvent_t e : ev) if (e) (void)hipEventDestroy(e);
+    return rc;
+  }
+  tr.mark("d2h issued");
+  // the queries in order, each query's rows over the assembly pool (assemble's own split) as soon
+  // as its copy has landed (one thread a query left each thread ~1 ms of a 12 h x 1000-group
+  // query's 12 MB of rows)
+  std::vector<int> rcs(nq, 0);
+  for (int64_t i = 0; i < nq; i++) {
+    if (hipEventSynchronize(ev[i]) != hipSuccess) {
+      rcs[i] = TSDB_E_HIP;
+      break;
+    }
+    const Plan& Pi = P[i];
+    uint8_t* f = hf + i * stride;
+    if (Pi.mode == MODE_ALL) {   // as collect: the single "all" point only for start_time in the scan window
+      const int64_t S0 = Pi.ss * 1000, E0 = Pi.se * 1000;
+      if (qr[i].start_time < S0 || qr[i].start_time > E0) std::fill(f, f + G * Pi.K, 0);
+    }
+    std::vector<uint32_t> a(ha + i * ga, ha + i * ga + ga);
+    ro_activity(c, Pi, G, a);
+    rcs[i] = assemble(c, &qr[i], Pi, G, hv + i * stride, f, a, &outs[i]);
+    if (rcs[i]) break;
+  }
+  tr.mark("host rows");
+  for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+  for (int i = 0; i < nq; i++)
+    if (rcs[i]) {
+      for (int j = 0; j < nq; j++) {
+        result_free(outs[j]);
+        outs[j] = nullptr;
+      }
+      return fail(rcs[i], rcs[i] == TSDB_E_HIP ? "result rows to the host" : "result allocation");
+    }
+  return 0;
+}
+}  // namespace tsdb
 
 // ===========================================================================
 // rollup codec and generation

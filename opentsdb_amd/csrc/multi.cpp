@@ -585,12 +585,9 @@ int run_partials_owner(MultiDev* m, const tsdbhip_query* qs, int nq, tsdbhip_res
     }
   rc = transfer(m, ys);
   if (rc) return rc;
-  // 5. the results on the host
+  // 5. the results on the host: the query list's rows in one copy per array, assembled side by side
   t0 = now_ms();
-  for (int i = 0; i < nq && !rc; i++)
-    rc = tsdbhip_assemble(m->root, &qs[i], G, static_cast<double*>(m->ov.p) + i * gk,
-                          static_cast<uint8_t*>(m->of.p) + i * gk, static_cast<uint32_t*>(m->oa.p) + i * std::max<int64_t>(1, G),
-                          &outs[i]);
+  rc = md_assemble(m->root, qs, nq, G, gk, m->ov.p, m->of.p, m->oa.p, outs);
   m->t_asm += now_ms() - t0;
   return rc;
 }
@@ -688,7 +685,7 @@ int run_sel_xchg(MultiDev* m, const tsdbhip_query* q, tsdbhip_result** out) {
   }
   rc = transfer(m, ys);
   t0 = now_ms();
-  if (!rc) rc = tsdbhip_assemble(m->root, q, G, m->ov.p, m->of.p, a.data(), out);
+  if (!rc) rc = md_assemble(m->root, q, 1, G, G * K, m->ov.p, m->of.p, a.data(), out);
   m->t_asm += now_ms() - t0;
   return rc;
 }

@@ -38,6 +38,10 @@ void partials_offsets(int64_t G, int64_t K, int64_t* off_b, int64_t* off_n, int6
                       int64_t* bytes);
 int md_partials_finish(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, unsigned char* state, int64_t g_fold,
                        const unsigned char* mini, int n_mini, double* out_val, uint8_t* out_flag, uint32_t* out_act);
+// nq queries' dense rows on the context's device (query i at i * stride values) -> nq results with
+// one copy per array and one synchronisation
+int md_assemble(tsdbhip_ctx* c, const tsdbhip_query* qs, int nq, int64_t G, int64_t stride, const void* val,
+                const void* flag, const void* act, tsdbhip_result** outs);
 // multi.cpp
 int md_load(tsdbhip_ctx* c, const tsdbhip_batch* b);
 int md_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp);
