@@ -382,8 +382,11 @@ int tsdbhip_assemble(tsdbhip_ctx* ctx, const tsdbhip_query* q, int64_t n_groups_
  * scan (each device compacts its series' rows) as tsdbhip_load shards a batch;
  * tsdbhip_rollup_run generates every device's series' rollup cells on that device and
  * tsdbhip_rollup_download returns them in the one-GPU order (function, batch series, time),
- * byte for byte the one-GPU cells.  The histogram path (its store resident on devices[0],
- * unsharded) and the expression functions run on devices[0].  tsdbhip_last_timing: per-device stage times are the maximum over
+ * byte for byte the one-GPU cells.  tsdbhip_load_histograms shards the histogram spans by whole
+ * groups over the devices (contiguous group-id runs balanced by column bytes; an ungrouped span is
+ * a unit of its own) and tsdbhip_hist_run / _range answer on every device and merge: groups in
+ * group-id order ("none": spans in batch order), the bucket dictionary the union of the devices'.
+ * The expression functions run on devices[0].  tsdbhip_last_timing: per-device stage times are the maximum over
  * the devices, counters are summed, total_ms is the host wall time of the call and exchange_ms
  * its gather + merge part. */
 enum { TSDB_SHARD_AUTO = -1 };

@@ -4859,7 +4859,10 @@ int ro_scan(tsdbhip_ctx* c, const Plan& P, bool reads_counts) {
     }
     if (first_err) return fail(first_err->err, first_err->msg);
     if (!in) continue;
-    if (!c->ro_unsup[s].empty()) return fail(TSDB_E_NOT_IMPLEMENTED, "rollup span: " + c->ro_unsup[s]);
+    // cells no HBase scan of a rollup table returns (a row key's cells arrive together, offsets stay
+    // inside the row span): refused as data RollupSeq does not take (IllegalDataException,
+    // RollupSeq.addRow src/rollup/RollupSeq.java:170-205), naming the case
+    if (!c->ro_unsup[s].empty()) return fail(TSDB_E_ILLEGAL_DATA, "rollup span: " + c->ro_unsup[s]);
     if (verr) return fail(TSDB_E_ILLEGAL_DATA, "rollup value of a bad length");
     if (cerr && reads_counts) return fail(TSDB_E_ILLEGAL_DATA, "rollup count of a bad length");
   }

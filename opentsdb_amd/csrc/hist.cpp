@@ -27,6 +27,11 @@ int set_error(int code, const std::string& msg);
 bool cal_prev_tz(const tsdbhip_tz* z, int64_t ts, int64_t n, int unit, int64_t* out);
 int64_t cal_step_tz(const tsdbhip_tz* z, int64_t t, int unit, int64_t n);
 int64_t cal_unit_ms(int unit);
+void*& ctx_md(tsdbhip_ctx* c);
+// multi.cpp: the histogram store of a multi-device context, whole groups per device
+int md_load_histograms(tsdbhip_ctx* c, const tsdbhip_hist_batch* hb);
+int md_hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end, int64_t ss, int64_t se, int n_pct,
+                const float* pct, int show_buckets, tsdbhip_hist_result** out);
 
 namespace {
 
@@ -161,11 +166,11 @@ void hist_release(void* h) {
 
 using namespace tsdb;
 
-// On a multi-device context (tsdbhip_init_devices) the histogram store is resident on its first
-// device: the context is itself an engine context on devices[0] (multi.cpp), whose store, stream
-// and lock serve the histogram entry points; the numeric batch stays sharded over the devices.
+// On a multi-device context (tsdbhip_init_devices) the histogram spans are sharded by whole groups
+// over the devices (multi.cpp md_load_histograms); every device's store is loaded here.
 extern "C" int tsdbhip_load_histograms(tsdbhip_ctx* c, const tsdbhip_hist_batch* hb) {
   if (!c || !hb) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
+  if (ctx_md(c)) return md_load_histograms(c, hb);
   std::lock_guard<std::mutex> lk(ctx_mutex(c));
   HOK(hipSetDevice(ctx_device(c)));
   hipStream_t st = ctx_stream(c);
@@ -353,12 +358,13 @@ extern "C" int tsdbhip_load_histograms(tsdbhip_ctx* c, const tsdbhip_hist_batch*
   return 0;
 }
 
-namespace {
+namespace tsdb {
 // start / end: HistogramSpanGroup bounds (ms); rows with base time in [row_lo, row_hi) are scanned
 int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end, int64_t ss, int64_t se, int n_pct,
              const float* pct, int show_buckets, tsdbhip_hist_result** out) {
   if (!c || !q || !out || n_pct < 0 || (n_pct && !pct)) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "null argument");
   *out = nullptr;
+  if (ctx_md(c)) return md_hist_run(c, q, start, end, ss, se, n_pct, pct, show_buckets, out);
   std::lock_guard<std::mutex> lk(ctx_mutex(c));
   HOK(hipSetDevice(ctx_device(c)));
   hipStream_t st = ctx_stream(c);
@@ -713,7 +719,98 @@ int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end,
   return 0;
 }
 
-}  // namespace
+// The devices' results of one histogram query (multi-device context, whole groups per device) as
+// the result of the whole store: the groups in group-id order ("none": the spans in batch order,
+// span_of[d] maps device d's span index to the batch's), the bucket dictionary the union of the
+// devices' (HistogramBucket order), each point's counts / presence moved to its buckets' places in
+// it (a bucket of another device's store is absent from the point: count 0, not present).
+int hist_merge(const std::vector<tsdbhip_hist_result*>& parts, const std::vector<const std::vector<int64_t>*>& span_of,
+               bool none, tsdbhip_hist_result** out) {
+  *out = nullptr;
+  const size_t np = parts.size();
+  if (!np) return set_error(TSDB_E_ILLEGAL_STATE, "no histogram store loaded (tsdbhip_load_histograms)");
+  const int n_pct = parts[0]->n_pct, sb = parts[0]->show_buckets;
+  auto ord = [](uint32_t lo, uint32_t up) { return ((uint64_t)ford(lo) << 32) | ford(up); };
+  std::vector<uint64_t> keys;
+  for (const tsdbhip_hist_result* r : parts)
+    for (int32_t b = 0; b < r->n_buckets; b++) keys.push_back(ord(r->bucket_lower[b], r->bucket_upper[b]));
+  std::sort(keys.begin(), keys.end());
+  keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+  const int64_t D = (int64_t)keys.size();
+  std::vector<std::vector<int32_t>> bmap(np);
+  for (size_t i = 0; i < np; i++) {
+    const tsdbhip_hist_result* r = parts[i];
+    bmap[i].resize(r->n_buckets);
+    for (int32_t b = 0; b < r->n_buckets; b++)
+      bmap[i][b] = (int32_t)(std::lower_bound(keys.begin(), keys.end(), ord(r->bucket_lower[b], r->bucket_upper[b])) - keys.begin());
+  }
+  struct Ent { int64_t key; int32_t part; int64_t g; };
+  std::vector<Ent> ents;
+  for (size_t i = 0; i < np; i++)
+    for (int64_t g = 0; g < parts[i]->n_groups; g++) {
+      const int32_t id = parts[i]->group_id[g];
+      ents.push_back({none ? (*span_of[i])[id] : (int64_t)id, (int32_t)i, g});
+    }
+  std::sort(ents.begin(), ents.end(), [](const Ent& a, const Ent& b) { return a.key < b.key; });
+  auto* R = new HistResultOwner();
+  const int64_t G = (int64_t)ents.size();
+  R->gid.resize(G);
+  R->gptr.assign(G + 1, 0);
+  for (int64_t e = 0; e < G; e++) {
+    const tsdbhip_hist_result* r = parts[ents[e].part];
+    R->gid[e] = (int32_t)ents[e].key;
+    R->gptr[e + 1] = R->gptr[e] + (r->group_ptr[ents[e].g + 1] - r->group_ptr[ents[e].g]);
+  }
+  const int64_t n_out = R->gptr[G];
+  R->ts.resize(n_out);
+  R->kind.resize(n_out);
+  R->pct.resize((size_t)n_out * n_pct);
+  if (sb) {
+    R->cnt.assign((size_t)n_out * (D + 2), 0);
+    R->pres.assign((size_t)n_out * D, 0);
+  }
+  for (int64_t e = 0; e < G; e++) {
+    const tsdbhip_hist_result* r = parts[ents[e].part];
+    const std::vector<int32_t>& bm = bmap[ents[e].part];
+    const int64_t Dl = r->n_buckets;
+    for (int64_t i = r->group_ptr[ents[e].g], o = R->gptr[e]; i < r->group_ptr[ents[e].g + 1]; i++, o++) {
+      R->ts[o] = r->ts_ms[i];
+      R->kind[o] = r->codec[i];
+      for (int j = 0; j < n_pct; j++) R->pct[(size_t)o * n_pct + j] = r->pct[(size_t)i * n_pct + j];
+      if (!sb) continue;
+      for (int64_t b = 0; b < Dl; b++) {
+        R->cnt[(size_t)o * (D + 2) + bm[b]] = r->count[(size_t)i * (Dl + 2) + b];
+        R->pres[(size_t)o * D + bm[b]] = r->present[(size_t)i * Dl + b];
+      }
+      R->cnt[(size_t)o * (D + 2) + D] = r->count[(size_t)i * (Dl + 2) + Dl];           // underflow
+      R->cnt[(size_t)o * (D + 2) + D + 1] = r->count[(size_t)i * (Dl + 2) + Dl + 1];   // overflow
+    }
+  }
+  R->blo.resize(D);
+  R->bup.resize(D);
+  auto unord = [](uint32_t k) { return (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k; };   // inverse of ford
+  for (int64_t b = 0; b < D; b++) {
+    R->blo[b] = unord((uint32_t)(keys[b] >> 32));
+    R->bup[b] = unord((uint32_t)keys[b]);
+  }
+  tsdbhip_hist_result& r = R->r;
+  r.n_groups = G;
+  r.group_id = R->gid.data();
+  r.group_ptr = R->gptr.data();
+  r.ts_ms = R->ts.data();
+  r.n_pct = n_pct;
+  r.pct = R->pct.data();
+  r.show_buckets = sb;
+  r.n_buckets = (int32_t)D;
+  r.bucket_lower = R->blo.data();
+  r.bucket_upper = R->bup.data();
+  r.count = sb ? R->cnt.data() : nullptr;
+  r.present = sb ? R->pres.data() : nullptr;
+  r.codec = R->kind.data();
+  *out = &R->r;
+  return 0;
+}
+}  // namespace tsdb
 
 extern "C" int tsdbhip_hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int n_pct, const float* pct, int show_buckets,
                                 tsdbhip_hist_result** out) {

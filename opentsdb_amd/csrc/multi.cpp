@@ -28,6 +28,7 @@
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <cstring>
 #include <numeric>
 #include <set>
 #include <string>
@@ -218,6 +219,11 @@ struct MultiDev {
   int ro_nf = 0;
   std::vector<std::vector<int64_t>> ro_cells;
   std::vector<std::vector<uint64_t>> ro_bytes;
+  // the histogram store (tsdbhip_load_histograms): whole groups per device; per device its spans'
+  // batch indices, and the devices holding spans
+  bool hist_loaded = false;
+  std::vector<int> hist_devs;
+  std::vector<std::vector<int64_t>> hist_series;
 };
 
 MultiDev* md_of(tsdbhip_ctx* c) { return static_cast<MultiDev*>(ctx_md(c)); }
@@ -1360,6 +1366,135 @@ int md_run_multi(tsdbhip_ctx* c, const tsdbhip_query* qs, int n, tsdbhip_result*
   }
   device_timing(m, now_ms() - t0, fused);
   return 0;
+}
+
+// Histogram spans over the devices: a HistogramSpanGroup is a sum over its
+// spans' histograms (HistogramAggregationIterator, src/core/HistogramAggregationIterator.java:
+// 91-287) with no cross-group state, so each device holds whole groups -- contiguous runs of
+// group ids, balanced by column bytes -- and answers them as one GPU does; an ungrouped span
+// (dropped by a group-by, its own group under "none") is a unit of its own.  hist_merge orders
+// the devices' groups (or the spans, "none") as one context does and unions the bucket dictionary.
+int md_load_histograms(tsdbhip_ctx* c, const tsdbhip_hist_batch* hb) {
+  MultiDev* m = md_of(c);
+  const int n = (int)m->devices.size();
+  m->hist_loaded = false;
+  m->hist_devs.clear();
+  m->hist_series.assign(n, {});
+  const int64_t NS = hb->n_series, NR = hb->n_rows, NC = hb->n_cells;
+  if (NS < 0 || NR < 0 || NC < 0 || !hb->series_row_ptr || (NR && (!hb->row_base_time || !hb->row_cell_ptr)) ||
+      (NC && (!hb->cell_qual_off || !hb->cell_val_off || !hb->qual || !hb->val)) || (NS && !hb->group_id))
+    return set_error(TSDB_E_ILLEGAL_ARGUMENT, "malformed histogram batch");
+  if (hb->series_row_ptr[0] != 0 || hb->series_row_ptr[NS] != NR || (NR && (hb->row_cell_ptr[0] != 0 || hb->row_cell_ptr[NR] != NC)))
+    return set_error(TSDB_E_ILLEGAL_ARGUMENT, "histogram batch offsets do not cover the rows / columns");
+  for (int64_t s = 0; s < NS; s++)
+    if (hb->series_row_ptr[s + 1] < hb->series_row_ptr[s]) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "row offsets not monotonic");
+  for (int64_t r = 0; r < NR; r++)
+    if (hb->row_cell_ptr[r + 1] < hb->row_cell_ptr[r]) return set_error(TSDB_E_ILLEGAL_ARGUMENT, "column offsets not monotonic");
+  for (int64_t k = 0; k < NC; k++)
+    if (hb->cell_qual_off[k + 1] < hb->cell_qual_off[k] || hb->cell_val_off[k + 1] < hb->cell_val_off[k])
+      return set_error(TSDB_E_ILLEGAL_ARGUMENT, "column byte offsets not monotonic");
+  // units: a group's spans, or one ungrouped span; in group-id order, ungrouped spans after
+  std::vector<int64_t> order(NS);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+    const int32_t ga = hb->group_id[a], gb = hb->group_id[b];
+    if ((ga < 0) != (gb < 0)) return gb < 0;
+    return ga >= 0 && ga < gb;
+  });
+  auto sbytes = [&](int64_t s) {
+    const int64_t c0 = hb->row_cell_ptr[hb->series_row_ptr[s]], c1 = hb->row_cell_ptr[hb->series_row_ptr[s + 1]];
+    return (double)(hb->cell_val_off[c1] - hb->cell_val_off[c0] + hb->cell_qual_off[c1] - hb->cell_qual_off[c0]) + 1.0;
+  };
+  double total = 0;
+  for (int64_t s = 0; s < NS; s++) total += sbytes(s);
+  std::vector<int> dev_of(NS, 0);
+  {
+    double acc = 0;
+    int d = 0;
+    for (int64_t i = 0; i < NS;) {
+      int64_t j = i + 1;   // the unit [i, j)
+      const int32_t g = hb->group_id[order[i]];
+      if (g >= 0)
+        while (j < NS && hb->group_id[order[j]] == g) j++;
+      double ub = 0;
+      for (int64_t k = i; k < j; k++) ub += sbytes(order[k]);
+      while (d < n - 1 && acc + ub / 2 > total * (d + 1) / n) d++;   // the unit's midpoint picks the device
+      for (int64_t k = i; k < j; k++) dev_of[order[k]] = d;
+      acc += ub;
+      i = j;
+    }
+  }
+  for (int64_t s = 0; s < NS; s++) m->hist_series[dev_of[s]].push_back(s);   // batch order on each device
+  for (int d = 0; d < n; d++)
+    if (!m->hist_series[d].empty() || (NS == 0 && d == 0)) m->hist_devs.push_back(d);
+  // each device's sub-batch (the same codec table, group ids kept)
+  struct Sub {
+    std::vector<int64_t> srp{0}, rcp{0};
+    std::vector<uint32_t> base;
+    std::vector<uint64_t> qo{0}, vo{0};
+    std::vector<uint8_t> q, v;
+    std::vector<int32_t> gid;
+  };
+  std::vector<Sub> subs(n);
+  for (int d : m->hist_devs) {
+    Sub& u = subs[d];
+    for (int64_t s : m->hist_series[d]) {
+      for (int64_t r = hb->series_row_ptr[s]; r < hb->series_row_ptr[s + 1]; r++) {
+        u.base.push_back(hb->row_base_time[r]);
+        for (int64_t k = hb->row_cell_ptr[r]; k < hb->row_cell_ptr[r + 1]; k++) {
+          u.q.insert(u.q.end(), hb->qual + hb->cell_qual_off[k], hb->qual + hb->cell_qual_off[k + 1]);
+          u.v.insert(u.v.end(), hb->val + hb->cell_val_off[k], hb->val + hb->cell_val_off[k + 1]);
+          u.qo.push_back(u.q.size());
+          u.vo.push_back(u.v.size());
+        }
+        u.rcp.push_back((int64_t)u.qo.size() - 1);
+      }
+      u.srp.push_back((int64_t)u.base.size());
+      u.gid.push_back(hb->group_id[s]);
+    }
+  }
+  const int rc = each_of(m, m->hist_devs, [&](int d) {
+    const Sub& u = subs[d];
+    tsdbhip_hist_batch sb{};
+    sb.n_series = (int64_t)u.gid.size();
+    sb.series_row_ptr = u.srp.data();
+    sb.n_rows = (int64_t)u.base.size();
+    sb.row_base_time = u.base.data();
+    sb.row_cell_ptr = u.rcp.data();
+    sb.n_cells = (int64_t)u.qo.size() - 1;
+    sb.cell_qual_off = u.qo.data();
+    sb.cell_val_off = u.vo.data();
+    sb.qual = u.q.data();
+    sb.val = u.v.data();
+    sb.group_id = u.gid.data();
+    std::memcpy(sb.codec, hb->codec, sizeof(sb.codec));
+    return tsdbhip_load_histograms(m->subs[d], &sb);
+  });
+  if (rc) return rc;
+  m->hist_loaded = true;
+  return 0;
+}
+
+int md_hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end, int64_t ss, int64_t se, int n_pct,
+                const float* pct, int show_buckets, tsdbhip_hist_result** out) {
+  MultiDev* m = md_of(c);
+  if (!m->hist_loaded) return set_error(TSDB_E_ILLEGAL_STATE, "no histogram store loaded (tsdbhip_load_histograms)");
+  const int n = (int)m->devices.size();
+  std::vector<tsdbhip_hist_result*> parts(n, nullptr);
+  int rc = each_of(m, m->hist_devs, [&](int d) {
+    return hist_run(m->subs[d], q, start, end, ss, se, n_pct, pct, show_buckets, &parts[d]);
+  });
+  if (!rc) {
+    std::vector<tsdbhip_hist_result*> ps;
+    std::vector<const std::vector<int64_t>*> span_of;
+    for (int d : m->hist_devs) {
+      ps.push_back(parts[d]);
+      span_of.push_back(&m->hist_series[d]);
+    }
+    rc = hist_merge(ps, span_of, q->aggregator == TSDB_AGG_NONE, out);
+  }
+  for (tsdbhip_hist_result* p : parts) tsdbhip_hist_result_free(p);
+  return rc;
 }
 
 int md_timing(tsdbhip_ctx* c, tsdbhip_timing* out) {

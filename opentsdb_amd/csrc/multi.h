@@ -42,7 +42,15 @@ int md_partials_finish(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t G, unsign
 // one copy per array and one synchronisation
 int md_assemble(tsdbhip_ctx* c, const tsdbhip_query* qs, int nq, int64_t G, int64_t stride, const void* val,
                 const void* flag, const void* act, tsdbhip_result** outs);
+// hist.cpp: one context's histogram query, and the devices' results merged into one
+int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end, int64_t ss, int64_t se, int n_pct,
+             const float* pct, int show_buckets, tsdbhip_hist_result** out);
+int hist_merge(const std::vector<tsdbhip_hist_result*>& parts, const std::vector<const std::vector<int64_t>*>& span_of,
+               bool none, tsdbhip_hist_result** out);
 // multi.cpp
+int md_load_histograms(tsdbhip_ctx* c, const tsdbhip_hist_batch* hb);
+int md_hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end, int64_t ss, int64_t se, int n_pct,
+                const float* pct, int show_buckets, tsdbhip_hist_result** out);
 int md_load(tsdbhip_ctx* c, const tsdbhip_batch* b);
 int md_synth(tsdbhip_ctx* c, const tsdbhip_synth_spec* sp);
 int md_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* rb);

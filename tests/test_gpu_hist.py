@@ -306,11 +306,14 @@ def test_gpu_calendar_downsampling(eng, dst_store, tz, spec):
         run_both(eng, dst_store, q, [50.0, 99.0], agg == "sum")
 
 
-def test_gpu_multi_device_context_runs_histograms(eng):
-    """A multi-device context (tsdbhip_init_devices; the one-GPU box repeats device 0) serves the
-    histogram path from its first device: the same answers as one device and the oracle, for
-    golden and random stores, beside a numeric batch sharded over its devices."""
-    md = Engine(devices=[0, 0])
+@pytest.mark.parametrize("n_dev", [2, 3])
+def test_gpu_multi_device_context_runs_histograms(eng, n_dev):
+    """A multi-device context (tsdbhip_init_devices; the one-GPU box repeats device 0) shards the
+    histogram spans by whole groups over its devices (multi.cpp md_load_histograms): the same
+    answers as one device and the oracle, for golden and random stores -- group-by and "none"
+    (spans in batch order), per-device bucket dictionaries merged (wild bounds, show_buckets),
+    ungrouped spans, more devices than groups."""
+    md = Engine(devices=[0] * n_dev)
     try:
         for gq in G["queries"][:6]:
             hb = U.store_batch(G["stores"][gq["store"]])
@@ -324,5 +327,17 @@ def test_gpu_multi_device_context_runs_histograms(eng):
             q = U.query(T0, T0 + 2 * 3600, agg, ds)
             got = run_both(md, hb, q, PCTS, True)
             U.same(got, run_both(eng, hb, q, PCTS, True))
+        for seed in range(3):   # wild bucket bounds: each device's dictionary differs
+            rng = np.random.default_rng(500 + seed)
+            hb = U.random_store(rng, n_series=9, n_rows=2, period_ms=20000, groups=5, layouts=4, wild=True,
+                                big_counts=seed == 1)
+            hb.group_id[::4] = -1   # ungrouped spans: dropped by a group-by, their own group under "none"
+            for agg, ds in [("sum", None), ("none", "1m-sum"), ("sum", "0all-sum")]:
+                q = U.query(T0, T0 + 2 * 3600, agg, ds)
+                got = run_both(md, hb, q, PCTS, True)
+                U.same(got, run_both(eng, hb, q, PCTS, True))
+        hb = U.random_store(np.random.default_rng(9), n_series=2, n_rows=2, period_ms=10000, groups=1, layouts=2)
+        q = U.query(T0, T0 + 2 * 3600, "sum", "1m-sum")   # one group: the other devices hold nothing
+        U.same(run_both(md, hb, q, PCTS, True), run_both(eng, hb, q, PCTS, True))
     finally:
         md.close()

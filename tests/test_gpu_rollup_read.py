@@ -112,6 +112,18 @@ def test_errors_match_oracle(eng):
     assert_groups_match(g, w, "sum", tol=0.0)
 
 
+def test_scan_impossible_cells_raise_illegal_data(eng):
+    """Cells an HBase scan of a rollup table cannot return -- one row key's cells split by another
+    key's, an offset past the row span -- are refused as IllegalDataException (RollupSeq.addRow,
+    src/rollup/RollupSeq.java:170-205), never as an unimplemented case."""
+    split = _batch([[(B, [(0, *_l(1))], []), (B + 21600, [(0, *_l(2))], []), (B, [(3, *_l(3))], [])]], counts=False)
+    past = _batch([[(B, [(0, *_l(1)), (40, *_l(2))], [])]], counts=False)   # 40 x 10m beyond a 6h row
+    for rb in (split, past):
+        with pytest.raises(EngineError) as ee:
+            eng.run_rollup_batch(rb, _q("10m-sum", "sum"))
+        assert ee.value.java == "IllegalDataException"
+
+
 def test_duplicates_fixed(eng):
     rb = _batch([[(B, [(1, *_l(1)), (1, 0xB, struct.pack(">f", 42.5))], [])]], counts=False, fix=True)
     g, w = both(eng, rb, _q("10m-sum", "sum"))
