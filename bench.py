@@ -210,17 +210,26 @@ def config3_block(args, device: int):
     eng = Engine(device)
     try:
         spec = c3_spec(args, 1)
+        # k_index at load: row classes, certificate, the vle -> int16 copy.  The store is loaded
+        # twice: the first load of a process also pays the first touch of ~25 GB of fresh device
+        # allocations; a serving process reloads into reused buffers, as the second load does
         eng.synth(*spec)
         eng.sync()
-        index_ms = eng.timing().index_ms   # k_index at load: row classes, certificate, the vle -> int16 copy
+        index_first_ms = eng.timing().index_ms
+        eng.synth(*spec)
+        eng.sync()
+        index_ms = eng.timing().index_ms
 
         def q(agg):
             return abi.new_query(T0, T0 + 3599, agg, ds_function=abi.AGG["avg"], ds_interval_ms=60000)
 
         out = {"workload": "BASELINE config 3 (1 h window): 10M series x 360 dp @10 s, int/float32 alternating, "
                            "1000 groups, 1m-avg", "index_ms": index_ms,
+               "index_first_load_ms": index_first_ms,
                "index_note": "load-time k_index pass (untimed in ms_per_step): row classification, the exactness "
-                             "certificate and the int16 copy of the vle integer values that k_short reads"}
+                             "certificate and the int16 copy of the vle integer values that k_short reads; "
+                             "index_ms is a reload into the process's reused buffers, index_first_load_ms the "
+                             "process's first load of the store (fresh allocations)"}
         if not args.no_parity:
             out["parity"] = md_parity(eng, device, spec, parity_queries(T0, T0 + 3599, 60000),
                                       "config 3, 1 h store", bounds=[0, spec[0]])
@@ -243,6 +252,7 @@ def config3_block(args, device: int):
                       "hbm_frac": tm.bytes / (k_ms / 1000) / 1e9 / BYTES_PEAK_GBS,
                       "hbm_frac_step": tm.bytes / (sum_ms / 1000) / 1e9 / BYTES_PEAK_GBS,
                       "cold_value": tm.datapoints / ((index_ms + sum_ms) / 1000),
+                      "cold_value_first_load": tm.datapoints / ((index_first_ms + sum_ms) / 1000),
                       "cold_note": "datapoints / (k_index at load + one step): every query on freshly scanned cells, "
                                    "the vle bytes decoded once"}
         ql = [q(a) for a in ("avg", "min", "max", "count", "dev")]
