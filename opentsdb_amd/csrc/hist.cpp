@@ -582,7 +582,9 @@ int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end,
     HOK(hipMemcpyAsync(S->q_gsp.p, gsp.data(), (G + 1) * 8, hipMemcpyHostToDevice, st));
     HOK(hipMemsetAsync(S->q_key.p, 0xFF, NP * 8 + 8, st));
     HOK(hipMemsetAsync(S->err.p, 0, 16, st));
-    HOK(hist_walk(p, S->q_gsp.as<int64_t>(), G, S->q_spq.as<int64_t>(), S->q_spts.as<int64_t>(), st));
+    int64_t max_spans = 0;
+    for (int64_t g = 0; g < G; g++) max_spans = std::max(max_spans, gsp[g + 1] - gsp[g]);
+    HOK(hist_walk(p, S->q_gsp.as<int64_t>(), G, max_spans, S->q_spq.as<int64_t>(), S->q_spts.as<int64_t>(), st));
     HOK(hipMemcpyAsync(err, S->err.p, 8, hipMemcpyDeviceToHost, st));
     HOK(hipStreamSynchronize(st));   // (gsp leaves scope)
     p.greedy = 1;

@@ -143,7 +143,8 @@ hipError_t hist_final(const HistQueryParams& p, hipStream_t s);
 hipError_t hist_scan(const uint32_t* flag, int64_t* out, int64_t n, void** tmp, size_t* tmp_bytes, hipStream_t s);
 // HistogramAggregationIterator.next()'s walk over raw spans some of which are out of time order
 // (one wave a group; span state in sp_q / sp_ts, [n_spans] scratch); gsp[G + 1]: the group's spans
-hipError_t hist_walk(const HistQueryParams& p, const int64_t* gsp, int64_t G, int64_t* sp_q, int64_t* sp_ts, hipStream_t s);
+hipError_t hist_walk(const HistQueryParams& p, const int64_t* gsp, int64_t G, int64_t max_spans, int64_t* sp_q,
+                     int64_t* sp_ts, hipStream_t s);
 hipError_t hist_sparse(const HistQueryParams& p, int64_t n_pos, uint64_t* key2, uint32_t* pos, uint32_t* pos2,
                        uint32_t* head, int64_t* incl, int64_t* pt_ts, int32_t* pt_group, int64_t* n_points,
                        void** tmp, size_t* tmp_bytes, hipStream_t s);

@@ -3,7 +3,11 @@
 queries timed on the device.
 
     python tools/hist_bench.py [--series 20000] [--buckets 20] [--period 10] [--hours 1]
-                               [--groups 64] [--ds 1m-sum] [--steps 10] [--check]
+                               [--groups 64] [--ds 1m-sum] [--steps 10] [--check] [--unsorted N]
+
+--unsorted N: the first two columns of the first row of N series (spread over the groups) trade
+qualifiers, so those spans yield a receding timestamp; with --ds none their groups take
+k_hist_walk (HistogramAggregationIterator's greedy walk) instead of the sorted union path.
 
 One JSON line: columns/s and the algorithmic bytes rate of the query (value bytes of the columns
 plus 21 B of per-column index: column offset 8, position->column 8, kind 1, slot 4).
@@ -28,7 +32,7 @@ from opentsdb_amd import histogram as H  # noqa: E402
 T0 = 1356998400
 
 
-def synth(n_series, n_buckets, period_s, hours, groups, seed=1):
+def synth(n_series, n_buckets, period_s, hours, groups, seed=1, unsorted=0):
     """Vectorised SimpleHistogram columns: one layout (log-spaced buckets), counts 0..999
     (1-2 byte varints), underflow / overflow < 128."""
     rng = np.random.default_rng(seed)
@@ -65,6 +69,11 @@ def synth(n_series, n_buckets, period_s, hours, groups, seed=1):
     offs = np.arange(per_row, dtype=np.int64) * period_s
     q1 = np.stack([np.full(per_row, 6, np.uint8), (offs >> 8).astype(np.uint8), (offs & 0xFF).astype(np.uint8)], 1)
     qual = np.tile(q1.reshape(-1), n_rows)
+    if unsorted:   # columns 0 and 1 of the series' first row trade qualifiers (a receding timestamp)
+        for sr in np.linspace(0, n_series - 1, unsorted).astype(np.int64):
+            c0 = int(sr) * hours * per_row
+            a, b = qual[3 * c0:3 * c0 + 3].copy(), qual[3 * c0 + 3:3 * c0 + 6].copy()
+            qual[3 * c0:3 * c0 + 3], qual[3 * c0 + 3:3 * c0 + 6] = b, a
     qoff = np.arange(n + 1, dtype=np.uint64) * 3
     srp = np.arange(n_series + 1, dtype=np.int64) * hours
     base = np.tile(T0 + 3600 * np.arange(hours, dtype=np.int64), n_series).astype(np.uint32)
@@ -86,9 +95,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--buckets-out", action="store_true", help="show_buckets")
     ap.add_argument("--check", action="store_true", help="compare with the oracle (test infrastructure)")
+    ap.add_argument("--unsorted", type=int, default=0, help="series with a receding timestamp (k_hist_walk groups)")
     a = ap.parse_args()
     t = time.time()
-    hb, vbytes = synth(a.series, a.buckets, a.period, a.hours, a.groups)
+    hb, vbytes = synth(a.series, a.buckets, a.period, a.hours, a.groups, unsorted=a.unsorted)
     synth_s = time.time() - t
     n = int(hb.cell_val_off.size - 1)
     eng = E.Engine(0)
@@ -115,7 +125,7 @@ def main():
             "algorithmic_bytes": alg, "GBps_alg": alg / dt / 1e9, "points_out": points, "groups": len(res),
             "config": {"series": a.series, "buckets": a.buckets, "period_s": a.period, "hours": a.hours,
                        "groups": a.groups, "downsample": a.ds, "aggregator": a.agg, "percentiles": pcts,
-                       "show_buckets": a.buckets_out},
+                       "show_buckets": a.buckets_out, "unsorted_series": a.unsorted},
             "synth_s": synth_s, "load_s": load_s}
     if a.check:
         from oracle import oracle as O
