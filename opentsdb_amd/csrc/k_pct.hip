@@ -563,12 +563,18 @@ __global__ __launch_bounds__(256) void k_emit(GridParams p) {
 // partials), the tile's series are checked for scan-range rows one a lane up front, and the
 // next series' buckets are loaded while the current one is folded -- k_emit walks each series'
 // rows for that check and stages the partials in LDS (0.62 ms over a 1M-series rollup table).
+// GA: the group aggregator the instantiation is specialised for (< 0: p.ga at run time) -- the
+// per-series work is a few dozen instructions, and the aggregator switch was a good part of them.
+// The ring loads unconditionally (the index clamped to the last active series): with conditional
+// loads the compiler waited for every outstanding load at each series (vmcnt(0)).
+template <int GA>
 __global__ __launch_bounds__(256) void k_emit_reg(GridParams p) {
   const int lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t tile = (int64_t)blockIdx.x * p.waves + wave;
   if (tile >= p.n_tiles) return;
   const int K = (int)p.K;
+  const int ga = GA < 0 ? p.ga : GA;
   const int64_t s0 = p.tile_begin[tile], s1 = p.tile_end[tile];
   bool mine = false;   // lane i: series s0 + i has a row in the scan range (tiles hold <= 64 series)
   if (s0 + lane < s1) {
@@ -581,36 +587,38 @@ __global__ __launch_bounds__(256) void k_emit_reg(GridParams p) {
   const uint64_t act = __ballot(mine);
   if (act && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
   RegPart RP;
-  rp_init(p.ga, RP);
+  rp_init(ga, RP);
+  if (!act) {
+    rp_store(p, tile, K, RP);
+    return;
+  }
   const bool inK = lane < K;
-  // the tile's active series in order, EMIT_D of them loaded ahead (a series' K buckets are one
-  // small load each: one series in flight left the wave waiting on every one -- rollup tables,
-  // 1M series x 24 buckets; 8 or 16 ahead measured no faster, profiles/r05ah)
-  constexpr int EMIT_D = 4;
+  const int64_t kl = inK ? lane : 0;   // (lanes past K read slot 0: in bounds, ignored)
+  const int nact = __popcll(act);
+  const int last = 63 - __clzll((long long)act);
   uint64_t rem = act;
-  bool pr[EMIT_D];
-  double v[EMIT_D];
-  bool live[EMIT_D];
-  auto fetch = [&](bool& pr_, double& v_, bool& live_) {
-    live_ = rem != 0;
-    pr_ = false;
-    v_ = 0.0;
-    if (!live_) return;
-    const int64_t s = s0 + (__ffsll((long long)rem) - 1);
+  auto next = [&]() {   // the next active series of the tile (the last one again once none is left)
+    const int i = rem ? __ffsll((long long)rem) - 1 : last;
     rem &= rem - 1;
-    if (inK) { pr_ = p.pre_pres[s * K + lane] != 0; v_ = p.pre_dense[s * K + lane]; }
+    return s0 + i;
   };
+  constexpr int EMIT_D = 4;
+  uint8_t pr[EMIT_D];
+  double v[EMIT_D];
 #pragma unroll
-  for (int d = 0; d < EMIT_D; d++) fetch(pr[d], v[d], live[d]);
-  while (live[0]) {
-    emit_series_reg(p, K, pr[0], v[0], RP);
+  for (int d = 0; d < EMIT_D; d++) {
+    const int64_t s = next();
+    pr[d] = p.pre_pres[s * K + kl];
+    v[d] = p.pre_dense[s * K + kl];
+  }
+  for (int j = 0; j < nact; j += EMIT_D) {
 #pragma unroll
-    for (int d = 0; d < EMIT_D - 1; d++) {
-      pr[d] = pr[d + 1];
-      v[d] = v[d + 1];
-      live[d] = live[d + 1];
+    for (int d = 0; d < EMIT_D; d++) {
+      if (j + d < nact) emit_series_reg(p, K, inK && pr[d] != 0, v[d], RP, ga);
+      const int64_t s = next();
+      pr[d] = p.pre_pres[s * K + kl];
+      v[d] = p.pre_dense[s * K + kl];
     }
-    fetch(pr[EMIT_D - 1], v[EMIT_D - 1], live[EMIT_D - 1]);
   }
   rp_store(p, tile, K, RP);
 }
@@ -2355,7 +2363,16 @@ hipError_t launch_emit(const GridParams& p, hipStream_t s) {
   if (p.K <= 64 && !p.rate) {
     GridParams q = p;
     q.waves = 4;
-    hipLaunchKernelGGL(k_emit_reg, dim3((unsigned)((p.n_tiles + 3) / 4)), dim3(256), 0, s, q);
+    const dim3 grid((unsigned)((p.n_tiles + 3) / 4));
+    switch (p.ga) {
+      case GA_SUM: hipLaunchKernelGGL(k_emit_reg<GA_SUM>, grid, dim3(256), 0, s, q); break;
+      case GA_AVG: hipLaunchKernelGGL(k_emit_reg<GA_AVG>, grid, dim3(256), 0, s, q); break;
+      case GA_COUNT: hipLaunchKernelGGL(k_emit_reg<GA_COUNT>, grid, dim3(256), 0, s, q); break;
+      case GA_MIN: hipLaunchKernelGGL(k_emit_reg<GA_MIN>, grid, dim3(256), 0, s, q); break;
+      case GA_MAX: hipLaunchKernelGGL(k_emit_reg<GA_MAX>, grid, dim3(256), 0, s, q); break;
+      case GA_DEV: hipLaunchKernelGGL(k_emit_reg<GA_DEV>, grid, dim3(256), 0, s, q); break;
+      default: hipLaunchKernelGGL(k_emit_reg<-1>, grid, dim3(256), 0, s, q); break;
+    }
     return hipGetLastError();
   }
   if (p.K > 64 && !p.rate) {

@@ -1172,10 +1172,14 @@ __device__ __forceinline__ bool slot_contribution(const GridParams& p, int K, bo
   return false;
 }
 
-__device__ __forceinline__ void emit_series_reg(const GridParams& p, int K, bool pr_in, double v, RegPart& P) {
+// (ga: the group aggregator, a compile-time constant where the caller is specialised for it)
+__device__ __forceinline__ void emit_series_reg(const GridParams& p, int K, bool pr_in, double v, RegPart& P, int ga) {
   double cv;
   bool uni;
-  if (slot_contribution(p, K, pr_in, v, cv, uni)) contribute_slot(p.ga, P, cv, uni);
+  if (slot_contribution(p, K, pr_in, v, cv, uni)) contribute_slot(ga, P, cv, uni);
+}
+__device__ __forceinline__ void emit_series_reg(const GridParams& p, int K, bool pr_in, double v, RegPart& P) {
+  emit_series_reg(p, K, pr_in, v, P, p.ga);
 }
 
 // Several group-by aggregators over one downsampling in one pass (tsdbhip_run_multi,
