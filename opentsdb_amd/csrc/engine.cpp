@@ -508,6 +508,8 @@ struct tsdbhip_ctx {
   DevBuf ro_partner;                   // [n_rows] a value row's lock-step count row (GridParams.ro_partner)
   DevBuf ro_pairs;                     // [ro_npairs] the packed value / count row pairs (k_ro_pairs)
   int64_t ro_npairs = 0;
+  DevBuf ro_runs, ro_rid;              // ... or as runs: [ro_nruns] RoRun, [ro_npairs] run of each pair
+  int64_t ro_nruns = 0;
   // query-time compaction (tsdbhip_load_cells): rows whose compaction failed, raised when a
   // query's scan range covers them (SaltScanner.processRow fails the scan)
   struct CmpErr { int64_t series, row; int64_t base; int32_t code; };
@@ -608,7 +610,7 @@ std::atomic<int64_t> g_opts[OPT_COUNT];
 const char* const kOptNames[OPT_COUNT] = {
     "FAST", "SHORT", "ROWS", "HWIN", "SEQ", "SEQ_ROWS", "SEQ_WAVE", "INDEX_GENERIC", "CMP_CHUNK", "CMP_ROWS",
     "CMP_ONEPASS", "PCT_ROWS", "PCT_KEYS", "PCT_VONLY", "PCT_V6", "SEL_FUSED", "SEL_COLS", "SEL_WIN", "SEL_WAVE",
-    "SEL_REG", "SELOPS", "RAW_LERPW", "RAW_SEL_TOP", "RAW_SEL_REG", "RO_FUSE", "MULTI_FUSE", "HIST_WINDOW",
+    "SEL_REG", "SELOPS", "RAW_LERPW", "RAW_SEL_TOP", "RAW_SEL_REG", "RO_FUSE", "RO_RUNS", "MULTI_FUSE", "HIST_WINDOW",
     "HIST_WS", "HIST_LAYOUT", "TRACE", "DBG"};
 int opt_index(const char* name) {
   if (!name) return -1;
@@ -809,6 +811,9 @@ static void release_batch(tsdbhip_ctx* c) {
   c->ro_partner.release();
   c->ro_pairs.release();
   c->ro_npairs = 0;
+  c->ro_runs.release();
+  c->ro_rid.release();
+  c->ro_nruns = 0;
   c->cmp_errs.clear();
   c->compact_ms = 0;
 }
@@ -1370,6 +1375,55 @@ int vle_put(std::vector<uint8_t>& out, int64_t v) {
   for (int i = n - 1; i >= 0; i--) out.push_back((uint8_t)((uint64_t)v >> (8 * i)));
   return n;
 }
+// The packed pairs as runs (RoRun): consecutive pairs of one series with equal meta whose base
+// time and byte offsets advance by one constant step each.  Kept only when the runs and the
+// per-pair run ids take less than the pairs (hour rows of equal shape: one run a series).
+static int ro_build_runs(tsdbhip_ctx* c) {
+  const int64_t n = c->ro_npairs;
+  c->ro_nruns = 0;
+  if (n <= 0 || opt_off(OPT_RO_RUNS)) return 0;
+  std::vector<RoPair> hp(n);
+  HIP_OK(hipMemcpy(hp.data(), c->ro_pairs.p, n * sizeof(RoPair), hipMemcpyDeviceToHost));
+  std::vector<RoRun> runs;
+  std::vector<uint32_t> rid(n);
+  auto same = [](const RoPair& a, const RoPair& b) {
+    return a.base == b.base && a.qoff == b.qoff && a.voff == b.voff && a.cvoff == b.cvoff && a.meta == b.meta &&
+           a.series == b.series;
+  };
+  for (int64_t i = 0; i < n; i++) {
+    const RoPair& P = hp[i];
+    bool cont = false;
+    if (!runs.empty()) {
+      RoRun& R = runs.back();
+      if (P.series == R.series && P.meta == R.meta) {
+        if ((int64_t)i - R.first == 1) {   // the run's second pair sets its step
+          const int64_t db = (int64_t)P.base - R.base0, dq = (int64_t)P.qoff - R.qoff0,
+                        dv = (int64_t)P.voff - R.voff0, dc = (int64_t)P.cvoff - R.cvoff0;
+          if (db > 0 && db % 3600 == 0 && db / 3600 < 256 && dq >= 0 && dq % 16 == 0 && dq / 16 < 128 && dv >= 0 &&
+              dv % 16 == 0 && dv / 16 < 512 && dc >= 0 && dc % 16 == 0 && dc / 16 < 256) {
+            R.step = (uint32_t)(dq / 16) | (uint32_t)(dv / 16) << 7 | (uint32_t)(dc / 16) << 16 | (uint32_t)(db / 3600) << 24;
+            cont = same(ro_run_pair(R, (uint32_t)i), P);
+            if (!cont) R.step = 0;
+          }
+        } else if ((int64_t)i - R.first > 1) {
+          cont = same(ro_run_pair(R, (uint32_t)i), P);
+        }
+      }
+    }
+    if (!cont) runs.push_back(RoRun{(uint32_t)i, P.base, P.qoff, P.voff, P.cvoff, P.meta, P.series, 0u});
+    rid[i] = (uint32_t)(runs.size() - 1);
+  }
+  const int64_t nr = (int64_t)runs.size();
+  if (nr * (int64_t)sizeof(RoRun) + n * 4 >= n * (int64_t)sizeof(RoPair)) return 0;   // the pairs are smaller
+  HIP_OK(c->ro_runs.ensure(nr * (int64_t)sizeof(RoRun)));
+  HIP_OK(c->ro_rid.ensure(n * 4));
+  HIP_OK(hipMemcpy(c->ro_runs.p, runs.data(), nr * sizeof(RoRun), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(c->ro_rid.p, rid.data(), n * 4, hipMemcpyHostToDevice));
+  c->ro_pairs.release();
+  c->ro_nruns = nr;
+  return 0;
+}
+
 
 }  // namespace
 
@@ -1620,6 +1674,8 @@ extern "C" int tsdbhip_load_rollup(tsdbhip_ctx* c, const tsdbhip_rollup_batch* r
       dv.release();   // (DevBuf frees nothing on its own)
       ds.release();
       HIP_OK(e);
+      int rc = ro_build_runs(c);
+      if (rc) return rc;
     } else {
       c->ro_npairs = 0;
     }
@@ -3157,6 +3213,10 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
         const int avg = P.ro_fuse == 1 ? 1 : 0;
         if (c->ro_npairs > 0) {
           rp.ro_pairs = c->ro_pairs.as<RoPair>();
+          if (c->ro_nruns) {
+            rp.ro_runs = c->ro_runs.as<RoRun>();
+            rp.ro_rid = c->ro_rid.as<uint32_t>();
+          }
           HIP_OK(launch_ro_pairs(rp, avg, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->ro_cmap.as<int64_t>(),
                                  c->ro_npairs, c->stream));
         } else {
@@ -3188,6 +3248,10 @@ int run_device(tsdbhip_ctx* c, const tsdbhip_query* q, const Plan& P, int64_t G,
         rp.redo_mark = c->sr_mark.as<uint32_t>();
         if (c->ro_active && c->ro_npairs > 0 && !P.none) {
           rp.ro_pairs = c->ro_pairs.as<RoPair>();   // a rollup batch's value rows, packed (k_ro_rows)
+          if (c->ro_nruns) {
+            rp.ro_runs = c->ro_runs.as<RoRun>();
+            rp.ro_rid = c->ro_rid.as<uint32_t>();
+          }
           HIP_OK(launch_ro_rows(rp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->ro_npairs, c->stream));
         } else {
           HIP_OK(launch_seq_rows(rp, P.f, c->pre_dense.as<double>(), c->pre_pres.as<uint8_t>(), c->h_srp[ns], c->stream));

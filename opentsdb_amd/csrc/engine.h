@@ -61,6 +61,29 @@ struct RoPair {
   int32_t series;   // the value series (resident position)
 };
 static_assert(sizeof(RoPair) == 24, "RoPair layout");
+// A run of RoPairs of one series that differ only by a constant step: the pair j rows into the
+// run is base0 + j * bstep * 3600 s, qoff0 + j * qs * 16 bytes, ...  A rollup table's hour rows
+// are such runs (one a series when every row holds the same cells), so the walk reads a 4-B run
+// id a pair and one 32-B run for every series instead of 24 B a pair (k_ro_pairs / k_ro_rows).
+struct RoRun {
+  uint32_t first;   // the run's first pair
+  uint32_t base0, qoff0, voff0, cvoff0;
+  uint32_t meta;    // RoPair::meta, equal over the run
+  int32_t series;
+  uint32_t step;    // qs (7 bits) | vs << 7 (9 bits) | cvs << 16 (8 bits) | bstep << 24 (8 bits)
+};
+static_assert(sizeof(RoRun) == 32, "RoRun layout");
+__host__ __device__ inline RoPair ro_run_pair(const RoRun& R, uint32_t i) {
+  const uint32_t j = i - R.first;
+  RoPair P;
+  P.base = R.base0 + j * ((R.step >> 24) * 3600u);
+  P.qoff = R.qoff0 + j * ((R.step & 0x7Fu) << 4);
+  P.voff = R.voff0 + j * (((R.step >> 7) & 0x1FFu) << 4);
+  P.cvoff = R.cvoff0 + j * (((R.step >> 16) & 0xFFu) << 4);
+  P.meta = R.meta;
+  P.series = R.series;
+  return P;
+}
 enum : uint32_t {
   RP_OK = 0x80000000u,    // k_seq_rows_ro's premises hold for the pair
   RP_VOK = 0x40000000u,   // k_seq_rows' premises hold for the value row alone
@@ -149,6 +172,8 @@ struct GridParams {
   const int32_t* ro_partner;   // [n_rows] rollup batch: a value row's count row (-1: a count row,
                                // -2: the count series does not mirror the value series' rows)
   const RoPair* ro_pairs;      // rollup batch: the packed value / count row pairs (k_ro_pairs)
+  const RoRun* ro_runs;        // ... or the pairs as runs (ro_runs[ro_rid[i]] holds pair i)
+  const uint32_t* ro_rid;
   // k_fast: geometry in "n-units" (seconds when every row has second qualifiers and the
   // interval / slot origin are whole seconds, else milliseconds) and the redo list
   int32_t unit_s;        // 1: n-units are seconds

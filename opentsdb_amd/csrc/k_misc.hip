@@ -717,31 +717,29 @@ __device__ __forceinline__ void ro_pair(const GridParams& p, double* __restrict_
   flush();
 }
 
-template <int AVG, int U>
+// pair i: from the packed table, or (RUN) from its run
+template <bool RUN>
+__device__ __forceinline__ RoPair ro_get(const GridParams& p, int64_t i) {
+  if (RUN) return ro_run_pair(p.ro_runs[p.ro_rid[i]], (uint32_t)i);
+  return p.ro_pairs[i];
+}
+
+template <int AVG, bool RUN>
 __global__ __launch_bounds__(256) void k_ro_pairs(GridParams p, double* __restrict__ dense, uint8_t* __restrict__ pres,
                                                   const int64_t* __restrict__ cmap, int64_t n) {
-  // U pairs a thread, blocks of U x 256 consecutive pairs (lane-contiguous for each u): every
-  // pair's descriptor loaded before any is walked
-  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x * U + threadIdx.x;
-  RoPair P[U];
-#pragma unroll
-  for (int u = 0; u < U; u++) {
-    const int64_t i = i0 + (int64_t)u * blockDim.x;
-    if (i < n) P[u] = p.ro_pairs[i];
-    else P[u].base = 0xFFFFFFFFu;   // (outside every scan range)
-  }
-#pragma unroll
-  for (int u = 0; u < U; u++) ro_pair<AVG>(p, dense, pres, cmap, P[u]);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  ro_pair<AVG>(p, dense, pres, cmap, ro_get<RUN>(p, i));
 }
 
 // k_seq_rows over a rollup batch's packed value rows (sum / min / max ... downsampling reads the
 // value series alone): the pair table's value fields, RP_VOK for k_seq_rows' premises.
-template <int F>
+template <int F, bool RUN>
 __global__ __launch_bounds__(256) void k_ro_rows(GridParams p, double* __restrict__ dense, uint8_t* __restrict__ pres,
                                                  int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const RoPair P = p.ro_pairs[i];
+  const RoPair P = ro_get<RUN>(p, i);
   if ((int64_t)P.base < p.ss || (int64_t)P.base >= p.se) return;
   const int64_t s = P.series;
   if (!(P.meta & RP_VOK)) {
@@ -823,9 +821,10 @@ __global__ __launch_bounds__(256) void k_ro_rows(GridParams p, double* __restric
 hipError_t launch_ro_rows(const GridParams& p, int f, double* dense, uint8_t* pres, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const unsigned nb = (unsigned)((n + 255) / 256);
-#define RORO_CASE(FF)                                                                    \
-  case FF:                                                                               \
-    hipLaunchKernelGGL(k_ro_rows<FF>, dim3(nb), dim3(256), 0, s, p, dense, pres, n);     \
+#define RORO_CASE(FF)                                                                      \
+  case FF:                                                                                 \
+    if (p.ro_runs) hipLaunchKernelGGL((k_ro_rows<FF, true>), dim3(nb), dim3(256), 0, s, p, dense, pres, n); \
+    else hipLaunchKernelGGL((k_ro_rows<FF, false>), dim3(nb), dim3(256), 0, s, p, dense, pres, n);         \
     break;
   switch (f) {
     RORO_CASE(F_SUM) RORO_CASE(F_AVG) RORO_CASE(F_COUNT) RORO_CASE(F_SQUARESUM) RORO_CASE(F_MIN) RORO_CASE(F_MAX)
@@ -841,8 +840,13 @@ hipError_t launch_ro_pairs(const GridParams& p, int avg, double* dense, uint8_t*
   if (n <= 0) return hipSuccess;
   // (2 or 4 pairs a thread, every descriptor loaded first, measured no faster: profiles/r05au)
   const unsigned nb = (unsigned)((n + 255) / 256);
-  if (avg) hipLaunchKernelGGL((k_ro_pairs<1, 1>), dim3(nb), dim3(256), 0, s, p, dense, pres, cmap, n);
-  else hipLaunchKernelGGL((k_ro_pairs<0, 1>), dim3(nb), dim3(256), 0, s, p, dense, pres, cmap, n);
+  if (p.ro_runs) {
+    if (avg) hipLaunchKernelGGL((k_ro_pairs<1, true>), dim3(nb), dim3(256), 0, s, p, dense, pres, cmap, n);
+    else hipLaunchKernelGGL((k_ro_pairs<0, true>), dim3(nb), dim3(256), 0, s, p, dense, pres, cmap, n);
+  } else {
+    if (avg) hipLaunchKernelGGL((k_ro_pairs<1, false>), dim3(nb), dim3(256), 0, s, p, dense, pres, cmap, n);
+    else hipLaunchKernelGGL((k_ro_pairs<0, false>), dim3(nb), dim3(256), 0, s, p, dense, pres, cmap, n);
+  }
   return hipGetLastError();
 }
 

@@ -602,7 +602,7 @@ __global__ __launch_bounds__(256) void k_emit_reg(GridParams p) {
     rem &= rem - 1;
     return s0 + i;
   };
-  constexpr int EMIT_D = 4;
+  constexpr int EMIT_D = 16;
   uint8_t pr[EMIT_D];
   double v[EMIT_D];
 #pragma unroll

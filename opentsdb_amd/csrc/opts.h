@@ -35,6 +35,7 @@ enum Opt : int {
   OPT_RAW_SEL_TOP,    // 0: raw percentiles through the per-point kernels
   OPT_RAW_SEL_REG,    // 0: the LDS-staged raw percentile kernel
   OPT_RO_FUSE,        // 0: rollup avg / count in two passes
+  OPT_RO_RUNS,        // 0: rollup pairs read packed, not as runs
   OPT_MULTI_FUSE,     // 0: tsdbhip_run_multi query by query
   OPT_HIST_WINDOW,    // 0: the per-column atomic histogram kernel
   OPT_HIST_WS,        // > 0: histogram windows of at most this many points

@@ -287,3 +287,37 @@ def test_fused_avg_count_stage(eng, monkeypatch, cnt_hi):
                 np.testing.assert_array_equal(b1, b2, err_msg=f"{ds} {agg}: fused vs separate passes")
                 np.testing.assert_array_equal(i1, i2, err_msg=f"{ds} {agg}")
             assert_groups_match(res["1"], O.run_rollup_query(rb, q), agg, tol=1e-12, ctx=f"{ds} {agg}")
+
+
+@pytest.mark.parametrize("p_cell", [1.0, 0.97])
+@pytest.mark.parametrize("floats", [False, True])
+def test_pair_runs_equal_packed_pairs(eng, p_cell, floats):
+    """Hour rows read as runs (RoRun: one descriptor a series' run of equal-shape rows and a run id
+    a row) give the answers of the packed 24-B pairs (option RO_RUNS = 0), bit for bit, and the
+    oracle's; rows with every cell present form one run a series, rows with cells missing at random
+    mostly runs of one row (the pairs are then kept)."""
+    rng = np.random.default_rng(31 + int(p_cell * 100) + floats)
+    rb = random_table(rng, 300, 7, 2, p_sum=p_cell, p_cnt=p_cell, floats=floats, span="1d")
+    try:
+        res = {}
+        for runs in ("-1", "0"):
+            set_option("RO_RUNS", runs)
+            eng.load_rollup(rb)
+            for ds, agg in (("1h-avg", "sum"), ("1h-count", "sum"), ("30m-sum", "max"), ("1h-max", "none"),
+                            ("1h-avg", "p90"), ("2h-min", "avg")):
+                q = _q(ds, agg, start=B + 1800, end=B + 2 * 86400 - 3600)
+                res[(runs, ds, agg)] = eng.run(q)
+        for (runs, ds, agg), got in res.items():
+            if runs != "-1":
+                continue
+            ref = res[("0", ds, agg)]
+            assert len(got) == len(ref)
+            for (g1, t1, b1, i1), (g2, t2, b2, i2) in zip(got, ref):
+                assert g1 == g2
+                np.testing.assert_array_equal(t1, t2, err_msg=f"{ds} {agg}")
+                np.testing.assert_array_equal(b1, b2, err_msg=f"{ds} {agg}: runs vs packed pairs")
+                np.testing.assert_array_equal(i1, i2, err_msg=f"{ds} {agg}")
+            q = _q(ds, agg, start=B + 1800, end=B + 2 * 86400 - 3600)
+            assert_groups_match(got, O.run_rollup_query(rb, q), agg, tol=1e-12, ctx=f"runs {ds} {agg}")
+    finally:
+        set_option("RO_RUNS", "-1")

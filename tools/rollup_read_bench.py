@@ -77,7 +77,11 @@ def main():
     ap.add_argument("--groups", type=int, default=64)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--opt", action="append", default=[], help="developer option NAME=VALUE (A/B runs)")
     a = ap.parse_args()
+    for kv in a.opt:
+        k, v = kv.split("=")
+        E.set_option(k, v)
     t = time.perf_counter()
     rb, n_cells = table(a.series, a.days, a.interval, a.span, a.groups)
     gen_s = time.perf_counter() - t
