@@ -55,6 +55,11 @@ def main():
     gen_s = time.perf_counter() - t
     if "--pinned-first" in sys.argv:   # (diagnostic: page-locked buffers before the context exists)
         cb = pinned(cb)
+    from opentsdb_amd.engine import set_option
+    for a in sys.argv:   # --opt=NAME=VALUE: a developer option (A/B runs)
+        if a.startswith("--opt="):
+            k, v = a[6:].split("=")
+            set_option(k, v)
     eng = Engine(0)
     if "--pinned" in sys.argv:
         cb = pinned(cb)
