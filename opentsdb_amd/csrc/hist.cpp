@@ -80,7 +80,7 @@ struct HistStore {
   std::vector<int32_t> group;                   // [n_series]
   // query scratch
   Buf q_rlo, q_rhi, q_out, q_slot, q_key, q_key2, q_pos, q_pos2, q_head, q_incl, q_point, q_ptts, q_ptgrp;
-  Buf q_vlen, q_voff, q_vpos;   // windowed accumulation: the spans' positions in output-group order
+  Buf q_vlen, q_voff, q_vpos, q_tix;   // windowed accumulation: the spans' positions in output-group order, their entries
   Buf q_caltab, q_spcal;         // calendar downsampling: boundary runs per span anchor
   Buf q_gsp, q_spq, q_spts;      // greedy walk over spans out of time order (k_hist_walk)
   Buf acc, pres, pkind, flag, ptout, err, pct;
@@ -90,7 +90,7 @@ struct HistStore {
   void release() {
     for (Buf* b : {&val, &voff, &codec, &status, &hkey, &hcount, &hidx, &dlo, &dup, &lkey, &lidx, &lkey2, &lidx2, &pos_cell, &pos_ts, &pos_kind,
                    &row_pos, &col_lid, &lay_col, &lay_off, &lay_di, &q_rlo, &q_rhi, &q_out, &q_slot, &q_key, &q_key2, &q_pos, &q_pos2, &q_head, &q_incl,
-                   &q_point, &q_ptts, &q_ptgrp, &q_vlen, &q_voff, &q_vpos, &q_caltab, &q_spcal, &q_gsp, &q_spq, &q_spts, &acc, &pres, &pkind, &flag, &ptout, &err, &pct, &o_ts, &o_grp,
+                   &q_point, &q_ptts, &q_ptgrp, &q_vlen, &q_voff, &q_vpos, &q_tix, &q_caltab, &q_spcal, &q_gsp, &q_spq, &q_spts, &acc, &pres, &pkind, &flag, &ptout, &err, &pct, &o_ts, &o_grp,
                    &o_kind, &o_pct, &o_cnt, &o_pres})
       b->release();
     if (tmp) (void)hipFree(tmp);
@@ -644,7 +644,9 @@ int hist_run(tsdbhip_ctx* c, const tsdbhip_query* q, int64_t start, int64_t end,
     int64_t nvp = 0;
     HOK(hist_vpos(S->q_rlo.as<int64_t>(), S->q_rhi.as<int64_t>(), S->row_pos.as<int64_t>(), nsp, S->q_vlen.as<uint32_t>(),
                   S->q_voff.as<int64_t>(), S->q_vpos.as<int32_t>(), &nvp, &S->tmp, &S->tmp_bytes, st));
-    HOK(hist_accum_window(p, S->q_vpos.as<int32_t>(), nvp, S->lkey2.as<uint64_t>(), S->lidx2.as<int32_t>(), S->lslots, st));
+    HOK(S->q_tix.ensure(nvp * 24 + 24));
+    HOK(hist_accum_window(p, S->q_vpos.as<int32_t>(), nvp, S->lkey2.as<uint64_t>(), S->lidx2.as<int32_t>(), S->lslots,
+                          S->q_tix.p, st));
   } else {
     HOK(hist_accum(p, NP, S->lds_dict ? S->lkey.as<uint64_t>() : nullptr, S->lds_dict ? S->lidx.as<int32_t>() : nullptr, st));
   }

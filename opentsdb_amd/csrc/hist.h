@@ -126,8 +126,9 @@ hipError_t hist_vpos(const int64_t* rlo, const int64_t* rhi, const int64_t* row_
 // points of the k_hist_accw LDS window for this query (0: the counters do not fit, use hist_accum)
 int hist_window_points(const HistQueryParams& p, int lslots);
 // windowed accumulation over vpos (spans sorted by output group); needs the LDS dictionary
+// tix_buf: nvp x 24 B of scratch (the positions' packed column entries, k_hist_tidx)
 hipError_t hist_accum_window(const HistQueryParams& p, const int32_t* vpos, int64_t nvp, const uint64_t* lkey,
-                             const int32_t* lidx, int lslots, hipStream_t s);
+                             const int32_t* lidx, int lslots, void* tix_buf, hipStream_t s);
 // Bucket layouts (load): a SimpleHistogram column with strictly increasing keys whose key bytes
 // equal the previous column's shares its layout; col_lid[c] = the layout, lay_col[l] = its first
 // column.  hist_layout_index writes col_lid / lay_col and returns the layout count;

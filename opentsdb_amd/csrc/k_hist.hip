@@ -920,8 +920,34 @@ __device__ void w_flush(const HistQueryParams& p, const Window& w, int64_t wb, i
   __syncthreads();
 }
 
+// A position's column as k_hist_accw reads it: one coalesced 24-B load a lane instead of the
+// vpos -> pos_point / pos_cell -> voff / col_lid chain (three dependent round trips a tile), so the
+// next tile's entries are in flight while the current tile is staged and parsed.
+struct HTIdx {
+  uint64_t vo0;    // the column's value bytes [vo0, vo0 + len)
+  uint32_t len;
+  uint32_t kind;   // pos_kind
+  int32_t pt;      // output point (-1: none)
+  int32_t lid;     // layout id (-1: none)
+};
+static_assert(sizeof(HTIdx) == 24, "HTIdx layout");
+
+__global__ void k_hist_tidx(HistQueryParams p, const int32_t* __restrict__ vpos, int64_t nvp, HTIdx* __restrict__ out) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= nvp) return;
+  const int64_t q = vpos[v];
+  const int64_t c = p.pos_cell[q];
+  HTIdx x;
+  x.vo0 = p.voff[c];
+  x.len = (uint32_t)(p.voff[c + 1] - x.vo0);
+  x.kind = p.pos_kind[q];
+  x.pt = p.pos_point ? p.pos_point[q] : p.pos_slot[q];
+  x.lid = p.col_lid ? p.col_lid[c] : -1;
+  out[v] = x;
+}
+
 template <bool PIPE, int SU>
-__global__ void __launch_bounds__(ATP) k_hist_accw(HistQueryParams p, const int32_t* __restrict__ vpos, int64_t nvp,
+__global__ void __launch_bounds__(ATP) k_hist_accw(HistQueryParams p, const HTIdx* __restrict__ tix, int64_t nvp,
                                                    int64_t chunk, const uint64_t* lkey_g, const int32_t* lidx_g, int WS,
                                                    int LS) {
   extern __shared__ uint4 smem4[];   // (16-byte aligned: the stage takes 16-byte stores)
@@ -945,11 +971,14 @@ __global__ void __launch_bounds__(ATP) k_hist_accw(HistQueryParams p, const int3
   const DictLds dict{lkey, lidx, (uint32_t)(LS - 1)};
   const int64_t v0 = (int64_t)blockIdx.x * chunk, v1 = min(nvp, v0 + chunk);
   int64_t wb = -1;
+  HTIdx nx{};
+  if (v0 + tid < v1) nx = tix[v0 + tid];
   for (int64_t t0 = v0; t0 < v1; t0 += ATP) {
-    const int64_t v = t0 + tid;
-    const bool in = v < v1;
-    const int64_t q = in ? (int64_t)vpos[v] : -1;
-    const int32_t pt = in ? (p.pos_point ? p.pos_point[q] : p.pos_slot[q]) : -1;
+    const bool in = t0 + tid < v1;
+    const HTIdx cur = nx;
+    if (t0 + ATP + tid < v1) nx = tix[t0 + ATP + tid];   // the next tile's entries, in flight from here
+    const int32_t pt = in ? cur.pt : -1;
+    const uint64_t vo0 = cur.vo0, vend = cur.vo0 + cur.len;
     // the tile's point range
     int32_t mn = pt >= 0 ? pt : INT32_MAX, mx = pt;
 #pragma unroll
@@ -959,11 +988,10 @@ __global__ void __launch_bounds__(ATP) k_hist_accw(HistQueryParams p, const int3
     }
     __syncthreads();   // the previous tile's stage and descriptors are consumed
     if (lane == 0) { red[wv * 2] = mn; red[wv * 2 + 1] = mx; }
-    // runs of consecutive cells (the stage plan)
-    const int64_t c = in ? p.pos_cell[q] : 0;
-    const int64_t cprev = __shfl_up(c, 1);
+    // runs of contiguous column bytes (the stage plan)
+    const uint64_t eprev = __shfl_up(vend, 1);
     const bool inprev = __shfl_up((int)in, 1) != 0;
-    bool head = in && (lane == 0 || !inprev || c != cprev + 1);
+    bool head = in && (lane == 0 || !inprev || vo0 != eprev);
     const uint64_t hb = __ballot(head);
     if (lane == 0) wheads[wv] = __popcll(hb);
     __syncthreads();
@@ -974,25 +1002,19 @@ __global__ void __launch_bounds__(ATP) k_hist_accw(HistQueryParams p, const int3
       if (wb >= 0) w_flush(p, win, wb, WS);
       wb = mn;
     }
-    // a run that crosses the wave boundary continues in wave 1's lane 0
+    // every wave's lane 0 starts a run, so no run crosses a wave boundary
     const int nh0 = wheads[0], nruns = nh0 + wheads[1];
     const int rid = (wv ? nh0 : 0) + (int)__popcll(hb & ((1ull << lane) - 1)) - (head ? 0 : 1);
     const bool fit = nruns <= WRUNS;
     if (fit && in) {
-      const uint64_t nxt_c = __shfl_down(c, 1);
+      const uint64_t nxt_b = __shfl_down(vo0, 1);
       const bool nxt_in = __shfl_down((int)in, 1) != 0;
-      // the last lane of a run: the next lane starts another run, is out, or is in the next wave
-      bool last = lane == 63 || !nxt_in || nxt_c != (uint64_t)c + 1;
-      if (lane == 63 && wv == 0) {
-        // continues into wave 1 only when wave 1's lane 0 is not a head: read it through LDS
-        last = true;
-      }
-      if (head) run_b0[rid] = p.voff[c];
-      if (last) run_b1[rid] = p.voff[c + 1];
+      const bool last = lane == 63 || !nxt_in || nxt_b != vend;
+      if (head) run_b0[rid] = vo0;
+      if (last) run_b1[rid] = vend;
     }
     __syncthreads();
-    // run r's dwords [w0, w1) at LDS dword base; wave 0's last run may continue in wave 1: the
-    // descriptor of a run that does not start with a head in wave 1 lane 0 is merged below
+    // run r's dwords [w0, w1) at LDS dword base
     uint64_t my_b0 = 0;
     uint32_t my_base = 0;
     bool staged = fit;
@@ -1034,13 +1056,13 @@ __global__ void __launch_bounds__(ATP) k_hist_accw(HistQueryParams p, const int3
     }
     if (pt < 0) continue;
     const int32_t local = pt - wb < WS ? (int32_t)(pt - wb) : -1;
-    const uint8_t kind = p.pos_kind[q];
+    const uint8_t kind = (uint8_t)cur.kind;
     if (staged) {
-      const uint64_t i0 = (uint64_t)my_base * 4 + (p.voff[c] - my_b0 * 4);
-      if (PIPE) accum_column_wp(p, win, pt, local, SrcW{stage}, i0, kind, dict, p.col_lid ? p.col_lid[c] : -1);
+      const uint64_t i0 = (uint64_t)my_base * 4 + (vo0 - my_b0 * 4);
+      if (PIPE) accum_column_wp(p, win, pt, local, SrcW{stage}, i0, kind, dict, cur.lid);
       else accum_column_w(p, win, pt, local, SrcW{stage}, i0, kind, dict);
     } else {
-      accum_column_w(p, win, pt, local, SrcW{reinterpret_cast<const uint32_t*>(p.val)}, p.voff[c], kind, dict);
+      accum_column_w(p, win, pt, local, SrcW{reinterpret_cast<const uint32_t*>(p.val)}, vo0, kind, dict);
     }
   }
   if (wb >= 0) w_flush(p, win, wb, WS);
@@ -1154,15 +1176,19 @@ int hist_window_points(const HistQueryParams& p, int lslots) {
 }
 
 hipError_t hist_accum_window(const HistQueryParams& p, const int32_t* vpos, int64_t nvp, const uint64_t* lkey,
-                             const int32_t* lidx, int lslots, hipStream_t s) {
+                             const int32_t* lidx, int lslots, void* tix_buf, hipStream_t s) {
   if (nvp <= 0) return hipSuccess;
+  HTIdx* tix = reinterpret_cast<HTIdx*>(tix_buf);
+  hipLaunchKernelGGL(k_hist_tidx, dim3((unsigned)((nvp + 255) / 256)), dim3(256), 0, s, p, vpos, nvp, tix);
   const int WS = hist_window_points(p, lslots);
   if (WS <= 0 || !lkey) return hipErrorInvalidValue;
   const size_t lds = (size_t)(STAGE_W + 8) * 4 + (size_t)lslots * 12 + (size_t)WS * p.C * 8 + (size_t)WS * 4 +
                      (p.pres ? (size_t)WS * p.W * 4 : 0);
   // the pipelined bucket loop with 4 staging loads in flight a thread.  r03o sweep of the
   // histogram bench query: 52 KB window + 4 in flight 2.60 ms; + 16 2.77; 80 KB 3.21 / 3.40; 160 KB
-  // 5.08; the unpipelined loop lost as well (those variants are gone)
+  // 5.08; the unpipelined loop lost as well (those variants are gone).  Round 6: the next
+  // tile's stage units in registers during the parse measured slower (1.80 vs 1.54 ms,
+  // profiles/r06as/): the parse, not the staging round trips, holds the tile
   const void* kf = reinterpret_cast<const void*>(&k_hist_accw<true, 4>);
   hipError_t e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -1173,7 +1199,7 @@ hipError_t hist_accum_window(const HistQueryParams& p, const int32_t* vpos, int6
   const int64_t want = std::min<int64_t>(tiles, (int64_t)cus * per_cu);
   const int64_t chunk = ((tiles + want - 1) / want) * ATP;
   const unsigned grid = (unsigned)((nvp + chunk - 1) / chunk);
-  hipLaunchKernelGGL((k_hist_accw<true, 4>), dim3(grid), dim3(ATP), lds, s, p, vpos, nvp, chunk, lkey, lidx, WS, lslots);
+  hipLaunchKernelGGL((k_hist_accw<true, 4>), dim3(grid), dim3(ATP), lds, s, p, tix, nvp, chunk, lkey, lidx, WS, lslots);
   return hipGetLastError();
 }
 hipError_t hist_layout_index(int64_t n_cells, const uint64_t* voff, const uint8_t* val, const uint8_t* status,
