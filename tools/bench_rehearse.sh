@@ -4,6 +4,7 @@
 #   rccl1 : torch.distributed.run, one rank, the RCCL (nccl) process group forced on
 #   gloo2 : torch.distributed.run, two ranks sharing GPU 0 over gloo (the exchange code of N>1)
 #   md2   : the one-process multi-device context over GPU 0 repeated twice (peer copies)
+#   md4   : the same over GPU 0 repeated four times
 # usage: tools/bench_rehearse.sh <tag> [steps...]   (outputs under gpurun_out/<tag>/)
 set -o pipefail
 tag=$1; shift
@@ -21,6 +22,7 @@ for s in $steps; do
     gloo2) TSDBHIP_BENCH_DIST=gloo TSDBHIP_BENCH_DEVICES=0,0 timeout -k 10 500 $TR --nproc-per-node 2 --master-port 29512 \
              bench.py --gpus 2 --series 500000 $C > $out/$s.jsonl 2> $out/$s.err ;;
     md2)   TSDBHIP_BENCH_DEVICES=0,0 timeout -k 10 500 python -u bench.py --gpus 2 --transport copy $C > $out/$s.jsonl 2> $out/$s.err ;;
+    md4)   TSDBHIP_BENCH_DEVICES=0,0,0,0 timeout -k 10 500 python -u bench.py --gpus 4 --transport copy $C > $out/$s.jsonl 2> $out/$s.err ;;
   esac
   rc=$?
   python3 - $out/$s.jsonl <<'PY' || true
