@@ -43,6 +43,42 @@ __device__ __forceinline__ void seq_values(const uint8_t* vb, int64_t i0, int vl
   }
 }
 
+// values of datapoints i0 .. i0 + 3 (i0 a multiple of 4) of a uniform row: seq_values' decode
+// in half the registers (the rollup pair walk, one hour row a thread)
+__device__ __forceinline__ void seq_values4(const uint8_t* vb, int64_t i0, int vl, const uint32_t fl[4], double val[4],
+                                            bool ints) {
+  if (vl == 8) {
+    const uint4* v = reinterpret_cast<const uint4*>(vb + i0 * 8);
+    const uint4 a0 = v[0], a1 = v[1];
+    const uint32_t ws[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint64_t b = ((uint64_t)__builtin_bswap32(ws[2 * j]) << 32) | __builtin_bswap32(ws[2 * j + 1]);
+      val[j] = (!ints && (fl[j] & 8)) ? __longlong_as_double((long long)b) : (double)(long long)b;
+    }
+  } else if (vl == 4) {
+    const uint4 a0 = *reinterpret_cast<const uint4*>(vb + i0 * 4);
+    const uint32_t ws[4] = {a0.x, a0.y, a0.z, a0.w};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t be = __builtin_bswap32(ws[j]);
+      val[j] = (!ints && (fl[j] & 8)) ? (double)__uint_as_float(be) : (double)(int32_t)be;
+    }
+  } else if (vl == 2) {
+    const uint2 a0 = *reinterpret_cast<const uint2*>(vb + i0 * 2);
+    const uint32_t ws[2] = {a0.x, a0.y};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t be = __builtin_bswap32(ws[j >> 1]);
+      val[j] = (double)(int16_t)(uint16_t)((j & 1) ? (be & 0xFFFF) : (be >> 16));
+    }
+  } else {
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(vb + i0);
+#pragma unroll
+    for (int j = 0; j < 4; j++) val[j] = (double)(int8_t)((w >> (j * 8)) & 0xFF);
+  }
+}
+
 // ---- k_seq_dense: Java's bucket order, one series per thread -------------------------
 // Sum / avg downsampling of rows whose values cannot add exactly in any order (ROW_NOCERT):
 // each thread walks its series' uniform rows in stored order, adding every bucket's values one
@@ -671,15 +707,16 @@ __device__ __forceinline__ void ro_pair(const GridParams& p, double* __restrict_
     dense[s * K + cur] = AVG ? (count == 0.0 ? 0.0 : sum / count) : count;
     pres[s * K + cur] = 1;
   };
-  const uint32_t fl_int[DPL] = {0, 0, 0, 0, 0, 0, 0, 0};   // count cells: integers
-  for (int64_t i0 = 0; i0 < (int64_t)ndp; i0 += DPL) {
-    const int nv = (int)min((int64_t)DPL, (int64_t)ndp - i0);
-    uint32_t off[DPL], fl[DPL];
+  // four datapoints a step (seq_values4): half the registers of an 8-point step, so more waves a
+  // SIMD hide the row loads (an hour row of 10m cells is 6 points)
+  for (int64_t i0 = 0; i0 < (int64_t)ndp; i0 += 4) {
+    const int nv = (int)min((int64_t)4, (int64_t)ndp - i0);
+    uint32_t off[4], fl[4];
     if (!q4) {
-      const uint4 q = *reinterpret_cast<const uint4*>(qb + i0 * 2);
-      const uint32_t ws[4] = {q.x, q.y, q.z, q.w};
+      const uint2 q = *reinterpret_cast<const uint2*>(qb + i0 * 2);
+      const uint32_t ws[2] = {q.x, q.y};
 #pragma unroll
-      for (int j = 0; j < DPL; j++) {
+      for (int j = 0; j < 4; j++) {
         const uint32_t be = __builtin_bswap32(ws[j >> 1]);
         const uint32_t qq = (j & 1) ? (be & 0xFFFF) : (be >> 16);
         off[j] = (qq >> 4) * 1000u;
@@ -687,20 +724,19 @@ __device__ __forceinline__ void ro_pair(const GridParams& p, double* __restrict_
       }
     } else {
       const uint4 q0 = *reinterpret_cast<const uint4*>(qb + i0 * 4);
-      const uint4 q1 = *reinterpret_cast<const uint4*>(qb + i0 * 4 + 16);
-      const uint32_t ws[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+      const uint32_t ws[4] = {q0.x, q0.y, q0.z, q0.w};
 #pragma unroll
-      for (int j = 0; j < DPL; j++) {
+      for (int j = 0; j < 4; j++) {
         const uint32_t qq = __builtin_bswap32(ws[j]);
         off[j] = (qq & 0x0FFFFFC0u) >> 6;
         fl[j] = qq & 0xF;
       }
     }
-    double val[DPL], cnt[DPL];
-    seq_values(vb, i0, vl, fl, val);
-    seq_values(vbc, i0, vlc, fl_int, cnt);
+    double val[4], cnt[4];
+    seq_values4(vb, i0, vl, fl, val, false);
+    seq_values4(vbc, i0, vlc, fl, cnt, true);   // (count cells: integers)
 #pragma unroll
-    for (int j = 0; j < DPL; j++) {
+    for (int j = 0; j < 4; j++) {
       if (j >= nv) break;
       const int k = slot_of(p, g, P.base, off[j]);
       if (k < 0) continue;
@@ -770,14 +806,14 @@ __global__ __launch_bounds__(256) void k_ro_rows(GridParams p, double* __restric
   BState st;
   bs_init<F>(st);
   int cur = -1;
-  for (int64_t i0 = 0; i0 < (int64_t)ndp; i0 += DPL) {
-    const int nv = (int)min((int64_t)DPL, (int64_t)ndp - i0);
-    uint32_t off[DPL], fl[DPL];
+  for (int64_t i0 = 0; i0 < (int64_t)ndp; i0 += 4) {   // four datapoints a step (as k_ro_pairs)
+    const int nv = (int)min((int64_t)4, (int64_t)ndp - i0);
+    uint32_t off[4], fl[4];
     if (!q4) {
-      const uint4 q = *reinterpret_cast<const uint4*>(qb + i0 * 2);
-      const uint32_t ws[4] = {q.x, q.y, q.z, q.w};
+      const uint2 q = *reinterpret_cast<const uint2*>(qb + i0 * 2);
+      const uint32_t ws[2] = {q.x, q.y};
 #pragma unroll
-      for (int j = 0; j < DPL; j++) {
+      for (int j = 0; j < 4; j++) {
         const uint32_t be = __builtin_bswap32(ws[j >> 1]);
         const uint32_t qq = (j & 1) ? (be & 0xFFFF) : (be >> 16);
         off[j] = (qq >> 4) * 1000u;
@@ -785,19 +821,18 @@ __global__ __launch_bounds__(256) void k_ro_rows(GridParams p, double* __restric
       }
     } else {
       const uint4 q0 = *reinterpret_cast<const uint4*>(qb + i0 * 4);
-      const uint4 q1 = *reinterpret_cast<const uint4*>(qb + i0 * 4 + 16);
-      const uint32_t ws[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+      const uint32_t ws[4] = {q0.x, q0.y, q0.z, q0.w};
 #pragma unroll
-      for (int j = 0; j < DPL; j++) {
+      for (int j = 0; j < 4; j++) {
         const uint32_t qq = __builtin_bswap32(ws[j]);
         off[j] = (qq & 0x0FFFFFC0u) >> 6;
         fl[j] = qq & 0xF;
       }
     }
-    double val[DPL];
-    seq_values(vb, i0, vl, fl, val);
+    double val[4];
+    seq_values4(vb, i0, vl, fl, val, false);
 #pragma unroll
-    for (int j = 0; j < DPL; j++) {
+    for (int j = 0; j < 4; j++) {
       if (j >= nv) break;
       const int k = slot_of(p, g, P.base, off[j]);
       if (k < 0) continue;
