@@ -100,8 +100,8 @@ static hipError_t launch_fast_t(const GridParams& p, hipStream_t s) {
     const int64_t nl = (p.n_launch > 0 ? p.n_launch : p.n_tiles) * std::max(1, (int)p.win_split);
     const int64_t blocks = (nl + p.waves - 1) / p.waves;
     const size_t lds = (size_t)p.wave_lds * p.waves;
-    if constexpr (QW == 2 && VL == 0) {
-      if (p.short6) {   // vle rows of <= 384 points: 6 a lane (the kernel hands longer rows back)
+    if constexpr (QW == 2 && (VL == 0 || VL == 4)) {
+      if (p.short6) {   // vle / float32 rows of <= 384 points: 6 a lane (the kernel hands longer rows back)
         if (p.multi)
           hipLaunchKernelGGL((k_hwin<F, QW, VL, 2, true, 6>), dim3((unsigned)blocks), dim3(64 * p.waves), lds, s, p,
                              p.rows, p.series_row_ptr, p.tile_begin, p.tile_end);
