@@ -196,7 +196,7 @@ const char* tsdbhip_last_error(void);
  * small compaction chunks, ...), by name without a prefix: FAST, SHORT, ROWS, HWIN, SEQ,
  * SEQ_ROWS, SEQ_WAVE, INDEX_GENERIC, CMP_CHUNK, CMP_ROWS, CMP_ONEPASS, PCT_ROWS, PCT_KEYS,
  * PCT_VONLY, PCT_V6, SEL_FUSED, SEL_COLS, SEL_WIN, SEL_WAVE, SEL_REG, SELOPS, RAW_LERPW,
- * RAW_SEL_TOP, RAW_SEL_REG, RO_FUSE, RO_RUNS, MULTI_FUSE, HIST_WINDOW, HIST_WS, HIST_LAYOUT, TRACE, DBG
+ * RAW_SEL_TOP, RAW_SEL_REG, RO_FUSE, RO_RUNS, MULTI_FUSE, EMIT_HALF, HIST_WINDOW, HIST_WS, HIST_LAYOUT, TRACE, DBG
  * (opentsdb_amd/csrc/opts.h says what each value does).  Process-wide; -1 resets an option to
  * its production choice, which is every option's initial state.  The library reads no
  * environment variable: an inherited environment cannot change its kernels.  DBG is honoured

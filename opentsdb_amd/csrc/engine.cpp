@@ -610,7 +610,7 @@ std::atomic<int64_t> g_opts[OPT_COUNT];
 const char* const kOptNames[OPT_COUNT] = {
     "FAST", "SHORT", "ROWS", "HWIN", "SEQ", "SEQ_ROWS", "SEQ_WAVE", "INDEX_GENERIC", "CMP_CHUNK", "CMP_ROWS",
     "CMP_ONEPASS", "PCT_ROWS", "PCT_KEYS", "PCT_VONLY", "PCT_V6", "SEL_FUSED", "SEL_COLS", "SEL_WIN", "SEL_WAVE",
-    "SEL_REG", "SELOPS", "RAW_LERPW", "RAW_SEL_TOP", "RAW_SEL_REG", "RO_FUSE", "RO_RUNS", "MULTI_FUSE", "HIST_WINDOW",
+    "SEL_REG", "SELOPS", "RAW_LERPW", "RAW_SEL_TOP", "RAW_SEL_REG", "RO_FUSE", "RO_RUNS", "MULTI_FUSE", "EMIT_HALF", "HIST_WINDOW",
     "HIST_WS", "HIST_LAYOUT", "TRACE", "DBG"};
 int opt_index(const char* name) {
   if (!name) return -1;

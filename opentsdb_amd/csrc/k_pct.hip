@@ -623,6 +623,125 @@ __global__ __launch_bounds__(256) void k_emit_reg(GridParams p) {
   rp_store(p, tile, K, RP);
 }
 
+// slot_contribution for a half wave (K <= 32): lanes 32h .. 32h + 31 are slots 0 .. 31 of one
+// series; presence, neighbours and shuffles stay inside the half
+__device__ __forceinline__ bool slot_contribution_half(const GridParams& p, int K, bool pr_in, bool valid, double v,
+                                                       double& cv, bool& uni) {
+  const int lane = lane_id(), h = lane >> 5, sl = lane & 31;
+  const bool inK = valid && sl < K;
+  const bool pr = inK && pr_in;
+  uni = false;
+  if (p.fill != TSDB_FILL_NONE && p.mode != MODE_ALL) {
+    const double fillv = (p.fill == TSDB_FILL_ZERO) ? 0.0 : (double)NAN;
+    if (!inK) return false;
+    if (!pr && p.fill == TSDB_FILL_SCALAR) set_err(p.err, TSDB_E_RUNTIME);
+    if (sl == 0 && p.skip0) return false;
+    cv = pr ? v : fillv;
+    uni = true;
+    return true;
+  }
+  const uint32_t pm = (uint32_t)(__ballot(pr) >> (32 * h));
+  if (pm == (K >= 32 ? 0xFFFFFFFFu : ((1u << K) - 1))) {   // every slot present: no interpolation
+    cv = v;
+    uni = inK;
+    return inK;
+  }
+  const uint32_t below = pm & ((1u << sl) - 1);
+  const uint32_t above = sl == 31 ? 0u : (pm & ~((2u << sl) - 1));
+  const int prv = below ? 31 - __clz((int)below) : -1;
+  const int nxt = above ? __ffs((int)above) - 1 : 32;
+  const bool need = inK && !pr && prv >= 0 && nxt < K;
+  double y0 = 0.0, y1 = 0.0;
+  if (__ballot(need)) {
+    y0 = __shfl(v, 32 * h + max(prv, 0), 64);
+    y1 = __shfl(v, 32 * h + min(nxt, 31), 64);
+  }
+  if (pr) {
+    cv = v;
+    uni = true;
+    return true;
+  }
+  if (need) {
+    cv = interp(p.interp, p, prv, y0, nxt, y1, sl);
+    return true;
+  }
+  return false;
+}
+
+// k_emit_reg for K <= 32: two series a step, the lower half wave the earlier one -- both halves
+// find their contributions (presence ballots, LERP neighbours) at once, and the lower half's
+// lanes fold the two into the slot's partial in series order, so the partial is the one-series-
+// a-step kernel's bit for bit.  Half the serial steps a tile, and every load instruction feeds
+// 2K lanes instead of K.
+template <int GA>
+__global__ __launch_bounds__(256) void k_emit_reg2(GridParams p) {
+  const int lane = lane_id(), h = lane >> 5, sl = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t tile = (int64_t)blockIdx.x * p.waves + wave;
+  if (tile >= p.n_tiles) return;
+  const int K = (int)p.K;
+  const int ga = GA < 0 ? p.ga : GA;
+  const int64_t s0 = p.tile_begin[tile], s1 = p.tile_end[tile];
+  bool mine = false;   // lane i: series s0 + i has a row in the scan range (tiles hold <= 64 series)
+  if (s0 + lane < s1) {
+    const int64_t s = s0 + lane;
+    for (int64_t r = p.series_row_ptr[s]; r < p.series_row_ptr[s + 1]; r++) {
+      const uint32_t base = p.rows[r].base;
+      if ((int64_t)base >= p.ss && (int64_t)base < p.se) { mine = true; break; }
+    }
+  }
+  const uint64_t act = __ballot(mine);
+  if (act && lane == 0) atomicOr(&p.group_active[p.tile_group[tile]], 1u);
+  RegPart RP;
+  rp_init(ga, RP);
+  if (!act) {
+    rp_store(p, tile, K, RP);
+    return;
+  }
+  const int64_t kl = sl < K ? sl : 0;   // (lanes past K read slot 0: in bounds, ignored)
+  const int nact = __popcll(act);
+  const int npair = (nact + 1) >> 1;
+  const int last = 63 - __clzll((long long)act);
+  uint64_t rem = act;
+  auto next = [&]() {   // this half's series of the next pair (the last one again once none is left)
+    const int a = rem ? __ffsll((long long)rem) - 1 : last;
+    rem &= rem - 1;
+    const int b = rem ? __ffsll((long long)rem) - 1 : last;
+    rem &= rem - 1;
+    return s0 + (h ? b : a);
+  };
+  constexpr int EMIT_D = 8;
+  uint8_t pr[EMIT_D];
+  double v[EMIT_D];
+#pragma unroll
+  for (int d = 0; d < EMIT_D; d++) {
+    const int64_t s = next();
+    pr[d] = p.pre_pres[s * K + kl];
+    v[d] = p.pre_dense[s * K + kl];
+  }
+  for (int j = 0; j < npair; j += EMIT_D) {
+#pragma unroll
+    for (int d = 0; d < EMIT_D; d++) {
+      if (j + d < npair) {
+        const bool valid = 2 * (j + d) + h < nact;
+        double cv = 0.0;
+        bool uni = false;
+        const bool c = slot_contribution_half(p, K, pr[d] != 0, valid, v[d], cv, uni);
+        const double cv1 = __shfl(cv, sl + 32, 64);
+        const int cu1 = __shfl((c ? 1 : 0) | (uni ? 2 : 0), sl + 32, 64);
+        if (h == 0) {
+          if (c) contribute_slot(ga, RP, cv, uni);
+          if (cu1 & 1) contribute_slot(ga, RP, cv1, (cu1 & 2) != 0);
+        }
+      }
+      const int64_t s = next();
+      pr[d] = p.pre_pres[s * K + kl];
+      v[d] = p.pre_dense[s * K + kl];
+    }
+  }
+  rp_store(p, tile, K, RP);
+}
+
 // k_emit for K > 64 without rate (a day of 1m buckets: K = 1440): one wave per (tile, window of
 // 64 slots), lane = slot, the window's tile partials in registers -- k_emit keeps K slots of
 // partials in LDS (35 KB a wave at K = 1440: one wave a block, four a CU).  The contributions of
@@ -2360,6 +2479,21 @@ hipError_t launch_pct_rows(const GridParams& p, int qw, int vl, hipStream_t s) {
 
 hipError_t launch_emit(const GridParams& p, hipStream_t s) {
   if (p.n_tiles == 0) return hipSuccess;
+  if (p.K <= 32 && !p.rate && !opt_off(OPT_EMIT_HALF)) {   // two series a step (half waves)
+    GridParams q = p;
+    q.waves = 4;
+    const dim3 grid((unsigned)((p.n_tiles + 3) / 4));
+    switch (p.ga) {
+      case GA_SUM: hipLaunchKernelGGL(k_emit_reg2<GA_SUM>, grid, dim3(256), 0, s, q); break;
+      case GA_AVG: hipLaunchKernelGGL(k_emit_reg2<GA_AVG>, grid, dim3(256), 0, s, q); break;
+      case GA_COUNT: hipLaunchKernelGGL(k_emit_reg2<GA_COUNT>, grid, dim3(256), 0, s, q); break;
+      case GA_MIN: hipLaunchKernelGGL(k_emit_reg2<GA_MIN>, grid, dim3(256), 0, s, q); break;
+      case GA_MAX: hipLaunchKernelGGL(k_emit_reg2<GA_MAX>, grid, dim3(256), 0, s, q); break;
+      case GA_DEV: hipLaunchKernelGGL(k_emit_reg2<GA_DEV>, grid, dim3(256), 0, s, q); break;
+      default: hipLaunchKernelGGL(k_emit_reg2<-1>, grid, dim3(256), 0, s, q); break;
+    }
+    return hipGetLastError();
+  }
   if (p.K <= 64 && !p.rate) {
     GridParams q = p;
     q.waves = 4;

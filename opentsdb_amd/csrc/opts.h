@@ -37,6 +37,7 @@ enum Opt : int {
   OPT_RO_FUSE,        // 0: rollup avg / count in two passes
   OPT_RO_RUNS,        // 0: rollup pairs read packed, not as runs
   OPT_MULTI_FUSE,     // 0: tsdbhip_run_multi query by query
+  OPT_EMIT_HALF,      // 0: no two-series-a-step group-by over stored buckets (k_emit_reg2, K <= 32)
   OPT_HIST_WINDOW,    // 0: the per-column atomic histogram kernel
   OPT_HIST_WS,        // > 0: histogram windows of at most this many points
   OPT_HIST_LAYOUT,    // 0: every histogram bucket through the keyed lookup

@@ -40,7 +40,7 @@ EXPORTS = [
 # developer options (tsdbhip_set_option, opentsdb_amd/csrc/opts.h)
 OPTIONS = ["FAST", "SHORT", "ROWS", "HWIN", "SEQ", "SEQ_ROWS", "SEQ_WAVE", "INDEX_GENERIC", "CMP_CHUNK", "CMP_ROWS",
            "CMP_ONEPASS", "PCT_ROWS", "PCT_KEYS", "PCT_VONLY", "PCT_V6", "SEL_FUSED", "SEL_COLS", "SEL_WIN", "SEL_WAVE",
-           "SEL_REG", "SELOPS", "RAW_LERPW", "RAW_SEL_TOP", "RAW_SEL_REG", "RO_FUSE", "RO_RUNS", "MULTI_FUSE", "HIST_WINDOW",
+           "SEL_REG", "SELOPS", "RAW_LERPW", "RAW_SEL_TOP", "RAW_SEL_REG", "RO_FUSE", "RO_RUNS", "MULTI_FUSE", "EMIT_HALF", "HIST_WINDOW",
            "HIST_WS", "HIST_LAYOUT", "TRACE", "DBG"]
 
 SHARD_AUTO, SHARD_SERIES, SHARD_GROUPS, SHARD_SPANS = -1, 0, 1, 2   # tsdbhip.h TSDB_SHARD_*

@@ -321,3 +321,32 @@ def test_pair_runs_equal_packed_pairs(eng, p_cell, floats):
             assert_groups_match(got, O.run_rollup_query(rb, q), agg, tol=1e-12, ctx=f"runs {ds} {agg}")
     finally:
         set_option("RO_RUNS", "-1")
+
+
+@pytest.mark.parametrize("floats", [False, True])
+def test_emit_half_waves_equal_full_waves(eng, floats):
+    """The group-by over stored buckets with K <= 32 takes two series a step (k_emit_reg2: each
+    half wave one series, the lower half folding both in series order): bit-identical to one series
+    a step (option EMIT_HALF = 0) for every group-by aggregator, with cells missing at random (LERP
+    across holes), fill policies and percentile / median group-bys of the stored buckets."""
+    rng = np.random.default_rng(57 + floats)
+    rb = random_table(rng, 150, 5, 2, p_sum=0.8, p_cnt=0.9, floats=floats, span="1d")
+    eng.load_rollup(rb)
+    specs = [("1h-avg", a) for a in ("sum", "avg", "min", "max", "dev", "count", "zimsum", "mimmax", "first",
+                                     "last", "p90", "median")]
+    specs += [("1h-avg-zero", "sum"), ("1h-avg-nan", "avg"), ("2h-count", "sum"), ("30m-sum", "max")]
+    try:
+        for ds, agg in specs:
+            q = _q(ds, agg, start=B + 1800, end=B + 2 * 86400 - 3600)
+            set_option("EMIT_HALF", None)
+            got = eng.run(q)
+            set_option("EMIT_HALF", 0)
+            ref = eng.run(q)
+            assert len(got) == len(ref)
+            for (g1, t1, b1, i1), (g2, t2, b2, i2) in zip(got, ref):
+                assert g1 == g2
+                np.testing.assert_array_equal(t1, t2, err_msg=f"{ds} {agg}")
+                np.testing.assert_array_equal(b1, b2, err_msg=f"{ds} {agg}: half waves vs full waves")
+                np.testing.assert_array_equal(i1, i2, err_msg=f"{ds} {agg}")
+    finally:
+        set_option("EMIT_HALF", None)
